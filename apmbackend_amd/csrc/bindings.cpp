@@ -1,0 +1,302 @@
+// Python bindings for the native runtime (pybind11, no torch headers).
+//
+//   _apm_native.Engine        -- the GPU pipeline (engine.h)
+//   _apm_native.JoinHarness   -- the host join workers alone, fed with Python-built events
+//                                (CPU-testable; used by tests/test_join_native.py)
+//   _apm_native.js_*          -- JS-exact number formatting helpers (parity tests)
+//   _apm_native.Tailer / proc_* / synth_* are registered from their own translation units.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+#include <memory>
+
+#include "kernels/kernel_api.h"
+#include "runtime/engine.h"
+#include "runtime/format.h"
+#include "runtime/jsutil.h"
+
+namespace py = pybind11;
+using namespace apm;
+
+void register_tailer(py::module_& m);
+void register_synth(py::module_& m);
+void register_procstat(py::module_& m);
+
+namespace {
+
+template <class T>
+T get(const py::dict& d, const char* k, T dflt) {
+  if (d.contains(k)) return d[k].cast<T>();
+  return dflt;
+}
+
+TzTable tz_from(const py::dict& d) {
+  TzTable tz{};
+  tz.n = 1;
+  tz.local_start[0] = INT64_MIN / 2;
+  tz.offset_ms[0] = 0;
+  if (d.contains("tz_table")) {
+    auto rows = d["tz_table"].cast<std::vector<std::pair<int64_t, int64_t>>>();
+    tz.n = (int)std::min<size_t>(rows.size(), 64);
+    for (int i = 0; i < tz.n; ++i) { tz.local_start[i] = rows[i].first; tz.offset_ms[i] = rows[i].second; }
+    if (tz.n == 0) { tz.n = 1; tz.local_start[0] = INT64_MIN / 2; tz.offset_ms[0] = 0; }
+  }
+  return tz;
+}
+
+EngineConfig config_from(const py::dict& d) {
+  EngineConfig c;
+  c.device = get<int>(d, "device", 0);
+  c.max_series = get<int32_t>(d, "max_series", c.max_series);
+  c.cell_cap = get<int32_t>(d, "cell_cap", c.cell_cap);
+  c.spill_cap = get<int32_t>(d, "spill_cap", c.spill_cap);
+  c.max_batch_bytes = get<uint64_t>(d, "max_batch_bytes", c.max_batch_bytes);
+  c.max_lines = get<uint32_t>(d, "max_lines", c.max_lines);
+  c.max_chunks = get<uint32_t>(d, "max_chunks", c.max_chunks);
+  c.pool_cap = get<int64_t>(d, "pool_cap", c.pool_cap);
+  c.max_tx_per_batch = get<int32_t>(d, "max_tx_per_batch", c.max_tx_per_batch);
+  c.max_alerts = get<int32_t>(d, "max_alerts", c.max_alerts);
+  c.ring_bytes = get<int>(d, "ring_bytes", c.ring_bytes);
+  c.exact_mean = get<int>(d, "exact_mean", c.exact_mean);
+  c.sigma_stddev = get<int>(d, "sigma_stddev", c.sigma_stddev);
+  c.resync_k = get<int>(d, "resync_k", c.resync_k);
+  c.emulate_aliasing = get<int>(d, "emulate_aliasing", c.emulate_aliasing);
+  if (d.contains("lags")) {
+    auto lags = d["lags"].cast<std::vector<std::tuple<int, double, double>>>();
+    c.n_lags = (int)std::min<size_t>(lags.size(), MAX_LAGS);
+    for (int i = 0; i < c.n_lags; ++i) {
+      c.lags[i] = std::get<0>(lags[i]);
+      c.thr[i] = std::get<1>(lags[i]);
+      c.infl[i] = std::get<2>(lags[i]);
+    }
+  }
+  if (d.contains("lag_suppressed")) {
+    auto v = d["lag_suppressed"].cast<std::vector<int>>();
+    for (size_t i = 0; i < v.size() && i < MAX_LAGS; ++i) c.lag_suppressed[i] = v[i];
+  }
+  c.alert_window = get<int>(d, "alert_window", c.alert_window);
+  c.alert_threshold = get<int>(d, "alert_threshold", c.alert_threshold);
+  c.hard_min_ms = get<double>(d, "hard_min_ms", c.hard_min_ms);
+  c.hard_min_tpm = get<double>(d, "hard_min_tpm", c.hard_min_tpm);
+  c.hard_max_ms = get<double>(d, "hard_max_ms", c.hard_max_ms);
+  c.both_only = get<int>(d, "both_only", c.both_only);
+  c.cooldown_ms = get<double>(d, "cooldown_ms", c.cooldown_ms);
+  c.cooldown_by_service = get<int>(d, "cooldown_by_service", c.cooldown_by_service);
+  c.alert_clock_entry = get<int>(d, "alert_clock_entry", c.alert_clock_entry);
+  c.interval_len = get<int>(d, "interval_len", c.interval_len);
+  c.window = get<int>(d, "window", c.window);
+  c.buffer = get<int>(d, "buffer", c.buffer);
+  c.record_ttl_ms = get<double>(d, "record_ttl_ms", c.record_ttl_ms);
+  c.acct_ttl_ms = get<double>(d, "acct_ttl_ms", c.acct_ttl_ms);
+  c.need_ttl_ms = get<double>(d, "need_ttl_ms", c.need_ttl_ms);
+  c.tz = tz_from(d);
+  c.join_threads = get<int>(d, "join_threads", c.join_threads);
+  c.keep_text = get<int>(d, "keep_text", c.keep_text);
+  c.keep_tx_records = get<int>(d, "keep_tx_records", c.keep_tx_records);
+  return c;
+}
+
+ServiceOverride override_from(const py::dict& d) {
+  ServiceOverride o;
+  if (d.contains("thr")) {
+    auto v = d["thr"].cast<std::vector<py::object>>();
+    for (size_t i = 0; i < v.size() && i < MAX_LAGS; ++i)
+      if (!v[i].is_none()) { o.has_thr[i] = true; o.thr[i] = v[i].cast<double>(); }
+  }
+  if (d.contains("infl")) {
+    auto v = d["infl"].cast<std::vector<py::object>>();
+    for (size_t i = 0; i < v.size() && i < MAX_LAGS; ++i)
+      if (!v[i].is_none()) { o.has_infl[i] = true; o.infl[i] = v[i].cast<double>(); }
+  }
+  o.hard_max = get<double>(d, "hard_max", 0.0);
+  o.suppressed = get<bool>(d, "suppressed", false);
+  return o;
+}
+
+std::vector<Chunk> chunks_from(const std::vector<std::tuple<int32_t, uint64_t, uint64_t>>& v) {
+  std::vector<Chunk> out;
+  out.reserve(v.size());
+  for (auto& t : v) out.push_back(Chunk{std::get<0>(t), std::get<1>(t), std::get<2>(t)});
+  return out;
+}
+
+py::dict metrics_dict(const EngineMetrics& m) {
+  py::dict d;
+  d["batches"] = m.batches; d["bytes"] = m.bytes; d["lines"] = m.lines; d["events"] = m.events;
+  d["tx"] = m.tx; d["tx_db"] = m.tx_db; d["tx_dropped"] = m.tx_dropped; d["rollovers"] = m.rollovers;
+  d["alerts"] = m.alerts; d["alert_candidates"] = m.alert_candidates; d["released"] = m.released;
+  d["t_parse_ms"] = m.t_parse_ms; d["t_join_ms"] = m.t_join_ms; d["t_stats_ms"] = m.t_stats_ms;
+  d["t_total_ms"] = m.t_total_ms;
+  d["rollover_latency_ms"] = m.rollover_latency_ms;
+  return d;
+}
+
+py::dict counters_dict(const JoinCounters& c) {
+  py::dict d;
+  d["events"] = c.events; d["tx"] = c.tx; d["tx_db"] = c.tx_db; d["expired_partials"] = c.expired_partials;
+  d["need_expired"] = c.need_expired; d["ejb_exit_unmatched"] = c.ejb_exit_unmatched;
+  d["invalid_acct"] = c.invalid_acct; d["audit_errors"] = c.audit_errors; d["host_fallback"] = c.host_fallback;
+  return d;
+}
+
+// Host join alone (CPU): events built by Python (apmbackend_amd.ops.parse_ref) are fed to the
+// shards exactly as Engine::process_batch does after the GPU parse.
+class JoinHarness {
+ public:
+  explicit JoinHarness(const py::dict& d) {
+    cfg_.record_ttl_ms = get<double>(d, "record_ttl_ms", 120000);
+    cfg_.acct_ttl_ms = get<double>(d, "acct_ttl_ms", 120000);
+    cfg_.need_ttl_ms = get<double>(d, "need_ttl_ms", 30000);
+    cfg_.tz = tz_from(d);
+  }
+  int32_t add_file(const std::string& path, int kind, const std::string& server) {
+    int32_t sid;
+    auto it = server_ids_.find(server);
+    if (it == server_ids_.end()) {
+      sid = (int32_t)servers_.size();
+      servers_.push_back(server);
+      server_ids_[server] = sid;
+      shards_.emplace_back(new JoinShard(cfg_, &dict_, &files_));
+    } else {
+      sid = it->second;
+    }
+    files_.push_back(FileInfo{path, sid, (uint8_t)kind});
+    return (int32_t)files_.size() - 1;
+  }
+  // events: bytes of packed apm::Event; batch: the batch bytes; chunk_file: chunk -> file id
+  std::vector<std::pair<std::string, std::string>> process(py::bytes events, py::bytes batch,
+                                                           std::vector<int32_t> chunk_file, double now) {
+    std::string ev = events;
+    std::string by = batch;
+    const Event* e = reinterpret_cast<const Event*>(ev.data());
+    const size_t n = ev.size() / sizeof(Event);
+    std::vector<std::pair<uint32_t, uint32_t>> range(shards_.size(), {0, 0});
+    uint32_t i = 0;
+    while (i < n) {
+      const int32_t srv = files_[chunk_file[e[i].chunk]].server;
+      uint32_t j = i;
+      while (j < n && files_[chunk_file[e[j].chunk]].server == srv) ++j;
+      range[srv] = {i, j};
+      i = j;
+    }
+    std::vector<std::pair<std::string, std::string>> out;
+    std::vector<TxOut> all;
+    for (size_t s = 0; s < shards_.size(); ++s) {
+      shards_[s]->out().clear();
+      shards_[s]->begin_batch(now, batch_no_);
+      if (range[s].second > range[s].first)
+        shards_[s]->process(e + range[s].first, range[s].second - range[s].first, (const uint8_t*)by.data(),
+                            chunk_file);
+      for (auto& t : shards_[s]->out()) all.push_back(t);
+    }
+    std::stable_sort(all.begin(), all.end(), [](const TxOut& a, const TxOut& b) { return a.seq < b.seq; });
+    for (auto& t : all) out.push_back({t.to_db ? "db_insert" : "transactions", fmt::tx_line(t, servers_, dict_)});
+    ++batch_no_;
+    return out;
+  }
+  py::dict counters() {
+    JoinCounters t;
+    for (auto& s : shards_) {
+      t.events += s->counters.events; t.tx += s->counters.tx; t.need_expired += s->counters.need_expired;
+      t.expired_partials += s->counters.expired_partials; t.ejb_exit_unmatched += s->counters.ejb_exit_unmatched;
+      t.invalid_acct += s->counters.invalid_acct; t.audit_errors += s->counters.audit_errors;
+      t.host_fallback += s->counters.host_fallback; t.tx_db += s->counters.tx_db;
+    }
+    return counters_dict(t);
+  }
+
+ private:
+  JoinConfig cfg_;
+  Dictionary dict_;
+  std::vector<FileInfo> files_;
+  std::vector<std::string> servers_;
+  std::unordered_map<std::string, int32_t> server_ids_;
+  std::vector<std::unique_ptr<JoinShard>> shards_;
+  uint64_t batch_no_ = 0;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_apm_native, m) {
+  m.doc() = "apm-mi355x native runtime (HIP kernels for gfx950 + host runtime)";
+  m.attr("EVENT_SIZE") = (int)sizeof(Event);
+  m.attr("NSLOT") = NSLOT;
+
+  py::class_<Engine>(m, "Engine")
+      .def(py::init([](const py::dict& d) { return new Engine(config_from(d)); }))
+      .def("add_file", &Engine::add_file)
+      .def("add_server", &Engine::add_server)
+      .def("set_override", [](Engine& e, const std::string& svc, const py::dict& d) { e.set_override(svc, override_from(d)); })
+      .def("clear_overrides", &Engine::clear_overrides)
+      .def("refresh_series_settings", &Engine::refresh_series_settings)
+      .def("process_batch",
+           [](Engine& e, py::buffer buf, const std::vector<std::tuple<int32_t, uint64_t, uint64_t>>& chunks,
+              double now) {
+             py::buffer_info bi = buf.request();
+             const uint8_t* p = (const uint8_t*)bi.ptr;
+             const uint64_t n = (uint64_t)(bi.size * bi.itemsize);
+             auto ch = chunks_from(chunks);
+             py::gil_scoped_release rel;
+             e.process_batch(p, n, ch, now);
+           },
+           py::arg("buf"), py::arg("chunks"), py::arg("now") = -1.0)
+      .def("process_batch_ptr",
+           [](Engine& e, uintptr_t ptr, uint64_t n, const std::vector<std::tuple<int32_t, uint64_t, uint64_t>>& chunks,
+              double now) {
+             auto ch = chunks_from(chunks);
+             py::gil_scoped_release rel;
+             e.process_batch((const uint8_t*)ptr, n, ch, now);
+           },
+           py::arg("ptr"), py::arg("n"), py::arg("chunks"), py::arg("now") = -1.0)
+      .def("take", &Engine::take)
+      .def("last_events", [](Engine& e) { return py::bytes(e.last_events()); })
+      .def("warm_history", &Engine::warm_history)
+      .def("metrics", [](Engine& e) { return metrics_dict(e.metrics()); })
+      .def("join_counters", [](Engine& e) { return counters_dict(e.join_counters()); })
+      .def("n_series", &Engine::n_series)
+      .def("n_services", &Engine::n_services)
+      .def("services", &Engine::services)
+      .def("servers", &Engine::servers)
+      .def("watermark", &Engine::watermark)
+      .def("device_bytes", &Engine::device_bytes)
+      .def("stream_handle", [](Engine& e) { return (uintptr_t)e.stream(); })
+      .def("comm_stream_handle", [](Engine& e) { return (uintptr_t)e.comm_stream(); })
+      .def("pack_service_moments", [](Engine& e, uintptr_t dst, int32_t cap) {
+        e.pack_service_moments((double*)dst, cap, e.comm_stream());
+      })
+      .def("winstats", [](Engine& e) {
+        std::vector<WinStat> w;
+        e.download_winstats(w);
+        std::vector<std::tuple<int, int, double, double, double, double>> out;
+        for (int i = 0; i < e.n_series(); ++i) out.emplace_back(w[i].active, w[i].n, w[i].tpm, w[i].avg, w[i].p75, w[i].p95);
+        return out;
+      });
+
+  py::class_<JoinHarness>(m, "JoinHarness")
+      .def(py::init<const py::dict&>())
+      .def("add_file", &JoinHarness::add_file)
+      .def("process", &JoinHarness::process)
+      .def("counters", &JoinHarness::counters);
+
+  m.def("alloc_pinned", &Engine::alloc_pinned);
+  m.def("free_pinned", &Engine::free_pinned);
+  m.def("memcpy_to", [](uintptr_t dst, py::bytes b, uint64_t off) {
+    std::string_view v = b;
+    std::memcpy((char*)dst + off, v.data(), v.size());
+  });
+  m.def("js_to_fixed", [](double x, int f) { return js::to_fixed(x, f); });
+  m.def("js_num_str", [](double x) { return js::num_str(x); });
+  m.def("js_parse_int", [](const std::string& s) { return js::parse_int(s); });
+  m.def("js_convert_date", [](const std::string& s, const py::dict& tz) {
+    double v;
+    TzTable t = tz_from(tz);
+    if (!js::convert_date(s, t, v)) return py::object(py::none());
+    return py::object(py::float_(v));
+  });
+  m.def("js_round_fixed", [](double x, int f) { return js_round_fixed(x, f); });
+
+  register_tailer(m);
+  register_synth(m);
+  register_procstat(m);
+}

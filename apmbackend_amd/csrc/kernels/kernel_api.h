@@ -1,0 +1,108 @@
+// Launch-side API of the CDNA4 kernels: argument structs + host entry points.
+// Included by the .hip translation units and by the host runtime (engine.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../apm_types.h"
+#include "common.h"
+
+namespace apm {
+
+struct StatsState {
+  int32_t* counts;        // [NSLOT][S]
+  int32_t* cells;         // [NSLOT][S][cap]
+  int32_t* spill_n;       // [NSLOT]
+  int32_t* spill_series;  // [NSLOT][spill_cap]
+  int32_t* spill_val;     // [NSLOT][spill_cap]
+  uint8_t* active;        // [S]
+  int32_t cap;
+  int32_t spill_cap;
+  int32_t S;
+};
+
+struct WindowArgs {
+  StatsState st;
+  int32_t win_slots[32];  // slot index per window bucket (-1 = bucket absent)
+  int32_t n_win;          // 31
+  double tpm_div;         // windowSz * intervalLen / 60
+  WinStat* out;           // [S]
+  int32_t* big_list;      // series deferred to the block pass
+  int32_t* big_n;
+  int32_t n_series;       // ids < n_series may be active
+};
+
+struct ZArgs {
+  void* ring;              // [NSTAT][LAG][S] of T for this lag
+  int32_t* len;            // [S]
+  double* sum;             // [NSTAT][S]
+  double* comp;            // [NSTAT][S]
+  int32_t* cnt;            // [NSTAT][S]
+  double* sumsq;           // [NSTAT][S]
+  double* sqcomp;          // [NSTAT][S]
+  const double* thr;       // [S]
+  const double* infl;      // [S]
+  const WinStat* win;      // [S]
+  ZOut* out;               // [S]
+  int32_t S;
+  int32_t n_series;
+  int32_t lag;
+  int32_t head;            // write position this rollover
+  int32_t exact;           // 1 = sequential mean every time
+  int32_t sigma_stddev;    // 0 = sqrt(mean) quirk, 1 = population sigma
+  int32_t resync_k;        // rolling mode: exact resync period (0 = never)
+  int64_t rollover_idx;
+};
+
+struct AlertArgs {
+  const WinStat* win;         // [S]
+  const ZOut* z;              // [S] for this lag
+  int32_t* counter;           // [S] leaky counter for this lag
+  const double* hard_max;     // [S] per-series effective hardMaxMsAlertThreshold
+  const uint8_t* suppressed;  // [S] service in suppressedServices
+  const uint64_t* emit_key;   // [S]
+  AlertRec* out;
+  int32_t* n_out;
+  int32_t n_series;
+  int32_t lag_idx;
+  int32_t n_lags;
+  int32_t lag_suppressed;
+  int32_t window;             // rollingAlertWindowSizeInIntervals
+  int32_t threshold;          // requiredNumberBadIntervalsInAlertWindowToTrigger
+  double hard_min_ms;
+  double hard_min_tpm;
+  int32_t both_only;
+  int32_t max_out;
+};
+
+}  // namespace apm
+
+extern "C" {
+// parse.hip
+size_t apm_parse_workspace_bytes(uint64_t max_bytes, uint32_t max_lines, uint32_t max_chunks);
+int apm_parse_batch(const uint8_t* d_bytes, uint64_t n_bytes, const uint32_t* d_chunk_begin,
+                    const uint8_t* d_chunk_kind, const uint32_t* d_chunk_file, uint32_t n_chunks,
+                    void* d_ws, uint32_t max_lines, apm::Event* d_events, uint32_t* d_n_events,
+                    uint32_t* d_n_lines, unsigned long long* d_watermark, uint8_t* d_file_open,
+                    const apm::TzTable* tz, hipStream_t stream);
+// stats.hip
+void apm_stats_clear_slot(apm::StatsState* st, int slot, hipStream_t stream);
+void apm_bucket_append(const apm::TxRec* d_tx, uint32_t lo, uint32_t hi, apm::StatsState* st,
+                       int64_t min_live_bucket, hipStream_t stream);
+void apm_window_stats(apm::WindowArgs* a, hipStream_t stream);
+void apm_pool_append(const apm::TxRec* d_tx, uint32_t lo, uint32_t hi, const int64_t* d_gid, int64_t* tail_end,
+                     int64_t* tail_gid, int64_t base, hipStream_t stream);
+size_t apm_release_tmp_bytes(int64_t cap);
+int apm_release_merge(const int64_t* pool_end, const int64_t* pool_gid, int64_t n_pool, const int64_t* tail_end,
+                      const int64_t* tail_gid, int64_t n_tail, int64_t* sort_end, int64_t* sort_gid,
+                      int64_t* out_end, int64_t* out_gid, void* tmp, size_t tmp_bytes, hipStream_t stream);
+// zscore.hip
+void apm_zscore(apm::ZArgs* a, int dtype_bytes, hipStream_t stream);
+void apm_zscore_warm(apm::ZArgs* a, int dtype_bytes, int fill, uint64_t seed, const apm::WinStat* base,
+                     hipStream_t stream);
+void apm_alert_eval(apm::AlertArgs* a, hipStream_t stream);
+// fleet.hip
+void apm_service_moments(const int32_t* series_service, const uint8_t* active, int32_t n_series, int32_t S,
+                         int32_t n_lags, int32_t n_services_cap, const double* const* sums, const double* const* comps,
+                         const int32_t* const* cnts, double* dst, hipStream_t stream);
+}

@@ -1,0 +1,337 @@
+// K7 bucket append, K8 window statistics, K9 ordered release.
+//
+// Reference behaviour: stream_calc_stats.js addData (:115-134), removeOldBuckets (:103-113),
+// generateAllStatsToQueue (:157-203) with util_methods.js calcPercentile (:112-142), and the
+// min-heap release writeHeapToQueue (:136-155) / binary_heap.js popAllLessOrEqualToScore.
+//
+// Layout (MI355X): samples live in a per-series ring of NSLOT=40 ten-second bucket cells,
+// cells[slot][series][CAP] (int32 elapsed ms) + counts[slot][series]; a live bucket b sits in
+// slot b % 40 (at most 37 buckets are live, so slots never alias).  Appends are one atomicAdd
+// per sample into the cell (overflow beyond CAP goes to a per-slot spill list).  At a rollover
+// every active series is reduced by one wave: the 31 window cells are gathered into LDS, summed,
+// bitonic-sorted in LDS and the two percentile ranks read out with the reference index rule.
+// Series too large for a wave's LDS tile are deferred to a block-wide pass.
+#include "kernel_api.h"
+
+#include <rocprim/rocprim.hpp>
+
+#include <algorithm>
+
+namespace apm {
+
+constexpr int WS_WAVES = 4;              // waves per block in the window kernel
+constexpr int WS_TILE = 1024;            // samples per wave held in LDS
+constexpr int BIG_TILE = 16384;          // samples per block in the large-series pass (64 KiB)
+
+
+// --------------------------------------------------------------------------------- K7
+// Appends tx[lo, hi) to their bucket cells. `slot_of` maps (bucket - slot_base) -> slot or -1
+// (bucket already deleted: the sample is dropped but the series still becomes active, as in
+// the reference where the late bucket is re-created and deleted at the next rollover).
+__global__ void k_bucket_append(const TxRec* __restrict__ tx, uint32_t lo, uint32_t hi, StatsState st,
+                                int64_t min_live_bucket) {
+  const uint32_t i = lo + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= hi) return;
+  const TxRec r = tx[i];
+  if (r.series < 0 || r.series >= st.S) return;
+  st.active[r.series] = 1;
+  const int64_t b = r.end_ms / 10000;  // endTs string minus its last 4 digits
+  if (b < min_live_bucket || r.elapsed == ELAPSED_NAN) return;
+  const int slot = (int)(b % NSLOT);
+  const size_t cidx = (size_t)slot * st.S + r.series;
+  const int k = atomicAdd(&st.counts[cidx], 1);
+  if (k < st.cap) {
+    st.cells[cidx * st.cap + k] = r.elapsed;
+  } else {
+    const int j = atomicAdd(&st.spill_n[slot], 1);
+    if (j < st.spill_cap) {
+      st.spill_series[(size_t)slot * st.spill_cap + j] = r.series;
+      st.spill_val[(size_t)slot * st.spill_cap + j] = r.elapsed;
+    }
+  }
+}
+
+__global__ void k_clear_slot(StatsState st, int slot) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < (uint32_t)st.S) st.counts[(size_t)slot * st.S + i] = 0;
+  if (i == 0) st.spill_n[slot] = 0;
+}
+
+// --------------------------------------------------------------------------------- K8
+
+__device__ __forceinline__ void percentile_ranks(int n, int pct, int& lo, int& hi) {
+  // calcPercentile: idx = p/100*n - 1; integral -> a[idx]; else ceil, last -> a[last],
+  // otherwise (a[i] + a[i+1]) / 2.  Computed in double exactly as JS does.
+  if (n <= 0) { lo = hi = -1; return; }
+  const double idx = ((double)pct / 100.0) * (double)n - 1.0;
+  if (n == 1 || idx == floor(idx)) { lo = hi = (int)idx; return; }
+  const int i = (int)ceil(idx);
+  lo = i;
+  hi = (i == n - 1) ? i : i + 1;
+}
+
+__device__ __forceinline__ double pct_value(const int32_t* a, int lo, int hi) {
+  if (lo < 0) return apm_nan();
+  if (lo == hi) return (double)a[lo];
+  return ((double)a[lo] + (double)a[hi]) / 2.0;
+}
+
+// Bitonic sort of n (power of two) ints in LDS by the lanes of one wave.
+__device__ inline void wave_bitonic(int32_t* a, int n, int lane) {
+  for (int k = 2; k <= n; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = lane; i < n; i += APM_WAVE) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const int32_t x = a[i], y = a[ixj];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) { a[i] = y; a[ixj] = x; }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    }
+  }
+}
+
+__device__ __forceinline__ void finish_series(const WindowArgs& a, int s, int n, long long sum,
+                                              const int32_t* sorted) {
+  WinStat w;
+  w.n = n;
+  w.active = 1;
+  w.tpm = js_round_fixed((double)n / a.tpm_div, 2);
+  if (n > 0) {
+    int lo, hi;
+    w.avg = js_round_fixed((double)sum / (double)n, 1);
+    percentile_ranks(n, 75, lo, hi);
+    w.p75 = js_round_fixed(pct_value(sorted, lo, hi), 1);
+    percentile_ranks(n, 95, lo, hi);
+    w.p95 = js_round_fixed(pct_value(sorted, lo, hi), 1);
+  } else {
+    w.avg = w.p75 = w.p95 = apm_nan();
+  }
+  a.out[s] = w;
+}
+
+__global__ __launch_bounds__(WS_WAVES * APM_WAVE) void k_window_stats(WindowArgs a) {
+  __shared__ int32_t tile[WS_WAVES][WS_TILE];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int s = blockIdx.x * WS_WAVES + wv;
+  if (s >= a.n_series) return;
+  if (!a.st.active[s]) {
+    if (lane == 0) { WinStat w{}; w.active = 0; w.n = 0; a.out[s] = w; }
+    return;
+  }
+  // per-window-bucket counts (lane r handles window bucket r)
+  int cnt = 0, slot = -1;
+  if (lane < a.n_win) {
+    slot = a.win_slots[lane];
+    if (slot >= 0) cnt = a.st.counts[(size_t)slot * a.st.S + s];
+  }
+  const int inl = min(cnt, a.st.cap);
+  const int spill = cnt - inl;
+  // exclusive prefix of inline counts across lanes
+  int pre = inl;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(pre, o, 64);
+    if (lane >= o) pre += v;
+  }
+  const int total_inl = __shfl(pre, 63, 64);
+  int total_spill = spill;
+  for (int o = 32; o > 0; o >>= 1) total_spill += __shfl_xor(total_spill, o, 64);
+  const int n = total_inl + total_spill;
+  if (n > WS_TILE) {
+    if (lane == 0) { const int j = atomicAdd(a.big_n, 1); a.big_list[j] = s; }
+    return;
+  }
+  int32_t* t = tile[wv];
+  pre -= inl;
+  long long sum = 0;
+  // gather inline samples: every lane copies its own cell (contiguous CAP run)
+  if (inl > 0) {
+    const int32_t* cell = a.st.cells + ((size_t)slot * a.st.S + s) * a.st.cap;
+    for (int k = 0; k < inl; ++k) { const int32_t v = cell[k]; t[pre + k] = v; sum += v; }
+  }
+  // spilled samples: scan the spill lists of the window slots (rare)
+  if (total_spill > 0) {
+    __builtin_amdgcn_wave_barrier();
+    int w = total_inl;
+    for (int r = 0; r < a.n_win; ++r) {
+      const int sl = a.win_slots[r];
+      if (sl < 0) continue;
+      const int ns = min(a.st.spill_n[sl], a.st.spill_cap);
+      for (int base = 0; base < ns; base += 64) {
+        const int j = base + lane;
+        bool hit = false;
+        int32_t v = 0;
+        if (j < ns) {
+          hit = a.st.spill_series[(size_t)sl * a.st.spill_cap + j] == s;
+          v = a.st.spill_val[(size_t)sl * a.st.spill_cap + j];
+        }
+        const unsigned long long m = __ballot(hit);
+        if (hit) {
+          const int off = __popcll(m & ((1ULL << lane) - 1ULL));
+          t[w + off] = v;
+          sum += v;
+        }
+        w += __popcll(m);
+      }
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+  // pad to a power of two and sort
+  int np2 = 64;
+  while (np2 < n) np2 <<= 1;
+  __builtin_amdgcn_wave_barrier();
+  for (int i = n + lane; i < np2; i += 64) t[i] = 0x7fffffff;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  if (n > 1) wave_bitonic(t, np2, lane);
+  if (lane == 0) finish_series(a, s, n, sum, t);
+}
+
+// Large series: one 1024-thread block per deferred series, block-wide bitonic in LDS.
+__global__ __launch_bounds__(1024) void k_window_stats_big(WindowArgs a) {
+  __shared__ int32_t t[BIG_TILE];
+  __shared__ long long red[16];
+  __shared__ int wpos;
+  const int nb = *a.big_n;
+  for (int bi = blockIdx.x; bi < nb; bi += gridDim.x) {
+    const int s = a.big_list[bi];
+    if (threadIdx.x == 0) wpos = 0;
+    __syncthreads();
+    long long sum = 0;
+    for (int r = 0; r < a.n_win; ++r) {
+      const int sl = a.win_slots[r];
+      if (sl < 0) continue;
+      const int cnt = a.st.counts[(size_t)sl * a.st.S + s];
+      const int inl = min(cnt, a.st.cap);
+      const int32_t* cell = a.st.cells + ((size_t)sl * a.st.S + s) * a.st.cap;
+      for (int k = threadIdx.x; k < inl; k += blockDim.x) {
+        const int32_t v = cell[k];
+        const int p = atomicAdd(&wpos, 1);
+        if (p < BIG_TILE) t[p] = v;
+        sum += v;
+      }
+      if (cnt > inl) {
+        const int ns = min(a.st.spill_n[sl], a.st.spill_cap);
+        for (int j = threadIdx.x; j < ns; j += blockDim.x) {
+          if (a.st.spill_series[(size_t)sl * a.st.spill_cap + j] == s) {
+            const int32_t v = a.st.spill_val[(size_t)sl * a.st.spill_cap + j];
+            const int p = atomicAdd(&wpos, 1);
+            if (p < BIG_TILE) t[p] = v;
+            sum += v;
+          }
+        }
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    const int n_all = wpos;
+    const int n = min(n_all, BIG_TILE);  // beyond the tile the percentile is clamped (counted)
+    int np2 = 1;
+    while (np2 < n) np2 <<= 1;
+    for (int i = n + threadIdx.x; i < np2; i += blockDim.x) t[i] = 0x7fffffff;
+    __syncthreads();
+    for (int k = 2; k <= np2; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = threadIdx.x; i < np2; i += blockDim.x) {
+          const int ixj = i ^ j;
+          if (ixj > i) {
+            const int32_t x = t[i], y = t[ixj];
+            const bool up = (i & k) == 0;
+            if ((x > y) == up) { t[i] = y; t[ixj] = x; }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    if (threadIdx.x == 0) {
+      long long tot = 0;
+      for (int w = 0; w < 16; ++w) tot += red[w];
+      finish_series(a, s, n_all, tot, t);
+    }
+    __syncthreads();
+  }
+}
+
+// --------------------------------------------------------------------------------- K9
+// The pending pool is kept sorted by (endTs, arrival gid).  New tx are appended to an unsorted
+// tail; at a rollover the tail is radix-sorted (stable, so arrival order breaks endTs ties),
+// merged behind the pool, and the released prefix (endTs <= edge) is handed to the sink.  The
+// prefix length is known on the host (it counts endTs per bucket as it emits tx), so no device
+// synchronisation is needed.
+__global__ void k_pool_append(const TxRec* __restrict__ tx, uint32_t lo, uint32_t hi, const int64_t* __restrict__ gid,
+                              int64_t* __restrict__ tail_end, int64_t* __restrict__ tail_gid, int64_t base) {
+  const uint32_t i = lo + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= hi) return;
+  tail_end[base + (i - lo)] = tx[i].end_ms;
+  tail_gid[base + (i - lo)] = gid[i];
+}
+
+}  // namespace apm
+
+extern "C" {
+
+using namespace apm;
+
+void apm_stats_clear_slot(StatsState* st, int slot, hipStream_t stream) {
+  hipLaunchKernelGGL(k_clear_slot, dim3((st->S + 255) / 256), dim3(256), 0, stream, *st, slot);
+}
+
+void apm_bucket_append(const TxRec* d_tx, uint32_t lo, uint32_t hi, StatsState* st, int64_t min_live_bucket,
+                       hipStream_t stream) {
+  if (hi <= lo) return;
+  hipLaunchKernelGGL(k_bucket_append, dim3((hi - lo + 255) / 256), dim3(256), 0, stream, d_tx, lo, hi, *st,
+                     min_live_bucket);
+}
+
+void apm_window_stats(WindowArgs* a, hipStream_t stream) {
+  HIP_OK(hipMemsetAsync(a->big_n, 0, 4, stream));
+  const int blocks = (a->n_series + WS_WAVES - 1) / WS_WAVES;
+  if (blocks == 0) return;
+  hipLaunchKernelGGL(k_window_stats, dim3(blocks), dim3(WS_WAVES * APM_WAVE), 0, stream, *a);
+  hipLaunchKernelGGL(k_window_stats_big, dim3(64), dim3(1024), 0, stream, *a);
+}
+
+void apm_pool_append(const TxRec* d_tx, uint32_t lo, uint32_t hi, const int64_t* d_gid, int64_t* tail_end,
+                     int64_t* tail_gid, int64_t base, hipStream_t stream) {
+  if (hi <= lo) return;
+  hipLaunchKernelGGL(k_pool_append, dim3((hi - lo + 255) / 256), dim3(256), 0, stream, d_tx, lo, hi, d_gid,
+                     tail_end, tail_gid, base);
+}
+
+size_t apm_release_tmp_bytes(int64_t cap) {
+  size_t a = 0, b = 0;
+  HIP_OK(rocprim::radix_sort_pairs(nullptr, a, (int64_t*)nullptr, (int64_t*)nullptr, (int64_t*)nullptr,
+                                   (int64_t*)nullptr, (size_t)cap, 0, 64, (hipStream_t)0));
+  HIP_OK(rocprim::merge(nullptr, b, (int64_t*)nullptr, (int64_t*)nullptr, (int64_t*)nullptr,
+                        (int64_t*)nullptr, (int64_t*)nullptr, (int64_t*)nullptr, (size_t)cap, (size_t)cap,
+                        rocprim::less<int64_t>(), (hipStream_t)0));
+  return std::max(a, b) + 4096;
+}
+
+// out = merge(pool[0..n_pool), sort(tail[0..n_tail)))   (stable: pool entries first on ties)
+int apm_release_merge(const int64_t* pool_end, const int64_t* pool_gid, int64_t n_pool, const int64_t* tail_end,
+                      const int64_t* tail_gid, int64_t n_tail, int64_t* sort_end, int64_t* sort_gid,
+                      int64_t* out_end, int64_t* out_gid, void* tmp, size_t tmp_bytes, hipStream_t stream) {
+  size_t need = 0;
+  if (n_tail > 0) {
+    HIP_OK(rocprim::radix_sort_pairs(nullptr, need, tail_end, sort_end, tail_gid, sort_gid, (size_t)n_tail, 0, 64,
+                                     stream));
+    if (need > tmp_bytes) return -1;
+    HIP_OK(rocprim::radix_sort_pairs(tmp, need, tail_end, sort_end, tail_gid, sort_gid, (size_t)n_tail, 0, 64,
+                                     stream));
+  }
+  if (n_pool + n_tail == 0) return 0;
+  HIP_OK(rocprim::merge(nullptr, need, pool_end, sort_end, out_end, pool_gid, sort_gid, out_gid, (size_t)n_pool,
+                        (size_t)n_tail, rocprim::less<int64_t>(), stream));
+  if (need > tmp_bytes) return -1;
+  HIP_OK(rocprim::merge(tmp, need, pool_end, sort_end, out_end, pool_gid, sort_gid, out_gid, (size_t)n_pool,
+                        (size_t)n_tail, rocprim::less<int64_t>(), stream));
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,783 @@
+// apm::Engine implementation -- see engine.h.
+#include "engine.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <queue>
+#include <stdexcept>
+
+#include "../kernels/kernel_api.h"
+#include "format.h"
+
+namespace apm {
+
+namespace {
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+constexpr int64_t NO_BUCKET = INT64_MIN;
+}  // namespace
+
+// ----------------------------------------------------------------------------- thread pool
+ThreadPool::ThreadPool(int n) {
+  for (int i = 0; i < n; ++i) {
+    workers_.emplace_back([this]() {
+      uint64_t seen = 0;
+      for (;;) {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&]() { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        while (next_ < n_tasks_) {
+          const int t = next_++;
+          lk.unlock();
+          (*fn_)(t);
+          lk.lock();
+          if (++done_ == n_tasks_) done_cv_.notify_all();
+        }
+      }
+    });
+  }
+}
+
+ThreadPool::~ThreadPool() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : workers_) t.join();
+}
+
+void ThreadPool::run(int n_tasks, const std::function<void(int)>& fn) {
+  if (n_tasks <= 0) return;
+  if (workers_.empty() || n_tasks == 1) {
+    for (int i = 0; i < n_tasks; ++i) fn(i);
+    return;
+  }
+  std::unique_lock<std::mutex> lk(mu_);
+  fn_ = &fn;
+  n_tasks_ = n_tasks;
+  next_ = 0;
+  done_ = 0;
+  ++gen_;
+  cv_.notify_all();
+  done_cv_.wait(lk, [&]() { return done_ == n_tasks_; });
+  fn_ = nullptr;
+}
+
+// ----------------------------------------------------------------------------- setup
+void* Engine::dmalloc(size_t bytes) {
+  void* p = nullptr;
+  bytes = (bytes + 255) & ~(size_t)255;
+  HIP_OK(hipMalloc(&p, bytes));
+  HIP_OK(hipMemset(p, 0, bytes));
+  allocations_.push_back(p);
+  device_bytes_ += bytes;
+  return p;
+}
+
+Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
+  HIP_OK(hipSetDevice(cfg_.device));
+  HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  HIP_OK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
+  HIP_OK(hipEventCreate(&ev_a_));
+  HIP_OK(hipEventCreate(&ev_b_));
+  const int32_t S = cfg_.max_series;
+  // parse
+  d_bytes_ = (uint8_t*)dmalloc(cfg_.max_batch_bytes + 256);
+  HIP_OK(hipHostMalloc((void**)&h_bytes_, cfg_.max_batch_bytes + 256, hipHostMallocDefault));
+  d_chunk_begin_ = (uint32_t*)dmalloc((cfg_.max_chunks + 2) * 4);
+  d_chunk_kind_ = (uint8_t*)dmalloc(cfg_.max_chunks + 2);
+  d_chunk_file_ = (uint32_t*)dmalloc((cfg_.max_chunks + 2) * 4);
+  HIP_OK(hipHostMalloc((void**)&h_chunk_begin_, (cfg_.max_chunks + 2) * 4, hipHostMallocDefault));
+  HIP_OK(hipHostMalloc((void**)&h_chunk_kind_, cfg_.max_chunks + 2, hipHostMallocDefault));
+  HIP_OK(hipHostMalloc((void**)&h_chunk_file_, (cfg_.max_chunks + 2) * 4, hipHostMallocDefault));
+  d_parse_ws_ = dmalloc(apm_parse_workspace_bytes(cfg_.max_batch_bytes, cfg_.max_lines, cfg_.max_chunks));
+  d_events_ = (Event*)dmalloc((size_t)cfg_.max_lines * sizeof(Event));
+  HIP_OK(hipHostMalloc((void**)&h_events_, (size_t)cfg_.max_lines * sizeof(Event), hipHostMallocDefault));
+  d_counts_ = (uint32_t*)dmalloc(16);
+  HIP_OK(hipHostMalloc((void**)&h_counts_, 16, hipHostMallocDefault));
+  d_watermark_ = (unsigned long long*)dmalloc(8);
+  HIP_OK(hipHostMalloc((void**)&h_watermark_, 8, hipHostMallocDefault));
+  d_file_open_ = (uint8_t*)dmalloc(1 << 16);
+  // stats
+  d_counts_cells_ = (int32_t*)dmalloc((size_t)NSLOT * S * 4);
+  d_cells_ = (int32_t*)dmalloc((size_t)NSLOT * S * cfg_.cell_cap * 4);
+  d_spill_n_ = (int32_t*)dmalloc(NSLOT * 4);
+  d_spill_series_ = (int32_t*)dmalloc((size_t)NSLOT * cfg_.spill_cap * 4);
+  d_spill_val_ = (int32_t*)dmalloc((size_t)NSLOT * cfg_.spill_cap * 4);
+  d_active_ = (uint8_t*)dmalloc(S);
+  d_win_ = (WinStat*)dmalloc((size_t)S * sizeof(WinStat));
+  d_big_list_ = (int32_t*)dmalloc((size_t)S * 4);
+  d_big_n_ = (int32_t*)dmalloc(4);
+  for (int i = 0; i < NSLOT; ++i) slot_bucket_[i] = NO_BUCKET;
+  // z-score
+  for (int l = 0; l < cfg_.n_lags; ++l) {
+    LagState& L = lag_[l];
+    L.ring = dmalloc((size_t)NSTAT * cfg_.lags[l] * S * cfg_.ring_bytes);
+    L.len = (int32_t*)dmalloc((size_t)S * 4);
+    L.sum = (double*)dmalloc((size_t)NSTAT * S * 8);
+    L.comp = (double*)dmalloc((size_t)NSTAT * S * 8);
+    L.sumsq = (double*)dmalloc((size_t)NSTAT * S * 8);
+    L.sqcomp = (double*)dmalloc((size_t)NSTAT * S * 8);
+    L.cnt = (int32_t*)dmalloc((size_t)NSTAT * S * 4);
+    L.thr = (double*)dmalloc((size_t)S * 8);
+    L.infl = (double*)dmalloc((size_t)S * 8);
+    L.out = (ZOut*)dmalloc((size_t)S * sizeof(ZOut));
+    L.counter = (int32_t*)dmalloc((size_t)S * 4);
+  }
+  {
+    const double* sp[MAX_LAGS] = {};
+    const double* cp[MAX_LAGS] = {};
+    const int32_t* np[MAX_LAGS] = {};
+    for (int l = 0; l < cfg_.n_lags; ++l) { sp[l] = lag_[l].sum; cp[l] = lag_[l].comp; np[l] = lag_[l].cnt; }
+    d_lag_sum_ptrs_ = dmalloc(sizeof(sp));
+    d_lag_comp_ptrs_ = dmalloc(sizeof(cp));
+    d_lag_cnt_ptrs_ = dmalloc(sizeof(np));
+    HIP_OK(hipMemcpy(d_lag_sum_ptrs_, sp, sizeof(sp), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_lag_comp_ptrs_, cp, sizeof(cp), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_lag_cnt_ptrs_, np, sizeof(np), hipMemcpyHostToDevice));
+    d_series_service_ = (int32_t*)dmalloc((size_t)S * 4);
+  }
+  d_hard_max_ = (double*)dmalloc((size_t)S * 8);
+  d_suppressed_ = (uint8_t*)dmalloc(S);
+  d_emit_key_ = (uint64_t*)dmalloc((size_t)S * 8);
+  // alerts
+  d_alerts_ = (AlertRec*)dmalloc((size_t)cfg_.max_alerts * sizeof(AlertRec));
+  d_n_alerts_ = (int32_t*)dmalloc(16);
+  HIP_OK(hipHostMalloc((void**)&h_alerts_, (size_t)cfg_.max_alerts * sizeof(AlertRec), hipHostMallocDefault));
+  HIP_OK(hipHostMalloc((void**)&h_n_alerts_, 16, hipHostMallocDefault));
+  // tx + release
+  d_tx_ = (TxRec*)dmalloc((size_t)cfg_.max_tx_per_batch * sizeof(TxRec));
+  HIP_OK(hipHostMalloc((void**)&h_tx_, (size_t)cfg_.max_tx_per_batch * sizeof(TxRec), hipHostMallocDefault));
+  d_gid_ = (int64_t*)dmalloc((size_t)cfg_.max_tx_per_batch * 8);
+  HIP_OK(hipHostMalloc((void**)&h_gid_, (size_t)cfg_.max_tx_per_batch * 8, hipHostMallocDefault));
+  d_tail_end_ = (int64_t*)dmalloc((size_t)cfg_.pool_cap * 8);
+  d_tail_gid_ = (int64_t*)dmalloc((size_t)cfg_.pool_cap * 8);
+  d_sort_end_ = (int64_t*)dmalloc((size_t)cfg_.pool_cap * 8);
+  d_sort_gid_ = (int64_t*)dmalloc((size_t)cfg_.pool_cap * 8);
+  for (int i = 0; i < 2; ++i) {
+    d_pool_end_[i] = (int64_t*)dmalloc((size_t)cfg_.pool_cap * 8);
+    d_pool_gid_[i] = (int64_t*)dmalloc((size_t)cfg_.pool_cap * 8);
+  }
+  release_tmp_bytes_ = apm_release_tmp_bytes(cfg_.pool_cap);
+  d_release_tmp_ = dmalloc(release_tmp_bytes_);
+  HIP_OK(hipHostMalloc((void**)&h_release_gid_, (size_t)cfg_.pool_cap * 8, hipHostMallocDefault));
+  // threads
+  int nt = cfg_.join_threads;
+  if (nt <= 0) nt = (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+  pool_.reset(new ThreadPool(nt > 1 ? nt : 0));
+  for (int l = 0; l < MAX_LAGS; ++l) { alias_thr_[l] = cfg_.thr[l]; alias_infl_[l] = cfg_.infl[l]; }
+  HIP_OK(hipStreamSynchronize(stream_));
+  HIP_OK(hipDeviceSynchronize());
+}
+
+Engine::~Engine() {
+  hipStreamSynchronize(stream_);
+  for (void* p : allocations_) hipFree(p);
+  hipHostFree(h_bytes_); hipHostFree(h_chunk_begin_); hipHostFree(h_chunk_kind_); hipHostFree(h_chunk_file_);
+  hipHostFree(h_events_); hipHostFree(h_counts_); hipHostFree(h_watermark_); hipHostFree(h_alerts_);
+  hipHostFree(h_n_alerts_); hipHostFree(h_tx_); hipHostFree(h_gid_); hipHostFree(h_release_gid_);
+  hipEventDestroy(ev_a_); hipEventDestroy(ev_b_);
+  hipStreamDestroy(stream_); hipStreamDestroy(comm_stream_);
+}
+
+int32_t Engine::add_server(const std::string& name) {
+  auto it = server_ids_.find(name);
+  if (it != server_ids_.end()) return it->second;
+  const int32_t id = (int32_t)servers_.size();
+  servers_.push_back(name);
+  server_ids_[name] = id;
+  server_rank_.push_back(-1);
+  server_next_service_.push_back(0);
+  JoinConfig jc;
+  jc.record_ttl_ms = cfg_.record_ttl_ms;
+  jc.acct_ttl_ms = cfg_.acct_ttl_ms;
+  jc.need_ttl_ms = cfg_.need_ttl_ms;
+  jc.tz = cfg_.tz;
+  shards_.emplace_back(new JoinShard(jc, &dict_, &files_));
+  return id;
+}
+
+int32_t Engine::add_file(const std::string& path, int kind, const std::string& server) {
+  const int32_t sid = add_server(server);
+  files_.push_back(FileInfo{path, sid, (uint8_t)kind});
+  if (files_.size() > (1 << 16)) throw std::runtime_error("too many files");
+  return (int32_t)files_.size() - 1;
+}
+
+void Engine::set_override(const std::string& service, const ServiceOverride& o) { overrides_[service] = o; }
+void Engine::clear_overrides() { overrides_.clear(); }
+
+// ----------------------------------------------------------------------------- series
+void Engine::compute_series_settings(int32_t s, double* thr, double* infl, double& hard_max, uint8_t& suppressed) {
+  const std::string& svc = dict_.service_name(series_[s].service);
+  auto it = overrides_.find(svc);
+  // z-score settings (stream_calc_z_score.js:106-150); with Q4 emulation the override is
+  // written into the shared defaults and leaks into every later lookup.
+  double* base_thr = cfg_.emulate_aliasing ? alias_thr_ : cfg_.thr;
+  double* base_infl = cfg_.emulate_aliasing ? alias_infl_ : cfg_.infl;
+  double t[MAX_LAGS], f[MAX_LAGS];
+  for (int l = 0; l < cfg_.n_lags; ++l) { t[l] = base_thr[l]; f[l] = base_infl[l]; }
+  if (it != overrides_.end()) {
+    for (int l = 0; l < cfg_.n_lags; ++l) {
+      if (it->second.has_thr[l] && (!cfg_.emulate_aliasing || it->second.thr[l] != 0)) t[l] = it->second.thr[l];
+      if (it->second.has_infl[l] && (!cfg_.emulate_aliasing || it->second.infl[l] != 0)) f[l] = it->second.infl[l];
+    }
+    if (cfg_.emulate_aliasing)
+      for (int l = 0; l < cfg_.n_lags; ++l) { alias_thr_[l] = t[l]; alias_infl_[l] = f[l]; }
+  }
+  for (int l = 0; l < cfg_.n_lags; ++l) { thr[l] = t[l]; infl[l] = f[l]; }
+  hard_max = cfg_.hard_max_ms;
+  suppressed = 0;
+  if (it != overrides_.end()) {
+    if (it->second.hard_max != 0) hard_max = it->second.hard_max;
+    suppressed = it->second.suppressed ? 1 : 0;
+  }
+}
+
+int32_t Engine::series_for(int32_t server, int32_t service) {
+  const uint64_t key = ((uint64_t)(uint32_t)server << 32) | (uint32_t)service;
+  auto it = series_map_.find(key);
+  if (it != series_map_.end()) return it->second;
+  if (n_series_ >= cfg_.max_series) return -1;
+  const int32_t s = n_series_++;
+  series_map_[key] = s;
+  if (server_rank_[server] < 0) server_rank_[server] = next_server_rank_++;
+  const uint64_t ek = ((uint64_t)server_rank_[server] << 24) | (uint64_t)(server_next_service_[server]++);
+  series_.push_back(SeriesInfo{server, service, ek});
+  h_emit_key_.push_back(ek);
+  h_thr_.resize((size_t)n_series_ * MAX_LAGS);
+  h_infl_.resize((size_t)n_series_ * MAX_LAGS);
+  h_hard_max_.push_back(cfg_.hard_max_ms);
+  h_suppressed_.push_back(0);
+  zscore_seen_.push_back(0);
+  h_active_.push_back(0);
+  return s;
+}
+
+// Series settings are resolved when the z-score stage first sees the series (its first `st`),
+// in emission order -- which is what makes Q4 emulation reproduce the reference exactly.
+void Engine::apply_series_settings(int32_t s) {
+  double thr[MAX_LAGS], infl[MAX_LAGS];
+  double hm;
+  uint8_t sup;
+  compute_series_settings(s, thr, infl, hm, sup);
+  for (int l = 0; l < MAX_LAGS; ++l) { h_thr_[(size_t)s * MAX_LAGS + l] = thr[l]; h_infl_[(size_t)s * MAX_LAGS + l] = infl[l]; }
+  h_hard_max_[s] = hm;
+  h_suppressed_[s] = sup;
+}
+
+void Engine::refresh_series_settings() {
+  // config hot reload (updateAllServiceSettings, stream_calc_z_score.js:152-167)
+  for (int l = 0; l < MAX_LAGS; ++l) { alias_thr_[l] = cfg_.thr[l]; alias_infl_[l] = cfg_.infl[l]; }
+  std::vector<int32_t> order(n_series_);
+  for (int32_t i = 0; i < n_series_; ++i) order[i] = i;
+  std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return series_[a].emit_key < series_[b].emit_key; });
+  for (int32_t s : order) if (zscore_seen_[s]) apply_series_settings(s);
+  uploaded_series_ = 0;
+  upload_series_tables();
+}
+
+void Engine::upload_series_tables() {
+  if (uploaded_series_ >= n_series_ && uploaded_series_ != 0) {
+    // thresholds may change for already-uploaded series (first st); upload everything dirty
+  }
+  const int32_t n = n_series_;
+  if (n == 0) return;
+  std::vector<double> col(n);
+  for (int l = 0; l < cfg_.n_lags; ++l) {
+    for (int32_t s = 0; s < n; ++s) col[s] = h_thr_[(size_t)s * MAX_LAGS + l];
+    HIP_OK(hipMemcpyAsync(lag_[l].thr, col.data(), (size_t)n * 8, hipMemcpyHostToDevice, stream_));
+    for (int32_t s = 0; s < n; ++s) col[s] = h_infl_[(size_t)s * MAX_LAGS + l];
+    HIP_OK(hipMemcpyAsync(lag_[l].infl, col.data(), (size_t)n * 8, hipMemcpyHostToDevice, stream_));
+  }
+  HIP_OK(hipMemcpyAsync(d_hard_max_, h_hard_max_.data(), (size_t)n * 8, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpyAsync(d_suppressed_, h_suppressed_.data(), (size_t)n, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpyAsync(d_emit_key_, h_emit_key_.data(), (size_t)n * 8, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));  // `col` is pageable and reused
+  uploaded_series_ = n;
+}
+
+JoinCounters Engine::join_counters() const {
+  JoinCounters t;
+  for (auto& s : shards_) {
+    const JoinCounters& c = s->counters;
+    t.events += c.events; t.tx += c.tx; t.tx_db += c.tx_db; t.expired_partials += c.expired_partials;
+    t.need_expired += c.need_expired; t.ejb_exit_unmatched += c.ejb_exit_unmatched;
+    t.invalid_acct += c.invalid_acct; t.audit_errors += c.audit_errors; t.host_fallback += c.host_fallback;
+  }
+  return t;
+}
+
+// ----------------------------------------------------------------------------- batch
+void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const std::vector<Chunk>& chunks_in,
+                           double now_override) {
+  const double t0 = now_ms();
+  if (n_bytes > cfg_.max_batch_bytes) throw std::runtime_error("batch larger than max_batch_bytes");
+  if (chunks_in.size() > cfg_.max_chunks) throw std::runtime_error("too many chunks in batch");
+  // Canonical order: chunks grouped by server (shard) then file, keeping the caller's order
+  // otherwise; the batch is re-laid out contiguously in that order in pinned memory.
+  std::vector<size_t> order(chunks_in.size());
+  for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+    return files_[chunks_in[a].file].server < files_[chunks_in[b].file].server;
+  });
+  std::vector<int32_t> chunk_file(chunks_in.size());
+  uint64_t off = 0;
+  // Fast path: chunks already canonical and contiguous from 0 (bench corpus, tailer output) ->
+  // no host copy; the H2D reads the caller's (ideally pinned) buffer directly.
+  bool canonical = true;
+  for (size_t k = 0; k < order.size(); ++k) {
+    const Chunk& c = chunks_in[k];
+    if (order[k] != k || c.begin != off) { canonical = false; break; }
+    off = c.end;
+  }
+  canonical = canonical && off == n_bytes && n_bytes + 64 <= cfg_.max_batch_bytes + 256;
+  const uint8_t* hb = h_bytes_;
+  if (canonical) {
+    hb = host_bytes;
+    for (size_t k = 0; k < order.size(); ++k) {
+      const Chunk& c = chunks_in[k];
+      if (c.end > c.begin && host_bytes[c.end - 1] != '\n') throw std::runtime_error("chunk must end with a newline");
+      h_chunk_begin_[k] = (uint32_t)c.begin;
+      h_chunk_kind_[k] = files_[c.file].kind;
+      h_chunk_file_[k] = (uint32_t)c.file;
+      chunk_file[k] = c.file;
+    }
+  } else {
+    off = 0;
+    const bool in_place = host_bytes == h_bytes_;
+    std::vector<uint8_t> tmp_copy;
+    const uint8_t* src = host_bytes;
+    if (in_place) {  // caller filled our staging buffer: copy aside before re-layout
+      tmp_copy.assign(host_bytes, host_bytes + n_bytes);
+      src = tmp_copy.data();
+    }
+    for (size_t k = 0; k < order.size(); ++k) {
+      const Chunk& c = chunks_in[order[k]];
+      const uint64_t len = c.end - c.begin;
+      if (len > 0 && src[c.end - 1] != '\n') throw std::runtime_error("chunk must end with a newline");
+      std::memcpy(h_bytes_ + off, src + c.begin, len);
+      h_chunk_begin_[k] = (uint32_t)off;
+      h_chunk_kind_[k] = files_[c.file].kind;
+      h_chunk_file_[k] = (uint32_t)c.file;
+      chunk_file[k] = c.file;
+      off += len;
+    }
+    std::memset(h_bytes_ + off, 0, 64);
+  }
+  const uint32_t n_chunks = (uint32_t)order.size();
+  h_chunk_begin_[n_chunks] = (uint32_t)off;
+  metrics_.bytes += off;
+  ++metrics_.batches;
+
+  // ---- K1/K2 on the GPU
+  HIP_OK(hipMemcpyAsync(d_bytes_, hb, off, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemsetAsync(d_bytes_ + off, 0, 64, stream_));
+  HIP_OK(hipMemcpyAsync(d_chunk_begin_, h_chunk_begin_, (n_chunks + 1) * 4, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpyAsync(d_chunk_kind_, h_chunk_kind_, n_chunks + 1, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpyAsync(d_chunk_file_, h_chunk_file_, (n_chunks + 1) * 4, hipMemcpyHostToDevice, stream_));
+  if (apm_parse_batch(d_bytes_, off, d_chunk_begin_, d_chunk_kind_, d_chunk_file_, n_chunks, d_parse_ws_,
+                      cfg_.max_lines, d_events_, d_counts_, d_counts_ + 1, d_watermark_, d_file_open_, &cfg_.tz,
+                      stream_) != 0)
+    throw std::runtime_error("parse workspace too small");
+  HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, 8, hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipMemcpyAsync(h_watermark_, d_watermark_, 8, hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+  const uint32_t n_events = h_counts_[0];
+  last_n_events_ = n_events;
+  const uint32_t n_lines = h_counts_[1];
+  if (n_lines > cfg_.max_lines) throw std::runtime_error("batch has more lines than max_lines");
+  metrics_.lines += n_lines;
+  metrics_.events += n_events;
+  if (n_events) {
+    HIP_OK(hipMemcpyAsync(h_events_, d_events_, (size_t)n_events * sizeof(Event), hipMemcpyDeviceToHost, stream_));
+    HIP_OK(hipStreamSynchronize(stream_));
+  }
+  const double t1 = now_ms();
+  metrics_.t_parse_ms += t1 - t0;
+
+  // ---- join on the host, one task per server shard
+  const double clock = now_override >= 0 ? now_override : watermark_;
+  std::vector<std::pair<uint32_t, uint32_t>> shard_range(shards_.size(), {0, 0});
+  {
+    // events are in chunk order and chunks are grouped by server -> contiguous per shard
+    uint32_t i = 0;
+    while (i < n_events) {
+      const int32_t srv = files_[chunk_file[h_events_[i].chunk]].server;
+      uint32_t j = i;
+      while (j < n_events && files_[chunk_file[h_events_[j].chunk]].server == srv) ++j;
+      shard_range[srv] = {i, j};
+      i = j;
+    }
+  }
+  pool_->run((int)shards_.size(), [&](int s) {
+    JoinShard& sh = *shards_[s];
+    sh.out().clear();
+    sh.begin_batch(clock, batch_no_);
+    const auto r = shard_range[s];
+    if (r.second > r.first) sh.process(h_events_ + r.first, r.second - r.first, hb, chunk_file);
+  });
+  // merge shard outputs by (expiry-before-lines, key)
+  std::vector<TxOut> txs;
+  {
+    size_t total = 0;
+    for (auto& sh : shards_) total += sh->out().size();
+    txs.reserve(total);
+    using Item = std::pair<uint64_t, std::pair<int, size_t>>;
+    std::priority_queue<Item, std::vector<Item>, std::greater<Item>> pq;
+    for (int s = 0; s < (int)shards_.size(); ++s)
+      if (!shards_[s]->out().empty()) pq.push({shards_[s]->out()[0].seq, {s, 0}});
+    while (!pq.empty()) {
+      auto it = pq.top();
+      pq.pop();
+      auto& v = shards_[it.second.first]->out();
+      txs.push_back(std::move(v[it.second.second]));
+      const size_t nx = it.second.second + 1;
+      if (nx < v.size()) pq.push({v[nx].seq, {it.second.first, nx}});
+    }
+  }
+  const double t2 = now_ms();
+  metrics_.t_join_ms += t2 - t1;
+
+  // ---- stats / z-score / alerts on the GPU
+  stats_for_batch(txs, t0);
+  const double t3 = now_ms();
+  metrics_.t_stats_ms += t3 - t2;
+  metrics_.t_total_ms += t3 - t0;
+
+  // advance the watermark clock (max leading timestamp seen so far)
+  const unsigned long long wm = *h_watermark_;
+  if (wm) {
+    const double w = (double)((long long)wm - (1LL << 62));
+    if (w > watermark_) watermark_ = w;
+  }
+  ++batch_no_;
+}
+
+void Engine::ensure_bucket_slot(int64_t b) {
+  const int slot = (int)(((b % NSLOT) + NSLOT) % NSLOT);
+  if (slot_bucket_[slot] == b) return;
+  if (slot_bucket_[slot] != NO_BUCKET) {
+    StatsState st{d_counts_cells_, d_cells_, d_spill_n_, d_spill_series_, d_spill_val_, d_active_,
+                  cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series};
+    apm_stats_clear_slot(&st, slot, stream_);
+  }
+  slot_bucket_[slot] = b;
+}
+
+void Engine::stats_for_batch(std::vector<TxOut>& txs, double batch_t0) {
+  const int keep = cfg_.keep_text;
+  const int64_t latest_at_start = latest_;
+  // split: audit non-Provider records go straight to db_insert (Q18)
+  std::vector<std::pair<uint32_t, int64_t>> triggers;  // (index in upload, new latest)
+  uint32_t n = 0;
+  for (uint32_t i = 0; i < txs.size(); ++i) {
+    TxOut& t = txs[i];
+    ++metrics_.tx;
+    if (t.to_db) {
+      ++metrics_.tx_db;
+      if (keep) text_["audit_db"].push_back(fmt::tx_line(t, servers_, dict_));
+      continue;
+    }
+    if (keep) text_["transactions"].push_back(fmt::tx_line(t, servers_, dict_));
+    // NaN / short endTs would wedge the reference's heap forever: dropped and counted (fix)
+    if (!(t.end_ms == t.end_ms) || t.end_ms < 10000) { ++metrics_.tx_dropped; continue; }
+    const int64_t end = (int64_t)t.end_ms;
+    const int64_t b = end / 10000;
+    // a tx with a newer bucket triggers the rollover *before* it is added (:348-370)
+    if (b > latest_) { triggers.push_back({n, b}); latest_ = b; }
+    if (n >= (uint32_t)cfg_.max_tx_per_batch) throw std::runtime_error("too many tx in one batch");
+    const int32_t s = series_for(t.server, t.service);
+    TxRec r;
+    r.end_ms = end;
+    r.series = s;
+    const double e = t.elapsed;
+    r.elapsed = (e == e && e >= -2147483647.0 && e <= 2147483647.0) ? (int32_t)e : ELAPSED_NAN;
+    h_tx_[n] = r;
+    const int64_t gid = next_gid_++;
+    h_gid_[n] = gid;
+    if (cfg_.keep_tx_records || keep) tx_records_.emplace(gid, t);
+    pool_bucket_count_[b] += 1;
+    if (end == b * 10000) pool_exact_edge_[b] += 1;
+    ++n;
+  }
+  if (n == 0) return;
+  HIP_OK(hipMemcpyAsync(d_tx_, h_tx_, (size_t)n * sizeof(TxRec), hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpyAsync(d_gid_, h_gid_, (size_t)n * 8, hipMemcpyHostToDevice, stream_));
+  StatsState st{d_counts_cells_, d_cells_, d_spill_n_, d_spill_series_, d_spill_val_, d_active_,
+                cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series};
+  const int64_t keep_iv = cfg_.window + cfg_.buffer;
+  auto append = [&](uint32_t lo, uint32_t hi, int64_t lat) {
+    if (hi <= lo) return;
+    const int64_t min_live = lat - keep_iv;
+    int64_t seen[8];
+    int nseen = 0;
+    for (uint32_t i = lo; i < hi; ++i) {
+      const TxRec& r = h_tx_[i];
+      if (r.series >= 0 && r.series < (int32_t)h_active_.size()) h_active_[r.series] = 1;
+      const int64_t b = r.end_ms / 10000;
+      if (b < min_live) continue;
+      bool dup = false;
+      for (int k = 0; k < nseen; ++k) dup |= seen[k] == b;
+      if (dup) continue;
+      ensure_bucket_slot(b);
+      if (nseen < 8) seen[nseen++] = b;
+    }
+    apm_bucket_append(d_tx_, lo, hi, &st, min_live, stream_);
+    apm_pool_append(d_tx_, lo, hi, d_gid_, d_tail_end_, d_tail_gid_, tail_n_, stream_);
+    tail_n_ += hi - lo;
+  };
+  uint32_t seg_lo = 0;
+  int64_t cur_latest = latest_at_start;
+  for (auto& tr : triggers) {
+    append(seg_lo, tr.first, cur_latest);
+    do_rollover(tr.second, batch_t0);
+    cur_latest = tr.second;
+    seg_lo = tr.first;
+  }
+  append(seg_lo, n, cur_latest);
+}
+
+void Engine::do_rollover(int64_t L, double batch_t0) {
+  const int64_t keep_iv = cfg_.window + cfg_.buffer;
+  ++metrics_.rollovers;
+  // removeOldBuckets(36): drop every bucket < L - 36
+  for (int i = 0; i < NSLOT; ++i) {
+    if (slot_bucket_[i] != NO_BUCKET && slot_bucket_[i] < L - keep_iv) {
+      StatsState st{d_counts_cells_, d_cells_, d_spill_n_, d_spill_series_, d_spill_val_, d_active_,
+                    cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series};
+      apm_stats_clear_slot(&st, i, stream_);
+      slot_bucket_[i] = NO_BUCKET;
+    }
+  }
+  const int64_t edge_ts = (L - cfg_.buffer - 1) * 10000;
+  // ---- K9 release: merge the sorted pool with the sorted tail, hand out endTs <= edge
+  {
+    int64_t released = 0;
+    for (auto it = pool_bucket_count_.begin(); it != pool_bucket_count_.end();) {
+      if (it->first * 10000 + 9999 <= edge_ts) { released += it->second; it = pool_bucket_count_.erase(it); }
+      else break;
+    }
+    const int64_t eb = edge_ts / 10000;
+    auto ex = pool_exact_edge_.find(eb);
+    if (ex != pool_exact_edge_.end()) {
+      released += ex->second;
+      pool_bucket_count_[eb] -= ex->second;
+      if (pool_bucket_count_[eb] == 0) pool_bucket_count_.erase(eb);
+      pool_exact_edge_.erase(ex);
+    }
+    for (auto it = pool_exact_edge_.begin(); it != pool_exact_edge_.end();) {
+      if (it->first < eb) it = pool_exact_edge_.erase(it); else break;
+    }
+    const int nxt = pool_cur_ ^ 1;
+    if (pool_n_ + tail_n_ > cfg_.pool_cap) throw std::runtime_error("release pool overflow");
+    if (apm_release_merge(d_pool_end_[pool_cur_] + pool_off_, d_pool_gid_[pool_cur_] + pool_off_, pool_n_,
+                          d_tail_end_, d_tail_gid_, tail_n_, d_sort_end_, d_sort_gid_, d_pool_end_[nxt],
+                          d_pool_gid_[nxt], d_release_tmp_, release_tmp_bytes_, stream_) != 0)
+      throw std::runtime_error("release tmp too small");
+    pool_cur_ = nxt;
+    pool_n_ = pool_n_ + tail_n_;
+    tail_n_ = 0;
+    if (released > pool_n_) released = pool_n_;
+    if ((cfg_.keep_tx_records || cfg_.keep_text) && released > 0) {
+      HIP_OK(hipMemcpyAsync(h_release_gid_, d_pool_gid_[pool_cur_], (size_t)released * 8, hipMemcpyDeviceToHost,
+                            stream_));
+      HIP_OK(hipStreamSynchronize(stream_));
+      for (int64_t i = 0; i < released; ++i) {
+        auto it = tx_records_.find(h_release_gid_[i]);
+        if (it == tx_records_.end()) continue;
+        if (cfg_.keep_text) text_["db"].push_back(fmt::tx_line(it->second, servers_, dict_));
+        tx_records_.erase(it);
+      }
+    }
+    metrics_.released += released;
+    pool_off_ = released;
+    pool_n_ -= released;
+    // the remaining pool now starts at pool_off_ inside the current buffer
+  }
+  // ---- first st for newly visible series: resolve their z-score settings in emission order
+  {
+    std::vector<int32_t> fresh;
+    for (int32_t s = 0; s < n_series_; ++s) if (!zscore_seen_[s]) fresh.push_back(s);
+    // a series is visible iff it had a tx before this rollover: all created series qualify except
+    // those whose first tx is the trigger or later -- the device `active` flag is authoritative;
+    // settings for not-yet-active series are computed now and harmlessly recomputed later.
+    std::sort(fresh.begin(), fresh.end(), [&](int32_t a, int32_t b) { return series_[a].emit_key < series_[b].emit_key; });
+    if (!fresh.empty()) {
+      bool dirty = false;
+      for (int32_t s : fresh) {
+        if (!h_active_[s]) continue;
+        zscore_seen_[s] = 1;
+        apply_series_settings(s);
+        dirty = true;
+      }
+      if (dirty) upload_series_tables();
+    }
+  }
+  // ---- K8 window statistics over buckets [L-36, L-6]
+  WindowArgs wa;
+  wa.st = StatsState{d_counts_cells_, d_cells_, d_spill_n_, d_spill_series_, d_spill_val_, d_active_,
+                     cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series};
+  wa.n_win = (int32_t)(keep_iv - cfg_.buffer + 1);
+  for (int r = 0; r < 32; ++r) wa.win_slots[r] = -1;
+  for (int r = 0; r < wa.n_win && r < 32; ++r) {
+    const int64_t b = L - keep_iv + r;
+    const int slot = (int)(((b % NSLOT) + NSLOT) % NSLOT);
+    wa.win_slots[r] = slot_bucket_[slot] == b ? slot : -1;
+  }
+  wa.tpm_div = (double)cfg_.window * cfg_.interval_len / 60.0;
+  wa.out = d_win_;
+  wa.big_list = d_big_list_;
+  wa.big_n = d_big_n_;
+  wa.n_series = n_series_;
+  apm_window_stats(&wa, stream_);
+  // ---- K10 z-score per LAG, K11 alert eval
+  HIP_OK(hipMemsetAsync(d_n_alerts_, 0, 4, stream_));
+  for (int l = 0; l < cfg_.n_lags; ++l) {
+    LagState& LS = lag_[l];
+    ZArgs za;
+    za.ring = LS.ring; za.len = LS.len; za.sum = LS.sum; za.comp = LS.comp; za.cnt = LS.cnt;
+    za.sumsq = LS.sumsq; za.sqcomp = LS.sqcomp; za.thr = LS.thr; za.infl = LS.infl; za.win = d_win_;
+    za.out = LS.out; za.S = cfg_.max_series; za.n_series = n_series_; za.lag = cfg_.lags[l];
+    za.head = (int32_t)(rollover_idx_ % cfg_.lags[l]);
+    za.exact = cfg_.exact_mean; za.sigma_stddev = cfg_.sigma_stddev; za.resync_k = cfg_.resync_k;
+    za.rollover_idx = rollover_idx_;
+    apm_zscore(&za, cfg_.ring_bytes, stream_);
+    AlertArgs aa;
+    aa.win = d_win_; aa.z = LS.out; aa.counter = LS.counter; aa.hard_max = d_hard_max_;
+    aa.suppressed = d_suppressed_; aa.emit_key = d_emit_key_; aa.out = d_alerts_; aa.n_out = d_n_alerts_;
+    aa.n_series = n_series_; aa.lag_idx = l; aa.n_lags = cfg_.n_lags; aa.lag_suppressed = cfg_.lag_suppressed[l];
+    aa.window = cfg_.alert_window; aa.threshold = cfg_.alert_threshold; aa.hard_min_ms = cfg_.hard_min_ms;
+    aa.hard_min_tpm = cfg_.hard_min_tpm; aa.both_only = cfg_.both_only; aa.max_out = cfg_.max_alerts;
+    apm_alert_eval(&aa, stream_);
+  }
+  ++rollover_idx_;
+  HIP_OK(hipMemcpyAsync(h_n_alerts_, d_n_alerts_, 4, hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+  metrics_.rollover_latency_ms.push_back(now_ms() - batch_t0);
+  if (cfg_.keep_text) format_rollover_text(edge_ts);
+  flush_alerts(edge_ts);
+}
+
+void Engine::flush_alerts(int64_t edge_ts) {
+  int32_t na = std::min(*h_n_alerts_, cfg_.max_alerts);
+  metrics_.alert_candidates += na;
+  if (na <= 0) return;
+  HIP_OK(hipMemcpyAsync(h_alerts_, d_alerts_, (size_t)na * sizeof(AlertRec), hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+  std::sort(h_alerts_, h_alerts_ + na, [](const AlertRec& a, const AlertRec& b) { return a.order < b.order; });
+  // per-(service|series) cooldown, first candidate in emission order wins (:436-468)
+  std::vector<WinStat> win;
+  std::vector<std::vector<ZOut>> z(cfg_.n_lags);
+  const bool need_rows = cfg_.keep_text != 0;
+  if (need_rows) {
+    download_winstats(win);
+    for (int l = 0; l < cfg_.n_lags; ++l) download_zout(l, z[l]);
+  }
+  const double now = cfg_.alert_clock_entry ? (double)edge_ts
+                                            : (double)std::chrono::duration_cast<std::chrono::milliseconds>(
+                                                  std::chrono::system_clock::now().time_since_epoch()).count();
+  for (int32_t i = 0; i < na; ++i) {
+    const AlertRec& r = h_alerts_[i];
+    const SeriesInfo& si = series_[r.series];
+    std::string key = dict_.service_name(si.service);
+    if (!cfg_.cooldown_by_service) key = servers_[si.server] + '\x01' + key;
+    auto it = last_alert_.find(key);
+    if (it != last_alert_.end() && !((now - it->second) / 1000.0 > cfg_.cooldown_ms / 1000.0)) continue;
+    last_alert_[key] = now;
+    ++metrics_.alerts;
+    if (need_rows) {
+      const std::string fs = fmt::fs_line(edge_ts, servers_[si.server], dict_.service_name(si.service),
+                                          cfg_.lags[r.lag_idx], win[r.series], z[r.lag_idx][r.series]);
+      text_["al"].push_back(fmt::al_line(now, edge_ts, servers_[si.server], dict_.service_name(si.service),
+                                         r.causes, fs));
+    }
+  }
+}
+
+void Engine::format_rollover_text(int64_t edge_ts) {
+  std::vector<WinStat> win;
+  download_winstats(win);
+  std::vector<std::vector<ZOut>> z(cfg_.n_lags);
+  for (int l = 0; l < cfg_.n_lags; ++l) download_zout(l, z[l]);
+  std::vector<int32_t> order;
+  for (int32_t s = 0; s < n_series_; ++s) if (win[s].active) order.push_back(s);
+  std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return series_[a].emit_key < series_[b].emit_key; });
+  auto& st = text_["st"];
+  auto& fs = text_["fs"];
+  // lag order: ascending LAG value (integer-keyed object iteration in the reference)
+  std::vector<int> lag_order(cfg_.n_lags);
+  for (int l = 0; l < cfg_.n_lags; ++l) lag_order[l] = l;
+  std::sort(lag_order.begin(), lag_order.end(), [&](int a, int b) { return cfg_.lags[a] < cfg_.lags[b]; });
+  for (int32_t s : order) {
+    const SeriesInfo& si = series_[s];
+    st.push_back(fmt::st_line(edge_ts, servers_[si.server], dict_.service_name(si.service), win[s]));
+    for (int l : lag_order)
+      fs.push_back(fmt::fs_line(edge_ts, servers_[si.server], dict_.service_name(si.service), cfg_.lags[l], win[s], z[l][s]));
+  }
+}
+
+void Engine::download_winstats(std::vector<WinStat>& out) {
+  out.resize(std::max(n_series_, 1));
+  if (n_series_ == 0) return;
+  HIP_OK(hipMemcpyAsync(out.data(), d_win_, (size_t)n_series_ * sizeof(WinStat), hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+}
+
+void Engine::download_zout(int l, std::vector<ZOut>& out) {
+  out.resize(std::max(n_series_, 1));
+  if (n_series_ == 0) return;
+  HIP_OK(hipMemcpyAsync(out.data(), lag_[l].out, (size_t)n_series_ * sizeof(ZOut), hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+}
+
+std::vector<std::string> Engine::take(const std::string& kind) {
+  std::vector<std::string> r;
+  r.swap(text_[kind]);
+  return r;
+}
+
+void Engine::warm_history(uint64_t seed) {
+  // Use the latest window stats as the per-series baseline; fill every lag ring completely.
+  for (int l = 0; l < cfg_.n_lags; ++l) {
+    LagState& LS = lag_[l];
+    ZArgs za{};
+    za.ring = LS.ring; za.len = LS.len; za.sum = LS.sum; za.comp = LS.comp; za.cnt = LS.cnt;
+    za.sumsq = LS.sumsq; za.sqcomp = LS.sqcomp; za.S = cfg_.max_series; za.n_series = n_series_;
+    za.lag = cfg_.lags[l]; za.head = (int32_t)(rollover_idx_ % cfg_.lags[l]);
+    apm_zscore_warm(&za, cfg_.ring_bytes, cfg_.lags[l], seed + l, d_win_, stream_);
+  }
+  HIP_OK(hipStreamSynchronize(stream_));
+}
+
+uintptr_t Engine::alloc_pinned(size_t n) {
+  void* p = nullptr;
+  HIP_OK(hipHostMalloc(&p, n + 256, hipHostMallocDefault));
+  return (uintptr_t)p;
+}
+
+void Engine::free_pinned(uintptr_t p) { hipHostFree((void*)p); }
+
+void Engine::pack_service_moments(double* d_dst, int32_t cap, hipStream_t stream) {
+  // series -> service table (grows with the dictionary)
+  if (series_service_uploaded_ < n_series_) {
+    std::vector<int32_t> sv(n_series_);
+    for (int32_t s = 0; s < n_series_; ++s) sv[s] = series_[s].service;
+    HIP_OK(hipMemcpyAsync(d_series_service_, sv.data(), (size_t)n_series_ * 4, hipMemcpyHostToDevice, stream_));
+    HIP_OK(hipStreamSynchronize(stream_));
+    series_service_uploaded_ = n_series_;
+  }
+  // the pack reads the z-score state written on the main stream: order comm after it
+  HIP_OK(hipEventRecord(ev_a_, stream_));
+  HIP_OK(hipStreamWaitEvent(stream, ev_a_, 0));
+  apm_service_moments(d_series_service_, d_active_, n_series_, cfg_.max_series, cfg_.n_lags, cap,
+                      (const double* const*)d_lag_sum_ptrs_, (const double* const*)d_lag_comp_ptrs_,
+                      (const int32_t* const*)d_lag_cnt_ptrs_, d_dst, stream);
+}
+
+}  // namespace apm

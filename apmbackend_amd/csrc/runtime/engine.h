@@ -1,0 +1,290 @@
+// apm::Engine -- one MI355X-resident APM pipeline (one process per GPU).
+//
+//   host batch (pinned) --H2D--> K1/K2 parse (GPU) --D2H events--> join workers (host, per JVM)
+//   --tx--> K7 bucket append / rollover: K8 window stats -> K10 z-score (per LAG) -> K11 alert
+//   eval (GPU) --D2H alert candidates--> cooldown + sinks (host).  K9 keeps the released-tx pool
+//   sorted by endTs on the GPU.
+//
+// The engine is the fused equivalent of the reference's five stage processes
+// (stream_parse_transactions -> stream_calc_stats -> stream_calc_z_score ->
+// stream_process_alerts -> stream_insert_db) with the RabbitMQ hops replaced by device buffers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../apm_types.h"
+#include "join.h"
+
+namespace apm {
+
+struct ServiceOverride {
+  bool has_thr[MAX_LAGS] = {false, false, false, false};
+  bool has_infl[MAX_LAGS] = {false, false, false, false};
+  double thr[MAX_LAGS] = {0, 0, 0, 0};
+  double infl[MAX_LAGS] = {0, 0, 0, 0};
+  double hard_max = 0;  // 0 = use default (the reference ignores falsy overrides)
+  bool suppressed = false;
+};
+
+struct EngineConfig {
+  int device = 0;
+  int32_t max_series = 1 << 17;
+  int32_t cell_cap = 16;
+  int32_t spill_cap = 1 << 20;
+  uint64_t max_batch_bytes = 64ull << 20;
+  uint32_t max_lines = 1u << 21;
+  uint32_t max_chunks = 4096;
+  int64_t pool_cap = 1 << 23;
+  int32_t max_tx_per_batch = 1 << 21;
+  int32_t max_alerts = 1 << 16;
+  int ring_bytes = 8;            // 8 = float64, 4 = float32
+  int exact_mean = 0;
+  int sigma_stddev = 0;
+  int resync_k = 360;
+  int n_lags = 2;
+  int32_t lags[MAX_LAGS] = {360, 8640, 0, 0};
+  double thr[MAX_LAGS] = {20.0, 15.0, 0, 0};
+  double infl[MAX_LAGS] = {0.1, 0.0, 0, 0};
+  int emulate_aliasing = 0;
+  // alerts (streamProcessAlerts)
+  int alert_window = 60;
+  int alert_threshold = 45;
+  double hard_min_ms = 200;
+  double hard_min_tpm = 1.0;
+  double hard_max_ms = 10000;
+  int both_only = 1;
+  int lag_suppressed[MAX_LAGS] = {0, 0, 0, 0};
+  double cooldown_ms = 15 * 60000.0;
+  int cooldown_by_service = 1;
+  int alert_clock_entry = 1;
+  // stats (streamCalcStats)
+  int interval_len = 10;
+  int window = 30;
+  int buffer = 6;
+  // parse
+  double record_ttl_ms = 120000, acct_ttl_ms = 120000, need_ttl_ms = 30000;
+  TzTable tz{};
+  int join_threads = 0;
+  // outputs
+  int keep_text = 0;        // format tx/st/fs/al lines for sinks/tests
+  int keep_tx_records = 0;  // keep full tx for the db release stream
+};
+
+struct Chunk {
+  int32_t file;
+  uint64_t begin, end;  // byte range in the batch (must end with '\n')
+};
+
+struct EngineMetrics {
+  uint64_t batches = 0, bytes = 0, lines = 0, events = 0, tx = 0, tx_db = 0, tx_dropped = 0;
+  uint64_t rollovers = 0, alerts = 0, alert_candidates = 0, series = 0, released = 0;
+  double t_parse_ms = 0, t_join_ms = 0, t_stats_ms = 0, t_total_ms = 0;
+  std::vector<double> rollover_latency_ms;   // batch arrival -> alert decision per rollover
+};
+
+class ThreadPool {
+ public:
+  explicit ThreadPool(int n);
+  ~ThreadPool();
+  void run(int n_tasks, const std::function<void(int)>& fn);
+  int size() const { return (int)workers_.size(); }
+
+ private:
+  std::vector<std::thread> workers_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int)>* fn_ = nullptr;
+  int n_tasks_ = 0, next_ = 0, done_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+class Engine {
+ public:
+  explicit Engine(const EngineConfig& cfg);
+  ~Engine();
+
+  int32_t add_server(const std::string& name);
+  int32_t add_file(const std::string& path, int kind, const std::string& server);
+  void set_override(const std::string& service, const ServiceOverride& o);
+  void clear_overrides();
+  void refresh_series_settings();
+
+  // Process one batch (synchronous). `now_override` < 0 uses the engine watermark clock.
+  void process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const std::vector<Chunk>& chunks,
+                     double now_override = -1.0);
+
+  // Text outputs accumulated since the last take (keep_text=1): "transactions", "audit_db",
+  // "db", "st", "fs", "al".
+  std::vector<std::string> take(const std::string& kind);
+
+  // Warm the z-score rings with a synthetic pre-history (benchmarks).
+  void warm_history(uint64_t seed);
+
+  // Fleet baseline exchange: per-service moments packed into `dst` (device pointer, doubles,
+  // layout [n_services][n_lags][NSTAT][3] = count, sum, sumsq of the current ring means).
+  int32_t n_services() const { return dict_.n_services(); }
+  void pack_service_moments(double* d_dst, int32_t n_services_cap, hipStream_t stream);
+
+  EngineMetrics metrics() const { return metrics_; }
+  const std::vector<std::string>& servers() const { return servers_; }
+  std::vector<std::string> services() const { return dict_.services_snapshot(); }
+  int32_t n_series() const { return n_series_; }
+  double watermark() const { return watermark_; }
+  hipStream_t stream() const { return stream_; }
+  hipStream_t comm_stream() const { return comm_stream_; }
+  size_t device_bytes() const { return device_bytes_; }
+  JoinCounters join_counters() const;
+
+  // events of the last batch (host copy) for kernel verification
+  std::string last_events() const { return std::string((const char*)h_events_, (size_t)last_n_events_ * sizeof(Event)); }
+  // pinned host memory for zero-copy ingest (bench corpus, tailer)
+  static uintptr_t alloc_pinned(size_t n);
+  static void free_pinned(uintptr_t p);
+
+  // Device views for tests / exchange
+  void download_winstats(std::vector<WinStat>& out);
+  void download_zout(int lag_idx, std::vector<ZOut>& out);
+
+ private:
+  struct SeriesInfo { int32_t server, service; uint64_t emit_key; };
+  int32_t series_for(int32_t server, int32_t service);
+  void apply_series_settings(int32_t s);
+  void compute_series_settings(int32_t s, double* thr, double* infl, double& hard_max, uint8_t& suppressed);
+  void stats_for_batch(std::vector<TxOut>& txs, double batch_t0);
+  void ensure_bucket_slot(int64_t b);
+  void do_rollover(int64_t L, double batch_t0);
+  void flush_alerts(int64_t edge_ts);
+  void format_rollover_text(int64_t edge_ts);
+  void upload_series_tables();
+  void* dmalloc(size_t bytes);
+
+  EngineConfig cfg_;
+  hipStream_t stream_ = nullptr, comm_stream_ = nullptr;
+  size_t device_bytes_ = 0;
+  std::vector<void*> allocations_;
+
+  // files / servers / dictionaries
+  std::vector<std::string> servers_;
+  std::unordered_map<std::string, int32_t> server_ids_;
+  std::vector<FileInfo> files_;
+  Dictionary dict_;
+  std::vector<std::unique_ptr<JoinShard>> shards_;  // one per server
+  std::unique_ptr<ThreadPool> pool_;
+
+  // series
+  std::unordered_map<uint64_t, int32_t> series_map_;
+  std::vector<SeriesInfo> series_;
+  int32_t n_series_ = 0;
+  std::vector<int32_t> server_rank_;            // first-appearance rank per server in the stats stream
+  std::vector<int32_t> server_next_service_;
+  int32_t next_server_rank_ = 0;
+  std::map<std::string, ServiceOverride> overrides_;
+  double alias_thr_[MAX_LAGS], alias_infl_[MAX_LAGS];  // defaults as mutated by Q4 emulation
+  std::vector<double> h_thr_, h_infl_, h_hard_max_;
+  std::vector<uint8_t> h_suppressed_;
+  std::vector<uint64_t> h_emit_key_;
+  int32_t uploaded_series_ = 0;
+  std::vector<int32_t> zscore_seen_;            // series already initialised in the z-score stage
+  std::vector<uint8_t> h_active_;               // host mirror of the stats `active` flag
+
+  // parse buffers
+  uint8_t* d_bytes_ = nullptr;
+  uint8_t* h_bytes_ = nullptr;                  // pinned staging
+  uint32_t* d_chunk_begin_ = nullptr;
+  uint8_t* d_chunk_kind_ = nullptr;
+  uint32_t* d_chunk_file_ = nullptr;
+  uint32_t* h_chunk_begin_ = nullptr;
+  uint8_t* h_chunk_kind_ = nullptr;
+  uint32_t* h_chunk_file_ = nullptr;
+  void* d_parse_ws_ = nullptr;
+  Event* d_events_ = nullptr;
+  Event* h_events_ = nullptr;
+  uint32_t* d_counts_ = nullptr;                // [0]=n_events [1]=n_lines
+  uint32_t* h_counts_ = nullptr;
+  unsigned long long* d_watermark_ = nullptr;
+  unsigned long long* h_watermark_ = nullptr;
+  uint8_t* d_file_open_ = nullptr;
+  TzTable* d_tz_unused_ = nullptr;
+
+  // stats state
+  int32_t* d_counts_cells_ = nullptr;
+  int32_t* d_cells_ = nullptr;
+  int32_t* d_spill_n_ = nullptr;
+  int32_t* d_spill_series_ = nullptr;
+  int32_t* d_spill_val_ = nullptr;
+  uint8_t* d_active_ = nullptr;
+  int64_t slot_bucket_[NSLOT];
+  int64_t latest_ = 0;
+  int64_t rollover_idx_ = 0;
+  WinStat* d_win_ = nullptr;
+  int32_t* d_big_list_ = nullptr;
+  int32_t* d_big_n_ = nullptr;
+
+  // z-score state per lag
+  struct LagState {
+    void* ring = nullptr;
+    int32_t* len = nullptr;
+    double *sum = nullptr, *comp = nullptr, *sumsq = nullptr, *sqcomp = nullptr;
+    int32_t* cnt = nullptr;
+    double *thr = nullptr, *infl = nullptr;
+    ZOut* out = nullptr;
+    int32_t* counter = nullptr;
+  } lag_[MAX_LAGS];
+  double* d_hard_max_ = nullptr;
+  void* d_lag_sum_ptrs_ = nullptr;
+  void* d_lag_comp_ptrs_ = nullptr;
+  void* d_lag_cnt_ptrs_ = nullptr;
+  int32_t* d_series_service_ = nullptr;
+  int32_t series_service_uploaded_ = 0;
+  uint8_t* d_suppressed_ = nullptr;
+  uint64_t* d_emit_key_ = nullptr;
+
+  // alerts
+  AlertRec* d_alerts_ = nullptr;
+  int32_t* d_n_alerts_ = nullptr;
+  AlertRec* h_alerts_ = nullptr;
+  int32_t* h_n_alerts_ = nullptr;
+  std::unordered_map<std::string, double> last_alert_;  // cooldown key -> alertTimestamp
+
+  // tx upload + release pool
+  TxRec* d_tx_ = nullptr;
+  TxRec* h_tx_ = nullptr;
+  int64_t* d_gid_ = nullptr;
+  int64_t* h_gid_ = nullptr;
+  int64_t *d_tail_end_ = nullptr, *d_tail_gid_ = nullptr, *d_sort_end_ = nullptr, *d_sort_gid_ = nullptr;
+  int64_t *d_pool_end_[2] = {nullptr, nullptr}, *d_pool_gid_[2] = {nullptr, nullptr};
+  int pool_cur_ = 0;
+  int64_t pool_off_ = 0, pool_n_ = 0, tail_n_ = 0;
+  void* d_release_tmp_ = nullptr;
+  size_t release_tmp_bytes_ = 0;
+  std::map<int64_t, int64_t> pool_bucket_count_;   // endTs bucket -> pending count (host mirror)
+  std::map<int64_t, int64_t> pool_exact_edge_;     // endTs == bucket start count
+  int64_t* h_release_gid_ = nullptr;
+  int64_t next_gid_ = 0;
+  std::unordered_map<int64_t, TxOut> tx_records_;  // keep_tx_records
+
+  uint32_t last_n_events_ = 0;
+
+  // watermark clock
+  double watermark_ = 0;
+  uint64_t batch_no_ = 0;
+
+  // text outputs
+  std::map<std::string, std::vector<std::string>> text_;
+  EngineMetrics metrics_;
+  hipEvent_t ev_a_, ev_b_;
+};
+
+}  // namespace apm

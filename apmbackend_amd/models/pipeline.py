@@ -1,0 +1,160 @@
+"""The flagship model: the fused MI355X APM pipeline.
+
+``APMEngine`` maps the reference configuration (``config/apm_config.json`` sections
+``streamParseTransactions`` .. ``streamProcessAlerts`` + the new ``gpu`` section) onto the native
+``_apm_native.Engine`` and exposes a batch API:
+
+    eng = APMEngine(cfg)
+    eng.process([(path, bytes), ...])          # one ingest batch (whole lines per file)
+    eng.take("fs"), eng.take("al"), ...        # reference wire-format records (keep_text=True)
+
+One engine == one GPU == one process; the multi-GPU runner (``parallel.dist``) shards JVM hosts
+across ranks.
+"""
+from __future__ import annotations
+
+import math
+from typing import Any, Dict, Iterable, List, Optional, Sequence, Tuple, Union
+
+from .. import _native
+from ..models.oracle import file_kind, server_of
+from ..ops.parse_ref import tz_table
+from ..utils.timeparse import TzOffset
+
+KIND_CODE = {"SOAP": 0, "SERVER": 1, "APP": 2}
+
+
+def engine_config(cfg: Dict[str, Any], device: int = 0, keep_text: bool = False, **kw) -> Dict[str, Any]:
+    g = cfg.get("gpu", {})
+    zc = cfg["streamCalcZScore"]
+    ac = cfg["streamProcessAlerts"]
+    sc = cfg["streamCalcStats"]
+    lags = sorted(((int(d["LAG"]), float(d["THRESHOLD"]), float(d["INFLUENCE"])) for d in zc["defaults"]),
+                  key=lambda x: x[0])
+    if len(lags) > 4:
+        raise ValueError("at most 4 LAG settings are supported per engine")
+    suppressed_lags = {int(x) for x in ac.get("suppressedLags", [])}
+    ring = {"float64": 8, "float32": 4}.get(g.get("ringDtype", "float64"), 8)
+    tz = TzOffset(g.get("timezone", "local"))
+    d = {
+        "device": device,
+        "max_series": int(g.get("maxSeries", 1 << 17)),
+        "cell_cap": int(g.get("bucketCellCapacity", 16)),
+        "spill_cap": int(g.get("bucketOverflowCapacity", 1 << 22)) // 40 or 1,
+        "max_batch_bytes": int(g.get("batchBytes", 32 << 20)) * 2,
+        "max_lines": int(g.get("maxLinesPerBatch", 1 << 20)) * 2,
+        "ring_bytes": ring,
+        "exact_mean": 1 if g.get("zscoreMeanMode", "rolling") == "exact" else 0,
+        "sigma_stddev": 1 if g.get("zscoreSigma", "sqrt_mean") == "stddev" else 0,
+        "resync_k": int(g.get("exactRecomputeEveryIntervals", 360)),
+        "emulate_aliasing": 1 if g.get("emulateOverrideAliasing", False) else 0,
+        "lags": lags,
+        "lag_suppressed": [1 if l[0] in suppressed_lags else 0 for l in lags],
+        "alert_window": int(ac["rollingAlertWindowSizeInIntervals"]),
+        "alert_threshold": int(ac["requiredNumberBadIntervalsInAlertWindowToTrigger"]),
+        "hard_min_ms": float(ac["hardMinMsAlertThreshold"]),
+        "hard_min_tpm": float(ac["hardMinTpmAlertThreshold"]),
+        "hard_max_ms": float(ac["hardMaxMsAlertThreshold"]),
+        "both_only": 1 if ac.get("alertOnBothOnly") else 0,
+        "cooldown_ms": float(ac["perServiceAlertCooldownInMinutes"]) * 60000.0,
+        "cooldown_by_service": 1 if g.get("cooldownKey", "service") == "service" else 0,
+        "alert_clock_entry": 1 if g.get("alertClock", "entry") == "entry" else 0,
+        "interval_len": int(sc["intervalLengthInSeconds"]),
+        "window": int(sc["windowSizeInIntervals"]),
+        "buffer": int(sc["bufferSizeInIntervals"]),
+        "record_ttl_ms": float(g.get("recordTtlSeconds", 120)) * 1000.0,
+        "acct_ttl_ms": float(g.get("acctTtlSeconds", 120)) * 1000.0,
+        "need_ttl_ms": float(g.get("needTtlSeconds", 30)) * 1000.0,
+        "tz_table": tz_table(tz),
+        "join_threads": int(g.get("joinThreads", 0)),
+        "keep_text": 1 if keep_text else 0,
+        "keep_tx_records": 1 if keep_text else 0,
+    }
+    if int(sc["intervalLengthInSeconds"]) != 10:
+        raise ValueError("intervalLengthInSeconds must be 10 (bucket label = endTs without 4 digits)")
+    d.update(kw)
+    return d
+
+
+def service_overrides(cfg: Dict[str, Any]) -> Dict[str, Dict[str, Any]]:
+    """Per-service override table: z-score THRESHOLD/INFLUENCE per LAG, alert hard max, suppression."""
+    zc = cfg["streamCalcZScore"]
+    ac = cfg["streamProcessAlerts"]
+    lags = sorted(int(d["LAG"]) for d in zc["defaults"])
+    out: Dict[str, Dict[str, Any]] = {}
+    for svc, per_lag in ((zc.get("overrides") or {}).get("services") or {}).items():
+        o = out.setdefault(svc, {"thr": [None] * len(lags), "infl": [None] * len(lags)})
+        for lag_key, vals in per_lag.items():
+            try:
+                li = lags.index(int(float(lag_key)))
+            except ValueError:
+                continue
+            if "THRESHOLD" in vals:
+                o["thr"][li] = float(vals["THRESHOLD"])
+            if "INFLUENCE" in vals:
+                o["infl"][li] = float(vals["INFLUENCE"])
+    for svc, vals in ((ac.get("overrides") or {}).get("services") or {}).items():
+        o = out.setdefault(svc, {"thr": [None] * len(lags), "infl": [None] * len(lags)})
+        hm = vals.get("hardMaxMsAlertThreshold")
+        if hm:
+            o["hard_max"] = float(hm)
+    for svc in ac.get("suppressedServices", []) or []:
+        o = out.setdefault(svc, {"thr": [None] * len(lags), "infl": [None] * len(lags)})
+        o["suppressed"] = True
+    return out
+
+
+class APMEngine:
+    def __init__(self, cfg: Dict[str, Any], device: int = 0, keep_text: bool = False, **kw):
+        self.cfg = cfg
+        self.N = _native.load()
+        self.ecfg = engine_config(cfg, device, keep_text, **kw)
+        self.eng = self.N.Engine(self.ecfg)
+        self.file_ids: Dict[str, int] = {}
+        self.apply_overrides(cfg)
+
+    def apply_overrides(self, cfg: Dict[str, Any]):
+        self.eng.clear_overrides()
+        for svc, o in service_overrides(cfg).items():
+            self.eng.set_override(svc, o)
+
+    def reload(self, cfg: Dict[str, Any]):
+        """Config hot reload: thresholds / overrides re-applied to every existing series."""
+        self.cfg = cfg
+        self.apply_overrides(cfg)
+        self.eng.refresh_series_settings()
+
+    def add_file(self, path: str, kind: Optional[str] = None, server: Optional[str] = None) -> int:
+        if path in self.file_ids:
+            return self.file_ids[path]
+        k = KIND_CODE[kind or file_kind(path)]
+        fid = self.eng.add_file(path, k, server or server_of(path))
+        self.file_ids[path] = fid
+        return fid
+
+    def process(self, chunks: Sequence[Tuple[Union[str, int], bytes]], now: Optional[float] = None):
+        parts, table = [], []
+        off = 0
+        for f, data in chunks:
+            if not data:
+                continue
+            if not data.endswith(b"\n"):
+                data = data + b"\n"
+            fid = f if isinstance(f, int) else self.add_file(f)
+            parts.append(data)
+            table.append((fid, off, off + len(data)))
+            off += len(data)
+        buf = b"".join(parts)
+        self.eng.process_batch(buf, table, -1.0 if now is None else float(now))
+
+    def process_lines(self, chunks: Sequence[Tuple[str, List[str]]], now: Optional[float] = None):
+        self.process([(fp, ("\n".join(ls) + "\n").encode("utf-8")) for fp, ls in chunks if ls], now)
+
+    def take(self, kind: str) -> List[str]:
+        return self.eng.take(kind)
+
+    def metrics(self) -> Dict[str, Any]:
+        m = self.eng.metrics()
+        m.update({"join": self.eng.join_counters(), "series": self.eng.n_series(),
+                  "device_bytes": self.eng.device_bytes()})
+        return m

@@ -120,6 +120,10 @@ def parse_int(s) -> float:
             return float("nan")
         s = js_str(s)
     s = str(s).lstrip(_WS)
+    hm = re.match(r"([+-]?)0[xX]([0-9a-fA-F]+)", s)
+    if hm:  # radix undefined + "0x" prefix -> hexadecimal
+        v = int(hm.group(2), 16) * (-1 if hm.group(1) == "-" else 1)
+        return v if abs(v) <= 2 ** 53 else float(v)
     m = _INT_RE.match(s)
     if not m:
         return float("nan")

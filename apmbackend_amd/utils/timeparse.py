@@ -155,7 +155,10 @@ def convert_string_date_to_ms(date_str: Optional[str], tz: Optional[TzOffset] = 
     nums = [js_number(get(i)) if get(i) is not None else NAN for i in range(7)]
     # new Date(y, m) with fewer args: missing args default (d=1, rest 0) -- but the reference
     # always passes 7 args, undefined -> NaN.
-    local = make_date_ms(nums[0], nums[1] - 1, nums[2], nums[3], nums[4], nums[5], nums[6])
+    y = nums[0]
+    if not math.isnan(y) and 0 <= math.trunc(y) <= 99:
+        y = 1900 + math.trunc(y)  # Date(y, m, ...) maps two-digit years to 19xx
+    local = make_date_ms(y, nums[1] - 1, nums[2], nums[3], nums[4], nums[5], nums[6])
     return (tz or default_tz()).local_to_utc(local)
 
 

@@ -1,0 +1,194 @@
+#!/usr/bin/env python3
+"""Headline benchmark: log-lines/sec z-scored (whole node) + p50 ingest->alert latency.
+
+BASELINE.json config 2/3: synthetic WildFly logs, 10k services (6k top-level EJB + 4k Provider
+sub-services), 8 JVM hosts per GPU ("one log shard"), the full reference chain
+parse -> join -> 10 s stats (31-bucket window, p75/p95) -> z-score at LAG 360 and 8640 (rings
+warmed with a synthetic pre-history so both lags produce bounds) -> alert decision, every step.
+
+One step = one ingest batch = 10 s of log time for every JVM of the shard (so every step
+contains one interval rollover).  The corpus is generated before the timed region into pinned
+host memory; the timed region covers H2D of the raw bytes, GPU parse, host join, GPU stats /
+z-score / alerts, and (N > 1) the RCCL all-reduce of the fleet-wide per-service baseline.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL over xGMI)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+REFERENCE_CPU_LINES_PER_S = None  # measured reference throughput (tools/measure_reference.py), if any
+
+
+def _load_reference_baseline():
+    p = os.path.join(ROOT, "profiles", "reference_cpu_baseline.json")
+    try:
+        with open(p) as fh:
+            return float(json.load(fh)["lines_per_sec"])
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--servers", type=int, default=8, help="JVM hosts per GPU (one log shard)")
+    ap.add_argument("--ejb", type=int, default=6000)
+    ap.add_argument("--providers", type=int, default=4000)
+    ap.add_argument("--tx-rate", type=float, default=250.0, help="log-time tx/s per JVM")
+    ap.add_argument("--batch-seconds", type=float, default=10.0)
+    ap.add_argument("--mean-mode", default="rolling", choices=["rolling", "exact"])
+    ap.add_argument("--ring", default="float64", choices=["float64", "float32"])
+    ap.add_argument("--gen-threads", type=int, default=16)
+    ap.add_argument("--no-warm", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from apmbackend_amd import _native
+    from apmbackend_amd.models.pipeline import APMEngine
+    from apmbackend_amd.parallel.fleet import FleetBaseline
+    from apmbackend_amd.utils.config import default_config
+
+    N = _native.load(build_if_missing=False)
+    n_services = args.ejb + args.providers
+    cfg = default_config()
+    cfg["gpu"].update({
+        "timezone": "UTC",
+        "maxSeries": max(4096, 1 << (args.servers * n_services - 1).bit_length()),
+        "batchBytes": 48 << 20,
+        "maxLinesPerBatch": 1 << 20,
+        "zscoreMeanMode": args.mean_mode,
+        "ringDtype": args.ring,
+        "bucketCellCapacity": 16,
+    })
+    eng = APMEngine(cfg, device=local, keep_text=False)
+    gen = N.SynthGen({"servers": args.servers, "ejb_services": args.ejb, "provider_services": args.providers,
+                      "tx_per_sec_per_server": args.tx_rate, "seed": 1 + rank,
+                      "server_offset": rank * args.servers})
+    for path, kind, server in gen.files():
+        eng.add_file(path, {0: "SOAP", 1: "SERVER", 2: "APP"}[kind], server)
+
+    # ---- corpus (untimed): warmup + steps batches of `batch_seconds` of log time, pinned
+    start = 1578391200000
+    step_ms = int(args.batch_seconds * 1000)
+    n_batches = args.warmup + args.steps + 2
+    batches = []
+    total = 0
+    raw = []
+    t_gen = time.time()
+    for b in range(n_batches):
+        data, chunks = gen.generate(start + (b + 1) * step_ms, args.gen_threads)
+        raw.append((data, chunks))
+        total += len(data) + 64
+    pinned = N.alloc_pinned(total)
+    off = 0
+    for data, chunks in raw:
+        N.memcpy_to(pinned, data, off)
+        batches.append((pinned + off, len(data), chunks))
+        off += len(data) + 64
+    del raw
+    t_gen = time.time() - t_gen
+
+    fleet = FleetBaseline(eng, world) if dist is not None else None
+
+    def step(i):
+        ptr, n, chunks = batches[i]
+        eng.eng.process_batch_ptr(ptr, n, chunks, -1.0)
+        if fleet is not None:
+            fleet.exchange()
+
+    # ---- warmup (first batches create the series; then the z-score rings get a pre-history)
+    for i in range(2):
+        step(i)
+    if not args.no_warm:
+        eng.eng.warm_history(12345 + rank)
+    for i in range(2, 2 + args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    m0 = eng.metrics()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(2 + args.warmup, 2 + args.warmup + args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    m1 = eng.metrics()
+    lines = m1["lines"] - m0["lines"]
+    lat = sorted(m1["rollover_latency_ms"][len(m0["rollover_latency_ms"]):]) or [float("nan")]
+    p50 = lat[len(lat) // 2]
+    stats = torch.tensor([float(lines), dt, p50, float(m1["tx"] - m0["tx"]),
+                          float(m1["bytes"] - m0["bytes"])], dtype=torch.float64, device="cuda")
+    if dist is not None:
+        summed = stats.clone()
+        dist.all_reduce(summed, op=dist.ReduceOp.SUM)
+        maxed = stats.clone()
+        dist.all_reduce(maxed, op=dist.ReduceOp.MAX)
+        lines_total, dt_max, p50_max = summed[0].item(), maxed[1].item(), maxed[2].item()
+        tx_total, bytes_total = summed[3].item(), summed[4].item()
+    else:
+        lines_total, dt_max, p50_max = lines, dt, p50
+        tx_total, bytes_total = float(m1["tx"] - m0["tx"]), float(m1["bytes"] - m0["bytes"])
+    value = lines_total / dt_max
+    ref = _load_reference_baseline()
+    if rank == 0:
+        out = {
+            "metric": "log-lines/sec z-scored (whole node)",
+            "value": round(value, 1),
+            "unit": "lines/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * dt_max / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (round(value / ref, 2) if ref else None),
+            "dtype": "fp64",
+            "data": "synthetic WildFly logs (native generator, seeded), random-init z-score pre-history",
+            "config": {
+                "model": f"apm-pipeline parse->join->stats->zscore(LAG 360,8640)->alerts, {n_services} services, "
+                         f"{args.servers} JVMs/GPU",
+                "global_batch": int(lines_total / args.steps),
+                "seq_len": 8640,
+                "parallelism": f"dp{world}",
+            },
+            "p50_ingest_to_alert_ms": round(p50_max, 3),
+            "tx_per_s": round(tx_total / dt_max, 1),
+            "ingest_GB_per_s": round(bytes_total / dt_max / 1e9, 3),
+            "series_per_gpu": eng.eng.n_series(),
+            "stage_ms_per_step": {k: round((m1[k] - m0[k]) / args.steps, 3)
+                                  for k in ("t_parse_ms", "t_join_ms", "t_stats_ms")},
+            "corpus_gen_s": round(t_gen, 2),
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    N.free_pinned(pinned)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,30 @@
+#!/bin/bash
+# GPU-box check used through gpurun: tests -> smoke -> bench -> optional rocprof.
+# Each GPU step has its own time limit; after a crash/abort/timeout nothing else touches the GPU.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+stop_on_fault() {  # $1 = rc, $2 = step name
+  case "$1" in
+    0|1) return 0 ;;
+    *) echo "GPU step $2 ended with rc=$1 -- stopping (no further GPU work)"; exit "$1" ;;
+  esac
+}
+STEPS="${STEPS:-tests smoke bench}"
+for s in $STEPS; do
+  case "$s" in
+    tests)
+      timeout -k 10 "${T_TESTS:-420}" python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} > gpurun_out/tests.log 2>&1
+      rc=$?; echo "tests rc=$rc"; tail -5 gpurun_out/tests.log; stop_on_fault $rc tests ;;
+    smoke)
+      timeout -k 10 "${T_SMOKE:-240}" python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+      rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log; stop_on_fault $rc smoke ;;
+    bench)
+      timeout -k 10 "${T_BENCH:-420}" python bench.py ${BENCH_ARGS:---steps 10 --warmup 3} > gpurun_out/bench.log 2>&1
+      rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.log; stop_on_fault $rc bench ;;
+    prof)
+      timeout -k 10 "${T_PROF:-420}" rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py ${PROF_ARGS:---steps 5 --warmup 2} > gpurun_out/prof.log 2>&1
+      rc=$?; echo "prof rc=$rc"; tail -3 gpurun_out/prof.log; stop_on_fault $rc prof ;;
+  esac
+done
