@@ -61,9 +61,9 @@ def _compile(src: str, is_hip: bool, force: bool, hmt: float) -> str:
     obj = _obj(src)
     if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hmt):
         return obj
-    cmd = [hipcc()] + COMMON + _includes()
+    cmd = [hipcc()] + COMMON + _includes() + [f"--offload-arch={ARCH}"]
     if is_hip:
-        cmd += [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
+        cmd += ["-munsafe-fp-atomics"]
     cmd += ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -83,7 +83,7 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = True) -> str:
     newest = max(os.path.getmtime(o) for o in objs)
     if force or not os.path.exists(TARGET) or os.path.getmtime(TARGET) < newest:
         cmd = [hipcc(), "-shared", f"--offload-arch={ARCH}", "-o", TARGET + ".tmp"] + objs + [
-            "-L" + os.path.join(ROCM, "lib"), "-lamdhip64", "-Wl,-rpath," + os.path.join(ROCM, "lib"),
+            "-L" + os.path.join(ROCM, "lib"), "-lamdhip64", "-lrccl", "-Wl,-rpath," + os.path.join(ROCM, "lib"),
             "-lpthread"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:

@@ -94,6 +94,7 @@ EngineConfig config_from(const py::dict& d) {
   c.join_threads = get<int>(d, "join_threads", c.join_threads);
   c.keep_text = get<int>(d, "keep_text", c.keep_text);
   c.keep_tx_records = get<int>(d, "keep_tx_records", c.keep_tx_records);
+  c.async_stats = get<int>(d, "async_stats", c.async_stats);
   return c;
 }
 
@@ -249,10 +250,15 @@ PYBIND11_MODULE(_apm_native, m) {
              e.process_batch((const uint8_t*)ptr, n, ch, now);
            },
            py::arg("ptr"), py::arg("n"), py::arg("chunks"), py::arg("now") = -1.0)
-      .def("take", &Engine::take)
+      .def("take", &Engine::take, py::call_guard<py::gil_scoped_release>())
+      .def("flush", &Engine::flush, py::call_guard<py::gil_scoped_release>())
       .def("last_events", [](Engine& e) { return py::bytes(e.last_events()); })
       .def("warm_history", &Engine::warm_history)
-      .def("metrics", [](Engine& e) { return metrics_dict(e.metrics()); })
+      .def("metrics", [](Engine& e) {
+        EngineMetrics m;
+        { py::gil_scoped_release rel; m = e.metrics(); }
+        return metrics_dict(m);
+      })
       .def("join_counters", [](Engine& e) { return counters_dict(e.join_counters()); })
       .def("n_series", &Engine::n_series)
       .def("n_services", &Engine::n_services)
@@ -262,6 +268,22 @@ PYBIND11_MODULE(_apm_native, m) {
       .def("device_bytes", &Engine::device_bytes)
       .def("stream_handle", [](Engine& e) { return (uintptr_t)e.stream(); })
       .def("comm_stream_handle", [](Engine& e) { return (uintptr_t)e.comm_stream(); })
+      .def_static("fleet_unique_id", []() {
+        auto v = Engine::fleet_unique_id();
+        return py::bytes((const char*)v.data(), v.size());
+      })
+      .def("fleet_init", [](Engine& e, py::bytes uid, int nranks, int rank, int32_t cap) {
+        std::string s = uid;
+        std::vector<uint8_t> v(s.begin(), s.end());
+        py::gil_scoped_release rel;
+        e.fleet_init(v, nranks, rank, cap);
+      })
+      .def("fleet_merged", [](Engine& e) {
+        std::vector<double> v;
+        { py::gil_scoped_release rel; v = e.fleet_merged(); }
+        return py::bytes((const char*)v.data(), v.size() * 8);
+      })
+      .def("fleet_rounds", &Engine::fleet_rounds)
       .def("pack_service_moments", [](Engine& e, uintptr_t dst, int32_t cap) {
         e.pack_service_moments((double*)dst, cap, e.comm_stream());
       })

@@ -83,6 +83,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipSetDevice(cfg_.device));
   HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   HIP_OK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
+  HIP_OK(hipStreamCreateWithFlags(&parse_stream_, hipStreamNonBlocking));
   HIP_OK(hipEventCreate(&ev_a_));
   HIP_OK(hipEventCreate(&ev_b_));
   const int32_t S = cfg_.max_series;
@@ -173,19 +174,33 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   for (int l = 0; l < MAX_LAGS; ++l) { alias_thr_[l] = cfg_.thr[l]; alias_infl_[l] = cfg_.infl[l]; }
   HIP_OK(hipStreamSynchronize(stream_));
   HIP_OK(hipDeviceSynchronize());
+  stats_thread_ = std::thread([this]() { hipSetDevice(cfg_.device); stats_worker(); });
 }
 
 Engine::~Engine() {
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_stop_ = true;
+  }
+  st_cv_.notify_all();
+  if (stats_thread_.joinable()) stats_thread_.join();
+  if (fleet_comm_) {
+    hipStreamSynchronize(comm_stream_);
+    ncclCommDestroy(fleet_comm_);
+    fleet_comm_ = nullptr;
+  }
   hipStreamSynchronize(stream_);
+  hipStreamSynchronize(parse_stream_);
   for (void* p : allocations_) hipFree(p);
   hipHostFree(h_bytes_); hipHostFree(h_chunk_begin_); hipHostFree(h_chunk_kind_); hipHostFree(h_chunk_file_);
   hipHostFree(h_events_); hipHostFree(h_counts_); hipHostFree(h_watermark_); hipHostFree(h_alerts_);
   hipHostFree(h_n_alerts_); hipHostFree(h_tx_); hipHostFree(h_gid_); hipHostFree(h_release_gid_);
   hipEventDestroy(ev_a_); hipEventDestroy(ev_b_);
-  hipStreamDestroy(stream_); hipStreamDestroy(comm_stream_);
+  hipStreamDestroy(stream_); hipStreamDestroy(comm_stream_); hipStreamDestroy(parse_stream_);
 }
 
 int32_t Engine::add_server(const std::string& name) {
+  flush();
   auto it = server_ids_.find(name);
   if (it != server_ids_.end()) return it->second;
   const int32_t id = (int32_t)servers_.size();
@@ -203,14 +218,21 @@ int32_t Engine::add_server(const std::string& name) {
 }
 
 int32_t Engine::add_file(const std::string& path, int kind, const std::string& server) {
+  flush();
   const int32_t sid = add_server(server);
   files_.push_back(FileInfo{path, sid, (uint8_t)kind});
   if (files_.size() > (1 << 16)) throw std::runtime_error("too many files");
   return (int32_t)files_.size() - 1;
 }
 
-void Engine::set_override(const std::string& service, const ServiceOverride& o) { overrides_[service] = o; }
-void Engine::clear_overrides() { overrides_.clear(); }
+void Engine::set_override(const std::string& service, const ServiceOverride& o) {
+  flush();
+  overrides_[service] = o;
+}
+void Engine::clear_overrides() {
+  flush();
+  overrides_.clear();
+}
 
 // ----------------------------------------------------------------------------- series
 void Engine::compute_series_settings(int32_t s, double* thr, double* infl, double& hard_max, uint8_t& suppressed) {
@@ -256,6 +278,7 @@ int32_t Engine::series_for(int32_t server, int32_t service) {
   h_suppressed_.push_back(0);
   zscore_seen_.push_back(0);
   h_active_.push_back(0);
+  unseen_.push_back(s);
   return s;
 }
 
@@ -272,34 +295,34 @@ void Engine::apply_series_settings(int32_t s) {
 }
 
 void Engine::refresh_series_settings() {
+  flush();
   // config hot reload (updateAllServiceSettings, stream_calc_z_score.js:152-167)
   for (int l = 0; l < MAX_LAGS; ++l) { alias_thr_[l] = cfg_.thr[l]; alias_infl_[l] = cfg_.infl[l]; }
   std::vector<int32_t> order(n_series_);
   for (int32_t i = 0; i < n_series_; ++i) order[i] = i;
   std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return series_[a].emit_key < series_[b].emit_key; });
   for (int32_t s : order) if (zscore_seen_[s]) apply_series_settings(s);
-  uploaded_series_ = 0;
-  upload_series_tables();
+  upload_series_tables(0);
 }
 
-void Engine::upload_series_tables() {
-  if (uploaded_series_ >= n_series_ && uploaded_series_ != 0) {
-    // thresholds may change for already-uploaded series (first st); upload everything dirty
-  }
+void Engine::upload_series_tables(int32_t lo) {
   const int32_t n = n_series_;
-  if (n == 0) return;
-  std::vector<double> col(n);
+  if (lo < 0) lo = 0;
+  if (n <= lo) return;
+  const size_t m = (size_t)(n - lo);
+  std::vector<double> col(m);
   for (int l = 0; l < cfg_.n_lags; ++l) {
-    for (int32_t s = 0; s < n; ++s) col[s] = h_thr_[(size_t)s * MAX_LAGS + l];
-    HIP_OK(hipMemcpyAsync(lag_[l].thr, col.data(), (size_t)n * 8, hipMemcpyHostToDevice, stream_));
-    for (int32_t s = 0; s < n; ++s) col[s] = h_infl_[(size_t)s * MAX_LAGS + l];
-    HIP_OK(hipMemcpyAsync(lag_[l].infl, col.data(), (size_t)n * 8, hipMemcpyHostToDevice, stream_));
+    for (size_t i = 0; i < m; ++i) col[i] = h_thr_[(size_t)(lo + i) * MAX_LAGS + l];
+    HIP_OK(hipMemcpyAsync(lag_[l].thr + lo, col.data(), m * 8, hipMemcpyHostToDevice, stream_));
+    HIP_OK(hipStreamSynchronize(stream_));  // `col` is pageable and reused
+    for (size_t i = 0; i < m; ++i) col[i] = h_infl_[(size_t)(lo + i) * MAX_LAGS + l];
+    HIP_OK(hipMemcpyAsync(lag_[l].infl + lo, col.data(), m * 8, hipMemcpyHostToDevice, stream_));
+    HIP_OK(hipStreamSynchronize(stream_));
   }
-  HIP_OK(hipMemcpyAsync(d_hard_max_, h_hard_max_.data(), (size_t)n * 8, hipMemcpyHostToDevice, stream_));
-  HIP_OK(hipMemcpyAsync(d_suppressed_, h_suppressed_.data(), (size_t)n, hipMemcpyHostToDevice, stream_));
-  HIP_OK(hipMemcpyAsync(d_emit_key_, h_emit_key_.data(), (size_t)n * 8, hipMemcpyHostToDevice, stream_));
-  HIP_OK(hipStreamSynchronize(stream_));  // `col` is pageable and reused
-  uploaded_series_ = n;
+  HIP_OK(hipMemcpyAsync(d_hard_max_ + lo, h_hard_max_.data() + lo, m * 8, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpyAsync(d_suppressed_ + lo, h_suppressed_.data() + lo, m, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpyAsync(d_emit_key_ + lo, h_emit_key_.data() + lo, m * 8, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
 }
 
 JoinCounters Engine::join_counters() const {
@@ -376,18 +399,18 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
   ++metrics_.batches;
 
   // ---- K1/K2 on the GPU
-  HIP_OK(hipMemcpyAsync(d_bytes_, hb, off, hipMemcpyHostToDevice, stream_));
-  HIP_OK(hipMemsetAsync(d_bytes_ + off, 0, 64, stream_));
-  HIP_OK(hipMemcpyAsync(d_chunk_begin_, h_chunk_begin_, (n_chunks + 1) * 4, hipMemcpyHostToDevice, stream_));
-  HIP_OK(hipMemcpyAsync(d_chunk_kind_, h_chunk_kind_, n_chunks + 1, hipMemcpyHostToDevice, stream_));
-  HIP_OK(hipMemcpyAsync(d_chunk_file_, h_chunk_file_, (n_chunks + 1) * 4, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpyAsync(d_bytes_, hb, off, hipMemcpyHostToDevice, parse_stream_));
+  HIP_OK(hipMemsetAsync(d_bytes_ + off, 0, 64, parse_stream_));
+  HIP_OK(hipMemcpyAsync(d_chunk_begin_, h_chunk_begin_, (n_chunks + 1) * 4, hipMemcpyHostToDevice, parse_stream_));
+  HIP_OK(hipMemcpyAsync(d_chunk_kind_, h_chunk_kind_, n_chunks + 1, hipMemcpyHostToDevice, parse_stream_));
+  HIP_OK(hipMemcpyAsync(d_chunk_file_, h_chunk_file_, (n_chunks + 1) * 4, hipMemcpyHostToDevice, parse_stream_));
   if (apm_parse_batch(d_bytes_, off, d_chunk_begin_, d_chunk_kind_, d_chunk_file_, n_chunks, d_parse_ws_,
                       cfg_.max_lines, d_events_, d_counts_, d_counts_ + 1, d_watermark_, d_file_open_, &cfg_.tz,
-                      stream_) != 0)
+                      parse_stream_) != 0)
     throw std::runtime_error("parse workspace too small");
-  HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, 8, hipMemcpyDeviceToHost, stream_));
-  HIP_OK(hipMemcpyAsync(h_watermark_, d_watermark_, 8, hipMemcpyDeviceToHost, stream_));
-  HIP_OK(hipStreamSynchronize(stream_));
+  HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, 8, hipMemcpyDeviceToHost, parse_stream_));
+  HIP_OK(hipMemcpyAsync(h_watermark_, d_watermark_, 8, hipMemcpyDeviceToHost, parse_stream_));
+  HIP_OK(hipStreamSynchronize(parse_stream_));
   const uint32_t n_events = h_counts_[0];
   last_n_events_ = n_events;
   const uint32_t n_lines = h_counts_[1];
@@ -395,8 +418,8 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
   metrics_.lines += n_lines;
   metrics_.events += n_events;
   if (n_events) {
-    HIP_OK(hipMemcpyAsync(h_events_, d_events_, (size_t)n_events * sizeof(Event), hipMemcpyDeviceToHost, stream_));
-    HIP_OK(hipStreamSynchronize(stream_));
+    HIP_OK(hipMemcpyAsync(h_events_, d_events_, (size_t)n_events * sizeof(Event), hipMemcpyDeviceToHost, parse_stream_));
+    HIP_OK(hipStreamSynchronize(parse_stream_));
   }
   const double t1 = now_ms();
   metrics_.t_parse_ms += t1 - t0;
@@ -444,11 +467,10 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
   const double t2 = now_ms();
   metrics_.t_join_ms += t2 - t1;
 
-  // ---- stats / z-score / alerts on the GPU
-  stats_for_batch(txs, t0);
-  const double t3 = now_ms();
-  metrics_.t_stats_ms += t3 - t2;
-  metrics_.t_total_ms += t3 - t0;
+  // ---- stats / z-score / alerts: handed to the stats thread, overlapping the next batch's
+  // H2D + parse (parse stream) and host join (pool) with this batch's GPU stats work.
+  post_stats(std::move(txs), t0);
+  metrics_.t_total_ms += now_ms() - t0;
 
   // advance the watermark clock (max leading timestamp seen so far)
   const unsigned long long wm = *h_watermark_;
@@ -457,6 +479,52 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
     if (w > watermark_) watermark_ = w;
   }
   ++batch_no_;
+}
+
+void Engine::stats_worker() {
+  for (;;) {
+    StatsJob job;
+    {
+      std::unique_lock<std::mutex> lk(st_mu_);
+      st_cv_.wait(lk, [&]() { return st_stop_ || st_has_job_; });
+      if (st_stop_ && !st_has_job_) return;
+      job = std::move(st_job_);
+      st_has_job_ = false;
+    }
+    const double t = now_ms();
+    try {
+      stats_for_batch(job.txs, job.t0);
+      fleet_exchange_locked();
+    } catch (const std::exception& e) {
+      std::lock_guard<std::mutex> g(st_mu_);
+      st_error_ = e.what();
+    }
+    {
+      std::lock_guard<std::mutex> g(st_mu_);
+      metrics_.t_stats_ms += now_ms() - t;
+      st_busy_ = false;
+    }
+    st_cv_.notify_all();
+  }
+}
+
+void Engine::post_stats(std::vector<TxOut>&& txs, double t0) {
+  std::unique_lock<std::mutex> lk(st_mu_);
+  st_cv_.wait(lk, [&]() { return !st_busy_; });
+  if (!st_error_.empty()) { std::string e = st_error_; st_error_.clear(); throw std::runtime_error(e); }
+  st_job_.txs = std::move(txs);
+  st_job_.t0 = t0;
+  st_has_job_ = true;
+  st_busy_ = true;
+  lk.unlock();
+  st_cv_.notify_all();
+  if (!cfg_.async_stats) flush();
+}
+
+void Engine::flush() {
+  std::unique_lock<std::mutex> lk(st_mu_);
+  st_cv_.wait(lk, [&]() { return !st_busy_; });
+  if (!st_error_.empty()) { std::string e = st_error_; st_error_.clear(); throw std::runtime_error(e); }
 }
 
 void Engine::ensure_bucket_slot(int64_t b) {
@@ -476,6 +544,7 @@ void Engine::stats_for_batch(std::vector<TxOut>& txs, double batch_t0) {
   // split: audit non-Provider records go straight to db_insert (Q18)
   std::vector<std::pair<uint32_t, int64_t>> triggers;  // (index in upload, new latest)
   uint32_t n = 0;
+  int64_t agg_b = INT64_MIN, agg_n = 0, agg_e = 0;
   for (uint32_t i = 0; i < txs.size(); ++i) {
     TxOut& t = txs[i];
     ++metrics_.tx;
@@ -502,9 +571,14 @@ void Engine::stats_for_batch(std::vector<TxOut>& txs, double batch_t0) {
     const int64_t gid = next_gid_++;
     h_gid_[n] = gid;
     if (cfg_.keep_tx_records || keep) tx_records_.emplace(gid, t);
-    pool_bucket_count_[b] += 1;
-    if (end == b * 10000) pool_exact_edge_[b] += 1;
+    if (b != agg_b) { if (agg_n) { pool_bucket_count_[agg_b] += agg_n; pool_exact_edge_[agg_b] += agg_e; } agg_b = b; agg_n = agg_e = 0; }
+    ++agg_n;
+    if (end == b * 10000) ++agg_e;
     ++n;
+  }
+  if (agg_n) { pool_bucket_count_[agg_b] += agg_n; pool_exact_edge_[agg_b] += agg_e; }
+  for (auto it = pool_exact_edge_.begin(); it != pool_exact_edge_.end();) {
+    if (it->second == 0) it = pool_exact_edge_.erase(it); else ++it;
   }
   if (n == 0) return;
   HIP_OK(hipMemcpyAsync(d_tx_, h_tx_, (size_t)n * sizeof(TxRec), hipMemcpyHostToDevice, stream_));
@@ -603,20 +677,21 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   // ---- first st for newly visible series: resolve their z-score settings in emission order
   {
     std::vector<int32_t> fresh;
-    for (int32_t s = 0; s < n_series_; ++s) if (!zscore_seen_[s]) fresh.push_back(s);
+    std::vector<int32_t> still;
+    for (int32_t s : unseen_) { if (h_active_[s]) fresh.push_back(s); else still.push_back(s); }
+    unseen_.swap(still);
     // a series is visible iff it had a tx before this rollover: all created series qualify except
     // those whose first tx is the trigger or later -- the device `active` flag is authoritative;
     // settings for not-yet-active series are computed now and harmlessly recomputed later.
     std::sort(fresh.begin(), fresh.end(), [&](int32_t a, int32_t b) { return series_[a].emit_key < series_[b].emit_key; });
     if (!fresh.empty()) {
-      bool dirty = false;
+      int32_t lo = INT32_MAX;
       for (int32_t s : fresh) {
-        if (!h_active_[s]) continue;
         zscore_seen_[s] = 1;
         apply_series_settings(s);
-        dirty = true;
+        lo = std::min(lo, s);
       }
-      if (dirty) upload_series_tables();
+      upload_series_tables(lo);
     }
   }
   // ---- K8 window statistics over buckets [L-36, L-6]
@@ -737,12 +812,14 @@ void Engine::download_zout(int l, std::vector<ZOut>& out) {
 }
 
 std::vector<std::string> Engine::take(const std::string& kind) {
+  flush();
   std::vector<std::string> r;
   r.swap(text_[kind]);
   return r;
 }
 
 void Engine::warm_history(uint64_t seed) {
+  flush();
   // Use the latest window stats as the per-series baseline; fill every lag ring completely.
   for (int l = 0; l < cfg_.n_lags; ++l) {
     LagState& LS = lag_[l];
@@ -763,12 +840,13 @@ uintptr_t Engine::alloc_pinned(size_t n) {
 
 void Engine::free_pinned(uintptr_t p) { hipHostFree((void*)p); }
 
-void Engine::pack_service_moments(double* d_dst, int32_t cap, hipStream_t stream) {
-  // series -> service table (grows with the dictionary)
+void Engine::pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream) {
+  // series -> service table (grows with the dictionary): upload only the new tail
   if (series_service_uploaded_ < n_series_) {
-    std::vector<int32_t> sv(n_series_);
-    for (int32_t s = 0; s < n_series_; ++s) sv[s] = series_[s].service;
-    HIP_OK(hipMemcpyAsync(d_series_service_, sv.data(), (size_t)n_series_ * 4, hipMemcpyHostToDevice, stream_));
+    const int32_t lo = series_service_uploaded_;
+    std::vector<int32_t> sv(n_series_ - lo);
+    for (int32_t s = lo; s < n_series_; ++s) sv[s - lo] = series_[s].service;
+    HIP_OK(hipMemcpyAsync(d_series_service_ + lo, sv.data(), sv.size() * 4, hipMemcpyHostToDevice, stream_));
     HIP_OK(hipStreamSynchronize(stream_));
     series_service_uploaded_ = n_series_;
   }
@@ -778,6 +856,64 @@ void Engine::pack_service_moments(double* d_dst, int32_t cap, hipStream_t stream
   apm_service_moments(d_series_service_, d_active_, n_series_, cfg_.max_series, cfg_.n_lags, cap,
                       (const double* const*)d_lag_sum_ptrs_, (const double* const*)d_lag_comp_ptrs_,
                       (const int32_t* const*)d_lag_cnt_ptrs_, d_dst, stream);
+}
+
+void Engine::pack_service_moments(double* d_dst, int32_t cap, hipStream_t stream) {
+  flush();  // series tables are owned by the stats thread
+  pack_moments_locked(d_dst, cap, stream);
+}
+
+// ---- native fleet exchange over RCCL -------------------------------------------------------
+// One all-reduce(SUM) per processed batch, issued by the stats thread on the comm stream right
+// after the batch's z-score work: it never blocks the host pipeline and overlaps the next
+// batch's parse + join.  Every rank processes the same number of batches (lock-step ingest), so
+// the collective sequence matches across ranks.  Two device slots: the exchange of batch i
+// lands in slot i%2 and `fleet_merged` reads the newest completed one.
+std::vector<uint8_t> Engine::fleet_unique_id() {
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) throw std::runtime_error("ncclGetUniqueId failed");
+  return std::vector<uint8_t>((uint8_t*)&id, (uint8_t*)&id + sizeof(id));
+}
+
+void Engine::fleet_init(const std::vector<uint8_t>& uid, int nranks, int rank, int32_t cap) {
+  flush();
+  if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("bad unique id size");
+  ncclUniqueId id;
+  std::memcpy(&id, uid.data(), sizeof(id));
+  HIP_OK(hipSetDevice(cfg_.device));
+  if (ncclCommInitRank(&fleet_comm_, nranks, id, rank) != ncclSuccess)
+    throw std::runtime_error("ncclCommInitRank failed");
+  fleet_cap_ = cap;
+  fleet_elems_ = (size_t)cap * cfg_.n_lags * NSTAT * 3;
+  for (int i = 0; i < 2; ++i) {
+    fleet_buf_[i] = (double*)dmalloc(fleet_elems_ * 8);
+    HIP_OK(hipMemset(fleet_buf_[i], 0, fleet_elems_ * 8));
+    HIP_OK(hipEventCreateWithFlags(&fleet_ev_[i], hipEventDisableTiming));
+  }
+  fleet_rounds_ = 0;
+}
+
+void Engine::fleet_exchange_locked() {
+  if (!fleet_comm_) return;
+  const int slot = (int)(fleet_rounds_ & 1);
+  // comm stream order: previous collective on this slot completed before we overwrite it
+  pack_moments_locked(fleet_buf_[slot], fleet_cap_, comm_stream_);
+  if (ncclAllReduce(fleet_buf_[slot], fleet_buf_[slot], fleet_elems_, ncclDouble, ncclSum, fleet_comm_,
+                    comm_stream_) != ncclSuccess)
+    throw std::runtime_error("ncclAllReduce failed");
+  HIP_OK(hipEventRecord(fleet_ev_[slot], comm_stream_));
+  ++fleet_rounds_;
+}
+
+std::vector<double> Engine::fleet_merged() {
+  flush();
+  std::vector<double> out;
+  if (!fleet_comm_ || fleet_rounds_ == 0) return out;
+  const int slot = (int)((fleet_rounds_ - 1) & 1);
+  HIP_OK(hipEventSynchronize(fleet_ev_[slot]));
+  out.resize(fleet_elems_);
+  HIP_OK(hipMemcpy(out.data(), fleet_buf_[slot], fleet_elems_ * 8, hipMemcpyDeviceToHost));
+  return out;
 }
 
 }  // namespace apm

@@ -10,6 +10,7 @@
 // stream_process_alerts -> stream_insert_db) with the RabbitMQ hops replaced by device buffers.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <atomic>
 #include <condition_variable>
@@ -79,6 +80,7 @@ struct EngineConfig {
   // outputs
   int keep_text = 0;        // format tx/st/fs/al lines for sinks/tests
   int keep_tx_records = 0;  // keep full tx for the db release stream
+  int async_stats = 1;      // overlap batch i's stats with batch i+1's parse + join
 };
 
 struct Chunk {
@@ -136,8 +138,15 @@ class Engine {
   // layout [n_services][n_lags][NSTAT][3] = count, sum, sumsq of the current ring means).
   int32_t n_services() const { return dict_.n_services(); }
   void pack_service_moments(double* d_dst, int32_t n_services_cap, hipStream_t stream);
+  // Native RCCL fleet exchange (see engine.cpp): rank 0 creates the id, every rank inits.
+  static std::vector<uint8_t> fleet_unique_id();
+  void fleet_init(const std::vector<uint8_t>& uid, int nranks, int rank, int32_t n_services_cap);
+  std::vector<double> fleet_merged();  // [cap][n_lags][NSTAT][3] of the newest exchange
+  uint64_t fleet_rounds() const { return fleet_rounds_; }
 
-  EngineMetrics metrics() const { return metrics_; }
+  // Wait for the in-flight stats stage (process_batch returns while it still runs).
+  void flush();
+  EngineMetrics metrics() { flush(); return metrics_; }
   const std::vector<std::string>& servers() const { return servers_; }
   std::vector<std::string> services() const { return dict_.services_snapshot(); }
   int32_t n_series() const { return n_series_; }
@@ -167,11 +176,30 @@ class Engine {
   void do_rollover(int64_t L, double batch_t0);
   void flush_alerts(int64_t edge_ts);
   void format_rollover_text(int64_t edge_ts);
-  void upload_series_tables();
+  void upload_series_tables(int32_t lo);
+  void pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream);
+  void fleet_exchange_locked();
+  void stats_worker();
+  void post_stats(std::vector<TxOut>&& txs, double t0);
   void* dmalloc(size_t bytes);
 
   EngineConfig cfg_;
-  hipStream_t stream_ = nullptr, comm_stream_ = nullptr;
+  hipStream_t stream_ = nullptr, comm_stream_ = nullptr, parse_stream_ = nullptr;
+  // fleet exchange
+  ncclComm_t fleet_comm_ = nullptr;
+  int32_t fleet_cap_ = 0;
+  size_t fleet_elems_ = 0;
+  double* fleet_buf_[2] = {nullptr, nullptr};
+  hipEvent_t fleet_ev_[2] = {nullptr, nullptr};
+  uint64_t fleet_rounds_ = 0;
+  // stats thread
+  struct StatsJob { std::vector<TxOut> txs; double t0 = 0; };
+  std::thread stats_thread_;
+  std::mutex st_mu_;
+  std::condition_variable st_cv_;
+  StatsJob st_job_;
+  bool st_has_job_ = false, st_busy_ = false, st_stop_ = false;
+  std::string st_error_;
   size_t device_bytes_ = 0;
   std::vector<void*> allocations_;
 
@@ -195,9 +223,9 @@ class Engine {
   std::vector<double> h_thr_, h_infl_, h_hard_max_;
   std::vector<uint8_t> h_suppressed_;
   std::vector<uint64_t> h_emit_key_;
-  int32_t uploaded_series_ = 0;
   std::vector<int32_t> zscore_seen_;            // series already initialised in the z-score stage
   std::vector<uint8_t> h_active_;               // host mirror of the stats `active` flag
+  std::vector<int32_t> unseen_;                 // series not yet initialised in the z-score stage
 
   // parse buffers
   uint8_t* d_bytes_ = nullptr;

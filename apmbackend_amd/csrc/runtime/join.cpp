@@ -1,6 +1,6 @@
-// Host join workers -- see join.h for the contract.  Each handler below cites the reference
-// lines whose behaviour it reproduces; tests/test_engine_parity.py checks the produced tx
-// stream byte-for-byte against the oracle (which itself is checked against the reference JS).
+// Host join workers -- see join.h for the contract.  Each handler cites the reference lines
+// whose behaviour it reproduces; tests/test_join_native.py checks the produced tx stream
+// byte-for-byte against the oracle (itself checked against the reference JS).
 #include "join.h"
 
 #include <algorithm>
@@ -10,17 +10,7 @@ namespace apm {
 
 namespace {
 
-std::string_view tok_or_undef(const std::vector<std::string_view>& t, size_t i) {
-  return i < t.size() ? t[i] : std::string_view("undefined");
-}
-bool has_tok(const std::vector<std::string_view>& t, size_t i) { return i < t.size(); }
-
-std::string strip_brackets(std::string_view s) {  // .replace(/[[\]]/g, '')
-  std::string r;
-  r.reserve(s.size());
-  for (char c : s) if (c != '[' && c != ']') r.push_back(c);
-  return r;
-}
+constexpr std::string_view kUndef("undefined");
 
 bool all_digits(std::string_view s) {
   if (s.empty()) return false;
@@ -37,6 +27,20 @@ bool icontains(std::string_view hay, std::string_view needle) {
     if (k == needle.size()) return true;
   }
   return false;
+}
+
+// .replace(/[[\]]/g, '') -- returns a view when there is nothing to strip except the common
+// "[x]" wrapper, else copies into `scratch`.
+std::string_view strip_brackets(std::string_view s, std::string& scratch) {
+  size_t a = 0, b = s.size();
+  if (a < b && s[a] == '[') ++a;
+  if (b > a && s[b - 1] == ']') --b;
+  bool inner = false;
+  for (size_t i = a; i < b; ++i) inner |= (s[i] == '[' || s[i] == ']');
+  if (!inner) return s.substr(a, b - a);
+  scratch.clear();
+  for (char c : s) if (c != '[' && c != ']') scratch.push_back(c);
+  return scratch;
 }
 
 // service.replace(/Provider\[/i, 'Provider:').replace(']', '')
@@ -102,15 +106,47 @@ bool baf_match(std::string_view line) {  // /\[[^ ]+] +INFO /
   return false;
 }
 
+// Token views for one event: GPU-provided offsets on the fast path, a JS-exact re-split when
+// the kernel deferred the line to the host (PM_HOST: non-ASCII whitespace, exotic numbers).
+struct Toks {
+  std::string_view t[16];
+  int n = 0;
+  void from_event(const Event& e, std::string_view line) {
+    n = e.ntok;
+    const uint16_t* se = &e.t0s;
+    for (int k = 0; k < 4 && k < n; ++k) t[k] = line.substr(se[2 * k], se[2 * k + 1] - se[2 * k]);
+  }
+  void from_line(std::string_view line) {
+    auto v = js::split_ws(line, 16);
+    n = (int)v.size();
+    for (int k = 0; k < n && k < 16; ++k) t[k] = v[k];
+  }
+  bool has(int i) const { return i < n; }
+  std::string_view get(int i) const { return i < n ? t[i] : kUndef; }
+};
+
 }  // namespace
 
 int32_t Dictionary::service_id(std::string_view normalized) {
   std::lock_guard<std::mutex> g(mu_);
-  auto it = svc_map_.find(std::string(normalized));
+  std::string key(normalized);
+  auto it = svc_map_.find(key);
   if (it != svc_map_.end()) return it->second;
   int32_t id = (int32_t)services_.size();
-  services_.emplace_back(normalized);
-  svc_map_.emplace(services_.back(), id);
+  services_.push_back(key);
+  svc_map_.emplace(std::move(key), id);
+  return id;
+}
+
+int32_t JoinShard::raw_service(std::string_view raw) {
+  const uint64_t h = key_of(raw);
+  auto it = raw_svc_map_.find(h);
+  if (it != raw_svc_map_.end() && raw_svc_[it->second].raw == raw) return it->second;
+  const std::string norm = normalize_service(raw);
+  RawService r{std::string(raw), dict_->service_id(norm), norm.size() >= 2 && norm[0] == 'S' && norm[1] == ':'};
+  raw_svc_.push_back(std::move(r));
+  const int32_t id = (int32_t)raw_svc_.size() - 1;
+  if (it == raw_svc_map_.end()) raw_svc_map_.emplace(h, id);
   return id;
 }
 
@@ -122,58 +158,76 @@ void JoinShard::begin_batch(double now_ms, uint64_t batch_no) {
   sweep();
 }
 
-JoinShard::NeedMap& JoinShard::need_map(const std::string& log_id) {
-  auto nit = need_.find(log_id);
-  if (nit == need_.end()) {
-    nit = need_.emplace(log_id, TtlEntry<NeedMap>{NeedMap{}, now_ + cfg_.need_ttl_ms}).first;
-    nit->second.v.created = (batch_no_ << 28) | (cur_line_ & 0xfffffff);
-    need_order_.emplace_back(log_id, nit->second.exp);
+JoinShard::NeedEntry& JoinShard::need_map(uint64_t key, std::string_view log_id) {
+  auto it = need_.find(key);
+  if (it == need_.end()) {
+    NeedEntry ne;
+    ne.exp = now_ + cfg_.need_ttl_ms;
+    ne.created = (batch_no_ << 28) | (cur_line_ & 0xfffffff);
+    ne.log_id.assign(log_id);
+    it = need_.emplace(key, std::move(ne)).first;
+    need_fifo_.emplace_back(key, it->second.exp);
   }
-  return nit->second.v;
+  return it->second;
+}
+
+JoinShard::RecordEntry& JoinShard::record_map(uint64_t key) {
+  auto it = record_.find(key);
+  if (it == record_.end()) {
+    it = record_.emplace(key, RecordEntry{now_ + cfg_.record_ttl_ms, {}}).first;
+    record_fifo_.emplace_back(key, it->second.exp);
+  }
+  return it->second;
 }
 
 void JoinShard::sweep() {
   // recordCache: expired partial maps are discarded (error log in the reference, :220-224)
-  for (auto it = record_.begin(); it != record_.end();) {
-    if (it->second.exp < now_) { counters.expired_partials += it->second.v.items.size(); it = record_.erase(it); }
-    else ++it;
+  while (!record_fifo_.empty() && record_fifo_.front().second < now_) {
+    auto k = record_fifo_.front();
+    record_fifo_.pop_front();
+    auto it = record_.find(k.first);
+    if (it == record_.end() || it->second.exp != k.second) continue;
+    counters.expired_partials += it->second.items.size();
+    record_.erase(it);
   }
   // needNumRecordCache: expiry emits every parked record with altAcctNum or '' (:226-239).
-  // Creation order == expiry order (the clock never goes back), so a FIFO gives NodeCache's
+  // Creation order == expiry order (the clock never goes back): the FIFO is NodeCache's
   // insertion-ordered sweep.
-  while (!need_order_.empty() && need_order_.front().second < now_) {
-    auto key = need_order_.front();
-    need_order_.pop_front();
-    auto it = need_.find(key.first);
-    if (it == need_.end() || it->second.exp != key.second) continue;
-    NeedMap nm = std::move(it->second.v);
+  while (!need_fifo_.empty() && need_fifo_.front().second < now_) {
+    auto k = need_fifo_.front();
+    need_fifo_.pop_front();
+    auto it = need_.find(k.first);
+    if (it == need_.end() || it->second.exp != k.second) continue;
+    NeedEntry ne = std::move(it->second);
     need_.erase(it);
-    expire_need(key.first, nm);
+    expire_need(ne);
   }
-  for (auto it = acct_.begin(); it != acct_.end();) {
-    if (it->second.exp < now_) it = acct_.erase(it); else ++it;
+  while (!acct_fifo_.empty() && acct_fifo_.front().second < now_) {
+    auto k = acct_fifo_.front();
+    acct_fifo_.pop_front();
+    auto it = acct_.find(k.first);
+    if (it != acct_.end() && it->second.exp == k.second) acct_.erase(it);
   }
 }
 
-void JoinShard::expire_need(const std::string& log_id, NeedMap& nm) {
+void JoinShard::expire_need(NeedEntry& nm) {
   sub_ = 0;
   for (auto& r : nm.items) {
     ++counters.need_expired;
-    const double acct = r.alt_acct.empty() ? js::nan() : js::parse_int(r.alt_acct);
-    output(r.server, r.service_raw, log_id, acct, r.start_ms, r.start_empty, r.end_ms, r.end_empty, r.elapsed,
+    output(r.server, r.svc, nm.log_id, r.alt_acct, r.start_ms, r.start_empty, r.end_ms, r.end_empty, r.elapsed,
            r.insert_to_db, nm.created);
   }
 }
 
 // outputRecord (:264-290)
-void JoinShard::output(int32_t server, std::string_view service_raw, std::string_view log_id, double acct,
-                       double start_ms, bool start_empty, double end_ms, bool end_empty, double elapsed,
-                       bool to_db, uint64_t seq) {
-  TxOut t;
+void JoinShard::output(int32_t server, int32_t svc, std::string_view log_id, double acct, double start_ms,
+                       bool start_empty, double end_ms, bool end_empty, double elapsed, bool to_db, uint64_t seq) {
+  out_.emplace_back();
+  TxOut& t = out_.back();
   t.seq = (seq << 12) | (sub_++ & 0xfff);
   t.server = server;
-  const std::string svc = normalize_service(service_raw);
-  t.service = dict_->service_id(svc);
+  const RawService& rs = raw_svc_[svc];
+  t.service = rs.norm_id;
   t.log_id.assign(log_id);
   t.acct = acct;
   double s = start_empty ? js::nan() : start_ms;
@@ -184,10 +238,9 @@ void JoinShard::output(int32_t server, std::string_view service_raw, std::string
   t.end_ms = end_empty ? js::nan() : (std::isfinite(end_ms) ? std::trunc(end_ms) : js::nan());
   t.elapsed = elapsed;
   t.to_db = to_db;
-  t.toplevel = svc.size() >= 2 && svc[0] == 'S' && svc[1] == ':';
+  t.toplevel = rs.toplevel;
   ++counters.tx;
   if (to_db) ++counters.tx_db;
-  out_.push_back(std::move(t));
 }
 
 // saveAcctNum (:294-327). source: 0 standard, 1 riskStrategy, 2 bafmetainfo.
@@ -198,41 +251,45 @@ void JoinShard::save_acct(std::string_view acct_raw, int32_t file, int source, s
     ++counters.invalid_acct;  // reference logs (and throws via the $currLogFp typo, Q16: fixed)
     return;
   }
-  std::string log_id;
+  std::string log_id_buf;
+  std::string_view log_id;
   if (source == 2) {
     if (alt_log_id.empty()) return;
-    log_id.assign(alt_log_id);
+    log_id = alt_log_id;
   } else {
     auto it = soap_.find(file);
-    log_id = (it != soap_.end() && it->second.has_log_id) ? it->second.log_id : std::string("undefined");
+    if (it != soap_.end() && it->second.has_log_id) { log_id_buf = it->second.log_id; log_id = log_id_buf; }
+    else log_id = kUndef;
   }
-  auto& ae = acct_[log_id];
-  ae.v.assign(acct);
+  const uint64_t key = key_of(log_id);
+  const double a = js::parse_int(acct);
+  auto& ae = acct_[key];
+  ae.acct = a;
   ae.exp = now_ + cfg_.acct_ttl_ms;
+  acct_fifo_.emplace_back(key, ae.exp);
   if (source != 2) soap_.erase(file);
-  auto nit = need_.find(log_id);
-  if (nit != need_.end()) {
-    const double a = js::parse_int(acct);
+  auto nit = need_.find(key);
+  if (nit != need_.end() && !nit->second.items.empty()) {
     const int32_t server = (*files_)[file].server;
-    for (auto& r : nit->second.v.items)
-      output(server, r.service_raw, log_id, a, r.start_ms, r.start_empty, r.end_ms, r.end_empty, r.elapsed, false,
-             seq);
-    nit->second.v.items.clear();
+    std::vector<Need> items;
+    items.swap(nit->second.items);  // the (now empty) map stays until it expires
+    for (auto& r : items)
+      output(server, r.svc, log_id, a, r.start_ms, r.start_empty, r.end_ms, r.end_empty, r.elapsed, false, seq);
   }
 }
 
 // attemptReadAccountNumberFromBAFInfo (:486-497)
-std::string JoinShard::baf_acct(std::string_view line, const std::vector<std::string_view>& toks, int32_t file,
-                                std::string_view log_id, uint64_t seq) {
-  if (!baf_match(line)) return std::string();
-  std::string_view t3 = has_tok(toks, 3) ? toks[3] : std::string_view();
+std::string_view JoinShard::baf_acct(std::string_view line, std::string_view t3, int32_t file,
+                                     std::string_view log_id, uint64_t seq, std::string& scratch) {
+  if (!baf_match(line)) return std::string_view();
   // .replace(/.*]\[/,'') -> drop through the last "]["
   size_t p = std::string_view::npos;
   for (size_t i = 0; i + 1 < t3.size(); ++i) if (t3[i] == ']' && t3[i + 1] == '[') p = i;
   if (p != std::string_view::npos) t3 = t3.substr(p + 2);
-  std::string s = strip_brackets(t3);
-  size_t c = s.rfind(':');
-  std::string acct = c == std::string::npos ? s : s.substr(c + 1);
+  scratch.clear();
+  for (char c : t3) if (c != '[' && c != ']') scratch.push_back(c);
+  size_t c = scratch.rfind(':');
+  std::string_view acct = c == std::string::npos ? std::string_view(scratch) : std::string_view(scratch).substr(c + 1);
   if (!acct.empty()) save_acct(acct, file, 2, log_id, seq);
   return acct;
 }
@@ -242,10 +299,11 @@ std::string JoinShard::baf_acct(std::string_view line, const std::vector<std::st
 void JoinShard::on_soap(const Event& e, std::string_view line, int32_t file, uint64_t seq) {
   const uint32_t m = e.mask;
   if (m & PM_SOAP_IN) {
-    auto toks = js::split_ws(line, 4);
+    Toks tk;
+    if (e.mask & PM_HOST) tk.from_line(line); else tk.from_event(e, line);
     SoapCtx c;
-    if (has_tok(toks, 1)) {
-      std::string_view t1 = toks[1];
+    if (tk.has(1)) {
+      std::string_view t1 = tk.t[1];
       size_t eq = t1.find('=');
       if (eq != std::string_view::npos) {
         size_t eq2 = t1.find('=', eq + 1);
@@ -253,7 +311,7 @@ void JoinShard::on_soap(const Event& e, std::string_view line, int32_t file, uin
         c.has_log_id = true;
       }
     }
-    soap_[file] = c;
+    soap_[file] = std::move(c);
   } else if (m & PM_SOAP_OUT) {
     soap_.erase(file);
   } else {
@@ -271,141 +329,150 @@ void JoinShard::on_soap(const Event& e, std::string_view line, int32_t file, uin
 
 void JoinShard::on_ejb(const Event& e, std::string_view line, int32_t file, bool entry, uint64_t seq) {
   const int32_t server = (*files_)[file].server;
-  auto toks = js::split_ws(line, 16);
-  const std::string log_id = strip_brackets(toks[0]);
+  const bool host = e.mask & PM_HOST;
+  Toks tk;
+  std::vector<std::string_view> all;
+  if (host) { all = js::split_ws(line, 16); tk.n = (int)all.size(); for (int k = 0; k < tk.n && k < 16; ++k) tk.t[k] = all[k]; }
+  else tk.from_event(e, line);
+  std::string scratch;
+  const std::string_view log_id = strip_brackets(tk.t[0], scratch);
   double ts;
   bool ts_empty = false;
-  if (!(e.mask & PM_HOST) && has_tok(toks, 2)) {
+  if (!host && tk.has(2)) {
     ts = e.ts;
   } else {
-    std::string tsstr = std::string(tok_or_undef(toks, 1)) + " " + std::string(tok_or_undef(toks, 2));
+    std::string tsstr = std::string(tk.get(1)) + " " + std::string(tk.get(2));
     if (!js::convert_date(tsstr, cfg_.tz, ts)) { ts_empty = true; ts = js::nan(); }
   }
+  std::string svc_buf = "S:";
   if (entry) {  // parseEjbCommonTimingEntry (:378-401)
     if (log_id.empty()) return;
-    std::string service = "S:" + std::string(tok_or_undef(toks, 13));
-    auto it = record_.find(log_id);
-    if (it == record_.end()) {
-      it = record_.emplace(log_id, TtlEntry<RecordMap>{RecordMap{}, now_ + cfg_.record_ttl_ms}).first;
-    }
-    auto& items = it->second.v.items;
-    auto f = std::find_if(items.begin(), items.end(), [&](const Partial& p) { return p.service_raw == service; });
+    if (host) svc_buf += std::string(tk.get(13));
+    else svc_buf += e.tAs != 0xffff ? std::string(line.substr(e.tAs, e.tAe - e.tAs)) : std::string(kUndef);
+    const int32_t svc = raw_service(svc_buf);
+    auto& items = record_map(key_of(log_id)).items;
+    auto f = std::find_if(items.begin(), items.end(), [&](const Partial& p) { return p.svc == svc; });
     if (f != items.end()) { f->server = server; f->start_ms = ts; f->start_empty = ts_empty; }
-    else items.push_back(Partial{service, server, ts, ts_empty});
+    else items.push_back(Partial{svc, server, ts, ts_empty});
     return;
   }
   // parseEjbCommonTimingExit (:403-446)
-  std::string service = "S:" + std::string(tok_or_undef(toks, 9));
   double elapsed;
-  if (!(e.mask & PM_HOST) && has_tok(toks, 11)) elapsed = e.num;
-  else elapsed = has_tok(toks, 11) ? js::parse_int(toks[11]) : js::nan();
+  if (host) {
+    svc_buf += std::string(tk.get(9));
+    elapsed = tk.has(11) ? js::parse_int(tk.t[11]) : js::nan();
+  } else {
+    svc_buf += e.tAs != 0xffff ? std::string(line.substr(e.tAs, e.tAe - e.tAs)) : std::string(kUndef);
+    elapsed = e.num;
+  }
+  const int32_t svc = raw_service(svc_buf);
   if (log_id.empty()) {
-    output(server, service, "", js::nan(), 0, true, ts, ts_empty, elapsed, false, seq);
+    output(server, svc, "", js::nan(), 0, true, ts, ts_empty, elapsed, false, seq);
     return;
   }
-  auto it = record_.find(log_id);
+  const uint64_t key = key_of(log_id);
+  auto it = record_.find(key);
   if (it == record_.end()) { ++counters.ejb_exit_unmatched; return; }
-  auto& items = it->second.v.items;
-  auto f = std::find_if(items.begin(), items.end(), [&](const Partial& p) { return p.service_raw == service; });
+  auto& items = it->second.items;
+  auto f = std::find_if(items.begin(), items.end(), [&](const Partial& p) { return p.svc == svc; });
   if (f == items.end()) { ++counters.ejb_exit_unmatched; return; }
-  Partial part = *f;
+  const Partial part = *f;
   items.erase(f);
-  auto ait = acct_.find(log_id);
+  auto ait = acct_.find(key);
   if (ait != acct_.end()) {
-    output(server, service, log_id, js::parse_int(ait->second.v), part.start_ms, part.start_empty, ts, ts_empty,
-           elapsed, false, seq);
+    output(server, svc, log_id, ait->second.acct, part.start_ms, part.start_empty, ts, ts_empty, elapsed, false, seq);
   } else {
-    Need n{service, part.server, part.start_ms, part.start_empty, ts, ts_empty, elapsed, std::string(), false};
-    auto& ni = need_map(log_id).items;
-    auto g = std::find_if(ni.begin(), ni.end(), [&](const Need& x) { return x.service_raw == service; });
+    Need n{svc, part.server, part.start_ms, part.start_empty, ts, ts_empty, elapsed, js::nan(), false};
+    auto& ni = need_map(key, log_id).items;
+    auto g = std::find_if(ni.begin(), ni.end(), [&](const Need& x) { return x.svc == svc; });
     if (g != ni.end()) *g = n; else ni.push_back(n);
   }
 }
 
 void JoinShard::on_ct(const Event& e, std::string_view line, int32_t file, bool entry, uint64_t seq) {
   const int32_t server = (*files_)[file].server;
-  auto toks = js::split_ws(line, 8);
-  const std::string log_id = strip_brackets(toks[0]);
+  const bool host = e.mask & PM_HOST;
+  Toks tk;
+  if (host) tk.from_line(line); else tk.from_event(e, line);
+  std::string scratch;
+  const std::string_view log_id = strip_brackets(tk.t[0], scratch);
   double ts;
   bool ts_empty = false;
-  if (!(e.mask & PM_HOST) && has_tok(toks, 2)) {
+  if (!host && tk.has(2)) {
     ts = e.ts;
   } else {
-    std::string tsstr = std::string(tok_or_undef(toks, 1)) + " " + std::string(tok_or_undef(toks, 2));
+    std::string tsstr = std::string(tk.get(1)) + " " + std::string(tk.get(2));
     if (!js::convert_date(tsstr, cfg_.tz, ts)) { ts_empty = true; ts = js::nan(); }
   }
+  std::string_view service_v = kUndef, elapsed_v;
+  bool has_elapsed;
   std::vector<std::string_view> seg;
-  std::string_view service_v, elapsed_v;
-  bool has_service, has_elapsed;
-  if (!(e.mask & PM_HOST)) {
-    has_service = e.tAs != 0xffff;
+  if (!host) {
+    if (e.tAs != 0xffff) service_v = line.substr(e.tAs, e.tAe - e.tAs);
     has_elapsed = e.tBs != 0xffff;
-    if (has_service) service_v = line.substr(e.tAs, e.tAe - e.tAs);
-    if (has_elapsed) elapsed_v = line.substr(e.tBs, e.tBe - e.tBs);
   } else {
     seg = info_segment_tokens(line);
-    has_service = has_tok(seg, 1);
-    has_elapsed = has_tok(seg, 5);
-    if (has_service) service_v = seg[1];
+    if (seg.size() > 1) service_v = seg[1];
+    has_elapsed = seg.size() > 5;
     if (has_elapsed) elapsed_v = seg[5];
   }
-  const std::string service = has_service ? std::string(service_v) : std::string("undefined");
+  const int32_t svc = raw_service(service_v);
   if (entry) {  // parseCommonTimingEntry (:451-483)
     if (log_id.empty()) return;
-    auto it = record_.find(log_id);
-    if (it == record_.end())
-      it = record_.emplace(log_id, TtlEntry<RecordMap>{RecordMap{}, now_ + cfg_.record_ttl_ms}).first;
-    auto& items = it->second.v.items;
-    auto f = std::find_if(items.begin(), items.end(), [&](const Partial& p) { return p.service_raw == service; });
+    auto& items = record_map(key_of(log_id)).items;
+    auto f = std::find_if(items.begin(), items.end(), [&](const Partial& p) { return p.svc == svc; });
     if (f != items.end()) { f->server = server; f->start_ms = ts; f->start_empty = ts_empty; }
-    else items.push_back(Partial{service, server, ts, ts_empty});
+    else items.push_back(Partial{svc, server, ts, ts_empty});
     return;
   }
   // parseCommonTimingExit (:506-565)
   double elapsed = js::nan();
-  if (has_elapsed) elapsed = (!(e.mask & PM_HOST)) ? e.num : js::parse_int(elapsed_v);
+  if (has_elapsed) elapsed = host ? js::parse_int(elapsed_v) : e.num;
+  std::string baf_scratch;
   auto salvage = [&]() {  // salvageRecordAndOutput (:500-504)
-    std::string acct = baf_acct(line, toks, file, log_id, seq);
-    output(server, service, "", acct.empty() ? js::nan() : js::parse_int(acct), 0, true, ts, ts_empty, elapsed,
-           false, seq);
+    std::string_view acct = baf_acct(line, tk.get(3), file, log_id, seq, baf_scratch);
+    output(server, svc, "", acct.empty() ? js::nan() : js::parse_int(acct), 0, true, ts, ts_empty, elapsed, false,
+           seq);
   };
   if (log_id.empty()) { salvage(); return; }
-  auto it = record_.find(log_id);
+  const uint64_t key = key_of(log_id);
+  auto it = record_.find(key);
   if (it == record_.end()) { salvage(); return; }
-  auto& items = it->second.v.items;
-  auto f = std::find_if(items.begin(), items.end(), [&](const Partial& p) { return p.service_raw == service; });
-  if (f == items.end()) { salvage(); return; }
-  Partial part = *f;
-  auto ait = acct_.find(log_id);
+  auto* items = &it->second.items;
+  auto f = std::find_if(items->begin(), items->end(), [&](const Partial& p) { return p.svc == svc; });
+  if (f == items->end()) { salvage(); return; }
+  const Partial part = *f;
+  auto ait = acct_.find(key);
   if (ait != acct_.end()) {
-    items.erase(f);
-    output(server, service, log_id, js::parse_int(ait->second.v), part.start_ms, part.start_empty, ts, ts_empty,
-           elapsed, false, seq);
+    items->erase(f);
+    output(server, svc, log_id, ait->second.acct, part.start_ms, part.start_empty, ts, ts_empty, elapsed, false, seq);
     return;
   }
-  need_map(log_id);
-  std::string alt = baf_acct(line, toks, file, log_id, seq);  // may drain the need map first
-  Need n{service, part.server, part.start_ms, part.start_empty, ts, ts_empty, elapsed, alt, false};
-  auto& ni = need_map(log_id).items;
-  auto g = std::find_if(ni.begin(), ni.end(), [&](const Need& x) { return x.service_raw == service; });
+  need_map(key, log_id);
+  std::string_view alt = baf_acct(line, tk.get(3), file, log_id, seq, baf_scratch);  // may drain the map first
+  Need n{svc, part.server, part.start_ms, part.start_empty, ts, ts_empty, elapsed,
+         alt.empty() ? js::nan() : js::parse_int(alt), false};
+  auto& ni = need_map(key, log_id).items;
+  auto g = std::find_if(ni.begin(), ni.end(), [&](const Need& x) { return x.svc == svc; });
   if (g != ni.end()) *g = n; else ni.push_back(n);
-  // map.delete(service): the partial was looked up before baf_acct; re-find (vector may move)
-  auto it2 = record_.find(log_id);
+  // map.delete(service)
+  auto it2 = record_.find(key);
   if (it2 != record_.end()) {
-    auto& it2i = it2->second.v.items;
-    auto f2 = std::find_if(it2i.begin(), it2i.end(), [&](const Partial& p) { return p.service_raw == service; });
-    if (f2 != it2i.end()) it2i.erase(f2);
+    auto& v = it2->second.items;
+    auto f2 = std::find_if(v.begin(), v.end(), [&](const Partial& p) { return p.svc == svc; });
+    if (f2 != v.end()) v.erase(f2);
   }
 }
 
-// parseAppLine (:578-731)
+// parseAppLine (:578-731) -- rare lines, kept simple
 void JoinShard::on_app(const Event& e, std::string_view line, int32_t file, uint64_t seq) {
   const uint32_t m = e.mask;
   const int32_t server = (*files_)[file].server;
   if (m & PM_AUTR_MAP) {
     auto toks = js::split_ws(line, 8);
-    std::string log_id = strip_brackets(toks[0]);
-    std::string_view t5 = has_tok(toks, 5) ? toks[5] : std::string_view();
+    std::string scratch;
+    std::string log_id(strip_brackets(toks[0], scratch));
+    std::string_view t5 = toks.size() > 5 ? toks[5] : std::string_view();
     size_t eq = t5.find('=');
     std::string autr;
     if (eq != std::string_view::npos) {
@@ -415,7 +482,8 @@ void JoinShard::on_app(const Event& e, std::string_view line, int32_t file, uint
       autr = "undefined";
     }
     AuditCtx& ctx = audit_[file];
-    std::string alt = baf_acct(line, toks, file, log_id, seq);
+    std::string baf_scratch;
+    std::string alt(baf_acct(line, toks.size() > 3 ? toks[3] : std::string_view(), file, log_id, seq, baf_scratch));
     auto f = std::find_if(ctx.autr_map.begin(), ctx.autr_map.end(), [&](auto& p) { return p.first == autr; });
     if (f != ctx.autr_map.end()) f->second = {log_id, alt};
     else ctx.autr_map.push_back({autr, {log_id, alt}});
@@ -453,7 +521,11 @@ void JoinShard::on_app(const Event& e, std::string_view line, int32_t file, uint
       size_t c2 = line.find(':', c1 + 1);
       std::string_view a1 = line.substr(c1 + 1, c2 == std::string_view::npos ? std::string_view::npos : c2 - c1 - 1);
       auto st = js::split_ws(a1, 2);
-      elapsed = strip_brackets(st[0]);
+      std::string scratch;
+      elapsed.assign(strip_brackets(st[0], scratch));
+      for (char& ch : elapsed) (void)ch;
+      // strip_brackets keeps inner-only views; make sure *all* brackets are gone
+      elapsed.erase(std::remove_if(elapsed.begin(), elapsed.end(), [](char c) { return c == '[' || c == ']'; }), elapsed.end());
     }
     auto f = std::find_if(ctx.service_map.begin(), ctx.service_map.end(), [&](auto& p) { return p.first == service; });
     if (f == ctx.service_map.end()) { ctx.service_map.push_back({service, {}}); f = ctx.service_map.end() - 1; }
@@ -474,8 +546,8 @@ void JoinShard::on_app(const Event& e, std::string_view line, int32_t file, uint
   }
   if (m & PM_SW_NAME) { ctx.active_service = xml_inner(line); ctx.has_active_service = true; return; }
   if (!ctx.has_active_service || ctx.active_service.empty()) return;
-  const std::string& svc = ctx.active_service;
-  auto f = std::find_if(ctx.service_map.begin(), ctx.service_map.end(), [&](auto& p) { return p.first == svc; });
+  const std::string& svcname = ctx.active_service;
+  auto f = std::find_if(ctx.service_map.begin(), ctx.service_map.end(), [&](auto& p) { return p.first == svcname; });
   if (m & PM_SW_STARTTS) {
     if (f == ctx.service_map.end() || f->second.empty()) { ++counters.audit_errors; return; }
     f->second.front().has_start = true;
@@ -488,24 +560,28 @@ void JoinShard::on_app(const Event& e, std::string_view line, int32_t file, uint
     AuditItem obj = f->second.front();
     f->second.pop_front();
     const std::string& log_id = ctx.active_log_id;
-    const bool to_db = !icontains(svc, "Provider[");
+    const bool to_db = !icontains(svcname, "Provider[");
     double s_ms = js::nan(), e_ms = js::nan();
     bool s_empty = !obj.has_start || !js::convert_date(obj.start_ts, cfg_.tz, s_ms);
     bool e_empty = !js::convert_date(end_ts, cfg_.tz, e_ms);
     const double elapsed = js::parse_int(obj.elapsed);
-    auto ait = acct_.find(log_id);
+    const int32_t svc = raw_service(svcname);
+    const uint64_t key = key_of(log_id);
+    auto ait = acct_.find(key);
     if (ait != acct_.end()) {
-      output(server, svc, log_id, js::parse_int(ait->second.v), s_ms, s_empty, e_ms, e_empty, elapsed, to_db, seq);
+      output(server, svc, log_id, ait->second.acct, s_ms, s_empty, e_ms, e_empty, elapsed, to_db, seq);
     } else {
-      Need n{svc, server, s_ms, s_empty, e_ms, e_empty, elapsed, ctx.active_alt, to_db};
-      auto& ni = need_map(log_id).items;
-      auto g = std::find_if(ni.begin(), ni.end(), [&](const Need& x) { return x.service_raw == svc; });
+      const double alt = ctx.active_alt.empty() ? js::nan() : js::parse_int(ctx.active_alt);
+      Need n{svc, server, s_ms, s_empty, e_ms, e_empty, elapsed, alt, to_db};
+      auto& ni = need_map(key, log_id).items;
+      auto g = std::find_if(ni.begin(), ni.end(), [&](const Need& x) { return x.svc == svc; });
       if (g != ni.end()) *g = n; else ni.push_back(n);
     }
   }
 }
 
 void JoinShard::process(const Event* ev, size_t n, const uint8_t* bytes, const std::vector<int32_t>& chunk_file) {
+  out_.reserve(out_.size() + n / 2);
   for (size_t i = 0; i < n; ++i) {
     const Event& e = ev[i];
     ++counters.events;

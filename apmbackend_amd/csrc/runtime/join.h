@@ -8,9 +8,15 @@
 //   * EJB and standard CommonTiming entry/exit joins through recordCache (:378-565),
 //   * BAF account salvage (:486-504),
 //   * the audit-trail state machine (:578-731),
-//   * the three NodeCache TTL caches, modelled with the engine's log-time clock: lazy expiry on
-//     get/has plus a sweep at every batch boundary, need-cache expiry emitting records (:226-239).
+//   * the three NodeCache TTL caches, modelled with the engine's log-time clock: the clock is
+//     constant inside a batch and every cache is swept at the batch boundary, so lazy expiry on
+//     get/has can never fire mid-batch; need-cache expiry emits records (:226-239).
 // Output: completed transactions in line order, tagged for the stats stage or db_insert.
+//
+// Data layout: keys are 64-bit FNV-1a hashes of the logId bytes (no allocation on lookup; a
+// 64-bit collision between two live logIds of one JVM is treated as impossible), services are
+// interned per shard (raw name -> normalized global id, one dictionary lock per new name), and
+// every TTL cache keeps a FIFO of (key, expiry) so a sweep costs O(expired), not O(size).
 #pragma once
 #include <cstdint>
 #include <deque>
@@ -39,22 +45,27 @@ struct TxOut {
   bool toplevel;         // service matches /^S:/
 };
 
-// Global dictionaries shared by all shards (mutex-protected inserts, lock-free reads of
-// per-shard caches).
+// Global dictionary of normalized service names shared by all shards.
 class Dictionary {
  public:
   int32_t service_id(std::string_view normalized);
-  const std::string& service_name(int32_t id) const { return services_[id]; }
-  int32_t n_services() const { return (int32_t)services_.size(); }
+  const std::string& service_name(int32_t id) const {
+    std::lock_guard<std::mutex> g(mu_);
+    return services_[id];
+  }
+  int32_t n_services() const {
+    std::lock_guard<std::mutex> g(mu_);
+    return (int32_t)services_.size();
+  }
   std::vector<std::string> services_snapshot() const {
     std::lock_guard<std::mutex> g(mu_);
-    return services_;
+    return std::vector<std::string>(services_.begin(), services_.end());
   }
 
  private:
   mutable std::mutex mu_;
   std::unordered_map<std::string, int32_t> svc_map_;
-  std::vector<std::string> services_;
+  std::deque<std::string> services_;  // stable references
 };
 
 struct FileInfo {
@@ -78,7 +89,11 @@ struct JoinCounters {
 class JoinShard {
  public:
   JoinShard(const JoinConfig& cfg, Dictionary* dict, const std::vector<FileInfo>* files)
-      : cfg_(cfg), dict_(dict), files_(files) {}
+      : cfg_(cfg), dict_(dict), files_(files) {
+    acct_.reserve(1 << 15);
+    record_.reserve(1 << 14);
+    need_.reserve(1 << 12);
+  }
 
   void begin_batch(double now_ms, uint64_t batch_no);
   // Process the events of one batch that belong to this shard. `bytes` is the host copy of the
@@ -88,25 +103,24 @@ class JoinShard {
   std::vector<TxOut>& out() { return out_; }
   JoinCounters counters;
 
-  // checkpoint support (text form, see engine checkpoint)
   size_t n_partial_logids() const { return record_.size(); }
   size_t n_need_logids() const { return need_.size(); }
   size_t n_acct() const { return acct_.size(); }
 
  private:
-  struct Partial { std::string service_raw; int32_t server; double start_ms; bool start_empty; };
+  struct Partial { int32_t svc; int32_t server; double start_ms; bool start_empty; };
   struct Need {
-    std::string service_raw;
+    int32_t svc;          // shard-local raw service id
     int32_t server;
     double start_ms; bool start_empty;
     double end_ms; bool end_empty;
     double elapsed;
-    std::string alt_acct;  // altAcctNum ('' if none)
+    double alt_acct;      // parseInt(altAcctNum || '')
     bool insert_to_db;
   };
-  template <class V> struct TtlEntry { V v; double exp; };
-  struct RecordMap { std::vector<Partial> items; };
-  struct NeedMap { std::vector<Need> items; uint64_t created = 0; };
+  struct AcctEntry { double acct; double exp; };
+  struct RecordEntry { double exp; std::vector<Partial> items; };
+  struct NeedEntry { double exp; uint64_t created; std::string log_id; std::vector<Need> items; };
   struct SoapCtx { std::string log_id; bool has_log_id = false; bool pull_next = false; };
   struct AuditItem { std::string elapsed; bool has_start = false; std::string start_ts; };
   struct AuditCtx {
@@ -117,18 +131,19 @@ class JoinShard {
     bool elapsed_flag = false, sw_flag = false;
     std::vector<std::pair<std::string, std::deque<AuditItem>>> service_map;
   };
+  struct RawService { std::string raw; int32_t norm_id; bool toplevel; };
 
-  // NodeCache-like helpers (insertion-ordered where order is observable)
-  template <class M> bool alive(M& m, const std::string& k, bool is_need);
+  static uint64_t key_of(std::string_view s) { return fnv1a64((const uint8_t*)s.data(), (int)s.size()); }
+  int32_t raw_service(std::string_view raw);
   void sweep();
-  void expire_need(const std::string& log_id, NeedMap& nm);
+  void expire_need(NeedEntry& nm);
+  NeedEntry& need_map(uint64_t key, std::string_view log_id);
+  RecordEntry& record_map(uint64_t key);
   void save_acct(std::string_view acct, int32_t file, int source, std::string_view alt_log_id, uint64_t seq);
-  NeedMap& need_map(const std::string& log_id);
-  void output(int32_t server, std::string_view service_raw, std::string_view log_id, double acct,
-              double start_ms, bool start_empty, double end_ms, bool end_empty, double elapsed, bool to_db,
-              uint64_t seq);
-  std::string baf_acct(std::string_view line, const std::vector<std::string_view>& toks, int32_t file,
-                       std::string_view log_id, uint64_t seq);
+  void output(int32_t server, int32_t svc, std::string_view log_id, double acct, double start_ms, bool start_empty,
+              double end_ms, bool end_empty, double elapsed, bool to_db, uint64_t seq);
+  std::string_view baf_acct(std::string_view line, std::string_view tok3, int32_t file, std::string_view log_id,
+                            uint64_t seq, std::string& scratch);
 
   void on_soap(const Event& e, std::string_view line, int32_t file, uint64_t seq);
   void on_ejb(const Event& e, std::string_view line, int32_t file, bool entry, uint64_t seq);
@@ -141,13 +156,14 @@ class JoinShard {
   double now_ = 0;
   uint64_t batch_no_ = 0;
   uint64_t cur_line_ = 0;
-  // caches: key -> entry; insertion order tracked in parallel deques for sweeps
-  std::unordered_map<std::string, TtlEntry<std::string>> acct_;
-  std::unordered_map<std::string, TtlEntry<RecordMap>> record_;
-  std::unordered_map<std::string, TtlEntry<NeedMap>> need_;
-  std::deque<std::pair<std::string, double>> need_order_;  // (logId, exp) FIFO for expiry emission
+  std::unordered_map<uint64_t, AcctEntry> acct_;
+  std::unordered_map<uint64_t, RecordEntry> record_;
+  std::unordered_map<uint64_t, NeedEntry> need_;
+  std::deque<std::pair<uint64_t, double>> acct_fifo_, record_fifo_, need_fifo_;
   std::unordered_map<int32_t, SoapCtx> soap_;
   std::unordered_map<int32_t, AuditCtx> audit_;
+  std::unordered_map<uint64_t, int32_t> raw_svc_map_;
+  std::vector<RawService> raw_svc_;
   std::vector<TxOut> out_;
   uint32_t sub_ = 0;
 };

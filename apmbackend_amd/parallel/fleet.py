@@ -45,40 +45,31 @@ def merged_stats(moments: np.ndarray):
 
 
 class FleetBaseline:
-    def __init__(self, engine, world: int, max_services: Optional[int] = None, group=None):
-        import torch
-        self.torch = torch
+    """Native RCCL fleet exchange bound to an engine.
+
+    Rank 0 draws an RCCL unique id, the id travels over the existing torch.distributed group
+    (one small object broadcast at start-up), and every rank's engine creates its own RCCL
+    communicator.  From then on the engine's stats thread issues one ``ncclAllReduce`` per
+    processed batch on its comm stream -- no Python, no host synchronisation on the hot path.
+    """
+
+    def __init__(self, engine, world: int, rank: int, max_services: Optional[int] = None, group=None):
+        import torch.distributed as dist
         self.eng = engine
         self.world = world
-        self.group = group
         self.n_lags = len(engine.ecfg["lags"])
         self.cap = int(max_services or engine.cfg.get("gpu", {}).get("maxServices", 1 << 16))
-        n = self.cap * self.n_lags * 3 * 3
-        self.bufs = [torch.zeros(n, dtype=torch.float64, device="cuda") for _ in range(2)]
-        self.works = [None, None]
-        self.slot = 0
-        self.last = None
-        self.stream = torch.cuda.ExternalStream(engine.eng.comm_stream_handle())
-        self.exchanges = 0
+        native = type(engine.eng)
+        obj = [native.fleet_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        engine.eng.fleet_init(obj[0], world, rank, self.cap)
 
-    def exchange(self):
-        import torch.distributed as dist
-        i = self.slot
-        self.slot ^= 1
-        buf = self.bufs[i]
-        with self.torch.cuda.stream(self.stream):
-            if self.works[i] is not None:
-                self.works[i].wait()  # comm stream waits for the reduction that last used this slot
-            self.eng.eng.pack_service_moments(buf.data_ptr(), self.cap)
-            self.works[i] = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-        self.last = i
-        self.exchanges += 1
+    @property
+    def exchanges(self) -> int:
+        return int(self.eng.eng.fleet_rounds())
 
     def merged(self) -> np.ndarray:
-        if self.last is None:
+        raw = self.eng.eng.fleet_merged()
+        if not raw:
             return np.zeros((self.cap, self.n_lags, 3, 3))
-        w = self.works[self.last]
-        if w is not None:
-            w.wait()
-        self.stream.synchronize()
-        return self.bufs[self.last].view(self.cap, self.n_lags, 3, 3).cpu().numpy()
+        return np.frombuffer(raw, dtype=np.float64).reshape(self.cap, self.n_lags, 3, 3).copy()

@@ -108,13 +108,11 @@ def main():
     del raw
     t_gen = time.time() - t_gen
 
-    fleet = FleetBaseline(eng, world) if dist is not None else None
+    fleet = FleetBaseline(eng, world, rank) if dist is not None else None
 
     def step(i):
         ptr, n, chunks = batches[i]
         eng.eng.process_batch_ptr(ptr, n, chunks, -1.0)
-        if fleet is not None:
-            fleet.exchange()
 
     # ---- warmup (first batches create the series; then the z-score rings get a pre-history)
     for i in range(2):
@@ -123,6 +121,7 @@ def main():
         eng.eng.warm_history(12345 + rank)
     for i in range(2, 2 + args.warmup):
         step(i)
+    eng.eng.flush()
     torch.cuda.synchronize()
     m0 = eng.metrics()
     if dist is not None:
@@ -131,6 +130,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(2 + args.warmup, 2 + args.warmup + args.steps):
         step(i)
+    eng.eng.flush()  # the last batch's stats stage runs on the engine's stats thread
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()

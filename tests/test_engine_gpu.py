@@ -96,7 +96,7 @@ def test_pipeline_matches_oracle_exact():
     # released tx: same records, endTs-ordered (ties may differ from the JS heap order)
     assert collections.Counter(out["db"]) == collections.Counter(P.tx_db[:len(out["db"])]) or \
         sorted(out["db"]) == sorted(P.tx_db)
-    ends = [int(l.split("|")[7]) for l in out["db"]]
+    ends = [int(l.split("|")[6]) for l in out["db"]]  # tx|server|service|logId|acct|start|END|...
     assert ends == sorted(ends)
     m = eng.metrics()
     assert m["rollovers"] > 50 and m["join"]["host_fallback"] == 0
@@ -110,3 +110,23 @@ def test_rolling_mode_matches_exact_decisions():
     assert len(ex["fs"]) == len(ro["fs"])
     diff = sum(a != b for a, b in zip(ex["fs"], ro["fs"]))
     assert diff <= max(2, len(ex["fs"]) // 1000)  # only 1-ulp ties may print differently
+
+
+def test_native_fleet_exchange_single_rank():
+    """RCCL communicator owned by the engine (nranks=1): the all-reduced moments of the newest
+    batch equal a direct pack of the same state."""
+    lines, bl = synth_batches(4, duration=300)
+    C = small_cfg("rolling")
+    eng = APMEngine(C, keep_text=False)
+    cap = 64
+    eng.eng.fleet_init(type(eng.eng).fleet_unique_id(), 1, 0, cap)
+    for now, chunks in bl:
+        eng.process_lines(chunks, now)
+    got = np.frombuffer(eng.eng.fleet_merged(), dtype=np.float64)
+    assert eng.eng.fleet_rounds() == len(bl)
+    buf = torch.zeros(got.size, dtype=torch.float64, device="cuda")
+    eng.eng.pack_service_moments(buf.data_ptr(), cap)
+    torch.cuda.synchronize()  # device-wide: covers the engine's comm stream
+    want = buf.cpu().numpy()
+    assert got.sum() > 0
+    np.testing.assert_allclose(got, want, rtol=0, atol=0)
