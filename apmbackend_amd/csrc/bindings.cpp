@@ -92,8 +92,7 @@ EngineConfig config_from(const py::dict& d) {
   c.need_ttl_ms = get<double>(d, "need_ttl_ms", c.need_ttl_ms);
   c.tz = tz_from(d);
   c.join_threads = get<int>(d, "join_threads", c.join_threads);
-  c.keep_text = get<int>(d, "keep_text", c.keep_text);
-  c.keep_tx_records = get<int>(d, "keep_tx_records", c.keep_tx_records);
+  c.outputs = get<uint32_t>(d, "outputs", c.outputs);
   c.async_stats = get<int>(d, "async_stats", c.async_stats);
   return c;
 }
@@ -127,6 +126,7 @@ py::dict metrics_dict(const EngineMetrics& m) {
   d["batches"] = m.batches; d["bytes"] = m.bytes; d["lines"] = m.lines; d["events"] = m.events;
   d["tx"] = m.tx; d["tx_db"] = m.tx_db; d["tx_dropped"] = m.tx_dropped; d["rollovers"] = m.rollovers;
   d["alerts"] = m.alerts; d["alert_candidates"] = m.alert_candidates; d["released"] = m.released;
+  d["formatted_bytes"] = m.formatted_bytes; d["format_fallbacks"] = m.format_fallbacks;
   d["t_parse_ms"] = m.t_parse_ms; d["t_join_ms"] = m.t_join_ms; d["t_stats_ms"] = m.t_stats_ms;
   d["t_total_ms"] = m.t_total_ms;
   d["rollover_latency_ms"] = m.rollover_latency_ms;
@@ -158,7 +158,7 @@ class JoinHarness {
       sid = (int32_t)servers_.size();
       servers_.push_back(server);
       server_ids_[server] = sid;
-      shards_.emplace_back(new JoinShard(cfg_, &dict_, &files_));
+      shards_.emplace_back(new JoinShard(cfg_, &dict_, &files_, &servers_));
     } else {
       sid = it->second;
     }
@@ -192,7 +192,8 @@ class JoinHarness {
       for (auto& t : shards_[s]->out()) all.push_back(t);
     }
     std::stable_sort(all.begin(), all.end(), [](const TxOut& a, const TxOut& b) { return a.seq < b.seq; });
-    for (auto& t : all) out.push_back({t.to_db ? "db_insert" : "transactions", fmt::tx_line(t, servers_, dict_)});
+    for (auto& t : all)
+      out.push_back({t.to_db ? "db_insert" : "transactions", shards_[t.server]->text().substr(t.line_off, t.line_len)});
     ++batch_no_;
     return out;
   }
@@ -252,6 +253,13 @@ PYBIND11_MODULE(_apm_native, m) {
            py::arg("ptr"), py::arg("n"), py::arg("chunks"), py::arg("now") = -1.0)
       .def("take", &Engine::take, py::call_guard<py::gil_scoped_release>())
       .def("flush", &Engine::flush, py::call_guard<py::gil_scoped_release>())
+      .def("take_bytes", [](Engine& e, const std::string& k) {
+        std::string b;
+        { py::gil_scoped_release rel; b = e.take_bytes(k); }
+        return py::bytes(b);
+      })
+      .def("set_sink_fd", &Engine::set_sink_fd, py::call_guard<py::gil_scoped_release>())
+      .def("sink_bytes", &Engine::sink_bytes)
       .def("last_events", [](Engine& e) { return py::bytes(e.last_events()); })
       .def("warm_history", &Engine::warm_history)
       .def("metrics", [](Engine& e) {
@@ -306,6 +314,23 @@ PYBIND11_MODULE(_apm_native, m) {
   m.def("memcpy_to", [](uintptr_t dst, py::bytes b, uint64_t off) {
     std::string_view v = b;
     std::memcpy((char*)dst + off, v.data(), v.size());
+  });
+  m.def("gpu_to_fixed", [](const std::vector<double>& xs, int f) {
+    // K12 number printer on the device (test hook): nf(x, f) per value
+    const int n = (int)xs.size();
+    double* dx = nullptr;
+    char* dout = nullptr;
+    std::vector<char> h((size_t)n * 32);
+    HIP_OK(hipMalloc(&dx, std::max(1, n) * 8));
+    HIP_OK(hipMalloc(&dout, std::max<size_t>(32, h.size())));
+    HIP_OK(hipMemcpy(dx, xs.data(), (size_t)n * 8, hipMemcpyHostToDevice));
+    apm_format_fixed_batch(dx, n, f, dout, 0);
+    HIP_OK(hipMemcpy(h.data(), dout, h.size(), hipMemcpyDeviceToHost));
+    HIP_OK(hipFree(dx));
+    HIP_OK(hipFree(dout));
+    std::vector<std::string> r;
+    for (int i = 0; i < n; ++i) r.emplace_back(h.data() + (size_t)i * 32);
+    return r;
   });
   m.def("js_to_fixed", [](double x, int f) { return js::to_fixed(x, f); });
   m.def("js_num_str", [](double x) { return js::num_str(x); });

@@ -52,6 +52,28 @@ struct ZArgs {
   int32_t sigma_stddev;    // 0 = sqrt(mean) quirk, 1 = population sigma
   int32_t resync_k;        // rolling mode: exact resync period (0 = never)
   int64_t rollover_idx;
+  // rolling-mode resync range of this rollover (host computes it; rs_n = 0 -> none)
+  int32_t rs_lo, rs_n, rs_parts;
+  double* rs_part;         // [NSTAT][rs_parts][rs_n][4] partial (sum, comp, sumsq, sqcomp)
+  int32_t* rs_cnt;         // [NSTAT][rs_parts][rs_n]
+};
+
+// K12 st/fs encoding (format.hip)
+struct FormatArgs {
+  const int32_t* perm;          // [n] series in emission order
+  const WinStat* win;           // [S]
+  const ZOut* z[MAX_LAGS];      // [S] per lag
+  const int4* series_names;     // [S] {server off, len, service off, len} into `names`
+  const char* names;
+  int64_t edge_ts;
+  int32_t n;
+  int32_t n_lags;
+  int32_t lag_order[MAX_LAGS];  // ascending LAG value
+  int32_t lag_value[MAX_LAGS];
+  int32_t want_st, want_fs;
+  uint32_t *st_len, *fs_len, *st_off, *fs_off;  // [n + 1]
+  char *st_out, *fs_out;
+  int32_t* fallback;
 };
 
 struct AlertArgs {
@@ -100,6 +122,10 @@ int apm_release_merge(const int64_t* pool_end, const int64_t* pool_gid, int64_t 
 void apm_zscore(apm::ZArgs* a, int dtype_bytes, hipStream_t stream);
 void apm_zscore_warm(apm::ZArgs* a, int dtype_bytes, int fill, uint64_t seed, const apm::WinStat* base,
                      hipStream_t stream);
+size_t apm_format_tmp_bytes(int32_t n_max);
+void apm_format_fixed_batch(const double* d_x, int n, int f, char* d_out, hipStream_t stream);
+int apm_format_plan(apm::FormatArgs* a, void* tmp, size_t tmp_bytes, hipStream_t stream);
+void apm_format_write(apm::FormatArgs* a, hipStream_t stream);
 void apm_alert_eval(apm::AlertArgs* a, hipStream_t stream);
 // fleet.hip
 void apm_service_moments(const int32_t* series_service, const uint8_t* active, int32_t n_series, int32_t S,

@@ -9,9 +9,16 @@
 // ring[lag][stat][pos][series]: every active series pushes exactly one value per rollover, so
 // all series of a lag share the write position (head = rollover index mod LAG) and a warp of
 // consecutive series reads/writes one contiguous row -> fully coalesced.  The mean is kept as a
-// compensated (Neumaier) fp64 running sum + valid count, updated O(1) per rollover; a staggered
-// exact sequential recompute (the JS summation order) resynchronises every K rollovers.  In
-// "exact" mode the sequential sum is recomputed every time, which is bit-identical to JS.
+// compensated (Neumaier) fp64 running sum + valid count, updated O(1) per rollover.  Drift is
+// bounded by a staggered resync: every rollover one contiguous range of R = ceil(S/K) series
+// gets its window re-summed from the ring by k_zscore_resync (a [64 series x P partitions] tile
+// grid: a wave covers 64 consecutive series of one ring row -> coalesced 512 B reads, and the
+// partitions spread the L-long walk over P waves), and k_zscore folds the P partials in a fixed
+// order.  In "exact" mode each thread re-sums its window sequentially (the JS summation order),
+// which is bit-identical to the reference.
+//
+// Ring dtype: fp64 (parity), fp32, or bf16 (capacity mode, BASELINE config 2): values are
+// rounded on store and every moment is taken over the value *as stored*.
 #include "kernel_api.h"
 
 namespace apm {
@@ -19,6 +26,17 @@ namespace apm {
 
 template <typename T> __device__ __forceinline__ double ld(const T* p) { return (double)*p; }
 template <typename T> __device__ __forceinline__ void st(T* p, double v) { *p = (T)v; }
+// bf16 ring: raw uint16 storage, round-to-nearest-even from fp32, NaN preserved
+template <> __device__ __forceinline__ double ld<uint16_t>(const uint16_t* p) {
+  return (double)__uint_as_float((uint32_t)*p << 16);
+}
+template <> __device__ __forceinline__ void st<uint16_t>(uint16_t* p, double v) {
+  const float f = (float)v;
+  uint32_t u = __float_as_uint(f);
+  if (f != f) { *p = 0x7FC0; return; }
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  *p = (uint16_t)(u >> 16);
+}
 
 __device__ __forceinline__ void neumaier(double& s, double& c, double x) {
   const double t = s + x;
@@ -27,6 +45,38 @@ __device__ __forceinline__ void neumaier(double& s, double& c, double x) {
 }
 
 __device__ __forceinline__ bool valid(double v) { return v == v; }
+
+// Partial window sums for the resync range [rs_lo, rs_lo + rs_n): block = 64 series x 4
+// partitions, grid = (ceil(rs_n/64), P/4, NSTAT).
+template <typename T>
+__global__ __launch_bounds__(256) void k_zscore_resync(ZArgs a) {
+  const int j = blockIdx.x * 64 + threadIdx.x;
+  const int p = blockIdx.y * 4 + threadIdx.y;
+  const int k = blockIdx.z;
+  if (j >= a.rs_n || p >= a.rs_parts) return;
+  const int s = a.rs_lo + j;
+  const int L = a.lag, S = a.S;
+  double sum = 0, comp = 0, sq = 0, sqc = 0;
+  int c = 0;
+  if (s < a.n_series) {
+    const int n = a.len[s];
+    const int per = (L + a.rs_parts - 1) / a.rs_parts;
+    const int i0 = p * per, i1 = min(n, i0 + per);
+    const int oldest = (a.head - n + L) % L;
+    const T* col = reinterpret_cast<const T*>(a.ring) + (size_t)k * L * S + s;
+    int pos = oldest + i0;
+    if (pos >= L) pos -= L;
+    for (int i = i0; i < i1; ++i) {
+      const double v = ld(col + (size_t)pos * S);
+      if (valid(v)) { neumaier(sum, comp, v); neumaier(sq, sqc, v * v); ++c; }
+      if (++pos == L) pos = 0;
+    }
+  }
+  const size_t o = ((size_t)k * a.rs_parts + p) * a.rs_n + j;
+  a.rs_part[o * 4 + 0] = sum; a.rs_part[o * 4 + 1] = comp;
+  a.rs_part[o * 4 + 2] = sq; a.rs_part[o * 4 + 3] = sqc;
+  a.rs_cnt[o] = c;
+}
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_zscore(ZArgs a) {
@@ -46,7 +96,8 @@ __global__ __launch_bounds__(256) void k_zscore(ZArgs a) {
   const int head = a.head;
   const int last_pos = head == 0 ? L - 1 : head - 1;
   const int oldest = (head - n + L) % L;
-  const bool resync = a.exact || (a.resync_k > 0 && ((a.rollover_idx + s) % a.resync_k) == 0);
+  const bool exact = a.exact != 0;
+  const bool resync = !exact && s >= a.rs_lo && s < a.rs_lo + a.rs_n;
   const double xs[NSTAT] = {w.avg, w.p75, w.p95};
 #pragma unroll
   for (int k = 0; k < NSTAT; ++k) {
@@ -54,7 +105,17 @@ __global__ __launch_bounds__(256) void k_zscore(ZArgs a) {
     double sum = a.sum[k * S + s], comp = a.comp[k * S + s];
     int c = a.cnt[k * S + s];
     double sq = a.sumsq[k * S + s], sqc = a.sqcomp[k * S + s];
-    if (resync && n > 0) {
+    if (resync) {
+      sum = 0; comp = 0; sq = 0; sqc = 0; c = 0;
+      const int j = s - a.rs_lo;
+      for (int p = 0; p < a.rs_parts; ++p) {  // fixed order -> deterministic
+        const size_t o = ((size_t)k * a.rs_parts + p) * a.rs_n + j;
+        neumaier(sum, comp, a.rs_part[o * 4 + 0]); comp += a.rs_part[o * 4 + 1];
+        neumaier(sq, sqc, a.rs_part[o * 4 + 2]); sqc += a.rs_part[o * 4 + 3];
+        c += a.rs_cnt[o];
+      }
+    }
+    if (exact && n > 0) {
       // sequential left-to-right sum from 0, as Array.prototype.average does
       double es = 0.0, eq = 0.0;
       int ec = 0;
@@ -72,7 +133,7 @@ __global__ __launch_bounds__(256) void k_zscore(ZArgs a) {
     int sig = 0;
     if (n >= L) {
       bool mean_ok = c > 0;
-      if (mean_ok) mean = resync ? sum / (double)c : (sum + comp) / (double)c;
+      if (mean_ok) mean = exact ? sum / (double)c : (sum + comp) / (double)c;
       double sd = apm_nan();
       bool sd_ok = false;
       if (mean_ok) {
@@ -195,21 +256,34 @@ __global__ __launch_bounds__(256) void k_alert_eval(AlertArgs a) {
 
 }  // namespace apm
 
+namespace apm {
+template <typename T>
+void launch_zscore(ZArgs* a, hipStream_t stream) {
+  if (!a->exact && a->rs_n > 0) {
+    const dim3 g((a->rs_n + 63) / 64, (a->rs_parts + 3) / 4, NSTAT), b(64, 4);
+    hipLaunchKernelGGL(k_zscore_resync<T>, g, b, 0, stream, *a);
+  }
+  hipLaunchKernelGGL(k_zscore<T>, dim3((a->n_series + 255) / 256), dim3(256), 0, stream, *a);
+}
+
+}  // namespace apm
+
 extern "C" {
 using namespace apm;
 
 void apm_zscore(ZArgs* a, int dtype_bytes, hipStream_t stream) {
   if (a->n_series <= 0) return;
-  const dim3 g((a->n_series + 255) / 256), b(256);
-  if (dtype_bytes == 8) hipLaunchKernelGGL(k_zscore<double>, g, b, 0, stream, *a);
-  else hipLaunchKernelGGL(k_zscore<float>, g, b, 0, stream, *a);
+  if (dtype_bytes == 8) launch_zscore<double>(a, stream);
+  else if (dtype_bytes == 4) launch_zscore<float>(a, stream);
+  else launch_zscore<uint16_t>(a, stream);
 }
 
 void apm_zscore_warm(ZArgs* a, int dtype_bytes, int fill, uint64_t seed, const WinStat* base, hipStream_t stream) {
   if (a->n_series <= 0) return;
   const dim3 g((a->n_series + 255) / 256), b(256);
   if (dtype_bytes == 8) hipLaunchKernelGGL(k_zscore_warm<double>, g, b, 0, stream, *a, fill, seed, base);
-  else hipLaunchKernelGGL(k_zscore_warm<float>, g, b, 0, stream, *a, fill, seed, base);
+  else if (dtype_bytes == 4) hipLaunchKernelGGL(k_zscore_warm<float>, g, b, 0, stream, *a, fill, seed, base);
+  else hipLaunchKernelGGL(k_zscore_warm<uint16_t>, g, b, 0, stream, *a, fill, seed, base);
 }
 
 void apm_alert_eval(AlertArgs* a, hipStream_t stream) {

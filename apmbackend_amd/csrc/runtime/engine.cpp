@@ -1,6 +1,11 @@
 // apm::Engine implementation -- see engine.h.
 #include "engine.h"
 
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstring>
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -130,6 +135,12 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     L.out = (ZOut*)dmalloc((size_t)S * sizeof(ZOut));
     L.counter = (int32_t*)dmalloc((size_t)S * 4);
   }
+  // rolling-mode resync scratch: one contiguous range of ceil(S / K) series per rollover
+  if (cfg_.resync_k > 0 && !cfg_.exact_mean) {
+    rs_range_ = (S + cfg_.resync_k - 1) / cfg_.resync_k;
+    rs_part_ = (double*)dmalloc((size_t)NSTAT * RS_PARTS * rs_range_ * 4 * 8);
+    rs_cnt_ = (int32_t*)dmalloc((size_t)NSTAT * RS_PARTS * rs_range_ * 4);
+  }
   {
     const double* sp[MAX_LAGS] = {};
     const double* cp[MAX_LAGS] = {};
@@ -146,6 +157,15 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   d_hard_max_ = (double*)dmalloc((size_t)S * 8);
   d_suppressed_ = (uint8_t*)dmalloc(S);
   d_emit_key_ = (uint64_t*)dmalloc((size_t)S * 8);
+  // K12 formatter
+  d_ser_names_ = (int32_t*)dmalloc((size_t)S * 16);
+  d_perm_ = (int32_t*)dmalloc((size_t)S * 4);
+  d_fmt_len_ = (uint32_t*)dmalloc((size_t)2 * (S + 1) * 4);
+  d_fmt_off_ = (uint32_t*)dmalloc((size_t)2 * (S + 1) * 4);
+  d_fmt_fallback_ = (int32_t*)dmalloc(4);
+  fmt_tmp_bytes_ = apm_format_tmp_bytes(S + 1);
+  d_fmt_tmp_ = dmalloc(fmt_tmp_bytes_);
+  HIP_OK(hipHostMalloc((void**)&h_fmt_meta_, 64, hipHostMallocDefault));
   // alerts
   d_alerts_ = (AlertRec*)dmalloc((size_t)cfg_.max_alerts * sizeof(AlertRec));
   d_n_alerts_ = (int32_t*)dmalloc(16);
@@ -195,6 +215,8 @@ Engine::~Engine() {
   hipHostFree(h_bytes_); hipHostFree(h_chunk_begin_); hipHostFree(h_chunk_kind_); hipHostFree(h_chunk_file_);
   hipHostFree(h_events_); hipHostFree(h_counts_); hipHostFree(h_watermark_); hipHostFree(h_alerts_);
   hipHostFree(h_n_alerts_); hipHostFree(h_tx_); hipHostFree(h_gid_); hipHostFree(h_release_gid_);
+  if (h_fmt_out_) hipHostFree(h_fmt_out_);
+  hipHostFree(h_fmt_meta_);
   hipEventDestroy(ev_a_); hipEventDestroy(ev_b_);
   hipStreamDestroy(stream_); hipStreamDestroy(comm_stream_); hipStreamDestroy(parse_stream_);
 }
@@ -213,7 +235,7 @@ int32_t Engine::add_server(const std::string& name) {
   jc.acct_ttl_ms = cfg_.acct_ttl_ms;
   jc.need_ttl_ms = cfg_.need_ttl_ms;
   jc.tz = cfg_.tz;
-  shards_.emplace_back(new JoinShard(jc, &dict_, &files_));
+  shards_.emplace_back(new JoinShard(jc, &dict_, &files_, &servers_));
   return id;
 }
 
@@ -272,6 +294,17 @@ int32_t Engine::series_for(int32_t server, int32_t service) {
   const uint64_t ek = ((uint64_t)server_rank_[server] << 24) | (uint64_t)(server_next_service_[server]++);
   series_.push_back(SeriesInfo{server, service, ek});
   h_emit_key_.push_back(ek);
+  {
+    if ((int32_t)server_name_off_.size() <= server) server_name_off_.resize(server + 1, -1);
+    if ((int32_t)service_name_off_.size() <= service) service_name_off_.resize(service + 1, -1);
+    if (server_name_off_[server] < 0) server_name_off_[server] = intern_name(servers_[server]);
+    if (service_name_off_[service] < 0) service_name_off_[service] = intern_name(dict_.service_name(service));
+    h_ser_names_.push_back(server_name_off_[server]);
+    h_ser_names_.push_back((int32_t)servers_[server].size());
+    h_ser_names_.push_back(service_name_off_[service]);
+    h_ser_names_.push_back((int32_t)dict_.service_name(service).size());
+    perm_dirty_ = true;
+  }
   h_thr_.resize((size_t)n_series_ * MAX_LAGS);
   h_infl_.resize((size_t)n_series_ * MAX_LAGS);
   h_hard_max_.push_back(cfg_.hard_max_ms);
@@ -482,19 +515,23 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
 }
 
 void Engine::stats_worker() {
+  StatsJob job;
   for (;;) {
-    StatsJob job;
     {
       std::unique_lock<std::mutex> lk(st_mu_);
       st_cv_.wait(lk, [&]() { return st_stop_ || st_has_job_; });
       if (st_stop_ && !st_has_job_) return;
-      job = std::move(st_job_);
+      job.txs.swap(st_job_.txs);
+      job.text.swap(st_job_.text);
+      job.t0 = st_job_.t0;
       st_has_job_ = false;
     }
     const double t = now_ms();
     try {
+      cur_text_ = &job.text;
       stats_for_batch(job.txs, job.t0);
       fleet_exchange_locked();
+      drain_sinks();
     } catch (const std::exception& e) {
       std::lock_guard<std::mutex> g(st_mu_);
       st_error_ = e.what();
@@ -513,6 +550,10 @@ void Engine::post_stats(std::vector<TxOut>&& txs, double t0) {
   st_cv_.wait(lk, [&]() { return !st_busy_; });
   if (!st_error_.empty()) { std::string e = st_error_; st_error_.clear(); throw std::runtime_error(e); }
   st_job_.txs = std::move(txs);
+  // hand the shards' formatted tx lines to the stats thread; the shards get the previous
+  // batch's (consumed) arenas back and reuse their capacity
+  st_job_.text.resize(shards_.size());
+  for (size_t i = 0; i < shards_.size(); ++i) st_job_.text[i].swap(shards_[i]->text());
   st_job_.t0 = t0;
   st_has_job_ = true;
   st_busy_ = true;
@@ -539,8 +580,13 @@ void Engine::ensure_bucket_slot(int64_t b) {
 }
 
 void Engine::stats_for_batch(std::vector<TxOut>& txs, double batch_t0) {
-  const int keep = cfg_.keep_text;
   const int64_t latest_at_start = latest_;
+  const bool w_tx = want(OUT_TRANSACTIONS), w_audit = want(OUT_AUDIT_DB), w_db = want(OUT_DB);
+  const std::vector<std::string>& text = *cur_text_;
+  // this batch's pending tx lines go into one release block
+  const uint32_t blk_id = line_block_seq_++;
+  LineBlock* blk = nullptr;
+  if (w_db) blk = &line_blocks_[blk_id];
   // split: audit non-Provider records go straight to db_insert (Q18)
   std::vector<std::pair<uint32_t, int64_t>> triggers;  // (index in upload, new latest)
   uint32_t n = 0;
@@ -550,10 +596,16 @@ void Engine::stats_for_batch(std::vector<TxOut>& txs, double batch_t0) {
     ++metrics_.tx;
     if (t.to_db) {
       ++metrics_.tx_db;
-      if (keep) text_["audit_db"].push_back(fmt::tx_line(t, servers_, dict_));
+      if (w_audit) {
+        blob_[OUT_AUDIT_DB].append(text[t.server], t.line_off, t.line_len);
+        blob_[OUT_AUDIT_DB] += '\n';
+      }
       continue;
     }
-    if (keep) text_["transactions"].push_back(fmt::tx_line(t, servers_, dict_));
+    if (w_tx) {
+      blob_[OUT_TRANSACTIONS].append(text[t.server], t.line_off, t.line_len);
+      blob_[OUT_TRANSACTIONS] += '\n';
+    }
     // NaN / short endTs would wedge the reference's heap forever: dropped and counted (fix)
     if (!(t.end_ms == t.end_ms) || t.end_ms < 10000) { ++metrics_.tx_dropped; continue; }
     const int64_t end = (int64_t)t.end_ms;
@@ -568,15 +620,23 @@ void Engine::stats_for_batch(std::vector<TxOut>& txs, double batch_t0) {
     const double e = t.elapsed;
     r.elapsed = (e == e && e >= -2147483647.0 && e <= 2147483647.0) ? (int32_t)e : ELAPSED_NAN;
     h_tx_[n] = r;
-    const int64_t gid = next_gid_++;
+    int64_t gid = next_gid_++;
+    if (blk) {
+      // [u32 len][bytes] records; the gid addresses the record
+      gid = ((int64_t)blk_id << 32) | (int64_t)blk->data.size();
+      const uint32_t len = t.line_len;
+      blk->data.append((const char*)&len, 4);
+      blk->data.append(text[t.server], t.line_off, t.line_len);
+      ++blk->live;
+    }
     h_gid_[n] = gid;
-    if (cfg_.keep_tx_records || keep) tx_records_.emplace(gid, t);
     if (b != agg_b) { if (agg_n) { pool_bucket_count_[agg_b] += agg_n; pool_exact_edge_[agg_b] += agg_e; } agg_b = b; agg_n = agg_e = 0; }
     ++agg_n;
     if (end == b * 10000) ++agg_e;
     ++n;
   }
   if (agg_n) { pool_bucket_count_[agg_b] += agg_n; pool_exact_edge_[agg_b] += agg_e; }
+  if (blk && blk->live == 0) line_blocks_.erase(blk_id);
   for (auto it = pool_exact_edge_.begin(); it != pool_exact_edge_.end();) {
     if (it->second == 0) it = pool_exact_edge_.erase(it); else ++it;
   }
@@ -658,15 +718,28 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
     pool_n_ = pool_n_ + tail_n_;
     tail_n_ = 0;
     if (released > pool_n_) released = pool_n_;
-    if ((cfg_.keep_tx_records || cfg_.keep_text) && released > 0) {
+    if (want(OUT_DB) && released > 0) {
       HIP_OK(hipMemcpyAsync(h_release_gid_, d_pool_gid_[pool_cur_], (size_t)released * 8, hipMemcpyDeviceToHost,
                             stream_));
       HIP_OK(hipStreamSynchronize(stream_));
+      std::string& out = blob_[OUT_DB];
+      uint32_t cur_id = UINT32_MAX;
+      LineBlock* cur = nullptr;
       for (int64_t i = 0; i < released; ++i) {
-        auto it = tx_records_.find(h_release_gid_[i]);
-        if (it == tx_records_.end()) continue;
-        if (cfg_.keep_text) text_["db"].push_back(fmt::tx_line(it->second, servers_, dict_));
-        tx_records_.erase(it);
+        const uint64_t g = (uint64_t)h_release_gid_[i];
+        const uint32_t id = (uint32_t)(g >> 32);
+        if (id != cur_id) {
+          auto it = line_blocks_.find(id);
+          cur = it == line_blocks_.end() ? nullptr : &it->second;
+          cur_id = id;
+        }
+        if (!cur) continue;
+        const size_t off = (size_t)(g & 0xffffffffu);
+        uint32_t len;
+        std::memcpy(&len, cur->data.data() + off, 4);
+        out.append(cur->data, off + 4, len);
+        out += '\n';
+        if (--cur->live == 0) { line_blocks_.erase(cur_id); cur = nullptr; cur_id = UINT32_MAX; }
       }
     }
     metrics_.released += released;
@@ -722,6 +795,11 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
     za.head = (int32_t)(rollover_idx_ % cfg_.lags[l]);
     za.exact = cfg_.exact_mean; za.sigma_stddev = cfg_.sigma_stddev; za.resync_k = cfg_.resync_k;
     za.rollover_idx = rollover_idx_;
+    za.rs_lo = 0; za.rs_n = 0; za.rs_parts = RS_PARTS; za.rs_part = rs_part_; za.rs_cnt = rs_cnt_;
+    if (rs_range_ > 0) {
+      za.rs_lo = (int32_t)((rollover_idx_ % cfg_.resync_k) * rs_range_);
+      za.rs_n = std::max(0, std::min(rs_range_, n_series_ - za.rs_lo));
+    }
     apm_zscore(&za, cfg_.ring_bytes, stream_);
     AlertArgs aa;
     aa.win = d_win_; aa.z = LS.out; aa.counter = LS.counter; aa.hard_max = d_hard_max_;
@@ -735,7 +813,7 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   HIP_OK(hipMemcpyAsync(h_n_alerts_, d_n_alerts_, 4, hipMemcpyDeviceToHost, stream_));
   HIP_OK(hipStreamSynchronize(stream_));
   metrics_.rollover_latency_ms.push_back(now_ms() - batch_t0);
-  if (cfg_.keep_text) format_rollover_text(edge_ts);
+  if (want(OUT_ST) || want(OUT_FS)) format_rollover_text(edge_ts);
   flush_alerts(edge_ts);
 }
 
@@ -749,7 +827,7 @@ void Engine::flush_alerts(int64_t edge_ts) {
   // per-(service|series) cooldown, first candidate in emission order wins (:436-468)
   std::vector<WinStat> win;
   std::vector<std::vector<ZOut>> z(cfg_.n_lags);
-  const bool need_rows = cfg_.keep_text != 0;
+  const bool need_rows = want(OUT_AL);
   if (need_rows) {
     download_winstats(win);
     for (int l = 0; l < cfg_.n_lags; ++l) download_zout(l, z[l]);
@@ -769,13 +847,139 @@ void Engine::flush_alerts(int64_t edge_ts) {
     if (need_rows) {
       const std::string fs = fmt::fs_line(edge_ts, servers_[si.server], dict_.service_name(si.service),
                                           cfg_.lags[r.lag_idx], win[r.series], z[r.lag_idx][r.series]);
-      text_["al"].push_back(fmt::al_line(now, edge_ts, servers_[si.server], dict_.service_name(si.service),
-                                         r.causes, fs));
+      blob_[OUT_AL] += fmt::al_line(now, edge_ts, servers_[si.server], dict_.service_name(si.service), r.causes, fs);
+      blob_[OUT_AL] += '\n';
     }
   }
 }
 
+int32_t Engine::intern_name(const std::string& name) {
+  auto it = name_off_.find(name);
+  if (it != name_off_.end()) return it->second;
+  const int32_t off = (int32_t)h_names_.size();
+  h_names_ += name;
+  name_off_.emplace(name, off);
+  return off;
+}
+
+void* Engine::regrow(void* old, size_t& cap, size_t need) {
+  if (need <= cap && old) return old;
+  size_t nc = std::max<size_t>(need + need / 2, 1 << 20);
+  if (old) {
+    HIP_OK(hipStreamSynchronize(stream_));
+    HIP_OK(hipFree(old));
+    allocations_.erase(std::remove(allocations_.begin(), allocations_.end(), old), allocations_.end());
+    device_bytes_ -= (cap + 255) & ~(size_t)255;
+  }
+  cap = nc;
+  return dmalloc(nc);
+}
+
+void Engine::sync_format_tables() {
+  if (names_uploaded_ < h_names_.size()) {
+    if (h_names_.size() > names_cap_) {
+      // grow: re-upload everything into the bigger buffer
+      d_names_ = (char*)regrow(d_names_, names_cap_, h_names_.size());
+      names_uploaded_ = 0;
+    }
+    HIP_OK(hipMemcpyAsync(d_names_ + names_uploaded_, h_names_.data() + names_uploaded_,
+                          h_names_.size() - names_uploaded_, hipMemcpyHostToDevice, stream_));
+    HIP_OK(hipStreamSynchronize(stream_));  // h_names_ may reallocate later
+    names_uploaded_ = h_names_.size();
+  }
+  if (ser_names_uploaded_ < n_series_) {
+    const int32_t lo = ser_names_uploaded_;
+    HIP_OK(hipMemcpyAsync(d_ser_names_ + (size_t)lo * 4, h_ser_names_.data() + (size_t)lo * 4,
+                          (size_t)(n_series_ - lo) * 16, hipMemcpyHostToDevice, stream_));
+    HIP_OK(hipStreamSynchronize(stream_));
+    ser_names_uploaded_ = n_series_;
+  }
+  if (perm_dirty_) {
+    h_perm_.resize(n_series_);
+    for (int32_t i = 0; i < n_series_; ++i) h_perm_[i] = i;
+    std::sort(h_perm_.begin(), h_perm_.end(),
+              [&](int32_t a, int32_t b) { return series_[a].emit_key < series_[b].emit_key; });
+    HIP_OK(hipMemcpyAsync(d_perm_, h_perm_.data(), (size_t)n_series_ * 4, hipMemcpyHostToDevice, stream_));
+    HIP_OK(hipStreamSynchronize(stream_));
+    perm_dirty_ = false;
+  }
+}
+
+void Engine::emit_bytes(int kind, const char* p, size_t n) {
+  if (!n) return;
+  if (sink_fd_[kind] >= 0) {
+    // keep stream order: whatever is buffered goes first, then straight from the staging buffer
+    drain_sinks();
+    while (n) {
+      const ssize_t w = ::write(sink_fd_[kind], p, n);
+      if (w < 0) {
+        if (errno == EINTR) continue;
+        throw std::runtime_error(std::string("sink write failed: ") + std::strerror(errno));
+      }
+      p += w;
+      n -= (size_t)w;
+      sink_bytes_[kind] += (size_t)w;
+    }
+    return;
+  }
+  blob_[kind].append(p, n);
+}
+
 void Engine::format_rollover_text(int64_t edge_ts) {
+  const int32_t n = n_series_;
+  if (n == 0) return;
+  sync_format_tables();
+  const int32_t S = cfg_.max_series;
+  FormatArgs fa{};
+  fa.perm = d_perm_;
+  fa.win = d_win_;
+  for (int l = 0; l < cfg_.n_lags; ++l) { fa.z[l] = lag_[l].out; fa.lag_value[l] = cfg_.lags[l]; }
+  std::vector<int> lag_order(cfg_.n_lags);
+  for (int l = 0; l < cfg_.n_lags; ++l) lag_order[l] = l;
+  std::sort(lag_order.begin(), lag_order.end(), [&](int a, int b) { return cfg_.lags[a] < cfg_.lags[b]; });
+  for (int l = 0; l < cfg_.n_lags; ++l) fa.lag_order[l] = lag_order[l];
+  fa.series_names = reinterpret_cast<const int4*>(d_ser_names_);
+  fa.names = d_names_;
+  fa.edge_ts = edge_ts;
+  fa.n = n;
+  fa.n_lags = cfg_.n_lags;
+  fa.want_st = want(OUT_ST);
+  fa.want_fs = want(OUT_FS);
+  fa.st_len = d_fmt_len_;
+  fa.fs_len = d_fmt_len_ + (S + 1);
+  fa.st_off = d_fmt_off_;
+  fa.fs_off = d_fmt_off_ + (S + 1);
+  fa.fallback = d_fmt_fallback_;
+  if (apm_format_plan(&fa, d_fmt_tmp_, fmt_tmp_bytes_, stream_) != 0) throw std::runtime_error("format scan failed");
+  HIP_OK(hipMemcpyAsync(h_fmt_meta_ + 0, fa.st_off + n, 4, hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipMemcpyAsync(h_fmt_meta_ + 1, fa.fs_off + n, 4, hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipMemcpyAsync(h_fmt_meta_ + 2, d_fmt_fallback_, 4, hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+  if (h_fmt_meta_[2]) {
+    ++metrics_.format_fallbacks;
+    format_rollover_text_host(edge_ts);
+    return;
+  }
+  const size_t st_total = h_fmt_meta_[0], fs_total = h_fmt_meta_[1];
+  d_fmt_out_[0] = (char*)regrow(d_fmt_out_[0], fmt_out_cap_[0], st_total + 1);
+  d_fmt_out_[1] = (char*)regrow(d_fmt_out_[1], fmt_out_cap_[1], fs_total + 1);
+  fa.st_out = d_fmt_out_[0];
+  fa.fs_out = d_fmt_out_[1];
+  apm_format_write(&fa, stream_);
+  if (st_total + fs_total > h_fmt_cap_) {
+    if (h_fmt_out_) HIP_OK(hipHostFree(h_fmt_out_));
+    h_fmt_cap_ = (st_total + fs_total) * 3 / 2 + (1 << 20);
+    HIP_OK(hipHostMalloc((void**)&h_fmt_out_, h_fmt_cap_, hipHostMallocDefault));
+  }
+  if (st_total) HIP_OK(hipMemcpyAsync(h_fmt_out_, fa.st_out, st_total, hipMemcpyDeviceToHost, stream_));
+  if (fs_total) HIP_OK(hipMemcpyAsync(h_fmt_out_ + st_total, fa.fs_out, fs_total, hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+  metrics_.formatted_bytes += st_total + fs_total;
+  emit_bytes(OUT_ST, h_fmt_out_, st_total);
+  emit_bytes(OUT_FS, h_fmt_out_ + st_total, fs_total);
+}
+
+void Engine::format_rollover_text_host(int64_t edge_ts) {
   std::vector<WinStat> win;
   download_winstats(win);
   std::vector<std::vector<ZOut>> z(cfg_.n_lags);
@@ -783,17 +987,21 @@ void Engine::format_rollover_text(int64_t edge_ts) {
   std::vector<int32_t> order;
   for (int32_t s = 0; s < n_series_; ++s) if (win[s].active) order.push_back(s);
   std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return series_[a].emit_key < series_[b].emit_key; });
-  auto& st = text_["st"];
-  auto& fs = text_["fs"];
+  std::string& st = blob_[OUT_ST];
+  std::string& fs = blob_[OUT_FS];
+  const bool w_st = want(OUT_ST), w_fs = want(OUT_FS);
   // lag order: ascending LAG value (integer-keyed object iteration in the reference)
   std::vector<int> lag_order(cfg_.n_lags);
   for (int l = 0; l < cfg_.n_lags; ++l) lag_order[l] = l;
   std::sort(lag_order.begin(), lag_order.end(), [&](int a, int b) { return cfg_.lags[a] < cfg_.lags[b]; });
   for (int32_t s : order) {
     const SeriesInfo& si = series_[s];
-    st.push_back(fmt::st_line(edge_ts, servers_[si.server], dict_.service_name(si.service), win[s]));
-    for (int l : lag_order)
-      fs.push_back(fmt::fs_line(edge_ts, servers_[si.server], dict_.service_name(si.service), cfg_.lags[l], win[s], z[l][s]));
+    if (w_st) { st += fmt::st_line(edge_ts, servers_[si.server], dict_.service_name(si.service), win[s]); st += '\n'; }
+    if (w_fs)
+      for (int l : lag_order) {
+        fs += fmt::fs_line(edge_ts, servers_[si.server], dict_.service_name(si.service), cfg_.lags[l], win[s], z[l][s]);
+        fs += '\n';
+      }
   }
 }
 
@@ -811,11 +1019,59 @@ void Engine::download_zout(int l, std::vector<ZOut>& out) {
   HIP_OK(hipStreamSynchronize(stream_));
 }
 
+const char* out_kind_name(int k) {
+  static const char* n[N_OUT] = {"transactions", "audit_db", "db", "st", "fs", "al"};
+  return n[k];
+}
+
+int out_kind_of(const std::string& name) {
+  for (int k = 0; k < N_OUT; ++k)
+    if (name == out_kind_name(k)) return k;
+  throw std::runtime_error("unknown output stream: " + name);
+}
+
 std::vector<std::string> Engine::take(const std::string& kind) {
-  flush();
+  const std::string b = take_bytes(kind);
   std::vector<std::string> r;
-  r.swap(text_[kind]);
+  size_t i = 0;
+  while (i < b.size()) {
+    size_t j = b.find('\n', i);
+    if (j == std::string::npos) j = b.size();
+    r.emplace_back(b, i, j - i);
+    i = j + 1;
+  }
   return r;
+}
+
+std::string Engine::take_bytes(const std::string& kind) {
+  flush();
+  std::string r;
+  r.swap(blob_[out_kind_of(kind)]);
+  return r;
+}
+
+void Engine::set_sink_fd(const std::string& kind, int fd) {
+  flush();
+  sink_fd_[out_kind_of(kind)] = fd;
+}
+
+void Engine::drain_sinks() {
+  for (int k = 0; k < N_OUT; ++k) {
+    if (sink_fd_[k] < 0 || blob_[k].empty()) continue;
+    const char* p = blob_[k].data();
+    size_t left = blob_[k].size();
+    while (left) {
+      const ssize_t w = ::write(sink_fd_[k], p, left);
+      if (w < 0) {
+        if (errno == EINTR) continue;
+        throw std::runtime_error(std::string("sink write failed: ") + std::strerror(errno));
+      }
+      p += w;
+      left -= (size_t)w;
+    }
+    sink_bytes_[k] += blob_[k].size();
+    blob_[k].clear();
+  }
 }
 
 void Engine::warm_history(uint64_t seed) {

@@ -49,7 +49,7 @@ struct EngineConfig {
   int64_t pool_cap = 1 << 23;
   int32_t max_tx_per_batch = 1 << 21;
   int32_t max_alerts = 1 << 16;
-  int ring_bytes = 8;            // 8 = float64, 4 = float32
+  int ring_bytes = 8;            // 8 = float64, 4 = float32, 2 = bfloat16
   int exact_mean = 0;
   int sigma_stddev = 0;
   int resync_k = 360;
@@ -77,11 +77,21 @@ struct EngineConfig {
   double record_ttl_ms = 120000, acct_ttl_ms = 120000, need_ttl_ms = 30000;
   TzTable tz{};
   int join_threads = 0;
-  // outputs
-  int keep_text = 0;        // format tx/st/fs/al lines for sinks/tests
-  int keep_tx_records = 0;  // keep full tx for the db release stream
+  // outputs: bit k of `outputs` materialises stream k (OutKind) in the reference wire format
+  uint32_t outputs = 0;
   int async_stats = 1;      // overlap batch i's stats with batch i+1's parse + join
 };
+
+// Output streams (queue names of the reference, config/apm_config.json:12,87,99-100,113-114,178):
+//   TRANSACTIONS  parse -> stats  tx lines   (only for the AMQP bridge; fused internally)
+//   AUDIT_DB      parse -> db     tx lines of audit non-Provider records (Q18)
+//   DB            stats -> db     released tx lines in endTs order (K9)
+//   ST            stats -> z      st lines  (fused internally; bridge only)
+//   FS            z -> alerts/db  fs lines (one per series per LAG)
+//   AL            alerts -> db    al lines
+enum OutKind { OUT_TRANSACTIONS = 0, OUT_AUDIT_DB, OUT_DB, OUT_ST, OUT_FS, OUT_AL, N_OUT };
+const char* out_kind_name(int k);
+int out_kind_of(const std::string& name);
 
 struct Chunk {
   int32_t file;
@@ -91,6 +101,7 @@ struct Chunk {
 struct EngineMetrics {
   uint64_t batches = 0, bytes = 0, lines = 0, events = 0, tx = 0, tx_db = 0, tx_dropped = 0;
   uint64_t rollovers = 0, alerts = 0, alert_candidates = 0, series = 0, released = 0;
+  uint64_t formatted_bytes = 0, format_fallbacks = 0;
   double t_parse_ms = 0, t_join_ms = 0, t_stats_ms = 0, t_total_ms = 0;
   std::vector<double> rollover_latency_ms;   // batch arrival -> alert decision per rollover
 };
@@ -127,9 +138,15 @@ class Engine {
   void process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const std::vector<Chunk>& chunks,
                      double now_override = -1.0);
 
-  // Text outputs accumulated since the last take (keep_text=1): "transactions", "audit_db",
-  // "db", "st", "fs", "al".
+  // Text outputs accumulated since the last take: "transactions", "audit_db", "db", "st", "fs",
+  // "al" (enabled by EngineConfig::outputs).  take() splits into lines; take_bytes() hands out
+  // the newline-terminated blob.
   std::vector<std::string> take(const std::string& kind);
+  std::string take_bytes(const std::string& kind);
+  // Route a stream to a file descriptor: the stats thread write()s each batch's blob to it (a
+  // COPY/queue spool file, a pipe to the DB loader, /dev/null).  fd < 0 detaches.
+  void set_sink_fd(const std::string& kind, int fd);
+  uint64_t sink_bytes(const std::string& kind) const { return sink_bytes_[out_kind_of(kind)]; }
 
   // Warm the z-score rings with a synthetic pre-history (benchmarks).
   void warm_history(uint64_t seed);
@@ -175,12 +192,19 @@ class Engine {
   void ensure_bucket_slot(int64_t b);
   void do_rollover(int64_t L, double batch_t0);
   void flush_alerts(int64_t edge_ts);
-  void format_rollover_text(int64_t edge_ts);
+  void format_rollover_text(int64_t edge_ts);       // K12 on the GPU
+  void format_rollover_text_host(int64_t edge_ts);  // fallback (|value| >= 1e13)
+  void sync_format_tables();
+  int32_t intern_name(const std::string& name);
+  void* regrow(void* old, size_t& cap, size_t need);
+  void emit_bytes(int kind, const char* p, size_t n);
   void upload_series_tables(int32_t lo);
   void pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream);
   void fleet_exchange_locked();
   void stats_worker();
   void post_stats(std::vector<TxOut>&& txs, double t0);
+  void drain_sinks();
+  bool want(int k) const { return (cfg_.outputs >> k) & 1u; }
   void* dmalloc(size_t bytes);
 
   EngineConfig cfg_;
@@ -193,7 +217,8 @@ class Engine {
   hipEvent_t fleet_ev_[2] = {nullptr, nullptr};
   uint64_t fleet_rounds_ = 0;
   // stats thread
-  struct StatsJob { std::vector<TxOut> txs; double t0 = 0; };
+  struct StatsJob { std::vector<TxOut> txs; std::vector<std::string> text; double t0 = 0; };
+  const std::vector<std::string>* cur_text_ = nullptr;  // text arenas of the job being processed
   std::thread stats_thread_;
   std::mutex st_mu_;
   std::condition_variable st_cv_;
@@ -270,6 +295,10 @@ class Engine {
     ZOut* out = nullptr;
     int32_t* counter = nullptr;
   } lag_[MAX_LAGS];
+  static constexpr int RS_PARTS = 64;
+  int32_t rs_range_ = 0;
+  double* rs_part_ = nullptr;
+  int32_t* rs_cnt_ = nullptr;
   double* d_hard_max_ = nullptr;
   void* d_lag_sum_ptrs_ = nullptr;
   void* d_lag_comp_ptrs_ = nullptr;
@@ -301,7 +330,12 @@ class Engine {
   std::map<int64_t, int64_t> pool_exact_edge_;     // endTs == bucket start count
   int64_t* h_release_gid_ = nullptr;
   int64_t next_gid_ = 0;
-  std::unordered_map<int64_t, TxOut> tx_records_;  // keep_tx_records
+  // Released-tx line store: each stats batch appends its pending tx lines to one block; the
+  // pool payload (gid) is (block << 32 | offset).  A block is freed when its last line is
+  // released (lines leave in endTs order, so blocks drain roughly in age order).
+  struct LineBlock { std::string data; int64_t live = 0; };
+  std::unordered_map<uint32_t, LineBlock> line_blocks_;
+  uint32_t line_block_seq_ = 0;
 
   uint32_t last_n_events_ = 0;
 
@@ -309,8 +343,32 @@ class Engine {
   double watermark_ = 0;
   uint64_t batch_no_ = 0;
 
+  // K12 formatter tables: names (server + service strings), per-series name refs, emission order
+  std::string h_names_;
+  std::unordered_map<std::string, int32_t> name_off_;
+  std::vector<int32_t> server_name_off_, service_name_off_;
+  std::vector<int32_t> h_ser_names_;            // 4 per series
+  std::vector<int32_t> h_perm_;
+  bool perm_dirty_ = true;
+  size_t names_uploaded_ = 0, names_cap_ = 0;
+  int32_t ser_names_uploaded_ = 0;
+  char* d_names_ = nullptr;
+  int32_t* d_ser_names_ = nullptr;
+  int32_t* d_perm_ = nullptr;
+  uint32_t *d_fmt_len_ = nullptr, *d_fmt_off_ = nullptr;  // [4][S + 1]: st_len, fs_len, st_off, fs_off
+  int32_t* d_fmt_fallback_ = nullptr;
+  void* d_fmt_tmp_ = nullptr;
+  size_t fmt_tmp_bytes_ = 0;
+  char* d_fmt_out_[2] = {nullptr, nullptr};
+  size_t fmt_out_cap_[2] = {0, 0};
+  char* h_fmt_out_ = nullptr;                    // pinned staging for the D2H of formatted text
+  size_t h_fmt_cap_ = 0;
+  uint32_t* h_fmt_meta_ = nullptr;               // pinned: st total, fs total, fallback
+
   // text outputs
-  std::map<std::string, std::vector<std::string>> text_;
+  std::string blob_[N_OUT];
+  int sink_fd_[N_OUT] = {-1, -1, -1, -1, -1, -1};
+  uint64_t sink_bytes_[N_OUT] = {0, 0, 0, 0, 0, 0};
   EngineMetrics metrics_;
   hipEvent_t ev_a_, ev_b_;
 };

@@ -1,5 +1,4 @@
-// Wire-format encoders (entries.js toCSVString): tx (:16-21), st (:71-73), fs (:116-118),
-// al (:214-216).  Numbers go through the JS-exact helpers in jsutil.h.
+// Wire-format encoders (entries.js toCSVString): st (:71-73), fs (:116-118), al (:214-216).  Numbers go through the JS-exact helpers in jsutil.h.
 #pragma once
 #include <string>
 #include <vector>
@@ -17,25 +16,7 @@ inline const char* cause_text(int i) {
   return t[i];
 }
 
-inline std::string tx_line(const TxOut& t, const std::vector<std::string>& servers, const Dictionary& dict) {
-  std::string s = "tx|";
-  s += servers[t.server];
-  s += '|';
-  s += dict.service_name(t.service);
-  s += '|';
-  s += t.log_id;
-  s += '|';
-  s += js::num_str(t.acct);
-  s += '|';
-  s += js::num_str(t.start_ms);
-  s += '|';
-  s += js::num_str(t.end_ms);
-  s += '|';
-  s += js::num_str(t.elapsed);
-  s += '|';
-  s += t.toplevel ? 'Y' : 'N';
-  return s;
-}
+// tx lines are formatted by the join workers (join.cpp JoinShard::output).
 
 inline std::string st_line(int64_t ts, const std::string& server, const std::string& service, const WinStat& w) {
   std::string s = "st|" + std::to_string(ts) + "|" + server + "|" + service + "|";

@@ -143,7 +143,7 @@ int32_t JoinShard::raw_service(std::string_view raw) {
   auto it = raw_svc_map_.find(h);
   if (it != raw_svc_map_.end() && raw_svc_[it->second].raw == raw) return it->second;
   const std::string norm = normalize_service(raw);
-  RawService r{std::string(raw), dict_->service_id(norm), norm.size() >= 2 && norm[0] == 'S' && norm[1] == ':'};
+  RawService r{std::string(raw), norm, dict_->service_id(norm), norm.size() >= 2 && norm[0] == 'S' && norm[1] == ':'};
   raw_svc_.push_back(std::move(r));
   const int32_t id = (int32_t)raw_svc_.size() - 1;
   if (it == raw_svc_map_.end()) raw_svc_map_.emplace(h, id);
@@ -153,6 +153,7 @@ int32_t JoinShard::raw_service(std::string_view raw) {
 // ----------------------------------------------------------------------------- clock / caches
 
 void JoinShard::begin_batch(double now_ms, uint64_t batch_no) {
+  text_.clear();
   now_ = now_ms;
   batch_no_ = batch_no;
   sweep();
@@ -228,17 +229,34 @@ void JoinShard::output(int32_t server, int32_t svc, std::string_view log_id, dou
   t.server = server;
   const RawService& rs = raw_svc_[svc];
   t.service = rs.norm_id;
-  t.log_id.assign(log_id);
-  t.acct = acct;
   double s = start_empty ? js::nan() : start_ms;
   const double e_for_sub = end_empty ? 0.0 : end_ms;  // JS: '' - n === -n
   if (!(s == s) || s == 0) s = e_for_sub - elapsed;
   // TxEntry parseInt's numbers through their string form: integral values pass unchanged
-  t.start_ms = std::isfinite(s) ? std::trunc(s) : js::nan();
+  const double start = std::isfinite(s) ? std::trunc(s) : js::nan();
   t.end_ms = end_empty ? js::nan() : (std::isfinite(end_ms) ? std::trunc(end_ms) : js::nan());
   t.elapsed = elapsed;
   t.to_db = to_db;
   t.toplevel = rs.toplevel;
+  // wire line, formatted here on the join worker (parallel across shards)
+  t.line_off = (uint32_t)text_.size();
+  text_ += "tx|";
+  text_ += (*servers_)[server];
+  text_ += '|';
+  text_ += rs.norm;
+  text_ += '|';
+  text_ += log_id;
+  text_ += '|';
+  js::append_num(text_, acct);
+  text_ += '|';
+  js::append_num(text_, start);
+  text_ += '|';
+  js::append_num(text_, t.end_ms);
+  text_ += '|';
+  js::append_num(text_, elapsed);
+  text_ += '|';
+  text_ += rs.toplevel ? 'Y' : 'N';
+  t.line_len = (uint32_t)(text_.size() - t.line_off);
   ++counters.tx;
   if (to_db) ++counters.tx_db;
 }

@@ -34,13 +34,12 @@ namespace apm {
 
 struct TxOut {
   uint64_t seq;          // merge key: line emissions (1<<63)|(line<<12)|sub; expiries creation<<12|sub
-  int32_t server;        // server id
+  int32_t server;        // server id (== shard index: the line lives in that shard's text arena)
   int32_t service;       // normalized service id
-  std::string log_id;
-  double acct;           // parseInt(acctNum)      (NaN prints "NaN")
-  double start_ms;       // startTs as TxEntry holds it (parseInt of startMs)
   double end_ms;         // endTs (NaN when '')
   double elapsed;        // parseInt(elapsed)
+  uint32_t line_off;     // wire-format tx line (entries.js:16-21, no newline) in the shard arena
+  uint32_t line_len;
   bool to_db;            // insertToDb (audit non-Provider records)
   bool toplevel;         // service matches /^S:/
 };
@@ -88,8 +87,9 @@ struct JoinCounters {
 
 class JoinShard {
  public:
-  JoinShard(const JoinConfig& cfg, Dictionary* dict, const std::vector<FileInfo>* files)
-      : cfg_(cfg), dict_(dict), files_(files) {
+  JoinShard(const JoinConfig& cfg, Dictionary* dict, const std::vector<FileInfo>* files,
+            const std::vector<std::string>* servers)
+      : cfg_(cfg), dict_(dict), files_(files), servers_(servers) {
     acct_.reserve(1 << 15);
     record_.reserve(1 << 14);
     need_.reserve(1 << 12);
@@ -101,6 +101,8 @@ class JoinShard {
   void process(const Event* ev, size_t n, const uint8_t* bytes, const std::vector<int32_t>& chunk_file);
 
   std::vector<TxOut>& out() { return out_; }
+  // Formatted tx lines of this batch (TxOut::line_off/len index into it); cleared by begin_batch.
+  std::string& text() { return text_; }
   JoinCounters counters;
 
   size_t n_partial_logids() const { return record_.size(); }
@@ -131,7 +133,7 @@ class JoinShard {
     bool elapsed_flag = false, sw_flag = false;
     std::vector<std::pair<std::string, std::deque<AuditItem>>> service_map;
   };
-  struct RawService { std::string raw; int32_t norm_id; bool toplevel; };
+  struct RawService { std::string raw; std::string norm; int32_t norm_id; bool toplevel; };
 
   static uint64_t key_of(std::string_view s) { return fnv1a64((const uint8_t*)s.data(), (int)s.size()); }
   int32_t raw_service(std::string_view raw);
@@ -153,6 +155,8 @@ class JoinShard {
   JoinConfig cfg_;
   Dictionary* dict_;
   const std::vector<FileInfo>* files_;
+  const std::vector<std::string>* servers_;
+  std::string text_;
   double now_ = 0;
   uint64_t batch_no_ = 0;
   uint64_t cur_line_ = 0;

@@ -259,6 +259,20 @@ inline std::string to_fixed(double x, int f) {
   return (neg ? "-" : "") + digits;
 }
 
+// Append String(x): integral values below 2^53 take a digit loop, everything else num_str.
+inline void append_num(std::string& out, double x) {
+  if (x == x && x == std::trunc(x) && std::fabs(x) < 9007199254740992.0 && !(x == 0 && std::signbit(x))) {
+    char buf[24];
+    int n = 0;
+    uint64_t v = (uint64_t)std::fabs(x);
+    do { buf[n++] = (char)('0' + v % 10); v /= 10; } while (v);
+    if (x < 0) out += '-';
+    while (n) out += buf[--n];
+    return;
+  }
+  out += num_str(x);
+}
+
 // entries.js nf(): undefined for NaN, else toFixed.
 inline std::string nf(double x, int f = 1) { return std::isnan(x) ? "undefined" : to_fixed(x, f); }
 

@@ -23,8 +23,24 @@ from ..utils.timeparse import TzOffset
 
 KIND_CODE = {"SOAP": 0, "SERVER": 1, "APP": 2}
 
+# Output streams (engine.h OutKind); the bit index is the position in this tuple.
+OUT_KINDS = ("transactions", "audit_db", "db", "st", "fs", "al")
+# What the reference persists (db_insert queue): released + audit tx, fs, al.  `transactions`
+# and `st` are internal hand-offs that only the AMQP bridge needs.
+DB_OUTPUTS = ("audit_db", "db", "fs", "al")
 
-def engine_config(cfg: Dict[str, Any], device: int = 0, keep_text: bool = False, **kw) -> Dict[str, Any]:
+
+def output_mask(kinds) -> int:
+    m = 0
+    for k in kinds:
+        m |= 1 << OUT_KINDS.index(k)
+    return m
+
+
+def engine_config(cfg: Dict[str, Any], device: int = 0, keep_text: bool = False, outputs=None,
+                  **kw) -> Dict[str, Any]:
+    """Engine settings from the reference config keys + the `gpu` section.  keep_text=True
+    materialises every stream; `outputs` (iterable of OUT_KINDS) selects explicitly."""
     g = cfg.get("gpu", {})
     zc = cfg["streamCalcZScore"]
     ac = cfg["streamProcessAlerts"]
@@ -34,7 +50,7 @@ def engine_config(cfg: Dict[str, Any], device: int = 0, keep_text: bool = False,
     if len(lags) > 4:
         raise ValueError("at most 4 LAG settings are supported per engine")
     suppressed_lags = {int(x) for x in ac.get("suppressedLags", [])}
-    ring = {"float64": 8, "float32": 4}.get(g.get("ringDtype", "float64"), 8)
+    ring = {"float64": 8, "float32": 4, "bfloat16": 2, "bf16": 2}.get(g.get("ringDtype", "float64"), 8)
     tz = TzOffset(g.get("timezone", "local"))
     d = {
         "device": device,
@@ -67,8 +83,7 @@ def engine_config(cfg: Dict[str, Any], device: int = 0, keep_text: bool = False,
         "need_ttl_ms": float(g.get("needTtlSeconds", 30)) * 1000.0,
         "tz_table": tz_table(tz),
         "join_threads": int(g.get("joinThreads", 0)),
-        "keep_text": 1 if keep_text else 0,
-        "keep_tx_records": 1 if keep_text else 0,
+        "outputs": output_mask(OUT_KINDS if keep_text else (outputs or ())),
     }
     if int(sc["intervalLengthInSeconds"]) != 10:
         raise ValueError("intervalLengthInSeconds must be 10 (bucket label = endTs without 4 digits)")
@@ -105,10 +120,10 @@ def service_overrides(cfg: Dict[str, Any]) -> Dict[str, Dict[str, Any]]:
 
 
 class APMEngine:
-    def __init__(self, cfg: Dict[str, Any], device: int = 0, keep_text: bool = False, **kw):
+    def __init__(self, cfg: Dict[str, Any], device: int = 0, keep_text: bool = False, outputs=None, **kw):
         self.cfg = cfg
         self.N = _native.load()
-        self.ecfg = engine_config(cfg, device, keep_text, **kw)
+        self.ecfg = engine_config(cfg, device, keep_text, outputs, **kw)
         self.eng = self.N.Engine(self.ecfg)
         self.file_ids: Dict[str, int] = {}
         self.apply_overrides(cfg)
@@ -152,6 +167,9 @@ class APMEngine:
 
     def take(self, kind: str) -> List[str]:
         return self.eng.take(kind)
+
+    def take_bytes(self, kind: str) -> bytes:
+        return self.eng.take_bytes(kind)
 
     def metrics(self) -> Dict[str, Any]:
         m = self.eng.metrics()

@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--ring", default="float64", choices=["float64", "float32"])
     ap.add_argument("--gen-threads", type=int, default=16)
     ap.add_argument("--no-warm", action="store_true")
+    ap.add_argument("--sink", default="/dev/null", help="file receiving the db_insert stream")
     args = ap.parse_args()
 
     import torch
@@ -80,7 +81,13 @@ def main():
         "ringDtype": args.ring,
         "bucketCellCapacity": 16,
     })
-    eng = APMEngine(cfg, device=local, keep_text=False)
+    # Materialise exactly what the reference hands to its db_insert stage (released + audit tx,
+    # fs, al) in the wire format and write it to a sink (/dev/null: the DB loader is out of scope).
+    from apmbackend_amd.models.pipeline import DB_OUTPUTS
+    eng = APMEngine(cfg, device=local, outputs=DB_OUTPUTS)
+    sink_fd = os.open(args.sink, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    for k in DB_OUTPUTS:
+        eng.eng.set_sink_fd(k, sink_fd)
     gen = N.SynthGen({"servers": args.servers, "ejb_services": args.ejb, "provider_services": args.providers,
                       "tx_per_sec_per_server": args.tx_rate, "seed": 1 + rank,
                       "server_offset": rank * args.servers})
@@ -138,6 +145,7 @@ def main():
     dt = time.perf_counter() - t0
     m1 = eng.metrics()
     lines = m1["lines"] - m0["lines"]
+    out_bytes = {k: eng.eng.sink_bytes(k) for k in DB_OUTPUTS}
     lat = sorted(m1["rollover_latency_ms"][len(m0["rollover_latency_ms"]):]) or [float("nan")]
     p50 = lat[len(lat) // 2]
     stats = torch.tensor([float(lines), dt, p50, float(m1["tx"] - m0["tx"]),
@@ -182,12 +190,14 @@ def main():
             "stage_ms_per_step": {k: round((m1[k] - m0[k]) / args.steps, 3)
                                   for k in ("t_parse_ms", "t_join_ms", "t_stats_ms")},
             "corpus_gen_s": round(t_gen, 2),
+            "db_insert_bytes_total": out_bytes,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
     N.free_pinned(pinned)
+    os.close(sink_fd)
 
 
 if __name__ == "__main__":

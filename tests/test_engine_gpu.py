@@ -102,14 +102,59 @@ def test_pipeline_matches_oracle_exact():
     assert m["rollovers"] > 50 and m["join"]["host_fallback"] == 0
 
 
-def test_rolling_mode_matches_exact_decisions():
+def _al_decisions(al):
+    # al|alertTs|entryTs|server|service|causes|<embedded fs>: the embedded fs carries printed
+    # means, which may differ by one ulp-tie between mean modes
+    return [l.split("|")[:6] for l in al]
+
+
+def _fs_means(fs):
+    out = []
+    for l in fs:
+        f = l.split("|")
+        out.append([float(v) if v not in ("undefined", "NaN") else float("nan")
+                    for part in f[6:9] for v in part.split(":")[1:4]])
+    return np.array(out)
+
+
+def _fs_signals(fs):
+    return np.array([[float(part.split(":")[4]) for part in l.split("|")[6:9]] for l in fs])
+
+
+@pytest.mark.parametrize("resync", [360, 4])
+def test_rolling_mode_matches_exact_decisions(resync):
     lines, bl = synth_batches(2)
     _, ex = _run_engine(small_cfg("exact"), bl)
-    _, ro = _run_engine(small_cfg("rolling"), bl)
-    assert ex["al"] == ro["al"]
+    C = small_cfg("rolling")
+    C["gpu"]["exactRecomputeEveryIntervals"] = resync
+    _, ro = _run_engine(C, bl)
+    assert _al_decisions(ex["al"]) == _al_decisions(ro["al"])
     assert len(ex["fs"]) == len(ro["fs"])
-    diff = sum(a != b for a, b in zip(ex["fs"], ro["fs"]))
-    assert diff <= max(2, len(ex["fs"]) // 1000)  # only 1-ulp ties may print differently
+    # The rolling sum differs from the JS left-to-right sum by a few ulps, so a mean that is an
+    # exact decimal tie (common: LAG-6 means of 1-dp values are k/60) may print the other way;
+    # signals can only flip when |x - mean| == T*sigma to the ulp.
+    sig_a, sig_b = _fs_signals(ex["fs"]), _fs_signals(ro["fs"])
+    assert (sig_a != sig_b).sum() <= max(2, sig_a.size // 2000)
+    a, b = _fs_means(ex["fs"]), _fs_means(ro["fs"])
+    np.testing.assert_allclose(a, b, rtol=0, atol=0.1001, equal_nan=True)  # tie printed either way
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_reduced_ring_dtype_runs_and_tracks(dtype):
+    lines, bl = synth_batches(5)
+    _, ex = _run_engine(small_cfg("exact"), bl)
+    C = small_cfg("rolling")
+    C["gpu"]["ringDtype"] = dtype
+    C["gpu"]["exactRecomputeEveryIntervals"] = 8
+    _, ro = _run_engine(C, bl)
+    assert len(ex["fs"]) == len(ro["fs"]) and len(ex["st"]) == len(ro["st"])
+    assert ex["st"] == ro["st"]  # window stats do not depend on the ring dtype
+    a, b = _fs_means(ex["fs"]), _fs_means(ro["fs"])
+    ok = ~np.isnan(a)
+    assert np.array_equal(ok, ~np.isnan(b))
+    # printed at 1 dp: a decimal tie can flip by 0.1 on top of the storage rounding
+    tol = 0.1001 + (1e-5 if dtype == "float32" else 1e-2) * np.abs(a[ok])
+    assert np.all(np.abs(a[ok] - b[ok]) <= tol)
 
 
 def test_native_fleet_exchange_single_rank():
@@ -130,3 +175,18 @@ def test_native_fleet_exchange_single_rank():
     want = buf.cpu().numpy()
     assert got.sum() > 0
     np.testing.assert_allclose(got, want, rtol=0, atol=0)
+
+
+def test_gpu_to_fixed_matches_host():
+    """K12 number printer (device) == js::to_fixed (host, verified against node) incl. ties."""
+    N = _native.load()
+    rng = np.random.default_rng(7)
+    xs = list(rng.uniform(-1e6, 1e6, 4000)) + list(rng.uniform(0, 10, 2000))
+    xs += [k / 20.0 for k in range(-400, 400)] + [k / 200.0 for k in range(-400, 400)]  # x.x5 / x.xx5 ties
+    xs += [k / 60.0 for k in range(0, 3000)] + [0.0, -0.0, 1e-9, -1e-9, 0.05, 0.15, 1.005, 2.675, 1e12 + 0.05]
+    xs += [float("nan")]
+    for f in (1, 2):
+        got = N.gpu_to_fixed(xs, f)
+        want = ["undefined" if x != x else N.js_to_fixed(x, f) for x in xs]
+        bad = [(x, g, w) for x, g, w in zip(xs, got, want) if g != w]
+        assert not bad, bad[:5]

@@ -24,7 +24,7 @@ for s in $STEPS; do
       timeout -k 10 "${T_BENCH:-420}" python bench.py ${BENCH_ARGS:---steps 10 --warmup 3} > gpurun_out/bench.log 2>&1
       rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.log; stop_on_fault $rc bench ;;
     prof)
-      timeout -k 10 "${T_PROF:-420}" rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py ${PROF_ARGS:---steps 5 --warmup 2} > gpurun_out/prof.log 2>&1
+      timeout -k 10 "${T_PROF:-420}" rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py ${PROF_ARGS:---steps 5 --warmup 2} > gpurun_out/prof.log 2>&1
       rc=$?; echo "prof rc=$rc"; tail -3 gpurun_out/prof.log; stop_on_fault $rc prof ;;
   esac
 done
