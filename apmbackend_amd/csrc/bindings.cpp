@@ -126,6 +126,9 @@ py::dict metrics_dict(const EngineMetrics& m) {
   d["batches"] = m.batches; d["bytes"] = m.bytes; d["lines"] = m.lines; d["events"] = m.events;
   d["tx"] = m.tx; d["tx_db"] = m.tx_db; d["tx_dropped"] = m.tx_dropped; d["rollovers"] = m.rollovers;
   d["alerts"] = m.alerts; d["alert_candidates"] = m.alert_candidates; d["released"] = m.released;
+  d["t_join_shards_ms"] = m.t_join_shards_ms; d["t_merge_ms"] = m.t_merge_ms;
+  d["t_stats_tx_ms"] = m.t_stats_tx_ms; d["t_rollover_ms"] = m.t_rollover_ms;
+  d["t_format_ms"] = m.t_format_ms; d["t_release_ms"] = m.t_release_ms;
   d["formatted_bytes"] = m.formatted_bytes; d["format_fallbacks"] = m.format_fallbacks;
   d["t_parse_ms"] = m.t_parse_ms; d["t_join_ms"] = m.t_join_ms; d["t_stats_ms"] = m.t_stats_ms;
   d["t_total_ms"] = m.t_total_ms;
@@ -314,6 +317,38 @@ PYBIND11_MODULE(_apm_native, m) {
   m.def("memcpy_to", [](uintptr_t dst, py::bytes b, uint64_t off) {
     std::string_view v = b;
     std::memcpy((char*)dst + off, v.data(), v.size());
+  });
+  m.def("flatmap_selftest", [](int n_ops, uint64_t seed, int key_space) {
+    // randomized FlatMap / SmallVec vs std containers (CPU test of the join's data structures)
+    FlatMap<int64_t> fm(16);
+    std::unordered_map<uint64_t, int64_t> ref;
+    uint64_t x = seed | 1;
+    auto rnd = [&]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
+    for (int i = 0; i < n_ops; ++i) {
+      const uint64_t k = 1 + rnd() % (uint64_t)key_space;
+      const int op = (int)(rnd() % 3);
+      if (op == 0) { fm[k] = (int64_t)i; ref[k] = i; }
+      else if (op == 1) { if (fm.erase(k) != (ref.erase(k) == 1)) return false; }
+      else {
+        int64_t* v = fm.find(k);
+        auto it = ref.find(k);
+        if ((v != nullptr) != (it != ref.end())) return false;
+        if (v && *v != it->second) return false;
+      }
+      if (fm.size() != ref.size()) return false;
+    }
+    SmallVec<int, 2> sv;
+    std::vector<int> rv;
+    for (int i = 0; i < 2000; ++i) {
+      if (rnd() % 3 || rv.empty()) { sv.push_back(i); rv.push_back(i); }
+      else {
+        const size_t j = rnd() % rv.size();
+        sv.erase(sv.begin() + j);
+        rv.erase(rv.begin() + j);
+      }
+      if (sv.size() != rv.size() || !std::equal(rv.begin(), rv.end(), sv.begin())) return false;
+    }
+    return true;
   });
   m.def("gpu_to_fixed", [](const std::vector<double>& xs, int f) {
     // K12 number printer on the device (test hook): nf(x, f) per value

@@ -284,12 +284,12 @@ void Engine::compute_series_settings(int32_t s, double* thr, double* infl, doubl
 }
 
 int32_t Engine::series_for(int32_t server, int32_t service) {
-  const uint64_t key = ((uint64_t)(uint32_t)server << 32) | (uint32_t)service;
-  auto it = series_map_.find(key);
-  if (it != series_map_.end()) return it->second;
+  const uint64_t key = ((uint64_t)(uint32_t)(server + 1) << 32) | (uint32_t)service;  // never 0 (FlatMap)
+  int32_t* slot = series_map_.find(key);
+  if (slot) return *slot - 1;
   if (n_series_ >= cfg_.max_series) return -1;
   const int32_t s = n_series_++;
-  series_map_[key] = s;
+  series_map_[key] = s + 1;
   if (server_rank_[server] < 0) server_rank_[server] = next_server_rank_++;
   const uint64_t ek = ((uint64_t)server_rank_[server] << 24) | (uint64_t)(server_next_service_[server]++);
   series_.push_back(SeriesInfo{server, service, ek});
@@ -478,27 +478,52 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
     const auto r = shard_range[s];
     if (r.second > r.first) sh.process(h_events_ + r.first, r.second - r.first, hb, chunk_file);
   });
-  // merge shard outputs by (expiry-before-lines, key)
+  const double t1b = now_ms();
+  metrics_.t_join_shards_ms += t1b - t1;
+  // Merge the shard outputs into the reference's single-stream order.  Cache-expiry emissions
+  // (seq bit 63 clear, keyed by creation) precede every line emission and may interleave across
+  // shards: k-way merge (rare).  Line emissions are keyed by the global line index, and each
+  // shard's lines form one contiguous range (chunks are grouped by server), so those parts are
+  // concatenated in range order.
   std::vector<TxOut> txs;
   {
+    const int ns = (int)shards_.size();
     size_t total = 0;
-    for (auto& sh : shards_) total += sh->out().size();
+    std::vector<size_t> split(ns, 0);
+    for (int k = 0; k < ns; ++k) {
+      auto& v = shards_[k]->out();
+      total += v.size();
+      size_t p = 0;
+      while (p < v.size() && !(v[p].seq >> 63)) ++p;
+      split[k] = p;
+    }
     txs.reserve(total);
     using Item = std::pair<uint64_t, std::pair<int, size_t>>;
     std::priority_queue<Item, std::vector<Item>, std::greater<Item>> pq;
-    for (int s = 0; s < (int)shards_.size(); ++s)
-      if (!shards_[s]->out().empty()) pq.push({shards_[s]->out()[0].seq, {s, 0}});
+    for (int k = 0; k < ns; ++k)
+      if (split[k] > 0) pq.push({shards_[k]->out()[0].seq, {k, 0}});
     while (!pq.empty()) {
       auto it = pq.top();
       pq.pop();
       auto& v = shards_[it.second.first]->out();
-      txs.push_back(std::move(v[it.second.second]));
+      txs.push_back(v[it.second.second]);
       const size_t nx = it.second.second + 1;
-      if (nx < v.size()) pq.push({v[nx].seq, {it.second.first, nx}});
+      if (nx < split[it.second.first]) pq.push({v[nx].seq, {it.second.first, nx}});
+    }
+    std::vector<int> order;
+    for (int k = 0; k < ns; ++k)
+      if (split[k] < shards_[k]->out().size()) order.push_back(k);
+    std::sort(order.begin(), order.end(), [&](int a, int b) {
+      return shards_[a]->out()[split[a]].seq < shards_[b]->out()[split[b]].seq;
+    });
+    for (int k : order) {
+      auto& v = shards_[k]->out();
+      txs.insert(txs.end(), v.begin() + split[k], v.end());
     }
   }
   const double t2 = now_ms();
   metrics_.t_join_ms += t2 - t1;
+  metrics_.t_merge_ms += t2 - t1b;
 
   // ---- stats / z-score / alerts: handed to the stats thread, overlapping the next batch's
   // H2D + parse (parse stream) and host join (pool) with this batch's GPU stats work.
@@ -580,6 +605,7 @@ void Engine::ensure_bucket_slot(int64_t b) {
 }
 
 void Engine::stats_for_batch(std::vector<TxOut>& txs, double batch_t0) {
+  const double ts0 = now_ms();
   const int64_t latest_at_start = latest_;
   const bool w_tx = want(OUT_TRANSACTIONS), w_audit = want(OUT_AUDIT_DB), w_db = want(OUT_DB);
   const std::vector<std::string>& text = *cur_text_;
@@ -640,6 +666,7 @@ void Engine::stats_for_batch(std::vector<TxOut>& txs, double batch_t0) {
   for (auto it = pool_exact_edge_.begin(); it != pool_exact_edge_.end();) {
     if (it->second == 0) it = pool_exact_edge_.erase(it); else ++it;
   }
+  metrics_.t_stats_tx_ms += now_ms() - ts0;
   if (n == 0) return;
   HIP_OK(hipMemcpyAsync(d_tx_, h_tx_, (size_t)n * sizeof(TxRec), hipMemcpyHostToDevice, stream_));
   HIP_OK(hipMemcpyAsync(d_gid_, h_gid_, (size_t)n * 8, hipMemcpyHostToDevice, stream_));
@@ -690,6 +717,7 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
     }
   }
   const int64_t edge_ts = (L - cfg_.buffer - 1) * 10000;
+  const double tr0 = now_ms();
   // ---- K9 release: merge the sorted pool with the sorted tail, hand out endTs <= edge
   {
     int64_t released = 0;
@@ -747,6 +775,8 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
     pool_n_ -= released;
     // the remaining pool now starts at pool_off_ inside the current buffer
   }
+  const double tr1 = now_ms();
+  metrics_.t_release_ms += tr1 - tr0;
   // ---- first st for newly visible series: resolve their z-score settings in emission order
   {
     std::vector<int32_t> fresh;
@@ -812,9 +842,12 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   ++rollover_idx_;
   HIP_OK(hipMemcpyAsync(h_n_alerts_, d_n_alerts_, 4, hipMemcpyDeviceToHost, stream_));
   HIP_OK(hipStreamSynchronize(stream_));
-  metrics_.rollover_latency_ms.push_back(now_ms() - batch_t0);
+  const double tr2 = now_ms();
+  metrics_.t_rollover_ms += tr2 - tr1;
+  metrics_.rollover_latency_ms.push_back(tr2 - batch_t0);
   if (want(OUT_ST) || want(OUT_FS)) format_rollover_text(edge_ts);
   flush_alerts(edge_ts);
+  metrics_.t_format_ms += now_ms() - tr2;
 }
 
 void Engine::flush_alerts(int64_t edge_ts) {

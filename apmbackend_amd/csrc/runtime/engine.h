@@ -103,6 +103,8 @@ struct EngineMetrics {
   uint64_t rollovers = 0, alerts = 0, alert_candidates = 0, series = 0, released = 0;
   uint64_t formatted_bytes = 0, format_fallbacks = 0;
   double t_parse_ms = 0, t_join_ms = 0, t_stats_ms = 0, t_total_ms = 0;
+  double t_join_shards_ms = 0, t_merge_ms = 0;                 // split of t_join_ms
+  double t_stats_tx_ms = 0, t_rollover_ms = 0, t_format_ms = 0, t_release_ms = 0;  // inside t_stats_ms
   std::vector<double> rollover_latency_ms;   // batch arrival -> alert decision per rollover
 };
 
@@ -237,7 +239,7 @@ class Engine {
   std::unique_ptr<ThreadPool> pool_;
 
   // series
-  std::unordered_map<uint64_t, int32_t> series_map_;
+  FlatMap<int32_t> series_map_{1 << 16};  // ((server + 1) << 32 | service) -> series + 1
   std::vector<SeriesInfo> series_;
   int32_t n_series_ = 0;
   std::vector<int32_t> server_rank_;            // first-appearance rank per server in the stats stream

@@ -5,6 +5,12 @@
 
 #include <algorithm>
 #include <cctype>
+#ifdef APM_JOIN_PROF
+#include <x86intrin.h>
+#include <cstdio>
+uint64_t prof_cyc[16], prof_n[16];
+struct ProfDump { ~ProfDump() { for (int i = 0; i < 16; ++i) if (prof_n[i]) fprintf(stderr, "kind %d: n=%lu avg=%.0f cyc\n", i, prof_n[i], (double)prof_cyc[i] / prof_n[i]); } } prof_dump;
+#endif
 
 namespace apm {
 
@@ -138,15 +144,22 @@ int32_t Dictionary::service_id(std::string_view normalized) {
   return id;
 }
 
-int32_t JoinShard::raw_service(std::string_view raw) {
-  const uint64_t h = key_of(raw);
-  auto it = raw_svc_map_.find(h);
-  if (it != raw_svc_map_.end() && raw_svc_[it->second].raw == raw) return it->second;
+int32_t JoinShard::raw_service(std::string_view prefix, std::string_view name) {
+  const uint64_t h = fnv1a64((const uint8_t*)name.data(), (int)name.size(),
+                             fnv1a64((const uint8_t*)prefix.data(), (int)prefix.size()));
+  int32_t* slot = raw_svc_map_.find(h);
+  if (slot) {
+    const std::string& r = raw_svc_[*slot - 1].raw;
+    if (r.size() == prefix.size() + name.size() && r.compare(0, prefix.size(), prefix) == 0 &&
+        r.compare(prefix.size(), name.size(), name) == 0)
+      return *slot - 1;
+  }
+  std::string raw(prefix);
+  raw += name;
   const std::string norm = normalize_service(raw);
-  RawService r{std::string(raw), norm, dict_->service_id(norm), norm.size() >= 2 && norm[0] == 'S' && norm[1] == ':'};
-  raw_svc_.push_back(std::move(r));
-  const int32_t id = (int32_t)raw_svc_.size() - 1;
-  if (it == raw_svc_map_.end()) raw_svc_map_.emplace(h, id);
+  const int32_t id = (int32_t)raw_svc_.size();
+  raw_svc_.push_back(RawService{raw, norm, dict_->service_id(norm), norm.size() >= 2 && norm[0] == 'S' && norm[1] == ':'});
+  if (!slot) raw_svc_map_[h] = id + 1;  // a colliding name is re-interned on every call (correct, slow)
   return id;
 }
 
@@ -160,25 +173,24 @@ void JoinShard::begin_batch(double now_ms, uint64_t batch_no) {
 }
 
 JoinShard::NeedEntry& JoinShard::need_map(uint64_t key, std::string_view log_id) {
-  auto it = need_.find(key);
-  if (it == need_.end()) {
-    NeedEntry ne;
+  auto r = need_.emplace(key);
+  NeedEntry& ne = *r.first;
+  if (r.second) {
     ne.exp = now_ + cfg_.need_ttl_ms;
     ne.created = (batch_no_ << 28) | (cur_line_ & 0xfffffff);
     ne.log_id.assign(log_id);
-    it = need_.emplace(key, std::move(ne)).first;
-    need_fifo_.emplace_back(key, it->second.exp);
+    need_fifo_.emplace_back(key, ne.exp);
   }
-  return it->second;
+  return ne;
 }
 
 JoinShard::RecordEntry& JoinShard::record_map(uint64_t key) {
-  auto it = record_.find(key);
-  if (it == record_.end()) {
-    it = record_.emplace(key, RecordEntry{now_ + cfg_.record_ttl_ms, {}}).first;
-    record_fifo_.emplace_back(key, it->second.exp);
+  auto r = record_.emplace(key);
+  if (r.second) {
+    r.first->exp = now_ + cfg_.record_ttl_ms;
+    record_fifo_.emplace_back(key, r.first->exp);
   }
-  return it->second;
+  return *r.first;
 }
 
 void JoinShard::sweep() {
@@ -186,10 +198,10 @@ void JoinShard::sweep() {
   while (!record_fifo_.empty() && record_fifo_.front().second < now_) {
     auto k = record_fifo_.front();
     record_fifo_.pop_front();
-    auto it = record_.find(k.first);
-    if (it == record_.end() || it->second.exp != k.second) continue;
-    counters.expired_partials += it->second.items.size();
-    record_.erase(it);
+    RecordEntry* it = record_.find(k.first);
+    if (!it || it->exp != k.second) continue;
+    counters.expired_partials += it->items.size();
+    record_.erase(k.first);
   }
   // needNumRecordCache: expiry emits every parked record with altAcctNum or '' (:226-239).
   // Creation order == expiry order (the clock never goes back): the FIFO is NodeCache's
@@ -197,17 +209,17 @@ void JoinShard::sweep() {
   while (!need_fifo_.empty() && need_fifo_.front().second < now_) {
     auto k = need_fifo_.front();
     need_fifo_.pop_front();
-    auto it = need_.find(k.first);
-    if (it == need_.end() || it->second.exp != k.second) continue;
-    NeedEntry ne = std::move(it->second);
-    need_.erase(it);
+    NeedEntry* it = need_.find(k.first);
+    if (!it || it->exp != k.second) continue;
+    NeedEntry ne = std::move(*it);
+    need_.erase(k.first);
     expire_need(ne);
   }
   while (!acct_fifo_.empty() && acct_fifo_.front().second < now_) {
     auto k = acct_fifo_.front();
     acct_fifo_.pop_front();
-    auto it = acct_.find(k.first);
-    if (it != acct_.end() && it->second.exp == k.second) acct_.erase(it);
+    AcctEntry* it = acct_.find(k.first);
+    if (it && it->exp == k.second) acct_.erase(k.first);
   }
 }
 
@@ -286,11 +298,11 @@ void JoinShard::save_acct(std::string_view acct_raw, int32_t file, int source, s
   ae.exp = now_ + cfg_.acct_ttl_ms;
   acct_fifo_.emplace_back(key, ae.exp);
   if (source != 2) soap_.erase(file);
-  auto nit = need_.find(key);
-  if (nit != need_.end() && !nit->second.items.empty()) {
+  NeedEntry* nit = need_.find(key);
+  if (nit && !nit->items.empty()) {
     const int32_t server = (*files_)[file].server;
     std::vector<Need> items;
-    items.swap(nit->second.items);  // the (now empty) map stays until it expires
+    items.swap(nit->items);  // the (now empty) map stays until it expires
     for (auto& r : items)
       output(server, r.svc, log_id, a, r.start_ms, r.start_empty, r.end_ms, r.end_empty, r.elapsed, false, seq);
   }
@@ -362,12 +374,10 @@ void JoinShard::on_ejb(const Event& e, std::string_view line, int32_t file, bool
     std::string tsstr = std::string(tk.get(1)) + " " + std::string(tk.get(2));
     if (!js::convert_date(tsstr, cfg_.tz, ts)) { ts_empty = true; ts = js::nan(); }
   }
-  std::string svc_buf = "S:";
   if (entry) {  // parseEjbCommonTimingEntry (:378-401)
     if (log_id.empty()) return;
-    if (host) svc_buf += std::string(tk.get(13));
-    else svc_buf += e.tAs != 0xffff ? std::string(line.substr(e.tAs, e.tAe - e.tAs)) : std::string(kUndef);
-    const int32_t svc = raw_service(svc_buf);
+    const std::string_view nm = host ? tk.get(13) : (e.tAs != 0xffff ? line.substr(e.tAs, e.tAe - e.tAs) : kUndef);
+    const int32_t svc = raw_service("S:", nm);
     auto& items = record_map(key_of(log_id)).items;
     auto f = std::find_if(items.begin(), items.end(), [&](const Partial& p) { return p.svc == svc; });
     if (f != items.end()) { f->server = server; f->start_ms = ts; f->start_empty = ts_empty; }
@@ -376,29 +386,30 @@ void JoinShard::on_ejb(const Event& e, std::string_view line, int32_t file, bool
   }
   // parseEjbCommonTimingExit (:403-446)
   double elapsed;
+  std::string_view nm;
   if (host) {
-    svc_buf += std::string(tk.get(9));
+    nm = tk.get(9);
     elapsed = tk.has(11) ? js::parse_int(tk.t[11]) : js::nan();
   } else {
-    svc_buf += e.tAs != 0xffff ? std::string(line.substr(e.tAs, e.tAe - e.tAs)) : std::string(kUndef);
+    nm = e.tAs != 0xffff ? line.substr(e.tAs, e.tAe - e.tAs) : kUndef;
     elapsed = e.num;
   }
-  const int32_t svc = raw_service(svc_buf);
+  const int32_t svc = raw_service("S:", nm);
   if (log_id.empty()) {
     output(server, svc, "", js::nan(), 0, true, ts, ts_empty, elapsed, false, seq);
     return;
   }
   const uint64_t key = key_of(log_id);
-  auto it = record_.find(key);
-  if (it == record_.end()) { ++counters.ejb_exit_unmatched; return; }
-  auto& items = it->second.items;
+  RecordEntry* it = record_.find(key);
+  if (!it) { ++counters.ejb_exit_unmatched; return; }
+  auto& items = it->items;
   auto f = std::find_if(items.begin(), items.end(), [&](const Partial& p) { return p.svc == svc; });
   if (f == items.end()) { ++counters.ejb_exit_unmatched; return; }
   const Partial part = *f;
   items.erase(f);
-  auto ait = acct_.find(key);
-  if (ait != acct_.end()) {
-    output(server, svc, log_id, ait->second.acct, part.start_ms, part.start_empty, ts, ts_empty, elapsed, false, seq);
+  AcctEntry* ait = acct_.find(key);
+  if (ait) {
+    output(server, svc, log_id, ait->acct, part.start_ms, part.start_empty, ts, ts_empty, elapsed, false, seq);
   } else {
     Need n{svc, part.server, part.start_ms, part.start_empty, ts, ts_empty, elapsed, js::nan(), false};
     auto& ni = need_map(key, log_id).items;
@@ -454,16 +465,16 @@ void JoinShard::on_ct(const Event& e, std::string_view line, int32_t file, bool 
   };
   if (log_id.empty()) { salvage(); return; }
   const uint64_t key = key_of(log_id);
-  auto it = record_.find(key);
-  if (it == record_.end()) { salvage(); return; }
-  auto* items = &it->second.items;
+  RecordEntry* it = record_.find(key);
+  if (!it) { salvage(); return; }
+  auto* items = &it->items;
   auto f = std::find_if(items->begin(), items->end(), [&](const Partial& p) { return p.svc == svc; });
   if (f == items->end()) { salvage(); return; }
   const Partial part = *f;
-  auto ait = acct_.find(key);
-  if (ait != acct_.end()) {
+  AcctEntry* ait = acct_.find(key);
+  if (ait) {
     items->erase(f);
-    output(server, svc, log_id, ait->second.acct, part.start_ms, part.start_empty, ts, ts_empty, elapsed, false, seq);
+    output(server, svc, log_id, ait->acct, part.start_ms, part.start_empty, ts, ts_empty, elapsed, false, seq);
     return;
   }
   need_map(key, log_id);
@@ -474,9 +485,9 @@ void JoinShard::on_ct(const Event& e, std::string_view line, int32_t file, bool 
   auto g = std::find_if(ni.begin(), ni.end(), [&](const Need& x) { return x.svc == svc; });
   if (g != ni.end()) *g = n; else ni.push_back(n);
   // map.delete(service)
-  auto it2 = record_.find(key);
-  if (it2 != record_.end()) {
-    auto& v = it2->second.items;
+  RecordEntry* it2 = record_.find(key);
+  if (it2) {
+    auto& v = it2->items;
     auto f2 = std::find_if(v.begin(), v.end(), [&](const Partial& p) { return p.svc == svc; });
     if (f2 != v.end()) v.erase(f2);
   }
@@ -585,9 +596,9 @@ void JoinShard::on_app(const Event& e, std::string_view line, int32_t file, uint
     const double elapsed = js::parse_int(obj.elapsed);
     const int32_t svc = raw_service(svcname);
     const uint64_t key = key_of(log_id);
-    auto ait = acct_.find(key);
-    if (ait != acct_.end()) {
-      output(server, svc, log_id, ait->second.acct, s_ms, s_empty, e_ms, e_empty, elapsed, to_db, seq);
+    AcctEntry* ait = acct_.find(key);
+    if (ait) {
+      output(server, svc, log_id, ait->acct, s_ms, s_empty, e_ms, e_empty, elapsed, to_db, seq);
     } else {
       const double alt = ctx.active_alt.empty() ? js::nan() : js::parse_int(ctx.active_alt);
       Need n{svc, server, s_ms, s_empty, e_ms, e_empty, elapsed, alt, to_db};
@@ -609,6 +620,9 @@ void JoinShard::process(const Event* ev, size_t n, const uint8_t* bytes, const s
     const uint64_t seq = (1ULL << 51) | e.line;  // << 12 in output(): bit 63 marks line emissions
     cur_line_ = e.line;
     sub_ = 0;
+#ifdef APM_JOIN_PROF
+    const uint64_t t0 = __rdtsc();
+#endif
     switch (e.kind) {
       case LK_SOAP: on_soap(e, line, file, seq); break;
       case LK_EJB_ENTRY: on_ejb(e, line, file, true, seq); break;
@@ -618,6 +632,10 @@ void JoinShard::process(const Event* ev, size_t n, const uint8_t* bytes, const s
       case LK_APP: on_app(e, line, file, seq); break;
       default: break;
     }
+#ifdef APM_JOIN_PROF
+    prof_cyc[e.kind & 15] += __rdtsc() - t0;
+    prof_n[e.kind & 15]++;
+#endif
   }
 }
 

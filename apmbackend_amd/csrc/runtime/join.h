@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "../apm_types.h"
+#include "flatmap.h"
 #include "jsutil.h"
 
 namespace apm {
@@ -89,11 +90,8 @@ class JoinShard {
  public:
   JoinShard(const JoinConfig& cfg, Dictionary* dict, const std::vector<FileInfo>* files,
             const std::vector<std::string>* servers)
-      : cfg_(cfg), dict_(dict), files_(files), servers_(servers) {
-    acct_.reserve(1 << 15);
-    record_.reserve(1 << 14);
-    need_.reserve(1 << 12);
-  }
+      : cfg_(cfg), dict_(dict), files_(files), servers_(servers), acct_(1 << 16), record_(1 << 16), need_(1 << 12),
+        raw_svc_map_(1 << 12) {}
 
   void begin_batch(double now_ms, uint64_t batch_no);
   // Process the events of one batch that belong to this shard. `bytes` is the host copy of the
@@ -120,9 +118,9 @@ class JoinShard {
     double alt_acct;      // parseInt(altAcctNum || '')
     bool insert_to_db;
   };
-  struct AcctEntry { double acct; double exp; };
-  struct RecordEntry { double exp; std::vector<Partial> items; };
-  struct NeedEntry { double exp; uint64_t created; std::string log_id; std::vector<Need> items; };
+  struct AcctEntry { double acct = 0; double exp = 0; };
+  struct RecordEntry { double exp = 0; SmallVec<Partial, 2> items; };
+  struct NeedEntry { double exp = 0; uint64_t created = 0; std::string log_id; std::vector<Need> items; };
   struct SoapCtx { std::string log_id; bool has_log_id = false; bool pull_next = false; };
   struct AuditItem { std::string elapsed; bool has_start = false; std::string start_ts; };
   struct AuditCtx {
@@ -136,7 +134,8 @@ class JoinShard {
   struct RawService { std::string raw; std::string norm; int32_t norm_id; bool toplevel; };
 
   static uint64_t key_of(std::string_view s) { return fnv1a64((const uint8_t*)s.data(), (int)s.size()); }
-  int32_t raw_service(std::string_view raw);
+  int32_t raw_service(std::string_view raw) { return raw_service(std::string_view(), raw); }
+  int32_t raw_service(std::string_view prefix, std::string_view name);  // interned prefix + name
   void sweep();
   void expire_need(NeedEntry& nm);
   NeedEntry& need_map(uint64_t key, std::string_view log_id);
@@ -160,13 +159,13 @@ class JoinShard {
   double now_ = 0;
   uint64_t batch_no_ = 0;
   uint64_t cur_line_ = 0;
-  std::unordered_map<uint64_t, AcctEntry> acct_;
-  std::unordered_map<uint64_t, RecordEntry> record_;
-  std::unordered_map<uint64_t, NeedEntry> need_;
+  FlatMap<AcctEntry> acct_;
+  FlatMap<RecordEntry> record_;
+  FlatMap<NeedEntry> need_;
   std::deque<std::pair<uint64_t, double>> acct_fifo_, record_fifo_, need_fifo_;
   std::unordered_map<int32_t, SoapCtx> soap_;
   std::unordered_map<int32_t, AuditCtx> audit_;
-  std::unordered_map<uint64_t, int32_t> raw_svc_map_;
+  FlatMap<int32_t> raw_svc_map_;  // hash(raw name) -> id + 1
   std::vector<RawService> raw_svc_;
   std::vector<TxOut> out_;
   uint32_t sub_ = 0;

@@ -246,7 +246,7 @@ inline std::string to_fixed(double x, int f) {
   // the ECMA-262 rule "n/10^f - x closest to 0, ties to the larger n" is decided exactly.
   long double scale = 1;
   for (int i = 0; i < f; ++i) scale *= 10;
-  const long double p = (long double)(neg ? -x : x) * scale;
+  const long double p = (long double)std::fabs(x) * scale;  // fabs: (-0).toFixed() is "0.0"
   const long double q = floorl(p);
   const long double n = (p - q) >= 0.5L ? q + 1 : q;
   char buf[64];

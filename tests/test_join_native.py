@@ -67,3 +67,9 @@ def test_js_number_helpers_match_python():
     for s in [" 12ab", "00123", "-7", "abc", "", "5555000011112222", "12345678901234567890", "0x1A"]:
         a, b = N.js_parse_int(s), jsfmt.parse_int(s)
         assert (a != a and b != b) or a == b, s
+
+
+@pytest.mark.parametrize("key_space", [50, 5000, 1 << 20])
+def test_flatmap_and_smallvec_against_std(key_space):
+    N = _native.load()
+    assert N.flatmap_selftest(200000, 12345 + key_space, key_space)
