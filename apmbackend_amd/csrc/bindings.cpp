@@ -256,6 +256,8 @@ PYBIND11_MODULE(_apm_native, m) {
            py::arg("ptr"), py::arg("n"), py::arg("chunks"), py::arg("now") = -1.0)
       .def("take", &Engine::take, py::call_guard<py::gil_scoped_release>())
       .def("flush", &Engine::flush, py::call_guard<py::gil_scoped_release>())
+      .def("save_state", &Engine::save_state, py::call_guard<py::gil_scoped_release>())
+      .def("load_state", &Engine::load_state, py::call_guard<py::gil_scoped_release>())
       .def("take_bytes", [](Engine& e, const std::string& k) {
         std::string b;
         { py::gil_scoped_release rel; b = e.take_bytes(k); }
@@ -274,6 +276,11 @@ PYBIND11_MODULE(_apm_native, m) {
       .def("n_series", &Engine::n_series)
       .def("n_services", &Engine::n_services)
       .def("services", &Engine::services)
+      .def("files", [](Engine& e) {
+        std::vector<std::tuple<std::string, int, std::string>> r;
+        for (auto& f : e.files()) r.emplace_back(f.path, (int)f.kind, e.servers()[f.server]);
+        return r;
+      })
       .def("servers", &Engine::servers)
       .def("watermark", &Engine::watermark)
       .def("device_bytes", &Engine::device_bytes)

@@ -1,0 +1,149 @@
+// Tiny tagged binary writer/reader for checkpoints (little-endian, host byte order).
+//
+// A file is: magic "APMCKPT\0", u32 version, then sections {u32 tag, u64 length, payload}.
+// Readers check every section tag in order, so a layout change fails loudly instead of
+// silently misreading.  Writers go to `<path>.tmp`, fsync, then rename (atomic replace --
+// the reference wrote its resume files in place).
+#pragma once
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+namespace apm {
+
+constexpr uint32_t kCkptVersion = 1;
+
+class BinWriter {
+ public:
+  explicit BinWriter(const std::string& path) : path_(path), tmp_(path + ".tmp") {
+    f_ = std::fopen(tmp_.c_str(), "wb");
+    if (!f_) throw std::runtime_error("checkpoint: cannot open " + tmp_ + ": " + std::strerror(errno));
+    std::setvbuf(f_, nullptr, _IOFBF, 1 << 22);
+    raw("APMCKPT", 8);
+    pod(kCkptVersion);
+  }
+  ~BinWriter() {
+    if (f_) { std::fclose(f_); std::remove(tmp_.c_str()); }
+  }
+  void raw(const void* p, size_t n) {
+    if (n && std::fwrite(p, 1, n, f_) != n) throw std::runtime_error("checkpoint: write failed");
+    bytes_ += n;
+  }
+  template <class T>
+  void pod(const T& v) {
+    static_assert(std::is_trivially_copyable<T>::value, "pod");
+    raw(&v, sizeof(T));
+  }
+  void str(const std::string& s) { pod<uint64_t>(s.size()); raw(s.data(), s.size()); }
+  template <class T>
+  void vec(const std::vector<T>& v) {
+    static_assert(std::is_trivially_copyable<T>::value, "vec");
+    pod<uint64_t>(v.size());
+    raw(v.data(), v.size() * sizeof(T));
+  }
+  void strs(const std::vector<std::string>& v) {
+    pod<uint64_t>(v.size());
+    for (auto& s : v) str(s);
+  }
+  // section framing: the length is patched in when the section ends
+  void begin(uint32_t tag) {
+    pod(tag);
+    std::fflush(f_);
+    sec_pos_ = std::ftell(f_);
+    pod<uint64_t>(0);
+  }
+  void end() {
+    const long here = std::ftell(f_);
+    const uint64_t len = (uint64_t)(here - sec_pos_ - 8);
+    std::fseek(f_, sec_pos_, SEEK_SET);
+    raw(&len, 8);
+    bytes_ -= 8;
+    std::fseek(f_, here, SEEK_SET);
+  }
+  void commit() {
+    pod<uint32_t>(0xE0Fu);  // end marker
+    if (std::fflush(f_) != 0) throw std::runtime_error("checkpoint: flush failed");
+    ::fsync(::fileno(f_));
+    std::fclose(f_);
+    f_ = nullptr;
+    if (std::rename(tmp_.c_str(), path_.c_str()) != 0)
+      throw std::runtime_error("checkpoint: rename failed: " + std::string(std::strerror(errno)));
+  }
+  uint64_t bytes() const { return bytes_; }
+
+ private:
+  std::string path_, tmp_;
+  FILE* f_ = nullptr;
+  long sec_pos_ = 0;
+  uint64_t bytes_ = 0;
+};
+
+class BinReader {
+ public:
+  explicit BinReader(const std::string& path) {
+    f_ = std::fopen(path.c_str(), "rb");
+    if (!f_) throw std::runtime_error("checkpoint: cannot open " + path + ": " + std::strerror(errno));
+    std::setvbuf(f_, nullptr, _IOFBF, 1 << 22);
+    char magic[8];
+    raw(magic, 8);
+    if (std::memcmp(magic, "APMCKPT", 8) != 0) throw std::runtime_error("checkpoint: bad magic");
+    const uint32_t v = pod<uint32_t>();
+    if (v != kCkptVersion) throw std::runtime_error("checkpoint: unsupported version " + std::to_string(v));
+  }
+  ~BinReader() { if (f_) std::fclose(f_); }
+  void raw(void* p, size_t n) {
+    if (n && std::fread(p, 1, n, f_) != n) throw std::runtime_error("checkpoint: truncated file");
+  }
+  template <class T>
+  T pod() {
+    T v;
+    raw(&v, sizeof(T));
+    return v;
+  }
+  template <class T>
+  void pod(T& v) { raw(&v, sizeof(T)); }
+  std::string str() {
+    const uint64_t n = pod<uint64_t>();
+    std::string s(n, '\0');
+    raw(&s[0], n);
+    return s;
+  }
+  template <class T>
+  std::vector<T> vec() {
+    const uint64_t n = pod<uint64_t>();
+    std::vector<T> v(n);
+    raw(v.data(), n * sizeof(T));
+    return v;
+  }
+  std::vector<std::string> strs() {
+    const uint64_t n = pod<uint64_t>();
+    std::vector<std::string> v;
+    v.reserve(n);
+    for (uint64_t i = 0; i < n; ++i) v.push_back(str());
+    return v;
+  }
+  void begin(uint32_t tag) {
+    const uint32_t t = pod<uint32_t>();
+    if (t != tag) throw std::runtime_error("checkpoint: expected section " + std::to_string(tag) + ", found " +
+                                           std::to_string(t));
+    pod<uint64_t>();
+  }
+  void end() {}
+  void finish() {
+    if (pod<uint32_t>() != 0xE0Fu) throw std::runtime_error("checkpoint: missing end marker");
+  }
+
+ private:
+  FILE* f_ = nullptr;
+};
+
+}  // namespace apm

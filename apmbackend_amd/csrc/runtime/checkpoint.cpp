@@ -1,0 +1,517 @@
+// Versioned binary checkpoint of one engine (one GPU / rank): everything needed to resume the
+// pipeline mid-stream with identical output.
+//
+// The reference persists each stage separately as JSON every 60 s and on SIGTERM
+// (stream_calc_stats.js:54-87 buckets + minHeap, stream_calc_z_score.js:37-64 per-lag history
+// lists, stream_process_alerts.js:111-142, stream_insert_db.js:166-180) and loses the parser's
+// join caches and tail positions on every restart.  Here one file holds:
+//   topology (servers, files, service dictionary), series table + settings, log-time clock,
+//   join caches of every shard (acct/record/need TTL caches, SOAP + audit contexts), the GPU
+//   parse carry (open elapsed sections), live bucket cells, the z-score rings + rolling moments
+//   + leaky counters of every LAG, the release pool + pending tx lines, alert cooldowns, and
+//   undelivered output.
+// Only the live part of device arrays is written: n_series columns of each ring row (2-D D2H
+// copies through a pinned bounce buffer), compacted bucket cells.  Tail offsets live with the
+// tailer (Python service writes them next to this file).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "binio.h"
+#include "engine.h"
+
+namespace apm {
+
+namespace {
+
+enum : uint32_t {
+  SEC_CONFIG = 1, SEC_TOPOLOGY, SEC_SERIES, SEC_CLOCK, SEC_JOIN, SEC_PARSE, SEC_BUCKETS, SEC_ZSCORE, SEC_POOL,
+  SEC_ALERTS, SEC_OUTPUTS, SEC_METRICS
+};
+
+struct SeriesRec { int32_t server, service; uint64_t emit_key; };
+struct I64Pair { int64_t a, b; };
+
+// 2-D device <-> file copies of `rows` rows of `width` bytes taken from a pitched device array.
+constexpr size_t kBounce = 64u << 20;
+
+void d2h_rows(BinWriter& w, const void* dev, size_t pitch, size_t width, size_t rows, void* bounce,
+              hipStream_t st) {
+  if (!width || !rows) return;
+  const size_t per = std::max<size_t>(1, kBounce / width);
+  for (size_t r = 0; r < rows; r += per) {
+    const size_t nr = std::min(per, rows - r);
+    HIP_OK(hipMemcpy2DAsync(bounce, width, (const char*)dev + r * pitch, pitch, width, nr, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    w.raw(bounce, width * nr);
+  }
+}
+
+void h2d_rows(BinReader& rd, void* dev, size_t pitch, size_t width, size_t rows, void* bounce, hipStream_t st) {
+  if (!width || !rows) return;
+  const size_t per = std::max<size_t>(1, kBounce / width);
+  for (size_t r = 0; r < rows; r += per) {
+    const size_t nr = std::min(per, rows - r);
+    rd.raw(bounce, width * nr);
+    HIP_OK(hipMemcpy2DAsync((char*)dev + r * pitch, pitch, bounce, width, width, nr, hipMemcpyHostToDevice, st));
+    HIP_OK(hipStreamSynchronize(st));
+  }
+}
+
+template <class T>
+void d2h_vec(BinWriter& w, const T* dev, size_t n, hipStream_t st) {
+  std::vector<T> h(n);
+  if (n) {
+    HIP_OK(hipMemcpyAsync(h.data(), dev, n * sizeof(T), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+  }
+  w.vec(h);
+}
+
+template <class T>
+size_t h2d_vec(BinReader& rd, T* dev, size_t cap, hipStream_t st) {
+  std::vector<T> h = rd.vec<T>();
+  if (h.size() > cap) throw std::runtime_error("checkpoint: array larger than this engine's capacity");
+  if (!h.empty()) {
+    HIP_OK(hipMemcpyAsync(dev, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, st));
+    HIP_OK(hipStreamSynchronize(st));
+  }
+  return h.size();
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------ JoinShard
+
+void JoinShard::save(BinWriter& w) {
+  w.pod(now_);
+  w.pod(batch_no_);
+  w.pod(counters);
+  // raw service interning (order defines the ids)
+  w.pod<uint64_t>(raw_svc_.size());
+  for (auto& r : raw_svc_) { w.str(r.raw); w.str(r.norm); w.pod(r.norm_id); w.pod(r.toplevel); }
+  // TTL caches
+  w.pod<uint64_t>(acct_.size());
+  acct_.for_each([&](uint64_t k, AcctEntry& e) { w.pod(k); w.pod(e); });
+  w.pod<uint64_t>(record_.size());
+  record_.for_each([&](uint64_t k, RecordEntry& e) {
+    w.pod(k);
+    w.pod(e.exp);
+    w.pod<uint64_t>(e.items.size());
+    for (auto& p : e.items) w.pod(p);
+  });
+  w.pod<uint64_t>(need_.size());
+  need_.for_each([&](uint64_t k, NeedEntry& e) {
+    w.pod(k);
+    w.pod(e.exp);
+    w.pod(e.created);
+    w.str(e.log_id);
+    w.vec(e.items);
+  });
+  for (auto* q : {&acct_fifo_, &record_fifo_, &need_fifo_}) {
+    w.pod<uint64_t>(q->size());
+    for (auto& x : *q) { w.pod(x.first); w.pod(x.second); }
+  }
+  // per-file contexts
+  w.pod<uint64_t>(soap_.size());
+  for (auto& kv : soap_) { w.pod(kv.first); w.str(kv.second.log_id); w.pod(kv.second.has_log_id); w.pod(kv.second.pull_next); }
+  w.pod<uint64_t>(audit_.size());
+  for (auto& kv : audit_) {
+    const AuditCtx& c = kv.second;
+    w.pod(kv.first);
+    w.pod<uint64_t>(c.autr_map.size());
+    for (auto& a : c.autr_map) { w.str(a.first); w.str(a.second.first); w.str(a.second.second); }
+    w.pod(c.active); w.str(c.active_log_id); w.str(c.active_alt); w.str(c.active_service);
+    w.pod(c.has_active_service); w.pod(c.elapsed_flag); w.pod(c.sw_flag);
+    w.pod<uint64_t>(c.service_map.size());
+    for (auto& sm : c.service_map) {
+      w.str(sm.first);
+      w.pod<uint64_t>(sm.second.size());
+      for (auto& it : sm.second) { w.str(it.elapsed); w.pod(it.has_start); w.str(it.start_ts); }
+    }
+  }
+}
+
+void JoinShard::load(BinReader& rd) {
+  rd.pod(now_);
+  rd.pod(batch_no_);
+  rd.pod(counters);
+  raw_svc_.clear();
+  raw_svc_map_.clear();
+  const uint64_t nr = rd.pod<uint64_t>();
+  for (uint64_t i = 0; i < nr; ++i) {
+    RawService r;
+    r.raw = rd.str();
+    r.norm = rd.str();
+    rd.pod(r.norm_id);
+    rd.pod(r.toplevel);
+    const uint64_t h = fnv1a64((const uint8_t*)r.raw.data(), (int)r.raw.size());
+    if (!raw_svc_map_.find(h)) raw_svc_map_[h] = (int32_t)i + 1;  // first occurrence wins, as when built
+    raw_svc_.push_back(std::move(r));
+  }
+  acct_.clear();
+  for (uint64_t n = rd.pod<uint64_t>(); n; --n) {
+    const uint64_t k = rd.pod<uint64_t>();
+    acct_[k] = rd.pod<AcctEntry>();
+  }
+  record_.clear();
+  for (uint64_t n = rd.pod<uint64_t>(); n; --n) {
+    const uint64_t k = rd.pod<uint64_t>();
+    RecordEntry& e = record_[k];
+    rd.pod(e.exp);
+    for (uint64_t m = rd.pod<uint64_t>(); m; --m) e.items.push_back(rd.pod<Partial>());
+  }
+  need_.clear();
+  for (uint64_t n = rd.pod<uint64_t>(); n; --n) {
+    const uint64_t k = rd.pod<uint64_t>();
+    NeedEntry& e = need_[k];
+    rd.pod(e.exp);
+    rd.pod(e.created);
+    e.log_id = rd.str();
+    e.items = rd.vec<Need>();
+  }
+  for (auto* q : {&acct_fifo_, &record_fifo_, &need_fifo_}) {
+    q->clear();
+    for (uint64_t n = rd.pod<uint64_t>(); n; --n) {
+      const uint64_t k = rd.pod<uint64_t>();
+      q->push_back({k, rd.pod<double>()});
+    }
+  }
+  soap_.clear();
+  for (uint64_t n = rd.pod<uint64_t>(); n; --n) {
+    const int32_t f = rd.pod<int32_t>();
+    SoapCtx c;
+    c.log_id = rd.str();
+    rd.pod(c.has_log_id);
+    rd.pod(c.pull_next);
+    soap_[f] = std::move(c);
+  }
+  audit_.clear();
+  for (uint64_t n = rd.pod<uint64_t>(); n; --n) {
+    const int32_t f = rd.pod<int32_t>();
+    AuditCtx& c = audit_[f];
+    for (uint64_t m = rd.pod<uint64_t>(); m; --m) {
+      std::string a = rd.str(), b = rd.str(), d = rd.str();
+      c.autr_map.push_back({a, {b, d}});
+    }
+    rd.pod(c.active); c.active_log_id = rd.str(); c.active_alt = rd.str(); c.active_service = rd.str();
+    rd.pod(c.has_active_service); rd.pod(c.elapsed_flag); rd.pod(c.sw_flag);
+    for (uint64_t m = rd.pod<uint64_t>(); m; --m) {
+      std::string name = rd.str();
+      std::deque<AuditItem> items;
+      for (uint64_t j = rd.pod<uint64_t>(); j; --j) {
+        AuditItem it;
+        it.elapsed = rd.str();
+        rd.pod(it.has_start);
+        it.start_ts = rd.str();
+        items.push_back(std::move(it));
+      }
+      c.service_map.push_back({name, std::move(items)});
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ Engine
+
+uint64_t Engine::save_state(const std::string& path) {
+  flush();
+  HIP_OK(hipStreamSynchronize(parse_stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+  HIP_OK(hipStreamSynchronize(comm_stream_));
+  const int32_t S = cfg_.max_series, n = n_series_;
+  void* bounce = nullptr;
+  HIP_OK(hipHostMalloc(&bounce, kBounce, hipHostMallocDefault));
+  struct Guard { void* p; ~Guard() { hipHostFree(p); } } guard{bounce};
+  BinWriter w(path);
+
+  w.begin(SEC_CONFIG);
+  w.pod(cfg_.max_series); w.pod(cfg_.n_lags); w.raw(cfg_.lags, sizeof(cfg_.lags)); w.pod(cfg_.ring_bytes);
+  w.pod(cfg_.cell_cap); w.pod(cfg_.spill_cap); w.pod(cfg_.pool_cap); w.pod(cfg_.window); w.pod(cfg_.buffer);
+  w.end();
+
+  w.begin(SEC_TOPOLOGY);
+  w.strs(servers_);
+  w.pod<uint64_t>(files_.size());
+  for (auto& f : files_) { w.str(f.path); w.pod(f.server); w.pod(f.kind); }
+  w.strs(dict_.services_snapshot());
+  w.end();
+
+  w.begin(SEC_SERIES);
+  {
+    std::vector<SeriesRec> sr(series_.size());
+    for (size_t i = 0; i < series_.size(); ++i) sr[i] = {series_[i].server, series_[i].service, series_[i].emit_key};
+    w.vec(sr);
+  }
+  w.vec(server_rank_); w.vec(server_next_service_); w.pod(next_server_rank_);
+  w.vec(h_thr_); w.vec(h_infl_); w.vec(h_hard_max_); w.vec(h_suppressed_); w.vec(h_emit_key_);
+  w.vec(zscore_seen_); w.vec(h_active_); w.vec(unseen_);
+  w.raw(alias_thr_, sizeof(alias_thr_)); w.raw(alias_infl_, sizeof(alias_infl_));
+  w.end();
+
+  w.begin(SEC_CLOCK);
+  w.pod(watermark_); w.pod(batch_no_); w.pod(latest_); w.pod(rollover_idx_);
+  w.raw(slot_bucket_, sizeof(slot_bucket_));
+  w.pod(next_gid_); w.pod(line_block_seq_);
+  w.end();
+
+  w.begin(SEC_JOIN);
+  w.pod<uint64_t>(shards_.size());
+  for (auto& sh : shards_) sh->save(w);
+  w.end();
+
+  w.begin(SEC_PARSE);
+  d2h_vec(w, d_file_open_, 1 << 16, stream_);
+  w.end();
+
+  w.begin(SEC_BUCKETS);
+  d2h_vec(w, d_active_, (size_t)n, stream_);
+  {
+    std::vector<int32_t> spill_n(NSLOT);
+    HIP_OK(hipMemcpy(spill_n.data(), d_spill_n_, NSLOT * 4, hipMemcpyDeviceToHost));
+    std::vector<int32_t> counts(n), cells((size_t)n * cfg_.cell_cap);
+    for (int slot = 0; slot < NSLOT; ++slot) {
+      if (slot_bucket_[slot] == NO_BUCKET) continue;
+      w.pod<int32_t>(slot);
+      HIP_OK(hipMemcpy(counts.data(), d_counts_cells_ + (size_t)slot * S, (size_t)n * 4, hipMemcpyDeviceToHost));
+      HIP_OK(hipMemcpy(cells.data(), d_cells_ + (size_t)slot * S * cfg_.cell_cap, (size_t)n * cfg_.cell_cap * 4,
+                       hipMemcpyDeviceToHost));
+      w.vec(counts);
+      std::vector<int32_t> packed;  // only the occupied cells
+      for (int32_t s = 0; s < n; ++s)
+        for (int32_t k = 0; k < std::min(counts[s], cfg_.cell_cap); ++k) packed.push_back(cells[(size_t)s * cfg_.cell_cap + k]);
+      w.vec(packed);
+      const int32_t ns = std::min(spill_n[slot], cfg_.spill_cap);
+      w.pod(spill_n[slot]);
+      d2h_vec(w, d_spill_series_ + (size_t)slot * cfg_.spill_cap, (size_t)ns, stream_);
+      d2h_vec(w, d_spill_val_ + (size_t)slot * cfg_.spill_cap, (size_t)ns, stream_);
+    }
+    w.pod<int32_t>(-1);
+  }
+  w.end();
+
+  w.begin(SEC_ZSCORE);
+  for (int l = 0; l < cfg_.n_lags; ++l) {
+    LagState& L = lag_[l];
+    d2h_vec(w, L.len, (size_t)n, stream_);
+    d2h_vec(w, L.counter, (size_t)n, stream_);
+    for (double* a : {L.sum, L.comp, L.sumsq, L.sqcomp}) d2h_rows(w, a, (size_t)S * 8, (size_t)n * 8, NSTAT, bounce, stream_);
+    d2h_rows(w, L.cnt, (size_t)S * 4, (size_t)n * 4, NSTAT, bounce, stream_);
+    const size_t rb = (size_t)cfg_.ring_bytes;
+    d2h_rows(w, L.ring, (size_t)S * rb, (size_t)n * rb, (size_t)NSTAT * cfg_.lags[l], bounce, stream_);
+  }
+  w.end();
+
+  w.begin(SEC_POOL);
+  w.pod(pool_off_); w.pod(pool_n_); w.pod(tail_n_);
+  {
+    std::vector<I64Pair> bc, ee;
+    for (auto& kv : pool_bucket_count_) bc.push_back({kv.first, kv.second});
+    for (auto& kv : pool_exact_edge_) ee.push_back({kv.first, kv.second});
+    w.vec(bc);
+    w.vec(ee);
+  }
+  d2h_vec(w, d_pool_end_[pool_cur_] + pool_off_, (size_t)pool_n_, stream_);
+  d2h_vec(w, d_pool_gid_[pool_cur_] + pool_off_, (size_t)pool_n_, stream_);
+  d2h_vec(w, d_tail_end_, (size_t)tail_n_, stream_);
+  d2h_vec(w, d_tail_gid_, (size_t)tail_n_, stream_);
+  w.pod<uint64_t>(line_blocks_.size());
+  for (auto& kv : line_blocks_) { w.pod(kv.first); w.pod(kv.second.live); w.str(kv.second.data); }
+  w.end();
+
+  w.begin(SEC_ALERTS);
+  w.pod<uint64_t>(last_alert_.size());
+  for (auto& kv : last_alert_) { w.str(kv.first); w.pod(kv.second); }
+  w.end();
+
+  w.begin(SEC_OUTPUTS);
+  for (int k = 0; k < N_OUT; ++k) w.str(blob_[k]);
+  w.end();
+
+  w.begin(SEC_METRICS);
+  {
+    EngineMetrics m = metrics_;
+    const uint64_t sc[] = {m.batches, m.bytes, m.lines, m.events, m.tx, m.tx_db, m.tx_dropped, m.rollovers,
+                           m.alerts, m.alert_candidates, m.released};
+    for (uint64_t v : sc) w.pod(v);
+  }
+  w.end();
+  w.commit();
+  return w.bytes();
+}
+
+void Engine::load_state(const std::string& path) {
+  flush();
+  if (batch_no_ != 0 || n_series_ != 0 || !files_.empty())
+    throw std::runtime_error("load_state needs a freshly constructed engine (no files, no batches)");
+  const int32_t S = cfg_.max_series;
+  void* bounce = nullptr;
+  HIP_OK(hipHostMalloc(&bounce, kBounce, hipHostMallocDefault));
+  struct Guard { void* p; ~Guard() { hipHostFree(p); } } guard{bounce};
+  BinReader rd(path);
+
+  rd.begin(SEC_CONFIG);
+  {
+    int32_t ms, cc, sc, win, buf;
+    int nl, rb;
+    int64_t pc;
+    int32_t lags[MAX_LAGS];
+    rd.pod(ms); rd.pod(nl); rd.raw(lags, sizeof(lags)); rd.pod(rb); rd.pod(cc); rd.pod(sc); rd.pod(pc);
+    rd.pod(win); rd.pod(buf);
+    if (nl != cfg_.n_lags || std::memcmp(lags, cfg_.lags, sizeof(lags)) != 0)
+      throw std::runtime_error("checkpoint: LAG set differs from this engine's configuration");
+    if (rb != cfg_.ring_bytes) throw std::runtime_error("checkpoint: ring dtype differs");
+    if (cc != cfg_.cell_cap || sc != cfg_.spill_cap) throw std::runtime_error("checkpoint: bucket cell layout differs");
+    if (win != cfg_.window || buf != cfg_.buffer) throw std::runtime_error("checkpoint: stats window differs");
+    (void)ms; (void)pc;  // capacities may grow; checked per array below
+  }
+
+  rd.begin(SEC_TOPOLOGY);
+  {
+    auto servers = rd.strs();
+    for (auto& s : servers) add_server(s);
+    const uint64_t nf = rd.pod<uint64_t>();
+    for (uint64_t i = 0; i < nf; ++i) {
+      std::string p = rd.str();
+      const int32_t srv = rd.pod<int32_t>();
+      const uint8_t kind = rd.pod<uint8_t>();
+      add_file(p, kind, servers.at(srv));
+    }
+    auto services = rd.strs();
+    for (size_t i = 0; i < services.size(); ++i)
+      if (dict_.service_id(services[i]) != (int32_t)i) throw std::runtime_error("checkpoint: dictionary mismatch");
+  }
+
+  rd.begin(SEC_SERIES);
+  {
+    auto sr = rd.vec<SeriesRec>();
+    if ((int64_t)sr.size() > S) throw std::runtime_error("checkpoint: more series than maxSeries");
+    server_rank_ = rd.vec<int32_t>();
+    server_next_service_ = rd.vec<int32_t>();
+    rd.pod(next_server_rank_);
+    h_thr_ = rd.vec<double>(); h_infl_ = rd.vec<double>(); h_hard_max_ = rd.vec<double>();
+    h_suppressed_ = rd.vec<uint8_t>(); h_emit_key_ = rd.vec<uint64_t>();
+    zscore_seen_ = rd.vec<int32_t>(); h_active_ = rd.vec<uint8_t>(); unseen_ = rd.vec<int32_t>();
+    rd.raw(alias_thr_, sizeof(alias_thr_)); rd.raw(alias_infl_, sizeof(alias_infl_));
+    series_.clear();
+    series_map_.clear();
+    for (size_t i = 0; i < sr.size(); ++i) {
+      series_.push_back(SeriesInfo{sr[i].server, sr[i].service, sr[i].emit_key});
+      series_map_[((uint64_t)(uint32_t)(sr[i].server + 1) << 32) | (uint32_t)sr[i].service] = (int32_t)i + 1;
+      // K12 name tables, rebuilt in creation order exactly as series_for builds them
+      const int32_t server = sr[i].server, service = sr[i].service;
+      if ((int32_t)server_name_off_.size() <= server) server_name_off_.resize(server + 1, -1);
+      if ((int32_t)service_name_off_.size() <= service) service_name_off_.resize(service + 1, -1);
+      if (server_name_off_[server] < 0) server_name_off_[server] = intern_name(servers_[server]);
+      if (service_name_off_[service] < 0) service_name_off_[service] = intern_name(dict_.service_name(service));
+      h_ser_names_.push_back(server_name_off_[server]);
+      h_ser_names_.push_back((int32_t)servers_[server].size());
+      h_ser_names_.push_back(service_name_off_[service]);
+      h_ser_names_.push_back((int32_t)dict_.service_name(service).size());
+    }
+    n_series_ = (int32_t)sr.size();
+    perm_dirty_ = true;
+    series_service_uploaded_ = 0;
+  }
+  const int32_t n = n_series_;
+
+  rd.begin(SEC_CLOCK);
+  rd.pod(watermark_); rd.pod(batch_no_); rd.pod(latest_); rd.pod(rollover_idx_);
+  rd.raw(slot_bucket_, sizeof(slot_bucket_));
+  rd.pod(next_gid_); rd.pod(line_block_seq_);
+
+  rd.begin(SEC_JOIN);
+  {
+    const uint64_t ns = rd.pod<uint64_t>();
+    if (ns != shards_.size()) throw std::runtime_error("checkpoint: shard count mismatch");
+    for (auto& sh : shards_) sh->load(rd);
+  }
+
+  rd.begin(SEC_PARSE);
+  h2d_vec(rd, d_file_open_, 1 << 16, stream_);
+
+  rd.begin(SEC_BUCKETS);
+  h2d_vec(rd, d_active_, (size_t)S, stream_);
+  {
+    std::vector<int32_t> cells((size_t)n * cfg_.cell_cap);
+    for (;;) {
+      const int32_t slot = rd.pod<int32_t>();
+      if (slot < 0) break;
+      if (slot >= NSLOT) throw std::runtime_error("checkpoint: bad slot");
+      auto counts = rd.vec<int32_t>();
+      auto packed = rd.vec<int32_t>();
+      if ((int32_t)counts.size() != n) throw std::runtime_error("checkpoint: bucket counts size");
+      size_t p = 0;
+      for (int32_t s = 0; s < n; ++s)
+        for (int32_t k = 0; k < std::min(counts[s], cfg_.cell_cap); ++k) cells[(size_t)s * cfg_.cell_cap + k] = packed.at(p++);
+      HIP_OK(hipMemcpy(d_counts_cells_ + (size_t)slot * S, counts.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+      HIP_OK(hipMemcpy(d_cells_ + (size_t)slot * S * cfg_.cell_cap, cells.data(), (size_t)n * cfg_.cell_cap * 4,
+                       hipMemcpyHostToDevice));
+      const int32_t sn = rd.pod<int32_t>();
+      HIP_OK(hipMemcpy(d_spill_n_ + slot, &sn, 4, hipMemcpyHostToDevice));
+      h2d_vec(rd, d_spill_series_ + (size_t)slot * cfg_.spill_cap, (size_t)cfg_.spill_cap, stream_);
+      h2d_vec(rd, d_spill_val_ + (size_t)slot * cfg_.spill_cap, (size_t)cfg_.spill_cap, stream_);
+    }
+  }
+
+  rd.begin(SEC_ZSCORE);
+  for (int l = 0; l < cfg_.n_lags; ++l) {
+    LagState& L = lag_[l];
+    h2d_vec(rd, L.len, (size_t)S, stream_);
+    h2d_vec(rd, L.counter, (size_t)S, stream_);
+    for (double* a : {L.sum, L.comp, L.sumsq, L.sqcomp}) h2d_rows(rd, a, (size_t)S * 8, (size_t)n * 8, NSTAT, bounce, stream_);
+    h2d_rows(rd, L.cnt, (size_t)S * 4, (size_t)n * 4, NSTAT, bounce, stream_);
+    const size_t rb = (size_t)cfg_.ring_bytes;
+    h2d_rows(rd, L.ring, (size_t)S * rb, (size_t)n * rb, (size_t)NSTAT * cfg_.lags[l], bounce, stream_);
+  }
+
+  rd.begin(SEC_POOL);
+  {
+    int64_t off, pn, tn;
+    rd.pod(off); rd.pod(pn); rd.pod(tn);
+    auto bc = rd.vec<I64Pair>();
+    auto ee = rd.vec<I64Pair>();
+    pool_bucket_count_.clear();
+    pool_exact_edge_.clear();
+    for (auto& x : bc) pool_bucket_count_[x.a] = x.b;
+    for (auto& x : ee) pool_exact_edge_[x.a] = x.b;
+    pool_cur_ = 0;
+    pool_off_ = 0;
+    pool_n_ = (int64_t)h2d_vec(rd, d_pool_end_[0], (size_t)cfg_.pool_cap, stream_);
+    h2d_vec(rd, d_pool_gid_[0], (size_t)cfg_.pool_cap, stream_);
+    tail_n_ = (int64_t)h2d_vec(rd, d_tail_end_, (size_t)cfg_.pool_cap, stream_);
+    h2d_vec(rd, d_tail_gid_, (size_t)cfg_.pool_cap, stream_);
+    if (pool_n_ != pn || tail_n_ != tn) throw std::runtime_error("checkpoint: pool size mismatch");
+    (void)off;
+    line_blocks_.clear();
+    for (uint64_t k = rd.pod<uint64_t>(); k; --k) {
+      const uint32_t id = rd.pod<uint32_t>();
+      LineBlock& b = line_blocks_[id];
+      rd.pod(b.live);
+      b.data = rd.str();
+    }
+  }
+
+  rd.begin(SEC_ALERTS);
+  last_alert_.clear();
+  for (uint64_t k = rd.pod<uint64_t>(); k; --k) {
+    std::string key = rd.str();
+    last_alert_[key] = rd.pod<double>();
+  }
+
+  rd.begin(SEC_OUTPUTS);
+  for (int k = 0; k < N_OUT; ++k) blob_[k] = rd.str();
+
+  rd.begin(SEC_METRICS);
+  {
+    uint64_t* sc[] = {&metrics_.batches, &metrics_.bytes, &metrics_.lines, &metrics_.events, &metrics_.tx,
+                      &metrics_.tx_db, &metrics_.tx_dropped, &metrics_.rollovers, &metrics_.alerts,
+                      &metrics_.alert_candidates, &metrics_.released};
+    for (uint64_t* v : sc) rd.pod(*v);
+  }
+  rd.finish();
+  upload_series_tables(0);
+  HIP_OK(hipStreamSynchronize(stream_));
+}
+
+}  // namespace apm

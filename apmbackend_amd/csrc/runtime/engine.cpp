@@ -22,7 +22,6 @@ namespace {
 double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
-constexpr int64_t NO_BUCKET = INT64_MIN;
 }  // namespace
 
 // ----------------------------------------------------------------------------- thread pool
@@ -539,6 +538,12 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
   ++batch_no_;
 }
 
+void Engine::recycle_arena(std::string&& a) {
+  a.clear();
+  std::lock_guard<std::mutex> g(arena_mu_);
+  if (arena_pool_.size() < 4 * shards_.size() + 8) arena_pool_.push_back(std::move(a));
+}
+
 void Engine::stats_worker() {
   StatsJob job;
   for (;;) {
@@ -578,7 +583,15 @@ void Engine::post_stats(std::vector<TxOut>&& txs, double t0) {
   // hand the shards' formatted tx lines to the stats thread; the shards get the previous
   // batch's (consumed) arenas back and reuse their capacity
   st_job_.text.resize(shards_.size());
-  for (size_t i = 0; i < shards_.size(); ++i) st_job_.text[i].swap(shards_[i]->text());
+  for (size_t i = 0; i < shards_.size(); ++i) {
+    st_job_.text[i].swap(shards_[i]->text());
+    // the returned string may be empty (its arena became a release block): hand the shard a
+    // recycled arena so the join workers never page-fault fresh memory
+    if (shards_[i]->text().capacity() < (1u << 20)) {
+      std::lock_guard<std::mutex> g(arena_mu_);
+      if (!arena_pool_.empty()) { shards_[i]->text().swap(arena_pool_.back()); arena_pool_.pop_back(); }
+    }
+  }
   st_job_.t0 = t0;
   st_has_job_ = true;
   st_busy_ = true;
@@ -608,11 +621,14 @@ void Engine::stats_for_batch(std::vector<TxOut>& txs, double batch_t0) {
   const double ts0 = now_ms();
   const int64_t latest_at_start = latest_;
   const bool w_tx = want(OUT_TRANSACTIONS), w_audit = want(OUT_AUDIT_DB), w_db = want(OUT_DB);
-  const std::vector<std::string>& text = *cur_text_;
-  // this batch's pending tx lines go into one release block
-  const uint32_t blk_id = line_block_seq_++;
-  LineBlock* blk = nullptr;
-  if (w_db) blk = &line_blocks_[blk_id];
+  std::vector<std::string>& text = *cur_text_;
+  // Each shard's text arena of this batch becomes a release block (zero copy): the pool payload
+  // of a pending tx addresses its line inside the arena, gid = block << 44 | offset << 12 | len.
+  const size_t n_arena = text.size();
+  std::vector<uint32_t> blk_id(n_arena, 0);
+  std::vector<int64_t> blk_live(n_arena, 0);
+  if (w_db)
+    for (size_t a = 0; a < n_arena; ++a) blk_id[a] = (line_block_seq_++) & 0xFFFFFu;
   // split: audit non-Provider records go straight to db_insert (Q18)
   std::vector<std::pair<uint32_t, int64_t>> triggers;  // (index in upload, new latest)
   uint32_t n = 0;
@@ -623,14 +639,12 @@ void Engine::stats_for_batch(std::vector<TxOut>& txs, double batch_t0) {
     if (t.to_db) {
       ++metrics_.tx_db;
       if (w_audit) {
-        blob_[OUT_AUDIT_DB].append(text[t.server], t.line_off, t.line_len);
-        blob_[OUT_AUDIT_DB] += '\n';
+        blob_[OUT_AUDIT_DB].append(text[t.server], t.line_off, t.line_len + 1);  // with its '\n'
       }
       continue;
     }
     if (w_tx) {
-      blob_[OUT_TRANSACTIONS].append(text[t.server], t.line_off, t.line_len);
-      blob_[OUT_TRANSACTIONS] += '\n';
+      blob_[OUT_TRANSACTIONS].append(text[t.server], t.line_off, t.line_len + 1);
     }
     // NaN / short endTs would wedge the reference's heap forever: dropped and counted (fix)
     if (!(t.end_ms == t.end_ms) || t.end_ms < 10000) { ++metrics_.tx_dropped; continue; }
@@ -647,13 +661,10 @@ void Engine::stats_for_batch(std::vector<TxOut>& txs, double batch_t0) {
     r.elapsed = (e == e && e >= -2147483647.0 && e <= 2147483647.0) ? (int32_t)e : ELAPSED_NAN;
     h_tx_[n] = r;
     int64_t gid = next_gid_++;
-    if (blk) {
-      // [u32 len][bytes] records; the gid addresses the record
-      gid = ((int64_t)blk_id << 32) | (int64_t)blk->data.size();
-      const uint32_t len = t.line_len;
-      blk->data.append((const char*)&len, 4);
-      blk->data.append(text[t.server], t.line_off, t.line_len);
-      ++blk->live;
+    if (w_db) {
+      gid = (int64_t)(((uint64_t)blk_id[t.server] << 44) | ((uint64_t)t.line_off << 12) |
+                      (uint64_t)std::min<uint32_t>(t.line_len, 4095));
+      ++blk_live[t.server];
     }
     h_gid_[n] = gid;
     if (b != agg_b) { if (agg_n) { pool_bucket_count_[agg_b] += agg_n; pool_exact_edge_[agg_b] += agg_e; } agg_b = b; agg_n = agg_e = 0; }
@@ -662,7 +673,13 @@ void Engine::stats_for_batch(std::vector<TxOut>& txs, double batch_t0) {
     ++n;
   }
   if (agg_n) { pool_bucket_count_[agg_b] += agg_n; pool_exact_edge_[agg_b] += agg_e; }
-  if (blk && blk->live == 0) line_blocks_.erase(blk_id);
+  for (size_t a = 0; a < n_arena; ++a)
+    if (blk_live[a] > 0) {
+      if (line_blocks_.count(blk_id[a])) throw std::runtime_error("release block id wrapped while still live");
+      LineBlock& b = line_blocks_[blk_id[a]];
+      b.data.swap(text[a]);  // the arena moves into the block; the job keeps an empty string
+      b.live = blk_live[a];
+    }
   for (auto it = pool_exact_edge_.begin(); it != pool_exact_edge_.end();) {
     if (it->second == 0) it = pool_exact_edge_.erase(it); else ++it;
   }
@@ -755,19 +772,23 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
       LineBlock* cur = nullptr;
       for (int64_t i = 0; i < released; ++i) {
         const uint64_t g = (uint64_t)h_release_gid_[i];
-        const uint32_t id = (uint32_t)(g >> 32);
+        const uint32_t id = (uint32_t)(g >> 44);
         if (id != cur_id) {
           auto it = line_blocks_.find(id);
           cur = it == line_blocks_.end() ? nullptr : &it->second;
           cur_id = id;
         }
         if (!cur) continue;
-        const size_t off = (size_t)(g & 0xffffffffu);
-        uint32_t len;
-        std::memcpy(&len, cur->data.data() + off, 4);
-        out.append(cur->data, off + 4, len);
-        out += '\n';
-        if (--cur->live == 0) { line_blocks_.erase(cur_id); cur = nullptr; cur_id = UINT32_MAX; }
+        const size_t off = (size_t)((g >> 12) & 0xffffffffu);
+        size_t len = (size_t)(g & 0xfff);
+        if (len == 4095) len = cur->data.find('\n', off) - off;  // long line: scan to its end
+        out.append(cur->data, off, len + 1);  // the arena stores each line with its '\n'
+        if (--cur->live == 0) {
+          recycle_arena(std::move(cur->data));
+          line_blocks_.erase(cur_id);
+          cur = nullptr;
+          cur_id = UINT32_MAX;
+        }
       }
     }
     metrics_.released += released;

@@ -29,6 +29,8 @@
 
 namespace apm {
 
+constexpr int64_t NO_BUCKET = INT64_MIN;  // empty bucket slot
+
 struct ServiceOverride {
   bool has_thr[MAX_LAGS] = {false, false, false, false};
   bool has_infl[MAX_LAGS] = {false, false, false, false};
@@ -150,6 +152,11 @@ class Engine {
   void set_sink_fd(const std::string& kind, int fd);
   uint64_t sink_bytes(const std::string& kind) const { return sink_bytes_[out_kind_of(kind)]; }
 
+  // Binary checkpoint of the whole pipeline state (checkpoint.cpp).  load_state needs a freshly
+  // constructed engine with the same LAG set / ring dtype / bucket layout.  Returns bytes written.
+  uint64_t save_state(const std::string& path);
+  void load_state(const std::string& path);
+
   // Warm the z-score rings with a synthetic pre-history (benchmarks).
   void warm_history(uint64_t seed);
 
@@ -167,6 +174,7 @@ class Engine {
   void flush();
   EngineMetrics metrics() { flush(); return metrics_; }
   const std::vector<std::string>& servers() const { return servers_; }
+  const std::vector<FileInfo>& files() const { return files_; }
   std::vector<std::string> services() const { return dict_.services_snapshot(); }
   int32_t n_series() const { return n_series_; }
   double watermark() const { return watermark_; }
@@ -220,7 +228,7 @@ class Engine {
   uint64_t fleet_rounds_ = 0;
   // stats thread
   struct StatsJob { std::vector<TxOut> txs; std::vector<std::string> text; double t0 = 0; };
-  const std::vector<std::string>* cur_text_ = nullptr;  // text arenas of the job being processed
+  std::vector<std::string>* cur_text_ = nullptr;  // text arenas of the job being processed
   std::thread stats_thread_;
   std::mutex st_mu_;
   std::condition_variable st_cv_;
@@ -337,6 +345,9 @@ class Engine {
   // released (lines leave in endTs order, so blocks drain roughly in age order).
   struct LineBlock { std::string data; int64_t live = 0; };
   std::unordered_map<uint32_t, LineBlock> line_blocks_;
+  std::mutex arena_mu_;
+  std::vector<std::string> arena_pool_;          // drained release blocks, reused as shard arenas
+  void recycle_arena(std::string&& a);
   uint32_t line_block_seq_ = 0;
 
   uint32_t last_n_events_ = 0;

@@ -167,6 +167,7 @@ int32_t JoinShard::raw_service(std::string_view prefix, std::string_view name) {
 
 void JoinShard::begin_batch(double now_ms, uint64_t batch_no) {
   text_.clear();
+  if (text_.capacity() < (1u << 20)) text_.reserve(1u << 20);  // arenas move into release blocks
   now_ = now_ms;
   batch_no_ = batch_no;
   sweep();
@@ -269,6 +270,7 @@ void JoinShard::output(int32_t server, int32_t svc, std::string_view log_id, dou
   text_ += '|';
   text_ += rs.toplevel ? 'Y' : 'N';
   t.line_len = (uint32_t)(text_.size() - t.line_off);
+  text_ += '\n';  // lines stay newline-terminated in the arena (zero-copy release, engine.cpp)
   ++counters.tx;
   if (to_db) ++counters.tx_db;
 }

@@ -33,6 +33,9 @@
 
 namespace apm {
 
+class BinWriter;
+class BinReader;
+
 struct TxOut {
   uint64_t seq;          // merge key: line emissions (1<<63)|(line<<12)|sub; expiries creation<<12|sub
   int32_t server;        // server id (== shard index: the line lives in that shard's text arena)
@@ -102,6 +105,10 @@ class JoinShard {
   // Formatted tx lines of this batch (TxOut::line_off/len index into it); cleared by begin_batch.
   std::string& text() { return text_; }
   JoinCounters counters;
+
+  // checkpoint (checkpoint.cpp)
+  void save(BinWriter& w);
+  void load(BinReader& r);
 
   size_t n_partial_logids() const { return record_.size(); }
   size_t n_need_logids() const { return need_.size(); }

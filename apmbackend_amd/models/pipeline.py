@@ -168,6 +168,15 @@ class APMEngine:
     def take(self, kind: str) -> List[str]:
         return self.eng.take(kind)
 
+    def save_state(self, path: str) -> int:
+        """Binary checkpoint of the whole pipeline (engine + join caches + pending output)."""
+        return self.eng.save_state(path)
+
+    def load_state(self, path: str):
+        """Resume from save_state() output; this engine must be fresh (no files, no batches)."""
+        self.eng.load_state(path)
+        self.file_ids = {p: i for i, (p, _k, _s) in enumerate(self.eng.files())}
+
     def take_bytes(self, kind: str) -> bytes:
         return self.eng.take_bytes(kind)
 

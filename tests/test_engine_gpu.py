@@ -190,3 +190,30 @@ def test_gpu_to_fixed_matches_host():
         want = ["undefined" if x != x else N.js_to_fixed(x, f) for x in xs]
         bad = [(x, g, w) for x, g, w in zip(xs, got, want) if g != w]
         assert not bad, bad[:5]
+
+
+@pytest.mark.parametrize("mode", ["exact", "rolling"])
+def test_checkpoint_resume_is_seamless(tmp_path, mode):
+    """save_state mid-stream -> fresh engine -> load_state -> continue == uninterrupted run."""
+    lines, bl = synth_batches(6, duration=900)
+    C = small_cfg(mode)
+    _, full = _run_engine(C, bl)
+    cut = len(bl) // 2
+    eng = APMEngine(C, keep_text=True)
+    out = collections.defaultdict(list)
+    for now, chunks in bl[:cut]:
+        eng.process_lines(chunks, now)
+        for k in ("transactions", "audit_db", "st", "fs", "al"):
+            out[k] += eng.take(k)  # "db" left pending on purpose: it must survive the checkpoint
+    ck = str(tmp_path / "engine.ckpt")
+    assert eng.save_state(ck) > 0
+    del eng
+    eng2 = APMEngine(C, keep_text=True)
+    eng2.load_state(ck)
+    for now, chunks in bl[cut:]:
+        eng2.process_lines(chunks, now)
+        for k in ("transactions", "audit_db", "db", "st", "fs", "al"):
+            out[k] += eng2.take(k)
+    for k in ("transactions", "audit_db", "st", "fs", "al"):
+        assert out[k] == full[k], k
+    assert collections.Counter(out["db"]) == collections.Counter(full["db"])
