@@ -16,6 +16,12 @@
 #include "runtime/format.h"
 #include "runtime/jsutil.h"
 
+namespace apm {
+namespace copyenc {
+void encode_blob(std::string_view blob, std::string* out, int64_t* counts);
+}
+}  // namespace apm
+
 namespace py = pybind11;
 using namespace apm;
 
@@ -324,6 +330,20 @@ PYBIND11_MODULE(_apm_native, m) {
   m.def("memcpy_to", [](uintptr_t dst, py::bytes b, uint64_t off) {
     std::string_view v = b;
     std::memcpy((char*)dst + off, v.data(), v.size());
+  });
+  m.def("copy_encode", [](py::bytes blob) {
+    // wire lines -> Postgres COPY text per table type (runtime/sinks.py is the Python twin)
+    std::string b = blob;
+    std::string out[4];
+    int64_t counts[4] = {0, 0, 0, 0};
+    {
+      py::gil_scoped_release rel;
+      copyenc::encode_blob(b, out, counts);
+    }
+    py::dict d;
+    const char* names[4] = {"tx", "fs", "al", "jx"};
+    for (int k = 0; k < 4; ++k) d[names[k]] = py::make_tuple(py::bytes(out[k]), counts[k]);
+    return d;
   });
   m.def("flatmap_selftest", [](int n_ops, uint64_t seed, int key_space) {
     // randomized FlatMap / SmallVec vs std containers (CPU test of the join's data structures)

@@ -1,0 +1,426 @@
+"""DB insert stage: buffered Postgres loading of the ``db_insert`` stream (reference
+``stream_insert_db.js:1-402``, ``dbstats.js:1-45``, row mappers ``entries.js:23-42,120-151,
+218-240,310-331``).
+
+Behaviour kept from the reference:
+
+* one buffer per record type (``tx``, ``fs``, ``al``, ``jx``); a record is converted to its row
+  object on arrival (``toPostgresObject``);
+* a buffer is flushed when it already holds ``dbInsertBufferLimit`` rows *before* the new row is
+  appended (so a flush carries at most ``limit`` rows, :341-345), or when
+  ``dbMaxTimeBetweenInsertsMs`` passed since the first row entered an empty buffer (:333-339);
+* a failed flush puts the rows back at the *front* of the buffer (:310-320) and is retried by the
+  next flush;
+* on shutdown every buffer is flushed and whatever is left is written to
+  ``bufferResumeFileFullPath`` in the reference's Map JSON format (util_methods.js:189-219);
+* ``DBStats`` logs rows inserted / total ms / ms per row every ``statLogIntervalInSeconds``.
+
+Changed on purpose:
+
+* rows are loaded with ``COPY ... FROM STDIN`` text format instead of multi-row ``INSERT``
+  (K13).  The encoder is native for the high-volume streams (``_apm_native.copy_encode``);
+  this module holds the Python definition it is tested against;
+* writers: ``psql`` pipe when a ``psql`` binary and DB settings exist, else a COPY spool
+  directory (``copySinkDir``; load later with ``\\copy``), or a null writer;
+* the resume file is actually re-loaded (the reference resets it, :176-180 -- Q19).
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import json
+import logging
+import math
+import os
+import shutil
+import subprocess
+import threading
+import time
+from collections import deque
+from typing import Any, Callable, Deque, Dict, Iterable, List, Optional, Sequence, Tuple
+
+from ..utils.jsfmt import js_str
+from ..utils.records import entry_from_csv
+
+log = logging.getLogger("apm.insert_db")
+
+# ColumnSets of stream_insert_db.js:149-160 (type -> config key of the table, columns)
+COLUMNS: Dict[str, Tuple[str, List[str]]] = {
+    "tx": ("dbTxTable", ["endts", "startts", "server", "service", "logid", "acctnum", "elapsed", "toplevel"]),
+    "fs": ("dbStatTable", ["timestamp", "server", "service", "tpm", "lag", "stats"]),
+    "al": ("dbAlertTable", ["entrytimestamp", "alerttimestamp", "server", "service", "cause", "entry"]),
+    "jx": ("dbJmxTable", ["timestamp", "server", "dsinusenodes", "dsactivenodes", "dsavailablenodes", "heapused",
+                          "heapcommitted", "heapmax", "metaused", "metacommitted", "metamax", "sysload", "classcnt",
+                          "threadcnt", "daemonthreadcnt", "beanpoolavailablecnt", "beanpoolcurrentsize",
+                          "beanpoolmaxsize"]),
+}
+TYPES = ("tx", "fs", "al", "jx")
+
+
+# --------------------------------------------------------------------------- COPY text encoding
+
+def _js_json(v: Any) -> str:
+    """JSON.stringify-compatible value text (numbers in JS String() form, dates ISO)."""
+    if v is None:
+        return "null"
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, (int, float)):
+        if isinstance(v, float) and (math.isnan(v) or math.isinf(v)):
+            return "null"
+        return js_str(v)
+    if isinstance(v, _dt.datetime):
+        return json.dumps(_iso_js(v))
+    if isinstance(v, dict):
+        return "{" + ",".join(json.dumps(str(k)) + ":" + _js_json(x) for k, x in v.items()) + "}"
+    if isinstance(v, (list, tuple)):
+        return "[" + ",".join(_js_json(x) for x in v) + "]"
+    return json.dumps(str(v), ensure_ascii=False)
+
+
+def _iso_js(d: _dt.datetime) -> str:
+    """Date.prototype.toISOString(): 2020-01-07T10:00:00.000Z"""
+    d = d.astimezone(_dt.timezone.utc)
+    return d.strftime("%Y-%m-%dT%H:%M:%S.") + f"{d.microsecond // 1000:03d}Z"
+
+
+def _pg_ts(d: _dt.datetime) -> str:
+    d = d.astimezone(_dt.timezone.utc)
+    return d.strftime("%Y-%m-%d %H:%M:%S.") + f"{d.microsecond // 1000:03d}+00"
+
+
+def _copy_escape(s: str) -> str:
+    return (s.replace("\\", "\\\\").replace("\t", "\\t").replace("\n", "\\n").replace("\r", "\\r"))
+
+
+def copy_field(v: Any) -> str:
+    if v is None:
+        return "\\N"
+    if isinstance(v, float) and (math.isnan(v) or math.isinf(v)):
+        return "\\N"
+    if isinstance(v, _dt.datetime):
+        return _pg_ts(v)
+    if isinstance(v, (dict, list)):
+        return _copy_escape(_js_json(v))
+    if isinstance(v, (int, float)) and not isinstance(v, bool):
+        return js_str(v)
+    return _copy_escape(str(v))
+
+
+def copy_row(rtype: str, row: Dict[str, Any]) -> str:
+    return "\t".join(copy_field(row.get(c)) for c in COLUMNS[rtype][1]) + "\n"
+
+
+def pg_row_from_line(line: str) -> Optional[Tuple[str, Dict[str, Any]]]:
+    """consumeMsg (:355-376): CSV -> entry -> toPostgresObject, for tx/fs/al/jx only."""
+    e = entry_from_csv(line)
+    if e is None or e.type not in COLUMNS:
+        return None
+    return e.type, e.to_pg_row()
+
+
+def _native():
+    try:
+        from .. import _native as nat
+        return nat.load(build_if_missing=False)
+    except Exception:  # pragma: no cover - no compiled extension: Python path
+        return None
+
+
+def copy_encode_native(lines: Sequence[str]) -> Optional[Dict[str, Tuple[bytes, int]]]:
+    """``_apm_native.copy_encode`` over newline-joined wire lines (None if not built)."""
+    N = _native()
+    if N is None:
+        return None
+    return N.copy_encode(("\n".join(lines) + "\n").encode("utf-8"))
+
+
+def copy_encode_lines(lines: Iterable[str]) -> Dict[str, List[str]]:
+    """Python definition of the native ``copy_encode``: wire lines -> COPY rows per type."""
+    out: Dict[str, List[str]] = {t: [] for t in TYPES}
+    for ln in lines:
+        if not ln:
+            continue
+        r = pg_row_from_line(ln)
+        if r is not None:
+            out[r[0]].append(copy_row(*r))
+    return out
+
+
+# --------------------------------------------------------------------------- stats
+
+class DBStats:
+    """dbstats.js: rows inserted and insert time, logged and reset every interval."""
+
+    def __init__(self, interval_s: float = 60.0):
+        self.interval = interval_s
+        self.rows = 0
+        self.ms = 0.0
+        self.total_rows = 0
+        self._lock = threading.Lock()
+
+    def add(self, rows: int, ms: float):
+        with self._lock:
+            self.rows += rows
+            self.ms += ms
+            self.total_rows += rows
+
+    def line(self) -> str:
+        avg = (self.ms / self.rows) if self.rows else float("nan")
+        return (f"DBRecordsIns: {self.rows} - TotalInsTime: {self.ms:.1f} ms - "
+                f"AvgDBInsTimePerRec: {avg:.3f} ms")
+
+    def log_and_reset(self, logger=log) -> str:
+        with self._lock:
+            s = self.line()
+            self.rows = 0
+            self.ms = 0.0
+        logger.info(s)
+        return s
+
+
+# --------------------------------------------------------------------------- writers
+
+class Writer:
+    """Loads COPY text rows into one table.  ``write`` raises on failure (rows are re-buffered)."""
+
+    def write(self, table: str, columns: Sequence[str], rows: Sequence[str]) -> None:  # pragma: no cover
+        raise NotImplementedError
+
+    def close(self) -> None:
+        pass
+
+
+class NullWriter(Writer):
+    def __init__(self):
+        self.rows = 0
+
+    def write(self, table, columns, rows):
+        self.rows += len(rows)
+
+
+class CopySpoolWriter(Writer):
+    """Appends COPY text to ``<dir>/<table>.copy`` (one file per table, rotated by size).
+
+    Load with: ``\\copy <table> (<columns>) FROM '<file>'`` -- a ``<table>.columns`` file next
+    to the data holds the column list."""
+
+    def __init__(self, directory: str, rotate_bytes: int = 1 << 30):
+        self.dir = directory
+        self.rotate = rotate_bytes
+        os.makedirs(directory, exist_ok=True)
+        self._fh: Dict[str, Any] = {}
+
+    def _file(self, table: str, columns: Sequence[str]):
+        fh = self._fh.get(table)
+        path = os.path.join(self.dir, f"{table}.copy")
+        if fh is not None and fh.tell() >= self.rotate:
+            fh.close()
+            os.replace(path, os.path.join(self.dir, f"{table}.{int(time.time() * 1000)}.copy"))
+            fh = None
+        if fh is None:
+            with open(os.path.join(self.dir, f"{table}.columns"), "w") as c:
+                c.write(",".join(columns) + "\n")
+            fh = open(path, "a", encoding="utf-8")
+            self._fh[table] = fh
+        return fh
+
+    def write(self, table, columns, rows):
+        fh = self._file(table, columns)
+        fh.write("".join(rows))
+        fh.flush()
+
+    def close(self):
+        for fh in self._fh.values():
+            fh.close()
+        self._fh.clear()
+
+
+class PsqlWriter(Writer):
+    """``COPY table (cols) FROM STDIN`` through the psql client (libpq)."""
+
+    def __init__(self, user: str, host: str, database: str, psql: Optional[str] = None):
+        self.psql = psql or shutil.which("psql")
+        if not self.psql:
+            raise RuntimeError("psql not found")
+        self.args = [self.psql, "-X", "-q", "-v", "ON_ERROR_STOP=1", "-U", user, "-h", host, "-d", database]
+
+    def write(self, table, columns, rows):
+        cmd = self.args + ["-c", f"COPY {table} ({', '.join(columns)}) FROM STDIN"]
+        r = subprocess.run(cmd, input="".join(rows).encode("utf-8"), capture_output=True, timeout=120)
+        if r.returncode != 0:
+            raise RuntimeError(r.stderr.decode(errors="replace").strip())
+
+
+def make_writer(ins_cfg: Dict[str, Any]) -> Writer:
+    mode = ins_cfg.get("sink", "auto")
+    if mode == "null":
+        return NullWriter()
+    if mode in ("auto", "psql") and shutil.which("psql") and ins_cfg.get("dbHost"):
+        return PsqlWriter(ins_cfg.get("dbUser", ""), ins_cfg["dbHost"], ins_cfg.get("dbDatabase", ""))
+    if mode == "psql":
+        raise RuntimeError("sink=psql requested but no psql client is installed")
+    return CopySpoolWriter(ins_cfg.get("copySinkDir", "/tmp/apm/copy"))
+
+
+# --------------------------------------------------------------------------- resume format
+
+def save_resume(path: str, buffers: Dict[str, Deque[Dict[str, Any]]]):
+    """util_methods.saveToResumeFile with the Map replacer: {"dataType":"Map","value":[...]}
+    (atomic: tmp + rename)."""
+    doc = {"dataType": "Map", "value": [[t, [_json_row(r) for r in rows]] for t, rows in buffers.items()]}
+    tmp = path + ".tmp"
+    os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+    with open(tmp, "w") as f:
+        json.dump(doc, f)
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(tmp, path)
+
+
+def _json_row(r: Any) -> Any:
+    if isinstance(r, dict):
+        return {k: _json_row(v) for k, v in r.items()}
+    if isinstance(r, _dt.datetime):
+        return _iso_js(r)
+    return r
+
+
+_TS_COLS = {"endts", "startts", "timestamp", "entrytimestamp", "alerttimestamp"}
+
+
+def load_resume(path: str) -> Dict[str, List[Dict[str, Any]]]:
+    """Reverse of save_resume; accepts the reference's own resume files too."""
+    if not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        doc = json.load(f)
+    if not (isinstance(doc, dict) and doc.get("dataType") == "Map"):
+        return {}
+    out = {}
+    for t, rows in doc["value"]:
+        conv = []
+        for r in rows:
+            rr = dict(r)
+            for k in _TS_COLS & set(rr):
+                if isinstance(rr[k], str):
+                    rr[k] = _dt.datetime.fromisoformat(rr[k].replace("Z", "+00:00"))
+            conv.append(rr)
+        out[t] = conv
+    return out
+
+
+# --------------------------------------------------------------------------- inserter
+
+class DBInserter:
+    """The consumer side of ``db_insert`` (one per node, or one per rank)."""
+
+    def __init__(self, cfg: Dict[str, Any], writer: Optional[Writer] = None,
+                 clock: Callable[[], float] = time.monotonic, stats: Optional[DBStats] = None):
+        ic = cfg["streamInsertDb"]
+        self.cfg = cfg
+        self.limit = int(ic.get("dbInsertBufferLimit", 1000))
+        self.max_wait_s = float(ic.get("dbMaxTimeBetweenInsertsMs", 5000)) / 1000.0
+        self.tables = {t: ic.get(key, t) for t, (key, _cols) in COLUMNS.items()}
+        self.writer = writer if writer is not None else make_writer(ic)
+        self.clock = clock
+        self.stats = stats or DBStats(float(cfg.get("statLogIntervalInSeconds", 60)))
+        self.buffers: Dict[str, Deque[Dict[str, Any]]] = {t: deque() for t in TYPES}
+        self.deadline: Dict[str, Optional[float]] = {t: None for t in TYPES}
+        self.failures = 0
+        self.native = bool(ic.get("nativeCopyEncoder", True))
+        self.resume_path = ic.get("bufferResumeFileFullPath")
+        if self.resume_path:
+            for t, rows in load_resume(self.resume_path).items():
+                if t in self.buffers:
+                    self.buffers[t].extend(rows)
+                    if rows:
+                        self.deadline[t] = self.clock() + self.max_wait_s
+
+    # -- ingest: buffers hold wire lines (encoded in bulk at flush) or row dicts (resumed)
+    def _add(self, rtype: str, item):
+        buf = self.buffers[rtype]
+        if not buf:
+            self.deadline[rtype] = self.clock() + self.max_wait_s
+        if len(buf) >= self.limit:
+            self.flush(rtype)
+        buf.append(item)
+
+    def add_row(self, rtype: str, row: Dict[str, Any]):
+        self._add(rtype, row)
+
+    def consume_line(self, line: str) -> bool:
+        t = line[:3]
+        if len(line) < 3 or t[2] != "|" or t[:2] not in self.buffers:
+            if line:
+                log.info("Not a tx, fs, al, or jx: %s", line)
+            return False
+        self._add(t[:2], line)
+        return True
+
+    def consume_bytes(self, blob: bytes) -> int:
+        n = 0
+        for ln in blob.decode("utf-8").split("\n"):
+            if ln:
+                n += self.consume_line(ln)
+        return n
+
+    def _encode(self, rtype: str, batch: List[Any]) -> List[str]:
+        rows: List[str] = []
+        i = 0
+        while i < len(batch):
+            if isinstance(batch[i], dict):
+                rows.append(copy_row(rtype, batch[i]))
+                i += 1
+                continue
+            j = i
+            while j < len(batch) and isinstance(batch[j], str):
+                j += 1
+            nat = copy_encode_native(batch[i:j]) if self.native else None
+            if nat is not None:
+                blob, cnt = nat[rtype]
+                rows.extend(ln + "\n" for ln in blob.decode("utf-8").split("\n")[:cnt])
+            else:
+                rows.extend(copy_encode_lines(batch[i:j])[rtype])
+            i = j
+        return rows
+
+    # -- flushing
+    def flush(self, rtype: str) -> int:
+        buf = self.buffers[rtype]
+        if not buf:
+            return 0
+        batch = list(buf)
+        buf.clear()
+        t0 = time.perf_counter()
+        try:
+            self.writer.write(self.tables[rtype], COLUMNS[rtype][1], self._encode(rtype, batch))
+        except Exception as e:  # rows go back to the front, retried on the next flush (:310-320)
+            self.failures += 1
+            log.error("Error during insert attempt: %s", e)
+            buf.extendleft(reversed(batch))
+            return 0
+        self.stats.add(len(batch), (time.perf_counter() - t0) * 1000.0)
+        return len(batch)
+
+    def tick(self) -> int:
+        """Timer half of the reference's setTimeout per buffer."""
+        now = self.clock()
+        n = 0
+        for t in TYPES:
+            d = self.deadline[t]
+            if d is not None and now >= d:
+                self.deadline[t] = None
+                n += self.flush(t)
+                if self.buffers[t]:
+                    self.deadline[t] = now + self.max_wait_s
+        return n
+
+    def flush_all(self) -> int:
+        return sum(self.flush(t) for t in TYPES)
+
+    def close(self):
+        self.flush_all()
+        if self.resume_path:
+            rows = {t: [r if isinstance(r, dict) else pg_row_from_line(r)[1] for r in b] for t, b in self.buffers.items()}
+            save_resume(self.resume_path, rows)
+        self.writer.close()

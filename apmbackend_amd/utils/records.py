@@ -260,9 +260,11 @@ def entry_from_csv(line: Union[str, bytes], delim: str = "|"):
         return StatEntry.make(a[1], a[2], a[3], a[4], a[5], a[6], a[7])
     if t == "fs":
         a = _pad(arr, 9)
-        av = _pad(a[6].split(":"), 5)
-        p75 = _pad(a[7].split(":"), 5)
-        p95 = _pad(a[8].split(":"), 5)
+        # a truncated record throws in entries.js (undefined.split); here missing groups are
+        # read as all-undefined so one bad line cannot take the consumer down
+        av = _pad(a[6].split(":") if a[6] is not None else [], 5)
+        p75 = _pad(a[7].split(":") if a[7] is not None else [], 5)
+        p95 = _pad(a[8].split(":") if a[8] is not None else [], 5)
         return FullStatEntry.make(a[1], a[2], a[3], a[5], a[4], *av, *p75, *p95)
     if t == "al":
         a = _pad(arr, 7)

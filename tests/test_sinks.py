@@ -1,0 +1,181 @@
+"""DB insert stage (runtime/sinks.py) against the reference's stream_insert_db.js behaviour."""
+import datetime as dt
+import json
+
+import pytest
+
+from apmbackend_amd.runtime import sinks
+from apmbackend_amd.utils.config import default_config
+
+TX = "tx|jvm01|S:getFoo|[L1]|12345|1578391200000|1578391200250|250|Y"
+FS = ("fs|1578391200000|jvm01|S:getFoo|360|1.20|250.0:240.1:200.0:280.2:1|300.0:undefined:undefined:"
+      "undefined:0.0|400.0:390.0:380.0:400.0:-1.0")
+AL = ("al|1578391201000|1578391200000|jvm01|S:getFoo|average exceeded hard ms threshold|"
+      + FS.replace("|", "&"))
+JX = "jx|1578391200000|jvm01|1|2|3|100|200|300|10|20|30|0.5|1000|50|20|5|6|7"
+
+
+class ListWriter(sinks.Writer):
+    def __init__(self, fail=0):
+        self.calls = []
+        self.fail = fail
+
+    def write(self, table, columns, rows):
+        if self.fail:
+            self.fail -= 1
+            raise RuntimeError("db down")
+        self.calls.append((table, list(columns), list(rows)))
+
+
+class Clock:
+    t = 0.0
+
+    def __call__(self):
+        return self.t
+
+
+def cfg(limit=3, wait_ms=5000, resume=None):
+    C = default_config()
+    C["streamInsertDb"]["dbInsertBufferLimit"] = limit
+    C["streamInsertDb"]["dbMaxTimeBetweenInsertsMs"] = wait_ms
+    C["streamInsertDb"]["bufferResumeFileFullPath"] = resume
+    return C
+
+
+def test_copy_rows_for_every_type():
+    rows = sinks.copy_encode_lines([TX, FS, AL, JX, "st|1|a|b|0.00|1.0|2.0|3.0", "garbage"])
+    tx = rows["tx"][0].rstrip("\n").split("\t")
+    assert tx == ["2020-01-07 10:00:00.250+00", "2020-01-07 10:00:00.000+00", "jvm01", "S:getFoo", "[L1]",
+                  "12345", "250", "Y"]
+    fs = rows["fs"][0].rstrip("\n").split("\t")
+    assert fs[:5] == ["2020-01-07 10:00:00.000+00", "jvm01", "S:getFoo", "1.2", "360"]
+    stats = json.loads(fs[5])
+    assert stats["average"] == 250 and stats["averagesignal"] == 1 and stats["per75avg"] is None
+    assert stats["per95signal"] == -1
+    assert '"per75signal":0' in fs[5]  # JS number text, not 0.0
+    al = rows["al"][0].rstrip("\n").split("\t")
+    assert al[0] == "2020-01-07 10:00:00.000+00" and al[1] == "2020-01-07 10:00:01.000+00"
+    assert json.loads(al[5])["server"] == "jvm01"
+    jx = rows["jx"][0].rstrip("\n").split("\t")
+    assert len(jx) == 18 and jx[11] == "0.5"
+    assert rows["tx"] and not any("st|" in r for r in sum(rows.values(), []))
+
+
+def test_copy_escaping_and_nulls():
+    line = "tx|jv\\m|S:a\tb|x|NaN|NaN|1578391200250|NaN|N"
+    row = sinks.copy_encode_lines([line])["tx"][0]
+    f = row.rstrip("\n").split("\t")
+    assert f[1] == "\\N" and f[2] == "jv\\\\m" and f[5] == "\\N" and f[6] == "\\N"
+    assert "S:a\\tb" in row
+
+
+def test_buffer_limit_flushes_before_append():
+    w = ListWriter()
+    ins = sinks.DBInserter(cfg(limit=3), writer=w, clock=Clock())
+    for _ in range(7):
+        ins.consume_line(TX)
+    # 4th row flushes 3, 7th row flushes 3 more, 1 left buffered
+    assert [len(c[2]) for c in w.calls] == [3, 3]
+    assert len(ins.buffers["tx"]) == 1
+    assert w.calls[0][0] == "tx" and w.calls[0][1][0] == "endts"
+
+
+def test_timeout_flush_and_failure_rebuffers_at_front():
+    clk = Clock()
+    w = ListWriter(fail=1)
+    ins = sinks.DBInserter(cfg(limit=1000, wait_ms=5000), writer=w, clock=clk)
+    ins.consume_line(AL)
+    clk.t = 4.9
+    assert ins.tick() == 0 and not w.calls
+    clk.t = 5.0
+    assert ins.tick() == 0 and ins.failures == 1  # writer failed: row kept
+    assert len(ins.buffers["al"]) == 1
+    ins.consume_line(AL.replace("jvm01", "jvm02"))
+    clk.t = 10.1
+    assert ins.tick() == 2
+    rows = w.calls[0][2]
+    assert "jvm01" in rows[0] and "jvm02" in rows[1]  # failed batch stays first
+    assert ins.stats.total_rows == 2
+    assert "DBRecordsIns: 2" in ins.stats.line()
+
+
+def test_resume_file_roundtrip(tmp_path):
+    path = str(tmp_path / "buf.resume")
+    w = ListWriter(fail=100)
+    ins = sinks.DBInserter(cfg(resume=path), writer=w, clock=Clock())
+    for ln in (TX, FS, AL, JX):
+        ins.consume_line(ln)
+    ins.close()  # flush fails -> everything persisted
+    doc = json.load(open(path))
+    assert doc["dataType"] == "Map" and [t for t, _ in doc["value"]] == ["tx", "fs", "al", "jx"]
+    assert doc["value"][0][1][0]["endts"] == "2020-01-07T10:00:00.250Z"
+    w2 = ListWriter()
+    ins2 = sinks.DBInserter(cfg(resume=path), writer=w2, clock=Clock())
+    assert sum(len(b) for b in ins2.buffers.values()) == 4
+    assert isinstance(ins2.buffers["tx"][0]["endts"], dt.datetime)
+    ins2.flush_all()
+    assert sorted(c[0] for c in w2.calls) == ["alerts", "jmx", "stats", "tx"]
+
+
+def test_spool_writer(tmp_path):
+    w = sinks.CopySpoolWriter(str(tmp_path))
+    ins = sinks.DBInserter(cfg(limit=2), writer=w, clock=Clock())
+    for _ in range(5):
+        ins.consume_line(TX)
+    ins.flush_all()
+    w.close()
+    data = open(tmp_path / "tx.copy").read().splitlines()
+    assert len(data) == 5
+    assert open(tmp_path / "tx.columns").read().strip().split(",")[0] == "endts"
+
+
+def _oracle_stream():
+    import copy
+    from apmbackend_amd.models.oracle import PipelineOracle
+    from apmbackend_amd.utils.synth import Anomaly, Generator, SynthConfig, batches, with_watermarks
+    from apmbackend_amd.utils.timeparse import TzOffset
+    UTC = TzOffset("UTC")
+    start = 1578391200000
+    an = [Anomaly("jvm00", "getSvc0001", start + 100_000, start + 700_000, 30.0)]
+    sc = SynthConfig(servers=2, duration_s=800, tx_per_sec_per_server=3, seed=11, ejb_services=3,
+                     provider_services=2, anomalies=an)
+    lines = Generator(sc).generate()
+    C = default_config()
+    C["streamCalcZScore"]["defaults"] = [{"LAG": 6, "THRESHOLD": 3.0, "INFLUENCE": 0.5}]
+    C["streamProcessAlerts"]["rollingAlertWindowSizeInIntervals"] = 5
+    C["streamProcessAlerts"]["requiredNumberBadIntervalsInAlertWindowToTrigger"] = 2
+    C["gpu"]["timezone"] = "UTC"
+    P = PipelineOracle(copy.deepcopy(C), UTC)
+    P.run_batches(with_watermarks(batches(lines, start, 5.0), UTC))
+    return P.tx_db + P.audit_db + P.fs + P.al
+
+
+def test_native_copy_encoder_matches_python():
+    from apmbackend_amd import _native
+    N = _native.load()
+    stream = _oracle_stream()
+    jx = [JX, "jx|1578391260000|jvm02|1|x|3|100|200|300|10|20|30|abc|1000|50|20|5|6"]
+    weird = ["tx|a\\b|S:x\ty|[L9]|0x1F|  12|1578391200250|NaN|Y", "tx|short", "fs|1578391200000|s|v|8640|Infinity|"
+             "1e3:-0:undefined:2.5e-7:-1|1:2:3:4:1.0|5:6:7:8:0.0", "al|1|2|s|v|c|fs&1578391200000&s&v&6&0.00&u:u:u:u:0"]
+    lines = stream + jx + weird
+    assert any(l.startswith("al|") for l in stream) and any(l.startswith("fs|") for l in stream)
+    want = sinks.copy_encode_lines(lines)
+    got = N.copy_encode(("\n".join(lines) + "\n").encode())
+    for t in sinks.TYPES:
+        blob, cnt = got[t]
+        assert cnt == len(want[t]), t
+        assert blob.decode() == "".join(want[t]), t
+
+
+def test_inserter_native_and_python_paths_agree(tmp_path):
+    stream = _oracle_stream()
+    outs = []
+    for native in (True, False):
+        C = cfg(limit=500)
+        C["streamInsertDb"]["nativeCopyEncoder"] = native
+        w = ListWriter()
+        ins = sinks.DBInserter(C, writer=w, clock=Clock())
+        ins.consume_bytes(("\n".join(stream) + "\n").encode())
+        ins.flush_all()
+        outs.append(sorted((c[0], tuple(c[2])) for c in w.calls))
+    assert outs[0] == outs[1] and len(outs[0]) >= 3
