@@ -21,8 +21,10 @@ class CpuOracleEngine:
     def __init__(self, cfg: Dict[str, Any]):
         g = cfg.get("gpu", {})
         self.tz = TzOffset(g.get("timezone", "local"))
-        self.P = PipelineOracle(copy.deepcopy(cfg), self.tz, alert_clock=g.get("alertClock", "entry"))
         self.files_: List[Tuple[str, int, str]] = []
+        self._server = {}
+        self.P = PipelineOracle(copy.deepcopy(cfg), self.tz, alert_clock=g.get("alertClock", "entry"),
+                                server_fn=lambda p: self._server.get(p, "undefined"))
         self.watermark = 0.0
         self._taken = {"transactions": 0, "audit_db": 0, "db": 0, "st": 0, "fs": 0, "al": 0}
         self.lines = 0
@@ -31,6 +33,7 @@ class CpuOracleEngine:
     # --- native Engine API subset
     def add_file(self, path: str, kind: int, server: str) -> int:
         self.files_.append((path, kind, server))
+        self._server[path] = server
         return len(self.files_) - 1
 
     def files(self):

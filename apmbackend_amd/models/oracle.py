@@ -309,8 +309,9 @@ class ParseOracle:
     """
 
     def __init__(self, emit: Callable[[str, str], None], tz: Optional[TzOffset] = None,
-                 record_ttl=120, acct_ttl=120, need_ttl=30):
+                 record_ttl=120, acct_ttl=120, need_ttl=30, server_fn: Callable[[str], str] = None):
         self.emit = emit
+        self.server_fn = server_fn or server_of  # path -> server (reference: split('/')[2])
         self.tz = tz or default_tz()
         self.now = 0.0
         clock = lambda: self.now
@@ -373,7 +374,7 @@ class ParseOracle:
             self.context.pop(fp, None)
         need_map = self.need_cache.get(log_id)
         if need_map:
-            srv = server_of(fp)
+            srv = self.server_fn(fp)
             for service, rec in list(need_map.items()):
                 self.output_record(srv, service, log_id, acct, rec.get("startTs"), rec.get("endTs"),
                                    rec.get("elapsed"))
@@ -594,7 +595,7 @@ class ParseOracle:
         if not line:
             return
         self.counters["lines"] += 1
-        server = server_of(fp)
+        server = self.server_fn(fp)
         kind = file_kind(fp)
         if kind == "SOAP":
             self._soap(line, fp)
@@ -855,7 +856,8 @@ class AlertsOracle:
 class PipelineOracle:
     """parse -> stats -> z-score -> alerts, with the queues modelled as in-order FIFOs."""
 
-    def __init__(self, cfg: Dict[str, Any], tz: Optional[TzOffset] = None, alert_clock="entry"):
+    def __init__(self, cfg: Dict[str, Any], tz: Optional[TzOffset] = None, alert_clock="entry",
+                 server_fn: Callable[[str], str] = None):
         self.cfg = cfg
         self.tx_db: List[str] = []
         self.audit_db: List[str] = []
@@ -871,7 +873,7 @@ class PipelineOracle:
         self.st = StatsOracle(self._on_st, self.tx_db.append, int(sc["intervalLengthInSeconds"]),
                               int(sc["windowSizeInIntervals"]), int(sc["bufferSizeInIntervals"]))
         self.parse = ParseOracle(self._on_tx, tz, g.get("recordTtlSeconds", 120),
-                                 g.get("acctTtlSeconds", 120), g.get("needTtlSeconds", 30))
+                                 g.get("acctTtlSeconds", 120), g.get("needTtlSeconds", 30), server_fn=server_fn)
 
     def _on_tx(self, queue, line):
         if queue == "db_insert":

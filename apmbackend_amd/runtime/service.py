@@ -1,0 +1,372 @@
+"""The per-GPU ingest service: tail -> engine -> sinks, the runnable form of the reference's five
+stage processes (stream_parse_transactions.js, stream_calc_stats.js, stream_calc_z_score.js,
+stream_process_alerts.js feeding stream_insert_db.js).
+
+One process per GPU (``torchrun`` / the supervisor set RANK, WORLD_SIZE, LOCAL_RANK):
+
+* **files** -- ``glob(appLogDirMaskPrefix/<maskSuffix>)`` (stream_parse_transactions.js:816-825),
+  server = the host path component; the JVM hosts are sharded over ranks
+  (parallel/dist.shard_servers) so every join and every series is rank-local;
+* **tailing** -- the native Tailer (pause-file contract of perl_tail.pl:36-41, persisted
+  offsets, rotation);
+* **engine** -- APMEngine (GPU) -- or, only when asked for, the CPU oracle adapter used by tests;
+* **outputs** -- ``gpu.outputMode``: ``inproc`` feeds the DB insert stage in this process
+  (runtime/sinks.DBInserter, COPY); ``amqp`` publishes the reference's queue contract
+  (``db_insert`` gets tx/fs/al like stream_process_alerts.js:618 forwards them; optional
+  ``bridgeQueues`` also mirror ``transactions``/``stats``/``z_score``) through runtime/queue.py;
+  alert lines also go to the e-mail notifier (runtime/notifier.py);
+* **checkpoint** -- every ``gpu.checkpointEverySeconds`` and on SIGTERM/SIGINT: the binary
+  engine checkpoint + tail offsets, written atomically; restored at start-up (the reference's
+  resume files, SURVEY §5.4, but covering the parser too);
+* **hot reload** -- ConfigWatcher: thresholds/overrides re-applied to live series, logger
+  re-pointed, notifier and sink limits updated; restart-only keys warn;
+* **control** -- SIGUSR1 = ``requestGC`` (util_methods.js:463-467): Python gc + malloc_trim +
+  memory report; fleet baseline exchange over RCCL when WORLD_SIZE > 1.
+"""
+from __future__ import annotations
+
+import ctypes
+import gc
+import glob
+import json
+import logging
+import os
+import signal
+import time
+from typing import Any, Callable, Dict, List, Optional, Sequence
+
+from ..models.oracle import file_kind, server_of
+from ..models.pipeline import DB_OUTPUTS, KIND_CODE, OUT_KINDS, APMEngine
+from ..parallel.dist import dist_env, shard_servers
+from ..utils.config import ConfigWatcher, as_bool, read_apm_config
+from . import logger as apmlog
+from .notifier import AlertNotifier
+from .sinks import DBInserter
+
+log = logging.getLogger("apm.service")
+
+RESTART_KEYS = ["apmConfigFilePath", "amqpConnectionString", "streamParseTransactions.appLogDirMaskPrefix",
+                "streamParseTransactions.maskSuffixes", "streamCalcStats.intervalLengthInSeconds",
+                "streamCalcStats.windowSizeInIntervals", "streamCalcStats.bufferSizeInIntervals",
+                "gpu.maxSeries", "gpu.ringDtype", "gpu.zscoreMeanMode", "gpu.outputMode"]
+
+
+def discover_files(cfg: Dict[str, Any]) -> List[str]:
+    pc = cfg["streamParseTransactions"]
+    prefix = pc.get("appLogDirMaskPrefix", "")
+    out = []
+    for suf in pc.get("maskSuffixes", []):
+        out += glob.glob(os.path.join(prefix, suf))
+    return sorted(set(out))
+
+
+class IngestService:
+    def __init__(self, cfg: Optional[Dict[str, Any]] = None, config_path: Optional[str] = None,
+                 engine: str = "native", files: Optional[Sequence[str]] = None, rank: Optional[int] = None,
+                 world: Optional[int] = None, clock: Callable[[], float] = time.time, install_signals: bool = False,
+                 server_of_path: Callable[[str], str] = server_of):
+        self.cfg = cfg if cfg is not None else read_apm_config(config_path, first_run=True)
+        g = self.cfg.setdefault("gpu", {})
+        r, w, local = dist_env()
+        self.rank = r if rank is None else rank
+        self.world = w if world is None else world
+        self.local_rank = local
+        self.clock = clock
+        self.server_of = server_of_path
+        apmlog.set_global_logger(self.cfg.get("logDir"), self._log_prefix(), colorize=True)
+        self.mode = g.get("outputMode", "inproc")
+        self.bridge = list(g.get("bridgeQueues", []))
+
+        # ---- files -> this rank's shard
+        all_files = list(files) if files is not None else discover_files(self.cfg)
+        servers = sorted({self.server_of(f) for f in all_files})
+        mine = set(shard_servers(servers, self.world)[self.rank]) if servers else set()
+        self.files = [f for f in all_files if self.server_of(f) in mine]
+        log.info("rank %d/%d: %d of %d files, servers %s", self.rank, self.world, len(self.files), len(all_files),
+                 sorted(mine))
+
+        # ---- engine
+        outs = set(DB_OUTPUTS)
+        if self.mode == "amqp":
+            outs |= {"transactions" if "transactions" in self.bridge else "", "st" if "stats" in self.bridge else ""}
+            outs.discard("")
+        self.outputs = [k for k in OUT_KINDS if k in outs]
+        if engine == "native":
+            self.eng = APMEngine(self.cfg, device=self.local_rank, outputs=self.outputs)
+            self.native = self.eng.eng
+        elif engine == "cpu-oracle":
+            from ..models.cpu_engine import CpuOracleEngine
+            self.eng = None
+            self.native = CpuOracleEngine(self.cfg)
+        else:
+            raise ValueError(f"unknown engine {engine!r}")
+
+        # ---- checkpoint restore (before files are registered: load_state re-registers them)
+        self.ckpt_dir = g.get("checkpointDir")
+        self.ckpt_every = float(g.get("checkpointEverySeconds",
+                                      self.cfg["streamCalcStats"].get("resumeFileSaveFrequencyInSeconds", 60)))
+        restored = self._restore() if (self.ckpt_dir and engine == "native") else False
+        if not restored:
+            for f in self.files:
+                self.native.add_file(f, KIND_CODE[file_kind(f)], self.server_of(f))
+        self.file_ids = {p: i for i, (p, _k, _s) in enumerate(self.native.files())}
+
+        # ---- tailer
+        from .. import _native
+        N = _native.load(build_if_missing=False)
+        pc = self.cfg["streamParseTransactions"]
+        self.pause_file = pc.get("tailPauseFileFullPath", "")
+        self.tailer = N.Tailer(self.pause_file, int(g.get("batchBytes", 32 << 20)))
+        from_start = as_bool(g.get("tailFromStart", False))
+        for p, fid in sorted(self.file_ids.items(), key=lambda kv: kv[1]):
+            self.tailer.add(p, fid, from_start)
+        self.offsets_path = pc.get("tailOffsetFileFullPath")
+        if restored:
+            self._restore_offsets()
+
+        # ---- outputs
+        self.inserter: Optional[DBInserter] = None
+        self.qm = None
+        self.producers: Dict[str, Any] = {}
+        if self.mode == "inproc":
+            self.inserter = DBInserter(self.cfg)
+        elif self.mode == "amqp":
+            from .queue import QueueManager
+            self.qm = QueueManager(self.cfg["amqpConnectionString"], self.cfg.get("statLogIntervalInSeconds", 60))
+            self.producers["db"] = self.qm.get_queue(self.cfg.get("dbInsertQueue", "db_insert"), "p")
+            qmap = {"transactions": self.cfg["streamParseTransactions"].get("outQueue", "transactions"),
+                    "stats": self.cfg["streamCalcStats"].get("outQueue", "stats")}
+            for q in self.bridge:
+                if q in qmap:
+                    self.producers[q] = self.qm.get_queue(qmap[q], "p")
+            self.qm.on("pause", lambda: log.info("queue backpressure: pausing ingest"))
+        elif self.mode != "none":
+            raise ValueError(f"unknown gpu.outputMode {self.mode!r}")
+        self.notifier = AlertNotifier(self.cfg, clock=clock) if self.rank == 0 or self.world == 1 else None
+
+        # ---- fleet exchange
+        self.fleet = None
+        if self.world > 1 and engine == "native" and as_bool(g.get("fleetBaseline", True)):
+            from ..parallel.fleet import FleetBaseline
+            self.fleet = FleetBaseline(self.eng, self.world, self.rank)
+
+        self.watcher = ConfigWatcher(self.cfg, self.reload, RESTART_KEYS) if self.cfg.get("apmConfigFilePath") else None
+        self._stop = False
+        self._gc_requested = False
+        self.batches = 0
+        self.last_ckpt = clock()
+        self.last_stat = clock()
+        self._m0 = self._metrics()
+        if install_signals:
+            signal.signal(signal.SIGTERM, self._on_signal)
+            signal.signal(signal.SIGINT, self._on_signal)
+            signal.signal(signal.SIGUSR1, lambda *a: setattr(self, "_gc_requested", True))
+
+    # ------------------------------------------------------------------ helpers
+    def _log_prefix(self) -> str:
+        base = self.cfg.get("gpu", {}).get("logFilePrefix", "apm_engine")
+        return f"{base}.rank{self.rank}" if self.world > 1 else base
+
+    def _ckpt_paths(self):
+        return (os.path.join(self.ckpt_dir, f"engine.rank{self.rank}.ckpt"),
+                os.path.join(self.ckpt_dir, f"tail.rank{self.rank}.json"))
+
+    def _restore(self) -> bool:
+        ck, _ = self._ckpt_paths()
+        if not os.path.exists(ck):
+            return False
+        try:
+            self.eng.load_state(ck)
+            log.info("resumed engine state from %s", ck)
+            known = {p for p, _k, _s in self.native.files()}
+            for f in self.files:  # files that appeared since the checkpoint
+                if f not in known:
+                    self.native.add_file(f, KIND_CODE[file_kind(f)], self.server_of(f))
+            return True
+        except Exception as e:
+            log.error("checkpoint %s could not be loaded (%s); starting fresh", ck, e)
+            raise
+
+    def _restore_offsets(self):
+        _, tp = self._ckpt_paths()
+        if not os.path.exists(tp):
+            return
+        with open(tp) as f:
+            offs = json.load(f)
+        for path, (off, ino) in offs.items():
+            self.tailer.set_offset(path, int(off), int(ino))
+
+    def checkpoint(self):
+        if not self.ckpt_dir or self.eng is None:
+            return None
+        os.makedirs(self.ckpt_dir, exist_ok=True)
+        ck, tp = self._ckpt_paths()
+        t0 = time.perf_counter()
+        # undelivered output goes out first so the checkpoint and the sinks agree
+        self._drain_outputs()
+        n = self.native.save_state(ck)
+        self.tailer.save_offsets(tp)
+        if self.offsets_path:
+            self.tailer.save_offsets(self.offsets_path)
+        log.info("checkpoint %s: %.1f MB in %.0f ms", ck, n / 1e6, (time.perf_counter() - t0) * 1e3)
+        self.last_ckpt = self.clock()
+        return ck
+
+    def _metrics(self) -> Dict[str, Any]:
+        m = self.native.metrics()
+        return m if isinstance(m, dict) else {}
+
+    def _on_signal(self, signum, frame):
+        log.info("Caught signal %d", signum)
+        self._stop = True
+
+    def stop(self):
+        self._stop = True
+
+    # ------------------------------------------------------------------ config reload
+    def reload(self, cfg: Dict[str, Any]):
+        self.cfg = cfg
+        apmlog.set_global_logger(cfg.get("logDir"), self._log_prefix())
+        if self.eng is not None:
+            self.eng.reload(cfg)
+        if self.notifier:
+            self.notifier.reload(cfg)
+        if self.inserter:
+            ic = cfg["streamInsertDb"]
+            self.inserter.limit = int(ic.get("dbInsertBufferLimit", self.inserter.limit))
+            self.inserter.max_wait_s = float(ic.get("dbMaxTimeBetweenInsertsMs", 5000)) / 1000.0
+        log.info("configuration reloaded")
+
+    # ------------------------------------------------------------------ outputs
+    def _drain_outputs(self) -> Dict[str, int]:
+        counts = {}
+        for k in self.outputs:
+            blob = self.native.take_bytes(k)
+            if not blob:
+                continue
+            counts[k] = blob.count(b"\n")
+            if k == "al" and self.notifier:
+                self.notifier.add_lines(blob.decode("utf-8").split("\n"))
+            if self.inserter is not None and k in DB_OUTPUTS:
+                self.inserter.consume_bytes(blob)
+            elif self.qm is not None:
+                if k in DB_OUTPUTS:
+                    prod = self.producers["db"]
+                elif k == "transactions":
+                    prod = self.producers.get("transactions")
+                else:
+                    prod = self.producers.get("stats")
+                if prod is not None:
+                    prod.write_lines(ln for ln in blob.decode("utf-8").split("\n") if ln)
+        return counts
+
+    def _housekeeping(self):
+        now = self.clock()
+        if self.inserter is not None:
+            self.inserter.tick()
+        if self.notifier is not None:
+            self.notifier.tick()
+        if self.watcher is not None:
+            try:
+                self.watcher.check_once()
+            except Exception as e:  # a broken config must not stop ingest
+                log.error("config reload failed: %s", e)
+        if self._gc_requested:
+            self._gc_requested = False
+            self.request_gc()
+        if self.ckpt_dir and self.eng is not None and now - self.last_ckpt >= self.ckpt_every:
+            self.checkpoint()
+        interval = float(self.cfg.get("statLogIntervalInSeconds", 60))
+        if now - self.last_stat >= interval:
+            self.log_stats(now - self.last_stat)
+            self.last_stat = now
+
+    def log_stats(self, dt_s: float):
+        m = self._metrics()
+        d = {k: m.get(k, 0) - self._m0.get(k, 0) for k in ("lines", "tx", "alerts", "rollovers", "batches")}
+        self._m0 = m
+        log.info("ENGINE lines/s: %.0f - tx/s: %.0f - rollovers: %d - alerts: %d - batches: %d - series: %s",
+                 d["lines"] / max(dt_s, 1e-9), d["tx"] / max(dt_s, 1e-9), d["rollovers"], d["alerts"], d["batches"],
+                 self.native.n_series() if hasattr(self.native, "n_series") else "?")
+        if self.inserter is not None:
+            self.inserter.stats.log_and_reset()
+        if self.qm is not None:
+            log.info(self.qm.stats.line())
+
+    def request_gc(self) -> str:
+        """requestGC: collect Python garbage and hand freed heap back to the OS."""
+        gc.collect()
+        try:
+            ctypes.CDLL("libc.so.6").malloc_trim(0)
+        except OSError:
+            pass
+        rss = 0
+        try:
+            with open("/proc/self/statm") as f:
+                rss = int(f.read().split()[1]) * os.sysconf("SC_PAGE_SIZE")
+        except OSError:
+            pass
+        msg = f"Running garbage collection! rss={rss / 2**20:.1f} MB"
+        log.info(msg)
+        return msg
+
+    # ------------------------------------------------------------------ main loop
+    def step(self) -> int:
+        """One poll: read new complete lines from every file and run them through the engine."""
+        if self.qm is not None and any(getattr(p, "paused", False) for p in self.producers.values()):
+            return 0  # downstream backpressure: hold the tails (pause-file semantics)
+        buf, chunks = self.tailer.poll()
+        if not chunks:
+            return 0
+        self.native.process_batch(buf, chunks, -1.0)
+        self.batches += 1
+        self._drain_outputs()
+        return len(buf)
+
+    def run(self, max_batches: Optional[int] = None, idle_sleep_s: float = 0.5,
+            until: Optional[Callable[[], bool]] = None):
+        log.info("ingest loop starting (mode=%s)", self.mode)
+        while not self._stop:
+            n = self.step()
+            self._housekeeping()
+            if max_batches is not None and self.batches >= max_batches:
+                break
+            if until is not None and until():
+                break
+            if n == 0:
+                time.sleep(idle_sleep_s)
+        self.shutdown()
+
+    def shutdown(self):
+        log.info("shutting down")
+        self.native.flush()
+        self._drain_outputs()
+        if self.ckpt_dir and self.eng is not None:
+            self.checkpoint()
+        if self.offsets_path:
+            self.tailer.save_offsets(self.offsets_path)
+        if self.inserter is not None:
+            self.inserter.close()
+        if self.notifier is not None:
+            self.notifier.tick()
+        if self.qm is not None:
+            self.qm.shutdown()
+
+
+def main(argv=None):  # pragma: no cover - process entry point
+    import argparse
+    ap = argparse.ArgumentParser(description="apmbackend_amd ingest service (one process per GPU)")
+    ap.add_argument("--config", default=None)
+    ap.add_argument("--engine", default="native", choices=["native", "cpu-oracle"])
+    ap.add_argument("--max-batches", type=int, default=None)
+    a = ap.parse_args(argv)
+    env_world = dist_env()[1]
+    if env_world > 1:
+        from ..parallel.dist import init_distributed
+        init_distributed()
+    svc = IngestService(config_path=a.config, engine=a.engine, install_signals=True)
+    svc.run(max_batches=a.max_batches)
+
+
+if __name__ == "__main__":  # pragma: no cover
+    main()

@@ -1,0 +1,157 @@
+"""Ingest service plumbing on CPU (the oracle engine stands in for the GPU engine):
+tail files -> engine -> DB insert stage / AMQP db_insert queue / e-mail notifier."""
+import copy
+import json
+import os
+import time
+
+import pytest
+
+from apmbackend_amd.models.oracle import PipelineOracle
+from apmbackend_amd.runtime import sinks
+from apmbackend_amd.runtime.amqp_broker import Broker
+from apmbackend_amd.runtime.service import IngestService
+from apmbackend_amd.utils.config import default_config
+from apmbackend_amd.utils.synth import Anomaly, Generator, SynthConfig, batches
+from apmbackend_amd.utils.timeparse import TzOffset, leading_line_ts
+
+UTC = TzOffset("UTC")
+START = 1578391200000
+
+
+class ListWriter(sinks.Writer):
+    def __init__(self):
+        self.rows = {}
+
+    def write(self, table, columns, rows):
+        self.rows.setdefault(table, []).extend(rows)
+
+
+def srv_of(p):
+    return p.split("/")[-2]
+
+
+def make_env(tmp_path, mode="inproc", servers=2, duration=400):
+    an = [Anomaly("jvm00", "getSvc0001", START + 60_000, START + 350_000, 40.0)]
+    sc = SynthConfig(servers=servers, duration_s=duration, tx_per_sec_per_server=3, seed=4, ejb_services=3,
+                     provider_services=2, anomalies=an)
+    lines = Generator(sc).generate()
+    C = default_config()
+    C["streamCalcZScore"]["defaults"] = [{"LAG": 6, "THRESHOLD": 3.0, "INFLUENCE": 0.5}]
+    C["streamProcessAlerts"]["rollingAlertWindowSizeInIntervals"] = 5
+    C["streamProcessAlerts"]["requiredNumberBadIntervalsInAlertWindowToTrigger"] = 2
+    C["streamProcessAlerts"]["alertCollectionIntervalInSeconds"] = 1
+    C["logDir"] = str(tmp_path / "logs")
+    C["apmConfigFilePath"] = None
+    C["streamParseTransactions"]["tailPauseFileFullPath"] = str(tmp_path / "PAUSE")
+    C["streamParseTransactions"]["tailOffsetFileFullPath"] = str(tmp_path / "offsets.json")
+    C["streamInsertDb"]["bufferResumeFileFullPath"] = str(tmp_path / "ins.resume")
+    C["gpu"].update({"timezone": "UTC", "outputMode": mode, "tailFromStart": True})
+    # files on disk: <tmp>/logs_in/<server>/<basename>
+    mapping = {}
+    for fp in lines:
+        server = fp.split("/")[2]
+        d = tmp_path / "in" / server
+        d.mkdir(parents=True, exist_ok=True)
+        mapping[fp] = str(d / os.path.basename(fp))
+        open(mapping[fp], "w").close()
+    return C, lines, mapping, sc
+
+
+def feed_in_steps(svc, lines, mapping, sc, oracle=None):
+    """Append one 5 s slice of every file, then run one service step (= one tailer poll)."""
+    bl = batches(lines, sc.start_ms, 5.0)
+    file_order = [p for p, _ in sorted(svc.file_ids.items(), key=lambda kv: kv[1])]
+    rev = {v: k for k, v in mapping.items()}
+    wm = 0.0
+    for chunks in bl:
+        for fp, ls in chunks:
+            with open(mapping[fp], "a") as f:
+                f.write("\n".join(ls) + "\n")
+        svc.step()
+        svc._housekeeping()
+        if oracle is not None:  # same batch: files in tailer order, watermark clock
+            by = dict(chunks)
+            oracle.parse.begin_batch(wm)
+            for p in file_order:
+                for ln in by.get(rev[p], []):
+                    oracle.parse.read_line(p, ln)
+                    v = leading_line_ts(ln, UTC)
+                    if v is not None and v > wm:
+                        wm = v
+
+
+def test_service_inproc_matches_oracle(tmp_path):
+    C, lines, mapping, sc = make_env(tmp_path)
+    svc = IngestService(C, engine="cpu-oracle", files=sorted(mapping.values()), rank=0, world=1,
+                        server_of_path=srv_of)
+    w = ListWriter()
+    svc.inserter.writer = w
+    P = PipelineOracle(copy.deepcopy(C), UTC, server_fn=srv_of)
+    feed_in_steps(svc, lines, mapping, sc, P)
+    svc.shutdown()
+    want = sinks.copy_encode_lines(P.tx_db + P.audit_db + P.fs + P.al)
+    assert sorted(w.rows["tx"]) == sorted(want["tx"]) and len(want["tx"]) > 100
+    assert w.rows["stats"] == want["fs"]
+    assert w.rows.get("alerts", []) == want["al"] and len(want["al"]) > 0
+    assert svc.notifier.emails >= 1 or svc.notifier.buffer
+    offs = json.load(open(tmp_path / "offsets.json"))
+    assert sorted(offs) == sorted(mapping.values())
+    assert all(v[0] == os.path.getsize(k) for k, v in offs.items())
+    logs = os.listdir(tmp_path / "logs")
+    assert any(l.startswith("apm_engine.log.") for l in logs)
+
+
+def test_pause_file_holds_the_tails(tmp_path):
+    C, lines, mapping, sc = make_env(tmp_path, duration=60)
+    svc = IngestService(C, engine="cpu-oracle", files=sorted(mapping.values()), rank=0, world=1,
+                        server_of_path=srv_of)
+    for chunks in batches(lines, sc.start_ms, 5.0):
+        for fp, ls in chunks:
+            with open(mapping[fp], "a") as f:
+                f.write("\n".join(ls) + "\n")
+    (tmp_path / "PAUSE").write_text("")
+    assert svc.step() == 0
+    os.remove(tmp_path / "PAUSE")
+    assert svc.step() > 0
+    svc.shutdown()
+
+
+def test_service_sharding_by_server(tmp_path):
+    C, lines, mapping, sc = make_env(tmp_path, servers=4, duration=30)
+    files = sorted(mapping.values())
+    per_rank = [IngestService(C, engine="cpu-oracle", files=files, rank=r, world=2, server_of_path=srv_of).files
+                for r in range(2)]
+    assert sorted(per_rank[0] + per_rank[1]) == files
+    assert not ({srv_of(f) for f in per_rank[0]} & {srv_of(f) for f in per_rank[1]})
+
+
+def test_service_amqp_mode_publishes_db_insert(tmp_path):
+    b = Broker(port=0).start()
+    try:
+        C, lines, mapping, sc = make_env(tmp_path, mode="amqp", duration=200)
+        C["amqpConnectionString"] = b.url
+        C["gpu"]["bridgeQueues"] = ["transactions"]
+        svc = IngestService(C, engine="cpu-oracle", files=sorted(mapping.values()), rank=0, world=1,
+                            server_of_path=srv_of)
+        feed_in_steps(svc, lines, mapping, sc)
+        svc.shutdown()
+        st = b.stats()
+        assert st["db_insert"]["messages"] > 0 and st["transactions"]["messages"] > 0
+        n_tx = st["transactions"]["messages"]
+        m = svc.native.metrics()
+        assert n_tx + 0 <= m["tx"]
+    finally:
+        b.stop()
+
+
+def test_request_gc_and_reload(tmp_path):
+    C, lines, mapping, sc = make_env(tmp_path, duration=30)
+    svc = IngestService(C, engine="cpu-oracle", files=sorted(mapping.values()), rank=0, world=1,
+                        server_of_path=srv_of)
+    assert "garbage collection" in svc.request_gc()
+    C2 = copy.deepcopy(C)
+    C2["streamInsertDb"]["dbInsertBufferLimit"] = 7
+    svc.reload(C2)
+    assert svc.inserter.limit == 7
+    svc.shutdown()

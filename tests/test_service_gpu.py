@@ -1,0 +1,83 @@
+"""Ingest service with the native GPU engine: equals the CPU oracle service, and a
+checkpoint / restart in the middle of the stream changes nothing."""
+import copy
+import os
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("no GPU", allow_module_level=True)
+
+from apmbackend_amd.runtime.service import IngestService  # noqa: E402
+from apmbackend_amd.utils.synth import batches  # noqa: E402
+from test_service import ListWriter, feed_in_steps, make_env, srv_of  # noqa: E402
+
+
+def gpu_cfg(C):
+    C["gpu"].update({"zscoreMeanMode": "exact", "maxSeries": 4096, "batchBytes": 4 << 20,
+                     "maxLinesPerBatch": 1 << 16, "bucketCellCapacity": 8, "bucketOverflowCapacity": 1 << 16,
+                     "emulateOverrideAliasing": True})
+    return C
+
+
+def run(svc, lines, mapping, sc, lo=0, hi=None):
+    bl = batches(lines, sc.start_ms, 5.0)[lo:hi]
+    for chunks in bl:
+        for fp, ls in chunks:
+            with open(mapping[fp], "a") as f:
+                f.write("\n".join(ls) + "\n")
+        svc.step()
+        svc._housekeeping()
+
+
+def test_native_service_matches_cpu_oracle_service(tmp_path):
+    outs = []
+    for engine in ("native", "cpu-oracle"):
+        d = tmp_path / engine
+        d.mkdir()
+        C, lines, mapping, sc = make_env(d)
+        gpu_cfg(C)
+        svc = IngestService(C, engine=engine, files=sorted(mapping.values()), rank=0, world=1, server_of_path=srv_of)
+        w = ListWriter()
+        svc.inserter.writer = w
+        run(svc, lines, mapping, sc)
+        svc.shutdown()
+        outs.append(w.rows)
+    nat, cpu = outs
+    assert nat["stats"] == cpu["stats"] and len(nat["stats"]) > 0
+    assert nat.get("alerts") == cpu.get("alerts")
+    assert sorted(nat["tx"]) == sorted(cpu["tx"])
+
+
+def test_service_checkpoint_restart_is_seamless(tmp_path):
+    res = []
+    for restart in (False, True):
+        d = tmp_path / ("restart" if restart else "straight")
+        d.mkdir()
+        C, lines, mapping, sc = make_env(d)
+        gpu_cfg(C)
+        C["gpu"]["checkpointDir"] = str(d / "ckpt")
+        C["gpu"]["checkpointEverySeconds"] = 1e9
+        nb = len(batches(lines, sc.start_ms, 5.0))
+        files = sorted(mapping.values())
+        w = ListWriter()
+        svc = IngestService(C, engine="native", files=files, rank=0, world=1, server_of_path=srv_of)
+        svc.inserter.writer = w
+        if restart:
+            run(svc, lines, mapping, sc, 0, nb // 2)
+            svc.shutdown()  # flush + checkpoint + offsets
+            del svc
+            svc = IngestService(C, engine="native", files=files, rank=0, world=1, server_of_path=srv_of)
+            svc.inserter.writer = w
+            run(svc, lines, mapping, sc, nb // 2, None)
+        else:
+            run(svc, lines, mapping, sc)
+        svc.shutdown()
+        assert os.path.exists(d / "ckpt" / "engine.rank0.ckpt")
+        res.append(w.rows)
+    a, b = res
+    assert a["stats"] == b["stats"] and len(a["stats"]) > 0
+    assert sorted(a["tx"]) == sorted(b["tx"])
+    assert a.get("alerts") == b.get("alerts")
