@@ -1,0 +1,443 @@
+"""Supervisor tree: the ``apm_manager.js`` equivalent (reference :1-649).
+
+* **modules** -- ``applicationManager.moduleSettings``; each entry starts one process (or, for
+  ``"ranks"``, one process per GPU with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set: the
+  torchrun-style launch of the per-GPU engine).  stdout/stderr go to
+  ``<logDir>/<name>.start.log`` (Module.startProcess :329-356); children run in their own
+  session so the supervisor's signals do not reach them.
+* **stale processes** -- instead of killing every process whose command line matches a script
+  name (Module.killExistingPIDs :274-295), each module records its PID in
+  ``<stateDir>/<name>.pid``; a stale PID is terminated only if its /proc cmdline still carries the
+  module's ``--apm-module=<name>`` marker.
+* **restart** -- on exit: Grafana annotation + manager alert, restart after
+  ``restartDelaySeconds`` (1 s), or ``crashLoopDelaySeconds`` (60 s) when it died less than
+  ``crashLoopWindowSeconds`` (5 s) after starting (childExitCB :303-327).  A rank group restarts as
+  a whole: RCCL communicators cannot lose a member, so the surviving ranks are stopped first.
+* **monitoring** every ``inspectionFrequencySeconds`` aligned to the clock
+  (monitorResourcesRecurs :514-530): liveness (kill(pid, 0)), per-module PSS/swap (native
+  /proc/<pid>/smaps_rollup reader, the pid_stats.py equivalent) and HBM per process (KFD sysfs)
+  against the module / global thresholds -> alert + ``requestGC`` (SIGUSR1) to the child
+  (inspectModules :475-512); disk space of the app mount (inspectDiskSpace :397-427); queue depth
+  when running with a broker (inspectQueues :429-453).
+* **alerts** -- buffered ``"<date> ::: text"`` lines mailed every
+  ``alertCollectionIntervalInSeconds`` with backoff up to ``maxCollectionIntervalInSeconds``
+  (the reference compares against the undefined ``minCollectionIntervalInSeconds`` and so never
+  backs off: quirk fixed);
+* **log retention** -- every 12 h delete logs older than ``appLogRetentionDays``.
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import json
+import logging
+import os
+import shlex
+import signal
+import subprocess
+import sys
+import time
+from typing import Any, Callable, Dict, List, Optional
+
+from ..utils.config import ConfigWatcher, as_bool, read_apm_config
+from . import logger as apmlog
+from .notifier import Mailer, post_annotation
+
+log = logging.getLogger("apm.manager")
+
+
+def log_date(t: float) -> str:
+    return _dt.datetime.fromtimestamp(t).strftime("%Y-%m-%d %H:%M:%S")
+
+
+def pid_exists(pid: int) -> bool:
+    try:
+        os.kill(pid, 0)
+        return True
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+
+
+def proc_cmdline(pid: int) -> str:
+    try:
+        with open(f"/proc/{pid}/cmdline", "rb") as f:
+            return f.read().replace(b"\0", b" ").decode(errors="replace")
+    except OSError:
+        return ""
+
+
+def pid_mem_swap_mb(pid: int):
+    """(PSS MiB, SwapPss MiB) -- the pid_stats.py -q -m numbers (native reader)."""
+    try:
+        from .. import _native
+        pss, swap = _native.load(build_if_missing=False).pid_pss_swap(int(pid))
+        if pss < 0:
+            return None, None
+        return pss / 2**20, max(swap, 0) / 2**20
+    except Exception:
+        from ..cli.pid_stats import pss_swap_bytes
+        pss, swap = pss_swap_bytes(pid)
+        return (None, None) if pss is None else (pss / 2**20, swap / 2**20)
+
+
+def pid_vram_mb(pid: int) -> float:
+    """HBM allocated by a process, from the KFD sysfs (sum over GPUs), 0 if unknown."""
+    d = f"/sys/class/kfd/kfd/proc/{pid}"
+    total = 0
+    try:
+        for name in os.listdir(d):
+            if name.startswith("vram_"):
+                with open(os.path.join(d, name)) as f:
+                    total += int(f.read().strip() or 0)
+    except OSError:
+        return 0.0
+    return total / 2**20
+
+
+def disk_usage(path: str):
+    st = os.statvfs(path)
+    size = st.f_blocks * st.f_frsize / 2**30
+    avail = st.f_bavail * st.f_frsize / 2**30
+    used = (st.f_blocks - st.f_bfree) * st.f_frsize / 2**30
+    pct = 100.0 * used / (used + avail) if used + avail else 0.0
+    return size, used, avail, pct
+
+
+class Proc:
+    def __init__(self, name: str, argv: List[str], env: Dict[str, str], log_path: str, pid_path: str):
+        self.name = name
+        self.argv = argv
+        self.env = env
+        self.log_path = log_path
+        self.pid_path = pid_path
+        self.popen: Optional[subprocess.Popen] = None
+        self.last_start = 0.0
+        self.restart_at: Optional[float] = None
+        self.restarts = 0
+
+    @property
+    def pid(self) -> Optional[int]:
+        return self.popen.pid if self.popen else None
+
+    def marker(self) -> str:
+        return f"--apm-module={self.name}"
+
+    def start(self, now: float):
+        os.makedirs(os.path.dirname(self.log_path) or ".", exist_ok=True)
+        out = open(self.log_path, "w")
+        env = dict(os.environ)
+        env.update(self.env)
+        self.popen = subprocess.Popen(self.argv + [self.marker()], stdin=subprocess.DEVNULL, stdout=out,
+                                      stderr=subprocess.STDOUT, env=env, start_new_session=True)
+        out.close()
+        self.last_start = now
+        self.restart_at = None
+        os.makedirs(os.path.dirname(self.pid_path) or ".", exist_ok=True)
+        with open(self.pid_path, "w") as f:
+            f.write(str(self.popen.pid))
+        log.info("Child process started via PID: %d (%s)", self.popen.pid, self.name)
+
+    def kill_stale(self):
+        """killExistingPIDs: only the PID this module recorded, and only if it is still ours."""
+        try:
+            with open(self.pid_path) as f:
+                pid = int(f.read().strip())
+        except (OSError, ValueError):
+            return None
+        if pid_exists(pid) and self.marker() in proc_cmdline(pid):
+            log.warning("Killing PID: %d (stale %s)", pid, self.name)
+            try:
+                os.kill(pid, signal.SIGTERM)
+            except OSError:
+                pass
+            return pid
+        return None
+
+    def stop(self, timeout: float = 10.0):
+        if self.popen and self.popen.poll() is None:
+            self.popen.terminate()
+            try:
+                self.popen.wait(timeout)
+            except subprocess.TimeoutExpired:
+                self.popen.kill()
+                self.popen.wait(5)
+
+    def poll(self) -> Optional[int]:
+        return self.popen.poll() if self.popen else None
+
+
+class Module:
+    """One moduleSettings entry: a single process or a group of GPU ranks."""
+
+    def __init__(self, setting: Dict[str, Any], mcfg: Dict[str, Any], cfg: Dict[str, Any], state_dir: str,
+                 config_path: Optional[str]):
+        self.s = setting
+        self.name = setting.get("name") or os.path.basename(setting.get("relativePath", "module")).split(".")[0]
+        if "module" in setting:
+            base = [sys.executable, "-m", setting["module"]]
+        else:
+            base = [sys.executable, os.path.join(cfg.get("appDirectory", "."), setting["relativePath"])]
+        argv = base + list(mcfg.get("sharedOpts", [])) + list(setting.get("args", []))
+        if config_path and setting.get("passConfig", True):
+            argv += ["--config", config_path]
+        ranks = setting.get("ranks", 0)
+        if ranks == "auto":
+            ranks = int(os.environ.get("APM_GPUS", "0")) or _gpu_count()
+        self.ranks = int(ranks or 0)
+        log_dir = cfg.get("logDir", "/tmp/apm/logs")
+        self.procs: List[Proc] = []
+        if self.ranks:
+            port = str(setting.get("masterPort", 29512))
+            for r in range(self.ranks):
+                env = {"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(self.ranks),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": port}
+                self.procs.append(Proc(f"{self.name}.rank{r}", argv, env,
+                                       os.path.join(log_dir, f"{self.name}.rank{r}.start.log"),
+                                       os.path.join(state_dir, f"{self.name}.rank{r}.pid")))
+        else:
+            self.procs.append(Proc(self.name, argv, dict(setting.get("env", {})),
+                                   os.path.join(log_dir, f"{self.name}.start.log"),
+                                   os.path.join(state_dir, f"{self.name}.pid")))
+
+    def setting(self, key: str, mcfg: Dict[str, Any]):
+        """getModuleSetting (:455-464): module value if set (0 counts), else the global one."""
+        v = self.s.get(key)
+        return v if (v or v == 0) and v is not None else mcfg.get(key)
+
+
+def _gpu_count() -> int:
+    try:
+        import torch
+        return torch.cuda.device_count()
+    except Exception:
+        return 0
+
+
+class Supervisor:
+    def __init__(self, cfg: Optional[Dict[str, Any]] = None, config_path: Optional[str] = None,
+                 clock: Callable[[], float] = time.time, mailer: Optional[Mailer] = None, annotate=post_annotation):
+        self.cfg = cfg if cfg is not None else read_apm_config(config_path, first_run=True)
+        self.config_path = config_path or self.cfg.get("apmConfigFilePath")
+        self.m = self.cfg["applicationManager"]
+        self.clock = clock
+        self.mailer = mailer or Mailer(outbox=os.path.join(self.cfg.get("logDir", "/tmp/apm/logs"), "outbox"))
+        self.annotate = annotate
+        apmlog.set_global_logger(self.cfg.get("logDir"), self.m.get("logFilePrefix", "apm_manager"))
+        self.state_dir = self.m.get("stateDir", os.path.join(os.path.dirname(self.cfg.get("logDir", "/tmp/apm/logs")),
+                                                             "state"))
+        self.modules = [Module(s, self.m, self.cfg, self.state_dir, self.config_path)
+                        for s in self.m.get("moduleSettings", []) if as_bool(s.get("enabled", True))]
+        self.alert_buffer: List[str] = []
+        self.alert_interval = float(self.m.get("alertCollectionIntervalInSeconds", 60))
+        self.next_alert = clock() + self.alert_interval
+        self.next_inspect = clock()
+        self.next_prune = clock()
+        self.emails = 0
+        self.gc_requests: List[str] = []
+        self._stop = False
+        self.watcher = (ConfigWatcher(self.cfg, self._reload, ["apmConfigFilePath", "logDir",
+                                                               "applicationManager.moduleSettings"])
+                        if self.config_path else None)
+
+    # ------------------------------------------------------------------ alerts
+    def add_alert(self, text: str):
+        self.alert_buffer.append(f"{log_date(self.clock())} ::: {text}")
+        log.warning(text)
+
+    def send_alerts(self) -> bool:
+        now = self.clock()
+        if now < self.next_alert:
+            return False
+        sent = False
+        interval = float(self.m.get("alertCollectionIntervalInSeconds", 60))
+        if self.alert_buffer:
+            interval = self.alert_interval
+            if as_bool(self.m.get("increaseCollectionIntervalAfterAlert", False)) and \
+                    interval < float(self.m.get("maxCollectionIntervalInSeconds", 3840)):
+                interval *= 2
+            body = "".join(f"Alert: {json.dumps(a)}\n" for a in self.alert_buffer)
+            body += f"\n\nCooldown until further alerts are sent: {int(interval)} seconds\n"
+            if as_bool(self.m.get("emailsEnabled", True)):
+                try:
+                    self.mailer.send(self.m.get("fromEmail", "apm@localhost"), self.m.get("emailList", ""),
+                                     "APM Manager Alerts", f"<pre>{body}</pre>")
+                    self.emails += 1
+                    sent = True
+                except Exception as e:
+                    log.error("manager e-mail failed: %s", e)
+            self.alert_buffer = []
+        self.alert_interval = interval
+        self.next_alert = now + interval
+        return sent
+
+    # ------------------------------------------------------------------ lifecycle
+    def start_all(self):
+        self.annotate(self.cfg.get("grafana", {}), "Restarting all modules", ["maintenance"])
+        for mod in self.modules:
+            for p in mod.procs:
+                p.kill_stale()
+        now = self.clock()
+        for mod in self.modules:
+            for p in mod.procs:
+                p.start(now)
+        log.info("Processes started.")
+
+    def stop_all(self):
+        for mod in self.modules:
+            for p in mod.procs:
+                p.stop()
+
+    def _on_exit(self, mod: Module, p: Proc, code: int, now: float):
+        log.error("Child exited: code:%s module: %s", code, p.name)
+        self.annotate(self.cfg.get("grafana", {}), f"Module exited: {p.name}", ["maintenance"])
+        self.add_alert(f"Child module exited: code:{code} module: {p.name}")
+        quick = now - p.last_start < float(self.m.get("crashLoopWindowSeconds", 5))
+        delay = float(self.m.get("crashLoopDelaySeconds", 60)) if quick else float(self.m.get("restartDelaySeconds", 1))
+        if quick:
+            log.warning("Time since last restart is under %ss: crash loop suspected, waiting %ss",
+                        self.m.get("crashLoopWindowSeconds", 5), delay)
+        targets = mod.procs if mod.ranks else [p]
+        for q in targets:  # a rank group restarts as a whole
+            if q is not p:
+                q.stop()
+            q.restart_at = now + delay
+
+    def check_children(self):
+        now = self.clock()
+        for mod in self.modules:
+            for p in mod.procs:
+                if p.restart_at is not None:
+                    if now >= p.restart_at:
+                        p.restarts += 1
+                        p.start(now)
+                        self.add_alert(f"Process restarted via startProcess: {p.name}")
+                    continue
+                code = p.poll()
+                if code is not None:
+                    self._on_exit(mod, p, code, now)
+
+    # ------------------------------------------------------------------ monitoring
+    def inspect(self):
+        self.inspect_disk()
+        self.inspect_queues()
+        self.inspect_modules()
+
+    def inspect_disk(self):
+        app = self.cfg.get("appDirectory", "/")
+        parts = os.path.abspath(app).split(os.sep)
+        mount = os.sep + parts[1] if len(parts) > 1 and parts[1] else os.sep
+        if not os.path.exists(mount):
+            return
+        size, used, avail, pct = disk_usage(mount)
+        if avail <= float(self.m.get("diskSpaceGBAvailableThreshold", 100)):
+            self.add_alert(f"Available disk space is low on mount: {mount} - Size: {size:.0f} GB, Used: {used:.0f} GB,"
+                           f" Available: {avail:.0f} GB, PercentUsed: {pct:.0f}%")
+        if pct > float(self.m.get("diskSpacePercentageUsedThreshold", 80)):
+            self.add_alert(f"Disk space percentage used is high on mount: {mount} - Size: {size:.0f} GB, Used: "
+                           f"{used:.0f} GB, Available: {avail:.0f} GB, PercentUsed: {pct:.0f}%")
+
+    def inspect_queues(self):
+        if self.cfg.get("gpu", {}).get("outputMode", "inproc") != "amqp":
+            return
+        try:
+            from .amqp import Connection
+            c = Connection(self.cfg["amqpConnectionString"], timeout=3)
+        except Exception as e:
+            self.add_alert(f"Could not inspect queues: broker unreachable: {e}")
+            return
+        try:
+            names = {self.cfg.get("dbInsertQueue", "db_insert")}
+            for q in names:
+                _n, msgs, _c = c.queue_declare(q, durable=True)
+                if msgs > float(self.m.get("queueMessageAlertThreshold", 1e6)):
+                    self.add_alert(f"Queue exceeded the message count threshold - Queue: {q} Threshold: "
+                                   f"{self.m.get('queueMessageAlertThreshold')} MessageCount: {msgs}")
+        finally:
+            c.close()
+
+    def inspect_modules(self):
+        for mod in self.modules:
+            for p in mod.procs:
+                if p.restart_at is not None or p.pid is None:
+                    continue
+                if not pid_exists(p.pid) or p.poll() is not None:
+                    continue  # handled by check_children
+                mem, swap = pid_mem_swap_mb(p.pid)
+                if mem is None:
+                    continue
+                trigger = False
+                mthr = float(mod.setting("moduleMemoryAlertThreshold", self.m) or 1e18)
+                if mem > mthr:
+                    self.add_alert(f"Child module exceeded the memory threshold - Module: {p.name} Threshold(Mb): "
+                                   f"{mthr} MemoryUsed(Mb): {mem:.1f}")
+                    trigger = True
+                sthr = float(mod.setting("moduleSwapAlertThreshold", self.m) or 1e18)
+                if swap > sthr:
+                    self.add_alert(f"Child module exceeded the swap threshold - Module: {p.name} Threshold(Mb): "
+                                   f"{sthr} SwapUsed(Mb): {swap:.1f}")
+                    trigger = True
+                gthr = mod.setting("moduleGpuMemoryAlertThreshold", self.m)
+                vram = pid_vram_mb(p.pid)
+                if gthr and vram > float(gthr):
+                    self.add_alert(f"Child module exceeded the GPU memory threshold - Module: {p.name} "
+                                   f"Threshold(Mb): {gthr} HBMUsed(Mb): {vram:.1f}")
+                if trigger:
+                    log.info("Sending garbage collection request to module: %s", p.name)
+                    self.gc_requests.append(p.name)
+                    try:
+                        os.kill(p.pid, signal.SIGUSR1)  # requestGC
+                    except OSError:
+                        pass
+
+    def _reload(self, cfg):
+        self.cfg = cfg
+        self.m = cfg["applicationManager"]
+        apmlog.set_global_logger(cfg.get("logDir"), self.m.get("logFilePrefix", "apm_manager"))
+
+    # ------------------------------------------------------------------ main loop
+    def tick(self):
+        now = self.clock()
+        self.check_children()
+        if now >= self.next_inspect:
+            self.inspect()
+            freq = float(self.m.get("inspectionFrequencySeconds", 60))
+            self.next_inspect = now + (freq - (int(now) % 60) % freq if freq < 60 else freq)
+        if now >= self.next_prune:
+            apmlog.prune_logs(self.cfg.get("logDir", "/tmp/apm/logs"), int(self.m.get("appLogRetentionDays", 7)), now)
+            self.next_prune = now + 12 * 3600
+        self.send_alerts()
+        if self.watcher is not None:
+            try:
+                self.watcher.check_once()
+            except Exception as e:
+                log.error("config reload failed: %s", e)
+
+    def run(self, tick_s: float = 0.5, until: Optional[Callable[[], bool]] = None):
+        self.start_all()
+        try:
+            while not self._stop:
+                self.tick()
+                if until is not None and until():
+                    break
+                time.sleep(tick_s)
+        finally:
+            self.stop_all()
+
+    def stop(self, *a):
+        self._stop = True
+
+
+def main(argv=None):  # pragma: no cover - process entry point
+    import argparse
+    ap = argparse.ArgumentParser(description="apmbackend_amd supervisor (apm_manager equivalent)")
+    ap.add_argument("--config", default=None)
+    a = ap.parse_args(argv)
+    sup = Supervisor(config_path=a.config)
+    signal.signal(signal.SIGTERM, sup.stop)
+    signal.signal(signal.SIGINT, sup.stop)
+    sup.run()
+
+
+if __name__ == "__main__":  # pragma: no cover
+    main()
