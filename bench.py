@@ -25,14 +25,13 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-REFERENCE_CPU_LINES_PER_S = None  # measured reference throughput (tools/measure_reference.py), if any
 
 
 def _load_reference_baseline():
     p = os.path.join(ROOT, "profiles", "reference_cpu_baseline.json")
     try:
         with open(p) as fh:
-            return float(json.load(fh)["lines_per_sec"])
+            return float(json.load(fh)["value"])
     except (OSError, KeyError, ValueError):
         return None
 
