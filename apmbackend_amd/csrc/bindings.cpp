@@ -263,6 +263,36 @@ PYBIND11_MODULE(_apm_native, m) {
       .def("take", &Engine::take, py::call_guard<py::gil_scoped_release>())
       .def("flush", &Engine::flush, py::call_guard<py::gil_scoped_release>())
       .def("save_state", &Engine::save_state, py::call_guard<py::gil_scoped_release>())
+      .def("export_series", &Engine::export_series, py::call_guard<py::gil_scoped_release>())
+      .def("import_series", &Engine::import_series, py::call_guard<py::gil_scoped_release>())
+      .def("export_buckets", [](Engine& e) {
+        BucketDump d;
+        { py::gil_scoped_release rel; d = e.export_buckets(); }
+        return py::make_tuple(d.latest, d.series, d.bucket, d.count, d.values);
+      })
+      .def("import_buckets", &Engine::import_buckets, py::call_guard<py::gil_scoped_release>())
+      .def("export_history", [](Engine& e, int lag_idx, int32_t lo, int32_t hi) {
+        std::vector<int32_t> len;
+        std::vector<double> vals;
+        { py::gil_scoped_release rel; e.export_history(lag_idx, lo, hi, len, vals); }
+        return py::make_tuple(len, py::bytes((const char*)vals.data(), vals.size() * 8));
+      })
+      .def("import_history", [](Engine& e, int lag_idx, const std::vector<int32_t>& series,
+                                const std::vector<int32_t>& len, py::bytes vals) {
+        std::string b = vals;
+        std::vector<double> v(b.size() / 8);
+        std::memcpy(v.data(), b.data(), v.size() * 8);
+        py::gil_scoped_release rel;
+        e.import_history(lag_idx, series, len, v);
+      })
+      .def("export_lag_settings", &Engine::export_lag_settings)
+      .def("export_pending", &Engine::export_pending, py::call_guard<py::gil_scoped_release>())
+      .def("import_pending", &Engine::import_pending, py::call_guard<py::gil_scoped_release>())
+      .def("export_cooldowns", &Engine::export_cooldowns)
+      .def("import_cooldowns", &Engine::import_cooldowns)
+      .def("export_alert_counters", &Engine::export_alert_counters)
+      .def("import_alert_counters", &Engine::import_alert_counters)
+      .def("cooldown_by_service", &Engine::cooldown_by_service)
       .def("load_state", &Engine::load_state, py::call_guard<py::gil_scoped_release>())
       .def("take_bytes", [](Engine& e, const std::string& k) {
         std::string b;

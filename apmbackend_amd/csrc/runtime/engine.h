@@ -95,6 +95,16 @@ enum OutKind { OUT_TRANSACTIONS = 0, OUT_AUDIT_DB, OUT_DB, OUT_ST, OUT_FS, OUT_A
 const char* out_kind_name(int k);
 int out_kind_of(const std::string& name);
 
+// Live bucket contents for the reference resume exporter: (series, bucket, count) rows and
+// the concatenated elapsed values.
+struct BucketDump {
+  int64_t latest = 0;
+  std::vector<int32_t> series;
+  std::vector<int64_t> bucket;
+  std::vector<int32_t> count;
+  std::vector<int32_t> values;
+};
+
 struct Chunk {
   int32_t file;
   uint64_t begin, end;  // byte range in the batch (must end with '\n')
@@ -157,6 +167,25 @@ class Engine {
   uint64_t save_state(const std::string& path);
   void load_state(const std::string& path);
 
+  // Structured state access for the reference resume importer/exporter (state_io.cpp).
+  std::vector<std::pair<std::string, std::string>> export_series();
+  int32_t import_series(const std::string& server, const std::string& service);
+  BucketDump export_buckets();
+  void import_buckets(int64_t latest, const std::vector<int32_t>& series, const std::vector<int64_t>& bucket,
+                      const std::vector<int32_t>& count, const std::vector<int32_t>& values);
+  // history of series [lo, hi) for one LAG: len[j], vals[j][stat][LAG] chronological (NaN pad)
+  void export_history(int lag_idx, int32_t lo, int32_t hi, std::vector<int32_t>& len, std::vector<double>& vals);
+  void import_history(int lag_idx, const std::vector<int32_t>& series, const std::vector<int32_t>& len,
+                      const std::vector<double>& vals);
+  std::vector<double> export_lag_settings(int lag_idx);  // [series][thr, infl]
+  std::vector<std::pair<int64_t, std::string>> export_pending();
+  void import_pending(const std::vector<int64_t>& ends, const std::vector<std::string>& lines);
+  std::vector<std::pair<std::string, double>> export_cooldowns();
+  void import_cooldowns(const std::vector<std::pair<std::string, double>>& c);
+  std::vector<int32_t> export_alert_counters(int lag_idx);
+  void import_alert_counters(int lag_idx, const std::vector<int32_t>& series, const std::vector<int32_t>& counts);
+  bool cooldown_by_service() const { return cfg_.cooldown_by_service != 0; }
+
   // Warm the z-score rings with a synthetic pre-history (benchmarks).
   void warm_history(uint64_t seed);
 
@@ -216,6 +245,7 @@ class Engine {
   void drain_sinks();
   bool want(int k) const { return (cfg_.outputs >> k) & 1u; }
   void* dmalloc(size_t bytes);
+  void require_fresh(const char* what);
 
   EngineConfig cfg_;
   hipStream_t stream_ = nullptr, comm_stream_ = nullptr, parse_stream_ = nullptr;
