@@ -94,7 +94,7 @@ def export_reference_resume(eng, chunk: int = 4096) -> Tuple[Dict, Dict, Dict]:
     # ---- alerts
     by_service = nat.cooldown_by_service()
     alerts = OrderedDict()
-    for key, ts in nat.export_cooldowns():
+    for key, ts in sorted(nat.export_cooldowns()):
         if by_service:
             alerts[key] = {"alertTimestamp": _num(ts), "service": key, "type": "al"}
         else:

@@ -78,7 +78,7 @@ def test_export_matches_reference_state_and_roundtrips():
     s2, z2, a2 = rc.export_reference_resume(eng2)
     assert norm_stats(s2) == norm_stats(stats)
     assert json.dumps(z2) == json.dumps(zscore)
-    assert a2["alerts"] == alerts["alerts"]
+    assert dict(a2["alerts"]) == dict(alerts["alerts"]) and len(alerts["alerts"]) > 0
 
 
 def test_import_then_continue_produces_stats_rows():
