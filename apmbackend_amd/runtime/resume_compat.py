@@ -111,8 +111,11 @@ def export_reference_resume(eng, chunk: int = 4096) -> Tuple[Dict, Dict, Dict]:
 
 
 def import_reference_resume(eng, stats: Optional[Dict] = None, zscore: Optional[Dict] = None,
-                            alerts: Optional[Dict] = None, restore_alert_counts: bool = False) -> Dict[str, int]:
-    """Seed a *fresh* engine (no batches yet) from reference resume documents."""
+                            alerts: Optional[Dict] = None, restore_alert_counts: bool = False,
+                            servers: Optional[set] = None) -> Dict[str, int]:
+    """Seed a *fresh* engine (no batches yet) from reference resume documents.  ``servers``
+    restricts the import to one rank's JVM hosts (multi-GPU: every rank imports its shard)."""
+    keep = (lambda srv: True) if servers is None else (lambda srv: srv in servers)
     nat = getattr(eng, "eng", eng)
     lags = [int(x[0]) if isinstance(x, (list, tuple)) else int(x) for x in eng.ecfg["lags"]]
     ids: Dict[Tuple[str, str], int] = {}
@@ -128,6 +131,8 @@ def import_reference_resume(eng, stats: Optional[Dict] = None, zscore: Optional[
         latest = int(stats.get("latestBucket") or 0)
         s_ids, bks, cnts, vals = [], [], [], []
         for srv, so in stats.get("servers", {}).items():
+            if not keep(srv):
+                continue
             for svc, sv in so.get("services", {}).items():
                 s = sid(srv, svc)
                 b = sv.get("buckets", {})
@@ -141,6 +146,8 @@ def import_reference_resume(eng, stats: Optional[Dict] = None, zscore: Optional[
         content = (stats.get("minHeap") or {}).get("content", [])
         ends, lines = [], []
         for o in content:
+            if not keep(o.get("server")):
+                continue
             tx = TxEntry.make(o.get("server"), o.get("service"), o.get("logId"), o.get("acctNum"), o.get("startTs"),
                               o.get("endTs"), o.get("elapsed"), o.get("topLevel"))
             e = tx.endTs
@@ -153,6 +160,8 @@ def import_reference_resume(eng, stats: Optional[Dict] = None, zscore: Optional[
     if zscore:
         per_lag: Dict[int, Tuple[List[int], List[int], List[np.ndarray]]] = {l: ([], [], []) for l in lags}
         for srv, so in zscore.get("servers", {}).items():
+            if not keep(srv):
+                continue
             for svc, sv in so.get("services", {}).items():
                 s = sid(srv, svc)
                 for lag_s, lo in sv.get("lags", {}).items():
@@ -187,6 +196,8 @@ def import_reference_resume(eng, stats: Optional[Dict] = None, zscore: Optional[
             for li, lag in enumerate(lags):
                 ss, cc = [], []
                 for srv, so in (alerts.get("recentAlertCounts") or {}).items():
+                    if not keep(srv):
+                        continue
                     for svc, lagd in so.items():
                         c = lagd.get(str(lag))
                         if c:

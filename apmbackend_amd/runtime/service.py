@@ -107,6 +107,8 @@ class IngestService:
                                       self.cfg["streamCalcStats"].get("resumeFileSaveFrequencyInSeconds", 60)))
         restored = self._restore() if (self.ckpt_dir and engine == "native") else False
         if not restored:
+            if engine == "native" and as_bool(g.get("importReferenceResume", False)):
+                self._import_reference(mine)
             for f in self.files:
                 self.native.add_file(f, KIND_CODE[file_kind(f)], self.server_of(f))
         self.file_ids = {p: i for i, (p, _k, _s) in enumerate(self.native.files())}
@@ -186,6 +188,19 @@ class IngestService:
         except Exception as e:
             log.error("checkpoint %s could not be loaded (%s); starting fresh", ck, e)
             raise
+
+    def _import_reference(self, servers):
+        """Cut-over from a running reference deployment: seed stats buckets, the release heap,
+        the z-score histories and alert cooldowns from its JSON resume files."""
+        from .resume_compat import import_reference_resume, read_docs
+        paths = [self.cfg["streamCalcStats"].get("resumeFileFullPath"),
+                 self.cfg["streamCalcZScore"].get("resumeFileFullPath"),
+                 self.cfg["streamProcessAlerts"].get("alertsResumeFileFullPath")]
+        stats, zscore, alerts = read_docs(paths)
+        if not (stats or zscore or alerts):
+            return
+        info = import_reference_resume(self.eng, stats, zscore, alerts, servers=set(servers))
+        log.info("imported reference resume files: %s", info)
 
     def _restore_offsets(self):
         _, tp = self._ckpt_paths()
