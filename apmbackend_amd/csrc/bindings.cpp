@@ -135,7 +135,7 @@ py::dict metrics_dict(const EngineMetrics& m) {
   d["t_join_shards_ms"] = m.t_join_shards_ms; d["t_merge_ms"] = m.t_merge_ms;
   d["t_stats_tx_ms"] = m.t_stats_tx_ms; d["t_rollover_ms"] = m.t_rollover_ms;
   d["t_format_ms"] = m.t_format_ms; d["t_release_ms"] = m.t_release_ms;
-  d["formatted_bytes"] = m.formatted_bytes; d["format_fallbacks"] = m.format_fallbacks;
+  d["formatted_bytes"] = m.formatted_bytes; d["lockstep_rollovers"] = m.lockstep_rollovers; d["format_fallbacks"] = m.format_fallbacks;
   d["t_parse_ms"] = m.t_parse_ms; d["t_join_ms"] = m.t_join_ms; d["t_stats_ms"] = m.t_stats_ms;
   d["t_total_ms"] = m.t_total_ms;
   d["rollover_latency_ms"] = m.rollover_latency_ms;
@@ -326,12 +326,12 @@ PYBIND11_MODULE(_apm_native, m) {
         auto v = Engine::fleet_unique_id();
         return py::bytes((const char*)v.data(), v.size());
       })
-      .def("fleet_init", [](Engine& e, py::bytes uid, int nranks, int rank, int32_t cap) {
-        std::string s = uid;
-        std::vector<uint8_t> v(s.begin(), s.end());
+      .def("fleet_init", [](Engine& e, py::bytes uid, int nranks, int rank, int32_t cap, py::bytes clock_uid) {
+        std::string s = uid, c = clock_uid;
+        std::vector<uint8_t> v(s.begin(), s.end()), cv(c.begin(), c.end());
         py::gil_scoped_release rel;
-        e.fleet_init(v, nranks, rank, cap);
-      })
+        e.fleet_init(v, cv, nranks, rank, cap);
+      }, py::arg("uid"), py::arg("nranks"), py::arg("rank"), py::arg("cap"), py::arg("clock_uid") = py::bytes(""))
       .def("fleet_merged", [](Engine& e) {
         std::vector<double> v;
         { py::gil_scoped_release rel; v = e.fleet_merged(); }

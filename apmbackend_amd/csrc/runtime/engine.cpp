@@ -208,6 +208,12 @@ Engine::~Engine() {
     ncclCommDestroy(fleet_comm_);
     fleet_comm_ = nullptr;
   }
+  if (clock_comm_) {
+    hipStreamSynchronize(parse_stream_);
+    ncclCommDestroy(clock_comm_);
+    clock_comm_ = nullptr;
+  }
+  if (h_sync_) hipHostFree(h_sync_);
   hipStreamSynchronize(stream_);
   hipStreamSynchronize(parse_stream_);
   for (void* p : allocations_) hipFree(p);
@@ -535,6 +541,15 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
     const double w = (double)((long long)wm - (1LL << 62));
     if (w > watermark_) watermark_ = w;
   }
+  if (clock_comm_) {  // lock-step: the cache clock is the node-wide watermark
+    h_sync_[0] = watermark_;
+    HIP_OK(hipMemcpyAsync(d_sync_, h_sync_, 8, hipMemcpyHostToDevice, parse_stream_));
+    if (ncclAllReduce(d_sync_, d_sync_, 1, ncclDouble, ncclMax, clock_comm_, parse_stream_) != ncclSuccess)
+      throw std::runtime_error("ncclAllReduce(watermark) failed");
+    HIP_OK(hipMemcpyAsync(h_sync_, d_sync_, 8, hipMemcpyDeviceToHost, parse_stream_));
+    HIP_OK(hipStreamSynchronize(parse_stream_));
+    watermark_ = h_sync_[0];
+  }
   ++batch_no_;
 }
 
@@ -560,6 +575,7 @@ void Engine::stats_worker() {
     try {
       cur_text_ = &job.text;
       stats_for_batch(job.txs, job.t0);
+      sync_latest_locked(job.t0);
       fleet_exchange_locked();
       drain_sinks();
     } catch (const std::exception& e) {
@@ -1185,14 +1201,26 @@ std::vector<uint8_t> Engine::fleet_unique_id() {
   return std::vector<uint8_t>((uint8_t*)&id, (uint8_t*)&id + sizeof(id));
 }
 
-void Engine::fleet_init(const std::vector<uint8_t>& uid, int nranks, int rank, int32_t cap) {
+void Engine::fleet_init(const std::vector<uint8_t>& uid, const std::vector<uint8_t>& clock_uid, int nranks, int rank,
+                        int32_t cap) {
   flush();
-  if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("bad unique id size");
+  if (uid.size() != sizeof(ncclUniqueId) || (!clock_uid.empty() && clock_uid.size() != sizeof(ncclUniqueId)))
+    throw std::runtime_error("bad unique id size");
   ncclUniqueId id;
   std::memcpy(&id, uid.data(), sizeof(id));
   HIP_OK(hipSetDevice(cfg_.device));
   if (ncclCommInitRank(&fleet_comm_, nranks, id, rank) != ncclSuccess)
     throw std::runtime_error("ncclCommInitRank failed");
+  // Lock-step clocks: a second communicator owned by the ingest (main) thread -- RCCL
+  // communicators must not be driven from two threads at once.
+  if (!clock_uid.empty()) {
+    ncclUniqueId cid;
+    std::memcpy(&cid, clock_uid.data(), sizeof(cid));
+    if (ncclCommInitRank(&clock_comm_, nranks, cid, rank) != ncclSuccess)
+      throw std::runtime_error("ncclCommInitRank (clock) failed");
+    d_sync_ = (double*)dmalloc(64);
+    HIP_OK(hipHostMalloc((void**)&h_sync_, 64, hipHostMallocDefault));
+  }
   fleet_cap_ = cap;
   fleet_elems_ = (size_t)cap * cfg_.n_lags * NSTAT * 3;
   for (int i = 0; i < 2; ++i) {
@@ -1201,6 +1229,24 @@ void Engine::fleet_init(const std::vector<uint8_t>& uid, int nranks, int rank, i
     HIP_OK(hipEventCreateWithFlags(&fleet_ev_[i], hipEventDisableTiming));
   }
   fleet_rounds_ = 0;
+}
+
+// Stats thread: every rank rolls over when any rank saw a newer bucket, exactly as the single
+// reference stats process rolls over on the first tx of a new bucket from any JVM.
+void Engine::sync_latest_locked(double batch_t0) {
+  if (!clock_comm_) return;
+  int64_t* d = reinterpret_cast<int64_t*>(d_sync_) + 4;
+  HIP_OK(hipMemcpyAsync(d, &latest_, 8, hipMemcpyHostToDevice, comm_stream_));
+  if (ncclAllReduce(d, d, 1, ncclInt64, ncclMax, fleet_comm_, comm_stream_) != ncclSuccess)
+    throw std::runtime_error("ncclAllReduce(latest) failed");
+  int64_t g = 0;
+  HIP_OK(hipMemcpyAsync(&g, d, 8, hipMemcpyDeviceToHost, comm_stream_));
+  HIP_OK(hipStreamSynchronize(comm_stream_));
+  if (g > latest_) {
+    latest_ = g;
+    ++metrics_.lockstep_rollovers;
+    do_rollover(g, batch_t0);
+  }
 }
 
 void Engine::fleet_exchange_locked() {

@@ -113,7 +113,7 @@ struct Chunk {
 struct EngineMetrics {
   uint64_t batches = 0, bytes = 0, lines = 0, events = 0, tx = 0, tx_db = 0, tx_dropped = 0;
   uint64_t rollovers = 0, alerts = 0, alert_candidates = 0, series = 0, released = 0;
-  uint64_t formatted_bytes = 0, format_fallbacks = 0;
+  uint64_t formatted_bytes = 0, format_fallbacks = 0, lockstep_rollovers = 0;
   double t_parse_ms = 0, t_join_ms = 0, t_stats_ms = 0, t_total_ms = 0;
   double t_join_shards_ms = 0, t_merge_ms = 0;                 // split of t_join_ms
   double t_stats_tx_ms = 0, t_rollover_ms = 0, t_format_ms = 0, t_release_ms = 0;  // inside t_stats_ms
@@ -195,7 +195,10 @@ class Engine {
   void pack_service_moments(double* d_dst, int32_t n_services_cap, hipStream_t stream);
   // Native RCCL fleet exchange (see engine.cpp): rank 0 creates the id, every rank inits.
   static std::vector<uint8_t> fleet_unique_id();
-  void fleet_init(const std::vector<uint8_t>& uid, int nranks, int rank, int32_t n_services_cap);
+  // clock_uid non-empty: lock-step clocks (node-wide watermark + rollover bucket) so N ranks
+  // reproduce the single-stream reference per series.
+  void fleet_init(const std::vector<uint8_t>& uid, const std::vector<uint8_t>& clock_uid, int nranks, int rank,
+                  int32_t n_services_cap);
   std::vector<double> fleet_merged();  // [cap][n_lags][NSTAT][3] of the newest exchange
   uint64_t fleet_rounds() const { return fleet_rounds_; }
 
@@ -240,6 +243,7 @@ class Engine {
   void upload_series_tables(int32_t lo);
   void pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream);
   void fleet_exchange_locked();
+  void sync_latest_locked(double batch_t0);
   void stats_worker();
   void post_stats(std::vector<TxOut>&& txs, double t0);
   void drain_sinks();
@@ -251,6 +255,9 @@ class Engine {
   hipStream_t stream_ = nullptr, comm_stream_ = nullptr, parse_stream_ = nullptr;
   // fleet exchange
   ncclComm_t fleet_comm_ = nullptr;
+  ncclComm_t clock_comm_ = nullptr;
+  double* d_sync_ = nullptr;
+  double* h_sync_ = nullptr;
   int32_t fleet_cap_ = 0;
   size_t fleet_elems_ = 0;
   double* fleet_buf_[2] = {nullptr, nullptr};

@@ -660,6 +660,13 @@ class StatsOracle:
         svc.setdefault(lab, []).append(jsfmt.parse_int(tx.elapsed))
         self.heap.push(tx)
 
+    def advance_to(self, latest: int):
+        """Multi-rank lock-step (parallel/dist): another rank saw bucket ``latest`` -- roll
+        over as the single reference stats process would have at that tx."""
+        if latest > self.latest:
+            self.latest = latest
+            self.rollover()
+
     def rollover(self):
         self.rollovers += 1
         for srv in self.servers.values():
@@ -893,10 +900,14 @@ class PipelineOracle:
         if al is not None:
             self.al.append(al.to_csv())
 
-    def run_batches(self, batches: Iterable[Tuple[float, List[Tuple[str, List[str]]]]]):
-        """batches: (now_ms, [(file_path, [lines...]), ...])"""
+    def run_batches(self, batches: Iterable[Tuple[float, List[Tuple[str, List[str]]]]],
+                    sync_latest: Optional[Callable[[int], int]] = None):
+        """batches: (now_ms, [(file_path, [lines...]), ...]).  ``sync_latest`` (multi-rank)
+        maps this rank's latest bucket to the global one after every batch."""
         for now, chunks in batches:
             self.parse.begin_batch(now)
             for fp, lines in chunks:
                 for ln in lines:
                     self.parse.read_line(fp, ln)
+            if sync_latest is not None:
+                self.st.advance_to(sync_latest(self.st.latest))

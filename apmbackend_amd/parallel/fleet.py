@@ -53,16 +53,18 @@ class FleetBaseline:
     processed batch on its comm stream -- no Python, no host synchronisation on the hot path.
     """
 
-    def __init__(self, engine, world: int, rank: int, max_services: Optional[int] = None, group=None):
+    def __init__(self, engine, world: int, rank: int, max_services: Optional[int] = None, group=None,
+                 lockstep: bool = True):
         import torch.distributed as dist
         self.eng = engine
         self.world = world
         self.n_lags = len(engine.ecfg["lags"])
         self.cap = int(max_services or engine.cfg.get("gpu", {}).get("maxServices", 1 << 16))
         native = type(engine.eng)
-        obj = [native.fleet_unique_id() if rank == 0 else None]
+        obj = [(native.fleet_unique_id(), native.fleet_unique_id() if lockstep else b"") if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0, group=group)
-        engine.eng.fleet_init(obj[0], world, rank, self.cap)
+        uid, clock_uid = obj[0]
+        engine.eng.fleet_init(uid, world, rank, self.cap, clock_uid)
 
     @property
     def exchanges(self) -> int:

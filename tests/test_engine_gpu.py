@@ -217,3 +217,24 @@ def test_checkpoint_resume_is_seamless(tmp_path, mode):
     for k in ("transactions", "audit_db", "st", "fs", "al"):
         assert out[k] == full[k], k
     assert collections.Counter(out["db"]) == collections.Counter(full["db"])
+
+
+def test_lockstep_clock_communicator_single_rank_is_transparent():
+    """fleet_init with the lock-step clock communicator (nranks=1): every batch runs the
+    watermark all-reduce (main thread) and the latest-bucket all-reduce (stats thread); with
+    one rank the output must be unchanged."""
+    lines, bl = synth_batches(9, duration=400)
+    C = small_cfg("exact")
+    _, plain = _run_engine(C, bl)
+    eng = APMEngine(C, keep_text=True)
+    E = type(eng.eng)
+    eng.eng.fleet_init(E.fleet_unique_id(), 1, 0, 64, E.fleet_unique_id())
+    out = collections.defaultdict(list)
+    for now, chunks in bl:
+        eng.process_lines(chunks, now)
+        for k in ("transactions", "st", "fs", "al"):
+            out[k] += eng.take(k)
+    for k in ("transactions", "st", "fs", "al"):
+        assert out[k] == plain[k], k
+    m = eng.metrics()
+    assert m["lockstep_rollovers"] == 0 and eng.eng.fleet_rounds() == len(bl)
