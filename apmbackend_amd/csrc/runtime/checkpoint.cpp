@@ -115,7 +115,11 @@ void JoinShard::save(BinWriter& w) {
   }
   // per-file contexts
   w.pod<uint64_t>(soap_.size());
-  for (auto& kv : soap_) { w.pod(kv.first); w.str(kv.second.log_id); w.pod(kv.second.has_log_id); w.pod(kv.second.pull_next); }
+  for (size_t f = 0; f < soap_.v.size(); ++f) {
+    if (!soap_.present[f]) continue;
+    const SoapCtx& c = soap_.v[f];
+    w.pod((int32_t)f); w.str(c.log_id); w.pod(c.has_log_id); w.pod(c.pull_next);
+  }
   w.pod<uint64_t>(audit_.size());
   for (auto& kv : audit_) {
     const AuditCtx& c = kv.second;
@@ -185,7 +189,7 @@ void JoinShard::load(BinReader& rd) {
     c.log_id = rd.str();
     rd.pod(c.has_log_id);
     rd.pod(c.pull_next);
-    soap_[f] = std::move(c);
+    soap_.put(f) = std::move(c);
   }
   audit_.clear();
   for (uint64_t n = rd.pod<uint64_t>(); n; --n) {

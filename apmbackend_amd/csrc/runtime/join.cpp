@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cctype>
+#include <cstring>
 #ifdef APM_JOIN_PROF
 #include <x86intrin.h>
 #include <cstdio>
@@ -251,26 +252,54 @@ void JoinShard::output(int32_t server, int32_t svc, std::string_view log_id, dou
   t.elapsed = elapsed;
   t.to_db = to_db;
   t.toplevel = rs.toplevel;
-  // wire line, formatted here on the join worker (parallel across shards)
+  // wire line, formatted here on the join worker (parallel across shards): one append of a
+  // stack-built line on the common path
   t.line_off = (uint32_t)text_.size();
-  text_ += "tx|";
-  text_ += (*servers_)[server];
-  text_ += '|';
-  text_ += rs.norm;
-  text_ += '|';
-  text_ += log_id;
-  text_ += '|';
-  js::append_num(text_, acct);
-  text_ += '|';
-  js::append_num(text_, start);
-  text_ += '|';
-  js::append_num(text_, t.end_ms);
-  text_ += '|';
-  js::append_num(text_, elapsed);
-  text_ += '|';
-  text_ += rs.toplevel ? 'Y' : 'N';
-  t.line_len = (uint32_t)(text_.size() - t.line_off);
-  text_ += '\n';  // lines stay newline-terminated in the arena (zero-copy release, engine.cpp)
+  const std::string& srv = (*servers_)[server];
+  char buf[512];
+  const size_t fixed = srv.size() + rs.norm.size() + log_id.size() + 3 + 8 + 4 * 32 + 2;
+  if (fixed <= sizeof(buf)) {
+    char* p = buf;
+    auto put = [&](const char* q, size_t n) { std::memcpy(p, q, n); p += n; };
+    put("tx|", 3);
+    put(srv.data(), srv.size());
+    *p++ = '|';
+    put(rs.norm.data(), rs.norm.size());
+    *p++ = '|';
+    put(log_id.data(), log_id.size());
+    *p++ = '|';
+    p = js::put_num(p, acct);
+    *p++ = '|';
+    p = js::put_num(p, start);
+    *p++ = '|';
+    p = js::put_num(p, t.end_ms);
+    *p++ = '|';
+    p = js::put_num(p, elapsed);
+    *p++ = '|';
+    *p++ = rs.toplevel ? 'Y' : 'N';
+    t.line_len = (uint32_t)(p - buf);
+    *p++ = '\n';
+    text_.append(buf, (size_t)(p - buf));
+  } else {
+    text_ += "tx|";
+    text_ += srv;
+    text_ += '|';
+    text_ += rs.norm;
+    text_ += '|';
+    text_ += log_id;
+    text_ += '|';
+    js::append_num(text_, acct);
+    text_ += '|';
+    js::append_num(text_, start);
+    text_ += '|';
+    js::append_num(text_, t.end_ms);
+    text_ += '|';
+    js::append_num(text_, elapsed);
+    text_ += '|';
+    text_ += rs.toplevel ? 'Y' : 'N';
+    t.line_len = (uint32_t)(text_.size() - t.line_off);
+    text_ += '\n';  // lines stay newline-terminated in the arena (zero-copy release, engine.cpp)
+  }
   ++counters.tx;
   if (to_db) ++counters.tx_db;
 }
@@ -283,14 +312,13 @@ void JoinShard::save_acct(std::string_view acct_raw, int32_t file, int source, s
     ++counters.invalid_acct;  // reference logs (and throws via the $currLogFp typo, Q16: fixed)
     return;
   }
-  std::string log_id_buf;
   std::string_view log_id;
   if (source == 2) {
     if (alt_log_id.empty()) return;
     log_id = alt_log_id;
   } else {
-    auto it = soap_.find(file);
-    if (it != soap_.end() && it->second.has_log_id) { log_id_buf = it->second.log_id; log_id = log_id_buf; }
+    SoapCtx* sc = soap_.find(file);
+    if (sc && sc->has_log_id) log_id = sc->log_id;  // storage survives soap_.erase below
     else log_id = kUndef;
   }
   const uint64_t key = key_of(log_id);
@@ -343,17 +371,20 @@ void JoinShard::on_soap(const Event& e, std::string_view line, int32_t file, uin
         c.has_log_id = true;
       }
     }
-    soap_[file] = std::move(c);
+    SoapCtx& dst = soap_.put(file);
+    dst.log_id.swap(c.log_id);
+    dst.has_log_id = c.has_log_id;
+    dst.pull_next = false;
   } else if (m & PM_SOAP_OUT) {
     soap_.erase(file);
   } else {
-    auto it = soap_.find(file);
-    if (it == soap_.end()) return;
+    SoapCtx* it = soap_.find(file);
+    if (!it) return;
     if (m & PM_SOAP_ACCT) {
       save_acct(angle_field2(line), file, 0, {}, seq);
     } else if (m & PM_SOAP_KEY) {
-      it->second.pull_next = true;
-    } else if ((m & PM_SOAP_VALUE) && it->second.pull_next) {
+      it->pull_next = true;
+    } else if ((m & PM_SOAP_VALUE) && it->pull_next) {
       save_acct(angle_field2(line), file, 1, {}, seq);
     }
   }

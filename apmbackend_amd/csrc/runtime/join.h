@@ -139,6 +139,21 @@ class JoinShard {
     std::vector<std::pair<std::string, std::deque<AuditItem>>> service_map;
   };
   struct RawService { std::string raw; std::string norm; int32_t norm_id; bool toplevel; };
+  // per-file SOAP request context, indexed by file id (erase keeps the string's storage, so a
+  // view of the last logId stays valid until the file's next request line)
+  struct SoapTable {
+    std::vector<SoapCtx> v;
+    std::vector<uint8_t> present;
+    SoapCtx* find(int32_t f) { return (f >= 0 && (size_t)f < v.size() && present[f]) ? &v[f] : nullptr; }
+    SoapCtx& put(int32_t f) {
+      if ((size_t)f >= v.size()) { v.resize((size_t)f + 1); present.resize((size_t)f + 1, 0); }
+      present[f] = 1;
+      return v[f];
+    }
+    void erase(int32_t f) { if (f >= 0 && (size_t)f < present.size()) present[f] = 0; }
+    size_t size() const { size_t n = 0; for (uint8_t p : present) n += p; return n; }
+    void clear() { v.clear(); present.clear(); }
+  };
 
   static uint64_t key_of(std::string_view s) { return fnv1a64((const uint8_t*)s.data(), (int)s.size()); }
   int32_t raw_service(std::string_view raw) { return raw_service(std::string_view(), raw); }
@@ -170,7 +185,7 @@ class JoinShard {
   FlatMap<RecordEntry> record_;
   FlatMap<NeedEntry> need_;
   std::deque<std::pair<uint64_t, double>> acct_fifo_, record_fifo_, need_fifo_;
-  std::unordered_map<int32_t, SoapCtx> soap_;
+  SoapTable soap_;
   std::unordered_map<int32_t, AuditCtx> audit_;
   FlatMap<int32_t> raw_svc_map_;  // hash(raw name) -> id + 1
   std::vector<RawService> raw_svc_;

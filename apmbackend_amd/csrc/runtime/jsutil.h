@@ -259,6 +259,23 @@ inline std::string to_fixed(double x, int f) {
   return (neg ? "-" : "") + digits;
 }
 
+// Write String(x) at p (at most 32 bytes: JS number strings are <= 25 chars); returns the end.
+inline char* put_num(char* p, double x) {
+  if (x == x && x == std::trunc(x) && std::fabs(x) < 9007199254740992.0 && !(x == 0 && std::signbit(x))) {
+    char tmp[20];
+    int n = 0;
+    uint64_t v = (uint64_t)std::fabs(x);
+    do { tmp[n++] = (char)('0' + v % 10); v /= 10; } while (v);
+    if (x < 0) *p++ = '-';
+    while (n) *p++ = tmp[--n];
+    return p;
+  }
+  const std::string s = num_str(x);  // NaN, fractions, huge: rare
+  const size_t n = std::min<size_t>(s.size(), 32);
+  std::memcpy(p, s.data(), n);
+  return p + n;
+}
+
 // Append String(x): integral values below 2^53 take a digit loop, everything else num_str.
 inline void append_num(std::string& out, double x) {
   if (x == x && x == std::trunc(x) && std::fabs(x) < 9007199254740992.0 && !(x == 0 && std::signbit(x))) {

@@ -36,6 +36,13 @@ def _load_reference_baseline():
         return None
 
 
+PRESETS = {
+    "headline": {},
+    "config2": {"ring": "bfloat16"},
+    "firehose": {"servers": 32, "ejb": 2000, "providers": 1125, "tx_rate": 62.5, "ring": "bfloat16"},
+}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -47,11 +54,18 @@ def main():
     ap.add_argument("--tx-rate", type=float, default=250.0, help="log-time tx/s per JVM")
     ap.add_argument("--batch-seconds", type=float, default=10.0)
     ap.add_argument("--mean-mode", default="rolling", choices=["rolling", "exact"])
-    ap.add_argument("--ring", default="float64", choices=["float64", "float32"])
+    ap.add_argument("--ring", default="float64", choices=["float64", "float32", "bfloat16"])
+    ap.add_argument("--preset", default="headline", choices=sorted(PRESETS),
+                    help="BASELINE.json configs: headline (8 JVMs x 10k services per GPU, fp64 rings), "
+                         "config2 (same shard, bf16 moment rings), firehose (config 5: 256 JVMs / ~100k "
+                         "services on 8 GPUs -> 32 JVMs x 3125 services per GPU, bf16 rings)")
     ap.add_argument("--gen-threads", type=int, default=16)
     ap.add_argument("--no-warm", action="store_true")
     ap.add_argument("--sink", default="/dev/null", help="file receiving the db_insert stream")
     args = ap.parse_args()
+    for k, v in PRESETS[args.preset].items():  # a preset overrides the defaults it names
+        if getattr(args, k) == ap.get_default(k):
+            setattr(args, k, v)
 
     import torch
     rank = int(os.environ.get("RANK", "0"))
@@ -181,6 +195,8 @@ def main():
                 "global_batch": int(lines_total / args.steps),
                 "seq_len": 8640,
                 "parallelism": f"dp{world}",
+                "preset": args.preset,
+                "ring_dtype": args.ring,
             },
             "p50_ingest_to_alert_ms": round(p50_max, 3),
             "tx_per_s": round(tx_total / dt_max, 1),
