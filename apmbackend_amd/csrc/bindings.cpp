@@ -293,6 +293,8 @@ PYBIND11_MODULE(_apm_native, m) {
       .def("export_alert_counters", &Engine::export_alert_counters)
       .def("import_alert_counters", &Engine::import_alert_counters)
       .def("cooldown_by_service", &Engine::cooldown_by_service)
+      .def("set_server_context", &Engine::set_server_context, py::arg("server"), py::arg("ts_ms"),
+           py::arg("gauges"), py::arg("host_load") = 0.0)
       .def("load_state", &Engine::load_state, py::call_guard<py::gil_scoped_release>())
       .def("take_bytes", [](Engine& e, const std::string& k) {
         std::string b;

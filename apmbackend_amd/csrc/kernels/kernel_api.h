@@ -58,6 +58,24 @@ struct ZArgs {
   int32_t* rs_cnt;         // [NSTAT][rs_parts][rs_n]
 };
 
+// K14 per-JVM rollup fused with exogenous gauges (context.hip)
+constexpr int ROLLUP_ACC = 6;    // live series, window tx, window elapsed sum, max p95 bits, #avg sig, #p75 sig
+constexpr int ROLLUP_OUT = 15;   // see k_server_fuse
+constexpr int CTX_FIELDS = 18;   // [0] gauge ts (ms), [1..16] JmxEntry gauges, [17] VM load
+struct RollupArgs {
+  const WinStat* win;
+  const int32_t* series_server;
+  const ZOut* z[MAX_LAGS];
+  int32_t n_lags;
+  int32_t n_series;
+  int32_t n_servers;
+  int64_t edge_ts;
+  double tpm_div;
+  const double* ctx;              // [n_servers][CTX_FIELDS]
+  unsigned long long* acc;        // [n_servers][ROLLUP_ACC]
+  double* out;                    // [n_servers][ROLLUP_OUT]
+};
+
 // K12 st/fs encoding (format.hip)
 struct FormatArgs {
   const int32_t* perm;          // [n] series in emission order
@@ -122,6 +140,7 @@ int apm_release_merge(const int64_t* pool_end, const int64_t* pool_gid, int64_t 
 void apm_zscore(apm::ZArgs* a, int dtype_bytes, hipStream_t stream);
 void apm_zscore_warm(apm::ZArgs* a, int dtype_bytes, int fill, uint64_t seed, const apm::WinStat* base,
                      hipStream_t stream);
+void apm_server_rollup(apm::RollupArgs* a, hipStream_t stream);
 size_t apm_format_tmp_bytes(int32_t n_max);
 void apm_format_fixed_batch(const double* d_x, int n, int f, char* d_out, hipStream_t stream);
 int apm_format_plan(apm::FormatArgs* a, void* tmp, size_t tmp_bytes, hipStream_t stream);

@@ -159,6 +159,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   // K12 formatter
   d_ser_names_ = (int32_t*)dmalloc((size_t)S * 16);
   d_perm_ = (int32_t*)dmalloc((size_t)S * 4);
+  d_series_server_ = (int32_t*)dmalloc((size_t)S * 4);
   d_fmt_len_ = (uint32_t*)dmalloc((size_t)2 * (S + 1) * 4);
   d_fmt_off_ = (uint32_t*)dmalloc((size_t)2 * (S + 1) * 4);
   d_fmt_fallback_ = (int32_t*)dmalloc(4);
@@ -221,6 +222,7 @@ Engine::~Engine() {
   hipHostFree(h_events_); hipHostFree(h_counts_); hipHostFree(h_watermark_); hipHostFree(h_alerts_);
   hipHostFree(h_n_alerts_); hipHostFree(h_tx_); hipHostFree(h_gid_); hipHostFree(h_release_gid_);
   if (h_fmt_out_) hipHostFree(h_fmt_out_);
+  if (h_roll_out_) hipHostFree(h_roll_out_);
   hipHostFree(h_fmt_meta_);
   hipEventDestroy(ev_a_); hipEventDestroy(ev_b_);
   hipStreamDestroy(stream_); hipStreamDestroy(comm_stream_); hipStreamDestroy(parse_stream_);
@@ -877,6 +879,7 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
     apm_alert_eval(&aa, stream_);
   }
   ++rollover_idx_;
+  if (want(OUT_SX)) server_rollup(edge_ts);
   HIP_OK(hipMemcpyAsync(h_n_alerts_, d_n_alerts_, 4, hipMemcpyDeviceToHost, stream_));
   HIP_OK(hipStreamSynchronize(stream_));
   const double tr2 = now_ms();
@@ -884,6 +887,7 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   metrics_.rollover_latency_ms.push_back(tr2 - batch_t0);
   if (want(OUT_ST) || want(OUT_FS)) format_rollover_text(edge_ts);
   flush_alerts(edge_ts);
+  if (want(OUT_SX)) format_server_rollup(edge_ts);
   metrics_.t_format_ms += now_ms() - tr2;
 }
 
@@ -1049,6 +1053,87 @@ void Engine::format_rollover_text(int64_t edge_ts) {
   emit_bytes(OUT_FS, h_fmt_out_ + st_total, fs_total);
 }
 
+bool Engine::set_server_context(const std::string& server, double ts_ms, const std::vector<double>& gauges,
+                                double host_load) {
+  flush();
+  auto it = server_ids_.find(server);
+  if (it == server_ids_.end()) return false;
+  const int32_t v = it->second;
+  if (h_ctx_.size() < (size_t)(v + 1) * CTX_FIELDS) h_ctx_.resize((size_t)(v + 1) * CTX_FIELDS, 0.0);
+  double* row = h_ctx_.data() + (size_t)v * CTX_FIELDS;
+  row[0] = ts_ms;
+  for (int k = 0; k < 16; ++k) row[1 + k] = k < (int)gauges.size() ? gauges[k] : apm_nan();
+  row[17] = host_load;
+  ctx_dirty_ = true;
+  return true;
+}
+
+void Engine::server_rollup(int64_t edge_ts) {
+  const int32_t nsv = (int32_t)servers_.size();
+  if (nsv == 0) return;
+  if ((size_t)nsv > roll_cap_) {  // grow (rare: new servers)
+    size_t cap = std::max<size_t>(64, (size_t)nsv * 2), c1 = 0, c2 = 0, c3 = 0;
+    d_ctx_ = (double*)regrow(d_ctx_, c1 = roll_cap_ * CTX_FIELDS * 8, cap * CTX_FIELDS * 8);
+    d_roll_acc_ = (unsigned long long*)regrow(d_roll_acc_, c2 = roll_cap_ * ROLLUP_ACC * 8, cap * ROLLUP_ACC * 8);
+    d_roll_out_ = (double*)regrow(d_roll_out_, c3 = roll_cap_ * ROLLUP_OUT * 8, cap * ROLLUP_OUT * 8);
+    if (h_roll_out_) HIP_OK(hipHostFree(h_roll_out_));
+    HIP_OK(hipHostMalloc((void**)&h_roll_out_, cap * ROLLUP_OUT * 8, hipHostMallocDefault));
+    roll_cap_ = cap;
+    ctx_dirty_ = true;
+  }
+  if (series_server_uploaded_ < n_series_) {
+    const int32_t lo = series_server_uploaded_;
+    std::vector<int32_t> sv(n_series_ - lo);
+    for (int32_t s = lo; s < n_series_; ++s) sv[s - lo] = series_[s].server;
+    HIP_OK(hipMemcpyAsync(d_series_server_ + lo, sv.data(), sv.size() * 4, hipMemcpyHostToDevice, stream_));
+    HIP_OK(hipStreamSynchronize(stream_));
+    series_server_uploaded_ = n_series_;
+  }
+  if (ctx_dirty_) {
+    std::vector<double> full((size_t)nsv * CTX_FIELDS, 0.0);
+    std::copy(h_ctx_.begin(), h_ctx_.begin() + std::min(h_ctx_.size(), full.size()), full.begin());
+    HIP_OK(hipMemcpyAsync(d_ctx_, full.data(), full.size() * 8, hipMemcpyHostToDevice, stream_));
+    HIP_OK(hipStreamSynchronize(stream_));
+    ctx_dirty_ = false;
+  }
+  RollupArgs ra{};
+  ra.win = d_win_;
+  ra.series_server = d_series_server_;
+  for (int l = 0; l < cfg_.n_lags; ++l) ra.z[l] = lag_[l].out;
+  ra.n_lags = cfg_.n_lags;
+  ra.n_series = n_series_;
+  ra.n_servers = nsv;
+  ra.edge_ts = edge_ts;
+  ra.tpm_div = (double)cfg_.window * cfg_.interval_len / 60.0;
+  ra.ctx = d_ctx_;
+  ra.acc = d_roll_acc_;
+  ra.out = d_roll_out_;
+  apm_server_rollup(&ra, stream_);
+  HIP_OK(hipMemcpyAsync(h_roll_out_, d_roll_out_, (size_t)nsv * ROLLUP_OUT * 8, hipMemcpyDeviceToHost, stream_));
+}
+
+void Engine::format_server_rollup(int64_t edge_ts) {
+  // sx|ts|server|liveSeries|tpm|avg|maxP95|avgSignals|p75Signals|heapUtil|metaUtil|dsUtil|sysLoad|
+  //   threads|beanUtil|gaugeAgeS|vmLoad|flags      (NaN prints 'undefined', like nf())
+  const int32_t nsv = (int32_t)servers_.size();
+  std::string& out = blob_[OUT_SX];
+  for (int32_t v = 0; v < nsv; ++v) {
+    if (server_rank_[v] < 0) continue;  // no transactions yet
+    const double* o = h_roll_out_ + (size_t)v * ROLLUP_OUT;
+    out += "sx|";
+    out += std::to_string(edge_ts);
+    out += '|';
+    out += servers_[v];
+    static const int fx[ROLLUP_OUT] = {0, 2, 1, 1, 0, 0, 3, 3, 3, 2, 0, 3, 1, 2, 0};
+    for (int k = 0; k < ROLLUP_OUT; ++k) {
+      out += '|';
+      if (fx[k] == 0 && o[k] == o[k]) js::append_num(out, o[k]);
+      else out += js::nf(o[k], fx[k]);
+    }
+    out += '\n';
+  }
+}
+
 void Engine::format_rollover_text_host(int64_t edge_ts) {
   std::vector<WinStat> win;
   download_winstats(win);
@@ -1090,7 +1175,7 @@ void Engine::download_zout(int l, std::vector<ZOut>& out) {
 }
 
 const char* out_kind_name(int k) {
-  static const char* n[N_OUT] = {"transactions", "audit_db", "db", "st", "fs", "al"};
+  static const char* n[N_OUT] = {"transactions", "audit_db", "db", "st", "fs", "al", "sx"};
   return n[k];
 }
 

@@ -91,7 +91,8 @@ struct EngineConfig {
 //   ST            stats -> z      st lines  (fused internally; bridge only)
 //   FS            z -> alerts/db  fs lines (one per series per LAG)
 //   AL            alerts -> db    al lines
-enum OutKind { OUT_TRANSACTIONS = 0, OUT_AUDIT_DB, OUT_DB, OUT_ST, OUT_FS, OUT_AL, N_OUT };
+//   SX            new: per-JVM rollup fused with JMX / VM gauges (K14), one line per server
+enum OutKind { OUT_TRANSACTIONS = 0, OUT_AUDIT_DB, OUT_DB, OUT_ST, OUT_FS, OUT_AL, OUT_SX, N_OUT };
 const char* out_kind_name(int k);
 int out_kind_of(const std::string& name);
 
@@ -161,6 +162,12 @@ class Engine {
   // COPY/queue spool file, a pipe to the DB loader, /dev/null).  fd < 0 detaches.
   void set_sink_fd(const std::string& kind, int fd);
   uint64_t sink_bytes(const std::string& kind) const { return sink_bytes_[out_kind_of(kind)]; }
+
+  // Exogenous per-JVM gauges (JMX jx record fields in JmxEntry order + VM load) fused into the
+  // per-interval server rollup (K14, "sx" stream).  Returns false for a server this engine
+  // does not own.
+  bool set_server_context(const std::string& server, double ts_ms, const std::vector<double>& gauges,
+                          double host_load);
 
   // Binary checkpoint of the whole pipeline state (checkpoint.cpp).  load_state needs a freshly
   // constructed engine with the same LAG set / ring dtype / bucket layout.  Returns bytes written.
@@ -417,8 +424,20 @@ class Engine {
 
   // text outputs
   std::string blob_[N_OUT];
-  int sink_fd_[N_OUT] = {-1, -1, -1, -1, -1, -1};
-  uint64_t sink_bytes_[N_OUT] = {0, 0, 0, 0, 0, 0};
+  int sink_fd_[N_OUT] = {-1, -1, -1, -1, -1, -1, -1};
+  uint64_t sink_bytes_[N_OUT] = {0, 0, 0, 0, 0, 0, 0};
+  // K14 server rollup + exogenous context
+  std::vector<double> h_ctx_;                    // [servers][CTX_FIELDS]
+  bool ctx_dirty_ = false;
+  size_t roll_cap_ = 0;                          // servers the device buffers hold
+  double* d_ctx_ = nullptr;
+  unsigned long long* d_roll_acc_ = nullptr;
+  double* d_roll_out_ = nullptr;
+  double* h_roll_out_ = nullptr;
+  int32_t* d_series_server_ = nullptr;
+  int32_t series_server_uploaded_ = 0;
+  void server_rollup(int64_t edge_ts);
+  void format_server_rollup(int64_t edge_ts);
   EngineMetrics metrics_;
   hipEvent_t ev_a_, ev_b_;
 };

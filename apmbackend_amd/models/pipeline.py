@@ -24,7 +24,7 @@ from ..utils.timeparse import TzOffset
 KIND_CODE = {"SOAP": 0, "SERVER": 1, "APP": 2}
 
 # Output streams (engine.h OutKind); the bit index is the position in this tuple.
-OUT_KINDS = ("transactions", "audit_db", "db", "st", "fs", "al")
+OUT_KINDS = ("transactions", "audit_db", "db", "st", "fs", "al", "sx")
 # What the reference persists (db_insert queue): released + audit tx, fs, al.  `transactions`
 # and `st` are internal hand-offs that only the AMQP bridge needs.
 DB_OUTPUTS = ("audit_db", "db", "fs", "al")
@@ -179,6 +179,15 @@ class APMEngine:
 
     def take_bytes(self, kind: str) -> bytes:
         return self.eng.take_bytes(kind)
+
+    def set_server_context(self, jx_line: str, vm_load: float = 0.0) -> bool:
+        """Feed a JMX ``jx`` record (pull_jvm_stats) into the per-JVM gauge table fused by K14."""
+        from ..utils.records import entry_from_csv
+        e = entry_from_csv(jx_line)
+        if e is None or e.type != "jx":
+            return False
+        vals = [float("nan") if v is None else float(v) for v in e.values]
+        return self.eng.set_server_context(e.server, float(e.timestamp), vals, float(vm_load))
 
     def metrics(self) -> Dict[str, Any]:
         m = self.eng.metrics()

@@ -238,3 +238,51 @@ def test_lockstep_clock_communicator_single_rank_is_transparent():
         assert out[k] == plain[k], k
     m = eng.metrics()
     assert m["lockstep_rollovers"] == 0 and eng.eng.fleet_rounds() == len(bl)
+
+
+def test_server_rollup_fuses_window_stats_with_jmx_gauges():
+    """K14: per-JVM rollup (sx) == aggregate of that interval's st rows, joined with the JVM's
+    JMX gauges."""
+    from apmbackend_amd.runtime.jmx import SyntheticJmx
+    from apmbackend_amd.utils.records import JmxEntry
+    lines, bl = synth_batches(10, duration=500)
+    C = small_cfg("exact")
+    eng = APMEngine(C, keep_text=True)
+    syn = SyntheticJmx(5)
+    jx = JmxEntry.from_stats(START, "jvm00", syn.payload("jvm00")).to_csv()
+    sx, st = [], []
+    for i, (now, chunks) in enumerate(bl):
+        eng.process_lines(chunks, now)
+        if i == 3:
+            assert eng.set_server_context(jx, vm_load=1.5)
+            assert not eng.eng.set_server_context("nope", 0.0, [0.0] * 16, 0.0)
+        sx += eng.take("sx")
+        st += eng.take("st")
+    assert sx
+    by_ts = collections.defaultdict(list)
+    for l in st:
+        f = l.split("|")
+        by_ts[(f[1], f[2])].append(f)
+    e = entry_from = None
+    from apmbackend_amd.utils.records import entry_from_csv
+    g = entry_from_csv(jx)
+    heap = g.values[3] / g.values[5]
+    checked = 0
+    for l in sx:
+        f = l.split("|")
+        ts, srv = f[1], f[2]
+        rows = by_ts[(ts, srv)]
+        assert int(f[3]) == len(rows)
+        tpm = sum(float(r[4]) for r in rows)
+        assert abs(float(f[4]) - tpm) <= 0.01 * len(rows) + 1e-9
+        ns = [float(r[4]) * 5 for r in rows]  # tpm = n / 5 for the 30 x 10 s window
+        avgs = [float(r[5]) if r[5] != "undefined" else 0.0 for r in rows]
+        if sum(ns) > 0:
+            want = sum(a * n for a, n in zip(avgs, ns)) / sum(ns)
+            assert abs(float(f[5]) - want) <= 0.06
+        if srv == "jvm00" and f[9] != "undefined":
+            assert abs(float(f[9]) - heap) < 1e-3 and float(f[16]) == 1.5
+            checked += 1
+        if srv != "jvm00":
+            assert f[9] == "undefined"
+    assert checked > 0
