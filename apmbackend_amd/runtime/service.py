@@ -87,6 +87,8 @@ class IngestService:
 
         # ---- engine
         outs = set(DB_OUTPUTS)
+        if as_bool(g.get("serverRollup", False)):  # K14 per-JVM rollup fused with JMX gauges
+            outs.add("sx")
         if self.mode == "amqp":
             outs |= {"transactions" if "transactions" in self.bridge else "", "st" if "stats" in self.bridge else ""}
             outs.discard("")
@@ -151,6 +153,13 @@ class IngestService:
         if self.world > 1 and engine == "native" and as_bool(g.get("fleetBaseline", True)):
             from ..parallel.fleet import FleetBaseline
             self.fleet = FleetBaseline(self.eng, self.world, self.rank)
+
+        # ---- in-process JMX poller (config 4: JMX gauges fused into the per-JVM rollup)
+        self.jmx = None
+        if as_bool(g.get("fuseJmx", False)) and self.cfg.get("pullJvmStats", {}).get("jvmHosts"):
+            from .jmx import JvmStatsPoller, SyntheticJmx, run_cli
+            runner = SyntheticJmx().runner if as_bool(g.get("syntheticJmx", False)) else run_cli
+            self.jmx = JvmStatsPoller(self.cfg, self._on_jx, runner=runner, clock=clock)
 
         self.watcher = ConfigWatcher(self.cfg, self.reload, RESTART_KEYS) if self.cfg.get("apmConfigFilePath") else None
         self._stop = False
@@ -275,8 +284,23 @@ class IngestService:
                     prod.write_lines(ln for ln in blob.decode("utf-8").split("\n") if ln)
         return counts
 
+    def _on_jx(self, line: str):
+        """A JMX record: to the DB like pull_jvm_stats.js does, and into the engine's gauges."""
+        if self.eng is not None:
+            try:
+                load = os.getloadavg()[0]
+            except OSError:
+                load = float("nan")
+            self.eng.set_server_context(line, load)
+        if self.inserter is not None:
+            self.inserter.consume_line(line)
+        elif self.qm is not None:
+            self.producers["db"].write_line(line)
+
     def _housekeeping(self):
         now = self.clock()
+        if self.jmx is not None:
+            self.jmx.tick()
         if self.inserter is not None:
             self.inserter.tick()
         if self.notifier is not None:

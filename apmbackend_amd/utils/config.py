@@ -53,11 +53,18 @@ GPU_DEFAULTS: Dict[str, Any] = {
     "acctTtlSeconds": 120,            # acctCache stdTTL (:213)
     "needTtlSeconds": 30,             # needNumRecordCache stdTTL (:218)
     "timezone": "local",              # tz for 'YYYY-MM-DD HH:MM:SS,mmm' timestamps
-    "fleetBaseline": True,            # RCCL all-reduce of per-service moments
-    "commBucketBytes": 4 << 20,
-    "emitTextRecords": False,         # format fs/al/tx lines on device (K12) for sinks
+    "fleetBaseline": True,            # RCCL all-reduce of per-service moments + lock-step clocks
     "joinThreads": 0,                 # host join worker threads (0 = auto)
-    "checkpointDir": "",
+    "checkpointDir": "",              # binary engine checkpoints (+ tail offsets) per rank
+    "checkpointEverySeconds": 60,
+    "importReferenceResume": False,   # seed a fresh engine from the reference's JSON resume files
+    "outputMode": "inproc",           # inproc (DB insert stage in-process) | amqp (queue bridge) | none
+    "bridgeQueues": [],               # amqp mode: also mirror "transactions" / "stats"
+    "tailFromStart": False,           # File::Tail starts at EOF; true reads existing content
+    "serverRollup": False,            # K14 "sx" stream: per-JVM rollup fused with JMX / VM gauges
+    "fuseJmx": False,                 # JMX poller inside the engine process feeding K14
+    "syntheticJmx": False,            # use the synthetic WildFly CLI (tests / benchmarks)
+    "logFilePrefix": "apm_engine",
 }
 
 _BOOL_STRINGS = {"true": True, "false": False, "1": True, "0": False, "yes": True, "no": False}
