@@ -83,7 +83,7 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = True) -> str:
     newest = max(os.path.getmtime(o) for o in objs)
     if force or not os.path.exists(TARGET) or os.path.getmtime(TARGET) < newest:
         cmd = [hipcc(), "-shared", f"--offload-arch={ARCH}", "-o", TARGET + ".tmp"] + objs + [
-            "-L" + os.path.join(ROCM, "lib"), "-lamdhip64", "-lrccl", "-Wl,-rpath," + os.path.join(ROCM, "lib"),
+            "-L" + os.path.join(ROCM, "lib"), "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx", "-Wl,-rpath," + os.path.join(ROCM, "lib"),
             "-lpthread"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:

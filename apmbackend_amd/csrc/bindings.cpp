@@ -293,6 +293,14 @@ PYBIND11_MODULE(_apm_native, m) {
       .def("export_alert_counters", &Engine::export_alert_counters)
       .def("import_alert_counters", &Engine::import_alert_counters)
       .def("cooldown_by_service", &Engine::cooldown_by_service)
+      .def("set_trace", &Engine::set_trace)
+      .def("take_trace", [](Engine& e) {
+        std::vector<TraceEvent> t;
+        { py::gil_scoped_release rel; t = e.take_trace(); }
+        py::list out;
+        for (auto& x : t) out.append(py::make_tuple(std::string(x.name), x.t0_ms, x.t1_ms, x.tid, x.batch));
+        return out;
+      })
       .def("set_server_context", &Engine::set_server_context, py::arg("server"), py::arg("ts_ms"),
            py::arg("gauges"), py::arg("host_load") = 0.0)
       .def("load_state", &Engine::load_state, py::call_guard<py::gil_scoped_release>())

@@ -1,6 +1,8 @@
 // apm::Engine implementation -- see engine.h.
 #include "engine.h"
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include <unistd.h>
 
 #include <cerrno>
@@ -380,6 +382,7 @@ JoinCounters Engine::join_counters() const {
 void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const std::vector<Chunk>& chunks_in,
                            double now_override) {
   const double t0 = now_ms();
+  roctxRangePushA("apm.parse");
   if (n_bytes > cfg_.max_batch_bytes) throw std::runtime_error("batch larger than max_batch_bytes");
   if (chunks_in.size() > cfg_.max_chunks) throw std::runtime_error("too many chunks in batch");
   // Canonical order: chunks grouped by server (shard) then file, keeping the caller's order
@@ -463,6 +466,9 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
   }
   const double t1 = now_ms();
   metrics_.t_parse_ms += t1 - t0;
+  roctxRangePop();
+  roctxRangePushA("apm.join");
+  trace_event("parse", t0, t1, 0);
 
   // ---- join on the host, one task per server shard
   const double clock = now_override >= 0 ? now_override : watermark_;
@@ -531,6 +537,9 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
   const double t2 = now_ms();
   metrics_.t_join_ms += t2 - t1;
   metrics_.t_merge_ms += t2 - t1b;
+  roctxRangePop();
+  trace_event("join", t1, t1b, 0);
+  trace_event("merge", t1b, t2, 0);
 
   // ---- stats / z-score / alerts: handed to the stats thread, overlapping the next batch's
   // H2D + parse (parse stream) and host join (pool) with this batch's GPU stats work.
@@ -555,6 +564,20 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
   ++batch_no_;
 }
 
+void Engine::trace_event(const char* name, double t0, double t1, int tid) {
+  if (!trace_on_) return;
+  std::lock_guard<std::mutex> g(trace_mu_);
+  if (trace_.size() < 1000000) trace_.push_back(TraceEvent{name, t0, t1, tid, batch_no_});
+}
+
+std::vector<TraceEvent> Engine::take_trace() {
+  flush();
+  std::lock_guard<std::mutex> g(trace_mu_);
+  std::vector<TraceEvent> r;
+  r.swap(trace_);
+  return r;
+}
+
 void Engine::recycle_arena(std::string&& a) {
   a.clear();
   std::lock_guard<std::mutex> g(arena_mu_);
@@ -574,6 +597,7 @@ void Engine::stats_worker() {
       st_has_job_ = false;
     }
     const double t = now_ms();
+    roctxRangePushA("apm.stats");
     try {
       cur_text_ = &job.text;
       stats_for_batch(job.txs, job.t0);
@@ -584,6 +608,8 @@ void Engine::stats_worker() {
       std::lock_guard<std::mutex> g(st_mu_);
       st_error_ = e.what();
     }
+    roctxRangePop();
+    trace_event("stats", t, now_ms(), 1);
     {
       std::lock_guard<std::mutex> g(st_mu_);
       metrics_.t_stats_ms += now_ms() - t;
@@ -884,11 +910,14 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   HIP_OK(hipStreamSynchronize(stream_));
   const double tr2 = now_ms();
   metrics_.t_rollover_ms += tr2 - tr1;
+  trace_event("release", tr0, tr1, 1);
+  trace_event("window+zscore+alerts", tr1, tr2, 1);
   metrics_.rollover_latency_ms.push_back(tr2 - batch_t0);
   if (want(OUT_ST) || want(OUT_FS)) format_rollover_text(edge_ts);
   flush_alerts(edge_ts);
   if (want(OUT_SX)) format_server_rollup(edge_ts);
   metrics_.t_format_ms += now_ms() - tr2;
+  trace_event("format+sinks", tr2, now_ms(), 1);
 }
 
 void Engine::flush_alerts(int64_t edge_ts) {

@@ -106,6 +106,14 @@ struct BucketDump {
   std::vector<int32_t> values;
 };
 
+// One stage interval of the pipeline (Chrome-trace "X" event); tid 0 = ingest, 1 = stats.
+struct TraceEvent {
+  const char* name;
+  double t0_ms, t1_ms;
+  int tid;
+  uint64_t batch;
+};
+
 struct Chunk {
   int32_t file;
   uint64_t begin, end;  // byte range in the batch (must end with '\n')
@@ -168,6 +176,10 @@ class Engine {
   // does not own.
   bool set_server_context(const std::string& server, double ts_ms, const std::vector<double>& gauges,
                           double host_load);
+
+  // Stage tracing (also emitted as roctx ranges for rocprofv3 --marker-trace).
+  void set_trace(bool on) { trace_on_ = on; }
+  std::vector<TraceEvent> take_trace();
 
   // Binary checkpoint of the whole pipeline state (checkpoint.cpp).  load_state needs a freshly
   // constructed engine with the same LAG set / ring dtype / bucket layout.  Returns bytes written.
@@ -257,6 +269,10 @@ class Engine {
   bool want(int k) const { return (cfg_.outputs >> k) & 1u; }
   void* dmalloc(size_t bytes);
   void require_fresh(const char* what);
+  void trace_event(const char* name, double t0, double t1, int tid);
+  bool trace_on_ = false;
+  std::mutex trace_mu_;
+  std::vector<TraceEvent> trace_;
 
   EngineConfig cfg_;
   hipStream_t stream_ = nullptr, comm_stream_ = nullptr, parse_stream_ = nullptr;

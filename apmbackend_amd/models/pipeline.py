@@ -180,6 +180,19 @@ class APMEngine:
     def take_bytes(self, kind: str) -> bytes:
         return self.eng.take_bytes(kind)
 
+    def dump_trace(self, path: str, pid: int = 0) -> int:
+        """Write the recorded stage intervals (set_trace(True) first) as a Chrome trace."""
+        import json
+        ev = self.eng.take_trace()
+        names = {0: "ingest (parse + join)", 1: "stats thread"}
+        out = [{"name": "thread_name", "ph": "M", "pid": pid, "tid": t, "args": {"name": n}} for t, n in names.items()]
+        for name, t0, t1, tid, batch in ev:
+            out.append({"name": name, "ph": "X", "ts": t0 * 1000.0, "dur": max(0.0, (t1 - t0) * 1000.0), "pid": pid,
+                        "tid": tid, "args": {"batch": batch}})
+        with open(path, "w") as f:
+            json.dump({"traceEvents": out, "displayTimeUnit": "ms"}, f)
+        return len(ev)
+
     def set_server_context(self, jx_line: str, vm_load: float = 0.0) -> bool:
         """Feed a JMX ``jx`` record (pull_jvm_stats) into the per-JVM gauge table fused by K14."""
         from ..utils.records import entry_from_csv

@@ -62,6 +62,7 @@ def main():
     ap.add_argument("--gen-threads", type=int, default=16)
     ap.add_argument("--no-warm", action="store_true")
     ap.add_argument("--sink", default="/dev/null", help="file receiving the db_insert stream")
+    ap.add_argument("--trace", default=None, help="write a Chrome trace of the pipeline stages (per rank)")
     args = ap.parse_args()
     for k, v in PRESETS[args.preset].items():  # a preset overrides the defaults it names
         if getattr(args, k) == ap.get_default(k):
@@ -129,6 +130,8 @@ def main():
     t_gen = time.time() - t_gen
 
     fleet = FleetBaseline(eng, world, rank) if dist is not None else None
+    if args.trace:
+        eng.eng.set_trace(True)
 
     def step(i):
         ptr, n, chunks = batches[i]
@@ -209,6 +212,8 @@ def main():
             "db_insert_bytes_total": out_bytes,
         }
         print(json.dumps(out), flush=True)
+    if args.trace:
+        eng.dump_trace(args.trace if world == 1 else f"{args.trace}.rank{rank}", pid=rank)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
