@@ -165,6 +165,11 @@ class IngestService:
         self._stop = False
         self._gc_requested = False
         self.batches = 0
+        self.polls = 0
+        # fault injection: {"rank", "dropBatchEvery", "duplicateBatchEvery",
+        # "exitAtBatch", "exitCode"} -- exercises restarts, checkpoint resume and data loss paths
+        self.fault = dict(g.get("faultInjection") or {})
+        self.faults = {"dropped": 0, "duplicated": 0}
         self.last_ckpt = clock()
         self.last_stat = clock()
         self._m0 = self._metrics()
@@ -357,8 +362,23 @@ class IngestService:
         buf, chunks = self.tailer.poll()
         if not chunks:
             return 0
+        self.polls += 1
+        fi = self.fault
+        if fi and fi.get("rank", self.rank) == self.rank:
+            if fi.get("exitAtBatch") and self.polls == int(fi["exitAtBatch"]):
+                log.error("fault injection: exiting at batch %d", self.polls)
+                os._exit(int(fi.get("exitCode", 13)))
+            if fi.get("dropBatchEvery") and self.polls % int(fi["dropBatchEvery"]) == 0:
+                log.warning("fault injection: dropping batch %d (%d bytes)", self.polls, len(buf))
+                self.faults["dropped"] += 1
+                return len(buf)
         self.native.process_batch(buf, chunks, -1.0)
         self.batches += 1
+        if fi and fi.get("rank", self.rank) == self.rank and fi.get("duplicateBatchEvery") \
+                and self.polls % int(fi["duplicateBatchEvery"]) == 0:
+            log.warning("fault injection: replaying batch %d", self.polls)
+            self.faults["duplicated"] += 1
+            self.native.process_batch(buf, chunks, -1.0)
         self._drain_outputs()
         return len(buf)
 

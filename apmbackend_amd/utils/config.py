@@ -65,6 +65,7 @@ GPU_DEFAULTS: Dict[str, Any] = {
     "fuseJmx": False,                 # JMX poller inside the engine process feeding K14
     "syntheticJmx": False,            # use the synthetic WildFly CLI (tests / benchmarks)
     "logFilePrefix": "apm_engine",
+    "faultInjection": {},             # {"rank", "dropBatchEvery", "duplicateBatchEvery", "exitAtBatch"}
 }
 
 _BOOL_STRINGS = {"true": True, "false": False, "1": True, "0": False, "yes": True, "no": False}

@@ -1,0 +1,72 @@
+"""Host C++ under AddressSanitizer + UndefinedBehaviorSanitizer: the join workers replay
+parse-kernel events (from the Python model of the kernels) and must (a) run clean under the
+sanitizers and (b) produce the same tx stream as the oracle.  GPU sanitizers are not used
+(host code only: every -fsanitize flag is passed with -Xarch_host)."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+from apmbackend_amd.models.oracle import ParseOracle, file_kind
+from apmbackend_amd.ops.parse_ref import parse_batch
+from apmbackend_amd.utils.synth import Generator, SynthConfig, batches, with_watermarks
+from apmbackend_amd.utils.timeparse import TzOffset
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "apmbackend_amd", "csrc")
+UTC = TzOffset("UTC")
+KINDS = {"SOAP": 0, "SERVER": 1, "APP": 2}
+
+pytestmark = pytest.mark.skipif(shutil.which("hipcc") is None and not os.path.exists("/opt/rocm/bin/hipcc"),
+                                reason="hipcc not available")
+
+
+def build(tmp):
+    exe = os.path.join(tmp, "join_replay")
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    san = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+           "-Xarch_host", "-fno-omit-frame-pointer", "-Xarch_host", "-fno-sanitize-recover=all"]
+    cmd = [hipcc, "-O1", "-g", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950", *san, "-I", CSRC,
+           os.path.join(ROOT, "tests", "native", "join_replay.cpp"), os.path.join(CSRC, "runtime", "join.cpp"),
+           "-o", exe, "-fsanitize=address,undefined"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return exe
+
+
+def test_join_under_asan_ubsan(tmp_path):
+    cfg = SynthConfig(servers=2, duration_s=240, tx_per_sec_per_server=3, seed=13, audit_fraction=0.3,
+                      soap_late_fraction=0.4, missing_logid_fraction=0.05, baf_fraction=0.5)
+    lines = Generator(cfg).generate()
+    bl = with_watermarks(batches(lines, cfg.start_ms, 5.0), UTC)
+    want = []
+    po = ParseOracle(lambda q, l: want.append(f"{q}\t{l}"), tz=UTC)
+    for now, chunks in bl:
+        po.begin_batch(now)
+        for fp, ls in chunks:
+            for ln in ls:
+                po.read_line(fp, ln)
+    paths = sorted(lines)
+    fid = {p: i for i, p in enumerate(paths)}
+    d = tmp_path / "replay"
+    d.mkdir()
+    with open(d / "files.txt", "w") as f:
+        for p in paths:
+            f.write(f"{p}\t{KINDS[file_kind(p)]}\t{p.split('/')[2]}\n")
+    fo = {}
+    for b, (now, chunks) in enumerate(bl):
+        bch = [(KINDS[file_kind(fp)], ("\n".join(ls) + "\n").encode()) for fp, ls in chunks]
+        cf = [fid[fp] for fp, _ in chunks]
+        ev, _, _, buf = parse_batch(bch, UTC, fo, cf)
+        (d / f"batch_{b}.events").write_bytes(ev.tobytes())
+        (d / f"batch_{b}.bytes").write_bytes(buf)
+        (d / f"batch_{b}.meta").write_text(f"{now:.0f}\n" + "\n".join(map(str, cf)) + "\n")
+    exe = build(str(tmp_path))
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:halt_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    r = subprocess.run([exe, str(d), str(len(bl))], capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr
+    got = r.stdout.splitlines()
+    assert got == want and len(want) > 100

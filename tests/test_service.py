@@ -155,3 +155,34 @@ def test_request_gc_and_reload(tmp_path):
     svc.reload(C2)
     assert svc.inserter.limit == 7
     svc.shutdown()
+
+
+def test_fault_injection_drop_and_duplicate(tmp_path):
+    C, lines, mapping, sc = make_env(tmp_path, duration=120)
+    C["gpu"]["faultInjection"] = {"dropBatchEvery": 5, "duplicateBatchEvery": 7}
+    svc = IngestService(C, engine="cpu-oracle", files=sorted(mapping.values()), rank=0, world=1,
+                        server_of_path=srv_of)
+    feed_in_steps(svc, lines, mapping, sc)
+    n = len(batches(lines, sc.start_ms, 5.0))
+    assert svc.faults == {"dropped": n // 5, "duplicated": len([i for i in range(1, n + 1) if i % 7 == 0 and i % 5])}
+    assert svc.native.batches == n - n // 5 + svc.faults["duplicated"]
+    svc.shutdown()
+
+
+def test_fault_injection_exit(tmp_path):
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
+        "from test_service import *\n"
+        "import pathlib\n"
+        "tmp = pathlib.Path(%r)\n"
+        "C, lines, mapping, sc = make_env(tmp, duration=60)\n"
+        "C['gpu']['faultInjection'] = {'exitAtBatch': 3, 'exitCode': 17}\n"
+        "svc = IngestService(C, engine='cpu-oracle', files=sorted(mapping.values()), rank=0, world=1, "
+        "server_of_path=srv_of)\n"
+        "feed_in_steps(svc, lines, mapping, sc)\n"
+    ) % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))), os.path.dirname(os.path.abspath(__file__)),
+         str(tmp_path))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, timeout=120)
+    assert r.returncode == 17, r.stderr.decode()[-2000:]
