@@ -133,6 +133,7 @@ py::dict metrics_dict(const EngineMetrics& m) {
   d["tx"] = m.tx; d["tx_db"] = m.tx_db; d["tx_dropped"] = m.tx_dropped; d["rollovers"] = m.rollovers;
   d["alerts"] = m.alerts; d["alert_candidates"] = m.alert_candidates; d["released"] = m.released;
   d["t_join_shards_ms"] = m.t_join_shards_ms; d["t_merge_ms"] = m.t_merge_ms;
+  d["t_shard_busy_ms"] = m.t_shard_busy_ms; d["t_shard_max_ms"] = m.t_shard_max_ms;
   d["t_stats_tx_ms"] = m.t_stats_tx_ms; d["t_rollover_ms"] = m.t_rollover_ms;
   d["t_format_ms"] = m.t_format_ms; d["t_release_ms"] = m.t_release_ms;
   d["formatted_bytes"] = m.formatted_bytes; d["lockstep_rollovers"] = m.lockstep_rollovers; d["format_fallbacks"] = m.format_fallbacks;
@@ -254,12 +255,17 @@ PYBIND11_MODULE(_apm_native, m) {
            py::arg("buf"), py::arg("chunks"), py::arg("now") = -1.0)
       .def("process_batch_ptr",
            [](Engine& e, uintptr_t ptr, uint64_t n, const std::vector<std::tuple<int32_t, uint64_t, uint64_t>>& chunks,
-              double now) {
+              double now, uintptr_t next_ptr, uint64_t next_n,
+              const std::vector<std::tuple<int32_t, uint64_t, uint64_t>>& next_chunks) {
              auto ch = chunks_from(chunks);
+             auto nch = chunks_from(next_chunks);
              py::gil_scoped_release rel;
-             e.process_batch((const uint8_t*)ptr, n, ch, now);
+             e.process_batch((const uint8_t*)ptr, n, ch, now, next_ptr ? (const uint8_t*)next_ptr : nullptr, next_n,
+                             next_ptr ? &nch : nullptr);
            },
-           py::arg("ptr"), py::arg("n"), py::arg("chunks"), py::arg("now") = -1.0)
+           py::arg("ptr"), py::arg("n"), py::arg("chunks"), py::arg("now") = -1.0, py::arg("next_ptr") = 0,
+           py::arg("next_n") = 0,
+           py::arg("next_chunks") = std::vector<std::tuple<int32_t, uint64_t, uint64_t>>())
       .def("take", &Engine::take, py::call_guard<py::gil_scoped_release>())
       .def("flush", &Engine::flush, py::call_guard<py::gil_scoped_release>())
       .def("save_state", &Engine::save_state, py::call_guard<py::gil_scoped_release>())

@@ -20,7 +20,7 @@
 
 namespace apm {
 
-constexpr uint32_t kCkptVersion = 1;
+constexpr uint32_t kCkptVersion = 2;
 
 class BinWriter {
  public:

@@ -90,7 +90,7 @@ void JoinShard::save(BinWriter& w) {
   w.pod(counters);
   // raw service interning (order defines the ids)
   w.pod<uint64_t>(raw_svc_.size());
-  for (auto& r : raw_svc_) { w.str(r.raw); w.str(r.norm); w.pod(r.norm_id); w.pod(r.toplevel); }
+  for (auto& r : raw_svc_) { w.str(r.raw); w.str(r.norm); w.pod(r.norm_id); w.pod(r.toplevel); w.pod(r.hash); }
   // TTL caches
   w.pod<uint64_t>(acct_.size());
   acct_.for_each([&](uint64_t k, AcctEntry& e) { w.pod(k); w.pod(e); });
@@ -143,6 +143,8 @@ void JoinShard::load(BinReader& rd) {
   rd.pod(counters);
   raw_svc_.clear();
   raw_svc_map_.clear();
+  svc_info_.clear();
+  svc_text_.clear();
   const uint64_t nr = rd.pod<uint64_t>();
   for (uint64_t i = 0; i < nr; ++i) {
     RawService r;
@@ -150,8 +152,11 @@ void JoinShard::load(BinReader& rd) {
     r.norm = rd.str();
     rd.pod(r.norm_id);
     rd.pod(r.toplevel);
-    const uint64_t h = fnv1a64((const uint8_t*)r.raw.data(), (int)r.raw.size());
-    if (!raw_svc_map_.find(h)) raw_svc_map_[h] = (int32_t)i + 1;  // first occurrence wins, as when built
+    rd.pod(r.hash);
+    if (!raw_svc_map_.find(r.hash)) raw_svc_map_[r.hash] = (int32_t)i + 1;  // first occurrence wins, as when built
+    svc_info_.push_back(SvcInfo{(uint32_t)svc_text_.size(), (uint32_t)r.norm.size(), r.norm_id, (uint32_t)r.raw.size(),
+                                r.toplevel});
+    svc_text_ += r.norm;
     raw_svc_.push_back(std::move(r));
   }
   acct_.clear();
@@ -220,6 +225,7 @@ void JoinShard::load(BinReader& rd) {
 
 uint64_t Engine::save_state(const std::string& path) {
   flush();
+  if (prefetched_) throw std::runtime_error("save_state: a prefetched batch is pending (process it first)");
   HIP_OK(hipStreamSynchronize(parse_stream_));
   HIP_OK(hipStreamSynchronize(stream_));
   HIP_OK(hipStreamSynchronize(comm_stream_));

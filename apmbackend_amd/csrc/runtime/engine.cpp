@@ -27,21 +27,28 @@ double now_ms() {
 }  // namespace
 
 // ----------------------------------------------------------------------------- thread pool
+// Static task placement: task t always runs on worker t % W.  A join shard's working set (its
+// TTL maps, several MB) then stays in one core's L2 / one CCD's L3 from batch to batch; with
+// first-come task grabbing every batch moved each shard to a cold core (measured: the same
+// join ran 2.2x slower per shard inside the engine than alone).
 ThreadPool::ThreadPool(int n) {
   for (int i = 0; i < n; ++i) {
-    workers_.emplace_back([this]() {
+    workers_.emplace_back([this, i, n]() {
       uint64_t seen = 0;
       for (;;) {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&]() { return stop_ || gen_ != seen; });
         if (stop_) return;
         seen = gen_;
-        while (next_ < n_tasks_) {
-          const int t = next_++;
-          lk.unlock();
-          (*fn_)(t);
+        const int n_tasks = n_tasks_;
+        const std::function<void(int)>* fn = fn_;
+        lk.unlock();
+        int mine = 0;
+        for (int t = i; t < n_tasks; t += n) { (*fn)(t); ++mine; }
+        if (mine) {
           lk.lock();
-          if (++done_ == n_tasks_) done_cv_.notify_all();
+          done_ += mine;
+          if (done_ == n_tasks_) done_cv_.notify_all();
         }
       }
     });
@@ -66,7 +73,6 @@ void ThreadPool::run(int n_tasks, const std::function<void(int)>& fn) {
   std::unique_lock<std::mutex> lk(mu_);
   fn_ = &fn;
   n_tasks_ = n_tasks;
-  next_ = 0;
   done_ = 0;
   ++gen_;
   cv_.notify_all();
@@ -95,20 +101,23 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   const int32_t S = cfg_.max_series;
   // parse
   d_bytes_ = (uint8_t*)dmalloc(cfg_.max_batch_bytes + 256);
-  HIP_OK(hipHostMalloc((void**)&h_bytes_, cfg_.max_batch_bytes + 256, hipHostMallocDefault));
+  for (int k = 0; k < 2; ++k) {
+    ParseSlot& ps = pslot_[k];
+    HIP_OK(hipHostMalloc((void**)&ps.h_bytes, cfg_.max_batch_bytes + 256, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void**)&ps.h_chunk_begin, (cfg_.max_chunks + 2) * 4, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void**)&ps.h_chunk_kind, cfg_.max_chunks + 2, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void**)&ps.h_chunk_file, (cfg_.max_chunks + 2) * 4, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void**)&ps.h_events, (size_t)cfg_.max_lines * sizeof(Event), hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void**)&ps.h_counts, 16, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void**)&ps.h_watermark, 8, hipHostMallocDefault));
+  }
   d_chunk_begin_ = (uint32_t*)dmalloc((cfg_.max_chunks + 2) * 4);
   d_chunk_kind_ = (uint8_t*)dmalloc(cfg_.max_chunks + 2);
   d_chunk_file_ = (uint32_t*)dmalloc((cfg_.max_chunks + 2) * 4);
-  HIP_OK(hipHostMalloc((void**)&h_chunk_begin_, (cfg_.max_chunks + 2) * 4, hipHostMallocDefault));
-  HIP_OK(hipHostMalloc((void**)&h_chunk_kind_, cfg_.max_chunks + 2, hipHostMallocDefault));
-  HIP_OK(hipHostMalloc((void**)&h_chunk_file_, (cfg_.max_chunks + 2) * 4, hipHostMallocDefault));
   d_parse_ws_ = dmalloc(apm_parse_workspace_bytes(cfg_.max_batch_bytes, cfg_.max_lines, cfg_.max_chunks));
   d_events_ = (Event*)dmalloc((size_t)cfg_.max_lines * sizeof(Event));
-  HIP_OK(hipHostMalloc((void**)&h_events_, (size_t)cfg_.max_lines * sizeof(Event), hipHostMallocDefault));
   d_counts_ = (uint32_t*)dmalloc(16);
-  HIP_OK(hipHostMalloc((void**)&h_counts_, 16, hipHostMallocDefault));
   d_watermark_ = (unsigned long long*)dmalloc(8);
-  HIP_OK(hipHostMalloc((void**)&h_watermark_, 8, hipHostMallocDefault));
   d_file_open_ = (uint8_t*)dmalloc(1 << 16);
   // stats
   d_counts_cells_ = (int32_t*)dmalloc((size_t)NSLOT * S * 4);
@@ -220,8 +229,11 @@ Engine::~Engine() {
   hipStreamSynchronize(stream_);
   hipStreamSynchronize(parse_stream_);
   for (void* p : allocations_) hipFree(p);
-  hipHostFree(h_bytes_); hipHostFree(h_chunk_begin_); hipHostFree(h_chunk_kind_); hipHostFree(h_chunk_file_);
-  hipHostFree(h_events_); hipHostFree(h_counts_); hipHostFree(h_watermark_); hipHostFree(h_alerts_);
+  for (auto& ps : pslot_) {
+    hipHostFree(ps.h_bytes); hipHostFree(ps.h_chunk_begin); hipHostFree(ps.h_chunk_kind); hipHostFree(ps.h_chunk_file);
+    hipHostFree(ps.h_events); hipHostFree(ps.h_counts); hipHostFree(ps.h_watermark);
+  }
+  hipHostFree(h_alerts_);
   hipHostFree(h_n_alerts_); hipHostFree(h_tx_); hipHostFree(h_gid_); hipHostFree(h_release_gid_);
   if (h_fmt_out_) hipHostFree(h_fmt_out_);
   if (h_roll_out_) hipHostFree(h_roll_out_);
@@ -379,10 +391,10 @@ JoinCounters Engine::join_counters() const {
 }
 
 // ----------------------------------------------------------------------------- batch
-void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const std::vector<Chunk>& chunks_in,
-                           double now_override) {
+// Stage a batch into a parse slot (canonical chunk order, pinned staging if needed) and enqueue
+// H2D + K1/K2 on the parse stream.  Nothing waits here.
+void Engine::launch_parse(ParseSlot& ps, const uint8_t* host_bytes, uint64_t n_bytes, const std::vector<Chunk>& chunks_in) {
   const double t0 = now_ms();
-  roctxRangePushA("apm.parse");
   if (n_bytes > cfg_.max_batch_bytes) throw std::runtime_error("batch larger than max_batch_bytes");
   if (chunks_in.size() > cfg_.max_chunks) throw std::runtime_error("too many chunks in batch");
   // Canonical order: chunks grouped by server (shard) then file, keeping the caller's order
@@ -392,7 +404,7 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
   std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
     return files_[chunks_in[a].file].server < files_[chunks_in[b].file].server;
   });
-  std::vector<int32_t> chunk_file(chunks_in.size());
+  ps.chunk_file.assign(chunks_in.size(), 0);
   uint64_t off = 0;
   // Fast path: chunks already canonical and contiguous from 0 (bench corpus, tailer output) ->
   // no host copy; the H2D reads the caller's (ideally pinned) buffer directly.
@@ -403,20 +415,20 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
     off = c.end;
   }
   canonical = canonical && off == n_bytes && n_bytes + 64 <= cfg_.max_batch_bytes + 256;
-  const uint8_t* hb = h_bytes_;
+  ps.hb = ps.h_bytes;
   if (canonical) {
-    hb = host_bytes;
+    ps.hb = host_bytes;
     for (size_t k = 0; k < order.size(); ++k) {
       const Chunk& c = chunks_in[k];
       if (c.end > c.begin && host_bytes[c.end - 1] != '\n') throw std::runtime_error("chunk must end with a newline");
-      h_chunk_begin_[k] = (uint32_t)c.begin;
-      h_chunk_kind_[k] = files_[c.file].kind;
-      h_chunk_file_[k] = (uint32_t)c.file;
-      chunk_file[k] = c.file;
+      ps.h_chunk_begin[k] = (uint32_t)c.begin;
+      ps.h_chunk_kind[k] = files_[c.file].kind;
+      ps.h_chunk_file[k] = (uint32_t)c.file;
+      ps.chunk_file[k] = c.file;
     }
   } else {
     off = 0;
-    const bool in_place = host_bytes == h_bytes_;
+    const bool in_place = host_bytes == ps.h_bytes;
     std::vector<uint8_t> tmp_copy;
     const uint8_t* src = host_bytes;
     if (in_place) {  // caller filled our staging buffer: copy aside before re-layout
@@ -427,45 +439,85 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
       const Chunk& c = chunks_in[order[k]];
       const uint64_t len = c.end - c.begin;
       if (len > 0 && src[c.end - 1] != '\n') throw std::runtime_error("chunk must end with a newline");
-      std::memcpy(h_bytes_ + off, src + c.begin, len);
-      h_chunk_begin_[k] = (uint32_t)off;
-      h_chunk_kind_[k] = files_[c.file].kind;
-      h_chunk_file_[k] = (uint32_t)c.file;
-      chunk_file[k] = c.file;
+      std::memcpy(ps.h_bytes + off, src + c.begin, len);
+      ps.h_chunk_begin[k] = (uint32_t)off;
+      ps.h_chunk_kind[k] = files_[c.file].kind;
+      ps.h_chunk_file[k] = (uint32_t)c.file;
+      ps.chunk_file[k] = c.file;
       off += len;
     }
-    std::memset(h_bytes_ + off, 0, 64);
+    std::memset(ps.h_bytes + off, 0, 64);
   }
   const uint32_t n_chunks = (uint32_t)order.size();
-  h_chunk_begin_[n_chunks] = (uint32_t)off;
+  ps.h_chunk_begin[n_chunks] = (uint32_t)off;
+  ps.n_bytes = off;
+  ps.src = host_bytes;
+  ps.src_n = n_bytes;
   metrics_.bytes += off;
   ++metrics_.batches;
 
-  // ---- K1/K2 on the GPU
-  HIP_OK(hipMemcpyAsync(d_bytes_, hb, off, hipMemcpyHostToDevice, parse_stream_));
+  // ---- K1/K2 on the GPU (d_bytes_, d_events_, d_counts_ are free: the previous parse was
+  // finished -- its events copied to its own host slot -- before this launch)
+  HIP_OK(hipMemcpyAsync(d_bytes_, ps.hb, off, hipMemcpyHostToDevice, parse_stream_));
   HIP_OK(hipMemsetAsync(d_bytes_ + off, 0, 64, parse_stream_));
-  HIP_OK(hipMemcpyAsync(d_chunk_begin_, h_chunk_begin_, (n_chunks + 1) * 4, hipMemcpyHostToDevice, parse_stream_));
-  HIP_OK(hipMemcpyAsync(d_chunk_kind_, h_chunk_kind_, n_chunks + 1, hipMemcpyHostToDevice, parse_stream_));
-  HIP_OK(hipMemcpyAsync(d_chunk_file_, h_chunk_file_, (n_chunks + 1) * 4, hipMemcpyHostToDevice, parse_stream_));
+  HIP_OK(hipMemcpyAsync(d_chunk_begin_, ps.h_chunk_begin, (n_chunks + 1) * 4, hipMemcpyHostToDevice, parse_stream_));
+  HIP_OK(hipMemcpyAsync(d_chunk_kind_, ps.h_chunk_kind, n_chunks + 1, hipMemcpyHostToDevice, parse_stream_));
+  HIP_OK(hipMemcpyAsync(d_chunk_file_, ps.h_chunk_file, (n_chunks + 1) * 4, hipMemcpyHostToDevice, parse_stream_));
   if (apm_parse_batch(d_bytes_, off, d_chunk_begin_, d_chunk_kind_, d_chunk_file_, n_chunks, d_parse_ws_,
                       cfg_.max_lines, d_events_, d_counts_, d_counts_ + 1, d_watermark_, d_file_open_, &cfg_.tz,
                       parse_stream_) != 0)
     throw std::runtime_error("parse workspace too small");
-  HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, 8, hipMemcpyDeviceToHost, parse_stream_));
-  HIP_OK(hipMemcpyAsync(h_watermark_, d_watermark_, 8, hipMemcpyDeviceToHost, parse_stream_));
+  HIP_OK(hipMemcpyAsync(ps.h_counts, d_counts_, 8, hipMemcpyDeviceToHost, parse_stream_));
+  HIP_OK(hipMemcpyAsync(ps.h_watermark, d_watermark_, 8, hipMemcpyDeviceToHost, parse_stream_));
+  ps.pending = true;
+  metrics_.t_parse_ms += now_ms() - t0;
+}
+
+// Wait for a launched parse and copy its events into the slot's pinned host buffer.
+void Engine::finish_parse(ParseSlot& ps) {
+  const double t0 = now_ms();
   HIP_OK(hipStreamSynchronize(parse_stream_));
-  const uint32_t n_events = h_counts_[0];
-  last_n_events_ = n_events;
-  const uint32_t n_lines = h_counts_[1];
-  if (n_lines > cfg_.max_lines) throw std::runtime_error("batch has more lines than max_lines");
-  metrics_.lines += n_lines;
-  metrics_.events += n_events;
-  if (n_events) {
-    HIP_OK(hipMemcpyAsync(h_events_, d_events_, (size_t)n_events * sizeof(Event), hipMemcpyDeviceToHost, parse_stream_));
+  ps.n_events = ps.h_counts[0];
+  ps.n_lines = ps.h_counts[1];
+  if (ps.n_lines > cfg_.max_lines) throw std::runtime_error("batch has more lines than max_lines");
+  metrics_.lines += ps.n_lines;
+  metrics_.events += ps.n_events;
+  if (ps.n_events) {
+    HIP_OK(hipMemcpyAsync(ps.h_events, d_events_, (size_t)ps.n_events * sizeof(Event), hipMemcpyDeviceToHost,
+                          parse_stream_));
     HIP_OK(hipStreamSynchronize(parse_stream_));
   }
+  ps.pending = false;
+  last_slot_ = (int)(&ps - pslot_);
+  metrics_.t_parse_ms += now_ms() - t0;
+}
+
+void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const std::vector<Chunk>& chunks_in,
+                           double now_override, const uint8_t* next_bytes, uint64_t next_n,
+                           const std::vector<Chunk>* next_chunks) {
+  const double t0 = now_ms();
+  roctxRangePushA("apm.parse");
+  ParseSlot& ps = pslot_[cur_slot_];
+  if (prefetched_) {
+    // the previous call already launched this batch's parse: it must be the same batch
+    if (ps.src != host_bytes || ps.src_n != n_bytes) throw std::runtime_error("batch differs from the prefetched one");
+    prefetched_ = false;
+  } else {
+    launch_parse(ps, host_bytes, n_bytes, chunks_in);
+  }
+  finish_parse(ps);
+  // Pipelining: the next batch's H2D + parse kernels run on the GPU while this batch is joined.
+  if (next_bytes && next_chunks) {
+    launch_parse(pslot_[cur_slot_ ^ 1], next_bytes, next_n, *next_chunks);
+    prefetched_ = true;
+  }
+  cur_slot_ ^= 1;
+  const uint8_t* hb = ps.hb;
+  const std::vector<int32_t>& chunk_file = ps.chunk_file;
+  const uint32_t n_events = ps.n_events;
+  const Event* h_events = ps.h_events;
+  last_n_events_ = n_events;
   const double t1 = now_ms();
-  metrics_.t_parse_ms += t1 - t0;
   roctxRangePop();
   roctxRangePushA("apm.join");
   trace_event("parse", t0, t1, 0);
@@ -477,22 +529,31 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
     // events are in chunk order and chunks are grouped by server -> contiguous per shard
     uint32_t i = 0;
     while (i < n_events) {
-      const int32_t srv = files_[chunk_file[h_events_[i].chunk]].server;
+      const int32_t srv = files_[chunk_file[h_events[i].chunk]].server;
       uint32_t j = i;
-      while (j < n_events && files_[chunk_file[h_events_[j].chunk]].server == srv) ++j;
+      while (j < n_events && files_[chunk_file[h_events[j].chunk]].server == srv) ++j;
       shard_range[srv] = {i, j};
       i = j;
     }
   }
+  shard_ms_.assign(shards_.size() * 16, 0.0);  // one cache line per shard
   pool_->run((int)shards_.size(), [&](int s) {
+    const double ts0 = now_ms();
     JoinShard& sh = *shards_[s];
     sh.out().clear();
     sh.begin_batch(clock, batch_no_);
     const auto r = shard_range[s];
-    if (r.second > r.first) sh.process(h_events_ + r.first, r.second - r.first, hb, chunk_file);
+    if (r.second > r.first) sh.process(h_events + r.first, r.second - r.first, hb, chunk_file);
+    shard_ms_[(size_t)s * 16] = now_ms() - ts0;
   });
   const double t1b = now_ms();
   metrics_.t_join_shards_ms += t1b - t1;
+  {
+    double sum = 0, mx = 0;
+    for (size_t s = 0; s < shards_.size(); ++s) { sum += shard_ms_[s * 16]; mx = std::max(mx, shard_ms_[s * 16]); }
+    metrics_.t_shard_busy_ms += shards_.empty() ? 0 : sum / shards_.size();
+    metrics_.t_shard_max_ms += mx;
+  }
   // Merge the shard outputs into the reference's single-stream order.  Cache-expiry emissions
   // (seq bit 63 clear, keyed by creation) precede every line emission and may interleave across
   // shards: k-way merge (rare).  Line emissions are keyed by the global line index, and each
@@ -547,7 +608,7 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
   metrics_.t_total_ms += now_ms() - t0;
 
   // advance the watermark clock (max leading timestamp seen so far)
-  const unsigned long long wm = *h_watermark_;
+  const unsigned long long wm = *ps.h_watermark;
   if (wm) {
     const double w = (double)((long long)wm - (1LL << 62));
     if (w > watermark_) watermark_ = w;

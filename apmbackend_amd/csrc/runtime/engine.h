@@ -125,6 +125,7 @@ struct EngineMetrics {
   uint64_t formatted_bytes = 0, format_fallbacks = 0, lockstep_rollovers = 0;
   double t_parse_ms = 0, t_join_ms = 0, t_stats_ms = 0, t_total_ms = 0;
   double t_join_shards_ms = 0, t_merge_ms = 0;                 // split of t_join_ms
+  double t_shard_busy_ms = 0, t_shard_max_ms = 0;              // per batch: mean / max of one shard's join
   double t_stats_tx_ms = 0, t_rollover_ms = 0, t_format_ms = 0, t_release_ms = 0;  // inside t_stats_ms
   std::vector<double> rollover_latency_ms;   // batch arrival -> alert decision per rollover
 };
@@ -141,7 +142,7 @@ class ThreadPool {
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
   const std::function<void(int)>* fn_ = nullptr;
-  int n_tasks_ = 0, next_ = 0, done_ = 0;
+  int n_tasks_ = 0, done_ = 0;
   uint64_t gen_ = 0;
   bool stop_ = false;
 };
@@ -157,9 +158,14 @@ class Engine {
   void clear_overrides();
   void refresh_series_settings();
 
-  // Process one batch (synchronous). `now_override` < 0 uses the engine watermark clock.
+  // Process one batch. `now_override` < 0 uses the engine watermark clock.  If the caller
+  // already has the next batch, passing it launches its H2D + parse kernels before this batch's
+  // host join (double-buffered parse slots); the next call must then pass that same batch (its
+  // bytes must stay valid until that call returns).
   void process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const std::vector<Chunk>& chunks,
-                     double now_override = -1.0);
+                     double now_override = -1.0, const uint8_t* next_bytes = nullptr, uint64_t next_n = 0,
+                     const std::vector<Chunk>* next_chunks = nullptr);
+  bool prefetch_pending() const { return prefetched_; }
 
   // Text outputs accumulated since the last take: "transactions", "audit_db", "db", "st", "fs",
   // "al" (enabled by EngineConfig::outputs).  take() splits into lines; take_bytes() hands out
@@ -235,7 +241,9 @@ class Engine {
   JoinCounters join_counters() const;
 
   // events of the last batch (host copy) for kernel verification
-  std::string last_events() const { return std::string((const char*)h_events_, (size_t)last_n_events_ * sizeof(Event)); }
+  std::string last_events() const {
+    return std::string((const char*)pslot_[last_slot_].h_events, (size_t)last_n_events_ * sizeof(Event));
+  }
   // pinned host memory for zero-copy ingest (bench corpus, tailer)
   static uintptr_t alloc_pinned(size_t n);
   static void free_pinned(uintptr_t p);
@@ -305,6 +313,7 @@ class Engine {
   Dictionary dict_;
   std::vector<std::unique_ptr<JoinShard>> shards_;  // one per server
   std::unique_ptr<ThreadPool> pool_;
+  std::vector<double> shard_ms_;  // per-shard join time of the current batch (stride 16)
 
   // series
   FlatMap<int32_t> series_map_{1 << 16};  // ((server + 1) << 32 | service) -> series + 1
@@ -324,20 +333,33 @@ class Engine {
 
   // parse buffers
   uint8_t* d_bytes_ = nullptr;
-  uint8_t* h_bytes_ = nullptr;                  // pinned staging
+  // double-buffered parse slots (host side): staging bytes, chunk tables, events, counters
+  struct ParseSlot {
+    uint8_t* h_bytes = nullptr;                 // pinned staging (non-canonical batches)
+    uint32_t* h_chunk_begin = nullptr;
+    uint8_t* h_chunk_kind = nullptr;
+    uint32_t* h_chunk_file = nullptr;
+    Event* h_events = nullptr;
+    uint32_t* h_counts = nullptr;               // [0]=n_events [1]=n_lines
+    unsigned long long* h_watermark = nullptr;
+    const uint8_t* hb = nullptr;                // bytes the join reads (caller's or staging)
+    const uint8_t* src = nullptr;               // caller's pointer (prefetch identity check)
+    uint64_t src_n = 0, n_bytes = 0;
+    std::vector<int32_t> chunk_file;
+    uint32_t n_events = 0, n_lines = 0;
+    bool pending = false;
+  } pslot_[2];
+  int cur_slot_ = 0, last_slot_ = 0;
+  bool prefetched_ = false;
+  void launch_parse(ParseSlot& ps, const uint8_t* host_bytes, uint64_t n_bytes, const std::vector<Chunk>& chunks);
+  void finish_parse(ParseSlot& ps);
   uint32_t* d_chunk_begin_ = nullptr;
   uint8_t* d_chunk_kind_ = nullptr;
   uint32_t* d_chunk_file_ = nullptr;
-  uint32_t* h_chunk_begin_ = nullptr;
-  uint8_t* h_chunk_kind_ = nullptr;
-  uint32_t* h_chunk_file_ = nullptr;
   void* d_parse_ws_ = nullptr;
   Event* d_events_ = nullptr;
-  Event* h_events_ = nullptr;
   uint32_t* d_counts_ = nullptr;                // [0]=n_events [1]=n_lines
-  uint32_t* h_counts_ = nullptr;
   unsigned long long* d_watermark_ = nullptr;
-  unsigned long long* h_watermark_ = nullptr;
   uint8_t* d_file_open_ = nullptr;
   TzTable* d_tz_unused_ = nullptr;
 

@@ -145,21 +145,26 @@ int32_t Dictionary::service_id(std::string_view normalized) {
   return id;
 }
 
-int32_t JoinShard::raw_service(std::string_view prefix, std::string_view name) {
-  const uint64_t h = fnv1a64((const uint8_t*)name.data(), (int)name.size(),
-                             fnv1a64((const uint8_t*)prefix.data(), (int)prefix.size()));
-  int32_t* slot = raw_svc_map_.find(h);
-  if (slot) {
-    const std::string& r = raw_svc_[*slot - 1].raw;
-    if (r.size() == prefix.size() + name.size() && r.compare(0, prefix.size(), prefix) == 0 &&
-        r.compare(prefix.size(), name.size(), name) == 0)
-      return *slot - 1;
+int32_t JoinShard::raw_service(bool ejb, std::string_view name) {
+  const uint64_t h = svc_hash(ejb, name);
+  const size_t raw_len = name.size() + (ejb ? 2 : 0);
+  if (const int32_t* slot = raw_svc_map_.find(h)) {
+    if (svc_info_[*slot - 1].raw_len == raw_len) return *slot - 1;
   }
-  std::string raw(prefix);
+  std::string raw(ejb ? "S:" : "");
   raw += name;
-  const std::string norm = normalize_service(raw);
+  return intern_service(std::move(raw), h);
+}
+
+int32_t JoinShard::intern_service(std::string raw, uint64_t h) {
+  std::string norm = normalize_service(raw);
   const int32_t id = (int32_t)raw_svc_.size();
-  raw_svc_.push_back(RawService{raw, norm, dict_->service_id(norm), norm.size() >= 2 && norm[0] == 'S' && norm[1] == ':'});
+  const bool top = norm.size() >= 2 && norm[0] == 'S' && norm[1] == ':';
+  const int32_t nid = dict_->service_id(norm);
+  svc_info_.push_back(SvcInfo{(uint32_t)svc_text_.size(), (uint32_t)norm.size(), nid, (uint32_t)raw.size(), top});
+  svc_text_ += norm;
+  raw_svc_.push_back(RawService{std::move(raw), std::move(norm), nid, top, h});
+  int32_t* slot = raw_svc_map_.find(h);
   if (!slot) raw_svc_map_[h] = id + 1;  // a colliding name is re-interned on every call (correct, slow)
   return id;
 }
@@ -196,8 +201,15 @@ JoinShard::RecordEntry& JoinShard::record_map(uint64_t key) {
 }
 
 void JoinShard::sweep() {
+  // every expiry is a random map access: request the slots a few entries ahead
+  constexpr size_t kAhead = 8;
+  for (size_t i = 0; i < kAhead && i < record_fifo_.size() && record_fifo_[i].second < now_; ++i)
+    record_.prefetch(record_fifo_[i].first);
+  for (size_t i = 0; i < kAhead && i < acct_fifo_.size() && acct_fifo_[i].second < now_; ++i)
+    acct_.prefetch(acct_fifo_[i].first);
   // recordCache: expired partial maps are discarded (error log in the reference, :220-224)
   while (!record_fifo_.empty() && record_fifo_.front().second < now_) {
+    if (record_fifo_.size() > kAhead && record_fifo_[kAhead].second < now_) record_.prefetch(record_fifo_[kAhead].first);
     auto k = record_fifo_.front();
     record_fifo_.pop_front();
     RecordEntry* it = record_.find(k.first);
@@ -218,6 +230,7 @@ void JoinShard::sweep() {
     expire_need(ne);
   }
   while (!acct_fifo_.empty() && acct_fifo_.front().second < now_) {
+    if (acct_fifo_.size() > kAhead && acct_fifo_[kAhead].second < now_) acct_.prefetch(acct_fifo_[kAhead].first);
     auto k = acct_fifo_.front();
     acct_fifo_.pop_front();
     AcctEntry* it = acct_.find(k.first);
@@ -241,7 +254,8 @@ void JoinShard::output(int32_t server, int32_t svc, std::string_view log_id, dou
   TxOut& t = out_.back();
   t.seq = (seq << 12) | (sub_++ & 0xfff);
   t.server = server;
-  const RawService& rs = raw_svc_[svc];
+  const SvcInfo& rs = svc_info_[svc];
+  const std::string_view norm(svc_text_.data() + rs.norm_off, rs.norm_len);
   t.service = rs.norm_id;
   double s = start_empty ? js::nan() : start_ms;
   const double e_for_sub = end_empty ? 0.0 : end_ms;  // JS: '' - n === -n
@@ -257,14 +271,14 @@ void JoinShard::output(int32_t server, int32_t svc, std::string_view log_id, dou
   t.line_off = (uint32_t)text_.size();
   const std::string& srv = (*servers_)[server];
   char buf[512];
-  const size_t fixed = srv.size() + rs.norm.size() + log_id.size() + 3 + 8 + 4 * 32 + 2;
+  const size_t fixed = srv.size() + norm.size() + log_id.size() + 3 + 8 + 4 * 32 + 2;
   if (fixed <= sizeof(buf)) {
     char* p = buf;
     auto put = [&](const char* q, size_t n) { std::memcpy(p, q, n); p += n; };
     put("tx|", 3);
     put(srv.data(), srv.size());
     *p++ = '|';
-    put(rs.norm.data(), rs.norm.size());
+    put(norm.data(), norm.size());
     *p++ = '|';
     put(log_id.data(), log_id.size());
     *p++ = '|';
@@ -284,7 +298,7 @@ void JoinShard::output(int32_t server, int32_t svc, std::string_view log_id, dou
     text_ += "tx|";
     text_ += srv;
     text_ += '|';
-    text_ += rs.norm;
+    text_ += norm;
     text_ += '|';
     text_ += log_id;
     text_ += '|';
@@ -410,11 +424,11 @@ void JoinShard::on_ejb(const Event& e, std::string_view line, int32_t file, bool
   if (entry) {  // parseEjbCommonTimingEntry (:378-401)
     if (log_id.empty()) return;
     const std::string_view nm = host ? tk.get(13) : (e.tAs != 0xffff ? line.substr(e.tAs, e.tAe - e.tAs) : kUndef);
-    const int32_t svc = raw_service("S:", nm);
+    const int32_t svc = raw_service(true, nm);
     auto& items = record_map(key_of(log_id)).items;
     auto f = std::find_if(items.begin(), items.end(), [&](const Partial& p) { return p.svc == svc; });
-    if (f != items.end()) { f->server = server; f->start_ms = ts; f->start_empty = ts_empty; }
-    else items.push_back(Partial{svc, server, ts, ts_empty});
+    if (f != items.end()) { f->server = server; f->start_ms = ts; }
+    else items.push_back(Partial{svc, server, ts});
     return;
   }
   // parseEjbCommonTimingExit (:403-446)
@@ -427,7 +441,7 @@ void JoinShard::on_ejb(const Event& e, std::string_view line, int32_t file, bool
     nm = e.tAs != 0xffff ? line.substr(e.tAs, e.tAe - e.tAs) : kUndef;
     elapsed = e.num;
   }
-  const int32_t svc = raw_service("S:", nm);
+  const int32_t svc = raw_service(true, nm);
   if (log_id.empty()) {
     output(server, svc, "", js::nan(), 0, true, ts, ts_empty, elapsed, false, seq);
     return;
@@ -442,9 +456,9 @@ void JoinShard::on_ejb(const Event& e, std::string_view line, int32_t file, bool
   items.erase(f);
   AcctEntry* ait = acct_.find(key);
   if (ait) {
-    output(server, svc, log_id, ait->acct, part.start_ms, part.start_empty, ts, ts_empty, elapsed, false, seq);
+    output(server, svc, log_id, ait->acct, part.start_ms, false, ts, ts_empty, elapsed, false, seq);
   } else {
-    Need n{svc, part.server, part.start_ms, part.start_empty, ts, ts_empty, elapsed, js::nan(), false};
+    Need n{svc, part.server, part.start_ms, false, ts, ts_empty, elapsed, js::nan(), false};
     auto& ni = need_map(key, log_id).items;
     auto g = std::find_if(ni.begin(), ni.end(), [&](const Need& x) { return x.svc == svc; });
     if (g != ni.end()) *g = n; else ni.push_back(n);
@@ -483,8 +497,8 @@ void JoinShard::on_ct(const Event& e, std::string_view line, int32_t file, bool 
     if (log_id.empty()) return;
     auto& items = record_map(key_of(log_id)).items;
     auto f = std::find_if(items.begin(), items.end(), [&](const Partial& p) { return p.svc == svc; });
-    if (f != items.end()) { f->server = server; f->start_ms = ts; f->start_empty = ts_empty; }
-    else items.push_back(Partial{svc, server, ts, ts_empty});
+    if (f != items.end()) { f->server = server; f->start_ms = ts; }
+    else items.push_back(Partial{svc, server, ts});
     return;
   }
   // parseCommonTimingExit (:506-565)
@@ -507,12 +521,12 @@ void JoinShard::on_ct(const Event& e, std::string_view line, int32_t file, bool 
   AcctEntry* ait = acct_.find(key);
   if (ait) {
     items->erase(f);
-    output(server, svc, log_id, ait->acct, part.start_ms, part.start_empty, ts, ts_empty, elapsed, false, seq);
+    output(server, svc, log_id, ait->acct, part.start_ms, false, ts, ts_empty, elapsed, false, seq);
     return;
   }
   need_map(key, log_id);
   std::string_view alt = baf_acct(line, tk.get(3), file, log_id, seq, baf_scratch);  // may drain the map first
-  Need n{svc, part.server, part.start_ms, part.start_empty, ts, ts_empty, elapsed,
+  Need n{svc, part.server, part.start_ms, false, ts, ts_empty, elapsed,
          alt.empty() ? js::nan() : js::parse_int(alt), false};
   auto& ni = need_map(key, log_id).items;
   auto g = std::find_if(ni.begin(), ni.end(), [&](const Need& x) { return x.svc == svc; });
@@ -642,9 +656,29 @@ void JoinShard::on_app(const Event& e, std::string_view line, int32_t file, uint
   }
 }
 
+// Lookahead half of process(): the slots of the logId maps and the service map an EJB /
+// CommonTiming event will probe, requested kLookahead events before the event is handled.
+void JoinShard::prefetch_event(const Event& e, const uint8_t* bytes) {
+  const uint8_t k = e.kind;
+  if (k < LK_EJB_ENTRY || k > LK_CT_EXIT || (e.mask & PM_HOST) || e.ntok == 0) return;
+  const char* l = (const char*)bytes + e.off;
+  const char* a = l + e.t0s;
+  const char* b = l + e.t0e;
+  if (a < b && *a == '[') ++a;
+  if (b > a && b[-1] == ']') --b;
+  const uint64_t key = key_of(std::string_view(a, (size_t)(b - a)));
+  record_.prefetch(key);
+  if (k == LK_EJB_EXIT || k == LK_CT_EXIT) acct_.prefetch(key);
+  if (e.tAs != 0xffff)
+    raw_svc_map_.prefetch(svc_hash(k <= LK_EJB_EXIT, std::string_view(l + e.tAs, (size_t)(e.tAe - e.tAs))));
+}
+
 void JoinShard::process(const Event* ev, size_t n, const uint8_t* bytes, const std::vector<int32_t>& chunk_file) {
+  constexpr size_t kLookahead = 10;
   out_.reserve(out_.size() + n / 2);
+  for (size_t i = 0; i < n && i < kLookahead; ++i) prefetch_event(ev[i], bytes);
   for (size_t i = 0; i < n; ++i) {
+    if (i + kLookahead < n) prefetch_event(ev[i + kLookahead], bytes);
     const Event& e = ev[i];
     ++counters.events;
     if (e.mask & PM_HOST) ++counters.host_fallback;
@@ -656,6 +690,7 @@ void JoinShard::process(const Event* ev, size_t n, const uint8_t* bytes, const s
 #ifdef APM_JOIN_PROF
     const uint64_t t0 = __rdtsc();
 #endif
+#ifndef APM_JOIN_NOOP
     switch (e.kind) {
       case LK_SOAP: on_soap(e, line, file, seq); break;
       case LK_EJB_ENTRY: on_ejb(e, line, file, true, seq); break;
@@ -665,6 +700,7 @@ void JoinShard::process(const Event* ev, size_t n, const uint8_t* bytes, const s
       case LK_APP: on_app(e, line, file, seq); break;
       default: break;
     }
+#endif
 #ifdef APM_JOIN_PROF
     prof_cyc[e.kind & 15] += __rdtsc() - t0;
     prof_n[e.kind & 15]++;

@@ -260,15 +260,36 @@ inline std::string to_fixed(double x, int f) {
 }
 
 // Write String(x) at p (at most 32 bytes: JS number strings are <= 25 chars); returns the end.
+// Decimal digits of v written at p (two digits per step from a 200-byte table); returns the end.
+inline char* put_u64(char* p, uint64_t v) {
+  static const char kPairs[201] =
+      "00010203040506070809101112131415161718192021222324252627282930313233343536373839"
+      "40414243444546474849505152535455565758596061626364656667686970717273747576777879"
+      "8081828384858687888990919293949596979899";
+  char tmp[24];
+  char* e = tmp + sizeof(tmp);
+  char* q = e;
+  while (v >= 100) {
+    const unsigned r = (unsigned)(v % 100);
+    v /= 100;
+    q -= 2;
+    std::memcpy(q, kPairs + 2 * r, 2);
+  }
+  if (v >= 10) {
+    q -= 2;
+    std::memcpy(q, kPairs + 2 * v, 2);
+  } else {
+    *--q = (char)('0' + v);
+  }
+  const size_t n = (size_t)(e - q);
+  std::memcpy(p, q, n);
+  return p + n;
+}
+
 inline char* put_num(char* p, double x) {
   if (x == x && x == std::trunc(x) && std::fabs(x) < 9007199254740992.0 && !(x == 0 && std::signbit(x))) {
-    char tmp[20];
-    int n = 0;
-    uint64_t v = (uint64_t)std::fabs(x);
-    do { tmp[n++] = (char)('0' + v % 10); v /= 10; } while (v);
     if (x < 0) *p++ = '-';
-    while (n) *p++ = tmp[--n];
-    return p;
+    return put_u64(p, (uint64_t)std::fabs(x));
   }
   const std::string s = num_str(x);  // NaN, fractions, huge: rare
   const size_t n = std::min<size_t>(s.size(), 32);

@@ -8,6 +8,9 @@
 //   batch_<i>.bytes    the batch bytes the events point into
 // Output: the tx lines in the engine's merge order ("<queue>\t<line>").
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
 #include <cstdio>
 #include <fstream>
 #include <iostream>
@@ -18,6 +21,10 @@
 #include <vector>
 
 #include "runtime/join.h"
+
+#ifdef JOIN_REPLAY_HIP
+#include <hip/hip_runtime.h>
+#endif
 
 using namespace apm;
 
@@ -52,6 +59,9 @@ int main(int argc, char** argv) {
   }
   JoinConfig cfg;  // UTC table: n = 0 -> offset 0
   Dictionary dict;
+  const bool quiet = std::getenv("JOIN_REPLAY_QUIET") != nullptr;  // timing mode (tools/join_prof.py)
+  double t_total = 0;
+  size_t ev_total = 0;
   std::vector<std::unique_ptr<JoinShard>> shards;
   for (size_t i = 0; i < servers.size(); ++i) shards.emplace_back(new JoinShard(cfg, &dict, &files, &servers));
   for (int b = 0; b < nb; ++b) {
@@ -62,22 +72,47 @@ int main(int argc, char** argv) {
     std::vector<int32_t> chunk_file;
     int32_t cf;
     while (meta >> cf) chunk_file.push_back(cf);
-    const std::string ev = slurp(pre + ".events");
-    const std::string by = slurp(pre + ".bytes");
-    const Event* e = reinterpret_cast<const Event*>(ev.data());
-    const size_t n = ev.size() / sizeof(Event);
+    const std::string ev_s = slurp(pre + ".events");
+    const std::string by_s = slurp(pre + ".bytes");
+    const char* ev_p = ev_s.data();
+    const char* by_p = by_s.data();
+#ifdef JOIN_REPLAY_HIP
+    // JOIN_REPLAY_PINNED=1: replay out of hipHostMalloc'd buffers, as the engine does
+    static char *pin_ev = nullptr, *pin_by = nullptr;
+    if (std::getenv("JOIN_REPLAY_PINNED")) {
+      if (!pin_ev) {
+        if (hipHostMalloc((void**)&pin_ev, 64 << 20, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void**)&pin_by, 64 << 20, hipHostMallocDefault) != hipSuccess) return 3;
+      }
+      std::memcpy(pin_ev, ev_s.data(), ev_s.size());
+      std::memcpy(pin_by, by_s.data(), by_s.size());
+      ev_p = pin_ev;
+      by_p = pin_by;
+    }
+#endif
+    const Event* e = reinterpret_cast<const Event*>(ev_p);
+    const size_t n = ev_s.size() / sizeof(Event);
     std::vector<TxOut> all;
     for (size_t s = 0; s < shards.size(); ++s) {
       shards[s]->out().clear();
       shards[s]->begin_batch(now, (uint64_t)b);
     }
+    const auto t0 = std::chrono::steady_clock::now();
     size_t i = 0;
     while (i < n) {
       const int32_t srv = files[chunk_file[e[i].chunk]].server;
       size_t j = i;
       while (j < n && files[chunk_file[e[j].chunk]].server == srv) ++j;
-      shards[srv]->process(e + i, j - i, (const uint8_t*)by.data(), chunk_file);
+      shards[srv]->process(e + i, j - i, (const uint8_t*)by_p, chunk_file);
       i = j;
+    }
+    const double dt = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (quiet) {
+      size_t tx = 0;
+      for (auto& sh : shards) tx += sh->out().size();
+      std::fprintf(stderr, "batch %d: events=%zu tx=%zu join=%.3f ms\n", b, n, tx, dt);
+      if (b > 0) { t_total += dt; ev_total += n; }
+      continue;
     }
     for (auto& sh : shards)
       for (auto& t : sh->out()) all.push_back(t);
@@ -86,5 +121,6 @@ int main(int argc, char** argv) {
       std::cout << (t.to_db ? "db_insert" : "transactions") << '\t'
                 << shards[t.server]->text().substr(t.line_off, t.line_len) << '\n';
   }
+  if (quiet && ev_total) std::fprintf(stderr, "steady: %.1f ns/event\n", t_total * 1e6 / ev_total);
   return 0;
 }

@@ -286,3 +286,39 @@ def test_server_rollup_fuses_window_stats_with_jmx_gauges():
         if srv != "jvm00":
             assert f[9] == "undefined"
     assert checked > 0
+
+
+def test_parse_prefetch_pipelining_is_transparent():
+    """process_batch(i, next=i+1) launches batch i+1's parse before batch i's join: outputs
+    must be identical to the plain sequence."""
+    lines, bl = synth_batches(11, duration=400)
+    C = small_cfg("exact")
+    _, plain = _run_engine(C, bl)
+    eng = APMEngine(C, keep_text=True)
+    N = eng.N
+    bufs = []
+    for now, chunks in bl:
+        parts, table, off = [], [], 0
+        for fp, ls in chunks:
+            data = ("\n".join(ls) + "\n").encode()
+            fid = eng.add_file(fp)
+            parts.append(data)
+            table.append((fid, off, off + len(data)))
+            off += len(data)
+        blob = b"".join(parts)
+        p = N.alloc_pinned(len(blob) + 64)
+        N.memcpy_to(p, blob, 0)
+        bufs.append((p, len(blob), table, now))
+    out = collections.defaultdict(list)
+    for i, (p, n, table, now) in enumerate(bufs):
+        if i + 1 < len(bufs):
+            q, m, t2, _ = bufs[i + 1]
+            eng.eng.process_batch_ptr(p, n, table, now, q, m, t2)
+        else:
+            eng.eng.process_batch_ptr(p, n, table, now)
+        for k in ("transactions", "audit_db", "st", "fs", "al"):
+            out[k] += eng.take(k)
+    for k in ("transactions", "audit_db", "st", "fs", "al"):
+        assert out[k] == plain[k], k
+    for p, *_ in bufs:
+        N.free_pinned(p)
