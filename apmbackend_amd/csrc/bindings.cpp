@@ -134,6 +134,7 @@ py::dict metrics_dict(const EngineMetrics& m) {
   d["alerts"] = m.alerts; d["alert_candidates"] = m.alert_candidates; d["released"] = m.released;
   d["t_join_shards_ms"] = m.t_join_shards_ms; d["t_merge_ms"] = m.t_merge_ms;
   d["t_shard_busy_ms"] = m.t_shard_busy_ms; d["t_shard_max_ms"] = m.t_shard_max_ms;
+  d["t_out_ms"] = m.t_out_ms;
   d["t_stats_tx_ms"] = m.t_stats_tx_ms; d["t_rollover_ms"] = m.t_rollover_ms;
   d["t_format_ms"] = m.t_format_ms; d["t_release_ms"] = m.t_release_ms;
   d["formatted_bytes"] = m.formatted_bytes; d["lockstep_rollovers"] = m.lockstep_rollovers; d["format_fallbacks"] = m.format_fallbacks;

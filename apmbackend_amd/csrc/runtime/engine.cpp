@@ -197,7 +197,11 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   }
   release_tmp_bytes_ = apm_release_tmp_bytes(cfg_.pool_cap);
   d_release_tmp_ = dmalloc(release_tmp_bytes_);
-  HIP_OK(hipHostMalloc((void**)&h_release_gid_, (size_t)cfg_.pool_cap * 8, hipHostMallocDefault));
+  for (int k = 0; k < 2; ++k) {
+    HIP_OK(hipHostMalloc((void**)&h_release_gid_[k], (size_t)cfg_.pool_cap * 8, hipHostMallocDefault));
+    HIP_OK(hipEventCreateWithFlags(&ev_rel_[k], hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_fmt_[k], hipEventDisableTiming));
+  }
   // threads
   int nt = cfg_.join_threads;
   if (nt <= 0) nt = (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
@@ -206,6 +210,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipStreamSynchronize(stream_));
   HIP_OK(hipDeviceSynchronize());
   stats_thread_ = std::thread([this]() { hipSetDevice(cfg_.device); stats_worker(); });
+  out_thread_ = std::thread([this]() { hipSetDevice(cfg_.device); out_worker(); });
 }
 
 Engine::~Engine() {
@@ -215,6 +220,12 @@ Engine::~Engine() {
   }
   st_cv_.notify_all();
   if (stats_thread_.joinable()) stats_thread_.join();
+  {
+    std::lock_guard<std::mutex> g(out_mu_);
+    out_stop_ = true;
+  }
+  out_cv_.notify_all();
+  if (out_thread_.joinable()) out_thread_.join();
   if (fleet_comm_) {
     hipStreamSynchronize(comm_stream_);
     ncclCommDestroy(fleet_comm_);
@@ -234,8 +245,13 @@ Engine::~Engine() {
     hipHostFree(ps.h_events); hipHostFree(ps.h_counts); hipHostFree(ps.h_watermark);
   }
   hipHostFree(h_alerts_);
-  hipHostFree(h_n_alerts_); hipHostFree(h_tx_); hipHostFree(h_gid_); hipHostFree(h_release_gid_);
-  if (h_fmt_out_) hipHostFree(h_fmt_out_);
+  hipHostFree(h_n_alerts_); hipHostFree(h_tx_); hipHostFree(h_gid_);
+  for (int k = 0; k < 2; ++k) {
+    hipHostFree(h_release_gid_[k]);
+    if (h_fmt_out_[k]) hipHostFree(h_fmt_out_[k]);
+    hipEventDestroy(ev_rel_[k]);
+    hipEventDestroy(ev_fmt_[k]);
+  }
   if (h_roll_out_) hipHostFree(h_roll_out_);
   hipHostFree(h_fmt_meta_);
   hipEventDestroy(ev_a_); hipEventDestroy(ev_b_);
@@ -664,7 +680,7 @@ void Engine::stats_worker() {
       stats_for_batch(job.txs, job.t0);
       sync_latest_locked(job.t0);
       fleet_exchange_locked();
-      drain_sinks();
+      drain_sinks(~kLaneKinds);
     } catch (const std::exception& e) {
       std::lock_guard<std::mutex> g(st_mu_);
       st_error_ = e.what();
@@ -684,6 +700,10 @@ void Engine::post_stats(std::vector<TxOut>&& txs, double t0) {
   std::unique_lock<std::mutex> lk(st_mu_);
   st_cv_.wait(lk, [&]() { return !st_busy_; });
   if (!st_error_.empty()) { std::string e = st_error_; st_error_.clear(); throw std::runtime_error(e); }
+  {
+    std::lock_guard<std::mutex> g(out_mu_);
+    if (!out_error_.empty()) { std::string e = out_error_; out_error_.clear(); throw std::runtime_error(e); }
+  }
   st_job_.txs = std::move(txs);
   // hand the shards' formatted tx lines to the stats thread; the shards get the previous
   // batch's (consumed) arenas back and reuse their capacity
@@ -708,7 +728,100 @@ void Engine::post_stats(std::vector<TxOut>&& txs, double t0) {
 void Engine::flush() {
   std::unique_lock<std::mutex> lk(st_mu_);
   st_cv_.wait(lk, [&]() { return !st_busy_; });
+  // the stats thread is idle, so no new output-lane task can appear
+  out_wait_idle();
+  {
+    std::lock_guard<std::mutex> g(out_mu_);
+    metrics_.t_out_ms += t_out_ms_;
+    t_out_ms_ = 0;
+    if (!out_error_.empty()) { std::string e = out_error_; out_error_.clear(); throw std::runtime_error(e); }
+  }
   if (!st_error_.empty()) { std::string e = st_error_; st_error_.clear(); throw std::runtime_error(e); }
+}
+
+// ----------------------------------------------------------------------------- output lane
+// The stats thread enqueues "wait for this D2H, then emit" tasks and moves on to the next
+// rollover / batch; the lane runs them in order.  It owns the db (released tx), st and fs
+// streams, so those blobs and sinks are only touched here (or with both lanes idle).
+void Engine::out_worker() {
+  for (;;) {
+    std::function<void()> fn;
+    {
+      std::unique_lock<std::mutex> lk(out_mu_);
+      out_cv_.wait(lk, [&]() { return out_stop_ || !out_q_.empty(); });
+      if (out_q_.empty()) return;  // stop requested and nothing left
+      fn = std::move(out_q_.front());
+      out_q_.pop_front();
+    }
+    const double t = now_ms();
+    std::string err;
+    try {
+      fn();
+    } catch (const std::exception& e) {
+      err = e.what();
+    }
+    {
+      std::lock_guard<std::mutex> g(out_mu_);
+      t_out_ms_ += now_ms() - t;
+      if (!err.empty() && out_error_.empty()) out_error_ = err;
+      ++out_done_;
+    }
+    out_cv_.notify_all();
+  }
+}
+
+uint64_t Engine::post_out(std::function<void()> fn) {
+  std::lock_guard<std::mutex> g(out_mu_);
+  out_q_.push_back(std::move(fn));
+  const uint64_t id = ++out_posted_;
+  out_cv_.notify_all();
+  return id;
+}
+
+void Engine::out_wait(uint64_t task) {
+  std::unique_lock<std::mutex> lk(out_mu_);
+  out_cv_.wait(lk, [&]() { return out_done_ >= task; });
+}
+
+void Engine::out_wait_idle() {
+  std::unique_lock<std::mutex> lk(out_mu_);
+  out_cv_.wait(lk, [&]() { return out_done_ >= out_posted_; });
+}
+
+// Released tx lines, in pool (endTs) order, gathered from the zero-copy line blocks.
+void Engine::release_gather(int k, int64_t released) {
+  HIP_OK(hipEventSynchronize(ev_rel_[k]));
+  const int64_t* gids = h_release_gid_[k];
+  std::string& out = blob_[OUT_DB];
+  uint32_t cur_id = UINT32_MAX;
+  LineBlock* cur = nullptr;
+  for (int64_t i = 0; i < released; ++i) {
+    const uint64_t g = (uint64_t)gids[i];
+    const uint32_t id = (uint32_t)(g >> 44);
+    if (id != cur_id) {
+      std::lock_guard<std::mutex> lk(blocks_mu_);
+      auto it = line_blocks_.find(id);
+      cur = it == line_blocks_.end() ? nullptr : &it->second;  // element references survive rehash
+      cur_id = id;
+    }
+    if (!cur) continue;
+    const size_t off = (size_t)((g >> 12) & 0xffffffffu);
+    size_t len = (size_t)(g & 0xfff);
+    if (len == 4095) len = cur->data.find('\n', off) - off;  // long line: scan to its end
+    out.append(cur->data, off, len + 1);  // the arena stores each line with its '\n'
+    if (--cur->live == 0) {
+      std::string data;
+      {
+        std::lock_guard<std::mutex> lk(blocks_mu_);
+        data.swap(cur->data);
+        line_blocks_.erase(cur_id);
+      }
+      recycle_arena(std::move(data));
+      cur = nullptr;
+      cur_id = UINT32_MAX;
+    }
+  }
+  drain_kind(OUT_DB);
 }
 
 void Engine::ensure_bucket_slot(int64_t b) {
@@ -780,6 +893,7 @@ void Engine::stats_for_batch(std::vector<TxOut>& txs, double batch_t0) {
   if (agg_n) { pool_bucket_count_[agg_b] += agg_n; pool_exact_edge_[agg_b] += agg_e; }
   for (size_t a = 0; a < n_arena; ++a)
     if (blk_live[a] > 0) {
+      std::lock_guard<std::mutex> lk(blocks_mu_);
       if (line_blocks_.count(blk_id[a])) throw std::runtime_error("release block id wrapped while still live");
       LineBlock& b = line_blocks_[blk_id[a]];
       b.data.swap(text[a]);  // the arena moves into the block; the job keeps an empty string
@@ -869,32 +983,15 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
     tail_n_ = 0;
     if (released > pool_n_) released = pool_n_;
     if (want(OUT_DB) && released > 0) {
-      HIP_OK(hipMemcpyAsync(h_release_gid_, d_pool_gid_[pool_cur_], (size_t)released * 8, hipMemcpyDeviceToHost,
+      // the D2H of the released ids is queued behind the merge; the output lane waits for it and
+      // gathers the lines while this thread continues with K8/K10/K11
+      const int k = rel_k_;
+      rel_k_ ^= 1;
+      out_wait(rel_task_[k]);  // the buffer's previous reader is done
+      HIP_OK(hipMemcpyAsync(h_release_gid_[k], d_pool_gid_[pool_cur_], (size_t)released * 8, hipMemcpyDeviceToHost,
                             stream_));
-      HIP_OK(hipStreamSynchronize(stream_));
-      std::string& out = blob_[OUT_DB];
-      uint32_t cur_id = UINT32_MAX;
-      LineBlock* cur = nullptr;
-      for (int64_t i = 0; i < released; ++i) {
-        const uint64_t g = (uint64_t)h_release_gid_[i];
-        const uint32_t id = (uint32_t)(g >> 44);
-        if (id != cur_id) {
-          auto it = line_blocks_.find(id);
-          cur = it == line_blocks_.end() ? nullptr : &it->second;
-          cur_id = id;
-        }
-        if (!cur) continue;
-        const size_t off = (size_t)((g >> 12) & 0xffffffffu);
-        size_t len = (size_t)(g & 0xfff);
-        if (len == 4095) len = cur->data.find('\n', off) - off;  // long line: scan to its end
-        out.append(cur->data, off, len + 1);  // the arena stores each line with its '\n'
-        if (--cur->live == 0) {
-          recycle_arena(std::move(cur->data));
-          line_blocks_.erase(cur_id);
-          cur = nullptr;
-          cur_id = UINT32_MAX;
-        }
-      }
+      HIP_OK(hipEventRecord(ev_rel_[k], stream_));
+      rel_task_[k] = post_out([this, k, released]() { release_gather(k, released); });
     }
     metrics_.released += released;
     pool_off_ = released;
@@ -1073,7 +1170,7 @@ void Engine::emit_bytes(int kind, const char* p, size_t n) {
   if (!n) return;
   if (sink_fd_[kind] >= 0) {
     // keep stream order: whatever is buffered goes first, then straight from the staging buffer
-    drain_sinks();
+    drain_kind(kind);
     while (n) {
       const ssize_t w = ::write(sink_fd_[kind], p, n);
       if (w < 0) {
@@ -1121,6 +1218,7 @@ void Engine::format_rollover_text(int64_t edge_ts) {
   HIP_OK(hipStreamSynchronize(stream_));
   if (h_fmt_meta_[2]) {
     ++metrics_.format_fallbacks;
+    out_wait_idle();  // st / fs are lane-owned streams
     format_rollover_text_host(edge_ts);
     return;
   }
@@ -1130,17 +1228,26 @@ void Engine::format_rollover_text(int64_t edge_ts) {
   fa.st_out = d_fmt_out_[0];
   fa.fs_out = d_fmt_out_[1];
   apm_format_write(&fa, stream_);
-  if (st_total + fs_total > h_fmt_cap_) {
-    if (h_fmt_out_) HIP_OK(hipHostFree(h_fmt_out_));
-    h_fmt_cap_ = (st_total + fs_total) * 3 / 2 + (1 << 20);
-    HIP_OK(hipHostMalloc((void**)&h_fmt_out_, h_fmt_cap_, hipHostMallocDefault));
+  // D2H into one of two pinned staging buffers; the output lane waits for it and emits st / fs
+  // while this thread goes on (alerts, next rollover / batch)
+  const int k = fmt_k_;
+  fmt_k_ ^= 1;
+  out_wait(fmt_task_[k]);
+  if (st_total + fs_total > h_fmt_cap_[k]) {
+    if (h_fmt_out_[k]) HIP_OK(hipHostFree(h_fmt_out_[k]));
+    h_fmt_cap_[k] = (st_total + fs_total) * 3 / 2 + (1 << 20);
+    HIP_OK(hipHostMalloc((void**)&h_fmt_out_[k], h_fmt_cap_[k], hipHostMallocDefault));
   }
-  if (st_total) HIP_OK(hipMemcpyAsync(h_fmt_out_, fa.st_out, st_total, hipMemcpyDeviceToHost, stream_));
-  if (fs_total) HIP_OK(hipMemcpyAsync(h_fmt_out_ + st_total, fa.fs_out, fs_total, hipMemcpyDeviceToHost, stream_));
-  HIP_OK(hipStreamSynchronize(stream_));
+  char* h = h_fmt_out_[k];
+  if (st_total) HIP_OK(hipMemcpyAsync(h, fa.st_out, st_total, hipMemcpyDeviceToHost, stream_));
+  if (fs_total) HIP_OK(hipMemcpyAsync(h + st_total, fa.fs_out, fs_total, hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipEventRecord(ev_fmt_[k], stream_));
   metrics_.formatted_bytes += st_total + fs_total;
-  emit_bytes(OUT_ST, h_fmt_out_, st_total);
-  emit_bytes(OUT_FS, h_fmt_out_ + st_total, fs_total);
+  fmt_task_[k] = post_out([this, k, h, st_total, fs_total]() {
+    HIP_OK(hipEventSynchronize(ev_fmt_[k]));
+    emit_bytes(OUT_ST, h, st_total);
+    emit_bytes(OUT_FS, h + st_total, fs_total);
+  });
 }
 
 bool Engine::set_server_context(const std::string& server, double ts_ms, const std::vector<double>& gauges,
@@ -1300,23 +1407,26 @@ void Engine::set_sink_fd(const std::string& kind, int fd) {
   sink_fd_[out_kind_of(kind)] = fd;
 }
 
-void Engine::drain_sinks() {
-  for (int k = 0; k < N_OUT; ++k) {
-    if (sink_fd_[k] < 0 || blob_[k].empty()) continue;
-    const char* p = blob_[k].data();
-    size_t left = blob_[k].size();
-    while (left) {
-      const ssize_t w = ::write(sink_fd_[k], p, left);
-      if (w < 0) {
-        if (errno == EINTR) continue;
-        throw std::runtime_error(std::string("sink write failed: ") + std::strerror(errno));
-      }
-      p += w;
-      left -= (size_t)w;
+void Engine::drain_kind(int k) {
+  if (sink_fd_[k] < 0 || blob_[k].empty()) return;
+  const char* p = blob_[k].data();
+  size_t left = blob_[k].size();
+  while (left) {
+    const ssize_t w = ::write(sink_fd_[k], p, left);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      throw std::runtime_error(std::string("sink write failed: ") + std::strerror(errno));
     }
-    sink_bytes_[k] += blob_[k].size();
-    blob_[k].clear();
+    p += w;
+    left -= (size_t)w;
   }
+  sink_bytes_[k] += blob_[k].size();
+  blob_[k].clear();
+}
+
+void Engine::drain_sinks(uint32_t kinds) {
+  for (int k = 0; k < N_OUT; ++k)
+    if ((kinds >> k) & 1u) drain_kind(k);
 }
 
 void Engine::warm_history(uint64_t seed) {

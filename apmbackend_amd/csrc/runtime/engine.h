@@ -15,6 +15,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
+#include <deque>
 #include <functional>
 #include <map>
 #include <memory>
@@ -93,6 +94,8 @@ struct EngineConfig {
 //   AL            alerts -> db    al lines
 //   SX            new: per-JVM rollup fused with JMX / VM gauges (K14), one line per server
 enum OutKind { OUT_TRANSACTIONS = 0, OUT_AUDIT_DB, OUT_DB, OUT_ST, OUT_FS, OUT_AL, OUT_SX, N_OUT };
+// streams written by the engine's output lane (released tx, st, fs); the stats thread owns the rest
+constexpr uint32_t kLaneKinds = (1u << OUT_DB) | (1u << OUT_ST) | (1u << OUT_FS);
 const char* out_kind_name(int k);
 int out_kind_of(const std::string& name);
 
@@ -127,6 +130,7 @@ struct EngineMetrics {
   double t_join_shards_ms = 0, t_merge_ms = 0;                 // split of t_join_ms
   double t_shard_busy_ms = 0, t_shard_max_ms = 0;              // per batch: mean / max of one shard's join
   double t_stats_tx_ms = 0, t_rollover_ms = 0, t_format_ms = 0, t_release_ms = 0;  // inside t_stats_ms
+  double t_out_ms = 0;                        // output lane: released-line gather + st/fs emission
   std::vector<double> rollover_latency_ms;   // batch arrival -> alert decision per rollover
 };
 
@@ -175,7 +179,7 @@ class Engine {
   // Route a stream to a file descriptor: the stats thread write()s each batch's blob to it (a
   // COPY/queue spool file, a pipe to the DB loader, /dev/null).  fd < 0 detaches.
   void set_sink_fd(const std::string& kind, int fd);
-  uint64_t sink_bytes(const std::string& kind) const { return sink_bytes_[out_kind_of(kind)]; }
+  uint64_t sink_bytes(const std::string& kind) { flush(); return sink_bytes_[out_kind_of(kind)]; }
 
   // Exogenous per-JVM gauges (JMX jx record fields in JmxEntry order + VM load) fused into the
   // per-interval server rollup (K14, "sx" stream).  Returns false for a server this engine
@@ -273,7 +277,15 @@ class Engine {
   void sync_latest_locked(double batch_t0);
   void stats_worker();
   void post_stats(std::vector<TxOut>&& txs, double t0);
-  void drain_sinks();
+  void drain_sinks(uint32_t kinds = ~0u);
+  void drain_kind(int k);
+  // output lane (see engine.cpp): waits for the D2H of released-tx ids / formatted text and
+  // writes those streams, off the stats thread's critical path
+  void out_worker();
+  uint64_t post_out(std::function<void()> fn);
+  void out_wait(uint64_t task);
+  void out_wait_idle();
+  void release_gather(int k, int64_t released);
   bool want(int k) const { return (cfg_.outputs >> k) & 1u; }
   void* dmalloc(size_t bytes);
   void require_fresh(const char* what);
@@ -303,6 +315,15 @@ class Engine {
   StatsJob st_job_;
   bool st_has_job_ = false, st_busy_ = false, st_stop_ = false;
   std::string st_error_;
+  // output lane: FIFO of emit tasks; it owns the db / st / fs streams (kLaneKinds)
+  std::thread out_thread_;
+  std::mutex out_mu_;
+  std::condition_variable out_cv_;
+  std::deque<std::function<void()>> out_q_;
+  uint64_t out_posted_ = 0, out_done_ = 0;
+  bool out_stop_ = false;
+  std::string out_error_;
+  double t_out_ms_ = 0;  // lane busy time (folded into metrics_ by flush)
   size_t device_bytes_ = 0;
   std::vector<void*> allocations_;
 
@@ -420,13 +441,17 @@ class Engine {
   size_t release_tmp_bytes_ = 0;
   std::map<int64_t, int64_t> pool_bucket_count_;   // endTs bucket -> pending count (host mirror)
   std::map<int64_t, int64_t> pool_exact_edge_;     // endTs == bucket start count
-  int64_t* h_release_gid_ = nullptr;
+  int64_t* h_release_gid_[2] = {nullptr, nullptr};  // ping-pong D2H targets of released ids
+  hipEvent_t ev_rel_[2] = {nullptr, nullptr};
+  uint64_t rel_task_[2] = {0, 0};                    // output-lane task that reads each buffer
+  int rel_k_ = 0;
   int64_t next_gid_ = 0;
   // Released-tx line store: each stats batch appends its pending tx lines to one block; the
   // pool payload (gid) is (block << 32 | offset).  A block is freed when its last line is
   // released (lines leave in endTs order, so blocks drain roughly in age order).
   struct LineBlock { std::string data; int64_t live = 0; };
-  std::unordered_map<uint32_t, LineBlock> line_blocks_;
+  std::unordered_map<uint32_t, LineBlock> line_blocks_;  // guarded by blocks_mu_ while the lanes run
+  std::mutex blocks_mu_;
   std::mutex arena_mu_;
   std::vector<std::string> arena_pool_;          // drained release blocks, reused as shard arenas
   void recycle_arena(std::string&& a);
@@ -456,8 +481,11 @@ class Engine {
   size_t fmt_tmp_bytes_ = 0;
   char* d_fmt_out_[2] = {nullptr, nullptr};
   size_t fmt_out_cap_[2] = {0, 0};
-  char* h_fmt_out_ = nullptr;                    // pinned staging for the D2H of formatted text
-  size_t h_fmt_cap_ = 0;
+  char* h_fmt_out_[2] = {nullptr, nullptr};      // pinned ping-pong staging for the D2H of formatted text
+  size_t h_fmt_cap_[2] = {0, 0};
+  hipEvent_t ev_fmt_[2] = {nullptr, nullptr};
+  uint64_t fmt_task_[2] = {0, 0};
+  int fmt_k_ = 0;
   uint32_t* h_fmt_meta_ = nullptr;               // pinned: st total, fs total, fallback
 
   // text outputs

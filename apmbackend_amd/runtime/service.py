@@ -30,6 +30,7 @@ import gc
 import glob
 import json
 import logging
+import math
 import os
 import signal
 import time
@@ -58,6 +59,17 @@ def discover_files(cfg: Dict[str, Any]) -> List[str]:
     for suf in pc.get("maskSuffixes", []):
         out += glob.glob(os.path.join(prefix, suf))
     return sorted(set(out))
+
+
+_STAGE_KEYS = ("t_parse_ms", "t_join_ms", "t_stats_ms", "t_out_ms")
+
+
+def _percentiles(xs, qs):
+    """Nearest-rank percentiles of xs ('-' when empty), formatted with 1 decimal."""
+    if not xs:
+        return ["-"] * len(qs)
+    v = sorted(xs)
+    return ["%.1f" % v[min(len(v) - 1, max(0, math.ceil(q / 100.0 * len(v)) - 1))] for q in qs]
 
 
 class IngestService:
@@ -173,6 +185,7 @@ class IngestService:
         self.last_ckpt = clock()
         self.last_stat = clock()
         self._m0 = self._metrics()
+        self._m0_prev = dict(self._m0)
         if install_signals:
             signal.signal(signal.SIGTERM, self._on_signal)
             signal.signal(signal.SIGINT, self._on_signal)
@@ -326,12 +339,25 @@ class IngestService:
             self.last_stat = now
 
     def log_stats(self, dt_s: float):
+        """Per statLogIntervalInSeconds: throughput, per-stage ms per batch, the ingest->alert
+        latency distribution of the interval's rollovers, HBM in use."""
         m = self._metrics()
         d = {k: m.get(k, 0) - self._m0.get(k, 0) for k in ("lines", "tx", "alerts", "rollovers", "batches")}
         self._m0 = m
         log.info("ENGINE lines/s: %.0f - tx/s: %.0f - rollovers: %d - alerts: %d - batches: %d - series: %s",
                  d["lines"] / max(dt_s, 1e-9), d["tx"] / max(dt_s, 1e-9), d["rollovers"], d["alerts"], d["batches"],
                  self.native.n_series() if hasattr(self.native, "n_series") else "?")
+        prev = getattr(self, "_m0_prev", {})
+        stages = {k: m.get(k, 0.0) - prev.get(k, 0.0) for k in _STAGE_KEYS}
+        nb = max(d["batches"], 1)
+        lat = list(m.get("rollover_latency_ms", []))[len(prev.get("rollover_latency_ms", [])):]
+        self._m0_prev = m
+        pct = _percentiles(lat, (50, 90, 99))
+        hbm = self.native.device_bytes() if hasattr(self.native, "device_bytes") else 0
+        log.info("ENGINE ms/batch parse %.2f join %.2f stats %.2f out %.2f - ingest->alert ms p50 %s p90 %s p99 %s "
+                 "- HBM %.2f GB - fleet rounds %s",
+                 *(stages[k] / nb for k in _STAGE_KEYS), *pct, hbm / 1e9,
+                 self.native.fleet_rounds() if hasattr(self.native, "fleet_rounds") else "-")
         if self.inserter is not None:
             self.inserter.stats.log_and_reset()
         if self.qm is not None:

@@ -218,7 +218,7 @@ def main():
             "series_per_gpu": eng.eng.n_series(),
             "stage_ms_per_step": {k: round((m1[k] - m0[k]) / args.steps, 3)
                                   for k in ("t_parse_ms", "t_join_ms", "t_join_shards_ms", "t_shard_busy_ms", "t_shard_max_ms", "t_merge_ms", "t_stats_ms",
-                                            "t_stats_tx_ms", "t_release_ms", "t_rollover_ms", "t_format_ms")},
+                                            "t_stats_tx_ms", "t_release_ms", "t_rollover_ms", "t_format_ms", "t_out_ms")},
             "corpus_gen_s": round(t_gen, 2),
             "db_insert_bytes_total": out_bytes,
         }

@@ -16,6 +16,7 @@
 #include <iostream>
 #include <memory>
 #include <sstream>
+#include <thread>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -60,6 +61,9 @@ int main(int argc, char** argv) {
   JoinConfig cfg;  // UTC table: n = 0 -> offset 0
   Dictionary dict;
   const bool quiet = std::getenv("JOIN_REPLAY_QUIET") != nullptr;  // timing mode (tools/join_prof.py)
+  // JOIN_REPLAY_THREADS=1: every shard of a batch is joined on its own thread, as in the engine
+  // (shared Dictionary, concurrent interning) -- the ThreadSanitizer configuration
+  const bool threaded = std::getenv("JOIN_REPLAY_THREADS") != nullptr;
   double t_total = 0;
   size_t ev_total = 0;
   std::vector<std::unique_ptr<JoinShard>> shards;
@@ -98,13 +102,24 @@ int main(int argc, char** argv) {
       shards[s]->begin_batch(now, (uint64_t)b);
     }
     const auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::vector<std::pair<size_t, size_t>>> range(shards.size());
     size_t i = 0;
     while (i < n) {
       const int32_t srv = files[chunk_file[e[i].chunk]].server;
       size_t j = i;
       while (j < n && files[chunk_file[e[j].chunk]].server == srv) ++j;
-      shards[srv]->process(e + i, j - i, (const uint8_t*)by_p, chunk_file);
+      range[srv].push_back({i, j});
       i = j;
+    }
+    auto run = [&](size_t s) {
+      for (auto& r : range[s]) shards[s]->process(e + r.first, r.second - r.first, (const uint8_t*)by_p, chunk_file);
+    };
+    if (threaded) {
+      std::vector<std::thread> th;
+      for (size_t s = 0; s < shards.size(); ++s) th.emplace_back(run, s);
+      for (auto& t : th) t.join();
+    } else {
+      for (size_t s = 0; s < shards.size(); ++s) run(s);
     }
     const double dt = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (quiet) {

@@ -322,3 +322,38 @@ def test_parse_prefetch_pipelining_is_transparent():
         assert out[k] == plain[k], k
     for p, *_ in bufs:
         N.free_pinned(p)
+
+
+@pytest.mark.parametrize("dtype", ["float64", "bfloat16"])
+def test_deterministic_replay(dtype):
+    """Same input, two engines: every output stream is bitwise identical (device atomics in
+    K7 / K14 and the K9 sort must not leak scheduling order into the results)."""
+    lines, bl = synth_batches(21, duration=500, servers=3)
+    C = small_cfg("rolling")
+    C["gpu"]["ringDtype"] = dtype
+    _, a = _run_engine(C, bl)
+    _, b = _run_engine(copy.deepcopy(C), bl)
+    for k in ("transactions", "audit_db", "db", "st", "fs", "al"):
+        assert a[k] == b[k], k
+    assert len(a["fs"]) > 100
+
+
+def test_sink_fds_match_in_memory_streams(tmp_path):
+    """The output lane (released tx, st, fs) and the stats thread (tx, audit, al) write their
+    streams straight to sink fds: the files equal the in-memory streams of a second engine."""
+    lines, bl = synth_batches(5, duration=600)
+    C = small_cfg("exact")
+    _, want = _run_engine(C, bl)
+    eng = APMEngine(copy.deepcopy(C), keep_text=True)
+    kinds = ("transactions", "audit_db", "db", "st", "fs", "al")
+    files = {k: open(tmp_path / f"{k}.out", "wb") for k in kinds}
+    for k in kinds:
+        eng.eng.set_sink_fd(k, files[k].fileno())
+    for now, chunks in bl:
+        eng.process_lines(chunks, now)
+    eng.eng.flush()
+    for k in kinds:
+        files[k].close()
+        got = (tmp_path / f"{k}.out").read_text().splitlines()
+        assert got == want[k], k
+        assert eng.eng.sink_bytes(k) == (tmp_path / f"{k}.out").stat().st_size

@@ -22,20 +22,25 @@ pytestmark = pytest.mark.skipif(shutil.which("hipcc") is None and not os.path.ex
                                 reason="hipcc not available")
 
 
-def build(tmp):
-    exe = os.path.join(tmp, "join_replay")
+def build(tmp, tsan=False):
+    exe = os.path.join(tmp, "join_replay_tsan" if tsan else "join_replay")
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
-    san = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
-           "-Xarch_host", "-fno-omit-frame-pointer", "-Xarch_host", "-fno-sanitize-recover=all"]
+    if tsan:
+        san = ["-Xarch_host", "-fsanitize=thread", "-Xarch_host", "-fno-omit-frame-pointer"]
+        link = ["-fsanitize=thread", "-pthread"]
+    else:
+        san = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+               "-Xarch_host", "-fno-omit-frame-pointer", "-Xarch_host", "-fno-sanitize-recover=all"]
+        link = ["-fsanitize=address,undefined"]
     cmd = [hipcc, "-O1", "-g", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950", *san, "-I", CSRC,
            os.path.join(ROOT, "tests", "native", "join_replay.cpp"), os.path.join(CSRC, "runtime", "join.cpp"),
-           "-o", exe, "-fsanitize=address,undefined"]
+           "-o", exe, *link]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     return exe
 
 
-def test_join_under_asan_ubsan(tmp_path):
+def _replay_dir(tmp_path):
     cfg = SynthConfig(servers=2, duration_s=240, tx_per_sec_per_server=3, seed=13, audit_fraction=0.3,
                       soap_late_fraction=0.4, missing_logid_fraction=0.05, baf_fraction=0.5)
     lines = Generator(cfg).generate()
@@ -62,11 +67,30 @@ def test_join_under_asan_ubsan(tmp_path):
         (d / f"batch_{b}.events").write_bytes(ev.tobytes())
         (d / f"batch_{b}.bytes").write_bytes(buf)
         (d / f"batch_{b}.meta").write_text(f"{now:.0f}\n" + "\n".join(map(str, cf)) + "\n")
+    return d, len(bl), want
+
+
+def test_join_under_asan_ubsan(tmp_path):
+    d, nb, want = _replay_dir(tmp_path)
     exe = build(str(tmp_path))
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:halt_on_error=1",
                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
-    r = subprocess.run([exe, str(d), str(len(bl))], capture_output=True, text=True, env=env, timeout=600)
+    r = subprocess.run([exe, str(d), str(nb)], capture_output=True, text=True, env=env, timeout=600)
     assert r.returncode == 0, r.stderr[-4000:]
     assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr
     got = r.stdout.splitlines()
     assert got == want and len(want) > 100
+
+
+def test_parallel_join_under_tsan(tmp_path):
+    """The engine joins every JVM shard on its own thread against one shared service dictionary:
+    the same replay, one thread per shard per batch, under ThreadSanitizer."""
+    d, nb, want = _replay_dir(tmp_path)
+    exe = build(str(tmp_path), tsan=True)
+    env = dict(os.environ, JOIN_REPLAY_THREADS="1", TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1")
+    r = subprocess.run([exe, str(d), str(nb)], capture_output=True, text=True, env=env, timeout=600)
+    if "FATAL: ThreadSanitizer" in r.stderr and "memory" in r.stderr:
+        pytest.skip("ThreadSanitizer cannot map its shadow memory on this kernel: " + r.stderr[-300:])
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "WARNING: ThreadSanitizer" not in r.stderr
+    assert r.stdout.splitlines() == want

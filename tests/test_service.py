@@ -186,3 +186,11 @@ def test_fault_injection_exit(tmp_path):
          str(tmp_path))
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, timeout=120)
     assert r.returncode == 17, r.stderr.decode()[-2000:]
+
+
+def test_latency_percentiles_nearest_rank():
+    from apmbackend_amd.runtime.service import _percentiles
+    assert _percentiles([], (50, 99)) == ["-", "-"]
+    xs = [float(i) for i in range(1, 101)]
+    assert _percentiles(xs, (50, 90, 99)) == ["50.0", "90.0", "99.0"]
+    assert _percentiles([7.0], (50, 99)) == ["7.0", "7.0"]
