@@ -45,6 +45,7 @@ enum : uint32_t {
   PM_BAF = 1u << 24,          // \[[^ ]+] +INFO   (BAF metadata present)
   PM_HOST = 1u << 25,         // non-ASCII / exotic number forms: host re-derives the fields
   PM_HAS_INFO2 = 1u << 26,    // a second "INFO" occurrence bounds the INFO segment
+  PM_KEYS = 1u << 27,         // EJB/CT: t0 is the bracket-stripped logId, key / svc hold its hashes
 };
 
 // One event per relevant line, in line order (ordered stream compaction).
@@ -63,9 +64,14 @@ struct Event {
   uint16_t tBs, tBe;    // ejb exit: token 11; ct exit: INFO-segment token 5
   double ts;            // parsed "t1 t2" timestamp in UTC ms (NaN if unparseable)
   double num;           // parseInt(elapsed token) (NaN if none)
+  // PM_KEYS events: the join's map keys, hashed on the GPU so the host never touches the line
+  // bytes of an entry event: key = hash_bytes(logId), svc = hash_bytes(service name, seed by
+  // kind: kHashSeedEjb for the "S:"-prefixed EJB names, kHashSeed for CommonTiming)
+  uint64_t key;
+  uint64_t svc;
 };
 
-static_assert(sizeof(Event) == 64, "Event layout");
+static_assert(sizeof(Event) == 80, "Event layout");
 
 // ----------------------------------------------------------------------------- transactions
 // A completed transaction handed from the join to the stats stage.

@@ -98,6 +98,7 @@ EngineConfig config_from(const py::dict& d) {
   c.need_ttl_ms = get<double>(d, "need_ttl_ms", c.need_ttl_ms);
   c.tz = tz_from(d);
   c.join_threads = get<int>(d, "join_threads", c.join_threads);
+  c.pin_threads = get<bool>(d, "pin_threads", c.pin_threads);
   c.outputs = get<uint32_t>(d, "outputs", c.outputs);
   c.async_stats = get<int>(d, "async_stats", c.async_stats);
   return c;
@@ -234,6 +235,10 @@ class JoinHarness {
 PYBIND11_MODULE(_apm_native, m) {
   m.doc() = "apm-mi355x native runtime (HIP kernels for gfx950 + host runtime)";
   m.attr("EVENT_SIZE") = (int)sizeof(Event);
+  m.def("hash_bytes", [](py::bytes b, uint64_t seed) {
+    const std::string s = b;
+    return hash_bytes(s.data(), s.size(), seed);
+  }, py::arg("data"), py::arg("seed") = kHashSeed);
   m.attr("NSLOT") = NSLOT;
 
   py::class_<Engine>(m, "Engine")
@@ -318,6 +323,7 @@ PYBIND11_MODULE(_apm_native, m) {
       })
       .def("set_sink_fd", &Engine::set_sink_fd, py::call_guard<py::gil_scoped_release>())
       .def("sink_bytes", &Engine::sink_bytes)
+      .def("lane_cpus", &Engine::lane_cpus)
       .def("last_events", [](Engine& e) { return py::bytes(e.last_events()); })
       .def("warm_history", &Engine::warm_history)
       .def("metrics", [](Engine& e) {

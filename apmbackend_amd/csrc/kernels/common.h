@@ -85,6 +85,35 @@ __host__ __device__ inline double js_round_fixed(double x, int f) {
   return neg ? -r : r;
 }
 
+// Join-key hash, shared by the parse kernel (which hashes logIds and service names into the
+// Event) and the host join / checkpoints: word-at-a-time, one 64x64->128 multiply folded per
+// 8 bytes (wyhash-style).  FNV-1a's byte-serial multiply chain cost ~4 cycles per byte.
+__host__ __device__ inline uint64_t hash_mix(uint64_t a, uint64_t b) {
+  const __uint128_t r = (__uint128_t)a * b;
+  return (uint64_t)r ^ (uint64_t)(r >> 64);
+}
+
+constexpr uint64_t kHashSeed = 0x243f6a8885a308d3ULL;     // logId keys, plain service names
+constexpr uint64_t kHashSeedEjb = 0x13198a2e03707344ULL;  // "S:" + EJB service names
+
+__host__ __device__ inline uint64_t hash_bytes(const void* data, size_t n, uint64_t seed = kHashSeed) {
+  const uint8_t* p = static_cast<const uint8_t*>(data);
+  uint64_t h = seed ^ hash_mix(n ^ 0xa0761d6478bd642fULL, 0xe7037ed1a0b428dbULL);
+  while (n >= 8) {
+    uint64_t w;
+    memcpy(&w, p, 8);
+    h = hash_mix(h ^ w, 0x8ebc6af09c88c6e3ULL);
+    p += 8;
+    n -= 8;
+  }
+  if (n) {
+    uint64_t w = 0;
+    memcpy(&w, p, n);
+    h = hash_mix(h ^ w ^ ((uint64_t)n << 59), 0x589965cc75374cc3ULL);
+  }
+  return hash_mix(h, 0x1d8e4e27c47d124fULL);
+}
+
 // 64-bit FNV-1a (host and device agree; used for dictionary keys).
 __host__ __device__ inline uint64_t fnv1a64(const uint8_t* p, int n, uint64_t h = 1469598103934665603ULL) {
   for (int i = 0; i < n; ++i) { h ^= p[i]; h *= 1099511628211ULL; }

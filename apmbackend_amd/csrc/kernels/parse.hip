@@ -247,6 +247,8 @@ __global__ __launch_bounds__(PARSE_BLOCK) void k_parse_lines(ParseArgs a) {
   ev.tAs = ev.tAe = ev.tBs = ev.tBe = 0xffff;
   ev.ts = apm_nan();
   ev.num = apm_nan();
+  ev.key = 0;
+  ev.svc = 0;
   const uint8_t fk = a.chunk_kind[ev.chunk];
   if (len <= 0 || len > 65000) {
     // empty lines are skipped by readLine; absurdly long lines go to the host verbatim
@@ -398,6 +400,24 @@ __global__ __launch_bounds__(PARSE_BLOCK) void k_parse_lines(ParseArgs a) {
     }
   }
   if (ts_host && kind >= LK_EJB_ENTRY && kind <= LK_CT_EXIT) m |= PM_HOST;
+  // join keys: logId = token 0 without its [..] wrapper (.replace(/[[\]]/g,'')); lines with
+  // brackets inside the logId keep the raw token and are keyed on the host
+  if (kind >= LK_EJB_ENTRY && kind <= LK_CT_EXIT && !(m & PM_HOST) && ntok >= 1) {
+    int a0 = ev.t0s, b0 = ev.t0e;
+    if (a0 < b0 && p[a0] == '[') ++a0;
+    if (b0 > a0 && p[b0 - 1] == ']') --b0;
+    bool inner = false;
+    for (int i = a0; i < b0; ++i) inner |= (p[i] == '[' || p[i] == ']');
+    if (!inner) {
+      ev.t0s = (uint16_t)a0;
+      ev.t0e = (uint16_t)b0;
+      ev.key = hash_bytes(p + a0, (size_t)(b0 - a0));
+      const uint64_t seed = kind <= LK_EJB_EXIT ? kHashSeedEjb : kHashSeed;
+      ev.svc = ev.tAs != 0xffff ? hash_bytes(p + ev.tAs, (size_t)(ev.tAe - ev.tAs), seed)
+                                : hash_bytes("undefined", 9, seed);
+      m |= PM_KEYS;
+    }
+  }
   ev.kind = kind;
   ev.mask = m;
   a.line_mask[li] = m;

@@ -1,6 +1,12 @@
 // apm::Engine implementation -- see engine.h.
 #include "engine.h"
 
+#include <pthread.h>
+#include <sched.h>
+
+#include <cctype>
+#include <fstream>
+
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <unistd.h>
@@ -26,14 +32,96 @@ double now_ms() {
 }
 }  // namespace
 
+// ----------------------------------------------------------------------------- CPU placement
+// Host lanes (join workers, stats thread, output lane) can be pinned to physical cores local to
+// the GPU's PCIe root: the pinned batch buffers and the device's DMA live on that NUMA node, and
+// a pinned join worker keeps its shard's maps in one core's L2 / one CCD's L3.  Ranks whose GPUs
+// share a NUMA node take disjoint slices of its cores (slice = rank among those GPUs).
+void pin_current_thread(int cpu) {
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  CPU_SET(cpu, &set);
+  pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+}
+
+namespace {
+std::vector<int> parse_cpulist(const std::string& s) {
+  std::vector<int> out;
+  size_t i = 0;
+  while (i < s.size()) {
+    size_t j = s.find(',', i);
+    if (j == std::string::npos) j = s.size();
+    const std::string tok = s.substr(i, j - i);
+    const size_t dash = tok.find('-');
+    try {
+      if (dash == std::string::npos) {
+        if (!tok.empty() && tok != "\n") out.push_back(std::stoi(tok));
+      } else {
+        const int a = std::stoi(tok.substr(0, dash)), b = std::stoi(tok.substr(dash + 1));
+        for (int c = a; c <= b; ++c) out.push_back(c);
+      }
+    } catch (...) {
+    }
+    i = j + 1;
+  }
+  return out;
+}
+
+std::string read_small(const std::string& path) {
+  std::ifstream f(path);
+  std::string s;
+  std::getline(f, s);
+  return s;
+}
+
+std::string pci_dir(int device) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) return "";
+  std::string b(bus);
+  for (char& c : b) c = (char)std::tolower((unsigned char)c);
+  return "/sys/bus/pci/devices/" + b;
+}
+}  // namespace
+
+std::vector<int> local_core_slice(int device) {
+  const std::string dir = pci_dir(device);
+  if (dir.empty()) return {};
+  const std::string mine = read_small(dir + "/local_cpulist");
+  std::vector<int> local = parse_cpulist(mine);
+  cpu_set_t allowed;
+  CPU_ZERO(&allowed);
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return {};
+  std::vector<int> cores;  // one CPU per physical core (the first SMT sibling), allowed for us
+  for (int c : local) {
+    if (!CPU_ISSET(c, &allowed)) continue;
+    const std::vector<int> sib =
+        parse_cpulist(read_small("/sys/devices/system/cpu/cpu" + std::to_string(c) + "/topology/thread_siblings_list"));
+    if (sib.empty() || sib[0] == c) cores.push_back(c);
+  }
+  int n_dev = 0;
+  if (hipGetDeviceCount(&n_dev) != hipSuccess) n_dev = device + 1;
+  int slot = 0, peers = 0;
+  for (int d = 0; d < n_dev; ++d) {
+    if (read_small(pci_dir(d) + "/local_cpulist") != mine) continue;
+    if (d < device) ++slot;
+    ++peers;
+  }
+  peers = std::max(peers, 1);
+  const size_t per = cores.size() / (size_t)peers;
+  if (per == 0) return {};
+  return std::vector<int>(cores.begin() + (ptrdiff_t)(slot * per), cores.begin() + (ptrdiff_t)((slot + 1) * per));
+}
+
 // ----------------------------------------------------------------------------- thread pool
 // Static task placement: task t always runs on worker t % W.  A join shard's working set (its
 // TTL maps, several MB) then stays in one core's L2 / one CCD's L3 from batch to batch; with
 // first-come task grabbing every batch moved each shard to a cold core (measured: the same
 // join ran 2.2x slower per shard inside the engine than alone).
-ThreadPool::ThreadPool(int n) {
+ThreadPool::ThreadPool(int n, const std::vector<int>& cpus) {
   for (int i = 0; i < n; ++i) {
-    workers_.emplace_back([this, i, n]() {
+    const int cpu = cpus.empty() ? -1 : cpus[(size_t)i % cpus.size()];
+    workers_.emplace_back([this, i, n, cpu]() {
+      if (cpu >= 0) pin_current_thread(cpu);
       uint64_t seen = 0;
       for (;;) {
         std::unique_lock<std::mutex> lk(mu_);
@@ -86,6 +174,10 @@ void* Engine::dmalloc(size_t bytes) {
   bytes = (bytes + 255) & ~(size_t)255;
   HIP_OK(hipMalloc(&p, bytes));
   HIP_OK(hipMemset(p, 0, bytes));
+  // hipMemset runs on the null stream, which does not order against the engine's non-blocking
+  // streams: without this, a buffer regrown mid-run could be zeroed *after* the first copy into
+  // it on stream_ (seen: K12 names table read back as zeros after a regrow)
+  HIP_OK(hipDeviceSynchronize());
   allocations_.push_back(p);
   device_bytes_ += bytes;
   return p;
@@ -203,14 +295,31 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     HIP_OK(hipEventCreateWithFlags(&ev_fmt_[k], hipEventDisableTiming));
   }
   // threads
+  const char* pin_env = std::getenv("APM_PIN_THREADS");
+  if (pin_env ? std::atoi(pin_env) != 0 : cfg_.pin_threads) lane_cpus_ = local_core_slice(cfg_.device);
   int nt = cfg_.join_threads;
   if (nt <= 0) nt = (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
-  pool_.reset(new ThreadPool(nt > 1 ? nt : 0));
+  {
+    // join workers take the first cores of the slice; the stats thread and output lane the next two
+    std::vector<int> wc(lane_cpus_.begin(), lane_cpus_.begin() + (ptrdiff_t)std::min<size_t>(lane_cpus_.size(), (size_t)std::max(nt, 0)));
+    pool_.reset(new ThreadPool(nt > 1 ? nt : 0, wc));
+  }
   for (int l = 0; l < MAX_LAGS; ++l) { alias_thr_[l] = cfg_.thr[l]; alias_infl_[l] = cfg_.infl[l]; }
   HIP_OK(hipStreamSynchronize(stream_));
   HIP_OK(hipDeviceSynchronize());
-  stats_thread_ = std::thread([this]() { hipSetDevice(cfg_.device); stats_worker(); });
-  out_thread_ = std::thread([this]() { hipSetDevice(cfg_.device); out_worker(); });
+  const int nt_used = std::max(cfg_.join_threads > 0 ? cfg_.join_threads : 0, pool_->size());
+  const int st_cpu = (int)lane_cpus_.size() > nt_used ? lane_cpus_[nt_used] : -1;
+  const int out_cpu = (int)lane_cpus_.size() > nt_used + 1 ? lane_cpus_[nt_used + 1] : -1;
+  stats_thread_ = std::thread([this, st_cpu]() {
+    if (st_cpu >= 0) pin_current_thread(st_cpu);
+    hipSetDevice(cfg_.device);
+    stats_worker();
+  });
+  out_thread_ = std::thread([this, out_cpu]() {
+    if (out_cpu >= 0) pin_current_thread(out_cpu);
+    hipSetDevice(cfg_.device);
+    out_worker();
+  });
 }
 
 Engine::~Engine() {
@@ -540,16 +649,27 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
 
   // ---- join on the host, one task per server shard
   const double clock = now_override >= 0 ? now_override : watermark_;
-  std::vector<std::pair<uint32_t, uint32_t>> shard_range(shards_.size(), {0, 0});
+  // Event ranges per shard without walking the events (15 MB of freshly DMA'd records): events
+  // are in chunk order, so each run of same-server chunks maps to one binary-searched range.
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> shard_range(shards_.size());
   {
-    // events are in chunk order and chunks are grouped by server -> contiguous per shard
-    uint32_t i = 0;
-    while (i < n_events) {
-      const int32_t srv = files_[chunk_file[h_events[i].chunk]].server;
-      uint32_t j = i;
-      while (j < n_events && files_[chunk_file[h_events[j].chunk]].server == srv) ++j;
-      shard_range[srv] = {i, j};
-      i = j;
+    auto first_event_of_chunk = [&](uint32_t c) {
+      uint32_t lo = 0, hi = n_events;
+      while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo) / 2;
+        if (h_events[mid].chunk < c) lo = mid + 1; else hi = mid;
+      }
+      return lo;
+    };
+    const uint32_t nc = (uint32_t)chunk_file.size();
+    uint32_t c = 0;
+    while (c < nc) {
+      const int32_t srv = files_[chunk_file[c]].server;
+      uint32_t d = c + 1;
+      while (d < nc && files_[chunk_file[d]].server == srv) ++d;
+      const uint32_t lo = first_event_of_chunk(c), hi = first_event_of_chunk(d);
+      if (hi > lo) shard_range[srv].push_back({lo, hi});
+      c = d;
     }
   }
   shard_ms_.assign(shards_.size() * 16, 0.0);  // one cache line per shard
@@ -558,8 +678,7 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
     JoinShard& sh = *shards_[s];
     sh.out().clear();
     sh.begin_batch(clock, batch_no_);
-    const auto r = shard_range[s];
-    if (r.second > r.first) sh.process(h_events + r.first, r.second - r.first, hb, chunk_file);
+    for (const auto& r : shard_range[s]) sh.process(h_events + r.first, r.second - r.first, hb, chunk_file);
     shard_ms_[(size_t)s * 16] = now_ms() - ts0;
   });
   const double t1b = now_ms();
@@ -606,10 +725,18 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
     std::sort(order.begin(), order.end(), [&](int a, int b) {
       return shards_[a]->out()[split[a]].seq < shards_[b]->out()[split[b]].seq;
     });
+    const size_t line_part = txs.size();
     for (int k : order) {
       auto& v = shards_[k]->out();
       txs.insert(txs.end(), v.begin() + split[k], v.end());
     }
+    // a server whose chunks are not contiguous in the batch has several line ranges: order the
+    // line emissions by their (line, sub) key
+    bool multi = false;
+    for (auto& r : shard_range) multi |= r.size() > 1;
+    if (multi)
+      std::stable_sort(txs.begin() + (ptrdiff_t)line_part, txs.end(),
+                       [](const TxOut& a, const TxOut& b) { return a.seq < b.seq; });
   }
   const double t2 = now_ms();
   metrics_.t_join_ms += t2 - t1;
@@ -1509,8 +1636,7 @@ void Engine::fleet_init(const std::vector<uint8_t>& uid, const std::vector<uint8
   fleet_cap_ = cap;
   fleet_elems_ = (size_t)cap * cfg_.n_lags * NSTAT * 3;
   for (int i = 0; i < 2; ++i) {
-    fleet_buf_[i] = (double*)dmalloc(fleet_elems_ * 8);
-    HIP_OK(hipMemset(fleet_buf_[i], 0, fleet_elems_ * 8));
+    fleet_buf_[i] = (double*)dmalloc(fleet_elems_ * 8);  // zeroed (and synchronised) by dmalloc
     HIP_OK(hipEventCreateWithFlags(&fleet_ev_[i], hipEventDisableTiming));
   }
   fleet_rounds_ = 0;

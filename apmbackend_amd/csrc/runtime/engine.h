@@ -80,6 +80,7 @@ struct EngineConfig {
   double record_ttl_ms = 120000, acct_ttl_ms = 120000, need_ttl_ms = 30000;
   TzTable tz{};
   int join_threads = 0;
+  bool pin_threads = false;  // pin host lanes to GPU-local physical cores (APM_PIN_THREADS overrides)
   // outputs: bit k of `outputs` materialises stream k (OutKind) in the reference wire format
   uint32_t outputs = 0;
   int async_stats = 1;      // overlap batch i's stats with batch i+1's parse + join
@@ -134,9 +135,12 @@ struct EngineMetrics {
   std::vector<double> rollover_latency_ms;   // batch arrival -> alert decision per rollover
 };
 
+void pin_current_thread(int cpu);
+std::vector<int> local_core_slice(int device);  // this GPU's share of its NUMA node's physical cores
+
 class ThreadPool {
  public:
-  explicit ThreadPool(int n);
+  explicit ThreadPool(int n, const std::vector<int>& cpus = {});
   ~ThreadPool();
   void run(int n_tasks, const std::function<void(int)>& fn);
   int size() const { return (int)workers_.size(); }
@@ -236,6 +240,7 @@ class Engine {
   EngineMetrics metrics() { flush(); return metrics_; }
   const std::vector<std::string>& servers() const { return servers_; }
   const std::vector<FileInfo>& files() const { return files_; }
+  const std::vector<int>& lane_cpus() const { return lane_cpus_; }
   std::vector<std::string> services() const { return dict_.services_snapshot(); }
   int32_t n_series() const { return n_series_; }
   double watermark() const { return watermark_; }
@@ -334,6 +339,7 @@ class Engine {
   Dictionary dict_;
   std::vector<std::unique_ptr<JoinShard>> shards_;  // one per server
   std::unique_ptr<ThreadPool> pool_;
+  std::vector<int> lane_cpus_;  // pinned placement (empty: unpinned)
   std::vector<double> shard_ms_;  // per-shard join time of the current batch (stride 16)
 
   // series

@@ -10,9 +10,7 @@
 // maps hold one or two services per logId, so the common case allocates nothing; the spill is a
 // single pointer so a map value stays within one cache line.
 //
-// hash_bytes: word-at-a-time 64-bit hash (128-bit multiply folding, wyhash-style) for the join
-// keys.  FNV-1a's byte-serial multiply chain cost ~4 cycles per byte on every event; this is
-// one multiply per 8 bytes.
+// Keys are hash_bytes() values (kernels/common.h), shared with the parse kernel.
 #pragma once
 #include <algorithm>
 #include <cstdint>
@@ -20,30 +18,9 @@
 #include <utility>
 #include <vector>
 
+#include "../kernels/common.h"
+
 namespace apm {
-
-inline uint64_t hash_mix(uint64_t a, uint64_t b) {
-  const __uint128_t r = (__uint128_t)a * b;
-  return (uint64_t)r ^ (uint64_t)(r >> 64);
-}
-
-inline uint64_t hash_bytes(const void* data, size_t n, uint64_t seed = 0x243f6a8885a308d3ULL) {
-  const uint8_t* p = static_cast<const uint8_t*>(data);
-  uint64_t h = seed ^ hash_mix(n ^ 0xa0761d6478bd642fULL, 0xe7037ed1a0b428dbULL);
-  while (n >= 8) {
-    uint64_t w;
-    std::memcpy(&w, p, 8);
-    h = hash_mix(h ^ w, 0x8ebc6af09c88c6e3ULL);
-    p += 8;
-    n -= 8;
-  }
-  if (n) {
-    uint64_t w = 0;
-    std::memcpy(&w, p, n);
-    h = hash_mix(h ^ w ^ ((uint64_t)n << 59), 0x589965cc75374cc3ULL);
-  }
-  return hash_mix(h, 0x1d8e4e27c47d124fULL);
-}
 
 template <class V>
 class FlatMap {

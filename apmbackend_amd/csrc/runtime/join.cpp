@@ -145,8 +145,7 @@ int32_t Dictionary::service_id(std::string_view normalized) {
   return id;
 }
 
-int32_t JoinShard::raw_service(bool ejb, std::string_view name) {
-  const uint64_t h = svc_hash(ejb, name);
+int32_t JoinShard::raw_service(uint64_t h, bool ejb, std::string_view name) {
   const size_t raw_len = name.size() + (ejb ? 2 : 0);
   if (const int32_t* slot = raw_svc_map_.find(h)) {
     if (svc_info_[*slot - 1].raw_len == raw_len) return *slot - 1;
@@ -412,7 +411,8 @@ void JoinShard::on_ejb(const Event& e, std::string_view line, int32_t file, bool
   if (host) { all = js::split_ws(line, 16); tk.n = (int)all.size(); for (int k = 0; k < tk.n && k < 16; ++k) tk.t[k] = all[k]; }
   else tk.from_event(e, line);
   std::string scratch;
-  const std::string_view log_id = strip_brackets(tk.t[0], scratch);
+  const bool keyed = e.mask & PM_KEYS;  // t0 already stripped, key / svc hashed by the kernel
+  const std::string_view log_id = keyed ? tk.t[0] : strip_brackets(tk.t[0], scratch);
   double ts;
   bool ts_empty = false;
   if (!host && tk.has(2)) {
@@ -424,8 +424,8 @@ void JoinShard::on_ejb(const Event& e, std::string_view line, int32_t file, bool
   if (entry) {  // parseEjbCommonTimingEntry (:378-401)
     if (log_id.empty()) return;
     const std::string_view nm = host ? tk.get(13) : (e.tAs != 0xffff ? line.substr(e.tAs, e.tAe - e.tAs) : kUndef);
-    const int32_t svc = raw_service(true, nm);
-    auto& items = record_map(key_of(log_id)).items;
+    const int32_t svc = keyed ? raw_service(e.svc, true, nm) : raw_service(true, nm);
+    auto& items = record_map(keyed ? e.key : key_of(log_id)).items;
     auto f = std::find_if(items.begin(), items.end(), [&](const Partial& p) { return p.svc == svc; });
     if (f != items.end()) { f->server = server; f->start_ms = ts; }
     else items.push_back(Partial{svc, server, ts});
@@ -441,12 +441,12 @@ void JoinShard::on_ejb(const Event& e, std::string_view line, int32_t file, bool
     nm = e.tAs != 0xffff ? line.substr(e.tAs, e.tAe - e.tAs) : kUndef;
     elapsed = e.num;
   }
-  const int32_t svc = raw_service(true, nm);
+  const int32_t svc = keyed ? raw_service(e.svc, true, nm) : raw_service(true, nm);
   if (log_id.empty()) {
     output(server, svc, "", js::nan(), 0, true, ts, ts_empty, elapsed, false, seq);
     return;
   }
-  const uint64_t key = key_of(log_id);
+  const uint64_t key = keyed ? e.key : key_of(log_id);
   RecordEntry* it = record_.find(key);
   if (!it) { ++counters.ejb_exit_unmatched; return; }
   auto& items = it->items;
@@ -471,7 +471,8 @@ void JoinShard::on_ct(const Event& e, std::string_view line, int32_t file, bool 
   Toks tk;
   if (host) tk.from_line(line); else tk.from_event(e, line);
   std::string scratch;
-  const std::string_view log_id = strip_brackets(tk.t[0], scratch);
+  const bool keyed = e.mask & PM_KEYS;
+  const std::string_view log_id = keyed ? tk.t[0] : strip_brackets(tk.t[0], scratch);
   double ts;
   bool ts_empty = false;
   if (!host && tk.has(2)) {
@@ -492,10 +493,10 @@ void JoinShard::on_ct(const Event& e, std::string_view line, int32_t file, bool 
     has_elapsed = seg.size() > 5;
     if (has_elapsed) elapsed_v = seg[5];
   }
-  const int32_t svc = raw_service(service_v);
+  const int32_t svc = keyed ? raw_service(e.svc, false, service_v) : raw_service(service_v);
   if (entry) {  // parseCommonTimingEntry (:451-483)
     if (log_id.empty()) return;
-    auto& items = record_map(key_of(log_id)).items;
+    auto& items = record_map(keyed ? e.key : key_of(log_id)).items;
     auto f = std::find_if(items.begin(), items.end(), [&](const Partial& p) { return p.svc == svc; });
     if (f != items.end()) { f->server = server; f->start_ms = ts; }
     else items.push_back(Partial{svc, server, ts});
@@ -511,7 +512,7 @@ void JoinShard::on_ct(const Event& e, std::string_view line, int32_t file, bool 
            seq);
   };
   if (log_id.empty()) { salvage(); return; }
-  const uint64_t key = key_of(log_id);
+  const uint64_t key = keyed ? e.key : key_of(log_id);
   RecordEntry* it = record_.find(key);
   if (!it) { salvage(); return; }
   auto* items = &it->items;
@@ -661,6 +662,15 @@ void JoinShard::on_app(const Event& e, std::string_view line, int32_t file, uint
 void JoinShard::prefetch_event(const Event& e, const uint8_t* bytes) {
   const uint8_t k = e.kind;
   if (k < LK_EJB_ENTRY || k > LK_CT_EXIT || (e.mask & PM_HOST) || e.ntok == 0) return;
+  if (e.mask & PM_KEYS) {  // hashed on the GPU
+    record_.prefetch(e.key);
+    raw_svc_map_.prefetch(e.svc);
+    if (k == LK_EJB_EXIT || k == LK_CT_EXIT) {
+      acct_.prefetch(e.key);
+      __builtin_prefetch(bytes + e.off + e.t0s);  // the logId is copied into the tx line
+    }
+    return;
+  }
   const char* l = (const char*)bytes + e.off;
   const char* a = l + e.t0s;
   const char* b = l + e.t0e;

@@ -168,13 +168,14 @@ class alignas(128) JoinShard {
     void clear() { v.clear(); present.clear(); }
   };
 
-  static constexpr uint64_t kSeedPlain = 0x243f6a8885a308d3ULL, kSeedEjb = 0x13198a2e03707344ULL;
   static uint64_t key_of(std::string_view s) { return hash_bytes(s.data(), s.size()); }
   static uint64_t svc_hash(bool ejb, std::string_view name) {
-    return hash_bytes(name.data(), name.size(), ejb ? kSeedEjb : kSeedPlain);
+    return hash_bytes(name.data(), name.size(), ejb ? kHashSeedEjb : kHashSeed);
   }
   int32_t raw_service(std::string_view raw) { return raw_service(false, raw); }
-  int32_t raw_service(bool ejb, std::string_view name);  // interned ("S:" if ejb) + name
+  int32_t raw_service(bool ejb, std::string_view name) { return raw_service(svc_hash(ejb, name), ejb, name); }
+  // interned ("S:" if ejb) + name with its hash precomputed (PM_KEYS events: by the parse kernel)
+  int32_t raw_service(uint64_t h, bool ejb, std::string_view name);
   int32_t intern_service(std::string raw, uint64_t h);
   void prefetch_event(const Event& e, const uint8_t* bytes);
   void sweep();

@@ -35,6 +35,7 @@ PM_IN_SECTION = 1 << 17
 PM_BAF = 1 << 24
 PM_HOST = 1 << 25
 PM_HAS_INFO2 = 1 << 26
+PM_KEYS = 1 << 27
 SOAP_BITS = PM_SOAP_IN | PM_SOAP_OUT | PM_SOAP_ACCT | PM_SOAP_KEY | PM_SOAP_VALUE
 AUDIT_BITS = (PM_AUTR_MAP | PM_AUTR_HDR | PM_EL_START | PM_EL_END | PM_SW_START | PM_SW_END | PM_SW_NAME
               | PM_SW_STARTTS | PM_SW_STOPTS)
@@ -45,9 +46,32 @@ EVENT_DTYPE = np.dtype([
     ("kind", "u1"), ("ntok", "u1"), ("pad0", "<u2"),
     ("t0s", "<u2"), ("t0e", "<u2"), ("t1s", "<u2"), ("t1e", "<u2"), ("t2s", "<u2"), ("t2e", "<u2"),
     ("t3s", "<u2"), ("t3e", "<u2"), ("tAs", "<u2"), ("tAe", "<u2"), ("tBs", "<u2"), ("tBe", "<u2"),
-    ("ts", "<f8"), ("num", "<f8"),
+    ("ts", "<f8"), ("num", "<f8"), ("key", "<u8"), ("svc", "<u8"),
 ])
-assert EVENT_DTYPE.itemsize == 64
+assert EVENT_DTYPE.itemsize == 80
+
+_M64 = (1 << 64) - 1
+HASH_SEED = 0x243f6a8885a308d3
+HASH_SEED_EJB = 0x13198a2e03707344
+
+
+def _mix(a: int, b: int) -> int:
+    r = (a & _M64) * (b & _M64)
+    return (r ^ (r >> 64)) & _M64
+
+
+def hash_bytes(data: bytes, seed: int = HASH_SEED) -> int:
+    """kernels/common.h::hash_bytes (join keys: logIds and service names)."""
+    n = len(data)
+    h = seed ^ _mix(n ^ 0xa0761d6478bd642f, 0xe7037ed1a0b428db)
+    i = 0
+    while n - i >= 8:
+        h = _mix(h ^ int.from_bytes(data[i:i + 8], "little"), 0x8ebc6af09c88c6e3)
+        i += 8
+    r = n - i
+    if r:
+        h = _mix(h ^ int.from_bytes(data[i:], "little") ^ ((r << 59) & _M64), 0x589965cc75374cc3)
+    return _mix(h, 0x1d8e4e27c47d124f)
 
 _WS = b" \t\n\r\x0b\x0c"
 
@@ -275,7 +299,20 @@ def parse_line(p: bytes, fk: int, tz: TzOffset):
                     num = v
     if ts_host and LK_EJB_ENTRY <= kind <= LK_CT_EXIT:
         m |= PM_HOST
-    return kind, m, min(ntok, 15), toks, tA, tB, ts, num, wm
+    key = svc = 0
+    if LK_EJB_ENTRY <= kind <= LK_CT_EXIT and not (m & PM_HOST) and ntok >= 1:
+        a0, b0 = toks[0]
+        if a0 < b0 and p[a0] == ord("["):
+            a0 += 1
+        if b0 > a0 and p[b0 - 1] == ord("]"):
+            b0 -= 1
+        if b"[" not in p[a0:b0] and b"]" not in p[a0:b0]:
+            toks = [(a0, b0)] + toks[1:]
+            key = hash_bytes(p[a0:b0])
+            seed = HASH_SEED_EJB if kind <= LK_EJB_EXIT else HASH_SEED
+            svc = hash_bytes(p[tA[0]:tA[1]] if tA[0] != NOTOK else b"undefined", seed)
+            m |= PM_KEYS
+    return kind, m, min(ntok, 15), toks, tA, tB, ts, num, wm, key, svc
 
 
 def parse_batch(chunks: Sequence[Tuple[int, bytes]], tz: TzOffset, file_open: dict = None,
@@ -299,11 +336,11 @@ def parse_batch(chunks: Sequence[Tuple[int, bytes]], tz: TzOffset, file_open: di
             ln = raw[:-1] if raw.endswith(b"\r") else raw
             rec = {"line": line_idx, "chunk": ci, "off": ln_off, "len": len(ln), "keep": False}
             if 0 < len(ln) <= 65000:
-                kind, m, ntok, toks, tA, tB, ts, num, w = parse_line(ln, fk, tz)
+                kind, m, ntok, toks, tA, tB, ts, num, w, key, svc = parse_line(ln, fk, tz)
                 if w is not None and (wm is None or w > wm):
                     wm = w
                 rec.update(kind=kind, mask=m, ntok=ntok, toks=toks, tA=tA, tB=tB, ts=ts, num=num,
-                           keep=kind != LK_NONE)
+                           keep=kind != LK_NONE, key=key, svc=svc)
             elif len(ln) > 65000:
                 rec.update(kind=LK_SOAP if fk == FILE_SOAP else LK_APP, mask=PM_HOST, ntok=0, toks=[],
                            tA=(NOTOK, NOTOK), tB=(NOTOK, NOTOK), ts=float("nan"), num=float("nan"), keep=True)
@@ -346,6 +383,7 @@ def parse_batch(chunks: Sequence[Tuple[int, bytes]], tz: TzOffset, file_open: di
         ev[i]["tAs"], ev[i]["tAe"] = r["tA"]
         ev[i]["tBs"], ev[i]["tBe"] = r["tB"]
         ev[i]["ts"] = r["ts"]; ev[i]["num"] = r["num"]
+        ev[i]["key"] = r.get("key", 0); ev[i]["svc"] = r.get("svc", 0)
     return ev, line_idx, wm, buf
 
 

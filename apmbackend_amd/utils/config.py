@@ -43,6 +43,7 @@ GPU_DEFAULTS: Dict[str, Any] = {
     "batchBytes": 32 << 20,           # bytes of raw log per ingest batch
     "maxLinesPerBatch": 1 << 20,
     "ringDtype": "float64",          # z-score history ring: float64 | float32 | bfloat16
+    "pinThreads": False,             # pin join workers / stats / output lanes to GPU-local cores
     "zscoreMeanMode": "rolling",      # rolling (O(1) compensated) | exact (sequential, JS-bit-exact)
     "zscoreSigma": "sqrt_mean",       # sqrt_mean (reference quirk Q1) | stddev (true sigma)
     "exactRecomputeEveryIntervals": 360,

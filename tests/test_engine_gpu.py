@@ -357,3 +357,23 @@ def test_sink_fds_match_in_memory_streams(tmp_path):
         got = (tmp_path / f"{k}.out").read_text().splitlines()
         assert got == want[k], k
         assert eng.eng.sink_bytes(k) == (tmp_path / f"{k}.out").stat().st_size
+
+
+def test_interleaved_server_chunks_match_oracle():
+    """Chunks of different JVMs interleaved inside a batch: the engine lays the batch out in its
+    canonical order (grouped by JVM, caller's order otherwise), i.e. the oracle run on that
+    order."""
+    lines, bl = synth_batches(8, duration=600, servers=3)
+    inter = []
+    for now, chunks in bl:
+        by_base = sorted(chunks, key=lambda c: (c[0].rsplit("/", 1)[-1], c[0]))
+        inter.append((now, by_base))
+    assert any(len({fp.split("/")[2] for fp, _ in ch[:3]}) > 1 for _, ch in inter)
+    C = small_cfg("exact")
+    P = PipelineOracle(copy.deepcopy(C), UTC)
+    P.run_batches([(now, sorted(ch, key=lambda c: c[0].split("/")[2])) for now, ch in inter])
+    eng, out = _run_engine(C, inter)
+    assert out["transactions"] == P.tx_out
+    assert out["audit_db"] == P.audit_db
+    assert out["st"] == P.stats
+    assert out["fs"] == P.fs

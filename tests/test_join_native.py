@@ -73,3 +73,15 @@ def test_js_number_helpers_match_python():
 def test_flatmap_and_smallvec_against_std(key_space):
     N = _native.load()
     assert N.flatmap_selftest(200000, 12345 + key_space, key_space)
+
+
+def test_join_key_hash_python_matches_native():
+    """ops.parse_ref.hash_bytes (the model of the kernel's key hash) == the C++ host/device one."""
+    import random
+    from apmbackend_amd.ops.parse_ref import HASH_SEED, HASH_SEED_EJB, hash_bytes
+    N = _native.load()
+    rng = random.Random(5)
+    for n in list(range(0, 40)) + [63, 64, 65, 200]:
+        b = bytes(rng.randrange(256) for _ in range(n))
+        for seed in (HASH_SEED, HASH_SEED_EJB):
+            assert hash_bytes(b, seed) == N.hash_bytes(b, seed)
