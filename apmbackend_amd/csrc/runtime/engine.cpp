@@ -337,13 +337,11 @@ Engine::~Engine() {
   if (out_thread_.joinable()) out_thread_.join();
   if (fleet_comm_) {
     hipStreamSynchronize(comm_stream_);
+    hipStreamSynchronize(coll_stream_);
     ncclCommDestroy(fleet_comm_);
     fleet_comm_ = nullptr;
-  }
-  if (clock_comm_) {
-    hipStreamSynchronize(parse_stream_);
-    ncclCommDestroy(clock_comm_);
-    clock_comm_ = nullptr;
+    for (int i = 0; i < 2; ++i) { hipEventDestroy(fleet_ev_[i]); hipEventDestroy(pack_ev_[i]); }
+    hipStreamDestroy(coll_stream_);
   }
   if (h_sync_) hipHostFree(h_sync_);
   hipStreamSynchronize(stream_);
@@ -745,26 +743,21 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
   trace_event("join", t1, t1b, 0);
   trace_event("merge", t1b, t2, 0);
 
-  // ---- stats / z-score / alerts: handed to the stats thread, overlapping the next batch's
-  // H2D + parse (parse stream) and host join (pool) with this batch's GPU stats work.
-  post_stats(std::move(txs), t0);
-  metrics_.t_total_ms += now_ms() - t0;
-
   // advance the watermark clock (max leading timestamp seen so far)
   const unsigned long long wm = *ps.h_watermark;
   if (wm) {
     const double w = (double)((long long)wm - (1LL << 62));
     if (w > watermark_) watermark_ = w;
   }
-  if (clock_comm_) {  // lock-step: the cache clock is the node-wide watermark
-    h_sync_[0] = watermark_;
-    HIP_OK(hipMemcpyAsync(d_sync_, h_sync_, 8, hipMemcpyHostToDevice, parse_stream_));
-    if (ncclAllReduce(d_sync_, d_sync_, 1, ncclDouble, ncclMax, clock_comm_, parse_stream_) != ncclSuccess)
-      throw std::runtime_error("ncclAllReduce(watermark) failed");
-    HIP_OK(hipMemcpyAsync(h_sync_, d_sync_, 8, hipMemcpyDeviceToHost, parse_stream_));
-    HIP_OK(hipStreamSynchronize(parse_stream_));
-    watermark_ = h_sync_[0];
-  }
+  // lock-step: node-wide watermark (cache clock of the next batch) and newest bucket
+  if (lockstep_) lockstep_sync(txs);
+
+  // ---- stats / z-score / alerts: handed to the stats thread, overlapping the next batch's
+  // H2D + parse (parse stream) and host join (pool) with this batch's GPU stats work.
+  post_stats(std::move(txs), t0, lockstep_ ? sync_latest_ : INT64_MIN);
+  // post_stats returned: the stats thread finished (and packed) every earlier batch
+  if (fleet_comm_) fleet_exchange_upto(fleet_posted_ - 1);
+  metrics_.t_total_ms += now_ms() - t0;
   ++batch_no_;
 }
 
@@ -798,6 +791,7 @@ void Engine::stats_worker() {
       job.txs.swap(st_job_.txs);
       job.text.swap(st_job_.text);
       job.t0 = st_job_.t0;
+      job.sync_latest = st_job_.sync_latest;
       st_has_job_ = false;
     }
     const double t = now_ms();
@@ -805,8 +799,8 @@ void Engine::stats_worker() {
     try {
       cur_text_ = &job.text;
       stats_for_batch(job.txs, job.t0);
-      sync_latest_locked(job.t0);
-      fleet_exchange_locked();
+      apply_latest_locked(job.sync_latest, job.t0);
+      fleet_pack_locked();
       drain_sinks(~kLaneKinds);
     } catch (const std::exception& e) {
       std::lock_guard<std::mutex> g(st_mu_);
@@ -823,7 +817,7 @@ void Engine::stats_worker() {
   }
 }
 
-void Engine::post_stats(std::vector<TxOut>&& txs, double t0) {
+void Engine::post_stats(std::vector<TxOut>&& txs, double t0, int64_t sync_latest) {
   std::unique_lock<std::mutex> lk(st_mu_);
   st_cv_.wait(lk, [&]() { return !st_busy_; });
   if (!st_error_.empty()) { std::string e = st_error_; st_error_.clear(); throw std::runtime_error(e); }
@@ -845,6 +839,8 @@ void Engine::post_stats(std::vector<TxOut>&& txs, double t0) {
     }
   }
   st_job_.t0 = t0;
+  st_job_.sync_latest = sync_latest;
+  if (fleet_comm_) ++fleet_posted_;
   st_has_job_ = true;
   st_busy_ = true;
   lk.unlock();
@@ -1601,12 +1597,17 @@ void Engine::pack_service_moments(double* d_dst, int32_t cap, hipStream_t stream
   pack_moments_locked(d_dst, cap, stream);
 }
 
-// ---- native fleet exchange over RCCL -------------------------------------------------------
-// One all-reduce(SUM) per processed batch, issued by the stats thread on the comm stream right
-// after the batch's z-score work: it never blocks the host pipeline and overlaps the next
-// batch's parse + join.  Every rank processes the same number of batches (lock-step ingest), so
-// the collective sequence matches across ranks.  Two device slots: the exchange of batch i
-// lands in slot i%2 and `fleet_merged` reads the newest completed one.
+// ---- native fleet exchange + lock-step clocks over RCCL --------------------------------------
+// ONE communicator per rank, driven only by the ingest thread on its own stream (coll_stream_).
+// Per batch i, every rank issues exactly, in this order:
+//   1. (lock-step) all-reduce(MAX) of {watermark, newest bucket} -- 16 B, host waits for it;
+//   2. (fleet)     all-reduce(SUM) of the per-service moments of batch i-1 -- async.
+// The moments of batch i-1 are packed by the stats thread on the comm stream (pack_ev_), which
+// is guaranteed enqueued once post_stats(i) returned.  A single issuing thread per communicator
+// and a fixed per-batch sequence make the collective order identical on every rank, whatever
+// the thread timing, and no other stream ever waits on a peer (two communicators driven from
+// two threads can deadlock once their streams share a hardware queue).  Two device slots: the
+// exchange of batch j lands in slot j%2; `fleet_merged` flushes the pending one and reads it.
 std::vector<uint8_t> Engine::fleet_unique_id() {
   ncclUniqueId id;
   if (ncclGetUniqueId(&id) != ncclSuccess) throw std::runtime_error("ncclGetUniqueId failed");
@@ -1616,66 +1617,92 @@ std::vector<uint8_t> Engine::fleet_unique_id() {
 void Engine::fleet_init(const std::vector<uint8_t>& uid, const std::vector<uint8_t>& clock_uid, int nranks, int rank,
                         int32_t cap) {
   flush();
+  if (fleet_comm_) throw std::runtime_error("fleet_init called twice");
   if (uid.size() != sizeof(ncclUniqueId) || (!clock_uid.empty() && clock_uid.size() != sizeof(ncclUniqueId)))
     throw std::runtime_error("bad unique id size");
+  if (cap <= 0) throw std::runtime_error("fleet_init: cap must be > 0");
   ncclUniqueId id;
   std::memcpy(&id, uid.data(), sizeof(id));
   HIP_OK(hipSetDevice(cfg_.device));
   if (ncclCommInitRank(&fleet_comm_, nranks, id, rank) != ncclSuccess)
     throw std::runtime_error("ncclCommInitRank failed");
-  // Lock-step clocks: a second communicator owned by the ingest (main) thread -- RCCL
-  // communicators must not be driven from two threads at once.
-  if (!clock_uid.empty()) {
-    ncclUniqueId cid;
-    std::memcpy(&cid, clock_uid.data(), sizeof(cid));
-    if (ncclCommInitRank(&clock_comm_, nranks, cid, rank) != ncclSuccess)
-      throw std::runtime_error("ncclCommInitRank (clock) failed");
+  HIP_OK(hipStreamCreateWithFlags(&coll_stream_, hipStreamNonBlocking));
+  lockstep_ = !clock_uid.empty();
+  if (lockstep_) {
     d_sync_ = (double*)dmalloc(64);
     HIP_OK(hipHostMalloc((void**)&h_sync_, 64, hipHostMallocDefault));
   }
+  sync_latest_ = latest_;  // the stats thread is idle (flush above)
   fleet_cap_ = cap;
   fleet_elems_ = (size_t)cap * cfg_.n_lags * NSTAT * 3;
   for (int i = 0; i < 2; ++i) {
     fleet_buf_[i] = (double*)dmalloc(fleet_elems_ * 8);  // zeroed (and synchronised) by dmalloc
     HIP_OK(hipEventCreateWithFlags(&fleet_ev_[i], hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&pack_ev_[i], hipEventDisableTiming));
   }
-  fleet_rounds_ = 0;
+  fleet_rounds_ = fleet_posted_ = fleet_packed_ = 0;
+}
+
+// Ingest thread, after the join of a batch: the node-wide watermark becomes the cache clock of
+// the next batch, and the node-wide newest bucket decides this batch's rollovers.  The bucket is
+// the one stats_for_batch derives (non-db tx with a usable endTs), so ranks agree on `latest`
+// without the stats thread touching the communicator.
+void Engine::lockstep_sync(const std::vector<TxOut>& txs) {
+  int64_t b = sync_latest_;
+  for (const TxOut& t : txs) {
+    if (t.to_db || !(t.end_ms == t.end_ms) || t.end_ms < 10000) continue;
+    const int64_t tb = (int64_t)t.end_ms / 10000;
+    if (tb > b) b = tb;
+  }
+  h_sync_[0] = watermark_;
+  h_sync_[1] = b == INT64_MIN ? -1.0 : (double)b;  // buckets < 2^53: exact in a double
+  HIP_OK(hipMemcpyAsync(d_sync_, h_sync_, 16, hipMemcpyHostToDevice, coll_stream_));
+  if (ncclAllReduce(d_sync_, d_sync_, 2, ncclDouble, ncclMax, fleet_comm_, coll_stream_) != ncclSuccess)
+    throw std::runtime_error("ncclAllReduce(lock-step clocks) failed");
+  HIP_OK(hipMemcpyAsync(h_sync_, d_sync_, 16, hipMemcpyDeviceToHost, coll_stream_));
+  HIP_OK(hipStreamSynchronize(coll_stream_));
+  watermark_ = h_sync_[0];
+  if (h_sync_[1] >= 0) sync_latest_ = std::max(sync_latest_, (int64_t)h_sync_[1]);
 }
 
 // Stats thread: every rank rolls over when any rank saw a newer bucket, exactly as the single
 // reference stats process rolls over on the first tx of a new bucket from any JVM.
-void Engine::sync_latest_locked(double batch_t0) {
-  if (!clock_comm_) return;
-  int64_t* d = reinterpret_cast<int64_t*>(d_sync_) + 4;
-  HIP_OK(hipMemcpyAsync(d, &latest_, 8, hipMemcpyHostToDevice, comm_stream_));
-  if (ncclAllReduce(d, d, 1, ncclInt64, ncclMax, fleet_comm_, comm_stream_) != ncclSuccess)
-    throw std::runtime_error("ncclAllReduce(latest) failed");
-  int64_t g = 0;
-  HIP_OK(hipMemcpyAsync(&g, d, 8, hipMemcpyDeviceToHost, comm_stream_));
-  HIP_OK(hipStreamSynchronize(comm_stream_));
-  if (g > latest_) {
-    latest_ = g;
-    ++metrics_.lockstep_rollovers;
-    do_rollover(g, batch_t0);
+void Engine::apply_latest_locked(int64_t g, double batch_t0) {
+  if (g == INT64_MIN || g <= latest_) return;
+  latest_ = g;
+  ++metrics_.lockstep_rollovers;
+  do_rollover(g, batch_t0);
+}
+
+// Stats thread: pack this batch's moments into its slot (after the slot's previous all-reduce).
+void Engine::fleet_pack_locked() {
+  if (!fleet_comm_) return;
+  const int slot = (int)(fleet_packed_ & 1);
+  if (fleet_packed_ >= 2) HIP_OK(hipStreamWaitEvent(comm_stream_, fleet_ev_[slot], 0));
+  pack_moments_locked(fleet_buf_[slot], fleet_cap_, comm_stream_);
+  HIP_OK(hipEventRecord(pack_ev_[slot], comm_stream_));
+  ++fleet_packed_;
+}
+
+// Ingest thread: all-reduce the packed batches [fleet_rounds_, rounds).
+void Engine::fleet_exchange_upto(uint64_t rounds) {
+  while (fleet_rounds_ < rounds) {
+    const int slot = (int)(fleet_rounds_ & 1);
+    HIP_OK(hipStreamWaitEvent(coll_stream_, pack_ev_[slot], 0));
+    if (ncclAllReduce(fleet_buf_[slot], fleet_buf_[slot], fleet_elems_, ncclDouble, ncclSum, fleet_comm_,
+                      coll_stream_) != ncclSuccess)
+      throw std::runtime_error("ncclAllReduce(fleet moments) failed");
+    HIP_OK(hipEventRecord(fleet_ev_[slot], coll_stream_));
+    ++fleet_rounds_;
   }
 }
 
-void Engine::fleet_exchange_locked() {
-  if (!fleet_comm_) return;
-  const int slot = (int)(fleet_rounds_ & 1);
-  // comm stream order: previous collective on this slot completed before we overwrite it
-  pack_moments_locked(fleet_buf_[slot], fleet_cap_, comm_stream_);
-  if (ncclAllReduce(fleet_buf_[slot], fleet_buf_[slot], fleet_elems_, ncclDouble, ncclSum, fleet_comm_,
-                    comm_stream_) != ncclSuccess)
-    throw std::runtime_error("ncclAllReduce failed");
-  HIP_OK(hipEventRecord(fleet_ev_[slot], comm_stream_));
-  ++fleet_rounds_;
-}
-
 std::vector<double> Engine::fleet_merged() {
-  flush();
+  flush();  // every posted batch is packed
   std::vector<double> out;
-  if (!fleet_comm_ || fleet_rounds_ == 0) return out;
+  if (!fleet_comm_) return out;
+  fleet_exchange_upto(fleet_posted_);
+  if (fleet_rounds_ == 0) return out;
   const int slot = (int)((fleet_rounds_ - 1) & 1);
   HIP_OK(hipEventSynchronize(fleet_ev_[slot]));
   out.resize(fleet_elems_);

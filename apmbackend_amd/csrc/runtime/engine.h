@@ -229,10 +229,13 @@ class Engine {
   // Native RCCL fleet exchange (see engine.cpp): rank 0 creates the id, every rank inits.
   static std::vector<uint8_t> fleet_unique_id();
   // clock_uid non-empty: lock-step clocks (node-wide watermark + rollover bucket) so N ranks
-  // reproduce the single-stream reference per series.
+  // reproduce the single-stream reference per series.  (Only its presence matters: every
+  // collective of a rank runs on ONE communicator, see engine.cpp.)
   void fleet_init(const std::vector<uint8_t>& uid, const std::vector<uint8_t>& clock_uid, int nranks, int rank,
                   int32_t n_services_cap);
-  std::vector<double> fleet_merged();  // [cap][n_lags][NSTAT][3] of the newest exchange
+  // Collective: call on every rank at the same point of the batch sequence.  Exchanges the
+  // batches not yet exchanged and returns [cap][n_lags][NSTAT][3] of the newest.
+  std::vector<double> fleet_merged();
   uint64_t fleet_rounds() const { return fleet_rounds_; }
 
   // Wait for the in-flight stats stage (process_batch returns while it still runs).
@@ -278,10 +281,12 @@ class Engine {
   void emit_bytes(int kind, const char* p, size_t n);
   void upload_series_tables(int32_t lo);
   void pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream);
-  void fleet_exchange_locked();
-  void sync_latest_locked(double batch_t0);
+  void fleet_pack_locked();
+  void fleet_exchange_upto(uint64_t rounds);
+  void lockstep_sync(const std::vector<TxOut>& txs);
+  void apply_latest_locked(int64_t g, double batch_t0);
   void stats_worker();
-  void post_stats(std::vector<TxOut>&& txs, double t0);
+  void post_stats(std::vector<TxOut>&& txs, double t0, int64_t sync_latest = INT64_MIN);
   void drain_sinks(uint32_t kinds = ~0u);
   void drain_kind(int k);
   // output lane (see engine.cpp): waits for the D2H of released-tx ids / formatted text and
@@ -301,18 +306,27 @@ class Engine {
 
   EngineConfig cfg_;
   hipStream_t stream_ = nullptr, comm_stream_ = nullptr, parse_stream_ = nullptr;
-  // fleet exchange
+  // fleet exchange + lock-step clocks: ONE communicator, driven only by the ingest thread on
+  // coll_stream_, so every rank issues the same collectives in the same order (engine.cpp)
   ncclComm_t fleet_comm_ = nullptr;
-  ncclComm_t clock_comm_ = nullptr;
+  hipStream_t coll_stream_ = nullptr;
+  bool lockstep_ = false;
+  int64_t sync_latest_ = INT64_MIN;  // ingest thread: node-wide newest bucket so far
   double* d_sync_ = nullptr;
   double* h_sync_ = nullptr;
   int32_t fleet_cap_ = 0;
   size_t fleet_elems_ = 0;
   double* fleet_buf_[2] = {nullptr, nullptr};
-  hipEvent_t fleet_ev_[2] = {nullptr, nullptr};
-  uint64_t fleet_rounds_ = 0;
+  hipEvent_t fleet_ev_[2] = {nullptr, nullptr};    // all-reduce of the slot done (coll stream)
+  hipEvent_t pack_ev_[2] = {nullptr, nullptr};     // pack of the slot done (comm stream)
+  uint64_t fleet_rounds_ = 0;  // exchanges issued (ingest thread)
+  uint64_t fleet_posted_ = 0;  // batches posted since fleet_init (ingest thread)
+  uint64_t fleet_packed_ = 0;  // batches packed (stats thread)
   // stats thread
-  struct StatsJob { std::vector<TxOut> txs; std::vector<std::string> text; double t0 = 0; };
+  struct StatsJob {
+    std::vector<TxOut> txs; std::vector<std::string> text; double t0 = 0;
+    int64_t sync_latest = INT64_MIN;  // lock-step: node-wide newest bucket after this batch
+  };
   std::vector<std::string>* cur_text_ = nullptr;  // text arenas of the job being processed
   std::thread stats_thread_;
   std::mutex st_mu_;

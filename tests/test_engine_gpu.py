@@ -220,9 +220,9 @@ def test_checkpoint_resume_is_seamless(tmp_path, mode):
 
 
 def test_lockstep_clock_communicator_single_rank_is_transparent():
-    """fleet_init with the lock-step clock communicator (nranks=1): every batch runs the
-    watermark all-reduce (main thread) and the latest-bucket all-reduce (stats thread); with
-    one rank the output must be unchanged."""
+    """fleet_init with lock-step clocks (nranks=1): every batch runs the {watermark, newest
+    bucket} all-reduce and the moments all-reduce of the previous batch, all on the ingest
+    thread's communicator; with one rank the output must be unchanged."""
     lines, bl = synth_batches(9, duration=400)
     C = small_cfg("exact")
     _, plain = _run_engine(C, bl)
@@ -237,7 +237,8 @@ def test_lockstep_clock_communicator_single_rank_is_transparent():
     for k in ("transactions", "st", "fs", "al"):
         assert out[k] == plain[k], k
     m = eng.metrics()
-    assert m["lockstep_rollovers"] == 0 and eng.eng.fleet_rounds() == len(bl)
+    assert m["lockstep_rollovers"] == 0 and eng.eng.fleet_rounds() == len(bl) - 1
+    assert len(eng.eng.fleet_merged()) > 0 and eng.eng.fleet_rounds() == len(bl)
 
 
 def test_server_rollup_fuses_window_stats_with_jmx_gauges():

@@ -26,5 +26,17 @@ for s in $STEPS; do
     prof)
       timeout -k 10 "${T_PROF:-420}" rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py ${PROF_ARGS:---steps 5 --warmup 2} > gpurun_out/prof.log 2>&1
       rc=$?; echo "prof rc=$rc"; tail -3 gpurun_out/prof.log; stop_on_fault $rc prof ;;
+    pmc)
+      # hardware counters of the engine's own kernels, one rocprofv3 pass per counter group
+      # (per-block limits: <= 8 SQ, <= 4 TCC -- FETCH_SIZE takes 3, WRITE_SIZE 2)
+      i=0
+      for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE" \
+                 "FETCH_SIZE TCP_TOTAL_CACHE_ACCESSES_sum" "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum" \
+                 "SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM"; do
+        i=$((i+1))
+        timeout -s KILL "${T_PMC:-120}" rocprofv3 --pmc $grp --kernel-trace --output-format csv --kernel-include-regex 'apm::' \
+          -d gpurun_out/pmc$i -o run -- python3 bench.py ${PMC_ARGS:---steps 3 --warmup 1} > gpurun_out/pmc$i.log 2>&1
+        rc=$?; echo "pmc pass $i rc=$rc"; tail -2 gpurun_out/pmc$i.log; stop_on_fault $rc pmc$i
+      done ;;
   esac
 done
