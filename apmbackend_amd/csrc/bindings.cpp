@@ -99,6 +99,7 @@ EngineConfig config_from(const py::dict& d) {
   c.tz = tz_from(d);
   c.join_threads = get<int>(d, "join_threads", c.join_threads);
   c.pin_threads = get<bool>(d, "pin_threads", c.pin_threads);
+  c.coll_timeout_ms = get<double>(d, "coll_timeout_ms", c.coll_timeout_ms);
   c.outputs = get<uint32_t>(d, "outputs", c.outputs);
   c.async_stats = get<int>(d, "async_stats", c.async_stats);
   return c;

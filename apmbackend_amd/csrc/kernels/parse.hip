@@ -195,6 +195,9 @@ __device__ __forceinline__ uint32_t find_chunk(const uint32_t* cb, uint32_t n_ch
   return lo;
 }
 
+__device__ __forceinline__ void parse_line(const ParseArgs& a, const uint8_t* __restrict__ base, uint32_t o,
+                                           uint32_t li, uint32_t ls, uint32_t le);
+
 // --------------------------------------------------------------------------------- K2
 __global__ __launch_bounds__(PARSE_BLOCK) void k_parse_lines(ParseArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[PARSE_LDS];
@@ -229,8 +232,18 @@ __global__ __launch_bounds__(PARSE_BLOCK) void k_parse_lines(ParseArgs a) {
     return;
   }
   const uint32_t ls = li == 0 ? 0 : a.line_end[li - 1] + 1;
-  uint32_t le = a.line_end[li];
-  const uint8_t* p = staged ? (lds + (ls - a0)) : (a.bytes + ls);
+  const uint32_t le = a.line_end[li];
+  // Two inlined copies of the line parser, one per address space.  A single copy behind
+  // `staged ? lds : global` sees a generic pointer and issues a flat load for every byte
+  // (rocprofv3 before the split: 9M VMEM reads per run, ~150 LDS conflict cycles per LDS op).
+  if (staged) parse_line(a, lds, ls - a0, li, ls, le);
+  else parse_line(a, a.bytes, ls, li, ls, le);
+}
+
+// One line: `base + o` is its first byte; `base` is 16-byte aligned (LDS stage or the batch).
+__device__ __forceinline__ void parse_line(const ParseArgs& a, const uint8_t* __restrict__ base, uint32_t o,
+                                           uint32_t li, uint32_t ls, uint32_t le) {
+  const uint8_t* __restrict__ p = base + o;
   int len = (int)(le - ls);
   if (len > 0 && p[len - 1] == '\r') --len;
 
@@ -268,8 +281,19 @@ __global__ __launch_bounds__(PARSE_BLOCK) void k_parse_lines(ParseArgs a) {
   bool ejb_entry = false, ejb_exit = false, ct_start = false, ct_stop = false;
   bool baf = false, nonascii = false;
   uint32_t m = 0;
+  // bytes arrive one aligned dword at a time (one ds_read_b32 / global_load_dword per 4 bytes);
+  // the pattern probes below re-read p[] only at their trigger characters
+  const uint32_t* __restrict__ wp = reinterpret_cast<const uint32_t*>(base) + (o >> 2);
+  int q = (int)(o & 3u);
+  uint32_t cw = wp[0] >> (8 * q);
   for (int i = 0; i < len; ++i) {
-    const uint8_t c = p[i];
+    const uint8_t c = (uint8_t)cw;
+    cw >>= 8;
+    if (++q == 4) {
+      q = 0;
+      ++wp;
+      if (i + 1 < len) cw = *wp;
+    }
     nonascii |= c >= 0x80;
     const bool w = is_ws(c);
     if (!w && !in_tok) { if (ntok < 16) ts_[ntok] = (uint16_t)i; in_tok = true; }

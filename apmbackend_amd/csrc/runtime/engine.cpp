@@ -200,6 +200,15 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     HIP_OK(hipHostMalloc((void**)&ps.h_chunk_kind, cfg_.max_chunks + 2, hipHostMallocDefault));
     HIP_OK(hipHostMalloc((void**)&ps.h_chunk_file, (cfg_.max_chunks + 2) * 4, hipHostMallocDefault));
     HIP_OK(hipHostMalloc((void**)&ps.h_events, (size_t)cfg_.max_lines * sizeof(Event), hipHostMallocDefault));
+    // APM_EVENTS_ZEROCOPY=1: the compaction kernel writes the events straight into this pinned
+    // slot (the copy rides along with the prefetched parse) instead of a 15 MB D2H the ingest
+    // thread waits for.  Measured A/B on MI355X (tools/ab_env.sh, 4 alternating rounds): -0.3 ms
+    // parse but +0.3 ms host join (the join then reads lines the GPU wrote over PCIe), i.e. no
+    // net change, so the DMA copy stays the default.
+    const char* zc = std::getenv("APM_EVENTS_ZEROCOPY");
+    void* dp = nullptr;
+    if (zc && std::atoi(zc) != 0 && hipHostGetDevicePointer(&dp, ps.h_events, 0) == hipSuccess)
+      ps.d_events_host = (Event*)dp;
     HIP_OK(hipHostMalloc((void**)&ps.h_counts, 16, hipHostMallocDefault));
     HIP_OK(hipHostMalloc((void**)&ps.h_watermark, 8, hipHostMallocDefault));
   }
@@ -338,7 +347,7 @@ Engine::~Engine() {
   if (fleet_comm_) {
     hipStreamSynchronize(comm_stream_);
     hipStreamSynchronize(coll_stream_);
-    ncclCommDestroy(fleet_comm_);
+    if (!comm_aborted_) ncclCommDestroy(fleet_comm_);  // an aborted communicator is already freed
     fleet_comm_ = nullptr;
     for (int i = 0; i < 2; ++i) { hipEventDestroy(fleet_ev_[i]); hipEventDestroy(pack_ev_[i]); }
     hipStreamDestroy(coll_stream_);
@@ -428,12 +437,22 @@ void Engine::compute_series_settings(int32_t s, double* thr, double* infl, doubl
 }
 
 int32_t Engine::series_for(int32_t server, int32_t service) {
+  // hot path (every tx of every batch): a dense per-server row indexed by the service id
+  // (servers x services ints, a few hundred KB that stay in cache) in front of the hash map
+  if ((size_t)server < ser_tab_.size() && (size_t)service < ser_tab_[server].size()) {
+    const int32_t hit = ser_tab_[server][service];
+    if (hit >= 0) return hit;
+  }
   const uint64_t key = ((uint64_t)(uint32_t)(server + 1) << 32) | (uint32_t)service;  // never 0 (FlatMap)
   int32_t* slot = series_map_.find(key);
-  if (slot) return *slot - 1;
+  if (slot) {
+    ser_tab_put(server, service, *slot - 1);
+    return *slot - 1;
+  }
   if (n_series_ >= cfg_.max_series) return -1;
   const int32_t s = n_series_++;
   series_map_[key] = s + 1;
+  ser_tab_put(server, service, s);
   if (server_rank_[server] < 0) server_rank_[server] = next_server_rank_++;
   const uint64_t ek = ((uint64_t)server_rank_[server] << 24) | (uint64_t)(server_next_service_[server]++);
   series_.push_back(SeriesInfo{server, service, ek});
@@ -587,7 +606,7 @@ void Engine::launch_parse(ParseSlot& ps, const uint8_t* host_bytes, uint64_t n_b
   HIP_OK(hipMemcpyAsync(d_chunk_kind_, ps.h_chunk_kind, n_chunks + 1, hipMemcpyHostToDevice, parse_stream_));
   HIP_OK(hipMemcpyAsync(d_chunk_file_, ps.h_chunk_file, (n_chunks + 1) * 4, hipMemcpyHostToDevice, parse_stream_));
   if (apm_parse_batch(d_bytes_, off, d_chunk_begin_, d_chunk_kind_, d_chunk_file_, n_chunks, d_parse_ws_,
-                      cfg_.max_lines, d_events_, d_counts_, d_counts_ + 1, d_watermark_, d_file_open_, &cfg_.tz,
+                      cfg_.max_lines, ps.d_events_host ? ps.d_events_host : d_events_, d_counts_, d_counts_ + 1, d_watermark_, d_file_open_, &cfg_.tz,
                       parse_stream_) != 0)
     throw std::runtime_error("parse workspace too small");
   HIP_OK(hipMemcpyAsync(ps.h_counts, d_counts_, 8, hipMemcpyDeviceToHost, parse_stream_));
@@ -605,7 +624,7 @@ void Engine::finish_parse(ParseSlot& ps) {
   if (ps.n_lines > cfg_.max_lines) throw std::runtime_error("batch has more lines than max_lines");
   metrics_.lines += ps.n_lines;
   metrics_.events += ps.n_events;
-  if (ps.n_events) {
+  if (ps.n_events && !ps.d_events_host) {
     HIP_OK(hipMemcpyAsync(ps.h_events, d_events_, (size_t)ps.n_events * sizeof(Event), hipMemcpyDeviceToHost,
                           parse_stream_));
     HIP_OK(hipStreamSynchronize(parse_stream_));
@@ -1643,11 +1662,45 @@ void Engine::fleet_init(const std::vector<uint8_t>& uid, const std::vector<uint8
   fleet_rounds_ = fleet_posted_ = fleet_packed_ = 0;
 }
 
+// Watchdog for the ingest thread's collectives.  A launch error or an asynchronous RCCL error
+// (peer gone, network fault) or a collective still pending after gpu.collectiveTimeoutSeconds
+// aborts the communicator (ncclCommAbort unblocks the wedged kernel) and throws: the service
+// exits non-zero and the supervisor restarts the whole rank group from its checkpoints, which is
+// how the node degrades / recovers instead of hanging every rank forever.
+void Engine::coll_check(ncclResult_t r, const char* what) {
+  if (r == ncclSuccess || r == ncclInProgress) return;
+  ncclCommAbort(fleet_comm_);
+  comm_aborted_ = true;
+  throw std::runtime_error(std::string("RCCL ") + what + " failed: " + ncclGetErrorString(r));
+}
+
+void Engine::coll_wait(hipStream_t s, hipEvent_t ev, const char* what) {
+  const double t0 = now_ms();
+  for (int spin = 0;; ++spin) {
+    const hipError_t e = ev ? hipEventQuery(ev) : hipStreamQuery(s);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) HIP_OK(e);
+    ncclResult_t ar = ncclSuccess;
+    if (ncclCommGetAsyncError(fleet_comm_, &ar) != ncclSuccess) ar = ncclSuccess;
+    if (ar != ncclSuccess && ar != ncclInProgress) coll_check(ar, what);
+    if (now_ms() - t0 > cfg_.coll_timeout_ms) {
+      ncclCommAbort(fleet_comm_);
+      comm_aborted_ = true;
+      throw std::runtime_error(std::string("RCCL ") + what + ": no completion after " +
+                               std::to_string((long long)cfg_.coll_timeout_ms) + " ms (peer rank dead or wedged)");
+    }
+    // the clock exchange is on the batch's critical path: spin briefly, then back off
+    if (spin < 4096) std::this_thread::yield();
+    else std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
+}
+
 // Ingest thread, after the join of a batch: the node-wide watermark becomes the cache clock of
 // the next batch, and the node-wide newest bucket decides this batch's rollovers.  The bucket is
 // the one stats_for_batch derives (non-db tx with a usable endTs), so ranks agree on `latest`
 // without the stats thread touching the communicator.
 void Engine::lockstep_sync(const std::vector<TxOut>& txs) {
+  if (comm_aborted_) throw std::runtime_error("RCCL communicator was aborted");
   int64_t b = sync_latest_;
   for (const TxOut& t : txs) {
     if (t.to_db || !(t.end_ms == t.end_ms) || t.end_ms < 10000) continue;
@@ -1657,10 +1710,9 @@ void Engine::lockstep_sync(const std::vector<TxOut>& txs) {
   h_sync_[0] = watermark_;
   h_sync_[1] = b == INT64_MIN ? -1.0 : (double)b;  // buckets < 2^53: exact in a double
   HIP_OK(hipMemcpyAsync(d_sync_, h_sync_, 16, hipMemcpyHostToDevice, coll_stream_));
-  if (ncclAllReduce(d_sync_, d_sync_, 2, ncclDouble, ncclMax, fleet_comm_, coll_stream_) != ncclSuccess)
-    throw std::runtime_error("ncclAllReduce(lock-step clocks) failed");
+  coll_check(ncclAllReduce(d_sync_, d_sync_, 2, ncclDouble, ncclMax, fleet_comm_, coll_stream_), "lock-step clocks");
   HIP_OK(hipMemcpyAsync(h_sync_, d_sync_, 16, hipMemcpyDeviceToHost, coll_stream_));
-  HIP_OK(hipStreamSynchronize(coll_stream_));
+  coll_wait(coll_stream_, nullptr, "lock-step clocks");
   watermark_ = h_sync_[0];
   if (h_sync_[1] >= 0) sync_latest_ = std::max(sync_latest_, (int64_t)h_sync_[1]);
 }
@@ -1686,12 +1738,12 @@ void Engine::fleet_pack_locked() {
 
 // Ingest thread: all-reduce the packed batches [fleet_rounds_, rounds).
 void Engine::fleet_exchange_upto(uint64_t rounds) {
+  if (comm_aborted_ && fleet_rounds_ < rounds) throw std::runtime_error("RCCL communicator was aborted");
   while (fleet_rounds_ < rounds) {
     const int slot = (int)(fleet_rounds_ & 1);
     HIP_OK(hipStreamWaitEvent(coll_stream_, pack_ev_[slot], 0));
-    if (ncclAllReduce(fleet_buf_[slot], fleet_buf_[slot], fleet_elems_, ncclDouble, ncclSum, fleet_comm_,
-                      coll_stream_) != ncclSuccess)
-      throw std::runtime_error("ncclAllReduce(fleet moments) failed");
+    coll_check(ncclAllReduce(fleet_buf_[slot], fleet_buf_[slot], fleet_elems_, ncclDouble, ncclSum, fleet_comm_,
+                             coll_stream_), "fleet moments");
     HIP_OK(hipEventRecord(fleet_ev_[slot], coll_stream_));
     ++fleet_rounds_;
   }
@@ -1704,7 +1756,7 @@ std::vector<double> Engine::fleet_merged() {
   fleet_exchange_upto(fleet_posted_);
   if (fleet_rounds_ == 0) return out;
   const int slot = (int)((fleet_rounds_ - 1) & 1);
-  HIP_OK(hipEventSynchronize(fleet_ev_[slot]));
+  coll_wait(nullptr, fleet_ev_[slot], "fleet moments");
   out.resize(fleet_elems_);
   HIP_OK(hipMemcpy(out.data(), fleet_buf_[slot], fleet_elems_ * 8, hipMemcpyDeviceToHost));
   return out;

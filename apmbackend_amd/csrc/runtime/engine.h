@@ -84,6 +84,9 @@ struct EngineConfig {
   // outputs: bit k of `outputs` materialises stream k (OutKind) in the reference wire format
   uint32_t outputs = 0;
   int async_stats = 1;      // overlap batch i's stats with batch i+1's parse + join
+  // RCCL watchdog: a collective not complete after this long (a dead or wedged peer) aborts the
+  // communicator and throws, so the supervisor restarts the rank group from its checkpoint
+  double coll_timeout_ms = 300000;
 };
 
 // Output streams (queue names of the reference, config/apm_config.json:12,87,99-100,113-114,178):
@@ -283,6 +286,8 @@ class Engine {
   void pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream);
   void fleet_pack_locked();
   void fleet_exchange_upto(uint64_t rounds);
+  void coll_check(ncclResult_t r, const char* what);
+  void coll_wait(hipStream_t s, hipEvent_t ev, const char* what);
   void lockstep_sync(const std::vector<TxOut>& txs);
   void apply_latest_locked(int64_t g, double batch_t0);
   void stats_worker();
@@ -309,6 +314,7 @@ class Engine {
   // fleet exchange + lock-step clocks: ONE communicator, driven only by the ingest thread on
   // coll_stream_, so every rank issues the same collectives in the same order (engine.cpp)
   ncclComm_t fleet_comm_ = nullptr;
+  bool comm_aborted_ = false;
   hipStream_t coll_stream_ = nullptr;
   bool lockstep_ = false;
   int64_t sync_latest_ = INT64_MIN;  // ingest thread: node-wide newest bucket so far
@@ -358,6 +364,14 @@ class Engine {
 
   // series
   FlatMap<int32_t> series_map_{1 << 16};  // ((server + 1) << 32 | service) -> series + 1
+  std::vector<std::vector<int32_t>> ser_tab_;  // cache of series_map_: [server][service] -> series / -1
+  void ser_tab_put(int32_t server, int32_t service, int32_t s) {
+    if (server < 0 || service < 0 || service >= (1 << 20)) return;
+    if ((size_t)server >= ser_tab_.size()) ser_tab_.resize((size_t)server + 1);
+    auto& row = ser_tab_[server];
+    if ((size_t)service >= row.size()) row.resize(std::max<size_t>((size_t)service + 1, row.size() * 2), -1);
+    row[service] = s;
+  }
   std::vector<SeriesInfo> series_;
   int32_t n_series_ = 0;
   std::vector<int32_t> server_rank_;            // first-appearance rank per server in the stats stream
@@ -381,6 +395,7 @@ class Engine {
     uint8_t* h_chunk_kind = nullptr;
     uint32_t* h_chunk_file = nullptr;
     Event* h_events = nullptr;
+    Event* d_events_host = nullptr;             // device alias of h_events (zero-copy compaction)
     uint32_t* h_counts = nullptr;               // [0]=n_events [1]=n_lines
     unsigned long long* h_watermark = nullptr;
     const uint8_t* hb = nullptr;                // bytes the join reads (caller's or staging)

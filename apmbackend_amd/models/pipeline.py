@@ -84,6 +84,7 @@ def engine_config(cfg: Dict[str, Any], device: int = 0, keep_text: bool = False,
         "tz_table": tz_table(tz),
         "join_threads": int(g.get("joinThreads", 0)),
         "pin_threads": bool(g.get("pinThreads", False)),
+        "coll_timeout_ms": float(g.get("collectiveTimeoutSeconds", 300)) * 1000.0,
         "outputs": output_mask(OUT_KINDS if keep_text else (outputs or ())),
     }
     if int(sc["intervalLengthInSeconds"]) != 10:

@@ -386,7 +386,11 @@ class IngestService:
         if self.qm is not None and any(getattr(p, "paused", False) for p in self.producers.values()):
             return 0  # downstream backpressure: hold the tails (pause-file semantics)
         buf, chunks = self.tailer.poll()
-        if not chunks:
+        # Lock-step ranks (native engine, world > 1): every process_batch runs the node-wide
+        # clock all-reduce, so every rank must call it once per poll -- with an empty batch when
+        # its tails have nothing new -- or the ranks' collective sequences diverge.
+        lockstep = self.fleet is not None
+        if not chunks and not lockstep:
             return 0
         self.polls += 1
         fi = self.fault
@@ -394,17 +398,22 @@ class IngestService:
             if fi.get("exitAtBatch") and self.polls == int(fi["exitAtBatch"]):
                 log.error("fault injection: exiting at batch %d", self.polls)
                 os._exit(int(fi.get("exitCode", 13)))
-            if fi.get("dropBatchEvery") and self.polls % int(fi["dropBatchEvery"]) == 0:
+            if chunks and fi.get("dropBatchEvery") and self.polls % int(fi["dropBatchEvery"]) == 0:
                 log.warning("fault injection: dropping batch %d (%d bytes)", self.polls, len(buf))
                 self.faults["dropped"] += 1
-                return len(buf)
+                if not lockstep:
+                    return len(buf)
+                buf, chunks = b"", []  # the rank still takes part in this poll's collectives
         self.native.process_batch(buf, chunks, -1.0)
         self.batches += 1
         if fi and fi.get("rank", self.rank) == self.rank and fi.get("duplicateBatchEvery") \
-                and self.polls % int(fi["duplicateBatchEvery"]) == 0:
-            log.warning("fault injection: replaying batch %d", self.polls)
-            self.faults["duplicated"] += 1
-            self.native.process_batch(buf, chunks, -1.0)
+                and chunks and self.polls % int(fi["duplicateBatchEvery"]) == 0:
+            if lockstep:  # a second process_batch on one rank only would desynchronise the ranks
+                log.warning("fault injection: duplicateBatchEvery is ignored for lock-step ranks")
+            else:
+                log.warning("fault injection: replaying batch %d", self.polls)
+                self.faults["duplicated"] += 1
+                self.native.process_batch(buf, chunks, -1.0)
         self._drain_outputs()
         return len(buf)
 

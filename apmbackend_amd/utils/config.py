@@ -56,6 +56,7 @@ GPU_DEFAULTS: Dict[str, Any] = {
     "timezone": "local",              # tz for 'YYYY-MM-DD HH:MM:SS,mmm' timestamps
     "fleetBaseline": True,            # RCCL all-reduce of per-service moments + lock-step clocks
     "joinThreads": 0,                 # host join worker threads (0 = auto)
+    "collectiveTimeoutSeconds": 300,  # RCCL watchdog: abort + exit when a collective hangs this long
     "checkpointDir": "",              # binary engine checkpoints (+ tail offsets) per rank
     "checkpointEverySeconds": 60,
     "importReferenceResume": False,   # seed a fresh engine from the reference's JSON resume files
