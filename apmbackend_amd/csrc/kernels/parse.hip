@@ -88,7 +88,8 @@ __global__ __launch_bounds__(NL_BLOCK) void k_nl_write(const uint8_t* __restrict
 
 // --------------------------------------------------------------------------------- K2 helpers
 __device__ __forceinline__ bool is_ws(uint8_t c) {
-  return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f';
+  // ' ' and \t \n \v \f \r (9..13) as one shift-and-mask
+  return c <= 32 && ((0x100003E00ULL >> c) & 1ULL);
 }
 __device__ __forceinline__ bool is_digit(uint8_t c) { return c >= '0' && c <= '9'; }
 __device__ __forceinline__ uint8_t lower(uint8_t c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
@@ -100,6 +101,29 @@ __device__ __forceinline__ bool match_at(const uint8_t* p, int i, int len, const
   for (int k = 0; k < N - 1; ++k)
     if (p[i + k] != (uint8_t)lit[k]) return false;
   return true;
+}
+
+// token indices the classifier reads -> register slot (tokens 0-3 for the Event, 1/2 for the
+// timestamp, 9/11/13 for the EJB service / elapsed fields)
+constexpr int NTOKSLOT = 7;
+__device__ __forceinline__ constexpr int tok_slot(int k) {
+  return k <= 3 ? k : (k == 9 ? 4 : (k == 11 ? 5 : (k == 13 ? 6 : 0)));
+}
+__device__ __forceinline__ void tok_put(uint16_t (&arr)[NTOKSLOT], int k, uint16_t v) {
+  constexpr int idx[NTOKSLOT] = {0, 1, 2, 3, 9, 11, 13};
+#pragma unroll
+  for (int j = 0; j < NTOKSLOT; ++j) arr[j] = k == idx[j] ? v : arr[j];
+}
+__device__ __forceinline__ void tok_put_if(uint16_t (&arr)[NTOKSLOT], bool on, int k, uint16_t v) {
+  tok_put(arr, on ? k : -1, v);
+}
+
+// four characters packed little-endian, as they sit in a byte window p[i-3..i]
+template <int N>
+__device__ __forceinline__ constexpr uint32_t pk4(const char (&lit)[N]) {
+  static_assert(N == 5, "pk4 takes exactly four characters");
+  return (uint32_t)(uint8_t)lit[0] | ((uint32_t)(uint8_t)lit[1] << 8) | ((uint32_t)(uint8_t)lit[2] << 16) |
+         ((uint32_t)(uint8_t)lit[3] << 24);
 }
 
 template <int N>
@@ -195,8 +219,8 @@ __device__ __forceinline__ uint32_t find_chunk(const uint32_t* cb, uint32_t n_ch
   return lo;
 }
 
-__device__ __forceinline__ void parse_line(const ParseArgs& a, const uint8_t* __restrict__ base, uint32_t o,
-                                           uint32_t li, uint32_t ls, uint32_t le);
+__device__ __forceinline__ unsigned long long parse_line(const ParseArgs& a, const uint8_t* __restrict__ base,
+                                                         uint32_t o, uint32_t li, uint32_t ls, uint32_t le);
 
 // --------------------------------------------------------------------------------- K2
 __global__ __launch_bounds__(PARSE_BLOCK) void k_parse_lines(ParseArgs a) {
@@ -227,22 +251,29 @@ __global__ __launch_bounds__(PARSE_BLOCK) void k_parse_lines(ParseArgs a) {
   }
   __syncthreads();
   const uint32_t li = first + threadIdx.x;
+  unsigned long long wm = 0;
   if (li >= last) {
     if (li < a.cap_lines) a.keep[li] = 0;
-    return;
+  } else {
+    const uint32_t ls = li == 0 ? 0 : a.line_end[li - 1] + 1;
+    const uint32_t le = a.line_end[li];
+    // Two inlined copies of the line parser, one per address space.  A single copy behind
+    // `staged ? lds : global` sees a generic pointer and issues a flat load for every byte
+    // (rocprofv3 before the split: 9M VMEM reads per run, ~150 LDS conflict cycles per LDS op).
+    wm = staged ? parse_line(a, lds, ls - a0, li, ls, le) : parse_line(a, a.bytes, ls, li, ls, le);
   }
-  const uint32_t ls = li == 0 ? 0 : a.line_end[li - 1] + 1;
-  const uint32_t le = a.line_end[li];
-  // Two inlined copies of the line parser, one per address space.  A single copy behind
-  // `staged ? lds : global` sees a generic pointer and issues a flat load for every byte
-  // (rocprofv3 before the split: 9M VMEM reads per run, ~150 LDS conflict cycles per LDS op).
-  if (staged) parse_line(a, lds, ls - a0, li, ls, le);
-  else parse_line(a, a.bytes, ls, li, ls, le);
+  // Watermark: one atomic per wave.  A per-lane atomicMax on the single watermark word put 64
+  // same-address atomics per wave through one L2 atomic unit, serialising the whole grid.
+  for (int off = APM_WAVE / 2; off > 0; off >>= 1) {
+    const unsigned long long o2 = __shfl_xor(wm, off, APM_WAVE);
+    wm = o2 > wm ? o2 : wm;
+  }
+  if ((threadIdx.x & (APM_WAVE - 1)) == 0 && wm) atomicMax(a.watermark, wm);
 }
 
 // One line: `base + o` is its first byte; `base` is 16-byte aligned (LDS stage or the batch).
-__device__ __forceinline__ void parse_line(const ParseArgs& a, const uint8_t* __restrict__ base, uint32_t o,
-                                           uint32_t li, uint32_t ls, uint32_t le) {
+__device__ __forceinline__ unsigned long long parse_line(const ParseArgs& a, const uint8_t* __restrict__ base,
+                                                         uint32_t o, uint32_t li, uint32_t ls, uint32_t le) {
   const uint8_t* __restrict__ p = base + o;
   int len = (int)(le - ls);
   if (len > 0 && p[len - 1] == '\r') --len;
@@ -269,11 +300,13 @@ __device__ __forceinline__ void parse_line(const ParseArgs& a, const uint8_t* __
     if (len > 65000) { ev.kind = fk == FILE_SOAP ? LK_SOAP : LK_APP; ev.mask = PM_HOST; }
     a.line_mask[li] = ev.mask;
     a.ev_tmp[li] = ev;
-    return;
+    return 0;
   }
 
   // ---- single pass: whitespace tokens 0..13, pattern tests, INFO occurrences
-  uint16_t ts_[16], te_[16];
+  // Start/end of the tokens the classifier reads (0-3, 9, 11, 13), kept in registers: an array
+  // indexed by the lane-varying token count forced a per-write waterfall / scratch access
+  uint16_t ts_[NTOKSLOT], te_[NTOKSLOT];
   int ntok = 0;
   bool in_tok = false;
   if (len > 0 && is_ws(p[0])) { ts_[0] = 0; te_[0] = 0; ntok = 1; }  // split gives '' first
@@ -281,59 +314,68 @@ __device__ __forceinline__ void parse_line(const ParseArgs& a, const uint8_t* __
   bool ejb_entry = false, ejb_exit = false, ct_start = false, ct_stop = false;
   bool baf = false, nonascii = false;
   uint32_t m = 0;
-  // bytes arrive one aligned dword at a time (one ds_read_b32 / global_load_dword per 4 bytes);
-  // the pattern probes below re-read p[] only at their trigger characters
-  const uint32_t* __restrict__ wp = reinterpret_cast<const uint32_t*>(base) + (o >> 2);
-  int q = (int)(o & 3u);
-  uint32_t cw = wp[0] >> (8 * q);
+  // The per-byte path is branch-free (rocprofv3: the branchy first version issued ~2 SALU
+  // exec-mask instructions per VALU one): token bounds by select, and pattern triggers tested on
+  // a 4-byte register window p[i-3..i] -- one uniform branch per byte, taken only when some
+  // lane's window equals a pattern's first four bytes; only then is the line re-read.
+  uint32_t win = 0, winl = 0;
   for (int i = 0; i < len; ++i) {
-    const uint8_t c = (uint8_t)cw;
-    cw >>= 8;
-    if (++q == 4) {
-      q = 0;
-      ++wp;
-      if (i + 1 < len) cw = *wp;
-    }
+    const uint8_t c = p[i];
     nonascii |= c >= 0x80;
     const bool w = is_ws(c);
-    if (!w && !in_tok) { if (ntok < 16) ts_[ntok] = (uint16_t)i; in_tok = true; }
-    if (w && in_tok) { if (ntok < 16) te_[ntok] = (uint16_t)i; ++ntok; in_tok = false; }
-    if (c == 'I' && match_at(p, i, len, "INFO")) {
-      if (info1 < 0) info1 = i;
-      else if (info2 < 0 && i >= info1 + 4) info2 = i;
-      int j = i + 4;
+    tok_put_if(ts_, !w && !in_tok, ntok, (uint16_t)i);
+    const bool tend = w && in_tok;
+    tok_put_if(te_, tend, ntok, (uint16_t)i);
+    ntok += tend ? 1 : 0;
+    in_tok = !w;
+    win = (win >> 8) | ((uint32_t)c << 24);
+    winl = (winl >> 8) | ((uint32_t)lower(c) << 24);
+    const bool probe = (win == pk4("INFO")) | (win == pk4(": Re")) | ((win & 0xffu) == '<');
+    if (!probe || i < 3) continue;
+    const int s = i - 3;
+    if (win == pk4("INFO")) {
+      if (info1 < 0) info1 = s;
+      else if (info2 < 0 && s >= info1 + 4) info2 = s;
+      int j = s + 4;
       while (j < len && p[j] == ' ') ++j;
       if (match_at(p, j, len, "[CommonTiming] The EJB")) ejb_entry = true;
       if (match_at(p, j, len, "[CommonTiming] Total time")) ejb_exit = true;
       if (match_at(p, j, len, "CommonTiming::Start")) ct_start = true;
       if (match_at(p, j, len, "CommonTiming::Stop")) ct_stop = true;
-      if (match_at(p, i, len, "INFO  auditTrailId=")) m |= PM_AUTR_MAP;
-    } else if (c == ']') {
-      // BAF: \[[^ ]+] +INFO   -> ']' then 1+ spaces then "INFO "
-      if (!baf && i + 1 < len && p[i + 1] == ' ') {
-        int j = i + 1;
-        while (j < len && p[j] == ' ') ++j;
-        if (match_at(p, j, len, "INFO ")) {
-          for (int k = i - 2; k >= 0 && p[k] != ' '; --k) {  // '[' with >=1 non-space before ']'
-            if (p[k] == '[' ) { bool ok = true; for (int q = k + 1; q < i; ++q) ok &= p[q] != ' '; if (ok) { baf = true; break; } }
-          }
-        }
+      if (match_at(p, s, len, "INFO  auditTrailId=")) m |= PM_AUTR_MAP;
+      // BAF  \[[^ ]+] +INFO  : the ']' is the last non-space before the spaces preceding an
+      // "INFO ", with a '[' at least two columns before it and no space in between
+      if (!baf && s + 4 < len && p[s + 4] == ' ' && s >= 1 && p[s - 1] == ' ') {
+        int k = s - 1;
+        while (k >= 0 && p[k] == ' ') --k;
+        if (k >= 0 && p[k] == ']')
+          for (int kk = k - 2; kk >= 0 && p[kk] != ' '; --kk)
+            if (p[kk] == '[') { baf = true; break; }
       }
-    } else if (c == '<') {
-      if (match_at(p, i, len, "<stopWatchList>")) m |= PM_SW_START;
-      if (match_at(p, i, len, "</stopWatchList>")) m |= PM_SW_END;
-      if (match_at(p, i, len, "<name>")) m |= PM_SW_NAME;
-      if (match_at(p, i, len, "<startTime>")) m |= PM_SW_STARTTS;
-      if (match_at(p, i, len, "<stopTime>")) m |= PM_SW_STOPTS;
-      if (match_at(p, i, len, "<value>")) m |= PM_SOAP_VALUE;
-      if (match_at_ci(p, i, len, "<accountnumber>")) m |= PM_SOAP_ACCT;
-      if (match_at_ci(p, i, len, "<key>accountnumber</key>")) m |= PM_SOAP_KEY;
-    } else if (c == ':') {
-      if (match_at(p, i, len, ": RequestTrace [stopWatchList=")) m |= PM_EL_START;
+    } else if (win == pk4(": Re")) {
+      if (match_at(p, s, len, ": RequestTrace [stopWatchList=")) m |= PM_EL_START;
+    } else if ((win & 0xffu) == '<') {
+      if (win == pk4("<sto")) {
+        if (match_at(p, s, len, "<stopWatchList>")) m |= PM_SW_START;
+        if (match_at(p, s, len, "<stopTime>")) m |= PM_SW_STOPTS;
+      } else if (win == pk4("</st")) {
+        if (match_at(p, s, len, "</stopWatchList>")) m |= PM_SW_END;
+      } else if (win == pk4("<nam")) {
+        if (match_at(p, s, len, "<name>")) m |= PM_SW_NAME;
+      } else if (win == pk4("<sta")) {
+        if (match_at(p, s, len, "<startTime>")) m |= PM_SW_STARTTS;
+      } else if (win == pk4("<val")) {
+        if (match_at(p, s, len, "<value>")) m |= PM_SOAP_VALUE;
+      }
+      if (winl == pk4("<acc")) {
+        if (match_at_ci(p, s, len, "<accountnumber>")) m |= PM_SOAP_ACCT;
+      } else if (winl == pk4("<key")) {
+        if (match_at_ci(p, s, len, "<key>accountnumber</key>")) m |= PM_SOAP_KEY;
+      }
     }
   }
-  if (in_tok) { if (ntok < 16) te_[ntok] = (uint16_t)len; ++ntok; }
-  else if (is_ws(p[len - 1]) && ntok < 16) { ts_[ntok] = te_[ntok] = (uint16_t)len; ++ntok; }  // trailing ''
+  if (in_tok) { tok_put(te_, ntok, (uint16_t)len); ++ntok; }
+  else if (is_ws(p[len - 1]) && ntok < 16) { tok_put(ts_, ntok, (uint16_t)len); tok_put(te_, ntok, (uint16_t)len); ++ntok; }  // trailing ''
   // line-anchored patterns
   if (p[0] == ']') m |= PM_EL_END;
   if (match_at(p, 0, len, "Audit Trail id")) {
@@ -354,7 +396,7 @@ __device__ __forceinline__ void parse_line(const ParseArgs& a, const uint8_t* __
 
   ev.ntok = (uint8_t)min(ntok, 15);
   auto tok = [&](int k, uint16_t& s, uint16_t& e) {
-    if (k < ntok && k < 16) { s = ts_[k]; e = te_[k]; }
+    if (k < ntok && k < 16) { s = ts_[tok_slot(k)]; e = te_[tok_slot(k)]; }
   };
   tok(0, ev.t0s, ev.t0e);
   tok(1, ev.t1s, ev.t1e);
@@ -363,14 +405,14 @@ __device__ __forceinline__ void parse_line(const ParseArgs& a, const uint8_t* __
 
   // ---- leading-timestamp watermark + ts field
   bool ts_host = false;  // only matters for the timestamped CommonTiming kinds
+  unsigned long long wm = 0;  // leading-timestamp watermark candidate (biased), 0 = none
   if (ntok >= 3) {
     double t;
     bool strict;
-    if (parse_log_ts(p, ts_[1], te_[1], ts_[2], te_[2], a.tz, t, strict)) {
+    if (parse_log_ts(p, ts_[tok_slot(1)], te_[tok_slot(1)], ts_[tok_slot(2)], te_[tok_slot(2)], a.tz, t, strict)) {
       ev.ts = t;
       if (strict && t == t) {
-        const unsigned long long biased = (unsigned long long)((long long)t + (1LL << 62));
-        atomicMax(a.watermark, biased);
+        wm = (unsigned long long)((long long)t + (1LL << 62));
       }
     } else {
       ts_host = true;
@@ -399,7 +441,7 @@ __device__ __forceinline__ void parse_line(const ParseArgs& a, const uint8_t* __
     } else if (kind == LK_EJB_EXIT) {
       tok(9, ev.tAs, ev.tAe);
       tok(11, ev.tBs, ev.tBe);
-      if (11 < ntok && !parse_int_tok(p, ts_[11], te_[11], ev.num)) m |= PM_HOST;
+      if (11 < ntok && !parse_int_tok(p, ts_[tok_slot(11)], te_[tok_slot(11)], ev.num)) m |= PM_HOST;
     } else if (kind == LK_CT_ENTRY || kind == LK_CT_EXIT) {
       // line.split(/INFO/)[1].trim().split(/[\s]+/)
       const int s0 = info1 + 4;
@@ -447,33 +489,86 @@ __device__ __forceinline__ void parse_line(const ParseArgs& a, const uint8_t* __
   a.line_mask[li] = m;
   a.keep[li] = kind != LK_NONE;
   a.ev_tmp[li] = ev;
+  return wm;
 }
 
 // Elapsed-section marking for app files: a line is "in section" when the last of
-// {EL_START (open), EL_END / AUTR_HDR (close)} before it in its file is an open.  One wave per
-// chunk walks its lines 64 at a time; the open state carries across batches per file.
-__global__ __launch_bounds__(APM_WAVE) void k_section_scan(const uint32_t* __restrict__ chunk_line_lo,
-                                                           const uint8_t* __restrict__ chunk_kind,
-                                                           const uint32_t* __restrict__ chunk_file,
-                                                           uint32_t n_chunks,
-                                                           uint32_t* __restrict__ line_mask,
-                                                           uint8_t* __restrict__ keep,
-                                                           Event* __restrict__ ev_tmp,
-                                                           uint8_t* __restrict__ file_open) {
+// {EL_START (open), EL_END (close)} before it in its file is an open; the state carries across
+// batches per file.  Two passes over SEC_SEGS segments per chunk (one wave each) instead of one
+// wave walking a whole chunk 64 lines at a time (~120 us of dependent loads per batch):
+//   k_section_summary: the last open/close event of each segment (0 none, 1 open, 2 close);
+//   k_section_apply:   incoming state = the nearest earlier segment with an event (else the
+//                      file's carried state), then the 64-lane ballot walk of its own segment.
+constexpr int SEC_SEGS = 32;
+
+__device__ __forceinline__ void section_events(uint32_t m, bool valid, bool& is_open, bool& is_close) {
+  is_open = valid && (m & PM_EL_START);
+  // Only `^]` can end a section (a header with an unknown autrId does not reset the flag, and
+  // a line that is also an auditTrailId map line never reaches the elapsed branch).  Treating
+  // fewer lines as closers can only over-approximate the section, which the host tolerates.
+  is_close = valid && (m & PM_EL_END) && !(m & PM_AUTR_MAP) && !is_open;
+}
+
+__device__ __forceinline__ void section_range(const uint32_t* chunk_line_lo, uint32_t c, int g, uint32_t& lo,
+                                              uint32_t& hi) {
+  const uint32_t c0 = chunk_line_lo[c], c1 = chunk_line_lo[c + 1];
+  const uint32_t n = c1 - c0;
+  const uint32_t seg = ((n + SEC_SEGS - 1) / SEC_SEGS + APM_WAVE - 1) / APM_WAVE * APM_WAVE;
+  lo = min(c1, c0 + (uint32_t)g * seg);
+  hi = min(c1, lo + seg);
+}
+
+__global__ __launch_bounds__(APM_WAVE) void k_section_summary(const uint32_t* __restrict__ chunk_line_lo,
+                                                              const uint8_t* __restrict__ chunk_kind,
+                                                              const uint32_t* __restrict__ chunk_file, uint32_t n_chunks,
+                                                              const uint32_t* __restrict__ line_mask,
+                                                              const uint8_t* __restrict__ file_open,
+                                                              uint8_t* __restrict__ seg_state,
+                                                              uint8_t* __restrict__ chunk_init) {
   const uint32_t c = blockIdx.x;
+  const int g = blockIdx.y;
   if (c >= n_chunks || chunk_kind[c] != FILE_APP) return;
   const int lane = threadIdx.x;
-  const uint32_t lo = chunk_line_lo[c], hi = chunk_line_lo[c + 1];
-  bool open = file_open[chunk_file[c]] != 0;
+  if (g == 0 && lane == 0) chunk_init[c] = file_open[chunk_file[c]];  // read before the apply pass writes it
+  uint32_t lo, hi;
+  section_range(chunk_line_lo, c, g, lo, hi);
+  uint8_t st = 0;
+  for (uint32_t base = lo; base < hi; base += APM_WAVE) {
+    const uint32_t li = base + lane;
+    const bool valid = li < hi;
+    bool is_open, is_close;
+    section_events(valid ? line_mask[li] : 0, valid, is_open, is_close);
+    const unsigned long long om = __ballot(is_open), cm = __ballot(is_close);
+    if (om | cm) st = ((om >> (63 - __clzll(om | cm))) & 1ULL) ? 1 : 2;
+  }
+  if (lane == 0) seg_state[(size_t)c * SEC_SEGS + g] = st;
+}
+
+__global__ __launch_bounds__(APM_WAVE) void k_section_apply(const uint32_t* __restrict__ chunk_line_lo,
+                                                            const uint8_t* __restrict__ chunk_kind,
+                                                            const uint32_t* __restrict__ chunk_file, uint32_t n_chunks,
+                                                            uint32_t* __restrict__ line_mask,
+                                                            uint8_t* __restrict__ keep, Event* __restrict__ ev_tmp,
+                                                            uint8_t* __restrict__ file_open,
+                                                            const uint8_t* __restrict__ seg_state,
+                                                            const uint8_t* __restrict__ chunk_init) {
+  const uint32_t c = blockIdx.x;
+  const int g = blockIdx.y;
+  if (c >= n_chunks || chunk_kind[c] != FILE_APP) return;
+  const int lane = threadIdx.x;
+  bool open = chunk_init[c] != 0;
+  for (int h = g - 1; h >= 0; --h) {
+    const uint8_t st = seg_state[(size_t)c * SEC_SEGS + h];
+    if (st) { open = st == 1; break; }
+  }
+  uint32_t lo, hi;
+  section_range(chunk_line_lo, c, g, lo, hi);
   for (uint32_t base = lo; base < hi; base += APM_WAVE) {
     const uint32_t li = base + lane;
     const bool valid = li < hi;
     const uint32_t m = valid ? line_mask[li] : 0;
-    const bool is_open = valid && (m & PM_EL_START);
-    // Only `^]` can end a section (a header with an unknown autrId does not reset the flag, and
-    // a line that is also an auditTrailId map line never reaches the elapsed branch).  Treating
-    // fewer lines as closers can only over-approximate the section, which the host tolerates.
-    const bool is_close = valid && (m & PM_EL_END) && !(m & PM_AUTR_MAP) && !is_open;
+    bool is_open, is_close;
+    section_events(m, valid, is_open, is_close);
     const unsigned long long om = __ballot(is_open);
     const unsigned long long cm = __ballot(is_close);
     const unsigned long long below = lane ? ((1ULL << lane) - 1ULL) : 0ULL;
@@ -500,7 +595,14 @@ __global__ __launch_bounds__(APM_WAVE) void k_section_scan(const uint32_t* __res
       open = (om >> l) & 1ULL;
     }
   }
-  if (lane == 0) file_open[chunk_file[c]] = open ? 1 : 0;
+  if (g == SEC_SEGS - 1 && lane == 0) {  // the chunk's final state, carried to the next batch
+    bool fin = chunk_init[c] != 0;
+    for (int h = SEC_SEGS - 1; h >= 0; --h) {
+      const uint8_t st = seg_state[(size_t)c * SEC_SEGS + h];
+      if (st) { fin = st == 1; break; }
+    }
+    file_open[chunk_file[c]] = fin ? 1 : 0;
+  }
 }
 
 __global__ void k_chunk_lines(const uint32_t* __restrict__ chunk_begin, uint32_t n_chunks,
@@ -539,6 +641,7 @@ size_t apm_parse_workspace_bytes(uint64_t max_bytes, uint32_t max_lines, uint32_
   b += (size_t)max_lines * (4 + 4 + 4 + 1) + 64;
   b += (size_t)max_lines * sizeof(Event) + 64;
   b += (size_t)(max_chunks + 2) * 4 + 256;
+  b += (size_t)(max_chunks + 2) * (SEC_SEGS + 1) + 256;  // section summaries + carried states
   b += APM_SCAN_TMP;
   return b;
 }
@@ -568,6 +671,8 @@ int apm_parse_batch(const uint8_t* d_bytes, uint64_t n_bytes, const uint32_t* d_
   uint32_t* pos = (uint32_t*)carve((size_t)max_lines * 4);
   uint8_t* keep = carve((size_t)max_lines);
   uint32_t* chunk_line_lo = (uint32_t*)carve((size_t)(n_chunks + 2) * 4);
+  uint8_t* seg_state = carve((size_t)(n_chunks + 2) * SEC_SEGS);
+  uint8_t* chunk_init = carve((size_t)(n_chunks + 2));
   void* scan_tmp = carve(APM_SCAN_TMP);
 
   hipLaunchKernelGGL(k_nl_count, dim3(tiles), dim3(NL_BLOCK), 0, stream, d_bytes, n_bytes, tile_counts);
@@ -598,8 +703,11 @@ int apm_parse_batch(const uint8_t* d_bytes, uint64_t n_bytes, const uint32_t* d_
                      stream, pa);
   hipLaunchKernelGGL(k_chunk_lines, dim3((n_chunks + 1 + 255) / 256), dim3(256), 0, stream, d_chunk_begin,
                      n_chunks, line_end, d_n_lines, chunk_line_lo);
-  hipLaunchKernelGGL(k_section_scan, dim3(n_chunks), dim3(APM_WAVE), 0, stream, chunk_line_lo, d_chunk_kind,
-                     d_chunk_file, n_chunks, line_mask, keep, ev_tmp, d_file_open);
+  hipLaunchKernelGGL(k_section_summary, dim3(n_chunks, SEC_SEGS), dim3(APM_WAVE), 0, stream, chunk_line_lo,
+                     d_chunk_kind, d_chunk_file, n_chunks, line_mask, d_file_open, seg_state, chunk_init);
+  hipLaunchKernelGGL(k_section_apply, dim3(n_chunks, SEC_SEGS), dim3(APM_WAVE), 0, stream, chunk_line_lo,
+                     d_chunk_kind, d_chunk_file, n_chunks, line_mask, keep, ev_tmp, d_file_open, seg_state,
+                     chunk_init);
   tmp_bytes = 0;
   HIP_OK(rocprim::exclusive_scan(nullptr, tmp_bytes, keep, pos, 0u, cap, rocprim::plus<uint32_t>(), stream));
   if (tmp_bytes > APM_SCAN_TMP) return -1;
