@@ -15,6 +15,7 @@
 #include <cstring>
 
 #include <algorithm>
+#include <exception>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -109,7 +110,29 @@ std::vector<int> local_core_slice(int device) {
   peers = std::max(peers, 1);
   const size_t per = cores.size() / (size_t)peers;
   if (per == 0) return {};
-  return std::vector<int>(cores.begin() + (ptrdiff_t)(slot * per), cores.begin() + (ptrdiff_t)((slot + 1) * per));
+  // L3 domains (one CCD each on EPYC: 8 cores, 32 MB).  Ranks sharing the NUMA node take whole
+  // CCDs where possible, and inside a slice consecutive lanes go round-robin over its CCDs, so
+  // the first join workers each get a private L3 for their shard's maps instead of eight
+  // workers sharing one CCD's L3 and its fabric link (CPU numbering interleaves CCDs).
+  auto l3_of = [](int c) {
+    const std::string id = read_small("/sys/devices/system/cpu/cpu" + std::to_string(c) + "/cache/index3/id");
+    try { return id.empty() ? 0 : std::stoi(id); } catch (...) { return 0; }
+  };
+  std::vector<std::pair<int, int>> keyed;  // (l3 id, cpu)
+  for (int c : cores) keyed.push_back({l3_of(c), c});
+  std::stable_sort(keyed.begin(), keyed.end());
+  std::vector<std::pair<int, int>> mine_sl(keyed.begin() + (ptrdiff_t)(slot * per),
+                                           keyed.begin() + (ptrdiff_t)((slot + 1) * per));
+  std::vector<std::vector<int>> groups;
+  for (size_t i = 0; i < mine_sl.size(); ++i) {
+    if (i == 0 || mine_sl[i].first != mine_sl[i - 1].first) groups.emplace_back();
+    groups.back().push_back(mine_sl[i].second);
+  }
+  std::vector<int> out;
+  for (size_t r = 0; out.size() < mine_sl.size(); ++r)
+    for (auto& g : groups)
+      if (r < g.size()) out.push_back(g[r]);
+  return out;
 }
 
 // ----------------------------------------------------------------------------- thread pool
@@ -152,10 +175,10 @@ ThreadPool::~ThreadPool() {
   for (auto& t : workers_) t.join();
 }
 
-void ThreadPool::run(int n_tasks, const std::function<void(int)>& fn) {
-  if (n_tasks <= 0) return;
-  if (workers_.empty() || n_tasks == 1) {
+void ThreadPool::run(int n_tasks, const std::function<void(int)>& fn, const std::function<void()>* meanwhile) {
+  if (n_tasks <= 0 || workers_.empty() || n_tasks == 1) {
     for (int i = 0; i < n_tasks; ++i) fn(i);
+    if (meanwhile) (*meanwhile)();
     return;
   }
   std::unique_lock<std::mutex> lk(mu_);
@@ -164,8 +187,16 @@ void ThreadPool::run(int n_tasks, const std::function<void(int)>& fn) {
   done_ = 0;
   ++gen_;
   cv_.notify_all();
+  std::exception_ptr err;
+  if (meanwhile) {
+    lk.unlock();
+    try { (*meanwhile)(); } catch (...) { err = std::current_exception(); }
+    lk.lock();
+  }
   done_cv_.wait(lk, [&]() { return done_ == n_tasks_; });
   fn_ = nullptr;
+  lk.unlock();
+  if (err) std::rethrow_exception(err);
 }
 
 // ----------------------------------------------------------------------------- setup
@@ -535,7 +566,8 @@ JoinCounters Engine::join_counters() const {
 // ----------------------------------------------------------------------------- batch
 // Stage a batch into a parse slot (canonical chunk order, pinned staging if needed) and enqueue
 // H2D + K1/K2 on the parse stream.  Nothing waits here.
-void Engine::launch_parse(ParseSlot& ps, const uint8_t* host_bytes, uint64_t n_bytes, const std::vector<Chunk>& chunks_in) {
+void Engine::launch_parse(ParseSlot& ps, const uint8_t* host_bytes, uint64_t n_bytes, const std::vector<Chunk>& chunks_in,
+                          bool speculative) {
   const double t0 = now_ms();
   if (n_bytes > cfg_.max_batch_bytes) throw std::runtime_error("batch larger than max_batch_bytes");
   if (chunks_in.size() > cfg_.max_chunks) throw std::runtime_error("too many chunks in batch");
@@ -611,6 +643,16 @@ void Engine::launch_parse(ParseSlot& ps, const uint8_t* host_bytes, uint64_t n_b
     throw std::runtime_error("parse workspace too small");
   HIP_OK(hipMemcpyAsync(ps.h_counts, d_counts_, 8, hipMemcpyDeviceToHost, parse_stream_));
   HIP_OK(hipMemcpyAsync(ps.h_watermark, d_watermark_, 8, hipMemcpyDeviceToHost, parse_stream_));
+  // Prefetched parse: the event count is only known on the device, so copy a guess (the last
+  // batch's count + 25 %) right behind the kernels.  The DMA then runs during the current
+  // batch's host join instead of on the ingest thread's critical path (15 MB, ~0.3 ms), and
+  // finish_parse copies only what the guess missed.
+  ps.spec_copied = 0;
+  if (speculative && !ps.d_events_host && spec_events_) {
+    ps.spec_copied = std::min<uint32_t>(spec_events_, cfg_.max_lines);
+    HIP_OK(hipMemcpyAsync(ps.h_events, d_events_, (size_t)ps.spec_copied * sizeof(Event), hipMemcpyDeviceToHost,
+                          parse_stream_));
+  }
   ps.pending = true;
   metrics_.t_parse_ms += now_ms() - t0;
 }
@@ -624,11 +666,14 @@ void Engine::finish_parse(ParseSlot& ps) {
   if (ps.n_lines > cfg_.max_lines) throw std::runtime_error("batch has more lines than max_lines");
   metrics_.lines += ps.n_lines;
   metrics_.events += ps.n_events;
-  if (ps.n_events && !ps.d_events_host) {
-    HIP_OK(hipMemcpyAsync(ps.h_events, d_events_, (size_t)ps.n_events * sizeof(Event), hipMemcpyDeviceToHost,
-                          parse_stream_));
+  if (ps.n_events > ps.spec_copied && !ps.d_events_host) {
+    const uint32_t lo = ps.spec_copied;
+    HIP_OK(hipMemcpyAsync(ps.h_events + lo, d_events_ + lo, (size_t)(ps.n_events - lo) * sizeof(Event),
+                          hipMemcpyDeviceToHost, parse_stream_));
     HIP_OK(hipStreamSynchronize(parse_stream_));
   }
+  ps.spec_copied = 0;
+  spec_events_ = ps.n_events + ps.n_events / 4 + 1024;
   ps.pending = false;
   last_slot_ = (int)(&ps - pslot_);
   metrics_.t_parse_ms += now_ms() - t0;
@@ -649,10 +694,14 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
   }
   finish_parse(ps);
   // Pipelining: the next batch's H2D + parse kernels run on the GPU while this batch is joined.
-  if (next_bytes && next_chunks) {
-    launch_parse(pslot_[cur_slot_ ^ 1], next_bytes, next_n, *next_chunks);
+  // Their host side (chunk table, ~15 launches, copies: ~0.3 ms) is issued by this thread while
+  // the join workers run, instead of ahead of them on the critical path.
+  ParseSlot& next_ps = pslot_[cur_slot_ ^ 1];
+  const bool launch_next = next_bytes && next_chunks;
+  const std::function<void()> launch_next_parse = [&]() {
+    launch_parse(next_ps, next_bytes, next_n, *next_chunks, /*speculative=*/true);
     prefetched_ = true;
-  }
+  };
   cur_slot_ ^= 1;
   const uint8_t* hb = ps.hb;
   const std::vector<int32_t>& chunk_file = ps.chunk_file;
@@ -697,7 +746,7 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
     sh.begin_batch(clock, batch_no_);
     for (const auto& r : shard_range[s]) sh.process(h_events + r.first, r.second - r.first, hb, chunk_file);
     shard_ms_[(size_t)s * 16] = now_ms() - ts0;
-  });
+  }, launch_next ? &launch_next_parse : nullptr);
   const double t1b = now_ms();
   metrics_.t_join_shards_ms += t1b - t1;
   {

@@ -145,7 +145,9 @@ class ThreadPool {
  public:
   explicit ThreadPool(int n, const std::vector<int>& cpus = {});
   ~ThreadPool();
-  void run(int n_tasks, const std::function<void(int)>& fn);
+  // `meanwhile` (optional) runs on the calling thread while the workers execute the tasks; an
+  // exception it throws is rethrown after every task has finished.
+  void run(int n_tasks, const std::function<void(int)>& fn, const std::function<void()>* meanwhile = nullptr);
   int size() const { return (int)workers_.size(); }
 
  private:
@@ -403,11 +405,14 @@ class Engine {
     uint64_t src_n = 0, n_bytes = 0;
     std::vector<int32_t> chunk_file;
     uint32_t n_events = 0, n_lines = 0;
+    uint32_t spec_copied = 0;                   // events already D2H'd behind the parse kernels
     bool pending = false;
   } pslot_[2];
+  uint32_t spec_events_ = 0;                    // speculative D2H size for the next prefetched parse
   int cur_slot_ = 0, last_slot_ = 0;
   bool prefetched_ = false;
-  void launch_parse(ParseSlot& ps, const uint8_t* host_bytes, uint64_t n_bytes, const std::vector<Chunk>& chunks);
+  void launch_parse(ParseSlot& ps, const uint8_t* host_bytes, uint64_t n_bytes, const std::vector<Chunk>& chunks,
+                    bool speculative = false);
   void finish_parse(ParseSlot& ps);
   uint32_t* d_chunk_begin_ = nullptr;
   uint8_t* d_chunk_kind_ = nullptr;

@@ -352,9 +352,10 @@ void JoinShard::save_acct(std::string_view acct_raw, int32_t file, int source, s
 }
 
 // attemptReadAccountNumberFromBAFInfo (:486-497)
-std::string_view JoinShard::baf_acct(std::string_view line, std::string_view t3, int32_t file,
+std::string_view JoinShard::baf_acct(const Event& e, std::string_view line, std::string_view t3, int32_t file,
                                      std::string_view log_id, uint64_t seq, std::string& scratch) {
-  if (!baf_match(line)) return std::string_view();
+  // the parse kernel already tested the pattern (PM_BAF) unless it deferred the line to the host
+  if (!((e.mask & PM_HOST) ? baf_match(line) : (e.mask & PM_BAF) != 0)) return std::string_view();
   // .replace(/.*]\[/,'') -> drop through the last "]["
   size_t p = std::string_view::npos;
   for (size_t i = 0; i + 1 < t3.size(); ++i) if (t3[i] == ']' && t3[i + 1] == '[') p = i;
@@ -374,20 +375,20 @@ void JoinShard::on_soap(const Event& e, std::string_view line, int32_t file, uin
   if (m & PM_SOAP_IN) {
     Toks tk;
     if (e.mask & PM_HOST) tk.from_line(line); else tk.from_event(e, line);
-    SoapCtx c;
+    // the context is reused per file: assigning into it keeps the logId string's capacity
+    SoapCtx& dst = soap_.put(file);
+    dst.has_log_id = false;
+    dst.pull_next = false;
     if (tk.has(1)) {
       std::string_view t1 = tk.t[1];
       size_t eq = t1.find('=');
       if (eq != std::string_view::npos) {
         size_t eq2 = t1.find('=', eq + 1);
-        c.log_id.assign(t1.substr(eq + 1, eq2 == std::string_view::npos ? std::string_view::npos : eq2 - eq - 1));
-        c.has_log_id = true;
+        dst.log_id.assign(t1.substr(eq + 1, eq2 == std::string_view::npos ? std::string_view::npos : eq2 - eq - 1));
+        dst.has_log_id = true;
       }
     }
-    SoapCtx& dst = soap_.put(file);
-    dst.log_id.swap(c.log_id);
-    dst.has_log_id = c.has_log_id;
-    dst.pull_next = false;
+    if (!dst.has_log_id) dst.log_id.clear();
   } else if (m & PM_SOAP_OUT) {
     soap_.erase(file);
   } else {
@@ -507,7 +508,7 @@ void JoinShard::on_ct(const Event& e, std::string_view line, int32_t file, bool 
   if (has_elapsed) elapsed = host ? js::parse_int(elapsed_v) : e.num;
   std::string baf_scratch;
   auto salvage = [&]() {  // salvageRecordAndOutput (:500-504)
-    std::string_view acct = baf_acct(line, tk.get(3), file, log_id, seq, baf_scratch);
+    std::string_view acct = baf_acct(e, line, tk.get(3), file, log_id, seq, baf_scratch);
     output(server, svc, "", acct.empty() ? js::nan() : js::parse_int(acct), 0, true, ts, ts_empty, elapsed, false,
            seq);
   };
@@ -526,7 +527,7 @@ void JoinShard::on_ct(const Event& e, std::string_view line, int32_t file, bool 
     return;
   }
   need_map(key, log_id);
-  std::string_view alt = baf_acct(line, tk.get(3), file, log_id, seq, baf_scratch);  // may drain the map first
+  std::string_view alt = baf_acct(e, line, tk.get(3), file, log_id, seq, baf_scratch);  // may drain the map first
   Need n{svc, part.server, part.start_ms, false, ts, ts_empty, elapsed,
          alt.empty() ? js::nan() : js::parse_int(alt), false};
   auto& ni = need_map(key, log_id).items;
@@ -560,7 +561,7 @@ void JoinShard::on_app(const Event& e, std::string_view line, int32_t file, uint
     }
     AuditCtx& ctx = audit_[file];
     std::string baf_scratch;
-    std::string alt(baf_acct(line, toks.size() > 3 ? toks[3] : std::string_view(), file, log_id, seq, baf_scratch));
+    std::string alt(baf_acct(e, line, toks.size() > 3 ? toks[3] : std::string_view(), file, log_id, seq, baf_scratch));
     auto f = std::find_if(ctx.autr_map.begin(), ctx.autr_map.end(), [&](auto& p) { return p.first == autr; });
     if (f != ctx.autr_map.end()) f->second = {log_id, alt};
     else ctx.autr_map.push_back({autr, {log_id, alt}});

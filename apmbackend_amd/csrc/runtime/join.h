@@ -185,7 +185,7 @@ class alignas(128) JoinShard {
   void save_acct(std::string_view acct, int32_t file, int source, std::string_view alt_log_id, uint64_t seq);
   void output(int32_t server, int32_t svc, std::string_view log_id, double acct, double start_ms, bool start_empty,
               double end_ms, bool end_empty, double elapsed, bool to_db, uint64_t seq);
-  std::string_view baf_acct(std::string_view line, std::string_view tok3, int32_t file, std::string_view log_id,
+  std::string_view baf_acct(const Event& e, std::string_view line, std::string_view tok3, int32_t file, std::string_view log_id,
                             uint64_t seq, std::string& scratch);
 
   void on_soap(const Event& e, std::string_view line, int32_t file, uint64_t seq);

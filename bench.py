@@ -224,6 +224,7 @@ def main():
             "ingest_GB_per_s": round(bytes_total / dt_max / 1e9, 3),
             "series_per_gpu": eng.eng.n_series(),
             "pinned_cpus": len(eng.eng.lane_cpus()),
+            "lane_cpus_head": list(eng.eng.lane_cpus())[:18],
             "stage_ms_per_step": {k: round((m1[k] - m0[k]) / args.steps, 3)
                                   for k in ("t_parse_ms", "t_join_ms", "t_join_shards_ms", "t_shard_busy_ms", "t_shard_max_ms", "t_merge_ms", "t_stats_ms",
                                             "t_stats_tx_ms", "t_release_ms", "t_rollover_ms", "t_format_ms", "t_out_ms")},
