@@ -422,6 +422,7 @@ void Engine::load_state(const std::string& path) {
     }
     n_series_ = (int32_t)sr.size();
     perm_dirty_ = true;
+    h_perm_.clear();
     series_service_uploaded_ = 0;
   }
   const int32_t n = n_series_;
