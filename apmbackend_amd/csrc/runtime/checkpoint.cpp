@@ -406,6 +406,7 @@ void Engine::load_state(const std::string& path) {
     series_.clear();
     series_map_.clear();
     ser_tab_.clear();
+    ser_raw_.clear();
     for (size_t i = 0; i < sr.size(); ++i) {
       series_.push_back(SeriesInfo{sr[i].server, sr[i].service, sr[i].emit_key});
       series_map_[((uint64_t)(uint32_t)(sr[i].server + 1) << 32) | (uint32_t)sr[i].service] = (int32_t)i + 1;

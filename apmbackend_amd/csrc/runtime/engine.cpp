@@ -1062,7 +1062,17 @@ void Engine::stats_for_batch(std::vector<TxOut>& txs, double batch_t0) {
     // a tx with a newer bucket triggers the rollover *before* it is added (:348-370)
     if (b > latest_) { triggers.push_back({n, b}); latest_ = b; }
     if (n >= (uint32_t)cfg_.max_tx_per_batch) throw std::runtime_error("too many tx in one batch");
-    const int32_t s = series_for(t.server, t.service);
+    int32_t s;
+    {
+      if ((size_t)t.server >= ser_raw_.size()) ser_raw_.resize((size_t)t.server + 1);
+      auto& row = ser_raw_[t.server];
+      if ((size_t)t.raw_svc >= row.size()) row.resize(std::max<size_t>((size_t)t.raw_svc + 1, row.size() * 2), -1);
+      s = row[t.raw_svc];
+      if (s < 0) {
+        s = series_for(t.server, t.service);
+        row[t.raw_svc] = s;  // -1 (series table full) stays uncached
+      }
+    }
     TxRec r;
     r.end_ms = end;
     r.series = s;

@@ -367,6 +367,10 @@ class Engine {
   // series
   FlatMap<int32_t> series_map_{1 << 16};  // ((server + 1) << 32 | service) -> series + 1
   std::vector<std::vector<int32_t>> ser_tab_;  // cache of series_map_: [server][service] -> series / -1
+  // [server][shard-local raw service id] -> series / -1: the tx loop's lookup.  Rows are as long
+  // as the shard's own service list (a few thousand), where ser_tab_ rows span the global
+  // service dictionary (100k ids x 32 servers = 12.8 MB for the firehose shard: a miss per tx).
+  std::vector<std::vector<int32_t>> ser_raw_;
   void ser_tab_put(int32_t server, int32_t service, int32_t s) {
     if (server < 0 || service < 0 || service >= (1 << 20)) return;
     if ((size_t)server >= ser_tab_.size()) ser_tab_.resize((size_t)server + 1);

@@ -256,6 +256,7 @@ void JoinShard::output(int32_t server, int32_t svc, std::string_view log_id, dou
   const SvcInfo& rs = svc_info_[svc];
   const std::string_view norm(svc_text_.data() + rs.norm_off, rs.norm_len);
   t.service = rs.norm_id;
+  t.raw_svc = svc;
   double s = start_empty ? js::nan() : start_ms;
   const double e_for_sub = end_empty ? 0.0 : end_ms;  // JS: '' - n === -n
   if (!(s == s) || s == 0) s = e_for_sub - elapsed;

@@ -47,6 +47,7 @@ struct TxOut {
   uint64_t seq;          // merge key: line emissions (1<<63)|(line<<12)|sub; expiries creation<<12|sub
   int32_t server;        // server id (== shard index: the line lives in that shard's text arena)
   int32_t service;       // normalized service id
+  int32_t raw_svc;       // the shard's interned raw service id (dense per shard: series lookup key)
   double end_ms;         // endTs (NaN when '')
   double elapsed;        // parseInt(elapsed)
   uint32_t line_off;     // wire-format tx line (entries.js:16-21, no newline) in the shard arena
