@@ -745,7 +745,9 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
     sh.out().clear();
     sh.begin_batch(clock, batch_no_);
     for (const auto& r : shard_range[s]) sh.process(h_events + r.first, r.second - r.first, hb, chunk_file);
-    shard_ms_[(size_t)s * 16] = now_ms() - ts0;
+    const double ts1 = now_ms();
+    shard_ms_[(size_t)s * 16] = ts1 - ts0;
+    trace_event("shard", ts0, ts1, 2 + s);
   }, launch_next ? &launch_next_parse : nullptr);
   const double t1b = now_ms();
   metrics_.t_join_shards_ms += t1b - t1;

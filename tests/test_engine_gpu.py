@@ -289,10 +289,31 @@ def test_server_rollup_fuses_window_stats_with_jmx_gauges():
     assert checked > 0
 
 
-def test_parse_prefetch_pipelining_is_transparent():
+def _regroup(bl, sizes):
+    """Concatenate consecutive batches (per file, in order) into groups of the given sizes."""
+    out, i, k = [], 0, 0
+    while i < len(bl):
+        n = sizes[k % len(sizes)]
+        k += 1
+        grp = bl[i:i + n]
+        i += n
+        per_file = collections.OrderedDict()
+        for _, chunks in grp:
+            for fp, ls in chunks:
+                per_file.setdefault(fp, []).extend(ls)
+        out.append((grp[-1][0], [(fp, ls) for fp, ls in per_file.items() if ls]))
+    return out
+
+
+@pytest.mark.parametrize("shape", ["uniform", "growing"])
+def test_parse_prefetch_pipelining_is_transparent(shape):
     """process_batch(i, next=i+1) launches batch i+1's parse before batch i's join: outputs
-    must be identical to the plain sequence."""
+    must be identical to the plain sequence.  "growing" alternates small and very large batches
+    so the speculative event D2H behind a prefetched parse (last count + 25 % + 1024) falls
+    short and finish_parse has to copy the remainder."""
     lines, bl = synth_batches(11, duration=400)
+    if shape == "growing":
+        bl = _regroup(bl, [1, 1, 24, 1, 30])
     C = small_cfg("exact")
     _, plain = _run_engine(C, bl)
     eng = APMEngine(C, keep_text=True)
