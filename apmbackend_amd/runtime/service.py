@@ -52,6 +52,20 @@ RESTART_KEYS = ["apmConfigFilePath", "amqpConnectionString", "streamParseTransac
                 "gpu.maxSeries", "gpu.ringDtype", "gpu.zscoreMeanMode", "gpu.outputMode"]
 
 
+def read_json(path: str) -> Dict[str, Any]:
+    with open(path) as f:
+        return json.load(f)
+
+
+def write_json_atomic(path: str, obj: Any):
+    tmp = f"{path}.tmp{os.getpid()}"
+    with open(tmp, "w") as f:
+        json.dump(obj, f)
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(tmp, path)
+
+
 def discover_files(cfg: Dict[str, Any]) -> List[str]:
     pc = cfg["streamParseTransactions"]
     prefix = pc.get("appLogDirMaskPrefix", "")
@@ -93,6 +107,7 @@ class IngestService:
         all_files = list(files) if files is not None else discover_files(self.cfg)
         servers = sorted({self.server_of(f) for f in all_files})
         mine = set(shard_servers(servers, self.world)[self.rank]) if servers else set()
+        self.my_servers = sorted(mine)
         self.files = [f for f in all_files if self.server_of(f) in mine]
         log.info("rank %d/%d: %d of %d files, servers %s", self.rank, self.world, len(self.files), len(all_files),
                  sorted(mine))
@@ -119,6 +134,7 @@ class IngestService:
         self.ckpt_dir = g.get("checkpointDir")
         self.ckpt_every = float(g.get("checkpointEverySeconds",
                                       self.cfg["streamCalcStats"].get("resumeFileSaveFrequencyInSeconds", 60)))
+        self.resharded = False
         restored = self._restore() if (self.ckpt_dir and engine == "native") else False
         if not restored:
             if engine == "native" and as_bool(g.get("importReferenceResume", False)):
@@ -139,6 +155,8 @@ class IngestService:
         self.offsets_path = pc.get("tailOffsetFileFullPath")
         if restored:
             self._restore_offsets()
+        elif self.resharded:
+            self._restore_offsets_resharded()
 
         # ---- outputs
         self.inserter: Optional[DBInserter] = None
@@ -200,9 +218,38 @@ class IngestService:
         return (os.path.join(self.ckpt_dir, f"engine.rank{self.rank}.ckpt"),
                 os.path.join(self.ckpt_dir, f"tail.rank{self.rank}.json"))
 
+    def _meta_path(self, rank: Optional[int] = None) -> str:
+        return os.path.join(self.ckpt_dir, f"meta.rank{self.rank if rank is None else rank}.json")
+
+    def _checkpoint_is_mine(self) -> bool:
+        """A rank's checkpoint is reused only if it was written for the same world size and
+        server shard, and is not stale relative to the other ranks' (a rank of an older, larger
+        world whose files survived a degrade).  Checkpoints without metadata predate it: mine."""
+        mp = self._meta_path()
+        if not os.path.exists(mp):
+            return True
+        meta = read_json(mp)
+        if meta.get("world") != self.world or sorted(meta.get("servers", [])) != self.my_servers:
+            log.warning("checkpoint of rank %d was written for world %s (servers %s); this rank now owns %s "
+                        "in world %d: re-sharded start", self.rank, meta.get("world"), meta.get("servers"),
+                        self.my_servers, self.world)
+            return False
+        newest = max((read_json(q).get("ts", 0.0) for q in glob.glob(os.path.join(self.ckpt_dir, "meta.rank*.json"))),
+                     default=0.0)
+        if newest - float(meta.get("ts", 0.0)) > 2 * self.ckpt_every + 60:
+            log.warning("checkpoint of rank %d is %.0f s older than the newest rank checkpoint: re-sharded start",
+                        self.rank, newest - float(meta.get("ts", 0.0)))
+            return False
+        return True
+
     def _restore(self) -> bool:
         ck, _ = self._ckpt_paths()
-        if not os.path.exists(ck):
+        if not os.path.exists(ck) and not glob.glob(os.path.join(self.ckpt_dir, "tail.rank*.json")):
+            return False
+        if not os.path.exists(ck) or not self._checkpoint_is_mine():
+            # world size changed (elastic degrade / grow): fresh engine state for this shard, tails
+            # resumed from whichever rank owned each file last (_restore_offsets_resharded)
+            self.resharded = True
             return False
         try:
             self.eng.load_state(ck)
@@ -238,6 +285,24 @@ class IngestService:
         for path, (off, ino) in offs.items():
             self.tailer.set_offset(path, int(off), int(ino))
 
+    def _restore_offsets_resharded(self):
+        """Tail offsets after a world-size change: for every file this rank now owns, the offset
+        from the most recently written tail file of any old rank that held it."""
+        best: Dict[str, Any] = {}
+        for tp in glob.glob(os.path.join(self.ckpt_dir, "tail.rank*.json")):
+            try:
+                mt = os.path.getmtime(tp)
+                offs = read_json(tp)
+            except (OSError, ValueError):
+                continue
+            for path, v in offs.items():
+                if path in self.file_ids and (path not in best or mt > best[path][0]):
+                    best[path] = (mt, v)
+        for path, (_mt, (off, ino)) in best.items():
+            self.tailer.set_offset(path, int(off), int(ino))
+        log.info("re-sharded start: resumed %d of %d tails from the previous world's offsets", len(best),
+                 len(self.file_ids))
+
     def checkpoint(self):
         if not self.ckpt_dir or self.eng is None:
             return None
@@ -248,6 +313,8 @@ class IngestService:
         self._drain_outputs()
         n = self.native.save_state(ck)
         self.tailer.save_offsets(tp)
+        write_json_atomic(self._meta_path(), {"world": self.world, "rank": self.rank, "servers": self.my_servers,
+                                              "ts": time.time()})
         if self.offsets_path:
             self.tailer.save_offsets(self.offsets_path)
         log.info("checkpoint %s: %.1f MB in %.0f ms", ck, n / 1e6, (time.perf_counter() - t0) * 1e3)

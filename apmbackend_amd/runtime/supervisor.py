@@ -13,6 +13,9 @@
   ``restartDelaySeconds`` (1 s), or ``crashLoopDelaySeconds`` (60 s) when it died less than
   ``crashLoopWindowSeconds`` (5 s) after starting (childExitCB :303-327).  A rank group restarts as
   a whole: RCCL communicators cannot lose a member, so the surviving ranks are stopped first.
+  **Elastic degrade**: a GPU whose rank keeps failing (``elasticMaxFailures`` within
+  ``elasticWindowSeconds``) is retired and the group restarts at the next smaller world size
+  (8 -> 4 -> 2 -> 1 by default), re-sharding the JVM hosts; see ``_elastic_degrade``.
 * **monitoring** every ``inspectionFrequencySeconds`` aligned to the clock
   (monitorResourcesRecurs :514-530): liveness (kill(pid, 0)), per-module PSS/swap (native
   /proc/<pid>/smaps_rollup reader, the pid_stats.py equivalent) and HBM per process (KFD sysfs)
@@ -186,19 +189,42 @@ class Module:
             ranks = int(os.environ.get("APM_GPUS", "0")) or _gpu_count()
         self.ranks = int(ranks or 0)
         log_dir = cfg.get("logDir", "/tmp/apm/logs")
+        self.argv, self.log_dir, self.state_dir = argv, log_dir, state_dir
         self.procs: List[Proc] = []
+        # elastic rank group: the GPUs it may use, the ones retired after repeated failures, the
+        # failure times per GPU, and the generation (bumped at every world-size change)
+        self.devices: List[int] = [int(d) for d in setting.get("devices", [])] or list(range(self.ranks))
+        self.explicit_devices = bool(setting.get("devices"))
+        self.bad_devices: set = set()
+        self.dev_failures: Dict[int, List[float]] = {}
+        self.generation = 0
         if self.ranks:
-            port = str(setting.get("masterPort", 29512))
-            for r in range(self.ranks):
-                env = {"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(self.ranks),
-                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": port}
-                self.procs.append(Proc(f"{self.name}.rank{r}", argv, env,
-                                       os.path.join(log_dir, f"{self.name}.rank{r}.start.log"),
-                                       os.path.join(state_dir, f"{self.name}.rank{r}.pid")))
+            self.build_ranks(self.ranks, self.devices[:self.ranks])
         else:
             self.procs.append(Proc(self.name, argv, dict(setting.get("env", {})),
                                    os.path.join(log_dir, f"{self.name}.start.log"),
                                    os.path.join(state_dir, f"{self.name}.pid")))
+
+    def build_ranks(self, world: int, devices: List[int]):
+        """(Re)create the rank processes: one per GPU in `devices`, WORLD_SIZE = world."""
+        self.ranks = world
+        self.active_devices = list(devices)
+        port = int(self.s.get("masterPort", 29512)) + self.generation  # fresh rendezvous per generation
+        self.procs = []
+        for r in range(world):
+            env = {"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(world),
+                   "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "APM_DEVICE": str(devices[r]),
+                   "APM_ELASTIC_GENERATION": str(self.generation)}
+            if self.explicit_devices or self.generation:
+                # LOCAL_RANK r indexes the visible list, so rank r drives physical GPU devices[r]
+                env["HIP_VISIBLE_DEVICES"] = ",".join(str(d) for d in devices)
+            self.procs.append(Proc(f"{self.name}.rank{r}", self.argv, env,
+                                   os.path.join(self.log_dir, f"{self.name}.rank{r}.start.log"),
+                                   os.path.join(self.state_dir, f"{self.name}.rank{r}.pid")))
+
+    def device_of(self, p: "Proc") -> Optional[int]:
+        v = p.env.get("APM_DEVICE")
+        return int(v) if v is not None else None
 
     def setting(self, key: str, mcfg: Dict[str, Any]):
         """getModuleSetting (:455-464): module value if set (0 counts), else the global one."""
@@ -288,7 +314,50 @@ class Supervisor:
             for p in mod.procs:
                 p.stop()
 
+    def _elastic_degrade(self, mod: Module, p: Proc, code: int, now: float) -> bool:
+        """Elastic rank group: a GPU whose rank failed `elasticMaxFailures` times
+        within `elasticWindowSeconds` is retired and the group restarts at the largest world size
+        the healthy GPUs allow (powers of two by default: 8 -> 4 -> 2 -> 1).  The new ranks shard
+        the JVM hosts over the new world; each resumes the tails of the files it now owns from the
+        old ranks' offsets (no data gap), and the series that moved rank start a fresh history."""
+        flag = mod.setting("elasticDegrade", self.m)
+        if not mod.ranks or code == 0 or (flag is not None and not as_bool(flag)):
+            return False
+        dev = mod.device_of(p)
+        if dev is None:
+            return False
+        window = float(mod.setting("elasticWindowSeconds", self.m) or 900)
+        limit = int(mod.setting("elasticMaxFailures", self.m) or 3)
+        hist = [t for t in mod.dev_failures.get(dev, []) if now - t <= window] + [now]
+        mod.dev_failures[dev] = hist
+        if len(hist) < limit:
+            return False
+        mod.bad_devices.add(dev)
+        healthy = [d for d in mod.devices if d not in mod.bad_devices]
+        world = len(healthy)
+        if str(mod.setting("elasticWorldSizes", self.m) or "pow2") == "pow2" and world:
+            world = 1 << (world.bit_length() - 1)
+        old_world = mod.ranks
+        for q in mod.procs:
+            q.stop()
+        if world == 0:
+            mod.procs = []
+            self.add_alert(f"Rank group {mod.name}: every GPU retired (last: {dev}); not restarting")
+            return True
+        mod.generation += 1
+        mod.build_ranks(world, healthy[:world])
+        delay = float(self.m.get("restartDelaySeconds", 1))
+        for q in mod.procs:
+            q.restart_at = now + delay
+        text = (f"Rank group {mod.name} degraded from {old_world} to {world} GPUs: GPU {dev} failed "
+                f"{len(hist)} times in {int(window)} s (generation {mod.generation}, GPUs {healthy[:world]})")
+        self.annotate(self.cfg.get("grafana", {}), text, ["maintenance"])
+        self.add_alert(text)
+        return True
+
     def _on_exit(self, mod: Module, p: Proc, code: int, now: float):
+        if p not in mod.procs:  # a rank retired by an elastic restart
+            return
         log.error("Child exited: code:%s module: %s", code, p.name)
         self.annotate(self.cfg.get("grafana", {}), f"Module exited: {p.name}", ["maintenance"])
         self.add_alert(f"Child module exited: code:{code} module: {p.name}")
@@ -297,6 +366,8 @@ class Supervisor:
         if quick:
             log.warning("Time since last restart is under %ss: crash loop suspected, waiting %ss",
                         self.m.get("crashLoopWindowSeconds", 5), delay)
+        if self._elastic_degrade(mod, p, code, now):
+            return
         targets = mod.procs if mod.ranks else [p]
         for q in targets:  # a rank group restarts as a whole
             if q is not p:

@@ -194,3 +194,63 @@ def test_latency_percentiles_nearest_rank():
     xs = [float(i) for i in range(1, 101)]
     assert _percentiles(xs, (50, 90, 99)) == ["50.0", "90.0", "99.0"]
     assert _percentiles([7.0], (50, 99)) == ["7.0", "7.0"]
+
+
+def test_resharded_restart_resumes_tails_from_previous_world(tmp_path):
+    """Elastic degrade 2 -> 1 ranks: the surviving rank's checkpoint metadata no longer matches
+    its shard, so it starts fresh but resumes every tail it now owns from the newest offset any
+    old rank recorded (no data gap, no replay)."""
+    from apmbackend_amd.parallel.dist import shard_servers
+    from apmbackend_amd.runtime.service import write_json_atomic
+    C, lines, mapping, sc = make_env(tmp_path, servers=4, duration=30)
+    files = sorted(mapping.values())
+    for f in files:  # some bytes to resume into
+        with open(f, "w") as fh:
+            fh.write("x" * 1000 + "\n")
+    ck = tmp_path / "ckpt"
+    ck.mkdir()
+    servers = sorted({srv_of(f) for f in files})
+    shards = shard_servers(servers, 2)
+    now = time.time()
+    for r in range(2):
+        mine = [f for f in files if srv_of(f) in shards[r]]
+        offs = {f: [100 + 10 * r + i, os.stat(f).st_ino] for i, f in enumerate(mine)}
+        offs[files[0]] = [7, os.stat(files[0]).st_ino]  # stale duplicate entry in both tail files
+        write_json_atomic(str(ck / f"tail.rank{r}.json"), offs)
+        os.utime(ck / f"tail.rank{r}.json", (now - 100 + r, now - 100 + r))
+        write_json_atomic(str(ck / f"meta.rank{r}.json"), {"world": 2, "rank": r, "servers": sorted(shards[r]),
+                                                           "ts": now - 100})
+    svc = IngestService(C, engine="cpu-oracle", files=files, rank=0, world=1, server_of_path=srv_of)
+    svc.ckpt_dir = str(ck)
+    assert not svc._checkpoint_is_mine()
+    svc._restore_offsets_resharded()
+    out = tmp_path / "resumed.json"
+    svc.tailer.save_offsets(str(out))
+    got = json.load(open(out))
+    for r in range(2):
+        for i, f in enumerate(f for f in files if srv_of(f) in shards[r]):
+            if f != files[0]:
+                assert got[f][0] == 100 + 10 * r + i, f
+    assert got[files[0]][0] == 7  # the newest tail file's value (rank 1's, written last)
+    svc.shutdown()
+
+
+def test_checkpoint_ownership_rules(tmp_path):
+    from apmbackend_amd.runtime.service import write_json_atomic
+    C, lines, mapping, sc = make_env(tmp_path, servers=2, duration=30)
+    files = sorted(mapping.values())
+    ck = tmp_path / "ckpt"
+    ck.mkdir()
+    svc = IngestService(C, engine="cpu-oracle", files=files, rank=0, world=1, server_of_path=srv_of)
+    svc.ckpt_dir = str(ck)
+    assert svc._checkpoint_is_mine()  # no metadata: a checkpoint from before metadata existed
+    now = time.time()
+    write_json_atomic(str(ck / "meta.rank0.json"), {"world": 1, "servers": svc.my_servers, "ts": now})
+    assert svc._checkpoint_is_mine()
+    # same shard, but far older than another rank's checkpoint: a survivor of an older world
+    write_json_atomic(str(ck / "meta.rank0.json"), {"world": 1, "servers": svc.my_servers, "ts": now - 10000})
+    write_json_atomic(str(ck / "meta.rank3.json"), {"world": 4, "servers": [], "ts": now})
+    assert not svc._checkpoint_is_mine()
+    write_json_atomic(str(ck / "meta.rank0.json"), {"world": 2, "servers": svc.my_servers, "ts": now})
+    assert not svc._checkpoint_is_mine()
+    svc.shutdown()

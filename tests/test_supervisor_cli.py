@@ -151,3 +151,54 @@ def test_backup(tmp_path):
     files = backup.backup(str(tmp_path), stamp="2026101512")
     assert any(f.endswith("apmbackend_amd/runtime/service.py.2026101512") for f in files)
     assert any(f.endswith("config/apm_config.json.2026101512") for f in files)
+
+
+def test_rank_group_elastic_degrade(tmp_path):
+    """A GPU whose rank keeps failing is retired: 4 GPUs -> 3 healthy -> world 2 (powers of two),
+    HIP_VISIBLE_DEVICES / WORLD_SIZE / MASTER_PORT of the new generation, alert + annotation."""
+    r = script(tmp_path, "rank.py", "import os\n"
+                                    "if os.environ['APM_DEVICE']=='1': sys.exit(2)\n"
+                                    "time.sleep(60)\n")
+    C = make_cfg(tmp_path, [{"name": "engine", "relativePath": r, "ranks": 4, "passConfig": False,
+                             "masterPort": 29600}],
+                 crashLoopWindowSeconds=0.0, restartDelaySeconds=0.05, elasticMaxFailures=3,
+                 elasticWindowSeconds=600)
+    notes = []
+    s = sup.Supervisor(C, mailer=Mailer(sendmail="/nonexistent", outbox=str(tmp_path / "out")),
+                       annotate=lambda g, text, tags: notes.append(text))
+    s.start_all()
+    mod = s.modules[0]
+    try:
+        assert [p.env["APM_DEVICE"] for p in mod.procs] == ["0", "1", "2", "3"]
+        assert "HIP_VISIBLE_DEVICES" not in mod.procs[0].env
+        assert wait_for(lambda: (s.check_children() or True) and mod.generation == 1, timeout=20)
+        assert mod.bad_devices == {1} and mod.ranks == 2
+        assert [p.env["WORLD_SIZE"] for p in mod.procs] == ["2", "2"]
+        assert all(p.env["HIP_VISIBLE_DEVICES"] == "0,2" for p in mod.procs)
+        assert [p.env["APM_DEVICE"] for p in mod.procs] == ["0", "2"]
+        assert mod.procs[0].env["MASTER_PORT"] == "29601"
+        assert any("degraded from 4 to 2 GPUs" in n for n in notes)
+        assert any("degraded from 4 to 2 GPUs" in a for a in s.alert_buffer)
+        # the new generation starts and stays up (device 1 is no longer used)
+        assert wait_for(lambda: (s.check_children() or True) and all(p.popen is not None for p in mod.procs))
+        time.sleep(0.3)
+        s.check_children()
+        assert all(p.poll() is None for p in mod.procs) and mod.generation == 1
+    finally:
+        s.stop_all()
+
+
+def test_elastic_degrade_can_be_disabled(tmp_path):
+    r = script(tmp_path, "rank.py", "sys.exit(2)\n")
+    C = make_cfg(tmp_path, [{"name": "engine", "relativePath": r, "ranks": 2, "passConfig": False,
+                             "elasticDegrade": False}],
+                 crashLoopWindowSeconds=0.0, restartDelaySeconds=0.05, elasticMaxFailures=1)
+    s = sup.Supervisor(C, mailer=Mailer(sendmail="/nonexistent", outbox=str(tmp_path / "out")),
+                       annotate=lambda *a: None)
+    s.start_all()
+    mod = s.modules[0]
+    try:
+        assert wait_for(lambda: (s.check_children() or True) and mod.procs[0].restarts >= 1)
+        assert mod.generation == 0 and mod.ranks == 2 and not mod.bad_devices
+    finally:
+        s.stop_all()
