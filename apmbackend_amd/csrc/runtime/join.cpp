@@ -663,6 +663,19 @@ void JoinShard::on_app(const Event& e, std::string_view line, int32_t file, uint
 // CommonTiming event will probe, requested kLookahead events before the event is handled.
 void JoinShard::prefetch_event(const Event& e, const uint8_t* bytes) {
   const uint8_t k = e.kind;
+  if (k == LK_SOAP) {
+    // A request line opens the SOAP context whose account line (a few lines later) writes
+    // acct_[logId] and probes need_[logId]: two random misses that nothing else prefetches
+    if ((e.mask & (PM_SOAP_IN | PM_HOST)) != PM_SOAP_IN || e.ntok < 2) return;
+    const std::string_view t1((const char*)bytes + e.off + e.t1s, (size_t)(e.t1e - e.t1s));
+    const size_t eq = t1.find('=');
+    if (eq == std::string_view::npos) return;
+    const size_t eq2 = t1.find('=', eq + 1);
+    const uint64_t key = key_of(t1.substr(eq + 1, eq2 == std::string_view::npos ? std::string_view::npos : eq2 - eq - 1));
+    acct_.prefetch(key);
+    need_.prefetch(key);
+    return;
+  }
   if (k < LK_EJB_ENTRY || k > LK_CT_EXIT || (e.mask & PM_HOST) || e.ntok == 0) return;
   if (e.mask & PM_KEYS) {  // hashed on the GPU
     record_.prefetch(e.key);
