@@ -78,15 +78,19 @@ __global__ __launch_bounds__(256) void k_zscore_resync(ZArgs a) {
   a.rs_cnt[o] = c;
 }
 
+// One thread per (series, stat): grid (ceil(n/256), NSTAT).  The three stats of a series are
+// independent recurrences, and a thread per series left ~1.2 waves per SIMD at 80k series --
+// too few to hide the HBM latency of its five moment loads + ring row per stat (73 us per LAG
+// at 80k series before the split).  k_zscore_commit then publishes `valid` and bumps the list
+// length (every stat thread must read the old length first).
 template <typename T>
 __global__ __launch_bounds__(256) void k_zscore(ZArgs a) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = blockIdx.y;
   if (s >= a.n_series) return;
   const WinStat w = a.win[s];
-  ZOut o;
-  o.valid = 0;
-  if (!w.active) { a.out[s] = o; return; }
-  o.valid = 1;
+  if (!w.active) return;
+  ZOut* const op = a.out + s;
   const int L = a.lag;
   const int S = a.S;
   const int n = a.len[s];
@@ -98,9 +102,7 @@ __global__ __launch_bounds__(256) void k_zscore(ZArgs a) {
   const int oldest = (head - n + L) % L;
   const bool exact = a.exact != 0;
   const bool resync = !exact && s >= a.rs_lo && s < a.rs_lo + a.rs_n;
-  const double xs[NSTAT] = {w.avg, w.p75, w.p95};
-#pragma unroll
-  for (int k = 0; k < NSTAT; ++k) {
+  {
     T* col = ring + (size_t)k * L * S + s;  // element pos at col[pos * S]
     double sum = a.sum[k * S + s], comp = a.comp[k * S + s];
     int c = a.cnt[k * S + s];
@@ -127,7 +129,7 @@ __global__ __launch_bounds__(256) void k_zscore(ZArgs a) {
       }
       sum = es; comp = 0.0; c = ec; sq = eq; sqc = 0.0;
     }
-    const double x = xs[k];
+    const double x = k == 0 ? w.avg : (k == 1 ? w.p75 : w.p95);
     double stored = x;
     double mean = apm_nan(), lb = apm_nan(), ub = apm_nan();
     int sig = 0;
@@ -165,10 +167,20 @@ __global__ __launch_bounds__(256) void k_zscore(ZArgs a) {
     if (valid(sv)) { neumaier(sum, comp, sv); neumaier(sq, sqc, sv * sv); ++c; }
     a.sum[k * S + s] = sum; a.comp[k * S + s] = comp; a.cnt[k * S + s] = c;
     a.sumsq[k * S + s] = sq; a.sqcomp[k * S + s] = sqc;
-    o.mean[k] = mean; o.lb[k] = lb; o.ub[k] = ub; o.sig[k] = (int8_t)sig;
+    op->mean[k] = mean; op->lb[k] = lb; op->ub[k] = ub; op->sig[k] = (int8_t)sig;
   }
-  a.len[s] = n < L ? n + 1 : L;
-  a.out[s] = o;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_zscore_commit(ZArgs a) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= a.n_series) return;
+  const bool act = a.win[s].active != 0;
+  a.out[s].valid = act ? 1 : 0;
+  if (act) {
+    const int n = a.len[s];
+    a.len[s] = n < a.lag ? n + 1 : a.lag;
+  }
 }
 
 // Warm start: fill a lag's ring with a synthetic pre-history (per-series baseline * jitter)
@@ -263,7 +275,8 @@ void launch_zscore(ZArgs* a, hipStream_t stream) {
     const dim3 g((a->rs_n + 63) / 64, (a->rs_parts + 3) / 4, NSTAT), b(64, 4);
     hipLaunchKernelGGL(k_zscore_resync<T>, g, b, 0, stream, *a);
   }
-  hipLaunchKernelGGL(k_zscore<T>, dim3((a->n_series + 255) / 256), dim3(256), 0, stream, *a);
+  hipLaunchKernelGGL(k_zscore<T>, dim3((a->n_series + 255) / 256, NSTAT), dim3(256), 0, stream, *a);
+  hipLaunchKernelGGL(k_zscore_commit<T>, dim3((a->n_series + 255) / 256), dim3(256), 0, stream, *a);
 }
 
 }  // namespace apm

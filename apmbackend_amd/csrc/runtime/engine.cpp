@@ -988,13 +988,24 @@ void Engine::release_gather(int k, int64_t released) {
   std::string& out = blob_[OUT_DB];
   uint32_t cur_id = UINT32_MAX;
   LineBlock* cur = nullptr;
+  // Released lines arrive in endTs order, so consecutive ones hop between the blocks of every
+  // shard and batch still pending (32 shards x ~20 batches for the firehose shard).  A
+  // direct-mapped cache of block pointers keeps the locked map lookup to once per block per
+  // release instead of once per line (60k lock + find per batch made this lane the bottleneck).
+  struct BlockSlot { uint32_t id = UINT32_MAX; LineBlock* b = nullptr; };
+  std::vector<BlockSlot> cache(1024);
   for (int64_t i = 0; i < released; ++i) {
     const uint64_t g = (uint64_t)gids[i];
     const uint32_t id = (uint32_t)(g >> 44);
     if (id != cur_id) {
-      std::lock_guard<std::mutex> lk(blocks_mu_);
-      auto it = line_blocks_.find(id);
-      cur = it == line_blocks_.end() ? nullptr : &it->second;  // element references survive rehash
+      BlockSlot& sl = cache[id & 1023u];
+      if (sl.id != id) {
+        std::lock_guard<std::mutex> lk(blocks_mu_);
+        auto it = line_blocks_.find(id);
+        sl.b = it == line_blocks_.end() ? nullptr : &it->second;  // element references survive rehash
+        sl.id = id;
+      }
+      cur = sl.b;
       cur_id = id;
     }
     if (!cur) continue;
@@ -1010,6 +1021,7 @@ void Engine::release_gather(int k, int64_t released) {
         line_blocks_.erase(cur_id);
       }
       recycle_arena(std::move(data));
+      cache[cur_id & 1023u] = BlockSlot{};
       cur = nullptr;
       cur_id = UINT32_MAX;
     }
