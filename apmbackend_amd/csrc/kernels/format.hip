@@ -77,12 +77,14 @@ __device__ __forceinline__ void head(Out& o, const char* tag, const FormatArgs& 
   o.c('|');
 }
 
+// st_dst / fs_dst: where this series' lines go (nullptr in the length pass)
 template <bool WRITE>
-__device__ void format_series(const FormatArgs& a, int32_t i, uint32_t* st_len, uint32_t* fs_len, bool& fb) {
+__device__ void format_series(const FormatArgs& a, int32_t i, char* st_dst, char* fs_dst, uint32_t* st_len,
+                              uint32_t* fs_len, bool& fb) {
   const int32_t s = a.perm[i];
   const WinStat w = a.win[s];
-  Out st{WRITE ? a.st_out + a.st_off[i] : nullptr};
-  Out fs{WRITE ? a.fs_out + a.fs_off[i] : nullptr};
+  Out st{WRITE ? st_dst : nullptr};
+  Out fs{WRITE ? fs_dst : nullptr};
   if (w.active) {
     if (a.want_st) {
       head(st, "st|", a, s);
@@ -121,15 +123,54 @@ __global__ __launch_bounds__(256) void k_format_len(FormatArgs a) {
   const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.n) return;
   bool fb = false;
-  format_series<false>(a, i, a.st_len, a.fs_len, fb);
+  format_series<false>(a, i, nullptr, nullptr, a.st_len, a.fs_len, fb);
   if (fb) atomicOr(a.fallback, 1);
 }
 
-__global__ __launch_bounds__(256) void k_format_write(FormatArgs a) {
-  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.n) return;
-  bool fb = false;
-  format_series<true>(a, i, nullptr, nullptr, fb);
+// Write pass, one wave per 64 consecutive series (emission order), so the wave's output is one
+// contiguous byte range per stream.  Each lane formats its lines into LDS at the same offset
+// modulo 4 as in the output, then the wave copies the range out with one dword per lane per
+// store (256 B per store instruction).  Formatting straight to HBM issued one single-byte store
+// per character with the 64 lanes ~300 B apart: 64 partial cache lines per instruction
+// (131 us for 25 MB at 80k series).  A block whose range does not fit the LDS stage (very long
+// names) writes directly, as before.
+constexpr int FMT_WAVE_SERIES = 64;
+constexpr uint32_t FMT_LDS_ST = 6144, FMT_LDS_FS = 24576;
+
+__device__ __forceinline__ void wave_copy_out(const char* __restrict__ lds, char* __restrict__ out, uint32_t g0,
+                                              uint32_t g1) {
+  const uint32_t a0 = g0 & ~3u;
+  const uint32_t nd = (g1 - a0 + 3) / 4;
+  for (uint32_t d = threadIdx.x; d < nd; d += FMT_WAVE_SERIES) {
+    const uint32_t ga = a0 + 4 * d;
+    if (ga >= g0 && ga + 4 <= g1) {
+      *reinterpret_cast<uint32_t*>(out + ga) = *reinterpret_cast<const uint32_t*>(lds + 4 * d);
+    } else {  // the block's first / last dword is shared with a neighbour: byte stores
+      for (uint32_t b = 0; b < 4; ++b)
+        if (ga + b >= g0 && ga + b < g1) out[ga + b] = lds[4 * d + b];
+    }
+  }
+}
+
+__global__ __launch_bounds__(FMT_WAVE_SERIES) void k_format_write(FormatArgs a) {
+  __shared__ __align__(16) char sst[FMT_LDS_ST];
+  __shared__ __align__(16) char sfs[FMT_LDS_FS];
+  const int32_t i0 = blockIdx.x * FMT_WAVE_SERIES;
+  const int32_t i1 = min(a.n, i0 + FMT_WAVE_SERIES);
+  const int32_t i = i0 + (int32_t)threadIdx.x;
+  const uint32_t st0 = a.st_off[i0], st1 = a.st_off[i1];
+  const uint32_t fs0 = a.fs_off[i0], fs1 = a.fs_off[i1];
+  const bool st_lds = (st1 - (st0 & ~3u)) <= FMT_LDS_ST;  // uniform across the block
+  const bool fs_lds = (fs1 - (fs0 & ~3u)) <= FMT_LDS_FS;
+  if (i < i1) {
+    bool fb = false;
+    char* stp = st_lds ? sst + (a.st_off[i] - (st0 & ~3u)) : a.st_out + a.st_off[i];
+    char* fsp = fs_lds ? sfs + (a.fs_off[i] - (fs0 & ~3u)) : a.fs_out + a.fs_off[i];
+    format_series<true>(a, i, stp, fsp, nullptr, nullptr, fb);
+  }
+  __syncthreads();
+  if (st_lds) wave_copy_out(sst, a.st_out, st0, st1);
+  if (fs_lds) wave_copy_out(sfs, a.fs_out, fs0, fs1);
 }
 
 __global__ void k_fixed_batch(const double* x, int n, int f, char* out) {
@@ -181,7 +222,8 @@ void apm_format_fixed_batch(const double* d_x, int n, int f, char* d_out, hipStr
 
 void apm_format_write(FormatArgs* a, hipStream_t stream) {
   if (a->n <= 0) return;
-  hipLaunchKernelGGL(k_format_write, dim3((a->n + 255) / 256), dim3(256), 0, stream, *a);
+  hipLaunchKernelGGL(k_format_write, dim3((a->n + FMT_WAVE_SERIES - 1) / FMT_WAVE_SERIES), dim3(FMT_WAVE_SERIES),
+                     0, stream, *a);
 }
 
 }  // extern "C"
