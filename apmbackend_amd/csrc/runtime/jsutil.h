@@ -63,7 +63,13 @@ inline std::string_view trim(std::string_view s) {
   const uint8_t* p = (const uint8_t*)s.data();
   const uint8_t* e = p + s.size();
   while (p < e) { int w = ws_len(p, e); if (!w) break; p += w; }
-  // right trim: walk forward remembering the last non-ws end
+  // right trim, ASCII fast path: drop ASCII whitespace from the end; the first non-whitespace
+  // ASCII byte ends the string.  A non-ASCII byte at the end (possibly the tail of a multi-byte
+  // whitespace such as U+00A0 / U+FEFF) falls back to the exact forward walk over [p, e).
+  while (e > p && e[-1] < 0x80) {
+    if (ws_len(e - 1, e) == 0) return std::string_view((const char*)p, e - p);
+    --e;
+  }
   const uint8_t* q = p;
   const uint8_t* last = p;
   while (q < e) { int w = ws_len(q, e); if (w) q += w; else { ++q; last = q; } }
