@@ -94,3 +94,17 @@ def test_parallel_join_under_tsan(tmp_path):
     assert r.returncode == 0, r.stderr[-4000:]
     assert "WARNING: ThreadSanitizer" not in r.stderr
     assert r.stdout.splitlines() == want
+
+
+def test_js_trim_fast_path_matches_code_point_walk(tmp_path):
+    """js::trim's ASCII right-trim fast path == the exact code-point walk (random byte mixes
+    of ASCII, JS Unicode whitespace and broken UTF-8), under ASan + UBSan."""
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    exe = str(tmp_path / "jsutil_fuzz")
+    cmd = [hipcc, "-O1", "-g", "-std=c++17", "--offload-arch=gfx950", "-Xarch_host", "-fsanitize=address",
+           "-Xarch_host", "-fsanitize=undefined", "-Xarch_host", "-fno-sanitize-recover=all", "-I", CSRC,
+           os.path.join(ROOT, "tests", "native", "jsutil_fuzz.cpp"), "-o", exe, "-fsanitize=address,undefined"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = subprocess.run([exe, "300000"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr[-2000:]
