@@ -679,6 +679,48 @@ void Engine::finish_parse(ParseSlot& ps) {
   metrics_.t_parse_ms += now_ms() - t0;
 }
 
+// Merge the shard outputs into the reference's single-stream order.  Cache-expiry emissions
+// (seq bit 63 clear, keyed by creation) precede every line emission and may interleave across
+// shards: k-way merge (rare).  Line emissions are keyed by the global line index, and each
+// shard's lines form one contiguous range (chunks are grouped by server), so those parts are
+// concatenated in range order; `multi` (a server with several line ranges in the batch) sorts
+// the line part by its (line, sub) key instead.
+static void merge_shard_outputs(const std::vector<std::vector<TxOut>>& outs, bool multi, std::vector<TxOut>& txs) {
+  txs.clear();
+  const int ns = (int)outs.size();
+  size_t total = 0;
+  std::vector<size_t> split(ns, 0);
+  for (int k = 0; k < ns; ++k) {
+    auto& v = outs[k];
+    total += v.size();
+    size_t p = 0;
+    while (p < v.size() && !(v[p].seq >> 63)) ++p;
+    split[k] = p;
+  }
+  txs.reserve(total);
+  using Item = std::pair<uint64_t, std::pair<int, size_t>>;
+  std::priority_queue<Item, std::vector<Item>, std::greater<Item>> pq;
+  for (int k = 0; k < ns; ++k)
+    if (split[k] > 0) pq.push({outs[k][0].seq, {k, 0}});
+  while (!pq.empty()) {
+    auto it = pq.top();
+    pq.pop();
+    auto& v = outs[it.second.first];
+    txs.push_back(v[it.second.second]);
+    const size_t nx = it.second.second + 1;
+    if (nx < split[it.second.first]) pq.push({v[nx].seq, {it.second.first, nx}});
+  }
+  std::vector<int> order;
+  for (int k = 0; k < ns; ++k)
+    if (split[k] < outs[k].size()) order.push_back(k);
+  std::sort(order.begin(), order.end(), [&](int a, int b) { return outs[a][split[a]].seq < outs[b][split[b]].seq; });
+  const size_t line_part = txs.size();
+  for (int k : order) txs.insert(txs.end(), outs[k].begin() + (ptrdiff_t)split[k], outs[k].end());
+  if (multi)
+    std::stable_sort(txs.begin() + (ptrdiff_t)line_part, txs.end(),
+                     [](const TxOut& a, const TxOut& b) { return a.seq < b.seq; });
+}
+
 void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const std::vector<Chunk>& chunks_in,
                            double now_override, const uint8_t* next_bytes, uint64_t next_n,
                            const std::vector<Chunk>* next_chunks) {
@@ -757,61 +799,28 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
     metrics_.t_shard_busy_ms += shards_.empty() ? 0 : sum / shards_.size();
     metrics_.t_shard_max_ms += mx;
   }
-  // Merge the shard outputs into the reference's single-stream order.  Cache-expiry emissions
-  // (seq bit 63 clear, keyed by creation) precede every line emission and may interleave across
-  // shards: k-way merge (rare).  Line emissions are keyed by the global line index, and each
-  // shard's lines form one contiguous range (chunks are grouped by server), so those parts are
-  // concatenated in range order.
-  std::vector<TxOut> txs;
+  // Hand the shard outputs over as they are (swapped out, the shards get recycled vectors back):
+  // the stats thread merges them into the single-stream order (merge_shard_outputs), which
+  // takes ~0.15 ms of copying off this thread's critical path.
+  std::vector<std::vector<TxOut>> outs(shards_.size());
   {
-    const int ns = (int)shards_.size();
-    size_t total = 0;
-    std::vector<size_t> split(ns, 0);
-    for (int k = 0; k < ns; ++k) {
-      auto& v = shards_[k]->out();
-      total += v.size();
-      size_t p = 0;
-      while (p < v.size() && !(v[p].seq >> 63)) ++p;
-      split[k] = p;
+    std::lock_guard<std::mutex> g(out_pool_mu_);
+    for (size_t k = 0; k < shards_.size(); ++k) {
+      outs[k].swap(shards_[k]->out());
+      if (!out_pool_.empty()) {
+        shards_[k]->out().swap(out_pool_.back());
+        out_pool_.pop_back();
+      }
     }
-    txs.reserve(total);
-    using Item = std::pair<uint64_t, std::pair<int, size_t>>;
-    std::priority_queue<Item, std::vector<Item>, std::greater<Item>> pq;
-    for (int k = 0; k < ns; ++k)
-      if (split[k] > 0) pq.push({shards_[k]->out()[0].seq, {k, 0}});
-    while (!pq.empty()) {
-      auto it = pq.top();
-      pq.pop();
-      auto& v = shards_[it.second.first]->out();
-      txs.push_back(v[it.second.second]);
-      const size_t nx = it.second.second + 1;
-      if (nx < split[it.second.first]) pq.push({v[nx].seq, {it.second.first, nx}});
-    }
-    std::vector<int> order;
-    for (int k = 0; k < ns; ++k)
-      if (split[k] < shards_[k]->out().size()) order.push_back(k);
-    std::sort(order.begin(), order.end(), [&](int a, int b) {
-      return shards_[a]->out()[split[a]].seq < shards_[b]->out()[split[b]].seq;
-    });
-    const size_t line_part = txs.size();
-    for (int k : order) {
-      auto& v = shards_[k]->out();
-      txs.insert(txs.end(), v.begin() + split[k], v.end());
-    }
-    // a server whose chunks are not contiguous in the batch has several line ranges: order the
-    // line emissions by their (line, sub) key
-    bool multi = false;
-    for (auto& r : shard_range) multi |= r.size() > 1;
-    if (multi)
-      std::stable_sort(txs.begin() + (ptrdiff_t)line_part, txs.end(),
-                       [](const TxOut& a, const TxOut& b) { return a.seq < b.seq; });
   }
+  bool multi = false;
+  for (auto& r : shard_range) multi |= r.size() > 1;
   const double t2 = now_ms();
   metrics_.t_join_ms += t2 - t1;
   metrics_.t_merge_ms += t2 - t1b;
   roctxRangePop();
   trace_event("join", t1, t1b, 0);
-  trace_event("merge", t1b, t2, 0);
+  trace_event("handoff", t1b, t2, 0);
 
   // advance the watermark clock (max leading timestamp seen so far)
   const unsigned long long wm = *ps.h_watermark;
@@ -820,11 +829,11 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
     if (w > watermark_) watermark_ = w;
   }
   // lock-step: node-wide watermark (cache clock of the next batch) and newest bucket
-  if (lockstep_) lockstep_sync(txs);
+  if (lockstep_) lockstep_sync(outs);
 
   // ---- stats / z-score / alerts: handed to the stats thread, overlapping the next batch's
   // H2D + parse (parse stream) and host join (pool) with this batch's GPU stats work.
-  post_stats(std::move(txs), t0, lockstep_ ? sync_latest_ : INT64_MIN);
+  post_stats(std::move(outs), multi, t0, lockstep_ ? sync_latest_ : INT64_MIN);
   // post_stats returned: the stats thread finished (and packed) every earlier batch
   if (fleet_comm_) fleet_exchange_upto(fleet_posted_ - 1);
   metrics_.t_total_ms += now_ms() - t0;
@@ -858,7 +867,8 @@ void Engine::stats_worker() {
       std::unique_lock<std::mutex> lk(st_mu_);
       st_cv_.wait(lk, [&]() { return st_stop_ || st_has_job_; });
       if (st_stop_ && !st_has_job_) return;
-      job.txs.swap(st_job_.txs);
+      job.outs.swap(st_job_.outs);
+      job.multi = st_job_.multi;
       job.text.swap(st_job_.text);
       job.t0 = st_job_.t0;
       job.sync_latest = st_job_.sync_latest;
@@ -868,6 +878,17 @@ void Engine::stats_worker() {
     roctxRangePushA("apm.stats");
     try {
       cur_text_ = &job.text;
+      const double tm = now_ms();
+      merge_shard_outputs(job.outs, job.multi, job.txs);
+      trace_event("merge", tm, now_ms(), 1);
+      {  // the shard vectors go back to the ingest thread with their capacity
+        std::lock_guard<std::mutex> g(out_pool_mu_);
+        for (auto& v : job.outs) {
+          v.clear();
+          if (out_pool_.size() < 2 * shards_.size() + 4) out_pool_.push_back(std::move(v));
+        }
+        job.outs.clear();
+      }
       stats_for_batch(job.txs, job.t0);
       apply_latest_locked(job.sync_latest, job.t0);
       fleet_pack_locked();
@@ -887,7 +908,7 @@ void Engine::stats_worker() {
   }
 }
 
-void Engine::post_stats(std::vector<TxOut>&& txs, double t0, int64_t sync_latest) {
+void Engine::post_stats(std::vector<std::vector<TxOut>>&& outs, bool multi, double t0, int64_t sync_latest) {
   std::unique_lock<std::mutex> lk(st_mu_);
   st_cv_.wait(lk, [&]() { return !st_busy_; });
   if (!st_error_.empty()) { std::string e = st_error_; st_error_.clear(); throw std::runtime_error(e); }
@@ -895,7 +916,8 @@ void Engine::post_stats(std::vector<TxOut>&& txs, double t0, int64_t sync_latest
     std::lock_guard<std::mutex> g(out_mu_);
     if (!out_error_.empty()) { std::string e = out_error_; out_error_.clear(); throw std::runtime_error(e); }
   }
-  st_job_.txs = std::move(txs);
+  st_job_.outs = std::move(outs);
+  st_job_.multi = multi;
   // hand the shards' formatted tx lines to the stats thread; the shards get the previous
   // batch's (consumed) arenas back and reuse their capacity
   st_job_.text.resize(shards_.size());
@@ -1788,14 +1810,15 @@ void Engine::coll_wait(hipStream_t s, hipEvent_t ev, const char* what) {
 // the next batch, and the node-wide newest bucket decides this batch's rollovers.  The bucket is
 // the one stats_for_batch derives (non-db tx with a usable endTs), so ranks agree on `latest`
 // without the stats thread touching the communicator.
-void Engine::lockstep_sync(const std::vector<TxOut>& txs) {
+void Engine::lockstep_sync(const std::vector<std::vector<TxOut>>& outs) {
   if (comm_aborted_) throw std::runtime_error("RCCL communicator was aborted");
   int64_t b = sync_latest_;
-  for (const TxOut& t : txs) {
-    if (t.to_db || !(t.end_ms == t.end_ms) || t.end_ms < 10000) continue;
-    const int64_t tb = (int64_t)t.end_ms / 10000;
-    if (tb > b) b = tb;
-  }
+  for (const auto& v : outs)
+    for (const TxOut& t : v) {
+      if (t.to_db || !(t.end_ms == t.end_ms) || t.end_ms < 10000) continue;
+      const int64_t tb = (int64_t)t.end_ms / 10000;
+      if (tb > b) b = tb;
+    }
   h_sync_[0] = watermark_;
   h_sync_[1] = b == INT64_MIN ? -1.0 : (double)b;  // buckets < 2^53: exact in a double
   HIP_OK(hipMemcpyAsync(d_sync_, h_sync_, 16, hipMemcpyHostToDevice, coll_stream_));

@@ -290,10 +290,10 @@ class Engine {
   void fleet_exchange_upto(uint64_t rounds);
   void coll_check(ncclResult_t r, const char* what);
   void coll_wait(hipStream_t s, hipEvent_t ev, const char* what);
-  void lockstep_sync(const std::vector<TxOut>& txs);
+  void lockstep_sync(const std::vector<std::vector<TxOut>>& outs);
   void apply_latest_locked(int64_t g, double batch_t0);
   void stats_worker();
-  void post_stats(std::vector<TxOut>&& txs, double t0, int64_t sync_latest = INT64_MIN);
+  void post_stats(std::vector<std::vector<TxOut>>&& outs, bool multi, double t0, int64_t sync_latest = INT64_MIN);
   void drain_sinks(uint32_t kinds = ~0u);
   void drain_kind(int k);
   // output lane (see engine.cpp): waits for the D2H of released-tx ids / formatted text and
@@ -332,6 +332,8 @@ class Engine {
   uint64_t fleet_packed_ = 0;  // batches packed (stats thread)
   // stats thread
   struct StatsJob {
+    std::vector<std::vector<TxOut>> outs;  // per shard, merged by the stats thread into txs
+    bool multi = false;
     std::vector<TxOut> txs; std::vector<std::string> text; double t0 = 0;
     int64_t sync_latest = INT64_MIN;  // lock-step: node-wide newest bucket after this batch
   };
@@ -340,6 +342,8 @@ class Engine {
   std::mutex st_mu_;
   std::condition_variable st_cv_;
   StatsJob st_job_;
+  std::vector<std::vector<TxOut>> out_pool_;  // emptied shard output vectors (capacity kept)
+  std::mutex out_pool_mu_;
   bool st_has_job_ = false, st_busy_ = false, st_stop_ = false;
   std::string st_error_;
   // output lane: FIFO of emit tasks; it owns the db / st / fs streams (kLaneKinds)
