@@ -362,9 +362,9 @@ PYBIND11_MODULE(_apm_native, m) {
         return py::bytes((const char*)v.data(), v.size() * 8);
       })
       .def("fleet_rounds", &Engine::fleet_rounds)
-      .def("pack_service_moments", [](Engine& e, uintptr_t dst, int32_t cap) {
-        e.pack_service_moments((double*)dst, cap, e.comm_stream());
-      })
+      .def("pack_service_moments", [](Engine& e, uintptr_t dst, int32_t cap, bool atomic_path) {
+        e.pack_service_moments((double*)dst, cap, e.comm_stream(), atomic_path);
+      }, py::arg("dst"), py::arg("cap"), py::arg("atomic_path") = false)
       .def("winstats", [](Engine& e) {
         std::vector<WinStat> w;
         e.download_winstats(w);

@@ -425,6 +425,7 @@ void Engine::load_state(const std::string& path) {
     perm_dirty_ = true;
     h_perm_.clear();
     series_service_uploaded_ = 0;
+    svc_csr_n_ = -1;
   }
   const int32_t n = n_series_;
 

@@ -392,6 +392,7 @@ Engine::~Engine() {
     hipHostFree(ps.h_events); hipHostFree(ps.h_counts); hipHostFree(ps.h_watermark);
   }
   hipHostFree(h_alerts_);
+  if (h_series_service_) hipHostFree(h_series_service_);
   hipHostFree(h_n_alerts_); hipHostFree(h_tx_); hipHostFree(h_gid_);
   for (int k = 0; k < 2; ++k) {
     hipHostFree(h_release_gid_[k]);
@@ -829,13 +830,21 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
     if (w > watermark_) watermark_ = w;
   }
   // lock-step: node-wide watermark (cache clock of the next batch) and newest bucket
-  if (lockstep_) lockstep_sync(outs);
+  if (lockstep_) {
+    const double tl = now_ms();
+    lockstep_sync(outs);
+    trace_event("lockstep", tl, now_ms(), 0);
+  }
 
   // ---- stats / z-score / alerts: handed to the stats thread, overlapping the next batch's
   // H2D + parse (parse stream) and host join (pool) with this batch's GPU stats work.
+  const double tp0 = now_ms();
   post_stats(std::move(outs), multi, t0, lockstep_ ? sync_latest_ : INT64_MIN);
+  const double tp1 = now_ms();
+  trace_event("post", tp0, tp1, 0);
   // post_stats returned: the stats thread finished (and packed) every earlier batch
   if (fleet_comm_) fleet_exchange_upto(fleet_posted_ - 1);
+  trace_event("fleet.exchange", tp1, now_ms(), 0);
   metrics_.t_total_ms += now_ms() - t0;
   ++batch_no_;
 }
@@ -1704,27 +1713,70 @@ uintptr_t Engine::alloc_pinned(size_t n) {
 
 void Engine::free_pinned(uintptr_t p) { hipHostFree((void*)p); }
 
-void Engine::pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream) {
+void Engine::pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream, bool atomic_path) {
   // series -> service table (grows with the dictionary): upload only the new tail
   if (series_service_uploaded_ < n_series_) {
+    // Pinned host mirror of the table: the series list is append-only, so each upload reads a
+    // region no earlier (possibly still in-flight) copy reads -- no stream sync on the stats thread.
     const int32_t lo = series_service_uploaded_;
-    std::vector<int32_t> sv(n_series_ - lo);
-    for (int32_t s = lo; s < n_series_; ++s) sv[s - lo] = series_[s].service;
-    HIP_OK(hipMemcpyAsync(d_series_service_ + lo, sv.data(), sv.size() * 4, hipMemcpyHostToDevice, stream_));
-    HIP_OK(hipStreamSynchronize(stream_));
+    if (!h_series_service_) {
+      void* p = nullptr;
+      HIP_OK(hipHostMalloc(&p, (size_t)cfg_.max_series * 4, hipHostMallocDefault));
+      h_series_service_ = (int32_t*)p;
+    }
+    if (lo == 0) HIP_OK(hipStreamSynchronize(stream_));  // table reset (load_state): rewrite from 0
+    for (int32_t s = lo; s < n_series_; ++s) h_series_service_[s] = series_[s].service;
+    HIP_OK(hipMemcpyAsync(d_series_service_ + lo, h_series_service_ + lo, (size_t)(n_series_ - lo) * 4,
+                          hipMemcpyHostToDevice, stream_));
     series_service_uploaded_ = n_series_;
   }
   // the pack reads the z-score state written on the main stream: order comm after it
   HIP_OK(hipEventRecord(ev_a_, stream_));
   HIP_OK(hipStreamWaitEvent(stream, ev_a_, 0));
+  if (!atomic_path && cfg_.n_lags * NSTAT * 2 + 1 <= 16) {
+    // MFMA Gram path (fleet.hip): series listed per service (CSR).  Series added since the CSR
+    // snapshot are accumulated by the atomic kernel on top; the CSR is rebuilt (host pass + a
+    // stream sync) only when that tail exceeds 1/8 of the table, i.e. O(log n) times while the
+    // dictionary grows instead of on every batch that adds a series.
+    if (svc_csr_n_ < 0 || svc_csr_cap_ != cap || (int64_t)(n_series_ - svc_csr_n_) * 8 > n_series_) {
+      h_svc_off_.assign((size_t)cap + 1, 0);
+      for (int32_t s = 0; s < n_series_; ++s) {
+        const int32_t v = series_[s].service;
+        if (v >= 0 && v < cap) ++h_svc_off_[(size_t)v + 1];
+      }
+      for (int32_t v = 0; v < cap; ++v) h_svc_off_[(size_t)v + 1] += h_svc_off_[v];
+      h_svc_ids_.assign(std::max<size_t>(1, (size_t)h_svc_off_[cap]), 0);
+      std::vector<int32_t> pos(h_svc_off_.begin(), h_svc_off_.end() - 1);
+      for (int32_t s = 0; s < n_series_; ++s) {
+        const int32_t v = series_[s].service;
+        if (v >= 0 && v < cap) h_svc_ids_[(size_t)pos[v]++] = s;
+      }
+      trace_event("fleet.csr", now_ms(), now_ms(), 1);
+      HIP_OK(hipStreamSynchronize(stream));  // an earlier pack may still read the old lists
+      d_svc_off_ = (int32_t*)regrow(d_svc_off_, svc_off_cap_, h_svc_off_.size() * 4);
+      d_svc_ids_ = (int32_t*)regrow(d_svc_ids_, svc_ids_cap_, h_svc_ids_.size() * 4);
+      HIP_OK(hipMemcpyAsync(d_svc_off_, h_svc_off_.data(), h_svc_off_.size() * 4, hipMemcpyHostToDevice, stream));
+      HIP_OK(hipMemcpyAsync(d_svc_ids_, h_svc_ids_.data(), h_svc_ids_.size() * 4, hipMemcpyHostToDevice, stream));
+      svc_csr_n_ = n_series_;
+      svc_csr_cap_ = cap;
+    }
+    if (apm_service_gram(d_svc_off_, d_svc_ids_, d_active_, cap, cfg_.max_series, cfg_.n_lags,
+                         (const double* const*)d_lag_sum_ptrs_, (const double* const*)d_lag_comp_ptrs_,
+                         (const int32_t* const*)d_lag_cnt_ptrs_, d_dst, stream) == 0) {
+      apm_service_moments_tail(d_series_service_, d_active_, svc_csr_n_, n_series_, cfg_.max_series, cfg_.n_lags,
+                               cap, (const double* const*)d_lag_sum_ptrs_, (const double* const*)d_lag_comp_ptrs_,
+                               (const int32_t* const*)d_lag_cnt_ptrs_, d_dst, stream);
+      return;
+    }
+  }
   apm_service_moments(d_series_service_, d_active_, n_series_, cfg_.max_series, cfg_.n_lags, cap,
                       (const double* const*)d_lag_sum_ptrs_, (const double* const*)d_lag_comp_ptrs_,
                       (const int32_t* const*)d_lag_cnt_ptrs_, d_dst, stream);
 }
 
-void Engine::pack_service_moments(double* d_dst, int32_t cap, hipStream_t stream) {
+void Engine::pack_service_moments(double* d_dst, int32_t cap, hipStream_t stream, bool atomic_path) {
   flush();  // series tables are owned by the stats thread
-  pack_moments_locked(d_dst, cap, stream);
+  pack_moments_locked(d_dst, cap, stream, atomic_path);
 }
 
 // ---- native fleet exchange + lock-step clocks over RCCL --------------------------------------
@@ -1756,7 +1808,13 @@ void Engine::fleet_init(const std::vector<uint8_t>& uid, const std::vector<uint8
   HIP_OK(hipSetDevice(cfg_.device));
   if (ncclCommInitRank(&fleet_comm_, nranks, id, rank) != ncclSuccess)
     throw std::runtime_error("ncclCommInitRank failed");
-  HIP_OK(hipStreamCreateWithFlags(&coll_stream_, hipStreamNonBlocking));
+  // Highest priority: with GPU_MAX_HW_QUEUES = 4 the engine's streams share hardware queues, and
+  // the 16-byte clock collective the ingest thread waits for would otherwise queue behind the
+  // stats stream's 20 MB st/fs D2H blit.
+  int prio_lo = 0, prio_hi = 0;
+  HIP_OK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+  HIP_OK(hipStreamCreateWithPriority(&coll_stream_, hipStreamNonBlocking, prio_hi));
+  fleet_nranks_ = nranks;
   lockstep_ = !clock_uid.empty();
   if (lockstep_) {
     d_sync_ = (double*)dmalloc(64);
@@ -1819,6 +1877,10 @@ void Engine::lockstep_sync(const std::vector<std::vector<TxOut>>& outs) {
       const int64_t tb = (int64_t)t.end_ms / 10000;
       if (tb > b) b = tb;
     }
+  if (fleet_nranks_ == 1) {  // MAX over one rank is the identity: no device round trip
+    if (b != INT64_MIN) sync_latest_ = std::max(sync_latest_, b);
+    return;
+  }
   h_sync_[0] = watermark_;
   h_sync_[1] = b == INT64_MIN ? -1.0 : (double)b;  // buckets < 2^53: exact in a double
   HIP_OK(hipMemcpyAsync(d_sync_, h_sync_, 16, hipMemcpyHostToDevice, coll_stream_));
@@ -1843,7 +1905,9 @@ void Engine::fleet_pack_locked() {
   if (!fleet_comm_) return;
   const int slot = (int)(fleet_packed_ & 1);
   if (fleet_packed_ >= 2) HIP_OK(hipStreamWaitEvent(comm_stream_, fleet_ev_[slot], 0));
+  const double t0 = now_ms();
   pack_moments_locked(fleet_buf_[slot], fleet_cap_, comm_stream_);
+  trace_event("fleet.pack", t0, now_ms(), 1);
   HIP_OK(hipEventRecord(pack_ev_[slot], comm_stream_));
   ++fleet_packed_;
 }

@@ -230,7 +230,8 @@ class Engine {
   // Fleet baseline exchange: per-service moments packed into `dst` (device pointer, doubles,
   // layout [n_services][n_lags][NSTAT][3] = count, sum, sumsq of the current ring means).
   int32_t n_services() const { return dict_.n_services(); }
-  void pack_service_moments(double* d_dst, int32_t n_services_cap, hipStream_t stream);
+  // atomic_path: the per-series fp64 atomic scatter instead of the MFMA Gram kernel (tests)
+  void pack_service_moments(double* d_dst, int32_t n_services_cap, hipStream_t stream, bool atomic_path = false);
   // Native RCCL fleet exchange (see engine.cpp): rank 0 creates the id, every rank inits.
   static std::vector<uint8_t> fleet_unique_id();
   // clock_uid non-empty: lock-step clocks (node-wide watermark + rollover bucket) so N ranks
@@ -285,7 +286,7 @@ class Engine {
   void* regrow(void* old, size_t& cap, size_t need);
   void emit_bytes(int kind, const char* p, size_t n);
   void upload_series_tables(int32_t lo);
-  void pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream);
+  void pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream, bool atomic_path = false);
   void fleet_pack_locked();
   void fleet_exchange_upto(uint64_t rounds);
   void coll_check(ncclResult_t r, const char* what);
@@ -327,6 +328,7 @@ class Engine {
   double* fleet_buf_[2] = {nullptr, nullptr};
   hipEvent_t fleet_ev_[2] = {nullptr, nullptr};    // all-reduce of the slot done (coll stream)
   hipEvent_t pack_ev_[2] = {nullptr, nullptr};     // pack of the slot done (comm stream)
+  int fleet_nranks_ = 0;
   uint64_t fleet_rounds_ = 0;  // exchanges issued (ingest thread)
   uint64_t fleet_posted_ = 0;  // batches posted since fleet_init (ingest thread)
   uint64_t fleet_packed_ = 0;  // batches packed (stats thread)
@@ -466,6 +468,13 @@ class Engine {
   void* d_lag_cnt_ptrs_ = nullptr;
   int32_t* d_series_service_ = nullptr;
   int32_t series_service_uploaded_ = 0;
+  // series grouped by service (CSR) for the MFMA Gram pack; rebuilt when series are added
+  std::vector<int32_t> h_svc_off_, h_svc_ids_;
+  int32_t* d_svc_off_ = nullptr;
+  int32_t* d_svc_ids_ = nullptr;
+  size_t svc_off_cap_ = 0, svc_ids_cap_ = 0;
+  int32_t svc_csr_n_ = -1, svc_csr_cap_ = -1;
+  int32_t* h_series_service_ = nullptr;  // pinned mirror of d_series_service_ (append-only uploads)
   uint8_t* d_suppressed_ = nullptr;
   uint64_t* d_emit_key_ = nullptr;
 

@@ -62,7 +62,8 @@ class FleetBaseline:
         self.cap = int(max_services or engine.cfg.get("gpu", {}).get("maxServices", 1 << 16))
         native = type(engine.eng)
         obj = [(native.fleet_unique_id(), native.fleet_unique_id() if lockstep else b"") if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0, group=group)
+        if world > 1:  # a single rank needs no rendezvous (bench.py --gpus 1 runs the same per-rank work)
+            dist.broadcast_object_list(obj, src=0, group=group)
         uid, clock_uid = obj[0]
         engine.eng.fleet_init(uid, world, rank, self.cap, clock_uid)
 

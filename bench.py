@@ -9,7 +9,8 @@ warmed with a synthetic pre-history so both lags produce bounds) -> alert decisi
 One step = one ingest batch = 10 s of log time for every JVM of the shard (so every step
 contains one interval rollover).  The corpus is generated before the timed region into pinned
 host memory; the timed region covers H2D of the raw bytes, GPU parse, host join, GPU stats /
-z-score / alerts, and (N > 1) the RCCL all-reduce of the fleet-wide per-service baseline.
+z-score / alerts, and the RCCL all-reduce of the fleet-wide per-service baseline (MFMA Gram pack) with the
+lock-step clock collective -- at every N, including N = 1, so per-rank work is the same at every N.
 
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL over xGMI)
@@ -70,6 +71,8 @@ def main():
     ap.add_argument("--no-warm", action="store_true")
     ap.add_argument("--sink", default="/dev/null", help="file receiving the db_insert stream")
     ap.add_argument("--no-prefetch", action="store_true", help="disable the next-batch parse overlap")
+    ap.add_argument("--no-fleet", action="store_true",
+                    help="skip the fleet baseline exchange / lock-step clocks (always on by default, also at N=1)")
     ap.add_argument("--trace", default=None, help="write a Chrome trace of the pipeline stages (per rank)")
     args = ap.parse_args()
     for k, v in PRESETS[args.preset].items():  # a preset overrides the defaults it names
@@ -137,7 +140,9 @@ def main():
     del raw
     t_gen = time.time() - t_gen
 
-    fleet = FleetBaseline(eng, world, rank) if dist is not None else None
+    # The fleet exchange (MFMA per-service Gram pack + RCCL all-reduce) and the lock-step clock
+    # collective run at every N, so each rank does the same work at N = 1 and N = 8 (weak scaling).
+    fleet = None if args.no_fleet else FleetBaseline(eng, world, rank)
     if args.trace:
         eng.eng.set_trace(True)
 

@@ -177,6 +177,36 @@ def test_native_fleet_exchange_single_rank():
     np.testing.assert_allclose(got, want, rtol=0, atol=0)
 
 
+def test_fleet_moments_mfma_gram_matches_atomic_scatter():
+    """The MFMA per-service Gram pack (v_mfma_f64_16x16x4f64, one wave per service) yields the
+    same {n, sum, sum^2} per (service, LAG, stat) as the per-series fp64 atomic scatter, and is
+    bitwise reproducible across calls."""
+    lines, bl = synth_batches(5, duration=300, servers=3)
+    bl = list(bl)
+    C = small_cfg("rolling")
+    eng = APMEngine(C, keep_text=False)
+    cap = 64
+    n = cap * 2 * 3 * 3
+    half = len(bl) // 8
+    for now, chunks in bl[:half]:
+        eng.process_lines(chunks, now)
+    # snapshot the per-service CSR early: series added afterwards take the atomic tail path
+    early = torch.zeros((n,), dtype=torch.float64, device="cuda")
+    eng.eng.pack_service_moments(early.data_ptr(), cap)
+    for now, chunks in bl[half:]:
+        eng.process_lines(chunks, now)
+    bufs = [torch.full((n,), -1.0, dtype=torch.float64, device="cuda") for _ in range(3)]
+    eng.eng.pack_service_moments(bufs[0].data_ptr(), cap, atomic_path=True)
+    eng.eng.pack_service_moments(bufs[1].data_ptr(), cap)
+    eng.eng.pack_service_moments(bufs[2].data_ptr(), cap)
+    torch.cuda.synchronize()
+    ref, got, again = (b.cpu().numpy().reshape(cap, 2, 3, 3) for b in bufs)
+    assert ref[..., 0].sum() > 10  # series with baselines on both LAGs
+    np.testing.assert_array_equal(got[..., 0], ref[..., 0])            # counts: exact
+    np.testing.assert_allclose(got[..., 1:], ref[..., 1:], rtol=1e-12, atol=1e-9)
+    np.testing.assert_array_equal(got, again)                          # deterministic
+
+
 def test_gpu_to_fixed_matches_host():
     """K12 number printer (device) == js::to_fixed (host, verified against node) incl. ties."""
     N = _native.load()
