@@ -1,3 +1,4 @@
+#include <cstdlib>
 // apm::Engine implementation -- see engine.h.
 #include "engine.h"
 
@@ -1813,7 +1814,10 @@ void Engine::fleet_init(const std::vector<uint8_t>& uid, const std::vector<uint8
   // stats stream's 20 MB st/fs D2H blit.
   int prio_lo = 0, prio_hi = 0;
   HIP_OK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-  HIP_OK(hipStreamCreateWithPriority(&coll_stream_, hipStreamNonBlocking, prio_hi));
+  const char* pe = std::getenv("APM_COLL_PRIO");  // diagnostic: 0 = default-priority collective stream
+  HIP_OK(hipStreamCreateWithPriority(&coll_stream_, hipStreamNonBlocking, pe && pe[0] == '0' ? prio_lo : prio_hi));
+  const char* se = std::getenv("APM_FLEET_SKIP_SOLO");  // diagnostic: skip the one-rank (identity) all-reduce
+  fleet_skip_solo_ = nranks == 1 && se && se[0] == '1';
   fleet_nranks_ = nranks;
   lockstep_ = !clock_uid.empty();
   if (lockstep_) {
@@ -1918,7 +1922,8 @@ void Engine::fleet_exchange_upto(uint64_t rounds) {
   while (fleet_rounds_ < rounds) {
     const int slot = (int)(fleet_rounds_ & 1);
     HIP_OK(hipStreamWaitEvent(coll_stream_, pack_ev_[slot], 0));
-    coll_check(ncclAllReduce(fleet_buf_[slot], fleet_buf_[slot], fleet_elems_, ncclDouble, ncclSum, fleet_comm_,
+    if (!fleet_skip_solo_)
+      coll_check(ncclAllReduce(fleet_buf_[slot], fleet_buf_[slot], fleet_elems_, ncclDouble, ncclSum, fleet_comm_,
                              coll_stream_), "fleet moments");
     HIP_OK(hipEventRecord(fleet_ev_[slot], coll_stream_));
     ++fleet_rounds_;

@@ -329,6 +329,7 @@ class Engine {
   hipEvent_t fleet_ev_[2] = {nullptr, nullptr};    // all-reduce of the slot done (coll stream)
   hipEvent_t pack_ev_[2] = {nullptr, nullptr};     // pack of the slot done (comm stream)
   int fleet_nranks_ = 0;
+  bool fleet_skip_solo_ = false;
   uint64_t fleet_rounds_ = 0;  // exchanges issued (ingest thread)
   uint64_t fleet_posted_ = 0;  // batches posted since fleet_init (ingest thread)
   uint64_t fleet_packed_ = 0;  // batches packed (stats thread)
