@@ -783,12 +783,22 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
     }
   }
   shard_ms_.assign(shards_.size() * 16, 0.0);  // one cache line per shard
+  shard_maxb_.assign(shards_.size() * 8, INT64_MIN);
   pool_->run((int)shards_.size(), [&](int s) {
     const double ts0 = now_ms();
     JoinShard& sh = *shards_[s];
     sh.out().clear();
     sh.begin_batch(clock, batch_no_);
     for (const auto& r : shard_range[s]) sh.process(h_events + r.first, r.second - r.first, hb, chunk_file);
+    if (lockstep_) {  // newest 10 s bucket of this shard's tx, for the lock-step clock (scanned in parallel here)
+      int64_t b = INT64_MIN;
+      for (const TxOut& t : sh.out()) {
+        if (t.to_db || !(t.end_ms == t.end_ms) || t.end_ms < 10000) continue;
+        const int64_t tb = (int64_t)t.end_ms / 10000;
+        if (tb > b) b = tb;
+      }
+      shard_maxb_[(size_t)s * 8] = b;
+    }
     const double ts1 = now_ms();
     shard_ms_[(size_t)s * 16] = ts1 - ts0;
     trace_event("shard", ts0, ts1, 2 + s);
@@ -833,7 +843,7 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
   // lock-step: node-wide watermark (cache clock of the next batch) and newest bucket
   if (lockstep_) {
     const double tl = now_ms();
-    lockstep_sync(outs);
+    lockstep_sync();
     trace_event("lockstep", tl, now_ms(), 0);
   }
 
@@ -1872,15 +1882,10 @@ void Engine::coll_wait(hipStream_t s, hipEvent_t ev, const char* what) {
 // the next batch, and the node-wide newest bucket decides this batch's rollovers.  The bucket is
 // the one stats_for_batch derives (non-db tx with a usable endTs), so ranks agree on `latest`
 // without the stats thread touching the communicator.
-void Engine::lockstep_sync(const std::vector<std::vector<TxOut>>& outs) {
+void Engine::lockstep_sync() {
   if (comm_aborted_) throw std::runtime_error("RCCL communicator was aborted");
   int64_t b = sync_latest_;
-  for (const auto& v : outs)
-    for (const TxOut& t : v) {
-      if (t.to_db || !(t.end_ms == t.end_ms) || t.end_ms < 10000) continue;
-      const int64_t tb = (int64_t)t.end_ms / 10000;
-      if (tb > b) b = tb;
-    }
+  for (size_t k = 0; k < shards_.size(); ++k) b = std::max(b, shard_maxb_[k * 8]);
   if (fleet_nranks_ == 1) {  // MAX over one rank is the identity: no device round trip
     if (b != INT64_MIN) sync_latest_ = std::max(sync_latest_, b);
     return;

@@ -291,7 +291,7 @@ class Engine {
   void fleet_exchange_upto(uint64_t rounds);
   void coll_check(ncclResult_t r, const char* what);
   void coll_wait(hipStream_t s, hipEvent_t ev, const char* what);
-  void lockstep_sync(const std::vector<std::vector<TxOut>>& outs);
+  void lockstep_sync();
   void apply_latest_locked(int64_t g, double batch_t0);
   void stats_worker();
   void post_stats(std::vector<std::vector<TxOut>>&& outs, bool multi, double t0, int64_t sync_latest = INT64_MIN);
@@ -330,6 +330,7 @@ class Engine {
   hipEvent_t pack_ev_[2] = {nullptr, nullptr};     // pack of the slot done (comm stream)
   int fleet_nranks_ = 0;
   bool fleet_skip_solo_ = false;
+  std::vector<int64_t> shard_maxb_;  // per-shard newest bucket (one cache line each), lock-step clock
   uint64_t fleet_rounds_ = 0;  // exchanges issued (ingest thread)
   uint64_t fleet_posted_ = 0;  // batches posted since fleet_init (ingest thread)
   uint64_t fleet_packed_ = 0;  // batches packed (stats thread)
