@@ -5,7 +5,8 @@ Each GPU owns a disjoint set of JVM hosts (``parallel.dist.shard_servers``), so 
 rank and never needs cross-GPU traffic.  What *is* global is the per-service view across all
 servers ("is getFoo slow everywhere or on one JVM?"): every interval each rank packs, per service
 and per LAG/stat, {#series with a baseline, sum of baseline means, sum of squared means} into a
-dense fp64 matrix on the engine's comm stream (``k_service_moments``) and one
+dense fp64 matrix on the engine's comm stream (``k_service_gram``: per-service Gram matrices on the
+MFMA f64 matrix cores, ``k_service_moments`` atomic scatter for the newest series) and one
 ``all_reduce(SUM)`` merges it.  The collective runs on the engine's second HIP stream, so it
 overlaps the next batch's H2D + parse kernels on the main stream; a two-slot buffer ring keeps
 the in-flight reduction from being overwritten.
