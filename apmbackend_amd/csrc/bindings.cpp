@@ -102,6 +102,11 @@ EngineConfig config_from(const py::dict& d) {
   c.coll_timeout_ms = get<double>(d, "coll_timeout_ms", c.coll_timeout_ms);
   c.outputs = get<uint32_t>(d, "outputs", c.outputs);
   c.async_stats = get<int>(d, "async_stats", c.async_stats);
+  c.device_join = get<int>(d, "device_join", c.device_join);
+  c.join_table_bits = get<int>(d, "join_table_bits", c.join_table_bits);
+  c.need_arena = get<uint32_t>(d, "need_arena", c.need_arena);
+  c.tx_ring_bytes = get<uint64_t>(d, "tx_ring_bytes", c.tx_ring_bytes);
+  c.max_raw_services = get<uint32_t>(d, "max_raw_services", c.max_raw_services);
   return c;
 }
 
@@ -142,6 +147,7 @@ py::dict metrics_dict(const EngineMetrics& m) {
   d["formatted_bytes"] = m.formatted_bytes; d["lockstep_rollovers"] = m.lockstep_rollovers; d["format_fallbacks"] = m.format_fallbacks;
   d["t_parse_ms"] = m.t_parse_ms; d["t_join_ms"] = m.t_join_ms; d["t_stats_ms"] = m.t_stats_ms;
   d["t_total_ms"] = m.t_total_ms;
+  d["series_overflow_tx"] = m.series_overflow_tx;
   d["rollover_latency_ms"] = m.rollover_latency_ms;
   return d;
 }

@@ -1,0 +1,1115 @@
+// K4/K5/K6 on the GPU: the transaction join of stream_parse_transactions.js and the tx wire
+// encoder (entries.js TxEntry.toCSVString), for every JVM of the rank at once.
+//
+// Reference: TTL caches recordCache / acctCache / needNumRecordCache (:211-239), saveAcctNum
+// (:294-327), parseSoapLine (:352-376), EJB entry/exit (:378-446), CommonTiming entry/exit
+// (:451-565), BAF salvage (:486-504), outputRecord (:264-290).  The host twin is
+// runtime/join.cpp (kept as the `joinOnDevice: false` path and as the checkpoint format).
+//
+// Pipeline per batch (all on the join stream; see devjoin_types.h for the state layout):
+//   k_build_ops    one lane per event -> JOp (field extraction, BAF account, SOAP effects)
+//   k_soap_*       per-file SOAP request context: segmented scan of transition functions
+//                  (summary -> per-file carry -> apply); account lines become JOP_ACCT
+//   k_claim        key-table slot per op (find-or-insert, CAS), service registry claim
+//   radix sort     ops by slot (stable: line order inside a key)
+//   k_exp_*        needNumRecordCache expiry of the regions whose TTL passed (creation order)
+//   k_group_walk   one lane per key: replays the key's ops in line order against its state
+//   k_place        outputs to their single-stream position (expiries first, then line order)
+// then, after the host named new services: k_resolve_len + scan (line lengths, stats index),
+// k_write (tx text into the HBM ring, TxRec for K7/K9, rollover candidates).
+#include "kernel_api.h"
+
+#include <rocprim/rocprim.hpp>
+
+#include <climits>
+#include <cstddef>
+
+#include "devjoin_api.h"
+#include "devjoin_dev.h"
+
+namespace apm {
+using namespace dj;
+
+namespace {
+
+constexpr int TB = 256;
+
+__device__ __forceinline__ uint32_t grid_n(uint32_t n) { return (n + TB - 1) / TB; }
+
+// ------------------------------------------------------------------------ host-event selection
+// Events the GPU does not resolve alone: audit lines (K5, host state machine), lines the parser
+// deferred (non-ASCII, exotic numbers / timestamps), logIds with inner brackets, and account
+// strings parseInt cannot decide in 64 bits.
+__device__ bool needs_host(const Event& e, const uint8_t* __restrict__ bytes) {
+  if (e.kind == LK_APP || (e.mask & PM_HOST)) return true;
+  const uint8_t* p = bytes + e.off;
+  if (e.kind >= LK_EJB_ENTRY && e.kind <= LK_CT_EXIT) {
+    if (!(e.mask & PM_KEYS) || e.ntok < 3) return true;
+    if (e.kind == LK_CT_EXIT && (e.mask & PM_BAF) && e.ntok >= 4) {
+      uint8_t acct[64];
+      const int n = baf_account(p, e.t3s, e.t3e, acct);
+      double v;
+      if (n < 0 || !simple_parse_int(acct, n, v)) return true;
+    }
+    return false;
+  }
+  if (e.kind == LK_SOAP) {
+    const uint32_t m = e.mask;
+    if (m & (PM_SOAP_IN | PM_SOAP_OUT)) return false;
+    if (m & (PM_SOAP_ACCT | PM_SOAP_VALUE)) {
+      if (!(m & PM_SOAP_ACCT) && (m & PM_SOAP_KEY)) return false;  // KEY branch wins
+      int fs, fe;
+      angle_field2(p, (int)e.len, fs, fe);
+      if (fs < 0) return false;
+      while (fs < fe && (p[fs] == ' ' || (p[fs] >= 9 && p[fs] <= 13))) ++fs;
+      while (fe > fs && (p[fe - 1] == ' ' || (p[fe - 1] >= 9 && p[fe - 1] <= 13))) --fe;
+      double v;
+      if (all_digits(p + fs, fe - fs) && !simple_parse_int(p + fs, fe - fs, v)) return true;
+    }
+    return false;
+  }
+  return false;
+}
+
+__global__ void k_host_flags(const Event* __restrict__ ev, const uint32_t* __restrict__ n_ev_dev,
+                             const uint8_t* __restrict__ bytes, uint8_t* __restrict__ flag, uint32_t cap) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cap) return;
+  const uint32_t n = *n_ev_dev;
+  flag[i] = (i < n && needs_host(ev[i], bytes)) ? 1 : 0;
+}
+
+__global__ void k_host_scatter(const Event* __restrict__ ev, const uint8_t* __restrict__ flag,
+                               const uint32_t* __restrict__ pos, uint32_t cap, const uint32_t* __restrict__ n_ev_dev,
+                               Event* __restrict__ out, uint32_t* __restrict__ out_idx, uint32_t* __restrict__ n_host) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t n = *n_ev_dev;
+  if (i == 0) *n_host = n == 0 ? 0 : pos[n - 1] + flag[n - 1];
+  if (i >= n || i >= cap || !flag[i]) return;
+  out[pos[i]] = ev[i];
+  out_idx[pos[i]] = i;
+}
+
+// ------------------------------------------------------------------------ op build
+enum : uint8_t { SC_NONE = 0, SC_IN = 1, SC_OUT = 2, SC_ACCT = 3, SC_KEY = 4, SC_VALUE = 5 };
+
+__device__ const HostOp* find_hop(const HostOp* __restrict__ h, uint32_t n, uint32_t ev) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (h[mid].ev < ev) lo = mid + 1; else hi = mid;
+  }
+  return (lo < n && h[lo].ev == ev) ? &h[lo] : nullptr;
+}
+
+__global__ void k_build_ops(DJArgs a) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n_ev) return;
+  const Event e = a.ev[i];
+  JOp op;
+  op.gkey = 0; op.svc = 0; op.ts = apm_nan(); op.num = apm_nan(); op.aux = apm_nan(); op.aux2 = apm_nan();
+  op.line = e.line; op.lid = 0; op.svc_ref = 0; op.lid_len = 0; op.svc_len = 0;
+  op.flags = 0; op.op = JOP_NONE; op.pad = 0;
+  const int32_t file = (int32_t)a.chunk_file[e.chunk];
+  const int32_t server = a.file_server[file];
+  op.server = server;
+  uint8_t code = SC_NONE;
+  double snum = apm_nan();
+  uint64_t shash = 0;
+  const uint8_t* p = a.bytes + e.off;
+  if (a.host_flag[i]) {
+    const HostOp* h = find_hop(a.hops, a.n_hops, i);
+    if (h) {
+      switch (h->kind) {
+        case HOP_JOIN: op = h->op; break;
+        case HOP_SOAP_IN: code = SC_IN; shash = h->lid_hash; break;
+        case HOP_SOAP_OUT: code = SC_OUT; break;
+        case HOP_SOAP_ACCT: if (h->op.flags & JF_BAF_VALID) { code = SC_ACCT; snum = h->op.num; } break;
+        case HOP_SOAP_KEY: code = SC_KEY; break;
+        case HOP_SOAP_VALUE: if (h->op.flags & JF_BAF_VALID) { code = SC_VALUE; snum = h->op.num; } break;
+        default: break;
+      }
+    }
+  } else if (e.kind >= LK_EJB_ENTRY && e.kind <= LK_CT_EXIT) {
+    const bool ejb = e.kind <= LK_EJB_EXIT;
+    const bool entry = e.kind == LK_EJB_ENTRY || e.kind == LK_CT_ENTRY;
+    op.lid = e.off + e.t0s;
+    op.lid_len = (uint16_t)(e.t0e - e.t0s);
+    op.svc = e.svc;
+    op.flags = JF_HAS_SVC | (ejb ? JF_EJB : 0);
+    if (e.tAs == 0xffff) op.flags |= JF_SVC_UNDEF;
+    else { op.svc_ref = e.off + e.tAs; op.svc_len = (uint16_t)(e.tAe - e.tAs); }
+    op.ts = e.ts;
+    const bool empty_lid = op.lid_len == 0;
+    if (entry) {
+      if (!empty_lid) { op.op = JOP_ENTRY; op.gkey = gkey_of(e.key, server); }
+      else op.flags = 0;  // parseEntry returns before naming the service
+    } else {
+      op.num = (e.kind == LK_EJB_EXIT || e.tBs != 0xffff) ? e.num : apm_nan();
+      if (e.kind == LK_CT_EXIT && (e.mask & PM_BAF)) {
+        uint8_t acct[64];
+        int n;
+        if (e.ntok >= 4) {
+          n = baf_account(p, e.t3s, e.t3e, acct);
+        } else {
+          const char* u = "undefined";
+          for (n = 0; n < 9; ++n) acct[n] = (uint8_t)u[n];
+        }
+        if (n > 0) {
+          double v = apm_nan();
+          simple_parse_int(acct, n, v);
+          op.flags |= JF_BAF;
+          op.aux = v;
+          if (all_digits(acct, n)) { op.flags |= JF_BAF_VALID; op.aux2 = v; }
+        }
+      }
+      if (empty_lid) op.op = JOP_DIRECT;
+      else { op.op = e.kind == LK_EJB_EXIT ? JOP_EJB_EXIT : JOP_CT_EXIT; op.gkey = gkey_of(e.key, server); }
+    }
+  } else if (e.kind == LK_SOAP) {
+    const uint32_t m = e.mask;
+    if (m & PM_SOAP_IN) {
+      code = SC_IN;
+      // ws[1].split('=')[1]; no '=' -> has_log_id false -> "undefined"
+      int s = -1, t = -1;
+      if (e.ntok >= 2) {
+        const int a0 = e.t1s, b0 = e.t1e;
+        for (int k = a0; k < b0; ++k) if (p[k] == '=') { s = k + 1; break; }
+        if (s >= 0) { t = b0; for (int k = s; k < b0; ++k) if (p[k] == '=') { t = k; break; } }
+      }
+      shash = s >= 0 ? hash_bytes(p + s, (size_t)(t - s)) : hash_bytes("undefined", 9);
+    } else if (m & PM_SOAP_OUT) {
+      code = SC_OUT;
+    } else if (m & (PM_SOAP_ACCT | PM_SOAP_KEY | PM_SOAP_VALUE)) {
+      const bool acct = m & PM_SOAP_ACCT;
+      if (!acct && (m & PM_SOAP_KEY)) {
+        code = SC_KEY;
+      } else {
+        int fs, fe;
+        angle_field2(p, (int)e.len, fs, fe);
+        bool valid = false;
+        if (fs >= 0) {
+          while (fs < fe && (p[fs] == ' ' || (p[fs] >= 9 && p[fs] <= 13))) ++fs;
+          while (fe > fs && (p[fe - 1] == ' ' || (p[fe - 1] >= 9 && p[fe - 1] <= 13))) --fe;
+          valid = all_digits(p + fs, fe - fs) && simple_parse_int(p + fs, fe - fs, snum);
+        }
+        if (valid) code = acct ? SC_ACCT : SC_VALUE;
+      }
+    }
+  }
+  a.ops[i] = op;
+  a.soap_code[i] = code;
+  a.soap_num[i] = snum;
+  a.soap_hash[i] = shash;
+}
+
+// ------------------------------------------------------------------------ SOAP context scan
+// State: CONST form {tag 0 none / 1 ctx / 2 ctx + pull_next, L = IN event + 1 (0: carried)}.
+// Functions: CONST (IN, OUT, valid account = saved and erased) or MAP (KEY, valid VALUE, others
+// identity) acting on the tag only.  Composition is associative, so a wave scans 64 events with
+// shuffles and chunks are split into segments whose summaries are chained per file.
+constexpr uint32_t F_CONST = 1u << 31;
+constexpr uint32_t F_ID = 1u | (2u << 2);
+constexpr uint32_t F_KEY = 2u | (2u << 2);
+constexpr uint32_t F_VALUE = 1u | (0u << 2);
+
+__device__ __forceinline__ uint32_t map_tag(uint32_t g, uint32_t tag) {
+  return tag == 0 ? 0u : (tag == 1 ? (g & 3u) : ((g >> 2) & 3u));
+}
+// g after f
+__device__ __forceinline__ uint32_t fcompose(uint32_t g, uint32_t f) {
+  if (g & F_CONST) return g;
+  if (f & F_CONST) {
+    const uint32_t t = map_tag(g, f & 3u);
+    return t ? (F_CONST | t | (f & ~(F_CONST | 3u))) : F_CONST;
+  }
+  return map_tag(g, f & 3u) | (map_tag(g, (f >> 2) & 3u) << 2);
+}
+__device__ __forceinline__ uint32_t code_fn(uint8_t c, uint32_t ev) {
+  switch (c) {
+    case SC_IN: return F_CONST | 1u | ((ev + 1) << 2);
+    case SC_OUT: case SC_ACCT: return F_CONST;
+    case SC_KEY: return F_KEY;
+    case SC_VALUE: return F_VALUE;
+    default: return F_ID;
+  }
+}
+
+__device__ __forceinline__ void soap_range(const uint32_t* lo_tab, uint32_t c, int g, uint32_t& lo, uint32_t& hi) {
+  const uint32_t c0 = lo_tab[c], c1 = lo_tab[c + 1];
+  const uint32_t n = c1 - c0;
+  const uint32_t seg = ((n + SOAP_SEGS - 1) / SOAP_SEGS + APM_WAVE - 1) / APM_WAVE * APM_WAVE;
+  lo = min(c1, c0 + (uint32_t)g * seg);
+  hi = min(c1, lo + seg);
+}
+
+// inclusive wave scan of transition functions (lane order = event order)
+__device__ __forceinline__ uint32_t wave_fscan(uint32_t f, int lane) {
+#pragma unroll
+  for (int d = 1; d < APM_WAVE; d <<= 1) {
+    const uint32_t o = __shfl_up(f, d, APM_WAVE);
+    if (lane >= d) f = fcompose(f, o);
+  }
+  return f;
+}
+
+__global__ void k_chunk_events(const Event* __restrict__ ev, uint32_t n_ev, uint32_t n_chunks, uint32_t* __restrict__ lo) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c > n_chunks) return;
+  uint32_t l = 0, h = n_ev;
+  while (l < h) {
+    const uint32_t mid = (l + h) >> 1;
+    if (ev[mid].chunk < c) l = mid + 1; else h = mid;
+  }
+  lo[c] = l;
+}
+
+__global__ __launch_bounds__(APM_WAVE) void k_soap_summary(DJArgs a) {
+  const uint32_t c = blockIdx.x;
+  const int g = blockIdx.y;
+  if (c >= a.n_chunks || a.chunk_kind[c] != FILE_SOAP) return;
+  const int lane = threadIdx.x;
+  uint32_t lo, hi;
+  soap_range(a.chunk_ev_lo, c, g, lo, hi);
+  uint32_t acc = F_ID;
+  for (uint32_t base = lo; base < hi; base += APM_WAVE) {
+    const uint32_t i = base + lane;
+    const uint32_t f = i < hi ? code_fn(a.soap_code[i], i) : F_ID;
+    const uint32_t inc = wave_fscan(f, lane);
+    acc = fcompose(__shfl(inc, APM_WAVE - 1, APM_WAVE), acc);
+  }
+  if (lane == 0) a.seg_f[(size_t)c * SOAP_SEGS + g] = acc;
+}
+
+__global__ void k_soap_carry(DJArgs a) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.n_chunks || a.chunk_kind[c] != FILE_SOAP || !a.chunk_first[c]) return;
+  const int32_t file = (int32_t)a.chunk_file[c];
+  const SoapState s0 = a.soap_state[file];
+  const uint64_t h0 = s0.lid_hash;
+  uint32_t st = F_CONST | (uint32_t)s0.tag;  // L = 0: the carried context
+  for (int32_t d = (int32_t)c; d >= 0; d = a.chunk_next[d]) {
+    a.chain_hash[d] = h0;
+    for (int g = 0; g < SOAP_SEGS; ++g) {
+      a.seg_in[(size_t)d * SOAP_SEGS + g] = st;
+      st = fcompose(a.seg_f[(size_t)d * SOAP_SEGS + g], st);
+    }
+  }
+  SoapState s1;
+  s1.tag = (int32_t)(st & 3u);
+  s1.undef = 0;
+  const uint32_t L = (st & ~F_CONST) >> 2;
+  s1.lid_hash = s1.tag == 0 ? 0 : (L == 0 ? h0 : a.soap_hash[L - 1]);
+  a.soap_state[file] = s1;
+}
+
+__global__ __launch_bounds__(APM_WAVE) void k_soap_apply(DJArgs a) {
+  const uint32_t c = blockIdx.x;
+  const int g = blockIdx.y;
+  if (c >= a.n_chunks || a.chunk_kind[c] != FILE_SOAP) return;
+  const int lane = threadIdx.x;
+  uint32_t lo, hi;
+  soap_range(a.chunk_ev_lo, c, g, lo, hi);
+  if (lo >= hi) return;
+  uint32_t st = a.seg_in[(size_t)c * SOAP_SEGS + g];
+  const uint64_t h0 = a.chain_hash[c];
+  const int32_t server = a.file_server[a.chunk_file[c]];
+  for (uint32_t base = lo; base < hi; base += APM_WAVE) {
+    const uint32_t i = base + lane;
+    const uint8_t code = i < hi ? a.soap_code[i] : SC_NONE;
+    const uint32_t f = code_fn(code, i);
+    const uint32_t inc = wave_fscan(f, lane);
+    uint32_t exc = __shfl_up(inc, 1, APM_WAVE);
+    if (lane == 0) exc = F_ID;
+    const uint32_t before = fcompose(exc, st);
+    const uint32_t tag = before & 3u;
+    if ((code == SC_ACCT && tag != 0) || (code == SC_VALUE && tag == 2)) {
+      const uint32_t L = (before & ~F_CONST) >> 2;
+      const uint64_t h = L == 0 ? h0 : a.soap_hash[L - 1];
+      JOp op = a.ops[i];
+      op.op = JOP_ACCT;
+      op.gkey = gkey_of(h, server);
+      op.num = a.soap_num[i];
+      op.server = server;
+      a.ops[i] = op;
+    }
+    st = fcompose(__shfl(inc, APM_WAVE - 1, APM_WAVE), st);
+  }
+}
+
+// ------------------------------------------------------------------------ tables
+__device__ uint32_t key_claim(KeyState* __restrict__ t, uint32_t mask, uint64_t k, JoinCounts* cnt) {
+  uint32_t h = home_of(k, mask);
+  for (uint32_t probe = 0; probe <= mask; ++probe) {
+    const uint32_t idx = (h + probe) & mask;
+    const uint64_t cur = __hip_atomic_load(&t[idx].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == k) return idx;
+    if (cur == 0) {
+      const unsigned long long prev = atomicCAS((unsigned long long*)&t[idx].key, 0ULL, (unsigned long long)k);
+      if (prev == 0) {
+        KeyState& s = t[idx];
+        s.acct = apm_nan();
+        s.acct_exp = -__builtin_inf();
+        s.rec_exp = -__builtin_inf();
+        s.need = -1;
+        s.n_part = 0;
+        atomicAdd(&cnt->n_keys_new, 1u);
+        return idx;
+      }
+      if (prev == k) return idx;
+    }
+  }
+  atomicAdd(&cnt->table_full, 1ULL);
+  return 0xffffffffu;
+}
+
+__device__ int32_t reg_find(const RegSlot* __restrict__ t, uint32_t mask, uint64_t k) {
+  uint32_t h = home_of(k, mask);
+  for (uint32_t probe = 0; probe <= mask; ++probe) {
+    const uint32_t idx = (h + probe) & mask;
+    const uint64_t cur = t[idx].key;
+    if (cur == k) return t[idx].raw;
+    if (cur == 0) return RAW_EMPTY;
+  }
+  return RAW_EMPTY;
+}
+
+__global__ void k_claim(DJArgs a) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n_ev) return;
+  const JOp& op = a.ops[i];
+  const uint32_t cap = a.table_mask + 1;
+  uint32_t key = cap + 1;  // no op
+  if (op.op == JOP_DIRECT) key = cap;
+  else if (op.op != JOP_NONE) {
+    const uint32_t s = key_claim(a.table, a.table_mask, op.gkey, a.counts);
+    key = s == 0xffffffffu ? cap + 1 : s;
+  }
+  a.op_slot[i] = key;
+  a.op_idx[i] = i;
+  if (op.op != JOP_NONE && (op.flags & JF_HAS_SVC)) {
+    const uint64_t k = regkey_of(op.svc, op.server);
+    uint32_t h = home_of(k, a.reg_mask);
+    for (uint32_t probe = 0; probe <= a.reg_mask; ++probe) {
+      const uint32_t idx = (h + probe) & a.reg_mask;
+      const uint64_t cur = __hip_atomic_load(&a.reg[idx].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur == k) break;
+      if (cur == 0) {
+        const unsigned long long prev = atomicCAS((unsigned long long*)&a.reg[idx].key, 0ULL, (unsigned long long)k);
+        if (prev == 0) {
+          a.reg[idx].raw = RAW_PENDING;
+          const uint32_t m = atomicAdd(&a.counts->n_miss, 1u);
+          if (m < a.miss_cap) {
+            RegMiss r;
+            r.svc = op.svc;
+            r.server = op.server;
+            r.name = op.svc_ref;
+            r.name_len = op.svc_len;
+            r.flags = op.flags & (JF_EJB | JF_SVC_UNDEF | JF_SVC_HOST);
+            r.slot = (int32_t)idx;
+            a.miss[m] = r;
+          }
+          break;
+        }
+        if (prev == k) break;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------ outputs
+// outputRecord (:264-290): start falls back to end - elapsed; numbers pass through parseInt.
+__device__ __forceinline__ TxDev make_tx(int32_t server, uint64_t svc, uint8_t src, uint32_t lid, uint32_t lid_len,
+                                         double acct, double start_ms, bool start_empty, double end_ms, bool end_empty,
+                                         double elapsed, bool to_db) {
+  TxDev t;
+  double s = start_empty ? apm_nan() : start_ms;
+  const double e_for_sub = end_empty ? 0.0 : end_ms;  // JS: '' - n === -n
+  if (!(s == s) || s == 0) s = e_for_sub - elapsed;
+  t.start = isfinite(s) ? trunc(s) : apm_nan();
+  t.end = end_empty ? apm_nan() : (isfinite(end_ms) ? trunc(end_ms) : apm_nan());
+  t.acct = acct;
+  t.elapsed = elapsed;
+  t.svc = svc;
+  t.server = server;
+  t.lid = lid;
+  t.lid_len = (uint16_t)lid_len;
+  t.lid_src = lid_len ? src : LID_NONE;
+  t.to_db = to_db ? 1 : 0;
+  t.raw = -1;
+  return t;
+}
+
+struct Emitter {
+  TxDev* stage;
+  DJOverflow* ovf;
+  uint32_t* ovf_n;  // JoinCounts::pad[0]: overflow cursor
+  uint32_t ev;
+  uint32_t sub;
+  __device__ void put(const TxDev& t) {
+    if (sub < 2) {
+      stage[(size_t)ev * 2 + sub] = t;
+    } else {
+      const uint32_t k = atomicAdd(ovf_n, 1u);
+      if (k < DJ_OVF_CAP) {
+        ovf[k].ev = ev;
+        ovf[k].sub = sub;
+        ovf[k].t = t;
+      }
+    }
+    ++sub;
+  }
+};
+
+__device__ __forceinline__ uint8_t lid_src_of(const JOp& op) { return (op.flags & JF_LID_HOST) ? LID_HOST : LID_BATCH; }
+
+// needNumRecordCache entry of this batch's region (all share the batch's TTL clock)
+__device__ int32_t need_alloc(DJArgs& a, const JOp& op, uint64_t gkey) {
+  const uint32_t k = atomicAdd(&a.counts->n_need_new, 1u);
+  if (k >= a.arena_limit) {
+    atomicAdd(&a.counts->need_overflow, 1ULL);
+    return -1;
+  }
+  const uint32_t idx = (uint32_t)((a.arena_base + k) & (uint64_t)(a.arena_cap - 1));
+  NeedEnt& ne = a.arena[idx];
+  ne.key = gkey;
+  ne.exp = a.now + a.need_ttl;
+  ne.created = (a.batch_no << 28) | (uint64_t)(op.line & 0xfffffffu);
+  ne.server = op.server;
+  ne.n = 0;
+  uint32_t n = op.lid_len;
+  if (n > NEED_LID) { atomicAdd(&a.counts->need_overflow, 1ULL); n = NEED_LID; }
+  ne.lid_len = (int32_t)n;
+  const uint8_t* src = (op.flags & JF_LID_HOST) ? a.hbuf + op.lid : a.bytes + op.lid;
+  for (uint32_t j = 0; j < n; ++j) ne.lid[j] = (char)src[j];
+  return (int32_t)idx;
+}
+
+__device__ void need_put(DJArgs& a, NeedEnt& ne, const NeedItem& it) {
+  for (int j = 0; j < ne.n; ++j)
+    if (ne.items[j].svc == it.svc) { ne.items[j] = it; return; }
+  if (ne.n < NEED_ITEMS) ne.items[ne.n++] = it;
+  else atomicAdd(&a.counts->need_overflow, 1ULL);
+}
+
+__device__ void need_drain(NeedEnt& ne, int32_t nidx, double acct, Emitter& em) {
+  // saveAcctNum: every parked record of the logId is output with the new account (to_db false)
+  for (int j = 0; j < ne.n; ++j) {
+    const NeedItem& r = ne.items[j];
+    em.put(make_tx(ne.server, r.svc, LID_NEED, (uint32_t)nidx, (uint32_t)ne.lid_len, acct, r.start,
+                   (r.flags & JF_START_EMPTY) != 0, r.end, (r.flags & JF_TS_EMPTY) != 0, r.elapsed, false));
+  }
+  ne.n = 0;
+}
+
+__global__ void k_group_walk(DJArgs a) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n_ev) return;
+  const uint32_t cap = a.table_mask + 1;
+  const uint32_t slot = a.op_slot_sorted[i];
+  if (slot > cap) return;  // no op
+  if (slot == cap) {       // JOP_DIRECT: empty logId, no cache state
+    const uint32_t ev = a.op_idx_sorted[i];
+    const JOp op = a.ops[ev];
+    Emitter em{a.stage, a.ovf, &a.counts->pad[0], ev, 0};
+    em.put(make_tx(op.server, op.svc, LID_NONE, 0, 0, (op.flags & JF_BAF) ? op.aux : apm_nan(), 0.0, true, op.ts,
+                   (op.flags & JF_TS_EMPTY) != 0, op.num, false));
+    a.out_cnt[ev] = em.sub;
+    return;
+  }
+  if (i > 0 && a.op_slot_sorted[i - 1] == slot) return;  // not the first op of its key
+  KeyState ks = a.table[slot];
+  const double now = a.now;
+  bool acct_live = ks.acct_exp >= now;
+  if (!(ks.rec_exp >= now) && ks.n_part > 0) {  // expired recordCache entry: discarded (:220-224)
+    atomicAdd(&a.counts->expired_partials, (unsigned long long)ks.n_part);
+    ks.n_part = 0;
+  }
+  NeedEnt* ne = nullptr;
+  int32_t nidx = -1;
+  if (ks.need >= 0) {
+    NeedEnt* c = &a.arena[ks.need];
+    if (c->key == ks.key && c->exp >= now) { ne = c; nidx = ks.need; }
+  }
+  for (uint32_t j = i; j < a.n_ev && a.op_slot_sorted[j] == slot; ++j) {
+    const uint32_t ev = a.op_idx_sorted[j];
+    const JOp op = a.ops[ev];
+    Emitter em{a.stage, a.ovf, &a.counts->pad[0], ev, 0};
+    const bool ts_empty = (op.flags & JF_TS_EMPTY) != 0;
+    switch (op.op) {
+      case JOP_ENTRY: {
+        if (!(ks.rec_exp >= now)) { ks.rec_exp = now + a.rec_ttl; ks.n_part = 0; }
+        int f = -1;
+        for (int k = 0; k < KS_PARTS; ++k) if (k < ks.n_part && ks.part_svc[k] == op.svc) f = k;
+        if (f >= 0) ks.part_start[f] = op.ts;
+        else if (ks.n_part < KS_PARTS) { ks.part_svc[ks.n_part] = op.svc; ks.part_start[ks.n_part] = op.ts; ++ks.n_part; }
+        else atomicAdd(&a.counts->partial_overflow, 1ULL);
+        break;
+      }
+      case JOP_EJB_EXIT:
+      case JOP_CT_EXIT: {
+        const bool ct = op.op == JOP_CT_EXIT;
+        int f = -1;
+        if (ks.rec_exp >= now)
+          for (int k = 0; k < KS_PARTS; ++k) if (k < ks.n_part && ks.part_svc[k] == op.svc) f = k;
+        if (f < 0) {
+          if (!ct) { atomicAdd(&a.counts->ejb_unmatched, 1ULL); break; }
+          // salvageRecordAndOutput (:500-504): BAF account saved under this logId, then the
+          // record is output without a logId
+          if ((op.flags & JF_BAF) && (op.flags & JF_BAF_VALID)) {
+            ks.acct = op.aux2; ks.acct_exp = now + a.acct_ttl; acct_live = true;
+            if (ne && ne->n) need_drain(*ne, nidx, op.aux2, em);
+          } else if (op.flags & JF_BAF) {
+            atomicAdd(&a.counts->invalid_acct, 1ULL);
+          }
+          em.put(make_tx(op.server, op.svc, LID_NONE, 0, 0, (op.flags & JF_BAF) ? op.aux : apm_nan(), 0.0, true,
+                         op.ts, ts_empty, op.num, false));
+          break;
+        }
+        const double pstart = ks.part_start[f];
+        auto remove_part = [&]() {
+          for (int k = 0; k < KS_PARTS - 1; ++k)
+            if (k >= f && k + 1 < ks.n_part) { ks.part_svc[k] = ks.part_svc[k + 1]; ks.part_start[k] = ks.part_start[k + 1]; }
+          --ks.n_part;
+        };
+        if (acct_live) {
+          remove_part();
+          em.put(make_tx(op.server, op.svc, lid_src_of(op), op.lid, op.lid_len, ks.acct, pstart, false, op.ts,
+                         ts_empty, op.num, false));
+          break;
+        }
+        if (!ne) { nidx = need_alloc(a, op, ks.key); ne = nidx >= 0 ? &a.arena[nidx] : nullptr; ks.need = nidx; }
+        double alt = apm_nan();
+        if (ct && (op.flags & JF_BAF)) {
+          alt = op.aux;
+          if (op.flags & JF_BAF_VALID) {  // may drain the records parked before this one
+            ks.acct = op.aux2; ks.acct_exp = now + a.acct_ttl; acct_live = true;
+            if (ne && ne->n) need_drain(*ne, nidx, op.aux2, em);
+          } else {
+            atomicAdd(&a.counts->invalid_acct, 1ULL);
+          }
+        }
+        if (ne) {
+          NeedItem it;
+          it.svc = op.svc; it.start = pstart; it.end = op.ts; it.elapsed = op.num; it.alt = alt;
+          it.flags = ts_empty ? JF_TS_EMPTY : 0; it.pad = 0;
+          need_put(a, *ne, it);
+        }
+        remove_part();
+        break;
+      }
+      case JOP_ACCT: {
+        ks.acct = op.num; ks.acct_exp = now + a.acct_ttl; acct_live = true;
+        if (ne && ne->n) need_drain(*ne, nidx, op.num, em);
+        break;
+      }
+      case JOP_AUDIT_TX: {
+        const bool to_db = (op.flags & JF_TO_DB) != 0;
+        if (acct_live) {
+          em.put(make_tx(op.server, op.svc, lid_src_of(op), op.lid, op.lid_len, ks.acct, op.aux,
+                         (op.flags & JF_START_EMPTY) != 0, op.ts, ts_empty, op.num, to_db));
+          break;
+        }
+        if (!ne) { nidx = need_alloc(a, op, ks.key); ne = nidx >= 0 ? &a.arena[nidx] : nullptr; ks.need = nidx; }
+        if (ne) {
+          NeedItem it;
+          it.svc = op.svc; it.start = op.aux; it.end = op.ts; it.elapsed = op.num; it.alt = op.aux2;
+          it.flags = (ts_empty ? JF_TS_EMPTY : 0) | ((op.flags & JF_START_EMPTY) ? JF_START_EMPTY : 0) | (to_db ? JF_TO_DB : 0);
+          it.pad = 0;
+          need_put(a, *ne, it);
+        }
+        break;
+      }
+      default: break;
+    }
+    a.out_cnt[ev] = em.sub;
+  }
+  a.table[slot] = ks;
+}
+
+// ---- expiry of needNumRecordCache regions (NodeCache 'expired' -> outputRecord, :226-239)
+__global__ void k_exp_keys(DJArgs a) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.n_exp_entries) return;
+  uint64_t rem = e, v = 0;
+  for (uint32_t r = 0; r < a.n_exp_regions; ++r) {
+    const uint64_t n = a.exp_hi[r] - a.exp_lo[r];
+    if (rem < n) { v = a.exp_lo[r] + rem; break; }
+    rem -= n;
+  }
+  const uint32_t idx = (uint32_t)(v & (uint64_t)(a.arena_cap - 1));
+  const NeedEnt& ne = a.arena[idx];
+  a.exp_key[e] = ne.n > 0 ? ne.created : ~0ULL;
+  a.exp_idx[e] = idx;
+  if (ne.n == 0) a.arena[idx].key = 0;  // drained entry: gone (k_exp_emit clears the others)
+}
+
+__global__ void k_exp_count(DJArgs a) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e > a.n_exp_entries) return;
+  if (e == a.n_exp_entries) { a.exp_cnt[e] = 0; return; }
+  a.exp_cnt[e] = a.exp_key_sorted[e] == ~0ULL ? 0u : (uint32_t)a.arena[a.exp_idx_sorted[e]].n;
+}
+
+__global__ void k_exp_emit(DJArgs a) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e == 0) {
+    a.counts->n_exp_out = a.n_exp_entries ? a.exp_pos[a.n_exp_entries] : 0;
+    atomicAdd(&a.counts->need_expired, (unsigned long long)a.counts->n_exp_out);
+  }
+  if (e >= a.n_exp_entries) return;
+  const uint32_t n = a.exp_cnt[e];
+  if (!n) return;
+  const uint32_t idx = a.exp_idx_sorted[e];
+  NeedEnt& ne = a.arena[idx];
+  const uint32_t base = a.exp_pos[e];
+  for (uint32_t k = 0; k < n && base + k < a.out_cap; ++k) {
+    const NeedItem& r = ne.items[k];
+    a.out[base + k] = make_tx(ne.server, r.svc, LID_NEED, idx, (uint32_t)ne.lid_len, r.alt, r.start,
+                              (r.flags & JF_START_EMPTY) != 0, r.end, (r.flags & JF_TS_EMPTY) != 0, r.elapsed,
+                              (r.flags & JF_TO_DB) != 0);
+  }
+  ne.n = 0;
+  ne.key = 0;  // the entry is gone (an expired region is reused by later batches)
+}
+
+__global__ void k_place(DJArgs a) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t base = a.counts->n_exp_out;
+  if (i == 0) a.counts->n_out = base + a.out_pos[a.n_ev];
+  if (i >= a.n_ev * 2) return;
+  const uint32_t ev = i >> 1, sub = i & 1;
+  if (sub >= a.out_cnt[ev]) return;
+  const uint32_t p = base + a.out_pos[ev] + sub;
+  if (p < a.out_cap) a.out[p] = a.stage[(size_t)ev * 2 + sub];
+}
+
+__global__ void k_place_ovf(DJArgs a) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t n = min(a.counts->pad[0], DJ_OVF_CAP);
+  if (k >= n) return;
+  const DJOverflow& o = a.ovf[k];
+  const uint32_t p = a.counts->n_exp_out + a.out_pos[o.ev] + o.sub;
+  if (p < a.out_cap) a.out[p] = o.t;
+}
+
+// ------------------------------------------------------------------------ format (K6)
+struct U4 {
+  uint32_t x, y, z, w;
+};
+struct U4Plus {
+  __device__ __host__ U4 operator()(const U4& a, const U4& b) const { return U4{a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w}; }
+};
+
+__device__ __forceinline__ const char* lid_ptr(const DJFormatArgs& f, const TxDev& t) {
+  switch (t.lid_src) {
+    case LID_BATCH: return (const char*)f.bytes + t.lid;
+    case LID_HOST: return (const char*)f.hbuf + t.lid;
+    case LID_NEED: return f.arena[t.lid & (f.arena_cap - 1)].lid;
+    default: return "";
+  }
+}
+
+__device__ __forceinline__ bool stat_usable(const TxDev& t) { return !t.to_db && t.end == t.end && t.end >= 10000.0; }
+
+__device__ uint32_t line_len(const DJFormatArgs& f, const TxDev& t) {
+  if (t.raw < 0) return 0;
+  const RawSvc rs = f.raw[t.raw];
+  uint32_t n = 3 + rs.srv_len + 1 + rs.norm_len + 1 + t.lid_len + 1;
+  n += js_num(nullptr, t.acct, nullptr) + 1 + js_num(nullptr, t.start, nullptr) + 1 + js_num(nullptr, t.end, nullptr) +
+       1 + js_num(nullptr, t.elapsed, nullptr) + 1 + 1;
+  return n + 1;  // '\n'
+}
+
+__global__ void k_resolve_len(DJFormatArgs f) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t n = f.n_out;
+  U4* lens = reinterpret_cast<U4*>(f.lens);
+  if (i == n) { lens[n] = U4{0, 0, 0, 0}; return; }
+  if (i > n) return;
+  TxDev t = f.out[i];
+  const int32_t raw = reg_find(f.reg, f.reg_mask, regkey_of(t.svc, t.server));
+  t.raw = raw >= 0 ? raw : -1;
+  f.out[i].raw = t.raw;
+  const uint32_t len = line_len(f, t);
+  const bool st = stat_usable(t);
+  lens[i] = U4{len, st ? 1u : 0u, t.to_db ? 0u : len, t.to_db ? len : 0u};
+  if (t.to_db) atomicAdd(&f.counts->n_db, 1u);
+  else if (!st) atomicAdd(&f.counts->n_dropped, 1u);
+}
+
+__global__ void k_plan_totals(DJFormatArgs f) {
+  const U4 o = reinterpret_cast<const U4*>(f.offs)[f.n_out];
+  f.counts->text_bytes = o.x;
+  f.counts->n_stats = o.y;
+  f.counts->tx_text_bytes = o.z;
+  f.counts->db_text_bytes = o.w;
+}
+
+__device__ __forceinline__ char* put_str(char* p, const char* s, int n) {
+  for (int i = 0; i < n; ++i) p[i] = s[i];
+  return p + n;
+}
+
+__global__ void k_write(DJFormatArgs f) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= f.n_out) return;
+  const TxDev t = f.out[i];
+  if (t.raw < 0) return;
+  const U4 o = reinterpret_cast<const U4*>(f.offs)[i];
+  const U4 l = reinterpret_cast<const U4*>(f.lens)[i];
+  const uint64_t vpos = f.ring_base + o.x;
+  char* p0 = f.ring + (vpos & (f.ring_cap - 1));
+  const RawSvc rs = f.raw[t.raw];
+  char* p = p0;
+  p = put_str(p, "tx|", 3);
+  p = put_str(p, f.names + rs.srv_off, rs.srv_len);
+  *p++ = '|';
+  p = put_str(p, f.names + rs.norm_off, rs.norm_len);
+  *p++ = '|';
+  p = put_str(p, lid_ptr(f, t), t.lid_len);
+  *p++ = '|';
+  bool inexact = false;
+  p += js_num(p, t.acct, &inexact); *p++ = '|';
+  p += js_num(p, t.start, &inexact); *p++ = '|';
+  p += js_num(p, t.end, &inexact); *p++ = '|';
+  p += js_num(p, t.elapsed, &inexact); *p++ = '|';
+  *p++ = rs.toplevel ? 'Y' : 'N';
+  *p++ = '\n';
+  const uint32_t len = l.x;
+  if (f.want_tx && !t.to_db) put_str(f.txt_tx + o.z, p0, (int)len);
+  if (f.want_db && t.to_db) put_str(f.txt_db + o.w, p0, (int)len);
+  if (l.y) {
+    const uint32_t j = o.y;
+    TxRec r;
+    r.end_ms = (int64_t)t.end;
+    const int32_t s = f.raw_series[t.raw];
+    r.series = s;
+    const double e = t.elapsed;
+    r.elapsed = (e == e && e >= -2147483647.0 && e <= 2147483647.0) ? (int32_t)e : ELAPSED_NAN;
+    f.tx[j] = r;
+    f.tx_raw[j] = t.raw;
+    f.tx_gid[j] = (int64_t)((vpos << 20) | (uint64_t)(len - 1));
+    f.tx_bucket[j] = r.end_ms / 10000;
+    if (s < 0) atomicMin(&f.raw_first[t.raw], (int32_t)j);
+  }
+}
+
+__global__ void k_cands(DJFormatArgs f, uint32_t n) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  if (j == 0 || f.tx_bmax[j] > f.tx_bmax[j - 1]) {
+    const uint32_t k = atomicAdd(&f.counts->n_cand, 1u);
+    f.cand[k] = j;
+    f.cand_bucket[k] = f.tx_bucket[j];
+  }
+  const int32_t r = f.tx_raw[j];
+  if (f.raw_series[r] < 0 && f.raw_first[r] == (int32_t)j) {
+    const uint32_t k = atomicAdd(&f.counts->n_unresolved, 1u);
+    f.unresolved[2 * k] = j;
+    f.unresolved[2 * k + 1] = (uint32_t)r;
+  }
+}
+
+__global__ void k_reset_first(DJFormatArgs f, uint32_t n) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const int32_t r = f.tx_raw[j];
+  if (f.raw_first[r] != INT_MAX) f.raw_first[r] = INT_MAX;
+}
+
+// ------------------------------------------------------------------------ rebuild / ring
+__global__ void k_rebuild(const KeyState* __restrict__ old, uint32_t old_cap, KeyState* __restrict__ fresh,
+                          uint32_t mask, const NeedEnt* __restrict__ arena, uint32_t arena_cap, double now,
+                          JoinCounts* cnt, unsigned long long* live) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= old_cap) return;
+  KeyState s = old[i];
+  if (!s.key) return;
+  const bool rec = s.rec_exp >= now && s.n_part > 0;
+  const bool acct = s.acct_exp >= now;
+  bool need = false;
+  if (s.need >= 0) {
+    const NeedEnt& ne = arena[(uint32_t)s.need & (arena_cap - 1)];
+    need = ne.key == s.key && ne.exp >= now;
+  }
+  if (!rec && s.n_part > 0 && !(s.rec_exp >= now)) atomicAdd(&cnt->expired_partials, (unsigned long long)s.n_part);
+  if (!rec && !acct && !need) return;
+  if (!(s.rec_exp >= now)) s.n_part = 0;
+  uint32_t h = home_of(s.key, mask);
+  for (uint32_t probe = 0; probe <= mask; ++probe) {
+    const uint32_t idx = (h + probe) & mask;
+    if (atomicCAS((unsigned long long*)&fresh[idx].key, 0ULL, (unsigned long long)s.key) == 0ULL) {
+      fresh[idx] = s;
+      atomicAdd(live, 1ULL);
+      return;
+    }
+  }
+}
+
+__global__ void k_gather_len(const int64_t* __restrict__ gid, int64_t n_upper, const int64_t* __restrict__ d_n,
+                             uint32_t* __restrict__ lens) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n_upper) return;
+  const int64_t n = d_n ? *d_n : n_upper;
+  lens[i] = i >= n ? 0u : (uint32_t)((uint64_t)gid[i] & 0xfffffu) + 1u;
+}
+
+__global__ void k_gather_copy(const int64_t* __restrict__ gid, int64_t n, const char* __restrict__ ring,
+                              uint64_t ring_cap, const uint32_t* __restrict__ offs, char* __restrict__ out) {
+  // one wave per line: lanes copy the line's bytes (lines are ~100 B)
+  const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / APM_WAVE;
+  const int lane = threadIdx.x & (APM_WAVE - 1);
+  if (w >= n) return;
+  const uint64_t g = (uint64_t)gid[w];
+  const uint64_t pos = g >> 20;
+  const uint32_t len = (uint32_t)(g & 0xfffffu) + 1u;
+  const char* src = ring + (pos & (ring_cap - 1));
+  char* dst = out + offs[w];
+  for (uint32_t k = lane; k < len; k += APM_WAVE) dst[k] = src[k];
+}
+
+__global__ void k_min_pos(const int64_t* __restrict__ gid, int64_t n, unsigned long long* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long v = i < n ? (unsigned long long)((uint64_t)gid[i] >> 20) : ~0ULL;
+  for (int o = APM_WAVE / 2; o > 0; o >>= 1) {
+    const unsigned long long x = __shfl_xor(v, o, APM_WAVE);
+    v = x < v ? x : v;
+  }
+  if ((threadIdx.x & (APM_WAVE - 1)) == 0 && v != ~0ULL) atomicMin(out, v);
+}
+
+__global__ void k_relocate(int64_t* __restrict__ gid, int64_t n, char* __restrict__ ring, uint64_t ring_cap,
+                           uint64_t below, uint64_t dst_base, unsigned long long* cursor) {
+  const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / APM_WAVE;
+  const int lane = threadIdx.x & (APM_WAVE - 1);
+  if (w >= n) return;
+  const uint64_t g = (uint64_t)gid[w];
+  const uint64_t pos = g >> 20;
+  if (pos >= below) return;
+  const uint32_t len = (uint32_t)(g & 0xfffffu) + 1u;
+  unsigned long long at = 0;
+  if (lane == 0) at = atomicAdd(cursor, (unsigned long long)len);
+  at = __shfl(at, 0, APM_WAVE);
+  const uint64_t np = dst_base + at;
+  const char* src = ring + (pos & (ring_cap - 1));
+  char* dst = ring + (np & (ring_cap - 1));
+  for (uint32_t k = lane; k < len; k += APM_WAVE) dst[k] = src[k];
+  if (lane == 0) gid[w] = (int64_t)((np << 20) | (g & 0xfffffu));
+}
+
+// ------------------------------------------------------------------------ small helpers
+__global__ void k_reg_fill(RegSlot* __restrict__ reg, const int32_t* __restrict__ pairs, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) reg[pairs[2 * i]].raw = pairs[2 * i + 1];
+}
+
+__global__ void k_scatter_i32(int32_t* __restrict__ dst, const int32_t* __restrict__ pairs, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[pairs[2 * i]] = pairs[2 * i + 1];
+}
+
+__global__ void k_fill_series(TxRec* __restrict__ tx, const int32_t* __restrict__ raw, uint32_t n,
+                              const int32_t* __restrict__ raw_series, unsigned long long* __restrict__ unmapped) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (tx[i].series >= 0) return;
+  const int32_t s = raw_series[raw[i]];
+  tx[i].series = s;
+  if (s < 0 && unmapped) atomicAdd(unmapped, 1ULL);  // series table full: counted, not silent
+}
+
+__global__ void k_gather_u8(const uint8_t* __restrict__ src, const int32_t* __restrict__ idx, uint32_t n,
+                            uint8_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = src[idx[i]];
+}
+
+// number of sorted endTs <= edge (upper bound)
+__global__ void k_count_le(const int64_t* __restrict__ end, int64_t n, int64_t edge, int64_t* __restrict__ out) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (end[mid] <= edge) lo = mid + 1; else hi = mid;
+  }
+  *out = lo;
+}
+
+}  // namespace
+}  // namespace apm
+
+extern "C" {
+using namespace apm;
+
+size_t apm_dj_tmp_bytes(uint32_t max_ev, uint32_t max_out, int table_bits) {
+  size_t a = 0, b = 0, c = 0, d = 0, e = 0;
+  const size_t n = std::max<size_t>(max_ev, 1) + 1;
+  HIP_OK(rocprim::exclusive_scan(nullptr, a, (uint8_t*)nullptr, (uint32_t*)nullptr, 0u, n, rocprim::plus<uint32_t>(),
+                                 (hipStream_t)0));
+  HIP_OK(rocprim::radix_sort_pairs(nullptr, b, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                   (uint32_t*)nullptr, n, 0, table_bits + 2, (hipStream_t)0));
+  HIP_OK(rocprim::radix_sort_pairs(nullptr, c, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
+                                   (uint32_t*)nullptr, n, 0, 64, (hipStream_t)0));
+  HIP_OK(rocprim::exclusive_scan(nullptr, d, (U4*)nullptr, (U4*)nullptr, U4{0, 0, 0, 0}, (size_t)max_out + 1, U4Plus(),
+                                 (hipStream_t)0));
+  HIP_OK(rocprim::inclusive_scan(nullptr, e, (int64_t*)nullptr, (int64_t*)nullptr, (size_t)max_out + 1,
+                                 rocprim::maximum<int64_t>(), (hipStream_t)0));
+  return std::max(std::max(std::max(a, b), std::max(c, d)), e) + 4096;
+}
+
+int apm_dj_select_host(DJArgs* a, const uint32_t* d_n_ev, uint32_t max_ev, hipStream_t s) {
+  if (max_ev == 0) { HIP_OK(hipMemsetAsync(a->n_host, 0, 4, s)); return 0; }
+  hipLaunchKernelGGL(k_host_flags, dim3((max_ev + TB - 1) / TB), dim3(TB), 0, s, a->ev, d_n_ev, a->bytes, a->host_flag,
+                     max_ev);
+  size_t need = 0;
+  HIP_OK(rocprim::exclusive_scan(nullptr, need, a->host_flag, a->host_pos, 0u, (size_t)max_ev,
+                                 rocprim::plus<uint32_t>(), s));
+  if (need > a->tmp_bytes) return -1;
+  HIP_OK(rocprim::exclusive_scan(a->tmp, need, a->host_flag, a->host_pos, 0u, (size_t)max_ev,
+                                 rocprim::plus<uint32_t>(), s));
+  hipLaunchKernelGGL(k_host_scatter, dim3((max_ev + TB - 1) / TB), dim3(TB), 0, s, a->ev, a->host_flag, a->host_pos,
+                     max_ev, d_n_ev, a->host_ev, a->host_ev_idx, a->n_host);
+  return 0;
+}
+
+int apm_dj_join(DJArgs* a, hipStream_t s) {
+  const uint32_t n = a->n_ev;
+  const uint32_t cap = a->table_mask + 1;
+  HIP_OK(hipMemsetAsync(a->counts, 0, offsetof(JoinCounts, ejb_unmatched), s));
+  if (n) {
+    HIP_OK(hipMemsetAsync(a->out_cnt, 0, ((size_t)n + 1) * 4, s));
+    hipLaunchKernelGGL(k_build_ops, dim3((n + TB - 1) / TB), dim3(TB), 0, s, *a);
+    hipLaunchKernelGGL(k_chunk_events, dim3((a->n_chunks + 1 + TB - 1) / TB), dim3(TB), 0, s, a->ev, n, a->n_chunks,
+                       a->chunk_ev_lo);
+    hipLaunchKernelGGL(k_soap_summary, dim3(a->n_chunks, SOAP_SEGS), dim3(APM_WAVE), 0, s, *a);
+    hipLaunchKernelGGL(k_soap_carry, dim3((a->n_chunks + 63) / 64), dim3(64), 0, s, *a);
+    hipLaunchKernelGGL(k_soap_apply, dim3(a->n_chunks, SOAP_SEGS), dim3(APM_WAVE), 0, s, *a);
+    hipLaunchKernelGGL(k_claim, dim3((n + TB - 1) / TB), dim3(TB), 0, s, *a);
+    size_t need = 0;
+    HIP_OK(rocprim::radix_sort_pairs(nullptr, need, a->op_slot, a->op_slot_sorted, a->op_idx, a->op_idx_sorted,
+                                     (size_t)n, 0, a->table_bits + 2, s));
+    if (need > a->tmp_bytes) return -1;
+    HIP_OK(rocprim::radix_sort_pairs(a->tmp, need, a->op_slot, a->op_slot_sorted, a->op_idx, a->op_idx_sorted,
+                                     (size_t)n, 0, a->table_bits + 2, s));
+  }
+  (void)cap;
+  // expiry first: its outputs precede every line emission, and it must read the expiring entries
+  // before this batch's region allocations (disjoint by construction) and drains
+  const uint32_t E = a->n_exp_entries;
+  if (E) {
+    hipLaunchKernelGGL(k_exp_keys, dim3((E + TB - 1) / TB), dim3(TB), 0, s, *a);
+    size_t need = 0;
+    HIP_OK(rocprim::radix_sort_pairs(nullptr, need, a->exp_key, a->exp_key_sorted, a->exp_idx, a->exp_idx_sorted,
+                                     (size_t)E, 0, 64, s));
+    if (need > a->tmp_bytes) return -1;
+    HIP_OK(rocprim::radix_sort_pairs(a->tmp, need, a->exp_key, a->exp_key_sorted, a->exp_idx, a->exp_idx_sorted,
+                                     (size_t)E, 0, 64, s));
+    hipLaunchKernelGGL(k_exp_count, dim3((E + 1 + TB - 1) / TB), dim3(TB), 0, s, *a);
+    need = 0;
+    HIP_OK(rocprim::exclusive_scan(nullptr, need, a->exp_cnt, a->exp_pos, 0u, (size_t)E + 1,
+                                   rocprim::plus<uint32_t>(), s));
+    if (need > a->tmp_bytes) return -1;
+    HIP_OK(rocprim::exclusive_scan(a->tmp, need, a->exp_cnt, a->exp_pos, 0u, (size_t)E + 1,
+                                   rocprim::plus<uint32_t>(), s));
+  }
+  hipLaunchKernelGGL(k_exp_emit, dim3((std::max<uint32_t>(E, 1) + TB - 1) / TB), dim3(TB), 0, s, *a);
+  if (n) {
+    hipLaunchKernelGGL(k_group_walk, dim3((n + TB - 1) / TB), dim3(TB), 0, s, *a);
+    size_t need = 0;
+    HIP_OK(rocprim::exclusive_scan(nullptr, need, a->out_cnt, a->out_pos, 0u, (size_t)n + 1,
+                                   rocprim::plus<uint32_t>(), s));
+    if (need > a->tmp_bytes) return -1;
+    HIP_OK(rocprim::exclusive_scan(a->tmp, need, a->out_cnt, a->out_pos, 0u, (size_t)n + 1,
+                                   rocprim::plus<uint32_t>(), s));
+    hipLaunchKernelGGL(k_place, dim3((2 * n + TB - 1) / TB), dim3(TB), 0, s, *a);
+    hipLaunchKernelGGL(k_place_ovf, dim3(DJ_OVF_CAP / TB), dim3(TB), 0, s, *a);
+  } else {
+    HIP_OK(hipMemsetAsync(a->out_pos, 0, 4, s));
+    hipLaunchKernelGGL(k_place, dim3(1), dim3(TB), 0, s, *a);
+  }
+  return 0;
+}
+
+int apm_dj_plan(DJFormatArgs* f, hipStream_t s) {
+  const uint32_t n = f->n_out;
+  hipLaunchKernelGGL(k_resolve_len, dim3((n + 1 + TB - 1) / TB), dim3(TB), 0, s, *f);
+  size_t need = 0;
+  U4* lens = reinterpret_cast<U4*>(f->lens);
+  U4* offs = reinterpret_cast<U4*>(f->offs);
+  HIP_OK(rocprim::exclusive_scan(nullptr, need, lens, offs, U4{0, 0, 0, 0}, (size_t)n + 1, U4Plus(), s));
+  if (need > f->tmp_bytes) return -1;
+  HIP_OK(rocprim::exclusive_scan(f->tmp, need, lens, offs, U4{0, 0, 0, 0}, (size_t)n + 1, U4Plus(), s));
+  hipLaunchKernelGGL(k_plan_totals, dim3(1), dim3(1), 0, s, *f);
+  return 0;
+}
+
+int apm_dj_write(DJFormatArgs* f, uint32_t n_stats, hipStream_t s) {
+  const uint32_t n = f->n_out;
+  if (n) hipLaunchKernelGGL(k_write, dim3((n + TB - 1) / TB), dim3(TB), 0, s, *f);
+  if (!n_stats) return 0;
+  size_t need = 0;
+  HIP_OK(rocprim::inclusive_scan(nullptr, need, f->tx_bucket, f->tx_bmax, (size_t)n_stats,
+                                 rocprim::maximum<int64_t>(), s));
+  if (need > f->tmp_bytes) return -1;
+  HIP_OK(rocprim::inclusive_scan(f->tmp, need, f->tx_bucket, f->tx_bmax, (size_t)n_stats,
+                                 rocprim::maximum<int64_t>(), s));
+  hipLaunchKernelGGL(k_cands, dim3((n_stats + TB - 1) / TB), dim3(TB), 0, s, *f, n_stats);
+  hipLaunchKernelGGL(k_reset_first, dim3((n_stats + TB - 1) / TB), dim3(TB), 0, s, *f, n_stats);
+  return 0;
+}
+
+void apm_dj_rebuild(const KeyState* old, uint32_t old_cap, KeyState* fresh, uint32_t fresh_mask, const NeedEnt* arena,
+                    uint32_t arena_cap, double now, JoinCounts* counts, unsigned long long* live, hipStream_t s) {
+  hipLaunchKernelGGL(k_rebuild, dim3((old_cap + TB - 1) / TB), dim3(TB), 0, s, old, old_cap, fresh, fresh_mask, arena,
+                     arena_cap, now, counts, live);
+}
+
+int apm_dj_gather_plan(const int64_t* gid, int64_t n_upper, const int64_t* d_n, uint32_t* lens, uint32_t* offs,
+                       void* tmp, size_t tmp_bytes, hipStream_t s) {
+  hipLaunchKernelGGL(k_gather_len, dim3((unsigned)((n_upper + 1 + TB - 1) / TB)), dim3(TB), 0, s, gid, n_upper, d_n, lens);
+  size_t need = 0;
+  HIP_OK(rocprim::exclusive_scan(nullptr, need, lens, offs, 0u, (size_t)n_upper + 1, rocprim::plus<uint32_t>(), s));
+  if (need > tmp_bytes) return -1;
+  HIP_OK(rocprim::exclusive_scan(tmp, need, lens, offs, 0u, (size_t)n_upper + 1, rocprim::plus<uint32_t>(), s));
+  return 0;
+}
+
+void apm_dj_gather_copy(const int64_t* gid, int64_t n, const char* ring, uint64_t ring_cap, const uint32_t* offs,
+                        char* out, hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t threads = n * APM_WAVE;
+  hipLaunchKernelGGL(k_gather_copy, dim3((unsigned)((threads + TB - 1) / TB)), dim3(TB), 0, s, gid, n, ring, ring_cap,
+                     offs, out);
+}
+
+void apm_dj_min_pos(const int64_t* gid, int64_t n, unsigned long long* out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_min_pos, dim3((unsigned)((n + TB - 1) / TB)), dim3(TB), 0, s, gid, n, out);
+}
+
+void apm_dj_relocate(int64_t* gid, int64_t n, char* ring, uint64_t ring_cap, uint64_t below, uint64_t dst_base,
+                     unsigned long long* cursor, hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t threads = n * APM_WAVE;
+  hipLaunchKernelGGL(k_relocate, dim3((unsigned)((threads + TB - 1) / TB)), dim3(TB), 0, s, gid, n, ring, ring_cap,
+                     below, dst_base, cursor);
+}
+
+void apm_dj_reg_fill(RegSlot* reg, const int32_t* pairs, uint32_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_reg_fill, dim3((n + TB - 1) / TB), dim3(TB), 0, s, reg, pairs, n);
+}
+void apm_dj_scatter_i32(int32_t* dst, const int32_t* pairs, uint32_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_scatter_i32, dim3((n + TB - 1) / TB), dim3(TB), 0, s, dst, pairs, n);
+}
+void apm_dj_fill_series(TxRec* tx, const int32_t* raw, uint32_t n, const int32_t* raw_series,
+                        unsigned long long* unmapped, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_fill_series, dim3((n + TB - 1) / TB), dim3(TB), 0, s, tx, raw, n, raw_series, unmapped);
+}
+void apm_dj_gather_u8(const uint8_t* src, const int32_t* idx, uint32_t n, uint8_t* out, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_gather_u8, dim3((n + TB - 1) / TB), dim3(TB), 0, s, src, idx, n, out);
+}
+void apm_dj_count_le(const int64_t* end, int64_t n, int64_t edge, int64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_count_le, dim3(1), dim3(1), 0, s, end, n, edge, out);
+}
+
+}  // extern "C"

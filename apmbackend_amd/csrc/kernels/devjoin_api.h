@@ -1,0 +1,166 @@
+// Launch-side API of the GPU join (devjoin.hip), used by runtime/devjoin.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../apm_types.h"
+#include "devjoin_types.h"
+
+namespace apm {
+
+constexpr int SOAP_SEGS = 16;            // scan segments per SOAP chunk
+constexpr uint32_t DJ_OVF_CAP = 1u << 16; // outputs beyond the first two of one op
+
+struct DJOverflow {
+  uint32_t ev, sub;
+  uint32_t pad[14];
+  TxDev t;
+};
+
+// Everything one batch of the device join touches.  Device pointers unless noted.
+struct DJArgs {
+  // ---- batch inputs
+  const Event* ev;
+  uint32_t n_ev;                  // host-known (parse counts)
+  const uint8_t* bytes;
+  const uint32_t* chunk_file;
+  const uint8_t* chunk_kind;
+  uint32_t n_chunks;
+  const int32_t* chunk_next;      // next chunk of the same file in this batch (-1)
+  const uint8_t* chunk_first;     // 1: first chunk of its file in this batch
+  const int32_t* file_server;     // global file id -> server id
+  const HostOp* hops;
+  uint32_t n_hops;
+  const uint8_t* hbuf;            // host op string bytes
+  double now;
+  uint64_t batch_no;
+  double rec_ttl, acct_ttl, need_ttl;
+  // ---- host-event selection (run right after the parse kernels)
+  uint8_t* host_flag;             // [n_ev]
+  uint32_t* host_pos;             // [n_ev + 1] exclusive scan
+  Event* host_ev;                 // compacted host events
+  uint32_t* host_ev_idx;
+  uint32_t* n_host;               // device count
+  // ---- op build + SOAP scan
+  JOp* ops;                       // [n_ev]
+  uint8_t* soap_code;             // [n_ev]
+  double* soap_num;
+  uint64_t* soap_hash;
+  uint32_t* chunk_ev_lo;          // [n_chunks + 1]
+  uint32_t* seg_f;                // [n_chunks][SOAP_SEGS] composed transition function
+  uint32_t* seg_in;               // incoming state per segment
+  uint64_t* chain_hash;           // per chunk: carried context hash of its file
+  SoapState* soap_state;          // [max files] carried per file
+  // ---- grouping
+  uint32_t* op_slot;              // [n_ev] sort keys (table slot / DIRECT / NONE)
+  uint32_t* op_slot_sorted;
+  uint32_t* op_idx;
+  uint32_t* op_idx_sorted;
+  void* tmp;                      // rocprim scratch
+  size_t tmp_bytes;
+  KeyState* table;
+  uint32_t table_mask;
+  int table_bits;
+  RegSlot* reg;
+  uint32_t reg_mask;
+  RegMiss* miss;
+  uint32_t miss_cap;
+  NeedEnt* arena;
+  uint32_t arena_cap;             // power of two
+  uint64_t arena_base;            // virtual index of this batch's region start
+  uint32_t arena_limit;           // entries this batch may allocate
+  // expiring need entries: virtual ranges [lo, hi) of the regions that expire now
+  const uint64_t* exp_lo;         // device
+  const uint64_t* exp_hi;
+  uint32_t n_exp_regions;
+  uint32_t n_exp_entries;         // host-known total
+  uint64_t* exp_key;              // [n_exp_entries] created (or max for empty)
+  uint64_t* exp_key_sorted;
+  uint32_t* exp_idx;
+  uint32_t* exp_idx_sorted;
+  uint32_t* exp_cnt;
+  uint32_t* exp_pos;
+  // ---- outputs
+  uint32_t* out_cnt;              // [n_ev + 1]
+  uint32_t* out_pos;
+  TxDev* stage;                   // [n_ev][2]
+  DJOverflow* ovf;
+  TxDev* out;                     // merged order
+  uint32_t out_cap;
+  JoinCounts* counts;
+};
+
+// Resolve / format / stats hand-off of the joined tx (after the host registered new services).
+struct DJFormatArgs {
+  TxDev* out;
+  uint32_t n_out;
+  const RegSlot* reg;
+  uint32_t reg_mask;
+  const RawSvc* raw;              // [raw id]
+  const int32_t* raw_series;      // [raw id] -> series (-1: none yet)
+  int32_t* raw_first;             // [raw id] scratch, INT_MAX between batches
+  const char* names;              // join names table
+  const uint8_t* bytes;
+  const uint8_t* hbuf;
+  const NeedEnt* arena;
+  uint32_t arena_cap;
+  // per tx {line length, stats flag, length if not to_db, length if to_db} and their scans
+  uint32_t* lens;                 // [n_out + 1] x 4
+  uint32_t* offs;                 // [n_out + 1] x 4 (exclusive)
+  // ring
+  char* ring;
+  uint64_t ring_cap;              // power of two
+  uint64_t ring_base;             // virtual position of this batch's text
+  // stats hand-off
+  TxRec* tx;                      // [n_stats]
+  int32_t* tx_raw;
+  int64_t* tx_gid;                // ring pos << 20 | len
+  int64_t* tx_bucket;
+  int64_t* tx_bmax;               // inclusive max scan
+  uint32_t* cand;                 // [n] rollover candidates (positions)
+  int64_t* cand_bucket;
+  uint32_t* unresolved;           // first appearances of raw ids with no series
+  char* txt_tx;                   // "transactions" stream (optional)
+  char* txt_db;                   // "audit_db" stream (optional)
+  int want_tx, want_db;
+  JoinCounts* counts;
+  void* tmp;
+  size_t tmp_bytes;
+};
+
+}  // namespace apm
+
+extern "C" {
+size_t apm_dj_tmp_bytes(uint32_t max_ev, uint32_t max_out, int table_bits);
+// parse stream, right after apm_parse_batch: select the events the host resolves and copy
+// them to a compact buffer (count in *a->n_host).
+int apm_dj_select_host(apm::DJArgs* a, const uint32_t* d_n_ev, uint32_t max_ev, hipStream_t s);
+// join stream: ops, SOAP scan, grouping, expiry, group walk, placement; counts -> a->counts.
+int apm_dj_join(apm::DJArgs* a, hipStream_t s);
+// after the host filled the PENDING registry slots: resolve raw ids, line lengths, scans.
+int apm_dj_plan(apm::DJFormatArgs* f, hipStream_t s);
+// text into the ring, stats arrays, rollover candidates, unresolved series, optional streams.
+int apm_dj_write(apm::DJFormatArgs* f, uint32_t n_stats, hipStream_t s);
+// key-table rebuild: live entries of `old` reinserted into `fresh` (zeroed by the caller).
+void apm_dj_rebuild(const apm::KeyState* old, uint32_t old_cap, apm::KeyState* fresh, uint32_t fresh_mask,
+                    const apm::NeedEnt* arena, uint32_t arena_cap, double now, apm::JoinCounts* counts,
+                    unsigned long long* live, hipStream_t s);
+// released lines (gids = ring pos << 20 | len): line lengths + offsets of the first *d_n of
+// n_upper gids (d_n null: all; offs[n_upper] = total bytes), then the copy into `out`
+int apm_dj_gather_plan(const int64_t* gid, int64_t n_upper, const int64_t* d_n, uint32_t* lens, uint32_t* offs,
+                       void* tmp, size_t tmp_bytes, hipStream_t s);
+void apm_dj_gather_copy(const int64_t* gid, int64_t n, const char* ring, uint64_t ring_cap, const uint32_t* offs,
+                        char* out, hipStream_t s);
+// min ring position among gids (for ring reuse); writes UINT64_MAX when n == 0
+void apm_dj_min_pos(const int64_t* gid, int64_t n, unsigned long long* out, hipStream_t s);
+// relocate gids below `below` (virtual ring pos): copy their lines to dst_base.. and rewrite
+void apm_dj_reg_fill(apm::RegSlot* reg, const int32_t* pairs, uint32_t n, hipStream_t s);
+void apm_dj_scatter_i32(int32_t* dst, const int32_t* pairs, uint32_t n, hipStream_t s);
+// stats thread: TxRec.series of tx whose raw service got its series after the batch was joined
+void apm_dj_fill_series(apm::TxRec* tx, const int32_t* raw, uint32_t n, const int32_t* raw_series,
+                        unsigned long long* unmapped, hipStream_t s);
+void apm_dj_gather_u8(const uint8_t* src, const int32_t* idx, uint32_t n, uint8_t* out, hipStream_t s);
+void apm_dj_count_le(const int64_t* end, int64_t n, int64_t edge, int64_t* out, hipStream_t s);
+void apm_dj_relocate(int64_t* gid, int64_t n, char* ring, uint64_t ring_cap, uint64_t below, uint64_t dst_base,
+                     unsigned long long* cursor, hipStream_t s);
+}

@@ -1,0 +1,196 @@
+// Device join (K4/K5/K6 on the GPU): record layouts shared by devjoin.hip and the host driver
+// (runtime/devjoin.cpp).
+//
+// The reference joins a logId's entry, exit and account lines through three TTL caches
+// (stream_parse_transactions.js:211-239 recordCache / acctCache / needNumRecordCache,
+// saveAcctNum :294-327, EJB exit :403-446, CT exit :506-565).  Every cache is keyed by the
+// logId of one JVM, so the join is independent per (server, logId): the GPU groups a batch's
+// join operations by that key (table slot), and one lane replays each group's operations in
+// line order against the key's state, which lives in HBM between batches:
+//   KeyState  -- acct cache entry + recordCache partial map of one key (128 B, one table slot)
+//   NeedEnt   -- needNumRecordCache entry (parked exits waiting for an account), arena-allocated
+//                per batch so a batch's entries expire together (their TTL clock is the batch's)
+// SOAP request contexts (per file) are resolved by a segmented scan over state-transition
+// functions; the audit-trail state machine (K5, rare multi-line blocks) and lines the parser
+// deferred to the host (PM_HOST) are resolved on the host into explicit ops (HostOp).
+#pragma once
+#include <stdint.h>
+
+namespace apm {
+
+// ------------------------------------------------------------------------------ join ops
+enum JOpKind : uint8_t {
+  JOP_NONE = 0,
+  JOP_ENTRY = 1,      // EJB / CommonTiming entry: recordCache[logId][svc] = start
+  JOP_EJB_EXIT = 2,   // EJB exit (logId non-empty)
+  JOP_CT_EXIT = 3,    // CommonTiming exit (logId non-empty), optional BAF account
+  JOP_ACCT = 4,       // saveAcctNum (SOAP account / value line, auditTrailId BAF account)
+  JOP_AUDIT_TX = 5,   // audit-trail stopTime record (parseAppLine :688-729)
+  JOP_DIRECT = 6,     // immediate output, no cache state (EJB exit / CT exit with an empty logId)
+};
+
+enum JOpFlags : uint16_t {
+  JF_TS_EMPTY = 1u << 0,     // end timestamp '' (convertStringDateToMs falsy)
+  JF_START_EMPTY = 1u << 1,  // audit: start timestamp ''
+  JF_BAF = 1u << 2,          // CT exit: BAF account string present (non-empty)
+  JF_BAF_VALID = 1u << 3,    // ... and it is all digits (saveAcctNum accepts it)
+  JF_TO_DB = 1u << 4,        // audit: insertToDb (non-Provider service, Q18)
+  JF_LID_HOST = 1u << 5,     // logId bytes live in the host op buffer (else: the batch bytes)
+  JF_SVC_UNDEF = 1u << 6,    // service token missing: the name is "undefined"
+  JF_SVC_HOST = 1u << 7,     // service name bytes in the host op buffer
+  JF_EJB = 1u << 8,          // EJB service ("S:" prefix, kHashSeedEjb)
+  JF_HAS_SVC = 1u << 9,      // op names a service (registry claim)
+};
+
+// One join operation per relevant event (line order), 80 B.
+struct JOp {
+  uint64_t gkey;     // join key = mix(hash(logId), server) (0: JOP_DIRECT)
+  uint64_t svc;      // raw service hash (seeded by kind)
+  double ts;         // ENTRY: start; EXIT / AUDIT: end (NaN = unparseable)
+  double num;        // EXIT / AUDIT: elapsed; ACCT: account value
+  double aux;        // CT exit: BAF account as output (parseInt); AUDIT: start
+  double aux2;       // CT exit: BAF account as saved; AUDIT: alt account (NaN none)
+  uint32_t line;     // line index in the batch (need-entry creation order)
+  uint32_t lid;      // logId bytes offset (batch bytes, or host buffer with JF_LID_HOST)
+  uint32_t svc_ref;  // service name bytes offset (batch bytes, or host buffer with JF_SVC_HOST)
+  uint16_t lid_len;
+  uint16_t svc_len;
+  int32_t server;
+  uint16_t flags;
+  uint8_t op;
+  uint8_t pad;
+  uint32_t pad2[2];
+};
+static_assert(sizeof(JOp) == 80, "JOp layout");
+
+// Host-resolved op for an event the GPU cannot resolve alone (audit lines, PM_HOST lines, SOAP
+// lines whose fields the host re-derived).  `ev` = event index; sorted by ev.
+enum HostOpKind : uint8_t {
+  HOP_JOIN = 1,       // a full JOp (op.op != JOP_NONE)
+  HOP_SOAP_IN = 2,    // SOAP request start; lid bytes in the host buffer (lid_len 0 + num=1: "undefined")
+  HOP_SOAP_OUT = 3,
+  HOP_SOAP_ACCT = 4,  // op.num = account, flags JF_BAF_VALID when valid
+  HOP_SOAP_KEY = 5,
+  HOP_SOAP_VALUE = 6,
+  HOP_SKIP = 7,       // event produces nothing
+};
+struct HostOp {
+  uint32_t ev;
+  uint8_t kind;
+  uint8_t pad[3];
+  uint64_t lid_hash;  // HOP_SOAP_IN: hash of the logId (or of "undefined")
+  JOp op;
+};
+static_assert(sizeof(HostOp) == 96, "HostOp layout");
+
+// ------------------------------------------------------------------------------ state
+constexpr int KS_PARTS = 5;
+struct KeyState {  // 128 B, one hash-table slot
+  uint64_t key;    // gkey, 0 = empty
+  double acct;
+  double acct_exp;  // acctCache entry live iff acct_exp >= now (-inf: none)
+  double rec_exp;   // recordCache entry live iff rec_exp >= now
+  int32_t need;     // NeedEnt arena index (-1 none)
+  int32_t n_part;
+  uint64_t part_svc[KS_PARTS];
+  double part_start[KS_PARTS];
+  uint64_t pad;
+};
+static_assert(sizeof(KeyState) == 128, "KeyState layout");
+
+constexpr int NEED_ITEMS = 7;
+constexpr int NEED_LID = 80;
+struct NeedItem {   // 48 B
+  uint64_t svc;
+  double start, end, elapsed, alt;
+  uint32_t flags;   // JF_START_EMPTY | JF_TS_EMPTY | JF_TO_DB
+  int32_t pad;
+};
+struct NeedEnt {    // 512 B
+  uint64_t key;
+  double exp;
+  uint64_t created;  // (batch_no << 28) | line
+  int32_t server;
+  int32_t n;         // items
+  int32_t lid_len;
+  int32_t pad;
+  char lid[NEED_LID];
+  NeedItem items[NEED_ITEMS];
+  uint8_t tail[56];
+};
+static_assert(sizeof(NeedEnt) == 512, "NeedEnt layout");
+
+// A completed transaction (outputRecord :264-290) before formatting, 64 B.
+enum : uint8_t { LID_NONE = 0, LID_BATCH = 1, LID_HOST = 2, LID_NEED = 3 };
+struct TxDev {
+  double end;       // endTs after parseInt (NaN: '')
+  double start;     // startTs after the start = end - elapsed fallback and parseInt
+  double acct;
+  double elapsed;
+  uint64_t svc;
+  int32_t server;
+  uint32_t lid;     // logId location (see lid_src)
+  uint16_t lid_len;
+  uint8_t lid_src;
+  uint8_t to_db;
+  int32_t raw;      // raw service id (registry), filled by the resolve pass
+  uint32_t pad[2];
+};
+static_assert(sizeof(TxDev) == 64, "TxDev layout");
+
+// Registry of (server, raw service hash) -> raw service id.  Slot value RAW_PENDING: claimed by
+// the GPU in this batch, the host assigns the id (names are interned on the host).
+constexpr int32_t RAW_EMPTY = -1;
+constexpr int32_t RAW_PENDING = -2;
+struct RegSlot {
+  uint64_t key;     // mix(svc, server) (0 empty)
+  int32_t raw;
+  int32_t pad;
+};
+struct RegMiss {    // a service seen for the first time (name bytes for the host)
+  uint64_t svc;
+  int32_t server;
+  uint32_t name;    // offset (batch bytes, or host buffer with JF_SVC_HOST)
+  uint16_t name_len;
+  uint16_t flags;   // JF_EJB | JF_SVC_UNDEF | JF_SVC_HOST
+  int32_t slot;
+};
+
+// Raw service table (host-filled): names for the tx line and the toplevel flag.
+struct RawSvc {
+  int32_t srv_off, srv_len;   // server name in the join names table
+  int32_t norm_off, norm_len; // normalized service name (Provider[x] -> Provider:x)
+  int32_t toplevel;           // normalized name starts with "S:"
+  int32_t pad;
+};
+
+// Per-file SOAP request context carried across batches.
+struct SoapState {
+  int32_t tag;        // 0 none, 1 present, 2 present + pull_next
+  int32_t undef;      // has_log_id false -> "undefined"
+  uint64_t lid_hash;  // hash(logId) of the context
+};
+
+// Batch counters written by the join kernels (D2H once per batch).
+struct JoinCounts {
+  uint32_t n_ops;
+  uint32_t n_out;          // tx produced (expiries + line emissions)
+  uint32_t n_exp_out;      // of which from expired need entries
+  uint32_t n_miss;         // new raw services
+  uint32_t n_need_new;     // need entries created
+  uint32_t n_keys_new;     // key-table slots claimed
+  uint32_t text_bytes;     // formatted tx text
+  uint32_t n_stats;        // tx handed to the stats stage (non-db, usable endTs)
+  uint32_t n_db;           // audit non-Provider tx (to_db)
+  uint32_t n_dropped;      // NaN / short endTs
+  uint32_t n_cand;         // rollover candidates
+  uint32_t n_unresolved;   // stats tx whose raw service has no series yet (first appearances)
+  uint32_t tx_text_bytes;  // "transactions" stream bytes
+  uint32_t db_text_bytes;  // "audit_db" stream bytes
+  uint32_t pad[2];
+  // sticky counters
+  unsigned long long ejb_unmatched, partial_overflow, need_overflow, expired_partials, need_expired,
+      invalid_acct, table_full, key_probe_max;
+};
+
+}  // namespace apm

@@ -225,6 +225,7 @@ void JoinShard::load(BinReader& rd) {
 
 uint64_t Engine::save_state(const std::string& path) {
   flush();
+  if (dev()) return save_state_dev(path);
   if (prefetched_) throw std::runtime_error("save_state: a prefetched batch is pending (process it first)");
   HIP_OK(hipStreamSynchronize(parse_stream_));
   HIP_OK(hipStreamSynchronize(stream_));
@@ -352,6 +353,7 @@ uint64_t Engine::save_state(const std::string& path) {
 
 void Engine::load_state(const std::string& path) {
   flush();
+  if (dev()) { load_state_dev(path); return; }
   if (batch_no_ != 0 || n_series_ != 0 || !files_.empty())
     throw std::runtime_error("load_state needs a freshly constructed engine (no files, no batches)");
   const int32_t S = cfg_.max_series;
@@ -526,6 +528,14 @@ void Engine::load_state(const std::string& path) {
   rd.finish();
   upload_series_tables(0);
   HIP_OK(hipStreamSynchronize(stream_));
+}
+
+uint64_t Engine::save_state_dev(const std::string&) {
+  throw std::runtime_error("save_state: not yet supported with gpu.joinOnDevice (set it to false to checkpoint)");
+}
+
+void Engine::load_state_dev(const std::string&) {
+  throw std::runtime_error("load_state: not yet supported with gpu.joinOnDevice (set it to false to checkpoint)");
 }
 
 }  // namespace apm

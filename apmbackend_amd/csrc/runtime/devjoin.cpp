@@ -1,0 +1,802 @@
+// Host driver of the GPU join -- see devjoin.h.  The audit-trail state machine and the PM_HOST
+// field re-derivation mirror runtime/join.cpp (JoinShard::on_app / on_ejb / on_ct / on_soap),
+// which stays the reference implementation of the cache semantics (`gpu.joinOnDevice: false`).
+#include "devjoin.h"
+
+#include <algorithm>
+#include <climits>
+#include <cstring>
+#include <stdexcept>
+
+#include "../kernels/common.h"
+#include "../kernels/devjoin_dev.h"
+#include "join_util.h"
+#include "jsutil.h"
+
+namespace apm {
+
+using namespace jstr;
+
+namespace {
+JOp blank_op(const Event& e, int32_t server) {
+  JOp op;
+  std::memset(&op, 0, sizeof(op));
+  op.ts = op.num = op.aux = op.aux2 = js::nan();
+  op.line = e.line;
+  op.server = server;
+  op.op = JOP_NONE;
+  return op;
+}
+
+uint64_t pow2_at_least(uint64_t v) {
+  uint64_t p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+}  // namespace
+
+void* DeviceJoin::dmalloc(size_t bytes) {
+  void* p = nullptr;
+  bytes = (bytes + 255) & ~(size_t)255;
+  HIP_OK(hipMalloc(&p, bytes));
+  HIP_OK(hipMemsetAsync(p, 0, bytes, stream_));
+  allocs_.push_back(p);
+  device_bytes_ += bytes;
+  return p;
+}
+
+DeviceJoin::DeviceJoin(const DevJoinConfig& cfg, Dictionary* dict, const std::vector<FileInfo>* files,
+                       const std::vector<std::string>* servers)
+    : cfg_(cfg), dict_(dict), files_(files), servers_(servers) {
+  cfg_.ring_bytes = pow2_at_least(std::max<uint64_t>(cfg_.ring_bytes, 1ull << 24));
+  cfg_.arena_cap = (uint32_t)pow2_at_least(std::max<uint32_t>(cfg_.arena_cap, 1024));
+  HIP_OK(hipSetDevice(cfg_.device));
+  HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  const uint32_t E = std::max<uint32_t>(cfg_.max_events, 1024);
+  out_cap_ = 2 * E + (1u << 16);
+  for (int k = 0; k < 2; ++k) {
+    Slot& s = sl_[k];
+    s.d_bytes = (uint8_t*)dmalloc(cfg_.max_batch_bytes + 256);
+    s.d_events = (Event*)dmalloc((size_t)E * sizeof(Event));
+    s.host_flag = (uint8_t*)dmalloc(E + 64);
+    s.host_pos = (uint32_t*)dmalloc(((size_t)E + 64) * 4);
+    s.d_host_ev = (Event*)dmalloc((size_t)E * sizeof(Event));
+    s.d_host_idx = (uint32_t*)dmalloc((size_t)E * 4);
+    s.d_n_host = (uint32_t*)dmalloc(64);
+    HIP_OK(hipHostMalloc((void**)&s.h_host_ev, (size_t)E * sizeof(Event), hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void**)&s.h_host_idx, (size_t)E * 4, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void**)&s.h_n_host, 64, hipHostMallocDefault));
+    s.d_chunk_next = (int32_t*)dmalloc(((size_t)cfg_.max_chunks + 2) * 4);
+    s.d_chunk_first = (uint8_t*)dmalloc((size_t)cfg_.max_chunks + 2);
+    HIP_OK(hipHostMalloc((void**)&s.h_chunk_next, ((size_t)cfg_.max_chunks + 2) * 4, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void**)&s.h_chunk_first, (size_t)cfg_.max_chunks + 2, hipHostMallocDefault));
+    s.d_tx = (TxRec*)dmalloc((size_t)out_cap_ * sizeof(TxRec));
+    s.d_tx_raw = (int32_t*)dmalloc((size_t)out_cap_ * 4);
+    s.d_tx_gid = (int64_t*)dmalloc((size_t)out_cap_ * 8);
+    HIP_OK(hipEventCreateWithFlags(&s.free_ev, hipEventDisableTiming));
+  }
+  table_cap_ = 1u << cfg_.table_bits;
+  d_table_ = (KeyState*)dmalloc((size_t)table_cap_ * sizeof(KeyState));
+  d_reg_ = (RegSlot*)dmalloc(((size_t)1 << cfg_.reg_bits) * sizeof(RegSlot));
+  miss_cap_ = E;
+  d_miss_ = (RegMiss*)dmalloc((size_t)miss_cap_ * sizeof(RegMiss));
+  HIP_OK(hipHostMalloc((void**)&h_miss_, (size_t)miss_cap_ * sizeof(RegMiss), hipHostMallocDefault));
+  d_arena_ = (NeedEnt*)dmalloc((size_t)cfg_.arena_cap * sizeof(NeedEnt));
+  d_exp_lo_ = (uint64_t*)dmalloc(8 * 4096);
+  d_exp_hi_ = (uint64_t*)dmalloc(8 * 4096);
+  HIP_OK(hipHostMalloc((void**)&h_exp_, 2 * 8 * 4096, hipHostMallocDefault));
+  soap_cap_ = 1u << 16;
+  d_soap_ = (SoapState*)dmalloc((size_t)soap_cap_ * sizeof(SoapState));
+  d_file_server_ = (int32_t*)dmalloc((size_t)soap_cap_ * 4);
+  d_rawtab_ = (RawSvc*)dmalloc((size_t)cfg_.max_raw * sizeof(RawSvc));
+  d_raw_series_ = (int32_t*)dmalloc((size_t)cfg_.max_raw * 4);
+  d_raw_first_ = (int32_t*)dmalloc((size_t)cfg_.max_raw * 4);
+  HIP_OK(hipMemsetAsync(d_raw_series_, 0xff, (size_t)cfg_.max_raw * 4, stream_));
+  HIP_OK(hipMemsetAsync(d_raw_first_, 0x7f, (size_t)cfg_.max_raw * 4, stream_));
+  raw_info_.reserve(cfg_.max_raw);
+  HIP_OK(hipHostMalloc((void**)&h_rawtab_, (size_t)cfg_.max_raw * sizeof(RawSvc), hipHostMallocDefault));
+  d_reg_fill_ = (int32_t*)dmalloc((size_t)E * 8);
+  HIP_OK(hipHostMalloc((void**)&h_reg_fill_, (size_t)E * 8, hipHostMallocDefault));
+  d_out_ = (TxDev*)dmalloc((size_t)out_cap_ * sizeof(TxDev));
+  d_lens_ = (uint32_t*)dmalloc(((size_t)out_cap_ + 1) * 16);
+  d_offs_ = (uint32_t*)dmalloc(((size_t)out_cap_ + 1) * 16);
+  d_bucket_ = (int64_t*)dmalloc((size_t)out_cap_ * 8);
+  d_bmax_ = (int64_t*)dmalloc((size_t)out_cap_ * 8);
+  d_cand_ = (uint32_t*)dmalloc((size_t)out_cap_ * 4);
+  d_cand_bucket_ = (int64_t*)dmalloc((size_t)out_cap_ * 8);
+  d_unres_ = (uint32_t*)dmalloc((size_t)out_cap_ * 8);
+  HIP_OK(hipHostMalloc((void**)&h_cand_, (size_t)out_cap_ * 4, hipHostMallocDefault));
+  HIP_OK(hipHostMalloc((void**)&h_cand_bucket_, (size_t)out_cap_ * 8, hipHostMallocDefault));
+  HIP_OK(hipHostMalloc((void**)&h_unres_, (size_t)out_cap_ * 8, hipHostMallocDefault));
+  tmp_bytes_ = std::max(apm_dj_tmp_bytes(E, out_cap_, cfg_.table_bits), apm_dj_tmp_bytes(cfg_.arena_cap, out_cap_, cfg_.table_bits));
+  d_tmp_ = dmalloc(tmp_bytes_);
+  sel_tmp_bytes_ = apm_dj_tmp_bytes(E, 1024, 8);
+  d_sel_tmp_ = dmalloc(sel_tmp_bytes_);
+  d_counts_ = (JoinCounts*)dmalloc(sizeof(JoinCounts));
+  HIP_OK(hipHostMalloc((void**)&h_counts_, sizeof(JoinCounts), hipHostMallocDefault));
+  std::memset(h_counts_, 0, sizeof(JoinCounts));
+  d_live_ = (unsigned long long*)dmalloc(64);
+  d_ops_ = (JOp*)dmalloc((size_t)E * sizeof(JOp));
+  d_soap_code_ = (uint8_t*)dmalloc(E);
+  d_soap_num_ = (double*)dmalloc((size_t)E * 8);
+  d_soap_hash_ = (uint64_t*)dmalloc((size_t)E * 8);
+  d_chunk_ev_lo_ = (uint32_t*)dmalloc(((size_t)cfg_.max_chunks + 2) * 4);
+  d_seg_f_ = (uint32_t*)dmalloc(((size_t)cfg_.max_chunks + 2) * SOAP_SEGS * 4);
+  d_seg_in_ = (uint32_t*)dmalloc(((size_t)cfg_.max_chunks + 2) * SOAP_SEGS * 4);
+  d_chain_hash_ = (uint64_t*)dmalloc(((size_t)cfg_.max_chunks + 2) * 8);
+  d_op_slot_ = (uint32_t*)dmalloc(((size_t)E + 1) * 4);
+  d_op_slot_sorted_ = (uint32_t*)dmalloc(((size_t)E + 1) * 4);
+  d_op_idx_ = (uint32_t*)dmalloc(((size_t)E + 1) * 4);
+  d_op_idx_sorted_ = (uint32_t*)dmalloc(((size_t)E + 1) * 4);
+  exp_cap_ = cfg_.arena_cap;
+  d_exp_key_ = (uint64_t*)dmalloc(((size_t)exp_cap_ + 1) * 8);
+  d_exp_key_sorted_ = (uint64_t*)dmalloc(((size_t)exp_cap_ + 1) * 8);
+  d_exp_idx_ = (uint32_t*)dmalloc(((size_t)exp_cap_ + 1) * 4);
+  d_exp_idx_sorted_ = (uint32_t*)dmalloc(((size_t)exp_cap_ + 1) * 4);
+  d_exp_cnt_ = (uint32_t*)dmalloc(((size_t)exp_cap_ + 1) * 4);
+  d_exp_pos_ = (uint32_t*)dmalloc(((size_t)exp_cap_ + 1) * 4);
+  d_out_cnt_ = (uint32_t*)dmalloc(((size_t)E + 1) * 4);
+  d_out_pos_ = (uint32_t*)dmalloc(((size_t)E + 1) * 4);
+  d_stage_ = (TxDev*)dmalloc((size_t)E * 2 * sizeof(TxDev));
+  d_ovf_ = (DJOverflow*)dmalloc((size_t)DJ_OVF_CAP * sizeof(DJOverflow));
+  d_ring_ = (char*)dmalloc(cfg_.ring_bytes);
+  HIP_OK(hipStreamSynchronize(stream_));
+}
+
+DeviceJoin::~DeviceJoin() {
+  hipStreamSynchronize(stream_);
+  for (auto& s : sl_) {
+    hipHostFree(s.h_host_ev); hipHostFree(s.h_host_idx); hipHostFree(s.h_n_host);
+    hipHostFree(s.h_chunk_next); hipHostFree(s.h_chunk_first);
+    hipEventDestroy(s.free_ev);
+  }
+  hipHostFree(h_miss_); hipHostFree(h_exp_); hipHostFree(h_rawtab_); hipHostFree(h_reg_fill_);
+  hipHostFree(h_cand_); hipHostFree(h_cand_bucket_); hipHostFree(h_unres_); hipHostFree(h_counts_);
+  if (h_hops_) hipHostFree(h_hops_);
+  if (h_hbuf_) hipHostFree(h_hbuf_);
+  if (h_txt_) hipHostFree(h_txt_);
+  for (void* p : allocs_) hipFree(p);
+  hipStreamDestroy(stream_);
+}
+
+// ---------------------------------------------------------------------------- parse-side hooks
+void DeviceJoin::select_host(int k, const uint32_t* d_n_ev, uint32_t max_ev, hipStream_t ps) {
+  Slot& s = sl_[k];
+  DJArgs a{};
+  a.ev = s.d_events;
+  a.bytes = s.d_bytes;
+  a.host_flag = s.host_flag;
+  a.host_pos = s.host_pos;
+  a.host_ev = s.d_host_ev;
+  a.host_ev_idx = s.d_host_idx;
+  a.n_host = s.d_n_host;
+  a.tmp = d_sel_tmp_;  // own scratch: the join of the previous batch runs concurrently
+  a.tmp_bytes = sel_tmp_bytes_;
+  if (apm_dj_select_host(&a, d_n_ev, std::min<uint32_t>(max_ev, cfg_.max_events), ps) != 0)
+    throw std::runtime_error("device join: scan scratch too small");
+  HIP_OK(hipMemcpyAsync(s.h_n_host, s.d_n_host, 4, hipMemcpyDeviceToHost, ps));
+  // speculative copy of the host events (last count + 25 %): usually all of them
+  s.spec = std::min<uint32_t>(cfg_.max_events, last_host_ + last_host_ / 4 + 256);
+  HIP_OK(hipMemcpyAsync(s.h_host_ev, s.d_host_ev, (size_t)s.spec * sizeof(Event), hipMemcpyDeviceToHost, ps));
+  HIP_OK(hipMemcpyAsync(s.h_host_idx, s.d_host_idx, (size_t)s.spec * 4, hipMemcpyDeviceToHost, ps));
+}
+
+void DeviceJoin::set_chunks(int k, const std::vector<int32_t>& chunk_file, const uint32_t* d_chunk_file,
+                            const uint8_t* d_chunk_kind, hipStream_t ps) {
+  Slot& s = sl_[k];
+  const uint32_t n = (uint32_t)chunk_file.size();
+  std::unordered_map<int32_t, int32_t> last;
+  for (uint32_t c = 0; c < n; ++c) {
+    s.h_chunk_next[c] = -1;
+    auto it = last.find(chunk_file[c]);
+    if (it == last.end()) {
+      s.h_chunk_first[c] = 1;
+    } else {
+      s.h_chunk_first[c] = 0;
+      s.h_chunk_next[it->second] = (int32_t)c;
+    }
+    last[chunk_file[c]] = (int32_t)c;
+  }
+  if (n) {
+    HIP_OK(hipMemcpyAsync(s.d_chunk_next, s.h_chunk_next, (size_t)n * 4, hipMemcpyHostToDevice, ps));
+    HIP_OK(hipMemcpyAsync(s.d_chunk_first, s.h_chunk_first, n, hipMemcpyHostToDevice, ps));
+  }
+  s.d_chunk_file = d_chunk_file;
+  s.d_chunk_kind = d_chunk_kind;
+  s.n_chunks = n;
+  s.chunk_file = chunk_file;
+}
+
+void DeviceJoin::finish_select(int k, hipStream_t ps) {
+  Slot& s = sl_[k];
+  const uint32_t n = *s.h_n_host;
+  if (n > s.spec) {
+    HIP_OK(hipMemcpyAsync(s.h_host_ev + s.spec, s.d_host_ev + s.spec, (size_t)(n - s.spec) * sizeof(Event),
+                          hipMemcpyDeviceToHost, ps));
+    HIP_OK(hipMemcpyAsync(s.h_host_idx + s.spec, s.d_host_idx + s.spec, (size_t)(n - s.spec) * 4,
+                          hipMemcpyDeviceToHost, ps));
+    HIP_OK(hipStreamSynchronize(ps));
+  }
+  last_host_ = n;
+}
+
+// ---------------------------------------------------------------------------- host pre-pass
+uint32_t DeviceJoin::put_hbuf(std::string_view s) {
+  const uint32_t off = (uint32_t)hbuf_.size();
+  hbuf_.append(s.data(), s.size());
+  return off;
+}
+
+void DeviceJoin::host_prepass(int k, const uint8_t* hb, uint32_t n_host) {
+  Slot& s = sl_[k];
+  hops_.clear();
+  hbuf_.clear();
+  for (uint32_t i = 0; i < n_host; ++i) {
+    const Event& e = s.h_host_ev[i];
+    const int32_t file = s.chunk_file[e.chunk];
+    if (e.mask & PM_HOST) ++host_pm_;
+    host_event(e, s.h_host_idx[i], hb, file);
+  }
+  host_events_ += n_host;
+}
+
+void DeviceJoin::host_event(const Event& e, uint32_t ev, const uint8_t* hb, int32_t file) {
+  const int32_t server = (*files_)[file].server;
+  const std::string_view line((const char*)hb + e.off, e.len);
+  if (e.kind == LK_APP) { on_app(e, ev, line, file, server); return; }
+  HostOp h;
+  std::memset(&h, 0, sizeof(h));
+  h.ev = ev;
+  h.op = blank_op(e, server);
+  JOp& op = h.op;
+  if (e.kind == LK_SOAP) {  // parseSoapLine (:352-376), fields only: the context scan is on the GPU
+    const uint32_t m = e.mask;
+    if (m & PM_SOAP_IN) {
+      auto toks = js::split_ws(line, 4);
+      std::string_view lid;
+      bool has = false;
+      if (toks.size() > 1) {
+        const std::string_view t1 = toks[1];
+        const size_t eq = t1.find('=');
+        if (eq != std::string_view::npos) {
+          const size_t eq2 = t1.find('=', eq + 1);
+          lid = t1.substr(eq + 1, eq2 == std::string_view::npos ? std::string_view::npos : eq2 - eq - 1);
+          has = true;
+        }
+      }
+      h.kind = HOP_SOAP_IN;
+      h.lid_hash = has ? hash_bytes(lid.data(), lid.size()) : hash_bytes("undefined", 9);
+    } else if (m & PM_SOAP_OUT) {
+      h.kind = HOP_SOAP_OUT;
+    } else if ((m & PM_SOAP_ACCT) || (!(m & PM_SOAP_KEY) && (m & PM_SOAP_VALUE))) {
+      const std::string_view acct = js::trim(angle_field2(line));
+      h.kind = (m & PM_SOAP_ACCT) ? HOP_SOAP_ACCT : HOP_SOAP_VALUE;
+      if (all_digits(acct)) { op.flags = JF_BAF_VALID; op.num = js::parse_int(acct); }
+    } else if (m & PM_SOAP_KEY) {
+      h.kind = HOP_SOAP_KEY;
+    } else {
+      return;
+    }
+    hops_.push_back(h);
+    return;
+  }
+  if (e.kind < LK_EJB_ENTRY || e.kind > LK_CT_EXIT) return;
+  // EJB / CommonTiming (:378-565): the host split (PM_HOST lines, bracketed logIds, short lines)
+  const bool ejb = e.kind <= LK_EJB_EXIT;
+  const bool entry = e.kind == LK_EJB_ENTRY || e.kind == LK_CT_ENTRY;
+  auto toks = js::split_ws(line, 16);
+  auto get = [&](size_t i) { return i < toks.size() ? toks[i] : kUndef; };
+  std::string scratch;
+  const std::string lid(strip_brackets(toks[0], scratch));
+  double ts;
+  bool ts_empty = false;
+  {
+    const std::string tsstr = std::string(get(1)) + " " + std::string(get(2));
+    if (!js::convert_date(tsstr, cfg_.tz, ts)) { ts_empty = true; ts = js::nan(); }
+  }
+  std::string_view name;
+  double elapsed = js::nan();
+  if (ejb) {
+    name = get(entry ? 13 : 9);
+    if (!entry && toks.size() > 11) elapsed = js::parse_int(toks[11]);
+  } else {
+    const auto seg = info_segment_tokens(line);
+    name = seg.size() > 1 ? seg[1] : kUndef;
+    if (!entry && seg.size() > 5) elapsed = js::parse_int(seg[5]);
+  }
+  if (entry && lid.empty()) return;  // parseEntry returns before anything else
+  op.svc = hash_bytes(name.data(), name.size(), ejb ? kHashSeedEjb : kHashSeed);
+  op.flags = JF_HAS_SVC | JF_SVC_HOST | (ejb ? JF_EJB : 0);
+  op.svc_ref = put_hbuf(name);
+  op.svc_len = (uint16_t)name.size();
+  op.ts = ts;
+  if (ts_empty) op.flags |= JF_TS_EMPTY;
+  if (!lid.empty()) {
+    op.lid = put_hbuf(lid);
+    op.lid_len = (uint16_t)std::min<size_t>(lid.size(), 0xffff);
+    op.flags |= JF_LID_HOST;
+    op.gkey = dj::gkey_of(hash_bytes(lid.data(), lid.size()), server);
+  }
+  if (entry) {
+    op.op = JOP_ENTRY;
+  } else {
+    op.num = elapsed;
+    if (!ejb) {
+      const bool use_baf = (e.mask & PM_HOST) ? baf_match(line) : (e.mask & PM_BAF) != 0;
+      if (use_baf) {
+        std::string_view t3 = get(3);
+        size_t p = std::string_view::npos;
+        for (size_t i = 0; i + 1 < t3.size(); ++i) if (t3[i] == ']' && t3[i + 1] == '[') p = i;
+        if (p != std::string_view::npos) t3 = t3.substr(p + 2);
+        std::string b;
+        for (char c : t3) if (c != '[' && c != ']') b.push_back(c);
+        const size_t c = b.rfind(':');
+        const std::string acct = c == std::string::npos ? b : b.substr(c + 1);
+        if (!acct.empty()) {
+          op.flags |= JF_BAF;
+          op.aux = js::parse_int(acct);
+          const std::string_view t = js::trim(acct);
+          if (all_digits(t)) { op.flags |= JF_BAF_VALID; op.aux2 = js::parse_int(t); }
+        }
+      }
+    }
+    op.op = lid.empty() ? JOP_DIRECT : (ejb ? JOP_EJB_EXIT : JOP_CT_EXIT);
+    if (lid.empty()) op.gkey = 0;
+  }
+  h.kind = HOP_JOIN;
+  hops_.push_back(h);
+}
+
+// parseAppLine (:578-731): the per-file audit state machine; cache effects become ops.
+void DeviceJoin::on_app(const Event& e, uint32_t ev, std::string_view line, int32_t file, int32_t server) {
+  const uint32_t m = e.mask;
+  auto push = [&](const JOp& op) {
+    HostOp h;
+    std::memset(&h, 0, sizeof(h));
+    h.ev = ev;
+    h.kind = HOP_JOIN;
+    h.op = op;
+    hops_.push_back(h);
+  };
+  if (m & PM_AUTR_MAP) {
+    auto toks = js::split_ws(line, 8);
+    std::string scratch;
+    const std::string log_id(strip_brackets(toks[0], scratch));
+    const std::string_view t5 = toks.size() > 5 ? toks[5] : std::string_view();
+    const size_t eq = t5.find('=');
+    std::string autr;
+    if (eq != std::string_view::npos) {
+      const size_t eq2 = t5.find('=', eq + 1);
+      autr.assign(t5.substr(eq + 1, eq2 == std::string_view::npos ? std::string_view::npos : eq2 - eq - 1));
+    } else {
+      autr = "undefined";
+    }
+    AuditCtx& ctx = audit_[file];
+    // attemptReadAccountNumberFromBAFInfo -> saveAcctNum(acct, 'bafmetainfo', logId)
+    std::string alt;
+    if ((e.mask & PM_HOST) ? baf_match(line) : (e.mask & PM_BAF) != 0) {
+      std::string_view t3 = toks.size() > 3 ? toks[3] : std::string_view();
+      size_t p = std::string_view::npos;
+      for (size_t i = 0; i + 1 < t3.size(); ++i) if (t3[i] == ']' && t3[i + 1] == '[') p = i;
+      if (p != std::string_view::npos) t3 = t3.substr(p + 2);
+      std::string b;
+      for (char c : t3) if (c != '[' && c != ']') b.push_back(c);
+      const size_t c = b.rfind(':');
+      alt = c == std::string::npos ? b : b.substr(c + 1);
+      if (!alt.empty()) {
+        const std::string_view t = js::trim(alt);
+        if (!all_digits(t)) {
+          ++host_invalid_acct_;
+        } else if (!log_id.empty()) {
+          JOp op = blank_op(e, server);
+          op.op = JOP_ACCT;
+          op.gkey = dj::gkey_of(hash_bytes(log_id.data(), log_id.size()), server);
+          op.num = js::parse_int(t);
+          push(op);
+        }
+      }
+    }
+    auto f = std::find_if(ctx.autr_map.begin(), ctx.autr_map.end(), [&](auto& q) { return q.first == autr; });
+    if (f != ctx.autr_map.end()) f->second = {log_id, alt};
+    else ctx.autr_map.push_back({autr, {log_id, alt}});
+    return;
+  }
+  if (m & PM_AUTR_HDR) {
+    auto cit = audit_.find(file);
+    if (cit == audit_.end()) { ++audit_errors_; return; }
+    AuditCtx& ctx = cit->second;
+    const size_t c1 = line.find(':');
+    const size_t c2 = line.find(':', c1 + 1);
+    const std::string autr(js::trim(line.substr(c1 + 1, c2 == std::string_view::npos ? std::string_view::npos : c2 - c1 - 1)));
+    auto f = std::find_if(ctx.autr_map.begin(), ctx.autr_map.end(), [&](auto& q) { return q.first == autr; });
+    if (f == ctx.autr_map.end() || f->second.first.empty()) { ++audit_errors_; return; }
+    ctx.service_map.clear();
+    ctx.active = true;
+    ctx.active_log_id = f->second.first;
+    ctx.active_alt = f->second.second;
+    ctx.elapsed_flag = false;
+    ctx.sw_flag = false;
+    ctx.has_active_service = false;
+    ctx.autr_map.erase(f);
+    return;
+  }
+  auto cit = audit_.find(file);
+  if (cit == audit_.end() || !cit->second.active) return;
+  AuditCtx& ctx = cit->second;
+  if (m & PM_EL_START) { ctx.elapsed_flag = true; return; }
+  if (ctx.elapsed_flag) {
+    if (m & PM_EL_END) { ctx.elapsed_flag = false; return; }
+    const size_t c1 = line.find(':');
+    const std::string service(js::trim(line.substr(0, c1)));
+    std::string elapsed;
+    if (c1 != std::string_view::npos) {
+      const size_t c2 = line.find(':', c1 + 1);
+      const std::string_view a1 = line.substr(c1 + 1, c2 == std::string_view::npos ? std::string_view::npos : c2 - c1 - 1);
+      auto st = js::split_ws(a1, 2);
+      for (char ch : st[0]) if (ch != '[' && ch != ']') elapsed.push_back(ch);
+    }
+    auto f = std::find_if(ctx.service_map.begin(), ctx.service_map.end(), [&](auto& q) { return q.first == service; });
+    if (f == ctx.service_map.end()) { ctx.service_map.push_back({service, {}}); f = ctx.service_map.end() - 1; }
+    f->second.push_back(AuditItem{elapsed, false, std::string()});
+    return;
+  }
+  if (m & PM_SW_START) { ctx.sw_flag = true; return; }
+  if (!ctx.sw_flag) return;
+  if (m & PM_SW_END) {
+    ctx.active = false;
+    ctx.active_log_id.clear();
+    ctx.active_alt.clear();
+    ctx.has_active_service = false;
+    ctx.elapsed_flag = false;
+    ctx.sw_flag = false;
+    ctx.service_map.clear();
+    return;
+  }
+  if (m & PM_SW_NAME) { ctx.active_service = xml_inner(line); ctx.has_active_service = true; return; }
+  if (!ctx.has_active_service || ctx.active_service.empty()) return;
+  const std::string& svcname = ctx.active_service;
+  auto f = std::find_if(ctx.service_map.begin(), ctx.service_map.end(), [&](auto& q) { return q.first == svcname; });
+  if (m & PM_SW_STARTTS) {
+    if (f == ctx.service_map.end() || f->second.empty()) { ++audit_errors_; return; }
+    f->second.front().has_start = true;
+    f->second.front().start_ts = xml_inner(line);
+    return;
+  }
+  if (m & PM_SW_STOPTS) {
+    const std::string end_ts = xml_inner(line);
+    if (f == ctx.service_map.end() || f->second.empty()) { ++audit_errors_; return; }
+    const AuditItem obj = f->second.front();
+    f->second.pop_front();
+    const std::string& log_id = ctx.active_log_id;
+    double s_ms = js::nan(), e_ms = js::nan();
+    const bool s_empty = !obj.has_start || !js::convert_date(obj.start_ts, cfg_.tz, s_ms);
+    const bool e_empty = !js::convert_date(end_ts, cfg_.tz, e_ms);
+    JOp op = blank_op(e, server);
+    op.op = JOP_AUDIT_TX;
+    op.gkey = dj::gkey_of(hash_bytes(log_id.data(), log_id.size()), server);
+    op.svc = hash_bytes(svcname.data(), svcname.size(), kHashSeed);
+    op.ts = e_ms;
+    op.num = js::parse_int(obj.elapsed);
+    op.aux = s_ms;
+    op.aux2 = ctx.active_alt.empty() ? js::nan() : js::parse_int(ctx.active_alt);
+    op.flags = JF_HAS_SVC | JF_SVC_HOST | JF_LID_HOST | (s_empty ? JF_START_EMPTY : 0) | (e_empty ? JF_TS_EMPTY : 0) |
+               (icontains(svcname, "Provider[") ? 0 : JF_TO_DB);
+    op.svc_ref = put_hbuf(svcname);
+    op.svc_len = (uint16_t)svcname.size();
+    op.lid = put_hbuf(log_id);
+    op.lid_len = (uint16_t)std::min<size_t>(log_id.size(), 0xffff);
+    push(op);
+  }
+}
+
+// ---------------------------------------------------------------------------- registration
+int32_t DeviceJoin::intern_name(const std::string& s) {
+  auto it = name_off_.find(s);
+  if (it != name_off_.end()) return it->second;
+  const int32_t off = (int32_t)names_.size();
+  names_ += s;
+  name_off_.emplace(s, off);
+  return off;
+}
+
+void DeviceJoin::register_misses(const uint8_t* hb, uint32_t n_miss, hipStream_t s) {
+  if (n_miss > miss_cap_) throw std::runtime_error("device join: service registry miss list overflow");
+  HIP_OK(hipMemcpyAsync(h_miss_, d_miss_, (size_t)n_miss * sizeof(RegMiss), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  const int32_t first = n_raw_.load(std::memory_order_relaxed);
+  int32_t n = first;
+  for (uint32_t i = 0; i < n_miss; ++i) {
+    const RegMiss& m = h_miss_[i];
+    std::string raw = (m.flags & JF_EJB) ? "S:" : "";
+    if (m.flags & JF_SVC_UNDEF) raw += "undefined";
+    else if (m.flags & JF_SVC_HOST) raw.append(hbuf_.data() + m.name, m.name_len);
+    else raw.append((const char*)hb + m.name, m.name_len);
+    const std::string norm = normalize_service(raw);
+    if ((uint32_t)n >= cfg_.max_raw) throw std::runtime_error("device join: more raw services than gpu.maxRawServices");
+    const int32_t nid = dict_->service_id(norm);
+    raw_info_.push_back(RawInfo{m.server, nid});
+    RawSvc& r = h_rawtab_[n];
+    r.srv_off = intern_name((*servers_)[m.server]);
+    r.srv_len = (int32_t)(*servers_)[m.server].size();
+    r.norm_off = intern_name(norm);
+    r.norm_len = (int32_t)norm.size();
+    r.toplevel = norm.size() >= 2 && norm[0] == 'S' && norm[1] == ':';
+    r.pad = 0;
+    h_reg_fill_[2 * i] = m.slot;
+    h_reg_fill_[2 * i + 1] = n;
+    ++n;
+  }
+  if (names_.size() > names_cap_) {
+    const size_t cap = std::max<size_t>(names_.size() * 2, 1 << 20);
+    char* p = nullptr;
+    HIP_OK(hipMalloc((void**)&p, cap));
+    if (d_names_) {
+      HIP_OK(hipMemcpyAsync(p, d_names_, names_uploaded_, hipMemcpyDeviceToDevice, s));
+      HIP_OK(hipStreamSynchronize(s));
+      HIP_OK(hipFree(d_names_));
+      device_bytes_ -= names_cap_;
+    }
+    d_names_ = p;
+    names_cap_ = cap;
+    device_bytes_ += cap;
+  }
+  if (names_.size() > names_uploaded_) {
+    HIP_OK(hipMemcpyAsync(d_names_ + names_uploaded_, names_.data() + names_uploaded_, names_.size() - names_uploaded_,
+                          hipMemcpyHostToDevice, s));
+    HIP_OK(hipStreamSynchronize(s));  // names_ may reallocate on the next registration
+    names_uploaded_ = names_.size();
+  }
+  HIP_OK(hipMemcpyAsync(d_rawtab_ + first, h_rawtab_ + first, (size_t)(n - first) * sizeof(RawSvc), hipMemcpyHostToDevice, s));
+  HIP_OK(hipMemcpyAsync(d_reg_fill_, h_reg_fill_, (size_t)n_miss * 8, hipMemcpyHostToDevice, s));
+  apm_dj_reg_fill(d_reg_, d_reg_fill_, n_miss, s);
+  n_raw_.store(n, std::memory_order_release);
+}
+
+// ---------------------------------------------------------------------------- ring
+uint64_t DeviceJoin::ring_reserve(uint64_t bytes) {
+  std::lock_guard<std::mutex> g(ring_mu_);
+  const uint64_t cap = cfg_.ring_bytes;
+  if (bytes > cap / 4) throw std::runtime_error("device join: one batch of tx text exceeds a quarter of gpu.txTextRingMB");
+  uint64_t base = ring_head_.load(std::memory_order_relaxed);
+  if ((base & (cap - 1)) + bytes > cap) base = (base + cap - 1) & ~(cap - 1);  // keep the region contiguous
+  const uint64_t low = ring_low_.load(std::memory_order_acquire);
+  if (base + bytes > low + cap)
+    throw std::runtime_error("device join: tx text ring exhausted (pending released-tx lines span more than "
+                             "gpu.txTextRingMB; raise it)");
+  ring_head_.store(base + bytes, std::memory_order_release);
+  return base;
+}
+
+void DeviceJoin::set_ring_low(uint64_t low) {
+  uint64_t cur = ring_low_.load(std::memory_order_relaxed);
+  while (low > cur && !ring_low_.compare_exchange_weak(cur, low)) {
+  }
+}
+
+// ---------------------------------------------------------------------------- batch
+void DeviceJoin::release_slot(int k, hipStream_t stats_stream) {
+  HIP_OK(hipEventRecord(sl_[k].free_ev, stats_stream));
+  sl_[k].used = true;
+}
+
+void DeviceJoin::maybe_rebuild(double now, hipStream_t s) {
+  if ((keys_live_ + keys_since_rebuild_) * 2 < table_cap_) return;
+  // reinsert the live keys (acct / record not expired, or a live need entry) into a fresh table
+  KeyState* fresh = nullptr;
+  HIP_OK(hipMalloc((void**)&fresh, (size_t)table_cap_ * sizeof(KeyState)));
+  HIP_OK(hipMemsetAsync(fresh, 0, (size_t)table_cap_ * sizeof(KeyState), s));
+  HIP_OK(hipMemsetAsync(d_live_, 0, 8, s));
+  apm_dj_rebuild(d_table_, table_cap_, fresh, table_cap_ - 1, d_arena_, cfg_.arena_cap, now, d_counts_, d_live_, s);
+  unsigned long long live = 0;
+  HIP_OK(hipMemcpyAsync(&live, d_live_, 8, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  for (auto& p : allocs_) if (p == d_table_) p = fresh;
+  HIP_OK(hipFree(d_table_));
+  d_table_ = fresh;
+  keys_live_ = live;
+  keys_since_rebuild_ = 0;
+  if (keys_live_ * 2 >= table_cap_)
+    throw std::runtime_error("device join: live join keys exceed half of gpu.joinTableSlots");
+}
+
+void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64_t batch_no, bool want_tx,
+                     bool want_db, DevJoinBatch& out) {
+  Slot& s = sl_[k];
+  hipStream_t st = stream_;
+  if (n_ev > cfg_.max_events) throw std::runtime_error("device join: more events than maxLinesPerBatch");
+  if (s.used) HIP_OK(hipStreamWaitEvent(st, s.free_ev, 0));  // the stats thread is done with the slot
+  events_ += n_ev;
+  // ---- host pre-pass (audit blocks, PM_HOST lines)
+  const uint32_t n_host = *s.h_n_host;
+  host_prepass(k, hb, n_host);
+  if (hops_.size() > h_hops_cap_) {
+    if (h_hops_) HIP_OK(hipHostFree(h_hops_));
+    h_hops_cap_ = hops_.size() * 2 + 1024;
+    HIP_OK(hipHostMalloc((void**)&h_hops_, h_hops_cap_ * sizeof(HostOp), hipHostMallocDefault));
+  }
+  if (hbuf_.size() > h_hbuf_cap_) {
+    if (h_hbuf_) HIP_OK(hipHostFree(h_hbuf_));
+    h_hbuf_cap_ = hbuf_.size() * 2 + (1 << 16);
+    HIP_OK(hipHostMalloc((void**)&h_hbuf_, h_hbuf_cap_, hipHostMallocDefault));
+  }
+  if (hops_.size() > d_hops_cap_) {
+    d_hops_cap_ = hops_.size() * 2 + 1024;
+    HostOp* p = nullptr;
+    HIP_OK(hipMalloc((void**)&p, d_hops_cap_ * sizeof(HostOp)));
+    allocs_.push_back(p);
+    d_hops_ = p;  // the old buffer stays allocated (rare growth)
+  }
+  if (hbuf_.size() > d_hbuf_cap_) {
+    d_hbuf_cap_ = hbuf_.size() * 2 + (1 << 16);
+    uint8_t* p = nullptr;
+    HIP_OK(hipMalloc((void**)&p, d_hbuf_cap_));
+    allocs_.push_back(p);
+    d_hbuf_ = p;
+  }
+  if (!hops_.empty()) {
+    std::memcpy(h_hops_, hops_.data(), hops_.size() * sizeof(HostOp));
+    HIP_OK(hipMemcpyAsync(d_hops_, h_hops_, hops_.size() * sizeof(HostOp), hipMemcpyHostToDevice, st));
+  }
+  if (!hbuf_.empty()) {
+    std::memcpy(h_hbuf_, hbuf_.data(), hbuf_.size());
+    HIP_OK(hipMemcpyAsync(d_hbuf_, h_hbuf_, hbuf_.size(), hipMemcpyHostToDevice, st));
+  }
+  // ---- file -> server table
+  if (files_->size() > files_uploaded_) {
+    if (files_->size() > soap_cap_) throw std::runtime_error("device join: too many files");
+    std::vector<int32_t> fs(files_->size() - files_uploaded_);
+    for (size_t i = files_uploaded_; i < files_->size(); ++i) fs[i - files_uploaded_] = (*files_)[i].server;
+    HIP_OK(hipMemcpyAsync(d_file_server_ + files_uploaded_, fs.data(), fs.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_OK(hipStreamSynchronize(st));
+    files_uploaded_ = files_->size();
+  }
+  // ---- needNumRecordCache regions whose TTL passed (front of the creation-ordered FIFO)
+  uint32_t n_reg = 0, n_exp = 0;
+  while (!regions_.empty() && regions_.front().exp < now && n_reg < 4096) {
+    h_exp_[n_reg] = regions_.front().lo;
+    h_exp_[4096 + n_reg] = regions_.front().hi;
+    n_exp += (uint32_t)(regions_.front().hi - regions_.front().lo);
+    regions_.pop_front();
+    ++n_reg;
+  }
+  if (n_reg) {
+    HIP_OK(hipMemcpyAsync(d_exp_lo_, h_exp_, (size_t)n_reg * 8, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(d_exp_hi_, h_exp_ + 4096, (size_t)n_reg * 8, hipMemcpyHostToDevice, st));
+  }
+  const uint64_t arena_low = regions_.empty() ? arena_head_ : regions_.front().lo;
+  const uint64_t arena_free = (uint64_t)cfg_.arena_cap - (arena_head_ - arena_low);
+  const uint32_t arena_limit = (uint32_t)std::min<uint64_t>(arena_free, cfg_.arena_cap / 2);
+  // ---- join
+  DJArgs& a = a_;
+  a = DJArgs{};
+  a.ev = s.d_events; a.n_ev = n_ev; a.bytes = s.d_bytes;
+  a.chunk_file = s.d_chunk_file; a.chunk_kind = s.d_chunk_kind; a.n_chunks = s.n_chunks;
+  a.chunk_next = s.d_chunk_next; a.chunk_first = s.d_chunk_first; a.file_server = d_file_server_;
+  a.hops = d_hops_; a.n_hops = (uint32_t)hops_.size(); a.hbuf = d_hbuf_;
+  a.now = now; a.batch_no = batch_no;
+  a.rec_ttl = cfg_.record_ttl_ms; a.acct_ttl = cfg_.acct_ttl_ms; a.need_ttl = cfg_.need_ttl_ms;
+  a.host_flag = s.host_flag;
+  a.ops = d_ops_; a.soap_code = d_soap_code_; a.soap_num = d_soap_num_; a.soap_hash = d_soap_hash_;
+  a.chunk_ev_lo = d_chunk_ev_lo_; a.seg_f = d_seg_f_; a.seg_in = d_seg_in_; a.chain_hash = d_chain_hash_;
+  a.soap_state = d_soap_;
+  a.op_slot = d_op_slot_; a.op_slot_sorted = d_op_slot_sorted_; a.op_idx = d_op_idx_; a.op_idx_sorted = d_op_idx_sorted_;
+  a.tmp = d_tmp_; a.tmp_bytes = tmp_bytes_;
+  a.table = d_table_; a.table_mask = table_cap_ - 1; a.table_bits = cfg_.table_bits;
+  a.reg = d_reg_; a.reg_mask = (1u << cfg_.reg_bits) - 1; a.miss = d_miss_; a.miss_cap = miss_cap_;
+  a.arena = d_arena_; a.arena_cap = cfg_.arena_cap; a.arena_base = arena_head_; a.arena_limit = arena_limit;
+  a.exp_lo = d_exp_lo_; a.exp_hi = d_exp_hi_; a.n_exp_regions = n_reg; a.n_exp_entries = n_exp;
+  a.exp_key = d_exp_key_; a.exp_key_sorted = d_exp_key_sorted_; a.exp_idx = d_exp_idx_;
+  a.exp_idx_sorted = d_exp_idx_sorted_; a.exp_cnt = d_exp_cnt_; a.exp_pos = d_exp_pos_;
+  a.out_cnt = d_out_cnt_; a.out_pos = d_out_pos_; a.stage = d_stage_; a.ovf = d_ovf_;
+  a.out = d_out_; a.out_cap = out_cap_; a.counts = d_counts_;
+  if (apm_dj_join(&a, st) != 0) throw std::runtime_error("device join: scan scratch too small");
+  HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));  // ---- sync A
+  const JoinCounts c = *h_counts_;
+  if (c.n_out > out_cap_) throw std::runtime_error("device join: more tx in one batch than the output capacity");
+  if (c.pad[0] > DJ_OVF_CAP) throw std::runtime_error("device join: output overflow list full");
+  if (c.n_need_new) {
+    const uint32_t cnt = std::min(c.n_need_new, arena_limit);
+    regions_.push_back(Region{arena_head_, arena_head_ + cnt, now + cfg_.need_ttl_ms});
+    arena_head_ += cnt;
+  }
+  keys_since_rebuild_ += c.n_keys_new;
+  if (c.n_miss) register_misses(hb, c.n_miss, st);
+  // ---- resolve + plan
+  DJFormatArgs& f = f_;
+  f = DJFormatArgs{};
+  f.out = d_out_; f.n_out = c.n_out; f.reg = d_reg_; f.reg_mask = (1u << cfg_.reg_bits) - 1;
+  f.raw = d_rawtab_; f.raw_series = d_raw_series_; f.raw_first = d_raw_first_; f.names = d_names_;
+  f.bytes = s.d_bytes; f.hbuf = d_hbuf_; f.arena = d_arena_; f.arena_cap = cfg_.arena_cap;
+  f.lens = d_lens_; f.offs = d_offs_; f.ring = d_ring_; f.ring_cap = cfg_.ring_bytes;
+  f.tx = s.d_tx; f.tx_raw = s.d_tx_raw; f.tx_gid = s.d_tx_gid; f.tx_bucket = d_bucket_; f.tx_bmax = d_bmax_;
+  f.cand = d_cand_; f.cand_bucket = d_cand_bucket_; f.unresolved = d_unres_;
+  f.want_tx = want_tx; f.want_db = want_db; f.counts = d_counts_; f.tmp = d_tmp_; f.tmp_bytes = tmp_bytes_;
+  if (apm_dj_plan(&f, st) != 0) throw std::runtime_error("device join: scan scratch too small");
+  HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));  // ---- sync B
+  const JoinCounts c2 = *h_counts_;
+  f.ring_base = ring_reserve(c2.text_bytes);
+  const size_t txt = (size_t)(want_tx ? c2.tx_text_bytes : 0) + (want_db ? c2.db_text_bytes : 0);
+  if (txt > txt_cap_) {
+    const size_t cap = txt * 2 + (1 << 20);
+    char* p = nullptr;
+    HIP_OK(hipMalloc((void**)&p, cap * 2));
+    if (d_txt_tx_) { HIP_OK(hipFree(d_txt_tx_)); device_bytes_ -= txt_cap_ * 2; }
+    d_txt_tx_ = p;
+    d_txt_db_ = p + cap;
+    txt_cap_ = cap;
+    device_bytes_ += cap * 2;
+  }
+  if (txt > h_txt_cap_) {
+    if (h_txt_) HIP_OK(hipHostFree(h_txt_));
+    h_txt_cap_ = txt * 2 + (1 << 20);
+    HIP_OK(hipHostMalloc((void**)&h_txt_, h_txt_cap_, hipHostMallocDefault));
+  }
+  f.txt_tx = d_txt_tx_;
+  f.txt_db = d_txt_db_;
+  if (apm_dj_write(&f, c2.n_stats, st) != 0) throw std::runtime_error("device join: scan scratch too small");
+  const uint32_t spec = std::min<uint32_t>(c2.n_stats, 4096);
+  if (spec) {
+    HIP_OK(hipMemcpyAsync(h_cand_, d_cand_, (size_t)spec * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(h_cand_bucket_, d_cand_bucket_, (size_t)spec * 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(h_unres_, d_unres_, (size_t)spec * 8, hipMemcpyDeviceToHost, st));
+  }
+  if (want_tx && c2.tx_text_bytes)
+    HIP_OK(hipMemcpyAsync(h_txt_, d_txt_tx_, c2.tx_text_bytes, hipMemcpyDeviceToHost, st));
+  if (want_db && c2.db_text_bytes)
+    HIP_OK(hipMemcpyAsync(h_txt_ + (want_tx ? c2.tx_text_bytes : 0), d_txt_db_, c2.db_text_bytes,
+                          hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));  // ---- sync C
+  const JoinCounts c3 = *h_counts_;
+  if (c3.n_cand > spec || c3.n_unresolved > spec) {
+    HIP_OK(hipMemcpyAsync(h_cand_, d_cand_, (size_t)c3.n_cand * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(h_cand_bucket_, d_cand_bucket_, (size_t)c3.n_cand * 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(h_unres_, d_unres_, (size_t)c3.n_unresolved * 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+  }
+  out.slot = k;
+  out.n_out = c3.n_out;
+  out.n_stats = c3.n_stats;
+  out.n_db = c3.n_db;
+  out.n_dropped = c3.n_dropped;
+  out.ring_base = f.ring_base;
+  out.d_tx = s.d_tx;
+  out.d_raw = s.d_tx_raw;
+  out.d_gid = s.d_tx_gid;
+  out.cands.resize(c3.n_cand);
+  out.max_bucket = INT64_MIN;
+  for (uint32_t i = 0; i < c3.n_cand; ++i) {
+    out.cands[i] = {h_cand_[i], h_cand_bucket_[i]};
+    out.max_bucket = std::max(out.max_bucket, h_cand_bucket_[i]);
+  }
+  std::sort(out.cands.begin(), out.cands.end());
+  out.unresolved.resize(c3.n_unresolved);
+  for (uint32_t i = 0; i < c3.n_unresolved; ++i) out.unresolved[i] = {h_unres_[2 * i], (int32_t)h_unres_[2 * i + 1]};
+  std::sort(out.unresolved.begin(), out.unresolved.end());
+  out.text_tx.clear();
+  out.text_db.clear();
+  if (want_tx) out.text_tx.assign(h_txt_, c2.tx_text_bytes);
+  if (want_db) out.text_db.assign(h_txt_ + (want_tx ? c2.tx_text_bytes : 0), c2.db_text_bytes);
+  tx_ += c3.n_out;
+  tx_db_ += c3.n_db;
+  maybe_rebuild(now, st);
+}
+
+JoinCounters DeviceJoin::counters() const {
+  const JoinCounts& c = *h_counts_;
+  JoinCounters t;
+  t.events = events_;
+  t.tx = tx_;
+  t.tx_db = tx_db_;
+  t.expired_partials = c.expired_partials;
+  t.need_expired = c.need_expired;
+  t.ejb_exit_unmatched = c.ejb_unmatched;
+  t.invalid_acct = c.invalid_acct + host_invalid_acct_;
+  t.audit_errors = audit_errors_;
+  t.host_fallback = host_pm_;  // lines the parser deferred (audit lines are host-resolved by design)
+  return t;
+}
+
+}  // namespace apm

@@ -1,0 +1,251 @@
+// Host driver of the GPU join (kernels/devjoin.hip): one per engine.
+//
+// Per batch (ingest thread):
+//   1. the parse stream selects the events the GPU does not resolve alone (apm_dj_select_host)
+//      and copies them to pinned memory with the parse counts;
+//   2. host pre-pass (this file): the audit-trail state machine (parseAppLine :578-731) and the
+//      field re-derivation of PM_HOST lines become HostOps (sorted by event);
+//   3. join kernels (ops, SOAP scan, grouping, expiry, group walk, placement)      -> sync A;
+//   4. new (server, raw service) names are interned on the host and the registry updated;
+//   5. resolve + line lengths + scans                                              -> sync B;
+//   6. tx text into the HBM ring, stats hand-off arrays, rollover candidates       -> sync C.
+// The stats thread then consumes the slot's device arrays (TxRec / raw id / ring gid), exactly
+// where the host join handed it TxOut vectors before.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdint>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../apm_types.h"
+#include "../kernels/devjoin_api.h"
+#include "join.h"
+
+namespace apm {
+
+struct DevJoinConfig {
+  uint32_t max_events = 1u << 21;   // events (relevant lines) per batch
+  uint64_t max_batch_bytes = 64ull << 20;
+  uint32_t max_chunks = 4096;
+  int table_bits = 21;              // key-table slots (KeyState, 128 B)
+  int reg_bits = 20;                // service registry slots
+  uint32_t max_raw = 1u << 20;      // distinct (server, raw service)
+  uint32_t arena_cap = 1u << 20;    // NeedEnt entries (512 B), power of two
+  uint64_t ring_bytes = 4ull << 30; // tx text ring (power of two)
+  double record_ttl_ms = 120000, acct_ttl_ms = 120000, need_ttl_ms = 30000;
+  TzTable tz{};
+  int device = 0;
+};
+
+// Result of one batch for the stats thread (device arrays live in the slot until released).
+struct DevJoinBatch {
+  int slot = 0;
+  uint32_t n_out = 0, n_stats = 0, n_db = 0, n_dropped = 0;
+  std::vector<std::pair<uint32_t, int64_t>> cands;      // (stats position, bucket), ascending
+  std::vector<std::pair<uint32_t, int32_t>> unresolved; // (stats position, raw id), ascending
+  std::string text_tx, text_db;                         // "transactions" / "audit_db" streams
+  uint64_t ring_base = 0;
+  int64_t max_bucket = INT64_MIN;
+  TxRec* d_tx = nullptr;
+  int32_t* d_raw = nullptr;
+  int64_t* d_gid = nullptr;
+};
+
+class DeviceJoin {
+ public:
+  DeviceJoin(const DevJoinConfig& cfg, Dictionary* dict, const std::vector<FileInfo>* files,
+             const std::vector<std::string>* servers);
+  ~DeviceJoin();
+
+  // device buffers the parse kernels of slot k write into
+  uint8_t* d_bytes(int k) { return sl_[k].d_bytes; }
+  Event* d_events(int k) { return sl_[k].d_events; }
+  // after the parse kernels (parse stream): select host events, queue their D2H (speculative)
+  void select_host(int k, const uint32_t* d_n_ev, uint32_t max_ev, hipStream_t ps);
+  // chunk tables of slot k for the SOAP chain (host computes next / first per file)
+  void set_chunks(int k, const std::vector<int32_t>& chunk_file, const uint32_t* d_chunk_file,
+                  const uint8_t* d_chunk_kind, hipStream_t ps);
+  // after the parse stream synced: finish the host-event copy (n_ev known)
+  void finish_select(int k, hipStream_t ps);
+  // the batch join; host_bytes = the host copy of the batch (same layout as d_bytes(k))
+  void run(int k, const uint8_t* host_bytes, uint32_t n_ev, double now, uint64_t batch_no, bool want_tx, bool want_db,
+           DevJoinBatch& out);
+  // the stats thread finished with slot k's arrays (event recorded on its stream)
+  void release_slot(int k, hipStream_t stats_stream);
+
+  // raw service table for the stats thread (append-only, never reallocated)
+  int32_t raw_server(int32_t raw) const { return raw_info_[raw].server; }
+  int32_t raw_service(int32_t raw) const { return raw_info_[raw].norm_id; }
+  int32_t n_raw() const { return n_raw_.load(std::memory_order_acquire); }
+  int32_t* d_raw_series() { return d_raw_series_; }
+
+  // text ring (virtual positions; physical = pos & (cap - 1))
+  char* ring() { return d_ring_; }
+  uint64_t ring_cap() const { return cfg_.ring_bytes; }
+  // stats thread: lowest position still referenced (pool / tail / unprocessed batches)
+  void set_ring_low(uint64_t low);
+  uint64_t ring_head() const { return ring_head_.load(std::memory_order_acquire); }
+  // reserve `bytes` at the ring head (thread-safe; relocation by the stats thread also uses it)
+  uint64_t ring_reserve(uint64_t bytes);
+
+  JoinCounters counters() const;
+  const JoinCounts& last_counts() const { return *h_counts_; }
+  size_t device_bytes() const { return device_bytes_; }
+
+ private:
+  struct Slot {
+    uint8_t* d_bytes = nullptr;
+    Event* d_events = nullptr;
+    uint8_t* host_flag = nullptr;
+    uint32_t* host_pos = nullptr;
+    Event* d_host_ev = nullptr;
+    uint32_t* d_host_idx = nullptr;
+    uint32_t* d_n_host = nullptr;
+    Event* h_host_ev = nullptr;        // pinned
+    uint32_t* h_host_idx = nullptr;    // pinned
+    uint32_t* h_n_host = nullptr;      // pinned
+    uint32_t spec = 0;                 // host events already copied speculatively
+    int32_t* d_chunk_next = nullptr;
+    uint8_t* d_chunk_first = nullptr;
+    int32_t* h_chunk_next = nullptr;   // pinned
+    uint8_t* h_chunk_first = nullptr;  // pinned
+    const uint32_t* d_chunk_file = nullptr;
+    const uint8_t* d_chunk_kind = nullptr;
+    uint32_t n_chunks = 0;
+    std::vector<int32_t> chunk_file;
+    // stats hand-off arrays
+    TxRec* d_tx = nullptr;
+    int32_t* d_tx_raw = nullptr;
+    int64_t* d_tx_gid = nullptr;
+    hipEvent_t free_ev = nullptr;      // recorded by the stats thread after its last use
+    bool used = false;
+  } sl_[2];
+
+  struct AuditItem { std::string elapsed; bool has_start = false; std::string start_ts; };
+  struct AuditCtx {
+    std::vector<std::pair<std::string, std::pair<std::string, std::string>>> autr_map;
+    bool active = false;
+    std::string active_log_id, active_alt, active_service;
+    bool has_active_service = false, elapsed_flag = false, sw_flag = false;
+    std::vector<std::pair<std::string, std::deque<AuditItem>>> service_map;
+  };
+  struct RawInfo { int32_t server; int32_t norm_id; };
+
+  void* dmalloc(size_t bytes);
+  void host_prepass(int k, const uint8_t* host_bytes, uint32_t n_host);
+  void host_event(const Event& e, uint32_t ev, const uint8_t* host_bytes, int32_t file);
+  void on_app(const Event& e, uint32_t ev, std::string_view line, int32_t file, int32_t server);
+  uint32_t put_hbuf(std::string_view s);
+  int32_t intern_name(const std::string& s);
+  void register_misses(const uint8_t* host_bytes, uint32_t n_miss, hipStream_t s);
+  void maybe_rebuild(double now, hipStream_t s);
+
+  DevJoinConfig cfg_;
+  Dictionary* dict_;
+  const std::vector<FileInfo>* files_;
+  const std::vector<std::string>* servers_;
+  hipStream_t stream_ = nullptr;  // join stream
+  size_t device_bytes_ = 0;
+  std::vector<void*> allocs_;
+
+  // host pre-pass output of the current batch
+  std::vector<HostOp> hops_;
+  std::string hbuf_;
+  HostOp* h_hops_ = nullptr;     // pinned
+  uint8_t* h_hbuf_ = nullptr;    // pinned
+  size_t h_hops_cap_ = 0, h_hbuf_cap_ = 0;
+  HostOp* d_hops_ = nullptr;
+  uint8_t* d_hbuf_ = nullptr;
+  size_t d_hops_cap_ = 0, d_hbuf_cap_ = 0;
+  std::unordered_map<int32_t, AuditCtx> audit_;
+  uint32_t last_host_ = 0;
+  void* d_sel_tmp_ = nullptr;  // rocprim scratch of the host-event selection (parse stream)
+  size_t sel_tmp_bytes_ = 0;
+  uint64_t audit_errors_ = 0, host_pm_ = 0, host_invalid_acct_ = 0, host_events_ = 0, events_ = 0, tx_ = 0, tx_db_ = 0;
+
+  // device state
+  DJArgs a_{};
+  DJFormatArgs f_{};
+  KeyState* d_table_ = nullptr;
+  uint32_t table_cap_ = 0;
+  uint64_t keys_since_rebuild_ = 0, keys_live_ = 0;
+  RegSlot* d_reg_ = nullptr;
+  RegMiss* d_miss_ = nullptr;
+  RegMiss* h_miss_ = nullptr;
+  uint32_t miss_cap_ = 0;
+  NeedEnt* d_arena_ = nullptr;
+  uint64_t arena_head_ = 0;      // virtual
+  struct Region { uint64_t lo, hi; double exp; };
+  std::deque<Region> regions_;   // live need regions, creation order
+  uint64_t* d_exp_lo_ = nullptr;
+  uint64_t* d_exp_hi_ = nullptr;
+  uint64_t* h_exp_ = nullptr;    // pinned [2][64]
+  SoapState* d_soap_ = nullptr;
+  uint32_t soap_cap_ = 0;
+  int32_t* d_file_server_ = nullptr;
+  size_t files_uploaded_ = 0;
+  RawSvc* d_rawtab_ = nullptr;
+  int32_t* d_raw_series_ = nullptr;
+  int32_t* d_raw_first_ = nullptr;
+  std::vector<RawInfo> raw_info_;          // reserved to max_raw: stable for the stats thread
+  std::atomic<int32_t> n_raw_{0};
+  std::string names_;
+  std::unordered_map<std::string, int32_t> name_off_;
+  char* d_names_ = nullptr;
+  size_t names_uploaded_ = 0, names_cap_ = 0;
+  int32_t* d_reg_fill_ = nullptr;          // (slot, raw) pairs
+  int32_t* h_reg_fill_ = nullptr;
+  RawSvc* h_rawtab_ = nullptr;
+  // outputs
+  TxDev* d_out_ = nullptr;
+  uint32_t out_cap_ = 0;
+  uint32_t* d_lens_ = nullptr;
+  uint32_t* d_offs_ = nullptr;
+  int64_t* d_bucket_ = nullptr;
+  int64_t* d_bmax_ = nullptr;
+  uint32_t* d_cand_ = nullptr;
+  int64_t* d_cand_bucket_ = nullptr;
+  uint32_t* d_unres_ = nullptr;
+  uint32_t* h_cand_ = nullptr;
+  int64_t* h_cand_bucket_ = nullptr;
+  uint32_t* h_unres_ = nullptr;
+  char* d_txt_tx_ = nullptr;
+  char* d_txt_db_ = nullptr;
+  size_t txt_cap_ = 0;
+  char* h_txt_ = nullptr;
+  size_t h_txt_cap_ = 0;
+  void* d_tmp_ = nullptr;
+  size_t tmp_bytes_ = 0;
+  JoinCounts* d_counts_ = nullptr;
+  JoinCounts* h_counts_ = nullptr;
+  unsigned long long* d_live_ = nullptr;
+  // scratch of the join kernels (sized by max_events)
+  JOp* d_ops_ = nullptr;
+  uint8_t* d_soap_code_ = nullptr;
+  double* d_soap_num_ = nullptr;
+  uint64_t* d_soap_hash_ = nullptr;
+  uint32_t* d_chunk_ev_lo_ = nullptr;
+  uint32_t* d_seg_f_ = nullptr;
+  uint32_t* d_seg_in_ = nullptr;
+  uint64_t* d_chain_hash_ = nullptr;
+  uint32_t *d_op_slot_ = nullptr, *d_op_slot_sorted_ = nullptr, *d_op_idx_ = nullptr, *d_op_idx_sorted_ = nullptr;
+  uint64_t *d_exp_key_ = nullptr, *d_exp_key_sorted_ = nullptr;
+  uint32_t *d_exp_idx_ = nullptr, *d_exp_idx_sorted_ = nullptr, *d_exp_cnt_ = nullptr, *d_exp_pos_ = nullptr;
+  uint32_t exp_cap_ = 0;
+  uint32_t* d_out_cnt_ = nullptr;
+  uint32_t* d_out_pos_ = nullptr;
+  TxDev* d_stage_ = nullptr;
+  DJOverflow* d_ovf_ = nullptr;
+  // ring
+  char* d_ring_ = nullptr;
+  std::mutex ring_mu_;
+  std::atomic<uint64_t> ring_head_{0};
+  std::atomic<uint64_t> ring_low_{0};
+};
+
+}  // namespace apm

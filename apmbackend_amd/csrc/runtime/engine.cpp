@@ -23,6 +23,7 @@
 #include <queue>
 #include <stdexcept>
 
+#include "../kernels/devjoin_api.h"
 #include "../kernels/kernel_api.h"
 #include "format.h"
 
@@ -224,13 +225,50 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipEventCreate(&ev_b_));
   const int32_t S = cfg_.max_series;
   // parse
-  d_bytes_ = (uint8_t*)dmalloc(cfg_.max_batch_bytes + 256);
+  if (cfg_.device_join) {
+    DevJoinConfig dc;
+    dc.max_events = cfg_.max_lines;
+    dc.max_batch_bytes = cfg_.max_batch_bytes;
+    dc.max_chunks = cfg_.max_chunks;
+    dc.table_bits = cfg_.join_table_bits;
+    dc.max_raw = cfg_.max_raw_services;
+    dc.arena_cap = cfg_.need_arena;
+    dc.ring_bytes = cfg_.tx_ring_bytes;
+    dc.record_ttl_ms = cfg_.record_ttl_ms;
+    dc.acct_ttl_ms = cfg_.acct_ttl_ms;
+    dc.need_ttl_ms = cfg_.need_ttl_ms;
+    dc.tz = cfg_.tz;
+    dc.device = cfg_.device;
+    dj_.reset(new DeviceJoin(dc, &dict_, &files_, &servers_));
+    device_bytes_ += dj_->device_bytes();
+    HIP_OK(hipStreamCreateWithFlags(&out_stream_, hipStreamNonBlocking));
+    d_ring_min_ = (unsigned long long*)dmalloc(64);
+    HIP_OK(hipHostMalloc((void**)&h_ring_min_, 64, hipHostMallocDefault));
+    *h_ring_min_ = ~0ULL;
+    d_rel_n_ = (int64_t*)dmalloc(64);
+    HIP_OK(hipHostMalloc((void**)&h_rel_n_, 64, hipHostMallocDefault));
+    d_rel_lens_ = (uint32_t*)dmalloc(((size_t)cfg_.pool_cap + 2) * 4);
+    d_rel_offs_ = (uint32_t*)dmalloc(((size_t)cfg_.pool_cap + 2) * 4);
+    HIP_OK(hipHostMalloc((void**)&h_rel_total_, 64, hipHostMallocDefault));
+    d_unmapped_ = (unsigned long long*)dmalloc(64);
+    d_unseen_idx_ = (int32_t*)dmalloc((size_t)cfg_.max_series * 4);
+    d_unseen_flag_ = (uint8_t*)dmalloc((size_t)cfg_.max_series);
+    HIP_OK(hipHostMalloc((void**)&h_unseen_flag_, (size_t)cfg_.max_series, hipHostMallocDefault));
+  } else {
+    d_bytes_ = (uint8_t*)dmalloc(cfg_.max_batch_bytes + 256);
+  }
   for (int k = 0; k < 2; ++k) {
     ParseSlot& ps = pslot_[k];
     HIP_OK(hipHostMalloc((void**)&ps.h_bytes, cfg_.max_batch_bytes + 256, hipHostMallocDefault));
     HIP_OK(hipHostMalloc((void**)&ps.h_chunk_begin, (cfg_.max_chunks + 2) * 4, hipHostMallocDefault));
     HIP_OK(hipHostMalloc((void**)&ps.h_chunk_kind, cfg_.max_chunks + 2, hipHostMallocDefault));
     HIP_OK(hipHostMalloc((void**)&ps.h_chunk_file, (cfg_.max_chunks + 2) * 4, hipHostMallocDefault));
+    d_chunk_begin_[k] = (uint32_t*)dmalloc((cfg_.max_chunks + 2) * 4);
+    d_chunk_kind_[k] = (uint8_t*)dmalloc(cfg_.max_chunks + 2);
+    d_chunk_file_[k] = (uint32_t*)dmalloc((cfg_.max_chunks + 2) * 4);
+    HIP_OK(hipHostMalloc((void**)&ps.h_counts, 16, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void**)&ps.h_watermark, 8, hipHostMallocDefault));
+    if (dev()) continue;  // the device join keeps events on the GPU
     HIP_OK(hipHostMalloc((void**)&ps.h_events, (size_t)cfg_.max_lines * sizeof(Event), hipHostMallocDefault));
     // APM_EVENTS_ZEROCOPY=1: the compaction kernel writes the events straight into this pinned
     // slot (the copy rides along with the prefetched parse) instead of a 15 MB D2H the ingest
@@ -241,14 +279,9 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     void* dp = nullptr;
     if (zc && std::atoi(zc) != 0 && hipHostGetDevicePointer(&dp, ps.h_events, 0) == hipSuccess)
       ps.d_events_host = (Event*)dp;
-    HIP_OK(hipHostMalloc((void**)&ps.h_counts, 16, hipHostMallocDefault));
-    HIP_OK(hipHostMalloc((void**)&ps.h_watermark, 8, hipHostMallocDefault));
   }
-  d_chunk_begin_ = (uint32_t*)dmalloc((cfg_.max_chunks + 2) * 4);
-  d_chunk_kind_ = (uint8_t*)dmalloc(cfg_.max_chunks + 2);
-  d_chunk_file_ = (uint32_t*)dmalloc((cfg_.max_chunks + 2) * 4);
   d_parse_ws_ = dmalloc(apm_parse_workspace_bytes(cfg_.max_batch_bytes, cfg_.max_lines, cfg_.max_chunks));
-  d_events_ = (Event*)dmalloc((size_t)cfg_.max_lines * sizeof(Event));
+  if (!dev()) d_events_ = (Event*)dmalloc((size_t)cfg_.max_lines * sizeof(Event));
   d_counts_ = (uint32_t*)dmalloc(16);
   d_watermark_ = (unsigned long long*)dmalloc(8);
   d_file_open_ = (uint8_t*)dmalloc(1 << 16);
@@ -329,6 +362,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     d_pool_gid_[i] = (int64_t*)dmalloc((size_t)cfg_.pool_cap * 8);
   }
   release_tmp_bytes_ = apm_release_tmp_bytes(cfg_.pool_cap);
+  if (dev()) release_tmp_bytes_ = std::max(release_tmp_bytes_, apm_dj_tmp_bytes((uint32_t)cfg_.pool_cap + 2, 1024, 8));
   d_release_tmp_ = dmalloc(release_tmp_bytes_);
   for (int k = 0; k < 2; ++k) {
     HIP_OK(hipHostMalloc((void**)&h_release_gid_[k], (size_t)cfg_.pool_cap * 8, hipHostMallocDefault));
@@ -390,7 +424,8 @@ Engine::~Engine() {
   for (void* p : allocations_) hipFree(p);
   for (auto& ps : pslot_) {
     hipHostFree(ps.h_bytes); hipHostFree(ps.h_chunk_begin); hipHostFree(ps.h_chunk_kind); hipHostFree(ps.h_chunk_file);
-    hipHostFree(ps.h_events); hipHostFree(ps.h_counts); hipHostFree(ps.h_watermark);
+    if (ps.h_events) hipHostFree(ps.h_events);
+    hipHostFree(ps.h_counts); hipHostFree(ps.h_watermark);
   }
   hipHostFree(h_alerts_);
   if (h_series_service_) hipHostFree(h_series_service_);
@@ -402,6 +437,14 @@ Engine::~Engine() {
     hipEventDestroy(ev_fmt_[k]);
   }
   if (h_roll_out_) hipHostFree(h_roll_out_);
+  if (dj_) {
+    hipStreamSynchronize(out_stream_);
+    hipHostFree(h_ring_min_); hipHostFree(h_rel_n_); hipHostFree(h_rel_total_); hipHostFree(h_unseen_flag_);
+    for (int k = 0; k < 2; ++k) if (h_rel_text_[k]) hipHostFree(h_rel_text_[k]);
+    if (h_pairs_) hipHostFree(h_pairs_);
+    dj_.reset();
+    hipStreamDestroy(out_stream_);
+  }
   hipHostFree(h_fmt_meta_);
   hipEventDestroy(ev_a_); hipEventDestroy(ev_b_);
   hipStreamDestroy(stream_); hipStreamDestroy(comm_stream_); hipStreamDestroy(parse_stream_);
@@ -555,6 +598,7 @@ void Engine::upload_series_tables(int32_t lo) {
 }
 
 JoinCounters Engine::join_counters() const {
+  if (dj_) return dj_->counters();
   JoinCounters t;
   for (auto& s : shards_) {
     const JoinCounters& c = s->counters;
@@ -632,17 +676,25 @@ void Engine::launch_parse(ParseSlot& ps, const uint8_t* host_bytes, uint64_t n_b
   metrics_.bytes += off;
   ++metrics_.batches;
 
-  // ---- K1/K2 on the GPU (d_bytes_, d_events_, d_counts_ are free: the previous parse was
-  // finished -- its events copied to its own host slot -- before this launch)
-  HIP_OK(hipMemcpyAsync(d_bytes_, ps.hb, off, hipMemcpyHostToDevice, parse_stream_));
-  HIP_OK(hipMemsetAsync(d_bytes_ + off, 0, 64, parse_stream_));
-  HIP_OK(hipMemcpyAsync(d_chunk_begin_, ps.h_chunk_begin, (n_chunks + 1) * 4, hipMemcpyHostToDevice, parse_stream_));
-  HIP_OK(hipMemcpyAsync(d_chunk_kind_, ps.h_chunk_kind, n_chunks + 1, hipMemcpyHostToDevice, parse_stream_));
-  HIP_OK(hipMemcpyAsync(d_chunk_file_, ps.h_chunk_file, (n_chunks + 1) * 4, hipMemcpyHostToDevice, parse_stream_));
-  if (apm_parse_batch(d_bytes_, off, d_chunk_begin_, d_chunk_kind_, d_chunk_file_, n_chunks, d_parse_ws_,
-                      cfg_.max_lines, ps.d_events_host ? ps.d_events_host : d_events_, d_counts_, d_counts_ + 1, d_watermark_, d_file_open_, &cfg_.tz,
+  // ---- K1/K2 on the GPU.  Host join: d_bytes_ / d_events_ are free (the previous parse was
+  // finished -- its events copied to its own host slot -- before this launch).  Device join: the
+  // slot's own device buffers (the other slot's batch may still be joined on the join stream).
+  const int k = (int)(&ps - pslot_);
+  uint8_t* dbytes = dev() ? dj_->d_bytes(k) : d_bytes_;
+  Event* devents = dev() ? dj_->d_events(k) : (ps.d_events_host ? ps.d_events_host : d_events_);
+  HIP_OK(hipMemcpyAsync(dbytes, ps.hb, off, hipMemcpyHostToDevice, parse_stream_));
+  HIP_OK(hipMemsetAsync(dbytes + off, 0, 64, parse_stream_));
+  HIP_OK(hipMemcpyAsync(d_chunk_begin_[k], ps.h_chunk_begin, (n_chunks + 1) * 4, hipMemcpyHostToDevice, parse_stream_));
+  HIP_OK(hipMemcpyAsync(d_chunk_kind_[k], ps.h_chunk_kind, n_chunks + 1, hipMemcpyHostToDevice, parse_stream_));
+  HIP_OK(hipMemcpyAsync(d_chunk_file_[k], ps.h_chunk_file, (n_chunks + 1) * 4, hipMemcpyHostToDevice, parse_stream_));
+  if (apm_parse_batch(dbytes, off, d_chunk_begin_[k], d_chunk_kind_[k], d_chunk_file_[k], n_chunks, d_parse_ws_,
+                      cfg_.max_lines, devents, d_counts_, d_counts_ + 1, d_watermark_, d_file_open_, &cfg_.tz,
                       parse_stream_) != 0)
     throw std::runtime_error("parse workspace too small");
+  if (dev()) {
+    dj_->set_chunks(k, ps.chunk_file, d_chunk_file_[k], d_chunk_kind_[k], parse_stream_);
+    dj_->select_host(k, d_counts_, cfg_.max_lines, parse_stream_);
+  }
   HIP_OK(hipMemcpyAsync(ps.h_counts, d_counts_, 8, hipMemcpyDeviceToHost, parse_stream_));
   HIP_OK(hipMemcpyAsync(ps.h_watermark, d_watermark_, 8, hipMemcpyDeviceToHost, parse_stream_));
   // Prefetched parse: the event count is only known on the device, so copy a guess (the last
@@ -650,7 +702,7 @@ void Engine::launch_parse(ParseSlot& ps, const uint8_t* host_bytes, uint64_t n_b
   // batch's host join instead of on the ingest thread's critical path (15 MB, ~0.3 ms), and
   // finish_parse copies only what the guess missed.
   ps.spec_copied = 0;
-  if (speculative && !ps.d_events_host && spec_events_) {
+  if (speculative && !dev() && !ps.d_events_host && spec_events_) {
     ps.spec_copied = std::min<uint32_t>(spec_events_, cfg_.max_lines);
     HIP_OK(hipMemcpyAsync(ps.h_events, d_events_, (size_t)ps.spec_copied * sizeof(Event), hipMemcpyDeviceToHost,
                           parse_stream_));
@@ -668,7 +720,9 @@ void Engine::finish_parse(ParseSlot& ps) {
   if (ps.n_lines > cfg_.max_lines) throw std::runtime_error("batch has more lines than max_lines");
   metrics_.lines += ps.n_lines;
   metrics_.events += ps.n_events;
-  if (ps.n_events > ps.spec_copied && !ps.d_events_host) {
+  if (dev()) {
+    dj_->finish_select((int)(&ps - pslot_), parse_stream_);
+  } else if (ps.n_events > ps.spec_copied && !ps.d_events_host) {
     const uint32_t lo = ps.spec_copied;
     HIP_OK(hipMemcpyAsync(ps.h_events + lo, d_events_ + lo, (size_t)(ps.n_events - lo) * sizeof(Event),
                           hipMemcpyDeviceToHost, parse_stream_));
@@ -737,6 +791,10 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
     launch_parse(ps, host_bytes, n_bytes, chunks_in);
   }
   finish_parse(ps);
+  if (dev()) {
+    process_batch_dev_tail(ps, t0, now_override, next_bytes, next_n, next_chunks);
+    return;
+  }
   // Pipelining: the next batch's H2D + parse kernels run on the GPU while this batch is joined.
   // Their host side (chunk table, ~15 launches, copies: ~0.3 ms) is issued by this thread while
   // the join workers run, instead of ahead of them on the critical path.
@@ -843,7 +901,9 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
   // lock-step: node-wide watermark (cache clock of the next batch) and newest bucket
   if (lockstep_) {
     const double tl = now_ms();
-    lockstep_sync();
+    int64_t bmax = INT64_MIN;
+    for (size_t k = 0; k < shards_.size(); ++k) bmax = std::max(bmax, shard_maxb_[k * 8]);
+    lockstep_sync(bmax);
     trace_event("lockstep", tl, now_ms(), 0);
   }
 
@@ -854,6 +914,51 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
   const double tp1 = now_ms();
   trace_event("post", tp0, tp1, 0);
   // post_stats returned: the stats thread finished (and packed) every earlier batch
+  if (fleet_comm_) fleet_exchange_upto(fleet_posted_ - 1);
+  trace_event("fleet.exchange", tp1, now_ms(), 0);
+  metrics_.t_total_ms += now_ms() - t0;
+  ++batch_no_;
+}
+
+// Device join (K4/K6 on the GPU): the next batch's parse is launched first (parse stream), then
+// this batch is joined on the join stream while it runs; the stats thread gets device arrays.
+void Engine::process_batch_dev_tail(ParseSlot& ps, double t0, double now_override, const uint8_t* next_bytes,
+                                    uint64_t next_n, const std::vector<Chunk>* next_chunks) {
+  const int k = (int)(&ps - pslot_);
+  if (next_bytes && next_chunks) {
+    launch_parse(pslot_[k ^ 1], next_bytes, next_n, *next_chunks, /*speculative=*/true);
+    prefetched_ = true;
+  }
+  cur_slot_ = k ^ 1;
+  last_n_events_ = ps.n_events;
+  const double t1 = now_ms();
+  roctxRangePop();
+  roctxRangePushA("apm.join");
+  trace_event("parse", t0, t1, 0);
+  const double clock = now_override >= 0 ? now_override : watermark_;
+  DevJoinBatch b;
+  dj_->run(k, ps.hb, ps.n_events, clock, batch_no_, want(OUT_TRANSACTIONS), want(OUT_AUDIT_DB), b);
+  const double t2 = now_ms();
+  metrics_.t_join_ms += t2 - t1;
+  metrics_.t_join_shards_ms += t2 - t1;
+  metrics_.t_shard_max_ms += t2 - t1;
+  metrics_.t_shard_busy_ms += t2 - t1;
+  roctxRangePop();
+  trace_event("join (GPU)", t1, t2, 0);
+  const unsigned long long wm = *ps.h_watermark;
+  if (wm) {
+    const double w = (double)((long long)wm - (1LL << 62));
+    if (w > watermark_) watermark_ = w;
+  }
+  if (lockstep_) {
+    const double tl = now_ms();
+    lockstep_sync(b.max_bucket);
+    trace_event("lockstep", tl, now_ms(), 0);
+  }
+  const double tp0 = now_ms();
+  post_stats_dev(std::move(b), t0, lockstep_ ? sync_latest_ : INT64_MIN);
+  const double tp1 = now_ms();
+  trace_event("post", tp0, tp1, 0);
   if (fleet_comm_) fleet_exchange_upto(fleet_posted_ - 1);
   trace_event("fleet.exchange", tp1, now_ms(), 0);
   metrics_.t_total_ms += now_ms() - t0;
@@ -892,24 +997,30 @@ void Engine::stats_worker() {
       job.text.swap(st_job_.text);
       job.t0 = st_job_.t0;
       job.sync_latest = st_job_.sync_latest;
+      job.dev = st_job_.dev;
+      std::swap(job.dj, st_job_.dj);
       st_has_job_ = false;
     }
     const double t = now_ms();
     roctxRangePushA("apm.stats");
     try {
-      cur_text_ = &job.text;
-      const double tm = now_ms();
-      merge_shard_outputs(job.outs, job.multi, job.txs);
-      trace_event("merge", tm, now_ms(), 1);
-      {  // the shard vectors go back to the ingest thread with their capacity
-        std::lock_guard<std::mutex> g(out_pool_mu_);
-        for (auto& v : job.outs) {
-          v.clear();
-          if (out_pool_.size() < 2 * shards_.size() + 4) out_pool_.push_back(std::move(v));
+      if (job.dev) {
+        stats_for_batch_dev(job.dj, job.t0);
+      } else {
+        cur_text_ = &job.text;
+        const double tm = now_ms();
+        merge_shard_outputs(job.outs, job.multi, job.txs);
+        trace_event("merge", tm, now_ms(), 1);
+        {  // the shard vectors go back to the ingest thread with their capacity
+          std::lock_guard<std::mutex> g(out_pool_mu_);
+          for (auto& v : job.outs) {
+            v.clear();
+            if (out_pool_.size() < 2 * shards_.size() + 4) out_pool_.push_back(std::move(v));
+          }
+          job.outs.clear();
         }
-        job.outs.clear();
+        stats_for_batch(job.txs, job.t0);
       }
-      stats_for_batch(job.txs, job.t0);
       apply_latest_locked(job.sync_latest, job.t0);
       fleet_pack_locked();
       drain_sinks(~kLaneKinds);
@@ -960,6 +1071,26 @@ void Engine::post_stats(std::vector<std::vector<TxOut>>&& outs, bool multi, doub
   if (!cfg_.async_stats) flush();
 }
 
+void Engine::post_stats_dev(DevJoinBatch&& b, double t0, int64_t sync_latest) {
+  std::unique_lock<std::mutex> lk(st_mu_);
+  st_cv_.wait(lk, [&]() { return !st_busy_; });
+  if (!st_error_.empty()) { std::string e = st_error_; st_error_.clear(); throw std::runtime_error(e); }
+  {
+    std::lock_guard<std::mutex> g(out_mu_);
+    if (!out_error_.empty()) { std::string e = out_error_; out_error_.clear(); throw std::runtime_error(e); }
+  }
+  st_job_.dev = true;
+  st_job_.dj = std::move(b);
+  st_job_.t0 = t0;
+  st_job_.sync_latest = sync_latest;
+  if (fleet_comm_) ++fleet_posted_;
+  st_has_job_ = true;
+  st_busy_ = true;
+  lk.unlock();
+  st_cv_.notify_all();
+  if (!cfg_.async_stats) flush();
+}
+
 void Engine::flush() {
   std::unique_lock<std::mutex> lk(st_mu_);
   st_cv_.wait(lk, [&]() { return !st_busy_; });
@@ -972,6 +1103,20 @@ void Engine::flush() {
     if (!out_error_.empty()) { std::string e = out_error_; out_error_.clear(); throw std::runtime_error(e); }
   }
   if (!st_error_.empty()) { std::string e = st_error_; st_error_.clear(); throw std::runtime_error(e); }
+  if (dev()) {
+    unsigned long long u = 0;
+    HIP_OK(hipMemcpyAsync(&u, d_unmapped_, 8, hipMemcpyDeviceToHost, stream_));
+    HIP_OK(hipStreamSynchronize(stream_));
+    metrics_.series_overflow_tx = u;
+  }
+}
+
+std::string Engine::last_events() const {
+  if (!dj_) return std::string((const char*)pslot_[last_slot_].h_events, (size_t)last_n_events_ * sizeof(Event));
+  std::string out((size_t)last_n_events_ * sizeof(Event), '\0');
+  if (last_n_events_)
+    HIP_OK(hipMemcpy(&out[0], const_cast<DeviceJoin&>(*dj_).d_events(last_slot_), out.size(), hipMemcpyDeviceToHost));
+  return out;
 }
 
 // ----------------------------------------------------------------------------- output lane
@@ -1198,6 +1343,96 @@ void Engine::stats_for_batch(std::vector<TxOut>& txs, double batch_t0) {
   append(seg_lo, n, cur_latest);
 }
 
+// Device join: the batch's tx are already on the GPU (TxRec / raw service id / ring gid in the
+// join slot, in single-stream order).  The host only resolves series for raw services seen for the
+// first time (first-appearance order = the reference's object insertion order) and splits the
+// batch at the rollover triggers.
+void Engine::stats_for_batch_dev(DevJoinBatch& b, double batch_t0) {
+  const double ts0 = now_ms();
+  cur_dj_ = &b;
+  metrics_.tx += b.n_out;
+  metrics_.tx_db += b.n_db;
+  metrics_.tx_dropped += b.n_dropped;
+  if (want(OUT_TRANSACTIONS)) blob_[OUT_TRANSACTIONS] += b.text_tx;
+  if (want(OUT_AUDIT_DB)) blob_[OUT_AUDIT_DB] += b.text_db;
+  if (!b.unresolved.empty()) {
+    std::vector<std::pair<int32_t, int32_t>> upd;
+    for (const auto& u : b.unresolved) {
+      const int32_t raw = u.second;
+      if ((size_t)raw >= h_raw_series_.size()) h_raw_series_.resize((size_t)raw + 1, -1);
+      if (h_raw_series_[raw] >= 0) continue;  // resolved meanwhile (the join read a stale -1)
+      const int32_t sr = series_for(dj_->raw_server(raw), dj_->raw_service(raw));
+      if (sr >= 0) { h_raw_series_[raw] = sr; upd.push_back({raw, sr}); }
+    }
+    if (!upd.empty()) {
+      if (upd.size() > pairs_cap_) {
+        if (h_pairs_) HIP_OK(hipHostFree(h_pairs_));
+        pairs_cap_ = upd.size() * 2 + 4096;
+        HIP_OK(hipHostMalloc((void**)&h_pairs_, pairs_cap_ * 8, hipHostMallocDefault));
+        d_pairs_ = (int32_t*)regrow(d_pairs_, pairs_bytes_, pairs_cap_ * 8);
+      }
+      HIP_OK(hipStreamSynchronize(stream_));  // the previous scatter's pinned pairs were consumed
+      for (size_t i = 0; i < upd.size(); ++i) { h_pairs_[2 * i] = upd[i].first; h_pairs_[2 * i + 1] = upd[i].second; }
+      HIP_OK(hipMemcpyAsync(d_pairs_, h_pairs_, upd.size() * 8, hipMemcpyHostToDevice, stream_));
+      apm_dj_scatter_i32(dj_->d_raw_series(), d_pairs_, (uint32_t)upd.size(), stream_);
+    }
+    apm_dj_fill_series(b.d_tx, b.d_raw, b.n_stats, dj_->d_raw_series(), d_unmapped_, stream_);
+  }
+  const int64_t latest_at_start = latest_;
+  std::vector<std::pair<uint32_t, int64_t>> triggers;  // a tx with a newer bucket rolls over first
+  for (const auto& c : b.cands)
+    if (c.second > latest_) { triggers.push_back(c); latest_ = c.second; }
+  metrics_.t_stats_tx_ms += now_ms() - ts0;
+  trace_event("tx loop", ts0, now_ms(), 1);
+  StatsState st{d_counts_cells_, d_cells_, d_spill_n_, d_spill_series_, d_spill_val_, d_active_,
+                cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series};
+  const int64_t keep_iv = cfg_.window + cfg_.buffer;
+  auto append = [&](uint32_t lo, uint32_t hi, int64_t lat) {
+    if (hi <= lo) return;
+    const int64_t min_live = lat - keep_iv;
+    // every live bucket slot is (re)bound: a slot still holding a bucket older than the window is
+    // cleared exactly as the first tx of a new bucket would clear it
+    for (int64_t bk = min_live; bk <= lat; ++bk) ensure_bucket_slot(bk);
+    if (tail_n_ + (int64_t)(hi - lo) > cfg_.pool_cap) throw std::runtime_error("release pool overflow");
+    apm_bucket_append(b.d_tx, lo, hi, &st, min_live, stream_);
+    apm_pool_append(b.d_tx, lo, hi, b.d_gid, d_tail_end_, d_tail_gid_, tail_n_, stream_);
+    tail_n_ += hi - lo;
+  };
+  uint32_t seg_lo = 0;
+  int64_t cur_latest = latest_at_start;
+  for (auto& tr : triggers) {
+    append(seg_lo, tr.first, cur_latest);
+    do_rollover(tr.second, batch_t0);
+    cur_latest = tr.second;
+    seg_lo = tr.first;
+  }
+  append(seg_lo, b.n_stats, cur_latest);
+  dj_->release_slot(b.slot, stream_);
+  cur_dj_ = nullptr;
+}
+
+// K8 needs the z-score settings of series that became visible before this rollover: with the
+// device join the host never sees individual tx, so the `active` flags of the still-unseen series
+// are read back (only while the series set grows).
+void Engine::refresh_unseen_active() {
+  if (unseen_.empty()) return;
+  const uint32_t n = (uint32_t)unseen_.size();
+  if ((size_t)n * 8 > pairs_cap_ * 8) {
+    if (h_pairs_) HIP_OK(hipHostFree(h_pairs_));
+    pairs_cap_ = (size_t)n * 2 + 4096;
+    HIP_OK(hipHostMalloc((void**)&h_pairs_, pairs_cap_ * 8, hipHostMallocDefault));
+    d_pairs_ = (int32_t*)regrow(d_pairs_, pairs_bytes_, pairs_cap_ * 8);
+  }
+  HIP_OK(hipStreamSynchronize(stream_));
+  std::memcpy(h_pairs_, unseen_.data(), (size_t)n * 4);
+  HIP_OK(hipMemcpyAsync(d_unseen_idx_, h_pairs_, (size_t)n * 4, hipMemcpyHostToDevice, stream_));
+  apm_dj_gather_u8(d_active_, d_unseen_idx_, n, d_unseen_flag_, stream_);
+  HIP_OK(hipMemcpyAsync(h_unseen_flag_, d_unseen_flag_, n, hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+  for (uint32_t i = 0; i < n; ++i)
+    if (h_unseen_flag_[i]) h_active_[unseen_[i]] = 1;
+}
+
 void Engine::do_rollover(int64_t L, double batch_t0) {
   const int64_t keep_iv = cfg_.window + cfg_.buffer;
   ++metrics_.rollovers;
@@ -1213,7 +1448,9 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   const int64_t edge_ts = (L - cfg_.buffer - 1) * 10000;
   const double tr0 = now_ms();
   // ---- K9 release: merge the sorted pool with the sorted tail, hand out endTs <= edge
-  {
+  if (dev()) {
+    release_device(edge_ts);
+  } else {
     int64_t released = 0;
     for (auto it = pool_bucket_count_.begin(); it != pool_bucket_count_.end();) {
       if (it->first * 10000 + 9999 <= edge_ts) { released += it->second; it = pool_bucket_count_.erase(it); }
@@ -1259,6 +1496,7 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   const double tr1 = now_ms();
   metrics_.t_release_ms += tr1 - tr0;
   // ---- first st for newly visible series: resolve their z-score settings in emission order
+  if (dev()) refresh_unseen_active();
   {
     std::vector<int32_t> fresh;
     std::vector<int32_t> still;
@@ -1324,6 +1562,7 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   if (want(OUT_SX)) server_rollup(edge_ts);
   HIP_OK(hipMemcpyAsync(h_n_alerts_, d_n_alerts_, 4, hipMemcpyDeviceToHost, stream_));
   HIP_OK(hipStreamSynchronize(stream_));
+  if (dev()) release_device_finish();
   const double tr2 = now_ms();
   metrics_.t_rollover_ms += tr2 - tr1;
   trace_event("release", tr0, tr1, 1);
@@ -1334,6 +1573,68 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   if (want(OUT_SX)) format_server_rollup(edge_ts);
   metrics_.t_format_ms += now_ms() - tr2;
   trace_event("format+sinks", tr2, now_ms(), 1);
+}
+
+// K9 with the device join, part 1 (before K8): merge the tail into the sorted pool, count the
+// released prefix (endTs <= edge) and plan its gather -- all on the stats stream, no host wait.
+void Engine::release_device(int64_t edge_ts) {
+  const int nxt = pool_cur_ ^ 1;
+  if (pool_n_ + tail_n_ > cfg_.pool_cap) throw std::runtime_error("release pool overflow");
+  if (apm_release_merge(d_pool_end_[pool_cur_] + pool_off_, d_pool_gid_[pool_cur_] + pool_off_, pool_n_, d_tail_end_,
+                        d_tail_gid_, tail_n_, d_sort_end_, d_sort_gid_, d_pool_end_[nxt], d_pool_gid_[nxt],
+                        d_release_tmp_, release_tmp_bytes_, stream_) != 0)
+    throw std::runtime_error("release tmp too small");
+  pool_cur_ = nxt;
+  pool_off_ = 0;
+  pool_n_ += tail_n_;
+  tail_n_ = 0;
+  apm_dj_count_le(d_pool_end_[pool_cur_], pool_n_, edge_ts, d_rel_n_, stream_);
+  HIP_OK(hipMemcpyAsync(h_rel_n_, d_rel_n_, 8, hipMemcpyDeviceToHost, stream_));
+  if (want(OUT_DB) && pool_n_ > 0) {
+    if (apm_dj_gather_plan(d_pool_gid_[pool_cur_], pool_n_, d_rel_n_, d_rel_lens_, d_rel_offs_, d_release_tmp_,
+                           release_tmp_bytes_, stream_) != 0)
+      throw std::runtime_error("release tmp too small");
+    HIP_OK(hipMemcpyAsync(h_rel_total_, d_rel_offs_ + pool_n_, 4, hipMemcpyDeviceToHost, stream_));
+  }
+}
+
+// Part 2 (after the rollover's stream sync): the released count is known; gather the lines out
+// of the HBM text ring into one blob, D2H it on the output lane, and publish the lowest ring
+// position still referenced so the ingest thread may reuse the ring below it.
+void Engine::release_device_finish() {
+  const int64_t released = std::min<int64_t>(*h_rel_n_, pool_n_);
+  if (want(OUT_DB) && released > 0) {
+    const size_t total = *h_rel_total_;
+    const int k = rel_k_;
+    rel_k_ ^= 1;
+    out_wait(rel_task_[k]);  // the buffer's previous reader is done
+    if (total + 64 > rel_text_cap_[k]) d_rel_text_[k] = (char*)regrow(d_rel_text_[k], rel_text_cap_[k], total + 64);
+    apm_dj_gather_copy(d_pool_gid_[pool_cur_], released, dj_->ring(), dj_->ring_cap(), d_rel_offs_, d_rel_text_[k], stream_);
+    HIP_OK(hipEventRecord(ev_rel_[k], stream_));
+    rel_task_[k] = post_out([this, k, total]() {
+      HIP_OK(hipEventSynchronize(ev_rel_[k]));
+      if (total > h_rel_text_cap_[k]) {
+        if (h_rel_text_[k]) HIP_OK(hipHostFree(h_rel_text_[k]));
+        h_rel_text_cap_[k] = total * 3 / 2 + (1 << 20);
+        HIP_OK(hipHostMalloc((void**)&h_rel_text_[k], h_rel_text_cap_[k], hipHostMallocDefault));
+      }
+      HIP_OK(hipMemcpyAsync(h_rel_text_[k], d_rel_text_[k], total, hipMemcpyDeviceToHost, out_stream_));
+      HIP_OK(hipStreamSynchronize(out_stream_));
+      emit_bytes(OUT_DB, h_rel_text_[k], total);
+    });
+  }
+  metrics_.released += released;
+  pool_off_ = released;
+  pool_n_ -= released;
+  // ring reuse bound: min position of the pool as of the previous rollover (its D2H is done)
+  // and the ring base of the batch being processed then
+  const uint64_t prev_min = *h_ring_min_;
+  const uint64_t low = std::min<uint64_t>(prev_min, ring_low_pending_);
+  if (low != UINT64_MAX) dj_->set_ring_low(low);
+  HIP_OK(hipMemsetAsync(d_ring_min_, 0xff, 8, stream_));
+  apm_dj_min_pos(d_pool_gid_[pool_cur_] + pool_off_, pool_n_, d_ring_min_, stream_);
+  HIP_OK(hipMemcpyAsync(h_ring_min_, d_ring_min_, 8, hipMemcpyDeviceToHost, stream_));
+  ring_low_pending_ = cur_dj_ ? cur_dj_->ring_base : dj_->ring_head();
 }
 
 void Engine::flush_alerts(int64_t edge_ts) {
@@ -1882,14 +2183,12 @@ void Engine::coll_wait(hipStream_t s, hipEvent_t ev, const char* what) {
 // the next batch, and the node-wide newest bucket decides this batch's rollovers.  The bucket is
 // the one stats_for_batch derives (non-db tx with a usable endTs), so ranks agree on `latest`
 // without the stats thread touching the communicator.
-void Engine::lockstep_sync() {
+void Engine::lockstep_sync(int64_t batch_max) {
   if (comm_aborted_) throw std::runtime_error("RCCL communicator was aborted");
-  int64_t b = sync_latest_;
-  for (size_t k = 0; k < shards_.size(); ++k) b = std::max(b, shard_maxb_[k * 8]);
-  if (fleet_nranks_ == 1) {  // MAX over one rank is the identity: no device round trip
-    if (b != INT64_MIN) sync_latest_ = std::max(sync_latest_, b);
-    return;
-  }
+  const int64_t b = std::max(sync_latest_, batch_max);
+  // The collective runs at every world size, N = 1 included (MAX over one rank is the identity,
+  // but the single-GPU run then does the same per-batch work -- H2D, all-reduce, D2H, wait --
+  // as each rank of an 8-GPU node, and this path stays exercised by the 1-GPU tests).
   h_sync_[0] = watermark_;
   h_sync_[1] = b == INT64_MIN ? -1.0 : (double)b;  // buckets < 2^53: exact in a double
   HIP_OK(hipMemcpyAsync(d_sync_, h_sync_, 16, hipMemcpyHostToDevice, coll_stream_));

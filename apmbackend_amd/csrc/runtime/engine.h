@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "../apm_types.h"
+#include "devjoin.h"
 #include "join.h"
 
 namespace apm {
@@ -87,6 +88,12 @@ struct EngineConfig {
   // RCCL watchdog: a collective not complete after this long (a dead or wedged peer) aborts the
   // communicator and throws, so the supervisor restarts the rank group from its checkpoint
   double coll_timeout_ms = 300000;
+  // K4/K6 on the GPU (devjoin.hip); 0 = host join workers (join.cpp)
+  int device_join = 1;
+  int join_table_bits = 21;          // key-table slots (128 B each)
+  uint32_t need_arena = 1u << 18;    // needNumRecordCache entries (512 B each)
+  uint64_t tx_ring_bytes = 4ull << 30;  // HBM text ring of pending (unreleased) tx lines
+  uint32_t max_raw_services = 1u << 20;
 };
 
 // Output streams (queue names of the reference, config/apm_config.json:12,87,99-100,113-114,178):
@@ -130,6 +137,7 @@ struct EngineMetrics {
   uint64_t batches = 0, bytes = 0, lines = 0, events = 0, tx = 0, tx_db = 0, tx_dropped = 0;
   uint64_t rollovers = 0, alerts = 0, alert_candidates = 0, series = 0, released = 0;
   uint64_t formatted_bytes = 0, format_fallbacks = 0, lockstep_rollovers = 0;
+  uint64_t series_overflow_tx = 0;  // tx whose series could not be created (gpu.maxSeries full)
   double t_parse_ms = 0, t_join_ms = 0, t_stats_ms = 0, t_total_ms = 0;
   double t_join_shards_ms = 0, t_merge_ms = 0;                 // split of t_join_ms
   double t_shard_busy_ms = 0, t_shard_max_ms = 0;              // per batch: mean / max of one shard's join
@@ -259,9 +267,7 @@ class Engine {
   JoinCounters join_counters() const;
 
   // events of the last batch (host copy) for kernel verification
-  std::string last_events() const {
-    return std::string((const char*)pslot_[last_slot_].h_events, (size_t)last_n_events_ * sizeof(Event));
-  }
+  std::string last_events() const;
   // pinned host memory for zero-copy ingest (bench corpus, tailer)
   static uintptr_t alloc_pinned(size_t n);
   static void free_pinned(uintptr_t p);
@@ -276,6 +282,13 @@ class Engine {
   void apply_series_settings(int32_t s);
   void compute_series_settings(int32_t s, double* thr, double* infl, double& hard_max, uint8_t& suppressed);
   void stats_for_batch(std::vector<TxOut>& txs, double batch_t0);
+  void stats_for_batch_dev(DevJoinBatch& b, double batch_t0);
+  void post_stats_dev(DevJoinBatch&& b, double t0, int64_t sync_latest);
+  void release_device(int64_t edge_ts);   // K9 with the device join: count + gather on the GPU
+  void release_device_finish();
+  void refresh_unseen_active();
+  uint64_t save_state_dev(const std::string& path);
+  void load_state_dev(const std::string& path);
   void ensure_bucket_slot(int64_t b);
   void do_rollover(int64_t L, double batch_t0);
   void flush_alerts(int64_t edge_ts);
@@ -291,7 +304,7 @@ class Engine {
   void fleet_exchange_upto(uint64_t rounds);
   void coll_check(ncclResult_t r, const char* what);
   void coll_wait(hipStream_t s, hipEvent_t ev, const char* what);
-  void lockstep_sync();
+  void lockstep_sync(int64_t batch_max_bucket);
   void apply_latest_locked(int64_t g, double batch_t0);
   void stats_worker();
   void post_stats(std::vector<std::vector<TxOut>>&& outs, bool multi, double t0, int64_t sync_latest = INT64_MIN);
@@ -340,6 +353,8 @@ class Engine {
     bool multi = false;
     std::vector<TxOut> txs; std::vector<std::string> text; double t0 = 0;
     int64_t sync_latest = INT64_MIN;  // lock-step: node-wide newest bucket after this batch
+    bool dev = false;                 // device join: `dj` instead of outs / txs
+    DevJoinBatch dj;
   };
   std::vector<std::string>* cur_text_ = nullptr;  // text arenas of the job being processed
   std::thread stats_thread_;
@@ -400,6 +415,32 @@ class Engine {
   std::vector<uint8_t> h_active_;               // host mirror of the stats `active` flag
   std::vector<int32_t> unseen_;                 // series not yet initialised in the z-score stage
 
+  // device join (cfg_.device_join): tables, ring, per-slot batch buffers
+  std::unique_ptr<DeviceJoin> dj_;
+  const DevJoinBatch* cur_dj_ = nullptr;       // stats thread: batch being processed
+  uint64_t ring_low_pending_ = UINT64_MAX;     // ring base of the batch at the last min_pos launch
+  unsigned long long* d_ring_min_ = nullptr;
+  unsigned long long* h_ring_min_ = nullptr;
+  int64_t* d_rel_n_ = nullptr;
+  int64_t* h_rel_n_ = nullptr;
+  uint32_t* d_rel_lens_ = nullptr;
+  uint32_t* d_rel_offs_ = nullptr;
+  uint32_t* h_rel_total_ = nullptr;            // [2]
+  char* d_rel_text_[2] = {nullptr, nullptr};
+  size_t rel_text_cap_[2] = {0, 0};
+  char* h_rel_text_[2] = {nullptr, nullptr};
+  size_t h_rel_text_cap_[2] = {0, 0};
+  hipStream_t out_stream_ = nullptr;
+  std::vector<int32_t> h_raw_series_;          // stats thread mirror of the raw -> series table
+  int32_t* h_pairs_ = nullptr;                 // pinned (index, value) pairs for small scatters
+  int32_t* d_pairs_ = nullptr;
+  size_t pairs_cap_ = 0, pairs_bytes_ = 0;
+  int32_t* d_unseen_idx_ = nullptr;
+  uint8_t* d_unseen_flag_ = nullptr;
+  uint8_t* h_unseen_flag_ = nullptr;
+  unsigned long long* d_unmapped_ = nullptr;
+  bool dev() const { return dj_ != nullptr; }
+
   // parse buffers
   uint8_t* d_bytes_ = nullptr;
   // double-buffered parse slots (host side): staging bytes, chunk tables, events, counters
@@ -425,10 +466,12 @@ class Engine {
   bool prefetched_ = false;
   void launch_parse(ParseSlot& ps, const uint8_t* host_bytes, uint64_t n_bytes, const std::vector<Chunk>& chunks,
                     bool speculative = false);
+  void process_batch_dev_tail(ParseSlot& ps, double t0, double now_override, const uint8_t* next_bytes,
+                              uint64_t next_n, const std::vector<Chunk>* next_chunks);
   void finish_parse(ParseSlot& ps);
-  uint32_t* d_chunk_begin_ = nullptr;
-  uint8_t* d_chunk_kind_ = nullptr;
-  uint32_t* d_chunk_file_ = nullptr;
+  uint32_t* d_chunk_begin_[2] = {nullptr, nullptr};  // per parse slot (the device join reads them)
+  uint8_t* d_chunk_kind_[2] = {nullptr, nullptr};
+  uint32_t* d_chunk_file_[2] = {nullptr, nullptr};
   void* d_parse_ws_ = nullptr;
   Event* d_events_ = nullptr;
   uint32_t* d_counts_ = nullptr;                // [0]=n_events [1]=n_lines

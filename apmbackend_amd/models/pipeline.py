@@ -85,6 +85,14 @@ def engine_config(cfg: Dict[str, Any], device: int = 0, keep_text: bool = False,
         "join_threads": int(g.get("joinThreads", 0)),
         "pin_threads": bool(g.get("pinThreads", False)),
         "coll_timeout_ms": float(g.get("collectiveTimeoutSeconds", 300)) * 1000.0,
+        # K4/K6 join on the GPU (devjoin.hip); false = host join workers (join.cpp)
+        "device_join": 1 if g.get("joinOnDevice", True) else 0,
+        "join_table_bits": max(10, (int(g.get("joinTableSlots", 1 << 21)) - 1).bit_length()),
+        "need_arena": int(g.get("needArenaEntries", 1 << 18)),
+        # the ring holds every tx line not yet released (~70 s of tx text); small test engines
+        # keep it proportional to their batch size
+        "tx_ring_bytes": min(int(g.get("txTextRingMB", 4096)), max(256, (128 * int(g.get("batchBytes", 32 << 20))) >> 20)) << 20,
+        "max_raw_services": max(int(g.get("maxRawServices", 1 << 18)), 2 * int(g.get("maxSeries", 1 << 17))),
         "outputs": output_mask(OUT_KINDS if keep_text else (outputs or ())),
     }
     if int(sc["intervalLengthInSeconds"]) != 10:
