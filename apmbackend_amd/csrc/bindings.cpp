@@ -148,6 +148,7 @@ py::dict metrics_dict(const EngineMetrics& m) {
   d["t_parse_ms"] = m.t_parse_ms; d["t_join_ms"] = m.t_join_ms; d["t_stats_ms"] = m.t_stats_ms;
   d["t_total_ms"] = m.t_total_ms;
   d["series_overflow_tx"] = m.series_overflow_tx;
+  d["spill_dropped"] = m.spill_dropped;
   d["rollover_latency_ms"] = m.rollover_latency_ms;
   return d;
 }

@@ -36,27 +36,41 @@ __host__ __device__ inline int put_dec(char* p, unsigned __int128 v) {
   return n;
 }
 
-__host__ __device__ inline int dec_len(unsigned __int128 v) {
+__host__ __device__ inline int u64_digits(uint64_t v) {
   int n = 1;
-  while (v >= 10) { v /= 10; ++n; }
+  uint64_t p = 10;
+  while (n < 20 && v >= p) { ++n; p *= 10; }
   return n;
+}
+
+// n decimal digits of v at p (64-bit constant divisions: multiply-high, no 128-bit arithmetic)
+__host__ __device__ inline void u64_write(char* p, uint64_t v, int n) {
+  for (int i = n - 1; i >= 0; --i) { p[i] = (char)('0' + (int)(v % 10)); v /= 10; }
 }
 
 __host__ __device__ inline int js_num(char* p, double x, bool* inexact) {
   // p == nullptr: length only
+  if (x != x) { if (p) { p[0] = 'N'; p[1] = 'a'; p[2] = 'N'; } return 3; }
+  const bool neg = x < 0;
+  const double ax = neg ? -x : x;
+  if (ax < 18014398509481984.0 && ax == floor(ax)) {  // integral, < 2^54: the common case
+    if (ax == 0) { if (p) p[0] = '0'; return 1; }    // -0 prints "0"
+    const uint64_t v = (uint64_t)ax;
+    const int nd = u64_digits(v);
+    if (p) {
+      if (neg) p[0] = '-';
+      u64_write(p + (neg ? 1 : 0), v, nd);
+    }
+    return nd + (neg ? 1 : 0);
+  }
   char buf[64];
   char* o = p ? p : buf;
-  if (x != x) { if (p) { o[0] = 'N'; o[1] = 'a'; o[2] = 'N'; } return 3; }
   int n = 0;
-  if (x < 0) { o[n++] = '-'; x = -x; }
+  if (neg) { o[n++] = '-'; x = ax; }
   if (x == __builtin_inf()) {
     const char* s = "Infinity";
     for (int i = 0; i < 8; ++i) o[n + i] = s[i];
     return n + 8;
-  }
-  if (x == 0) { o[0] = '0'; return 1; }  // -0 prints "0"
-  if (x < 18014398509481984.0 && x == floor(x)) {  // < 2^54
-    return n + put_dec(o + n, (unsigned __int128)(uint64_t)x);
   }
   if (x < 1.7014118346046923e38 && x == floor(x)) {  // < 2^127
     int e2;

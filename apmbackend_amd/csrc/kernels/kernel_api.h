@@ -19,6 +19,7 @@ struct StatsState {
   int32_t cap;
   int32_t spill_cap;
   int32_t S;
+  unsigned long long* spill_drop = nullptr;  // samples lost to a full spill list (reported)
 };
 
 struct WindowArgs {

@@ -47,6 +47,8 @@ __global__ void k_bucket_append(const TxRec* __restrict__ tx, uint32_t lo, uint3
     if (j < st.spill_cap) {
       st.spill_series[(size_t)slot * st.spill_cap + j] = r.series;
       st.spill_val[(size_t)slot * st.spill_cap + j] = r.elapsed;
+    } else if (st.spill_drop) {
+      atomicAdd(st.spill_drop, 1ULL);
     }
   }
 }
@@ -191,6 +193,79 @@ __global__ __launch_bounds__(WS_WAVES * APM_WAVE) void k_window_stats(WindowArgs
   if (lane == 0) finish_series(a, s, n, sum, t);
 }
 
+// Every sample of series s in the window (inline cells + spill lists), visited by the block.
+template <class F>
+__device__ __forceinline__ void for_each_window_sample(const WindowArgs& a, int s, F&& f) {
+  for (int r = 0; r < a.n_win; ++r) {
+    const int sl = a.win_slots[r];
+    if (sl < 0) continue;
+    const int cnt = a.st.counts[(size_t)sl * a.st.S + s];
+    const int inl = min(cnt, a.st.cap);
+    const int32_t* cell = a.st.cells + ((size_t)sl * a.st.S + s) * a.st.cap;
+    for (int k = threadIdx.x; k < inl; k += blockDim.x) f(cell[k]);
+    if (cnt > inl) {
+      const int ns = min(a.st.spill_n[sl], a.st.spill_cap);
+      for (int j = threadIdx.x; j < ns; j += blockDim.x)
+        if (a.st.spill_series[(size_t)sl * a.st.spill_cap + j] == s) f(a.st.spill_val[(size_t)sl * a.st.spill_cap + j]);
+    }
+  }
+}
+
+// Exact k-th smallest samples for windows beyond BIG_TILE: radix select, 8 bits per pass, the
+// up to four ranks of the p75 / p95 formula (percentile_ranks) selected together.  `scratch`
+// holds 4 x 256 histogram bins (the LDS tile of the caller).
+__device__ void window_select(const WindowArgs& a, int s, int n, long long sum, int32_t* scratch) {
+  __shared__ uint32_t prefix[4];
+  __shared__ int32_t want[4];
+  int ranks[4];
+  percentile_ranks(n, 75, ranks[0], ranks[1]);
+  percentile_ranks(n, 95, ranks[2], ranks[3]);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(scratch);
+  if (threadIdx.x < 4) { prefix[threadIdx.x] = 0; want[threadIdx.x] = ranks[threadIdx.x]; }
+  __syncthreads();
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = 24 - 8 * pass;
+    const uint32_t hi_mask = pass == 0 ? 0u : ~((1u << (shift + 8)) - 1u);
+    for (int i = threadIdx.x; i < 4 * 256; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    uint32_t pf[4];
+    for (int r = 0; r < 4; ++r) pf[r] = prefix[r];
+    for_each_window_sample(a, s, [&](int32_t v) {
+      const uint32_t u = (uint32_t)v ^ 0x80000000u;  // order-preserving unsigned key
+      const uint32_t bin = (u >> shift) & 255u;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if ((u & hi_mask) == (pf[r] & hi_mask)) atomicAdd(&hist[r * 256 + bin], 1u);
+    });
+    __syncthreads();
+    if (threadIdx.x < 4) {
+      const int r = threadIdx.x;
+      int k = want[r];
+      uint32_t b = 0;
+      for (; b < 256; ++b) {
+        const int c = (int)hist[r * 256 + b];
+        if (k < c) break;
+        k -= c;
+      }
+      want[r] = k;
+      prefix[r] |= (b & 255u) << shift;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    int32_t val[4];
+    for (int r = 0; r < 4; ++r) val[r] = (int32_t)(prefix[r] ^ 0x80000000u);
+    WinStat w;
+    w.n = n;
+    w.active = 1;
+    w.tpm = js_round_fixed((double)n / a.tpm_div, 2);
+    w.avg = js_round_fixed((double)sum / (double)n, 1);
+    w.p75 = js_round_fixed(ranks[0] == ranks[1] ? (double)val[0] : ((double)val[0] + (double)val[1]) / 2.0, 1);
+    w.p95 = js_round_fixed(ranks[2] == ranks[3] ? (double)val[2] : ((double)val[2] + (double)val[3]) / 2.0, 1);
+    a.out[s] = w;
+  }
+}
+
 // Large series: one 1024-thread block per deferred series, block-wide bitonic in LDS.
 __global__ __launch_bounds__(1024) void k_window_stats_big(WindowArgs a) {
   __shared__ int32_t t[BIG_TILE];
@@ -230,7 +305,16 @@ __global__ __launch_bounds__(1024) void k_window_stats_big(WindowArgs a) {
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sum;
     __syncthreads();
     const int n_all = wpos;
-    const int n = min(n_all, BIG_TILE);  // beyond the tile the percentile is clamped (counted)
+    if (n_all > BIG_TILE) {
+      // hotter than the LDS tile: the four order statistics the reference percentile formula
+      // reads are selected exactly by a 4-pass radix select over the window's samples
+      long long tot = 0;
+      for (int w = 0; w < 16; ++w) tot += red[w];
+      window_select(a, s, n_all, tot, t);
+      __syncthreads();
+      continue;
+    }
+    const int n = n_all;
     int np2 = 1;
     while (np2 < n) np2 <<= 1;
     for (int i = n + threadIdx.x; i < np2; i += blockDim.x) t[i] = 0x7fffffff;

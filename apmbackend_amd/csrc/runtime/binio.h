@@ -20,7 +20,7 @@
 
 namespace apm {
 
-constexpr uint32_t kCkptVersion = 2;
+constexpr uint32_t kCkptVersion = 3;  // 3: join section carries the join mode (host / GPU)
 
 class BinWriter {
  public:

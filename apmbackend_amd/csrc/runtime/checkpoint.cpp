@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cstring>
 
+#include "../kernels/devjoin_api.h"
 #include "binio.h"
 #include "engine.h"
 
@@ -225,7 +226,6 @@ void JoinShard::load(BinReader& rd) {
 
 uint64_t Engine::save_state(const std::string& path) {
   flush();
-  if (dev()) return save_state_dev(path);
   if (prefetched_) throw std::runtime_error("save_state: a prefetched batch is pending (process it first)");
   HIP_OK(hipStreamSynchronize(parse_stream_));
   HIP_OK(hipStreamSynchronize(stream_));
@@ -267,8 +267,14 @@ uint64_t Engine::save_state(const std::string& path) {
   w.end();
 
   w.begin(SEC_JOIN);
-  w.pod<uint64_t>(shards_.size());
-  for (auto& sh : shards_) sh->save(w);
+  w.pod<uint8_t>(dev() ? 1 : 0);
+  if (dev()) {
+    dj_->save(w);
+    w.vec(h_raw_series_);
+  } else {
+    w.pod<uint64_t>(shards_.size());
+    for (auto& sh : shards_) sh->save(w);
+  }
   w.end();
 
   w.begin(SEC_PARSE);
@@ -325,9 +331,26 @@ uint64_t Engine::save_state(const std::string& path) {
   d2h_vec(w, d_pool_end_[pool_cur_] + pool_off_, (size_t)pool_n_, stream_);
   d2h_vec(w, d_pool_gid_[pool_cur_] + pool_off_, (size_t)pool_n_, stream_);
   d2h_vec(w, d_tail_end_, (size_t)tail_n_, stream_);
-  d2h_vec(w, d_tail_gid_, (size_t)tail_n_, stream_);
-  w.pod<uint64_t>(line_blocks_.size());
-  for (auto& kv : line_blocks_) { w.pod(kv.first); w.pod(kv.second.live); w.str(kv.second.data); }
+  if (dev()) {
+    // pending lines live in the HBM text ring: saved as one blob (pool lines, then tail lines)
+    // with each gid rebased to its offset in the blob
+    std::vector<int64_t> gids((size_t)(pool_n_ + tail_n_));
+    if (pool_n_) HIP_OK(hipMemcpy(gids.data(), d_pool_gid_[pool_cur_] + pool_off_, (size_t)pool_n_ * 8, hipMemcpyDeviceToHost));
+    if (tail_n_) HIP_OK(hipMemcpy(gids.data() + pool_n_, d_tail_gid_, (size_t)tail_n_ * 8, hipMemcpyDeviceToHost));
+    std::string text = ring_text(d_pool_gid_[pool_cur_] + pool_off_, pool_n_) + ring_text(d_tail_gid_, tail_n_);
+    uint64_t off = 0;
+    for (auto& g : gids) {
+      const uint64_t len = (uint64_t)g & 0xfffffu;
+      g = (int64_t)((off << 20) | len);
+      off += len + 1;
+    }
+    w.vec(gids);
+    w.str(text);
+  } else {
+    d2h_vec(w, d_tail_gid_, (size_t)tail_n_, stream_);
+    w.pod<uint64_t>(line_blocks_.size());
+    for (auto& kv : line_blocks_) { w.pod(kv.first); w.pod(kv.second.live); w.str(kv.second.data); }
+  }
   w.end();
 
   w.begin(SEC_ALERTS);
@@ -353,7 +376,6 @@ uint64_t Engine::save_state(const std::string& path) {
 
 void Engine::load_state(const std::string& path) {
   flush();
-  if (dev()) { load_state_dev(path); return; }
   if (batch_no_ != 0 || n_series_ != 0 || !files_.empty())
     throw std::runtime_error("load_state needs a freshly constructed engine (no files, no batches)");
   const int32_t S = cfg_.max_series;
@@ -438,9 +460,28 @@ void Engine::load_state(const std::string& path) {
 
   rd.begin(SEC_JOIN);
   {
-    const uint64_t ns = rd.pod<uint64_t>();
-    if (ns != shards_.size()) throw std::runtime_error("checkpoint: shard count mismatch");
-    for (auto& sh : shards_) sh->load(rd);
+    const uint8_t mode = rd.pod<uint8_t>();
+    if (mode != (dev() ? 1 : 0))
+      throw std::runtime_error("checkpoint: written with a different gpu.joinOnDevice setting");
+    if (dev()) {
+      dj_->load(rd);
+      h_raw_series_ = rd.vec<int32_t>();
+      std::vector<int32_t> pairs;
+      for (size_t i = 0; i < h_raw_series_.size(); ++i)
+        if (h_raw_series_[i] >= 0) { pairs.push_back((int32_t)i); pairs.push_back(h_raw_series_[i]); }
+      if (!pairs.empty()) {
+        int32_t* d = nullptr;
+        HIP_OK(hipMalloc((void**)&d, pairs.size() * 4));
+        HIP_OK(hipMemcpy(d, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice));
+        apm_dj_scatter_i32(dj_->d_raw_series(), d, (uint32_t)(pairs.size() / 2), stream_);
+        HIP_OK(hipStreamSynchronize(stream_));
+        HIP_OK(hipFree(d));
+      }
+    } else {
+      const uint64_t ns = rd.pod<uint64_t>();
+      if (ns != shards_.size()) throw std::runtime_error("checkpoint: shard count mismatch");
+      for (auto& sh : shards_) sh->load(rd);
+    }
   }
 
   rd.begin(SEC_PARSE);
@@ -496,16 +537,30 @@ void Engine::load_state(const std::string& path) {
     pool_n_ = (int64_t)h2d_vec(rd, d_pool_end_[0], (size_t)cfg_.pool_cap, stream_);
     h2d_vec(rd, d_pool_gid_[0], (size_t)cfg_.pool_cap, stream_);
     tail_n_ = (int64_t)h2d_vec(rd, d_tail_end_, (size_t)cfg_.pool_cap, stream_);
-    h2d_vec(rd, d_tail_gid_, (size_t)cfg_.pool_cap, stream_);
-    if (pool_n_ != pn || tail_n_ != tn) throw std::runtime_error("checkpoint: pool size mismatch");
-    (void)off;
-    line_blocks_.clear();
-    for (uint64_t k = rd.pod<uint64_t>(); k; --k) {
-      const uint32_t id = rd.pod<uint32_t>();
-      LineBlock& b = line_blocks_[id];
-      rd.pod(b.live);
-      b.data = rd.str();
+    if (dev()) {
+      auto gids = rd.vec<int64_t>();
+      const std::string text = rd.str();
+      if ((int64_t)gids.size() != pool_n_ + tail_n_) throw std::runtime_error("checkpoint: pool size mismatch");
+      // the blob goes to the start of the (fresh) ring: blob offsets are ring positions
+      if (text.size() > dj_->ring_cap() / 2) throw std::runtime_error("checkpoint: pending tx text exceeds the ring");
+      if (!text.empty()) HIP_OK(hipMemcpy(dj_->ring(), text.data(), text.size(), hipMemcpyHostToDevice));
+      dj_->reset_ring(text.size());
+      if (pool_n_) HIP_OK(hipMemcpy(d_pool_gid_[0], gids.data(), (size_t)pool_n_ * 8, hipMemcpyHostToDevice));
+      if (tail_n_) HIP_OK(hipMemcpy(d_tail_gid_, gids.data() + pool_n_, (size_t)tail_n_ * 8, hipMemcpyHostToDevice));
+      *h_ring_min_ = ~0ULL;
+      ring_low_pending_ = UINT64_MAX;
+    } else {
+      h2d_vec(rd, d_tail_gid_, (size_t)cfg_.pool_cap, stream_);
+      if (pool_n_ != pn || tail_n_ != tn) throw std::runtime_error("checkpoint: pool size mismatch");
+      line_blocks_.clear();
+      for (uint64_t k = rd.pod<uint64_t>(); k; --k) {
+        const uint32_t id = rd.pod<uint32_t>();
+        LineBlock& b = line_blocks_[id];
+        rd.pod(b.live);
+        b.data = rd.str();
+      }
     }
+    (void)off;
   }
 
   rd.begin(SEC_ALERTS);
@@ -530,12 +585,24 @@ void Engine::load_state(const std::string& path) {
   HIP_OK(hipStreamSynchronize(stream_));
 }
 
-uint64_t Engine::save_state_dev(const std::string&) {
-  throw std::runtime_error("save_state: not yet supported with gpu.joinOnDevice (set it to false to checkpoint)");
-}
-
-void Engine::load_state_dev(const std::string&) {
-  throw std::runtime_error("load_state: not yet supported with gpu.joinOnDevice (set it to false to checkpoint)");
+// Text of `n` pending lines (gids into the HBM ring) in gid order, each with its '\n'.
+std::string Engine::ring_text(const int64_t* d_gid, int64_t n) {
+  if (n <= 0) return std::string();
+  if (apm_dj_gather_plan(d_gid, n, nullptr, d_rel_lens_, d_rel_offs_, d_release_tmp_, release_tmp_bytes_, stream_) != 0)
+    throw std::runtime_error("ring_text: scratch too small");
+  uint32_t total = 0;
+  HIP_OK(hipMemcpyAsync(&total, d_rel_offs_ + n, 4, hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+  std::string out(total, '\0');
+  if (total) {
+    char* d = nullptr;
+    HIP_OK(hipMalloc((void**)&d, total));
+    apm_dj_gather_copy(d_gid, n, dj_->ring(), dj_->ring_cap(), d_rel_offs_, d, stream_);
+    HIP_OK(hipMemcpyAsync(&out[0], d, total, hipMemcpyDeviceToHost, stream_));
+    HIP_OK(hipStreamSynchronize(stream_));
+    HIP_OK(hipFree(d));
+  }
+  return out;
 }
 
 }  // namespace apm

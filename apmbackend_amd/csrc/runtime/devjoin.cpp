@@ -4,11 +4,13 @@
 #include "devjoin.h"
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
 #include <cstring>
 #include <stdexcept>
 
 #include "../kernels/common.h"
+#include "binio.h"
 #include "../kernels/devjoin_dev.h"
 #include "join_util.h"
 #include "jsutil.h"
@@ -18,6 +20,10 @@ namespace apm {
 using namespace jstr;
 
 namespace {
+double clock_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 JOp blank_op(const Event& e, int32_t server) {
   JOp op;
   std::memset(&op, 0, sizeof(op));
@@ -221,29 +227,71 @@ void DeviceJoin::finish_select(int k, hipStream_t ps) {
 }
 
 // ---------------------------------------------------------------------------- host pre-pass
-uint32_t DeviceJoin::put_hbuf(std::string_view s) {
-  const uint32_t off = (uint32_t)hbuf_.size();
-  hbuf_.append(s.data(), s.size());
-  return off;
-}
-
-void DeviceJoin::host_prepass(int k, const uint8_t* hb, uint32_t n_host) {
+// One task per file with host events (audit state is per file, cache effects are ops resolved
+// on the GPU in line order), run on the engine's worker pool; the per-file op lists are then
+// merged by event index and their string buffers concatenated.
+void DeviceJoin::host_prepass(int k, const uint8_t* hb, uint32_t n_host, const ParallelFor& parallel) {
   Slot& s = sl_[k];
   hops_.clear();
   hbuf_.clear();
+  std::unordered_map<int32_t, int> task_of;
+  int nt = 0;
   for (uint32_t i = 0; i < n_host; ++i) {
-    const Event& e = s.h_host_ev[i];
-    const int32_t file = s.chunk_file[e.chunk];
-    if (e.mask & PM_HOST) ++host_pm_;
-    host_event(e, s.h_host_idx[i], hb, file);
+    const int32_t file = s.chunk_file[s.h_host_ev[i].chunk];
+    auto it = task_of.find(file);
+    int t;
+    if (it == task_of.end()) {
+      t = nt++;
+      task_of.emplace(file, t);
+      if ((int)tasks_.size() < nt) tasks_.emplace_back();
+      PrepassTask& T = tasks_[t];
+      T.file = file;
+      T.ctx = &audit_[file];  // created here, single-threaded
+      T.idx.clear(); T.hops.clear(); T.hbuf.clear();
+      T.audit_errors = T.invalid_acct = T.pm_host = 0;
+    } else {
+      t = it->second;
+    }
+    tasks_[t].idx.push_back(i);
+  }
+  auto work = [&](int t) {
+    PrepassTask& T = tasks_[t];
+    for (uint32_t i : T.idx) host_event(T, s.h_host_ev[i], s.h_host_idx[i], hb);
+  };
+  if (parallel && nt > 1) parallel(nt, work);
+  else for (int t = 0; t < nt; ++t) work(t);
+  // merge by event index (each task's list ascends); rebase the host-buffer offsets
+  size_t total = 0;
+  std::vector<uint32_t> base(nt);
+  for (int t = 0; t < nt; ++t) {
+    base[t] = (uint32_t)hbuf_.size();
+    hbuf_ += tasks_[t].hbuf;
+    total += tasks_[t].hops.size();
+    audit_errors_ += tasks_[t].audit_errors;
+    host_invalid_acct_ += tasks_[t].invalid_acct;
+    host_pm_ += tasks_[t].pm_host;
+  }
+  hops_.reserve(total);
+  std::vector<size_t> pos(nt, 0);
+  for (;;) {
+    int best = -1;
+    uint32_t bev = UINT32_MAX;
+    for (int t = 0; t < nt; ++t)
+      if (pos[t] < tasks_[t].hops.size() && tasks_[t].hops[pos[t]].ev < bev) { bev = tasks_[t].hops[pos[t]].ev; best = t; }
+    if (best < 0) break;
+    HostOp h = tasks_[best].hops[pos[best]++];
+    if (h.op.flags & JF_LID_HOST) h.op.lid += base[best];
+    if (h.op.flags & JF_SVC_HOST) h.op.svc_ref += base[best];
+    hops_.push_back(h);
   }
   host_events_ += n_host;
 }
 
-void DeviceJoin::host_event(const Event& e, uint32_t ev, const uint8_t* hb, int32_t file) {
-  const int32_t server = (*files_)[file].server;
+void DeviceJoin::host_event(PrepassTask& T, const Event& e, uint32_t ev, const uint8_t* hb) {
+  const int32_t server = (*files_)[T.file].server;
   const std::string_view line((const char*)hb + e.off, e.len);
-  if (e.kind == LK_APP) { on_app(e, ev, line, file, server); return; }
+  if (e.mask & PM_HOST) ++T.pm_host;
+  if (e.kind == LK_APP) { on_app(T, e, ev, line, server); return; }
   HostOp h;
   std::memset(&h, 0, sizeof(h));
   h.ev = ev;
@@ -277,7 +325,7 @@ void DeviceJoin::host_event(const Event& e, uint32_t ev, const uint8_t* hb, int3
     } else {
       return;
     }
-    hops_.push_back(h);
+    T.hops.push_back(h);
     return;
   }
   if (e.kind < LK_EJB_ENTRY || e.kind > LK_CT_EXIT) return;
@@ -307,12 +355,12 @@ void DeviceJoin::host_event(const Event& e, uint32_t ev, const uint8_t* hb, int3
   if (entry && lid.empty()) return;  // parseEntry returns before anything else
   op.svc = hash_bytes(name.data(), name.size(), ejb ? kHashSeedEjb : kHashSeed);
   op.flags = JF_HAS_SVC | JF_SVC_HOST | (ejb ? JF_EJB : 0);
-  op.svc_ref = put_hbuf(name);
+  op.svc_ref = T.put(name);
   op.svc_len = (uint16_t)name.size();
   op.ts = ts;
   if (ts_empty) op.flags |= JF_TS_EMPTY;
   if (!lid.empty()) {
-    op.lid = put_hbuf(lid);
+    op.lid = T.put(lid);
     op.lid_len = (uint16_t)std::min<size_t>(lid.size(), 0xffff);
     op.flags |= JF_LID_HOST;
     op.gkey = dj::gkey_of(hash_bytes(lid.data(), lid.size()), server);
@@ -344,11 +392,11 @@ void DeviceJoin::host_event(const Event& e, uint32_t ev, const uint8_t* hb, int3
     if (lid.empty()) op.gkey = 0;
   }
   h.kind = HOP_JOIN;
-  hops_.push_back(h);
+  T.hops.push_back(h);
 }
 
 // parseAppLine (:578-731): the per-file audit state machine; cache effects become ops.
-void DeviceJoin::on_app(const Event& e, uint32_t ev, std::string_view line, int32_t file, int32_t server) {
+void DeviceJoin::on_app(PrepassTask& T, const Event& e, uint32_t ev, std::string_view line, int32_t server) {
   const uint32_t m = e.mask;
   auto push = [&](const JOp& op) {
     HostOp h;
@@ -356,7 +404,7 @@ void DeviceJoin::on_app(const Event& e, uint32_t ev, std::string_view line, int3
     h.ev = ev;
     h.kind = HOP_JOIN;
     h.op = op;
-    hops_.push_back(h);
+    T.hops.push_back(h);
   };
   if (m & PM_AUTR_MAP) {
     auto toks = js::split_ws(line, 8);
@@ -371,7 +419,7 @@ void DeviceJoin::on_app(const Event& e, uint32_t ev, std::string_view line, int3
     } else {
       autr = "undefined";
     }
-    AuditCtx& ctx = audit_[file];
+    AuditCtx& ctx = *T.ctx;
     // attemptReadAccountNumberFromBAFInfo -> saveAcctNum(acct, 'bafmetainfo', logId)
     std::string alt;
     if ((e.mask & PM_HOST) ? baf_match(line) : (e.mask & PM_BAF) != 0) {
@@ -386,7 +434,7 @@ void DeviceJoin::on_app(const Event& e, uint32_t ev, std::string_view line, int3
       if (!alt.empty()) {
         const std::string_view t = js::trim(alt);
         if (!all_digits(t)) {
-          ++host_invalid_acct_;
+          ++T.invalid_acct;
         } else if (!log_id.empty()) {
           JOp op = blank_op(e, server);
           op.op = JOP_ACCT;
@@ -402,14 +450,12 @@ void DeviceJoin::on_app(const Event& e, uint32_t ev, std::string_view line, int3
     return;
   }
   if (m & PM_AUTR_HDR) {
-    auto cit = audit_.find(file);
-    if (cit == audit_.end()) { ++audit_errors_; return; }
-    AuditCtx& ctx = cit->second;
+    AuditCtx& ctx = *T.ctx;
     const size_t c1 = line.find(':');
     const size_t c2 = line.find(':', c1 + 1);
     const std::string autr(js::trim(line.substr(c1 + 1, c2 == std::string_view::npos ? std::string_view::npos : c2 - c1 - 1)));
     auto f = std::find_if(ctx.autr_map.begin(), ctx.autr_map.end(), [&](auto& q) { return q.first == autr; });
-    if (f == ctx.autr_map.end() || f->second.first.empty()) { ++audit_errors_; return; }
+    if (f == ctx.autr_map.end() || f->second.first.empty()) { ++T.audit_errors; return; }
     ctx.service_map.clear();
     ctx.active = true;
     ctx.active_log_id = f->second.first;
@@ -420,9 +466,8 @@ void DeviceJoin::on_app(const Event& e, uint32_t ev, std::string_view line, int3
     ctx.autr_map.erase(f);
     return;
   }
-  auto cit = audit_.find(file);
-  if (cit == audit_.end() || !cit->second.active) return;
-  AuditCtx& ctx = cit->second;
+  AuditCtx& ctx = *T.ctx;
+  if (!ctx.active) return;
   if (m & PM_EL_START) { ctx.elapsed_flag = true; return; }
   if (ctx.elapsed_flag) {
     if (m & PM_EL_END) { ctx.elapsed_flag = false; return; }
@@ -457,14 +502,14 @@ void DeviceJoin::on_app(const Event& e, uint32_t ev, std::string_view line, int3
   const std::string& svcname = ctx.active_service;
   auto f = std::find_if(ctx.service_map.begin(), ctx.service_map.end(), [&](auto& q) { return q.first == svcname; });
   if (m & PM_SW_STARTTS) {
-    if (f == ctx.service_map.end() || f->second.empty()) { ++audit_errors_; return; }
+    if (f == ctx.service_map.end() || f->second.empty()) { ++T.audit_errors; return; }
     f->second.front().has_start = true;
     f->second.front().start_ts = xml_inner(line);
     return;
   }
   if (m & PM_SW_STOPTS) {
     const std::string end_ts = xml_inner(line);
-    if (f == ctx.service_map.end() || f->second.empty()) { ++audit_errors_; return; }
+    if (f == ctx.service_map.end() || f->second.empty()) { ++T.audit_errors; return; }
     const AuditItem obj = f->second.front();
     f->second.pop_front();
     const std::string& log_id = ctx.active_log_id;
@@ -481,9 +526,9 @@ void DeviceJoin::on_app(const Event& e, uint32_t ev, std::string_view line, int3
     op.aux2 = ctx.active_alt.empty() ? js::nan() : js::parse_int(ctx.active_alt);
     op.flags = JF_HAS_SVC | JF_SVC_HOST | JF_LID_HOST | (s_empty ? JF_START_EMPTY : 0) | (e_empty ? JF_TS_EMPTY : 0) |
                (icontains(svcname, "Provider[") ? 0 : JF_TO_DB);
-    op.svc_ref = put_hbuf(svcname);
+    op.svc_ref = T.put(svcname);
     op.svc_len = (uint16_t)svcname.size();
-    op.lid = put_hbuf(log_id);
+    op.lid = T.put(log_id);
     op.lid_len = (uint16_t)std::min<size_t>(log_id.size(), 0xffff);
     push(op);
   }
@@ -514,7 +559,7 @@ void DeviceJoin::register_misses(const uint8_t* hb, uint32_t n_miss, hipStream_t
     const std::string norm = normalize_service(raw);
     if ((uint32_t)n >= cfg_.max_raw) throw std::runtime_error("device join: more raw services than gpu.maxRawServices");
     const int32_t nid = dict_->service_id(norm);
-    raw_info_.push_back(RawInfo{m.server, nid});
+    raw_info_.push_back(RawInfo{m.server, nid, m.svc});
     RawSvc& r = h_rawtab_[n];
     r.srv_off = intern_name((*servers_)[m.server]);
     r.srv_len = (int32_t)(*servers_)[m.server].size();
@@ -600,15 +645,16 @@ void DeviceJoin::maybe_rebuild(double now, hipStream_t s) {
 }
 
 void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64_t batch_no, bool want_tx,
-                     bool want_db, DevJoinBatch& out) {
+                     bool want_db, DevJoinBatch& out, const ParallelFor& parallel) {
   Slot& s = sl_[k];
   hipStream_t st = stream_;
   if (n_ev > cfg_.max_events) throw std::runtime_error("device join: more events than maxLinesPerBatch");
   if (s.used) HIP_OK(hipStreamWaitEvent(st, s.free_ev, 0));  // the stats thread is done with the slot
   events_ += n_ev;
+  phase_t[0] = clock_ms();
   // ---- host pre-pass (audit blocks, PM_HOST lines)
   const uint32_t n_host = *s.h_n_host;
-  host_prepass(k, hb, n_host);
+  host_prepass(k, hb, n_host, parallel);
   if (hops_.size() > h_hops_cap_) {
     if (h_hops_) HIP_OK(hipHostFree(h_hops_));
     h_hops_cap_ = hops_.size() * 2 + 1024;
@@ -689,9 +735,12 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64
   a.exp_idx_sorted = d_exp_idx_sorted_; a.exp_cnt = d_exp_cnt_; a.exp_pos = d_exp_pos_;
   a.out_cnt = d_out_cnt_; a.out_pos = d_out_pos_; a.stage = d_stage_; a.ovf = d_ovf_;
   a.out = d_out_; a.out_cap = out_cap_; a.counts = d_counts_;
+  phase_t[1] = clock_ms();
   if (apm_dj_join(&a, st) != 0) throw std::runtime_error("device join: scan scratch too small");
   HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost, st));
+  phase_t[2] = clock_ms();
   HIP_OK(hipStreamSynchronize(st));  // ---- sync A
+  phase_t[3] = clock_ms();
   const JoinCounts c = *h_counts_;
   if (c.n_out > out_cap_) throw std::runtime_error("device join: more tx in one batch than the output capacity");
   if (c.pad[0] > DJ_OVF_CAP) throw std::runtime_error("device join: output overflow list full");
@@ -702,6 +751,7 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64
   }
   keys_since_rebuild_ += c.n_keys_new;
   if (c.n_miss) register_misses(hb, c.n_miss, st);
+  phase_t[4] = clock_ms();
   // ---- resolve + plan
   DJFormatArgs& f = f_;
   f = DJFormatArgs{};
@@ -715,6 +765,7 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64
   if (apm_dj_plan(&f, st) != 0) throw std::runtime_error("device join: scan scratch too small");
   HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));  // ---- sync B
+  phase_t[5] = clock_ms();
   const JoinCounts c2 = *h_counts_;
   f.ring_base = ring_reserve(c2.text_bytes);
   const size_t txt = (size_t)(want_tx ? c2.tx_text_bytes : 0) + (want_db ? c2.db_text_bytes : 0);
@@ -749,6 +800,7 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64
                           hipMemcpyDeviceToHost, st));
   HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));  // ---- sync C
+  phase_t[6] = clock_ms();
   const JoinCounts c3 = *h_counts_;
   if (c3.n_cand > spec || c3.n_unresolved > spec) {
     HIP_OK(hipMemcpyAsync(h_cand_, d_cand_, (size_t)c3.n_cand * 4, hipMemcpyDeviceToHost, st));
@@ -782,6 +834,7 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64
   tx_ += c3.n_out;
   tx_db_ += c3.n_db;
   maybe_rebuild(now, st);
+  phase_t[7] = clock_ms();
 }
 
 JoinCounters DeviceJoin::counters() const {
@@ -797,6 +850,174 @@ JoinCounters DeviceJoin::counters() const {
   t.audit_errors = audit_errors_;
   t.host_fallback = host_pm_;  // lines the parser deferred (audit lines are host-resolved by design)
   return t;
+}
+
+// ---------------------------------------------------------------------------- checkpoint
+void DeviceJoin::save(BinWriter& w) {
+  hipStream_t st = stream_;
+  HIP_OK(hipStreamSynchronize(st));
+  HIP_OK(hipMemcpy(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost));
+  w.pod(*h_counts_);
+  for (uint64_t v : {events_, tx_, tx_db_, audit_errors_, host_pm_, host_invalid_acct_, host_events_}) w.pod(v);
+  // key table: live (non-empty) slots only
+  {
+    std::vector<KeyState> tab(table_cap_), live;
+    HIP_OK(hipMemcpy(tab.data(), d_table_, (size_t)table_cap_ * sizeof(KeyState), hipMemcpyDeviceToHost));
+    for (const KeyState& k : tab) if (k.key) live.push_back(k);
+    w.vec(live);
+  }
+  // needNumRecordCache regions + their arena entries
+  w.pod(arena_head_);
+  w.pod<uint64_t>(regions_.size());
+  for (const Region& r : regions_) { w.pod(r.lo); w.pod(r.hi); w.pod(r.exp); }
+  {
+    const uint64_t lo = regions_.empty() ? arena_head_ : regions_.front().lo;
+    std::vector<NeedEnt> ents((size_t)(arena_head_ - lo));
+    for (uint64_t v = lo; v < arena_head_; ++v)
+      HIP_OK(hipMemcpy(&ents[(size_t)(v - lo)], d_arena_ + (v & (cfg_.arena_cap - 1)), sizeof(NeedEnt), hipMemcpyDeviceToHost));
+    w.vec(ents);
+  }
+  // SOAP contexts of every file
+  {
+    std::vector<SoapState> ss(files_->size());
+    if (!ss.empty()) HIP_OK(hipMemcpy(ss.data(), d_soap_, ss.size() * sizeof(SoapState), hipMemcpyDeviceToHost));
+    w.vec(ss);
+  }
+  // raw service registry (names are re-derived from the dictionary on load)
+  {
+    const int32_t n = n_raw();
+    std::vector<RawInfo> ri(raw_info_.begin(), raw_info_.begin() + n);
+    w.vec(ri);
+    std::vector<int32_t> top(n);
+    for (int32_t i = 0; i < n; ++i) top[i] = h_rawtab_[i].toplevel;
+    w.vec(top);
+  }
+  // audit-trail contexts (per file)
+  w.pod<uint64_t>(audit_.size());
+  for (auto& kv : audit_) {
+    const AuditCtx& c = kv.second;
+    w.pod(kv.first);
+    w.pod<uint64_t>(c.autr_map.size());
+    for (auto& a : c.autr_map) { w.str(a.first); w.str(a.second.first); w.str(a.second.second); }
+    w.pod(c.active); w.str(c.active_log_id); w.str(c.active_alt); w.str(c.active_service);
+    w.pod(c.has_active_service); w.pod(c.elapsed_flag); w.pod(c.sw_flag);
+    w.pod<uint64_t>(c.service_map.size());
+    for (auto& sm : c.service_map) {
+      w.str(sm.first);
+      w.pod<uint64_t>(sm.second.size());
+      for (auto& it : sm.second) { w.str(it.elapsed); w.pod(it.has_start); w.str(it.start_ts); }
+    }
+  }
+}
+
+void DeviceJoin::load(BinReader& rd) {
+  hipStream_t st = stream_;
+  JoinCounts c;
+  rd.pod(c);
+  HIP_OK(hipMemcpy(d_counts_, &c, sizeof(JoinCounts), hipMemcpyHostToDevice));
+  *h_counts_ = c;
+  for (uint64_t* v : {&events_, &tx_, &tx_db_, &audit_errors_, &host_pm_, &host_invalid_acct_, &host_events_}) rd.pod(*v);
+  {
+    auto live = rd.vec<KeyState>();
+    if (live.size() * 2 > table_cap_) throw std::runtime_error("checkpoint: join keys exceed gpu.joinTableSlots");
+    if (!live.empty()) {
+      KeyState* tmp = nullptr;
+      HIP_OK(hipMalloc((void**)&tmp, live.size() * sizeof(KeyState)));
+      HIP_OK(hipMemcpy(tmp, live.data(), live.size() * sizeof(KeyState), hipMemcpyHostToDevice));
+      HIP_OK(hipMemsetAsync(d_live_, 0, 8, st));
+      // every saved slot is reinserted (now = -inf keeps them all)
+      apm_dj_rebuild(tmp, (uint32_t)live.size(), d_table_, table_cap_ - 1, d_arena_, cfg_.arena_cap, -__builtin_inf(),
+                     d_counts_, d_live_, st);
+      HIP_OK(hipStreamSynchronize(st));
+      HIP_OK(hipFree(tmp));
+    }
+    keys_live_ = live.size();
+    keys_since_rebuild_ = 0;
+  }
+  rd.pod(arena_head_);
+  regions_.clear();
+  for (uint64_t n = rd.pod<uint64_t>(); n; --n) {
+    Region r;
+    rd.pod(r.lo); rd.pod(r.hi); rd.pod(r.exp);
+    regions_.push_back(r);
+  }
+  {
+    auto ents = rd.vec<NeedEnt>();
+    const uint64_t lo = regions_.empty() ? arena_head_ : regions_.front().lo;
+    if (ents.size() != arena_head_ - lo) throw std::runtime_error("checkpoint: need arena size mismatch");
+    for (uint64_t v = lo; v < arena_head_; ++v)
+      HIP_OK(hipMemcpy(d_arena_ + (v & (cfg_.arena_cap - 1)), &ents[(size_t)(v - lo)], sizeof(NeedEnt), hipMemcpyHostToDevice));
+  }
+  {
+    auto ss = rd.vec<SoapState>();
+    if (ss.size() > soap_cap_) throw std::runtime_error("checkpoint: too many files");
+    if (!ss.empty()) HIP_OK(hipMemcpy(d_soap_, ss.data(), ss.size() * sizeof(SoapState), hipMemcpyHostToDevice));
+  }
+  {
+    auto ri = rd.vec<RawInfo>();
+    auto top = rd.vec<int32_t>();
+    if (ri.size() > cfg_.max_raw) throw std::runtime_error("checkpoint: more raw services than gpu.maxRawServices");
+    const uint32_t rmask = (1u << cfg_.reg_bits) - 1;
+    std::vector<RegSlot> reg((size_t)rmask + 1);
+    for (auto& r : reg) { r.key = 0; r.raw = RAW_EMPTY; r.pad = 0; }
+    raw_info_.clear();
+    for (size_t i = 0; i < ri.size(); ++i) {
+      raw_info_.push_back(ri[i]);
+      RawSvc& r = h_rawtab_[i];
+      const std::string& srv = (*servers_)[ri[i].server];
+      const std::string norm = dict_->service_name(ri[i].norm_id);
+      r.srv_off = intern_name(srv);
+      r.srv_len = (int32_t)srv.size();
+      r.norm_off = intern_name(norm);
+      r.norm_len = (int32_t)norm.size();
+      r.toplevel = top[i];
+      r.pad = 0;
+      const uint64_t k = dj::regkey_of(ri[i].svc, ri[i].server);
+      for (uint32_t h = dj::home_of(k, rmask);; h = (h + 1) & rmask)
+        if (!reg[h].key) { reg[h].key = k; reg[h].raw = (int32_t)i; break; }
+    }
+    HIP_OK(hipMemcpy(d_reg_, reg.data(), reg.size() * sizeof(RegSlot), hipMemcpyHostToDevice));
+    if (!ri.empty()) HIP_OK(hipMemcpy(d_rawtab_, h_rawtab_, ri.size() * sizeof(RawSvc), hipMemcpyHostToDevice));
+    if (names_.size() > names_cap_) {
+      names_cap_ = std::max<size_t>(names_.size() * 2, 1 << 20);
+      HIP_OK(hipMalloc((void**)&d_names_, names_cap_));
+      device_bytes_ += names_cap_;
+    }
+    if (!names_.empty()) HIP_OK(hipMemcpy(d_names_, names_.data(), names_.size(), hipMemcpyHostToDevice));
+    names_uploaded_ = names_.size();
+    n_raw_.store((int32_t)ri.size(), std::memory_order_release);
+  }
+  audit_.clear();
+  for (uint64_t n = rd.pod<uint64_t>(); n; --n) {
+    const int32_t f = rd.pod<int32_t>();
+    AuditCtx& c = audit_[f];
+    for (uint64_t k = rd.pod<uint64_t>(); k; --k) {
+      std::string a = rd.str(), b = rd.str(), d = rd.str();
+      c.autr_map.push_back({a, {b, d}});
+    }
+    rd.pod(c.active); c.active_log_id = rd.str(); c.active_alt = rd.str(); c.active_service = rd.str();
+    rd.pod(c.has_active_service); rd.pod(c.elapsed_flag); rd.pod(c.sw_flag);
+    for (uint64_t k = rd.pod<uint64_t>(); k; --k) {
+      std::string name = rd.str();
+      std::deque<AuditItem> q;
+      for (uint64_t j = rd.pod<uint64_t>(); j; --j) {
+        AuditItem it;
+        it.elapsed = rd.str();
+        rd.pod(it.has_start);
+        it.start_ts = rd.str();
+        q.push_back(it);
+      }
+      c.service_map.push_back({name, q});
+    }
+  }
+  files_uploaded_ = 0;
+  HIP_OK(hipStreamSynchronize(st));
+}
+
+void DeviceJoin::reset_ring(uint64_t head) {
+  std::lock_guard<std::mutex> g(ring_mu_);
+  ring_head_.store(head, std::memory_order_release);
+  ring_low_.store(0, std::memory_order_release);
 }
 
 }  // namespace apm

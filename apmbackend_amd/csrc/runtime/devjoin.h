@@ -17,6 +17,7 @@
 #include <atomic>
 #include <cstdint>
 #include <deque>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -73,8 +74,10 @@ class DeviceJoin {
   // after the parse stream synced: finish the host-event copy (n_ev known)
   void finish_select(int k, hipStream_t ps);
   // the batch join; host_bytes = the host copy of the batch (same layout as d_bytes(k))
+  // `parallel(n, fn)` runs fn(0..n-1) on the engine's worker pool (host pre-pass per file)
+  using ParallelFor = std::function<void(int, const std::function<void(int)>&)>;
   void run(int k, const uint8_t* host_bytes, uint32_t n_ev, double now, uint64_t batch_no, bool want_tx, bool want_db,
-           DevJoinBatch& out);
+           DevJoinBatch& out, const ParallelFor& parallel = nullptr);
   // the stats thread finished with slot k's arrays (event recorded on its stream)
   void release_slot(int k, hipStream_t stats_stream);
 
@@ -92,8 +95,18 @@ class DeviceJoin {
   uint64_t ring_head() const { return ring_head_.load(std::memory_order_acquire); }
   // reserve `bytes` at the ring head (thread-safe; relocation by the stats thread also uses it)
   uint64_t ring_reserve(uint64_t bytes);
+  void reset_ring(uint64_t head);  // checkpoint load: pending lines were placed at [0, head)
 
   JoinCounters counters() const;
+
+  // checkpoint of the GPU join state (checkpoint.cpp): key table (live entries), need arena
+  // (live regions), SOAP contexts, service registry, audit contexts, counters
+  void save(class BinWriter& w);
+  void load(class BinReader& r);
+  // phase boundaries of the last run() (steady-clock ms): prepass, join launched, sync A,
+  // registered, sync B, sync C, end -- for the engine's stage trace
+  static constexpr int kPhases = 7;
+  double phase_t[kPhases + 1] = {0};
   const JoinCounts& last_counts() const { return *h_counts_; }
   size_t device_bytes() const { return device_bytes_; }
 
@@ -134,13 +147,22 @@ class DeviceJoin {
     bool has_active_service = false, elapsed_flag = false, sw_flag = false;
     std::vector<std::pair<std::string, std::deque<AuditItem>>> service_map;
   };
-  struct RawInfo { int32_t server; int32_t norm_id; };
+  struct RawInfo { int32_t server; int32_t norm_id; uint64_t svc; };
 
   void* dmalloc(size_t bytes);
-  void host_prepass(int k, const uint8_t* host_bytes, uint32_t n_host);
-  void host_event(const Event& e, uint32_t ev, const uint8_t* host_bytes, int32_t file);
-  void on_app(const Event& e, uint32_t ev, std::string_view line, int32_t file, int32_t server);
-  uint32_t put_hbuf(std::string_view s);
+  // One file's share of the host pre-pass (files are independent: the audit context is per file)
+  struct PrepassTask {
+    int32_t file = -1;
+    AuditCtx* ctx = nullptr;
+    std::vector<uint32_t> idx;   // host-event indices (ascending)
+    std::vector<HostOp> hops;
+    std::string hbuf;
+    uint64_t audit_errors = 0, invalid_acct = 0, pm_host = 0;
+    uint32_t put(std::string_view s) { const uint32_t o = (uint32_t)hbuf.size(); hbuf.append(s.data(), s.size()); return o; }
+  };
+  void host_prepass(int k, const uint8_t* host_bytes, uint32_t n_host, const ParallelFor& parallel);
+  void host_event(PrepassTask& t, const Event& e, uint32_t ev, const uint8_t* host_bytes);
+  void on_app(PrepassTask& t, const Event& e, uint32_t ev, std::string_view line, int32_t server);
   int32_t intern_name(const std::string& s);
   void register_misses(const uint8_t* host_bytes, uint32_t n_miss, hipStream_t s);
   void maybe_rebuild(double now, hipStream_t s);
@@ -163,6 +185,7 @@ class DeviceJoin {
   uint8_t* d_hbuf_ = nullptr;
   size_t d_hops_cap_ = 0, d_hbuf_cap_ = 0;
   std::unordered_map<int32_t, AuditCtx> audit_;
+  std::vector<PrepassTask> tasks_;
   uint32_t last_host_ = 0;
   void* d_sel_tmp_ = nullptr;  // rocprim scratch of the host-event selection (parse stream)
   size_t sel_tmp_bytes_ = 0;

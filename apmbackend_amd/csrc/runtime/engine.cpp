@@ -291,6 +291,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   d_spill_n_ = (int32_t*)dmalloc(NSLOT * 4);
   d_spill_series_ = (int32_t*)dmalloc((size_t)NSLOT * cfg_.spill_cap * 4);
   d_spill_val_ = (int32_t*)dmalloc((size_t)NSLOT * cfg_.spill_cap * 4);
+  d_spill_drop_ = (unsigned long long*)dmalloc(64);
   d_active_ = (uint8_t*)dmalloc(S);
   d_win_ = (WinStat*)dmalloc((size_t)S * sizeof(WinStat));
   d_big_list_ = (int32_t*)dmalloc((size_t)S * 4);
@@ -441,7 +442,10 @@ Engine::~Engine() {
     hipStreamSynchronize(out_stream_);
     hipHostFree(h_ring_min_); hipHostFree(h_rel_n_); hipHostFree(h_rel_total_); hipHostFree(h_unseen_flag_);
     for (int k = 0; k < 2; ++k) if (h_rel_text_[k]) hipHostFree(h_rel_text_[k]);
-    if (h_pairs_) hipHostFree(h_pairs_);
+    for (int k = 0; k < 2; ++k) {
+      if (h_pairs_k_[k]) hipHostFree(h_pairs_k_[k]);
+      if (pairs_ev_[k]) hipEventDestroy(pairs_ev_[k]);
+    }
     dj_.reset();
     hipStreamDestroy(out_stream_);
   }
@@ -937,7 +941,8 @@ void Engine::process_batch_dev_tail(ParseSlot& ps, double t0, double now_overrid
   trace_event("parse", t0, t1, 0);
   const double clock = now_override >= 0 ? now_override : watermark_;
   DevJoinBatch b;
-  dj_->run(k, ps.hb, ps.n_events, clock, batch_no_, want(OUT_TRANSACTIONS), want(OUT_AUDIT_DB), b);
+  const DeviceJoin::ParallelFor par = [this](int n, const std::function<void(int)>& fn) { pool_->run(n, fn); };
+  dj_->run(k, ps.hb, ps.n_events, clock, batch_no_, want(OUT_TRANSACTIONS), want(OUT_AUDIT_DB), b, par);
   const double t2 = now_ms();
   metrics_.t_join_ms += t2 - t1;
   metrics_.t_join_shards_ms += t2 - t1;
@@ -945,6 +950,11 @@ void Engine::process_batch_dev_tail(ParseSlot& ps, double t0, double now_overrid
   metrics_.t_shard_busy_ms += t2 - t1;
   roctxRangePop();
   trace_event("join (GPU)", t1, t2, 0);
+  if (trace_on_) {
+    static const char* names[DeviceJoin::kPhases] = {"dj.prepass", "dj.launch", "dj.syncA", "dj.register",
+                                                     "dj.plan+syncB", "dj.write+syncC", "dj.tail"};
+    for (int i = 0; i < DeviceJoin::kPhases; ++i) trace_event(names[i], dj_->phase_t[i], dj_->phase_t[i + 1], 2);
+  }
   const unsigned long long wm = *ps.h_watermark;
   if (wm) {
     const double w = (double)((long long)wm - (1LL << 62));
@@ -1103,11 +1113,13 @@ void Engine::flush() {
     if (!out_error_.empty()) { std::string e = out_error_; out_error_.clear(); throw std::runtime_error(e); }
   }
   if (!st_error_.empty()) { std::string e = st_error_; st_error_.clear(); throw std::runtime_error(e); }
-  if (dev()) {
-    unsigned long long u = 0;
-    HIP_OK(hipMemcpyAsync(&u, d_unmapped_, 8, hipMemcpyDeviceToHost, stream_));
+  {
+    unsigned long long u[2] = {0, 0};
+    if (dev()) HIP_OK(hipMemcpyAsync(&u[0], d_unmapped_, 8, hipMemcpyDeviceToHost, stream_));
+    HIP_OK(hipMemcpyAsync(&u[1], d_spill_drop_, 8, hipMemcpyDeviceToHost, stream_));
     HIP_OK(hipStreamSynchronize(stream_));
-    metrics_.series_overflow_tx = u;
+    metrics_.series_overflow_tx = u[0];
+    metrics_.spill_dropped = u[1];
   }
 }
 
@@ -1221,7 +1233,7 @@ void Engine::ensure_bucket_slot(int64_t b) {
   if (slot_bucket_[slot] == b) return;
   if (slot_bucket_[slot] != NO_BUCKET) {
     StatsState st{d_counts_cells_, d_cells_, d_spill_n_, d_spill_series_, d_spill_val_, d_active_,
-                  cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series};
+                  cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series, d_spill_drop_};
     apm_stats_clear_slot(&st, slot, stream_);
   }
   slot_bucket_[slot] = b;
@@ -1310,7 +1322,7 @@ void Engine::stats_for_batch(std::vector<TxOut>& txs, double batch_t0) {
   HIP_OK(hipMemcpyAsync(d_tx_, h_tx_, (size_t)n * sizeof(TxRec), hipMemcpyHostToDevice, stream_));
   HIP_OK(hipMemcpyAsync(d_gid_, h_gid_, (size_t)n * 8, hipMemcpyHostToDevice, stream_));
   StatsState st{d_counts_cells_, d_cells_, d_spill_n_, d_spill_series_, d_spill_val_, d_active_,
-                cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series};
+                cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series, d_spill_drop_};
   const int64_t keep_iv = cfg_.window + cfg_.buffer;
   auto append = [&](uint32_t lo, uint32_t hi, int64_t lat) {
     if (hi <= lo) return;
@@ -1365,15 +1377,10 @@ void Engine::stats_for_batch_dev(DevJoinBatch& b, double batch_t0) {
       if (sr >= 0) { h_raw_series_[raw] = sr; upd.push_back({raw, sr}); }
     }
     if (!upd.empty()) {
-      if (upd.size() > pairs_cap_) {
-        if (h_pairs_) HIP_OK(hipHostFree(h_pairs_));
-        pairs_cap_ = upd.size() * 2 + 4096;
-        HIP_OK(hipHostMalloc((void**)&h_pairs_, pairs_cap_ * 8, hipHostMallocDefault));
-        d_pairs_ = (int32_t*)regrow(d_pairs_, pairs_bytes_, pairs_cap_ * 8);
-      }
-      HIP_OK(hipStreamSynchronize(stream_));  // the previous scatter's pinned pairs were consumed
-      for (size_t i = 0; i < upd.size(); ++i) { h_pairs_[2 * i] = upd[i].first; h_pairs_[2 * i + 1] = upd[i].second; }
-      HIP_OK(hipMemcpyAsync(d_pairs_, h_pairs_, upd.size() * 8, hipMemcpyHostToDevice, stream_));
+      int32_t* hp = pinned_pairs(upd.size() * 2);
+      for (size_t i = 0; i < upd.size(); ++i) { hp[2 * i] = upd[i].first; hp[2 * i + 1] = upd[i].second; }
+      HIP_OK(hipMemcpyAsync(d_pairs_, hp, upd.size() * 8, hipMemcpyHostToDevice, stream_));
+      pinned_pairs_done();
       apm_dj_scatter_i32(dj_->d_raw_series(), d_pairs_, (uint32_t)upd.size(), stream_);
     }
     apm_dj_fill_series(b.d_tx, b.d_raw, b.n_stats, dj_->d_raw_series(), d_unmapped_, stream_);
@@ -1385,7 +1392,7 @@ void Engine::stats_for_batch_dev(DevJoinBatch& b, double batch_t0) {
   metrics_.t_stats_tx_ms += now_ms() - ts0;
   trace_event("tx loop", ts0, now_ms(), 1);
   StatsState st{d_counts_cells_, d_cells_, d_spill_n_, d_spill_series_, d_spill_val_, d_active_,
-                cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series};
+                cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series, d_spill_drop_};
   const int64_t keep_iv = cfg_.window + cfg_.buffer;
   auto append = [&](uint32_t lo, uint32_t hi, int64_t lat) {
     if (hi <= lo) return;
@@ -1411,21 +1418,37 @@ void Engine::stats_for_batch_dev(DevJoinBatch& b, double batch_t0) {
   cur_dj_ = nullptr;
 }
 
+// Pinned staging for the stats thread's small H2D uploads (raw -> series pairs, unseen series
+// ids): two buffers used alternately, each reused only after its previous copy completed, so
+// the upload never waits for the whole stats stream.
+int32_t* Engine::pinned_pairs(size_t n_ints) {
+  const int k = pairs_k_;
+  if (pairs_ev_[k]) HIP_OK(hipEventSynchronize(pairs_ev_[k]));
+  else HIP_OK(hipEventCreateWithFlags(&pairs_ev_[k], hipEventDisableTiming));
+  if (n_ints > h_pairs_cap_[k]) {
+    if (h_pairs_k_[k]) HIP_OK(hipHostFree(h_pairs_k_[k]));
+    h_pairs_cap_[k] = n_ints * 2 + 8192;
+    HIP_OK(hipHostMalloc((void**)&h_pairs_k_[k], h_pairs_cap_[k] * 4, hipHostMallocDefault));
+  }
+  if (n_ints * 4 > pairs_bytes_) d_pairs_ = (int32_t*)regrow(d_pairs_, pairs_bytes_, n_ints * 8 + 65536);
+  return h_pairs_k_[k];
+}
+
+void Engine::pinned_pairs_done() {
+  HIP_OK(hipEventRecord(pairs_ev_[pairs_k_], stream_));
+  pairs_k_ ^= 1;
+}
+
 // K8 needs the z-score settings of series that became visible before this rollover: with the
 // device join the host never sees individual tx, so the `active` flags of the still-unseen series
 // are read back (only while the series set grows).
 void Engine::refresh_unseen_active() {
   if (unseen_.empty()) return;
   const uint32_t n = (uint32_t)unseen_.size();
-  if ((size_t)n * 8 > pairs_cap_ * 8) {
-    if (h_pairs_) HIP_OK(hipHostFree(h_pairs_));
-    pairs_cap_ = (size_t)n * 2 + 4096;
-    HIP_OK(hipHostMalloc((void**)&h_pairs_, pairs_cap_ * 8, hipHostMallocDefault));
-    d_pairs_ = (int32_t*)regrow(d_pairs_, pairs_bytes_, pairs_cap_ * 8);
-  }
-  HIP_OK(hipStreamSynchronize(stream_));
-  std::memcpy(h_pairs_, unseen_.data(), (size_t)n * 4);
-  HIP_OK(hipMemcpyAsync(d_unseen_idx_, h_pairs_, (size_t)n * 4, hipMemcpyHostToDevice, stream_));
+  int32_t* hp = pinned_pairs(n);
+  std::memcpy(hp, unseen_.data(), (size_t)n * 4);
+  HIP_OK(hipMemcpyAsync(d_unseen_idx_, hp, (size_t)n * 4, hipMemcpyHostToDevice, stream_));
+  pinned_pairs_done();
   apm_dj_gather_u8(d_active_, d_unseen_idx_, n, d_unseen_flag_, stream_);
   HIP_OK(hipMemcpyAsync(h_unseen_flag_, d_unseen_flag_, n, hipMemcpyDeviceToHost, stream_));
   HIP_OK(hipStreamSynchronize(stream_));
@@ -1440,7 +1463,7 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   for (int i = 0; i < NSLOT; ++i) {
     if (slot_bucket_[i] != NO_BUCKET && slot_bucket_[i] < L - keep_iv) {
       StatsState st{d_counts_cells_, d_cells_, d_spill_n_, d_spill_series_, d_spill_val_, d_active_,
-                    cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series};
+                    cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series, d_spill_drop_};
       apm_stats_clear_slot(&st, i, stream_);
       slot_bucket_[i] = NO_BUCKET;
     }
@@ -1519,7 +1542,7 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   // ---- K8 window statistics over buckets [L-36, L-6]
   WindowArgs wa;
   wa.st = StatsState{d_counts_cells_, d_cells_, d_spill_n_, d_spill_series_, d_spill_val_, d_active_,
-                     cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series};
+                     cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series, d_spill_drop_};
   wa.n_win = (int32_t)(keep_iv - cfg_.buffer + 1);
   for (int r = 0; r < 32; ++r) wa.win_slots[r] = -1;
   for (int r = 0; r < wa.n_win && r < 32; ++r) {

@@ -138,6 +138,7 @@ struct EngineMetrics {
   uint64_t rollovers = 0, alerts = 0, alert_candidates = 0, series = 0, released = 0;
   uint64_t formatted_bytes = 0, format_fallbacks = 0, lockstep_rollovers = 0;
   uint64_t series_overflow_tx = 0;  // tx whose series could not be created (gpu.maxSeries full)
+  uint64_t spill_dropped = 0;       // samples lost to a full bucket spill list (gpu.bucketOverflowCapacity)
   double t_parse_ms = 0, t_join_ms = 0, t_stats_ms = 0, t_total_ms = 0;
   double t_join_shards_ms = 0, t_merge_ms = 0;                 // split of t_join_ms
   double t_shard_busy_ms = 0, t_shard_max_ms = 0;              // per batch: mean / max of one shard's join
@@ -287,8 +288,7 @@ class Engine {
   void release_device(int64_t edge_ts);   // K9 with the device join: count + gather on the GPU
   void release_device_finish();
   void refresh_unseen_active();
-  uint64_t save_state_dev(const std::string& path);
-  void load_state_dev(const std::string& path);
+  std::string ring_text(const int64_t* d_gid, int64_t n);  // pending lines out of the HBM ring
   void ensure_bucket_slot(int64_t b);
   void do_rollover(int64_t L, double batch_t0);
   void flush_alerts(int64_t edge_ts);
@@ -432,9 +432,14 @@ class Engine {
   size_t h_rel_text_cap_[2] = {0, 0};
   hipStream_t out_stream_ = nullptr;
   std::vector<int32_t> h_raw_series_;          // stats thread mirror of the raw -> series table
-  int32_t* h_pairs_ = nullptr;                 // pinned (index, value) pairs for small scatters
+  int32_t* h_pairs_k_[2] = {nullptr, nullptr};  // pinned staging of small uploads (alternating)
+  size_t h_pairs_cap_[2] = {0, 0};
+  hipEvent_t pairs_ev_[2] = {nullptr, nullptr};
+  int pairs_k_ = 0;
   int32_t* d_pairs_ = nullptr;
-  size_t pairs_cap_ = 0, pairs_bytes_ = 0;
+  size_t pairs_bytes_ = 0;
+  int32_t* pinned_pairs(size_t n_ints);
+  void pinned_pairs_done();
   int32_t* d_unseen_idx_ = nullptr;
   uint8_t* d_unseen_flag_ = nullptr;
   uint8_t* h_unseen_flag_ = nullptr;
@@ -485,6 +490,7 @@ class Engine {
   int32_t* d_spill_n_ = nullptr;
   int32_t* d_spill_series_ = nullptr;
   int32_t* d_spill_val_ = nullptr;
+  unsigned long long* d_spill_drop_ = nullptr;  // K7 samples lost to a full spill list
   uint8_t* d_active_ = nullptr;
   int64_t slot_bucket_[NSLOT];
   int64_t latest_ = 0;

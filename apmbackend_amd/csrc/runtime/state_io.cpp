@@ -291,6 +291,17 @@ std::vector<std::pair<int64_t, std::string>> Engine::export_pending() {
     HIP_OK(hipMemcpy(gids.data() + pool_n_, d_tail_gid_, (size_t)tail_n_ * 8, hipMemcpyDeviceToHost));
   }
   std::vector<std::pair<int64_t, std::string>> r;
+  if (dev()) {  // lines in the HBM text ring (gather order = pool, then tail)
+    const std::string text = ring_text(d_pool_gid_[pool_cur_] + pool_off_, pool_n_) + ring_text(d_tail_gid_, tail_n_);
+    size_t p = 0;
+    for (size_t i = 0; i < ends.size(); ++i) {
+      const size_t len = (size_t)((uint64_t)gids[i] & 0xfffffu);
+      r.emplace_back(ends[i], text.substr(p, len));
+      p += len + 1;
+    }
+    std::stable_sort(r.begin(), r.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+    return r;
+  }
   for (size_t i = 0; i < ends.size(); ++i) {
     const uint64_t g = (uint64_t)gids[i];
     auto it = line_blocks_.find((uint32_t)(g >> 44));
@@ -313,6 +324,22 @@ void Engine::import_pending(const std::vector<int64_t>& ends, const std::vector<
   if (ends.size() != lines.size()) throw std::runtime_error("import_pending: sizes differ");
   if (ends.empty()) return;
   if (pool_n_ + tail_n_ + (int64_t)ends.size() > cfg_.pool_cap) throw std::runtime_error("import_pending: pool full");
+  if (dev()) {  // into the HBM text ring
+    std::string text;
+    std::vector<int64_t> gid(ends.size());
+    for (size_t i = 0; i < ends.size(); ++i) {
+      gid[i] = (int64_t)(((uint64_t)text.size() << 20) | (uint64_t)std::min<size_t>(lines[i].size(), 0xfffff));
+      text += lines[i];
+      text += '\n';
+    }
+    const uint64_t base = dj_->ring_reserve(text.size());
+    for (auto& g : gid) g = (int64_t)(((((uint64_t)g >> 20) + base) << 20) | ((uint64_t)g & 0xfffffu));
+    HIP_OK(hipMemcpy(dj_->ring() + (base & (dj_->ring_cap() - 1)), text.data(), text.size(), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_tail_end_ + tail_n_, ends.data(), ends.size() * 8, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_tail_gid_ + tail_n_, gid.data(), ends.size() * 8, hipMemcpyHostToDevice));
+    tail_n_ += (int64_t)ends.size();
+    return;
+  }
   const uint32_t id = (line_block_seq_++) & 0xFFFFFu;
   LineBlock& blk = line_blocks_[id];
   std::vector<int64_t> gid(ends.size());
