@@ -9,10 +9,11 @@
 //   pass 2  same lane re-formats straight into the output at its offset
 // Number printing reproduces Number.prototype.toFixed exactly: the rounding decision uses the
 // error-free product x*10^f = p + e (fma), ties to the larger n (ECMA-262 21.1.3.3), then the
-// integer n is printed with the decimal point inserted f digits from the right.  Magnitudes
-// >= 1e13 (where the exact-decision argument needs more care, and JS switches to exponent
-// notation at 1e21) set a fallback flag and the host formats that rollover instead.
+// integer n is printed with the decimal point inserted f digits from the right.  From 2^52 the
+// scaled product is an integer and the error term alone decides; from 2^53 the value itself is
+// an integer; from 1e21 JS prints String(x).  Only |x| >= 2^127 is not exact (flagged, counted).
 #include "kernel_api.h"  // (common.h pulls <cstring> in before rocprim)
+#include "devjoin_dev.h"
 
 #include <rocprim/rocprim.hpp>
 
@@ -48,14 +49,22 @@ struct Out {
     if (x != x) { s("undefined", 9); return; }
     const bool neg = x < 0;
     const double ax = neg ? -x : x;
-    if (!(ax < 1e13)) { fallback = true; return; }
+    if (!(ax < 9007199254740992.0)) {  // >= 2^53: integral values (rare)
+      big(neg, ax, f, fallback);
+      return;
+    }
     const double scale = f == 1 ? 10.0 : 100.0;
     const double pr = ax * scale;
-    const double e = fma(ax, scale, -pr);
-    const double q = floor(pr);
-    const double d = (pr - q) - 0.5;
-    uint64_t nn = (uint64_t)q;
-    if (d > 0 || (d == 0 && e >= 0)) ++nn;
+    const double e = fma(ax, scale, -pr);  // exact: x * 10^f = pr + e
+    uint64_t nn;
+    if (pr >= 4503599627370496.0) {  // pr >= 2^52 is an integer: n = nearest integer to pr + e
+      nn = (uint64_t)pr + (uint64_t)(int64_t)floor(e + 0.5);
+    } else {
+      const double q = floor(pr);
+      const double d = (pr - q) - 0.5;
+      nn = (uint64_t)q;
+      if (d > 0 || (d == 0 && e >= 0)) ++nn;
+    }
     if (neg) c('-');
     const uint64_t sc = f == 1 ? 10 : 100;
     u(nn / sc);
@@ -63,6 +72,24 @@ struct Out {
     const uint64_t fr = nn % sc;
     if (f == 2) { c((char)('0' + fr / 10)); c((char)('0' + fr % 10)); }
     else c((char)('0' + fr));
+  }
+  // |x| >= 2^53: x is an integer, so toFixed prints its digits and f zeros below 1e21 and
+  // String(x) (exponent form) from 1e21 (ECMA-262 Number.prototype.toFixed step 10); exact up
+  // to 2^127 (128-bit digits, shortest round-trip for String), `fallback` marks larger values.
+  __device__ __noinline__ void big(bool neg, double ax, int f, bool& fallback) {
+    char buf[64];
+    if (ax >= 1e21) {
+      bool inexact = false;
+      const int k = dj::js_num(buf, neg ? -ax : ax, &inexact);
+      if (inexact) fallback = true;
+      s(buf, k);
+      return;
+    }
+    if (neg) c('-');
+    const int k = dj::put_dec(buf, (unsigned __int128)ax);
+    s(buf, k);
+    c('.');
+    for (int i = 0; i < f; ++i) c('0');
   }
 };
 
@@ -121,10 +148,11 @@ __device__ void format_series(const FormatArgs& a, int32_t i, char* st_dst, char
 
 __global__ __launch_bounds__(256) void k_format_len(FormatArgs a) {
   const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == a.n) { a.st_len[a.n] = 0; a.fs_len[a.n] = 0; return; }  // scan sentinel (-> totals)
   if (i >= a.n) return;
   bool fb = false;
   format_series<false>(a, i, nullptr, nullptr, a.st_len, a.fs_len, fb);
-  if (fb) atomicOr(a.fallback, 1);
+  if (fb) atomicAdd(a.fallback, 1);
 }
 
 // Write pass, one wave per 64 consecutive series (emission order), so the wave's output is one
@@ -201,10 +229,8 @@ size_t apm_format_tmp_bytes(int32_t n_max) {
 // The *_len / *_off arrays hold n + 1 entries.
 int apm_format_plan(FormatArgs* a, void* tmp, size_t tmp_bytes, hipStream_t stream) {
   if (a->n <= 0) return 0;
-  HIP_OK(hipMemsetAsync(a->fallback, 0, 4, stream));
-  HIP_OK(hipMemsetAsync(a->st_len + a->n, 0, 4, stream));
-  HIP_OK(hipMemsetAsync(a->fs_len + a->n, 0, 4, stream));
-  hipLaunchKernelGGL(k_format_len, dim3((a->n + 255) / 256), dim3(256), 0, stream, *a);
+  // a->fallback accumulates (values beyond 2^127, printed inexactly) and is never reset here
+  hipLaunchKernelGGL(k_format_len, dim3((a->n + 1 + 255) / 256), dim3(256), 0, stream, *a);
   size_t need = tmp_bytes;
   if (rocprim::exclusive_scan(tmp, need, a->st_len, a->st_off, 0u, (size_t)a->n + 1, rocprim::plus<uint32_t>(),
                               stream) != hipSuccess)

@@ -444,6 +444,7 @@ void Engine::load_state(const std::string& path) {
       h_ser_names_.push_back((int32_t)servers_[server].size());
       h_ser_names_.push_back(service_name_off_[service]);
       h_ser_names_.push_back((int32_t)dict_.service_name(service).size());
+      max_name_len_ = std::max(max_name_len_, servers_[server].size() + dict_.service_name(service).size());
     }
     n_series_ = (int32_t)sr.size();
     perm_dirty_ = true;

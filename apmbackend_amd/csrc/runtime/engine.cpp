@@ -221,6 +221,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   HIP_OK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
   HIP_OK(hipStreamCreateWithFlags(&parse_stream_, hipStreamNonBlocking));
+  HIP_OK(hipStreamCreateWithFlags(&out_stream_, hipStreamNonBlocking));
   HIP_OK(hipEventCreate(&ev_a_));
   HIP_OK(hipEventCreate(&ev_b_));
   const int32_t S = cfg_.max_series;
@@ -241,7 +242,6 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     dc.device = cfg_.device;
     dj_.reset(new DeviceJoin(dc, &dict_, &files_, &servers_));
     device_bytes_ += dj_->device_bytes();
-    HIP_OK(hipStreamCreateWithFlags(&out_stream_, hipStreamNonBlocking));
     d_ring_min_ = (unsigned long long*)dmalloc(64);
     HIP_OK(hipHostMalloc((void**)&h_ring_min_, 64, hipHostMallocDefault));
     *h_ring_min_ = ~0ULL;
@@ -442,14 +442,16 @@ Engine::~Engine() {
     hipStreamSynchronize(out_stream_);
     hipHostFree(h_ring_min_); hipHostFree(h_rel_n_); hipHostFree(h_rel_total_); hipHostFree(h_unseen_flag_);
     for (int k = 0; k < 2; ++k) if (h_rel_text_[k]) hipHostFree(h_rel_text_[k]);
-    for (int k = 0; k < 2; ++k) {
-      if (h_pairs_k_[k]) hipHostFree(h_pairs_k_[k]);
-      if (pairs_ev_[k]) hipEventDestroy(pairs_ev_[k]);
-    }
+
     dj_.reset();
-    hipStreamDestroy(out_stream_);
   }
+  hipStreamSynchronize(out_stream_);
+  hipStreamDestroy(out_stream_);
   hipHostFree(h_fmt_meta_);
+  for (int k = 0; k < kStage; ++k) {
+    if (h_stage_[k]) hipHostFree(h_stage_[k]);
+    if (stage_ev_[k]) hipEventDestroy(stage_ev_[k]);
+  }
   hipEventDestroy(ev_a_); hipEventDestroy(ev_b_);
   hipStreamDestroy(stream_); hipStreamDestroy(comm_stream_); hipStreamDestroy(parse_stream_);
 }
@@ -554,7 +556,16 @@ int32_t Engine::series_for(int32_t server, int32_t service) {
   h_suppressed_.push_back(0);
   zscore_seen_.push_back(0);
   h_active_.push_back(0);
-  unseen_.push_back(s);
+  max_name_len_ = std::max(max_name_len_, servers_[server].size() + dict_.service_name(service).size());
+  if (cfg_.emulate_aliasing) {
+    // Q4 emulation: settings depend on the order in which the z-score stage first sees series
+    // (their first st), resolved at the rollover that makes them visible
+    unseen_.push_back(s);
+  } else {
+    // order-independent settings: resolved now, uploaded with the batch's new series
+    apply_series_settings(s);
+    zscore_seen_[s] = 1;
+  }
   return s;
 }
 
@@ -586,19 +597,30 @@ void Engine::upload_series_tables(int32_t lo) {
   if (lo < 0) lo = 0;
   if (n <= lo) return;
   const size_t m = (size_t)(n - lo);
-  std::vector<double> col(m);
-  for (int l = 0; l < cfg_.n_lags; ++l) {
-    for (size_t i = 0; i < m; ++i) col[i] = h_thr_[(size_t)(lo + i) * MAX_LAGS + l];
-    HIP_OK(hipMemcpyAsync(lag_[l].thr + lo, col.data(), m * 8, hipMemcpyHostToDevice, stream_));
-    HIP_OK(hipStreamSynchronize(stream_));  // `col` is pageable and reused
-    for (size_t i = 0; i < m; ++i) col[i] = h_infl_[(size_t)(lo + i) * MAX_LAGS + l];
-    HIP_OK(hipMemcpyAsync(lag_[l].infl + lo, col.data(), m * 8, hipMemcpyHostToDevice, stream_));
-    HIP_OK(hipStreamSynchronize(stream_));
+  // one pinned staging area: [thr, infl] per LAG, hard max, emit key (8 B each), suppressed
+  const int L = cfg_.n_lags;
+  char* st = stage(m * (8 * (2 * L + 2) + 1));
+  double* col = (double*)st;
+  for (int l = 0; l < L; ++l) {
+    double* t = col + (size_t)(2 * l) * m;
+    double* f = col + (size_t)(2 * l + 1) * m;
+    for (size_t i = 0; i < m; ++i) {
+      t[i] = h_thr_[(size_t)(lo + i) * MAX_LAGS + l];
+      f[i] = h_infl_[(size_t)(lo + i) * MAX_LAGS + l];
+    }
+    HIP_OK(hipMemcpyAsync(lag_[l].thr + lo, t, m * 8, hipMemcpyHostToDevice, stream_));
+    HIP_OK(hipMemcpyAsync(lag_[l].infl + lo, f, m * 8, hipMemcpyHostToDevice, stream_));
   }
-  HIP_OK(hipMemcpyAsync(d_hard_max_ + lo, h_hard_max_.data() + lo, m * 8, hipMemcpyHostToDevice, stream_));
-  HIP_OK(hipMemcpyAsync(d_suppressed_ + lo, h_suppressed_.data() + lo, m, hipMemcpyHostToDevice, stream_));
-  HIP_OK(hipMemcpyAsync(d_emit_key_ + lo, h_emit_key_.data() + lo, m * 8, hipMemcpyHostToDevice, stream_));
-  HIP_OK(hipStreamSynchronize(stream_));
+  double* hm = col + (size_t)(2 * L) * m;
+  uint64_t* ek = (uint64_t*)(col + (size_t)(2 * L + 1) * m);
+  uint8_t* sp = (uint8_t*)(col + (size_t)(2 * L + 2) * m);
+  std::memcpy(hm, h_hard_max_.data() + lo, m * 8);
+  std::memcpy(ek, h_emit_key_.data() + lo, m * 8);
+  std::memcpy(sp, h_suppressed_.data() + lo, m);
+  HIP_OK(hipMemcpyAsync(d_hard_max_ + lo, hm, m * 8, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpyAsync(d_emit_key_ + lo, ek, m * 8, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpyAsync(d_suppressed_ + lo, sp, m, hipMemcpyHostToDevice, stream_));
+  stage_done();
 }
 
 JoinCounters Engine::join_counters() const {
@@ -1110,16 +1132,21 @@ void Engine::flush() {
     std::lock_guard<std::mutex> g(out_mu_);
     metrics_.t_out_ms += t_out_ms_;
     t_out_ms_ = 0;
+    metrics_.formatted_bytes += formatted_bytes_lane_;
+    formatted_bytes_lane_ = 0;
     if (!out_error_.empty()) { std::string e = out_error_; out_error_.clear(); throw std::runtime_error(e); }
   }
   if (!st_error_.empty()) { std::string e = st_error_; st_error_.clear(); throw std::runtime_error(e); }
   {
     unsigned long long u[2] = {0, 0};
+    int32_t fb = 0;
     if (dev()) HIP_OK(hipMemcpyAsync(&u[0], d_unmapped_, 8, hipMemcpyDeviceToHost, stream_));
     HIP_OK(hipMemcpyAsync(&u[1], d_spill_drop_, 8, hipMemcpyDeviceToHost, stream_));
+    HIP_OK(hipMemcpyAsync(&fb, d_fmt_fallback_, 4, hipMemcpyDeviceToHost, stream_));
     HIP_OK(hipStreamSynchronize(stream_));
     metrics_.series_overflow_tx = u[0];
     metrics_.spill_dropped = u[1];
+    metrics_.format_fallbacks = (uint64_t)fb;
   }
 }
 
@@ -1241,6 +1268,7 @@ void Engine::ensure_bucket_slot(int64_t b) {
 
 void Engine::stats_for_batch(std::vector<TxOut>& txs, double batch_t0) {
   const double ts0 = now_ms();
+  const int32_t n_series_at_start = n_series_;
   const int64_t latest_at_start = latest_;
   const bool w_tx = want(OUT_TRANSACTIONS), w_audit = want(OUT_AUDIT_DB), w_db = want(OUT_DB);
   std::vector<std::string>& text = *cur_text_;
@@ -1305,6 +1333,7 @@ void Engine::stats_for_batch(std::vector<TxOut>& txs, double batch_t0) {
     ++n;
   }
   if (agg_n) { pool_bucket_count_[agg_b] += agg_n; pool_exact_edge_[agg_b] += agg_e; }
+  if (n_series_ > n_series_at_start && !cfg_.emulate_aliasing) upload_series_tables(n_series_at_start);
   for (size_t a = 0; a < n_arena; ++a)
     if (blk_live[a] > 0) {
       std::lock_guard<std::mutex> lk(blocks_mu_);
@@ -1368,6 +1397,7 @@ void Engine::stats_for_batch_dev(DevJoinBatch& b, double batch_t0) {
   if (want(OUT_TRANSACTIONS)) blob_[OUT_TRANSACTIONS] += b.text_tx;
   if (want(OUT_AUDIT_DB)) blob_[OUT_AUDIT_DB] += b.text_db;
   if (!b.unresolved.empty()) {
+    const int32_t n_before = n_series_;
     std::vector<std::pair<int32_t, int32_t>> upd;
     for (const auto& u : b.unresolved) {
       const int32_t raw = u.second;
@@ -1384,6 +1414,7 @@ void Engine::stats_for_batch_dev(DevJoinBatch& b, double batch_t0) {
       apm_dj_scatter_i32(dj_->d_raw_series(), d_pairs_, (uint32_t)upd.size(), stream_);
     }
     apm_dj_fill_series(b.d_tx, b.d_raw, b.n_stats, dj_->d_raw_series(), d_unmapped_, stream_);
+    if (n_series_ > n_before && !cfg_.emulate_aliasing) upload_series_tables(n_before);
   }
   const int64_t latest_at_start = latest_;
   std::vector<std::pair<uint32_t, int64_t>> triggers;  // a tx with a newer bucket rolls over first
@@ -1421,22 +1452,26 @@ void Engine::stats_for_batch_dev(DevJoinBatch& b, double batch_t0) {
 // Pinned staging for the stats thread's small H2D uploads (raw -> series pairs, unseen series
 // ids): two buffers used alternately, each reused only after its previous copy completed, so
 // the upload never waits for the whole stats stream.
-int32_t* Engine::pinned_pairs(size_t n_ints) {
-  const int k = pairs_k_;
-  if (pairs_ev_[k]) HIP_OK(hipEventSynchronize(pairs_ev_[k]));
-  else HIP_OK(hipEventCreateWithFlags(&pairs_ev_[k], hipEventDisableTiming));
-  if (n_ints > h_pairs_cap_[k]) {
-    if (h_pairs_k_[k]) HIP_OK(hipHostFree(h_pairs_k_[k]));
-    h_pairs_cap_[k] = n_ints * 2 + 8192;
-    HIP_OK(hipHostMalloc((void**)&h_pairs_k_[k], h_pairs_cap_[k] * 4, hipHostMallocDefault));
+char* Engine::stage(size_t bytes) {
+  const int k = stage_k_;
+  if (stage_ev_[k]) HIP_OK(hipEventSynchronize(stage_ev_[k]));
+  else HIP_OK(hipEventCreateWithFlags(&stage_ev_[k], hipEventDisableTiming));
+  if (bytes > h_stage_cap_[k]) {
+    if (h_stage_[k]) HIP_OK(hipHostFree(h_stage_[k]));
+    h_stage_cap_[k] = bytes * 2 + (1 << 16);
+    HIP_OK(hipHostMalloc((void**)&h_stage_[k], h_stage_cap_[k], hipHostMallocDefault));
   }
-  if (n_ints * 4 > pairs_bytes_) d_pairs_ = (int32_t*)regrow(d_pairs_, pairs_bytes_, n_ints * 8 + 65536);
-  return h_pairs_k_[k];
+  return h_stage_[k];
 }
 
-void Engine::pinned_pairs_done() {
-  HIP_OK(hipEventRecord(pairs_ev_[pairs_k_], stream_));
-  pairs_k_ ^= 1;
+void Engine::stage_done() {
+  HIP_OK(hipEventRecord(stage_ev_[stage_k_], stream_));
+  stage_k_ = (stage_k_ + 1) % kStage;
+}
+
+int32_t* Engine::pinned_pairs(size_t n_ints) {
+  if (n_ints * 4 > pairs_bytes_) d_pairs_ = (int32_t*)regrow(d_pairs_, pairs_bytes_, n_ints * 8 + 65536);
+  return (int32_t*)stage(n_ints * 4);
 }
 
 // K8 needs the z-score settings of series that became visible before this rollover: with the
@@ -1719,22 +1754,27 @@ void* Engine::regrow(void* old, size_t& cap, size_t need) {
 }
 
 void Engine::sync_format_tables() {
+  // uploads go through the pinned stager: nothing here waits for the stats stream
   if (names_uploaded_ < h_names_.size()) {
     if (h_names_.size() > names_cap_) {
       // grow: re-upload everything into the bigger buffer
       d_names_ = (char*)regrow(d_names_, names_cap_, h_names_.size());
       names_uploaded_ = 0;
     }
-    HIP_OK(hipMemcpyAsync(d_names_ + names_uploaded_, h_names_.data() + names_uploaded_,
-                          h_names_.size() - names_uploaded_, hipMemcpyHostToDevice, stream_));
-    HIP_OK(hipStreamSynchronize(stream_));  // h_names_ may reallocate later
+    const size_t nb = h_names_.size() - names_uploaded_;
+    char* st = stage(nb);
+    std::memcpy(st, h_names_.data() + names_uploaded_, nb);
+    HIP_OK(hipMemcpyAsync(d_names_ + names_uploaded_, st, nb, hipMemcpyHostToDevice, stream_));
+    stage_done();
     names_uploaded_ = h_names_.size();
   }
   if (ser_names_uploaded_ < n_series_) {
     const int32_t lo = ser_names_uploaded_;
-    HIP_OK(hipMemcpyAsync(d_ser_names_ + (size_t)lo * 4, h_ser_names_.data() + (size_t)lo * 4,
-                          (size_t)(n_series_ - lo) * 16, hipMemcpyHostToDevice, stream_));
-    HIP_OK(hipStreamSynchronize(stream_));
+    const size_t nb = (size_t)(n_series_ - lo) * 16;
+    char* st = stage(nb);
+    std::memcpy(st, h_ser_names_.data() + (size_t)lo * 4, nb);
+    HIP_OK(hipMemcpyAsync(d_ser_names_ + (size_t)lo * 4, st, nb, hipMemcpyHostToDevice, stream_));
+    stage_done();
     ser_names_uploaded_ = n_series_;
   }
   if (perm_dirty_) {
@@ -1753,8 +1793,11 @@ void Engine::sync_format_tables() {
       std::merge(h_perm_.begin(), h_perm_.end(), fresh.begin(), fresh.end(), merged.begin(), by_key);
       h_perm_.swap(merged);
     }
-    HIP_OK(hipMemcpyAsync(d_perm_, h_perm_.data(), (size_t)n_series_ * 4, hipMemcpyHostToDevice, stream_));
-    HIP_OK(hipStreamSynchronize(stream_));
+    const size_t nb = (size_t)n_series_ * 4;
+    char* st = stage(nb);
+    std::memcpy(st, h_perm_.data(), nb);
+    HIP_OK(hipMemcpyAsync(d_perm_, st, nb, hipMemcpyHostToDevice, stream_));
+    stage_done();
     perm_dirty_ = false;
   }
 }
@@ -1805,43 +1848,41 @@ void Engine::format_rollover_text(int64_t edge_ts) {
   fa.st_off = d_fmt_off_;
   fa.fs_off = d_fmt_off_ + (S + 1);
   fa.fallback = d_fmt_fallback_;
-  if (apm_format_plan(&fa, d_fmt_tmp_, fmt_tmp_bytes_, stream_) != 0) throw std::runtime_error("format scan failed");
-  HIP_OK(hipMemcpyAsync(h_fmt_meta_ + 0, fa.st_off + n, 4, hipMemcpyDeviceToHost, stream_));
-  HIP_OK(hipMemcpyAsync(h_fmt_meta_ + 1, fa.fs_off + n, 4, hipMemcpyDeviceToHost, stream_));
-  HIP_OK(hipMemcpyAsync(h_fmt_meta_ + 2, d_fmt_fallback_, 4, hipMemcpyDeviceToHost, stream_));
-  HIP_OK(hipStreamSynchronize(stream_));
-  trace_event("fmt.plan", tf0, now_ms(), 1);
-  if (h_fmt_meta_[2]) {
-    ++metrics_.format_fallbacks;
-    out_wait_idle();  // st / fs are lane-owned streams
-    format_rollover_text_host(edge_ts);
-    return;
-  }
-  const size_t st_total = h_fmt_meta_[0], fs_total = h_fmt_meta_[1];
-  d_fmt_out_[0] = (char*)regrow(d_fmt_out_[0], fmt_out_cap_[0], st_total + 1);
-  d_fmt_out_[1] = (char*)regrow(d_fmt_out_[1], fmt_out_cap_[1], fs_total + 1);
-  fa.st_out = d_fmt_out_[0];
-  fa.fs_out = d_fmt_out_[1];
-  apm_format_write(&fa, stream_);
-  // D2H into one of two pinned staging buffers; the output lane waits for it and emits st / fs
-  // while this thread goes on (alerts, next rollover / batch)
+  // Output bound from the name lengths (numbers are at most ~25 characters), so nothing waits
+  // for the length pass: the output lane reads the real totals after the event.
   const int k = fmt_k_;
   fmt_k_ ^= 1;
   const double tf1 = now_ms();
-  out_wait(fmt_task_[k]);
+  out_wait(fmt_task_[k]);  // slot k's previous D2H + emission is done
   trace_event("fmt.wait_lane", tf1, now_ms(), 1);
-  if (st_total + fs_total > h_fmt_cap_[k]) {
-    if (h_fmt_out_[k]) HIP_OK(hipHostFree(h_fmt_out_[k]));
-    h_fmt_cap_[k] = (st_total + fs_total) * 3 / 2 + (1 << 20);
-    HIP_OK(hipHostMalloc((void**)&h_fmt_out_[k], h_fmt_cap_[k], hipHostMallocDefault));
-  }
-  char* h = h_fmt_out_[k];
-  if (st_total) HIP_OK(hipMemcpyAsync(h, fa.st_out, st_total, hipMemcpyDeviceToHost, stream_));
-  if (fs_total) HIP_OK(hipMemcpyAsync(h + st_total, fa.fs_out, fs_total, hipMemcpyDeviceToHost, stream_));
+  const size_t st_cap = fa.want_st ? (size_t)n * (176 + max_name_len_) : 0;
+  const size_t fs_cap = fa.want_fs ? (size_t)n * cfg_.n_lags * (560 + max_name_len_) : 0;
+  if (st_cap + fs_cap + 64 > fmt_out_cap_[k]) d_fmt_out_[k] = (char*)regrow(d_fmt_out_[k], fmt_out_cap_[k], st_cap + fs_cap + 64);
+  fa.st_out = d_fmt_out_[k];
+  fa.fs_out = d_fmt_out_[k] + st_cap;
+  if (apm_format_plan(&fa, d_fmt_tmp_, fmt_tmp_bytes_, stream_) != 0) throw std::runtime_error("format scan failed");
+  apm_format_write(&fa, stream_);
+  HIP_OK(hipMemcpyAsync(h_fmt_meta_ + 4 * k + 0, fa.st_off + n, 4, hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipMemcpyAsync(h_fmt_meta_ + 4 * k + 1, fa.fs_off + n, 4, hipMemcpyDeviceToHost, stream_));
   HIP_OK(hipEventRecord(ev_fmt_[k], stream_));
-  metrics_.formatted_bytes += st_total + fs_total;
-  fmt_task_[k] = post_out([this, k, h, st_total, fs_total]() {
+  trace_event("fmt.plan", tf0, now_ms(), 1);
+  char* dst = d_fmt_out_[k];
+  fmt_task_[k] = post_out([this, k, dst, st_cap]() {
     HIP_OK(hipEventSynchronize(ev_fmt_[k]));
+    const size_t st_total = h_fmt_meta_[4 * k], fs_total = h_fmt_meta_[4 * k + 1];
+    if (st_total + fs_total > h_fmt_cap_[k]) {
+      if (h_fmt_out_[k]) HIP_OK(hipHostFree(h_fmt_out_[k]));
+      h_fmt_cap_[k] = (st_total + fs_total) * 3 / 2 + (1 << 20);
+      HIP_OK(hipHostMalloc((void**)&h_fmt_out_[k], h_fmt_cap_[k], hipHostMallocDefault));
+    }
+    char* h = h_fmt_out_[k];
+    if (st_total) HIP_OK(hipMemcpyAsync(h, dst, st_total, hipMemcpyDeviceToHost, out_stream_));
+    if (fs_total) HIP_OK(hipMemcpyAsync(h + st_total, dst + st_cap, fs_total, hipMemcpyDeviceToHost, out_stream_));
+    HIP_OK(hipStreamSynchronize(out_stream_));
+    {
+      std::lock_guard<std::mutex> g(out_mu_);
+      formatted_bytes_lane_ += st_total + fs_total;
+    }
     emit_bytes(OUT_ST, h, st_total);
     emit_bytes(OUT_FS, h + st_total, fs_total);
   });

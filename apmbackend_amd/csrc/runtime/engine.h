@@ -374,6 +374,7 @@ class Engine {
   bool out_stop_ = false;
   std::string out_error_;
   double t_out_ms_ = 0;  // lane busy time (folded into metrics_ by flush)
+  uint64_t formatted_bytes_lane_ = 0;  // st/fs bytes emitted by the lane (folded by flush)
   size_t device_bytes_ = 0;
   std::vector<void*> allocations_;
 
@@ -432,14 +433,20 @@ class Engine {
   size_t h_rel_text_cap_[2] = {0, 0};
   hipStream_t out_stream_ = nullptr;
   std::vector<int32_t> h_raw_series_;          // stats thread mirror of the raw -> series table
-  int32_t* h_pairs_k_[2] = {nullptr, nullptr};  // pinned staging of small uploads (alternating)
-  size_t h_pairs_cap_[2] = {0, 0};
-  hipEvent_t pairs_ev_[2] = {nullptr, nullptr};
-  int pairs_k_ = 0;
+  // pinned staging of the stats thread's H2D uploads: kStage buffers used in rotation, each
+  // reused only after its previous copy completed (an event), so no upload waits for the stream
+  static constexpr int kStage = 4;
+  char* h_stage_[kStage] = {};
+  size_t h_stage_cap_[kStage] = {};
+  hipEvent_t stage_ev_[kStage] = {};
+  int stage_k_ = 0;
+  char* stage(size_t bytes);
+  void stage_done();
   int32_t* d_pairs_ = nullptr;
   size_t pairs_bytes_ = 0;
   int32_t* pinned_pairs(size_t n_ints);
-  void pinned_pairs_done();
+  void pinned_pairs_done() { stage_done(); }
+  size_t max_name_len_ = 0;  // longest server + service name of any series (K12 output bound)
   int32_t* d_unseen_idx_ = nullptr;
   uint8_t* d_unseen_flag_ = nullptr;
   uint8_t* h_unseen_flag_ = nullptr;
@@ -594,7 +601,7 @@ class Engine {
   hipEvent_t ev_fmt_[2] = {nullptr, nullptr};
   uint64_t fmt_task_[2] = {0, 0};
   int fmt_k_ = 0;
-  uint32_t* h_fmt_meta_ = nullptr;               // pinned: st total, fs total, fallback
+  uint32_t* h_fmt_meta_ = nullptr;               // pinned: per slot k, [4k] st total, [4k+1] fs total
 
   // text outputs
   std::string blob_[N_OUT];
