@@ -100,6 +100,7 @@ EngineConfig config_from(const py::dict& d) {
   c.join_threads = get<int>(d, "join_threads", c.join_threads);
   c.pin_threads = get<bool>(d, "pin_threads", c.pin_threads);
   c.coll_timeout_ms = get<double>(d, "coll_timeout_ms", c.coll_timeout_ms);
+  c.node_cooldown = get<int>(d, "node_cooldown", c.node_cooldown);
   c.outputs = get<uint32_t>(d, "outputs", c.outputs);
   c.async_stats = get<int>(d, "async_stats", c.async_stats);
   c.device_join = get<int>(d, "device_join", c.device_join);
@@ -249,6 +250,10 @@ PYBIND11_MODULE(_apm_native, m) {
   }, py::arg("data"), py::arg("seed") = kHashSeed);
   m.attr("NSLOT") = NSLOT;
 
+  py::class_<LocalGroup, std::shared_ptr<LocalGroup>>(m, "LocalCollGroup")
+      .def(py::init([](int n, double timeout_ms) { return make_local_group(n, timeout_ms); }), py::arg("n"),
+           py::arg("timeout_ms") = 120000.0);
+
   py::class_<Engine>(m, "Engine")
       .def(py::init([](const py::dict& d) { return new Engine(config_from(d)); }))
       .def("add_file", &Engine::add_file)
@@ -369,6 +374,12 @@ PYBIND11_MODULE(_apm_native, m) {
         return py::bytes((const char*)v.data(), v.size() * 8);
       })
       .def("fleet_rounds", &Engine::fleet_rounds)
+      .def("fleet_init_local", [](Engine& e, std::shared_ptr<LocalGroup> g, int rank, int32_t cap, bool lockstep) {
+        py::gil_scoped_release rel;
+        e.fleet_init_local(std::move(g), rank, cap, lockstep);
+      }, py::arg("group"), py::arg("rank"), py::arg("cap"), py::arg("lockstep") = true)
+      .def("set_server_index", &Engine::set_server_index)
+      .def("node_drain", [](Engine& e) { py::gil_scoped_release rel; e.node_drain(); })
       .def("pack_service_moments", [](Engine& e, uintptr_t dst, int32_t cap, bool atomic_path) {
         e.pack_service_moments((double*)dst, cap, e.comm_stream(), atomic_path);
       }, py::arg("dst"), py::arg("cap"), py::arg("atomic_path") = false)

@@ -147,6 +147,10 @@ void apm_format_fixed_batch(const double* d_x, int n, int f, char* d_out, hipStr
 int apm_format_plan(apm::FormatArgs* a, void* tmp, size_t tmp_bytes, hipStream_t stream);
 void apm_format_write(apm::FormatArgs* a, hipStream_t stream);
 void apm_alert_eval(apm::AlertArgs* a, hipStream_t stream);
+// rows of the alert candidates (window stats + the candidate LAG's z-score output), compacted in
+// candidate order: the host formats al rows from n records instead of downloading every series
+void apm_alert_gather(const apm::AlertRec* alerts, int32_t n, const apm::WinStat* win, const apm::ZOut* const* z_by_lag,
+                      int32_t n_lags, apm::WinStat* win_out, apm::ZOut* z_out, hipStream_t stream);
 // fleet.hip
 void apm_service_moments(const int32_t* series_service, const uint8_t* active, int32_t n_series, int32_t S,
                          int32_t n_lags, int32_t n_services_cap, const double* const* sums, const double* const* comps,

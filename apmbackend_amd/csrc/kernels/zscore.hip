@@ -299,6 +299,32 @@ void apm_zscore_warm(ZArgs* a, int dtype_bytes, int fill, uint64_t seed, const W
   else hipLaunchKernelGGL(k_zscore_warm<uint16_t>, g, b, 0, stream, *a, fill, seed, base);
 }
 
+struct AlertGather {
+  const AlertRec* alerts;
+  const WinStat* win;
+  const ZOut* z[MAX_LAGS];
+  WinStat* win_out;
+  ZOut* z_out;
+  int32_t n;
+};
+
+__global__ void k_alert_gather(AlertGather a) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  const AlertRec r = a.alerts[i];
+  a.win_out[i] = a.win[r.series];
+  a.z_out[i] = a.z[r.lag_idx][r.series];
+}
+
+void apm_alert_gather(const AlertRec* alerts, int32_t n, const WinStat* win, const ZOut* const* z_by_lag, int32_t n_lags,
+                      WinStat* win_out, ZOut* z_out, hipStream_t stream) {
+  if (n <= 0) return;
+  AlertGather a{};
+  a.alerts = alerts; a.win = win; a.win_out = win_out; a.z_out = z_out; a.n = n;
+  for (int l = 0; l < n_lags && l < MAX_LAGS; ++l) a.z[l] = z_by_lag[l];
+  hipLaunchKernelGGL(k_alert_gather, dim3((n + 255) / 256), dim3(256), 0, stream, a);
+}
+
 void apm_alert_eval(AlertArgs* a, hipStream_t stream) {
   if (a->n_series <= 0) return;
   hipLaunchKernelGGL(k_alert_eval, dim3((a->n_series + 255) / 256), dim3(256), 0, stream, *a);

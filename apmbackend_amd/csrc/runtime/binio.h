@@ -20,7 +20,7 @@
 
 namespace apm {
 
-constexpr uint32_t kCkptVersion = 3;  // 3: join section carries the join mode (host / GPU)
+constexpr uint32_t kCkptVersion = 4;  // 3: join section carries the join mode (host / GPU); 4: node-wide server order
 
 class BinWriter {
  public:

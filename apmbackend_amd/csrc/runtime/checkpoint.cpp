@@ -255,6 +255,7 @@ uint64_t Engine::save_state(const std::string& path) {
     w.vec(sr);
   }
   w.vec(server_rank_); w.vec(server_next_service_); w.pod(next_server_rank_);
+  w.vec(server_gidx_); w.vec(server_first_batch_);
   w.vec(h_thr_); w.vec(h_infl_); w.vec(h_hard_max_); w.vec(h_suppressed_); w.vec(h_emit_key_);
   w.vec(zscore_seen_); w.vec(h_active_); w.vec(unseen_);
   w.raw(alias_thr_, sizeof(alias_thr_)); w.raw(alias_infl_, sizeof(alias_infl_));
@@ -423,6 +424,8 @@ void Engine::load_state(const std::string& path) {
     server_rank_ = rd.vec<int32_t>();
     server_next_service_ = rd.vec<int32_t>();
     rd.pod(next_server_rank_);
+    server_gidx_ = rd.vec<int32_t>();
+    server_first_batch_ = rd.vec<int64_t>();
     h_thr_ = rd.vec<double>(); h_infl_ = rd.vec<double>(); h_hard_max_ = rd.vec<double>();
     h_suppressed_ = rd.vec<uint8_t>(); h_emit_key_ = rd.vec<uint64_t>();
     zscore_seen_ = rd.vec<int32_t>(); h_active_ = rd.vec<uint8_t>(); unseen_ = rd.vec<int32_t>();

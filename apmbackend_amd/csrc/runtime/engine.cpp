@@ -348,6 +348,10 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   d_alerts_ = (AlertRec*)dmalloc((size_t)cfg_.max_alerts * sizeof(AlertRec));
   d_n_alerts_ = (int32_t*)dmalloc(16);
   HIP_OK(hipHostMalloc((void**)&h_alerts_, (size_t)cfg_.max_alerts * sizeof(AlertRec), hipHostMallocDefault));
+  d_alert_win_ = (WinStat*)dmalloc((size_t)cfg_.max_alerts * sizeof(WinStat));
+  d_alert_z_ = (ZOut*)dmalloc((size_t)cfg_.max_alerts * sizeof(ZOut));
+  HIP_OK(hipHostMalloc((void**)&h_alert_win_, (size_t)cfg_.max_alerts * sizeof(WinStat), hipHostMallocDefault));
+  HIP_OK(hipHostMalloc((void**)&h_alert_z_, (size_t)cfg_.max_alerts * sizeof(ZOut), hipHostMallocDefault));
   HIP_OK(hipHostMalloc((void**)&h_n_alerts_, 16, hipHostMallocDefault));
   // tx + release
   d_tx_ = (TxRec*)dmalloc((size_t)cfg_.max_tx_per_batch * sizeof(TxRec));
@@ -411,12 +415,14 @@ Engine::~Engine() {
   }
   out_cv_.notify_all();
   if (out_thread_.joinable()) out_thread_.join();
-  if (fleet_comm_) {
+  if (coll_) {
     hipStreamSynchronize(comm_stream_);
     hipStreamSynchronize(coll_stream_);
-    if (!comm_aborted_) ncclCommDestroy(fleet_comm_);  // an aborted communicator is already freed
-    fleet_comm_ = nullptr;
+    coll_.reset();
     for (int i = 0; i < 2; ++i) { hipEventDestroy(fleet_ev_[i]); hipEventDestroy(pack_ev_[i]); }
+    if (node_ev_) hipEventDestroy(node_ev_);
+    if (h_node_send_) hipHostFree(h_node_send_);
+    if (h_node_recv_) hipHostFree(h_node_recv_);
     hipStreamDestroy(coll_stream_);
   }
   if (h_sync_) hipHostFree(h_sync_);
@@ -429,6 +435,8 @@ Engine::~Engine() {
     hipHostFree(ps.h_counts); hipHostFree(ps.h_watermark);
   }
   hipHostFree(h_alerts_);
+  hipHostFree(h_alert_win_);
+  hipHostFree(h_alert_z_);
   if (h_series_service_) hipHostFree(h_series_service_);
   hipHostFree(h_n_alerts_); hipHostFree(h_tx_); hipHostFree(h_gid_);
   for (int k = 0; k < 2; ++k) {
@@ -465,6 +473,8 @@ int32_t Engine::add_server(const std::string& name) {
   server_ids_[name] = id;
   server_rank_.push_back(-1);
   server_next_service_.push_back(0);
+  server_gidx_.push_back(id);
+  server_first_batch_.push_back(-1);
   JoinConfig jc;
   jc.record_ttl_ms = cfg_.record_ttl_ms;
   jc.acct_ttl_ms = cfg_.acct_ttl_ms;
@@ -535,7 +545,10 @@ int32_t Engine::series_for(int32_t server, int32_t service) {
   const int32_t s = n_series_++;
   series_map_[key] = s + 1;
   ser_tab_put(server, service, s);
-  if (server_rank_[server] < 0) server_rank_[server] = next_server_rank_++;
+  if (server_rank_[server] < 0) {
+    server_rank_[server] = next_server_rank_++;
+    server_first_batch_[server] = (int64_t)stats_seq_;
+  }
   const uint64_t ek = ((uint64_t)server_rank_[server] << 24) | (uint64_t)(server_next_service_[server]++);
   series_.push_back(SeriesInfo{server, service, ek});
   h_emit_key_.push_back(ek);
@@ -940,7 +953,7 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
   const double tp1 = now_ms();
   trace_event("post", tp0, tp1, 0);
   // post_stats returned: the stats thread finished (and packed) every earlier batch
-  if (fleet_comm_) fleet_exchange_upto(fleet_posted_ - 1);
+  if (coll_) fleet_exchange_upto(fleet_posted_ - 1);
   trace_event("fleet.exchange", tp1, now_ms(), 0);
   metrics_.t_total_ms += now_ms() - t0;
   ++batch_no_;
@@ -991,7 +1004,7 @@ void Engine::process_batch_dev_tail(ParseSlot& ps, double t0, double now_overrid
   post_stats_dev(std::move(b), t0, lockstep_ ? sync_latest_ : INT64_MIN);
   const double tp1 = now_ms();
   trace_event("post", tp0, tp1, 0);
-  if (fleet_comm_) fleet_exchange_upto(fleet_posted_ - 1);
+  if (coll_) fleet_exchange_upto(fleet_posted_ - 1);
   trace_event("fleet.exchange", tp1, now_ms(), 0);
   metrics_.t_total_ms += now_ms() - t0;
   ++batch_no_;
@@ -1030,12 +1043,17 @@ void Engine::stats_worker() {
       job.t0 = st_job_.t0;
       job.sync_latest = st_job_.sync_latest;
       job.dev = st_job_.dev;
+      job.seq = st_job_.seq;
+      job.round = st_job_.round;
       std::swap(job.dj, st_job_.dj);
       st_has_job_ = false;
     }
     const double t = now_ms();
     roctxRangePushA("apm.stats");
     try {
+      stats_seq_ = job.seq;
+      stats_round_ = job.round;
+      if (node_mode_) node_take_text();
       if (job.dev) {
         stats_for_batch_dev(job.dj, job.t0);
       } else {
@@ -1095,7 +1113,9 @@ void Engine::post_stats(std::vector<std::vector<TxOut>>&& outs, bool multi, doub
   }
   st_job_.t0 = t0;
   st_job_.sync_latest = sync_latest;
-  if (fleet_comm_) ++fleet_posted_;
+  st_job_.seq = batch_no_;
+  st_job_.round = fleet_posted_;
+  if (coll_) ++fleet_posted_;
   st_has_job_ = true;
   st_busy_ = true;
   lk.unlock();
@@ -1115,7 +1135,9 @@ void Engine::post_stats_dev(DevJoinBatch&& b, double t0, int64_t sync_latest) {
   st_job_.dj = std::move(b);
   st_job_.t0 = t0;
   st_job_.sync_latest = sync_latest;
-  if (fleet_comm_) ++fleet_posted_;
+  st_job_.seq = batch_no_;
+  st_job_.round = fleet_posted_;
+  if (coll_) ++fleet_posted_;
   st_has_job_ = true;
   st_busy_ = true;
   lk.unlock();
@@ -1137,6 +1159,12 @@ void Engine::flush() {
     if (!out_error_.empty()) { std::string e = out_error_; out_error_.clear(); throw std::runtime_error(e); }
   }
   if (!st_error_.empty()) { std::string e = st_error_; st_error_.clear(); throw std::runtime_error(e); }
+  if (node_mode_) {  // decided node-wide alerts (ingest thread) -> the al stream
+    node_take_text();
+    drain_kind(OUT_AL);
+    metrics_.alerts += node_alerts_;
+    node_alerts_ = 0;
+  }
   {
     unsigned long long u[2] = {0, 0};
     int32_t fb = 0;
@@ -1699,21 +1727,60 @@ void Engine::flush_alerts(int64_t edge_ts) {
   int32_t na = std::min(*h_n_alerts_, cfg_.max_alerts);
   metrics_.alert_candidates += na;
   if (na <= 0) return;
-  HIP_OK(hipMemcpyAsync(h_alerts_, d_alerts_, (size_t)na * sizeof(AlertRec), hipMemcpyDeviceToHost, stream_));
-  HIP_OK(hipStreamSynchronize(stream_));
-  std::sort(h_alerts_, h_alerts_ + na, [](const AlertRec& a, const AlertRec& b) { return a.order < b.order; });
-  // per-(service|series) cooldown, first candidate in emission order wins (:436-468)
-  std::vector<WinStat> win;
-  std::vector<std::vector<ZOut>> z(cfg_.n_lags);
   const bool need_rows = want(OUT_AL);
   if (need_rows) {
-    download_winstats(win);
-    for (int l = 0; l < cfg_.n_lags; ++l) download_zout(l, z[l]);
+    const ZOut* zl[MAX_LAGS] = {};
+    for (int l = 0; l < cfg_.n_lags; ++l) zl[l] = lag_[l].out;
+    apm_alert_gather(d_alerts_, na, d_win_, zl, cfg_.n_lags, d_alert_win_, d_alert_z_, stream_);
+    HIP_OK(hipMemcpyAsync(h_alert_win_, d_alert_win_, (size_t)na * sizeof(WinStat), hipMemcpyDeviceToHost, stream_));
+    HIP_OK(hipMemcpyAsync(h_alert_z_, d_alert_z_, (size_t)na * sizeof(ZOut), hipMemcpyDeviceToHost, stream_));
   }
+  HIP_OK(hipMemcpyAsync(h_alerts_, d_alerts_, (size_t)na * sizeof(AlertRec), hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+  // candidate i's rows are win_of(i) / z_of(i) in device order; decide in emission order
+  std::vector<int32_t> ord((size_t)na);
+  for (int32_t i = 0; i < na; ++i) ord[i] = i;
+  std::sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return h_alerts_[a].order < h_alerts_[b].order; });
+  // per-(service|series) cooldown, first candidate in emission order wins (:436-468)
   const double now = cfg_.alert_clock_entry ? (double)edge_ts
                                             : (double)std::chrono::duration_cast<std::chrono::milliseconds>(
                                                   std::chrono::system_clock::now().time_since_epoch()).count();
-  for (int32_t i = 0; i < na; ++i) {
+  if (node_mode_) {
+    // node-wide cooldown: queue the candidates (decided by the ingest thread, node_resolve)
+    std::lock_guard<std::mutex> g(node_mu_);
+    for (int32_t j = 0; j < na; ++j) {
+      const int32_t i = ord[j];
+      const AlertRec& r = h_alerts_[i];
+      const SeriesInfo& si = series_[r.series];
+      const std::string& svc = dict_.service_name(si.service);
+      NodePayload p;
+      p.seq_batch = stats_round_;
+      p.c = NodeCand{};
+      p.c.edge_ts = edge_ts;
+      p.c.first_batch = server_first_batch_[si.server];
+      p.c.gidx = server_gidx_[si.server];
+      p.c.seq = (uint32_t)(si.emit_key & 0xffffffu);
+      p.c.lag_idx = r.lag_idx;
+      p.c.causes = r.causes;
+      uint64_t h = hash_bytes((const uint8_t*)svc.data(), svc.size());
+      if (!cfg_.cooldown_by_service) {
+        const std::string& sv = servers_[si.server];
+        h = hash_mix(h, hash_bytes((const uint8_t*)sv.data(), sv.size()));
+      }
+      p.c.key = h;
+      p.c.now = now;
+      p.c.rank = coll_->rank();
+      p.c.local_id = node_next_id_++;
+      p.server = servers_[si.server];
+      p.service = svc;
+      if (need_rows)
+        p.fs = fmt::fs_line(edge_ts, servers_[si.server], svc, cfg_.lags[r.lag_idx], h_alert_win_[i], h_alert_z_[i]);
+      node_q_.push_back(std::move(p));
+    }
+    return;
+  }
+  for (int32_t j = 0; j < na; ++j) {
+    const int32_t i = ord[j];
     const AlertRec& r = h_alerts_[i];
     const SeriesInfo& si = series_[r.series];
     std::string key = dict_.service_name(si.service);
@@ -1724,7 +1791,7 @@ void Engine::flush_alerts(int64_t edge_ts) {
     ++metrics_.alerts;
     if (need_rows) {
       const std::string fs = fmt::fs_line(edge_ts, servers_[si.server], dict_.service_name(si.service),
-                                          cfg_.lags[r.lag_idx], win[r.series], z[r.lag_idx][r.series]);
+                                          cfg_.lags[r.lag_idx], h_alert_win_[i], h_alert_z_[i]);
       blob_[OUT_AL] += fmt::al_line(now, edge_ts, servers_[si.server], dict_.service_name(si.service), r.causes, fs);
       blob_[OUT_AL] += '\n';
     }
@@ -2166,24 +2233,30 @@ void Engine::pack_service_moments(double* d_dst, int32_t cap, hipStream_t stream
 // the thread timing, and no other stream ever waits on a peer (two communicators driven from
 // two threads can deadlock once their streams share a hardware queue).  Two device slots: the
 // exchange of batch j lands in slot j%2; `fleet_merged` flushes the pending one and reads it.
-std::vector<uint8_t> Engine::fleet_unique_id() {
-  ncclUniqueId id;
-  if (ncclGetUniqueId(&id) != ncclSuccess) throw std::runtime_error("ncclGetUniqueId failed");
-  return std::vector<uint8_t>((uint8_t*)&id, (uint8_t*)&id + sizeof(id));
-}
+std::vector<uint8_t> Engine::fleet_unique_id() { return rccl_unique_id(); }
 
 void Engine::fleet_init(const std::vector<uint8_t>& uid, const std::vector<uint8_t>& clock_uid, int nranks, int rank,
                         int32_t cap) {
   flush();
-  if (fleet_comm_) throw std::runtime_error("fleet_init called twice");
-  if (uid.size() != sizeof(ncclUniqueId) || (!clock_uid.empty() && clock_uid.size() != sizeof(ncclUniqueId)))
-    throw std::runtime_error("bad unique id size");
+  if (coll_) throw std::runtime_error("fleet_init called twice");
+  if (!clock_uid.empty() && clock_uid.size() != uid.size()) throw std::runtime_error("bad unique id size");
   if (cap <= 0) throw std::runtime_error("fleet_init: cap must be > 0");
-  ncclUniqueId id;
-  std::memcpy(&id, uid.data(), sizeof(id));
   HIP_OK(hipSetDevice(cfg_.device));
-  if (ncclCommInitRank(&fleet_comm_, nranks, id, rank) != ncclSuccess)
-    throw std::runtime_error("ncclCommInitRank failed");
+  coll_ = make_rccl_collective(uid, nranks, rank);
+  fleet_setup(cap, !clock_uid.empty());
+}
+
+void Engine::fleet_init_local(std::shared_ptr<LocalGroup> group, int rank, int32_t cap, bool lockstep) {
+  flush();
+  if (coll_) throw std::runtime_error("fleet_init called twice");
+  if (cap <= 0) throw std::runtime_error("fleet_init: cap must be > 0");
+  HIP_OK(hipSetDevice(cfg_.device));
+  coll_ = make_local_collective(std::move(group), rank);
+  fleet_setup(cap, lockstep);
+}
+
+void Engine::fleet_setup(int32_t cap, bool lockstep) {
+  const int nranks = coll_->nranks();
   // Highest priority: with GPU_MAX_HW_QUEUES = 4 the engine's streams share hardware queues, and
   // the 16-byte clock collective the ingest thread waits for would otherwise queue behind the
   // stats stream's 20 MB st/fs D2H blit.
@@ -2194,7 +2267,7 @@ void Engine::fleet_init(const std::vector<uint8_t>& uid, const std::vector<uint8
   const char* se = std::getenv("APM_FLEET_SKIP_SOLO");  // diagnostic: skip the one-rank (identity) all-reduce
   fleet_skip_solo_ = nranks == 1 && se && se[0] == '1';
   fleet_nranks_ = nranks;
-  lockstep_ = !clock_uid.empty();
+  lockstep_ = lockstep;
   if (lockstep_) {
     d_sync_ = (double*)dmalloc(64);
     HIP_OK(hipHostMalloc((void**)&h_sync_, 64, hipHostMallocDefault));
@@ -2208,6 +2281,15 @@ void Engine::fleet_init(const std::vector<uint8_t>& uid, const std::vector<uint8
     HIP_OK(hipEventCreateWithFlags(&pack_ev_[i], hipEventDisableTiming));
   }
   fleet_rounds_ = fleet_posted_ = fleet_packed_ = 0;
+  node_mode_ = lockstep_ && cfg_.node_cooldown != 0;
+  if (node_mode_) {
+    const size_t per = sizeof(NodeHdr) + (size_t)node_cap_ * sizeof(NodeCand);
+    d_node_send_ = (uint8_t*)dmalloc(per);
+    d_node_recv_ = (uint8_t*)dmalloc(per * (size_t)nranks);
+    HIP_OK(hipHostMalloc((void**)&h_node_send_, per, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void**)&h_node_recv_, per * (size_t)nranks, hipHostMallocDefault));
+    HIP_OK(hipEventCreateWithFlags(&node_ev_, hipEventDisableTiming));
+  }
 }
 
 // Watchdog for the ingest thread's collectives.  A launch error or an asynchronous RCCL error
@@ -2215,25 +2297,19 @@ void Engine::fleet_init(const std::vector<uint8_t>& uid, const std::vector<uint8
 // aborts the communicator (ncclCommAbort unblocks the wedged kernel) and throws: the service
 // exits non-zero and the supervisor restarts the whole rank group from its checkpoints, which is
 // how the node degrades / recovers instead of hanging every rank forever.
-void Engine::coll_check(ncclResult_t r, const char* what) {
-  if (r == ncclSuccess || r == ncclInProgress) return;
-  ncclCommAbort(fleet_comm_);
-  comm_aborted_ = true;
-  throw std::runtime_error(std::string("RCCL ") + what + " failed: " + ncclGetErrorString(r));
-}
-
 void Engine::coll_wait(hipStream_t s, hipEvent_t ev, const char* what) {
   const double t0 = now_ms();
   for (int spin = 0;; ++spin) {
     const hipError_t e = ev ? hipEventQuery(ev) : hipStreamQuery(s);
     if (e == hipSuccess) return;
     if (e != hipErrorNotReady) HIP_OK(e);
-    ncclResult_t ar = ncclSuccess;
-    if (ncclCommGetAsyncError(fleet_comm_, &ar) != ncclSuccess) ar = ncclSuccess;
-    if (ar != ncclSuccess && ar != ncclInProgress) coll_check(ar, what);
+    const std::string ae = coll_->async_error();
+    if (!ae.empty()) {
+      coll_->abort();
+      throw std::runtime_error(std::string("collective ") + what + " failed: " + ae);
+    }
     if (now_ms() - t0 > cfg_.coll_timeout_ms) {
-      ncclCommAbort(fleet_comm_);
-      comm_aborted_ = true;
+      coll_->abort();
       throw std::runtime_error(std::string("RCCL ") + what + ": no completion after " +
                                std::to_string((long long)cfg_.coll_timeout_ms) + " ms (peer rank dead or wedged)");
     }
@@ -2248,7 +2324,7 @@ void Engine::coll_wait(hipStream_t s, hipEvent_t ev, const char* what) {
 // the one stats_for_batch derives (non-db tx with a usable endTs), so ranks agree on `latest`
 // without the stats thread touching the communicator.
 void Engine::lockstep_sync(int64_t batch_max) {
-  if (comm_aborted_) throw std::runtime_error("RCCL communicator was aborted");
+  if (coll_->aborted()) throw std::runtime_error("collective communicator was aborted");
   const int64_t b = std::max(sync_latest_, batch_max);
   // The collective runs at every world size, N = 1 included (MAX over one rank is the identity,
   // but the single-GPU run then does the same per-batch work -- H2D, all-reduce, D2H, wait --
@@ -2256,11 +2332,13 @@ void Engine::lockstep_sync(int64_t batch_max) {
   h_sync_[0] = watermark_;
   h_sync_[1] = b == INT64_MIN ? -1.0 : (double)b;  // buckets < 2^53: exact in a double
   HIP_OK(hipMemcpyAsync(d_sync_, h_sync_, 16, hipMemcpyHostToDevice, coll_stream_));
-  coll_check(ncclAllReduce(d_sync_, d_sync_, 2, ncclDouble, ncclMax, fleet_comm_, coll_stream_), "lock-step clocks");
+  coll_->all_reduce_f64(d_sync_, 2, /*max=*/true, coll_stream_);
   HIP_OK(hipMemcpyAsync(h_sync_, d_sync_, 16, hipMemcpyDeviceToHost, coll_stream_));
   coll_wait(coll_stream_, nullptr, "lock-step clocks");
   watermark_ = h_sync_[0];
   if (h_sync_[1] >= 0) sync_latest_ = std::max(sync_latest_, (int64_t)h_sync_[1]);
+  // the coll stream is in order: the previous batch's alert gather has landed too
+  if (node_round_pending_) node_resolve();
 }
 
 // Stats thread: every rank rolls over when any rank saw a newer bucket, exactly as the single
@@ -2274,7 +2352,7 @@ void Engine::apply_latest_locked(int64_t g, double batch_t0) {
 
 // Stats thread: pack this batch's moments into its slot (after the slot's previous all-reduce).
 void Engine::fleet_pack_locked() {
-  if (!fleet_comm_) return;
+  if (!coll_) return;
   const int slot = (int)(fleet_packed_ & 1);
   if (fleet_packed_ >= 2) HIP_OK(hipStreamWaitEvent(comm_stream_, fleet_ev_[slot], 0));
   const double t0 = now_ms();
@@ -2286,14 +2364,13 @@ void Engine::fleet_pack_locked() {
 
 // Ingest thread: all-reduce the packed batches [fleet_rounds_, rounds).
 void Engine::fleet_exchange_upto(uint64_t rounds) {
-  if (comm_aborted_ && fleet_rounds_ < rounds) throw std::runtime_error("RCCL communicator was aborted");
+  if (coll_->aborted() && fleet_rounds_ < rounds) throw std::runtime_error("collective communicator was aborted");
   while (fleet_rounds_ < rounds) {
     const int slot = (int)(fleet_rounds_ & 1);
     HIP_OK(hipStreamWaitEvent(coll_stream_, pack_ev_[slot], 0));
-    if (!fleet_skip_solo_)
-      coll_check(ncclAllReduce(fleet_buf_[slot], fleet_buf_[slot], fleet_elems_, ncclDouble, ncclSum, fleet_comm_,
-                             coll_stream_), "fleet moments");
+    if (!fleet_skip_solo_) coll_->all_reduce_f64(fleet_buf_[slot], fleet_elems_, /*max=*/false, coll_stream_);
     HIP_OK(hipEventRecord(fleet_ev_[slot], coll_stream_));
+    if (node_mode_) node_round(fleet_rounds_, /*wait=*/false);
     ++fleet_rounds_;
   }
 }
@@ -2301,7 +2378,7 @@ void Engine::fleet_exchange_upto(uint64_t rounds) {
 std::vector<double> Engine::fleet_merged() {
   flush();  // every posted batch is packed
   std::vector<double> out;
-  if (!fleet_comm_) return out;
+  if (!coll_) return out;
   fleet_exchange_upto(fleet_posted_);
   if (fleet_rounds_ == 0) return out;
   const int slot = (int)((fleet_rounds_ - 1) & 1);
@@ -2309,6 +2386,126 @@ std::vector<double> Engine::fleet_merged() {
   out.resize(fleet_elems_);
   HIP_OK(hipMemcpy(out.data(), fleet_buf_[slot], fleet_elems_ * 8, hipMemcpyDeviceToHost));
   return out;
+}
+
+// ---- node-wide alert cooldown -------------------------------------------------------------
+// The reference has ONE alerts process: a service alerting on two JVMs in the same interval
+// yields one alert, the first in the z-score stage's emission order, and the cooldown then
+// silences the service everywhere (stream_process_alerts.js:436-468).  With the servers sharded
+// over ranks, every rank queues its candidates (flush_alerts) and the ingest thread all-gathers
+// them once per exchanged batch (a fixed-size record block per rank, behind the fleet
+// all-reduce on the same stream).  A block's header says whether the rank has sent every
+// candidate of the batches exchanged so far; once all ranks have, every rank sorts the pooled
+// candidates in the global emission order -- (interval edge, server first-batch, node-wide
+// server index, service order, LAG) -- and applies the same cooldown map, so all ranks agree and
+// each emits the al rows of its own winners.  The gather lands before the next batch's clock
+// collective returns (same in-order stream), so the decision costs no extra wait.
+void Engine::set_server_index(const std::string& server, int32_t global_index) {
+  flush();
+  const int32_t id = add_server(server);
+  server_gidx_[id] = global_index;
+}
+
+void Engine::node_take_text() {
+  std::lock_guard<std::mutex> g(node_mu_);
+  if (node_text_.empty()) return;
+  blob_[OUT_AL] += node_text_;
+  node_text_.clear();
+}
+
+void Engine::node_round(uint64_t round, bool wait) {
+  if (node_round_pending_) {
+    coll_wait(nullptr, node_ev_, "node alerts");
+    node_resolve();
+  }
+  const size_t per = sizeof(NodeHdr) + (size_t)node_cap_ * sizeof(NodeCand);
+  NodeHdr* hdr = (NodeHdr*)h_node_send_;
+  NodeCand* out = (NodeCand*)(h_node_send_ + sizeof(NodeHdr));
+  std::memset(hdr, 0, sizeof(NodeHdr));
+  {
+    std::lock_guard<std::mutex> g(node_mu_);
+    int32_t n = 0;
+    while (n < node_cap_ && !node_q_.empty() && node_q_.front().seq_batch <= round) {
+      NodePayload& p = node_q_.front();
+      out[n++] = p.c;
+      const uint32_t id = p.c.local_id;
+      node_sent_.emplace(id, std::move(p));
+      node_q_.pop_front();
+    }
+    hdr->count = n;
+    hdr->all_sent = node_q_.empty() || node_q_.front().seq_batch > round;
+  }
+  const size_t used = sizeof(NodeHdr) + (size_t)hdr->count * sizeof(NodeCand);
+  HIP_OK(hipMemcpyAsync(d_node_send_, h_node_send_, used, hipMemcpyHostToDevice, coll_stream_));
+  coll_->all_gather(d_node_send_, d_node_recv_, per, coll_stream_);
+  HIP_OK(hipMemcpyAsync(h_node_recv_, d_node_recv_, per * (size_t)fleet_nranks_, hipMemcpyDeviceToHost, coll_stream_));
+  HIP_OK(hipEventRecord(node_ev_, coll_stream_));
+  node_round_pending_ = true;
+  if (wait) {
+    coll_wait(nullptr, node_ev_, "node alerts");
+    node_resolve();
+  }
+}
+
+void Engine::node_resolve() {
+  node_round_pending_ = false;
+  const size_t per = sizeof(NodeHdr) + (size_t)node_cap_ * sizeof(NodeCand);
+  bool all = true;
+  for (int r = 0; r < fleet_nranks_; ++r) {
+    const NodeHdr* h = (const NodeHdr*)(h_node_recv_ + per * (size_t)r);
+    const NodeCand* c = (const NodeCand*)(h_node_recv_ + per * (size_t)r + sizeof(NodeHdr));
+    if (h->count < 0 || h->count > node_cap_) throw std::runtime_error("node alerts: corrupt candidate block");
+    node_pool_.insert(node_pool_.end(), c, c + h->count);
+    all = all && h->all_sent != 0;
+  }
+  node_all_sent_ = all;
+  if (!all) return;  // some rank still holds candidates of an exchanged batch: decide later
+  std::sort(node_pool_.begin(), node_pool_.end(), [](const NodeCand& a, const NodeCand& b) {
+    if (a.edge_ts != b.edge_ts) return a.edge_ts < b.edge_ts;
+    if (a.first_batch != b.first_batch) return a.first_batch < b.first_batch;
+    if (a.gidx != b.gidx) return a.gidx < b.gidx;
+    if (a.seq != b.seq) return a.seq < b.seq;
+    return a.lag_idx < b.lag_idx;
+  });
+  const int me = coll_->rank();
+  std::string text;
+  for (const NodeCand& c : node_pool_) {
+    char key[20];
+    key[0] = '\x02';  // node-wide keys (hashes) share the checkpointed cooldown map
+    for (int i = 0; i < 16; ++i) key[1 + i] = "0123456789abcdef"[(c.key >> (60 - 4 * i)) & 15];
+    const std::string k(key, 17);
+    auto it = last_alert_.find(k);
+    if (it != last_alert_.end() && !((c.now - it->second) / 1000.0 > cfg_.cooldown_ms / 1000.0)) continue;
+    last_alert_[k] = c.now;
+    if (c.rank != me) continue;
+    ++node_alerts_;
+    auto p = node_sent_.find(c.local_id);
+    if (p == node_sent_.end()) throw std::runtime_error("node alerts: lost candidate payload");
+    if (want(OUT_AL)) {
+      text += fmt::al_line(c.now, c.edge_ts, p->second.server, p->second.service, c.causes, p->second.fs);
+      text += '\n';
+    }
+  }
+  node_pool_.clear();
+  node_sent_.clear();  // everything sent so far was in this pool
+  if (!text.empty()) {
+    std::lock_guard<std::mutex> g(node_mu_);
+    node_text_ += text;
+  }
+}
+
+void Engine::node_drain() {
+  flush();
+  if (!coll_ || !node_mode_) return;
+  fleet_exchange_upto(fleet_posted_);
+  if (node_round_pending_) {
+    coll_wait(nullptr, node_ev_, "node alerts");
+    node_resolve();
+  }
+  // every rank computes the same node_all_sent_, so the extra rounds match across ranks
+  const uint64_t last = fleet_rounds_ ? fleet_rounds_ - 1 : 0;
+  while (!node_all_sent_) node_round(last, /*wait=*/true);
+  flush();  // folds the decided rows into the al stream
 }
 
 }  // namespace apm

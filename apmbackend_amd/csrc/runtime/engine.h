@@ -10,7 +10,6 @@
 // stream_process_alerts -> stream_insert_db) with the RabbitMQ hops replaced by device buffers.
 #pragma once
 #include <hip/hip_runtime.h>
-#include <rccl/rccl.h>
 
 #include <atomic>
 #include <condition_variable>
@@ -26,6 +25,7 @@
 #include <vector>
 
 #include "../apm_types.h"
+#include "collective.h"
 #include "devjoin.h"
 #include "join.h"
 
@@ -88,6 +88,9 @@ struct EngineConfig {
   // RCCL watchdog: a collective not complete after this long (a dead or wedged peer) aborts the
   // communicator and throws, so the supervisor restarts the rank group from its checkpoint
   double coll_timeout_ms = 300000;
+  // lock-step ranks resolve the per-service alert cooldown node-wide: alert candidates are
+  // all-gathered and decided in the global emission order (engine.cpp, "node-wide cooldown")
+  int node_cooldown = 1;
   // K4/K6 on the GPU (devjoin.hip); 0 = host join workers (join.cpp)
   int device_join = 1;
   int join_table_bits = 21;          // key-table slots (128 B each)
@@ -252,6 +255,15 @@ class Engine {
   // batches not yet exchanged and returns [cap][n_lags][NSTAT][3] of the newest.
   std::vector<double> fleet_merged();
   uint64_t fleet_rounds() const { return fleet_rounds_; }
+  // Same exchange over an in-process group (tests: N engines of one process share one GPU).
+  void fleet_init_local(std::shared_ptr<LocalGroup> group, int rank, int32_t n_services_cap, bool lockstep);
+  // Position of `server` in the node-wide server list (ranks own disjoint slices of it).  The
+  // node-wide alert order ranks servers by (first batch with a series, this index); default =
+  // local registration order, which is the global order on a single rank.
+  void set_server_index(const std::string& server, int32_t global_index);
+  // Collective: resolve every queued node-wide alert candidate (end of stream / before reading
+  // the al stream).  Extra exchange rounds run until every rank's queue is empty.
+  void node_drain();
 
   // Wait for the in-flight stats stage (process_batch returns while it still runs).
   void flush();
@@ -302,7 +314,11 @@ class Engine {
   void pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream, bool atomic_path = false);
   void fleet_pack_locked();
   void fleet_exchange_upto(uint64_t rounds);
-  void coll_check(ncclResult_t r, const char* what);
+  void fleet_setup(int32_t cap, bool lockstep);
+  // node-wide cooldown (ingest thread): one all-gather round per exchanged batch
+  void node_round(uint64_t upto_seq, bool wait);
+  void node_resolve();
+  void node_take_text();
   void coll_wait(hipStream_t s, hipEvent_t ev, const char* what);
   void lockstep_sync(int64_t batch_max_bucket);
   void apply_latest_locked(int64_t g, double batch_t0);
@@ -329,8 +345,7 @@ class Engine {
   hipStream_t stream_ = nullptr, comm_stream_ = nullptr, parse_stream_ = nullptr;
   // fleet exchange + lock-step clocks: ONE communicator, driven only by the ingest thread on
   // coll_stream_, so every rank issues the same collectives in the same order (engine.cpp)
-  ncclComm_t fleet_comm_ = nullptr;
-  bool comm_aborted_ = false;
+  std::unique_ptr<Collective> coll_;
   hipStream_t coll_stream_ = nullptr;
   bool lockstep_ = false;
   int64_t sync_latest_ = INT64_MIN;  // ingest thread: node-wide newest bucket so far
@@ -347,6 +362,45 @@ class Engine {
   uint64_t fleet_rounds_ = 0;  // exchanges issued (ingest thread)
   uint64_t fleet_posted_ = 0;  // batches posted since fleet_init (ingest thread)
   uint64_t fleet_packed_ = 0;  // batches packed (stats thread)
+  // ---- node-wide alert cooldown.  The stats thread queues this rank's candidates (with their
+  // al-row payload, formatted while the rollover's stats are current); the ingest thread
+  // all-gathers them once per exchanged batch and, when every rank has sent everything up to
+  // that batch, decides all pooled candidates in the global order -- identically on every rank.
+  struct NodeCand {  // wire record (64 B), same on every rank
+    int64_t edge_ts;
+    int64_t first_batch;  // batch in which the server got its first series
+    int32_t gidx;         // node-wide server index
+    uint32_t seq;         // service first-appearance order within the server
+    int32_t lag_idx;
+    uint32_t causes;
+    uint64_t key;         // cooldown key hash (service, or server + service)
+    double now;           // alert timestamp
+    int32_t rank;
+    uint32_t local_id;    // index into the owner's payload list
+    uint64_t pad;
+  };
+  struct NodeHdr { int32_t count, all_sent, pad[14]; };  // 64 B
+  struct NodePayload { uint64_t seq_batch; NodeCand c; std::string server, service, fs; };
+  bool node_mode_ = false;
+  int32_t node_cap_ = 512;                 // candidates per rank per round
+  std::mutex node_mu_;                     // node_q_ / node_text_
+  std::deque<NodePayload> node_q_;         // stats thread -> ingest thread (unsent)
+  std::unordered_map<uint32_t, NodePayload> node_sent_;  // sent, awaiting a decision (ingest)
+  uint32_t node_next_id_ = 0;
+  std::vector<NodeCand> node_pool_;        // gathered, undecided (ingest thread)
+  std::string node_text_;                  // decided al rows of this rank -> blob_[OUT_AL]
+  uint64_t node_alerts_ = 0;
+  bool node_round_pending_ = false;        // a gather is in flight (coll stream)
+  bool node_all_sent_ = true;              // every rank's last round sent everything
+  uint8_t* d_node_send_ = nullptr;
+  uint8_t* d_node_recv_ = nullptr;
+  uint8_t* h_node_send_ = nullptr;         // pinned
+  uint8_t* h_node_recv_ = nullptr;         // pinned
+  hipEvent_t node_ev_ = nullptr;
+  uint64_t stats_seq_ = 0;                 // stats thread: batch index of the job being processed
+  uint64_t stats_round_ = 0;               // stats thread: its exchange round
+  std::vector<int32_t> server_gidx_;
+  std::vector<int64_t> server_first_batch_;
   // stats thread
   struct StatsJob {
     std::vector<std::vector<TxOut>> outs;  // per shard, merged by the stats thread into txs
@@ -354,6 +408,8 @@ class Engine {
     std::vector<TxOut> txs; std::vector<std::string> text; double t0 = 0;
     int64_t sync_latest = INT64_MIN;  // lock-step: node-wide newest bucket after this batch
     bool dev = false;                 // device join: `dj` instead of outs / txs
+    uint64_t seq = 0;                 // batch index (the ingest thread's batch_no_)
+    uint64_t round = 0;               // exchange round (posts since fleet_init)
     DevJoinBatch dj;
   };
   std::vector<std::string>* cur_text_ = nullptr;  // text arenas of the job being processed
@@ -540,6 +596,10 @@ class Engine {
   AlertRec* d_alerts_ = nullptr;
   int32_t* d_n_alerts_ = nullptr;
   AlertRec* h_alerts_ = nullptr;
+  WinStat* d_alert_win_ = nullptr;  // candidate rows, compacted (apm_alert_gather)
+  ZOut* d_alert_z_ = nullptr;
+  WinStat* h_alert_win_ = nullptr;  // pinned
+  ZOut* h_alert_z_ = nullptr;       // pinned
   int32_t* h_n_alerts_ = nullptr;
   std::unordered_map<std::string, double> last_alert_;  // cooldown key -> alertTimestamp
 

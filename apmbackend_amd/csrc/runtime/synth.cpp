@@ -104,6 +104,11 @@ struct Params {
   int sub_min = 1, sub_max = 3;
   uint64_t seed = 1;
   int server_offset = 0;  // rank * servers: distinct JVM names per GPU shard
+  // planted incident: EJB services getSvc0000 .. getSvc(anomaly_services-1) run anomaly_factor
+  // times slower on every JVM from anomaly_start_ms on (the bench's alert rows)
+  int anomaly_services = 0;
+  double anomaly_factor = 1.0;
+  int64_t anomaly_start_ms = INT64_MAX;
 };
 
 class ServerGen {
@@ -175,7 +180,8 @@ class ServerGen {
     const int ejb = (int)(rng_.next() % (uint64_t)p_.ejb_services);
     char svc[32];
     snprintf(svc, sizeof(svc), "getSvc%04d", ejb);
-    const int64_t total = elapsed(base_elapsed(0xABCDEFULL + ejb));
+    int64_t total = elapsed(base_elapsed(0xABCDEFULL + ejb));
+    if (ejb < p_.anomaly_services && t0 >= p_.anomaly_start_ms) total = (int64_t)((double)total * p_.anomaly_factor);
     const int64_t t_end = t0 + total;
     const bool late = rng_.uni() < p_.late;
     const bool no_acct = rng_.uni() < p_.no_acct;
@@ -330,6 +336,8 @@ void register_synth(py::module_& m) {
         g("noise_per_tx", p.noise_per_tx); g("riskid", p.riskid); g("baf", p.baf); g("audit", p.audit);
         g("missing", p.missing); g("late", p.late); g("no_acct", p.no_acct); g("sub_min", p.sub_min);
         g("sub_max", p.sub_max); g("seed", p.seed); g("server_offset", p.server_offset);
+        g("anomaly_services", p.anomaly_services); g("anomaly_factor", p.anomaly_factor);
+        g("anomaly_start_ms", p.anomaly_start_ms);
         return new SynthGen(p);
       }))
       .def("files", &SynthGen::files)

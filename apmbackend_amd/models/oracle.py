@@ -849,13 +849,29 @@ class AlertsOracle:
             return None
         now = en.timestamp if self.clock == "entry" else self.wall()
         al = AlertEntry.make(now, en.timestamp, en.server, en.service, ",".join(causes), en.to_csv())
-        ck = en.service if self.cooldown_key == "service" else f"{en.server}\x00{en.service}"
+        return al if self.admit(al) else None
+
+    def cooldown_key_of(self, server: str, service: str) -> str:
+        return service if self.cooldown_key == "service" else f"{server}\x00{service}"
+
+    def admit(self, al: AlertEntry) -> bool:
+        """The per-service cooldown (:436-468): the first candidate in emission order wins."""
+        ac = self.cfg["streamProcessAlerts"]
+        ck = self.cooldown_key_of(al.server, al.service)
         last = self.alerts.get(ck)
-        if last is None or (now - last.alertTimestamp) / 1000 > ac["perServiceAlertCooldownInMinutes"] * 60:
+        if last is None or (al.alertTimestamp - last.alertTimestamp) / 1000 > ac["perServiceAlertCooldownInMinutes"] * 60:
             self.alerts[ck] = al
             self.alert_buffer.append(al)
-            return al
-        return None
+            return True
+        return False
+
+    def evaluate(self, en: FullStatEntry) -> Optional[AlertEntry]:
+        """The leaky counter alone: the candidate an fs row raises, before the cooldown."""
+        saved, self.admit = self.admit, (lambda al: True)
+        try:
+            return self.process(en)
+        finally:
+            self.admit = saved
 
 
 # ----------------------------------------------------------------------------- full chain
@@ -864,8 +880,23 @@ class PipelineOracle:
     """parse -> stats -> z-score -> alerts, with the queues modelled as in-order FIFOs."""
 
     def __init__(self, cfg: Dict[str, Any], tz: Optional[TzOffset] = None, alert_clock="entry",
-                 server_fn: Callable[[str], str] = None):
+                 server_fn: Callable[[str], str] = None,
+                 node_exchange: Optional[Callable[[list], list]] = None,
+                 server_index: Optional[Dict[str, int]] = None):
+        """``node_exchange`` (multi-rank, servers sharded over ranks): the cooldown is decided
+        node-wide.  Alert candidates are queued with their global emission-order key and, after
+        every batch, ``node_exchange(mine)`` returns every rank's candidates; each rank applies
+        the same cooldown in the same order and keeps its own winners (engine.cpp "node-wide
+        cooldown").  ``server_index``: node-wide server positions (the key's tie-break within
+        one batch)."""
         self.cfg = cfg
+        self.node_exchange = node_exchange
+        self.server_index = server_index or {}
+        self._batch_no = 0
+        self._first_batch: Dict[str, int] = {}
+        self._svc_seq: Dict[Tuple[str, str], int] = {}
+        self._node_q: list = []
+        self._fs_no = 0
         self.tx_db: List[str] = []
         self.audit_db: List[str] = []
         self.stats: List[str] = []
@@ -887,7 +918,11 @@ class PipelineOracle:
             self.audit_db.append(line)
         else:
             self.tx_out.append(line)
+            n = len(self.st.servers)
             self.st.consume(line)
+            if len(self.st.servers) != n:  # a server's first series: its node-wide order key
+                for srv in list(self.st.servers)[n:]:
+                    self._first_batch.setdefault(srv, self._batch_no)
 
     def _on_st(self, line):
         self.stats.append(line)
@@ -896,9 +931,29 @@ class PipelineOracle:
     def _on_fs(self, line):
         self.fs.append(line)
         en = entry_from_csv(line)
+        if self.node_exchange is not None:
+            al = self.alerts.evaluate(en)
+            if al is not None:
+                sk = (en.server, en.service)
+                if sk not in self._svc_seq:
+                    self._svc_seq[sk] = list(self.st.servers[en.server]).index(en.service)
+                self._fs_no += 1
+                key = (int(en.timestamp), self._first_batch.get(en.server, -1),
+                       self.server_index.get(en.server, 0), self._svc_seq[sk], self._fs_no)
+                self._node_q.append((key, al.to_csv()))
+            return
         al = self.alerts.process(en)
         if al is not None:
             self.al.append(al.to_csv())
+
+    def _node_resolve(self):
+        mine = set(c for _k, c in self._node_q)
+        every = self.node_exchange(self._node_q)
+        self._node_q = []
+        for _key, csv in sorted(every):
+            al = entry_from_csv(csv)
+            if self.alerts.admit(al) and csv in mine:
+                self.al.append(csv)
 
     def run_batches(self, batches: Iterable[Tuple[float, List[Tuple[str, List[str]]]]],
                     sync_latest: Optional[Callable[[int], int]] = None):
@@ -911,3 +966,6 @@ class PipelineOracle:
                     self.parse.read_line(fp, ln)
             if sync_latest is not None:
                 self.st.advance_to(sync_latest(self.st.latest))
+            if self.node_exchange is not None:
+                self._node_resolve()
+            self._batch_no += 1

@@ -16,7 +16,7 @@ LAGs -- small and latency-bound on xGMI, so one flat all_reduce per interval (no
 """
 from __future__ import annotations
 
-from typing import Optional
+from typing import Optional, Sequence
 
 import numpy as np
 
@@ -55,18 +55,33 @@ class FleetBaseline:
     """
 
     def __init__(self, engine, world: int, rank: int, max_services: Optional[int] = None, group=None,
-                 lockstep: bool = True):
-        import torch.distributed as dist
+                 lockstep: bool = True, local_group=None, servers: Optional[Sequence[str]] = None):
+        """``local_group`` (tests): a ``LocalCollGroup`` joining N engines of this process instead
+        of RCCL.  ``servers``: the node-wide server list -- each owned server's position in it
+        orders the node-wide alert decisions (default: this rank's registration order)."""
         self.eng = engine
         self.world = world
         self.n_lags = len(engine.ecfg["lags"])
         self.cap = int(max_services or engine.cfg.get("gpu", {}).get("maxServices", 1 << 16))
+        if servers is not None:
+            index = {s: i for i, s in enumerate(servers)}
+            for s in engine.eng.servers():
+                if s in index:
+                    engine.eng.set_server_index(s, index[s])
+        if local_group is not None:
+            engine.eng.fleet_init_local(local_group, rank, self.cap, lockstep)
+            return
+        import torch.distributed as dist
         native = type(engine.eng)
         obj = [(native.fleet_unique_id(), native.fleet_unique_id() if lockstep else b"") if rank == 0 else None]
         if world > 1:  # a single rank needs no rendezvous (bench.py --gpus 1 runs the same per-rank work)
             dist.broadcast_object_list(obj, src=0, group=group)
         uid, clock_uid = obj[0]
         engine.eng.fleet_init(uid, world, rank, self.cap, clock_uid)
+
+    def drain_alerts(self):
+        """Collective: decide every queued node-wide alert candidate (end of stream)."""
+        self.eng.eng.node_drain()
 
     @property
     def exchanges(self) -> int:

@@ -106,6 +106,7 @@ class IngestService:
         # ---- files -> this rank's shard
         all_files = list(files) if files is not None else discover_files(self.cfg)
         servers = sorted({self.server_of(f) for f in all_files})
+        self.all_servers = servers
         mine = set(shard_servers(servers, self.world)[self.rank]) if servers else set()
         self.my_servers = sorted(mine)
         self.files = [f for f in all_files if self.server_of(f) in mine]
@@ -182,7 +183,7 @@ class IngestService:
         self.fleet = None
         if self.world > 1 and engine == "native" and as_bool(g.get("fleetBaseline", True)):
             from ..parallel.fleet import FleetBaseline
-            self.fleet = FleetBaseline(self.eng, self.world, self.rank)
+            self.fleet = FleetBaseline(self.eng, self.world, self.rank, servers=self.all_servers)
 
         # ---- in-process JMX poller (config 4: JMX gauges fused into the per-JVM rollup)
         self.jmx = None
@@ -450,13 +451,17 @@ class IngestService:
     # ------------------------------------------------------------------ main loop
     def step(self) -> int:
         """One poll: read new complete lines from every file and run them through the engine."""
-        if self.qm is not None and any(getattr(p, "paused", False) for p in self.producers.values()):
-            return 0  # downstream backpressure: hold the tails (pause-file semantics)
-        buf, chunks = self.tailer.poll()
         # Lock-step ranks (native engine, world > 1): every process_batch runs the node-wide
         # clock all-reduce, so every rank must call it once per poll -- with an empty batch when
-        # its tails have nothing new -- or the ranks' collective sequences diverge.
+        # its tails have nothing new or downstream is paused -- or the collective sequences diverge.
         lockstep = self.fleet is not None
+        if self.qm is not None and any(getattr(p, "paused", False) for p in self.producers.values()):
+            # downstream backpressure: hold the tails (pause-file semantics)
+            if not lockstep:
+                return 0
+            buf, chunks = b"", []
+        else:
+            buf, chunks = self.tailer.poll()
         if not chunks and not lockstep:
             return 0
         self.polls += 1
@@ -500,6 +505,10 @@ class IngestService:
 
     def shutdown(self):
         log.info("shutting down")
+        if self.fleet is not None and not self._stop:
+            # coordinated end (same batch count on every rank): decide the queued node-wide
+            # alert candidates -- a collective, so not on a signal-driven (per-rank) stop
+            self.fleet.drain_alerts()
         self.native.flush()
         self._drain_outputs()
         if self.ckpt_dir and self.eng is not None:

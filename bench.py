@@ -73,6 +73,10 @@ def main():
     ap.add_argument("--no-prefetch", action="store_true", help="disable the next-batch parse overlap")
     ap.add_argument("--no-fleet", action="store_true",
                     help="skip the fleet baseline exchange / lock-step clocks (always on by default, also at N=1)")
+    ap.add_argument("--anomaly-services", type=int, default=16,
+                    help="planted incident: EJB services getSvc0000.. run --anomaly-factor x slower on every "
+                         "JVM from the first batch after the history warm-up (the bench's al rows)")
+    ap.add_argument("--anomaly-factor", type=float, default=25.0)
     ap.add_argument("--trace", default=None, help="write a Chrome trace of the pipeline stages (per rank)")
     args = ap.parse_args()
     for k, v in PRESETS[args.preset].items():  # a preset overrides the defaults it names
@@ -113,15 +117,17 @@ def main():
     sink_fd = os.open(args.sink, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
     for k in DB_OUTPUTS:
         eng.eng.set_sink_fd(k, sink_fd)
+    start = 1578391200000
+    step_ms = int(args.batch_seconds * 1000)
     gen = N.SynthGen({"servers": args.servers, "ejb_services": args.ejb, "provider_services": args.providers,
                       "tx_per_sec_per_server": args.tx_rate, "seed": 1 + rank,
-                      "server_offset": rank * args.servers})
+                      "server_offset": rank * args.servers,
+                      "anomaly_services": args.anomaly_services, "anomaly_factor": args.anomaly_factor,
+                      "anomaly_start_ms": start + 2 * step_ms})
     for path, kind, server in gen.files():
         eng.add_file(path, {0: "SOAP", 1: "SERVER", 2: "APP"}[kind], server)
 
     # ---- corpus (untimed): warmup + steps batches of `batch_seconds` of log time, pinned
-    start = 1578391200000
-    step_ms = int(args.batch_seconds * 1000)
     n_batches = args.warmup + args.steps + 2
     batches = []
     total = 0
@@ -142,7 +148,8 @@ def main():
 
     # The fleet exchange (MFMA per-service Gram pack + RCCL all-reduce) and the lock-step clock
     # collective run at every N, so each rank does the same work at N = 1 and N = 8 (weak scaling).
-    fleet = None if args.no_fleet else FleetBaseline(eng, world, rank)
+    servers_all = [f"jvm{i:03d}" for i in range(world * args.servers)]  # every rank's SynthGen names
+    fleet = None if args.no_fleet else FleetBaseline(eng, world, rank, servers=servers_all)
     if args.trace:
         eng.eng.set_trace(True)
 
@@ -168,6 +175,16 @@ def main():
     for i in range(2, 2 + args.warmup):
         step(i)
     eng.eng.flush()
+    if args.anomaly_services > 0:
+        # alert pre-history: the planted incident's series enter the timed region one bad
+        # interval short of the leaky counter's trigger (as if degraded for the whole alert
+        # window), like the z-score rings' synthetic pre-history above
+        ac = cfg["streamProcessAlerts"]
+        need = int(ac["requiredNumberBadIntervalsInAlertWindowToTrigger"]) - 1
+        hot = {f"getSvc{j:04d}" for j in range(args.anomaly_services)}
+        ser = [i for i, (_srv, svc) in enumerate(eng.eng.export_series()) if svc.split(":")[-1] in hot]
+        for li in range(len(eng.ecfg["lags"])):
+            eng.eng.import_alert_counters(li, ser, [need] * len(ser))
     torch.cuda.synchronize()
     m0 = eng.metrics()
     if dist is not None:
@@ -182,6 +199,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    if fleet is not None:
+        fleet.drain_alerts()  # untimed: decide the last batch's node-wide alert candidates
     m1 = eng.metrics()
     lines = m1["lines"] - m0["lines"]
     out_bytes = {k: eng.eng.sink_bytes(k) for k in DB_OUTPUTS}
@@ -213,8 +232,9 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (round(value / ref, 2) if ref else None),
-            "dtype": "fp64",
-            "data": "synthetic WildFly logs (native generator, seeded), random-init z-score pre-history",
+            "dtype": {"float64": "fp64", "float32": "fp32", "bfloat16": "bf16"}[args.ring],
+            "data": "synthetic WildFly logs (native generator, seeded; planted slow-service incident), "
+                    "random-init z-score and alert-counter pre-history",
             "config": {
                 "model": f"apm-pipeline parse->join->stats->zscore(LAG 360,8640)->alerts, {n_services} services, "
                          f"{args.servers} JVMs/GPU",
@@ -235,6 +255,8 @@ def main():
                                             "t_stats_tx_ms", "t_release_ms", "t_rollover_ms", "t_format_ms", "t_out_ms")},
             "corpus_gen_s": round(t_gen, 2),
             "db_insert_bytes_total": out_bytes,
+            "alerts": int(m1["alerts"] - m0["alerts"]),
+            "alert_candidates": int(m1["alert_candidates"] - m0["alert_candidates"]),
         }
         print(json.dumps(out), flush=True)
     if args.trace:

@@ -31,7 +31,12 @@ def free_port():
 
 
 def corpus():
-    an = [Anomaly("jvm01", "getSvc0001", START + 100_000, START + 500_000, 30.0)]
+    # the same services degrade on JVMs of different shards: the per-service cooldown (default
+    # 15 min) must then be decided node-wide, in the single process's emission order
+    an = [Anomaly("jvm01", "getSvc0001", START + 100_000, START + 500_000, 30.0),
+          Anomaly("jvm02", "getSvc0001", START + 100_000, START + 500_000, 30.0),
+          Anomaly("jvm03", "getSvc0002", START + 150_000, START + 500_000, 30.0),
+          Anomaly("jvm04", "getSvc0002", START + 200_000, START + 500_000, 30.0)]
     sc = SynthConfig(servers=4, duration_s=600, tx_per_sec_per_server=2, seed=21, ejb_services=3,
                      provider_services=2, anomalies=an)
     return Generator(sc).generate(), sc
@@ -42,18 +47,17 @@ def cfg():
     C["streamCalcZScore"]["defaults"] = [{"LAG": 6, "THRESHOLD": 3.0, "INFLUENCE": 0.5}]
     C["streamProcessAlerts"]["rollingAlertWindowSizeInIntervals"] = 5
     C["streamProcessAlerts"]["requiredNumberBadIntervalsInAlertWindowToTrigger"] = 2
-    C["streamProcessAlerts"]["perServiceAlertCooldownInMinutes"] = 0
     C["gpu"]["timezone"] = "UTC"
     return C
 
 
-def run_shard(lines, sc, servers, sync=None):
+def run_shard(lines, sc, servers, sync=None, node_exchange=None, server_index=None):
     """One rank's pipeline over its servers.  Batches are cut on the global timeline (all ranks
     ingest the same wall-clock slices) and the watermark clock is the global one, as the
     engine ranks see it through the lock-step exchange."""
     bl = with_watermarks(batches(lines, sc.start_ms, 5.0), UTC)
     mine = [(now, [(fp, ls) for fp, ls in chunks if fp.split("/")[2] in servers]) for now, chunks in bl]
-    P = PipelineOracle(copy.deepcopy(cfg()), UTC)
+    P = PipelineOracle(copy.deepcopy(cfg()), UTC, node_exchange=node_exchange, server_index=server_index)
     P.run_batches(mine, sync_latest=sync)
     return P
 
@@ -78,7 +82,12 @@ def _worker(rank, world, port, out_q):
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             return int(t.item())
 
-        P = run_shard(lines, sc, set(mine), sync)
+        def node_exchange(cands):  # the engine's per-batch all-gather of alert candidates
+            out = [None] * world
+            dist.all_gather_object(out, cands)
+            return [c for r in out for c in r]
+
+        P = run_shard(lines, sc, set(mine), sync, node_exchange, {s: i for i, s in enumerate(servers)})
         # fleet moments: per-series baseline means of the last fs rows -> packed per service
         svc_ids = {}
         means, ss = [], []
@@ -130,7 +139,13 @@ def test_sharded_ranks_reproduce_single_rank_per_series(world):
             for k, v in per_series(r[idx]).items():
                 got[k] += v
         assert got == per_series(full.stats if name == "st" else full.fs), name
-    assert sorted(l for r in res for l in r[4]) == sorted(full.al) and len(full.al) > 0
+    # alerts: the node-wide cooldown reproduces the single alerts process (one per service)
+    assert sorted(l for r in res for l in r[4]) == sorted(full.al) and len(full.al) >= 2
+    alerted = collections.Counter(l.split("|")[4].split(":")[-1] for l in full.al)
+    assert set(alerted) == {"getSvc0001", "getSvc0002"}
+    # ... and within the cooldown each service alerts from one JVM although two JVMs degrade
+    for svc in alerted:
+        assert len({l.split("|")[3] for l in full.al if l.split("|")[4].endswith(svc)}) == 1
     # fleet moments: the all-reduced pack equals the pack over every series at once
     all_svcs = sorted({l.split("|")[3] for l in full.fs})
     idx = {s: i for i, s in enumerate(all_svcs)}

@@ -264,11 +264,14 @@ def test_lockstep_clock_communicator_single_rank_is_transparent():
         eng.process_lines(chunks, now)
         for k in ("transactions", "st", "fs", "al"):
             out[k] += eng.take(k)
-    for k in ("transactions", "st", "fs", "al"):
-        assert out[k] == plain[k], k
     m = eng.metrics()
     assert m["lockstep_rollovers"] == 0 and eng.eng.fleet_rounds() == len(bl) - 1
-    assert len(eng.eng.fleet_merged()) > 0 and eng.eng.fleet_rounds() == len(bl)
+    # node-wide cooldown: the last batches' alert candidates are decided by the drain
+    eng.eng.node_drain()
+    out["al"] += eng.take("al")
+    for k in ("transactions", "st", "fs", "al"):
+        assert out[k] == plain[k], k
+    assert len(eng.eng.fleet_merged()) > 0 and eng.eng.fleet_rounds() >= len(bl)
 
 
 def test_server_rollup_fuses_window_stats_with_jmx_gauges():

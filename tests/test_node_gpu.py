@@ -1,0 +1,132 @@
+"""Multi-rank native engines on ONE GPU: the node's collectives (lock-step clocks, fleet moments,
+node-wide alert candidates) run over an in-process group (``LocalCollGroup``) instead of RCCL,
+so a 2- or 4-rank node is checked against the single-process reference without 2-4 GPUs.
+
+Each rank owns a shard of the JVM hosts (parallel.dist.shard_servers) and runs its own engine
+on its own host thread, exactly as the per-GPU processes of a node do.  The union of the ranks'
+st / fs streams must equal the single-stream oracle per series, and the al stream must equal the
+oracle's with the DEFAULT 15-minute per-service cooldown -- two JVMs on different ranks degrade
+on the same service, and only the first candidate in the reference's emission order may alert.
+"""
+import collections
+import copy
+import threading
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover - CPU containers
+    pytest.skip("no GPU", allow_module_level=True)
+
+from apmbackend_amd import _native  # noqa: E402
+from apmbackend_amd.models.oracle import PipelineOracle  # noqa: E402
+from apmbackend_amd.models.pipeline import APMEngine  # noqa: E402
+from apmbackend_amd.parallel.dist import shard_servers  # noqa: E402
+from apmbackend_amd.parallel.fleet import FleetBaseline  # noqa: E402
+from apmbackend_amd.utils.config import default_config  # noqa: E402
+from apmbackend_amd.utils.synth import Anomaly, Generator, SynthConfig, batches, with_watermarks  # noqa: E402
+from apmbackend_amd.utils.timeparse import TzOffset  # noqa: E402
+
+UTC = TzOffset("UTC")
+START = 1578391200000
+
+
+def node_cfg():
+    C = default_config()
+    C["streamCalcZScore"]["defaults"] = [{"LAG": 6, "THRESHOLD": 3.0, "INFLUENCE": 0.5},
+                                         {"LAG": 30, "THRESHOLD": 2.0, "INFLUENCE": 0.0}]
+    C["streamProcessAlerts"]["rollingAlertWindowSizeInIntervals"] = 5
+    C["streamProcessAlerts"]["requiredNumberBadIntervalsInAlertWindowToTrigger"] = 2
+    # perServiceAlertCooldownInMinutes: the default (15)
+    C["gpu"].update({"zscoreMeanMode": "exact", "timezone": "UTC", "maxSeries": 4096, "batchBytes": 4 << 20,
+                     "maxLinesPerBatch": 1 << 16, "bucketCellCapacity": 8, "bucketOverflowCapacity": 1 << 16})
+    return C
+
+
+def corpus():
+    an = [Anomaly("jvm01", "getSvc0001", START + 100_000, START + 900_000, 30.0),
+          Anomaly("jvm02", "getSvc0001", START + 100_000, START + 900_000, 30.0),
+          Anomaly("jvm03", "getSvc0002", START + 150_000, START + 900_000, 30.0),
+          Anomaly("jvm04", "getSvc0002", START + 200_000, START + 900_000, 30.0),
+          Anomaly("jvm02", "getSvc0003", START + 600_000, START + 900_000, 40.0)]
+    sc = SynthConfig(servers=4, duration_s=1000, tx_per_sec_per_server=3, seed=21, ejb_services=3,
+                     provider_services=2, anomalies=an)
+    lines = Generator(sc).generate()
+    return lines, with_watermarks(batches(lines, sc.start_ms, 5.0), UTC)
+
+
+def server_of(fp):
+    return fp.split("/")[2]
+
+
+def per_series(stream):
+    d = collections.defaultdict(list)
+    for l in stream:
+        f = l.split("|")
+        d[(f[2], f[3])].append(l)
+    return d
+
+
+def run_node(world, bl, servers):
+    """`world` engines, one host thread each, joined by an in-process collective group."""
+    group = _native.load().LocalCollGroup(world, 120000.0)
+    shards = shard_servers(servers, world)
+    engs, outs, errs = [], [], []
+    for r in range(world):
+        eng = APMEngine(copy.deepcopy(node_cfg()), keep_text=True)
+        # register this rank's files up front, in the global layout order
+        for _now, chunks in bl:
+            for fp, _ls in chunks:
+                if server_of(fp) in shards[r]:
+                    eng.add_file(fp)
+        engs.append(eng)
+        outs.append(collections.defaultdict(list))
+    fleets = [None] * world
+
+    def rank_main(r):
+        try:
+            fleets[r] = FleetBaseline(engs[r], world, r, max_services=64, local_group=group, servers=servers)
+            for now, chunks in bl:
+                engs[r].process_lines([(fp, ls) for fp, ls in chunks if server_of(fp) in shards[r]], now)
+                for k in ("st", "fs", "al"):
+                    outs[r][k] += engs[r].take(k)
+            fleets[r].drain_alerts()
+            for k in ("st", "fs", "al"):
+                outs[r][k] += engs[r].take(k)
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append((r, repr(e)))
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(600)
+    assert not errs, errs
+    assert all(not t.is_alive() for t in th)
+    return engs, outs
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_local_group_node_matches_single_process(world):
+    lines, bl = corpus()
+    servers = sorted({server_of(fp) for fp in lines})
+    P = PipelineOracle(copy.deepcopy(node_cfg()), UTC)
+    P.run_batches(bl)
+    engs, outs = run_node(world, bl, servers)
+    for name, want in (("st", P.stats), ("fs", P.fs)):
+        got = collections.defaultdict(list)
+        for o in outs:
+            for k, v in per_series(o[name]).items():
+                got[k] += v
+        assert got == per_series(want), name
+    al = sorted(l for o in outs for l in o["al"])
+    assert al == sorted(P.al)
+    svcs = collections.Counter(l.split("|")[4] for l in P.al)
+    assert {"S:getSvc0001", "S:getSvc0002"} <= set(svcs)
+    ms = [e.metrics() for e in engs]
+    assert sum(m["alerts"] for m in ms) == len(P.al)
+    if world > 1:
+        # candidates were raised on more ranks than alerted: the cooldown was decided node-wide
+        assert sum(m["alert_candidates"] for m in ms) > len(P.al)
