@@ -432,3 +432,42 @@ def test_interleaved_server_chunks_match_oracle():
     assert out["audit_db"] == P.audit_db
     assert out["st"] == P.stats
     assert out["fs"] == P.fs
+
+
+_HOT = {}
+
+
+def _hot_corpus():
+    """One JVM, one EJB service at 200 tx/s (+2 provider sub-services hit 1-3x per tx): the
+    service's 31-bucket window holds ~62k samples -- far past K8's LDS tile (16k), so the
+    multi-pass radix select runs -- and its buckets overflow small cells into the spill list."""
+    if "bl" not in _HOT:
+        sc = SynthConfig(servers=1, duration_s=390, tx_per_sec_per_server=200, ejb_services=1, provider_services=2,
+                         seed=5, noise_lines_per_tx=0, audit_fraction=0.0)
+        lines = Generator(sc).generate()
+        _HOT["bl"] = with_watermarks(batches(lines, sc.start_ms, 5.0), UTC)
+        C = small_cfg("exact")
+        C["gpu"]["emulateOverrideAliasing"] = False
+        C["streamCalcZScore"]["overrides"]["services"] = {}
+        P = PipelineOracle(copy.deepcopy(C), UTC)
+        P.run_batches(_HOT["bl"])
+        _HOT["P"] = P
+    return _HOT["bl"], _HOT["P"]
+
+
+@pytest.mark.parametrize("cells", [8, 64])
+def test_hot_series_and_spill_match_oracle(cells):
+    bl, P = _hot_corpus()
+    C = small_cfg("exact")
+    C["gpu"]["emulateOverrideAliasing"] = False
+    C["streamCalcZScore"]["overrides"]["services"] = {}
+    C["gpu"].update({"bucketCellCapacity": cells, "bucketOverflowCapacity": 1 << 21, "batchBytes": 16 << 20,
+                     "maxLinesPerBatch": 1 << 18})
+    eng, out = _run_engine(C, bl)
+    # the hot series really is hot: ~60k samples in its last window
+    last = [l for l in P.stats if "getSvc0000" in l][-1].split("|")
+    assert float(last[4]) * 5 > 55000  # tpm x 5 min
+    assert out["st"] == P.stats
+    assert out["fs"] == P.fs
+    m = eng.metrics()
+    assert m["spill_dropped"] == 0 and m["series_overflow_tx"] == 0
