@@ -150,6 +150,7 @@ py::dict metrics_dict(const EngineMetrics& m) {
   d["t_total_ms"] = m.t_total_ms;
   d["series_overflow_tx"] = m.series_overflow_tx;
   d["spill_dropped"] = m.spill_dropped;
+  d["nan_windows_clipped"] = m.nan_windows_clipped;
   d["rollover_latency_ms"] = m.rollover_latency_ms;
   return d;
 }

@@ -19,7 +19,14 @@ struct StatsState {
   int32_t cap;
   int32_t spill_cap;
   int32_t S;
-  unsigned long long* spill_drop = nullptr;  // samples lost to a full spill list (reported)
+  unsigned long long* spill_drop = nullptr;  // [0] samples lost to a full spill list, [1] NaN windows clipped
+  // NaN elapsed samples (stream_calc_stats.js:131 pushes parseInt -> NaN): once a series holds one,
+  // the JS binaryInsert order of every later sample in its windows matters, so the series' samples
+  // are appended in arrival order (not atomic order) while a NaN is live in its window.
+  int32_t* nan_until = nullptr;  // [S] last bucket whose window can still see a NaN sample (INT32_MIN = none)
+  int32_t* ord_list = nullptr;   // [max_tx] tx indices deferred to the ordered append
+  int32_t* ord_n = nullptr;
+  int32_t keep = 0;              // windowSz + intervalBufferSz
 };
 
 struct WindowArgs {
@@ -30,8 +37,13 @@ struct WindowArgs {
   WinStat* out;           // [S]
   int32_t* big_list;      // series deferred to the block pass
   int32_t* big_n;
+  int32_t* nan_list;      // series whose window holds a NaN sample (JS insertion emulation)
+  int32_t* nan_n;
+  int32_t* js_scratch;    // [JS_BLOCKS][js_cap] ordered window samples of a NaN series
+  int32_t js_cap;
   int32_t n_series;       // ids < n_series may be active
 };
+constexpr int JS_BLOCKS = 8;
 
 struct ZArgs {
   void* ring;              // [NSTAT][LAG][S] of T for this lag
@@ -130,6 +142,8 @@ int apm_parse_batch(const uint8_t* d_bytes, uint64_t n_bytes, const uint32_t* d_
 void apm_stats_clear_slot(apm::StatsState* st, int slot, hipStream_t stream);
 void apm_bucket_append(const apm::TxRec* d_tx, uint32_t lo, uint32_t hi, apm::StatsState* st,
                        int64_t min_live_bucket, hipStream_t stream);
+// marks series with a NaN elapsed sample in tx[0, n) (before any of the batch is appended)
+void apm_nan_mark(const apm::TxRec* d_tx, uint32_t n, apm::StatsState* st, hipStream_t stream);
 void apm_window_stats(apm::WindowArgs* a, hipStream_t stream);
 void apm_pool_append(const apm::TxRec* d_tx, uint32_t lo, uint32_t hi, const int64_t* d_gid, int64_t* tail_end,
                      int64_t* tail_gid, int64_t base, hipStream_t stream);

@@ -36,7 +36,12 @@ __global__ void k_bucket_append(const TxRec* __restrict__ tx, uint32_t lo, uint3
   if (r.series < 0 || r.series >= st.S) return;
   st.active[r.series] = 1;
   const int64_t b = r.end_ms / 10000;  // endTs string minus its last 4 digits
-  if (b < min_live_bucket || r.elapsed == ELAPSED_NAN) return;
+  if (b < min_live_bucket) return;
+  // NaN samples are kept (sentinel ELAPSED_NAN): they count toward tpm and poison the average
+  if (st.nan_until && b <= (int64_t)st.nan_until[r.series]) {
+    st.ord_list[atomicAdd(st.ord_n, 1)] = (int32_t)i;  // arrival order matters: ordered pass
+    return;
+  }
   const int slot = (int)(b % NSLOT);
   const size_t cidx = (size_t)slot * st.S + r.series;
   const int k = atomicAdd(&st.counts[cidx], 1);
@@ -50,6 +55,103 @@ __global__ void k_bucket_append(const TxRec* __restrict__ tx, uint32_t lo, uint3
     } else if (st.spill_drop) {
       atomicAdd(st.spill_drop, 1ULL);
     }
+  }
+}
+
+__global__ void k_nan_mark(const TxRec* __restrict__ tx, uint32_t n, StatsState st) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const TxRec r = tx[i];
+  if (r.elapsed != ELAPSED_NAN || r.series < 0 || r.series >= st.S) return;
+  atomicMax(&st.nan_until[r.series], (int32_t)(r.end_ms / 10000) + st.keep);
+}
+
+// Ordered append of the deferred tx (series with a live NaN): one block sorts the deferred
+// entries by (cell, tx index) in LDS, so every cell receives its samples in arrival order and
+// the spill entries of one run are reserved contiguously.  Entries are taken in tx-index ranges
+// that hold at most ORD_TILE of them (indices are unique), processed in index order.
+constexpr int ORD_TILE = 4096;
+__global__ __launch_bounds__(1024) void k_bucket_append_ordered(const TxRec* __restrict__ tx, uint32_t lo, uint32_t hi,
+                                                               StatsState st) {
+  __shared__ unsigned long long key[ORD_TILE];
+  __shared__ int32_t pos[ORD_TILE];
+  __shared__ int32_t sp0[ORD_TILE];
+  __shared__ int m_sh;
+  const int n_ord = *st.ord_n;
+  if (n_ord == 0) return;
+  const uint32_t span = hi - lo;
+  const uint32_t R = n_ord <= ORD_TILE ? span : (uint32_t)ORD_TILE;
+  for (uint32_t r0 = 0; r0 < span; r0 += R) {
+    if (threadIdx.x == 0) m_sh = 0;
+    __syncthreads();
+    for (int j = threadIdx.x; j < n_ord; j += blockDim.x) {
+      const uint32_t i = (uint32_t)st.ord_list[j];
+      if (i - lo >= r0 && i - lo < r0 + R) {
+        const TxRec r = tx[i];
+        const uint32_t cell = (uint32_t)((r.end_ms / 10000) % NSLOT) * (uint32_t)st.S + (uint32_t)r.series;
+        key[atomicAdd(&m_sh, 1)] = ((unsigned long long)cell << 32) | i;
+      }
+    }
+    __syncthreads();
+    const int m = m_sh;
+    if (m == 0) continue;  // uniform
+    int np2 = 1;
+    while (np2 < m) np2 <<= 1;
+    for (int k = m + threadIdx.x; k < np2; k += blockDim.x) key[k] = ~0ULL;
+    __syncthreads();
+    for (int k = 2; k <= np2; k <<= 1)
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = threadIdx.x; i < np2; i += blockDim.x) {
+          const int ixj = i ^ j;
+          if (ixj > i) {
+            const unsigned long long x = key[i], y = key[ixj];
+            if ((x > y) == ((i & k) == 0)) { key[i] = y; key[ixj] = x; }
+          }
+        }
+        __syncthreads();
+      }
+    // position of every entry = cell count before this range + rank inside its run
+    for (int k = threadIdx.x; k < m; k += blockDim.x) {
+      const uint32_t cell = (uint32_t)(key[k] >> 32);
+      int a = 0, b = k;  // first index of the run
+      while (a < b) { const int mid = (a + b) >> 1; if ((uint32_t)(key[mid] >> 32) < cell) a = mid + 1; else b = mid; }
+      pos[k] = st.counts[cell] + (k - a);
+    }
+    __syncthreads();
+    // run heads publish the new count and reserve the run's spill entries in one piece
+    for (int k = threadIdx.x; k < m; k += blockDim.x) {
+      const uint32_t cell = (uint32_t)(key[k] >> 32);
+      if (k > 0 && (uint32_t)(key[k - 1] >> 32) == cell) continue;
+      int a = k, b = m;  // one past the run
+      while (a < b) { const int mid = (a + b) >> 1; if ((uint32_t)(key[mid] >> 32) <= cell) a = mid + 1; else b = mid; }
+      const int base = pos[k], end = base + (a - k);
+      st.counts[cell] = end;
+      const int first_sp = max(base, st.cap);
+      sp0[k] = end > first_sp ? atomicAdd(&st.spill_n[cell / (uint32_t)st.S], end - first_sp) - first_sp : 0;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < m; k += blockDim.x) {
+      const uint32_t cell = (uint32_t)(key[k] >> 32);
+      const uint32_t i = (uint32_t)key[k];
+      const int p = pos[k];
+      const int32_t v = tx[i].elapsed;
+      if (p < st.cap) {
+        st.cells[(size_t)cell * st.cap + p] = v;
+      } else {
+        int a = 0, b = k;
+        while (a < b) { const int mid = (a + b) >> 1; if ((uint32_t)(key[mid] >> 32) < cell) a = mid + 1; else b = mid; }
+        const int slot = (int)(cell / (uint32_t)st.S);
+        const int j = sp0[a] + p;
+        if (j < st.spill_cap) {
+          st.spill_series[(size_t)slot * st.spill_cap + j] = (int32_t)(cell % (uint32_t)st.S);
+          st.spill_val[(size_t)slot * st.spill_cap + j] = v;
+        } else if (st.spill_drop) {
+          atomicAdd(st.spill_drop, 1ULL);
+        }
+      }
+    }
+    __threadfence();
+    __syncthreads();
   }
 }
 
@@ -151,9 +253,10 @@ __global__ __launch_bounds__(WS_WAVES * APM_WAVE) void k_window_stats(WindowArgs
   pre -= inl;
   long long sum = 0;
   // gather inline samples: every lane copies its own cell (contiguous CAP run)
+  int nan = 0;
   if (inl > 0) {
     const int32_t* cell = a.st.cells + ((size_t)slot * a.st.S + s) * a.st.cap;
-    for (int k = 0; k < inl; ++k) { const int32_t v = cell[k]; t[pre + k] = v; sum += v; }
+    for (int k = 0; k < inl; ++k) { const int32_t v = cell[k]; t[pre + k] = v; sum += v; nan += v == ELAPSED_NAN; }
   }
   // spilled samples: scan the spill lists of the window slots (rare)
   if (total_spill > 0) {
@@ -176,12 +279,18 @@ __global__ __launch_bounds__(WS_WAVES * APM_WAVE) void k_window_stats(WindowArgs
           const int off = __popcll(m & ((1ULL << lane) - 1ULL));
           t[w + off] = v;
           sum += v;
+          nan += v == ELAPSED_NAN;
         }
         w += __popcll(m);
       }
     }
   }
   for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+  for (int o = 32; o > 0; o >>= 1) nan += __shfl_xor(nan, o, 64);
+  if (nan > 0) {  // NaN in the window: JS insertion order decides the percentiles
+    if (lane == 0) a.nan_list[atomicAdd(a.nan_n, 1)] = s;
+    return;
+  }
   // pad to a power of two and sort
   int np2 = 64;
   while (np2 < n) np2 <<= 1;
@@ -270,13 +379,14 @@ __device__ void window_select(const WindowArgs& a, int s, int n, long long sum, 
 __global__ __launch_bounds__(1024) void k_window_stats_big(WindowArgs a) {
   __shared__ int32_t t[BIG_TILE];
   __shared__ long long red[16];
-  __shared__ int wpos;
+  __shared__ int wpos, wnan;
   const int nb = *a.big_n;
   for (int bi = blockIdx.x; bi < nb; bi += gridDim.x) {
     const int s = a.big_list[bi];
-    if (threadIdx.x == 0) wpos = 0;
+    if (threadIdx.x == 0) { wpos = 0; wnan = 0; }
     __syncthreads();
     long long sum = 0;
+    int nan = 0;
     for (int r = 0; r < a.n_win; ++r) {
       const int sl = a.win_slots[r];
       if (sl < 0) continue;
@@ -288,6 +398,7 @@ __global__ __launch_bounds__(1024) void k_window_stats_big(WindowArgs a) {
         const int p = atomicAdd(&wpos, 1);
         if (p < BIG_TILE) t[p] = v;
         sum += v;
+        nan += v == ELAPSED_NAN;
       }
       if (cnt > inl) {
         const int ns = min(a.st.spill_n[sl], a.st.spill_cap);
@@ -297,14 +408,21 @@ __global__ __launch_bounds__(1024) void k_window_stats_big(WindowArgs a) {
             const int p = atomicAdd(&wpos, 1);
             if (p < BIG_TILE) t[p] = v;
             sum += v;
+            nan += v == ELAPSED_NAN;
           }
         }
       }
     }
     for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sum;
+    if (nan) atomicAdd(&wnan, nan);
     __syncthreads();
     const int n_all = wpos;
+    if (wnan > 0) {  // uniform: NaN windows go to the JS insertion emulation
+      if (threadIdx.x == 0) a.nan_list[atomicAdd(a.nan_n, 1)] = s;
+      __syncthreads();
+      continue;
+    }
     if (n_all > BIG_TILE) {
       // hotter than the LDS tile: the four order statistics the reference percentile formula
       // reads are selected exactly by a 4-pass radix select over the window's samples
@@ -341,6 +459,139 @@ __global__ __launch_bounds__(1024) void k_window_stats_big(WindowArgs a) {
   }
 }
 
+// Windows holding a NaN sample: windowSortedElapTimes is built by binaryConcat'ing the window
+// buckets in key order (stream_calc_stats.js:172-178); NaN compares 'equal' to everything in the
+// binary search (util_methods.js:57-95), so the array stops being sorted and the percentile
+// ranks read whatever the insertion order put there.  One block per series replays it exactly:
+// samples gathered bucket by bucket in arrival order (inline cell, then the series' spill
+// entries), the prefix before the first NaN sorted (any order of it yields the same sorted
+// array), the rest inserted one by one with a block-parallel tail shift.  Rare by construction.
+__device__ __forceinline__ double js_elem(int32_t v) { return v == ELAPSED_NAN ? apm_nan() : (double)v; }
+
+__global__ __launch_bounds__(1024) void k_window_stats_js(WindowArgs a) {
+  __shared__ int32_t lds[BIG_TILE];
+  __shared__ int wsum[16], wpos, ins_at, first_nan;
+  const int nn = *a.nan_n;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int32_t* const gbuf = a.js_scratch + (size_t)blockIdx.x * a.js_cap;
+  for (int bi = blockIdx.x; bi < nn; bi += gridDim.x) {
+    const int s = a.nan_list[bi];
+    if (threadIdx.x == 0) { wpos = 0; first_nan = INT32_MAX; }
+    __syncthreads();
+    for (int r = 0; r < a.n_win; ++r) {
+      const int sl = a.win_slots[r];
+      if (sl < 0) continue;
+      const int cnt = a.st.counts[(size_t)sl * a.st.S + s];
+      const int inl = min(cnt, a.st.cap);
+      const int base = wpos;
+      const int32_t* cell = a.st.cells + ((size_t)sl * a.st.S + s) * a.st.cap;
+      for (int k = threadIdx.x; k < inl; k += blockDim.x)
+        if (base + k < a.js_cap) gbuf[base + k] = cell[k];
+      __syncthreads();
+      if (threadIdx.x == 0) wpos = base + inl;
+      __syncthreads();
+      if (cnt > inl) {  // the series' spill entries in list order (ordered block compaction)
+        const int ns = min(a.st.spill_n[sl], a.st.spill_cap);
+        for (int j0 = 0; j0 < ns; j0 += blockDim.x) {
+          const int j = j0 + threadIdx.x;
+          const bool hit = j < ns && a.st.spill_series[(size_t)sl * a.st.spill_cap + j] == s;
+          const unsigned long long m = __ballot(hit);
+          if (lane == 0) wsum[wv] = __popcll(m);
+          __syncthreads();
+          int before = wpos;
+          for (int w = 0; w < wv; ++w) before += wsum[w];
+          if (hit) {
+            const int p = before + __popcll(m & ((1ULL << lane) - 1ULL));
+            if (p < a.js_cap) gbuf[p] = a.st.spill_val[(size_t)sl * a.st.spill_cap + j];
+          }
+          __syncthreads();
+          if (threadIdx.x == 0) { int t = 0; for (int w = 0; w < 16; ++w) t += wsum[w]; wpos += t; }
+          __syncthreads();
+        }
+      }
+    }
+    const int n_all = wpos;
+    const int n = min(n_all, a.js_cap);
+    if (n_all > a.js_cap && threadIdx.x == 0 && a.st.spill_drop) atomicAdd(a.st.spill_drop + 1, 1ULL);
+    int32_t* buf = n <= BIG_TILE ? lds : gbuf;
+    if (buf == lds)
+      for (int k = threadIdx.x; k < n; k += blockDim.x) lds[k] = gbuf[k];
+    __syncthreads();
+    for (int k = threadIdx.x; k < n; k += blockDim.x)
+      if (buf[k] == ELAPSED_NAN) atomicMin(&first_nan, k);
+    __syncthreads();
+    const int f = min(first_nan, n);
+    // sorted prefix (bitonic in LDS when it fits, else insertion below covers it too)
+    int done = 0;
+    if (buf == lds && f > 1) {
+      int np2 = 1;
+      while (np2 < f) np2 <<= 1;
+      if (np2 <= BIG_TILE) {
+        // pad with +inf past f: the tail [f, n) is parked in gbuf and copied back after the sort
+        for (int k = f + threadIdx.x; k < np2; k += blockDim.x) lds[k] = 0x7fffffff;
+        __syncthreads();
+        for (int k = 2; k <= np2; k <<= 1)
+          for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < np2; i += blockDim.x) {
+              const int ixj = i ^ j;
+              if (ixj > i) {
+                const int32_t x = lds[i], y = lds[ixj];
+                if ((x > y) == ((i & k) == 0)) { lds[i] = y; lds[ixj] = x; }
+              }
+            }
+            __syncthreads();
+          }
+        for (int k = f + threadIdx.x; k < n; k += blockDim.x) lds[k] = gbuf[k];
+        __syncthreads();
+        done = f;
+      }
+    }
+    if (done == 0) done = min(n, 1);
+    for (int k = done; k < n; ++k) {
+      const int32_t v = buf[k];
+      if (threadIdx.x == 0) {
+        int lo = 0, hi = k - 1, at = -1;
+        const bool vn = v == ELAPSED_NAN;
+        while (lo <= hi) {
+          const int m = (lo + hi) >> 1;
+          const int32_t x = buf[m];
+          if (!vn && x != ELAPSED_NAN && x < v) lo = m + 1;
+          else if (!vn && x != ELAPSED_NAN && x > v) hi = m - 1;
+          else { at = m; break; }
+        }
+        ins_at = at >= 0 ? at : lo;
+      }
+      __syncthreads();
+      const int at = ins_at;
+      // shift buf[at, k) right by one, last chunk first
+      for (int c = k - 1; c >= at; c -= (int)blockDim.x) {
+        const int idx = c - (int)threadIdx.x;
+        int32_t x = 0;
+        if (idx >= at) x = buf[idx];
+        __syncthreads();
+        if (idx >= at) buf[idx + 1] = x;
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) buf[at] = v;
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      WinStat w;
+      w.n = n_all;
+      w.active = 1;
+      w.tpm = js_round_fixed((double)n_all / a.tpm_div, 2);
+      w.avg = apm_nan();  // the NaN poisons windowRtTotalSum
+      int lo, hi;
+      percentile_ranks(n, 75, lo, hi);
+      w.p75 = js_round_fixed(lo == hi ? js_elem(buf[lo]) : (js_elem(buf[lo]) + js_elem(buf[hi])) / 2.0, 1);
+      percentile_ranks(n, 95, lo, hi);
+      w.p95 = js_round_fixed(lo == hi ? js_elem(buf[lo]) : (js_elem(buf[lo]) + js_elem(buf[hi])) / 2.0, 1);
+      a.out[s] = w;
+    }
+    __syncthreads();
+  }
+}
+
 // --------------------------------------------------------------------------------- K9
 // The pending pool is kept sorted by (endTs, arrival gid).  New tx are appended to an unsorted
 // tail; at a rollover the tail is radix-sorted (stable, so arrival order breaks endTs ties),
@@ -368,16 +619,25 @@ void apm_stats_clear_slot(StatsState* st, int slot, hipStream_t stream) {
 void apm_bucket_append(const TxRec* d_tx, uint32_t lo, uint32_t hi, StatsState* st, int64_t min_live_bucket,
                        hipStream_t stream) {
   if (hi <= lo) return;
+  if (st->ord_n) HIP_OK(hipMemsetAsync(st->ord_n, 0, 4, stream));
   hipLaunchKernelGGL(k_bucket_append, dim3((hi - lo + 255) / 256), dim3(256), 0, stream, d_tx, lo, hi, *st,
                      min_live_bucket);
+  if (st->ord_n) hipLaunchKernelGGL(k_bucket_append_ordered, dim3(1), dim3(1024), 0, stream, d_tx, lo, hi, *st);
+}
+
+void apm_nan_mark(const TxRec* d_tx, uint32_t n, StatsState* st, hipStream_t stream) {
+  if (n == 0 || !st->nan_until) return;
+  hipLaunchKernelGGL(k_nan_mark, dim3((n + 255) / 256), dim3(256), 0, stream, d_tx, n, *st);
 }
 
 void apm_window_stats(WindowArgs* a, hipStream_t stream) {
   HIP_OK(hipMemsetAsync(a->big_n, 0, 4, stream));
+  HIP_OK(hipMemsetAsync(a->nan_n, 0, 4, stream));
   const int blocks = (a->n_series + WS_WAVES - 1) / WS_WAVES;
   if (blocks == 0) return;
   hipLaunchKernelGGL(k_window_stats, dim3(blocks), dim3(WS_WAVES * APM_WAVE), 0, stream, *a);
   hipLaunchKernelGGL(k_window_stats_big, dim3(64), dim3(1024), 0, stream, *a);
+  hipLaunchKernelGGL(k_window_stats_js, dim3(JS_BLOCKS), dim3(1024), 0, stream, *a);
 }
 
 void apm_pool_append(const TxRec* d_tx, uint32_t lo, uint32_t hi, const int64_t* d_gid, int64_t* tail_end,

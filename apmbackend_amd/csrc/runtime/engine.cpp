@@ -296,6 +296,13 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   d_win_ = (WinStat*)dmalloc((size_t)S * sizeof(WinStat));
   d_big_list_ = (int32_t*)dmalloc((size_t)S * 4);
   d_big_n_ = (int32_t*)dmalloc(4);
+  d_nan_until_ = (int32_t*)dmalloc((size_t)S * 4);
+  HIP_OK(hipMemset(d_nan_until_, 0x80, (size_t)S * 4));  // 0x80808080: far below any bucket
+  d_ord_list_ = (int32_t*)dmalloc((size_t)std::max<int64_t>(cfg_.max_tx_per_batch, cfg_.max_lines) * 4);
+  d_ord_n_ = (int32_t*)dmalloc(4);
+  d_nan_list_ = (int32_t*)dmalloc((size_t)S * 4);
+  d_nan_n_ = (int32_t*)dmalloc(4);
+  d_js_scratch_ = (int32_t*)dmalloc((size_t)JS_BLOCKS * kJsCap * 4);
   for (int i = 0; i < NSLOT; ++i) slot_bucket_[i] = NO_BUCKET;
   // z-score
   for (int l = 0; l < cfg_.n_lags; ++l) {
@@ -1166,14 +1173,15 @@ void Engine::flush() {
     node_alerts_ = 0;
   }
   {
-    unsigned long long u[2] = {0, 0};
+    unsigned long long u[3] = {0, 0, 0};
     int32_t fb = 0;
     if (dev()) HIP_OK(hipMemcpyAsync(&u[0], d_unmapped_, 8, hipMemcpyDeviceToHost, stream_));
-    HIP_OK(hipMemcpyAsync(&u[1], d_spill_drop_, 8, hipMemcpyDeviceToHost, stream_));
+    HIP_OK(hipMemcpyAsync(&u[1], d_spill_drop_, 16, hipMemcpyDeviceToHost, stream_));
     HIP_OK(hipMemcpyAsync(&fb, d_fmt_fallback_, 4, hipMemcpyDeviceToHost, stream_));
     HIP_OK(hipStreamSynchronize(stream_));
     metrics_.series_overflow_tx = u[0];
     metrics_.spill_dropped = u[1];
+    metrics_.nan_windows_clipped = u[2];
     metrics_.format_fallbacks = (uint64_t)fb;
   }
 }
@@ -1283,12 +1291,21 @@ void Engine::release_gather(int k, int64_t released) {
   drain_kind(OUT_DB);
 }
 
+StatsState Engine::stats_state() const {
+  StatsState st{d_counts_cells_, d_cells_, d_spill_n_, d_spill_series_, d_spill_val_, d_active_,
+                cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series, d_spill_drop_};
+  st.nan_until = d_nan_until_;
+  st.ord_list = d_ord_list_;
+  st.ord_n = d_ord_n_;
+  st.keep = (int32_t)(cfg_.window + cfg_.buffer);
+  return st;
+}
+
 void Engine::ensure_bucket_slot(int64_t b) {
   const int slot = (int)(((b % NSLOT) + NSLOT) % NSLOT);
   if (slot_bucket_[slot] == b) return;
   if (slot_bucket_[slot] != NO_BUCKET) {
-    StatsState st{d_counts_cells_, d_cells_, d_spill_n_, d_spill_series_, d_spill_val_, d_active_,
-                  cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series, d_spill_drop_};
+    StatsState st = stats_state();
     apm_stats_clear_slot(&st, slot, stream_);
   }
   slot_bucket_[slot] = b;
@@ -1378,8 +1395,8 @@ void Engine::stats_for_batch(std::vector<TxOut>& txs, double batch_t0) {
   if (n == 0) return;
   HIP_OK(hipMemcpyAsync(d_tx_, h_tx_, (size_t)n * sizeof(TxRec), hipMemcpyHostToDevice, stream_));
   HIP_OK(hipMemcpyAsync(d_gid_, h_gid_, (size_t)n * 8, hipMemcpyHostToDevice, stream_));
-  StatsState st{d_counts_cells_, d_cells_, d_spill_n_, d_spill_series_, d_spill_val_, d_active_,
-                cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series, d_spill_drop_};
+  StatsState st = stats_state();
+  apm_nan_mark(d_tx_, n, &st, stream_);
   const int64_t keep_iv = cfg_.window + cfg_.buffer;
   auto append = [&](uint32_t lo, uint32_t hi, int64_t lat) {
     if (hi <= lo) return;
@@ -1450,8 +1467,8 @@ void Engine::stats_for_batch_dev(DevJoinBatch& b, double batch_t0) {
     if (c.second > latest_) { triggers.push_back(c); latest_ = c.second; }
   metrics_.t_stats_tx_ms += now_ms() - ts0;
   trace_event("tx loop", ts0, now_ms(), 1);
-  StatsState st{d_counts_cells_, d_cells_, d_spill_n_, d_spill_series_, d_spill_val_, d_active_,
-                cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series, d_spill_drop_};
+  StatsState st = stats_state();
+  apm_nan_mark(b.d_tx, b.n_stats, &st, stream_);
   const int64_t keep_iv = cfg_.window + cfg_.buffer;
   auto append = [&](uint32_t lo, uint32_t hi, int64_t lat) {
     if (hi <= lo) return;
@@ -1525,8 +1542,7 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   // removeOldBuckets(36): drop every bucket < L - 36
   for (int i = 0; i < NSLOT; ++i) {
     if (slot_bucket_[i] != NO_BUCKET && slot_bucket_[i] < L - keep_iv) {
-      StatsState st{d_counts_cells_, d_cells_, d_spill_n_, d_spill_series_, d_spill_val_, d_active_,
-                    cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series, d_spill_drop_};
+      StatsState st = stats_state();
       apm_stats_clear_slot(&st, i, stream_);
       slot_bucket_[i] = NO_BUCKET;
     }
@@ -1604,8 +1620,7 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   }
   // ---- K8 window statistics over buckets [L-36, L-6]
   WindowArgs wa;
-  wa.st = StatsState{d_counts_cells_, d_cells_, d_spill_n_, d_spill_series_, d_spill_val_, d_active_,
-                     cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series, d_spill_drop_};
+  wa.st = stats_state();
   wa.n_win = (int32_t)(keep_iv - cfg_.buffer + 1);
   for (int r = 0; r < 32; ++r) wa.win_slots[r] = -1;
   for (int r = 0; r < wa.n_win && r < 32; ++r) {
@@ -1617,6 +1632,10 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   wa.out = d_win_;
   wa.big_list = d_big_list_;
   wa.big_n = d_big_n_;
+  wa.nan_list = d_nan_list_;
+  wa.nan_n = d_nan_n_;
+  wa.js_scratch = d_js_scratch_;
+  wa.js_cap = kJsCap;
   wa.n_series = n_series_;
   apm_window_stats(&wa, stream_);
   // ---- K10 z-score per LAG, K11 alert eval

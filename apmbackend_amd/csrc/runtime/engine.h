@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "../apm_types.h"
+#include "../kernels/kernel_api.h"
 #include "collective.h"
 #include "devjoin.h"
 #include "join.h"
@@ -142,6 +143,7 @@ struct EngineMetrics {
   uint64_t formatted_bytes = 0, format_fallbacks = 0, lockstep_rollovers = 0;
   uint64_t series_overflow_tx = 0;  // tx whose series could not be created (gpu.maxSeries full)
   uint64_t spill_dropped = 0;       // samples lost to a full bucket spill list (gpu.bucketOverflowCapacity)
+  uint64_t nan_windows_clipped = 0; // NaN windows larger than the JS-emulation scratch (percentiles clipped)
   double t_parse_ms = 0, t_join_ms = 0, t_stats_ms = 0, t_total_ms = 0;
   double t_join_shards_ms = 0, t_merge_ms = 0;                 // split of t_join_ms
   double t_shard_busy_ms = 0, t_shard_max_ms = 0;              // per batch: mean / max of one shard's join
@@ -561,6 +563,14 @@ class Engine {
   WinStat* d_win_ = nullptr;
   int32_t* d_big_list_ = nullptr;
   int32_t* d_big_n_ = nullptr;
+  int32_t* d_nan_until_ = nullptr;   // [S] NaN-live horizon per series (ordered K7 append)
+  int32_t* d_ord_list_ = nullptr;
+  int32_t* d_ord_n_ = nullptr;
+  int32_t* d_nan_list_ = nullptr;    // K8 series whose window holds a NaN sample
+  int32_t* d_nan_n_ = nullptr;
+  int32_t* d_js_scratch_ = nullptr;  // [JS_BLOCKS][kJsCap]
+  static constexpr int32_t kJsCap = 1 << 18;
+  StatsState stats_state() const;
 
   // z-score state per lag
   struct LagState {

@@ -76,6 +76,39 @@ def true_stddev(values: Iterable) -> Optional[float]:
     return math.sqrt(var) if var != 0 else None
 
 
+def js_binary_insert(arr: List[float], v: float) -> None:
+    """Array.prototype.binaryInsert(v, duplicate=true) (util_methods.js:57-95) with the default
+    comparator.  NaN compares 'equal' to everything, so once a NaN is in the array the result
+    is no longer sorted and depends on the insertion order -- reproduced exactly here."""
+    lo, hi = 0, len(arr) - 1
+    while lo <= hi:
+        m = (lo + hi) >> 1
+        a = arr[m]
+        if a < v:
+            lo = m + 1
+        elif a > v:
+            hi = m - 1
+        else:  # equal, or either side NaN
+            arr.insert(m, v)
+            return
+    arr.insert(lo, v)
+
+
+def js_window_array(bucket_arrays) -> List[float]:
+    """windowSortedElapTimes of generateAllStatsToQueue (stream_calc_stats.js:172-178): the
+    window buckets binaryConcat'ed in key order.  Without NaN this is just the sorted union."""
+    out: List[float] = []
+    if not any(v != v for arr in bucket_arrays for v in arr):
+        for arr in bucket_arrays:
+            out.extend(arr)
+        out.sort()
+        return out
+    for arr in bucket_arrays:
+        for v in arr:
+            js_binary_insert(out, v)
+    return out
+
+
 def calc_percentile(arr: List[float], percentile: float):
     """Array.prototype.calcPercentile (util_methods.js:112-142) on a sorted array."""
     n = len(arr)
@@ -678,18 +711,20 @@ class StatsOracle:
             self.emit_db(tx.to_csv())
         for server, srv in self.servers.items():
             for service, svc in srv.items():
-                vals: List[int] = []
+                win: List[List[int]] = []
                 cnt = 0
                 total = 0
-                for b, arr in svc.items():
+                # bucket keys are integer-like, so Object.entries visits them ascending
+                for b in sorted(svc):
+                    arr = svc[b]
                     if self.latest - self.keep <= b <= self.latest - self.buffer:
                         cnt += len(arr)
                         for v in arr:
                             total += v
-                        vals.extend(arr)
+                        win.append(arr)
                 avg = p75 = p95 = None
                 if cnt != 0:
-                    vals.sort()
+                    vals = js_window_array(win)
                     avg = total / cnt
                     p75 = calc_percentile(vals, 75)
                     p95 = calc_percentile(vals, 95)

@@ -471,3 +471,35 @@ def test_hot_series_and_spill_match_oracle(cells):
     assert out["fs"] == P.fs
     m = eng.metrics()
     assert m["spill_dropped"] == 0 and m["series_overflow_tx"] == 0
+
+
+def _nan_corpus(rate=0.03, seed=1):
+    """synth corpus with some CommonTiming::Stop lines carrying a non-numeric elapsed: the tx is
+    still emitted, its elapsed parses to NaN (stream_calc_stats.js:131)."""
+    import random
+    rng = random.Random(seed)
+    lines, _ = synth_batches(seed)
+    out = {}
+    for fp, rows in lines.items():
+        out[fp] = [(a, b, ln.replace(" - total time ", " - total time x", 1)
+                    if "CommonTiming::Stop:" in ln and rng.random() < rate else ln) for a, b, ln in rows]
+    return with_watermarks(batches(out, START, 5.0), UTC)
+
+
+def test_nan_elapsed_matches_oracle():
+    """NaN elapsed samples: counted in tpm, average undefined, and the p75/p95 of every window
+    holding one read the JS binaryInsert order (device: ordered K7 append while a NaN is live,
+    K8 JS-insertion replay)."""
+    bl = _nan_corpus()
+    C = small_cfg("exact")
+    P = PipelineOracle(copy.deepcopy(C), UTC)
+    P.run_batches(bl)
+    nan_st = [l for l in P.stats if l.split("|")[5] == "undefined" and l.split("|")[4] != "0.00"]
+    assert len(nan_st) > 20
+    eng, out = _run_engine(C, bl)
+    assert out["transactions"] == P.tx_out
+    assert out["st"] == P.stats
+    assert out["fs"] == P.fs
+    assert out["al"] == P.al
+    m = eng.metrics()
+    assert m["nan_windows_clipped"] == 0

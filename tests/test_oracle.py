@@ -177,3 +177,31 @@ def test_util_methods_match_reference_js():
     for l, v in zip(lists, res["stddev"]):
         mine = js_stddev(l)
         assert (mine is None and v is None) or mine == v
+
+
+@requires_reference
+def test_stats_nan_elapsed_matches_reference_js():
+    """A tx whose elapsed is not a number (e.g. a CT exit line carrying 'time') is pushed as
+    parseInt -> NaN: it counts toward tpm, poisons the average and lands wherever the JS
+    binaryInsert's NaN comparisons put it, so later percentiles depend on arrival order
+    (stream_calc_stats.js:131,172-184, util_methods.js:57-106)."""
+    import random
+    import refjs
+    _, bl = _synth(2, duration=900)
+    P = PipelineOracle(default_config(), UTC)
+    P.run_batches(bl)
+    rng = random.Random(11)
+    lines = []
+    for ln in P.tx_out:
+        f = ln.split("|")
+        if f[0] == "tx" and rng.random() < 0.02:
+            f[7] = rng.choice(["time", "NaN", "", "abc"])
+        lines.append("|".join(f))
+    js = refjs.stats(lines)
+    out_st, out_db = [], []
+    so = StatsOracle(out_st.append, out_db.append)
+    for ln in lines:
+        so.consume(ln)
+    assert any(l.split("|")[5] == "undefined" and l.split("|")[4] != "0.00" for l in js["st"])
+    assert js["st"] == out_st
+    assert js["db"] == out_db
