@@ -288,7 +288,26 @@ PYBIND11_MODULE(_apm_native, m) {
            py::arg("next_chunks") = std::vector<std::tuple<int32_t, uint64_t, uint64_t>>())
       .def("take", &Engine::take, py::call_guard<py::gil_scoped_release>())
       .def("flush", &Engine::flush, py::call_guard<py::gil_scoped_release>())
-      .def("save_state", &Engine::save_state, py::call_guard<py::gil_scoped_release>())
+      .def("save_state", [](Engine& e, const std::string& path, py::bytes extra) {
+             std::string x = extra;
+             py::gil_scoped_release rel;
+             return e.save_state(path, x);
+           }, py::arg("path"), py::arg("extra") = py::bytes(""))
+      .def("checkpoint_async", [](Engine& e, const std::string& prefix, py::bytes extra, bool force_base) {
+             std::string x = extra;
+             py::gil_scoped_release rel;
+             return e.checkpoint_async(prefix, x, force_base);
+           }, py::arg("prefix"), py::arg("extra") = py::bytes(""), py::arg("force_base") = false)
+      .def("checkpoint_wait", &Engine::checkpoint_wait, py::call_guard<py::gil_scoped_release>())
+      .def("checkpoint_info", [](Engine& e) {
+        const CheckpointInfo c = e.checkpoint_info();
+        py::dict d;
+        d["busy"] = c.busy; d["done"] = c.done; d["skipped"] = c.skipped; d["sync_fallbacks"] = c.sync_fallbacks;
+        d["chain_len"] = c.chain_len; d["last_base"] = c.last_base; d["last_stall_ms"] = c.last_stall_ms;
+        d["last_write_ms"] = c.last_write_ms; d["last_bytes"] = c.last_bytes; d["stage_bytes"] = c.stage_bytes;
+        d["last_ring_rows"] = c.last_ring_rows;
+        return d;
+      })
       .def("export_series", &Engine::export_series, py::call_guard<py::gil_scoped_release>())
       .def("import_series", &Engine::import_series, py::call_guard<py::gil_scoped_release>())
       .def("export_buckets", [](Engine& e) {
@@ -329,7 +348,11 @@ PYBIND11_MODULE(_apm_native, m) {
       })
       .def("set_server_context", &Engine::set_server_context, py::arg("server"), py::arg("ts_ms"),
            py::arg("gauges"), py::arg("host_load") = 0.0)
-      .def("load_state", &Engine::load_state, py::call_guard<py::gil_scoped_release>())
+      .def("load_state", [](Engine& e, const std::string& path) {
+             std::string x;
+             { py::gil_scoped_release rel; x = e.load_state(path); }
+             return py::bytes(x);
+           })
       .def("take_bytes", [](Engine& e, const std::string& k) {
         std::string b;
         { py::gil_scoped_release rel; b = e.take_bytes(k); }

@@ -11,6 +11,7 @@
 #include <cerrno>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <stdexcept>
@@ -20,7 +21,9 @@
 
 namespace apm {
 
-constexpr uint32_t kCkptVersion = 4;  // 3: join section carries the join mode (host / GPU); 4: node-wide server order
+// 3: join section carries the join mode (host / GPU); 4: node-wide server order; 5: rings in their own
+// trailing section (full or dirty rows, for incremental checkpoints) + NaN horizons + an opaque extra
+constexpr uint32_t kCkptVersion = 5;
 
 class BinWriter {
  public:
@@ -31,8 +34,28 @@ class BinWriter {
     raw("APMCKPT", 8);
     pod(kCkptVersion);
   }
+  // In-memory writer (no header): sections serialised into a malloc'd buffer (open_memstream),
+  // later spliced into a file by the asynchronous checkpoint writer.
+  struct Memory {};
+  explicit BinWriter(Memory) {
+    f_ = open_memstream(&mem_buf_, &mem_len_);
+    if (!f_) throw std::runtime_error("checkpoint: open_memstream failed");
+  }
+  std::string take_memory() {
+    std::fflush(f_);
+    std::fclose(f_);
+    f_ = nullptr;
+    std::string out(mem_buf_, mem_len_);
+    std::free(mem_buf_);
+    mem_buf_ = nullptr;
+    return out;
+  }
   ~BinWriter() {
-    if (f_) { std::fclose(f_); std::remove(tmp_.c_str()); }
+    if (f_) {
+      std::fclose(f_);
+      if (!tmp_.empty()) std::remove(tmp_.c_str());
+    }
+    std::free(mem_buf_);
   }
   void raw(const void* p, size_t n) {
     if (n && std::fwrite(p, 1, n, f_) != n) throw std::runtime_error("checkpoint: write failed");
@@ -85,6 +108,8 @@ class BinWriter {
   FILE* f_ = nullptr;
   long sec_pos_ = 0;
   uint64_t bytes_ = 0;
+  char* mem_buf_ = nullptr;
+  size_t mem_len_ = 0;
 };
 
 class BinReader {
@@ -138,6 +163,16 @@ class BinReader {
     pod<uint64_t>();
   }
   void end() {}
+  // Skips whole sections until `tag` (its header consumed), for readers that want one part.
+  void skip_to(uint32_t tag) {
+    for (;;) {
+      const uint32_t t = pod<uint32_t>();
+      if (t == 0xE0Fu) throw std::runtime_error("checkpoint: section " + std::to_string(tag) + " not found");
+      const uint64_t len = pod<uint64_t>();
+      if (t == tag) return;
+      if (std::fseek(f_, (long)len, SEEK_CUR) != 0) throw std::runtime_error("checkpoint: seek failed");
+    }
+  }
   void finish() {
     if (pod<uint32_t>() != 0xE0Fu) throw std::runtime_error("checkpoint: missing end marker");
   }

@@ -15,8 +15,13 @@
 // tailer (Python service writes them next to this file).
 #include <hip/hip_runtime.h>
 
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <chrono>
 #include <cstring>
+#include <memory>
 
 #include "../kernels/devjoin_api.h"
 #include "binio.h"
@@ -28,7 +33,7 @@ namespace {
 
 enum : uint32_t {
   SEC_CONFIG = 1, SEC_TOPOLOGY, SEC_SERIES, SEC_CLOCK, SEC_JOIN, SEC_PARSE, SEC_BUCKETS, SEC_ZSCORE, SEC_POOL,
-  SEC_ALERTS, SEC_OUTPUTS, SEC_METRICS
+  SEC_ALERTS, SEC_OUTPUTS, SEC_METRICS, SEC_RING, SEC_EXTRA
 };
 
 struct SeriesRec { int32_t server, service; uint64_t emit_key; };
@@ -36,6 +41,10 @@ struct I64Pair { int64_t a, b; };
 
 // 2-D device <-> file copies of `rows` rows of `width` bytes taken from a pitched device array.
 constexpr size_t kBounce = 64u << 20;
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 void d2h_rows(BinWriter& w, const void* dev, size_t pitch, size_t width, size_t rows, void* bounce,
               hipStream_t st) {
@@ -224,17 +233,47 @@ void JoinShard::load(BinReader& rd) {
 
 // ------------------------------------------------------------------------------ Engine
 
-uint64_t Engine::save_state(const std::string& path) {
+void Engine::checkpoint_quiesce(const char* what) {
   flush();
-  if (prefetched_) throw std::runtime_error("save_state: a prefetched batch is pending (process it first)");
+  if (prefetched_) throw std::runtime_error(std::string(what) + ": a prefetched batch is pending (process it first)");
   HIP_OK(hipStreamSynchronize(parse_stream_));
   HIP_OK(hipStreamSynchronize(stream_));
   HIP_OK(hipStreamSynchronize(comm_stream_));
-  const int32_t S = cfg_.max_series, n = n_series_;
+}
+
+uint64_t Engine::save_state(const std::string& path, const std::string& extra) {
+  checkpoint_wait();  // an asynchronous checkpoint in flight finishes first
+  checkpoint_quiesce("save_state");
   void* bounce = nullptr;
   HIP_OK(hipHostMalloc(&bounce, kBounce, hipHostMallocDefault));
   struct Guard { void* p; ~Guard() { hipHostFree(p); } } guard{bounce};
   BinWriter w(path);
+  write_small_sections(w);
+  // rings: every row of every LAG, synchronously through the bounce buffer
+  w.begin(SEC_RING);
+  const int32_t S = cfg_.max_series, n = n_series_;
+  const size_t rb = (size_t)cfg_.ring_bytes;
+  for (int l = 0; l < cfg_.n_lags; ++l) {
+    std::vector<int32_t> heads(cfg_.lags[l]);
+    for (int32_t h = 0; h < cfg_.lags[l]; ++h) heads[h] = h;
+    w.pod<int32_t>(n);
+    w.vec(heads);
+    d2h_rows(w, lag_[l].ring, (size_t)S * rb, (size_t)n * rb, (size_t)NSTAT * cfg_.lags[l], bounce, stream_);
+  }
+  w.end();
+  w.begin(SEC_EXTRA);
+  w.str(extra);
+  w.end();
+  w.commit();
+  ck_all_dirty_ = true;  // a standalone file does not extend an incremental chain
+  return w.bytes();
+}
+
+// Every section but the rings.  Device arrays are read synchronously (the engine is quiescent).
+void Engine::write_small_sections(BinWriter& w) {
+  const int32_t S = cfg_.max_series, n = n_series_;
+  if (!h_ck_bounce_) HIP_OK(hipHostMalloc(&h_ck_bounce_, kBounce, hipHostMallocDefault));
+  void* bounce = h_ck_bounce_;
 
   w.begin(SEC_CONFIG);
   w.pod(cfg_.max_series); w.pod(cfg_.n_lags); w.raw(cfg_.lags, sizeof(cfg_.lags)); w.pod(cfg_.ring_bytes);
@@ -306,6 +345,7 @@ uint64_t Engine::save_state(const std::string& path) {
     }
     w.pod<int32_t>(-1);
   }
+  d2h_vec(w, d_nan_until_, (size_t)n, stream_);
   w.end();
 
   w.begin(SEC_ZSCORE);
@@ -315,8 +355,6 @@ uint64_t Engine::save_state(const std::string& path) {
     d2h_vec(w, L.counter, (size_t)n, stream_);
     for (double* a : {L.sum, L.comp, L.sumsq, L.sqcomp}) d2h_rows(w, a, (size_t)S * 8, (size_t)n * 8, NSTAT, bounce, stream_);
     d2h_rows(w, L.cnt, (size_t)S * 4, (size_t)n * 4, NSTAT, bounce, stream_);
-    const size_t rb = (size_t)cfg_.ring_bytes;
-    d2h_rows(w, L.ring, (size_t)S * rb, (size_t)n * rb, (size_t)NSTAT * cfg_.lags[l], bounce, stream_);
   }
   w.end();
 
@@ -371,11 +409,104 @@ uint64_t Engine::save_state(const std::string& path) {
     for (uint64_t v : sc) w.pod(v);
   }
   w.end();
-  w.commit();
-  return w.bytes();
 }
 
-void Engine::load_state(const std::string& path) {
+namespace {
+bool is_chain_manifest(const std::string& path) {
+  FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) throw std::runtime_error("checkpoint: cannot open " + path);
+  char m[8] = {0};
+  const size_t got = std::fread(m, 1, 8, f);
+  std::fclose(f);
+  return got == 8 && std::memcmp(m, "APMCHAIN", 8) == 0;
+}
+
+std::string dir_of(const std::string& path) {
+  const size_t slash = path.rfind('/');
+  return slash == std::string::npos ? "." : (slash == 0 ? "/" : path.substr(0, slash));
+}
+
+// manifest: "APMCHAIN 1\n" then one file name (relative to the manifest's directory) per line,
+// base first, increments in order
+std::vector<std::string> read_chain(const std::string& path) {
+  FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) throw std::runtime_error("checkpoint: cannot open " + path);
+  std::vector<std::string> out;
+  char line[4096];
+  bool first = true;
+  while (std::fgets(line, sizeof line, f)) {
+    std::string l(line);
+    while (!l.empty() && (l.back() == '\n' || l.back() == '\r')) l.pop_back();
+    if (first) { first = false; continue; }
+    if (!l.empty()) out.push_back(dir_of(path) + "/" + l);
+  }
+  std::fclose(f);
+  if (out.empty()) throw std::runtime_error("checkpoint: empty chain manifest " + path);
+  return out;
+}
+
+void fsync_dir(const std::string& path) {
+  const int dfd = ::open(dir_of(path).c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+  if (dfd >= 0) { ::fsync(dfd); ::close(dfd); }
+}
+
+void write_text_atomic(const std::string& path, const std::string& body) {
+  const std::string tmp = path + ".tmp";
+  FILE* f = std::fopen(tmp.c_str(), "wb");
+  if (!f) throw std::runtime_error("checkpoint: cannot open " + tmp);
+  if (std::fwrite(body.data(), 1, body.size(), f) != body.size()) { std::fclose(f); throw std::runtime_error("checkpoint: write failed"); }
+  std::fflush(f);
+  ::fsync(::fileno(f));
+  std::fclose(f);
+  if (std::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("checkpoint: rename failed");
+  fsync_dir(path);
+}
+}  // namespace
+
+std::string Engine::load_state(const std::string& path) {
+  if (is_chain_manifest(path)) {
+    // incremental chain: the newest file holds the current small state; rings are the base's rows
+    // overwritten by each increment's dirty rows, in order
+    const std::vector<std::string> chain = read_chain(path);
+    std::string extra = load_small_state(chain.back());
+    for (const auto& f : chain) apply_ring_file(f);
+    ck_all_dirty_ = true;
+    return extra;
+  }
+  std::string extra = load_small_state(path);
+  apply_ring_file(path);
+  ck_all_dirty_ = true;
+  return extra;
+}
+
+void Engine::apply_ring_file(const std::string& path) {
+  void* bounce = nullptr;
+  HIP_OK(hipHostMalloc(&bounce, kBounce, hipHostMallocDefault));
+  struct Guard { void* p; ~Guard() { hipHostFree(p); } } guard{bounce};
+  BinReader rd(path);
+  rd.skip_to(SEC_RING);
+  const int32_t S = cfg_.max_series;
+  const size_t rb = (size_t)cfg_.ring_bytes;
+  for (int l = 0; l < cfg_.n_lags; ++l) {
+    const int32_t nc = rd.pod<int32_t>();
+    const std::vector<int32_t> heads = rd.vec<int32_t>();
+    if (nc > n_series_) throw std::runtime_error("checkpoint: ring section wider than the series table");
+    for (int32_t h : heads)
+      if (h < 0 || h >= cfg_.lags[l]) throw std::runtime_error("checkpoint: bad ring row");
+    for (int k = 0; k < NSTAT; ++k)
+      for (size_t i = 0; i < heads.size();) {  // runs of consecutive rows are contiguous in the file
+        size_t j = i + 1;
+        while (j < heads.size() && heads[j] == heads[j - 1] + 1) ++j;
+        char* dst = (char*)lag_[l].ring + ((size_t)k * cfg_.lags[l] + (size_t)heads[i]) * S * rb;
+        h2d_rows(rd, dst, (size_t)S * rb, (size_t)nc * rb, j - i, bounce, stream_);
+        i = j;
+      }
+  }
+  HIP_OK(hipStreamSynchronize(stream_));
+}
+
+std::string Engine::load_small_state(const std::string& path) {
+  checkpoint_wait();
   flush();
   if (batch_no_ != 0 || n_series_ != 0 || !files_.empty())
     throw std::runtime_error("load_state needs a freshly constructed engine (no files, no batches)");
@@ -514,6 +645,7 @@ void Engine::load_state(const std::string& path) {
       h2d_vec(rd, d_spill_val_ + (size_t)slot * cfg_.spill_cap, (size_t)cfg_.spill_cap, stream_);
     }
   }
+  h2d_vec(rd, d_nan_until_, (size_t)S, stream_);
 
   rd.begin(SEC_ZSCORE);
   for (int l = 0; l < cfg_.n_lags; ++l) {
@@ -522,8 +654,6 @@ void Engine::load_state(const std::string& path) {
     h2d_vec(rd, L.counter, (size_t)S, stream_);
     for (double* a : {L.sum, L.comp, L.sumsq, L.sqcomp}) h2d_rows(rd, a, (size_t)S * 8, (size_t)n * 8, NSTAT, bounce, stream_);
     h2d_rows(rd, L.cnt, (size_t)S * 4, (size_t)n * 4, NSTAT, bounce, stream_);
-    const size_t rb = (size_t)cfg_.ring_bytes;
-    h2d_rows(rd, L.ring, (size_t)S * rb, (size_t)n * rb, (size_t)NSTAT * cfg_.lags[l], bounce, stream_);
   }
 
   rd.begin(SEC_POOL);
@@ -584,9 +714,237 @@ void Engine::load_state(const std::string& path) {
                       &metrics_.alert_candidates, &metrics_.released};
     for (uint64_t* v : sc) rd.pod(*v);
   }
+  rd.skip_to(SEC_EXTRA);
+  std::string extra = rd.str();
   rd.finish();
   upload_series_tables(0);
   HIP_OK(hipStreamSynchronize(stream_));
+  return extra;
+}
+
+// ------------------------------------------------------------------------------ async checkpoint
+//
+// The ingest thread pays only for a consistent snapshot: the small sections are serialised to
+// memory (their device arrays are small), and the ring rows written since the previous
+// checkpoint (one row per rollover per LAG; all rows for a new base) are copied D2D into an HBM
+// staging area on the engine stream -- ~5 TB/s, so even a full 17 GB ring costs a few ms.  A
+// writer thread then drains the staging area D2H on its own stream through a pinned bounce
+// buffer, writes + fsyncs the file, and appends it to the chain manifest (atomic rename).  A new
+// base starts a fresh chain (and retires the old files) after kMaxChain increments.
+int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& extra, bool force_base) {
+  {
+    std::lock_guard<std::mutex> lk(ck_mu_);
+    if (ck_busy_) { ++ck_skipped_; return -1; }
+  }
+  const double t0 = now_ms();
+  checkpoint_quiesce("checkpoint_async");
+  auto job = std::make_shared<CkJob>();
+  const bool base = force_base || ck_all_dirty_ || ck_chain_.empty() || ck_prefix_ != prefix ||
+                    (int)ck_chain_.size() > kMaxChain;
+  job->base = base;
+  job->prefix = prefix;
+  job->seq = ++ck_seq_;
+  job->name = prefix.substr(prefix.rfind('/') + 1) + (base ? ".b" : ".i") + std::to_string(job->seq) + ".ckpt";
+  job->path = dir_of(prefix) + "/" + job->name;
+  job->extra = extra;
+  {
+    BinWriter mw{BinWriter::Memory{}};
+    write_small_sections(mw);
+    job->blob = mw.take_memory();
+  }
+  // dirty ring rows -> HBM staging (D2D, stream-ordered after the quiesce point)
+  const int32_t S = cfg_.max_series, n = n_series_;
+  const size_t rb = (size_t)cfg_.ring_bytes;
+  const int64_t r1 = rollover_idx_;
+  size_t need = 0;
+  for (int l = 0; l < cfg_.n_lags; ++l) {
+    const int32_t L = cfg_.lags[l];
+    CkJob::Lag lg;
+    lg.n_cols = n;
+    const int64_t dirty = base ? L : std::min<int64_t>(L, r1 - ck_ridx_);
+    const int32_t h0 = base || dirty == L ? 0 : (int32_t)(ck_ridx_ % L);
+    for (int64_t i = 0; i < dirty; ++i) lg.heads.push_back((int32_t)((h0 + i) % L));
+    lg.off = need;
+    need += (size_t)NSTAT * lg.heads.size() * n * rb;
+    job->lags.push_back(std::move(lg));
+  }
+  if (need > ck_stage_bytes_) {
+    if (d_ck_stage_) HIP_OK(hipFree(d_ck_stage_));
+    d_ck_stage_ = nullptr;
+    ck_stage_bytes_ = 0;
+    const size_t want = need + need / 8;  // room for the series table to grow
+    if (hipMalloc(&d_ck_stage_, want) != hipSuccess) {
+      (void)hipGetLastError();
+      d_ck_stage_ = nullptr;
+      // not enough HBM for a snapshot: fall back to the synchronous writer
+      ck_all_dirty_ = true;
+      const uint64_t bytes = save_state(job->path, extra);
+      job->base = true;
+      finish_chain(job, bytes);
+      ck_last_stall_ms_ = now_ms() - t0;
+      ++ck_sync_fallbacks_;
+      ck_ridx_ = r1;
+      ck_all_dirty_ = false;
+      return job->seq;
+    }
+    ck_stage_bytes_ = want;
+  }
+  for (int l = 0; l < cfg_.n_lags; ++l) {
+    const CkJob::Lag& lg = job->lags[l];
+    const int32_t L = cfg_.lags[l];
+    char* dst = (char*)d_ck_stage_ + lg.off;
+    for (int k = 0; k < NSTAT; ++k)
+      for (size_t i = 0; i < lg.heads.size();) {
+        size_t j = i + 1;
+        while (j < lg.heads.size() && lg.heads[j] == lg.heads[j - 1] + 1) ++j;
+        const char* src = (const char*)lag_[l].ring + ((size_t)k * L + (size_t)lg.heads[i]) * S * rb;
+        if (n > 0)
+          HIP_OK(hipMemcpy2DAsync(dst, (size_t)n * rb, src, (size_t)S * rb, (size_t)n * rb, j - i,
+                                  hipMemcpyDeviceToDevice, stream_));
+        dst += (j - i) * (size_t)n * rb;
+        i = j;
+      }
+  }
+  if (!ck_ev_) HIP_OK(hipEventCreateWithFlags(&ck_ev_, hipEventDisableTiming));
+  HIP_OK(hipEventRecord(ck_ev_, stream_));
+  ck_ridx_ = r1;
+  ck_all_dirty_ = false;
+  ck_prefix_ = prefix;
+  ck_last_stall_ms_ = now_ms() - t0;
+  ck_last_mode_ = base ? 1 : 0;
+  ck_last_ring_rows_ = 0;
+  for (const auto& lg : job->lags) ck_last_ring_rows_ += (int64_t)lg.heads.size();
+  {
+    std::lock_guard<std::mutex> lk(ck_mu_);
+    ck_busy_ = true;
+    ck_job_ = job;
+  }
+  if (!ck_thread_.joinable()) ck_thread_ = std::thread([this] { checkpoint_writer(); });
+  ck_cv_.notify_all();
+  return job->seq;
+}
+
+void Engine::checkpoint_writer() {
+  if (!ck_stream_) HIP_OK(hipStreamCreateWithFlags(&ck_stream_, hipStreamNonBlocking));
+  void* bounce = nullptr;
+  HIP_OK(hipHostMalloc(&bounce, kBounce, hipHostMallocDefault));
+  for (;;) {
+    std::shared_ptr<CkJob> job;
+    {
+      std::unique_lock<std::mutex> lk(ck_mu_);
+      ck_cv_.wait(lk, [&] { return ck_stop_ || ck_job_ != nullptr; });
+      if (ck_stop_ && !ck_job_) break;
+      job = ck_job_;
+    }
+    const double t0 = now_ms();
+    uint64_t bytes = 0;
+    std::string err;
+    try {
+      HIP_OK(hipEventSynchronize(ck_ev_));
+      BinWriter w(job->path);
+      w.raw(job->blob.data(), job->blob.size());
+      w.begin(SEC_RING);
+      const size_t rb = (size_t)cfg_.ring_bytes;
+      for (const auto& lg : job->lags) {
+        w.pod<int32_t>(lg.n_cols);
+        w.vec(lg.heads);
+        size_t left = (size_t)NSTAT * lg.heads.size() * (size_t)lg.n_cols * rb;
+        const char* src = (const char*)d_ck_stage_ + lg.off;
+        while (left) {
+          const size_t c = std::min(left, kBounce);
+          HIP_OK(hipMemcpyAsync(bounce, src, c, hipMemcpyDeviceToHost, ck_stream_));
+          HIP_OK(hipStreamSynchronize(ck_stream_));
+          w.raw(bounce, c);
+          src += c;
+          left -= c;
+        }
+      }
+      w.end();
+      w.begin(SEC_EXTRA);
+      w.str(job->extra);
+      w.end();
+      w.commit();
+      fsync_dir(job->path);
+      bytes = w.bytes();
+      finish_chain(job, bytes);
+    } catch (const std::exception& e) {
+      err = e.what();
+    }
+    {
+      std::lock_guard<std::mutex> lk(ck_mu_);
+      ck_last_write_ms_ = now_ms() - t0;
+      if (!err.empty()) {
+        ck_error_ = err;
+        ck_all_dirty_ = true;  // the chain did not get this increment: restart with a base
+      } else {
+        ck_last_bytes_ = bytes;
+        ++ck_done_;
+      }
+      ck_job_.reset();
+      ck_busy_ = false;
+    }
+    ck_cv_.notify_all();
+  }
+  hipHostFree(bounce);
+}
+
+// Appends a written file to the chain manifest (or starts a new chain with a base) and removes
+// the files the new manifest no longer names.
+void Engine::finish_chain(const std::shared_ptr<CkJob>& job, uint64_t bytes) {
+  (void)bytes;
+  std::vector<std::string> old;
+  if (job->base) {
+    old = ck_chain_;
+    ck_chain_.assign(1, job->name);
+  } else {
+    ck_chain_.push_back(job->name);
+  }
+  std::string body = "APMCHAIN 1\n";
+  for (const auto& f : ck_chain_) body += f + "\n";
+  write_text_atomic(job->prefix + ".ckpt", body);
+  for (const auto& f : old)
+    if (f != job->name) std::remove((dir_of(job->prefix) + "/" + f).c_str());
+}
+
+uint64_t Engine::checkpoint_wait() {
+  std::unique_lock<std::mutex> lk(ck_mu_);
+  ck_cv_.wait(lk, [&] { return !ck_busy_; });
+  if (!ck_error_.empty()) {
+    std::string e = ck_error_;
+    ck_error_.clear();
+    throw std::runtime_error("checkpoint writer: " + e);
+  }
+  return ck_last_bytes_;
+}
+
+void Engine::checkpoint_shutdown() {
+  {
+    std::lock_guard<std::mutex> lk(ck_mu_);
+    ck_stop_ = true;
+  }
+  ck_cv_.notify_all();
+  if (ck_thread_.joinable()) ck_thread_.join();
+  if (d_ck_stage_) { hipFree(d_ck_stage_); d_ck_stage_ = nullptr; }
+  if (h_ck_bounce_) { hipHostFree(h_ck_bounce_); h_ck_bounce_ = nullptr; }
+  if (ck_ev_) { hipEventDestroy(ck_ev_); ck_ev_ = nullptr; }
+  if (ck_stream_) { hipStreamDestroy(ck_stream_); ck_stream_ = nullptr; }
+}
+
+CheckpointInfo Engine::checkpoint_info() {
+  std::lock_guard<std::mutex> lk(ck_mu_);
+  CheckpointInfo c;
+  c.busy = ck_busy_;
+  c.done = ck_done_;
+  c.skipped = ck_skipped_;
+  c.sync_fallbacks = ck_sync_fallbacks_;
+  c.chain_len = (int)ck_chain_.size();
+  c.last_base = ck_last_mode_ == 1;
+  c.last_stall_ms = ck_last_stall_ms_;
+  c.last_write_ms = ck_last_write_ms_;
+  c.last_bytes = ck_last_bytes_;
+  c.stage_bytes = ck_stage_bytes_;
+  c.last_ring_rows = ck_last_ring_rows_;
+  return c;
 }
 
 // Text of `n` pending lines (gids into the HBM ring) in gid order, each with its '\n'.

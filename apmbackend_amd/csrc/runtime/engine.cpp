@@ -410,6 +410,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
 }
 
 Engine::~Engine() {
+  checkpoint_shutdown();
   {
     std::lock_guard<std::mutex> g(st_mu_);
     st_stop_ = true;
@@ -2155,6 +2156,7 @@ void Engine::drain_sinks(uint32_t kinds) {
 
 void Engine::warm_history(uint64_t seed) {
   flush();
+  ck_all_dirty_ = true;  // every ring row rewritten: the next checkpoint is a base
   // Use the latest window stats as the per-series baseline; fill every lag ring completely.
   for (int l = 0; l < cfg_.n_lags; ++l) {
     LagState& LS = lag_[l];

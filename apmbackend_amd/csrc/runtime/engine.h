@@ -137,6 +137,16 @@ struct Chunk {
   uint64_t begin, end;  // byte range in the batch (must end with '\n')
 };
 
+struct CheckpointInfo {
+  bool busy = false;
+  uint64_t done = 0, skipped = 0, sync_fallbacks = 0;
+  int chain_len = 0;
+  bool last_base = false;
+  double last_stall_ms = 0, last_write_ms = 0;
+  uint64_t last_bytes = 0, stage_bytes = 0;
+  int64_t last_ring_rows = 0;  // ring rows (over all LAGs) the last checkpoint carried
+};
+
 struct EngineMetrics {
   uint64_t batches = 0, bytes = 0, lines = 0, events = 0, tx = 0, tx_db = 0, tx_dropped = 0;
   uint64_t rollovers = 0, alerts = 0, alert_candidates = 0, series = 0, released = 0;
@@ -216,8 +226,18 @@ class Engine {
 
   // Binary checkpoint of the whole pipeline state (checkpoint.cpp).  load_state needs a freshly
   // constructed engine with the same LAG set / ring dtype / bucket layout.  Returns bytes written.
-  uint64_t save_state(const std::string& path);
-  void load_state(const std::string& path);
+  // `extra` is an opaque blob stored with the state (the service keeps its tail offsets there, so
+  // one fsync + rename covers both); load_state returns it.  load_state also accepts a chain
+  // manifest written by checkpoint_async (base + increments).
+  uint64_t save_state(const std::string& path, const std::string& extra = std::string());
+  std::string load_state(const std::string& path);
+  // Asynchronous incremental checkpoint into `<prefix>.ckpt` (chain manifest) + `<prefix>.{b,i}N.ckpt`:
+  // the calling thread pays for a consistent snapshot (small sections + dirty ring rows copied
+  // D2D into HBM staging); a writer thread does the D2H, file write and fsync.  Returns the
+  // checkpoint sequence number, or -1 when the previous one is still being written (skipped).
+  int64_t checkpoint_async(const std::string& prefix, const std::string& extra, bool force_base = false);
+  uint64_t checkpoint_wait();  // waits for the writer; rethrows its error
+  CheckpointInfo checkpoint_info();
 
   // Structured state access for the reference resume importer/exporter (state_io.cpp).
   std::vector<std::pair<std::string, std::string>> export_series();
@@ -571,6 +591,40 @@ class Engine {
   int32_t* d_js_scratch_ = nullptr;  // [JS_BLOCKS][kJsCap]
   static constexpr int32_t kJsCap = 1 << 18;
   StatsState stats_state() const;
+
+  // checkpoint (checkpoint.cpp)
+  struct CkJob {
+    struct Lag { int32_t n_cols = 0; std::vector<int32_t> heads; size_t off = 0; };
+    bool base = false;
+    int64_t seq = 0;
+    std::string prefix, name, path, blob, extra;
+    std::vector<Lag> lags;
+  };
+  static constexpr int kMaxChain = 16;
+  void checkpoint_quiesce(const char* what);
+  void write_small_sections(class BinWriter& w);
+  std::string load_small_state(const std::string& path);
+  void apply_ring_file(const std::string& path);
+  void checkpoint_writer();
+  void finish_chain(const std::shared_ptr<CkJob>& job, uint64_t bytes);
+  void checkpoint_shutdown();
+  std::mutex ck_mu_;
+  std::condition_variable ck_cv_;
+  std::thread ck_thread_;
+  std::shared_ptr<CkJob> ck_job_;
+  bool ck_busy_ = false, ck_stop_ = false, ck_all_dirty_ = true;
+  std::string ck_error_, ck_prefix_;
+  std::vector<std::string> ck_chain_;
+  int64_t ck_seq_ = 0, ck_ridx_ = 0;
+  int ck_last_mode_ = 0;
+  uint64_t ck_done_ = 0, ck_skipped_ = 0, ck_sync_fallbacks_ = 0, ck_last_bytes_ = 0;
+  int64_t ck_last_ring_rows_ = 0;
+  double ck_last_stall_ms_ = 0, ck_last_write_ms_ = 0;
+  void* d_ck_stage_ = nullptr;
+  size_t ck_stage_bytes_ = 0;
+  void* h_ck_bounce_ = nullptr;
+  hipEvent_t ck_ev_ = nullptr;
+  hipStream_t ck_stream_ = nullptr;
 
   // z-score state per lag
   struct LagState {

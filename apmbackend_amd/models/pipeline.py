@@ -180,14 +180,28 @@ class APMEngine:
     def take(self, kind: str) -> List[str]:
         return self.eng.take(kind)
 
-    def save_state(self, path: str) -> int:
-        """Binary checkpoint of the whole pipeline (engine + join caches + pending output)."""
-        return self.eng.save_state(path)
+    def save_state(self, path: str, extra: bytes = b"") -> int:
+        """Binary checkpoint of the whole pipeline (engine + join caches + pending output);
+        ``extra`` is stored with it (one atomic file)."""
+        return self.eng.save_state(path, extra)
 
-    def load_state(self, path: str):
-        """Resume from save_state() output; this engine must be fresh (no files, no batches)."""
-        self.eng.load_state(path)
+    def checkpoint_async(self, prefix: str, extra: bytes = b"", force_base: bool = False) -> int:
+        """Incremental asynchronous checkpoint (``<prefix>.ckpt`` chain manifest): returns its
+        sequence number, or -1 if the previous one is still being written."""
+        return self.eng.checkpoint_async(prefix, extra, force_base)
+
+    def checkpoint_wait(self) -> int:
+        return self.eng.checkpoint_wait()
+
+    def checkpoint_info(self) -> dict:
+        return self.eng.checkpoint_info()
+
+    def load_state(self, path: str) -> bytes:
+        """Resume from save_state() / checkpoint_async() output; this engine must be fresh (no
+        files, no batches).  Returns the ``extra`` blob stored with the state."""
+        extra = self.eng.load_state(path)
         self.file_ids = {p: i for i, (p, _k, _s) in enumerate(self.eng.files())}
+        return extra
 
     def take_bytes(self, kind: str) -> bytes:
         return self.eng.take_bytes(kind)

@@ -136,6 +136,7 @@ class IngestService:
         self.ckpt_every = float(g.get("checkpointEverySeconds",
                                       self.cfg["streamCalcStats"].get("resumeFileSaveFrequencyInSeconds", 60)))
         self.resharded = False
+        self._ckpt_extra = b""
         restored = self._restore() if (self.ckpt_dir and engine == "native") else False
         if not restored:
             if engine == "native" and as_bool(g.get("importReferenceResume", False)):
@@ -149,15 +150,32 @@ class IngestService:
         N = _native.load(build_if_missing=False)
         pc = self.cfg["streamParseTransactions"]
         self.pause_file = pc.get("tailPauseFileFullPath", "")
-        self.tailer = N.Tailer(self.pause_file, int(g.get("batchBytes", 32 << 20)))
+        self.batch_bytes = int(g.get("batchBytes", 32 << 20))
+        self.tailer = N.Tailer(self.pause_file, self.batch_bytes, int(g.get("tailReadThreads", 3)))
         from_start = as_bool(g.get("tailFromStart", False))
+        # batches are laid out grouped by the engine's server order: the engine's canonical
+        # (zero-copy) batch layout
+        srv_order: Dict[str, int] = {}
+        if hasattr(self.native, "servers"):
+            srv_order = {name: i for i, name in enumerate(self.native.servers())}
         for p, fid in sorted(self.file_ids.items(), key=lambda kv: kv[1]):
-            self.tailer.add(p, fid, from_start)
+            grp = srv_order.setdefault(self.server_of(p), len(srv_order))
+            self.tailer.add(p, fid, from_start, grp)
         self.offsets_path = pc.get("tailOffsetFileFullPath")
         if restored:
             self._restore_offsets()
         elif self.resharded:
             self._restore_offsets_resharded()
+        # read-ahead into pinned slots (native engine): the tailer fills the next slot while the
+        # engine works on the current one, and the engine prefetches (H2D + parse) the batch after
+        self.readahead = engine == "native" and as_bool(g.get("tailReadAhead", True))
+        self._slots: List[int] = []
+        self._held = None  # batch taken from the read-ahead ring and handed to the engine as prefetch
+        self._stopping = False
+        if self.readahead:
+            self._slot_bytes = self.batch_bytes
+            self._slots = [N.alloc_pinned(self._slot_bytes + 256) for _ in range(int(g.get("tailReadAheadSlots", 3)))]
+            self.tailer.start(self._slots, self._slot_bytes, float(g.get("tailIdleMs", 50.0)))
 
         # ---- outputs
         self.inserter: Optional[DBInserter] = None
@@ -253,7 +271,7 @@ class IngestService:
             self.resharded = True
             return False
         try:
-            self.eng.load_state(ck)
+            self._ckpt_extra = self.eng.load_state(ck)
             log.info("resumed engine state from %s", ck)
             known = {p for p, _k, _s in self.native.files()}
             for f in self.files:  # files that appeared since the checkpoint
@@ -278,11 +296,20 @@ class IngestService:
         log.info("imported reference resume files: %s", info)
 
     def _restore_offsets(self):
-        _, tp = self._ckpt_paths()
-        if not os.path.exists(tp):
-            return
-        with open(tp) as f:
-            offs = json.load(f)
+        # the offsets stored inside the engine checkpoint belong to exactly that state (one
+        # atomic file); the separate tail file is only a fallback for older checkpoints
+        offs = None
+        if self._ckpt_extra:
+            try:
+                offs = json.loads(self._ckpt_extra.decode("utf-8")).get("tail")
+            except (ValueError, UnicodeDecodeError):
+                offs = None
+        if offs is None:
+            _, tp = self._ckpt_paths()
+            if not os.path.exists(tp):
+                return
+            with open(tp) as f:
+                offs = json.load(f)
         for path, (off, ino) in offs.items():
             self.tailer.set_offset(path, int(off), int(ino))
 
@@ -304,21 +331,38 @@ class IngestService:
         log.info("re-sharded start: resumed %d of %d tails from the previous world's offsets", len(best),
                  len(self.file_ids))
 
-    def checkpoint(self):
+    def checkpoint(self, wait: bool = False):
+        """Incremental asynchronous checkpoint: the engine snapshots its state (dirty ring rows
+        D2D into HBM staging) and a writer thread persists it; the tail offsets of exactly that
+        state travel inside the engine file (one fsync + atomic rename covers both)."""
         if not self.ckpt_dir or self.eng is None:
             return None
+        if self._held is not None:
+            return None  # a prefetched batch is in the engine: the next step processes it first
         os.makedirs(self.ckpt_dir, exist_ok=True)
         ck, tp = self._ckpt_paths()
         t0 = time.perf_counter()
         # undelivered output goes out first so the checkpoint and the sinks agree
         self._drain_outputs()
-        n = self.native.save_state(ck)
+        extra = json.dumps({"tail": json.loads(self.tailer.offsets_json()), "world": self.world,
+                            "rank": self.rank, "servers": self.my_servers}).encode("utf-8")
+        prefix = ck[:-len(".ckpt")]
+        seq = self.eng.checkpoint_async(prefix, extra)
+        if seq < 0:
+            log.warning("checkpoint skipped: the previous one is still being written")
+            return None
+        if wait:
+            self.eng.checkpoint_wait()
         self.tailer.save_offsets(tp)
         write_json_atomic(self._meta_path(), {"world": self.world, "rank": self.rank, "servers": self.my_servers,
                                               "ts": time.time()})
         if self.offsets_path:
             self.tailer.save_offsets(self.offsets_path)
-        log.info("checkpoint %s: %.1f MB in %.0f ms", ck, n / 1e6, (time.perf_counter() - t0) * 1e3)
+        info = self.eng.checkpoint_info()
+        log.info("checkpoint %s #%d (%s): ingest stall %.1f ms (call %.0f ms)%s", ck, seq,
+                 "base" if info["last_base"] else "increment", info["last_stall_ms"],
+                 (time.perf_counter() - t0) * 1e3,
+                 f", written {info['last_bytes'] / 1e6:.1f} MB" if wait else "")
         self.last_ckpt = self.clock()
         return ck
 
@@ -455,7 +499,10 @@ class IngestService:
         # clock all-reduce, so every rank must call it once per poll -- with an empty batch when
         # its tails have nothing new or downstream is paused -- or the collective sequences diverge.
         lockstep = self.fleet is not None
-        if self.qm is not None and any(getattr(p, "paused", False) for p in self.producers.values()):
+        paused = self.qm is not None and any(getattr(p, "paused", False) for p in self.producers.values())
+        if self.readahead:
+            return self._step_readahead(lockstep, paused)
+        if paused:
             # downstream backpressure: hold the tails (pause-file semantics)
             if not lockstep:
                 return 0
@@ -489,6 +536,68 @@ class IngestService:
         self._drain_outputs()
         return len(buf)
 
+    def _ckpt_due(self) -> bool:
+        return bool(self.ckpt_dir) and self.eng is not None and self.clock() - self.last_ckpt >= self.ckpt_every
+
+    def _step_readahead(self, lockstep: bool, paused: bool) -> int:
+        """step() over the tailer's read-ahead ring: batches arrive in pinned slots, the batch
+        after the current one (if already read) is handed to the engine as its prefetch."""
+        cur = self._held
+        self._held = None
+        if cur is None and not paused:
+            cur = self.tailer.next(0.0)
+        if cur is None and not lockstep:
+            return 0
+        self.polls += 1
+        fi = self.fault
+        mine = bool(fi) and fi.get("rank", self.rank) == self.rank
+        if mine and fi.get("exitAtBatch") and self.polls == int(fi["exitAtBatch"]):
+            log.error("fault injection: exiting at batch %d", self.polls)
+            os._exit(int(fi.get("exitCode", 13)))
+        if cur is None:  # lock-step poll with nothing to read (or paused downstream)
+            self.native.process_batch(b"", [], -1.0)
+            self.batches += 1
+            self._drain_outputs()
+            return 0
+        slot, ptr, n, chunks, bid = cur
+        if mine and fi.get("dropBatchEvery") and self.polls % int(fi["dropBatchEvery"]) == 0:
+            log.warning("fault injection: dropping batch %d (%d bytes)", self.polls, n)
+            self.faults["dropped"] += 1
+            self.tailer.release(slot)
+            self.tailer.commit(bid)
+            if lockstep:
+                self.native.process_batch(b"", [], -1.0)
+                self.batches += 1
+            return n
+        dup = mine and fi.get("duplicateBatchEvery") and self.polls % int(fi["duplicateBatchEvery"]) == 0
+        nxt = None
+        if not paused and not dup and not self._ckpt_due() and not self._stopping:
+            nxt = self.tailer.next(0.0)
+        if nxt is not None:
+            self.native.process_batch_ptr(ptr, n, chunks, -1.0, nxt[1], nxt[2], nxt[3])
+        else:
+            self.native.process_batch_ptr(ptr, n, chunks, -1.0)
+        self.batches += 1
+        if dup:
+            if lockstep:
+                log.warning("fault injection: duplicateBatchEvery is ignored for lock-step ranks")
+            else:
+                log.warning("fault injection: replaying batch %d", self.polls)
+                self.faults["duplicated"] += 1
+                self.native.process_batch_ptr(ptr, n, chunks, -1.0)
+        self.tailer.release(slot)
+        self.tailer.commit(bid)
+        self._held = nxt
+        self._drain_outputs()
+        return n
+
+    def _idle(self, idle_sleep_s: float):
+        if self.readahead:
+            if self._held is None:
+                self._held = self.tailer.next(idle_sleep_s * 1000.0)
+        else:
+            self.tailer.wait(idle_sleep_s * 1000.0)
+
     def run(self, max_batches: Optional[int] = None, idle_sleep_s: float = 0.5,
             until: Optional[Callable[[], bool]] = None):
         log.info("ingest loop starting (mode=%s)", self.mode)
@@ -500,7 +609,7 @@ class IngestService:
             if until is not None and until():
                 break
             if n == 0:
-                time.sleep(idle_sleep_s)
+                self._idle(idle_sleep_s)
         self.shutdown()
 
     def shutdown(self):
@@ -509,12 +618,22 @@ class IngestService:
             # coordinated end (same batch count on every rank): decide the queued node-wide
             # alert candidates -- a collective, so not on a signal-driven (per-rank) stop
             self.fleet.drain_alerts()
+        self._stopping = True
+        while self._held is not None:  # a prefetched batch is processed before the final checkpoint
+            self.step()
         self.native.flush()
         self._drain_outputs()
+        if self.readahead:
+            self.tailer.stop()
         if self.ckpt_dir and self.eng is not None:
-            self.checkpoint()
+            self.eng.checkpoint_wait()
+            self.checkpoint(wait=True)
         if self.offsets_path:
             self.tailer.save_offsets(self.offsets_path)
+        for p in self._slots:
+            from .. import _native
+            _native.load(build_if_missing=False).free_pinned(p)
+        self._slots = []
         if self.inserter is not None:
             self.inserter.close()
         if self.notifier is not None:

@@ -503,3 +503,43 @@ def test_nan_elapsed_matches_oracle():
     assert out["al"] == P.al
     m = eng.metrics()
     assert m["nan_windows_clipped"] == 0
+
+
+@pytest.mark.parametrize("mode", ["exact", "rolling"])
+def test_incremental_checkpoint_chain_resume(tmp_path, mode):
+    """checkpoint_async: a base, then increments holding only the ring rows written since the
+    previous checkpoint (one per rollover per LAG); a fresh engine restored from the chain
+    manifest (base + increments) continues exactly like the uninterrupted run."""
+    lines, bl = synth_batches(6, duration=900)
+    C = small_cfg(mode)
+    _, full = _run_engine(C, bl)
+    cut = [len(bl) // 4, len(bl) // 2, (2 * len(bl)) // 3]
+    eng = APMEngine(C, keep_text=True)
+    out = collections.defaultdict(list)
+    prefix = str(tmp_path / "engine.rank0")
+    infos = []
+    for i, (now, chunks) in enumerate(bl[:cut[-1]]):
+        eng.process_lines(chunks, now)
+        for k in ("transactions", "audit_db", "st", "fs", "al"):
+            out[k] += eng.take(k)
+        if i + 1 in cut:
+            assert eng.checkpoint_async(prefix, b'{"tail": {"x": [%d, 0]}}' % i) > 0
+            eng.checkpoint_wait()
+            infos.append(eng.checkpoint_info())
+    assert infos[0]["last_base"] and not infos[1]["last_base"] and not infos[2]["last_base"]
+    assert infos[2]["chain_len"] == 3
+    # the base carries every ring row (LAG 6 + 30); increments only the rows of their rollovers
+    assert infos[0]["last_ring_rows"] == 36
+    assert 0 < infos[1]["last_ring_rows"] < 36 and 0 < infos[2]["last_ring_rows"] < 36
+    manifest = open(prefix + ".ckpt", "rb").read()
+    assert manifest.startswith(b"APMCHAIN") and manifest.count(b".ckpt") == 3
+    del eng
+    eng2 = APMEngine(C, keep_text=True)
+    extra = eng2.load_state(prefix + ".ckpt")
+    assert extra == b'{"tail": {"x": [%d, 0]}}' % (cut[-1] - 1)
+    for now, chunks in bl[cut[-1]:]:
+        eng2.process_lines(chunks, now)
+        for k in ("transactions", "audit_db", "db", "st", "fs", "al"):
+            out[k] += eng2.take(k)
+    for k in ("transactions", "audit_db", "st", "fs", "al"):
+        assert out[k] == full[k], k

@@ -254,3 +254,41 @@ def test_checkpoint_ownership_rules(tmp_path):
     write_json_atomic(str(ck / "meta.rank0.json"), {"world": 2, "servers": svc.my_servers, "ts": now})
     assert not svc._checkpoint_is_mine()
     svc.shutdown()
+
+
+def test_paused_lockstep_rank_still_joins_the_collective():
+    """under downstream backpressure a lock-step rank holds its tails but still calls
+    process_batch (with an empty batch) once per poll, so the ranks' collective sequences stay
+    aligned; a rank without lock-step just skips the poll."""
+    from apmbackend_amd.runtime.service import IngestService
+
+    class Prod:
+        paused = True
+
+    class Tail:
+        polled = 0
+
+        def poll(self):
+            Tail.polled += 1
+            return b"x\n", [(0, 0, 2)]
+
+    class Eng:
+        calls = []
+
+        def process_batch(self, buf, chunks, now):
+            Eng.calls.append((buf, list(chunks)))
+
+        def take_bytes(self, k):
+            return b""
+
+    for lockstep in (True, False):
+        Eng.calls, Tail.polled = [], 0
+        svc = IngestService.__new__(IngestService)
+        svc.qm, svc.producers = object(), {"db": Prod()}
+        svc.fleet = object() if lockstep else None
+        svc.readahead, svc.tailer, svc.native = False, Tail(), Eng()
+        svc.polls, svc.batches, svc.fault, svc.rank, svc.outputs = 0, 0, {}, 0, []
+        svc.inserter, svc.notifier = None, None
+        svc.step()
+        assert Tail.polled == 0
+        assert Eng.calls == ([(b"", [])] if lockstep else [])
