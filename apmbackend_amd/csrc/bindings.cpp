@@ -28,6 +28,7 @@ using namespace apm;
 void register_tailer(py::module_& m);
 void register_synth(py::module_& m);
 void register_procstat(py::module_& m);
+void register_dbsink(py::module_& m);
 
 namespace {
 
@@ -151,6 +152,7 @@ py::dict metrics_dict(const EngineMetrics& m) {
   d["series_overflow_tx"] = m.series_overflow_tx;
   d["spill_dropped"] = m.spill_dropped;
   d["nan_windows_clipped"] = m.nan_windows_clipped;
+  d["tx_capacity_grows"] = m.tx_capacity_grows;
   d["rollover_latency_ms"] = m.rollover_latency_ms;
   return d;
 }
@@ -359,6 +361,7 @@ PYBIND11_MODULE(_apm_native, m) {
         return py::bytes(b);
       })
       .def("set_sink_fd", &Engine::set_sink_fd, py::call_guard<py::gil_scoped_release>())
+      .def("set_fs_copy", &Engine::set_fs_copy, py::call_guard<py::gil_scoped_release>())
       .def("sink_bytes", &Engine::sink_bytes)
       .def("lane_cpus", &Engine::lane_cpus)
       .def("last_events", [](Engine& e) { return py::bytes(e.last_events()); })
@@ -504,4 +507,5 @@ PYBIND11_MODULE(_apm_native, m) {
   register_tailer(m);
   register_synth(m);
   register_procstat(m);
+  register_dbsink(m);
 }

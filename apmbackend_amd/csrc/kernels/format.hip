@@ -44,15 +44,8 @@ struct Out {
   __device__ __forceinline__ void i64(int64_t v) {
     if (v < 0) { c('-'); u((uint64_t)(-v)); } else u((uint64_t)v);
   }
-  // nf(x, f): 'undefined' for NaN, else x.toFixed(f)
-  __device__ __forceinline__ void fixed(double x, int f, bool& fallback) {
-    if (x != x) { s("undefined", 9); return; }
-    const bool neg = x < 0;
-    const double ax = neg ? -x : x;
-    if (!(ax < 9007199254740992.0)) {  // >= 2^53: integral values (rare)
-      big(neg, ax, f, fallback);
-      return;
-    }
+  // toFixed's integer n for |x| < 2^53: x * 10^f rounded, ties to the larger n (ECMA-262 21.1.3.3)
+  __device__ __forceinline__ static uint64_t fixed_n(double ax, int f) {
     const double scale = f == 1 ? 10.0 : 100.0;
     const double pr = ax * scale;
     const double e = fma(ax, scale, -pr);  // exact: x * 10^f = pr + e
@@ -65,6 +58,18 @@ struct Out {
       nn = (uint64_t)q;
       if (d > 0 || (d == 0 && e >= 0)) ++nn;
     }
+    return nn;
+  }
+  // nf(x, f): 'undefined' for NaN, else x.toFixed(f)
+  __device__ __forceinline__ void fixed(double x, int f, bool& fallback) {
+    if (x != x) { s("undefined", 9); return; }
+    const bool neg = x < 0;
+    const double ax = neg ? -x : x;
+    if (!(ax < 9007199254740992.0)) {  // >= 2^53: integral values (rare)
+      big(neg, ax, f, fallback);
+      return;
+    }
+    const uint64_t nn = fixed_n(ax, f);
     if (neg) c('-');
     const uint64_t sc = f == 1 ? 10 : 100;
     u(nn / sc);
@@ -72,6 +77,50 @@ struct Out {
     const uint64_t fr = nn % sc;
     if (f == 2) { c((char)('0' + fr / 10)); c((char)('0' + fr % 10)); }
     else c((char)('0' + fr));
+  }
+  // String(parseFloat(x.toFixed(f))) -- a number as the DB row holds it (copyenc.cpp parses the
+  // wire text back and prints it JS-style): NaN -> `nul` ('null' in JSON, '\N' as a COPY field).
+  // Below 10^15 significant units the parsed value's shortest form is the toFixed text with
+  // trailing fraction zeros dropped (a <= 15-digit decimal round-trips uniquely); -0 prints 0.
+  __device__ __forceinline__ void js_fixed(double x, int f, bool json, bool& fallback) {
+    if (x != x) { if (json) s("null", 4); else s("\\N", 2); return; }
+    const bool neg = x < 0;
+    const double ax = neg ? -x : x;
+    if (!(ax < 9007199254740992.0)) {  // integral: toFixed -> parseFloat gives x back
+      char buf[64];
+      bool inexact = false;
+      const int k = dj::js_num(buf, x, &inexact);
+      if (inexact) fallback = true;
+      s(buf, k);
+      return;
+    }
+    const uint64_t nn = fixed_n(ax, f);
+    if (nn == 0) { c('0'); return; }
+    if (nn >= 1000000000000000ULL) fallback = true;
+    if (neg) c('-');
+    const uint64_t sc = f == 1 ? 10 : 100;
+    u(nn / sc);
+    uint64_t fr = nn % sc;
+    if (fr == 0) return;
+    c('.');
+    if (f == 2) {
+      c((char)('0' + fr / 10));
+      if (fr % 10) c((char)('0' + fr % 10));
+    } else {
+      c((char)('0' + fr));
+    }
+  }
+  // a name as a COPY text field
+  __device__ __forceinline__ void copy_text(const char* src, int len) {
+    for (int i = 0; i < len; ++i) {
+      const char ch = src[i];
+      if (ch == '\\' || ch == '\t' || ch == '\n' || ch == '\r') {
+        c('\\');
+        c(ch == '\\' ? '\\' : (ch == '\t' ? 't' : (ch == '\n' ? 'n' : 'r')));
+      } else {
+        c(ch);
+      }
+    }
   }
   // |x| >= 2^53: x is an integer, so toFixed prints its digits and f zeros below 1e21 and
   // String(x) (exponent form) from 1e21 (ECMA-262 Number.prototype.toFixed step 10); exact up
@@ -120,7 +169,43 @@ __device__ void format_series(const FormatArgs& a, int32_t i, char* st_dst, char
       st.fixed(w.p75, 1, fb); st.c('|');
       st.fixed(w.p95, 1, fb); st.c('\n');
     }
-    if (a.want_fs) {
+    if (a.want_fs && a.fs_copy) {
+      // FullStatEntry.toPostgresObject (entries.js:120-151) as COPY text, field for field what
+      // copyenc.cpp makes of the wire line
+      const double x[NSTAT] = {w.avg, w.p75, w.p95};
+      const int4 nm = a.series_names[s];
+      for (int li = 0; li < a.n_lags; ++li) {
+        const int l = a.lag_order[li];
+        const ZOut z = a.z[l][s];
+        fs.s(a.ts_copy, a.ts_copy_len);
+        fs.c('\t');
+        fs.copy_text(a.names + nm.x, nm.y);
+        fs.c('\t');
+        fs.copy_text(a.names + nm.z, nm.w);
+        fs.c('\t');
+        fs.js_fixed(w.tpm, 2, false, fb);
+        fs.c('\t');
+        fs.u((uint64_t)a.lag_value[l]);
+        fs.s("\t{\"average\":", 12);
+        for (int k = 0; k < NSTAT; ++k) {
+          if (k == 1) fs.s(",\"per75\":", 9);
+          if (k == 2) fs.s(",\"per95\":", 9);
+          const char* nmk = k == 0 ? "average" : (k == 1 ? "per75" : "per95");
+          const int nl = k == 0 ? 7 : 5;
+          fs.js_fixed(x[k], 1, true, fb);
+          fs.s(",\"", 2); fs.s(nmk, nl); fs.s("avg\":", 5);
+          fs.js_fixed(z.mean[k], 1, true, fb);
+          fs.s(",\"", 2); fs.s(nmk, nl); fs.s("lb\":", 4);
+          fs.js_fixed(z.lb[k], 1, true, fb);
+          fs.s(",\"", 2); fs.s(nmk, nl); fs.s("ub\":", 4);
+          fs.js_fixed(z.ub[k], 1, true, fb);
+          fs.s(",\"", 2); fs.s(nmk, nl); fs.s("signal\":", 8);
+          fs.i64(z.sig[k]);
+        }
+        fs.c('}');
+        fs.c('\n');
+      }
+    } else if (a.want_fs) {
       const double x[NSTAT] = {w.avg, w.p75, w.p95};
       for (int li = 0; li < a.n_lags; ++li) {
         const int l = a.lag_order[li];
@@ -163,7 +248,7 @@ __global__ __launch_bounds__(256) void k_format_len(FormatArgs a) {
 // (131 us for 25 MB at 80k series).  A block whose range does not fit the LDS stage (very long
 // names) writes directly, as before.
 constexpr int FMT_WAVE_SERIES = 64;
-constexpr uint32_t FMT_LDS_ST = 6144, FMT_LDS_FS = 24576;
+constexpr uint32_t FMT_LDS_ST = 6144, FMT_LDS_FS = 24576, FMT_LDS_FS_COPY = 53248;
 
 __device__ __forceinline__ void wave_copy_out(const char* __restrict__ lds, char* __restrict__ out, uint32_t g0,
                                               uint32_t g1) {
@@ -180,16 +265,17 @@ __device__ __forceinline__ void wave_copy_out(const char* __restrict__ lds, char
   }
 }
 
+template <uint32_t LDS_FS>
 __global__ __launch_bounds__(FMT_WAVE_SERIES) void k_format_write(FormatArgs a) {
   __shared__ __align__(16) char sst[FMT_LDS_ST];
-  __shared__ __align__(16) char sfs[FMT_LDS_FS];
+  __shared__ __align__(16) char sfs[LDS_FS];
   const int32_t i0 = blockIdx.x * FMT_WAVE_SERIES;
   const int32_t i1 = min(a.n, i0 + FMT_WAVE_SERIES);
   const int32_t i = i0 + (int32_t)threadIdx.x;
   const uint32_t st0 = a.st_off[i0], st1 = a.st_off[i1];
   const uint32_t fs0 = a.fs_off[i0], fs1 = a.fs_off[i1];
   const bool st_lds = (st1 - (st0 & ~3u)) <= FMT_LDS_ST;  // uniform across the block
-  const bool fs_lds = (fs1 - (fs0 & ~3u)) <= FMT_LDS_FS;
+  const bool fs_lds = (fs1 - (fs0 & ~3u)) <= LDS_FS;
   if (i < i1) {
     bool fb = false;
     char* stp = st_lds ? sst + (a.st_off[i] - (st0 & ~3u)) : a.st_out + a.st_off[i];
@@ -248,8 +334,11 @@ void apm_format_fixed_batch(const double* d_x, int n, int f, char* d_out, hipStr
 
 void apm_format_write(FormatArgs* a, hipStream_t stream) {
   if (a->n <= 0) return;
-  hipLaunchKernelGGL(k_format_write, dim3((a->n + FMT_WAVE_SERIES - 1) / FMT_WAVE_SERIES), dim3(FMT_WAVE_SERIES),
-                     0, stream, *a);
+  const dim3 grid((a->n + FMT_WAVE_SERIES - 1) / FMT_WAVE_SERIES);
+  if (a->fs_copy && a->want_fs)  // COPY rows are ~2x the wire line: a bigger LDS stage
+    hipLaunchKernelGGL(k_format_write<FMT_LDS_FS_COPY>, grid, dim3(FMT_WAVE_SERIES), 0, stream, *a);
+  else
+    hipLaunchKernelGGL(k_format_write<FMT_LDS_FS>, grid, dim3(FMT_WAVE_SERIES), 0, stream, *a);
 }
 
 }  // extern "C"

@@ -102,6 +102,11 @@ struct FormatArgs {
   int32_t lag_order[MAX_LAGS];  // ascending LAG value
   int32_t lag_value[MAX_LAGS];
   int32_t want_st, want_fs;
+  // fs as Postgres COPY rows (the DB sink's K13 encoding fused into K12): the fs stream then
+  // carries `timestamp \t server \t service \t tpm \t lag \t stats-json` rows (copyenc.cpp)
+  int32_t fs_copy;
+  int32_t ts_copy_len;
+  char ts_copy[32];        // edge_ts as 'YYYY-MM-DD HH:MM:SS.mmm+00'
   uint32_t *st_len, *fs_len, *st_off, *fs_off;  // [n + 1]
   char *st_out, *fs_out;
   int32_t* fallback;

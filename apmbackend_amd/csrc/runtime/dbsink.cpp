@@ -1,0 +1,563 @@
+// Native DB insert stage: the MI355X-native replacement of stream_insert_db.js's buffering +
+// pg-promise multi-row INSERT path (stream_insert_db.js:277-353, dbstats.js:1-45).
+//
+// Semantics kept from the reference:
+//  * one buffer per record type (tx / fs / al / jx, entries.js toPostgresObject types);
+//  * a buffer already holding `limit` rows is flushed *before* the next row is appended (so one
+//    flush carries at most `limit` rows, :341-345), and `max_wait_ms` after the first row entered
+//    an empty buffer it is flushed by the timer (:333-339);
+//  * a failed flush puts its rows back at the *front* of the buffer, retried with the next flush
+//    (:310-320); DBStats rows / ms are kept per interval (dbstats.js).
+// Changed for throughput:
+//  * rows travel as wire lines until a flush; the COPY text encoding (copyenc.cpp) runs on a pool
+//    of encoder threads, and one writer thread loads the encoded flushes in submission order;
+//  * loading is `COPY table (cols) FROM STDIN` -- through one long-lived `psql` process per sink
+//    (each flush one COPY, acknowledged with an `\echo` marker carrying psql's :ERROR), or as
+//    append-only COPY spool files (`<table>.copy`, rotated by size; load with \copy), or null.
+//  * The caller's thread only splits lines into the per-type buffers (memchr speed).
+#include <fcntl.h>
+#include <poll.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <signal.h>
+#include <spawn.h>
+#include <sys/stat.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <vector>
+
+#include "engine.h"
+
+extern char** environ;
+
+namespace py = pybind11;
+
+namespace apm {
+namespace copyenc {
+void encode_blob(std::string_view blob, std::string* out, int64_t* counts);
+}
+
+namespace {
+
+double mono_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int type_of(std::string_view line) {
+  if (line.size() < 3 || line[2] != '|') return -1;
+  const char a = line[0], b = line[1];
+  if (a == 't' && b == 'x') return 0;
+  if (a == 'f' && b == 's') return 1;
+  if (a == 'a' && b == 'l') return 2;
+  if (a == 'j' && b == 'x') return 3;
+  return -1;
+}
+
+bool write_all(int fd, const char* p, size_t n) {
+  while (n) {
+    const ssize_t w = ::write(fd, p, n);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    p += w;
+    n -= (size_t)w;
+  }
+  return true;
+}
+
+// ----------------------------------------------------------------------------- writers
+struct Writer {
+  virtual ~Writer() = default;
+  // returns "" on success, else the error text
+  virtual std::string write(int type, const std::string& table, const std::string& columns, const std::string& rows) = 0;
+};
+
+struct NullWriter : Writer {
+  std::string write(int, const std::string&, const std::string&, const std::string&) override { return ""; }
+};
+
+// Append-only COPY text files, one per table, rotated by size.
+struct SpoolWriter : Writer {
+  std::string dir;
+  uint64_t rotate;
+  int fd[4] = {-1, -1, -1, -1};
+  uint64_t size[4] = {0, 0, 0, 0};
+  SpoolWriter(std::string d, uint64_t r) : dir(std::move(d)), rotate(r) {
+    ::mkdir(dir.c_str(), 0755);
+  }
+  ~SpoolWriter() override {
+    for (int f : fd)
+      if (f >= 0) ::close(f);
+  }
+  std::string write(int type, const std::string& table, const std::string& columns, const std::string& rows) override {
+    const std::string path = dir + "/" + table + ".copy";
+    if (fd[type] >= 0 && rotate && size[type] >= rotate) {
+      ::close(fd[type]);
+      fd[type] = -1;
+      const auto ms = (long long)std::chrono::duration_cast<std::chrono::milliseconds>(
+                          std::chrono::system_clock::now().time_since_epoch()).count();
+      ::rename(path.c_str(), (dir + "/" + table + "." + std::to_string(ms) + ".copy").c_str());
+    }
+    if (fd[type] < 0) {
+      const std::string cpath = dir + "/" + table + ".columns";
+      const int cf = ::open(cpath.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+      if (cf >= 0) {
+        const std::string c = columns + "\n";
+        write_all(cf, c.data(), c.size());
+        ::close(cf);
+      }
+      fd[type] = ::open(path.c_str(), O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
+      if (fd[type] < 0) return "cannot open " + path + ": " + std::strerror(errno);
+      struct stat st;
+      size[type] = ::fstat(fd[type], &st) == 0 ? (uint64_t)st.st_size : 0;
+    }
+    if (!write_all(fd[type], rows.data(), rows.size())) return std::string("spool write failed: ") + std::strerror(errno);
+    size[type] += rows.size();
+    return "";
+  }
+};
+
+// One long-lived psql process: every flush is `COPY t (cols) FROM STDIN;` + rows + `\.`, then
+// `\echo APMACK <seq> :ERROR` -- psql prints `APMACK <seq> false` when the COPY committed.  A
+// dead process is restarted by the next flush (that flush fails and is re-buffered).
+struct PsqlWriter : Writer {
+  std::vector<std::string> argv;
+  pid_t pid = -1;
+  int in = -1, out = -1;
+  uint64_t seq = 0;
+  std::string rbuf;
+  double timeout_ms;
+  explicit PsqlWriter(std::vector<std::string> a, double t) : argv(std::move(a)), timeout_ms(t) {}
+  ~PsqlWriter() override { stop(); }
+  void stop() {
+    if (in >= 0) { ::close(in); in = -1; }
+    if (out >= 0) { ::close(out); out = -1; }
+    if (pid > 0) {
+      int st = 0;
+      for (int i = 0; i < 50 && ::waitpid(pid, &st, WNOHANG) == 0; ++i) ::usleep(20000);
+      if (::waitpid(pid, &st, WNOHANG) == 0) { ::kill(pid, SIGTERM); ::waitpid(pid, &st, 0); }
+      pid = -1;
+    }
+    rbuf.clear();
+  }
+  std::string start() {
+    int pin[2], pout[2];
+    if (::pipe2(pin, O_CLOEXEC) != 0 || ::pipe2(pout, O_CLOEXEC) != 0) return "pipe failed";
+    posix_spawn_file_actions_t fa;
+    posix_spawn_file_actions_init(&fa);
+    posix_spawn_file_actions_adddup2(&fa, pin[0], 0);
+    posix_spawn_file_actions_adddup2(&fa, pout[1], 1);
+    std::vector<char*> av;
+    for (auto& s : argv) av.push_back(const_cast<char*>(s.c_str()));
+    av.push_back(nullptr);
+    const int rc = posix_spawnp(&pid, av[0], &fa, nullptr, av.data(), environ);
+    posix_spawn_file_actions_destroy(&fa);
+    ::close(pin[0]);
+    ::close(pout[1]);
+    if (rc != 0) {
+      ::close(pin[1]);
+      ::close(pout[0]);
+      pid = -1;
+      return std::string("cannot start ") + argv[0] + ": " + std::strerror(rc);
+    }
+    in = pin[1];
+    out = pout[0];
+    return "";
+  }
+  std::string write(int, const std::string& table, const std::string& columns, const std::string& rows) override {
+    if (pid < 0) {
+      std::string e = start();
+      if (!e.empty()) return e;
+    }
+    const uint64_t s = ++seq;
+    std::string head = "COPY " + table + " (" + columns + ") FROM STDIN;\n";
+    std::string tail = "\\.\n\\echo APMACK " + std::to_string(s) + " :ERROR\n";
+    if (!write_all(in, head.data(), head.size()) || !write_all(in, rows.data(), rows.size()) ||
+        !write_all(in, tail.data(), tail.size())) {
+      stop();
+      return "psql pipe closed";
+    }
+    const std::string want = "APMACK " + std::to_string(s) + " ";
+    const double t_end = mono_ms() + timeout_ms;
+    for (;;) {
+      size_t nl;
+      while ((nl = rbuf.find('\n')) != std::string::npos) {
+        std::string line = rbuf.substr(0, nl);
+        rbuf.erase(0, nl + 1);
+        if (line.compare(0, want.size(), want) == 0) {
+          const std::string v = line.substr(want.size());
+          return v == "false" ? "" : "COPY into " + table + " failed (psql :ERROR=" + v + ")";
+        }
+      }
+      const double left = t_end - mono_ms();
+      if (left <= 0) { stop(); return "psql did not acknowledge the COPY"; }
+      struct pollfd p{out, POLLIN, 0};
+      if (::poll(&p, 1, (int)left) <= 0) continue;
+      char b[4096];
+      const ssize_t r = ::read(out, b, sizeof b);
+      if (r <= 0) { stop(); return "psql exited"; }
+      rbuf.append(b, (size_t)r);
+    }
+  }
+};
+
+}  // namespace
+
+class DbSink : public ByteSink {
+ public:
+  DbSink(int64_t limit, double max_wait_ms, std::vector<std::string> tables, std::vector<std::string> columns,
+         const std::string& writer, const std::vector<std::string>& arg, uint64_t rotate_bytes, int encoders)
+      : limit_(std::max<int64_t>(1, limit)), max_wait_ms_(max_wait_ms), tables_(std::move(tables)),
+        columns_(std::move(columns)) {
+    if (tables_.size() != 4 || columns_.size() != 4) throw std::runtime_error("DbSink: 4 tables / column lists");
+    if (writer == "null") w_.reset(new NullWriter());
+    else if (writer == "spool") w_.reset(new SpoolWriter(arg.at(0), rotate_bytes));
+    else if (writer == "psql") w_.reset(new PsqlWriter(arg, 120000.0));
+    else throw std::runtime_error("DbSink: unknown writer " + writer);
+    for (int i = 0; i < std::max(1, encoders); ++i) enc_.emplace_back([this] { encode_loop(); });
+    wr_ = std::thread([this] { write_loop(); });
+  }
+  ~DbSink() override { shutdown(); }
+
+  // engine output lane -> sink (Engine::set_byte_sink)
+  void write_bytes(int, const char* p, size_t n) override { consume(std::string_view(p, n)); }
+
+  // Splits a newline-separated blob of wire lines into the type buffers (runs of one type are
+  // appended with one copy); returns accepted lines.
+  int64_t consume(std::string_view blob) {
+    const double now = mono_ms();
+    int64_t n = 0;
+    std::lock_guard<std::mutex> lk(mu_);
+    size_t i = 0;
+    int run_t = -1;
+    size_t run_b = 0;
+    int64_t run_n = 0;
+    auto close_run = [&](size_t end) {
+      if (run_t >= 0 && run_n) append_run_locked(run_t, blob.data() + run_b, end - run_b, run_n, now);
+      run_t = -1;
+      run_n = 0;
+    };
+    while (i < blob.size()) {
+      const char* q = (const char*)std::memchr(blob.data() + i, '\n', blob.size() - i);
+      const size_t j = q ? (size_t)(q - blob.data()) : blob.size();
+      if (j > i) {
+        const int t = type_of(blob.substr(i, j - i));
+        if (t != run_t || buf_[t < 0 ? 0 : t].n + run_n >= limit_) close_run(i);
+        if (t < 0) {
+          ++not_db_;
+        } else {
+          if (run_t < 0) { run_t = t; run_b = i; }
+          ++run_n;
+          ++n;
+        }
+      } else {
+        close_run(i);
+      }
+      i = j + 1;
+    }
+    close_run(std::min(i, blob.size()));
+    return n;
+  }
+
+  // Rows already in COPY text for `type` (the engine's fs stream in COPY mode): buffered and
+  // flushed with the same limit / timer rules, written without encoding.
+  int64_t consume_encoded(int type, std::string_view blob) {
+    const double now = mono_ms();
+    std::lock_guard<std::mutex> lk(mu_);
+    encoded_[type] = true;
+    int64_t n = 0;
+    size_t i = 0;
+    while (i < blob.size()) {
+      // the rows that fit the buffer before its limit
+      const int64_t room = std::max<int64_t>(1, limit_ - buf_[type].n);
+      size_t j = i;
+      int64_t k = 0;
+      while (k < room && j < blob.size()) {
+        const char* q = (const char*)std::memchr(blob.data() + j, '\n', blob.size() - j);
+        j = q ? (size_t)(q - blob.data()) + 1 : blob.size();
+        ++k;
+      }
+      append_run_locked(type, blob.data() + i, j - i, k, now);
+      n += k;
+      i = j;
+    }
+    return n;
+  }
+
+  // Rows already in COPY text (e.g. re-loaded from a resume file) queued as one flush.
+  void add_encoded(int type, std::string rows, int64_t n) {
+    auto j = std::make_shared<Job>();
+    j->type = type;
+    j->n = n;
+    j->encoded = std::move(rows);
+    j->ready = true;
+    std::lock_guard<std::mutex> lk(mu_);
+    j->seq = next_seq_++;
+    order_.push_back(j);
+    cv_.notify_all();
+  }
+
+  int tick() {
+    const double now = mono_ms();
+    int k = 0;
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int t = 0; t < 4; ++t)
+      if (buf_[t].n > 0 && now >= buf_[t].deadline) { submit_locked(t); ++k; }
+    return k;
+  }
+
+  void flush_all() {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int t = 0; t < 4; ++t)
+      if (buf_[t].n > 0) submit_locked(t);
+  }
+
+  // Waits until every submitted flush was written (or failed and re-buffered).
+  void drain() {
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return order_.empty(); });
+  }
+
+  // Final flush; returns what could not be written, per type, as wire lines (the caller keeps
+  // it in the resume file).
+  std::vector<std::string> close() {
+    flush_all();
+    drain();
+    shutdown();
+    std::vector<std::string> left(4);
+    for (int t = 0; t < 4; ++t) left[t] = buf_[t].lines;
+    return left;
+  }
+
+  py::dict stats() {
+    std::lock_guard<std::mutex> lk(mu_);
+    py::dict d;
+    d["rows"] = rows_;
+    d["ms"] = ms_;
+    d["flushes"] = flushes_;
+    d["failures"] = failures_;
+    d["queued"] = (int64_t)order_.size();
+    d["not_db_lines"] = not_db_;
+    d["bytes"] = bytes_;
+    int64_t buffered = 0;
+    for (auto& b : buf_) buffered += b.n;
+    d["buffered"] = buffered;
+    d["last_error"] = last_error_;
+    return d;
+  }
+
+  // (rows, ms) since the previous call -- DBStats' per-interval line
+  std::pair<int64_t, double> take_interval() {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto r = std::make_pair(rows_ - rows_mark_, ms_ - ms_mark_);
+    rows_mark_ = rows_;
+    ms_mark_ = ms_;
+    return r;
+  }
+
+  bool is_encoded(int t) {
+    std::lock_guard<std::mutex> lk(mu_);
+    return encoded_[t];
+  }
+
+  void set_limit(int64_t limit, double max_wait_ms) {
+    std::lock_guard<std::mutex> lk(mu_);
+    limit_ = std::max<int64_t>(1, limit);
+    max_wait_ms_ = max_wait_ms;
+  }
+
+ private:
+  struct Buf {
+    std::string lines;
+    int64_t n = 0;
+    double deadline = 0;
+  };
+  struct Job {
+    int type = 0;
+    int64_t n = 0;
+    uint64_t seq = 0;
+    std::string lines, encoded;
+    bool taken = false, ready = false;
+  };
+
+  // Appends `nrows` complete lines of type t; the buffer is flushed first when it is full.
+  void append_run_locked(int t, const char* p, size_t len, int64_t nrows, double now) {
+    Buf& b = buf_[t];
+    if (b.n >= limit_) submit_locked(t);
+    if (b.n == 0) b.deadline = now + max_wait_ms_;
+    b.lines.append(p, len);
+    if (len && p[len - 1] != '\n') b.lines += '\n';
+    b.n += nrows;
+  }
+
+  void submit_locked(int t) {
+    auto j = std::make_shared<Job>();
+    j->type = t;
+    j->n = buf_[t].n;
+    j->seq = next_seq_++;
+    if (encoded_[t]) {  // COPY text already: straight to the writer
+      j->encoded.swap(buf_[t].lines);
+      j->ready = true;
+    } else {
+      j->lines.swap(buf_[t].lines);
+      to_encode_.push_back(j);
+    }
+    buf_[t].n = 0;
+    order_.push_back(j);
+    cv_.notify_all();
+  }
+
+  void encode_loop() {
+    for (;;) {
+      std::shared_ptr<Job> j;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !to_encode_.empty(); });
+        if (to_encode_.empty()) return;  // stop_ and nothing left
+        j = to_encode_.front();
+        to_encode_.pop_front();
+      }
+      std::string out[4];
+      int64_t counts[4] = {0, 0, 0, 0};
+      copyenc::encode_blob(j->lines, out, counts);
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        j->encoded.swap(out[j->type]);
+        j->ready = true;
+      }
+      cv_.notify_all();
+    }
+  }
+
+  void write_loop() {
+    for (;;) {
+      std::shared_ptr<Job> j;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return (!order_.empty() && order_.front()->ready) || (stop_ && order_.empty()); });
+        if (order_.empty()) return;
+        j = order_.front();
+      }
+      const double t0 = mono_ms();
+      const std::string err = w_->write(j->type, tables_[j->type], columns_[j->type], j->encoded);
+      const double dt = mono_ms() - t0;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        order_.pop_front();
+        if (err.empty()) {
+          rows_ += j->n;
+          ms_ += dt;
+          bytes_ += (int64_t)j->encoded.size();
+          ++flushes_;
+        } else {
+          ++failures_;
+          last_error_ = err;
+          const std::string& back = encoded_[j->type] ? j->encoded : j->lines;
+          if (!back.empty()) {  // back to the front of its buffer (:310-320)
+            Buf& b = buf_[j->type];
+            if (b.n == 0) b.deadline = mono_ms() + max_wait_ms_;
+            b.lines.insert(0, back);
+            b.n += j->n;
+          }
+        }
+      }
+      done_cv_.notify_all();
+    }
+  }
+
+  void shutdown() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (stop_) return;
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : enc_) t.join();
+    if (wr_.joinable()) wr_.join();
+    w_.reset();
+  }
+
+  int64_t limit_;
+  double max_wait_ms_;
+  std::vector<std::string> tables_, columns_;
+  std::unique_ptr<Writer> w_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  Buf buf_[4];
+  bool encoded_[4] = {false, false, false, false};  // type buffered as COPY rows (engine-encoded)
+  std::deque<std::shared_ptr<Job>> order_, to_encode_;
+  uint64_t next_seq_ = 0;
+  bool stop_ = false;
+  std::vector<std::thread> enc_;
+  std::thread wr_;
+  int64_t rows_ = 0, flushes_ = 0, failures_ = 0, not_db_ = 0, bytes_ = 0, rows_mark_ = 0;
+  double ms_ = 0, ms_mark_ = 0;
+  std::string last_error_;
+};
+
+// Engine output stream -> sink, as wire lines or (type >= 0) as COPY rows of that type.
+struct SinkRoute : ByteSink {
+  std::shared_ptr<DbSink> sink;
+  int type;
+  SinkRoute(std::shared_ptr<DbSink> s, int t) : sink(std::move(s)), type(t) {}
+  void write_bytes(int kind, const char* p, size_t n) override {
+    if (type >= 0) sink->consume_encoded(type, std::string_view(p, n));
+    else sink->write_bytes(kind, p, n);
+  }
+};
+
+}  // namespace apm
+
+void register_dbsink(py::module_& m) {
+  using apm::DbSink;
+  using apm::Engine;
+  py::class_<DbSink, std::shared_ptr<DbSink>>(m, "DbSink")
+      .def(py::init<int64_t, double, std::vector<std::string>, std::vector<std::string>, std::string,
+                    std::vector<std::string>, uint64_t, int>(),
+           py::arg("limit"), py::arg("max_wait_ms"), py::arg("tables"), py::arg("columns"), py::arg("writer"),
+           py::arg("arg"), py::arg("rotate_bytes") = 1ull << 30, py::arg("encoders") = 2)
+      .def("consume", [](DbSink& s, py::bytes b) {
+        std::string_view v = b;
+        py::gil_scoped_release rel;
+        return s.consume(v);
+      })
+      .def("add_encoded", [](DbSink& s, int type, py::bytes rows, int64_t n) { s.add_encoded(type, rows, n); })
+      .def("tick", &DbSink::tick, py::call_guard<py::gil_scoped_release>())
+      .def("flush_all", &DbSink::flush_all, py::call_guard<py::gil_scoped_release>())
+      .def("drain", &DbSink::drain, py::call_guard<py::gil_scoped_release>())
+      .def("close", [](DbSink& s) {
+        std::vector<std::string> left;
+        { py::gil_scoped_release rel; left = s.close(); }
+        py::list out;
+        for (auto& l : left) out.append(py::bytes(l));
+        return out;
+      })
+      .def("stats", &DbSink::stats)
+      .def("take_interval", &DbSink::take_interval)
+      .def("set_limit", &DbSink::set_limit)
+      .def("is_encoded", &DbSink::is_encoded)
+      .def("consume_encoded", [](DbSink& s, int type, py::bytes b) {
+        std::string_view v = b;
+        py::gil_scoped_release rel;
+        return s.consume_encoded(type, v);
+      });
+  m.def("attach_sink", [](Engine& e, const std::string& kind, std::shared_ptr<DbSink> s, int encoded_type) {
+    py::gil_scoped_release rel;
+    e.set_byte_sink(kind, std::make_shared<apm::SinkRoute>(std::move(s), encoded_type));
+  }, py::arg("engine"), py::arg("kind"), py::arg("sink"), py::arg("encoded_type") = -1);
+  m.def("detach_sink", [](Engine& e, const std::string& kind) {
+    py::gil_scoped_release rel;
+    e.set_byte_sink(kind, nullptr);
+  }, py::arg("engine"), py::arg("kind"));
+}

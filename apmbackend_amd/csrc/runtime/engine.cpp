@@ -298,7 +298,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   d_big_n_ = (int32_t*)dmalloc(4);
   d_nan_until_ = (int32_t*)dmalloc((size_t)S * 4);
   HIP_OK(hipMemset(d_nan_until_, 0x80, (size_t)S * 4));  // 0x80808080: far below any bucket
-  d_ord_list_ = (int32_t*)dmalloc((size_t)std::max<int64_t>(cfg_.max_tx_per_batch, cfg_.max_lines) * 4);
+  ord_cap_ = std::max<int64_t>(cfg_.max_tx_per_batch, cfg_.max_lines);
+  d_ord_list_ = (int32_t*)dmalloc((size_t)ord_cap_ * 4);
   d_ord_n_ = (int32_t*)dmalloc(4);
   d_nan_list_ = (int32_t*)dmalloc((size_t)S * 4);
   d_nan_n_ = (int32_t*)dmalloc(4);
@@ -1292,6 +1293,35 @@ void Engine::release_gather(int k, int64_t released) {
   drain_kind(OUT_DB);
 }
 
+// The per-batch tx staging (host pinned + device) doubles instead of failing the batch; the
+// `keep` tx already staged are carried over.  Runs on the stats thread between batches' copies.
+void Engine::grow_tx_capacity(uint32_t need, uint32_t keep) {
+  int64_t cap = std::max<int64_t>(cfg_.max_tx_per_batch, 1024);
+  while (cap < (int64_t)need) cap *= 2;
+  HIP_OK(hipStreamSynchronize(stream_));  // no copy / kernel still reads the old buffers
+  TxRec* h_tx = nullptr;
+  int64_t* h_gid = nullptr;
+  HIP_OK(hipHostMalloc((void**)&h_tx, (size_t)cap * sizeof(TxRec), hipHostMallocDefault));
+  HIP_OK(hipHostMalloc((void**)&h_gid, (size_t)cap * 8, hipHostMallocDefault));
+  std::memcpy(h_tx, h_tx_, (size_t)keep * sizeof(TxRec));
+  std::memcpy(h_gid, h_gid_, (size_t)keep * 8);
+  hipHostFree(h_tx_);
+  hipHostFree(h_gid_);
+  h_tx_ = h_tx;
+  h_gid_ = h_gid;
+  HIP_OK(hipFree(d_tx_));
+  HIP_OK(hipFree(d_gid_));
+  d_tx_ = (TxRec*)dmalloc((size_t)cap * sizeof(TxRec));
+  d_gid_ = (int64_t*)dmalloc((size_t)cap * 8);
+  if (cap > std::max<int64_t>(ord_cap_, 0)) {
+    HIP_OK(hipFree(d_ord_list_));
+    d_ord_list_ = (int32_t*)dmalloc((size_t)cap * 4);
+    ord_cap_ = cap;
+  }
+  cfg_.max_tx_per_batch = (int32_t)cap;
+  ++metrics_.tx_capacity_grows;
+}
+
 StatsState Engine::stats_state() const {
   StatsState st{d_counts_cells_, d_cells_, d_spill_n_, d_spill_series_, d_spill_val_, d_active_,
                 cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series, d_spill_drop_};
@@ -1348,7 +1378,7 @@ void Engine::stats_for_batch(std::vector<TxOut>& txs, double batch_t0) {
     const int64_t b = end / 10000;
     // a tx with a newer bucket triggers the rollover *before* it is added (:348-370)
     if (b > latest_) { triggers.push_back({n, b}); latest_ = b; }
-    if (n >= (uint32_t)cfg_.max_tx_per_batch) throw std::runtime_error("too many tx in one batch");
+    if (n >= (uint32_t)cfg_.max_tx_per_batch) grow_tx_capacity(n + 1, n);  // e.g. a burst of need-cache expiries
     int32_t s;
     {
       if ((size_t)t.server >= ser_raw_.size()) ser_raw_.resize((size_t)t.server + 1);
@@ -1889,8 +1919,37 @@ void Engine::sync_format_tables() {
   }
 }
 
+// ms since the epoch -> Postgres COPY timestamp text 'YYYY-MM-DD HH:MM:SS.mmm+00' (copyenc.cpp
+// c_ts); returns the length written to out (>= 27 bytes)
+int Engine::pg_timestamp(int64_t ms, char* out) {
+  int64_t days = ms / 86400000, rem = ms % 86400000;
+  if (rem < 0) { rem += 86400000; --days; }
+  days += 719468;
+  const int64_t era = (days >= 0 ? days : days - 146096) / 146097;
+  const unsigned doe = (unsigned)(days - era * 146097);
+  const unsigned yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+  const unsigned doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+  const unsigned mp = (5 * doy + 2) / 153;
+  const unsigned d = doy - (153 * mp + 2) / 5 + 1;
+  const unsigned m = mp < 10 ? mp + 3 : mp - 9;
+  const int y = (int)(yoe + era * 400) + (m <= 2);
+  return std::snprintf(out, 32, "%04d-%02u-%02u %02d:%02d:%02d.%03d+00", y, m, d, (int)(rem / 3600000),
+                       (int)(rem / 60000 % 60), (int)(rem / 1000 % 60), (int)(rem % 1000));
+}
+
+void Engine::set_fs_copy(bool on) {
+  flush();
+  fs_copy_ = on;
+}
+
 void Engine::emit_bytes(int kind, const char* p, size_t n) {
   if (!n) return;
+  if (byte_sink_[kind]) {
+    drain_kind(kind);
+    byte_sink_[kind]->write_bytes(kind, p, n);
+    sink_bytes_[kind] += n;
+    return;
+  }
   if (sink_fd_[kind] >= 0) {
     // keep stream order: whatever is buffered goes first, then straight from the staging buffer
     drain_kind(kind);
@@ -1930,6 +1989,8 @@ void Engine::format_rollover_text(int64_t edge_ts) {
   fa.n_lags = cfg_.n_lags;
   fa.want_st = want(OUT_ST);
   fa.want_fs = want(OUT_FS);
+  fa.fs_copy = fs_copy_ ? 1 : 0;
+  if (fs_copy_) fa.ts_copy_len = pg_timestamp(edge_ts, fa.ts_copy);
   fa.st_len = d_fmt_len_;
   fa.fs_len = d_fmt_len_ + (S + 1);
   fa.st_off = d_fmt_off_;
@@ -1943,7 +2004,7 @@ void Engine::format_rollover_text(int64_t edge_ts) {
   out_wait(fmt_task_[k]);  // slot k's previous D2H + emission is done
   trace_event("fmt.wait_lane", tf1, now_ms(), 1);
   const size_t st_cap = fa.want_st ? (size_t)n * (176 + max_name_len_) : 0;
-  const size_t fs_cap = fa.want_fs ? (size_t)n * cfg_.n_lags * (560 + max_name_len_) : 0;
+  const size_t fs_cap = fa.want_fs ? (size_t)n * cfg_.n_lags * (fs_copy_ ? 720 + 2 * max_name_len_ : 560 + max_name_len_) : 0;
   if (st_cap + fs_cap + 64 > fmt_out_cap_[k]) d_fmt_out_[k] = (char*)regrow(d_fmt_out_[k], fmt_out_cap_[k], st_cap + fs_cap + 64);
   fa.st_out = d_fmt_out_[k];
   fa.fs_out = d_fmt_out_[k] + st_cap;
@@ -2132,7 +2193,18 @@ void Engine::set_sink_fd(const std::string& kind, int fd) {
   sink_fd_[out_kind_of(kind)] = fd;
 }
 
+void Engine::set_byte_sink(const std::string& kind, std::shared_ptr<ByteSink> sink) {
+  flush();
+  byte_sink_[out_kind_of(kind)] = std::move(sink);
+}
+
 void Engine::drain_kind(int k) {
+  if (byte_sink_[k] && !blob_[k].empty()) {
+    byte_sink_[k]->write_bytes(k, blob_[k].data(), blob_[k].size());
+    sink_bytes_[k] += blob_[k].size();
+    blob_[k].clear();
+    return;
+  }
   if (sink_fd_[k] < 0 || blob_[k].empty()) return;
   const char* p = blob_[k].data();
   size_t left = blob_[k].size();

@@ -137,6 +137,12 @@ struct Chunk {
   uint64_t begin, end;  // byte range in the batch (must end with '\n')
 };
 
+// In-process consumer of an output stream (runtime/dbsink.cpp DbSink).
+struct ByteSink {
+  virtual ~ByteSink() = default;
+  virtual void write_bytes(int kind, const char* p, size_t n) = 0;
+};
+
 struct CheckpointInfo {
   bool busy = false;
   uint64_t done = 0, skipped = 0, sync_fallbacks = 0;
@@ -154,6 +160,7 @@ struct EngineMetrics {
   uint64_t series_overflow_tx = 0;  // tx whose series could not be created (gpu.maxSeries full)
   uint64_t spill_dropped = 0;       // samples lost to a full bucket spill list (gpu.bucketOverflowCapacity)
   uint64_t nan_windows_clipped = 0; // NaN windows larger than the JS-emulation scratch (percentiles clipped)
+  uint64_t tx_capacity_grows = 0;   // per-batch tx staging doubled (instead of failing the batch)
   double t_parse_ms = 0, t_join_ms = 0, t_stats_ms = 0, t_total_ms = 0;
   double t_join_shards_ms = 0, t_merge_ms = 0;                 // split of t_join_ms
   double t_shard_busy_ms = 0, t_shard_max_ms = 0;              // per batch: mean / max of one shard's join
@@ -212,6 +219,13 @@ class Engine {
   // Route a stream to a file descriptor: the stats thread write()s each batch's blob to it (a
   // COPY/queue spool file, a pipe to the DB loader, /dev/null).  fd < 0 detaches.
   void set_sink_fd(const std::string& kind, int fd);
+  // Route a stream to an in-process consumer (the native DB sink): the output lane hands it each
+  // batch's bytes directly -- no Python, no extra copy.  nullptr detaches.
+  void set_byte_sink(const std::string& kind, std::shared_ptr<ByteSink> sink);
+  // fs stream as Postgres COPY rows (K12 formats the DB row directly; the DB sink skips encoding)
+  void set_fs_copy(bool on);
+  bool fs_copy() const { return fs_copy_; }
+  static int pg_timestamp(int64_t ms, char* out);
   uint64_t sink_bytes(const std::string& kind) { flush(); return sink_bytes_[out_kind_of(kind)]; }
 
   // Exogenous per-JVM gauges (JMX jx record fields in JmxEntry order + VM load) fused into the
@@ -591,6 +605,8 @@ class Engine {
   int32_t* d_js_scratch_ = nullptr;  // [JS_BLOCKS][kJsCap]
   static constexpr int32_t kJsCap = 1 << 18;
   StatsState stats_state() const;
+  void grow_tx_capacity(uint32_t need, uint32_t keep);
+  int64_t ord_cap_ = 0;
 
   // checkpoint (checkpoint.cpp)
   struct CkJob {
@@ -730,6 +746,8 @@ class Engine {
   // text outputs
   std::string blob_[N_OUT];
   int sink_fd_[N_OUT] = {-1, -1, -1, -1, -1, -1, -1};
+  std::shared_ptr<ByteSink> byte_sink_[N_OUT];
+  bool fs_copy_ = false;
   uint64_t sink_bytes_[N_OUT] = {0, 0, 0, 0, 0, 0, 0};
   // K14 server rollup + exogenous context
   std::vector<double> h_ctx_;                    // [servers][CTX_FIELDS]

@@ -59,6 +59,8 @@ def engine_config(cfg: Dict[str, Any], device: int = 0, keep_text: bool = False,
         "spill_cap": int(g.get("bucketOverflowCapacity", 1 << 22)) // 40 or 1,
         "max_batch_bytes": int(g.get("batchBytes", 32 << 20)) * 2,
         "max_lines": int(g.get("maxLinesPerBatch", 1 << 20)) * 2,
+        # host-join tx staging per batch (grows by doubling when a batch needs more)
+        "max_tx_per_batch": int(g.get("maxTxPerBatch", int(g.get("maxLinesPerBatch", 1 << 20)) * 2)),
         "ring_bytes": ring,
         "exact_mean": 1 if g.get("zscoreMeanMode", "rolling") == "exact" else 0,
         "sigma_stddev": 1 if g.get("zscoreSigma", "sqrt_mean") == "stddev" else 0,

@@ -162,6 +162,8 @@ class IngestService:
             grp = srv_order.setdefault(self.server_of(p), len(srv_order))
             self.tailer.add(p, fid, from_start, grp)
         self.offsets_path = pc.get("tailOffsetFileFullPath")
+        if self.offsets_path:
+            os.makedirs(os.path.dirname(os.path.abspath(self.offsets_path)), exist_ok=True)
         if restored:
             self._restore_offsets()
         elif self.resharded:
@@ -172,6 +174,9 @@ class IngestService:
         self._slots: List[int] = []
         self._held = None  # batch taken from the read-ahead ring and handed to the engine as prefetch
         self._stopping = False
+        self.perf = {"wait_s": 0.0, "engine_s": 0.0, "outputs_s": 0.0, "batches": 0, "bytes": 0, "prefetched": 0}
+        self._drain_every_s = float(g.get("outputDrainMs", 250.0)) / 1000.0
+        self._last_drain = 0.0
         if self.readahead:
             self._slot_bytes = self.batch_bytes
             self._slots = [N.alloc_pinned(self._slot_bytes + 256) for _ in range(int(g.get("tailReadAheadSlots", 3)))]
@@ -183,6 +188,10 @@ class IngestService:
         self.producers: Dict[str, Any] = {}
         if self.mode == "inproc":
             self.inserter = DBInserter(self.cfg)
+            if engine == "native":
+                # db / audit / fs go engine output lane -> native sink directly; al stays on the
+                # Python side (the e-mail notifier reads it too)
+                self.inserter.attach_engine(self.native, [k for k in self.outputs if k in DB_OUTPUTS and k != "al"])
         elif self.mode == "amqp":
             from .queue import QueueManager
             self.qm = QueueManager(self.cfg["amqpConnectionString"], self.cfg.get("statLogIntervalInSeconds", 60))
@@ -542,10 +551,14 @@ class IngestService:
     def _step_readahead(self, lockstep: bool, paused: bool) -> int:
         """step() over the tailer's read-ahead ring: batches arrive in pinned slots, the batch
         after the current one (if already read) is handed to the engine as its prefetch."""
+        pf = self.perf
+        t0 = time.perf_counter()
         cur = self._held
         self._held = None
         if cur is None and not paused:
             cur = self.tailer.next(0.0)
+        t1 = time.perf_counter()
+        pf["wait_s"] += t1 - t0
         if cur is None and not lockstep:
             return 0
         self.polls += 1
@@ -573,10 +586,16 @@ class IngestService:
         nxt = None
         if not paused and not dup and not self._ckpt_due() and not self._stopping:
             nxt = self.tailer.next(0.0)
+        t2 = time.perf_counter()
         if nxt is not None:
             self.native.process_batch_ptr(ptr, n, chunks, -1.0, nxt[1], nxt[2], nxt[3])
         else:
             self.native.process_batch_ptr(ptr, n, chunks, -1.0)
+        t3 = time.perf_counter()
+        pf["engine_s"] += t3 - t2
+        pf["batches"] += 1
+        pf["bytes"] += n
+        pf["prefetched"] += nxt is not None
         self.batches += 1
         if dup:
             if lockstep:
@@ -588,10 +607,20 @@ class IngestService:
         self.tailer.release(slot)
         self.tailer.commit(bid)
         self._held = nxt
-        self._drain_outputs()
+        t4 = time.perf_counter()
+        # take_bytes waits for the engine's in-flight stats stage: with the DB streams going
+        # straight to the native sink, the remaining Python-side streams (al -> notifier) are
+        # collected every outputDrainMs instead of once per batch, so batches stay pipelined
+        if self._drain_every_s <= 0 or t4 - self._last_drain >= self._drain_every_s:
+            self._drain_outputs()
+            self._last_drain = time.perf_counter()
+        pf["outputs_s"] += time.perf_counter() - t4
         return n
 
     def _idle(self, idle_sleep_s: float):
+        if self.readahead and self._drain_every_s > 0:
+            self._drain_outputs()
+            self._last_drain = time.perf_counter()
         if self.readahead:
             if self._held is None:
                 self._held = self.tailer.next(idle_sleep_s * 1000.0)

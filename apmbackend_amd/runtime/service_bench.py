@@ -1,0 +1,124 @@
+"""Production-path benchmark (``bench.py --path service``): real log files -> native tailer
+(read-ahead into pinned slots) -> engine -> native DB sink (COPY spool) -- the path a deployment
+runs, next to the headline which feeds the engine from memory.
+
+The corpus is the headline's (SynthGen, same shard shape); it is appended to real files under
+``--service-dir`` (default /dev/shm) before the timed region, so the timed region measures the
+service catching up on a backlog: tailer reads, H2D, GPU pipeline, sink encoding and writes,
+every tail offset committed.  The z-score rings get the same synthetic pre-history as the
+headline.  Reported: lines/s through the service, the DB rows/s the sink wrote, and the sink's
+encode/write share.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import tempfile
+import time
+from typing import Any, Dict
+
+
+def run(args, cfg: Dict[str, Any], N, rank: int = 0) -> Dict[str, Any]:
+    from .service import IngestService
+
+    base = args.service_dir or ("/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir())
+    root = tempfile.mkdtemp(prefix="apm_svc_bench_", dir=base)
+    try:
+        return _run(args, cfg, N, rank, root, IngestService)
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+
+
+def _run(args, cfg, N, rank, root, IngestService):
+    start = 1578391200000
+    step_ms = int(args.batch_seconds * 1000)
+    gen = N.SynthGen({"servers": args.servers, "ejb_services": args.ejb, "provider_services": args.providers,
+                      "tx_per_sec_per_server": args.tx_rate, "seed": 1 + rank,
+                      "server_offset": rank * args.servers,
+                      "anomaly_services": args.anomaly_services, "anomaly_factor": args.anomaly_factor,
+                      "anomaly_start_ms": start + 2 * step_ms})
+    paths = []
+    for p, _kind, server in gen.files():
+        d = os.path.join(root, "logs", server)
+        os.makedirs(d, exist_ok=True)
+        fp = os.path.join(d, os.path.basename(p))
+        open(fp, "wb").close()
+        paths.append(fp)
+    fds = [os.open(p, os.O_WRONLY | os.O_APPEND) for p in paths]
+    written = [0]
+
+    def append(b0, b1):
+        for b in range(b0, b1):
+            data, chunks = gen.generate(start + (b + 1) * step_ms, args.gen_threads)
+            mv = memoryview(data)
+            for fid, lo, hi in chunks:
+                os.write(fds[fid], mv[lo:hi])
+            written[0] += len(data)
+
+    g = cfg["gpu"]
+    g.update({"tailFromStart": True, "tailReadAhead": True, "tailIdleMs": 1.0, "tailReadThreads": 4,
+              "checkpointDir": None, "fleetBaseline": False})
+    ic = cfg["streamInsertDb"]
+    ic.update({"sink": args.service_sink, "copySinkDir": os.path.join(root, "spool"),
+               "encoderThreads": args.encoder_threads, "copySinkRotateBytes": 1 << 62})
+    cfg["logDir"] = os.path.join(root, "log")
+    cfg["streamParseTransactions"]["tailOffsetFileFullPath"] = os.path.join(root, "state", "tail_offsets.json")
+    cfg["streamInsertDb"]["bufferResumeFileFullPath"] = os.path.join(root, "state", "db_resume.json")
+    srv_of = lambda p: p.split("/")[-2]  # noqa: E731
+    svc = IngestService(cfg, engine="native", files=paths, rank=0, world=1, server_of_path=srv_of)
+
+    def drain():
+        while sum(o[1] for o in svc.tailer.offsets()) < written[0] or svc._held is not None:
+            if svc.step() == 0:
+                svc._idle(0.001)
+
+    append(0, 2)
+    drain()
+    svc.eng.eng.flush()
+    svc.eng.eng.warm_history(12345 + rank)
+    append(2, 2 + args.warmup)
+    drain()
+    svc.eng.eng.flush()
+    svc.inserter.flush_all()
+    append(2 + args.warmup, 2 + args.warmup + args.steps)  # the backlog the timed region consumes
+    m0 = svc.eng.metrics()
+    s0 = svc.inserter.sink_stats()
+    import torch
+    torch.cuda.synchronize()
+    if args.trace:
+        svc.eng.eng.set_trace(True)
+    pf0 = dict(svc.perf)
+    t0 = time.perf_counter()
+    drain()
+    svc.eng.eng.flush()
+    svc._drain_outputs()
+    t_engine = time.perf_counter() - t0
+    svc.inserter.flush_all()  # every row of the timed batches encoded and written
+    dt = time.perf_counter() - t0
+    m1 = svc.eng.metrics()
+    s1 = svc.inserter.sink_stats()
+    tstats = svc.tailer.stats()
+    if args.trace:
+        svc.eng.dump_trace(args.trace)
+    pf = {k: svc.perf[k] - pf0[k] for k in pf0}
+    svc.shutdown()
+    for fd in fds:
+        os.close(fd)
+    lines = m1["lines"] - m0["lines"]
+    rows = s1.get("rows", 0) - s0.get("rows", 0)
+    return {
+        "lines": lines,
+        "seconds": dt,
+        "lines_per_s": lines / dt,
+        "lines_per_s_engine_drained": lines / t_engine,
+        "db_rows_per_s": rows / dt,
+        "db_rows": rows,
+        "db_bytes": s1.get("bytes", 0) - s0.get("bytes", 0),
+        "sink": args.service_sink,
+        "sink_write_ms": s1.get("ms", 0.0) - s0.get("ms", 0.0),
+        "sink_failures": s1.get("failures", 0),
+        "tailer": {k: tstats[k] for k in ("batches", "bytes_read", "read_threads")},
+        "ingest_GB_per_s": (m1["bytes"] - m0["bytes"]) / dt / 1e9,
+        "loop": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in pf.items()},
+        "mean_batch_MB": round(pf["bytes"] / max(pf["batches"], 1) / 1e6, 3),
+    }

@@ -110,12 +110,53 @@ def copy_row(rtype: str, row: Dict[str, Any]) -> str:
     return "\t".join(copy_field(row.get(c)) for c in COLUMNS[rtype][1]) + "\n"
 
 
+def _copy_unescape(s: str) -> Optional[str]:
+    if s == "\\N":
+        return None
+    out, i = [], 0
+    while i < len(s):
+        ch = s[i]
+        if ch == "\\" and i + 1 < len(s):
+            nx = s[i + 1]
+            out.append({"t": "\t", "n": "\n", "r": "\r"}.get(nx, nx))
+            i += 2
+        else:
+            out.append(ch)
+            i += 1
+    return "".join(out)
+
+
+def pg_row_from_copy(rtype: str, row: str) -> Dict[str, Any]:
+    """A COPY text row (copy_row / the GPU's fs COPY rows) back to its row object -- for the
+    resume file when rows are still buffered at shutdown."""
+    cols = COLUMNS[rtype][1]
+    vals = [_copy_unescape(f) for f in row.rstrip("\n").split("\t")]
+    out: Dict[str, Any] = {}
+    for c, v in zip(cols, vals):
+        if v is None:
+            out[c] = None
+        elif c in _TS_COLS:
+            out[c] = _dt.datetime.strptime(v[:-3], "%Y-%m-%d %H:%M:%S.%f").replace(tzinfo=_dt.timezone.utc)
+        elif c in ("stats", "entry"):
+            out[c] = json.loads(v)
+        elif c in ("tpm", "elapsed", "acctnum") or rtype == "jx" and c not in ("server",):
+            f = float(v)
+            out[c] = int(f) if f.is_integer() and "." not in v and "e" not in v else f
+        else:
+            out[c] = v
+    return out
+
+
 def pg_row_from_line(line: str) -> Optional[Tuple[str, Dict[str, Any]]]:
     """consumeMsg (:355-376): CSV -> entry -> toPostgresObject, for tx/fs/al/jx only."""
     e = entry_from_csv(line)
     if e is None or e.type not in COLUMNS:
         return None
     return e.type, e.to_pg_row()
+
+
+def as_bool_cfg(v) -> bool:
+    return v if isinstance(v, bool) else str(v).lower() in ("1", "true", "yes", "on")
 
 
 def _native():
@@ -251,6 +292,20 @@ class PsqlWriter(Writer):
             raise RuntimeError(r.stderr.decode(errors="replace").strip())
 
 
+def native_writer_spec(ins_cfg: Dict[str, Any]) -> Optional[Tuple[str, List[str]]]:
+    """(writer kind, args) of the native DbSink for this configuration, mirroring make_writer."""
+    mode = ins_cfg.get("sink", "auto")
+    if mode == "null":
+        return "null", []
+    psql = ins_cfg.get("psqlPath") or shutil.which("psql")
+    if mode in ("auto", "psql") and psql and ins_cfg.get("dbHost"):
+        return "psql", [psql, "-X", "-q", "-v", "ON_ERROR_STOP=0", "-U", ins_cfg.get("dbUser", ""),
+                        "-h", ins_cfg["dbHost"], "-d", ins_cfg.get("dbDatabase", ""), "-f", "-"]
+    if mode == "psql":
+        raise RuntimeError("sink=psql requested but no psql client is installed")
+    return "spool", [ins_cfg.get("copySinkDir", "/tmp/apm/copy")]
+
+
 def make_writer(ins_cfg: Dict[str, Any]) -> Writer:
     mode = ins_cfg.get("sink", "auto")
     if mode == "null":
@@ -312,16 +367,20 @@ def load_resume(path: str) -> Dict[str, List[Dict[str, Any]]]:
 # --------------------------------------------------------------------------- inserter
 
 class DBInserter:
-    """The consumer side of ``db_insert`` (one per node, or one per rank)."""
+    """The consumer side of ``db_insert`` (one per node, or one per rank).
+
+    With the configured writers (spool / psql / null) the buffering, COPY encoding and loading
+    run in the native ``DbSink`` (csrc/runtime/dbsink.cpp: per-type buffers, encoder thread pool,
+    one ordered writer thread, a persistent psql process); the Python path below serves custom
+    ``Writer`` objects (tests, embedding) and is the reference definition of the semantics."""
 
     def __init__(self, cfg: Dict[str, Any], writer: Optional[Writer] = None,
                  clock: Callable[[], float] = time.monotonic, stats: Optional[DBStats] = None):
         ic = cfg["streamInsertDb"]
         self.cfg = cfg
-        self.limit = int(ic.get("dbInsertBufferLimit", 1000))
-        self.max_wait_s = float(ic.get("dbMaxTimeBetweenInsertsMs", 5000)) / 1000.0
+        self._limit = int(ic.get("dbInsertBufferLimit", 1000))
+        self._max_wait_s = float(ic.get("dbMaxTimeBetweenInsertsMs", 5000)) / 1000.0
         self.tables = {t: ic.get(key, t) for t, (key, _cols) in COLUMNS.items()}
-        self.writer = writer if writer is not None else make_writer(ic)
         self.clock = clock
         self.stats = stats or DBStats(float(cfg.get("statLogIntervalInSeconds", 60)))
         self.buffers: Dict[str, Deque[Dict[str, Any]]] = {t: deque() for t in TYPES}
@@ -329,12 +388,94 @@ class DBInserter:
         self.failures = 0
         self.native = bool(ic.get("nativeCopyEncoder", True))
         self.resume_path = ic.get("bufferResumeFileFullPath")
+        self.core = None
+        self.gpu_fs_copy = as_bool_cfg(ic.get("gpuFsCopyRows", True))
+        self._writer: Optional[Writer] = writer
+        if writer is None:
+            N = _native() if as_bool_cfg(ic.get("nativeSink", True)) else None
+            if N is not None and hasattr(N, "DbSink"):
+                kind, args = native_writer_spec(ic)
+                self.core = N.DbSink(self._limit, self._max_wait_s * 1000.0, [self.tables[t] for t in TYPES],
+                                     [", ".join(COLUMNS[t][1]) for t in TYPES], kind, args,
+                                     int(ic.get("copySinkRotateBytes", 1 << 30)), int(ic.get("encoderThreads", 2)))
+            else:
+                self._writer = make_writer(ic)
         if self.resume_path:
             for t, rows in load_resume(self.resume_path).items():
-                if t in self.buffers:
-                    self.buffers[t].extend(rows)
-                    if rows:
+                if t in self.buffers and rows:
+                    if self.core is not None:
+                        self.core.add_encoded(TYPES.index(t), "".join(copy_row(t, r) for r in rows).encode("utf-8"),
+                                              len(rows))
+                    else:
+                        self.buffers[t].extend(rows)
                         self.deadline[t] = self.clock() + self.max_wait_s
+
+    # -- configuration (hot reload) and writer injection
+    @property
+    def limit(self) -> int:
+        return self._limit
+
+    @limit.setter
+    def limit(self, v: int):
+        self._limit = int(v)
+        if self.core is not None:
+            self.core.set_limit(self._limit, self._max_wait_s * 1000.0)
+
+    @property
+    def max_wait_s(self) -> float:
+        return self._max_wait_s
+
+    @max_wait_s.setter
+    def max_wait_s(self, v: float):
+        self._max_wait_s = float(v)
+        if self.core is not None:
+            self.core.set_limit(self._limit, self._max_wait_s * 1000.0)
+
+    @property
+    def writer(self) -> Optional[Writer]:
+        return self._writer
+
+    def attach_engine(self, native_engine, kinds: Sequence[str]) -> bool:
+        """Let the engine's output lane hand ``kinds`` straight to the native sink (no Python,
+        no extra copy).  Returns False on the Python path."""
+        if self.core is None:
+            return False
+        N = _native()
+        fs_copy = "fs" in kinds and self.gpu_fs_copy
+        for k in kinds:
+            if k == "fs" and fs_copy:
+                # K12 formats the fs rows as COPY text on the GPU; the sink writes them as is
+                native_engine.set_fs_copy(True)
+                N.attach_sink(native_engine, k, self.core, TYPES.index("fs"))
+            else:
+                N.attach_sink(native_engine, k, self.core)
+        self._attached = (native_engine, list(kinds), fs_copy)
+        return True
+
+    def _detach(self):
+        att = getattr(self, "_attached", None)
+        if att:
+            N = _native()
+            for k in att[1]:
+                N.detach_sink(att[0], k)
+            if att[2]:
+                att[0].set_fs_copy(False)
+            self._attached = None
+
+    @writer.setter
+    def writer(self, w: Writer):
+        """Injecting a Python writer switches to the Python path (anything the native sink still
+        buffers is handed over first)."""
+        self._detach()
+        if self.core is not None:
+            enc = [self.core.is_encoded(i) for i in range(len(TYPES))]
+            left = self.core.close()
+            self.core = None
+            for t, blob, e in zip(TYPES, left, enc):
+                for ln in blob.decode("utf-8").split("\n"):
+                    if ln:
+                        self._add(t, pg_row_from_copy(t, ln) if e else ln)
+        self._writer = w
 
     # -- ingest: buffers hold wire lines (encoded in bulk at flush) or row dicts (resumed)
     def _add(self, rtype: str, item):
@@ -349,6 +490,8 @@ class DBInserter:
         self._add(rtype, row)
 
     def consume_line(self, line: str) -> bool:
+        if self.core is not None:
+            return self.core.consume((line + "\n").encode("utf-8")) > 0
         t = line[:3]
         if len(line) < 3 or t[2] != "|" or t[:2] not in self.buffers:
             if line:
@@ -358,6 +501,8 @@ class DBInserter:
         return True
 
     def consume_bytes(self, blob: bytes) -> int:
+        if self.core is not None:
+            return self.core.consume(blob)
         n = 0
         for ln in blob.decode("utf-8").split("\n"):
             if ln:
@@ -404,6 +549,9 @@ class DBInserter:
 
     def tick(self) -> int:
         """Timer half of the reference's setTimeout per buffer."""
+        if self.core is not None:
+            self._sync_stats()
+            return self.core.tick()
         now = self.clock()
         n = 0
         for t in TYPES:
@@ -416,11 +564,38 @@ class DBInserter:
         return n
 
     def flush_all(self) -> int:
+        if self.core is not None:
+            before = self.core.stats()["rows"]
+            self.core.flush_all()
+            self.core.drain()
+            self._sync_stats()
+            return self.core.stats()["rows"] - before
         return sum(self.flush(t) for t in TYPES)
 
+    def _sync_stats(self):
+        rows, ms = self.core.take_interval()
+        if rows or ms:
+            self.stats.add(rows, ms)
+        self.failures = self.core.stats()["failures"]
+
+    def sink_stats(self) -> Dict[str, Any]:
+        return dict(self.core.stats()) if self.core is not None else {"rows": self.stats.total_rows,
+                                                                      "failures": self.failures}
+
     def close(self):
-        self.flush_all()
+        self._detach()
+        if self.core is not None:
+            enc = [self.core.is_encoded(i) for i in range(len(TYPES))]
+            left = self.core.close()
+            self._sync_stats()
+            self.core = None
+            for t, blob, e in zip(TYPES, left, enc):
+                self.buffers[t].extend((pg_row_from_copy(t, ln) if e else ln)
+                                       for ln in blob.decode("utf-8").split("\n") if ln)
+        else:
+            self.flush_all()
         if self.resume_path:
             rows = {t: [r if isinstance(r, dict) else pg_row_from_line(r)[1] for r in b] for t, b in self.buffers.items()}
             save_resume(self.resume_path, rows)
-        self.writer.close()
+        if self._writer is not None:
+            self._writer.close()

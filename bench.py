@@ -78,6 +78,12 @@ def main():
                          "JVM from the first batch after the history warm-up (the bench's al rows)")
     ap.add_argument("--anomaly-factor", type=float, default=25.0)
     ap.add_argument("--trace", default=None, help="write a Chrome trace of the pipeline stages (per rank)")
+    ap.add_argument("--path", default="memory", choices=["memory", "service"],
+                    help="memory: the headline (engine fed from pinned memory); service: the production path "
+                         "(log files -> tailer read-ahead -> engine -> native COPY sink), 1 GPU")
+    ap.add_argument("--service-dir", default=None, help="--path service: where the log files / spool go")
+    ap.add_argument("--service-sink", default="spool", choices=["spool", "null"])
+    ap.add_argument("--encoder-threads", type=int, default=8)
     args = ap.parse_args()
     for k, v in PRESETS[args.preset].items():  # a preset overrides the defaults it names
         if getattr(args, k) == ap.get_default(k):
@@ -110,6 +116,24 @@ def main():
         "ringDtype": args.ring,
         "bucketCellCapacity": 16,
     })
+    if args.path == "service":
+        from apmbackend_amd.runtime import service_bench
+        r = service_bench.run(args, cfg, N, rank)
+        if rank == 0:
+            ref = _load_reference_baseline()
+            print(json.dumps({
+                "metric": "log-lines/sec z-scored (whole node), production service path",
+                "value": round(r["lines_per_s"], 1), "unit": "lines/s", "n_gpus": 1, "steps": args.steps,
+                "warmup": args.warmup, "higher_is_better": True, "scaling": "weak",
+                "vs_baseline": round(r["lines_per_s"] / ref, 2) if ref else None,
+                "dtype": {"float64": "fp64", "float32": "fp32", "bfloat16": "bf16"}[args.ring],
+                "data": "synthetic WildFly logs written to real files (native generator, seeded)",
+                "config": {"model": f"tail->parse->join->stats->zscore(LAG 360,8640)->alerts->COPY sink, "
+                                    f"{n_services} services, {args.servers} JVMs/GPU", "preset": args.preset,
+                           "ring_dtype": args.ring, "sink": args.service_sink},
+                "service": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()},
+            }), flush=True)
+        return
     # Materialise exactly what the reference hands to its db_insert stage (released + audit tx,
     # fs, al) in the wire format and write it to a sink (/dev/null: the DB loader is out of scope).
     from apmbackend_amd.models.pipeline import DB_OUTPUTS

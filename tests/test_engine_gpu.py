@@ -543,3 +543,37 @@ def test_incremental_checkpoint_chain_resume(tmp_path, mode):
             out[k] += eng2.take(k)
     for k in ("transactions", "audit_db", "st", "fs", "al"):
         assert out[k] == full[k], k
+
+
+def test_host_join_tx_staging_grows_instead_of_failing():
+    """Host-join mode with a tiny per-batch tx staging: the engine doubles it mid-batch (was: a
+    'too many tx in one batch' exception) and the output is unchanged."""
+    lines, bl = synth_batches(1, duration=600)
+    C = small_cfg("exact")
+    C["gpu"]["joinOnDevice"] = False
+    P = PipelineOracle(copy.deepcopy(C), UTC)
+    P.run_batches(bl)
+    C["gpu"]["maxTxPerBatch"] = 16
+    eng, out = _run_engine(C, bl)
+    assert out["transactions"] == P.tx_out
+    assert out["st"] == P.stats and out["fs"] == P.fs
+    assert eng.metrics()["tx_capacity_grows"] > 0
+
+
+def test_fs_copy_rows_on_gpu_match_host_encoder():
+    """K12 in COPY mode (the DB sink's row encoding fused into the GPU formatter): every fs row
+    equals what the host COPY encoder (copyenc.cpp / sinks.copy_encode_lines) makes of the wire
+    line -- numbers re-printed JS-style, NaN -> null, names COPY-escaped."""
+    from apmbackend_amd.runtime import sinks
+    lines, bl = synth_batches(3, duration=700)
+    C = small_cfg("exact")
+    _, wire = _run_engine(C, bl)
+    eng = APMEngine(C, keep_text=True)
+    eng.eng.set_fs_copy(True)
+    got = []
+    for now, chunks in bl:
+        eng.process_lines(chunks, now)
+        got += eng.take("fs")
+    want = [r.rstrip("\n") for r in sinks.copy_encode_lines(wire["fs"])["fs"]]
+    assert len(want) > 100 and got == want
+    assert any("null" in r for r in got)  # undefined window stats

@@ -1,4 +1,6 @@
 """DB insert stage (runtime/sinks.py) against the reference's stream_insert_db.js behaviour."""
+import os
+import time
 import datetime as dt
 import json
 
@@ -179,3 +181,95 @@ def test_inserter_native_and_python_paths_agree(tmp_path):
         ins.flush_all()
         outs.append(sorted((c[0], tuple(c[2])) for c in w.calls))
     assert outs[0] == outs[1] and len(outs[0]) >= 3
+
+
+# ----------------------------------------------------------------------------- native DbSink
+
+def _wire_lines(n=40):
+    from apmbackend_amd.utils.records import StatEntry, TxEntry
+    out = []
+    for i in range(n):
+        out.append(TxEntry("srv", f"S:svc{i % 3}", f"LOG{i}", "1234", 1578391200000 + i, 1578391200100 + i,
+                           str(100 + i), "Y").to_csv())
+        out.append(f"fs|{1578391200000 + i}|srv|S:svc{i % 3}|12.50|6|100.0:99.5:90.1:110.2:0|"
+                   f"120.0:119.0:100.0:130.0:1|150.0:149.0:140.0:160.0:0")
+    out.append("junk line")
+    return out
+
+
+def _native_ok():
+    N = sinks._native()
+    return N is not None and hasattr(N, "DbSink")
+
+
+@pytest.mark.skipif(not _native_ok(), reason="native extension not built")
+def test_native_sink_spool_matches_python_encoder(tmp_path):
+    lines = _wire_lines()
+    C = cfg(limit=7)
+    C["streamInsertDb"].update({"sink": "spool", "copySinkDir": str(tmp_path / "spool")})
+    ins = sinks.DBInserter(C, clock=Clock())
+    assert ins.core is not None
+    assert ins.consume_bytes(("\n".join(lines) + "\n").encode()) == len(lines) - 1
+    ins.close()
+    want = sinks.copy_encode_lines(lines)
+    for t in ("tx", "fs"):
+        table = C["streamInsertDb"][sinks.COLUMNS[t][0]]
+        got = open(tmp_path / "spool" / f"{table}.copy").read()
+        assert got == "".join(want[t])
+        assert open(tmp_path / "spool" / f"{table}.columns").read().strip() == ", ".join(sinks.COLUMNS[t][1])
+    assert ins.stats.total_rows == len(lines) - 1
+
+
+@pytest.mark.skipif(not _native_ok(), reason="native extension not built")
+def test_native_sink_limit_and_timer_semantics():
+    from apmbackend_amd import _native
+    N = _native.load(build_if_missing=False)
+    s = N.DbSink(3, 50.0, ["t_tx", "t_fs", "t_al", "t_jx"], ["a", "b", "c", "d"], "null", [], 0, 1)
+    tx = [l for l in _wire_lines() if l.startswith("tx|")][:7]
+    s.consume(("\n".join(tx) + "\n").encode())
+    s.drain()
+    st = s.stats()
+    # flushed before the 4th and 7th rows were appended: 2 flushes x 3 rows, 1 row buffered
+    assert st["flushes"] == 2 and st["rows"] == 6 and st["buffered"] == 1
+    assert s.tick() == 0  # deadline not reached yet
+    time.sleep(0.08)
+    assert s.tick() == 1
+    s.drain()
+    assert s.stats()["rows"] == 7 and s.stats()["buffered"] == 0
+    assert s.close() == [b"", b"", b"", b""]
+
+
+@pytest.mark.skipif(not _native_ok(), reason="native extension not built")
+def test_native_sink_persistent_psql_copy_and_rebuffer(tmp_path, monkeypatch):
+    """One long-lived psql process, one acknowledged COPY per flush; a failed COPY puts its rows
+    back at the front of the buffer and they go out with the next flush once the table works."""
+    import sys
+    out = tmp_path / "pg"
+    out.mkdir()
+    monkeypatch.setenv("FAKE_PSQL_OUT", str(out))
+    monkeypatch.setenv("FAKE_PSQL_FAIL", "apm_stats")
+    from apmbackend_amd import _native
+    N = _native.load(build_if_missing=False)
+    fake = [sys.executable, os.path.join(os.path.dirname(__file__), "fixtures", "fake_psql.py")]
+    s = N.DbSink(1000, 1e9, ["apm_tx", "apm_stats", "apm_alerts", "apm_jmx"], ["a", "b", "c", "d"], "psql", fake, 0, 2)
+    lines = _wire_lines(10)
+    s.consume(("\n".join(lines) + "\n").encode())
+    s.flush_all()
+    s.drain()
+    st = s.stats()
+    assert st["rows"] == 10 and st["failures"] == 1 and st["buffered"] == 10  # fs rows re-buffered
+    assert "apm_stats" in st["last_error"]
+    want = sinks.copy_encode_lines(lines)
+    assert open(out / "apm_tx.rows").read() == "".join(want["tx"])
+    monkeypatch.setenv("FAKE_PSQL_FAIL", "")  # the running psql keeps failing that table...
+    left = s.close()
+    assert left[1].count(b"\n") == 10  # ...so close() hands the rows back (resume file)
+    assert left[0] == b""
+
+
+def test_copy_rows_parse_back_for_the_resume_file():
+    lines = _wire_lines(6)
+    enc = sinks.copy_encode_lines(lines)
+    for t in ("tx", "fs"):
+        for row in enc[t]:
+            assert sinks.copy_row(t, sinks.pg_row_from_copy(t, row)) == row
