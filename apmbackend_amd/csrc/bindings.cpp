@@ -68,6 +68,7 @@ EngineConfig config_from(const py::dict& d) {
   c.exact_mean = get<int>(d, "exact_mean", c.exact_mean);
   c.sigma_stddev = get<int>(d, "sigma_stddev", c.sigma_stddev);
   c.resync_k = get<int>(d, "resync_k", c.resync_k);
+  c.resync_mfma = get<bool>(d, "resync_mfma", c.resync_mfma);
   c.emulate_aliasing = get<int>(d, "emulate_aliasing", c.emulate_aliasing);
   if (d.contains("lags")) {
     auto lags = d["lags"].cast<std::vector<std::tuple<int, double, double>>>();
@@ -401,6 +402,13 @@ PYBIND11_MODULE(_apm_native, m) {
         return py::bytes((const char*)v.data(), v.size() * 8);
       })
       .def("fleet_rounds", &Engine::fleet_rounds)
+      .def("fleet_slot_names", [](Engine& e) { return e.fleet_slot_names(); })
+      .def("fleet_info", [](Engine& e) {
+        py::dict d;
+        const auto i = e.fleet_info();
+        d["slots"] = i[0]; d["registry_rounds"] = i[1]; d["registry_overflow"] = i[2]; d["fb_rows"] = i[3];
+        return d;
+      })
       .def("fleet_init_local", [](Engine& e, std::shared_ptr<LocalGroup> g, int rank, int32_t cap, bool lockstep) {
         py::gil_scoped_release rel;
         e.fleet_init_local(std::move(g), rank, cap, lockstep);
@@ -433,15 +441,15 @@ PYBIND11_MODULE(_apm_native, m) {
   m.def("copy_encode", [](py::bytes blob) {
     // wire lines -> Postgres COPY text per table type (runtime/sinks.py is the Python twin)
     std::string b = blob;
-    std::string out[4];
-    int64_t counts[4] = {0, 0, 0, 0};
+    std::string out[5];
+    int64_t counts[5] = {0, 0, 0, 0, 0};
     {
       py::gil_scoped_release rel;
       copyenc::encode_blob(b, out, counts);
     }
     py::dict d;
-    const char* names[4] = {"tx", "fs", "al", "jx"};
-    for (int k = 0; k < 4; ++k) d[names[k]] = py::make_tuple(py::bytes(out[k]), counts[k]);
+    const char* names[5] = {"tx", "fs", "al", "jx", "fb"};
+    for (int k = 0; k < 5; ++k) d[names[k]] = py::make_tuple(py::bytes(out[k]), counts[k]);
     return d;
   });
   m.def("flatmap_selftest", [](int n_ops, uint64_t seed, int key_space) {

@@ -287,6 +287,74 @@ __global__ __launch_bounds__(FMT_WAVE_SERIES) void k_format_write(FormatArgs a) 
   if (fs_lds) wave_copy_out(sfs, a.fs_out, fs0, fs1);
 }
 
+// ---- fb: fleet baseline rows ------------------------------------------------------------
+// wire: fb|<edge_ts>|<service>|<lag>|<n>|<avg mean>:<avg std>|<p75 mean>:<p75 std>|<p95 mean>:<p95 std>
+// COPY: <ts>\t<service>\t<lag>\t<n>\t{"averagemean":..,"averagestd":..,"per75mean":..,...}
+// mean / std: of the series' z-score baseline means across the fleet (population std).
+template <bool WRITE>
+__device__ void fleet_row(const FleetFormatArgs& a, int32_t i, char* dst, uint32_t* len, bool& fb) {
+  const int32_t slot = i / a.n_lags, li = i % a.n_lags;
+  const int l = a.lag_order[li];
+  const double* m = a.moments + ((size_t)slot * a.n_lags + l) * NSTAT * 3;
+  Out o{WRITE ? dst : nullptr};
+  const double n0 = m[0];
+  if (n0 > 0) {
+    const int2 nm = a.names[slot];
+    double mean[NSTAT], sd[NSTAT];
+    for (int k = 0; k < NSTAT; ++k) {
+      const double n = m[k * 3 + 0];
+      if (n > 0) {
+        mean[k] = m[k * 3 + 1] / n;
+        sd[k] = sqrt(fmax(m[k * 3 + 2] / n - mean[k] * mean[k], 0.0));
+      } else {
+        mean[k] = sd[k] = apm_nan();
+      }
+    }
+    if (a.copy) {
+      o.s(a.ts, a.ts_len); o.c('\t');
+      o.copy_text(a.chars + nm.x, nm.y); o.c('\t');
+      o.u((uint64_t)a.lag_value[l]); o.c('\t');
+      o.u((uint64_t)n0); o.c('\t');
+      const char* key[NSTAT] = {"average", "per75", "per95"};
+      const int kl[NSTAT] = {7, 5, 5};
+      o.c('{');
+      for (int k = 0; k < NSTAT; ++k) {
+        if (k) o.c(',');
+        o.c('"'); o.s(key[k], kl[k]); o.s("mean\":", 6); o.js_fixed(mean[k], 1, true, fb);
+        o.s(",\"", 2); o.s(key[k], kl[k]); o.s("std\":", 5); o.js_fixed(sd[k], 1, true, fb);
+      }
+      o.c('}');
+    } else {
+      o.s("fb|", 3); o.i64(a.edge_ts); o.c('|');
+      o.s(a.chars + nm.x, nm.y); o.c('|');
+      o.u((uint64_t)a.lag_value[l]); o.c('|');
+      o.u((uint64_t)n0);
+      for (int k = 0; k < NSTAT; ++k) {
+        o.c('|'); o.fixed(mean[k], 1, fb); o.c(':'); o.fixed(sd[k], 1, fb);
+      }
+    }
+    o.c('\n');
+  }
+  if (!WRITE) len[i] = o.n;
+}
+
+__global__ __launch_bounds__(256) void k_fleet_len(FleetFormatArgs a) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int32_t n = a.n_slots * a.n_lags;
+  if (i == n) { a.len[n] = 0; return; }
+  if (i > n) return;
+  bool fb = false;
+  fleet_row<false>(a, i, nullptr, a.len, fb);
+  if (fb) atomicAdd(a.fallback, 1);
+}
+
+__global__ __launch_bounds__(256) void k_fleet_write(FleetFormatArgs a) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n_slots * a.n_lags) return;
+  bool fb = false;
+  fleet_row<true>(a, i, a.out + a.off[i], nullptr, fb);
+}
+
 __global__ void k_fixed_batch(const double* x, int n, int f, char* out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -330,6 +398,21 @@ int apm_format_plan(FormatArgs* a, void* tmp, size_t tmp_bytes, hipStream_t stre
 // Test hook: nf(x[i], f) into 32-byte NUL-terminated slots.
 void apm_format_fixed_batch(const double* d_x, int n, int f, char* d_out, hipStream_t stream) {
   if (n > 0) hipLaunchKernelGGL(k_fixed_batch, dim3((n + 255) / 256), dim3(256), 0, stream, d_x, n, f, d_out);
+}
+
+size_t apm_fleet_format_tmp_bytes(int32_t n_rows) { return apm_format_tmp_bytes(n_rows); }
+
+// lengths + scan + write; afterwards off[n_rows] holds the total bytes (device)
+int apm_fleet_format(FleetFormatArgs* a, void* tmp, size_t tmp_bytes, hipStream_t stream) {
+  const int32_t n = a->n_slots * a->n_lags;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_fleet_len, dim3((n + 1 + 255) / 256), dim3(256), 0, stream, *a);
+  size_t need = tmp_bytes;
+  if (rocprim::exclusive_scan(tmp, need, a->len, a->off, 0u, (size_t)n + 1, rocprim::plus<uint32_t>(), stream) !=
+      hipSuccess)
+    return -1;
+  hipLaunchKernelGGL(k_fleet_write, dim3((n + 255) / 256), dim3(256), 0, stream, *a);
+  return 0;
 }
 
 void apm_format_write(FormatArgs* a, hipStream_t stream) {

@@ -67,6 +67,7 @@ struct ZArgs {
   int64_t rollover_idx;
   // rolling-mode resync range of this rollover (host computes it; rs_n = 0 -> none)
   int32_t rs_lo, rs_n, rs_parts;
+  int32_t rs_mfma;         // 1: window re-sum as MFMA tile reductions (k_zscore_resync_mfma)
   double* rs_part;         // [NSTAT][rs_parts][rs_n][4] partial (sum, comp, sumsq, sqcomp)
   int32_t* rs_cnt;         // [NSTAT][rs_parts][rs_n]
 };
@@ -109,6 +110,24 @@ struct FormatArgs {
   char ts_copy[32];        // edge_ts as 'YYYY-MM-DD HH:MM:SS.mmm+00'
   uint32_t *st_len, *fs_len, *st_off, *fs_off;  // [n + 1]
   char *st_out, *fs_out;
+  int32_t* fallback;
+};
+
+// fb rows: the fleet-merged per-service baseline (all ranks' series of a service), one row per
+// (service slot, LAG) with a baseline, after the moments all-reduce (format.hip)
+struct FleetFormatArgs {
+  const double* moments;   // [cap][n_lags][NSTAT][3] {n, sum of means, sum of squared means}
+  const int2* names;       // [n_slots] {offset, length} into chars
+  const char* chars;
+  int32_t n_slots, n_lags;
+  int32_t lag_order[MAX_LAGS], lag_value[MAX_LAGS];
+  int64_t edge_ts;
+  int32_t copy;            // 1: Postgres COPY rows (apm_fleet_stats), 0: fb wire lines
+  int32_t ts_len;
+  char ts[32];
+  uint32_t* len;           // [n_slots * n_lags + 1]
+  uint32_t* off;
+  char* out;
   int32_t* fallback;
 };
 
@@ -166,6 +185,8 @@ void apm_format_fixed_batch(const double* d_x, int n, int f, char* d_out, hipStr
 int apm_format_plan(apm::FormatArgs* a, void* tmp, size_t tmp_bytes, hipStream_t stream);
 void apm_format_write(apm::FormatArgs* a, hipStream_t stream);
 void apm_alert_eval(apm::AlertArgs* a, hipStream_t stream);
+size_t apm_fleet_format_tmp_bytes(int32_t n_rows);
+int apm_fleet_format(apm::FleetFormatArgs* a, void* tmp, size_t tmp_bytes, hipStream_t stream);
 // rows of the alert candidates (window stats + the candidate LAG's z-score output), compacted in
 // candidate order: the host formats al rows from n records instead of downloading every series
 void apm_alert_gather(const apm::AlertRec* alerts, int32_t n, const apm::WinStat* win, const apm::ZOut* const* z_by_lag,

@@ -78,6 +78,74 @@ __global__ __launch_bounds__(256) void k_zscore_resync(ZArgs a) {
   a.rs_cnt[o] = c;
 }
 
+// The same partial sums on the matrix cores.  A wave owns 16 consecutive series x one partition
+// and walks the partition's window positions two at a time; each step is one
+// v_mfma_f64_16x16x4f64 with
+//   A[i][k] (16 series x 4):  k=0: v(i, pos), k=1: v(i, pos+1), k=2: v(i, pos)^2, k=3: v(i, pos+1)^2
+//   B[k][j] (4 x 16, const):  column 0 = (1,1,0,0), column 1 = (0,0,1,1), other columns 0
+// so C[i][0] accumulates the window sum and C[i][1] the sum of squares of series i: a masked
+// ones-matrix tile reduction over the [LAG x series] ring slab (values outside a series' window
+// and NaN entries enter as 0 and are not counted).  The accumulation is plain fp64 in the matrix
+// core (no Neumaier term: partial comp = 0), which is what rolling mode's periodic resync needs.
+// Grid: (ceil(rs_n / 16), ceil(P / 4), NSTAT), 4 waves per block (one partition each).
+typedef double apm_f64x4z __attribute__((ext_vector_type(4)));
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_zscore_resync_mfma(ZArgs a) {
+  __shared__ double g[4][16][3];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int i16 = lane & 15, kk = lane >> 4;       // A operand: series i16, column kk
+  const int j = blockIdx.x * 16 + i16;
+  const int p = blockIdx.y * 4 + wave;
+  const int k = blockIdx.z;
+  const int L = a.lag, S = a.S;
+  const bool part_ok = p < a.rs_parts;             // uniform per wave
+  const int s = a.rs_lo + j;
+  const bool ser_ok = j < a.rs_n && s < a.n_series;
+  const int n = ser_ok ? a.len[s] : 0;
+  const int per = (L + a.rs_parts - 1) / a.rs_parts;
+  const int i0 = p * per;
+  const int oldest = (a.head - n + L) % L;
+  const T* col = reinterpret_cast<const T*>(a.ring) + (size_t)k * L * S + (ser_ok ? s : 0);
+  const int which = kk & 1;                         // pos or pos + 1
+  const bool square = kk >= 2;
+  const double bval = (i16 == 0 && kk < 2) || (i16 == 1 && kk >= 2) ? 1.0 : 0.0;  // B[kk][i16]
+  apm_f64x4z acc = {0.0, 0.0, 0.0, 0.0};
+  int cnt = 0;
+  if (part_ok) {
+    for (int i = i0; i < i0 + per && i < L; i += 2) {  // uniform bounds across the wave
+      const int wi = i + which;
+      double v = 0.0;
+      if (ser_ok && wi < i0 + per && wi < n) {
+        int pos = oldest + wi;
+        if (pos >= L) pos -= L;
+        const double x = ld(col + (size_t)pos * S);
+        if (valid(x)) {
+          v = square ? x * x : x;
+          if (!square) ++cnt;
+        }
+      }
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v, bval, acc, 0, 0, 0);
+    }
+  }
+  // counts: lanes kk = 0, 1 of series i16 (lanes i16 and i16 + 16)
+  cnt += __shfl_down(cnt, 16, 64);
+  // D[row][col]: lane l, accumulator r holds row 4 r + l / 16, column l % 16
+  if (i16 < 2)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) g[wave][4 * r + kk][i16] = acc[r];
+  if (kk == 0) g[wave][i16][2] = (double)cnt;
+  __syncthreads();
+  if (part_ok && kk == 0 && j < a.rs_n) {
+    const size_t o = ((size_t)k * a.rs_parts + p) * a.rs_n + j;
+    a.rs_part[o * 4 + 0] = g[wave][i16][0];
+    a.rs_part[o * 4 + 1] = 0.0;
+    a.rs_part[o * 4 + 2] = g[wave][i16][1];
+    a.rs_part[o * 4 + 3] = 0.0;
+    a.rs_cnt[o] = (int)g[wave][i16][2];
+  }
+}
+
 // One thread per (series, stat): grid (ceil(n/256), NSTAT).  The three stats of a series are
 // independent recurrences, and a thread per series left ~1.2 waves per SIMD at 80k series --
 // too few to hide the HBM latency of its five moment loads + ring row per stat (73 us per LAG
@@ -272,8 +340,13 @@ namespace apm {
 template <typename T>
 void launch_zscore(ZArgs* a, hipStream_t stream) {
   if (!a->exact && a->rs_n > 0) {
-    const dim3 g((a->rs_n + 63) / 64, (a->rs_parts + 3) / 4, NSTAT), b(64, 4);
-    hipLaunchKernelGGL(k_zscore_resync<T>, g, b, 0, stream, *a);
+    if (a->rs_mfma) {
+      const dim3 g((a->rs_n + 15) / 16, (a->rs_parts + 3) / 4, NSTAT);
+      hipLaunchKernelGGL(k_zscore_resync_mfma<T>, g, dim3(256), 0, stream, *a);
+    } else {
+      const dim3 g((a->rs_n + 63) / 64, (a->rs_parts + 3) / 4, NSTAT), b(64, 4);
+      hipLaunchKernelGGL(k_zscore_resync<T>, g, b, 0, stream, *a);
+    }
   }
   hipLaunchKernelGGL(k_zscore<T>, dim3((a->n_series + 255) / 256, NSTAT), dim3(256), 0, stream, *a);
   hipLaunchKernelGGL(k_zscore_commit<T>, dim3((a->n_series + 255) / 256), dim3(256), 0, stream, *a);

@@ -198,8 +198,8 @@ void fs_row_json(std::string& out, const Fields& a) {
 
 }  // namespace
 
-// Returns the type index (0 tx, 1 fs, 2 al, 3 jx) the row was appended to, or -1.
-int encode_line(std::string_view line, std::string* out /*[4]*/) {
+// Returns the type index (0 tx, 1 fs, 2 al, 3 jx, 4 fb) the row was appended to, or -1.
+int encode_line(std::string_view line, std::string* out /*[5]*/) {
   Fields a;
   split(line, '|', a);
   const std::string_view t = a.f[0];
@@ -242,6 +242,30 @@ int encode_line(std::string_view line, std::string* out /*[4]*/) {
     copy_escape(o, js);
     o += '\n';
     return 2;
+  }
+  if (t == "fb") {  // fleet baseline: timestamp, service, lag, nseries, stats json
+    std::string& o = out[4];
+    c_ts(o, a, 1); o += '\t';
+    c_str(o, a, 2); o += '\t';
+    c_str(o, a, 3); o += '\t';
+    c_num(o, a.has(4) ? js::parse_int(a.f[4]) : js::nan()); o += '\t';
+    static const char* names[3] = {"average", "per75", "per95"};
+    std::string js = "{";
+    for (int k = 0; k < 3; ++k) {
+      Fields p;
+      if (a.has(5 + k)) split(a.f[5 + k], ':', p);
+      for (int j = 0; j < 2; ++j) {
+        if (k || j) js += ',';
+        js += '"';
+        js += names[k];
+        js += j ? "std\":" : "mean\":";
+        j_num(js, p.has(j) ? parse_float(p.f[j]) : js::nan());
+      }
+    }
+    js += '}';
+    copy_escape(o, js);
+    o += '\n';
+    return 4;
   }
   if (t == "jx") {
     std::string& o = out[3];

@@ -49,6 +49,8 @@ void encode_blob(std::string_view blob, std::string* out, int64_t* counts);
 
 namespace {
 
+constexpr int NT = 5;  // tx, fs, al, jx, fb
+
 double mono_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -60,6 +62,7 @@ int type_of(std::string_view line) {
   if (a == 'f' && b == 's') return 1;
   if (a == 'a' && b == 'l') return 2;
   if (a == 'j' && b == 'x') return 3;
+  if (a == 'f' && b == 'b') return 4;
   return -1;
 }
 
@@ -91,8 +94,8 @@ struct NullWriter : Writer {
 struct SpoolWriter : Writer {
   std::string dir;
   uint64_t rotate;
-  int fd[4] = {-1, -1, -1, -1};
-  uint64_t size[4] = {0, 0, 0, 0};
+  int fd[NT] = {-1, -1, -1, -1, -1};
+  uint64_t size[NT] = {0, 0, 0, 0, 0};
   SpoolWriter(std::string d, uint64_t r) : dir(std::move(d)), rotate(r) {
     ::mkdir(dir.c_str(), 0755);
   }
@@ -220,7 +223,7 @@ class DbSink : public ByteSink {
          const std::string& writer, const std::vector<std::string>& arg, uint64_t rotate_bytes, int encoders)
       : limit_(std::max<int64_t>(1, limit)), max_wait_ms_(max_wait_ms), tables_(std::move(tables)),
         columns_(std::move(columns)) {
-    if (tables_.size() != 4 || columns_.size() != 4) throw std::runtime_error("DbSink: 4 tables / column lists");
+    if (tables_.size() != NT || columns_.size() != NT) throw std::runtime_error("DbSink: 5 tables / column lists");
     if (writer == "null") w_.reset(new NullWriter());
     else if (writer == "spool") w_.reset(new SpoolWriter(arg.at(0), rotate_bytes));
     else if (writer == "psql") w_.reset(new PsqlWriter(arg, 120000.0));
@@ -312,14 +315,14 @@ class DbSink : public ByteSink {
     const double now = mono_ms();
     int k = 0;
     std::lock_guard<std::mutex> lk(mu_);
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < NT; ++t)
       if (buf_[t].n > 0 && now >= buf_[t].deadline) { submit_locked(t); ++k; }
     return k;
   }
 
   void flush_all() {
     std::lock_guard<std::mutex> lk(mu_);
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < NT; ++t)
       if (buf_[t].n > 0) submit_locked(t);
   }
 
@@ -335,8 +338,8 @@ class DbSink : public ByteSink {
     flush_all();
     drain();
     shutdown();
-    std::vector<std::string> left(4);
-    for (int t = 0; t < 4; ++t) left[t] = buf_[t].lines;
+    std::vector<std::string> left(NT);
+    for (int t = 0; t < NT; ++t) left[t] = buf_[t].lines;
     return left;
   }
 
@@ -428,8 +431,8 @@ class DbSink : public ByteSink {
         j = to_encode_.front();
         to_encode_.pop_front();
       }
-      std::string out[4];
-      int64_t counts[4] = {0, 0, 0, 0};
+      std::string out[NT];
+      int64_t counts[NT] = {0, 0, 0, 0, 0};
       copyenc::encode_blob(j->lines, out, counts);
       {
         std::lock_guard<std::mutex> lk(mu_);
@@ -494,8 +497,8 @@ class DbSink : public ByteSink {
   std::unique_ptr<Writer> w_;
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
-  Buf buf_[4];
-  bool encoded_[4] = {false, false, false, false};  // type buffered as COPY rows (engine-encoded)
+  Buf buf_[NT];
+  bool encoded_[NT] = {false, false, false, false, false};  // type buffered as COPY rows (engine-encoded)
   std::deque<std::shared_ptr<Job>> order_, to_encode_;
   uint64_t next_seq_ = 0;
   bool stop_ = false;

@@ -1309,12 +1309,12 @@ void Engine::grow_tx_capacity(uint32_t need, uint32_t keep) {
   hipHostFree(h_gid_);
   h_tx_ = h_tx;
   h_gid_ = h_gid;
-  HIP_OK(hipFree(d_tx_));
-  HIP_OK(hipFree(d_gid_));
+  dfree(d_tx_);
+  dfree(d_gid_);
   d_tx_ = (TxRec*)dmalloc((size_t)cap * sizeof(TxRec));
   d_gid_ = (int64_t*)dmalloc((size_t)cap * 8);
   if (cap > std::max<int64_t>(ord_cap_, 0)) {
-    HIP_OK(hipFree(d_ord_list_));
+    dfree(d_ord_list_);
     d_ord_list_ = (int32_t*)dmalloc((size_t)cap * 4);
     ord_cap_ = cap;
   }
@@ -1579,6 +1579,7 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
     }
   }
   const int64_t edge_ts = (L - cfg_.buffer - 1) * 10000;
+  last_edge_ts_ = edge_ts;
   const double tr0 = now_ms();
   // ---- K9 release: merge the sorted pool with the sorted tail, hand out endTs <= edge
   if (dev()) {
@@ -1681,6 +1682,7 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
     za.exact = cfg_.exact_mean; za.sigma_stddev = cfg_.sigma_stddev; za.resync_k = cfg_.resync_k;
     za.rollover_idx = rollover_idx_;
     za.rs_lo = 0; za.rs_n = 0; za.rs_parts = RS_PARTS; za.rs_part = rs_part_; za.rs_cnt = rs_cnt_;
+    za.rs_mfma = cfg_.resync_mfma ? 1 : 0;
     if (rs_range_ > 0) {
       za.rs_lo = (int32_t)((rollover_idx_ % cfg_.resync_k) * rs_range_);
       za.rs_n = std::max(0, std::min(rs_range_, n_series_ - za.rs_lo));
@@ -1855,6 +1857,13 @@ int32_t Engine::intern_name(const std::string& name) {
   h_names_ += name;
   name_off_.emplace(name, off);
   return off;
+}
+
+// Frees a dmalloc'd buffer and forgets it (the destructor frees what is still listed).
+void Engine::dfree(void* p) {
+  if (!p) return;
+  HIP_OK(hipFree(p));
+  allocations_.erase(std::remove(allocations_.begin(), allocations_.end(), p), allocations_.end());
 }
 
 void* Engine::regrow(void* old, size_t& cap, size_t need) {
@@ -2158,7 +2167,7 @@ void Engine::download_zout(int l, std::vector<ZOut>& out) {
 }
 
 const char* out_kind_name(int k) {
-  static const char* n[N_OUT] = {"transactions", "audit_db", "db", "st", "fs", "al", "sx"};
+  static const char* n[N_OUT] = {"transactions", "audit_db", "db", "st", "fs", "al", "sx", "fb"};
   return n[k];
 }
 
@@ -2250,6 +2259,10 @@ uintptr_t Engine::alloc_pinned(size_t n) {
 void Engine::free_pinned(uintptr_t p) { hipHostFree((void*)p); }
 
 void Engine::pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream, bool atomic_path) {
+  if (coll_) {  // node-wide slots: queue new services, adopt the slots the last round assigned
+    reg_collect_locked();
+    reg_apply_locked();
+  }
   // series -> service table (grows with the dictionary): upload only the new tail
   if (series_service_uploaded_ < n_series_) {
     // Pinned host mirror of the table: the series list is append-only, so each upload reads a
@@ -2260,8 +2273,8 @@ void Engine::pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream,
       HIP_OK(hipHostMalloc(&p, (size_t)cfg_.max_series * 4, hipHostMallocDefault));
       h_series_service_ = (int32_t*)p;
     }
-    if (lo == 0) HIP_OK(hipStreamSynchronize(stream_));  // table reset (load_state): rewrite from 0
-    for (int32_t s = lo; s < n_series_; ++s) h_series_service_[s] = series_[s].service;
+    if (lo == 0) HIP_OK(hipStreamSynchronize(stream_));  // table reset (load_state / new slots): rewrite from 0
+    for (int32_t s = lo; s < n_series_; ++s) h_series_service_[s] = svc_key(s);
     HIP_OK(hipMemcpyAsync(d_series_service_ + lo, h_series_service_ + lo, (size_t)(n_series_ - lo) * 4,
                           hipMemcpyHostToDevice, stream_));
     series_service_uploaded_ = n_series_;
@@ -2277,14 +2290,14 @@ void Engine::pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream,
     if (svc_csr_n_ < 0 || svc_csr_cap_ != cap || (int64_t)(n_series_ - svc_csr_n_) * 8 > n_series_) {
       h_svc_off_.assign((size_t)cap + 1, 0);
       for (int32_t s = 0; s < n_series_; ++s) {
-        const int32_t v = series_[s].service;
+        const int32_t v = svc_key(s);
         if (v >= 0 && v < cap) ++h_svc_off_[(size_t)v + 1];
       }
       for (int32_t v = 0; v < cap; ++v) h_svc_off_[(size_t)v + 1] += h_svc_off_[v];
       h_svc_ids_.assign(std::max<size_t>(1, (size_t)h_svc_off_[cap]), 0);
       std::vector<int32_t> pos(h_svc_off_.begin(), h_svc_off_.end() - 1);
       for (int32_t s = 0; s < n_series_; ++s) {
-        const int32_t v = series_[s].service;
+        const int32_t v = svc_key(s);
         if (v >= 0 && v < cap) h_svc_ids_[(size_t)pos[v]++] = s;
       }
       trace_event("fleet.csr", now_ms(), now_ms(), 1);
@@ -2374,6 +2387,17 @@ void Engine::fleet_setup(int32_t cap, bool lockstep) {
     HIP_OK(hipEventCreateWithFlags(&pack_ev_[i], hipEventDisableTiming));
   }
   fleet_rounds_ = fleet_posted_ = fleet_packed_ = 0;
+  if (!lockstep_ && nranks > 1)
+    throw std::runtime_error("fleet baseline across ranks needs lock-step rounds (node-wide service registry)");
+  d_reg_send_ = (uint8_t*)dmalloc(kRegBlock);
+  d_reg_recv_ = (uint8_t*)dmalloc(kRegBlock * (size_t)nranks);
+  HIP_OK(hipHostMalloc((void**)&h_reg_send_, kRegBlock, hipHostMallocDefault));
+  HIP_OK(hipHostMalloc((void**)&h_reg_recv_, kRegBlock * (size_t)nranks, hipHostMallocDefault));
+  fleet_slot_.clear();
+  reg_queued_.clear();
+  reg_scan_series_ = 0;
+  series_service_uploaded_ = 0;  // rows become node-wide slots
+  svc_csr_n_ = -1;
   node_mode_ = lockstep_ && cfg_.node_cooldown != 0;
   if (node_mode_) {
     const size_t per = sizeof(NodeHdr) + (size_t)node_cap_ * sizeof(NodeCand);
@@ -2424,12 +2448,14 @@ void Engine::lockstep_sync(int64_t batch_max) {
   // as each rank of an 8-GPU node, and this path stays exercised by the 1-GPU tests).
   h_sync_[0] = watermark_;
   h_sync_[1] = b == INT64_MIN ? -1.0 : (double)b;  // buckets < 2^53: exact in a double
-  HIP_OK(hipMemcpyAsync(d_sync_, h_sync_, 16, hipMemcpyHostToDevice, coll_stream_));
-  coll_->all_reduce_f64(d_sync_, 2, /*max=*/true, coll_stream_);
-  HIP_OK(hipMemcpyAsync(h_sync_, d_sync_, 16, hipMemcpyDeviceToHost, coll_stream_));
+  h_sync_[2] = (double)reg_pending_count();        // any rank with unregistered services?
+  HIP_OK(hipMemcpyAsync(d_sync_, h_sync_, 24, hipMemcpyHostToDevice, coll_stream_));
+  coll_->all_reduce_f64(d_sync_, 3, /*max=*/true, coll_stream_);
+  HIP_OK(hipMemcpyAsync(h_sync_, d_sync_, 24, hipMemcpyDeviceToHost, coll_stream_));
   coll_wait(coll_stream_, nullptr, "lock-step clocks");
   watermark_ = h_sync_[0];
   if (h_sync_[1] >= 0) sync_latest_ = std::max(sync_latest_, (int64_t)h_sync_[1]);
+  if (h_sync_[2] > 0) reg_round();  // every rank sees the same max: all enter the gather
   // the coll stream is in order: the previous batch's alert gather has landed too
   if (node_round_pending_) node_resolve();
 }
@@ -2448,6 +2474,9 @@ void Engine::fleet_pack_locked() {
   if (!coll_) return;
   const int slot = (int)(fleet_packed_ & 1);
   if (fleet_packed_ >= 2) HIP_OK(hipStreamWaitEvent(comm_stream_, fleet_ev_[slot], 0));
+  // a rollover happened since the previous pack: this exchange's merge is that interval's fb
+  pack_edge_[slot] = metrics_.rollovers != last_edge_seen_ ? last_edge_ts_ : 0;
+  last_edge_seen_ = metrics_.rollovers;
   const double t0 = now_ms();
   pack_moments_locked(fleet_buf_[slot], fleet_cap_, comm_stream_);
   trace_event("fleet.pack", t0, now_ms(), 1);
@@ -2462,6 +2491,7 @@ void Engine::fleet_exchange_upto(uint64_t rounds) {
     const int slot = (int)(fleet_rounds_ & 1);
     HIP_OK(hipStreamWaitEvent(coll_stream_, pack_ev_[slot], 0));
     if (!fleet_skip_solo_) coll_->all_reduce_f64(fleet_buf_[slot], fleet_elems_, /*max=*/false, coll_stream_);
+    if (pack_edge_[slot] && want(OUT_FB) && coll_->rank() == 0) fleet_emit_fb(slot);
     HIP_OK(hipEventRecord(fleet_ev_[slot], coll_stream_));
     if (node_mode_) node_round(fleet_rounds_, /*wait=*/false);
     ++fleet_rounds_;

@@ -58,6 +58,7 @@ struct EngineConfig {
   int exact_mean = 0;
   int sigma_stddev = 0;
   int resync_k = 360;
+  bool resync_mfma = true;  // rolling-mode window re-sum on the matrix cores
   int n_lags = 2;
   int32_t lags[MAX_LAGS] = {360, 8640, 0, 0};
   double thr[MAX_LAGS] = {20.0, 15.0, 0, 0};
@@ -108,7 +109,7 @@ struct EngineConfig {
 //   FS            z -> alerts/db  fs lines (one per series per LAG)
 //   AL            alerts -> db    al lines
 //   SX            new: per-JVM rollup fused with JMX / VM gauges (K14), one line per server
-enum OutKind { OUT_TRANSACTIONS = 0, OUT_AUDIT_DB, OUT_DB, OUT_ST, OUT_FS, OUT_AL, OUT_SX, N_OUT };
+enum OutKind { OUT_TRANSACTIONS = 0, OUT_AUDIT_DB, OUT_DB, OUT_ST, OUT_FS, OUT_AL, OUT_SX, OUT_FB, N_OUT };
 // streams written by the engine's output lane (released tx, st, fs); the stats thread owns the rest
 constexpr uint32_t kLaneKinds = (1u << OUT_DB) | (1u << OUT_ST) | (1u << OUT_FS);
 const char* out_kind_name(int k);
@@ -290,6 +291,14 @@ class Engine {
   // Collective: call on every rank at the same point of the batch sequence.  Exchanges the
   // batches not yet exchanged and returns [cap][n_lags][NSTAT][3] of the newest.
   std::vector<double> fleet_merged();
+  // node-wide slot -> service name (rows of fleet_merged), and {slots, registry rounds, slots
+  // refused (maxServices full), fb rows emitted}
+  std::vector<std::string> fleet_slot_names() { flush(); return reg_names_; }
+  std::vector<uint64_t> fleet_info() {
+    flush();
+    out_wait_idle();
+    return {(uint64_t)reg_names_.size(), reg_rounds_, reg_overflow_, fb_rows_};
+  }
   uint64_t fleet_rounds() const { return fleet_rounds_; }
   // Same exchange over an in-process group (tests: N engines of one process share one GPU).
   void fleet_init_local(std::shared_ptr<LocalGroup> group, int rank, int32_t n_services_cap, bool lockstep);
@@ -345,6 +354,7 @@ class Engine {
   void sync_format_tables();
   int32_t intern_name(const std::string& name);
   void* regrow(void* old, size_t& cap, size_t need);
+  void dfree(void* p);
   void emit_bytes(int kind, const char* p, size_t n);
   void upload_series_tables(int32_t lo);
   void pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream, bool atomic_path = false);
@@ -427,6 +437,55 @@ class Engine {
   std::string node_text_;                  // decided al rows of this rank -> blob_[OUT_AL]
   uint64_t node_alerts_ = 0;
   bool node_round_pending_ = false;        // a gather is in flight (coll stream)
+  // ---- node-wide service registry (fleet.cpp).  Each rank interns services in its own order,
+  // so the moments matrix is indexed by a node-wide *slot*: new services travel (hash + name) in
+  // an all-gather of the lock-step round, and every rank assigns slots to unseen hashes in rank
+  // order -- identical tables everywhere, no coordinator.
+  static constexpr size_t kRegBlock = 65536;
+  static constexpr int kRegMaxEntries = 1024;
+  struct RegPending { int32_t id; uint64_t hash; std::string name; uint64_t tag; };  // tag: batch queued in
+  std::mutex reg_mu_;
+  std::deque<RegPending> reg_pending_;                     // stats thread -> ingest thread
+  struct RegAssigned { int32_t id, slot; uint64_t tag; };  // adopted by the pack of batch >= tag
+  std::vector<RegAssigned> reg_assigned_;                  // ingest -> stats thread
+  std::vector<uint8_t> reg_queued_;                        // stats thread: dict id queued
+  int32_t reg_scan_series_ = 0;                            // stats thread: series scanned
+  std::vector<int32_t> fleet_slot_;                        // stats thread: dict id -> slot (-1)
+  std::unordered_map<uint64_t, int32_t> reg_slot_;         // ingest thread: hash -> slot
+  std::vector<std::string> reg_names_;                     // ingest thread: slot -> name
+  uint64_t reg_overflow_ = 0, reg_rounds_ = 0;
+  uint8_t *d_reg_send_ = nullptr, *d_reg_recv_ = nullptr, *h_reg_send_ = nullptr, *h_reg_recv_ = nullptr;
+  int32_t reg_sent_ = 0;
+  void reg_collect_locked();                 // stats thread: queue services of new series
+  void reg_apply_locked();                   // stats thread: adopt assigned slots
+  int32_t reg_pending_count();
+  void reg_round();                          // ingest thread: all-gather + slot assignment
+  int32_t svc_key(int32_t s) const;          // moments row of series s (slot, or dict id alone)
+  // ---- fb stream: fleet-merged per-service baselines (rank 0, after a rollover's exchange)
+  int64_t pack_edge_[2] = {0, 0};            // stats thread: newest rollover edge of the packed batch
+  int64_t last_edge_ts_ = 0;                 // stats thread: newest rollover edge so far
+  uint64_t last_edge_seen_ = 0;
+  std::string h_fb_chars_;                   // slot names (ingest thread)
+  std::vector<int32_t> h_fb_names_;          // {off, len} per slot
+  char* d_fb_chars_ = nullptr;
+  size_t fb_chars_cap_ = 0, fb_chars_up_ = 0;
+  int32_t* d_fb_names_ = nullptr;
+  size_t fb_names_cap_ = 0;
+  int32_t fb_slots_up_ = 0;
+  uint32_t *d_fb_len_ = nullptr, *d_fb_off_ = nullptr;
+  void* d_fb_tmp_ = nullptr;
+  size_t fb_tmp_bytes_ = 0;
+  char* d_fb_out_[2] = {nullptr, nullptr};
+  size_t fb_out_cap_[2] = {0, 0};
+  char* h_fb_out_[2] = {nullptr, nullptr};
+  size_t h_fb_cap_[2] = {0, 0};
+  uint32_t* h_fb_total_ = nullptr;
+  hipEvent_t fb_ev_[2] = {nullptr, nullptr};
+  uint64_t fb_task_[2] = {0, 0};
+  int fb_k_ = 0;
+  uint64_t fb_rows_ = 0;
+  int32_t fb_rows_cap_ = 0;
+  void fleet_emit_fb(int slot);              // ingest thread, after the slot's all-reduce
   bool node_all_sent_ = true;              // every rank's last round sent everything
   uint8_t* d_node_send_ = nullptr;
   uint8_t* d_node_recv_ = nullptr;
@@ -745,10 +804,10 @@ class Engine {
 
   // text outputs
   std::string blob_[N_OUT];
-  int sink_fd_[N_OUT] = {-1, -1, -1, -1, -1, -1, -1};
+  int sink_fd_[N_OUT] = {-1, -1, -1, -1, -1, -1, -1, -1};
   std::shared_ptr<ByteSink> byte_sink_[N_OUT];
   bool fs_copy_ = false;
-  uint64_t sink_bytes_[N_OUT] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t sink_bytes_[N_OUT] = {0, 0, 0, 0, 0, 0, 0, 0};
   // K14 server rollup + exogenous context
   std::vector<double> h_ctx_;                    // [servers][CTX_FIELDS]
   bool ctx_dirty_ = false;

@@ -1,0 +1,225 @@
+// Node-wide service registry and the fb (fleet baseline) stream.
+//
+// The fleet all-reduce (engine.cpp fleet_exchange_upto) sums a [slot][lag][stat][3] moments
+// matrix over the ranks.  Each rank interns services in its own first-appearance order, so the
+// matrix row of a service must be a node-wide *slot*, agreed without a coordinator:
+//   * the stats thread queues every service of a newly created series (hash + name, tagged with
+//     the batch it was packed in);
+//   * the ingest thread's lock-step all-reduce carries "entries pending" (MAX over ranks); when
+//     any rank has some, every rank enters one all-gather of fixed-size blocks
+//     {count, (hash, name)...} and assigns slots to unseen hashes in rank order -- the same
+//     table on every rank;
+//   * the stats thread adopts the (service, slot) pairs at the pack of the batch they were
+//     assigned in (a batch tag), so every rank starts counting a service in the same exchange.
+// Only entries queued two or more batches back are sent: post_stats(k - 1) returning guarantees
+// the stats thread finished batch k - 2 on every rank, so block contents do not depend on thread
+// timing and the slot numbering is deterministic.
+//
+// fb rows (rank 0): after the all-reduce of a batch whose stats performed a rollover, K12's fleet
+// formatter (format.hip) turns the merged moments into one row per (service, LAG) -- the fleet
+// mean and spread of the per-JVM z-score baselines ("is getFoo slow on one JVM or everywhere?",
+// SURVEY §2.4) -- either as `fb|...` wire lines or as COPY rows for the DB sink
+// (apm_fleet_stats), D2H'd and emitted by the output lane.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "engine.h"
+
+namespace apm {
+
+namespace {
+uint64_t fnv1a(const std::string& s) {
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : s) { h ^= c; h *= 1099511628211ull; }
+  return h ? h : 1;
+}
+struct RegHdr { int32_t count, bytes; };
+struct RegEntry { uint64_t hash; uint32_t off, len; };
+}  // namespace
+
+int32_t Engine::svc_key(int32_t s) const {
+  const int32_t v = series_[s].service;
+  if (!coll_ || !lockstep_) return v;  // one rank without lock-step: the dictionary id is node-wide
+  return (size_t)v < fleet_slot_.size() ? fleet_slot_[v] : -1;
+}
+
+void Engine::reg_collect_locked() {
+  if (!lockstep_) return;
+  std::lock_guard<std::mutex> g(reg_mu_);
+  for (; reg_scan_series_ < n_series_; ++reg_scan_series_) {
+    const int32_t v = series_[reg_scan_series_].service;
+    if ((size_t)v >= reg_queued_.size()) reg_queued_.resize((size_t)v + 1, 0);
+    if (reg_queued_[v]) continue;
+    reg_queued_[v] = 1;
+    const std::string name = dict_.service_name(v);
+    reg_pending_.push_back(RegPending{v, fnv1a(name), name, fleet_packed_});
+  }
+}
+
+void Engine::reg_apply_locked() {
+  std::lock_guard<std::mutex> g(reg_mu_);
+  bool any = false;
+  size_t keep = 0;
+  for (size_t i = 0; i < reg_assigned_.size(); ++i) {
+    const RegAssigned& a = reg_assigned_[i];
+    if (a.tag > fleet_packed_) { reg_assigned_[keep++] = a; continue; }
+    if ((size_t)a.id >= fleet_slot_.size()) fleet_slot_.resize((size_t)a.id + 1, -1);
+    fleet_slot_[a.id] = a.slot;
+    any = true;
+  }
+  reg_assigned_.resize(keep);
+  if (any) {  // some series change rows: rewrite the series -> row table and the Gram CSR
+    series_service_uploaded_ = 0;
+    svc_csr_n_ = -1;
+  }
+}
+
+int32_t Engine::reg_pending_count() {
+  std::lock_guard<std::mutex> g(reg_mu_);
+  int32_t n = 0;
+  for (const auto& p : reg_pending_) {
+    if (p.tag + 2 > fleet_posted_) break;  // queued in a batch the stats thread may still be on
+    ++n;
+  }
+  return n;
+}
+
+void Engine::reg_round() {
+  const int nr = fleet_nranks_;
+  RegHdr* hdr = (RegHdr*)h_reg_send_;
+  RegEntry* ent = (RegEntry*)(h_reg_send_ + sizeof(RegHdr));
+  char* chars = (char*)(ent + kRegMaxEntries);
+  const size_t char_cap = kRegBlock - sizeof(RegHdr) - sizeof(RegEntry) * kRegMaxEntries;
+  int32_t n = 0;
+  uint32_t used = 0;
+  {
+    std::lock_guard<std::mutex> g(reg_mu_);
+    for (const auto& p : reg_pending_) {
+      if (p.tag + 2 > fleet_posted_ || n >= kRegMaxEntries) break;
+      const uint32_t len = (uint32_t)std::min<size_t>(p.name.size(), 4096);
+      if (used + len > char_cap) break;
+      ent[n] = RegEntry{p.hash, used, len};
+      std::memcpy(chars + used, p.name.data(), len);
+      used += len;
+      ++n;
+    }
+  }
+  hdr->count = n;
+  hdr->bytes = (int32_t)used;
+  HIP_OK(hipMemcpyAsync(d_reg_send_, h_reg_send_, kRegBlock, hipMemcpyHostToDevice, coll_stream_));
+  coll_->all_gather(d_reg_send_, d_reg_recv_, kRegBlock, coll_stream_);
+  HIP_OK(hipMemcpyAsync(h_reg_recv_, d_reg_recv_, kRegBlock * (size_t)nr, hipMemcpyDeviceToHost, coll_stream_));
+  coll_wait(coll_stream_, nullptr, "service registry");
+  ++reg_rounds_;
+  // every rank walks the same blocks in the same order: identical slot tables
+  const int32_t cap = fleet_cap_;
+  for (int r = 0; r < nr; ++r) {
+    const uint8_t* blk = h_reg_recv_ + kRegBlock * (size_t)r;
+    const RegHdr* h = (const RegHdr*)blk;
+    const RegEntry* e = (const RegEntry*)(blk + sizeof(RegHdr));
+    const char* c = (const char*)(e + kRegMaxEntries);
+    for (int32_t i = 0; i < h->count; ++i) {
+      if (reg_slot_.count(e[i].hash)) continue;
+      if ((int32_t)reg_names_.size() >= cap) { reg_slot_[e[i].hash] = -1; ++reg_overflow_; continue; }
+      const int32_t slot = (int32_t)reg_names_.size();
+      reg_slot_[e[i].hash] = slot;
+      reg_names_.emplace_back(c + e[i].off, e[i].len);
+      h_fb_names_.push_back((int32_t)h_fb_chars_.size());
+      h_fb_names_.push_back((int32_t)e[i].len);
+      h_fb_chars_.append(c + e[i].off, e[i].len);
+    }
+  }
+  // this rank's sent entries now have slots: hand them to the stats thread (adopted at the pack
+  // of the batch this round belongs to, on every rank)
+  std::lock_guard<std::mutex> g(reg_mu_);
+  for (int32_t i = 0; i < n; ++i) {
+    const RegPending& p = reg_pending_.front();
+    reg_assigned_.push_back(RegAssigned{p.id, reg_slot_[p.hash], fleet_posted_});
+    reg_pending_.pop_front();
+  }
+}
+
+void Engine::fleet_emit_fb(int slot) {
+  const int32_t n_slots = (int32_t)reg_names_.size();
+  if (n_slots == 0) return;
+  const int k = fb_k_;
+  fb_k_ ^= 1;
+  out_wait(fb_task_[k]);  // slot k's previous D2H + emission is done
+  // slot names -> device (coll stream: ordered before the format kernels)
+  if (fb_chars_up_ < h_fb_chars_.size()) {
+    if (h_fb_chars_.size() > fb_chars_cap_) {
+      d_fb_chars_ = (char*)regrow(d_fb_chars_, fb_chars_cap_, h_fb_chars_.size() * 2 + 4096);
+      fb_chars_up_ = 0;
+    }
+    HIP_OK(hipMemcpyAsync(d_fb_chars_ + fb_chars_up_, h_fb_chars_.data() + fb_chars_up_,
+                          h_fb_chars_.size() - fb_chars_up_, hipMemcpyHostToDevice, coll_stream_));
+    HIP_OK(hipStreamSynchronize(coll_stream_));  // pageable source: keep it alive until copied
+    fb_chars_up_ = h_fb_chars_.size();
+  }
+  if (fb_slots_up_ < n_slots) {
+    if ((size_t)n_slots * 8 > fb_names_cap_) {
+      d_fb_names_ = (int32_t*)regrow(d_fb_names_, fb_names_cap_, (size_t)n_slots * 16 + 4096);
+      fb_slots_up_ = 0;
+    }
+    HIP_OK(hipMemcpyAsync(d_fb_names_ + 2 * fb_slots_up_, h_fb_names_.data() + 2 * fb_slots_up_,
+                          (size_t)(n_slots - fb_slots_up_) * 8, hipMemcpyHostToDevice, coll_stream_));
+    HIP_OK(hipStreamSynchronize(coll_stream_));
+    fb_slots_up_ = n_slots;
+  }
+  const int32_t rows = n_slots * cfg_.n_lags;
+  if (!d_fb_len_ || rows + 1 > (int32_t)(fb_tmp_bytes_ ? fb_rows_cap_ : 0)) {
+    if (d_fb_len_) { dfree(d_fb_len_); dfree(d_fb_off_); dfree(d_fb_tmp_); }
+    fb_rows_cap_ = std::max<int32_t>(rows + 1, 2 * fleet_cap_ * cfg_.n_lags + 1);
+    d_fb_len_ = (uint32_t*)dmalloc((size_t)fb_rows_cap_ * 4);
+    d_fb_off_ = (uint32_t*)dmalloc((size_t)fb_rows_cap_ * 4);
+    fb_tmp_bytes_ = apm_fleet_format_tmp_bytes(fb_rows_cap_);
+    d_fb_tmp_ = dmalloc(fb_tmp_bytes_);
+    if (!h_fb_total_) HIP_OK(hipHostMalloc((void**)&h_fb_total_, 16, hipHostMallocDefault));
+    for (auto& e : fb_ev_)
+      if (!e) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  size_t longest = 0;
+  for (size_t i = 1; i < h_fb_names_.size(); i += 2) longest = std::max<size_t>(longest, (size_t)h_fb_names_[i]);
+  const size_t cap_bytes = (size_t)rows * (260 + 2 * longest) + 64;
+  if (cap_bytes > fb_out_cap_[k]) d_fb_out_[k] = (char*)regrow(d_fb_out_[k], fb_out_cap_[k], cap_bytes);
+  FleetFormatArgs fa{};
+  fa.moments = fleet_buf_[slot];
+  fa.names = reinterpret_cast<const int2*>(d_fb_names_);
+  fa.chars = d_fb_chars_;
+  fa.n_slots = n_slots;
+  fa.n_lags = cfg_.n_lags;
+  std::vector<int> order(cfg_.n_lags);
+  for (int l = 0; l < cfg_.n_lags; ++l) order[l] = l;
+  std::sort(order.begin(), order.end(), [&](int a, int b) { return cfg_.lags[a] < cfg_.lags[b]; });
+  for (int l = 0; l < cfg_.n_lags; ++l) { fa.lag_order[l] = order[l]; fa.lag_value[l] = cfg_.lags[l]; }
+  fa.edge_ts = pack_edge_[slot];
+  fa.copy = fs_copy_ ? 1 : 0;
+  fa.ts_len = pg_timestamp(fa.edge_ts, fa.ts);
+  fa.len = d_fb_len_;
+  fa.off = d_fb_off_;
+  fa.out = d_fb_out_[k];
+  fa.fallback = d_fmt_fallback_;
+  if (apm_fleet_format(&fa, d_fb_tmp_, fb_tmp_bytes_, coll_stream_) != 0) throw std::runtime_error("fb format scan failed");
+  HIP_OK(hipMemcpyAsync(h_fb_total_ + k, d_fb_off_ + rows, 4, hipMemcpyDeviceToHost, coll_stream_));
+  HIP_OK(hipEventRecord(fb_ev_[k], coll_stream_));
+  char* dst = d_fb_out_[k];
+  fb_task_[k] = post_out([this, k, dst]() {
+    HIP_OK(hipEventSynchronize(fb_ev_[k]));
+    const size_t total = h_fb_total_[k];
+    if (total > h_fb_cap_[k]) {
+      if (h_fb_out_[k]) HIP_OK(hipHostFree(h_fb_out_[k]));
+      h_fb_cap_[k] = total * 3 / 2 + (1 << 16);
+      HIP_OK(hipHostMalloc((void**)&h_fb_out_[k], h_fb_cap_[k], hipHostMallocDefault));
+    }
+    if (total) {
+      HIP_OK(hipMemcpy(h_fb_out_[k], dst, total, hipMemcpyDeviceToHost));
+      size_t rows = 0;
+      for (size_t i = 0; i < total; ++i) rows += h_fb_out_[k][i] == '\n';
+      fb_rows_ += rows;
+      emit_bytes(OUT_FB, h_fb_out_[k], total);
+    }
+  });
+}
+
+}  // namespace apm

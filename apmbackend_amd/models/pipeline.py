@@ -24,7 +24,7 @@ from ..utils.timeparse import TzOffset
 KIND_CODE = {"SOAP": 0, "SERVER": 1, "APP": 2}
 
 # Output streams (engine.h OutKind); the bit index is the position in this tuple.
-OUT_KINDS = ("transactions", "audit_db", "db", "st", "fs", "al", "sx")
+OUT_KINDS = ("transactions", "audit_db", "db", "st", "fs", "al", "sx", "fb")
 # What the reference persists (db_insert queue): released + audit tx, fs, al.  `transactions`
 # and `st` are internal hand-offs that only the AMQP bridge needs.
 DB_OUTPUTS = ("audit_db", "db", "fs", "al")
@@ -65,6 +65,7 @@ def engine_config(cfg: Dict[str, Any], device: int = 0, keep_text: bool = False,
         "exact_mean": 1 if g.get("zscoreMeanMode", "rolling") == "exact" else 0,
         "sigma_stddev": 1 if g.get("zscoreSigma", "sqrt_mean") == "stddev" else 0,
         "resync_k": int(g.get("exactRecomputeEveryIntervals", 360)),
+        "resync_mfma": bool(g.get("resyncOnMatrixCores", True)),
         "emulate_aliasing": 1 if g.get("emulateOverrideAliasing", False) else 0,
         "lags": lags,
         "lag_suppressed": [1 if l[0] in suppressed_lags else 0 for l in lags],

@@ -117,10 +117,14 @@ class IngestService:
         outs = set(DB_OUTPUTS)
         if as_bool(g.get("serverRollup", False)):  # K14 per-JVM rollup fused with JMX gauges
             outs.add("sx")
+        if self.world > 1 and engine == "native" and as_bool(g.get("fleetBaseline", True)) \
+                and as_bool(g.get("fleetBaselineRows", True)):
+            outs.add("fb")  # fleet-merged per-service baselines (rank 0 emits them)
         if self.mode == "amqp":
             outs |= {"transactions" if "transactions" in self.bridge else "", "st" if "stats" in self.bridge else ""}
             outs.discard("")
         self.outputs = [k for k in OUT_KINDS if k in outs]
+        self.outs_set = set(self.outputs)
         if engine == "native":
             self.eng = APMEngine(self.cfg, device=self.local_rank, outputs=self.outputs)
             self.native = self.eng.eng
@@ -191,7 +195,8 @@ class IngestService:
             if engine == "native":
                 # db / audit / fs go engine output lane -> native sink directly; al stays on the
                 # Python side (the e-mail notifier reads it too)
-                self.inserter.attach_engine(self.native, [k for k in self.outputs if k in DB_OUTPUTS and k != "al"])
+                self.inserter.attach_engine(self.native, [k for k in self.outputs
+                                                          if (k in DB_OUTPUTS and k != "al") or k == "fb"])
         elif self.mode == "amqp":
             from .queue import QueueManager
             self.qm = QueueManager(self.cfg["amqpConnectionString"], self.cfg.get("statLogIntervalInSeconds", 60))
@@ -201,6 +206,8 @@ class IngestService:
             for q in self.bridge:
                 if q in qmap:
                     self.producers[q] = self.qm.get_queue(qmap[q], "p")
+            if "fb" in self.outs_set:  # not a db_insert record type of the reference: own queue
+                self.producers["fleet"] = self.qm.get_queue(g.get("fleetQueue", "fleet_baseline"), "p")
             self.qm.on("pause", lambda: log.info("queue backpressure: pausing ingest"))
         elif self.mode != "none":
             raise ValueError(f"unknown gpu.outputMode {self.mode!r}")
@@ -410,10 +417,12 @@ class IngestService:
             counts[k] = blob.count(b"\n")
             if k == "al" and self.notifier:
                 self.notifier.add_lines(blob.decode("utf-8").split("\n"))
-            if self.inserter is not None and k in DB_OUTPUTS:
+            if self.inserter is not None and (k in DB_OUTPUTS or k == "fb"):
                 self.inserter.consume_bytes(blob)
             elif self.qm is not None:
-                if k in DB_OUTPUTS:
+                if k == "fb":
+                    prod = self.producers.get("fleet")
+                elif k in DB_OUTPUTS:
                     prod = self.producers["db"]
                 elif k == "transactions":
                     prod = self.producers.get("transactions")

@@ -52,8 +52,10 @@ COLUMNS: Dict[str, Tuple[str, List[str]]] = {
                           "heapcommitted", "heapmax", "metaused", "metacommitted", "metamax", "sysload", "classcnt",
                           "threadcnt", "daemonthreadcnt", "beanpoolavailablecnt", "beanpoolcurrentsize",
                           "beanpoolmaxsize"]),
+    # fleet-merged per-service baselines (fb records, rank 0): not part of the reference schema
+    "fb": ("dbFleetTable", ["timestamp", "service", "lag", "nseries", "stats"]),
 }
-TYPES = ("tx", "fs", "al", "jx")
+TYPES = ("tx", "fs", "al", "jx", "fb")
 
 
 # --------------------------------------------------------------------------- COPY text encoding
@@ -139,7 +141,7 @@ def pg_row_from_copy(rtype: str, row: str) -> Dict[str, Any]:
             out[c] = _dt.datetime.strptime(v[:-3], "%Y-%m-%d %H:%M:%S.%f").replace(tzinfo=_dt.timezone.utc)
         elif c in ("stats", "entry"):
             out[c] = json.loads(v)
-        elif c in ("tpm", "elapsed", "acctnum") or rtype == "jx" and c not in ("server",):
+        elif c in ("tpm", "elapsed", "acctnum", "nseries") or rtype == "jx" and c not in ("server",):
             f = float(v)
             out[c] = int(f) if f.is_integer() and "." not in v and "e" not in v else f
         else:
@@ -322,7 +324,9 @@ def make_writer(ins_cfg: Dict[str, Any]) -> Writer:
 def save_resume(path: str, buffers: Dict[str, Deque[Dict[str, Any]]]):
     """util_methods.saveToResumeFile with the Map replacer: {"dataType":"Map","value":[...]}
     (atomic: tmp + rename)."""
-    doc = {"dataType": "Map", "value": [[t, [_json_row(r) for r in rows]] for t, rows in buffers.items()]}
+    # the reference's four buffers always; the fleet buffer (our addition) only when it holds rows
+    doc = {"dataType": "Map", "value": [[t, [_json_row(r) for r in rows]] for t, rows in buffers.items()
+                                        if t != "fb" or rows]}
     tmp = path + ".tmp"
     os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
     with open(tmp, "w") as f:
@@ -380,7 +384,7 @@ class DBInserter:
         self.cfg = cfg
         self._limit = int(ic.get("dbInsertBufferLimit", 1000))
         self._max_wait_s = float(ic.get("dbMaxTimeBetweenInsertsMs", 5000)) / 1000.0
-        self.tables = {t: ic.get(key, t) for t, (key, _cols) in COLUMNS.items()}
+        self.tables = {t: ic.get(key, "apm_fleet_stats" if t == "fb" else t) for t, (key, _cols) in COLUMNS.items()}
         self.clock = clock
         self.stats = stats or DBStats(float(cfg.get("statLogIntervalInSeconds", 60)))
         self.buffers: Dict[str, Deque[Dict[str, Any]]] = {t: deque() for t in TYPES}
@@ -441,12 +445,13 @@ class DBInserter:
         if self.core is None:
             return False
         N = _native()
-        fs_copy = "fs" in kinds and self.gpu_fs_copy
+        fs_copy = self.gpu_fs_copy and ("fs" in kinds or "fb" in kinds)
+        if fs_copy:
+            # K12 (fs) and the fleet formatter (fb) write COPY text on the GPU; the sink stores it as is
+            native_engine.set_fs_copy(True)
         for k in kinds:
-            if k == "fs" and fs_copy:
-                # K12 formats the fs rows as COPY text on the GPU; the sink writes them as is
-                native_engine.set_fs_copy(True)
-                N.attach_sink(native_engine, k, self.core, TYPES.index("fs"))
+            if k in ("fs", "fb") and fs_copy:
+                N.attach_sink(native_engine, k, self.core, TYPES.index(k))
             else:
                 N.attach_sink(native_engine, k, self.core)
         self._attached = (native_engine, list(kinds), fs_copy)

@@ -246,6 +246,29 @@ def _pad(arr: List[str], n: int) -> List[Optional[str]]:
     return list(arr) + [None] * max(0, n - len(arr))
 
 
+@dataclass
+class FleetEntry:
+    """``fb|ts|service|lag|nseries|avgMean:avgStd|p75Mean:p75Std|p95Mean:p95Std`` -- the
+    fleet-merged per-service baseline (no reference counterpart: the reference has one process
+    per stage and no cross-JVM view).  Emitted by rank 0 after each interval's RCCL merge."""
+    timestamp: Num
+    service: str
+    lag: str
+    nseries: Num
+    stats: List[Num]  # [avg mean, avg std, p75 mean, p75 std, p95 mean, p95 std]
+    type: str = "fb"
+
+    def to_csv(self) -> str:
+        g = [f"{nf(self.stats[2 * k], 1)}:{nf(self.stats[2 * k + 1], 1)}" for k in range(3)]
+        return f"fb|{js_str(self.timestamp)}|{self.service}|{self.lag}|{js_str(self.nseries)}|" + "|".join(g)
+
+    def to_pg_row(self) -> Dict[str, Any]:
+        keys = ("averagemean", "averagestd", "per75mean", "per75std", "per95mean", "per95std")
+        return {"timestamp": _ms_to_dt(self.timestamp), "service": self.service, "lag": self.lag,
+                "nseries": _num_or_none(self.nseries),
+                "stats": {k: _num_or_none(v) for k, v in zip(keys, self.stats)}}
+
+
 def entry_from_csv(line: Union[str, bytes], delim: str = "|"):
     """EntryFactory.getEntryFromCSV (entries.js:174-193). Returns None for unknown types."""
     if isinstance(line, bytes):
@@ -272,7 +295,14 @@ def entry_from_csv(line: Union[str, bytes], delim: str = "|"):
     if t == "jx":
         a = _pad(arr, 19)
         return JmxEntry.make(a[1], a[2], *a[3:19])
+    if t == "fb":
+        a = _pad(arr, 8)
+        st: List[Num] = []
+        for g in a[5:8]:
+            p = _pad(g.split(":") if g is not None else [], 2)
+            st += [parse_float(p[0]), parse_float(p[1])]
+        return FleetEntry(parse_int(a[1]), a[2], a[3], parse_int(a[4]), st)
     return None
 
 
-RECORD_TYPES = ("tx", "st", "fs", "al", "jx")
+RECORD_TYPES = ("tx", "st", "fs", "al", "jx", "fb")

@@ -137,9 +137,10 @@ def main():
     # Materialise exactly what the reference hands to its db_insert stage (released + audit tx,
     # fs, al) in the wire format and write it to a sink (/dev/null: the DB loader is out of scope).
     from apmbackend_amd.models.pipeline import DB_OUTPUTS
-    eng = APMEngine(cfg, device=local, outputs=DB_OUTPUTS)
+    outs = DB_OUTPUTS + ("fb",)  # + the fleet-merged per-service baselines (rank 0, every interval)
+    eng = APMEngine(cfg, device=local, outputs=outs)
     sink_fd = os.open(args.sink, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
-    for k in DB_OUTPUTS:
+    for k in outs:
         eng.eng.set_sink_fd(k, sink_fd)
     start = 1578391200000
     step_ms = int(args.batch_seconds * 1000)
@@ -227,7 +228,7 @@ def main():
         fleet.drain_alerts()  # untimed: decide the last batch's node-wide alert candidates
     m1 = eng.metrics()
     lines = m1["lines"] - m0["lines"]
-    out_bytes = {k: eng.eng.sink_bytes(k) for k in DB_OUTPUTS}
+    out_bytes = {k: eng.eng.sink_bytes(k) for k in outs}
     lat = sorted(m1["rollover_latency_ms"][len(m0["rollover_latency_ms"]):]) or [float("nan")]
     p50 = lat[len(lat) // 2]
     stats = torch.tensor([float(lines), dt, p50, float(m1["tx"] - m0["tx"]),

@@ -170,7 +170,7 @@ def test_native_fleet_exchange_single_rank():
     got = np.frombuffer(eng.eng.fleet_merged(), dtype=np.float64)
     assert eng.eng.fleet_rounds() == len(bl)
     buf = torch.zeros(got.size, dtype=torch.float64, device="cuda")
-    eng.eng.pack_service_moments(buf.data_ptr(), cap)
+    eng.eng.pack_service_moments(buf.data_ptr(), cap)  # one rank, no lock-step: rows = dictionary ids
     torch.cuda.synchronize()  # device-wide: covers the engine's comm stream
     want = buf.cpu().numpy()
     assert got.sum() > 0
@@ -577,3 +577,22 @@ def test_fs_copy_rows_on_gpu_match_host_encoder():
     want = [r.rstrip("\n") for r in sinks.copy_encode_lines(wire["fs"])["fs"]]
     assert len(want) > 100 and got == want
     assert any("null" in r for r in got)  # undefined window stats
+
+
+def test_resync_on_matrix_cores_matches_valu_resync():
+    """Rolling mode's staggered exact re-sum as MFMA tile reductions (v_mfma_f64_16x16x4f64
+    over [16 series x 2 window rows] with a ones/squares B operand) vs the VALU Neumaier walk:
+    same signals and alerts; printed means agree (fp64 sums, different order)."""
+    lines, bl = synth_batches(8, duration=900)
+    res = {}
+    for mfma in (True, False):
+        C = small_cfg("rolling")
+        C["gpu"]["exactRecomputeEveryIntervals"] = 3
+        C["gpu"]["resyncOnMatrixCores"] = mfma
+        _, out = _run_engine(C, bl)
+        res[mfma] = out
+    assert _al_decisions(res[True]["al"]) == _al_decisions(res[False]["al"])
+    a, b = res[True]["fs"], res[False]["fs"]
+    assert len(a) == len(b) > 100
+    diff = sum(x != y for x, y in zip(a, b))
+    assert diff <= len(a) // 200, diff

@@ -90,10 +90,10 @@ def run_node(world, bl, servers):
             fleets[r] = FleetBaseline(engs[r], world, r, max_services=64, local_group=group, servers=servers)
             for now, chunks in bl:
                 engs[r].process_lines([(fp, ls) for fp, ls in chunks if server_of(fp) in shards[r]], now)
-                for k in ("st", "fs", "al"):
+                for k in ("st", "fs", "al", "fb"):
                     outs[r][k] += engs[r].take(k)
             fleets[r].drain_alerts()
-            for k in ("st", "fs", "al"):
+            for k in ("st", "fs", "al", "fb"):
                 outs[r][k] += engs[r].take(k)
         except Exception as e:  # pragma: no cover - reported below
             errs.append((r, repr(e)))
@@ -130,3 +130,43 @@ def test_local_group_node_matches_single_process(world):
     if world > 1:
         # candidates were raised on more ranks than alerted: the cooldown was decided node-wide
         assert sum(m["alert_candidates"] for m in ms) > len(P.al)
+
+
+def _fleet_by_name(eng):
+    import numpy as np
+    names = eng.eng.fleet_slot_names()
+    m = np.frombuffer(eng.eng.fleet_merged(), dtype=np.float64).reshape(64, 2, 3, 3)
+    return {n: m[i] for i, n in enumerate(names)}, m[len(names):]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_fleet_registry_merges_services_node_wide(world):
+    """Ranks intern services in different orders; the moments matrix is indexed by node-wide
+    slots (hash + name all-gathered in the lock-step round, assigned in rank order), so the
+    merged per-service baselines of a 2/4-rank node equal the 1-rank ones service by service,
+    every rank holds the same table, and rank 0 emits the interval's fb rows."""
+    import numpy as np
+    lines, bl = corpus()
+    servers = sorted({server_of(fp) for fp in lines})
+    e1, o1 = run_node(1, bl, servers)
+    ref, _ = _fleet_by_name(e1[0])
+    engs, outs = run_node(world, bl, servers)
+    tables = [_fleet_by_name(e) for e in engs]
+    names0 = engs[0].eng.fleet_slot_names()
+    for e, (t, rest) in zip(engs, tables):
+        assert e.eng.fleet_slot_names() == names0  # same registry on every rank
+        assert not rest.any()  # nothing outside the registered slots
+    got = tables[0][0]
+    assert set(got) == set(ref) and len(ref) >= 5
+    for name in ref:
+        np.testing.assert_allclose(got[name], ref[name], rtol=1e-12, atol=1e-9)
+    # fb rows: rank 0 only, one per (service, LAG) with a baseline, every interval after warm-up
+    assert all(not o["fb"] for o in outs[1:])
+    fb = outs[0]["fb"]
+    assert fb and all(l.startswith("fb|") for l in fb)
+    last_ts = max(int(l.split("|")[1]) for l in fb)
+    last = [l for l in fb if int(l.split("|")[1]) == last_ts]
+    ref_last = [l for l in o1[0]["fb"] if int(l.split("|")[1]) == last_ts]
+    key = lambda l: (l.split("|")[2], l.split("|")[3])
+    assert sorted(map(key, last)) == sorted(map(key, ref_last))
+    assert engs[0].eng.fleet_info()["fb_rows"] == len(fb)

@@ -224,7 +224,7 @@ def test_native_sink_spool_matches_python_encoder(tmp_path):
 def test_native_sink_limit_and_timer_semantics():
     from apmbackend_amd import _native
     N = _native.load(build_if_missing=False)
-    s = N.DbSink(3, 50.0, ["t_tx", "t_fs", "t_al", "t_jx"], ["a", "b", "c", "d"], "null", [], 0, 1)
+    s = N.DbSink(3, 50.0, ["t_tx", "t_fs", "t_al", "t_jx", "t_fb"], ["a", "b", "c", "d", "e"], "null", [], 0, 1)
     tx = [l for l in _wire_lines() if l.startswith("tx|")][:7]
     s.consume(("\n".join(tx) + "\n").encode())
     s.drain()
@@ -236,7 +236,7 @@ def test_native_sink_limit_and_timer_semantics():
     assert s.tick() == 1
     s.drain()
     assert s.stats()["rows"] == 7 and s.stats()["buffered"] == 0
-    assert s.close() == [b"", b"", b"", b""]
+    assert s.close() == [b"", b"", b"", b"", b""]
 
 
 @pytest.mark.skipif(not _native_ok(), reason="native extension not built")
@@ -251,7 +251,8 @@ def test_native_sink_persistent_psql_copy_and_rebuffer(tmp_path, monkeypatch):
     from apmbackend_amd import _native
     N = _native.load(build_if_missing=False)
     fake = [sys.executable, os.path.join(os.path.dirname(__file__), "fixtures", "fake_psql.py")]
-    s = N.DbSink(1000, 1e9, ["apm_tx", "apm_stats", "apm_alerts", "apm_jmx"], ["a", "b", "c", "d"], "psql", fake, 0, 2)
+    s = N.DbSink(1000, 1e9, ["apm_tx", "apm_stats", "apm_alerts", "apm_jmx", "apm_fleet_stats"], ["a", "b", "c", "d", "e"],
+                 "psql", fake, 0, 2)
     lines = _wire_lines(10)
     s.consume(("\n".join(lines) + "\n").encode())
     s.flush_all()
@@ -273,3 +274,16 @@ def test_copy_rows_parse_back_for_the_resume_file():
     for t in ("tx", "fs"):
         for row in enc[t]:
             assert sinks.copy_row(t, sinks.pg_row_from_copy(t, row)) == row
+
+
+def test_fleet_rows_encode_natively_like_python():
+    from apmbackend_amd.utils.records import entry_from_csv
+    lines = ["fb|1578391200000|S:getFoo|6|8|123.4:5.6|130.0:7.0|undefined:undefined",
+             "fb|1578391210000|Provider:cb-util-001|360|3|0.5:0.0|1.2:0.3|9.9:1.0"]
+    assert entry_from_csv(lines[0]).to_csv() == lines[0]
+    want = sinks.copy_encode_lines(lines)
+    nat = sinks.copy_encode_native(lines)
+    if nat is not None:
+        assert nat["fb"][0].decode() == "".join(want["fb"]) and nat["fb"][1] == 2
+    assert want["fb"][0].startswith("2020-01-07 10:00:00.000+00\tS:getFoo\t6\t8\t{\"averagemean\":123.4,")
+    assert '"per95mean":null' in want["fb"][0]
