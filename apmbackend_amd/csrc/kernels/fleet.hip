@@ -5,8 +5,9 @@
 // series' current LAG-window mean (the z-score "avg"), read from the O(1) running sums.  The
 // layout is a dense fp64 matrix so one all_reduce(SUM) over xGMI merges all ranks; the merged
 // per-service mean/variance of baselines is what the survey calls the global merge (§2.4).
-// Two implementations: the MFMA Gram kernel (default, deterministic) and a per-series fp64
-// atomic scatter (reference / fallback for more than two LAGs).
+// Two implementations: the MFMA Gram kernel (default, deterministic: series added since the
+// CSR snapshot go through a second, per-batch tail CSR accumulated by the same kernel) and a
+// per-series fp64 atomic scatter (reference / fallback for more than two LAGs).
 #include "kernel_api.h"
 
 namespace apm {
@@ -53,6 +54,8 @@ constexpr int GRAM_WAVES = 4;
 
 __global__ __launch_bounds__(GRAM_WAVES * 64) void k_service_gram(const int32_t* __restrict__ svc_off,
                                                                 const int32_t* __restrict__ svc_ids,
+                                                                const int32_t* __restrict__ svc_map,
+                                                                int32_t accumulate,
                                                                 const uint8_t* __restrict__ active,
                                                                 int32_t n_services, int32_t S, int32_t n_lags,
                                                                 const double* const* __restrict__ sums,
@@ -91,10 +94,17 @@ __global__ __launch_bounds__(GRAM_WAVES * 64) void k_service_gram(const int32_t*
   __syncthreads();
   if (svc < n_services && lane < P) {
     const int p = lane, l = p / NSTAT, k = p % NSTAT;
-    double* o = dst + (((size_t)svc * n_lags + l) * NSTAT + k) * 3;
-    o[0] = g[wave][1 + p][1 + p];
-    o[1] = g[wave][0][1 + P + p];
-    o[2] = g[wave][1 + P + p][1 + P + p];
+    const int row = svc_map ? svc_map[svc] : svc;  // tail CSR: entry -> service row
+    double* o = dst + (((size_t)row * n_lags + l) * NSTAT + k) * 3;
+    if (accumulate) {  // one wave per service, entries in fixed order: still deterministic
+      o[0] += g[wave][1 + p][1 + p];
+      o[1] += g[wave][0][1 + P + p];
+      o[2] += g[wave][1 + P + p][1 + P + p];
+    } else {
+      o[0] = g[wave][1 + p][1 + p];
+      o[1] = g[wave][0][1 + P + p];
+      o[2] = g[wave][1 + P + p][1 + P + p];
+    }
   }
 }
 
@@ -103,12 +113,13 @@ __global__ __launch_bounds__(GRAM_WAVES * 64) void k_service_gram(const int32_t*
 extern "C" int apm_service_gram(const int32_t* svc_off, const int32_t* svc_ids, const uint8_t* active,
                                 int32_t n_services, int32_t S, int32_t n_lags, const double* const* sums,
                                 const double* const* comps, const int32_t* const* cnts, double* dst,
-                                hipStream_t stream) {
+                                hipStream_t stream, const int32_t* svc_map, int32_t accumulate) {
   using namespace apm;
   if (n_lags * NSTAT * 2 + 1 > 16) return -1;  // more features than one 16x16 Gram holds
   if (n_services <= 0) return 0;
   hipLaunchKernelGGL(k_service_gram, dim3((n_services + GRAM_WAVES - 1) / GRAM_WAVES), dim3(GRAM_WAVES * 64), 0,
-                     stream, svc_off, svc_ids, active, n_services, S, n_lags, sums, comps, cnts, dst);
+                     stream, svc_off, svc_ids, svc_map, accumulate, active, n_services, S, n_lags, sums, comps, cnts,
+                     dst);
   return 0;
 }
 

@@ -201,5 +201,6 @@ void apm_service_moments_tail(const int32_t* series_service, const uint8_t* acti
                               hipStream_t stream);
 int apm_service_gram(const int32_t* svc_off, const int32_t* svc_ids, const uint8_t* active, int32_t n_services,
                      int32_t S, int32_t n_lags, const double* const* sums, const double* const* comps,
-                     const int32_t* const* cnts, double* dst, hipStream_t stream);
+                     const int32_t* const* cnts, double* dst, hipStream_t stream, const int32_t* svc_map = nullptr,
+                     int32_t accumulate = 0);
 }

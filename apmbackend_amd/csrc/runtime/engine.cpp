@@ -223,6 +223,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipStreamCreateWithFlags(&parse_stream_, hipStreamNonBlocking));
   HIP_OK(hipStreamCreateWithFlags(&out_stream_, hipStreamNonBlocking));
   HIP_OK(hipEventCreate(&ev_a_));
+  HIP_OK(hipEventCreateWithFlags(&tail_csr_ev_, hipEventDisableTiming));
   HIP_OK(hipEventCreate(&ev_b_));
   const int32_t S = cfg_.max_series;
   // parse
@@ -469,7 +470,8 @@ Engine::~Engine() {
     if (h_stage_[k]) hipHostFree(h_stage_[k]);
     if (stage_ev_[k]) hipEventDestroy(stage_ev_[k]);
   }
-  hipEventDestroy(ev_a_); hipEventDestroy(ev_b_);
+  hipEventDestroy(ev_a_); hipEventDestroy(ev_b_); hipEventDestroy(tail_csr_ev_);
+  if (h_tail_csr_) hipHostFree(h_tail_csr_);
   hipStreamDestroy(stream_); hipStreamDestroy(comm_stream_); hipStreamDestroy(parse_stream_);
 }
 
@@ -2301,7 +2303,11 @@ void Engine::pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream,
         if (v >= 0 && v < cap) h_svc_ids_[(size_t)pos[v]++] = s;
       }
       trace_event("fleet.csr", now_ms(), now_ms(), 1);
-      HIP_OK(hipStreamSynchronize(stream));  // an earlier pack may still read the old lists
+      // an earlier pack may still read the old lists; on the comm stream that pack can sit
+      // behind an all-reduce, so wait with the collective watchdog rather than a bare sync
+      HIP_OK(hipEventRecord(ev_a_, stream));
+      if (coll_) coll_wait(nullptr, ev_a_, "fleet CSR rebuild");
+      else HIP_OK(hipEventSynchronize(ev_a_));
       d_svc_off_ = (int32_t*)regrow(d_svc_off_, svc_off_cap_, h_svc_off_.size() * 4);
       d_svc_ids_ = (int32_t*)regrow(d_svc_ids_, svc_ids_cap_, h_svc_ids_.size() * 4);
       HIP_OK(hipMemcpyAsync(d_svc_off_, h_svc_off_.data(), h_svc_off_.size() * 4, hipMemcpyHostToDevice, stream));
@@ -2312,9 +2318,45 @@ void Engine::pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream,
     if (apm_service_gram(d_svc_off_, d_svc_ids_, d_active_, cap, cfg_.max_series, cfg_.n_lags,
                          (const double* const*)d_lag_sum_ptrs_, (const double* const*)d_lag_comp_ptrs_,
                          (const int32_t* const*)d_lag_cnt_ptrs_, d_dst, stream) == 0) {
-      apm_service_moments_tail(d_series_service_, d_active_, svc_csr_n_, n_series_, cfg_.max_series, cfg_.n_lags,
-                               cap, (const double* const*)d_lag_sum_ptrs_, (const double* const*)d_lag_comp_ptrs_,
-                               (const int32_t* const*)d_lag_cnt_ptrs_, d_dst, stream);
+      // series added since the snapshot: a small per-batch CSR of just those series (by service,
+      // in series order) accumulated by the same Gram kernel -- the pack stays deterministic
+      if (n_series_ > svc_csr_n_) {
+        std::vector<std::pair<int32_t, int32_t>> tail;  // (row, series)
+        for (int32_t s = svc_csr_n_; s < n_series_; ++s) {
+          const int32_t v = svc_key(s);
+          if (v >= 0 && v < cap) tail.push_back({v, s});
+        }
+        std::stable_sort(tail.begin(), tail.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+        const size_t nt = tail.size();
+        last_gram_tail_ = (int64_t)nt;
+        if (nt) {
+          // one pinned block per call: [map m][off m+1][ids nt]
+          std::vector<int32_t> map, off, ids;
+          for (size_t i = 0; i < nt; ++i) {
+            if (i == 0 || tail[i].first != tail[i - 1].first) { map.push_back(tail[i].first); off.push_back((int32_t)i); }
+            ids.push_back(tail[i].second);
+          }
+          off.push_back((int32_t)nt);
+          const size_t m = map.size(), nb = (m + (m + 1) + nt) * 4;
+          if (nb > tail_csr_cap_) {
+            if (h_tail_csr_) HIP_OK(hipHostFree(h_tail_csr_));
+            HIP_OK(hipStreamSynchronize(stream));
+            tail_csr_cap_ = nb * 2 + 4096;
+            HIP_OK(hipHostMalloc((void**)&h_tail_csr_, tail_csr_cap_, hipHostMallocDefault));
+            d_tail_csr_ = (int32_t*)regrow(d_tail_csr_, d_tail_csr_cap_, tail_csr_cap_);
+          } else {
+            HIP_OK(hipEventSynchronize(tail_csr_ev_));  // the previous tail upload has been read
+          }
+          std::memcpy(h_tail_csr_, map.data(), m * 4);
+          std::memcpy(h_tail_csr_ + m, off.data(), (m + 1) * 4);
+          std::memcpy(h_tail_csr_ + 2 * m + 1, ids.data(), nt * 4);
+          HIP_OK(hipMemcpyAsync(d_tail_csr_, h_tail_csr_, nb, hipMemcpyHostToDevice, stream));
+          HIP_OK(hipEventRecord(tail_csr_ev_, stream));
+          apm_service_gram(d_tail_csr_ + m, d_tail_csr_ + 2 * m + 1, d_active_, (int32_t)m, cfg_.max_series,
+                           cfg_.n_lags, (const double* const*)d_lag_sum_ptrs_, (const double* const*)d_lag_comp_ptrs_,
+                           (const int32_t* const*)d_lag_cnt_ptrs_, d_dst, stream, d_tail_csr_, 1);
+        }
+      }
       return;
     }
   }

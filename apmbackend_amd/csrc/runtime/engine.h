@@ -727,6 +727,13 @@ class Engine {
   int32_t* d_svc_ids_ = nullptr;
   size_t svc_off_cap_ = 0, svc_ids_cap_ = 0;
   int32_t svc_csr_n_ = -1, svc_csr_cap_ = -1;
+  int32_t* h_tail_csr_ = nullptr;  // per-batch CSR of the series added since the snapshot (pinned)
+  int32_t* d_tail_csr_ = nullptr;
+  size_t tail_csr_cap_ = 0, d_tail_csr_cap_ = 0;
+  hipEvent_t tail_csr_ev_ = nullptr;
+ public:
+  int64_t last_gram_tail_ = 0;  // series the last Gram pack took from the tail CSR (tests)
+ private:
   int32_t* h_series_service_ = nullptr;  // pinned mirror of d_series_service_ (append-only uploads)
   uint8_t* d_suppressed_ = nullptr;
   uint64_t* d_emit_key_ = nullptr;

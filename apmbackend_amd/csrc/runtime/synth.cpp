@@ -109,6 +109,12 @@ struct Params {
   int anomaly_services = 0;
   double anomaly_factor = 1.0;
   int64_t anomaly_start_ms = INT64_MAX;
+  // distinct service pools (BASELINE config 5: 100k services over 256 JVMs): JVM g draws its
+  // ejb_services / provider_services names from a window of the pool starting at g * count, so
+  // neighbouring JVMs share part of their services and the node holds ejb_pool + provider_pool
+  // distinct names.  0 = every JVM uses the same names.
+  int ejb_pool = 0;
+  int provider_pool = 0;
 };
 
 class ServerGen {
@@ -179,7 +185,11 @@ class ServerGen {
     app_int(acct, 1000000000000000LL + (int64_t)(rng_.next() % 8999999999999999ULL));
     const int ejb = (int)(rng_.next() % (uint64_t)p_.ejb_services);
     char svc[32];
-    snprintf(svc, sizeof(svc), "getSvc%04d", ejb);
+    if (p_.ejb_pool > 0)
+      snprintf(svc, sizeof(svc), "getSvc%05d",
+               (int)(((int64_t)(idx_ + p_.server_offset) * p_.ejb_services + ejb) % p_.ejb_pool));
+    else
+      snprintf(svc, sizeof(svc), "getSvc%04d", ejb);
     int64_t total = elapsed(base_elapsed(0xABCDEFULL + ejb));
     if (ejb < p_.anomaly_services && t0 >= p_.anomaly_start_ms) total = (int64_t)((double)total * p_.anomaly_factor);
     const int64_t t_end = t0 + total;
@@ -216,7 +226,11 @@ class ServerGen {
     for (int i = 0; i < nsub; ++i) {
       const int pv = (int)(rng_.next() % (uint64_t)p_.provider_services);
       char pn[48];
-      snprintf(pn, sizeof(pn), "Provider[cb-util-%03d]", pv);
+      if (p_.provider_pool > 0)
+        snprintf(pn, sizeof(pn), "Provider[cb-util-%05d]",
+                 (int)(((int64_t)(idx_ + p_.server_offset) * p_.provider_services + pv) % p_.provider_pool));
+      else
+        snprintf(pn, sizeof(pn), "Provider[cb-util-%03d]", pv);
       int64_t el = elapsed(base_elapsed(0x55AA55ULL + pv) * 0.4);
       int64_t s_t = std::min(cursor, t_end - 1), e_t = std::min(s_t + el, t_end - 1);
       el = std::max<int64_t>(0, e_t - s_t);
@@ -337,7 +351,7 @@ void register_synth(py::module_& m) {
         g("missing", p.missing); g("late", p.late); g("no_acct", p.no_acct); g("sub_min", p.sub_min);
         g("sub_max", p.sub_max); g("seed", p.seed); g("server_offset", p.server_offset);
         g("anomaly_services", p.anomaly_services); g("anomaly_factor", p.anomaly_factor);
-        g("anomaly_start_ms", p.anomaly_start_ms);
+        g("anomaly_start_ms", p.anomaly_start_ms); g("ejb_pool", p.ejb_pool); g("provider_pool", p.provider_pool);
         return new SynthGen(p);
       }))
       .def("files", &SynthGen::files)

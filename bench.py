@@ -46,8 +46,17 @@ def _load_reference_baseline():
 
 PRESETS = {
     "headline": {},
+    # BASELINE config 2: 1 shard, 10k services, bf16 moment rings
     "config2": {"ring": "bfloat16"},
-    "firehose": {"servers": 32, "ejb": 2000, "providers": 1125, "tx_rate": 62.5, "ring": "bfloat16"},
+    # config 4: JMX (pull_jvm_stats) gauges + VM load fused with the transaction stream per JVM
+    # (K14 server rollup, `sx` rows) -- gauges pushed for every JVM every batch
+    "config4": {"jmx": True},
+    # config 5 (per GPU of the 8-GPU node): 256 JVMs / 100k distinct services -> 32 JVMs per GPU,
+    # each drawing 3125 services from a 64k EJB + 36k provider name pool (~100k series per GPU),
+    # bf16 rings sized for 3M series (~170 GB of HBM per GPU), fs/fb rows as COPY text into the
+    # native DB sink (spool), alerts + paging (notifier) on
+    "firehose": {"servers": 32, "ejb": 2000, "providers": 1125, "tx_rate": 62.5, "ring": "bfloat16",
+                 "ejb_pool": 64000, "provider_pool": 36000, "max_series": 3_000_000, "db_sink": "spool"},
 }
 
 
@@ -68,6 +77,13 @@ def main():
                          "config2 (same shard, bf16 moment rings), firehose (config 5: 256 JVMs / ~100k "
                          "services on 8 GPUs -> 32 JVMs x 3125 services per GPU, bf16 rings)")
     ap.add_argument("--gen-threads", type=int, default=16)
+    ap.add_argument("--ejb-pool", type=int, default=0, help="distinct EJB service names node-wide (0: shared)")
+    ap.add_argument("--provider-pool", type=int, default=0)
+    ap.add_argument("--max-series", type=int, default=0, help="series capacity per GPU (0: fit the shard)")
+    ap.add_argument("--jmx", action="store_true", help="config 4: fuse per-JVM JMX gauges + VM load (sx rows)")
+    ap.add_argument("--db-sink", default="none", choices=["none", "spool", "null"],
+                    help="db_insert streams into the native COPY sink (fs/fb COPY-formatted on the GPU) "
+                         "instead of raw text to --sink")
     ap.add_argument("--no-warm", action="store_true")
     ap.add_argument("--sink", default="/dev/null", help="file receiving the db_insert stream")
     ap.add_argument("--no-prefetch", action="store_true", help="disable the next-batch parse overlap")
@@ -109,12 +125,13 @@ def main():
     cfg = default_config()
     cfg["gpu"].update({
         "timezone": "UTC",
-        "maxSeries": max(4096, 1 << (args.servers * n_services - 1).bit_length()),
+        "maxSeries": args.max_series or max(4096, 1 << (args.servers * n_services - 1).bit_length()),
         "batchBytes": 48 << 20,
         "maxLinesPerBatch": 1 << 20,
         "zscoreMeanMode": args.mean_mode,
         "ringDtype": args.ring,
         "bucketCellCapacity": 16,
+        "serverRollup": bool(args.jmx),
     })
     if args.path == "service":
         from apmbackend_amd.runtime import service_bench
@@ -138,17 +155,34 @@ def main():
     # fs, al) in the wire format and write it to a sink (/dev/null: the DB loader is out of scope).
     from apmbackend_amd.models.pipeline import DB_OUTPUTS
     outs = DB_OUTPUTS + ("fb",)  # + the fleet-merged per-service baselines (rank 0, every interval)
+    if args.jmx:
+        outs = outs + ("sx",)
     eng = APMEngine(cfg, device=local, outputs=outs)
     sink_fd = os.open(args.sink, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    inserter = spool_dir = None
+    if args.db_sink != "none":
+        # production DB path: engine output lane -> native DbSink (COPY spool / null); al also
+        # feeds the e-mail notifier ("paging"), as in the service
+        import tempfile
+        from apmbackend_amd.runtime.notifier import AlertNotifier
+        from apmbackend_amd.runtime.sinks import DBInserter
+        spool_dir = tempfile.mkdtemp(prefix="apm_bench_spool_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+        cfg["streamInsertDb"].update({"sink": args.db_sink, "copySinkDir": spool_dir, "encoderThreads": 8,
+                                      "copySinkRotateBytes": 1 << 62})
+        inserter = DBInserter(cfg)
+        inserter.attach_engine(eng.eng, [k for k in outs if k in ("audit_db", "db", "fs", "fb")])
+        notifier = AlertNotifier(cfg)
     for k in outs:
-        eng.eng.set_sink_fd(k, sink_fd)
+        if inserter is None or k == "sx":
+            eng.eng.set_sink_fd(k, sink_fd)
     start = 1578391200000
     step_ms = int(args.batch_seconds * 1000)
     gen = N.SynthGen({"servers": args.servers, "ejb_services": args.ejb, "provider_services": args.providers,
                       "tx_per_sec_per_server": args.tx_rate, "seed": 1 + rank,
                       "server_offset": rank * args.servers,
                       "anomaly_services": args.anomaly_services, "anomaly_factor": args.anomaly_factor,
-                      "anomaly_start_ms": start + 2 * step_ms})
+                      "anomaly_start_ms": start + 2 * step_ms, "ejb_pool": args.ejb_pool,
+                      "provider_pool": args.provider_pool})
     for path, kind, server in gen.files():
         eng.add_file(path, {0: "SOAP", 1: "SERVER", 2: "APP"}[kind], server)
 
@@ -181,10 +215,21 @@ def main():
     last = 2 + args.warmup + args.steps - 1
     first_timed = 2 + args.warmup
 
+    jmx_lines = []
+    if args.jmx:  # one JMX record per JVM per batch (pull_jvm_stats.js at the bench's time scale)
+        from apmbackend_amd.runtime.jmx import SyntheticJmx
+        from apmbackend_amd.utils.records import JmxEntry
+        syn = SyntheticJmx(11 + rank)
+        jvms = sorted({srv for _p, _k, srv in gen.files()})
+        for b in range(n_batches):
+            jmx_lines.append([JmxEntry.from_stats(start + b * step_ms, srv, syn.payload(srv)).to_csv() for srv in jvms])
+
     def step(i):
         # the next batch's H2D + parse kernels are launched before this batch's host join
         # (double-buffered parse slots).  No prefetch across the timing boundaries: every timed
         # batch is parsed inside the timed region, and the last one has no successor.
+        for jl in (jmx_lines[i] if jmx_lines else ()):
+            eng.set_server_context(jl, vm_load=1.0 + 0.01 * (i % 50))
         ptr, n, chunks = batches[i]
         if i < last and i + 1 != first_timed and not args.no_prefetch:
             nptr, nn, nchunks = batches[i + 1]
@@ -206,8 +251,14 @@ def main():
         # window), like the z-score rings' synthetic pre-history above
         ac = cfg["streamProcessAlerts"]
         need = int(ac["requiredNumberBadIntervalsInAlertWindowToTrigger"]) - 1
-        hot = {f"getSvc{j:04d}" for j in range(args.anomaly_services)}
-        ser = [i for i, (_srv, svc) in enumerate(eng.eng.export_series()) if svc.split(":")[-1] in hot]
+        def hot_names(server):  # SynthGen's planted services as named on this JVM
+            if not args.ejb_pool:
+                return {f"getSvc{j:04d}" for j in range(args.anomaly_services)}
+            g = int(server[3:])
+            return {f"getSvc{(g * args.ejb + j) % args.ejb_pool:05d}" for j in range(args.anomaly_services)}
+        hot_by_server = {}
+        ser = [i for i, (srv, svc) in enumerate(eng.eng.export_series())
+               if svc.split(":")[-1] in hot_by_server.setdefault(srv, hot_names(srv))]
         for li in range(len(eng.ecfg["lags"])):
             eng.eng.import_alert_counters(li, ser, [need] * len(ser))
     torch.cuda.synchronize()
@@ -219,6 +270,13 @@ def main():
     for i in range(2 + args.warmup, 2 + args.warmup + args.steps):
         step(i)
     eng.eng.flush()  # the last batch's stats stage runs on the engine's stats thread
+    if inserter is not None:  # alerts paged + every DB row of the timed batches written
+        al = eng.eng.take_bytes("al")
+        if al:
+            inserter.consume_bytes(al)
+            notifier.add_lines(al.decode("utf-8").split("\n"))
+            notifier.tick()
+        inserter.flush_all()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -282,7 +340,14 @@ def main():
             "db_insert_bytes_total": out_bytes,
             "alerts": int(m1["alerts"] - m0["alerts"]),
             "alert_candidates": int(m1["alert_candidates"] - m0["alert_candidates"]),
+            "device_GB": round(eng.eng.device_bytes() / 1e9, 1),
         }
+        if inserter is not None:
+            st = inserter.sink_stats()
+            out["db_sink"] = {"writer": args.db_sink, "rows": st.get("rows"), "bytes": st.get("bytes"),
+                              "rows_per_s": round(st.get("rows", 0) / dt_max, 1), "failures": st.get("failures")}
+        if args.jmx:
+            out["sx_bytes"] = eng.eng.sink_bytes("sx")
         print(json.dumps(out), flush=True)
     if args.trace:
         eng.dump_trace(args.trace if world == 1 else f"{args.trace}.rank{rank}", pid=rank)
@@ -291,6 +356,10 @@ def main():
         dist.destroy_process_group()
     N.free_pinned(pinned)
     os.close(sink_fd)
+    if inserter is not None:
+        import shutil
+        inserter.close()
+        shutil.rmtree(spool_dir, ignore_errors=True)
 
 
 if __name__ == "__main__":

@@ -180,24 +180,27 @@ def test_native_fleet_exchange_single_rank():
 def test_fleet_moments_mfma_gram_matches_atomic_scatter():
     """The MFMA per-service Gram pack (v_mfma_f64_16x16x4f64, one wave per service) yields the
     same {n, sum, sum^2} per (service, LAG, stat) as the per-series fp64 atomic scatter, and is
-    bitwise reproducible across calls."""
-    lines, bl = synth_batches(5, duration=300, servers=3)
+    bitwise reproducible across calls -- including series created after the CSR snapshot, which
+    go through the per-batch tail CSR (a 9th JVM that starts logging late)."""
+    lines, bl = synth_batches(5, duration=300, servers=9)
     bl = list(bl)
     C = small_cfg("rolling")
     eng = APMEngine(C, keep_text=False)
     cap = 64
     n = cap * 2 * 3 * 3
-    half = len(bl) // 8
-    for now, chunks in bl[:half]:
-        eng.process_lines(chunks, now)
-    # snapshot the per-service CSR early: series added afterwards take the atomic tail path
+    cut = (len(bl) * 3) // 5
+    late = "jvm08"
+    for now, chunks in bl[:cut]:
+        eng.process_lines([(fp, ls) for fp, ls in chunks if late not in fp], now)
+    # snapshot the per-service CSR: jvm08's series arrive afterwards (1/9 of the table)
     early = torch.zeros((n,), dtype=torch.float64, device="cuda")
     eng.eng.pack_service_moments(early.data_ptr(), cap)
-    for now, chunks in bl[half:]:
+    for now, chunks in bl[cut:]:
         eng.process_lines(chunks, now)
     bufs = [torch.full((n,), -1.0, dtype=torch.float64, device="cuda") for _ in range(3)]
     eng.eng.pack_service_moments(bufs[0].data_ptr(), cap, atomic_path=True)
     eng.eng.pack_service_moments(bufs[1].data_ptr(), cap)
+    assert eng.eng.gram_tail_series() > 0  # the tail CSR path really ran
     eng.eng.pack_service_moments(bufs[2].data_ptr(), cap)
     torch.cuda.synchronize()
     ref, got, again = (b.cpu().numpy().reshape(cap, 2, 3, 3) for b in bufs)
