@@ -289,6 +289,11 @@ PYBIND11_MODULE(_apm_native, m) {
            py::arg("ptr"), py::arg("n"), py::arg("chunks"), py::arg("now") = -1.0, py::arg("next_ptr") = 0,
            py::arg("next_n") = 0,
            py::arg("next_chunks") = std::vector<std::tuple<int32_t, uint64_t, uint64_t>>())
+      .def("process_tx_lines", [](Engine& e, py::bytes b, double now) {
+             std::string v = b;
+             py::gil_scoped_release rel;
+             e.process_tx_lines(v, now);
+           }, py::arg("blob"), py::arg("now") = -1.0)
       .def("take", &Engine::take, py::call_guard<py::gil_scoped_release>())
       .def("flush", &Engine::flush, py::call_guard<py::gil_scoped_release>())
       .def("save_state", [](Engine& e, const std::string& path, py::bytes extra) {

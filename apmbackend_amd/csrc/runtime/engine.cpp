@@ -1021,6 +1021,61 @@ void Engine::process_batch_dev_tail(ParseSlot& ps, double t0, double now_overrid
   ++batch_no_;
 }
 
+// Transactions from a reference parser stage (the `transactions` queue, entries.js TxEntry
+// CSV) enter at the stats stage: one TxOut per line in arrival order, the line itself kept as the
+// pending tx text for the release (db stream).  Host-join mode only (the shards' text arenas
+// carry the lines; the device join has no such input).
+void Engine::process_tx_lines(const std::string& blob, double now) {
+  if (dev()) throw std::runtime_error("process_tx_lines needs gpu.joinOnDevice = false");
+  const double t0 = now_ms();
+  std::vector<std::vector<TxOut>> outs(shards_.size());
+  uint64_t line = 0;
+  size_t i = 0;
+  while (i < blob.size()) {
+    size_t j = blob.find('\n', i);
+    if (j == std::string::npos) j = blob.size();
+    const std::string_view ln(blob.data() + i, j - i);
+    i = j + 1;
+    if (ln.size() < 3 || ln.compare(0, 3, "tx|") != 0) continue;
+    std::string_view f[9];
+    int nf = 0;
+    size_t a = 0;
+    while (nf < 9) {
+      const size_t b = ln.find('|', a);
+      f[nf++] = ln.substr(a, b == std::string_view::npos ? std::string_view::npos : b - a);
+      if (b == std::string_view::npos) break;
+      a = b + 1;
+    }
+    if (nf < 8) { ++metrics_.tx_dropped; continue; }
+    const std::string srv(f[1]);
+    const auto known = server_ids_.find(srv);
+    const int32_t sid = known != server_ids_.end() ? known->second : add_server(srv);
+    if ((size_t)sid >= outs.size()) outs.resize(shards_.size());
+    const int32_t svc = dict_.service_id(f[2]);
+    std::string& arena = shards_[sid]->text();
+    TxOut t{};
+    t.seq = (1ULL << 63) | (line++ << 12);
+    t.server = sid;
+    t.service = svc;
+    t.raw_svc = svc;
+    t.end_ms = js::parse_int(f[6]);
+    t.elapsed = js::parse_int(f[7]);
+    t.line_off = (uint32_t)arena.size();
+    t.line_len = (uint32_t)ln.size();
+    t.to_db = false;
+    t.toplevel = nf > 8 && f[8] == "Y";
+    arena.append(ln.data(), ln.size());
+    arena += '\n';
+    outs[sid].push_back(t);
+  }
+  if (now >= 0 && now > watermark_) watermark_ = now;
+  outs.resize(shards_.size());
+  metrics_.lines += line;
+  post_stats(std::move(outs), /*multi=*/true, t0, INT64_MIN);
+  metrics_.t_total_ms += now_ms() - t0;
+  ++batch_no_;
+}
+
 void Engine::trace_event(const char* name, double t0, double t1, int tid) {
   if (!trace_on_) return;
   std::lock_guard<std::mutex> g(trace_mu_);

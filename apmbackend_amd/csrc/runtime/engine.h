@@ -211,6 +211,8 @@ class Engine {
                      double now_override = -1.0, const uint8_t* next_bytes = nullptr, uint64_t next_n = 0,
                      const std::vector<Chunk>* next_chunks = nullptr);
   bool prefetch_pending() const { return prefetched_; }
+  // tx CSV lines (a reference parser stage's `transactions` queue) straight into the stats stage
+  void process_tx_lines(const std::string& blob, double now = -1.0);
 
   // Text outputs accumulated since the last take: "transactions", "audit_db", "db", "st", "fs",
   // "al" (enabled by EngineConfig::outputs).  take() splits into lines; take_bytes() hands out

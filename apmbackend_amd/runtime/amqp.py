@@ -34,6 +34,8 @@ Q_DECLARE, Q_DECLARE_OK, Q_PURGE, Q_PURGE_OK = (50, 10), (50, 11), (50, 30), (50
 B_QOS, B_QOS_OK, B_CONSUME, B_CONSUME_OK = (60, 10), (60, 11), (60, 20), (60, 21)
 B_CANCEL, B_CANCEL_OK, B_PUBLISH, B_DELIVER = (60, 30), (60, 31), (60, 40), (60, 60)
 B_GET, B_GET_OK, B_GET_EMPTY, B_ACK = (60, 70), (60, 71), (60, 72), (60, 80)
+B_NACK = (60, 120)
+CONFIRM_SELECT, CONFIRM_SELECT_OK = (85, 10), (85, 11)
 
 
 class AMQPError(RuntimeError):
@@ -299,6 +301,12 @@ class Connection:
         self.flow_active = True
         self.on_pause = on_pause
         self.on_resume = on_resume
+        # publisher confirms (confirm.select): broker basic.ack / basic.nack per publish sequence
+        self.confirming = False
+        self._pub_seq = 0
+        self._unconfirmed: set = set()
+        self._nacked: list = []
+        self._confirm_cv = threading.Condition()
         self._handshake(p)
         self._reader = threading.Thread(target=self._read_loop, name="amqp-reader", daemon=True)
         self._reader.start()
@@ -420,6 +428,14 @@ class Connection:
             self._rpc.put(("error", f"connection closed by broker: {code} {text}"))
         elif cm == B_CANCEL:  # broker-side consumer cancel notification
             self._consumers.pop(r.shortstr(), None)
+        elif cm in (B_ACK, B_NACK) and self.confirming:  # publisher confirm
+            tag, multiple = r.longlong(), r.bit()
+            with self._confirm_cv:
+                done = {t for t in self._unconfirmed if t <= tag} if multiple else {tag}
+                if cm == B_NACK:
+                    self._nacked.extend(sorted(done & self._unconfirmed))
+                self._unconfirmed -= done
+                self._confirm_cv.notify_all()
         else:
             self._rpc.put((cm, r))
 
@@ -443,11 +459,43 @@ class Connection:
         data = method_frame(self.ch, B_PUBLISH, Writer().short(0).shortstr(exchange).shortstr(queue)
                             .bit(False).bit(False).bytes())
         data += content_frames(self.ch, body, self.frame_max, delivery_mode=2 if persistent else None)
-        self._send(data)
+        with self._wlock:  # the confirm sequence number follows the wire order of publishes
+            if self.confirming:
+                self._pub_seq += 1
+                with self._confirm_cv:
+                    self._unconfirmed.add(self._pub_seq)
+            self.sock.sendall(data)
         return self.flow_active and not self.blocked
+
+    def confirm_select(self):
+        """Put the channel in confirm mode (RabbitMQ publisher confirms)."""
+        if not self.confirming:
+            self._call(CONFIRM_SELECT, Writer().bit(False).bytes(), CONFIRM_SELECT_OK)
+            self.confirming = True
+
+    def wait_confirms(self, timeout: float = 30.0) -> bool:
+        """Blocks until every publish so far is acked; raises if the broker nacked any or the
+        connection died.  Returns False on timeout."""
+        import time as _t
+        end = _t.monotonic() + timeout
+        with self._confirm_cv:
+            while self._unconfirmed:
+                if self.closed:
+                    raise AMQPError("connection lost with unconfirmed publishes")
+                left = end - _t.monotonic()
+                if left <= 0:
+                    return False
+                self._confirm_cv.wait(min(left, 0.2))
+            if self._nacked:
+                n, self._nacked = self._nacked, []
+                raise AMQPError(f"broker nacked {len(n)} publishes")
+        return True
 
     def consume(self, queue: str, callback: Callable[[Message], None], consumer_tag: str = "",
                 no_ack: bool = False) -> str:
+        if not consumer_tag:  # a client-chosen tag: deliveries can race the consume-ok
+            import uuid
+            consumer_tag = f"apm.ctag-{uuid.uuid4().hex[:12]}"
         self._consumers[consumer_tag] = callback  # registered first: deliveries may race the -ok
         args = (Writer().short(0).shortstr(queue).shortstr(consumer_tag).bit(False).bit(no_ack).bit(False)
                 .bit(False).table({}).bytes())

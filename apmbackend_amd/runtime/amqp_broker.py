@@ -18,7 +18,7 @@ import struct
 import threading
 from typing import Deque, Dict, List, Optional, Tuple
 
-from .amqp import (B_ACK, B_CANCEL, B_CANCEL_OK, B_CONSUME, B_CONSUME_OK, B_DELIVER, B_GET, B_GET_EMPTY, B_GET_OK,
+from .amqp import (CONFIRM_SELECT, CONFIRM_SELECT_OK, B_ACK, B_CANCEL, B_CANCEL_OK, B_CONSUME, B_CONSUME_OK, B_DELIVER, B_GET, B_GET_EMPTY, B_GET_OK,
                    B_PUBLISH, B_QOS, B_QOS_OK, CH_CLOSE, CH_CLOSE_OK, CH_FLOW_OK, CH_OPEN, CH_OPEN_OK,
                    CONN_BLOCKED, CONN_CLOSE, CONN_CLOSE_OK, CONN_OPEN, CONN_OPEN_OK, CONN_START, CONN_START_OK,
                    CONN_TUNE, CONN_TUNE_OK, CONN_UNBLOCKED, FRAME_BODY, FRAME_HEADER, FRAME_METHOD, PROTOCOL_HEADER,
@@ -35,6 +35,7 @@ class _Queue:
         self.rr = 0
         self.published = 0
         self.delivered = 0
+        self.bytes = 0  # bodies held (the supervisor's per-queue memory view)
 
 
 class _Consumer:
@@ -106,6 +107,7 @@ class Broker:
                 return
             body, redelivered = q.msgs.popleft()
             q.delivered += 1
+            q.bytes -= len(body)
             c.conn.deliver(c, q, body, redelivered)
         self.check_alarm()
 
@@ -136,6 +138,8 @@ class _Conn:
         self.consumers: Dict[str, _Consumer] = {}
         self.pub: Optional[List] = None  # [queue_name, size, body]
         self.alive = True
+        self.confirm = False   # confirm.select'ed channel: every publish is acked in order
+        self.pub_seq = 0
 
     def send_raw(self, data: bytes):
         try:
@@ -203,6 +207,7 @@ class _Conn:
             for tag in sorted(self.unacked, reverse=True):
                 q, body = self.unacked[tag]
                 q.msgs.appendleft((body, True))
+                q.bytes += len(body)
             touched = {q for q, _ in self.unacked.values()}
             self.unacked.clear()
             for q in touched:
@@ -217,12 +222,15 @@ class _Conn:
         self.pub = None
         with self.b.lock:
             q = self.b.queues.get(name)
-            if q is None:  # default exchange drops unroutable messages
-                return
-            q.msgs.append((bytes(body), False))
-            q.published += 1
-            self.b.dispatch(q)
-            self.b.check_alarm()
+            if q is not None:  # the default exchange drops unroutable messages (still confirmed)
+                q.msgs.append((bytes(body), False))
+                q.published += 1
+                q.bytes += len(body)
+                self.b.dispatch(q)
+                self.b.check_alarm()
+        if self.confirm:
+            self.pub_seq += 1
+            self.send_raw(method_frame(1, B_ACK, Writer().longlong(self.pub_seq).bit(False).bytes()))
 
     def on_method(self, ch: int, payload: bytes) -> bool:
         r = Reader(payload)
@@ -309,6 +317,11 @@ class _Conn:
                 if c and c in c.queue.consumers:
                     c.queue.consumers.remove(c)
             self.send_raw(method_frame(ch, B_CANCEL_OK, Writer().shortstr(tag).bytes()))
+        elif cm == CONFIRM_SELECT:
+            nowait = r.bit()
+            self.confirm = True
+            if not nowait:
+                self.send_raw(method_frame(ch, CONFIRM_SELECT_OK))
         elif cm == B_PUBLISH:
             r.short()
             _exchange, rkey = r.shortstr(), r.shortstr()
@@ -324,6 +337,7 @@ class _Conn:
                     return True
                 body, redelivered = q.msgs.popleft()
                 q.delivered += 1
+                q.bytes -= len(body)
                 tag = self.next_tag
                 self.next_tag += 1
                 if not no_ack:

@@ -219,8 +219,14 @@ class ConsumerQueue:
 
 
 class QueueManager:
-    def __init__(self, url: str = "local://", stat_interval_s: float = 60.0, local_capacity: int = 0):
+    def __init__(self, url: str = "local://", stat_interval_s: float = 60.0, local_capacity: int = 0,
+                 confirms: bool = False, persistent: bool = False):
+        """``confirms``: publisher confirms on the producer channel (wait_confirms() before the
+        caller commits its own progress, e.g. tail offsets -> at-least-once delivery across a
+        crash); ``persistent``: delivery_mode 2 (durable queues keep them across a broker restart)."""
         self.url = url
+        self.confirms = confirms
+        self.persistent = persistent
         self.backend = "local" if url.startswith("local:") else "amqp"
         self.stats = QueueStats(stat_interval_s)
         self.queues: Dict[str, object] = {}
@@ -244,6 +250,8 @@ class QueueManager:
         if self._prod is None:
             from .amqp import Connection
             self._prod = Connection(self.url, on_pause=self._broker_pause, on_resume=self._broker_resume)
+            if self.confirms:
+                self._prod.confirm_select()
         return self._prod
 
     def _consumer_conn(self):
@@ -263,7 +271,14 @@ class QueueManager:
     def _publish(self, name: str, body: bytes) -> bool:
         if self.backend == "local":
             return LOCAL.put(name, body)
-        return self._producer_conn().publish(name, body)
+        return self._producer_conn().publish(name, body, persistent=self.persistent)
+
+    def wait_confirms(self, timeout: float = 30.0) -> bool:
+        """Every message published so far is safely with the broker (no-op without confirms or
+        on the in-process backend)."""
+        if self.backend == "local" or not self.confirms or self._prod is None:
+            return True
+        return self._prod.wait_confirms(timeout)
 
     def _on_producer_pause(self, q: ProducerQueue):
         with self._lock:

@@ -102,6 +102,14 @@ class IngestService:
         apmlog.set_global_logger(self.cfg.get("logDir"), self._log_prefix(), colorize=True)
         self.mode = g.get("outputMode", "inproc")
         self.bridge = list(g.get("bridgeQueues", []))
+        # inputMode "transactions": a reference parser stage (stream_parse_transactions.js) keeps
+        # tailing and publishing `transactions`; this engine consumes them and takes over stats,
+        # z-score, alerts and the DB hand-off (mixed deployment / staged cut-over)
+        self.input_mode = g.get("inputMode", "logs")
+        if self.input_mode == "transactions":
+            if engine != "native":
+                raise ValueError("inputMode=transactions needs the native engine")
+            g["joinOnDevice"] = False  # tx arrive joined: the host stats path takes them
 
         # ---- files -> this rank's shard
         all_files = list(files) if files is not None else discover_files(self.cfg)
@@ -125,6 +133,8 @@ class IngestService:
             outs.discard("")
         self.outputs = [k for k in OUT_KINDS if k in outs]
         self.outs_set = set(self.outputs)
+        if self.mode == "amqp" and "z_score" in self.bridge:
+            self.outputs = [k for k in OUT_KINDS if k in set(self.outputs) | {"fs"}]
         if engine == "native":
             self.eng = APMEngine(self.cfg, device=self.local_rank, outputs=self.outputs)
             self.native = self.eng.eng
@@ -174,7 +184,7 @@ class IngestService:
             self._restore_offsets_resharded()
         # read-ahead into pinned slots (native engine): the tailer fills the next slot while the
         # engine works on the current one, and the engine prefetches (H2D + parse) the batch after
-        self.readahead = engine == "native" and as_bool(g.get("tailReadAhead", True))
+        self.readahead = engine == "native" and as_bool(g.get("tailReadAhead", True)) and self.input_mode == "logs"
         self._slots: List[int] = []
         self._held = None  # batch taken from the read-ahead ring and handed to the engine as prefetch
         self._stopping = False
@@ -199,10 +209,13 @@ class IngestService:
                                                           if (k in DB_OUTPUTS and k != "al") or k == "fb"])
         elif self.mode == "amqp":
             from .queue import QueueManager
-            self.qm = QueueManager(self.cfg["amqpConnectionString"], self.cfg.get("statLogIntervalInSeconds", 60))
+            self.qm = QueueManager(self.cfg["amqpConnectionString"], self.cfg.get("statLogIntervalInSeconds", 60),
+                                   confirms=as_bool(g.get("publisherConfirms", True)),
+                                   persistent=as_bool(g.get("persistentMessages", True)))
             self.producers["db"] = self.qm.get_queue(self.cfg.get("dbInsertQueue", "db_insert"), "p")
             qmap = {"transactions": self.cfg["streamParseTransactions"].get("outQueue", "transactions"),
-                    "stats": self.cfg["streamCalcStats"].get("outQueue", "stats")}
+                    "stats": self.cfg["streamCalcStats"].get("outQueue", "stats"),
+                    "z_score": self.cfg["streamCalcZScore"].get("outQueue", "z_score")}
             for q in self.bridge:
                 if q in qmap:
                     self.producers[q] = self.qm.get_queue(qmap[q], "p")
@@ -212,6 +225,19 @@ class IngestService:
         elif self.mode != "none":
             raise ValueError(f"unknown gpu.outputMode {self.mode!r}")
         self.notifier = AlertNotifier(self.cfg, clock=clock) if self.rank == 0 or self.world == 1 else None
+
+        # ---- input queue (inputMode transactions)
+        self.in_qm = None
+        self._in_lines: List[bytes] = []
+        if self.input_mode == "transactions":
+            import threading
+            from .queue import QueueManager as _QM
+            self._in_lock = threading.Lock()
+            self.in_qm = self.qm if self.qm is not None else _QM(self.cfg["amqpConnectionString"],
+                                                                 self.cfg.get("statLogIntervalInSeconds", 60))
+            inq = self.cfg["streamCalcStats"].get("inQueue", "transactions")
+            self.in_queue = self.in_qm.get_queue(inq, "c", self._on_tx_message)
+            self.in_queue.start_consume()
 
         # ---- fleet exchange
         self.fleet = None
@@ -360,6 +386,10 @@ class IngestService:
         t0 = time.perf_counter()
         # undelivered output goes out first so the checkpoint and the sinks agree
         self._drain_outputs()
+        if self.qm is not None and not self.qm.wait_confirms(float(self.cfg["gpu"].get("confirmTimeoutSeconds", 60))):
+            # offsets may only advance past data the broker has taken responsibility for
+            log.warning("checkpoint postponed: the broker has not confirmed every publish yet")
+            return None
         extra = json.dumps({"tail": json.loads(self.tailer.offsets_json()), "world": self.world,
                             "rank": self.rank, "servers": self.my_servers}).encode("utf-8")
         prefix = ck[:-len(".ckpt")]
@@ -430,6 +460,8 @@ class IngestService:
                     prod = self.producers.get("stats")
                 if prod is not None:
                     prod.write_lines(ln for ln in blob.decode("utf-8").split("\n") if ln)
+                if k == "fs" and "z_score" in self.producers:  # the z-score stage's output queue
+                    self.producers["z_score"].write_lines(ln for ln in blob.decode("utf-8").split("\n") if ln)
         return counts
 
     def _on_jx(self, line: str):
@@ -518,6 +550,8 @@ class IngestService:
         # its tails have nothing new or downstream is paused -- or the collective sequences diverge.
         lockstep = self.fleet is not None
         paused = self.qm is not None and any(getattr(p, "paused", False) for p in self.producers.values())
+        if self.input_mode == "transactions":
+            return 0 if paused and not lockstep else self._step_tx(lockstep)
         if self.readahead:
             return self._step_readahead(lockstep, paused)
         if paused:
@@ -553,6 +587,22 @@ class IngestService:
                 self.native.process_batch(buf, chunks, -1.0)
         self._drain_outputs()
         return len(buf)
+
+    def _on_tx_message(self, body: bytes):
+        with self._in_lock:
+            self._in_lines.append(body)
+
+    def _step_tx(self, lockstep: bool) -> int:
+        with self._in_lock:
+            lines, self._in_lines = self._in_lines, []
+        if not lines and not lockstep:
+            return 0
+        blob = b"\n".join(ln.rstrip(b"\n") for ln in lines) + (b"\n" if lines else b"")
+        self.native.process_tx_lines(blob, -1.0)
+        self.polls += 1
+        self.batches += 1
+        self._drain_outputs()
+        return len(blob)
 
     def _ckpt_due(self) -> bool:
         return bool(self.ckpt_dir) and self.eng is not None and self.clock() - self.last_ckpt >= self.ckpt_every
@@ -677,7 +727,10 @@ class IngestService:
         if self.notifier is not None:
             self.notifier.tick()
         if self.qm is not None:
+            self.qm.wait_confirms(float(self.cfg["gpu"].get("confirmTimeoutSeconds", 60)))
             self.qm.shutdown()
+        if self.in_qm is not None and self.in_qm is not self.qm:
+            self.in_qm.shutdown()
 
 
 def main(argv=None):  # pragma: no cover - process entry point

@@ -390,8 +390,10 @@ class Supervisor:
 
     # ------------------------------------------------------------------ monitoring
     def inspect(self):
+        broker_up = self.inspect_broker()
         self.inspect_disk()
-        self.inspect_queues()
+        if broker_up:
+            self.inspect_queues()
         self.inspect_modules()
 
     def inspect_disk(self):
@@ -408,24 +410,117 @@ class Supervisor:
             self.add_alert(f"Disk space percentage used is high on mount: {mount} - Size: {size:.0f} GB, Used: "
                            f"{used:.0f} GB, Available: {avail:.0f} GB, PercentUsed: {pct:.0f}%")
 
-    def inspect_queues(self):
-        if self.cfg.get("gpu", {}).get("outputMode", "inproc") != "amqp":
-            return
-        try:
+    # ---- broker supervision (apm_manager.js rabbitMQIsRunning / startRabbitMQ :134-155,
+    # inspectQueues :429-453, monitorResourcesRecurs :517-521)
+    def _uses_broker(self) -> bool:
+        g = self.cfg.get("gpu", {})
+        return g.get("outputMode", "inproc") == "amqp" or g.get("inputMode", "logs") == "transactions"
+
+    def _rabbitmqctl(self) -> Optional[str]:
+        sbin = self.m.get("rabbitSbinPath")
+        p = os.path.join(sbin, "rabbitmqctl") if sbin else None
+        return p if p and os.path.exists(p) else None
+
+    def broker_is_running(self) -> bool:
+        ctl = self._rabbitmqctl()
+        if ctl:
+            try:
+                return subprocess.run([ctl, "status"], capture_output=True, timeout=30).returncode == 0
+            except (OSError, subprocess.TimeoutExpired):
+                return False
+        try:  # no RabbitMQ tooling (our own broker, or a remote one): an AMQP handshake decides
             from .amqp import Connection
-            c = Connection(self.cfg["amqpConnectionString"], timeout=3)
-        except Exception as e:
-            self.add_alert(f"Could not inspect queues: broker unreachable: {e}")
-            return
+            Connection(self.cfg["amqpConnectionString"], timeout=3).close()
+            return True
+        except Exception:
+            return False
+
+    def start_broker(self):
+        log.info("Attempting to start the message broker...")
+        sbin = self.m.get("rabbitSbinPath")
+        server = os.path.join(sbin, "rabbitmq-server") if sbin else None
         try:
-            names = {self.cfg.get("dbInsertQueue", "db_insert")}
-            for q in names:
+            if server and os.path.exists(server):
+                out = subprocess.run([server, "-detached"], capture_output=True, timeout=60)
+                log.info("RabbitMQ started! Output: %s", out.stdout.decode(errors="replace").strip())
+            elif self.m.get("brokerCommand"):
+                # a configured broker command (e.g. python -m apmbackend_amd.runtime.amqp_broker),
+                # started detached like rabbitmq-server -detached
+                argv = shlex.split(self.m["brokerCommand"])
+                with open(os.path.join(self.cfg.get("logDir") or ".", "broker.start.log"), "a") as lf:
+                    subprocess.Popen(argv, stdout=lf, stderr=subprocess.STDOUT, start_new_session=True)
+            else:
+                self.add_alert("Broker is down and neither applicationManager.rabbitSbinPath nor brokerCommand "
+                               "is configured to start it")
+                return
+        except Exception as e:
+            log.error("Start of the broker threw an error: %s", e)
+            self.add_alert(f"Start of RabbitMQ threw an error: {e}")
+
+    def inspect_broker(self) -> bool:
+        """Liveness + auto-start; True when the broker is up."""
+        if not self._uses_broker():
+            return True
+        now = self.clock()
+        if self.broker_is_running():
+            return True
+        if now < getattr(self, "_broker_grace_until", 0.0):
+            return False  # a start is in progress (the reference sleeps 30 s here)
+        self.add_alert("RabbitMQ is down, attempting to restart it.")
+        self.start_broker()
+        self._broker_grace_until = now + float(self.m.get("brokerStartGraceSeconds", 30))
+        return False
+
+    def _queue_rows(self):
+        """(name, messages, memory MB or None) per queue."""
+        ctl = self._rabbitmqctl()
+        if ctl:
+            out = subprocess.run([ctl, "list_queues", "--quiet", "--no-table-headers", "name", "messages_ram",
+                                  "message_bytes_ram", "messages_persistent", "message_bytes_persistent", "memory"],
+                                 capture_output=True, timeout=60)
+            if out.returncode != 0:
+                raise RuntimeError(out.stderr.decode(errors="replace").strip())
+            rows = []
+            for line in out.stdout.decode(errors="replace").splitlines():
+                f = line.split()
+                if len(f) < 6:
+                    continue
+                rows.append((f[0], int(f[1]) + int(f[3]), int(f[5]) / 1024.0 / 1024.0))
+            return rows
+        from .amqp import Connection
+        c = Connection(self.cfg["amqpConnectionString"], timeout=3)
+        try:
+            names = [self.cfg.get("dbInsertQueue", "db_insert"),
+                     self.cfg["streamParseTransactions"].get("outQueue", "transactions"),
+                     self.cfg["streamCalcStats"].get("outQueue", "stats"),
+                     self.cfg["streamCalcZScore"].get("outQueue", "z_score"),
+                     self.cfg.get("gpu", {}).get("fleetQueue", "fleet_baseline")]
+            rows = []
+            for q in dict.fromkeys(names):
                 _n, msgs, _c = c.queue_declare(q, durable=True)
-                if msgs > float(self.m.get("queueMessageAlertThreshold", 1e6)):
-                    self.add_alert(f"Queue exceeded the message count threshold - Queue: {q} Threshold: "
-                                   f"{self.m.get('queueMessageAlertThreshold')} MessageCount: {msgs}")
+                rows.append((q, msgs, None))
+            return rows
         finally:
             c.close()
+
+    def inspect_queues(self):
+        if not self._uses_broker():
+            return
+        try:
+            rows = self._queue_rows()
+        except Exception as e:
+            self.add_alert(f"Could not inspect queues via rabbit controller: {e}")
+            return
+        cnt_thr = float(self.m.get("queueMessageAlertThreshold", 1e6))
+        mem_thr = float(self.m.get("queueMemoryAlertThreshold", 1e9))
+        for name, msgs, mem_mb in rows:
+            log.debug("QUEUE: %s Count: %d MemMb: %s", name, msgs, "-" if mem_mb is None else f"{mem_mb:.1f}")
+            if msgs > cnt_thr:
+                self.add_alert(f"Queue exceeded the message count threshold - Queue: {name} Threshold: "
+                               f"{self.m.get('queueMessageAlertThreshold')} MessageCount: {msgs}")
+            if mem_mb is not None and mem_mb > mem_thr:
+                self.add_alert(f"Queue exceeded the memory threshold - Queue: {name} Threshold: "
+                               f"{self.m.get('queueMemoryAlertThreshold')} MemoryUsed(Mb): {mem_mb:.1f}")
 
     def inspect_modules(self):
         for mod in self.modules:

@@ -136,3 +136,18 @@ def test_queue_stats_alignment():
     s.add_counter("a", "c")
     s.incr("a", 3)
     assert s.line() == "IN<a: 3" and s.line() == "IN<a: 0"
+
+
+def test_publisher_confirms_and_persistent_messages(broker):
+    """Q15: the bridge publishes persistent messages on a confirm.select'ed channel and can wait
+    until the broker acknowledged everything (before committing tail offsets)."""
+    qm = QueueManager(broker.url, confirms=True, persistent=True)
+    p = qm.get_queue("db_insert", "p")
+    for i in range(200):
+        p.write_line(f"fs|{i}")
+    assert qm.wait_confirms(10.0)
+    assert qm._prod._unconfirmed == set() and qm._prod._pub_seq == 200
+    assert broker.stats()["db_insert"]["messages"] == 200
+    qm.shutdown()
+    local = QueueManager("local://", confirms=True)
+    assert local.wait_confirms(0.1)  # in-process backend: nothing to wait for

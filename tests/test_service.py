@@ -286,7 +286,7 @@ def test_paused_lockstep_rank_still_joins_the_collective():
         svc = IngestService.__new__(IngestService)
         svc.qm, svc.producers = object(), {"db": Prod()}
         svc.fleet = object() if lockstep else None
-        svc.readahead, svc.tailer, svc.native = False, Tail(), Eng()
+        svc.readahead, svc.tailer, svc.native, svc.input_mode = False, Tail(), Eng(), "logs"
         svc.polls, svc.batches, svc.fault, svc.rank, svc.outputs = 0, 0, {}, 0, []
         svc.inserter, svc.notifier = None, None
         svc.step()

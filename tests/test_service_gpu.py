@@ -121,3 +121,74 @@ def test_readahead_service_processes_every_line(tmp_path):
     key = lambda rows: sorted("\t".join(r.split("\t")[:5] + r.split("\t")[6:]) for r in rows)
     assert key(nat["tx"]) == key(cpu["tx"]) and len(nat["tx"]) > 0
     assert len(nat["stats"]) > 0
+
+
+def test_transactions_queue_roundtrip_with_reference_stages(tmp_path):
+    """Mixed deployment: a reference parser stage publishes tx lines (entries.js TxEntry CSV,
+    one message per line) to `transactions`; the GPU engine (inputMode transactions) takes over
+    stats / z-score / alerts and publishes fs to `z_score` -- what stream_process_alerts.js
+    consumes -- and tx / fs / al to db_insert, persistent and publisher-confirmed."""
+    import time as _time
+    from apmbackend_amd.models.oracle import PipelineOracle
+    from apmbackend_amd.runtime.amqp_broker import Broker
+    from apmbackend_amd.runtime.queue import QueueManager
+    from apmbackend_amd.utils.synth import with_watermarks
+    from apmbackend_amd.utils.timeparse import TzOffset
+    C, lines, mapping, sc = make_env(tmp_path)
+    gpu_cfg(C)
+    P = PipelineOracle(copy.deepcopy(C), TzOffset("UTC"))
+    P.run_batches(with_watermarks(batches(lines, sc.start_ms, 5.0), TzOffset("UTC")))
+    assert P.tx_out and P.fs and P.al
+    b = Broker(port=0).start()
+    try:
+        C["amqpConnectionString"] = b.url
+        C["gpu"].update({"outputMode": "amqp", "inputMode": "transactions", "bridgeQueues": ["z_score"]})
+        svc = IngestService(C, engine="native", files=[], rank=0, world=1, server_of_path=srv_of)
+        ref = QueueManager(b.url)  # the reference parser's producer side
+        prod = ref.get_queue("transactions", "p")
+        for i in range(0, len(P.tx_out), 37):
+            prod.write_lines(P.tx_out[i:i + 37])
+            _time.sleep(0.01)
+            svc.step()
+        deadline = _time.time() + 60
+        while svc.native.metrics()["tx"] < len(P.tx_out) and _time.time() < deadline:
+            svc.step()
+            _time.sleep(0.02)
+        svc.native.flush()
+        svc._drain_outputs()
+        assert svc.native.metrics()["tx"] == len(P.tx_out), (svc.native.metrics()["tx"], len(P.tx_out), {
+            k: (getattr(p, "paused", None), p.buffer_count()) for k, p in svc.producers.items()}, b.stats())
+        assert svc.qm.wait_confirms(10.0)
+        got_z, got_db = [], []
+        zc = amqp_collect(b.url, "z_score", got_z)
+        dc = amqp_collect(b.url, "db_insert", got_db)
+        assert wait_until(lambda: len(got_z) >= len(P.fs))
+        assert got_z == P.fs
+        assert wait_until(lambda: sum(1 for l in got_db if l.startswith("al|")) >= len(P.al)
+                          and sum(1 for l in got_db if l.startswith("fs|")) >= len(P.fs))
+        assert [l for l in got_db if l.startswith("al|")] == P.al
+        assert [l for l in got_db if l.startswith("fs|")] == P.fs
+        zc.close()
+        dc.close()
+        svc.shutdown()
+        ref.shutdown()
+    finally:
+        b.stop()
+
+
+def wait_until(pred, timeout=20.0):
+    import time as _time
+    t0 = _time.time()
+    while _time.time() - t0 < timeout:
+        if pred():
+            return True
+        _time.sleep(0.05)
+    return pred()
+
+
+def amqp_collect(url, queue, out):
+    from apmbackend_amd.runtime.amqp import Connection
+    c = Connection(url)
+    c.queue_declare(queue)
+    c.consume(queue, lambda m: (out.append(m.body.decode()), c.ack(m.delivery_tag)))
+    return c

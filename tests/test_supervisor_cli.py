@@ -202,3 +202,33 @@ def test_elastic_degrade_can_be_disabled(tmp_path):
         assert mod.generation == 0 and mod.ranks == 2 and not mod.bad_devices
     finally:
         s.stop_all()
+
+
+def test_broker_liveness_autostart_and_queue_thresholds(tmp_path):
+    """monitorResourcesRecurs / rabbitMQIsRunning / startRabbitMQ / inspectQueues
+    (apm_manager.js:134-155, 429-453, 517-521) with a stand-in rabbitmqctl + rabbitmq-server."""
+    sbin = tmp_path / "sbin"
+    sbin.mkdir()
+    up = tmp_path / "broker_up"
+    (sbin / "rabbitmqctl").write_text(
+        "#!/bin/sh\n"
+        f"[ -f {up} ] || exit 2\n"
+        "if [ \"$1\" = list_queues ]; then\n"
+        "  echo 'db_insert 5 100 2000000 900000000 1300000000'\n"
+        "  echo 'transactions 3 10 0 0 4096'\n"
+        "fi\n")
+    (sbin / "rabbitmq-server").write_text(f"#!/bin/sh\ntouch {up}\necho started\n")
+    for f in ("rabbitmqctl", "rabbitmq-server"):
+        os.chmod(sbin / f, 0o755)
+    C = make_cfg(tmp_path, [], rabbitSbinPath=str(sbin), queueMessageAlertThreshold=1000000,
+                 queueMemoryAlertThreshold=1000, brokerStartGraceSeconds=0)
+    C["gpu"]["outputMode"] = "amqp"
+    s = sup.Supervisor(C, mailer=Mailer(outbox=str(tmp_path / "out")))
+    assert not s.broker_is_running()
+    assert not s.inspect_broker()  # down -> alert + rabbitmq-server -detached
+    assert up.exists() and s.broker_is_running()
+    s.inspect_queues()
+    alerts = "\n".join(s.alert_buffer)
+    assert "RabbitMQ is down" in alerts
+    assert "message count threshold - Queue: db_insert" in alerts and "MessageCount: 2000005" in alerts
+    assert "memory threshold - Queue: db_insert" in alerts and "transactions" not in alerts.split("memory")[-1]
