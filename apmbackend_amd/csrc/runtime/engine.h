@@ -443,8 +443,10 @@ class Engine {
   // so the moments matrix is indexed by a node-wide *slot*: new services travel (hash + name) in
   // an all-gather of the lock-step round, and every rank assigns slots to unseen hashes in rank
   // order -- identical tables everywhere, no coordinator.
-  static constexpr size_t kRegBlock = 65536;
-  static constexpr int kRegMaxEntries = 1024;
+  // one round carries a whole shard's worth of new services (10k names ~ 400 KB), so the
+  // registry settles within the first batches instead of trickling through the timed region
+  static constexpr size_t kRegBlock = 1 << 20;
+  static constexpr int kRegMaxEntries = 32768;
   struct RegPending { int32_t id; uint64_t hash; std::string name; uint64_t tag; };  // tag: batch queued in
   std::mutex reg_mu_;
   std::deque<RegPending> reg_pending_;                     // stats thread -> ingest thread
