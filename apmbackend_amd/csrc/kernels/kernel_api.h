@@ -187,10 +187,12 @@ void apm_format_write(apm::FormatArgs* a, hipStream_t stream);
 void apm_alert_eval(apm::AlertArgs* a, hipStream_t stream);
 size_t apm_fleet_format_tmp_bytes(int32_t n_rows);
 int apm_fleet_format(apm::FleetFormatArgs* a, void* tmp, size_t tmp_bytes, hipStream_t stream);
-// rows of the alert candidates (window stats + the candidate LAG's z-score output), compacted in
-// candidate order: the host formats al rows from n records instead of downloading every series
-void apm_alert_gather(const apm::AlertRec* alerts, int32_t n, const apm::WinStat* win, const apm::ZOut* const* z_by_lag,
-                      int32_t n_lags, apm::WinStat* win_out, apm::ZOut* z_out, hipStream_t stream);
+// after K11: the candidate count (clamped to max_n), the candidates and -- rows != 0 -- their window
+// stats and candidate-LAG z-score rows, written into host-mapped pinned buffers (device pointers
+// of hipHostMalloc memory) in candidate order
+void apm_alert_gather(const apm::AlertRec* alerts, const int32_t* n_dev, int32_t max_n, const apm::WinStat* win,
+                      const apm::ZOut* const* z_by_lag, int32_t n_lags, int32_t rows, apm::AlertRec* alerts_out,
+                      apm::WinStat* win_out, apm::ZOut* z_out, int32_t* n_out, hipStream_t stream);
 // fleet.hip
 void apm_service_moments(const int32_t* series_service, const uint8_t* active, int32_t n_series, int32_t S,
                          int32_t n_lags, int32_t n_services_cap, const double* const* sums, const double* const* comps,

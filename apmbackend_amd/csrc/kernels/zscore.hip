@@ -374,28 +374,41 @@ void apm_zscore_warm(ZArgs* a, int dtype_bytes, int fill, uint64_t seed, const W
 
 struct AlertGather {
   const AlertRec* alerts;
+  const int32_t* n_dev;  // the K11 candidate count (device)
   const WinStat* win;
   const ZOut* z[MAX_LAGS];
+  AlertRec* alerts_out;  // host-mapped pinned buffers: the records land in host memory directly
   WinStat* win_out;
   ZOut* z_out;
-  int32_t n;
+  int32_t* n_out;
+  int32_t max_n;
+  int32_t rows;
 };
 
+// One pass after K11: the candidate count, the candidates and (for al rows) their window stats and
+// z-score rows are written straight into pinned host memory, so the stats thread learns the
+// count, and reads the rows, by waiting on one event instead of a stream drain + three D2H copies.
 __global__ void k_alert_gather(AlertGather a) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.n) return;
+  const int n = min(*a.n_dev, a.max_n);
+  if (i == 0) *a.n_out = n;
+  if (i >= n) return;
   const AlertRec r = a.alerts[i];
+  a.alerts_out[i] = r;
+  if (!a.rows) return;
   a.win_out[i] = a.win[r.series];
   a.z_out[i] = a.z[r.lag_idx][r.series];
 }
 
-void apm_alert_gather(const AlertRec* alerts, int32_t n, const WinStat* win, const ZOut* const* z_by_lag, int32_t n_lags,
-                      WinStat* win_out, ZOut* z_out, hipStream_t stream) {
-  if (n <= 0) return;
+void apm_alert_gather(const AlertRec* alerts, const int32_t* n_dev, int32_t max_n, const WinStat* win,
+                      const ZOut* const* z_by_lag, int32_t n_lags, int32_t rows, AlertRec* alerts_out, WinStat* win_out,
+                      ZOut* z_out, int32_t* n_out, hipStream_t stream) {
+  if (max_n <= 0) return;
   AlertGather a{};
-  a.alerts = alerts; a.win = win; a.win_out = win_out; a.z_out = z_out; a.n = n;
+  a.alerts = alerts; a.n_dev = n_dev; a.win = win; a.alerts_out = alerts_out; a.win_out = win_out; a.z_out = z_out;
+  a.n_out = n_out; a.max_n = max_n; a.rows = rows;
   for (int l = 0; l < n_lags && l < MAX_LAGS; ++l) a.z[l] = z_by_lag[l];
-  hipLaunchKernelGGL(k_alert_gather, dim3((n + 255) / 256), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(k_alert_gather, dim3((max_n + 255) / 256), dim3(256), 0, stream, a);
 }
 
 void apm_alert_eval(AlertArgs* a, hipStream_t stream) {

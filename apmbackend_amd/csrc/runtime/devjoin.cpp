@@ -236,8 +236,14 @@ void DeviceJoin::host_prepass(int k, const uint8_t* hb, uint32_t n_host, const P
   hbuf_.clear();
   std::unordered_map<int32_t, int> task_of;
   int nt = 0;
+  int32_t last_file = -1;
+  int last_t = -1;
   for (uint32_t i = 0; i < n_host; ++i) {
     const int32_t file = s.chunk_file[s.h_host_ev[i].chunk];
+    if (file == last_file) {  // events come in chunk order: runs of one file
+      tasks_[last_t].idx.push_back(i);
+      continue;
+    }
     auto it = task_of.find(file);
     int t;
     if (it == task_of.end()) {
@@ -252,6 +258,8 @@ void DeviceJoin::host_prepass(int k, const uint8_t* hb, uint32_t n_host, const P
     } else {
       t = it->second;
     }
+    last_file = file;
+    last_t = t;
     tasks_[t].idx.push_back(i);
   }
   auto work = [&](int t) {
@@ -644,8 +652,20 @@ void DeviceJoin::maybe_rebuild(double now, hipStream_t s) {
     throw std::runtime_error("device join: live join keys exceed half of gpu.joinTableSlots");
 }
 
+void DeviceJoin::prepass_ahead(int k, const uint8_t* hb, const ParallelFor& parallel) {
+  if (ahead_k_ >= 0) throw std::runtime_error("device join: a pre-pass is already ahead");
+  // hops_ / hbuf_ still hold the running batch's ops (register_misses reads hbuf_ after sync A)
+  std::swap(hops_, hops_ahead_);
+  std::swap(hbuf_, hbuf_ahead_);
+  host_prepass(k, hb, *sl_[k].h_n_host, parallel);
+  std::swap(hops_, hops_ahead_);
+  std::swap(hbuf_, hbuf_ahead_);
+  ahead_k_ = k;
+}
+
 void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64_t batch_no, bool want_tx,
-                     bool want_db, DevJoinBatch& out, const ParallelFor& parallel) {
+                     bool want_db, DevJoinBatch& out, const ParallelFor& parallel,
+                     const std::function<void()>* meanwhile) {
   Slot& s = sl_[k];
   hipStream_t st = stream_;
   if (n_ev > cfg_.max_events) throw std::runtime_error("device join: more events than maxLinesPerBatch");
@@ -653,8 +673,18 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64
   events_ += n_ev;
   phase_t[0] = clock_ms();
   // ---- host pre-pass (audit blocks, PM_HOST lines)
-  const uint32_t n_host = *s.h_n_host;
-  host_prepass(k, hb, n_host, parallel);
+  if (ahead_k_ == k) {  // done by prepass_ahead while the previous batch's kernels ran
+    std::swap(hops_, hops_ahead_);
+    std::swap(hbuf_, hbuf_ahead_);
+    ahead_k_ = -1;
+  } else {
+    if (ahead_k_ >= 0) throw std::runtime_error("device join: pre-pass ahead for another slot");
+    host_prepass(k, hb, *s.h_n_host, parallel);
+  }
+  phase_t[1] = clock_ms();
+  spans.clear();
+  double sp = phase_t[1];
+  auto span = [&](const char* name) { const double t = clock_ms(); spans.push_back({name, {sp, t}}); sp = t; };
   if (hops_.size() > h_hops_cap_) {
     if (h_hops_) HIP_OK(hipHostFree(h_hops_));
     h_hops_cap_ = hops_.size() * 2 + 1024;
@@ -665,6 +695,7 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64
     h_hbuf_cap_ = hbuf_.size() * 2 + (1 << 16);
     HIP_OK(hipHostMalloc((void**)&h_hbuf_, h_hbuf_cap_, hipHostMallocDefault));
   }
+  span("u.hostgrow");
   if (hops_.size() > d_hops_cap_) {
     d_hops_cap_ = hops_.size() * 2 + 1024;
     HostOp* p = nullptr;
@@ -679,13 +710,18 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64
     allocs_.push_back(p);
     d_hbuf_ = p;
   }
+  span("u.devgrow");
   if (!hops_.empty()) {
     std::memcpy(h_hops_, hops_.data(), hops_.size() * sizeof(HostOp));
+    span("u.hops.memcpy");
     HIP_OK(hipMemcpyAsync(d_hops_, h_hops_, hops_.size() * sizeof(HostOp), hipMemcpyHostToDevice, st));
+    span("u.hops.h2d");
   }
   if (!hbuf_.empty()) {
     std::memcpy(h_hbuf_, hbuf_.data(), hbuf_.size());
+    span("u.hbuf.memcpy");
     HIP_OK(hipMemcpyAsync(d_hbuf_, h_hbuf_, hbuf_.size(), hipMemcpyHostToDevice, st));
+    span("u.hbuf.h2d");
   }
   // ---- file -> server table
   if (files_->size() > files_uploaded_) {
@@ -709,6 +745,7 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64
     HIP_OK(hipMemcpyAsync(d_exp_lo_, h_exp_, (size_t)n_reg * 8, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(d_exp_hi_, h_exp_ + 4096, (size_t)n_reg * 8, hipMemcpyHostToDevice, st));
   }
+  span("u.files+exp");
   const uint64_t arena_low = regions_.empty() ? arena_head_ : regions_.front().lo;
   const uint64_t arena_free = (uint64_t)cfg_.arena_cap - (arena_head_ - arena_low);
   const uint32_t arena_limit = (uint32_t)std::min<uint64_t>(arena_free, cfg_.arena_cap / 2);
@@ -735,12 +772,13 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64
   a.exp_idx_sorted = d_exp_idx_sorted_; a.exp_cnt = d_exp_cnt_; a.exp_pos = d_exp_pos_;
   a.out_cnt = d_out_cnt_; a.out_pos = d_out_pos_; a.stage = d_stage_; a.ovf = d_ovf_;
   a.out = d_out_; a.out_cap = out_cap_; a.counts = d_counts_;
-  phase_t[1] = clock_ms();
+  phase_t[2] = clock_ms();
   if (apm_dj_join(&a, st) != 0) throw std::runtime_error("device join: scan scratch too small");
   HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost, st));
-  phase_t[2] = clock_ms();
-  HIP_OK(hipStreamSynchronize(st));  // ---- sync A
+  if (meanwhile) (*meanwhile)();
   phase_t[3] = clock_ms();
+  HIP_OK(hipStreamSynchronize(st));  // ---- sync A
+  phase_t[4] = clock_ms();
   const JoinCounts c = *h_counts_;
   if (c.n_out > out_cap_) throw std::runtime_error("device join: more tx in one batch than the output capacity");
   if (c.pad[0] > DJ_OVF_CAP) throw std::runtime_error("device join: output overflow list full");
@@ -751,7 +789,7 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64
   }
   keys_since_rebuild_ += c.n_keys_new;
   if (c.n_miss) register_misses(hb, c.n_miss, st);
-  phase_t[4] = clock_ms();
+  phase_t[5] = clock_ms();
   // ---- resolve + plan
   DJFormatArgs& f = f_;
   f = DJFormatArgs{};
@@ -765,7 +803,7 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64
   if (apm_dj_plan(&f, st) != 0) throw std::runtime_error("device join: scan scratch too small");
   HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));  // ---- sync B
-  phase_t[5] = clock_ms();
+  phase_t[6] = clock_ms();
   const JoinCounts c2 = *h_counts_;
   f.ring_base = ring_reserve(c2.text_bytes);
   const size_t txt = (size_t)(want_tx ? c2.tx_text_bytes : 0) + (want_db ? c2.db_text_bytes : 0);
@@ -800,7 +838,7 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64
                           hipMemcpyDeviceToHost, st));
   HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));  // ---- sync C
-  phase_t[6] = clock_ms();
+  phase_t[7] = clock_ms();
   const JoinCounts c3 = *h_counts_;
   if (c3.n_cand > spec || c3.n_unresolved > spec) {
     HIP_OK(hipMemcpyAsync(h_cand_, d_cand_, (size_t)c3.n_cand * 4, hipMemcpyDeviceToHost, st));
@@ -834,7 +872,7 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64
   tx_ += c3.n_out;
   tx_db_ += c3.n_db;
   maybe_rebuild(now, st);
-  phase_t[7] = clock_ms();
+  phase_t[8] = clock_ms();
 }
 
 JoinCounters DeviceJoin::counters() const {

@@ -76,8 +76,13 @@ class DeviceJoin {
   // the batch join; host_bytes = the host copy of the batch (same layout as d_bytes(k))
   // `parallel(n, fn)` runs fn(0..n-1) on the engine's worker pool (host pre-pass per file)
   using ParallelFor = std::function<void(int, const std::function<void(int)>&)>;
+  // `meanwhile` runs on this thread after the join kernels are queued, before the first wait
   void run(int k, const uint8_t* host_bytes, uint32_t n_ev, double now, uint64_t batch_no, bool want_tx, bool want_db,
-           DevJoinBatch& out, const ParallelFor& parallel = nullptr);
+           DevJoinBatch& out, const ParallelFor& parallel = nullptr, const std::function<void()>* meanwhile = nullptr);
+  // the host pre-pass of the NEXT batch (slot k, its parse finished), run while this batch's join
+  // kernels execute; run(k) then uploads its ops instead of doing the pre-pass itself.  The audit
+  // state is host-only and advanced in batch order, so the result is the same.
+  void prepass_ahead(int k, const uint8_t* host_bytes, const ParallelFor& parallel);
   // the stats thread finished with slot k's arrays (event recorded on its stream)
   void release_slot(int k, hipStream_t stats_stream);
 
@@ -105,8 +110,9 @@ class DeviceJoin {
   void load(class BinReader& r);
   // phase boundaries of the last run() (steady-clock ms): prepass, join launched, sync A,
   // registered, sync B, sync C, end -- for the engine's stage trace
-  static constexpr int kPhases = 7;
+  static constexpr int kPhases = 8;
   double phase_t[kPhases + 1] = {0};
+  std::vector<std::pair<const char*, std::pair<double, double>>> spans;  // finer trace spans of run()
   const JoinCounts& last_counts() const { return *h_counts_; }
   size_t device_bytes() const { return device_bytes_; }
 
@@ -178,6 +184,9 @@ class DeviceJoin {
   // host pre-pass output of the current batch
   std::vector<HostOp> hops_;
   std::string hbuf_;
+  std::vector<HostOp> hops_ahead_;  // prepass_ahead's result for slot ahead_k_
+  std::string hbuf_ahead_;
+  int ahead_k_ = -1;
   HostOp* h_hops_ = nullptr;     // pinned
   uint8_t* h_hbuf_ = nullptr;    // pinned
   size_t h_hops_cap_ = 0, h_hbuf_cap_ = 0;

@@ -222,9 +222,9 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
   HIP_OK(hipStreamCreateWithFlags(&parse_stream_, hipStreamNonBlocking));
   HIP_OK(hipStreamCreateWithFlags(&out_stream_, hipStreamNonBlocking));
-  HIP_OK(hipEventCreate(&ev_a_));
+  HIP_OK(hipEventCreateWithFlags(&ev_a_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&tail_csr_ev_, hipEventDisableTiming));
-  HIP_OK(hipEventCreate(&ev_b_));
+  HIP_OK(hipEventCreateWithFlags(&ev_b_, hipEventDisableTiming));
   const int32_t S = cfg_.max_series;
   // parse
   if (cfg_.device_join) {
@@ -357,11 +357,14 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   d_alerts_ = (AlertRec*)dmalloc((size_t)cfg_.max_alerts * sizeof(AlertRec));
   d_n_alerts_ = (int32_t*)dmalloc(16);
   HIP_OK(hipHostMalloc((void**)&h_alerts_, (size_t)cfg_.max_alerts * sizeof(AlertRec), hipHostMallocDefault));
-  d_alert_win_ = (WinStat*)dmalloc((size_t)cfg_.max_alerts * sizeof(WinStat));
-  d_alert_z_ = (ZOut*)dmalloc((size_t)cfg_.max_alerts * sizeof(ZOut));
   HIP_OK(hipHostMalloc((void**)&h_alert_win_, (size_t)cfg_.max_alerts * sizeof(WinStat), hipHostMallocDefault));
   HIP_OK(hipHostMalloc((void**)&h_alert_z_, (size_t)cfg_.max_alerts * sizeof(ZOut), hipHostMallocDefault));
   HIP_OK(hipHostMalloc((void**)&h_n_alerts_, 16, hipHostMallocDefault));
+  HIP_OK(hipHostGetDevicePointer((void**)&hd_alerts_, h_alerts_, 0));
+  HIP_OK(hipHostGetDevicePointer((void**)&hd_alert_win_, h_alert_win_, 0));
+  HIP_OK(hipHostGetDevicePointer((void**)&hd_alert_z_, h_alert_z_, 0));
+  HIP_OK(hipHostGetDevicePointer((void**)&hd_n_alerts_, h_n_alerts_, 0));
+  HIP_OK(hipEventCreateWithFlags(&ev_alerts_, hipEventDisableTiming));
   // tx + release
   d_tx_ = (TxRec*)dmalloc((size_t)cfg_.max_tx_per_batch * sizeof(TxRec));
   HIP_OK(hipHostMalloc((void**)&h_tx_, (size_t)cfg_.max_tx_per_batch * sizeof(TxRec), hipHostMallocDefault));
@@ -448,7 +451,7 @@ Engine::~Engine() {
   hipHostFree(h_alert_win_);
   hipHostFree(h_alert_z_);
   if (h_series_service_) hipHostFree(h_series_service_);
-  hipHostFree(h_n_alerts_); hipHostFree(h_tx_); hipHostFree(h_gid_);
+  hipHostFree(h_n_alerts_); hipEventDestroy(ev_alerts_); hipHostFree(h_tx_); hipHostFree(h_gid_);
   for (int k = 0; k < 2; ++k) {
     hipHostFree(h_release_gid_[k]);
     if (h_fmt_out_[k]) hipHostFree(h_fmt_out_[k]);
@@ -840,7 +843,7 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
   } else {
     launch_parse(ps, host_bytes, n_bytes, chunks_in);
   }
-  finish_parse(ps);
+  if (ps.pending) finish_parse(ps);  // (the device join may have finished it ahead)
   if (dev()) {
     process_batch_dev_tail(ps, t0, now_override, next_bytes, next_n, next_chunks);
     return;
@@ -988,7 +991,18 @@ void Engine::process_batch_dev_tail(ParseSlot& ps, double t0, double now_overrid
   const double clock = now_override >= 0 ? now_override : watermark_;
   DevJoinBatch b;
   const DeviceJoin::ParallelFor par = [this](int n, const std::function<void(int)>& fn) { pool_->run(n, fn); };
-  dj_->run(k, ps.hb, ps.n_events, clock, batch_no_, want(OUT_TRANSACTIONS), want(OUT_AUDIT_DB), b, par);
+  // while this batch's join kernels run: finish the next batch's parse and do its host pre-pass
+  // (audit blocks), taking both off the next batch's critical path
+  const std::function<void()> ahead = [this, k, &par]() {
+    ParseSlot& nx = pslot_[k ^ 1];
+    const double ta = now_ms();
+    finish_parse(nx);
+    dj_->prepass_ahead(k ^ 1, nx.hb, par);
+    trace_event("next parse+prepass", ta, now_ms(), 2);
+  };
+  static const bool ahead_on = [] { const char* e = std::getenv("APM_PREPASS_AHEAD"); return !e || e[0] != '0'; }();
+  dj_->run(k, ps.hb, ps.n_events, clock, batch_no_, want(OUT_TRANSACTIONS), want(OUT_AUDIT_DB), b, par,
+           prefetched_ && ahead_on ? &ahead : nullptr);
   const double t2 = now_ms();
   metrics_.t_join_ms += t2 - t1;
   metrics_.t_join_shards_ms += t2 - t1;
@@ -997,9 +1011,10 @@ void Engine::process_batch_dev_tail(ParseSlot& ps, double t0, double now_overrid
   roctxRangePop();
   trace_event("join (GPU)", t1, t2, 0);
   if (trace_on_) {
-    static const char* names[DeviceJoin::kPhases] = {"dj.prepass", "dj.launch", "dj.syncA", "dj.register",
-                                                     "dj.plan+syncB", "dj.write+syncC", "dj.tail"};
+    static const char* names[DeviceJoin::kPhases] = {"dj.prepass", "dj.upload", "dj.launch", "dj.syncA",
+                                                     "dj.register", "dj.plan+syncB", "dj.write+syncC", "dj.tail"};
     for (int i = 0; i < DeviceJoin::kPhases; ++i) trace_event(names[i], dj_->phase_t[i], dj_->phase_t[i + 1], 2);
+    for (const auto& sp : dj_->spans) trace_event(sp.first, sp.second.first, sp.second.second, 2);
   }
   const unsigned long long wm = *ps.h_watermark;
   if (wm) {
@@ -1755,19 +1770,32 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   }
   ++rollover_idx_;
   if (want(OUT_SX)) server_rollup(edge_ts);
-  HIP_OK(hipMemcpyAsync(h_n_alerts_, d_n_alerts_, 4, hipMemcpyDeviceToHost, stream_));
-  HIP_OK(hipStreamSynchronize(stream_));
-  if (dev()) release_device_finish();
+  // the candidates go straight to pinned host memory; the st/fs formatting is queued behind them
+  // and runs on the GPU while this thread waits for the candidates only and decides the alerts
+  {
+    const ZOut* zl[MAX_LAGS] = {};
+    for (int l = 0; l < cfg_.n_lags; ++l) zl[l] = lag_[l].out;
+    apm_alert_gather(d_alerts_, d_n_alerts_, cfg_.max_alerts, d_win_, zl, cfg_.n_lags, want(OUT_AL) ? 1 : 0,
+                     hd_alerts_, hd_alert_win_, hd_alert_z_, hd_n_alerts_, stream_);
+    HIP_OK(hipEventRecord(ev_alerts_, stream_));
+  }
   const double tr2 = now_ms();
-  metrics_.t_rollover_ms += tr2 - tr1;
+  if (want(OUT_ST) || want(OUT_FS)) format_rollover_text(edge_ts);
+  const double tr3 = now_ms();
+  HIP_OK(hipEventSynchronize(ev_alerts_));
+  const double tr4 = now_ms();
+  if (dev()) release_device_finish();
+  metrics_.t_rollover_ms += tr2 - tr1 + tr4 - tr3;
   trace_event("release", tr0, tr1, 1);
   trace_event("window+zscore+alerts", tr1, tr2, 1);
-  metrics_.rollover_latency_ms.push_back(tr2 - batch_t0);
-  if (want(OUT_ST) || want(OUT_FS)) format_rollover_text(edge_ts);
+  trace_event("format (launch)", tr2, tr3, 1);
+  trace_event("rollover wait", tr3, tr4, 1);
+  metrics_.rollover_latency_ms.push_back(tr4 - batch_t0);
   flush_alerts(edge_ts);
+  trace_event("alerts", tr4, now_ms(), 1);
   if (want(OUT_SX)) format_server_rollup(edge_ts);
-  metrics_.t_format_ms += now_ms() - tr2;
-  trace_event("format+sinks", tr2, now_ms(), 1);
+  metrics_.t_format_ms += now_ms() - tr4 + tr3 - tr2;
+  trace_event("alerts+sinks", tr4, now_ms(), 1);
 }
 
 // K9 with the device join, part 1 (before K8): merge the tail into the sorted pool, count the
@@ -1833,19 +1861,10 @@ void Engine::release_device_finish() {
 }
 
 void Engine::flush_alerts(int64_t edge_ts) {
-  int32_t na = std::min(*h_n_alerts_, cfg_.max_alerts);
+  const int32_t na = *h_n_alerts_;  // apm_alert_gather's clamped count (ev_alerts_ has completed)
   metrics_.alert_candidates += na;
   if (na <= 0) return;
   const bool need_rows = want(OUT_AL);
-  if (need_rows) {
-    const ZOut* zl[MAX_LAGS] = {};
-    for (int l = 0; l < cfg_.n_lags; ++l) zl[l] = lag_[l].out;
-    apm_alert_gather(d_alerts_, na, d_win_, zl, cfg_.n_lags, d_alert_win_, d_alert_z_, stream_);
-    HIP_OK(hipMemcpyAsync(h_alert_win_, d_alert_win_, (size_t)na * sizeof(WinStat), hipMemcpyDeviceToHost, stream_));
-    HIP_OK(hipMemcpyAsync(h_alert_z_, d_alert_z_, (size_t)na * sizeof(ZOut), hipMemcpyDeviceToHost, stream_));
-  }
-  HIP_OK(hipMemcpyAsync(h_alerts_, d_alerts_, (size_t)na * sizeof(AlertRec), hipMemcpyDeviceToHost, stream_));
-  HIP_OK(hipStreamSynchronize(stream_));
   // candidate i's rows are win_of(i) / z_of(i) in device order; decide in emission order
   std::vector<int32_t> ord((size_t)na);
   for (int32_t i = 0; i < na; ++i) ord[i] = i;
@@ -1882,8 +1901,8 @@ void Engine::flush_alerts(int64_t edge_ts) {
       p.c.local_id = node_next_id_++;
       p.server = servers_[si.server];
       p.service = svc;
-      if (need_rows)
-        p.fs = fmt::fs_line(edge_ts, servers_[si.server], svc, cfg_.lags[r.lag_idx], h_alert_win_[i], h_alert_z_[i]);
+      if (need_rows) { p.w = h_alert_win_[i]; p.z = h_alert_z_[i]; }
+      p.lag = cfg_.lags[r.lag_idx];
       node_q_.push_back(std::move(p));
     }
     return;
@@ -2316,10 +2335,12 @@ uintptr_t Engine::alloc_pinned(size_t n) {
 void Engine::free_pinned(uintptr_t p) { hipHostFree((void*)p); }
 
 void Engine::pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream, bool atomic_path) {
+  const double tp0 = now_ms();
   if (coll_) {  // node-wide slots: queue new services, adopt the slots the last round assigned
     reg_collect_locked();
     reg_apply_locked();
   }
+  trace_event("pack.registry", tp0, now_ms(), 1);
   // series -> service table (grows with the dictionary): upload only the new tail
   if (series_service_uploaded_ < n_series_) {
     // Pinned host mirror of the table: the series list is append-only, so each upload reads a
@@ -2369,13 +2390,22 @@ void Engine::pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream,
       HIP_OK(hipMemcpyAsync(d_svc_ids_, h_svc_ids_.data(), h_svc_ids_.size() * 4, hipMemcpyHostToDevice, stream));
       svc_csr_n_ = n_series_;
       svc_csr_cap_ = cap;
+      tail_csr_for_ = {-1, -1};
     }
+    const double tg0 = now_ms();
     if (apm_service_gram(d_svc_off_, d_svc_ids_, d_active_, cap, cfg_.max_series, cfg_.n_lags,
                          (const double* const*)d_lag_sum_ptrs_, (const double* const*)d_lag_comp_ptrs_,
                          (const int32_t* const*)d_lag_cnt_ptrs_, d_dst, stream) == 0) {
       // series added since the snapshot: a small per-batch CSR of just those series (by service,
       // in series order) accumulated by the same Gram kernel -- the pack stays deterministic
-      if (n_series_ > svc_csr_n_) {
+      if (n_series_ > svc_csr_n_ && tail_csr_for_ == std::make_pair(svc_csr_n_, n_series_)) {
+        // same tail as the previous pack (no series since): the uploaded lists are still valid
+        if (tail_csr_m_)
+          apm_service_gram(d_tail_csr_ + tail_csr_m_, d_tail_csr_ + 2 * tail_csr_m_ + 1, d_active_, tail_csr_m_,
+                           cfg_.max_series, cfg_.n_lags, (const double* const*)d_lag_sum_ptrs_,
+                           (const double* const*)d_lag_comp_ptrs_, (const int32_t* const*)d_lag_cnt_ptrs_, d_dst,
+                           stream, d_tail_csr_, 1);
+      } else if (n_series_ > svc_csr_n_) {
         std::vector<std::pair<int32_t, int32_t>> tail;  // (row, series)
         for (int32_t s = svc_csr_n_; s < n_series_; ++s) {
           const int32_t v = svc_key(s);
@@ -2384,6 +2414,8 @@ void Engine::pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream,
         std::stable_sort(tail.begin(), tail.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
         const size_t nt = tail.size();
         last_gram_tail_ = (int64_t)nt;
+        tail_csr_for_ = {svc_csr_n_, n_series_};
+        tail_csr_m_ = 0;
         if (nt) {
           // one pinned block per call: [map m][off m+1][ids nt]
           std::vector<int32_t> map, off, ids;
@@ -2393,6 +2425,7 @@ void Engine::pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream,
           }
           off.push_back((int32_t)nt);
           const size_t m = map.size(), nb = (m + (m + 1) + nt) * 4;
+          tail_csr_m_ = (int32_t)m;
           if (nb > tail_csr_cap_) {
             if (h_tail_csr_) HIP_OK(hipHostFree(h_tail_csr_));
             HIP_OK(hipStreamSynchronize(stream));
@@ -2412,6 +2445,7 @@ void Engine::pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream,
                            (const int32_t* const*)d_lag_cnt_ptrs_, d_dst, stream, d_tail_csr_, 1);
         }
       }
+      trace_event("pack.gram", tg0, now_ms(), 1);
       return;
     }
   }
@@ -2702,7 +2736,9 @@ void Engine::node_resolve() {
     auto p = node_sent_.find(c.local_id);
     if (p == node_sent_.end()) throw std::runtime_error("node alerts: lost candidate payload");
     if (want(OUT_AL)) {
-      text += fmt::al_line(c.now, c.edge_ts, p->second.server, p->second.service, c.causes, p->second.fs);
+      const NodePayload& q = p->second;
+      const std::string fs = fmt::fs_line(c.edge_ts, q.server, q.service, q.lag, q.w, q.z);
+      text += fmt::al_line(c.now, c.edge_ts, q.server, q.service, c.causes, fs);
       text += '\n';
     }
   }

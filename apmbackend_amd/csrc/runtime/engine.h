@@ -428,7 +428,8 @@ class Engine {
     uint64_t pad;
   };
   struct NodeHdr { int32_t count, all_sent, pad[14]; };  // 64 B
-  struct NodePayload { uint64_t seq_batch; NodeCand c; std::string server, service, fs; };
+  // a candidate's fs text is formatted only if it wins the node-wide cooldown (node_resolve)
+  struct NodePayload { uint64_t seq_batch; NodeCand c; std::string server, service; WinStat w; ZOut z; int32_t lag; };
   bool node_mode_ = false;
   int32_t node_cap_ = 512;                 // candidates per rank per round
   std::mutex node_mu_;                     // node_q_ / node_text_
@@ -735,6 +736,8 @@ class Engine {
   int32_t* d_tail_csr_ = nullptr;
   size_t tail_csr_cap_ = 0, d_tail_csr_cap_ = 0;
   hipEvent_t tail_csr_ev_ = nullptr;
+  std::pair<int32_t, int32_t> tail_csr_for_{-1, -1};  // (CSR snapshot size, n_series) of the uploaded tail
+  int32_t tail_csr_m_ = 0;
  public:
   int64_t last_gram_tail_ = 0;  // series the last Gram pack took from the tail CSR (tests)
  private:
@@ -746,11 +749,14 @@ class Engine {
   AlertRec* d_alerts_ = nullptr;
   int32_t* d_n_alerts_ = nullptr;
   AlertRec* h_alerts_ = nullptr;
-  WinStat* d_alert_win_ = nullptr;  // candidate rows, compacted (apm_alert_gather)
-  ZOut* d_alert_z_ = nullptr;
-  WinStat* h_alert_win_ = nullptr;  // pinned
+  WinStat* h_alert_win_ = nullptr;  // pinned; candidate rows written by apm_alert_gather
   ZOut* h_alert_z_ = nullptr;       // pinned
   int32_t* h_n_alerts_ = nullptr;
+  AlertRec* hd_alerts_ = nullptr;  // device views of the four pinned buffers above
+  WinStat* hd_alert_win_ = nullptr;
+  ZOut* hd_alert_z_ = nullptr;
+  int32_t* hd_n_alerts_ = nullptr;
+  hipEvent_t ev_alerts_ = nullptr;  // the rollover's candidates are in host memory
   std::unordered_map<std::string, double> last_alert_;  // cooldown key -> alertTimestamp
 
   // tx upload + release pool

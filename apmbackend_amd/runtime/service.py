@@ -189,6 +189,7 @@ class IngestService:
         self._held = None  # batch taken from the read-ahead ring and handed to the engine as prefetch
         self._stopping = False
         self.perf = {"wait_s": 0.0, "engine_s": 0.0, "outputs_s": 0.0, "batches": 0, "bytes": 0, "prefetched": 0}
+        self.batch_log = None  # a list to record every read-ahead batch (bytes, chunks) in (tests)
         self._drain_every_s = float(g.get("outputDrainMs", 250.0)) / 1000.0
         self._last_drain = 0.0
         if self.readahead:
@@ -645,6 +646,9 @@ class IngestService:
         nxt = None
         if not paused and not dup and not self._ckpt_due() and not self._stopping:
             nxt = self.tailer.next(0.0)
+        if self.batch_log is not None:
+            import ctypes
+            self.batch_log.append((ctypes.string_at(ptr, n), list(chunks)))
         t2 = time.perf_counter()
         if nxt is not None:
             self.native.process_batch_ptr(ptr, n, chunks, -1.0, nxt[1], nxt[2], nxt[3])

@@ -84,43 +84,49 @@ def test_service_checkpoint_restart_is_seamless(tmp_path):
 
 
 def test_readahead_service_processes_every_line(tmp_path):
-    """Production path: tailer read-ahead into pinned slots + engine prefetch of the next batch.
-    Batching follows the file writes (not the test's steps), so tx records (batch-invariant
-    here) are compared with the CPU oracle service, and every byte is consumed and committed."""
+    """Production path: tailer read-ahead into pinned slots + engine prefetch of the next batch,
+    with the files appended while the read-ahead thread runs.  Every byte is consumed and
+    committed, and the outputs equal the CPU oracle fed the very batches the tailer formed (the
+    reference's cross-file join depends on how the files interleave, so batches are replayed
+    rather than assumed: tests/test_tailer.py covers the batching itself)."""
     import time as _time
-    outs = []
-    for engine in ("native", "cpu-oracle"):
-        d = tmp_path / engine
-        d.mkdir()
-        C, lines, mapping, sc = make_env(d)
-        gpu_cfg(C)
-        C["gpu"]["tailReadAhead"] = engine == "native"
-        C["gpu"]["tailIdleMs"] = 5.0
-        svc = IngestService(C, engine=engine, files=sorted(mapping.values()), rank=0, world=1,
-                            server_of_path=srv_of)
-        w = ListWriter()
-        svc.inserter.writer = w
-        for chunks in batches(lines, sc.start_ms, 5.0):
-            for fp, ls in chunks:
-                with open(mapping[fp], "a") as f:
-                    f.write("\n".join(ls) + "\n")
-            svc.step()
-        total = sum(os.path.getsize(f) for f in mapping.values())
-        deadline = _time.time() + 60
-        while _time.time() < deadline:
-            svc.step()
-            svc._idle(0.01)
-            if sum(o[1] for o in svc.tailer.offsets()) == total and svc._held is None:
-                break
-        assert sum(o[1] for o in svc.tailer.offsets()) == total
-        svc.shutdown()
-        outs.append(w.rows)
-    nat, cpu = outs
-    # the account join depends on batch boundaries (need-cache TTL on the batch clock), as in
-    # the reference: compare the tx identities without the account column
-    key = lambda rows: sorted("\t".join(r.split("\t")[:5] + r.split("\t")[6:]) for r in rows)
-    assert key(nat["tx"]) == key(cpu["tx"]) and len(nat["tx"]) > 0
-    assert len(nat["stats"]) > 0
+    from apmbackend_amd.models.oracle import PipelineOracle
+    from apmbackend_amd.runtime import sinks
+    from apmbackend_amd.utils.synth import with_watermarks
+    from apmbackend_amd.utils.timeparse import TzOffset
+    C, lines, mapping, sc = make_env(tmp_path)
+    gpu_cfg(C)
+    C["gpu"]["tailReadAhead"] = True
+    C["gpu"]["tailIdleMs"] = 5.0
+    svc = IngestService(copy.deepcopy(C), engine="native", files=sorted(mapping.values()), rank=0, world=1,
+                        server_of_path=srv_of)
+    svc.batch_log = []
+    w = ListWriter()
+    svc.inserter.writer = w
+    for chunks in batches(lines, sc.start_ms, 5.0):
+        for fp, ls in chunks:
+            with open(mapping[fp], "a") as f:
+                f.write("\n".join(ls) + "\n")
+        svc.step()
+    total = sum(os.path.getsize(f) for f in mapping.values())
+    deadline = _time.time() + 60
+    while _time.time() < deadline:
+        svc.step()
+        svc._idle(0.01)
+        if sum(o[1] for o in svc.tailer.offsets()) == total and svc._held is None:
+            break
+    assert sum(o[1] for o in svc.tailer.offsets()) == total
+    path_of = {i: p for p, i in svc.file_ids.items()}
+    svc.shutdown()
+    assert svc.perf["prefetched"] > 0 and len(svc.batch_log) > 3
+    bl = [[(path_of[fid], data[lo:hi].decode().rstrip("\n").split("\n")) for fid, lo, hi in ch]
+          for data, ch in svc.batch_log]
+    P = PipelineOracle(copy.deepcopy(C), TzOffset("UTC"), server_fn=srv_of)
+    P.run_batches(with_watermarks(bl, TzOffset("UTC")))
+    want = sinks.copy_encode_lines(P.tx_db + P.audit_db + P.fs + P.al)
+    assert sorted(w.rows["tx"]) == sorted(want["tx"]) and len(want["tx"]) > 100
+    assert w.rows["stats"] == want["fs"] and len(want["fs"]) > 0
+    assert w.rows.get("alerts", []) == want["al"]
 
 
 def test_transactions_queue_roundtrip_with_reference_stages(tmp_path):

@@ -1,6 +1,5 @@
 set -u
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_engine_gpu.py -x -v --timeout 200 --timeout-method thread -k "gram or fleet" > gpurun_out/t.log 2>&1; rc=$?; tail -6 gpurun_out/t.log; [ $rc -le 1 ] || exit $rc
-for p in config4 firehose; do
-timeout -k 10 400 python bench.py --preset $p --steps 10 --warmup 3 > gpurun_out/bench_$p.log 2>&1; rc=$?; echo "$p rc=$rc"; tail -1 gpurun_out/bench_$p.log | cut -c1-1500; [ $rc -le 1 ] || exit $rc
+for a in 1 0 1; do
+APM_PREPASS_AHEAD=$a timeout -k 10 200 python -u -m pytest tests/test_service_gpu.py -x -q --timeout 100 --timeout-method thread -k readahead > gpurun_out/t_$a.log 2>&1; rc=$?; echo "ahead=$a rc=$rc"; grep "^E " gpurun_out/t_$a.log | head -8; [ $rc -le 1 ] || exit $rc
 done
