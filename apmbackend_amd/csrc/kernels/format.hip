@@ -33,12 +33,27 @@ struct Out {
       for (int i = 0; i < len; ++i) p[n + i] = src[i];
     n += len;
   }
+  // Unsigned decimal.  Nearly every value fits 32 bits, where division by 10 is a multiply-high
+  // (64-bit division is a long emulated sequence on CDNA); the length pass only counts digits.
   __device__ __forceinline__ void u(uint64_t v) {
+    if (v <= 0xffffffffull) { u32((uint32_t)v); return; }
     char buf[20];
     int k = 0;
     do { buf[k++] = (char)('0' + v % 10); v /= 10; } while (v);
     if (p)
       for (int i = 0; i < k; ++i) p[n + i] = buf[k - 1 - i];
+    n += k;
+  }
+  __device__ __forceinline__ static int digits32(uint32_t v) {
+    return v < 10u ? 1 : v < 100u ? 2 : v < 1000u ? 3 : v < 10000u ? 4 : v < 100000u ? 5
+         : v < 1000000u ? 6 : v < 10000000u ? 7 : v < 100000000u ? 8 : v < 1000000000u ? 9 : 10;
+  }
+  __device__ __forceinline__ void u32(uint32_t v) {
+    const int k = digits32(v);
+    if (p) {
+      char* q = p + n + k;
+      do { *--q = (char)('0' + v % 10u); v /= 10u; } while (v);
+    }
     n += k;
   }
   __device__ __forceinline__ void i64(int64_t v) {
@@ -60,6 +75,17 @@ struct Out {
     }
     return nn;
   }
+  // nn = ip * 10^f + fr with constant divisors (32-bit when nn fits: nearly always)
+  __device__ __forceinline__ static void split_fixed(uint64_t nn, int f, uint64_t& ip, uint32_t& fr) {
+    if (nn <= 0xffffffffull) {
+      const uint32_t v = (uint32_t)nn;
+      if (f == 1) { ip = v / 10u; fr = v % 10u; } else { ip = v / 100u; fr = v % 100u; }
+    } else if (f == 1) {
+      ip = nn / 10u; fr = (uint32_t)(nn % 10u);
+    } else {
+      ip = nn / 100u; fr = (uint32_t)(nn % 100u);
+    }
+  }
   // nf(x, f): 'undefined' for NaN, else x.toFixed(f)
   __device__ __forceinline__ void fixed(double x, int f, bool& fallback) {
     if (x != x) { s("undefined", 9); return; }
@@ -71,11 +97,12 @@ struct Out {
     }
     const uint64_t nn = fixed_n(ax, f);
     if (neg) c('-');
-    const uint64_t sc = f == 1 ? 10 : 100;
-    u(nn / sc);
+    uint64_t ip;
+    uint32_t fr;
+    split_fixed(nn, f, ip, fr);
+    u(ip);
     c('.');
-    const uint64_t fr = nn % sc;
-    if (f == 2) { c((char)('0' + fr / 10)); c((char)('0' + fr % 10)); }
+    if (f == 2) { c((char)('0' + fr / 10u)); c((char)('0' + fr % 10u)); }
     else c((char)('0' + fr));
   }
   // String(parseFloat(x.toFixed(f))) -- a number as the DB row holds it (copyenc.cpp parses the
@@ -98,14 +125,15 @@ struct Out {
     if (nn == 0) { c('0'); return; }
     if (nn >= 1000000000000000ULL) fallback = true;
     if (neg) c('-');
-    const uint64_t sc = f == 1 ? 10 : 100;
-    u(nn / sc);
-    uint64_t fr = nn % sc;
+    uint64_t ip;
+    uint32_t fr;
+    split_fixed(nn, f, ip, fr);
+    u(ip);
     if (fr == 0) return;
     c('.');
     if (f == 2) {
-      c((char)('0' + fr / 10));
-      if (fr % 10) c((char)('0' + fr % 10));
+      c((char)('0' + fr / 10u));
+      if (fr % 10u) c((char)('0' + fr % 10u));
     } else {
       c((char)('0' + fr));
     }
@@ -144,8 +172,7 @@ struct Out {
 
 __device__ __forceinline__ void head(Out& o, const char* tag, const FormatArgs& a, int32_t s) {
   o.s(tag, 3);
-  o.i64(a.edge_ts);
-  o.c('|');
+  o.s(a.ts_wire, a.ts_wire_len);
   const int4 nm = a.series_names[s];
   o.s(a.names + nm.x, nm.y);
   o.c('|');

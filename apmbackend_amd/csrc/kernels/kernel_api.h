@@ -108,6 +108,8 @@ struct FormatArgs {
   int32_t fs_copy;
   int32_t ts_copy_len;
   char ts_copy[32];        // edge_ts as 'YYYY-MM-DD HH:MM:SS.mmm+00'
+  int32_t ts_wire_len;
+  char ts_wire[24];        // "<edge_ts>|" as the wire lines' second field (printed once, on the host)
   uint32_t *st_len, *fs_len, *st_off, *fs_off;  // [n + 1]
   char *st_out, *fs_out;
   int32_t* fallback;

@@ -230,10 +230,11 @@ void DeviceJoin::finish_select(int k, hipStream_t ps) {
 // One task per file with host events (audit state is per file, cache effects are ops resolved
 // on the GPU in line order), run on the engine's worker pool; the per-file op lists are then
 // merged by event index and their string buffers concatenated.
-void DeviceJoin::host_prepass(int k, const uint8_t* hb, uint32_t n_host, const ParallelFor& parallel) {
+void DeviceJoin::host_prepass(int k, const uint8_t* hb, uint32_t n_host, const ParallelFor& parallel,
+                              std::vector<HostOp>& hops_out, std::string& hbuf_out) {
   Slot& s = sl_[k];
-  hops_.clear();
-  hbuf_.clear();
+  hops_out.clear();
+  hbuf_out.clear();
   std::unordered_map<int32_t, int> task_of;
   int nt = 0;
   int32_t last_file = -1;
@@ -272,14 +273,14 @@ void DeviceJoin::host_prepass(int k, const uint8_t* hb, uint32_t n_host, const P
   size_t total = 0;
   std::vector<uint32_t> base(nt);
   for (int t = 0; t < nt; ++t) {
-    base[t] = (uint32_t)hbuf_.size();
-    hbuf_ += tasks_[t].hbuf;
+    base[t] = (uint32_t)hbuf_out.size();
+    hbuf_out += tasks_[t].hbuf;
     total += tasks_[t].hops.size();
     audit_errors_ += tasks_[t].audit_errors;
     host_invalid_acct_ += tasks_[t].invalid_acct;
     host_pm_ += tasks_[t].pm_host;
   }
-  hops_.reserve(total);
+  hops_out.reserve(total);
   std::vector<size_t> pos(nt, 0);
   for (;;) {
     int best = -1;
@@ -290,7 +291,7 @@ void DeviceJoin::host_prepass(int k, const uint8_t* hb, uint32_t n_host, const P
     HostOp h = tasks_[best].hops[pos[best]++];
     if (h.op.flags & JF_LID_HOST) h.op.lid += base[best];
     if (h.op.flags & JF_SVC_HOST) h.op.svc_ref += base[best];
-    hops_.push_back(h);
+    hops_out.push_back(h);
   }
   host_events_ += n_host;
 }
@@ -654,12 +655,8 @@ void DeviceJoin::maybe_rebuild(double now, hipStream_t s) {
 
 void DeviceJoin::prepass_ahead(int k, const uint8_t* hb, const ParallelFor& parallel) {
   if (ahead_k_ >= 0) throw std::runtime_error("device join: a pre-pass is already ahead");
-  // hops_ / hbuf_ still hold the running batch's ops (register_misses reads hbuf_ after sync A)
-  std::swap(hops_, hops_ahead_);
-  std::swap(hbuf_, hbuf_ahead_);
-  host_prepass(k, hb, *sl_[k].h_n_host, parallel);
-  std::swap(hops_, hops_ahead_);
-  std::swap(hbuf_, hbuf_ahead_);
+  // hops_ / hbuf_ hold the running batch's ops (register_misses reads hbuf_ after sync A)
+  host_prepass(k, hb, *sl_[k].h_n_host, parallel, hops_ahead_, hbuf_ahead_);
   ahead_k_ = k;
 }
 
@@ -679,7 +676,7 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64
     ahead_k_ = -1;
   } else {
     if (ahead_k_ >= 0) throw std::runtime_error("device join: pre-pass ahead for another slot");
-    host_prepass(k, hb, *s.h_n_host, parallel);
+    host_prepass(k, hb, *s.h_n_host, parallel, hops_, hbuf_);
   }
   phase_t[1] = clock_ms();
   spans.clear();

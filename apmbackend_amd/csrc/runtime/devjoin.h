@@ -79,9 +79,10 @@ class DeviceJoin {
   // `meanwhile` runs on this thread after the join kernels are queued, before the first wait
   void run(int k, const uint8_t* host_bytes, uint32_t n_ev, double now, uint64_t batch_no, bool want_tx, bool want_db,
            DevJoinBatch& out, const ParallelFor& parallel = nullptr, const std::function<void()>* meanwhile = nullptr);
-  // the host pre-pass of the NEXT batch (slot k, its parse finished), run while this batch's join
-  // kernels execute; run(k) then uploads its ops instead of doing the pre-pass itself.  The audit
-  // state is host-only and advanced in batch order, so the result is the same.
+  // the host pre-pass of the NEXT batch (slot k, its parse finished), run on another thread while
+  // this batch's join completes; run(k) then uploads its ops instead of doing the pre-pass
+  // itself.  The audit state is host-only and advanced in batch order, so the result is the same.
+  // The caller orders it: run(k) starts only after prepass_ahead(k) returned.
   void prepass_ahead(int k, const uint8_t* host_bytes, const ParallelFor& parallel);
   // the stats thread finished with slot k's arrays (event recorded on its stream)
   void release_slot(int k, hipStream_t stats_stream);
@@ -166,7 +167,8 @@ class DeviceJoin {
     uint64_t audit_errors = 0, invalid_acct = 0, pm_host = 0;
     uint32_t put(std::string_view s) { const uint32_t o = (uint32_t)hbuf.size(); hbuf.append(s.data(), s.size()); return o; }
   };
-  void host_prepass(int k, const uint8_t* host_bytes, uint32_t n_host, const ParallelFor& parallel);
+  void host_prepass(int k, const uint8_t* host_bytes, uint32_t n_host, const ParallelFor& parallel,
+                    std::vector<HostOp>& hops, std::string& hbuf);
   void host_event(PrepassTask& t, const Event& e, uint32_t ev, const uint8_t* host_bytes);
   void on_app(PrepassTask& t, const Event& e, uint32_t ev, std::string_view line, int32_t server);
   int32_t intern_name(const std::string& s);

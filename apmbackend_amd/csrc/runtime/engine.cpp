@@ -415,6 +415,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
 }
 
 Engine::~Engine() {
+  ahead_lane_.reset();  // drains a pending next-batch pre-pass before the join state goes
   checkpoint_shutdown();
   {
     std::lock_guard<std::mutex> g(st_mu_);
@@ -843,7 +844,12 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
   } else {
     launch_parse(ps, host_bytes, n_bytes, chunks_in);
   }
-  if (ps.pending) finish_parse(ps);  // (the device join may have finished it ahead)
+  if (ahead_task_) {  // the previous call finished this batch's parse (+ pre-pass) on the lane
+    const uint64_t t = ahead_task_;
+    ahead_task_ = 0;
+    ahead_lane_->wait(t);
+  }
+  if (ps.pending) finish_parse(ps);
   if (dev()) {
     process_batch_dev_tail(ps, t0, now_override, next_bytes, next_n, next_chunks);
     return;
@@ -991,14 +997,18 @@ void Engine::process_batch_dev_tail(ParseSlot& ps, double t0, double now_overrid
   const double clock = now_override >= 0 ? now_override : watermark_;
   DevJoinBatch b;
   const DeviceJoin::ParallelFor par = [this](int n, const std::function<void(int)>& fn) { pool_->run(n, fn); };
-  // while this batch's join kernels run: finish the next batch's parse and do its host pre-pass
-  // (audit blocks), taking both off the next batch's critical path
-  const std::function<void()> ahead = [this, k, &par]() {
-    ParseSlot& nx = pslot_[k ^ 1];
-    const double ta = now_ms();
-    finish_parse(nx);
-    dj_->prepass_ahead(k ^ 1, nx.hb, par);
-    trace_event("next parse+prepass", ta, now_ms(), 2);
+  // once this batch's join kernels are queued, a lane thread finishes the next batch's parse and
+  // does its host pre-pass (audit blocks) while this thread completes the batch (join waits,
+  // clocks, hand-off): both leave the next batch's critical path
+  const std::function<void()> ahead = [this, k, par]() {
+    if (!ahead_lane_) ahead_lane_.reset(new TaskLane());
+    ahead_task_ = ahead_lane_->post([this, k, par]() {
+      ParseSlot& nx = pslot_[k ^ 1];
+      const double ta = now_ms();
+      finish_parse(nx);
+      dj_->prepass_ahead(k ^ 1, nx.hb, par);
+      trace_event("next parse+prepass", ta, now_ms(), 3);
+    });
   };
   static const bool ahead_on = [] { const char* e = std::getenv("APM_PREPASS_AHEAD"); return !e || e[0] != '0'; }();
   dj_->run(k, ps.hb, ps.n_events, clock, batch_no_, want(OUT_TRANSACTIONS), want(OUT_AUDIT_DB), b, par,
@@ -1296,6 +1306,57 @@ void Engine::out_worker() {
       ++out_done_;
     }
     out_cv_.notify_all();
+  }
+}
+
+TaskLane::TaskLane() {
+  th_ = std::thread([this]() {
+    for (;;) {
+      std::function<void()> fn;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&]() { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;
+        fn = std::move(q_.front());
+        q_.pop_front();
+      }
+      std::string err;
+      try {
+        fn();
+      } catch (const std::exception& e) {
+        err = e.what();
+      }
+      std::lock_guard<std::mutex> g(mu_);
+      if (!err.empty() && err_.empty()) err_ = err;
+      ++done_;
+      cv_.notify_all();
+    }
+  });
+}
+
+TaskLane::~TaskLane() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+    cv_.notify_all();
+  }
+  th_.join();
+}
+
+uint64_t TaskLane::post(std::function<void()> fn) {
+  std::lock_guard<std::mutex> g(mu_);
+  q_.push_back(std::move(fn));
+  cv_.notify_all();
+  return ++posted_;
+}
+
+void TaskLane::wait(uint64_t id) {
+  std::unique_lock<std::mutex> lk(mu_);
+  cv_.wait(lk, [&]() { return done_ >= id; });
+  if (!err_.empty()) {
+    const std::string e = err_;
+    err_.clear();
+    throw std::runtime_error(e);
   }
 }
 
@@ -2076,6 +2137,7 @@ void Engine::format_rollover_text(int64_t edge_ts) {
   fa.want_fs = want(OUT_FS);
   fa.fs_copy = fs_copy_ ? 1 : 0;
   if (fs_copy_) fa.ts_copy_len = pg_timestamp(edge_ts, fa.ts_copy);
+  fa.ts_wire_len = std::snprintf(fa.ts_wire, sizeof fa.ts_wire, "%lld|", (long long)edge_ts);
   fa.st_len = d_fmt_len_;
   fa.fs_len = d_fmt_len_ + (S + 1);
   fa.st_off = d_fmt_off_;

@@ -192,6 +192,25 @@ class ThreadPool {
   bool stop_ = false;
 };
 
+// One background thread running posted tasks in order; wait(id) returns once task `id` is done
+// and rethrows the first exception a task threw.
+class TaskLane {
+ public:
+  TaskLane();
+  ~TaskLane();
+  uint64_t post(std::function<void()> fn);
+  void wait(uint64_t id);
+
+ private:
+  std::thread th_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  uint64_t posted_ = 0, done_ = 0;
+  std::string err_;
+  bool stop_ = false;
+};
+
 class Engine {
  public:
   explicit Engine(const EngineConfig& cfg);
@@ -541,6 +560,9 @@ class Engine {
   Dictionary dict_;
   std::vector<std::unique_ptr<JoinShard>> shards_;  // one per server
   std::unique_ptr<ThreadPool> pool_;
+  // device join: the next batch's parse finish + host pre-pass, overlapping this batch's join
+  std::unique_ptr<TaskLane> ahead_lane_;
+  uint64_t ahead_task_ = 0;
   std::vector<int> lane_cpus_;  // pinned placement (empty: unpinned)
   std::vector<double> shard_ms_;  // per-shard join time of the current batch (stride 16)
 
