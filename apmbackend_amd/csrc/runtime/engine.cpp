@@ -2419,9 +2419,11 @@ void Engine::pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream,
                           hipMemcpyHostToDevice, stream_));
     series_service_uploaded_ = n_series_;
   }
-  // the pack reads the z-score state written on the main stream: order comm after it
-  HIP_OK(hipEventRecord(ev_a_, stream_));
-  HIP_OK(hipStreamWaitEvent(stream, ev_a_, 0));
+  // the pack reads the z-score state written on the main stream: order another stream after it
+  if (stream != stream_) {
+    HIP_OK(hipEventRecord(ev_a_, stream_));
+    HIP_OK(hipStreamWaitEvent(stream, ev_a_, 0));
+  }
   if (!atomic_path && cfg_.n_lags * NSTAT * 2 + 1 <= 16) {
     // MFMA Gram path (fleet.hip): series listed per service (CSR).  Series added since the CSR
     // snapshot are accumulated by the atomic kernel on top; the CSR is rebuilt (host pass + a
@@ -2526,7 +2528,7 @@ void Engine::pack_service_moments(double* d_dst, int32_t cap, hipStream_t stream
 // Per batch i, every rank issues exactly, in this order:
 //   1. (lock-step) all-reduce(MAX) of {watermark, newest bucket} -- 16 B, host waits for it;
 //   2. (fleet)     all-reduce(SUM) of the per-service moments of batch i-1 -- async.
-// The moments of batch i-1 are packed by the stats thread on the comm stream (pack_ev_), which
+// The moments of batch i-1 are packed by the stats thread on the stats stream (pack_ev_), which
 // is guaranteed enqueued once post_stats(i) returned.  A single issuing thread per communicator
 // and a fixed per-batch sequence make the collective order identical on every rank, whatever
 // the thread timing, and no other stream ever waits on a peer (two communicators driven from
@@ -2666,14 +2668,18 @@ void Engine::apply_latest_locked(int64_t g, double batch_t0) {
 void Engine::fleet_pack_locked() {
   if (!coll_) return;
   const int slot = (int)(fleet_packed_ & 1);
-  if (fleet_packed_ >= 2) HIP_OK(hipStreamWaitEvent(comm_stream_, fleet_ev_[slot], 0));
+  // The slot's previous all-reduce (batch - 2) has long finished: check it on the host (with the
+  // collective watchdog) instead of a device-side wait, so the stats stream never depends on a
+  // peer, and pack on the stats stream itself -- a cross-stream wait makes the next enqueue on
+  // the waiting stream block the host until the awaited work is done.
+  if (fleet_packed_ >= 2) coll_wait(nullptr, fleet_ev_[slot], "fleet slot reuse");
   // a rollover happened since the previous pack: this exchange's merge is that interval's fb
   pack_edge_[slot] = metrics_.rollovers != last_edge_seen_ ? last_edge_ts_ : 0;
   last_edge_seen_ = metrics_.rollovers;
   const double t0 = now_ms();
-  pack_moments_locked(fleet_buf_[slot], fleet_cap_, comm_stream_);
+  pack_moments_locked(fleet_buf_[slot], fleet_cap_, stream_);
   trace_event("fleet.pack", t0, now_ms(), 1);
-  HIP_OK(hipEventRecord(pack_ev_[slot], comm_stream_));
+  HIP_OK(hipEventRecord(pack_ev_[slot], stream_));
   ++fleet_packed_;
 }
 
