@@ -1144,6 +1144,7 @@ void Engine::stats_worker() {
     try {
       stats_seq_ = job.seq;
       stats_round_ = job.round;
+      apply_ctx_pending(job.seq);
       if (node_mode_) node_take_text();
       if (job.dev) {
         stats_for_batch_dev(job.dj, job.t0);
@@ -1250,6 +1251,7 @@ void Engine::flush() {
     if (!out_error_.empty()) { std::string e = out_error_; out_error_.clear(); throw std::runtime_error(e); }
   }
   if (!st_error_.empty()) { std::string e = st_error_; st_error_.clear(); throw std::runtime_error(e); }
+  apply_ctx_pending(UINT64_MAX);  // the stats thread is idle
   if (node_mode_) {  // decided node-wide alerts (ingest thread) -> the al stream
     node_take_text();
     drain_kind(OUT_AL);
@@ -2183,19 +2185,35 @@ void Engine::format_rollover_text(int64_t edge_ts) {
   });
 }
 
+// Ingest (caller) thread: the sample applies from the next processed batch on.
 bool Engine::set_server_context(const std::string& server, double ts_ms, const std::vector<double>& gauges,
                                 double host_load) {
-  flush();
   auto it = server_ids_.find(server);
   if (it == server_ids_.end()) return false;
-  const int32_t v = it->second;
-  if (h_ctx_.size() < (size_t)(v + 1) * CTX_FIELDS) h_ctx_.resize((size_t)(v + 1) * CTX_FIELDS, 0.0);
-  double* row = h_ctx_.data() + (size_t)v * CTX_FIELDS;
-  row[0] = ts_ms;
-  for (int k = 0; k < 16; ++k) row[1 + k] = k < (int)gauges.size() ? gauges[k] : apm_nan();
-  row[17] = host_load;
-  ctx_dirty_ = true;
+  CtxUpdate u;
+  u.batch = batch_no_;
+  u.server = it->second;
+  u.row[0] = ts_ms;
+  for (int k = 0; k < 16; ++k) u.row[1 + k] = k < (int)gauges.size() ? gauges[k] : apm_nan();
+  u.row[17] = host_load;
+  std::lock_guard<std::mutex> g(ctx_mu_);
+  ctx_pending_.push_back(u);
   return true;
+}
+
+// Stats thread (or a caller with the stats thread idle): fold the samples of batches <= upto.
+void Engine::apply_ctx_pending(uint64_t upto) {
+  std::lock_guard<std::mutex> g(ctx_mu_);
+  size_t k = 0;
+  for (const CtxUpdate& u : ctx_pending_) {
+    if (u.batch > upto) break;  // tags ascend
+    const int32_t v = u.server;
+    if (h_ctx_.size() < (size_t)(v + 1) * CTX_FIELDS) h_ctx_.resize((size_t)(v + 1) * CTX_FIELDS, 0.0);
+    std::copy(u.row, u.row + CTX_FIELDS, h_ctx_.data() + (size_t)v * CTX_FIELDS);
+    ctx_dirty_ = true;
+    ++k;
+  }
+  ctx_pending_.erase(ctx_pending_.begin(), ctx_pending_.begin() + (ptrdiff_t)k);
 }
 
 void Engine::server_rollup(int64_t edge_ts) {
@@ -2219,11 +2237,13 @@ void Engine::server_rollup(int64_t edge_ts) {
     HIP_OK(hipStreamSynchronize(stream_));
     series_server_uploaded_ = n_series_;
   }
-  if (ctx_dirty_) {
-    std::vector<double> full((size_t)nsv * CTX_FIELDS, 0.0);
-    std::copy(h_ctx_.begin(), h_ctx_.begin() + std::min(h_ctx_.size(), full.size()), full.begin());
-    HIP_OK(hipMemcpyAsync(d_ctx_, full.data(), full.size() * 8, hipMemcpyHostToDevice, stream_));
-    HIP_OK(hipStreamSynchronize(stream_));
+  if (ctx_dirty_) {  // (a JMX sample per server per batch: pinned staging, no stream sync)
+    const size_t nb = (size_t)nsv * CTX_FIELDS * 8;
+    double* full = reinterpret_cast<double*>(stage(nb));
+    std::fill(full, full + (size_t)nsv * CTX_FIELDS, 0.0);
+    std::copy(h_ctx_.begin(), h_ctx_.begin() + std::min(h_ctx_.size(), (size_t)nsv * CTX_FIELDS), full);
+    HIP_OK(hipMemcpyAsync(d_ctx_, full, nb, hipMemcpyHostToDevice, stream_));
+    stage_done();
     ctx_dirty_ = false;
   }
   RollupArgs ra{};

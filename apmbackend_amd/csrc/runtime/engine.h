@@ -848,8 +848,14 @@ class Engine {
   bool fs_copy_ = false;
   uint64_t sink_bytes_[N_OUT] = {0, 0, 0, 0, 0, 0, 0, 0};
   // K14 server rollup + exogenous context
-  std::vector<double> h_ctx_;                    // [servers][CTX_FIELDS]
+  std::vector<double> h_ctx_;                    // [servers][CTX_FIELDS] (stats thread)
   bool ctx_dirty_ = false;
+  // set_server_context -> stats thread: rows tagged with the batch they precede, applied when
+  // the stats thread starts that batch (no pipeline drain per JMX sample)
+  struct CtxUpdate { uint64_t batch; int32_t server; double row[CTX_FIELDS]; };
+  std::mutex ctx_mu_;
+  std::vector<CtxUpdate> ctx_pending_;
+  void apply_ctx_pending(uint64_t upto);
   size_t roll_cap_ = 0;                          // servers the device buffers hold
   double* d_ctx_ = nullptr;
   unsigned long long* d_roll_acc_ = nullptr;
