@@ -370,6 +370,10 @@ class Engine {
   void ensure_bucket_slot(int64_t b);
   void do_rollover(int64_t L, double batch_t0);
   void flush_alerts(int64_t edge_ts);
+  void finish_rollover();
+  bool roll_pending_ = false;  // do_rollover queued; its decision is made by finish_rollover
+  int64_t roll_edge_ts_ = 0;
+  double roll_batch_t0_ = 0;
   void format_rollover_text(int64_t edge_ts);       // K12 on the GPU
   void format_rollover_text_host(int64_t edge_ts);  // fallback (|value| >= 1e13)
   void sync_format_tables();
