@@ -25,6 +25,7 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -274,8 +275,11 @@ class DbSink : public ByteSink {
   }
 
   // Rows already in COPY text for `type` (the engine's fs stream in COPY mode): buffered and
-  // flushed with the same limit / timer rules, written without encoding.
+  // flushed with the same limit / timer rules, written without encoding.  A rollover's fs rows
+  // (tens of MB) are cut at the flush limit and copied into their flush jobs by several threads;
+  // the resulting buffers and jobs are exactly those of the serial path.
   int64_t consume_encoded(int type, std::string_view blob) {
+    if (blob.size() >= kParallelBytes) return consume_encoded_parallel(type, blob);
     const double now = mono_ms();
     std::lock_guard<std::mutex> lk(mu_);
     encoded_[type] = true;
@@ -296,6 +300,94 @@ class DbSink : public ByteSink {
       i = j;
     }
     return n;
+  }
+
+  static constexpr size_t kParallelBytes = 4u << 20;
+
+  template <class F>
+  static void parallel_for(int n, const F& fn) {
+    std::vector<std::thread> th;
+    for (int i = 1; i < n; ++i) th.emplace_back([&fn, i] { fn(i); });
+    fn(0);
+    for (auto& t : th) t.join();
+  }
+
+  int64_t consume_encoded_parallel(int type, std::string_view blob) {
+    const double now = mono_ms();
+    const char* d = blob.data();
+    const size_t size = blob.size();
+    const int P = (int)std::max<size_t>(2, std::min<size_t>(8, size >> 20));
+    // parts start at line starts
+    std::vector<size_t> b(P + 1, size);
+    b[0] = 0;
+    for (int p = 1; p < P; ++p) {
+      const size_t x = std::max(b[p - 1], size * (size_t)p / (size_t)P);
+      const char* q = x < size ? (const char*)std::memchr(d + x, '\n', size - x) : nullptr;
+      b[p] = q ? (size_t)(q - d) + 1 : size;
+    }
+    std::vector<int64_t> cnt(P, 0);
+    parallel_for(P, [&](int p) {
+      const size_t lo = b[p], hi = b[p + 1];
+      int64_t c = std::count(d + lo, d + hi, '\n');
+      if (hi > lo && d[hi - 1] != '\n') ++c;  // an unterminated last row (the serial path counts it)
+      cnt[p] = c;
+    });
+    std::vector<int64_t> r0(P + 1, 0);
+    for (int p = 0; p < P; ++p) r0[p + 1] = r0[p] + cnt[p];
+    const int64_t total = r0[P];
+    if (total == 0) return 0;
+    std::lock_guard<std::mutex> lk(mu_);
+    encoded_[type] = true;
+    // a full buffer is flushed before anything is added (as append_run_locked does); then the
+    // serial path's flushes hold `limit` consecutive rows each: A0 tops the buffer up to the
+    // limit, every later flush is `limit` rows of the blob, the remainder stays buffered
+    if (buf_[type].n >= limit_) submit_locked(type);
+    const int64_t room = limit_ - buf_[type].n;
+    std::vector<int64_t> cut;  // row index (from the blob start) where each append ends
+    for (int64_t c = std::min(room, total); ; c = std::min(c + limit_, total)) {
+      cut.push_back(c);
+      if (c == total) break;
+    }
+    // byte offset of each cut: found by the part holding its last row
+    std::vector<size_t> off(cut.size(), size);
+    parallel_for(P, [&](int p) {
+      size_t k = (size_t)(std::lower_bound(cut.begin(), cut.end(), r0[p] + 1) - cut.begin());
+      int64_t row = r0[p];
+      size_t i = b[p];
+      while (k < cut.size() && cut[k] <= r0[p + 1] && i < b[p + 1]) {
+        const char* q = (const char*)std::memchr(d + i, '\n', b[p + 1] - i);
+        i = q ? (size_t)(q - d) + 1 : b[p + 1];
+        if (++row == cut[k]) off[k++] = i;
+      }
+    });
+    // flushes: [buffer + A0], A1, ..., A(m-1); Am stays buffered
+    const size_t m = cut.size() - 1;
+    append_run_locked(type, d, off[0], cut[0], now);
+    if (m == 0) return total;
+    submit_locked(type);
+    std::vector<std::shared_ptr<Job>> mid(m - 1);
+    for (size_t k = 1; k < m; ++k) {
+      auto j = std::make_shared<Job>();
+      j->type = type;
+      j->n = cut[k] - cut[k - 1];
+      j->encoded.resize(off[k] - off[k - 1]);
+      mid[k - 1] = std::move(j);
+    }
+    if (!mid.empty()) {
+      const int T = (int)std::min<size_t>((size_t)P, mid.size());
+      parallel_for(T, [&](int t) {
+        for (size_t k = (size_t)t; k < mid.size(); k += (size_t)T)
+          std::memcpy(&mid[k]->encoded[0], d + off[k], mid[k]->encoded.size());
+      });
+      for (auto& j : mid) {
+        j->seq = next_seq_++;
+        j->ready = true;
+        order_.push_back(j);
+      }
+      cv_.notify_all();
+    }
+    append_run_locked(type, d + off[m - 1], off[m] - off[m - 1], cut[m] - cut[m - 1], now);
+    return total;
   }
 
   // Rows already in COPY text (e.g. re-loaded from a resume file) queued as one flush.

@@ -1923,9 +1923,13 @@ void Engine::release_device_finish() {
         h_rel_text_cap_[k] = total * 3 / 2 + (1 << 20);
         HIP_OK(hipHostMalloc((void**)&h_rel_text_[k], h_rel_text_cap_[k], hipHostMallocDefault));
       }
+      const double tl0 = now_ms();
       HIP_OK(hipMemcpyAsync(h_rel_text_[k], d_rel_text_[k], total, hipMemcpyDeviceToHost, out_stream_));
       HIP_OK(hipStreamSynchronize(out_stream_));
+      const double tl1 = now_ms();
       emit_bytes(OUT_DB, h_rel_text_[k], total);
+      trace_event("lane db D2H", tl0, tl1, 4);
+      trace_event("lane db emit", tl1, now_ms(), 4);
     });
   }
   metrics_.released += released;
@@ -2192,6 +2196,7 @@ void Engine::format_rollover_text(int64_t edge_ts) {
       HIP_OK(hipHostMalloc((void**)&h_fmt_out_[k], h_fmt_cap_[k], hipHostMallocDefault));
     }
     char* h = h_fmt_out_[k];
+    const double tl0 = now_ms();
     if (st_total) HIP_OK(hipMemcpyAsync(h, dst, st_total, hipMemcpyDeviceToHost, out_stream_));
     if (fs_total) HIP_OK(hipMemcpyAsync(h + st_total, dst + st_cap, fs_total, hipMemcpyDeviceToHost, out_stream_));
     HIP_OK(hipStreamSynchronize(out_stream_));
@@ -2199,8 +2204,11 @@ void Engine::format_rollover_text(int64_t edge_ts) {
       std::lock_guard<std::mutex> g(out_mu_);
       formatted_bytes_lane_ += st_total + fs_total;
     }
+    const double tl1 = now_ms();
     emit_bytes(OUT_ST, h, st_total);
     emit_bytes(OUT_FS, h + st_total, fs_total);
+    trace_event("lane st/fs D2H", tl0, tl1, 4);
+    trace_event("lane st/fs emit", tl1, now_ms(), 4);
   });
 }
 

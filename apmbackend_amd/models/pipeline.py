@@ -213,7 +213,7 @@ class APMEngine:
         """Write the recorded stage intervals (set_trace(True) first) as a Chrome trace."""
         import json
         ev = self.eng.take_trace()
-        names = {0: "ingest (parse + join)", 1: "stats thread", 2: "device join phases", 3: "next-batch lane"}
+        names = {0: "ingest (parse + join)", 1: "stats thread", 2: "device join phases", 3: "next-batch lane", 4: "output lane"}
         out = [{"name": "thread_name", "ph": "M", "pid": pid, "tid": t, "args": {"name": n}} for t, n in names.items()]
         for name, t0, t1, tid, batch in ev:
             out.append({"name": name, "ph": "X", "ts": t0 * 1000.0, "dur": max(0.0, (t1 - t0) * 1000.0), "pid": pid,

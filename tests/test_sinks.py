@@ -287,3 +287,42 @@ def test_fleet_rows_encode_natively_like_python():
         assert nat["fb"][0].decode() == "".join(want["fb"]) and nat["fb"][1] == 2
     assert want["fb"][0].startswith("2020-01-07 10:00:00.000+00\tS:getFoo\t6\t8\t{\"averagemean\":123.4,")
     assert '"per95mean":null' in want["fb"][0]
+
+
+@pytest.mark.skipif(not _native_ok(), reason="native extension not built")
+@pytest.mark.parametrize("limit,pre", [(1000, 0), (1000, 437), (1000, 1000), (7, 3), (1, 0)])
+def test_native_sink_parallel_cut_equals_serial(tmp_path, limit, pre):
+    """A rollover's COPY rows (> 4 MB) are cut at the flush limit and copied by several threads;
+    the flushes (rows each, order, bytes) and the buffered remainder must be those of the serial
+    path, which the same rows fed in small pieces take -- whatever the buffer held before."""
+    import random
+    from apmbackend_amd import _native
+    N = _native.load(build_if_missing=False)
+    rng = random.Random(limit * 1000 + pre)
+    rows = [("r%07d\t" % i) + "x" * rng.randint(5, 400) + "\n" for i in range(30000)]
+    head, body = "".join(rows[:pre]), "".join(rows[pre:])
+    assert len(body) > 4 << 20
+    results = []
+    for mode in ("one-shot", "pieces"):
+        d = tmp_path / mode
+        s = N.DbSink(limit, 1e9, ["t_tx", "t_fs", "t_al", "t_jx", "t_fb"], ["a", "b", "c", "d", "e"], "spool",
+                     [str(d)], 1 << 62, 2)
+        if head:
+            s.consume_encoded(1, head.encode())
+        if mode == "one-shot":
+            assert s.consume_encoded(1, body.encode()) == len(rows) - pre
+        else:
+            b = body.encode()
+            pos = 0
+            while pos < len(b):  # < 4 MB pieces at row boundaries: the serial path
+                end = b.find(b"\n", min(len(b) - 1, pos + (1 << 20))) + 1
+                s.consume_encoded(1, b[pos:end])
+                pos = end
+        s.drain()
+        st = s.stats()
+        s.flush_all()
+        s.drain()
+        results.append((st["flushes"], st["rows"], st["buffered"], open(d / "t_fs.copy").read()))
+    assert results[0] == results[1]
+    assert results[0][3] == head + body
+    assert results[0][1] == (len(rows) - results[0][2])
