@@ -279,7 +279,7 @@ class DbSink : public ByteSink {
   // (tens of MB) are cut at the flush limit and copied into their flush jobs by several threads;
   // the resulting buffers and jobs are exactly those of the serial path.
   int64_t consume_encoded(int type, std::string_view blob) {
-    if (blob.size() >= kParallelBytes) return consume_encoded_parallel(type, blob);
+    if (blob.size() >= kParallelBytes && blob.size() < (1ull << 32)) return consume_encoded_parallel(type, blob);
     const double now = mono_ms();
     std::lock_guard<std::mutex> lk(mu_);
     encoded_[type] = true;
@@ -303,6 +303,20 @@ class DbSink : public ByteSink {
   }
 
   static constexpr size_t kParallelBytes = 4u << 20;
+  static constexpr size_t kSpares = 256;
+
+  // Flush buffers are recycled: a rollover's COPY rows are tens of MB in ~250 KB flushes, and
+  // fresh allocations of that size are mmap'd and page-faulted in on every batch.
+  std::string take_spare_locked() {
+    if (spare_.empty()) return std::string();
+    std::string s = std::move(spare_.back());
+    spare_.pop_back();
+    s.clear();
+    return s;
+  }
+  void give_spare_locked(std::string&& s) {
+    if (spare_.size() < kSpares && s.capacity() >= (64u << 10)) spare_.push_back(std::move(s));
+  }
 
   template <class F>
   static void parallel_for(int n, const F& fn) {
@@ -325,15 +339,21 @@ class DbSink : public ByteSink {
       const char* q = x < size ? (const char*)std::memchr(d + x, '\n', size - x) : nullptr;
       b[p] = q ? (size_t)(q - d) + 1 : size;
     }
-    std::vector<int64_t> cnt(P, 0);
+    // one pass per part: the end offset of every row (a row is a line; an unterminated tail
+    // counts as one, as on the serial path)
+    std::vector<std::vector<uint32_t>> ends(P);
     parallel_for(P, [&](int p) {
-      const size_t lo = b[p], hi = b[p + 1];
-      int64_t c = std::count(d + lo, d + hi, '\n');
-      if (hi > lo && d[hi - 1] != '\n') ++c;  // an unterminated last row (the serial path counts it)
-      cnt[p] = c;
+      std::vector<uint32_t>& e = ends[p];
+      e.reserve((b[p + 1] - b[p]) / 128 + 16);
+      size_t i = b[p];
+      while (i < b[p + 1]) {
+        const char* q = (const char*)std::memchr(d + i, '\n', b[p + 1] - i);
+        i = q ? (size_t)(q - d) + 1 : b[p + 1];
+        e.push_back((uint32_t)(i - b[p]));
+      }
     });
     std::vector<int64_t> r0(P + 1, 0);
-    for (int p = 0; p < P; ++p) r0[p + 1] = r0[p] + cnt[p];
+    for (int p = 0; p < P; ++p) r0[p + 1] = r0[p] + (int64_t)ends[p].size();
     const int64_t total = r0[P];
     if (total == 0) return 0;
     std::lock_guard<std::mutex> lk(mu_);
@@ -348,18 +368,14 @@ class DbSink : public ByteSink {
       cut.push_back(c);
       if (c == total) break;
     }
-    // byte offset of each cut: found by the part holding its last row
-    std::vector<size_t> off(cut.size(), size);
-    parallel_for(P, [&](int p) {
-      size_t k = (size_t)(std::lower_bound(cut.begin(), cut.end(), r0[p] + 1) - cut.begin());
-      int64_t row = r0[p];
-      size_t i = b[p];
-      while (k < cut.size() && cut[k] <= r0[p + 1] && i < b[p + 1]) {
-        const char* q = (const char*)std::memchr(d + i, '\n', b[p + 1] - i);
-        i = q ? (size_t)(q - d) + 1 : b[p + 1];
-        if (++row == cut[k]) off[k++] = i;
+    std::vector<size_t> off(cut.size());
+    {
+      int p = 0;
+      for (size_t k = 0; k < cut.size(); ++k) {
+        while (cut[k] > r0[p + 1]) ++p;
+        off[k] = b[p] + ends[p][(size_t)(cut[k] - r0[p] - 1)];
       }
-    });
+    }
     // flushes: [buffer + A0], A1, ..., A(m-1); Am stays buffered
     const size_t m = cut.size() - 1;
     append_run_locked(type, d, off[0], cut[0], now);
@@ -370,14 +386,14 @@ class DbSink : public ByteSink {
       auto j = std::make_shared<Job>();
       j->type = type;
       j->n = cut[k] - cut[k - 1];
-      j->encoded.resize(off[k] - off[k - 1]);
+      j->encoded = take_spare_locked();  // recycled capacity: no page faults, no zero fill
       mid[k - 1] = std::move(j);
     }
     if (!mid.empty()) {
       const int T = (int)std::min<size_t>((size_t)P, mid.size());
       parallel_for(T, [&](int t) {
         for (size_t k = (size_t)t; k < mid.size(); k += (size_t)T)
-          std::memcpy(&mid[k]->encoded[0], d + off[k], mid[k]->encoded.size());
+          mid[k]->encoded.assign(d + off[k], off[k + 1] - off[k]);
       });
       for (auto& j : mid) {
         j->seq = next_seq_++;
@@ -508,6 +524,7 @@ class DbSink : public ByteSink {
       j->lines.swap(buf_[t].lines);
       to_encode_.push_back(j);
     }
+    buf_[t].lines = take_spare_locked();
     buf_[t].n = 0;
     order_.push_back(j);
     cv_.notify_all();
@@ -555,6 +572,8 @@ class DbSink : public ByteSink {
           ms_ += dt;
           bytes_ += (int64_t)j->encoded.size();
           ++flushes_;
+          give_spare_locked(std::move(j->encoded));
+          give_spare_locked(std::move(j->lines));
         } else {
           ++failures_;
           last_error_ = err;
@@ -592,6 +611,7 @@ class DbSink : public ByteSink {
   Buf buf_[NT];
   bool encoded_[NT] = {false, false, false, false, false};  // type buffered as COPY rows (engine-encoded)
   std::deque<std::shared_ptr<Job>> order_, to_encode_;
+  std::vector<std::string> spare_;
   uint64_t next_seq_ = 0;
   bool stop_ = false;
   std::vector<std::thread> enc_;
@@ -646,6 +666,10 @@ void register_dbsink(py::module_& m) {
         std::string_view v = b;
         py::gil_scoped_release rel;
         return s.consume_encoded(type, v);
+      })
+      .def("consume_encoded_ptr", [](DbSink& s, int type, uintptr_t p, size_t n) {
+        py::gil_scoped_release rel;  // rows in caller-owned (e.g. pinned) memory
+        return s.consume_encoded(type, std::string_view(reinterpret_cast<const char*>(p), n));
       });
   m.def("attach_sink", [](Engine& e, const std::string& kind, std::shared_ptr<DbSink> s, int encoded_type) {
     py::gil_scoped_release rel;
