@@ -26,6 +26,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -85,6 +86,16 @@ struct Writer {
   virtual ~Writer() = default;
   // returns "" on success, else the error text
   virtual std::string write(int type, const std::string& table, const std::string& columns, const std::string& rows) = 0;
+  // Several consecutive flushes of one type, in order; returns how many were written (the rest
+  // failed with `err`).  Default: one at a time.
+  virtual size_t write_run(int type, const std::string& table, const std::string& columns,
+                           const std::vector<const std::string*>& rows, std::string& err) {
+    for (size_t i = 0; i < rows.size(); ++i) {
+      err = write(type, table, columns, *rows[i]);
+      if (!err.empty()) return i;
+    }
+    return rows.size();
+  }
 };
 
 struct NullWriter : Writer {
@@ -121,14 +132,62 @@ struct SpoolWriter : Writer {
         write_all(cf, c.data(), c.size());
         ::close(cf);
       }
-      fd[type] = ::open(path.c_str(), O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
+      // not O_APPEND: pwrite on an O_APPEND fd ignores its offset on Linux (write_run)
+      fd[type] = ::open(path.c_str(), O_WRONLY | O_CREAT | O_CLOEXEC, 0644);
       if (fd[type] < 0) return "cannot open " + path + ": " + std::strerror(errno);
       struct stat st;
       size[type] = ::fstat(fd[type], &st) == 0 ? (uint64_t)st.st_size : 0;
     }
-    if (!write_all(fd[type], rows.data(), rows.size())) return std::string("spool write failed: ") + std::strerror(errno);
+    if (rows.empty()) return "";
+    if (::lseek(fd[type], (off_t)size[type], SEEK_SET) < 0 || !write_all(fd[type], rows.data(), rows.size()))
+      return std::string("spool write failed: ") + std::strerror(errno);
     size[type] += rows.size();
     return "";
+  }
+  // A run of flushes (a rollover's fs rows: tens of MB): offsets are fixed by the order, so the
+  // copies into the file run on several threads (pwrite at the reserved offsets); a failure
+  // truncates the file back and fails the whole run, which is re-buffered in order.
+  size_t write_run(int type, const std::string& table, const std::string& columns,
+                   const std::vector<const std::string*>& rows, std::string& err) override {
+    size_t total = 0;
+    for (const std::string* r : rows) total += r->size();
+    if (rows.size() < 4 || total < (8u << 20)) return Writer::write_run(type, table, columns, rows, err);
+    err = write(type, table, columns, std::string());  // rotation / open, no bytes
+    if (!err.empty()) return 0;
+    const uint64_t base = size[type];
+    const int f = fd[type];
+    std::vector<uint64_t> at(rows.size());
+    uint64_t pos = base;
+    for (size_t i = 0; i < rows.size(); ++i) { at[i] = pos; pos += rows[i]->size(); }
+    std::atomic<bool> bad{false};
+    const int T = (int)std::min<size_t>(4, rows.size());
+    std::vector<std::thread> th;
+    auto work = [&](int t) {
+      for (size_t i = (size_t)t; i < rows.size() && !bad.load(); i += (size_t)T) {
+        const char* p = rows[i]->data();
+        size_t n = rows[i]->size();
+        uint64_t o = at[i];
+        while (n) {
+          const ssize_t w = ::pwrite(f, p, n, (off_t)o);
+          if (w < 0) {
+            if (errno == EINTR) continue;
+            bad = true;
+            break;
+          }
+          p += w; n -= (size_t)w; o += (uint64_t)w;
+        }
+      }
+    };
+    for (int t = 1; t < T; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+    if (bad) {
+      err = std::string("spool write failed: ") + std::strerror(errno);
+      if (::ftruncate(f, (off_t)base) != 0) err += " (and the truncate back failed)";
+      return 0;
+    }
+    size[type] = pos;
+    return rows.size();
   }
 };
 
@@ -554,35 +613,49 @@ class DbSink : public ByteSink {
 
   void write_loop() {
     for (;;) {
-      std::shared_ptr<Job> j;
+      std::vector<std::shared_ptr<Job>> run;  // consecutive ready flushes of one type
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return (!order_.empty() && order_.front()->ready) || (stop_ && order_.empty()); });
         if (order_.empty()) return;
-        j = order_.front();
+        const int t = order_.front()->type;
+        for (size_t i = 0; i < order_.size() && i < 256 && order_[i]->ready && order_[i]->type == t; ++i)
+          run.push_back(order_[i]);
       }
+      const int t = run[0]->type;
+      std::vector<const std::string*> rows;
+      for (auto& j : run) rows.push_back(&j->encoded);
+      std::string err;
       const double t0 = mono_ms();
-      const std::string err = w_->write(j->type, tables_[j->type], columns_[j->type], j->encoded);
+      const size_t ok = w_->write_run(t, tables_[t], columns_[t], rows, err);
       const double dt = mono_ms() - t0;
       {
         std::lock_guard<std::mutex> lk(mu_);
-        order_.pop_front();
-        if (err.empty()) {
-          rows_ += j->n;
-          ms_ += dt;
-          bytes_ += (int64_t)j->encoded.size();
+        for (size_t i = 0; i < run.size(); ++i) order_.pop_front();
+        for (size_t i = 0; i < ok; ++i) {
+          Job& j = *run[i];
+          rows_ += j.n;
+          bytes_ += (int64_t)j.encoded.size();
           ++flushes_;
-          give_spare_locked(std::move(j->encoded));
-          give_spare_locked(std::move(j->lines));
-        } else {
-          ++failures_;
+          give_spare_locked(std::move(j.encoded));
+          give_spare_locked(std::move(j.lines));
+        }
+        ms_ += dt;
+        if (ok < run.size()) {
+          failures_ += (int64_t)(run.size() - ok);
           last_error_ = err;
-          const std::string& back = encoded_[j->type] ? j->encoded : j->lines;
-          if (!back.empty()) {  // back to the front of its buffer (:310-320)
-            Buf& b = buf_[j->type];
+          // back to the front of its buffer, in order (:310-320)
+          Buf& b = buf_[t];
+          std::string back;
+          int64_t n = 0;
+          for (size_t i = ok; i < run.size(); ++i) {
+            back += encoded_[t] ? run[i]->encoded : run[i]->lines;
+            n += run[i]->n;
+          }
+          if (!back.empty()) {
             if (b.n == 0) b.deadline = mono_ms() + max_wait_ms_;
             b.lines.insert(0, back);
-            b.n += j->n;
+            b.n += n;
           }
         }
       }

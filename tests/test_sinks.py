@@ -299,7 +299,7 @@ def test_native_sink_parallel_cut_equals_serial(tmp_path, limit, pre):
     from apmbackend_amd import _native
     N = _native.load(build_if_missing=False)
     rng = random.Random(limit * 1000 + pre)
-    rows = [("r%07d\t" % i) + "x" * rng.randint(5, 400) + "\n" for i in range(30000)]
+    rows = [("r%07d\t" % i) + "x" * rng.randint(5, 400) + "\n" for i in range(50000)]  # > 8 MB: parallel spool writes too
     head, body = "".join(rows[:pre]), "".join(rows[pre:])
     assert len(body) > 4 << 20
     results = []
