@@ -22,6 +22,7 @@
 #include <signal.h>
 #include <spawn.h>
 #include <sys/stat.h>
+#include <sys/uio.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -144,50 +145,45 @@ struct SpoolWriter : Writer {
     size[type] += rows.size();
     return "";
   }
-  // A run of flushes (a rollover's fs rows: tens of MB): offsets are fixed by the order, so the
-  // copies into the file run on several threads (pwrite at the reserved offsets); a failure
-  // truncates the file back and fails the whole run, which is re-buffered in order.
+  // A run of flushes: one writev per run (tmpfs serialises writers on the inode, so copying a
+  // run on several threads measured slower: 174-191 ms vs 115 ms for 0.5 GB).
   size_t write_run(int type, const std::string& table, const std::string& columns,
                    const std::vector<const std::string*>& rows, std::string& err) override {
-    size_t total = 0;
-    for (const std::string* r : rows) total += r->size();
-    if (rows.size() < 4 || total < (8u << 20)) return Writer::write_run(type, table, columns, rows, err);
     err = write(type, table, columns, std::string());  // rotation / open, no bytes
     if (!err.empty()) return 0;
-    const uint64_t base = size[type];
-    const int f = fd[type];
-    std::vector<uint64_t> at(rows.size());
-    uint64_t pos = base;
-    for (size_t i = 0; i < rows.size(); ++i) { at[i] = pos; pos += rows[i]->size(); }
-    std::atomic<bool> bad{false};
-    const int T = (int)std::min<size_t>(4, rows.size());
-    std::vector<std::thread> th;
-    auto work = [&](int t) {
-      for (size_t i = (size_t)t; i < rows.size() && !bad.load(); i += (size_t)T) {
-        const char* p = rows[i]->data();
-        size_t n = rows[i]->size();
-        uint64_t o = at[i];
-        while (n) {
-          const ssize_t w = ::pwrite(f, p, n, (off_t)o);
-          if (w < 0) {
-            if (errno == EINTR) continue;
-            bad = true;
-            break;
-          }
-          p += w; n -= (size_t)w; o += (uint64_t)w;
+    size_t done = 0;
+    while (done < rows.size()) {
+      struct iovec iov[64];
+      int k = 0;
+      size_t bytes = 0;
+      for (size_t i = done; i < rows.size() && k < 64; ++i, ++k) {
+        iov[k].iov_base = const_cast<char*>(rows[i]->data());
+        iov[k].iov_len = rows[i]->size();
+        bytes += rows[i]->size();
+      }
+      if (::lseek(fd[type], (off_t)size[type], SEEK_SET) < 0) { err = std::strerror(errno); return done; }
+      size_t left = bytes;
+      int first = 0;
+      while (left) {
+        const ssize_t w = ::writev(fd[type], iov + first, k - first);
+        if (w < 0) {
+          if (errno == EINTR) continue;
+          err = std::string("spool write failed: ") + std::strerror(errno);
+          if (::ftruncate(fd[type], (off_t)size[type]) != 0) err += " (and the truncate back failed)";
+          return done;
+        }
+        left -= (size_t)w;
+        size_t adv = (size_t)w;
+        while (first < k && adv >= iov[first].iov_len) { adv -= iov[first].iov_len; ++first; }
+        if (first < k && adv) {
+          iov[first].iov_base = (char*)iov[first].iov_base + adv;
+          iov[first].iov_len -= adv;
         }
       }
-    };
-    for (int t = 1; t < T; ++t) th.emplace_back(work, t);
-    work(0);
-    for (auto& x : th) x.join();
-    if (bad) {
-      err = std::string("spool write failed: ") + std::strerror(errno);
-      if (::ftruncate(f, (off_t)base) != 0) err += " (and the truncate back failed)";
-      return 0;
+      size[type] += bytes;
+      done += (size_t)k;
     }
-    size[type] = pos;
-    return rows.size();
+    return done;
   }
 };
 
