@@ -90,6 +90,20 @@ struct RollupArgs {
   double* out;                    // [n_servers][ROLLUP_OUT]
 };
 
+// apm_export: device scalars -> pinned host memory (stats.hip)
+struct ExportArgs {
+  static constexpr int kMax = 8;
+  void* src[kMax];  // device scalars
+  void* dst[kMax];  // device views of pinned host memory
+  uint64_t reset_val[kMax];
+  uint8_t bytes[kMax];  // 4 or 8
+  uint8_t reset[kMax];
+  int32_t n;
+  void add(void* s, void* d, int nb, bool rst = false, uint64_t rv = 0) {
+    src[n] = s; dst[n] = d; bytes[n] = (uint8_t)nb; reset[n] = rst ? 1 : 0; reset_val[n] = rv; ++n;
+  }
+};
+
 // K12 st/fs encoding (format.hip)
 struct FormatArgs {
   const int32_t* perm;          // [n] series in emission order
@@ -177,6 +191,8 @@ size_t apm_release_tmp_bytes(int64_t cap);
 int apm_release_merge(const int64_t* pool_end, const int64_t* pool_gid, int64_t n_pool, const int64_t* tail_end,
                       const int64_t* tail_gid, int64_t n_tail, int64_t* sort_end, int64_t* sort_gid,
                       int64_t* out_end, int64_t* out_gid, void* tmp, size_t tmp_bytes, hipStream_t stream);
+// device scalars (4 or 8 bytes) -> host-mapped pinned memory, optional device reset afterwards
+void apm_export(const apm::ExportArgs* a, hipStream_t stream);
 // zscore.hip
 void apm_zscore(apm::ZArgs* a, int dtype_bytes, hipStream_t stream);
 void apm_zscore_warm(apm::ZArgs* a, int dtype_bytes, int fill, uint64_t seed, const apm::WinStat* base,

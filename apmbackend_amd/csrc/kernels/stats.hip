@@ -79,6 +79,8 @@ __global__ __launch_bounds__(1024) void k_bucket_append_ordered(const TxRec* __r
   __shared__ int m_sh;
   const int n_ord = *st.ord_n;
   if (n_ord == 0) return;
+  __syncthreads();  // every thread has read the count: reset it for the next append
+  if (threadIdx.x == 0) *st.ord_n = 0;
   const uint32_t span = hi - lo;
   const uint32_t R = n_ord <= ORD_TILE ? span : (uint32_t)ORD_TILE;
   for (uint32_t r0 = 0; r0 < span; r0 += R) {
@@ -606,11 +608,31 @@ __global__ void k_pool_append(const TxRec* __restrict__ tx, uint32_t lo, uint32_
   tail_gid[base + (i - lo)] = gid[i];
 }
 
+// Device scalars -> host-mapped pinned memory in one launch (instead of one blit per value);
+// entries with a reset flag get their device value rewritten after the read.
+__global__ void k_export(ExportArgs a) {
+  const int i = threadIdx.x;
+  if (i >= a.n) return;
+  if (a.bytes[i] == 8) {
+    unsigned long long* s = (unsigned long long*)a.src[i];
+    *(unsigned long long*)a.dst[i] = *s;
+    if (a.reset[i]) *s = a.reset_val[i];
+  } else {
+    uint32_t* s = (uint32_t*)a.src[i];
+    *(uint32_t*)a.dst[i] = *s;
+    if (a.reset[i]) *s = (uint32_t)a.reset_val[i];
+  }
+}
+
 }  // namespace apm
 
 extern "C" {
 
 using namespace apm;
+
+void apm_export(const ExportArgs* a, hipStream_t stream) {
+  if (a->n > 0) hipLaunchKernelGGL(k_export, dim3(1), dim3(64), 0, stream, *a);
+}
 
 void apm_stats_clear_slot(StatsState* st, int slot, hipStream_t stream) {
   hipLaunchKernelGGL(k_clear_slot, dim3((st->S + 255) / 256), dim3(256), 0, stream, *st, slot);
@@ -619,7 +641,7 @@ void apm_stats_clear_slot(StatsState* st, int slot, hipStream_t stream) {
 void apm_bucket_append(const TxRec* d_tx, uint32_t lo, uint32_t hi, StatsState* st, int64_t min_live_bucket,
                        hipStream_t stream) {
   if (hi <= lo) return;
-  if (st->ord_n) HIP_OK(hipMemsetAsync(st->ord_n, 0, 4, stream));
+  // ord_n is zero here: k_bucket_append_ordered resets it after reading
   hipLaunchKernelGGL(k_bucket_append, dim3((hi - lo + 255) / 256), dim3(256), 0, stream, d_tx, lo, hi, *st,
                      min_live_bucket);
   if (st->ord_n) hipLaunchKernelGGL(k_bucket_append_ordered, dim3(1), dim3(1024), 0, stream, d_tx, lo, hi, *st);
@@ -630,9 +652,8 @@ void apm_nan_mark(const TxRec* d_tx, uint32_t n, StatsState* st, hipStream_t str
   hipLaunchKernelGGL(k_nan_mark, dim3((n + 255) / 256), dim3(256), 0, stream, d_tx, n, *st);
 }
 
+// big_n / nan_n must be zero on entry (the engine clears them with the rollover's other counters)
 void apm_window_stats(WindowArgs* a, hipStream_t stream) {
-  HIP_OK(hipMemsetAsync(a->big_n, 0, 4, stream));
-  HIP_OK(hipMemsetAsync(a->nan_n, 0, 4, stream));
   const int blocks = (a->n_series + WS_WAVES - 1) / WS_WAVES;
   if (blocks == 0) return;
   hipLaunchKernelGGL(k_window_stats, dim3(blocks), dim3(WS_WAVES * APM_WAVE), 0, stream, *a);

@@ -244,13 +244,17 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     dj_.reset(new DeviceJoin(dc, &dict_, &files_, &servers_));
     device_bytes_ += dj_->device_bytes();
     d_ring_min_ = (unsigned long long*)dmalloc(64);
+    HIP_OK(hipMemset(d_ring_min_, 0xff, 8));  // (the export after each min pass restores it)
     HIP_OK(hipHostMalloc((void**)&h_ring_min_, 64, hipHostMallocDefault));
+    HIP_OK(hipHostGetDevicePointer((void**)&hd_ring_min_, h_ring_min_, 0));
     *h_ring_min_ = ~0ULL;
     d_rel_n_ = (int64_t*)dmalloc(64);
     HIP_OK(hipHostMalloc((void**)&h_rel_n_, 64, hipHostMallocDefault));
+    HIP_OK(hipHostGetDevicePointer((void**)&hd_rel_n_, h_rel_n_, 0));
     d_rel_lens_ = (uint32_t*)dmalloc(((size_t)cfg_.pool_cap + 2) * 4);
     d_rel_offs_ = (uint32_t*)dmalloc(((size_t)cfg_.pool_cap + 2) * 4);
     HIP_OK(hipHostMalloc((void**)&h_rel_total_, 64, hipHostMallocDefault));
+    HIP_OK(hipHostGetDevicePointer((void**)&hd_rel_total_, h_rel_total_, 0));
     d_unmapped_ = (unsigned long long*)dmalloc(64);
     d_unseen_idx_ = (int32_t*)dmalloc((size_t)cfg_.max_series * 4);
     d_unseen_flag_ = (uint8_t*)dmalloc((size_t)cfg_.max_series);
@@ -296,14 +300,15 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   d_active_ = (uint8_t*)dmalloc(S);
   d_win_ = (WinStat*)dmalloc((size_t)S * sizeof(WinStat));
   d_big_list_ = (int32_t*)dmalloc((size_t)S * 4);
-  d_big_n_ = (int32_t*)dmalloc(4);
+  // per-rollover counters in one block, cleared by one memset: [0] big, [1] nan, [2] alert candidates
+  d_big_n_ = (int32_t*)dmalloc(64);
   d_nan_until_ = (int32_t*)dmalloc((size_t)S * 4);
   HIP_OK(hipMemset(d_nan_until_, 0x80, (size_t)S * 4));  // 0x80808080: far below any bucket
   ord_cap_ = std::max<int64_t>(cfg_.max_tx_per_batch, cfg_.max_lines);
   d_ord_list_ = (int32_t*)dmalloc((size_t)ord_cap_ * 4);
   d_ord_n_ = (int32_t*)dmalloc(4);
   d_nan_list_ = (int32_t*)dmalloc((size_t)S * 4);
-  d_nan_n_ = (int32_t*)dmalloc(4);
+  d_nan_n_ = d_big_n_ + 1;
   d_js_scratch_ = (int32_t*)dmalloc((size_t)JS_BLOCKS * kJsCap * 4);
   for (int i = 0; i < NSLOT; ++i) slot_bucket_[i] = NO_BUCKET;
   // z-score
@@ -353,9 +358,10 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   fmt_tmp_bytes_ = apm_format_tmp_bytes(S + 1);
   d_fmt_tmp_ = dmalloc(fmt_tmp_bytes_);
   HIP_OK(hipHostMalloc((void**)&h_fmt_meta_, 64, hipHostMallocDefault));
+  HIP_OK(hipHostGetDevicePointer((void**)&hd_fmt_meta_, h_fmt_meta_, 0));
   // alerts
   d_alerts_ = (AlertRec*)dmalloc((size_t)cfg_.max_alerts * sizeof(AlertRec));
-  d_n_alerts_ = (int32_t*)dmalloc(16);
+  d_n_alerts_ = d_big_n_ + 2;
   HIP_OK(hipHostMalloc((void**)&h_alerts_, (size_t)cfg_.max_alerts * sizeof(AlertRec), hipHostMallocDefault));
   HIP_OK(hipHostMalloc((void**)&h_alert_win_, (size_t)cfg_.max_alerts * sizeof(WinStat), hipHostMallocDefault));
   HIP_OK(hipHostMalloc((void**)&h_alert_z_, (size_t)cfg_.max_alerts * sizeof(ZOut), hipHostMallocDefault));
@@ -1806,9 +1812,9 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   wa.js_scratch = d_js_scratch_;
   wa.js_cap = kJsCap;
   wa.n_series = n_series_;
+  HIP_OK(hipMemsetAsync(d_big_n_, 0, 12, stream_));  // big / nan windows, alert candidates
   apm_window_stats(&wa, stream_);
   // ---- K10 z-score per LAG, K11 alert eval
-  HIP_OK(hipMemsetAsync(d_n_alerts_, 0, 4, stream_));
   for (int l = 0; l < cfg_.n_lags; ++l) {
     LagState& LS = lag_[l];
     ZArgs za;
@@ -1894,13 +1900,15 @@ void Engine::release_device(int64_t edge_ts) {
   pool_n_ += tail_n_;
   tail_n_ = 0;
   apm_dj_count_le(d_pool_end_[pool_cur_], pool_n_, edge_ts, d_rel_n_, stream_);
-  HIP_OK(hipMemcpyAsync(h_rel_n_, d_rel_n_, 8, hipMemcpyDeviceToHost, stream_));
+  ExportArgs ex{};
+  ex.add(d_rel_n_, hd_rel_n_, 8);
   if (want(OUT_DB) && pool_n_ > 0) {
     if (apm_dj_gather_plan(d_pool_gid_[pool_cur_], pool_n_, d_rel_n_, d_rel_lens_, d_rel_offs_, d_release_tmp_,
                            release_tmp_bytes_, stream_) != 0)
       throw std::runtime_error("release tmp too small");
-    HIP_OK(hipMemcpyAsync(h_rel_total_, d_rel_offs_ + pool_n_, 4, hipMemcpyDeviceToHost, stream_));
+    ex.add(d_rel_offs_ + pool_n_, hd_rel_total_, 4);
   }
+  apm_export(&ex, stream_);
 }
 
 // Part 2 (after the rollover's stream sync): the released count is known; gather the lines out
@@ -1940,9 +1948,11 @@ void Engine::release_device_finish() {
   const uint64_t prev_min = *h_ring_min_;
   const uint64_t low = std::min<uint64_t>(prev_min, ring_low_pending_);
   if (low != UINT64_MAX) dj_->set_ring_low(low);
-  HIP_OK(hipMemsetAsync(d_ring_min_, 0xff, 8, stream_));
+  // d_ring_min_ is UINT64_MAX here: the export below resets it after reading
   apm_dj_min_pos(d_pool_gid_[pool_cur_] + pool_off_, pool_n_, d_ring_min_, stream_);
-  HIP_OK(hipMemcpyAsync(h_ring_min_, d_ring_min_, 8, hipMemcpyDeviceToHost, stream_));
+  ExportArgs ex{};
+  ex.add(d_ring_min_, hd_ring_min_, 8, /*reset=*/true, ~0ull);
+  apm_export(&ex, stream_);
   ring_low_pending_ = cur_dj_ ? cur_dj_->ring_base : dj_->ring_head();
 }
 
@@ -2182,8 +2192,12 @@ void Engine::format_rollover_text(int64_t edge_ts) {
   fa.fs_out = d_fmt_out_[k] + st_cap;
   if (apm_format_plan(&fa, d_fmt_tmp_, fmt_tmp_bytes_, stream_) != 0) throw std::runtime_error("format scan failed");
   apm_format_write(&fa, stream_);
-  HIP_OK(hipMemcpyAsync(h_fmt_meta_ + 4 * k + 0, fa.st_off + n, 4, hipMemcpyDeviceToHost, stream_));
-  HIP_OK(hipMemcpyAsync(h_fmt_meta_ + 4 * k + 1, fa.fs_off + n, 4, hipMemcpyDeviceToHost, stream_));
+  {
+    ExportArgs ex{};
+    ex.add(fa.st_off + n, hd_fmt_meta_ + 4 * k + 0, 4);
+    ex.add(fa.fs_off + n, hd_fmt_meta_ + 4 * k + 1, 4);
+    apm_export(&ex, stream_);
+  }
   HIP_OK(hipEventRecord(ev_fmt_[k], stream_));
   trace_event("fmt.plan", tf0, now_ms(), 1);
   char* dst = d_fmt_out_[k];

@@ -604,11 +604,14 @@ class Engine {
   uint64_t ring_low_pending_ = UINT64_MAX;     // ring base of the batch at the last min_pos launch
   unsigned long long* d_ring_min_ = nullptr;
   unsigned long long* h_ring_min_ = nullptr;
+  unsigned long long* hd_ring_min_ = nullptr;  // device view (apm_export)
   int64_t* d_rel_n_ = nullptr;
   int64_t* h_rel_n_ = nullptr;
+  int64_t* hd_rel_n_ = nullptr;
   uint32_t* d_rel_lens_ = nullptr;
   uint32_t* d_rel_offs_ = nullptr;
   uint32_t* h_rel_total_ = nullptr;            // [2]
+  uint32_t* hd_rel_total_ = nullptr;
   char* d_rel_text_[2] = {nullptr, nullptr};
   size_t rel_text_cap_[2] = {0, 0};
   char* h_rel_text_[2] = {nullptr, nullptr};
@@ -844,6 +847,7 @@ class Engine {
   uint64_t fmt_task_[2] = {0, 0};
   int fmt_k_ = 0;
   uint32_t* h_fmt_meta_ = nullptr;               // pinned: per slot k, [4k] st total, [4k+1] fs total
+  uint32_t* hd_fmt_meta_ = nullptr;
 
   // text outputs
   std::string blob_[N_OUT];
