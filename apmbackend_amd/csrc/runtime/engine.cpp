@@ -223,7 +223,6 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipStreamCreateWithFlags(&parse_stream_, hipStreamNonBlocking));
   HIP_OK(hipStreamCreateWithFlags(&out_stream_, hipStreamNonBlocking));
   HIP_OK(hipEventCreateWithFlags(&ev_a_, hipEventDisableTiming));
-  HIP_OK(hipEventCreateWithFlags(&tail_csr_ev_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_b_, hipEventDisableTiming));
   const int32_t S = cfg_.max_series;
   // parse
@@ -480,8 +479,11 @@ Engine::~Engine() {
     if (h_stage_[k]) hipHostFree(h_stage_[k]);
     if (stage_ev_[k]) hipEventDestroy(stage_ev_[k]);
   }
-  hipEventDestroy(ev_a_); hipEventDestroy(ev_b_); hipEventDestroy(tail_csr_ev_);
-  if (h_tail_csr_) hipHostFree(h_tail_csr_);
+  hipEventDestroy(ev_a_); hipEventDestroy(ev_b_);
+  for (int k = 0; k < 2; ++k) {
+    if (tail_csr_ev_[k]) hipEventDestroy(tail_csr_ev_[k]);
+    if (h_tail_csr_[k]) hipHostFree(h_tail_csr_[k]);
+  }
   hipStreamDestroy(stream_); hipStreamDestroy(comm_stream_); hipStreamDestroy(parse_stream_);
 }
 
@@ -1961,10 +1963,18 @@ void Engine::flush_alerts(int64_t edge_ts) {
   metrics_.alert_candidates += na;
   if (na <= 0) return;
   const bool need_rows = want(OUT_AL);
+  // one sequential copy out of the GPU-written pinned buffers before the sort's random reads
+  std::vector<AlertRec> alerts(h_alerts_, h_alerts_ + na);
+  std::vector<WinStat> awin;
+  std::vector<ZOut> az;
+  if (need_rows) {
+    awin.assign(h_alert_win_, h_alert_win_ + na);
+    az.assign(h_alert_z_, h_alert_z_ + na);
+  }
   // candidate i's rows are win_of(i) / z_of(i) in device order; decide in emission order
   std::vector<int32_t> ord((size_t)na);
   for (int32_t i = 0; i < na; ++i) ord[i] = i;
-  std::sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return h_alerts_[a].order < h_alerts_[b].order; });
+  std::sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return alerts[a].order < alerts[b].order; });
   // per-(service|series) cooldown, first candidate in emission order wins (:436-468)
   const double now = cfg_.alert_clock_entry ? (double)edge_ts
                                             : (double)std::chrono::duration_cast<std::chrono::milliseconds>(
@@ -1974,7 +1984,7 @@ void Engine::flush_alerts(int64_t edge_ts) {
     std::lock_guard<std::mutex> g(node_mu_);
     for (int32_t j = 0; j < na; ++j) {
       const int32_t i = ord[j];
-      const AlertRec& r = h_alerts_[i];
+      const AlertRec& r = alerts[i];
       const SeriesInfo& si = series_[r.series];
       const std::string& svc = dict_.service_name(si.service);
       NodePayload p;
@@ -1997,7 +2007,7 @@ void Engine::flush_alerts(int64_t edge_ts) {
       p.c.local_id = node_next_id_++;
       p.server = servers_[si.server];
       p.service = svc;
-      if (need_rows) { p.w = h_alert_win_[i]; p.z = h_alert_z_[i]; }
+      if (need_rows) { p.w = awin[i]; p.z = az[i]; }
       p.lag = cfg_.lags[r.lag_idx];
       node_q_.push_back(std::move(p));
     }
@@ -2005,7 +2015,7 @@ void Engine::flush_alerts(int64_t edge_ts) {
   }
   for (int32_t j = 0; j < na; ++j) {
     const int32_t i = ord[j];
-    const AlertRec& r = h_alerts_[i];
+    const AlertRec& r = alerts[i];
     const SeriesInfo& si = series_[r.series];
     std::string key = dict_.service_name(si.service);
     if (!cfg_.cooldown_by_service) key = servers_[si.server] + '\x01' + key;
@@ -2015,7 +2025,7 @@ void Engine::flush_alerts(int64_t edge_ts) {
     ++metrics_.alerts;
     if (need_rows) {
       const std::string fs = fmt::fs_line(edge_ts, servers_[si.server], dict_.service_name(si.service),
-                                          cfg_.lags[r.lag_idx], h_alert_win_[i], h_alert_z_[i]);
+                                          cfg_.lags[r.lag_idx], awin[i], az[i]);
       blob_[OUT_AL] += fmt::al_line(now, edge_ts, servers_[si.server], dict_.service_name(si.service), r.causes, fs);
       blob_[OUT_AL] += '\n';
     }
@@ -2516,6 +2526,7 @@ void Engine::pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream,
       svc_csr_n_ = n_series_;
       svc_csr_cap_ = cap;
       tail_csr_for_ = {-1, -1};
+      tail_upto_ = -1;  // rows may have moved (registry adoption): the tail is rebuilt from the snapshot
     }
     const double tg0 = now_ms();
     if (apm_service_gram(d_svc_off_, d_svc_ids_, d_active_, cap, cfg_.max_series, cfg_.n_lags,
@@ -2531,40 +2542,48 @@ void Engine::pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream,
                            (const double* const*)d_lag_comp_ptrs_, (const int32_t* const*)d_lag_cnt_ptrs_, d_dst,
                            stream, d_tail_csr_, 1);
       } else if (n_series_ > svc_csr_n_) {
-        std::vector<std::pair<int32_t, int32_t>> tail;  // (row, series)
-        for (int32_t s = svc_csr_n_; s < n_series_; ++s) {
+        // the tail grows with the series table: fold only the series added since the last pack
+        if (tail_upto_ < svc_csr_n_) { tail_by_svc_.clear(); tail_upto_ = svc_csr_n_; }
+        for (int32_t s = tail_upto_; s < n_series_; ++s) {
           const int32_t v = svc_key(s);
-          if (v >= 0 && v < cap) tail.push_back({v, s});
+          if (v >= 0 && v < cap) tail_by_svc_[v].push_back(s);
         }
-        std::stable_sort(tail.begin(), tail.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
-        const size_t nt = tail.size();
+        tail_upto_ = n_series_;
+        size_t nt = 0;
+        for (const auto& e : tail_by_svc_) nt += e.second.size();
         last_gram_tail_ = (int64_t)nt;
         tail_csr_for_ = {svc_csr_n_, n_series_};
         tail_csr_m_ = 0;
         if (nt) {
-          // one pinned block per call: [map m][off m+1][ids nt]
-          std::vector<int32_t> map, off, ids;
-          for (size_t i = 0; i < nt; ++i) {
-            if (i == 0 || tail[i].first != tail[i - 1].first) { map.push_back(tail[i].first); off.push_back((int32_t)i); }
-            ids.push_back(tail[i].second);
-          }
-          off.push_back((int32_t)nt);
-          const size_t m = map.size(), nb = (m + (m + 1) + nt) * 4;
+          // one pinned block per call: [map m][off m+1][ids nt]; two blocks alternate, so the one
+          // written now was last read by the upload two packs ago
+          const size_t m = tail_by_svc_.size(), nb = (m + (m + 1) + nt) * 4;
           tail_csr_m_ = (int32_t)m;
-          if (nb > tail_csr_cap_) {
-            if (h_tail_csr_) HIP_OK(hipHostFree(h_tail_csr_));
-            HIP_OK(hipStreamSynchronize(stream));
-            tail_csr_cap_ = nb * 2 + 4096;
-            HIP_OK(hipHostMalloc((void**)&h_tail_csr_, tail_csr_cap_, hipHostMallocDefault));
-            d_tail_csr_ = (int32_t*)regrow(d_tail_csr_, d_tail_csr_cap_, tail_csr_cap_);
-          } else {
-            HIP_OK(hipEventSynchronize(tail_csr_ev_));  // the previous tail upload has been read
+          const int k = tail_k_;
+          tail_k_ ^= 1;
+          if (!tail_csr_ev_[k]) HIP_OK(hipEventCreateWithFlags(&tail_csr_ev_[k], hipEventDisableTiming));
+          else HIP_OK(hipEventSynchronize(tail_csr_ev_[k]));
+          if (nb > tail_csr_cap_[k]) {
+            if (h_tail_csr_[k]) HIP_OK(hipHostFree(h_tail_csr_[k]));
+            tail_csr_cap_[k] = nb * 2 + 4096;
+            HIP_OK(hipHostMalloc((void**)&h_tail_csr_[k], tail_csr_cap_[k], hipHostMallocDefault));
           }
-          std::memcpy(h_tail_csr_, map.data(), m * 4);
-          std::memcpy(h_tail_csr_ + m, off.data(), (m + 1) * 4);
-          std::memcpy(h_tail_csr_ + 2 * m + 1, ids.data(), nt * 4);
-          HIP_OK(hipMemcpyAsync(d_tail_csr_, h_tail_csr_, nb, hipMemcpyHostToDevice, stream));
-          HIP_OK(hipEventRecord(tail_csr_ev_, stream));
+          if (nb > d_tail_csr_cap_) d_tail_csr_ = (int32_t*)regrow(d_tail_csr_, d_tail_csr_cap_, nb * 2 + 4096);
+          int32_t* h = h_tail_csr_[k];
+          int32_t* hmap = h;
+          int32_t* hoff = h + m;
+          int32_t* hids = h + 2 * m + 1;
+          size_t r = 0, o = 0;
+          for (const auto& e : tail_by_svc_) {
+            hmap[r] = e.first;
+            hoff[r] = (int32_t)o;
+            std::memcpy(hids + o, e.second.data(), e.second.size() * 4);
+            o += e.second.size();
+            ++r;
+          }
+          hoff[m] = (int32_t)o;
+          HIP_OK(hipMemcpyAsync(d_tail_csr_, h, nb, hipMemcpyHostToDevice, stream));
+          HIP_OK(hipEventRecord(tail_csr_ev_[k], stream));
           apm_service_gram(d_tail_csr_ + m, d_tail_csr_ + 2 * m + 1, d_active_, (int32_t)m, cfg_.max_series,
                            cfg_.n_lags, (const double* const*)d_lag_sum_ptrs_, (const double* const*)d_lag_comp_ptrs_,
                            (const int32_t* const*)d_lag_cnt_ptrs_, d_dst, stream, d_tail_csr_, 1);

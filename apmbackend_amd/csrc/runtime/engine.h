@@ -620,7 +620,7 @@ class Engine {
   std::vector<int32_t> h_raw_series_;          // stats thread mirror of the raw -> series table
   // pinned staging of the stats thread's H2D uploads: kStage buffers used in rotation, each
   // reused only after its previous copy completed (an event), so no upload waits for the stream
-  static constexpr int kStage = 4;
+  static constexpr int kStage = 32;  // > the uploads of a few batches (a batch with new series makes ~10)
   char* h_stage_[kStage] = {};
   size_t h_stage_cap_[kStage] = {};
   hipEvent_t stage_ev_[kStage] = {};
@@ -761,12 +761,16 @@ class Engine {
   int32_t* d_svc_ids_ = nullptr;
   size_t svc_off_cap_ = 0, svc_ids_cap_ = 0;
   int32_t svc_csr_n_ = -1, svc_csr_cap_ = -1;
-  int32_t* h_tail_csr_ = nullptr;  // per-batch CSR of the series added since the snapshot (pinned)
+  int32_t* h_tail_csr_[2] = {nullptr, nullptr};  // per-batch CSR of the series added since the snapshot (pinned, alternating)
+  size_t tail_csr_cap_[2] = {0, 0};
+  hipEvent_t tail_csr_ev_[2] = {nullptr, nullptr};
+  int tail_k_ = 0;
   int32_t* d_tail_csr_ = nullptr;
-  size_t tail_csr_cap_ = 0, d_tail_csr_cap_ = 0;
-  hipEvent_t tail_csr_ev_ = nullptr;
+  size_t d_tail_csr_cap_ = 0;
   std::pair<int32_t, int32_t> tail_csr_for_{-1, -1};  // (CSR snapshot size, n_series) of the uploaded tail
   int32_t tail_csr_m_ = 0;
+  std::map<int32_t, std::vector<int32_t>> tail_by_svc_;  // the tail's series per row, in series order
+  int32_t tail_upto_ = -1;                               // series [svc_csr_n_, tail_upto_) are in it
  public:
   int64_t last_gram_tail_ = 0;  // series the last Gram pack took from the tail CSR (tests)
  private:
