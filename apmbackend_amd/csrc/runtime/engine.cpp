@@ -1879,11 +1879,13 @@ void Engine::finish_rollover() {
   HIP_OK(hipEventSynchronize(ev_alerts_));
   const double t1 = now_ms();
   if (dev()) release_device_finish();
+  const double t2 = now_ms();
   metrics_.t_rollover_ms += t1 - t0;
   trace_event("rollover wait", t0, t1, 1);
+  trace_event("release finish", t1, t2, 1);
   metrics_.rollover_latency_ms.push_back(t1 - roll_batch_t0_);
   flush_alerts(roll_edge_ts_);
-  trace_event("alerts", t1, now_ms(), 1);
+  trace_event("alerts", t2, now_ms(), 1);
   if (want(OUT_SX)) format_server_rollup(roll_edge_ts_);
   metrics_.t_format_ms += now_ms() - t1;
 }
@@ -1922,7 +1924,9 @@ void Engine::release_device_finish() {
     const size_t total = *h_rel_total_;
     const int k = rel_k_;
     rel_k_ ^= 1;
+    const double tw = now_ms();
     out_wait(rel_task_[k]);  // the buffer's previous reader is done
+    trace_event("rel.wait_lane", tw, now_ms(), 1);
     if (total + 64 > rel_text_cap_[k]) d_rel_text_[k] = (char*)regrow(d_rel_text_[k], rel_text_cap_[k], total + 64);
     apm_dj_gather_copy(d_pool_gid_[pool_cur_], released, dj_->ring(), dj_->ring_cap(), d_rel_offs_, d_rel_text_[k], stream_);
     HIP_OK(hipEventRecord(ev_rel_[k], stream_));
