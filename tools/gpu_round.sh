@@ -20,5 +20,7 @@ timeout -k 10 300 python bench.py --steps 20 --warmup 5 --trace $O/mem_trace.jso
 python tools/trace_summary.py $O/mem_trace.json > $O/mem_trace_summary.txt
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 10 --warmup 3 > $O/prof.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES --kernel-trace --output-format csv --kernel-include-regex 'apm::' -d $O/pmc_mfma -o run -- python3 bench.py --steps 3 --warmup 1 > $O/pmc_mfma.log 2>&1 || exit $?
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE WRITE_SIZE SQ_WAVES SQ_BUSY_CYCLES --kernel-trace --output-format csv --kernel-include-regex 'apm::' -d $O/pmc_hbm -o run -- python3 bench.py --steps 3 --warmup 1 > $O/pmc_hbm.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv --kernel-include-regex 'apm::' -d $O/pmc_fetch -o run -- python3 bench.py --steps 3 --warmup 1 > $O/pmc_fetch.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE TCC_HIT TCC_MISS --kernel-trace --output-format csv --kernel-include-regex 'apm::' -d $O/pmc_write -o run -- python3 bench.py --steps 3 --warmup 1 > $O/pmc_write.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS --kernel-trace --output-format csv --kernel-include-regex 'apm::' -d $O/pmc_lds -o run -- python3 bench.py --steps 3 --warmup 1 > $O/pmc_lds.log 2>&1 || exit $?
 echo all done

@@ -60,7 +60,8 @@ def main(root, dst, title="rocprofv3 hardware counters"):
             gbs = f"{by / t / 1e9:.0f}" if t > 0 and by > 0 else "-"
             vpw = f"{c['SQ_INSTS_VALU'] / c['SQ_WAVES']:.0f}" if c.get("SQ_WAVES") else "-"
             lds = f"{c['SQ_LDS_BANK_CONFLICT'] / c['SQ_INSTS_LDS']:.2f}" if c.get("SQ_INSTS_LDS") else "-"
-            h, m = c.get("TCC_HIT_sum", 0.0), c.get("TCC_MISS_sum", 0.0)
+            h = c.get("TCC_HIT_sum", c.get("TCC_HIT", 0.0))
+            m = c.get("TCC_MISS_sum", c.get("TCC_MISS", 0.0))
             hit = f"{100.0 * h / (h + m):.0f}" if h + m > 0 else "-"
             f.write(f"| {k} | {t * 1e3:.3f} | {gbs} | {vpw} | {lds} | {hit} |\n")
         f.write("\n## Raw counters\n\n| kernel | " + " | ".join(cols) + " |\n|---|" + "---|" * len(cols) + "\n")
