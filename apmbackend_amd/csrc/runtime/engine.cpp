@@ -1677,8 +1677,12 @@ char* Engine::stage(size_t bytes) {
   if (stage_ev_[k]) HIP_OK(hipEventSynchronize(stage_ev_[k]));
   else HIP_OK(hipEventCreateWithFlags(&stage_ev_[k], hipEventDisableTiming));
   if (bytes > h_stage_cap_[k]) {
+    // slots rotate over uploads of very different sizes (80k-series permutation vs a JMX row):
+    // grow each to the largest request seen so far, so the ring stops reallocating (a pinned
+    // free + alloc costs ~1 ms) after one pass instead of after every slot met every size
+    stage_max_ = std::max(stage_max_, bytes);
     if (h_stage_[k]) HIP_OK(hipHostFree(h_stage_[k]));
-    h_stage_cap_[k] = bytes * 2 + (1 << 16);
+    h_stage_cap_[k] = std::max<size_t>(stage_max_ * 2, 1 << 20);
     HIP_OK(hipHostMalloc((void**)&h_stage_[k], h_stage_cap_[k], hipHostMallocDefault));
   }
   return h_stage_[k];
@@ -2284,12 +2288,12 @@ void Engine::server_rollup(int64_t edge_ts) {
     roll_cap_ = cap;
     ctx_dirty_ = true;
   }
-  if (series_server_uploaded_ < n_series_) {
+  if (series_server_uploaded_ < n_series_) {  // new series: pinned stager, no stream sync
     const int32_t lo = series_server_uploaded_;
-    std::vector<int32_t> sv(n_series_ - lo);
+    int32_t* sv = reinterpret_cast<int32_t*>(stage((size_t)(n_series_ - lo) * 4));
     for (int32_t s = lo; s < n_series_; ++s) sv[s - lo] = series_[s].server;
-    HIP_OK(hipMemcpyAsync(d_series_server_ + lo, sv.data(), sv.size() * 4, hipMemcpyHostToDevice, stream_));
-    HIP_OK(hipStreamSynchronize(stream_));
+    HIP_OK(hipMemcpyAsync(d_series_server_ + lo, sv, (size_t)(n_series_ - lo) * 4, hipMemcpyHostToDevice, stream_));
+    stage_done();
     series_server_uploaded_ = n_series_;
   }
   if (ctx_dirty_) {  // (a JMX sample per server per batch: pinned staging, no stream sync)

