@@ -421,6 +421,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
 
 Engine::~Engine() {
   ahead_lane_.reset();  // drains a pending next-batch pre-pass before the join state goes
+  fb_lane_.reset();     // and a pending fb emission before its buffers
   checkpoint_shutdown();
   {
     std::lock_guard<std::mutex> g(st_mu_);
@@ -1251,6 +1252,7 @@ void Engine::flush() {
   st_cv_.wait(lk, [&]() { return !st_busy_; });
   // the stats thread is idle, so no new output-lane task can appear
   out_wait_idle();
+  if (fb_lane_) fb_lane_->wait_all();
   {
     std::lock_guard<std::mutex> g(out_mu_);
     metrics_.t_out_ms += t_out_ms_;
@@ -1359,6 +1361,15 @@ uint64_t TaskLane::post(std::function<void()> fn) {
   q_.push_back(std::move(fn));
   cv_.notify_all();
   return ++posted_;
+}
+
+void TaskLane::wait_all() {
+  uint64_t id;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    id = posted_;
+  }
+  wait(id);
 }
 
 void TaskLane::wait(uint64_t id) {

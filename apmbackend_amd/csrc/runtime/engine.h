@@ -200,6 +200,7 @@ class TaskLane {
   ~TaskLane();
   uint64_t post(std::function<void()> fn);
   void wait(uint64_t id);
+  void wait_all();
 
  private:
   std::thread th_;
@@ -316,8 +317,7 @@ class Engine {
   // refused (maxServices full), fb rows emitted}
   std::vector<std::string> fleet_slot_names() { flush(); return reg_names_; }
   std::vector<uint64_t> fleet_info() {
-    flush();
-    out_wait_idle();
+    flush();  // (waits for both emission lanes)
     return {(uint64_t)reg_names_.size(), reg_rounds_, reg_overflow_, fb_rows_};
   }
   uint64_t fleet_rounds() const { return fleet_rounds_; }
@@ -566,6 +566,7 @@ class Engine {
   std::unique_ptr<ThreadPool> pool_;
   // device join: the next batch's parse finish + host pre-pass, overlapping this batch's join
   std::unique_ptr<TaskLane> ahead_lane_;
+  std::unique_ptr<TaskLane> fb_lane_;  // rank 0's fb rows: D2H + emission beside the output lane
   uint64_t ahead_task_ = 0;
   std::vector<int> lane_cpus_;  // pinned placement (empty: unpinned)
   std::vector<double> shard_ms_;  // per-shard join time of the current batch (stride 16)

@@ -24,6 +24,8 @@
 
 #include <cstring>
 
+#include <algorithm>
+
 #include "engine.h"
 
 namespace apm {
@@ -145,7 +147,8 @@ void Engine::fleet_emit_fb(int slot) {
   if (n_slots == 0) return;
   const int k = fb_k_;
   fb_k_ ^= 1;
-  out_wait(fb_task_[k]);  // slot k's previous D2H + emission is done
+  if (!fb_lane_) fb_lane_.reset(new TaskLane());  // fb rows get their own emission lane
+  fb_lane_->wait(fb_task_[k]);  // slot k's previous D2H + emission is done
   // slot names -> device (coll stream: ordered before the format kernels)
   if (fb_chars_up_ < h_fb_chars_.size()) {
     if (h_fb_chars_.size() > fb_chars_cap_) {
@@ -204,7 +207,7 @@ void Engine::fleet_emit_fb(int slot) {
   HIP_OK(hipMemcpyAsync(h_fb_total_ + k, d_fb_off_ + rows, 4, hipMemcpyDeviceToHost, coll_stream_));
   HIP_OK(hipEventRecord(fb_ev_[k], coll_stream_));
   char* dst = d_fb_out_[k];
-  fb_task_[k] = post_out([this, k, dst]() {
+  fb_task_[k] = fb_lane_->post([this, k, dst]() {
     HIP_OK(hipEventSynchronize(fb_ev_[k]));
     const size_t total = h_fb_total_[k];
     if (total > h_fb_cap_[k]) {
@@ -214,9 +217,7 @@ void Engine::fleet_emit_fb(int slot) {
     }
     if (total) {
       HIP_OK(hipMemcpy(h_fb_out_[k], dst, total, hipMemcpyDeviceToHost));
-      size_t rows = 0;
-      for (size_t i = 0; i < total; ++i) rows += h_fb_out_[k][i] == '\n';
-      fb_rows_ += rows;
+      fb_rows_ += (uint64_t)std::count(h_fb_out_[k], h_fb_out_[k] + total, '\n');
       emit_bytes(OUT_FB, h_fb_out_[k], total);
     }
   });
