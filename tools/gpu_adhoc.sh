@@ -1,8 +1,6 @@
 set -u
-mkdir -p gpurun_out/ev
-for i in 1 2 3; do
-timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/ev/headline_$i.log 2>&1 || exit $?; tail -1 gpurun_out/ev/headline_$i.log | cut -c60-150
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_engine_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t.log 2>&1; rc=$?; tail -1 gpurun_out/t.log; [ $rc -eq 0 ] || exit $rc
+for a in 1 0 1 0 1 0; do
+APM_PULL_H2D=$a timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_ab.log 2>&1; rc=$?; echo "pull=$a $(tail -1 gpurun_out/bench_ab.log | cut -c60-150)"; [ $rc -eq 0 ] || exit $rc
 done
-timeout -k 10 300 python bench.py --preset config2 --steps 20 --warmup 5 > gpurun_out/ev/config2.log 2>&1 || exit $?; tail -1 gpurun_out/ev/config2.log | cut -c60-150
-timeout -k 10 420 python bench.py --preset firehose --steps 10 --warmup 3 --trace gpurun_out/ev/fh_trace.json > gpurun_out/ev/firehose.log 2>&1 || exit $?; tail -1 gpurun_out/ev/firehose.log | cut -c60-150
-python tools/trace_summary.py gpurun_out/ev/fh_trace.json 5 | grep -v " u\." 
