@@ -395,7 +395,9 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   const char* pin_env = std::getenv("APM_PIN_THREADS");
   if (pin_env ? std::atoi(pin_env) != 0 : cfg_.pin_threads) lane_cpus_ = local_core_slice(cfg_.device);
   int nt = cfg_.join_threads;
-  if (nt <= 0) nt = (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+  // host join: one worker per JVM shard (up to 16); device join: the pool only runs the audit
+  // pre-pass (one task per app log), so 8 threads -- 8 ranks per node stay at ~100 threads
+  if (nt <= 0) nt = (int)std::min<unsigned>(cfg_.device_join ? 8 : 16, std::max(1u, std::thread::hardware_concurrency()));
   {
     // join workers take the first cores of the slice; the stats thread and output lane the next two
     std::vector<int> wc(lane_cpus_.begin(), lane_cpus_.begin() + (ptrdiff_t)std::min<size_t>(lane_cpus_.size(), (size_t)std::max(nt, 0)));
