@@ -50,8 +50,10 @@ class FleetBaseline:
 
     Rank 0 draws an RCCL unique id, the id travels over the existing torch.distributed group
     (one small object broadcast at start-up), and every rank's engine creates its own RCCL
-    communicator.  From then on the engine's stats thread issues one ``ncclAllReduce`` per
-    processed batch on its comm stream -- no Python, no host synchronisation on the hot path.
+    communicator.  From then on the engine's ingest thread issues, per batch and in a fixed order,
+    the lock-step clock all-reduce, the node-wide registry all-gather (rounds with new services)
+    and the fleet-moment all-reduce of the previous batch (packed by the stats thread) -- no
+    Python on the hot path (csrc/runtime/engine.cpp, fleet.cpp).
     """
 
     def __init__(self, engine, world: int, rank: int, max_services: Optional[int] = None, group=None,
