@@ -100,6 +100,7 @@ def main():
     ap.add_argument("--service-dir", default=None, help="--path service: where the log files / spool go")
     ap.add_argument("--service-sink", default="spool", choices=["spool", "null"])
     ap.add_argument("--encoder-threads", type=int, default=8)
+    ap.add_argument("--join-threads", type=int, default=0, help="engine worker pool (0 = auto)")
     args = ap.parse_args()
     for k, v in PRESETS[args.preset].items():  # a preset overrides the defaults it names
         if getattr(args, k) == ap.get_default(k):
@@ -132,6 +133,7 @@ def main():
         "ringDtype": args.ring,
         "bucketCellCapacity": 16,
         "serverRollup": bool(args.jmx),
+        "joinThreads": args.join_threads,
     })
     if args.path == "service":
         from apmbackend_amd.runtime import service_bench
