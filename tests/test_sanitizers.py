@@ -108,3 +108,41 @@ def test_js_trim_fast_path_matches_code_point_walk(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     r = subprocess.run([exe, "300000"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr[-2000:]
+
+
+def _build_dbsink(tmp, san, link):
+    import sysconfig
+    import pybind11
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    exe = os.path.join(tmp, "dbsink_stress")
+    cmd = [hipcc, "-O1", "-g", "-std=c++17", "--offload-arch=gfx950", *san, "-I", CSRC, "-I", pybind11.get_include(),
+           "-I", sysconfig.get_paths()["include"], os.path.join(ROOT, "tests", "native", "dbsink_stress.cpp"),
+           os.path.join(CSRC, "runtime", "copyenc.cpp"), "-o", exe, *link, "-pthread",
+           "-Wl,--unresolved-symbols=ignore-all"]  # the (unused) Python bindings and Engine hooks
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return exe
+
+
+@pytest.mark.parametrize("tool", ["asan", "tsan"])
+def test_db_sink_under_sanitizers(tmp_path, tool):
+    """The native DB sink's threads (parallel row cutter, encoder pool, ordered spool writer, a
+    ticking / flushing caller) under AddressSanitizer + UBSan and under ThreadSanitizer: every
+    pre-encoded row reaches its spool file once and in order."""
+    if tool == "tsan":
+        san = ["-Xarch_host", "-fsanitize=thread", "-Xarch_host", "-fno-omit-frame-pointer"]
+        link = ["-fsanitize=thread"]
+        env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1")
+    else:
+        san = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+               "-Xarch_host", "-fno-omit-frame-pointer", "-Xarch_host", "-fno-sanitize-recover=all"]
+        link = ["-fsanitize=address,undefined"]
+        env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1", UBSAN_OPTIONS="print_stacktrace=1")
+    exe = _build_dbsink(str(tmp_path), san, link)
+    spool = tmp_path / "spool"
+    r = subprocess.run([exe, str(spool)], capture_output=True, text=True, env=env, timeout=600)
+    if tool == "tsan" and "FATAL: ThreadSanitizer" in r.stderr and "memory" in r.stderr:
+        pytest.skip("ThreadSanitizer cannot map its shadow memory on this kernel: " + r.stderr[-300:])
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "WARNING: ThreadSanitizer" not in r.stderr and "runtime error" not in r.stderr
+    assert r.stdout.startswith("ok")
