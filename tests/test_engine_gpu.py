@@ -277,12 +277,13 @@ def test_lockstep_clock_communicator_single_rank_is_transparent():
     assert len(eng.eng.fleet_merged()) > 0 and eng.eng.fleet_rounds() >= len(bl)
 
 
-def test_server_rollup_fuses_window_stats_with_jmx_gauges():
+@pytest.mark.parametrize("servers", [2, 70])
+def test_server_rollup_fuses_window_stats_with_jmx_gauges(servers):
     """K14: per-JVM rollup (sx) == aggregate of that interval's st rows, joined with the JVM's
-    JMX gauges."""
+    JMX gauges.  70 JVMs exceed the block-local (LDS) accumulators: global-atomic path."""
     from apmbackend_amd.runtime.jmx import SyntheticJmx
     from apmbackend_amd.utils.records import JmxEntry
-    lines, bl = synth_batches(10, duration=500)
+    lines, bl = synth_batches(10, duration=500 if servers <= 2 else 200, servers=servers)
     C = small_cfg("exact")
     eng = APMEngine(C, keep_text=True)
     syn = SyntheticJmx(5)
