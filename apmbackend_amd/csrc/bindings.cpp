@@ -408,6 +408,7 @@ PYBIND11_MODULE(_apm_native, m) {
       })
       .def("fleet_rounds", &Engine::fleet_rounds)
       .def("gram_tail_series", [](Engine& e) { return e.last_gram_tail_; })
+      .def("node_metrics", &Engine::node_metrics)
       .def("fleet_slot_names", [](Engine& e) { return e.fleet_slot_names(); })
       .def("fleet_info", [](Engine& e) {
         py::dict d;

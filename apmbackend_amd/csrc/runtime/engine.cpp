@@ -424,6 +424,9 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
 Engine::~Engine() {
   ahead_lane_.reset();  // drains a pending next-batch pre-pass before the join state goes
   fb_lane_.reset();     // and a pending fb emission before its buffers
+  if (nm_ev_) { hipEventSynchronize(nm_ev_); hipEventDestroy(nm_ev_); }
+  if (h_nm_send_) hipHostFree(h_nm_send_);
+  if (h_nm_recv_) hipHostFree(h_nm_recv_);
   checkpoint_shutdown();
   {
     std::lock_guard<std::mutex> g(st_mu_);
@@ -2797,10 +2800,49 @@ void Engine::fleet_exchange_upto(uint64_t rounds) {
                                    : fleet_elems_;
     if (!fleet_skip_solo_ && n_red) coll_->all_reduce_f64(fleet_buf_[slot], n_red, /*max=*/false, coll_stream_);
     if (pack_edge_[slot] && want(OUT_FB) && coll_->rank() == 0) fleet_emit_fb(slot);
+    if (pack_edge_[slot]) node_metrics_round();  // (edges are identical on every lock-step rank)
     HIP_OK(hipEventRecord(fleet_ev_[slot], coll_stream_));
     if (node_mode_) node_round(fleet_rounds_, /*wait=*/false);
     ++fleet_rounds_;
   }
+}
+
+void Engine::node_metrics_round() {
+  // nm_mu_ is held across harvest and re-launch so node_metrics() never reads h_nm_recv_ while
+  // the next copy into it is queued
+  std::lock_guard<std::mutex> g(nm_mu_);
+  if (!d_nm_) {
+    d_nm_ = (double*)dmalloc(kNodeMetrics * 8);
+    HIP_OK(hipHostMalloc((void**)&h_nm_send_, kNodeMetrics * 8, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void**)&h_nm_recv_, kNodeMetrics * 8, hipHostMallocDefault));
+    HIP_OK(hipEventCreateWithFlags(&nm_ev_, hipEventDisableTiming));
+  } else if (nm_pending_) {
+    coll_wait(nullptr, nm_ev_, "node metrics");  // the previous interval's: long done
+    node_metrics_.assign(h_nm_recv_, h_nm_recv_ + kNodeMetrics);
+    nm_pending_ = false;
+  }
+  // counters written by other lanes are read as they stand: the element count, not the values,
+  // must agree across ranks
+  auto ld = [](const uint64_t& x) { return (double)__atomic_load_n(&x, __ATOMIC_RELAXED); };
+  const EngineMetrics& m = metrics_;
+  const double v[kNodeMetrics] = {1.0, ld(m.batches), ld(m.lines), ld(m.events), ld(m.bytes), ld(m.tx),
+                                  ld(m.tx_db), ld(m.released), ld(m.rollovers), ld(m.alert_candidates),
+                                  ld(m.alerts), (double)__atomic_load_n(&n_series_, __ATOMIC_RELAXED)};
+  std::memcpy(h_nm_send_, v, sizeof v);
+  HIP_OK(hipMemcpyAsync(d_nm_, h_nm_send_, sizeof v, hipMemcpyHostToDevice, coll_stream_));
+  coll_->all_reduce_f64(d_nm_, kNodeMetrics, /*max=*/false, coll_stream_);
+  HIP_OK(hipMemcpyAsync(h_nm_recv_, d_nm_, sizeof v, hipMemcpyDeviceToHost, coll_stream_));
+  HIP_OK(hipEventRecord(nm_ev_, coll_stream_));
+  nm_pending_ = true;
+}
+
+std::vector<double> Engine::node_metrics() {
+  std::lock_guard<std::mutex> g(nm_mu_);
+  if (nm_pending_ && hipEventQuery(nm_ev_) == hipSuccess) {
+    node_metrics_.assign(h_nm_recv_, h_nm_recv_ + kNodeMetrics);
+    nm_pending_ = false;
+  }
+  return node_metrics_;
 }
 
 std::vector<double> Engine::fleet_merged() {

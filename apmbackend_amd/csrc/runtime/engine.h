@@ -321,6 +321,9 @@ class Engine {
     return {(uint64_t)reg_names_.size(), reg_rounds_, reg_overflow_, fb_rows_};
   }
   uint64_t fleet_rounds() const { return fleet_rounds_; }
+  // node-wide sums of {ranks, batches, lines, events, bytes, tx, tx_db, released, rollovers,
+  // alert candidates, alerts, series} as of the last interval edge's exchange (empty: none yet)
+  std::vector<double> node_metrics();
   // Same exchange over an in-process group (tests: N engines of one process share one GPU).
   void fleet_init_local(std::shared_ptr<LocalGroup> group, int rank, int32_t n_services_cap, bool lockstep);
   // Position of `server` in the node-wide server list (ranks own disjoint slices of it).  The
@@ -567,6 +570,17 @@ class Engine {
   // device join: the next batch's parse finish + host pre-pass, overlapping this batch's join
   std::unique_ptr<TaskLane> ahead_lane_;
   std::unique_ptr<TaskLane> fb_lane_;  // rank 0's fb rows: D2H + emission beside the output lane
+  // node-wide counters: all-reduce(SUM) of this rank's counters at every interval edge, async on
+  // the collective stream (SURVEY 2.4 "ncclAllReduce of counters/metrics")
+  static constexpr int kNodeMetrics = 12;
+  double* d_nm_ = nullptr;
+  double* h_nm_send_ = nullptr;
+  double* h_nm_recv_ = nullptr;
+  hipEvent_t nm_ev_ = nullptr;
+  bool nm_pending_ = false;
+  std::mutex nm_mu_;
+  std::vector<double> node_metrics_;  // last completed reduction
+  void node_metrics_round();
   uint64_t ahead_task_ = 0;
   std::vector<int> lane_cpus_;  // pinned placement (empty: unpinned)
   std::vector<double> shard_ms_;  // per-shard join time of the current batch (stride 16)

@@ -231,6 +231,15 @@ class APMEngine:
         vals = [float("nan") if v is None else float(v) for v in e.values]
         return self.eng.set_server_context(e.server, float(e.timestamp), vals, float(vm_load))
 
+    NODE_METRICS = ("ranks", "batches", "lines", "events", "bytes", "tx", "tx_db", "released", "rollovers",
+                    "alert_candidates", "alerts", "series")
+
+    def node_metrics(self) -> Dict[str, float]:
+        """Node-wide sums of the per-rank counters as of the last interval edge (one RCCL
+        all-reduce per interval on the collective stream); empty before the first edge or when
+        no fleet exchange is configured."""
+        return dict(zip(self.NODE_METRICS, self.eng.node_metrics()))
+
     def metrics(self) -> Dict[str, Any]:
         m = self.eng.metrics()
         m.update({"join": self.eng.join_counters(), "series": self.eng.n_series(),

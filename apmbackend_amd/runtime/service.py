@@ -521,6 +521,12 @@ class IngestService:
                  "- HBM %.2f GB - fleet rounds %s",
                  *(stages[k] / nb for k in _STAGE_KEYS), *pct, hbm / 1e9,
                  self.native.fleet_rounds() if hasattr(self.native, "fleet_rounds") else "-")
+        nm = list(self.native.node_metrics()) if hasattr(self.native, "node_metrics") else []
+        if nm and nm[0] > 1 and getattr(self, "rank", 0) == 0:
+            prev_nm = getattr(self, "_nm_prev", None) or [0.0] * len(nm)
+            self._nm_prev = nm
+            log.info("NODE ranks: %d - lines: %d (+%d) - tx: %d - alerts: %d - series: %d", nm[0], nm[2],
+                     nm[2] - prev_nm[2], nm[5], nm[10], nm[11])
         if self.inserter is not None:
             self.inserter.stats.log_and_reset()
         if self.qm is not None:

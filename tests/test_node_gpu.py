@@ -130,6 +130,14 @@ def test_local_group_node_matches_single_process(world):
     if world > 1:
         # candidates were raised on more ranks than alerted: the cooldown was decided node-wide
         assert sum(m["alert_candidates"] for m in ms) > len(P.al)
+    # node-wide counters (all-reduce SUM at each interval edge): same vector on every rank,
+    # field 0 counts the ranks, the line count is the node's as of the last edge
+    nms = [e.eng.node_metrics() for e in engs]
+    assert nms[0] and all(nm == nms[0] for nm in nms)
+    nm = nms[0]
+    assert nm[0] == world
+    assert 0 < nm[2] <= sum(m["lines"] for m in ms)
+    assert nm[1] >= world  # every rank counted its batches
 
 
 def _fleet_by_name(eng):
