@@ -107,9 +107,10 @@ struct NullWriter : Writer {
 struct SpoolWriter : Writer {
   std::string dir;
   uint64_t rotate;
+  std::string suffix;  // "" for lane 0, ".lane<k>" for writer lane k
   int fd[NT] = {-1, -1, -1, -1, -1};
   uint64_t size[NT] = {0, 0, 0, 0, 0};
-  SpoolWriter(std::string d, uint64_t r) : dir(std::move(d)), rotate(r) {
+  SpoolWriter(std::string d, uint64_t r, std::string sfx = "") : dir(std::move(d)), rotate(r), suffix(std::move(sfx)) {
     ::mkdir(dir.c_str(), 0755);
   }
   ~SpoolWriter() override {
@@ -117,21 +118,25 @@ struct SpoolWriter : Writer {
       if (f >= 0) ::close(f);
   }
   std::string write(int type, const std::string& table, const std::string& columns, const std::string& rows) override {
-    const std::string path = dir + "/" + table + ".copy";
+    const std::string path = dir + "/" + table + suffix + ".copy";
     if (fd[type] >= 0 && rotate && size[type] >= rotate) {
       ::close(fd[type]);
       fd[type] = -1;
       const auto ms = (long long)std::chrono::duration_cast<std::chrono::milliseconds>(
                           std::chrono::system_clock::now().time_since_epoch()).count();
-      ::rename(path.c_str(), (dir + "/" + table + "." + std::to_string(ms) + ".copy").c_str());
+      ::rename(path.c_str(), (dir + "/" + table + suffix + "." + std::to_string(ms) + ".copy").c_str());
     }
     if (fd[type] < 0) {
+      // <table>.columns, shared by the lanes' files: written under a per-lane name and renamed
+      // into place (every lane writes the same text, so concurrent renames are harmless)
       const std::string cpath = dir + "/" + table + ".columns";
-      const int cf = ::open(cpath.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+      const std::string tpath = cpath + suffix + ".tmp";
+      const int cf = ::open(tpath.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
       if (cf >= 0) {
         const std::string c = columns + "\n";
-        write_all(cf, c.data(), c.size());
+        const bool ok = write_all(cf, c.data(), c.size());
         ::close(cf);
+        if (!ok || ::rename(tpath.c_str(), cpath.c_str()) != 0) ::unlink(tpath.c_str());
       }
       // not O_APPEND: pwrite on an O_APPEND fd ignores its offset on Linux (write_run)
       fd[type] = ::open(path.c_str(), O_WRONLY | O_CREAT | O_CLOEXEC, 0644);
@@ -276,16 +281,22 @@ struct PsqlWriter : Writer {
 class DbSink : public ByteSink {
  public:
   DbSink(int64_t limit, double max_wait_ms, std::vector<std::string> tables, std::vector<std::string> columns,
-         const std::string& writer, const std::vector<std::string>& arg, uint64_t rotate_bytes, int encoders)
+         const std::string& writer, const std::vector<std::string>& arg, uint64_t rotate_bytes, int encoders,
+         int lanes = 1)
       : limit_(std::max<int64_t>(1, limit)), max_wait_ms_(max_wait_ms), tables_(std::move(tables)),
-        columns_(std::move(columns)) {
+        columns_(std::move(columns)), lanes_(std::max(1, std::min(lanes, 64))), order_((size_t)lanes_) {
     if (tables_.size() != NT || columns_.size() != NT) throw std::runtime_error("DbSink: 5 tables / column lists");
-    if (writer == "null") w_.reset(new NullWriter());
-    else if (writer == "spool") w_.reset(new SpoolWriter(arg.at(0), rotate_bytes));
-    else if (writer == "psql") w_.reset(new PsqlWriter(arg, 120000.0));
-    else throw std::runtime_error("DbSink: unknown writer " + writer);
+    // Writer lanes: `lanes` independent writers (own spool files / own psql connection), each
+    // writing its share of the flushes in submission order -- the reference's pg Pool likewise
+    // keeps several INSERTs in flight (stream_insert_db.js:277-327).
+    for (int l = 0; l < lanes_; ++l) {
+      if (writer == "null") w_.emplace_back(new NullWriter());
+      else if (writer == "spool") w_.emplace_back(new SpoolWriter(arg.at(0), rotate_bytes, l ? ".lane" + std::to_string(l) : ""));
+      else if (writer == "psql") w_.emplace_back(new PsqlWriter(arg, 120000.0));
+      else throw std::runtime_error("DbSink: unknown writer " + writer);
+    }
     for (int i = 0; i < std::max(1, encoders); ++i) enc_.emplace_back([this] { encode_loop(); });
-    wr_ = std::thread([this] { write_loop(); });
+    for (int l = 0; l < lanes_; ++l) wr_.emplace_back([this, l] { write_loop(l); });
   }
   ~DbSink() override { shutdown(); }
 
@@ -453,7 +464,7 @@ class DbSink : public ByteSink {
       for (auto& j : mid) {
         j->seq = next_seq_++;
         j->ready = true;
-        order_.push_back(j);
+        enqueue_locked(j);
       }
       cv_.notify_all();
     }
@@ -470,7 +481,7 @@ class DbSink : public ByteSink {
     j->ready = true;
     std::lock_guard<std::mutex> lk(mu_);
     j->seq = next_seq_++;
-    order_.push_back(j);
+    enqueue_locked(j);
     cv_.notify_all();
   }
 
@@ -492,7 +503,7 @@ class DbSink : public ByteSink {
   // Waits until every submitted flush was written (or failed and re-buffered).
   void drain() {
     std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [&] { return order_.empty(); });
+    done_cv_.wait(lk, [&] { return queued_locked() == 0; });
   }
 
   // Final flush; returns what could not be written, per type, as wire lines (the caller keeps
@@ -513,7 +524,8 @@ class DbSink : public ByteSink {
     d["ms"] = ms_;
     d["flushes"] = flushes_;
     d["failures"] = failures_;
-    d["queued"] = (int64_t)order_.size();
+    d["queued"] = queued_locked();
+    d["lanes"] = lanes_;
     d["not_db_lines"] = not_db_;
     d["bytes"] = bytes_;
     int64_t buffered = 0;
@@ -581,8 +593,20 @@ class DbSink : public ByteSink {
     }
     buf_[t].lines = take_spare_locked();
     buf_[t].n = 0;
-    order_.push_back(j);
+    enqueue_locked(j);
     cv_.notify_all();
+  }
+
+  // A flush goes to the next writer lane; lanes take their jobs in order.  Round robin over
+  // blocks of kLaneBlock flushes, so a lane still sees runs of one type to write with one writev.
+  static constexpr uint64_t kLaneBlock = 16;
+  void enqueue_locked(const std::shared_ptr<Job>& j) {
+    order_[(size_t)((rr_++ / kLaneBlock) % (uint64_t)lanes_)].push_back(j);
+  }
+  int64_t queued_locked() const {
+    int64_t q = 0;
+    for (auto& o : order_) q += (int64_t)o.size();
+    return q;
   }
 
   void encode_loop() {
@@ -607,27 +631,29 @@ class DbSink : public ByteSink {
     }
   }
 
-  void write_loop() {
+  void write_loop(int lane) {
+    std::deque<std::shared_ptr<Job>>& order = order_[(size_t)lane];
+    Writer& w = *w_[(size_t)lane];
     for (;;) {
       std::vector<std::shared_ptr<Job>> run;  // consecutive ready flushes of one type
       {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return (!order_.empty() && order_.front()->ready) || (stop_ && order_.empty()); });
-        if (order_.empty()) return;
-        const int t = order_.front()->type;
-        for (size_t i = 0; i < order_.size() && i < 256 && order_[i]->ready && order_[i]->type == t; ++i)
-          run.push_back(order_[i]);
+        cv_.wait(lk, [&] { return (!order.empty() && order.front()->ready) || (stop_ && order.empty()); });
+        if (order.empty()) return;
+        const int t = order.front()->type;
+        for (size_t i = 0; i < order.size() && i < 256 && order[i]->ready && order[i]->type == t; ++i)
+          run.push_back(order[i]);
       }
       const int t = run[0]->type;
       std::vector<const std::string*> rows;
       for (auto& j : run) rows.push_back(&j->encoded);
       std::string err;
       const double t0 = mono_ms();
-      const size_t ok = w_->write_run(t, tables_[t], columns_[t], rows, err);
+      const size_t ok = w.write_run(t, tables_[t], columns_[t], rows, err);
       const double dt = mono_ms() - t0;
       {
         std::lock_guard<std::mutex> lk(mu_);
-        for (size_t i = 0; i < run.size(); ++i) order_.pop_front();
+        for (size_t i = 0; i < run.size(); ++i) order.pop_front();
         for (size_t i = 0; i < ok; ++i) {
           Job& j = *run[i];
           rows_ += j.n;
@@ -636,7 +662,7 @@ class DbSink : public ByteSink {
           give_spare_locked(std::move(j.encoded));
           give_spare_locked(std::move(j.lines));
         }
-        ms_ += dt;
+        ms_ = std::max(ms_, lane_ms_[lane] += dt);  // wall time of the busiest lane
         if (ok < run.size()) {
           failures_ += (int64_t)(run.size() - ok);
           last_error_ = err;
@@ -667,24 +693,29 @@ class DbSink : public ByteSink {
     }
     cv_.notify_all();
     for (auto& t : enc_) t.join();
-    if (wr_.joinable()) wr_.join();
-    w_.reset();
+    for (auto& t : wr_)
+      if (t.joinable()) t.join();
+    w_.clear();
   }
 
   int64_t limit_;
   double max_wait_ms_;
   std::vector<std::string> tables_, columns_;
-  std::unique_ptr<Writer> w_;
+  int lanes_;
+  std::vector<std::unique_ptr<Writer>> w_;  // one per lane
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
   Buf buf_[NT];
   bool encoded_[NT] = {false, false, false, false, false};  // type buffered as COPY rows (engine-encoded)
-  std::deque<std::shared_ptr<Job>> order_, to_encode_;
+  std::vector<std::deque<std::shared_ptr<Job>>> order_;  // per writer lane, submission order
+  std::deque<std::shared_ptr<Job>> to_encode_;
+  uint64_t rr_ = 0;
+  double lane_ms_[64] = {};
   std::vector<std::string> spare_;
   uint64_t next_seq_ = 0;
   bool stop_ = false;
   std::vector<std::thread> enc_;
-  std::thread wr_;
+  std::vector<std::thread> wr_;
   int64_t rows_ = 0, flushes_ = 0, failures_ = 0, not_db_ = 0, bytes_ = 0, rows_mark_ = 0;
   double ms_ = 0, ms_mark_ = 0;
   std::string last_error_;
@@ -708,9 +739,9 @@ void register_dbsink(py::module_& m) {
   using apm::Engine;
   py::class_<DbSink, std::shared_ptr<DbSink>>(m, "DbSink")
       .def(py::init<int64_t, double, std::vector<std::string>, std::vector<std::string>, std::string,
-                    std::vector<std::string>, uint64_t, int>(),
+                    std::vector<std::string>, uint64_t, int, int>(),
            py::arg("limit"), py::arg("max_wait_ms"), py::arg("tables"), py::arg("columns"), py::arg("writer"),
-           py::arg("arg"), py::arg("rotate_bytes") = 1ull << 30, py::arg("encoders") = 2)
+           py::arg("arg"), py::arg("rotate_bytes") = 1ull << 30, py::arg("encoders") = 2, py::arg("lanes") = 1)
       .def("consume", [](DbSink& s, py::bytes b) {
         std::string_view v = b;
         py::gil_scoped_release rel;

@@ -60,7 +60,8 @@ def _run(args, cfg, N, rank, root, IngestService):
               "checkpointDir": None, "fleetBaseline": False})
     ic = cfg["streamInsertDb"]
     ic.update({"sink": args.service_sink, "copySinkDir": os.path.join(root, "spool"),
-               "encoderThreads": args.encoder_threads, "copySinkRotateBytes": 1 << 62})
+               "encoderThreads": args.encoder_threads, "copySinkRotateBytes": 1 << 62,
+               "writerLanes": getattr(args, "writer_lanes", 1)})
     cfg["logDir"] = os.path.join(root, "log")
     cfg["streamParseTransactions"]["tailOffsetFileFullPath"] = os.path.join(root, "state", "tail_offsets.json")
     cfg["streamInsertDb"]["bufferResumeFileFullPath"] = os.path.join(root, "state", "db_resume.json")
@@ -115,6 +116,7 @@ def _run(args, cfg, N, rank, root, IngestService):
         "db_rows": rows,
         "db_bytes": s1.get("bytes", 0) - s0.get("bytes", 0),
         "sink": args.service_sink,
+        "writer_lanes": s1.get("lanes", 1),
         "sink_write_ms": s1.get("ms", 0.0) - s0.get("ms", 0.0),
         "sink_failures": s1.get("failures", 0),
         "tailer": {k: tstats[k] for k in ("batches", "bytes_read", "read_threads")},

@@ -100,6 +100,7 @@ def main():
     ap.add_argument("--service-dir", default=None, help="--path service: where the log files / spool go")
     ap.add_argument("--service-sink", default="spool", choices=["spool", "null"])
     ap.add_argument("--encoder-threads", type=int, default=8)
+    ap.add_argument("--writer-lanes", type=int, default=4, help="DB sink writer lanes (spool files / psql connections)")
     ap.add_argument("--join-threads", type=int, default=0, help="engine worker pool (0 = auto)")
     args = ap.parse_args()
     for k, v in PRESETS[args.preset].items():  # a preset overrides the defaults it names
@@ -170,6 +171,7 @@ def main():
         from apmbackend_amd.runtime.sinks import DBInserter
         spool_dir = tempfile.mkdtemp(prefix="apm_bench_spool_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
         cfg["streamInsertDb"].update({"sink": args.db_sink, "copySinkDir": spool_dir, "encoderThreads": 8,
+                                      "writerLanes": args.writer_lanes,
                                       "copySinkRotateBytes": 1 << 62})
         inserter = DBInserter(cfg)
         inserter.attach_engine(eng.eng, [k for k in outs if k in ("audit_db", "db", "fs", "fb")])
@@ -353,7 +355,8 @@ def main():
         if inserter is not None:
             st = inserter.sink_stats()
             out["db_sink"] = {"writer": args.db_sink, "rows": st.get("rows"), "bytes": st.get("bytes"),
-                              "rows_per_s": round(st.get("rows", 0) / dt_max, 1), "failures": st.get("failures")}
+                              "rows_per_s": round(st.get("rows", 0) / dt_max, 1), "failures": st.get("failures"),
+                              "lanes": st.get("lanes")}
         if args.jmx:
             out["sx_bytes"] = eng.eng.sink_bytes("sx")
         print(json.dumps(out), flush=True)

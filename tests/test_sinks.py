@@ -326,3 +326,44 @@ def test_native_sink_parallel_cut_equals_serial(tmp_path, limit, pre):
     assert results[0] == results[1]
     assert results[0][3] == head + body
     assert results[0][1] == (len(rows) - results[0][2])
+
+
+@pytest.mark.parametrize("lanes", [2, 4])
+def test_native_sink_writer_lanes_write_every_row_once_in_lane_order(tmp_path, lanes):
+    """Writer lanes (dbsink.cpp): flushes go round-robin (blocks of 16) to `lanes` independent
+    writers, each with its own spool file per table.  Every row lands exactly once, the
+    `<table>.columns` file is shared, and each lane's file holds its rows in submission order
+    (a subsequence of the input).  Serial mixed-type input (wire lines) and a parallel-cut COPY blob
+    both go through the lanes."""
+    import glob
+    import random
+    from apmbackend_amd import _native
+    N = _native.load(build_if_missing=False)
+    rng = random.Random(lanes)
+    d = tmp_path / "spool"
+    s = N.DbSink(7, 1e9, ["t_tx", "t_fs", "t_al", "t_jx", "t_fb"], ["a", "b", "c", "d", "e"], "spool",
+                 [str(d)], 1 << 62, 2, lanes)
+    rows = [("r%07d\t" % i) + "y" * rng.randint(5, 300) + "\n" for i in range(40000)]
+    blob = "".join(rows)
+    assert len(blob) > 4 << 20  # parallel cut path
+    assert s.consume_encoded(1, blob.encode()) == len(rows)
+    small = [("s%05d\t" % i) + "z\n" for i in range(500)]
+    for i in range(0, len(small), 13):
+        s.consume_encoded(1, "".join(small[i:i + 13]).encode())
+    s.flush_all()
+    s.drain()
+    st = s.stats()
+    s.close()
+    assert st["lanes"] == lanes and st["failures"] == 0 and st["rows"] == len(rows) + len(small)
+    files = sorted(glob.glob(str(d / "t_fs*.copy")))
+    assert len(files) == lanes, files
+    order = {r: i for i, r in enumerate(rows + small)}
+    seen = []
+    for f in files:
+        got = open(f).read().splitlines(keepends=True)
+        idx = [order[r] for r in got]
+        assert idx == sorted(idx), f"{f}: rows out of submission order"
+        seen += got
+    assert sorted(seen) == sorted(rows + small)
+    assert open(d / "t_fs.columns").read() == "b\n"
+    assert not glob.glob(str(d / "*.tmp"))
