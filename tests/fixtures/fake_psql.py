@@ -21,6 +21,10 @@ for line in sys.stdin:
             rows.append(line)
         continue
     if line.startswith("COPY "):
+        if not globals().get("_seen"):
+            _seen = True  # one line per connection: the writer-lane tests count them
+            with open(os.path.join(out_dir, "connections"), "a") as f:
+                f.write(f"{os.getpid()}\n")
         table = line.split()[1]
     elif line.startswith("\\echo APMACK"):
         n = line.split()[2]

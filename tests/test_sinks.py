@@ -367,3 +367,29 @@ def test_native_sink_writer_lanes_write_every_row_once_in_lane_order(tmp_path, l
     assert sorted(seen) == sorted(rows + small)
     assert open(d / "t_fs.columns").read() == "b\n"
     assert not glob.glob(str(d / "*.tmp"))
+
+
+def test_native_sink_psql_writer_lanes_use_one_connection_each(tmp_path, monkeypatch):
+    """`lanes` = 3: three long-lived psql connections, each acknowledging its own COPYs; every
+    row is committed once."""
+    import sys
+    out = tmp_path / "pg"
+    out.mkdir()
+    monkeypatch.setenv("FAKE_PSQL_OUT", str(out))
+    monkeypatch.setenv("FAKE_PSQL_FAIL", "")
+    from apmbackend_amd import _native
+    N = _native.load(build_if_missing=False)
+    fake = [sys.executable, os.path.join(os.path.dirname(__file__), "fixtures", "fake_psql.py")]
+    s = N.DbSink(5, 1e9, ["apm_tx", "apm_stats", "apm_alerts", "apm_jmx", "apm_fleet_stats"], ["a", "b", "c", "d", "e"],
+                 "psql", fake, 0, 2, 3)
+    lines = [l for l in _wire_lines(400) if l.startswith("tx|")]
+    assert len(lines) >= 160  # >= 32 flushes of 5: all three lanes get work
+    s.consume(("\n".join(lines) + "\n").encode())
+    s.flush_all()
+    s.drain()
+    st = s.stats()
+    s.close()
+    assert st["failures"] == 0 and st["rows"] == len(lines) and st["lanes"] == 3
+    want = sinks.copy_encode_lines(lines)["tx"]
+    assert sorted(open(out / "apm_tx.rows").read().splitlines(keepends=True)) == sorted(want)
+    assert len(set(open(out / "connections").read().split())) == 3
