@@ -317,7 +317,9 @@ def test_server_rollup_fuses_window_stats_with_jmx_gauges(servers):
         avgs = [float(r[5]) if r[5] != "undefined" else 0.0 for r in rows]
         if sum(ns) > 0:
             want = sum(a * n for a, n in zip(avgs, ns)) / sum(ns)
-            assert abs(float(f[5]) - want) <= 0.06
+            # sx prints the exact window mean with toFixed(1); the st rows it is checked against
+            # print their means with toFixed(1) too: each side is off by <= 0.05
+            assert abs(float(f[5]) - want) <= 0.1 + 1e-9
         if srv == "jvm00" and f[9] != "undefined":
             assert abs(float(f[9]) - heap) < 1e-3 and float(f[16]) == 1.5
             checked += 1
