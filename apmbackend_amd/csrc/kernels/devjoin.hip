@@ -873,8 +873,20 @@ __global__ __launch_bounds__(1024) void k_min_pos(const int64_t* __restrict__ gi
   // grid-stride per lane, wave shuffle, one LDS pass per block, one atomic per block (a single
   // atomicMin per wave on one address serialised ~6k waves in the L2 atomic unit: 81 us)
   __shared__ unsigned long long red[1024 / APM_WAVE];
+  // four independent loads in flight per lane per step: one load per step left every lane
+  // waiting a full HBM latency per element
   unsigned long long v = ~0ULL;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    const uint64_t g0 = (uint64_t)gid[i], g1 = (uint64_t)gid[i + stride];
+    const uint64_t g2 = (uint64_t)gid[i + 2 * stride], g3 = (uint64_t)gid[i + 3 * stride];
+    const unsigned long long a = (g0 >> 20) < (g1 >> 20) ? (g0 >> 20) : (g1 >> 20);
+    const unsigned long long b = (g2 >> 20) < (g3 >> 20) ? (g2 >> 20) : (g3 >> 20);
+    const unsigned long long m = a < b ? a : b;
+    v = m < v ? m : v;
+  }
+  for (; i < n; i += stride) {
     const unsigned long long p = (unsigned long long)((uint64_t)gid[i] >> 20);
     v = p < v ? p : v;
   }
@@ -1095,7 +1107,8 @@ void apm_dj_gather_copy(const int64_t* gid, int64_t n, const char* ring, uint64_
 
 void apm_dj_min_pos(const int64_t* gid, int64_t n, unsigned long long* out, hipStream_t s) {
   if (n <= 0) return;
-  const unsigned blocks = (unsigned)std::min<int64_t>(256, (n + 1023) / 1024);
+  // >= 2 blocks per CU once the pool is large (512 atomics at most on the one result word)
+  const unsigned blocks = (unsigned)std::min<int64_t>(512, (n + 1023) / 1024);
   hipLaunchKernelGGL(k_min_pos, dim3(blocks), dim3(1024), 0, s, gid, n, out);
 }
 
