@@ -521,6 +521,12 @@ class IngestService:
                  "- HBM %.2f GB - fleet rounds %s",
                  *(stages[k] / nb for k in _STAGE_KEYS), *pct, hbm / 1e9,
                  self.native.fleet_rounds() if hasattr(self.native, "fleet_rounds") else "-")
+        # capacity overflows: window samples past the spill area (gpu.bucketOverflowCapacity) or
+        # series past gpu.maxSeries make that interval's statistics wrong -- say so every interval
+        lost = {k: int(m.get(k, 0)) for k in ("spill_dropped", "series_overflow_tx", "tx_dropped")}
+        if any(lost.values()):
+            log.warning("ENGINE capacity exceeded (totals): %s -- raise gpu.bucketOverflowCapacity / gpu.maxSeries",
+                     ", ".join(f"{k}={v}" for k, v in lost.items()))
         nm = list(self.native.node_metrics()) if hasattr(self.native, "node_metrics") else []
         if nm and nm[0] > 1 and getattr(self, "rank", 0) == 0:
             prev_nm = getattr(self, "_nm_prev", None) or [0.0] * len(nm)

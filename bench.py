@@ -348,6 +348,9 @@ def main():
                                             "t_stats_tx_ms", "t_release_ms", "t_rollover_ms", "t_format_ms", "t_out_ms")},
             "corpus_gen_s": round(t_gen, 2),
             "db_insert_bytes_total": out_bytes,
+            # capacity overflows (must be 0: a dropped window sample makes that interval's st wrong)
+            "spill_dropped": int(m1.get("spill_dropped", 0)),
+            "series_overflow_tx": int(m1.get("series_overflow_tx", 0)),
             "alerts": int(m1["alerts"] - m0["alerts"]),
             "alert_candidates": int(m1["alert_candidates"] - m0["alert_candidates"]),
             "device_GB": round(eng.eng.device_bytes() / 1e9, 1),

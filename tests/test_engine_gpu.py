@@ -285,6 +285,10 @@ def test_server_rollup_fuses_window_stats_with_jmx_gauges(servers):
     from apmbackend_amd.utils.records import JmxEntry
     lines, bl = synth_batches(10, duration=500 if servers <= 2 else 200, servers=servers)
     C = small_cfg("exact")
+    # 70 JVMs' hot series overflow small_cfg's 64k-entry spill area (window samples past it are
+    # dropped and that interval's st is wrong): size it for the shard, and check st against the
+    # CPU oracle so the rollup is compared with correct window statistics
+    C["gpu"]["bucketOverflowCapacity"] = 1 << 22
     eng = APMEngine(C, keep_text=True)
     syn = SyntheticJmx(5)
     jx = JmxEntry.from_stats(START, "jvm00", syn.payload("jvm00")).to_csv()
@@ -297,6 +301,10 @@ def test_server_rollup_fuses_window_stats_with_jmx_gauges(servers):
         sx += eng.take("sx")
         st += eng.take("st")
     assert sx
+    assert eng.metrics()["spill_dropped"] == 0
+    P = PipelineOracle(copy.deepcopy(C), UTC)
+    P.run_batches(bl)
+    assert st == P.stats
     by_ts = collections.defaultdict(list)
     for l in st:
         f = l.split("|")
