@@ -52,8 +52,11 @@ __global__ void k_bucket_append(const TxRec* __restrict__ tx, uint32_t lo, uint3
     if (j < st.spill_cap) {
       st.spill_series[(size_t)slot * st.spill_cap + j] = r.series;
       st.spill_val[(size_t)slot * st.spill_cap + j] = r.elapsed;
-    } else if (st.spill_drop) {
-      atomicAdd(st.spill_drop, 1ULL);
+    } else {
+      // spill list full: the sample is lost -- take it back out of the cell count, so the
+      // count K8 trusts stays the number of stored samples (never reads unwritten positions)
+      atomicSub(&st.counts[cidx], 1);
+      if (st.spill_drop) atomicAdd(st.spill_drop, 1ULL);
     }
   }
 }
@@ -130,6 +133,12 @@ __global__ __launch_bounds__(1024) void k_bucket_append_ordered(const TxRec* __r
       st.counts[cell] = end;
       const int first_sp = max(base, st.cap);
       sp0[k] = end > first_sp ? atomicAdd(&st.spill_n[cell / (uint32_t)st.S], end - first_sp) - first_sp : 0;
+      // a full spill list drops the run's tail (spill index sp0 + p >= spill_cap): the cell keeps
+      // the count of the samples actually stored (see k_bucket_append)
+      if (end > first_sp) {
+        const int stored_end = max(first_sp, min(end, st.spill_cap - sp0[k]));
+        if (stored_end < end) st.counts[cell] = stored_end;
+      }
     }
     __syncthreads();
     for (int k = threadIdx.x; k < m; k += blockDim.x) {

@@ -610,3 +610,26 @@ def test_resync_on_matrix_cores_matches_valu_resync():
     assert len(a) == len(b) > 100
     diff = sum(x != y for x, y in zip(a, b))
     assert diff <= len(a) // 200, diff
+
+
+def test_spill_overflow_drops_samples_without_corrupting_windows():
+    """48 JVMs with a 64k-entry spill area: hot series' window samples overflow it.  The lost
+    samples are counted (spill_dropped) and taken out of their cell counts, so K8 never reads
+    unwritten positions: every st value stays within the range of the input's elapsed times
+    (before the fix: percentiles of ~1e9 read from unwritten memory, varying run to run)."""
+    lines, bl = synth_batches(10, duration=120, servers=48)
+    C = small_cfg("exact")
+    assert C["gpu"]["bucketOverflowCapacity"] == 1 << 16
+    P = PipelineOracle(copy.deepcopy(C), UTC)
+    P.run_batches(bl)
+    hi = max(float(v) for l in P.stats for v in l.split("|")[5:8] if v != "undefined")
+    eng = APMEngine(C, keep_text=True)
+    st = []
+    for now, chunks in bl:
+        eng.process_lines(chunks, now)
+        st += eng.take("st")
+    assert eng.metrics()["spill_dropped"] > 0
+    assert len(st) == len(P.stats)
+    for l in st:
+        for v in l.split("|")[5:8]:
+            assert v == "undefined" or 0.0 <= float(v) <= hi, l
