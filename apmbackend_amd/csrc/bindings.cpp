@@ -108,6 +108,7 @@ EngineConfig config_from(const py::dict& d) {
   c.device_join = get<int>(d, "device_join", c.device_join);
   c.join_table_bits = get<int>(d, "join_table_bits", c.join_table_bits);
   c.need_arena = get<uint32_t>(d, "need_arena", c.need_arena);
+  c.join_chain_blocks = get<uint32_t>(d, "join_chain_blocks", c.join_chain_blocks);
   c.tx_ring_bytes = get<uint64_t>(d, "tx_ring_bytes", c.tx_ring_bytes);
   c.max_raw_services = get<uint32_t>(d, "max_raw_services", c.max_raw_services);
   return c;
@@ -163,6 +164,12 @@ py::dict counters_dict(const JoinCounters& c) {
   d["events"] = c.events; d["tx"] = c.tx; d["tx_db"] = c.tx_db; d["expired_partials"] = c.expired_partials;
   d["need_expired"] = c.need_expired; d["ejb_exit_unmatched"] = c.ejb_exit_unmatched;
   d["invalid_acct"] = c.invalid_acct; d["audit_errors"] = c.audit_errors; d["host_fallback"] = c.host_fallback;
+  d["partial_overflow"] = c.partial_overflow; d["need_overflow"] = c.need_overflow; d["table_full"] = c.table_full;
+  d["pool_exhausted"] = c.pool_exhausted; d["chain_partial_blocks"] = c.chain_partial_blocks;
+  d["chain_need_blocks"] = c.chain_need_blocks; d["chain_logid_blocks"] = c.chain_logid_blocks;
+  d["table_slots"] = c.table_slots; d["table_grows"] = c.table_grows; d["table_rebuilds"] = c.table_rebuilds;
+  d["need_arena_entries"] = c.need_arena_entries; d["arena_grows"] = c.arena_grows;
+  d["chain_pool_blocks"] = c.chain_pool_blocks; d["pool_grows"] = c.pool_grows;
   return d;
 }
 

@@ -353,6 +353,7 @@ __device__ uint32_t key_claim(KeyState* __restrict__ t, uint32_t mask, uint64_t 
         s.rec_exp = -__builtin_inf();
         s.need = -1;
         s.n_part = 0;
+        s.pblk = 0;
         atomicAdd(&cnt->n_keys_new, 1u);
         return idx;
       }
@@ -417,6 +418,137 @@ __global__ void k_claim(DJArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------ chain-block pool
+// Free block indices live in a ring: allocation takes positions [head, tail) (tail is fixed while
+// the allocating kernel runs), frees append at ptail, and k_pool_fix publishes the freed ones
+// (tail = ptail) once no allocating kernel is in flight.  So a block freed in a batch is never
+// reused in that batch: k_write may still read a logId chain its expiry just released.  The host
+// grows the pool before a batch until its free count covers the batch's worst case.
+__device__ __forceinline__ uint8_t* blk_ptr(uint8_t* pool, int32_t b1) { return pool + (size_t)(b1 - 1) * CHAIN_BLK; }
+__device__ __forceinline__ const uint8_t* blk_ptr(const uint8_t* pool, int32_t b1) {
+  return pool + (size_t)(b1 - 1) * CHAIN_BLK;
+}
+__device__ __forceinline__ int32_t blk_next(const uint8_t* pool, int32_t b1) { return *(const int32_t*)blk_ptr(pool, b1); }
+
+__device__ int32_t blk_alloc(const DJArgs& a) {
+  const unsigned long long k = atomicAdd(&a.counts->pool_head, 1ULL);
+  const unsigned long long tail = __hip_atomic_load(&a.counts->pool_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (k >= tail) { atomicAdd(&a.counts->pool_fail, 1ULL); return 0; }
+  const uint32_t b = a.pool_ring[k & a.pool_mask];
+  *(int32_t*)(a.pool + (size_t)b * CHAIN_BLK) = 0;  // next
+  return (int32_t)b + 1;
+}
+
+__device__ void chain_free(const uint8_t* pool, uint32_t* ring, uint32_t mask, JoinCounts* c, int32_t b1) {
+  while (b1) {
+    const int32_t nx = blk_next(pool, b1);
+    const unsigned long long k = atomicAdd(&c->pool_ptail, 1ULL);
+    ring[k & mask] = (uint32_t)(b1 - 1);
+    b1 = nx;
+  }
+}
+
+// block `bi` (0-based) of a chain
+__device__ __forceinline__ int32_t chain_at(const uint8_t* pool, int32_t b1, int bi) {
+  for (; bi > 0; --bi) b1 = blk_next(pool, b1);
+  return b1;
+}
+
+// ---- open partials of a key (recordCache[logId] map): inline slots, then the PartBlk chain.
+// A key's map holds one partial per service, so the order of the set is not observable (the
+// reference only looks entries up by service and discards them on expiry).
+__device__ int part_find(const DJArgs& a, const KeyState& ks, uint64_t svc) {
+  int f = -1;
+#pragma unroll
+  for (int k = 0; k < KS_PARTS; ++k)
+    if (k < ks.n_part && ks.part_svc[k] == svc) f = k;
+  if (f >= 0 || ks.n_part <= KS_PARTS) return f;
+  int j = KS_PARTS;
+  for (int32_t b = ks.pblk; b && j < ks.n_part; b = blk_next(a.pool, b)) {
+    const PartBlk* pb = (const PartBlk*)blk_ptr(a.pool, b);
+    for (int k = 0; k < PBLK_N && j < ks.n_part; ++k, ++j)
+      if (pb->svc[k] == svc) return j;
+  }
+  return -1;
+}
+
+__device__ __forceinline__ PartBlk* part_blk(const DJArgs& a, const KeyState& ks, int j) {
+  return (PartBlk*)blk_ptr(a.pool, chain_at(a.pool, ks.pblk, (j - KS_PARTS) / PBLK_N));
+}
+
+__device__ double part_get_start(const DJArgs& a, const KeyState& ks, int f) {
+  if (f >= KS_PARTS) return part_blk(a, ks, f)->start[(f - KS_PARTS) % PBLK_N];
+  double v = 0;
+#pragma unroll
+  for (int k = 0; k < KS_PARTS; ++k)
+    if (k == f) v = ks.part_start[k];
+  return v;
+}
+
+__device__ void part_set(const DJArgs& a, KeyState& ks, int f, uint64_t svc, double start) {
+  if (f >= KS_PARTS) {
+    PartBlk* pb = part_blk(a, ks, f);
+    pb->svc[(f - KS_PARTS) % PBLK_N] = svc;
+    pb->start[(f - KS_PARTS) % PBLK_N] = start;
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < KS_PARTS; ++k)
+    if (k == f) { ks.part_svc[k] = svc; ks.part_start[k] = start; }
+}
+
+__device__ bool part_append(const DJArgs& a, KeyState& ks, uint64_t svc, double start) {
+  const int n = ks.n_part;
+  if (n >= KS_PARTS && (n - KS_PARTS) % PBLK_N == 0) {  // the chain needs a new block
+    const int32_t nb = blk_alloc(a);
+    if (!nb) return false;
+    atomicAdd(&a.counts->chain_parts, 1ULL);
+    const int bi = (n - KS_PARTS) / PBLK_N;
+    if (bi == 0) ks.pblk = nb;
+    else *(int32_t*)blk_ptr(a.pool, chain_at(a.pool, ks.pblk, bi - 1)) = nb;
+  }
+  ks.n_part = n + 1;
+  part_set(a, ks, n, svc, start);
+  return true;
+}
+
+// map.delete(service): the last partial moves into the hole; an emptied tail block is freed
+__device__ void part_remove(const DJArgs& a, KeyState& ks, int f) {
+  const int last = ks.n_part - 1;
+  if (f != last) {
+    uint64_t sv = 0;
+    double st = 0;
+    if (last >= KS_PARTS) {
+      const PartBlk* pb = part_blk(a, ks, last);
+      sv = pb->svc[(last - KS_PARTS) % PBLK_N];
+      st = pb->start[(last - KS_PARTS) % PBLK_N];
+    } else {
+#pragma unroll
+      for (int k = 0; k < KS_PARTS; ++k)
+        if (k == last) { sv = ks.part_svc[k]; st = ks.part_start[k]; }
+    }
+    part_set(a, ks, f, sv, st);
+  }
+  ks.n_part = last;
+  if (last >= KS_PARTS && (last - KS_PARTS) % PBLK_N == 0) {
+    const int bi = (last - KS_PARTS) / PBLK_N;
+    if (bi == 0) {
+      chain_free(a.pool, a.pool_ring, a.pool_mask, a.counts, ks.pblk);
+      ks.pblk = 0;
+    } else {
+      int32_t* link = (int32_t*)blk_ptr(a.pool, chain_at(a.pool, ks.pblk, bi - 1));
+      chain_free(a.pool, a.pool_ring, a.pool_mask, a.counts, *link);
+      *link = 0;
+    }
+  }
+}
+
+__device__ void part_clear(const DJArgs& a, KeyState& ks) {
+  if (ks.pblk) chain_free(a.pool, a.pool_ring, a.pool_mask, a.counts, ks.pblk);
+  ks.pblk = 0;
+  ks.n_part = 0;
+}
+
 // ------------------------------------------------------------------------ outputs
 // outputRecord (:264-290): start falls back to end - elapsed; numbers pass through parseInt.
 __device__ __forceinline__ TxDev make_tx(int32_t server, uint64_t svc, uint8_t src, uint32_t lid, uint32_t lid_len,
@@ -477,28 +609,78 @@ __device__ int32_t need_alloc(DJArgs& a, const JOp& op, uint64_t gkey) {
   ne.created = (a.batch_no << 28) | (uint64_t)(op.line & 0xfffffffu);
   ne.server = op.server;
   ne.n = 0;
+  ne.iblk = 0;
+  ne.lblk = 0;
+  ne.vidx = a.arena_base + k;
   uint32_t n = op.lid_len;
-  if (n > NEED_LID) { atomicAdd(&a.counts->need_overflow, 1ULL); n = NEED_LID; }
-  ne.lid_len = (int32_t)n;
   const uint8_t* src = (op.flags & JF_LID_HOST) ? a.hbuf + op.lid : a.bytes + op.lid;
-  for (uint32_t j = 0; j < n; ++j) ne.lid[j] = (char)src[j];
+  for (uint32_t j = 0; j < n && j < (uint32_t)NEED_LID; ++j) ne.lid[j] = (char)src[j];
+  // a logId longer than the inline bytes continues in a LidBlk chain (the tx line prints it whole)
+  int32_t prev = 0;
+  for (uint32_t o = NEED_LID; o < n; o += LBLK_N) {
+    const int32_t b = blk_alloc(a);
+    if (!b) { atomicAdd(&a.counts->need_overflow, 1ULL); n = o; break; }
+    atomicAdd(&a.counts->chain_lids, 1ULL);
+    if (prev) *(int32_t*)blk_ptr(a.pool, prev) = b;
+    else ne.lblk = b;
+    LidBlk* lb = (LidBlk*)blk_ptr(a.pool, b);
+    const uint32_t m = min((uint32_t)LBLK_N, n - o);
+    for (uint32_t j = 0; j < m; ++j) lb->b[j] = (char)src[o + j];
+    prev = b;
+  }
+  ne.lid_len = (int32_t)n;
   return (int32_t)idx;
 }
 
+// needMap.set(service, rec): a Map keeps the first insertion position of a service and replaces
+// its value; new services append (inline items, then the NeedBlk chain)
 __device__ void need_put(DJArgs& a, NeedEnt& ne, const NeedItem& it) {
-  for (int j = 0; j < ne.n; ++j)
+  const int n = ne.n;
+  for (int j = 0; j < n && j < NEED_ITEMS; ++j)
     if (ne.items[j].svc == it.svc) { ne.items[j] = it; return; }
-  if (ne.n < NEED_ITEMS) ne.items[ne.n++] = it;
-  else atomicAdd(&a.counts->need_overflow, 1ULL);
+  if (n > NEED_ITEMS) {
+    int j = NEED_ITEMS;
+    for (int32_t b = ne.iblk; b && j < n; b = blk_next(a.pool, b)) {
+      NeedBlk* nb = (NeedBlk*)blk_ptr(a.pool, b);
+      for (int k = 0; k < NBLK_N && j < n; ++k, ++j)
+        if (nb->items[k].svc == it.svc) { nb->items[k] = it; return; }
+    }
+  }
+  if (n < NEED_ITEMS) { ne.items[n] = it; ne.n = n + 1; return; }
+  const int j = n - NEED_ITEMS;
+  int32_t b;
+  if (j % NBLK_N == 0) {
+    b = blk_alloc(a);
+    if (!b) { atomicAdd(&a.counts->need_overflow, 1ULL); return; }
+    atomicAdd(&a.counts->chain_items, 1ULL);
+    if (j == 0) ne.iblk = b;
+    else *(int32_t*)blk_ptr(a.pool, chain_at(a.pool, ne.iblk, j / NBLK_N - 1)) = b;
+  } else {
+    b = chain_at(a.pool, ne.iblk, j / NBLK_N);
+  }
+  ((NeedBlk*)blk_ptr(a.pool, b))->items[j % NBLK_N] = it;
+  ne.n = n + 1;
 }
 
-__device__ void need_drain(NeedEnt& ne, int32_t nidx, double acct, Emitter& em) {
-  // saveAcctNum: every parked record of the logId is output with the new account (to_db false)
+__device__ __forceinline__ const NeedItem& need_item(const uint8_t* pool, const NeedEnt& ne, int j, int32_t& b) {
+  // j-th item; `b` = the block of item j - 1 (walks forward one block at a time)
+  if (j < NEED_ITEMS) return ne.items[j];
+  const int k = (j - NEED_ITEMS) % NBLK_N;
+  if (k == 0) b = (j == NEED_ITEMS) ? ne.iblk : blk_next(pool, b);
+  return ((const NeedBlk*)blk_ptr(pool, b))->items[k];
+}
+
+__device__ void need_drain(DJArgs& a, NeedEnt& ne, int32_t nidx, double acct, Emitter& em) {
+  // saveAcctNum: every parked record of the logId is output with the new account (to_db false),
+  // in insertion order (needMap.forEach)
+  int32_t b = 0;
   for (int j = 0; j < ne.n; ++j) {
-    const NeedItem& r = ne.items[j];
+    const NeedItem& r = need_item(a.pool, ne, j, b);
     em.put(make_tx(ne.server, r.svc, LID_NEED, (uint32_t)nidx, (uint32_t)ne.lid_len, acct, r.start,
                    (r.flags & JF_START_EMPTY) != 0, r.end, (r.flags & JF_TS_EMPTY) != 0, r.elapsed, false));
   }
+  if (ne.iblk) chain_free(a.pool, a.pool_ring, a.pool_mask, a.counts, ne.iblk);
+  ne.iblk = 0;
   ne.n = 0;
 }
 
@@ -523,7 +705,7 @@ __global__ void k_group_walk(DJArgs a) {
   bool acct_live = ks.acct_exp >= now;
   if (!(ks.rec_exp >= now) && ks.n_part > 0) {  // expired recordCache entry: discarded (:220-224)
     atomicAdd(&a.counts->expired_partials, (unsigned long long)ks.n_part);
-    ks.n_part = 0;
+    part_clear(a, ks);
   }
   NeedEnt* ne = nullptr;
   int32_t nidx = -1;
@@ -538,27 +720,23 @@ __global__ void k_group_walk(DJArgs a) {
     const bool ts_empty = (op.flags & JF_TS_EMPTY) != 0;
     switch (op.op) {
       case JOP_ENTRY: {
-        if (!(ks.rec_exp >= now)) { ks.rec_exp = now + a.rec_ttl; ks.n_part = 0; }
-        int f = -1;
-        for (int k = 0; k < KS_PARTS; ++k) if (k < ks.n_part && ks.part_svc[k] == op.svc) f = k;
-        if (f >= 0) ks.part_start[f] = op.ts;
-        else if (ks.n_part < KS_PARTS) { ks.part_svc[ks.n_part] = op.svc; ks.part_start[ks.n_part] = op.ts; ++ks.n_part; }
-        else atomicAdd(&a.counts->partial_overflow, 1ULL);
+        if (!(ks.rec_exp >= now)) { ks.rec_exp = now + a.rec_ttl; part_clear(a, ks); }
+        const int f = part_find(a, ks, op.svc);
+        if (f >= 0) part_set(a, ks, f, op.svc, op.ts);
+        else if (!part_append(a, ks, op.svc, op.ts)) atomicAdd(&a.counts->partial_overflow, 1ULL);
         break;
       }
       case JOP_EJB_EXIT:
       case JOP_CT_EXIT: {
         const bool ct = op.op == JOP_CT_EXIT;
-        int f = -1;
-        if (ks.rec_exp >= now)
-          for (int k = 0; k < KS_PARTS; ++k) if (k < ks.n_part && ks.part_svc[k] == op.svc) f = k;
+        const int f = (ks.rec_exp >= now) ? part_find(a, ks, op.svc) : -1;
         if (f < 0) {
           if (!ct) { atomicAdd(&a.counts->ejb_unmatched, 1ULL); break; }
           // salvageRecordAndOutput (:500-504): BAF account saved under this logId, then the
           // record is output without a logId
           if ((op.flags & JF_BAF) && (op.flags & JF_BAF_VALID)) {
             ks.acct = op.aux2; ks.acct_exp = now + a.acct_ttl; acct_live = true;
-            if (ne && ne->n) need_drain(*ne, nidx, op.aux2, em);
+            if (ne && ne->n) need_drain(a, *ne, nidx, op.aux2, em);
           } else if (op.flags & JF_BAF) {
             atomicAdd(&a.counts->invalid_acct, 1ULL);
           }
@@ -566,12 +744,8 @@ __global__ void k_group_walk(DJArgs a) {
                          op.ts, ts_empty, op.num, false));
           break;
         }
-        const double pstart = ks.part_start[f];
-        auto remove_part = [&]() {
-          for (int k = 0; k < KS_PARTS - 1; ++k)
-            if (k >= f && k + 1 < ks.n_part) { ks.part_svc[k] = ks.part_svc[k + 1]; ks.part_start[k] = ks.part_start[k + 1]; }
-          --ks.n_part;
-        };
+        const double pstart = part_get_start(a, ks, f);
+        auto remove_part = [&]() { part_remove(a, ks, f); };
         if (acct_live) {
           remove_part();
           em.put(make_tx(op.server, op.svc, lid_src_of(op), op.lid, op.lid_len, ks.acct, pstart, false, op.ts,
@@ -584,7 +758,7 @@ __global__ void k_group_walk(DJArgs a) {
           alt = op.aux;
           if (op.flags & JF_BAF_VALID) {  // may drain the records parked before this one
             ks.acct = op.aux2; ks.acct_exp = now + a.acct_ttl; acct_live = true;
-            if (ne && ne->n) need_drain(*ne, nidx, op.aux2, em);
+            if (ne && ne->n) need_drain(a, *ne, nidx, op.aux2, em);
           } else {
             atomicAdd(&a.counts->invalid_acct, 1ULL);
           }
@@ -600,7 +774,7 @@ __global__ void k_group_walk(DJArgs a) {
       }
       case JOP_ACCT: {
         ks.acct = op.num; ks.acct_exp = now + a.acct_ttl; acct_live = true;
-        if (ne && ne->n) need_drain(*ne, nidx, op.num, em);
+        if (ne && ne->n) need_drain(a, *ne, nidx, op.num, em);
         break;
       }
       case JOP_AUDIT_TX: {
@@ -641,7 +815,10 @@ __global__ void k_exp_keys(DJArgs a) {
   const NeedEnt& ne = a.arena[idx];
   a.exp_key[e] = ne.n > 0 ? ne.created : ~0ULL;
   a.exp_idx[e] = idx;
-  if (ne.n == 0) a.arena[idx].key = 0;  // drained entry: gone (k_exp_emit clears the others)
+  if (ne.n == 0) {  // drained entry: gone (k_exp_emit clears the others)
+    a.arena[idx].key = 0;
+    if (ne.lblk) chain_free(a.pool, a.pool_ring, a.pool_mask, a.counts, ne.lblk);
+  }
 }
 
 __global__ void k_exp_count(DJArgs a) {
@@ -663,12 +840,18 @@ __global__ void k_exp_emit(DJArgs a) {
   const uint32_t idx = a.exp_idx_sorted[e];
   NeedEnt& ne = a.arena[idx];
   const uint32_t base = a.exp_pos[e];
+  int32_t b = 0;
   for (uint32_t k = 0; k < n && base + k < a.out_cap; ++k) {
-    const NeedItem& r = ne.items[k];
+    const NeedItem& r = need_item(a.pool, ne, (int)k, b);
     a.out[base + k] = make_tx(ne.server, r.svc, LID_NEED, idx, (uint32_t)ne.lid_len, r.alt, r.start,
                               (r.flags & JF_START_EMPTY) != 0, r.end, (r.flags & JF_TS_EMPTY) != 0, r.elapsed,
                               (r.flags & JF_TO_DB) != 0);
   }
+  // chains go back to the pool; their bytes stay readable until the next batch (k_write still
+  // prints this entry's logId: `lblk` is left in place)
+  if (ne.iblk) chain_free(a.pool, a.pool_ring, a.pool_mask, a.counts, ne.iblk);
+  if (ne.lblk) chain_free(a.pool, a.pool_ring, a.pool_mask, a.counts, ne.lblk);
+  ne.iblk = 0;
   ne.n = 0;
   ne.key = 0;  // the entry is gone (an expired region is reused by later batches)
 }
@@ -708,6 +891,26 @@ __device__ __forceinline__ const char* lid_ptr(const DJFormatArgs& f, const TxDe
     case LID_NEED: return f.arena[t.lid & (f.arena_cap - 1)].lid;
     default: return "";
   }
+}
+
+__device__ char* put_lid(const DJFormatArgs& f, const TxDev& t, char* p) {
+  if (t.lid_src != LID_NEED || t.lid_len <= NEED_LID) {
+    const char* s = lid_ptr(f, t);
+    for (int i = 0; i < t.lid_len; ++i) p[i] = s[i];
+    return p + t.lid_len;
+  }
+  const NeedEnt& ne = f.arena[t.lid & (f.arena_cap - 1)];
+  for (int i = 0; i < NEED_LID; ++i) p[i] = ne.lid[i];
+  p += NEED_LID;
+  int rem = (int)t.lid_len - NEED_LID;
+  for (int32_t b = ne.lblk; b && rem > 0; b = blk_next(f.pool, b)) {
+    const LidBlk* lb = (const LidBlk*)blk_ptr(f.pool, b);
+    const int m = rem < LBLK_N ? rem : LBLK_N;
+    for (int i = 0; i < m; ++i) p[i] = lb->b[i];
+    p += m;
+    rem -= m;
+  }
+  return p;
 }
 
 __device__ __forceinline__ bool stat_usable(const TxDev& t) { return !t.to_db && t.end == t.end && t.end >= 10000.0; }
@@ -767,7 +970,7 @@ __global__ void k_write(DJFormatArgs f) {
   *p++ = '|';
   p = put_str(p, f.names + rs.norm_off, rs.norm_len);
   *p++ = '|';
-  p = put_str(p, lid_ptr(f, t), t.lid_len);
+  p = put_lid(f, t, p);
   *p++ = '|';
   bool inexact = false;
   p += js_num(p, t.acct, &inexact); *p++ = '|';
@@ -821,7 +1024,8 @@ __global__ void k_reset_first(DJFormatArgs f, uint32_t n) {
 // ------------------------------------------------------------------------ rebuild / ring
 __global__ void k_rebuild(const KeyState* __restrict__ old, uint32_t old_cap, KeyState* __restrict__ fresh,
                           uint32_t mask, const NeedEnt* __restrict__ arena, uint32_t arena_cap, double now,
-                          JoinCounts* cnt, unsigned long long* live) {
+                          JoinCounts* cnt, unsigned long long* live, const uint8_t* pool, uint32_t* pool_ring,
+                          uint32_t pool_mask) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= old_cap) return;
   KeyState s = old[i];
@@ -834,6 +1038,10 @@ __global__ void k_rebuild(const KeyState* __restrict__ old, uint32_t old_cap, Ke
     need = ne.key == s.key && ne.exp >= now;
   }
   if (!rec && s.n_part > 0 && !(s.rec_exp >= now)) atomicAdd(&cnt->expired_partials, (unsigned long long)s.n_part);
+  if (!rec && s.pblk) {  // the partials are dropped with the key (or with their expired map)
+    chain_free(pool, pool_ring, pool_mask, cnt, s.pblk);
+    s.pblk = 0;
+  }
   if (!rec && !acct && !need) return;
   if (!(s.rec_exp >= now)) s.n_part = 0;
   uint32_t h = home_of(s.key, mask);
@@ -919,6 +1127,56 @@ __global__ void k_relocate(int64_t* __restrict__ gid, int64_t n, char* __restric
   char* dst = ring + (np & (ring_cap - 1));
   for (uint32_t k = lane; k < len; k += APM_WAVE) dst[k] = src[k];
   if (lane == 0) gid[w] = (int64_t)((np << 20) | (g & 0xfffffu));
+}
+
+// ------------------------------------------------------------------------ pool / arena upkeep
+__global__ void k_pool_fix(JoinCounts* c) {
+  const unsigned long long h = c->pool_head, t = c->pool_tail;
+  c->pool_head = h < t ? h : t;  // failed allocations overshoot head
+  c->pool_tail = c->pool_ptail;
+}
+
+__global__ void k_pool_init(uint32_t* ring, uint32_t n, JoinCounts* c) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) ring[i] = i;
+  if (i == 0) { c->pool_head = 0; c->pool_tail = n; c->pool_ptail = n; }
+}
+
+__global__ void k_pool_grow(const uint32_t* __restrict__ old_ring, uint32_t old_mask, uint32_t* __restrict__ fresh,
+                            uint32_t old_n, uint32_t new_n, const JoinCounts* c) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned long long head = c->pool_head;
+  const uint32_t avail = (uint32_t)(c->pool_tail - head);
+  if (i < avail) fresh[i] = old_ring[(head + i) & old_mask];
+  else if (i < avail + (new_n - old_n)) fresh[i] = old_n + (i - avail);
+}
+
+__global__ void k_pool_grow_set(JoinCounts* c, uint32_t old_n, uint32_t new_n) {
+  const unsigned long long avail = c->pool_tail - c->pool_head;
+  c->pool_head = 0;
+  c->pool_tail = c->pool_ptail = avail + (new_n - old_n);
+}
+
+__global__ void k_arena_move(const NeedEnt* __restrict__ old, uint32_t old_cap, NeedEnt* __restrict__ fresh,
+                             uint32_t fresh_cap, uint64_t lo, uint64_t n) {
+  constexpr int Q = sizeof(NeedEnt) / 16;
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t e = t / Q;
+  if (e >= n) return;
+  const uint64_t v = lo + e;
+  const uint4* s = reinterpret_cast<const uint4*>(old + (v & (old_cap - 1)));
+  uint4* d = reinterpret_cast<uint4*>(fresh + (v & (fresh_cap - 1)));
+  d[t % Q] = s[t % Q];
+}
+
+__global__ void k_arena_remap(KeyState* __restrict__ table, uint32_t cap, const NeedEnt* __restrict__ old,
+                              uint32_t old_cap, uint32_t fresh_cap, uint64_t lo, uint64_t hi) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cap) return;
+  KeyState& s = table[i];
+  if (!s.key || s.need < 0) return;
+  const NeedEnt& ne = old[(uint32_t)s.need & (old_cap - 1)];
+  s.need = (ne.key == s.key && ne.vidx >= lo && ne.vidx < hi) ? (int32_t)(ne.vidx & (fresh_cap - 1)) : -1;
 }
 
 // ------------------------------------------------------------------------ small helpers
@@ -1050,6 +1308,7 @@ int apm_dj_join(DJArgs* a, hipStream_t s) {
     HIP_OK(hipMemsetAsync(a->out_pos, 0, 4, s));
     hipLaunchKernelGGL(k_place, dim3(1), dim3(TB), 0, s, *a);
   }
+  hipLaunchKernelGGL(k_pool_fix, dim3(1), dim3(1), 0, s, a->counts);
   return 0;
 }
 
@@ -1082,9 +1341,33 @@ int apm_dj_write(DJFormatArgs* f, uint32_t n_stats, hipStream_t s) {
 }
 
 void apm_dj_rebuild(const KeyState* old, uint32_t old_cap, KeyState* fresh, uint32_t fresh_mask, const NeedEnt* arena,
-                    uint32_t arena_cap, double now, JoinCounts* counts, unsigned long long* live, hipStream_t s) {
-  hipLaunchKernelGGL(k_rebuild, dim3((old_cap + TB - 1) / TB), dim3(TB), 0, s, old, old_cap, fresh, fresh_mask, arena,
-                     arena_cap, now, counts, live);
+                    uint32_t arena_cap, double now, JoinCounts* counts, unsigned long long* live, uint8_t* pool,
+                    uint32_t* pool_ring, uint32_t pool_mask, hipStream_t s) {
+  if (old_cap)
+    hipLaunchKernelGGL(k_rebuild, dim3((old_cap + TB - 1) / TB), dim3(TB), 0, s, old, old_cap, fresh, fresh_mask, arena,
+                       arena_cap, now, counts, live, pool, pool_ring, pool_mask);
+  hipLaunchKernelGGL(k_pool_fix, dim3(1), dim3(1), 0, s, counts);
+}
+
+void apm_dj_pool_init(uint32_t* ring, uint32_t n, JoinCounts* counts, hipStream_t s) {
+  hipLaunchKernelGGL(k_pool_init, dim3((n + TB - 1) / TB), dim3(TB), 0, s, ring, n, counts);
+}
+
+void apm_dj_pool_grow(const uint32_t* old_ring, uint32_t old_mask, uint32_t* fresh_ring, uint32_t old_n, uint32_t new_n,
+                      JoinCounts* counts, hipStream_t s) {
+  hipLaunchKernelGGL(k_pool_grow, dim3((new_n + TB - 1) / TB), dim3(TB), 0, s, old_ring, old_mask, fresh_ring, old_n,
+                     new_n, counts);
+  hipLaunchKernelGGL(k_pool_grow_set, dim3(1), dim3(1), 0, s, counts, old_n, new_n);
+}
+
+void apm_dj_arena_grow(const NeedEnt* old, uint32_t old_cap, NeedEnt* fresh, uint32_t fresh_cap, uint64_t lo,
+                       uint64_t hi, KeyState* table, uint32_t table_cap, hipStream_t s) {
+  const uint64_t n = hi - lo;
+  const uint64_t threads = n * (sizeof(NeedEnt) / 16);
+  if (n) hipLaunchKernelGGL(k_arena_move, dim3((unsigned)((threads + TB - 1) / TB)), dim3(TB), 0, s, old, old_cap, fresh,
+                            fresh_cap, lo, n);
+  hipLaunchKernelGGL(k_arena_remap, dim3((table_cap + TB - 1) / TB), dim3(TB), 0, s, table, table_cap, old, old_cap,
+                     fresh_cap, lo, hi);
 }
 
 int apm_dj_gather_plan(const int64_t* gid, int64_t n_upper, const int64_t* d_n, uint32_t* lens, uint32_t* offs,

@@ -69,6 +69,9 @@ struct DJArgs {
   uint32_t arena_cap;             // power of two
   uint64_t arena_base;            // virtual index of this batch's region start
   uint32_t arena_limit;           // entries this batch may allocate
+  uint8_t* pool;                  // chain blocks (CHAIN_BLK bytes each)
+  uint32_t* pool_ring;            // free block indices (ring of pool_mask + 1)
+  uint32_t pool_mask;
   // expiring need entries: virtual ranges [lo, hi) of the regions that expire now
   const uint64_t* exp_lo;         // device
   const uint64_t* exp_hi;
@@ -104,6 +107,7 @@ struct DJFormatArgs {
   const uint8_t* hbuf;
   const NeedEnt* arena;
   uint32_t arena_cap;
+  const uint8_t* pool;            // chain blocks (long logIds of need entries)
   // per tx {line length, stats flag, length if not to_db, length if to_db} and their scans
   uint32_t* lens;                 // [n_out + 1] x 4
   uint32_t* offs;                 // [n_out + 1] x 4 (exclusive)
@@ -142,9 +146,20 @@ int apm_dj_plan(apm::DJFormatArgs* f, hipStream_t s);
 // text into the ring, stats arrays, rollover candidates, unresolved series, optional streams.
 int apm_dj_write(apm::DJFormatArgs* f, uint32_t n_stats, hipStream_t s);
 // key-table rebuild: live entries of `old` reinserted into `fresh` (zeroed by the caller).
+// Dropped keys / expired partials free their chain blocks into the pool (pool may be null when
+// `now` is -inf: nothing is dropped).
 void apm_dj_rebuild(const apm::KeyState* old, uint32_t old_cap, apm::KeyState* fresh, uint32_t fresh_mask,
                     const apm::NeedEnt* arena, uint32_t arena_cap, double now, apm::JoinCounts* counts,
-                    unsigned long long* live, hipStream_t s);
+                    unsigned long long* live, uint8_t* pool, uint32_t* pool_ring, uint32_t pool_mask, hipStream_t s);
+// chain-block pool: ring = identity (all `n` blocks free), counters head = 0, tail = ptail = n
+void apm_dj_pool_init(uint32_t* ring, uint32_t n, apm::JoinCounts* counts, hipStream_t s);
+// pool growth: the free entries of the old ring, then blocks [old_n, new_n), into `fresh_ring`
+void apm_dj_pool_grow(const uint32_t* old_ring, uint32_t old_mask, uint32_t* fresh_ring, uint32_t old_n, uint32_t new_n,
+                      apm::JoinCounts* counts, hipStream_t s);
+// need-arena growth: live entries [lo, hi) (virtual) move to their slots in the bigger arena, and
+// every key's `need` index follows its entry
+void apm_dj_arena_grow(const apm::NeedEnt* old, uint32_t old_cap, apm::NeedEnt* fresh, uint32_t fresh_cap, uint64_t lo,
+                       uint64_t hi, apm::KeyState* table, uint32_t table_cap, hipStream_t s);
 // released lines (gids = ring pos << 20 | len): line lengths + offsets of the first *d_n of
 // n_upper gids (d_n null: all; offs[n_upper] = total bytes), then the copy into `out`
 int apm_dj_gather_plan(const int64_t* gid, int64_t n_upper, const int64_t* d_n, uint32_t* lens, uint32_t* offs,

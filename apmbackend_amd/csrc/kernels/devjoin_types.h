@@ -84,6 +84,11 @@ struct HostOp {
 static_assert(sizeof(HostOp) == 96, "HostOp layout");
 
 // ------------------------------------------------------------------------------ state
+// The reference caches are unbounded JS Maps (recordCache / needNumRecordCache `maxKeys: -1`,
+// :211-218): a logId may hold any number of open partials and parked records, and logIds have
+// any length.  The common case lives inline in the table slot / arena entry; everything beyond
+// it goes to chains of 256-byte blocks in a device block pool (index + 1 links, 0 = none),
+// allocated and freed by the join kernels (ChainPool below).  Nothing is dropped.
 constexpr int KS_PARTS = 5;
 struct KeyState {  // 128 B, one hash-table slot
   uint64_t key;    // gkey, 0 = empty
@@ -91,10 +96,11 @@ struct KeyState {  // 128 B, one hash-table slot
   double acct_exp;  // acctCache entry live iff acct_exp >= now (-inf: none)
   double rec_exp;   // recordCache entry live iff rec_exp >= now
   int32_t need;     // NeedEnt arena index (-1 none)
-  int32_t n_part;
+  int32_t n_part;   // open partials: [0, KS_PARTS) inline, the rest in the PartBlk chain
   uint64_t part_svc[KS_PARTS];
   double part_start[KS_PARTS];
-  uint64_t pad;
+  int32_t pblk;     // PartBlk chain (block index + 1, 0 none)
+  int32_t pad;
 };
 static_assert(sizeof(KeyState) == 128, "KeyState layout");
 
@@ -111,14 +117,41 @@ struct NeedEnt {    // 512 B
   double exp;
   uint64_t created;  // (batch_no << 28) | line
   int32_t server;
-  int32_t n;         // items
-  int32_t lid_len;
+  int32_t n;         // items: [0, NEED_ITEMS) inline, the rest in the NeedBlk chain (insertion order)
+  int32_t lid_len;   // full logId length: [0, NEED_LID) inline, the rest in the LidBlk chain
   int32_t pad;
   char lid[NEED_LID];
   NeedItem items[NEED_ITEMS];
-  uint8_t tail[56];
+  int32_t iblk;      // NeedBlk chain (block index + 1, 0 none)
+  int32_t lblk;      // LidBlk chain
+  uint64_t vidx;     // virtual arena index (arena growth remaps the table's `need` through it)
+  uint8_t tail[40];
 };
 static_assert(sizeof(NeedEnt) == 512, "NeedEnt layout");
+
+// ---- chain blocks (256 B, one pool)
+constexpr int CHAIN_BLK = 256;
+constexpr int PBLK_N = 15;   // partials per block
+constexpr int NBLK_N = 5;    // parked records per block
+constexpr int LBLK_N = 240;  // logId bytes per block
+struct PartBlk {
+  int32_t next;
+  int32_t pad[3];
+  uint64_t svc[PBLK_N];
+  double start[PBLK_N];
+};
+struct NeedBlk {
+  int32_t next;
+  int32_t pad[3];
+  NeedItem items[NBLK_N];
+};
+struct LidBlk {
+  int32_t next;
+  int32_t pad[3];
+  char b[LBLK_N];
+};
+static_assert(sizeof(PartBlk) == CHAIN_BLK && sizeof(NeedBlk) == CHAIN_BLK && sizeof(LidBlk) == CHAIN_BLK,
+              "chain block layout");
 
 // A completed transaction (outputRecord :264-290) before formatting, 64 B.
 enum : uint8_t { LID_NONE = 0, LID_BATCH = 1, LID_HOST = 2, LID_NEED = 3 };
@@ -191,6 +224,10 @@ struct JoinCounts {
   // sticky counters
   unsigned long long ejb_unmatched, partial_overflow, need_overflow, expired_partials, need_expired,
       invalid_acct, table_full, key_probe_max;
+  // chain-block pool: free-index ring positions (virtual).  Allocation takes [head, tail); frees
+  // append at ptail; k_pool_fix publishes them (tail = ptail) after the kernels that allocate.
+  unsigned long long pool_head, pool_tail, pool_ptail, pool_fail;
+  unsigned long long chain_parts, chain_items, chain_lids;  // blocks ever allocated, by kind
 };
 
 }  // namespace apm

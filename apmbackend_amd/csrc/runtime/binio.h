@@ -23,7 +23,7 @@ namespace apm {
 
 // 3: join section carries the join mode (host / GPU); 4: node-wide server order; 5: rings in their own
 // trailing section (full or dirty rows, for incremental checkpoints) + NaN horizons + an opaque extra
-constexpr uint32_t kCkptVersion = 5;
+constexpr uint32_t kCkptVersion = 6;
 
 class BinWriter {
  public:

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <chrono>
 #include <climits>
+#include <cstddef>
 #include <cstring>
 #include <stdexcept>
 
@@ -51,6 +52,15 @@ void* DeviceJoin::dmalloc(size_t bytes) {
   return p;
 }
 
+// the join stream must be idle (callers synchronize first)
+void DeviceJoin::dfree(void* p, size_t bytes) {
+  if (!p) return;
+  auto it = std::find(allocs_.begin(), allocs_.end(), p);
+  if (it != allocs_.end()) allocs_.erase(it);
+  HIP_OK(hipFree(p));
+  device_bytes_ -= (bytes + 255) & ~(size_t)255;
+}
+
 DeviceJoin::DeviceJoin(const DevJoinConfig& cfg, Dictionary* dict, const std::vector<FileInfo>* files,
                        const std::vector<std::string>* servers)
     : cfg_(cfg), dict_(dict), files_(files), servers_(servers) {
@@ -81,7 +91,8 @@ DeviceJoin::DeviceJoin(const DevJoinConfig& cfg, Dictionary* dict, const std::ve
     s.d_tx_gid = (int64_t*)dmalloc((size_t)out_cap_ * 8);
     HIP_OK(hipEventCreateWithFlags(&s.free_ev, hipEventDisableTiming));
   }
-  table_cap_ = 1u << cfg_.table_bits;
+  table_bits_ = cfg_.table_bits;
+  table_cap_ = 1u << table_bits_;
   d_table_ = (KeyState*)dmalloc((size_t)table_cap_ * sizeof(KeyState));
   d_reg_ = (RegSlot*)dmalloc(((size_t)1 << cfg_.reg_bits) * sizeof(RegSlot));
   miss_cap_ = E;
@@ -114,14 +125,22 @@ DeviceJoin::DeviceJoin(const DevJoinConfig& cfg, Dictionary* dict, const std::ve
   HIP_OK(hipHostMalloc((void**)&h_cand_, (size_t)out_cap_ * 4, hipHostMallocDefault));
   HIP_OK(hipHostMalloc((void**)&h_cand_bucket_, (size_t)out_cap_ * 8, hipHostMallocDefault));
   HIP_OK(hipHostMalloc((void**)&h_unres_, (size_t)out_cap_ * 8, hipHostMallocDefault));
-  tmp_bytes_ = std::max(apm_dj_tmp_bytes(E, out_cap_, cfg_.table_bits), apm_dj_tmp_bytes(cfg_.arena_cap, out_cap_, cfg_.table_bits));
-  d_tmp_ = dmalloc(tmp_bytes_);
+  ensure_tmp();
   sel_tmp_bytes_ = apm_dj_tmp_bytes(E, 1024, 8);
   d_sel_tmp_ = dmalloc(sel_tmp_bytes_);
   d_counts_ = (JoinCounts*)dmalloc(sizeof(JoinCounts));
   HIP_OK(hipHostMalloc((void**)&h_counts_, sizeof(JoinCounts), hipHostMallocDefault));
   std::memset(h_counts_, 0, sizeof(JoinCounts));
   d_live_ = (unsigned long long*)dmalloc(64);
+  HIP_OK(hipHostMalloc((void**)&h_live_, 64, hipHostMallocDefault));
+  // chain-block pool (overflow of the per-key partial / parked-record / logId storage); grows
+  // before any batch whose worst case exceeds its free blocks
+  pool_n_ = (uint32_t)pow2_at_least(cfg_.pool_blocks ? std::max<uint32_t>(cfg_.pool_blocks, 1024)
+                                                   : std::max<uint32_t>(E / 2, 1u << 16));
+  d_pool_ = (uint8_t*)dmalloc((size_t)pool_n_ * CHAIN_BLK);
+  d_pool_ring_ = (uint32_t*)dmalloc((size_t)pool_n_ * 4);
+  apm_dj_pool_init(d_pool_ring_, pool_n_, d_counts_, stream_);
+  h_counts_->pool_tail = h_counts_->pool_ptail = pool_n_;
   d_ops_ = (JOp*)dmalloc((size_t)E * sizeof(JOp));
   d_soap_code_ = (uint8_t*)dmalloc(E);
   d_soap_num_ = (double*)dmalloc((size_t)E * 8);
@@ -157,7 +176,7 @@ DeviceJoin::~DeviceJoin() {
     hipEventDestroy(s.free_ev);
   }
   hipHostFree(h_miss_); hipHostFree(h_exp_); hipHostFree(h_rawtab_); hipHostFree(h_reg_fill_);
-  hipHostFree(h_cand_); hipHostFree(h_cand_bucket_); hipHostFree(h_unres_); hipHostFree(h_counts_);
+  hipHostFree(h_cand_); hipHostFree(h_cand_bucket_); hipHostFree(h_unres_); hipHostFree(h_counts_); hipHostFree(h_live_);
   if (h_hops_) hipHostFree(h_hops_);
   if (h_hbuf_) hipHostFree(h_hbuf_);
   if (h_txt_) hipHostFree(h_txt_);
@@ -633,24 +652,125 @@ void DeviceJoin::release_slot(int k, hipStream_t stats_stream) {
   sl_[k].used = true;
 }
 
-void DeviceJoin::maybe_rebuild(double now, hipStream_t s) {
-  if ((keys_live_ + keys_since_rebuild_) * 2 < table_cap_) return;
-  // reinsert the live keys (acct / record not expired, or a live need entry) into a fresh table
-  KeyState* fresh = nullptr;
-  HIP_OK(hipMalloc((void**)&fresh, (size_t)table_cap_ * sizeof(KeyState)));
-  HIP_OK(hipMemsetAsync(fresh, 0, (size_t)table_cap_ * sizeof(KeyState), s));
-  HIP_OK(hipMemsetAsync(d_live_, 0, 8, s));
-  apm_dj_rebuild(d_table_, table_cap_, fresh, table_cap_ - 1, d_arena_, cfg_.arena_cap, now, d_counts_, d_live_, s);
-  unsigned long long live = 0;
-  HIP_OK(hipMemcpyAsync(&live, d_live_, 8, hipMemcpyDeviceToHost, s));
-  HIP_OK(hipStreamSynchronize(s));
-  for (auto& p : allocs_) if (p == d_table_) p = fresh;
-  HIP_OK(hipFree(d_table_));
+void DeviceJoin::ensure_tmp() {
+  const uint32_t E = std::max<uint32_t>(cfg_.max_events, 1024);
+  const size_t need = std::max(apm_dj_tmp_bytes(E, out_cap_, table_bits_), apm_dj_tmp_bytes(cfg_.arena_cap, out_cap_, table_bits_));
+  if (need <= tmp_bytes_ && d_tmp_) return;
+  if (d_tmp_) {
+    HIP_OK(hipStreamSynchronize(stream_));
+    dfree(d_tmp_, tmp_bytes_);
+  }
+  tmp_bytes_ = need;
+  d_tmp_ = dmalloc(tmp_bytes_);
+}
+
+// Reinsert the live keys (acct / record not expired, or a live need entry) into a clean table of
+// `new_cap` slots.  Same size: the spare buffer (no allocation on the ingest path).
+void DeviceJoin::rebuild_table(double now, uint32_t new_cap) {
+  hipStream_t st = stream_;
+  KeyState* fresh;
+  const bool same = new_cap == table_cap_;
+  if (same && d_table_spare_) fresh = d_table_spare_;
+  else fresh = (KeyState*)dmalloc((size_t)new_cap * sizeof(KeyState));
+  HIP_OK(hipMemsetAsync(fresh, 0, (size_t)new_cap * sizeof(KeyState), st));
+  HIP_OK(hipMemsetAsync(d_live_, 0, 8, st));
+  apm_dj_rebuild(d_table_, table_cap_, fresh, new_cap - 1, d_arena_, cfg_.arena_cap, now, d_counts_, d_live_, d_pool_,
+                 d_pool_ring_, pool_n_ - 1, st);
+  HIP_OK(hipMemcpyAsync(h_live_, d_live_, 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  if (same) {
+    d_table_spare_ = d_table_;
+  } else {
+    dfree(d_table_, (size_t)table_cap_ * sizeof(KeyState));
+    if (d_table_spare_) dfree(d_table_spare_, (size_t)table_cap_ * sizeof(KeyState));
+    d_table_spare_ = nullptr;
+    ++table_grows_;
+  }
   d_table_ = fresh;
-  keys_live_ = live;
+  table_cap_ = new_cap;
+  table_bits_ = 0;
+  while ((1u << table_bits_) < table_cap_) ++table_bits_;
+  keys_live_ = *h_live_;
   keys_since_rebuild_ = 0;
-  if (keys_live_ * 2 >= table_cap_)
-    throw std::runtime_error("device join: live join keys exceed half of gpu.joinTableSlots");
+  ++table_rebuilds_;
+  ensure_tmp();  // the grouping sort's key width follows the table
+}
+
+// Need entries at virtual [lo, arena_head_) move to the same virtual slots of a bigger ring; the
+// table's `need` links follow them (through NeedEnt::vidx).
+void DeviceJoin::grow_arena(uint32_t new_cap, uint64_t lo) {
+  hipStream_t st = stream_;
+  NeedEnt* fresh = (NeedEnt*)dmalloc((size_t)new_cap * sizeof(NeedEnt));
+  apm_dj_arena_grow(d_arena_, cfg_.arena_cap, fresh, new_cap, lo, arena_head_, d_table_, table_cap_, st);
+  HIP_OK(hipStreamSynchronize(st));
+  dfree(d_arena_, (size_t)cfg_.arena_cap * sizeof(NeedEnt));
+  d_arena_ = fresh;
+  // expiry scratch is sized by the arena
+  for (void* p : {(void*)d_exp_key_, (void*)d_exp_key_sorted_}) dfree(p, ((size_t)exp_cap_ + 1) * 8);
+  for (void* p : {(void*)d_exp_idx_, (void*)d_exp_idx_sorted_, (void*)d_exp_cnt_, (void*)d_exp_pos_})
+    dfree(p, ((size_t)exp_cap_ + 1) * 4);
+  cfg_.arena_cap = new_cap;
+  exp_cap_ = new_cap;
+  d_exp_key_ = (uint64_t*)dmalloc(((size_t)exp_cap_ + 1) * 8);
+  d_exp_key_sorted_ = (uint64_t*)dmalloc(((size_t)exp_cap_ + 1) * 8);
+  d_exp_idx_ = (uint32_t*)dmalloc(((size_t)exp_cap_ + 1) * 4);
+  d_exp_idx_sorted_ = (uint32_t*)dmalloc(((size_t)exp_cap_ + 1) * 4);
+  d_exp_cnt_ = (uint32_t*)dmalloc(((size_t)exp_cap_ + 1) * 4);
+  d_exp_pos_ = (uint32_t*)dmalloc(((size_t)exp_cap_ + 1) * 4);
+  ensure_tmp();
+  ++arena_grows_;
+}
+
+uint64_t DeviceJoin::pool_avail(bool exact) {
+  if (exact) {
+    HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost, stream_));
+    HIP_OK(hipStreamSynchronize(stream_));
+  }
+  return h_counts_->pool_tail - h_counts_->pool_head;
+}
+
+void DeviceJoin::grow_pool(uint64_t need_free) {
+  hipStream_t st = stream_;
+  const uint64_t avail = pool_avail(true);
+  uint64_t n = pool_n_;
+  while (avail + (n - pool_n_) < need_free) n *= 2;
+  if (n >= (1ull << 31)) throw std::runtime_error("device join: chain pool beyond 2^31 blocks");
+  uint8_t* pool = (uint8_t*)dmalloc((size_t)n * CHAIN_BLK);
+  uint32_t* ring = (uint32_t*)dmalloc((size_t)n * 4);
+  HIP_OK(hipMemcpyAsync(pool, d_pool_, (size_t)pool_n_ * CHAIN_BLK, hipMemcpyDeviceToDevice, st));
+  apm_dj_pool_grow(d_pool_ring_, pool_n_ - 1, ring, pool_n_, (uint32_t)n, d_counts_, st);
+  HIP_OK(hipStreamSynchronize(st));
+  dfree(d_pool_, (size_t)pool_n_ * CHAIN_BLK);
+  dfree(d_pool_ring_, (size_t)pool_n_ * 4);
+  d_pool_ = pool;
+  d_pool_ring_ = ring;
+  pool_n_ = (uint32_t)n;
+  pool_avail(true);
+  ++pool_grows_;
+}
+
+void DeviceJoin::ensure_capacity(uint32_t n_ev, uint64_t bytes, double now) {
+  // key table: every op of the batch may claim a new key
+  if ((keys_live_ + keys_since_rebuild_ + n_ev) * 2 > table_cap_) {
+    rebuild_table(now, table_cap_);
+    uint64_t cap = table_cap_;
+    while ((keys_live_ + n_ev) * 2 > cap) cap *= 2;
+    if (cap >= (1ull << 31)) throw std::runtime_error("device join: key table beyond 2^31 slots");
+    if (cap != table_cap_) rebuild_table(now, (uint32_t)cap);
+  }
+  // need arena: every op may open one entry; entries of the regions expiring in this batch stay
+  // untouched until k_write printed their logIds
+  {
+    const uint64_t low = regions_.empty() ? arena_head_ : regions_.front().lo;
+    const uint64_t used = arena_head_ - low;
+    uint64_t cap = cfg_.arena_cap;
+    while (cap - used < n_ev) cap *= 2;
+    if (cap >= (1ull << 31)) throw std::runtime_error("device join: need arena beyond 2^31 entries");
+    if (cap != cfg_.arena_cap) grow_arena((uint32_t)cap, low);
+  }
+  // chain pool: one block per op (a partial or a parked record) + the logId bytes of new entries
+  const uint64_t need = 2ull * n_ev + bytes / LBLK_N + 64;
+  if (pool_avail(false) < need && pool_avail(true) < need) grow_pool(need);
 }
 
 void DeviceJoin::prepass_ahead(int k, const uint8_t* hb, const ParallelFor& parallel) {
@@ -660,13 +780,12 @@ void DeviceJoin::prepass_ahead(int k, const uint8_t* hb, const ParallelFor& para
   ahead_k_ = k;
 }
 
-void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64_t batch_no, bool want_tx,
-                     bool want_db, DevJoinBatch& out, const ParallelFor& parallel,
+void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, double now, uint64_t batch_no,
+                     bool want_tx, bool want_db, DevJoinBatch& out, const ParallelFor& parallel,
                      const std::function<void()>* meanwhile) {
   Slot& s = sl_[k];
   hipStream_t st = stream_;
   if (n_ev > cfg_.max_events) throw std::runtime_error("device join: more events than maxLinesPerBatch");
-  if (s.used) HIP_OK(hipStreamWaitEvent(st, s.free_ev, 0));  // the stats thread is done with the slot
   events_ += n_ev;
   phase_t[0] = clock_ms();
   // ---- host pre-pass (audit blocks, PM_HOST lines)
@@ -729,6 +848,10 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64
     HIP_OK(hipStreamSynchronize(st));
     files_uploaded_ = files_->size();
   }
+  ensure_capacity(n_ev, n_bytes + hbuf_.size(), now);
+  span("u.capacity");
+  const uint64_t arena_low = regions_.empty() ? arena_head_ : regions_.front().lo;  // before expiry
+  const uint32_t arena_limit = (uint32_t)((uint64_t)cfg_.arena_cap - (arena_head_ - arena_low));
   // ---- needNumRecordCache regions whose TTL passed (front of the creation-ordered FIFO)
   uint32_t n_reg = 0, n_exp = 0;
   while (!regions_.empty() && regions_.front().exp < now && n_reg < 4096) {
@@ -743,9 +866,6 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64
     HIP_OK(hipMemcpyAsync(d_exp_hi_, h_exp_ + 4096, (size_t)n_reg * 8, hipMemcpyHostToDevice, st));
   }
   span("u.files+exp");
-  const uint64_t arena_low = regions_.empty() ? arena_head_ : regions_.front().lo;
-  const uint64_t arena_free = (uint64_t)cfg_.arena_cap - (arena_head_ - arena_low);
-  const uint32_t arena_limit = (uint32_t)std::min<uint64_t>(arena_free, cfg_.arena_cap / 2);
   // ---- join
   DJArgs& a = a_;
   a = DJArgs{};
@@ -761,7 +881,8 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64
   a.soap_state = d_soap_;
   a.op_slot = d_op_slot_; a.op_slot_sorted = d_op_slot_sorted_; a.op_idx = d_op_idx_; a.op_idx_sorted = d_op_idx_sorted_;
   a.tmp = d_tmp_; a.tmp_bytes = tmp_bytes_;
-  a.table = d_table_; a.table_mask = table_cap_ - 1; a.table_bits = cfg_.table_bits;
+  a.table = d_table_; a.table_mask = table_cap_ - 1; a.table_bits = table_bits_;
+  a.pool = d_pool_; a.pool_ring = d_pool_ring_; a.pool_mask = pool_n_ - 1;
   a.reg = d_reg_; a.reg_mask = (1u << cfg_.reg_bits) - 1; a.miss = d_miss_; a.miss_cap = miss_cap_;
   a.arena = d_arena_; a.arena_cap = cfg_.arena_cap; a.arena_base = arena_head_; a.arena_limit = arena_limit;
   a.exp_lo = d_exp_lo_; a.exp_hi = d_exp_hi_; a.n_exp_regions = n_reg; a.n_exp_entries = n_exp;
@@ -769,6 +890,9 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64
   a.exp_idx_sorted = d_exp_idx_sorted_; a.exp_cnt = d_exp_cnt_; a.exp_pos = d_exp_pos_;
   a.out_cnt = d_out_cnt_; a.out_pos = d_out_pos_; a.stage = d_stage_; a.ovf = d_ovf_;
   a.out = d_out_; a.out_cap = out_cap_; a.counts = d_counts_;
+  // the stats thread is done with the slot's hand-off arrays (after the capacity upkeep, which
+  // may synchronize this stream and must not wait for the stats thread)
+  if (s.used) HIP_OK(hipStreamWaitEvent(st, s.free_ev, 0));
   phase_t[2] = clock_ms();
   if (apm_dj_join(&a, st) != 0) throw std::runtime_error("device join: scan scratch too small");
   HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost, st));
@@ -792,7 +916,7 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64
   f = DJFormatArgs{};
   f.out = d_out_; f.n_out = c.n_out; f.reg = d_reg_; f.reg_mask = (1u << cfg_.reg_bits) - 1;
   f.raw = d_rawtab_; f.raw_series = d_raw_series_; f.raw_first = d_raw_first_; f.names = d_names_;
-  f.bytes = s.d_bytes; f.hbuf = d_hbuf_; f.arena = d_arena_; f.arena_cap = cfg_.arena_cap;
+  f.bytes = s.d_bytes; f.hbuf = d_hbuf_; f.arena = d_arena_; f.arena_cap = cfg_.arena_cap; f.pool = d_pool_;
   f.lens = d_lens_; f.offs = d_offs_; f.ring = d_ring_; f.ring_cap = cfg_.ring_bytes;
   f.tx = s.d_tx; f.tx_raw = s.d_tx_raw; f.tx_gid = s.d_tx_gid; f.tx_bucket = d_bucket_; f.tx_bmax = d_bmax_;
   f.cand = d_cand_; f.cand_bucket = d_cand_bucket_; f.unresolved = d_unres_;
@@ -868,7 +992,6 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, double now, uint64
   if (want_db) out.text_db.assign(h_txt_ + (want_tx ? c2.tx_text_bytes : 0), c2.db_text_bytes);
   tx_ += c3.n_out;
   tx_db_ += c3.n_db;
-  maybe_rebuild(now, st);
   phase_t[8] = clock_ms();
 }
 
@@ -884,6 +1007,20 @@ JoinCounters DeviceJoin::counters() const {
   t.invalid_acct = c.invalid_acct + host_invalid_acct_;
   t.audit_errors = audit_errors_;
   t.host_fallback = host_pm_;  // lines the parser deferred (audit lines are host-resolved by design)
+  t.partial_overflow = c.partial_overflow;
+  t.need_overflow = c.need_overflow;
+  t.table_full = c.table_full;
+  t.pool_exhausted = c.pool_fail;
+  t.chain_partial_blocks = c.chain_parts;
+  t.chain_need_blocks = c.chain_items;
+  t.chain_logid_blocks = c.chain_lids;
+  t.table_slots = table_cap_;
+  t.table_grows = table_grows_;
+  t.table_rebuilds = table_rebuilds_;
+  t.need_arena_entries = cfg_.arena_cap;
+  t.arena_grows = arena_grows_;
+  t.chain_pool_blocks = pool_n_;
+  t.pool_grows = pool_grows_;
   return t;
 }
 
@@ -895,23 +1032,54 @@ void DeviceJoin::save(BinWriter& w) {
   w.pod(*h_counts_);
   for (uint64_t v : {events_, tx_, tx_db_, audit_errors_, host_pm_, host_invalid_acct_, host_events_}) w.pod(v);
   // key table: live (non-empty) slots only
+  std::vector<KeyState> live;
   {
-    std::vector<KeyState> tab(table_cap_), live;
+    std::vector<KeyState> tab(table_cap_);
     HIP_OK(hipMemcpy(tab.data(), d_table_, (size_t)table_cap_ * sizeof(KeyState), hipMemcpyDeviceToHost));
     for (const KeyState& k : tab) if (k.key) live.push_back(k);
-    w.vec(live);
   }
-  // needNumRecordCache regions + their arena entries
+  // needNumRecordCache regions + their arena entries (arena capacity first: the table's `need`
+  // links are physical slots of an arena of that size)
+  const uint64_t lo = regions_.empty() ? arena_head_ : regions_.front().lo;
+  std::vector<NeedEnt> ents((size_t)(arena_head_ - lo));
+  for (uint64_t v = lo; v < arena_head_; ++v)
+    HIP_OK(hipMemcpy(&ents[(size_t)(v - lo)], d_arena_ + (v & (cfg_.arena_cap - 1)), sizeof(NeedEnt), hipMemcpyDeviceToHost));
+  // chain blocks reachable from the live state, renumbered 1..n in the file
+  struct Blk { uint8_t b[CHAIN_BLK]; };
+  std::vector<Blk> blocks;
+  {
+    bool any = false;
+    for (const KeyState& k : live) any |= k.pblk != 0;
+    for (const NeedEnt& e : ents) any |= e.iblk != 0 || e.lblk != 0;
+    if (any) {
+      std::vector<Blk> pool(pool_n_);
+      HIP_OK(hipMemcpy(pool.data(), d_pool_, (size_t)pool_n_ * CHAIN_BLK, hipMemcpyDeviceToHost));
+      auto copy_chain = [&](int32_t b1) -> int32_t {
+        int32_t head = 0, prev = 0;
+        for (; b1; b1 = *(const int32_t*)pool[(size_t)b1 - 1].b) {
+          blocks.push_back(pool[(size_t)b1 - 1]);
+          const int32_t nb = (int32_t)blocks.size();
+          *(int32_t*)blocks.back().b = 0;
+          if (prev) *(int32_t*)blocks[(size_t)prev - 1].b = nb;
+          else head = nb;
+          prev = nb;
+        }
+        return head;
+      };
+      for (KeyState& k : live) k.pblk = copy_chain(k.pblk);
+      for (NeedEnt& e : ents) {
+        e.iblk = e.key ? copy_chain(e.iblk) : 0;
+        e.lblk = e.key ? copy_chain(e.lblk) : 0;
+      }
+    }
+  }
+  w.vec(live);
+  w.pod(cfg_.arena_cap);
   w.pod(arena_head_);
   w.pod<uint64_t>(regions_.size());
   for (const Region& r : regions_) { w.pod(r.lo); w.pod(r.hi); w.pod(r.exp); }
-  {
-    const uint64_t lo = regions_.empty() ? arena_head_ : regions_.front().lo;
-    std::vector<NeedEnt> ents((size_t)(arena_head_ - lo));
-    for (uint64_t v = lo; v < arena_head_; ++v)
-      HIP_OK(hipMemcpy(&ents[(size_t)(v - lo)], d_arena_ + (v & (cfg_.arena_cap - 1)), sizeof(NeedEnt), hipMemcpyDeviceToHost));
-    w.vec(ents);
-  }
+  w.vec(ents);
+  w.vec(blocks);
   // SOAP contexts of every file
   {
     std::vector<SoapState> ss(files_->size());
@@ -954,20 +1122,54 @@ void DeviceJoin::load(BinReader& rd) {
   for (uint64_t* v : {&events_, &tx_, &tx_db_, &audit_errors_, &host_pm_, &host_invalid_acct_, &host_events_}) rd.pod(*v);
   {
     auto live = rd.vec<KeyState>();
-    if (live.size() * 2 > table_cap_) throw std::runtime_error("checkpoint: join keys exceed gpu.joinTableSlots");
+    uint64_t cap = table_cap_;
+    while (live.size() * 2 > cap) cap *= 2;  // the saving process may have grown its table
+    HIP_OK(hipStreamSynchronize(st));
+    if (cap != table_cap_) {
+      dfree(d_table_, (size_t)table_cap_ * sizeof(KeyState));
+      if (d_table_spare_) dfree(d_table_spare_, (size_t)table_cap_ * sizeof(KeyState));
+      d_table_spare_ = nullptr;
+      table_cap_ = (uint32_t)cap;
+      table_bits_ = 0;
+      while ((1u << table_bits_) < table_cap_) ++table_bits_;
+      d_table_ = (KeyState*)dmalloc((size_t)table_cap_ * sizeof(KeyState));
+      ensure_tmp();
+    } else {
+      HIP_OK(hipMemsetAsync(d_table_, 0, (size_t)table_cap_ * sizeof(KeyState), st));
+    }
     if (!live.empty()) {
       KeyState* tmp = nullptr;
       HIP_OK(hipMalloc((void**)&tmp, live.size() * sizeof(KeyState)));
       HIP_OK(hipMemcpy(tmp, live.data(), live.size() * sizeof(KeyState), hipMemcpyHostToDevice));
       HIP_OK(hipMemsetAsync(d_live_, 0, 8, st));
-      // every saved slot is reinserted (now = -inf keeps them all)
+      // every saved slot is reinserted (now = -inf keeps them all, chains included)
       apm_dj_rebuild(tmp, (uint32_t)live.size(), d_table_, table_cap_ - 1, d_arena_, cfg_.arena_cap, -__builtin_inf(),
-                     d_counts_, d_live_, st);
+                     d_counts_, d_live_, d_pool_, d_pool_ring_, pool_n_ - 1, st);
       HIP_OK(hipStreamSynchronize(st));
       HIP_OK(hipFree(tmp));
     }
     keys_live_ = live.size();
     keys_since_rebuild_ = 0;
+  }
+  {
+    const uint32_t saved_cap = rd.pod<uint32_t>();
+    if (saved_cap != cfg_.arena_cap) {  // the `need` links are slots of the saver's arena size
+      HIP_OK(hipStreamSynchronize(st));
+      dfree(d_arena_, (size_t)cfg_.arena_cap * sizeof(NeedEnt));
+      cfg_.arena_cap = saved_cap;
+      d_arena_ = (NeedEnt*)dmalloc((size_t)cfg_.arena_cap * sizeof(NeedEnt));
+      for (void* p : {(void*)d_exp_key_, (void*)d_exp_key_sorted_}) dfree(p, ((size_t)exp_cap_ + 1) * 8);
+      for (void* p : {(void*)d_exp_idx_, (void*)d_exp_idx_sorted_, (void*)d_exp_cnt_, (void*)d_exp_pos_})
+        dfree(p, ((size_t)exp_cap_ + 1) * 4);
+      exp_cap_ = saved_cap;
+      d_exp_key_ = (uint64_t*)dmalloc(((size_t)exp_cap_ + 1) * 8);
+      d_exp_key_sorted_ = (uint64_t*)dmalloc(((size_t)exp_cap_ + 1) * 8);
+      d_exp_idx_ = (uint32_t*)dmalloc(((size_t)exp_cap_ + 1) * 4);
+      d_exp_idx_sorted_ = (uint32_t*)dmalloc(((size_t)exp_cap_ + 1) * 4);
+      d_exp_cnt_ = (uint32_t*)dmalloc(((size_t)exp_cap_ + 1) * 4);
+      d_exp_pos_ = (uint32_t*)dmalloc(((size_t)exp_cap_ + 1) * 4);
+      ensure_tmp();
+    }
   }
   rd.pod(arena_head_);
   regions_.clear();
@@ -982,6 +1184,29 @@ void DeviceJoin::load(BinReader& rd) {
     if (ents.size() != arena_head_ - lo) throw std::runtime_error("checkpoint: need arena size mismatch");
     for (uint64_t v = lo; v < arena_head_; ++v)
       HIP_OK(hipMemcpy(d_arena_ + (v & (cfg_.arena_cap - 1)), &ents[(size_t)(v - lo)], sizeof(NeedEnt), hipMemcpyHostToDevice));
+  }
+  {
+    // chain blocks: saved 1..n, loaded into blocks 0..n-1 of a fresh pool whose first n ring
+    // entries (identity) are taken
+    struct Blk { uint8_t b[CHAIN_BLK]; };
+    auto blocks = rd.vec<Blk>();
+    HIP_OK(hipStreamSynchronize(st));
+    uint64_t n = pool_n_;
+    while (n < 2 * blocks.size() + (1u << 16)) n *= 2;
+    if (n != pool_n_) {
+      dfree(d_pool_, (size_t)pool_n_ * CHAIN_BLK);
+      dfree(d_pool_ring_, (size_t)pool_n_ * 4);
+      pool_n_ = (uint32_t)n;
+      d_pool_ = (uint8_t*)dmalloc((size_t)pool_n_ * CHAIN_BLK);
+      d_pool_ring_ = (uint32_t*)dmalloc((size_t)pool_n_ * 4);
+    }
+    if (!blocks.empty())
+      HIP_OK(hipMemcpy(d_pool_, blocks.data(), blocks.size() * CHAIN_BLK, hipMemcpyHostToDevice));
+    apm_dj_pool_init(d_pool_ring_, pool_n_, d_counts_, st);
+    const unsigned long long taken = blocks.size();
+    HIP_OK(hipMemcpyAsync((uint8_t*)d_counts_ + offsetof(JoinCounts, pool_head), &taken, 8, hipMemcpyHostToDevice, st));
+    HIP_OK(hipStreamSynchronize(st));
+    pool_avail(true);
   }
   {
     auto ss = rd.vec<SoapState>();

@@ -36,7 +36,8 @@ struct DevJoinConfig {
   int table_bits = 21;              // key-table slots (KeyState, 128 B)
   int reg_bits = 20;                // service registry slots
   uint32_t max_raw = 1u << 20;      // distinct (server, raw service)
-  uint32_t arena_cap = 1u << 20;    // NeedEnt entries (512 B), power of two
+  uint32_t arena_cap = 1u << 20;    // NeedEnt entries (512 B), power of two (grows)
+  uint32_t pool_blocks = 0;         // initial chain-block pool (256 B blocks; 0 = auto, grows)
   uint64_t ring_bytes = 4ull << 30; // tx text ring (power of two)
   double record_ttl_ms = 120000, acct_ttl_ms = 120000, need_ttl_ms = 30000;
   TzTable tz{};
@@ -77,8 +78,9 @@ class DeviceJoin {
   // `parallel(n, fn)` runs fn(0..n-1) on the engine's worker pool (host pre-pass per file)
   using ParallelFor = std::function<void(int, const std::function<void(int)>&)>;
   // `meanwhile` runs on this thread after the join kernels are queued, before the first wait
-  void run(int k, const uint8_t* host_bytes, uint32_t n_ev, double now, uint64_t batch_no, bool want_tx, bool want_db,
-           DevJoinBatch& out, const ParallelFor& parallel = nullptr, const std::function<void()>* meanwhile = nullptr);
+  void run(int k, const uint8_t* host_bytes, uint32_t n_ev, uint64_t n_bytes, double now, uint64_t batch_no, bool want_tx,
+           bool want_db, DevJoinBatch& out, const ParallelFor& parallel = nullptr,
+           const std::function<void()>* meanwhile = nullptr);
   // the host pre-pass of the NEXT batch (slot k, its parse finished), run on another thread while
   // this batch's join completes; run(k) then uploads its ops instead of doing the pre-pass
   // itself.  The audit state is host-only and advanced in batch order, so the result is the same.
@@ -173,7 +175,17 @@ class DeviceJoin {
   void on_app(PrepassTask& t, const Event& e, uint32_t ev, std::string_view line, int32_t server);
   int32_t intern_name(const std::string& s);
   void register_misses(const uint8_t* host_bytes, uint32_t n_miss, hipStream_t s);
-  void maybe_rebuild(double now, hipStream_t s);
+  // Capacity before a batch of n_ev events (`bytes` of lines + host-op bytes): the key table keeps
+  // every key of the batch under half load (rebuilt, then doubled), the need arena can open one
+  // entry per event, the chain pool covers one block per event plus every logId byte.  All grow;
+  // none drops state.  Expiring need regions are still live here (they are emitted this batch).
+  void ensure_capacity(uint32_t n_ev, uint64_t bytes, double now);
+  void rebuild_table(double now, uint32_t new_cap);
+  void grow_arena(uint32_t new_cap, uint64_t lo);
+  void grow_pool(uint64_t need_free);
+  uint64_t pool_avail(bool exact);
+  void ensure_tmp();
+  void dfree(void* p, size_t bytes);
 
   DevJoinConfig cfg_;
   Dictionary* dict_;
@@ -206,8 +218,16 @@ class DeviceJoin {
   DJArgs a_{};
   DJFormatArgs f_{};
   KeyState* d_table_ = nullptr;
+  KeyState* d_table_spare_ = nullptr;  // same-size rebuild target (no allocation per rebuild)
   uint32_t table_cap_ = 0;
+  int table_bits_ = 0;
   uint64_t keys_since_rebuild_ = 0, keys_live_ = 0;
+  uint8_t* d_pool_ = nullptr;          // chain blocks
+  uint32_t* d_pool_ring_ = nullptr;    // free-index ring
+  uint32_t pool_n_ = 0;                // blocks (power of two)
+  unsigned long long* h_live_ = nullptr;  // pinned
+  // growth events (reported in counters())
+  uint64_t table_grows_ = 0, arena_grows_ = 0, pool_grows_ = 0, table_rebuilds_ = 0;
   RegSlot* d_reg_ = nullptr;
   RegMiss* d_miss_ = nullptr;
   RegMiss* h_miss_ = nullptr;

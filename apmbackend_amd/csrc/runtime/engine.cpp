@@ -234,6 +234,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     dc.table_bits = cfg_.join_table_bits;
     dc.max_raw = cfg_.max_raw_services;
     dc.arena_cap = cfg_.need_arena;
+    dc.pool_blocks = cfg_.join_chain_blocks;
     dc.ring_bytes = cfg_.tx_ring_bytes;
     dc.record_ttl_ms = cfg_.record_ttl_ms;
     dc.acct_ttl_ms = cfg_.acct_ttl_ms;
@@ -1025,7 +1026,7 @@ void Engine::process_batch_dev_tail(ParseSlot& ps, double t0, double now_overrid
     });
   };
   static const bool ahead_on = [] { const char* e = std::getenv("APM_PREPASS_AHEAD"); return !e || e[0] != '0'; }();
-  dj_->run(k, ps.hb, ps.n_events, clock, batch_no_, want(OUT_TRANSACTIONS), want(OUT_AUDIT_DB), b, par,
+  dj_->run(k, ps.hb, ps.n_events, ps.n_bytes, clock, batch_no_, want(OUT_TRANSACTIONS), want(OUT_AUDIT_DB), b, par,
            prefetched_ && ahead_on ? &ahead : nullptr);
   const double t2 = now_ms();
   metrics_.t_join_ms += t2 - t1;

@@ -97,6 +97,7 @@ struct EngineConfig {
   int device_join = 1;
   int join_table_bits = 21;          // key-table slots (128 B each)
   uint32_t need_arena = 1u << 18;    // needNumRecordCache entries (512 B each)
+  uint32_t join_chain_blocks = 0;    // initial chain-block pool of the GPU join (256 B each; 0 = auto)
   uint64_t tx_ring_bytes = 4ull << 30;  // HBM text ring of pending (unreleased) tx lines
   uint32_t max_raw_services = 1u << 20;
 };

@@ -95,6 +95,11 @@ struct JoinConfig {
 struct JoinCounters {
   uint64_t events = 0, tx = 0, tx_db = 0, expired_partials = 0, need_expired = 0;
   uint64_t ejb_exit_unmatched = 0, invalid_acct = 0, audit_errors = 0, host_fallback = 0;
+  // device join capacity: losses (must stay 0: every structure grows) and growth / chain use
+  uint64_t partial_overflow = 0, need_overflow = 0, table_full = 0, pool_exhausted = 0;
+  uint64_t chain_partial_blocks = 0, chain_need_blocks = 0, chain_logid_blocks = 0;
+  uint64_t table_slots = 0, table_grows = 0, table_rebuilds = 0, need_arena_entries = 0, arena_grows = 0;
+  uint64_t chain_pool_blocks = 0, pool_grows = 0;
 };
 
 // Cache-line aligned: the shards of a process are joined concurrently, one worker each, and

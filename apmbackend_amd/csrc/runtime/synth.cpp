@@ -115,6 +115,9 @@ struct Params {
   // distinct names.  0 = every JVM uses the same names.
   int ejb_pool = 0;
   int provider_pool = 0;
+  // capacity stress (see utils/synth.py): overlapping provider calls, longer logIds
+  bool overlap_subs = false;
+  int logid_pad = 0;
 };
 
 class ServerGen {
@@ -178,6 +181,11 @@ class ServerGen {
       char b[16];
       snprintf(b, sizeof(b), "%08llu", (unsigned long long)n_);
       log_id += b;
+      if (p_.logid_pad > 0) {
+        static const char pad[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789abcdefghijklmnopqrstuvwxyz";
+        log_id.push_back('-');
+        for (int i = 0; i < p_.logid_pad; ++i) log_id.push_back(pad[i % 62]);
+      }
     }
     const bool missing = rng_.uni() < p_.missing;
     const std::string lid = missing ? std::string() : log_id;
@@ -232,7 +240,14 @@ class ServerGen {
       else
         snprintf(pn, sizeof(pn), "Provider[cb-util-%03d]", pv);
       int64_t el = elapsed(base_elapsed(0x55AA55ULL + pv) * 0.4);
-      int64_t s_t = std::min(cursor, t_end - 1), e_t = std::min(s_t + el, t_end - 1);
+      int64_t s_t, e_t;
+      if (p_.overlap_subs) {
+        s_t = std::min<int64_t>(t0 + 1 + i, t_end - 1);
+        e_t = std::min<int64_t>(std::max<int64_t>(s_t + el, t0 + 1 + nsub), t_end - 1);
+      } else {
+        s_t = std::min(cursor, t_end - 1);
+        e_t = std::min(s_t + el, t_end - 1);
+      }
       el = std::max<int64_t>(0, e_t - s_t);
       subs.push_back(Sub{pn, s_t, e_t, el});
       cursor = e_t + 1;
@@ -352,6 +367,7 @@ void register_synth(py::module_& m) {
         g("sub_max", p.sub_max); g("seed", p.seed); g("server_offset", p.server_offset);
         g("anomaly_services", p.anomaly_services); g("anomaly_factor", p.anomaly_factor);
         g("anomaly_start_ms", p.anomaly_start_ms); g("ejb_pool", p.ejb_pool); g("provider_pool", p.provider_pool);
+        g("overlap_subs", p.overlap_subs); g("logid_pad", p.logid_pad);
         return new SynthGen(p);
       }))
       .def("files", &SynthGen::files)

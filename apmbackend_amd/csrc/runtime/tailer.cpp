@@ -663,7 +663,14 @@ class Tailer {
             std::lock_guard<std::mutex> lk(mu_);
             r.chunks.clear();
             r.id = read_batch((char*)slots_[slot], std::min(slot_bytes_, max_batch_), r.chunks, r.n);
-            if (r.n == 0) commit_locked(r.id);  // empty batches carry no offsets to wait for
+            // An empty read only restates positions of earlier batches (or moves a drained
+            // rotation to the new inode).  Committing it would commit every earlier batch still
+            // waiting in a slot, before the engine has its lines -- a checkpoint would then store
+            // offsets past state it does not hold.  So it commits only when nothing is pending.
+            if (r.n == 0) {
+              if (pending_.begin()->first == r.id) commit_locked(r.id);
+              else pending_.erase(r.id);
+            }
           }
           if (r.n > 0) break;
           {

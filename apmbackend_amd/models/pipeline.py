@@ -94,6 +94,7 @@ def engine_config(cfg: Dict[str, Any], device: int = 0, keep_text: bool = False,
         "device_join": 1 if g.get("joinOnDevice", True) else 0,
         "join_table_bits": max(10, (int(g.get("joinTableSlots", 1 << 21)) - 1).bit_length()),
         "need_arena": int(g.get("needArenaEntries", 1 << 18)),
+        "join_chain_blocks": int(g.get("joinChainBlocks", 0)),
         # the ring holds every tx line not yet released (~70 s of tx text); small test engines
         # keep it proportional to their batch size
         "tx_ring_bytes": min(int(g.get("txTextRingMB", 4096)), max(256, (128 * int(g.get("batchBytes", 32 << 20))) >> 20)) << 20,

@@ -57,8 +57,9 @@ GPU_DEFAULTS: Dict[str, Any] = {
     "fleetBaseline": True,            # RCCL all-reduce of per-service moments + lock-step clocks
     "joinThreads": 0,                 # host join worker threads (0 = auto; joinOnDevice false)
     "joinOnDevice": True,             # K4/K6 join + tx encoding on the GPU (false: host join workers)
-    "joinTableSlots": 1 << 21,        # GPU join key table (logId keys, 128 B per slot)
-    "needArenaEntries": 1 << 18,      # GPU needNumRecordCache entries (512 B each)
+    "joinTableSlots": 1 << 21,        # GPU join key table (logId keys, 128 B per slot) -- grows
+    "needArenaEntries": 1 << 18,      # GPU needNumRecordCache entries (512 B each) -- grows
+    "joinChainBlocks": 0,             # GPU join overflow chains (256 B blocks; 0 = auto) -- grows
     "txTextRingMB": 4096,             # HBM ring holding pending (unreleased) tx lines
     "maxRawServices": 1 << 18,        # distinct (server, raw service name) pairs
     "collectiveTimeoutSeconds": 300,  # RCCL watchdog: abort + exit when a collective hangs this long

@@ -20,6 +20,7 @@ import random
 from typing import Dict, List, Optional, Sequence, Tuple
 
 LOG_DIR = "/net/{server}/export/jvm1/log/{file}"
+_PAD = "ABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789abcdefghijklmnopqrstuvwxyz"
 
 
 @dataclasses.dataclass
@@ -49,6 +50,11 @@ class SynthConfig:
     soap_late_fraction: float = 0.1   # account arrives after the exits (exercises need cache)
     no_acct_fraction: float = 0.03    # never gets an account (exercises expiry)
     anomalies: Sequence[Anomaly] = ()
+    # capacity stress: every provider call of a request opens before any closes (many open
+    # partials per logId, many parked records when the account is late), and logIds get this
+    # many extra characters (the device join keeps 80 inline)
+    overlap_subs: bool = False
+    logid_pad: int = 0
     seed: int = 1234
     tz_offset_ms: int = 0             # log timestamps written in this offset (UTC default)
 
@@ -108,6 +114,8 @@ class Generator:
         c, rng = self.cfg, self.rng
         tz = c.tz_offset_ms
         log_id = f"{server.upper()}-{idx:08d}"
+        if c.logid_pad:
+            log_id += "-" + (_PAD * (c.logid_pad // len(_PAD) + 1))[:c.logid_pad]
         missing = rng.random() < c.missing_logid_fraction
         lid = "" if missing else log_id
         acct = str(rng.randint(10 ** 15, 10 ** 16 - 1))
@@ -139,12 +147,16 @@ class Generator:
         use_audit = rng.random() < c.audit_fraction and not missing
         sub_records = []
         cursor = t0 + 1
-        for _ in range(n_sub):
+        for i in range(n_sub):
             p = rng.choice(self.prov)
             svc = f"Provider[{p}]"
             el = self._elapsed(server, svc, cursor)
-            s_t = min(cursor, t_end - 1)
-            e_t = min(s_t + el, t_end - 1)
+            if c.overlap_subs:  # all starts (t0+1 .. t0+n_sub) before all stops
+                s_t = min(t0 + 1 + i, t_end - 1)
+                e_t = min(max(s_t + el, t0 + 1 + n_sub), t_end - 1)
+            else:
+                s_t = min(cursor, t_end - 1)
+                e_t = min(s_t + el, t_end - 1)
             el = max(0, e_t - s_t)
             sub_records.append((svc, s_t, e_t, el))
             cursor = e_t + 1

@@ -633,3 +633,76 @@ def test_spill_overflow_drops_samples_without_corrupting_windows():
     for l in st:
         for v in l.split("|")[5:8]:
             assert v == "undefined" or 0.0 <= float(v) <= hi, l
+
+
+def _capacity_corpus(seed=12, servers=2, duration=300):
+    """Requests touching 12-20 provider services that all open before any closes (up to 20 open
+    partials per logId), late SOAP accounts (up to 20 parked records per logId) and 130-byte
+    logIds: past every inline capacity of the device join (5 partials, 7 parked records, 80
+    logId bytes), which the reference does not have (unbounded Maps,
+    stream_parse_transactions.js:215-218,433-437,548-555)."""
+    cfg = SynthConfig(servers=servers, duration_s=duration, tx_per_sec_per_server=3, seed=seed,
+                      ejb_services=4, provider_services=30, sub_calls=(12, 20), overlap_subs=True,
+                      logid_pad=120, soap_late_fraction=0.6, audit_fraction=0.1, no_acct_fraction=0.05)
+    lines = Generator(cfg).generate()
+    return with_watermarks(batches(lines, cfg.start_ms, 5.0), UTC)
+
+
+def _assert_streams(out, P):
+    assert out["transactions"] == P.tx_out
+    assert out["audit_db"] == P.audit_db
+    assert out["st"] == P.stats
+    assert out["fs"] == P.fs
+    assert out["al"] == P.al
+
+
+def test_join_overflow_chains_match_oracle():
+    bl = _capacity_corpus()
+    C = small_cfg("exact")
+    P = PipelineOracle(copy.deepcopy(C), UTC)
+    P.run_batches(bl)
+    assert max(len(l.split("|")[3]) for l in P.tx_out) > 120
+    eng, out = _run_engine(C, bl)
+    _assert_streams(out, P)
+    j = eng.metrics()["join"]
+    assert j["partial_overflow"] == 0 and j["need_overflow"] == 0 and j["table_full"] == 0
+    assert j["pool_exhausted"] == 0
+    # the chains were really used: > 5 open partials, > 7 parked records, logIds > 80 bytes
+    assert j["chain_partial_blocks"] > 0 and j["chain_need_blocks"] > 0 and j["chain_logid_blocks"] > 0
+
+
+def test_join_tables_grow_instead_of_failing(tmp_path):
+    """Key table, need arena and chain pool all start at 1024 entries: each batch's worst case
+    exceeds them, so the join grows them between batches (was: a throw once live keys passed half
+    of gpu.joinTableSlots, and silently dropped parked records past the arena).  A checkpoint
+    taken mid-run with the grown tables and live chains restores into an engine of default size
+    and continues identically."""
+    bl = _capacity_corpus(seed=13)
+    C = small_cfg("exact")
+    C["gpu"].update({"joinTableSlots": 1024, "needArenaEntries": 1024, "joinChainBlocks": 1024})
+    P = PipelineOracle(copy.deepcopy(C), UTC)
+    P.run_batches(bl)
+    eng = APMEngine(C, keep_text=True)
+    out = collections.defaultdict(list)
+    cut = len(bl) // 2
+    prefix = str(tmp_path / "engine.rank0")
+    for i, (now, chunks) in enumerate(bl[:cut]):
+        eng.process_lines(chunks, now)
+        for k in ("transactions", "audit_db", "st", "fs", "al"):
+            out[k] += eng.take(k)
+    j = eng.metrics()["join"]
+    assert j["table_grows"] > 0 and j["arena_grows"] > 0 and j["pool_grows"] > 0, j
+    assert j["table_slots"] > 1024 and j["need_arena_entries"] > 1024 and j["chain_pool_blocks"] > 1024
+    eng.save_state(prefix + ".bin")
+    del eng
+    C2 = small_cfg("exact")
+    eng2 = APMEngine(C2, keep_text=True)
+    eng2.load_state(prefix + ".bin")
+    for now, chunks in bl[cut:]:
+        eng2.process_lines(chunks, now)
+        for k in ("transactions", "audit_db", "st", "fs", "al"):
+            out[k] += eng2.take(k)
+    _assert_streams(out, P)
+    j2 = eng2.metrics()["join"]
+    assert j2["partial_overflow"] == 0 and j2["need_overflow"] == 0 and j2["table_full"] == 0
+    assert j2["pool_exhausted"] == 0

@@ -85,3 +85,15 @@ def test_join_key_hash_python_matches_native():
         b = bytes(rng.randrange(256) for _ in range(n))
         for seed in (HASH_SEED, HASH_SEED_EJB):
             assert hash_bytes(b, seed) == N.hash_bytes(b, seed)
+
+
+def test_native_join_many_services_long_logids():
+    """12-20 overlapping provider calls per request, late accounts and 150-byte logIds: the host
+    join keeps every open partial and parked record (the reference caches are unbounded Maps,
+    stream_parse_transactions.js:215-218,433-437,548-555)."""
+    want, got, nc, oc = run_both(11, servers=2, duration=240, sub_calls=(12, 20), overlap_subs=True,
+                                 provider_services=30, logid_pad=150, soap_late_fraction=0.6,
+                                 audit_fraction=0.1)
+    assert max(len(l.split("|")[3]) for _, l in want) > 150
+    assert nc["need_expired"] == oc["need_expired"]
+    assert want == got

@@ -186,3 +186,32 @@ def test_readahead_ring_over_caller_slots(tmp_path):
     t.stop()
     assert got == want
     assert [o[1] for o in t.offsets()] == [os.path.getsize(f) for f in files]
+
+
+def test_idle_read_ahead_does_not_commit_a_waiting_batch(tmp_path):
+    """the read-ahead thread's empty polls used to commit every earlier batch,
+    including one still sitting in a ready slot, so a checkpoint could record offsets past lines
+    the engine never processed.  Offsets now move only with commit(id) of the batch itself."""
+    f = tmp_path / "a.log"
+    f.write_bytes(b"")
+    slots = [ctypes.create_string_buffer((64 << 10) + 256) for _ in range(2)]
+    t = N.Tailer("", 64 << 10, 2)
+    t.add(str(f), 0, True, 0)
+    t.start([ctypes.addressof(s) for s in slots], 64 << 10, 2.0)
+    with open(f, "ab") as fh:
+        fh.write(b"alpha\nbeta\n")
+    deadline = time.time() + 10
+    r = None
+    while r is None and time.time() < deadline:
+        r = t.next(200.0)
+    assert r is not None
+    slot, ptr, n, chunks, bid = r
+    assert ctypes.string_at(ptr, n) == b"alpha\nbeta\n"
+    time.sleep(0.2)  # the read-ahead thread polls the idle file ~100 times meanwhile
+    assert t.offsets()[0][1] == 0
+    t.release(slot)
+    time.sleep(0.05)
+    assert t.offsets()[0][1] == 0
+    t.commit(bid)
+    assert t.offsets()[0][1] == 11
+    t.stop()
