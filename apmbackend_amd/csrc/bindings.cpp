@@ -155,6 +155,8 @@ py::dict metrics_dict(const EngineMetrics& m) {
   d["spill_dropped"] = m.spill_dropped;
   d["nan_windows_clipped"] = m.nan_windows_clipped;
   d["tx_capacity_grows"] = m.tx_capacity_grows;
+  d["spill_grows"] = m.spill_grows;
+  d["spill_capacity"] = m.spill_capacity;
   d["rollover_latency_ms"] = m.rollover_latency_ms;
   return d;
 }

@@ -13,7 +13,7 @@ struct StatsState {
   int32_t* counts;        // [NSLOT][S]
   int32_t* cells;         // [NSLOT][S][cap]
   int32_t* spill_n;       // [NSLOT]
-  int32_t* spill_series;  // [NSLOT][spill_cap]
+  int32_t* spill_series;  // [NSLOT][spill_cap]  (sorted by series, stably, before every K8)
   int32_t* spill_val;     // [NSLOT][spill_cap]
   uint8_t* active;        // [S]
   int32_t cap;
@@ -27,6 +27,9 @@ struct StatsState {
   int32_t* ord_list = nullptr;   // [max_tx] tx indices deferred to the ordered append
   int32_t* ord_n = nullptr;
   int32_t keep = 0;              // windowSz + intervalBufferSz
+  // host-mapped pinned [NSLOT]: spill_n after each append (the host's exact fill level, read once
+  // the append's event completed; it sizes the spill area so no sample is ever dropped)
+  int32_t* spill_snap = nullptr;
 };
 
 struct WindowArgs {
@@ -185,6 +188,11 @@ void apm_bucket_append(const apm::TxRec* d_tx, uint32_t lo, uint32_t hi, apm::St
 // marks series with a NaN elapsed sample in tx[0, n) (before any of the batch is appended)
 void apm_nan_mark(const apm::TxRec* d_tx, uint32_t n, apm::StatsState* st, hipStream_t stream);
 void apm_window_stats(apm::WindowArgs* a, hipStream_t stream);
+// before K8: every slot's spill list [slot * cap, + spill_n[slot]) sorted by series, stably (a
+// series' samples keep their arrival order), into (series_out, val_out); the caller swaps buffers
+size_t apm_spill_sort_tmp_bytes(int32_t spill_cap, int32_t S);
+int apm_spill_sort(const apm::StatsState* st, int32_t* series_out, int32_t* val_out, void* tmp, size_t tmp_bytes,
+                   hipStream_t stream);
 void apm_pool_append(const apm::TxRec* d_tx, uint32_t lo, uint32_t hi, const int64_t* d_gid, int64_t* tail_end,
                      int64_t* tail_gid, int64_t base, hipStream_t stream);
 size_t apm_release_tmp_bytes(int64_t cap);

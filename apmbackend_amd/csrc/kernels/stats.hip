@@ -11,6 +11,11 @@
 // every active series is reduced by one wave: the 31 window cells are gathered into LDS, summed,
 // bitonic-sorted in LDS and the two percentile ranks read out with the reference index rule.
 // Series too large for a wave's LDS tile are deferred to a block-wide pass.
+// Spill lists: the reference window is an unbounded array (stream_calc_stats.js:127-131), so the
+// host sizes the spill area from the device's exact fill levels before every append and never
+// lets a sample be lost; before K8 every list is sorted by series (stable, rocprim segmented
+// radix sort), so a series' spilled samples are one contiguous run found by binary search
+// instead of a scan of the whole list per series.
 #include "kernel_api.h"
 
 #include <rocprim/rocprim.hpp>
@@ -81,7 +86,11 @@ __global__ __launch_bounds__(1024) void k_bucket_append_ordered(const TxRec* __r
   __shared__ int32_t sp0[ORD_TILE];
   __shared__ int m_sh;
   const int n_ord = *st.ord_n;
-  if (n_ord == 0) return;
+  if (n_ord == 0) {
+    // every append of this call is done (stream order): publish the fill levels to the host
+    if (st.spill_snap && threadIdx.x < NSLOT) st.spill_snap[threadIdx.x] = st.spill_n[threadIdx.x];
+    return;
+  }
   __syncthreads();  // every thread has read the count: reset it for the next append
   if (threadIdx.x == 0) *st.ord_n = 0;
   const uint32_t span = hi - lo;
@@ -164,6 +173,7 @@ __global__ __launch_bounds__(1024) void k_bucket_append_ordered(const TxRec* __r
     __threadfence();
     __syncthreads();
   }
+  if (st.spill_snap && threadIdx.x < NSLOT) st.spill_snap[threadIdx.x] = st.spill_n[threadIdx.x];
 }
 
 __global__ void k_clear_slot(StatsState st, int slot) {
@@ -173,6 +183,21 @@ __global__ void k_clear_slot(StatsState st, int slot) {
 }
 
 // --------------------------------------------------------------------------------- K8
+// first position of series s in a slot's sorted spill list [0, n)
+__device__ __forceinline__ int spill_lower(const int32_t* keys, int n, int32_t s) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (keys[mid] < s) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+// the run of series s's spilled samples in slot sl: [*first, *first + cnt - cap)
+__device__ __forceinline__ const int32_t* spill_run(const StatsState& st, int sl, int s) {
+  const size_t base = (size_t)sl * st.spill_cap;
+  const int ns = min(st.spill_n[sl], st.spill_cap);
+  return st.spill_val + base + spill_lower(st.spill_series + base, ns, s);
+}
 
 __device__ __forceinline__ void percentile_ranks(int n, int pct, int& lo, int& hi) {
   // calcPercentile: idx = p/100*n - 1; integral -> a[idx]; else ceil, last -> a[last],
@@ -269,30 +294,30 @@ __global__ __launch_bounds__(WS_WAVES * APM_WAVE) void k_window_stats(WindowArgs
     const int32_t* cell = a.st.cells + ((size_t)slot * a.st.S + s) * a.st.cap;
     for (int k = 0; k < inl; ++k) { const int32_t v = cell[k]; t[pre + k] = v; sum += v; nan += v == ELAPSED_NAN; }
   }
-  // spilled samples: scan the spill lists of the window slots (rare)
+  // spilled samples: each window bucket's run in its slot's sorted spill list (binary search by
+  // the lane owning the bucket), copied by the whole wave
   if (total_spill > 0) {
+    const int32_t* run = spill > 0 ? spill_run(a.st, slot, s) : nullptr;
+    int spre = spill;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(spre, o, 64);
+      if (lane >= o) spre += v;
+    }
+    spre -= spill;
     __builtin_amdgcn_wave_barrier();
-    int w = total_inl;
-    for (int r = 0; r < a.n_win; ++r) {
-      const int sl = a.win_slots[r];
-      if (sl < 0) continue;
-      const int ns = min(a.st.spill_n[sl], a.st.spill_cap);
-      for (int base = 0; base < ns; base += 64) {
-        const int j = base + lane;
-        bool hit = false;
-        int32_t v = 0;
-        if (j < ns) {
-          hit = a.st.spill_series[(size_t)sl * a.st.spill_cap + j] == s;
-          v = a.st.spill_val[(size_t)sl * a.st.spill_cap + j];
-        }
-        const unsigned long long m = __ballot(hit);
-        if (hit) {
-          const int off = __popcll(m & ((1ULL << lane) - 1ULL));
-          t[w + off] = v;
-          sum += v;
-          nan += v == ELAPSED_NAN;
-        }
-        w += __popcll(m);
+    unsigned long long todo = __ballot(spill > 0);
+    while (todo) {
+      const int r = __ffsll((long long)todo) - 1;
+      todo &= todo - 1;
+      const int m = __shfl(spill, r, 64);
+      const int off = total_inl + __shfl(spre, r, 64);
+      const uintptr_t rp = (uintptr_t)__shfl((long long)(uintptr_t)run, r, 64);
+      const int32_t* src = (const int32_t*)rp;
+      for (int k = lane; k < m; k += 64) {
+        const int32_t v = src[k];
+        t[off + k] = v;
+        sum += v;
+        nan += v == ELAPSED_NAN;
       }
     }
   }
@@ -324,9 +349,8 @@ __device__ __forceinline__ void for_each_window_sample(const WindowArgs& a, int 
     const int32_t* cell = a.st.cells + ((size_t)sl * a.st.S + s) * a.st.cap;
     for (int k = threadIdx.x; k < inl; k += blockDim.x) f(cell[k]);
     if (cnt > inl) {
-      const int ns = min(a.st.spill_n[sl], a.st.spill_cap);
-      for (int j = threadIdx.x; j < ns; j += blockDim.x)
-        if (a.st.spill_series[(size_t)sl * a.st.spill_cap + j] == s) f(a.st.spill_val[(size_t)sl * a.st.spill_cap + j]);
+      const int32_t* run = spill_run(a.st, sl, s);
+      for (int k = threadIdx.x; k < cnt - inl; k += blockDim.x) f(run[k]);
     }
   }
 }
@@ -412,15 +436,13 @@ __global__ __launch_bounds__(1024) void k_window_stats_big(WindowArgs a) {
         nan += v == ELAPSED_NAN;
       }
       if (cnt > inl) {
-        const int ns = min(a.st.spill_n[sl], a.st.spill_cap);
-        for (int j = threadIdx.x; j < ns; j += blockDim.x) {
-          if (a.st.spill_series[(size_t)sl * a.st.spill_cap + j] == s) {
-            const int32_t v = a.st.spill_val[(size_t)sl * a.st.spill_cap + j];
-            const int p = atomicAdd(&wpos, 1);
-            if (p < BIG_TILE) t[p] = v;
-            sum += v;
-            nan += v == ELAPSED_NAN;
-          }
+        const int32_t* run = spill_run(a.st, sl, s);
+        for (int k = threadIdx.x; k < cnt - inl; k += blockDim.x) {
+          const int32_t v = run[k];
+          const int p = atomicAdd(&wpos, 1);
+          if (p < BIG_TILE) t[p] = v;
+          sum += v;
+          nan += v == ELAPSED_NAN;
         }
       }
     }
@@ -501,24 +523,14 @@ __global__ __launch_bounds__(1024) void k_window_stats_js(WindowArgs a) {
       __syncthreads();
       if (threadIdx.x == 0) wpos = base + inl;
       __syncthreads();
-      if (cnt > inl) {  // the series' spill entries in list order (ordered block compaction)
-        const int ns = min(a.st.spill_n[sl], a.st.spill_cap);
-        for (int j0 = 0; j0 < ns; j0 += blockDim.x) {
-          const int j = j0 + threadIdx.x;
-          const bool hit = j < ns && a.st.spill_series[(size_t)sl * a.st.spill_cap + j] == s;
-          const unsigned long long m = __ballot(hit);
-          if (lane == 0) wsum[wv] = __popcll(m);
-          __syncthreads();
-          int before = wpos;
-          for (int w = 0; w < wv; ++w) before += wsum[w];
-          if (hit) {
-            const int p = before + __popcll(m & ((1ULL << lane) - 1ULL));
-            if (p < a.js_cap) gbuf[p] = a.st.spill_val[(size_t)sl * a.st.spill_cap + j];
-          }
-          __syncthreads();
-          if (threadIdx.x == 0) { int t = 0; for (int w = 0; w < 16; ++w) t += wsum[w]; wpos += t; }
-          __syncthreads();
-        }
+      if (cnt > inl) {  // the series' spill run: arrival order (the list sort is stable)
+        const int32_t* run = spill_run(a.st, sl, s);
+        const int m = cnt - inl;
+        for (int k = threadIdx.x; k < m; k += blockDim.x)
+          if (base + inl + k < a.js_cap) gbuf[base + inl + k] = run[k];
+        __syncthreads();
+        if (threadIdx.x == 0) wpos = base + inl + m;
+        __syncthreads();
       }
     }
     const int n_all = wpos;
@@ -668,6 +680,45 @@ void apm_window_stats(WindowArgs* a, hipStream_t stream) {
   hipLaunchKernelGGL(k_window_stats, dim3(blocks), dim3(WS_WAVES * APM_WAVE), 0, stream, *a);
   hipLaunchKernelGGL(k_window_stats_big, dim3(64), dim3(1024), 0, stream, *a);
   hipLaunchKernelGGL(k_window_stats_js, dim3(JS_BLOCKS), dim3(1024), 0, stream, *a);
+}
+
+namespace {
+// segment [slot * cap, slot * cap + spill_n[slot]) (one functor type for both offset iterators)
+struct SpillOff {
+  const int32_t* n;  // null: segment begin
+  int32_t cap;
+  __host__ __device__ int operator()(int slot) const { return slot * cap + (n ? min(n[slot], cap) : 0); }
+};
+int key_bits(int32_t S) {
+  int b = 1;
+  while ((1ll << b) < (long long)S) ++b;
+  return b;
+}
+}  // namespace
+
+size_t apm_spill_sort_tmp_bytes(int32_t spill_cap, int32_t S) {
+  size_t need = 0;
+  const auto beg = rocprim::make_transform_iterator(rocprim::make_counting_iterator(0), SpillOff{nullptr, spill_cap});
+  const auto end = rocprim::make_transform_iterator(rocprim::make_counting_iterator(0), SpillOff{nullptr, spill_cap});
+  HIP_OK(rocprim::segmented_radix_sort_pairs(nullptr, need, (int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr,
+                                             (int32_t*)nullptr, (size_t)NSLOT * spill_cap, (unsigned)NSLOT, beg, end, 0,
+                                             key_bits(S), (hipStream_t)0));
+  return need + 4096;
+}
+
+int apm_spill_sort(const StatsState* st, int32_t* series_out, int32_t* val_out, void* tmp, size_t tmp_bytes,
+                   hipStream_t stream) {
+  size_t need = 0;
+  const auto beg = rocprim::make_transform_iterator(rocprim::make_counting_iterator(0), SpillOff{nullptr, st->spill_cap});
+  const auto end = rocprim::make_transform_iterator(rocprim::make_counting_iterator(0), SpillOff{st->spill_n, st->spill_cap});
+  HIP_OK(rocprim::segmented_radix_sort_pairs(nullptr, need, st->spill_series, series_out, st->spill_val, val_out,
+                                             (size_t)NSLOT * st->spill_cap, (unsigned)NSLOT, beg, end, 0, key_bits(st->S),
+                                             stream));
+  if (need > tmp_bytes) return -1;
+  HIP_OK(rocprim::segmented_radix_sort_pairs(tmp, need, st->spill_series, series_out, st->spill_val, val_out,
+                                             (size_t)NSLOT * st->spill_cap, (unsigned)NSLOT, beg, end, 0, key_bits(st->S),
+                                             stream));
+  return 0;
 }
 
 void apm_pool_append(const TxRec* d_tx, uint32_t lo, uint32_t hi, const int64_t* d_gid, int64_t* tail_end,

@@ -527,7 +527,8 @@ std::string Engine::load_small_state(const std::string& path) {
     if (nl != cfg_.n_lags || std::memcmp(lags, cfg_.lags, sizeof(lags)) != 0)
       throw std::runtime_error("checkpoint: LAG set differs from this engine's configuration");
     if (rb != cfg_.ring_bytes) throw std::runtime_error("checkpoint: ring dtype differs");
-    if (cc != cfg_.cell_cap || sc != cfg_.spill_cap) throw std::runtime_error("checkpoint: bucket cell layout differs");
+    if (cc != cfg_.cell_cap) throw std::runtime_error("checkpoint: bucket cell layout differs");
+    if (sc > cfg_.spill_cap) grow_spill(sc);  // the saving engine had grown its spill lists
     if (win != cfg_.window || buf != cfg_.buffer) throw std::runtime_error("checkpoint: stats window differs");
     (void)ms; (void)pc;  // capacities may grow; checked per array below
   }
@@ -646,6 +647,7 @@ std::string Engine::load_small_state(const std::string& path) {
     }
   }
   h2d_vec(rd, d_nan_until_, (size_t)S, stream_);
+  spill_resync();  // the restored fill levels bound the next appends
 
   rd.begin(SEC_ZSCORE);
   for (int l = 0; l < cfg_.n_lags; ++l) {

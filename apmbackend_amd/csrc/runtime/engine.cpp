@@ -296,6 +296,15 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   d_spill_n_ = (int32_t*)dmalloc(NSLOT * 4);
   d_spill_series_ = (int32_t*)dmalloc((size_t)NSLOT * cfg_.spill_cap * 4);
   d_spill_val_ = (int32_t*)dmalloc((size_t)NSLOT * cfg_.spill_cap * 4);
+  d_spill_series_alt_ = (int32_t*)dmalloc((size_t)NSLOT * cfg_.spill_cap * 4);
+  d_spill_val_alt_ = (int32_t*)dmalloc((size_t)NSLOT * cfg_.spill_cap * 4);
+  spill_tmp_bytes_ = apm_spill_sort_tmp_bytes(cfg_.spill_cap, S);
+  d_spill_tmp_ = dmalloc(spill_tmp_bytes_);
+  HIP_OK(hipHostMalloc((void**)&h_spill_snap_, NSLOT * 4, hipHostMallocDefault));
+  HIP_OK(hipHostGetDevicePointer((void**)&hd_spill_snap_, h_spill_snap_, 0));
+  std::memset(h_spill_snap_, 0, NSLOT * 4);
+  for (auto& m : spill_mark_) HIP_OK(hipEventCreateWithFlags(&m.ev, hipEventDisableTiming));
+  metrics_.spill_capacity = cfg_.spill_cap;
   d_spill_drop_ = (unsigned long long*)dmalloc(64);
   d_active_ = (uint8_t*)dmalloc(S);
   d_win_ = (WinStat*)dmalloc((size_t)S * sizeof(WinStat));
@@ -427,6 +436,8 @@ Engine::~Engine() {
   fb_lane_.reset();     // and a pending fb emission before its buffers
   if (nm_ev_) { hipEventSynchronize(nm_ev_); hipEventDestroy(nm_ev_); }
   if (h_nm_send_) hipHostFree(h_nm_send_);
+  if (h_spill_snap_) hipHostFree(h_spill_snap_);
+  for (auto& m : spill_mark_) if (m.ev) hipEventDestroy(m.ev);
   if (h_nm_recv_) hipHostFree(h_nm_recv_);
   checkpoint_shutdown();
   {
@@ -1490,7 +1501,98 @@ StatsState Engine::stats_state() const {
   st.ord_list = d_ord_list_;
   st.ord_n = d_ord_n_;
   st.keep = (int32_t)(cfg_.window + cfg_.buffer);
+  st.spill_snap = hd_spill_snap_;
   return st;
+}
+
+// ---- spill sizing: the reference window is unbounded (stream_calc_stats.js:127-131), so an
+// append never starts unless every live slot's list can take all of its samples.
+void Engine::spill_reserve(uint32_t n) {
+  if (n == 0) return;
+  // newest completed snapshot (the K7 kernel wrote h_spill_snap_ at or after that point; the
+  // values only grow until a clear, and clears after the mark are handled by spill_clear_at_)
+  const SpillMark* mk = nullptr;
+  for (int i = 0; i < kSpillMarks; ++i) {
+    const SpillMark& m = spill_mark_[(spill_mark_k_ + kSpillMarks - 1 - i) % kSpillMarks];
+    if (!m.live) continue;
+    if (hipEventQuery(m.ev) == hipSuccess) { mk = &m; break; }
+  }
+  int64_t worst = 0;
+  for (int s = 0; s < NSLOT; ++s) {
+    if (slot_bucket_[s] == NO_BUCKET) continue;
+    int64_t b = (int64_t)(spill_added_ - spill_clear_at_[s]);
+    if (mk && spill_clear_at_[s] <= mk->added) b = std::min<int64_t>(b, (int64_t)h_spill_snap_[s] + (int64_t)(spill_added_ - mk->added));
+    worst = std::max(worst, b);
+  }
+  if (worst + (int64_t)n <= cfg_.spill_cap) return;
+  // the bound is too loose: read the exact levels (stream drain, rare), then grow if needed
+  spill_resync();
+  worst = 0;
+  for (int s = 0; s < NSLOT; ++s)
+    if (slot_bucket_[s] != NO_BUCKET) worst = std::max<int64_t>(worst, h_spill_snap_[s]);
+  if (worst + (int64_t)n <= cfg_.spill_cap) return;
+  int64_t cap = cfg_.spill_cap;
+  while (worst + (int64_t)n > cap) cap *= 2;
+  if (cap > INT32_MAX / NSLOT) throw std::runtime_error("bucket spill lists beyond 2^31 entries");
+  grow_spill((int32_t)cap);
+}
+
+// exact fill levels now (drains the stats stream): the newest snapshot, every older one retired
+void Engine::spill_resync() {
+  HIP_OK(hipStreamSynchronize(stream_));
+  std::vector<int32_t> exact(NSLOT);
+  HIP_OK(hipMemcpy(exact.data(), d_spill_n_, NSLOT * 4, hipMemcpyDeviceToHost));
+  for (auto& m : spill_mark_) m.live = false;
+  std::memcpy(h_spill_snap_, exact.data(), NSLOT * 4);
+  spill_mark_[0].added = spill_added_;
+  spill_mark_[0].live = true;
+  HIP_OK(hipEventRecord(spill_mark_[0].ev, stream_));
+  HIP_OK(hipEventSynchronize(spill_mark_[0].ev));
+  spill_mark_k_ = 1;
+  for (int s = 0; s < NSLOT; ++s) spill_clear_at_[s] = std::min(spill_clear_at_[s], spill_added_);
+}
+
+// after an append's kernels were queued: its snapshot point
+void Engine::spill_marked() {
+  SpillMark& m = spill_mark_[spill_mark_k_];
+  m.added = spill_added_;
+  m.live = true;
+  HIP_OK(hipEventRecord(m.ev, stream_));
+  spill_mark_k_ = (spill_mark_k_ + 1) % kSpillMarks;
+}
+
+// Every slot list keeps its entries at the same positions of a longer row.
+void Engine::grow_spill(int32_t cap) {
+  HIP_OK(hipStreamSynchronize(stream_));
+  const size_t old = (size_t)cfg_.spill_cap;
+  int32_t* ser = (int32_t*)dmalloc((size_t)NSLOT * cap * 4);
+  int32_t* val = (int32_t*)dmalloc((size_t)NSLOT * cap * 4);
+  HIP_OK(hipMemcpy2DAsync(ser, (size_t)cap * 4, d_spill_series_, old * 4, old * 4, NSLOT, hipMemcpyDeviceToDevice, stream_));
+  HIP_OK(hipMemcpy2DAsync(val, (size_t)cap * 4, d_spill_val_, old * 4, old * 4, NSLOT, hipMemcpyDeviceToDevice, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+  dfree(d_spill_series_);
+  dfree(d_spill_val_);
+  dfree(d_spill_series_alt_);
+  dfree(d_spill_val_alt_);
+  dfree(d_spill_tmp_);
+  d_spill_series_ = ser;
+  d_spill_val_ = val;
+  d_spill_series_alt_ = (int32_t*)dmalloc((size_t)NSLOT * cap * 4);
+  d_spill_val_alt_ = (int32_t*)dmalloc((size_t)NSLOT * cap * 4);
+  cfg_.spill_cap = cap;
+  spill_tmp_bytes_ = apm_spill_sort_tmp_bytes(cfg_.spill_cap, cfg_.max_series);
+  d_spill_tmp_ = dmalloc(spill_tmp_bytes_);
+  ++metrics_.spill_grows;
+  metrics_.spill_capacity = cap;
+}
+
+// before K8: each slot's list sorted by series (stable), the live and sort buffers swapped
+void Engine::spill_sort() {
+  StatsState st = stats_state();
+  if (apm_spill_sort(&st, d_spill_series_alt_, d_spill_val_alt_, d_spill_tmp_, spill_tmp_bytes_, stream_) != 0)
+    throw std::runtime_error("spill sort scratch too small");
+  std::swap(d_spill_series_, d_spill_series_alt_);
+  std::swap(d_spill_val_, d_spill_val_alt_);
 }
 
 void Engine::ensure_bucket_slot(int64_t b) {
@@ -1500,6 +1602,7 @@ void Engine::ensure_bucket_slot(int64_t b) {
     StatsState st = stats_state();
     apm_stats_clear_slot(&st, slot, stream_);
   }
+  spill_clear_at_[slot] = spill_added_;
   slot_bucket_[slot] = b;
 }
 
@@ -1587,8 +1690,10 @@ void Engine::stats_for_batch(std::vector<TxOut>& txs, double batch_t0) {
   if (n == 0) return;
   HIP_OK(hipMemcpyAsync(d_tx_, h_tx_, (size_t)n * sizeof(TxRec), hipMemcpyHostToDevice, stream_));
   HIP_OK(hipMemcpyAsync(d_gid_, h_gid_, (size_t)n * 8, hipMemcpyHostToDevice, stream_));
-  StatsState st = stats_state();
-  apm_nan_mark(d_tx_, n, &st, stream_);
+  {
+    StatsState st = stats_state();
+    apm_nan_mark(d_tx_, n, &st, stream_);
+  }
   const int64_t keep_iv = cfg_.window + cfg_.buffer;
   auto append = [&](uint32_t lo, uint32_t hi, int64_t lat) {
     if (hi <= lo) return;
@@ -1606,7 +1711,11 @@ void Engine::stats_for_batch(std::vector<TxOut>& txs, double batch_t0) {
       ensure_bucket_slot(b);
       if (nseen < 8) seen[nseen++] = b;
     }
+    spill_reserve(hi - lo);
+    StatsState st = stats_state();
     apm_bucket_append(d_tx_, lo, hi, &st, min_live, stream_);
+    spill_added_ += hi - lo;
+    spill_marked();
     apm_pool_append(d_tx_, lo, hi, d_gid_, d_tail_end_, d_tail_gid_, tail_n_, stream_);
     tail_n_ += hi - lo;
   };
@@ -1659,8 +1768,10 @@ void Engine::stats_for_batch_dev(DevJoinBatch& b, double batch_t0) {
     if (c.second > latest_) { triggers.push_back(c); latest_ = c.second; }
   metrics_.t_stats_tx_ms += now_ms() - ts0;
   trace_event("tx loop", ts0, now_ms(), 1);
-  StatsState st = stats_state();
-  apm_nan_mark(b.d_tx, b.n_stats, &st, stream_);
+  {
+    StatsState st = stats_state();
+    apm_nan_mark(b.d_tx, b.n_stats, &st, stream_);
+  }
   const int64_t keep_iv = cfg_.window + cfg_.buffer;
   auto append = [&](uint32_t lo, uint32_t hi, int64_t lat) {
     if (hi <= lo) return;
@@ -1669,7 +1780,11 @@ void Engine::stats_for_batch_dev(DevJoinBatch& b, double batch_t0) {
     // cleared exactly as the first tx of a new bucket would clear it
     for (int64_t bk = min_live; bk <= lat; ++bk) ensure_bucket_slot(bk);
     if (tail_n_ + (int64_t)(hi - lo) > cfg_.pool_cap) throw std::runtime_error("release pool overflow");
+    spill_reserve(hi - lo);
+    StatsState st = stats_state();
     apm_bucket_append(b.d_tx, lo, hi, &st, min_live, stream_);
+    spill_added_ += hi - lo;
+    spill_marked();
     apm_pool_append(b.d_tx, lo, hi, b.d_gid, d_tail_end_, d_tail_gid_, tail_n_, stream_);
     tail_n_ += hi - lo;
   };
@@ -1742,6 +1857,7 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
       StatsState st = stats_state();
       apm_stats_clear_slot(&st, i, stream_);
       slot_bucket_[i] = NO_BUCKET;
+      spill_clear_at_[i] = spill_added_;
     }
   }
   const int64_t edge_ts = (L - cfg_.buffer - 1) * 10000;
@@ -1817,6 +1933,7 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
     }
   }
   // ---- K8 window statistics over buckets [L-36, L-6]
+  spill_sort();
   WindowArgs wa;
   wa.st = stats_state();
   wa.n_win = (int32_t)(keep_iv - cfg_.buffer + 1);

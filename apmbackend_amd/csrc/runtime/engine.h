@@ -163,6 +163,8 @@ struct EngineMetrics {
   uint64_t spill_dropped = 0;       // samples lost to a full bucket spill list (gpu.bucketOverflowCapacity)
   uint64_t nan_windows_clipped = 0; // NaN windows larger than the JS-emulation scratch (percentiles clipped)
   uint64_t tx_capacity_grows = 0;   // per-batch tx staging doubled (instead of failing the batch)
+  uint64_t spill_grows = 0;         // bucket spill lists grown (instead of dropping window samples)
+  int64_t spill_capacity = 0;       // spill entries per bucket slot (current)
   double t_parse_ms = 0, t_join_ms = 0, t_stats_ms = 0, t_total_ms = 0;
   double t_join_shards_ms = 0, t_merge_ms = 0;                 // split of t_join_ms
   double t_shard_busy_ms = 0, t_shard_max_ms = 0;              // per batch: mean / max of one shard's join
@@ -699,6 +701,27 @@ class Engine {
   int32_t* d_spill_n_ = nullptr;
   int32_t* d_spill_series_ = nullptr;
   int32_t* d_spill_val_ = nullptr;
+  int32_t* d_spill_series_alt_ = nullptr;  // sort target before K8 (swapped with the live lists)
+  int32_t* d_spill_val_alt_ = nullptr;
+  void* d_spill_tmp_ = nullptr;
+  size_t spill_tmp_bytes_ = 0;
+  int32_t* h_spill_snap_ = nullptr;   // pinned [NSLOT], written by K7 after every append
+  int32_t* hd_spill_snap_ = nullptr;  // its device alias
+  // Spill sizing (no sample is ever dropped): spill_n[slot] <= spill_bound(slot) = the exact fill
+  // of the newest completed append snapshot + every sample appended after it (any may spill), or
+  // every sample appended since the slot was cleared.  spill_reserve() grows the lists before an
+  // append whose worst case exceeds them.
+  uint64_t spill_added_ = 0;
+  uint64_t spill_clear_at_[NSLOT] = {};
+  struct SpillMark { hipEvent_t ev = nullptr; uint64_t added = 0; bool live = false; };
+  static constexpr int kSpillMarks = 4;
+  SpillMark spill_mark_[kSpillMarks];
+  int spill_mark_k_ = 0;
+  void spill_reserve(uint32_t n);
+  void spill_marked();
+  void spill_resync();
+  void grow_spill(int32_t cap);
+  void spill_sort();
   unsigned long long* d_spill_drop_ = nullptr;  // K7 samples lost to a full spill list
   uint8_t* d_active_ = nullptr;
   int64_t slot_bucket_[NSLOT];

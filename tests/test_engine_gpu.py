@@ -285,10 +285,8 @@ def test_server_rollup_fuses_window_stats_with_jmx_gauges(servers):
     from apmbackend_amd.utils.records import JmxEntry
     lines, bl = synth_batches(10, duration=500 if servers <= 2 else 200, servers=servers)
     C = small_cfg("exact")
-    # 70 JVMs' hot series overflow small_cfg's 64k-entry spill area (window samples past it are
-    # dropped and that interval's st is wrong): size it for the shard, and check st against the
-    # CPU oracle so the rollup is compared with correct window statistics
-    C["gpu"]["bucketOverflowCapacity"] = 1 << 22
+    # 70 JVMs' hot series overflow small_cfg's 64k-entry spill area: the lists grow (no sample is
+    # lost), and st is checked against the CPU oracle so the rollup sees exact window statistics
     eng = APMEngine(C, keep_text=True)
     syn = SyntheticJmx(5)
     jx = JmxEntry.from_stats(START, "jvm00", syn.payload("jvm00")).to_csv()
@@ -612,27 +610,23 @@ def test_resync_on_matrix_cores_matches_valu_resync():
     assert diff <= len(a) // 200, diff
 
 
-def test_spill_overflow_drops_samples_without_corrupting_windows():
-    """48 JVMs with a 64k-entry spill area: hot series' window samples overflow it.  The lost
-    samples are counted (spill_dropped) and taken out of their cell counts, so K8 never reads
-    unwritten positions: every st value stays within the range of the input's elapsed times
-    (before the fix: percentiles of ~1e9 read from unwritten memory, varying run to run)."""
+def test_spill_lists_grow_and_match_oracle():
+    """48 JVMs with a 64k-entry spill area (1638 per bucket slot): hot series' window samples
+    overflow it.  The reference window is unbounded (stream_calc_stats.js:127-131): the engine
+    grows the spill lists between appends from the device's fill levels (was: samples dropped and
+    counted in spill_dropped), and the sorted-by-series lists give K8 each series' run by binary
+    search.  st / fs equal the CPU oracle."""
     lines, bl = synth_batches(10, duration=120, servers=48)
     C = small_cfg("exact")
     assert C["gpu"]["bucketOverflowCapacity"] == 1 << 16
     P = PipelineOracle(copy.deepcopy(C), UTC)
     P.run_batches(bl)
-    hi = max(float(v) for l in P.stats for v in l.split("|")[5:8] if v != "undefined")
-    eng = APMEngine(C, keep_text=True)
-    st = []
-    for now, chunks in bl:
-        eng.process_lines(chunks, now)
-        st += eng.take("st")
-    assert eng.metrics()["spill_dropped"] > 0
-    assert len(st) == len(P.stats)
-    for l in st:
-        for v in l.split("|")[5:8]:
-            assert v == "undefined" or 0.0 <= float(v) <= hi, l
+    eng, out = _run_engine(C, bl)
+    m = eng.metrics()
+    assert m["spill_grows"] > 0 and m["spill_dropped"] == 0, m
+    assert m["spill_capacity"] > (1 << 16) // 40
+    assert out["st"] == P.stats
+    assert out["fs"] == P.fs
 
 
 def _capacity_corpus(seed=12, servers=2, duration=300):
