@@ -265,12 +265,18 @@ struct PsqlWriter : Writer {
         }
       }
       const double left = t_end - mono_ms();
-      if (left <= 0) { stop(); return "psql did not acknowledge the COPY"; }
+      // the whole COPY (with its terminator) was sent: it may have committed.  A retry could
+      // duplicate every row, so the outcome is reported as unknown ('?') and not retried.
+      if (left <= 0) {
+        stop();
+        return "?psql did not acknowledge the COPY into " + table + " within " + std::to_string((int)(timeout_ms / 1000)) +
+               " s: outcome unknown, not retried (would risk duplicate rows)";
+      }
       struct pollfd p{out, POLLIN, 0};
       if (::poll(&p, 1, (int)left) <= 0) continue;
       char b[4096];
       const ssize_t r = ::read(out, b, sizeof b);
-      if (r <= 0) { stop(); return "psql exited"; }
+      if (r <= 0) { stop(); return "?psql exited before acknowledging the COPY into " + table + ": outcome unknown, not retried"; }
       rbuf.append(b, (size_t)r);
     }
   }
@@ -282,7 +288,7 @@ class DbSink : public ByteSink {
  public:
   DbSink(int64_t limit, double max_wait_ms, std::vector<std::string> tables, std::vector<std::string> columns,
          const std::string& writer, const std::vector<std::string>& arg, uint64_t rotate_bytes, int encoders,
-         int lanes = 1)
+         int lanes = 1, double ack_timeout_ms = 120000.0)
       : limit_(std::max<int64_t>(1, limit)), max_wait_ms_(max_wait_ms), tables_(std::move(tables)),
         columns_(std::move(columns)), lanes_(std::max(1, std::min(lanes, 64))), order_((size_t)lanes_) {
     if (tables_.size() != NT || columns_.size() != NT) throw std::runtime_error("DbSink: 5 tables / column lists");
@@ -292,7 +298,7 @@ class DbSink : public ByteSink {
     for (int l = 0; l < lanes_; ++l) {
       if (writer == "null") w_.emplace_back(new NullWriter());
       else if (writer == "spool") w_.emplace_back(new SpoolWriter(arg.at(0), rotate_bytes, l ? ".lane" + std::to_string(l) : ""));
-      else if (writer == "psql") w_.emplace_back(new PsqlWriter(arg, 120000.0));
+      else if (writer == "psql") w_.emplace_back(new PsqlWriter(arg, ack_timeout_ms));
       else throw std::runtime_error("DbSink: unknown writer " + writer);
     }
     for (int i = 0; i < std::max(1, encoders); ++i) enc_.emplace_back([this] { encode_loop(); });
@@ -532,6 +538,8 @@ class DbSink : public ByteSink {
     for (auto& b : buf_) buffered += b.n;
     d["buffered"] = buffered;
     d["last_error"] = last_error_;
+    d["doubtful_rows"] = doubtful_rows_;
+    d["doubtful_flushes"] = doubtful_flushes_;
     return d;
   }
 
@@ -666,11 +674,17 @@ class DbSink : public ByteSink {
         if (ok < run.size()) {
           failures_ += (int64_t)(run.size() - ok);
           last_error_ = err;
+          size_t retry_from = ok;
+          if (!err.empty() && err[0] == '?') {  // outcome unknown: that flush is not retried
+            doubtful_rows_ += run[ok]->n;
+            ++doubtful_flushes_;
+            retry_from = ok + 1;
+          }
           // back to the front of its buffer, in order (:310-320)
           Buf& b = buf_[t];
           std::string back;
           int64_t n = 0;
-          for (size_t i = ok; i < run.size(); ++i) {
+          for (size_t i = retry_from; i < run.size(); ++i) {
             back += encoded_[t] ? run[i]->encoded : run[i]->lines;
             n += run[i]->n;
           }
@@ -717,6 +731,7 @@ class DbSink : public ByteSink {
   std::vector<std::thread> enc_;
   std::vector<std::thread> wr_;
   int64_t rows_ = 0, flushes_ = 0, failures_ = 0, not_db_ = 0, bytes_ = 0, rows_mark_ = 0;
+  int64_t doubtful_rows_ = 0, doubtful_flushes_ = 0;  // psql flushes whose commit is unknown (not retried)
   double ms_ = 0, ms_mark_ = 0;
   std::string last_error_;
 };
@@ -739,9 +754,10 @@ void register_dbsink(py::module_& m) {
   using apm::Engine;
   py::class_<DbSink, std::shared_ptr<DbSink>>(m, "DbSink")
       .def(py::init<int64_t, double, std::vector<std::string>, std::vector<std::string>, std::string,
-                    std::vector<std::string>, uint64_t, int, int>(),
+                    std::vector<std::string>, uint64_t, int, int, double>(),
            py::arg("limit"), py::arg("max_wait_ms"), py::arg("tables"), py::arg("columns"), py::arg("writer"),
-           py::arg("arg"), py::arg("rotate_bytes") = 1ull << 30, py::arg("encoders") = 2, py::arg("lanes") = 1)
+           py::arg("arg"), py::arg("rotate_bytes") = 1ull << 30, py::arg("encoders") = 2, py::arg("lanes") = 1,
+           py::arg("ack_timeout_ms") = 120000.0)
       .def("consume", [](DbSink& s, py::bytes b) {
         std::string_view v = b;
         py::gil_scoped_release rel;

@@ -2918,7 +2918,9 @@ void Engine::fleet_exchange_upto(uint64_t rounds) {
                                    : fleet_elems_;
     if (!fleet_skip_solo_ && n_red) coll_->all_reduce_f64(fleet_buf_[slot], n_red, /*max=*/false, coll_stream_);
     if (pack_edge_[slot] && want(OUT_FB) && coll_->rank() == 0) fleet_emit_fb(slot);
-    if (pack_edge_[slot]) node_metrics_round();  // (edges are identical on every lock-step rank)
+    // edges are identical on every rank only in lock-step mode (fleet_setup refuses multi-rank
+    // without it): the extra all-reduce must never pair with another rank's fleet all-reduce
+    if (pack_edge_[slot] && (lockstep_ || fleet_nranks_ == 1)) node_metrics_round();
     HIP_OK(hipEventRecord(fleet_ev_[slot], coll_stream_));
     if (node_mode_) node_round(fleet_rounds_, /*wait=*/false);
     ++fleet_rounds_;

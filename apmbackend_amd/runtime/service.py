@@ -387,6 +387,18 @@ class IngestService:
         t0 = time.perf_counter()
         # undelivered output goes out first so the checkpoint and the sinks agree
         self._drain_outputs()
+        if self.inserter is not None and self.mode == "inproc":
+            # the engine's output lane feeds the native sink directly: hand over everything of the
+            # batches this checkpoint covers, then write it (flush + writer drain), so the offsets
+            # below never run ahead of rows the DB has not acknowledged (stream_insert_db.js
+            # persists its buffers on exit for the same reason, :222-244)
+            self.native.flush()
+            self.inserter.flush_all()
+            st = self.inserter.sink_stats()
+            if st.get("buffered", 0) or st.get("queued", 0):
+                log.warning("checkpoint postponed: %s DB rows not written yet (sink failures: %s)",
+                            st.get("buffered", 0) + st.get("queued", 0), st.get("failures"))
+                return None
         if self.qm is not None and not self.qm.wait_confirms(float(self.cfg["gpu"].get("confirmTimeoutSeconds", 60))):
             # offsets may only advance past data the broker has taken responsibility for
             log.warning("checkpoint postponed: the broker has not confirmed every publish yet")
@@ -524,9 +536,17 @@ class IngestService:
         # capacity overflows: window samples past the spill area (gpu.bucketOverflowCapacity) or
         # series past gpu.maxSeries make that interval's statistics wrong -- say so every interval
         lost = {k: int(m.get(k, 0)) for k in ("spill_dropped", "series_overflow_tx", "tx_dropped")}
+        j = m.get("join", {})
+        lost.update({f"join_{k}": int(j.get(k, 0)) for k in ("partial_overflow", "need_overflow", "table_full",
+                                                           "pool_exhausted")})
         if any(lost.values()):
-            log.warning("ENGINE capacity exceeded (totals): %s -- raise gpu.bucketOverflowCapacity / gpu.maxSeries",
+            log.warning("ENGINE capacity exceeded (totals): %s -- raise gpu.maxSeries (the other structures grow)",
                      ", ".join(f"{k}={v}" for k, v in lost.items()))
+        grows = {"spill": int(m.get("spill_grows", 0)),
+                 **{k: int(j.get(k + "_grows", 0)) for k in ("table", "arena", "pool")}}
+        if grows != getattr(self, "_grows_prev", grows):
+            log.info("ENGINE capacity grown (totals): %s", ", ".join(f"{k}={v}" for k, v in grows.items()))
+        self._grows_prev = grows
         nm = list(self.native.node_metrics()) if hasattr(self.native, "node_metrics") else []
         if nm and nm[0] > 1 and getattr(self, "rank", 0) == 0:
             prev_nm = getattr(self, "_nm_prev", None) or [0.0] * len(nm)

@@ -402,7 +402,8 @@ class DBInserter:
                 self.core = N.DbSink(self._limit, self._max_wait_s * 1000.0, [self.tables[t] for t in TYPES],
                                      [", ".join(COLUMNS[t][1]) for t in TYPES], kind, args,
                                      int(ic.get("copySinkRotateBytes", 1 << 30)), int(ic.get("encoderThreads", 2)),
-                                     int(ic.get("writerLanes", 1)))
+                                     int(ic.get("writerLanes", 1)),
+                                     float(ic.get("psqlAckTimeoutSeconds", 120)) * 1000.0)
             else:
                 self._writer = make_writer(ic)
         if self.resume_path:

@@ -287,13 +287,13 @@ def main():
             notifier.add_lines(al.decode("utf-8").split("\n"))
             notifier.tick()
         inserter.flush_all()
+    if fleet is not None:
+        fleet.drain_alerts()  # the last batch's node-wide alert decision is part of the work timed
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    if fleet is not None:
-        fleet.drain_alerts()  # untimed: decide the last batch's node-wide alert candidates
     m1 = eng.metrics()
     lines = m1["lines"] - m0["lines"]
     out_bytes = {k: eng.eng.sink_bytes(k) for k in outs}
@@ -351,6 +351,10 @@ def main():
             # capacity overflows (must be 0: a dropped window sample makes that interval's st wrong)
             "spill_dropped": int(m1.get("spill_dropped", 0)),
             "series_overflow_tx": int(m1.get("series_overflow_tx", 0)),
+            "join_lost": {k: int(m1["join"].get(k, 0)) for k in ("partial_overflow", "need_overflow", "table_full",
+                                                                 "pool_exhausted")},
+            "capacity_grows": {"spill": int(m1.get("spill_grows", 0)),
+                               **{k: int(m1["join"].get(k + "_grows", 0)) for k in ("table", "arena", "pool")}},
             "alerts": int(m1["alerts"] - m0["alerts"]),
             "alert_candidates": int(m1["alert_candidates"] - m0["alert_candidates"]),
             "device_GB": round(eng.eng.device_bytes() / 1e9, 1),

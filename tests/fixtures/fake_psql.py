@@ -8,11 +8,13 @@ import sys
 
 out_dir = os.environ["FAKE_PSQL_OUT"]
 fail = os.environ.get("FAKE_PSQL_FAIL", "")
-table, rows, err = None, [], False
+hang = os.environ.get("FAKE_PSQL_HANG", "")  # commits this table's rows, then never acknowledges
+table, rows, err, last = None, [], False, None
 for line in sys.stdin:
     if table is not None:
         if line == "\\.\n":
             err = table == fail
+            last = table
             if not err:
                 with open(os.path.join(out_dir, table + ".rows"), "a") as f:
                     f.write("".join(rows))
@@ -27,6 +29,9 @@ for line in sys.stdin:
                 f.write(f"{os.getpid()}\n")
         table = line.split()[1]
     elif line.startswith("\\echo APMACK"):
+        if hang and last == hang:
+            import time
+            time.sleep(60)
         n = line.split()[2]
         sys.stdout.write(f"APMACK {n} {'true' if err else 'false'}\n")
         sys.stdout.flush()

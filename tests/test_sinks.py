@@ -393,3 +393,31 @@ def test_native_sink_psql_writer_lanes_use_one_connection_each(tmp_path, monkeyp
     want = sinks.copy_encode_lines(lines)["tx"]
     assert sorted(open(out / "apm_tx.rows").read().splitlines(keepends=True)) == sorted(want)
     assert len(set(open(out / "connections").read().split())) == 3
+
+
+def test_native_sink_psql_unacknowledged_copy_is_not_retried(tmp_path, monkeypatch):
+    """a COPY whose acknowledgement never arrives may have committed (the whole
+    COPY and its terminator were sent).  Re-buffering it duplicated its rows in the DB; now the
+    flush is reported as 'outcome unknown' (doubtful_rows), not retried, and the timeout is
+    streamInsertDb.psqlAckTimeoutSeconds."""
+    import sys
+    out = tmp_path / "pg"
+    out.mkdir()
+    monkeypatch.setenv("FAKE_PSQL_OUT", str(out))
+    monkeypatch.setenv("FAKE_PSQL_HANG", "apm_stats")
+    from apmbackend_amd import _native
+    N = _native.load(build_if_missing=False)
+    fake = [sys.executable, os.path.join(os.path.dirname(__file__), "fixtures", "fake_psql.py")]
+    s = N.DbSink(1000, 1e9, ["apm_tx", "apm_stats", "apm_alerts", "apm_jmx", "apm_fleet_stats"], ["a", "b", "c", "d", "e"],
+                 "psql", fake, 0, 2, 1, 500.0)
+    lines = _wire_lines(10)
+    s.consume(("\n".join(lines) + "\n").encode())
+    s.flush_all()
+    s.drain()
+    st = s.stats()
+    assert st["doubtful_rows"] == 10 and st["doubtful_flushes"] == 1
+    assert st["buffered"] == 0  # not re-buffered: no duplicate on the next flush
+    assert "outcome unknown" in st["last_error"]
+    want = sinks.copy_encode_lines(lines)
+    assert open(out / "apm_stats.rows").read() == "".join(want["fs"])  # committed exactly once
+    s.close()
