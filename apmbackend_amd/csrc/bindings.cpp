@@ -263,6 +263,27 @@ PYBIND11_MODULE(_apm_native, m) {
   }, py::arg("data"), py::arg("seed") = kHashSeed);
   m.attr("NSLOT") = NSLOT;
 
+  // TCP host transport on host buffers (CPU tests of the multi-process collective path)
+  py::class_<Collective>(m, "HostCollective")
+      .def(py::init([](const std::string& addr, int port, int n, int rank, double timeout_ms) {
+             py::gil_scoped_release rel;
+             return make_host_collective(addr, port, n, rank, timeout_ms).release();
+           }),
+           py::arg("addr"), py::arg("port"), py::arg("nranks"), py::arg("rank"), py::arg("timeout_ms") = 30000.0)
+      .def("all_reduce", [](Collective& c, std::vector<double> v, bool max) {
+        py::gil_scoped_release rel;
+        return c.all_reduce_host(v, max);
+      }, py::arg("values"), py::arg("max") = false)
+      .def("all_gather", [](Collective& c, py::bytes b) {
+        std::string s = b;
+        std::vector<uint8_t> v(s.begin(), s.end()), out;
+        { py::gil_scoped_release rel; out = c.all_gather_host(v); }
+        return py::bytes((const char*)out.data(), out.size());
+      })
+      .def("abort", &Collective::abort)
+      .def("aborted", &Collective::aborted)
+      .def_property_readonly("rank", &Collective::rank)
+      .def_property_readonly("nranks", &Collective::nranks);
   py::class_<LocalGroup, std::shared_ptr<LocalGroup>>(m, "LocalCollGroup")
       .def(py::init([](int n, double timeout_ms) { return make_local_group(n, timeout_ms); }), py::arg("n"),
            py::arg("timeout_ms") = 120000.0);
@@ -429,6 +450,11 @@ PYBIND11_MODULE(_apm_native, m) {
         py::gil_scoped_release rel;
         e.fleet_init_local(std::move(g), rank, cap, lockstep);
       }, py::arg("group"), py::arg("rank"), py::arg("cap"), py::arg("lockstep") = true)
+      .def("fleet_init_host", [](Engine& e, const std::string& addr, int port, int nranks, int rank, int32_t cap,
+                                 bool lockstep) {
+        py::gil_scoped_release rel;
+        e.fleet_init_host(addr, port, nranks, rank, cap, lockstep);
+      }, py::arg("addr"), py::arg("port"), py::arg("nranks"), py::arg("rank"), py::arg("cap"), py::arg("lockstep") = true)
       .def("set_server_index", &Engine::set_server_index)
       .def("node_drain", [](Engine& e) { py::gil_scoped_release rel; e.node_drain(); })
       .def("pack_service_moments", [](Engine& e, uintptr_t dst, int32_t cap, bool atomic_path) {

@@ -1,5 +1,16 @@
-// Collective backends: RCCL (production) and an in-process rendezvous (tests).
+// Collective backends: RCCL (production), TCP host transport (multi-process on one GPU), and an
+// in-process rendezvous (tests).
 #include "collective.h"
+
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <thread>
 
 #include <rccl/rccl.h>
 
@@ -162,6 +173,240 @@ class LocalCollective final : public Collective {
 
 std::unique_ptr<Collective> make_local_collective(std::shared_ptr<LocalGroup> g, int rank) {
   return std::unique_ptr<Collective>(new LocalCollective(std::move(g), rank));
+}
+
+}  // namespace apm
+
+// --------------------------------------------------------------------- host transport (TCP)
+
+namespace apm {
+namespace {
+
+double mono_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+class HostCollective final : public Collective {
+ public:
+  HostCollective(const std::string& addr, int port, int nranks, int rank, double timeout_ms)
+      : n_(nranks), r_(rank), timeout_ms_(timeout_ms), fd_((size_t)std::max(nranks, 1), -1) {
+    if (rank < 0 || rank >= nranks) throw std::runtime_error("host collective: rank out of range");
+    if (nranks == 1) return;
+    sockaddr_in sa{};
+    sa.sin_family = AF_INET;
+    sa.sin_port = htons((uint16_t)port);
+    if (inet_pton(AF_INET, addr.c_str(), &sa.sin_addr) != 1) throw std::runtime_error("host collective: bad address " + addr);
+    const double t_end = mono_ms() + timeout_ms_;
+    if (rank == 0) {
+      const int ls = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+      if (ls < 0) throw std::runtime_error("host collective: socket failed");
+      const int one = 1;
+      ::setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+      if (::bind(ls, (sockaddr*)&sa, sizeof sa) != 0 || ::listen(ls, nranks) != 0) {
+        const std::string e = std::strerror(errno);
+        ::close(ls);
+        throw std::runtime_error("host collective: cannot listen on " + addr + ":" + std::to_string(port) + ": " + e);
+      }
+      for (int got = 1; got < nranks;) {
+        pollfd p{ls, POLLIN, 0};
+        const double left = t_end - mono_ms();
+        if (left <= 0 || ::poll(&p, 1, (int)left) <= 0) {
+          ::close(ls);
+          shutdown_all();
+          throw std::runtime_error("host collective: only " + std::to_string(got) + " of " + std::to_string(nranks) +
+                                   " ranks connected in time");
+        }
+        const int c = ::accept4(ls, nullptr, nullptr, SOCK_CLOEXEC);
+        if (c < 0) continue;
+        int32_t peer = -1;
+        if (!recv_all(c, &peer, 4, t_end) || peer <= 0 || peer >= nranks || fd_[(size_t)peer] >= 0) {
+          ::close(c);
+          continue;
+        }
+        tune(c);
+        fd_[(size_t)peer] = c;
+        ++got;
+      }
+      ::close(ls);
+    } else {
+      for (;;) {
+        const int c = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+        if (c < 0) throw std::runtime_error("host collective: socket failed");
+        if (::connect(c, (sockaddr*)&sa, sizeof sa) == 0) {
+          tune(c);
+          const int32_t me = rank;
+          if (!send_all(c, &me, 4)) { ::close(c); throw std::runtime_error("host collective: hello failed"); }
+          fd_[0] = c;
+          break;
+        }
+        ::close(c);
+        if (mono_ms() > t_end) throw std::runtime_error("host collective: rank 0 not reachable at " + addr + ":" + std::to_string(port));
+        std::this_thread::sleep_for(std::chrono::milliseconds(20));
+      }
+    }
+  }
+  ~HostCollective() override { shutdown_all(); }
+  int nranks() const override { return n_; }
+  int rank() const override { return r_; }
+
+  void all_reduce_f64(double* buf, size_t n, bool max, hipStream_t s) override {
+    std::vector<double> mine(n);
+    HIP_OK(hipStreamSynchronize(s));
+    HIP_OK(hipMemcpy(mine.data(), buf, n * 8, hipMemcpyDeviceToHost));
+    const std::vector<double> out = all_reduce_host(mine, max);
+    HIP_OK(hipMemcpy(buf, out.data(), n * 8, hipMemcpyHostToDevice));
+  }
+
+  void all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    std::vector<uint8_t> mine(bytes);
+    HIP_OK(hipStreamSynchronize(s));
+    HIP_OK(hipMemcpy(mine.data(), send, bytes, hipMemcpyDeviceToHost));
+    const std::vector<uint8_t> out = all_gather_host(mine);
+    HIP_OK(hipMemcpy(recv, out.data(), out.size(), hipMemcpyHostToDevice));
+  }
+
+  // rank 0 reduces in rank order: the same bits on every rank, every run
+  std::vector<double> all_reduce_host(const std::vector<double>& v, bool max) override {
+    const size_t n = v.size();
+    std::vector<uint8_t> mine(n * 8);
+    std::memcpy(mine.data(), v.data(), n * 8);
+    const std::vector<uint8_t> out = exchange(max ? 1u : 2u, std::move(mine), [&](std::vector<std::vector<uint8_t>>& all) {
+      std::vector<uint8_t> r(all[0]);
+      double* o = (double*)r.data();
+      for (size_t k = 1; k < all.size(); ++k) {
+        const double* a = (const double*)all[k].data();
+        for (size_t i = 0; i < n; ++i) o[i] = max ? (a[i] > o[i] ? a[i] : o[i]) : o[i] + a[i];
+      }
+      return r;
+    });
+    std::vector<double> res(n);
+    std::memcpy(res.data(), out.data(), n * 8);
+    return res;
+  }
+
+  std::vector<uint8_t> all_gather_host(const std::vector<uint8_t>& v) override {
+    const size_t bytes = v.size();
+    return exchange(3u, std::vector<uint8_t>(v), [&](std::vector<std::vector<uint8_t>>& all) {
+      std::vector<uint8_t> r(bytes * all.size());
+      for (size_t k = 0; k < all.size(); ++k) std::memcpy(r.data() + k * bytes, all[k].data(), bytes);
+      return r;
+    });
+  }
+
+  std::string async_error() override { return aborted_ ? "host collective aborted: " + err_ : ""; }
+  void abort() override {
+    if (err_.empty()) err_ = "aborted";
+    aborted_ = true;
+    shutdown_all();
+  }
+  bool aborted() const override { return aborted_; }
+
+ private:
+  struct Hdr { uint32_t magic, op; uint64_t seq, bytes; };
+  static constexpr uint32_t kMagic = 0x41504d43;  // "APMC"
+
+  static void tune(int fd) {
+    const int one = 1;
+    ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+  }
+  static bool send_all(int fd, const void* p, size_t n) {
+    const char* c = (const char*)p;
+    while (n) {
+      const ssize_t w = ::send(fd, c, n, MSG_NOSIGNAL);
+      if (w < 0 && errno == EINTR) continue;
+      if (w <= 0) return false;
+      c += w;
+      n -= (size_t)w;
+    }
+    return true;
+  }
+  // false on EOF / error / deadline
+  static bool recv_all(int fd, void* p, size_t n, double t_end) {
+    char* c = (char*)p;
+    while (n) {
+      pollfd q{fd, POLLIN, 0};
+      const double left = t_end - mono_ms();
+      if (left <= 0) return false;
+      const int pr = ::poll(&q, 1, (int)std::min(left, 1000.0));
+      if (pr < 0 && errno == EINTR) continue;
+      if (pr <= 0) continue;
+      const ssize_t r = ::recv(fd, c, n, 0);
+      if (r < 0 && (errno == EINTR || errno == EAGAIN)) continue;
+      if (r <= 0) return false;
+      c += r;
+      n -= (size_t)r;
+    }
+    return true;
+  }
+  void shutdown_all() {
+    for (int& f : fd_) {
+      if (f >= 0) { ::shutdown(f, SHUT_RDWR); ::close(f); f = -1; }
+    }
+  }
+  [[noreturn]] void fail(const std::string& why) {
+    err_ = why;
+    aborted_ = true;
+    shutdown_all();
+    throw std::runtime_error("host collective: " + why);
+  }
+
+  template <class F>
+  std::vector<uint8_t> exchange(uint32_t op, std::vector<uint8_t>&& mine, F&& combine) {
+    if (aborted_) throw std::runtime_error("host collective aborted: " + err_);
+    const uint64_t seq = ++seq_;
+    if (n_ == 1) {
+      std::vector<std::vector<uint8_t>> all(1);
+      all[0] = std::move(mine);
+      return combine(all);
+    }
+    const double t_end = mono_ms() + timeout_ms_;
+    const Hdr h{kMagic, op, seq, (uint64_t)mine.size()};
+    if (r_ != 0) {
+      if (!send_all(fd_[0], &h, sizeof h) || !send_all(fd_[0], mine.data(), mine.size()))
+        fail("rank 0 closed its connection (peer process gone)");
+      Hdr rh{};
+      if (!recv_all(fd_[0], &rh, sizeof rh, t_end))
+        fail(mono_ms() >= t_end ? "no reply from rank 0 within the collective timeout"
+                                : "rank 0 closed its connection (peer process gone)");
+      if (rh.magic != kMagic || rh.op != op || rh.seq != seq) fail("protocol mismatch (ranks issued different collectives)");
+      std::vector<uint8_t> out(rh.bytes);
+      if (!recv_all(fd_[0], out.data(), out.size(), t_end)) fail("rank 0 connection lost mid-message");
+      return out;
+    }
+    std::vector<std::vector<uint8_t>> all((size_t)n_);
+    all[0] = std::move(mine);
+    for (int r = 1; r < n_; ++r) {
+      Hdr ph{};
+      if (!recv_all(fd_[(size_t)r], &ph, sizeof ph, t_end))
+        fail(mono_ms() >= t_end ? "rank " + std::to_string(r) + " did not arrive within the collective timeout"
+                                : "rank " + std::to_string(r) + " closed its connection (peer process gone)");
+      if (ph.magic != kMagic || ph.op != op || ph.seq != seq || ph.bytes != h.bytes)
+        fail("protocol mismatch with rank " + std::to_string(r) + " (ranks issued different collectives)");
+      all[(size_t)r].resize(ph.bytes);
+      if (!recv_all(fd_[(size_t)r], all[(size_t)r].data(), ph.bytes, t_end))
+        fail("rank " + std::to_string(r) + " connection lost mid-message");
+    }
+    std::vector<uint8_t> out = combine(all);
+    const Hdr oh{kMagic, op, seq, (uint64_t)out.size()};
+    for (int r = 1; r < n_; ++r)
+      if (!send_all(fd_[(size_t)r], &oh, sizeof oh) || !send_all(fd_[(size_t)r], out.data(), out.size()))
+        fail("rank " + std::to_string(r) + " closed its connection (peer process gone)");
+    return out;
+  }
+
+  int n_, r_;
+  double timeout_ms_;
+  std::vector<int> fd_;  // rank 0: one per peer; others: [0] = rank 0
+  uint64_t seq_ = 0;
+  bool aborted_ = false;
+  std::string err_;
+};
+
+}  // namespace
+
+std::unique_ptr<Collective> make_host_collective(const std::string& addr, int port, int nranks, int rank,
+                                                 double timeout_ms) {
+  return std::unique_ptr<Collective>(new HostCollective(addr, port, nranks, rank, timeout_ms));
 }
 
 }  // namespace apm

@@ -1,7 +1,9 @@
 // Collective backend of the engine's node-wide exchanges (lock-step clocks, fleet moments,
 // node-wide alert candidates).  Production: one RCCL communicator per rank over xGMI
-// (RcclCollective).  Tests: LocalCollective -- N engines of ONE process (one GPU) joined through
-// a host rendezvous, so a 2/4-rank node can be checked against a 1-rank run without 2/4 GPUs.
+// (RcclCollective).  Host transport: HostCollective -- one process per rank joined by TCP
+// through rank 0 (ranks sharing one GPU, or nodes without a working RCCL path); it is how the
+// multi-PROCESS node is exercised on a one-GPU box.  Tests: LocalCollective -- N engines of ONE
+// process (one GPU) joined through a host rendezvous.
 //
 // Every call is issued by the engine's ingest thread in a fixed per-batch sequence (see
 // Engine::fleet_exchange_upto), which makes the call order identical on every rank.
@@ -12,6 +14,7 @@
 #include <cstdint>
 #include <mutex>
 #include <memory>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -31,6 +34,13 @@ class Collective {
   // unblock / release a wedged communicator; later calls throw
   virtual void abort() = 0;
   virtual bool aborted() const = 0;
+  // host-buffer variants (HostCollective: CPU tests of the transport without a GPU)
+  virtual std::vector<double> all_reduce_host(const std::vector<double>&, bool) {
+    throw std::runtime_error("host-buffer collectives: HostCollective only");
+  }
+  virtual std::vector<uint8_t> all_gather_host(const std::vector<uint8_t>&) {
+    throw std::runtime_error("host-buffer collectives: HostCollective only");
+  }
 };
 
 std::vector<uint8_t> rccl_unique_id();
@@ -54,6 +64,14 @@ struct LocalGroup {
   void rendezvous(std::unique_lock<std::mutex>& lk);  // blocks until all n ranks called it
 };
 std::shared_ptr<LocalGroup> make_local_group(int n, double timeout_ms = 120000.0);
+
+// TCP star through rank 0 (`addr`:`port`): rank 0 listens, the others connect (retrying until
+// `timeout_ms`).  Every call is synchronous on the host: the stream is drained, the buffer copied
+// to the host, exchanged, reduced by rank 0 in rank order (deterministic) and copied back.  A peer
+// that closes its connection (process gone) or does not arrive within `timeout_ms` makes the call
+// throw after shutting every connection down, so the remaining ranks fail the same way.
+std::unique_ptr<Collective> make_host_collective(const std::string& addr, int port, int nranks, int rank,
+                                                 double timeout_ms);
 std::unique_ptr<Collective> make_local_collective(std::shared_ptr<LocalGroup> g, int rank);
 
 }  // namespace apm

@@ -2778,6 +2778,15 @@ void Engine::fleet_init_local(std::shared_ptr<LocalGroup> group, int rank, int32
   fleet_setup(cap, lockstep);
 }
 
+void Engine::fleet_init_host(const std::string& addr, int port, int nranks, int rank, int32_t cap, bool lockstep) {
+  flush();
+  if (coll_) throw std::runtime_error("fleet_init called twice");
+  if (cap <= 0) throw std::runtime_error("fleet_init: cap must be > 0");
+  HIP_OK(hipSetDevice(cfg_.device));
+  coll_ = make_host_collective(addr, port, nranks, rank, cfg_.coll_timeout_ms);
+  fleet_setup(cap, lockstep);
+}
+
 void Engine::fleet_setup(int32_t cap, bool lockstep) {
   const int nranks = coll_->nranks();
   // Highest priority: with GPU_MAX_HW_QUEUES = 4 the engine's streams share hardware queues, and

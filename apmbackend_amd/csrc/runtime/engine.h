@@ -329,6 +329,8 @@ class Engine {
   std::vector<double> node_metrics();
   // Same exchange over an in-process group (tests: N engines of one process share one GPU).
   void fleet_init_local(std::shared_ptr<LocalGroup> group, int rank, int32_t n_services_cap, bool lockstep);
+  // one process per rank over the TCP host transport (collective.h: HostCollective)
+  void fleet_init_host(const std::string& addr, int port, int nranks, int rank, int32_t n_services_cap, bool lockstep);
   // Position of `server` in the node-wide server list (ranks own disjoint slices of it).  The
   // node-wide alert order ranks servers by (first batch with a series, this index); default =
   // local registration order, which is the global order on a single rank.

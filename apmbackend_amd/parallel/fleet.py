@@ -57,10 +57,15 @@ class FleetBaseline:
     """
 
     def __init__(self, engine, world: int, rank: int, max_services: Optional[int] = None, group=None,
-                 lockstep: bool = True, local_group=None, servers: Optional[Sequence[str]] = None):
+                 lockstep: bool = True, local_group=None, servers: Optional[Sequence[str]] = None,
+                 backend: Optional[str] = None):
         """``local_group`` (tests): a ``LocalCollGroup`` joining N engines of this process instead
         of RCCL.  ``servers``: the node-wide server list -- each owned server's position in it
-        orders the node-wide alert decisions (default: this rank's registration order)."""
+        orders the node-wide alert decisions (default: this rank's registration order).
+        ``backend``: ``rccl`` (default; ``gpu.collectiveBackend``) or ``host`` -- the TCP host
+        transport through rank 0 at MASTER_ADDR : MASTER_PORT + 11 (``APM_HOST_COLL_PORT``
+        overrides), for ranks sharing a GPU or nodes without an RCCL path; no torch.distributed
+        group is needed for it."""
         self.eng = engine
         self.world = world
         self.n_lags = len(engine.ecfg["lags"])
@@ -73,6 +78,15 @@ class FleetBaseline:
         if local_group is not None:
             engine.eng.fleet_init_local(local_group, rank, self.cap, lockstep)
             return
+        backend = backend or str(engine.cfg.get("gpu", {}).get("collectiveBackend", "rccl"))
+        if backend == "host":
+            import os
+            addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+            port = int(os.environ.get("APM_HOST_COLL_PORT") or int(os.environ.get("MASTER_PORT", "29500")) + 11)
+            engine.eng.fleet_init_host(addr, port, world, rank, self.cap, lockstep)
+            return
+        if backend != "rccl":
+            raise ValueError(f"unknown collective backend {backend!r} (rccl / host)")
         import torch.distributed as dist
         native = type(engine.eng)
         obj = [(native.fleet_unique_id(), native.fleet_unique_id() if lockstep else b"") if rank == 0 else None]

@@ -162,3 +162,61 @@ def test_sharded_ranks_reproduce_single_rank_per_series(world):
         assert r[6] == {"al": float(len(full.al)), "fs": float(len(full.fs))}
     mean, std, n = merged_stats(want)
     assert (n[:, 0, 0] > 0).all()
+
+
+def _host_coll_worker(rank, world, port, die_rank, out_q):
+    from apmbackend_amd import _native
+    N = _native.load(build_if_missing=False)
+    try:
+        c = N.HostCollective("127.0.0.1", port, world, rank, 20000.0)
+        vals = [float(rank + 1) * 0.1, float(-rank), 2.0 ** -(rank + 3)]
+        s = c.all_reduce(vals, False)
+        m = c.all_reduce(vals, True)
+        g = c.all_gather(bytes([rank]) * 3)
+        res = {"sum": s, "max": m, "gather": g}
+        if rank == die_rank:
+            os._exit(9)  # a crash: no goodbye, the kernel closes the socket
+        try:
+            c.all_reduce(vals, False)
+            res["after"] = "ok"
+        except Exception as e:  # the survivors must fail promptly, not hang
+            res["after"] = str(e)
+        out_q.put((rank, res))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        out_q.put((rank, {"error": repr(e)}))
+
+
+@pytest.mark.parametrize("world,die", [(2, -1), (4, -1), (4, 2), (3, 0)])
+def test_host_collective_transport_across_processes(world, die):
+    """HostCollective (the engine's TCP transport for ranks sharing a GPU): SUM reduced by rank 0
+    in rank order (bit-identical on every rank), MAX, all-gather in rank order; a rank process
+    that dies makes every survivor's next collective fail at once (peer gone), which is what the
+    engine's watchdog turns into abort + non-zero exit."""
+    import time
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_host_coll_worker, args=(r, world, port, die, q)) for r in range(world)]
+    t0 = time.time()
+    for p in procs:
+        p.start()
+    alive = world - (1 if die >= 0 else 0)
+    res = dict(q.get(timeout=120) for _ in range(alive))
+    for p in procs:
+        p.join(60)
+    assert time.time() - t0 < 60  # no survivor waited for the 20 s collective timeout... twice
+    want_sum = [0.0, 0.0, 0.0]
+    for r in range(world):
+        v = [float(r + 1) * 0.1, float(-r), 2.0 ** -(r + 3)]
+        want_sum = [a + b for a, b in zip(want_sum, v)]
+    for r, d in res.items():
+        assert "error" not in d, d
+        assert d["sum"] == want_sum  # same order of additions as rank 0's loop
+        assert d["max"] == [world * 0.1, 0.0, 0.125]
+        assert d["gather"] == b"".join(bytes([k]) * 3 for k in range(world))
+        if die < 0:
+            assert d["after"] == "ok"
+        else:
+            assert "closed its connection" in d["after"] or "connection lost" in d["after"], d["after"]
+    if die >= 0:
+        assert procs[die].exitcode == 9

@@ -178,3 +178,140 @@ def test_fleet_registry_merges_services_node_wide(world):
     key = lambda l: (l.split("|")[2], l.split("|")[3])
     assert sorted(map(key, last)) == sorted(map(key, ref_last))
     assert engs[0].eng.fleet_info()["fb_rows"] == len(fb)
+
+
+# ---------------------------------------------------------------- multi-PROCESS node (TCP transport)
+import json  # noqa: E402
+import os  # noqa: E402
+import socket  # noqa: E402
+import subprocess  # noqa: E402
+import sys  # noqa: E402
+import time  # noqa: E402
+
+FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures")
+sys.path.insert(0, FIX)
+import node_rank  # noqa: E402
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_env(rank, world, port):
+    env = dict(os.environ)
+    env.update(RANK=str(rank), LOCAL_RANK="0", WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+               PYTHONUNBUFFERED="1")
+    return env
+
+
+def _process_outputs(out, world):
+    outs = []
+    for r in range(world):
+        d = {}
+        for k in node_rank.KINDS:
+            with open(os.path.join(out, f"rank{r}.{k}")) as f:
+                d[k] = [l for l in f.read().split("\n") if l]
+        outs.append(d)
+    return outs
+
+
+def _assert_node_equals_oracle(outs, P):
+    for name, want in (("st", P.stats), ("fs", P.fs)):
+        got = collections.defaultdict(list)
+        for o in outs:
+            for k, v in per_series(o[name]).items():
+                got[k] += v
+        assert got == per_series(want), name
+    assert sorted(l for o in outs for l in o["al"]) == sorted(P.al)
+
+
+def _oracle():
+    lines, bl = node_rank.corpus()
+    P = PipelineOracle(copy.deepcopy(node_rank.node_cfg()), UTC)
+    P.run_batches(bl)
+    assert {"S:getSvc0001", "S:getSvc0002"} <= {l.split("|")[4] for l in P.al}
+    return P
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_process_node_over_host_transport_matches_single_process(tmp_path, world):
+    """`world` OS processes, one native engine each on the shared GPU, node-wide exchanges over the
+    TCP host transport (HostCollective): the per-series st / fs streams and the alerts (default
+    15-minute node-wide cooldown) equal the single-stream oracle -- the multi-process node of
+    BASELINE config 3, executed instead of simulated by threads."""
+    P = _oracle()
+    out = str(tmp_path / "node")
+    port = _free_port()
+    procs = [subprocess.Popen([sys.executable, os.path.join(FIX, "node_rank.py"), out, "--ckpt-every", "0",
+                               "--idle", "0"], env=_rank_env(r, world, port), stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT) for r in range(world)]
+    try:
+        logs = [p.communicate(timeout=400)[0].decode() for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert all(p.returncode == 0 for p in procs), logs
+    _assert_node_equals_oracle(_process_outputs(out, world), P)
+    done = [json.load(open(os.path.join(out, f"done.rank{r}"))) for r in range(world)]
+    assert sum(d["alerts"] for d in done) == len(P.al)
+    assert sum(d["alert_candidates"] for d in done) > len(P.al)  # the cooldown was decided node-wide
+    nm = done[0]["node_metrics"]
+    assert nm[0] == world and all(d["node_metrics"][0] == world for d in done)
+
+
+def test_peer_process_death_aborts_the_group_and_supervisor_resumes_from_checkpoints(tmp_path):
+    """A rank process dies mid-run (fault injection: os._exit after batch 110).  The survivor's
+    next collective fails at once (peer gone), it aborts and exits non-zero; the supervisor
+    (apm_manager.js:303-356 semantics, rank group restarted as a whole) restarts the group, every
+    rank resumes from the newest checkpoint the whole group has (batch 80), and the node's output
+    is exactly the uninterrupted one."""
+    from apmbackend_amd.runtime import supervisor as sup
+    from apmbackend_amd.runtime.notifier import Mailer
+    from apmbackend_amd.utils.config import default_config
+    P = _oracle()
+    out = str(tmp_path / "node")
+    C = default_config()
+    C["logDir"] = str(tmp_path / "logs")
+    C["appDirectory"] = FIX
+    C["apmConfigFilePath"] = None
+    C["applicationManager"].update({
+        "moduleSettings": [{"name": "node", "relativePath": "node_rank.py", "ranks": 2, "passConfig": False,
+                            "args": [out, "--ckpt-every", "40", "--kill", "1:110"], "masterPort": _free_port(),
+                            "elasticDegrade": False}],
+        "stateDir": str(tmp_path / "state"), "restartDelaySeconds": 0.5, "crashLoopWindowSeconds": 0.0,
+        "inspectionFrequencySeconds": 3600, "alertCollectionIntervalInSeconds": 3600,
+        "diskSpaceGBAvailableThreshold": 0, "diskSpacePercentageUsedThreshold": 101})
+    s = sup.Supervisor(C, mailer=Mailer(sendmail="/nonexistent", outbox=str(tmp_path / "out")),
+                       annotate=lambda *a: None)
+    s.start_all()
+    mod = s.modules[0]
+    try:
+        t_end = time.time() + 600
+        log0 = ""
+        log_path = os.path.join(C["logDir"], "node.rank0.start.log")
+        while time.time() < t_end and not all(os.path.exists(os.path.join(out, f"done.rank{r}")) for r in range(2)):
+            time.sleep(1.0)  # slow polling: the survivor notices the dead peer on its own first
+            # (a restart truncates the start log, as the reference's openSync(.., 'w') does: keep
+            # the first generation's before the supervisor restarts it)
+            if not log0 and os.path.exists(log_path):
+                txt = open(log_path).read()
+                if "host collective" in txt:
+                    log0 = txt
+            s.check_children()
+        assert all(os.path.exists(os.path.join(out, f"done.rank{r}")) for r in range(2)), "group did not finish"
+        assert os.path.exists(os.path.join(out, "killed"))
+        assert all(p.restarts >= 1 for p in mod.procs)  # the group restarted as a whole
+        assert "peer process gone" in log0, log0[-2000:]
+        assert any("exited: code:17" in a for a in s.alert_buffer), s.alert_buffer
+        assert any("node.rank0" in a and "code:1" in a for a in s.alert_buffer), s.alert_buffer
+        done = [json.load(open(os.path.join(out, f"done.rank{r}"))) for r in range(2)]
+        assert [d["start"] for d in done] == [80, 80]
+    finally:
+        open(os.path.join(out, "stop"), "w").close()
+        s.stop_all()
+    _assert_node_equals_oracle(_process_outputs(out, 2), P)
