@@ -326,6 +326,10 @@ PYBIND11_MODULE(_apm_native, m) {
            }, py::arg("blob"), py::arg("now") = -1.0)
       .def("take", &Engine::take, py::call_guard<py::gil_scoped_release>())
       .def("flush", &Engine::flush, py::call_guard<py::gil_scoped_release>())
+      .def("dump_state", [](Engine& e, const std::string& path, const std::string& reason) {
+        py::gil_scoped_release rel;
+        return e.dump_state(path, reason);
+      })
       .def("save_state", [](Engine& e, const std::string& path, py::bytes extra) {
              std::string x = extra;
              py::gil_scoped_release rel;

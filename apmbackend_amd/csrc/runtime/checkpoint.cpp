@@ -33,7 +33,7 @@ namespace {
 
 enum : uint32_t {
   SEC_CONFIG = 1, SEC_TOPOLOGY, SEC_SERIES, SEC_CLOCK, SEC_JOIN, SEC_PARSE, SEC_BUCKETS, SEC_ZSCORE, SEC_POOL,
-  SEC_ALERTS, SEC_OUTPUTS, SEC_METRICS, SEC_RING, SEC_EXTRA
+  SEC_ALERTS, SEC_OUTPUTS, SEC_METRICS, SEC_RING, SEC_EXTRA, SEC_DUMP = 100
 };
 
 struct SeriesRec { int32_t server, service; uint64_t emit_key; };
@@ -239,6 +239,74 @@ void Engine::checkpoint_quiesce(const char* what) {
   HIP_OK(hipStreamSynchronize(parse_stream_));
   HIP_OK(hipStreamSynchronize(stream_));
   HIP_OK(hipStreamSynchronize(comm_stream_));
+}
+
+uint64_t Engine::dump_state(const std::string& path, const std::string& reason) {
+  std::string j = "{";
+  auto num = [&](const char* k, double v) {
+    char b[64];
+    std::snprintf(b, sizeof b, "%.17g", v);
+    if (j.size() > 1) j += ",";
+    j += "\"" + std::string(k) + "\":" + (v == v && v - v == 0 ? std::string(b) : std::string("null"));
+  };
+  auto arr = [&](const char* k, const std::vector<double>& v) {
+    if (j.size() > 1) j += ",";
+    j += "\"" + std::string(k) + "\":[";
+    for (size_t i = 0; i < v.size(); ++i) {
+      char b[64];
+      std::snprintf(b, sizeof b, "%.17g", v[i]);
+      j += (i ? "," : "") + (v[i] == v[i] && v[i] - v[i] == 0 ? std::string(b) : std::string("null"));
+    }
+    j += "]";
+  };
+  const EngineMetrics& m = metrics_;
+  num("batch_no", (double)batch_no_);
+  num("watermark_ms", watermark_);
+  num("latest_bucket", (double)latest_);
+  num("rollover_idx", (double)rollover_idx_);
+  num("n_series", (double)n_series_);
+  num("max_series", (double)cfg_.max_series);
+  num("device_bytes", (double)device_bytes_);
+  num("batches", (double)m.batches); num("lines", (double)m.lines); num("bytes", (double)m.bytes);
+  num("events", (double)m.events); num("tx", (double)m.tx); num("tx_dropped", (double)m.tx_dropped);
+  num("rollovers", (double)m.rollovers); num("alerts", (double)m.alerts); num("released", (double)m.released);
+  num("series_overflow_tx", (double)m.series_overflow_tx); num("spill_dropped", (double)m.spill_dropped);
+  num("spill_capacity", (double)cfg_.spill_cap); num("spill_grows", (double)m.spill_grows);
+  num("pending_tx", (double)(pool_n_ + tail_n_)); num("pending_tx_capacity", (double)cfg_.pool_cap);
+  {
+    std::vector<double> sb(NSLOT), sn(NSLOT);
+    for (int s = 0; s < NSLOT; ++s) {
+      sb[s] = slot_bucket_[s] == NO_BUCKET ? -1.0 : (double)slot_bucket_[s];
+      sn[s] = h_spill_snap_ ? (double)h_spill_snap_[s] : -1.0;
+    }
+    arr("slot_bucket", sb);
+    arr("spill_fill_last_snapshot", sn);
+  }
+  if (dj_) {
+    const JoinCounters c = dj_->counters();
+    num("join_tx", (double)c.tx); num("join_partial_overflow", (double)c.partial_overflow);
+    num("join_need_overflow", (double)c.need_overflow); num("join_table_full", (double)c.table_full);
+    num("join_pool_exhausted", (double)c.pool_exhausted); num("join_table_slots", (double)c.table_slots);
+    num("join_keys_live", (double)dj_->keys_live()); num("join_need_live", (double)dj_->need_live());
+    num("join_need_arena", (double)c.need_arena_entries); num("join_chain_pool_blocks", (double)c.chain_pool_blocks);
+    num("join_raw_services", (double)dj_->n_raw());
+    num("tx_ring_head", (double)dj_->ring_head()); num("tx_ring_low", (double)dj_->ring_low());
+    num("tx_ring_capacity", (double)dj_->ring_cap());
+  }
+  if (coll_) {
+    num("coll_nranks", coll_->nranks());
+    num("coll_rank", coll_->rank());
+    num("coll_aborted", coll_->aborted() ? 1 : 0);
+    num("fleet_rounds", (double)fleet_rounds_);
+  }
+  j += "}";
+  BinWriter w(path);
+  w.begin(SEC_DUMP);
+  w.str(reason);
+  w.str(j);
+  w.end();
+  w.commit();
+  return w.bytes();
 }
 
 uint64_t Engine::save_state(const std::string& path, const std::string& extra) {

@@ -101,6 +101,9 @@ class DeviceJoin {
   // stats thread: lowest position still referenced (pool / tail / unprocessed batches)
   void set_ring_low(uint64_t low);
   uint64_t ring_head() const { return ring_head_.load(std::memory_order_acquire); }
+  uint64_t ring_low() const { return ring_low_.load(std::memory_order_acquire); }
+  uint64_t keys_live() const { return keys_live_ + keys_since_rebuild_; }
+  uint64_t need_live() const { return arena_head_ - (regions_.empty() ? arena_head_ : regions_.front().lo); }
   // reserve `bytes` at the ring head (thread-safe; relocation by the stats thread also uses it)
   uint64_t ring_reserve(uint64_t bytes);
   void reset_ring(uint64_t head);  // checkpoint load: pending lines were placed at [0, head)

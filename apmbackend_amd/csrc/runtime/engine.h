@@ -270,6 +270,11 @@ class Engine {
   // one fsync + rename covers both); load_state returns it.  load_state also accepts a chain
   // manifest written by checkpoint_async (base + increments).
   uint64_t save_state(const std::string& path, const std::string& extra = std::string());
+  // Fatal-path state dump (the analogue of the reference's heapdump / node-oom-heapdump,
+  // apm_manager.js:12-18): host-side state only -- a faulted GPU context cannot be read -- as one
+  // section of the checkpoint file format: reason, clocks, batch ids, counters, capacities and
+  // fill levels (JSON text).  Returns the bytes written.
+  uint64_t dump_state(const std::string& path, const std::string& reason);
   std::string load_state(const std::string& path);
   // Asynchronous incremental checkpoint into `<prefix>.ckpt` (chain manifest) + `<prefix>.{b,i}N.ckpt`:
   // the calling thread pays for a consistent snapshot (small sections + dirty ring rows copied

@@ -90,8 +90,9 @@ class IngestService:
     def __init__(self, cfg: Optional[Dict[str, Any]] = None, config_path: Optional[str] = None,
                  engine: str = "native", files: Optional[Sequence[str]] = None, rank: Optional[int] = None,
                  world: Optional[int] = None, clock: Callable[[], float] = time.time, install_signals: bool = False,
-                 server_of_path: Callable[[str], str] = server_of):
+                 server_of_path: Callable[[str], str] = server_of, trace_path: Optional[str] = None):
         self.cfg = cfg if cfg is not None else read_apm_config(config_path, first_run=True)
+        self.trace_path = trace_path or self.cfg.get("gpu", {}).get("tracePath") or None
         g = self.cfg.setdefault("gpu", {})
         r, w, local = dist_env()
         self.rank = r if rank is None else rank
@@ -138,6 +139,8 @@ class IngestService:
         if engine == "native":
             self.eng = APMEngine(self.cfg, device=self.local_rank, outputs=self.outputs)
             self.native = self.eng.eng
+            if self.trace_path:
+                self.native.set_trace(True)
         elif engine == "cpu-oracle":
             from ..models.cpu_engine import CpuOracleEngine
             self.eng = None
@@ -725,19 +728,42 @@ class IngestService:
     def run(self, max_batches: Optional[int] = None, idle_sleep_s: float = 0.5,
             until: Optional[Callable[[], bool]] = None):
         log.info("ingest loop starting (mode=%s)", self.mode)
-        while not self._stop:
-            n = self.step()
-            self._housekeeping()
-            if max_batches is not None and self.batches >= max_batches:
-                break
-            if until is not None and until():
-                break
-            if n == 0:
-                self._idle(idle_sleep_s)
+        try:
+            while not self._stop:
+                n = self.step()
+                self._housekeeping()
+                if max_batches is not None and self.batches >= max_batches:
+                    break
+                if until is not None and until():
+                    break
+                if n == 0:
+                    self._idle(idle_sleep_s)
+        except BaseException as e:
+            # HIP error, capacity throw, collective abort, ...: leave the engine's state behind
+            # before the non-zero exit (the reference's node-oom-heapdump, apm_manager.js:12-18)
+            if not isinstance(e, (KeyboardInterrupt, SystemExit)):
+                self.fatal_dump(e)
+            raise
         self.shutdown()
+
+    def fatal_dump(self, exc: BaseException) -> Optional[str]:
+        """Write the engine's host-side state (clocks, batch ids, counters, capacities, fill levels)
+        with the failure reason into ``<checkpointDir or logDir>/engine.rank<r>.fatal.<ts>.dump``
+        (checkpoint file format, one section; ``read_state_dump`` parses it)."""
+        if self.eng is None or not hasattr(self.native, "dump_state"):
+            return None
+        d = self.ckpt_dir or self.cfg.get("logDir") or "."
+        return write_fatal_dump(self.native, d, self.rank, exc)
 
     def shutdown(self):
         log.info("shutting down")
+        if self.trace_path and self.eng is not None:
+            try:
+                self.eng.dump_trace(self.trace_path if self.world == 1 else f"{self.trace_path}.rank{self.rank}",
+                                    pid=self.rank)
+                log.info("stage trace written to %s", self.trace_path)
+            except Exception as e:  # pragma: no cover
+                log.warning("stage trace not written: %s", e)
         if self.fleet is not None and not self._stop:
             # coordinated end (same batch count on every rank): decide the queued node-wide
             # alert candidates -- a collective, so not on a signal-driven (per-rank) stop
@@ -769,18 +795,63 @@ class IngestService:
             self.in_qm.shutdown()
 
 
+def write_fatal_dump(native, directory: str, rank: int, exc: BaseException) -> Optional[str]:
+    """Engine state dump on a fatal error; never raises (the original error is what matters)."""
+    try:
+        os.makedirs(directory, exist_ok=True)
+        path = os.path.join(directory, f"engine.rank{rank}.fatal.{time.strftime('%Y%m%d%H%M%S')}.dump")
+        native.dump_state(path, f"{type(exc).__name__}: {exc}")
+        log.error("fatal: %s -- engine state dumped to %s", exc, path)
+        return path
+    except Exception as e2:  # pragma: no cover - best effort
+        log.error("fatal: %s -- state dump failed: %s", exc, e2)
+        return None
+
+
+def read_state_dump(path: str) -> Dict[str, Any]:
+    """Parse a fatal dump (binio framing: magic, version, {tag, length, payload}..., end)."""
+    import struct
+    with open(path, "rb") as f:
+        data = f.read()
+    if data[:8] != b"APMCKPT\0":
+        raise ValueError("not an engine checkpoint / dump file")
+    off = 12
+    while off + 4 <= len(data):
+        tag = struct.unpack_from("<I", data, off)[0]
+        if tag == 0xE0F:
+            break
+        ln = struct.unpack_from("<Q", data, off + 4)[0]
+        body = data[off + 12: off + 12 + ln]
+        if tag == 100:
+            n1 = struct.unpack_from("<Q", body, 0)[0]
+            reason = body[8:8 + n1].decode()
+            n2 = struct.unpack_from("<Q", body, 8 + n1)[0]
+            state = json.loads(body[16 + n1:16 + n1 + n2].decode())
+            state["reason"] = reason
+            return state
+        off += 12 + ln
+    raise ValueError("no dump section")
+
+
 def main(argv=None):  # pragma: no cover - process entry point
     import argparse
     ap = argparse.ArgumentParser(description="apmbackend_amd ingest service (one process per GPU)")
     ap.add_argument("--config", default=None)
     ap.add_argument("--engine", default="native", choices=["native", "cpu-oracle"])
     ap.add_argument("--max-batches", type=int, default=None)
+    # per-module profiling hooks (the reference starts every module with --inspect=<port>,
+    # apm_manager.js:263-267): a Chrome trace of the engine's stages written at shutdown; the
+    # engine's roctx ranges (apm.parse / apm.join / ...) are always emitted for rocprofv3
+    # --marker-trace
+    ap.add_argument("--trace", default=None, help="write a Chrome trace of the pipeline stages here at shutdown")
     a = ap.parse_args(argv)
     env_world = dist_env()[1]
-    if env_world > 1:
+    if env_world > 1 and str(read_apm_config(a.config, first_run=True).get("gpu", {}).get(
+            "collectiveBackend", "rccl")) != "host":
         from ..parallel.dist import init_distributed
         init_distributed()
-    svc = IngestService(config_path=a.config, engine=a.engine, install_signals=True)
+    svc = IngestService(config_path=a.config, engine=a.engine, install_signals=True,
+                        trace_path=a.trace)
     svc.run(max_batches=a.max_batches)
 
 

@@ -700,3 +700,25 @@ def test_join_tables_grow_instead_of_failing(tmp_path):
     j2 = eng2.metrics()["join"]
     assert j2["partial_overflow"] == 0 and j2["need_overflow"] == 0 and j2["table_full"] == 0
     assert j2["pool_exhausted"] == 0
+
+
+def test_fatal_error_leaves_a_state_dump(tmp_path):
+    """A fatal engine error (here: a batch larger than gpu.batchBytes -- the same path as a HIP
+    error or a capacity throw) leaves a host-side state dump next to the checkpoints before the
+    non-zero exit: the reference's heapdump / node-oom-heapdump (apm_manager.js:12-18)."""
+    from apmbackend_amd.runtime.service import read_state_dump, write_fatal_dump
+    lines, bl = synth_batches(1, duration=200)
+    C = small_cfg("exact")
+    eng = APMEngine(C, keep_text=True)
+    for now, chunks in bl[:10]:
+        eng.process_lines(chunks, now)
+    fp = bl[3][1][0][0]
+    with pytest.raises(RuntimeError) as ei:
+        eng.process_lines([(fp, ["x" * 4096] * 4096)], bl[10][0])  # 16 MB > batchBytes (4 MB)
+    path = write_fatal_dump(eng.eng, str(tmp_path), 0, ei.value)
+    d = read_state_dump(path)
+    assert "larger than" in d["reason"]
+    m = eng.metrics()
+    assert d["batches"] == m["batches"] and d["lines"] == m["lines"] and d["n_series"] == eng.eng.n_series()
+    assert d["rollovers"] == m["rollovers"] > 0 and d["join_table_slots"] >= 1024
+    assert len(d["slot_bucket"]) == 40 and d["tx_ring_head"] > 0
