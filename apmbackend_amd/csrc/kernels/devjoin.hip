@@ -1063,18 +1063,39 @@ __global__ void k_gather_len(const int64_t* __restrict__ gid, int64_t n_upper, c
   lens[i] = i >= n ? 0u : (uint32_t)((uint64_t)gid[i] & 0xfffffu) + 1u;
 }
 
-__global__ void k_gather_copy(const int64_t* __restrict__ gid, int64_t n, const char* __restrict__ ring,
-                              uint64_t ring_cap, const uint32_t* __restrict__ offs, char* __restrict__ out) {
-  // one wave per line: lanes copy the line's bytes (lines are ~100 B)
-  const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / APM_WAVE;
-  const int lane = threadIdx.x & (APM_WAVE - 1);
-  if (w >= n) return;
-  const uint64_t g = (uint64_t)gid[w];
-  const uint64_t pos = g >> 20;
-  const uint32_t len = (uint32_t)(g & 0xfffffu) + 1u;
-  const char* src = ring + (pos & (ring_cap - 1));
-  char* dst = out + offs[w];
-  for (uint32_t k = lane; k < len; k += APM_WAVE) dst[k] = src[k];
+// Released lines out of the text ring into one contiguous blob, output-centric: one lane per
+// 16-byte output chunk finds its first line by binary search over the line offsets, gathers its
+// 16 bytes (crossing into the next lines as needed) and writes them with one 16-byte store --
+// fully coalesced writes, ~24x fewer lanes than a wave per ~100-byte line with byte stores.
+__global__ __launch_bounds__(256) void k_gather_copy(const int64_t* __restrict__ gid, int64_t n,
+                                                     const char* __restrict__ ring, uint64_t ring_cap,
+                                                     const uint32_t* __restrict__ offs, char* __restrict__ out) {
+  const uint32_t total = offs[n];
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t start = c * 16;
+  if (start >= total) return;
+  int64_t lo = 0, hi = n;  // last line with offs[l] <= start
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (offs[mid] <= start) lo = mid; else hi = mid;
+  }
+  int64_t l = lo;
+  uint32_t l_off = offs[l], l_end = offs[l + 1];
+  const char* src = ring + (((uint64_t)gid[l] >> 20) & (ring_cap - 1));
+  union { uint4 v; char b[16]; } u;
+  const uint32_t m = (uint32_t)min<uint64_t>(16, total - start);
+  for (uint32_t k = 0; k < m; ++k) {
+    const uint32_t pos = (uint32_t)start + k;
+    while (pos >= l_end) {  // next line (lines are never empty: each ends with '\n')
+      ++l;
+      l_off = l_end;
+      l_end = offs[l + 1];
+      src = ring + (((uint64_t)gid[l] >> 20) & (ring_cap - 1));
+    }
+    u.b[k] = src[pos - l_off];
+  }
+  if (m == 16) *reinterpret_cast<uint4*>(out + start) = u.v;
+  else for (uint32_t k = 0; k < m; ++k) out[start + k] = u.b[k];
 }
 
 __global__ __launch_bounds__(1024) void k_min_pos(const int64_t* __restrict__ gid, int64_t n, unsigned long long* out) {
@@ -1381,10 +1402,10 @@ int apm_dj_gather_plan(const int64_t* gid, int64_t n_upper, const int64_t* d_n, 
 }
 
 void apm_dj_gather_copy(const int64_t* gid, int64_t n, const char* ring, uint64_t ring_cap, const uint32_t* offs,
-                        char* out, hipStream_t s) {
-  if (n <= 0) return;
-  const int64_t threads = n * APM_WAVE;
-  hipLaunchKernelGGL(k_gather_copy, dim3((unsigned)((threads + TB - 1) / TB)), dim3(TB), 0, s, gid, n, ring, ring_cap,
+                        char* out, uint64_t total_bytes, hipStream_t s) {
+  if (n <= 0 || total_bytes == 0) return;
+  const uint64_t chunks = (total_bytes + 15) / 16;
+  hipLaunchKernelGGL(k_gather_copy, dim3((unsigned)((chunks + TB - 1) / TB)), dim3(TB), 0, s, gid, n, ring, ring_cap,
                      offs, out);
 }
 

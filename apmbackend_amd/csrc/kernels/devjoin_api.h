@@ -164,8 +164,9 @@ void apm_dj_arena_grow(const apm::NeedEnt* old, uint32_t old_cap, apm::NeedEnt* 
 // n_upper gids (d_n null: all; offs[n_upper] = total bytes), then the copy into `out`
 int apm_dj_gather_plan(const int64_t* gid, int64_t n_upper, const int64_t* d_n, uint32_t* lens, uint32_t* offs,
                        void* tmp, size_t tmp_bytes, hipStream_t s);
+// `out` must hold offs[n] = total_bytes bytes (16-byte aligned)
 void apm_dj_gather_copy(const int64_t* gid, int64_t n, const char* ring, uint64_t ring_cap, const uint32_t* offs,
-                        char* out, hipStream_t s);
+                        char* out, uint64_t total_bytes, hipStream_t s);
 // min ring position among gids (for ring reuse); writes UINT64_MAX when n == 0
 void apm_dj_min_pos(const int64_t* gid, int64_t n, unsigned long long* out, hipStream_t s);
 // relocate gids below `below` (virtual ring pos): copy their lines to dst_base.. and rewrite

@@ -1028,8 +1028,8 @@ std::string Engine::ring_text(const int64_t* d_gid, int64_t n) {
   std::string out(total, '\0');
   if (total) {
     char* d = nullptr;
-    HIP_OK(hipMalloc((void**)&d, total));
-    apm_dj_gather_copy(d_gid, n, dj_->ring(), dj_->ring_cap(), d_rel_offs_, d, stream_);
+    HIP_OK(hipMalloc((void**)&d, ((size_t)total + 15) & ~(size_t)15));
+    apm_dj_gather_copy(d_gid, n, dj_->ring(), dj_->ring_cap(), d_rel_offs_, d, total, stream_);
     HIP_OK(hipMemcpyAsync(&out[0], d, total, hipMemcpyDeviceToHost, stream_));
     HIP_OK(hipStreamSynchronize(stream_));
     HIP_OK(hipFree(d));

@@ -211,6 +211,7 @@ void* Engine::dmalloc(size_t bytes) {
   // streams: without this, a buffer regrown mid-run could be zeroed *after* the first copy into
   // it on stream_ (seen: K12 names table read back as zeros after a regrow)
   HIP_OK(hipDeviceSynchronize());
+  std::lock_guard<std::mutex> g(alloc_mu_);  // the stats thread and the rollover lane allocate
   allocations_.push_back(p);
   device_bytes_ += bytes;
   return p;
@@ -432,6 +433,10 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
 }
 
 Engine::~Engine() {
+  if (roll_lane_) {  // a pending rollover half reads buffers freed below
+    try { roll_lane_->wait_all(); } catch (...) {}
+    roll_lane_.reset();
+  }
   ahead_lane_.reset();  // drains a pending next-batch pre-pass before the join state goes
   fb_lane_.reset();     // and a pending fb emission before its buffers
   if (nm_ev_) { hipEventSynchronize(nm_ev_); hipEventDestroy(nm_ev_); }
@@ -591,7 +596,10 @@ int32_t Engine::series_for(int32_t server, int32_t service) {
     server_first_batch_[server] = (int64_t)stats_seq_;
   }
   const uint64_t ek = ((uint64_t)server_rank_[server] << 24) | (uint64_t)(server_next_service_[server]++);
-  series_.push_back(SeriesInfo{server, service, ek});
+  {
+    std::lock_guard<std::mutex> g(series_mu_);
+    series_.push_back(SeriesInfo{server, service, ek});
+  }
   h_emit_key_.push_back(ek);
   {
     if ((int32_t)server_name_off_.size() <= server) server_name_off_.resize(server + 1, -1);
@@ -1171,7 +1179,7 @@ void Engine::stats_worker() {
       stats_seq_ = job.seq;
       stats_round_ = job.round;
       apply_ctx_pending(job.seq);
-      if (node_mode_) node_take_text();
+      node_take_text();  // al rows decided by the rollover lane / the node rounds
       if (job.dev) {
         stats_for_batch_dev(job.dj, job.t0);
       } else {
@@ -1191,7 +1199,21 @@ void Engine::stats_worker() {
       }
       apply_latest_locked(job.sync_latest, job.t0);
       fleet_pack_locked();
-      finish_rollover();
+      if (roll_pending_) finish_rollover();  // (a rollover the lane does not take: decided here)
+      if (node_mode_) {
+        // round marker: every rollover of this batch has queued its alert candidates once the
+        // lane (FIFO) got here -- the ingest thread's node round waits for it (wait_roll_round)
+        const int64_t r = (int64_t)job.round;
+        auto mark = [this, r]() {
+          {
+            std::lock_guard<std::mutex> g(roll_mu_);
+            roll_done_round_ = std::max(roll_done_round_, r);
+          }
+          roll_cv_.notify_all();
+        };
+        if (roll_lane_) roll_lane_->post(mark);
+        else mark();
+      }
       drain_sinks(~kLaneKinds);
     } catch (const std::exception& e) {
       std::lock_guard<std::mutex> g(st_mu_);
@@ -1267,7 +1289,13 @@ void Engine::post_stats_dev(DevJoinBatch&& b, double t0, int64_t sync_latest) {
 void Engine::flush() {
   std::unique_lock<std::mutex> lk(st_mu_);
   st_cv_.wait(lk, [&]() { return !st_busy_; });
-  // the stats thread is idle, so no new output-lane task can appear
+  // the stats thread is idle: complete its last rollover (lane), then no new output-lane task
+  // can appear
+  try {
+    finish_rollover();
+  } catch (const std::exception& e) {
+    if (st_error_.empty()) st_error_ = e.what();
+  }
   out_wait_idle();
   if (fb_lane_) fb_lane_->wait_all();
   {
@@ -1280,9 +1308,9 @@ void Engine::flush() {
   }
   if (!st_error_.empty()) { std::string e = st_error_; st_error_.clear(); throw std::runtime_error(e); }
   apply_ctx_pending(UINT64_MAX);  // the stats thread is idle
-  if (node_mode_) {  // decided node-wide alerts (ingest thread) -> the al stream
-    node_take_text();
-    drain_kind(OUT_AL);
+  node_take_text();  // decided alerts (rollover lane / node rounds) -> the al stream
+  drain_kind(OUT_AL);
+  if (node_mode_) {
     metrics_.alerts += node_alerts_;
     node_alerts_ = 0;
   }
@@ -2001,18 +2029,43 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   roll_pending_ = true;
   roll_edge_ts_ = edge_ts;
   roll_batch_t0_ = batch_t0;
-  // Deciding right away measured faster than queueing the rest of the batch first (1.79 vs
-  // 2.12 ms per step, same box): the released lines' gather and its D2H start sooner.
-  // APM_DEFER_ROLLOVER=1 keeps the decision pending until the end of the job (A/B switch).
-  static const bool defer = [] { const char* e = std::getenv("APM_DEFER_ROLLOVER"); return e && e[0] == '1'; }();
-  if (!defer) finish_rollover();
+  roll_round_ = stats_round_;
+  roll_ring_base_ = cur_dj_ ? cur_dj_->ring_base : (dj_ ? dj_->ring_head() : 0);
+  // The decision runs on the rollover lane as soon as the GPU chain is done, while this thread
+  // goes on (APM_ROLL_LANE=0: decide right here, the previous behaviour; sx rows always here).
+  static const bool lane = [] { const char* e = std::getenv("APM_ROLL_LANE"); return !e || e[0] != '0'; }();
+  if (lane && !want(OUT_SX)) {
+    if (!roll_lane_) roll_lane_.reset(new TaskLane());
+    roll_pending_ = false;
+    roll_posted_ = true;
+    roll_task_ = roll_lane_->post([this]() { finish_rollover_body(); });
+  } else {
+    finish_rollover();
+  }
 }
 
 // Second half of a rollover, once its GPU chain has produced the candidates and the released
 // count: queue the released lines' gather, decide the alerts, format the sx rows.
 void Engine::finish_rollover() {
+  if (roll_posted_) {
+    const double t0 = now_ms();
+    roll_lane_->wait(roll_task_);
+    roll_posted_ = false;
+    trace_event("roll.lane wait", t0, now_ms(), 1);
+    return;
+  }
   if (!roll_pending_) return;
   roll_pending_ = false;
+  finish_rollover_body();
+}
+
+// Node mode: the ingest thread exchanges round q's alert candidates only once the lane queued them.
+void Engine::wait_roll_round(uint64_t round) {
+  std::unique_lock<std::mutex> lk(roll_mu_);
+  roll_cv_.wait(lk, [&]() { return roll_done_round_ >= (int64_t)round; });
+}
+
+void Engine::finish_rollover_body() {
   const double t0 = now_ms();
   HIP_OK(hipEventSynchronize(ev_alerts_));
   const double t1 = now_ms();
@@ -2066,7 +2119,8 @@ void Engine::release_device_finish() {
     out_wait(rel_task_[k]);  // the buffer's previous reader is done
     trace_event("rel.wait_lane", tw, now_ms(), 1);
     if (total + 64 > rel_text_cap_[k]) d_rel_text_[k] = (char*)regrow(d_rel_text_[k], rel_text_cap_[k], total + 64);
-    apm_dj_gather_copy(d_pool_gid_[pool_cur_], released, dj_->ring(), dj_->ring_cap(), d_rel_offs_, d_rel_text_[k], stream_);
+    apm_dj_gather_copy(d_pool_gid_[pool_cur_], released, dj_->ring(), dj_->ring_cap(), d_rel_offs_, d_rel_text_[k], total,
+                       stream_);
     HIP_OK(hipEventRecord(ev_rel_[k], stream_));
     rel_task_[k] = post_out([this, k, total]() {
       HIP_OK(hipEventSynchronize(ev_rel_[k]));
@@ -2097,7 +2151,7 @@ void Engine::release_device_finish() {
   ExportArgs ex{};
   ex.add(d_ring_min_, hd_ring_min_, 8, /*reset=*/true, ~0ull);
   apm_export(&ex, stream_);
-  ring_low_pending_ = cur_dj_ ? cur_dj_->ring_base : dj_->ring_head();
+  ring_low_pending_ = roll_ring_base_;
 }
 
 void Engine::flush_alerts(int64_t edge_ts) {
@@ -2121,6 +2175,7 @@ void Engine::flush_alerts(int64_t edge_ts) {
   const double now = cfg_.alert_clock_entry ? (double)edge_ts
                                             : (double)std::chrono::duration_cast<std::chrono::milliseconds>(
                                                   std::chrono::system_clock::now().time_since_epoch()).count();
+  std::lock_guard<std::mutex> sg(series_mu_);  // series_ may grow on the stats thread meanwhile
   if (node_mode_) {
     // node-wide cooldown: queue the candidates (decided by the ingest thread, node_resolve)
     std::lock_guard<std::mutex> g(node_mu_);
@@ -2130,7 +2185,7 @@ void Engine::flush_alerts(int64_t edge_ts) {
       const SeriesInfo& si = series_[r.series];
       const std::string& svc = dict_.service_name(si.service);
       NodePayload p;
-      p.seq_batch = stats_round_;
+      p.seq_batch = roll_round_;
       p.c = NodeCand{};
       p.c.edge_ts = edge_ts;
       p.c.first_batch = server_first_batch_[si.server];
@@ -2155,6 +2210,7 @@ void Engine::flush_alerts(int64_t edge_ts) {
     }
     return;
   }
+  std::string text;
   for (int32_t j = 0; j < na; ++j) {
     const int32_t i = ord[j];
     const AlertRec& r = alerts[i];
@@ -2168,9 +2224,13 @@ void Engine::flush_alerts(int64_t edge_ts) {
     if (need_rows) {
       const std::string fs = fmt::fs_line(edge_ts, servers_[si.server], dict_.service_name(si.service),
                                           cfg_.lags[r.lag_idx], awin[i], az[i]);
-      blob_[OUT_AL] += fmt::al_line(now, edge_ts, servers_[si.server], dict_.service_name(si.service), r.causes, fs);
-      blob_[OUT_AL] += '\n';
+      text += fmt::al_line(now, edge_ts, servers_[si.server], dict_.service_name(si.service), r.causes, fs);
+      text += '\n';
     }
+  }
+  if (!text.empty()) {  // (possibly the rollover lane) -> the al stream via node_text_
+    std::lock_guard<std::mutex> g(node_mu_);
+    node_text_ += text;
   }
 }
 
@@ -2187,6 +2247,7 @@ int32_t Engine::intern_name(const std::string& name) {
 void Engine::dfree(void* p) {
   if (!p) return;
   HIP_OK(hipFree(p));
+  std::lock_guard<std::mutex> g(alloc_mu_);
   allocations_.erase(std::remove(allocations_.begin(), allocations_.end(), p), allocations_.end());
 }
 
@@ -2196,6 +2257,7 @@ void* Engine::regrow(void* old, size_t& cap, size_t need) {
   if (old) {
     HIP_OK(hipStreamSynchronize(stream_));
     HIP_OK(hipFree(old));
+    std::lock_guard<std::mutex> g(alloc_mu_);
     allocations_.erase(std::remove(allocations_.begin(), allocations_.end(), old), allocations_.end());
     device_bytes_ -= (cap + 255) & ~(size_t)255;
   }
@@ -3012,11 +3074,21 @@ void Engine::node_take_text() {
   node_text_.clear();
 }
 
-void Engine::node_round(uint64_t round, bool wait) {
+void Engine::node_round(uint64_t round, bool wait, bool all) {
   if (node_round_pending_) {
     coll_wait(nullptr, node_ev_, "node alerts");
     node_resolve();
   }
+  // With the rollover lane a batch's candidates are queued after its stats job: round q carries
+  // the candidates of batches <= q - 1 (whose lane work is long done), the drain everything.
+  // Every rank uses the same rule, so the pools and decisions stay identical across ranks.
+  uint64_t upto = round;
+  if (!all && roll_lane_) {
+    if (round == 0) upto = UINT64_MAX;  // nothing yet (seq_batch <= -1)
+    else upto = round - 1;
+  }
+  if (upto != UINT64_MAX) wait_roll_round(upto);
+  else if (all) wait_roll_round(round);
   const size_t per = sizeof(NodeHdr) + (size_t)node_cap_ * sizeof(NodeCand);
   NodeHdr* hdr = (NodeHdr*)h_node_send_;
   NodeCand* out = (NodeCand*)(h_node_send_ + sizeof(NodeHdr));
@@ -3024,7 +3096,7 @@ void Engine::node_round(uint64_t round, bool wait) {
   {
     std::lock_guard<std::mutex> g(node_mu_);
     int32_t n = 0;
-    while (n < node_cap_ && !node_q_.empty() && node_q_.front().seq_batch <= round) {
+    while (upto != UINT64_MAX && n < node_cap_ && !node_q_.empty() && node_q_.front().seq_batch <= upto) {
       NodePayload& p = node_q_.front();
       out[n++] = p.c;
       const uint32_t id = p.c.local_id;
@@ -3032,7 +3104,7 @@ void Engine::node_round(uint64_t round, bool wait) {
       node_q_.pop_front();
     }
     hdr->count = n;
-    hdr->all_sent = node_q_.empty() || node_q_.front().seq_batch > round;
+    hdr->all_sent = upto == UINT64_MAX || node_q_.empty() || node_q_.front().seq_batch > upto;
   }
   const size_t used = sizeof(NodeHdr) + (size_t)hdr->count * sizeof(NodeCand);
   HIP_OK(hipMemcpyAsync(d_node_send_, h_node_send_, used, hipMemcpyHostToDevice, coll_stream_));
@@ -3105,7 +3177,7 @@ void Engine::node_drain() {
   }
   // every rank computes the same node_all_sent_, so the extra rounds match across ranks
   const uint64_t last = fleet_rounds_ ? fleet_rounds_ - 1 : 0;
-  while (!node_all_sent_) node_round(last, /*wait=*/true);
+  while (!node_all_sent_) node_round(last, /*wait=*/true, /*all=*/true);
   flush();  // folds the decided rows into the al stream
 }
 

@@ -387,6 +387,22 @@ class Engine {
   bool roll_pending_ = false;  // do_rollover queued; its decision is made by finish_rollover
   int64_t roll_edge_ts_ = 0;
   double roll_batch_t0_ = 0;
+  uint64_t roll_round_ = 0;        // exchange round of the pending rollover's batch
+  uint64_t roll_ring_base_ = 0;    // text-ring base of the batch being processed at the rollover
+  // Rollover lane: the second half of a rollover (wait for the candidates and the released count,
+  // queue the released lines' gather, decide the alerts) runs here, so the stats thread goes on
+  // with the next batch instead of waiting for its GPU chain.  The next rollover (or flush) waits
+  // for it first; series_mu_ guards series_ growth against the lane's reads.
+  std::unique_ptr<TaskLane> roll_lane_;
+  uint64_t roll_task_ = 0;
+  bool roll_posted_ = false;
+  std::mutex series_mu_;
+  std::mutex alloc_mu_;            // allocations_ / device_bytes_
+  std::mutex roll_mu_;
+  std::condition_variable roll_cv_;
+  int64_t roll_done_round_ = -1;   // newest round whose alert candidates are queued (node mode)
+  void finish_rollover_body();
+  void wait_roll_round(uint64_t round);
   void format_rollover_text(int64_t edge_ts);       // K12 on the GPU
   void format_rollover_text_host(int64_t edge_ts);  // fallback (|value| >= 1e13)
   void sync_format_tables();
@@ -400,7 +416,7 @@ class Engine {
   void fleet_exchange_upto(uint64_t rounds);
   void fleet_setup(int32_t cap, bool lockstep);
   // node-wide cooldown (ingest thread): one all-gather round per exchanged batch
-  void node_round(uint64_t upto_seq, bool wait);
+  void node_round(uint64_t round, bool wait, bool all = false);
   void node_resolve();
   void node_take_text();
   void coll_wait(hipStream_t s, hipEvent_t ev, const char* what);

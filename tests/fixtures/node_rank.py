@@ -83,7 +83,7 @@ def main(argv=None):
     ap.add_argument("--ckpt-every", type=int, default=40)
     ap.add_argument("--kill", default="", help="RANK:BATCH -- that rank dies after that batch, once")
     ap.add_argument("--idle", type=float, default=600.0)
-    a = ap.parse_args(argv)
+    a, _unknown = ap.parse_known_args(argv)  # the supervisor appends --apm-module=<name>
     rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
     os.makedirs(a.out, exist_ok=True)
     ck_dir = os.path.join(a.out, "ckpt")

@@ -294,8 +294,13 @@ def test_peer_process_death_aborts_the_group_and_supervisor_resumes_from_checkpo
         t_end = time.time() + 600
         log0 = ""
         log_path = os.path.join(C["logDir"], "node.rank0.start.log")
+        t_print = time.time()
         while time.time() < t_end and not all(os.path.exists(os.path.join(out, f"done.rank{r}")) for r in range(2)):
             time.sleep(1.0)  # slow polling: the survivor notices the dead peer on its own first
+            if time.time() - t_print > 15:
+                t_print = time.time()
+                print(f"[peer-death test] restarts {[p.restarts for p in mod.procs]} "
+                      f"alerts {len(s.alert_buffer)}", flush=True)
             # (a restart truncates the start log, as the reference's openSync(.., 'w') does: keep
             # the first generation's before the supervisor restarts it)
             if not log0 and os.path.exists(log_path):
