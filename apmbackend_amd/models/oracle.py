@@ -41,7 +41,17 @@ def _valid(v) -> bool:
 
 def js_average(values: Iterable) -> Optional[float]:
     """Array.prototype.average (util_methods.js:10-24): mean of defined, non-NaN entries,
-    summed left to right from 0 in double precision; ``None`` when there are none."""
+    summed left to right from 0 in double precision; ``None`` when there are none.
+
+    A history list that offers ``float_view()`` (a float64 array, NaN = undefined; used by the
+    bench-scale tests for LAG 8640) is summed by ``np.add.accumulate``: the same sequential
+    left-to-right double additions, in C."""
+    view = getattr(values, "float_view", None)
+    if view is not None:
+        import numpy as np
+        a = view()
+        a = a[~np.isnan(a)]
+        return float(np.add.accumulate(a)[-1] / a.size) if a.size else None
     cnt = 0
     s = 0
     for v in values:
@@ -57,7 +67,7 @@ def js_stddev(values: Iterable) -> Optional[float]:
     """Array.prototype.standardDeviation *as the reference computes it* (Q1):
     ``average()`` ignores its argument, so the result is ``sqrt(mean)`` (``None`` if the mean
     is 0/undefined, NaN if negative)."""
-    vals = list(values)
+    vals = values if hasattr(values, "float_view") else list(values)
     avg = js_average(vals)
     if avg is None or (isinstance(avg, float) and math.isnan(avg)):
         return None

@@ -205,3 +205,24 @@ def test_stats_nan_elapsed_matches_reference_js():
     assert any(l.split("|")[5] == "undefined" and l.split("|")[4] != "0.00" for l in js["st"])
     assert js["st"] == out_st
     assert js["db"] == out_db
+
+
+def test_js_average_float_view_path_is_the_same_left_to_right_sum():
+    """oracle.js_average's numpy path (histories offering float_view(), used at LAG 8640 in the
+    bench-scale GPU test) performs the same sequential double additions as the Python loop."""
+    import random
+
+    import numpy as np
+    from apmbackend_amd.models.oracle import js_average, js_stddev
+
+    class View(list):
+        def float_view(self):
+            return np.array([np.nan if v is None else v for v in self], dtype=np.float64)
+
+    rng = random.Random(3)
+    for n in (1, 7, 360, 8640):
+        vals = [rng.choice([None, float("nan")]) if rng.random() < 0.05 else rng.lognormvariate(5, 1.5)
+                for _ in range(n)]
+        assert js_average(View(vals)) == js_average(vals)
+        assert js_stddev(View(vals)) == js_stddev(vals)
+    assert js_average(View([None, float("nan")])) is None

@@ -13,6 +13,7 @@ the tolerances of the small-scale tests (test_engine_gpu: a printed 1-dp tie may
 bf16 storage adds 1e-2 relative), signals may differ only on exact-tie boundaries, and the st
 rows (window statistics) are identical.
 """
+import collections
 import random
 
 import numpy as np
@@ -112,3 +113,136 @@ def test_headline_shard_rolling_and_bf16_track_exact_mode():
     sx, sr, sb = signals(fs["exact"]), signals(fs["rolling"]), signals(fs["bf16"])
     assert (sx != sr).sum() <= max(2, sx.size // 2000)
     assert (sx != sb).sum() <= sx.size // 100  # bf16: decisions on the same side for >= 99 %
+
+
+class _History:
+    """A z-score history list (avgList / per75List / per95List) backed by a float64 buffer: the
+    list operations ZScoreOracle uses, plus float_view() for oracle.js_average's C path."""
+
+    def __init__(self, values=(), cap=8640):
+        self.buf = np.full(2 * max(cap, 16) + 8, np.nan)
+        self.lo = 0
+        self.hi = 0
+        for v in values:
+            self.append(v)
+
+    def __len__(self):
+        return self.hi - self.lo
+
+    def __getitem__(self, i):
+        if i < 0:
+            i += len(self)
+        v = self.buf[self.lo + i]
+        return None if np.isnan(v) else float(v)
+
+    def pop(self, i):
+        assert i == 0
+        self.lo += 1
+
+    def append(self, v):
+        if self.hi == self.buf.size:
+            n = len(self)
+            self.buf[:n] = self.buf[self.lo:self.hi]
+            self.lo, self.hi = 0, n
+        self.buf[self.hi] = np.nan if v is None else float(v)
+        self.hi += 1
+
+    def float_view(self):
+        return self.buf[self.lo:self.hi]
+
+
+def test_headline_shard_sample_matches_cpu_oracle():
+    """the headline shard (8 JVMs x 10k services, LAG 360 / 8640, exact mode, fp64
+    rings, the bench's warmed pre-history) for 50 ten-second intervals, and for a fixed random
+    sample of 200 series every st and fs record equal to the CPU oracle's (StatsOracle +
+    ZScoreOracle, the reference's stream_calc_stats / stream_calc_z_score semantics).  The oracle
+    starts from the engine's exported state after the warm-up (window buckets, the 1-day z-score
+    histories), so LAG 8640 needs no day of input, and consumes the engine's own tx stream (whose
+    equality with the parse oracle is pinned at small scale), including every rollover trigger."""
+    from apmbackend_amd.models.oracle import StatsOracle, ZScoreOracle
+    from apmbackend_amd.utils.config import zscore_lag_settings
+    N = _native.load(build_if_missing=False)
+    gen = N.SynthGen({"servers": 8, "ejb_services": 6000, "provider_services": 4000, "tx_per_sec_per_server": 250.0,
+                      "seed": 3, "anomaly_services": 16, "anomaly_factor": 25.0,
+                      "anomaly_start_ms": START + 2 * STEP_MS})
+    C = bench_cfg("exact", "float64")
+    eng = APMEngine(C, outputs=("transactions", "st", "fs"))
+    for path, kind, server in gen.files():
+        eng.add_file(path, {0: "SOAP", 1: "SERVER", 2: "APP"}[kind], server)
+    for b in range(2):
+        data, chunks = gen.generate(START + (b + 1) * STEP_MS, 16)
+        eng.eng.process_batch(data, chunks, -1.0)
+    eng.eng.warm_history(12345)
+    eng.eng.flush()
+    for k in ("transactions", "st", "fs"):
+        eng.take_bytes(k)
+    # ---- oracle seeded with the engine's state for a fixed sample of series
+    series = [tuple(s) for s in eng.eng.export_series()]
+    assert len(series) > 40000
+    sample = sorted(random.Random(11).sample(range(len(series)), 200))
+    keep = {series[i] for i in sample}
+    st_out, fs_out = [], []
+    so = StatsOracle(st_out.append, lambda _l: None)
+    zo = ZScoreOracle(C, fs_out.append)
+    latest, s_ids, buckets, counts, values = eng.eng.export_buckets()
+    so.latest = int(latest)
+    for srv, svc in sorted(keep, key=lambda k: series.index(k)):  # creation order
+        so.servers.setdefault(srv, collections.OrderedDict())[svc] = {}
+    off = 0
+    for s, b, c in zip(s_ids, buckets, counts):
+        if tuple(series[s]) in keep:
+            srv, svc = series[s]
+            so.servers[srv][svc][int(b)] = [int(v) for v in values[off:off + c]]
+        off += c
+    lags = [int(x[0]) for x in eng.ecfg["lags"]]
+    for i in sample:
+        srv, svc = series[i]
+        node = {}
+        settings = {int(el["LAG"]): el for el in zscore_lag_settings(C, svc, False)}
+        for li, lag in enumerate(lags):
+            lens, raw = eng.eng.export_history(li, i, i + 1)
+            vals = np.frombuffer(raw, dtype=np.float64).reshape(1, 3, lag)
+            d = {"THRESHOLD": settings[lag]["THRESHOLD"], "INFLUENCE": settings[lag]["INFLUENCE"]}
+            for k, name in enumerate(("avgList", "per75List", "per95List")):
+                d[name] = _History(vals[0, k, :lens[0]], lag)
+            node[lag] = d
+        zo.servers.setdefault(srv, collections.OrderedDict())[svc] = node
+    # ---- 50 intervals: the engine, and the oracle on the engine's tx stream
+    eng_st, eng_fs, oracle_st = [], [], []
+    for b in range(2, 2 + INTERVALS):
+        data, chunks = gen.generate(START + (b + 1) * STEP_MS, 16)
+        eng.eng.process_batch(data, chunks, -1.0)
+        tx = eng.take_bytes("transactions").decode().split("\n")
+        eng_st += [l for l in eng.take_bytes("st").decode().split("\n") if l and tuple(l.split("|")[2:4]) in keep]
+        eng_fs += [l for l in eng.take_bytes("fs").decode().split("\n") if l and tuple(l.split("|")[2:4]) in keep]
+        for line in tx:
+            if not line:
+                continue
+            f = line.split("|")
+            end = f[6]
+            if len(end) <= 4 or not end.isdigit():
+                continue
+            lab = int(end[:-4])
+            if lab > so.latest:
+                so.latest = lab
+                so.rollover()
+            if (f[1], f[2]) in keep:
+                so.servers[f[1]][f[2]].setdefault(lab, []).append(int(f[7]))
+        for l in st_out:
+            zo.consume(l)
+        oracle_st += st_out
+        del st_out[:]
+    assert eng.metrics()["rollovers"] >= INTERVALS
+    # st: the oracle's rollovers emitted them (consumed into fs above); rebuild per series
+    def per_series(lines):
+        d = {}
+        for l in lines:
+            d.setdefault(tuple(l.split("|")[2:4]), []).append(l)
+        return d
+    assert per_series(eng_st) == per_series(oracle_st)
+    got_fs, want_fs = per_series(eng_fs), per_series(fs_out)
+    assert set(got_fs) == keep
+    assert got_fs == want_fs
+    assert sum(len(v) for v in got_fs.values()) >= 200 * 2 * (INTERVALS - 2)
+    # some sampled series signal (the planted incident / the warm history's spread)
+    assert any(part.split(":")[4] not in ("0", "0.0") for l in eng_fs for part in l.split("|")[6:9])
