@@ -150,6 +150,7 @@ class IngestService:
 
         # ---- checkpoint restore (before files are registered: load_state re-registers them)
         self.ckpt_dir = g.get("checkpointDir")
+        self.n_checkpoints = 0
         self.ckpt_every = float(g.get("checkpointEverySeconds",
                                       self.cfg["streamCalcStats"].get("resumeFileSaveFrequencyInSeconds", 60)))
         self.resharded = False
@@ -245,7 +246,10 @@ class IngestService:
 
         # ---- fleet exchange
         self.fleet = None
-        if self.world > 1 and engine == "native" and as_bool(g.get("fleetBaseline", True)):
+        # (gpu.fleetSingleRank: the exchange also at world 1 -- the same per-rank work as each rank
+        # of a node, as the headline bench runs it)
+        if (self.world > 1 or as_bool(g.get("fleetSingleRank", False))) and engine == "native" \
+                and as_bool(g.get("fleetBaseline", True)):
             from ..parallel.fleet import FleetBaseline
             self.fleet = FleetBaseline(self.eng, self.world, self.rank, servers=self.all_servers)
 
@@ -413,6 +417,7 @@ class IngestService:
         if seq < 0:
             log.warning("checkpoint skipped: the previous one is still being written")
             return None
+        self.n_checkpoints += 1
         if wait:
             self.eng.checkpoint_wait()
         self.tailer.save_offsets(tp)

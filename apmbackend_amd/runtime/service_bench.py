@@ -3,11 +3,15 @@
 runs, next to the headline which feeds the engine from memory.
 
 The corpus is the headline's (SynthGen, same shard shape); it is appended to real files under
-``--service-dir`` (default /dev/shm) before the timed region, so the timed region measures the
-service catching up on a backlog: tailer reads, H2D, GPU pipeline, sink encoding and writes,
-every tail offset committed.  The z-score rings get the same synthetic pre-history as the
-headline.  Reported: lines/s through the service, the DB rows/s the sink wrote, and the sink's
-encode/write share.
+``--service-dir`` (default: a directory next to bench.py, i.e. a disk-backed filesystem, not
+tmpfs) before the timed region, so the timed region measures the service catching up on a
+backlog: tailer reads, H2D, GPU pipeline, sink encoding and writes, every tail offset committed.
+The z-score rings get the same synthetic pre-history as the headline.  As in production: the
+incremental checkpoint runs every 60 s of *log* time (the service clock is the engine's log-time
+watermark, so the compressed bench takes one every 6 batches; ``--service-ckpt off`` for the A/B),
+the fleet exchange + lock-step clocks run as at the headline (``--service-fleet``), and the COPY
+spool is on the same disk.  Reported: lines/s through the service, the DB rows/s the sink wrote,
+the sink's encode/write share, the checkpoints taken and their ingest stall.
 """
 from __future__ import annotations
 
@@ -21,7 +25,9 @@ from typing import Any, Dict
 def run(args, cfg: Dict[str, Any], N, rank: int = 0) -> Dict[str, Any]:
     from .service import IngestService
 
-    base = args.service_dir or ("/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir())
+    base = args.service_dir or os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__)))), ".service_bench")
+    os.makedirs(base, exist_ok=True)
     root = tempfile.mkdtemp(prefix="apm_svc_bench_", dir=base)
     try:
         return _run(args, cfg, N, rank, root, IngestService)
@@ -56,8 +62,11 @@ def _run(args, cfg, N, rank, root, IngestService):
             written[0] += len(data)
 
     g = cfg["gpu"]
+    ckpt = getattr(args, "service_ckpt", "on") == "on"
+    fleet = getattr(args, "service_fleet", "on") == "on"
     g.update({"tailFromStart": True, "tailReadAhead": True, "tailIdleMs": 1.0, "tailReadThreads": 4,
-              "checkpointDir": None, "fleetBaseline": False})
+              "checkpointDir": os.path.join(root, "ckpt") if ckpt else None, "checkpointEverySeconds": 60,
+              "fleetBaseline": fleet, "fleetSingleRank": fleet})
     ic = cfg["streamInsertDb"]
     ic.update({"sink": args.service_sink, "copySinkDir": os.path.join(root, "spool"),
                "encoderThreads": args.encoder_threads, "copySinkRotateBytes": 1 << 62,
@@ -66,7 +75,16 @@ def _run(args, cfg, N, rank, root, IngestService):
     cfg["streamParseTransactions"]["tailOffsetFileFullPath"] = os.path.join(root, "state", "tail_offsets.json")
     cfg["streamInsertDb"]["bufferResumeFileFullPath"] = os.path.join(root, "state", "db_resume.json")
     srv_of = lambda p: p.split("/")[-2]  # noqa: E731
-    svc = IngestService(cfg, engine="native", files=paths, rank=0, world=1, server_of_path=srv_of)
+    # the service's clock = log time (the engine's watermark): checkpoints / stat lines every 60 s
+    # of log time, as a real-time deployment has them, at the bench's compressed pace
+    holder = {}
+
+    def log_clock():
+        e = holder.get("svc")
+        return e.native.watermark() / 1000.0 if e is not None and e.eng is not None else 0.0
+
+    svc = IngestService(cfg, engine="native", files=paths, rank=0, world=1, server_of_path=srv_of, clock=log_clock)
+    holder["svc"] = svc
 
     def drain():
         while sum(o[1] for o in svc.tailer.offsets()) < written[0] or svc._held is not None:
@@ -84,6 +102,8 @@ def _run(args, cfg, N, rank, root, IngestService):
     append(2 + args.warmup, 2 + args.warmup + args.steps)  # the backlog the timed region consumes
     m0 = svc.eng.metrics()
     s0 = svc.inserter.sink_stats()
+    ck0 = svc.eng.eng.checkpoint_info() if ckpt else None
+    n_ck0 = svc.n_checkpoints if hasattr(svc, "n_checkpoints") else 0
     import torch
     torch.cuda.synchronize()
     if args.trace:
@@ -99,6 +119,8 @@ def _run(args, cfg, N, rank, root, IngestService):
     m1 = svc.eng.metrics()
     s1 = svc.inserter.sink_stats()
     tstats = svc.tailer.stats()
+    ck1 = svc.eng.eng.checkpoint_info() if ckpt else None
+    n_ck = (svc.n_checkpoints if hasattr(svc, "n_checkpoints") else 0) - n_ck0
     if args.trace:
         svc.eng.dump_trace(args.trace)
     pf = {k: svc.perf[k] - pf0[k] for k in pf0}
@@ -123,4 +145,24 @@ def _run(args, cfg, N, rank, root, IngestService):
         "ingest_GB_per_s": (m1["bytes"] - m0["bytes"]) / dt / 1e9,
         "loop": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in pf.items()},
         "mean_batch_MB": round(pf["bytes"] / max(pf["batches"], 1) / 1e6, 3),
+        "checkpoints": n_ck,
+        "checkpoint_info": {k: ck1[k] for k in ck1} if ck1 else None,
+        "fleet": fleet,
+        "fs_type": _fs_type(root),
+        "batches": pf["batches"],
     }
+
+
+def _fs_type(path: str) -> str:
+    """Filesystem type of the mount holding `path` (/proc/mounts, longest prefix)."""
+    best, typ = "", "?"
+    try:
+        with open("/proc/mounts") as f:
+            for line in f:
+                parts = line.split()
+                mp, fst = parts[1], parts[2]
+                if os.path.abspath(path).startswith(mp) and len(mp) > len(best):
+                    best, typ = mp, fst
+    except OSError:
+        pass
+    return typ

@@ -99,6 +99,10 @@ def main():
                          "(log files -> tailer read-ahead -> engine -> native COPY sink), 1 GPU")
     ap.add_argument("--service-dir", default=None, help="--path service: where the log files / spool go")
     ap.add_argument("--service-sink", default="spool", choices=["spool", "null"])
+    ap.add_argument("--service-ckpt", default="on", choices=["on", "off"],
+                    help="--path service: incremental checkpoints every 60 s of log time (6 batches)")
+    ap.add_argument("--service-fleet", default="on", choices=["on", "off"],
+                    help="--path service: fleet exchange + lock-step clocks at world 1 (as the headline)")
     ap.add_argument("--encoder-threads", type=int, default=8)
     ap.add_argument("--writer-lanes", type=int, default=4, help="DB sink writer lanes (spool files / psql connections)")
     ap.add_argument("--join-threads", type=int, default=0, help="engine worker pool (0 = auto)")
