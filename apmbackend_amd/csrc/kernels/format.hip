@@ -21,40 +21,83 @@ namespace apm {
 
 namespace {
 
-struct Out {
-  char* p;      // nullptr in the length pass
+// Line writer.  W = false: the length pass (counts only).  W = true: bytes are packed into a
+// 32-bit register and stored one aligned dword at a time; only the first and last dword of a
+// line, which it shares with its neighbours' lines, are written bytewise.  (One ds_write_b8 per
+// character from 64 lanes ~300 B apart was the write pass's cost: 8.65 LDS bank-conflict cycles
+// per instruction, profiles/r2_pmc_kernels.md.)
+template <bool W>
+struct OutT {
+  char* base;   // the line's first byte (W)
+  uint32_t mis; // base's offset inside its dword
   uint32_t n = 0;
+  uint32_t acc = 0;
+  __device__ __forceinline__ explicit OutT(char* p) : base(p), mis(W ? (uint32_t)((uintptr_t)p & 3u) : 0u) {}
+  __device__ __forceinline__ void store_dword() {
+    // acc holds the dword ending at byte n - 1 (absolute alignment)
+    if (n >= 4) {
+      *reinterpret_cast<uint32_t*>(base + n - 4) = acc;
+    } else {  // the line's first dword is shared with the previous line
+      for (uint32_t b = 0; b < n; ++b) base[b] = (char)(acc >> (8u * ((mis + b) & 3u)));
+    }
+    acc = 0;
+  }
   __device__ __forceinline__ void c(char ch) {
-    if (p) p[n] = ch;
-    ++n;
+    if (W) {
+      const uint32_t k = (mis + n) & 3u;
+      acc |= (uint32_t)(uint8_t)ch << (8u * k);
+      ++n;
+      if (k == 3u) store_dword();
+    } else {
+      ++n;
+    }
+  }
+  // the line's last (partial) dword, shared with the next line
+  __device__ __forceinline__ void finish() {
+    if (!W) return;
+    const uint32_t k = (mis + n) & 3u;
+    if (k == 0) return;
+    const uint32_t b0 = n > k ? n - k : 0;
+    for (uint32_t b = b0; b < n; ++b) base[b] = (char)(acc >> (8u * ((mis + b) & 3u)));
   }
   __device__ __forceinline__ void s(const char* src, int len) {
-    if (p)
-      for (int i = 0; i < len; ++i) p[n + i] = src[i];
-    n += len;
-  }
-  // Unsigned decimal.  Nearly every value fits 32 bits, where division by 10 is a multiply-high
-  // (64-bit division is a long emulated sequence on CDNA); the length pass only counts digits.
-  __device__ __forceinline__ void u(uint64_t v) {
-    if (v <= 0xffffffffull) { u32((uint32_t)v); return; }
-    char buf[20];
-    int k = 0;
-    do { buf[k++] = (char)('0' + v % 10); v /= 10; } while (v);
-    if (p)
-      for (int i = 0; i < k; ++i) p[n + i] = buf[k - 1 - i];
-    n += k;
+    if (W) {
+      for (int i = 0; i < len; ++i) c(src[i]);
+    } else {
+      n += len;
+    }
   }
   __device__ __forceinline__ static int digits32(uint32_t v) {
     return v < 10u ? 1 : v < 100u ? 2 : v < 1000u ? 3 : v < 10000u ? 4 : v < 100000u ? 5
          : v < 1000000u ? 6 : v < 10000000u ? 7 : v < 100000000u ? 8 : v < 1000000000u ? 9 : 10;
   }
+  // Unsigned decimal.  Nearly every value fits 32 bits, where division by 10 is a multiply-high
+  // (64-bit division is a long emulated sequence on CDNA); the length pass only counts digits.
   __device__ __forceinline__ void u32(uint32_t v) {
     const int k = digits32(v);
-    if (p) {
-      char* q = p + n + k;
-      do { *--q = (char)('0' + v % 10u); v /= 10u; } while (v);
+    if (!W) { n += k; return; }
+    // digits least significant first into three registers, emitted most significant first
+    uint32_t w[3] = {0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      if (j < k) {
+        const uint32_t d = v % 10u;
+        v /= 10u;
+        const int pos = k - 1 - j;
+        w[pos >> 2] |= (uint32_t)('0' + d) << (8 * (pos & 3));
+      }
     }
-    n += k;
+#pragma unroll
+    for (int j = 0; j < 10; ++j)
+      if (j < k) c((char)(w[j >> 2] >> (8 * (j & 3))));
+  }
+  __device__ __forceinline__ void u(uint64_t v) {
+    if (v <= 0xffffffffull) { u32((uint32_t)v); return; }
+    char buf[20];
+    int k = 0;
+    do { buf[k++] = (char)('0' + v % 10); v /= 10; } while (v);
+    if (W) for (int i = 0; i < k; ++i) c(buf[k - 1 - i]);
+    else n += k;
   }
   __device__ __forceinline__ void i64(int64_t v) {
     if (v < 0) { c('-'); u((uint64_t)(-v)); } else u((uint64_t)v);
@@ -170,7 +213,8 @@ struct Out {
   }
 };
 
-__device__ __forceinline__ void head(Out& o, const char* tag, const FormatArgs& a, int32_t s) {
+template <bool W>
+__device__ __forceinline__ void head(OutT<W>& o, const char* tag, const FormatArgs& a, int32_t s) {
   o.s(tag, 3);
   o.s(a.ts_wire, a.ts_wire_len);
   const int4 nm = a.series_names[s];
@@ -180,108 +224,117 @@ __device__ __forceinline__ void head(Out& o, const char* tag, const FormatArgs& 
   o.c('|');
 }
 
-// st_dst / fs_dst: where this series' lines go (nullptr in the length pass)
-template <bool WRITE>
-__device__ void format_series(const FormatArgs& a, int32_t i, char* st_dst, char* fs_dst, uint32_t* st_len,
-                              uint32_t* fs_len, bool& fb) {
+// st line of emission position i (empty for a series without a tx yet)
+template <bool W>
+__device__ void st_line(const FormatArgs& a, int32_t i, OutT<W>& st, bool& fb) {
   const int32_t s = a.perm[i];
   const WinStat w = a.win[s];
-  Out st{WRITE ? st_dst : nullptr};
-  Out fs{WRITE ? fs_dst : nullptr};
-  if (w.active) {
-    if (a.want_st) {
-      head(st, "st|", a, s);
-      st.fixed(w.tpm, 2, fb); st.c('|');
-      st.fixed(w.avg, 1, fb); st.c('|');
-      st.fixed(w.p75, 1, fb); st.c('|');
-      st.fixed(w.p95, 1, fb); st.c('\n');
-    }
-    if (a.want_fs && a.fs_copy) {
-      // FullStatEntry.toPostgresObject (entries.js:120-151) as COPY text, field for field what
-      // copyenc.cpp makes of the wire line
-      const double x[NSTAT] = {w.avg, w.p75, w.p95};
-      const int4 nm = a.series_names[s];
-      for (int li = 0; li < a.n_lags; ++li) {
-        const int l = a.lag_order[li];
-        const ZOut z = a.z[l][s];
-        fs.s(a.ts_copy, a.ts_copy_len);
-        fs.c('\t');
-        fs.copy_text(a.names + nm.x, nm.y);
-        fs.c('\t');
-        fs.copy_text(a.names + nm.z, nm.w);
-        fs.c('\t');
-        fs.js_fixed(w.tpm, 2, false, fb);
-        fs.c('\t');
-        fs.u((uint64_t)a.lag_value[l]);
-        fs.s("\t{\"average\":", 12);
-        for (int k = 0; k < NSTAT; ++k) {
-          if (k == 1) fs.s(",\"per75\":", 9);
-          if (k == 2) fs.s(",\"per95\":", 9);
-          const char* nmk = k == 0 ? "average" : (k == 1 ? "per75" : "per95");
-          const int nl = k == 0 ? 7 : 5;
-          fs.js_fixed(x[k], 1, true, fb);
-          fs.s(",\"", 2); fs.s(nmk, nl); fs.s("avg\":", 5);
-          fs.js_fixed(z.mean[k], 1, true, fb);
-          fs.s(",\"", 2); fs.s(nmk, nl); fs.s("lb\":", 4);
-          fs.js_fixed(z.lb[k], 1, true, fb);
-          fs.s(",\"", 2); fs.s(nmk, nl); fs.s("ub\":", 4);
-          fs.js_fixed(z.ub[k], 1, true, fb);
-          fs.s(",\"", 2); fs.s(nmk, nl); fs.s("signal\":", 8);
-          fs.i64(z.sig[k]);
-        }
-        fs.c('}');
-        fs.c('\n');
-      }
-    } else if (a.want_fs) {
-      const double x[NSTAT] = {w.avg, w.p75, w.p95};
-      for (int li = 0; li < a.n_lags; ++li) {
-        const int l = a.lag_order[li];
-        const ZOut z = a.z[l][s];
-        head(fs, "fs|", a, s);
-        fs.u((uint64_t)a.lag_value[l]);
-        fs.c('|');
-        fs.fixed(w.tpm, 2, fb);
-        for (int k = 0; k < NSTAT; ++k) {
-          fs.c('|');
-          fs.fixed(x[k], 1, fb); fs.c(':');
-          fs.fixed(z.mean[k], 1, fb); fs.c(':');
-          fs.fixed(z.lb[k], 1, fb); fs.c(':');
-          fs.fixed(z.ub[k], 1, fb); fs.c(':');
-          // averageSignal is printed raw, the percentile signals through nf (entries.js:117)
-          if (k == 0) fs.i64(z.sig[k]);
-          else fs.fixed((double)z.sig[k], 1, fb);
-        }
-        fs.c('\n');
-      }
-    }
-  }
-  if (!WRITE) { st_len[i] = st.n; fs_len[i] = fs.n; }
+  if (!w.active) return;
+  head(st, "st|", a, s);
+  st.fixed(w.tpm, 2, fb); st.c('|');
+  st.fixed(w.avg, 1, fb); st.c('|');
+  st.fixed(w.p75, 1, fb); st.c('|');
+  st.fixed(w.p95, 1, fb); st.c('\n');
 }
 
+// fs line j = (emission position i, LAG rank li): lines of one series are consecutive, LAGs
+// ascending (FullStatEntry per LAG, stream_calc_z_score.js:282-306)
+template <bool W>
+__device__ void fs_line(const FormatArgs& a, int32_t j, OutT<W>& fs, bool& fb) {
+  const int32_t i = j / a.n_lags, li = j - i * a.n_lags;
+  const int32_t s = a.perm[i];
+  const WinStat w = a.win[s];
+  if (!w.active) return;
+  const int l = a.lag_order[li];
+  const ZOut z = a.z[l][s];
+  const double x[NSTAT] = {w.avg, w.p75, w.p95};
+  if (a.fs_copy) {
+    // FullStatEntry.toPostgresObject (entries.js:120-151) as COPY text, field for field what
+    // copyenc.cpp makes of the wire line
+    const int4 nm = a.series_names[s];
+    fs.s(a.ts_copy, a.ts_copy_len);
+    fs.c('\t');
+    fs.copy_text(a.names + nm.x, nm.y);
+    fs.c('\t');
+    fs.copy_text(a.names + nm.z, nm.w);
+    fs.c('\t');
+    fs.js_fixed(w.tpm, 2, false, fb);
+    fs.c('\t');
+    fs.u((uint64_t)a.lag_value[l]);
+    fs.s("\t{\"average\":", 12);
+    for (int k = 0; k < NSTAT; ++k) {
+      if (k == 1) fs.s(",\"per75\":", 9);
+      if (k == 2) fs.s(",\"per95\":", 9);
+      const char* nmk = k == 0 ? "average" : (k == 1 ? "per75" : "per95");
+      const int nl = k == 0 ? 7 : 5;
+      fs.js_fixed(x[k], 1, true, fb);
+      fs.s(",\"", 2); fs.s(nmk, nl); fs.s("avg\":", 5);
+      fs.js_fixed(z.mean[k], 1, true, fb);
+      fs.s(",\"", 2); fs.s(nmk, nl); fs.s("lb\":", 4);
+      fs.js_fixed(z.lb[k], 1, true, fb);
+      fs.s(",\"", 2); fs.s(nmk, nl); fs.s("ub\":", 4);
+      fs.js_fixed(z.ub[k], 1, true, fb);
+      fs.s(",\"", 2); fs.s(nmk, nl); fs.s("signal\":", 8);
+      fs.i64(z.sig[k]);
+    }
+    fs.c('}');
+    fs.c('\n');
+  } else {
+    head(fs, "fs|", a, s);
+    fs.u((uint64_t)a.lag_value[l]);
+    fs.c('|');
+    fs.fixed(w.tpm, 2, fb);
+    for (int k = 0; k < NSTAT; ++k) {
+      fs.c('|');
+      fs.fixed(x[k], 1, fb); fs.c(':');
+      fs.fixed(z.mean[k], 1, fb); fs.c(':');
+      fs.fixed(z.lb[k], 1, fb); fs.c(':');
+      fs.fixed(z.ub[k], 1, fb); fs.c(':');
+      // averageSignal is printed raw, the percentile signals through nf (entries.js:117)
+      if (k == 0) fs.i64(z.sig[k]);
+      else fs.fixed((double)z.sig[k], 1, fb);
+    }
+    fs.c('\n');
+  }
+}
+
+// Length pass: one lane per LINE (st: n, fs: n * n_lags), not per series -- ~3x the waves of
+// a series per lane, which the formatting's long dependent VALU chains need for latency hiding
+// (80k series were ~1.2 waves per SIMD).
 __global__ __launch_bounds__(256) void k_format_len(FormatArgs a) {
-  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == a.n) { a.st_len[a.n] = 0; a.fs_len[a.n] = 0; return; }  // scan sentinel (-> totals)
-  if (i >= a.n) return;
+  const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int32_t nfs = a.n * a.n_lags;
   bool fb = false;
-  format_series<false>(a, i, nullptr, nullptr, a.st_len, a.fs_len, fb);
+  if (j < a.n) {
+    OutT<false> o(nullptr);
+    if (a.want_st) st_line(a, j, o, fb);
+    a.st_len[j] = o.n;
+  } else if (j == a.n) {
+    a.st_len[a.n] = 0;  // scan sentinel (-> total)
+  }
+  if (j < nfs) {
+    OutT<false> o(nullptr);
+    if (a.want_fs) fs_line(a, j, o, fb);
+    a.fs_len[j] = o.n;
+  } else if (j == nfs) {
+    a.fs_len[nfs] = 0;
+  }
   if (fb) atomicAdd(a.fallback, 1);
 }
 
-// Write pass, one wave per 64 consecutive series (emission order), so the wave's output is one
-// contiguous byte range per stream.  Each lane formats its lines into LDS at the same offset
-// modulo 4 as in the output, then the wave copies the range out with one dword per lane per
-// store (256 B per store instruction).  Formatting straight to HBM issued one single-byte store
-// per character with the 64 lanes ~300 B apart: 64 partial cache lines per instruction
-// (131 us for 25 MB at 80k series).  A block whose range does not fit the LDS stage (very long
-// names) writes directly, as before.
-constexpr int FMT_WAVE_SERIES = 64;
-constexpr uint32_t FMT_LDS_ST = 6144, FMT_LDS_FS = 24576, FMT_LDS_FS_COPY = 53248;
+// Write pass, one wave per 64 consecutive lines of one stream, so the wave's output is one
+// contiguous byte range.  Each lane formats its line into an LDS stage at the same offset modulo
+// 4 as in the output (dword stores, see OutT), then the wave copies the range out one dword per
+// lane per store (256 B per store instruction).  A block whose range does not fit the stage
+// (very long names) writes its lines to HBM directly.
+constexpr int FMT_WAVE_LINES = 64;
+constexpr uint32_t FMT_LDS = 24576, FMT_LDS_COPY = 49152;
 
 __device__ __forceinline__ void wave_copy_out(const char* __restrict__ lds, char* __restrict__ out, uint32_t g0,
                                               uint32_t g1) {
   const uint32_t a0 = g0 & ~3u;
   const uint32_t nd = (g1 - a0 + 3) / 4;
-  for (uint32_t d = threadIdx.x; d < nd; d += FMT_WAVE_SERIES) {
+  for (uint32_t d = threadIdx.x; d < nd; d += FMT_WAVE_LINES) {
     const uint32_t ga = a0 + 4 * d;
     if (ga >= g0 && ga + 4 <= g1) {
       *reinterpret_cast<uint32_t*>(out + ga) = *reinterpret_cast<const uint32_t*>(lds + 4 * d);
@@ -292,26 +345,27 @@ __device__ __forceinline__ void wave_copy_out(const char* __restrict__ lds, char
   }
 }
 
-template <uint32_t LDS_FS>
-__global__ __launch_bounds__(FMT_WAVE_SERIES) void k_format_write(FormatArgs a) {
-  __shared__ __align__(16) char sst[FMT_LDS_ST];
-  __shared__ __align__(16) char sfs[LDS_FS];
-  const int32_t i0 = blockIdx.x * FMT_WAVE_SERIES;
-  const int32_t i1 = min(a.n, i0 + FMT_WAVE_SERIES);
-  const int32_t i = i0 + (int32_t)threadIdx.x;
-  const uint32_t st0 = a.st_off[i0], st1 = a.st_off[i1];
-  const uint32_t fs0 = a.fs_off[i0], fs1 = a.fs_off[i1];
-  const bool st_lds = (st1 - (st0 & ~3u)) <= FMT_LDS_ST;  // uniform across the block
-  const bool fs_lds = (fs1 - (fs0 & ~3u)) <= LDS_FS;
-  if (i < i1) {
+template <uint32_t LDS>
+__global__ __launch_bounds__(FMT_WAVE_LINES) void k_format_write(FormatArgs a, int32_t st_blocks) {
+  __shared__ __align__(16) char stage[LDS];
+  const bool is_st = (int32_t)blockIdx.x < st_blocks;
+  const int32_t nl = is_st ? a.n : a.n * a.n_lags;
+  const int32_t j0 = (is_st ? (int32_t)blockIdx.x : (int32_t)blockIdx.x - st_blocks) * FMT_WAVE_LINES;
+  const int32_t j1 = min(nl, j0 + FMT_WAVE_LINES);
+  const int32_t j = j0 + (int32_t)threadIdx.x;
+  const uint32_t* off = is_st ? a.st_off : a.fs_off;
+  char* out = is_st ? a.st_out : a.fs_out;
+  const uint32_t g0 = off[j0], g1 = off[j1];
+  const bool lds = (g1 - (g0 & ~3u)) <= LDS;  // uniform across the block
+  if (j < j1) {
     bool fb = false;
-    char* stp = st_lds ? sst + (a.st_off[i] - (st0 & ~3u)) : a.st_out + a.st_off[i];
-    char* fsp = fs_lds ? sfs + (a.fs_off[i] - (fs0 & ~3u)) : a.fs_out + a.fs_off[i];
-    format_series<true>(a, i, stp, fsp, nullptr, nullptr, fb);
+    OutT<true> o(lds ? stage + (off[j] - (g0 & ~3u)) : out + off[j]);
+    if (is_st) st_line(a, j, o, fb);
+    else fs_line(a, j, o, fb);
+    o.finish();
   }
   __syncthreads();
-  if (st_lds) wave_copy_out(sst, a.st_out, st0, st1);
-  if (fs_lds) wave_copy_out(sfs, a.fs_out, fs0, fs1);
+  if (lds) wave_copy_out(stage, out, g0, g1);
 }
 
 // ---- fb: fleet baseline rows ------------------------------------------------------------
@@ -323,7 +377,7 @@ __device__ void fleet_row(const FleetFormatArgs& a, int32_t i, char* dst, uint32
   const int32_t slot = i / a.n_lags, li = i % a.n_lags;
   const int l = a.lag_order[li];
   const double* m = a.moments + ((size_t)slot * a.n_lags + l) * NSTAT * 3;
-  Out o{WRITE ? dst : nullptr};
+  OutT<WRITE> o(WRITE ? dst : nullptr);
   const double n0 = m[0];
   if (n0 > 0) {
     const int2 nm = a.names[slot];
@@ -362,6 +416,7 @@ __device__ void fleet_row(const FleetFormatArgs& a, int32_t i, char* dst, uint32
     }
     o.c('\n');
   }
+  o.finish();
   if (!WRITE) len[i] = o.n;
 }
 
@@ -386,10 +441,16 @@ __global__ void k_fixed_batch(const double* x, int n, int f, char* out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   bool fb = false;
-  Out o{out + (size_t)i * 32};
+  OutT<true> o(out + (size_t)i * 32);
   o.fixed(x[i], f, fb);
-  if (fb) { o.n = 0; o.s("<fallback>", 10); }
   o.c('\0');
+  o.finish();
+  if (fb) {
+    OutT<true> q(out + (size_t)i * 32);
+    q.s("<fallback>", 10);
+    q.c('\0');
+    q.finish();
+  }
 }
 
 }  // namespace
@@ -411,13 +472,15 @@ size_t apm_format_tmp_bytes(int32_t n_max) {
 int apm_format_plan(FormatArgs* a, void* tmp, size_t tmp_bytes, hipStream_t stream) {
   if (a->n <= 0) return 0;
   // a->fallback accumulates (values beyond 2^127, printed inexactly) and is never reset here
-  hipLaunchKernelGGL(k_format_len, dim3((a->n + 1 + 255) / 256), dim3(256), 0, stream, *a);
+  const int32_t lanes = a->n * a->n_lags + 1;  // >= n + 1 (n_lags >= 1)
+  hipLaunchKernelGGL(k_format_len, dim3((lanes + 255) / 256), dim3(256), 0, stream, *a);
   size_t need = tmp_bytes;
   if (rocprim::exclusive_scan(tmp, need, a->st_len, a->st_off, 0u, (size_t)a->n + 1, rocprim::plus<uint32_t>(),
                               stream) != hipSuccess)
     return -1;
-  if (rocprim::exclusive_scan(tmp, need, a->fs_len, a->fs_off, 0u, (size_t)a->n + 1, rocprim::plus<uint32_t>(),
-                              stream) != hipSuccess)
+  need = tmp_bytes;
+  if (rocprim::exclusive_scan(tmp, need, a->fs_len, a->fs_off, 0u, (size_t)a->n * a->n_lags + 1,
+                              rocprim::plus<uint32_t>(), stream) != hipSuccess)
     return -1;
   return 0;
 }
@@ -444,11 +507,14 @@ int apm_fleet_format(FleetFormatArgs* a, void* tmp, size_t tmp_bytes, hipStream_
 
 void apm_format_write(FormatArgs* a, hipStream_t stream) {
   if (a->n <= 0) return;
-  const dim3 grid((a->n + FMT_WAVE_SERIES - 1) / FMT_WAVE_SERIES);
+  const int32_t st_blocks = a->want_st ? (a->n + FMT_WAVE_LINES - 1) / FMT_WAVE_LINES : 0;
+  const int32_t fs_blocks = a->want_fs ? (a->n * a->n_lags + FMT_WAVE_LINES - 1) / FMT_WAVE_LINES : 0;
+  const dim3 grid(st_blocks + fs_blocks);
+  if (grid.x == 0) return;
   if (a->fs_copy && a->want_fs)  // COPY rows are ~2x the wire line: a bigger LDS stage
-    hipLaunchKernelGGL(k_format_write<FMT_LDS_FS_COPY>, grid, dim3(FMT_WAVE_SERIES), 0, stream, *a);
+    hipLaunchKernelGGL(k_format_write<FMT_LDS_COPY>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);
   else
-    hipLaunchKernelGGL(k_format_write<FMT_LDS_FS>, grid, dim3(FMT_WAVE_SERIES), 0, stream, *a);
+    hipLaunchKernelGGL(k_format_write<FMT_LDS>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);
 }
 
 }  // extern "C"

@@ -127,7 +127,7 @@ struct FormatArgs {
   char ts_copy[32];        // edge_ts as 'YYYY-MM-DD HH:MM:SS.mmm+00'
   int32_t ts_wire_len;
   char ts_wire[24];        // "<edge_ts>|" as the wire lines' second field (printed once, on the host)
-  uint32_t *st_len, *fs_len, *st_off, *fs_off;  // [n + 1]
+  uint32_t *st_len, *fs_len, *st_off, *fs_off;  // st [n + 1], fs per (series, LAG) line [n * n_lags + 1]
   char *st_out, *fs_out;
   int32_t* fallback;
 };

@@ -362,10 +362,11 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   d_ser_names_ = (int32_t*)dmalloc((size_t)S * 16);
   d_perm_ = (int32_t*)dmalloc((size_t)S * 4);
   d_series_server_ = (int32_t*)dmalloc((size_t)S * 4);
-  d_fmt_len_ = (uint32_t*)dmalloc((size_t)2 * (S + 1) * 4);
-  d_fmt_off_ = (uint32_t*)dmalloc((size_t)2 * (S + 1) * 4);
+  // st lengths/offsets [S + 1], then fs per (series, LAG) line [S * MAX_LAGS + 1]
+  d_fmt_len_ = (uint32_t*)dmalloc(((size_t)(S + 1) + (size_t)S * MAX_LAGS + 1) * 4);
+  d_fmt_off_ = (uint32_t*)dmalloc(((size_t)(S + 1) + (size_t)S * MAX_LAGS + 1) * 4);
   d_fmt_fallback_ = (int32_t*)dmalloc(4);
-  fmt_tmp_bytes_ = apm_format_tmp_bytes(S + 1);
+  fmt_tmp_bytes_ = apm_format_tmp_bytes((int32_t)((size_t)S * MAX_LAGS + 1));
   d_fmt_tmp_ = dmalloc(fmt_tmp_bytes_);
   HIP_OK(hipHostMalloc((void**)&h_fmt_meta_, 64, hipHostMallocDefault));
   HIP_OK(hipHostGetDevicePointer((void**)&hd_fmt_meta_, h_fmt_meta_, 0));
@@ -2409,7 +2410,7 @@ void Engine::format_rollover_text(int64_t edge_ts) {
   {
     ExportArgs ex{};
     ex.add(fa.st_off + n, hd_fmt_meta_ + 4 * k + 0, 4);
-    ex.add(fa.fs_off + n, hd_fmt_meta_ + 4 * k + 1, 4);
+    ex.add(fa.fs_off + (size_t)n * cfg_.n_lags, hd_fmt_meta_ + 4 * k + 1, 4);
     apm_export(&ex, stream_);
   }
   HIP_OK(hipEventRecord(ev_fmt_[k], stream_));

@@ -902,7 +902,7 @@ class Engine {
   char* d_names_ = nullptr;
   int32_t* d_ser_names_ = nullptr;
   int32_t* d_perm_ = nullptr;
-  uint32_t *d_fmt_len_ = nullptr, *d_fmt_off_ = nullptr;  // [4][S + 1]: st_len, fs_len, st_off, fs_off
+  uint32_t *d_fmt_len_ = nullptr, *d_fmt_off_ = nullptr;  // st [S + 1] then fs [S * MAX_LAGS + 1] (len, off)
   int32_t* d_fmt_fallback_ = nullptr;
   void* d_fmt_tmp_ = nullptr;
   size_t fmt_tmp_bytes_ = 0;

@@ -12,7 +12,8 @@
 * **restart** -- on exit: Grafana annotation + manager alert, restart after
   ``restartDelaySeconds`` (1 s), or ``crashLoopDelaySeconds`` (60 s) when it died less than
   ``crashLoopWindowSeconds`` (5 s) after starting (childExitCB :303-327).  A rank group restarts as
-  a whole: RCCL communicators cannot lose a member, so the surviving ranks are stopped first.
+  a whole: RCCL communicators cannot lose a member, so the surviving ranks, given
+  ``groupAbortGraceSeconds`` (5 s) to abort on their own (exit codes reported), are stopped first.
   **Elastic degrade**: a GPU whose rank keeps failing (``elasticMaxFailures`` within
   ``elasticWindowSeconds``) is retired and the group restarts at the next smaller world size
   (8 -> 4 -> 2 -> 1 by default), re-sharding the JVM hosts; see ``_elastic_degrade``.
@@ -369,9 +370,21 @@ class Supervisor:
         if self._elastic_degrade(mod, p, code, now):
             return
         targets = mod.procs if mod.ranks else [p]
-        for q in targets:  # a rank group restarts as a whole
-            if q is not p:
-                q.stop()
+        # A rank group restarts as a whole.  The survivors are expected to notice the dead peer on
+        # their own (collective watchdog / peer EOF), abort and exit non-zero: give them
+        # `groupAbortGraceSeconds` to do so (their exit codes are reported), then terminate them.
+        grace_end = time.monotonic() + float(self.m.get("groupAbortGraceSeconds", 5))
+        for q in targets:
+            if q is not p and q.restart_at is None:
+                qc = q.poll()
+                while qc is None and time.monotonic() < grace_end:
+                    time.sleep(0.05)
+                    qc = q.poll()
+                if qc is not None:
+                    log.error("Child exited: code:%s module: %s (rank group peer)", qc, q.name)
+                    self.add_alert(f"Child module exited: code:{qc} module: {q.name}")
+                else:
+                    q.stop()
             q.restart_at = now + delay
 
     def check_children(self):
