@@ -172,6 +172,7 @@ py::dict counters_dict(const JoinCounters& c) {
   d["table_slots"] = c.table_slots; d["table_grows"] = c.table_grows; d["table_rebuilds"] = c.table_rebuilds;
   d["need_arena_entries"] = c.need_arena_entries; d["arena_grows"] = c.arena_grows;
   d["chain_pool_blocks"] = c.chain_pool_blocks; d["pool_grows"] = c.pool_grows;
+  d["host_events"] = c.host_events;
   return d;
 }
 

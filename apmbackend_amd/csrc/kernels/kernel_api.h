@@ -201,6 +201,9 @@ int apm_release_merge(const int64_t* pool_end, const int64_t* pool_gid, int64_t 
                       int64_t* out_end, int64_t* out_gid, void* tmp, size_t tmp_bytes, hipStream_t stream);
 // device scalars (4 or 8 bytes) -> host-mapped pinned memory, optional device reset afterwards
 void apm_export(const apm::ExportArgs* a, hipStream_t stream);
+// copy by a kernel (src / dst may be device views of pinned host memory): ordered on `stream`,
+// never blocks the calling thread
+void apm_copy(void* dst, const void* src, size_t bytes, hipStream_t stream);
 // zscore.hip
 void apm_zscore(apm::ZArgs* a, int dtype_bytes, hipStream_t stream);
 void apm_zscore_warm(apm::ZArgs* a, int dtype_bytes, int fill, uint64_t seed, const apm::WinStat* base,

@@ -316,61 +316,82 @@ __device__ __forceinline__ unsigned long long parse_line(const ParseArgs& a, con
   uint32_t m = 0;
   // The per-byte path is branch-free (rocprofv3: the branchy first version issued ~2 SALU
   // exec-mask instructions per VALU one): token bounds by select, and pattern triggers tested on
-  // a 4-byte register window p[i-3..i] -- one uniform branch per byte, taken only when some
-  // lane's window equals a pattern's first four bytes; only then is the line re-read.
-  uint32_t win = 0, winl = 0;
-  for (int i = 0; i < len; ++i) {
-    const uint8_t c = p[i];
-    nonascii |= c >= 0x80;
-    const bool w = is_ws(c);
-    tok_put_if(ts_, !w && !in_tok, ntok, (uint16_t)i);
-    const bool tend = w && in_tok;
-    tok_put_if(te_, tend, ntok, (uint16_t)i);
-    ntok += tend ? 1 : 0;
-    in_tok = !w;
-    win = (win >> 8) | ((uint32_t)c << 24);
-    winl = (winl >> 8) | ((uint32_t)lower(c) << 24);
-    const bool probe = (win == pk4("INFO")) | (win == pk4(": Re")) | ((win & 0xffu) == '<');
-    if (!probe || i < 3) continue;
-    const int s = i - 3;
-    if (win == pk4("INFO")) {
-      if (info1 < 0) info1 = s;
-      else if (info2 < 0 && s >= info1 + 4) info2 = s;
-      int j = s + 4;
-      while (j < len && p[j] == ' ') ++j;
-      if (match_at(p, j, len, "[CommonTiming] The EJB")) ejb_entry = true;
-      if (match_at(p, j, len, "[CommonTiming] Total time")) ejb_exit = true;
-      if (match_at(p, j, len, "CommonTiming::Start")) ct_start = true;
-      if (match_at(p, j, len, "CommonTiming::Stop")) ct_stop = true;
-      if (match_at(p, s, len, "INFO  auditTrailId=")) m |= PM_AUTR_MAP;
-      // BAF  \[[^ ]+] +INFO  : the ']' is the last non-space before the spaces preceding an
-      // "INFO ", with a '[' at least two columns before it and no space in between
-      if (!baf && s + 4 < len && p[s + 4] == ' ' && s >= 1 && p[s - 1] == ' ') {
-        int k = s - 1;
-        while (k >= 0 && p[k] == ' ') --k;
-        if (k >= 0 && p[k] == ']')
-          for (int kk = k - 2; kk >= 0 && p[kk] != ' '; --kk)
-            if (p[kk] == '[') { baf = true; break; }
-      }
-    } else if (win == pk4(": Re")) {
-      if (match_at(p, s, len, ": RequestTrace [stopWatchList=")) m |= PM_EL_START;
-    } else if ((win & 0xffu) == '<') {
-      if (win == pk4("<sto")) {
-        if (match_at(p, s, len, "<stopWatchList>")) m |= PM_SW_START;
-        if (match_at(p, s, len, "<stopTime>")) m |= PM_SW_STOPTS;
-      } else if (win == pk4("</st")) {
-        if (match_at(p, s, len, "</stopWatchList>")) m |= PM_SW_END;
-      } else if (win == pk4("<nam")) {
-        if (match_at(p, s, len, "<name>")) m |= PM_SW_NAME;
-      } else if (win == pk4("<sta")) {
-        if (match_at(p, s, len, "<startTime>")) m |= PM_SW_STARTTS;
-      } else if (win == pk4("<val")) {
-        if (match_at(p, s, len, "<value>")) m |= PM_SOAP_VALUE;
-      }
-      if (winl == pk4("<acc")) {
-        if (match_at_ci(p, s, len, "<accountnumber>")) m |= PM_SOAP_ACCT;
-      } else if (winl == pk4("<key")) {
-        if (match_at_ci(p, s, len, "<key>accountnumber</key>")) m |= PM_SOAP_KEY;
+  // a 4-byte register window p[i-3..i].  Bytes arrive 16 at a time (one aligned 16-byte load:
+  // ds_read_b128 from the stage), so a lane waits on memory once per 16 bytes instead of once
+  // per byte; positions where some pattern's first four bytes end are collected in a bit mask
+  // and matched after the 16 bytes, in order (the rare path re-reads the line).
+  uint32_t win = 0;
+  const uint8_t* __restrict__ al = base + (o & ~15u);
+  const int lead = (int)(o & 15u);
+  for (int g = -lead; g < len; g += 16, al += 16) {
+    const uint4 v = *reinterpret_cast<const uint4*>(al);
+    const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+    uint32_t hits = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int i = g + k;
+      const bool act = i >= 0 && i < len;
+      const uint8_t c = (uint8_t)(vw[k >> 2] >> (8 * (k & 3)));
+      nonascii |= act && c >= 0x80;
+      const bool w = is_ws(c);
+      tok_put_if(ts_, act && !w && !in_tok, ntok, (uint16_t)i);
+      const bool tend = act && w && in_tok;
+      tok_put_if(te_, tend, ntok, (uint16_t)i);
+      ntok += tend ? 1 : 0;
+      in_tok = act ? !w : in_tok;
+      const uint32_t nwin = (win >> 8) | ((uint32_t)c << 24);
+      win = act ? nwin : win;
+      // ('<' also covers the case-insensitive "<acc" / "<key" triggers)
+      const bool probe = (win == pk4("INFO")) | (win == pk4(": Re")) | ((win & 0xffu) == '<');
+      hits |= (act && i >= 3 && probe) ? (1u << k) : 0u;
+    }
+    while (hits) {
+      const int k = __builtin_ctz(hits);
+      hits &= hits - 1;
+      const int s = g + k - 3;
+      const uint32_t w4 = (uint32_t)p[s] | ((uint32_t)p[s + 1] << 8) | ((uint32_t)p[s + 2] << 16) |
+                          ((uint32_t)p[s + 3] << 24);
+      const uint32_t w4l = (uint32_t)lower(p[s]) | ((uint32_t)lower(p[s + 1]) << 8) |
+                           ((uint32_t)lower(p[s + 2]) << 16) | ((uint32_t)lower(p[s + 3]) << 24);
+      if (w4 == pk4("INFO")) {
+        if (info1 < 0) info1 = s;
+        else if (info2 < 0 && s >= info1 + 4) info2 = s;
+        int j = s + 4;
+        while (j < len && p[j] == ' ') ++j;
+        if (match_at(p, j, len, "[CommonTiming] The EJB")) ejb_entry = true;
+        if (match_at(p, j, len, "[CommonTiming] Total time")) ejb_exit = true;
+        if (match_at(p, j, len, "CommonTiming::Start")) ct_start = true;
+        if (match_at(p, j, len, "CommonTiming::Stop")) ct_stop = true;
+        if (match_at(p, s, len, "INFO  auditTrailId=")) m |= PM_AUTR_MAP;
+        // BAF  \[[^ ]+] +INFO  : the ']' is the last non-space before the spaces preceding an
+        // "INFO ", with a '[' at least two columns before it and no space in between
+        if (!baf && s + 4 < len && p[s + 4] == ' ' && s >= 1 && p[s - 1] == ' ') {
+          int kk0 = s - 1;
+          while (kk0 >= 0 && p[kk0] == ' ') --kk0;
+          if (kk0 >= 0 && p[kk0] == ']')
+            for (int kk = kk0 - 2; kk >= 0 && p[kk] != ' '; --kk)
+              if (p[kk] == '[') { baf = true; break; }
+        }
+      } else if (w4 == pk4(": Re")) {
+        if (match_at(p, s, len, ": RequestTrace [stopWatchList=")) m |= PM_EL_START;
+      } else if ((w4 & 0xffu) == '<') {
+        if (w4 == pk4("<sto")) {
+          if (match_at(p, s, len, "<stopWatchList>")) m |= PM_SW_START;
+          if (match_at(p, s, len, "<stopTime>")) m |= PM_SW_STOPTS;
+        } else if (w4 == pk4("</st")) {
+          if (match_at(p, s, len, "</stopWatchList>")) m |= PM_SW_END;
+        } else if (w4 == pk4("<nam")) {
+          if (match_at(p, s, len, "<name>")) m |= PM_SW_NAME;
+        } else if (w4 == pk4("<sta")) {
+          if (match_at(p, s, len, "<startTime>")) m |= PM_SW_STARTTS;
+        } else if (w4 == pk4("<val")) {
+          if (match_at(p, s, len, "<value>")) m |= PM_SOAP_VALUE;
+        }
+        if (w4l == pk4("<acc")) {
+          if (match_at_ci(p, s, len, "<accountnumber>")) m |= PM_SOAP_ACCT;
+        } else if (w4l == pk4("<key")) {
+          if (match_at_ci(p, s, len, "<key>accountnumber</key>")) m |= PM_SOAP_KEY;
+        }
       }
     }
   }

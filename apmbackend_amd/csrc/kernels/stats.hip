@@ -645,11 +645,44 @@ __global__ void k_export(ExportArgs a) {
   }
 }
 
+// Plain copy by a kernel, for small per-batch transfers between device memory and host-mapped
+// pinned memory (src or dst may be the device view of a hipHostMalloc buffer).  hipMemcpyAsync
+// of a few KB from pinned memory held the calling thread for up to 0.6 ms behind other copies
+// on this pool (trace span u.hops.h2d, profiles/r3_*); a kernel read over the host link is
+// ordered on the stream like any launch and never blocks the host.  W: bytes per lane per step.
+template <typename W>
+__global__ __launch_bounds__(256) void k_copy(W* __restrict__ dst, const W* __restrict__ src, size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = src[i];
+}
+
 }  // namespace apm
 
 extern "C" {
 
 using namespace apm;
+
+void apm_copy(void* dst, const void* src, size_t bytes, hipStream_t stream) {
+  if (bytes == 0) return;
+  const uintptr_t a = (uintptr_t)dst | (uintptr_t)src;
+  auto launch = [&](auto* d, const auto* s, size_t n) {
+    const size_t blocks = std::min<size_t>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_copy, dim3((unsigned)blocks), dim3(256), 0, stream, d, s, n);
+  };
+  if ((a & 15) == 0) {
+    const size_t n16 = bytes / 16;
+    if (n16) launch((uint4*)dst, (const uint4*)src, n16);
+    const size_t done = n16 * 16;
+    if (bytes > done) launch((uint8_t*)dst + done, (const uint8_t*)src + done, bytes - done);
+  } else if ((a & 3) == 0) {
+    const size_t n4 = bytes / 4;
+    if (n4) launch((uint32_t*)dst, (const uint32_t*)src, n4);
+    const size_t done = n4 * 4;
+    if (bytes > done) launch((uint8_t*)dst + done, (const uint8_t*)src + done, bytes - done);
+  } else {
+    launch((uint8_t*)dst, (const uint8_t*)src, bytes);
+  }
+}
 
 void apm_export(const ExportArgs* a, hipStream_t stream) {
   if (a->n > 0) hipLaunchKernelGGL(k_export, dim3(1), dim3(64), 0, stream, *a);

@@ -238,7 +238,6 @@ void Engine::checkpoint_quiesce(const char* what) {
   if (prefetched_) throw std::runtime_error(std::string(what) + ": a prefetched batch is pending (process it first)");
   HIP_OK(hipStreamSynchronize(parse_stream_));
   HIP_OK(hipStreamSynchronize(stream_));
-  HIP_OK(hipStreamSynchronize(comm_stream_));
 }
 
 uint64_t Engine::dump_state(const std::string& path, const std::string& reason) {

@@ -13,6 +13,7 @@
 #include "../kernels/common.h"
 #include "binio.h"
 #include "../kernels/devjoin_dev.h"
+#include "../kernels/kernel_api.h"
 #include "join_util.h"
 #include "jsutil.h"
 
@@ -67,7 +68,16 @@ DeviceJoin::DeviceJoin(const DevJoinConfig& cfg, Dictionary* dict, const std::ve
   cfg_.ring_bytes = pow2_at_least(std::max<uint64_t>(cfg_.ring_bytes, 1ull << 24));
   cfg_.arena_cap = (uint32_t)pow2_at_least(std::max<uint32_t>(cfg_.arena_cap, 1024));
   HIP_OK(hipSetDevice(cfg_.device));
-  HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  // The join is the ingest thread's critical path (it waits for it twice per batch); the stats,
+  // output and next-batch parse streams carry bulk work that is pipelined behind it.  A
+  // high-priority stream gets a hardware queue of its own instead of sharing one (round robin
+  // over GPU_MAX_HW_QUEUES = 4) with a 20 MB st/fs D2H blit.  APM_JOIN_PRIO=0: default priority.
+  {
+    int lo = 0, hi = 0;
+    HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    const char* pe = std::getenv("APM_JOIN_PRIO");
+    HIP_OK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, pe && pe[0] == '0' ? lo : hi));
+  }
   const uint32_t E = std::max<uint32_t>(cfg_.max_events, 1024);
   out_cap_ = 2 * E + (1u << 16);
   for (int k = 0; k < 2; ++k) {
@@ -102,6 +112,7 @@ DeviceJoin::DeviceJoin(const DevJoinConfig& cfg, Dictionary* dict, const std::ve
   d_exp_lo_ = (uint64_t*)dmalloc(8 * 4096);
   d_exp_hi_ = (uint64_t*)dmalloc(8 * 4096);
   HIP_OK(hipHostMalloc((void**)&h_exp_, 2 * 8 * 4096, hipHostMallocDefault));
+  HIP_OK(hipHostGetDevicePointer((void**)&hd_exp_, h_exp_, 0));
   soap_cap_ = 1u << 16;
   d_soap_ = (SoapState*)dmalloc((size_t)soap_cap_ * sizeof(SoapState));
   d_file_server_ = (int32_t*)dmalloc((size_t)soap_cap_ * 4);
@@ -805,11 +816,13 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
     if (h_hops_) HIP_OK(hipHostFree(h_hops_));
     h_hops_cap_ = hops_.size() * 2 + 1024;
     HIP_OK(hipHostMalloc((void**)&h_hops_, h_hops_cap_ * sizeof(HostOp), hipHostMallocDefault));
+    HIP_OK(hipHostGetDevicePointer((void**)&hd_hops_, h_hops_, 0));
   }
   if (hbuf_.size() > h_hbuf_cap_) {
     if (h_hbuf_) HIP_OK(hipHostFree(h_hbuf_));
     h_hbuf_cap_ = hbuf_.size() * 2 + (1 << 16);
     HIP_OK(hipHostMalloc((void**)&h_hbuf_, h_hbuf_cap_, hipHostMallocDefault));
+    HIP_OK(hipHostGetDevicePointer((void**)&hd_hbuf_, h_hbuf_, 0));
   }
   span("u.hostgrow");
   if (hops_.size() > d_hops_cap_) {
@@ -830,13 +843,13 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
   if (!hops_.empty()) {
     std::memcpy(h_hops_, hops_.data(), hops_.size() * sizeof(HostOp));
     span("u.hops.memcpy");
-    HIP_OK(hipMemcpyAsync(d_hops_, h_hops_, hops_.size() * sizeof(HostOp), hipMemcpyHostToDevice, st));
+    apm_copy(d_hops_, hd_hops_, hops_.size() * sizeof(HostOp), st);  // (kernel copy: never blocks)
     span("u.hops.h2d");
   }
   if (!hbuf_.empty()) {
     std::memcpy(h_hbuf_, hbuf_.data(), hbuf_.size());
     span("u.hbuf.memcpy");
-    HIP_OK(hipMemcpyAsync(d_hbuf_, h_hbuf_, hbuf_.size(), hipMemcpyHostToDevice, st));
+    apm_copy(d_hbuf_, hd_hbuf_, hbuf_.size(), st);
     span("u.hbuf.h2d");
   }
   // ---- file -> server table
@@ -862,8 +875,8 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
     ++n_reg;
   }
   if (n_reg) {
-    HIP_OK(hipMemcpyAsync(d_exp_lo_, h_exp_, (size_t)n_reg * 8, hipMemcpyHostToDevice, st));
-    HIP_OK(hipMemcpyAsync(d_exp_hi_, h_exp_ + 4096, (size_t)n_reg * 8, hipMemcpyHostToDevice, st));
+    apm_copy(d_exp_lo_, hd_exp_, (size_t)n_reg * 8, st);
+    apm_copy(d_exp_hi_, (const uint64_t*)hd_exp_ + 4096, (size_t)n_reg * 8, st);
   }
   span("u.files+exp");
   // ---- join
@@ -1021,6 +1034,7 @@ JoinCounters DeviceJoin::counters() const {
   t.arena_grows = arena_grows_;
   t.chain_pool_blocks = pool_n_;
   t.pool_grows = pool_grows_;
+  t.host_events = host_events_;
   return t;
 }
 

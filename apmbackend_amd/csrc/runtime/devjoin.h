@@ -206,6 +206,9 @@ class DeviceJoin {
   int ahead_k_ = -1;
   HostOp* h_hops_ = nullptr;     // pinned
   uint8_t* h_hbuf_ = nullptr;    // pinned
+  const void* hd_hops_ = nullptr;  // device views (apm_copy reads them over the host link)
+  const void* hd_hbuf_ = nullptr;
+  const void* hd_exp_ = nullptr;
   size_t h_hops_cap_ = 0, h_hbuf_cap_ = 0;
   HostOp* d_hops_ = nullptr;
   uint8_t* d_hbuf_ = nullptr;

@@ -220,7 +220,6 @@ void* Engine::dmalloc(size_t bytes) {
 Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipSetDevice(cfg_.device));
   HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-  HIP_OK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
   HIP_OK(hipStreamCreateWithFlags(&parse_stream_, hipStreamNonBlocking));
   HIP_OK(hipStreamCreateWithFlags(&out_stream_, hipStreamNonBlocking));
   HIP_OK(hipEventCreateWithFlags(&ev_a_, hipEventDisableTiming));
@@ -459,7 +458,6 @@ Engine::~Engine() {
   out_cv_.notify_all();
   if (out_thread_.joinable()) out_thread_.join();
   if (coll_) {
-    hipStreamSynchronize(comm_stream_);
     hipStreamSynchronize(coll_stream_);
     coll_.reset();
     for (int i = 0; i < 2; ++i) { hipEventDestroy(fleet_ev_[i]); hipEventDestroy(pack_ev_[i]); }
@@ -508,7 +506,7 @@ Engine::~Engine() {
     if (tail_csr_ev_[k]) hipEventDestroy(tail_csr_ev_[k]);
     if (h_tail_csr_[k]) hipHostFree(h_tail_csr_[k]);
   }
-  hipStreamDestroy(stream_); hipStreamDestroy(comm_stream_); hipStreamDestroy(parse_stream_);
+  hipStreamDestroy(stream_); hipStreamDestroy(parse_stream_);
 }
 
 int32_t Engine::add_server(const std::string& name) {
@@ -671,8 +669,8 @@ void Engine::upload_series_tables(int32_t lo) {
       t[i] = h_thr_[(size_t)(lo + i) * MAX_LAGS + l];
       f[i] = h_infl_[(size_t)(lo + i) * MAX_LAGS + l];
     }
-    HIP_OK(hipMemcpyAsync(lag_[l].thr + lo, t, m * 8, hipMemcpyHostToDevice, stream_));
-    HIP_OK(hipMemcpyAsync(lag_[l].infl + lo, f, m * 8, hipMemcpyHostToDevice, stream_));
+    h2d(lag_[l].thr + lo, t, m * 8, stream_);
+    h2d(lag_[l].infl + lo, f, m * 8, stream_);
   }
   double* hm = col + (size_t)(2 * L) * m;
   uint64_t* ek = (uint64_t*)(col + (size_t)(2 * L + 1) * m);
@@ -680,9 +678,9 @@ void Engine::upload_series_tables(int32_t lo) {
   std::memcpy(hm, h_hard_max_.data() + lo, m * 8);
   std::memcpy(ek, h_emit_key_.data() + lo, m * 8);
   std::memcpy(sp, h_suppressed_.data() + lo, m);
-  HIP_OK(hipMemcpyAsync(d_hard_max_ + lo, hm, m * 8, hipMemcpyHostToDevice, stream_));
-  HIP_OK(hipMemcpyAsync(d_emit_key_ + lo, ek, m * 8, hipMemcpyHostToDevice, stream_));
-  HIP_OK(hipMemcpyAsync(d_suppressed_ + lo, sp, m, hipMemcpyHostToDevice, stream_));
+  h2d(d_hard_max_ + lo, hm, m * 8, stream_);
+  h2d(d_emit_key_ + lo, ek, m * 8, stream_);
+  h2d(d_suppressed_ + lo, sp, m, stream_);
   stage_done();
 }
 
@@ -773,9 +771,9 @@ void Engine::launch_parse(ParseSlot& ps, const uint8_t* host_bytes, uint64_t n_b
   Event* devents = dev() ? dj_->d_events(k) : (ps.d_events_host ? ps.d_events_host : d_events_);
   HIP_OK(hipMemcpyAsync(dbytes, ps.hb, off, hipMemcpyHostToDevice, parse_stream_));
   HIP_OK(hipMemsetAsync(dbytes + off, 0, 64, parse_stream_));
-  HIP_OK(hipMemcpyAsync(d_chunk_begin_[k], ps.h_chunk_begin, (n_chunks + 1) * 4, hipMemcpyHostToDevice, parse_stream_));
-  HIP_OK(hipMemcpyAsync(d_chunk_kind_[k], ps.h_chunk_kind, n_chunks + 1, hipMemcpyHostToDevice, parse_stream_));
-  HIP_OK(hipMemcpyAsync(d_chunk_file_[k], ps.h_chunk_file, (n_chunks + 1) * 4, hipMemcpyHostToDevice, parse_stream_));
+  h2d(d_chunk_begin_[k], ps.h_chunk_begin, (n_chunks + 1) * 4, parse_stream_);
+  h2d(d_chunk_kind_[k], ps.h_chunk_kind, n_chunks + 1, parse_stream_);
+  h2d(d_chunk_file_[k], ps.h_chunk_file, (n_chunks + 1) * 4, parse_stream_);
   if (apm_parse_batch(dbytes, off, d_chunk_begin_[k], d_chunk_kind_[k], d_chunk_file_[k], n_chunks, d_parse_ws_,
                       cfg_.max_lines, devents, d_counts_, d_counts_ + 1, d_watermark_, d_file_open_, &cfg_.tz,
                       parse_stream_) != 0)
@@ -784,8 +782,8 @@ void Engine::launch_parse(ParseSlot& ps, const uint8_t* host_bytes, uint64_t n_b
     dj_->set_chunks(k, ps.chunk_file, d_chunk_file_[k], d_chunk_kind_[k], parse_stream_);
     dj_->select_host(k, d_counts_, cfg_.max_lines, parse_stream_);
   }
-  HIP_OK(hipMemcpyAsync(ps.h_counts, d_counts_, 8, hipMemcpyDeviceToHost, parse_stream_));
-  HIP_OK(hipMemcpyAsync(ps.h_watermark, d_watermark_, 8, hipMemcpyDeviceToHost, parse_stream_));
+  d2h(ps.h_counts, d_counts_, 8, parse_stream_);
+  d2h(ps.h_watermark, d_watermark_, 8, parse_stream_);
   // Prefetched parse: the event count is only known on the device, so copy a guess (the last
   // batch's count + 25 %) right behind the kernels.  The DMA then runs during the current
   // batch's host join instead of on the ingest thread's critical path (15 MB, ~0.3 ms), and
@@ -1181,6 +1179,7 @@ void Engine::stats_worker() {
       stats_round_ = job.round;
       apply_ctx_pending(job.seq);
       node_take_text();  // al rows decided by the rollover lane / the node rounds
+      trace_event("st.pre", t, now_ms(), 1);
       if (job.dev) {
         stats_for_batch_dev(job.dj, job.t0);
       } else {
@@ -1198,7 +1197,9 @@ void Engine::stats_worker() {
         }
         stats_for_batch(job.txs, job.t0);
       }
+      const double ta = now_ms();
       apply_latest_locked(job.sync_latest, job.t0);
+      trace_event("st.apply_latest", ta, now_ms(), 1);
       fleet_pack_locked();
       if (roll_pending_) finish_rollover();  // (a rollover the lane does not take: decided here)
       if (node_mode_) {
@@ -1215,7 +1216,9 @@ void Engine::stats_worker() {
         if (roll_lane_) roll_lane_->post(mark);
         else mark();
       }
+      const double td = now_ms();
       drain_sinks(~kLaneKinds);
+      trace_event("st.drain", td, now_ms(), 1);
     } catch (const std::exception& e) {
       std::lock_guard<std::mutex> g(st_mu_);
       st_error_ = e.what();
@@ -1784,7 +1787,7 @@ void Engine::stats_for_batch_dev(DevJoinBatch& b, double batch_t0) {
     if (!upd.empty()) {
       int32_t* hp = pinned_pairs(upd.size() * 2);
       for (size_t i = 0; i < upd.size(); ++i) { hp[2 * i] = upd[i].first; hp[2 * i + 1] = upd[i].second; }
-      HIP_OK(hipMemcpyAsync(d_pairs_, hp, upd.size() * 8, hipMemcpyHostToDevice, stream_));
+      h2d(d_pairs_, hp, upd.size() * 8, stream_);
       pinned_pairs_done();
       apm_dj_scatter_i32(dj_->d_raw_series(), d_pairs_, (uint32_t)upd.size(), stream_);
     }
@@ -1804,6 +1807,8 @@ void Engine::stats_for_batch_dev(DevJoinBatch& b, double batch_t0) {
   const int64_t keep_iv = cfg_.window + cfg_.buffer;
   auto append = [&](uint32_t lo, uint32_t hi, int64_t lat) {
     if (hi <= lo) return;
+    const double ta = now_ms();
+    struct Span { Engine* e; double t; ~Span() { e->trace_event("st.append", t, now_ms(), 1); } } span{this, ta};
     const int64_t min_live = lat - keep_iv;
     // every live bucket slot is (re)bound: a slot still holding a bucket older than the window is
     // cleared exactly as the first tx of a new bucket would clear it
@@ -1826,8 +1831,28 @@ void Engine::stats_for_batch_dev(DevJoinBatch& b, double batch_t0) {
     seg_lo = tr.first;
   }
   append(seg_lo, b.n_stats, cur_latest);
+  const double trs = now_ms();
   dj_->release_slot(b.slot, stream_);
+  trace_event("st.release_slot", trs, now_ms(), 1);
   cur_dj_ = nullptr;
+}
+
+// Small per-batch transfers between device memory and pinned (hipHostMalloc) host buffers run
+// as kernel copies over the host link (apm_copy): hipMemcpyAsync of a few KB from pinned memory
+// held the calling thread for up to 0.6 ms on this pool (trace span u.hops.h2d), a launch never
+// does.  Bulk transfers (batch bytes, st/fs text) stay on the DMA engines.
+void Engine::h2d(void* d, const void* h, size_t n, hipStream_t s) {
+  if (n == 0) return;
+  void* hv = nullptr;
+  HIP_OK(hipHostGetDevicePointer(&hv, const_cast<void*>(h), 0));
+  apm_copy(d, hv, n, s);
+}
+
+void Engine::d2h(void* h, const void* d, size_t n, hipStream_t s) {
+  if (n == 0) return;
+  void* hv = nullptr;
+  HIP_OK(hipHostGetDevicePointer(&hv, h, 0));
+  apm_copy(hv, d, n, s);
 }
 
 // Pinned staging for the stats thread's small H2D uploads (raw -> series pairs, unseen series
@@ -1867,10 +1892,10 @@ void Engine::refresh_unseen_active() {
   const uint32_t n = (uint32_t)unseen_.size();
   int32_t* hp = pinned_pairs(n);
   std::memcpy(hp, unseen_.data(), (size_t)n * 4);
-  HIP_OK(hipMemcpyAsync(d_unseen_idx_, hp, (size_t)n * 4, hipMemcpyHostToDevice, stream_));
+  h2d(d_unseen_idx_, hp, (size_t)n * 4, stream_);
   pinned_pairs_done();
   apm_dj_gather_u8(d_active_, d_unseen_idx_, n, d_unseen_flag_, stream_);
-  HIP_OK(hipMemcpyAsync(h_unseen_flag_, d_unseen_flag_, n, hipMemcpyDeviceToHost, stream_));
+  d2h(h_unseen_flag_, d_unseen_flag_, n, stream_);
   HIP_OK(hipStreamSynchronize(stream_));
   for (uint32_t i = 0; i < n; ++i)
     if (h_unseen_flag_[i]) h_active_[unseen_[i]] = 1;
@@ -1942,6 +1967,8 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   metrics_.t_release_ms += tr1 - tr0;
   // ---- first st for newly visible series: resolve their z-score settings in emission order
   if (dev()) refresh_unseen_active();
+  const double tu = now_ms();
+  trace_event("ro.unseen", tr1, tu, 1);
   {
     std::vector<int32_t> fresh;
     std::vector<int32_t> still;
@@ -1961,8 +1988,11 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
       upload_series_tables(lo);
     }
   }
+  const double tsp = now_ms();
+  trace_event("ro.fresh", tu, tsp, 1);
   // ---- K8 window statistics over buckets [L-36, L-6]
   spill_sort();
+  trace_event("ro.spill_sort", tsp, now_ms(), 1);
   WindowArgs wa;
   wa.st = stats_state();
   wa.n_win = (int32_t)(keep_iv - cfg_.buffer + 1);
@@ -2020,6 +2050,7 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
     HIP_OK(hipEventRecord(ev_alerts_, stream_));
   }
   const double tr2 = now_ms();
+  trace_event("ro.K8-K11 launch", tsp, tr2, 1);
   if (want(OUT_ST) || want(OUT_FS)) format_rollover_text(edge_ts);
   const double tr3 = now_ms();
   metrics_.t_rollover_ms += tr2 - tr1;
@@ -2277,7 +2308,7 @@ void Engine::sync_format_tables() {
     const size_t nb = h_names_.size() - names_uploaded_;
     char* st = stage(nb);
     std::memcpy(st, h_names_.data() + names_uploaded_, nb);
-    HIP_OK(hipMemcpyAsync(d_names_ + names_uploaded_, st, nb, hipMemcpyHostToDevice, stream_));
+    h2d(d_names_ + names_uploaded_, st, nb, stream_);
     stage_done();
     names_uploaded_ = h_names_.size();
   }
@@ -2286,7 +2317,7 @@ void Engine::sync_format_tables() {
     const size_t nb = (size_t)(n_series_ - lo) * 16;
     char* st = stage(nb);
     std::memcpy(st, h_ser_names_.data() + (size_t)lo * 4, nb);
-    HIP_OK(hipMemcpyAsync(d_ser_names_ + (size_t)lo * 4, st, nb, hipMemcpyHostToDevice, stream_));
+    h2d(d_ser_names_ + (size_t)lo * 4, st, nb, stream_);
     stage_done();
     ser_names_uploaded_ = n_series_;
   }
@@ -2309,7 +2340,7 @@ void Engine::sync_format_tables() {
     const size_t nb = (size_t)n_series_ * 4;
     char* st = stage(nb);
     std::memcpy(st, h_perm_.data(), nb);
-    HIP_OK(hipMemcpyAsync(d_perm_, st, nb, hipMemcpyHostToDevice, stream_));
+    h2d(d_perm_, st, nb, stream_);
     stage_done();
     perm_dirty_ = false;
   }
@@ -2369,6 +2400,7 @@ void Engine::format_rollover_text(int64_t edge_ts) {
   if (n == 0) return;
   const double tf0 = now_ms();
   sync_format_tables();
+  trace_event("fmt.tables", tf0, now_ms(), 1);
   const int32_t S = cfg_.max_series;
   FormatArgs fa{};
   fa.perm = d_perm_;
@@ -2405,8 +2437,12 @@ void Engine::format_rollover_text(int64_t edge_ts) {
   if (st_cap + fs_cap + 64 > fmt_out_cap_[k]) d_fmt_out_[k] = (char*)regrow(d_fmt_out_[k], fmt_out_cap_[k], st_cap + fs_cap + 64);
   fa.st_out = d_fmt_out_[k];
   fa.fs_out = d_fmt_out_[k] + st_cap;
+  const double tpl = now_ms();
   if (apm_format_plan(&fa, d_fmt_tmp_, fmt_tmp_bytes_, stream_) != 0) throw std::runtime_error("format scan failed");
+  const double tpw = now_ms();
+  trace_event("fmt.len+scans", tpl, tpw, 1);
   apm_format_write(&fa, stream_);
+  trace_event("fmt.write", tpw, now_ms(), 1);
   {
     ExportArgs ex{};
     ex.add(fa.st_off + n, hd_fmt_meta_ + 4 * k + 0, 4);
@@ -2489,7 +2525,7 @@ void Engine::server_rollup(int64_t edge_ts) {
     const int32_t lo = series_server_uploaded_;
     int32_t* sv = reinterpret_cast<int32_t*>(stage((size_t)(n_series_ - lo) * 4));
     for (int32_t s = lo; s < n_series_; ++s) sv[s - lo] = series_[s].server;
-    HIP_OK(hipMemcpyAsync(d_series_server_ + lo, sv, (size_t)(n_series_ - lo) * 4, hipMemcpyHostToDevice, stream_));
+    h2d(d_series_server_ + lo, sv, (size_t)(n_series_ - lo) * 4, stream_);
     stage_done();
     series_server_uploaded_ = n_series_;
   }
@@ -2498,7 +2534,7 @@ void Engine::server_rollup(int64_t edge_ts) {
     double* full = reinterpret_cast<double*>(stage(nb));
     std::fill(full, full + (size_t)nsv * CTX_FIELDS, 0.0);
     std::copy(h_ctx_.begin(), h_ctx_.begin() + std::min(h_ctx_.size(), (size_t)nsv * CTX_FIELDS), full);
-    HIP_OK(hipMemcpyAsync(d_ctx_, full, nb, hipMemcpyHostToDevice, stream_));
+    h2d(d_ctx_, full, nb, stream_);
     stage_done();
     ctx_dirty_ = false;
   }
@@ -2938,9 +2974,9 @@ void Engine::lockstep_sync(int64_t batch_max) {
   h_sync_[0] = watermark_;
   h_sync_[1] = b == INT64_MIN ? -1.0 : (double)b;  // buckets < 2^53: exact in a double
   h_sync_[2] = (double)reg_pending_count();        // any rank with unregistered services?
-  HIP_OK(hipMemcpyAsync(d_sync_, h_sync_, 24, hipMemcpyHostToDevice, coll_stream_));
+  h2d(d_sync_, h_sync_, 24, coll_stream_);
   coll_->all_reduce_f64(d_sync_, 3, /*max=*/true, coll_stream_);
-  HIP_OK(hipMemcpyAsync(h_sync_, d_sync_, 24, hipMemcpyDeviceToHost, coll_stream_));
+  d2h(h_sync_, d_sync_, 24, coll_stream_);
   coll_wait(coll_stream_, nullptr, "lock-step clocks");
   watermark_ = h_sync_[0];
   if (h_sync_[1] >= 0) sync_latest_ = std::max(sync_latest_, (int64_t)h_sync_[1]);
@@ -3021,9 +3057,9 @@ void Engine::node_metrics_round() {
                                   ld(m.tx_db), ld(m.released), ld(m.rollovers), ld(m.alert_candidates),
                                   ld(m.alerts), (double)__atomic_load_n(&n_series_, __ATOMIC_RELAXED)};
   std::memcpy(h_nm_send_, v, sizeof v);
-  HIP_OK(hipMemcpyAsync(d_nm_, h_nm_send_, sizeof v, hipMemcpyHostToDevice, coll_stream_));
+  h2d(d_nm_, h_nm_send_, sizeof v, coll_stream_);
   coll_->all_reduce_f64(d_nm_, kNodeMetrics, /*max=*/false, coll_stream_);
-  HIP_OK(hipMemcpyAsync(h_nm_recv_, d_nm_, sizeof v, hipMemcpyDeviceToHost, coll_stream_));
+  d2h(h_nm_recv_, d_nm_, sizeof v, coll_stream_);
   HIP_OK(hipEventRecord(nm_ev_, coll_stream_));
   nm_pending_ = true;
 }
@@ -3108,9 +3144,9 @@ void Engine::node_round(uint64_t round, bool wait, bool all) {
     hdr->all_sent = upto == UINT64_MAX || node_q_.empty() || node_q_.front().seq_batch > upto;
   }
   const size_t used = sizeof(NodeHdr) + (size_t)hdr->count * sizeof(NodeCand);
-  HIP_OK(hipMemcpyAsync(d_node_send_, h_node_send_, used, hipMemcpyHostToDevice, coll_stream_));
+  h2d(d_node_send_, h_node_send_, used, coll_stream_);
   coll_->all_gather(d_node_send_, d_node_recv_, per, coll_stream_);
-  HIP_OK(hipMemcpyAsync(h_node_recv_, d_node_recv_, per * (size_t)fleet_nranks_, hipMemcpyDeviceToHost, coll_stream_));
+  d2h(h_node_recv_, d_node_recv_, per * (size_t)fleet_nranks_, coll_stream_);
   HIP_OK(hipEventRecord(node_ev_, coll_stream_));
   node_round_pending_ = true;
   if (wait) {

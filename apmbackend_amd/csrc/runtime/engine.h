@@ -354,7 +354,7 @@ class Engine {
   int32_t n_series() const { return n_series_; }
   double watermark() const { return watermark_; }
   hipStream_t stream() const { return stream_; }
-  hipStream_t comm_stream() const { return comm_stream_; }
+  hipStream_t comm_stream() const { return stream_; }  // (the stats stream: callers flush() first)
   size_t device_bytes() const { return device_bytes_; }
   JoinCounters join_counters() const;
 
@@ -442,7 +442,7 @@ class Engine {
   std::vector<TraceEvent> trace_;
 
   EngineConfig cfg_;
-  hipStream_t stream_ = nullptr, comm_stream_ = nullptr, parse_stream_ = nullptr;
+  hipStream_t stream_ = nullptr, parse_stream_ = nullptr;
   // fleet exchange + lock-step clocks: ONE communicator, driven only by the ingest thread on
   // coll_stream_, so every rank issues the same collectives in the same order (engine.cpp)
   std::unique_ptr<Collective> coll_;
@@ -667,6 +667,8 @@ class Engine {
   size_t stage_max_ = 0;
   hipEvent_t stage_ev_[kStage] = {};
   int stage_k_ = 0;
+  void h2d(void* d, const void* h_pinned, size_t n, hipStream_t s);  // kernel copies (never block)
+  void d2h(void* h_pinned, const void* d, size_t n, hipStream_t s);
   char* stage(size_t bytes);
   void stage_done();
   int32_t* d_pairs_ = nullptr;

@@ -100,6 +100,7 @@ struct JoinCounters {
   uint64_t chain_partial_blocks = 0, chain_need_blocks = 0, chain_logid_blocks = 0;
   uint64_t table_slots = 0, table_grows = 0, table_rebuilds = 0, need_arena_entries = 0, arena_grows = 0;
   uint64_t chain_pool_blocks = 0, pool_grows = 0;
+  uint64_t host_events = 0;  // events resolved by the host pre-pass (audit blocks, PM_HOST lines)
 };
 
 // Cache-line aligned: the shards of a process are joined concurrently, one worker each, and

@@ -93,6 +93,9 @@ def main():
                     help="planted incident: EJB services getSvc0000.. run --anomaly-factor x slower on every "
                          "JVM from the first batch after the history warm-up (the bench's al rows)")
     ap.add_argument("--anomaly-factor", type=float, default=25.0)
+    ap.add_argument("--audit-fraction", type=float, default=0.02,
+                    help="share of requests logged with an audit trail (K5: the per-file state machine "
+                         "runs in the host pre-pass)")
     ap.add_argument("--trace", default=None, help="write a Chrome trace of the pipeline stages (per rank)")
     ap.add_argument("--path", default="memory", choices=["memory", "service"],
                     help="memory: the headline (engine fed from pinned memory); service: the production path "
@@ -190,7 +193,7 @@ def main():
                       "server_offset": rank * args.servers,
                       "anomaly_services": args.anomaly_services, "anomaly_factor": args.anomaly_factor,
                       "anomaly_start_ms": start + 2 * step_ms, "ejb_pool": args.ejb_pool,
-                      "provider_pool": args.provider_pool})
+                      "provider_pool": args.provider_pool, "audit": args.audit_fraction})
     for path, kind, server in gen.files():
         eng.add_file(path, {0: "SOAP", 1: "SERVER", 2: "APP"}[kind], server)
 
@@ -359,6 +362,9 @@ def main():
                                                                  "pool_exhausted")},
             "capacity_grows": {"spill": int(m1.get("spill_grows", 0)),
                                **{k: int(m1["join"].get(k + "_grows", 0)) for k in ("table", "arena", "pool")}},
+            "audit_fraction": args.audit_fraction,
+            "host_prepass_events_per_step": round((m1["join"].get("host_events", 0) - m0["join"].get("host_events", 0))
+                                                  / args.steps, 1),
             "alerts": int(m1["alerts"] - m0["alerts"]),
             "alert_candidates": int(m1["alert_candidates"] - m0["alert_candidates"]),
             "device_GB": round(eng.eng.device_bytes() / 1e9, 1),
