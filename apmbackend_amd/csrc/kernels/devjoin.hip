@@ -26,6 +26,7 @@
 
 #include "devjoin_api.h"
 #include "devjoin_dev.h"
+#include "textout.h"
 
 namespace apm {
 using namespace dj;
@@ -893,26 +894,6 @@ __device__ __forceinline__ const char* lid_ptr(const DJFormatArgs& f, const TxDe
   }
 }
 
-__device__ char* put_lid(const DJFormatArgs& f, const TxDev& t, char* p) {
-  if (t.lid_src != LID_NEED || t.lid_len <= NEED_LID) {
-    const char* s = lid_ptr(f, t);
-    for (int i = 0; i < t.lid_len; ++i) p[i] = s[i];
-    return p + t.lid_len;
-  }
-  const NeedEnt& ne = f.arena[t.lid & (f.arena_cap - 1)];
-  for (int i = 0; i < NEED_LID; ++i) p[i] = ne.lid[i];
-  p += NEED_LID;
-  int rem = (int)t.lid_len - NEED_LID;
-  for (int32_t b = ne.lblk; b && rem > 0; b = blk_next(f.pool, b)) {
-    const LidBlk* lb = (const LidBlk*)blk_ptr(f.pool, b);
-    const int m = rem < LBLK_N ? rem : LBLK_N;
-    for (int i = 0; i < m; ++i) p[i] = lb->b[i];
-    p += m;
-    rem -= m;
-  }
-  return p;
-}
-
 __device__ __forceinline__ bool stat_usable(const TxDev& t) { return !t.to_db && t.end == t.end && t.end >= 10000.0; }
 
 __device__ uint32_t line_len(const DJFormatArgs& f, const TxDev& t) {
@@ -949,11 +930,38 @@ __global__ void k_plan_totals(DJFormatArgs f) {
   f.counts->db_text_bytes = o.w;
 }
 
-__device__ __forceinline__ char* put_str(char* p, const char* s, int n) {
-  for (int i = 0; i < n; ++i) p[i] = s[i];
-  return p + n;
+// One tx wire line (TransactionEntry.toCSVString) through a line writer
+template <class O>
+__device__ __forceinline__ void tx_line(const DJFormatArgs& f, const TxDev& t, const RawSvc& rs, O& o, bool& inexact) {
+  o.lit("tx|");
+  o.s(f.names + rs.srv_off, rs.srv_len);
+  o.c('|');
+  o.s(f.names + rs.norm_off, rs.norm_len);
+  o.c('|');
+  if (t.lid_src != LID_NEED || t.lid_len <= NEED_LID) {
+    o.s(lid_ptr(f, t), t.lid_len);
+  } else {
+    const NeedEnt& ne = f.arena[t.lid & (f.arena_cap - 1)];
+    o.s((const char*)ne.lid, NEED_LID);
+    int rem = (int)t.lid_len - NEED_LID;
+    for (int32_t b = ne.lblk; b && rem > 0; b = blk_next(f.pool, b)) {
+      const LidBlk* lb = (const LidBlk*)blk_ptr(f.pool, b);
+      const int m = rem < LBLK_N ? rem : LBLK_N;
+      o.s((const char*)lb->b, m);
+      rem -= m;
+    }
+  }
+  o.c('|');
+  o.jsnum(t.acct, inexact); o.c('|');
+  o.jsnum(t.start, inexact); o.c('|');
+  o.jsnum(t.end, inexact); o.c('|');
+  o.jsnum(t.elapsed, inexact); o.c('|');
+  o.c(rs.toplevel ? 'Y' : 'N');
+  o.c('\n');
 }
 
+// The lines of consecutive tx are adjacent in the ring and in the tx / db text, so each lane
+// writes whole dwords (textout.h) instead of one byte store per character.
 __global__ void k_write(DJFormatArgs f) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= f.n_out) return;
@@ -964,24 +972,23 @@ __global__ void k_write(DJFormatArgs f) {
   const uint64_t vpos = f.ring_base + o.x;
   char* p0 = f.ring + (vpos & (f.ring_cap - 1));
   const RawSvc rs = f.raw[t.raw];
-  char* p = p0;
-  p = put_str(p, "tx|", 3);
-  p = put_str(p, f.names + rs.srv_off, rs.srv_len);
-  *p++ = '|';
-  p = put_str(p, f.names + rs.norm_off, rs.norm_len);
-  *p++ = '|';
-  p = put_lid(f, t, p);
-  *p++ = '|';
   bool inexact = false;
-  p += js_num(p, t.acct, &inexact); *p++ = '|';
-  p += js_num(p, t.start, &inexact); *p++ = '|';
-  p += js_num(p, t.end, &inexact); *p++ = '|';
-  p += js_num(p, t.elapsed, &inexact); *p++ = '|';
-  *p++ = rs.toplevel ? 'Y' : 'N';
-  *p++ = '\n';
+  {
+    OutT<true> w(p0);
+    tx_line(f, t, rs, w, inexact);
+    w.finish();
+  }
   const uint32_t len = l.x;
-  if (f.want_tx && !t.to_db) put_str(f.txt_tx + o.z, p0, (int)len);
-  if (f.want_db && t.to_db) put_str(f.txt_db + o.w, p0, (int)len);
+  if (f.want_tx && !t.to_db) {
+    OutT<true> w(f.txt_tx + o.z);
+    tx_line(f, t, rs, w, inexact);
+    w.finish();
+  }
+  if (f.want_db && t.to_db) {
+    OutT<true> w(f.txt_db + o.w);
+    tx_line(f, t, rs, w, inexact);
+    w.finish();
+  }
   if (l.y) {
     const uint32_t j = o.y;
     TxRec r;

@@ -14,6 +14,7 @@
 // an integer; from 1e21 JS prints String(x).  Only |x| >= 2^127 is not exact (flagged, counted).
 #include "kernel_api.h"  // (common.h pulls <cstring> in before rocprim)
 #include "devjoin_dev.h"
+#include "textout.h"
 
 #include <rocprim/rocprim.hpp>
 
@@ -21,202 +22,10 @@ namespace apm {
 
 namespace {
 
-// Line writer.  W = false: the length pass (counts only).  W = true: bytes are packed into a
-// 32-bit register and stored one aligned dword at a time; only the first and last dword of a
-// line, which it shares with its neighbours' lines, are written bytewise.  (One ds_write_b8 per
-// character from 64 lanes ~300 B apart was the write pass's cost: 8.65 LDS bank-conflict cycles
-// per instruction, profiles/r2_pmc_kernels.md.)
 template <bool W>
-struct OutT {
-  char* base;   // the line's first byte (W)
-  uint32_t mis; // base's offset inside its dword
-  uint32_t n = 0;
-  uint32_t acc = 0;
-  __device__ __forceinline__ explicit OutT(char* p) : base(p), mis(W ? (uint32_t)((uintptr_t)p & 3u) : 0u) {}
-  __device__ __forceinline__ void store_dword() {
-    // acc holds the dword ending at byte n - 1 (absolute alignment)
-    if (n >= 4) {
-      *reinterpret_cast<uint32_t*>(base + n - 4) = acc;
-    } else {  // the line's first dword is shared with the previous line
-      for (uint32_t b = 0; b < n; ++b) base[b] = (char)(acc >> (8u * ((mis + b) & 3u)));
-    }
-    acc = 0;
-  }
-  __device__ __forceinline__ void c(char ch) {
-    if (W) {
-      const uint32_t k = (mis + n) & 3u;
-      acc |= (uint32_t)(uint8_t)ch << (8u * k);
-      ++n;
-      if (k == 3u) store_dword();
-    } else {
-      ++n;
-    }
-  }
-  // the line's last (partial) dword, shared with the next line
-  __device__ __forceinline__ void finish() {
-    if (!W) return;
-    const uint32_t k = (mis + n) & 3u;
-    if (k == 0) return;
-    const uint32_t b0 = n > k ? n - k : 0;
-    for (uint32_t b = b0; b < n; ++b) base[b] = (char)(acc >> (8u * ((mis + b) & 3u)));
-  }
-  __device__ __forceinline__ void s(const char* src, int len) {
-    if (W) {
-      for (int i = 0; i < len; ++i) c(src[i]);
-    } else {
-      n += len;
-    }
-  }
-  __device__ __forceinline__ static int digits32(uint32_t v) {
-    return v < 10u ? 1 : v < 100u ? 2 : v < 1000u ? 3 : v < 10000u ? 4 : v < 100000u ? 5
-         : v < 1000000u ? 6 : v < 10000000u ? 7 : v < 100000000u ? 8 : v < 1000000000u ? 9 : 10;
-  }
-  // Unsigned decimal.  Nearly every value fits 32 bits, where division by 10 is a multiply-high
-  // (64-bit division is a long emulated sequence on CDNA); the length pass only counts digits.
-  __device__ __forceinline__ void u32(uint32_t v) {
-    const int k = digits32(v);
-    if (!W) { n += k; return; }
-    // digits least significant first into three registers, emitted most significant first
-    uint32_t w[3] = {0, 0, 0};
-#pragma unroll
-    for (int j = 0; j < 10; ++j) {
-      if (j < k) {
-        const uint32_t d = v % 10u;
-        v /= 10u;
-        const int pos = k - 1 - j;
-        w[pos >> 2] |= (uint32_t)('0' + d) << (8 * (pos & 3));
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 10; ++j)
-      if (j < k) c((char)(w[j >> 2] >> (8 * (j & 3))));
-  }
-  __device__ __forceinline__ void u(uint64_t v) {
-    if (v <= 0xffffffffull) { u32((uint32_t)v); return; }
-    char buf[20];
-    int k = 0;
-    do { buf[k++] = (char)('0' + v % 10); v /= 10; } while (v);
-    if (W) for (int i = 0; i < k; ++i) c(buf[k - 1 - i]);
-    else n += k;
-  }
-  __device__ __forceinline__ void i64(int64_t v) {
-    if (v < 0) { c('-'); u((uint64_t)(-v)); } else u((uint64_t)v);
-  }
-  // toFixed's integer n for |x| < 2^53: x * 10^f rounded, ties to the larger n (ECMA-262 21.1.3.3)
-  __device__ __forceinline__ static uint64_t fixed_n(double ax, int f) {
-    const double scale = f == 1 ? 10.0 : 100.0;
-    const double pr = ax * scale;
-    const double e = fma(ax, scale, -pr);  // exact: x * 10^f = pr + e
-    uint64_t nn;
-    if (pr >= 4503599627370496.0) {  // pr >= 2^52 is an integer: n = nearest integer to pr + e
-      nn = (uint64_t)pr + (uint64_t)(int64_t)floor(e + 0.5);
-    } else {
-      const double q = floor(pr);
-      const double d = (pr - q) - 0.5;
-      nn = (uint64_t)q;
-      if (d > 0 || (d == 0 && e >= 0)) ++nn;
-    }
-    return nn;
-  }
-  // nn = ip * 10^f + fr with constant divisors (32-bit when nn fits: nearly always)
-  __device__ __forceinline__ static void split_fixed(uint64_t nn, int f, uint64_t& ip, uint32_t& fr) {
-    if (nn <= 0xffffffffull) {
-      const uint32_t v = (uint32_t)nn;
-      if (f == 1) { ip = v / 10u; fr = v % 10u; } else { ip = v / 100u; fr = v % 100u; }
-    } else if (f == 1) {
-      ip = nn / 10u; fr = (uint32_t)(nn % 10u);
-    } else {
-      ip = nn / 100u; fr = (uint32_t)(nn % 100u);
-    }
-  }
-  // nf(x, f): 'undefined' for NaN, else x.toFixed(f)
-  __device__ __forceinline__ void fixed(double x, int f, bool& fallback) {
-    if (x != x) { s("undefined", 9); return; }
-    const bool neg = x < 0;
-    const double ax = neg ? -x : x;
-    if (!(ax < 9007199254740992.0)) {  // >= 2^53: integral values (rare)
-      big(neg, ax, f, fallback);
-      return;
-    }
-    const uint64_t nn = fixed_n(ax, f);
-    if (neg) c('-');
-    uint64_t ip;
-    uint32_t fr;
-    split_fixed(nn, f, ip, fr);
-    u(ip);
-    c('.');
-    if (f == 2) { c((char)('0' + fr / 10u)); c((char)('0' + fr % 10u)); }
-    else c((char)('0' + fr));
-  }
-  // String(parseFloat(x.toFixed(f))) -- a number as the DB row holds it (copyenc.cpp parses the
-  // wire text back and prints it JS-style): NaN -> `nul` ('null' in JSON, '\N' as a COPY field).
-  // Below 10^15 significant units the parsed value's shortest form is the toFixed text with
-  // trailing fraction zeros dropped (a <= 15-digit decimal round-trips uniquely); -0 prints 0.
-  __device__ __forceinline__ void js_fixed(double x, int f, bool json, bool& fallback) {
-    if (x != x) { if (json) s("null", 4); else s("\\N", 2); return; }
-    const bool neg = x < 0;
-    const double ax = neg ? -x : x;
-    if (!(ax < 9007199254740992.0)) {  // integral: toFixed -> parseFloat gives x back
-      char buf[64];
-      bool inexact = false;
-      const int k = dj::js_num(buf, x, &inexact);
-      if (inexact) fallback = true;
-      s(buf, k);
-      return;
-    }
-    const uint64_t nn = fixed_n(ax, f);
-    if (nn == 0) { c('0'); return; }
-    if (nn >= 1000000000000000ULL) fallback = true;
-    if (neg) c('-');
-    uint64_t ip;
-    uint32_t fr;
-    split_fixed(nn, f, ip, fr);
-    u(ip);
-    if (fr == 0) return;
-    c('.');
-    if (f == 2) {
-      c((char)('0' + fr / 10u));
-      if (fr % 10u) c((char)('0' + fr % 10u));
-    } else {
-      c((char)('0' + fr));
-    }
-  }
-  // a name as a COPY text field
-  __device__ __forceinline__ void copy_text(const char* src, int len) {
-    for (int i = 0; i < len; ++i) {
-      const char ch = src[i];
-      if (ch == '\\' || ch == '\t' || ch == '\n' || ch == '\r') {
-        c('\\');
-        c(ch == '\\' ? '\\' : (ch == '\t' ? 't' : (ch == '\n' ? 'n' : 'r')));
-      } else {
-        c(ch);
-      }
-    }
-  }
-  // |x| >= 2^53: x is an integer, so toFixed prints its digits and f zeros below 1e21 and
-  // String(x) (exponent form) from 1e21 (ECMA-262 Number.prototype.toFixed step 10); exact up
-  // to 2^127 (128-bit digits, shortest round-trip for String), `fallback` marks larger values.
-  __device__ __noinline__ void big(bool neg, double ax, int f, bool& fallback) {
-    char buf[64];
-    if (ax >= 1e21) {
-      bool inexact = false;
-      const int k = dj::js_num(buf, neg ? -ax : ax, &inexact);
-      if (inexact) fallback = true;
-      s(buf, k);
-      return;
-    }
-    if (neg) c('-');
-    const int k = dj::put_dec(buf, (unsigned __int128)ax);
-    s(buf, k);
-    c('.');
-    for (int i = 0; i < f; ++i) c('0');
-  }
-};
-
-template <bool W>
-__device__ __forceinline__ void head(OutT<W>& o, const char* tag, const FormatArgs& a, int32_t s) {
-  o.s(tag, 3);
-  o.s(a.ts_wire, a.ts_wire_len);
+__device__ __forceinline__ void head(OutT<W>& o, bool st, const FormatArgs& a, int32_t s) {
+  if (st) o.lit("st|"); else o.lit("fs|");
+  o.sb(a.ts_wire, a.ts_wire_len);
   const int4 nm = a.series_names[s];
   o.s(a.names + nm.x, nm.y);
   o.c('|');
@@ -226,11 +35,11 @@ __device__ __forceinline__ void head(OutT<W>& o, const char* tag, const FormatAr
 
 // st line of emission position i (empty for a series without a tx yet)
 template <bool W>
-__device__ void st_line(const FormatArgs& a, int32_t i, OutT<W>& st, bool& fb) {
+__device__ __forceinline__ void st_line(const FormatArgs& a, int32_t i, OutT<W>& st, bool& fb) {
   const int32_t s = a.perm[i];
   const WinStat w = a.win[s];
   if (!w.active) return;
-  head(st, "st|", a, s);
+  head(st, true, a, s);
   st.fixed(w.tpm, 2, fb); st.c('|');
   st.fixed(w.avg, 1, fb); st.c('|');
   st.fixed(w.p75, 1, fb); st.c('|');
@@ -240,7 +49,7 @@ __device__ void st_line(const FormatArgs& a, int32_t i, OutT<W>& st, bool& fb) {
 // fs line j = (emission position i, LAG rank li): lines of one series are consecutive, LAGs
 // ascending (FullStatEntry per LAG, stream_calc_z_score.js:282-306)
 template <bool W>
-__device__ void fs_line(const FormatArgs& a, int32_t j, OutT<W>& fs, bool& fb) {
+__device__ __forceinline__ void fs_line(const FormatArgs& a, int32_t j, OutT<W>& fs, bool& fb) {
   const int32_t i = j / a.n_lags, li = j - i * a.n_lags;
   const int32_t s = a.perm[i];
   const WinStat w = a.win[s];
@@ -252,7 +61,7 @@ __device__ void fs_line(const FormatArgs& a, int32_t j, OutT<W>& fs, bool& fb) {
     // FullStatEntry.toPostgresObject (entries.js:120-151) as COPY text, field for field what
     // copyenc.cpp makes of the wire line
     const int4 nm = a.series_names[s];
-    fs.s(a.ts_copy, a.ts_copy_len);
+    fs.sb(a.ts_copy, a.ts_copy_len);
     fs.c('\t');
     fs.copy_text(a.names + nm.x, nm.y);
     fs.c('\t');
@@ -261,29 +70,31 @@ __device__ void fs_line(const FormatArgs& a, int32_t j, OutT<W>& fs, bool& fb) {
     fs.js_fixed(w.tpm, 2, false, fb);
     fs.c('\t');
     fs.u((uint64_t)a.lag_value[l]);
-    fs.s("\t{\"average\":", 12);
+    fs.lit("\t{\"average\":");
+#pragma unroll
     for (int k = 0; k < NSTAT; ++k) {
-      if (k == 1) fs.s(",\"per75\":", 9);
-      if (k == 2) fs.s(",\"per95\":", 9);
+      if (k == 1) fs.lit(",\"per75\":");
+      if (k == 2) fs.lit(",\"per95\":");
       const char* nmk = k == 0 ? "average" : (k == 1 ? "per75" : "per95");
       const int nl = k == 0 ? 7 : 5;
       fs.js_fixed(x[k], 1, true, fb);
-      fs.s(",\"", 2); fs.s(nmk, nl); fs.s("avg\":", 5);
+      fs.lit(",\""); fs.sb(nmk, nl); fs.lit("avg\":");
       fs.js_fixed(z.mean[k], 1, true, fb);
-      fs.s(",\"", 2); fs.s(nmk, nl); fs.s("lb\":", 4);
+      fs.lit(",\""); fs.sb(nmk, nl); fs.lit("lb\":");
       fs.js_fixed(z.lb[k], 1, true, fb);
-      fs.s(",\"", 2); fs.s(nmk, nl); fs.s("ub\":", 4);
+      fs.lit(",\""); fs.sb(nmk, nl); fs.lit("ub\":");
       fs.js_fixed(z.ub[k], 1, true, fb);
-      fs.s(",\"", 2); fs.s(nmk, nl); fs.s("signal\":", 8);
+      fs.lit(",\""); fs.sb(nmk, nl); fs.lit("signal\":");
       fs.i64(z.sig[k]);
     }
     fs.c('}');
     fs.c('\n');
   } else {
-    head(fs, "fs|", a, s);
+    head(fs, false, a, s);
     fs.u((uint64_t)a.lag_value[l]);
     fs.c('|');
     fs.fixed(w.tpm, 2, fb);
+#pragma unroll
     for (int k = 0; k < NSTAT; ++k) {
       fs.c('|');
       fs.fixed(x[k], 1, fb); fs.c(':');
@@ -373,7 +184,7 @@ __global__ __launch_bounds__(FMT_WAVE_LINES) void k_format_write(FormatArgs a, i
 // COPY: <ts>\t<service>\t<lag>\t<n>\t{"averagemean":..,"averagestd":..,"per75mean":..,...}
 // mean / std: of the series' z-score baseline means across the fleet (population std).
 template <bool WRITE>
-__device__ void fleet_row(const FleetFormatArgs& a, int32_t i, char* dst, uint32_t* len, bool& fb) {
+__device__ __forceinline__ void fleet_row(const FleetFormatArgs& a, int32_t i, char* dst, uint32_t* len, bool& fb) {
   const int32_t slot = i / a.n_lags, li = i % a.n_lags;
   const int l = a.lag_order[li];
   const double* m = a.moments + ((size_t)slot * a.n_lags + l) * NSTAT * 3;
@@ -392,7 +203,7 @@ __device__ void fleet_row(const FleetFormatArgs& a, int32_t i, char* dst, uint32
       }
     }
     if (a.copy) {
-      o.s(a.ts, a.ts_len); o.c('\t');
+      o.sb(a.ts, a.ts_len); o.c('\t');
       o.copy_text(a.chars + nm.x, nm.y); o.c('\t');
       o.u((uint64_t)a.lag_value[l]); o.c('\t');
       o.u((uint64_t)n0); o.c('\t');
@@ -401,12 +212,12 @@ __device__ void fleet_row(const FleetFormatArgs& a, int32_t i, char* dst, uint32
       o.c('{');
       for (int k = 0; k < NSTAT; ++k) {
         if (k) o.c(',');
-        o.c('"'); o.s(key[k], kl[k]); o.s("mean\":", 6); o.js_fixed(mean[k], 1, true, fb);
-        o.s(",\"", 2); o.s(key[k], kl[k]); o.s("std\":", 5); o.js_fixed(sd[k], 1, true, fb);
+        o.c('"'); o.sb(key[k], kl[k]); o.lit("mean\":"); o.js_fixed(mean[k], 1, true, fb);
+        o.lit(",\""); o.sb(key[k], kl[k]); o.lit("std\":"); o.js_fixed(sd[k], 1, true, fb);
       }
       o.c('}');
     } else {
-      o.s("fb|", 3); o.i64(a.edge_ts); o.c('|');
+      o.lit("fb|"); o.i64(a.edge_ts); o.c('|');
       o.s(a.chars + nm.x, nm.y); o.c('|');
       o.u((uint64_t)a.lag_value[l]); o.c('|');
       o.u((uint64_t)n0);
@@ -447,7 +258,7 @@ __global__ void k_fixed_batch(const double* x, int n, int f, char* out) {
   o.finish();
   if (fb) {
     OutT<true> q(out + (size_t)i * 32);
-    q.s("<fallback>", 10);
+    q.lit("<fallback>");
     q.c('\0');
     q.finish();
   }

@@ -651,9 +651,13 @@ __global__ void k_export(ExportArgs a) {
 // on this pool (trace span u.hops.h2d, profiles/r3_*); a kernel read over the host link is
 // ordered on the stream like any launch and never blocks the host.  W: bytes per lane per step.
 template <typename W>
-__global__ __launch_bounds__(256) void k_copy(W* __restrict__ dst, const W* __restrict__ src, size_t n) {
+__global__ __launch_bounds__(256) void k_copy(W* __restrict__ dst, const W* __restrict__ src, size_t n,
+                                              uint8_t* __restrict__ tdst, const uint8_t* __restrict__ tsrc,
+                                              uint32_t tail) {
   const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = src[i];
+  const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (size_t i = t0; i < n; i += stride) dst[i] = src[i];
+  if (t0 < tail) tdst[t0] = tsrc[t0];  // the bytes after the last full W (same launch)
 }
 
 }  // namespace apm
@@ -665,23 +669,15 @@ using namespace apm;
 void apm_copy(void* dst, const void* src, size_t bytes, hipStream_t stream) {
   if (bytes == 0) return;
   const uintptr_t a = (uintptr_t)dst | (uintptr_t)src;
-  auto launch = [&](auto* d, const auto* s, size_t n) {
-    const size_t blocks = std::min<size_t>((n + 255) / 256, 1024);
-    hipLaunchKernelGGL(k_copy, dim3((unsigned)blocks), dim3(256), 0, stream, d, s, n);
+  auto launch = [&](auto* d, const auto* s, size_t w) {
+    const size_t n = bytes / w, done = n * w;
+    const size_t blocks = std::max<size_t>(1, std::min<size_t>((n + 255) / 256, 1024));
+    hipLaunchKernelGGL(k_copy, dim3((unsigned)blocks), dim3(256), 0, stream, d, s, n, (uint8_t*)dst + done,
+                       (const uint8_t*)src + done, (uint32_t)(bytes - done));
   };
-  if ((a & 15) == 0) {
-    const size_t n16 = bytes / 16;
-    if (n16) launch((uint4*)dst, (const uint4*)src, n16);
-    const size_t done = n16 * 16;
-    if (bytes > done) launch((uint8_t*)dst + done, (const uint8_t*)src + done, bytes - done);
-  } else if ((a & 3) == 0) {
-    const size_t n4 = bytes / 4;
-    if (n4) launch((uint32_t*)dst, (const uint32_t*)src, n4);
-    const size_t done = n4 * 4;
-    if (bytes > done) launch((uint8_t*)dst + done, (const uint8_t*)src + done, bytes - done);
-  } else {
-    launch((uint8_t*)dst, (const uint8_t*)src, bytes);
-  }
+  if ((a & 15) == 0) launch((uint4*)dst, (const uint4*)src, 16);
+  else if ((a & 3) == 0) launch((uint32_t*)dst, (const uint32_t*)src, 4);
+  else launch((uint8_t*)dst, (const uint8_t*)src, 1);
 }
 
 void apm_export(const ExportArgs* a, hipStream_t stream) {

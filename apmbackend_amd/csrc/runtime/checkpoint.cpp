@@ -651,6 +651,8 @@ std::string Engine::load_small_state(const std::string& path) {
     n_series_ = (int32_t)sr.size();
     perm_dirty_ = true;
     h_perm_.clear();
+    h_perm_key_.clear();
+    perm_uploaded_ = 0;
     series_service_uploaded_ = 0;
     svc_csr_n_ = -1;
   }

@@ -898,6 +898,8 @@ class Engine {
   std::vector<int32_t> server_name_off_, service_name_off_;
   std::vector<int32_t> h_ser_names_;            // 4 per series
   std::vector<int32_t> h_perm_;
+  std::vector<uint64_t> h_perm_key_;  // emit keys of h_perm_, same order
+  int64_t perm_uploaded_ = 0;          // d_perm_ holds h_perm_[0, perm_uploaded_)
   bool perm_dirty_ = true;
   size_t names_uploaded_ = 0, names_cap_ = 0;
   int32_t ser_names_uploaded_ = 0;
