@@ -35,6 +35,12 @@ namespace {
 
 constexpr int TB = 256;
 
+// Op grouping sort (table slot, ~20 bits, 100k-300k ops): rocprim's default switches to onesweep
+// only above 1M items and below that runs a block sort + ~8 merge passes (~140 us per batch on
+// the join's critical path, profiles/r3_*); onesweep does 3 digit passes.
+using OpSortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                             rocprim::default_config, 0>;
+
 __device__ __forceinline__ uint32_t grid_n(uint32_t n) { return (n + TB - 1) / TB; }
 
 // ------------------------------------------------------------------------ host-event selection
@@ -1071,26 +1077,60 @@ __global__ void k_gather_len(const int64_t* __restrict__ gid, int64_t n_upper, c
 }
 
 // Released lines out of the text ring into one contiguous blob, output-centric: one lane per
-// 16-byte output chunk finds its first line by binary search over the line offsets, gathers its
-// 16 bytes (crossing into the next lines as needed) and writes them with one 16-byte store --
-// fully coalesced writes, ~24x fewer lanes than a wave per ~100-byte line with byte stores.
+// 16-byte output chunk.  The block's first and last line are found by two lanes (binary search
+// over the line offsets) and shared through LDS, so each lane searches only the ~30 lines of its
+// block; a chunk inside one line is read with two aligned 16-byte loads and a byte funnel shift
+// (v_alignbyte), a chunk across line ends byte by byte; every lane writes one 16-byte store.
+__device__ __forceinline__ uint32_t line_of(const uint32_t* __restrict__ offs, int64_t lo, int64_t hi, uint64_t pos) {
+  // last l in [lo, hi) with offs[l] <= pos
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (offs[mid] <= pos) lo = mid; else hi = mid;
+  }
+  return (uint32_t)lo;
+}
+
 __global__ __launch_bounds__(256) void k_gather_copy(const int64_t* __restrict__ gid, int64_t n,
                                                      const char* __restrict__ ring, uint64_t ring_cap,
                                                      const uint32_t* __restrict__ offs, char* __restrict__ out) {
+  __shared__ uint32_t blk[2];
   const uint32_t total = offs[n];
-  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t start = c * 16;
-  if (start >= total) return;
-  int64_t lo = 0, hi = n;  // last line with offs[l] <= start
-  while (hi - lo > 1) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (offs[mid] <= start) lo = mid; else hi = mid;
+  const uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x * 16;
+  if (b0 >= total) return;  // (uniform per block)
+  if (threadIdx.x < 2) {
+    const uint64_t pos = threadIdx.x == 0 ? b0 : min<uint64_t>(b0 + (uint64_t)blockDim.x * 16, total) - 1;
+    blk[threadIdx.x] = line_of(offs, 0, n, pos);
   }
-  int64_t l = lo;
+  __syncthreads();
+  const uint64_t start = b0 + (uint64_t)threadIdx.x * 16;
+  if (start >= total) return;
+  int64_t l = line_of(offs, blk[0], (int64_t)blk[1] + 1, start);
   uint32_t l_off = offs[l], l_end = offs[l + 1];
   const char* src = ring + (((uint64_t)gid[l] >> 20) & (ring_cap - 1));
-  union { uint4 v; char b[16]; } u;
   const uint32_t m = (uint32_t)min<uint64_t>(16, total - start);
+  uint4 r;
+  if (m == 16 && start + 16 <= l_end) {
+    const char* p = src + (start - l_off);
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 15u);
+    const uint4* pa = reinterpret_cast<const uint4*>(p - sh);
+    const uint4 v0 = pa[0];
+    const uint4 v1 = sh ? pa[1] : v0;  // (the second block holds bytes of this line: in the ring)
+    const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    const uint32_t q = sh >> 2, rb = sh & 3u;
+    uint32_t d[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const uint32_t a0 = w[k], a1 = w[k < 7 ? k + 1 : 7], a2 = w[k < 6 ? k + 2 : 7], a3 = w[k < 5 ? k + 3 : 7];
+      d[k] = q == 0 ? a0 : q == 1 ? a1 : q == 2 ? a2 : a3;
+    }
+    r.x = __builtin_amdgcn_alignbyte(d[1], d[0], rb);
+    r.y = __builtin_amdgcn_alignbyte(d[2], d[1], rb);
+    r.z = __builtin_amdgcn_alignbyte(d[3], d[2], rb);
+    r.w = __builtin_amdgcn_alignbyte(d[4], d[3], rb);
+    *reinterpret_cast<uint4*>(out + start) = r;
+    return;
+  }
+  union { uint4 v; char b[16]; } u;
   for (uint32_t k = 0; k < m; ++k) {
     const uint32_t pos = (uint32_t)start + k;
     while (pos >= l_end) {  // next line (lines are never empty: each ends with '\n')
@@ -1255,7 +1295,7 @@ size_t apm_dj_tmp_bytes(uint32_t max_ev, uint32_t max_out, int table_bits) {
   const size_t n = std::max<size_t>(max_ev, 1) + 1;
   HIP_OK(rocprim::exclusive_scan(nullptr, a, (uint8_t*)nullptr, (uint32_t*)nullptr, 0u, n, rocprim::plus<uint32_t>(),
                                  (hipStream_t)0));
-  HIP_OK(rocprim::radix_sort_pairs(nullptr, b, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
+  HIP_OK(rocprim::radix_sort_pairs<OpSortCfg>(nullptr, b, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                    (uint32_t*)nullptr, n, 0, table_bits + 2, (hipStream_t)0));
   HIP_OK(rocprim::radix_sort_pairs(nullptr, c, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
                                    (uint32_t*)nullptr, n, 0, 64, (hipStream_t)0));
@@ -1295,10 +1335,10 @@ int apm_dj_join(DJArgs* a, hipStream_t s) {
     hipLaunchKernelGGL(k_soap_apply, dim3(a->n_chunks, SOAP_SEGS), dim3(APM_WAVE), 0, s, *a);
     hipLaunchKernelGGL(k_claim, dim3((n + TB - 1) / TB), dim3(TB), 0, s, *a);
     size_t need = 0;
-    HIP_OK(rocprim::radix_sort_pairs(nullptr, need, a->op_slot, a->op_slot_sorted, a->op_idx, a->op_idx_sorted,
+    HIP_OK(rocprim::radix_sort_pairs<OpSortCfg>(nullptr, need, a->op_slot, a->op_slot_sorted, a->op_idx, a->op_idx_sorted,
                                      (size_t)n, 0, a->table_bits + 2, s));
     if (need > a->tmp_bytes) return -1;
-    HIP_OK(rocprim::radix_sort_pairs(a->tmp, need, a->op_slot, a->op_slot_sorted, a->op_idx, a->op_idx_sorted,
+    HIP_OK(rocprim::radix_sort_pairs<OpSortCfg>(a->tmp, need, a->op_slot, a->op_slot_sorted, a->op_idx, a->op_idx_sorted,
                                      (size_t)n, 0, a->table_bits + 2, s));
   }
   (void)cap;

@@ -18,6 +18,8 @@
 
 #include <rocprim/rocprim.hpp>
 
+#include <cstdlib>
+
 namespace apm {
 
 namespace {
@@ -139,7 +141,10 @@ __global__ __launch_bounds__(256) void k_format_len(FormatArgs a) {
 // lane per store (256 B per store instruction).  A block whose range does not fit the stage
 // (very long names) writes its lines to HBM directly.
 constexpr int FMT_WAVE_LINES = 64;
-constexpr uint32_t FMT_LDS = 24576, FMT_LDS_COPY = 49152;
+// Stage size: 24 KB per 64-lane block held the write pass to 1.5 waves per SIMD (LDS-bound
+// occupancy) for a latency-bound per-lane formatter; 8 KB fits a block of typical lines (st ~90 B,
+// fs ~150 B) and allows 5 (VGPR-bound).  APM_FMT_STAGE=0 writes straight to HBM (dword stores).
+constexpr uint32_t FMT_LDS = 8192, FMT_LDS_COPY = 16384;
 
 __device__ __forceinline__ void wave_copy_out(const char* __restrict__ lds, char* __restrict__ out, uint32_t g0,
                                               uint32_t g1) {
@@ -158,7 +163,7 @@ __device__ __forceinline__ void wave_copy_out(const char* __restrict__ lds, char
 
 template <uint32_t LDS>
 __global__ __launch_bounds__(FMT_WAVE_LINES) void k_format_write(FormatArgs a, int32_t st_blocks) {
-  __shared__ __align__(16) char stage[LDS];
+  __shared__ __align__(16) char stage[LDS ? LDS : 16];
   const bool is_st = (int32_t)blockIdx.x < st_blocks;
   const int32_t nl = is_st ? a.n : a.n * a.n_lags;
   const int32_t j0 = (is_st ? (int32_t)blockIdx.x : (int32_t)blockIdx.x - st_blocks) * FMT_WAVE_LINES;
@@ -167,7 +172,7 @@ __global__ __launch_bounds__(FMT_WAVE_LINES) void k_format_write(FormatArgs a, i
   const uint32_t* off = is_st ? a.st_off : a.fs_off;
   char* out = is_st ? a.st_out : a.fs_out;
   const uint32_t g0 = off[j0], g1 = off[j1];
-  const bool lds = (g1 - (g0 & ~3u)) <= LDS;  // uniform across the block
+  const bool lds = LDS != 0 && (g1 - (g0 & ~3u)) <= LDS;  // uniform across the block
   if (j < j1) {
     bool fb = false;
     OutT<true> o(lds ? stage + (off[j] - (g0 & ~3u)) : out + off[j]);
@@ -322,7 +327,13 @@ void apm_format_write(FormatArgs* a, hipStream_t stream) {
   const int32_t fs_blocks = a->want_fs ? (a->n * a->n_lags + FMT_WAVE_LINES - 1) / FMT_WAVE_LINES : 0;
   const dim3 grid(st_blocks + fs_blocks);
   if (grid.x == 0) return;
-  if (a->fs_copy && a->want_fs)  // COPY rows are ~2x the wire line: a bigger LDS stage
+  static const int stage_mode = [] {
+    const char* e = std::getenv("APM_FMT_STAGE");  // diagnostic: 0 = no LDS stage
+    return e ? std::atoi(e) : 1;
+  }();
+  if (stage_mode == 0)
+    hipLaunchKernelGGL(k_format_write<0>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);
+  else if (a->fs_copy && a->want_fs)  // COPY rows are ~2x the wire line: a bigger LDS stage
     hipLaunchKernelGGL(k_format_write<FMT_LDS_COPY>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);
   else
     hipLaunchKernelGGL(k_format_write<FMT_LDS>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);

@@ -169,6 +169,14 @@ struct AlertArgs {
   double hard_min_tpm;
   int32_t both_only;
   int32_t max_out;
+  // Device-side cooldown pre-filter: time of the latest alert of the series' cooldown key (NaN:
+  // none).  A candidate the host's cooldown would certainly suppress -- same expression, same
+  // `now` -- is not emitted (cooldown times only grow, so a stale value can only let through a
+  // candidate the host then suppresses).  An alert storm otherwise ships ~20k candidates per
+  // rollover to the host decision.
+  const double* cool_t;       // [S] or nullptr
+  double now;
+  double cool_s;              // cooldown in seconds (perServiceAlertCooldownInMinutes * 60)
 };
 
 }  // namespace apm
@@ -214,6 +222,8 @@ void apm_format_fixed_batch(const double* d_x, int n, int f, char* d_out, hipStr
 int apm_format_plan(apm::FormatArgs* a, void* tmp, size_t tmp_bytes, hipStream_t stream);
 void apm_format_write(apm::FormatArgs* a, hipStream_t stream);
 void apm_alert_eval(apm::AlertArgs* a, hipStream_t stream);
+// dst[idx[i]] = val[i]; idx / val may be device views of pinned host memory
+void apm_scatter_f64(double* dst, const int32_t* idx, const double* val, int32_t n, hipStream_t stream);
 size_t apm_fleet_format_tmp_bytes(int32_t n_rows);
 int apm_fleet_format(apm::FleetFormatArgs* a, void* tmp, size_t tmp_bytes, hipStream_t stream);
 // after K11: the candidate count (clamped to max_n), the candidates and -- rows != 0 -- their window

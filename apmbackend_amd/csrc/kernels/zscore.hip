@@ -320,6 +320,10 @@ __global__ __launch_bounds__(256) void k_alert_eval(AlertArgs a) {
   if (!inc && cnt > 0) --cnt;
   if (cnt < 0) cnt = 0;
   a.counter[s] = cnt;
+  if (trigger && a.cool_t) {
+    const double ct = a.cool_t[s];
+    if (ct == ct && !((a.now - ct) / 1000.0 > a.cool_s)) trigger = false;  // in cooldown (host rule)
+  }
   if (trigger) {
     const int j = atomicAdd(a.n_out, 1);
     if (j < a.max_out) {
@@ -332,6 +336,12 @@ __global__ __launch_bounds__(256) void k_alert_eval(AlertArgs a) {
       a.out[j] = r;
     }
   }
+}
+
+__global__ void k_scatter_f64(double* __restrict__ dst, const int32_t* __restrict__ idx,
+                              const double* __restrict__ val, int32_t n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[idx[i]] = val[i];
 }
 
 }  // namespace apm
@@ -356,6 +366,10 @@ void launch_zscore(ZArgs* a, hipStream_t stream) {
 
 extern "C" {
 using namespace apm;
+
+void apm_scatter_f64(double* dst, const int32_t* idx, const double* val, int32_t n, hipStream_t stream) {
+  if (n > 0) hipLaunchKernelGGL(k_scatter_f64, dim3((n + 255) / 256), dim3(256), 0, stream, dst, idx, val, n);
+}
 
 void apm_zscore(ZArgs* a, int dtype_bytes, hipStream_t stream) {
   if (a->n_series <= 0) return;

@@ -460,8 +460,11 @@ void Engine::write_small_sections(BinWriter& w) {
   w.end();
 
   w.begin(SEC_ALERTS);
-  w.pod<uint64_t>(last_alert_.size());
-  for (auto& kv : last_alert_) { w.str(kv.first); w.pod(kv.second); }
+  {
+    const auto cool = cooldown_entries();
+    w.pod<uint64_t>(cool.size());
+    for (auto& kv : cool) { w.str(kv.first); w.pod(kv.second); }
+  }
   w.end();
 
   w.begin(SEC_OUTPUTS);
@@ -770,10 +773,12 @@ std::string Engine::load_small_state(const std::string& path) {
 
   rd.begin(SEC_ALERTS);
   last_alert_.clear();
+  node_cool_.clear();
   for (uint64_t k = rd.pod<uint64_t>(); k; --k) {
     std::string key = rd.str();
-    last_alert_[key] = rd.pod<double>();
+    put_cooldown(key, rd.pod<double>());
   }
+  rebuild_cool();
 
   rd.begin(SEC_OUTPUTS);
   for (int k = 0; k < N_OUT; ++k) blob_[k] = rd.str();

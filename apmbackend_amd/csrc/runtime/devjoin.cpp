@@ -814,26 +814,26 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
   auto span = [&](const char* name) { const double t = clock_ms(); spans.push_back({name, {sp, t}}); sp = t; };
   if (hops_.size() > h_hops_cap_) {
     if (h_hops_) HIP_OK(hipHostFree(h_hops_));
-    h_hops_cap_ = hops_.size() * 2 + 1024;
+    h_hops_cap_ = hops_.size() * 2 + 65536;
     HIP_OK(hipHostMalloc((void**)&h_hops_, h_hops_cap_ * sizeof(HostOp), hipHostMallocDefault));
     HIP_OK(hipHostGetDevicePointer((void**)&hd_hops_, h_hops_, 0));
   }
   if (hbuf_.size() > h_hbuf_cap_) {
     if (h_hbuf_) HIP_OK(hipHostFree(h_hbuf_));
-    h_hbuf_cap_ = hbuf_.size() * 2 + (1 << 16);
+    h_hbuf_cap_ = hbuf_.size() * 2 + (4 << 20);
     HIP_OK(hipHostMalloc((void**)&h_hbuf_, h_hbuf_cap_, hipHostMallocDefault));
     HIP_OK(hipHostGetDevicePointer((void**)&hd_hbuf_, h_hbuf_, 0));
   }
   span("u.hostgrow");
   if (hops_.size() > d_hops_cap_) {
-    d_hops_cap_ = hops_.size() * 2 + 1024;
+    d_hops_cap_ = hops_.size() * 2 + 65536;
     HostOp* p = nullptr;
     HIP_OK(hipMalloc((void**)&p, d_hops_cap_ * sizeof(HostOp)));
     allocs_.push_back(p);
     d_hops_ = p;  // the old buffer stays allocated (rare growth)
   }
   if (hbuf_.size() > d_hbuf_cap_) {
-    d_hbuf_cap_ = hbuf_.size() * 2 + (1 << 16);
+    d_hbuf_cap_ = hbuf_.size() * 2 + (4 << 20);
     uint8_t* p = nullptr;
     HIP_OK(hipMalloc((void**)&p, d_hbuf_cap_));
     allocs_.push_back(p);
@@ -942,7 +942,7 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
   f.ring_base = ring_reserve(c2.text_bytes);
   const size_t txt = (size_t)(want_tx ? c2.tx_text_bytes : 0) + (want_db ? c2.db_text_bytes : 0);
   if (txt > txt_cap_) {
-    const size_t cap = txt * 2 + (1 << 20);
+    const size_t cap = txt * 2 + (16 << 20);  // (grows at most a few times: a regrow costs ms)
     char* p = nullptr;
     HIP_OK(hipMalloc((void**)&p, cap * 2));
     if (d_txt_tx_) { HIP_OK(hipFree(d_txt_tx_)); device_bytes_ -= txt_cap_ * 2; }
@@ -953,7 +953,7 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
   }
   if (txt > h_txt_cap_) {
     if (h_txt_) HIP_OK(hipHostFree(h_txt_));
-    h_txt_cap_ = txt * 2 + (1 << 20);
+    h_txt_cap_ = txt * 2 + (32 << 20);
     HIP_OK(hipHostMalloc((void**)&h_txt_, h_txt_cap_, hipHostMallocDefault));
   }
   f.txt_tx = d_txt_tx_;

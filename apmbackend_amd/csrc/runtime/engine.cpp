@@ -356,6 +356,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   }
   d_hard_max_ = (double*)dmalloc((size_t)S * 8);
   d_suppressed_ = (uint8_t*)dmalloc(S);
+  d_cool_t_ = (double*)dmalloc((size_t)S * 8);
+  HIP_OK(hipMemsetAsync(d_cool_t_, 0xff, (size_t)S * 8, stream_));  // NaN: no cooldown
   d_emit_key_ = (uint64_t*)dmalloc((size_t)S * 8);
   // K12 formatter
   d_ser_names_ = (int32_t*)dmalloc((size_t)S * 16);
@@ -487,6 +489,8 @@ Engine::~Engine() {
     hipEventDestroy(ev_fmt_[k]);
   }
   if (h_roll_out_) hipHostFree(h_roll_out_);
+  if (cool_ev_) { hipEventSynchronize(cool_ev_); hipEventDestroy(cool_ev_); }
+  if (h_cool_idx_) { hipHostFree(h_cool_idx_); hipHostFree(h_cool_val_); }
   if (dj_) {
     hipStreamSynchronize(out_stream_);
     hipHostFree(h_ring_min_); hipHostFree(h_rel_n_); hipHostFree(h_rel_total_); hipHostFree(h_unseen_flag_);
@@ -598,6 +602,7 @@ int32_t Engine::series_for(int32_t server, int32_t service) {
   {
     std::lock_guard<std::mutex> g(series_mu_);
     series_.push_back(SeriesInfo{server, service, ek});
+    cool_series_[cool_key_of(s)].push_back(s);
   }
   h_emit_key_.push_back(ek);
   {
@@ -1904,6 +1909,10 @@ void Engine::refresh_unseen_active() {
 void Engine::do_rollover(int64_t L, double batch_t0) {
   finish_rollover();  // a previous rollover of this job still owns the candidate buffers
   const int64_t keep_iv = cfg_.window + cfg_.buffer;
+  // the decision's clock, fixed before K11 so its cooldown pre-filter and the host decide alike
+  roll_now_ = cfg_.alert_clock_entry ? (double)((L - cfg_.buffer - 1) * 10000)
+                                     : (double)std::chrono::duration_cast<std::chrono::milliseconds>(
+                                           std::chrono::system_clock::now().time_since_epoch()).count();
   ++metrics_.rollovers;
   // removeOldBuckets(36): drop every bucket < L - 36
   for (int i = 0; i < NSLOT; ++i) {
@@ -2036,6 +2045,7 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
     aa.n_series = n_series_; aa.lag_idx = l; aa.n_lags = cfg_.n_lags; aa.lag_suppressed = cfg_.lag_suppressed[l];
     aa.window = cfg_.alert_window; aa.threshold = cfg_.alert_threshold; aa.hard_min_ms = cfg_.hard_min_ms;
     aa.hard_min_tpm = cfg_.hard_min_tpm; aa.both_only = cfg_.both_only; aa.max_out = cfg_.max_alerts;
+    aa.cool_t = d_cool_t_; aa.now = roll_now_; aa.cool_s = cfg_.cooldown_ms / 1000.0;
     apm_alert_eval(&aa, stream_);
   }
   ++rollover_idx_;
@@ -2158,7 +2168,7 @@ void Engine::release_device_finish() {
       HIP_OK(hipEventSynchronize(ev_rel_[k]));
       if (total > h_rel_text_cap_[k]) {
         if (h_rel_text_[k]) HIP_OK(hipHostFree(h_rel_text_[k]));
-        h_rel_text_cap_[k] = total * 3 / 2 + (1 << 20);
+        h_rel_text_cap_[k] = total * 2 + (4 << 20);  // (a pinned allocation costs ms: 2x headroom)
         HIP_OK(hipHostMalloc((void**)&h_rel_text_[k], h_rel_text_cap_[k], hipHostMallocDefault));
       }
       const double tl0 = now_ms();
@@ -2204,10 +2214,8 @@ void Engine::flush_alerts(int64_t edge_ts) {
   for (int32_t i = 0; i < na; ++i) ord[i] = i;
   std::sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return alerts[a].order < alerts[b].order; });
   // per-(service|series) cooldown, first candidate in emission order wins (:436-468)
-  const double now = cfg_.alert_clock_entry ? (double)edge_ts
-                                            : (double)std::chrono::duration_cast<std::chrono::milliseconds>(
-                                                  std::chrono::system_clock::now().time_since_epoch()).count();
-  std::lock_guard<std::mutex> sg(series_mu_);  // series_ may grow on the stats thread meanwhile
+  const double now = cfg_.alert_clock_entry ? (double)edge_ts : roll_now_;
+  std::unique_lock<std::mutex> sg(series_mu_);  // series_ may grow on the stats thread meanwhile
   if (node_mode_) {
     // node-wide cooldown: queue the candidates (decided by the ingest thread, node_resolve)
     std::lock_guard<std::mutex> g(node_mu_);
@@ -2234,8 +2242,7 @@ void Engine::flush_alerts(int64_t edge_ts) {
       p.c.now = now;
       p.c.rank = coll_->rank();
       p.c.local_id = node_next_id_++;
-      p.server = servers_[si.server];
-      p.service = svc;
+      p.series = r.series;
       if (need_rows) { p.w = awin[i]; p.z = az[i]; }
       p.lag = cfg_.lags[r.lag_idx];
       node_q_.push_back(std::move(p));
@@ -2243,6 +2250,7 @@ void Engine::flush_alerts(int64_t edge_ts) {
     return;
   }
   std::string text;
+  std::vector<std::pair<uint64_t, double>> wins;
   for (int32_t j = 0; j < na; ++j) {
     const int32_t i = ord[j];
     const AlertRec& r = alerts[i];
@@ -2252,6 +2260,7 @@ void Engine::flush_alerts(int64_t edge_ts) {
     auto it = last_alert_.find(key);
     if (it != last_alert_.end() && !((now - it->second) / 1000.0 > cfg_.cooldown_ms / 1000.0)) continue;
     last_alert_[key] = now;
+    wins.push_back({cool_key_of(r.series), now});
     ++metrics_.alerts;
     if (need_rows) {
       const std::string fs = fmt::fs_line(edge_ts, servers_[si.server], dict_.service_name(si.service),
@@ -2260,10 +2269,76 @@ void Engine::flush_alerts(int64_t edge_ts) {
       text += '\n';
     }
   }
+  sg.unlock();
+  if (!wins.empty()) cool_mark(wins, stream_);
   if (!text.empty()) {  // (possibly the rollover lane) -> the al stream via node_text_
     std::lock_guard<std::mutex> g(node_mu_);
     node_text_ += text;
   }
+}
+
+uint64_t Engine::cool_key_of(int32_t s) const {
+  const SeriesInfo& si = series_[s];
+  const std::string& svc = dict_.service_name(si.service);
+  uint64_t h = hash_bytes((const uint8_t*)svc.data(), svc.size());
+  if (!cfg_.cooldown_by_service) {
+    const std::string& sv = servers_[si.server];
+    h = hash_mix(h, hash_bytes((const uint8_t*)sv.data(), sv.size()));
+  }
+  return h;
+}
+
+// Alerts decided (key, time): every local series of the key gets the time in d_cool_t_ (a scatter
+// reading the pinned staging directly).  Called by the one thread that decides alerts.
+void Engine::cool_mark(const std::vector<std::pair<uint64_t, double>>& wins, hipStream_t st) {
+  std::vector<std::pair<int32_t, double>> upd;
+  {
+    std::lock_guard<std::mutex> g(series_mu_);
+    for (const auto& w : wins) {
+      auto it = cool_series_.find(w.first);
+      if (it == cool_series_.end()) continue;
+      for (int32_t s : it->second) upd.push_back({s, w.second});
+    }
+  }
+  if (upd.empty()) return;
+  if (!cool_ev_) HIP_OK(hipEventCreateWithFlags(&cool_ev_, hipEventDisableTiming));
+  else HIP_OK(hipEventSynchronize(cool_ev_));  // the previous scatter read the staging
+  if (upd.size() > cool_cap_) {
+    if (h_cool_idx_) { HIP_OK(hipHostFree(h_cool_idx_)); HIP_OK(hipHostFree(h_cool_val_)); }
+    cool_cap_ = std::max<size_t>(upd.size() * 2, 4096);
+    HIP_OK(hipHostMalloc((void**)&h_cool_idx_, cool_cap_ * 4, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void**)&h_cool_val_, cool_cap_ * 8, hipHostMallocDefault));
+  }
+  for (size_t i = 0; i < upd.size(); ++i) { h_cool_idx_[i] = upd[i].first; h_cool_val_[i] = upd[i].second; }
+  int32_t* di = nullptr;
+  double* dv = nullptr;
+  HIP_OK(hipHostGetDevicePointer((void**)&di, h_cool_idx_, 0));
+  HIP_OK(hipHostGetDevicePointer((void**)&dv, h_cool_val_, 0));
+  apm_scatter_f64(d_cool_t_, di, dv, (int32_t)upd.size(), st);
+  HIP_OK(hipEventRecord(cool_ev_, st));
+}
+
+// After a restore / cooldown import: the key map and d_cool_t_ from series_ and both maps.
+void Engine::rebuild_cool() {
+  std::vector<double> t((size_t)std::max(n_series_, 1), std::nan(""));
+  {
+    std::lock_guard<std::mutex> g(series_mu_);
+    cool_series_.clear();
+    for (int32_t s = 0; s < n_series_; ++s) {
+      const uint64_t k = cool_key_of(s);
+      cool_series_[k].push_back(s);
+      auto nc = node_cool_.find(k);
+      if (nc != node_cool_.end()) t[s] = nc->second;
+      const SeriesInfo& si = series_[s];
+      std::string key = dict_.service_name(si.service);
+      if (!cfg_.cooldown_by_service) key = servers_[si.server] + '\x01' + key;
+      auto la = last_alert_.find(key);
+      if (la != last_alert_.end() && !(la->second <= t[s])) t[s] = la->second;
+    }
+  }
+  HIP_OK(hipMemsetAsync(d_cool_t_, 0xff, (size_t)cfg_.max_series * 8, stream_));
+  if (n_series_ > 0) HIP_OK(hipMemcpyAsync(d_cool_t_, t.data(), (size_t)n_series_ * 8, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
 }
 
 int32_t Engine::intern_name(const std::string& name) {
@@ -2285,7 +2360,9 @@ void Engine::dfree(void* p) {
 
 void* Engine::regrow(void* old, size_t& cap, size_t need) {
   if (need <= cap && old) return old;
-  size_t nc = std::max<size_t>(need + need / 2, 1 << 20);
+  // 2x headroom: a regrow syncs the stream and hipFree waits for the device (a few ms of one
+  // batch), so the per-batch buffers must stop growing during the warm-up
+  size_t nc = std::max<size_t>(2 * need, 4 << 20);
   if (old) {
     HIP_OK(hipStreamSynchronize(stream_));
     HIP_OK(hipFree(old));
@@ -2477,7 +2554,7 @@ void Engine::format_rollover_text(int64_t edge_ts) {
     const size_t st_total = h_fmt_meta_[4 * k], fs_total = h_fmt_meta_[4 * k + 1];
     if (st_total + fs_total > h_fmt_cap_[k]) {
       if (h_fmt_out_[k]) HIP_OK(hipHostFree(h_fmt_out_[k]));
-      h_fmt_cap_[k] = (st_total + fs_total) * 3 / 2 + (1 << 20);
+      h_fmt_cap_[k] = (st_total + fs_total) * 2 + (4 << 20);
       HIP_OK(hipHostMalloc((void**)&h_fmt_out_[k], h_fmt_cap_[k], hipHostMallocDefault));
     }
     char* h = h_fmt_out_[k];
@@ -3156,8 +3233,8 @@ void Engine::node_round(uint64_t round, bool wait, bool all) {
     while (upto != UINT64_MAX && n < node_cap_ && !node_q_.empty() && node_q_.front().seq_batch <= upto) {
       NodePayload& p = node_q_.front();
       out[n++] = p.c;
-      const uint32_t id = p.c.local_id;
-      node_sent_.emplace(id, std::move(p));
+      if (node_sent_.empty()) node_sent_base_ = p.c.local_id;
+      node_sent_.push_back(p);
       node_q_.pop_front();
     }
     hdr->count = n;
@@ -3197,27 +3274,37 @@ void Engine::node_resolve() {
   });
   const int me = coll_->rank();
   std::string text;
+  std::vector<const NodePayload*> won;
+  std::vector<const NodeCand*> won_c;
+  std::vector<std::pair<uint64_t, double>> wins;
   for (const NodeCand& c : node_pool_) {
-    char key[20];
-    key[0] = '\x02';  // node-wide keys (hashes) share the checkpointed cooldown map
-    for (int i = 0; i < 16; ++i) key[1 + i] = "0123456789abcdef"[(c.key >> (60 - 4 * i)) & 15];
-    const std::string k(key, 17);
-    auto it = last_alert_.find(k);
-    if (it != last_alert_.end() && !((c.now - it->second) / 1000.0 > cfg_.cooldown_ms / 1000.0)) continue;
-    last_alert_[k] = c.now;
+    auto it = node_cool_.find(c.key);
+    if (it != node_cool_.end() && !((c.now - it->second) / 1000.0 > cfg_.cooldown_ms / 1000.0)) continue;
+    node_cool_[c.key] = c.now;
+    wins.push_back({c.key, c.now});
     if (c.rank != me) continue;
     ++node_alerts_;
-    auto p = node_sent_.find(c.local_id);
-    if (p == node_sent_.end()) throw std::runtime_error("node alerts: lost candidate payload");
-    if (want(OUT_AL)) {
-      const NodePayload& q = p->second;
-      const std::string fs = fmt::fs_line(c.edge_ts, q.server, q.service, q.lag, q.w, q.z);
-      text += fmt::al_line(c.now, c.edge_ts, q.server, q.service, c.causes, fs);
+    const uint32_t idx = c.local_id - node_sent_base_;
+    if (idx >= node_sent_.size()) throw std::runtime_error("node alerts: lost candidate payload");
+    won.push_back(&node_sent_[idx]);
+    won_c.push_back(&c);
+  }
+  if (want(OUT_AL) && !won.empty()) {
+    std::lock_guard<std::mutex> sg(series_mu_);  // series_ may grow on the stats thread meanwhile
+    for (size_t i = 0; i < won.size(); ++i) {
+      const NodePayload& q = *won[i];
+      const NodeCand& c = *won_c[i];
+      const SeriesInfo& si = series_[q.series];
+      const std::string& server = servers_[si.server];
+      const std::string& service = dict_.service_name(si.service);
+      const std::string fs = fmt::fs_line(c.edge_ts, server, service, q.lag, q.w, q.z);
+      text += fmt::al_line(c.now, c.edge_ts, server, service, c.causes, fs);
       text += '\n';
     }
   }
   node_pool_.clear();
   node_sent_.clear();  // everything sent so far was in this pool
+  if (!wins.empty()) cool_mark(wins, coll_stream_);
   if (!text.empty()) {
     std::lock_guard<std::mutex> g(node_mu_);
     node_text_ += text;

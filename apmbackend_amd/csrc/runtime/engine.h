@@ -481,12 +481,17 @@ class Engine {
   };
   struct NodeHdr { int32_t count, all_sent, pad[14]; };  // 64 B
   // a candidate's fs text is formatted only if it wins the node-wide cooldown (node_resolve)
-  struct NodePayload { uint64_t seq_batch; NodeCand c; std::string server, service; WinStat w; ZOut z; int32_t lag; };
+  // (no strings: an alert storm queues thousands of candidates per rollover; names are looked up
+  // for the winners only)
+  struct NodePayload { uint64_t seq_batch; NodeCand c; int32_t series; int32_t lag; WinStat w; ZOut z; };
   bool node_mode_ = false;
   int32_t node_cap_ = 512;                 // candidates per rank per round
   std::mutex node_mu_;                     // node_q_ / node_text_
   std::deque<NodePayload> node_q_;         // stats thread -> ingest thread (unsent)
-  std::unordered_map<uint32_t, NodePayload> node_sent_;  // sent, awaiting a decision (ingest)
+  std::deque<NodePayload> node_sent_;      // sent, awaiting a decision (ingest); local ids are
+  uint32_t node_sent_base_ = 0;            // consecutive: payload of id i = node_sent_[i - base]
+  // node-wide cooldowns by key hash (checkpointed inside last_alert_ as "\x02" + 16 hex digits)
+  std::unordered_map<uint64_t, double> node_cool_;
   uint32_t node_next_id_ = 0;
   std::vector<NodeCand> node_pool_;        // gathered, undecided (ingest thread)
   std::string node_text_;                  // decided al rows of this rank -> blob_[OUT_AL]
@@ -856,6 +861,45 @@ class Engine {
   int32_t* hd_n_alerts_ = nullptr;
   hipEvent_t ev_alerts_ = nullptr;  // the rollover's candidates are in host memory
   std::unordered_map<std::string, double> last_alert_;  // cooldown key -> alertTimestamp
+  // K11 cooldown pre-filter (AlertArgs::cool_t): per series, the time of its cooldown key's latest
+  // alert; cool_series_ maps a key (hash as in NodeCand::key) to this rank's series (series_mu_)
+  double* d_cool_t_ = nullptr;
+  std::unordered_map<uint64_t, std::vector<int32_t>> cool_series_;
+  double roll_now_ = 0;                    // `now` of the rollover in flight (K11 and the decision)
+  int32_t* h_cool_idx_ = nullptr;          // pinned staging of cooldown updates
+  double* h_cool_val_ = nullptr;
+  size_t cool_cap_ = 0;
+  hipEvent_t cool_ev_ = nullptr;
+  uint64_t cool_key_of(int32_t s) const;   // (series_mu_ held, or the series_ owner)
+  void cool_mark(const std::vector<std::pair<uint64_t, double>>& wins, hipStream_t st);
+  void rebuild_cool();
+  static std::string node_cool_key(uint64_t k) {
+    std::string s(17, '\x02');
+    for (int i = 0; i < 16; ++i) s[1 + i] = "0123456789abcdef"[(k >> (60 - 4 * i)) & 15];
+    return s;
+  }
+  static bool parse_node_cool_key(const std::string& s, uint64_t& k) {
+    if (s.size() != 17 || s[0] != '\x02') return false;
+    k = 0;
+    for (int i = 1; i < 17; ++i) {
+      const char c = s[i];
+      const int v = c >= '0' && c <= '9' ? c - '0' : (c >= 'a' && c <= 'f' ? c - 'a' + 10 : -1);
+      if (v < 0) return false;
+      k = (k << 4) | (uint64_t)v;
+    }
+    return true;
+  }
+  // every cooldown entry, node-wide ones in their string form (checkpoint / export)
+  std::vector<std::pair<std::string, double>> cooldown_entries() const {
+    std::vector<std::pair<std::string, double>> v(last_alert_.begin(), last_alert_.end());
+    for (auto& kv : node_cool_) v.emplace_back(node_cool_key(kv.first), kv.second);
+    return v;
+  }
+  void put_cooldown(const std::string& key, double t) {
+    uint64_t k;
+    if (parse_node_cool_key(key, k)) node_cool_[k] = t;
+    else last_alert_[key] = t;
+  }
 
   // tx upload + release pool
   TxRec* d_tx_ = nullptr;

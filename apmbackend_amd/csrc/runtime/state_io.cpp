@@ -362,12 +362,13 @@ void Engine::import_pending(const std::vector<int64_t>& ends, const std::vector<
 
 std::vector<std::pair<std::string, double>> Engine::export_cooldowns() {
   flush();
-  return std::vector<std::pair<std::string, double>>(last_alert_.begin(), last_alert_.end());
+  return cooldown_entries();
 }
 
 void Engine::import_cooldowns(const std::vector<std::pair<std::string, double>>& c) {
   flush();
-  for (auto& kv : c) last_alert_[kv.first] = kv.second;
+  for (auto& kv : c) put_cooldown(kv.first, kv.second);
+  rebuild_cool();
 }
 
 std::vector<int32_t> Engine::export_alert_counters(int lag_idx) {
