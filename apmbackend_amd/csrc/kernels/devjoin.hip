@@ -22,6 +22,7 @@
 #include <rocprim/rocprim.hpp>
 
 #include <climits>
+#include <cstdlib>
 #include <cstddef>
 
 #include "devjoin_api.h"
@@ -1020,7 +1021,11 @@ __global__ void k_cands(DJFormatArgs f, uint32_t n) {
     f.cand_bucket[k] = f.tx_bucket[j];
   }
   const int32_t r = f.tx_raw[j];
-  if (f.raw_series[r] < 0 && f.raw_first[r] == (int32_t)j) {
+  // raw_first[r] == j: k_write stored series -1 for tx j (the first such of raw r).  Not
+  // `raw_series[r] < 0` re-read here: the stats stream's scatter of a newly resolved raw may land
+  // between k_write and this kernel, and the tx would then keep series -1 unreported (a lost
+  // sample, seen as a flaky st difference between two identical engines).
+  if (f.raw_first[r] == (int32_t)j) {
     const uint32_t k = atomicAdd(&f.counts->n_unresolved, 1u);
     f.unresolved[2 * k] = j;
     f.unresolved[2 * k + 1] = (uint32_t)r;
@@ -1334,12 +1339,21 @@ int apm_dj_join(DJArgs* a, hipStream_t s) {
     hipLaunchKernelGGL(k_soap_carry, dim3((a->n_chunks + 63) / 64), dim3(64), 0, s, *a);
     hipLaunchKernelGGL(k_soap_apply, dim3(a->n_chunks, SOAP_SEGS), dim3(APM_WAVE), 0, s, *a);
     hipLaunchKernelGGL(k_claim, dim3((n + TB - 1) / TB), dim3(TB), 0, s, *a);
+    static const bool merge_sort = [] { const char* e = std::getenv("APM_OPSORT"); return e && e[0] == 'm'; }();
     size_t need = 0;
-    HIP_OK(rocprim::radix_sort_pairs<OpSortCfg>(nullptr, need, a->op_slot, a->op_slot_sorted, a->op_idx, a->op_idx_sorted,
-                                     (size_t)n, 0, a->table_bits + 2, s));
-    if (need > a->tmp_bytes) return -1;
-    HIP_OK(rocprim::radix_sort_pairs<OpSortCfg>(a->tmp, need, a->op_slot, a->op_slot_sorted, a->op_idx, a->op_idx_sorted,
-                                     (size_t)n, 0, a->table_bits + 2, s));
+    if (merge_sort) {  // diagnostic: rocprim's default (block sort + merge passes)
+      HIP_OK(rocprim::radix_sort_pairs(nullptr, need, a->op_slot, a->op_slot_sorted, a->op_idx, a->op_idx_sorted,
+                                       (size_t)n, 0, a->table_bits + 2, s));
+      if (need > a->tmp_bytes) return -1;
+      HIP_OK(rocprim::radix_sort_pairs(a->tmp, need, a->op_slot, a->op_slot_sorted, a->op_idx, a->op_idx_sorted,
+                                       (size_t)n, 0, a->table_bits + 2, s));
+    } else {
+      HIP_OK(rocprim::radix_sort_pairs<OpSortCfg>(nullptr, need, a->op_slot, a->op_slot_sorted, a->op_idx,
+                                                  a->op_idx_sorted, (size_t)n, 0, a->table_bits + 2, s));
+      if (need > a->tmp_bytes) return -1;
+      HIP_OK(rocprim::radix_sort_pairs<OpSortCfg>(a->tmp, need, a->op_slot, a->op_slot_sorted, a->op_idx,
+                                                  a->op_idx_sorted, (size_t)n, 0, a->table_bits + 2, s));
+    }
   }
   (void)cap;
   // expiry first: its outputs precede every line emission, and it must read the expiring entries
