@@ -142,7 +142,8 @@ py::dict metrics_dict(const EngineMetrics& m) {
   py::dict d;
   d["batches"] = m.batches; d["bytes"] = m.bytes; d["lines"] = m.lines; d["events"] = m.events;
   d["tx"] = m.tx; d["tx_db"] = m.tx_db; d["tx_dropped"] = m.tx_dropped; d["rollovers"] = m.rollovers;
-  d["alerts"] = m.alerts; d["alert_candidates"] = m.alert_candidates; d["released"] = m.released;
+  d["alerts"] = m.alerts; d["alert_candidates"] = m.alert_candidates;
+  d["alert_candidates_dropped"] = m.alert_candidates_dropped; d["released"] = m.released;
   d["t_join_shards_ms"] = m.t_join_shards_ms; d["t_merge_ms"] = m.t_merge_ms;
   d["t_shard_busy_ms"] = m.t_shard_busy_ms; d["t_shard_max_ms"] = m.t_shard_max_ms;
   d["t_out_ms"] = m.t_out_ms;

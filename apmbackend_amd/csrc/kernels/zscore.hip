@@ -404,8 +404,9 @@ struct AlertGather {
 // count, and reads the rows, by waiting on one event instead of a stream drain + three D2H copies.
 __global__ void k_alert_gather(AlertGather a) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int n = min(*a.n_dev, a.max_n);
-  if (i == 0) *a.n_out = n;
+  const int raw = *a.n_dev;
+  const int n = min(raw, a.max_n);
+  if (i == 0) { a.n_out[0] = n; a.n_out[1] = raw; }  // (raw > n: candidates dropped, counted)
   if (i >= n) return;
   const AlertRec r = a.alerts[i];
   a.alerts_out[i] = r;

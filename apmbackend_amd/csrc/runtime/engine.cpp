@@ -2197,8 +2197,9 @@ void Engine::release_device_finish() {
 }
 
 void Engine::flush_alerts(int64_t edge_ts) {
-  const int32_t na = *h_n_alerts_;  // apm_alert_gather's clamped count (ev_alerts_ has completed)
+  const int32_t na = h_n_alerts_[0];  // apm_alert_gather's clamped count (ev_alerts_ has completed)
   metrics_.alert_candidates += na;
+  if (h_n_alerts_[1] > na) metrics_.alert_candidates_dropped += (uint64_t)(h_n_alerts_[1] - na);
   if (na <= 0) return;
   const bool need_rows = want(OUT_AL);
   // one sequential copy out of the GPU-written pinned buffers before the sort's random reads

@@ -158,6 +158,7 @@ struct CheckpointInfo {
 struct EngineMetrics {
   uint64_t batches = 0, bytes = 0, lines = 0, events = 0, tx = 0, tx_db = 0, tx_dropped = 0;
   uint64_t rollovers = 0, alerts = 0, alert_candidates = 0, series = 0, released = 0;
+  uint64_t alert_candidates_dropped = 0;  // beyond maxAlertCandidates in one rollover (reported)
   uint64_t formatted_bytes = 0, format_fallbacks = 0, lockstep_rollovers = 0;
   uint64_t series_overflow_tx = 0;  // tx whose series could not be created (gpu.maxSeries full)
   uint64_t spill_dropped = 0;       // samples lost to a full bucket spill list (gpu.bucketOverflowCapacity)
@@ -485,7 +486,9 @@ class Engine {
   // for the winners only)
   struct NodePayload { uint64_t seq_batch; NodeCand c; int32_t series; int32_t lag; WinStat w; ZOut z; };
   bool node_mode_ = false;
-  int32_t node_cap_ = 512;                 // candidates per rank per round
+  // candidates per rank per round: an alert storm (thousands of new keys per interval) must not
+  // outgrow the exchange, or the unsent backlog and the decision lag grow without bound
+  int32_t node_cap_ = 4096;
   std::mutex node_mu_;                     // node_q_ / node_text_
   std::deque<NodePayload> node_q_;         // stats thread -> ingest thread (unsent)
   std::deque<NodePayload> node_sent_;      // sent, awaiting a decision (ingest); local ids are

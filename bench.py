@@ -93,6 +93,11 @@ def main():
                     help="planted incident: EJB services getSvc0000.. run --anomaly-factor x slower on every "
                          "JVM from the first batch after the history warm-up (the bench's al rows)")
     ap.add_argument("--anomaly-factor", type=float, default=25.0)
+    ap.add_argument("--pre-batches", type=int, default=33,
+                    help="untimed batches before the synthetic z-score pre-history is drawn: the 31-bucket "
+                         "window is full by then, so the history is drawn around the steady window stats "
+                         "(drawn around a 2-bucket window it sat ~20 %% below the real p75/p95 and turned "
+                         "the run into an alert storm after ~50 batches)")
     ap.add_argument("--audit-fraction", type=float, default=0.02,
                     help="share of requests logged with an audit trail (K5: the per-file state machine "
                          "runs in the host pre-pass)")
@@ -187,18 +192,19 @@ def main():
         if inserter is None or k == "sx":
             eng.eng.set_sink_fd(k, sink_fd)
     start = 1578391200000
+    PRE = max(2, args.pre_batches)  # pre-history batches (untimed, before warm_history)
     step_ms = int(args.batch_seconds * 1000)
     gen = N.SynthGen({"servers": args.servers, "ejb_services": args.ejb, "provider_services": args.providers,
                       "tx_per_sec_per_server": args.tx_rate, "seed": 1 + rank,
                       "server_offset": rank * args.servers,
                       "anomaly_services": args.anomaly_services, "anomaly_factor": args.anomaly_factor,
-                      "anomaly_start_ms": start + 2 * step_ms, "ejb_pool": args.ejb_pool,
+                      "anomaly_start_ms": start + PRE * step_ms, "ejb_pool": args.ejb_pool,
                       "provider_pool": args.provider_pool, "audit": args.audit_fraction})
     for path, kind, server in gen.files():
         eng.add_file(path, {0: "SOAP", 1: "SERVER", 2: "APP"}[kind], server)
 
     # ---- corpus (untimed): warmup + steps batches of `batch_seconds` of log time, pinned
-    n_batches = args.warmup + args.steps + 2
+    n_batches = args.warmup + args.steps + PRE
     batches = []
     total = 0
     raw = []
@@ -223,8 +229,8 @@ def main():
     if args.trace:
         eng.eng.set_trace(True)
 
-    last = 2 + args.warmup + args.steps - 1
-    first_timed = 2 + args.warmup
+    last = PRE + args.warmup + args.steps - 1
+    first_timed = PRE + args.warmup
 
     jmx_lines = []
     if args.jmx:  # one JMX record per JVM per batch (pull_jvm_stats.js at the bench's time scale)
@@ -255,11 +261,11 @@ def main():
             eng.eng.process_batch_ptr(ptr, n, chunks, -1.0)
 
     # ---- warmup (first batches create the series; then the z-score rings get a pre-history)
-    for i in range(2):
+    for i in range(PRE):
         step(i)
     if not args.no_warm:
         eng.eng.warm_history(12345 + rank)
-    for i in range(2, 2 + args.warmup):
+    for i in range(PRE, PRE + args.warmup):
         step(i)
     eng.eng.flush()
     if args.anomaly_services > 0:
@@ -284,7 +290,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(2 + args.warmup, 2 + args.warmup + args.steps):
+    for i in range(PRE, PRE + args.warmup + args.steps)[args.warmup:]:
         step(i)
     eng.eng.flush()  # the last batch's stats stage runs on the engine's stats thread
     if inserter is not None:  # alerts paged + every DB row of the timed batches written
@@ -362,11 +368,13 @@ def main():
                                                                  "pool_exhausted")},
             "capacity_grows": {"spill": int(m1.get("spill_grows", 0)),
                                **{k: int(m1["join"].get(k + "_grows", 0)) for k in ("table", "arena", "pool")}},
+            "pre_history_batches": PRE,
             "audit_fraction": args.audit_fraction,
             "host_prepass_events_per_step": round((m1["join"].get("host_events", 0) - m0["join"].get("host_events", 0))
                                                   / args.steps, 1),
             "alerts": int(m1["alerts"] - m0["alerts"]),
             "alert_candidates": int(m1["alert_candidates"] - m0["alert_candidates"]),
+            "alert_candidates_dropped": int(m1.get("alert_candidates_dropped", 0)),
             "device_GB": round(eng.eng.device_bytes() / 1e9, 1),
         }
         if inserter is not None:
