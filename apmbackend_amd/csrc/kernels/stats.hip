@@ -656,7 +656,12 @@ __global__ __launch_bounds__(256) void k_copy(W* __restrict__ dst, const W* __re
                                               uint32_t tail) {
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (size_t i = t0; i < n; i += stride) dst[i] = src[i];
+  size_t i = t0;
+  for (; i + 3 * stride < n; i += 4 * stride) {  // four loads in flight per lane (host-link latency)
+    const W a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    dst[i] = a; dst[i + stride] = b; dst[i + 2 * stride] = c; dst[i + 3 * stride] = d;
+  }
+  for (; i < n; i += stride) dst[i] = src[i];
   if (t0 < tail) tdst[t0] = tsrc[t0];  // the bytes after the last full W (same launch)
 }
 

@@ -77,6 +77,8 @@ DeviceJoin::DeviceJoin(const DevJoinConfig& cfg, Dictionary* dict, const std::ve
     HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     const char* pe = std::getenv("APM_JOIN_PRIO");
     HIP_OK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, pe && pe[0] == '0' ? lo : hi));
+    HIP_OK(hipStreamCreateWithPriority(&up_stream_, hipStreamNonBlocking, hi));
+    HIP_OK(hipEventCreateWithFlags(&up_ev_, hipEventDisableTiming));
   }
   const uint32_t E = std::max<uint32_t>(cfg_.max_events, 1024);
   out_cap_ = 2 * E + (1u << 16);
@@ -193,6 +195,8 @@ DeviceJoin::~DeviceJoin() {
   if (h_txt_) hipHostFree(h_txt_);
   for (void* p : allocs_) hipFree(p);
   hipStreamDestroy(stream_);
+  if (up_stream_) { hipStreamSynchronize(up_stream_); hipStreamDestroy(up_stream_); }
+  if (up_ev_) hipEventDestroy(up_ev_);
 }
 
 // ---------------------------------------------------------------------------- parse-side hooks
@@ -815,13 +819,13 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
   if (hops_.size() > h_hops_cap_) {
     if (h_hops_) HIP_OK(hipHostFree(h_hops_));
     h_hops_cap_ = hops_.size() * 2 + 65536;
-    HIP_OK(hipHostMalloc((void**)&h_hops_, h_hops_cap_ * sizeof(HostOp), hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void**)&h_hops_, h_hops_cap_ * sizeof(HostOp), host_flags_()));
     HIP_OK(hipHostGetDevicePointer((void**)&hd_hops_, h_hops_, 0));
   }
   if (hbuf_.size() > h_hbuf_cap_) {
     if (h_hbuf_) HIP_OK(hipHostFree(h_hbuf_));
     h_hbuf_cap_ = hbuf_.size() * 2 + (4 << 20);
-    HIP_OK(hipHostMalloc((void**)&h_hbuf_, h_hbuf_cap_, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void**)&h_hbuf_, h_hbuf_cap_, host_flags_()));
     HIP_OK(hipHostGetDevicePointer((void**)&hd_hbuf_, h_hbuf_, 0));
   }
   span("u.hostgrow");
@@ -840,17 +844,31 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
     d_hbuf_ = p;
   }
   span("u.devgrow");
+  // The host ops (~160 KB a batch) are read by a kernel over the host link.  A DMA copy queues
+  // behind the next batch's 22 MB of log bytes on the copy engine: on its own stream it cost
+  // 1.44-1.50 vs 1.20-1.23 ms per step (A/B, 60 steps), on the join stream hipMemcpyAsync also
+  // held this thread ~0.6 ms.  APM_HOPS_COPY=dma: the DMA path on its own stream.
+  static const bool kcopy = [] { const char* e = std::getenv("APM_HOPS_COPY"); return !e || e[0] != 'd'; }();
+  bool uploaded = false;
   if (!hops_.empty()) {
     std::memcpy(h_hops_, hops_.data(), hops_.size() * sizeof(HostOp));
     span("u.hops.memcpy");
-    apm_copy(d_hops_, hd_hops_, hops_.size() * sizeof(HostOp), st);  // (kernel copy: never blocks)
+    if (kcopy) apm_copy(d_hops_, hd_hops_, hops_.size() * sizeof(HostOp), st);
+    else HIP_OK(hipMemcpyAsync(d_hops_, h_hops_, hops_.size() * sizeof(HostOp), hipMemcpyHostToDevice, up_stream_));
+    uploaded = true;
     span("u.hops.h2d");
   }
   if (!hbuf_.empty()) {
     std::memcpy(h_hbuf_, hbuf_.data(), hbuf_.size());
     span("u.hbuf.memcpy");
-    apm_copy(d_hbuf_, hd_hbuf_, hbuf_.size(), st);
+    if (kcopy) apm_copy(d_hbuf_, hd_hbuf_, hbuf_.size(), st);
+    else HIP_OK(hipMemcpyAsync(d_hbuf_, h_hbuf_, hbuf_.size(), hipMemcpyHostToDevice, up_stream_));
+    uploaded = true;
     span("u.hbuf.h2d");
+  }
+  if (uploaded && !kcopy) {
+    HIP_OK(hipEventRecord(up_ev_, up_stream_));
+    HIP_OK(hipStreamWaitEvent(st, up_ev_, 0));
   }
   // ---- file -> server table
   if (files_->size() > files_uploaded_) {

@@ -195,6 +195,17 @@ class DeviceJoin {
   const std::vector<FileInfo>* files_;
   const std::vector<std::string>* servers_;
   hipStream_t stream_ = nullptr;  // join stream
+  hipStream_t up_stream_ = nullptr;  // host-op uploads by DMA (nothing queued ahead of them)
+  // flags of the host-op staging (read by a kernel over the host link): APM_HOPS_NC=1 allocates it
+  // non-coherent (the GPU may then fetch whole cache lines)
+  static unsigned host_flags_() {
+    static const unsigned f = [] {
+      const char* e = std::getenv("APM_HOPS_NC");
+      return (e && e[0] == '1') ? (unsigned)hipHostMallocNonCoherent : (unsigned)hipHostMallocDefault;
+    }();
+    return f;
+  }
+  hipEvent_t up_ev_ = nullptr;
   size_t device_bytes_ = 0;
   std::vector<void*> allocs_;
 

@@ -38,11 +38,14 @@ def run(args, cfg: Dict[str, Any], N, rank: int = 0) -> Dict[str, Any]:
 def _run(args, cfg, N, rank, root, IngestService):
     start = 1578391200000
     step_ms = int(args.batch_seconds * 1000)
+    # pre-history batches before the synthetic z-score history (as the headline: bench.py
+    # --pre-batches): the 31-bucket window is full when the history is drawn
+    PRE = max(2, getattr(args, "pre_batches", 33))
     gen = N.SynthGen({"servers": args.servers, "ejb_services": args.ejb, "provider_services": args.providers,
                       "tx_per_sec_per_server": args.tx_rate, "seed": 1 + rank,
                       "server_offset": rank * args.servers,
                       "anomaly_services": args.anomaly_services, "anomaly_factor": args.anomaly_factor,
-                      "anomaly_start_ms": start + 2 * step_ms})
+                      "anomaly_start_ms": start + PRE * step_ms})
     paths = []
     for p, _kind, server in gen.files():
         d = os.path.join(root, "logs", server)
@@ -91,15 +94,15 @@ def _run(args, cfg, N, rank, root, IngestService):
             if svc.step() == 0:
                 svc._idle(0.001)
 
-    append(0, 2)
+    append(0, PRE)
     drain()
     svc.eng.eng.flush()
     svc.eng.eng.warm_history(12345 + rank)
-    append(2, 2 + args.warmup)
+    append(PRE, PRE + args.warmup)
     drain()
     svc.eng.eng.flush()
     svc.inserter.flush_all()
-    append(2 + args.warmup, 2 + args.warmup + args.steps)  # the backlog the timed region consumes
+    append(PRE + args.warmup, PRE + args.warmup + args.steps)  # the backlog the timed region consumes
     m0 = svc.eng.metrics()
     s0 = svc.inserter.sink_stats()
     ck0 = svc.eng.eng.checkpoint_info() if ckpt else None
@@ -150,6 +153,7 @@ def _run(args, cfg, N, rank, root, IngestService):
         "fleet": fleet,
         "fs_type": _fs_type(root),
         "batches": pf["batches"],
+        "pre_history_batches": PRE,
     }
 
 
