@@ -90,8 +90,12 @@ def _run(args, cfg, N, rank, root, IngestService):
     holder["svc"] = svc
 
     def drain():
+        # the service loop (IngestService.run): step + housekeeping (checkpoints on the log-time
+        # clock, stat lines, sink ticks), idle wait when nothing was read
         while sum(o[1] for o in svc.tailer.offsets()) < written[0] or svc._held is not None:
-            if svc.step() == 0:
+            n = svc.step()
+            svc._housekeeping()
+            if n == 0:
                 svc._idle(0.001)
 
     append(0, PRE)
