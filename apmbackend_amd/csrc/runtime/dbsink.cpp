@@ -31,6 +31,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <deque>
 #include <memory>
 #include <mutex>
@@ -86,13 +87,13 @@ bool write_all(int fd, const char* p, size_t n) {
 struct Writer {
   virtual ~Writer() = default;
   // returns "" on success, else the error text
-  virtual std::string write(int type, const std::string& table, const std::string& columns, const std::string& rows) = 0;
+  virtual std::string write(int type, const std::string& table, const std::string& columns, std::string_view rows) = 0;
   // Several consecutive flushes of one type, in order; returns how many were written (the rest
   // failed with `err`).  Default: one at a time.
   virtual size_t write_run(int type, const std::string& table, const std::string& columns,
-                           const std::vector<const std::string*>& rows, std::string& err) {
+                           const std::vector<std::string_view>& rows, std::string& err) {
     for (size_t i = 0; i < rows.size(); ++i) {
-      err = write(type, table, columns, *rows[i]);
+      err = write(type, table, columns, rows[i]);
       if (!err.empty()) return i;
     }
     return rows.size();
@@ -100,7 +101,7 @@ struct Writer {
 };
 
 struct NullWriter : Writer {
-  std::string write(int, const std::string&, const std::string&, const std::string&) override { return ""; }
+  std::string write(int, const std::string&, const std::string&, std::string_view) override { return ""; }
 };
 
 // Append-only COPY text files, one per table, rotated by size.
@@ -117,7 +118,7 @@ struct SpoolWriter : Writer {
     for (int f : fd)
       if (f >= 0) ::close(f);
   }
-  std::string write(int type, const std::string& table, const std::string& columns, const std::string& rows) override {
+  std::string write(int type, const std::string& table, const std::string& columns, std::string_view rows) override {
     const std::string path = dir + "/" + table + suffix + ".copy";
     if (fd[type] >= 0 && rotate && size[type] >= rotate) {
       ::close(fd[type]);
@@ -153,7 +154,7 @@ struct SpoolWriter : Writer {
   // A run of flushes: one writev per run (tmpfs serialises writers on the inode, so copying a
   // run on several threads measured slower: 174-191 ms vs 115 ms for 0.5 GB).
   size_t write_run(int type, const std::string& table, const std::string& columns,
-                   const std::vector<const std::string*>& rows, std::string& err) override {
+                   const std::vector<std::string_view>& rows, std::string& err) override {
     err = write(type, table, columns, std::string());  // rotation / open, no bytes
     if (!err.empty()) return 0;
     size_t done = 0;
@@ -162,9 +163,9 @@ struct SpoolWriter : Writer {
       int k = 0;
       size_t bytes = 0;
       for (size_t i = done; i < rows.size() && k < 64; ++i, ++k) {
-        iov[k].iov_base = const_cast<char*>(rows[i]->data());
-        iov[k].iov_len = rows[i]->size();
-        bytes += rows[i]->size();
+        iov[k].iov_base = const_cast<char*>(rows[i].data());
+        iov[k].iov_len = rows[i].size();
+        bytes += rows[i].size();
       }
       if (::lseek(fd[type], (off_t)size[type], SEEK_SET) < 0) { err = std::strerror(errno); return done; }
       size_t left = bytes;
@@ -239,7 +240,7 @@ struct PsqlWriter : Writer {
     out = pout[0];
     return "";
   }
-  std::string write(int, const std::string& table, const std::string& columns, const std::string& rows) override {
+  std::string write(int, const std::string& table, const std::string& columns, std::string_view rows) override {
     if (pid < 0) {
       std::string e = start();
       if (!e.empty()) return e;
@@ -350,8 +351,9 @@ class DbSink : public ByteSink {
   // flushed with the same limit / timer rules, written without encoding.  A rollover's fs rows
   // (tens of MB) are cut at the flush limit and copied into their flush jobs by several threads;
   // the resulting buffers and jobs are exactly those of the serial path.
-  int64_t consume_encoded(int type, std::string_view blob) {
-    if (blob.size() >= kParallelBytes && blob.size() < (1ull << 32)) return consume_encoded_parallel(type, blob);
+  int64_t consume_encoded(int type, std::string_view blob, std::shared_ptr<const void> hold = nullptr) {
+    if (blob.size() >= kParallelBytes && blob.size() < (1ull << 32))
+      return consume_encoded_parallel(type, blob, std::move(hold));
     const double now = mono_ms();
     std::lock_guard<std::mutex> lk(mu_);
     encoded_[type] = true;
@@ -390,15 +392,71 @@ class DbSink : public ByteSink {
     if (spare_.size() < kSpares && s.capacity() >= (64u << 10)) spare_.push_back(std::move(s));
   }
 
-  template <class F>
-  static void parallel_for(int n, const F& fn) {
+  // A few long-lived helper threads for the row scan of large COPY blobs (spawning 2 x 8 threads
+  // per hand-off cost ~0.5 ms of the output lane per batch).  One run at a time; the caller works too.
+  struct Helpers {
+    std::mutex run_mu, mu;
+    std::condition_variable cv, done_cv;
     std::vector<std::thread> th;
-    for (int i = 1; i < n; ++i) th.emplace_back([&fn, i] { fn(i); });
-    fn(0);
-    for (auto& t : th) t.join();
+    const std::function<void(int)>* fn = nullptr;
+    int n = 0, next = 0, finished = 0;
+    uint64_t gen = 0;
+    bool stop = false;
+    void take_and_run() {  // (mu held on entry and exit)
+      while (next < n) {
+        const int i = next++;
+        const std::function<void(int)>* f = fn;
+        mu.unlock();
+        (*f)(i);
+        mu.lock();
+        if (++finished == n) done_cv.notify_all();
+      }
+    }
+    void loop() {
+      std::unique_lock<std::mutex> lk(mu);
+      uint64_t seen = 0;
+      for (;;) {
+        cv.wait(lk, [&] { return stop || gen != seen; });
+        if (stop) return;
+        seen = gen;
+        take_and_run();
+      }
+    }
+    void run(int count, const std::function<void(int)>& f) {
+      std::lock_guard<std::mutex> rg(run_mu);
+      std::unique_lock<std::mutex> lk(mu);
+      if (th.empty())
+        for (int i = 0; i < 7; ++i) th.emplace_back([this] { loop(); });
+      fn = &f;
+      n = count;
+      next = 0;
+      finished = 0;
+      ++gen;
+      cv.notify_all();
+      take_and_run();
+      done_cv.wait(lk, [&] { return finished == n; });
+      fn = nullptr;
+    }
+    ~Helpers() {
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        stop = true;
+      }
+      cv.notify_all();
+      for (auto& t : th) t.join();
+    }
+  };
+  Helpers helpers_;
+  template <class F>
+  void parallel_for(int n, const F& fn) {
+    const std::function<void(int)> f = [&fn](int i) { fn(i); };
+    helpers_.run(n, f);
   }
 
-  int64_t consume_encoded_parallel(int type, std::string_view blob) {
+  // With `hold` (the caller's buffer stays valid until released) the middle flushes reference the
+  // blob instead of copying it: a firehose rollover hands ~80 MB of COPY rows per batch, and the
+  // copy into flush strings was most of the output lane's time.
+  int64_t consume_encoded_parallel(int type, std::string_view blob, std::shared_ptr<const void> hold = nullptr) {
     const double now = mono_ms();
     const char* d = blob.data();
     const size_t size = blob.size();
@@ -458,15 +516,22 @@ class DbSink : public ByteSink {
       auto j = std::make_shared<Job>();
       j->type = type;
       j->n = cut[k] - cut[k - 1];
-      j->encoded = take_spare_locked();  // recycled capacity: no page faults, no zero fill
+      if (hold) {
+        j->ext = std::string_view(d + off[k - 1], off[k] - off[k - 1]);
+        j->hold = hold;
+      } else {
+        j->encoded = take_spare_locked();  // recycled capacity: no page faults, no zero fill
+      }
       mid[k - 1] = std::move(j);
     }
     if (!mid.empty()) {
-      const int T = (int)std::min<size_t>((size_t)P, mid.size());
-      parallel_for(T, [&](int t) {
-        for (size_t k = (size_t)t; k < mid.size(); k += (size_t)T)
-          mid[k]->encoded.assign(d + off[k], off[k + 1] - off[k]);
-      });
+      if (!hold) {
+        const int T = (int)std::min<size_t>((size_t)P, mid.size());
+        parallel_for(T, [&](int t) {
+          for (size_t k = (size_t)t; k < mid.size(); k += (size_t)T)
+            mid[k]->encoded.assign(d + off[k], off[k + 1] - off[k]);
+        });
+      }
       for (auto& j : mid) {
         j->seq = next_seq_++;
         j->ready = true;
@@ -574,7 +639,12 @@ class DbSink : public ByteSink {
     int64_t n = 0;
     uint64_t seq = 0;
     std::string lines, encoded;
+    // zero-copy flush: COPY rows in the caller's (engine's pinned) buffer, kept alive and unchanged
+    // until `hold` is released (the engine reuses the buffer only then)
+    std::string_view ext;
+    std::shared_ptr<const void> hold;
     bool taken = false, ready = false;
+    std::string_view data() const { return ext.data() ? ext : std::string_view(encoded); }
   };
 
   // Appends `nrows` complete lines of type t; the buffer is flushed first when it is full.
@@ -653,8 +723,8 @@ class DbSink : public ByteSink {
           run.push_back(order[i]);
       }
       const int t = run[0]->type;
-      std::vector<const std::string*> rows;
-      for (auto& j : run) rows.push_back(&j->encoded);
+      std::vector<std::string_view> rows;
+      for (auto& j : run) rows.push_back(j->data());
       std::string err;
       const double t0 = mono_ms();
       const size_t ok = w.write_run(t, tables_[t], columns_[t], rows, err);
@@ -665,10 +735,12 @@ class DbSink : public ByteSink {
         for (size_t i = 0; i < ok; ++i) {
           Job& j = *run[i];
           rows_ += j.n;
-          bytes_ += (int64_t)j.encoded.size();
+          bytes_ += (int64_t)j.data().size();
           ++flushes_;
           give_spare_locked(std::move(j.encoded));
           give_spare_locked(std::move(j.lines));
+          j.ext = std::string_view();
+          j.hold.reset();
         }
         ms_ = std::max(ms_, lane_ms_[lane] += dt);  // wall time of the busiest lane
         if (ok < run.size()) {
@@ -685,7 +757,9 @@ class DbSink : public ByteSink {
           std::string back;
           int64_t n = 0;
           for (size_t i = retry_from; i < run.size(); ++i) {
-            back += encoded_[t] ? run[i]->encoded : run[i]->lines;
+            if (encoded_[t]) back.append(run[i]->data());
+            else back += run[i]->lines;
+            run[i]->hold.reset();
             n += run[i]->n;
           }
           if (!back.empty()) {
@@ -743,6 +817,10 @@ struct SinkRoute : ByteSink {
   SinkRoute(std::shared_ptr<DbSink> s, int t) : sink(std::move(s)), type(t) {}
   void write_bytes(int kind, const char* p, size_t n) override {
     if (type >= 0) sink->consume_encoded(type, std::string_view(p, n));
+    else sink->write_bytes(kind, p, n);
+  }
+  void write_bytes_held(int kind, const char* p, size_t n, std::shared_ptr<const void> hold) override {
+    if (type >= 0) sink->consume_encoded(type, std::string_view(p, n), std::move(hold));
     else sink->write_bytes(kind, p, n);
   }
 };

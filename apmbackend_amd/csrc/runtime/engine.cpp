@@ -484,6 +484,11 @@ Engine::~Engine() {
   hipHostFree(h_n_alerts_); hipEventDestroy(ev_alerts_); hipHostFree(h_tx_); hipHostFree(h_gid_);
   for (int k = 0; k < 2; ++k) {
     hipHostFree(h_release_gid_[k]);
+    {  // the sink's references to the staging buffers (its writers drain them; bounded wait)
+      FmtHolds& hs = *fmt_holds_;
+      std::unique_lock<std::mutex> lk(hs.mu);
+      if (!hs.cv.wait_for(lk, std::chrono::seconds(60), [&] { return hs.n[k] == 0; })) continue;
+    }
     if (h_fmt_out_[k]) hipHostFree(h_fmt_out_[k]);
     hipEventDestroy(ev_rel_[k]);
     hipEventDestroy(ev_fmt_[k]);
@@ -2493,6 +2498,32 @@ void Engine::emit_bytes(int kind, const char* p, size_t n) {
   blob_[kind].append(p, n);
 }
 
+void Engine::emit_bytes_held(int kind, const char* p, size_t n, int k) {
+  if (!n) return;
+  if (!byte_sink_[kind]) { emit_bytes(kind, p, n); return; }
+  drain_kind(kind);
+  std::shared_ptr<FmtHolds> hs = fmt_holds_;
+  {
+    std::lock_guard<std::mutex> g(hs->mu);
+    ++hs->n[k];
+  }
+  std::shared_ptr<const void> hold(p, [hs, k](const void*) {
+    {
+      std::lock_guard<std::mutex> g(hs->mu);
+      --hs->n[k];
+    }
+    hs->cv.notify_all();
+  });
+  byte_sink_[kind]->write_bytes_held(kind, p, n, std::move(hold));
+  sink_bytes_[kind] += n;
+}
+
+void Engine::wait_fmt_holds(int k) {
+  FmtHolds& hs = *fmt_holds_;
+  std::unique_lock<std::mutex> lk(hs.mu);
+  hs.cv.wait(lk, [&] { return hs.n[k] == 0; });
+}
+
 void Engine::format_rollover_text(int64_t edge_ts) {
   const int32_t n = n_series_;
   if (n == 0) return;
@@ -2553,6 +2584,7 @@ void Engine::format_rollover_text(int64_t edge_ts) {
   fmt_task_[k] = post_out([this, k, dst, st_cap]() {
     HIP_OK(hipEventSynchronize(ev_fmt_[k]));
     const size_t st_total = h_fmt_meta_[4 * k], fs_total = h_fmt_meta_[4 * k + 1];
+    wait_fmt_holds(k);  // the sink still writes from this buffer (zero-copy COPY rows)
     if (st_total + fs_total > h_fmt_cap_[k]) {
       if (h_fmt_out_[k]) HIP_OK(hipHostFree(h_fmt_out_[k]));
       h_fmt_cap_[k] = (st_total + fs_total) * 2 + (4 << 20);
@@ -2569,7 +2601,7 @@ void Engine::format_rollover_text(int64_t edge_ts) {
     }
     const double tl1 = now_ms();
     emit_bytes(OUT_ST, h, st_total);
-    emit_bytes(OUT_FS, h + st_total, fs_total);
+    emit_bytes_held(OUT_FS, h + st_total, fs_total, k);
     trace_event("lane st/fs D2H", tl0, tl1, 4);
     trace_event("lane st/fs emit", tl1, now_ms(), 4);
   });

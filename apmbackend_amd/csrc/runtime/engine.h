@@ -143,6 +143,12 @@ struct Chunk {
 struct ByteSink {
   virtual ~ByteSink() = default;
   virtual void write_bytes(int kind, const char* p, size_t n) = 0;
+  // [p, p + n) stays valid and unchanged until `hold` is released: a sink may keep references
+  // instead of copying (default: copy)
+  virtual void write_bytes_held(int kind, const char* p, size_t n, std::shared_ptr<const void> hold) {
+    (void)hold;
+    write_bytes(kind, p, n);
+  }
 };
 
 struct CheckpointInfo {
@@ -411,6 +417,15 @@ class Engine {
   void* regrow(void* old, size_t& cap, size_t need);
   void dfree(void* p);
   void emit_bytes(int kind, const char* p, size_t n);
+  // staging buffer k (st/fs 0, 1; fb 2, 3) is referenced by the sink until its holds are released
+  void emit_bytes_held(int kind, const char* p, size_t n, int k);
+  void wait_fmt_holds(int k);
+  struct FmtHolds {  // shared with the holds: a release after the engine is gone stays safe
+    std::mutex mu;
+    std::condition_variable cv;
+    int n[4] = {0, 0, 0, 0};  // st/fs staging 0, 1; fb staging 2, 3
+  };
+  std::shared_ptr<FmtHolds> fmt_holds_ = std::make_shared<FmtHolds>();
   void upload_series_tables(int32_t lo);
   void pack_moments_locked(double* d_dst, int32_t cap, hipStream_t stream, bool atomic_path = false);
   void fleet_pack_locked();
