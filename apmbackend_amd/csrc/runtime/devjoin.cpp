@@ -1074,8 +1074,13 @@ void DeviceJoin::save(BinWriter& w) {
   // links are physical slots of an arena of that size)
   const uint64_t lo = regions_.empty() ? arena_head_ : regions_.front().lo;
   std::vector<NeedEnt> ents((size_t)(arena_head_ - lo));
-  for (uint64_t v = lo; v < arena_head_; ++v)
-    HIP_OK(hipMemcpy(&ents[(size_t)(v - lo)], d_arena_ + (v & (cfg_.arena_cap - 1)), sizeof(NeedEnt), hipMemcpyDeviceToHost));
+  if (!ents.empty()) {  // the live range of the arena ring in (at most) two copies, not one per entry
+    const uint64_t cap = cfg_.arena_cap, first = lo & (cap - 1);
+    const uint64_t n1 = std::min<uint64_t>(ents.size(), cap - first);
+    HIP_OK(hipMemcpy(ents.data(), d_arena_ + first, (size_t)n1 * sizeof(NeedEnt), hipMemcpyDeviceToHost));
+    if (ents.size() > n1)
+      HIP_OK(hipMemcpy(ents.data() + n1, d_arena_, (size_t)(ents.size() - n1) * sizeof(NeedEnt), hipMemcpyDeviceToHost));
+  }
   // chain blocks reachable from the live state, renumbered 1..n in the file
   struct Blk { uint8_t b[CHAIN_BLK]; };
   std::vector<Blk> blocks;

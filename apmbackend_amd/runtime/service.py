@@ -389,6 +389,13 @@ class IngestService:
             return None
         if self._held is not None:
             return None  # a prefetched batch is in the engine: the next step processes it first
+        ci = getattr(self.eng, "checkpoint_info", None)
+        if ci is not None and ci().get("busy"):
+            # the previous checkpoint is still being written: try again at the next interval
+            # (draining the pipeline and the sink first only to be told "busy" cost a full drain
+            # per batch while a base checkpoint was written)
+            self.last_ckpt = self.clock()
+            return None
         os.makedirs(self.ckpt_dir, exist_ok=True)
         ck, tp = self._ckpt_paths()
         t0 = time.perf_counter()
