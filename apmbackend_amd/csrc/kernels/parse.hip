@@ -23,7 +23,7 @@ namespace apm {
 constexpr int NL_BLOCK = 256;
 constexpr int NL_TILE = NL_BLOCK * 16;     // bytes per block in the newline pass
 constexpr int PARSE_BLOCK = 256;           // lines per block in the parse pass
-constexpr int PARSE_LDS = 40 * 1024;       // staged bytes per block (4 blocks / CU)
+constexpr int PARSE_LDS = 32 * 1024;       // staged bytes per block (+ 8 KB token table: 4 blocks / CU)
 
 // --------------------------------------------------------------------------------- K1
 __global__ __launch_bounds__(NL_BLOCK) void k_nl_count(const uint8_t* __restrict__ bytes, uint64_t n,
@@ -117,6 +117,9 @@ __device__ __forceinline__ void tok_put(uint16_t (&arr)[NTOKSLOT], int k, uint16
 __device__ __forceinline__ void tok_put_if(uint16_t (&arr)[NTOKSLOT], bool on, int k, uint16_t v) {
   tok_put(arr, on ? k : -1, v);
 }
+// token index -> slot (0xF: a token the classifier never reads), one nibble per index 0..15
+constexpr uint64_t kTokSlotTab = 0xFF6F5F4FFFFF3210ULL;
+__device__ __forceinline__ int tok_slot_of(int k) { return k < 16 ? (int)((kTokSlotTab >> (4 * k)) & 0xFu) : 15; }
 
 // four characters packed little-endian, as they sit in a byte window p[i-3..i]
 template <int N>
@@ -220,11 +223,15 @@ __device__ __forceinline__ uint32_t find_chunk(const uint32_t* cb, uint32_t n_ch
 }
 
 __device__ __forceinline__ unsigned long long parse_line(const ParseArgs& a, const uint8_t* __restrict__ base,
-                                                         uint32_t o, uint32_t li, uint32_t ls, uint32_t le);
+                                                         uint32_t o, uint32_t li, uint32_t ls, uint32_t le,
+                                                         uint16_t* tp);
 
 // --------------------------------------------------------------------------------- K2
 __global__ __launch_bounds__(PARSE_BLOCK) void k_parse_lines(ParseArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[PARSE_LDS];
+  // token start/end positions of the tokens the classifier reads, slot-major (lane-adjacent
+  // entries): one LDS store per token boundary instead of a 7-way register select per byte
+  __shared__ uint16_t tok_lds[2 * NTOKSLOT][PARSE_BLOCK];
   const uint32_t n_lines = *a.n_lines_dev;
   const uint32_t first = blockIdx.x * PARSE_BLOCK;
   if (first >= n_lines) {
@@ -260,7 +267,8 @@ __global__ __launch_bounds__(PARSE_BLOCK) void k_parse_lines(ParseArgs a) {
     // Two inlined copies of the line parser, one per address space.  A single copy behind
     // `staged ? lds : global` sees a generic pointer and issues a flat load for every byte
     // (rocprofv3 before the split: 9M VMEM reads per run, ~150 LDS conflict cycles per LDS op).
-    wm = staged ? parse_line(a, lds, ls - a0, li, ls, le) : parse_line(a, a.bytes, ls, li, ls, le);
+    wm = staged ? parse_line(a, lds, ls - a0, li, ls, le, &tok_lds[0][threadIdx.x])
+                : parse_line(a, a.bytes, ls, li, ls, le, &tok_lds[0][threadIdx.x]);
   }
   // Watermark: one atomic per wave.  A per-lane atomicMax on the single watermark word put 64
   // same-address atomics per wave through one L2 atomic unit, serialising the whole grid.
@@ -272,8 +280,11 @@ __global__ __launch_bounds__(PARSE_BLOCK) void k_parse_lines(ParseArgs a) {
 }
 
 // One line: `base + o` is its first byte; `base` is 16-byte aligned (LDS stage or the batch).
+// tp: this lane's column of the block's token table (entry k at tp[k * PARSE_BLOCK]; starts in
+// rows 0..6, ends in rows 7..13)
 __device__ __forceinline__ unsigned long long parse_line(const ParseArgs& a, const uint8_t* __restrict__ base,
-                                                         uint32_t o, uint32_t li, uint32_t ls, uint32_t le) {
+                                                         uint32_t o, uint32_t li, uint32_t ls, uint32_t le,
+                                                         uint16_t* tp) {
   const uint8_t* __restrict__ p = base + o;
   int len = (int)(le - ls);
   if (len > 0 && p[len - 1] == '\r') --len;
@@ -306,10 +317,11 @@ __device__ __forceinline__ unsigned long long parse_line(const ParseArgs& a, con
   // ---- single pass: whitespace tokens 0..13, pattern tests, INFO occurrences
   // Start/end of the tokens the classifier reads (0-3, 9, 11, 13), kept in registers: an array
   // indexed by the lane-varying token count forced a per-write waterfall / scratch access
-  uint16_t ts_[NTOKSLOT], te_[NTOKSLOT];
+  auto TS = [&](int sl) -> uint16_t& { return tp[sl * PARSE_BLOCK]; };
+  auto TE = [&](int sl) -> uint16_t& { return tp[(NTOKSLOT + sl) * PARSE_BLOCK]; };
   int ntok = 0;
   bool in_tok = false;
-  if (len > 0 && is_ws(p[0])) { ts_[0] = 0; te_[0] = 0; ntok = 1; }  // split gives '' first
+  if (len > 0 && is_ws(p[0])) { TS(0) = 0; TE(0) = 0; ntok = 1; }  // split gives '' first
   int info1 = -1, info2 = -1;
   bool ejb_entry = false, ejb_exit = false, ct_start = false, ct_stop = false;
   bool baf = false, nonascii = false;
@@ -334,9 +346,15 @@ __device__ __forceinline__ unsigned long long parse_line(const ParseArgs& a, con
       const uint8_t c = (uint8_t)(vw[k >> 2] >> (8 * (k & 3)));
       nonascii |= act && c >= 0x80;
       const bool w = is_ws(c);
-      tok_put_if(ts_, act && !w && !in_tok, ntok, (uint16_t)i);
+      const bool tstart = act && !w && !in_tok;
       const bool tend = act && w && in_tok;
-      tok_put_if(te_, tend, ntok, (uint16_t)i);
+      if (tstart | tend) {
+        const int sl = tok_slot_of(ntok);
+        if (sl != 15) {
+          if (tstart) TS(sl) = (uint16_t)i;
+          else TE(sl) = (uint16_t)i;
+        }
+      }
       ntok += tend ? 1 : 0;
       in_tok = act ? !w : in_tok;
       const uint32_t nwin = (win >> 8) | ((uint32_t)c << 24);
@@ -395,8 +413,15 @@ __device__ __forceinline__ unsigned long long parse_line(const ParseArgs& a, con
       }
     }
   }
-  if (in_tok) { tok_put(te_, ntok, (uint16_t)len); ++ntok; }
-  else if (is_ws(p[len - 1]) && ntok < 16) { tok_put(ts_, ntok, (uint16_t)len); tok_put(te_, ntok, (uint16_t)len); ++ntok; }  // trailing ''
+  if (in_tok) {
+    const int sl = tok_slot_of(ntok);
+    if (sl != 15) TE(sl) = (uint16_t)len;
+    ++ntok;
+  } else if (is_ws(p[len - 1]) && ntok < 16) {  // trailing ''
+    const int sl = tok_slot_of(ntok);
+    if (sl != 15) { TS(sl) = (uint16_t)len; TE(sl) = (uint16_t)len; }
+    ++ntok;
+  }
   // line-anchored patterns
   if (p[0] == ']') m |= PM_EL_END;
   if (match_at(p, 0, len, "Audit Trail id")) {
@@ -417,7 +442,7 @@ __device__ __forceinline__ unsigned long long parse_line(const ParseArgs& a, con
 
   ev.ntok = (uint8_t)min(ntok, 15);
   auto tok = [&](int k, uint16_t& s, uint16_t& e) {
-    if (k < ntok && k < 16) { s = ts_[tok_slot(k)]; e = te_[tok_slot(k)]; }
+    if (k < ntok && k < 16) { s = TS(tok_slot(k)); e = TE(tok_slot(k)); }
   };
   tok(0, ev.t0s, ev.t0e);
   tok(1, ev.t1s, ev.t1e);
@@ -430,7 +455,7 @@ __device__ __forceinline__ unsigned long long parse_line(const ParseArgs& a, con
   if (ntok >= 3) {
     double t;
     bool strict;
-    if (parse_log_ts(p, ts_[tok_slot(1)], te_[tok_slot(1)], ts_[tok_slot(2)], te_[tok_slot(2)], a.tz, t, strict)) {
+    if (parse_log_ts(p, TS(tok_slot(1)), TE(tok_slot(1)), TS(tok_slot(2)), TE(tok_slot(2)), a.tz, t, strict)) {
       ev.ts = t;
       if (strict && t == t) {
         wm = (unsigned long long)((long long)t + (1LL << 62));
@@ -462,7 +487,7 @@ __device__ __forceinline__ unsigned long long parse_line(const ParseArgs& a, con
     } else if (kind == LK_EJB_EXIT) {
       tok(9, ev.tAs, ev.tAe);
       tok(11, ev.tBs, ev.tBe);
-      if (11 < ntok && !parse_int_tok(p, ts_[tok_slot(11)], te_[tok_slot(11)], ev.num)) m |= PM_HOST;
+      if (11 < ntok && !parse_int_tok(p, TS(tok_slot(11)), TE(tok_slot(11)), ev.num)) m |= PM_HOST;
     } else if (kind == LK_CT_ENTRY || kind == LK_CT_EXIT) {
       // line.split(/INFO/)[1].trim().split(/[\s]+/)
       const int s0 = info1 + 4;
