@@ -3137,7 +3137,9 @@ void Engine::fleet_pack_locked() {
   pack_edge_[slot] = metrics_.rollovers != last_edge_seen_ ? last_edge_ts_ : 0;
   last_edge_seen_ = metrics_.rollovers;
   const double t0 = now_ms();
-  pack_moments_locked(fleet_buf_[slot], fleet_cap_, stream_);
+  // APM_FLEET_ATOMIC=1: the per-series fp64 atomic scatter instead of the MFMA Gram pack (A/B)
+  static const bool atomic_pack = [] { const char* x = std::getenv("APM_FLEET_ATOMIC"); return x && x[0] == '1'; }();
+  pack_moments_locked(fleet_buf_[slot], fleet_cap_, stream_, atomic_pack);
   trace_event("fleet.pack", t0, now_ms(), 1);
   HIP_OK(hipEventRecord(pack_ev_[slot], stream_));
   ++fleet_packed_;

@@ -98,6 +98,8 @@ def main():
                          "window is full by then, so the history is drawn around the steady window stats "
                          "(drawn around a 2-bucket window it sat ~20 %% below the real p75/p95 and turned "
                          "the run into an alert storm after ~50 batches)")
+    ap.add_argument("--resync", default="mfma", choices=["mfma", "valu"],
+                    help="K10 rolling-sum resync on the matrix cores (v_mfma_f64_16x16x4) or on the VALU (A/B)")
     ap.add_argument("--audit-fraction", type=float, default=0.02,
                     help="share of requests logged with an audit trail (K5: the per-file state machine "
                          "runs in the host pre-pass)")
@@ -147,6 +149,7 @@ def main():
         "bucketCellCapacity": 16,
         "serverRollup": bool(args.jmx),
         "joinThreads": args.join_threads,
+        "resyncOnMatrixCores": args.resync == "mfma",
     })
     if args.path == "service":
         from apmbackend_amd.runtime import service_bench
