@@ -1422,6 +1422,24 @@ int apm_dj_write(DJFormatArgs* f, uint32_t n_stats, hipStream_t s) {
   return 0;
 }
 
+namespace {
+struct KeyLive {
+  __device__ bool operator()(const KeyState& k) const { return k.key != 0; }
+};
+}  // namespace
+
+size_t apm_dj_live_tmp_bytes(uint32_t cap) {
+  size_t b = 0;
+  HIP_OK(rocprim::select(nullptr, b, (const KeyState*)nullptr, (KeyState*)nullptr, (uint32_t*)nullptr, cap, KeyLive(),
+                         (hipStream_t)0));
+  return b;
+}
+
+void apm_dj_live_compact(const KeyState* table, uint32_t cap, KeyState* out, uint32_t* d_n, void* tmp,
+                         size_t tmp_bytes, hipStream_t s) {
+  HIP_OK(rocprim::select(tmp, tmp_bytes, table, out, d_n, cap, KeyLive(), s));
+}
+
 void apm_dj_rebuild(const KeyState* old, uint32_t old_cap, KeyState* fresh, uint32_t fresh_mask, const NeedEnt* arena,
                     uint32_t arena_cap, double now, JoinCounts* counts, unsigned long long* live, uint8_t* pool,
                     uint32_t* pool_ring, uint32_t pool_mask, hipStream_t s) {

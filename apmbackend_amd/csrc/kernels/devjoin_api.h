@@ -151,6 +151,11 @@ int apm_dj_write(apm::DJFormatArgs* f, uint32_t n_stats, hipStream_t s);
 void apm_dj_rebuild(const apm::KeyState* old, uint32_t old_cap, apm::KeyState* fresh, uint32_t fresh_mask,
                     const apm::NeedEnt* arena, uint32_t arena_cap, double now, apm::JoinCounts* counts,
                     unsigned long long* live, uint8_t* pool, uint32_t* pool_ring, uint32_t pool_mask, hipStream_t s);
+// Checkpoint: the occupied slots (key != 0) of the key table, in slot order, into `out`;
+// *d_n = their count.  tmp: apm_dj_live_tmp_bytes(cap) bytes.
+size_t apm_dj_live_tmp_bytes(uint32_t cap);
+void apm_dj_live_compact(const apm::KeyState* table, uint32_t cap, apm::KeyState* out, uint32_t* d_n, void* tmp,
+                         size_t tmp_bytes, hipStream_t s);
 // chain-block pool: ring = identity (all `n` blocks free), counters head = 0, tail = ptail = n
 void apm_dj_pool_init(uint32_t* ring, uint32_t n, apm::JoinCounts* counts, hipStream_t s);
 // pool growth: the free entries of the old ring, then blocks [old_n, new_n), into `fresh_ring`

@@ -69,8 +69,21 @@ void h2d_rows(BinReader& rd, void* dev, size_t pitch, size_t width, size_t rows,
   }
 }
 
+// A device array as BinWriter::vec writes it.  With a pinned bounce buffer the D2H runs at
+// full link speed (a pageable destination is staged by the runtime in small pieces).
 template <class T>
-void d2h_vec(BinWriter& w, const T* dev, size_t n, hipStream_t st) {
+void d2h_vec(BinWriter& w, const T* dev, size_t n, hipStream_t st, void* bounce = nullptr) {
+  if (bounce) {
+    w.pod<uint64_t>(n);
+    const size_t per = kBounce / sizeof(T);
+    for (size_t i = 0; i < n; i += per) {
+      const size_t c = std::min(per, n - i);
+      HIP_OK(hipMemcpyAsync(bounce, dev + i, c * sizeof(T), hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      w.raw(bounce, c * sizeof(T));
+    }
+    return;
+  }
   std::vector<T> h(n);
   if (n) {
     HIP_OK(hipMemcpyAsync(h.data(), dev, n * sizeof(T), hipMemcpyDeviceToHost, st));
@@ -373,6 +386,13 @@ void Engine::write_small_sections(BinWriter& w) {
   w.pod(next_gid_); w.pod(line_block_seq_);
   w.end();
 
+  double tt = now_ms();
+  auto mark = [&](const char* name) {  // per-section spans of the ingest stall (trace)
+    const double t = now_ms();
+    trace_event(name, tt, t, 0);
+    tt = t;
+  };
+  mark("ck.host");
   w.begin(SEC_JOIN);
   w.pod<uint8_t>(dev() ? 1 : 0);
   if (dev()) {
@@ -384,47 +404,65 @@ void Engine::write_small_sections(BinWriter& w) {
   }
   w.end();
 
+  mark("ck.join");
   w.begin(SEC_PARSE);
-  d2h_vec(w, d_file_open_, 1 << 16, stream_);
+  d2h_vec(w, d_file_open_, 1 << 16, stream_, bounce);
   w.end();
 
   w.begin(SEC_BUCKETS);
-  d2h_vec(w, d_active_, (size_t)n, stream_);
+  d2h_vec(w, d_active_, (size_t)n, stream_, bounce);
   {
     std::vector<int32_t> spill_n(NSLOT);
     HIP_OK(hipMemcpy(spill_n.data(), d_spill_n_, NSLOT * 4, hipMemcpyDeviceToHost));
-    std::vector<int32_t> counts(n), cells((size_t)n * cfg_.cell_cap);
+    std::vector<int32_t> counts(n), packed;
+    const int32_t cap = cfg_.cell_cap;
+    const size_t per = std::max<size_t>(1, kBounce / ((size_t)cap * 4));  // series per bounce fill
     for (int slot = 0; slot < NSLOT; ++slot) {
       if (slot_bucket_[slot] == NO_BUCKET) continue;
       w.pod<int32_t>(slot);
-      HIP_OK(hipMemcpy(counts.data(), d_counts_cells_ + (size_t)slot * S, (size_t)n * 4, hipMemcpyDeviceToHost));
-      HIP_OK(hipMemcpy(cells.data(), d_cells_ + (size_t)slot * S * cfg_.cell_cap, (size_t)n * cfg_.cell_cap * 4,
-                       hipMemcpyDeviceToHost));
+      HIP_OK(hipMemcpyAsync(bounce, d_counts_cells_ + (size_t)slot * S, (size_t)n * 4, hipMemcpyDeviceToHost, stream_));
+      HIP_OK(hipStreamSynchronize(stream_));
+      std::memcpy(counts.data(), bounce, (size_t)n * 4);
       w.vec(counts);
-      std::vector<int32_t> packed;  // only the occupied cells
-      for (int32_t s = 0; s < n; ++s)
-        for (int32_t k = 0; k < std::min(counts[s], cfg_.cell_cap); ++k) packed.push_back(cells[(size_t)s * cfg_.cell_cap + k]);
+      size_t total = 0;
+      for (int32_t s = 0; s < n; ++s) total += (size_t)std::min(counts[s], cap);
+      packed.resize(total);  // only the occupied cells
+      size_t o = 0;
+      for (int32_t s0 = 0; s0 < n; s0 += (int32_t)per) {
+        const int32_t s1 = std::min<int32_t>(n, s0 + (int32_t)per);
+        HIP_OK(hipMemcpyAsync(bounce, d_cells_ + ((size_t)slot * S + s0) * cap, (size_t)(s1 - s0) * cap * 4,
+                              hipMemcpyDeviceToHost, stream_));
+        HIP_OK(hipStreamSynchronize(stream_));
+        const int32_t* c = (const int32_t*)bounce;
+        for (int32_t s = s0; s < s1; ++s) {
+          const int32_t k = std::min(counts[s], cap);
+          std::memcpy(packed.data() + o, c + (size_t)(s - s0) * cap, (size_t)k * 4);
+          o += (size_t)k;
+        }
+      }
       w.vec(packed);
       const int32_t ns = std::min(spill_n[slot], cfg_.spill_cap);
       w.pod(spill_n[slot]);
-      d2h_vec(w, d_spill_series_ + (size_t)slot * cfg_.spill_cap, (size_t)ns, stream_);
-      d2h_vec(w, d_spill_val_ + (size_t)slot * cfg_.spill_cap, (size_t)ns, stream_);
+      d2h_vec(w, d_spill_series_ + (size_t)slot * cfg_.spill_cap, (size_t)ns, stream_, bounce);
+      d2h_vec(w, d_spill_val_ + (size_t)slot * cfg_.spill_cap, (size_t)ns, stream_, bounce);
     }
     w.pod<int32_t>(-1);
   }
-  d2h_vec(w, d_nan_until_, (size_t)n, stream_);
+  d2h_vec(w, d_nan_until_, (size_t)n, stream_, bounce);
   w.end();
 
+  mark("ck.buckets");
   w.begin(SEC_ZSCORE);
   for (int l = 0; l < cfg_.n_lags; ++l) {
     LagState& L = lag_[l];
-    d2h_vec(w, L.len, (size_t)n, stream_);
-    d2h_vec(w, L.counter, (size_t)n, stream_);
+    d2h_vec(w, L.len, (size_t)n, stream_, bounce);
+    d2h_vec(w, L.counter, (size_t)n, stream_, bounce);
     for (double* a : {L.sum, L.comp, L.sumsq, L.sqcomp}) d2h_rows(w, a, (size_t)S * 8, (size_t)n * 8, NSTAT, bounce, stream_);
     d2h_rows(w, L.cnt, (size_t)S * 4, (size_t)n * 4, NSTAT, bounce, stream_);
   }
   w.end();
 
+  mark("ck.zscore");
   w.begin(SEC_POOL);
   w.pod(pool_off_); w.pod(pool_n_); w.pod(tail_n_);
   {
@@ -434,9 +472,9 @@ void Engine::write_small_sections(BinWriter& w) {
     w.vec(bc);
     w.vec(ee);
   }
-  d2h_vec(w, d_pool_end_[pool_cur_] + pool_off_, (size_t)pool_n_, stream_);
-  d2h_vec(w, d_pool_gid_[pool_cur_] + pool_off_, (size_t)pool_n_, stream_);
-  d2h_vec(w, d_tail_end_, (size_t)tail_n_, stream_);
+  d2h_vec(w, d_pool_end_[pool_cur_] + pool_off_, (size_t)pool_n_, stream_, bounce);
+  d2h_vec(w, d_pool_gid_[pool_cur_] + pool_off_, (size_t)pool_n_, stream_, bounce);
+  d2h_vec(w, d_tail_end_, (size_t)tail_n_, stream_, bounce);
   if (dev()) {
     // pending lines live in the HBM text ring: saved as one blob (pool lines, then tail lines)
     // with each gid rebased to its offset in the blob
@@ -459,6 +497,7 @@ void Engine::write_small_sections(BinWriter& w) {
   }
   w.end();
 
+  mark("ck.pool");
   w.begin(SEC_ALERTS);
   {
     const auto cool = cooldown_entries();
@@ -814,6 +853,7 @@ int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& e
   }
   const double t0 = now_ms();
   checkpoint_quiesce("checkpoint_async");
+  trace_event("ck.quiesce", t0, now_ms(), 0);
   auto job = std::make_shared<CkJob>();
   const bool base = force_base || ck_all_dirty_ || ck_chain_.empty() || ck_prefix_ != prefix ||
                     (int)ck_chain_.size() > kMaxChain;

@@ -1063,12 +1063,25 @@ void DeviceJoin::save(BinWriter& w) {
   HIP_OK(hipMemcpy(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost));
   w.pod(*h_counts_);
   for (uint64_t v : {events_, tx_, tx_db_, audit_errors_, host_pm_, host_invalid_acct_, host_events_}) w.pod(v);
-  // key table: live (non-empty) slots only
+  // key table: live (non-empty) slots only, selected on the device -- the whole table is
+  // 2M x 128 B and its D2H copy was most of a base checkpoint's ingest stall
   std::vector<KeyState> live;
   {
-    std::vector<KeyState> tab(table_cap_);
-    HIP_OK(hipMemcpy(tab.data(), d_table_, (size_t)table_cap_ * sizeof(KeyState), hipMemcpyDeviceToHost));
-    for (const KeyState& k : tab) if (k.key) live.push_back(k);
+    const size_t tb = apm_dj_live_tmp_bytes(table_cap_);
+    KeyState* out = d_table_spare_;
+    void* tmp = nullptr;
+    uint32_t* d_n = nullptr;
+    if (!out) HIP_OK(hipMalloc((void**)&out, (size_t)table_cap_ * sizeof(KeyState)));
+    HIP_OK(hipMalloc(&tmp, tb + 64));
+    d_n = (uint32_t*)((char*)tmp + tb);
+    apm_dj_live_compact(d_table_, table_cap_, out, d_n, tmp, tb, st);
+    uint32_t n_live = 0;
+    HIP_OK(hipMemcpyAsync(&n_live, d_n, 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    live.resize(n_live);
+    if (n_live) HIP_OK(hipMemcpy(live.data(), out, (size_t)n_live * sizeof(KeyState), hipMemcpyDeviceToHost));
+    HIP_OK(hipFree(tmp));
+    if (out != d_table_spare_) HIP_OK(hipFree(out));
   }
   // needNumRecordCache regions + their arena entries (arena capacity first: the table's `need`
   // links are physical slots of an arena of that size)

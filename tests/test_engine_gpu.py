@@ -52,7 +52,9 @@ def synth_batches(seed=1, duration=1200, servers=2):
     return lines, with_watermarks(batches(lines, cfg.start_ms, 5.0), UTC)
 
 
-def test_parse_kernel_matches_model():
+@pytest.mark.parametrize("mode", ["tile", "line"])
+def test_parse_kernel_matches_model(mode, monkeypatch):
+    monkeypatch.setenv("APM_PARSE", mode)
     lines, bl = synth_batches(3, duration=120)
     C = small_cfg()
     eng = APMEngine(C, keep_text=False)
@@ -722,3 +724,88 @@ def test_fatal_error_leaves_a_state_dump(tmp_path):
     assert d["batches"] == m["batches"] and d["lines"] == m["lines"] and d["n_series"] == eng.eng.n_series()
     assert d["rollovers"] == m["rollovers"] > 0 and d["join_table_slots"] >= 1024
     assert len(d["slot_bucket"]) == 40 and d["tx_ring_head"] > 0
+
+
+def _edge_corpus(seed, n=4000):
+    """Realistic lines with tokenizer edge cases mixed in: leading / trailing whitespace (space,
+    tab, VT, FF), CR and CR CR before LF, whitespace-only and empty lines, non-ASCII bytes,
+    repeated INFO, '<' tags at the line end, 20+ tokens, and 1-6 KB lines (they cross the
+    parse kernel's per-block stage boundaries)."""
+    import random
+    rng = random.Random(seed)
+    ts = "2020-01-07 10:00:{:02d},{:03d}"
+    server, app, soap = [], [], []
+    for i in range(n):
+        lid = f"id{rng.randint(0, 50):04d}"
+        t = ts.format(rng.randint(0, 59), rng.randint(0, 999))
+        pre = "[baf][x:y:1234] " if rng.random() < 0.3 else ""
+        svc = f"Provider[p{rng.randint(0, 3)}]"
+        r = rng.random()
+        if r < 0.2:
+            line, dst = f"[{lid}] {t} INFO  [CommonTiming] The EJB call started for bean Delegation method: ejb{i % 5}", server
+        elif r < 0.35:
+            line, dst = f"[{lid}] {t} INFO  [CommonTiming] Total time taken for: ejb{i % 5} - {rng.randint(1, 900)} ms", server
+        elif r < 0.5:
+            line, dst = f"[{lid}] {t} {pre}INFO  CommonTiming::Start: {svc} begin", app
+        elif r < 0.65:
+            line, dst = f"[{lid}] {t} {pre}INFO  CommonTiming::Stop: {svc} - total time {rng.randint(0, 500)} ms", app
+        elif r < 0.7:
+            line, dst = f"[{lid}] {t} [baf][x:1] INFO  auditTrailId=A{i:07d}", app
+        elif r < 0.73:
+            line, dst = rng.choice(["Audit Trail id : A1", "Audit Trail id   :A2", "]", "<stopWatchList>",
+                                    "</stopWatchList>", f"  <name>{svc}</name>",
+                                    "  <startTime>2020-01-07T10:00:00.000Z</startTime>",
+                                    "  <stopTime>2020-01-07T10:00:00.010Z</stopTime>",
+                                    f"[{lid}] {t} INFO  com.acme.Audit: RequestTrace [stopWatchList="]), app
+        elif r < 0.8:
+            line, dst = rng.choice([f"=== jbossId={lid} IO=I", f"=== jbossId={lid} IO=O",
+                                    "      <key>AccountNumber</key>", "      <value>123</value>",
+                                    "      <ACCOUNTNUMBER>99</ACCOUNTNUMBER>", "<acc", "x <key"]), soap
+        else:
+            line = f"[{lid}] {t} DEBUG noise " + " ".join(f"w{k}" for k in range(rng.randint(0, 24)))
+            dst = rng.choice([server, app, soap])
+        m = rng.random()
+        if m < 0.08:
+            line = rng.choice([" ", "\t", "  ", "\x0b", "\x0c "]) + line
+        elif m < 0.16:
+            line = line + rng.choice([" ", "\t", "\r", "  \r", "\r\r", " x", "\x0c"])
+        elif m < 0.2:
+            line = line.replace(" ", rng.choice(["\t", "  ", " \t "]), rng.randint(1, 4))
+        elif m < 0.23:
+            line = rng.choice(["", " ", "\t\t", "\r", "   \r"])
+        elif m < 0.26:
+            line = line[: len(line) // 2] + "é€" + line[len(line) // 2:]
+        elif m < 0.29:
+            line = line + " INFO again INFO" + rng.choice(["", " <", " <na", " <name>", " <sto"])
+        elif m < 0.31:
+            line = line + " pad" * rng.randint(250, 1500)
+        elif m < 0.32:
+            line = "x" * rng.randint(1000, 6000) + " " + line
+        dst.append(line)
+    return {"/logs/jvm00/server.log": server, "/logs/jvm00/app.log": app, "/logs/jvm00/soap_io.log": soap}
+
+
+@pytest.mark.parametrize("mode", ["tile", "line"])
+@pytest.mark.parametrize("seed", [3, 4])
+def test_parse_kernel_edge_lines_match_model(seed, mode, monkeypatch):
+    """K1/K2 on lines built to hit the tokenizer's and the pattern scan's corner cases (see
+    _edge_corpus) == the Python model, field for field; both K2 kernels (cooperative tiles, and
+    APM_PARSE=line: one lane per line)."""
+    monkeypatch.setenv("APM_PARSE", mode)
+    files = _edge_corpus(seed)
+    C = small_cfg()
+    eng = APMEngine(C, keep_text=False)
+    raw = [(fp, ("\n".join(ls) + "\n").encode("utf-8")) for fp, ls in files.items()]
+    eng.process(raw, START + 60_000)
+    got = np.frombuffer(eng.eng.last_events(), dtype=EVENT_DTYPE)
+    bch = [(KINDS[file_kind(fp)], b) for fp, b in raw]
+    cf = [eng.file_ids[fp] for fp, _ in raw]
+    want, _, _, _ = parse_batch(bch, UTC, {}, cf)
+    assert len(got) == len(want)
+    for name in EVENT_DTYPE.names:
+        a, b = got[name], want[name]
+        if a.dtype.kind == "f":
+            assert np.array_equal(a, b, equal_nan=True), name
+        else:
+            bad = np.flatnonzero(a != b)
+            assert bad.size == 0, (name, bad[:5], a[bad[:5]], b[bad[:5]])
