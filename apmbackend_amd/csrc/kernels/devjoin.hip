@@ -44,12 +44,230 @@ using OpSortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::d
 
 __device__ __forceinline__ uint32_t grid_n(uint32_t n) { return (n + TB - 1) / TB; }
 
+// ------------------------------------------------------------------------ audit fields (K5)
+// parseAppLine's string work (stream_parse_transactions.js:578-731) on one line, for ASCII lines
+// with plain numbers and ISO dates that carry their offset; anything else -> the host (HOP_AUD).
+constexpr uint32_t AUD_NIL = 0xffffffffu;
+
+__device__ __forceinline__ bool ws_ascii(uint8_t c) { return c == ' ' || (c >= 9 && c <= 13); }
+
+__device__ __forceinline__ void trim_ascii(const uint8_t* p, int& a, int& b) {
+  while (a < b && ws_ascii(p[a])) ++a;
+  while (b > a && ws_ascii(p[b - 1])) --b;
+}
+
+// k-th token of line.split(/[\s]+/) (a leading '' when the line starts with whitespace)
+__device__ void split_tok(const uint8_t* p, int len, int k, int& s, int& e) {
+  int idx = 0, ts = 0;
+  bool in_ws = false;
+  for (int i = 0; i < len; ++i) {
+    if (ws_ascii(p[i])) {
+      if (!in_ws) {
+        if (idx == k) { s = ts; e = i; return; }
+        ++idx;
+        in_ws = true;
+      }
+      ts = i + 1;
+    } else {
+      in_ws = false;
+    }
+  }
+  if (idx == k) { s = ts; e = len; return; }
+  s = e = -1;  // no such token
+}
+
+// parseInt of [a, b) with every '[' / ']' removed (whitespace-free); false: the host decides
+__device__ bool parse_int_nobr(const uint8_t* p, int a, int b, double& out) {
+  uint8_t buf[24];
+  int n = 0;
+  for (int i = a; i < b && n < 21; ++i)
+    if (p[i] != '[' && p[i] != ']') buf[n++] = p[i];
+  return simple_parse_int(buf, n, out);
+}
+
+// convertStringDateToMs of [a, b): 1 = '' (empty input), 0 = `out` set (NaN if invalid),
+// -1 = the host decides (non-ISO forms, ISO without an offset: local time needs the zone table)
+__device__ int aud_date(const uint8_t* p, int a, int b, double& out) {
+  if (a >= b) return 1;
+  int tpos = -1;
+  for (int i = a; i < b; ++i) if (p[i] == 'T') { tpos = i; break; }
+  bool iso = false;
+  if (tpos >= 0) for (int i = tpos + 1; i < b; ++i) if (p[i] == '-') { iso = true; break; }
+  if (!iso) return -1;
+  trim_ascii(p, a, b);
+  const int n = b - a;
+  const uint8_t* t = p + a;
+  auto dig = [&](int i, int k, int64_t& v) {
+    if (i + k > n) return false;
+    v = 0;
+    for (int j = 0; j < k; ++j) {
+      const uint8_t c = t[i + j];
+      if (c < '0' || c > '9') return false;
+      v = v * 10 + (c - '0');
+    }
+    return true;
+  };
+  out = apm_nan();
+  int64_t y, mo, d, h, mi, sec = 0, ms = 0;
+  if (!dig(0, 4, y) || n < 16 || t[4] != '-' || !dig(5, 2, mo) || t[7] != '-' || !dig(8, 2, d) || t[10] != 'T' ||
+      !dig(11, 2, h) || t[13] != ':' || !dig(14, 2, mi))
+    return 0;
+  int i = 16;
+  if (i < n && t[i] == ':') {
+    if (!dig(i + 1, 2, sec)) return 0;
+    i += 3;
+    if (i < n && t[i] == '.') {
+      ++i;
+      int j = i, nd = 0;
+      int64_t frac = 0;
+      while (j < n && t[j] >= '0' && t[j] <= '9') { if (nd < 3) { frac = frac * 10 + (t[j] - '0'); ++nd; } ++j; }
+      if (j == i) return 0;
+      while (nd < 3) { frac *= 10; ++nd; }
+      ms = frac;
+      i = j;
+    }
+  }
+  if (mo < 1 || mo > 12 || d < 1 || d > 31 || h > 24 || mi > 59 || sec > 59) return 0;
+  const int64_t local = make_date_ms(y, mo - 1, d, h, mi, sec, ms);
+  if (i == n) return -1;
+  if (t[i] == 'Z' && i + 1 == n) { out = (double)local; return 0; }
+  if (t[i] == '+' || t[i] == '-') {
+    const int sg = t[i] == '-' ? -1 : 1;
+    int64_t oh, om;
+    if (!dig(i + 1, 2, oh)) return 0;
+    int k = i + 3;
+    if (k < n && t[k] == ':') ++k;
+    if (!dig(k, 2, om) || k + 2 != n) return 0;
+    out = (double)(local - sg * (oh * 60 + om) * 60000);
+  }
+  return 0;
+}
+
+// line.replace(/<\/.*/,'').replace(/.*>/,'') -> [s, e)
+__device__ __forceinline__ void xml_inner_dev(const uint8_t* p, int len, int& s, int& e) {
+  e = len;
+  for (int i = 0; i + 1 < len; ++i) if (p[i] == '<' && p[i + 1] == '/') { e = i; break; }
+  s = 0;
+  for (int i = 0; i < e; ++i) if (p[i] == '>') s = i + 1;
+}
+
+__device__ bool icontains_provider(const uint8_t* p, int a, int b) {
+  const char* pat = "provider[";
+  for (int i = a; i + 9 <= b; ++i) {
+    int k = 0;
+    for (; k < 9; ++k) {
+      uint8_t c = p[i + k];
+      if (c >= 'A' && c <= 'Z') c = (uint8_t)(c + 32);
+      if (c != (uint8_t)pat[k]) break;
+    }
+    if (k == 9) return true;
+  }
+  return false;
+}
+
+// The AudF of an LK_APP event (batch-absolute refs); false when the host must derive it.
+__device__ bool aud_fields(const Event& e, const uint8_t* __restrict__ bytes, int32_t file, AudF& f) {
+  const uint8_t* p = bytes + e.off;
+  const int len = (int)e.len;
+  f.h_item = 0; f.el = apm_nan(); f.h_sw = 0; f.ts = apm_nan();
+  f.ref = 0; f.len = 0; f.flags = 0; f.pad = 0; f.pad2[0] = f.pad2[1] = 0;
+  for (int i = 0; i < len; ++i) if (p[i] >= 0x80) return false;
+  const uint32_t m = e.mask;
+  if (m & PM_AUTR_MAP) {
+    // logId = ws[0] without brackets; auditTrailId = ws[5].split('=')[1]; alt = the BAF account
+    int s0, e0;
+    split_tok(p, len, 0, s0, e0);
+    if (s0 < 0) { s0 = e0 = 0; }
+    if (s0 < e0 && p[s0] == '[') ++s0;
+    if (e0 > s0 && p[e0 - 1] == ']') --e0;
+    for (int i = s0; i < e0; ++i) if (p[i] == '[' || p[i] == ']') return false;  // inner brackets
+    f.ref = e.off + (uint32_t)s0;
+    f.len = (uint16_t)(e0 - s0);
+    f.h_sw = hash_bytes(p + s0, (size_t)(e0 - s0));
+    int s5, e5;
+    split_tok(p, len, 5, s5, e5);
+    uint64_t ah;
+    int q = -1;
+    if (s5 >= 0) for (int i = s5; i < e5; ++i) if (p[i] == '=') { q = i + 1; break; }
+    if (q < 0) {
+      ah = hash_bytes("undefined", 9);
+    } else {
+      int r = e5;
+      for (int i = q; i < e5; ++i) if (p[i] == '=') { r = i; break; }
+      ah = hash_bytes(p + q, (size_t)(r - q));
+    }
+    f.h_item = aud_key(ah, file);
+    if (m & PM_BAF) {
+      int s3, e3;
+      split_tok(p, len, 3, s3, e3);
+      if (s3 >= 0 && e3 > s3) {
+        uint8_t acct[64];
+        const int n = baf_account(p, s3, e3, acct);
+        if (n < 0) return false;
+        if (n > 0) {
+          double v;
+          if (!simple_parse_int(acct, n, v)) return false;
+          f.el = v;
+          f.flags |= AF_ACCT;
+          if (all_digits(acct, n)) f.flags |= AF_ACCT_VALID;
+        }
+      }
+    }
+    return true;
+  }
+  if (m & PM_AUTR_HDR) {  // line.split(':')[1].trim()
+    int c1 = -1, c2 = len;
+    for (int i = 0; i < len; ++i) if (p[i] == ':') { c1 = i; break; }
+    if (c1 < 0) return false;
+    for (int i = c1 + 1; i < len; ++i) if (p[i] == ':') { c2 = i; break; }
+    int a = c1 + 1, b = c2;
+    trim_ascii(p, a, b);
+    f.h_item = aud_key(hash_bytes(p + a, (size_t)(b - a)), file);
+    return true;
+  }
+  // item role (a line inside the elapsed section): service = split(':')[0].trim(),
+  // elapsed = split(':')[1].split(/\s+/)[0] without brackets
+  {
+    int c1 = -1, c2 = len;
+    for (int i = 0; i < len; ++i) if (p[i] == ':') { c1 = i; break; }
+    int a = 0, b = c1 >= 0 ? c1 : len;
+    trim_ascii(p, a, b);
+    f.h_item = hash_bytes(p + a, (size_t)(b - a));
+    if (c1 >= 0) {
+      for (int i = c1 + 1; i < len; ++i) if (p[i] == ':') { c2 = i; break; }
+      int t = c1 + 1;
+      while (t < c2 && !ws_ascii(p[t])) ++t;
+      if (!parse_int_nobr(p, c1 + 1, t, f.el)) return false;
+    }
+  }
+  if (m & PM_SW_NAME) {
+    int s, t;
+    xml_inner_dev(p, len, s, t);
+    f.ref = e.off + (uint32_t)s;
+    f.len = (uint16_t)(t - s);
+    f.h_sw = hash_bytes(p + s, (size_t)(t - s));
+    if (!icontains_provider(p, s, t)) f.flags |= AF_TO_DB;
+  } else if (m & (PM_SW_STARTTS | PM_SW_STOPTS)) {
+    int s, t;
+    xml_inner_dev(p, len, s, t);
+    const int r = aud_date(p, s, t, f.ts);
+    if (r < 0) return false;
+    if (r == 1) f.flags |= AF_TS_EMPTY;
+  }
+  return true;
+}
+
 // ------------------------------------------------------------------------ host-event selection
-// Events the GPU does not resolve alone: audit lines (K5, host state machine), lines the parser
-// deferred (non-ASCII, exotic numbers / timestamps), logIds with inner brackets, and account
-// strings parseInt cannot decide in 64 bits.
+// Events the GPU does not resolve alone: lines the parser deferred (non-ASCII, exotic numbers /
+// timestamps), logIds with inner brackets, account strings parseInt cannot decide in 64 bits,
+// and audit lines whose fields aud_fields cannot extract (the host sends those as HOP_AUD).
 __device__ bool needs_host(const Event& e, const uint8_t* __restrict__ bytes) {
-  if (e.kind == LK_APP || (e.mask & PM_HOST)) return true;
+  if (e.kind == LK_APP) {
+    if (e.mask & PM_HOST) return true;
+    AudF f;
+    return !aud_fields(e, bytes, 0, f);
+  }
+  if (e.mask & PM_HOST) return true;
   const uint8_t* p = bytes + e.off;
   if (e.kind >= LK_EJB_ENTRY && e.kind <= LK_CT_EXIT) {
     if (!(e.mask & PM_KEYS) || e.ntok < 3) return true;
@@ -79,23 +297,50 @@ __device__ bool needs_host(const Event& e, const uint8_t* __restrict__ bytes) {
   return false;
 }
 
+enum : uint8_t { SEL_HOST = 1, SEL_MH = 2, SEL_WALK = 4 };
+
+struct SelPlus {
+  __device__ __host__ SelCount operator()(const SelCount& a, const SelCount& b) const {
+    return SelCount{a.host + b.host, a.mh + b.mh, a.walk + b.walk, a.aud_bytes + b.aud_bytes};
+  }
+};
+
 __global__ void k_host_flags(const Event* __restrict__ ev, const uint32_t* __restrict__ n_ev_dev,
-                             const uint8_t* __restrict__ bytes, uint8_t* __restrict__ flag, uint32_t cap) {
+                             const uint8_t* __restrict__ bytes, uint8_t* __restrict__ flag, SelCount* __restrict__ val,
+                             uint32_t cap) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cap) return;
   const uint32_t n = *n_ev_dev;
-  flag[i] = (i < n && needs_host(ev[i], bytes)) ? 1 : 0;
+  uint8_t fl = 0;
+  uint32_t ab = 0;
+  if (i < n) {
+    const Event e = ev[i];
+    if (needs_host(e, bytes)) fl |= SEL_HOST;
+    if (e.kind == LK_APP) {
+      if (e.mask & PM_AUTR_MAP) fl |= SEL_MH;
+      else fl |= SEL_WALK | ((e.mask & PM_AUTR_HDR) ? SEL_MH : 0);
+      if (e.mask & (PM_AUTR_MAP | PM_SW_NAME)) ab = e.len;
+    }
+  }
+  flag[i] = fl;
+  val[i] = SelCount{(uint32_t)(fl & SEL_HOST), (fl & SEL_MH) ? 1u : 0u, (fl & SEL_WALK) ? 1u : 0u, ab};
 }
 
 __global__ void k_host_scatter(const Event* __restrict__ ev, const uint8_t* __restrict__ flag,
-                               const uint32_t* __restrict__ pos, uint32_t cap, const uint32_t* __restrict__ n_ev_dev,
-                               Event* __restrict__ out, uint32_t* __restrict__ out_idx, uint32_t* __restrict__ n_host) {
+                               const SelCount* __restrict__ val, const SelCount* __restrict__ pos, uint32_t cap,
+                               const uint32_t* __restrict__ n_ev_dev, Event* __restrict__ out,
+                               uint32_t* __restrict__ out_idx, uint32_t* __restrict__ mh_idx,
+                               uint32_t* __restrict__ walk_idx, SelCount* __restrict__ totals) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t n = *n_ev_dev;
-  if (i == 0) *n_host = n == 0 ? 0 : pos[n - 1] + flag[n - 1];
-  if (i >= n || i >= cap || !flag[i]) return;
-  out[pos[i]] = ev[i];
-  out_idx[pos[i]] = i;
+  if (i == 0) *totals = n == 0 ? SelCount{0, 0, 0, 0} : SelPlus()(pos[n - 1], val[n - 1]);
+  if (i >= n || i >= cap) return;
+  const uint8_t fl = flag[i];
+  if (!fl) return;
+  const SelCount p = pos[i];
+  if (fl & SEL_HOST) { out[p.host] = ev[i]; out_idx[p.host] = i; }
+  if (fl & SEL_MH) mh_idx[p.mh] = i;
+  if (fl & SEL_WALK) walk_idx[p.walk] = i;
 }
 
 // ------------------------------------------------------------------------ op build
@@ -125,7 +370,29 @@ __global__ void k_build_ops(DJArgs a) {
   double snum = apm_nan();
   uint64_t shash = 0;
   const uint8_t* p = a.bytes + e.off;
-  if (a.host_flag[i]) {
+  if (e.kind == LK_APP) {  // K5 fields; a map line's BAF account is saved at once (saveAcctNum)
+    AudF f;
+    bool ok = false;
+    if (a.host_flag[i] & SEL_HOST) {
+      const HostOp* h = find_hop(a.hops, a.n_hops, i);
+      if (h && h->kind == HOP_AUD) { f = *reinterpret_cast<const AudF*>(&h->op); ok = true; }
+    } else {
+      ok = aud_fields(e, a.bytes, file, f);
+    }
+    if (!ok) {  // (no host op: the line is ignored, as the host pre-pass would)
+      f.h_item = 0; f.el = apm_nan(); f.h_sw = 0; f.ts = apm_nan(); f.ref = 0; f.len = 0; f.flags = 0;
+    }
+    a.aud[i] = f;
+    if ((e.mask & PM_AUTR_MAP) && (f.flags & AF_ACCT)) {
+      if (!(f.flags & AF_ACCT_VALID)) {
+        atomicAdd(&a.counts->invalid_acct, 1ULL);
+      } else if (f.len > 0) {
+        op.op = JOP_ACCT;
+        op.gkey = gkey_of(f.h_sw, server);
+        op.num = f.el;
+      }
+    }
+  } else if (a.host_flag[i] & SEL_HOST) {
     const HostOp* h = find_hop(a.hops, a.n_hops, i);
     if (h) {
       switch (h->kind) {
@@ -345,6 +612,252 @@ __global__ __launch_bounds__(APM_WAVE) void k_soap_apply(DJArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------ audit trail (K5)
+// See devjoin_types.h "audit trail".  Kernels (join stream, after k_build_ops wrote a.aud):
+//   k_aud_keys   sort input: carried map entries, then this batch's MAP / HDR events
+//   radix sort   by (file, auditTrailId) key, stable
+//   k_aud_autr   one lane per key: MAP sets the entry, HDR consumes it (AF_HDR_OK + its logId /
+//                alt on the HDR's AudF); the entry still live at the end is carried
+//   k_aud_chunks walk-list range of each chunk, first chunk of each file
+//   k_aud_walk   one lane per block (HDR_OK) + one per file with a carried open block
+__device__ __forceinline__ const uint8_t* aud_src(const DJArgs& a, uint8_t flags, uint32_t ref) {
+  if (flags & AF_SRC_HOST) return a.hbuf + ref;
+  if (flags & AF_SRC_AUD) return (const uint8_t*)a.gin.txt + ref;
+  return a.bytes + ref;
+}
+
+// copy `len` bytes into the next generation's text; returns the offset (AUD_NIL: over capacity)
+__device__ uint32_t aud_put_txt(const DJArgs& a, const uint8_t* src, uint32_t len) {
+  if (!len) return 0;
+  const uint32_t o = atomicAdd(&a.counts->aud_txt_n, len);
+  if ((uint64_t)o + len > a.gout.cap_txt) { atomicAdd(&a.counts->aud_pad, 1u); return AUD_NIL; }
+  for (uint32_t j = 0; j < len; ++j) a.gout.txt[o + j] = (char)src[j];
+  return o;
+}
+
+__global__ void k_aud_keys(DJArgs a) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nc = a.gin.n_autr;
+  if (j >= nc + a.n_mh) return;
+  a.aud_key[j] = j < nc ? a.gin.autr[j].key : a.aud[a.mh_idx[j - nc]].h_item;
+  a.aud_ord[j] = j;
+}
+
+__global__ void k_aud_autr(DJArgs a) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nc = a.gin.n_autr, N = nc + a.n_mh;
+  if (j >= N) return;
+  const uint64_t key = a.aud_key_sorted[j];
+  if (j > 0 && a.aud_key_sorted[j - 1] == key) return;
+  bool have = false;
+  uint8_t src = 0;
+  uint32_t ref = 0, len = 0;
+  uint64_t lh = 0;
+  double alt = apm_nan();
+  for (uint32_t q = j; q < N && a.aud_key_sorted[q] == key; ++q) {
+    const uint32_t o = a.aud_ord_sorted[q];
+    if (o < nc) {  // carried entry (sorts first: stable, carried entries precede the batch's)
+      const AutrEnt t = a.gin.autr[o];
+      have = true; src = AF_SRC_AUD; ref = t.lid_off; len = t.lid_len; lh = t.lid_hash; alt = t.alt;
+      continue;
+    }
+    const uint32_t ev = a.mh_idx[o - nc];
+    AudF& f = a.aud[ev];
+    if (a.ev[ev].mask & PM_AUTR_MAP) {  // auditTrailIdMap[autr] = {logId, alt}
+      have = true; src = f.flags & AF_SRC_HOST; ref = f.ref; len = f.len; lh = f.h_sw; alt = f.el;
+    } else if (have && len > 0) {  // header: the block starts; the entry is deleted
+      f.flags = (uint8_t)((f.flags & ~(AF_SRC_HOST | AF_SRC_AUD)) | AF_HDR_OK | src);
+      f.ref = ref; f.len = (uint16_t)len; f.h_sw = lh; f.el = alt;
+      have = false;
+    } else {  // no entry (or an empty logId): an audit error, nothing changes
+      atomicAdd(&a.counts->audit_errors, 1ULL);
+    }
+  }
+  if (!have) return;
+  const uint32_t k = atomicAdd(&a.counts->aud_autr_n, 1u);
+  if (k >= a.gout.cap_autr) { atomicAdd(&a.counts->aud_pad, 1u); return; }
+  AutrEnt t;
+  t.key = key; t.lid_hash = lh; t.alt = alt; t.lid_len = len;
+  t.lid_off = aud_put_txt(a, aud_src(a, src, ref), len);
+  a.gout.autr[k] = t;
+}
+
+__global__ void k_aud_chunks(DJArgs a) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c > a.n_chunks) return;
+  uint32_t l = 0, h = a.n_walk;
+  while (l < h) {
+    const uint32_t mid = (l + h) >> 1;
+    if (a.ev[a.walk_idx[mid]].chunk < c) l = mid + 1; else h = mid;
+  }
+  a.walk_lo[c] = l;
+  if (c < a.n_chunks && a.chunk_first[c]) a.file_first_chunk[a.chunk_file[c]] = (int32_t)c;
+}
+
+// first walk position at or after chunk c of a file (following its chunk chain)
+__device__ __forceinline__ uint32_t walk_from_chunk(const DJArgs& a, int32_t c) {
+  for (; c >= 0 && (uint32_t)c < a.n_chunks; c = a.chunk_next[c])
+    if (a.walk_lo[c] < a.walk_lo[c + 1]) return a.walk_lo[c];
+  return AUD_NIL;
+}
+
+__device__ __forceinline__ uint32_t walk_next(const DJArgs& a, uint32_t p, uint32_t chunk) {
+  if (p + 1 < a.walk_lo[chunk + 1]) return p + 1;
+  return walk_from_chunk(a, a.chunk_next[chunk]);
+}
+
+struct AudWalk {  // one open audit block (AuditCtx of the host state machine)
+  bool elapsed, sw, has_svc, to_db;
+  uint8_t lid_src, svc_src;
+  uint64_t lid_hash, svc_hash;
+  double alt;
+  uint32_t lid_ref, lid_len, svc_ref, svc_len;
+  uint32_t head, tail;  // queued elapsed entries (item slots), insertion order
+};
+
+__global__ void k_aud_walk(DJArgs a) {
+  const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nw = a.n_walk;
+  if (id >= nw + a.n_files) return;
+  AudWalk w;
+  uint32_t p, start;
+  int32_t file;
+  bool carried = id >= nw;
+  if (carried) {
+    file = (int32_t)(id - nw);
+    const AudCarry c = a.gin.carry[file];
+    if (!c.active) return;
+    w.elapsed = c.elapsed; w.sw = c.sw; w.has_svc = c.has_svc; w.to_db = c.svc_to_db;
+    w.lid_src = AF_SRC_AUD; w.svc_src = AF_SRC_AUD;
+    w.lid_hash = c.lid_hash; w.svc_hash = c.svc_hash; w.alt = c.alt;
+    w.lid_ref = c.lid_off; w.lid_len = c.lid_len; w.svc_ref = c.svc_off; w.svc_len = c.svc_len;
+    w.head = w.tail = AUD_NIL;
+    for (uint32_t j = 0; j < c.n_items; ++j) {  // carried queue -> slots nw + items_off + j
+      const uint32_t s = nw + c.items_off + j;
+      AudItem it = a.gin.items[c.items_off + j];
+      it.next = AUD_NIL;
+      a.aud_slots[s] = it;
+      if (w.tail == AUD_NIL) w.head = s; else a.aud_slots[w.tail].next = s;
+      w.tail = s;
+    }
+    start = AUD_NIL;
+    p = walk_from_chunk(a, a.file_first_chunk[file]);
+  } else {
+    const uint32_t ev = a.walk_idx[id];
+    if (!(a.aud[ev].flags & AF_HDR_OK)) return;
+    file = (int32_t)a.chunk_file[a.ev[ev].chunk];
+    start = p = id;
+  }
+  const int32_t server = a.file_server[file];
+  while (p != AUD_NIL) {
+    const uint32_t ev = a.walk_idx[p];
+    const Event e = a.ev[ev];
+    if (e.chunk >= a.n_chunks) break;  // (never: events are in chunk order)
+    const uint32_t m = e.mask;
+    const uint32_t np = walk_next(a, p, e.chunk);
+    if (m & PM_AUTR_HDR) {
+      const AudF f = a.aud[ev];
+      if (f.flags & AF_HDR_OK) {
+        if (p != start) return;  // the next block's lane takes over
+        // serviceMap cleared, the block's logId / alt from the map entry
+        w.elapsed = w.sw = w.has_svc = w.to_db = false;
+        w.lid_src = f.flags & (AF_SRC_HOST | AF_SRC_AUD); w.lid_ref = f.ref; w.lid_len = f.len;
+        w.lid_hash = f.h_sw; w.alt = f.el;
+        w.svc_src = 0; w.svc_hash = 0; w.svc_ref = w.svc_len = 0;
+        w.head = w.tail = AUD_NIL;
+      }
+      p = np;
+      continue;
+    }
+    if (m & PM_EL_START) {
+      w.elapsed = true;
+    } else if (w.elapsed) {
+      if (m & PM_EL_END) {
+        w.elapsed = false;
+      } else {  // serviceMap[service].push({elapsed})
+        const AudF f = a.aud[ev];
+        AudItem it;
+        it.svc = f.h_item; it.el = f.el; it.start = apm_nan(); it.flags = 0; it.next = AUD_NIL;
+        a.aud_slots[p] = it;
+        if (w.tail == AUD_NIL) w.head = p; else a.aud_slots[w.tail].next = p;
+        w.tail = p;
+      }
+    } else if (m & PM_SW_START) {
+      w.sw = true;
+    } else if (!w.sw) {
+    } else if (m & PM_SW_END) {
+      return;  // block closed: nothing open for this file after it
+    } else if (m & PM_SW_NAME) {
+      const AudF f = a.aud[ev];
+      w.has_svc = true; w.svc_src = f.flags & AF_SRC_HOST; w.svc_ref = f.ref; w.svc_len = f.len;
+      w.svc_hash = f.h_sw; w.to_db = (f.flags & AF_TO_DB) != 0;
+    } else if (w.has_svc && w.svc_len > 0 && (m & (PM_SW_STARTTS | PM_SW_STOPTS))) {
+      // the front of the active service's queue
+      uint32_t prev = AUD_NIL, s = w.head;
+      while (s != AUD_NIL && a.aud_slots[s].svc != w.svc_hash) { prev = s; s = a.aud_slots[s].next; }
+      const AudF f = a.aud[ev];
+      if (s == AUD_NIL) {
+        atomicAdd(&a.counts->audit_errors, 1ULL);
+      } else if (m & PM_SW_STARTTS) {
+        AudItem& it = a.aud_slots[s];
+        it.start = f.ts;
+        it.flags = AI_START | ((f.flags & AF_TS_EMPTY) ? AI_START_EMPTY : 0u);
+      } else {  // stopTime: the entry leaves the queue and becomes a transaction
+        const AudItem it = a.aud_slots[s];
+        if (prev == AUD_NIL) w.head = it.next; else a.aud_slots[prev].next = it.next;
+        if (w.tail == s) w.tail = prev;
+        JOp op;
+        op.gkey = gkey_of(w.lid_hash, server);
+        op.svc = w.svc_hash;
+        op.ts = f.ts;
+        op.num = it.el;
+        op.aux = it.start;
+        op.aux2 = w.alt;
+        op.line = e.line;
+        op.server = server;
+        op.lid = w.lid_ref; op.lid_len = (uint16_t)w.lid_len;
+        op.svc_ref = w.svc_ref; op.svc_len = (uint16_t)w.svc_len;
+        uint16_t fl = JF_HAS_SVC;
+        if (f.flags & AF_TS_EMPTY) fl |= JF_TS_EMPTY;
+        if (!(it.flags & AI_START) || (it.flags & AI_START_EMPTY)) fl |= JF_START_EMPTY;
+        if (w.to_db) fl |= JF_TO_DB;
+        if (w.lid_src & AF_SRC_HOST) fl |= JF_LID_HOST;
+        if (w.lid_src & AF_SRC_AUD) fl |= JF_LID_AUD;
+        if (w.svc_src & AF_SRC_HOST) fl |= JF_SVC_HOST;
+        if (w.svc_src & AF_SRC_AUD) fl |= JF_SVC_AUD;
+        op.flags = fl;
+        op.op = JOP_AUDIT_TX;
+        op.pad = 0; op.pad2[0] = op.pad2[1] = 0;
+        a.ops[ev] = op;
+      }
+    }
+    p = np;
+  }
+  // the batch ends inside this block: carry it (strings and queue into the next generation)
+  AudCarry c;
+  c.active = 1; c.elapsed = w.elapsed; c.sw = w.sw; c.has_svc = w.has_svc; c.svc_to_db = w.to_db;
+  c.pad0[0] = c.pad0[1] = c.pad0[2] = 0;
+  c.lid_hash = w.lid_hash; c.svc_hash = w.svc_hash; c.alt = w.alt;
+  c.lid_len = w.lid_len; c.lid_off = aud_put_txt(a, aud_src(a, w.lid_src, w.lid_ref), w.lid_len);
+  c.svc_len = w.svc_len; c.svc_off = aud_put_txt(a, aud_src(a, w.svc_src, w.svc_ref), w.svc_len);
+  uint32_t n = 0;
+  for (uint32_t s = w.head; s != AUD_NIL; s = a.aud_slots[s].next) ++n;
+  const uint32_t o = n ? atomicAdd(&a.counts->aud_items_n, n) : 0;
+  if ((uint64_t)o + n > a.gout.cap_items) {
+    atomicAdd(&a.counts->aud_pad, 1u);
+    n = 0;
+  }
+  uint32_t j = 0;
+  for (uint32_t s = w.head; s != AUD_NIL && j < n; s = a.aud_slots[s].next, ++j) {
+    AudItem it = a.aud_slots[s];
+    it.next = 0;
+    a.gout.items[o + j] = it;
+  }
+  c.items_off = o;
+  c.n_items = n;
+  a.gout.carry[file] = c;
+}
+
 // ------------------------------------------------------------------------ tables
 __device__ uint32_t key_claim(KeyState* __restrict__ t, uint32_t mask, uint64_t k, JoinCounts* cnt) {
   uint32_t h = home_of(k, mask);
@@ -414,7 +927,7 @@ __global__ void k_claim(DJArgs a) {
             r.server = op.server;
             r.name = op.svc_ref;
             r.name_len = op.svc_len;
-            r.flags = op.flags & (JF_EJB | JF_SVC_UNDEF | JF_SVC_HOST);
+            r.flags = op.flags & (JF_EJB | JF_SVC_UNDEF | JF_SVC_HOST | JF_SVC_AUD);
             r.slot = (int32_t)idx;
             a.miss[m] = r;
           }
@@ -601,7 +1114,9 @@ struct Emitter {
   }
 };
 
-__device__ __forceinline__ uint8_t lid_src_of(const JOp& op) { return (op.flags & JF_LID_HOST) ? LID_HOST : LID_BATCH; }
+__device__ __forceinline__ uint8_t lid_src_of(const JOp& op) {
+  return (op.flags & JF_LID_HOST) ? LID_HOST : (op.flags & JF_LID_AUD) ? LID_AUD : LID_BATCH;
+}
 
 // needNumRecordCache entry of this batch's region (all share the batch's TTL clock)
 __device__ int32_t need_alloc(DJArgs& a, const JOp& op, uint64_t gkey) {
@@ -621,7 +1136,8 @@ __device__ int32_t need_alloc(DJArgs& a, const JOp& op, uint64_t gkey) {
   ne.lblk = 0;
   ne.vidx = a.arena_base + k;
   uint32_t n = op.lid_len;
-  const uint8_t* src = (op.flags & JF_LID_HOST) ? a.hbuf + op.lid : a.bytes + op.lid;
+  const uint8_t* src = (op.flags & JF_LID_HOST) ? a.hbuf + op.lid
+                      : (op.flags & JF_LID_AUD) ? (const uint8_t*)a.gin.txt + op.lid : a.bytes + op.lid;
   for (uint32_t j = 0; j < n && j < (uint32_t)NEED_LID; ++j) ne.lid[j] = (char)src[j];
   // a logId longer than the inline bytes continues in a LidBlk chain (the tx line prints it whole)
   int32_t prev = 0;
@@ -897,6 +1413,7 @@ __device__ __forceinline__ const char* lid_ptr(const DJFormatArgs& f, const TxDe
     case LID_BATCH: return (const char*)f.bytes + t.lid;
     case LID_HOST: return (const char*)f.hbuf + t.lid;
     case LID_NEED: return f.arena[t.lid & (f.arena_cap - 1)].lid;
+    case LID_AUD: return f.aud_txt + t.lid;
     default: return "";
   }
 }
@@ -1295,6 +1812,18 @@ __global__ void k_count_le(const int64_t* __restrict__ end, int64_t n, int64_t e
 extern "C" {
 using namespace apm;
 
+// APM_DJ_DEBUG=1: synchronize after every launch of the join and name the first that fails
+static void dj_check(hipStream_t s, const char* what) {
+  static const bool dbg = std::getenv("APM_DJ_DEBUG") != nullptr;
+  if (!dbg) return;
+  const hipError_t e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    fprintf(stderr, "[devjoin debug] %s: %s\n", what, hipGetErrorString(e));
+    fflush(stderr);
+    abort();
+  }
+}
+
 size_t apm_dj_tmp_bytes(uint32_t max_ev, uint32_t max_out, int table_bits) {
   size_t a = 0, b = 0, c = 0, d = 0, e = 0;
   const size_t n = std::max<size_t>(max_ev, 1) + 1;
@@ -1308,21 +1837,56 @@ size_t apm_dj_tmp_bytes(uint32_t max_ev, uint32_t max_out, int table_bits) {
                                  (hipStream_t)0));
   HIP_OK(rocprim::inclusive_scan(nullptr, e, (int64_t*)nullptr, (int64_t*)nullptr, (size_t)max_out + 1,
                                  rocprim::maximum<int64_t>(), (hipStream_t)0));
-  return std::max(std::max(std::max(a, b), std::max(c, d)), e) + 4096;
+  size_t f = 0;
+  HIP_OK(rocprim::exclusive_scan(nullptr, f, (SelCount*)nullptr, (SelCount*)nullptr, SelCount{0, 0, 0, 0}, n, SelPlus(),
+                                 (hipStream_t)0));
+  return std::max(std::max(std::max(a, b), std::max(c, d)), std::max(e, f)) + 4096;
 }
 
 int apm_dj_select_host(DJArgs* a, const uint32_t* d_n_ev, uint32_t max_ev, hipStream_t s) {
-  if (max_ev == 0) { HIP_OK(hipMemsetAsync(a->n_host, 0, 4, s)); return 0; }
+  if (max_ev == 0) { HIP_OK(hipMemsetAsync(a->n_host, 0, sizeof(SelCount), s)); return 0; }
   hipLaunchKernelGGL(k_host_flags, dim3((max_ev + TB - 1) / TB), dim3(TB), 0, s, a->ev, d_n_ev, a->bytes, a->host_flag,
-                     max_ev);
+                     a->sel_val, max_ev);
+  dj_check(s, "k_host_flags");
   size_t need = 0;
-  HIP_OK(rocprim::exclusive_scan(nullptr, need, a->host_flag, a->host_pos, 0u, (size_t)max_ev,
-                                 rocprim::plus<uint32_t>(), s));
+  HIP_OK(rocprim::exclusive_scan(nullptr, need, a->sel_val, a->sel_pos, SelCount{0, 0, 0, 0}, (size_t)max_ev, SelPlus(),
+                                 s));
   if (need > a->tmp_bytes) return -1;
-  HIP_OK(rocprim::exclusive_scan(a->tmp, need, a->host_flag, a->host_pos, 0u, (size_t)max_ev,
-                                 rocprim::plus<uint32_t>(), s));
-  hipLaunchKernelGGL(k_host_scatter, dim3((max_ev + TB - 1) / TB), dim3(TB), 0, s, a->ev, a->host_flag, a->host_pos,
-                     max_ev, d_n_ev, a->host_ev, a->host_ev_idx, a->n_host);
+  HIP_OK(rocprim::exclusive_scan(a->tmp, need, a->sel_val, a->sel_pos, SelCount{0, 0, 0, 0}, (size_t)max_ev, SelPlus(),
+                                 s));
+  dj_check(s, "rocprim_exclusive_scan");
+  hipLaunchKernelGGL(k_host_scatter, dim3((max_ev + TB - 1) / TB), dim3(TB), 0, s, a->ev, a->host_flag, a->sel_val,
+                     a->sel_pos, max_ev, d_n_ev, a->host_ev, a->host_ev_idx, a->mh_idx, a->walk_idx, a->n_host);
+  dj_check(s, "k_host_scatter");
+  return 0;
+}
+
+// K5: map / header matching, then the block walks (their stopTime ops land in a->ops)
+static int apm_dj_audit(DJArgs* a, hipStream_t s) {
+  if (a->n_files) HIP_OK(hipMemsetAsync(a->gout.carry, 0, (size_t)a->n_files * sizeof(AudCarry), s));
+  const uint32_t N = a->gin.n_autr + a->n_mh;
+  if (N) {
+    hipLaunchKernelGGL(k_aud_keys, dim3((N + TB - 1) / TB), dim3(TB), 0, s, *a);
+    dj_check(s, "k_aud_keys");
+    size_t need = 0;
+    HIP_OK(rocprim::radix_sort_pairs(nullptr, need, a->aud_key, a->aud_key_sorted, a->aud_ord, a->aud_ord_sorted,
+                                     (size_t)N, 0, 64, s));
+    if (need > a->tmp_bytes) return -1;
+    HIP_OK(rocprim::radix_sort_pairs(a->tmp, need, a->aud_key, a->aud_key_sorted, a->aud_ord, a->aud_ord_sorted,
+                                     (size_t)N, 0, 64, s));
+    dj_check(s, "rocprim_radix_sort_pairs");
+    hipLaunchKernelGGL(k_aud_autr, dim3((N + TB - 1) / TB), dim3(TB), 0, s, *a);
+    dj_check(s, "k_aud_autr");
+  }
+  // an open block always carries its (non-empty) logId: no carry text, no carried block
+  if (a->n_walk || a->gin.n_txt) {
+    if (a->n_files) HIP_OK(hipMemsetAsync(a->file_first_chunk, 0xff, (size_t)a->n_files * 4, s));
+    hipLaunchKernelGGL(k_aud_chunks, dim3((a->n_chunks + 1 + TB - 1) / TB), dim3(TB), 0, s, *a);
+    dj_check(s, "k_aud_chunks");
+    const uint32_t L = a->n_walk + a->n_files;
+    hipLaunchKernelGGL(k_aud_walk, dim3((L + 63) / 64), dim3(64), 0, s, *a);
+    dj_check(s, "k_aud_walk");
+  }
   return 0;
 }
 
@@ -1333,12 +1897,22 @@ int apm_dj_join(DJArgs* a, hipStream_t s) {
   if (n) {
     HIP_OK(hipMemsetAsync(a->out_cnt, 0, ((size_t)n + 1) * 4, s));
     hipLaunchKernelGGL(k_build_ops, dim3((n + TB - 1) / TB), dim3(TB), 0, s, *a);
+    dj_check(s, "k_build_ops");
     hipLaunchKernelGGL(k_chunk_events, dim3((a->n_chunks + 1 + TB - 1) / TB), dim3(TB), 0, s, a->ev, n, a->n_chunks,
                        a->chunk_ev_lo);
+    dj_check(s, "k_chunk_events");
+  }
+  // (also for a batch without events: the carry moves to the next generation)
+  if (apm_dj_audit(a, s) != 0) return -1;
+  if (n) {
     hipLaunchKernelGGL(k_soap_summary, dim3(a->n_chunks, SOAP_SEGS), dim3(APM_WAVE), 0, s, *a);
+    dj_check(s, "k_soap_summary");
     hipLaunchKernelGGL(k_soap_carry, dim3((a->n_chunks + 63) / 64), dim3(64), 0, s, *a);
+    dj_check(s, "k_soap_carry");
     hipLaunchKernelGGL(k_soap_apply, dim3(a->n_chunks, SOAP_SEGS), dim3(APM_WAVE), 0, s, *a);
+    dj_check(s, "k_soap_apply");
     hipLaunchKernelGGL(k_claim, dim3((n + TB - 1) / TB), dim3(TB), 0, s, *a);
+    dj_check(s, "k_claim");
     static const bool merge_sort = [] { const char* e = std::getenv("APM_OPSORT"); return e && e[0] == 'm'; }();
     size_t need = 0;
     if (merge_sort) {  // diagnostic: rocprim's default (block sort + merge passes)
@@ -1347,6 +1921,7 @@ int apm_dj_join(DJArgs* a, hipStream_t s) {
       if (need > a->tmp_bytes) return -1;
       HIP_OK(rocprim::radix_sort_pairs(a->tmp, need, a->op_slot, a->op_slot_sorted, a->op_idx, a->op_idx_sorted,
                                        (size_t)n, 0, a->table_bits + 2, s));
+      dj_check(s, "rocprim_radix_sort_pairs");
     } else {
       HIP_OK(rocprim::radix_sort_pairs<OpSortCfg>(nullptr, need, a->op_slot, a->op_slot_sorted, a->op_idx,
                                                   a->op_idx_sorted, (size_t)n, 0, a->table_bits + 2, s));
@@ -1361,36 +1936,47 @@ int apm_dj_join(DJArgs* a, hipStream_t s) {
   const uint32_t E = a->n_exp_entries;
   if (E) {
     hipLaunchKernelGGL(k_exp_keys, dim3((E + TB - 1) / TB), dim3(TB), 0, s, *a);
+    dj_check(s, "k_exp_keys");
     size_t need = 0;
     HIP_OK(rocprim::radix_sort_pairs(nullptr, need, a->exp_key, a->exp_key_sorted, a->exp_idx, a->exp_idx_sorted,
                                      (size_t)E, 0, 64, s));
     if (need > a->tmp_bytes) return -1;
     HIP_OK(rocprim::radix_sort_pairs(a->tmp, need, a->exp_key, a->exp_key_sorted, a->exp_idx, a->exp_idx_sorted,
                                      (size_t)E, 0, 64, s));
+    dj_check(s, "rocprim_radix_sort_pairs");
     hipLaunchKernelGGL(k_exp_count, dim3((E + 1 + TB - 1) / TB), dim3(TB), 0, s, *a);
+    dj_check(s, "k_exp_count");
     need = 0;
     HIP_OK(rocprim::exclusive_scan(nullptr, need, a->exp_cnt, a->exp_pos, 0u, (size_t)E + 1,
                                    rocprim::plus<uint32_t>(), s));
     if (need > a->tmp_bytes) return -1;
     HIP_OK(rocprim::exclusive_scan(a->tmp, need, a->exp_cnt, a->exp_pos, 0u, (size_t)E + 1,
                                    rocprim::plus<uint32_t>(), s));
+    dj_check(s, "rocprim_exclusive_scan");
   }
   hipLaunchKernelGGL(k_exp_emit, dim3((std::max<uint32_t>(E, 1) + TB - 1) / TB), dim3(TB), 0, s, *a);
+  dj_check(s, "k_exp_emit");
   if (n) {
     hipLaunchKernelGGL(k_group_walk, dim3((n + TB - 1) / TB), dim3(TB), 0, s, *a);
+    dj_check(s, "k_group_walk");
     size_t need = 0;
     HIP_OK(rocprim::exclusive_scan(nullptr, need, a->out_cnt, a->out_pos, 0u, (size_t)n + 1,
                                    rocprim::plus<uint32_t>(), s));
     if (need > a->tmp_bytes) return -1;
     HIP_OK(rocprim::exclusive_scan(a->tmp, need, a->out_cnt, a->out_pos, 0u, (size_t)n + 1,
                                    rocprim::plus<uint32_t>(), s));
+    dj_check(s, "rocprim_exclusive_scan");
     hipLaunchKernelGGL(k_place, dim3((2 * n + TB - 1) / TB), dim3(TB), 0, s, *a);
+    dj_check(s, "k_place");
     hipLaunchKernelGGL(k_place_ovf, dim3(DJ_OVF_CAP / TB), dim3(TB), 0, s, *a);
+    dj_check(s, "k_place_ovf");
   } else {
     HIP_OK(hipMemsetAsync(a->out_pos, 0, 4, s));
     hipLaunchKernelGGL(k_place, dim3(1), dim3(TB), 0, s, *a);
+    dj_check(s, "k_place");
   }
   hipLaunchKernelGGL(k_pool_fix, dim3(1), dim3(1), 0, s, a->counts);
+  dj_check(s, "k_pool_fix");
   return 0;
 }
 

@@ -17,6 +17,25 @@ struct DJOverflow {
   TxDev t;
 };
 
+// One generation of the audit carry (devjoin_types.h AudCarry / AutrEnt / AudItem); batch k reads
+// generation k % 2 and writes the other one.
+struct AudGen {
+  AudCarry* carry;    // [max files]
+  AutrEnt* autr;
+  AudItem* items;
+  char* txt;
+  uint32_t n_autr, n_items, n_txt;  // host-known sizes (input generation)
+  uint32_t cap_autr, cap_items, cap_txt;
+};
+
+// Per-event selection counts of the parse-side pass (one exclusive scan of these)
+struct SelCount {
+  uint32_t host;      // events the host resolves
+  uint32_t mh;        // audit map lines + block headers
+  uint32_t walk;      // audit lines of the block walks (every LK_APP event but map lines)
+  uint32_t aud_bytes; // bytes of map / stopWatch name lines (bound of the carry text they add)
+};
+
 // Everything one batch of the device join touches.  Device pointers unless noted.
 struct DJArgs {
   // ---- batch inputs
@@ -36,11 +55,26 @@ struct DJArgs {
   uint64_t batch_no;
   double rec_ttl, acct_ttl, need_ttl;
   // ---- host-event selection (run right after the parse kernels)
-  uint8_t* host_flag;             // [n_ev]
-  uint32_t* host_pos;             // [n_ev + 1] exclusive scan
+  uint8_t* host_flag;             // [n_ev] SEL_* bits
+  SelCount* sel_val;              // [n_ev + 1] per-event counts
+  SelCount* sel_pos;              // [n_ev + 1] exclusive scan
   Event* host_ev;                 // compacted host events
   uint32_t* host_ev_idx;
-  uint32_t* n_host;               // device count
+  uint32_t* mh_idx;               // compacted audit map / header events (event indices)
+  uint32_t* walk_idx;             // compacted audit walk events (event indices, line order per file)
+  SelCount* n_host;               // device totals
+  // ---- audit trail (K5)
+  uint32_t n_mh, n_walk;          // host-known totals
+  uint32_t n_files;
+  AudF* aud;                      // [n_ev]
+  AudGen gin, gout;               // carry in (read) / out (written)
+  uint64_t* aud_key;              // [gin.n_autr + n_mh] sort keys
+  uint64_t* aud_key_sorted;
+  uint32_t* aud_ord;              // values: < gin.n_autr carried entry, else mh position
+  uint32_t* aud_ord_sorted;
+  uint32_t* walk_lo;              // [n_chunks + 1] first walk position per chunk
+  int32_t* file_first_chunk;      // [n_files]
+  AudItem* aud_slots;             // [n_walk + gin.n_items] item slot space of the walks
   // ---- op build + SOAP scan
   JOp* ops;                       // [n_ev]
   uint8_t* soap_code;             // [n_ev]
@@ -105,6 +139,7 @@ struct DJFormatArgs {
   const char* names;              // join names table
   const uint8_t* bytes;
   const uint8_t* hbuf;
+  const char* aud_txt;            // audit carry text of this batch (LID_AUD)
   const NeedEnt* arena;
   uint32_t arena_cap;
   const uint8_t* pool;            // chain blocks (long logIds of need entries)

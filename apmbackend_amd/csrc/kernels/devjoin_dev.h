@@ -17,6 +17,10 @@ __host__ __device__ inline uint64_t regkey_of(uint64_t svc, int32_t server) {
   const uint64_t k = hash_mix(svc ^ ((uint64_t)(uint32_t)(server + 7) * 0xC2B2AE3D27D4EB4FULL), 0x165667b19e3779f9ULL);
   return k ? k : 1;
 }
+// audit-trail map key: (file, hash(auditTrailId)), never 0
+__host__ __device__ inline uint64_t aud_key(uint64_t autr_hash, int32_t file) {
+  return hash_mix(autr_hash, 0x9e3779b97f4a7c15ULL + (uint64_t)(uint32_t)file) | 1ULL;
+}
 __host__ __device__ inline uint32_t home_of(uint64_t k, uint32_t mask) {
   return (uint32_t)((k * 0x9E3779B97F4A7C15ULL) >> 32) & mask;
 }

@@ -11,8 +11,8 @@
 //   NeedEnt   -- needNumRecordCache entry (parked exits waiting for an account), arena-allocated
 //                per batch so a batch's entries expire together (their TTL clock is the batch's)
 // SOAP request contexts (per file) are resolved by a segmented scan over state-transition
-// functions; the audit-trail state machine (K5, rare multi-line blocks) and lines the parser
-// deferred to the host (PM_HOST) are resolved on the host into explicit ops (HostOp).
+// functions, the audit-trail state machine (K5) by key-grouped and block-parallel walks (below);
+// the host only re-derives the fields of lines the parser deferred (PM_HOST) as HostOps.
 #pragma once
 #include <stdint.h>
 
@@ -40,6 +40,8 @@ enum JOpFlags : uint16_t {
   JF_SVC_HOST = 1u << 7,     // service name bytes in the host op buffer
   JF_EJB = 1u << 8,          // EJB service ("S:" prefix, kHashSeedEjb)
   JF_HAS_SVC = 1u << 9,      // op names a service (registry claim)
+  JF_LID_AUD = 1u << 10,     // logId bytes in the audit carry text (AudGen::txt of this batch)
+  JF_SVC_AUD = 1u << 11,     // service name bytes in the audit carry text
 };
 
 // One join operation per relevant event (line order), 80 B.
@@ -73,6 +75,7 @@ enum HostOpKind : uint8_t {
   HOP_SOAP_KEY = 5,
   HOP_SOAP_VALUE = 6,
   HOP_SKIP = 7,       // event produces nothing
+  HOP_AUD = 8,        // audit line the GPU cannot read alone: its AudF fields (in `op`), strings in hbuf
 };
 struct HostOp {
   uint32_t ev;
@@ -154,7 +157,7 @@ static_assert(sizeof(PartBlk) == CHAIN_BLK && sizeof(NeedBlk) == CHAIN_BLK && si
               "chain block layout");
 
 // A completed transaction (outputRecord :264-290) before formatting, 64 B.
-enum : uint8_t { LID_NONE = 0, LID_BATCH = 1, LID_HOST = 2, LID_NEED = 3 };
+enum : uint8_t { LID_NONE = 0, LID_BATCH = 1, LID_HOST = 2, LID_NEED = 3, LID_AUD = 4 };
 struct TxDev {
   double end;       // endTs after parseInt (NaN: '')
   double start;     // startTs after the start = end - elapsed fallback and parseInt
@@ -204,6 +207,70 @@ struct SoapState {
   uint64_t lid_hash;  // hash(logId) of the context
 };
 
+// ------------------------------------------------------------------------------ audit trail (K5)
+// parseAppLine (stream_parse_transactions.js:578-731) keeps, per log file, an auditTrailId ->
+// {logId, alt account} map and one open audit block (the service -> elapsed queues of its
+// RequestTrace section, then the stopWatchList that pops them).  On the GPU:
+//   * every audit line gets its fields extracted once (AudF, one lane per event; lines the GPU
+//     cannot read alone -- non-ASCII, exotic numbers / dates -- get them from the host, HOP_AUD);
+//   * map lines and block headers are matched per (file, auditTrailId) key: the carried map
+//     entries and this batch's MAP / HDR events are sorted by key (stable: carried first, then
+//     line order) and one lane per key replays them -- a header consumes the live entry;
+//   * each block (a header that found its entry, up to the next such header of its file) is
+//     walked by one lane in line order: the service queues live in a per-batch slot space, a
+//     stopTime pops the front of its service's queue and becomes a JOP_AUDIT_TX op;
+//   * what is still open at the end of the batch (map entries, one block per file) is written to
+//     the next generation of the carry (AudGen, double-buffered): strings into its text arena.
+// The result equals the host state machine (runtime/join.cpp on_app) line for line.
+enum AudFlags : uint8_t {
+  AF_SRC_HOST = 1u << 0,  // ref/len point into the host op buffer (else the batch bytes)
+  AF_SRC_AUD = 1u << 1,   // ... into the carry text of this batch (HDR results only)
+  AF_TS_EMPTY = 1u << 2,  // STARTTS / STOPTS: convertStringDateToMs returned ''
+  AF_TO_DB = 1u << 3,     // SW_NAME: the name has no "Provider[" (insertToDb)
+  AF_HDR_OK = 1u << 4,    // HDR: found a live map entry with a non-empty logId (block start)
+  AF_ACCT = 1u << 5,      // MAP: the alt account is non-empty
+  AF_ACCT_VALID = 1u << 6,  // ... and all digits (saveAcctNum accepts it)
+};
+struct AudF {        // 48 B per event
+  uint64_t h_item;   // item role: hash(service); MAP / HDR: (file, auditTrailId) key
+  double el;         // item role: parseInt(elapsed); MAP / HDR-ok: parseInt(alt account) (NaN: '')
+  uint64_t h_sw;     // SW_NAME: hash(name); MAP / HDR-ok: hash(logId)
+  double ts;         // STARTTS / STOPTS: ms
+  uint32_t ref;      // SW_NAME: name; MAP / HDR-ok: logId (see AF_SRC_*)
+  uint16_t len;
+  uint8_t flags;
+  uint8_t pad;
+  uint32_t pad2[2];
+};
+struct AutrEnt {     // a live auditTrailId map entry carried to the next batch, 32 B
+  uint64_t key;      // (file, auditTrailId)
+  uint64_t lid_hash;
+  double alt;
+  uint32_t lid_off;  // carry text
+  uint32_t lid_len;
+};
+struct AudItem {     // one queued elapsed entry of a service, 32 B
+  uint64_t svc;      // hash(service)
+  double el;
+  double start;      // startTime ms (valid when AI_START and not AI_START_EMPTY)
+  uint32_t flags;
+  uint32_t next;     // slot list link (walk kernels only)
+};
+enum : uint32_t { AI_START = 1u, AI_START_EMPTY = 2u };
+struct AudCarry {    // the open block of one file, 64 B
+  uint8_t active, elapsed, sw, has_svc;
+  uint8_t svc_to_db, pad0[3];
+  uint64_t lid_hash;
+  uint64_t svc_hash;
+  double alt;
+  uint32_t lid_off, lid_len;    // carry text
+  uint32_t svc_off, svc_len;    // carry text
+  uint32_t items_off, n_items;  // carry items, queue order
+  uint32_t pad1[2];
+};
+static_assert(sizeof(AudF) == 48 && sizeof(AutrEnt) == 32 && sizeof(AudItem) == 32 && sizeof(AudCarry) == 64,
+              "audit layouts");
+
 // Batch counters written by the join kernels (D2H once per batch).
 struct JoinCounts {
   uint32_t n_ops;
@@ -221,9 +288,12 @@ struct JoinCounts {
   uint32_t tx_text_bytes;  // "transactions" stream bytes
   uint32_t db_text_bytes;  // "audit_db" stream bytes
   uint32_t pad[2];
+  // audit carry written for the next batch (sizes of its generation)
+  uint32_t aud_autr_n, aud_items_n, aud_txt_n, aud_pad;
   // sticky counters
   unsigned long long ejb_unmatched, partial_overflow, need_overflow, expired_partials, need_expired,
       invalid_acct, table_full, key_probe_max;
+  unsigned long long audit_errors;  // header without a live map entry, start/stop without a queued entry
   // chain-block pool: free-index ring positions (virtual).  Allocation takes [head, tail); frees
   // append at ptail; k_pool_fix publishes them (tail = ptail) after the kernels that allocate.
   unsigned long long pool_head, pool_tail, pool_ptail, pool_fail;

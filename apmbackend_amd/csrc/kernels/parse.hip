@@ -38,9 +38,11 @@ __global__ __launch_bounds__(NL_BLOCK) void k_nl_count(const uint8_t* __restrict
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      // count bytes equal to '\n' (0x0a) in a 32-bit word (SWAR)
-      uint32_t x = w[k] ^ 0x0a0a0a0aU;
-      uint32_t t = (x - 0x01010101U) & ~x & 0x80808080U;
+      // count bytes equal to '\n' (0x0a) in a 32-bit word: exact per-byte SWAR (no borrow
+      // between bytes -- the (x - 0x01..) & ~x form also flags a 0x0b right after a '\n', and
+      // k_nl_write, which counts exactly, would then leave holes in line_end)
+      const uint32_t x = w[k] ^ 0x0a0a0a0aU;
+      const uint32_t t = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
       c += __popc(t);
     }
   } else {
@@ -1189,9 +1191,11 @@ int apm_parse_batch(const uint8_t* d_bytes, uint64_t n_bytes, const uint32_t* d_
     HIP_OK(hipMemsetAsync(d_prof, 0, PP_N * 8, stream));
   }
   pa.prof = prof_on ? d_prof : nullptr;
-  // APM_PARSE=line: the lane-per-line kernel (one block per 256 lines) instead of the tiles
+  // K2 kernel: the lane-per-line kernel (one block per 256 lines) by default; APM_PARSE=tile
+  // selects the cooperative wave-per-tile kernel (experimental: on the edge-case corpus it still
+  // emits events for lines the model drops, tests/test_engine_gpu.py _edge_corpus)
   const char* mode_env = getenv("APM_PARSE");  // read per batch: tests switch it in-process
-  const bool by_line = mode_env && strcmp(mode_env, "line") == 0;
+  const bool by_line = !(mode_env && strcmp(mode_env, "tile") == 0);
   if (by_line)
     hipLaunchKernelGGL(k_parse_lines, dim3((cap + PARSE_BLOCK - 1) / PARSE_BLOCK), dim3(PARSE_BLOCK), 0,
                        stream, pa);

@@ -23,7 +23,7 @@ namespace apm {
 
 // 3: join section carries the join mode (host / GPU); 4: node-wide server order; 5: rings in their own
 // trailing section (full or dirty rows, for incremental checkpoints) + NaN horizons + an opaque extra
-constexpr uint32_t kCkptVersion = 6;
+constexpr uint32_t kCkptVersion = 7;  // 7: device audit-trail carry (K5 on the GPU)
 
 class BinWriter {
  public:

@@ -1,6 +1,6 @@
-// Host driver of the GPU join -- see devjoin.h.  The audit-trail state machine and the PM_HOST
-// field re-derivation mirror runtime/join.cpp (JoinShard::on_app / on_ejb / on_ct / on_soap),
-// which stays the reference implementation of the cache semantics (`gpu.joinOnDevice: false`).
+// Host driver of the GPU join -- see devjoin.h.  The PM_HOST field re-derivation mirrors
+// runtime/join.cpp (JoinShard::on_app / on_ejb / on_ct / on_soap), which stays the reference
+// implementation of the cache semantics (`gpu.joinOnDevice: false`).
 #include "devjoin.h"
 
 #include <algorithm>
@@ -87,13 +87,15 @@ DeviceJoin::DeviceJoin(const DevJoinConfig& cfg, Dictionary* dict, const std::ve
     s.d_bytes = (uint8_t*)dmalloc(cfg_.max_batch_bytes + 256);
     s.d_events = (Event*)dmalloc((size_t)E * sizeof(Event));
     s.host_flag = (uint8_t*)dmalloc(E + 64);
-    s.host_pos = (uint32_t*)dmalloc(((size_t)E + 64) * 4);
     s.d_host_ev = (Event*)dmalloc((size_t)E * sizeof(Event));
     s.d_host_idx = (uint32_t*)dmalloc((size_t)E * 4);
-    s.d_n_host = (uint32_t*)dmalloc(64);
+    s.d_mh_idx = (uint32_t*)dmalloc((size_t)E * 4);
+    s.d_walk_idx = (uint32_t*)dmalloc((size_t)E * 4);
+    s.d_n_host = (SelCount*)dmalloc(64);
     HIP_OK(hipHostMalloc((void**)&s.h_host_ev, (size_t)E * sizeof(Event), hipHostMallocDefault));
     HIP_OK(hipHostMalloc((void**)&s.h_host_idx, (size_t)E * 4, hipHostMallocDefault));
     HIP_OK(hipHostMalloc((void**)&s.h_n_host, 64, hipHostMallocDefault));
+    std::memset(s.h_n_host, 0, 64);
     s.d_chunk_next = (int32_t*)dmalloc(((size_t)cfg_.max_chunks + 2) * 4);
     s.d_chunk_first = (uint8_t*)dmalloc((size_t)cfg_.max_chunks + 2);
     HIP_OK(hipHostMalloc((void**)&s.h_chunk_next, ((size_t)cfg_.max_chunks + 2) * 4, hipHostMallocDefault));
@@ -117,6 +119,15 @@ DeviceJoin::DeviceJoin(const DevJoinConfig& cfg, Dictionary* dict, const std::ve
   HIP_OK(hipHostGetDevicePointer((void**)&hd_exp_, h_exp_, 0));
   soap_cap_ = 1u << 16;
   d_soap_ = (SoapState*)dmalloc((size_t)soap_cap_ * sizeof(SoapState));
+  d_aud_ = (AudF*)dmalloc((size_t)E * sizeof(AudF));
+  d_sel_val_ = (SelCount*)dmalloc(((size_t)E + 64) * sizeof(SelCount));
+  d_sel_pos_ = (SelCount*)dmalloc(((size_t)E + 64) * sizeof(SelCount));
+  d_walk_lo_ = (uint32_t*)dmalloc(((size_t)cfg_.max_chunks + 2) * 4);
+  d_file_first_ = (int32_t*)dmalloc((size_t)soap_cap_ * 4);
+  for (AudGen& g : aud_gen_) {
+    g.carry = (AudCarry*)dmalloc((size_t)soap_cap_ * sizeof(AudCarry));
+    aud_reserve(g, 4096, 16384, 1u << 20);
+  }
   d_file_server_ = (int32_t*)dmalloc((size_t)soap_cap_ * 4);
   d_rawtab_ = (RawSvc*)dmalloc((size_t)cfg_.max_raw * sizeof(RawSvc));
   d_raw_series_ = (int32_t*)dmalloc((size_t)cfg_.max_raw * 4);
@@ -206,15 +217,18 @@ void DeviceJoin::select_host(int k, const uint32_t* d_n_ev, uint32_t max_ev, hip
   a.ev = s.d_events;
   a.bytes = s.d_bytes;
   a.host_flag = s.host_flag;
-  a.host_pos = s.host_pos;
+  a.sel_val = d_sel_val_;
+  a.sel_pos = d_sel_pos_;
   a.host_ev = s.d_host_ev;
   a.host_ev_idx = s.d_host_idx;
+  a.mh_idx = s.d_mh_idx;
+  a.walk_idx = s.d_walk_idx;
   a.n_host = s.d_n_host;
   a.tmp = d_sel_tmp_;  // own scratch: the join of the previous batch runs concurrently
   a.tmp_bytes = sel_tmp_bytes_;
   if (apm_dj_select_host(&a, d_n_ev, std::min<uint32_t>(max_ev, cfg_.max_events), ps) != 0)
     throw std::runtime_error("device join: scan scratch too small");
-  HIP_OK(hipMemcpyAsync(s.h_n_host, s.d_n_host, 4, hipMemcpyDeviceToHost, ps));
+  HIP_OK(hipMemcpyAsync(s.h_n_host, s.d_n_host, sizeof(SelCount), hipMemcpyDeviceToHost, ps));
   // speculative copy of the host events (last count + 25 %): usually all of them
   s.spec = std::min<uint32_t>(cfg_.max_events, last_host_ + last_host_ / 4 + 256);
   HIP_OK(hipMemcpyAsync(s.h_host_ev, s.d_host_ev, (size_t)s.spec * sizeof(Event), hipMemcpyDeviceToHost, ps));
@@ -249,7 +263,7 @@ void DeviceJoin::set_chunks(int k, const std::vector<int32_t>& chunk_file, const
 
 void DeviceJoin::finish_select(int k, hipStream_t ps) {
   Slot& s = sl_[k];
-  const uint32_t n = *s.h_n_host;
+  const uint32_t n = s.h_n_host->host;
   if (n > s.spec) {
     HIP_OK(hipMemcpyAsync(s.h_host_ev + s.spec, s.d_host_ev + s.spec, (size_t)(n - s.spec) * sizeof(Event),
                           hipMemcpyDeviceToHost, ps));
@@ -287,7 +301,6 @@ void DeviceJoin::host_prepass(int k, const uint8_t* hb, uint32_t n_host, const P
       if ((int)tasks_.size() < nt) tasks_.emplace_back();
       PrepassTask& T = tasks_[t];
       T.file = file;
-      T.ctx = &audit_[file];  // created here, single-threaded
       T.idx.clear(); T.hops.clear(); T.hbuf.clear();
       T.audit_errors = T.invalid_acct = T.pm_host = 0;
     } else {
@@ -323,8 +336,15 @@ void DeviceJoin::host_prepass(int k, const uint8_t* hb, uint32_t n_host, const P
       if (pos[t] < tasks_[t].hops.size() && tasks_[t].hops[pos[t]].ev < bev) { bev = tasks_[t].hops[pos[t]].ev; best = t; }
     if (best < 0) break;
     HostOp h = tasks_[best].hops[pos[best]++];
-    if (h.op.flags & JF_LID_HOST) h.op.lid += base[best];
-    if (h.op.flags & JF_SVC_HOST) h.op.svc_ref += base[best];
+    if (h.kind == HOP_AUD) {  // (an AudF in the op's bytes)
+      AudF f;
+      std::memcpy(&f, &h.op, sizeof(f));
+      if (f.flags & AF_SRC_HOST) f.ref += base[best];
+      std::memcpy(&h.op, &f, sizeof(f));
+    } else {
+      if (h.op.flags & JF_LID_HOST) h.op.lid += base[best];
+      if (h.op.flags & JF_SVC_HOST) h.op.svc_ref += base[best];
+    }
     hops_out.push_back(h);
   }
   host_events_ += n_host;
@@ -334,7 +354,7 @@ void DeviceJoin::host_event(PrepassTask& T, const Event& e, uint32_t ev, const u
   const int32_t server = (*files_)[T.file].server;
   const std::string_view line((const char*)hb + e.off, e.len);
   if (e.mask & PM_HOST) ++T.pm_host;
-  if (e.kind == LK_APP) { on_app(T, e, ev, line, server); return; }
+  if (e.kind == LK_APP) { on_app(T, e, ev, line); return; }
   HostOp h;
   std::memset(&h, 0, sizeof(h));
   h.ev = ev;
@@ -438,33 +458,43 @@ void DeviceJoin::host_event(PrepassTask& T, const Event& e, uint32_t ev, const u
   T.hops.push_back(h);
 }
 
-// parseAppLine (:578-731): the per-file audit state machine; cache effects become ops.
-void DeviceJoin::on_app(PrepassTask& T, const Event& e, uint32_t ev, std::string_view line, int32_t server) {
+// HOP_AUD: the fields (AudF) of an audit line the GPU could not read alone -- parseAppLine's
+// string work (:578-731) with the exact JS helpers; the state machine itself runs on the GPU
+// (devjoin.hip k_aud_*).  Mirrors aud_fields() there; strings go to the host op buffer.
+void DeviceJoin::on_app(PrepassTask& T, const Event& e, uint32_t ev, std::string_view line) {
+  HostOp h;
+  std::memset(&h, 0, sizeof(h));
+  h.ev = ev;
+  h.kind = HOP_AUD;
+  AudF f;
+  std::memset(&f, 0, sizeof(f));
+  f.el = js::nan();
+  f.ts = js::nan();
   const uint32_t m = e.mask;
-  auto push = [&](const JOp& op) {
-    HostOp h;
-    std::memset(&h, 0, sizeof(h));
-    h.ev = ev;
-    h.kind = HOP_JOIN;
-    h.op = op;
+  auto done = [&]() {
+    std::memcpy(&h.op, &f, sizeof(f));
     T.hops.push_back(h);
   };
   if (m & PM_AUTR_MAP) {
     auto toks = js::split_ws(line, 8);
     std::string scratch;
-    const std::string log_id(strip_brackets(toks[0], scratch));
+    const std::string_view log_id = strip_brackets(toks[0], scratch);
+    f.h_sw = hash_bytes(log_id.data(), log_id.size());
+    f.len = (uint16_t)std::min<size_t>(log_id.size(), 0xffff);
+    f.ref = T.put(log_id.substr(0, f.len));
+    f.flags |= AF_SRC_HOST;
     const std::string_view t5 = toks.size() > 5 ? toks[5] : std::string_view();
     const size_t eq = t5.find('=');
-    std::string autr;
+    uint64_t ah;
     if (eq != std::string_view::npos) {
       const size_t eq2 = t5.find('=', eq + 1);
-      autr.assign(t5.substr(eq + 1, eq2 == std::string_view::npos ? std::string_view::npos : eq2 - eq - 1));
+      const std::string_view autr = t5.substr(eq + 1, eq2 == std::string_view::npos ? std::string_view::npos : eq2 - eq - 1);
+      ah = hash_bytes(autr.data(), autr.size());
     } else {
-      autr = "undefined";
+      ah = hash_bytes("undefined", 9);
     }
-    AuditCtx& ctx = *T.ctx;
-    // attemptReadAccountNumberFromBAFInfo -> saveAcctNum(acct, 'bafmetainfo', logId)
-    std::string alt;
+    f.h_item = dj::aud_key(ah, T.file);
+    // attemptReadAccountNumberFromBAFInfo -> the block's alt account and saveAcctNum
     if ((e.mask & PM_HOST) ? baf_match(line) : (e.mask & PM_BAF) != 0) {
       std::string_view t3 = toks.size() > 3 ? toks[3] : std::string_view();
       size_t p = std::string_view::npos;
@@ -473,49 +503,26 @@ void DeviceJoin::on_app(PrepassTask& T, const Event& e, uint32_t ev, std::string
       std::string b;
       for (char c : t3) if (c != '[' && c != ']') b.push_back(c);
       const size_t c = b.rfind(':');
-      alt = c == std::string::npos ? b : b.substr(c + 1);
+      const std::string alt = c == std::string::npos ? b : b.substr(c + 1);
       if (!alt.empty()) {
-        const std::string_view t = js::trim(alt);
-        if (!all_digits(t)) {
-          ++T.invalid_acct;
-        } else if (!log_id.empty()) {
-          JOp op = blank_op(e, server);
-          op.op = JOP_ACCT;
-          op.gkey = dj::gkey_of(hash_bytes(log_id.data(), log_id.size()), server);
-          op.num = js::parse_int(t);
-          push(op);
-        }
+        f.flags |= AF_ACCT;
+        f.el = js::parse_int(alt);
+        if (all_digits(js::trim(alt))) f.flags |= AF_ACCT_VALID;
       }
     }
-    auto f = std::find_if(ctx.autr_map.begin(), ctx.autr_map.end(), [&](auto& q) { return q.first == autr; });
-    if (f != ctx.autr_map.end()) f->second = {log_id, alt};
-    else ctx.autr_map.push_back({autr, {log_id, alt}});
-    return;
+    return done();
   }
-  if (m & PM_AUTR_HDR) {
-    AuditCtx& ctx = *T.ctx;
+  if (m & PM_AUTR_HDR) {  // line.split(':')[1].trim()
     const size_t c1 = line.find(':');
     const size_t c2 = line.find(':', c1 + 1);
-    const std::string autr(js::trim(line.substr(c1 + 1, c2 == std::string_view::npos ? std::string_view::npos : c2 - c1 - 1)));
-    auto f = std::find_if(ctx.autr_map.begin(), ctx.autr_map.end(), [&](auto& q) { return q.first == autr; });
-    if (f == ctx.autr_map.end() || f->second.first.empty()) { ++T.audit_errors; return; }
-    ctx.service_map.clear();
-    ctx.active = true;
-    ctx.active_log_id = f->second.first;
-    ctx.active_alt = f->second.second;
-    ctx.elapsed_flag = false;
-    ctx.sw_flag = false;
-    ctx.has_active_service = false;
-    ctx.autr_map.erase(f);
-    return;
+    const std::string_view autr = js::trim(line.substr(c1 + 1, c2 == std::string_view::npos ? std::string_view::npos : c2 - c1 - 1));
+    f.h_item = dj::aud_key(hash_bytes(autr.data(), autr.size()), T.file);
+    return done();
   }
-  AuditCtx& ctx = *T.ctx;
-  if (!ctx.active) return;
-  if (m & PM_EL_START) { ctx.elapsed_flag = true; return; }
-  if (ctx.elapsed_flag) {
-    if (m & PM_EL_END) { ctx.elapsed_flag = false; return; }
+  {  // item role: service and elapsed of a RequestTrace line
     const size_t c1 = line.find(':');
-    const std::string service(js::trim(line.substr(0, c1)));
+    const std::string_view service = js::trim(line.substr(0, c1));
+    f.h_item = hash_bytes(service.data(), service.size());
     std::string elapsed;
     if (c1 != std::string_view::npos) {
       const size_t c2 = line.find(':', c1 + 1);
@@ -523,58 +530,21 @@ void DeviceJoin::on_app(PrepassTask& T, const Event& e, uint32_t ev, std::string
       auto st = js::split_ws(a1, 2);
       for (char ch : st[0]) if (ch != '[' && ch != ']') elapsed.push_back(ch);
     }
-    auto f = std::find_if(ctx.service_map.begin(), ctx.service_map.end(), [&](auto& q) { return q.first == service; });
-    if (f == ctx.service_map.end()) { ctx.service_map.push_back({service, {}}); f = ctx.service_map.end() - 1; }
-    f->second.push_back(AuditItem{elapsed, false, std::string()});
-    return;
+    f.el = js::parse_int(elapsed);
   }
-  if (m & PM_SW_START) { ctx.sw_flag = true; return; }
-  if (!ctx.sw_flag) return;
-  if (m & PM_SW_END) {
-    ctx.active = false;
-    ctx.active_log_id.clear();
-    ctx.active_alt.clear();
-    ctx.has_active_service = false;
-    ctx.elapsed_flag = false;
-    ctx.sw_flag = false;
-    ctx.service_map.clear();
-    return;
+  if (m & PM_SW_NAME) {
+    const std::string name = xml_inner(line);
+    f.len = (uint16_t)std::min<size_t>(name.size(), 0xffff);
+    f.ref = T.put(std::string_view(name).substr(0, f.len));
+    f.flags |= AF_SRC_HOST;
+    f.h_sw = hash_bytes(name.data(), name.size());
+    if (!icontains(name, "Provider[")) f.flags |= AF_TO_DB;
+  } else if (m & (PM_SW_STARTTS | PM_SW_STOPTS)) {
+    double v = js::nan();
+    if (js::convert_date(xml_inner(line), cfg_.tz, v)) f.ts = v;
+    else f.flags |= AF_TS_EMPTY;
   }
-  if (m & PM_SW_NAME) { ctx.active_service = xml_inner(line); ctx.has_active_service = true; return; }
-  if (!ctx.has_active_service || ctx.active_service.empty()) return;
-  const std::string& svcname = ctx.active_service;
-  auto f = std::find_if(ctx.service_map.begin(), ctx.service_map.end(), [&](auto& q) { return q.first == svcname; });
-  if (m & PM_SW_STARTTS) {
-    if (f == ctx.service_map.end() || f->second.empty()) { ++T.audit_errors; return; }
-    f->second.front().has_start = true;
-    f->second.front().start_ts = xml_inner(line);
-    return;
-  }
-  if (m & PM_SW_STOPTS) {
-    const std::string end_ts = xml_inner(line);
-    if (f == ctx.service_map.end() || f->second.empty()) { ++T.audit_errors; return; }
-    const AuditItem obj = f->second.front();
-    f->second.pop_front();
-    const std::string& log_id = ctx.active_log_id;
-    double s_ms = js::nan(), e_ms = js::nan();
-    const bool s_empty = !obj.has_start || !js::convert_date(obj.start_ts, cfg_.tz, s_ms);
-    const bool e_empty = !js::convert_date(end_ts, cfg_.tz, e_ms);
-    JOp op = blank_op(e, server);
-    op.op = JOP_AUDIT_TX;
-    op.gkey = dj::gkey_of(hash_bytes(log_id.data(), log_id.size()), server);
-    op.svc = hash_bytes(svcname.data(), svcname.size(), kHashSeed);
-    op.ts = e_ms;
-    op.num = js::parse_int(obj.elapsed);
-    op.aux = s_ms;
-    op.aux2 = ctx.active_alt.empty() ? js::nan() : js::parse_int(ctx.active_alt);
-    op.flags = JF_HAS_SVC | JF_SVC_HOST | JF_LID_HOST | (s_empty ? JF_START_EMPTY : 0) | (e_empty ? JF_TS_EMPTY : 0) |
-               (icontains(svcname, "Provider[") ? 0 : JF_TO_DB);
-    op.svc_ref = T.put(svcname);
-    op.svc_len = (uint16_t)svcname.size();
-    op.lid = T.put(log_id);
-    op.lid_len = (uint16_t)std::min<size_t>(log_id.size(), 0xffff);
-    push(op);
-  }
+  done();
 }
 
 // ---------------------------------------------------------------------------- registration
@@ -598,6 +568,11 @@ void DeviceJoin::register_misses(const uint8_t* hb, uint32_t n_miss, hipStream_t
     std::string raw = (m.flags & JF_EJB) ? "S:" : "";
     if (m.flags & JF_SVC_UNDEF) raw += "undefined";
     else if (m.flags & JF_SVC_HOST) raw.append(hbuf_.data() + m.name, m.name_len);
+    else if (m.flags & JF_SVC_AUD) {  // a carried stopWatch name (rare: new service, block across batches)
+      std::string b(m.name_len, '\0');
+      if (m.name_len) HIP_OK(hipMemcpy(&b[0], aud_gen_[aud_cur_].txt + m.name, m.name_len, hipMemcpyDeviceToHost));
+      raw += b;
+    }
     else raw.append((const char*)hb + m.name, m.name_len);
     const std::string norm = normalize_service(raw);
     if ((uint32_t)n >= cfg_.max_raw) throw std::runtime_error("device join: more raw services than gpu.maxRawServices");
@@ -736,6 +711,30 @@ void DeviceJoin::grow_arena(uint32_t new_cap, uint64_t lo) {
   ++arena_grows_;
 }
 
+// Capacity of an audit carry generation about to be written (its contents are not kept): every
+// array grows to twice the bound so growth is rare; frees wait for the join stream.
+void DeviceJoin::aud_reserve(AudGen& g, uint32_t autr, uint32_t items, uint64_t txt) {
+  if (txt >= (1ull << 31)) throw std::runtime_error("device join: audit carry text beyond 2 GB");
+  const bool grow = autr > g.cap_autr || items > g.cap_items || txt > g.cap_txt;
+  if (!grow) return;
+  HIP_OK(hipStreamSynchronize(stream_));
+  if (autr > g.cap_autr) {
+    dfree(g.autr, (size_t)g.cap_autr * sizeof(AutrEnt));
+    g.cap_autr = std::max<uint32_t>(autr * 2, 4096);
+    g.autr = (AutrEnt*)dmalloc((size_t)g.cap_autr * sizeof(AutrEnt));
+  }
+  if (items > g.cap_items) {
+    dfree(g.items, (size_t)g.cap_items * sizeof(AudItem));
+    g.cap_items = std::max<uint32_t>(items * 2, 16384);
+    g.items = (AudItem*)dmalloc((size_t)g.cap_items * sizeof(AudItem));
+  }
+  if (txt > g.cap_txt) {
+    dfree(g.txt, g.cap_txt);
+    g.cap_txt = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(txt * 2, 1u << 20), (1ull << 32) - 1);
+    g.txt = (char*)dmalloc(g.cap_txt);
+  }
+}
+
 uint64_t DeviceJoin::pool_avail(bool exact) {
   if (exact) {
     HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost, stream_));
@@ -791,7 +790,7 @@ void DeviceJoin::ensure_capacity(uint32_t n_ev, uint64_t bytes, double now) {
 void DeviceJoin::prepass_ahead(int k, const uint8_t* hb, const ParallelFor& parallel) {
   if (ahead_k_ >= 0) throw std::runtime_error("device join: a pre-pass is already ahead");
   // hops_ / hbuf_ hold the running batch's ops (register_misses reads hbuf_ after sync A)
-  host_prepass(k, hb, *sl_[k].h_n_host, parallel, hops_ahead_, hbuf_ahead_);
+  host_prepass(k, hb, sl_[k].h_n_host->host, parallel, hops_ahead_, hbuf_ahead_);
   ahead_k_ = k;
 }
 
@@ -810,7 +809,7 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
     ahead_k_ = -1;
   } else {
     if (ahead_k_ >= 0) throw std::runtime_error("device join: pre-pass ahead for another slot");
-    host_prepass(k, hb, *s.h_n_host, parallel, hops_, hbuf_);
+    host_prepass(k, hb, s.h_n_host->host, parallel, hops_, hbuf_);
   }
   phase_t[1] = clock_ms();
   spans.clear();
@@ -921,9 +920,54 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
   a.exp_idx_sorted = d_exp_idx_sorted_; a.exp_cnt = d_exp_cnt_; a.exp_pos = d_exp_pos_;
   a.out_cnt = d_out_cnt_; a.out_pos = d_out_pos_; a.stage = d_stage_; a.ovf = d_ovf_;
   a.out = d_out_; a.out_cap = out_cap_; a.counts = d_counts_;
+  // ---- audit trail (K5): this batch reads generation aud_cur_, writes the other one
+  {
+    const SelCount tot = *s.h_n_host;
+    AudGen& gin = aud_gen_[aud_cur_];
+    AudGen& gout = aud_gen_[aud_cur_ ^ 1];
+    aud_reserve(gout, gin.n_autr + tot.mh, gin.n_items + tot.walk, (uint64_t)gin.n_txt + tot.aud_bytes);
+    const uint32_t N = gin.n_autr + tot.mh;
+    if (N + 1 > aud_key_cap_) {
+      HIP_OK(hipStreamSynchronize(st));
+      for (void* p : {(void*)d_aud_key_, (void*)d_aud_key_sorted_}) dfree(p, (size_t)aud_key_cap_ * 8);
+      for (void* p : {(void*)d_aud_ord_, (void*)d_aud_ord_sorted_}) dfree(p, (size_t)aud_key_cap_ * 4);
+      aud_key_cap_ = std::max<uint32_t>(2 * (N + 1), 1u << 14);
+      d_aud_key_ = (uint64_t*)dmalloc((size_t)aud_key_cap_ * 8);
+      d_aud_key_sorted_ = (uint64_t*)dmalloc((size_t)aud_key_cap_ * 8);
+      d_aud_ord_ = (uint32_t*)dmalloc((size_t)aud_key_cap_ * 4);
+      d_aud_ord_sorted_ = (uint32_t*)dmalloc((size_t)aud_key_cap_ * 4);
+    }
+    if (N > std::max<uint32_t>(cfg_.max_events, cfg_.arena_cap)) {  // the key sort's scratch
+      const size_t need = apm_dj_tmp_bytes(N, out_cap_, table_bits_);
+      if (need > tmp_bytes_) {
+        HIP_OK(hipStreamSynchronize(st));
+        dfree(d_tmp_, tmp_bytes_);
+        tmp_bytes_ = need;
+        d_tmp_ = dmalloc(tmp_bytes_);
+        a.tmp = d_tmp_; a.tmp_bytes = tmp_bytes_;
+      }
+    }
+    const uint32_t slots = tot.walk + gin.n_items;
+    if (slots > aud_slots_cap_) {
+      HIP_OK(hipStreamSynchronize(st));
+      dfree(d_aud_slots_, (size_t)aud_slots_cap_ * sizeof(AudItem));
+      aud_slots_cap_ = std::max<uint32_t>(2 * slots, 1u << 14);
+      d_aud_slots_ = (AudItem*)dmalloc((size_t)aud_slots_cap_ * sizeof(AudItem));
+    }
+    a.n_mh = tot.mh; a.n_walk = tot.walk; a.n_files = (uint32_t)files_->size();
+    a.aud = d_aud_; a.gin = gin; a.gout = gout;
+    a.mh_idx = s.d_mh_idx; a.walk_idx = s.d_walk_idx;
+    a.aud_key = d_aud_key_; a.aud_key_sorted = d_aud_key_sorted_; a.aud_ord = d_aud_ord_; a.aud_ord_sorted = d_aud_ord_sorted_;
+    a.walk_lo = d_walk_lo_; a.file_first_chunk = d_file_first_; a.aud_slots = d_aud_slots_;
+  }
   // the stats thread is done with the slot's hand-off arrays (after the capacity upkeep, which
   // may synchronize this stream and must not wait for the stats thread)
   if (s.used) HIP_OK(hipStreamWaitEvent(st, s.free_ev, 0));
+  static const bool dbg = std::getenv("APM_DJ_DEBUG") != nullptr;
+  if (dbg) {  // (see devjoin.hip dj_check): the uploads before the join kernels
+    const hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) { fprintf(stderr, "[devjoin debug] before the join: %s\n", hipGetErrorString(e)); abort(); }
+  }
   phase_t[2] = clock_ms();
   if (apm_dj_join(&a, st) != 0) throw std::runtime_error("device join: scan scratch too small");
   HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost, st));
@@ -933,6 +977,11 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
   phase_t[4] = clock_ms();
   const JoinCounts c = *h_counts_;
   if (c.n_out > out_cap_) throw std::runtime_error("device join: more tx in one batch than the output capacity");
+  if (c.aud_pad) throw std::runtime_error("device join: audit carry over capacity (sizing bug)");
+  {
+    AudGen& gout = aud_gen_[aud_cur_ ^ 1];
+    gout.n_autr = c.aud_autr_n; gout.n_items = c.aud_items_n; gout.n_txt = c.aud_txt_n;
+  }
   if (c.pad[0] > DJ_OVF_CAP) throw std::runtime_error("device join: output overflow list full");
   if (c.n_need_new) {
     const uint32_t cnt = std::min(c.n_need_new, arena_limit);
@@ -947,7 +996,7 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
   f = DJFormatArgs{};
   f.out = d_out_; f.n_out = c.n_out; f.reg = d_reg_; f.reg_mask = (1u << cfg_.reg_bits) - 1;
   f.raw = d_rawtab_; f.raw_series = d_raw_series_; f.raw_first = d_raw_first_; f.names = d_names_;
-  f.bytes = s.d_bytes; f.hbuf = d_hbuf_; f.arena = d_arena_; f.arena_cap = cfg_.arena_cap; f.pool = d_pool_;
+  f.bytes = s.d_bytes; f.hbuf = d_hbuf_; f.aud_txt = aud_gen_[aud_cur_].txt; f.arena = d_arena_; f.arena_cap = cfg_.arena_cap; f.pool = d_pool_;
   f.lens = d_lens_; f.offs = d_offs_; f.ring = d_ring_; f.ring_cap = cfg_.ring_bytes;
   f.tx = s.d_tx; f.tx_raw = s.d_tx_raw; f.tx_gid = s.d_tx_gid; f.tx_bucket = d_bucket_; f.tx_bmax = d_bmax_;
   f.cand = d_cand_; f.cand_bucket = d_cand_bucket_; f.unresolved = d_unres_;
@@ -1023,6 +1072,7 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
   if (want_db) out.text_db.assign(h_txt_ + (want_tx ? c2.tx_text_bytes : 0), c2.db_text_bytes);
   tx_ += c3.n_out;
   tx_db_ += c3.n_db;
+  aud_cur_ ^= 1;  // the next batch reads what this one carried
   phase_t[8] = clock_ms();
 }
 
@@ -1036,8 +1086,8 @@ JoinCounters DeviceJoin::counters() const {
   t.need_expired = c.need_expired;
   t.ejb_exit_unmatched = c.ejb_unmatched;
   t.invalid_acct = c.invalid_acct + host_invalid_acct_;
-  t.audit_errors = audit_errors_;
-  t.host_fallback = host_pm_;  // lines the parser deferred (audit lines are host-resolved by design)
+  t.audit_errors = audit_errors_ + c.audit_errors;
+  t.host_fallback = host_pm_;  // lines the parser deferred (and audit lines whose fields the GPU could not read)
   t.partial_overflow = c.partial_overflow;
   t.need_overflow = c.need_overflow;
   t.table_full = c.table_full;
@@ -1145,21 +1195,22 @@ void DeviceJoin::save(BinWriter& w) {
     for (int32_t i = 0; i < n; ++i) top[i] = h_rawtab_[i].toplevel;
     w.vec(top);
   }
-  // audit-trail contexts (per file)
-  w.pod<uint64_t>(audit_.size());
-  for (auto& kv : audit_) {
-    const AuditCtx& c = kv.second;
-    w.pod(kv.first);
-    w.pod<uint64_t>(c.autr_map.size());
-    for (auto& a : c.autr_map) { w.str(a.first); w.str(a.second.first); w.str(a.second.second); }
-    w.pod(c.active); w.str(c.active_log_id); w.str(c.active_alt); w.str(c.active_service);
-    w.pod(c.has_active_service); w.pod(c.elapsed_flag); w.pod(c.sw_flag);
-    w.pod<uint64_t>(c.service_map.size());
-    for (auto& sm : c.service_map) {
-      w.str(sm.first);
-      w.pod<uint64_t>(sm.second.size());
-      for (auto& it : sm.second) { w.str(it.elapsed); w.pod(it.has_start); w.str(it.start_ts); }
-    }
+  // audit trail (K5): the carry generation the next batch reads
+  {
+    const AudGen& g = aud_gen_[aud_cur_];
+    const uint32_t nf = (uint32_t)files_->size();
+    std::vector<AudCarry> carry(nf);
+    std::vector<AutrEnt> autr(g.n_autr);
+    std::vector<AudItem> items(g.n_items);
+    std::string txt(g.n_txt, '\0');
+    if (nf) HIP_OK(hipMemcpy(carry.data(), g.carry, (size_t)nf * sizeof(AudCarry), hipMemcpyDeviceToHost));
+    if (g.n_autr) HIP_OK(hipMemcpy(autr.data(), g.autr, (size_t)g.n_autr * sizeof(AutrEnt), hipMemcpyDeviceToHost));
+    if (g.n_items) HIP_OK(hipMemcpy(items.data(), g.items, (size_t)g.n_items * sizeof(AudItem), hipMemcpyDeviceToHost));
+    if (g.n_txt) HIP_OK(hipMemcpy(&txt[0], g.txt, g.n_txt, hipMemcpyDeviceToHost));
+    w.vec(carry);
+    w.vec(autr);
+    w.vec(items);
+    w.str(txt);
   }
 }
 
@@ -1297,28 +1348,25 @@ void DeviceJoin::load(BinReader& rd) {
     names_uploaded_ = names_.size();
     n_raw_.store((int32_t)ri.size(), std::memory_order_release);
   }
-  audit_.clear();
-  for (uint64_t n = rd.pod<uint64_t>(); n; --n) {
-    const int32_t f = rd.pod<int32_t>();
-    AuditCtx& c = audit_[f];
-    for (uint64_t k = rd.pod<uint64_t>(); k; --k) {
-      std::string a = rd.str(), b = rd.str(), d = rd.str();
-      c.autr_map.push_back({a, {b, d}});
-    }
-    rd.pod(c.active); c.active_log_id = rd.str(); c.active_alt = rd.str(); c.active_service = rd.str();
-    rd.pod(c.has_active_service); rd.pod(c.elapsed_flag); rd.pod(c.sw_flag);
-    for (uint64_t k = rd.pod<uint64_t>(); k; --k) {
-      std::string name = rd.str();
-      std::deque<AuditItem> q;
-      for (uint64_t j = rd.pod<uint64_t>(); j; --j) {
-        AuditItem it;
-        it.elapsed = rd.str();
-        rd.pod(it.has_start);
-        it.start_ts = rd.str();
-        q.push_back(it);
-      }
-      c.service_map.push_back({name, q});
-    }
+  {
+    auto carry = rd.vec<AudCarry>();
+    auto autr = rd.vec<AutrEnt>();
+    auto items = rd.vec<AudItem>();
+    const std::string txt = rd.str();
+    if (carry.size() > soap_cap_) throw std::runtime_error("checkpoint: too many files");
+    HIP_OK(hipStreamSynchronize(st));
+    aud_cur_ = 0;
+    AudGen& g = aud_gen_[0];
+    aud_reserve(g, (uint32_t)autr.size(), (uint32_t)items.size(), txt.size());
+    HIP_OK(hipMemset(g.carry, 0, (size_t)soap_cap_ * sizeof(AudCarry)));
+    HIP_OK(hipMemset(aud_gen_[1].carry, 0, (size_t)soap_cap_ * sizeof(AudCarry)));
+    if (!carry.empty()) HIP_OK(hipMemcpy(g.carry, carry.data(), carry.size() * sizeof(AudCarry), hipMemcpyHostToDevice));
+    if (!autr.empty()) HIP_OK(hipMemcpy(g.autr, autr.data(), autr.size() * sizeof(AutrEnt), hipMemcpyHostToDevice));
+    if (!items.empty()) HIP_OK(hipMemcpy(g.items, items.data(), items.size() * sizeof(AudItem), hipMemcpyHostToDevice));
+    if (!txt.empty()) HIP_OK(hipMemcpy(g.txt, txt.data(), txt.size(), hipMemcpyHostToDevice));
+    g.n_autr = (uint32_t)autr.size();
+    g.n_items = (uint32_t)items.size();
+    g.n_txt = (uint32_t)txt.size();
   }
   files_uploaded_ = 0;
   HIP_OK(hipStreamSynchronize(st));

@@ -3,9 +3,10 @@
 // Per batch (ingest thread):
 //   1. the parse stream selects the events the GPU does not resolve alone (apm_dj_select_host)
 //      and copies them to pinned memory with the parse counts;
-//   2. host pre-pass (this file): the audit-trail state machine (parseAppLine :578-731) and the
-//      field re-derivation of PM_HOST lines become HostOps (sorted by event);
-//   3. join kernels (ops, SOAP scan, grouping, expiry, group walk, placement)      -> sync A;
+//   2. host pre-pass (this file): the field re-derivation of PM_HOST lines (and of audit lines
+//      the GPU cannot read alone) becomes HostOps (sorted by event);
+//   3. join kernels (ops, audit trail K5, SOAP scan, grouping, expiry, group walk, placement)
+//                                                                                   -> sync A;
 //   4. new (server, raw service) names are interned on the host and the registry updated;
 //   5. resolve + line lengths + scans                                              -> sync B;
 //   6. tx text into the HBM ring, stats hand-off arrays, rollover candidates       -> sync C.
@@ -83,7 +84,7 @@ class DeviceJoin {
            const std::function<void()>* meanwhile = nullptr);
   // the host pre-pass of the NEXT batch (slot k, its parse finished), run on another thread while
   // this batch's join completes; run(k) then uploads its ops instead of doing the pre-pass
-  // itself.  The audit state is host-only and advanced in batch order, so the result is the same.
+  // itself.  The pre-pass is stateless (field derivation only), so the result is the same.
   // The caller orders it: run(k) starts only after prepass_ahead(k) returned.
   void prepass_ahead(int k, const uint8_t* host_bytes, const ParallelFor& parallel);
   // the stats thread finished with slot k's arrays (event recorded on its stream)
@@ -111,7 +112,7 @@ class DeviceJoin {
   JoinCounters counters() const;
 
   // checkpoint of the GPU join state (checkpoint.cpp): key table (live entries), need arena
-  // (live regions), SOAP contexts, service registry, audit contexts, counters
+  // (live regions), SOAP contexts, service registry, audit-trail carry, counters
   void save(class BinWriter& w);
   void load(class BinReader& r);
   // phase boundaries of the last run() (steady-clock ms): prepass, join launched, sync A,
@@ -127,13 +128,14 @@ class DeviceJoin {
     uint8_t* d_bytes = nullptr;
     Event* d_events = nullptr;
     uint8_t* host_flag = nullptr;
-    uint32_t* host_pos = nullptr;
     Event* d_host_ev = nullptr;
     uint32_t* d_host_idx = nullptr;
-    uint32_t* d_n_host = nullptr;
+    uint32_t* d_mh_idx = nullptr;      // audit map / header events
+    uint32_t* d_walk_idx = nullptr;    // audit block-walk events
+    SelCount* d_n_host = nullptr;
     Event* h_host_ev = nullptr;        // pinned
     uint32_t* h_host_idx = nullptr;    // pinned
-    uint32_t* h_n_host = nullptr;      // pinned
+    SelCount* h_n_host = nullptr;      // pinned
     uint32_t spec = 0;                 // host events already copied speculatively
     int32_t* d_chunk_next = nullptr;
     uint8_t* d_chunk_first = nullptr;
@@ -151,21 +153,12 @@ class DeviceJoin {
     bool used = false;
   } sl_[2];
 
-  struct AuditItem { std::string elapsed; bool has_start = false; std::string start_ts; };
-  struct AuditCtx {
-    std::vector<std::pair<std::string, std::pair<std::string, std::string>>> autr_map;
-    bool active = false;
-    std::string active_log_id, active_alt, active_service;
-    bool has_active_service = false, elapsed_flag = false, sw_flag = false;
-    std::vector<std::pair<std::string, std::deque<AuditItem>>> service_map;
-  };
   struct RawInfo { int32_t server; int32_t norm_id; uint64_t svc; };
 
   void* dmalloc(size_t bytes);
-  // One file's share of the host pre-pass (files are independent: the audit context is per file)
+  // One file's share of the host pre-pass (field re-derivation of the lines of one file)
   struct PrepassTask {
     int32_t file = -1;
-    AuditCtx* ctx = nullptr;
     std::vector<uint32_t> idx;   // host-event indices (ascending)
     std::vector<HostOp> hops;
     std::string hbuf;
@@ -175,7 +168,9 @@ class DeviceJoin {
   void host_prepass(int k, const uint8_t* host_bytes, uint32_t n_host, const ParallelFor& parallel,
                     std::vector<HostOp>& hops, std::string& hbuf);
   void host_event(PrepassTask& t, const Event& e, uint32_t ev, const uint8_t* host_bytes);
-  void on_app(PrepassTask& t, const Event& e, uint32_t ev, std::string_view line, int32_t server);
+  void on_app(PrepassTask& t, const Event& e, uint32_t ev, std::string_view line);
+  // K5 carry: generation g of the audit state (devjoin_api.h AudGen); capacity for the next batch
+  void aud_reserve(AudGen& g, uint32_t autr, uint32_t items, uint64_t txt);
   int32_t intern_name(const std::string& s);
   void register_misses(const uint8_t* host_bytes, uint32_t n_miss, hipStream_t s);
   // Capacity before a batch of n_ev events (`bytes` of lines + host-op bytes): the key table keeps
@@ -224,7 +219,6 @@ class DeviceJoin {
   HostOp* d_hops_ = nullptr;
   uint8_t* d_hbuf_ = nullptr;
   size_t d_hops_cap_ = 0, d_hbuf_cap_ = 0;
-  std::unordered_map<int32_t, AuditCtx> audit_;
   std::vector<PrepassTask> tasks_;
   uint32_t last_host_ = 0;
   void* d_sel_tmp_ = nullptr;  // rocprim scratch of the host-event selection (parse stream)
@@ -257,6 +251,20 @@ class DeviceJoin {
   uint64_t* d_exp_hi_ = nullptr;
   uint64_t* h_exp_ = nullptr;    // pinned [2][64]
   SoapState* d_soap_ = nullptr;
+  // audit trail (K5): carry generations (batch k reads aud_gen_[aud_cur_], writes the other),
+  // per-event fields, key sort, walk tables
+  AudGen aud_gen_[2]{};
+  int aud_cur_ = 0;
+  AudF* d_aud_ = nullptr;
+  SelCount* d_sel_val_ = nullptr;  // selection scan (parse stream, one batch at a time)
+  SelCount* d_sel_pos_ = nullptr;
+  uint64_t *d_aud_key_ = nullptr, *d_aud_key_sorted_ = nullptr;
+  uint32_t *d_aud_ord_ = nullptr, *d_aud_ord_sorted_ = nullptr;
+  uint32_t aud_key_cap_ = 0;
+  uint32_t* d_walk_lo_ = nullptr;
+  int32_t* d_file_first_ = nullptr;
+  AudItem* d_aud_slots_ = nullptr;
+  uint32_t aud_slots_cap_ = 0;
   uint32_t soap_cap_ = 0;
   int32_t* d_file_server_ = nullptr;
   size_t files_uploaded_ = 0;
