@@ -56,26 +56,6 @@ __device__ __forceinline__ void trim_ascii(const uint8_t* p, int& a, int& b) {
   while (b > a && ws_ascii(p[b - 1])) --b;
 }
 
-// k-th token of line.split(/[\s]+/) (a leading '' when the line starts with whitespace)
-__device__ void split_tok(const uint8_t* p, int len, int k, int& s, int& e) {
-  int idx = 0, ts = 0;
-  bool in_ws = false;
-  for (int i = 0; i < len; ++i) {
-    if (ws_ascii(p[i])) {
-      if (!in_ws) {
-        if (idx == k) { s = ts; e = i; return; }
-        ++idx;
-        in_ws = true;
-      }
-      ts = i + 1;
-    } else {
-      in_ws = false;
-    }
-  }
-  if (idx == k) { s = ts; e = len; return; }
-  s = e = -1;  // no such token
-}
-
 // parseInt of [a, b) with every '[' / ']' removed (whitespace-free); false: the host decides
 __device__ bool parse_int_nobr(const uint8_t* p, int a, int b, double& out) {
   uint8_t buf[24];
@@ -143,14 +123,6 @@ __device__ int aud_date(const uint8_t* p, int a, int b, double& out) {
   return 0;
 }
 
-// line.replace(/<\/.*/,'').replace(/.*>/,'') -> [s, e)
-__device__ __forceinline__ void xml_inner_dev(const uint8_t* p, int len, int& s, int& e) {
-  e = len;
-  for (int i = 0; i + 1 < len; ++i) if (p[i] == '<' && p[i + 1] == '/') { e = i; break; }
-  s = 0;
-  for (int i = 0; i < e; ++i) if (p[i] == '>') s = i + 1;
-}
-
 __device__ bool icontains_provider(const uint8_t* p, int a, int b) {
   const char* pat = "provider[";
   for (int i = a; i + 9 <= b; ++i) {
@@ -165,18 +137,80 @@ __device__ bool icontains_provider(const uint8_t* p, int a, int b) {
   return false;
 }
 
+// One pass over a line, 16 bytes per aligned load (the byte loops of the first version cost
+// ~350 us per batch in dependent loads): non-ASCII, the first two ':' , split(/\s+/) tokens
+// 0..5, the '=' of token 5, the first "</" and the last '>' before it.
+struct LineScan {
+  bool nonascii;
+  int c1, c2;           // first ':' (-1), the next ':' after it (len)
+  int ts[6], te[6];     // tokens 0..5 of line.split(/[\s]+/) (ts -1: no such token)
+  int eq1, eq2;         // first '=' of token 5 (-1), the next '=' (token end)
+  int lt, gt;           // first "</" (len), last '>' before it (-1)
+};
+
+__device__ void line_scan(const uint8_t* __restrict__ p, int len, LineScan& L) {
+  L.nonascii = false;
+  L.c1 = -1; L.c2 = len;
+  for (int k = 0; k < 6; ++k) L.ts[k] = L.te[k] = -1;
+  L.eq1 = L.eq2 = -1;
+  L.lt = len; L.gt = -1;
+  int tok = 0, tstart = 0;  // current token index / its start
+  bool in_ws = false, lt_found = false;
+  uint8_t prev = 0;
+  const uintptr_t a0 = (uintptr_t)p & ~(uintptr_t)15;
+  const int lead = (int)((uintptr_t)p - a0);
+  for (int base = -lead; base < len; base += 16) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p + base);
+    const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int i = base + j;
+      if (i < 0 || i >= len) continue;
+      const uint8_t c = (uint8_t)(w4[j >> 2] >> (8 * (j & 3)));
+      L.nonascii |= c >= 0x80;
+      if (c == ':') {
+        if (L.c1 < 0) L.c1 = i;
+        else if (L.c2 == len) L.c2 = i;
+      }
+      if (!lt_found) {
+        if (prev == '<' && c == '/') { L.lt = i - 1; lt_found = true; }
+        else if (c == '>') L.gt = i;
+      }
+      if (ws_ascii(c)) {
+        if (!in_ws) {
+          if (tok < 6) { L.ts[tok] = tstart; L.te[tok] = i; }
+          ++tok;
+          in_ws = true;
+        }
+        tstart = i + 1;
+      } else {
+        in_ws = false;
+        if (tok == 5 && c == '=') {
+          if (L.eq1 < 0) L.eq1 = i + 1;
+          else if (L.eq2 < 0) L.eq2 = i;
+        }
+      }
+      prev = c;
+    }
+  }
+  if (tok < 6) { L.ts[tok] = tstart; L.te[tok] = len; }
+  if (L.eq1 >= 0 && L.eq2 < 0) L.eq2 = L.te[5];
+  if (lt_found && L.gt >= L.lt) L.gt = -1;  // ('>' at the "</" itself is after it)
+}
+
 // The AudF of an LK_APP event (batch-absolute refs); false when the host must derive it.
 __device__ bool aud_fields(const Event& e, const uint8_t* __restrict__ bytes, int32_t file, AudF& f) {
   const uint8_t* p = bytes + e.off;
   const int len = (int)e.len;
   f.h_item = 0; f.el = apm_nan(); f.h_sw = 0; f.ts = apm_nan();
   f.ref = 0; f.len = 0; f.flags = 0; f.pad = 0; f.pad2[0] = f.pad2[1] = 0;
-  for (int i = 0; i < len; ++i) if (p[i] >= 0x80) return false;
+  LineScan L;
+  line_scan(p, len, L);
+  if (L.nonascii) return false;
   const uint32_t m = e.mask;
   if (m & PM_AUTR_MAP) {
     // logId = ws[0] without brackets; auditTrailId = ws[5].split('=')[1]; alt = the BAF account
-    int s0, e0;
-    split_tok(p, len, 0, s0, e0);
+    int s0 = L.ts[0], e0 = L.te[0];
     if (s0 < 0) { s0 = e0 = 0; }
     if (s0 < e0 && p[s0] == '[') ++s0;
     if (e0 > s0 && p[e0 - 1] == ']') --e0;
@@ -184,43 +218,25 @@ __device__ bool aud_fields(const Event& e, const uint8_t* __restrict__ bytes, in
     f.ref = e.off + (uint32_t)s0;
     f.len = (uint16_t)(e0 - s0);
     f.h_sw = hash_bytes(p + s0, (size_t)(e0 - s0));
-    int s5, e5;
-    split_tok(p, len, 5, s5, e5);
-    uint64_t ah;
-    int q = -1;
-    if (s5 >= 0) for (int i = s5; i < e5; ++i) if (p[i] == '=') { q = i + 1; break; }
-    if (q < 0) {
-      ah = hash_bytes("undefined", 9);
-    } else {
-      int r = e5;
-      for (int i = q; i < e5; ++i) if (p[i] == '=') { r = i; break; }
-      ah = hash_bytes(p + q, (size_t)(r - q));
-    }
+    const uint64_t ah = L.eq1 < 0 ? hash_bytes("undefined", 9) : hash_bytes(p + L.eq1, (size_t)(L.eq2 - L.eq1));
     f.h_item = aud_key(ah, file);
-    if (m & PM_BAF) {
-      int s3, e3;
-      split_tok(p, len, 3, s3, e3);
-      if (s3 >= 0 && e3 > s3) {
-        uint8_t acct[64];
-        const int n = baf_account(p, s3, e3, acct);
-        if (n < 0) return false;
-        if (n > 0) {
-          double v;
-          if (!simple_parse_int(acct, n, v)) return false;
-          f.el = v;
-          f.flags |= AF_ACCT;
-          if (all_digits(acct, n)) f.flags |= AF_ACCT_VALID;
-        }
+    if ((m & PM_BAF) && L.ts[3] >= 0 && L.te[3] > L.ts[3]) {
+      uint8_t acct[64];
+      const int n = baf_account(p, L.ts[3], L.te[3], acct);
+      if (n < 0) return false;
+      if (n > 0) {
+        double v;
+        if (!simple_parse_int(acct, n, v)) return false;
+        f.el = v;
+        f.flags |= AF_ACCT;
+        if (all_digits(acct, n)) f.flags |= AF_ACCT_VALID;
       }
     }
     return true;
   }
   if (m & PM_AUTR_HDR) {  // line.split(':')[1].trim()
-    int c1 = -1, c2 = len;
-    for (int i = 0; i < len; ++i) if (p[i] == ':') { c1 = i; break; }
-    if (c1 < 0) return false;
-    for (int i = c1 + 1; i < len; ++i) if (p[i] == ':') { c2 = i; break; }
-    int a = c1 + 1, b = c2;
+    if (L.c1 < 0) return false;
+    int a = L.c1 + 1, b = L.c2;
     trim_ascii(p, a, b);
     f.h_item = aud_key(hash_bytes(p + a, (size_t)(b - a)), file);
     return true;
@@ -228,31 +244,27 @@ __device__ bool aud_fields(const Event& e, const uint8_t* __restrict__ bytes, in
   // item role (a line inside the elapsed section): service = split(':')[0].trim(),
   // elapsed = split(':')[1].split(/\s+/)[0] without brackets
   {
-    int c1 = -1, c2 = len;
-    for (int i = 0; i < len; ++i) if (p[i] == ':') { c1 = i; break; }
-    int a = 0, b = c1 >= 0 ? c1 : len;
+    int a = 0, b = L.c1 >= 0 ? L.c1 : len;
     trim_ascii(p, a, b);
     f.h_item = hash_bytes(p + a, (size_t)(b - a));
-    if (c1 >= 0) {
-      for (int i = c1 + 1; i < len; ++i) if (p[i] == ':') { c2 = i; break; }
-      int t = c1 + 1;
-      while (t < c2 && !ws_ascii(p[t])) ++t;
-      if (!parse_int_nobr(p, c1 + 1, t, f.el)) return false;
+    if (L.c1 >= 0) {
+      int t = L.c1 + 1;
+      while (t < L.c2 && !ws_ascii(p[t])) ++t;
+      if (!parse_int_nobr(p, L.c1 + 1, t, f.el)) return false;
     }
   }
-  if (m & PM_SW_NAME) {
-    int s, t;
-    xml_inner_dev(p, len, s, t);
-    f.ref = e.off + (uint32_t)s;
-    f.len = (uint16_t)(t - s);
-    f.h_sw = hash_bytes(p + s, (size_t)(t - s));
-    if (!icontains_provider(p, s, t)) f.flags |= AF_TO_DB;
-  } else if (m & (PM_SW_STARTTS | PM_SW_STOPTS)) {
-    int s, t;
-    xml_inner_dev(p, len, s, t);
-    const int r = aud_date(p, s, t, f.ts);
-    if (r < 0) return false;
-    if (r == 1) f.flags |= AF_TS_EMPTY;
+  if (m & (PM_SW_NAME | PM_SW_STARTTS | PM_SW_STOPTS)) {
+    const int t = L.lt, s = L.gt >= 0 ? L.gt + 1 : 0;  // line.replace(/<\/.*/,'').replace(/.*>/,'')
+    if (m & PM_SW_NAME) {
+      f.ref = e.off + (uint32_t)s;
+      f.len = (uint16_t)(t - s);
+      f.h_sw = hash_bytes(p + s, (size_t)(t - s));
+      if (!icontains_provider(p, s, t)) f.flags |= AF_TO_DB;
+    } else {
+      const int r = aud_date(p, s, t, f.ts);
+      if (r < 0) return false;
+      if (r == 1) f.flags |= AF_TS_EMPTY;
+    }
   }
   return true;
 }
@@ -262,12 +274,7 @@ __device__ bool aud_fields(const Event& e, const uint8_t* __restrict__ bytes, in
 // timestamps), logIds with inner brackets, account strings parseInt cannot decide in 64 bits,
 // and audit lines whose fields aud_fields cannot extract (the host sends those as HOP_AUD).
 __device__ bool needs_host(const Event& e, const uint8_t* __restrict__ bytes) {
-  if (e.kind == LK_APP) {
-    if (e.mask & PM_HOST) return true;
-    AudF f;
-    return !aud_fields(e, bytes, 0, f);
-  }
-  if (e.mask & PM_HOST) return true;
+  if (e.mask & PM_HOST) return true;  // (LK_APP events are decided by k_host_flags itself)
   const uint8_t* p = bytes + e.off;
   if (e.kind >= LK_EJB_ENTRY && e.kind <= LK_CT_EXIT) {
     if (!(e.mask & PM_KEYS) || e.ntok < 3) return true;
@@ -305,8 +312,11 @@ struct SelPlus {
   }
 };
 
+// Per event: host / audit-list flags and counts; the AudF of every audit line the GPU reads
+// (computed once here, on the parse stream, and read by the join's k_build_ops)
 __global__ void k_host_flags(const Event* __restrict__ ev, const uint32_t* __restrict__ n_ev_dev,
-                             const uint8_t* __restrict__ bytes, uint8_t* __restrict__ flag, SelCount* __restrict__ val,
+                             const uint8_t* __restrict__ bytes, const uint32_t* __restrict__ chunk_file,
+                             uint8_t* __restrict__ flag, SelCount* __restrict__ val, AudF* __restrict__ aud,
                              uint32_t cap) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cap) return;
@@ -315,7 +325,17 @@ __global__ void k_host_flags(const Event* __restrict__ ev, const uint32_t* __res
   uint32_t ab = 0;
   if (i < n) {
     const Event e = ev[i];
-    if (needs_host(e, bytes)) fl |= SEL_HOST;
+    if (e.kind == LK_APP) {
+      bool host = (e.mask & PM_HOST) != 0;
+      if (!host) {
+        AudF f;
+        host = !aud_fields(e, bytes, (int32_t)chunk_file[e.chunk], f);
+        if (!host) aud[i] = f;
+      }
+      if (host) fl |= SEL_HOST;
+    } else if (needs_host(e, bytes)) {
+      fl |= SEL_HOST;
+    }
     if (e.kind == LK_APP) {
       if (e.mask & PM_AUTR_MAP) fl |= SEL_MH;
       else fl |= SEL_WALK | ((e.mask & PM_AUTR_HDR) ? SEL_MH : 0);
@@ -376,13 +396,13 @@ __global__ void k_build_ops(DJArgs a) {
     if (a.host_flag[i] & SEL_HOST) {
       const HostOp* h = find_hop(a.hops, a.n_hops, i);
       if (h && h->kind == HOP_AUD) { f = *reinterpret_cast<const AudF*>(&h->op); ok = true; }
+      if (!ok) {  // (no host op: the line is ignored, as the host pre-pass would)
+        f.h_item = 0; f.el = apm_nan(); f.h_sw = 0; f.ts = apm_nan(); f.ref = 0; f.len = 0; f.flags = 0;
+      }
+      a.aud[i] = f;
     } else {
-      ok = aud_fields(e, a.bytes, file, f);
+      f = a.aud[i];  // k_host_flags derived it
     }
-    if (!ok) {  // (no host op: the line is ignored, as the host pre-pass would)
-      f.h_item = 0; f.el = apm_nan(); f.h_sw = 0; f.ts = apm_nan(); f.ref = 0; f.len = 0; f.flags = 0;
-    }
-    a.aud[i] = f;
     if ((e.mask & PM_AUTR_MAP) && (f.flags & AF_ACCT)) {
       if (!(f.flags & AF_ACCT_VALID)) {
         atomicAdd(&a.counts->invalid_acct, 1ULL);
@@ -1845,8 +1865,8 @@ size_t apm_dj_tmp_bytes(uint32_t max_ev, uint32_t max_out, int table_bits) {
 
 int apm_dj_select_host(DJArgs* a, const uint32_t* d_n_ev, uint32_t max_ev, hipStream_t s) {
   if (max_ev == 0) { HIP_OK(hipMemsetAsync(a->n_host, 0, sizeof(SelCount), s)); return 0; }
-  hipLaunchKernelGGL(k_host_flags, dim3((max_ev + TB - 1) / TB), dim3(TB), 0, s, a->ev, d_n_ev, a->bytes, a->host_flag,
-                     a->sel_val, max_ev);
+  hipLaunchKernelGGL(k_host_flags, dim3((max_ev + TB - 1) / TB), dim3(TB), 0, s, a->ev, d_n_ev, a->bytes, a->chunk_file,
+                     a->host_flag, a->sel_val, a->aud, max_ev);
   dj_check(s, "k_host_flags");
   size_t need = 0;
   HIP_OK(rocprim::exclusive_scan(nullptr, need, a->sel_val, a->sel_pos, SelCount{0, 0, 0, 0}, (size_t)max_ev, SelPlus(),

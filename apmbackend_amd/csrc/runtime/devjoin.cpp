@@ -91,6 +91,7 @@ DeviceJoin::DeviceJoin(const DevJoinConfig& cfg, Dictionary* dict, const std::ve
     s.d_host_idx = (uint32_t*)dmalloc((size_t)E * 4);
     s.d_mh_idx = (uint32_t*)dmalloc((size_t)E * 4);
     s.d_walk_idx = (uint32_t*)dmalloc((size_t)E * 4);
+    s.d_aud = (AudF*)dmalloc((size_t)E * sizeof(AudF));
     s.d_n_host = (SelCount*)dmalloc(64);
     HIP_OK(hipHostMalloc((void**)&s.h_host_ev, (size_t)E * sizeof(Event), hipHostMallocDefault));
     HIP_OK(hipHostMalloc((void**)&s.h_host_idx, (size_t)E * 4, hipHostMallocDefault));
@@ -119,7 +120,6 @@ DeviceJoin::DeviceJoin(const DevJoinConfig& cfg, Dictionary* dict, const std::ve
   HIP_OK(hipHostGetDevicePointer((void**)&hd_exp_, h_exp_, 0));
   soap_cap_ = 1u << 16;
   d_soap_ = (SoapState*)dmalloc((size_t)soap_cap_ * sizeof(SoapState));
-  d_aud_ = (AudF*)dmalloc((size_t)E * sizeof(AudF));
   d_sel_val_ = (SelCount*)dmalloc(((size_t)E + 64) * sizeof(SelCount));
   d_sel_pos_ = (SelCount*)dmalloc(((size_t)E + 64) * sizeof(SelCount));
   d_walk_lo_ = (uint32_t*)dmalloc(((size_t)cfg_.max_chunks + 2) * 4);
@@ -217,6 +217,8 @@ void DeviceJoin::select_host(int k, const uint32_t* d_n_ev, uint32_t max_ev, hip
   a.ev = s.d_events;
   a.bytes = s.d_bytes;
   a.host_flag = s.host_flag;
+  a.chunk_file = s.d_chunk_file;  // (set_chunks ran first)
+  a.aud = s.d_aud;
   a.sel_val = d_sel_val_;
   a.sel_pos = d_sel_pos_;
   a.host_ev = s.d_host_ev;
@@ -955,7 +957,7 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
       d_aud_slots_ = (AudItem*)dmalloc((size_t)aud_slots_cap_ * sizeof(AudItem));
     }
     a.n_mh = tot.mh; a.n_walk = tot.walk; a.n_files = (uint32_t)files_->size();
-    a.aud = d_aud_; a.gin = gin; a.gout = gout;
+    a.aud = s.d_aud; a.gin = gin; a.gout = gout;
     a.mh_idx = s.d_mh_idx; a.walk_idx = s.d_walk_idx;
     a.aud_key = d_aud_key_; a.aud_key_sorted = d_aud_key_sorted_; a.aud_ord = d_aud_ord_; a.aud_ord_sorted = d_aud_ord_sorted_;
     a.walk_lo = d_walk_lo_; a.file_first_chunk = d_file_first_; a.aud_slots = d_aud_slots_;

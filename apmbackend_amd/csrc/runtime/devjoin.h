@@ -132,6 +132,7 @@ class DeviceJoin {
     uint32_t* d_host_idx = nullptr;
     uint32_t* d_mh_idx = nullptr;      // audit map / header events
     uint32_t* d_walk_idx = nullptr;    // audit block-walk events
+    AudF* d_aud = nullptr;             // audit fields per event (parse-side selection writes them)
     SelCount* d_n_host = nullptr;
     Event* h_host_ev = nullptr;        // pinned
     uint32_t* h_host_idx = nullptr;    // pinned
@@ -255,7 +256,6 @@ class DeviceJoin {
   // per-event fields, key sort, walk tables
   AudGen aud_gen_[2]{};
   int aud_cur_ = 0;
-  AudF* d_aud_ = nullptr;
   SelCount* d_sel_val_ = nullptr;  // selection scan (parse stream, one batch at a time)
   SelCount* d_sel_pos_ = nullptr;
   uint64_t *d_aud_key_ = nullptr, *d_aud_key_sorted_ = nullptr;
