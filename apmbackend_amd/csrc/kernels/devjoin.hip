@@ -57,12 +57,23 @@ __device__ __forceinline__ void trim_ascii(const uint8_t* p, int& a, int& b) {
 }
 
 // parseInt of [a, b) with every '[' / ']' removed (whitespace-free); false: the host decides
+// (sign / hex prefix / more than 19 digits) -- simple_parse_int() without the copy
 __device__ bool parse_int_nobr(const uint8_t* p, int a, int b, double& out) {
-  uint8_t buf[24];
-  int n = 0;
-  for (int i = a; i < b && n < 21; ++i)
-    if (p[i] != '[' && p[i] != ']') buf[n++] = p[i];
-  return simple_parse_int(buf, n, out);
+  uint64_t x = 0;
+  int nd = 0, k = 0;
+  for (int i = a; i < b; ++i) {
+    const uint8_t ch = p[i];
+    if (ch == '[' || ch == ']') continue;
+    if (k == 0 && (ch == '+' || ch == '-')) return false;
+    if (k == 1 && nd == 1 && x == 0 && (ch == 'x' || ch == 'X')) return false;
+    ++k;
+    if (ch < '0' || ch > '9') break;
+    if (nd >= 19) return false;
+    x = x * 10 + (ch - '0');
+    ++nd;
+  }
+  out = nd == 0 ? apm_nan() : (double)x;
+  return true;
 }
 
 // convertStringDateToMs of [a, b): 1 = '' (empty input), 0 = `out` set (NaN if invalid),
@@ -143,17 +154,17 @@ __device__ bool icontains_provider(const uint8_t* p, int a, int b) {
 struct LineScan {
   bool nonascii;
   int c1, c2;           // first ':' (-1), the next ':' after it (len)
-  int ts[6], te[6];     // tokens 0..5 of line.split(/[\s]+/) (ts -1: no such token)
-  int eq1, eq2;         // first '=' of token 5 (-1), the next '=' (token end)
+  int t0s, t0e, t3s, t3e, t5s, t5e;  // tokens 0, 3, 5 of line.split(/[\s]+/) (start -1: none)
+  int eq1, eq2;         // first '=' of token 5 (+1; -1 none), the next '=' (token end if none)
   int lt, gt;           // first "</" (len), last '>' before it (-1)
 };
 
+// (scalars only: an indexed token array would live in scratch memory)
 __device__ void line_scan(const uint8_t* __restrict__ p, int len, LineScan& L) {
-  L.nonascii = false;
-  L.c1 = -1; L.c2 = len;
-  for (int k = 0; k < 6; ++k) L.ts[k] = L.te[k] = -1;
-  L.eq1 = L.eq2 = -1;
-  L.lt = len; L.gt = -1;
+  bool na = false;
+  int c1 = -1, c2 = len;
+  int t0s = -1, t0e = -1, t3s = -1, t3e = -1, t5s = -1, t5e = -1;
+  int eq1 = -1, eq2 = -1, lt = len, gt = -1;
   int tok = 0, tstart = 0;  // current token index / its start
   bool in_ws = false, lt_found = false;
   uint8_t prev = 0;
@@ -167,18 +178,20 @@ __device__ void line_scan(const uint8_t* __restrict__ p, int len, LineScan& L) {
       const int i = base + j;
       if (i < 0 || i >= len) continue;
       const uint8_t c = (uint8_t)(w4[j >> 2] >> (8 * (j & 3)));
-      L.nonascii |= c >= 0x80;
+      na |= c >= 0x80;
       if (c == ':') {
-        if (L.c1 < 0) L.c1 = i;
-        else if (L.c2 == len) L.c2 = i;
+        if (c1 < 0) c1 = i;
+        else if (c2 == len) c2 = i;
       }
       if (!lt_found) {
-        if (prev == '<' && c == '/') { L.lt = i - 1; lt_found = true; }
-        else if (c == '>') L.gt = i;
+        if (prev == '<' && c == '/') { lt = i - 1; lt_found = true; }
+        else if (c == '>') gt = i;
       }
       if (ws_ascii(c)) {
         if (!in_ws) {
-          if (tok < 6) { L.ts[tok] = tstart; L.te[tok] = i; }
+          if (tok == 0) { t0s = tstart; t0e = i; }
+          else if (tok == 3) { t3s = tstart; t3e = i; }
+          else if (tok == 5) { t5s = tstart; t5e = i; }
           ++tok;
           in_ws = true;
         }
@@ -186,16 +199,56 @@ __device__ void line_scan(const uint8_t* __restrict__ p, int len, LineScan& L) {
       } else {
         in_ws = false;
         if (tok == 5 && c == '=') {
-          if (L.eq1 < 0) L.eq1 = i + 1;
-          else if (L.eq2 < 0) L.eq2 = i;
+          if (eq1 < 0) eq1 = i + 1;
+          else if (eq2 < 0) eq2 = i;
         }
       }
       prev = c;
     }
   }
-  if (tok < 6) { L.ts[tok] = tstart; L.te[tok] = len; }
-  if (L.eq1 >= 0 && L.eq2 < 0) L.eq2 = L.te[5];
-  if (lt_found && L.gt >= L.lt) L.gt = -1;  // ('>' at the "</" itself is after it)
+  if (tok == 0) { t0s = tstart; t0e = len; }
+  else if (tok == 3) { t3s = tstart; t3e = len; }
+  else if (tok == 5) { t5s = tstart; t5e = len; }
+  if (eq1 >= 0 && eq2 < 0) eq2 = t5e;
+  L.nonascii = na; L.c1 = c1; L.c2 = c2;
+  L.t0s = t0s; L.t0e = t0e; L.t3s = t3s; L.t3e = t3e; L.t5s = t5s; L.t5e = t5e;
+  L.eq1 = eq1; L.eq2 = eq2; L.lt = lt; L.gt = gt;
+}
+
+// attemptReadAccountNumberFromBAFInfo on token 3 [a, b) without a copy: the token after the last
+// "][", brackets removed, after the last ':' (= baf_account()).  n = its length; digits = all
+// digits; v = parseInt; false: the host decides (sign / hex prefix / more than 19 digits).
+__device__ bool baf_account_scan(const uint8_t* p, int a, int b, int& n, bool& digits, double& v) {
+  int st = a;
+  for (int i = a; i + 1 < b; ++i) if (p[i] == ']' && p[i + 1] == '[') st = i + 2;
+  int c = st;
+  for (int i = st; i < b; ++i) if (p[i] == ':') c = i + 1;
+  n = 0;
+  digits = true;
+  uint64_t x = 0;
+  int nd = 0;
+  bool in_digits = true;  // the parseInt prefix is still running
+  for (int i = c; i < b; ++i) {
+    const uint8_t ch = p[i];
+    if (ch == '[' || ch == ']') continue;
+    const bool d = ch >= '0' && ch <= '9';
+    if (n == 0 && (ch == '+' || ch == '-')) return false;
+    if (n == 1 && nd == 1 && x == 0 && (ch == 'x' || ch == 'X')) return false;
+    digits &= d;
+    if (in_digits) {
+      if (d) {
+        if (nd >= 19) return false;
+        x = x * 10 + (ch - '0');
+        ++nd;
+      } else {
+        in_digits = false;
+      }
+    }
+    ++n;
+  }
+  v = nd == 0 ? apm_nan() : (double)x;
+  if (n == 0) digits = false;
+  return true;
 }
 
 // The AudF of an LK_APP event (batch-absolute refs); false when the host must derive it.
@@ -210,7 +263,7 @@ __device__ bool aud_fields(const Event& e, const uint8_t* __restrict__ bytes, in
   const uint32_t m = e.mask;
   if (m & PM_AUTR_MAP) {
     // logId = ws[0] without brackets; auditTrailId = ws[5].split('=')[1]; alt = the BAF account
-    int s0 = L.ts[0], e0 = L.te[0];
+    int s0 = L.t0s, e0 = L.t0e;
     if (s0 < 0) { s0 = e0 = 0; }
     if (s0 < e0 && p[s0] == '[') ++s0;
     if (e0 > s0 && p[e0 - 1] == ']') --e0;
@@ -220,16 +273,15 @@ __device__ bool aud_fields(const Event& e, const uint8_t* __restrict__ bytes, in
     f.h_sw = hash_bytes(p + s0, (size_t)(e0 - s0));
     const uint64_t ah = L.eq1 < 0 ? hash_bytes("undefined", 9) : hash_bytes(p + L.eq1, (size_t)(L.eq2 - L.eq1));
     f.h_item = aud_key(ah, file);
-    if ((m & PM_BAF) && L.ts[3] >= 0 && L.te[3] > L.ts[3]) {
-      uint8_t acct[64];
-      const int n = baf_account(p, L.ts[3], L.te[3], acct);
-      if (n < 0) return false;
+    if ((m & PM_BAF) && L.t3s >= 0 && L.t3e > L.t3s) {
+      int n;
+      bool digits;
+      double v;
+      if (!baf_account_scan(p, L.t3s, L.t3e, n, digits, v)) return false;
       if (n > 0) {
-        double v;
-        if (!simple_parse_int(acct, n, v)) return false;
         f.el = v;
         f.flags |= AF_ACCT;
-        if (all_digits(acct, n)) f.flags |= AF_ACCT_VALID;
+        if (digits) f.flags |= AF_ACCT_VALID;
       }
     }
     return true;
@@ -279,10 +331,10 @@ __device__ bool needs_host(const Event& e, const uint8_t* __restrict__ bytes) {
   if (e.kind >= LK_EJB_ENTRY && e.kind <= LK_CT_EXIT) {
     if (!(e.mask & PM_KEYS) || e.ntok < 3) return true;
     if (e.kind == LK_CT_EXIT && (e.mask & PM_BAF) && e.ntok >= 4) {
-      uint8_t acct[64];
-      const int n = baf_account(p, e.t3s, e.t3e, acct);
+      int n;
+      bool digits;
       double v;
-      if (n < 0 || !simple_parse_int(acct, n, v)) return true;
+      if (!baf_account_scan(p, e.t3s, e.t3e, n, digits, v)) return true;
     }
     return false;
   }
@@ -306,18 +358,22 @@ __device__ bool needs_host(const Event& e, const uint8_t* __restrict__ bytes) {
 
 enum : uint8_t { SEL_HOST = 1, SEL_MH = 2, SEL_WALK = 4 };
 
-struct SelPlus {
-  __device__ __host__ SelCount operator()(const SelCount& a, const SelCount& b) const {
-    return SelCount{a.host + b.host, a.mh + b.mh, a.walk + b.walk, a.aud_bytes + b.aud_bytes};
-  }
-};
+// Per-event selection counts packed into one u64 for the exclusive scan (a 16-byte struct scan
+// took ~180 us per batch over 1M entries; u64 takes rocprim's atomic look-back path):
+// host bits 0-21, mh bits 22-42, walk bits 43-63 (maxLinesPerBatch < 2^21, checked at init)
+constexpr int SEL_MH_SHIFT = 22, SEL_WALK_SHIFT = 43;
+__device__ __forceinline__ SelCount sel_unpack(uint64_t v) {
+  return SelCount{(uint32_t)(v & ((1ull << SEL_MH_SHIFT) - 1)),
+                  (uint32_t)((v >> SEL_MH_SHIFT) & ((1ull << (SEL_WALK_SHIFT - SEL_MH_SHIFT)) - 1)),
+                  (uint32_t)(v >> SEL_WALK_SHIFT), 0u};
+}
 
 // Per event: host / audit-list flags and counts; the AudF of every audit line the GPU reads
 // (computed once here, on the parse stream, and read by the join's k_build_ops)
 __global__ void k_host_flags(const Event* __restrict__ ev, const uint32_t* __restrict__ n_ev_dev,
                              const uint8_t* __restrict__ bytes, const uint32_t* __restrict__ chunk_file,
-                             uint8_t* __restrict__ flag, SelCount* __restrict__ val, AudF* __restrict__ aud,
-                             uint32_t cap) {
+                             uint8_t* __restrict__ flag, uint64_t* __restrict__ val, AudF* __restrict__ aud,
+                             SelCount* __restrict__ totals, uint32_t cap) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cap) return;
   const uint32_t n = *n_ev_dev;
@@ -343,21 +399,28 @@ __global__ void k_host_flags(const Event* __restrict__ ev, const uint32_t* __res
     }
   }
   flag[i] = fl;
-  val[i] = SelCount{(uint32_t)(fl & SEL_HOST), (fl & SEL_MH) ? 1u : 0u, (fl & SEL_WALK) ? 1u : 0u, ab};
+  val[i] = (uint64_t)(fl & SEL_HOST) | ((fl & SEL_MH) ? 1ull << SEL_MH_SHIFT : 0ull) |
+           ((fl & SEL_WALK) ? 1ull << SEL_WALK_SHIFT : 0ull);
+  // bytes of map / stopWatch-name lines: one atomic per wave (totals zeroed before the launch)
+  for (int o = APM_WAVE / 2; o > 0; o >>= 1) ab += __shfl_xor(ab, o, APM_WAVE);
+  if ((threadIdx.x & (APM_WAVE - 1)) == 0 && ab) atomicAdd(&totals->aud_bytes, ab);
 }
 
 __global__ void k_host_scatter(const Event* __restrict__ ev, const uint8_t* __restrict__ flag,
-                               const SelCount* __restrict__ val, const SelCount* __restrict__ pos, uint32_t cap,
+                               const uint64_t* __restrict__ val, const uint64_t* __restrict__ pos, uint32_t cap,
                                const uint32_t* __restrict__ n_ev_dev, Event* __restrict__ out,
                                uint32_t* __restrict__ out_idx, uint32_t* __restrict__ mh_idx,
                                uint32_t* __restrict__ walk_idx, SelCount* __restrict__ totals) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t n = *n_ev_dev;
-  if (i == 0) *totals = n == 0 ? SelCount{0, 0, 0, 0} : SelPlus()(pos[n - 1], val[n - 1]);
+  if (i == 0) {
+    const SelCount t = sel_unpack(n == 0 ? 0ull : pos[n - 1] + val[n - 1]);
+    totals->host = t.host; totals->mh = t.mh; totals->walk = t.walk;
+  }
   if (i >= n || i >= cap) return;
   const uint8_t fl = flag[i];
   if (!fl) return;
-  const SelCount p = pos[i];
+  const SelCount p = sel_unpack(pos[i]);
   if (fl & SEL_HOST) { out[p.host] = ev[i]; out_idx[p.host] = i; }
   if (fl & SEL_MH) mh_idx[p.mh] = i;
   if (fl & SEL_WALK) walk_idx[p.walk] = i;
@@ -442,20 +505,14 @@ __global__ void k_build_ops(DJArgs a) {
     } else {
       op.num = (e.kind == LK_EJB_EXIT || e.tBs != 0xffff) ? e.num : apm_nan();
       if (e.kind == LK_CT_EXIT && (e.mask & PM_BAF)) {
-        uint8_t acct[64];
-        int n;
-        if (e.ntok >= 4) {
-          n = baf_account(p, e.t3s, e.t3e, acct);
-        } else {
-          const char* u = "undefined";
-          for (n = 0; n < 9; ++n) acct[n] = (uint8_t)u[n];
-        }
+        int n = 9;  // fewer than 4 tokens: the account string is "undefined" (NaN, not digits)
+        bool digits = false;
+        double v = apm_nan();
+        if (e.ntok >= 4) baf_account_scan(p, e.t3s, e.t3e, n, digits, v);  // (needs_host: it succeeds)
         if (n > 0) {
-          double v = apm_nan();
-          simple_parse_int(acct, n, v);
           op.flags |= JF_BAF;
           op.aux = v;
-          if (all_digits(acct, n)) { op.flags |= JF_BAF_VALID; op.aux2 = v; }
+          if (digits) { op.flags |= JF_BAF_VALID; op.aux2 = v; }
         }
       }
       if (empty_lid) op.op = JOP_DIRECT;
@@ -1858,22 +1915,23 @@ size_t apm_dj_tmp_bytes(uint32_t max_ev, uint32_t max_out, int table_bits) {
   HIP_OK(rocprim::inclusive_scan(nullptr, e, (int64_t*)nullptr, (int64_t*)nullptr, (size_t)max_out + 1,
                                  rocprim::maximum<int64_t>(), (hipStream_t)0));
   size_t f = 0;
-  HIP_OK(rocprim::exclusive_scan(nullptr, f, (SelCount*)nullptr, (SelCount*)nullptr, SelCount{0, 0, 0, 0}, n, SelPlus(),
-                                 (hipStream_t)0));
+  HIP_OK(rocprim::exclusive_scan(nullptr, f, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint64_t)0, n,
+                                 rocprim::plus<uint64_t>(), (hipStream_t)0));
   return std::max(std::max(std::max(a, b), std::max(c, d)), std::max(e, f)) + 4096;
 }
 
 int apm_dj_select_host(DJArgs* a, const uint32_t* d_n_ev, uint32_t max_ev, hipStream_t s) {
-  if (max_ev == 0) { HIP_OK(hipMemsetAsync(a->n_host, 0, sizeof(SelCount), s)); return 0; }
+  HIP_OK(hipMemsetAsync(a->n_host, 0, sizeof(SelCount), s));
+  if (max_ev == 0) return 0;
   hipLaunchKernelGGL(k_host_flags, dim3((max_ev + TB - 1) / TB), dim3(TB), 0, s, a->ev, d_n_ev, a->bytes, a->chunk_file,
-                     a->host_flag, a->sel_val, a->aud, max_ev);
+                     a->host_flag, a->sel_val, a->aud, a->n_host, max_ev);
   dj_check(s, "k_host_flags");
   size_t need = 0;
-  HIP_OK(rocprim::exclusive_scan(nullptr, need, a->sel_val, a->sel_pos, SelCount{0, 0, 0, 0}, (size_t)max_ev, SelPlus(),
-                                 s));
+  HIP_OK(rocprim::exclusive_scan(nullptr, need, a->sel_val, a->sel_pos, (uint64_t)0, (size_t)max_ev,
+                                 rocprim::plus<uint64_t>(), s));
   if (need > a->tmp_bytes) return -1;
-  HIP_OK(rocprim::exclusive_scan(a->tmp, need, a->sel_val, a->sel_pos, SelCount{0, 0, 0, 0}, (size_t)max_ev, SelPlus(),
-                                 s));
+  HIP_OK(rocprim::exclusive_scan(a->tmp, need, a->sel_val, a->sel_pos, (uint64_t)0, (size_t)max_ev,
+                                 rocprim::plus<uint64_t>(), s));
   dj_check(s, "rocprim_exclusive_scan");
   hipLaunchKernelGGL(k_host_scatter, dim3((max_ev + TB - 1) / TB), dim3(TB), 0, s, a->ev, a->host_flag, a->sel_val,
                      a->sel_pos, max_ev, d_n_ev, a->host_ev, a->host_ev_idx, a->mh_idx, a->walk_idx, a->n_host);

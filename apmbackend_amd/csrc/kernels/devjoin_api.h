@@ -56,8 +56,8 @@ struct DJArgs {
   double rec_ttl, acct_ttl, need_ttl;
   // ---- host-event selection (run right after the parse kernels)
   uint8_t* host_flag;             // [n_ev] SEL_* bits
-  SelCount* sel_val;              // [n_ev + 1] per-event counts
-  SelCount* sel_pos;              // [n_ev + 1] exclusive scan
+  uint64_t* sel_val;              // [n_ev + 1] per-event counts, packed (devjoin.hip sel_unpack)
+  uint64_t* sel_pos;              // [n_ev + 1] exclusive scan
   Event* host_ev;                 // compacted host events
   uint32_t* host_ev_idx;
   uint32_t* mh_idx;               // compacted audit map / header events (event indices)

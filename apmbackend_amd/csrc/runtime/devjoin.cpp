@@ -120,8 +120,9 @@ DeviceJoin::DeviceJoin(const DevJoinConfig& cfg, Dictionary* dict, const std::ve
   HIP_OK(hipHostGetDevicePointer((void**)&hd_exp_, h_exp_, 0));
   soap_cap_ = 1u << 16;
   d_soap_ = (SoapState*)dmalloc((size_t)soap_cap_ * sizeof(SoapState));
-  d_sel_val_ = (SelCount*)dmalloc(((size_t)E + 64) * sizeof(SelCount));
-  d_sel_pos_ = (SelCount*)dmalloc(((size_t)E + 64) * sizeof(SelCount));
+  if (E >= (1u << 21)) throw std::runtime_error("device join: gpu.maxLinesPerBatch must be below 2^21");
+  d_sel_val_ = (uint64_t*)dmalloc(((size_t)E + 64) * 8);
+  d_sel_pos_ = (uint64_t*)dmalloc(((size_t)E + 64) * 8);
   d_walk_lo_ = (uint32_t*)dmalloc(((size_t)cfg_.max_chunks + 2) * 4);
   d_file_first_ = (int32_t*)dmalloc((size_t)soap_cap_ * 4);
   for (AudGen& g : aud_gen_) {

@@ -31,7 +31,7 @@
 namespace apm {
 
 struct DevJoinConfig {
-  uint32_t max_events = 1u << 21;   // events (relevant lines) per batch
+  uint32_t max_events = 1u << 20;   // events (relevant lines) per batch (< 2^21: packed selection scan)
   uint64_t max_batch_bytes = 64ull << 20;
   uint32_t max_chunks = 4096;
   int table_bits = 21;              // key-table slots (KeyState, 128 B)
@@ -256,8 +256,8 @@ class DeviceJoin {
   // per-event fields, key sort, walk tables
   AudGen aud_gen_[2]{};
   int aud_cur_ = 0;
-  SelCount* d_sel_val_ = nullptr;  // selection scan (parse stream, one batch at a time)
-  SelCount* d_sel_pos_ = nullptr;
+  uint64_t* d_sel_val_ = nullptr;  // selection scan (parse stream, one batch at a time)
+  uint64_t* d_sel_pos_ = nullptr;
   uint64_t *d_aud_key_ = nullptr, *d_aud_key_sorted_ = nullptr;
   uint32_t *d_aud_ord_ = nullptr, *d_aud_ord_sorted_ = nullptr;
   uint32_t aud_key_cap_ = 0;

@@ -58,7 +58,8 @@ def engine_config(cfg: Dict[str, Any], device: int = 0, keep_text: bool = False,
         "cell_cap": int(g.get("bucketCellCapacity", 16)),
         "spill_cap": int(g.get("bucketOverflowCapacity", 1 << 22)) // 40 or 1,
         "max_batch_bytes": int(g.get("batchBytes", 32 << 20)) * 2,
-        "max_lines": int(g.get("maxLinesPerBatch", 1 << 20)) * 2,
+        # (below 2^21: the device join packs its per-event selection counts into 21-bit fields)
+        "max_lines": min(int(g.get("maxLinesPerBatch", 1 << 20)) * 2, (1 << 21) - 1),
         # host-join tx staging per batch (grows by doubling when a batch needs more)
         "max_tx_per_batch": int(g.get("maxTxPerBatch", int(g.get("maxLinesPerBatch", 1 << 20)) * 2)),
         "ring_bytes": ring,
