@@ -1846,6 +1846,18 @@ __global__ void k_arena_remap(KeyState* __restrict__ table, uint32_t cap, const 
   s.need = (ne.key == s.key && ne.vidx >= lo && ne.vidx < hi) ? (int32_t)(ne.vidx & (fresh_cap - 1)) : -1;
 }
 
+// ------------------------------------------------------------------------ checkpoint helpers
+// chain blocks idx[0..n) (1-based) -> out[0..n), 16 bytes per lane
+__global__ void k_gather_blocks(const uint8_t* __restrict__ pool, const int32_t* __restrict__ idx, uint32_t n,
+                                uint8_t* __restrict__ out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  constexpr uint32_t Q = CHAIN_BLK / 16;
+  if (t >= n * Q) return;
+  const uint32_t b = t / Q, q = t % Q;
+  reinterpret_cast<uint4*>(out)[(size_t)b * Q + q] =
+      reinterpret_cast<const uint4*>(pool + (size_t)(idx[b] - 1) * CHAIN_BLK)[q];
+}
+
 // ------------------------------------------------------------------------ small helpers
 __global__ void k_reg_fill(RegSlot* __restrict__ reg, const int32_t* __restrict__ pairs, uint32_t n) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2111,6 +2123,12 @@ void apm_dj_rebuild(const KeyState* old, uint32_t old_cap, KeyState* fresh, uint
     hipLaunchKernelGGL(k_rebuild, dim3((old_cap + TB - 1) / TB), dim3(TB), 0, s, old, old_cap, fresh, fresh_mask, arena,
                        arena_cap, now, counts, live, pool, pool_ring, pool_mask);
   hipLaunchKernelGGL(k_pool_fix, dim3(1), dim3(1), 0, s, counts);
+}
+
+void apm_dj_gather_blocks(const uint8_t* pool, const int32_t* idx, uint32_t n, uint8_t* out, hipStream_t s) {
+  if (!n) return;
+  const uint32_t t = n * (CHAIN_BLK / 16);
+  hipLaunchKernelGGL(k_gather_blocks, dim3((t + TB - 1) / TB), dim3(TB), 0, s, pool, idx, n, out);
 }
 
 void apm_dj_pool_init(uint32_t* ring, uint32_t n, JoinCounts* counts, hipStream_t s) {

@@ -191,6 +191,8 @@ void apm_dj_rebuild(const apm::KeyState* old, uint32_t old_cap, apm::KeyState* f
 size_t apm_dj_live_tmp_bytes(uint32_t cap);
 void apm_dj_live_compact(const apm::KeyState* table, uint32_t cap, apm::KeyState* out, uint32_t* d_n, void* tmp,
                          size_t tmp_bytes, hipStream_t s);
+// checkpoint: chain blocks idx[0..n) (1-based block numbers, device) gathered into out (device)
+void apm_dj_gather_blocks(const uint8_t* pool, const int32_t* idx, uint32_t n, uint8_t* out, hipStream_t s);
 // chain-block pool: ring = identity (all `n` blocks free), counters head = 0, tail = ptail = n
 void apm_dj_pool_init(uint32_t* ring, uint32_t n, apm::JoinCounts* counts, hipStream_t s);
 // pool growth: the free entries of the old ring, then blocks [old_n, new_n), into `fresh_ring`

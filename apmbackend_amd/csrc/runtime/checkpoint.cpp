@@ -25,6 +25,7 @@
 
 #include "../kernels/devjoin_api.h"
 #include "binio.h"
+#include "d2h.h"
 #include "engine.h"
 
 namespace apm {
@@ -479,9 +480,8 @@ void Engine::write_small_sections(BinWriter& w) {
     // pending lines live in the HBM text ring: saved as one blob (pool lines, then tail lines)
     // with each gid rebased to its offset in the blob
     std::vector<int64_t> gids((size_t)(pool_n_ + tail_n_));
-    if (pool_n_) HIP_OK(hipMemcpy(gids.data(), d_pool_gid_[pool_cur_] + pool_off_, (size_t)pool_n_ * 8, hipMemcpyDeviceToHost));
-    if (tail_n_) HIP_OK(hipMemcpy(gids.data() + pool_n_, d_tail_gid_, (size_t)tail_n_ * 8, hipMemcpyDeviceToHost));
-    std::string text = ring_text(d_pool_gid_[pool_cur_] + pool_off_, pool_n_) + ring_text(d_tail_gid_, tail_n_);
+    d2h_bounced(gids.data(), d_pool_gid_[pool_cur_] + pool_off_, (size_t)pool_n_ * 8, stream_, (char*)bounce, kBounce);
+    d2h_bounced(gids.data() + pool_n_, d_tail_gid_, (size_t)tail_n_ * 8, stream_, (char*)bounce, kBounce);
     uint64_t off = 0;
     for (auto& g : gids) {
       const uint64_t len = (uint64_t)g & 0xfffffu;
@@ -489,7 +489,28 @@ void Engine::write_small_sections(BinWriter& w) {
       off += len + 1;
     }
     w.vec(gids);
-    w.str(text);
+    // the text (pool lines, then tail lines): gathered on the device, written straight from the
+    // pinned bounce into the snapshot (was: a hipMalloc + pageable copy + two string copies)
+    const int64_t* srcs[2] = {d_pool_gid_[pool_cur_] + pool_off_, d_tail_gid_};
+    const int64_t cnt[2] = {pool_n_, tail_n_};
+    uint32_t tot[2] = {0, 0};
+    for (int k = 0; k < 2; ++k) {
+      if (cnt[k] <= 0) continue;
+      if (apm_dj_gather_plan(srcs[k], cnt[k], nullptr, d_rel_lens_, d_rel_offs_, d_release_tmp_, release_tmp_bytes_, stream_) != 0)
+        throw std::runtime_error("checkpoint: ring text scratch too small");
+      HIP_OK(hipMemcpyAsync(&tot[k], d_rel_offs_ + cnt[k], 4, hipMemcpyDeviceToHost, stream_));
+      HIP_OK(hipStreamSynchronize(stream_));
+      if (!tot[k]) continue;
+      const size_t need = ((size_t)tot[k] + 15) & ~(size_t)15;
+      if (need > ck_text_cap_[k]) {
+        if (d_ck_text_[k]) HIP_OK(hipFree(d_ck_text_[k]));
+        ck_text_cap_[k] = need + need / 4;
+        HIP_OK(hipMalloc((void**)&d_ck_text_[k], ck_text_cap_[k]));
+      }
+      apm_dj_gather_copy(srcs[k], cnt[k], dj_->ring(), dj_->ring_cap(), d_rel_offs_, d_ck_text_[k], tot[k], stream_);
+    }
+    w.pod<uint64_t>((uint64_t)tot[0] + tot[1]);
+    for (int k = 0; k < 2; ++k) write_dev(w, d_ck_text_[k], tot[k], stream_, (char*)bounce, kBounce);
   } else {
     d2h_vec(w, d_tail_gid_, (size_t)tail_n_, stream_);
     w.pod<uint64_t>(line_blocks_.size());
@@ -864,9 +885,10 @@ int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& e
   job->path = dir_of(prefix) + "/" + job->name;
   job->extra = extra;
   {
-    BinWriter mw{BinWriter::Memory{}};
+    BinWriter mw{BinWriter::Memory{}, ck_blob_hint_};
     write_small_sections(mw);
     job->blob = mw.take_memory();
+    ck_blob_hint_ = job->blob.size() + job->blob.size() / 8 + (1u << 20);
   }
   // dirty ring rows -> HBM staging (D2D, stream-ordered after the quiesce point)
   const int32_t S = cfg_.max_series, n = n_series_;

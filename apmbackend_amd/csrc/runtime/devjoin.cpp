@@ -12,6 +12,7 @@
 
 #include "../kernels/common.h"
 #include "binio.h"
+#include "d2h.h"
 #include "../kernels/devjoin_dev.h"
 #include "../kernels/kernel_api.h"
 #include "join_util.h"
@@ -205,6 +206,7 @@ DeviceJoin::~DeviceJoin() {
   if (h_hops_) hipHostFree(h_hops_);
   if (h_hbuf_) hipHostFree(h_hbuf_);
   if (h_txt_) hipHostFree(h_txt_);
+  if (h_ck_bounce_) hipHostFree(h_ck_bounce_);
   for (void* p : allocs_) hipFree(p);
   hipStreamDestroy(stream_);
   if (up_stream_) { hipStreamSynchronize(up_stream_); hipStreamDestroy(up_stream_); }
@@ -1132,7 +1134,8 @@ void DeviceJoin::save(BinWriter& w) {
     HIP_OK(hipMemcpyAsync(&n_live, d_n, 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     live.resize(n_live);
-    if (n_live) HIP_OK(hipMemcpy(live.data(), out, (size_t)n_live * sizeof(KeyState), hipMemcpyDeviceToHost));
+    if (!h_ck_bounce_) HIP_OK(hipHostMalloc((void**)&h_ck_bounce_, kCkBounce, hipHostMallocDefault));
+    d2h_bounced(live.data(), out, (size_t)n_live * sizeof(KeyState), st, h_ck_bounce_, kCkBounce);
     HIP_OK(hipFree(tmp));
     if (out != d_table_spare_) HIP_OK(hipFree(out));
   }
@@ -1143,38 +1146,57 @@ void DeviceJoin::save(BinWriter& w) {
   if (!ents.empty()) {  // the live range of the arena ring in (at most) two copies, not one per entry
     const uint64_t cap = cfg_.arena_cap, first = lo & (cap - 1);
     const uint64_t n1 = std::min<uint64_t>(ents.size(), cap - first);
-    HIP_OK(hipMemcpy(ents.data(), d_arena_ + first, (size_t)n1 * sizeof(NeedEnt), hipMemcpyDeviceToHost));
+    if (!h_ck_bounce_) HIP_OK(hipHostMalloc((void**)&h_ck_bounce_, kCkBounce, hipHostMallocDefault));
+    d2h_bounced(ents.data(), d_arena_ + first, (size_t)n1 * sizeof(NeedEnt), st, h_ck_bounce_, kCkBounce);
     if (ents.size() > n1)
-      HIP_OK(hipMemcpy(ents.data() + n1, d_arena_, (size_t)(ents.size() - n1) * sizeof(NeedEnt), hipMemcpyDeviceToHost));
+      d2h_bounced(ents.data() + n1, d_arena_, (size_t)(ents.size() - n1) * sizeof(NeedEnt), st, h_ck_bounce_, kCkBounce);
   }
-  // chain blocks reachable from the live state, renumbered 1..n in the file
+  // chain blocks reachable from the live state, renumbered 1..n in the file.  Only those blocks
+  // are read (gathered on the device one chain level at a time): the whole pool is ~256 MB and
+  // its copy was most of a checkpoint's ingest stall once any chain existed.
   struct Blk { uint8_t b[CHAIN_BLK]; };
   std::vector<Blk> blocks;
   {
-    bool any = false;
-    for (const KeyState& k : live) any |= k.pblk != 0;
-    for (const NeedEnt& e : ents) any |= e.iblk != 0 || e.lblk != 0;
-    if (any) {
-      std::vector<Blk> pool(pool_n_);
-      HIP_OK(hipMemcpy(pool.data(), d_pool_, (size_t)pool_n_ * CHAIN_BLK, hipMemcpyDeviceToHost));
-      auto copy_chain = [&](int32_t b1) -> int32_t {
-        int32_t head = 0, prev = 0;
-        for (; b1; b1 = *(const int32_t*)pool[(size_t)b1 - 1].b) {
-          blocks.push_back(pool[(size_t)b1 - 1]);
-          const int32_t nb = (int32_t)blocks.size();
-          *(int32_t*)blocks.back().b = 0;
-          if (prev) *(int32_t*)blocks[(size_t)prev - 1].b = nb;
-          else head = nb;
-          prev = nb;
-        }
-        return head;
-      };
-      for (KeyState& k : live) k.pblk = copy_chain(k.pblk);
-      for (NeedEnt& e : ents) {
-        e.iblk = e.key ? copy_chain(e.iblk) : 0;
-        e.lblk = e.key ? copy_chain(e.lblk) : 0;
-      }
+    // level 0: every chain head, with where its new number goes
+    std::vector<int32_t> cur;          // pool block numbers (1-based) to fetch
+    std::vector<int32_t*> slot_of;     // where each fetched block's new number is stored
+    for (KeyState& k : live) if (k.pblk) { cur.push_back(k.pblk); slot_of.push_back(&k.pblk); }
+    for (NeedEnt& e : ents) {
+      if (!e.key) { e.iblk = e.lblk = 0; continue; }
+      if (e.iblk) { cur.push_back(e.iblk); slot_of.push_back(&e.iblk); }
+      if (e.lblk) { cur.push_back(e.lblk); slot_of.push_back(&e.lblk); }
     }
+    std::vector<int32_t> parent(cur.size(), -1);  // index in `blocks` of the predecessor (-1: a head)
+    int32_t* d_idx = nullptr;
+    uint8_t* d_out = nullptr;
+    size_t cap = 0;
+    while (!cur.empty()) {
+      if (cur.size() > cap) {
+        if (d_idx) { HIP_OK(hipFree(d_idx)); HIP_OK(hipFree(d_out)); }
+        cap = cur.size() * 2;
+        HIP_OK(hipMalloc((void**)&d_idx, cap * 4));
+        HIP_OK(hipMalloc((void**)&d_out, cap * CHAIN_BLK));
+      }
+      HIP_OK(hipMemcpyAsync(d_idx, cur.data(), cur.size() * 4, hipMemcpyHostToDevice, st));
+      apm_dj_gather_blocks(d_pool_, d_idx, (uint32_t)cur.size(), d_out, st);
+      const size_t base = blocks.size();
+      blocks.resize(base + cur.size());
+      HIP_OK(hipMemcpyAsync(blocks.data() + base, d_out, cur.size() * CHAIN_BLK, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      std::vector<int32_t> nxt, nparent;
+      for (size_t i = 0; i < cur.size(); ++i) {
+        const int32_t nb = (int32_t)(base + i + 1);  // new number of this block
+        if (parent[i] < 0) *slot_of[i] = nb;
+        else *(int32_t*)blocks[(size_t)parent[i]].b = nb;
+        const int32_t next = *(const int32_t*)blocks[base + i].b;
+        *(int32_t*)blocks[base + i].b = 0;
+        if (next) { nxt.push_back(next); nparent.push_back((int32_t)(base + i)); }
+      }
+      cur.swap(nxt);
+      parent.swap(nparent);
+      slot_of.assign(cur.size(), nullptr);
+    }
+    if (d_idx) { HIP_OK(hipFree(d_idx)); HIP_OK(hipFree(d_out)); }
   }
   w.vec(live);
   w.pod(cfg_.arena_cap);

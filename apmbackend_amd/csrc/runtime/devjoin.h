@@ -265,6 +265,9 @@ class DeviceJoin {
   int32_t* d_file_first_ = nullptr;
   AudItem* d_aud_slots_ = nullptr;
   uint32_t aud_slots_cap_ = 0;
+  // checkpoint: pinned bounce for the large D2H reads of save()
+  static constexpr size_t kCkBounce = 32u << 20;
+  char* h_ck_bounce_ = nullptr;
   uint32_t soap_cap_ = 0;
   int32_t* d_file_server_ = nullptr;
   size_t files_uploaded_ = 0;

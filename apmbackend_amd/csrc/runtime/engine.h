@@ -11,6 +11,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "binio.h"
+
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
@@ -794,7 +796,8 @@ class Engine {
     struct Lag { int32_t n_cols = 0; std::vector<int32_t> heads; size_t off = 0; };
     bool base = false;
     int64_t seq = 0;
-    std::string prefix, name, path, blob, extra;
+    std::string prefix, name, path, extra;
+    MemBlob blob;                 // the small sections, serialised at the snapshot
     std::vector<Lag> lags;
   };
   static constexpr int kMaxChain = 16;
@@ -820,6 +823,9 @@ class Engine {
   void* d_ck_stage_ = nullptr;
   size_t ck_stage_bytes_ = 0;
   void* h_ck_bounce_ = nullptr;
+  size_t ck_blob_hint_ = 0;         // size of the last small-section blob (reserve)
+  char* d_ck_text_[2] = {nullptr, nullptr};  // pending-line text gathered for a checkpoint
+  size_t ck_text_cap_[2] = {0, 0};
   hipEvent_t ck_ev_ = nullptr;
   hipStream_t ck_stream_ = nullptr;
 
