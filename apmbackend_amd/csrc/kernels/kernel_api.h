@@ -190,6 +190,12 @@ int apm_parse_batch(const uint8_t* d_bytes, uint64_t n_bytes, const uint32_t* d_
                     uint32_t* d_n_lines, unsigned long long* d_watermark, uint8_t* d_file_open,
                     const apm::TzTable* tz, hipStream_t stream);
 // stats.hip
+// checkpoint: occupied cells of k bucket slots packed on the device (entry i * n + s = slot
+// d_slots[i], series s); offs[k * n] = total cells.  lens / offs: k * n + 1 entries.
+size_t apm_ck_pack_tmp_bytes(uint64_t n_entries);
+int apm_ck_pack_cells(const int32_t* counts, const int32_t* cells, const int32_t* d_slots, int k, int32_t n, int32_t S,
+                      int32_t cap, uint32_t* lens, uint32_t* offs, void* tmp, size_t tmp_bytes, int32_t* packed,
+                      hipStream_t s);
 void apm_stats_clear_slot(apm::StatsState* st, int slot, hipStream_t stream);
 void apm_bucket_append(const apm::TxRec* d_tx, uint32_t lo, uint32_t hi, apm::StatsState* st,
                        int64_t min_live_bucket, hipStream_t stream);

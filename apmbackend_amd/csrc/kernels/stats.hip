@@ -667,6 +667,32 @@ __global__ __launch_bounds__(256) void k_copy(W* __restrict__ dst, const W* __re
 
 }  // namespace apm
 
+// ------------------------------------------------------------------------ checkpoint packing
+// The occupied cells of the live bucket slots, packed on the device for the checkpoint (the host
+// used to copy every slot's full cell array and pack it series by series on the ingest thread).
+// Entry i * n + s = (slot[i], series s): lens = min(count, cap), scanned, then gathered.
+__global__ void k_ck_lens(const int32_t* __restrict__ counts, const int32_t* __restrict__ slots, int k, int32_t n,
+                          int32_t S, int32_t cap, uint32_t* __restrict__ lens) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t N = (uint64_t)k * n;
+  if (t > N) return;
+  if (t == N) { lens[N] = 0; return; }
+  const int i = (int)(t / (uint64_t)n), s = (int)(t % (uint64_t)n);
+  const int32_t c = counts[(size_t)slots[i] * S + s];
+  lens[t] = (uint32_t)(c < cap ? (c > 0 ? c : 0) : cap);
+}
+
+__global__ void k_ck_pack(const int32_t* __restrict__ cells, const int32_t* __restrict__ slots, int k, int32_t n,
+                          int32_t S, int32_t cap, const uint32_t* __restrict__ lens, const uint32_t* __restrict__ offs,
+                          int32_t* __restrict__ packed) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (uint64_t)k * n) return;
+  const int i = (int)(t / (uint64_t)n), s = (int)(t % (uint64_t)n);
+  const int32_t* src = cells + ((size_t)slots[i] * S + s) * cap;
+  int32_t* dst = packed + offs[t];
+  for (uint32_t j = 0; j < lens[t]; ++j) dst[j] = src[j];
+}
+
 extern "C" {
 
 using namespace apm;
@@ -793,4 +819,24 @@ int apm_release_merge(const int64_t* pool_end, const int64_t* pool_gid, int64_t 
   return 0;
 }
 
+
+size_t apm_ck_pack_tmp_bytes(uint64_t n_entries) {
+  size_t b = 0;
+  HIP_OK(rocprim::exclusive_scan(nullptr, b, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)n_entries + 1,
+                                 rocprim::plus<uint32_t>(), (hipStream_t)0));
+  return b;
+}
+
+int apm_ck_pack_cells(const int32_t* counts, const int32_t* cells, const int32_t* d_slots, int k, int32_t n, int32_t S,
+                      int32_t cap, uint32_t* lens, uint32_t* offs, void* tmp, size_t tmp_bytes, int32_t* packed,
+                      hipStream_t s) {
+  const uint64_t N = (uint64_t)k * n;
+  hipLaunchKernelGGL(k_ck_lens, dim3((unsigned)((N + 1 + 255) / 256)), dim3(256), 0, s, counts, d_slots, k, n, S, cap, lens);
+  size_t need = 0;
+  HIP_OK(rocprim::exclusive_scan(nullptr, need, lens, offs, 0u, (size_t)N + 1, rocprim::plus<uint32_t>(), s));
+  if (need > tmp_bytes) return -1;
+  HIP_OK(rocprim::exclusive_scan(tmp, need, lens, offs, 0u, (size_t)N + 1, rocprim::plus<uint32_t>(), s));
+  if (N) hipLaunchKernelGGL(k_ck_pack, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, cells, d_slots, k, n, S, cap, lens, offs, packed);
+  return 0;
+}
 }  // extern "C"

@@ -415,33 +415,43 @@ void Engine::write_small_sections(BinWriter& w) {
   {
     std::vector<int32_t> spill_n(NSLOT);
     HIP_OK(hipMemcpy(spill_n.data(), d_spill_n_, NSLOT * 4, hipMemcpyDeviceToHost));
-    std::vector<int32_t> counts(n), packed;
+    // the occupied cells of every live slot, packed on the device in one pass (scan + gather),
+    // then written per slot straight from the pinned bounce
+    std::vector<int32_t> slots;
+    for (int slot = 0; slot < NSLOT; ++slot)
+      if (slot_bucket_[slot] != NO_BUCKET) slots.push_back(slot);
+    const int k = (int)slots.size();
     const int32_t cap = cfg_.cell_cap;
-    const size_t per = std::max<size_t>(1, kBounce / ((size_t)cap * 4));  // series per bounce fill
-    for (int slot = 0; slot < NSLOT; ++slot) {
-      if (slot_bucket_[slot] == NO_BUCKET) continue;
-      w.pod<int32_t>(slot);
-      HIP_OK(hipMemcpyAsync(bounce, d_counts_cells_ + (size_t)slot * S, (size_t)n * 4, hipMemcpyDeviceToHost, stream_));
-      HIP_OK(hipStreamSynchronize(stream_));
-      std::memcpy(counts.data(), bounce, (size_t)n * 4);
-      w.vec(counts);
-      size_t total = 0;
-      for (int32_t s = 0; s < n; ++s) total += (size_t)std::min(counts[s], cap);
-      packed.resize(total);  // only the occupied cells
-      size_t o = 0;
-      for (int32_t s0 = 0; s0 < n; s0 += (int32_t)per) {
-        const int32_t s1 = std::min<int32_t>(n, s0 + (int32_t)per);
-        HIP_OK(hipMemcpyAsync(bounce, d_cells_ + ((size_t)slot * S + s0) * cap, (size_t)(s1 - s0) * cap * 4,
-                              hipMemcpyDeviceToHost, stream_));
-        HIP_OK(hipStreamSynchronize(stream_));
-        const int32_t* c = (const int32_t*)bounce;
-        for (int32_t s = s0; s < s1; ++s) {
-          const int32_t k = std::min(counts[s], cap);
-          std::memcpy(packed.data() + o, c + (size_t)(s - s0) * cap, (size_t)k * 4);
-          o += (size_t)k;
-        }
+    const uint64_t N = (uint64_t)k * (uint64_t)n;
+    std::vector<uint32_t> bnd((size_t)k + 1, 0);
+    if (N) {
+      if (N + 1 > ck_pack_n_) {
+        for (void* q : {(void*)d_ck_lens_, (void*)d_ck_offs_, (void*)d_ck_packed_, d_ck_ptmp_})
+          if (q) HIP_OK(hipFree(q));
+        ck_pack_n_ = (N + 1) * 5 / 4;
+        ck_ptmp_bytes_ = apm_ck_pack_tmp_bytes(ck_pack_n_);
+        HIP_OK(hipMalloc((void**)&d_ck_lens_, ck_pack_n_ * 4));
+        HIP_OK(hipMalloc((void**)&d_ck_offs_, ck_pack_n_ * 4));
+        HIP_OK(hipMalloc((void**)&d_ck_packed_, ck_pack_n_ * (size_t)cap * 4));
+        HIP_OK(hipMalloc(&d_ck_ptmp_, ck_ptmp_bytes_));
       }
-      w.vec(packed);
+      if (!d_ck_slots_) HIP_OK(hipMalloc((void**)&d_ck_slots_, NSLOT * 4));
+      HIP_OK(hipMemcpyAsync(d_ck_slots_, slots.data(), (size_t)k * 4, hipMemcpyHostToDevice, stream_));
+      if (apm_ck_pack_cells(d_counts_cells_, d_cells_, d_ck_slots_, k, n, S, cap, d_ck_lens_, d_ck_offs_, d_ck_ptmp_,
+                            ck_ptmp_bytes_, d_ck_packed_, stream_) != 0)
+        throw std::runtime_error("checkpoint: cell packing scratch too small");
+      for (int i = 0; i <= k; ++i)
+        HIP_OK(hipMemcpyAsync(&bnd[(size_t)i], d_ck_offs_ + (size_t)i * n, 4, hipMemcpyDeviceToHost, stream_));
+      HIP_OK(hipStreamSynchronize(stream_));
+    }
+    for (int i = 0; i < k; ++i) {
+      const int slot = slots[(size_t)i];
+      w.pod<int32_t>(slot);
+      w.pod<uint64_t>((uint64_t)n);  // counts (vec layout)
+      write_dev(w, d_counts_cells_ + (size_t)slot * S, (size_t)n * 4, stream_, (char*)bounce, kBounce);
+      const uint64_t tot = bnd[(size_t)i + 1] - bnd[(size_t)i];
+      w.pod<uint64_t>(tot);  // packed cells (vec layout)
+      write_dev(w, d_ck_packed_ + bnd[(size_t)i], (size_t)tot * 4, stream_, (char*)bounce, kBounce);
       const int32_t ns = std::min(spill_n[slot], cfg_.spill_cap);
       w.pod(spill_n[slot]);
       d2h_vec(w, d_spill_series_ + (size_t)slot * cfg_.spill_cap, (size_t)ns, stream_, bounce);

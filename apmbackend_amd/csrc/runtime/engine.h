@@ -826,6 +826,13 @@ class Engine {
   size_t ck_blob_hint_ = 0;         // size of the last small-section blob (reserve)
   char* d_ck_text_[2] = {nullptr, nullptr};  // pending-line text gathered for a checkpoint
   size_t ck_text_cap_[2] = {0, 0};
+  // checkpoint cell packing (device scan + gather of the occupied bucket cells)
+  int32_t* d_ck_slots_ = nullptr;
+  uint32_t *d_ck_lens_ = nullptr, *d_ck_offs_ = nullptr;
+  int32_t* d_ck_packed_ = nullptr;
+  void* d_ck_ptmp_ = nullptr;
+  uint64_t ck_pack_n_ = 0;
+  size_t ck_ptmp_bytes_ = 0;
   hipEvent_t ck_ev_ = nullptr;
   hipStream_t ck_stream_ = nullptr;
 
