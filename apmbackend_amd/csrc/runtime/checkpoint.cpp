@@ -398,6 +398,7 @@ void Engine::write_small_sections(BinWriter& w) {
   w.pod<uint8_t>(dev() ? 1 : 0);
   if (dev()) {
     dj_->save(w);
+    for (const auto& sp : dj_->save_spans) trace_event(sp.first, sp.second.first, sp.second.second, 0);
     w.vec(h_raw_series_);
   } else {
     w.pod<uint64_t>(shards_.size());

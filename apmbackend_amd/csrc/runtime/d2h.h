@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <memory>
 
 #include "../kernels/common.h"
 #include "binio.h"
@@ -32,6 +33,29 @@ inline void d2h_bounced(void* dst, const void* dev, size_t n, hipStream_t st, ch
 // n device bytes appended to the writer in place
 inline void write_dev(BinWriter& w, const void* dev, size_t n, hipStream_t st, char* bounce, size_t bounce_bytes) {
   w.raw_fill(n, [&](char* dst) { d2h_bounced(dst, dev, n, st, bounce, bounce_bytes); });
+}
+
+// An array of trivially copyable records without the zero fill of std::vector::resize (the
+// snapshot overwrites every byte); written in the BinWriter::vec layout.
+template <class T>
+struct PodBuf {
+  std::unique_ptr<T[]> p;
+  size_t n = 0;
+  void resize_uninit(size_t k) {
+    p.reset(k ? new T[k] : nullptr);
+    n = k;
+  }
+  T* data() { return p.get(); }
+  size_t size() const { return n; }
+  bool empty() const { return n == 0; }
+  T* begin() { return p.get(); }
+  T* end() { return p.get() + n; }
+  T& operator[](size_t i) { return p[i]; }
+};
+template <class T>
+void write_vec(BinWriter& w, const PodBuf<T>& v) {
+  w.pod<uint64_t>(v.n);
+  w.raw(v.p.get(), v.n * sizeof(T));
 }
 
 }  // namespace apm

@@ -1114,13 +1114,16 @@ JoinCounters DeviceJoin::counters() const {
 // ---------------------------------------------------------------------------- checkpoint
 void DeviceJoin::save(BinWriter& w) {
   hipStream_t st = stream_;
+  save_spans.clear();
+  double sp0 = clock_ms();
+  auto span = [&](const char* name) { const double t = clock_ms(); save_spans.push_back({name, {sp0, t}}); sp0 = t; };
   HIP_OK(hipStreamSynchronize(st));
   HIP_OK(hipMemcpy(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost));
   w.pod(*h_counts_);
   for (uint64_t v : {events_, tx_, tx_db_, audit_errors_, host_pm_, host_invalid_acct_, host_events_}) w.pod(v);
   // key table: live (non-empty) slots only, selected on the device -- the whole table is
   // 2M x 128 B and its D2H copy was most of a base checkpoint's ingest stall
-  std::vector<KeyState> live;
+  PodBuf<KeyState> live;
   {
     const size_t tb = apm_dj_live_tmp_bytes(table_cap_);
     KeyState* out = d_table_spare_;
@@ -1133,16 +1136,18 @@ void DeviceJoin::save(BinWriter& w) {
     uint32_t n_live = 0;
     HIP_OK(hipMemcpyAsync(&n_live, d_n, 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
-    live.resize(n_live);
+    live.resize_uninit(n_live);
     if (!h_ck_bounce_) HIP_OK(hipHostMalloc((void**)&h_ck_bounce_, kCkBounce, hipHostMallocDefault));
     d2h_bounced(live.data(), out, (size_t)n_live * sizeof(KeyState), st, h_ck_bounce_, kCkBounce);
     HIP_OK(hipFree(tmp));
     if (out != d_table_spare_) HIP_OK(hipFree(out));
   }
+  span("ck.j.table");
   // needNumRecordCache regions + their arena entries (arena capacity first: the table's `need`
   // links are physical slots of an arena of that size)
   const uint64_t lo = regions_.empty() ? arena_head_ : regions_.front().lo;
-  std::vector<NeedEnt> ents((size_t)(arena_head_ - lo));
+  PodBuf<NeedEnt> ents;
+  ents.resize_uninit((size_t)(arena_head_ - lo));
   if (!ents.empty()) {  // the live range of the arena ring in (at most) two copies, not one per entry
     const uint64_t cap = cfg_.arena_cap, first = lo & (cap - 1);
     const uint64_t n1 = std::min<uint64_t>(ents.size(), cap - first);
@@ -1151,6 +1156,7 @@ void DeviceJoin::save(BinWriter& w) {
     if (ents.size() > n1)
       d2h_bounced(ents.data() + n1, d_arena_, (size_t)(ents.size() - n1) * sizeof(NeedEnt), st, h_ck_bounce_, kCkBounce);
   }
+  span("ck.j.arena");
   // chain blocks reachable from the live state, renumbered 1..n in the file.  Only those blocks
   // are read (gathered on the device one chain level at a time): the whole pool is ~256 MB and
   // its copy was most of a checkpoint's ingest stall once any chain existed.
@@ -1198,13 +1204,15 @@ void DeviceJoin::save(BinWriter& w) {
     }
     if (d_idx) { HIP_OK(hipFree(d_idx)); HIP_OK(hipFree(d_out)); }
   }
-  w.vec(live);
+  span("ck.j.chains");
+  write_vec(w, live);
   w.pod(cfg_.arena_cap);
   w.pod(arena_head_);
   w.pod<uint64_t>(regions_.size());
   for (const Region& r : regions_) { w.pod(r.lo); w.pod(r.hi); w.pod(r.exp); }
-  w.vec(ents);
+  write_vec(w, ents);
   w.vec(blocks);
+  span("ck.j.write");
   // SOAP contexts of every file
   {
     std::vector<SoapState> ss(files_->size());
@@ -1220,6 +1228,7 @@ void DeviceJoin::save(BinWriter& w) {
     for (int32_t i = 0; i < n; ++i) top[i] = h_rawtab_[i].toplevel;
     w.vec(top);
   }
+  span("ck.j.soap+registry");
   // audit trail (K5): the carry generation the next batch reads
   {
     const AudGen& g = aud_gen_[aud_cur_];
@@ -1237,6 +1246,7 @@ void DeviceJoin::save(BinWriter& w) {
     w.vec(items);
     w.str(txt);
   }
+  span("ck.j.audit");
 }
 
 void DeviceJoin::load(BinReader& rd) {

@@ -120,6 +120,7 @@ class DeviceJoin {
   static constexpr int kPhases = 8;
   double phase_t[kPhases + 1] = {0};
   std::vector<std::pair<const char*, std::pair<double, double>>> spans;  // finer trace spans of run()
+  std::vector<std::pair<const char*, std::pair<double, double>>> save_spans;  // spans of the last save()
   const JoinCounts& last_counts() const { return *h_counts_; }
   size_t device_bytes() const { return device_bytes_; }
 

@@ -27,6 +27,3 @@ ev=t['traceEvents'] if isinstance(t,dict) else t
 for e in ev:
     if e.get('name','').startswith('ck.'): print(e['name'], round(e.get('dur',0)/1000,2), 'ms')
 PY
-timeout -k 10 420 python bench.py --preset firehose --steps 20 --warmup 5 --trace $O/fh_trace.json > $O/firehose_20.log 2>&1; rc=$?
-echo "firehose rc=$rc"; tail -1 $O/firehose_20.log | cut -c1-160
-python3 tools/trace_summary.py $O/fh_trace.json > $O/fh_trace_summary.txt 2>&1 || true
