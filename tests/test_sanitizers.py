@@ -146,3 +146,20 @@ def test_db_sink_under_sanitizers(tmp_path, tool):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "WARNING: ThreadSanitizer" not in r.stderr and "runtime error" not in r.stderr
     assert r.stdout.startswith("ok")
+
+
+def test_checkpoint_memory_writer_matches_file_writer(tmp_path):
+    """binio.h: sections written by the in-memory writer (reserved MemBlob, in-place fills,
+    patched section lengths) and spliced after the file header -- the asynchronous checkpoint
+    path -- are byte-identical to the same sections written to a file; under ASan/UBSan."""
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    exe = str(tmp_path / "binio_test")
+    san = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+           "-Xarch_host", "-fno-omit-frame-pointer", "-Xarch_host", "-fno-sanitize-recover=all"]
+    cmd = [hipcc, "-O1", "-g", "-std=c++17", "--offload-arch=gfx950", *san, "-I", CSRC,
+           os.path.join(ROOT, "tests", "native", "binio_test.cpp"), "-o", exe, "-fsanitize=address,undefined"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1", UBSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0 and "ALL OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
