@@ -222,7 +222,6 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   HIP_OK(hipStreamCreateWithFlags(&parse_stream_, hipStreamNonBlocking));
   HIP_OK(hipStreamCreateWithFlags(&out_stream_, hipStreamNonBlocking));
-  HIP_OK(hipStreamCreateWithFlags(&out_stream2_, hipStreamNonBlocking));
   HIP_OK(hipEventCreateWithFlags(&ev_a_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_b_, hipEventDisableTiming));
   const int32_t S = cfg_.max_series;
@@ -506,8 +505,6 @@ Engine::~Engine() {
   }
   hipStreamSynchronize(out_stream_);
   hipStreamDestroy(out_stream_);
-  hipStreamSynchronize(out_stream2_);
-  hipStreamDestroy(out_stream2_);
   hipHostFree(h_fmt_meta_);
   for (int k = 0; k < kStage; ++k) {
     if (h_stage_[k]) hipHostFree(h_stage_[k]);
@@ -2595,19 +2592,8 @@ void Engine::format_rollover_text(int64_t edge_ts) {
     }
     char* h = h_fmt_out_[k];
     const double tl0 = now_ms();
-    // the fs text (~20 MB at the headline) in two halves on two streams: two copies in flight
-    // (APM_OUT_SPLIT=0: one stream, the previous behaviour)
-    static const bool split = [] { const char* e = std::getenv("APM_OUT_SPLIT"); return !e || e[0] != '0'; }();
     if (st_total) HIP_OK(hipMemcpyAsync(h, dst, st_total, hipMemcpyDeviceToHost, out_stream_));
-    if (fs_total && split && fs_total >= (4u << 20)) {
-      const size_t half = (fs_total / 2) & ~(size_t)4095;
-      HIP_OK(hipMemcpyAsync(h + st_total, dst + st_cap, half, hipMemcpyDeviceToHost, out_stream2_));
-      HIP_OK(hipMemcpyAsync(h + st_total + half, dst + st_cap + half, fs_total - half, hipMemcpyDeviceToHost,
-                            out_stream_));
-      HIP_OK(hipStreamSynchronize(out_stream2_));
-    } else if (fs_total) {
-      HIP_OK(hipMemcpyAsync(h + st_total, dst + st_cap, fs_total, hipMemcpyDeviceToHost, out_stream_));
-    }
+    if (fs_total) HIP_OK(hipMemcpyAsync(h + st_total, dst + st_cap, fs_total, hipMemcpyDeviceToHost, out_stream_));
     HIP_OK(hipStreamSynchronize(out_stream_));
     {
       std::lock_guard<std::mutex> g(out_mu_);

@@ -683,7 +683,6 @@ class Engine {
   char* h_rel_text_[2] = {nullptr, nullptr};
   size_t h_rel_text_cap_[2] = {0, 0};
   hipStream_t out_stream_ = nullptr;
-  hipStream_t out_stream2_ = nullptr;  // second half of the large st/fs D2H
   std::vector<int32_t> h_raw_series_;          // stats thread mirror of the raw -> series table
   // pinned staging of the stats thread's H2D uploads: kStage buffers used in rotation, each
   // reused only after its previous copy completed (an event), so no upload waits for the stream
