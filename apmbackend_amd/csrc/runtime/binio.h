@@ -149,6 +149,10 @@ class BinWriter {
       throw std::runtime_error("checkpoint: rename failed: " + std::string(std::strerror(errno)));
   }
   uint64_t bytes() const { return bytes_; }
+  // memory mode: current size, and a pointer to an earlier offset (valid until the next write)
+  bool is_memory() const { return mem_; }
+  size_t mem_pos() const { return buf_.size(); }
+  char* mem_at(size_t off) { return buf_.p + off; }
 
  private:
   std::string path_, tmp_;

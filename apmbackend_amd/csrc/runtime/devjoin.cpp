@@ -1112,65 +1112,72 @@ JoinCounters DeviceJoin::counters() const {
 }
 
 // ---------------------------------------------------------------------------- checkpoint
-void DeviceJoin::save(BinWriter& w) {
+// Key table (live slots), need arena (live regions) and the chain blocks they reach, into a
+// memory writer: vec(live KeyState), arena_cap, arena_head, regions, vec(NeedEnt), vec(blocks)
+// -- chain links renumbered 1..n in the file, in place in the writer's buffer.
+void DeviceJoin::save_tables(BinWriter& w) {
   hipStream_t st = stream_;
-  save_spans.clear();
-  double sp0 = clock_ms();
-  auto span = [&](const char* name) { const double t = clock_ms(); save_spans.push_back({name, {sp0, t}}); sp0 = t; };
-  HIP_OK(hipStreamSynchronize(st));
-  HIP_OK(hipMemcpy(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost));
-  w.pod(*h_counts_);
-  for (uint64_t v : {events_, tx_, tx_db_, audit_errors_, host_pm_, host_invalid_acct_, host_events_}) w.pod(v);
-  // key table: live (non-empty) slots only, selected on the device -- the whole table is
-  // 2M x 128 B and its D2H copy was most of a base checkpoint's ingest stall
-  PodBuf<KeyState> live;
+  double sp = clock_ms();
+  auto span = [&](const char* name) { const double t = clock_ms(); save_spans.push_back({name, {sp, t}}); sp = t; };
+  if (!h_ck_bounce_) HIP_OK(hipHostMalloc((void**)&h_ck_bounce_, kCkBounce, hipHostMallocDefault));
+  // live (non-empty) slots, selected on the device
+  uint32_t n_live = 0;
+  size_t live_off = 0;
   {
     const size_t tb = apm_dj_live_tmp_bytes(table_cap_);
     KeyState* out = d_table_spare_;
     void* tmp = nullptr;
-    uint32_t* d_n = nullptr;
     if (!out) HIP_OK(hipMalloc((void**)&out, (size_t)table_cap_ * sizeof(KeyState)));
     HIP_OK(hipMalloc(&tmp, tb + 64));
-    d_n = (uint32_t*)((char*)tmp + tb);
+    uint32_t* d_n = (uint32_t*)((char*)tmp + tb);
     apm_dj_live_compact(d_table_, table_cap_, out, d_n, tmp, tb, st);
-    uint32_t n_live = 0;
     HIP_OK(hipMemcpyAsync(&n_live, d_n, 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
-    live.resize_uninit(n_live);
-    if (!h_ck_bounce_) HIP_OK(hipHostMalloc((void**)&h_ck_bounce_, kCkBounce, hipHostMallocDefault));
-    d2h_bounced(live.data(), out, (size_t)n_live * sizeof(KeyState), st, h_ck_bounce_, kCkBounce);
+    w.pod<uint64_t>(n_live);
+    live_off = w.mem_pos();
+    write_dev(w, out, (size_t)n_live * sizeof(KeyState), st, h_ck_bounce_, kCkBounce);
     HIP_OK(hipFree(tmp));
     if (out != d_table_spare_) HIP_OK(hipFree(out));
   }
   span("ck.j.table");
   // needNumRecordCache regions + their arena entries (arena capacity first: the table's `need`
   // links are physical slots of an arena of that size)
+  w.pod(cfg_.arena_cap);
+  w.pod(arena_head_);
+  w.pod<uint64_t>(regions_.size());
+  for (const Region& r : regions_) { w.pod(r.lo); w.pod(r.hi); w.pod(r.exp); }
   const uint64_t lo = regions_.empty() ? arena_head_ : regions_.front().lo;
-  PodBuf<NeedEnt> ents;
-  ents.resize_uninit((size_t)(arena_head_ - lo));
-  if (!ents.empty()) {  // the live range of the arena ring in (at most) two copies, not one per entry
+  const size_t n_ents = (size_t)(arena_head_ - lo);
+  w.pod<uint64_t>(n_ents);
+  const size_t ents_off = w.mem_pos();
+  if (n_ents) {  // the live range of the arena ring in (at most) two copies, not one per entry
     const uint64_t cap = cfg_.arena_cap, first = lo & (cap - 1);
-    const uint64_t n1 = std::min<uint64_t>(ents.size(), cap - first);
-    if (!h_ck_bounce_) HIP_OK(hipHostMalloc((void**)&h_ck_bounce_, kCkBounce, hipHostMallocDefault));
-    d2h_bounced(ents.data(), d_arena_ + first, (size_t)n1 * sizeof(NeedEnt), st, h_ck_bounce_, kCkBounce);
-    if (ents.size() > n1)
-      d2h_bounced(ents.data() + n1, d_arena_, (size_t)(ents.size() - n1) * sizeof(NeedEnt), st, h_ck_bounce_, kCkBounce);
+    const uint64_t n1 = std::min<uint64_t>(n_ents, cap - first);
+    write_dev(w, d_arena_ + first, (size_t)n1 * sizeof(NeedEnt), st, h_ck_bounce_, kCkBounce);
+    if (n_ents > n1) write_dev(w, d_arena_, (size_t)(n_ents - n1) * sizeof(NeedEnt), st, h_ck_bounce_, kCkBounce);
   }
   span("ck.j.arena");
   // chain blocks reachable from the live state, renumbered 1..n in the file.  Only those blocks
-  // are read (gathered on the device one chain level at a time): the whole pool is ~256 MB and
-  // its copy was most of a checkpoint's ingest stall once any chain existed.
+  // are read (gathered on the device one chain level at a time): the whole pool is ~256 MB.
+  auto get32 = [&](size_t off) { int32_t v; std::memcpy(&v, w.mem_at(off), 4); return v; };
+  auto put32 = [&](size_t off, int32_t v) { std::memcpy(w.mem_at(off), &v, 4); };
   struct Blk { uint8_t b[CHAIN_BLK]; };
   std::vector<Blk> blocks;
   {
-    // level 0: every chain head, with where its new number goes
-    std::vector<int32_t> cur;          // pool block numbers (1-based) to fetch
-    std::vector<int32_t*> slot_of;     // where each fetched block's new number is stored
-    for (KeyState& k : live) if (k.pblk) { cur.push_back(k.pblk); slot_of.push_back(&k.pblk); }
-    for (NeedEnt& e : ents) {
-      if (!e.key) { e.iblk = e.lblk = 0; continue; }
-      if (e.iblk) { cur.push_back(e.iblk); slot_of.push_back(&e.iblk); }
-      if (e.lblk) { cur.push_back(e.lblk); slot_of.push_back(&e.lblk); }
+    std::vector<int32_t> cur;      // pool block numbers (1-based) to fetch
+    std::vector<size_t> slot_of;   // level 0: where (writer offset) each head's new number goes
+    for (uint32_t i = 0; i < n_live; ++i) {
+      const size_t o = live_off + (size_t)i * sizeof(KeyState) + offsetof(KeyState, pblk);
+      if (const int32_t b = get32(o)) { cur.push_back(b); slot_of.push_back(o); }
+    }
+    for (size_t i = 0; i < n_ents; ++i) {
+      const size_t e = ents_off + i * sizeof(NeedEnt);
+      uint64_t key;
+      std::memcpy(&key, w.mem_at(e + offsetof(NeedEnt, key)), 8);
+      const size_t oi = e + offsetof(NeedEnt, iblk), ol = e + offsetof(NeedEnt, lblk);
+      if (!key) { put32(oi, 0); put32(ol, 0); continue; }
+      if (const int32_t b = get32(oi)) { cur.push_back(b); slot_of.push_back(oi); }
+      if (const int32_t b = get32(ol)) { cur.push_back(b); slot_of.push_back(ol); }
     }
     std::vector<int32_t> parent(cur.size(), -1);  // index in `blocks` of the predecessor (-1: a head)
     int32_t* d_idx = nullptr;
@@ -1192,7 +1199,7 @@ void DeviceJoin::save(BinWriter& w) {
       std::vector<int32_t> nxt, nparent;
       for (size_t i = 0; i < cur.size(); ++i) {
         const int32_t nb = (int32_t)(base + i + 1);  // new number of this block
-        if (parent[i] < 0) *slot_of[i] = nb;
+        if (parent[i] < 0) put32(slot_of[i], nb);
         else *(int32_t*)blocks[(size_t)parent[i]].b = nb;
         const int32_t next = *(const int32_t*)blocks[base + i].b;
         *(int32_t*)blocks[base + i].b = 0;
@@ -1200,19 +1207,34 @@ void DeviceJoin::save(BinWriter& w) {
       }
       cur.swap(nxt);
       parent.swap(nparent);
-      slot_of.assign(cur.size(), nullptr);
     }
     if (d_idx) { HIP_OK(hipFree(d_idx)); HIP_OK(hipFree(d_out)); }
   }
   span("ck.j.chains");
-  write_vec(w, live);
-  w.pod(cfg_.arena_cap);
-  w.pod(arena_head_);
-  w.pod<uint64_t>(regions_.size());
-  for (const Region& r : regions_) { w.pod(r.lo); w.pod(r.hi); w.pod(r.exp); }
-  write_vec(w, ents);
   w.vec(blocks);
-  span("ck.j.write");
+}
+
+void DeviceJoin::save(BinWriter& w) {
+  hipStream_t st = stream_;
+  save_spans.clear();
+  double sp0 = clock_ms();
+  auto span = [&](const char* name) { const double t = clock_ms(); save_spans.push_back({name, {sp0, t}}); sp0 = t; };
+  HIP_OK(hipStreamSynchronize(st));
+  HIP_OK(hipMemcpy(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost));
+  w.pod(*h_counts_);
+  for (uint64_t v : {events_, tx_, tx_db_, audit_errors_, host_pm_, host_invalid_acct_, host_events_}) w.pod(v);
+  // key table, need arena and chain blocks: built straight into a memory writer (the async
+  // checkpoint's own; a file writer gets them spliced in), so the ~100 MB of live key slots are
+  // copied once (pinned bounce -> snapshot) and the chain numbers are fixed up in place
+  if (w.is_memory()) {
+    save_tables(w);
+  } else {
+    BinWriter mw{BinWriter::Memory{}};
+    save_tables(mw);
+    const MemBlob b = mw.take_memory();
+    w.raw(b.data(), b.size());
+  }
+  sp0 = clock_ms();
   // SOAP contexts of every file
   {
     std::vector<SoapState> ss(files_->size());

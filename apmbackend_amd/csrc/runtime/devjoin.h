@@ -171,6 +171,7 @@ class DeviceJoin {
                     std::vector<HostOp>& hops, std::string& hbuf);
   void host_event(PrepassTask& t, const Event& e, uint32_t ev, const uint8_t* host_bytes);
   void on_app(PrepassTask& t, const Event& e, uint32_t ev, std::string_view line);
+  void save_tables(class BinWriter& w);  // checkpoint: key table, need arena, chain blocks (memory writer)
   // K5 carry: generation g of the audit state (devjoin_api.h AudGen); capacity for the next batch
   void aud_reserve(AudGen& g, uint32_t autr, uint32_t items, uint64_t txt);
   int32_t intern_name(const std::string& s);
