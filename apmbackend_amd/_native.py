@@ -31,12 +31,37 @@ def load(build_if_missing: bool = True):
         from .build_native import build
         build(verbose=False)
     try:
-        _mod = importlib.import_module("apmbackend_amd._apm_native")
+        mod = importlib.import_module("apmbackend_amd._apm_native")
     except ImportError as e:  # pragma: no cover - exercised only on broken installs
         raise RuntimeError(
             "apmbackend_amd native extension is missing or failed to load; run "
             "`python -m apmbackend_amd.build_native` (hipcc, gfx950)") from e
+    check_provenance(mod)
+    _mod = mod
     return _mod
+
+
+def check_provenance(mod, strict=None):
+    """The .so carries the sha256 of the csrc/ tree it was linked from.  A mismatch with the
+    sources next to it (a stale build shipped with a newer tree) is an error on a GPU box -- the
+    tests and the bench must run the code at HEAD -- and a warning elsewhere.  APM_ALLOW_STALE_NATIVE=1
+    downgrades it (A/B experiments with a deliberately old build)."""
+    from .build_native import CSRC, csrc_hash
+    embedded = mod.csrc_hash() if hasattr(mod, "csrc_hash") else "<none>"
+    if not os.path.isdir(CSRC):  # an installed package without sources: nothing to compare
+        return embedded
+    here = csrc_hash()
+    if embedded == here:
+        return embedded
+    msg = (f"stale native extension: {mod.__file__} was built from csrc hash {embedded}, the sources here "
+           f"hash to {here}; rebuild with `python -m apmbackend_amd.build_native`")
+    if strict is None:
+        strict = torch.cuda.is_available() and os.environ.get("APM_ALLOW_STALE_NATIVE") != "1"
+    if strict:
+        raise RuntimeError(msg)
+    import warnings
+    warnings.warn(msg)
+    return embedded
 
 
 def gpu_available() -> bool:

@@ -52,7 +52,38 @@ def _headers_mtime() -> float:
     return max((os.path.getmtime(h) for h in hs), default=0.0)
 
 
+def csrc_hash() -> str:
+    """sha256 over every native source (path + bytes), embedded in the .so at link time so
+    ``_native.load()`` can refuse an extension built from a different tree."""
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(CSRC, "**", "*"), recursive=True))
+    for f in files:
+        if os.path.isfile(f) and f.endswith((".hip", ".cpp", ".h")):
+            h.update(os.path.relpath(f, CSRC).encode() + b"\0")
+            with open(f, "rb") as fh:
+                h.update(fh.read())
+            h.update(b"\0")
+    return h.hexdigest()[:32]
+
+
+def _provenance_src(digest: str) -> str:
+    """A generated translation unit holding the source hash (rewritten only when it changes)."""
+    path = os.path.join(BUILD, "provenance.cpp")
+    text = f'extern "C" const char* apm_csrc_hash() {{ return "{digest}"; }}\n'
+    old = None
+    if os.path.exists(path):
+        with open(path) as fh:
+            old = fh.read()
+    if old != text:
+        with open(path, "w") as fh:
+            fh.write(text)
+    return path
+
+
 def _obj(src: str) -> str:
+    if not os.path.abspath(src).startswith(CSRC + os.sep):
+        return os.path.join(BUILD, os.path.basename(src) + ".o")
     rel = os.path.relpath(src, CSRC).replace(os.sep, "_")
     return os.path.join(BUILD, rel + ".o")
 
@@ -71,17 +102,26 @@ def _compile(src: str, is_hip: bool, force: bool, hmt: float) -> str:
     return obj
 
 
+LAST_BUILD = {"relinked": False, "compiled": 0, "hash": None}
+
+
 def build(force: bool = False, jobs: int = 0, verbose: bool = True) -> str:
     os.makedirs(BUILD, exist_ok=True)
     hips, cpps = _sources()
+    digest = csrc_hash()
+    cpps = cpps + [_provenance_src(digest)]
     hmt = _headers_mtime()
+    before = {s: (os.path.getmtime(_obj(s)) if os.path.exists(_obj(s)) else 0.0) for s in hips + cpps}
     jobs = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(jobs) as ex:
         futs = [ex.submit(_compile, s, True, force, hmt) for s in hips]
         futs += [ex.submit(_compile, s, False, force, hmt) for s in cpps]
         objs = [f.result() for f in futs]
     newest = max(os.path.getmtime(o) for o in objs)
+    LAST_BUILD.update(relinked=False, hash=digest,
+                      compiled=sum(1 for s_ in hips + cpps if os.path.getmtime(_obj(s_)) != before[s_]))
     if force or not os.path.exists(TARGET) or os.path.getmtime(TARGET) < newest:
+        LAST_BUILD["relinked"] = True
         cmd = [hipcc(), "-shared", f"--offload-arch={ARCH}", "-o", TARGET + ".tmp"] + objs + [
             "-L" + os.path.join(ROCM, "lib"), "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx", "-Wl,-rpath," + os.path.join(ROCM, "lib"),
             "-lpthread"]

@@ -102,6 +102,7 @@ EngineConfig config_from(const py::dict& d) {
   c.join_threads = get<int>(d, "join_threads", c.join_threads);
   c.pin_threads = get<bool>(d, "pin_threads", c.pin_threads);
   c.coll_timeout_ms = get<double>(d, "coll_timeout_ms", c.coll_timeout_ms);
+  c.coll_init_timeout_ms = get<double>(d, "coll_init_timeout_ms", c.coll_init_timeout_ms);
   c.node_cooldown = get<int>(d, "node_cooldown", c.node_cooldown);
   c.outputs = get<uint32_t>(d, "outputs", c.outputs);
   c.async_stats = get<int>(d, "async_stats", c.async_stats);
@@ -147,6 +148,7 @@ py::dict metrics_dict(const EngineMetrics& m) {
   d["t_join_shards_ms"] = m.t_join_shards_ms; d["t_merge_ms"] = m.t_merge_ms;
   d["t_shard_busy_ms"] = m.t_shard_busy_ms; d["t_shard_max_ms"] = m.t_shard_max_ms;
   d["t_out_ms"] = m.t_out_ms;
+  d["t_lockstep_ms"] = m.t_lockstep_ms; d["t_lockstep_max_ms"] = m.t_lockstep_max_ms;
   d["t_stats_tx_ms"] = m.t_stats_tx_ms; d["t_rollover_ms"] = m.t_rollover_ms;
   d["t_format_ms"] = m.t_format_ms; d["t_release_ms"] = m.t_release_ms;
   d["formatted_bytes"] = m.formatted_bytes; d["lockstep_rollovers"] = m.lockstep_rollovers; d["format_fallbacks"] = m.format_fallbacks;
@@ -256,8 +258,11 @@ class JoinHarness {
 
 }  // namespace
 
+extern "C" const char* apm_csrc_hash();  // build/native/provenance.cpp (generated at build time)
+
 PYBIND11_MODULE(_apm_native, m) {
   m.doc() = "apm-mi355x native runtime (HIP kernels for gfx950 + host runtime)";
+  m.def("csrc_hash", []() { return std::string(apm_csrc_hash()); });
   m.attr("EVENT_SIZE") = (int)sizeof(Event);
   m.def("hash_bytes", [](py::bytes b, uint64_t seed) {
     const std::string s = b;
@@ -449,7 +454,7 @@ PYBIND11_MODULE(_apm_native, m) {
       .def("fleet_info", [](Engine& e) {
         py::dict d;
         const auto i = e.fleet_info();
-        d["slots"] = i[0]; d["registry_rounds"] = i[1]; d["registry_overflow"] = i[2]; d["fb_rows"] = i[3];
+        d["slots"] = i[0]; d["registry_rounds"] = i[1]; d["registry_overflow"] = i[2]; d["fb_rows"] = i[3]; d["nranks"] = i[4];
         return d;
       })
       .def("fleet_init_local", [](Engine& e, std::shared_ptr<LocalGroup> g, int rank, int32_t cap, bool lockstep) {

@@ -1675,73 +1675,106 @@ __global__ void k_gather_len(const int64_t* __restrict__ gid, int64_t n_upper, c
   lens[i] = i >= n ? 0u : (uint32_t)((uint64_t)gid[i] & 0xfffffu) + 1u;
 }
 
-// Released lines out of the text ring into one contiguous blob, output-centric: one lane per
-// 16-byte output chunk.  The block's first and last line are found by two lanes (binary search
-// over the line offsets) and shared through LDS, so each lane searches only the ~30 lines of its
-// block; a chunk inside one line is read with two aligned 16-byte loads and a byte funnel shift
-// (v_alignbyte), a chunk across line ends byte by byte; every lane writes one 16-byte store.
-__device__ __forceinline__ uint32_t line_of(const uint32_t* __restrict__ offs, int64_t lo, int64_t hi, uint64_t pos) {
-  // last l in [lo, hi) with offs[l] <= pos
-  while (hi - lo > 1) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (offs[mid] <= pos) lo = mid; else hi = mid;
+// Released lines out of the text ring into one contiguous blob, line-block-centric.  A block
+// owns GL_LINES consecutive output lines: their offsets and ring positions are staged in LDS by
+// one coalesced load, then the block's lanes copy the block's byte range in 16-byte output
+// chunks -- the chunk's line by a binary search over the LDS offsets, the bytes by aligned
+// 16-byte ring loads and a byte funnel shift (v_alignbyte), two lines merged by a byte mask,
+// one 16-byte store.  (The previous output-centric kernel searched the line offsets in HBM: a
+// chain of ~20 dependent global loads per block before any byte moved -- 22-26 GB/s.)
+constexpr int GL_LINES = 128;
+constexpr int GL_TB = 256;
+
+// 16 bytes at byte offset o (0..16) of the 32-byte window w[0..7]
+__device__ __forceinline__ uint4 window16(const uint32_t (&w)[8], uint32_t o) {
+  const uint32_t q = o >> 2, rb = o & 3u;
+  uint32_t d[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const uint32_t a0 = w[k < 8 ? k : 7], a1 = w[k + 1 < 8 ? k + 1 : 7], a2 = w[k + 2 < 8 ? k + 2 : 7],
+                   a3 = w[k + 3 < 8 ? k + 3 : 7], a4 = w[k + 4 < 8 ? k + 4 : 7];
+    d[k] = q == 0 ? a0 : q == 1 ? a1 : q == 2 ? a2 : q == 3 ? a3 : a4;
   }
-  return (uint32_t)lo;
+  uint4 r;
+  r.x = __builtin_amdgcn_alignbyte(d[1], d[0], rb);
+  r.y = __builtin_amdgcn_alignbyte(d[2], d[1], rb);
+  r.z = __builtin_amdgcn_alignbyte(d[3], d[2], rb);
+  r.w = __builtin_amdgcn_alignbyte(d[4], d[3], rb);
+  return r;
 }
 
-__global__ __launch_bounds__(256) void k_gather_copy(const int64_t* __restrict__ gid, int64_t n,
-                                                     const char* __restrict__ ring, uint64_t ring_cap,
-                                                     const uint32_t* __restrict__ offs, char* __restrict__ out) {
-  __shared__ uint32_t blk[2];
-  const uint32_t total = offs[n];
-  const uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x * 16;
-  if (b0 >= total) return;  // (uniform per block)
-  if (threadIdx.x < 2) {
-    const uint64_t pos = threadIdx.x == 0 ? b0 : min<uint64_t>(b0 + (uint64_t)blockDim.x * 16, total) - 1;
-    blk[threadIdx.x] = line_of(offs, 0, n, pos);
-  }
+// 16 bytes starting at p, of which only the first `avail` (>= 1) are known to be inside the
+// line (the ring allocation): the second aligned block is loaded only when those bytes reach it.
+__device__ __forceinline__ uint4 load_line16(const char* p, uint32_t avail) {
+  const uint32_t sh = (uint32_t)((uintptr_t)p & 15u);
+  const uint4* pa = reinterpret_cast<const uint4*>(p - sh);
+  const uint4 v0 = pa[0];
+  const uint4 v1 = sh + avail > 16u ? pa[1] : v0;
+  const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+  return window16(w, sh);
+}
+
+// bytes [0, k) from a, [k, 16) from b
+__device__ __forceinline__ uint4 merge16(uint4 a, uint4 b, uint32_t k) {
+  auto m = [k](uint32_t x, uint32_t y, uint32_t i) -> uint32_t {
+    const uint32_t lo = 4u * i;
+    if (k >= lo + 4u) return x;
+    if (k <= lo) return y;
+    const uint32_t mask = (1u << (8u * (k - lo))) - 1u;
+    return (x & mask) | (y & ~mask);
+  };
+  return make_uint4(m(a.x, b.x, 0), m(a.y, b.y, 1), m(a.z, b.z, 2), m(a.w, b.w, 3));
+}
+
+__global__ __launch_bounds__(GL_TB) void k_gather_lines(const int64_t* __restrict__ gid, int64_t n,
+                                                        const char* __restrict__ ring, uint64_t ring_cap,
+                                                        const uint32_t* __restrict__ offs, char* __restrict__ out) {
+  __shared__ uint32_t s_off[GL_LINES + 1];
+  __shared__ uint64_t s_src[GL_LINES];
+  const int64_t l0 = (int64_t)blockIdx.x * GL_LINES;
+  const int cnt = (int)min<int64_t>(GL_LINES, n - l0);
+  for (int i = threadIdx.x; i <= cnt; i += GL_TB) s_off[i] = offs[l0 + i];
+  for (int i = threadIdx.x; i < cnt; i += GL_TB) s_src[i] = ((uint64_t)gid[l0 + i] >> 20) & (ring_cap - 1);
   __syncthreads();
-  const uint64_t start = b0 + (uint64_t)threadIdx.x * 16;
-  if (start >= total) return;
-  int64_t l = line_of(offs, blk[0], (int64_t)blk[1] + 1, start);
-  uint32_t l_off = offs[l], l_end = offs[l + 1];
-  const char* src = ring + (((uint64_t)gid[l] >> 20) & (ring_cap - 1));
-  const uint32_t m = (uint32_t)min<uint64_t>(16, total - start);
-  uint4 r;
-  if (m == 16 && start + 16 <= l_end) {
-    const char* p = src + (start - l_off);
-    const uint32_t sh = (uint32_t)((uintptr_t)p & 15u);
-    const uint4* pa = reinterpret_cast<const uint4*>(p - sh);
-    const uint4 v0 = pa[0];
-    const uint4 v1 = sh ? pa[1] : v0;  // (the second block holds bytes of this line: in the ring)
-    const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-    const uint32_t q = sh >> 2, rb = sh & 3u;
-    uint32_t d[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      const uint32_t a0 = w[k], a1 = w[k < 7 ? k + 1 : 7], a2 = w[k < 6 ? k + 2 : 7], a3 = w[k < 5 ? k + 3 : 7];
-      d[k] = q == 0 ? a0 : q == 1 ? a1 : q == 2 ? a2 : a3;
+  const uint32_t O0 = s_off[0], O1 = s_off[cnt];
+  const uint32_t c0 = O0 >> 4, c1 = (O1 + 15u) >> 4;
+  int lo_hint = 0;
+  for (uint32_t c = c0 + threadIdx.x; c < c1; c += GL_TB) {
+    const uint32_t p = c << 4;
+    // last line l with s_off[l] <= max(p, O0) (chunks advance, so the search starts at the hint)
+    const uint32_t q = p < O0 ? O0 : p;
+    int lo = lo_hint, hi = cnt;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (s_off[mid] <= q) lo = mid; else hi = mid;
     }
-    r.x = __builtin_amdgcn_alignbyte(d[1], d[0], rb);
-    r.y = __builtin_amdgcn_alignbyte(d[2], d[1], rb);
-    r.z = __builtin_amdgcn_alignbyte(d[3], d[2], rb);
-    r.w = __builtin_amdgcn_alignbyte(d[4], d[3], rb);
-    *reinterpret_cast<uint4*>(out + start) = r;
-    return;
-  }
-  union { uint4 v; char b[16]; } u;
-  for (uint32_t k = 0; k < m; ++k) {
-    const uint32_t pos = (uint32_t)start + k;
-    while (pos >= l_end) {  // next line (lines are never empty: each ends with '\n')
-      ++l;
-      l_off = l_end;
-      l_end = offs[l + 1];
-      src = ring + (((uint64_t)gid[l] >> 20) & (ring_cap - 1));
+    lo_hint = lo;
+    if (p >= O0 && p + 16u <= O1) {
+      const uint32_t eA = s_off[lo + 1];
+      const char* a = ring + s_src[lo] + (p - s_off[lo]);
+      if (p + 16u <= eA) {  // one line
+        *reinterpret_cast<uint4*>(out + p) = load_line16(a, 16u);
+        continue;
+      }
+      if (lo + 2 <= cnt && p + 16u <= s_off[lo + 2]) {  // two lines: A's tail, then B's head
+        const uint32_t dA = eA - p;  // 1..15
+        const uint4 va = load_line16(a, dA);
+        const uint4 vb = load_line16(ring + s_src[lo + 1], 16u - dA);
+        const uint32_t w[8] = {0u, 0u, 0u, 0u, vb.x, vb.y, vb.z, vb.w};
+        *reinterpret_cast<uint4*>(out + p) = merge16(va, window16(w, 16u - dA), dA);
+        continue;
+      }
     }
-    u.b[k] = src[pos - l_off];
+    // block edges (bytes of a neighbouring block are not ours) and chunks over 3+ lines: bytes
+    int l = lo;
+    for (uint32_t k = 0; k < 16u; ++k) {
+      const uint32_t pos = p + k;
+      if (pos < O0) continue;
+      if (pos >= O1) break;
+      while (pos >= s_off[l + 1]) ++l;
+      out[pos] = ring[s_src[l] + (pos - s_off[l])];
+    }
   }
-  if (m == 16) *reinterpret_cast<uint4*>(out + start) = u.v;
-  else for (uint32_t k = 0; k < m; ++k) out[start + k] = u.b[k];
 }
 
 __global__ __launch_bounds__(1024) void k_min_pos(const int64_t* __restrict__ gid, int64_t n, unsigned long long* out) {
@@ -2165,9 +2198,9 @@ int apm_dj_gather_plan(const int64_t* gid, int64_t n_upper, const int64_t* d_n, 
 void apm_dj_gather_copy(const int64_t* gid, int64_t n, const char* ring, uint64_t ring_cap, const uint32_t* offs,
                         char* out, uint64_t total_bytes, hipStream_t s) {
   if (n <= 0 || total_bytes == 0) return;
-  const uint64_t chunks = (total_bytes + 15) / 16;
-  hipLaunchKernelGGL(k_gather_copy, dim3((unsigned)((chunks + TB - 1) / TB)), dim3(TB), 0, s, gid, n, ring, ring_cap,
-                     offs, out);
+  (void)total_bytes;  // (the blocks derive their byte ranges from offs)
+  hipLaunchKernelGGL(k_gather_lines, dim3((unsigned)((n + GL_LINES - 1) / GL_LINES)), dim3(GL_TB), 0, s, gid, n, ring,
+                     ring_cap, offs, out);
 }
 
 void apm_dj_min_pos(const int64_t* gid, int64_t n, unsigned long long* out, hipStream_t s) {

@@ -425,18 +425,37 @@ void Engine::write_small_sections(BinWriter& w) {
     const int32_t cap = cfg_.cell_cap;
     const uint64_t N = (uint64_t)k * (uint64_t)n;
     std::vector<uint32_t> bnd((size_t)k + 1, 0);
+    // the packing scratch is about one more copy of the window cells: when HBM cannot hold it the
+    // cells are packed on the host instead (slower, same bytes) -- a checkpoint never fails on it
+    bool dev_pack = false;
     if (N) {
       if (N + 1 > ck_pack_n_) {
-        for (void* q : {(void*)d_ck_lens_, (void*)d_ck_offs_, (void*)d_ck_packed_, d_ck_ptmp_})
-          if (q) HIP_OK(hipFree(q));
-        ck_pack_n_ = (N + 1) * 5 / 4;
-        ck_ptmp_bytes_ = apm_ck_pack_tmp_bytes(ck_pack_n_);
-        HIP_OK(hipMalloc((void**)&d_ck_lens_, ck_pack_n_ * 4));
-        HIP_OK(hipMalloc((void**)&d_ck_offs_, ck_pack_n_ * 4));
-        HIP_OK(hipMalloc((void**)&d_ck_packed_, ck_pack_n_ * (size_t)cap * 4));
-        HIP_OK(hipMalloc(&d_ck_ptmp_, ck_ptmp_bytes_));
+        auto drop = [this]() {
+          for (void** q : {(void**)&d_ck_lens_, (void**)&d_ck_offs_, (void**)&d_ck_packed_, &d_ck_ptmp_}) {
+            dfree(*q);
+            *q = nullptr;
+          }
+          ck_pack_n_ = 0;
+          ck_ptmp_bytes_ = 0;
+        };
+        drop();
+        const uint64_t want = (N + 1) * 5 / 4;
+        const size_t tb = apm_ck_pack_tmp_bytes(want);
+        d_ck_lens_ = (uint32_t*)dmalloc_try(want * 4);
+        d_ck_offs_ = (uint32_t*)dmalloc_try(want * 4);
+        d_ck_packed_ = (int32_t*)dmalloc_try(want * (size_t)cap * 4);
+        d_ck_ptmp_ = dmalloc_try(tb);
+        if (d_ck_lens_ && d_ck_offs_ && d_ck_packed_ && d_ck_ptmp_) {
+          ck_pack_n_ = want;
+          ck_ptmp_bytes_ = tb;
+        } else {
+          drop();
+        }
       }
-      if (!d_ck_slots_) HIP_OK(hipMalloc((void**)&d_ck_slots_, NSLOT * 4));
+      if (!d_ck_slots_) d_ck_slots_ = (int32_t*)dmalloc_try(NSLOT * 4);
+      dev_pack = ck_pack_n_ >= N + 1 && d_ck_slots_;
+    }
+    if (dev_pack) {
       HIP_OK(hipMemcpyAsync(d_ck_slots_, slots.data(), (size_t)k * 4, hipMemcpyHostToDevice, stream_));
       if (apm_ck_pack_cells(d_counts_cells_, d_cells_, d_ck_slots_, k, n, S, cap, d_ck_lens_, d_ck_offs_, d_ck_ptmp_,
                             ck_ptmp_bytes_, d_ck_packed_, stream_) != 0)
@@ -450,9 +469,20 @@ void Engine::write_small_sections(BinWriter& w) {
       w.pod<int32_t>(slot);
       w.pod<uint64_t>((uint64_t)n);  // counts (vec layout)
       write_dev(w, d_counts_cells_ + (size_t)slot * S, (size_t)n * 4, stream_, (char*)bounce, kBounce);
-      const uint64_t tot = bnd[(size_t)i + 1] - bnd[(size_t)i];
-      w.pod<uint64_t>(tot);  // packed cells (vec layout)
-      write_dev(w, d_ck_packed_ + bnd[(size_t)i], (size_t)tot * 4, stream_, (char*)bounce, kBounce);
+      if (dev_pack) {
+        const uint64_t tot = bnd[(size_t)i + 1] - bnd[(size_t)i];
+        w.pod<uint64_t>(tot);  // packed cells (vec layout)
+        write_dev(w, d_ck_packed_ + bnd[(size_t)i], (size_t)tot * 4, stream_, (char*)bounce, kBounce);
+      } else {  // host packing (no HBM for the scratch)
+        std::vector<int32_t> cnt((size_t)n), cells((size_t)n * cap), packed;
+        d2h_bounced(cnt.data(), d_counts_cells_ + (size_t)slot * S, (size_t)n * 4, stream_, (char*)bounce, kBounce);
+        d2h_bounced(cells.data(), d_cells_ + (size_t)slot * S * cap, (size_t)n * cap * 4, stream_, (char*)bounce, kBounce);
+        for (int32_t j = 0; j < n; ++j) {
+          const int32_t c = std::max(0, std::min(cnt[(size_t)j], cap));
+          packed.insert(packed.end(), cells.begin() + (ptrdiff_t)j * cap, cells.begin() + (ptrdiff_t)j * cap + c);
+        }
+        w.vec(packed);
+      }
       const int32_t ns = std::min(spill_n[slot], cfg_.spill_cap);
       w.pod(spill_n[slot]);
       d2h_vec(w, d_spill_series_ + (size_t)slot * cfg_.spill_cap, (size_t)ns, stream_, bounce);
@@ -514,14 +544,25 @@ void Engine::write_small_sections(BinWriter& w) {
       if (!tot[k]) continue;
       const size_t need = ((size_t)tot[k] + 15) & ~(size_t)15;
       if (need > ck_text_cap_[k]) {
-        if (d_ck_text_[k]) HIP_OK(hipFree(d_ck_text_[k]));
+        dfree(d_ck_text_[k]);
         ck_text_cap_[k] = need + need / 4;
-        HIP_OK(hipMalloc((void**)&d_ck_text_[k], ck_text_cap_[k]));
+        d_ck_text_[k] = (char*)dmalloc_try(ck_text_cap_[k]);
+        if (!d_ck_text_[k]) ck_text_cap_[k] = 0;
       }
-      apm_dj_gather_copy(srcs[k], cnt[k], dj_->ring(), dj_->ring_cap(), d_rel_offs_, d_ck_text_[k], tot[k], stream_);
+      if (d_ck_text_[k])
+        apm_dj_gather_copy(srcs[k], cnt[k], dj_->ring(), dj_->ring_cap(), d_rel_offs_, d_ck_text_[k], tot[k], stream_);
     }
     w.pod<uint64_t>((uint64_t)tot[0] + tot[1]);
-    for (int k = 0; k < 2; ++k) write_dev(w, d_ck_text_[k], tot[k], stream_, (char*)bounce, kBounce);
+    for (int k = 0; k < 2; ++k) {
+      if (!tot[k]) continue;
+      if (d_ck_text_[k] && ck_text_cap_[k] >= tot[k]) {
+        write_dev(w, d_ck_text_[k], tot[k], stream_, (char*)bounce, kBounce);
+      } else {  // no HBM for the gather target: line by line out of the ring on the host
+        const std::string t = ring_text(srcs[k], cnt[k]);
+        if (t.size() != tot[k]) throw std::runtime_error("checkpoint: pending-line text size changed");
+        w.raw(t.data(), t.size());
+      }
+    }
   } else {
     d2h_vec(w, d_tail_gid_, (size_t)tail_n_, stream_);
     w.pod<uint64_t>(line_blocks_.size());

@@ -29,11 +29,51 @@ namespace {
 
 class RcclCollective final : public Collective {
  public:
-  RcclCollective(const std::vector<uint8_t>& uid, int nranks, int rank) : n_(nranks), r_(rank) {
+  RcclCollective(const std::vector<uint8_t>& uid, int nranks, int rank, double init_timeout_ms)
+      : n_(nranks), r_(rank) {
     if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("bad RCCL unique id size");
+    if (rank < 0 || rank >= nranks) throw std::runtime_error("RCCL: rank out of range");
+    // The blocking init runs on a helper thread bound to this thread's device; the caller waits
+    // on a deadline.  State lives in a shared block so an abandoned init can still finish (or
+    // stay blocked) without touching this object.
+    struct Init {
+      std::mutex mu;
+      std::condition_variable cv;
+      bool done = false;
+      ncclResult_t res = ncclInternalError;
+      ncclComm_t comm = nullptr;
+    };
+    auto st = std::make_shared<Init>();
     ncclUniqueId id;
     std::memcpy(&id, uid.data(), sizeof(id));
-    if (ncclCommInitRank(&comm_, nranks, id, rank) != ncclSuccess) throw std::runtime_error("ncclCommInitRank failed");
+    int dev = 0;
+    HIP_OK(hipGetDevice(&dev));
+    std::thread([st, id, nranks, rank, dev]() {
+      ncclComm_t c = nullptr;
+      ncclResult_t r = hipSetDevice(dev) == hipSuccess ? ncclCommInitRank(&c, nranks, id, rank) : ncclUnhandledCudaError;
+      std::lock_guard<std::mutex> g(st->mu);
+      st->res = r;
+      st->comm = c;
+      st->done = true;
+      st->cv.notify_all();
+    }).detach();
+    std::unique_lock<std::mutex> lk(st->mu);
+    const bool ok = st->cv.wait_for(lk, std::chrono::microseconds((int64_t)(init_timeout_ms * 1000)),
+                                    [&]() { return st->done; });
+    if (!ok)
+      throw std::runtime_error("RCCL communicator init did not complete within " +
+                               std::to_string((long long)(init_timeout_ms / 1000)) + " s (rank " +
+                               std::to_string(rank) + " of " + std::to_string(nranks) +
+                               "): a peer rank never joined (crashed before init, different world size, "
+                               "or two ranks on one GPU -- use gpu.collectiveBackend=host for that)");
+    if (st->res != ncclSuccess)
+      throw std::runtime_error(std::string("ncclCommInitRank failed (rank ") + std::to_string(rank) + " of " +
+                               std::to_string(nranks) + "): " + ncclGetErrorString(st->res));
+    comm_ = st->comm;
+    int cnt = 0;
+    if (ncclCommCount(comm_, &cnt) != ncclSuccess || cnt != nranks)
+      throw std::runtime_error("RCCL communicator has " + std::to_string(cnt) + " ranks, expected " +
+                               std::to_string(nranks));
   }
   ~RcclCollective() override {
     if (comm_ && !aborted_) ncclCommDestroy(comm_);  // an aborted communicator is already freed
@@ -79,8 +119,9 @@ std::vector<uint8_t> rccl_unique_id() {
   return std::vector<uint8_t>((uint8_t*)&id, (uint8_t*)&id + sizeof(id));
 }
 
-std::unique_ptr<Collective> make_rccl_collective(const std::vector<uint8_t>& uid, int nranks, int rank) {
-  return std::unique_ptr<Collective>(new RcclCollective(uid, nranks, rank));
+std::unique_ptr<Collective> make_rccl_collective(const std::vector<uint8_t>& uid, int nranks, int rank,
+                                                 double init_timeout_ms) {
+  return std::unique_ptr<Collective>(new RcclCollective(uid, nranks, rank, init_timeout_ms));
 }
 
 // ----------------------------------------------------------------------- in-process group

@@ -44,7 +44,12 @@ class Collective {
 };
 
 std::vector<uint8_t> rccl_unique_id();
-std::unique_ptr<Collective> make_rccl_collective(const std::vector<uint8_t>& uid, int nranks, int rank);
+// ncclCommInitRank under a deadline: a rank whose peers never arrive (a rank that crashed before
+// its init, mismatched world sizes, two ranks on one device) throws a clear error after
+// `init_timeout_ms` instead of blocking forever.  The blocked init thread is abandoned; the
+// caller is expected to exit the process.
+std::unique_ptr<Collective> make_rccl_collective(const std::vector<uint8_t>& uid, int nranks, int rank,
+                                                 double init_timeout_ms = 120000.0);
 
 // In-process group of `n` ranks (test backend).  Each rank's engine runs on its own host thread;
 // a call blocks until all n ranks made it (timeout -> throws).

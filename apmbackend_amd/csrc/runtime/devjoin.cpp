@@ -1340,8 +1340,17 @@ void DeviceJoin::load(BinReader& rd) {
     auto ents = rd.vec<NeedEnt>();
     const uint64_t lo = regions_.empty() ? arena_head_ : regions_.front().lo;
     if (ents.size() != arena_head_ - lo) throw std::runtime_error("checkpoint: need arena size mismatch");
-    for (uint64_t v = lo; v < arena_head_; ++v)
-      HIP_OK(hipMemcpy(d_arena_ + (v & (cfg_.arena_cap - 1)), &ents[(size_t)(v - lo)], sizeof(NeedEnt), hipMemcpyHostToDevice));
+    // the live range [lo, head) of the ring: at most two bulk copies, split at the wrap point
+    // (mirrors save_tables; restore time no longer scales with one copy per entry)
+    const uint64_t cap = cfg_.arena_cap;
+    if (ents.size() > cap) throw std::runtime_error("checkpoint: need arena larger than the ring");
+    if (!ents.empty()) {
+      const uint64_t first = lo & (cap - 1);
+      const uint64_t n1 = std::min<uint64_t>(ents.size(), cap - first);
+      HIP_OK(hipMemcpy(d_arena_ + first, ents.data(), n1 * sizeof(NeedEnt), hipMemcpyHostToDevice));
+      if (ents.size() > n1)
+        HIP_OK(hipMemcpy(d_arena_, ents.data() + n1, (ents.size() - n1) * sizeof(NeedEnt), hipMemcpyHostToDevice));
+    }
   }
   {
     // chain blocks: saved 1..n, loaded into blocks 0..n-1 of a fresh pool whose first n ring

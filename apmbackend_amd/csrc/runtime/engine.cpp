@@ -213,6 +213,23 @@ void* Engine::dmalloc(size_t bytes) {
   HIP_OK(hipDeviceSynchronize());
   std::lock_guard<std::mutex> g(alloc_mu_);  // the stats thread and the rollover lane allocate
   allocations_.push_back(p);
+  alloc_bytes_[p] = bytes;
+  device_bytes_ += bytes;
+  return p;
+}
+
+// Optional scratch (checkpoint packing): nullptr instead of a throw when HBM is short, no zeroing
+// and no device-wide sync; counted in device_bytes_ and freed by dfree / the destructor.
+void* Engine::dmalloc_try(size_t bytes) {
+  void* p = nullptr;
+  bytes = (bytes + 255) & ~(size_t)255;
+  if (hipMalloc(&p, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> g(alloc_mu_);
+  allocations_.push_back(p);
+  alloc_bytes_[p] = bytes;
   device_bytes_ += bytes;
   return p;
 }
@@ -422,6 +439,14 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   const int nt_used = std::max(cfg_.join_threads > 0 ? cfg_.join_threads : 0, pool_->size());
   const int st_cpu = (int)lane_cpus_.size() > nt_used ? lane_cpus_[nt_used] : -1;
   const int out_cpu = (int)lane_cpus_.size() > nt_used + 1 ? lane_cpus_[nt_used + 1] : -1;
+  // The rollover lane mode is fixed before the first batch: node_round derives its candidate
+  // cutoff from it, so every rank must use the same rule from round 0 (and the ingest thread must
+  // never read a lane pointer the stats thread creates).  sx rows are decided on the stats thread.
+  {
+    const char* e = std::getenv("APM_ROLL_LANE");
+    roll_lane_mode_ = (!e || e[0] != '0') && !want(OUT_SX);
+    if (roll_lane_mode_) roll_lane_.reset(new TaskLane());
+  }
   stats_thread_ = std::thread([this, st_cpu]() {
     if (st_cpu >= 0) pin_current_thread(st_cpu);
     hipSetDevice(cfg_.device);
@@ -1006,7 +1031,10 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
     int64_t bmax = INT64_MIN;
     for (size_t k = 0; k < shards_.size(); ++k) bmax = std::max(bmax, shard_maxb_[k * 8]);
     lockstep_sync(bmax);
-    trace_event("lockstep", tl, now_ms(), 0);
+    const double te = now_ms();
+    metrics_.t_lockstep_ms += te - tl;
+    metrics_.t_lockstep_max_ms = std::max(metrics_.t_lockstep_max_ms, te - tl);
+    trace_event("lockstep", tl, te, 0);
   }
 
   // ---- stats / z-score / alerts: handed to the stats thread, overlapping the next batch's
@@ -1077,7 +1105,10 @@ void Engine::process_batch_dev_tail(ParseSlot& ps, double t0, double now_overrid
   if (lockstep_) {
     const double tl = now_ms();
     lockstep_sync(b.max_bucket);
-    trace_event("lockstep", tl, now_ms(), 0);
+    const double te = now_ms();
+    metrics_.t_lockstep_ms += te - tl;
+    metrics_.t_lockstep_max_ms = std::max(metrics_.t_lockstep_max_ms, te - tl);
+    trace_event("lockstep", tl, te, 0);
   }
   const double tp0 = now_ms();
   post_stats_dev(std::move(b), t0, lockstep_ ? sync_latest_ : INT64_MIN);
@@ -2080,9 +2111,7 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   roll_ring_base_ = cur_dj_ ? cur_dj_->ring_base : (dj_ ? dj_->ring_head() : 0);
   // The decision runs on the rollover lane as soon as the GPU chain is done, while this thread
   // goes on (APM_ROLL_LANE=0: decide right here, the previous behaviour; sx rows always here).
-  static const bool lane = [] { const char* e = std::getenv("APM_ROLL_LANE"); return !e || e[0] != '0'; }();
-  if (lane && !want(OUT_SX)) {
-    if (!roll_lane_) roll_lane_.reset(new TaskLane());
+  if (roll_lane_mode_) {
     roll_pending_ = false;
     roll_posted_ = true;
     roll_task_ = roll_lane_->post([this]() { finish_rollover_body(); });
@@ -2362,6 +2391,11 @@ void Engine::dfree(void* p) {
   HIP_OK(hipFree(p));
   std::lock_guard<std::mutex> g(alloc_mu_);
   allocations_.erase(std::remove(allocations_.begin(), allocations_.end(), p), allocations_.end());
+  auto it = alloc_bytes_.find(p);
+  if (it != alloc_bytes_.end()) {
+    device_bytes_ -= it->second;
+    alloc_bytes_.erase(it);
+  }
 }
 
 void* Engine::regrow(void* old, size_t& cap, size_t need) {
@@ -2374,7 +2408,11 @@ void* Engine::regrow(void* old, size_t& cap, size_t need) {
     HIP_OK(hipFree(old));
     std::lock_guard<std::mutex> g(alloc_mu_);
     allocations_.erase(std::remove(allocations_.begin(), allocations_.end(), old), allocations_.end());
-    device_bytes_ -= (cap + 255) & ~(size_t)255;
+    auto it = alloc_bytes_.find(old);
+    if (it != alloc_bytes_.end()) {
+      device_bytes_ -= it->second;
+      alloc_bytes_.erase(it);
+    }
   }
   cap = nc;
   return dmalloc(nc);
@@ -2994,7 +3032,7 @@ void Engine::fleet_init(const std::vector<uint8_t>& uid, const std::vector<uint8
   if (!clock_uid.empty() && clock_uid.size() != uid.size()) throw std::runtime_error("bad unique id size");
   if (cap <= 0) throw std::runtime_error("fleet_init: cap must be > 0");
   HIP_OK(hipSetDevice(cfg_.device));
-  coll_ = make_rccl_collective(uid, nranks, rank);
+  coll_ = make_rccl_collective(uid, nranks, rank, cfg_.coll_init_timeout_ms);
   fleet_setup(cap, !clock_uid.empty());
 }
 
@@ -3252,7 +3290,7 @@ void Engine::node_round(uint64_t round, bool wait, bool all) {
   // the candidates of batches <= q - 1 (whose lane work is long done), the drain everything.
   // Every rank uses the same rule, so the pools and decisions stay identical across ranks.
   uint64_t upto = round;
-  if (!all && roll_lane_) {
+  if (!all && roll_lane_mode_) {
     if (round == 0) upto = UINT64_MAX;  // nothing yet (seq_batch <= -1)
     else upto = round - 1;
   }

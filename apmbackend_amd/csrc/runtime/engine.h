@@ -92,6 +92,7 @@ struct EngineConfig {
   // RCCL watchdog: a collective not complete after this long (a dead or wedged peer) aborts the
   // communicator and throws, so the supervisor restarts the rank group from its checkpoint
   double coll_timeout_ms = 300000;
+  double coll_init_timeout_ms = 120000;  // RCCL communicator init deadline (fail fast, no silent hang)
   // lock-step ranks resolve the per-service alert cooldown node-wide: alert candidates are
   // all-gathered and decided in the global emission order (engine.cpp, "node-wide cooldown")
   int node_cooldown = 1;
@@ -179,6 +180,7 @@ struct EngineMetrics {
   double t_shard_busy_ms = 0, t_shard_max_ms = 0;              // per batch: mean / max of one shard's join
   double t_stats_tx_ms = 0, t_rollover_ms = 0, t_format_ms = 0, t_release_ms = 0;  // inside t_stats_ms
   double t_out_ms = 0;                        // output lane: released-line gather + st/fs emission
+  double t_lockstep_ms = 0, t_lockstep_max_ms = 0;  // ingest thread in the per-batch clock collective (sum / worst)
   std::vector<double> rollover_latency_ms;   // batch arrival -> alert decision per rollover
 };
 
@@ -335,7 +337,7 @@ class Engine {
   std::vector<std::string> fleet_slot_names() { flush(); return reg_names_; }
   std::vector<uint64_t> fleet_info() {
     flush();  // (waits for both emission lanes)
-    return {(uint64_t)reg_names_.size(), reg_rounds_, reg_overflow_, fb_rows_};
+    return {(uint64_t)reg_names_.size(), reg_rounds_, reg_overflow_, fb_rows_, (uint64_t)fleet_nranks_};
   }
   uint64_t fleet_rounds() const { return fleet_rounds_; }
   // node-wide sums of {ranks, batches, lines, events, bytes, tx, tx_db, released, rollovers,
@@ -403,6 +405,7 @@ class Engine {
   // with the next batch instead of waiting for its GPU chain.  The next rollover (or flush) waits
   // for it first; series_mu_ guards series_ growth against the lane's reads.
   std::unique_ptr<TaskLane> roll_lane_;
+  bool roll_lane_mode_ = false;  // fixed at construction (APM_ROLL_LANE, outputs): same on every rank
   uint64_t roll_task_ = 0;
   bool roll_posted_ = false;
   std::mutex series_mu_;
@@ -453,6 +456,7 @@ class Engine {
   void release_gather(int k, int64_t released);
   bool want(int k) const { return (cfg_.outputs >> k) & 1u; }
   void* dmalloc(size_t bytes);
+  void* dmalloc_try(size_t bytes);
   void require_fresh(const char* what);
   void trace_event(const char* name, double t0, double t1, int tid);
   bool trace_on_ = false;
@@ -610,6 +614,7 @@ class Engine {
   uint64_t formatted_bytes_lane_ = 0;  // st/fs bytes emitted by the lane (folded by flush)
   size_t device_bytes_ = 0;
   std::vector<void*> allocations_;
+  std::unordered_map<void*, size_t> alloc_bytes_;
 
   // files / servers / dictionaries
   std::vector<std::string> servers_;

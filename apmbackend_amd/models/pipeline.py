@@ -89,6 +89,7 @@ def engine_config(cfg: Dict[str, Any], device: int = 0, keep_text: bool = False,
         "join_threads": int(g.get("joinThreads", 0)),
         "pin_threads": bool(g.get("pinThreads", False)),
         "coll_timeout_ms": float(g.get("collectiveTimeoutSeconds", 300)) * 1000.0,
+        "coll_init_timeout_ms": float(g.get("collectiveInitTimeoutSeconds", 120)) * 1000.0,
         # lock-step ranks decide the alert cooldown node-wide (one alert per service per node)
         "node_cooldown": 1 if g.get("nodeCooldown", True) else 0,
         # K4/K6 join on the GPU (devjoin.hip); false = host join workers (join.cpp)

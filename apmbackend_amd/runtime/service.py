@@ -329,8 +329,21 @@ class IngestService:
                     self.native.add_file(f, KIND_CODE[file_kind(f)], self.server_of(f))
             return True
         except Exception as e:
-            log.error("checkpoint %s could not be loaded (%s); starting fresh", ck, e)
-            raise
+            if "unsupported version" not in str(e):
+                log.error("checkpoint %s could not be loaded (%s); refusing to start (move it aside to "
+                          "start fresh)", ck, e)
+                raise
+            # written by an older / newer build (incompatible section layout): keep it for
+            # inspection and start this shard fresh instead of crash-looping under the supervisor
+            stamp = time.strftime("%Y%m%d%H%M%S")
+            moved = []
+            for f in [ck] + glob.glob(ck[:-len(".ckpt")] + ".*.ckpt" if ck.endswith(".ckpt") else ck + ".*"):
+                if os.path.exists(f):
+                    os.replace(f, f"{f}.incompatible-{stamp}")
+                    moved.append(os.path.basename(f))
+            log.warning("checkpoint %s has an incompatible format version (%s): moved %s aside, starting this "
+                        "shard with fresh engine state", ck, e, ", ".join(moved))
+            return False
 
     def _import_reference(self, servers):
         """Cut-over from a running reference deployment: seed stats buckets, the release heap,

@@ -63,6 +63,7 @@ GPU_DEFAULTS: Dict[str, Any] = {
     "txTextRingMB": 4096,             # HBM ring holding pending (unreleased) tx lines
     "maxRawServices": 1 << 18,        # distinct (server, raw service name) pairs
     "collectiveTimeoutSeconds": 300,  # RCCL watchdog: abort + exit when a collective hangs this long
+    "collectiveInitTimeoutSeconds": 120,  # RCCL communicator init deadline (a peer that never joins -> clear error)
     "collectiveBackend": "rccl",      # node-wide exchanges: rccl (xGMI) or host (TCP via rank 0, ranks sharing a GPU)
     "checkpointDir": "",              # binary engine checkpoints (+ tail offsets) per rank
     "checkpointEverySeconds": 60,

@@ -116,6 +116,12 @@ def main():
     ap.add_argument("--encoder-threads", type=int, default=8)
     ap.add_argument("--writer-lanes", type=int, default=4, help="DB sink writer lanes (spool files / psql connections)")
     ap.add_argument("--join-threads", type=int, default=0, help="engine worker pool (0 = auto)")
+    ap.add_argument("--coll", default="auto", choices=["auto", "rccl", "host"],
+                    help="engine collectives at N > 1: rccl (one GPU per rank, xGMI) or host (TCP via rank 0; "
+                         "ranks sharing a GPU -- RCCL refuses two ranks on one device).  auto: rccl when every "
+                         "local rank has its own GPU")
+    ap.add_argument("--rank-report", default=None,
+                    help="directory: every rank writes rank<R>.json (its lines, node-wide counters, per-step times)")
     args = ap.parse_args()
     for k, v in PRESETS[args.preset].items():  # a preset overrides the defaults it names
         if getattr(args, k) == ap.get_default(k):
@@ -125,11 +131,27 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    n_dev = torch.cuda.device_count()  # (does not initialise the GPU)
+    if n_dev < 1:
+        raise SystemExit("bench.py needs a GPU")
+    device = local % n_dev
+    coll = args.coll
+    if coll == "auto":
+        coll = "rccl" if world == 1 or local_world <= n_dev else "host"
+    if coll == "rccl" and local_world > n_dev:
+        raise SystemExit(f"--coll rccl needs one GPU per rank ({local_world} local ranks, {n_dev} GPUs)")
     dist = None
     if world > 1:
+        # The bench's own group (start barrier, uid broadcast, final reductions) is gloo on the
+        # host: the engine's node-wide exchanges run on its own RCCL communicator (or the TCP host
+        # transport), so no torch NCCL communicator competes with it for the xGMI links.
+        import datetime
+
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=600))
+    torch.cuda.set_device(device)
 
     from apmbackend_amd import _native
     from apmbackend_amd.models.pipeline import APMEngine
@@ -175,7 +197,7 @@ def main():
     outs = DB_OUTPUTS + ("fb",)  # + the fleet-merged per-service baselines (rank 0, every interval)
     if args.jmx:
         outs = outs + ("sx",)
-    eng = APMEngine(cfg, device=local, outputs=outs)
+    eng = APMEngine(cfg, device=device, outputs=outs)
     sink_fd = os.open(args.sink, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
     inserter = spool_dir = None
     if args.db_sink != "none":
@@ -228,7 +250,16 @@ def main():
     # The fleet exchange (MFMA per-service Gram pack + RCCL all-reduce) and the lock-step clock
     # collective run at every N, so each rank does the same work at N = 1 and N = 8 (weak scaling).
     servers_all = [f"jvm{i:03d}" for i in range(world * args.servers)]  # every rank's SynthGen names
-    fleet = None if args.no_fleet else FleetBaseline(eng, world, rank, servers=servers_all)
+    fleet = None
+    if not args.no_fleet:
+        try:
+            fleet = FleetBaseline(eng, world, rank, servers=servers_all, backend=coll)
+        except RuntimeError as e:  # e.g. RCCL init deadline: fail fast, never hang the node
+            print(f"[bench rank {rank}] collective init failed: {e}", file=sys.stderr, flush=True)
+            os._exit(3)
+    comm_ranks = int(eng.eng.fleet_info()["nranks"]) if fleet is not None else 0
+    if fleet is not None and comm_ranks != world:
+        raise SystemExit(f"engine communicator has {comm_ranks} ranks, expected {world}")
     if args.trace:
         eng.eng.set_trace(True)
 
@@ -293,8 +324,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    step_ms = []
     for i in range(PRE, PRE + args.warmup + args.steps)[args.warmup:]:
+        ts = time.perf_counter()
         step(i)
+        step_ms.append(1000.0 * (time.perf_counter() - ts))
     eng.eng.flush()  # the last batch's stats stage runs on the engine's stats thread
     if inserter is not None:  # alerts paged + every DB row of the timed batches written
         al = eng.eng.take_bytes("al")
@@ -315,18 +349,30 @@ def main():
     out_bytes = {k: eng.eng.sink_bytes(k) for k in outs}
     lat = sorted(m1["rollover_latency_ms"][len(m0["rollover_latency_ms"]):]) or [float("nan")]
     p50 = lat[len(lat) // 2]
+    ss = sorted(step_ms)
+    step_p50, step_p99 = ss[len(ss) // 2], ss[min(len(ss) - 1, (99 * len(ss)) // 100)]
+    lock_ms = (m1["t_lockstep_ms"] - m0["t_lockstep_ms"]) / args.steps
     stats = torch.tensor([float(lines), dt, p50, float(m1["tx"] - m0["tx"]),
-                          float(m1["bytes"] - m0["bytes"])], dtype=torch.float64, device="cuda")
+                          float(m1["bytes"] - m0["bytes"]), step_p50, step_p99, ss[-1], lock_ms,
+                          m1["t_lockstep_max_ms"]], dtype=torch.float64)
     if dist is not None:
         summed = stats.clone()
         dist.all_reduce(summed, op=dist.ReduceOp.SUM)
         maxed = stats.clone()
         dist.all_reduce(maxed, op=dist.ReduceOp.MAX)
-        lines_total, dt_max, p50_max = summed[0].item(), maxed[1].item(), maxed[2].item()
-        tx_total, bytes_total = summed[3].item(), summed[4].item()
     else:
-        lines_total, dt_max, p50_max = lines, dt, p50
-        tx_total, bytes_total = float(m1["tx"] - m0["tx"]), float(m1["bytes"] - m0["bytes"])
+        summed = maxed = stats
+    lines_total, dt_max, p50_max = summed[0].item(), maxed[1].item(), maxed[2].item()
+    tx_total, bytes_total = summed[3].item(), summed[4].item()
+    node_m = eng.eng.node_metrics() if fleet is not None else []
+    if args.rank_report:
+        os.makedirs(args.rank_report, exist_ok=True)
+        with open(os.path.join(args.rank_report, f"rank{rank}.json"), "w") as fh:
+            json.dump({"rank": rank, "world": world, "device": device, "coll": coll, "comm_ranks": comm_ranks,
+                       "lines_timed": lines, "timed_s": dt, "lines_total": m1["lines"], "tx_total": m1["tx"],
+                       "node_metrics": list(node_m), "step_ms": [round(x, 4) for x in step_ms],
+                       "lockstep_ms_per_step": lock_ms, "lockstep_max_ms": m1["t_lockstep_max_ms"],
+                       "alerts": int(m1["alerts"])}, fh)
     value = lines_total / dt_max
     ref = _load_reference_baseline()
     if rank == 0:
@@ -334,7 +380,7 @@ def main():
             "metric": "log-lines/sec z-scored (whole node)",
             "value": round(value, 1),
             "unit": "lines/s",
-            "n_gpus": world,
+            "n_gpus": min(world, n_dev),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1000.0 * dt_max / args.steps, 3),
@@ -353,6 +399,15 @@ def main():
                 "preset": args.preset,
                 "ring_dtype": args.ring,
             },
+            "n_ranks": world,
+            "collective": coll,
+            "comm_nranks": comm_ranks,
+            "lines_total": int(lines_total),
+            "step_ms_p50": round(maxed[5].item(), 3),
+            "step_ms_p99": round(maxed[6].item(), 3),
+            "step_ms_max": round(maxed[7].item(), 3),
+            "t_lockstep_ms": round(maxed[8].item(), 4),
+            "t_lockstep_max_ms": round(maxed[9].item(), 3),
             "p50_ingest_to_alert_ms": round(p50_max, 3),
             "tx_per_s": round(tx_total / dt_max, 1),
             "ingest_GB_per_s": round(bytes_total / dt_max / 1e9, 3),
