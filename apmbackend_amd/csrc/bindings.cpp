@@ -302,6 +302,27 @@ PYBIND11_MODULE(_apm_native, m) {
       .def("set_override", [](Engine& e, const std::string& svc, const py::dict& d) { e.set_override(svc, override_from(d)); })
       .def("clear_overrides", &Engine::clear_overrides)
       .def("refresh_series_settings", &Engine::refresh_series_settings)
+      .def("stage_reconfig", [](Engine& e, const py::dict& ecfg, const py::dict& overrides, uint64_t gen) {
+        const EngineConfig c = config_from(ecfg);
+        ReconfigSpec r;
+        r.gen = gen;
+        r.n_lags = c.n_lags;
+        for (int l = 0; l < MAX_LAGS; ++l) {
+          r.lags[l] = c.lags[l]; r.thr[l] = c.thr[l]; r.infl[l] = c.infl[l]; r.lag_suppressed[l] = c.lag_suppressed[l];
+        }
+        r.alert_window = c.alert_window; r.alert_threshold = c.alert_threshold; r.both_only = c.both_only;
+        r.hard_min_ms = c.hard_min_ms; r.hard_min_tpm = c.hard_min_tpm; r.hard_max_ms = c.hard_max_ms;
+        r.cooldown_ms = c.cooldown_ms;
+        for (auto kv : overrides) r.overrides[kv.first.cast<std::string>()] = override_from(kv.second.cast<py::dict>());
+        e.stage_reconfig(r);
+      }, py::arg("ecfg"), py::arg("overrides"), py::arg("gen"))
+      .def("reconfig_info", [](Engine& e) {
+        py::dict d;
+        d["applied_gen"] = e.reconfig_applied_gen(); d["applied"] = e.reconfigs_applied();
+        d["lag_set_changes"] = e.lag_set_changes();
+        return d;
+      })
+      .def("lag_values", &Engine::lag_values)
       .def("process_batch",
            [](Engine& e, py::buffer buf, const std::vector<std::tuple<int32_t, uint64_t, uint64_t>>& chunks,
               double now) {

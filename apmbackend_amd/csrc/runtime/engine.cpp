@@ -1219,6 +1219,7 @@ void Engine::stats_worker() {
       stats_seq_ = job.seq;
       stats_round_ = job.round;
       apply_ctx_pending(job.seq);
+      apply_reconfig_pending(job.seq);
       node_take_text();  // al rows decided by the rollover lane / the node rounds
       trace_event("st.pre", t, now_ms(), 1);
       if (job.dev) {
@@ -1353,6 +1354,7 @@ void Engine::flush() {
   }
   if (!st_error_.empty()) { std::string e = st_error_; st_error_.clear(); throw std::runtime_error(e); }
   apply_ctx_pending(UINT64_MAX);  // the stats thread is idle
+  apply_reconfig_pending(UINT64_MAX);  // (tags >= batch_no_: no job of an earlier batch is left)
   node_take_text();  // decided alerts (rollover lane / node rounds) -> the al stream
   drain_kind(OUT_AL);
   if (node_mode_) {
@@ -3073,7 +3075,7 @@ void Engine::fleet_setup(int32_t cap, bool lockstep) {
   }
   sync_latest_ = latest_;  // the stats thread is idle (flush above)
   fleet_cap_ = cap;
-  fleet_elems_ = (size_t)cap * cfg_.n_lags * NSTAT * 3;
+  fleet_elems_ = (size_t)cap * MAX_LAGS * NSTAT * 3;  // (capacity: a reload may change the LAG count)
   for (int i = 0; i < 2; ++i) {
     fleet_buf_[i] = (double*)dmalloc(fleet_elems_ * 8);  // zeroed (and synchronised) by dmalloc
     HIP_OK(hipEventCreateWithFlags(&fleet_ev_[i], hipEventDisableTiming));
@@ -3092,6 +3094,7 @@ void Engine::fleet_setup(int32_t cap, bool lockstep) {
   series_service_uploaded_ = 0;  // rows become node-wide slots
   svc_csr_n_ = -1;
   node_mode_ = lockstep_ && cfg_.node_cooldown != 0;
+  node_cool_ms_ = cfg_.cooldown_ms;
   if (node_mode_) {
     const size_t per = sizeof(NodeHdr) + (size_t)node_cap_ * sizeof(NodeCand);
     d_node_send_ = (uint8_t*)dmalloc(per);
@@ -3142,12 +3145,14 @@ void Engine::lockstep_sync(int64_t batch_max) {
   h_sync_[0] = watermark_;
   h_sync_[1] = b == INT64_MIN ? -1.0 : (double)b;  // buckets < 2^53: exact in a double
   h_sync_[2] = (double)reg_pending_count();        // any rank with unregistered services?
-  h2d(d_sync_, h_sync_, 24, coll_stream_);
-  coll_->all_reduce_f64(d_sync_, 3, /*max=*/true, coll_stream_);
-  d2h(h_sync_, d_sync_, 24, coll_stream_);
+  h_sync_[3] = -(double)reconfig_staged_gen();     // MAX of -gen: the node's oldest newest reload
+  h2d(d_sync_, h_sync_, 32, coll_stream_);
+  coll_->all_reduce_f64(d_sync_, 4, /*max=*/true, coll_stream_);
+  d2h(h_sync_, d_sync_, 32, coll_stream_);
   coll_wait(coll_stream_, nullptr, "lock-step clocks");
   watermark_ = h_sync_[0];
   if (h_sync_[1] >= 0) sync_latest_ = std::max(sync_latest_, (int64_t)h_sync_[1]);
+  if (h_sync_[3] < 0) reconfig_agree((uint64_t)(-h_sync_[3]));  // every rank has it: same batch everywhere
   if (h_sync_[2] > 0) reg_round();  // every rank sees the same max: all enter the gather
   // the coll stream is in order: the previous batch's alert gather has landed too
   if (node_round_pending_) node_resolve();
@@ -3177,6 +3182,8 @@ void Engine::fleet_pack_locked() {
   const double t0 = now_ms();
   // APM_FLEET_ATOMIC=1: the per-series fp64 atomic scatter instead of the MFMA Gram pack (A/B)
   static const bool atomic_pack = [] { const char* x = std::getenv("APM_FLEET_ATOMIC"); return x && x[0] == '1'; }();
+  pack_nlags_[slot] = cfg_.n_lags;
+  for (int l = 0; l < MAX_LAGS; ++l) pack_lags_[slot][l] = cfg_.lags[l];
   pack_moments_locked(fleet_buf_[slot], fleet_cap_, stream_, atomic_pack);
   trace_event("fleet.pack", t0, now_ms(), 1);
   HIP_OK(hipEventRecord(pack_ev_[slot], stream_));
@@ -3192,8 +3199,9 @@ void Engine::fleet_exchange_upto(uint64_t rounds) {
     // Only the registered node-wide slots carry moments (identical count on every rank: the
     // registry rounds are collective), not the whole table: 10k services of a 64k-slot table
     // is 1.4 MB on the wire per batch instead of 9.4 MB.
-    const size_t n_red = lockstep_ ? std::min<size_t>(reg_names_.size(), (size_t)fleet_cap_) * cfg_.n_lags * NSTAT * 3
-                                   : fleet_elems_;
+    const size_t per_svc = (size_t)pack_nlags_[slot] * NSTAT * 3;
+    const size_t n_red = lockstep_ ? std::min<size_t>(reg_names_.size(), (size_t)fleet_cap_) * per_svc
+                                   : (size_t)fleet_cap_ * per_svc;
     if (!fleet_skip_solo_ && n_red) coll_->all_reduce_f64(fleet_buf_[slot], n_red, /*max=*/false, coll_stream_);
     if (pack_edge_[slot] && want(OUT_FB) && coll_->rank() == 0) fleet_emit_fb(slot);
     // edges are identical on every rank only in lock-step mode (fleet_setup refuses multi-rank
@@ -3251,8 +3259,9 @@ std::vector<double> Engine::fleet_merged() {
   if (fleet_rounds_ == 0) return out;
   const int slot = (int)((fleet_rounds_ - 1) & 1);
   coll_wait(nullptr, fleet_ev_[slot], "fleet moments");
-  out.resize(fleet_elems_);
-  HIP_OK(hipMemcpy(out.data(), fleet_buf_[slot], fleet_elems_ * 8, hipMemcpyDeviceToHost));
+  const size_t n = (size_t)fleet_cap_ * pack_nlags_[slot] * NSTAT * 3;  // [cap][n_lags of the pack][NSTAT][3]
+  out.resize(n);
+  HIP_OK(hipMemcpy(out.data(), fleet_buf_[slot], n * 8, hipMemcpyDeviceToHost));
   return out;
 }
 
@@ -3352,7 +3361,7 @@ void Engine::node_resolve() {
   std::vector<std::pair<uint64_t, double>> wins;
   for (const NodeCand& c : node_pool_) {
     auto it = node_cool_.find(c.key);
-    if (it != node_cool_.end() && !((c.now - it->second) / 1000.0 > cfg_.cooldown_ms / 1000.0)) continue;
+    if (it != node_cool_.end() && !((c.now - it->second) / 1000.0 > node_cool_ms_ / 1000.0)) continue;
     node_cool_[c.key] = c.now;
     wins.push_back({c.key, c.now});
     if (c.rank != me) continue;

@@ -45,6 +45,21 @@ struct ServiceOverride {
   bool suppressed = false;
 };
 
+// A config reload as the engine applies it (reconfig.cpp): the new LAG set with its default
+// THRESHOLD / INFLUENCE / suppression, the alert gates, and the per-service override table (LAG
+// positions in the new order).  `gen` orders reloads (the config file's mtime in ms).
+struct ReconfigSpec {
+  uint64_t gen = 0;
+  int n_lags = 0;
+  int32_t lags[MAX_LAGS] = {0, 0, 0, 0};
+  double thr[MAX_LAGS] = {0, 0, 0, 0};
+  double infl[MAX_LAGS] = {0, 0, 0, 0};
+  int lag_suppressed[MAX_LAGS] = {0, 0, 0, 0};
+  int alert_window = 60, alert_threshold = 45, both_only = 1;
+  double hard_min_ms = 200, hard_min_tpm = 1.0, hard_max_ms = 10000, cooldown_ms = 15 * 60000.0;
+  std::map<std::string, ServiceOverride> overrides;
+};
+
 struct EngineConfig {
   int device = 0;
   int32_t max_series = 1 << 17;
@@ -236,6 +251,13 @@ class Engine {
   void set_override(const std::string& service, const ServiceOverride& o);
   void clear_overrides();
   void refresh_series_settings();
+  // Config hot reload without a pipeline drain (reconfig.cpp): staged now, applied by the stats
+  // thread at a batch boundary (with lock-step ranks: the same boundary on every rank).
+  void stage_reconfig(const ReconfigSpec& spec);
+  uint64_t reconfig_applied_gen() const { return rc_applied_gen_.load(); }
+  uint64_t reconfigs_applied() const { return reconfigs_applied_.load(); }
+  uint64_t lag_set_changes() const { return lag_set_changes_.load(); }
+  std::vector<int32_t> lag_values() { flush(); return std::vector<int32_t>(cfg_.lags, cfg_.lags + cfg_.n_lags); }
 
   // Process one batch. `now_override` < 0 uses the engine watermark clock.  If the caller
   // already has the next batch, passing it launches its H2D + parse kernels before this batch's
@@ -383,6 +405,19 @@ class Engine {
   struct SeriesInfo { int32_t server, service; uint64_t emit_key; };
   int32_t series_for(int32_t server, int32_t service);
   void apply_series_settings(int32_t s);
+  // live reconfiguration (reconfig.cpp)
+  std::mutex rc_mu_;
+  std::deque<ReconfigSpec> rc_staged_;                           // lock-step: awaiting the node
+  std::deque<std::pair<uint64_t, ReconfigSpec>> rc_tagged_;      // (batch, spec), batches ascend
+  std::atomic<uint64_t> rc_applied_gen_{0}, reconfigs_applied_{0}, lag_set_changes_{0};
+  std::map<int32_t, int32_t*> counter_stash_;                    // removed LAG -> its alert counters
+  uint64_t reconfig_staged_gen();
+  void reconfig_agree(uint64_t node_min);
+  void apply_reconfig_pending(uint64_t upto);
+  void apply_reconfig(const ReconfigSpec& r);
+  // LAG set of each fleet slot's pack (the exchange and the fb rows run on the ingest thread)
+  int pack_nlags_[2] = {0, 0};
+  int32_t pack_lags_[2][MAX_LAGS] = {};
   void compute_series_settings(int32_t s, double* thr, double* infl, double& hard_max, uint8_t& suppressed);
   void stats_for_batch(std::vector<TxOut>& txs, double batch_t0);
   void stats_for_batch_dev(DevJoinBatch& b, double batch_t0);
@@ -507,6 +542,7 @@ class Engine {
   // for the winners only)
   struct NodePayload { uint64_t seq_batch; NodeCand c; int32_t series; int32_t lag; WinStat w; ZOut z; };
   bool node_mode_ = false;
+  double node_cool_ms_ = 0;  // ingest thread's cooldown (a reload switches it at the agreed batch)
   // candidates per rank per round: an alert storm (thousands of new keys per interval) must not
   // outgrow the exchange, or the unsent backlog and the decision lag grow without bound
   int32_t node_cap_ = 4096;

@@ -170,10 +170,12 @@ void Engine::fleet_emit_fb(int slot) {
     HIP_OK(hipStreamSynchronize(coll_stream_));
     fb_slots_up_ = n_slots;
   }
-  const int32_t rows = n_slots * cfg_.n_lags;
+  const int n_lags = pack_nlags_[slot];  // the LAG set of this slot's pack (a reload may have changed cfg_)
+  const int32_t* lags = pack_lags_[slot];
+  const int32_t rows = n_slots * n_lags;
   if (!d_fb_len_ || rows + 1 > (int32_t)(fb_tmp_bytes_ ? fb_rows_cap_ : 0)) {
     if (d_fb_len_) { dfree(d_fb_len_); dfree(d_fb_off_); dfree(d_fb_tmp_); }
-    fb_rows_cap_ = std::max<int32_t>(rows + 1, 2 * fleet_cap_ * cfg_.n_lags + 1);
+    fb_rows_cap_ = std::max<int32_t>(rows + 1, 2 * fleet_cap_ * n_lags + 1);
     d_fb_len_ = (uint32_t*)dmalloc((size_t)fb_rows_cap_ * 4);
     d_fb_off_ = (uint32_t*)dmalloc((size_t)fb_rows_cap_ * 4);
     fb_tmp_bytes_ = apm_fleet_format_tmp_bytes(fb_rows_cap_);
@@ -191,11 +193,11 @@ void Engine::fleet_emit_fb(int slot) {
   fa.names = reinterpret_cast<const int2*>(d_fb_names_);
   fa.chars = d_fb_chars_;
   fa.n_slots = n_slots;
-  fa.n_lags = cfg_.n_lags;
-  std::vector<int> order(cfg_.n_lags);
-  for (int l = 0; l < cfg_.n_lags; ++l) order[l] = l;
-  std::sort(order.begin(), order.end(), [&](int a, int b) { return cfg_.lags[a] < cfg_.lags[b]; });
-  for (int l = 0; l < cfg_.n_lags; ++l) { fa.lag_order[l] = order[l]; fa.lag_value[l] = cfg_.lags[l]; }
+  fa.n_lags = n_lags;
+  std::vector<int> order(n_lags);
+  for (int l = 0; l < n_lags; ++l) order[l] = l;
+  std::sort(order.begin(), order.end(), [&](int a, int b) { return lags[a] < lags[b]; });
+  for (int l = 0; l < n_lags; ++l) { fa.lag_order[l] = order[l]; fa.lag_value[l] = lags[l]; }
   fa.edge_ts = pack_edge_[slot];
   fa.copy = fs_copy_ ? 1 : 0;
   fa.ts_len = pg_timestamp(fa.edge_ts, fa.ts);

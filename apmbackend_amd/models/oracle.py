@@ -784,6 +784,25 @@ class ZScoreOracle:
     def settings(self, service):
         return zscore_lag_settings(self.cfg, service, self.emulate_aliasing)
 
+    def reload(self, cfg: Dict[str, Any]):
+        """The watcher callback (stream_calc_z_score.js:362-382): updateAllServiceSettings --
+        every series gets the new THRESHOLD / INFLUENCE of every configured LAG, a new LAG an
+        empty history -- then removeStaleLagData drops the LAGs no longer configured."""
+        self.cfg = cfg
+        for srv in self.servers.values():
+            for service, lags in srv.items():
+                settings = self.settings(service)
+                for el in settings:
+                    lag = int(el["LAG"])
+                    if lag in lags:
+                        lags[lag]["THRESHOLD"], lags[lag]["INFLUENCE"] = el["THRESHOLD"], el["INFLUENCE"]
+                    else:
+                        lags[lag] = {"THRESHOLD": el["THRESHOLD"], "INFLUENCE": el["INFLUENCE"],
+                                     "avgList": [], "per75List": [], "per95List": []}
+                keep = {int(el["LAG"]) for el in settings}
+                for lag in [x for x in lags if x not in keep]:
+                    del lags[lag]
+
     def consume(self, csv_line: str):
         e = entry_from_csv(csv_line)
         if e is not None and e.type == "st":
@@ -957,6 +976,13 @@ class PipelineOracle:
                               int(sc["windowSizeInIntervals"]), int(sc["bufferSizeInIntervals"]))
         self.parse = ParseOracle(self._on_tx, tz, g.get("recordTtlSeconds", 120),
                                  g.get("acctTtlSeconds", 120), g.get("needTtlSeconds", 30), server_fn=server_fn)
+
+    def reload(self, cfg: Dict[str, Any]):
+        """Config hot reload between two batches: z-score settings / LAG set (ZScoreOracle.reload)
+        and every alert gate (read from the config per fs entry)."""
+        self.cfg = cfg
+        self.zs.reload(cfg)
+        self.alerts.cfg = cfg
 
     def _on_tx(self, queue, line):
         if queue == "db_insert":

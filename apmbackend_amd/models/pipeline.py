@@ -13,13 +13,17 @@ across ranks.
 """
 from __future__ import annotations
 
+import logging
 import math
+import os
 from typing import Any, Dict, Iterable, List, Optional, Sequence, Tuple, Union
 
 from .. import _native
 from ..models.oracle import file_kind, server_of
 from ..ops.parse_ref import tz_table
 from ..utils.timeparse import TzOffset
+
+log = logging.getLogger("apm.pipeline")
 
 KIND_CODE = {"SOAP": 0, "SERVER": 1, "APP": 2}
 
@@ -137,6 +141,22 @@ def service_overrides(cfg: Dict[str, Any]) -> Dict[str, Dict[str, Any]]:
     return out
 
 
+_last_gen = [0]
+
+
+def _reload_generation(cfg: Dict[str, Any]) -> int:
+    """Reload generation: the config file's mtime in ms (identical on every rank of a node, so
+    the ranks agree on which reload they apply), else a local counter."""
+    path = cfg.get("apmConfigFilePath")
+    g = 0
+    if path and os.path.exists(path):
+        g = os.stat(path).st_mtime_ns // 1_000_000
+    if g <= 0:
+        g = _last_gen[0] + 1
+    _last_gen[0] = max(_last_gen[0], g)
+    return g
+
+
 class APMEngine:
     def __init__(self, cfg: Dict[str, Any], device: int = 0, keep_text: bool = False, outputs=None, **kw):
         self.cfg = cfg
@@ -151,11 +171,28 @@ class APMEngine:
         for svc, o in service_overrides(cfg).items():
             self.eng.set_override(svc, o)
 
-    def reload(self, cfg: Dict[str, Any]):
-        """Config hot reload: thresholds / overrides re-applied to every existing series."""
+    # engine settings a reload applies live (reconfig.cpp); any other change needs a restart
+    LIVE_KEYS = ("lags", "lag_suppressed", "alert_window", "alert_threshold", "hard_min_ms", "hard_min_tpm",
+                 "hard_max_ms", "both_only", "cooldown_ms")
+
+    def reload(self, cfg: Dict[str, Any], gen: Optional[int] = None) -> List[str]:
+        """Config hot reload (the reference's watchAPMConfig callbacks): z-score defaults and
+        per-service overrides re-applied to every series, LAGs added (empty history) or removed
+        (removeStaleLagData), every alert gate replaced -- staged now, applied by the engine at the
+        next batch boundary (the same boundary on every lock-step rank).  Returns the engine
+        settings that changed but need a restart (they are not applied)."""
+        new = engine_config(cfg, self.ecfg["device"], outputs=())
+        restart = sorted(k for k in new if k not in self.LIVE_KEYS and k not in ("outputs", "tz_table")
+                         and new[k] != self.ecfg.get(k))
+        if restart:
+            log.warning("config reload: %s changed but need a restart (not applied)", ", ".join(restart))
+        if gen is None:
+            gen = _reload_generation(cfg)
+        self.eng.stage_reconfig(new, service_overrides(cfg), int(gen))
+        for k in self.LIVE_KEYS:
+            self.ecfg[k] = new[k]
         self.cfg = cfg
-        self.apply_overrides(cfg)
-        self.eng.refresh_series_settings()
+        return restart
 
     def add_file(self, path: str, kind: Optional[str] = None, server: Optional[str] = None) -> int:
         if path in self.file_ids:

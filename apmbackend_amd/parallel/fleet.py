@@ -107,4 +107,5 @@ class FleetBaseline:
         raw = self.eng.eng.fleet_merged()
         if not raw:
             return np.zeros((self.cap, self.n_lags, 3, 3))
-        return np.frombuffer(raw, dtype=np.float64).reshape(self.cap, self.n_lags, 3, 3).copy()
+        # (the LAG count is the one of the newest exchanged pack: a reload may have changed it)
+        return np.frombuffer(raw, dtype=np.float64).reshape(self.cap, -1, 3, 3).copy()

@@ -261,6 +261,7 @@ class IngestService:
             self.jmx = JvmStatsPoller(self.cfg, self._on_jx, runner=runner, clock=clock)
 
         self.watcher = ConfigWatcher(self.cfg, self.reload, RESTART_KEYS) if self.cfg.get("apmConfigFilePath") else None
+        self._config_paused = self._consume_paused(self.cfg)
         self._stop = False
         self._gc_requested = False
         self.batches = 0
@@ -465,9 +466,22 @@ class IngestService:
         self._stop = True
 
     # ------------------------------------------------------------------ config reload
+    @staticmethod
+    def _consume_paused(cfg: Dict[str, Any]) -> bool:
+        """consumeQueue false on a fused stage (stats / z-score / alerts) stops consumption, as
+        the reference's watchers do (stream_calc_stats.js:251-258 and its twins): the fused engine
+        holds its input instead -- tails keep their offsets, the backlog is processed in order once
+        consumption resumes (lock-step ranks keep polling with empty batches)."""
+        return not all(bool((cfg.get(sec) or {}).get("consumeQueue", True))
+                       for sec in ("streamCalcStats", "streamCalcZScore", "streamProcessAlerts"))
+
     def reload(self, cfg: Dict[str, Any]):
         self.cfg = cfg
         apmlog.set_global_logger(cfg.get("logDir"), self._log_prefix())
+        paused = self._consume_paused(cfg)
+        if paused != self._config_paused:
+            log.info("%s consume from watcher!", "Stopping" if paused else "Starting")
+            self._config_paused = paused
         if self.eng is not None:
             self.eng.reload(cfg)
         if self.notifier:
@@ -611,8 +625,9 @@ class IngestService:
         # its tails have nothing new or downstream is paused -- or the collective sequences diverge.
         lockstep = self.fleet is not None
         paused = self.qm is not None and any(getattr(p, "paused", False) for p in self.producers.values())
+        paused = paused or self._config_paused
         if self.input_mode == "transactions":
-            return 0 if paused and not lockstep else self._step_tx(lockstep)
+            return 0 if paused and not lockstep else self._step_tx(lockstep, paused)
         if self.readahead:
             return self._step_readahead(lockstep, paused)
         if paused:
@@ -653,9 +668,11 @@ class IngestService:
         with self._in_lock:
             self._in_lines.append(body)
 
-    def _step_tx(self, lockstep: bool) -> int:
-        with self._in_lock:
-            lines, self._in_lines = self._in_lines, []
+    def _step_tx(self, lockstep: bool, paused: bool = False) -> int:
+        lines = []
+        if not paused:  # (paused lock-step ranks still take part in the poll's collectives)
+            with self._in_lock:
+                lines, self._in_lines = self._in_lines, []
         if not lines and not lockstep:
             return 0
         blob = b"\n".join(ln.rstrip(b"\n") for ln in lines) + (b"\n" if lines else b"")

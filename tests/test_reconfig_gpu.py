@@ -1,0 +1,79 @@
+"""Live reconfiguration: a config reload mid-stream changes z-score thresholds, alert gates and
+the LAG set, and the engine's st / fs / al streams stay equal to the oracle that applies the same
+reload between the same two batches (stream_calc_z_score.js:152-193,362-382 updateAllServiceSettings
++ removeStaleLagData; stream_process_alerts.js:335-471 gates read per fs entry)."""
+import collections
+import copy
+import os
+import sys
+
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from test_engine_gpu import UTC, small_cfg, synth_batches  # noqa: E402
+
+from apmbackend_amd.models.oracle import PipelineOracle  # noqa: E402
+from apmbackend_amd.models.pipeline import APMEngine  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _reloads():
+    C0 = small_cfg("exact")
+    C1 = copy.deepcopy(C0)
+    zc, ac = C1["streamCalcZScore"], C1["streamProcessAlerts"]
+    # thresholds, a new LAG (12: empty history) and a removed one (30: history dropped)
+    zc["defaults"] = [{"LAG": 6, "THRESHOLD": 2.5, "INFLUENCE": 0.5}, {"LAG": 12, "THRESHOLD": 2.0, "INFLUENCE": 0.2}]
+    zc["overrides"]["services"]["S:getSvc0002"] = {"12": {"THRESHOLD": 3.5}}
+    # alert gates
+    ac.update({"hardMinMsAlertThreshold": 150, "alertOnBothOnly": False, "rollingAlertWindowSizeInIntervals": 8,
+               "requiredNumberBadIntervalsInAlertWindowToTrigger": 2, "suppressedServices": ["S:getSvc0003"]})
+    C2 = copy.deepcopy(C1)
+    zc, ac = C2["streamCalcZScore"], C2["streamProcessAlerts"]
+    # LAG 30 comes back (empty history, its alert counters resume), LAG 12 suppressed, cooldown 1 min
+    zc["defaults"].append({"LAG": 30, "THRESHOLD": 1.5, "INFLUENCE": 0.0})
+    ac.update({"suppressedLags": [12], "perServiceAlertCooldownInMinutes": 1, "hardMaxMsAlertThreshold": 5000,
+               "suppressedServices": []})
+    return C0, C1, C2
+
+
+def test_reload_thresholds_gates_and_lag_set_mid_stream():
+    _lines, bl = synth_batches(1)
+    C0, C1, C2 = _reloads()
+    k1, k2 = 100, 170
+    P = PipelineOracle(copy.deepcopy(C0), UTC)
+    P.run_batches(bl[:k1])
+    P.reload(copy.deepcopy(C1))
+    P.run_batches(bl[k1:k2])
+    P.reload(copy.deepcopy(C2))
+    P.run_batches(bl[k2:])
+    assert len(P.al) > 0
+
+    eng = APMEngine(copy.deepcopy(C0), keep_text=True)
+    out = collections.defaultdict(list)
+    for i, (now, chunks) in enumerate(bl):
+        if i == k1:
+            assert eng.reload(copy.deepcopy(C1), gen=1) == []  # nothing here needs a restart
+        if i == k2:
+            eng.reload(copy.deepcopy(C2), gen=2)
+        eng.process_lines(chunks, now)
+        for k in ("st", "fs", "al"):
+            out[k] += eng.take(k)
+    info = eng.eng.reconfig_info()
+    assert info["applied"] == 2 and info["applied_gen"] == 2 and info["lag_set_changes"] == 2
+    assert eng.eng.lag_values() == [6, 12, 30]
+    assert out["st"] == P.stats
+    lags = lambda fs: collections.Counter(l.split("|")[4] for l in fs)
+    assert lags(out["fs"]) == lags(P.fs) and set(lags(P.fs)) == {"6", "12", "30"}
+    assert out["fs"] == P.fs
+    assert out["al"] == P.al
+
+
+def test_reload_warns_about_restart_keys():
+    C0 = small_cfg("exact")
+    eng = APMEngine(copy.deepcopy(C0), keep_text=True)
+    C1 = copy.deepcopy(C0)
+    C1["gpu"]["maxSeries"] = 8192
+    C1["streamCalcStats"]["windowSizeInIntervals"] = 20
+    restart = eng.reload(C1, gen=1)
+    assert "max_series" in restart and "window" in restart
