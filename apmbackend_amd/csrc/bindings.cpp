@@ -323,6 +323,16 @@ PYBIND11_MODULE(_apm_native, m) {
         return d;
       })
       .def("lag_values", &Engine::lag_values)
+      .def("cache_stats", [](Engine& e) {
+        std::vector<uint64_t> v;
+        { py::gil_scoped_release rel; v = e.cache_stats(); }
+        py::dict d;
+        if (v.size() == 6) {
+          d["slots"] = v[0]; d["occupied"] = v[1]; d["acct"] = v[2]; d["record"] = v[3]; d["partials"] = v[4];
+          d["need"] = v[5];
+        }
+        return d;
+      })
       .def("process_batch",
            [](Engine& e, py::buffer buf, const std::vector<std::tuple<int32_t, uint64_t, uint64_t>>& chunks,
               double now) {

@@ -1777,6 +1777,30 @@ __global__ __launch_bounds__(GL_TB) void k_gather_lines(const int64_t* __restric
   }
 }
 
+// Join-cache occupancy at clock `now` (the reference's CACHE_STATS, stream_parse_transactions.js:
+// 329-335): [0] occupied table slots, [1] acctCache entries live, [2] recordCache entries live,
+// [3] open partials in them, [4] needNumRecordCache entries (parked logIds).  Grid-stride, wave
+// reduction, one atomic per wave per counter.
+__global__ __launch_bounds__(256) void k_cache_stats(const KeyState* __restrict__ t, uint32_t cap, double now,
+                                                     unsigned long long* __restrict__ out) {
+  unsigned long long c[5] = {0, 0, 0, 0, 0};
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += gridDim.x * blockDim.x) {
+    const KeyState& k = t[i];
+    if (!k.key) continue;
+    c[0] += 1;
+    c[1] += k.acct_exp >= now;
+    const bool rec = k.rec_exp >= now && k.n_part > 0;
+    c[2] += rec;
+    c[3] += rec ? (unsigned long long)k.n_part : 0ull;
+    c[4] += k.need >= 0;
+  }
+  for (int j = 0; j < 5; ++j) {
+    unsigned long long v = c[j];
+    for (int o = APM_WAVE / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, APM_WAVE);
+    if ((threadIdx.x & (APM_WAVE - 1)) == 0 && v) atomicAdd(out + j, v);
+  }
+}
+
 __global__ __launch_bounds__(1024) void k_min_pos(const int64_t* __restrict__ gid, int64_t n, unsigned long long* out) {
   // grid-stride per lane, wave shuffle, one LDS pass per block, one atomic per block (a single
   // atomicMin per wave on one address serialised ~6k waves in the L2 atomic unit: 81 us)
@@ -2231,6 +2255,12 @@ void apm_dj_fill_series(TxRec* tx, const int32_t* raw, uint32_t n, const int32_t
 void apm_dj_gather_u8(const uint8_t* src, const int32_t* idx, uint32_t n, uint8_t* out, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_gather_u8, dim3((n + TB - 1) / TB), dim3(TB), 0, s, src, idx, n, out);
 }
+void apm_dj_cache_stats(const apm::KeyState* table, uint32_t cap, double now, unsigned long long* out, hipStream_t s) {
+  HIP_OK(hipMemsetAsync(out, 0, 5 * sizeof(unsigned long long), s));
+  const unsigned blocks = std::max(1u, std::min<unsigned>(1024, (cap + TB - 1) / TB));
+  hipLaunchKernelGGL(k_cache_stats, dim3(blocks), dim3(TB), 0, s, table, cap, now, out);
+}
+
 void apm_dj_count_le(const int64_t* end, int64_t n, int64_t edge, int64_t* out, hipStream_t s) {
   hipLaunchKernelGGL(k_count_le, dim3(1), dim3(1), 0, s, end, n, edge, out);
 }

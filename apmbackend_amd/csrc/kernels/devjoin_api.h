@@ -218,6 +218,7 @@ void apm_dj_scatter_i32(int32_t* dst, const int32_t* pairs, uint32_t n, hipStrea
 void apm_dj_fill_series(apm::TxRec* tx, const int32_t* raw, uint32_t n, const int32_t* raw_series,
                         unsigned long long* unmapped, hipStream_t s);
 void apm_dj_gather_u8(const uint8_t* src, const int32_t* idx, uint32_t n, uint8_t* out, hipStream_t s);
+void apm_dj_cache_stats(const apm::KeyState* table, uint32_t cap, double now, unsigned long long* out, hipStream_t s);
 void apm_dj_count_le(const int64_t* end, int64_t n, int64_t edge, int64_t* out, hipStream_t s);
 void apm_dj_relocate(int64_t* gid, int64_t n, char* ring, uint64_t ring_cap, uint64_t below, uint64_t dst_base,
                      unsigned long long* cursor, hipStream_t s);

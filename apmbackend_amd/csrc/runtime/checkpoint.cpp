@@ -34,7 +34,7 @@ namespace {
 
 enum : uint32_t {
   SEC_CONFIG = 1, SEC_TOPOLOGY, SEC_SERIES, SEC_CLOCK, SEC_JOIN, SEC_PARSE, SEC_BUCKETS, SEC_ZSCORE, SEC_POOL,
-  SEC_ALERTS, SEC_OUTPUTS, SEC_METRICS, SEC_RING, SEC_EXTRA, SEC_DUMP = 100
+  SEC_ALERTS, SEC_OUTPUTS, SEC_METRICS, SEC_RING, SEC_EXTRA, SEC_DUMP = 100, SEC_DUMP_SERIES = 101
 };
 
 struct SeriesRec { int32_t server, service; uint64_t emit_key; };
@@ -318,8 +318,83 @@ uint64_t Engine::dump_state(const std::string& path, const std::string& reason) 
   w.str(reason);
   w.str(j);
   w.end();
+  write_series_dump(w);
   w.commit();
   return w.bytes();
+}
+
+// Per-series device state of the fatal dump (SEC_DUMP_SERIES): the window statistics of the last
+// rollover, and per LAG the history length, leaky alert counter, z-score bounds / signals and
+// rolling moments -- the ring-buffer metadata and per-series state SURVEY 2.2 maps heapdump to.
+// Best effort: a faulted device context cannot be read; the section then says so (and why).
+void Engine::write_series_dump(BinWriter& w) {
+  const int32_t n = n_series_, S = cfg_.max_series;
+  std::string err;
+  auto rd = [&](void* dst, const void* src, size_t bytes) {
+    if (!err.empty() || !bytes) return;
+    const hipError_t e = hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) err = hipGetErrorString(e);
+  };
+  std::vector<WinStat> win((size_t)n);
+  rd(win.data(), d_win_, (size_t)n * sizeof(WinStat));
+  struct PerLag { std::vector<int32_t> len, counter, cnt; std::vector<ZOut> z; std::vector<double> sum; };
+  std::vector<PerLag> pl((size_t)cfg_.n_lags);
+  for (int l = 0; l < cfg_.n_lags; ++l) {
+    PerLag& p = pl[(size_t)l];
+    p.len.resize((size_t)n); p.counter.resize((size_t)n); p.z.resize((size_t)n);
+    p.sum.resize((size_t)n * NSTAT); p.cnt.resize((size_t)n * NSTAT);
+    rd(p.len.data(), lag_[l].len, (size_t)n * 4);
+    rd(p.counter.data(), lag_[l].counter, (size_t)n * 4);
+    rd(p.z.data(), lag_[l].out, (size_t)n * sizeof(ZOut));
+    for (int k = 0; k < NSTAT; ++k) {
+      rd(p.sum.data() + (size_t)k * n, lag_[l].sum + (size_t)k * S, (size_t)n * 8);
+      rd(p.cnt.data() + (size_t)k * n, lag_[l].cnt + (size_t)k * S, (size_t)n * 4);
+    }
+  }
+  if (!err.empty()) (void)hipGetLastError();
+  std::string h = "{\"n\":" + std::to_string(err.empty() ? n : 0) + ",\"lags\":[";
+  for (int l = 0; l < cfg_.n_lags; ++l) h += (l ? "," : "") + std::to_string(cfg_.lags[l]);
+  h += "],\"device_readable\":" + std::string(err.empty() ? "true" : "false") + ",\"error\":\"";
+  for (char c : err) h += (c == '"' || c == '\\') ? ' ' : c;
+  h += "\"}";
+  w.begin(SEC_DUMP_SERIES);
+  w.str(h);
+  const int32_t m = err.empty() ? n : 0;
+  std::vector<std::string> srv((size_t)m), svc((size_t)m);
+  {
+    std::lock_guard<std::mutex> g(series_mu_);
+    for (int32_t s = 0; s < m; ++s) {
+      srv[(size_t)s] = servers_[series_[s].server];
+      svc[(size_t)s] = dict_.service_name(series_[s].service);
+    }
+  }
+  w.strs(srv);
+  w.strs(svc);
+  std::vector<double> wv((size_t)m * 6);
+  for (int32_t s = 0; s < m; ++s) {
+    const WinStat& x = win[(size_t)s];
+    double* o = wv.data() + (size_t)s * 6;
+    o[0] = x.tpm; o[1] = x.avg; o[2] = x.p75; o[3] = x.p95; o[4] = x.n; o[5] = x.active;
+  }
+  w.vec(wv);
+  for (int l = 0; l < cfg_.n_lags; ++l) {
+    PerLag& p = pl[(size_t)l];
+    if (!m) { p.len.clear(); p.counter.clear(); p.sum.clear(); p.cnt.clear(); }
+    std::vector<double> zv((size_t)m * 4 * NSTAT);
+    for (int32_t s = 0; s < m; ++s) {
+      const ZOut& z = p.z[(size_t)s];
+      double* o = zv.data() + (size_t)s * 4 * NSTAT;
+      for (int k = 0; k < NSTAT; ++k) {
+        o[k] = z.mean[k]; o[NSTAT + k] = z.lb[k]; o[2 * NSTAT + k] = z.ub[k]; o[3 * NSTAT + k] = z.sig[k];
+      }
+    }
+    w.vec(p.len);
+    w.vec(p.counter);
+    w.vec(zv);
+    w.vec(p.sum);
+    w.vec(p.cnt);
+  }
+  w.end();
 }
 
 uint64_t Engine::save_state(const std::string& path, const std::string& extra) {

@@ -78,8 +78,6 @@ DeviceJoin::DeviceJoin(const DevJoinConfig& cfg, Dictionary* dict, const std::ve
     HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     const char* pe = std::getenv("APM_JOIN_PRIO");
     HIP_OK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, pe && pe[0] == '0' ? lo : hi));
-    HIP_OK(hipStreamCreateWithPriority(&up_stream_, hipStreamNonBlocking, hi));
-    HIP_OK(hipEventCreateWithFlags(&up_ev_, hipEventDisableTiming));
   }
   const uint32_t E = std::max<uint32_t>(cfg_.max_events, 1024);
   out_cap_ = 2 * E + (1u << 16);
@@ -209,8 +207,6 @@ DeviceJoin::~DeviceJoin() {
   if (h_ck_bounce_) hipHostFree(h_ck_bounce_);
   for (void* p : allocs_) hipFree(p);
   hipStreamDestroy(stream_);
-  if (up_stream_) { hipStreamSynchronize(up_stream_); hipStreamDestroy(up_stream_); }
-  if (up_ev_) hipEventDestroy(up_ev_);
 }
 
 // ---------------------------------------------------------------------------- parse-side hooks
@@ -848,31 +844,21 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
     d_hbuf_ = p;
   }
   span("u.devgrow");
-  // The host ops (~160 KB a batch) are read by a kernel over the host link.  A DMA copy queues
-  // behind the next batch's 22 MB of log bytes on the copy engine: on its own stream it cost
-  // 1.44-1.50 vs 1.20-1.23 ms per step (A/B, 60 steps), on the join stream hipMemcpyAsync also
-  // held this thread ~0.6 ms.  APM_HOPS_COPY=dma: the DMA path on its own stream.
-  static const bool kcopy = [] { const char* e = std::getenv("APM_HOPS_COPY"); return !e || e[0] != 'd'; }();
-  bool uploaded = false;
+  // The host ops (~160 KB a batch) are read by a kernel over the host link (apm_copy on the join
+  // stream).  A DMA copy queues behind the next batch's 22 MB of log bytes on the copy engine: on
+  // its own stream it cost 1.44-1.50 vs 1.20-1.23 ms per step (round-3 A/B, 60 steps), and a fifth
+  // stream for it shares the 4 hardware queues -- so no separate upload stream exists.
   if (!hops_.empty()) {
     std::memcpy(h_hops_, hops_.data(), hops_.size() * sizeof(HostOp));
     span("u.hops.memcpy");
-    if (kcopy) apm_copy(d_hops_, hd_hops_, hops_.size() * sizeof(HostOp), st);
-    else HIP_OK(hipMemcpyAsync(d_hops_, h_hops_, hops_.size() * sizeof(HostOp), hipMemcpyHostToDevice, up_stream_));
-    uploaded = true;
+    apm_copy(d_hops_, hd_hops_, hops_.size() * sizeof(HostOp), st);
     span("u.hops.h2d");
   }
   if (!hbuf_.empty()) {
     std::memcpy(h_hbuf_, hbuf_.data(), hbuf_.size());
     span("u.hbuf.memcpy");
-    if (kcopy) apm_copy(d_hbuf_, hd_hbuf_, hbuf_.size(), st);
-    else HIP_OK(hipMemcpyAsync(d_hbuf_, h_hbuf_, hbuf_.size(), hipMemcpyHostToDevice, up_stream_));
-    uploaded = true;
+    apm_copy(d_hbuf_, hd_hbuf_, hbuf_.size(), st);
     span("u.hbuf.h2d");
-  }
-  if (uploaded && !kcopy) {
-    HIP_OK(hipEventRecord(up_ev_, up_stream_));
-    HIP_OK(hipStreamWaitEvent(st, up_ev_, 0));
   }
   // ---- file -> server table
   if (files_->size() > files_uploaded_) {
@@ -1079,6 +1065,15 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
   tx_db_ += c3.n_db;
   aud_cur_ ^= 1;  // the next batch reads what this one carried
   phase_t[8] = clock_ms();
+}
+
+std::vector<uint64_t> DeviceJoin::cache_stats(double now) {
+  if (!d_cstats_) d_cstats_ = (unsigned long long*)dmalloc(64);
+  unsigned long long h[5] = {0, 0, 0, 0, 0};
+  apm_dj_cache_stats(d_table_, table_cap_, now, d_cstats_, stream_);
+  HIP_OK(hipMemcpyAsync(h, d_cstats_, sizeof h, hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+  return {(uint64_t)table_cap_, h[0], h[1], h[2], h[3], h[4]};
 }
 
 JoinCounters DeviceJoin::counters() const {

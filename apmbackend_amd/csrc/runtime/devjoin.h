@@ -110,6 +110,9 @@ class DeviceJoin {
   void reset_ring(uint64_t head);  // checkpoint load: pending lines were placed at [0, head)
 
   JoinCounters counters() const;
+  // occupancy of the join caches at clock `now` (join stream idle): table slots, occupied, acct
+  // live, record live, open partials, need live -- the reference's CACHE_STATS
+  std::vector<uint64_t> cache_stats(double now);
 
   // checkpoint of the GPU join state (checkpoint.cpp): key table (live entries), need arena
   // (live regions), SOAP contexts, service registry, audit-trail carry, counters
@@ -193,7 +196,6 @@ class DeviceJoin {
   const std::vector<FileInfo>* files_;
   const std::vector<std::string>* servers_;
   hipStream_t stream_ = nullptr;  // join stream
-  hipStream_t up_stream_ = nullptr;  // host-op uploads by DMA (nothing queued ahead of them)
   // flags of the host-op staging (read by a kernel over the host link): APM_HOPS_NC=1 allocates it
   // non-coherent (the GPU may then fetch whole cache lines)
   static unsigned host_flags_() {
@@ -203,7 +205,6 @@ class DeviceJoin {
     }();
     return f;
   }
-  hipEvent_t up_ev_ = nullptr;
   size_t device_bytes_ = 0;
   std::vector<void*> allocs_;
 
@@ -232,6 +233,7 @@ class DeviceJoin {
   DJArgs a_{};
   DJFormatArgs f_{};
   KeyState* d_table_ = nullptr;
+  unsigned long long* d_cstats_ = nullptr;  // cache_stats result (5 counters)
   KeyState* d_table_spare_ = nullptr;  // same-size rebuild target (no allocation per rebuild)
   uint32_t table_cap_ = 0;
   int table_bits_ = 0;

@@ -719,6 +719,15 @@ void Engine::upload_series_tables(int32_t lo) {
   stage_done();
 }
 
+std::vector<uint64_t> Engine::cache_stats() {
+  flush();
+  if (dj_) {
+    HIP_OK(hipStreamSynchronize(parse_stream_));
+    return dj_->cache_stats(watermark_);
+  }
+  return {};
+}
+
 JoinCounters Engine::join_counters() const {
   if (dj_) return dj_->counters();
   JoinCounters t;

@@ -390,6 +390,9 @@ class Engine {
   hipStream_t comm_stream() const { return stream_; }  // (the stats stream: callers flush() first)
   size_t device_bytes() const { return device_bytes_; }
   JoinCounters join_counters() const;
+  // join-cache occupancy (device join: a reduction over the key table at the watermark clock;
+  // host join: the shards' map sizes): {slots, occupied, acct, record, partials, need}
+  std::vector<uint64_t> cache_stats();
 
   // events of the last batch (host copy) for kernel verification
   std::string last_events() const;
@@ -844,6 +847,7 @@ class Engine {
   static constexpr int kMaxChain = 16;
   void checkpoint_quiesce(const char* what);
   void write_small_sections(class BinWriter& w);
+  void write_series_dump(class BinWriter& w);
   std::string load_small_state(const std::string& path);
   void apply_ring_file(const std::string& path);
   void checkpoint_writer();

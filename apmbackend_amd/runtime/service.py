@@ -584,6 +584,12 @@ class IngestService:
         if any(lost.values()):
             log.warning("ENGINE capacity exceeded (totals): %s -- raise gpu.maxSeries (the other structures grow)",
                      ", ".join(f"{k}={v}" for k, v in lost.items()))
+        # CACHE_STATS (stream_parse_transactions.js:329-335): live entries of the join caches
+        cs = self.native.cache_stats() if hasattr(self.native, "cache_stats") else {}
+        if cs:
+            log.info("CACHE_STATS acctCache: %d - recordCache: %d (%d open partials) - needNumRecordCache: %d "
+                     "- key table %d / %d slots (load %.3f)", cs["acct"], cs["record"], cs["partials"], cs["need"],
+                     cs["occupied"], cs["slots"], cs["occupied"] / max(cs["slots"], 1))
         grows = {"spill": int(m.get("spill_grows", 0)),
                  **{k: int(j.get(k + "_grows", 0)) for k in ("table", "arena", "pool")}}
         if grows != getattr(self, "_grows_prev", grows):
@@ -857,7 +863,9 @@ def read_state_dump(path: str) -> Dict[str, Any]:
         data = f.read()
     if data[:8] != b"APMCKPT\0":
         raise ValueError("not an engine checkpoint / dump file")
+    import numpy as np
     off = 12
+    state = None
     while off + 4 <= len(data):
         tag = struct.unpack_from("<I", data, off)[0]
         if tag == 0xE0F:
@@ -870,9 +878,50 @@ def read_state_dump(path: str) -> Dict[str, Any]:
             n2 = struct.unpack_from("<Q", body, 8 + n1)[0]
             state = json.loads(body[16 + n1:16 + n1 + n2].decode())
             state["reason"] = reason
-            return state
+        elif tag == 101 and state is not None:
+            state["series"] = _read_series_dump(body, np)
         off += 12 + ln
-    raise ValueError("no dump section")
+    if state is None:
+        raise ValueError("no dump section")
+    return state
+
+
+def _read_series_dump(body: bytes, np) -> Dict[str, Any]:
+    """SEC_DUMP_SERIES (checkpoint.cpp write_series_dump): names, window stats of the last
+    rollover, and per LAG the history length, alert counter, z-score bounds / signals, moments."""
+    import struct
+    pos = [0]
+
+    def u64():
+        v = struct.unpack_from("<Q", body, pos[0])[0]
+        pos[0] += 8
+        return v
+
+    def text():
+        n = u64()
+        v = body[pos[0]:pos[0] + n].decode()
+        pos[0] += n
+        return v
+
+    def vec(dt):
+        n = u64()
+        a = np.frombuffer(body, dtype=dt, count=n, offset=pos[0]).copy()
+        pos[0] += n * np.dtype(dt).itemsize
+        return a
+
+    hdr = json.loads(text())
+    n = hdr["n"]
+    out: Dict[str, Any] = dict(hdr)
+    out["server"] = [text() for _ in range(u64())]
+    out["service"] = [text() for _ in range(u64())]
+    out["window"] = vec("<f8").reshape(n, 6)  # tpm, avg, p75, p95, n, active
+    out["per_lag"] = {}
+    for lag in hdr["lags"]:
+        out["per_lag"][lag] = {"len": vec("<i4"), "counter": vec("<i4"),
+                               "z": vec("<f8").reshape(n, 4, 3),  # mean / lb / ub / signal x (avg, p75, p95)
+                               "sum": vec("<f8").reshape(3, n) if n else np.zeros((3, 0)),
+                               "cnt": vec("<i4").reshape(3, n) if n else np.zeros((3, 0), np.int32)}
+    return out
 
 
 def main(argv=None):  # pragma: no cover - process entry point

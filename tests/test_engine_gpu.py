@@ -724,6 +724,14 @@ def test_fatal_error_leaves_a_state_dump(tmp_path):
     assert d["batches"] == m["batches"] and d["lines"] == m["lines"] and d["n_series"] == eng.eng.n_series()
     assert d["rollovers"] == m["rollovers"] > 0 and d["join_table_slots"] >= 1024
     assert len(d["slot_bucket"]) == 40 and d["tx_ring_head"] > 0
+    # per-series device state (SEC_DUMP_SERIES): read back and checked against the engine
+    sd = d["series"]
+    assert sd["device_readable"] and sd["n"] == eng.eng.n_series() and sd["lags"] == [6, 30]
+    assert list(zip(sd["server"], sd["service"])) == [tuple(x) for x in eng.eng.export_series()]
+    assert (sd["window"][:, 5] == 1).sum() > 0 and sd["window"].shape == (sd["n"], 6)
+    for li, lag in enumerate(sd["lags"]):
+        pl = sd["per_lag"][lag]
+        assert pl["len"].max() == min(lag, m["rollovers"]) and list(pl["counter"]) == list(eng.eng.export_alert_counters(li))
 
 
 def _edge_corpus(seed, n=4000):
