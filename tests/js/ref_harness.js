@@ -59,10 +59,21 @@ function runZScore(req) {
   const consume = sliceFunction(src('stream_calc_z_score.js'), 'function consumeMsg(msg)');
   ctx.outQueue = { writeLineToQueue: (l) => out.push(l) };
   ctx.ZSCORECONFIG = { verboseQueueWrite: false, ...cfg.streamCalcZScore };
-  const fn = vm.runInContext('(function(){\n' + cls + '\nconst zscore = new ZScoreParser();\n' +
-      'const entryFactory = new EntryFactory();\n' + consume + '\nreturn consumeMsg; })()', ctx,
+  const api = vm.runInContext('(function(){\n' + cls + '\nconst zscore = new ZScoreParser();\n' +
+      'const entryFactory = new EntryFactory();\n' + consume + '\nreturn { consumeMsg, zscore }; })()', ctx,
       { filename: 'stream_calc_z_score.slice.js' });
-  for (const line of req.lines) fn({ content: Buffer.from(line) });
+  // reloads: [{at: line index, configText}] -- the watcher callback of stream_calc_z_score.js:
+  // 362-382 (new ZSCORECONFIG, updateAllServiceSettings, removeStaleLagData) before line `at`
+  const reloads = (req.reloads || []).slice().sort((a, b) => a.at - b.at);
+  req.lines.forEach((line, i) => {
+    while (reloads.length && reloads[0].at === i) {
+      const c = JSON.parse(stripJSON(reloads.shift().configText));
+      ctx.ZSCORECONFIG = { verboseQueueWrite: false, ...c.streamCalcZScore };
+      api.zscore.updateAllServiceSettings();
+      api.zscore.removeStaleLagData();
+    }
+    api.consumeMsg({ content: Buffer.from(line) });
+  });
   return out;
 }
 
@@ -74,7 +85,16 @@ function runAlerts(req) {
   const mgr = vm.runInContext('(function(){\n' + cls + '\nreturn new AlertsManager(); })()', ctx,
       { filename: 'stream_process_alerts.slice.js' });
   const ef = new ctx.EntryFactory();
-  for (const line of req.lines) {
+  // reloads: [{at, configText}] -- every gate is read from ALERTSCONFIG per entry, so a reload
+  // is the new ALERTSCONFIG from line `at` on (stream_process_alerts.js:540-556)
+  const reloads = (req.reloads || []).slice().sort((a, b) => a.at - b.at);
+  for (let i = 0; i < req.lines.length; ++i) {
+    const line = req.lines[i];
+    while (reloads.length && reloads[0].at === i) {
+      const c = JSON.parse(stripJSON(reloads.shift().configText));
+      ctx.ALERTSCONFIG = c.streamProcessAlerts;
+      ctx.APMCONFIG = c;
+    }
     const en = ef.getEntryFromCSV(line);
     if (req.clock === 'entry') clock.now = en.timestamp;
     const al = mgr.processFSEntry(en);

@@ -26,12 +26,15 @@ def stats(lines):
     return run({"mode": "stats", "lines": lines})
 
 
-def zscore(config_text, lines):
-    return run({"mode": "zscore", "configText": config_text, "lines": lines})
+def zscore(config_text, lines, reloads=()):
+    """reloads: [(line index, config text)] applied as the reference's watcher does."""
+    return run({"mode": "zscore", "configText": config_text, "lines": lines,
+                "reloads": [{"at": a, "configText": t} for a, t in reloads]})
 
 
-def alerts(config_text, lines, clock="entry"):
-    return run({"mode": "alerts", "configText": config_text, "lines": lines, "clock": clock})
+def alerts(config_text, lines, clock="entry", reloads=()):
+    return run({"mode": "alerts", "configText": config_text, "lines": lines, "clock": clock,
+                "reloads": [{"at": a, "configText": t} for a, t in reloads]})
 
 
 def util(**kw):

@@ -226,3 +226,49 @@ def test_js_average_float_view_path_is_the_same_left_to_right_sum():
         assert js_average(View(vals)) == js_average(vals)
         assert js_stddev(View(vals)) == js_stddev(vals)
     assert js_average(View([None, float("nan")])) is None
+
+
+@requires_reference
+def test_config_reload_oracle_matches_reference_js():
+    """The oracle's reload (thresholds, a LAG added / removed / re-added, alert gates) against the
+    reference's own watcher callbacks run on the same st / fs streams: updateAllServiceSettings +
+    removeStaleLagData (stream_calc_z_score.js:362-382) and the per-entry ALERTSCONFIG reads."""
+    import refjs
+    start = 1578391200000
+    an = [Anomaly("jvm00", "getSvc0001", start + 400_000, start + 1500_000, 30.0)]
+    _, bl = _synth(1, duration=1500, anomalies=an)
+    C0 = default_config()
+    C0["streamCalcZScore"]["defaults"] = [{"LAG": 6, "THRESHOLD": 3.0, "INFLUENCE": 0.5},
+                                          {"LAG": 30, "THRESHOLD": 2.0, "INFLUENCE": 0.0}]
+    C0["streamCalcZScore"]["overrides"]["services"]["S:getSvc0002"] = {"6": {"THRESHOLD": 4.0, "INFLUENCE": 0.25}}
+    C0["streamProcessAlerts"].update({"rollingAlertWindowSizeInIntervals": 10,
+                                      "requiredNumberBadIntervalsInAlertWindowToTrigger": 3,
+                                      "perServiceAlertCooldownInMinutes": 2})
+    C0["gpu"]["emulateOverrideAliasing"] = True
+    C1 = copy.deepcopy(C0)
+    C1["streamCalcZScore"]["defaults"] = [{"LAG": 6, "THRESHOLD": 2.5, "INFLUENCE": 0.5},
+                                          {"LAG": 12, "THRESHOLD": 2.0, "INFLUENCE": 0.2}]
+    C1["streamCalcZScore"]["overrides"]["services"]["S:getSvc0002"] = {"12": {"THRESHOLD": 3.5}}
+    C1["streamProcessAlerts"].update({"hardMinMsAlertThreshold": 150, "alertOnBothOnly": False,
+                                      "rollingAlertWindowSizeInIntervals": 8,
+                                      "requiredNumberBadIntervalsInAlertWindowToTrigger": 2,
+                                      "suppressedServices": ["S:getSvc0003"]})
+    C2 = copy.deepcopy(C1)
+    C2["streamCalcZScore"]["defaults"].append({"LAG": 30, "THRESHOLD": 1.5, "INFLUENCE": 0.0})
+    C2["streamProcessAlerts"].update({"suppressedLags": [12], "perServiceAlertCooldownInMinutes": 1,
+                                      "hardMaxMsAlertThreshold": 5000, "suppressedServices": []})
+    k1, k2 = len(bl) * 2 // 5, len(bl) * 7 // 10
+    P = PipelineOracle(copy.deepcopy(C0), UTC)
+    P.run_batches(bl[:k1])
+    at_st1, at_fs1 = len(P.stats), len(P.fs)
+    P.reload(copy.deepcopy(C1))
+    P.run_batches(bl[k1:k2])
+    at_st2, at_fs2 = len(P.stats), len(P.fs)
+    P.reload(copy.deepcopy(C2))
+    P.run_batches(bl[k2:])
+    assert {l.split("|")[4] for l in P.fs[at_fs2:]} == {"6", "12", "30"}
+    assert "30" not in {l.split("|")[4] for l in P.fs[at_fs1:at_fs2]}
+    fs = refjs.zscore(json.dumps(C0), P.stats, reloads=[(at_st1, json.dumps(C1)), (at_st2, json.dumps(C2))])
+    assert fs == P.fs
+    al = refjs.alerts(json.dumps(C0), P.fs, "entry", reloads=[(at_fs1, json.dumps(C1)), (at_fs2, json.dumps(C2))])
+    assert al == P.al and len(al) > 0

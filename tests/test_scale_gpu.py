@@ -246,3 +246,71 @@ def test_headline_shard_sample_matches_cpu_oracle():
     assert sum(len(v) for v in got_fs.values()) >= 200 * 2 * (INTERVALS - 2)
     # some sampled series signal (the planted incident / the warm history's spread)
     assert any(part.split(":")[4] not in ("0", "0.0") for l in eng_fs for part in l.split("|")[6:9])
+
+
+@pytest.mark.parametrize("audit", [0.02, 0.25])
+def test_headline_shard_device_join_equals_host_join(audit):
+    """parse + join pinned at bench scale.  The headline shard (8 JVMs x 10k
+    services, 250 tx/s per JVM) with audit trails on `audit` of the requests, overlapping provider
+    calls (12-20 per request: the partial chains) and 90-byte logIds (the logId chains), 30
+    ten-second batches through the GPU join (K4/K5/K6 on the device) and through the independent
+    host join workers (join.cpp, the reference's per-line state machine in C++): the
+    `transactions` and `audit_db` streams are equal as sequences, the released `db` stream is the
+    same multiset of lines, each in endTs order (stream_parse_transactions.js:264-327, 378-731)."""
+    N = _native.load(build_if_missing=False)
+    opts = {"servers": 8, "ejb_services": 6000, "provider_services": 4000, "tx_per_sec_per_server": 250.0,
+            "seed": 5, "audit": audit, "overlap_subs": True, "logid_pad": 80}
+    gen = N.SynthGen(opts)
+    engines = {}
+    for name, dev in (("device", True), ("host", False)):
+        C = bench_cfg("exact", "float64")
+        C["gpu"]["joinOnDevice"] = dev
+        engines[name] = APMEngine(C, outputs=("transactions", "audit_db", "db"))
+        for path, kind, server in gen.files():
+            engines[name].add_file(path, {0: "SOAP", 1: "SERVER", 2: "APP"}[kind], server)
+    got = {n: collections.defaultdict(list) for n in engines}
+    for b in range(30):
+        data, chunks = gen.generate(START + (b + 1) * STEP_MS, 16)
+        for name, e in engines.items():
+            e.eng.process_batch(data, chunks, -1.0)
+            for k in ("transactions", "audit_db", "db"):
+                got[name][k] += [l for l in e.take_bytes(k).decode().split("\n") if l]
+    d, h = got["device"], got["host"]
+    assert len(d["transactions"]) > 30 * 8 * 250 * 10 * 0.9
+    assert d["transactions"] == h["transactions"]
+    assert len(d["audit_db"]) > 0 and d["audit_db"] == h["audit_db"]
+    assert len(d["db"]) > 0 and collections.Counter(d["db"]) == collections.Counter(h["db"])
+    for k in ("device", "host"):
+        ends = [int(l.split("|")[6]) for l in got[k]["db"]]
+        assert ends == sorted(ends)
+    jd = engines["device"].metrics()["join"]
+    assert jd["chain_partial_blocks"] > 0 and jd["chain_logid_blocks"] > 0  # the chain paths ran
+    assert all(jd.get(k, 0) == 0 for k in ("partial_overflow", "need_overflow", "table_full", "pool_exhausted"))
+
+
+@pytest.mark.parametrize("variant", ["base", "host_join", "cells16", "cells64_spill1M", "spill1M", "maxSeries64k"])
+def test_window_stats_match_oracle_under_capacity_variants(variant):
+    """(was tools/diag/st_vs_oracle_variants.py) 48 JVMs, the st stream of every capacity variant
+    equals the CPU oracle's: inline cells vs spill lists, the host join, a tight series table."""
+    import copy
+
+    from apmbackend_amd.models.oracle import PipelineOracle
+    import test_engine_gpu as T
+    g = {"base": {}, "host_join": {"joinOnDevice": False}, "cells16": {"bucketCellCapacity": 16},
+         "cells64_spill1M": {"bucketCellCapacity": 64, "bucketOverflowCapacity": 1 << 20},
+         "spill1M": {"bucketOverflowCapacity": 1 << 20}, "maxSeries64k": {"maxSeries": 1 << 16}}[variant]
+    _lines, bl = T.synth_batches(10, duration=120, servers=48)
+    P = PipelineOracle(copy.deepcopy(T.small_cfg("exact")), T.UTC)
+    P.run_batches(bl)
+    C = T.small_cfg("exact")
+    C["gpu"].update(g)
+    eng = APMEngine(C, keep_text=True)
+    st, tx = [], []
+    for now, chunks in bl:
+        eng.process_lines(chunks, now)
+        st += eng.take("st")
+        tx += eng.take("transactions")
+    assert st == P.stats
+    assert tx == P.tx_out
+    m = eng.metrics()
+    assert m["spill_dropped"] == 0 and m["series_overflow_tx"] == 0
