@@ -27,6 +27,7 @@
 
 #include "devjoin_api.h"
 #include "devjoin_dev.h"
+#include "devscan.h"
 #include "textout.h"
 
 namespace apm {
@@ -375,8 +376,8 @@ __global__ void k_host_flags(const Event* __restrict__ ev, const uint32_t* __res
                              uint8_t* __restrict__ flag, uint64_t* __restrict__ val, AudF* __restrict__ aud,
                              SelCount* __restrict__ totals, uint32_t cap) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= cap) return;
-  const uint32_t n = *n_ev_dev;
+  const uint32_t n = min(*n_ev_dev, cap);
+  if (blockIdx.x * blockDim.x >= n) return;  // (uniform per block: the grid is sized for the capacity)
   uint8_t fl = 0;
   uint32_t ab = 0;
   if (i < n) {
@@ -398,33 +399,41 @@ __global__ void k_host_flags(const Event* __restrict__ ev, const uint32_t* __res
       if (e.mask & (PM_AUTR_MAP | PM_SW_NAME)) ab = e.len;
     }
   }
-  flag[i] = fl;
-  val[i] = (uint64_t)(fl & SEL_HOST) | ((fl & SEL_MH) ? 1ull << SEL_MH_SHIFT : 0ull) |
-           ((fl & SEL_WALK) ? 1ull << SEL_WALK_SHIFT : 0ull);
+  if (i < n) {
+    flag[i] = fl;
+    val[i] = (uint64_t)(fl & SEL_HOST) | ((fl & SEL_MH) ? 1ull << SEL_MH_SHIFT : 0ull) |
+             ((fl & SEL_WALK) ? 1ull << SEL_WALK_SHIFT : 0ull);
+  }
   // bytes of map / stopWatch-name lines: one atomic per wave (totals zeroed before the launch)
   for (int o = APM_WAVE / 2; o > 0; o >>= 1) ab += __shfl_xor(ab, o, APM_WAVE);
   if ((threadIdx.x & (APM_WAVE - 1)) == 0 && ab) atomicAdd(&totals->aud_bytes, ab);
 }
 
-__global__ void k_host_scatter(const Event* __restrict__ ev, const uint8_t* __restrict__ flag,
-                               const uint64_t* __restrict__ val, const uint64_t* __restrict__ pos, uint32_t cap,
-                               const uint32_t* __restrict__ n_ev_dev, Event* __restrict__ out,
-                               uint32_t* __restrict__ out_idx, uint32_t* __restrict__ mh_idx,
-                               uint32_t* __restrict__ walk_idx, SelCount* __restrict__ totals) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t n = *n_ev_dev;
-  if (i == 0) {
-    const SelCount t = sel_unpack(n == 0 ? 0ull : pos[n - 1] + val[n - 1]);
-    totals->host = t.host; totals->mh = t.mh; totals->walk = t.walk;
+// host / map-header / walk lists, in event order (devscan.h over the batch's events only)
+struct SelValF {
+  const uint64_t* val;
+  __device__ uint64_t operator()(uint32_t i) const { return val[i]; }
+};
+struct SelScatterG {
+  const Event* ev;
+  const uint8_t* flag;
+  const uint64_t* total;
+  Event* out;
+  uint32_t *out_idx, *mh_idx, *walk_idx;
+  SelCount* totals;
+  __device__ void operator()(uint32_t i, uint64_t pos) const {
+    if (i == 0) {
+      const SelCount t = sel_unpack(*total);
+      totals->host = t.host; totals->mh = t.mh; totals->walk = t.walk;
+    }
+    const uint8_t fl = flag[i];
+    if (!fl) return;
+    const SelCount p = sel_unpack(pos);
+    if (fl & SEL_HOST) { out[p.host] = ev[i]; out_idx[p.host] = i; }
+    if (fl & SEL_MH) mh_idx[p.mh] = i;
+    if (fl & SEL_WALK) walk_idx[p.walk] = i;
   }
-  if (i >= n || i >= cap) return;
-  const uint8_t fl = flag[i];
-  if (!fl) return;
-  const SelCount p = sel_unpack(pos[i]);
-  if (fl & SEL_HOST) { out[p.host] = ev[i]; out_idx[p.host] = i; }
-  if (fl & SEL_MH) mh_idx[p.mh] = i;
-  if (fl & SEL_WALK) walk_idx[p.walk] = i;
-}
+};
 
 // ------------------------------------------------------------------------ op build
 enum : uint8_t { SC_NONE = 0, SC_IN = 1, SC_OUT = 2, SC_ACCT = 3, SC_KEY = 4, SC_VALUE = 5 };
@@ -605,8 +614,13 @@ __device__ __forceinline__ uint32_t wave_fscan(uint32_t f, int lane) {
   return f;
 }
 
-__global__ void k_chunk_events(const Event* __restrict__ ev, uint32_t n_ev, uint32_t n_chunks, uint32_t* __restrict__ lo) {
+// (also the folded fills of the join's counters and per-event output counts: the grid covers
+// max(n_chunks, n_ev) + 1 lanes, and it runs before any kernel that touches them)
+__global__ void k_chunk_events(const Event* __restrict__ ev, uint32_t n_ev, uint32_t n_chunks, uint32_t* __restrict__ lo,
+                               uint32_t* __restrict__ zero_words, uint32_t n_zero_words, uint32_t* __restrict__ out_cnt) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < n_zero_words) zero_words[c] = 0;
+  if (c <= n_ev) out_cnt[c] = 0;
   if (c > n_chunks) return;
   uint32_t l = 0, h = n_ev;
   while (l < h) {
@@ -1995,16 +2009,14 @@ int apm_dj_select_host(DJArgs* a, const uint32_t* d_n_ev, uint32_t max_ev, hipSt
   hipLaunchKernelGGL(k_host_flags, dim3((max_ev + TB - 1) / TB), dim3(TB), 0, s, a->ev, d_n_ev, a->bytes, a->chunk_file,
                      a->host_flag, a->sel_val, a->aud, a->n_host, max_ev);
   dj_check(s, "k_host_flags");
-  size_t need = 0;
-  HIP_OK(rocprim::exclusive_scan(nullptr, need, a->sel_val, a->sel_pos, (uint64_t)0, (size_t)max_ev,
-                                 rocprim::plus<uint64_t>(), s));
-  if (need > a->tmp_bytes) return -1;
-  HIP_OK(rocprim::exclusive_scan(a->tmp, need, a->sel_val, a->sel_pos, (uint64_t)0, (size_t)max_ev,
-                                 rocprim::plus<uint64_t>(), s));
-  dj_check(s, "rocprim_exclusive_scan");
-  hipLaunchKernelGGL(k_host_scatter, dim3((max_ev + TB - 1) / TB), dim3(TB), 0, s, a->ev, a->host_flag, a->sel_val,
-                     a->sel_pos, max_ev, d_n_ev, a->host_ev, a->host_ev_idx, a->mh_idx, a->walk_idx, a->n_host);
-  dj_check(s, "k_host_scatter");
+  // sel_pos: the tile sums, then the packed total (sel_pos has max_ev + 64 entries)
+  uint64_t* total = a->sel_pos + (max_ev + DS_TILE - 1) / DS_TILE + 1;
+  if (ds_scan_apply<uint64_t>(SelValF{a->sel_val},
+                              SelScatterG{a->ev, a->host_flag, total, a->host_ev, a->host_ev_idx, a->mh_idx,
+                                          a->walk_idx, a->n_host},
+                              d_n_ev, max_ev, a->sel_pos, total, s) != 0)
+    return -1;
+  dj_check(s, "k_ds_scan (host selection)");
   return 0;
 }
 
@@ -2040,14 +2052,17 @@ static int apm_dj_audit(DJArgs* a, hipStream_t s) {
 int apm_dj_join(DJArgs* a, hipStream_t s) {
   const uint32_t n = a->n_ev;
   const uint32_t cap = a->table_mask + 1;
-  HIP_OK(hipMemsetAsync(a->counts, 0, offsetof(JoinCounts, ejb_unmatched), s));
+  static_assert(offsetof(JoinCounts, ejb_unmatched) % 4 == 0, "JoinCounts zero range");
+  const uint32_t zw = (uint32_t)(offsetof(JoinCounts, ejb_unmatched) / 4);
   if (n) {
-    HIP_OK(hipMemsetAsync(a->out_cnt, 0, ((size_t)n + 1) * 4, s));
+    const uint32_t lanes = std::max(std::max(a->n_chunks + 1, n + 1), zw);
+    hipLaunchKernelGGL(k_chunk_events, dim3((lanes + TB - 1) / TB), dim3(TB), 0, s, a->ev, n, a->n_chunks,
+                       a->chunk_ev_lo, (uint32_t*)a->counts, zw, a->out_cnt);
+    dj_check(s, "k_chunk_events");
     hipLaunchKernelGGL(k_build_ops, dim3((n + TB - 1) / TB), dim3(TB), 0, s, *a);
     dj_check(s, "k_build_ops");
-    hipLaunchKernelGGL(k_chunk_events, dim3((a->n_chunks + 1 + TB - 1) / TB), dim3(TB), 0, s, a->ev, n, a->n_chunks,
-                       a->chunk_ev_lo);
-    dj_check(s, "k_chunk_events");
+  } else {
+    HIP_OK(hipMemsetAsync(a->counts, 0, offsetof(JoinCounts, ejb_unmatched), s));
   }
   // (also for a batch without events: the carry moves to the next generation)
   if (apm_dj_audit(a, s) != 0) return -1;

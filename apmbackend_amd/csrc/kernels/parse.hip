@@ -16,6 +16,8 @@
 
 #include <rocprim/rocprim.hpp>
 
+#include "devscan.h"
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -30,8 +32,12 @@ constexpr int PARSE_LDS = 32 * 1024;       // staged bytes per block (+ 8 KB tok
 
 // --------------------------------------------------------------------------------- K1
 __global__ __launch_bounds__(NL_BLOCK) void k_nl_count(const uint8_t* __restrict__ bytes, uint64_t n,
-                                                      uint32_t* __restrict__ tile_counts) {
+                                                      uint32_t* __restrict__ tile_counts, uint8_t* __restrict__ pad) {
   const uint64_t base = (uint64_t)blockIdx.x * NL_TILE + threadIdx.x * 16;
+  // (folded fills) the 64 zero bytes after the batch that K2's 16-byte loads may touch, and the
+  // scan's extra tile entry -- no block reads either of them
+  if (blockIdx.x == 0 && threadIdx.x < 64) pad[threadIdx.x] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 64) tile_counts[gridDim.x] = 0;
   int c = 0;
   if (base + 16 <= n) {
     const uint4 v = *reinterpret_cast<const uint4*>(bytes + base);
@@ -1104,11 +1110,18 @@ __global__ void k_chunk_lines(const uint32_t* __restrict__ chunk_begin, uint32_t
   chunk_line_lo[c] = lo;
 }
 
-__global__ void k_compact(const Event* __restrict__ ev_tmp, const uint8_t* __restrict__ keep,
-                          const uint32_t* __restrict__ pos, uint32_t n, Event* __restrict__ out) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n && keep[i]) out[pos[i]] = ev_tmp[i];
-}
+struct KeepF {
+  const uint8_t* keep;
+  __device__ uint32_t operator()(uint32_t i) const { return keep[i]; }
+};
+struct CompactG {  // keep[i]: event i lands at its rank among the kept lines (line order)
+  const uint8_t* keep;
+  const Event* ev_tmp;
+  Event* out;
+  __device__ void operator()(uint32_t i, uint32_t p) const {
+    if (keep[i]) out[p] = ev_tmp[i];
+  }
+};
 
 }  // namespace apm
 
@@ -1141,6 +1154,7 @@ int apm_parse_batch(const uint8_t* d_bytes, uint64_t n_bytes, const uint32_t* d_
   if (tiles == 0 || n_chunks == 0) {
     HIP_OK(hipMemsetAsync(d_n_events, 0, 4, stream));
     HIP_OK(hipMemsetAsync(d_n_lines, 0, 4, stream));
+    HIP_OK(hipMemsetAsync(const_cast<uint8_t*>(d_bytes) + n_bytes, 0, 64, stream));
     return 0;
   }
   const uint32_t cap = (uint32_t)std::min<uint64_t>(max_lines, n_bytes);
@@ -1158,8 +1172,8 @@ int apm_parse_batch(const uint8_t* d_bytes, uint64_t n_bytes, const uint32_t* d_
   uint8_t* chunk_init = carve((size_t)(n_chunks + 2));
   void* scan_tmp = carve(APM_SCAN_TMP);
 
-  hipLaunchKernelGGL(k_nl_count, dim3(tiles), dim3(NL_BLOCK), 0, stream, d_bytes, n_bytes, tile_counts);
-  HIP_OK(hipMemsetAsync(tile_counts + tiles, 0, 4, stream));
+  hipLaunchKernelGGL(k_nl_count, dim3(tiles), dim3(NL_BLOCK), 0, stream, d_bytes, n_bytes, tile_counts,
+                     const_cast<uint8_t*>(d_bytes) + n_bytes);
   size_t tmp_bytes = 0;
   HIP_OK(rocprim::exclusive_scan(nullptr, tmp_bytes, tile_counts, tile_off, 0u, tiles + 1,
                                  rocprim::plus<uint32_t>(), stream));
@@ -1219,15 +1233,11 @@ int apm_parse_batch(const uint8_t* d_bytes, uint64_t n_bytes, const uint32_t* d_
   hipLaunchKernelGGL(k_section_apply, dim3(n_chunks, SEC_SEGS), dim3(APM_WAVE), 0, stream, chunk_line_lo,
                      d_chunk_kind, d_chunk_file, n_chunks, line_mask, keep, ev_tmp, d_file_open, seg_state,
                      chunk_init);
-  tmp_bytes = 0;
-  HIP_OK(rocprim::exclusive_scan(nullptr, tmp_bytes, keep, pos, 0u, cap, rocprim::plus<uint32_t>(), stream));
-  if (tmp_bytes > APM_SCAN_TMP) return -1;
-  HIP_OK(rocprim::exclusive_scan(scan_tmp, tmp_bytes, keep, pos, 0u, cap, rocprim::plus<uint32_t>(), stream));
-  hipLaunchKernelGGL(k_compact, dim3((cap + 255) / 256), dim3(256), 0, stream, ev_tmp, keep, pos, cap, d_events);
-  tmp_bytes = 0;
-  HIP_OK(rocprim::reduce(nullptr, tmp_bytes, keep, d_n_events, 0u, cap, rocprim::plus<uint32_t>(), stream));
-  if (tmp_bytes > APM_SCAN_TMP) return -1;
-  HIP_OK(rocprim::reduce(scan_tmp, tmp_bytes, keep, d_n_events, 0u, cap, rocprim::plus<uint32_t>(), stream));
+  // ordered compaction of the kept events over the batch's lines only (devscan.h: the count is
+  // read on the device; `pos` holds the tile sums), the event count -> *d_n_events
+  if (ds_scan_apply<uint32_t>(KeepF{keep}, CompactG{keep, ev_tmp, d_events}, d_n_lines, cap, pos, d_n_events,
+                              stream) != 0)
+    return -1;
   return 0;
 }
 

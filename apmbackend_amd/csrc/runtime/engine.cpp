@@ -814,7 +814,7 @@ void Engine::launch_parse(ParseSlot& ps, const uint8_t* host_bytes, uint64_t n_b
   uint8_t* dbytes = dev() ? dj_->d_bytes(k) : d_bytes_;
   Event* devents = dev() ? dj_->d_events(k) : (ps.d_events_host ? ps.d_events_host : d_events_);
   HIP_OK(hipMemcpyAsync(dbytes, ps.hb, off, hipMemcpyHostToDevice, parse_stream_));
-  HIP_OK(hipMemsetAsync(dbytes + off, 0, 64, parse_stream_));
+  // (apm_parse_batch zeroes the 64 bytes after the batch inside its first kernel)
   h2d(d_chunk_begin_[k], ps.h_chunk_begin, (n_chunks + 1) * 4, parse_stream_);
   h2d(d_chunk_kind_[k], ps.h_chunk_kind, n_chunks + 1, parse_stream_);
   h2d(d_chunk_file_[k], ps.h_chunk_file, (n_chunks + 1) * 4, parse_stream_);

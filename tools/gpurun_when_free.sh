@@ -3,9 +3,20 @@
 # free / infrastructure back-off / box lost while being prepared).  A command that ran -- whatever
 # its exit status -- is never re-submitted.
 #   tools/gpurun_when_free.sh LOG TIMEOUT 'command'
+# (run a copy -- bash reads a script while it runs: `cp tools/gpurun_when_free.sh /tmp/gw.sh`, with
+#  REPO=/root/repo -- so editing the tree's copy never changes a wrapper in flight)
 log=$1; to=$2; cmd=$3
+REPO=${REPO:-$(cd "$(dirname "$0")/.." && pwd)}
+fresh() {  # the in-tree .so was linked from the csrc/ now in the tree (else the GPU run would refuse it)
+  (cd "$REPO" && timeout 120 python -c "
+from apmbackend_amd import _native
+from apmbackend_amd.build_native import csrc_hash
+import sys
+sys.exit(0 if _native.load(build_if_missing=False).csrc_hash() == csrc_hash() else 1)" 2>/dev/null)
+}
 for attempt in 1 2 3 4 5 6 7 8 9 10 11 12; do
-  /usr/local/graft/bin/gpurun --timeout "$to" -- "$cmd" > "$log" 2>&1
+  while ! fresh; do echo "[attempt $attempt] .so stale (rebuild pending): waiting" >> "$log.attempts"; sleep 30; done
+  (cd "$REPO" && /usr/local/graft/bin/gpurun --timeout "$to" -- "$cmd") > "$log" 2>&1
   rc=$?
   if grep -qE "no free box right now|backing off after the last attempt|stopped responding while being prepared" "$log" \
      && ! grep -qE "status=(ok|fail|timeout|error)" "$log"; then
