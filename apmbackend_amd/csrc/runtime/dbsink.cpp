@@ -32,6 +32,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <deque>
 #include <memory>
 #include <mutex>
@@ -622,6 +623,51 @@ class DbSink : public ByteSink {
     return encoded_[t];
   }
 
+  // ---- checkpoint support: an acknowledged-flush watermark instead of a drain.
+  // Every flush gets a sequence number when it is submitted; `acked` = the smallest sequence not
+  // yet written (all earlier flushes are in the database / spool).  set_ack_file() makes each
+  // writer lane record {incarnation, acked} in a 16-byte file after every write (no fsync: it
+  // survives a process crash, like the spool files themselves).  snapshot_pending() submits the
+  // partial buffers and copies every flush not yet acknowledged -- without waiting for a writer --
+  // so a checkpoint can carry them: on restore, the flushes at or above the file's watermark are
+  // submitted again (the ones written after the snapshot were acknowledged in the file).
+  struct PendingJob { uint64_t seq; int type; bool encoded; int64_t n; std::string data; };
+  void set_ack_file(const std::string& path, uint64_t incarnation) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (ack_fd_ >= 0) ::close(ack_fd_);
+    ack_fd_ = ::open(path.c_str(), O_WRONLY | O_CREAT | O_CLOEXEC, 0644);
+    if (ack_fd_ < 0) throw std::runtime_error("DbSink: cannot open ack file " + path);
+    incarnation_ = incarnation;
+    write_ack_locked();
+  }
+  // Rows that failed go back to their buffer and keep their first sequence as a floor (`floor`
+  // of the job that carries them next), so the watermark never passes rows not yet written.
+  uint64_t acked_locked() const {
+    uint64_t a = next_seq_;
+    for (auto& kv : live_) a = std::min(a, kv.second->floor);
+    for (int t = 0; t < NT; ++t)
+      if (buf_[t].n > 0) a = std::min(a, rebuf_floor_[t]);
+    return a;
+  }
+  uint64_t acked() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return acked_locked();
+  }
+  std::pair<uint64_t, std::vector<PendingJob>> snapshot_pending() {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int t = 0; t < NT; ++t)
+      if (buf_[t].n > 0) submit_locked(t);
+    std::vector<PendingJob> out;
+    out.reserve(live_.size());
+    for (auto& kv : live_) {
+      const Job& j = *kv.second;
+      // (a flush may still be on its way through an encoder: its wire lines are the payload then)
+      const bool enc = j.ready;
+      out.push_back(PendingJob{j.seq, j.type, enc, j.n, std::string(enc ? j.data() : std::string_view(j.lines))});
+    }
+    return {acked_locked(), std::move(out)};
+  }
+
   void set_limit(int64_t limit, double max_wait_ms) {
     std::lock_guard<std::mutex> lk(mu_);
     limit_ = std::max<int64_t>(1, limit);
@@ -643,6 +689,7 @@ class DbSink : public ByteSink {
     // until `hold` is released (the engine reuses the buffer only then)
     std::string_view ext;
     std::shared_ptr<const void> hold;
+    uint64_t floor = UINT64_MAX;  // smallest sequence whose rows this flush carries (re-buffered rows)
     bool taken = false, ready = false;
     std::string_view data() const { return ext.data() ? ext : std::string_view(encoded); }
   };
@@ -662,6 +709,8 @@ class DbSink : public ByteSink {
     j->type = t;
     j->n = buf_[t].n;
     j->seq = next_seq_++;
+    j->floor = std::min(j->seq, rebuf_floor_[t]);
+    rebuf_floor_[t] = UINT64_MAX;
     if (encoded_[t]) {  // COPY text already: straight to the writer
       j->encoded.swap(buf_[t].lines);
       j->ready = true;
@@ -680,6 +729,13 @@ class DbSink : public ByteSink {
   static constexpr uint64_t kLaneBlock = 16;
   void enqueue_locked(const std::shared_ptr<Job>& j) {
     order_[(size_t)((rr_++ / kLaneBlock) % (uint64_t)lanes_)].push_back(j);
+    if (j->floor == UINT64_MAX) j->floor = j->seq;
+    live_[j->seq] = j;
+  }
+  void write_ack_locked() {
+    if (ack_fd_ < 0) return;
+    const uint64_t v[2] = {incarnation_, acked_locked()};
+    if (::pwrite(ack_fd_, v, sizeof v, 0) != (ssize_t)sizeof v) last_error_ = "ack file write failed";
   }
   int64_t queued_locked() const {
     int64_t q = 0;
@@ -731,7 +787,10 @@ class DbSink : public ByteSink {
       const double dt = mono_ms() - t0;
       {
         std::lock_guard<std::mutex> lk(mu_);
-        for (size_t i = 0; i < run.size(); ++i) order.pop_front();
+        for (size_t i = 0; i < run.size(); ++i) {
+          order.pop_front();
+          live_.erase(run[i]->seq);  // written, doubtful (not retried) or back in its buffer
+        }
         for (size_t i = 0; i < ok; ++i) {
           Job& j = *run[i];
           rows_ += j.n;
@@ -761,6 +820,7 @@ class DbSink : public ByteSink {
             else back += run[i]->lines;
             run[i]->hold.reset();
             n += run[i]->n;
+            rebuf_floor_[t] = std::min(rebuf_floor_[t], run[i]->floor);
           }
           if (!back.empty()) {
             if (b.n == 0) b.deadline = mono_ms() + max_wait_ms_;
@@ -768,6 +828,7 @@ class DbSink : public ByteSink {
             b.n += n;
           }
         }
+        write_ack_locked();
       }
       done_cv_.notify_all();
     }
@@ -784,6 +845,7 @@ class DbSink : public ByteSink {
     for (auto& t : wr_)
       if (t.joinable()) t.join();
     w_.clear();
+    if (ack_fd_ >= 0) { ::close(ack_fd_); ack_fd_ = -1; }
   }
 
   int64_t limit_;
@@ -801,6 +863,10 @@ class DbSink : public ByteSink {
   double lane_ms_[64] = {};
   std::vector<std::string> spare_;
   uint64_t next_seq_ = 0;
+  std::map<uint64_t, std::shared_ptr<Job>> live_;  // submitted, not yet written (by sequence)
+  uint64_t rebuf_floor_[NT] = {UINT64_MAX, UINT64_MAX, UINT64_MAX, UINT64_MAX, UINT64_MAX};
+  int ack_fd_ = -1;
+  uint64_t incarnation_ = 0;
   bool stop_ = false;
   std::vector<std::thread> enc_;
   std::vector<std::thread> wr_;
@@ -856,6 +922,15 @@ void register_dbsink(py::module_& m) {
       .def("take_interval", &DbSink::take_interval)
       .def("set_limit", &DbSink::set_limit)
       .def("is_encoded", &DbSink::is_encoded)
+      .def("set_ack_file", &DbSink::set_ack_file)
+      .def("acked", &DbSink::acked)
+      .def("snapshot_pending", [](DbSink& s) {
+        std::pair<uint64_t, std::vector<DbSink::PendingJob>> r;
+        { py::gil_scoped_release rel; r = s.snapshot_pending(); }
+        py::list jobs;
+        for (auto& j : r.second) jobs.append(py::make_tuple(j.seq, j.type, j.encoded, j.n, py::bytes(j.data)));
+        return py::make_tuple(r.first, jobs);
+      })
       .def("consume_encoded", [](DbSink& s, int type, py::bytes b) {
         std::string_view v = b;
         py::gil_scoped_release rel;

@@ -207,6 +207,13 @@ class IngestService:
         self.producers: Dict[str, Any] = {}
         if self.mode == "inproc":
             self.inserter = DBInserter(self.cfg)
+            self._sink_incarnation = int.from_bytes(os.urandom(8), "little") >> 1
+            self.sink_pending_rows = 0
+            if self.ckpt_dir:
+                os.makedirs(self.ckpt_dir, exist_ok=True)
+                if restored:
+                    self._restore_sink()  # (reads the previous incarnation's ack file first)
+                self.inserter.set_ack_file(self._sink_ack_path(), self._sink_incarnation)
             if engine == "native":
                 # db / audit / fs go engine output lane -> native sink directly; al stays on the
                 # Python side (the e-mail notifier reads it too)
@@ -346,6 +353,55 @@ class IngestService:
                         "shard with fresh engine state", ck, e, ", ".join(moved))
             return False
 
+    # ------------------------------------------------------------------ sink watermark
+    def _sink_ack_path(self) -> str:
+        return os.path.join(self.ckpt_dir, f"sink.rank{self.rank}.ack")
+
+    def _snapshot_sink(self) -> Optional[Dict[str, Any]]:
+        """The DB sink's unacknowledged flushes -> <ckdir>/sink_pending.rank<r>.<n>.bin (fsync +
+        rename before the engine checkpoint that names it is published)."""
+        from .sinks import write_sink_snapshot
+        acked, jobs = self.inserter.snapshot_pending()
+        name = f"sink_pending.rank{self.rank}.{self.n_checkpoints + 1}.bin"
+        write_sink_snapshot(os.path.join(self.ckpt_dir, name), jobs)
+        # the pending files of older checkpoints are no longer referenced (keep the previous one)
+        for old in glob.glob(os.path.join(self.ckpt_dir, f"sink_pending.rank{self.rank}.*.bin")):
+            try:
+                k = int(old.rsplit(".", 2)[-2])
+            except ValueError:
+                continue
+            if k < self.n_checkpoints:
+                try:
+                    os.remove(old)
+                except OSError:
+                    pass
+        self.sink_pending_rows = sum(int(j[3]) for j in jobs)
+        return {"incarnation": self._sink_incarnation, "acked": acked, "pending": name, "jobs": len(jobs),
+                "rows": self.sink_pending_rows}
+
+    def _restore_sink(self):
+        """After a restore: re-submit the checkpoint's pending flushes that the sink did not
+        acknowledge before the process ended (its ack file; a different incarnation in the file --
+        an interrupted earlier restore -- means nothing is known: everything is re-submitted, at
+        least once)."""
+        from .sinks import read_sink_ack, read_sink_snapshot
+        try:
+            meta = json.loads(self._ckpt_extra.decode("utf-8")).get("sink") if self._ckpt_extra else None
+        except (ValueError, AttributeError):
+            meta = None
+        if not meta:
+            return 0
+        path = os.path.join(self.ckpt_dir, meta["pending"])
+        if not os.path.exists(path):
+            log.warning("checkpoint names sink snapshot %s, which is missing: its rows are lost", path)
+            return 0
+        acked_now = read_sink_ack(self._sink_ack_path(), int(meta["incarnation"]))
+        n, jobs = read_sink_snapshot(path, acked_now)
+        rows = self.inserter.resubmit(jobs)
+        log.info("sink: re-submitted %d flushes (%d rows) of the checkpoint's %d unacknowledged ones", len(jobs),
+                 rows, n)
+        return rows
+
     def _import_reference(self, servers):
         """Cut-over from a running reference deployment: seed stats buckets, the release heap,
         the z-score histories and alert cooldowns from its JSON resume files."""
@@ -415,24 +471,22 @@ class IngestService:
         t0 = time.perf_counter()
         # undelivered output goes out first so the checkpoint and the sinks agree
         self._drain_outputs()
+        sink_meta = None
         if self.inserter is not None and self.mode == "inproc":
-            # the engine's output lane feeds the native sink directly: hand over everything of the
-            # batches this checkpoint covers, then write it (flush + writer drain), so the offsets
-            # below never run ahead of rows the DB has not acknowledged (stream_insert_db.js
-            # persists its buffers on exit for the same reason, :222-244)
+            # The engine's output lane feeds the native sink directly.  Every row of the batches this
+            # checkpoint covers is handed over (flush: the engine pipeline, not the database), then
+            # the rows the DB has not acknowledged yet are snapshotted into the checkpoint instead
+            # of being waited for: ingest never waits for the DB writer, and a restore submits
+            # exactly the flushes the sink's acknowledged watermark (its ack file) does not cover
+            # (stream_insert_db.js persists its buffers on exit for the same reason, :222-244).
             self.native.flush()
-            self.inserter.flush_all()
-            st = self.inserter.sink_stats()
-            if st.get("buffered", 0) or st.get("queued", 0):
-                log.warning("checkpoint postponed: %s DB rows not written yet (sink failures: %s)",
-                            st.get("buffered", 0) + st.get("queued", 0), st.get("failures"))
-                return None
+            sink_meta = self._snapshot_sink()
         if self.qm is not None and not self.qm.wait_confirms(float(self.cfg["gpu"].get("confirmTimeoutSeconds", 60))):
             # offsets may only advance past data the broker has taken responsibility for
             log.warning("checkpoint postponed: the broker has not confirmed every publish yet")
             return None
         extra = json.dumps({"tail": json.loads(self.tailer.offsets_json()), "world": self.world,
-                            "rank": self.rank, "servers": self.my_servers}).encode("utf-8")
+                            "rank": self.rank, "servers": self.my_servers, "sink": sink_meta}).encode("utf-8")
         prefix = ck[:-len(".ckpt")]
         seq = self.eng.checkpoint_async(prefix, extra)
         if seq < 0:

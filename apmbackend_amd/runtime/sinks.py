@@ -370,6 +370,53 @@ def load_resume(path: str) -> Dict[str, List[Dict[str, Any]]]:
 
 # --------------------------------------------------------------------------- inserter
 
+# ---- checkpointed sink snapshots (service.checkpoint / _restore_sink)
+def write_sink_snapshot(path: str, jobs) -> None:
+    """The sink's unacknowledged flushes [(seq, type index, encoded, rows, bytes)], fsync'd and
+    renamed into place (it must be durable before the checkpoint naming it is published)."""
+    import struct
+    tmp = path + ".tmp"
+    with open(tmp, "wb") as f:
+        f.write(struct.pack("<8sQ", b"APMSINK1", len(jobs)))
+        for seq, ti, enc, rows, data in jobs:
+            f.write(struct.pack("<QIBqQ", int(seq), int(ti), 1 if enc else 0, int(rows), len(data)))
+            f.write(data)
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(tmp, path)
+
+
+def read_sink_ack(path: str, incarnation: int) -> int:
+    """The acknowledged watermark the sink of `incarnation` left in its ack file, or -1 when the
+    file is missing or belongs to another incarnation (then nothing is known to be written)."""
+    import struct
+    try:
+        with open(path, "rb") as f:
+            inc, acked = struct.unpack("<QQ", f.read(16))
+    except (OSError, struct.error):
+        return -1
+    return int(acked) if inc == int(incarnation) else -1
+
+
+def read_sink_snapshot(path: str, acked: int):
+    """(flushes in the snapshot, [the ones at or above `acked`])."""
+    import struct
+    with open(path, "rb") as f:
+        data = f.read()
+    magic, n = struct.unpack_from("<8sQ", data, 0)
+    if magic != b"APMSINK1":
+        raise RuntimeError(f"{path}: not a sink snapshot")
+    off, jobs = 16, []
+    hdr = struct.calcsize("<QIBqQ")
+    for _ in range(n):
+        seq, ti, enc, rows, ln = struct.unpack_from("<QIBqQ", data, off)
+        off += hdr
+        if seq >= acked:
+            jobs.append((seq, ti, bool(enc), rows, data[off:off + ln]))
+        off += ln
+    return n, jobs
+
+
 class DBInserter:
     """The consumer side of ``db_insert`` (one per node, or one per rank).
 
@@ -578,6 +625,39 @@ class DBInserter:
             self._sync_stats()
             return self.core.stats()["rows"] - before
         return sum(self.flush(t) for t in TYPES)
+
+    # -- checkpoint support (service.checkpoint): the acknowledged watermark instead of a drain
+    def set_ack_file(self, path: str, incarnation: int):
+        if self.core is not None:
+            self.core.set_ack_file(path, int(incarnation))
+
+    def snapshot_pending(self):
+        """(acked watermark, [(seq, type index, encoded, rows, bytes)]) of every row consumed
+        but not yet written -- taken without waiting for a writer (native sink)."""
+        if self.core is not None:
+            acked, jobs = self.core.snapshot_pending()
+            return int(acked), [tuple(j) for j in jobs]
+        # the Python path (custom writers) has no acknowledgement watermark: it writes its buffers
+        # out synchronously instead, so nothing is pending
+        self.flush_all()
+        return 0, []
+
+    def resubmit(self, jobs) -> int:
+        """Queue flushes taken from a checkpoint's snapshot again (restore after a crash)."""
+        n = 0
+        for _seq, ti, encoded, rows, data in jobs:
+            t = TYPES[int(ti)]
+            if self.core is not None:
+                if encoded:
+                    self.core.add_encoded(int(ti), data, int(rows))
+                else:
+                    self.core.consume(data)
+            else:
+                for ln in data.decode("utf-8").split("\n"):
+                    if ln:
+                        self._add(t, pg_row_from_copy(t, ln) if encoded else ln)
+            n += int(rows)
+        return n
 
     def _sync_stats(self):
         rows, ms = self.core.take_interval()

@@ -421,3 +421,64 @@ def test_native_sink_psql_unacknowledged_copy_is_not_retried(tmp_path, monkeypat
     want = sinks.copy_encode_lines(lines)
     assert open(out / "apm_stats.rows").read() == "".join(want["fs"])  # committed exactly once
     s.close()
+
+
+def test_sink_snapshot_watermark_restores_unwritten_rows_once(tmp_path, monkeypatch):
+    """checkpoints snapshot the sink's unacknowledged flushes instead of draining
+    it.  Flushes the writer acknowledged after the snapshot are skipped on restore (the ack file's
+    watermark), flushes it never wrote are submitted again -- every row lands exactly once."""
+    import sys
+    from apmbackend_amd import _native
+    N = _native.load(build_if_missing=False)
+    tables = ["apm_tx", "apm_stats", "apm_alerts", "apm_jmx", "apm_fleet_stats"]
+    fake = [sys.executable, os.path.join(os.path.dirname(__file__), "fixtures", "fake_psql.py")]
+    out = tmp_path / "pg"
+    out.mkdir()
+    monkeypatch.setenv("FAKE_PSQL_OUT", str(out))
+    monkeypatch.setenv("FAKE_PSQL_FAIL", "apm_stats")  # the stats table is down: fs flushes fail
+    ack = str(tmp_path / "sink.ack")
+    s = N.DbSink(1000, 1e9, tables, ["a", "b", "c", "d", "e"], "psql", fake, 0, 2)
+    s.set_ack_file(ack, 7)
+    lines = _wire_lines(10)
+    s.consume(("\n".join(lines) + "\n").encode())
+    s.flush_all()
+    s.drain()
+    acked_before, jobs = s.snapshot_pending()  # (no drain: the fs rows are back in their buffer)
+    assert sum(j[3] for j in jobs) == 10 and {j[1] for j in jobs} == {1}
+    snap = str(tmp_path / "pending.bin")
+    sinks.write_sink_snapshot(snap, jobs)
+    s.close()  # "crash": the fs rows were never written
+    acked = sinks.read_sink_ack(ack, 7)
+    assert acked >= 0 and sinks.read_sink_ack(ack, 8) == -1  # another incarnation: unknown
+    n, todo = sinks.read_sink_snapshot(snap, acked)
+    assert n == len(jobs) and sum(j[3] for j in todo) == 10
+    monkeypatch.setenv("FAKE_PSQL_FAIL", "")  # the restarted service: table back
+    s2 = N.DbSink(1000, 1e9, tables, ["a", "b", "c", "d", "e"], "psql", fake, 0, 2)
+    for _seq, ti, enc, rows, data in todo:
+        if enc:
+            s2.add_encoded(ti, data, rows)
+        else:
+            s2.consume(data)
+    s2.flush_all()
+    s2.drain()
+    s2.close()
+    want = sinks.copy_encode_lines(lines)
+    assert open(out / "apm_tx.rows").read() == "".join(want["tx"])
+    assert open(out / "apm_stats.rows").read() == "".join(want["fs"])
+
+
+def test_sink_snapshot_of_acknowledged_flushes_restores_nothing(tmp_path):
+    from apmbackend_amd import _native
+    N = _native.load(build_if_missing=False)
+    tables = ["apm_tx", "apm_stats", "apm_alerts", "apm_jmx", "apm_fleet_stats"]
+    ack = str(tmp_path / "sink.ack")
+    s = N.DbSink(3, 1e9, tables, ["a", "b", "c", "d", "e"], "spool", [str(tmp_path / "spool")], 1 << 30, 2, 2)
+    s.set_ack_file(ack, 11)
+    lines = _wire_lines(40)
+    s.consume(("\n".join(lines) + "\n").encode())
+    _acked, jobs = s.snapshot_pending()  # taken while the lanes may still be writing
+    sinks.write_sink_snapshot(str(tmp_path / "p.bin"), jobs)
+    s.drain()  # everything gets written and acknowledged
+    s.close()
+    _n, todo = sinks.read_sink_snapshot(str(tmp_path / "p.bin"), sinks.read_sink_ack(ack, 11))
+    assert todo == []

@@ -18,6 +18,7 @@
 #   preset:NAME        bench.py --preset NAME (config2, config4, firehose) 20/5
 #   service            bench.py --path service (production path, checkpoints on), 200 steps
 #   prof               rocprofv3 --kernel-trace --stats of bench.py 20/5
+#   timeline           rocprofv3 --kernel-trace --memory-copy-trace (tools/gpu_timeline.py reads it)
 #   pmc:C1,C2,...      one rocprofv3 --pmc pass of bench.py 10/3 (keep within one pass's counter budget)
 #   env:K=V            export K=V for the following tasks (A/B switches)
 #   py:MODULE          python -m MODULE (diagnostics under tools/)
@@ -56,6 +57,8 @@ for task in "$@"; do
     service) run "service_$n" 600 python -u bench.py --path service --steps 200 --warmup 5 --service-dir /tmp/apm_svc ;;
     prof) run "prof_$n" 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$n" -o run -- \
             python3 bench.py --steps 20 --warmup 5 ;;
+    timeline) run "timeline_$n" 400 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$O/tl_$n" -o run -- \
+                python3 bench.py --steps 20 --warmup 5 ;;
     pmc:*) c=${task#pmc:}; run "pmc_$n" 120 rocprofv3 --pmc ${c//,/ } --output-format csv -d "$O/pmc_$n" -o run -- \
              python3 bench.py --steps 10 --warmup 3 ;;
     env:*) export "${task#env:}"; echo "[env] ${task#env:}" ;;

@@ -56,6 +56,8 @@ def main():
     ks = _rows(a.dir, "*kernel_trace.csv")
     cs = _rows(a.dir, "*memory_copy_trace.csv")
     kern = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in ks]
+    qcol = next((c for c in ("Stream_Id", "Queue_Id") if ks and c in ks[0]), None)
+    kq = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get(qcol, "?")) for r in ks] if qcol else []
     cop = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Direction", "copy")) for r in cs]
     anchors = sorted(s for s, _e, n in kern if a.anchor in n)
     if len(anchors) < a.steps + 1:
@@ -73,6 +75,15 @@ def main():
     print(f"copies busy (union):  {cb / 1e6 / n:.3f} ms/batch ({100.0 * cb / wall:.1f} %)")
     print(f"GPU busy (kernels + copies, union): {ab / 1e6 / n:.3f} ms/batch ({100.0 * ab / wall:.1f} %)")
     print(f"kernel launches per batch: {len(kin) / n:.1f}, copies per batch: {len(cin) / n:.1f}")
+    if kq:  # busy time per stream / hardware queue: which one is saturated
+        byq = collections.defaultdict(list)
+        for s_, e_, q in kq:
+            if e_ > t0 and s_ < t1:
+                byq[q].append((max(s_, t0), min(e_, t1)))
+        print(f"\n| {qcol} | kernels/batch | busy ms/batch | busy % |\n|---|---|---|---|")
+        for q, iv in sorted(byq.items(), key=lambda x: -_union(x[1])):
+            u = _union(iv)
+            print(f"| {q} | {len(iv) / n:.1f} | {u / 1e6 / n:.3f} | {100.0 * u / wall:.1f} |")
     by = collections.defaultdict(lambda: [0, 0])
     for s, e, nm in kin:
         by[short(nm)][0] += e - s
