@@ -388,6 +388,10 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   d_fmt_tmp_ = dmalloc(fmt_tmp_bytes_);
   HIP_OK(hipHostMalloc((void**)&h_fmt_meta_, 64, hipHostMallocDefault));
   HIP_OK(hipHostGetDevicePointer((void**)&hd_fmt_meta_, h_fmt_meta_, 0));
+  {
+    const char* e = std::getenv("APM_FMT_HOST");
+    fmt_host_ = e && e[0] == '1';
+  }
   // alerts
   d_alerts_ = (AlertRec*)dmalloc((size_t)cfg_.max_alerts * sizeof(AlertRec));
   d_n_alerts_ = d_big_n_ + 2;
@@ -2612,9 +2616,24 @@ void Engine::format_rollover_text(int64_t edge_ts) {
   trace_event("fmt.wait_lane", tf1, now_ms(), 1);
   const size_t st_cap = fa.want_st ? (size_t)n * (176 + max_name_len_) : 0;
   const size_t fs_cap = fa.want_fs ? (size_t)n * cfg_.n_lags * (fs_copy_ ? 720 + 2 * max_name_len_ : 560 + max_name_len_) : 0;
-  if (st_cap + fs_cap + 64 > fmt_out_cap_[k]) d_fmt_out_[k] = (char*)regrow(d_fmt_out_[k], fmt_out_cap_[k], st_cap + fs_cap + 64);
-  fa.st_out = d_fmt_out_[k];
-  fa.fs_out = d_fmt_out_[k] + st_cap;
+  if (fmt_host_) {
+    // the kernel writes into the pinned buffer itself: the sink must be done with its contents
+    const double th = now_ms();
+    wait_fmt_holds(k);
+    trace_event("fmt.wait_holds", th, now_ms(), 1);
+    if (st_cap + fs_cap + 64 > h_fmt_cap_[k]) {
+      if (h_fmt_out_[k]) HIP_OK(hipHostFree(h_fmt_out_[k]));
+      h_fmt_cap_[k] = (st_cap + fs_cap + 64) * 5 / 4;
+      HIP_OK(hipHostMalloc((void**)&h_fmt_out_[k], h_fmt_cap_[k], hipHostMallocDefault));
+      HIP_OK(hipHostGetDevicePointer((void**)&hd_fmt_out_[k], h_fmt_out_[k], 0));
+    }
+    fa.st_out = hd_fmt_out_[k];
+    fa.fs_out = hd_fmt_out_[k] + st_cap;
+  } else {
+    if (st_cap + fs_cap + 64 > fmt_out_cap_[k]) d_fmt_out_[k] = (char*)regrow(d_fmt_out_[k], fmt_out_cap_[k], st_cap + fs_cap + 64);
+    fa.st_out = d_fmt_out_[k];
+    fa.fs_out = d_fmt_out_[k] + st_cap;
+  }
   const double tpl = now_ms();
   if (apm_format_plan(&fa, d_fmt_tmp_, fmt_tmp_bytes_, stream_) != 0) throw std::runtime_error("format scan failed");
   const double tpw = now_ms();
@@ -2630,6 +2649,23 @@ void Engine::format_rollover_text(int64_t edge_ts) {
   HIP_OK(hipEventRecord(ev_fmt_[k], stream_));
   trace_event("fmt.plan", tf0, now_ms(), 1);
   char* dst = d_fmt_out_[k];
+  if (fmt_host_) {
+    fmt_task_[k] = post_out([this, k, st_cap]() {
+      const double tl0 = now_ms();
+      HIP_OK(hipEventSynchronize(ev_fmt_[k]));  // the text is in host memory once K12 completed
+      const size_t st_total = h_fmt_meta_[4 * k], fs_total = h_fmt_meta_[4 * k + 1];
+      {
+        std::lock_guard<std::mutex> g(out_mu_);
+        formatted_bytes_lane_ += st_total + fs_total;
+      }
+      const double tl1 = now_ms();
+      emit_bytes(OUT_ST, h_fmt_out_[k], st_total);
+      emit_bytes_held(OUT_FS, h_fmt_out_[k] + st_cap, fs_total, k);
+      trace_event("lane st/fs wait (direct)", tl0, tl1, 4);
+      trace_event("lane st/fs emit", tl1, now_ms(), 4);
+    });
+    return;
+  }
   fmt_task_[k] = post_out([this, k, dst, st_cap]() {
     HIP_OK(hipEventSynchronize(ev_fmt_[k]));
     const size_t st_total = h_fmt_meta_[4 * k], fs_total = h_fmt_meta_[4 * k + 1];

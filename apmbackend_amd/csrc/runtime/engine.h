@@ -1034,6 +1034,10 @@ class Engine {
   size_t fmt_out_cap_[2] = {0, 0};
   char* h_fmt_out_[2] = {nullptr, nullptr};      // pinned ping-pong staging for the D2H of formatted text
   size_t h_fmt_cap_[2] = {0, 0};
+  // APM_FMT_HOST=1: K12 writes the st/fs text straight into h_fmt_out_ (device alias hd_fmt_out_)
+  // over the host link -- no HBM round trip, no D2H copy on the output lane
+  bool fmt_host_ = false;
+  char* hd_fmt_out_[2] = {nullptr, nullptr};
   hipEvent_t ev_fmt_[2] = {nullptr, nullptr};
   uint64_t fmt_task_[2] = {0, 0};
   int fmt_k_ = 0;

@@ -86,6 +86,8 @@ def main():
                          "instead of raw text to --sink")
     ap.add_argument("--no-warm", action="store_true")
     ap.add_argument("--sink", default="/dev/null", help="file receiving the db_insert stream")
+    ap.add_argument("--spool-dir", default=os.environ.get("APM_SPOOL_DIR", "/var/tmp" if os.path.isdir("/var/tmp") else None),
+                    help="--db-sink spool: where the COPY spool files go (a disk, not tmpfs)")
     ap.add_argument("--no-prefetch", action="store_true", help="disable the next-batch parse overlap")
     ap.add_argument("--no-fleet", action="store_true",
                     help="skip the fleet baseline exchange / lock-step clocks (always on by default, also at N=1)")
@@ -206,7 +208,8 @@ def main():
         import tempfile
         from apmbackend_amd.runtime.notifier import AlertNotifier
         from apmbackend_amd.runtime.sinks import DBInserter
-        spool_dir = tempfile.mkdtemp(prefix="apm_bench_spool_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+        # on disk (the firehose number was measured into tmpfs before)
+        spool_dir = tempfile.mkdtemp(prefix="apm_bench_spool_", dir=args.spool_dir)
         cfg["streamInsertDb"].update({"sink": args.db_sink, "copySinkDir": spool_dir, "encoderThreads": 8,
                                       "writerLanes": args.writer_lanes,
                                       "copySinkRotateBytes": 1 << 62})
