@@ -2418,19 +2418,24 @@ void* Engine::regrow(void* old, size_t& cap, size_t need) {
   // 2x headroom: a regrow syncs the stream and hipFree waits for the device (a few ms of one
   // batch), so the per-batch buffers must stop growing during the warm-up
   size_t nc = std::max<size_t>(2 * need, 4 << 20);
-  if (old) {
-    HIP_OK(hipStreamSynchronize(stream_));
-    HIP_OK(hipFree(old));
-    std::lock_guard<std::mutex> g(alloc_mu_);
-    allocations_.erase(std::remove(allocations_.begin(), allocations_.end(), old), allocations_.end());
-    auto it = alloc_bytes_.find(old);
-    if (it != alloc_bytes_.end()) {
-      device_bytes_ -= it->second;
-      alloc_bytes_.erase(it);
-    }
-  }
+  // The old buffer is retired, not freed: kernels still in flight on any stream may read it, and
+  // hipFree would wait for the whole device (the collective stream included).  Retired buffers
+  // stay listed in allocations_ (and counted) until the engine goes away; with 2x growth they
+  // add up to less than the live buffer.
+  (void)old;
   cap = nc;
-  return dmalloc(nc);
+  void* p = nullptr;
+  const size_t bytes = (nc + 255) & ~(size_t)255;
+  HIP_OK(hipMalloc(&p, bytes));
+  // zeroed in order on the stats stream; the sync orders it for the other streams' later work
+  // without waiting for them (dmalloc's device-wide sync is for construction time)
+  HIP_OK(hipMemsetAsync(p, 0, bytes, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+  std::lock_guard<std::mutex> g(alloc_mu_);
+  allocations_.push_back(p);
+  alloc_bytes_[p] = bytes;
+  device_bytes_ += bytes;
+  return p;
 }
 
 void Engine::sync_format_tables() {
