@@ -357,6 +357,64 @@ __device__ bool needs_host(const Event& e, const uint8_t* __restrict__ bytes) {
   return false;
 }
 
+// Non-audit events: the byte-level fields the join needs, derived once on the parse stream (next
+// to needs_host, which scans the same bytes) and stored in the event's AudF slot, so k_build_ops
+// -- on the join stream, the ingest thread's critical path -- only reads them:
+//   CT exit with a BAF token: the account scan (el = value, PRE_BAF / PRE_BAF_VALID);
+//   SOAP request start: hash of the logId field (h_item);  SOAP account / value: the parsed
+//   number (el, PRE_SOAP_VALID).
+// Returns -1: the host derives the event (needs_host), 0: nothing stored, 1: stored in f.
+enum : uint8_t { PRE_BAF = 1, PRE_BAF_VALID = 2, PRE_SOAP_VALID = 4 };
+__device__ int pre_fields(const Event& e, const uint8_t* __restrict__ bytes, AudF& f) {
+  if (e.mask & PM_HOST) return -1;
+  const uint8_t* p = bytes + e.off;
+  f.h_item = 0; f.el = apm_nan(); f.h_sw = 0; f.ts = apm_nan(); f.ref = 0; f.len = 0; f.flags = 0; f.pad = 0;
+  if (e.kind >= LK_EJB_ENTRY && e.kind <= LK_CT_EXIT) {
+    if (!(e.mask & PM_KEYS) || e.ntok < 3) return -1;
+    if (e.kind == LK_CT_EXIT && (e.mask & PM_BAF)) {
+      int n = 9;  // fewer than 4 tokens: the account string is "undefined" (NaN, not digits)
+      bool digits = false;
+      double v = apm_nan();
+      if (e.ntok >= 4 && !baf_account_scan(p, e.t3s, e.t3e, n, digits, v)) return -1;
+      f.el = v;
+      f.flags = (uint8_t)((n > 0 ? PRE_BAF : 0) | (digits ? PRE_BAF_VALID : 0));
+      return 1;
+    }
+    return 0;
+  }
+  if (e.kind == LK_SOAP) {
+    const uint32_t m = e.mask;
+    if (m & PM_SOAP_IN) {  // ws[1].split('=')[1]; no '=' -> has_log_id false -> "undefined"
+      int s = -1, t = -1;
+      if (e.ntok >= 2) {
+        const int a0 = e.t1s, b0 = e.t1e;
+        for (int k = a0; k < b0; ++k) if (p[k] == '=') { s = k + 1; break; }
+        if (s >= 0) { t = b0; for (int k = s; k < b0; ++k) if (p[k] == '=') { t = k; break; } }
+      }
+      f.h_item = s >= 0 ? hash_bytes(p + s, (size_t)(t - s)) : hash_bytes("undefined", 9);
+      return 1;
+    }
+    if (m & PM_SOAP_OUT) return 0;
+    if (m & (PM_SOAP_ACCT | PM_SOAP_VALUE)) {
+      if (!(m & PM_SOAP_ACCT) && (m & PM_SOAP_KEY)) return 0;  // KEY branch wins
+      int fs, fe;
+      angle_field2(p, (int)e.len, fs, fe);
+      if (fs >= 0) {
+        while (fs < fe && (p[fs] == ' ' || (p[fs] >= 9 && p[fs] <= 13))) ++fs;
+        while (fe > fs && (p[fe - 1] == ' ' || (p[fe - 1] >= 9 && p[fe - 1] <= 13))) --fe;
+        if (all_digits(p + fs, fe - fs)) {
+          double v;
+          if (!simple_parse_int(p + fs, fe - fs, v)) return -1;
+          f.el = v;
+          f.flags = PRE_SOAP_VALID;
+        }
+      }
+      return 1;
+    }
+  }
+  return 0;
+}
+
 enum : uint8_t { SEL_HOST = 1, SEL_MH = 2, SEL_WALK = 4 };
 
 // Per-event selection counts packed into one u64 for the exclusive scan (a 16-byte struct scan
@@ -390,8 +448,11 @@ __global__ void k_host_flags(const Event* __restrict__ ev, const uint32_t* __res
         if (!host) aud[i] = f;
       }
       if (host) fl |= SEL_HOST;
-    } else if (needs_host(e, bytes)) {
-      fl |= SEL_HOST;
+    } else {
+      AudF f;
+      const int r = pre_fields(e, bytes, f);
+      if (r < 0) fl |= SEL_HOST;
+      else if (r > 0) aud[i] = f;  // read by k_build_ops
     }
     if (e.kind == LK_APP) {
       if (e.mask & PM_AUTR_MAP) fl |= SEL_MH;
@@ -513,15 +574,12 @@ __global__ void k_build_ops(DJArgs a) {
       else op.flags = 0;  // parseEntry returns before naming the service
     } else {
       op.num = (e.kind == LK_EJB_EXIT || e.tBs != 0xffff) ? e.num : apm_nan();
-      if (e.kind == LK_CT_EXIT && (e.mask & PM_BAF)) {
-        int n = 9;  // fewer than 4 tokens: the account string is "undefined" (NaN, not digits)
-        bool digits = false;
-        double v = apm_nan();
-        if (e.ntok >= 4) baf_account_scan(p, e.t3s, e.t3e, n, digits, v);  // (needs_host: it succeeds)
-        if (n > 0) {
+      if (e.kind == LK_CT_EXIT && (e.mask & PM_BAF)) {  // account scanned by k_host_flags (pre_fields)
+        const AudF& f = a.aud[i];
+        if (f.flags & PRE_BAF) {
           op.flags |= JF_BAF;
-          op.aux = v;
-          if (digits) { op.flags |= JF_BAF_VALID; op.aux2 = v; }
+          op.aux = f.el;
+          if (f.flags & PRE_BAF_VALID) { op.flags |= JF_BAF_VALID; op.aux2 = f.el; }
         }
       }
       if (empty_lid) op.op = JOP_DIRECT;
@@ -529,16 +587,10 @@ __global__ void k_build_ops(DJArgs a) {
     }
   } else if (e.kind == LK_SOAP) {
     const uint32_t m = e.mask;
+    // (the logId hash / the account number come from k_host_flags' pre_fields)
     if (m & PM_SOAP_IN) {
       code = SC_IN;
-      // ws[1].split('=')[1]; no '=' -> has_log_id false -> "undefined"
-      int s = -1, t = -1;
-      if (e.ntok >= 2) {
-        const int a0 = e.t1s, b0 = e.t1e;
-        for (int k = a0; k < b0; ++k) if (p[k] == '=') { s = k + 1; break; }
-        if (s >= 0) { t = b0; for (int k = s; k < b0; ++k) if (p[k] == '=') { t = k; break; } }
-      }
-      shash = s >= 0 ? hash_bytes(p + s, (size_t)(t - s)) : hash_bytes("undefined", 9);
+      shash = a.aud[i].h_item;
     } else if (m & PM_SOAP_OUT) {
       code = SC_OUT;
     } else if (m & (PM_SOAP_ACCT | PM_SOAP_KEY | PM_SOAP_VALUE)) {
@@ -546,15 +598,11 @@ __global__ void k_build_ops(DJArgs a) {
       if (!acct && (m & PM_SOAP_KEY)) {
         code = SC_KEY;
       } else {
-        int fs, fe;
-        angle_field2(p, (int)e.len, fs, fe);
-        bool valid = false;
-        if (fs >= 0) {
-          while (fs < fe && (p[fs] == ' ' || (p[fs] >= 9 && p[fs] <= 13))) ++fs;
-          while (fe > fs && (p[fe - 1] == ' ' || (p[fe - 1] >= 9 && p[fe - 1] <= 13))) --fe;
-          valid = all_digits(p + fs, fe - fs) && simple_parse_int(p + fs, fe - fs, snum);
+        const AudF& f = a.aud[i];
+        if (f.flags & PRE_SOAP_VALID) {
+          snum = f.el;
+          code = acct ? SC_ACCT : SC_VALUE;
         }
-        if (valid) code = acct ? SC_ACCT : SC_VALUE;
       }
     }
   }
