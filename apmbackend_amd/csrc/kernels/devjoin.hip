@@ -1623,17 +1623,56 @@ __device__ __forceinline__ void tx_line(const DJFormatArgs& f, const TxDev& t, c
   o.c('\n');
 }
 
-// The lines of consecutive tx are adjacent in the ring and in the tx / db text, so each lane
-// writes whole dwords (textout.h) instead of one byte store per character.
-__global__ void k_write(DJFormatArgs f) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= f.n_out) return;
-  const TxDev t = f.out[i];
-  if (t.raw < 0) return;
+// The lines of consecutive tx are adjacent in the ring (and in the tx / db text).  One 64-lane
+// block per 64 consecutive tx: each lane formats its ring line into an LDS stage at the line's
+// offset modulo 4 (dword stores, textout.h), then the wave copies the block's byte range out one
+// dword per lane per store -- 256 contiguous bytes per store instruction instead of 64 lanes
+// storing into 64 lines ~95 B apart.  A block whose lines do not fit the stage (logIds of kB)
+// writes its lines to the ring directly.  (The batch's ring region never wraps: ring_reserve.)
+constexpr int TXW_LINES = 64;
+constexpr uint32_t TXW_LDS = 8192;
+__device__ __forceinline__ void write_one(const DJFormatArgs& f, const TxDev& t, uint32_t i, char* staged_line);
+
+__device__ __forceinline__ void txw_copy_out(const char* __restrict__ lds, char* __restrict__ out, uint32_t g0,
+                                             uint32_t g1) {
+  const uint32_t a0 = g0 & ~3u;
+  const uint32_t nd = (g1 - a0 + 3) / 4;
+  for (uint32_t d = threadIdx.x; d < nd; d += TXW_LINES) {
+    const uint32_t ga = a0 + 4 * d;
+    if (ga >= g0 && ga + 4 <= g1) {
+      *reinterpret_cast<uint32_t*>(out + ga) = *reinterpret_cast<const uint32_t*>(lds + 4 * d);
+    } else {  // the block's first / last dword is shared with a neighbouring block: byte stores
+      for (uint32_t b = 0; b < 4; ++b)
+        if (ga + b >= g0 && ga + b < g1) out[ga + b] = lds[4 * d + b];
+    }
+  }
+}
+
+__global__ __launch_bounds__(TXW_LINES) void k_write(DJFormatArgs f) {
+  __shared__ __align__(16) char stage[TXW_LDS];
+  const uint32_t j0 = blockIdx.x * TXW_LINES;
+  const uint32_t j1 = min(f.n_out, j0 + TXW_LINES);
+  const uint32_t i = j0 + threadIdx.x;
+  const U4* offs = reinterpret_cast<const U4*>(f.offs);
+  // physical ring offsets of the block's byte range (contiguous: the region does not wrap)
+  const uint64_t rb = f.ring_base & (f.ring_cap - 1);
+  const uint32_t p0 = (uint32_t)(rb + offs[j0].x), p1 = (uint32_t)(rb + offs[j1].x);
+  const bool staged = p1 - (p0 & ~3u) <= TXW_LDS;  // uniform across the block
+  if (i < j1) {
+    const TxDev t = f.out[i];
+    if (t.raw >= 0) write_one(f, t, i, staged ? stage + ((uint32_t)(rb + offs[i].x) - (p0 & ~3u)) : nullptr);
+  }
+  if (staged) {
+    __syncthreads();
+    txw_copy_out(stage, f.ring, p0, p1);
+  }
+}
+
+__device__ __forceinline__ void write_one(const DJFormatArgs& f, const TxDev& t, uint32_t i, char* staged_line) {
   const U4 o = reinterpret_cast<const U4*>(f.offs)[i];
   const U4 l = reinterpret_cast<const U4*>(f.lens)[i];
   const uint64_t vpos = f.ring_base + o.x;
-  char* p0 = f.ring + (vpos & (f.ring_cap - 1));
+  char* p0 = staged_line ? staged_line : f.ring + (vpos & (f.ring_cap - 1));
   const RawSvc rs = f.raw[t.raw];
   bool inexact = false;
   {
@@ -2205,7 +2244,7 @@ int apm_dj_plan(DJFormatArgs* f, hipStream_t s) {
 
 int apm_dj_write(DJFormatArgs* f, uint32_t n_stats, hipStream_t s) {
   const uint32_t n = f->n_out;
-  if (n) hipLaunchKernelGGL(k_write, dim3((n + TB - 1) / TB), dim3(TB), 0, s, *f);
+  if (n) hipLaunchKernelGGL(k_write, dim3((n + TXW_LINES - 1) / TXW_LINES), dim3(TXW_LINES), 0, s, *f);
   if (!n_stats) return 0;
   size_t need = 0;
   HIP_OK(rocprim::inclusive_scan(nullptr, need, f->tx_bucket, f->tx_bmax, (size_t)n_stats,
