@@ -69,8 +69,9 @@ __global__ __launch_bounds__(NL_BLOCK) void k_nl_count(const uint8_t* __restrict
 // Writes the byte position of every '\n' (= line end) in order; tile_off = exclusive scan.
 __global__ __launch_bounds__(NL_BLOCK) void k_nl_write(const uint8_t* __restrict__ bytes, uint64_t n,
                                                       const uint32_t* __restrict__ tile_off,
-                                                      uint32_t* __restrict__ line_end) {
+                                                      uint32_t* __restrict__ line_end, uint32_t* __restrict__ n_lines) {
   const uint64_t base = (uint64_t)blockIdx.x * NL_TILE + threadIdx.x * 16;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *n_lines = tile_off[gridDim.x];  // (folded D2D copy)
   uint8_t b[16];
   int c = 0;
   if (base + 16 <= n) {
@@ -1180,8 +1181,8 @@ int apm_parse_batch(const uint8_t* d_bytes, uint64_t n_bytes, const uint32_t* d_
   if (tmp_bytes > APM_SCAN_TMP) return -1;
   HIP_OK(rocprim::exclusive_scan(scan_tmp, tmp_bytes, tile_counts, tile_off, 0u, tiles + 1,
                                  rocprim::plus<uint32_t>(), stream));
-  hipLaunchKernelGGL(k_nl_write, dim3(tiles), dim3(NL_BLOCK), 0, stream, d_bytes, n_bytes, tile_off, line_end);
-  HIP_OK(hipMemcpyAsync(d_n_lines, tile_off + tiles, 4, hipMemcpyDeviceToDevice, stream));
+  hipLaunchKernelGGL(k_nl_write, dim3(tiles), dim3(NL_BLOCK), 0, stream, d_bytes, n_bytes, tile_off, line_end,
+                     d_n_lines);
 
   ParseArgs pa;
   pa.bytes = d_bytes;
