@@ -152,6 +152,8 @@ def main():
 
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if local_world == world:  # one node: gloo over loopback (the hostname may not resolve)
+            os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
         dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=600))
     torch.cuda.set_device(device)
 
