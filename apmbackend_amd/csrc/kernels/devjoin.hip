@@ -998,7 +998,10 @@ __global__ void k_aud_walk(DJArgs a) {
 }
 
 // ------------------------------------------------------------------------ tables
-__device__ uint32_t key_claim(KeyState* __restrict__ t, uint32_t mask, uint64_t k, JoinCounts* cnt) {
+// (`fresh`: set when this call created the key; the caller counts new keys once per wave -- a
+// per-lane atomicAdd on the one n_keys_new word put ~every logId of the batch through a single
+// L2 atomic unit)
+__device__ uint32_t key_claim(KeyState* __restrict__ t, uint32_t mask, uint64_t k, JoinCounts* cnt, bool& fresh) {
   uint32_t h = home_of(k, mask);
   for (uint32_t probe = 0; probe <= mask; ++probe) {
     const uint32_t idx = (h + probe) & mask;
@@ -1014,7 +1017,7 @@ __device__ uint32_t key_claim(KeyState* __restrict__ t, uint32_t mask, uint64_t 
         s.need = -1;
         s.n_part = 0;
         s.pblk = 0;
-        atomicAdd(&cnt->n_keys_new, 1u);
+        fresh = true;
         return idx;
       }
       if (prev == k) return idx;
@@ -1041,10 +1044,16 @@ __global__ void k_claim(DJArgs a) {
   const JOp& op = a.ops[i];
   const uint32_t cap = a.table_mask + 1;
   uint32_t key = cap + 1;  // no op
+  bool fresh = false;
   if (op.op == JOP_DIRECT) key = cap;
   else if (op.op != JOP_NONE) {
-    const uint32_t s = key_claim(a.table, a.table_mask, op.gkey, a.counts);
+    const uint32_t s = key_claim(a.table, a.table_mask, op.gkey, a.counts, fresh);
     key = s == 0xffffffffu ? cap + 1 : s;
+  }
+  {  // new keys: one atomic per wave
+    const uint64_t b = __ballot(fresh);
+    const uint32_t lead = (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1u;
+    if (b && (threadIdx.x & (APM_WAVE - 1)) == lead) atomicAdd(&a.counts->n_keys_new, (uint32_t)__popcll(b));
   }
   a.op_slot[i] = key;
   a.op_idx[i] = i;
