@@ -14,7 +14,7 @@ from apmbackend_amd.build_native import csrc_hash
 import sys
 sys.exit(0 if _native.load(build_if_missing=False).csrc_hash() == csrc_hash() else 1)" 2>/dev/null)
 }
-for attempt in 1 2 3 4 5 6 7 8 9 10 11 12; do
+for attempt in $(seq 1 ${ATTEMPTS:-40}); do
   while ! fresh; do echo "[attempt $attempt] .so stale (rebuild pending): waiting" >> "$log.attempts"; sleep 30; done
   (cd "$REPO" && /usr/local/graft/bin/gpurun --timeout "$to" -- "$cmd") > "$log" 2>&1
   rc=$?
