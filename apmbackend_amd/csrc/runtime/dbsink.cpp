@@ -487,6 +487,38 @@ class DbSink : public ByteSink {
     for (int p = 0; p < P; ++p) r0[p + 1] = r0[p] + (int64_t)ends[p].size();
     const int64_t total = r0[P];
     if (total == 0) return 0;
+    // the blob offset where each cut (a row count from the blob start) ends
+    int pi = 0;
+    auto end_of = [&](int64_t c) {
+      while (c > r0[pi + 1]) ++pi;
+      return b[pi] + ends[pi][(size_t)(c - r0[pi] - 1)];
+    };
+    return cut_and_submit(type, d, total, end_of, hold, now, P);
+  }
+
+  // Rows whose boundaries the producer already knows (the engine's fs COPY rows: K12's exclusive
+  // scan of the row lengths): row r is [row_off[r], row_off[r + 1]) of the blob, empty rows are
+  // skipped.  No scan of the text -- the flushes are exactly those of consume_encoded.
+  int64_t consume_encoded_rows(int type, std::string_view blob, const uint32_t* row_off, size_t nrows,
+                               std::shared_ptr<const void> hold = nullptr) {
+    if (blob.size() >= (1ull << 32) || nrows == 0 || row_off[nrows] != blob.size() || row_off[0] != 0)
+      return consume_encoded(type, blob, std::move(hold));
+    const double now = mono_ms();
+    std::vector<uint32_t> ends;
+    ends.reserve(nrows);
+    for (size_t r = 0; r < nrows; ++r)
+      if (row_off[r + 1] > row_off[r]) ends.push_back(row_off[r + 1]);
+    const int64_t total = (int64_t)ends.size();
+    if (total == 0) return 0;
+    auto end_of = [&](int64_t c) { return (size_t)ends[(size_t)c - 1]; };
+    return cut_and_submit(type, blob.data(), total, end_of, hold, now,
+                          (int)std::max<size_t>(2, std::min<size_t>(8, blob.size() >> 20)));
+  }
+
+  // `total` rows starting at d; end_of(c) = blob offset where the first c rows end (c ascending).
+  template <class EndOf>
+  int64_t cut_and_submit(int type, const char* d, int64_t total, EndOf& end_of,
+                         const std::shared_ptr<const void>& hold, double now, int P) {
     std::lock_guard<std::mutex> lk(mu_);
     encoded_[type] = true;
     // a full buffer is flushed before anything is added (as append_run_locked does); then the
@@ -500,13 +532,7 @@ class DbSink : public ByteSink {
       if (c == total) break;
     }
     std::vector<size_t> off(cut.size());
-    {
-      int p = 0;
-      for (size_t k = 0; k < cut.size(); ++k) {
-        while (cut[k] > r0[p + 1]) ++p;
-        off[k] = b[p] + ends[p][(size_t)(cut[k] - r0[p] - 1)];
-      }
-    }
+    for (size_t k = 0; k < cut.size(); ++k) off[k] = end_of(cut[k]);
     // flushes: [buffer + A0], A1, ..., A(m-1); Am stays buffered
     const size_t m = cut.size() - 1;
     append_run_locked(type, d, off[0], cut[0], now);
@@ -889,6 +915,11 @@ struct SinkRoute : ByteSink {
     if (type >= 0) sink->consume_encoded(type, std::string_view(p, n), std::move(hold));
     else sink->write_bytes(kind, p, n);
   }
+  void write_rows_held(int kind, const char* p, size_t n, const uint32_t* row_off, size_t nrows,
+                       std::shared_ptr<const void> hold) override {
+    if (type >= 0) sink->consume_encoded_rows(type, std::string_view(p, n), row_off, nrows, std::move(hold));
+    else sink->write_bytes(kind, p, n);
+  }
 };
 
 }  // namespace apm
@@ -935,6 +966,12 @@ void register_dbsink(py::module_& m) {
         std::string_view v = b;
         py::gil_scoped_release rel;
         return s.consume_encoded(type, v);
+      })
+      .def("consume_encoded_rows", [](DbSink& s, int type, py::bytes b, std::vector<uint32_t> off) {
+        std::string_view v = b;
+        if (off.empty()) throw std::invalid_argument("row offsets: nrows + 1 entries");
+        py::gil_scoped_release rel;
+        return s.consume_encoded_rows(type, v, off.data(), off.size() - 1);
       })
       .def("consume_encoded_ptr", [](DbSink& s, int type, uintptr_t p, size_t n) {
         py::gil_scoped_release rel;  // rows in caller-owned (e.g. pinned) memory

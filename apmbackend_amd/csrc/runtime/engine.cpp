@@ -519,6 +519,7 @@ Engine::~Engine() {
       if (!hs.cv.wait_for(lk, std::chrono::seconds(60), [&] { return hs.n[k] == 0; })) continue;
     }
     if (h_fmt_out_[k]) hipHostFree(h_fmt_out_[k]);
+    if (h_fs_off_[k]) hipHostFree(h_fs_off_[k]);
     hipEventDestroy(ev_rel_[k]);
     hipEventDestroy(ev_fmt_[k]);
   }
@@ -2556,7 +2557,7 @@ void Engine::emit_bytes(int kind, const char* p, size_t n) {
   blob_[kind].append(p, n);
 }
 
-void Engine::emit_bytes_held(int kind, const char* p, size_t n, int k) {
+void Engine::emit_bytes_held(int kind, const char* p, size_t n, int k, const uint32_t* row_off, size_t nrows) {
   if (!n) return;
   if (!byte_sink_[kind]) { emit_bytes(kind, p, n); return; }
   drain_kind(kind);
@@ -2572,7 +2573,8 @@ void Engine::emit_bytes_held(int kind, const char* p, size_t n, int k) {
     }
     hs->cv.notify_all();
   });
-  byte_sink_[kind]->write_bytes_held(kind, p, n, std::move(hold));
+  if (row_off) byte_sink_[kind]->write_rows_held(kind, p, n, row_off, nrows, std::move(hold));
+  else byte_sink_[kind]->write_bytes_held(kind, p, n, std::move(hold));
   sink_bytes_[kind] += n;
 }
 
@@ -2651,6 +2653,18 @@ void Engine::format_rollover_text(int64_t edge_ts) {
     ex.add(fa.fs_off + (size_t)n * cfg_.n_lags, hd_fmt_meta_ + 4 * k + 1, 4);
     apm_export(&ex, stream_);
   }
+  fs_rows_[k] = 0;
+  if (fa.want_fs && byte_sink_[OUT_FS]) {
+    // the row offsets for the sink's flush cuts (slot k's lane is done with the previous ones)
+    const size_t rows = (size_t)n * cfg_.n_lags;
+    if (rows + 1 > h_fs_off_cap_[k]) {
+      if (h_fs_off_[k]) HIP_OK(hipHostFree(h_fs_off_[k]));
+      h_fs_off_cap_[k] = (rows + 1) * 5 / 4;
+      HIP_OK(hipHostMalloc((void**)&h_fs_off_[k], h_fs_off_cap_[k] * 4, hipHostMallocDefault));
+    }
+    d2h(h_fs_off_[k], fa.fs_off, (rows + 1) * 4, stream_);
+    fs_rows_[k] = rows;
+  }
   HIP_OK(hipEventRecord(ev_fmt_[k], stream_));
   trace_event("fmt.plan", tf0, now_ms(), 1);
   char* dst = d_fmt_out_[k];
@@ -2665,7 +2679,7 @@ void Engine::format_rollover_text(int64_t edge_ts) {
       }
       const double tl1 = now_ms();
       emit_bytes(OUT_ST, h_fmt_out_[k], st_total);
-      emit_bytes_held(OUT_FS, h_fmt_out_[k] + st_cap, fs_total, k);
+      emit_bytes_held(OUT_FS, h_fmt_out_[k] + st_cap, fs_total, k, fs_rows_[k] ? h_fs_off_[k] : nullptr, fs_rows_[k]);
       trace_event("lane st/fs wait (direct)", tl0, tl1, 4);
       trace_event("lane st/fs emit", tl1, now_ms(), 4);
     });
@@ -2691,7 +2705,7 @@ void Engine::format_rollover_text(int64_t edge_ts) {
     }
     const double tl1 = now_ms();
     emit_bytes(OUT_ST, h, st_total);
-    emit_bytes_held(OUT_FS, h + st_total, fs_total, k);
+    emit_bytes_held(OUT_FS, h + st_total, fs_total, k, fs_rows_[k] ? h_fs_off_[k] : nullptr, fs_rows_[k]);
     trace_event("lane st/fs D2H", tl0, tl1, 4);
     trace_event("lane st/fs emit", tl1, now_ms(), 4);
   });

@@ -167,6 +167,14 @@ struct ByteSink {
     (void)hold;
     write_bytes(kind, p, n);
   }
+  // Same, with the row boundaries known: row r is [row_off[r], row_off[r + 1]) (nrows + 1
+  // entries, row_off[nrows] == n; empty rows allowed).  row_off is only read during the call.
+  virtual void write_rows_held(int kind, const char* p, size_t n, const uint32_t* row_off, size_t nrows,
+                               std::shared_ptr<const void> hold) {
+    (void)row_off;
+    (void)nrows;
+    write_bytes_held(kind, p, n, std::move(hold));
+  }
 };
 
 struct CheckpointInfo {
@@ -461,7 +469,8 @@ class Engine {
   void dfree(void* p);
   void emit_bytes(int kind, const char* p, size_t n);
   // staging buffer k (st/fs 0, 1; fb 2, 3) is referenced by the sink until its holds are released
-  void emit_bytes_held(int kind, const char* p, size_t n, int k);
+  void emit_bytes_held(int kind, const char* p, size_t n, int k, const uint32_t* row_off = nullptr,
+                       size_t nrows = 0);
   void wait_fmt_holds(int k);
   struct FmtHolds {  // shared with the holds: a release after the engine is gone stays safe
     std::mutex mu;
@@ -1042,6 +1051,11 @@ class Engine {
   uint64_t fmt_task_[2] = {0, 0};
   int fmt_k_ = 0;
   uint32_t* h_fmt_meta_ = nullptr;               // pinned: per slot k, [4k] st total, [4k+1] fs total
+  // pinned: per slot k, the fs row offsets of the last format (K12's scan), so a COPY sink cuts
+  // its flushes without scanning the text
+  uint32_t* h_fs_off_[2] = {nullptr, nullptr};
+  size_t h_fs_off_cap_[2] = {0, 0};
+  size_t fs_rows_[2] = {0, 0};
   uint32_t* hd_fmt_meta_ = nullptr;
 
   // text outputs

@@ -328,6 +328,43 @@ def test_native_sink_parallel_cut_equals_serial(tmp_path, limit, pre):
     assert results[0][1] == (len(rows) - results[0][2])
 
 
+@pytest.mark.skipif(not _native_ok(), reason="native extension not built")
+@pytest.mark.parametrize("limit,pre,size", [(1000, 0, 50000), (1000, 437, 50000), (7, 3, 3000), (1000, 10, 300)])
+def test_native_sink_row_offset_cut_equals_scan(tmp_path, limit, pre, size):
+    """The engine hands its fs COPY rows with K12's row offsets (write_rows_held): the sink cuts
+    its flushes from the offsets (empty rows skipped) instead of scanning the text.  Flushes,
+    rows and bytes must equal the scanning path's, small and large blobs alike."""
+    import random
+    from apmbackend_amd import _native
+    N = _native.load(build_if_missing=False)
+    rng = random.Random(limit + pre + size)
+    rows = [("r%07d\t" % i) + "x" * rng.randint(5, 400) + "\n" for i in range(size)]
+    head, body = "".join(rows[:pre]), "".join(rows[pre:])
+    off = [0]
+    for r in rows[pre:]:
+        while rng.random() < 0.2:  # inactive (series, LAG) cells: zero-length rows
+            off.append(off[-1])
+        off.append(off[-1] + len(r))
+    results = []
+    for mode in ("scan", "offsets"):
+        d = tmp_path / mode
+        s = N.DbSink(limit, 1e9, ["t_tx", "t_fs", "t_al", "t_jx", "t_fb"], ["a", "b", "c", "d", "e"], "spool",
+                     [str(d)], 1 << 62, 2)
+        if head:
+            s.consume_encoded(1, head.encode())
+        if mode == "scan":
+            assert s.consume_encoded(1, body.encode()) == len(rows) - pre
+        else:
+            assert s.consume_encoded_rows(1, body.encode(), off) == len(rows) - pre
+        s.drain()
+        st = s.stats()
+        s.flush_all()
+        s.drain()
+        results.append((st["flushes"], st["rows"], st["buffered"], open(d / "t_fs.copy").read()))
+    assert results[0] == results[1]
+    assert results[0][3] == head + body
+
+
 @pytest.mark.parametrize("lanes", [2, 4])
 def test_native_sink_writer_lanes_write_every_row_once_in_lane_order(tmp_path, lanes):
     """Writer lanes (dbsink.cpp): flushes go round-robin (blocks of 16) to `lanes` independent
