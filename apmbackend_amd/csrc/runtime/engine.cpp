@@ -529,7 +529,15 @@ Engine::~Engine() {
   if (dj_) {
     hipStreamSynchronize(out_stream_);
     hipHostFree(h_ring_min_); hipHostFree(h_rel_n_); hipHostFree(h_rel_total_); hipHostFree(h_unseen_flag_);
-    for (int k = 0; k < 2; ++k) if (h_rel_text_[k]) hipHostFree(h_rel_text_[k]);
+    for (int k = 0; k < 2; ++k) {
+      {  // zero-copy db rows still referenced by the sink (bounded wait, as for st/fs)
+        FmtHolds& hs = *fmt_holds_;
+        std::unique_lock<std::mutex> lk(hs.mu);
+        if (!hs.cv.wait_for(lk, std::chrono::seconds(60), [&] { return hs.n[4 + k] == 0; })) continue;
+      }
+      if (h_rel_text_[k]) hipHostFree(h_rel_text_[k]);
+      if (h_rel_offs_[k]) hipHostFree(h_rel_offs_[k]);
+    }
 
     dj_.reset();
   }
@@ -2213,9 +2221,21 @@ void Engine::release_device_finish() {
     if (total + 64 > rel_text_cap_[k]) d_rel_text_[k] = (char*)regrow(d_rel_text_[k], rel_text_cap_[k], total + 64);
     apm_dj_gather_copy(d_pool_gid_[pool_cur_], released, dj_->ring(), dj_->ring_cap(), d_rel_offs_, d_rel_text_[k], total,
                        stream_);
+    // a COPY sink cuts its flushes from the row offsets (d_rel_offs_ is rewritten by the next
+    // release: copied here, in stream order)
+    const bool rows = byte_sink_[OUT_DB] != nullptr;
+    if (rows) {
+      if ((size_t)released + 1 > h_rel_offs_cap_[k]) {
+        if (h_rel_offs_[k]) HIP_OK(hipHostFree(h_rel_offs_[k]));
+        h_rel_offs_cap_[k] = ((size_t)released + 1) * 2;
+        HIP_OK(hipHostMalloc((void**)&h_rel_offs_[k], h_rel_offs_cap_[k] * 4, hipHostMallocDefault));
+      }
+      d2h(h_rel_offs_[k], d_rel_offs_, ((size_t)released + 1) * 4, stream_);
+    }
     HIP_OK(hipEventRecord(ev_rel_[k], stream_));
-    rel_task_[k] = post_out([this, k, total]() {
+    rel_task_[k] = post_out([this, k, total, rows, released]() {
       HIP_OK(hipEventSynchronize(ev_rel_[k]));
+      wait_fmt_holds(4 + k);  // the sink still writes from this buffer (zero-copy COPY rows)
       if (total > h_rel_text_cap_[k]) {
         if (h_rel_text_[k]) HIP_OK(hipHostFree(h_rel_text_[k]));
         h_rel_text_cap_[k] = total * 2 + (4 << 20);  // (a pinned allocation costs ms: 2x headroom)
@@ -2225,7 +2245,8 @@ void Engine::release_device_finish() {
       HIP_OK(hipMemcpyAsync(h_rel_text_[k], d_rel_text_[k], total, hipMemcpyDeviceToHost, out_stream_));
       HIP_OK(hipStreamSynchronize(out_stream_));
       const double tl1 = now_ms();
-      emit_bytes(OUT_DB, h_rel_text_[k], total);
+      if (rows) emit_bytes_held(OUT_DB, h_rel_text_[k], total, 4 + k, h_rel_offs_[k], (size_t)released);
+      else emit_bytes(OUT_DB, h_rel_text_[k], total);
       trace_event("lane db D2H", tl0, tl1, 4);
       trace_event("lane db emit", tl1, now_ms(), 4);
     });

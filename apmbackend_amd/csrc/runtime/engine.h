@@ -475,7 +475,7 @@ class Engine {
   struct FmtHolds {  // shared with the holds: a release after the engine is gone stays safe
     std::mutex mu;
     std::condition_variable cv;
-    int n[4] = {0, 0, 0, 0};  // st/fs staging 0, 1; fb staging 2, 3
+    int n[6] = {0, 0, 0, 0, 0, 0};  // st/fs staging 0, 1; fb staging 2, 3; released db text 4, 5
   };
   std::shared_ptr<FmtHolds> fmt_holds_ = std::make_shared<FmtHolds>();
   void upload_series_tables(int32_t lo);
@@ -735,6 +735,8 @@ class Engine {
   size_t rel_text_cap_[2] = {0, 0};
   char* h_rel_text_[2] = {nullptr, nullptr};
   size_t h_rel_text_cap_[2] = {0, 0};
+  uint32_t* h_rel_offs_[2] = {nullptr, nullptr};  // pinned: the released rows' offsets (sink flush cuts)
+  size_t h_rel_offs_cap_[2] = {0, 0};
   hipStream_t out_stream_ = nullptr;
   std::vector<int32_t> h_raw_series_;          // stats thread mirror of the raw -> series table
   // pinned staging of the stats thread's H2D uploads: kStage buffers used in rotation, each
