@@ -664,11 +664,17 @@ __device__ __forceinline__ uint32_t wave_fscan(uint32_t f, int lane) {
 
 // (also the folded fills of the join's counters and per-event output counts: the grid covers
 // max(n_chunks, n_ev) + 1 lanes, and it runs before any kernel that touches them)
+// (also the batch's zero fills of the join stream: the JoinCounts prefix, out_cnt, the audit
+// carry of the next generation and the per-file first-chunk marks -- one launch, no memsets)
 __global__ void k_chunk_events(const Event* __restrict__ ev, uint32_t n_ev, uint32_t n_chunks, uint32_t* __restrict__ lo,
-                               uint32_t* __restrict__ zero_words, uint32_t n_zero_words, uint32_t* __restrict__ out_cnt) {
+                               uint32_t* __restrict__ zero_words, uint32_t n_zero_words, uint32_t* __restrict__ out_cnt,
+                               uint32_t* __restrict__ carry_words, uint32_t n_carry_words,
+                               uint32_t* __restrict__ first_chunk, uint32_t n_files) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c < n_zero_words) zero_words[c] = 0;
   if (c <= n_ev) out_cnt[c] = 0;
+  if (c < n_carry_words) carry_words[c] = 0;
+  if (c < n_files) first_chunk[c] = 0xffffffffu;
   if (c > n_chunks) return;
   uint32_t l = 0, h = n_ev;
   while (l < h) {
@@ -2117,8 +2123,9 @@ int apm_dj_select_host(DJArgs* a, const uint32_t* d_n_ev, uint32_t max_ev, hipSt
 }
 
 // K5: map / header matching, then the block walks (their stopTime ops land in a->ops)
-static int apm_dj_audit(DJArgs* a, hipStream_t s) {
-  if (a->n_files) HIP_OK(hipMemsetAsync(a->gout.carry, 0, (size_t)a->n_files * sizeof(AudCarry), s));
+static int apm_dj_audit(DJArgs* a, bool filled, hipStream_t s) {
+  // (filled: k_chunk_events already zeroed the carry and the first-chunk marks)
+  if (a->n_files && !filled) HIP_OK(hipMemsetAsync(a->gout.carry, 0, (size_t)a->n_files * sizeof(AudCarry), s));
   const uint32_t N = a->gin.n_autr + a->n_mh;
   if (N) {
     hipLaunchKernelGGL(k_aud_keys, dim3((N + TB - 1) / TB), dim3(TB), 0, s, *a);
@@ -2135,7 +2142,7 @@ static int apm_dj_audit(DJArgs* a, hipStream_t s) {
   }
   // an open block always carries its (non-empty) logId: no carry text, no carried block
   if (a->n_walk || a->gin.n_txt) {
-    if (a->n_files) HIP_OK(hipMemsetAsync(a->file_first_chunk, 0xff, (size_t)a->n_files * 4, s));
+    if (a->n_files && !filled) HIP_OK(hipMemsetAsync(a->file_first_chunk, 0xff, (size_t)a->n_files * 4, s));
     hipLaunchKernelGGL(k_aud_chunks, dim3((a->n_chunks + 1 + TB - 1) / TB), dim3(TB), 0, s, *a);
     dj_check(s, "k_aud_chunks");
     const uint32_t L = a->n_walk + a->n_files;
@@ -2151,9 +2158,12 @@ int apm_dj_join(DJArgs* a, hipStream_t s) {
   static_assert(offsetof(JoinCounts, ejb_unmatched) % 4 == 0, "JoinCounts zero range");
   const uint32_t zw = (uint32_t)(offsetof(JoinCounts, ejb_unmatched) / 4);
   if (n) {
-    const uint32_t lanes = std::max(std::max(a->n_chunks + 1, n + 1), zw);
+    static_assert(sizeof(AudCarry) % 4 == 0, "carry words");
+    const uint32_t cw = a->n_files * (uint32_t)(sizeof(AudCarry) / 4);
+    const uint32_t lanes = std::max(std::max(std::max(a->n_chunks + 1, n + 1), zw), cw);
     hipLaunchKernelGGL(k_chunk_events, dim3((lanes + TB - 1) / TB), dim3(TB), 0, s, a->ev, n, a->n_chunks,
-                       a->chunk_ev_lo, (uint32_t*)a->counts, zw, a->out_cnt);
+                       a->chunk_ev_lo, (uint32_t*)a->counts, zw, a->out_cnt, (uint32_t*)a->gout.carry, cw,
+                       (uint32_t*)a->file_first_chunk, a->n_files);
     dj_check(s, "k_chunk_events");
     hipLaunchKernelGGL(k_build_ops, dim3((n + TB - 1) / TB), dim3(TB), 0, s, *a);
     dj_check(s, "k_build_ops");
@@ -2161,7 +2171,7 @@ int apm_dj_join(DJArgs* a, hipStream_t s) {
     HIP_OK(hipMemsetAsync(a->counts, 0, offsetof(JoinCounts, ejb_unmatched), s));
   }
   // (also for a batch without events: the carry moves to the next generation)
-  if (apm_dj_audit(a, s) != 0) return -1;
+  if (apm_dj_audit(a, n != 0, s) != 0) return -1;
   if (n) {
     hipLaunchKernelGGL(k_soap_summary, dim3(a->n_chunks, SOAP_SEGS), dim3(APM_WAVE), 0, s, *a);
     dj_check(s, "k_soap_summary");
