@@ -322,7 +322,7 @@ class DbSink : public ByteSink {
     size_t run_b = 0;
     int64_t run_n = 0;
     auto close_run = [&](size_t end) {
-      if (run_t >= 0 && run_n) append_run_locked(run_t, blob.data() + run_b, end - run_b, run_n, now);
+      if (run_t >= 0 && run_n) append_run_locked(run_t, blob.data() + run_b, end - run_b, run_n, now, false);
       run_t = -1;
       run_n = 0;
     };
@@ -358,6 +358,7 @@ class DbSink : public ByteSink {
     const double now = mono_ms();
     std::lock_guard<std::mutex> lk(mu_);
     encoded_[type] = true;
+    if (buf_[type].n > 0 && !buf_[type].enc) submit_locked(type);
     int64_t n = 0;
     size_t i = 0;
     while (i < blob.size()) {
@@ -370,7 +371,7 @@ class DbSink : public ByteSink {
         j = q ? (size_t)(q - blob.data()) + 1 : blob.size();
         ++k;
       }
-      append_run_locked(type, blob.data() + i, j - i, k, now);
+      append_run_locked(type, blob.data() + i, j - i, k, now, true);
       n += k;
       i = j;
     }
@@ -521,6 +522,7 @@ class DbSink : public ByteSink {
                          const std::shared_ptr<const void>& hold, double now, int P) {
     std::lock_guard<std::mutex> lk(mu_);
     encoded_[type] = true;
+    if (buf_[type].n > 0 && !buf_[type].enc) submit_locked(type);
     // a full buffer is flushed before anything is added (as append_run_locked does); then the
     // serial path's flushes hold `limit` consecutive rows each: A0 tops the buffer up to the
     // limit, every later flush is `limit` rows of the blob, the remainder stays buffered
@@ -535,7 +537,7 @@ class DbSink : public ByteSink {
     for (size_t k = 0; k < cut.size(); ++k) off[k] = end_of(cut[k]);
     // flushes: [buffer + A0], A1, ..., A(m-1); Am stays buffered
     const size_t m = cut.size() - 1;
-    append_run_locked(type, d, off[0], cut[0], now);
+    append_run_locked(type, d, off[0], cut[0], now, true);
     if (m == 0) return total;
     submit_locked(type);
     std::vector<std::shared_ptr<Job>> mid(m - 1);
@@ -566,7 +568,7 @@ class DbSink : public ByteSink {
       }
       cv_.notify_all();
     }
-    append_run_locked(type, d + off[m - 1], off[m] - off[m - 1], cut[m] - cut[m - 1], now);
+    append_run_locked(type, d + off[m - 1], off[m] - off[m - 1], cut[m] - cut[m - 1], now, true);
     return total;
   }
 
@@ -644,9 +646,10 @@ class DbSink : public ByteSink {
     return r;
   }
 
+  // the format of what type t's buffer holds (close() returns it as is)
   bool is_encoded(int t) {
     std::lock_guard<std::mutex> lk(mu_);
-    return encoded_[t];
+    return buf_[t].n > 0 ? buf_[t].enc : encoded_[t];
   }
 
   // ---- checkpoint support: an acknowledged-flush watermark instead of a drain.
@@ -705,6 +708,7 @@ class DbSink : public ByteSink {
     std::string lines;
     int64_t n = 0;
     double deadline = 0;
+    bool enc = false;  // lines are COPY rows (else wire lines, encoded at submit)
   };
   struct Job {
     int type = 0;
@@ -720,11 +724,13 @@ class DbSink : public ByteSink {
     std::string_view data() const { return ext.data() ? ext : std::string_view(encoded); }
   };
 
-  // Appends `nrows` complete lines of type t; the buffer is flushed first when it is full.
-  void append_run_locked(int t, const char* p, size_t len, int64_t nrows, double now) {
+  // Appends `nrows` complete lines of type t (COPY rows if enc, else wire lines); the buffer is
+  // flushed first when it is full or holds the other format (one table may get engine-encoded
+  // rows from one stream and wire lines from another: the db and audit_db streams).
+  void append_run_locked(int t, const char* p, size_t len, int64_t nrows, double now, bool enc) {
     Buf& b = buf_[t];
-    if (b.n >= limit_) submit_locked(t);
-    if (b.n == 0) b.deadline = now + max_wait_ms_;
+    if (b.n >= limit_ || (b.n > 0 && b.enc != enc)) submit_locked(t);
+    if (b.n == 0) { b.deadline = now + max_wait_ms_; b.enc = enc; }
     b.lines.append(p, len);
     if (len && p[len - 1] != '\n') b.lines += '\n';
     b.n += nrows;
@@ -737,7 +743,7 @@ class DbSink : public ByteSink {
     j->seq = next_seq_++;
     j->floor = std::min(j->seq, rebuf_floor_[t]);
     rebuf_floor_[t] = UINT64_MAX;
-    if (encoded_[t]) {  // COPY text already: straight to the writer
+    if (buf_[t].enc) {  // COPY text already: straight to the writer
       j->encoded.swap(buf_[t].lines);
       j->ready = true;
     } else {
@@ -838,18 +844,30 @@ class DbSink : public ByteSink {
             retry_from = ok + 1;
           }
           // back to the front of its buffer, in order (:310-320)
+          // (wire lines stay wire lines; if COPY rows are involved -- a flush that came in
+          // encoded, or a buffer holding them -- everything goes back as COPY rows: a written
+          // flush always has its COPY text)
           Buf& b = buf_[t];
+          bool as_copy = b.n > 0 && b.enc;
+          for (size_t i = retry_from; i < run.size(); ++i) as_copy |= run[i]->lines.empty();
           std::string back;
           int64_t n = 0;
           for (size_t i = retry_from; i < run.size(); ++i) {
-            if (encoded_[t]) back.append(run[i]->data());
+            if (as_copy) back.append(run[i]->data());
             else back += run[i]->lines;
             run[i]->hold.reset();
             n += run[i]->n;
             rebuf_floor_[t] = std::min(rebuf_floor_[t], run[i]->floor);
           }
           if (!back.empty()) {
+            if (as_copy && b.n > 0 && !b.enc) {  // the buffer's wire lines -> COPY rows
+              std::string out[NT];
+              int64_t counts[NT] = {0, 0, 0, 0, 0};
+              copyenc::encode_blob(b.lines, out, counts);
+              b.lines.swap(out[t]);
+            }
             if (b.n == 0) b.deadline = mono_ms() + max_wait_ms_;
+            b.enc = as_copy;
             b.lines.insert(0, back);
             b.n += n;
           }

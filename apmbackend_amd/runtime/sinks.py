@@ -522,8 +522,8 @@ class DBInserter:
         buffers is handed over first)."""
         self._detach()
         if self.core is not None:
-            enc = [self.core.is_encoded(i) for i in range(len(TYPES))]
             left = self.core.close()
+            enc = [self.core.is_encoded(i) for i in range(len(TYPES))]  # (the leftovers' format)
             self.core = None
             for t, blob, e in zip(TYPES, left, enc):
                 for ln in blob.decode("utf-8").split("\n"):
@@ -672,8 +672,8 @@ class DBInserter:
     def close(self):
         self._detach()
         if self.core is not None:
-            enc = [self.core.is_encoded(i) for i in range(len(TYPES))]
             left = self.core.close()
+            enc = [self.core.is_encoded(i) for i in range(len(TYPES))]  # (the leftovers' format)
             self._sync_stats()
             self.core = None
             for t, blob, e in zip(TYPES, left, enc):

@@ -18,7 +18,7 @@ for attempt in $(seq 1 ${ATTEMPTS:-40}); do
   while ! fresh; do echo "[attempt $attempt] .so stale (rebuild pending): waiting" >> "$log.attempts"; sleep 30; done
   (cd "$REPO" && /usr/local/graft/bin/gpurun --timeout "$to" -- "$cmd") > "$log" 2>&1
   rc=$?
-  if grep -qE "no free box right now|backing off after the last attempt|stopped responding while being prepared" "$log" \
+  if grep -qE "no free box right now|backing off after the last attempt|stopped responding while being prepared|nothing was charged" "$log" \
      && ! grep -qE "status=(ok|fail|timeout|error)" "$log"; then
     echo "[attempt $attempt] nothing ran; waiting" >> "$log.attempts"
     sleep 150
