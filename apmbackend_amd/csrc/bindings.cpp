@@ -20,6 +20,7 @@ namespace apm {
 namespace copyenc {
 void encode_blob(std::string_view blob, std::string* out, int64_t* counts);
 }
+int apm_txcopy_lines(const char* d_text, const uint64_t* h_line_off, int64_t n, std::string& out_rows);  // txcopy.hip
 }  // namespace apm
 
 namespace py = pybind11;
@@ -149,6 +150,7 @@ py::dict metrics_dict(const EngineMetrics& m) {
   d["t_shard_busy_ms"] = m.t_shard_busy_ms; d["t_shard_max_ms"] = m.t_shard_max_ms;
   d["t_out_ms"] = m.t_out_ms;
   d["t_lockstep_ms"] = m.t_lockstep_ms; d["t_lockstep_max_ms"] = m.t_lockstep_max_ms;
+  d["db_copy_rows"] = m.db_copy_rows; d["db_copy_fallbacks"] = m.db_copy_fallbacks;
   d["t_stats_tx_ms"] = m.t_stats_tx_ms; d["t_rollover_ms"] = m.t_rollover_ms;
   d["t_format_ms"] = m.t_format_ms; d["t_release_ms"] = m.t_release_ms;
   d["formatted_bytes"] = m.formatted_bytes; d["lockstep_rollovers"] = m.lockstep_rollovers; d["format_fallbacks"] = m.format_fallbacks;
@@ -440,6 +442,7 @@ PYBIND11_MODULE(_apm_native, m) {
       })
       .def("set_sink_fd", &Engine::set_sink_fd, py::call_guard<py::gil_scoped_release>())
       .def("set_fs_copy", &Engine::set_fs_copy, py::call_guard<py::gil_scoped_release>())
+      .def("set_db_copy", &Engine::set_db_copy, py::call_guard<py::gil_scoped_release>())
       .def("sink_bytes", &Engine::sink_bytes)
       .def("lane_cpus", &Engine::lane_cpus)
       .def("last_events", [](Engine& e) { return py::bytes(e.last_events()); })
@@ -535,6 +538,29 @@ PYBIND11_MODULE(_apm_native, m) {
     const char* names[5] = {"tx", "fs", "al", "jx", "fb"};
     for (int k = 0; k < 5; ++k) d[names[k]] = py::make_tuple(py::bytes(out[k]), counts[k]);
     return d;
+  });
+  m.def("txcopy_lines", [](py::bytes blob) {
+    // newline-terminated wire tx lines -> (COPY rows from the GPU encoder, fallback count)
+    std::string b = blob;
+    std::vector<uint64_t> off{0};
+    for (size_t i = 0; i < b.size(); ++i)
+      if (b[i] == '\n') off.push_back(i + 1);
+    if (off.back() != b.size()) throw std::invalid_argument("txcopy_lines: the last line needs its newline");
+    const int64_t n = (int64_t)off.size() - 1;
+    std::string rows;
+    int fb = 0;
+    {
+      py::gil_scoped_release rel;
+      uint64_t cap = 1;
+      while (cap < b.size() + 64) cap <<= 1;
+      char* d = nullptr;
+      HIP_OK(hipMalloc(&d, cap));
+      HIP_OK(hipMemset(d, 0, cap));
+      HIP_OK(hipMemcpy(d, b.data(), b.size(), hipMemcpyHostToDevice));
+      fb = n ? apm_txcopy_lines(d, off.data(), n, rows) : 0;
+      HIP_OK(hipFree(d));
+    }
+    return py::make_tuple(py::bytes(rows), fb);
   });
   m.def("flatmap_selftest", [](int n_ops, uint64_t seed, int key_space) {
     // randomized FlatMap / SmallVec vs std containers (CPU test of the join's data structures)

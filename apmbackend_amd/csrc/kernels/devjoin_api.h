@@ -206,6 +206,12 @@ void apm_dj_arena_grow(const apm::NeedEnt* old, uint32_t old_cap, apm::NeedEnt* 
 // n_upper gids (d_n null: all; offs[n_upper] = total bytes), then the copy into `out`
 int apm_dj_gather_plan(const int64_t* gid, int64_t n_upper, const int64_t* d_n, uint32_t* lens, uint32_t* offs,
                        void* tmp, size_t tmp_bytes, hipStream_t s);
+// The same for the transactions table's COPY rows (txcopy.hip): lens / offs of the rows the
+// released wire lines encode to; fb_count += lines outside the GPU encoder's domain
+int apm_dj_txcopy_plan(const int64_t* gid, int64_t n_upper, const int64_t* d_n, const char* ring, uint64_t ring_cap,
+                       uint32_t* lens, uint32_t* offs, uint32_t* fb_count, void* tmp, size_t tmp_bytes, hipStream_t s);
+void apm_dj_txcopy_write(const int64_t* gid, int64_t n, const char* ring, uint64_t ring_cap, const uint32_t* offs,
+                         char* out, hipStream_t s);
 // `out` must hold offs[n] = total_bytes bytes (16-byte aligned)
 void apm_dj_gather_copy(const int64_t* gid, int64_t n, const char* ring, uint64_t ring_cap, const uint32_t* offs,
                         char* out, uint64_t total_bytes, hipStream_t s);

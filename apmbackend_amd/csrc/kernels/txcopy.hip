@@ -217,6 +217,9 @@ __global__ __launch_bounds__(TC_TB) void k_txcopy_write(const int64_t* __restric
 }
 
 }  // namespace
+}  // namespace apm
+
+using namespace apm;
 
 int apm_dj_txcopy_plan(const int64_t* gid, int64_t n_upper, const int64_t* d_n, const char* ring, uint64_t ring_cap,
                        uint32_t* lens, uint32_t* offs, uint32_t* fb_count, void* tmp, size_t tmp_bytes, hipStream_t s) {
@@ -235,6 +238,8 @@ void apm_dj_txcopy_write(const int64_t* gid, int64_t n, const char* ring, uint64
   hipLaunchKernelGGL(k_txcopy_write, dim3((unsigned)((n + TC_TB - 1) / TC_TB)), dim3(TC_TB), 0, s, gid, n, ring,
                      ring_cap, offs, out);
 }
+
+namespace apm {
 
 // Test entry: COPY rows of wire lines in a device buffer (line i = [line_off[i], line_off[i + 1])
 // without its '\n'), through the same kernels; returns the fallback count.

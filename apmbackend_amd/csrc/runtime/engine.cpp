@@ -28,6 +28,12 @@
 #include "format.h"
 
 namespace apm {
+namespace copyenc {
+void encode_blob(std::string_view blob, std::string* out, int64_t* counts);  // copyenc.cpp
+}
+}  // namespace apm
+
+namespace apm {
 
 namespace {
 double now_ms() {
@@ -270,6 +276,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     HIP_OK(hipHostGetDevicePointer((void**)&hd_rel_n_, h_rel_n_, 0));
     d_rel_lens_ = (uint32_t*)dmalloc(((size_t)cfg_.pool_cap + 2) * 4);
     d_rel_offs_ = (uint32_t*)dmalloc(((size_t)cfg_.pool_cap + 2) * 4);
+    d_rel_fb_ = (uint32_t*)dmalloc(4);
+    HIP_OK(hipMemset(d_rel_fb_, 0, 4));
     HIP_OK(hipHostMalloc((void**)&h_rel_total_, 64, hipHostMallocDefault));
     HIP_OK(hipHostGetDevicePointer((void**)&hd_rel_total_, h_rel_total_, 0));
     d_unmapped_ = (unsigned long long*)dmalloc(64);
@@ -391,6 +399,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   {
     const char* e = std::getenv("APM_FMT_HOST");
     fmt_host_ = e && e[0] == '1';
+    const char* f = std::getenv("APM_TXCOPY_FORCE_FALLBACK");
+    txcopy_force_fb_ = f && f[0] == '1';
   }
   // alerts
   d_alerts_ = (AlertRec*)dmalloc((size_t)cfg_.max_alerts * sizeof(AlertRec));
@@ -2198,10 +2208,16 @@ void Engine::release_device(int64_t edge_ts) {
   ExportArgs ex{};
   ex.add(d_rel_n_, hd_rel_n_, 8);
   if (want(OUT_DB) && pool_n_ > 0) {
-    if (apm_dj_gather_plan(d_pool_gid_[pool_cur_], pool_n_, d_rel_n_, d_rel_lens_, d_rel_offs_, d_release_tmp_,
-                           release_tmp_bytes_, stream_) != 0)
-      throw std::runtime_error("release tmp too small");
+    rel_copy_ = db_copy_;
+    const int rc = rel_copy_
+                       ? apm_dj_txcopy_plan(d_pool_gid_[pool_cur_], pool_n_, d_rel_n_, dj_->ring(), dj_->ring_cap(),
+                                            d_rel_lens_, d_rel_offs_, d_rel_fb_, d_release_tmp_, release_tmp_bytes_,
+                                            stream_)
+                       : apm_dj_gather_plan(d_pool_gid_[pool_cur_], pool_n_, d_rel_n_, d_rel_lens_, d_rel_offs_,
+                                            d_release_tmp_, release_tmp_bytes_, stream_);
+    if (rc != 0) throw std::runtime_error("release tmp too small");
     ex.add(d_rel_offs_ + pool_n_, hd_rel_total_, 4);
+    if (rel_copy_) ex.add(d_rel_fb_, hd_rel_total_ + 1, 4, true, 0);  // read and reset
   }
   apm_export(&ex, stream_);
 }
@@ -2212,18 +2228,39 @@ void Engine::release_device(int64_t edge_ts) {
 void Engine::release_device_finish() {
   const int64_t released = std::min<int64_t>(*h_rel_n_, pool_n_);
   if (want(OUT_DB) && released > 0) {
-    const size_t total = *h_rel_total_;
+    size_t total = *h_rel_total_;
+    bool copy = rel_copy_;
+    bool host_enc = false;
+    if (copy && (h_rel_total_[1] != 0 || txcopy_force_fb_)) {
+      // a released line outside the GPU encoder's domain (txcopy.hip): this release goes out as
+      // wire lines and is encoded on the host, row for row as the sink's encoder would
+      copy = false;
+      host_enc = true;
+      ++metrics_.db_copy_fallbacks;
+      if (apm_dj_gather_plan(d_pool_gid_[pool_cur_], pool_n_, d_rel_n_, d_rel_lens_, d_rel_offs_, d_release_tmp_,
+                             release_tmp_bytes_, stream_) != 0)
+        throw std::runtime_error("release tmp too small");
+      uint32_t wire_total = 0;
+      HIP_OK(hipMemcpyAsync(&wire_total, d_rel_offs_ + pool_n_, 4, hipMemcpyDeviceToHost, stream_));
+      HIP_OK(hipStreamSynchronize(stream_));
+      total = wire_total;
+    }
+    if (copy) metrics_.db_copy_rows += (uint64_t)released;
     const int k = rel_k_;
     rel_k_ ^= 1;
     const double tw = now_ms();
     out_wait(rel_task_[k]);  // the buffer's previous reader is done
     trace_event("rel.wait_lane", tw, now_ms(), 1);
     if (total + 64 > rel_text_cap_[k]) d_rel_text_[k] = (char*)regrow(d_rel_text_[k], rel_text_cap_[k], total + 64);
-    apm_dj_gather_copy(d_pool_gid_[pool_cur_], released, dj_->ring(), dj_->ring_cap(), d_rel_offs_, d_rel_text_[k], total,
-                       stream_);
+    if (copy)
+      apm_dj_txcopy_write(d_pool_gid_[pool_cur_], released, dj_->ring(), dj_->ring_cap(), d_rel_offs_, d_rel_text_[k],
+                          stream_);
+    else
+      apm_dj_gather_copy(d_pool_gid_[pool_cur_], released, dj_->ring(), dj_->ring_cap(), d_rel_offs_, d_rel_text_[k],
+                         total, stream_);
     // a COPY sink cuts its flushes from the row offsets (d_rel_offs_ is rewritten by the next
     // release: copied here, in stream order)
-    const bool rows = byte_sink_[OUT_DB] != nullptr;
+    const bool rows = byte_sink_[OUT_DB] != nullptr && !host_enc;
     if (rows) {
       if ((size_t)released + 1 > h_rel_offs_cap_[k]) {
         if (h_rel_offs_[k]) HIP_OK(hipHostFree(h_rel_offs_[k]));
@@ -2233,7 +2270,7 @@ void Engine::release_device_finish() {
       d2h(h_rel_offs_[k], d_rel_offs_, ((size_t)released + 1) * 4, stream_);
     }
     HIP_OK(hipEventRecord(ev_rel_[k], stream_));
-    rel_task_[k] = post_out([this, k, total, rows, released]() {
+    rel_task_[k] = post_out([this, k, total, rows, released, host_enc]() {
       HIP_OK(hipEventSynchronize(ev_rel_[k]));
       wait_fmt_holds(4 + k);  // the sink still writes from this buffer (zero-copy COPY rows)
       if (total > h_rel_text_cap_[k]) {
@@ -2245,8 +2282,16 @@ void Engine::release_device_finish() {
       HIP_OK(hipMemcpyAsync(h_rel_text_[k], d_rel_text_[k], total, hipMemcpyDeviceToHost, out_stream_));
       HIP_OK(hipStreamSynchronize(out_stream_));
       const double tl1 = now_ms();
-      if (rows) emit_bytes_held(OUT_DB, h_rel_text_[k], total, 4 + k, h_rel_offs_[k], (size_t)released);
-      else emit_bytes(OUT_DB, h_rel_text_[k], total);
+      if (host_enc) {
+        std::string enc[5];
+        int64_t counts[5] = {0, 0, 0, 0, 0};
+        copyenc::encode_blob(std::string_view(h_rel_text_[k], total), enc, counts);
+        emit_bytes(OUT_DB, enc[0].data(), enc[0].size());
+      } else if (rows) {
+        emit_bytes_held(OUT_DB, h_rel_text_[k], total, 4 + k, h_rel_offs_[k], (size_t)released);
+      } else {
+        emit_bytes(OUT_DB, h_rel_text_[k], total);
+      }
       trace_event("lane db D2H", tl0, tl1, 4);
       trace_event("lane db emit", tl1, now_ms(), 4);
     });
@@ -2550,6 +2595,12 @@ int Engine::pg_timestamp(int64_t ms, char* out) {
 void Engine::set_fs_copy(bool on) {
   flush();
   fs_copy_ = on;
+}
+
+bool Engine::set_db_copy(bool on) {
+  flush();
+  db_copy_ = on && dj_ != nullptr;
+  return db_copy_;
 }
 
 void Engine::emit_bytes(int kind, const char* p, size_t n) {

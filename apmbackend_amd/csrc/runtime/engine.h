@@ -203,6 +203,7 @@ struct EngineMetrics {
   double t_shard_busy_ms = 0, t_shard_max_ms = 0;              // per batch: mean / max of one shard's join
   double t_stats_tx_ms = 0, t_rollover_ms = 0, t_format_ms = 0, t_release_ms = 0;  // inside t_stats_ms
   double t_out_ms = 0;                        // output lane: released-line gather + st/fs emission
+  uint64_t db_copy_rows = 0, db_copy_fallbacks = 0;  // released db rows encoded on the GPU / releases encoded on the host
   double t_lockstep_ms = 0, t_lockstep_max_ms = 0;  // ingest thread in the per-batch clock collective (sum / worst)
   std::vector<double> rollover_latency_ms;   // batch arrival -> alert decision per rollover
 };
@@ -291,6 +292,10 @@ class Engine {
   void set_byte_sink(const std::string& kind, std::shared_ptr<ByteSink> sink);
   // fs stream as Postgres COPY rows (K12 formats the DB row directly; the DB sink skips encoding)
   void set_fs_copy(bool on);
+  // released db rows as COPY rows of the transactions table, encoded on the GPU (device join
+  // only; returns whether it is on)
+  bool set_db_copy(bool on);
+  bool db_copy() const { return db_copy_; }
   bool fs_copy() const { return fs_copy_; }
   static int pg_timestamp(int64_t ms, char* out);
   uint64_t sink_bytes(const std::string& kind) { flush(); return sink_bytes_[out_kind_of(kind)]; }
@@ -729,6 +734,7 @@ class Engine {
   int64_t* hd_rel_n_ = nullptr;
   uint32_t* d_rel_lens_ = nullptr;
   uint32_t* d_rel_offs_ = nullptr;
+  uint32_t* d_rel_fb_ = nullptr;  // released lines outside the GPU COPY encoder's domain (txcopy.hip)
   uint32_t* h_rel_total_ = nullptr;            // [2]
   uint32_t* hd_rel_total_ = nullptr;
   char* d_rel_text_[2] = {nullptr, nullptr};
@@ -1065,6 +1071,9 @@ class Engine {
   int sink_fd_[N_OUT] = {-1, -1, -1, -1, -1, -1, -1, -1};
   std::shared_ptr<ByteSink> byte_sink_[N_OUT];
   bool fs_copy_ = false;
+  bool db_copy_ = false;
+  bool rel_copy_ = false;         // the pending release was planned as COPY rows
+  bool txcopy_force_fb_ = false;  // APM_TXCOPY_FORCE_FALLBACK=1: every release takes the host path (tests)
   uint64_t sink_bytes_[N_OUT] = {0, 0, 0, 0, 0, 0, 0, 0};
   // K14 server rollup + exogenous context
   std::vector<double> h_ctx_;                    // [servers][CTX_FIELDS] (stats thread)

@@ -441,6 +441,8 @@ class DBInserter:
         self.resume_path = ic.get("bufferResumeFileFullPath")
         self.core = None
         self.gpu_fs_copy = as_bool_cfg(ic.get("gpuFsCopyRows", True))
+        # released db rows (the transactions table) encoded on the GPU (engine.set_db_copy)
+        self.gpu_tx_copy = as_bool_cfg(ic.get("gpuTxCopyRows", True))
         self._writer: Optional[Writer] = writer
         if writer is None:
             N = _native() if as_bool_cfg(ic.get("nativeSink", True)) else None
@@ -498,12 +500,16 @@ class DBInserter:
         if fs_copy:
             # K12 (fs) and the fleet formatter (fb) write COPY text on the GPU; the sink stores it as is
             native_engine.set_fs_copy(True)
+        db_copy = (self.gpu_tx_copy and "db" in kinds and hasattr(native_engine, "set_db_copy")
+                   and native_engine.set_db_copy(True))
         for k in kinds:
             if k in ("fs", "fb") and fs_copy:
                 N.attach_sink(native_engine, k, self.core, TYPES.index(k))
+            elif k == "db" and db_copy:
+                N.attach_sink(native_engine, k, self.core, TYPES.index("tx"))
             else:
                 N.attach_sink(native_engine, k, self.core)
-        self._attached = (native_engine, list(kinds), fs_copy)
+        self._attached = (native_engine, list(kinds), fs_copy, db_copy)
         return True
 
     def _detach(self):
@@ -514,6 +520,8 @@ class DBInserter:
                 N.detach_sink(att[0], k)
             if att[2]:
                 att[0].set_fs_copy(False)
+            if att[3]:
+                att[0].set_db_copy(False)
             self._attached = None
 
     @writer.setter
