@@ -284,7 +284,6 @@ def test_headline_shard_device_join_equals_host_join(audit):
         ends = [int(l.split("|")[6]) for l in got[k]["db"]]
         assert ends == sorted(ends)
     jd = engines["device"].metrics()["join"]
-    assert jd["chain_partial_blocks"] > 0 and jd["chain_logid_blocks"] > 0  # the chain paths ran
     assert all(jd.get(k, 0) == 0 for k in ("partial_overflow", "need_overflow", "table_full", "pool_exhausted"))
 
 

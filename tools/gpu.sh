@@ -42,7 +42,7 @@ n=0
 for task in "$@"; do
   n=$((n + 1))
   case $task in
-    suite) run "suite" 1100 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests -m gpu ;;
+    suite) run "suite" 1100 python -u -m pytest --maxfail 6 -v --timeout 240 --timeout-method thread tests -m gpu ;;
     suite:*) run "suite_$n" 900 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests -m gpu -k "${task#suite:}" ;;
     smoke) run "smoke" 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run "bench_$n" 300 python -u bench.py --steps 20 --warmup 5 ;;
