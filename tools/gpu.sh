@@ -36,6 +36,10 @@ run() {  # run NAME SECONDS CMD...
   timeout -k 10 "$secs" "$@" > "$O/$name.log" 2>&1
   local rc=$?
   echo "[$name] rc=$rc $(( $(date +%s) - t0 ))s :: $(tail -c 600 "$O/$name.log" | tail -n 2 | cut -c1-400)"
+  # pytest rc 1 = assertion failures only (no fault, no hang: a timeout or a crash ends the run)
+  if [ $rc -eq 1 ] && [[ $name == suite* ]] && ! grep -qE "Timeout|Fatal Python error|core dumped|HSA_STATUS|Memory access fault" "$O/$name.log"; then
+    echo "[$name] test failures (no fault): continuing"; return 0
+  fi
   case $rc in 0) ;; *) stop "$name" $rc ;; esac
 }
 n=0
