@@ -12,7 +12,7 @@
 //
 // Outside the domain handled here the line is flagged (`fb` counter) and the engine encodes
 // the whole release on the host instead: a first field other than "tx", a numeric field with
-// leading whitespace or control bytes, a hex prefix, or more than 15 significant digits.
+// leading whitespace or control bytes, a hex prefix, or more than 19 significant digits.
 #include "kernel_api.h"
 
 #include <rocprim/rocprim.hpp>
@@ -86,7 +86,7 @@ __device__ __forceinline__ bool parse_int_field(const char* p, uint32_t s, uint3
     if (d > 9) break;
     any = true;
     if (sig || d) {
-      if (++sig > 15) { fb = true; return false; }
+      if (++sig > 19) { fb = true; return false; }  // (19 digits always fit 64 bits)
       v = v * 10 + d;
     }
   }
@@ -97,8 +97,12 @@ template <bool W>
 __device__ __forceinline__ void put_ts(OutT<W>& o, const TxFields& f, int k, bool& fb) {
   bool neg;
   uint64_t v;
-  if (!f.has(k) || !parse_int_field(f.p, f.st(k), f.en(k), neg, v, fb)) { o.lit("\\N"); return; }
-  const int64_t t = neg ? -(int64_t)v : (int64_t)v;  // |t| < 10^15 ms: inside ts_text's range
+  // (ts_text's range: |ms| <= 8.64e15, exact in a double)
+  if (!f.has(k) || !parse_int_field(f.p, f.st(k), f.en(k), neg, v, fb) || v > 8640000000000000ull) {
+    o.lit("\\N");
+    return;
+  }
+  const int64_t t = neg ? -(int64_t)v : (int64_t)v;
   int64_t days = t / 86400000, rem = t % 86400000;
   if (rem < 0) { rem += 86400000; --days; }
   int y;
@@ -150,8 +154,11 @@ __device__ __forceinline__ void put_int(OutT<W>& o, const TxFields& f, int k, bo
   bool neg;
   uint64_t v;
   if (!f.has(k) || !parse_int_field(f.p, f.st(k), f.en(k), neg, v, fb)) { o.lit("\\N"); return; }
-  if (neg && v) o.c('-');  // -0 prints 0
-  o.u(v);
+  // String(parseInt(x)): the digits are an exact integer v; the parsed Number is v rounded to a
+  // double (nearest-even, as the host's strtod), printed JS-style (exact below 2^53; -0 -> 0)
+  bool inexact = false;
+  const double x = (double)v;
+  o.jsnum(neg ? -x : x, inexact);
 }
 
 template <bool W>

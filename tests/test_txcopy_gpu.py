@@ -35,6 +35,8 @@ EDGE = [
     "tx|s|n|l|1.2345e+21|0|-1|0|Y",
     "tx|s|n|l|-0|86399999|1|007|Y",
     "tx|s|n|l|999999999999999|999999999999999|-999999999999999|1|Y",
+    "tx|s|n|l|1321867455355857|8640000000000000|8640000000000001|9007199254740993|Y",
+    "tx|s|n|l|9999999999999999999|-8640000000000000|99999999999999999|-12345678901234567|Y",
     "tx|s|n|l|-62135596800000|-62135596800001|-62198755200000|000000000000000000001|Y",
     "tx|s|n|l",
     "tx|s",
@@ -49,7 +51,7 @@ EDGE = [
 
 OUTSIDE = [
     "tx|a|b|c| 5|1|1|1|Y",
-    "tx|a|b|c|1234567890123456|1|1|1|Y",
+    "tx|a|b|c|12345678901234567890|1|1|1|Y",
     "tq|a|b|c|1|1|1|1|Y",
     "tx|a|b|c|0x10|1|1|1|Y",
     "tx|a|b|c|1|\t1|1|1|Y",
@@ -86,12 +88,15 @@ def test_txcopy_random_lines_equal_host_encoder():
     alphabet = "abcXYZ019|\\\t-._:"
 
     def name():
-        return "".join(rng.choice(alphabet) for _ in range(rng.randint(0, 40)))
+        # (a '|' inside a name shifts the fields: a name may land in a numeric field, so none
+        # starts the way a numeric field outside the GPU domain does -- tab, long digit runs)
+        s = "".join(rng.choice(alphabet) for _ in range(rng.randint(0, 40)))
+        return ("a" + s) if s[:1] in ("\t", "-", "0", "1", "9") else s
 
     def num():
         r = rng.random()
-        if r < 0.5:
-            return str(rng.randint(-10 ** rng.randint(1, 15) + 1, 10 ** rng.randint(1, 15) - 1))
+        if r < 0.5:  # up to 19 digits: above 2^53 the parsed Number is rounded, then printed
+            return str(rng.randint(-10 ** rng.randint(1, 19) + 1, 10 ** rng.randint(1, 19) - 1))
         if r < 0.6:
             return "NaN"
         if r < 0.7:
