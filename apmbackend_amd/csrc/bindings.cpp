@@ -21,6 +21,7 @@ namespace copyenc {
 void encode_blob(std::string_view blob, std::string* out, int64_t* counts);
 }
 int apm_txcopy_lines(const char* d_text, const uint64_t* h_line_off, int64_t n, std::string& out_rows);  // txcopy.hip
+std::vector<double> apm_release_bench(int64_t n, int iters, uint64_t seed);                               // txcopy.hip
 }  // namespace apm
 
 namespace py = pybind11;
@@ -539,6 +540,23 @@ PYBIND11_MODULE(_apm_native, m) {
     for (int k = 0; k < 5; ++k) d[names[k]] = py::make_tuple(py::bytes(out[k]), counts[k]);
     return d;
   });
+  m.def("set_blocking_sync", [](int device) {
+    // before anything else creates the device's runtime state (bench.py, ranks sharing a GPU):
+    // stream / event waits block instead of spinning
+    HIP_OK(hipSetDevice(device));
+    return hipSetDeviceFlags(hipDeviceScheduleBlockingSync) == hipSuccess;
+  });
+  m.def("release_bench", [](int64_t n, int iters, uint64_t seed) {
+    std::vector<double> r;
+    {
+      py::gil_scoped_release rel;
+      r = apm_release_bench(n, iters, seed);
+    }
+    py::dict d;
+    const char* k[7] = {"lines", "wire_bytes", "copy_bytes", "gather_us", "txcopy_us", "txcopy_write_us", "fallbacks"};
+    for (int i = 0; i < 7; ++i) d[k[i]] = r[(size_t)i];
+    return d;
+  }, py::arg("n") = 60000, py::arg("iters") = 20, py::arg("seed") = 1);
   m.def("txcopy_lines", [](py::bytes blob) {
     // newline-terminated wire tx lines -> (COPY rows from the GPU encoder, fallback count)
     std::string b = blob;

@@ -15,6 +15,11 @@
 // leading whitespace or control bytes, a hex prefix, or more than 19 significant digits.
 #include "kernel_api.h"
 
+#include <algorithm>
+#include <random>
+#include <string>
+#include <vector>
+
 #include <rocprim/rocprim.hpp>
 
 #include "devjoin_api.h"
@@ -287,6 +292,92 @@ int apm_txcopy_lines(const char* d_text, const uint64_t* h_line_off, int64_t n, 
   HIP_OK(hipFree(d_offs));
   HIP_OK(hipFree(d_fb));
   return (int)fb;
+}
+
+
+// Isolated timing of the release kernels (tools/release_bench.py): n synthetic wire tx lines
+// (16-digit accounts, 13-digit timestamps, ~100 B) laid out contiguously in a ring, released in
+// a shuffled order (released lines hop between the batch regions of the ring), gathered `iters`
+// times by k_gather_lines and encoded as COPY rows by the txcopy kernels, each alone on one
+// stream.  Returns {lines, wire_bytes, copy_bytes, gather_us, txcopy_us (plan + write),
+// txcopy_write_us, fallbacks}.
+std::vector<double> apm_release_bench(int64_t n, int iters, uint64_t seed) {
+  std::mt19937_64 rng(seed);
+  std::string text;
+  std::vector<int64_t> gid((size_t)n);
+  char buf[256];
+  for (int64_t i = 0; i < n; ++i) {
+    const int jvm = (int)(rng() % 8), svc = (int)(rng() % 10000);
+    const unsigned long long acct = 1000000000000000ull + rng() % 9000000000000000ull;
+    const long long start = 1578391200000ll + (long long)(rng() % 600000), el = (long long)(rng() % 2000);
+    const int k = std::snprintf(buf, sizeof buf, "tx|jvm%02d|S:getSvc%04d|JVM%02d-%08lld|%llu|%lld|%lld|%lld|%c", jvm,
+                                svc, jvm, (long long)i, acct, start, start + el, el, (rng() & 1) ? 'Y' : 'N');
+    gid[(size_t)i] = (int64_t)(((uint64_t)text.size() << 20) | (uint64_t)k);
+    text.append(buf, (size_t)k);
+    text += '\n';
+  }
+  std::shuffle(gid.begin(), gid.end(), rng);
+  uint64_t cap = 1;
+  while (cap < text.size() + 64) cap <<= 1;
+  char *d_ring = nullptr, *d_out = nullptr;
+  int64_t* d_gid = nullptr;
+  uint32_t *d_lens = nullptr, *d_offs = nullptr, *d_fb = nullptr;
+  HIP_OK(hipMalloc(&d_ring, cap));
+  HIP_OK(hipMemset(d_ring, 0, cap));
+  HIP_OK(hipMemcpy(d_ring, text.data(), text.size(), hipMemcpyHostToDevice));
+  HIP_OK(hipMalloc(&d_gid, (size_t)n * 8 + 8));
+  HIP_OK(hipMemcpy(d_gid, gid.data(), (size_t)n * 8, hipMemcpyHostToDevice));
+  HIP_OK(hipMalloc(&d_lens, ((size_t)n + 1) * 4));
+  HIP_OK(hipMalloc(&d_offs, ((size_t)n + 1) * 4));
+  HIP_OK(hipMalloc(&d_fb, 4));
+  HIP_OK(hipMemset(d_fb, 0, 4));
+  HIP_OK(hipMalloc(&d_out, text.size() * 3 + 64));
+  size_t need = 0;
+  HIP_OK(rocprim::exclusive_scan(nullptr, need, d_lens, d_offs, 0u, (size_t)n + 1, rocprim::plus<uint32_t>(), 0));
+  void* tmp = nullptr;
+  HIP_OK(hipMalloc(&tmp, need + 256));
+  hipStream_t st;
+  HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  hipEvent_t e0, e1;
+  HIP_OK(hipEventCreate(&e0));
+  HIP_OK(hipEventCreate(&e1));
+  auto elapsed_us = [&]() {
+    float ms = 0;
+    HIP_OK(hipEventSynchronize(e1));
+    HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+    return 1000.0 * ms / iters;
+  };
+  // wire gather
+  if (apm_dj_gather_plan(d_gid, n, nullptr, d_lens, d_offs, tmp, need + 256, st) != 0) throw std::runtime_error("bench scan");
+  apm_dj_gather_copy(d_gid, n, d_ring, cap, d_offs, d_out, text.size(), st);  // warm
+  HIP_OK(hipEventRecord(e0, st));
+  for (int i = 0; i < iters; ++i) apm_dj_gather_copy(d_gid, n, d_ring, cap, d_offs, d_out, text.size(), st);
+  HIP_OK(hipEventRecord(e1, st));
+  const double gather_us = elapsed_us();
+  // COPY rows: plan + write, then write alone
+  if (apm_dj_txcopy_plan(d_gid, n, nullptr, d_ring, cap, d_lens, d_offs, d_fb, tmp, need + 256, st) != 0)
+    throw std::runtime_error("bench scan");
+  HIP_OK(hipEventRecord(e0, st));
+  for (int i = 0; i < iters; ++i) {
+    if (apm_dj_txcopy_plan(d_gid, n, nullptr, d_ring, cap, d_lens, d_offs, d_fb, tmp, need + 256, st) != 0)
+      throw std::runtime_error("bench scan");
+    apm_dj_txcopy_write(d_gid, n, d_ring, cap, d_offs, d_out, st);
+  }
+  HIP_OK(hipEventRecord(e1, st));
+  const double txcopy_us = elapsed_us();
+  HIP_OK(hipEventRecord(e0, st));
+  for (int i = 0; i < iters; ++i) apm_dj_txcopy_write(d_gid, n, d_ring, cap, d_offs, d_out, st);
+  HIP_OK(hipEventRecord(e1, st));
+  const double write_us = elapsed_us();
+  uint32_t copy_bytes = 0, fb = 0;
+  HIP_OK(hipMemcpy(&copy_bytes, d_offs + n, 4, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(&fb, d_fb, 4, hipMemcpyDeviceToHost));
+  HIP_OK(hipEventDestroy(e0));
+  HIP_OK(hipEventDestroy(e1));
+  HIP_OK(hipStreamDestroy(st));
+  for (void* p : {(void*)d_ring, (void*)d_out, (void*)d_gid, (void*)d_lens, (void*)d_offs, (void*)d_fb, tmp})
+    HIP_OK(hipFree(p));
+  return {(double)n, (double)text.size(), (double)copy_bytes, gather_us, txcopy_us, write_us, (double)fb};
 }
 
 }  // namespace apm

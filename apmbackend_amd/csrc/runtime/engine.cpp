@@ -242,6 +242,15 @@ void* Engine::dmalloc_try(size_t bytes) {
 
 Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipSetDevice(cfg_.device));
+  {
+    // Ranks sharing one GPU (a rehearsal of the node on one card): host threads that spin in
+    // every stream / event wait multiply by the rank count and starve each other of the box's
+    // CPU share -- there the waits block instead (APM_BLOCKING_SYNC=1; bench.py sets it when
+    // local ranks outnumber the GPUs).  Best effort: the flag cannot change on a device whose
+    // runtime state exists already.
+    const char* e = std::getenv("APM_BLOCKING_SYNC");
+    if (e && e[0] == '1') (void)hipSetDeviceFlags(hipDeviceScheduleBlockingSync);
+  }
   HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   HIP_OK(hipStreamCreateWithFlags(&parse_stream_, hipStreamNonBlocking));
   HIP_OK(hipStreamCreateWithFlags(&out_stream_, hipStreamNonBlocking));

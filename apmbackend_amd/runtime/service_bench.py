@@ -67,7 +67,8 @@ def _run(args, cfg, N, rank, root, IngestService):
     g = cfg["gpu"]
     ckpt = getattr(args, "service_ckpt", "on") == "on"
     fleet = getattr(args, "service_fleet", "on") == "on"
-    g.update({"tailFromStart": True, "tailReadAhead": True, "tailIdleMs": 1.0, "tailReadThreads": 4,
+    g.update({"tailFromStart": True, "tailReadAhead": True, "tailIdleMs": 1.0,
+              "tailReadThreads": getattr(args, "tail_read_threads", 8),
               "checkpointDir": os.path.join(root, "ckpt") if ckpt else None, "checkpointEverySeconds": 60,
               "fleetBaseline": fleet, "fleetSingleRank": fleet})
     ic = cfg["streamInsertDb"]

@@ -122,6 +122,10 @@ def main():
                     help="engine collectives at N > 1: rccl (one GPU per rank, xGMI) or host (TCP via rank 0; "
                          "ranks sharing a GPU -- RCCL refuses two ranks on one device).  auto: rccl when every "
                          "local rank has its own GPU")
+    ap.add_argument("--blocking-sync", default="auto", choices=["auto", "on", "off"],
+                    help="host waits block instead of spinning; auto: on when local ranks share a GPU "
+                         "(their spinning threads multiply past the box's CPU share)")
+    ap.add_argument("--tail-read-threads", type=int, default=8, help="--path service: tailer pread threads")
     ap.add_argument("--rank-report", default=None,
                     help="directory: every rank writes rank<R>.json (its lines, node-wide counters, per-step times)")
     args = ap.parse_args()
@@ -155,9 +159,13 @@ def main():
         if local_world == world:  # one node: gloo over loopback (the hostname may not resolve)
             os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
         dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=600))
+    from apmbackend_amd import _native
+    blocking = args.blocking_sync == "on" or (args.blocking_sync == "auto" and local_world > n_dev)
+    if blocking:  # before torch creates the device's runtime state
+        os.environ["APM_BLOCKING_SYNC"] = "1"
+        _native.load(build_if_missing=False).set_blocking_sync(device)
     torch.cuda.set_device(device)
 
-    from apmbackend_amd import _native
     from apmbackend_amd.models.pipeline import APMEngine
     from apmbackend_amd.parallel.fleet import FleetBaseline
     from apmbackend_amd.utils.config import default_config
@@ -404,7 +412,7 @@ def main():
                 "preset": args.preset,
                 "ring_dtype": args.ring,
             },
-            "n_ranks": world,
+            "n_ranks": world, "blocking_sync": blocking,
             "collective": coll,
             "comm_nranks": comm_ranks,
             "lines_total": int(lines_total),

@@ -20,6 +20,7 @@
 #   prof               rocprofv3 --kernel-trace --stats of bench.py 20/5
 #   timeline           rocprofv3 --kernel-trace --memory-copy-trace (tools/gpu_timeline.py reads it)
 #   pmc:C1,C2,...      one rocprofv3 --pmc pass of bench.py 10/3 (keep within one pass's counter budget)
+#   service:T          the same with T tailer read threads
 #   env:K=V            export K=V for the following tasks (A/B switches)
 #   py:MODULE          python -m MODULE (diagnostics under tools/)
 set -u
@@ -59,6 +60,8 @@ for task in "$@"; do
         --rank-report "$O/ranks${w}_$n" ;;
     preset:*) run "preset_${task#preset:}_$n" 500 python -u bench.py --preset "${task#preset:}" --steps 20 --warmup 5 ;;
     service) run "service_$n" 600 python -u bench.py --path service --steps 200 --warmup 5 --service-dir /tmp/apm_svc ;;
+    service:*) run "service${task#service:}_$n" 600 python -u bench.py --path service --steps 200 --warmup 5 \
+                 --service-dir /tmp/apm_svc --tail-read-threads "${task#service:}" ;;
     prof) run "prof_$n" 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$n" -o run -- \
             python3 bench.py --steps 20 --warmup 5 ;;
     timeline) run "timeline_$n" 400 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$O/tl_$n" -o run -- \
