@@ -410,6 +410,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     fmt_host_ = e && e[0] == '1';
     const char* f = std::getenv("APM_TXCOPY_FORCE_FALLBACK");
     txcopy_force_fb_ = f && f[0] == '1';
+    const char* d = std::getenv("APM_D2H_KERNEL");
+    d2h_kernel_ = d && d[0] == '1';
   }
   // alerts
   d_alerts_ = (AlertRec*)dmalloc((size_t)cfg_.max_alerts * sizeof(AlertRec));
@@ -1932,6 +1934,12 @@ void Engine::h2d(void* d, const void* h, size_t n, hipStream_t s) {
   apm_copy(d, hv, n, s);
 }
 
+void Engine::lane_d2h(void* h, const void* d, size_t n) {
+  if (!n) return;
+  if (d2h_kernel_) d2h(h, d, n, out_stream_);
+  else HIP_OK(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, out_stream_));
+}
+
 void Engine::d2h(void* h, const void* d, size_t n, hipStream_t s) {
   if (n == 0) return;
   void* hv = nullptr;
@@ -2288,7 +2296,7 @@ void Engine::release_device_finish() {
         HIP_OK(hipHostMalloc((void**)&h_rel_text_[k], h_rel_text_cap_[k], hipHostMallocDefault));
       }
       const double tl0 = now_ms();
-      HIP_OK(hipMemcpyAsync(h_rel_text_[k], d_rel_text_[k], total, hipMemcpyDeviceToHost, out_stream_));
+      lane_d2h(h_rel_text_[k], d_rel_text_[k], total);
       HIP_OK(hipStreamSynchronize(out_stream_));
       const double tl1 = now_ms();
       if (host_enc) {
@@ -2777,8 +2785,8 @@ void Engine::format_rollover_text(int64_t edge_ts) {
     }
     char* h = h_fmt_out_[k];
     const double tl0 = now_ms();
-    if (st_total) HIP_OK(hipMemcpyAsync(h, dst, st_total, hipMemcpyDeviceToHost, out_stream_));
-    if (fs_total) HIP_OK(hipMemcpyAsync(h + st_total, dst + st_cap, fs_total, hipMemcpyDeviceToHost, out_stream_));
+    if (st_total) lane_d2h(h, dst, st_total);
+    if (fs_total) lane_d2h(h + st_total, dst + st_cap, fs_total);
     HIP_OK(hipStreamSynchronize(out_stream_));
     {
       std::lock_guard<std::mutex> g(out_mu_);

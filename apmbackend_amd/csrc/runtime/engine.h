@@ -1073,7 +1073,11 @@ class Engine {
   bool fs_copy_ = false;
   bool db_copy_ = false;
   bool rel_copy_ = false;         // the pending release was planned as COPY rows
-  bool txcopy_force_fb_ = false;  // APM_TXCOPY_FORCE_FALLBACK=1: every release takes the host path (tests)
+  bool txcopy_force_fb_ = false;
+  // APM_D2H_KERNEL=1: the output lane's D2H of st / fs / db text by the engine's copy kernel
+  // (16-byte lanes, up to 1024 blocks, into the mapped pinned buffer) instead of hipMemcpyAsync
+  bool d2h_kernel_ = false;
+  void lane_d2h(void* h, const void* d, size_t n);  // APM_TXCOPY_FORCE_FALLBACK=1: every release takes the host path (tests)
   uint64_t sink_bytes_[N_OUT] = {0, 0, 0, 0, 0, 0, 0, 0};
   // K14 server rollup + exogenous context
   std::vector<double> h_ctx_;                    // [servers][CTX_FIELDS] (stats thread)

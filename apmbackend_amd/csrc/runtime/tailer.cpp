@@ -597,6 +597,22 @@ class Tailer {
       }
       if (pos > begin) chunks.emplace_back(f.file_id, begin, pos);
     }
+    // A busy log (the SOAP / app logs of a JVM) is most of a batch: one pread per file left a
+    // few threads copying megabytes each while the rest idled (7-8 GB/s whatever the pool size).
+    // Large reads are split into kSplit pieces, so the pool copies the page cache in parallel.
+    {
+      constexpr uint64_t kSplit = 1ull << 20;
+      std::vector<Part> split;
+      split.reserve(parts.size() + pos / kSplit + 1);
+      for (const Part& p : parts) {
+        if (p.len <= kSplit + kSplit / 2) { split.push_back(p); continue; }
+        for (uint64_t o = 0; o < p.len; o += kSplit) {
+          const uint64_t n = std::min(kSplit, p.len - o);
+          split.push_back({p.file, p.old, p.src + o, n, p.dst + o, p.add_nl && o + n == p.len});
+        }
+      }
+      parts.swap(split);
+    }
     std::atomic<int> short_reads{0};
     pool_.run(parts.size(), [&](size_t k) {
       const Part& p = parts[k];

@@ -161,6 +161,12 @@ def main():
         dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=600))
     from apmbackend_amd import _native
     blocking = args.blocking_sync == "on" or (args.blocking_sync == "auto" and local_world > n_dev)
+    if local_world > n_dev:
+        # ranks sharing a GPU: each process maps its streams onto GPU_MAX_HW_QUEUES hardware
+        # queues (4 by default); past the card's queue slots the scheduler time-slices whole
+        # processes (4 ranks x 4 queues: 34 ms steps).  Share 8 queues among the card's ranks.
+        per_gpu = -(-local_world // n_dev)
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(1, 8 // per_gpu)))
     if blocking:  # before torch creates the device's runtime state
         os.environ["APM_BLOCKING_SYNC"] = "1"
         _native.load(build_if_missing=False).set_blocking_sync(device)
@@ -412,7 +418,7 @@ def main():
                 "preset": args.preset,
                 "ring_dtype": args.ring,
             },
-            "n_ranks": world, "blocking_sync": blocking,
+            "n_ranks": world, "blocking_sync": blocking, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
             "collective": coll,
             "comm_nranks": comm_ranks,
             "lines_total": int(lines_total),

@@ -57,6 +57,28 @@ def test_line_longer_than_the_per_file_budget(tmp_path):
         assert len(_lines(got, i)) == 1000
 
 
+def test_large_reads_are_split_across_the_pool(tmp_path):
+    """A file contributing megabytes to one batch is read in 1 MiB pieces by the pool (one pread
+    per file left one thread copying most of the batch): the batch is byte-identical, lines
+    straddling the piece boundaries included, for every pool size."""
+    import random
+    rng = random.Random(3)
+    files = [tmp_path / f"f{i}.log" for i in range(3)]
+    want = []
+    for i, f in enumerate(files):
+        rows = [(b"%d-%07d " % (i, k)) + b"y" * rng.randint(0, 700) for k in range(12000 if i != 1 else 40)]
+        f.write_bytes(b"\n".join(rows) + b"\n")
+        want.append(rows)
+    assert files[0].stat().st_size > 3 << 20
+    for threads in (0, 1, 5):
+        t = N.Tailer("", 64 << 20, threads)
+        for i, f in enumerate(files):
+            t.add(str(f), i, True, i)
+        got = _drain(t)
+        for i in range(3):
+            assert _lines(got, i) == want[i], (threads, i)
+
+
 def test_line_longer_than_a_batch_is_skipped_and_counted(tmp_path):
     p = tmp_path / "a.log"
     p.write_bytes(b"x\n" + b"Y" * (300 << 10) + b"\nz\n")

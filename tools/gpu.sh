@@ -66,7 +66,7 @@ for task in "$@"; do
             python3 bench.py --steps 20 --warmup 5 ;;
     timeline) run "timeline_$n" 400 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$O/tl_$n" -o run -- \
                 python3 bench.py --steps 20 --warmup 5 ;;
-    pmc:*) c=${task#pmc:}; run "pmc_$n" 120 rocprofv3 --pmc ${c//,/ } --output-format csv -d "$O/pmc_$n" -o run -- \
+    pmc:*) c=${task#pmc:}; run "pmc_$n" 120 rocprofv3 --kernel-trace --pmc ${c//,/ } --output-format csv -d "$O/pmc_$n" -o run -- \
              python3 bench.py --steps 10 --warmup 3 ;;
     env:*) export "${task#env:}"; echo "[env] ${task#env:}" ;;
     py:*) run "py_$n" 600 python -u -m "${task#py:}" "$O" ;;
