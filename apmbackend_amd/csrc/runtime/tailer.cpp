@@ -395,6 +395,8 @@ class Tailer {
     d["overlong_lines_skipped"] = overlong_;
     d["unterminated_lines_closed"] = closed_partial_;
     d["read_threads"] = pool_.size() + 1;
+    d["plan_ms"] = plan_ms_;
+    d["read_ms"] = read_ms_;
     return d;
   }
   uint64_t bytes_read() const { return bytes_read_; }
@@ -525,6 +527,7 @@ class Tailer {
       pending_[id] = ends;
       return id;
     }
+    const auto tp0 = std::chrono::steady_clock::now();
     for (auto& f : files_) check_rotation(f);
     // budgets: starved files first (their whole next line), then a fair share for everyone
     const size_t nf = files_.size();
@@ -614,6 +617,7 @@ class Tailer {
       parts.swap(split);
     }
     std::atomic<int> short_reads{0};
+    const auto tp1 = std::chrono::steady_clock::now();
     pool_.run(parts.size(), [&](size_t k) {
       const Part& p = parts[k];
       const TailFile& f = files_[p.file];
@@ -648,6 +652,9 @@ class Tailer {
     if (pos) std::memset(dst + pos, 0, std::min<uint64_t>(64, cap + 64 - pos));
     bytes_read_ += pos;
     ++batches_;
+    const auto tp2 = std::chrono::steady_clock::now();
+    plan_ms_ += std::chrono::duration<double, std::milli>(tp1 - tp0).count();
+    read_ms_ += std::chrono::duration<double, std::milli>(tp2 - tp1).count();
     return id;
   }
 
@@ -718,6 +725,7 @@ class Tailer {
   std::map<int64_t, std::vector<std::pair<size_t, std::pair<uint64_t, uint64_t>>>> pending_;
   int64_t next_id_ = 0;
   uint64_t bytes_read_ = 0, batches_ = 0, rotations_ = 0, truncations_ = 0, overlong_ = 0, closed_partial_ = 0;
+  double plan_ms_ = 0, read_ms_ = 0;  // read_batch: planning (sizes, tail probes) / the parallel preads
   ReadPool pool_;
   int ino_fd_ = -1;
   std::set<std::string> dirs_;

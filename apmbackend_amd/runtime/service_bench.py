@@ -90,14 +90,23 @@ def _run(args, cfg, N, rank, root, IngestService):
     svc = IngestService(cfg, engine="native", files=paths, rank=0, world=1, server_of_path=srv_of, clock=log_clock)
     holder["svc"] = svc
 
+    loop_t = {"step_s": 0.0, "housekeeping_s": 0.0, "idle_s": 0.0, "idles": 0}
+
     def drain():
         # the service loop (IngestService.run): step + housekeeping (checkpoints on the log-time
         # clock, stat lines, sink ticks), idle wait when nothing was read
         while sum(o[1] for o in svc.tailer.offsets()) < written[0] or svc._held is not None:
+            ta = time.perf_counter()
             n = svc.step()
+            tb = time.perf_counter()
             svc._housekeeping()
+            tc = time.perf_counter()
+            loop_t["step_s"] += tb - ta
+            loop_t["housekeeping_s"] += tc - tb
             if n == 0:
                 svc._idle(0.001)
+                loop_t["idle_s"] += time.perf_counter() - tc
+                loop_t["idles"] += 1
 
     append(0, PRE)
     drain()
@@ -117,6 +126,8 @@ def _run(args, cfg, N, rank, root, IngestService):
     if args.trace:
         svc.eng.eng.set_trace(True)
     pf0 = dict(svc.perf)
+    tl0 = dict(loop_t)
+    ts0 = svc.tailer.stats()
     t0 = time.perf_counter()
     drain()
     svc.eng.eng.flush()
@@ -149,7 +160,9 @@ def _run(args, cfg, N, rank, root, IngestService):
         "writer_lanes": s1.get("lanes", 1),
         "sink_write_ms": s1.get("ms", 0.0) - s0.get("ms", 0.0),
         "sink_failures": s1.get("failures", 0),
-        "tailer": {k: tstats[k] for k in ("batches", "bytes_read", "read_threads")},
+        "tailer": {**{k: tstats[k] for k in ("batches", "bytes_read", "read_threads")},
+                   **{k + "_timed": tstats.get(k, 0) - ts0.get(k, 0) for k in ("batches", "bytes_read", "plan_ms", "read_ms")}},
+        "drain_loop": {k: round(loop_t[k] - tl0[k], 4) for k in loop_t},
         "ingest_GB_per_s": (m1["bytes"] - m0["bytes"]) / dt / 1e9,
         "loop": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in pf.items()},
         "mean_batch_MB": round(pf["bytes"] / max(pf["batches"], 1) / 1e6, 3),

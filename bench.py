@@ -166,7 +166,7 @@ def main():
         # queues (4 by default); past the card's queue slots the scheduler time-slices whole
         # processes (4 ranks x 4 queues: 34 ms steps).  Share 8 queues among the card's ranks.
         per_gpu = -(-local_world // n_dev)
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(1, 8 // per_gpu)))
+        os.environ["GPU_MAX_HW_QUEUES"] = str(max(1, 8 // per_gpu))
     if blocking:  # before torch creates the device's runtime state
         os.environ["APM_BLOCKING_SYNC"] = "1"
         _native.load(build_if_missing=False).set_blocking_sync(device)

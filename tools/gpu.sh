@@ -18,6 +18,7 @@
 #   preset:NAME        bench.py --preset NAME (config2, config4, firehose) 20/5
 #   service            bench.py --path service (production path, checkpoints on), 200 steps
 #   prof               rocprofv3 --kernel-trace --stats of bench.py 20/5
+#   profser            the same with every kernel serialised (AMD_SERIALIZE_KERNEL=3): isolated kernel times
 #   timeline           rocprofv3 --kernel-trace --memory-copy-trace (tools/gpu_timeline.py reads it)
 #   pmc:C1,C2,...      one rocprofv3 --pmc pass of bench.py 10/3 (keep within one pass's counter budget)
 #   service:T          the same with T tailer read threads
@@ -64,6 +65,8 @@ for task in "$@"; do
                  --service-dir /tmp/apm_svc --tail-read-threads "${task#service:}" ;;
     prof) run "prof_$n" 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$n" -o run -- \
             python3 bench.py --steps 20 --warmup 5 ;;
+    profser) AMD_SERIALIZE_KERNEL=3 run "profser_$n" 600 rocprofv3 --kernel-trace --stats --output-format csv \
+               -d "$O/profser_$n" -o run -- python3 bench.py --steps 10 --warmup 3 ;;
     timeline) run "timeline_$n" 400 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$O/tl_$n" -o run -- \
                 python3 bench.py --steps 20 --warmup 5 ;;
     pmc:*) c=${task#pmc:}; run "pmc_$n" 120 rocprofv3 --kernel-trace --pmc ${c//,/ } --output-format csv -d "$O/pmc_$n" -o run -- \
