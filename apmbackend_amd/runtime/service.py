@@ -192,7 +192,8 @@ class IngestService:
         self._slots: List[int] = []
         self._held = None  # batch taken from the read-ahead ring and handed to the engine as prefetch
         self._stopping = False
-        self.perf = {"wait_s": 0.0, "engine_s": 0.0, "outputs_s": 0.0, "batches": 0, "bytes": 0, "prefetched": 0}
+        self.perf = {"wait_s": 0.0, "engine_s": 0.0, "outputs_s": 0.0, "batches": 0, "bytes": 0, "prefetched": 0,
+                     "ckpt_s": 0.0, "ckpt_flush_s": 0.0, "ckpt_sink_snapshot_s": 0.0}
         self.batch_log = None  # a list to record every read-ahead batch (bytes, chunks) in (tests)
         self._drain_every_s = float(g.get("outputDrainMs", 250.0)) / 1000.0
         self._last_drain = 0.0
@@ -479,8 +480,12 @@ class IngestService:
             # of being waited for: ingest never waits for the DB writer, and a restore submits
             # exactly the flushes the sink's acknowledged watermark (its ack file) does not cover
             # (stream_insert_db.js persists its buffers on exit for the same reason, :222-244).
+            tf = time.perf_counter()
             self.native.flush()
+            ts = time.perf_counter()
             sink_meta = self._snapshot_sink()
+            self.perf["ckpt_flush_s"] = self.perf.get("ckpt_flush_s", 0.0) + ts - tf
+            self.perf["ckpt_sink_snapshot_s"] = self.perf.get("ckpt_sink_snapshot_s", 0.0) + time.perf_counter() - ts
         if self.qm is not None and not self.qm.wait_confirms(float(self.cfg["gpu"].get("confirmTimeoutSeconds", 60))):
             # offsets may only advance past data the broker has taken responsibility for
             log.warning("checkpoint postponed: the broker has not confirmed every publish yet")
@@ -493,6 +498,7 @@ class IngestService:
             log.warning("checkpoint skipped: the previous one is still being written")
             return None
         self.n_checkpoints += 1
+        self.perf["ckpt_s"] = self.perf.get("ckpt_s", 0.0) + time.perf_counter() - t0
         if wait:
             self.eng.checkpoint_wait()
         self.tailer.save_offsets(tp)
