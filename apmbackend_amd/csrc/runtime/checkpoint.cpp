@@ -994,7 +994,8 @@ std::string Engine::load_small_state(const std::string& path) {
 // writer thread then drains the staging area D2H on its own stream through a pinned bounce
 // buffer, writes + fsyncs the file, and appends it to the chain manifest (atomic rename).  A new
 // base starts a fresh chain (and retires the old files) after kMaxChain increments.
-int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& extra, bool force_base) {
+int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& extra, bool force_base,
+                                 std::function<void()> pre_commit) {
   {
     std::lock_guard<std::mutex> lk(ck_mu_);
     if (ck_busy_) { ++ck_skipped_; return -1; }
@@ -1011,6 +1012,7 @@ int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& e
   job->name = prefix.substr(prefix.rfind('/') + 1) + (base ? ".b" : ".i") + std::to_string(job->seq) + ".ckpt";
   job->path = dir_of(prefix) + "/" + job->name;
   job->extra = extra;
+  job->pre_commit = std::move(pre_commit);
   {
     BinWriter mw{BinWriter::Memory{}, ck_blob_hint_};
     write_small_sections(mw);
@@ -1045,6 +1047,7 @@ int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& e
       ck_all_dirty_ = true;
       const uint64_t bytes = save_state(job->path, extra);
       job->base = true;
+      if (job->pre_commit) job->pre_commit();
       finish_chain(job, bytes);
       ck_last_stall_ms_ = now_ms() - t0;
       ++ck_sync_fallbacks_;
@@ -1131,6 +1134,7 @@ void Engine::checkpoint_writer() {
       w.commit();
       fsync_dir(job->path);
       bytes = w.bytes();
+      if (job->pre_commit) job->pre_commit();
       finish_chain(job, bytes);
     } catch (const std::exception& e) {
       err = e.what();

@@ -287,6 +287,8 @@ struct PsqlWriter : Writer {
 }  // namespace
 
 class DbSink : public ByteSink {
+  struct Job;
+
  public:
   DbSink(int64_t limit, double max_wait_ms, std::vector<std::string> tables, std::vector<std::string> columns,
          const std::string& writer, const std::vector<std::string>& arg, uint64_t rotate_bytes, int encoders,
@@ -697,6 +699,83 @@ class DbSink : public ByteSink {
     return {acked_locked(), std::move(out)};
   }
 
+  // Asynchronous form of snapshot_pending for the checkpoint writer: the capture (ingest thread,
+  // sink lock held for microseconds) takes references to the unacknowledged flushes instead of
+  // copying them; snapshot_write (the engine's checkpoint writer thread) writes them to `path`
+  // -- the layout runtime/sinks.py write_sink_snapshot uses -- fsyncs, renames, and releases the
+  // references.  Until then the writer lanes keep those flushes' buffers (zero-copy engine
+  // buffers stay held).
+  struct Snapshot {
+    uint64_t acked = 0;
+    int64_t rows = 0;
+    std::vector<std::shared_ptr<Job>> jobs;
+    std::vector<uint8_t> enc;
+    bool released = false;
+  };
+  std::shared_ptr<Snapshot> snapshot_capture() {
+    auto snap = std::make_shared<Snapshot>();
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int t = 0; t < NT; ++t)
+      if (buf_[t].n > 0) submit_locked(t);
+    snap->jobs.reserve(live_.size());
+    for (auto& kv : live_) {
+      const std::shared_ptr<Job>& j = kv.second;
+      ++j->snap_refs;
+      snap->jobs.push_back(j);
+      snap->enc.push_back(j->ready ? 1 : 0);  // (a flush still in an encoder: its wire lines)
+      snap->rows += j->n;
+    }
+    snap->acked = acked_locked();
+    return snap;
+  }
+  void snapshot_release(Snapshot& snap) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (snap.released) return;
+    snap.released = true;
+    for (auto& j : snap.jobs)
+      if (--j->snap_refs == 0 && j->written) release_job_locked(*j);
+  }
+  void snapshot_write(Snapshot& snap, const std::string& path) {
+    const std::string tmp = path + ".tmp";
+    const int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    if (fd < 0) { snapshot_release(snap); throw std::runtime_error("sink snapshot: cannot create " + tmp); }
+    std::string head;
+    auto put = [&head](const void* p, size_t n) { head.append((const char*)p, n); };
+    bool ok = true;
+    auto flush_head = [&]() {
+      if (!head.empty() && !write_all(fd, head.data(), head.size())) ok = false;
+      head.clear();
+    };
+    const uint64_t count = snap.jobs.size();
+    put("APMSINK1", 8);
+    put(&count, 8);
+    for (size_t k = 0; k < snap.jobs.size() && ok; ++k) {
+      const Job& j = *snap.jobs[k];
+      // (read without the lock: snap_refs keeps the writer lanes and encoders off these fields)
+      const std::string_view d = snap.enc[k] ? j.data() : std::string_view(j.lines);
+      const uint64_t seq = j.seq, len = d.size();
+      const uint32_t ti = (uint32_t)j.type;
+      const uint8_t e = snap.enc[k];
+      const int64_t rows = j.n;
+      put(&seq, 8); put(&ti, 4); put(&e, 1); put(&rows, 8); put(&len, 8);  // struct "<QIBqQ"
+      if (len >= (1u << 16)) {
+        flush_head();
+        if (ok && !write_all(fd, d.data(), d.size())) ok = false;
+      } else {
+        head.append(d.data(), d.size());
+        if (head.size() >= (4u << 20)) flush_head();
+      }
+    }
+    flush_head();
+    snapshot_release(snap);
+    if (!ok || ::fdatasync(fd) != 0) {
+      ::close(fd);
+      throw std::runtime_error("sink snapshot: write failed: " + tmp);
+    }
+    ::close(fd);
+    if (std::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("sink snapshot: rename failed: " + path);
+  }
+
   void set_limit(int64_t limit, double max_wait_ms) {
     std::lock_guard<std::mutex> lk(mu_);
     limit_ = std::max<int64_t>(1, limit);
@@ -721,6 +800,10 @@ class DbSink : public ByteSink {
     std::shared_ptr<const void> hold;
     uint64_t floor = UINT64_MAX;  // smallest sequence whose rows this flush carries (re-buffered rows)
     bool taken = false, ready = false;
+    // a checkpoint snapshot is writing this flush's rows (snapshot_capture .. snapshot_write):
+    // the writer lane leaves its buffers alone and `written` defers their release
+    int snap_refs = 0;
+    bool written = false;
     std::string_view data() const { return ext.data() ? ext : std::string_view(encoded); }
   };
 
@@ -754,6 +837,25 @@ class DbSink : public ByteSink {
     buf_[t].n = 0;
     enqueue_locked(j);
     cv_.notify_all();
+  }
+
+  void release_job_locked(Job& j) {
+    give_spare_locked(std::move(j.encoded));
+    give_spare_locked(std::move(j.lines));
+    j.ext = std::string_view();
+    j.hold.reset();
+  }
+  static bool write_all(int fd, const char* p, size_t n) {
+    while (n) {
+      const ssize_t w = ::write(fd, p, n);
+      if (w < 0) {
+        if (errno == EINTR) continue;
+        return false;
+      }
+      p += w;
+      n -= (size_t)w;
+    }
+    return true;
   }
 
   // A flush goes to the next writer lane; lanes take their jobs in order.  Round robin over
@@ -828,10 +930,8 @@ class DbSink : public ByteSink {
           rows_ += j.n;
           bytes_ += (int64_t)j.data().size();
           ++flushes_;
-          give_spare_locked(std::move(j.encoded));
-          give_spare_locked(std::move(j.lines));
-          j.ext = std::string_view();
-          j.hold.reset();
+          if (j.snap_refs) { j.written = true; continue; }  // released by snapshot_write
+          release_job_locked(j);
         }
         ms_ = std::max(ms_, lane_ms_[lane] += dt);  // wall time of the busiest lane
         if (ok < run.size()) {
@@ -855,7 +955,7 @@ class DbSink : public ByteSink {
           for (size_t i = retry_from; i < run.size(); ++i) {
             if (as_copy) back.append(run[i]->data());
             else back += run[i]->lines;
-            run[i]->hold.reset();
+            if (!run[i]->snap_refs) run[i]->hold.reset();
             n += run[i]->n;
             rebuf_floor_[t] = std::min(rebuf_floor_[t], run[i]->floor);
           }
@@ -940,11 +1040,38 @@ struct SinkRoute : ByteSink {
   }
 };
 
+// A captured sink snapshot held by Python until the engine's checkpoint takes it; releases the
+// flushes' references if it is never written (busy checkpoint, failed write).
+struct SinkSnapHandle {
+  std::shared_ptr<DbSink> sink;
+  std::shared_ptr<DbSink::Snapshot> snap;
+  ~SinkSnapHandle() {
+    if (sink && snap) sink->snapshot_release(*snap);
+  }
+};
+
 }  // namespace apm
 
 void register_dbsink(py::module_& m) {
   using apm::DbSink;
   using apm::Engine;
+  using apm::SinkSnapHandle;
+  py::class_<SinkSnapHandle, std::shared_ptr<SinkSnapHandle>>(m, "SinkSnapshot")
+      .def_property_readonly("acked", [](const SinkSnapHandle& h) { return h.snap->acked; })
+      .def_property_readonly("jobs", [](const SinkSnapHandle& h) { return h.snap->jobs.size(); })
+      .def_property_readonly("rows", [](const SinkSnapHandle& h) { return h.snap->rows; })
+      .def("write", [](SinkSnapHandle& h, const std::string& path) {
+        py::gil_scoped_release rel;  // (synchronous form: tests, the sync checkpoint fallback)
+        h.sink->snapshot_write(*h.snap, path);
+      });
+  m.def("checkpoint_async_sink", [](Engine& e, const std::string& prefix, py::bytes extra, bool force_base,
+                                    std::shared_ptr<SinkSnapHandle> h, const std::string& path) {
+    // the engine's checkpoint writer writes the sink snapshot after the checkpoint file is
+    // durable and before the manifest names it (both or neither become the restore point)
+    std::string x = extra;
+    py::gil_scoped_release rel;
+    return e.checkpoint_async(prefix, x, force_base, [h, path]() { h->sink->snapshot_write(*h->snap, path); });
+  }, py::arg("engine"), py::arg("prefix"), py::arg("extra"), py::arg("force_base"), py::arg("snapshot"), py::arg("path"));
   py::class_<DbSink, std::shared_ptr<DbSink>>(m, "DbSink")
       .def(py::init<int64_t, double, std::vector<std::string>, std::vector<std::string>, std::string,
                     std::vector<std::string>, uint64_t, int, int, double>(),
@@ -973,6 +1100,15 @@ void register_dbsink(py::module_& m) {
       .def("is_encoded", &DbSink::is_encoded)
       .def("set_ack_file", &DbSink::set_ack_file)
       .def("acked", &DbSink::acked)
+      .def("snapshot_capture", [](std::shared_ptr<DbSink> s) {
+        auto h = std::make_shared<SinkSnapHandle>();
+        h->sink = s;
+        {
+          py::gil_scoped_release rel;
+          h->snap = s->snapshot_capture();
+        }
+        return h;
+      })
       .def("snapshot_pending", [](DbSink& s) {
         std::pair<uint64_t, std::vector<DbSink::PendingJob>> r;
         { py::gil_scoped_release rel; r = s.snapshot_pending(); }

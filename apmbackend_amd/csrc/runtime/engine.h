@@ -326,7 +326,8 @@ class Engine {
   // the calling thread pays for a consistent snapshot (small sections + dirty ring rows copied
   // D2D into HBM staging); a writer thread does the D2H, file write and fsync.  Returns the
   // checkpoint sequence number, or -1 when the previous one is still being written (skipped).
-  int64_t checkpoint_async(const std::string& prefix, const std::string& extra, bool force_base = false);
+  int64_t checkpoint_async(const std::string& prefix, const std::string& extra, bool force_base = false,
+                           std::function<void()> pre_commit = {});
   uint64_t checkpoint_wait();  // waits for the writer; rethrows its error
   CheckpointInfo checkpoint_info();
 
@@ -860,6 +861,9 @@ class Engine {
     std::string prefix, name, path, extra;
     MemBlob blob;                 // the small sections, serialised at the snapshot
     std::vector<Lag> lags;
+    // run by the writer thread after the file is durable, before the manifest names it (the DB
+    // sink's pending-flush snapshot): a throw fails this checkpoint
+    std::function<void()> pre_commit;
   };
   static constexpr int kMaxChain = 16;
   void checkpoint_quiesce(const char* what);

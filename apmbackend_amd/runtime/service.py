@@ -44,6 +44,15 @@ from . import logger as apmlog
 from .notifier import AlertNotifier
 from .sinks import DBInserter
 
+
+def _native_mod():
+    """The native extension if it is built (the sink snapshot path needs it), else None."""
+    try:
+        from .. import _native
+        return _native.load(build_if_missing=False)
+    except Exception:  # noqa: BLE001 - CPU containers without the .so
+        return None
+
 log = logging.getLogger("apm.service")
 
 RESTART_KEYS = ["apmConfigFilePath", "amqpConnectionString", "streamParseTransactions.appLogDirMaskPrefix",
@@ -365,7 +374,13 @@ class IngestService:
         acked, jobs = self.inserter.snapshot_pending()
         name = f"sink_pending.rank{self.rank}.{self.n_checkpoints + 1}.bin"
         write_sink_snapshot(os.path.join(self.ckpt_dir, name), jobs)
-        # the pending files of older checkpoints are no longer referenced (keep the previous one)
+        self._prune_sink_snapshots()
+        self.sink_pending_rows = sum(int(j[3]) for j in jobs)
+        return {"incarnation": self._sink_incarnation, "acked": acked, "pending": name, "jobs": len(jobs),
+                "rows": self.sink_pending_rows}
+
+    def _prune_sink_snapshots(self):
+        """The pending files of older checkpoints are no longer referenced (keep the previous one)."""
         for old in glob.glob(os.path.join(self.ckpt_dir, f"sink_pending.rank{self.rank}.*.bin")):
             try:
                 k = int(old.rsplit(".", 2)[-2])
@@ -376,9 +391,6 @@ class IngestService:
                     os.remove(old)
                 except OSError:
                     pass
-        self.sink_pending_rows = sum(int(j[3]) for j in jobs)
-        return {"incarnation": self._sink_incarnation, "acked": acked, "pending": name, "jobs": len(jobs),
-                "rows": self.sink_pending_rows}
 
     def _restore_sink(self):
         """After a restore: re-submit the checkpoint's pending flushes that the sink did not
@@ -473,6 +485,7 @@ class IngestService:
         # undelivered output goes out first so the checkpoint and the sinks agree
         self._drain_outputs()
         sink_meta = None
+        sink_snap = None  # (native sink: written by the engine's checkpoint writer, see below)
         if self.inserter is not None and self.mode == "inproc":
             # The engine's output lane feeds the native sink directly.  Every row of the batches this
             # checkpoint covers is handed over (flush: the engine pipeline, not the database), then
@@ -483,7 +496,20 @@ class IngestService:
             tf = time.perf_counter()
             self.native.flush()
             ts = time.perf_counter()
-            sink_meta = self._snapshot_sink()
+            N = _native_mod()
+            core = getattr(self.inserter, "core", None)
+            if core is not None and hasattr(core, "snapshot_capture") and hasattr(self.eng, "eng") \
+                    and N is not None and hasattr(N, "checkpoint_async_sink"):
+                # references to the unacknowledged flushes now (microseconds under the sink
+                # lock); the engine's checkpoint writer thread writes + fsyncs them after the
+                # checkpoint file and before the manifest names it -- ingest does not wait
+                sink_snap = core.snapshot_capture()
+                name = f"sink_pending.rank{self.rank}.{self.n_checkpoints + 1}.bin"
+                self.sink_pending_rows = int(sink_snap.rows)
+                sink_meta = {"incarnation": self._sink_incarnation, "acked": int(sink_snap.acked), "pending": name,
+                             "jobs": int(sink_snap.jobs), "rows": self.sink_pending_rows}
+            else:
+                sink_meta = self._snapshot_sink()
             self.perf["ckpt_flush_s"] = self.perf.get("ckpt_flush_s", 0.0) + ts - tf
             self.perf["ckpt_sink_snapshot_s"] = self.perf.get("ckpt_sink_snapshot_s", 0.0) + time.perf_counter() - ts
         if self.qm is not None and not self.qm.wait_confirms(float(self.cfg["gpu"].get("confirmTimeoutSeconds", 60))):
@@ -493,7 +519,13 @@ class IngestService:
         extra = json.dumps({"tail": json.loads(self.tailer.offsets_json()), "world": self.world,
                             "rank": self.rank, "servers": self.my_servers, "sink": sink_meta}).encode("utf-8")
         prefix = ck[:-len(".ckpt")]
-        seq = self.eng.checkpoint_async(prefix, extra)
+        if sink_snap is not None:
+            seq = _native_mod().checkpoint_async_sink(self.eng.eng, prefix, extra, False, sink_snap,
+                                                      os.path.join(self.ckpt_dir, sink_meta["pending"]))
+            del sink_snap  # (a skipped checkpoint releases the references here)
+            self._prune_sink_snapshots()
+        else:
+            seq = self.eng.checkpoint_async(prefix, extra)
         if seq < 0:
             log.warning("checkpoint skipped: the previous one is still being written")
             return None

@@ -198,3 +198,52 @@ def amqp_collect(url, queue, out):
     c.queue_declare(queue)
     c.consume(queue, lambda m: (out.append(m.body.decode()), c.ack(m.delivery_tag)))
     return c
+
+
+def _spool_rows(d):
+    import collections
+    import glob as g
+    rows = collections.defaultdict(collections.Counter)
+    for p in g.glob(os.path.join(d, "*.copy")):
+        table = os.path.basename(p).split(".")[0].rsplit("_lane", 1)[0]
+        with open(p) as f:
+            rows[table].update(l for l in f.read().split("\n") if l)
+    return rows
+
+
+def test_native_sink_checkpoint_snapshots_keep_every_row_once(tmp_path):
+    """VERDICT r3 #5 on the GPU service path: the native COPY sink (GPU-encoded fs / db rows,
+    2 writer lanes) with a checkpoint at every poll -- each one captures the sink's unacknowledged
+    flushes by reference and the engine's checkpoint writer persists them before the manifest
+    names it.  The spool holds exactly the rows of a run without checkpoints, and the named
+    snapshot files exist and parse."""
+    from apmbackend_amd.runtime import sinks
+    res = []
+    for ck in (False, True):
+        d = tmp_path / ("ck" if ck else "plain")
+        d.mkdir()
+        C, lines, mapping, sc = make_env(d)
+        gpu_cfg(C)
+        C["streamInsertDb"].update({"sink": "spool", "copySinkDir": str(d / "spool"), "writerLanes": 2,
+                                    "copySinkRotateBytes": 1 << 40})
+        if ck:
+            C["gpu"]["checkpointDir"] = str(d / "ckpt")
+            C["gpu"]["checkpointEverySeconds"] = 0
+        svc = IngestService(C, engine="native", files=sorted(mapping.values()), rank=0, world=1, server_of_path=srv_of)
+        assert svc.inserter.core is not None
+        run(svc, lines, mapping, sc)
+        if ck:
+            assert svc.n_checkpoints >= 3
+            svc.eng.checkpoint_wait()
+            extra = open(os.path.join(d, "ckpt", "engine.rank0.ckpt"), "rb").read()
+            assert extra.startswith(b"APMCHAIN")
+            snaps = [p for p in os.listdir(d / "ckpt") if p.startswith("sink_pending.")]
+            assert snaps
+            for p in snaps:
+                sinks.read_sink_snapshot(str(d / "ckpt" / p), 0)
+        svc.shutdown()
+        res.append(_spool_rows(str(d / "spool")))
+    a, b = res
+    assert set(a) == set(b) and sum(len(c) for c in a.values()) > 0
+    for t in a:
+        assert a[t] == b[t], t

@@ -460,7 +460,8 @@ def test_native_sink_psql_unacknowledged_copy_is_not_retried(tmp_path, monkeypat
     s.close()
 
 
-def test_sink_snapshot_watermark_restores_unwritten_rows_once(tmp_path, monkeypatch):
+@pytest.mark.parametrize("mode", ["copy", "capture"])
+def test_sink_snapshot_watermark_restores_unwritten_rows_once(tmp_path, monkeypatch, mode):
     """checkpoints snapshot the sink's unacknowledged flushes instead of draining
     it.  Flushes the writer acknowledged after the snapshot are skipped on restore (the ack file's
     watermark), flushes it never wrote are submitted again -- every row lands exactly once."""
@@ -480,15 +481,23 @@ def test_sink_snapshot_watermark_restores_unwritten_rows_once(tmp_path, monkeypa
     s.consume(("\n".join(lines) + "\n").encode())
     s.flush_all()
     s.drain()
-    acked_before, jobs = s.snapshot_pending()  # (no drain: the fs rows are back in their buffer)
-    assert sum(j[3] for j in jobs) == 10 and {j[1] for j in jobs} == {1}
     snap = str(tmp_path / "pending.bin")
-    sinks.write_sink_snapshot(snap, jobs)
+    if mode == "copy":
+        acked_before, jobs = s.snapshot_pending()  # (no drain: the fs rows are back in their buffer)
+        assert sum(j[3] for j in jobs) == 10 and {j[1] for j in jobs} == {1}
+        sinks.write_sink_snapshot(snap, jobs)
+        n_jobs = len(jobs)
+    else:
+        # the checkpoint writer's form: references taken now, written (and released) later
+        h = s.snapshot_capture()
+        assert h.rows == 10 and h.jobs >= 1
+        h.write(snap)
+        n_jobs = h.jobs
     s.close()  # "crash": the fs rows were never written
     acked = sinks.read_sink_ack(ack, 7)
     assert acked >= 0 and sinks.read_sink_ack(ack, 8) == -1  # another incarnation: unknown
     n, todo = sinks.read_sink_snapshot(snap, acked)
-    assert n == len(jobs) and sum(j[3] for j in todo) == 10
+    assert n == n_jobs and sum(j[3] for j in todo) == 10
     monkeypatch.setenv("FAKE_PSQL_FAIL", "")  # the restarted service: table back
     s2 = N.DbSink(1000, 1e9, tables, ["a", "b", "c", "d", "e"], "psql", fake, 0, 2)
     for _seq, ti, enc, rows, data in todo:
@@ -504,7 +513,8 @@ def test_sink_snapshot_watermark_restores_unwritten_rows_once(tmp_path, monkeypa
     assert open(out / "apm_stats.rows").read() == "".join(want["fs"])
 
 
-def test_sink_snapshot_of_acknowledged_flushes_restores_nothing(tmp_path):
+@pytest.mark.parametrize("mode", ["copy", "capture"])
+def test_sink_snapshot_of_acknowledged_flushes_restores_nothing(tmp_path, mode):
     from apmbackend_amd import _native
     N = _native.load(build_if_missing=False)
     tables = ["apm_tx", "apm_stats", "apm_alerts", "apm_jmx", "apm_fleet_stats"]
@@ -513,8 +523,13 @@ def test_sink_snapshot_of_acknowledged_flushes_restores_nothing(tmp_path):
     s.set_ack_file(ack, 11)
     lines = _wire_lines(40)
     s.consume(("\n".join(lines) + "\n").encode())
-    _acked, jobs = s.snapshot_pending()  # taken while the lanes may still be writing
-    sinks.write_sink_snapshot(str(tmp_path / "p.bin"), jobs)
+    if mode == "copy":
+        _acked, jobs = s.snapshot_pending()  # taken while the lanes may still be writing
+        sinks.write_sink_snapshot(str(tmp_path / "p.bin"), jobs)
+    else:
+        h = s.snapshot_capture()  # the lanes keep writing (and acknowledging) meanwhile
+        s.drain()
+        h.write(str(tmp_path / "p.bin"))  # written flushes released only now
     s.drain()  # everything gets written and acknowledged
     s.close()
     _n, todo = sinks.read_sink_snapshot(str(tmp_path / "p.bin"), sinks.read_sink_ack(ack, 11))
