@@ -326,16 +326,16 @@ PYBIND11_MODULE(_apm_native, m) {
         return d;
       })
       .def("lag_values", &Engine::lag_values)
-      .def("cache_stats", [](Engine& e) {
+      .def("cache_stats", [](Engine& e, bool drain) {
         std::vector<uint64_t> v;
-        { py::gil_scoped_release rel; v = e.cache_stats(); }
+        { py::gil_scoped_release rel; v = e.cache_stats(drain); }
         py::dict d;
         if (v.size() == 6) {
           d["slots"] = v[0]; d["occupied"] = v[1]; d["acct"] = v[2]; d["record"] = v[3]; d["partials"] = v[4];
           d["need"] = v[5];
         }
         return d;
-      })
+      }, py::arg("drain") = true)
       .def("process_batch",
            [](Engine& e, py::buffer buf, const std::vector<std::tuple<int32_t, uint64_t, uint64_t>>& chunks,
               double now) {
@@ -448,11 +448,13 @@ PYBIND11_MODULE(_apm_native, m) {
       .def("lane_cpus", &Engine::lane_cpus)
       .def("last_events", [](Engine& e) { return py::bytes(e.last_events()); })
       .def("warm_history", &Engine::warm_history)
-      .def("metrics", [](Engine& e) {
+      .def("metrics", [](Engine& e, bool drain) {
+        // drain=False: the counters as they stand (a batch or two behind), without draining the
+        // pipeline -- the periodic stat lines must not stall ingest
         EngineMetrics m;
-        { py::gil_scoped_release rel; m = e.metrics(); }
+        { py::gil_scoped_release rel; m = drain ? e.metrics() : e.metrics_nowait(); }
         return metrics_dict(m);
-      })
+      }, py::arg("drain") = true)
       .def("join_counters", [](Engine& e) { return counters_dict(e.join_counters()); })
       .def("n_series", &Engine::n_series)
       .def("n_services", &Engine::n_services)

@@ -26,6 +26,7 @@ struct StatsState {
   int32_t* nan_until = nullptr;  // [S] last bucket whose window can still see a NaN sample (INT32_MIN = none)
   int32_t* ord_list = nullptr;   // [max_tx] tx indices deferred to the ordered append
   int32_t* ord_n = nullptr;
+  uint32_t* ord_done = nullptr;  // blocks of the ordered append finished (the last one resets ord_n)
   int32_t keep = 0;              // windowSz + intervalBufferSz
   // host-mapped pinned [NSLOT]: spill_n after each append (the host's exact fill level, read once
   // the append's event completed; it sizes the spill area so no sample is ever dropped)

@@ -85,14 +85,16 @@ __global__ __launch_bounds__(1024) void k_bucket_append_ordered(const TxRec* __r
   __shared__ int32_t pos[ORD_TILE];
   __shared__ int32_t sp0[ORD_TILE];
   __shared__ int m_sh;
+  // Cells are partitioned over the blocks (cell % gridDim.x): a cell's samples, their order and
+  // their spill run all belong to one block, so the blocks sort and place independently (one
+  // block for every cell cost 60-70 us a call -- a serial tail on the stats stream).
   const int n_ord = *st.ord_n;
   if (n_ord == 0) {
     // every append of this call is done (stream order): publish the fill levels to the host
-    if (st.spill_snap && threadIdx.x < NSLOT) st.spill_snap[threadIdx.x] = st.spill_n[threadIdx.x];
+    if (blockIdx.x == 0 && st.spill_snap && threadIdx.x < NSLOT) st.spill_snap[threadIdx.x] = st.spill_n[threadIdx.x];
     return;
   }
-  __syncthreads();  // every thread has read the count: reset it for the next append
-  if (threadIdx.x == 0) *st.ord_n = 0;
+  const uint32_t G = gridDim.x, blk = blockIdx.x;
   const uint32_t span = hi - lo;
   const uint32_t R = n_ord <= ORD_TILE ? span : (uint32_t)ORD_TILE;
   for (uint32_t r0 = 0; r0 < span; r0 += R) {
@@ -103,7 +105,7 @@ __global__ __launch_bounds__(1024) void k_bucket_append_ordered(const TxRec* __r
       if (i - lo >= r0 && i - lo < r0 + R) {
         const TxRec r = tx[i];
         const uint32_t cell = (uint32_t)((r.end_ms / 10000) % NSLOT) * (uint32_t)st.S + (uint32_t)r.series;
-        key[atomicAdd(&m_sh, 1)] = ((unsigned long long)cell << 32) | i;
+        if (cell % G == blk) key[atomicAdd(&m_sh, 1)] = ((unsigned long long)cell << 32) | i;
       }
     }
     __syncthreads();
@@ -173,7 +175,19 @@ __global__ __launch_bounds__(1024) void k_bucket_append_ordered(const TxRec* __r
     __threadfence();
     __syncthreads();
   }
-  if (st.spill_snap && threadIdx.x < NSLOT) st.spill_snap[threadIdx.x] = st.spill_n[threadIdx.x];
+  // the last block to finish resets the count for the next append and publishes the fill levels
+  __shared__ bool last;
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(st.ord_done, 1u) == G - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) {
+    *st.ord_n = 0;
+    *st.ord_done = 0;
+  }
+  if (st.spill_snap && threadIdx.x < NSLOT) st.spill_snap[threadIdx.x] = atomicAdd(&st.spill_n[threadIdx.x], 0);
 }
 
 __global__ void k_clear_slot(StatsState st, int slot) {
@@ -725,7 +739,7 @@ void apm_bucket_append(const TxRec* d_tx, uint32_t lo, uint32_t hi, StatsState* 
   // ord_n is zero here: k_bucket_append_ordered resets it after reading
   hipLaunchKernelGGL(k_bucket_append, dim3((hi - lo + 255) / 256), dim3(256), 0, stream, d_tx, lo, hi, *st,
                      min_live_bucket);
-  if (st->ord_n) hipLaunchKernelGGL(k_bucket_append_ordered, dim3(1), dim3(1024), 0, stream, d_tx, lo, hi, *st);
+  if (st->ord_n) hipLaunchKernelGGL(k_bucket_append_ordered, dim3(64), dim3(1024), 0, stream, d_tx, lo, hi, *st);
 }
 
 void apm_nan_mark(const TxRec* d_tx, uint32_t n, StatsState* st, hipStream_t stream) {

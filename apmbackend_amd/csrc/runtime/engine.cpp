@@ -349,7 +349,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipMemset(d_nan_until_, 0x80, (size_t)S * 4));  // 0x80808080: far below any bucket
   ord_cap_ = std::max<int64_t>(cfg_.max_tx_per_batch, cfg_.max_lines);
   d_ord_list_ = (int32_t*)dmalloc((size_t)ord_cap_ * 4);
-  d_ord_n_ = (int32_t*)dmalloc(4);
+  d_ord_n_ = (int32_t*)dmalloc(8);  // [0] ord_n, [1] ordered-append blocks done
   d_nan_list_ = (int32_t*)dmalloc((size_t)S * 4);
   d_nan_n_ = d_big_n_ + 1;
   d_js_scratch_ = (int32_t*)dmalloc((size_t)JS_BLOCKS * kJsCap * 4);
@@ -753,11 +753,11 @@ void Engine::upload_series_tables(int32_t lo) {
   stage_done();
 }
 
-std::vector<uint64_t> Engine::cache_stats() {
-  flush();
+std::vector<uint64_t> Engine::cache_stats(bool drain) {
+  if (drain) flush();
   if (dj_) {
-    HIP_OK(hipStreamSynchronize(parse_stream_));
-    return dj_->cache_stats(watermark_);
+    if (drain) HIP_OK(hipStreamSynchronize(parse_stream_));
+    return dj_->cache_stats(watermark_);  // (ordered on the join stream)
   }
   return {};
 }
@@ -1618,6 +1618,7 @@ StatsState Engine::stats_state() const {
   st.nan_until = d_nan_until_;
   st.ord_list = d_ord_list_;
   st.ord_n = d_ord_n_;
+  st.ord_done = (uint32_t*)(d_ord_n_ + 1);
   st.keep = (int32_t)(cfg_.window + cfg_.buffer);
   st.spill_snap = hd_spill_snap_;
   return st;

@@ -394,6 +394,14 @@ class Engine {
   // Wait for the in-flight stats stage (process_batch returns while it still runs).
   void flush();
   EngineMetrics metrics() { flush(); return metrics_; }
+  EngineMetrics metrics_nowait() {
+    std::lock_guard<std::mutex> g(out_mu_);
+    EngineMetrics m = metrics_;
+    m.t_out_ms += t_out_ms_;
+    return m;
+  }
+  // (cache_stats(false): the join table as the join stream leaves it, without draining)
+  std::vector<uint64_t> cache_stats(bool drain);
   const std::vector<std::string>& servers() const { return servers_; }
   const std::vector<FileInfo>& files() const { return files_; }
   const std::vector<int>& lane_cpus() const { return lane_cpus_; }
@@ -406,7 +414,7 @@ class Engine {
   JoinCounters join_counters() const;
   // join-cache occupancy (device join: a reduction over the key table at the watermark clock;
   // host join: the shards' map sizes): {slots, occupied, acct, record, partials, need}
-  std::vector<uint64_t> cache_stats();
+  std::vector<uint64_t> cache_stats() { return cache_stats(true); }
 
   // events of the last batch (host copy) for kernel verification
   std::string last_events() const;

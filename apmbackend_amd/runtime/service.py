@@ -546,8 +546,11 @@ class IngestService:
         self.last_ckpt = self.clock()
         return ck
 
-    def _metrics(self) -> Dict[str, Any]:
-        m = self.native.metrics()
+    def _metrics(self, drain: bool = True) -> Dict[str, Any]:
+        try:
+            m = self.native.metrics(drain=drain)
+        except TypeError:  # engines without the non-draining form (CPU oracle)
+            m = self.native.metrics()
         return m if isinstance(m, dict) else {}
 
     def _on_signal(self, signum, frame):
@@ -649,8 +652,9 @@ class IngestService:
 
     def log_stats(self, dt_s: float):
         """Per statLogIntervalInSeconds: throughput, per-stage ms per batch, the ingest->alert
-        latency distribution of the interval's rollovers, HBM in use."""
-        m = self._metrics()
+        latency distribution of the interval's rollovers, HBM in use.  The counters are
+        read without draining the pipeline (a batch behind at most): a stat line never stalls ingest."""
+        m = self._metrics(drain=False)
         d = {k: m.get(k, 0) - self._m0.get(k, 0) for k in ("lines", "tx", "alerts", "rollovers", "batches")}
         self._m0 = m
         log.info("ENGINE lines/s: %.0f - tx/s: %.0f - rollovers: %d - alerts: %d - batches: %d - series: %s",
@@ -677,7 +681,7 @@ class IngestService:
             log.warning("ENGINE capacity exceeded (totals): %s -- raise gpu.maxSeries (the other structures grow)",
                      ", ".join(f"{k}={v}" for k, v in lost.items()))
         # CACHE_STATS (stream_parse_transactions.js:329-335): live entries of the join caches
-        cs = self.native.cache_stats() if hasattr(self.native, "cache_stats") else {}
+        cs = self.native.cache_stats(drain=False) if hasattr(self.native, "cache_stats") else {}
         if cs:
             log.info("CACHE_STATS acctCache: %d - recordCache: %d (%d open partials) - needNumRecordCache: %d "
                      "- key table %d / %d slots (load %.3f)", cs["acct"], cs["record"], cs["partials"], cs["need"],

@@ -18,6 +18,7 @@
 #   preset:NAME        bench.py --preset NAME (config2, config4, firehose) 20/5
 #   service            bench.py --path service (production path, checkpoints on), 200 steps
 #   prof               rocprofv3 --kernel-trace --stats of bench.py 20/5
+#   trace              bench.py 60/5 with the engine's Chrome trace (tools/trace_summary.py reads it)
 #   profser            the same with every kernel serialised (AMD_SERIALIZE_KERNEL=3): isolated kernel times
 #   timeline           rocprofv3 --kernel-trace --memory-copy-trace (tools/gpu_timeline.py reads it)
 #   pmc:C1,C2,...      one rocprofv3 --pmc pass of bench.py 10/3 (keep within one pass's counter budget)
@@ -65,6 +66,7 @@ for task in "$@"; do
                  --service-dir /tmp/apm_svc --tail-read-threads "${task#service:}" ;;
     prof) run "prof_$n" 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$n" -o run -- \
             python3 bench.py --steps 20 --warmup 5 ;;
+    trace) run "trace_$n" 300 python -u bench.py --steps 60 --warmup 5 --trace "$O/trace_$n.json" ;;
     profser) AMD_SERIALIZE_KERNEL=3 run "profser_$n" 600 rocprofv3 --kernel-trace --stats --output-format csv \
                -d "$O/profser_$n" -o run -- python3 bench.py --steps 10 --warmup 3 ;;
     timeline) run "timeline_$n" 400 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$O/tl_$n" -o run -- \
