@@ -123,8 +123,25 @@ struct OutT {
     for (int j = 9; j >= 0; --j)
       if (j < k) c((char)('0' + (v / P10[j]) % 10u));
   }
+  // exactly 8 digits (leading zeros), 32-bit constant divisions
+  __device__ __forceinline__ void u32_fixed8(uint32_t r) {
+    if (!W) { n += 8; return; }
+    constexpr uint32_t P10[8] = {1u, 10u, 100u, 1000u, 10000u, 100000u, 1000000u, 10000000u};
+#pragma unroll
+    for (int j = 7; j >= 0; --j) c((char)('0' + (r / P10[j]) % 10u));
+  }
+  // Above 2^32 -- the tx lines' epoch-ms timestamps and 16-digit account numbers, three per
+  // line -- one 64-bit division by 10^8 splits v into two 32-bit halves formatted in registers
+  // (the digit loop over 64-bit values into a local buffer lived in scratch memory).
   __device__ __forceinline__ void u(uint64_t v) {
     if (v <= 0xffffffffull) { u32((uint32_t)v); return; }
+    if (v < 100000000ull * 0xffffffffull) {
+      const uint64_t q = v / 100000000ull;
+      const uint32_t r = (uint32_t)(v - q * 100000000ull);
+      u32((uint32_t)q);
+      u32_fixed8(r);
+      return;
+    }
     char buf[24];
     const uint32_t k = text_u64(buf, v);
     s(buf, (int)k);
