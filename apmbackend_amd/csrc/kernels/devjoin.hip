@@ -1608,9 +1608,29 @@ __global__ void k_plan_totals(DJFormatArgs f) {
   f.counts->db_text_bytes = o.w;
 }
 
-// One tx wire line (TransactionEntry.toCSVString) through a line writer
+// One tx wire line (TransactionEntry.toCSVString) through a line writer: the head (names and
+// logId: copies) and the tail (numbers: formatting) -- k_write gives them to different waves.
+__device__ __forceinline__ uint32_t tx_head_len(const TxDev& t, const RawSvc& rs) {
+  return 3u + rs.srv_len + 1u + rs.norm_len + 1u + t.lid_len + 1u;
+}
+template <class O>
+__device__ __forceinline__ void tx_line_head(const DJFormatArgs& f, const TxDev& t, const RawSvc& rs, O& o);
+template <class O>
+__device__ __forceinline__ void tx_line_tail(const TxDev& t, const RawSvc& rs, O& o, bool& inexact) {
+  o.jsnum(t.acct, inexact); o.c('|');
+  o.jsnum(t.start, inexact); o.c('|');
+  o.jsnum(t.end, inexact); o.c('|');
+  o.jsnum(t.elapsed, inexact); o.c('|');
+  o.c(rs.toplevel ? 'Y' : 'N');
+  o.c('\n');
+}
 template <class O>
 __device__ __forceinline__ void tx_line(const DJFormatArgs& f, const TxDev& t, const RawSvc& rs, O& o, bool& inexact) {
+  tx_line_head(f, t, rs, o);
+  tx_line_tail(t, rs, o, inexact);
+}
+template <class O>
+__device__ __forceinline__ void tx_line_head(const DJFormatArgs& f, const TxDev& t, const RawSvc& rs, O& o) {
   o.lit("tx|");
   o.s(f.names + rs.srv_off, rs.srv_len);
   o.c('|');
@@ -1630,12 +1650,6 @@ __device__ __forceinline__ void tx_line(const DJFormatArgs& f, const TxDev& t, c
     }
   }
   o.c('|');
-  o.jsnum(t.acct, inexact); o.c('|');
-  o.jsnum(t.start, inexact); o.c('|');
-  o.jsnum(t.end, inexact); o.c('|');
-  o.jsnum(t.elapsed, inexact); o.c('|');
-  o.c(rs.toplevel ? 'Y' : 'N');
-  o.c('\n');
 }
 
 // The lines of consecutive tx are adjacent in the ring (and in the tx / db text).  One 64-lane
@@ -1645,14 +1659,16 @@ __device__ __forceinline__ void tx_line(const DJFormatArgs& f, const TxDev& t, c
 // storing into 64 lines ~95 B apart.  A block whose lines do not fit the stage (logIds of kB)
 // writes its lines to the ring directly.  (The batch's ring region never wraps: ring_reserve.)
 constexpr int TXW_LINES = 64;
+constexpr int TXW_THREADS = 2 * TXW_LINES;  // wave 0: the lines' heads, wave 1: their tails
 constexpr uint32_t TXW_LDS = 8192;
 __device__ __forceinline__ void write_one(const DJFormatArgs& f, const TxDev& t, uint32_t i, char* staged_line);
+__device__ __forceinline__ void write_tail(const DJFormatArgs& f, const TxDev& t, uint32_t i, char* staged_line);
 
 __device__ __forceinline__ void txw_copy_out(const char* __restrict__ lds, char* __restrict__ out, uint32_t g0,
                                              uint32_t g1) {
   const uint32_t a0 = g0 & ~3u;
   const uint32_t nd = (g1 - a0 + 3) / 4;
-  for (uint32_t d = threadIdx.x; d < nd; d += TXW_LINES) {
+  for (uint32_t d = threadIdx.x; d < nd; d += blockDim.x) {
     const uint32_t ga = a0 + 4 * d;
     if (ga >= g0 && ga + 4 <= g1) {
       *reinterpret_cast<uint32_t*>(out + ga) = *reinterpret_cast<const uint32_t*>(lds + 4 * d);
@@ -1663,11 +1679,12 @@ __device__ __forceinline__ void txw_copy_out(const char* __restrict__ lds, char*
   }
 }
 
-__global__ __launch_bounds__(TXW_LINES) void k_write(DJFormatArgs f) {
+__global__ __launch_bounds__(TXW_THREADS) void k_write(DJFormatArgs f) {
   __shared__ __align__(16) char stage[TXW_LDS];
   const uint32_t j0 = blockIdx.x * TXW_LINES;
   const uint32_t j1 = min(f.n_out, j0 + TXW_LINES);
-  const uint32_t i = j0 + threadIdx.x;
+  const bool tail = threadIdx.x >= (unsigned)TXW_LINES;  // uniform per wave
+  const uint32_t i = j0 + (threadIdx.x & (TXW_LINES - 1));
   const U4* offs = reinterpret_cast<const U4*>(f.offs);
   // physical ring offsets of the block's byte range (contiguous: the region does not wrap)
   const uint64_t rb = f.ring_base & (f.ring_cap - 1);
@@ -1675,7 +1692,11 @@ __global__ __launch_bounds__(TXW_LINES) void k_write(DJFormatArgs f) {
   const bool staged = p1 - (p0 & ~3u) <= TXW_LDS;  // uniform across the block
   if (i < j1) {
     const TxDev t = f.out[i];
-    if (t.raw >= 0) write_one(f, t, i, staged ? stage + ((uint32_t)(rb + offs[i].x) - (p0 & ~3u)) : nullptr);
+    char* const sl = staged ? stage + ((uint32_t)(rb + offs[i].x) - (p0 & ~3u)) : nullptr;
+    if (t.raw >= 0) {
+      if (tail) write_tail(f, t, i, sl);
+      else write_one(f, t, i, sl);
+    }
   }
   if (staged) {
     __syncthreads();
@@ -1683,6 +1704,19 @@ __global__ __launch_bounds__(TXW_LINES) void k_write(DJFormatArgs f) {
   }
 }
 
+// the numbers of the ring line, after its head (the other wave of the block writes the head)
+__device__ __forceinline__ void write_tail(const DJFormatArgs& f, const TxDev& t, uint32_t i, char* staged_line) {
+  const U4 o = reinterpret_cast<const U4*>(f.offs)[i];
+  const uint64_t vpos = f.ring_base + o.x;
+  char* p0 = staged_line ? staged_line : f.ring + (vpos & (f.ring_cap - 1));
+  const RawSvc rs = f.raw[t.raw];
+  bool inexact = false;
+  OutT<true> w(p0 + tx_head_len(t, rs));
+  tx_line_tail(t, rs, w, inexact);
+  w.finish();
+}
+
+// the head of the ring line, the tx / db stream copies of the whole line, the stats record
 __device__ __forceinline__ void write_one(const DJFormatArgs& f, const TxDev& t, uint32_t i, char* staged_line) {
   const U4 o = reinterpret_cast<const U4*>(f.offs)[i];
   const U4 l = reinterpret_cast<const U4*>(f.lens)[i];
@@ -1692,7 +1726,7 @@ __device__ __forceinline__ void write_one(const DJFormatArgs& f, const TxDev& t,
   bool inexact = false;
   {
     OutT<true> w(p0);
-    tx_line(f, t, rs, w, inexact);
+    tx_line_head(f, t, rs, w);
     w.finish();
   }
   const uint32_t len = l.x;
@@ -2263,7 +2297,7 @@ int apm_dj_plan(DJFormatArgs* f, hipStream_t s) {
 
 int apm_dj_write(DJFormatArgs* f, uint32_t n_stats, hipStream_t s) {
   const uint32_t n = f->n_out;
-  if (n) hipLaunchKernelGGL(k_write, dim3((n + TXW_LINES - 1) / TXW_LINES), dim3(TXW_LINES), 0, s, *f);
+  if (n) hipLaunchKernelGGL(k_write, dim3((n + TXW_LINES - 1) / TXW_LINES), dim3(TXW_THREADS), 0, s, *f);
   if (!n_stats) return 0;
   size_t need = 0;
   HIP_OK(rocprim::inclusive_scan(nullptr, need, f->tx_bucket, f->tx_bmax, (size_t)n_stats,
