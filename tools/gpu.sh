@@ -23,6 +23,7 @@
 #   timeline           rocprofv3 --kernel-trace --memory-copy-trace (tools/gpu_timeline.py reads it)
 #   pmc:C1,C2,...      one rocprofv3 --pmc pass of bench.py 10/3 (keep within one pass's counter budget)
 #   service:T          the same with T tailer read threads
+#   benchx:A,B         bench.py 20/5 with extra arguments A B (commas become spaces)
 #   env:K=V            export K=V for the following tasks (A/B switches)
 #   py:MODULE          python -m MODULE (diagnostics under tools/)
 set -u
@@ -54,6 +55,7 @@ for task in "$@"; do
     smoke) run "smoke" 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run "bench_$n" 300 python -u bench.py --steps 20 --warmup 5 ;;
     bench:*) run "bench_$n" 400 python -u bench.py --steps "${task#bench:}" --warmup 5 ;;
+    benchx:*) a=${task#benchx:}; run "benchx_$n" 300 python -u bench.py --steps 20 --warmup 5 ${a//,/ } ;;
     bench200) run "bench200_$n" 400 python -u bench.py --steps 200 --warmup 5 ;;
     ranks:*)
       w=${task#ranks:}
