@@ -96,7 +96,22 @@ __global__ __launch_bounds__(1024) void k_bucket_append_ordered(const TxRec* __r
   }
   const uint32_t G = gridDim.x, blk = blockIdx.x;
   const uint32_t span = hi - lo;
-  const uint32_t R = n_ord <= ORD_TILE ? span : (uint32_t)ORD_TILE;
+  // this block's entries: all in one pass when they fit the LDS tile (nearly always: ~n_ord / G),
+  // else in tx-index ranges of ORD_TILE (a range holds at most ORD_TILE entries)
+  if (threadIdx.x == 0) m_sh = 0;
+  __syncthreads();
+  {
+    int mine = 0;
+    for (int j = threadIdx.x; j < n_ord; j += blockDim.x) {
+      const TxRec r = tx[st.ord_list[j]];
+      const uint32_t cell = (uint32_t)((r.end_ms / 10000) % NSLOT) * (uint32_t)st.S + (uint32_t)r.series;
+      mine += cell % G == blk;
+    }
+    if (mine) atomicAdd(&m_sh, mine);
+  }
+  __syncthreads();
+  const uint32_t R = m_sh <= ORD_TILE ? span : (uint32_t)ORD_TILE;
+  __syncthreads();
   for (uint32_t r0 = 0; r0 < span; r0 += R) {
     if (threadIdx.x == 0) m_sh = 0;
     __syncthreads();

@@ -1125,8 +1125,20 @@ void Engine::process_batch_dev_tail(ParseSlot& ps, double t0, double now_overrid
     });
   };
   static const bool ahead_on = [] { const char* e = std::getenv("APM_PREPASS_AHEAD"); return !e || e[0] != '0'; }();
+  // while this batch's join kernels run: the next batch's parse / pre-pass (ahead lane) and the
+  // previous batches' fleet exchange (collective, enqueued on the coll stream in round order --
+  // before this batch's lock-step all-reduce, as when it ran after the previous hand-off)
+  const bool do_ahead = prefetched_ && ahead_on;
+  const std::function<void()> meanwhile = [this, &ahead, do_ahead]() {
+    if (do_ahead) ahead();
+    if (coll_ && fleet_due_ > fleet_rounds_) {
+      const double tf = now_ms();
+      fleet_exchange_upto(fleet_due_);
+      trace_event("fleet.exchange", tf, now_ms(), 0);
+    }
+  };
   dj_->run(k, ps.hb, ps.n_events, ps.n_bytes, clock, batch_no_, want(OUT_TRANSACTIONS), want(OUT_AUDIT_DB), b, par,
-           prefetched_ && ahead_on ? &ahead : nullptr);
+           &meanwhile);
   const double t2 = now_ms();
   metrics_.t_join_ms += t2 - t1;
   metrics_.t_join_shards_ms += t2 - t1;
@@ -1157,8 +1169,7 @@ void Engine::process_batch_dev_tail(ParseSlot& ps, double t0, double now_overrid
   post_stats_dev(std::move(b), t0, lockstep_ ? sync_latest_ : INT64_MIN);
   const double tp1 = now_ms();
   trace_event("post", tp0, tp1, 0);
-  if (coll_) fleet_exchange_upto(fleet_posted_ - 1);
-  trace_event("fleet.exchange", tp1, now_ms(), 0);
+  if (coll_) fleet_due_ = fleet_posted_ - 1;  // exchanged during the next batch's join (see above)
   metrics_.t_total_ms += now_ms() - t0;
   ++batch_no_;
 }

@@ -544,6 +544,9 @@ class Engine {
   std::vector<int64_t> shard_maxb_;  // per-shard newest bucket (one cache line each), lock-step clock
   uint64_t fleet_rounds_ = 0;  // exchanges issued (ingest thread)
   uint64_t fleet_posted_ = 0;  // batches posted since fleet_init (ingest thread)
+  // device-join batches defer their fleet exchange (rounds < fleet_due_) into the next batch's
+  // join-kernel window; every later caller exchanges up to fleet_posted_ anyway
+  uint64_t fleet_due_ = 0;
   uint64_t fleet_packed_ = 0;  // batches packed (stats thread)
   // ---- node-wide alert cooldown.  The stats thread queues this rank's candidates (with their
   // al-row payload, formatted while the rollover's stats are current); the ingest thread
