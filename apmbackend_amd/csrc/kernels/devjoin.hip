@@ -42,6 +42,16 @@ constexpr int TB = 256;
 // the join's critical path, profiles/r3_*); onesweep does 3 digit passes.
 using OpSortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
                                              rocprim::default_config, 0>;
+// APM_OPSORT=11: 11-bit digits -- two passes for the ~20-22 key bits instead of three
+using OpSortCfg11 = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>, 11,
+                                        rocprim::block_radix_rank_algorithm::match>,
+    0>;
+static bool opsort11() {
+  static const bool v = [] { const char* e = std::getenv("APM_OPSORT"); return e && e[0] == '1' && e[1] == '1'; }();
+  return v;
+}
 
 __device__ __forceinline__ uint32_t grid_n(uint32_t n) { return (n + TB - 1) / TB; }
 
@@ -2127,6 +2137,13 @@ size_t apm_dj_tmp_bytes(uint32_t max_ev, uint32_t max_out, int table_bits) {
                                  (hipStream_t)0));
   HIP_OK(rocprim::radix_sort_pairs<OpSortCfg>(nullptr, b, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                    (uint32_t*)nullptr, n, 0, table_bits + 2, (hipStream_t)0));
+  {
+    size_t b11 = 0;
+    HIP_OK(rocprim::radix_sort_pairs<OpSortCfg11>(nullptr, b11, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                  (uint32_t*)nullptr, (uint32_t*)nullptr, n, 0, table_bits + 2,
+                                                  (hipStream_t)0));
+    b = std::max(b, b11);
+  }
   HIP_OK(rocprim::radix_sort_pairs(nullptr, c, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
                                    (uint32_t*)nullptr, n, 0, 64, (hipStream_t)0));
   HIP_OK(rocprim::exclusive_scan(nullptr, d, (U4*)nullptr, (U4*)nullptr, U4{0, 0, 0, 0}, (size_t)max_out + 1, U4Plus(),
@@ -2224,6 +2241,12 @@ int apm_dj_join(DJArgs* a, hipStream_t s) {
       HIP_OK(rocprim::radix_sort_pairs(a->tmp, need, a->op_slot, a->op_slot_sorted, a->op_idx, a->op_idx_sorted,
                                        (size_t)n, 0, a->table_bits + 2, s));
       dj_check(s, "rocprim_radix_sort_pairs");
+    } else if (opsort11()) {
+      HIP_OK(rocprim::radix_sort_pairs<OpSortCfg11>(nullptr, need, a->op_slot, a->op_slot_sorted, a->op_idx,
+                                                    a->op_idx_sorted, (size_t)n, 0, a->table_bits + 2, s));
+      if (need > a->tmp_bytes) return -1;
+      HIP_OK(rocprim::radix_sort_pairs<OpSortCfg11>(a->tmp, need, a->op_slot, a->op_slot_sorted, a->op_idx,
+                                                    a->op_idx_sorted, (size_t)n, 0, a->table_bits + 2, s));
     } else {
       HIP_OK(rocprim::radix_sort_pairs<OpSortCfg>(nullptr, need, a->op_slot, a->op_slot_sorted, a->op_idx,
                                                   a->op_idx_sorted, (size_t)n, 0, a->table_bits + 2, s));
