@@ -251,9 +251,30 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     const char* e = std::getenv("APM_BLOCKING_SYNC");
     if (e && e[0] == '1') (void)hipSetDeviceFlags(hipDeviceScheduleBlockingSync);
   }
-  HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-  HIP_OK(hipStreamCreateWithFlags(&parse_stream_, hipStreamNonBlocking));
-  HIP_OK(hipStreamCreateWithFlags(&out_stream_, hipStreamNonBlocking));
+  {
+    // The device join's kernels are the ingest thread's critical chain, and most of them are
+    // small, latency-bound grids: sharing every SIMD with the parse / stats / output kernels of
+    // the other streams stretched them 5-10x in the bench timeline (k_aud_walk 47 us alone,
+    // ~190 us co-running).  APM_CU_RESERVE=N keeps N CUs (every (CUs/N)-th, so spread over the
+    // XCDs) out of those streams' CU masks; the join stream keeps all CUs.
+    const char* e = std::getenv("APM_CU_RESERVE");
+    int n_cu = 0;
+    HIP_OK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, cfg_.device));
+    const int reserve = e ? std::atoi(e) : 0;
+    if (reserve > 0 && reserve < n_cu / 2) {
+      const int stride = n_cu / reserve;
+      std::vector<uint32_t> mask((size_t)(n_cu + 31) / 32, 0u);
+      for (int c = 0; c < n_cu; ++c)
+        if (c % stride != stride - 1) mask[(size_t)c / 32] |= 1u << (c % 32);
+      for (hipStream_t* s : {&stream_, &parse_stream_, &out_stream_})
+        HIP_OK(hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data()));
+      cu_reserved_ = reserve;
+    } else {
+      HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+      HIP_OK(hipStreamCreateWithFlags(&parse_stream_, hipStreamNonBlocking));
+      HIP_OK(hipStreamCreateWithFlags(&out_stream_, hipStreamNonBlocking));
+    }
+  }
   HIP_OK(hipEventCreateWithFlags(&ev_a_, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&ev_b_, hipEventDisableTiming));
   const int32_t S = cfg_.max_series;

@@ -1092,6 +1092,7 @@ class Engine {
   // APM_D2H_KERNEL=1: the output lane's D2H of st / fs / db text by the engine's copy kernel
   // (16-byte lanes, up to 1024 blocks, into the mapped pinned buffer) instead of hipMemcpyAsync
   bool d2h_kernel_ = false;
+  int cu_reserved_ = 0;  // CUs kept out of the parse / stats / output streams (APM_CU_RESERVE)
   void lane_d2h(void* h, const void* d, size_t n);  // APM_TXCOPY_FORCE_FALLBACK=1: every release takes the host path (tests)
   uint64_t sink_bytes_[N_OUT] = {0, 0, 0, 0, 0, 0, 0, 0};
   // K14 server rollup + exogenous context
