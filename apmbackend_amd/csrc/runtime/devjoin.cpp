@@ -790,9 +790,11 @@ void DeviceJoin::ensure_capacity(uint32_t n_ev, uint64_t bytes, double now) {
     live_pending_ = false;
   }
   if ((keys_live_ + keys_since_rebuild_ + n_ev) * 2 > table_cap_) {
-    // steady state: the live count after the previous rebuild predicts this one's with room to
-    // spare -- rebuild in stream order; otherwise (growth may be due) wait for the count
-    if (table_rebuilds_ > 0 && (keys_live_ + keys_live_ / 4 + n_ev) * 2 <= table_cap_) {
+    // steady state: the live count after the previous rebuild (+1/8) and this batch's ops keep the
+    // table at most 5/8 full -- rebuild in stream order; otherwise (growth may be due) wait for
+    // the count.  (A table a little past half full only probes longer; the count read at the
+    // next check grows it if the live keys really grew.)
+    if (table_rebuilds_ > 0 && (keys_live_ + keys_live_ / 8 + n_ev) * 8 <= (uint64_t)table_cap_ * 5) {
       rebuild_table_async(now);
       return ensure_rest(n_ev, bytes);
     }
