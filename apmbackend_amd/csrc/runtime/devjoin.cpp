@@ -194,6 +194,7 @@ DeviceJoin::DeviceJoin(const DevJoinConfig& cfg, Dictionary* dict, const std::ve
 
 DeviceJoin::~DeviceJoin() {
   hipStreamSynchronize(stream_);
+  if (live_ev_) hipEventDestroy(live_ev_);
   for (auto& s : sl_) {
     hipHostFree(s.h_host_ev); hipHostFree(s.h_host_idx); hipHostFree(s.h_n_host);
     hipHostFree(s.h_chunk_next); hipHostFree(s.h_chunk_first);
@@ -671,6 +672,7 @@ void DeviceJoin::rebuild_table(double now, uint32_t new_cap) {
   HIP_OK(hipStreamSynchronize(st));
   if (same) {
     d_table_spare_ = d_table_;
+    spare_clean_ = false;
   } else {
     dfree(d_table_, (size_t)table_cap_ * sizeof(KeyState));
     if (d_table_spare_) dfree(d_table_spare_, (size_t)table_cap_ * sizeof(KeyState));
@@ -693,17 +695,37 @@ void DeviceJoin::rebuild_table(double now, uint32_t new_cap) {
 // stalled the ingest thread ~0.5 ms every ~32 batches at the headline rate: the p99 step.)
 void DeviceJoin::rebuild_table_async(double now) {
   hipStream_t st = stream_;
-  KeyState* fresh = d_table_spare_ ? d_table_spare_ : (KeyState*)dmalloc((size_t)table_cap_ * sizeof(KeyState));
-  HIP_OK(hipMemsetAsync(fresh, 0, (size_t)table_cap_ * sizeof(KeyState), st));
+  KeyState* fresh = d_table_spare_;
+  if (!fresh) fresh = (KeyState*)dmalloc((size_t)table_cap_ * sizeof(KeyState));  // (zeroed)
+  else if (!spare_clean_) HIP_OK(hipMemsetAsync(fresh, 0, (size_t)table_cap_ * sizeof(KeyState), st));
   HIP_OK(hipMemsetAsync(d_live_, 0, 8, st));
   apm_dj_rebuild(d_table_, table_cap_, fresh, table_cap_ - 1, d_arena_, cfg_.arena_cap, now, d_counts_, d_live_,
                  d_pool_, d_pool_ring_, pool_n_ - 1, st);
   HIP_OK(hipMemcpyAsync(h_live_, d_live_, 8, hipMemcpyDeviceToHost, st));
-  d_table_spare_ = d_table_;  // (cleared by the next rebuild, after this batch's kernels)
+  if (!live_ev_) HIP_OK(hipEventCreateWithFlags(&live_ev_, hipEventDisableTiming));
+  HIP_OK(hipEventRecord(live_ev_, st));
+  d_table_spare_ = d_table_;  // (zeroed later, in an idle gap of the join stream)
+  spare_clean_ = false;
   d_table_ = fresh;
   keys_since_rebuild_ = 0;
   live_pending_ = true;
   ++table_rebuilds_;
+}
+
+// After a batch's last sync the join stream idles while the host finishes the batch (hand-off,
+// clocks) and starts the next one: the key table's upkeep runs there instead of in front of the
+// next batch's kernels -- the rebuild when the next batch (estimated as large as this one) would
+// trigger it, else zeroing the spare table so a later rebuild skips its memset.  The clock is
+// this batch's: only entries expired at it are dropped (later expiries are checked by the kernels).
+void DeviceJoin::idle_upkeep(double now, uint32_t n_next) {
+  if (live_pending_) return;  // a rebuild's count is still unread
+  if ((keys_live_ + keys_since_rebuild_ + n_next) * 2 > table_cap_ && table_rebuilds_ > 0 &&
+      (keys_live_ + keys_live_ / 8 + n_next) * 8 <= (uint64_t)table_cap_ * 5) {
+    rebuild_table_async(now);
+  } else if (d_table_spare_ && !spare_clean_) {
+    HIP_OK(hipMemsetAsync(d_table_spare_, 0, (size_t)table_cap_ * sizeof(KeyState), stream_));
+    spare_clean_ = true;
+  }
 }
 
 // Need entries at virtual [lo, arena_head_) move to the same virtual slots of a bigger ring; the
@@ -785,7 +807,8 @@ void DeviceJoin::grow_pool(uint64_t need_free) {
 
 void DeviceJoin::ensure_capacity(uint32_t n_ev, uint64_t bytes, double now) {
   // key table: every op of the batch may claim a new key
-  if (live_pending_) {  // the previous in-order rebuild's count (its batch synchronised the stream)
+  if (live_pending_) {  // the in-order rebuild's count (queued at the previous batch's end)
+    HIP_OK(hipEventSynchronize(live_ev_));
     keys_live_ = *h_live_;
     live_pending_ = false;
   }
@@ -1099,6 +1122,7 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
   tx_ += c3.n_out;
   tx_db_ += c3.n_db;
   aud_cur_ ^= 1;  // the next batch reads what this one carried
+  idle_upkeep(now, n_ev);
   phase_t[8] = clock_ms();
 }
 

@@ -187,6 +187,7 @@ class DeviceJoin {
   void rebuild_table(double now, uint32_t new_cap);
   void rebuild_table_async(double now);
   void ensure_rest(uint32_t n_ev, uint64_t bytes);  // ensure_capacity after the key table
+  void idle_upkeep(double now, uint32_t n_next);    // end of a batch: table upkeep while the host works
   void grow_arena(uint32_t new_cap, uint64_t lo);
   void grow_pool(uint64_t need_free);
   uint64_t pool_avail(bool exact);
@@ -241,6 +242,8 @@ class DeviceJoin {
   int table_bits_ = 0;
   uint64_t keys_since_rebuild_ = 0, keys_live_ = 0;
   bool live_pending_ = false;  // an in-order rebuild's live count is on its way to h_live_
+  hipEvent_t live_ev_ = nullptr;  // recorded after that count's D2H
+  bool spare_clean_ = false;   // d_table_spare_ is zeroed (the next rebuild skips its memset)
   uint8_t* d_pool_ = nullptr;          // chain blocks
   uint32_t* d_pool_ring_ = nullptr;    // free-index ring
   uint32_t pool_n_ = 0;                // blocks (power of two)
