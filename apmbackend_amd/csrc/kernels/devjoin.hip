@@ -332,41 +332,6 @@ __device__ bool aud_fields(const Event& e, const uint8_t* __restrict__ bytes, in
   return true;
 }
 
-// ------------------------------------------------------------------------ host-event selection
-// Events the GPU does not resolve alone: lines the parser deferred (non-ASCII, exotic numbers /
-// timestamps), logIds with inner brackets, account strings parseInt cannot decide in 64 bits,
-// and audit lines whose fields aud_fields cannot extract (the host sends those as HOP_AUD).
-__device__ bool needs_host(const Event& e, const uint8_t* __restrict__ bytes) {
-  if (e.mask & PM_HOST) return true;  // (LK_APP events are decided by k_host_flags itself)
-  const uint8_t* p = bytes + e.off;
-  if (e.kind >= LK_EJB_ENTRY && e.kind <= LK_CT_EXIT) {
-    if (!(e.mask & PM_KEYS) || e.ntok < 3) return true;
-    if (e.kind == LK_CT_EXIT && (e.mask & PM_BAF) && e.ntok >= 4) {
-      int n;
-      bool digits;
-      double v;
-      if (!baf_account_scan(p, e.t3s, e.t3e, n, digits, v)) return true;
-    }
-    return false;
-  }
-  if (e.kind == LK_SOAP) {
-    const uint32_t m = e.mask;
-    if (m & (PM_SOAP_IN | PM_SOAP_OUT)) return false;
-    if (m & (PM_SOAP_ACCT | PM_SOAP_VALUE)) {
-      if (!(m & PM_SOAP_ACCT) && (m & PM_SOAP_KEY)) return false;  // KEY branch wins
-      int fs, fe;
-      angle_field2(p, (int)e.len, fs, fe);
-      if (fs < 0) return false;
-      while (fs < fe && (p[fs] == ' ' || (p[fs] >= 9 && p[fs] <= 13))) ++fs;
-      while (fe > fs && (p[fe - 1] == ' ' || (p[fe - 1] >= 9 && p[fe - 1] <= 13))) --fe;
-      double v;
-      if (all_digits(p + fs, fe - fs) && !simple_parse_int(p + fs, fe - fs, v)) return true;
-    }
-    return false;
-  }
-  return false;
-}
-
 // Non-audit events: the byte-level fields the join needs, derived once on the parse stream (next
 // to needs_host, which scans the same bytes) and stored in the event's AudF slot, so k_build_ops
 // -- on the join stream, the ingest thread's critical path -- only reads them:
@@ -375,6 +340,39 @@ __device__ bool needs_host(const Event& e, const uint8_t* __restrict__ bytes) {
 //   number (el, PRE_SOAP_VALID).
 // Returns -1: the host derives the event (needs_host), 0: nothing stored, 1: stored in f.
 enum : uint8_t { PRE_BAF = 1, PRE_BAF_VALID = 2, PRE_SOAP_VALID = 4 };
+// split(/<|>/)[2] of the ASCII-trimmed line [0, len) (dj::angle_field2), on the device: the
+// delimiters of each dword found exactly by SWAR over aligned 16-byte loads -- one load per 16
+// bytes instead of a dependent byte load per character (lane per SOAP line, ~100-200 bytes).
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {  // 0x80 in every zero byte of x
+  return ~((((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) | 0x7f7f7f7fu);
+}
+__device__ void angle_field2_dev(const uint8_t* __restrict__ p, int len, int& fs, int& fe) {
+  auto ws = [](uint8_t c) { return c == ' ' || (c >= 9 && c <= 13); };
+  int a = 0, b = len;
+  while (a < b && ws(p[a])) ++a;
+  while (b > a && ws(p[b - 1])) --b;
+  fs = fe = -1;
+  int seen = 0, start = -1;
+  const int lead = (int)((uintptr_t)(p + a) & 15u);
+  const uint4* q = reinterpret_cast<const uint4*>(p + a - lead);
+  for (int g = a - lead; g < b; g += 16, ++q) {
+    const uint4 v = *q;
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint32_t m = zero_bytes(w[k] ^ 0x3c3c3c3cu) | zero_bytes(w[k] ^ 0x3e3e3e3eu);  // '<' | '>'
+      while (m) {
+        const int i = g + 4 * k + (__builtin_ctz(m) >> 3);
+        m &= m - 1;
+        if (i < a || i >= b) continue;
+        if (seen == 2) { fs = start; fe = i; return; }
+        if (++seen == 2) start = i + 1;
+      }
+    }
+  }
+  if (seen == 2) { fs = start; fe = b; }
+}
+
 __device__ int pre_fields(const Event& e, const uint8_t* __restrict__ bytes, AudF& f) {
   if (e.mask & PM_HOST) return -1;
   const uint8_t* p = bytes + e.off;
@@ -408,7 +406,7 @@ __device__ int pre_fields(const Event& e, const uint8_t* __restrict__ bytes, Aud
     if (m & (PM_SOAP_ACCT | PM_SOAP_VALUE)) {
       if (!(m & PM_SOAP_ACCT) && (m & PM_SOAP_KEY)) return 0;  // KEY branch wins
       int fs, fe;
-      angle_field2(p, (int)e.len, fs, fe);
+      angle_field2_dev(p, (int)e.len, fs, fe);
       if (fs >= 0) {
         while (fs < fe && (p[fs] == ' ' || (p[fs] >= 9 && p[fs] <= 13))) ++fs;
         while (fe > fs && (p[fe - 1] == ' ' || (p[fe - 1] >= 9 && p[fe - 1] <= 13))) --fe;
