@@ -718,8 +718,12 @@ void DeviceJoin::rebuild_table_async(double now) {
 // trigger it, else zeroing the spare table so a later rebuild skips its memset.  The clock is
 // this batch's: only entries expired at it are dropped (later expiries are checked by the kernels).
 void DeviceJoin::idle_upkeep(double now, uint32_t n_next) {
-  if (live_pending_) return;  // a rebuild's count is still unread
-  if ((keys_live_ + keys_since_rebuild_ + n_next) * 2 > table_cap_ && table_rebuilds_ > 0 &&
+  static const int mode = [] {  // APM_IDLE_UPKEEP: 0 off, 1 spare zeroing only, 2 (default) + rebuild
+    const char* e = std::getenv("APM_IDLE_UPKEEP");
+    return e ? std::atoi(e) : 2;
+  }();
+  if (mode == 0 || live_pending_) return;  // (a rebuild's count is still unread)
+  if (mode >= 2 && (keys_live_ + keys_since_rebuild_ + n_next) * 2 > table_cap_ && table_rebuilds_ > 0 &&
       (keys_live_ + keys_live_ / 8 + n_next) * 8 <= (uint64_t)table_cap_ * 5) {
     rebuild_table_async(now);
   } else if (d_table_spare_ && !spare_clean_) {
