@@ -373,7 +373,7 @@ __device__ void angle_field2_dev(const uint8_t* __restrict__ p, int len, int& fs
   if (seen == 2) { fs = start; fe = b; }
 }
 
-__device__ int pre_fields(const Event& e, const uint8_t* __restrict__ bytes, AudF& f) {
+__device__ int pre_fields(const Event& e, const uint8_t* __restrict__ bytes, AudF& f, bool bytewise) {
   if (e.mask & PM_HOST) return -1;
   const uint8_t* p = bytes + e.off;
   f.h_item = 0; f.el = apm_nan(); f.h_sw = 0; f.ts = apm_nan(); f.ref = 0; f.len = 0; f.flags = 0; f.pad = 0;
@@ -406,7 +406,8 @@ __device__ int pre_fields(const Event& e, const uint8_t* __restrict__ bytes, Aud
     if (m & (PM_SOAP_ACCT | PM_SOAP_VALUE)) {
       if (!(m & PM_SOAP_ACCT) && (m & PM_SOAP_KEY)) return 0;  // KEY branch wins
       int fs, fe;
-      angle_field2_dev(p, (int)e.len, fs, fe);
+      if (bytewise) angle_field2(p, (int)e.len, fs, fe);  // (APM_PRE_BYTEWISE: A/B switch)
+      else angle_field2_dev(p, (int)e.len, fs, fe);
       if (fs >= 0) {
         while (fs < fe && (p[fs] == ' ' || (p[fs] >= 9 && p[fs] <= 13))) ++fs;
         while (fe > fs && (p[fe - 1] == ' ' || (p[fe - 1] >= 9 && p[fe - 1] <= 13))) --fe;
@@ -440,7 +441,7 @@ __device__ __forceinline__ SelCount sel_unpack(uint64_t v) {
 __global__ void k_host_flags(const Event* __restrict__ ev, const uint32_t* __restrict__ n_ev_dev,
                              const uint8_t* __restrict__ bytes, const uint32_t* __restrict__ chunk_file,
                              uint8_t* __restrict__ flag, uint64_t* __restrict__ val, AudF* __restrict__ aud,
-                             SelCount* __restrict__ totals, uint32_t cap) {
+                             SelCount* __restrict__ totals, uint32_t cap, int bytewise) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t n = min(*n_ev_dev, cap);
   if (blockIdx.x * blockDim.x >= n) return;  // (uniform per block: the grid is sized for the capacity)
@@ -458,7 +459,7 @@ __global__ void k_host_flags(const Event* __restrict__ ev, const uint32_t* __res
       if (host) fl |= SEL_HOST;
     } else {
       AudF f;
-      const int r = pre_fields(e, bytes, f);
+      const int r = pre_fields(e, bytes, f, bytewise != 0);
       if (r < 0) fl |= SEL_HOST;
       else if (r > 0) aud[i] = f;  // read by k_build_ops
     }
@@ -2154,11 +2155,15 @@ size_t apm_dj_tmp_bytes(uint32_t max_ev, uint32_t max_out, int table_bits) {
   return std::max(std::max(std::max(a, b), std::max(c, d)), std::max(e, f)) + 4096;
 }
 
+static int pre_bytewise() {
+  static const int v = [] { const char* e = std::getenv("APM_PRE_BYTEWISE"); return e && e[0] == '1' ? 1 : 0; }();
+  return v;
+}
 int apm_dj_select_host(DJArgs* a, const uint32_t* d_n_ev, uint32_t max_ev, hipStream_t s) {
   HIP_OK(hipMemsetAsync(a->n_host, 0, sizeof(SelCount), s));
   if (max_ev == 0) return 0;
   hipLaunchKernelGGL(k_host_flags, dim3((max_ev + TB - 1) / TB), dim3(TB), 0, s, a->ev, d_n_ev, a->bytes, a->chunk_file,
-                     a->host_flag, a->sel_val, a->aud, a->n_host, max_ev);
+                     a->host_flag, a->sel_val, a->aud, a->n_host, max_ev, pre_bytewise());
   dj_check(s, "k_host_flags");
   // sel_pos: the tile sums, then the packed total (sel_pos has max_ev + 64 entries)
   uint64_t* total = a->sel_pos + (max_ev + DS_TILE - 1) / DS_TILE + 1;

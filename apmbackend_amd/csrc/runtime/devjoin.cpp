@@ -1196,6 +1196,7 @@ void DeviceJoin::save_tables(BinWriter& w) {
     write_dev(w, out, (size_t)n_live * sizeof(KeyState), st, h_ck_bounce_, kCkBounce);
     HIP_OK(hipFree(tmp));
     if (out != d_table_spare_) HIP_OK(hipFree(out));
+    else spare_clean_ = false;  // (the compaction scratch: a rebuild must clear it again)
   }
   span("ck.j.table");
   // needNumRecordCache regions + their arena entries (arena capacity first: the table's `need`
@@ -1403,6 +1404,10 @@ void DeviceJoin::load(BinReader& rd) {
     // (mirrors save_tables; restore time no longer scales with one copy per entry)
     const uint64_t cap = cfg_.arena_cap;
     if (ents.size() > cap) throw std::runtime_error("checkpoint: need arena larger than the ring");
+    // dmalloc zeroes on the join stream; the blocking copies below run on the null stream, which
+    // does not order against it -- without this wait a regrown buffer's memset could land after
+    // the restored contents (seen: restored logId chain blocks read back as zeros)
+    HIP_OK(hipStreamSynchronize(st));
     if (!ents.empty()) {
       const uint64_t first = lo & (cap - 1);
       const uint64_t n1 = std::min<uint64_t>(ents.size(), cap - first);
@@ -1425,6 +1430,7 @@ void DeviceJoin::load(BinReader& rd) {
       pool_n_ = (uint32_t)n;
       d_pool_ = (uint8_t*)dmalloc((size_t)pool_n_ * CHAIN_BLK);
       d_pool_ring_ = (uint32_t*)dmalloc((size_t)pool_n_ * 4);
+      HIP_OK(hipStreamSynchronize(st));  // (the zeroing before the null-stream copy, as above)
     }
     if (!blocks.empty())
       HIP_OK(hipMemcpy(d_pool_, blocks.data(), blocks.size() * CHAIN_BLK, hipMemcpyHostToDevice));
@@ -1483,6 +1489,7 @@ void DeviceJoin::load(BinReader& rd) {
     aud_cur_ = 0;
     AudGen& g = aud_gen_[0];
     aud_reserve(g, (uint32_t)autr.size(), (uint32_t)items.size(), txt.size());
+    HIP_OK(hipStreamSynchronize(st));  // (its zeroing before the null-stream copies, as above)
     HIP_OK(hipMemset(g.carry, 0, (size_t)soap_cap_ * sizeof(AudCarry)));
     HIP_OK(hipMemset(aud_gen_[1].carry, 0, (size_t)soap_cap_ * sizeof(AudCarry)));
     if (!carry.empty()) HIP_OK(hipMemcpy(g.carry, carry.data(), carry.size() * sizeof(AudCarry), hipMemcpyHostToDevice));

@@ -669,7 +669,8 @@ def test_join_overflow_chains_match_oracle():
     assert j["chain_partial_blocks"] > 0 and j["chain_need_blocks"] > 0 and j["chain_logid_blocks"] > 0
 
 
-def test_join_tables_grow_instead_of_failing(tmp_path):
+@pytest.mark.parametrize("restore", [True, False], ids=["ckpt", "same"])
+def test_join_tables_grow_instead_of_failing(tmp_path, restore):
     """Key table, need arena and chain pool all start at 1024 entries: each batch's worst case
     exceeds them, so the join grows them between batches (was: a throw once live keys passed half
     of gpu.joinTableSlots, and silently dropped parked records past the arena).  A checkpoint
@@ -684,22 +685,36 @@ def test_join_tables_grow_instead_of_failing(tmp_path):
     out = collections.defaultdict(list)
     cut = len(bl) // 2
     prefix = str(tmp_path / "engine.rank0")
+    marks = []  # tx lines out after each batch
     for i, (now, chunks) in enumerate(bl[:cut]):
         eng.process_lines(chunks, now)
         for k in ("transactions", "audit_db", "st", "fs", "al"):
             out[k] += eng.take(k)
+        marks.append(len(out["transactions"]))
     j = eng.metrics()["join"]
     assert j["table_grows"] > 0 and j["arena_grows"] > 0 and j["pool_grows"] > 0, j
     assert j["table_slots"] > 1024 and j["need_arena_entries"] > 1024 and j["chain_pool_blocks"] > 1024
-    eng.save_state(prefix + ".bin")
-    del eng
-    C2 = small_cfg("exact")
-    eng2 = APMEngine(C2, keep_text=True)
-    eng2.load_state(prefix + ".bin")
+    if restore:
+        eng.save_state(prefix + ".bin")
+        del eng
+        C2 = small_cfg("exact")
+        eng2 = APMEngine(C2, keep_text=True)
+        eng2.load_state(prefix + ".bin")
+    else:
+        eng2 = eng
     for now, chunks in bl[cut:]:
         eng2.process_lines(chunks, now)
         for k in ("transactions", "audit_db", "st", "fs", "al"):
             out[k] += eng2.take(k)
+        marks.append(len(out["transactions"]))
+    got, want = out["transactions"], P.tx_out
+    d = next((i for i, (a, b) in enumerate(zip(got, want)) if a != b), min(len(got), len(want)))
+    if d < max(len(got), len(want)):
+        at = next((b for b, m in enumerate(marks) if m > d), len(marks))
+        bad = sum(1 for a, b in zip(got, want) if a != b)
+        pytest.fail(f"tx stream differs first at line {d} (batch {at}, cut {cut}; {bad} lines differ, "
+                    f"{len(got)} vs {len(want)}): {got[d][:160] if d < len(got) else None!r} != "
+                    f"{want[d][:160] if d < len(want) else None!r}")
     _assert_streams(out, P)
     j2 = eng2.metrics()["join"]
     assert j2["partial_overflow"] == 0 and j2["need_overflow"] == 0 and j2["table_full"] == 0
