@@ -22,6 +22,7 @@ void encode_blob(std::string_view blob, std::string* out, int64_t* counts);
 }
 int apm_txcopy_lines(const char* d_text, const uint64_t* h_line_off, int64_t n, std::string& out_rows);  // txcopy.hip
 std::vector<double> apm_release_bench(int64_t n, int iters, uint64_t seed);                               // txcopy.hip
+std::vector<double> apm_dj_rebuild_selftest(uint32_t cap, double load, double dead, uint64_t seed, bool copy);  // devjoin.hip
 }  // namespace apm
 
 namespace py = pybind11;
@@ -559,6 +560,17 @@ PYBIND11_MODULE(_apm_native, m) {
     for (int i = 0; i < 7; ++i) d[k[i]] = r[(size_t)i];
     return d;
   }, py::arg("n") = 60000, py::arg("iters") = 20, py::arg("seed") = 1);
+  m.def("dj_rebuild_selftest", [](uint32_t cap, double load, double dead, uint64_t seed, bool copy) {
+    std::vector<double> r;
+    {
+      py::gil_scoped_release rel;
+      r = apm_dj_rebuild_selftest(cap, load, dead, seed, copy);
+    }
+    py::dict d;
+    const char* k[8] = {"live", "want_live", "found", "dead_left", "occupied", "probes_before", "probes_after", "us"};
+    for (int i = 0; i < 8; ++i) d[k[i]] = r[(size_t)i];
+    return d;
+  }, py::arg("cap"), py::arg("load") = 0.55, py::arg("dead") = 0.3, py::arg("seed") = 1, py::arg("copy") = false);
   m.def("txcopy_lines", [](py::bytes blob) {
     // newline-terminated wire tx lines -> (COPY rows from the GPU encoder, fallback count)
     std::string b = blob;

@@ -24,6 +24,8 @@
 #include <climits>
 #include <cstdlib>
 #include <cstddef>
+#include <cstring>
+#include <vector>
 
 #include "devjoin_api.h"
 #include "devjoin_dev.h"
@@ -1826,6 +1828,83 @@ __global__ void k_rebuild(const KeyState* __restrict__ old, uint32_t old_cap, Ke
   }
 }
 
+// Same-size rebuild in place.  A linear-probing table is a set of clusters (maximal runs of
+// occupied slots); every key's home lies in its own cluster, so dropping the dead keys of a cluster
+// and sliding each live one back to max(its home, the slot after the previous live one) keeps
+// every key reachable from its home -- cluster by cluster, with no other cluster touched.  One
+// thread owns the clusters that start in its RB_SEG-slot segment (walking past the segment's end
+// when a cluster does); the vacated tail slots get key 0.  No second table, no memset of one, no
+// atomics on the table: k_rebuild (the growth path) reinserted every live key by CAS into a zeroed
+// copy -- ~0.42 ms a rebuild at the headline's 2M slots, the periodic p99 step.
+constexpr uint32_t RB_SEG = 8;
+
+// The first cluster start of each segment, found before any slot moves (the owner of the
+// previous segment's last cluster may vacate slot lo-1 while this segment is compacted).
+__global__ void k_rebuild_starts(const KeyState* __restrict__ t, uint32_t cap, uint32_t* __restrict__ starts) {
+  const uint32_t seg = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t n_seg = cap / RB_SEG;
+  if (seg >= n_seg) return;
+  const uint32_t mask = cap - 1, lo = seg * RB_SEG, hi = lo + RB_SEG;
+  uint32_t p = lo;
+  if (t[(lo + mask) & mask].key != 0)  // slot lo-1 occupied: the cluster through lo is not ours
+    while (p < hi && t[p].key != 0) ++p;
+  starts[seg] = p;
+}
+
+__device__ __forceinline__ bool rb_live(KeyState& s, const NeedEnt* __restrict__ arena, uint32_t arena_cap, double now,
+                                        JoinCounts* cnt, const uint8_t* pool, uint32_t* pool_ring, uint32_t pool_mask,
+                                        bool& changed) {
+  // (the liveness rules of k_rebuild)
+  const bool rec = s.rec_exp >= now && s.n_part > 0;
+  const bool acct = s.acct_exp >= now;
+  bool need = false;
+  if (s.need >= 0) {
+    const NeedEnt& ne = arena[(uint32_t)s.need & (arena_cap - 1)];
+    need = ne.key == s.key && ne.exp >= now;
+  }
+  if (!rec && s.n_part > 0 && !(s.rec_exp >= now)) atomicAdd(&cnt->expired_partials, (unsigned long long)s.n_part);
+  if (!rec && s.pblk) {
+    chain_free(pool, pool_ring, pool_mask, cnt, s.pblk);
+    s.pblk = 0;
+    changed = true;
+  }
+  if (!rec && !acct && !need) return false;
+  if (!(s.rec_exp >= now) && s.n_part != 0) { s.n_part = 0; changed = true; }
+  return true;
+}
+
+__global__ void k_rebuild_inplace(KeyState* __restrict__ t, uint32_t cap, const uint32_t* __restrict__ starts,
+                                  const NeedEnt* __restrict__ arena, uint32_t arena_cap, double now, JoinCounts* cnt,
+                                  unsigned long long* live, const uint8_t* pool, uint32_t* pool_ring,
+                                  uint32_t pool_mask) {
+  const uint32_t seg = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t n_seg = cap / RB_SEG;
+  uint32_t n_live = 0;
+  if (seg < n_seg) {
+    const uint32_t mask = cap - 1, hi = seg * RB_SEG + RB_SEG;
+    uint64_t p = starts[seg];  // (unwrapped positions: a cluster may run past the table's end)
+    while (p < hi) {
+      if (t[p & mask].key == 0) { ++p; continue; }
+      uint64_t w = p;  // next slot to fill
+      uint64_t q = p;
+      for (; t[q & mask].key != 0; ++q) {
+        KeyState s = t[q & mask];
+        bool changed = false;
+        if (!rb_live(s, arena, arena_cap, now, cnt, pool, pool_ring, pool_mask, changed)) continue;
+        const uint64_t home = q - (((uint32_t)q - home_of(s.key, mask)) & mask);
+        const uint64_t to = home > w ? home : w;
+        if (to != q || changed) t[to & mask] = s;
+        w = to + 1;
+        ++n_live;
+      }
+      for (uint64_t z = w; z < q; ++z) t[z & mask].key = 0;  // the vacated tail
+      p = q + 1;
+    }
+  }
+  for (int o = APM_WAVE / 2; o > 0; o >>= 1) n_live += __shfl_xor(n_live, o, APM_WAVE);
+  if ((threadIdx.x & (APM_WAVE - 1)) == 0 && n_live) atomicAdd(live, (unsigned long long)n_live);
+}
+
 __global__ void k_gather_len(const int64_t* __restrict__ gid, int64_t n_upper, const int64_t* __restrict__ d_n,
                              uint32_t* __restrict__ lens) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2352,6 +2431,108 @@ size_t apm_dj_live_tmp_bytes(uint32_t cap) {
 void apm_dj_live_compact(const KeyState* table, uint32_t cap, KeyState* out, uint32_t* d_n, void* tmp,
                          size_t tmp_bytes, hipStream_t s) {
   HIP_OK(rocprim::select(tmp, tmp_bytes, table, out, d_n, cap, KeyLive(), s));
+}
+
+size_t apm_dj_rebuild_scratch_bytes(uint32_t cap) { return ((size_t)cap / RB_SEG + 1) * 4; }
+
+void apm_dj_rebuild_inplace(KeyState* table, uint32_t cap, uint32_t* scratch, const NeedEnt* arena, uint32_t arena_cap,
+                            double now, JoinCounts* counts, unsigned long long* live, uint8_t* pool,
+                            uint32_t* pool_ring, uint32_t pool_mask, hipStream_t s) {
+  if (cap < RB_SEG || (cap & (cap - 1))) throw std::runtime_error("in-place rebuild: table size not a power of two >= 8");
+  const uint32_t n_seg = cap / RB_SEG;
+  hipLaunchKernelGGL(k_rebuild_starts, dim3((n_seg + TB - 1) / TB), dim3(TB), 0, s, table, cap, scratch);
+  dj_check(s, "k_rebuild_starts");
+  hipLaunchKernelGGL(k_rebuild_inplace, dim3((n_seg + TB - 1) / TB), dim3(TB), 0, s, table, cap, scratch, arena,
+                     arena_cap, now, counts, live, pool, pool_ring, pool_mask);
+  dj_check(s, "k_rebuild_inplace");
+  hipLaunchKernelGGL(k_pool_fix, dim3(1), dim3(1), 0, s, counts);
+}
+
+// Test entry (bindings: dj_rebuild_selftest): a table of `cap` slots filled to `load` by linear
+// probing with random keys, a `dead` fraction of them expired (no account / record / need), the
+// in-place (or, copy=true, the reinsert) rebuild run on it, and the result checked on the host.
+// out: {live counted on the device, live expected, survivors reachable from their home with the
+// payload they had, dead keys left, slots occupied after, probe length sum before, after, rebuild us}
+std::vector<double> apm_dj_rebuild_selftest(uint32_t cap, double load, double dead, uint64_t seed, bool copy) {
+  std::vector<KeyState> h(cap);
+  std::memset(h.data(), 0, (size_t)cap * sizeof(KeyState));
+  const uint32_t mask = cap - 1;
+  uint64_t x = seed * 0x9E3779B97F4A7C15ull + 1;
+  auto rnd = [&]() { x ^= x >> 12; x ^= x << 25; x ^= x >> 27; return x * 0x2545F4914F6CDD1Dull; };
+  const double now = 1000.0;
+  const uint32_t n = (uint32_t)(load * cap);
+  uint64_t want_live = 0, probes_before = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    uint64_t k = rnd() | 1;
+    uint32_t idx = home_of(k, mask);
+    uint32_t d = 0;
+    while (h[idx].key && h[idx].key != k) { idx = (idx + 1) & mask; ++d; }
+    if (h[idx].key == k) continue;
+    KeyState& e = h[idx];
+    e.key = k;
+    const bool is_dead = (double)(rnd() >> 11) * (1.0 / 9007199254740992.0) < dead;
+    e.acct = (double)(k % 1000003);  // payload
+    e.acct_exp = is_dead ? now - 1 : now + 10;
+    e.rec_exp = -__builtin_inf();
+    e.need = -1;
+    e.n_part = 0;
+    e.pblk = 0;
+    want_live += !is_dead;
+    probes_before += d;
+  }
+  KeyState* d_t = nullptr;
+  KeyState* d_f = nullptr;
+  uint32_t* d_scr = nullptr;
+  NeedEnt* d_arena = nullptr;
+  JoinCounts* d_c = nullptr;
+  unsigned long long* d_live = nullptr;
+  HIP_OK(hipMalloc((void**)&d_t, (size_t)cap * sizeof(KeyState)));
+  HIP_OK(hipMalloc((void**)&d_f, (size_t)cap * sizeof(KeyState)));
+  HIP_OK(hipMalloc((void**)&d_scr, apm_dj_rebuild_scratch_bytes(cap)));
+  HIP_OK(hipMalloc((void**)&d_arena, sizeof(NeedEnt)));
+  HIP_OK(hipMalloc((void**)&d_c, sizeof(JoinCounts)));
+  HIP_OK(hipMalloc((void**)&d_live, 8));
+  HIP_OK(hipMemset(d_arena, 0, sizeof(NeedEnt)));
+  HIP_OK(hipMemset(d_c, 0, sizeof(JoinCounts)));
+  HIP_OK(hipMemset(d_live, 0, 8));
+  HIP_OK(hipMemset(d_f, 0, (size_t)cap * sizeof(KeyState)));
+  HIP_OK(hipMemcpy(d_t, h.data(), (size_t)cap * sizeof(KeyState), hipMemcpyHostToDevice));
+  hipEvent_t e0, e1;
+  HIP_OK(hipEventCreate(&e0));
+  HIP_OK(hipEventCreate(&e1));
+  HIP_OK(hipEventRecord(e0, 0));
+  if (copy)
+    apm_dj_rebuild(d_t, cap, d_f, mask, d_arena, 1, now, d_c, d_live, nullptr, nullptr, 0, 0);
+  else
+    apm_dj_rebuild_inplace(d_t, cap, d_scr, d_arena, 1, now, d_c, d_live, nullptr, nullptr, 0, 0);
+  HIP_OK(hipEventRecord(e1, 0));
+  HIP_OK(hipEventSynchronize(e1));
+  float ms = 0;
+  HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+  unsigned long long live = 0;
+  HIP_OK(hipMemcpy(&live, d_live, 8, hipMemcpyDeviceToHost));
+  std::vector<KeyState> r(cap);
+  HIP_OK(hipMemcpy(r.data(), copy ? d_f : d_t, (size_t)cap * sizeof(KeyState), hipMemcpyDeviceToHost));
+  for (void* p : {(void*)d_t, (void*)d_f, (void*)d_scr, (void*)d_arena, (void*)d_c, (void*)d_live}) HIP_OK(hipFree(p));
+  HIP_OK(hipEventDestroy(e0));
+  HIP_OK(hipEventDestroy(e1));
+  uint64_t found = 0, dead_left = 0, occupied = 0, probes_after = 0;
+  for (uint32_t i = 0; i < cap; ++i) {
+    const KeyState& e = h[i];
+    if (!e.key) continue;
+    uint32_t idx = home_of(e.key, mask), d = 0;
+    while (r[idx].key && r[idx].key != e.key && d <= mask) { idx = (idx + 1) & mask; ++d; }
+    const bool there = r[idx].key == e.key;
+    if (e.acct_exp >= now) {
+      found += there && r[idx].acct == e.acct && r[idx].acct_exp == e.acct_exp && r[idx].need == -1;
+      probes_after += d;
+    } else {
+      dead_left += there;
+    }
+  }
+  for (uint32_t i = 0; i < cap; ++i) occupied += r[i].key != 0;
+  return {(double)live, (double)want_live, (double)found, (double)dead_left, (double)occupied, (double)probes_before,
+          (double)probes_after, 1000.0 * ms};
 }
 
 void apm_dj_rebuild(const KeyState* old, uint32_t old_cap, KeyState* fresh, uint32_t fresh_mask, const NeedEnt* arena,

@@ -186,6 +186,13 @@ int apm_dj_write(apm::DJFormatArgs* f, uint32_t n_stats, hipStream_t s);
 void apm_dj_rebuild(const apm::KeyState* old, uint32_t old_cap, apm::KeyState* fresh, uint32_t fresh_mask,
                     const apm::NeedEnt* arena, uint32_t arena_cap, double now, apm::JoinCounts* counts,
                     unsigned long long* live, uint8_t* pool, uint32_t* pool_ring, uint32_t pool_mask, hipStream_t s);
+// The same rebuild in place (same size; cap a power of two >= 8): each cluster of the linear-
+// probing table keeps its live keys, slid back towards their homes.  scratch:
+// apm_dj_rebuild_scratch_bytes(cap) bytes of device memory.
+size_t apm_dj_rebuild_scratch_bytes(uint32_t cap);
+void apm_dj_rebuild_inplace(apm::KeyState* table, uint32_t cap, uint32_t* scratch, const apm::NeedEnt* arena,
+                            uint32_t arena_cap, double now, apm::JoinCounts* counts, unsigned long long* live,
+                            uint8_t* pool, uint32_t* pool_ring, uint32_t pool_mask, hipStream_t s);
 // Checkpoint: the occupied slots (key != 0) of the key table, in slot order, into `out`;
 // *d_n = their count.  tmp: apm_dj_live_tmp_bytes(cap) bytes.
 size_t apm_dj_live_tmp_bytes(uint32_t cap);

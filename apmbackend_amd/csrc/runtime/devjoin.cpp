@@ -692,21 +692,35 @@ void DeviceJoin::rebuild_table(double now, uint32_t new_cap) {
 
 // The same-size rebuild in stream order, without waiting for it: the live count arrives in h_live_
 // with the batch's own syncs and is read at the next capacity check.  (A synchronous rebuild
-// stalled the ingest thread ~0.5 ms every ~32 batches at the headline rate: the p99 step.)
+// stalled the ingest thread ~0.5 ms every ~32 batches at the headline rate: the p99 step.)  It
+// compacts the table's clusters in place (apm_dj_rebuild_inplace): no second table to zero and
+// fill.  APM_REBUILD_COPY=1 keeps the reinsert-into-the-spare form (A/B).
 void DeviceJoin::rebuild_table_async(double now) {
+  static const bool copy = [] { const char* e = std::getenv("APM_REBUILD_COPY"); return e && e[0] == '1'; }();
   hipStream_t st = stream_;
-  KeyState* fresh = d_table_spare_;
-  if (!fresh) fresh = (KeyState*)dmalloc((size_t)table_cap_ * sizeof(KeyState));  // (zeroed)
-  else if (!spare_clean_) HIP_OK(hipMemsetAsync(fresh, 0, (size_t)table_cap_ * sizeof(KeyState), st));
   HIP_OK(hipMemsetAsync(d_live_, 0, 8, st));
-  apm_dj_rebuild(d_table_, table_cap_, fresh, table_cap_ - 1, d_arena_, cfg_.arena_cap, now, d_counts_, d_live_,
-                 d_pool_, d_pool_ring_, pool_n_ - 1, st);
+  if (copy) {
+    KeyState* fresh = d_table_spare_;
+    if (!fresh) fresh = (KeyState*)dmalloc((size_t)table_cap_ * sizeof(KeyState));  // (zeroed)
+    else if (!spare_clean_) HIP_OK(hipMemsetAsync(fresh, 0, (size_t)table_cap_ * sizeof(KeyState), st));
+    apm_dj_rebuild(d_table_, table_cap_, fresh, table_cap_ - 1, d_arena_, cfg_.arena_cap, now, d_counts_, d_live_,
+                   d_pool_, d_pool_ring_, pool_n_ - 1, st);
+    d_table_spare_ = d_table_;  // (zeroed later, in an idle gap of the join stream)
+    spare_clean_ = false;
+    d_table_ = fresh;
+  } else {
+    const size_t need = apm_dj_rebuild_scratch_bytes(table_cap_);
+    if (need > rb_scratch_bytes_) {
+      if (d_rb_scratch_) dfree(d_rb_scratch_, rb_scratch_bytes_);
+      d_rb_scratch_ = (uint32_t*)dmalloc(need);
+      rb_scratch_bytes_ = need;
+    }
+    apm_dj_rebuild_inplace(d_table_, table_cap_, d_rb_scratch_, d_arena_, cfg_.arena_cap, now, d_counts_, d_live_,
+                           d_pool_, d_pool_ring_, pool_n_ - 1, st);
+  }
   HIP_OK(hipMemcpyAsync(h_live_, d_live_, 8, hipMemcpyDeviceToHost, st));
   if (!live_ev_) HIP_OK(hipEventCreateWithFlags(&live_ev_, hipEventDisableTiming));
   HIP_OK(hipEventRecord(live_ev_, st));
-  d_table_spare_ = d_table_;  // (zeroed later, in an idle gap of the join stream)
-  spare_clean_ = false;
-  d_table_ = fresh;
   keys_since_rebuild_ = 0;
   live_pending_ = true;
   ++table_rebuilds_;

@@ -244,6 +244,8 @@ class DeviceJoin {
   bool live_pending_ = false;  // an in-order rebuild's live count is on its way to h_live_
   hipEvent_t live_ev_ = nullptr;  // recorded after that count's D2H
   bool spare_clean_ = false;   // d_table_spare_ is zeroed (the next rebuild skips its memset)
+  uint32_t* d_rb_scratch_ = nullptr;  // per-segment cluster starts of the in-place rebuild
+  size_t rb_scratch_bytes_ = 0;
   uint8_t* d_pool_ = nullptr;          // chain blocks
   uint32_t* d_pool_ring_ = nullptr;    // free-index ring
   uint32_t pool_n_ = 0;                // blocks (power of two)
