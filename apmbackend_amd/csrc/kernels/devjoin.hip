@@ -1887,7 +1887,7 @@ __global__ void k_rebuild_inplace(KeyState* __restrict__ t, uint32_t cap, const 
       if (t[p & mask].key == 0) { ++p; continue; }
       uint64_t w = p;  // next slot to fill
       uint64_t q = p;
-      for (; t[q & mask].key != 0; ++q) {
+      for (; t[q & mask].key != 0 && q < p + cap; ++q) {  // (bounded: a full table has no cluster end)
         KeyState s = t[q & mask];
         bool changed = false;
         if (!rb_live(s, arena, arena_cap, now, cnt, pool, pool_ring, pool_mask, changed)) continue;
