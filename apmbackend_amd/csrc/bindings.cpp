@@ -22,7 +22,6 @@ void encode_blob(std::string_view blob, std::string* out, int64_t* counts);
 }
 int apm_txcopy_lines(const char* d_text, const uint64_t* h_line_off, int64_t n, std::string& out_rows);  // txcopy.hip
 std::vector<double> apm_release_bench(int64_t n, int iters, uint64_t seed);                               // txcopy.hip
-std::vector<double> apm_dj_rebuild_selftest(uint32_t cap, double load, double dead, uint64_t seed, bool copy);  // devjoin.hip
 }  // namespace apm
 
 namespace py = pybind11;

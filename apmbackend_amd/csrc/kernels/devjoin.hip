@@ -2534,7 +2534,6 @@ std::vector<double> apm_dj_rebuild_selftest(uint32_t cap, double load, double de
   return {(double)live, (double)want_live, (double)found, (double)dead_left, (double)occupied, (double)probes_before,
           (double)probes_after, 1000.0 * ms};
 }
-
 void apm_dj_rebuild(const KeyState* old, uint32_t old_cap, KeyState* fresh, uint32_t fresh_mask, const NeedEnt* arena,
                     uint32_t arena_cap, double now, JoinCounts* counts, unsigned long long* live, uint8_t* pool,
                     uint32_t* pool_ring, uint32_t pool_mask, hipStream_t s) {

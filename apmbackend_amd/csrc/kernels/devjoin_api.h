@@ -1,5 +1,6 @@
 // Launch-side API of the GPU join (devjoin.hip), used by runtime/devjoin.cpp.
 #pragma once
+#include <vector>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -190,6 +191,8 @@ void apm_dj_rebuild(const apm::KeyState* old, uint32_t old_cap, apm::KeyState* f
 // probing table keeps its live keys, slid back towards their homes.  scratch:
 // apm_dj_rebuild_scratch_bytes(cap) bytes of device memory.
 size_t apm_dj_rebuild_scratch_bytes(uint32_t cap);
+// test entry: the rebuild on a synthetic table, checked on the host (see devjoin.hip)
+std::vector<double> apm_dj_rebuild_selftest(uint32_t cap, double load, double dead, uint64_t seed, bool copy);
 void apm_dj_rebuild_inplace(apm::KeyState* table, uint32_t cap, uint32_t* scratch, const apm::NeedEnt* arena,
                             uint32_t arena_cap, double now, apm::JoinCounts* counts, unsigned long long* live,
                             uint8_t* pool, uint32_t* pool_ring, uint32_t pool_mask, hipStream_t s);
