@@ -1831,7 +1831,8 @@ __global__ void k_rebuild(const KeyState* __restrict__ old, uint32_t old_cap, Ke
 // Same-size rebuild in place.  A linear-probing table is a set of clusters (maximal runs of
 // occupied slots); every key's home lies in its own cluster, so dropping the dead keys of a cluster
 // and sliding each live one back to max(its home, the slot after the previous live one) keeps
-// every key reachable from its home -- cluster by cluster, with no other cluster touched.  One
+// every key reachable from its home -- cluster by cluster, with no other cluster touched (a slot
+// left free before a key whose home lies past it is emptied: nothing probes through it).  One
 // thread owns the clusters that start in its RB_SEG-slot segment (walking past the segment's end
 // when a cluster does); the vacated tail slots get key 0.  No second table, no memset of one, no
 // atomics on the table: k_rebuild (the growth path) reinserted every live key by CAS into a zeroed
@@ -1893,6 +1894,7 @@ __global__ void k_rebuild_inplace(KeyState* __restrict__ t, uint32_t cap, const 
         if (!rb_live(s, arena, arena_cap, now, cnt, pool, pool_ring, pool_mask, changed)) continue;
         const uint64_t home = q - (((uint32_t)q - home_of(s.key, mask)) & mask);
         const uint64_t to = home > w ? home : w;
+        for (uint64_t z = w; z < to; ++z) t[z & mask].key = 0;  // a gap no later key probes through
         if (to != q || changed) t[to & mask] = s;
         w = to + 1;
         ++n_live;
