@@ -662,6 +662,16 @@ void DeviceJoin::rebuild_table(double now, uint32_t new_cap) {
   hipStream_t st = stream_;
   KeyState* fresh;
   const bool same = new_cap == table_cap_;
+  if (same && !rebuild_copy()) {  // in place (apm_dj_rebuild_inplace), then wait for the count
+    rebuild_inplace(now);
+    HIP_OK(hipMemcpyAsync(h_live_, d_live_, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    keys_live_ = *h_live_;
+    keys_since_rebuild_ = 0;
+    live_pending_ = false;
+    ++table_rebuilds_;
+    return;
+  }
   if (same && d_table_spare_) fresh = d_table_spare_;
   else fresh = (KeyState*)dmalloc((size_t)new_cap * sizeof(KeyState));
   HIP_OK(hipMemsetAsync(fresh, 0, (size_t)new_cap * sizeof(KeyState), st));
@@ -695,11 +705,27 @@ void DeviceJoin::rebuild_table(double now, uint32_t new_cap) {
 // stalled the ingest thread ~0.5 ms every ~32 batches at the headline rate: the p99 step.)  It
 // compacts the table's clusters in place (apm_dj_rebuild_inplace): no second table to zero and
 // fill.  APM_REBUILD_COPY=1 keeps the reinsert-into-the-spare form (A/B).
-void DeviceJoin::rebuild_table_async(double now) {
+bool DeviceJoin::rebuild_copy() {
   static const bool copy = [] { const char* e = std::getenv("APM_REBUILD_COPY"); return e && e[0] == '1'; }();
+  return copy;
+}
+
+void DeviceJoin::rebuild_inplace(double now) {
+  const size_t need = apm_dj_rebuild_scratch_bytes(table_cap_);
+  if (need > rb_scratch_bytes_) {
+    if (d_rb_scratch_) dfree(d_rb_scratch_, rb_scratch_bytes_);
+    d_rb_scratch_ = (uint32_t*)dmalloc(need);
+    rb_scratch_bytes_ = need;
+  }
+  HIP_OK(hipMemsetAsync(d_live_, 0, 8, stream_));
+  apm_dj_rebuild_inplace(d_table_, table_cap_, d_rb_scratch_, d_arena_, cfg_.arena_cap, now, d_counts_, d_live_,
+                         d_pool_, d_pool_ring_, pool_n_ - 1, stream_);
+}
+
+void DeviceJoin::rebuild_table_async(double now) {
   hipStream_t st = stream_;
-  HIP_OK(hipMemsetAsync(d_live_, 0, 8, st));
-  if (copy) {
+  if (rebuild_copy()) {
+    HIP_OK(hipMemsetAsync(d_live_, 0, 8, st));
     KeyState* fresh = d_table_spare_;
     if (!fresh) fresh = (KeyState*)dmalloc((size_t)table_cap_ * sizeof(KeyState));  // (zeroed)
     else if (!spare_clean_) HIP_OK(hipMemsetAsync(fresh, 0, (size_t)table_cap_ * sizeof(KeyState), st));
@@ -709,14 +735,7 @@ void DeviceJoin::rebuild_table_async(double now) {
     spare_clean_ = false;
     d_table_ = fresh;
   } else {
-    const size_t need = apm_dj_rebuild_scratch_bytes(table_cap_);
-    if (need > rb_scratch_bytes_) {
-      if (d_rb_scratch_) dfree(d_rb_scratch_, rb_scratch_bytes_);
-      d_rb_scratch_ = (uint32_t*)dmalloc(need);
-      rb_scratch_bytes_ = need;
-    }
-    apm_dj_rebuild_inplace(d_table_, table_cap_, d_rb_scratch_, d_arena_, cfg_.arena_cap, now, d_counts_, d_live_,
-                           d_pool_, d_pool_ring_, pool_n_ - 1, st);
+    rebuild_inplace(now);
   }
   HIP_OK(hipMemcpyAsync(h_live_, d_live_, 8, hipMemcpyDeviceToHost, st));
   if (!live_ev_) HIP_OK(hipEventCreateWithFlags(&live_ev_, hipEventDisableTiming));

@@ -187,6 +187,8 @@ class DeviceJoin {
   void rebuild_table(double now, uint32_t new_cap);
   void rebuild_table_async(double now);
   void ensure_rest(uint32_t n_ev, uint64_t bytes);  // ensure_capacity after the key table
+  void rebuild_inplace(double now);                  // same-size rebuild, queued (count -> d_live_)
+  static bool rebuild_copy();                        // APM_REBUILD_COPY=1: reinsert into the spare (A/B)
   void idle_upkeep(double now, uint32_t n_next);    // end of a batch: table upkeep while the host works
   void grow_arena(uint32_t new_cap, uint64_t lo);
   void grow_pool(uint64_t need_free);
