@@ -1830,9 +1830,8 @@ __global__ void k_rebuild(const KeyState* __restrict__ old, uint32_t old_cap, Ke
 
 // Same-size rebuild in place.  A linear-probing table is a set of clusters (maximal runs of
 // occupied slots); every key's home lies in its own cluster, so dropping the dead keys of a cluster
-// and sliding each live one back to max(its home, the slot after the previous live one) keeps
-// every key reachable from its home -- cluster by cluster, with no other cluster touched (a slot
-// left free before a key whose home lies past it is emptied: nothing probes through it).  One
+// and re-inserting the live ones in slot order into the emptied cluster keeps every key
+// reachable from its home -- cluster by cluster, with no other cluster touched.  One
 // thread owns the clusters that start in its RB_SEG-slot segment (walking past the segment's end
 // when a cluster does); the vacated tail slots get key 0.  No second table, no memset of one, no
 // atomics on the table: k_rebuild (the growth path) reinserted every live key by CAS into a zeroed
@@ -1874,10 +1873,16 @@ __device__ __forceinline__ bool rb_live(KeyState& s, const NeedEnt* __restrict__
   return true;
 }
 
-__global__ void k_rebuild_inplace(KeyState* __restrict__ t, uint32_t cap, const uint32_t* __restrict__ starts,
-                                  const NeedEnt* __restrict__ arena, uint32_t arena_cap, double now, JoinCounts* cnt,
-                                  unsigned long long* live, const uint8_t* pool, uint32_t* pool_ring,
-                                  uint32_t pool_mask) {
+constexpr int RB_TB = 128;      // threads per block of k_rebuild_inplace
+constexpr int RB_BITS = 1024;   // longest cluster compacted (longer ones are left as they are)
+__global__ __launch_bounds__(RB_TB) void k_rebuild_inplace(KeyState* __restrict__ t, uint32_t cap,
+                                                           const uint32_t* __restrict__ starts,
+                                                           const NeedEnt* __restrict__ arena, uint32_t arena_cap,
+                                                           double now, JoinCounts* cnt, unsigned long long* live,
+                                                           const uint8_t* pool, uint32_t* pool_ring, uint32_t pool_mask) {
+  // per thread: which slots of its current cluster hold a placed key (LDS, 128 B a thread)
+  __shared__ uint32_t occ_s[RB_TB][RB_BITS / 32];
+  uint32_t* occ = occ_s[threadIdx.x];
   const uint32_t seg = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t n_seg = cap / RB_SEG;
   uint32_t n_live = 0;
@@ -1886,20 +1891,32 @@ __global__ void k_rebuild_inplace(KeyState* __restrict__ t, uint32_t cap, const 
     uint64_t p = starts[seg];  // (unwrapped positions: a cluster may run past the table's end)
     while (p < hi) {
       if (t[p & mask].key == 0) { ++p; continue; }
-      uint64_t w = p;  // next slot to fill
       uint64_t q = p;
-      for (; t[q & mask].key != 0 && q < p + cap; ++q) {  // (bounded: a full table has no cluster end)
-        KeyState s = t[q & mask];
+      while (t[q & mask].key != 0 && q < p + cap) ++q;  // the cluster is [p, q) (bounded: a full table)
+      const uint32_t L = (uint32_t)(q - p);
+      if (L > RB_BITS) {  // (not at <= 5/8 load in practice) left as it is: its keys count as live
+        n_live += L;
+        p = q + 1;
+        continue;
+      }
+      for (uint32_t i = 0; i < (L + 31) / 32; ++i) occ[i] = 0;
+      // The live keys re-inserted in slot order into the emptied cluster: each at the first free
+      // slot at or after its home.  A key never lands past its old slot (the keys placed before
+      // it came from slots before it, each no later than it was), so the walk reads every slot
+      // before anything is written there.
+      for (uint64_t r = p; r < q; ++r) {
+        KeyState s = t[r & mask];
         bool changed = false;
         if (!rb_live(s, arena, arena_cap, now, cnt, pool, pool_ring, pool_mask, changed)) continue;
-        const uint64_t home = q - (((uint32_t)q - home_of(s.key, mask)) & mask);
-        const uint64_t to = home > w ? home : w;
-        for (uint64_t z = w; z < to; ++z) t[z & mask].key = 0;  // a gap no later key probes through
-        if (to != q || changed) t[to & mask] = s;
-        w = to + 1;
+        uint32_t i = (uint32_t)(r - (((uint32_t)r - home_of(s.key, mask)) & mask) - p);  // home, from p
+        while (i < L && (occ[i >> 5] & (1u << (i & 31)))) ++i;  // (<= r - p, see above)
+        if (i >= L) i = (uint32_t)(r - p);  // (unreachable; keeps the LDS index in range)
+        occ[i >> 5] |= 1u << (i & 31);
+        if (p + i != r || changed) t[(p + i) & mask] = s;
         ++n_live;
       }
-      for (uint64_t z = w; z < q; ++z) t[z & mask].key = 0;  // the vacated tail
+      for (uint32_t i = 0; i < L; ++i)  // every slot no key was placed in is empty now
+        if (!(occ[i >> 5] & (1u << (i & 31)))) t[(p + i) & mask].key = 0;
       p = q + 1;
     }
   }
@@ -2444,7 +2461,7 @@ void apm_dj_rebuild_inplace(KeyState* table, uint32_t cap, uint32_t* scratch, co
   const uint32_t n_seg = cap / RB_SEG;
   hipLaunchKernelGGL(k_rebuild_starts, dim3((n_seg + TB - 1) / TB), dim3(TB), 0, s, table, cap, scratch);
   dj_check(s, "k_rebuild_starts");
-  hipLaunchKernelGGL(k_rebuild_inplace, dim3((n_seg + TB - 1) / TB), dim3(TB), 0, s, table, cap, scratch, arena,
+  hipLaunchKernelGGL(k_rebuild_inplace, dim3((n_seg + RB_TB - 1) / RB_TB), dim3(RB_TB), 0, s, table, cap, scratch, arena,
                      arena_cap, now, counts, live, pool, pool_ring, pool_mask);
   dj_check(s, "k_rebuild_inplace");
   hipLaunchKernelGGL(k_pool_fix, dim3(1), dim3(1), 0, s, counts);
