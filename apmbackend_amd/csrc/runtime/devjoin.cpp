@@ -1216,9 +1216,11 @@ void DeviceJoin::save_tables(BinWriter& w) {
   size_t live_off = 0;
   {
     const size_t tb = apm_dj_live_tmp_bytes(table_cap_);
+    // the spare table is the compaction target (kept: the in-place rebuild leaves no spare, and a
+    // hipMalloc / hipFree of a table-sized buffer per checkpoint costs milliseconds and a device sync)
+    if (!d_table_spare_) d_table_spare_ = (KeyState*)dmalloc((size_t)table_cap_ * sizeof(KeyState));
     KeyState* out = d_table_spare_;
     void* tmp = nullptr;
-    if (!out) HIP_OK(hipMalloc((void**)&out, (size_t)table_cap_ * sizeof(KeyState)));
     HIP_OK(hipMalloc(&tmp, tb + 64));
     uint32_t* d_n = (uint32_t*)((char*)tmp + tb);
     apm_dj_live_compact(d_table_, table_cap_, out, d_n, tmp, tb, st);
@@ -1228,8 +1230,7 @@ void DeviceJoin::save_tables(BinWriter& w) {
     live_off = w.mem_pos();
     write_dev(w, out, (size_t)n_live * sizeof(KeyState), st, h_ck_bounce_, kCkBounce);
     HIP_OK(hipFree(tmp));
-    if (out != d_table_spare_) HIP_OK(hipFree(out));
-    else spare_clean_ = false;  // (the compaction scratch: a rebuild must clear it again)
+    spare_clean_ = false;  // (the compaction scratch: a rebuild must clear it again)
   }
   span("ck.j.table");
   // needNumRecordCache regions + their arena entries (arena capacity first: the table's `need`
