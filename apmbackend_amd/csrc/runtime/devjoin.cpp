@@ -757,9 +757,9 @@ void DeviceJoin::idle_upkeep(double now, uint32_t n_next) {
   }();
   if (mode == 0 || live_pending_) return;  // (a rebuild's count is still unread)
   if (mode >= 2 && (keys_live_ + keys_since_rebuild_ + n_next) * 2 > table_cap_ && table_rebuilds_ > 0 &&
-      (keys_live_ + keys_live_ / 8 + n_next) * 8 <= (uint64_t)table_cap_ * 5) {
+      async_rebuild_fits(n_next)) {
     rebuild_table_async(now);
-  } else if (d_table_spare_ && !spare_clean_) {
+  } else if (rebuild_copy() && d_table_spare_ && !spare_clean_) {
     HIP_OK(hipMemsetAsync(d_table_spare_, 0, (size_t)table_cap_ * sizeof(KeyState), stream_));
     spare_clean_ = true;
   }
@@ -850,11 +850,12 @@ void DeviceJoin::ensure_capacity(uint32_t n_ev, uint64_t bytes, double now) {
     live_pending_ = false;
   }
   if ((keys_live_ + keys_since_rebuild_ + n_ev) * 2 > table_cap_) {
-    // steady state: the live count after the previous rebuild (+1/8) and this batch's ops keep the
-    // table at most 5/8 full -- rebuild in stream order; otherwise (growth may be due) wait for
-    // the count.  (A table a little past half full only probes longer; the count read at the
-    // next check grows it if the live keys really grew.)
-    if (table_rebuilds_ > 0 && (keys_live_ + keys_live_ / 8 + n_ev) * 8 <= (uint64_t)table_cap_ * 5) {
+    // steady state: every key the queued rebuild may keep (the live count after the previous
+    // rebuild plus the keys claimed since) and this batch's ops keep the table at most 5/8 full
+    // -- rebuild in stream order; otherwise (growth may be due) wait for the count.  (A table a
+    // little past half full only probes longer; the count read at the next check grows it if the
+    // live keys really grew.)
+    if (table_rebuilds_ > 0 && async_rebuild_fits(n_ev)) {
       rebuild_table_async(now);
       return ensure_rest(n_ev, bytes);
     }
@@ -1230,7 +1231,9 @@ void DeviceJoin::save_tables(BinWriter& w) {
     live_off = w.mem_pos();
     write_dev(w, out, (size_t)n_live * sizeof(KeyState), st, h_ck_bounce_, kCkBounce);
     HIP_OK(hipFree(tmp));
-    spare_clean_ = false;  // (the compaction scratch: a rebuild must clear it again)
+    // (the compaction scratch: only the reinsert rebuild (APM_REBUILD_COPY=1) targets the spare
+    // and needs it zeroed again; the in-place rebuild never reads it)
+    if (rebuild_copy()) spare_clean_ = false;
   }
   span("ck.j.table");
   // needNumRecordCache regions + their arena entries (arena capacity first: the table's `need`

@@ -186,6 +186,11 @@ class DeviceJoin {
   void ensure_capacity(uint32_t n_ev, uint64_t bytes, double now);
   void rebuild_table(double now, uint32_t new_cap);
   void rebuild_table_async(double now);
+  // a rebuild queued without waiting for its live count is safe only if the worst case -- every
+  // key since the last count still live, plus n_ev new keys -- stays within 5/8 of the table
+  bool async_rebuild_fits(uint64_t n_ev) const {
+    return (keys_live_ + keys_since_rebuild_ + n_ev) * 8 <= (uint64_t)table_cap_ * 5;
+  }
   void ensure_rest(uint32_t n_ev, uint64_t bytes);  // ensure_capacity after the key table
   void rebuild_inplace(double now);                  // same-size rebuild, queued (count -> d_live_)
   static bool rebuild_copy();                        // APM_REBUILD_COPY=1: reinsert into the spare (A/B)

@@ -214,9 +214,11 @@ void* Engine::dmalloc(size_t bytes) {
   HIP_OK(hipMalloc(&p, bytes));
   HIP_OK(hipMemset(p, 0, bytes));
   // hipMemset runs on the null stream, which does not order against the engine's non-blocking
-  // streams: without this, a buffer regrown mid-run could be zeroed *after* the first copy into
-  // it on stream_ (seen: K12 names table read back as zeros after a regrow)
-  HIP_OK(hipDeviceSynchronize());
+  // streams: without this wait, a buffer regrown mid-run could be zeroed *after* the first copy
+  // into it on stream_ (seen: K12 names table read back as zeros after a regrow).  The null
+  // stream only, not the device: a device-wide sync would also wait for the collective stream
+  // (a lock-step all-reduce waiting for a peer rank).
+  HIP_OK(hipStreamSynchronize(nullptr));
   std::lock_guard<std::mutex> g(alloc_mu_);  // the stats thread and the rollover lane allocate
   allocations_.push_back(p);
   alloc_bytes_[p] = bytes;

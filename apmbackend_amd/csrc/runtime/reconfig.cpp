@@ -83,8 +83,12 @@ void Engine::apply_reconfig(const ReconfigSpec& r) {
   bool lag_change = r.n_lags != cfg_.n_lags;
   for (int l = 0; l < r.n_lags && !lag_change; ++l) lag_change = r.lags[l] != cfg_.lags[l];
   if (lag_change) {
-    // kernels of the previous rollover (formatting, packing) still read the old per-LAG arrays
-    HIP_OK(hipDeviceSynchronize());
+    // kernels of the previous rollover (formatting on the output stream, K10/K11 and the fleet
+    // pack on the stats stream) still read the old per-LAG arrays.  Only those two streams: a
+    // device-wide sync would also wait for the collective stream, whose lock-step all-reduce may
+    // be waiting for a peer -- tying this thread to peer progress (fleet_pack_locked avoids it)
+    HIP_OK(hipStreamSynchronize(stream_));
+    HIP_OK(hipStreamSynchronize(out_stream_));
     const int32_t S = cfg_.max_series;
     LagState nl[MAX_LAGS] = {};
     bool kept[MAX_LAGS] = {false, false, false, false};

@@ -34,7 +34,7 @@ import math
 import os
 import signal
 import time
-from typing import Any, Callable, Dict, List, Optional, Sequence
+from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
 from ..models.oracle import file_kind, server_of
 from ..models.pipeline import DB_OUTPUTS, KIND_CODE, OUT_KINDS, APMEngine
@@ -160,6 +160,10 @@ class IngestService:
         # ---- checkpoint restore (before files are registered: load_state re-registers them)
         self.ckpt_dir = g.get("checkpointDir")
         self.n_checkpoints = 0
+        # sink snapshot named by the last checkpoint known to be committed (in the chain
+        # manifest), and (name, writer completions before it) of the last one started
+        self._sink_committed: Optional[str] = None
+        self._ck_started: Optional[Tuple[str, int]] = None
         self.ckpt_every = float(g.get("checkpointEverySeconds",
                                       self.cfg["streamCalcStats"].get("resumeFileSaveFrequencyInSeconds", 60)))
         self.resharded = False
@@ -372,25 +376,47 @@ class IngestService:
         rename before the engine checkpoint that names it is published)."""
         from .sinks import write_sink_snapshot
         acked, jobs = self.inserter.snapshot_pending()
-        name = f"sink_pending.rank{self.rank}.{self.n_checkpoints + 1}.bin"
+        name = self._sink_snapshot_name()
         write_sink_snapshot(os.path.join(self.ckpt_dir, name), jobs)
-        self._prune_sink_snapshots()
+        self._prune_sink_snapshots(name)
         self.sink_pending_rows = sum(int(j[3]) for j in jobs)
         return {"incarnation": self._sink_incarnation, "acked": acked, "pending": name, "jobs": len(jobs),
                 "rows": self.sink_pending_rows}
 
-    def _prune_sink_snapshots(self):
-        """The pending files of older checkpoints are no longer referenced (keep the previous one)."""
+    def _note_checkpoint_outcome(self):
+        """The checkpoint started last has finished (the writer is idle): if the writer completed
+        it, its sink snapshot is now the one the chain manifest names.  A failed write leaves the
+        manifest -- and the snapshot it names -- at the checkpoint before."""
+        if self._ck_started is None or self.eng is None:
+            return
+        ci = getattr(self.eng, "checkpoint_info", None)
+        info = ci() if ci is not None else {}
+        if info.get("busy"):
+            return
+        name, done_before = self._ck_started
+        if int(info.get("done", done_before + 1)) > done_before:
+            self._sink_committed = name
+        else:
+            log.warning("checkpoint with sink snapshot %s was not committed: keeping %s", name,
+                        self._sink_committed)
+        self._ck_started = None
+
+    def _prune_sink_snapshots(self, keep: str):
+        """Removes this rank's sink snapshots except `keep` (the checkpoint being written) and the
+        one the committed checkpoint names (a restore before `keep` commits needs it).  Pruning
+        follows commits, not starts: a checkpoint whose write failed never retires its
+        predecessor's snapshot (checkpoint() notes the previous one's outcome first)."""
+        keep_set = {keep, self._sink_committed}
         for old in glob.glob(os.path.join(self.ckpt_dir, f"sink_pending.rank{self.rank}.*.bin")):
-            try:
-                k = int(old.rsplit(".", 2)[-2])
-            except ValueError:
+            if os.path.basename(old) in keep_set:
                 continue
-            if k < self.n_checkpoints:
-                try:
-                    os.remove(old)
-                except OSError:
-                    pass
+            try:
+                os.remove(old)
+            except OSError:
+                pass
+
+    def _sink_snapshot_name(self) -> str:
+        return f"sink_pending.rank{self.rank}.{self._sink_incarnation:x}.{self.n_checkpoints + 1}.bin"
 
     def _restore_sink(self):
         """After a restore: re-submit the checkpoint's pending flushes that the sink did not
@@ -404,6 +430,7 @@ class IngestService:
             meta = None
         if not meta:
             return 0
+        self._sink_committed = meta["pending"]  # named by the restored chain: kept until a newer commit
         path = os.path.join(self.ckpt_dir, meta["pending"])
         if not os.path.exists(path):
             log.warning("checkpoint names sink snapshot %s, which is missing: its rows are lost", path)
@@ -482,6 +509,10 @@ class IngestService:
         os.makedirs(self.ckpt_dir, exist_ok=True)
         ck, tp = self._ckpt_paths()
         t0 = time.perf_counter()
+        # the previous checkpoint is finished here (the writer is idle): learn whether it
+        # committed before any snapshot is pruned, and count the completions before this one
+        self._note_checkpoint_outcome()
+        done_before = int(ci().get("done", 0)) if ci is not None else 0
         # undelivered output goes out first so the checkpoint and the sinks agree
         self._drain_outputs()
         sink_meta = None
@@ -504,7 +535,7 @@ class IngestService:
                 # lock); the engine's checkpoint writer thread writes + fsyncs them after the
                 # checkpoint file and before the manifest names it -- ingest does not wait
                 sink_snap = core.snapshot_capture()
-                name = f"sink_pending.rank{self.rank}.{self.n_checkpoints + 1}.bin"
+                name = self._sink_snapshot_name()
                 self.sink_pending_rows = int(sink_snap.rows)
                 sink_meta = {"incarnation": self._sink_incarnation, "acked": int(sink_snap.acked), "pending": name,
                              "jobs": int(sink_snap.jobs), "rows": self.sink_pending_rows}
@@ -523,12 +554,14 @@ class IngestService:
             seq = _native_mod().checkpoint_async_sink(self.eng.eng, prefix, extra, False, sink_snap,
                                                       os.path.join(self.ckpt_dir, sink_meta["pending"]))
             del sink_snap  # (a skipped checkpoint releases the references here)
-            self._prune_sink_snapshots()
         else:
             seq = self.eng.checkpoint_async(prefix, extra)
         if seq < 0:
             log.warning("checkpoint skipped: the previous one is still being written")
             return None
+        if sink_meta is not None:
+            self._ck_started = (sink_meta["pending"], done_before)
+            self._prune_sink_snapshots(sink_meta["pending"])
         self.n_checkpoints += 1
         self.perf["ckpt_s"] = self.perf.get("ckpt_s", 0.0) + time.perf_counter() - t0
         if wait:

@@ -292,3 +292,43 @@ def test_paused_lockstep_rank_still_joins_the_collective():
         svc.step()
         assert Tail.polled == 0
         assert Eng.calls == ([(b"", [])] if lockstep else [])
+
+
+def test_sink_snapshot_pruning_follows_commits(tmp_path):
+    """a sink snapshot is retired only once a LATER checkpoint committed.  Checkpoint
+    #2's write fails in the writer thread (the chain manifest still names #1); starting #3 must not
+    delete #1's pending file, which a crash before #3 commits would restore from."""
+    class FakeEngine:
+        def __init__(self):
+            self.done, self.busy = 0, False
+
+        def checkpoint_info(self):
+            return {"busy": self.busy, "done": self.done}
+
+    svc = IngestService.__new__(IngestService)
+    svc.ckpt_dir, svc.rank, svc.n_checkpoints = str(tmp_path), 0, 0
+    svc._sink_incarnation, svc._sink_committed, svc._ck_started = 0xabc, None, None
+    svc.eng = FakeEngine()
+
+    def start(ok):  # what checkpoint() does around one native async checkpoint
+        svc._note_checkpoint_outcome()
+        done_before = svc.eng.done
+        name = svc._sink_snapshot_name()
+        open(os.path.join(svc.ckpt_dir, name), "wb").close()
+        svc._ck_started = (name, done_before)
+        svc.eng.busy = True
+        svc._prune_sink_snapshots(name)
+        svc.n_checkpoints += 1
+        svc.eng.done += 1 if ok else 0  # the writer thread finishes (or fails) it
+        svc.eng.busy = False
+        return name
+
+    n1 = start(True)
+    n2 = start(False)   # #2's write fails: manifest still names #1
+    assert set(os.listdir(tmp_path)) == {n1, n2}
+    n3 = start(True)    # starting #3: #1 is still the committed restore point
+    assert n1 in os.listdir(tmp_path) and n3 in os.listdir(tmp_path)
+    assert n2 not in os.listdir(tmp_path)  # never named by a committed checkpoint
+    n4 = start(True)    # #3 committed: #1 may go now
+    assert set(os.listdir(tmp_path)) == {n3, n4}
+    assert svc._sink_committed == n3
