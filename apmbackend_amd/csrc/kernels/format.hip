@@ -189,8 +189,8 @@ __global__ __launch_bounds__(FMT_WAVE_LINES) void k_format_write(FormatArgs a, i
 // COPY: <ts>\t<service>\t<lag>\t<n>\t{"averagemean":..,"averagestd":..,"per75mean":..,...}
 // mean / std: of the series' z-score baseline means across the fleet (population std).
 template <bool WRITE>
-__device__ __forceinline__ void fleet_row(const FleetFormatArgs& a, int32_t i, char* dst, uint32_t* len, bool& fb) {
-  const int32_t slot = i / a.n_lags, li = i % a.n_lags;
+__device__ __forceinline__ uint32_t fleet_row(const FleetFormatArgs& a, int32_t i, char* dst, bool& fb) {
+  const int32_t slot = a.slot_lo + i / a.n_lags, li = i % a.n_lags;
   const int l = a.lag_order[li];
   const double* m = a.moments + ((size_t)slot * a.n_lags + l) * NSTAT * 3;
   OutT<WRITE> o(WRITE ? dst : nullptr);
@@ -233,24 +233,74 @@ __device__ __forceinline__ void fleet_row(const FleetFormatArgs& a, int32_t i, c
     o.c('\n');
   }
   o.finish();
-  if (!WRITE) len[i] = o.n;
+  return o.n;
 }
 
-__global__ __launch_bounds__(256) void k_fleet_len(FleetFormatArgs a) {
-  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+// One pass (was: length kernel + rocprim scan + write kernel, three launches of ~80 blocks that
+// left most CUs idle): one wave per 64 rows counts its rows' bytes, scans them across lanes, gets
+// its byte offset from the waves before it by a decoupled look-back over epoch-tagged status
+// words (blocks start in index order, so a wave only ever waits for a wave that is running or
+// done), formats its rows into an LDS stage laid out like the output and copies the stage out
+// with dword stores.  Status word: flag (bits 62-63: 1 = the wave's own total, 2 = inclusive
+// prefix) | epoch (bits 32-61) | bytes (bits 0-31).
+constexpr uint32_t FLEET_LDS = 16384;
+constexpr unsigned long long FST_AGG = 1ull << 62, FST_INC = 2ull << 62;
+
+__device__ __forceinline__ unsigned long long fleet_status(uint32_t epoch, unsigned long long flag, uint32_t v) {
+  return flag | ((unsigned long long)(epoch & 0x3fffffffu) << 32) | v;
+}
+
+__global__ __launch_bounds__(FMT_WAVE_LINES) void k_fleet_rows(FleetFormatArgs a) {
+  __shared__ __align__(16) char stage[FLEET_LDS];
   const int32_t n = a.n_slots * a.n_lags;
-  if (i == n) { a.len[n] = 0; return; }
-  if (i > n) return;
+  const int32_t i = (int32_t)blockIdx.x * FMT_WAVE_LINES + (int32_t)threadIdx.x;
+  const int lane = (int)threadIdx.x;
   bool fb = false;
-  fleet_row<false>(a, i, nullptr, a.len, fb);
-  if (fb) atomicAdd(a.fallback, 1);
-}
-
-__global__ __launch_bounds__(256) void k_fleet_write(FleetFormatArgs a) {
-  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.n_slots * a.n_lags) return;
-  bool fb = false;
-  fleet_row<true>(a, i, a.out + a.off[i], nullptr, fb);
+  const uint32_t len = i < n ? fleet_row<false>(a, i, nullptr, fb) : 0u;
+  // wave scan of the row lengths
+  uint32_t inc = len;
+#pragma unroll
+  for (int d = 1; d < FMT_WAVE_LINES; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d, FMT_WAVE_LINES);
+    if (lane >= d) inc += y;
+  }
+  const uint32_t total = __shfl(inc, FMT_WAVE_LINES - 1, FMT_WAVE_LINES);
+  // look-back: lane 0 publishes the wave's total, then sums its predecessors'
+  uint32_t prefix = 0;
+  if (lane == 0) {
+    const uint32_t b = blockIdx.x;
+    const unsigned long long ep = (unsigned long long)(a.epoch & 0x3fffffffu);
+    if (b == 0) {
+      __hip_atomic_store(&a.status[0], fleet_status(a.epoch, FST_INC, total), __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(&a.status[b], fleet_status(a.epoch, FST_AGG, total), __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      for (int32_t j = (int32_t)b - 1; j >= 0;) {
+        const unsigned long long w =
+            __hip_atomic_load(&a.status[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if (((w >> 32) & 0x3fffffffull) != ep || (w >> 62) == 0) {
+          __builtin_amdgcn_s_sleep(1);  // wave j has not published yet (it is running)
+          continue;
+        }
+        prefix += (uint32_t)w;
+        if ((w >> 62) == 2) break;
+        --j;
+      }
+      __hip_atomic_store(&a.status[b], fleet_status(a.epoch, FST_INC, prefix + total), __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (b == gridDim.x - 1) *a.total = prefix + total;
+  }
+  prefix = __shfl(prefix, 0, FMT_WAVE_LINES);
+  const uint32_t g0 = prefix, g1 = prefix + total;
+  const uint32_t off = prefix + inc - len;
+  const bool lds = (g1 - (g0 & ~3u)) <= FLEET_LDS;  // uniform across the wave
+  if (fb) atomicAdd(a.fallback, 1);  // (counted once, from the length pass)
+  bool fb2 = false;
+  if (i < n && len) fleet_row<true>(a, i, lds ? stage + (off - (g0 & ~3u)) : a.out + off, fb2);
+  __syncthreads();
+  if (lds) wave_copy_out(stage, a.out, g0, g1);
 }
 
 __global__ void k_fixed_batch(const double* x, int n, int f, char* out) {
@@ -306,19 +356,18 @@ void apm_format_fixed_batch(const double* d_x, int n, int f, char* d_out, hipStr
   if (n > 0) hipLaunchKernelGGL(k_fixed_batch, dim3((n + 255) / 256), dim3(256), 0, stream, d_x, n, f, d_out);
 }
 
-size_t apm_fleet_format_tmp_bytes(int32_t n_rows) { return apm_format_tmp_bytes(n_rows); }
+uint32_t apm_fleet_format_blocks(int32_t n_rows) {
+  return (uint32_t)((std::max<int32_t>(n_rows, 1) + FMT_WAVE_LINES - 1) / FMT_WAVE_LINES);
+}
 
-// lengths + scan + write; afterwards off[n_rows] holds the total bytes (device)
-int apm_fleet_format(FleetFormatArgs* a, void* tmp, size_t tmp_bytes, hipStream_t stream) {
+// one launch; afterwards *a->total holds the bytes written (device)
+void apm_fleet_format(FleetFormatArgs* a, hipStream_t stream) {
   const int32_t n = a->n_slots * a->n_lags;
-  if (n <= 0) return 0;
-  hipLaunchKernelGGL(k_fleet_len, dim3((n + 1 + 255) / 256), dim3(256), 0, stream, *a);
-  size_t need = tmp_bytes;
-  if (rocprim::exclusive_scan(tmp, need, a->len, a->off, 0u, (size_t)n + 1, rocprim::plus<uint32_t>(), stream) !=
-      hipSuccess)
-    return -1;
-  hipLaunchKernelGGL(k_fleet_write, dim3((n + 255) / 256), dim3(256), 0, stream, *a);
-  return 0;
+  if (n <= 0) {
+    HIP_OK(hipMemsetAsync(a->total, 0, 4, stream));
+    return;
+  }
+  hipLaunchKernelGGL(k_fleet_rows, dim3(apm_fleet_format_blocks(n)), dim3(FMT_WAVE_LINES), 0, stream, *a);
 }
 
 void apm_format_write(FormatArgs* a, hipStream_t stream) {

@@ -134,23 +134,24 @@ struct FormatArgs {
 };
 
 // fb rows: the fleet-merged per-service baseline (all ranks' series of a service), one row per
-// (service slot, LAG) with a baseline, after the moments all-reduce (format.hip)
+// (service slot, LAG) with a baseline, after the moments all-reduce (format.hip).  Every rank
+// formats the rows of its own slice of the slots [slot_lo, slot_lo + n_slots).
 struct FleetFormatArgs {
   const double* moments;   // [cap][n_lags][NSTAT][3] {n, sum of means, sum of squared means}
-  const int2* names;       // [n_slots] {offset, length} into chars
+  const int2* names;       // [all slots] {offset, length} into chars
   const char* chars;
-  int32_t n_slots, n_lags;
+  int32_t slot_lo, n_slots, n_lags;
   int32_t lag_order[MAX_LAGS], lag_value[MAX_LAGS];
   int64_t edge_ts;
   int32_t copy;            // 1: Postgres COPY rows (apm_fleet_stats), 0: fb wire lines
   int32_t ts_len;
   char ts[32];
-  uint32_t* len;           // [n_slots * n_lags + 1]
-  uint32_t* off;
+  unsigned long long* status;  // [blocks] look-back state of the one-pass offsets (epoch-tagged)
+  uint32_t epoch;          // != 0, new per launch: stale status words never match
+  uint32_t* total;         // bytes written (device)
   char* out;
   int32_t* fallback;
 };
-
 struct AlertArgs {
   const WinStat* win;         // [S]
   const ZOut* z;              // [S] for this lag
@@ -231,8 +232,9 @@ void apm_format_write(apm::FormatArgs* a, hipStream_t stream);
 void apm_alert_eval(apm::AlertArgs* a, hipStream_t stream);
 // dst[idx[i]] = val[i]; idx / val may be device views of pinned host memory
 void apm_scatter_f64(double* dst, const int32_t* idx, const double* val, int32_t n, hipStream_t stream);
-size_t apm_fleet_format_tmp_bytes(int32_t n_rows);
-int apm_fleet_format(apm::FleetFormatArgs* a, void* tmp, size_t tmp_bytes, hipStream_t stream);
+// blocks of the one-pass fb formatter for `n_rows` rows (the status array's length)
+uint32_t apm_fleet_format_blocks(int32_t n_rows);
+void apm_fleet_format(apm::FleetFormatArgs* a, hipStream_t stream);
 // after K11: the candidate count (clamped to max_n), the candidates and -- rows != 0 -- their window
 // stats and candidate-LAG z-score rows, written into host-mapped pinned buffers (device pointers
 // of hipHostMalloc memory) in candidate order

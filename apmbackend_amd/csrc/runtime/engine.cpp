@@ -535,7 +535,14 @@ Engine::~Engine() {
   if (coll_) {
     hipStreamSynchronize(coll_stream_);
     coll_.reset();
-    for (int i = 0; i < 2; ++i) { hipEventDestroy(fleet_ev_[i]); hipEventDestroy(pack_ev_[i]); }
+    if (fb_stream_) hipStreamSynchronize(fb_stream_);
+    for (int i = 0; i < 2; ++i) {
+      hipEventDestroy(fleet_ev_[i]); hipEventDestroy(pack_ev_[i]);
+      if (fb_src_ev_[i]) hipEventDestroy(fb_src_ev_[i]);
+      if (fb_ev_[i]) hipEventDestroy(fb_ev_[i]);
+    }
+    if (h_fb_total_) hipHostFree(h_fb_total_);
+    if (fb_stream_) hipStreamDestroy(fb_stream_);
     if (node_ev_) hipEventDestroy(node_ev_);
     if (h_node_send_) hipHostFree(h_node_send_);
     if (h_node_recv_) hipHostFree(h_node_recv_);
@@ -3268,7 +3275,12 @@ void Engine::fleet_setup(int32_t cap, bool lockstep) {
     fleet_buf_[i] = (double*)dmalloc(fleet_elems_ * 8);  // zeroed (and synchronised) by dmalloc
     HIP_OK(hipEventCreateWithFlags(&fleet_ev_[i], hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&pack_ev_[i], hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&fb_src_ev_[i], hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&fb_ev_[i], hipEventDisableTiming));
   }
+  // fb rows: lowest priority (off every critical path; the output lane drains them)
+  HIP_OK(hipStreamCreateWithPriority(&fb_stream_, hipStreamNonBlocking, prio_lo));
+  HIP_OK(hipHostMalloc((void**)&h_fb_total_, 16, hipHostMallocDefault));
   fleet_rounds_ = fleet_posted_ = fleet_packed_ = 0;
   if (!lockstep_ && nranks > 1)
     throw std::runtime_error("fleet baseline across ranks needs lock-step rounds (node-wide service registry)");
@@ -3391,11 +3403,19 @@ void Engine::fleet_exchange_upto(uint64_t rounds) {
     const size_t n_red = lockstep_ ? std::min<size_t>(reg_names_.size(), (size_t)fleet_cap_) * per_svc
                                    : (size_t)fleet_cap_ * per_svc;
     if (!fleet_skip_solo_ && n_red) coll_->all_reduce_f64(fleet_buf_[slot], n_red, /*max=*/false, coll_stream_);
-    if (pack_edge_[slot] && want(OUT_FB) && coll_->rank() == 0) fleet_emit_fb(slot);
+    // fb rows: every rank its slice, on the fb stream behind this all-reduce -- the next batch's
+    // clock all-reduce on this in-order stream never waits for formatting
+    bool fb_queued = false;
+    if (pack_edge_[slot] && want(OUT_FB)) {
+      HIP_OK(hipEventRecord(fb_src_ev_[slot], coll_stream_));
+      fb_queued = fleet_emit_fb(slot);
+    }
     // edges are identical on every rank only in lock-step mode (fleet_setup refuses multi-rank
     // without it): the extra all-reduce must never pair with another rank's fleet all-reduce
     if (pack_edge_[slot] && (lockstep_ || fleet_nranks_ == 1)) node_metrics_round();
-    HIP_OK(hipEventRecord(fleet_ev_[slot], coll_stream_));
+    // the slot is free again (its next pack may overwrite it) once the all-reduce -- and the fb
+    // rows reading it, which wait for the all-reduce -- are done
+    HIP_OK(hipEventRecord(fleet_ev_[slot], fb_queued ? fb_stream_ : coll_stream_));
     if (node_mode_) node_round(fleet_rounds_, /*wait=*/false);
     ++fleet_rounds_;
   }

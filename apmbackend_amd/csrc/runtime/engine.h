@@ -623,9 +623,10 @@ class Engine {
   int32_t* d_fb_names_ = nullptr;
   size_t fb_names_cap_ = 0;
   int32_t fb_slots_up_ = 0;
-  uint32_t *d_fb_len_ = nullptr, *d_fb_off_ = nullptr;
-  void* d_fb_tmp_ = nullptr;
-  size_t fb_tmp_bytes_ = 0;
+  unsigned long long* d_fb_status_ = nullptr;  // one-pass formatter's look-back words (+ 2 totals)
+  uint32_t fb_status_n_ = 0, fb_epoch_ = 0;
+  hipStream_t fb_stream_ = nullptr;          // fb formatting (low priority; never the collective stream)
+  hipEvent_t fb_src_ev_[2] = {nullptr, nullptr};   // moments slot all-reduced (coll stream)
   char* d_fb_out_[2] = {nullptr, nullptr};
   size_t fb_out_cap_[2] = {0, 0};
   char* h_fb_out_[2] = {nullptr, nullptr};
@@ -635,8 +636,7 @@ class Engine {
   uint64_t fb_task_[2] = {0, 0};
   int fb_k_ = 0;
   uint64_t fb_rows_ = 0;
-  int32_t fb_rows_cap_ = 0;
-  void fleet_emit_fb(int slot);              // ingest thread, after the slot's all-reduce
+  bool fleet_emit_fb(int slot);              // ingest thread, after the slot's all-reduce
   bool node_all_sent_ = true;              // every rank's last round sent everything
   uint8_t* d_node_send_ = nullptr;
   uint8_t* d_node_recv_ = nullptr;

@@ -15,8 +15,9 @@
 // the stats thread finished batch k - 2 on every rank, so block contents do not depend on thread
 // timing and the slot numbering is deterministic.
 //
-// fb rows (rank 0): after the all-reduce of a batch whose stats performed a rollover, K12's fleet
-// formatter (format.hip) turns the merged moments into one row per (service, LAG) -- the fleet
+// fb rows (every rank, its slice of the slots): after the all-reduce of a batch whose stats
+// performed a rollover, K12's fleet formatter (format.hip) turns the merged moments into one row
+// per (service, LAG) -- the fleet
 // mean and spread of the per-JVM z-score baselines ("is getFoo slow on one JVM or everywhere?",
 // SURVEY §2.4) -- either as `fb|...` wire lines or as COPY rows for the DB sink
 // (apm_fleet_stats), D2H'd and emitted by the output lane.
@@ -142,57 +143,70 @@ void Engine::reg_round() {
   }
 }
 
-void Engine::fleet_emit_fb(int slot) {
-  const int32_t n_slots = (int32_t)reg_names_.size();
-  if (n_slots == 0) return;
+// fb rows of the exchange in moments slot `slot`, formatted on fb_stream_ (low priority) after
+// the all-reduce (fb_src_ev_) -- never on the collective stream, where the next batch's 16-byte
+// clock all-reduce, which every rank's ingest thread waits for, would queue behind them.  Each
+// rank formats and emits its own slice of the service slots (all ranks hold the merged moments),
+// so the formatting cost is split N ways instead of falling on rank 0 inside every rank's step.
+// Returns true when the rows were queued (fb_stream_ then waits for fb_src_ev_[slot]).
+bool Engine::fleet_emit_fb(int slot) {
+  const int32_t n_all = (int32_t)reg_names_.size();
+  if (n_all == 0) return false;
+  const int nr = std::max(1, fleet_nranks_), me = coll_->rank();
+  const int32_t lo = (int32_t)((int64_t)n_all * me / nr), hi = (int32_t)((int64_t)n_all * (me + 1) / nr);
   const int k = fb_k_;
   fb_k_ ^= 1;
   if (!fb_lane_) fb_lane_.reset(new TaskLane());  // fb rows get their own emission lane
   fb_lane_->wait(fb_task_[k]);  // slot k's previous D2H + emission is done
-  // slot names -> device (coll stream: ordered before the format kernels)
+  // slot names -> device, on the fb stream BEFORE it waits for this exchange's all-reduce: the
+  // host waits for the upload (pageable source) and only the fb stream's earlier work, which
+  // waited for an exchange that completed long ago -- never for a peer rank
+  bool uploaded = false;
   if (fb_chars_up_ < h_fb_chars_.size()) {
     if (h_fb_chars_.size() > fb_chars_cap_) {
+      HIP_OK(hipStreamSynchronize(fb_stream_));  // (regrow frees the buffer the stream may read)
       d_fb_chars_ = (char*)regrow(d_fb_chars_, fb_chars_cap_, h_fb_chars_.size() * 2 + 4096);
       fb_chars_up_ = 0;
     }
     HIP_OK(hipMemcpyAsync(d_fb_chars_ + fb_chars_up_, h_fb_chars_.data() + fb_chars_up_,
-                          h_fb_chars_.size() - fb_chars_up_, hipMemcpyHostToDevice, coll_stream_));
-    HIP_OK(hipStreamSynchronize(coll_stream_));  // pageable source: keep it alive until copied
+                          h_fb_chars_.size() - fb_chars_up_, hipMemcpyHostToDevice, fb_stream_));
     fb_chars_up_ = h_fb_chars_.size();
+    uploaded = true;
   }
-  if (fb_slots_up_ < n_slots) {
-    if ((size_t)n_slots * 8 > fb_names_cap_) {
-      d_fb_names_ = (int32_t*)regrow(d_fb_names_, fb_names_cap_, (size_t)n_slots * 16 + 4096);
+  if (fb_slots_up_ < n_all) {
+    if ((size_t)n_all * 8 > fb_names_cap_) {
+      HIP_OK(hipStreamSynchronize(fb_stream_));
+      d_fb_names_ = (int32_t*)regrow(d_fb_names_, fb_names_cap_, (size_t)n_all * 16 + 4096);
       fb_slots_up_ = 0;
     }
     HIP_OK(hipMemcpyAsync(d_fb_names_ + 2 * fb_slots_up_, h_fb_names_.data() + 2 * fb_slots_up_,
-                          (size_t)(n_slots - fb_slots_up_) * 8, hipMemcpyHostToDevice, coll_stream_));
-    HIP_OK(hipStreamSynchronize(coll_stream_));
-    fb_slots_up_ = n_slots;
+                          (size_t)(n_all - fb_slots_up_) * 8, hipMemcpyHostToDevice, fb_stream_));
+    fb_slots_up_ = n_all;
+    uploaded = true;
   }
+  if (uploaded) HIP_OK(hipStreamSynchronize(fb_stream_));  // pageable sources: keep them alive until copied
   const int n_lags = pack_nlags_[slot];  // the LAG set of this slot's pack (a reload may have changed cfg_)
   const int32_t* lags = pack_lags_[slot];
-  const int32_t rows = n_slots * n_lags;
-  if (!d_fb_len_ || rows + 1 > (int32_t)(fb_tmp_bytes_ ? fb_rows_cap_ : 0)) {
-    if (d_fb_len_) { dfree(d_fb_len_); dfree(d_fb_off_); dfree(d_fb_tmp_); }
-    fb_rows_cap_ = std::max<int32_t>(rows + 1, 2 * fleet_cap_ * n_lags + 1);
-    d_fb_len_ = (uint32_t*)dmalloc((size_t)fb_rows_cap_ * 4);
-    d_fb_off_ = (uint32_t*)dmalloc((size_t)fb_rows_cap_ * 4);
-    fb_tmp_bytes_ = apm_fleet_format_tmp_bytes(fb_rows_cap_);
-    d_fb_tmp_ = dmalloc(fb_tmp_bytes_);
-    if (!h_fb_total_) HIP_OK(hipHostMalloc((void**)&h_fb_total_, 16, hipHostMallocDefault));
-    for (auto& e : fb_ev_)
-      if (!e) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  const int32_t rows = (hi - lo) * n_lags;
+  const uint32_t blocks = apm_fleet_format_blocks(rows);
+  if (blocks > fb_status_n_) {
+    HIP_OK(hipStreamSynchronize(fb_stream_));
+    if (d_fb_status_) dfree(d_fb_status_);
+    fb_status_n_ = std::max<uint32_t>(blocks * 2, apm_fleet_format_blocks(2 * fleet_cap_ * MAX_LAGS));
+    d_fb_status_ = (unsigned long long*)dmalloc((size_t)fb_status_n_ * 8 + 64);
   }
   size_t longest = 0;
   for (size_t i = 1; i < h_fb_names_.size(); i += 2) longest = std::max<size_t>(longest, (size_t)h_fb_names_[i]);
   const size_t cap_bytes = (size_t)rows * (260 + 2 * longest) + 64;
   if (cap_bytes > fb_out_cap_[k]) d_fb_out_[k] = (char*)regrow(d_fb_out_[k], fb_out_cap_[k], cap_bytes);
+  // the exchange's all-reduce (coll stream) before the rows read the merged moments
+  HIP_OK(hipStreamWaitEvent(fb_stream_, fb_src_ev_[slot], 0));
   FleetFormatArgs fa{};
   fa.moments = fleet_buf_[slot];
   fa.names = reinterpret_cast<const int2*>(d_fb_names_);
   fa.chars = d_fb_chars_;
-  fa.n_slots = n_slots;
+  fa.slot_lo = lo;
+  fa.n_slots = hi - lo;
   fa.n_lags = n_lags;
   std::vector<int> order(n_lags);
   for (int l = 0; l < n_lags; ++l) order[l] = l;
@@ -201,13 +215,16 @@ void Engine::fleet_emit_fb(int slot) {
   fa.edge_ts = pack_edge_[slot];
   fa.copy = fs_copy_ ? 1 : 0;
   fa.ts_len = pg_timestamp(fa.edge_ts, fa.ts);
-  fa.len = d_fb_len_;
-  fa.off = d_fb_off_;
+  fa.status = d_fb_status_;
+  fb_epoch_ = (fb_epoch_ + 1) & 0x3fffffffu;
+  if (fb_epoch_ == 0) fb_epoch_ = 1;  // (status words start zeroed: epoch 0 never matches)
+  fa.epoch = fb_epoch_;
+  fa.total = reinterpret_cast<uint32_t*>(d_fb_status_ + fb_status_n_) + k;
   fa.out = d_fb_out_[k];
   fa.fallback = d_fmt_fallback_;
-  if (apm_fleet_format(&fa, d_fb_tmp_, fb_tmp_bytes_, coll_stream_) != 0) throw std::runtime_error("fb format scan failed");
-  HIP_OK(hipMemcpyAsync(h_fb_total_ + k, d_fb_off_ + rows, 4, hipMemcpyDeviceToHost, coll_stream_));
-  HIP_OK(hipEventRecord(fb_ev_[k], coll_stream_));
+  apm_fleet_format(&fa, fb_stream_);
+  HIP_OK(hipMemcpyAsync(h_fb_total_ + k, fa.total, 4, hipMemcpyDeviceToHost, fb_stream_));
+  HIP_OK(hipEventRecord(fb_ev_[k], fb_stream_));
   char* dst = d_fb_out_[k];
   fb_task_[k] = fb_lane_->post([this, k, dst]() {
     HIP_OK(hipEventSynchronize(fb_ev_[k]));
@@ -226,6 +243,7 @@ void Engine::fleet_emit_fb(int slot) {
       emit_bytes_held(OUT_FB, h_fb_out_[k], total, 2 + k);
     }
   });
+  return true;
 }
 
 }  // namespace apm

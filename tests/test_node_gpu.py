@@ -152,7 +152,7 @@ def test_fleet_registry_merges_services_node_wide(world):
     """Ranks intern services in different orders; the moments matrix is indexed by node-wide
     slots (hash + name all-gathered in the lock-step round, assigned in rank order), so the
     merged per-service baselines of a 2/4-rank node equal the 1-rank ones service by service,
-    every rank holds the same table, and rank 0 emits the interval's fb rows."""
+    every rank holds the same table, and the ranks emit the interval's fb rows in disjoint slices."""
     import numpy as np
     lines, bl = corpus()
     servers = sorted({server_of(fp) for fp in lines})
@@ -168,16 +168,21 @@ def test_fleet_registry_merges_services_node_wide(world):
     assert set(got) == set(ref) and len(ref) >= 5
     for name in ref:
         np.testing.assert_allclose(got[name], ref[name], rtol=1e-12, atol=1e-9)
-    # fb rows: rank 0 only, one per (service, LAG) with a baseline, every interval after warm-up
-    assert all(not o["fb"] for o in outs[1:])
-    fb = outs[0]["fb"]
+    # fb rows: every rank formats and emits its own slice of the node-wide slots (the merged
+    # moments are on every rank), one row per (service, LAG) with a baseline, every interval
+    # after warm-up; the slices are disjoint and together are the 1-rank stream, row for row
+    fb = [l for o in outs for l in o["fb"]]
     assert fb and all(l.startswith("fb|") for l in fb)
-    last_ts = max(int(l.split("|")[1]) for l in fb)
-    last = [l for l in fb if int(l.split("|")[1]) == last_ts]
-    ref_last = [l for l in o1[0]["fb"] if int(l.split("|")[1]) == last_ts]
-    key = lambda l: (l.split("|")[2], l.split("|")[3])
-    assert sorted(map(key, last)) == sorted(map(key, ref_last))
-    assert engs[0].eng.fleet_info()["fb_rows"] == len(fb)
+    assert sum(1 for o in outs if o["fb"]) == world  # the formatting is split, not rank 0's alone
+    key = lambda l: (l.split("|")[1], l.split("|")[2], l.split("|")[3])
+    for o in outs:
+        assert len(set(map(key, o["fb"]))) == len(o["fb"])
+    ref_fb = o1[0]["fb"]
+    assert sorted(map(key, fb)) == sorted(map(key, ref_fb))
+    # values: fp64 sums in another order, printed to 1 dp (a last-bit tie could flip a digit)
+    same = len(set(fb) & set(ref_fb))
+    assert same >= len(ref_fb) - len(ref_fb) // 100, (same, len(ref_fb))
+    assert sum(e.eng.fleet_info()["fb_rows"] for e in engs) == len(fb)
 
 
 # ---------------------------------------------------------------- multi-PROCESS node (TCP transport)
