@@ -175,7 +175,7 @@ py::dict counters_dict(const JoinCounters& c) {
   d["partial_overflow"] = c.partial_overflow; d["need_overflow"] = c.need_overflow; d["table_full"] = c.table_full;
   d["pool_exhausted"] = c.pool_exhausted; d["chain_partial_blocks"] = c.chain_partial_blocks;
   d["chain_need_blocks"] = c.chain_need_blocks; d["chain_logid_blocks"] = c.chain_logid_blocks;
-  d["table_slots"] = c.table_slots; d["table_grows"] = c.table_grows; d["table_rebuilds"] = c.table_rebuilds;
+  d["table_slots"] = c.table_slots; d["table_grows"] = c.table_grows; d["table_rebuilds"] = c.table_rebuilds; d["trims"] = c.trims;
   d["need_arena_entries"] = c.need_arena_entries; d["arena_grows"] = c.arena_grows;
   d["chain_pool_blocks"] = c.chain_pool_blocks; d["pool_grows"] = c.pool_grows;
   d["host_events"] = c.host_events;
@@ -467,6 +467,7 @@ PYBIND11_MODULE(_apm_native, m) {
       .def("servers", &Engine::servers)
       .def("watermark", &Engine::watermark)
       .def("device_bytes", &Engine::device_bytes)
+      .def("trim_device_memory", &Engine::trim_device_memory, py::call_guard<py::gil_scoped_release>())
       .def("stream_handle", [](Engine& e) { return (uintptr_t)e.stream(); })
       .def("comm_stream_handle", [](Engine& e) { return (uintptr_t)e.comm_stream(); })
       .def_static("fleet_unique_id", []() {

@@ -265,8 +265,8 @@ __device__ bool baf_account_scan(const uint8_t* p, int a, int b, int& n, bool& d
 }
 
 // The AudF of an LK_APP event (batch-absolute refs); false when the host must derive it.
-__device__ bool aud_fields(const Event& e, const uint8_t* __restrict__ bytes, int32_t file, AudF& f) {
-  const uint8_t* p = bytes + e.off;
+// p: the line's first byte (the batch, or k_host_flags' LDS stage at the same offset mod 16).
+__device__ bool aud_fields(const Event& e, const uint8_t* __restrict__ p, int32_t file, AudF& f) {
   const int len = (int)e.len;
   f.h_item = 0; f.el = apm_nan(); f.h_sw = 0; f.ts = apm_nan();
   f.ref = 0; f.len = 0; f.flags = 0; f.pad = 0; f.pad2[0] = f.pad2[1] = 0;
@@ -375,9 +375,8 @@ __device__ void angle_field2_dev(const uint8_t* __restrict__ p, int len, int& fs
   if (seen == 2) { fs = start; fe = b; }
 }
 
-__device__ int pre_fields(const Event& e, const uint8_t* __restrict__ bytes, AudF& f, bool bytewise) {
+__device__ int pre_fields(const Event& e, const uint8_t* __restrict__ p, AudF& f, bool bytewise) {
   if (e.mask & PM_HOST) return -1;
-  const uint8_t* p = bytes + e.off;
   f.h_item = 0; f.el = apm_nan(); f.h_sw = 0; f.ts = apm_nan(); f.ref = 0; f.len = 0; f.flags = 0; f.pad = 0;
   if (e.kind >= LK_EJB_ENTRY && e.kind <= LK_CT_EXIT) {
     if (!(e.mask & PM_KEYS) || e.ntok < 3) return -1;
@@ -439,11 +438,51 @@ __device__ __forceinline__ SelCount sel_unpack(uint64_t v) {
 }
 
 // Per event: host / audit-list flags and counts; the AudF of every audit line the GPU reads
-// (computed once here, on the parse stream, and read by the join's k_build_ops)
-__global__ void k_host_flags(const Event* __restrict__ ev, const uint32_t* __restrict__ n_ev_dev,
-                             const uint8_t* __restrict__ bytes, const uint32_t* __restrict__ chunk_file,
-                             uint8_t* __restrict__ flag, uint64_t* __restrict__ val, AudF* __restrict__ aud,
-                             SelCount* __restrict__ totals, uint32_t cap, int bytewise) {
+// (computed once here, on the parse stream, and read by the join's k_build_ops).
+//
+// The byte work (the audit line scan, the SOAP logId / account fields, the BAF account token) is
+// a lane walking its own line.  Reading the batch directly, every step of those walks waited on
+// a dependent global load: 130 us a batch for ~45k events (profiles/r4_x, the largest kernel of
+// the join side).  Now each lane first copies its line into an LDS slot with independent 16-byte
+// loads (all in flight at once: one memory latency per line), at the same offset modulo 16 so
+// the walks' aligned vector reads stay aligned, and walks it there.  Lines longer than a slot
+// (rare) walk the batch as before.  APM_HF_STAGE=0 keeps the unstaged walk (A/B).
+constexpr int HF_SLOT = 256;  // staged bytes per lane (64 KB per 256-lane block: 2 blocks per CU)
+
+__device__ __forceinline__ bool hf_needs_bytes(const Event& e) {
+  if (e.kind == LK_APP) return !(e.mask & PM_HOST);
+  if (e.mask & PM_HOST) return false;
+  if (e.kind == LK_CT_EXIT) return (e.mask & PM_KEYS) && e.ntok >= 3 && (e.mask & PM_BAF);
+  if (e.kind == LK_SOAP) return (e.mask & (PM_SOAP_IN | PM_SOAP_ACCT | PM_SOAP_VALUE)) != 0;
+  return false;
+}
+
+__device__ __forceinline__ uint8_t hf_fields(const Event& e, const uint8_t* __restrict__ p, int32_t file, AudF* aud,
+                                             uint32_t i, int bytewise) {
+  uint8_t fl = 0;
+  if (e.kind == LK_APP) {
+    bool host = (e.mask & PM_HOST) != 0;
+    if (!host) {
+      AudF f;
+      host = !aud_fields(e, p, file, f);
+      if (!host) aud[i] = f;
+    }
+    if (host) fl |= SEL_HOST;
+  } else {
+    AudF f;
+    const int r = pre_fields(e, p, f, bytewise != 0);
+    if (r < 0) fl |= SEL_HOST;
+    else if (r > 0) aud[i] = f;  // read by k_build_ops
+  }
+  return fl;
+}
+
+__global__ __launch_bounds__(TB) void k_host_flags(const Event* __restrict__ ev, const uint32_t* __restrict__ n_ev_dev,
+                                                   const uint8_t* __restrict__ bytes, const uint32_t* __restrict__ chunk_file,
+                                                   uint8_t* __restrict__ flag, uint64_t* __restrict__ val,
+                                                   AudF* __restrict__ aud, SelCount* __restrict__ totals, uint32_t cap,
+                                                   int bytewise, int staged) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage[TB * HF_SLOT];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t n = min(*n_ev_dev, cap);
   if (blockIdx.x * blockDim.x >= n) return;  // (uniform per block: the grid is sized for the capacity)
@@ -451,20 +490,26 @@ __global__ void k_host_flags(const Event* __restrict__ ev, const uint32_t* __res
   uint32_t ab = 0;
   if (i < n) {
     const Event e = ev[i];
-    if (e.kind == LK_APP) {
-      bool host = (e.mask & PM_HOST) != 0;
-      if (!host) {
-        AudF f;
-        host = !aud_fields(e, bytes, (int32_t)chunk_file[e.chunk], f);
-        if (!host) aud[i] = f;
-      }
-      if (host) fl |= SEL_HOST;
-    } else {
-      AudF f;
-      const int r = pre_fields(e, bytes, f, bytewise != 0);
-      if (r < 0) fl |= SEL_HOST;
-      else if (r > 0) aud[i] = f;  // read by k_build_ops
+    const int32_t file = e.kind == LK_APP ? (int32_t)chunk_file[e.chunk] : 0;
+    // (staging only decides where the walk reads: a staged line is a complete copy, so the field
+    // functions -- which read bytes only in the cases hf_needs_bytes names -- are unchanged)
+    const uint8_t* p = bytes + e.off;
+    const uint32_t lead = e.off & 15u;
+    const uint32_t nvec = (lead + e.len + 15u) >> 4;
+    if (staged && hf_needs_bytes(e) && nvec * 16u <= (uint32_t)HF_SLOT) {
+      // the line's aligned 16-byte blocks, every load issued before the first LDS store
+      const uint4* __restrict__ src = reinterpret_cast<const uint4*>(bytes + (e.off - lead));
+      uint4* dst = reinterpret_cast<uint4*>(stage + threadIdx.x * HF_SLOT);
+      uint4 v[HF_SLOT / 16];
+#pragma unroll
+      for (int k = 0; k < HF_SLOT / 16; ++k)
+        if ((uint32_t)k < nvec) v[k] = src[k];
+#pragma unroll
+      for (int k = 0; k < HF_SLOT / 16; ++k)
+        if ((uint32_t)k < nvec) dst[k] = v[k];
+      p = stage + threadIdx.x * HF_SLOT + lead;
     }
+    fl = hf_fields(e, p, file, aud, i, bytewise);
     if (e.kind == LK_APP) {
       if (e.mask & PM_AUTR_MAP) fl |= SEL_MH;
       else fl |= SEL_WALK | ((e.mask & PM_AUTR_HDR) ? SEL_MH : 0);
@@ -2257,11 +2302,15 @@ static int pre_bytewise() {
   static const int v = [] { const char* e = std::getenv("APM_PRE_BYTEWISE"); return e && e[0] == '1' ? 1 : 0; }();
   return v;
 }
+static int hf_staged() {
+  static const int v = [] { const char* e = std::getenv("APM_HF_STAGE"); return e && e[0] == '0' ? 0 : 1; }();
+  return v;
+}
 int apm_dj_select_host(DJArgs* a, const uint32_t* d_n_ev, uint32_t max_ev, hipStream_t s) {
   HIP_OK(hipMemsetAsync(a->n_host, 0, sizeof(SelCount), s));
   if (max_ev == 0) return 0;
   hipLaunchKernelGGL(k_host_flags, dim3((max_ev + TB - 1) / TB), dim3(TB), 0, s, a->ev, d_n_ev, a->bytes, a->chunk_file,
-                     a->host_flag, a->sel_val, a->aud, a->n_host, max_ev, pre_bytewise());
+                     a->host_flag, a->sel_val, a->aud, a->n_host, max_ev, pre_bytewise(), hf_staged());
   dj_check(s, "k_host_flags");
   // sel_pos: the tile sums, then the packed total (sel_pos has max_ev + 64 entries)
   uint64_t* total = a->sel_pos + (max_ev + DS_TILE - 1) / DS_TILE + 1;

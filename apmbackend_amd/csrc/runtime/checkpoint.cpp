@@ -1036,9 +1036,7 @@ int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& e
     job->lags.push_back(std::move(lg));
   }
   if (need > ck_stage_bytes_) {
-    if (d_ck_stage_) HIP_OK(hipFree(d_ck_stage_));
-    d_ck_stage_ = nullptr;
-    ck_stage_bytes_ = 0;
+    free_ck_stage();
     const size_t want = need + need / 8;  // room for the series table to grow
     if (hipMalloc(&d_ck_stage_, want) != hipSuccess) {
       (void)hipGetLastError();
@@ -1056,6 +1054,8 @@ int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& e
       return job->seq;
     }
     ck_stage_bytes_ = want;
+    std::lock_guard<std::mutex> g(alloc_mu_);
+    device_bytes_ += want;
   }
   for (int l = 0; l < cfg_.n_lags; ++l) {
     const CkJob::Lag& lg = job->lags[l];
@@ -1090,6 +1090,15 @@ int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& e
   if (!ck_thread_.joinable()) ck_thread_ = std::thread([this] { checkpoint_writer(); });
   ck_cv_.notify_all();
   return job->seq;
+}
+
+void Engine::free_ck_stage() {
+  if (!d_ck_stage_) return;
+  HIP_OK(hipFree(d_ck_stage_));
+  d_ck_stage_ = nullptr;
+  std::lock_guard<std::mutex> g(alloc_mu_);
+  device_bytes_ -= ck_stage_bytes_;
+  ck_stage_bytes_ = 0;
 }
 
 void Engine::checkpoint_writer() {
@@ -1193,7 +1202,7 @@ void Engine::checkpoint_shutdown() {
   }
   ck_cv_.notify_all();
   if (ck_thread_.joinable()) ck_thread_.join();
-  if (d_ck_stage_) { hipFree(d_ck_stage_); d_ck_stage_ = nullptr; }
+  if (d_ck_stage_) { hipFree(d_ck_stage_); d_ck_stage_ = nullptr; ck_stage_bytes_ = 0; }
   if (h_ck_bounce_) { hipHostFree(h_ck_bounce_); h_ck_bounce_ = nullptr; }
   if (ck_ev_) { hipEventDestroy(ck_ev_); ck_ev_ = nullptr; }
   if (ck_stream_) { hipStreamDestroy(ck_stream_); ck_stream_ = nullptr; }

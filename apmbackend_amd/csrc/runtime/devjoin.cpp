@@ -107,6 +107,8 @@ DeviceJoin::DeviceJoin(const DevJoinConfig& cfg, Dictionary* dict, const std::ve
   }
   table_bits_ = cfg_.table_bits;
   table_cap_ = 1u << table_bits_;
+  init_table_cap_ = table_cap_;
+  init_arena_cap_ = cfg_.arena_cap;
   d_table_ = (KeyState*)dmalloc((size_t)table_cap_ * sizeof(KeyState));
   d_reg_ = (RegSlot*)dmalloc(((size_t)1 << cfg_.reg_bits) * sizeof(RegSlot));
   miss_cap_ = E;
@@ -1164,6 +1166,52 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
   phase_t[8] = clock_ms();
 }
 
+size_t DeviceJoin::trim(double now) {
+  hipStream_t st = stream_;
+  HIP_OK(hipStreamSynchronize(st));
+  if (live_pending_) {
+    HIP_OK(hipEventSynchronize(live_ev_));
+    keys_live_ = *h_live_;
+    live_pending_ = false;
+  }
+  const size_t before = device_bytes_;
+  const uint64_t tg = table_grows_, ag = arena_grows_;  // (a shrink is not a growth event)
+  auto pow2_at_least = [](uint64_t v) { uint64_t p = 1; while (p < v) p <<= 1; return p; };
+  // key table: an exact live count first (same-size rebuild, expired keys dropped at `now`)
+  rebuild_table(now, table_cap_);
+  const uint64_t want = std::max<uint64_t>(init_table_cap_, pow2_at_least(std::max<uint64_t>(keys_live_ * 4, 8)));
+  if (want < table_cap_) rebuild_table(now, (uint32_t)want);  // reinserts into a fresh, smaller table
+  if (d_table_spare_) {  // (re-made on demand: checkpoint compaction, APM_REBUILD_COPY)
+    dfree(d_table_spare_, (size_t)table_cap_ * sizeof(KeyState));
+    d_table_spare_ = nullptr;
+    spare_clean_ = false;
+  }
+  if (d_rb_scratch_) {  // sized by the table: re-made by the next in-place rebuild
+    dfree(d_rb_scratch_, rb_scratch_bytes_);
+    d_rb_scratch_ = nullptr;
+    rb_scratch_bytes_ = 0;
+  }
+  // need arena: live entries [lo, head) move into a smaller ring (their virtual indices stay)
+  {
+    const uint64_t lo = regions_.empty() ? arena_head_ : regions_.front().lo;
+    const uint64_t live = arena_head_ - lo;
+    const uint64_t acap = std::max<uint64_t>(init_arena_cap_, pow2_at_least(std::max<uint64_t>(live * 4, 1024)));
+    if (acap < cfg_.arena_cap) grow_arena((uint32_t)acap, lo);
+  }
+  // tx / audit text staging of the write pass (re-made by the next batch that needs it)
+  if (d_txt_tx_) {
+    HIP_OK(hipFree(d_txt_tx_));
+    device_bytes_ -= txt_cap_ * 2;
+    d_txt_tx_ = d_txt_db_ = nullptr;
+    txt_cap_ = 0;
+  }
+  HIP_OK(hipStreamSynchronize(st));
+  table_grows_ = tg;
+  arena_grows_ = ag;
+  ++trims_;
+  return before > device_bytes_ ? before - device_bytes_ : 0;
+}
+
 std::vector<uint64_t> DeviceJoin::cache_stats(double now) {
   if (!d_cstats_) d_cstats_ = (unsigned long long*)dmalloc(64);
   unsigned long long h[5] = {0, 0, 0, 0, 0};
@@ -1195,6 +1243,7 @@ JoinCounters DeviceJoin::counters() const {
   t.table_slots = table_cap_;
   t.table_grows = table_grows_;
   t.table_rebuilds = table_rebuilds_;
+  t.trims = trims_;
   t.need_arena_entries = cfg_.arena_cap;
   t.arena_grows = arena_grows_;
   t.chain_pool_blocks = pool_n_;

@@ -126,6 +126,10 @@ class DeviceJoin {
   std::vector<std::pair<const char*, std::pair<double, double>>> save_spans;  // spans of the last save()
   const JoinCounts& last_counts() const { return *h_counts_; }
   size_t device_bytes() const { return device_bytes_; }
+  // requestGC (join stream idle, between batches): the grow-only key table and need arena go
+  // back to the smallest power of two (not below their configured size) that keeps their live
+  // entries at <= 1/4 load, the spare table and text staging are released.  Returns bytes freed.
+  size_t trim(double now);
 
  private:
   struct Slot {
@@ -202,6 +206,7 @@ class DeviceJoin {
   void dfree(void* p, size_t bytes);
 
   DevJoinConfig cfg_;
+  uint32_t init_table_cap_ = 0, init_arena_cap_ = 0;  // configured sizes: trim never goes below
   Dictionary* dict_;
   const std::vector<FileInfo>* files_;
   const std::vector<std::string>* servers_;
@@ -258,7 +263,7 @@ class DeviceJoin {
   uint32_t pool_n_ = 0;                // blocks (power of two)
   unsigned long long* h_live_ = nullptr;  // pinned
   // growth events (reported in counters())
-  uint64_t table_grows_ = 0, arena_grows_ = 0, pool_grows_ = 0, table_rebuilds_ = 0;
+  uint64_t table_grows_ = 0, arena_grows_ = 0, pool_grows_ = 0, table_rebuilds_ = 0, trims_ = 0;
   RegSlot* d_reg_ = nullptr;
   RegMiss* d_miss_ = nullptr;
   RegMiss* h_miss_ = nullptr;

@@ -296,8 +296,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     dc.need_ttl_ms = cfg_.need_ttl_ms;
     dc.tz = cfg_.tz;
     dc.device = cfg_.device;
-    dj_.reset(new DeviceJoin(dc, &dict_, &files_, &servers_));
-    device_bytes_ += dj_->device_bytes();
+    dj_.reset(new DeviceJoin(dc, &dict_, &files_, &servers_));  // (its bytes: device_bytes())
     d_ring_min_ = (unsigned long long*)dmalloc(64);
     HIP_OK(hipMemset(d_ring_min_, 0xff, 8));  // (the export after each min pass restores it)
     HIP_OK(hipHostMalloc((void**)&h_ring_min_, 64, hipHostMallocDefault));
@@ -351,6 +350,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   d_counts_cells_ = (int32_t*)dmalloc((size_t)NSLOT * S * 4);
   d_cells_ = (int32_t*)dmalloc((size_t)NSLOT * S * cfg_.cell_cap * 4);
   d_spill_n_ = (int32_t*)dmalloc(NSLOT * 4);
+  init_spill_cap_ = cfg_.spill_cap;
   d_spill_series_ = (int32_t*)dmalloc((size_t)NSLOT * cfg_.spill_cap * 4);
   d_spill_val_ = (int32_t*)dmalloc((size_t)NSLOT * cfg_.spill_cap * 4);
   d_spill_series_alt_ = (int32_t*)dmalloc((size_t)NSLOT * cfg_.spill_cap * 4);
@@ -1723,12 +1723,18 @@ void Engine::spill_marked() {
 
 // Every slot list keeps its entries at the same positions of a longer row.
 void Engine::grow_spill(int32_t cap) {
+  resize_spill(cap);
+  ++metrics_.spill_grows;
+}
+
+void Engine::resize_spill(int32_t cap) {
   HIP_OK(hipStreamSynchronize(stream_));
   const size_t old = (size_t)cfg_.spill_cap;
+  const size_t w = std::min(old, (size_t)cap) * 4;  // (a shrink keeps every slot's fill: cap >= it)
   int32_t* ser = (int32_t*)dmalloc((size_t)NSLOT * cap * 4);
   int32_t* val = (int32_t*)dmalloc((size_t)NSLOT * cap * 4);
-  HIP_OK(hipMemcpy2DAsync(ser, (size_t)cap * 4, d_spill_series_, old * 4, old * 4, NSLOT, hipMemcpyDeviceToDevice, stream_));
-  HIP_OK(hipMemcpy2DAsync(val, (size_t)cap * 4, d_spill_val_, old * 4, old * 4, NSLOT, hipMemcpyDeviceToDevice, stream_));
+  HIP_OK(hipMemcpy2DAsync(ser, (size_t)cap * 4, d_spill_series_, old * 4, w, NSLOT, hipMemcpyDeviceToDevice, stream_));
+  HIP_OK(hipMemcpy2DAsync(val, (size_t)cap * 4, d_spill_val_, old * 4, w, NSLOT, hipMemcpyDeviceToDevice, stream_));
   HIP_OK(hipStreamSynchronize(stream_));
   dfree(d_spill_series_);
   dfree(d_spill_val_);
@@ -1742,8 +1748,40 @@ void Engine::grow_spill(int32_t cap) {
   cfg_.spill_cap = cap;
   spill_tmp_bytes_ = apm_spill_sort_tmp_bytes(cfg_.spill_cap, cfg_.max_series);
   d_spill_tmp_ = dmalloc(spill_tmp_bytes_);
-  ++metrics_.spill_grows;
   metrics_.spill_capacity = cap;
+}
+
+std::pair<size_t, size_t> Engine::trim_device_memory() {
+  checkpoint_wait();  // the writer reads the staging buffer
+  flush();            // the stats thread, rollover lane and output lane idle
+  const size_t before = device_bytes();
+  HIP_OK(hipStreamSynchronize(stream_));
+  if (dj_) dj_->trim(watermark_);
+  // spill lists: back to max(configured, 2x the fullest slot)
+  {
+    std::vector<int32_t> fill(NSLOT);
+    HIP_OK(hipMemcpy(fill.data(), d_spill_n_, NSLOT * 4, hipMemcpyDeviceToHost));
+    int32_t mx = 0;
+    for (int32_t f : fill) mx = std::max(mx, std::min(f, cfg_.spill_cap));
+    const int32_t want = std::max<int32_t>(init_spill_cap_, ((2 * mx + 1023) / 1024) * 1024);
+    if (want < cfg_.spill_cap) resize_spill(want);
+  }
+  // checkpoint packing scratch and the incremental checkpoint's staging (re-made by the next one;
+  // a staging allocation that then fails falls back to the synchronous writer)
+  for (void** q : {(void**)&d_ck_lens_, (void**)&d_ck_offs_, (void**)&d_ck_packed_, &d_ck_ptmp_}) {
+    dfree(*q);
+    *q = nullptr;
+  }
+  ck_pack_n_ = 0;
+  ck_ptmp_bytes_ = 0;
+  for (int k = 0; k < 2; ++k) {
+    dfree(d_ck_text_[k]);
+    d_ck_text_[k] = nullptr;
+    ck_text_cap_[k] = 0;
+  }
+  free_ck_stage();
+  HIP_OK(hipStreamSynchronize(stream_));
+  return {before, device_bytes()};
 }
 
 // before K8: each slot's list sorted by series (stable), the live and sort buffers swapped

@@ -410,7 +410,14 @@ class Engine {
   double watermark() const { return watermark_; }
   hipStream_t stream() const { return stream_; }
   hipStream_t comm_stream() const { return stream_; }  // (the stats stream: callers flush() first)
-  size_t device_bytes() const { return device_bytes_; }
+  // HBM held: the engine's own buffers plus the device join's (which grow and shrink)
+  size_t device_bytes() const { return device_bytes_ + (dj_ ? dj_->device_bytes() : 0); }
+  // requestGC (util_methods.js:398-417 runGC, sent by apm_manager.js:475-512 on a memory
+  // threshold): between batches, hand grow-only device memory back -- the join's key table and
+  // need arena shrink to their live entries (>= their configured size), spill lists above 2x
+  // their fill, checkpoint packing scratch and staging (re-made on demand).  Returns
+  // {bytes before, bytes after}.
+  std::pair<size_t, size_t> trim_device_memory();
   JoinCounters join_counters() const;
   // join-cache occupancy (device join: a reduction over the key table at the watermark clock;
   // host join: the shards' map sizes): {slots, occupied, acct, record, partials, need}
@@ -883,6 +890,9 @@ class Engine {
   std::string load_small_state(const std::string& path);
   void apply_ring_file(const std::string& path);
   void checkpoint_writer();
+  void free_ck_stage();
+  void resize_spill(int32_t cap);  // grow_spill / the trim (cap >= every slot's fill)
+  int32_t init_spill_cap_ = 0;
   void finish_chain(const std::shared_ptr<CkJob>& job, uint64_t bytes);
   void checkpoint_shutdown();
   std::mutex ck_mu_;

@@ -98,7 +98,7 @@ struct JoinCounters {
   // device join capacity: losses (must stay 0: every structure grows) and growth / chain use
   uint64_t partial_overflow = 0, need_overflow = 0, table_full = 0, pool_exhausted = 0;
   uint64_t chain_partial_blocks = 0, chain_need_blocks = 0, chain_logid_blocks = 0;
-  uint64_t table_slots = 0, table_grows = 0, table_rebuilds = 0, need_arena_entries = 0, arena_grows = 0;
+  uint64_t table_slots = 0, table_grows = 0, table_rebuilds = 0, need_arena_entries = 0, arena_grows = 0, trims = 0;
   uint64_t chain_pool_blocks = 0, pool_grows = 0;
   uint64_t host_events = 0;  // events resolved by the host pre-pass (audit blocks, PM_HOST lines)
 };

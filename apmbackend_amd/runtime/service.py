@@ -673,7 +673,7 @@ class IngestService:
                 self.watcher.check_once()
             except Exception as e:  # a broken config must not stop ingest
                 log.error("config reload failed: %s", e)
-        if self._gc_requested:
+        if self._gc_requested and self._held is None:  # (a held prefetch: the next poll does not prefetch)
             self._gc_requested = False
             self.request_gc()
         if self.ckpt_dir and self.eng is not None and now - self.last_ckpt >= self.ckpt_every:
@@ -736,7 +736,15 @@ class IngestService:
             log.info(self.qm.stats.line())
 
     def request_gc(self) -> str:
-        """requestGC: collect Python garbage and hand freed heap back to the OS."""
+        """requestGC (util_methods.js:398-417): collect Python garbage and hand freed heap back to
+        the OS, and -- the engine's share of a process is mostly HBM -- give the grow-only device
+        structures back (join key table / need arena shrunk to their live entries, spill lists,
+        checkpoint scratch), at this batch boundary."""
+        hbm = ""
+        trim = getattr(self.native, "trim_device_memory", None)
+        if trim is not None and self._held is None:
+            before, after = trim()
+            hbm = f" hbm={before / 2**30:.3f} GB -> {after / 2**30:.3f} GB"
         gc.collect()
         try:
             ctypes.CDLL("libc.so.6").malloc_trim(0)
@@ -748,7 +756,7 @@ class IngestService:
                 rss = int(f.read().split()[1]) * os.sysconf("SC_PAGE_SIZE")
         except OSError:
             pass
-        msg = f"Running garbage collection! rss={rss / 2**20:.1f} MB"
+        msg = f"Running garbage collection! rss={rss / 2**20:.1f} MB{hbm}"
         log.info(msg)
         return msg
 
@@ -856,7 +864,7 @@ class IngestService:
             return n
         dup = mine and fi.get("duplicateBatchEvery") and self.polls % int(fi["duplicateBatchEvery"]) == 0
         nxt = None
-        if not paused and not dup and not self._ckpt_due() and not self._stopping:
+        if not paused and not dup and not self._ckpt_due() and not self._stopping and not self._gc_requested:
             nxt = self.tailer.next(0.0)
         if self.batch_log is not None:
             import ctypes

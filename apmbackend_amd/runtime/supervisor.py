@@ -561,6 +561,7 @@ class Supervisor:
                 if gthr and vram > float(gthr):
                     self.add_alert(f"Child module exceeded the GPU memory threshold - Module: {p.name} "
                                    f"Threshold(Mb): {gthr} HBMUsed(Mb): {vram:.1f}")
+                    trigger = True  # the child's requestGC trims its grow-only device memory
                 if trigger:
                     log.info("Sending garbage collection request to module: %s", p.name)
                     self.gc_requests.append(p.name)

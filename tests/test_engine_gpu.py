@@ -721,6 +721,76 @@ def test_join_tables_grow_instead_of_failing(tmp_path, restore):
     assert j2["pool_exhausted"] == 0
 
 
+def _burst_then_trickle(seed=21):
+    """jvm00: a burst of 40 tx/s (2-5 provider calls each) in the first 30 s, then silence;
+    jvm01: 1 tx/s from 200 s on.  The burst grows the join tables; once the trickle has moved the
+    watermark past the 120 s TTLs, the burst's keys are dead."""
+    a = Generator(SynthConfig(servers=2, duration_s=420, tx_per_sec_per_server=40, seed=seed, ejb_services=6,
+                              provider_services=8, sub_calls=(2, 5))).generate()
+    b = Generator(SynthConfig(servers=2, duration_s=420, tx_per_sec_per_server=1, seed=seed + 1,
+                              ejb_services=6, provider_services=8)).generate()
+    lines = {}
+    for f, v in a.items():
+        if "/jvm00/" in f:
+            lines[f] = [x for x in v if x[0] < START + 30_000]
+    for f, v in b.items():
+        if "/jvm01/" in f:
+            lines[f] = [x for x in v if x[0] >= START + 200_000]
+    return with_watermarks(batches(lines, START, 5.0), UTC)
+
+
+def test_bursty_all_new_key_batches_never_fill_the_table():
+    """a burst of all-new logIds, a quiet stretch (its keys expire), new keys again, on
+    a 1024-slot key table.  The stream-ordered rebuild is only taken when the worst case -- every
+    key claimed since the last live count still live, plus the batch -- fits 5/8 of the table;
+    otherwise the join waits for the count and grows.  No op may be dropped (table_full == 0) and
+    the streams equal the oracle."""
+    bl = _burst_then_trickle()
+    C = small_cfg("exact")
+    C["gpu"].update({"joinTableSlots": 1024, "needArenaEntries": 1024, "joinChainBlocks": 1024})
+    P = PipelineOracle(copy.deepcopy(C), UTC)
+    P.run_batches(bl)
+    eng, out = _run_engine(C, bl)
+    _assert_streams(out, P)
+    j = eng.metrics()["join"]
+    assert j["table_full"] == 0 and j["partial_overflow"] == 0 and j["need_overflow"] == 0, j
+    assert j["table_rebuilds"] > 2 and j["table_grows"] > 0, j
+
+
+def test_request_gc_trims_device_memory():
+    """requestGC for HBM (util_methods.js:398-417 runGC, apm_manager.js:475-512): a burst grows
+    the join's key table; once its keys expired, trim_device_memory at a batch boundary shrinks
+    the table back to its live entries (never below the configured size) and frees the
+    checkpoint scratch, and the pipeline continues with outputs equal to the oracle."""
+    bl = _burst_then_trickle(seed=31)
+    C = small_cfg("exact")
+    C["gpu"].update({"joinTableSlots": 1024, "needArenaEntries": 1024, "joinChainBlocks": 1024})
+    P = PipelineOracle(copy.deepcopy(C), UTC)
+    P.run_batches(bl)
+    eng = APMEngine(C, keep_text=True)
+    out = collections.defaultdict(list)
+    cut = next(i for i, (now, _c) in enumerate(bl) if now > START + 360_000)
+    for now, chunks in bl[:cut]:
+        eng.process_lines(chunks, now)
+        for k in ("transactions", "audit_db", "st", "fs", "al"):
+            out[k] += eng.take(k)
+    j0 = eng.metrics()["join"]
+    assert j0["table_slots"] > 1024, j0
+    before, after = eng.eng.trim_device_memory()
+    j1 = eng.metrics()["join"]
+    assert after < before and eng.eng.device_bytes() == after, (before, after)
+    assert j1["trims"] == 1 and j1["table_slots"] < j0["table_slots"], (j0["table_slots"], j1["table_slots"])
+    assert j1["table_slots"] >= 1024 and j1["need_arena_entries"] >= 1024
+    assert j1["table_grows"] == j0["table_grows"]  # (a shrink is not counted as growth)
+    for now, chunks in bl[cut:]:
+        eng.process_lines(chunks, now)
+        for k in ("transactions", "audit_db", "st", "fs", "al"):
+            out[k] += eng.take(k)
+    _assert_streams(out, P)
+    j2 = eng.metrics()["join"]
+    assert j2["table_full"] == 0 and j2["partial_overflow"] == 0 and j2["need_overflow"] == 0
+
+
 def test_fatal_error_leaves_a_state_dump(tmp_path):
     """A fatal engine error (here: a batch larger than gpu.batchBytes -- the same path as a HIP
     error or a capacity throw) leaves a host-side state dump next to the checkpoints before the
