@@ -87,7 +87,7 @@ constexpr int32_t ELAPSED_NAN = (int32_t)0x80000000;
 // ----------------------------------------------------------------------------- stats / z-score
 constexpr int NSLOT = 40;          // bucket ring slots per series (window 31 + buffer + slack)
 constexpr int NSTAT = 3;           // avg, p75, p95
-constexpr int MAX_LAGS = 4;
+constexpr int MAX_LAGS = 8;           // LAG settings per engine (the reference: any number)
 
 // Per-series window statistics produced at a rollover (values already rounded the way the
 // z-score stage sees them after the `st` wire format: tpm 2 dp, the rest 1 dp).

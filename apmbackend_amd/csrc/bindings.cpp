@@ -316,6 +316,7 @@ PYBIND11_MODULE(_apm_native, m) {
         r.alert_window = c.alert_window; r.alert_threshold = c.alert_threshold; r.both_only = c.both_only;
         r.hard_min_ms = c.hard_min_ms; r.hard_min_tpm = c.hard_min_tpm; r.hard_max_ms = c.hard_max_ms;
         r.cooldown_ms = c.cooldown_ms;
+        r.interval_len = c.interval_len; r.window = c.window; r.buffer = c.buffer;
         for (auto kv : overrides) r.overrides[kv.first.cast<std::string>()] = override_from(kv.second.cast<py::dict>());
         e.stage_reconfig(r);
       }, py::arg("ecfg"), py::arg("overrides"), py::arg("gen"))
@@ -323,6 +324,7 @@ PYBIND11_MODULE(_apm_native, m) {
         py::dict d;
         d["applied_gen"] = e.reconfig_applied_gen(); d["applied"] = e.reconfigs_applied();
         d["lag_set_changes"] = e.lag_set_changes();
+        d["window_changes"] = e.window_changes();
         return d;
       })
       .def("lag_values", &Engine::lag_values)

@@ -24,7 +24,7 @@ namespace apm {
 
 // 3: join section carries the join mode (host / GPU); 4: node-wide server order; 5: rings in their own
 // trailing section (full or dirty rows, for incremental checkpoints) + NaN horizons + an opaque extra
-constexpr uint32_t kCkptVersion = 7;  // 7: device audit-trail carry (K5 on the GPU)
+constexpr uint32_t kCkptVersion = 8;  // 7: device audit-trail carry (K5 on the GPU); 8: 8 LAG slots
 
 // A malloc'd byte buffer (no zero-fill on growth), owned and move-only.
 struct MemBlob {

@@ -243,6 +243,9 @@ void* Engine::dmalloc_try(size_t bytes) {
 }
 
 Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
+  check_window(cfg_.window, cfg_.buffer, cfg_.interval_len);
+  if (cfg_.n_lags < 1 || cfg_.n_lags > MAX_LAGS)
+    throw std::runtime_error("engine: 1.." + std::to_string(MAX_LAGS) + " LAG settings");
   HIP_OK(hipSetDevice(cfg_.device));
   {
     // Ranks sharing one GPU (a rehearsal of the node on one card): host threads that spin in

@@ -57,8 +57,13 @@ struct ReconfigSpec {
   int lag_suppressed[MAX_LAGS] = {0, 0, 0, 0};
   int alert_window = 60, alert_threshold = 45, both_only = 1;
   double hard_min_ms = 200, hard_min_tpm = 1.0, hard_max_ms = 10000, cooldown_ms = 15 * 60000.0;
+  int interval_len = 10, window = 30, buffer = 6;  // streamCalcStats (live: the next rollover on)
   std::map<std::string, ServiceOverride> overrides;
 };
+
+// Bounds of the stats window the bucket ring holds: K8 reads window + 1 buckets (at most 32
+// slots of its argument block), removeOldBuckets keeps window + buffer (NSLOT ring slots).
+void check_window(int window, int buffer, int interval_len);
 
 struct EngineConfig {
   int device = 0;
@@ -266,6 +271,7 @@ class Engine {
   uint64_t reconfig_applied_gen() const { return rc_applied_gen_.load(); }
   uint64_t reconfigs_applied() const { return reconfigs_applied_.load(); }
   uint64_t lag_set_changes() const { return lag_set_changes_.load(); }
+  uint64_t window_changes() const { return window_changes_.load(); }
   std::vector<int32_t> lag_values() { flush(); return std::vector<int32_t>(cfg_.lags, cfg_.lags + cfg_.n_lags); }
 
   // Process one batch. `now_override` < 0 uses the engine watermark clock.  If the caller
@@ -441,7 +447,7 @@ class Engine {
   std::mutex rc_mu_;
   std::deque<ReconfigSpec> rc_staged_;                           // lock-step: awaiting the node
   std::deque<std::pair<uint64_t, ReconfigSpec>> rc_tagged_;      // (batch, spec), batches ascend
-  std::atomic<uint64_t> rc_applied_gen_{0}, reconfigs_applied_{0}, lag_set_changes_{0};
+  std::atomic<uint64_t> rc_applied_gen_{0}, reconfigs_applied_{0}, lag_set_changes_{0}, window_changes_{0};
   std::map<int32_t, int32_t*> counter_stash_;                    // removed LAG -> its alert counters
   uint64_t reconfig_staged_gen();
   void reconfig_agree(uint64_t node_min);

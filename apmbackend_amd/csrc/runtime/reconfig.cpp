@@ -33,8 +33,18 @@ double now_ms() {
 }
 }  // namespace
 
+void check_window(int window, int buffer, int interval_len) {
+  if (window < 1 || window + 1 > 32 || buffer < 0 || window + buffer + 1 > NSLOT || interval_len < 1)
+    throw std::runtime_error("stats window: windowSizeInIntervals 1..31, windowSizeInIntervals + bufferSizeInIntervals "
+                             "<= " + std::to_string(NSLOT - 1) + ", intervalLengthInSeconds >= 1 (got " +
+                             std::to_string(window) + " / " + std::to_string(buffer) + " / " +
+                             std::to_string(interval_len) + ")");
+}
+
 void Engine::stage_reconfig(const ReconfigSpec& spec) {
-  if (spec.n_lags < 1 || spec.n_lags > MAX_LAGS) throw std::runtime_error("reconfigure: 1..4 LAG settings");
+  if (spec.n_lags < 1 || spec.n_lags > MAX_LAGS)
+    throw std::runtime_error("reconfigure: 1.." + std::to_string(MAX_LAGS) + " LAG settings");
+  check_window(spec.window, spec.buffer, spec.interval_len);
   for (int l = 0; l < spec.n_lags; ++l)
     if (spec.lags[l] < 1) throw std::runtime_error("reconfigure: LAG must be >= 1");
   std::lock_guard<std::mutex> g(rc_mu_);
@@ -91,7 +101,7 @@ void Engine::apply_reconfig(const ReconfigSpec& r) {
     HIP_OK(hipStreamSynchronize(out_stream_));
     const int32_t S = cfg_.max_series;
     LagState nl[MAX_LAGS] = {};
-    bool kept[MAX_LAGS] = {false, false, false, false};
+    bool kept[MAX_LAGS] = {};
     for (int i = 0; i < r.n_lags; ++i) {
       int j = -1;
       for (int o = 0; o < cfg_.n_lags; ++o)
@@ -150,6 +160,24 @@ void Engine::apply_reconfig(const ReconfigSpec& r) {
     cfg_.infl[l] = l < r.n_lags ? r.infl[l] : 0.0;
     cfg_.lag_suppressed[l] = l < r.n_lags ? r.lag_suppressed[l] : 0;
   }
+  // stats (stream_calc_stats.js:228-261 re-reads them on every change; used from the next
+  // rollover on).  removeOldBuckets keeps NUM_KEEP_INTERVALS = window + buffer buckets: a larger
+  // window fills in as new buckets arrive (older ones were deleted at the last rollover, here as
+  // there); a NaN-poisoned series stays poisoned until its bucket leaves the new keep range.
+  if (r.window != cfg_.window || r.buffer != cfg_.buffer) {
+    const int32_t dk = (r.window + r.buffer) - (cfg_.window + cfg_.buffer);
+    if (dk != 0 && n_series_ > 0) {
+      HIP_OK(hipStreamSynchronize(stream_));
+      std::vector<int32_t> nu((size_t)n_series_);
+      HIP_OK(hipMemcpy(nu.data(), d_nan_until_, nu.size() * 4, hipMemcpyDeviceToHost));
+      for (auto& v : nu) v += dk;  // (never poisoned: 0x80808080, far below any bucket either way)
+      HIP_OK(hipMemcpy(d_nan_until_, nu.data(), nu.size() * 4, hipMemcpyHostToDevice));
+    }
+    cfg_.window = r.window;
+    cfg_.buffer = r.buffer;
+    ++window_changes_;
+  }
+  cfg_.interval_len = r.interval_len;
   cfg_.alert_window = r.alert_window;
   cfg_.alert_threshold = r.alert_threshold;
   cfg_.hard_min_ms = r.hard_min_ms;

@@ -983,6 +983,14 @@ class PipelineOracle:
         self.cfg = cfg
         self.zs.reload(cfg)
         self.alerts.cfg = cfg
+        # stream_calc_stats.js watcher (:228-261): getParseSettings re-read, used from the next
+        # rollover (removeOldBuckets / window / TPM divisor / edge)
+        sc = cfg["streamCalcStats"]
+        st = self.st
+        st.interval_len = int(sc["intervalLengthInSeconds"])
+        st.window = int(sc["windowSizeInIntervals"])
+        st.buffer = int(sc["bufferSizeInIntervals"])
+        st.keep = st.window + st.buffer
 
     def _on_tx(self, queue, line):
         if queue == "db_insert":

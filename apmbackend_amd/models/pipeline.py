@@ -32,6 +32,7 @@ OUT_KINDS = ("transactions", "audit_db", "db", "st", "fs", "al", "sx", "fb")
 # What the reference persists (db_insert queue): released + audit tx, fs, al.  `transactions`
 # and `st` are internal hand-offs that only the AMQP bridge needs.
 DB_OUTPUTS = ("audit_db", "db", "fs", "al")
+MAX_LAGS = 8  # apm_types.h MAX_LAGS: LAG settings per engine
 
 
 def output_mask(kinds) -> int:
@@ -51,8 +52,8 @@ def engine_config(cfg: Dict[str, Any], device: int = 0, keep_text: bool = False,
     sc = cfg["streamCalcStats"]
     lags = sorted(((int(d["LAG"]), float(d["THRESHOLD"]), float(d["INFLUENCE"])) for d in zc["defaults"]),
                   key=lambda x: x[0])
-    if len(lags) > 4:
-        raise ValueError("at most 4 LAG settings are supported per engine")
+    if len(lags) > MAX_LAGS:
+        raise ValueError(f"at most {MAX_LAGS} LAG settings are supported per engine")
     suppressed_lags = {int(x) for x in ac.get("suppressedLags", [])}
     ring = {"float64": 8, "float32": 4, "bfloat16": 2, "bf16": 2}.get(g.get("ringDtype", "float64"), 8)
     tz = TzOffset(g.get("timezone", "local"))
@@ -107,8 +108,12 @@ def engine_config(cfg: Dict[str, Any], device: int = 0, keep_text: bool = False,
         "max_raw_services": max(int(g.get("maxRawServices", 1 << 18)), 2 * int(g.get("maxSeries", 1 << 17))),
         "outputs": output_mask(OUT_KINDS if keep_text else (outputs or ())),
     }
-    if int(sc["intervalLengthInSeconds"]) != 10:
-        raise ValueError("intervalLengthInSeconds must be 10 (bucket label = endTs without 4 digits)")
+    # intervalLengthInSeconds only scales the TPM divisor: the bucket label is endTs without its
+    # last 4 digits whatever the interval (stream_calc_stats.js:89-96, :186), as here
+    w, b = d["window"], d["buffer"]
+    if not (1 <= w <= 31 and b >= 0 and w + b <= 39 and d["interval_len"] >= 1):
+        raise ValueError(f"stats window: windowSizeInIntervals 1..31, window + bufferSizeInIntervals <= 39, "
+                         f"intervalLengthInSeconds >= 1 (got {w} / {b} / {d['interval_len']})")
     d.update(kw)
     return d
 
@@ -173,7 +178,7 @@ class APMEngine:
 
     # engine settings a reload applies live (reconfig.cpp); any other change needs a restart
     LIVE_KEYS = ("lags", "lag_suppressed", "alert_window", "alert_threshold", "hard_min_ms", "hard_min_tpm",
-                 "hard_max_ms", "both_only", "cooldown_ms")
+                 "hard_max_ms", "both_only", "cooldown_ms", "interval_len", "window", "buffer")
 
     def reload(self, cfg: Dict[str, Any], gen: Optional[int] = None) -> List[str]:
         """Config hot reload (the reference's watchAPMConfig callbacks): z-score defaults and

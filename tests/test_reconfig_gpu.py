@@ -69,11 +69,56 @@ def test_reload_thresholds_gates_and_lag_set_mid_stream():
     assert out["al"] == P.al
 
 
+def test_reload_stats_window_interval_and_many_lags():
+    """The stats settings apply live too (stream_calc_stats.js:228-261 getParseSettings re-read on
+    every change, used at the next rollover): the window shrinks 30 -> 20 with a 4-interval buffer
+    and a 15 s intervalLengthInSeconds (TPM divisor :186), then grows to 31 (it fills in from the
+    buckets removeOldBuckets kept), with 5 and then 6 LAGs (more than the old 4-LAG cap;
+    stream_calc_z_score.js:216 iterates any number).  st / fs / al equal the oracle applying the
+    same reloads between the same batches."""
+    _lines, bl = synth_batches(2)
+    C0 = small_cfg("exact")
+    C0["streamCalcZScore"]["defaults"] = [{"LAG": l, "THRESHOLD": t, "INFLUENCE": i} for l, t, i in
+                                          ((3, 3.0, 0.5), (6, 3.0, 0.5), (12, 2.5, 0.2), (20, 2.0, 0.0),
+                                           (30, 2.0, 0.0))]
+    C1 = copy.deepcopy(C0)
+    C1["streamCalcStats"].update({"windowSizeInIntervals": 20, "bufferSizeInIntervals": 4,
+                                  "intervalLengthInSeconds": 15})
+    C2 = copy.deepcopy(C1)
+    C2["streamCalcStats"].update({"windowSizeInIntervals": 31, "bufferSizeInIntervals": 6,
+                                  "intervalLengthInSeconds": 10})
+    C2["streamCalcZScore"]["defaults"].append({"LAG": 45, "THRESHOLD": 1.5, "INFLUENCE": 0.1})
+    k1, k2 = 90, 160
+    P = PipelineOracle(copy.deepcopy(C0), UTC)
+    P.run_batches(bl[:k1])
+    P.reload(copy.deepcopy(C1))
+    P.run_batches(bl[k1:k2])
+    P.reload(copy.deepcopy(C2))
+    P.run_batches(bl[k2:])
+    eng = APMEngine(copy.deepcopy(C0), keep_text=True)
+    out = collections.defaultdict(list)
+    for i, (now, chunks) in enumerate(bl):
+        if i == k1:
+            assert eng.reload(copy.deepcopy(C1), gen=1) == []
+        if i == k2:
+            assert eng.reload(copy.deepcopy(C2), gen=2) == []
+        eng.process_lines(chunks, now)
+        for k in ("st", "fs", "al"):
+            out[k] += eng.take(k)
+    info = eng.eng.reconfig_info()
+    assert info["applied"] == 2 and info["window_changes"] == 2 and info["lag_set_changes"] == 1
+    assert eng.eng.lag_values() == [3, 6, 12, 20, 30, 45]
+    assert out["st"] == P.stats and len(P.stats) > 1000
+    assert out["fs"] == P.fs
+    assert {l.split("|")[4] for l in P.fs} == {"3", "6", "12", "20", "30", "45"}
+    assert out["al"] == P.al
+
+
 def test_reload_warns_about_restart_keys():
     C0 = small_cfg("exact")
     eng = APMEngine(copy.deepcopy(C0), keep_text=True)
     C1 = copy.deepcopy(C0)
     C1["gpu"]["maxSeries"] = 8192
-    C1["streamCalcStats"]["windowSizeInIntervals"] = 20
+    C1["streamCalcStats"]["windowSizeInIntervals"] = 20  # (live since round 5)
     restart = eng.reload(C1, gen=1)
-    assert "max_series" in restart and "window" in restart
+    assert "max_series" in restart and "window" not in restart
