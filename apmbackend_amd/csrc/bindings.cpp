@@ -15,6 +15,7 @@
 #include "runtime/engine.h"
 #include "runtime/format.h"
 #include "runtime/jsutil.h"
+#include "runtime/merge.h"
 
 namespace apm {
 namespace copyenc {
@@ -468,6 +469,7 @@ PYBIND11_MODULE(_apm_native, m) {
       })
       .def("servers", &Engine::servers)
       .def("watermark", &Engine::watermark)
+      .def("batch_no", &Engine::batch_no)
       .def("device_bytes", &Engine::device_bytes)
       .def("trim_device_memory", &Engine::trim_device_memory, py::call_guard<py::gil_scoped_release>())
       .def("stream_handle", [](Engine& e) { return (uintptr_t)e.stream(); })
@@ -526,6 +528,25 @@ PYBIND11_MODULE(_apm_native, m) {
       .def("counters", &JoinHarness::counters);
 
   m.def("alloc_pinned", &Engine::alloc_pinned);
+  // re-shard merge of old ranks' checkpoints (runtime/merge.h), host only
+  m.def("checkpoint_batches", &checkpoint_batches, py::arg("path"));
+  m.def("merge_checkpoints", [](const std::vector<std::string>& inputs, const std::vector<std::string>& servers,
+                                const std::string& out, const py::bytes& extra, uint64_t batch_no) {
+    MergeResult r;
+    const std::string ex = extra;
+    {
+      py::gil_scoped_release rel;
+      r = merge_checkpoints(inputs, servers, out, ex, batch_no);
+    }
+    py::dict d;
+    d["batch_no"] = r.batch_no; d["series"] = r.series; d["keys"] = r.keys; d["need"] = r.need;
+    d["pending"] = r.pending; d["raw"] = r.raw; d["files"] = r.files; d["servers"] = r.servers;
+    d["used"] = r.used;
+    py::list ex_l;
+    for (const auto& e : r.extras) ex_l.append(py::bytes(e));
+    d["extras"] = ex_l;
+    return d;
+  }, py::arg("inputs"), py::arg("servers"), py::arg("out"), py::arg("extra") = py::bytes(""), py::arg("batch_no") = 0);
   m.def("free_pinned", &Engine::free_pinned);
   m.def("memcpy_to", [](uintptr_t dst, py::bytes b, uint64_t off) {
     std::string_view v = b;

@@ -266,7 +266,7 @@ __device__ bool baf_account_scan(const uint8_t* p, int a, int b, int& n, bool& d
 
 // The AudF of an LK_APP event (batch-absolute refs); false when the host must derive it.
 // p: the line's first byte (the batch, or k_host_flags' LDS stage at the same offset mod 16).
-__device__ bool aud_fields(const Event& e, const uint8_t* __restrict__ p, int32_t file, AudF& f) {
+__device__ bool aud_fields(const Event& e, const uint8_t* __restrict__ p, uint64_t fkey, AudF& f) {
   const int len = (int)e.len;
   f.h_item = 0; f.el = apm_nan(); f.h_sw = 0; f.ts = apm_nan();
   f.ref = 0; f.len = 0; f.flags = 0; f.pad = 0; f.pad2[0] = f.pad2[1] = 0;
@@ -285,7 +285,7 @@ __device__ bool aud_fields(const Event& e, const uint8_t* __restrict__ p, int32_
     f.len = (uint16_t)(e0 - s0);
     f.h_sw = hash_bytes(p + s0, (size_t)(e0 - s0));
     const uint64_t ah = L.eq1 < 0 ? hash_bytes("undefined", 9) : hash_bytes(p + L.eq1, (size_t)(L.eq2 - L.eq1));
-    f.h_item = aud_key(ah, file);
+    f.h_item = aud_key(ah, fkey);
     if ((m & PM_BAF) && L.t3s >= 0 && L.t3e > L.t3s) {
       int n;
       bool digits;
@@ -303,7 +303,7 @@ __device__ bool aud_fields(const Event& e, const uint8_t* __restrict__ p, int32_
     if (L.c1 < 0) return false;
     int a = L.c1 + 1, b = L.c2;
     trim_ascii(p, a, b);
-    f.h_item = aud_key(hash_bytes(p + a, (size_t)(b - a)), file);
+    f.h_item = aud_key(hash_bytes(p + a, (size_t)(b - a)), fkey);
     return true;
   }
   // item role (a line inside the elapsed section): service = split(':')[0].trim(),
@@ -457,14 +457,14 @@ __device__ __forceinline__ bool hf_needs_bytes(const Event& e) {
   return false;
 }
 
-__device__ __forceinline__ uint8_t hf_fields(const Event& e, const uint8_t* __restrict__ p, int32_t file, AudF* aud,
+__device__ __forceinline__ uint8_t hf_fields(const Event& e, const uint8_t* __restrict__ p, uint64_t fkey, AudF* aud,
                                              uint32_t i, int bytewise) {
   uint8_t fl = 0;
   if (e.kind == LK_APP) {
     bool host = (e.mask & PM_HOST) != 0;
     if (!host) {
       AudF f;
-      host = !aud_fields(e, p, file, f);
+      host = !aud_fields(e, p, fkey, f);
       if (!host) aud[i] = f;
     }
     if (host) fl |= SEL_HOST;
@@ -479,6 +479,7 @@ __device__ __forceinline__ uint8_t hf_fields(const Event& e, const uint8_t* __re
 
 __global__ __launch_bounds__(TB) void k_host_flags(const Event* __restrict__ ev, const uint32_t* __restrict__ n_ev_dev,
                                                    const uint8_t* __restrict__ bytes, const uint32_t* __restrict__ chunk_file,
+                                                   const uint64_t* __restrict__ file_fkey,
                                                    uint8_t* __restrict__ flag, uint64_t* __restrict__ val,
                                                    AudF* __restrict__ aud, SelCount* __restrict__ totals, uint32_t cap,
                                                    int bytewise, int staged) {
@@ -490,7 +491,7 @@ __global__ __launch_bounds__(TB) void k_host_flags(const Event* __restrict__ ev,
   uint32_t ab = 0;
   if (i < n) {
     const Event e = ev[i];
-    const int32_t file = e.kind == LK_APP ? (int32_t)chunk_file[e.chunk] : 0;
+    const uint64_t fkey = e.kind == LK_APP ? file_fkey[chunk_file[e.chunk]] : 0;
     // (staging only decides where the walk reads: a staged line is a complete copy, so the field
     // functions -- which read bytes only in the cases hf_needs_bytes names -- are unchanged)
     const uint8_t* p = bytes + e.off;
@@ -509,7 +510,7 @@ __global__ __launch_bounds__(TB) void k_host_flags(const Event* __restrict__ ev,
         if ((uint32_t)k < nvec) dst[k] = v[k];
       p = stage + threadIdx.x * HF_SLOT + lead;
     }
-    fl = hf_fields(e, p, file, aud, i, bytewise);
+    fl = hf_fields(e, p, fkey, aud, i, bytewise);
     if (e.kind == LK_APP) {
       if (e.mask & PM_AUTR_MAP) fl |= SEL_MH;
       else fl |= SEL_WALK | ((e.mask & PM_AUTR_HDR) ? SEL_MH : 0);
@@ -574,6 +575,7 @@ __global__ void k_build_ops(DJArgs a) {
   op.flags = 0; op.op = JOP_NONE; op.pad = 0;
   const int32_t file = (int32_t)a.chunk_file[e.chunk];
   const int32_t server = a.file_server[file];
+  const uint64_t skey = a.file_skey[file];
   op.server = server;
   uint8_t code = SC_NONE;
   double snum = apm_nan();
@@ -597,7 +599,7 @@ __global__ void k_build_ops(DJArgs a) {
         atomicAdd(&a.counts->invalid_acct, 1ULL);
       } else if (f.len > 0) {
         op.op = JOP_ACCT;
-        op.gkey = gkey_of(f.h_sw, server);
+        op.gkey = gkey_of(f.h_sw, skey);
         op.num = f.el;
       }
     }
@@ -626,7 +628,7 @@ __global__ void k_build_ops(DJArgs a) {
     op.ts = e.ts;
     const bool empty_lid = op.lid_len == 0;
     if (entry) {
-      if (!empty_lid) { op.op = JOP_ENTRY; op.gkey = gkey_of(e.key, server); }
+      if (!empty_lid) { op.op = JOP_ENTRY; op.gkey = gkey_of(e.key, skey); }
       else op.flags = 0;  // parseEntry returns before naming the service
     } else {
       op.num = (e.kind == LK_EJB_EXIT || e.tBs != 0xffff) ? e.num : apm_nan();
@@ -639,7 +641,7 @@ __global__ void k_build_ops(DJArgs a) {
         }
       }
       if (empty_lid) op.op = JOP_DIRECT;
-      else { op.op = e.kind == LK_EJB_EXIT ? JOP_EJB_EXIT : JOP_CT_EXIT; op.gkey = gkey_of(e.key, server); }
+      else { op.op = e.kind == LK_EJB_EXIT ? JOP_EJB_EXIT : JOP_CT_EXIT; op.gkey = gkey_of(e.key, skey); }
     }
   } else if (e.kind == LK_SOAP) {
     const uint32_t m = e.mask;
@@ -790,6 +792,7 @@ __global__ __launch_bounds__(APM_WAVE) void k_soap_apply(DJArgs a) {
   uint32_t st = a.seg_in[(size_t)c * SOAP_SEGS + g];
   const uint64_t h0 = a.chain_hash[c];
   const int32_t server = a.file_server[a.chunk_file[c]];
+  const uint64_t skey = a.file_skey[a.chunk_file[c]];
   for (uint32_t base = lo; base < hi; base += APM_WAVE) {
     const uint32_t i = base + lane;
     const uint8_t code = i < hi ? a.soap_code[i] : SC_NONE;
@@ -804,7 +807,7 @@ __global__ __launch_bounds__(APM_WAVE) void k_soap_apply(DJArgs a) {
       const uint64_t h = L == 0 ? h0 : a.soap_hash[L - 1];
       JOp op = a.ops[i];
       op.op = JOP_ACCT;
-      op.gkey = gkey_of(h, server);
+      op.gkey = gkey_of(h, skey);
       op.num = a.soap_num[i];
       op.server = server;
       a.ops[i] = op;
@@ -950,6 +953,7 @@ __global__ void k_aud_walk(DJArgs a) {
     start = p = id;
   }
   const int32_t server = a.file_server[file];
+  const uint64_t skey = a.file_skey[file];
   while (p != AUD_NIL) {
     const uint32_t ev = a.walk_idx[p];
     const Event e = a.ev[ev];
@@ -1008,7 +1012,7 @@ __global__ void k_aud_walk(DJArgs a) {
         if (prev == AUD_NIL) w.head = it.next; else a.aud_slots[prev].next = it.next;
         if (w.tail == s) w.tail = prev;
         JOp op;
-        op.gkey = gkey_of(w.lid_hash, server);
+        op.gkey = gkey_of(w.lid_hash, skey);
         op.svc = w.svc_hash;
         op.ts = f.ts;
         op.num = it.el;
@@ -1063,7 +1067,8 @@ __global__ void k_aud_walk(DJArgs a) {
 // (`fresh`: set when this call created the key; the caller counts new keys once per wave -- a
 // per-lane atomicAdd on the one n_keys_new word put ~every logId of the batch through a single
 // L2 atomic unit)
-__device__ uint32_t key_claim(KeyState* __restrict__ t, uint32_t mask, uint64_t k, JoinCounts* cnt, bool& fresh) {
+__device__ uint32_t key_claim(KeyState* __restrict__ t, uint32_t mask, uint64_t k, int32_t server, JoinCounts* cnt,
+                              bool& fresh) {
   uint32_t h = home_of(k, mask);
   for (uint32_t probe = 0; probe <= mask; ++probe) {
     const uint32_t idx = (h + probe) & mask;
@@ -1079,6 +1084,7 @@ __device__ uint32_t key_claim(KeyState* __restrict__ t, uint32_t mask, uint64_t 
         s.need = -1;
         s.n_part = 0;
         s.pblk = 0;
+        s.server = server;
         fresh = true;
         return idx;
       }
@@ -1109,7 +1115,7 @@ __global__ void k_claim(DJArgs a) {
   bool fresh = false;
   if (op.op == JOP_DIRECT) key = cap;
   else if (op.op != JOP_NONE) {
-    const uint32_t s = key_claim(a.table, a.table_mask, op.gkey, a.counts, fresh);
+    const uint32_t s = key_claim(a.table, a.table_mask, op.gkey, op.server, a.counts, fresh);
     key = s == 0xffffffffu ? cap + 1 : s;
   }
   {  // new keys: one atomic per wave
@@ -2310,6 +2316,7 @@ int apm_dj_select_host(DJArgs* a, const uint32_t* d_n_ev, uint32_t max_ev, hipSt
   HIP_OK(hipMemsetAsync(a->n_host, 0, sizeof(SelCount), s));
   if (max_ev == 0) return 0;
   hipLaunchKernelGGL(k_host_flags, dim3((max_ev + TB - 1) / TB), dim3(TB), 0, s, a->ev, d_n_ev, a->bytes, a->chunk_file,
+                     a->file_fkey,
                      a->host_flag, a->sel_val, a->aud, a->n_host, max_ev, pre_bytewise(), hf_staged());
   dj_check(s, "k_host_flags");
   // sel_pos: the tile sums, then the packed total (sel_pos has max_ev + 64 entries)

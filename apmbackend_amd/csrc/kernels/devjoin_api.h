@@ -49,6 +49,11 @@ struct DJArgs {
   const int32_t* chunk_next;      // next chunk of the same file in this batch (-1)
   const uint8_t* chunk_first;     // 1: first chunk of its file in this batch
   const int32_t* file_server;     // global file id -> server id
+  // world-invariant keys (hash of the server name / of the file path) that the join's table keys
+  // mix in instead of the engine-local ids: a checkpoint's key table, need arena and audit carry
+  // stay valid when a re-sharded engine numbers its servers and files differently (merge.cpp)
+  const uint64_t* file_skey;      // global file id -> key of its server
+  const uint64_t* file_fkey;      // global file id -> key of the file
   const HostOp* hops;
   uint32_t n_hops;
   const uint8_t* hbuf;            // host op string bytes

@@ -9,17 +9,25 @@
 namespace apm {
 namespace dj {
 
-__host__ __device__ inline uint64_t gkey_of(uint64_t lid_hash, int32_t server) {
-  const uint64_t k = hash_mix(lid_hash ^ ((uint64_t)(uint32_t)(server + 1) * 0x9E3779B97F4A7C15ULL), 0xd6e8feb86659fd93ULL);
+// join key of a logId on one JVM: skey = world-invariant key of the server (server_key_of)
+__host__ __device__ inline uint64_t gkey_of(uint64_t lid_hash, uint64_t skey) {
+  const uint64_t k = hash_mix(lid_hash ^ (skey * 0x9E3779B97F4A7C15ULL), 0xd6e8feb86659fd93ULL);
   return k ? k : 1;
+}
+// world-invariant keys of a server name / a log file path (the engine's ids are per rank)
+__host__ __device__ inline uint64_t server_key_of(const char* name, size_t n) {
+  return hash_bytes(name, n, 0x5e7e7e7e5e7e7e7eULL) | 1ULL;
+}
+__host__ __device__ inline uint64_t file_key_of(const char* path, size_t n) {
+  return hash_bytes(path, n, 0xf11ef11ef11ef11eULL) | 1ULL;
 }
 __host__ __device__ inline uint64_t regkey_of(uint64_t svc, int32_t server) {
   const uint64_t k = hash_mix(svc ^ ((uint64_t)(uint32_t)(server + 7) * 0xC2B2AE3D27D4EB4FULL), 0x165667b19e3779f9ULL);
   return k ? k : 1;
 }
-// audit-trail map key: (file, hash(auditTrailId)), never 0
-__host__ __device__ inline uint64_t aud_key(uint64_t autr_hash, int32_t file) {
-  return hash_mix(autr_hash, 0x9e3779b97f4a7c15ULL + (uint64_t)(uint32_t)file) | 1ULL;
+// audit-trail map key: (file key, hash(auditTrailId)), never 0
+__host__ __device__ inline uint64_t aud_key(uint64_t autr_hash, uint64_t fkey) {
+  return hash_mix(autr_hash, 0x9e3779b97f4a7c15ULL + fkey) | 1ULL;
 }
 __host__ __device__ inline uint32_t home_of(uint64_t k, uint32_t mask) {
   return (uint32_t)((k * 0x9E3779B97F4A7C15ULL) >> 32) & mask;

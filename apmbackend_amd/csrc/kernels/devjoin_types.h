@@ -103,7 +103,7 @@ struct KeyState {  // 128 B, one hash-table slot
   uint64_t part_svc[KS_PARTS];
   double part_start[KS_PARTS];
   int32_t pblk;     // PartBlk chain (block index + 1, 0 none)
-  int32_t pad;
+  int32_t server;   // engine server id of the key (a re-shard keeps the keys of the servers it owns)
 };
 static_assert(sizeof(KeyState) == 128, "KeyState layout");
 

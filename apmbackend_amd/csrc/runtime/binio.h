@@ -26,6 +26,12 @@ namespace apm {
 // trailing section (full or dirty rows, for incremental checkpoints) + NaN horizons + an opaque extra
 constexpr uint32_t kCkptVersion = 8;  // 7: device audit-trail carry (K5 on the GPU); 8: 8 LAG slots
 
+// Section tags, in file order (checkpoint.cpp writes / reads them, merge.cpp re-shards them).
+enum : uint32_t {
+  SEC_CONFIG = 1, SEC_TOPOLOGY, SEC_SERIES, SEC_CLOCK, SEC_JOIN, SEC_PARSE, SEC_BUCKETS, SEC_ZSCORE, SEC_POOL,
+  SEC_ALERTS, SEC_OUTPUTS, SEC_METRICS, SEC_RING, SEC_EXTRA, SEC_DUMP = 100, SEC_DUMP_SERIES = 101
+};
+
 // A malloc'd byte buffer (no zero-fill on growth), owned and move-only.
 struct MemBlob {
   char* p = nullptr;
@@ -226,6 +232,9 @@ class BinReader {
   }
   void finish() {
     if (pod<uint32_t>() != 0xE0Fu) throw std::runtime_error("checkpoint: missing end marker");
+  }
+  void skip(uint64_t n) {
+    if (n && std::fseek(f_, (long)n, SEEK_CUR) != 0) throw std::runtime_error("checkpoint: seek failed");
   }
 
  private:

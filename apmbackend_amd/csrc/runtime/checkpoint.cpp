@@ -32,11 +32,6 @@ namespace apm {
 
 namespace {
 
-enum : uint32_t {
-  SEC_CONFIG = 1, SEC_TOPOLOGY, SEC_SERIES, SEC_CLOCK, SEC_JOIN, SEC_PARSE, SEC_BUCKETS, SEC_ZSCORE, SEC_POOL,
-  SEC_ALERTS, SEC_OUTPUTS, SEC_METRICS, SEC_RING, SEC_EXTRA, SEC_DUMP = 100, SEC_DUMP_SERIES = 101
-};
-
 struct SeriesRec { int32_t server, service; uint64_t emit_key; };
 struct I64Pair { int64_t a, b; };
 

@@ -131,6 +131,10 @@ DeviceJoin::DeviceJoin(const DevJoinConfig& cfg, Dictionary* dict, const std::ve
     aud_reserve(g, 4096, 16384, 1u << 20);
   }
   d_file_server_ = (int32_t*)dmalloc((size_t)soap_cap_ * 4);
+  d_file_skey_ = (uint64_t*)dmalloc((size_t)soap_cap_ * 8);
+  d_file_fkey_ = (uint64_t*)dmalloc((size_t)soap_cap_ * 8);
+  h_file_skey_.reserve(soap_cap_);  // (the pre-pass lane reads them while files are added)
+  h_file_fkey_.reserve(soap_cap_);
   d_rawtab_ = (RawSvc*)dmalloc((size_t)cfg_.max_raw * sizeof(RawSvc));
   d_raw_series_ = (int32_t*)dmalloc((size_t)cfg_.max_raw * 4);
   d_raw_first_ = (int32_t*)dmalloc((size_t)cfg_.max_raw * 4);
@@ -213,13 +217,34 @@ DeviceJoin::~DeviceJoin() {
 }
 
 // ---------------------------------------------------------------------------- parse-side hooks
+// World-invariant keys of the files registered since the last call (their server's and their
+// own), host copies (read by the pre-pass lane: reserved, never reallocated) and device tables
+// (blocking copy: ordered before any kernel launched after it, on any stream).
+void DeviceJoin::sync_file_keys() {
+  const size_t n = files_->size();
+  if (n <= h_file_fkey_.size()) return;
+  if (n > soap_cap_) throw std::runtime_error("device join: too many files");
+  const size_t lo = h_file_fkey_.size();
+  if (lo == 0) HIP_OK(hipStreamSynchronize(stream_));  // (dmalloc zeroed the tables on the join stream)
+  for (size_t i = lo; i < n; ++i) {
+    const FileInfo& f = (*files_)[i];
+    const std::string& srv = (*servers_)[f.server];
+    h_file_skey_.push_back(dj::server_key_of(srv.data(), srv.size()));
+    h_file_fkey_.push_back(dj::file_key_of(f.path.data(), f.path.size()));
+  }
+  HIP_OK(hipMemcpy(d_file_skey_ + lo, h_file_skey_.data() + lo, (n - lo) * 8, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(d_file_fkey_ + lo, h_file_fkey_.data() + lo, (n - lo) * 8, hipMemcpyHostToDevice));
+}
+
 void DeviceJoin::select_host(int k, const uint32_t* d_n_ev, uint32_t max_ev, hipStream_t ps) {
   Slot& s = sl_[k];
+  sync_file_keys();
   DJArgs a{};
   a.ev = s.d_events;
   a.bytes = s.d_bytes;
   a.host_flag = s.host_flag;
   a.chunk_file = s.d_chunk_file;  // (set_chunks ran first)
+  a.file_fkey = d_file_fkey_;
   a.aud = s.d_aud;
   a.sel_val = d_sel_val_;
   a.sel_pos = d_sel_pos_;
@@ -430,7 +455,7 @@ void DeviceJoin::host_event(PrepassTask& T, const Event& e, uint32_t ev, const u
     op.lid = T.put(lid);
     op.lid_len = (uint16_t)std::min<size_t>(lid.size(), 0xffff);
     op.flags |= JF_LID_HOST;
-    op.gkey = dj::gkey_of(hash_bytes(lid.data(), lid.size()), server);
+    op.gkey = dj::gkey_of(hash_bytes(lid.data(), lid.size()), h_file_skey_[T.file]);
   }
   if (entry) {
     op.op = JOP_ENTRY;
@@ -497,7 +522,7 @@ void DeviceJoin::on_app(PrepassTask& T, const Event& e, uint32_t ev, std::string
     } else {
       ah = hash_bytes("undefined", 9);
     }
-    f.h_item = dj::aud_key(ah, T.file);
+    f.h_item = dj::aud_key(ah, h_file_fkey_[T.file]);
     // attemptReadAccountNumberFromBAFInfo -> the block's alt account and saveAcctNum
     if ((e.mask & PM_HOST) ? baf_match(line) : (e.mask & PM_BAF) != 0) {
       std::string_view t3 = toks.size() > 3 ? toks[3] : std::string_view();
@@ -520,7 +545,7 @@ void DeviceJoin::on_app(PrepassTask& T, const Event& e, uint32_t ev, std::string
     const size_t c1 = line.find(':');
     const size_t c2 = line.find(':', c1 + 1);
     const std::string_view autr = js::trim(line.substr(c1 + 1, c2 == std::string_view::npos ? std::string_view::npos : c2 - c1 - 1));
-    f.h_item = dj::aud_key(hash_bytes(autr.data(), autr.size()), T.file);
+    f.h_item = dj::aud_key(hash_bytes(autr.data(), autr.size()), h_file_fkey_[T.file]);
     return done();
   }
   {  // item role: service and elapsed of a RequestTrace line
@@ -958,7 +983,8 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
     apm_copy(d_hbuf_, hd_hbuf_, hbuf_.size(), st);
     span("u.hbuf.h2d");
   }
-  // ---- file -> server table
+  // ---- file -> server table (and the files' keys, normally synced by the parse's select_host)
+  sync_file_keys();
   if (files_->size() > files_uploaded_) {
     if (files_->size() > soap_cap_) throw std::runtime_error("device join: too many files");
     std::vector<int32_t> fs(files_->size() - files_uploaded_);
@@ -991,6 +1017,7 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
   a.ev = s.d_events; a.n_ev = n_ev; a.bytes = s.d_bytes;
   a.chunk_file = s.d_chunk_file; a.chunk_kind = s.d_chunk_kind; a.n_chunks = s.n_chunks;
   a.chunk_next = s.d_chunk_next; a.chunk_first = s.d_chunk_first; a.file_server = d_file_server_;
+  a.file_skey = d_file_skey_; a.file_fkey = d_file_fkey_;
   a.hops = d_hops_; a.n_hops = (uint32_t)hops_.size(); a.hbuf = d_hbuf_;
   a.now = now; a.batch_no = batch_no;
   a.rec_ttl = cfg_.record_ttl_ms; a.acct_ttl = cfg_.acct_ttl_ms; a.need_ttl = cfg_.need_ttl_ms;

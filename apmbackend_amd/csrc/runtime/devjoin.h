@@ -294,6 +294,10 @@ class DeviceJoin {
   char* h_ck_bounce_ = nullptr;
   uint32_t soap_cap_ = 0;
   int32_t* d_file_server_ = nullptr;
+  uint64_t* d_file_skey_ = nullptr;      // per file: world-invariant key of its server (gkey_of)
+  uint64_t* d_file_fkey_ = nullptr;      // per file: world-invariant key of the file (aud_key)
+  std::vector<uint64_t> h_file_skey_, h_file_fkey_;
+  void sync_file_keys();
   size_t files_uploaded_ = 0;
   RawSvc* d_rawtab_ = nullptr;
   int32_t* d_raw_series_ = nullptr;

@@ -414,6 +414,7 @@ class Engine {
   std::vector<std::string> services() const { return dict_.services_snapshot(); }
   int32_t n_series() const { return n_series_; }
   double watermark() const { return watermark_; }
+  uint64_t batch_no() const { return batch_no_; }  // batches processed (node-wide equal in lock-step)
   hipStream_t stream() const { return stream_; }
   hipStream_t comm_stream() const { return stream_; }  // (the stats stream: callers flush() first)
   // HBM held: the engine's own buffers plus the device join's (which grow and shrink)

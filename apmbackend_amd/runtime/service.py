@@ -33,6 +33,7 @@ import logging
 import math
 import os
 import signal
+import sys
 import time
 from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -43,6 +44,17 @@ from ..utils.config import ConfigWatcher, as_bool, read_apm_config
 from . import logger as apmlog
 from .notifier import AlertNotifier
 from .sinks import DBInserter
+
+
+# Exit status of a rank that stops because a PEER rank failed (its collectives aborted): the
+# supervisor does not count it against this rank's GPU (runtime/supervisor.py).
+PEER_FAILURE_EXIT = 75
+
+
+def is_peer_failure(e: BaseException) -> bool:
+    m = str(e)
+    return ("peer process gone" in m or "peer rank dead" in m or "communicator was aborted" in m
+            or ("collective" in m and "failed" in m and "peer" in m))
 
 
 def _native_mod():
@@ -167,6 +179,9 @@ class IngestService:
         self.ckpt_every = float(g.get("checkpointEverySeconds",
                                       self.cfg["streamCalcStats"].get("resumeFileSaveFrequencyInSeconds", 60)))
         self.resharded = False
+        self._ckpt_epoch: Optional[int] = None
+        self._merge_sinks: List[Tuple[int, Dict[str, Any]]] = []
+        self.reshard_info: Optional[Dict[str, Any]] = None
         self._ckpt_extra = b""
         restored = self._restore() if (self.ckpt_dir and engine == "native") else False
         if not restored:
@@ -227,6 +242,8 @@ class IngestService:
                 os.makedirs(self.ckpt_dir, exist_ok=True)
                 if restored:
                     self._restore_sink()  # (reads the previous incarnation's ack file first)
+                    for r, meta in self._merge_sinks:  # re-shard: the old ranks' pending rows
+                        self._restore_sink(meta, r)
                 self.inserter.set_ack_file(self._sink_ack_path(), self._sink_incarnation)
             if engine == "native":
                 # db / audit / fs go engine output lane -> native sink directly; al stays on the
@@ -338,8 +355,15 @@ class IngestService:
         if not os.path.exists(ck) and not glob.glob(os.path.join(self.ckpt_dir, "tail.rank*.json")):
             return False
         if not os.path.exists(ck) or not self._checkpoint_is_mine():
-            # world size changed (elastic degrade / grow): fresh engine state for this shard, tails
-            # resumed from whichever rank owned each file last (_restore_offsets_resharded)
+            # world size changed (elastic degrade / grow): this rank's state is merged from the
+            # previous world's checkpoints of the servers it now owns (merge.cpp); only when they
+            # are missing / unreadable does the shard start fresh, with tails resumed from
+            # whichever rank owned each file last (_restore_offsets_resharded)
+            try:
+                if self._restore_merged():
+                    return True
+            except Exception as e:
+                log.error("re-shard merge failed (%s): this shard starts with fresh engine state", e)
             self.resharded = True
             return False
         try:
@@ -366,6 +390,81 @@ class IngestService:
             log.warning("checkpoint %s has an incompatible format version (%s): moved %s aside, starting this "
                         "shard with fresh engine state", ck, e, ", ".join(moved))
             return False
+
+    def _restore_merged(self) -> bool:
+        """Elastic re-shard: the previous world's rank checkpoints that hold any of this rank's
+        servers are merged at their newest common batch into this rank's starting state -- window
+        buckets, z-score rings and moments, alert counters, join caches and parked records, pending
+        release lines of exactly these servers (the reference resumes every per-series history
+        from its resume files, stream_calc_stats.js:54-87, stream_calc_z_score.js:37-64,
+        stream_process_alerts.js:111-142).  Tail offsets come from the same checkpoints."""
+        g = self.cfg.get("gpu", {})
+        if not as_bool(g.get("reshardMerge", True)):
+            return False
+        metas = []
+        for p in glob.glob(os.path.join(self.ckpt_dir, "meta.rank*.json")):
+            try:
+                m = read_json(p)
+                m["_rank"] = int(os.path.basename(p)[len("meta.rank"):-len(".json")])
+                metas.append(m)
+            except (OSError, ValueError):
+                continue
+        prev = [m for m in metas if m.get("world") != self.world]
+        if not prev:
+            return False
+        old_world = max(prev, key=lambda m: float(m.get("ts", 0.0)))["world"]
+        old = {m["_rank"]: m for m in prev if m.get("world") == old_world}
+        mine = set(self.my_servers)
+        inputs = [r for r in sorted(old) if mine & set(old[r].get("servers", []))]
+        held = set().union(*(set(old[r].get("servers", [])) for r in inputs)) if inputs else set()
+        if not inputs or len(old) != old_world:
+            log.warning("re-shard: %d of %d rank checkpoints of world %s found; servers %s start fresh",
+                        len(old), old_world, old_world, sorted(mine))
+            return False
+        paths = [os.path.join(self.ckpt_dir, f"engine.rank{r}.ckpt") for r in inputs]
+        missing = [p for p in paths if not os.path.exists(p)]
+        if missing:
+            log.warning("re-shard: checkpoints %s missing: this shard starts fresh", missing)
+            return False
+        N = _native_mod()
+        out = os.path.join(self.ckpt_dir, f"engine.rank{self.rank}.resharded.{os.getpid()}.ckpt")
+        t0 = time.perf_counter()
+        info = N.merge_checkpoints(paths, sorted(mine), out, b"")
+        try:
+            self.eng.load_state(out)
+        finally:
+            try:
+                os.remove(out)
+            except OSError:
+                pass
+        tails: Dict[str, Any] = {}
+        for r, ex in zip(inputs, info["extras"]):
+            try:
+                doc = json.loads(bytes(ex).decode("utf-8")) if ex else {}
+            except (ValueError, UnicodeDecodeError):
+                doc = {}
+            for path, v in (doc.get("tail") or {}).items():
+                if self.server_of(path) in mine:
+                    tails[path] = v
+            # an old rank's unacknowledged DB rows are re-submitted once: by the new owner of its
+            # first server
+            srv0 = sorted(old[r].get("servers", []))[:1]
+            if doc.get("sink") and srv0 and srv0[0] in mine:
+                self._merge_sinks.append((r, doc["sink"]))
+        self._ckpt_extra = json.dumps({"tail": tails}).encode("utf-8")
+        known = {p for p, _k, _s in self.native.files()}
+        for f in self.files:
+            if f not in known:
+                self.native.add_file(f, KIND_CODE[file_kind(f)], self.server_of(f))
+        self.reshard_info = {k: info[k] for k in ("batch_no", "series", "keys", "need", "pending", "raw", "files",
+                                                 "servers")}
+        self.reshard_info.update({"from_world": old_world, "from_ranks": inputs,
+                                  "seconds": round(time.perf_counter() - t0, 3)})
+        log.warning("re-sharded start: world %s -> %d, rank %d merged ranks %s at batch %d: %d series, %d join "
+                    "keys, %d parked records, %d pending lines (servers %s; %s held by the inputs)", old_world,
+                    self.world, self.rank, inputs, info["batch_no"], info["series"], info["keys"], info["need"],
+                    info["pending"], sorted(mine), "all" if mine <= held else sorted(mine & held))
+        return True
 
     # ------------------------------------------------------------------ sink watermark
     def _sink_ack_path(self) -> str:
@@ -418,24 +517,27 @@ class IngestService:
     def _sink_snapshot_name(self) -> str:
         return f"sink_pending.rank{self.rank}.{self._sink_incarnation:x}.{self.n_checkpoints + 1}.bin"
 
-    def _restore_sink(self):
+    def _restore_sink(self, meta: Optional[Dict[str, Any]] = None, ack_rank: Optional[int] = None):
         """After a restore: re-submit the checkpoint's pending flushes that the sink did not
         acknowledge before the process ended (its ack file; a different incarnation in the file --
         an interrupted earlier restore -- means nothing is known: everything is re-submitted, at
         least once)."""
         from .sinks import read_sink_ack, read_sink_snapshot
-        try:
-            meta = json.loads(self._ckpt_extra.decode("utf-8")).get("sink") if self._ckpt_extra else None
-        except (ValueError, AttributeError):
-            meta = None
+        if meta is None:
+            try:
+                meta = json.loads(self._ckpt_extra.decode("utf-8")).get("sink") if self._ckpt_extra else None
+            except (ValueError, AttributeError):
+                meta = None
         if not meta:
             return 0
-        self._sink_committed = meta["pending"]  # named by the restored chain: kept until a newer commit
+        if ack_rank is None:
+            self._sink_committed = meta["pending"]  # named by the restored chain: kept until a newer commit
         path = os.path.join(self.ckpt_dir, meta["pending"])
         if not os.path.exists(path):
             log.warning("checkpoint names sink snapshot %s, which is missing: its rows are lost", path)
             return 0
-        acked_now = read_sink_ack(self._sink_ack_path(), int(meta["incarnation"]))
+        ack = self._sink_ack_path() if ack_rank is None else os.path.join(self.ckpt_dir, f"sink.rank{ack_rank}.ack")
+        acked_now = read_sink_ack(ack, int(meta["incarnation"]))
         n, jobs = read_sink_snapshot(path, acked_now)
         rows = self.inserter.resubmit(jobs)
         log.info("sink: re-submitted %d flushes (%d rows) of the checkpoint's %d unacknowledged ones", len(jobs),
@@ -676,8 +778,10 @@ class IngestService:
         if self._gc_requested and self._held is None:  # (a held prefetch: the next poll does not prefetch)
             self._gc_requested = False
             self.request_gc()
-        if self.ckpt_dir and self.eng is not None and now - self.last_ckpt >= self.ckpt_every:
+        if self._ckpt_due():
             self.checkpoint()
+            if self._lockstep_ckpt():  # (advanced on every rank alike, written or skipped)
+                self._ckpt_epoch = int(self.native.batch_no()) // self._ckpt_every_batches()
         interval = float(self.cfg.get("statLogIntervalInSeconds", 60))
         if now - self.last_stat >= interval:
             self.log_stats(now - self.last_stat)
@@ -825,8 +929,29 @@ class IngestService:
         self._drain_outputs()
         return len(blob)
 
-    def _ckpt_due(self) -> bool:
-        return bool(self.ckpt_dir) and self.eng is not None and self.clock() - self.last_ckpt >= self.ckpt_every
+    def _lockstep_ckpt(self) -> bool:
+        """Lock-step ranks checkpoint at the same batches (every gpu.checkpointEveryBatches): any
+        batch every rank has a checkpoint for is a consistent node state -- what a same-world
+        restart resumes from and a re-shard merges (merge.cpp needs one common batch)."""
+        return self.fleet is not None and self.world > 1
+
+    def _ckpt_every_batches(self) -> int:
+        g = self.cfg.get("gpu", {})
+        k = int(g.get("checkpointEveryBatches", 0) or 0)
+        if k <= 0:
+            k = 1 if self.ckpt_every <= 0 else max(1, int(round(self.ckpt_every / float(g.get("pollSeconds", 1.0)))))
+        return k
+
+    def _ckpt_due(self, ahead: int = 0) -> bool:
+        if not self.ckpt_dir or self.eng is None:
+            return False
+        if self._lockstep_ckpt():
+            k = self._ckpt_every_batches()
+            b = int(self.native.batch_no()) + ahead
+            if self._ckpt_epoch is None:
+                self._ckpt_epoch = (b - ahead) // k
+            return b // k > self._ckpt_epoch
+        return self.clock() - self.last_ckpt >= self.ckpt_every
 
     def _step_readahead(self, lockstep: bool, paused: bool) -> int:
         """step() over the tailer's read-ahead ring: batches arrive in pinned slots, the batch
@@ -864,7 +989,7 @@ class IngestService:
             return n
         dup = mine and fi.get("duplicateBatchEvery") and self.polls % int(fi["duplicateBatchEvery"]) == 0
         nxt = None
-        if not paused and not dup and not self._ckpt_due() and not self._stopping and not self._gc_requested:
+        if not paused and not dup and not self._ckpt_due(ahead=1) and not self._stopping and not self._gc_requested:
             nxt = self.tailer.next(0.0)
         if self.batch_log is not None:
             import ctypes
@@ -1080,7 +1205,15 @@ def main(argv=None):  # pragma: no cover - process entry point
         init_distributed()
     svc = IngestService(config_path=a.config, engine=a.engine, install_signals=True,
                         trace_path=a.trace)
-    svc.run(max_batches=a.max_batches)
+    try:
+        svc.run(max_batches=a.max_batches)
+    except RuntimeError as e:
+        if is_peer_failure(e):
+            # a peer rank died or hung: this rank is healthy -- say so in the exit status, so the
+            # supervisor's elastic degrade blames the rank that failed first, not its survivors
+            log.error("collective peer failure: %s", e)
+            sys.exit(PEER_FAILURE_EXIT)
+        raise
 
 
 if __name__ == "__main__":  # pragma: no cover

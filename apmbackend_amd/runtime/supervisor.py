@@ -46,6 +46,9 @@ from ..utils.config import ConfigWatcher, as_bool, read_apm_config
 from . import logger as apmlog
 from .notifier import Mailer, post_annotation
 
+# exit status of a rank that stopped because a peer rank failed (runtime/service.py)
+PEER_FAILURE_EXIT = 75
+
 log = logging.getLogger("apm.manager")
 
 
@@ -322,7 +325,7 @@ class Supervisor:
         the JVM hosts over the new world; each resumes the tails of the files it now owns from the
         old ranks' offsets (no data gap), and the series that moved rank start a fresh history."""
         flag = mod.setting("elasticDegrade", self.m)
-        if not mod.ranks or code == 0 or (flag is not None and not as_bool(flag)):
+        if not mod.ranks or code in (0, PEER_FAILURE_EXIT) or (flag is not None and not as_bool(flag)):
             return False
         dev = mod.device_of(p)
         if dev is None:
@@ -390,6 +393,15 @@ class Supervisor:
     def check_children(self):
         now = self.clock()
         for mod in self.modules:
+            if mod.ranks:
+                # a rank group: when several ranks have exited since the last poll, the one that
+                # failed first is the one whose exit is not a survivor's PEER_FAILURE_EXIT (the
+                # others aborted their collectives because it died) -- that rank's GPU is blamed
+                exited = [(p, p.poll()) for p in mod.procs if p.restart_at is None]
+                exited = [(p, c) for p, c in exited if c is not None]
+                if exited:
+                    first = next(((p, c) for p, c in exited if c not in (0, PEER_FAILURE_EXIT)), exited[0])
+                    self._on_exit(mod, first[0], first[1], now)
             for p in mod.procs:
                 if p.restart_at is not None:
                     if now >= p.restart_at:
