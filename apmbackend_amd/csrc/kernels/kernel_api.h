@@ -46,6 +46,7 @@ struct WindowArgs {
   int32_t* js_scratch;    // [JS_BLOCKS][js_cap] ordered window samples of a NaN series
   int32_t js_cap;
   int32_t n_series;       // ids < n_series may be active
+  int32_t lds_sort;       // APM_K8_LDS=1: the LDS bitonic for every window (A/B of the register sort)
 };
 constexpr int JS_BLOCKS = 8;
 

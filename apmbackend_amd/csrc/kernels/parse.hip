@@ -10,8 +10,10 @@
 // line one lane, stages the block's byte range in LDS (64 KiB) and classifies the line with a
 // single pass that tests all pattern families at each byte; relevant lines become fixed-layout
 // Event records written in line order by an ordered stream compaction (flag scan).  Noise lines
-// (the vast majority) never leave the GPU.  Stateful joins run downstream on the host join
-// workers, which read strings from the pinned host copy of the same bytes.
+// (the vast majority) never leave the GPU.  The stateful join (K4-K6) runs downstream on the
+// GPU too (devjoin.hip), reading the same device bytes; only the rare lines it cannot read alone
+// (non-ASCII, exotic number / date forms) are re-derived by the host pre-pass from the pinned
+// host copy (runtime/devjoin.cpp).
 #include "kernel_api.h"
 
 #include <rocprim/rocprim.hpp>

@@ -356,10 +356,47 @@ __global__ __launch_bounds__(WS_WAVES * APM_WAVE) void k_window_stats(WindowArgs
     if (lane == 0) a.nan_list[atomicAdd(a.nan_n, 1)] = s;
     return;
   }
-  // pad to a power of two and sort
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  if (n <= APM_WAVE && !a.lds_sort) {
+    // The usual window (~20 samples): one sample per lane, a bitonic network over the lanes in
+    // registers -- 21 shuffle + min/max steps, no LDS round trips or wave barriers (the LDS
+    // network padded every series to 64 and cost 21 LDS passes; profiles/r4_pm: 100 us per
+    // rollover at 19 % L2 hit).  The percentile ranks are read back by shuffles.
+    int32_t v = lane < n ? t[lane] : 0x7fffffff;
+#pragma unroll
+    for (int k = 2; k <= APM_WAVE; k <<= 1) {
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        const int32_t o = __shfl_xor(v, j, APM_WAVE);
+        const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+        v = keep_min ? min(v, o) : max(v, o);
+      }
+    }
+    int l75, h75, l95, h95;
+    percentile_ranks(n, 75, l75, h75);
+    percentile_ranks(n, 95, l95, h95);
+    const int32_t a75 = __shfl(v, max(l75, 0), APM_WAVE), b75 = __shfl(v, max(h75, 0), APM_WAVE);
+    const int32_t a95 = __shfl(v, max(l95, 0), APM_WAVE), b95 = __shfl(v, max(h95, 0), APM_WAVE);
+    if (lane == 0) {
+      WinStat w;
+      w.n = n;
+      w.active = 1;
+      w.tpm = js_round_fixed((double)n / a.tpm_div, 2);
+      if (n > 0) {
+        w.avg = js_round_fixed((double)sum / (double)n, 1);
+        w.p75 = js_round_fixed(l75 == h75 ? (double)a75 : ((double)a75 + (double)b75) / 2.0, 1);
+        w.p95 = js_round_fixed(l95 == h95 ? (double)a95 : ((double)a95 + (double)b95) / 2.0, 1);
+      } else {
+        w.avg = w.p75 = w.p95 = apm_nan();
+      }
+      a.out[s] = w;
+    }
+    return;
+  }
+  // pad to a power of two and sort in LDS
   int np2 = 64;
   while (np2 < n) np2 <<= 1;
-  __builtin_amdgcn_wave_barrier();
   for (int i = n + lane; i < np2; i += 64) t[i] = 0x7fffffff;
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -2182,6 +2182,10 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
     wa.win_slots[r] = slot_bucket_[slot] == b ? slot : -1;
   }
   wa.tpm_div = (double)cfg_.window * cfg_.interval_len / 60.0;
+  {
+    static const int lds = [] { const char* e = std::getenv("APM_K8_LDS"); return e && e[0] == '1' ? 1 : 0; }();
+    wa.lds_sort = lds;
+  }
   wa.out = d_win_;
   wa.big_list = d_big_list_;
   wa.big_n = d_big_n_;

@@ -35,7 +35,7 @@ def _bench_json(stdout: str):
     return json.loads(rows[0])
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 4])
 def test_bench_torchrun_ranks_share_one_gpu(tmp_path, world):
     rep = str(tmp_path / "ranks")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
@@ -58,8 +58,13 @@ def test_bench_torchrun_ranks_share_one_gpu(tmp_path, world):
         assert len(x["step_ms"]) == 6
     assert sum(x["lines_timed"] for x in reps) == out["lines_total"]
     # the node-wide line counter (as of the last exchanged interval edge) is a sum over ranks
-    assert reps[0]["node_metrics"][2] == reps[1]["node_metrics"][2] <= sum(x["lines_total"] for x in reps)
-    assert reps[0]["node_metrics"][2] > max(x["lines_total"] for x in reps) * 1.5
+    assert all(x["node_metrics"][2] == reps[0]["node_metrics"][2] for x in reps)
+    assert reps[0]["node_metrics"][2] <= sum(x["lines_total"] for x in reps)
+    assert reps[0]["node_metrics"][2] > max(x["lines_total"] for x in reps) * (world - 0.5)
+    # fb rows are formatted by every rank (its slice of the node-wide services), off the
+    # collective stream: no rank carries the node's fb formatting inside its lock-step exchange
+    p50 = [sorted(x["step_ms"])[len(x["step_ms"]) // 2] for x in reps]
+    print(f"[{world} ranks] per-rank step p50 {p50}")
     print(f"[{world} ranks] {out['value'] / 1e6:.1f} M lines/s, step p50 {out['step_ms_p50']} ms, "
           f"p99 {out['step_ms_p99']} ms, lockstep {out['t_lockstep_ms']} ms/step ({time.time() - t0:.0f} s)")
 
