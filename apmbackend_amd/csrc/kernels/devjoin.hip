@@ -44,15 +44,21 @@ constexpr int TB = 256;
 // the join's critical path, profiles/r3_*); onesweep does 3 digit passes.
 using OpSortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
                                              rocprim::default_config, 0>;
-// APM_OPSORT=11: 11-bit digits -- two passes for the ~20-22 key bits instead of three
+// 11-bit digits: two onesweep passes for keys up to 22 bits instead of three
 using OpSortCfg11 = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
     rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>, 11,
                                         rocprim::block_radix_rank_algorithm::match>,
     0>;
-static bool opsort11() {
-  static const bool v = [] { const char* e = std::getenv("APM_OPSORT"); return e && e[0] == '1' && e[1] == '1'; }();
-  return v;
+// Op keys are table slots [0, cap), cap (JOP_DIRECT) and cap + 1 (no op): table_bits + 1 bits.
+// (They were sorted over table_bits + 2 bits: 23 for the 2M-slot table, three passes of any digit
+// width up to 11.)  With <= 22 bits the 11-bit onesweep takes two.  APM_OPSORT=8: the 8-bit
+// onesweep (three passes), =m: rocprim's default dispatch (A/B).
+static int op_sort_bits(int table_bits) { return table_bits + 1; }
+static bool opsort11(int table_bits) {
+  static const int mode = [] { const char* e = std::getenv("APM_OPSORT"); return e ? (int)e[0] : 0; }();
+  if (mode == '8' || mode == 'm') return false;
+  return op_sort_bits(table_bits) <= 22;
 }
 
 __device__ __forceinline__ uint32_t grid_n(uint32_t n) { return (n + TB - 1) / TB; }
@@ -2284,11 +2290,11 @@ size_t apm_dj_tmp_bytes(uint32_t max_ev, uint32_t max_out, int table_bits) {
   HIP_OK(rocprim::exclusive_scan(nullptr, a, (uint8_t*)nullptr, (uint32_t*)nullptr, 0u, n, rocprim::plus<uint32_t>(),
                                  (hipStream_t)0));
   HIP_OK(rocprim::radix_sort_pairs<OpSortCfg>(nullptr, b, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                   (uint32_t*)nullptr, n, 0, table_bits + 2, (hipStream_t)0));
+                                   (uint32_t*)nullptr, n, 0, op_sort_bits(table_bits), (hipStream_t)0));
   {
     size_t b11 = 0;
     HIP_OK(rocprim::radix_sort_pairs<OpSortCfg11>(nullptr, b11, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                                  (uint32_t*)nullptr, (uint32_t*)nullptr, n, 0, table_bits + 2,
+                                                  (uint32_t*)nullptr, (uint32_t*)nullptr, n, 0, op_sort_bits(table_bits),
                                                   (hipStream_t)0));
     b = std::max(b, b11);
   }
@@ -2393,23 +2399,23 @@ int apm_dj_join(DJArgs* a, hipStream_t s) {
     size_t need = 0;
     if (merge_sort) {  // diagnostic: rocprim's default (block sort + merge passes)
       HIP_OK(rocprim::radix_sort_pairs(nullptr, need, a->op_slot, a->op_slot_sorted, a->op_idx, a->op_idx_sorted,
-                                       (size_t)n, 0, a->table_bits + 2, s));
+                                       (size_t)n, 0, op_sort_bits(a->table_bits), s));
       if (need > a->tmp_bytes) return -1;
       HIP_OK(rocprim::radix_sort_pairs(a->tmp, need, a->op_slot, a->op_slot_sorted, a->op_idx, a->op_idx_sorted,
-                                       (size_t)n, 0, a->table_bits + 2, s));
+                                       (size_t)n, 0, op_sort_bits(a->table_bits), s));
       dj_check(s, "rocprim_radix_sort_pairs");
-    } else if (opsort11()) {
+    } else if (opsort11(a->table_bits)) {
       HIP_OK(rocprim::radix_sort_pairs<OpSortCfg11>(nullptr, need, a->op_slot, a->op_slot_sorted, a->op_idx,
-                                                    a->op_idx_sorted, (size_t)n, 0, a->table_bits + 2, s));
+                                                    a->op_idx_sorted, (size_t)n, 0, op_sort_bits(a->table_bits), s));
       if (need > a->tmp_bytes) return -1;
       HIP_OK(rocprim::radix_sort_pairs<OpSortCfg11>(a->tmp, need, a->op_slot, a->op_slot_sorted, a->op_idx,
-                                                    a->op_idx_sorted, (size_t)n, 0, a->table_bits + 2, s));
+                                                    a->op_idx_sorted, (size_t)n, 0, op_sort_bits(a->table_bits), s));
     } else {
       HIP_OK(rocprim::radix_sort_pairs<OpSortCfg>(nullptr, need, a->op_slot, a->op_slot_sorted, a->op_idx,
-                                                  a->op_idx_sorted, (size_t)n, 0, a->table_bits + 2, s));
+                                                  a->op_idx_sorted, (size_t)n, 0, op_sort_bits(a->table_bits), s));
       if (need > a->tmp_bytes) return -1;
       HIP_OK(rocprim::radix_sort_pairs<OpSortCfg>(a->tmp, need, a->op_slot, a->op_slot_sorted, a->op_idx,
-                                                  a->op_idx_sorted, (size_t)n, 0, a->table_bits + 2, s));
+                                                  a->op_idx_sorted, (size_t)n, 0, op_sort_bits(a->table_bits), s));
     }
   }
   (void)cap;
