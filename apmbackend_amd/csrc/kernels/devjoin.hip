@@ -894,14 +894,14 @@ __global__ void k_aud_autr(DJArgs a) {
 
 __global__ void k_aud_chunks(DJArgs a) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c > a.n_chunks) return;
-  uint32_t l = 0, h = a.n_walk;
-  while (l < h) {
-    const uint32_t mid = (l + h) >> 1;
-    if (a.ev[a.walk_idx[mid]].chunk < c) l = mid + 1; else h = mid;
-  }
-  a.walk_lo[c] = l;
   if (c < a.n_chunks && a.chunk_first[c]) a.file_first_chunk[a.chunk_file[c]] = (int32_t)c;
+  // walk_lo[k] = first walk position of chunk k: lane q owns the boundaries between walk
+  // positions q - 1 and q (walk events are in chunk order), as k_chunk_events does for events
+  const uint32_t nw = a.n_walk;
+  if (c > nw) return;
+  const uint32_t prev = c == 0 ? 0u : a.ev[a.walk_idx[c - 1]].chunk + 1u;
+  const uint32_t cur = c == nw ? a.n_chunks + 1u : min(a.ev[a.walk_idx[c]].chunk, a.n_chunks) + 1u;
+  for (uint32_t k = prev; k < cur && k <= a.n_chunks; ++k) a.walk_lo[k] = c;
 }
 
 // first walk position at or after chunk c of a file (following its chunk chain)
@@ -2357,7 +2357,8 @@ static int apm_dj_audit(DJArgs* a, bool filled, hipStream_t s) {
   // an open block always carries its (non-empty) logId: no carry text, no carried block
   if (a->n_walk || a->gin.n_txt) {
     if (a->n_files && !filled) HIP_OK(hipMemsetAsync(a->file_first_chunk, 0xff, (size_t)a->n_files * 4, s));
-    hipLaunchKernelGGL(k_aud_chunks, dim3((a->n_chunks + 1 + TB - 1) / TB), dim3(TB), 0, s, *a);
+    const uint32_t lanes = std::max(a->n_chunks + 1, a->n_walk + 1);
+    hipLaunchKernelGGL(k_aud_chunks, dim3((lanes + TB - 1) / TB), dim3(TB), 0, s, *a);
     dj_check(s, "k_aud_chunks");
     const uint32_t L = a->n_walk + a->n_files;
     hipLaunchKernelGGL(k_aud_walk, dim3((L + 63) / 64), dim3(64), 0, s, *a);
