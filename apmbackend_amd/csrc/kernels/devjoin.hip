@@ -1668,12 +1668,21 @@ __global__ void k_resolve_len(DJFormatArgs f) {
   else if (!st) atomicAdd(&f.counts->n_dropped, 1u);
 }
 
+// Totals, the batch's ring region and the write verdict (DeviceJoin::ring_reserve's rules, from
+// the head / low the host passed: the low only grows, so a stale one is the stricter bound).
 __global__ void k_plan_totals(DJFormatArgs f) {
   const U4 o = reinterpret_cast<const U4*>(f.offs)[f.n_out];
   f.counts->text_bytes = o.x;
   f.counts->n_stats = o.y;
   f.counts->tx_text_bytes = o.z;
   f.counts->db_text_bytes = o.w;
+  const uint64_t base = ring_place(f.ring_head, o.x, f.ring_cap);
+  uint32_t v = DJ_WRITE_OK;
+  if ((uint64_t)o.x > f.ring_cap / 4) v = DJ_WRITE_TOO_BIG;
+  else if (base + o.x > f.ring_low + f.ring_cap) v = DJ_WRITE_RING_FULL;
+  else if ((f.want_tx && o.z > f.txt_cap) || (f.want_db && o.w > f.txt_cap)) v = DJ_WRITE_TXT;
+  *f.ring_pos = base;
+  f.counts->pad[1] = v;
 }
 
 // One tx wire line (TransactionEntry.toCSVString) through a line writer: the head (names and
@@ -1729,8 +1738,10 @@ __device__ __forceinline__ void tx_line_head(const DJFormatArgs& f, const TxDev&
 constexpr int TXW_LINES = 64;
 constexpr int TXW_THREADS = 2 * TXW_LINES;  // wave 0: the lines' heads, wave 1: their tails
 constexpr uint32_t TXW_LDS = 8192;
-__device__ __forceinline__ void write_one(const DJFormatArgs& f, const TxDev& t, uint32_t i, char* staged_line);
-__device__ __forceinline__ void write_tail(const DJFormatArgs& f, const TxDev& t, uint32_t i, char* staged_line);
+__device__ __forceinline__ void write_one(const DJFormatArgs& f, const TxDev& t, uint32_t i, uint64_t ring_base,
+                                          char* staged_line);
+__device__ __forceinline__ void write_tail(const DJFormatArgs& f, const TxDev& t, uint32_t i, uint64_t ring_base,
+                                           char* staged_line);
 
 __device__ __forceinline__ void txw_copy_out(const char* __restrict__ lds, char* __restrict__ out, uint32_t g0,
                                              uint32_t g1) {
@@ -1749,21 +1760,23 @@ __device__ __forceinline__ void txw_copy_out(const char* __restrict__ lds, char*
 
 __global__ __launch_bounds__(TXW_THREADS) void k_write(DJFormatArgs f) {
   __shared__ __align__(16) char stage[TXW_LDS];
+  if (f.counts->pad[1] != DJ_WRITE_OK) return;  // (uniform: the plan's verdict)
+  const uint64_t ring_base = *f.ring_pos;
   const uint32_t j0 = blockIdx.x * TXW_LINES;
   const uint32_t j1 = min(f.n_out, j0 + TXW_LINES);
   const bool tail = threadIdx.x >= (unsigned)TXW_LINES;  // uniform per wave
   const uint32_t i = j0 + (threadIdx.x & (TXW_LINES - 1));
   const U4* offs = reinterpret_cast<const U4*>(f.offs);
   // physical ring offsets of the block's byte range (contiguous: the region does not wrap)
-  const uint64_t rb = f.ring_base & (f.ring_cap - 1);
+  const uint64_t rb = ring_base & (f.ring_cap - 1);
   const uint32_t p0 = (uint32_t)(rb + offs[j0].x), p1 = (uint32_t)(rb + offs[j1].x);
   const bool staged = p1 - (p0 & ~3u) <= TXW_LDS;  // uniform across the block
   if (i < j1) {
     const TxDev t = f.out[i];
     char* const sl = staged ? stage + ((uint32_t)(rb + offs[i].x) - (p0 & ~3u)) : nullptr;
     if (t.raw >= 0) {
-      if (tail) write_tail(f, t, i, sl);
-      else write_one(f, t, i, sl);
+      if (tail) write_tail(f, t, i, ring_base, sl);
+      else write_one(f, t, i, ring_base, sl);
     }
   }
   if (staged) {
@@ -1773,9 +1786,10 @@ __global__ __launch_bounds__(TXW_THREADS) void k_write(DJFormatArgs f) {
 }
 
 // the numbers of the ring line, after its head (the other wave of the block writes the head)
-__device__ __forceinline__ void write_tail(const DJFormatArgs& f, const TxDev& t, uint32_t i, char* staged_line) {
+__device__ __forceinline__ void write_tail(const DJFormatArgs& f, const TxDev& t, uint32_t i, uint64_t ring_base,
+                                           char* staged_line) {
   const U4 o = reinterpret_cast<const U4*>(f.offs)[i];
-  const uint64_t vpos = f.ring_base + o.x;
+  const uint64_t vpos = ring_base + o.x;
   char* p0 = staged_line ? staged_line : f.ring + (vpos & (f.ring_cap - 1));
   const RawSvc rs = f.raw[t.raw];
   bool inexact = false;
@@ -1785,10 +1799,11 @@ __device__ __forceinline__ void write_tail(const DJFormatArgs& f, const TxDev& t
 }
 
 // the head of the ring line, the tx / db stream copies of the whole line, the stats record
-__device__ __forceinline__ void write_one(const DJFormatArgs& f, const TxDev& t, uint32_t i, char* staged_line) {
+__device__ __forceinline__ void write_one(const DJFormatArgs& f, const TxDev& t, uint32_t i, uint64_t ring_base,
+                                          char* staged_line) {
   const U4 o = reinterpret_cast<const U4*>(f.offs)[i];
   const U4 l = reinterpret_cast<const U4*>(f.lens)[i];
-  const uint64_t vpos = f.ring_base + o.x;
+  const uint64_t vpos = ring_base + o.x;
   char* p0 = staged_line ? staged_line : f.ring + (vpos & (f.ring_cap - 1));
   const RawSvc rs = f.raw[t.raw];
   bool inexact = false;
@@ -1824,9 +1839,9 @@ __device__ __forceinline__ void write_one(const DJFormatArgs& f, const TxDev& t,
   }
 }
 
-__global__ void k_cands(DJFormatArgs f, uint32_t n) {
+__global__ void k_cands(DJFormatArgs f) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
+  if (f.counts->pad[1] != DJ_WRITE_OK || j >= f.counts->n_stats) return;
   if (j == 0 || f.tx_bmax[j] > f.tx_bmax[j - 1]) {
     const uint32_t k = atomicAdd(&f.counts->n_cand, 1u);
     f.cand[k] = j;
@@ -1844,9 +1859,9 @@ __global__ void k_cands(DJFormatArgs f, uint32_t n) {
   }
 }
 
-__global__ void k_reset_first(DJFormatArgs f, uint32_t n) {
+__global__ void k_reset_first(DJFormatArgs f) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
+  if (f.counts->pad[1] != DJ_WRITE_OK || j >= f.counts->n_stats) return;
   const int32_t r = f.tx_raw[j];
   if (f.raw_first[r] != INT_MAX) f.raw_first[r] = INT_MAX;
 }
@@ -2482,18 +2497,19 @@ int apm_dj_plan(DJFormatArgs* f, hipStream_t s) {
   return 0;
 }
 
-int apm_dj_write(DJFormatArgs* f, uint32_t n_stats, hipStream_t s) {
+// Sized by n_out (host-known after sync A): the stats count n_stats <= n_out is on the device
+// only.  The max scan runs over n_out entries -- the ones past n_stats are stale and affect no
+// prefix below it.
+int apm_dj_write(DJFormatArgs* f, hipStream_t s) {
   const uint32_t n = f->n_out;
-  if (n) hipLaunchKernelGGL(k_write, dim3((n + TXW_LINES - 1) / TXW_LINES), dim3(TXW_THREADS), 0, s, *f);
-  if (!n_stats) return 0;
+  if (!n) return 0;
+  hipLaunchKernelGGL(k_write, dim3((n + TXW_LINES - 1) / TXW_LINES), dim3(TXW_THREADS), 0, s, *f);
   size_t need = 0;
-  HIP_OK(rocprim::inclusive_scan(nullptr, need, f->tx_bucket, f->tx_bmax, (size_t)n_stats,
-                                 rocprim::maximum<int64_t>(), s));
+  HIP_OK(rocprim::inclusive_scan(nullptr, need, f->tx_bucket, f->tx_bmax, (size_t)n, rocprim::maximum<int64_t>(), s));
   if (need > f->tmp_bytes) return -1;
-  HIP_OK(rocprim::inclusive_scan(f->tmp, need, f->tx_bucket, f->tx_bmax, (size_t)n_stats,
-                                 rocprim::maximum<int64_t>(), s));
-  hipLaunchKernelGGL(k_cands, dim3((n_stats + TB - 1) / TB), dim3(TB), 0, s, *f, n_stats);
-  hipLaunchKernelGGL(k_reset_first, dim3((n_stats + TB - 1) / TB), dim3(TB), 0, s, *f, n_stats);
+  HIP_OK(rocprim::inclusive_scan(f->tmp, need, f->tx_bucket, f->tx_bmax, (size_t)n, rocprim::maximum<int64_t>(), s));
+  hipLaunchKernelGGL(k_cands, dim3((n + TB - 1) / TB), dim3(TB), 0, s, *f);
+  hipLaunchKernelGGL(k_reset_first, dim3((n + TB - 1) / TB), dim3(TB), 0, s, *f);
   return 0;
 }
 

@@ -12,6 +12,21 @@ namespace apm {
 constexpr int SOAP_SEGS = 16;            // scan segments per SOAP chunk
 constexpr uint32_t DJ_OVF_CAP = 1u << 16; // outputs beyond the first two of one op
 
+// The plan's write verdict (JoinCounts::pad[1]): the write pass runs only on DJ_WRITE_OK.
+enum : uint32_t {
+  DJ_WRITE_OK = 0,
+  DJ_WRITE_TXT = 1,       // the tx / audit_db text exceeds the staging (host: grow, write again)
+  DJ_WRITE_TOO_BIG = 2,   // one batch's ring text over a quarter of the ring
+  DJ_WRITE_RING_FULL = 3, // the pending released-tx lines would be overwritten
+};
+
+// Where a batch of `bytes` ring text goes (virtual position): after `head`, moved to the next
+// ring start when it would wrap (the region stays contiguous).  Device (k_plan_totals) and host
+// (DeviceJoin::run, after sync C) compute it alike.
+__host__ __device__ inline uint64_t ring_place(uint64_t head, uint64_t bytes, uint64_t cap) {
+  return ((head & (cap - 1)) + bytes > cap) ? (head + cap - 1) & ~(cap - 1) : head;
+}
+
 struct DJOverflow {
   uint32_t ev, sub;
   uint32_t pad[14];
@@ -155,7 +170,12 @@ struct DJFormatArgs {
   // ring
   char* ring;
   uint64_t ring_cap;              // power of two
-  uint64_t ring_base;             // virtual position of this batch's text
+  // The batch's ring region is placed on the device (k_plan_totals: ring_place from the head the
+  // host knows at launch), so no host round trip sits between the plan and the write pass.
+  uint64_t ring_head;             // virtual ring head before this batch (host's, at launch)
+  uint64_t ring_low;              // oldest pending ring byte (host's, at launch; only grows)
+  uint64_t* ring_pos;             // [1] device: this batch's ring base (written by k_plan_totals)
+  uint64_t txt_cap;               // bytes of txt_tx and of txt_db
   // stats hand-off
   TxRec* tx;                      // [n_stats]
   int32_t* tx_raw;
@@ -182,10 +202,13 @@ size_t apm_dj_tmp_bytes(uint32_t max_ev, uint32_t max_out, int table_bits);
 int apm_dj_select_host(apm::DJArgs* a, const uint32_t* d_n_ev, uint32_t max_ev, hipStream_t s);
 // join stream: ops, SOAP scan, grouping, expiry, group walk, placement; counts -> a->counts.
 int apm_dj_join(apm::DJArgs* a, hipStream_t s);
-// after the host filled the PENDING registry slots: resolve raw ids, line lengths, scans.
+// after the host filled the PENDING registry slots: resolve raw ids, line lengths, scans, the
+// ring placement and the write verdict (counts->pad[1], DJ_WRITE_*).
 int apm_dj_plan(apm::DJFormatArgs* f, hipStream_t s);
 // text into the ring, stats arrays, rollover candidates, unresolved series, optional streams.
-int apm_dj_write(apm::DJFormatArgs* f, uint32_t n_stats, hipStream_t s);
+// Nothing is written unless the plan's verdict was DJ_WRITE_OK (n_out: the tx count, a bound of
+// the stats count the kernels read from counts).
+int apm_dj_write(apm::DJFormatArgs* f, hipStream_t s);
 // key-table rebuild: live entries of `old` reinserted into `fresh` (zeroed by the caller).
 // Dropped keys / expired partials free their chain blocks into the pool (pool may be null when
 // `now` is -inf: nothing is dropped).

@@ -195,7 +195,22 @@ DeviceJoin::DeviceJoin(const DevJoinConfig& cfg, Dictionary* dict, const std::ve
   d_stage_ = (TxDev*)dmalloc((size_t)E * 2 * sizeof(TxDev));
   d_ovf_ = (DJOverflow*)dmalloc((size_t)DJ_OVF_CAP * sizeof(DJOverflow));
   d_ring_ = (char*)dmalloc(cfg_.ring_bytes);
+  d_ring_pos_ = (uint64_t*)dmalloc(8);
   HIP_OK(hipStreamSynchronize(stream_));
+}
+
+// the tx / audit_db text staging of the write pass: >= `bytes` each (the join stream is idle or
+// about to use it after this call; hipFree orders against the device)
+void DeviceJoin::ensure_txt(size_t bytes) {
+  if (bytes <= txt_cap_ && d_txt_tx_) return;
+  const size_t cap = std::max(bytes, txt_cap_);
+  char* p = nullptr;
+  HIP_OK(hipMalloc((void**)&p, cap * 2));
+  if (d_txt_tx_) { HIP_OK(hipFree(d_txt_tx_)); device_bytes_ -= txt_cap_ * 2; }
+  d_txt_tx_ = p;
+  d_txt_db_ = p + cap;
+  txt_cap_ = cap;
+  device_bytes_ += cap * 2;
 }
 
 DeviceJoin::~DeviceJoin() {
@@ -212,6 +227,7 @@ DeviceJoin::~DeviceJoin() {
   if (h_hbuf_) hipHostFree(h_hbuf_);
   if (h_txt_) hipHostFree(h_txt_);
   if (h_ck_bounce_) hipHostFree(h_ck_bounce_);
+  if (d_txt_tx_) hipFree(d_txt_tx_);
   for (void* p : allocs_) hipFree(p);
   hipStreamDestroy(stream_);
 }
@@ -1117,58 +1133,94 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
   f.tx = s.d_tx; f.tx_raw = s.d_tx_raw; f.tx_gid = s.d_tx_gid; f.tx_bucket = d_bucket_; f.tx_bmax = d_bmax_;
   f.cand = d_cand_; f.cand_bucket = d_cand_bucket_; f.unresolved = d_unres_;
   f.want_tx = want_tx; f.want_db = want_db; f.counts = d_counts_; f.tmp = d_tmp_; f.tmp_bytes = tmp_bytes_;
-  if (apm_dj_plan(&f, st) != 0) throw std::runtime_error("device join: scan scratch too small");
-  HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost, st));
-  HIP_OK(hipStreamSynchronize(st));  // ---- sync B
-  phase_t[6] = clock_ms();
-  const JoinCounts c2 = *h_counts_;
-  f.ring_base = ring_reserve(c2.text_bytes);
-  const size_t txt = (size_t)(want_tx ? c2.tx_text_bytes : 0) + (want_db ? c2.db_text_bytes : 0);
-  if (txt > txt_cap_) {
-    const size_t cap = txt * 2 + (16 << 20);  // (grows at most a few times: a regrow costs ms)
-    char* p = nullptr;
-    HIP_OK(hipMalloc((void**)&p, cap * 2));
-    if (d_txt_tx_) { HIP_OK(hipFree(d_txt_tx_)); device_bytes_ -= txt_cap_ * 2; }
-    d_txt_tx_ = p;
-    d_txt_db_ = p + cap;
-    txt_cap_ = cap;
-    device_bytes_ += cap * 2;
-  }
-  if (txt > h_txt_cap_) {
-    if (h_txt_) HIP_OK(hipHostFree(h_txt_));
-    h_txt_cap_ = txt * 2 + (32 << 20);
-    HIP_OK(hipHostMalloc((void**)&h_txt_, h_txt_cap_, hipHostMallocDefault));
-  }
+  // the ring region and the write verdict are decided on the device (k_plan_totals): no sync
+  // between the plan and the write pass; the host learns both at sync C
+  const uint64_t ring_head = ring_head_.load(std::memory_order_acquire);
+  f.ring_head = ring_head;
+  f.ring_low = ring_low_.load(std::memory_order_acquire);
+  f.ring_pos = d_ring_pos_;
+  if (want_tx || want_db) ensure_txt(std::max<size_t>(txt_cap_, 4u << 20));
   f.txt_tx = d_txt_tx_;
   f.txt_db = d_txt_db_;
-  if (apm_dj_write(&f, c2.n_stats, st) != 0) throw std::runtime_error("device join: scan scratch too small");
-  const uint32_t spec = std::min<uint32_t>(c2.n_stats, 4096);
-  if (spec) {
-    HIP_OK(hipMemcpyAsync(h_cand_, d_cand_, (size_t)spec * 4, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipMemcpyAsync(h_cand_bucket_, d_cand_bucket_, (size_t)spec * 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipMemcpyAsync(h_unres_, d_unres_, (size_t)spec * 8, hipMemcpyDeviceToHost, st));
+  f.txt_cap = txt_cap_;
+  if (apm_dj_plan(&f, st) != 0) throw std::runtime_error("device join: scan scratch too small");
+  phase_t[6] = clock_ms();
+  // copy-backs sized before the sizes are known: the previous batch's x 2 (the rest after sync C)
+  const uint32_t spec = std::min<uint32_t>(c.n_out, std::max<uint32_t>(2 * last_cands_, 1024));
+  const size_t spec_tx = want_tx ? std::min<size_t>(txt_cap_, 2 * (size_t)last_tx_bytes_ + 65536) : 0;
+  const size_t spec_db = want_db ? std::min<size_t>(txt_cap_, 2 * (size_t)last_db_bytes_ + 65536) : 0;
+  if (spec_tx + spec_db > h_txt_cap_) {
+    if (h_txt_) HIP_OK(hipHostFree(h_txt_));
+    h_txt_cap_ = (spec_tx + spec_db) * 2 + (4 << 20);
+    HIP_OK(hipHostMalloc((void**)&h_txt_, h_txt_cap_, hipHostMallocDefault));
   }
-  if (want_tx && c2.tx_text_bytes)
-    HIP_OK(hipMemcpyAsync(h_txt_, d_txt_tx_, c2.tx_text_bytes, hipMemcpyDeviceToHost, st));
-  if (want_db && c2.db_text_bytes)
-    HIP_OK(hipMemcpyAsync(h_txt_ + (want_tx ? c2.tx_text_bytes : 0), d_txt_db_, c2.db_text_bytes,
-                          hipMemcpyDeviceToHost, st));
-  HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost, st));
-  HIP_OK(hipStreamSynchronize(st));  // ---- sync C
+  auto write_and_copy = [&] {
+    if (apm_dj_write(&f, st) != 0) throw std::runtime_error("device join: scan scratch too small");
+    if (spec) {
+      HIP_OK(hipMemcpyAsync(h_cand_, d_cand_, (size_t)spec * 4, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipMemcpyAsync(h_cand_bucket_, d_cand_bucket_, (size_t)spec * 8, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipMemcpyAsync(h_unres_, d_unres_, (size_t)spec * 8, hipMemcpyDeviceToHost, st));
+    }
+    if (spec_tx) HIP_OK(hipMemcpyAsync(h_txt_, d_txt_tx_, spec_tx, hipMemcpyDeviceToHost, st));
+    if (spec_db) HIP_OK(hipMemcpyAsync(h_txt_ + spec_tx, d_txt_db_, spec_db, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));  // ---- sync C
+  };
+  write_and_copy();
+  JoinCounts c3 = *h_counts_;
+  if (c3.pad[1] == DJ_WRITE_TXT) {  // the staging grows; the write pass runs again (it wrote nothing)
+    ensure_txt(std::max<size_t>(c3.tx_text_bytes, c3.db_text_bytes) * 2 + (16 << 20));
+    f.txt_tx = d_txt_tx_;
+    f.txt_db = d_txt_db_;
+    f.txt_cap = txt_cap_;
+    static_assert(DJ_WRITE_OK == 0, "the verdict is cleared by a zero fill");
+    HIP_OK(hipMemsetAsync(&d_counts_->pad[1], 0, 4, st));
+    ++write_regrows_;
+    write_and_copy();
+    c3 = *h_counts_;
+  }
+  if (c3.pad[1] == DJ_WRITE_TOO_BIG)
+    throw std::runtime_error("device join: one batch of tx text exceeds a quarter of gpu.txTextRingMB");
+  if (c3.pad[1] == DJ_WRITE_RING_FULL)
+    throw std::runtime_error("device join: tx text ring exhausted (pending released-tx lines span more than "
+                             "gpu.txTextRingMB; raise it)");
+  if (c3.pad[1] != DJ_WRITE_OK) throw std::runtime_error("device join: write pass skipped");
   phase_t[7] = clock_ms();
-  const JoinCounts c3 = *h_counts_;
-  if (c3.n_cand > spec || c3.n_unresolved > spec) {
-    HIP_OK(hipMemcpyAsync(h_cand_, d_cand_, (size_t)c3.n_cand * 4, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipMemcpyAsync(h_cand_bucket_, d_cand_bucket_, (size_t)c3.n_cand * 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipMemcpyAsync(h_unres_, d_unres_, (size_t)c3.n_unresolved * 8, hipMemcpyDeviceToHost, st));
+  const uint64_t ring_base = ring_place(ring_head, c3.text_bytes, cfg_.ring_bytes);
+  {
+    std::lock_guard<std::mutex> g(ring_mu_);
+    ring_head_.store(ring_base + c3.text_bytes, std::memory_order_release);
+  }
+  const uint32_t tx_bytes = want_tx ? c3.tx_text_bytes : 0, db_bytes = want_db ? c3.db_text_bytes : 0;
+  if (c3.n_cand > spec || c3.n_unresolved > spec || tx_bytes > spec_tx || db_bytes > spec_db) {
+    if (c3.n_cand > spec || c3.n_unresolved > spec) {
+      HIP_OK(hipMemcpyAsync(h_cand_, d_cand_, (size_t)c3.n_cand * 4, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipMemcpyAsync(h_cand_bucket_, d_cand_bucket_, (size_t)c3.n_cand * 8, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipMemcpyAsync(h_unres_, d_unres_, (size_t)c3.n_unresolved * 8, hipMemcpyDeviceToHost, st));
+    }
+    if (tx_bytes > spec_tx || db_bytes > spec_db) {  // (both streams again, into a larger buffer)
+      if ((size_t)tx_bytes + db_bytes > h_txt_cap_) {
+        HIP_OK(hipStreamSynchronize(st));
+        if (h_txt_) HIP_OK(hipHostFree(h_txt_));
+        h_txt_cap_ = ((size_t)tx_bytes + db_bytes) * 2 + (4 << 20);
+        HIP_OK(hipHostMalloc((void**)&h_txt_, h_txt_cap_, hipHostMallocDefault));
+      }
+      if (tx_bytes) HIP_OK(hipMemcpyAsync(h_txt_, d_txt_tx_, tx_bytes, hipMemcpyDeviceToHost, st));
+      if (db_bytes) HIP_OK(hipMemcpyAsync(h_txt_ + tx_bytes, d_txt_db_, db_bytes, hipMemcpyDeviceToHost, st));
+    }
     HIP_OK(hipStreamSynchronize(st));
   }
+  const char* h_tx_txt = h_txt_;
+  const char* h_db_txt = h_txt_ + ((tx_bytes > spec_tx || db_bytes > spec_db) ? tx_bytes : spec_tx);
+  last_tx_bytes_ = tx_bytes;
+  last_db_bytes_ = db_bytes;
+  last_cands_ = std::max(c3.n_cand, c3.n_unresolved);
   out.slot = k;
   out.n_out = c3.n_out;
   out.n_stats = c3.n_stats;
   out.n_db = c3.n_db;
   out.n_dropped = c3.n_dropped;
-  out.ring_base = f.ring_base;
+  out.ring_base = ring_base;
   out.d_tx = s.d_tx;
   out.d_raw = s.d_tx_raw;
   out.d_gid = s.d_tx_gid;
@@ -1184,8 +1236,8 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
   std::sort(out.unresolved.begin(), out.unresolved.end());
   out.text_tx.clear();
   out.text_db.clear();
-  if (want_tx) out.text_tx.assign(h_txt_, c2.tx_text_bytes);
-  if (want_db) out.text_db.assign(h_txt_ + (want_tx ? c2.tx_text_bytes : 0), c2.db_text_bytes);
+  if (want_tx) out.text_tx.assign(h_tx_txt, tx_bytes);
+  if (want_db) out.text_db.assign(h_db_txt, db_bytes);
   tx_ += c3.n_out;
   tx_db_ += c3.n_db;
   aud_cur_ ^= 1;  // the next batch reads what this one carried

@@ -329,6 +329,12 @@ class DeviceJoin {
   size_t txt_cap_ = 0;
   char* h_txt_ = nullptr;
   size_t h_txt_cap_ = 0;
+  // copied back before their sizes are known (no sync between the plan and the write): the
+  // previous batch's sizes x 2; a larger batch copies the rest after sync C
+  uint32_t last_tx_bytes_ = 0, last_db_bytes_ = 0, last_cands_ = 0;
+  uint64_t* d_ring_pos_ = nullptr;  // this batch's ring base (k_plan_totals)
+  uint64_t write_regrows_ = 0;      // write passes redone after the text staging grew
+  void ensure_txt(size_t bytes);
   void* d_tmp_ = nullptr;
   size_t tmp_bytes_ = 0;
   JoinCounts* d_counts_ = nullptr;

@@ -1181,7 +1181,7 @@ void Engine::process_batch_dev_tail(ParseSlot& ps, double t0, double now_overrid
   trace_event("join (GPU)", t1, t2, 0);
   if (trace_on_) {
     static const char* names[DeviceJoin::kPhases] = {"dj.prepass", "dj.upload", "dj.launch", "dj.syncA",
-                                                     "dj.register", "dj.plan+syncB", "dj.write+syncC", "dj.tail"};
+                                                     "dj.register", "dj.plan", "dj.write+syncC", "dj.tail"};
     for (int i = 0; i < DeviceJoin::kPhases; ++i) trace_event(names[i], dj_->phase_t[i], dj_->phase_t[i + 1], 2);
     for (const auto& sp : dj_->spans) trace_event(sp.first, sp.second.first, sp.second.second, 2);
   }
