@@ -39,27 +39,19 @@ namespace {
 
 constexpr int TB = 256;
 
-// Op grouping sort (table slot, ~20 bits, 100k-300k ops): rocprim's default switches to onesweep
-// only above 1M items and below that runs a block sort + ~8 merge passes (~140 us per batch on
-// the join's critical path, profiles/r3_*); onesweep does 3 digit passes.
+// Op grouping by sort (APM_OPSORT=sort, the A/B form of the slot lists, DJArgs::slot_head).  Keys
+// are table slots [0, cap), cap (JOP_DIRECT) and cap + 1 (no op): table_bits + 1 bits; onesweep
+// with 11-bit digits (two passes up to 22 bits), 8-bit digits above.  (rocprim's default runs a
+// block sort + ~8 merge passes below 1M items: ~140 us per batch, profiles/r3_*.)
 using OpSortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
                                              rocprim::default_config, 0>;
-// 11-bit digits: two onesweep passes for keys up to 22 bits instead of three
 using OpSortCfg11 = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
     rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>, 11,
                                         rocprim::block_radix_rank_algorithm::match>,
     0>;
-// Op keys are table slots [0, cap), cap (JOP_DIRECT) and cap + 1 (no op): table_bits + 1 bits.
-// (They were sorted over table_bits + 2 bits: 23 for the 2M-slot table, three passes of any digit
-// width up to 11.)  With <= 22 bits the 11-bit onesweep takes two.  APM_OPSORT=8: the 8-bit
-// onesweep (three passes), =m: rocprim's default dispatch (A/B).
 static int op_sort_bits(int table_bits) { return table_bits + 1; }
-static bool opsort11(int table_bits) {
-  static const int mode = [] { const char* e = std::getenv("APM_OPSORT"); return e ? (int)e[0] : 0; }();
-  if (mode == '8' || mode == 'm') return false;
-  return op_sort_bits(table_bits) <= 22;
-}
+static bool opsort11(int table_bits) { return op_sort_bits(table_bits) <= 22; }
 
 __device__ __forceinline__ uint32_t grid_n(uint32_t n) { return (n + TB - 1) / TB; }
 
@@ -1130,7 +1122,12 @@ __global__ void k_claim(DJArgs a) {
     if (b && (threadIdx.x & (APM_WAVE - 1)) == lead) atomicAdd(&a.counts->n_keys_new, (uint32_t)__popcll(b));
   }
   a.op_slot[i] = key;
-  a.op_idx[i] = i;
+  if (a.group_sort) {
+    a.op_idx[i] = i;
+  } else {  // push onto the key's list (the op that finds it empty leads the group)
+    if (i == 0) { a.big[0] = 0; a.big[1] = 0; }
+    a.op_idx[i] = key < cap ? atomicExch(&a.slot_head[key], i) : ~0u;
+  }
   if (op.op != JOP_NONE && (op.flags & JF_HAS_SVC)) {
     const uint64_t k = regkey_of(op.svc, op.server);
     uint32_t h = home_of(k, a.reg_mask);
@@ -1430,22 +1427,118 @@ __device__ void need_drain(DJArgs& a, NeedEnt& ne, int32_t nidx, double acct, Em
   ne.n = 0;
 }
 
+__device__ __forceinline__ void walk_direct(const DJArgs& a, uint32_t ev) {  // JOP_DIRECT: empty logId, no cache state
+  const JOp op = a.ops[ev];
+  Emitter em{a.stage, a.ovf, &a.counts->pad[0], ev, 0};
+  em.put(make_tx(op.server, op.svc, LID_NONE, 0, 0, (op.flags & JF_BAF) ? op.aux : apm_nan(), 0.0, true, op.ts,
+                 (op.flags & JF_TS_EMPTY) != 0, op.num, false));
+  a.out_cnt[ev] = em.sub;
+}
+
+template <class M>
+__device__ void walk_group(DJArgs& a, uint32_t slot, const M& mem, uint32_t g);
+
+// Slot lists (DJArgs::slot_head): the group's leader collects its members (pushed in any order)
+// and walks them in line order.  Up to GW_SMALL members are insertion-sorted in registers; a
+// larger group is queued for k_group_walk_big (its list is left in place).
+constexpr uint32_t GW_SMALL = 16;
 __global__ void k_group_walk(DJArgs a) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.n_ev) return;
   const uint32_t cap = a.table_mask + 1;
-  const uint32_t slot = a.op_slot_sorted[i];
-  if (slot > cap) return;  // no op
-  if (slot == cap) {       // JOP_DIRECT: empty logId, no cache state
-    const uint32_t ev = a.op_idx_sorted[i];
-    const JOp op = a.ops[ev];
-    Emitter em{a.stage, a.ovf, &a.counts->pad[0], ev, 0};
-    em.put(make_tx(op.server, op.svc, LID_NONE, 0, 0, (op.flags & JF_BAF) ? op.aux : apm_nan(), 0.0, true, op.ts,
-                   (op.flags & JF_TS_EMPTY) != 0, op.num, false));
-    a.out_cnt[ev] = em.sub;
+  if (a.group_sort) {
+    const uint32_t slot = a.op_slot_sorted[i];
+    if (slot > cap) return;  // no op
+    if (slot == cap) { walk_direct(a, a.op_idx_sorted[i]); return; }
+    if (i > 0 && a.op_slot_sorted[i - 1] == slot) return;  // not the first op of its key
+    uint32_t g = 1;
+    while (i + g < a.n_ev && a.op_slot_sorted[i + g] == slot) ++g;
+    const uint32_t* m = a.op_idx_sorted + i;
+    walk_group(a, slot, [m](uint32_t q) { return m[q]; }, g);
     return;
   }
-  if (i > 0 && a.op_slot_sorted[i - 1] == slot) return;  // not the first op of its key
+  const uint32_t slot = a.op_slot[i];
+  if (slot > cap) return;
+  if (slot == cap) { walk_direct(a, i); return; }
+  if (a.op_idx[i] != ~0u) return;  // not the group's leader (its list was not empty)
+  uint32_t m[GW_SMALL];
+  uint32_t g = 0;
+  for (uint32_t j = a.slot_head[slot]; j != ~0u; j = a.op_idx[j]) {
+    if (g == GW_SMALL) {
+      a.op_slot_sorted[atomicAdd(&a.big[0], 1u)] = slot;
+      return;
+    }
+    uint32_t p = g++;
+    for (; p > 0 && m[p - 1] > j; --p) m[p] = m[p - 1];
+    m[p] = j;
+  }
+  a.slot_head[slot] = ~0u;
+  walk_group(a, slot, [&m](uint32_t q) { return m[q]; }, g);
+}
+
+// Ascending sort of v[0, g) by one workgroup (LDS or global memory): a bitonic network whose merge
+// steps start with the mirrored comparison, so every comparator puts the smaller value first and
+// the virtual padding to a power of two (+inf past g) never moves.
+__device__ void block_sort_asc(uint32_t* v, uint32_t g) {
+  uint32_t np2 = 1;
+  while (np2 < g) np2 <<= 1;
+  for (uint32_t k = 2; k <= np2; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t t = threadIdx.x; t < np2 / 2; t += blockDim.x) {
+        uint32_t lo, hi;
+        if (j == (k >> 1)) {
+          lo = (t / j) * k + t % j;
+          hi = (t / j) * k + k - 1 - t % j;
+        } else {
+          lo = (t / j) * 2 * j + t % j;
+          hi = lo + j;
+        }
+        if (hi < g) {
+          const uint32_t x = v[lo], y = v[hi];
+          if (x > y) { v[lo] = y; v[hi] = x; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Groups of more than GW_SMALL ops (hot keys): one workgroup each -- thread 0 gathers the list,
+// the workgroup sorts it (LDS up to GWB_LDS members), thread 0 walks it.
+constexpr uint32_t GWB_LDS = 4096;
+constexpr int GWB_THREADS = 256;
+__global__ __launch_bounds__(GWB_THREADS) void k_group_walk_big(DJArgs a) {
+  __shared__ uint32_t lds[GWB_LDS];
+  __shared__ uint32_t s_g, s_off;
+  const uint32_t nb = a.big[0];
+  for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    const uint32_t slot = a.op_slot_sorted[b];
+    if (threadIdx.x == 0) {
+      uint32_t g = 0;
+      for (uint32_t j = a.slot_head[slot]; j != ~0u; j = a.op_idx[j]) ++g;
+      const uint32_t off = atomicAdd(&a.big[1], g);  // (members of all groups <= n_ev)
+      uint32_t k = 0;
+      for (uint32_t j = a.slot_head[slot]; j != ~0u; j = a.op_idx[j]) a.op_idx_sorted[off + k++] = j;
+      a.slot_head[slot] = ~0u;
+      s_g = g;
+      s_off = off;
+    }
+    __syncthreads();
+    const uint32_t g = s_g;
+    uint32_t* v = a.op_idx_sorted + s_off;
+    if (g <= GWB_LDS) {
+      for (uint32_t t = threadIdx.x; t < g; t += blockDim.x) lds[t] = v[t];
+      __syncthreads();
+      v = lds;
+    }
+    block_sort_asc(v, g);
+    if (threadIdx.x == 0) walk_group(a, slot, [v](uint32_t q) { return v[q]; }, g);
+    __syncthreads();
+  }
+}
+
+template <class M>
+__device__ void walk_group(DJArgs& a, uint32_t slot, const M& mem, uint32_t g) {
   KeyState ks = a.table[slot];
   const double now = a.now;
   bool acct_live = ks.acct_exp >= now;
@@ -1459,8 +1552,8 @@ __global__ void k_group_walk(DJArgs a) {
     NeedEnt* c = &a.arena[ks.need];
     if (c->key == ks.key && c->exp >= now) { ne = c; nidx = ks.need; }
   }
-  for (uint32_t j = i; j < a.n_ev && a.op_slot_sorted[j] == slot; ++j) {
-    const uint32_t ev = a.op_idx_sorted[j];
+  for (uint32_t q = 0; q < g; ++q) {
+    const uint32_t ev = mem(q);
     const JOp op = a.ops[ev];
     Emitter em{a.stage, a.ovf, &a.counts->pad[0], ev, 0};
     const bool ts_empty = (op.flags & JF_TS_EMPTY) != 0;
@@ -2411,15 +2504,9 @@ int apm_dj_join(DJArgs* a, hipStream_t s) {
     dj_check(s, "k_soap_apply");
     hipLaunchKernelGGL(k_claim, dim3((n + TB - 1) / TB), dim3(TB), 0, s, *a);
     dj_check(s, "k_claim");
-    static const bool merge_sort = [] { const char* e = std::getenv("APM_OPSORT"); return e && e[0] == 'm'; }();
     size_t need = 0;
-    if (merge_sort) {  // diagnostic: rocprim's default (block sort + merge passes)
-      HIP_OK(rocprim::radix_sort_pairs(nullptr, need, a->op_slot, a->op_slot_sorted, a->op_idx, a->op_idx_sorted,
-                                       (size_t)n, 0, op_sort_bits(a->table_bits), s));
-      if (need > a->tmp_bytes) return -1;
-      HIP_OK(rocprim::radix_sort_pairs(a->tmp, need, a->op_slot, a->op_slot_sorted, a->op_idx, a->op_idx_sorted,
-                                       (size_t)n, 0, op_sort_bits(a->table_bits), s));
-      dj_check(s, "rocprim_radix_sort_pairs");
+    if (!a->group_sort) {
+      // (slot lists: no sort)
     } else if (opsort11(a->table_bits)) {
       HIP_OK(rocprim::radix_sort_pairs<OpSortCfg11>(nullptr, need, a->op_slot, a->op_slot_sorted, a->op_idx,
                                                     a->op_idx_sorted, (size_t)n, 0, op_sort_bits(a->table_bits), s));
@@ -2463,6 +2550,10 @@ int apm_dj_join(DJArgs* a, hipStream_t s) {
   if (n) {
     hipLaunchKernelGGL(k_group_walk, dim3((n + TB - 1) / TB), dim3(TB), 0, s, *a);
     dj_check(s, "k_group_walk");
+    if (!a->group_sort) {  // (a few idle workgroups when no group is big)
+      hipLaunchKernelGGL(k_group_walk_big, dim3(32), dim3(GWB_THREADS), 0, s, *a);
+      dj_check(s, "k_group_walk_big");
+    }
     size_t need = 0;
     HIP_OK(rocprim::exclusive_scan(nullptr, need, a->out_cnt, a->out_pos, 0u, (size_t)n + 1,
                                    rocprim::plus<uint32_t>(), s));

@@ -106,11 +106,18 @@ struct DJArgs {
   uint32_t* seg_in;               // incoming state per segment
   uint64_t* chain_hash;           // per chunk: carried context hash of its file
   SoapState* soap_state;          // [max files] carried per file
-  // ---- grouping
-  uint32_t* op_slot;              // [n_ev] sort keys (table slot / DIRECT / NONE)
-  uint32_t* op_slot_sorted;
-  uint32_t* op_idx;
-  uint32_t* op_idx_sorted;
+  // ---- grouping.  Default (slot lists): k_claim pushes each op onto its key's list
+  // (slot_head[slot] <- op, op_idx[op] = the previous head); the op that found the list empty
+  // leads the group -- it collects and orders the members (k_group_walk; groups of more than
+  // GW_SMALL ops go to k_group_walk_big, one workgroup each) and empties the list again.
+  // APM_OPSORT=sort: the stable radix sort of (slot, op) pairs (the round-4 form, for A/B).
+  uint32_t* op_slot;              // [n_ev] table slot / DIRECT / NONE
+  uint32_t* op_slot_sorted;       // sort: sorted slots; lists: the big groups' leaders
+  uint32_t* op_idx;               // sort: op indices; lists: the next (earlier-pushed) member
+  uint32_t* op_idx_sorted;        // sort: sorted op indices; lists: the big groups' members
+  uint32_t* slot_head;            // lists: [table cap] list heads, ~0u between batches
+  uint32_t* big;                  // lists: [2] big groups, their members (zeroed by k_claim)
+  int group_sort;                 // 1: the radix-sort grouping
   void* tmp;                      // rocprim scratch
   size_t tmp_bytes;
   KeyState* table;

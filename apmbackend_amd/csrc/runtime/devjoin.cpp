@@ -196,6 +196,11 @@ DeviceJoin::DeviceJoin(const DevJoinConfig& cfg, Dictionary* dict, const std::ve
   d_ovf_ = (DJOverflow*)dmalloc((size_t)DJ_OVF_CAP * sizeof(DJOverflow));
   d_ring_ = (char*)dmalloc(cfg_.ring_bytes);
   d_ring_pos_ = (uint64_t*)dmalloc(8);
+  d_big_ = (uint32_t*)dmalloc(8);
+  {
+    const char* e = std::getenv("APM_OPSORT");
+    group_sort_ = e && std::strcmp(e, "sort") == 0;
+  }
   HIP_OK(hipStreamSynchronize(stream_));
 }
 
@@ -1043,6 +1048,13 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
   a.soap_state = d_soap_;
   a.op_slot = d_op_slot_; a.op_slot_sorted = d_op_slot_sorted_; a.op_idx = d_op_idx_; a.op_idx_sorted = d_op_idx_sorted_;
   a.tmp = d_tmp_; a.tmp_bytes = tmp_bytes_;
+  if (!group_sort_ && heads_cap_ != table_cap_) {  // (the join stream is ordered after any rebuild)
+    if (d_slot_head_) { HIP_OK(hipStreamSynchronize(st)); dfree(d_slot_head_, (size_t)heads_cap_ * 4); }
+    d_slot_head_ = (uint32_t*)dmalloc((size_t)table_cap_ * 4);
+    HIP_OK(hipMemsetAsync(d_slot_head_, 0xff, (size_t)table_cap_ * 4, st));
+    heads_cap_ = table_cap_;
+  }
+  a.slot_head = d_slot_head_; a.big = d_big_; a.group_sort = group_sort_ ? 1 : 0;
   a.table = d_table_; a.table_mask = table_cap_ - 1; a.table_bits = table_bits_;
   a.pool = d_pool_; a.pool_ring = d_pool_ring_; a.pool_mask = pool_n_ - 1;
   a.reg = d_reg_; a.reg_mask = (1u << cfg_.reg_bits) - 1; a.miss = d_miss_; a.miss_cap = miss_cap_;
@@ -1264,6 +1276,11 @@ size_t DeviceJoin::trim(double now) {
     dfree(d_table_spare_, (size_t)table_cap_ * sizeof(KeyState));
     d_table_spare_ = nullptr;
     spare_clean_ = false;
+  }
+  if (d_slot_head_) {  // sized by the table: re-made by the next batch
+    dfree(d_slot_head_, (size_t)heads_cap_ * 4);
+    d_slot_head_ = nullptr;
+    heads_cap_ = 0;
   }
   if (d_rb_scratch_) {  // sized by the table: re-made by the next in-place rebuild
     dfree(d_rb_scratch_, rb_scratch_bytes_);

@@ -333,6 +333,12 @@ class DeviceJoin {
   // previous batch's sizes x 2; a larger batch copies the rest after sync C
   uint32_t last_tx_bytes_ = 0, last_db_bytes_ = 0, last_cands_ = 0;
   uint64_t* d_ring_pos_ = nullptr;  // this batch's ring base (k_plan_totals)
+  // op grouping by slot lists (DJArgs::slot_head): one head per table slot, all empty between
+  // batches (so a same-size rebuild keeps them valid); re-made when the table size changes
+  uint32_t* d_slot_head_ = nullptr;
+  uint32_t heads_cap_ = 0;
+  uint32_t* d_big_ = nullptr;
+  bool group_sort_ = false;  // APM_OPSORT=sort
   uint64_t write_regrows_ = 0;      // write passes redone after the text staging grew
   void ensure_txt(size_t bytes);
   void* d_tmp_ = nullptr;

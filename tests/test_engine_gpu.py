@@ -669,6 +669,24 @@ def test_join_overflow_chains_match_oracle():
     assert j["chain_partial_blocks"] > 0 and j["chain_need_blocks"] > 0 and j["chain_logid_blocks"] > 0
 
 
+def test_hot_logid_groups_match_oracle():
+    """Keys with thousands of ops in one batch.  The join groups a batch's ops by key with slot
+    lists (devjoin.hip k_claim / k_group_walk): a key with more than 16 ops is walked by
+    k_group_walk_big, which sorts its members in LDS up to 4096 and in global memory above --
+    these logIds carry 40 to 4850 provider lines in one batch."""
+    cfg = SynthConfig(servers=1, duration_s=40, tx_per_sec_per_server=0.5, seed=5, sub_calls=(20, 2500),
+                      ejb_services=2, provider_services=8, audit_fraction=0.0, soap_late_fraction=0.3)
+    lines = Generator(cfg).generate()
+    bl = with_watermarks(batches(lines, cfg.start_ms, 5.0), UTC)
+    C = small_cfg("exact")
+    P = PipelineOracle(copy.deepcopy(C), UTC)
+    P.run_batches(bl)
+    eng, out = _run_engine(C, bl)
+    _assert_streams(out, P)
+    j = eng.metrics()["join"]
+    assert j["partial_overflow"] == 0 and j["table_full"] == 0 and j["pool_exhausted"] == 0
+
+
 @pytest.mark.parametrize("restore", [True, False], ids=["ckpt", "same"])
 def test_join_tables_grow_instead_of_failing(tmp_path, restore):
     """Key table, need arena and chain pool all start at 1024 entries: each batch's worst case
