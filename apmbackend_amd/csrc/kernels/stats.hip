@@ -764,11 +764,15 @@ extern "C" {
 using namespace apm;
 
 void apm_copy(void* dst, const void* src, size_t bytes, hipStream_t stream) {
+  apm_copy_capped(dst, src, bytes, 1024, stream);
+}
+
+void apm_copy_capped(void* dst, const void* src, size_t bytes, uint32_t max_blocks, hipStream_t stream) {
   if (bytes == 0) return;
   const uintptr_t a = (uintptr_t)dst | (uintptr_t)src;
   auto launch = [&](auto* d, const auto* s, size_t w) {
     const size_t n = bytes / w, done = n * w;
-    const size_t blocks = std::max<size_t>(1, std::min<size_t>((n + 255) / 256, 1024));
+    const size_t blocks = std::max<size_t>(1, std::min<size_t>((n + 255) / 256, std::max<uint32_t>(max_blocks, 1)));
     hipLaunchKernelGGL(k_copy, dim3((unsigned)blocks), dim3(256), 0, stream, d, s, n, (uint8_t*)dst + done,
                        (const uint8_t*)src + done, (uint32_t)(bytes - done));
   };

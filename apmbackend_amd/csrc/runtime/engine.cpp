@@ -438,6 +438,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     txcopy_force_fb_ = f && f[0] == '1';
     const char* d = std::getenv("APM_D2H_KERNEL");
     d2h_kernel_ = d && d[0] == '1';
+    const char* b = std::getenv("APM_D2H_BLOCKS");
+    d2h_blocks_ = b ? (uint32_t)std::max(1, std::atoi(b)) : 32u;
   }
   // alerts
   d_alerts_ = (AlertRec*)dmalloc((size_t)cfg_.max_alerts * sizeof(AlertRec));
@@ -2019,8 +2021,13 @@ void Engine::h2d(void* d, const void* h, size_t n, hipStream_t s) {
 
 void Engine::lane_d2h(void* h, const void* d, size_t n) {
   if (!n) return;
-  if (d2h_kernel_) d2h(h, d, n, out_stream_);
-  else HIP_OK(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, out_stream_));
+  if (d2h_kernel_) {
+    void* hv = nullptr;
+    HIP_OK(hipHostGetDevicePointer(&hv, h, 0));
+    apm_copy_capped(hv, d, n, d2h_blocks_, out_stream_);
+  } else {
+    HIP_OK(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, out_stream_));
+  }
 }
 
 void Engine::d2h(void* h, const void* d, size_t n, hipStream_t s) {

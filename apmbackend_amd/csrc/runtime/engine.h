@@ -1107,8 +1107,10 @@ class Engine {
   bool rel_copy_ = false;         // the pending release was planned as COPY rows
   bool txcopy_force_fb_ = false;
   // APM_D2H_KERNEL=1: the output lane's D2H of st / fs / db text by the engine's copy kernel
-  // (16-byte lanes, up to 1024 blocks, into the mapped pinned buffer) instead of hipMemcpyAsync
+  // (16-byte lanes, at most APM_D2H_BLOCKS workgroups -- default 32 -- into the mapped pinned
+  // buffer) instead of hipMemcpyAsync (ROCclr's blit: one 512-lane workgroup on every CU)
   bool d2h_kernel_ = false;
+  uint32_t d2h_blocks_ = 32;
   int cu_reserved_ = 0;  // CUs kept out of the parse / stats / output streams (APM_CU_RESERVE)
   void lane_d2h(void* h, const void* d, size_t n);  // APM_TXCOPY_FORCE_FALLBACK=1: every release takes the host path (tests)
   uint64_t sink_bytes_[N_OUT] = {0, 0, 0, 0, 0, 0, 0, 0};

@@ -179,9 +179,17 @@ def test_fleet_registry_merges_services_node_wide(world):
         assert len(set(map(key, o["fb"]))) == len(o["fb"])
     ref_fb = o1[0]["fb"]
     assert sorted(map(key, fb)) == sorted(map(key, ref_fb))
-    # values: fp64 sums in another order, printed to 1 dp (a last-bit tie could flip a digit)
+    # values: fp64 sums in another order, printed to 1 dp.  The std is sqrt(E[x^2] - mean^2): a
+    # std on a .x5 tie (two series 0.1 apart: common with 1-dp means) prints either way, so rows
+    # agree field by field to one printed digit
+    def vals(l):
+        f = l.split("|")
+        return [float(f[4])] + [float(v) for part in f[5:8] for v in part.split(":")]
+    ref_by_key = {key(l): vals(l) for l in ref_fb}
+    for l in fb:
+        np.testing.assert_allclose(vals(l), ref_by_key[key(l)], rtol=0, atol=0.1001, err_msg=l)
     same = len(set(fb) & set(ref_fb))
-    assert same >= len(ref_fb) - len(ref_fb) // 100, (same, len(ref_fb))
+    assert same >= len(ref_fb) * 9 // 10, (same, len(ref_fb))
     assert sum(e.eng.fleet_info()["fb_rows"] for e in engs) == len(fb)
 
 

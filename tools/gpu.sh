@@ -25,6 +25,7 @@
 #   service:T          the same with T tailer read threads
 #   benchx:A,B         bench.py 20/5 with extra arguments A B (commas become spaces)
 #   env:K=V            export K=V for the following tasks (A/B switches)
+#   unenv:K            unset K for the following tasks
 #   py:MODULE          python -m MODULE (diagnostics under tools/)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -76,6 +77,7 @@ for task in "$@"; do
     pmc:*) c=${task#pmc:}; run "pmc_$n" 120 rocprofv3 --kernel-trace --pmc ${c//,/ } --output-format csv -d "$O/pmc_$n" -o run -- \
              python3 bench.py --steps 10 --warmup 3 ;;
     env:*) export "${task#env:}"; echo "[env] ${task#env:}" ;;
+    unenv:*) unset "${task#unenv:}"; echo "[unenv] ${task#unenv:}" ;;
     py:*) run "py_$n" 600 python -u -m "${task#py:}" "$O" ;;
     *) echo "unknown task $task"; exit 2 ;;
   esac
