@@ -21,6 +21,7 @@
 
 #include <rocprim/rocprim.hpp>
 
+#include <chrono>
 #include <climits>
 #include <cstdlib>
 #include <cstddef>
@@ -1439,9 +1440,30 @@ template <class M>
 __device__ void walk_group(DJArgs& a, uint32_t slot, const M& mem, uint32_t g);
 
 // Slot lists (DJArgs::slot_head): the group's leader collects its members (pushed in any order)
-// and walks them in line order.  Up to GW_SMALL members are insertion-sorted in registers; a
-// larger group is queued for k_group_walk_big (its list is left in place).
+// and walks them in line order.  Up to GW_SMALL members are kept sorted in registers -- every
+// index is a compile-time one (insertion by min / max over the whole unrolled row, selection by
+// a compare chain), so nothing goes to scratch memory; a larger group is queued for
+// k_group_walk_big (its list is left in place).
 constexpr uint32_t GW_SMALL = 16;
+struct GwRow {
+  uint32_t m[GW_SMALL];
+  __device__ __forceinline__ void clear() {
+#pragma unroll
+    for (uint32_t k = 0; k < GW_SMALL; ++k) m[k] = ~0u;
+  }
+  // m ascending, +inf padded: m' = sorted(m + {j}) minus its largest (an +inf while not full)
+  __device__ __forceinline__ void insert(uint32_t j) {
+#pragma unroll
+    for (uint32_t k = GW_SMALL - 1; k >= 1; --k) m[k] = min(m[k], max(m[k - 1], j));
+    m[0] = min(m[0], j);
+  }
+  __device__ __forceinline__ uint32_t at(uint32_t q) const {
+    uint32_t v = m[0];
+#pragma unroll
+    for (uint32_t k = 1; k < GW_SMALL; ++k) v = q == k ? m[k] : v;
+    return v;
+  }
+};
 __global__ void k_group_walk(DJArgs a) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.n_ev) return;
@@ -1461,19 +1483,19 @@ __global__ void k_group_walk(DJArgs a) {
   if (slot > cap) return;
   if (slot == cap) { walk_direct(a, i); return; }
   if (a.op_idx[i] != ~0u) return;  // not the group's leader (its list was not empty)
-  uint32_t m[GW_SMALL];
+  GwRow m;
+  m.clear();
   uint32_t g = 0;
   for (uint32_t j = a.slot_head[slot]; j != ~0u; j = a.op_idx[j]) {
     if (g == GW_SMALL) {
       a.op_slot_sorted[atomicAdd(&a.big[0], 1u)] = slot;
       return;
     }
-    uint32_t p = g++;
-    for (; p > 0 && m[p - 1] > j; --p) m[p] = m[p - 1];
-    m[p] = j;
+    ++g;
+    m.insert(j);
   }
   a.slot_head[slot] = ~0u;
-  walk_group(a, slot, [&m](uint32_t q) { return m[q]; }, g);
+  walk_group(a, slot, [&m](uint32_t q) { return m.at(q); }, g);
 }
 
 // Ascending sort of v[0, g) by one workgroup (LDS or global memory): a bitonic network whose merge
@@ -2381,7 +2403,24 @@ extern "C" {
 using namespace apm;
 
 // APM_DJ_DEBUG=1: synchronize after every launch of the join and name the first that fails
+// APM_DJ_MARKS=1: the host clock after each launch of the join chain (apm_dj_marks; the engine
+// turns them into trace spans): where the ingest thread's launch time goes.  Diagnostics for
+// one engine per process (the marks are process-wide).
+static bool dj_marks_on() {
+  static const bool v = [] { const char* e = std::getenv("APM_DJ_MARKS"); return e && e[0] == '1'; }();
+  return v;
+}
+constexpr int DJ_MARKS = 64;
+static double g_mark_t[DJ_MARKS];
+static const char* g_mark_n[DJ_MARKS];
+static int g_mark_k = 0;
+
 static void dj_check(hipStream_t s, const char* what) {
+  if (dj_marks_on() && g_mark_k < DJ_MARKS) {
+    g_mark_t[g_mark_k] =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    g_mark_n[g_mark_k++] = what;
+  }
   static const bool dbg = std::getenv("APM_DJ_DEBUG") != nullptr;
   if (!dbg) return;
   const hipError_t e = hipStreamSynchronize(s);
@@ -2390,6 +2429,13 @@ static void dj_check(hipStream_t s, const char* what) {
     fflush(stderr);
     abort();
   }
+}
+
+int apm_dj_take_marks(double* t, const char** names, int cap) {
+  const int k = std::min(g_mark_k, cap);
+  for (int i = 0; i < k; ++i) { t[i] = g_mark_t[i]; names[i] = g_mark_n[i]; }
+  g_mark_k = 0;
+  return k;
 }
 
 size_t apm_dj_tmp_bytes(uint32_t max_ev, uint32_t max_out, int table_bits) {
@@ -2578,13 +2624,16 @@ int apm_dj_join(DJArgs* a, hipStream_t s) {
 int apm_dj_plan(DJFormatArgs* f, hipStream_t s) {
   const uint32_t n = f->n_out;
   hipLaunchKernelGGL(k_resolve_len, dim3((n + 1 + TB - 1) / TB), dim3(TB), 0, s, *f);
+  dj_check(s, "k_resolve_len");
   size_t need = 0;
   U4* lens = reinterpret_cast<U4*>(f->lens);
   U4* offs = reinterpret_cast<U4*>(f->offs);
   HIP_OK(rocprim::exclusive_scan(nullptr, need, lens, offs, U4{0, 0, 0, 0}, (size_t)n + 1, U4Plus(), s));
   if (need > f->tmp_bytes) return -1;
   HIP_OK(rocprim::exclusive_scan(f->tmp, need, lens, offs, U4{0, 0, 0, 0}, (size_t)n + 1, U4Plus(), s));
+  dj_check(s, "rocprim_exclusive_scan (plan)");
   hipLaunchKernelGGL(k_plan_totals, dim3(1), dim3(1), 0, s, *f);
+  dj_check(s, "k_plan_totals");
   return 0;
 }
 
@@ -2595,12 +2644,15 @@ int apm_dj_write(DJFormatArgs* f, hipStream_t s) {
   const uint32_t n = f->n_out;
   if (!n) return 0;
   hipLaunchKernelGGL(k_write, dim3((n + TXW_LINES - 1) / TXW_LINES), dim3(TXW_THREADS), 0, s, *f);
+  dj_check(s, "k_write");
   size_t need = 0;
   HIP_OK(rocprim::inclusive_scan(nullptr, need, f->tx_bucket, f->tx_bmax, (size_t)n, rocprim::maximum<int64_t>(), s));
   if (need > f->tmp_bytes) return -1;
   HIP_OK(rocprim::inclusive_scan(f->tmp, need, f->tx_bucket, f->tx_bmax, (size_t)n, rocprim::maximum<int64_t>(), s));
+  dj_check(s, "rocprim_inclusive_scan (bucket max)");
   hipLaunchKernelGGL(k_cands, dim3((n + TB - 1) / TB), dim3(TB), 0, s, *f);
   hipLaunchKernelGGL(k_reset_first, dim3((n + TB - 1) / TB), dim3(TB), 0, s, *f);
+  dj_check(s, "k_cands+k_reset_first");
   return 0;
 }
 

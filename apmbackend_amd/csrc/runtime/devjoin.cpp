@@ -1255,6 +1255,16 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
   aud_cur_ ^= 1;  // the next batch reads what this one carried
   idle_upkeep(now, n_ev);
   phase_t[8] = clock_ms();
+  {  // APM_DJ_MARKS=1: one span per launch (host time from the previous mark)
+    double t[64];
+    const char* nm[64];
+    const int m = apm_dj_take_marks(t, nm, 64);
+    double prev = phase_t[2];
+    for (int i = 0; i < m; ++i) {
+      spans.push_back({nm[i], {prev, t[i]}});
+      prev = t[i];
+    }
+  }
 }
 
 size_t DeviceJoin::trim(double now) {

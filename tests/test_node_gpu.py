@@ -350,6 +350,7 @@ def _all_outputs(out):
     return outs
 
 
+@pytest.mark.timeout(600)
 def test_elastic_degrade_keeps_state_across_the_world_change(tmp_path):
     """4 rank processes (host transport, one GPU); the rank on GPU 1 keeps dying
     after batch 110, so the supervisor retires GPU 1 and restarts the group with 2 ranks.  Each new
