@@ -1038,9 +1038,9 @@ int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& e
       d_ck_stage_ = nullptr;
       // not enough HBM for a snapshot: fall back to the synchronous writer
       ck_all_dirty_ = true;
+      if (job->pre_commit) job->pre_commit();  // (first: see checkpoint_writer)
       const uint64_t bytes = save_state(job->path, extra);
       job->base = true;
-      if (job->pre_commit) job->pre_commit();
       finish_chain(job, bytes);
       ck_last_stall_ms_ = now_ms() - t0;
       ++ck_sync_fallbacks_;
@@ -1112,6 +1112,11 @@ void Engine::checkpoint_writer() {
     uint64_t bytes = 0;
     std::string err;
     try {
+      // The sink snapshot first: its flushes' buffers (zero-copy engine text held by the writer
+      // lanes) are released once its bytes are written, not after the engine's state file and its
+      // fsync -- the engine's double-buffered output text never waits for a checkpoint write.
+      // (It only has to be in place before the manifest names this checkpoint: finish_chain.)
+      if (job->pre_commit) job->pre_commit();
       HIP_OK(hipEventSynchronize(ck_ev_));
       BinWriter w(job->path);
       w.raw(job->blob.data(), job->blob.size());
@@ -1138,7 +1143,6 @@ void Engine::checkpoint_writer() {
       w.commit();
       fsync_dir(job->path);
       bytes = w.bytes();
-      if (job->pre_commit) job->pre_commit();
       finish_chain(job, bytes);
     } catch (const std::exception& e) {
       err = e.what();

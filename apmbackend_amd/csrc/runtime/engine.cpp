@@ -438,6 +438,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     txcopy_force_fb_ = f && f[0] == '1';
     const char* d = std::getenv("APM_D2H_KERNEL");
     d2h_kernel_ = d && d[0] == '1';
+    const char* sd = std::getenv("APM_D2H_SDMA");
+    d2h_sdma_ = sd && sd[0] == '1';
     const char* b = std::getenv("APM_D2H_BLOCKS");
     d2h_blocks_ = b ? (uint32_t)std::max(1, std::atoi(b)) : 32u;
   }
@@ -2025,6 +2027,8 @@ void Engine::lane_d2h(void* h, const void* d, size_t n) {
     void* hv = nullptr;
     HIP_OK(hipHostGetDevicePointer(&hv, h, 0));
     apm_copy_capped(hv, d, n, d2h_blocks_, out_stream_);
+  } else if (d2h_sdma_) {  // a copy engine instead of ROCclr's blit kernel (A/B)
+    HIP_OK(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToDeviceNoCU, out_stream_));
   } else {
     HIP_OK(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, out_stream_));
   }

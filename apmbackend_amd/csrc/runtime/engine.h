@@ -886,8 +886,9 @@ class Engine {
     std::string prefix, name, path, extra;
     MemBlob blob;                 // the small sections, serialised at the snapshot
     std::vector<Lag> lags;
-    // run by the writer thread after the file is durable, before the manifest names it (the DB
-    // sink's pending-flush snapshot): a throw fails this checkpoint
+    // run by the writer thread before it writes the engine's file (the DB sink's pending-flush
+    // snapshot, whose held buffers it releases once written); the manifest names the checkpoint
+    // only after both: a throw fails this checkpoint
     std::function<void()> pre_commit;
   };
   static constexpr int kMaxChain = 16;
@@ -1111,6 +1112,9 @@ class Engine {
   // buffer) instead of hipMemcpyAsync (ROCclr's blit: one 512-lane workgroup on every CU)
   bool d2h_kernel_ = false;
   uint32_t d2h_blocks_ = 32;
+  // APM_D2H_SDMA=1: the same copies as hipMemcpyDeviceToDeviceNoCU into the pinned buffer (a DMA
+  // engine, no compute units)
+  bool d2h_sdma_ = false;
   int cu_reserved_ = 0;  // CUs kept out of the parse / stats / output streams (APM_CU_RESERVE)
   void lane_d2h(void* h, const void* d, size_t n);  // APM_TXCOPY_FORCE_FALLBACK=1: every release takes the host path (tests)
   uint64_t sink_bytes_[N_OUT] = {0, 0, 0, 0, 0, 0, 0, 0};

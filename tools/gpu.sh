@@ -11,6 +11,7 @@
 # Tasks:
 #   suite              pytest -m gpu (thread-method timeouts, stops at the first failure)
 #   suite:EXPR         pytest -m gpu -k EXPR
+#   suiteall:EXPR      the same without stopping at the first failure
 #   smoke              __graft_entry__.smoke()
 #   bench[:STEPS]      driver-shaped bench.py (warmup 5), default 20 steps
 #   bench200           200-step headline (steady state)
@@ -23,6 +24,7 @@
 #   timeline           rocprofv3 --kernel-trace --memory-copy-trace (tools/gpu_timeline.py reads it)
 #   pmc:C1,C2,...      one rocprofv3 --pmc pass of bench.py 10/3 (keep within one pass's counter budget)
 #   service:T          the same with T tailer read threads
+#   servicetrace       the service path with the engine's Chrome trace
 #   benchx:A,B         bench.py 20/5 with extra arguments A B (commas become spaces)
 #   env:K=V            export K=V for the following tasks (A/B switches)
 #   unenv:K            unset K for the following tasks
@@ -52,6 +54,7 @@ for task in "$@"; do
   n=$((n + 1))
   case $task in
     suite) run "suite" 1100 python -u -m pytest --maxfail 6 -v --timeout 240 --timeout-method thread tests -m gpu ;;
+    suiteall:*) run "suite_$n" 1000 python -u -m pytest --maxfail 10 -v --timeout 240 --timeout-method thread tests -m gpu -k "${task#suiteall:}" ;;
     suite:*) run "suite_$n" 900 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests -m gpu -k "${task#suite:}" ;;
     smoke) run "smoke" 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run "bench_$n" 300 python -u bench.py --steps 20 --warmup 5 ;;
@@ -65,6 +68,8 @@ for task in "$@"; do
         --rank-report "$O/ranks${w}_$n" ;;
     preset:*) run "preset_${task#preset:}_$n" 500 python -u bench.py --preset "${task#preset:}" --steps 20 --warmup 5 ;;
     service) run "service_$n" 600 python -u bench.py --path service --steps 200 --warmup 5 --service-dir /tmp/apm_svc ;;
+    servicetrace) run "servicetrace_$n" 600 python -u bench.py --path service --steps 200 --warmup 5 \
+                    --service-dir /tmp/apm_svc --trace "$O/servicetrace_$n.json" ;;
     service:*) run "service${task#service:}_$n" 600 python -u bench.py --path service --steps 200 --warmup 5 \
                  --service-dir /tmp/apm_svc --tail-read-threads "${task#service:}" ;;
     prof) run "prof_$n" 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$n" -o run -- \
