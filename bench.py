@@ -348,6 +348,7 @@ def main():
         ts = time.perf_counter()
         step(i)
         step_ms.append(1000.0 * (time.perf_counter() - ts))
+    t_steps = time.perf_counter()
     eng.eng.flush()  # the last batch's stats stage runs on the engine's stats thread
     if inserter is not None:  # alerts paged + every DB row of the timed batches written
         al = eng.eng.take_bytes("al")
@@ -425,6 +426,10 @@ def main():
             "step_ms_p50": round(maxed[5].item(), 3),
             "step_ms_p99": round(maxed[6].item(), 3),
             "step_ms_max": round(maxed[7].item(), 3),
+            # rank 0's steps (ingest side returns) and the drain after the last one (its stats,
+            # outputs, alert decision): ms_per_step = (sum(step_ms) + drain_ms) / steps
+            "step_ms": [round(x, 3) for x in step_ms],
+            "drain_ms": round(1000.0 * (t0 + dt - t_steps), 3),
             "t_lockstep_ms": round(maxed[8].item(), 4),
             "t_lockstep_max_ms": round(maxed[9].item(), 3),
             "p50_ingest_to_alert_ms": round(p50_max, 3),
