@@ -224,6 +224,8 @@ void apm_copy(void* dst, const void* src, size_t bytes, hipStream_t stream);
 // the same on at most `max_blocks` workgroups of 256 (a host-link copy that leaves the CUs to
 // the kernels running beside it)
 void apm_copy_capped(void* dst, const void* src, size_t bytes, uint32_t max_blocks, hipStream_t stream);
+// up to 8 doubles -> device memory, passed as kernel arguments (nothing read over the host link)
+void apm_set_f64(double* dst, const double* vals, int n, hipStream_t stream);
 // zscore.hip
 void apm_zscore(apm::ZArgs* a, int dtype_bytes, hipStream_t stream);
 void apm_zscore_warm(apm::ZArgs* a, int dtype_bytes, int fill, uint64_t seed, const apm::WinStat* base,

@@ -759,6 +759,15 @@ __global__ void k_ck_pack(const int32_t* __restrict__ cells, const int32_t* __re
   for (uint32_t j = 0; j < lens[t]; ++j) dst[j] = src[j];
 }
 
+// up to 8 doubles from the kernel arguments (no host-memory read on the device side: a small
+// H2D that waits behind nothing on the host link)
+struct F64x8 {
+  double v[8];
+};
+__global__ void k_set_f64(double* __restrict__ dst, F64x8 v, int n) {
+  if ((int)threadIdx.x < n) dst[threadIdx.x] = v.v[threadIdx.x];
+}
+
 extern "C" {
 
 using namespace apm;
@@ -779,6 +788,13 @@ void apm_copy_capped(void* dst, const void* src, size_t bytes, uint32_t max_bloc
   if ((a & 15) == 0) launch((uint4*)dst, (const uint4*)src, 16);
   else if ((a & 3) == 0) launch((uint32_t*)dst, (const uint32_t*)src, 4);
   else launch((uint8_t*)dst, (const uint8_t*)src, 1);
+}
+
+void apm_set_f64(double* dst, const double* vals, int n, hipStream_t stream) {
+  F64x8 v{};
+  n = std::min(std::max(n, 0), 8);
+  for (int i = 0; i < n; ++i) v.v[i] = vals[i];
+  hipLaunchKernelGGL(k_set_f64, dim3(1), dim3(64), 0, stream, dst, v, n);
 }
 
 void apm_export(const ExportArgs* a, hipStream_t stream) {

@@ -3402,7 +3402,9 @@ void Engine::lockstep_sync(int64_t batch_max) {
   h_sync_[1] = b == INT64_MIN ? -1.0 : (double)b;  // buckets < 2^53: exact in a double
   h_sync_[2] = (double)reg_pending_count();        // any rank with unregistered services?
   h_sync_[3] = -(double)reconfig_staged_gen();     // MAX of -gen: the node's oldest newest reload
-  h2d(d_sync_, h_sync_, 32, coll_stream_);
+  // the values travel as kernel arguments: a kernel reading them from pinned memory queues its
+  // PCIe read behind the output lane's D2H traffic (tens of us in the bench timeline)
+  apm_set_f64(d_sync_, h_sync_, 4, coll_stream_);
   coll_->all_reduce_f64(d_sync_, 4, /*max=*/true, coll_stream_);
   d2h(h_sync_, d_sync_, 32, coll_stream_);
   coll_wait(coll_stream_, nullptr, "lock-step clocks");
@@ -3589,7 +3591,9 @@ void Engine::node_round(uint64_t round, bool wait, bool all) {
   const size_t used = sizeof(NodeHdr) + (size_t)hdr->count * sizeof(NodeCand);
   h2d(d_node_send_, h_node_send_, used, coll_stream_);
   coll_->all_gather(d_node_send_, d_node_recv_, per, coll_stream_);
-  d2h(h_node_recv_, d_node_recv_, per * (size_t)fleet_nranks_, coll_stream_);
+  // one rank: its own block, of known size (the blocks of other ranks have host-unknown counts:
+  // the whole fixed-size block each)
+  d2h(h_node_recv_, d_node_recv_, fleet_nranks_ == 1 ? used : per * (size_t)fleet_nranks_, coll_stream_);
   HIP_OK(hipEventRecord(node_ev_, coll_stream_));
   node_round_pending_ = true;
   if (wait) {

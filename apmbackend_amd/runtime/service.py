@@ -221,7 +221,8 @@ class IngestService:
         self._held = None  # batch taken from the read-ahead ring and handed to the engine as prefetch
         self._stopping = False
         self.perf = {"wait_s": 0.0, "engine_s": 0.0, "outputs_s": 0.0, "batches": 0, "bytes": 0, "prefetched": 0,
-                     "ckpt_s": 0.0, "ckpt_flush_s": 0.0, "ckpt_sink_snapshot_s": 0.0}
+                     "ckpt_s": 0.0, "ckpt_flush_s": 0.0, "ckpt_sink_snapshot_s": 0.0,
+                     "hk_ticks_s": 0.0, "hk_watch_s": 0.0, "hk_ckpt_s": 0.0, "hk_stats_s": 0.0}
         self.batch_log = None  # a list to record every read-ahead batch (bytes, chunks) in (tests)
         self._drain_every_s = float(g.get("outputDrainMs", 250.0)) / 1000.0
         self._last_drain = 0.0
@@ -764,12 +765,15 @@ class IngestService:
 
     def _housekeeping(self):
         now = self.clock()
+        pf = self.perf
+        t0 = time.perf_counter()
         if self.jmx is not None:
             self.jmx.tick()
         if self.inserter is not None:
             self.inserter.tick()
         if self.notifier is not None:
             self.notifier.tick()
+        t1 = time.perf_counter()
         if self.watcher is not None:
             try:
                 self.watcher.check_once()
@@ -778,14 +782,20 @@ class IngestService:
         if self._gc_requested and self._held is None:  # (a held prefetch: the next poll does not prefetch)
             self._gc_requested = False
             self.request_gc()
+        t2 = time.perf_counter()
         if self._ckpt_due():
             self.checkpoint()
             if self._lockstep_ckpt():  # (advanced on every rank alike, written or skipped)
                 self._ckpt_epoch = int(self.native.batch_no()) // self._ckpt_every_batches()
+        t3 = time.perf_counter()
         interval = float(self.cfg.get("statLogIntervalInSeconds", 60))
         if now - self.last_stat >= interval:
             self.log_stats(now - self.last_stat)
             self.last_stat = now
+        t4 = time.perf_counter()
+        # where the drain loop's housekeeping goes (service_bench reports these)
+        for k, v in (("hk_ticks_s", t1 - t0), ("hk_watch_s", t2 - t1), ("hk_ckpt_s", t3 - t2), ("hk_stats_s", t4 - t3)):
+            pf[k] = pf.get(k, 0.0) + v
 
     def log_stats(self, dt_s: float):
         """Per statLogIntervalInSeconds: throughput, per-stage ms per batch, the ingest->alert
