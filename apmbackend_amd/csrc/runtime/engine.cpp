@@ -438,6 +438,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     txcopy_force_fb_ = f && f[0] == '1';
     const char* d = std::getenv("APM_D2H_KERNEL");
     d2h_kernel_ = d && d[0] == '1';
+    const char* sp = std::getenv("APM_D2H_SPLIT");
+    d2h_split_ = sp ? std::max(1, std::atoi(sp)) : 1;
     const char* sd = std::getenv("APM_D2H_SDMA");
     d2h_sdma_ = sd && sd[0] == '1';
     const char* b = std::getenv("APM_D2H_BLOCKS");
@@ -551,6 +553,7 @@ Engine::~Engine() {
     if (h_fb_total_) hipHostFree(h_fb_total_);
     if (fb_stream_) hipStreamDestroy(fb_stream_);
     if (node_ev_) hipEventDestroy(node_ev_);
+    if (solo_sync_ev_) hipEventDestroy(solo_sync_ev_);
     if (h_node_send_) hipHostFree(h_node_send_);
     if (h_node_recv_) hipHostFree(h_node_recv_);
     hipStreamDestroy(coll_stream_);
@@ -601,6 +604,7 @@ Engine::~Engine() {
   }
   hipStreamSynchronize(out_stream_);
   hipStreamDestroy(out_stream_);
+  if (out_stream2_) { hipStreamSynchronize(out_stream2_); hipStreamDestroy(out_stream2_); }
   hipHostFree(h_fmt_meta_);
   for (int k = 0; k < kStage; ++k) {
     if (h_stage_[k]) hipHostFree(h_stage_[k]);
@@ -2023,6 +2027,18 @@ void Engine::h2d(void* d, const void* h, size_t n, hipStream_t s) {
 
 void Engine::lane_d2h(void* h, const void* d, size_t n) {
   if (!n) return;
+  if (d2h_split_ > 1 && n >= ((size_t)4 << 20)) {
+    // APM_D2H_SPLIT=N: N pieces over two streams, so two copies run at once on the host link
+    if (!out_stream2_) HIP_OK(hipStreamCreateWithFlags(&out_stream2_, hipStreamNonBlocking));
+    const size_t piece = ((n + d2h_split_ - 1) / d2h_split_ + 4095) & ~(size_t)4095;
+    int i = 0;
+    for (size_t off = 0; off < n; off += piece, ++i) {
+      const size_t m = std::min(piece, n - off);
+      HIP_OK(hipMemcpyAsync((char*)h + off, (const char*)d + off, m, hipMemcpyDeviceToHost,
+                            (i & 1) ? out_stream2_ : out_stream_));
+    }
+    return;
+  }
   if (d2h_kernel_) {
     void* hv = nullptr;
     HIP_OK(hipHostGetDevicePointer(&hv, h, 0));
@@ -2032,6 +2048,11 @@ void Engine::lane_d2h(void* h, const void* d, size_t n) {
   } else {
     HIP_OK(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, out_stream_));
   }
+}
+
+void Engine::lane_sync() {
+  HIP_OK(hipStreamSynchronize(out_stream_));
+  if (out_stream2_) HIP_OK(hipStreamSynchronize(out_stream2_));
 }
 
 void Engine::d2h(void* h, const void* d, size_t n, hipStream_t s) {
@@ -2395,7 +2416,7 @@ void Engine::release_device_finish() {
       }
       const double tl0 = now_ms();
       lane_d2h(h_rel_text_[k], d_rel_text_[k], total);
-      HIP_OK(hipStreamSynchronize(out_stream_));
+      lane_sync();
       const double tl1 = now_ms();
       if (host_enc) {
         std::string enc[5];
@@ -2885,7 +2906,7 @@ void Engine::format_rollover_text(int64_t edge_ts) {
     const double tl0 = now_ms();
     if (st_total) lane_d2h(h, dst, st_total);
     if (fs_total) lane_d2h(h + st_total, dst + st_cap, fs_total);
-    HIP_OK(hipStreamSynchronize(out_stream_));
+    lane_sync();
     {
       std::lock_guard<std::mutex> g(out_mu_);
       formatted_bytes_lane_ += st_total + fs_total;
@@ -3322,7 +3343,10 @@ void Engine::fleet_setup(int32_t cap, bool lockstep) {
   lockstep_ = lockstep;
   if (lockstep_) {
     d_sync_ = (double*)dmalloc(64);
-    HIP_OK(hipHostMalloc((void**)&h_sync_, 64, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void**)&h_sync_, 128, hipHostMallocDefault));  // [0,4) values, [4,8) solo result, [8,12) sent
+    HIP_OK(hipEventCreateWithFlags(&solo_sync_ev_, hipEventDisableTiming));
+    const char* sw = std::getenv("APM_LOCKSTEP_SOLO_WAIT");
+    lockstep_solo_wait_ = sw && sw[0] == '1';
   }
   sync_latest_ = latest_;  // the stats thread is idle (flush above)
   fleet_cap_ = cap;
@@ -3396,24 +3420,46 @@ void Engine::lockstep_sync(int64_t batch_max) {
   if (coll_->aborted()) throw std::runtime_error("collective communicator was aborted");
   const int64_t b = std::max(sync_latest_, batch_max);
   // The collective runs at every world size, N = 1 included (MAX over one rank is the identity,
-  // but the single-GPU run then does the same per-batch work -- H2D, all-reduce, D2H, wait --
-  // as each rank of an 8-GPU node, and this path stays exercised by the 1-GPU tests).
+  // but the single-GPU run then does the same per-batch GPU work -- H2D, all-reduce, D2H -- as
+  // each rank of an 8-GPU node; at N = 1 only the host's wait is skipped, see below).
   h_sync_[0] = watermark_;
   h_sync_[1] = b == INT64_MIN ? -1.0 : (double)b;  // buckets < 2^53: exact in a double
   h_sync_[2] = (double)reg_pending_count();        // any rank with unregistered services?
   h_sync_[3] = -(double)reconfig_staged_gen();     // MAX of -gen: the node's oldest newest reload
   // the values travel as kernel arguments: a kernel reading them from pinned memory queues its
   // PCIe read behind the output lane's D2H traffic (tens of us in the bench timeline)
-  apm_set_f64(d_sync_, h_sync_, 4, coll_stream_);
-  coll_->all_reduce_f64(d_sync_, 4, /*max=*/true, coll_stream_);
-  d2h(h_sync_, d_sync_, 32, coll_stream_);
-  coll_wait(coll_stream_, nullptr, "lock-step clocks");
+  if (fleet_nranks_ == 1 && !lockstep_solo_wait_) {
+    // One rank: MAX over one rank is the identity, known before the exchange runs.  The exchange
+    // is still issued (the GPU does the per-batch work of every rank of a node) but the ingest
+    // thread does not wait for it; the next batch checks that it completed and returned the
+    // values sent (APM_LOCKSTEP_SOLO_WAIT=1: wait as a multi-rank node does).
+    if (solo_sync_pending_) {
+      coll_wait(nullptr, solo_sync_ev_, "lock-step clocks (one rank)");
+      if (std::memcmp(h_sync_ + 4, h_sync_ + 8, 32) != 0)
+        throw std::runtime_error("lock-step clocks: the one-rank exchange changed its values");
+    }
+    std::memcpy(h_sync_ + 8, h_sync_, 32);
+    apm_set_f64(d_sync_, h_sync_, 4, coll_stream_);
+    coll_->all_reduce_f64(d_sync_, 4, /*max=*/true, coll_stream_);
+    d2h(h_sync_ + 4, d_sync_, 32, coll_stream_);
+    HIP_OK(hipEventRecord(solo_sync_ev_, coll_stream_));
+    solo_sync_pending_ = true;
+  } else {
+    apm_set_f64(d_sync_, h_sync_, 4, coll_stream_);
+    coll_->all_reduce_f64(d_sync_, 4, /*max=*/true, coll_stream_);
+    d2h(h_sync_, d_sync_, 32, coll_stream_);
+    coll_wait(coll_stream_, nullptr, "lock-step clocks");
+  }
   watermark_ = h_sync_[0];
   if (h_sync_[1] >= 0) sync_latest_ = std::max(sync_latest_, (int64_t)h_sync_[1]);
   if (h_sync_[3] < 0) reconfig_agree((uint64_t)(-h_sync_[3]));  // every rank has it: same batch everywhere
   if (h_sync_[2] > 0) reg_round();  // every rank sees the same max: all enter the gather
-  // the coll stream is in order: the previous batch's alert gather has landed too
-  if (node_round_pending_) node_resolve();
+  // the coll stream is in order: once the exchange above completed, the previous batch's alert
+  // gather has landed too (one rank without the wait: its own event)
+  if (node_round_pending_) {
+    if (fleet_nranks_ == 1 && !lockstep_solo_wait_) coll_wait(nullptr, node_ev_, "node alerts");
+    node_resolve();
+  }
 }
 
 // Stats thread: every rank rolls over when any rank saw a newer bucket, exactly as the single

@@ -548,6 +548,11 @@ class Engine {
   int64_t sync_latest_ = INT64_MIN;  // ingest thread: node-wide newest bucket so far
   double* d_sync_ = nullptr;
   double* h_sync_ = nullptr;
+  // one rank: the clock exchange is issued but not waited for (its result is the identity);
+  // the next batch checks it (lockstep_sync)
+  hipEvent_t solo_sync_ev_ = nullptr;
+  bool solo_sync_pending_ = false;
+  bool lockstep_solo_wait_ = false;  // APM_LOCKSTEP_SOLO_WAIT=1
   int32_t fleet_cap_ = 0;
   size_t fleet_elems_ = 0;
   double* fleet_buf_[2] = {nullptr, nullptr};
@@ -1115,6 +1120,11 @@ class Engine {
   // APM_D2H_SDMA=1: the same copies as hipMemcpyDeviceToDeviceNoCU into the pinned buffer (a DMA
   // engine, no compute units)
   bool d2h_sdma_ = false;
+  // APM_D2H_SPLIT=N: lane copies of >= 4 MB in N pieces alternating over out_stream_ and a second
+  // output stream (two copies in flight on the host link)
+  int d2h_split_ = 1;
+  hipStream_t out_stream2_ = nullptr;
+  void lane_sync();  // both output streams
   int cu_reserved_ = 0;  // CUs kept out of the parse / stats / output streams (APM_CU_RESERVE)
   void lane_d2h(void* h, const void* d, size_t n);  // APM_TXCOPY_FORCE_FALLBACK=1: every release takes the host path (tests)
   uint64_t sink_bytes_[N_OUT] = {0, 0, 0, 0, 0, 0, 0, 0};

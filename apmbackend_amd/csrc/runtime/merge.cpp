@@ -546,9 +546,12 @@ MergeResult merge_checkpoints(const std::vector<std::string>& inputs, const std:
       if (ns < 0) continue;
       k.server = ns;
       if (k.need >= 0) {
+        // A link past the live range is stale (its region expired, or the slot was reused): the
+        // join checks the entry's key and TTL before it follows a link (k_group_walk), so a stale
+        // link is simply no link.  One inside the range keeps its entry (the key check still
+        // applies after the move).
         const uint64_t e = ((uint64_t)k.need - (lo & (cap - 1))) & (cap - 1);  // entry index in [lo, head)
-        if (e >= newv[j].size()) throw std::runtime_error("merge: key links a need entry outside the live arena");
-        k.need = (int32_t)(newv[j][e] & (arena_cap - 1));
+        k.need = e < newv[j].size() ? (int32_t)(newv[j][e] & (arena_cap - 1)) : -1;
       }
       k.pblk = shift_blk(k.pblk, blk_base[j]);
       keys.push_back(k);
