@@ -437,6 +437,7 @@ class DBInserter:
         self.buffers: Dict[str, Deque[Dict[str, Any]]] = {t: deque() for t in TYPES}
         self.deadline: Dict[str, Optional[float]] = {t: None for t in TYPES}
         self.failures = 0
+        self._stats_synced = 0.0  # monotonic time of the last interval-counter read (tick)
         self.native = bool(ic.get("nativeCopyEncoder", True))
         self.resume_path = ic.get("bufferResumeFileFullPath")
         self.core = None
@@ -612,7 +613,12 @@ class DBInserter:
     def tick(self) -> int:
         """Timer half of the reference's setTimeout per buffer."""
         if self.core is not None:
-            self._sync_stats()
+            # the interval counters are for the stat lines: read them at most every 50 ms (each
+            # read takes the sink's lock, contended by its writer lanes while a backlog drains)
+            t = time.monotonic()
+            if t - self._stats_synced >= 0.05:
+                self._stats_synced = t
+                self._sync_stats()
             return self.core.tick()
         now = self.clock()
         n = 0
