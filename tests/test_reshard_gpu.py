@@ -31,7 +31,7 @@ from apmbackend_amd.models.pipeline import APMEngine  # noqa: E402
 from apmbackend_amd.parallel.dist import shard_servers  # noqa: E402
 from apmbackend_amd.parallel.fleet import FleetBaseline  # noqa: E402
 
-KINDS = ("st", "fs", "al")
+KINDS = ("st", "fs", "al", "transactions")
 
 
 def run_phase(world, bl, servers, load=None, save=None, cfg=None):
@@ -108,14 +108,28 @@ def test_degrade_4_to_2_keeps_every_series_state(tmp_path):
     assert sum(i["series"] for i in infos) > 0
     # phase 2: 2 ranks from the merged states over the rest of the corpus
     e2, o2 = run_phase(2, bl[cut:], servers, load=new)
-    for k in KINDS:
+    # joined transactions: the same multiset (emission order across ranks is free)
+    tx_ref = sorted(l for o in ref for l in o["transactions"])
+    tx_got = sorted(l for o in o1 + o2 for l in o["transactions"])
+    if tx_got != tx_ref:
+        import collections as _c
+        cg, cr = _c.Counter(tx_got), _c.Counter(tx_ref)
+        print("tx only in the re-sharded run:", list((cg - cr).elements())[:5])
+        print("tx only in the reference run:", list((cr - cg).elements())[:5])
+    assert len(tx_got) == len(tx_ref) and tx_got == tx_ref
+    for k in ("st", "fs", "al"):
         want = _by_series(ref, k)
         got = _by_series(o1, k)
         for key, v in _by_series(o2, k).items():
             got[key] += v
         assert set(got) == set(want), k
         bad = [key for key in want if got[key] != want[key]]
-        assert not bad, (k, bad[:3], [(got[b][:2], want[b][:2]) for b in bad[:1]])
+        for b in bad[:3]:
+            g, w = got[b], want[b]
+            i = next((j for j in range(min(len(g), len(w))) if g[j] != w[j]), min(len(g), len(w)))
+            print(f"{k} {b}: {len(g)} vs {len(w)} lines, first difference at {i} (phase 1 has "
+                  f"{len(_by_series(o1, k)[b])}):\n  got  {g[max(0, i - 1):i + 2]}\n  want {w[max(0, i - 1):i + 2]}")
+        assert not bad, (k, len(bad), bad[:3])
     assert sum(len(o["al"]) for o in ref) > 0
     # the restored engines hold every series of their servers
     n_series = sum(e.eng.n_series() for e in e2)
