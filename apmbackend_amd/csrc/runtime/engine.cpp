@@ -438,6 +438,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     txcopy_force_fb_ = f && f[0] == '1';
     const char* d = std::getenv("APM_D2H_KERNEL");
     d2h_kernel_ = d && d[0] == '1';
+    const char* rl = std::getenv("APM_REL_LANE");
+    rel_lane_on_ = !(rl && rl[0] == '0');
     const char* sp = std::getenv("APM_D2H_SPLIT");
     d2h_split_ = sp ? std::max(1, std::atoi(sp)) : 1;
     const char* sd = std::getenv("APM_D2H_SDMA");
@@ -541,6 +543,10 @@ Engine::~Engine() {
   }
   out_cv_.notify_all();
   if (out_thread_.joinable()) out_thread_.join();
+  if (rel_lane_) {  // pending db releases read the buffers freed below
+    try { rel_lane_->wait_all(); } catch (...) {}
+    rel_lane_.reset();
+  }
   if (coll_) {
     hipStreamSynchronize(coll_stream_);
     coll_.reset();
@@ -605,6 +611,7 @@ Engine::~Engine() {
   hipStreamSynchronize(out_stream_);
   hipStreamDestroy(out_stream_);
   if (out_stream2_) { hipStreamSynchronize(out_stream2_); hipStreamDestroy(out_stream2_); }
+  if (rel_stream_) { hipStreamSynchronize(rel_stream_); hipStreamDestroy(rel_stream_); }
   hipHostFree(h_fmt_meta_);
   for (int k = 0; k < kStage; ++k) {
     if (h_stage_[k]) hipHostFree(h_stage_[k]);
@@ -1577,12 +1584,27 @@ uint64_t Engine::post_out(std::function<void()> fn) {
   return id;
 }
 
+uint64_t Engine::post_rel(std::function<void()> fn) {
+  if (!rel_lane_on_) return post_out(std::move(fn));
+  if (!rel_lane_) {
+    rel_lane_.reset(new TaskLane());
+    HIP_OK(hipStreamCreateWithFlags(&rel_stream_, hipStreamNonBlocking));
+  }
+  return rel_lane_->post(std::move(fn));
+}
+
+void Engine::rel_wait(uint64_t task) {
+  if (!rel_lane_on_) { out_wait(task); return; }
+  if (rel_lane_ && task) rel_lane_->wait(task);
+}
+
 void Engine::out_wait(uint64_t task) {
   std::unique_lock<std::mutex> lk(out_mu_);
   out_cv_.wait(lk, [&]() { return out_done_ >= task; });
 }
 
 void Engine::out_wait_idle() {
+  if (rel_lane_) rel_lane_->wait_all();
   std::unique_lock<std::mutex> lk(out_mu_);
   out_cv_.wait(lk, [&]() { return out_done_ >= out_posted_; });
 }
@@ -2025,8 +2047,12 @@ void Engine::h2d(void* d, const void* h, size_t n, hipStream_t s) {
   apm_copy(d, hv, n, s);
 }
 
-void Engine::lane_d2h(void* h, const void* d, size_t n) {
+void Engine::lane_d2h(void* h, const void* d, size_t n, hipStream_t s) {
   if (!n) return;
+  if (s && s != out_stream_) {  // the release lane's stream: one blit copy
+    HIP_OK(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, s));
+    return;
+  }
   if (d2h_split_ > 1 && n >= ((size_t)4 << 20)) {
     // APM_D2H_SPLIT=N: N pieces over two streams, so two copies run at once on the host link
     if (!out_stream2_) HIP_OK(hipStreamCreateWithFlags(&out_stream2_, hipStreamNonBlocking));
@@ -2163,11 +2189,11 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
       // gathers the lines while this thread continues with K8/K10/K11
       const int k = rel_k_;
       rel_k_ ^= 1;
-      out_wait(rel_task_[k]);  // the buffer's previous reader is done
+      rel_wait(rel_task_[k]);  // the buffer's previous reader is done
       HIP_OK(hipMemcpyAsync(h_release_gid_[k], d_pool_gid_[pool_cur_], (size_t)released * 8, hipMemcpyDeviceToHost,
                             stream_));
       HIP_OK(hipEventRecord(ev_rel_[k], stream_));
-      rel_task_[k] = post_out([this, k, released]() { release_gather(k, released); });
+      rel_task_[k] = post_rel([this, k, released]() { release_gather(k, released); });
     }
     metrics_.released += released;
     pool_off_ = released;
@@ -2385,7 +2411,7 @@ void Engine::release_device_finish() {
     const int k = rel_k_;
     rel_k_ ^= 1;
     const double tw = now_ms();
-    out_wait(rel_task_[k]);  // the buffer's previous reader is done
+    rel_wait(rel_task_[k]);  // the buffer's previous reader is done
     trace_event("rel.wait_lane", tw, now_ms(), 1);
     if (total + 64 > rel_text_cap_[k]) d_rel_text_[k] = (char*)regrow(d_rel_text_[k], rel_text_cap_[k], total + 64);
     if (copy)
@@ -2406,7 +2432,7 @@ void Engine::release_device_finish() {
       d2h(h_rel_offs_[k], d_rel_offs_, ((size_t)released + 1) * 4, stream_);
     }
     HIP_OK(hipEventRecord(ev_rel_[k], stream_));
-    rel_task_[k] = post_out([this, k, total, rows, released, host_enc]() {
+    rel_task_[k] = post_rel([this, k, total, rows, released, host_enc]() {
       HIP_OK(hipEventSynchronize(ev_rel_[k]));
       wait_fmt_holds(4 + k);  // the sink still writes from this buffer (zero-copy COPY rows)
       if (total > h_rel_text_cap_[k]) {
@@ -2415,8 +2441,13 @@ void Engine::release_device_finish() {
         HIP_OK(hipHostMalloc((void**)&h_rel_text_[k], h_rel_text_cap_[k], hipHostMallocDefault));
       }
       const double tl0 = now_ms();
-      lane_d2h(h_rel_text_[k], d_rel_text_[k], total);
-      lane_sync();
+      if (rel_lane_on_) {
+        lane_d2h(h_rel_text_[k], d_rel_text_[k], total, rel_stream_);
+        HIP_OK(hipStreamSynchronize(rel_stream_));
+      } else {
+        lane_d2h(h_rel_text_[k], d_rel_text_[k], total);
+        lane_sync();
+      }
       const double tl1 = now_ms();
       if (host_enc) {
         std::string enc[5];

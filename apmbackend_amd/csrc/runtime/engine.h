@@ -1048,6 +1048,14 @@ class Engine {
   int64_t* h_release_gid_[2] = {nullptr, nullptr};  // ping-pong D2H targets of released ids
   hipEvent_t ev_rel_[2] = {nullptr, nullptr};
   uint64_t rel_task_[2] = {0, 0};                    // output-lane task that reads each buffer
+  // Released db lines get a lane (thread) and a stream of their own (APM_REL_LANE=0: the st / fs
+  // output lane, as before): their D2H + emission overlap the st / fs D2H instead of queueing
+  // behind it in one FIFO -- the production path is output-lane bound (profiles/r5_e).
+  std::unique_ptr<TaskLane> rel_lane_;
+  hipStream_t rel_stream_ = nullptr;
+  bool rel_lane_on_ = true;
+  uint64_t post_rel(std::function<void()> fn);
+  void rel_wait(uint64_t task);
   int rel_k_ = 0;
   int64_t next_gid_ = 0;
   // Released-tx line store: each stats batch appends its pending tx lines to one block; the
@@ -1126,7 +1134,7 @@ class Engine {
   hipStream_t out_stream2_ = nullptr;
   void lane_sync();  // both output streams
   int cu_reserved_ = 0;  // CUs kept out of the parse / stats / output streams (APM_CU_RESERVE)
-  void lane_d2h(void* h, const void* d, size_t n);  // APM_TXCOPY_FORCE_FALLBACK=1: every release takes the host path (tests)
+  void lane_d2h(void* h, const void* d, size_t n, hipStream_t s = nullptr);  // (null: the output stream)  // APM_TXCOPY_FORCE_FALLBACK=1: every release takes the host path (tests)
   uint64_t sink_bytes_[N_OUT] = {0, 0, 0, 0, 0, 0, 0, 0};
   // K14 server rollup + exogenous context
   std::vector<double> h_ctx_;                    // [servers][CTX_FIELDS] (stats thread)

@@ -116,6 +116,10 @@ def test_degrade_4_to_2_keeps_every_series_state(tmp_path):
         cg, cr = _c.Counter(tx_got), _c.Counter(tx_ref)
         print("tx only in the re-sharded run:", list((cg - cr).elements())[:5])
         print("tx only in the reference run:", list((cr - cg).elements())[:5])
+        for line in list((cg - cr).elements())[:3]:
+            lid = line.split("|")[3]
+            for name, outs in (("phase 1", o1), ("phase 2", o2), ("reference", ref)):
+                print(f"  {lid} {name}:", [l for o in outs for l in o["transactions"] if l.split("|")[3] == lid])
     assert len(tx_got) == len(tx_ref) and tx_got == tx_ref
     for k in ("st", "fs", "al"):
         want = _by_series(ref, k)
