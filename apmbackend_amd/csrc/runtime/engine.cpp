@@ -2433,8 +2433,12 @@ void Engine::release_device_finish() {
     }
     HIP_OK(hipEventRecord(ev_rel_[k], stream_));
     rel_task_[k] = post_rel([this, k, total, rows, released, host_enc]() {
+      const double tw0 = now_ms();
       HIP_OK(hipEventSynchronize(ev_rel_[k]));
+      const double tw1 = now_ms();
       wait_fmt_holds(4 + k);  // the sink still writes from this buffer (zero-copy COPY rows)
+      trace_event("lane db wait gather", tw0, tw1, 4);
+      trace_event("lane db wait sink", tw1, now_ms(), 4);
       if (total > h_rel_text_cap_[k]) {
         if (h_rel_text_[k]) HIP_OK(hipHostFree(h_rel_text_[k]));
         h_rel_text_cap_[k] = total * 2 + (4 << 20);  // (a pinned allocation costs ms: 2x headroom)
@@ -2925,9 +2929,13 @@ void Engine::format_rollover_text(int64_t edge_ts) {
     return;
   }
   fmt_task_[k] = post_out([this, k, dst, st_cap]() {
+    const double tw0 = now_ms();
     HIP_OK(hipEventSynchronize(ev_fmt_[k]));
     const size_t st_total = h_fmt_meta_[4 * k], fs_total = h_fmt_meta_[4 * k + 1];
+    const double tw1 = now_ms();
     wait_fmt_holds(k);  // the sink still writes from this buffer (zero-copy COPY rows)
+    trace_event("lane st/fs wait format", tw0, tw1, 4);
+    trace_event("lane st/fs wait sink", tw1, now_ms(), 4);
     if (st_total + fs_total > h_fmt_cap_[k]) {
       if (h_fmt_out_[k]) HIP_OK(hipHostFree(h_fmt_out_[k]));
       h_fmt_cap_[k] = (st_total + fs_total) * 2 + (4 << 20);

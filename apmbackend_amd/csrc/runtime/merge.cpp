@@ -514,17 +514,20 @@ MergeResult merge_checkpoints(const std::vector<std::string>& inputs, const std:
         NeedEnt ne = x.ents.at(e);
         newv[o.j][e] = cur;
         ne.vidx = cur;
-        if (ne.key) {
-          const int32_t ns = ne.server >= 0 ? smap[o.j].at((size_t)ne.server) : -1;
-          if (ns < 0) {
-            ne.key = 0;  // a server this rank does not own: a dead slot (keeps the region contiguous)
-            ne.iblk = ne.lblk = 0;
-          } else {
-            ne.server = ns;
-            ne.iblk = shift_blk(ne.iblk, blk_base[o.j]);
-            ne.lblk = shift_blk(ne.lblk, blk_base[o.j]);
-            ++res.need;
-          }
+        // The expiry emits every entry of an expiring region that still holds records, whatever its
+        // key (k_exp_keys / k_exp_emit), under the entry's server: an entry of a server this rank
+        // does not own must hold nothing (else its records are emitted here too, under whatever
+        // server its old id now names), and an empty one nothing to free.
+        const int32_t ns = ne.key && ne.server >= 0 ? smap[o.j].at((size_t)ne.server) : -1;
+        if (ns < 0) {
+          ne.key = 0;  // not this rank's (or already gone): a dead slot (keeps the region contiguous)
+          ne.n = 0;
+          ne.iblk = ne.lblk = 0;
+        } else {
+          ne.server = ns;
+          ne.iblk = shift_blk(ne.iblk, blk_base[o.j]);
+          ne.lblk = shift_blk(ne.lblk, blk_base[o.j]);
+          ++res.need;
         }
         ents.push_back(ne);
         ++cur;

@@ -25,6 +25,7 @@
 #   pmc:C1,C2,...      one rocprofv3 --pmc pass of bench.py 10/3 (keep within one pass's counter budget)
 #   service:T          the same with T tailer read threads
 #   servicetrace       the service path with the engine's Chrome trace
+#   servicex:A,B       the service path with extra bench.py arguments A B
 #   benchx:A,B         bench.py 20/5 with extra arguments A B (commas become spaces)
 #   env:K=V            export K=V for the following tasks (A/B switches)
 #   unenv:K            unset K for the following tasks
@@ -68,6 +69,8 @@ for task in "$@"; do
         --rank-report "$O/ranks${w}_$n" ;;
     preset:*) run "preset_${task#preset:}_$n" 500 python -u bench.py --preset "${task#preset:}" --steps 20 --warmup 5 ;;
     service) run "service_$n" 600 python -u bench.py --path service --steps 200 --warmup 5 --service-dir /tmp/apm_svc ;;
+    servicex:*) a=${task#servicex:}; run "servicex_$n" 600 python -u bench.py --path service --steps 200 --warmup 5 \
+                  --service-dir /tmp/apm_svc ${a//,/ } ;;
     servicetrace) run "servicetrace_$n" 600 python -u bench.py --path service --steps 200 --warmup 5 \
                     --service-dir /tmp/apm_svc --trace "$O/servicetrace_$n.json" ;;
     service:*) run "service${task#service:}_$n" 600 python -u bench.py --path service --steps 200 --warmup 5 \
