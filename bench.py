@@ -350,6 +350,7 @@ def main():
         step_ms.append(1000.0 * (time.perf_counter() - ts))
     t_steps = time.perf_counter()
     eng.eng.flush()  # the last batch's stats stage runs on the engine's stats thread
+    t_flushed = time.perf_counter()
     if inserter is not None:  # alerts paged + every DB row of the timed batches written
         al = eng.eng.take_bytes("al")
         if al:
@@ -430,6 +431,7 @@ def main():
             # outputs, alert decision): ms_per_step = (sum(step_ms) + drain_ms) / steps
             "step_ms": [round(x, 3) for x in step_ms],
             "drain_ms": round(1000.0 * (t0 + dt - t_steps), 3),
+            "drain_flush_ms": round(1000.0 * (t_flushed - t_steps), 3),  # the engine's lanes (stats, outputs)
             "t_lockstep_ms": round(maxed[8].item(), 4),
             "t_lockstep_max_ms": round(maxed[9].item(), 3),
             "p50_ingest_to_alert_ms": round(p50_max, 3),
