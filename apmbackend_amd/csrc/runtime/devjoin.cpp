@@ -1049,12 +1049,21 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
   a.op_slot = d_op_slot_; a.op_slot_sorted = d_op_slot_sorted_; a.op_idx = d_op_idx_; a.op_idx_sorted = d_op_idx_sorted_;
   a.tmp = d_tmp_; a.tmp_bytes = tmp_bytes_;
   if (!group_sort_ && heads_cap_ != table_cap_) {  // (the join stream is ordered after any rebuild)
-    if (d_slot_head_) { HIP_OK(hipStreamSynchronize(st)); dfree(d_slot_head_, (size_t)heads_cap_ * 4); }
+    if (d_slot_head_) {
+      HIP_OK(hipStreamSynchronize(st));
+      dfree(d_slot_head_, (size_t)heads_cap_ * 4);
+      dfree(d_slot_cnt_, (size_t)heads_cap_ * 4);
+      dfree(d_slot_mem_, (size_t)heads_cap_ * GW_MEM * 4);
+    }
     d_slot_head_ = (uint32_t*)dmalloc((size_t)table_cap_ * 4);
     HIP_OK(hipMemsetAsync(d_slot_head_, 0xff, (size_t)table_cap_ * 4, st));
+    d_slot_cnt_ = (uint32_t*)dmalloc((size_t)table_cap_ * 4);  // (zeroed)
+    d_slot_mem_ = (uint32_t*)dmalloc((size_t)table_cap_ * GW_MEM * 4);
     heads_cap_ = table_cap_;
   }
-  a.slot_head = d_slot_head_; a.big = d_big_; a.group_sort = group_sort_ ? 1 : 0;
+  if (!group_sort_ && !d_op_link_) d_op_link_ = (uint32_t*)dmalloc(((size_t)cfg_.max_events + 1) * 4);
+  a.slot_head = d_slot_head_; a.slot_cnt = d_slot_cnt_; a.slot_mem = d_slot_mem_; a.op_link = d_op_link_;
+  a.big = d_big_; a.group_sort = group_sort_ ? 1 : 0;
   a.table = d_table_; a.table_mask = table_cap_ - 1; a.table_bits = table_bits_;
   a.pool = d_pool_; a.pool_ring = d_pool_ring_; a.pool_mask = pool_n_ - 1;
   a.reg = d_reg_; a.reg_mask = (1u << cfg_.reg_bits) - 1; a.miss = d_miss_; a.miss_cap = miss_cap_;
@@ -1289,7 +1298,9 @@ size_t DeviceJoin::trim(double now) {
   }
   if (d_slot_head_) {  // sized by the table: re-made by the next batch
     dfree(d_slot_head_, (size_t)heads_cap_ * 4);
-    d_slot_head_ = nullptr;
+    dfree(d_slot_cnt_, (size_t)heads_cap_ * 4);
+    dfree(d_slot_mem_, (size_t)heads_cap_ * GW_MEM * 4);
+    d_slot_head_ = d_slot_cnt_ = d_slot_mem_ = nullptr;
     heads_cap_ = 0;
   }
   if (d_rb_scratch_) {  // sized by the table: re-made by the next in-place rebuild

@@ -8,7 +8,8 @@
 //   3. join kernels (ops, audit trail K5, SOAP scan, grouping, expiry, group walk, placement)
 //                                                                                   -> sync A;
 //   4. new (server, raw service) names are interned on the host and the registry updated;
-//   5. resolve + line lengths + scans                                              -> sync B;
+//   5. resolve + line lengths + scans, the batch's ring region and write verdict (placed on the
+//      device: no host sync here);
 //   6. tx text into the HBM ring, stats hand-off arrays, rollover candidates       -> sync C.
 // The stats thread then consumes the slot's device arrays (TxRec / raw id / ring gid), exactly
 // where the host join handed it TxOut vectors before.
@@ -336,6 +337,9 @@ class DeviceJoin {
   // op grouping by slot lists (DJArgs::slot_head): one head per table slot, all empty between
   // batches (so a same-size rebuild keeps them valid); re-made when the table size changes
   uint32_t* d_slot_head_ = nullptr;
+  uint32_t* d_slot_cnt_ = nullptr;
+  uint32_t* d_slot_mem_ = nullptr;
+  uint32_t* d_op_link_ = nullptr;
   uint32_t heads_cap_ = 0;
   uint32_t* d_big_ = nullptr;
   bool group_sort_ = false;  // APM_OPSORT=sort

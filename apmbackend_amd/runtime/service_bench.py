@@ -130,11 +130,16 @@ def _run(args, cfg, N, rank, root, IngestService):
     ts0 = svc.tailer.stats()
     t0 = time.perf_counter()
     drain()
+    ta = time.perf_counter()
     svc.eng.eng.flush()
+    tb = time.perf_counter()
     svc._drain_outputs()
     t_engine = time.perf_counter() - t0
+    tc = time.perf_counter()
     svc.inserter.flush_all()  # every row of the timed batches encoded and written
     dt = time.perf_counter() - t0
+    tail = {"loop_s": round(ta - t0, 4), "engine_flush_s": round(tb - ta, 4), "drain_outputs_s": round(tc - tb, 4),
+            "sink_flush_all_s": round(t0 + dt - tc, 4)}
     m1 = svc.eng.metrics()
     s1 = svc.inserter.sink_stats()
     tstats = svc.tailer.stats()
@@ -163,6 +168,7 @@ def _run(args, cfg, N, rank, root, IngestService):
         "tailer": {**{k: tstats[k] for k in ("batches", "bytes_read", "read_threads")},
                    **{k + "_timed": tstats.get(k, 0) - ts0.get(k, 0) for k in ("batches", "bytes_read", "plan_ms", "read_ms")}},
         "drain_loop": {k: round(loop_t[k] - tl0[k], 4) for k in loop_t},
+        "timed_split": tail,  # the drain loop, then the engine's pipeline tail, outputs, the sink's last writes
         "ingest_GB_per_s": (m1["bytes"] - m0["bytes"]) / dt / 1e9,
         "loop": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in pf.items()},
         "mean_batch_MB": round(pf["bytes"] / max(pf["batches"], 1) / 1e6, 3),
