@@ -391,6 +391,7 @@ PYBIND11_MODULE(_apm_native, m) {
         d["busy"] = c.busy; d["done"] = c.done; d["skipped"] = c.skipped; d["sync_fallbacks"] = c.sync_fallbacks;
         d["chain_len"] = c.chain_len; d["last_base"] = c.last_base; d["last_stall_ms"] = c.last_stall_ms;
         d["last_write_ms"] = c.last_write_ms; d["last_bytes"] = c.last_bytes; d["stage_bytes"] = c.stage_bytes;
+        d["last_deferred_bytes"] = c.last_deferred_bytes;
         d["last_ring_rows"] = c.last_ring_rows;
         return d;
       })

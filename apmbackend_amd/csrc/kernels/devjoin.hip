@@ -1489,6 +1489,12 @@ __global__ void k_group_walk(DJArgs a) {
   if (slot > cap) return;
   if (slot == cap) { walk_direct(a, i); return; }
   if (a.op_idx[i] != 0) return;  // not the group's leader
+  // the count and the whole member row in one round of independent loads (the row's 64 bytes
+  // are one line; its unused tail is ignored)
+  const uint4* row = reinterpret_cast<const uint4*>(a.slot_mem + (size_t)slot * GW_MEM);
+  uint4 v[GW_MEM / 4];
+#pragma unroll
+  for (uint32_t q = 0; q < GW_MEM / 4; ++q) v[q] = row[q];
   const uint32_t g = a.slot_cnt[slot];
   if (g > GW_SMALL) {
     a.op_slot_sorted[atomicAdd(&a.big[0], 1u)] = slot;
@@ -1497,11 +1503,6 @@ __global__ void k_group_walk(DJArgs a) {
   a.slot_cnt[slot] = 0;
   GwRow m;
   m.clear();
-  const uint4* row = reinterpret_cast<const uint4*>(a.slot_mem + (size_t)slot * GW_MEM);
-  uint4 v[GW_MEM / 4];
-#pragma unroll
-  for (uint32_t q = 0; q < GW_MEM / 4; ++q)
-    if (4 * q < g) v[q] = row[q];
 #pragma unroll
   for (uint32_t q = 0; q < GW_MEM / 4; ++q) {
     if (4 * q + 0 < g) m.insert(v[q].x);

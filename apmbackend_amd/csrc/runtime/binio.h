@@ -84,6 +84,13 @@ class BinWriter {
       if (!tmp_.empty()) std::remove(tmp_.c_str());
     }
   }
+  bool memory() const { return mem_; }
+  // memory mode: n bytes left for a later fill (a deferred device copy, d2h.h); their offset
+  size_t hole(size_t n) {
+    char* at = buf_.grow(n);
+    bytes_ += n;
+    return (size_t)(at - buf_.data());
+  }
   void raw(const void* p, size_t n) {
     if (mem_) {
       if (n) std::memcpy(buf_.grow(n), p, n);

@@ -45,6 +45,8 @@ double now_ms() {
 void d2h_rows(BinWriter& w, const void* dev, size_t pitch, size_t width, size_t rows, void* bounce,
               hipStream_t st) {
   if (!width || !rows) return;
+  if (CkDefer* d = ck_defer())
+    if (d->take(w, dev, pitch, width, rows, st)) return;
   const size_t per = std::max<size_t>(1, kBounce / width);
   for (size_t r = 0; r < rows; r += per) {
     const size_t nr = std::min(per, rows - r);
@@ -71,13 +73,7 @@ template <class T>
 void d2h_vec(BinWriter& w, const T* dev, size_t n, hipStream_t st, void* bounce = nullptr) {
   if (bounce) {
     w.pod<uint64_t>(n);
-    const size_t per = kBounce / sizeof(T);
-    for (size_t i = 0; i < n; i += per) {
-      const size_t c = std::min(per, n - i);
-      HIP_OK(hipMemcpyAsync(bounce, dev + i, c * sizeof(T), hipMemcpyDeviceToHost, st));
-      HIP_OK(hipStreamSynchronize(st));
-      w.raw(bounce, c * sizeof(T));
-    }
+    write_dev(w, dev, n * sizeof(T), st, (char*)bounce, kBounce);  // (deferred while a snapshot is taken)
     return;
   }
   std::vector<T> h(n);
@@ -1009,8 +1005,46 @@ int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& e
   job->extra = extra;
   job->pre_commit = std::move(pre_commit);
   {
+    // the small sections' device reads become D2D copies into HBM staging (sized by the previous
+    // snapshot's want; a read that does not fit is done synchronously, as before)
+    CkDefer def;
+    if (ck_defer_want_ > ck_defer_cap_) {
+      if (d_ck_defer_) {
+        HIP_OK(hipFree(d_ck_defer_));
+        std::lock_guard<std::mutex> g(alloc_mu_);
+        device_bytes_ -= ck_defer_cap_;
+      }
+      const size_t cap = ck_defer_want_ + ck_defer_want_ / 4;
+      if (hipMalloc((void**)&d_ck_defer_, cap) != hipSuccess) {
+        (void)hipGetLastError();
+        d_ck_defer_ = nullptr;
+        ck_defer_cap_ = 0;
+      } else {
+        ck_defer_cap_ = cap;
+        std::lock_guard<std::mutex> g(alloc_mu_);
+        device_bytes_ += cap;
+      }
+    }
+    def.stage = d_ck_defer_;
+    def.cap = ck_defer_cap_;
     BinWriter mw{BinWriter::Memory{}, ck_blob_hint_};
-    write_small_sections(mw);
+    ck_defer() = &def;
+    try {
+      write_small_sections(mw);
+    } catch (...) {
+      ck_defer() = nullptr;
+      throw;
+    }
+    ck_defer() = nullptr;
+    ck_defer_want_ = def.want;
+    ck_deferred_bytes_ = def.used;
+    if (def.streams.size() > 4) throw std::runtime_error("checkpoint: deferred reads on more than 4 streams");
+    for (size_t i = 0; i < def.streams.size(); ++i) {
+      if (!ck_defer_ev_[i]) HIP_OK(hipEventCreateWithFlags(&ck_defer_ev_[i], hipEventDisableTiming));
+      HIP_OK(hipEventRecord(ck_defer_ev_[i], def.streams[i]));
+      job->defer_evs.push_back(ck_defer_ev_[i]);
+    }
+    for (const auto& h : def.holes) job->holes.push_back({h.blob_off, h.stage_off, h.len});
     job->blob = mw.take_memory();
     ck_blob_hint_ = job->blob.size() + job->blob.size() / 8 + (1u << 20);
   }
@@ -1118,6 +1152,9 @@ void Engine::checkpoint_writer() {
       // (It only has to be in place before the manifest names this checkpoint: finish_chain.)
       if (job->pre_commit) job->pre_commit();
       HIP_OK(hipEventSynchronize(ck_ev_));
+      for (hipEvent_t e : job->defer_evs) HIP_OK(hipEventSynchronize(e));
+      for (const auto& h : job->holes)  // the deferred small-section reads, into their blob holes
+        d2h_bounced(job->blob.p + h[0], d_ck_defer_ + h[1], h[2], ck_stream_, (char*)bounce, kBounce);
       BinWriter w(job->path);
       w.raw(job->blob.data(), job->blob.size());
       w.begin(SEC_RING);
@@ -1202,6 +1239,9 @@ void Engine::checkpoint_shutdown() {
   ck_cv_.notify_all();
   if (ck_thread_.joinable()) ck_thread_.join();
   if (d_ck_stage_) { hipFree(d_ck_stage_); d_ck_stage_ = nullptr; ck_stage_bytes_ = 0; }
+  if (d_ck_defer_) { hipFree(d_ck_defer_); d_ck_defer_ = nullptr; ck_defer_cap_ = 0; }
+  for (hipEvent_t& e : ck_defer_ev_)
+    if (e) { hipEventDestroy(e); e = nullptr; }
   if (h_ck_bounce_) { hipHostFree(h_ck_bounce_); h_ck_bounce_ = nullptr; }
   if (ck_ev_) { hipEventDestroy(ck_ev_); ck_ev_ = nullptr; }
   if (ck_stream_) { hipStreamDestroy(ck_stream_); ck_stream_ = nullptr; }
@@ -1221,6 +1261,7 @@ CheckpointInfo Engine::checkpoint_info() {
   c.last_bytes = ck_last_bytes_;
   c.stage_bytes = ck_stage_bytes_;
   c.last_ring_rows = ck_last_ring_rows_;
+  c.last_deferred_bytes = ck_deferred_bytes_;
   return c;
 }
 

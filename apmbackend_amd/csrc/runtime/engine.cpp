@@ -1813,6 +1813,13 @@ std::pair<size_t, size_t> Engine::trim_device_memory() {
     ck_text_cap_[k] = 0;
   }
   free_ck_stage();
+  if (d_ck_defer_) {  // the deferred small-section staging (the writer is idle: checkpoint_wait)
+    HIP_OK(hipFree(d_ck_defer_));
+    d_ck_defer_ = nullptr;
+    std::lock_guard<std::mutex> g(alloc_mu_);
+    device_bytes_ -= ck_defer_cap_;
+    ck_defer_cap_ = 0;
+  }
   HIP_OK(hipStreamSynchronize(stream_));
   return {before, device_bytes()};
 }

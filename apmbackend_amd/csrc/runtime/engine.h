@@ -13,6 +13,7 @@
 
 #include "binio.h"
 
+#include <array>
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
@@ -190,6 +191,7 @@ struct CheckpointInfo {
   double last_stall_ms = 0, last_write_ms = 0;
   uint64_t last_bytes = 0, stage_bytes = 0;
   int64_t last_ring_rows = 0;  // ring rows (over all LAGs) the last checkpoint carried
+  uint64_t last_deferred_bytes = 0;  // small-section bytes the last snapshot read D2D (not on the ingest thread)
 };
 
 struct EngineMetrics {
@@ -895,8 +897,17 @@ class Engine {
     // snapshot, whose held buffers it releases once written); the manifest names the checkpoint
     // only after both: a throw fails this checkpoint
     std::function<void()> pre_commit;
+    // deferred device reads of the small sections (d2h.h CkDefer): blob holes the writer fills
+    // from the staging once the events of the D2D copies completed
+    std::vector<std::array<size_t, 3>> holes;  // {blob offset, staging offset, bytes}
+    std::vector<hipEvent_t> defer_evs;
   };
   static constexpr int kMaxChain = 16;
+  // staging of the deferred small-section reads (one checkpoint in flight at a time)
+  char* d_ck_defer_ = nullptr;
+  size_t ck_defer_cap_ = 0, ck_defer_want_ = 0;
+  hipEvent_t ck_defer_ev_[4] = {nullptr, nullptr, nullptr, nullptr};
+  uint64_t ck_deferred_bytes_ = 0;  // of the last snapshot (checkpoint_info)
   void checkpoint_quiesce(const char* what);
   void write_small_sections(class BinWriter& w);
   void write_series_dump(class BinWriter& w);
