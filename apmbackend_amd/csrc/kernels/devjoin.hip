@@ -2447,6 +2447,21 @@ static void dj_check(hipStream_t s, const char* what) {
   }
 }
 
+// one 4-byte field (at byte `off`) of each of n records of `stride` bytes -> out[n] (8-byte: two
+// consecutive words, out[2i], out[2i+1])
+__global__ void k_gather_field(const uint8_t* __restrict__ base, size_t stride, uint32_t n, int words,
+                               uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(base + (size_t)i * stride);
+  for (int k = 0; k < words; ++k) out[(size_t)i * words + k] = p[k];
+}
+
+void apm_dj_gather_field(const void* base, size_t stride, uint32_t n, int words, uint32_t* out, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_gather_field, dim3((n + TB - 1) / TB), dim3(TB), 0, s, (const uint8_t*)base, stride, n, words, out);
+}
+
 int apm_dj_take_marks(double* t, const char** names, int cap) {
   const int k = std::min(g_mark_k, cap);
   for (int i = 0; i < k; ++i) { t[i] = g_mark_t[i]; names[i] = g_mark_n[i]; }

@@ -213,6 +213,9 @@ size_t apm_dj_tmp_bytes(uint32_t max_ev, uint32_t max_out, int table_bits);
 // APM_DJ_MARKS=1: host clock (ms, steady clock) after each launch of the join chain since the
 // last call, with the launch names; returns the count (at most cap)
 int apm_dj_take_marks(double* t, const char** names, int cap);
+// a 4-byte field (words = 1) or 8-byte field (words = 2) at `base` (offset included) of n records
+// of `stride` bytes, packed into out (checkpoint: the chain heads of the key table / arena)
+void apm_dj_gather_field(const void* base, size_t stride, uint32_t n, int words, uint32_t* out, hipStream_t s);
 // parse stream, right after apm_parse_batch: select the events the host resolves and copy
 // them to a compact buffer (count in *a->n_host).
 int apm_dj_select_host(apm::DJArgs* a, const uint32_t* d_n_ev, uint32_t max_ev, hipStream_t s);

@@ -1038,13 +1038,12 @@ int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& e
     ck_defer() = nullptr;
     ck_defer_want_ = def.want;
     ck_deferred_bytes_ = def.used;
-    if (def.streams.size() > 4) throw std::runtime_error("checkpoint: deferred reads on more than 4 streams");
-    for (size_t i = 0; i < def.streams.size(); ++i) {
-      if (!ck_defer_ev_[i]) HIP_OK(hipEventCreateWithFlags(&ck_defer_ev_[i], hipEventDisableTiming));
-      HIP_OK(hipEventRecord(ck_defer_ev_[i], def.streams[i]));
-      job->defer_evs.push_back(ck_defer_ev_[i]);
-    }
+    // the D2D copies complete before the engine resumes (~TB/s: under a millisecond for the
+    // snapshot's ~100 MB): a source array another stream writes next (the parse carry on the parse
+    // stream, the z-score state on the rollover lane's) cannot change under a queued copy
+    for (hipStream_t ds : def.streams) HIP_OK(hipStreamSynchronize(ds));
     for (const auto& h : def.holes) job->holes.push_back({h.blob_off, h.stage_off, h.len});
+    job->patches = std::move(def.patches);
     job->blob = mw.take_memory();
     ck_blob_hint_ = job->blob.size() + job->blob.size() / 8 + (1u << 20);
   }
@@ -1152,9 +1151,9 @@ void Engine::checkpoint_writer() {
       // (It only has to be in place before the manifest names this checkpoint: finish_chain.)
       if (job->pre_commit) job->pre_commit();
       HIP_OK(hipEventSynchronize(ck_ev_));
-      for (hipEvent_t e : job->defer_evs) HIP_OK(hipEventSynchronize(e));
       for (const auto& h : job->holes)  // the deferred small-section reads, into their blob holes
         d2h_bounced(job->blob.p + h[0], d_ck_defer_ + h[1], h[2], ck_stream_, (char*)bounce, kBounce);
+      for (const auto& pt : job->patches) std::memcpy(job->blob.p + pt.first, &pt.second, 4);
       BinWriter w(job->path);
       w.raw(job->blob.data(), job->blob.size());
       w.begin(SEC_RING);
@@ -1240,8 +1239,6 @@ void Engine::checkpoint_shutdown() {
   if (ck_thread_.joinable()) ck_thread_.join();
   if (d_ck_stage_) { hipFree(d_ck_stage_); d_ck_stage_ = nullptr; ck_stage_bytes_ = 0; }
   if (d_ck_defer_) { hipFree(d_ck_defer_); d_ck_defer_ = nullptr; ck_defer_cap_ = 0; }
-  for (hipEvent_t& e : ck_defer_ev_)
-    if (e) { hipEventDestroy(e); e = nullptr; }
   if (h_ck_bounce_) { hipHostFree(h_ck_bounce_); h_ck_bounce_ = nullptr; }
   if (ck_ev_) { hipEventDestroy(ck_ev_); ck_ev_ = nullptr; }
   if (ck_stream_) { hipStreamDestroy(ck_stream_); ck_stream_ = nullptr; }

@@ -33,9 +33,9 @@ inline void d2h_bounced(void* dst, const void* dev, size_t n, hipStream_t st, ch
 
 // Deferred device reads of an asynchronous checkpoint (Engine::checkpoint_async): while one is set
 // on the thread that serialises the snapshot, write_dev / write_dev_rows into an in-memory writer
-// copy the bytes D2D into HBM staging (stream-ordered, ~TB/s) and leave a hole in the blob; the
-// checkpoint writer thread fills the holes (D2H through its bounce) before it writes the file.
-// The ingest thread then pays for the D2D copies instead of the host-link reads (the join table,
+// copy the bytes D2D into HBM staging (~TB/s; the snapshot waits for those copies) and leave a hole
+// in the blob; the checkpoint writer thread fills the holes (D2H through its bounce) before it
+// writes the file.  The ingest thread no longer pays for the host-link reads (the join table,
 // window cells, pending-line text: ~36 ms per checkpoint at the production path, profiles/r5_e).
 struct CkDefer {
   struct Hole { size_t blob_off, stage_off, len; };
@@ -44,6 +44,9 @@ struct CkDefer {
   size_t want = 0;         // bytes the last snapshot would have deferred (sizes the next staging)
   std::vector<Hole> holes;
   std::vector<hipStream_t> streams;  // streams the D2D copies were queued on
+  // 4-byte values the writer stores into the blob after it filled the holes (fix-ups of bytes
+  // that may sit in a hole: the join's chain block numbers, DeviceJoin::save_tables)
+  std::vector<std::pair<size_t, int32_t>> patches;
   bool take(BinWriter& w, const void* dev, size_t pitch, size_t width, size_t rows, hipStream_t st) {
     const size_t n = width * rows;
     want += (n + 255) & ~(size_t)255;

@@ -1421,8 +1421,49 @@ void DeviceJoin::save_tables(BinWriter& w) {
   span("ck.j.arena");
   // chain blocks reachable from the live state, renumbered 1..n in the file.  Only those blocks
   // are read (gathered on the device one chain level at a time): the whole pool is ~256 MB.
-  auto get32 = [&](size_t off) { int32_t v; std::memcpy(&v, w.mem_at(off), 4); return v; };
-  auto put32 = [&](size_t off, int32_t v) { std::memcpy(w.mem_at(off), &v, 4); };
+  // The chain heads (key partials, entry items / logIds) are read from the device (the snapshot's
+  // table and arena bytes may still be on their way: CkDefer holes) and the renumbered heads are
+  // written into the blob -- or, while the snapshot defers its reads, recorded as patches the
+  // checkpoint writer applies after it filled the holes.
+  CkDefer* const defer = ck_defer();
+  auto put32 = [&](size_t off, int32_t v) {
+    if (defer) defer->patches.push_back({off, v});
+    else std::memcpy(w.mem_at(off), &v, 4);
+  };
+  // the fields gathered on the device into one packed buffer, then one D2H:
+  // [pblk x n_live][key (2 words) x n_ents][iblk x n_ents][lblk x n_ents]
+  std::vector<int32_t> pblk(n_live), iblk(n_ents), lblk(n_ents);
+  std::vector<uint64_t> ekey(n_ents);
+  {
+    const size_t words = (size_t)n_live + 4 * n_ents;
+    uint32_t* d_f = nullptr;
+    if (words) HIP_OK(hipMalloc((void**)&d_f, words * 4));
+    apm_dj_gather_field((const char*)d_table_spare_ + offsetof(KeyState, pblk), sizeof(KeyState), n_live, 1, d_f, st);
+    uint32_t* fk = d_f + n_live;
+    uint32_t* fi = fk + 2 * n_ents;
+    uint32_t* fl = fi + n_ents;
+    if (n_ents) {
+      const uint64_t cap = cfg_.arena_cap, first = lo & (cap - 1);
+      const uint64_t n1 = std::min<uint64_t>(n_ents, cap - first);
+      for (int part = 0; part < 2; ++part) {
+        const size_t at = part ? (size_t)n1 : 0, cnt = part ? (size_t)(n_ents - n1) : (size_t)n1;
+        const char* src = (const char*)(d_arena_ + (part ? 0 : first));
+        apm_dj_gather_field(src + offsetof(NeedEnt, key), sizeof(NeedEnt), (uint32_t)cnt, 2, fk + 2 * at, st);
+        apm_dj_gather_field(src + offsetof(NeedEnt, iblk), sizeof(NeedEnt), (uint32_t)cnt, 1, fi + at, st);
+        apm_dj_gather_field(src + offsetof(NeedEnt, lblk), sizeof(NeedEnt), (uint32_t)cnt, 1, fl + at, st);
+      }
+    }
+    if (words) {
+      std::vector<uint32_t> h(words);
+      HIP_OK(hipMemcpyAsync(h.data(), d_f, words * 4, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      HIP_OK(hipFree(d_f));
+      std::memcpy(pblk.data(), h.data(), (size_t)n_live * 4);
+      std::memcpy(ekey.data(), h.data() + n_live, n_ents * 8);
+      std::memcpy(iblk.data(), h.data() + n_live + 2 * n_ents, n_ents * 4);
+      std::memcpy(lblk.data(), h.data() + n_live + 3 * n_ents, n_ents * 4);
+    }
+  }
   struct Blk { uint8_t b[CHAIN_BLK]; };
   std::vector<Blk> blocks;
   {
@@ -1430,16 +1471,14 @@ void DeviceJoin::save_tables(BinWriter& w) {
     std::vector<size_t> slot_of;   // level 0: where (writer offset) each head's new number goes
     for (uint32_t i = 0; i < n_live; ++i) {
       const size_t o = live_off + (size_t)i * sizeof(KeyState) + offsetof(KeyState, pblk);
-      if (const int32_t b = get32(o)) { cur.push_back(b); slot_of.push_back(o); }
+      if (const int32_t b = pblk[i]) { cur.push_back(b); slot_of.push_back(o); }
     }
     for (size_t i = 0; i < n_ents; ++i) {
       const size_t e = ents_off + i * sizeof(NeedEnt);
-      uint64_t key;
-      std::memcpy(&key, w.mem_at(e + offsetof(NeedEnt, key)), 8);
       const size_t oi = e + offsetof(NeedEnt, iblk), ol = e + offsetof(NeedEnt, lblk);
-      if (!key) { put32(oi, 0); put32(ol, 0); continue; }
-      if (const int32_t b = get32(oi)) { cur.push_back(b); slot_of.push_back(oi); }
-      if (const int32_t b = get32(ol)) { cur.push_back(b); slot_of.push_back(ol); }
+      if (!ekey[i]) { put32(oi, 0); put32(ol, 0); continue; }
+      if (const int32_t b = iblk[i]) { cur.push_back(b); slot_of.push_back(oi); }
+      if (const int32_t b = lblk[i]) { cur.push_back(b); slot_of.push_back(ol); }
     }
     std::vector<int32_t> parent(cur.size(), -1);  // index in `blocks` of the predecessor (-1: a head)
     int32_t* d_idx = nullptr;
@@ -1492,7 +1531,10 @@ void DeviceJoin::save(BinWriter& w) {
     save_tables(w);
   } else {
     BinWriter mw{BinWriter::Memory{}};
+    CkDefer* const d = ck_defer();
+    ck_defer() = nullptr;  // (a temporary writer: its holes would never be filled)
     save_tables(mw);
+    ck_defer() = d;
     const MemBlob b = mw.take_memory();
     w.raw(b.data(), b.size());
   }

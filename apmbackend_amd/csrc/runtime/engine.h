@@ -898,15 +898,14 @@ class Engine {
     // only after both: a throw fails this checkpoint
     std::function<void()> pre_commit;
     // deferred device reads of the small sections (d2h.h CkDefer): blob holes the writer fills
-    // from the staging once the events of the D2D copies completed
+    // from the staging (the D2D copies into it completed within the snapshot)
     std::vector<std::array<size_t, 3>> holes;  // {blob offset, staging offset, bytes}
-    std::vector<hipEvent_t> defer_evs;
+    std::vector<std::pair<size_t, int32_t>> patches;  // stored after the holes are filled
   };
   static constexpr int kMaxChain = 16;
   // staging of the deferred small-section reads (one checkpoint in flight at a time)
   char* d_ck_defer_ = nullptr;
   size_t ck_defer_cap_ = 0, ck_defer_want_ = 0;
-  hipEvent_t ck_defer_ev_[4] = {nullptr, nullptr, nullptr, nullptr};
   uint64_t ck_deferred_bytes_ = 0;  // of the last snapshot (checkpoint_info)
   void checkpoint_quiesce(const char* what);
   void write_small_sections(class BinWriter& w);

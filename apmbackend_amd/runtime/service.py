@@ -222,7 +222,8 @@ class IngestService:
         self._stopping = False
         self.perf = {"wait_s": 0.0, "engine_s": 0.0, "outputs_s": 0.0, "batches": 0, "bytes": 0, "prefetched": 0,
                      "ckpt_s": 0.0, "ckpt_flush_s": 0.0, "ckpt_sink_snapshot_s": 0.0,
-                     "hk_ticks_s": 0.0, "hk_watch_s": 0.0, "hk_ckpt_s": 0.0, "hk_stats_s": 0.0}
+                     "hk_ticks_s": 0.0, "hk_watch_s": 0.0, "hk_ckpt_s": 0.0, "hk_stats_s": 0.0,
+                     "hk_jmx_s": 0.0, "hk_sink_s": 0.0}
         self.batch_log = None  # a list to record every read-ahead batch (bytes, chunks) in (tests)
         self._drain_every_s = float(g.get("outputDrainMs", 250.0)) / 1000.0
         self._last_drain = 0.0
@@ -769,11 +770,15 @@ class IngestService:
         t0 = time.perf_counter()
         if self.jmx is not None:
             self.jmx.tick()
+        ta = time.perf_counter()
         if self.inserter is not None:
             self.inserter.tick()
+        tb = time.perf_counter()
         if self.notifier is not None:
             self.notifier.tick()
         t1 = time.perf_counter()
+        pf["hk_jmx_s"] = pf.get("hk_jmx_s", 0.0) + ta - t0
+        pf["hk_sink_s"] = pf.get("hk_sink_s", 0.0) + tb - ta
         if self.watcher is not None:
             try:
                 self.watcher.check_once()
