@@ -1125,15 +1125,9 @@ __global__ void k_claim(DJArgs a) {
   a.op_slot[i] = key;
   if (a.group_sort) {
     a.op_idx[i] = i;
-  } else {  // a rank in the key's group (rank 0 leads it)
+  } else {  // push onto the key's list (the op that finds it empty leads the group)
     if (i == 0) { a.big[0] = 0; a.big[1] = 0; }
-    uint32_t r = ~0u;
-    if (key < cap) {
-      r = atomicAdd(&a.slot_cnt[key], 1u);
-      if (r < GW_MEM) a.slot_mem[(size_t)key * GW_MEM + r] = i;
-      else a.op_link[i] = atomicExch(&a.slot_head[key], i);
-    }
-    a.op_idx[i] = r;
+    a.op_idx[i] = key < cap ? atomicExch(&a.slot_head[key], i) : ~0u;
   }
   if (op.op != JOP_NONE && (op.flags & JF_HAS_SVC)) {
     const uint64_t k = regkey_of(op.svc, op.server);
@@ -1445,12 +1439,12 @@ __device__ __forceinline__ void walk_direct(const DJArgs& a, uint32_t ev) {  // 
 template <class M>
 __device__ void walk_group(DJArgs& a, uint32_t slot, const M& mem, uint32_t g);
 
-// Counted slots (DJArgs::slot_cnt / slot_mem): the group's leader reads its members (in rank
-// order, which is no line order) and walks them in line order.  Up to GW_SMALL members are kept
-// sorted in registers -- every index is a compile-time one (insertion by min / max over the whole
-// unrolled row, selection by a compare chain), so nothing goes to scratch memory; a larger group
-// is queued for k_group_walk_big (its count, row and overflow list are left in place).
-constexpr uint32_t GW_SMALL = GW_MEM;
+// Slot lists (DJArgs::slot_head): the group's leader collects its members (pushed in any order)
+// and walks them in line order.  Up to GW_SMALL members are kept sorted in registers -- every
+// index is a compile-time one (insertion by min / max over the whole unrolled row, selection by
+// a compare chain), so nothing goes to scratch memory; a larger group is queued for
+// k_group_walk_big (its list is left in place).
+constexpr uint32_t GW_SMALL = 16;
 struct GwRow {
   uint32_t m[GW_SMALL];
   __device__ __forceinline__ void clear() {
@@ -1488,28 +1482,19 @@ __global__ void k_group_walk(DJArgs a) {
   const uint32_t slot = a.op_slot[i];
   if (slot > cap) return;
   if (slot == cap) { walk_direct(a, i); return; }
-  if (a.op_idx[i] != 0) return;  // not the group's leader
-  // the count and the whole member row in one round of independent loads (the row's 64 bytes
-  // are one line; its unused tail is ignored)
-  const uint4* row = reinterpret_cast<const uint4*>(a.slot_mem + (size_t)slot * GW_MEM);
-  uint4 v[GW_MEM / 4];
-#pragma unroll
-  for (uint32_t q = 0; q < GW_MEM / 4; ++q) v[q] = row[q];
-  const uint32_t g = a.slot_cnt[slot];
-  if (g > GW_SMALL) {
-    a.op_slot_sorted[atomicAdd(&a.big[0], 1u)] = slot;
-    return;
-  }
-  a.slot_cnt[slot] = 0;
+  if (a.op_idx[i] != ~0u) return;  // not the group's leader (its list was not empty)
   GwRow m;
   m.clear();
-#pragma unroll
-  for (uint32_t q = 0; q < GW_MEM / 4; ++q) {
-    if (4 * q + 0 < g) m.insert(v[q].x);
-    if (4 * q + 1 < g) m.insert(v[q].y);
-    if (4 * q + 2 < g) m.insert(v[q].z);
-    if (4 * q + 3 < g) m.insert(v[q].w);
+  uint32_t g = 0;
+  for (uint32_t j = a.slot_head[slot]; j != ~0u; j = a.op_idx[j]) {
+    if (g == GW_SMALL) {
+      a.op_slot_sorted[atomicAdd(&a.big[0], 1u)] = slot;
+      return;
+    }
+    ++g;
+    m.insert(j);
   }
+  a.slot_head[slot] = ~0u;
   walk_group(a, slot, [&m](uint32_t q) { return m.at(q); }, g);
 }
 
@@ -1551,14 +1536,13 @@ __global__ __launch_bounds__(GWB_THREADS) void k_group_walk_big(DJArgs a) {
   for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
     const uint32_t slot = a.op_slot_sorted[b];
     if (threadIdx.x == 0) {
-      const uint32_t g = a.slot_cnt[slot];  // the row's GW_MEM members, then the overflow list
+      uint32_t g = 0;
+      for (uint32_t j = a.slot_head[slot]; j != ~0u; j = a.op_idx[j]) ++g;
       const uint32_t off = atomicAdd(&a.big[1], g);  // (members of all groups <= n_ev)
       uint32_t k = 0;
-      for (; k < GW_MEM; ++k) a.op_idx_sorted[off + k] = a.slot_mem[(size_t)slot * GW_MEM + k];
-      for (uint32_t j = a.slot_head[slot]; j != ~0u && k < g; j = a.op_link[j]) a.op_idx_sorted[off + k++] = j;
+      for (uint32_t j = a.slot_head[slot]; j != ~0u; j = a.op_idx[j]) a.op_idx_sorted[off + k++] = j;
       a.slot_head[slot] = ~0u;
-      a.slot_cnt[slot] = 0;
-      s_g = k;
+      s_g = g;
       s_off = off;
     }
     __syncthreads();

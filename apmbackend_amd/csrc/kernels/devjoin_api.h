@@ -11,7 +11,6 @@ namespace apm {
 
 constexpr int SOAP_SEGS = 16;            // scan segments per SOAP chunk
 constexpr uint32_t DJ_OVF_CAP = 1u << 16; // outputs beyond the first two of one op
-constexpr uint32_t GW_MEM = 16;           // member row of a key's group (DJArgs::slot_mem)
 
 // The plan's write verdict (JoinCounts::pad[1]): the write pass runs only on DJ_WRITE_OK.
 enum : uint32_t {
@@ -107,22 +106,17 @@ struct DJArgs {
   uint32_t* seg_in;               // incoming state per segment
   uint64_t* chain_hash;           // per chunk: carried context hash of its file
   SoapState* soap_state;          // [max files] carried per file
-  // ---- grouping.  Default (counted slots): k_claim takes a rank r in its key's group by one
-  // atomic add on slot_cnt[slot] and stores its op index in the key's member row
-  // slot_mem[slot][r] (r < GW_MEM; later members go onto an overflow list, slot_head / op_link);
-  // the rank-0 op leads the group -- it reads the count and the row (independent loads), orders
-  // the members in registers and walks them (k_group_walk; groups of more than GW_MEM ops go to
-  // k_group_walk_big, one workgroup each), and zeroes the count again.
+  // ---- grouping.  Default (slot lists): k_claim pushes each op onto its key's list
+  // (slot_head[slot] <- op, op_idx[op] = the previous head); the op that found the list empty
+  // leads the group -- it collects and orders the members (k_group_walk; groups of more than
+  // GW_SMALL ops go to k_group_walk_big, one workgroup each) and empties the list again.
   // APM_OPSORT=sort: the stable radix sort of (slot, op) pairs (the round-4 form, for A/B).
   uint32_t* op_slot;              // [n_ev] table slot / DIRECT / NONE
-  uint32_t* op_slot_sorted;       // sort: sorted slots; slots: the big groups' leaders
-  uint32_t* op_idx;               // sort: op indices; slots: the op's rank in its group
-  uint32_t* op_idx_sorted;        // sort: sorted op indices; slots: the big groups' members
-  uint32_t* slot_cnt;             // slots: [table cap] group sizes, 0 between batches
-  uint32_t* slot_mem;             // slots: [table cap][GW_MEM] the first members (op indices)
-  uint32_t* slot_head;            // slots: [table cap] overflow lists, ~0u between batches
-  uint32_t* op_link;              // slots: [n_ev] next member of an overflow list
-  uint32_t* big;                  // slots: [2] big groups, their members (zeroed by k_claim)
+  uint32_t* op_slot_sorted;       // sort: sorted slots; lists: the big groups' leaders
+  uint32_t* op_idx;               // sort: op indices; lists: the next (earlier-pushed) member
+  uint32_t* op_idx_sorted;        // sort: sorted op indices; lists: the big groups' members
+  uint32_t* slot_head;            // lists: [table cap] list heads, ~0u between batches
+  uint32_t* big;                  // lists: [2] big groups, their members (zeroed by k_claim)
   int group_sort;                 // 1: the radix-sort grouping
   void* tmp;                      // rocprim scratch
   size_t tmp_bytes;

@@ -228,6 +228,8 @@ DeviceJoin::~DeviceJoin() {
   }
   hipHostFree(h_miss_); hipHostFree(h_exp_); hipHostFree(h_rawtab_); hipHostFree(h_reg_fill_);
   hipHostFree(h_cand_); hipHostFree(h_cand_bucket_); hipHostFree(h_unres_); hipHostFree(h_counts_); hipHostFree(h_live_);
+  if (h_cstats_) hipHostFree(h_cstats_);
+  if (cstats_ev_) hipEventDestroy(cstats_ev_);
   if (h_hops_) hipHostFree(h_hops_);
   if (h_hbuf_) hipHostFree(h_hbuf_);
   if (h_txt_) hipHostFree(h_txt_);
@@ -1049,21 +1051,12 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
   a.op_slot = d_op_slot_; a.op_slot_sorted = d_op_slot_sorted_; a.op_idx = d_op_idx_; a.op_idx_sorted = d_op_idx_sorted_;
   a.tmp = d_tmp_; a.tmp_bytes = tmp_bytes_;
   if (!group_sort_ && heads_cap_ != table_cap_) {  // (the join stream is ordered after any rebuild)
-    if (d_slot_head_) {
-      HIP_OK(hipStreamSynchronize(st));
-      dfree(d_slot_head_, (size_t)heads_cap_ * 4);
-      dfree(d_slot_cnt_, (size_t)heads_cap_ * 4);
-      dfree(d_slot_mem_, (size_t)heads_cap_ * GW_MEM * 4);
-    }
+    if (d_slot_head_) { HIP_OK(hipStreamSynchronize(st)); dfree(d_slot_head_, (size_t)heads_cap_ * 4); }
     d_slot_head_ = (uint32_t*)dmalloc((size_t)table_cap_ * 4);
     HIP_OK(hipMemsetAsync(d_slot_head_, 0xff, (size_t)table_cap_ * 4, st));
-    d_slot_cnt_ = (uint32_t*)dmalloc((size_t)table_cap_ * 4);  // (zeroed)
-    d_slot_mem_ = (uint32_t*)dmalloc((size_t)table_cap_ * GW_MEM * 4);
     heads_cap_ = table_cap_;
   }
-  if (!group_sort_ && !d_op_link_) d_op_link_ = (uint32_t*)dmalloc(((size_t)cfg_.max_events + 1) * 4);
-  a.slot_head = d_slot_head_; a.slot_cnt = d_slot_cnt_; a.slot_mem = d_slot_mem_; a.op_link = d_op_link_;
-  a.big = d_big_; a.group_sort = group_sort_ ? 1 : 0;
+  a.slot_head = d_slot_head_; a.big = d_big_; a.group_sort = group_sort_ ? 1 : 0;
   a.table = d_table_; a.table_mask = table_cap_ - 1; a.table_bits = table_bits_;
   a.pool = d_pool_; a.pool_ring = d_pool_ring_; a.pool_mask = pool_n_ - 1;
   a.reg = d_reg_; a.reg_mask = (1u << cfg_.reg_bits) - 1; a.miss = d_miss_; a.miss_cap = miss_cap_;
@@ -1298,9 +1291,7 @@ size_t DeviceJoin::trim(double now) {
   }
   if (d_slot_head_) {  // sized by the table: re-made by the next batch
     dfree(d_slot_head_, (size_t)heads_cap_ * 4);
-    dfree(d_slot_cnt_, (size_t)heads_cap_ * 4);
-    dfree(d_slot_mem_, (size_t)heads_cap_ * GW_MEM * 4);
-    d_slot_head_ = d_slot_cnt_ = d_slot_mem_ = nullptr;
+    d_slot_head_ = nullptr;
     heads_cap_ = 0;
   }
   if (d_rb_scratch_) {  // sized by the table: re-made by the next in-place rebuild
@@ -1329,13 +1320,36 @@ size_t DeviceJoin::trim(double now) {
   return before > device_bytes_ ? before - device_bytes_ : 0;
 }
 
-std::vector<uint64_t> DeviceJoin::cache_stats(double now) {
-  if (!d_cstats_) d_cstats_ = (unsigned long long*)dmalloc(64);
-  unsigned long long h[5] = {0, 0, 0, 0, 0};
-  apm_dj_cache_stats(d_table_, table_cap_, now, d_cstats_, stream_);
-  HIP_OK(hipMemcpyAsync(h, d_cstats_, sizeof h, hipMemcpyDeviceToHost, stream_));
-  HIP_OK(hipStreamSynchronize(stream_));
-  return {(uint64_t)table_cap_, h[0], h[1], h[2], h[3], h[4]};
+std::vector<uint64_t> DeviceJoin::cache_stats(double now, bool sync) {
+  if (!d_cstats_) {
+    d_cstats_ = (unsigned long long*)dmalloc(64);
+    HIP_OK(hipHostMalloc((void**)&h_cstats_, 64, hipHostMallocDefault));
+    HIP_OK(hipEventCreateWithFlags(&cstats_ev_, hipEventDisableTiming));
+  }
+  // A stat line (sync = false) reads the previous interval's counts when they are ready and
+  // queues this interval's count on the join stream -- no host wait on the ingest path; the
+  // drained form (sync) counts now and waits.
+  if (!sync && cstats_pending_ && hipEventQuery(cstats_ev_) == hipSuccess) {
+    std::memcpy(cstats_last_, h_cstats_, sizeof cstats_last_);
+    cstats_last_cap_ = cstats_cap_;
+    cstats_pending_ = false;
+  }
+  if (sync || !cstats_pending_) {
+    apm_dj_cache_stats(d_table_, table_cap_, now, d_cstats_, stream_);
+    HIP_OK(hipMemcpyAsync(h_cstats_, d_cstats_, 5 * 8, hipMemcpyDeviceToHost, stream_));
+    HIP_OK(hipEventRecord(cstats_ev_, stream_));
+    cstats_cap_ = table_cap_;
+    cstats_pending_ = true;
+    if (sync || !cstats_have_) {
+      HIP_OK(hipEventSynchronize(cstats_ev_));
+      std::memcpy(cstats_last_, h_cstats_, sizeof cstats_last_);
+      cstats_last_cap_ = cstats_cap_;
+      cstats_pending_ = false;
+      cstats_have_ = true;
+    }
+  }
+  const unsigned long long* h = cstats_last_;
+  return {(uint64_t)cstats_last_cap_, h[0], h[1], h[2], h[3], h[4]};
 }
 
 JoinCounters DeviceJoin::counters() const {

@@ -113,14 +113,15 @@ class DeviceJoin {
   JoinCounters counters() const;
   // occupancy of the join caches at clock `now` (join stream idle): table slots, occupied, acct
   // live, record live, open partials, need live -- the reference's CACHE_STATS
-  std::vector<uint64_t> cache_stats(double now);
+  // (sync = false: the counts of the previous call, the new count queued -- stat lines)
+  std::vector<uint64_t> cache_stats(double now, bool sync = true);
 
   // checkpoint of the GPU join state (checkpoint.cpp): key table (live entries), need arena
   // (live regions), SOAP contexts, service registry, audit-trail carry, counters
   void save(class BinWriter& w);
   void load(class BinReader& r);
   // phase boundaries of the last run() (steady-clock ms): prepass, join launched, sync A,
-  // registered, sync B, sync C, end -- for the engine's stage trace
+  // registered, plan queued, sync C, end -- for the engine's stage trace
   static constexpr int kPhases = 8;
   double phase_t[kPhases + 1] = {0};
   std::vector<std::pair<const char*, std::pair<double, double>>> spans;  // finer trace spans of run()
@@ -250,6 +251,11 @@ class DeviceJoin {
   DJFormatArgs f_{};
   KeyState* d_table_ = nullptr;
   unsigned long long* d_cstats_ = nullptr;  // cache_stats result (5 counters)
+  unsigned long long* h_cstats_ = nullptr;  // (pinned)
+  unsigned long long cstats_last_[5] = {0, 0, 0, 0, 0};
+  uint32_t cstats_cap_ = 0, cstats_last_cap_ = 0;
+  hipEvent_t cstats_ev_ = nullptr;
+  bool cstats_pending_ = false, cstats_have_ = false;
   KeyState* d_table_spare_ = nullptr;  // same-size rebuild target (no allocation per rebuild)
   uint32_t table_cap_ = 0;
   int table_bits_ = 0;
@@ -337,9 +343,6 @@ class DeviceJoin {
   // op grouping by slot lists (DJArgs::slot_head): one head per table slot, all empty between
   // batches (so a same-size rebuild keeps them valid); re-made when the table size changes
   uint32_t* d_slot_head_ = nullptr;
-  uint32_t* d_slot_cnt_ = nullptr;
-  uint32_t* d_slot_mem_ = nullptr;
-  uint32_t* d_op_link_ = nullptr;
   uint32_t heads_cap_ = 0;
   uint32_t* d_big_ = nullptr;
   bool group_sort_ = false;  // APM_OPSORT=sort

@@ -805,7 +805,7 @@ std::vector<uint64_t> Engine::cache_stats(bool drain) {
   if (drain) flush();
   if (dj_) {
     if (drain) HIP_OK(hipStreamSynchronize(parse_stream_));
-    return dj_->cache_stats(watermark_);  // (ordered on the join stream)
+    return dj_->cache_stats(watermark_, drain);  // (ordered on the join stream; a stat line does not wait)
   }
   return {};
 }
