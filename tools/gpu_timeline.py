@@ -94,6 +94,23 @@ def main():
     print("\n| kernel | calls/batch | us/batch |\n|---|---|---|")
     for k, (t, c) in sorted(by.items(), key=lambda x: -x[1][0])[:40]:
         print(f"| {k} | {c / n:.1f} | {t / 1e3 / n:.1f} |")
+    if qcol:  # the runtime's own kernels (hipMemsetAsync fills, hipMemcpyAsync blits) per stream
+        rt = collections.defaultdict(lambda: [0, 0])
+        for r in ks:
+            s_, e_ = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            if not (e_ > t0 and s_ < t1):
+                continue
+            nm = r["Kernel_Name"]
+            kind = "fill" if "fillBuffer" in nm else ("blit" if "copyBuffer" in nm or "copyImage" in nm else None)
+            if kind:
+                rt[(kind, r.get(qcol, "?"))][0] += 1
+                rt[(kind, r.get(qcol, "?"))][1] += e_ - s_
+        print(f"\n| runtime kernel | {qcol} | per batch | us/batch |\n|---|---|---|---|")
+        for (kind, q), (c, t) in sorted(rt.items()):
+            print(f"| {kind} | {q} | {c / n:.1f} | {t / 1e3 / n:.1f} |")
+        for kind in ("fill", "blit"):
+            c = sum(v[0] for (k, _q), v in rt.items() if k == kind)
+            print(f"{kind}s per batch (all streams): {c / n:.1f}")
 
 
 if __name__ == "__main__":
