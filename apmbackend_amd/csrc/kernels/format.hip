@@ -377,11 +377,15 @@ void apm_format_write(FormatArgs* a, hipStream_t stream) {
   const dim3 grid(st_blocks + fs_blocks);
   if (grid.x == 0) return;
   static const int stage_mode = [] {
-    const char* e = std::getenv("APM_FMT_STAGE");  // diagnostic: 0 = no LDS stage
+    const char* e = std::getenv("APM_FMT_STAGE");  // diagnostic: 0 = no LDS stage, 12 / 16 = KB
     return e ? std::atoi(e) : 1;
   }();
   if (stage_mode == 0)
     hipLaunchKernelGGL(k_format_write<0>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);
+  else if (stage_mode == 12)
+    hipLaunchKernelGGL(k_format_write<12288>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);
+  else if (stage_mode == 16)
+    hipLaunchKernelGGL(k_format_write<FMT_LDS_COPY>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);
   else if (a->fs_copy && a->want_fs)  // COPY rows are ~2x the wire line: a bigger LDS stage
     hipLaunchKernelGGL(k_format_write<FMT_LDS_COPY>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);
   else

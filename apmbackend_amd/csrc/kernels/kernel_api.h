@@ -95,6 +95,20 @@ struct RollupArgs {
   double* out;                    // [n_servers][ROLLUP_OUT]
 };
 
+// apm_copy_segs: up to 8 device -> device / host-mapped copies in one launch (stats.hip)
+struct CopySeg {
+  void* dst;
+  const void* src;
+  size_t bytes;
+};
+struct CopySegs {
+  CopySeg seg[8];
+  int32_t n = 0;
+  void add(void* d, const void* s, size_t b) {
+    if (b) seg[n++] = CopySeg{d, s, b};
+  }
+};
+
 // apm_export: device scalars -> pinned host memory (stats.hip)
 struct ExportArgs {
   static constexpr int kMax = 8;
@@ -224,6 +238,7 @@ void apm_copy(void* dst, const void* src, size_t bytes, hipStream_t stream);
 // the same on at most `max_blocks` workgroups of 256 (a host-link copy that leaves the CUs to
 // the kernels running beside it)
 void apm_copy_capped(void* dst, const void* src, size_t bytes, uint32_t max_blocks, hipStream_t stream);
+void apm_copy_segs(const apm::CopySegs* c, hipStream_t stream);
 // up to 8 doubles -> device memory, passed as kernel arguments (nothing read over the host link)
 void apm_set_f64(double* dst, const double* vals, int n, hipStream_t stream);
 // zscore.hip

@@ -759,6 +759,28 @@ __global__ void k_ck_pack(const int32_t* __restrict__ cells, const int32_t* __re
   for (uint32_t j = 0; j < lens[t]; ++j) dst[j] = src[j];
 }
 
+// Up to 8 copies in one launch (blockIdx.y = the copy): the join's sync-C read-back (counts,
+// rollover candidates, unresolved series, audit_db text) into host-mapped pinned memory as one
+// kernel instead of a blit per array.
+__global__ void k_copy_segs(apm::CopySegs c) {
+  const apm::CopySeg& g = c.seg[blockIdx.y];
+  if (blockIdx.y >= (unsigned)c.n) return;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uintptr_t al = (uintptr_t)g.dst | (uintptr_t)g.src;
+  if ((al & 15) == 0) {
+    const size_t n16 = g.bytes / 16;
+    for (size_t i = t; i < n16; i += stride) reinterpret_cast<uint4*>(g.dst)[i] = reinterpret_cast<const uint4*>(g.src)[i];
+    for (size_t i = n16 * 16 + t; i < g.bytes; i += stride) ((uint8_t*)g.dst)[i] = ((const uint8_t*)g.src)[i];
+  } else if ((al & 3) == 0) {
+    const size_t n4 = g.bytes / 4;
+    for (size_t i = t; i < n4; i += stride) reinterpret_cast<uint32_t*>(g.dst)[i] = reinterpret_cast<const uint32_t*>(g.src)[i];
+    for (size_t i = n4 * 4 + t; i < g.bytes; i += stride) ((uint8_t*)g.dst)[i] = ((const uint8_t*)g.src)[i];
+  } else {
+    for (size_t i = t; i < g.bytes; i += stride) ((uint8_t*)g.dst)[i] = ((const uint8_t*)g.src)[i];
+  }
+}
+
 // up to 8 doubles from the kernel arguments (no host-memory read on the device side: a small
 // H2D that waits behind nothing on the host link)
 struct F64x8 {
@@ -788,6 +810,14 @@ void apm_copy_capped(void* dst, const void* src, size_t bytes, uint32_t max_bloc
   if ((a & 15) == 0) launch((uint4*)dst, (const uint4*)src, 16);
   else if ((a & 3) == 0) launch((uint32_t*)dst, (const uint32_t*)src, 4);
   else launch((uint8_t*)dst, (const uint8_t*)src, 1);
+}
+
+void apm_copy_segs(const CopySegs* c, hipStream_t stream) {
+  if (c->n <= 0) return;
+  size_t mx = 0;
+  for (int i = 0; i < c->n; ++i) mx = std::max(mx, c->seg[i].bytes);
+  const unsigned bx = (unsigned)std::max<size_t>(1, std::min<size_t>((mx / 16 + 255) / 256, 64));
+  hipLaunchKernelGGL(k_copy_segs, dim3(bx, (unsigned)c->n), dim3(256), 0, stream, *c);
 }
 
 void apm_set_f64(double* dst, const double* vals, int n, hipStream_t stream) {

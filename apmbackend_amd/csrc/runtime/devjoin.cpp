@@ -7,6 +7,7 @@
 #include <chrono>
 #include <climits>
 #include <cstddef>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -1168,16 +1169,41 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
     h_txt_cap_ = (spec_tx + spec_db) * 2 + (4 << 20);
     HIP_OK(hipHostMalloc((void**)&h_txt_, h_txt_cap_, hipHostMallocDefault));
   }
+  // the read-back: one kernel writing the host-mapped buffers (a blit per array before: six
+  // launches on the join lane's critical path)
+  auto mapped = [](void* h) {
+    void* d = nullptr;
+    HIP_OK(hipHostGetDevicePointer(&d, h, 0));
+    return d;
+  };
   auto write_and_copy = [&] {
     if (apm_dj_write(&f, st) != 0) throw std::runtime_error("device join: scan scratch too small");
-    if (spec) {
-      HIP_OK(hipMemcpyAsync(h_cand_, d_cand_, (size_t)spec * 4, hipMemcpyDeviceToHost, st));
-      HIP_OK(hipMemcpyAsync(h_cand_bucket_, d_cand_bucket_, (size_t)spec * 8, hipMemcpyDeviceToHost, st));
-      HIP_OK(hipMemcpyAsync(h_unres_, d_unres_, (size_t)spec * 8, hipMemcpyDeviceToHost, st));
+    static const bool seg = [] {  // A/B: APM_DJ_SEGCOPY=0 -> a blit per array
+      const char* e = std::getenv("APM_DJ_SEGCOPY");
+      return !e || std::atoi(e) != 0;
+    }();
+    if (!seg) {
+      if (spec) {
+        HIP_OK(hipMemcpyAsync(h_cand_, d_cand_, (size_t)spec * 4, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipMemcpyAsync(h_cand_bucket_, d_cand_bucket_, (size_t)spec * 8, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipMemcpyAsync(h_unres_, d_unres_, (size_t)spec * 8, hipMemcpyDeviceToHost, st));
+      }
+      if (spec_tx) HIP_OK(hipMemcpyAsync(h_txt_, d_txt_tx_, spec_tx, hipMemcpyDeviceToHost, st));
+      if (spec_db) HIP_OK(hipMemcpyAsync(h_txt_ + spec_tx, d_txt_db_, spec_db, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));  // ---- sync C
+      return;
     }
-    if (spec_tx) HIP_OK(hipMemcpyAsync(h_txt_, d_txt_tx_, spec_tx, hipMemcpyDeviceToHost, st));
-    if (spec_db) HIP_OK(hipMemcpyAsync(h_txt_ + spec_tx, d_txt_db_, spec_db, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(JoinCounts), hipMemcpyDeviceToHost, st));
+    CopySegs cs;
+    if (spec) {
+      cs.add(mapped(h_cand_), d_cand_, (size_t)spec * 4);
+      cs.add(mapped(h_cand_bucket_), d_cand_bucket_, (size_t)spec * 8);
+      cs.add(mapped(h_unres_), d_unres_, (size_t)spec * 8);
+    }
+    if (spec_tx) cs.add(mapped(h_txt_), d_txt_tx_, spec_tx);
+    if (spec_db) cs.add((char*)mapped(h_txt_) + spec_tx, d_txt_db_, spec_db);
+    cs.add(mapped(h_counts_), d_counts_, sizeof(JoinCounts));
+    apm_copy_segs(&cs, st);
     HIP_OK(hipStreamSynchronize(st));  // ---- sync C
   };
   write_and_copy();
