@@ -191,6 +191,7 @@ class Tailer {
 
   void add(const std::string& path, int32_t file_id, bool from_start, int32_t group) {
     std::lock_guard<std::mutex> lk(mu_);
+    std::lock_guard<std::mutex> ck(cmu_);
     TailFile f;
     f.path = path;
     f.file_id = file_id;
@@ -230,6 +231,7 @@ class Tailer {
       buf.resize(max_batch_ + 64);
       std::lock_guard<std::mutex> lk(mu_);
       id = read_batch(&buf[0], max_batch_, chunks, n);
+      std::lock_guard<std::mutex> ck(cmu_);
       commit_locked(id);
     }
     buf.resize(n);
@@ -247,8 +249,10 @@ class Tailer {
     return {n, chunks, id};
   }
 
+  // (the commit lock only: the read-ahead thread holds mu_ through a whole batch read, ~0.7 ms,
+  // which the ingest loop's per-batch commit waited out)
   void commit(int64_t id) {
-    std::lock_guard<std::mutex> lk(mu_);
+    std::lock_guard<std::mutex> lk(cmu_);
     commit_locked(id);
   }
 
@@ -324,7 +328,7 @@ class Tailer {
   }
 
   std::string offsets_json() const {
-    std::lock_guard<std::mutex> lk(mu_);
+    std::lock_guard<std::mutex> lk(cmu_);
     std::string o = "{";
     for (size_t i = 0; i < files_.size(); ++i) {
       if (i) o += ",";
@@ -365,6 +369,7 @@ class Tailer {
 
   void set_offset(const std::string& path, uint64_t offset, uint64_t inode) {
     std::lock_guard<std::mutex> lk(mu_);
+    std::lock_guard<std::mutex> ck(cmu_);
     for (auto& f : files_) {
       if (f.path != path) continue;
       struct stat st;
@@ -379,7 +384,7 @@ class Tailer {
   }
 
   std::vector<std::tuple<std::string, uint64_t, uint64_t>> offsets() const {
-    std::lock_guard<std::mutex> lk(mu_);
+    std::lock_guard<std::mutex> lk(cmu_);
     std::vector<std::tuple<std::string, uint64_t, uint64_t>> r;
     for (auto& f : files_) r.emplace_back(f.path, f.committed, f.committed_ino);
     return r;
@@ -524,6 +529,7 @@ class Tailer {
     const int64_t id = next_id_++;
     std::vector<std::pair<size_t, std::pair<uint64_t, uint64_t>>> ends;  // file -> (offset, ino)
     if (paused() || files_.empty()) {
+      std::lock_guard<std::mutex> ck(cmu_);
       pending_[id] = ends;
       return id;
     }
@@ -629,6 +635,7 @@ class Tailer {
       // a file shrank between the probe and the read (truncation race): keep nothing of this
       // batch; the next poll re-plans from the same offsets
       chunks.clear();
+      std::lock_guard<std::mutex> ck(cmu_);
       pending_[id] = ends;
       return id;
     }
@@ -647,7 +654,10 @@ class Tailer {
       if (f.old_fd >= 0) ends.push_back({i, {f.old_offset, f.old_ino}});
       else ends.push_back({i, {f.offset, f.ino}});
     }
-    pending_[id] = std::move(ends);
+    {
+      std::lock_guard<std::mutex> ck(cmu_);
+      pending_[id] = std::move(ends);
+    }
     n_out = pos;
     if (pos) std::memset(dst + pos, 0, std::min<uint64_t>(64, cap + 64 - pos));
     bytes_read_ += pos;
@@ -658,7 +668,7 @@ class Tailer {
     return id;
   }
 
-  void commit_locked(int64_t id) {
+  void commit_locked(int64_t id) {  // cmu_ held
     for (auto it = pending_.begin(); it != pending_.end() && it->first <= id;) {
       for (const auto& e : it->second) {
         files_[e.first].committed = e.second.first;
@@ -691,6 +701,7 @@ class Tailer {
             // waiting in a slot, before the engine has its lines -- a checkpoint would then store
             // offsets past state it does not hold.  So it commits only when nothing is pending.
             if (r.n == 0) {
+              std::lock_guard<std::mutex> ck(cmu_);
               if (pending_.begin()->first == r.id) commit_locked(r.id);
               else pending_.erase(r.id);
             }
@@ -718,7 +729,10 @@ class Tailer {
 
   std::string pause_file_;
   uint64_t max_batch_;
+  // mu_: the read state (files_' read positions and fds, the read-ahead's batch reads);
+  // cmu_: the commit state (pending_, files_' committed positions).  Order: mu_ before cmu_.
   mutable std::mutex mu_;
+  mutable std::mutex cmu_;
   std::vector<TailFile> files_;
   std::vector<size_t> order_;
   std::vector<char> scratch_;

@@ -223,6 +223,7 @@ class IngestService:
         self.perf = {"wait_s": 0.0, "engine_s": 0.0, "outputs_s": 0.0, "batches": 0, "bytes": 0, "prefetched": 0,
                      "ckpt_s": 0.0, "ckpt_flush_s": 0.0, "ckpt_sink_snapshot_s": 0.0,
                      "hk_ticks_s": 0.0, "hk_watch_s": 0.0, "hk_ckpt_s": 0.0, "hk_stats_s": 0.0,
+                     "next_s": 0.0, "commit_s": 0.0,
                      "hk_jmx_s": 0.0, "hk_sink_s": 0.0}
         self.batch_log = None  # a list to record every read-ahead batch (bytes, chunks) in (tests)
         self._drain_every_s = float(g.get("outputDrainMs", 250.0)) / 1000.0
@@ -1010,6 +1011,7 @@ class IngestService:
             import ctypes
             self.batch_log.append((ctypes.string_at(ptr, n), list(chunks)))
         t2 = time.perf_counter()
+        pf["next_s"] = pf.get("next_s", 0.0) + t2 - t1
         if nxt is not None:
             self.native.process_batch_ptr(ptr, n, chunks, -1.0, nxt[1], nxt[2], nxt[3])
         else:
@@ -1031,6 +1033,7 @@ class IngestService:
         self.tailer.commit(bid)
         self._held = nxt
         t4 = time.perf_counter()
+        pf["commit_s"] = pf.get("commit_s", 0.0) + t4 - t3
         # take_bytes waits for the engine's in-flight stats stage: with the DB streams going
         # straight to the native sink, the remaining Python-side streams (al -> notifier) are
         # collected every outputDrainMs instead of once per batch, so batches stay pipelined

@@ -90,13 +90,18 @@ def _run(args, cfg, N, rank, root, IngestService):
     svc = IngestService(cfg, engine="native", files=paths, rank=0, world=1, server_of_path=srv_of, clock=log_clock)
     holder["svc"] = svc
 
-    loop_t = {"step_s": 0.0, "housekeeping_s": 0.0, "idle_s": 0.0, "idles": 0}
+    loop_t = {"step_s": 0.0, "housekeeping_s": 0.0, "idle_s": 0.0, "idles": 0, "cond_s": 0.0}
 
     def drain():
         # the service loop (IngestService.run): step + housekeeping (checkpoints on the log-time
         # clock, stat lines, sink ticks), idle wait when nothing was read
-        while sum(o[1] for o in svc.tailer.offsets()) < written[0] or svc._held is not None:
+        while True:
+            tz = time.perf_counter()
+            more = sum(o[1] for o in svc.tailer.offsets()) < written[0] or svc._held is not None
             ta = time.perf_counter()
+            loop_t["cond_s"] += ta - tz
+            if not more:
+                break
             n = svc.step()
             tb = time.perf_counter()
             svc._housekeeping()
