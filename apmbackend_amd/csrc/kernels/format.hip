@@ -141,10 +141,12 @@ __global__ __launch_bounds__(256) void k_format_len(FormatArgs a) {
 // lane per store (256 B per store instruction).  A block whose range does not fit the stage
 // (very long names) writes its lines to HBM directly.
 constexpr int FMT_WAVE_LINES = 64;
-// Stage size: 24 KB per 64-lane block held the write pass to 1.5 waves per SIMD (LDS-bound
-// occupancy) for a latency-bound per-lane formatter; 8 KB fits a block of typical lines (st ~90 B,
-// fs ~150 B) and allows 5 (VGPR-bound).  APM_FMT_STAGE=0 writes straight to HBM (dword stores).
-constexpr uint32_t FMT_LDS = 8192, FMT_LDS_COPY = 16384;
+// Stage size: the smallest of 8 / 12 / 16 / 24 KB that holds a 64-line block of the previous
+// batch's longer stream (FormatArgs::stage_hint, x1.25).  A fixed 8 KB stage held only st blocks:
+// 64 fs wire lines (~150 B) are ~9.6 KB, so nearly every fs block wrote to HBM directly (46 of 7233
+// LDS instructions per dispatch, profiles/r5_n); 12 KB: the write pass 75 -> 47 us per batch,
+// 16 KB (fewer blocks per CU) 77 us (profiles/r5_o).  APM_FMT_STAGE=0 / 8 / 12 / 16 / 24 forces one.
+constexpr uint32_t FMT_LDS = 8192;
 
 __device__ __forceinline__ void wave_copy_out(const char* __restrict__ lds, char* __restrict__ out, uint32_t g0,
                                               uint32_t g1) {
@@ -376,20 +378,21 @@ void apm_format_write(FormatArgs* a, hipStream_t stream) {
   const int32_t fs_blocks = a->want_fs ? (a->n * a->n_lags + FMT_WAVE_LINES - 1) / FMT_WAVE_LINES : 0;
   const dim3 grid(st_blocks + fs_blocks);
   if (grid.x == 0) return;
-  static const int stage_mode = [] {
-    const char* e = std::getenv("APM_FMT_STAGE");  // diagnostic: 0 = no LDS stage, 12 / 16 = KB
-    return e ? std::atoi(e) : 1;
+  static const int forced = [] {
+    const char* e = std::getenv("APM_FMT_STAGE");  // diagnostic: stage KB (0 = no LDS stage)
+    return e ? std::atoi(e) : -1;
   }();
-  if (stage_mode == 0)
+  const uint32_t want = forced >= 0 ? (uint32_t)forced * 1024u : (a->stage_hint ? a->stage_hint : 12288u);
+  if (forced == 0)
     hipLaunchKernelGGL(k_format_write<0>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);
-  else if (stage_mode == 12)
-    hipLaunchKernelGGL(k_format_write<12288>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);
-  else if (stage_mode == 16)
-    hipLaunchKernelGGL(k_format_write<FMT_LDS_COPY>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);
-  else if (a->fs_copy && a->want_fs)  // COPY rows are ~2x the wire line: a bigger LDS stage
-    hipLaunchKernelGGL(k_format_write<FMT_LDS_COPY>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);
-  else
+  else if (want <= FMT_LDS)
     hipLaunchKernelGGL(k_format_write<FMT_LDS>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);
+  else if (want <= 12288)
+    hipLaunchKernelGGL(k_format_write<12288>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);
+  else if (want <= 16384)
+    hipLaunchKernelGGL(k_format_write<16384>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);
+  else
+    hipLaunchKernelGGL(k_format_write<24576>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);
 }
 
 }  // extern "C"

@@ -2895,6 +2895,7 @@ void Engine::format_rollover_text(int64_t edge_ts) {
   if (apm_format_plan(&fa, d_fmt_tmp_, fmt_tmp_bytes_, stream_) != 0) throw std::runtime_error("format scan failed");
   const double tpw = now_ms();
   trace_event("fmt.len+scans", tpl, tpw, 1);
+  fa.stage_hint = fmt_block_bytes_.load(std::memory_order_relaxed);
   apm_format_write(&fa, stream_);
   trace_event("fmt.write", tpw, now_ms(), 1);
   {
@@ -2918,11 +2919,13 @@ void Engine::format_rollover_text(int64_t edge_ts) {
   HIP_OK(hipEventRecord(ev_fmt_[k], stream_));
   trace_event("fmt.plan", tf0, now_ms(), 1);
   char* dst = d_fmt_out_[k];
+  const size_t n_st = fa.want_st ? (size_t)n : 0, n_fs = fa.want_fs ? (size_t)n * cfg_.n_lags : 0;
   if (fmt_host_) {
-    fmt_task_[k] = post_out([this, k, st_cap]() {
+    fmt_task_[k] = post_out([this, k, st_cap, n_st, n_fs]() {
       const double tl0 = now_ms();
       HIP_OK(hipEventSynchronize(ev_fmt_[k]));  // the text is in host memory once K12 completed
       const size_t st_total = h_fmt_meta_[4 * k], fs_total = h_fmt_meta_[4 * k + 1];
+      note_fmt_block(st_total, n_st, fs_total, n_fs);
       {
         std::lock_guard<std::mutex> g(out_mu_);
         formatted_bytes_lane_ += st_total + fs_total;
@@ -2935,10 +2938,11 @@ void Engine::format_rollover_text(int64_t edge_ts) {
     });
     return;
   }
-  fmt_task_[k] = post_out([this, k, dst, st_cap]() {
+  fmt_task_[k] = post_out([this, k, dst, st_cap, n_st, n_fs]() {
     const double tw0 = now_ms();
     HIP_OK(hipEventSynchronize(ev_fmt_[k]));
     const size_t st_total = h_fmt_meta_[4 * k], fs_total = h_fmt_meta_[4 * k + 1];
+    note_fmt_block(st_total, n_st, fs_total, n_fs);
     const double tw1 = now_ms();
     wait_fmt_holds(k);  // the sink still writes from this buffer (zero-copy COPY rows)
     trace_event("lane st/fs wait format", tw0, tw1, 4);
