@@ -170,20 +170,59 @@ __global__ __launch_bounds__(FMT_WAVE_LINES) void k_format_write(FormatArgs a, i
   const int32_t nl = is_st ? a.n : a.n * a.n_lags;
   const int32_t j0 = (is_st ? (int32_t)blockIdx.x : (int32_t)blockIdx.x - st_blocks) * FMT_WAVE_LINES;
   const int32_t j1 = min(nl, j0 + FMT_WAVE_LINES);
-  const int32_t j = j0 + (int32_t)threadIdx.x;
+  const int lane = (int)threadIdx.x;
+  const int32_t j = j0 + lane;
   const uint32_t* off = is_st ? a.st_off : a.fs_off;
   char* out = is_st ? a.st_out : a.fs_out;
-  const uint32_t g0 = off[j0], g1 = off[j1];
-  const bool lds = LDS != 0 && (g1 - (g0 & ~3u)) <= LDS;  // uniform across the block
+  uint32_t oj = 0, len = 0;
+  if (j < j1) {
+    oj = off[j];
+    len = off[j + 1] - oj;
+  }
+  // Stage layout: each line in dwords of its own (the byte offset inside its first dword as in
+  // the output), consecutive lines an ODD number of dwords apart.  With the output's layout, 64
+  // lines of one length (a run of series with names of one length) started on few banks -- an
+  // 8-way conflict for a 160-byte line -- 5.1-6.6 conflict cycles per LDS instruction
+  // (profiles/r5_p); odd strides put 32 such lines on 32 banks.
+  const uint32_t nd = len ? ((oj & 3u) + len + 3u) >> 2 : 0u;
+  const uint32_t pitch = nd ? (nd | 1u) : 0u;
+  uint32_t inc = pitch;
+#pragma unroll
+  for (int d = 1; d < FMT_WAVE_LINES; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d, FMT_WAVE_LINES);
+    if (lane >= d) inc += y;
+  }
+  const uint32_t total = __shfl(inc, FMT_WAVE_LINES - 1, FMT_WAVE_LINES);
+  const uint32_t sd = inc - pitch;  // the line's first stage dword
+  const bool lds = LDS != 0 && total * 4u <= LDS;  // uniform across the block
   if (j < j1) {
     bool fb = false;
-    OutT<true> o(lds ? stage + (off[j] - (g0 & ~3u)) : out + off[j]);
+    OutT<true> o(lds ? stage + 4u * sd + (oj & 3u) : out + oj);
     if (is_st) st_line(a, j, o, fb);
     else fs_line(a, j, o, fb);
     o.finish();
   }
+  if (!lds) return;
   __syncthreads();
-  if (lds) wave_copy_out(stage, out, g0, g1);
+  // copy-out, one line per step: consecutive stage dwords (no conflicts), contiguous global
+  // stores; a line's first / last dword, shared with its neighbours, bytewise
+  for (int32_t l = 0; l < j1 - j0; ++l) {
+    const uint32_t n_l = (uint32_t)__builtin_amdgcn_readlane((int)nd, l);
+    if (!n_l) continue;
+    const uint32_t s_l = (uint32_t)__builtin_amdgcn_readlane((int)sd, l);
+    const uint32_t o_l = (uint32_t)__builtin_amdgcn_readlane((int)oj, l);
+    const uint32_t e_l = o_l + (uint32_t)__builtin_amdgcn_readlane((int)len, l);
+    for (uint32_t t = (uint32_t)lane; t < n_l; t += FMT_WAVE_LINES) {
+      const uint32_t v = *reinterpret_cast<const uint32_t*>(stage + 4u * (s_l + t));
+      const uint32_t ga = (o_l & ~3u) + 4u * t;
+      if (ga >= o_l && ga + 4u <= e_l) {
+        *reinterpret_cast<uint32_t*>(out + ga) = v;
+      } else {
+        for (uint32_t b = 0; b < 4; ++b)
+          if (ga + b >= o_l && ga + b < e_l) out[ga + b] = (char)(v >> (8u * b));
+      }
+    }
+  }
 }
 
 // ---- fb: fleet baseline rows ------------------------------------------------------------
