@@ -446,7 +446,12 @@ __device__ __forceinline__ SelCount sel_unpack(uint64_t v) {
 // loads (all in flight at once: one memory latency per line), at the same offset modulo 16 so
 // the walks' aligned vector reads stay aligned, and walks it there.  Lines longer than a slot
 // (rare) walk the batch as before.  APM_HF_STAGE=0 keeps the unstaged walk (A/B).
-constexpr int HF_SLOT = 256;  // staged bytes per lane (64 KB per 256-lane block: 2 blocks per CU)
+constexpr int HF_SLOT = 256;  // staged bytes per lane
+// Slot pitch 272 B (68 dwords): with 256 B every lane's slot began on bank 0, so the 16 lanes of a
+// ds_read_b128 group reading the same 16-byte block of their lines hit the same 4 banks -- 16.04
+// conflict cycles per LDS instruction (profiles/r5_p); 68 dwords apart, 16 lanes cover all 64
+// banks, and the b128 stores' 8-lane groups all 32.  68 KB per 256-lane block: still 2 per CU.
+constexpr int HF_PITCH = HF_SLOT + 16;
 
 __device__ __forceinline__ bool hf_needs_bytes(const Event& e) {
   if (e.kind == LK_APP) return !(e.mask & PM_HOST);
@@ -482,7 +487,7 @@ __global__ __launch_bounds__(TB) void k_host_flags(const Event* __restrict__ ev,
                                                    uint8_t* __restrict__ flag, uint64_t* __restrict__ val,
                                                    AudF* __restrict__ aud, SelCount* __restrict__ totals, uint32_t cap,
                                                    int bytewise, int staged) {
-  __shared__ __attribute__((aligned(16))) uint8_t stage[TB * HF_SLOT];
+  __shared__ __attribute__((aligned(16))) uint8_t stage[TB * HF_PITCH];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t n = min(*n_ev_dev, cap);
   if (blockIdx.x * blockDim.x >= n) return;  // (uniform per block: the grid is sized for the capacity)
@@ -499,7 +504,7 @@ __global__ __launch_bounds__(TB) void k_host_flags(const Event* __restrict__ ev,
     if (staged && hf_needs_bytes(e) && nvec * 16u <= (uint32_t)HF_SLOT) {
       // the line's aligned 16-byte blocks, every load issued before the first LDS store
       const uint4* __restrict__ src = reinterpret_cast<const uint4*>(bytes + (e.off - lead));
-      uint4* dst = reinterpret_cast<uint4*>(stage + threadIdx.x * HF_SLOT);
+      uint4* dst = reinterpret_cast<uint4*>(stage + threadIdx.x * HF_PITCH);
       uint4 v[HF_SLOT / 16];
 #pragma unroll
       for (int k = 0; k < HF_SLOT / 16; ++k)
@@ -507,7 +512,7 @@ __global__ __launch_bounds__(TB) void k_host_flags(const Event* __restrict__ ev,
 #pragma unroll
       for (int k = 0; k < HF_SLOT / 16; ++k)
         if ((uint32_t)k < nvec) dst[k] = v[k];
-      p = stage + threadIdx.x * HF_SLOT + lead;
+      p = stage + threadIdx.x * HF_PITCH + lead;
     }
     fl = hf_fields(e, p, fkey, aud, i, bytewise);
     if (e.kind == LK_APP) {
