@@ -203,24 +203,40 @@ __global__ __launch_bounds__(FMT_WAVE_LINES) void k_format_write(FormatArgs a, i
     o.finish();
   }
   if (!lds) return;
+  // copy-out in output order (consecutive dwords per lane group: contiguous stores, consecutive
+  // stage dwords within a line).  The non-empty lines, compacted, tile [g0, g1): an output dword
+  // belongs to the last line starting at or before its last byte, plus -- when that line starts
+  // inside it -- the lines before (their bytes below its start).
+  __shared__ uint32_t lo_s[FMT_WAVE_LINES + 1], ls_s[FMT_WAVE_LINES];
+  const uint64_t ne_mask = __ballot(nd != 0u);
+  const uint32_t ne = (uint32_t)__popcll(ne_mask);
+  if (nd) {
+    const uint32_t c = (uint32_t)__popcll(ne_mask & ((1ull << lane) - 1ull));
+    lo_s[c] = oj;
+    ls_s[c] = sd - (oj >> 2);  // stage dword of output dword d = ls + d
+  }
+  if (lane == 0) lo_s[ne] = ~0u;
   __syncthreads();
-  // copy-out, one line per step: consecutive stage dwords (no conflicts), contiguous global
-  // stores; a line's first / last dword, shared with its neighbours, bytewise
-  for (int32_t l = 0; l < j1 - j0; ++l) {
-    const uint32_t n_l = (uint32_t)__builtin_amdgcn_readlane((int)nd, l);
-    if (!n_l) continue;
-    const uint32_t s_l = (uint32_t)__builtin_amdgcn_readlane((int)sd, l);
-    const uint32_t o_l = (uint32_t)__builtin_amdgcn_readlane((int)oj, l);
-    const uint32_t e_l = o_l + (uint32_t)__builtin_amdgcn_readlane((int)len, l);
-    for (uint32_t t = (uint32_t)lane; t < n_l; t += FMT_WAVE_LINES) {
-      const uint32_t v = *reinterpret_cast<const uint32_t*>(stage + 4u * (s_l + t));
-      const uint32_t ga = (o_l & ~3u) + 4u * t;
-      if (ga >= o_l && ga + 4u <= e_l) {
-        *reinterpret_cast<uint32_t*>(out + ga) = v;
-      } else {
-        for (uint32_t b = 0; b < 4; ++b)
-          if (ga + b >= o_l && ga + b < e_l) out[ga + b] = (char)(v >> (8u * b));
-      }
+  if (ne == 0) return;
+  const uint32_t g0 = off[j0], g1 = off[j1];
+  const uint32_t d0 = g0 >> 2, d1 = (g1 + 3u) >> 2;
+  uint32_t c = 0;
+  for (uint32_t d = d0 + (uint32_t)lane; d < d1; d += FMT_WAVE_LINES) {
+    const uint32_t b0 = 4u * d;
+    while (lo_s[c + 1] <= b0 + 3u) ++c;
+    uint32_t v = *reinterpret_cast<const uint32_t*>(stage + 4u * (ls_s[c] + d));
+    for (uint32_t k = c, lim = lo_s[c]; lim > b0 && k > 0;) {  // the dword's bytes below line k's start
+      --k;
+      const uint32_t w = *reinterpret_cast<const uint32_t*>(stage + 4u * (ls_s[k] + d));
+      const uint32_t keep = 0xffffffffu << (8u * (lim - b0));  // bytes >= lim stay
+      v = (v & keep) | (w & ~keep);
+      lim = lo_s[k];
+    }
+    if (b0 >= g0 && b0 + 4u <= g1) {
+      *reinterpret_cast<uint32_t*>(out + b0) = v;
+    } else {  // the block's first / last dword is shared with a neighbouring block: byte stores
+      for (uint32_t b = 0; b < 4; ++b)
+        if (b0 + b >= g0 && b0 + b < g1) out[b0 + b] = (char)(v >> (8u * b));
     }
   }
 }
