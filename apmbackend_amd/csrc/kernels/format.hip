@@ -203,40 +203,48 @@ __global__ __launch_bounds__(FMT_WAVE_LINES) void k_format_write(FormatArgs a, i
     o.finish();
   }
   if (!lds) return;
-  // copy-out in output order (consecutive dwords per lane group: contiguous stores, consecutive
-  // stage dwords within a line).  The non-empty lines, compacted, tile [g0, g1): an output dword
-  // belongs to the last line starting at or before its last byte, plus -- when that line starts
-  // inside it -- the lines before (their bytes below its start).
+  // copy-out in output order, 64 dwords per step (contiguous stores, consecutive stage dwords
+  // within a line).  The non-empty lines, compacted, tile [g0, g1); a step ORs in, line by line
+  // (a scalar loop, ~2-3 lines per 256-byte window), each line's bytes of the lanes' dwords.
   __shared__ uint32_t lo_s[FMT_WAVE_LINES + 1], ls_s[FMT_WAVE_LINES];
   const uint64_t ne_mask = __ballot(nd != 0u);
   const uint32_t ne = (uint32_t)__popcll(ne_mask);
+  if (ne == 0) return;
+  const uint32_t g0 = off[j0], g1 = off[j1];
   if (nd) {
     const uint32_t c = (uint32_t)__popcll(ne_mask & ((1ull << lane) - 1ull));
     lo_s[c] = oj;
     ls_s[c] = sd - (oj >> 2);  // stage dword of output dword d = ls + d
   }
-  if (lane == 0) lo_s[ne] = ~0u;
+  if (lane == 0) lo_s[ne] = g1;
   __syncthreads();
-  if (ne == 0) return;
-  const uint32_t g0 = off[j0], g1 = off[j1];
+  const uint32_t lo_r = (uint32_t)lane < ne ? lo_s[lane] : g1;
+  const uint32_t hi_r = (uint32_t)lane < ne ? lo_s[lane + 1] : g1;
+  const uint32_t ls_r = (uint32_t)lane < ne ? ls_s[lane] : 0u;
   const uint32_t d0 = g0 >> 2, d1 = (g1 + 3u) >> 2;
-  uint32_t c = 0;
-  for (uint32_t d = d0 + (uint32_t)lane; d < d1; d += FMT_WAVE_LINES) {
-    const uint32_t b0 = 4u * d;
-    while (lo_s[c + 1] <= b0 + 3u) ++c;
-    uint32_t v = *reinterpret_cast<const uint32_t*>(stage + 4u * (ls_s[c] + d));
-    for (uint32_t k = c, lim = lo_s[c]; lim > b0 && k > 0;) {  // the dword's bytes below line k's start
-      --k;
-      const uint32_t w = *reinterpret_cast<const uint32_t*>(stage + 4u * (ls_s[k] + d));
-      const uint32_t keep = 0xffffffffu << (8u * (lim - b0));  // bytes >= lim stay
-      v = (v & keep) | (w & ~keep);
-      lim = lo_s[k];
+  int32_t c = 0;  // uniform: the first line not yet wholly copied
+  for (uint32_t w = d0; w < d1; w += FMT_WAVE_LINES) {
+    const uint32_t d = w + (uint32_t)lane, b0 = 4u * d, wend = 4u * (w + FMT_WAVE_LINES);
+    uint32_t v = 0;
+    for (; c < (int32_t)ne; ++c) {
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)lo_r, c);
+      if (lo >= wend) break;
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)hi_r, c);
+      const uint32_t ls = (uint32_t)__builtin_amdgcn_readlane((int)ls_r, c);
+      if (b0 + 4u > lo && b0 < hi) {
+        const uint32_t x = *reinterpret_cast<const uint32_t*>(stage + 4u * (ls + d));
+        const uint32_t lb = lo > b0 ? lo - b0 : 0u, hb = hi < b0 + 4u ? hi - b0 : 4u;
+        v |= x & (uint32_t)(((1ull << (8u * hb)) - 1ull) & ~((1ull << (8u * lb)) - 1ull));
+      }
+      if (hi > wend) break;  // continues into the next window
     }
-    if (b0 >= g0 && b0 + 4u <= g1) {
-      *reinterpret_cast<uint32_t*>(out + b0) = v;
-    } else {  // the block's first / last dword is shared with a neighbouring block: byte stores
-      for (uint32_t b = 0; b < 4; ++b)
-        if (b0 + b >= g0 && b0 + b < g1) out[b0 + b] = (char)(v >> (8u * b));
+    if (d < d1) {
+      if (b0 >= g0 && b0 + 4u <= g1) {
+        *reinterpret_cast<uint32_t*>(out + b0) = v;
+      } else {  // the block's first / last dword is shared with a neighbouring block: byte stores
+        for (uint32_t b = 0; b < 4; ++b)
+          if (b0 + b >= g0 && b0 + b < g1) out[b0 + b] = (char)(v >> (8u * b));
+      }
     }
   }
 }

@@ -590,6 +590,12 @@ Engine::~Engine() {
     hipEventDestroy(ev_rel_[k]);
     hipEventDestroy(ev_fmt_[k]);
   }
+  for (int r = 0; r < FMT_RING; ++r) {
+    FmtHolds& hs = *fmt_holds_;
+    std::unique_lock<std::mutex> lk(hs.mu);
+    if (!hs.cv.wait_for(lk, std::chrono::seconds(60), [&] { return hs.n[6 + r] == 0; })) continue;
+    if (h_fmt_ring_[r]) hipHostFree(h_fmt_ring_[r]);
+  }
   if (h_roll_out_) hipHostFree(h_roll_out_);
   if (cool_ev_) { hipEventSynchronize(cool_ev_); hipEventDestroy(cool_ev_); }
   if (h_cool_idx_) { hipHostFree(h_cool_idx_); hipHostFree(h_cool_val_); }
@@ -2938,21 +2944,23 @@ void Engine::format_rollover_text(int64_t edge_ts) {
     });
     return;
   }
-  fmt_task_[k] = post_out([this, k, dst, st_cap, n_st, n_fs]() {
+  const int hk = fmt_ring_k_;
+  fmt_ring_k_ = (fmt_ring_k_ + 1) % FMT_RING;
+  fmt_task_[k] = post_out([this, k, hk, dst, st_cap, n_st, n_fs]() {
     const double tw0 = now_ms();
     HIP_OK(hipEventSynchronize(ev_fmt_[k]));
     const size_t st_total = h_fmt_meta_[4 * k], fs_total = h_fmt_meta_[4 * k + 1];
     note_fmt_block(st_total, n_st, fs_total, n_fs);
     const double tw1 = now_ms();
-    wait_fmt_holds(k);  // the sink still writes from this buffer (zero-copy COPY rows)
+    wait_fmt_holds(6 + hk);  // the sink still writes from this ring slot (zero-copy COPY rows)
     trace_event("lane st/fs wait format", tw0, tw1, 4);
     trace_event("lane st/fs wait sink", tw1, now_ms(), 4);
-    if (st_total + fs_total > h_fmt_cap_[k]) {
-      if (h_fmt_out_[k]) HIP_OK(hipHostFree(h_fmt_out_[k]));
-      h_fmt_cap_[k] = (st_total + fs_total) * 2 + (4 << 20);
-      HIP_OK(hipHostMalloc((void**)&h_fmt_out_[k], h_fmt_cap_[k], hipHostMallocDefault));
+    if (st_total + fs_total > h_fmt_ring_cap_[hk]) {
+      if (h_fmt_ring_[hk]) HIP_OK(hipHostFree(h_fmt_ring_[hk]));
+      h_fmt_ring_cap_[hk] = (st_total + fs_total) * 5 / 4 + (4 << 20);
+      HIP_OK(hipHostMalloc((void**)&h_fmt_ring_[hk], h_fmt_ring_cap_[hk], hipHostMallocDefault));
     }
-    char* h = h_fmt_out_[k];
+    char* h = h_fmt_ring_[hk];
     const double tl0 = now_ms();
     if (st_total) lane_d2h(h, dst, st_total);
     if (fs_total) lane_d2h(h + st_total, dst + st_cap, fs_total);
@@ -2963,7 +2971,7 @@ void Engine::format_rollover_text(int64_t edge_ts) {
     }
     const double tl1 = now_ms();
     emit_bytes(OUT_ST, h, st_total);
-    emit_bytes_held(OUT_FS, h + st_total, fs_total, k, fs_rows_[k] ? h_fs_off_[k] : nullptr, fs_rows_[k]);
+    emit_bytes_held(OUT_FS, h + st_total, fs_total, 6 + hk, fs_rows_[k] ? h_fs_off_[k] : nullptr, fs_rows_[k]);
     trace_event("lane st/fs D2H", tl0, tl1, 4);
     trace_event("lane st/fs emit", tl1, now_ms(), 4);
   });

@@ -502,10 +502,13 @@ class Engine {
   void emit_bytes_held(int kind, const char* p, size_t n, int k, const uint32_t* row_off = nullptr,
                        size_t nrows = 0);
   void wait_fmt_holds(int k);
+  static constexpr int FMT_RING = 4;
   struct FmtHolds {  // shared with the holds: a release after the engine is gone stays safe
     std::mutex mu;
     std::condition_variable cv;
-    int n[6] = {0, 0, 0, 0, 0, 0};  // st/fs staging 0, 1; fb staging 2, 3; released db text 4, 5
+    // st/fs device-written staging 0, 1 (APM_FMT_HOST); fb staging 2, 3; released db text 4, 5;
+    // st/fs host ring 6 .. 6 + FMT_RING
+    int n[6 + FMT_RING] = {};
   };
   std::shared_ptr<FmtHolds> fmt_holds_ = std::make_shared<FmtHolds>();
   void upload_series_tables(int32_t lo);
@@ -1113,6 +1116,13 @@ class Engine {
   char* hd_fmt_out_[2] = {nullptr, nullptr};
   hipEvent_t ev_fmt_[2] = {nullptr, nullptr};
   uint64_t fmt_task_[2] = {0, 0};
+  // Pinned st/fs staging the output lane copies into, a ring deeper than the device double
+  // buffer: the sink's spool writers hold a slot until written (zero-copy COPY rows), and with
+  // the two device slots the lane waited for the writes of the batch before last (0.42 ms per
+  // batch, profiles/r5_q/service_trace_summary.txt).
+  char* h_fmt_ring_[FMT_RING] = {};
+  size_t h_fmt_ring_cap_[FMT_RING] = {};
+  int fmt_ring_k_ = 0;  // stats thread
   // K12's LDS stage: bytes of a 64-line block of the longer stream in the last batch, x1.25
   std::atomic<uint32_t> fmt_block_bytes_{0};
   void note_fmt_block(size_t st_bytes, size_t st_lines, size_t fs_bytes, size_t fs_lines) {
