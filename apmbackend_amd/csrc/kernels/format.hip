@@ -24,8 +24,8 @@ namespace apm {
 
 namespace {
 
-template <bool W>
-__device__ __forceinline__ void head(OutT<W>& o, bool st, const FormatArgs& a, int32_t s) {
+template <class O>
+__device__ __forceinline__ void head(O& o, bool st, const FormatArgs& a, int32_t s) {
   if (st) o.lit("st|"); else o.lit("fs|");
   o.sb(a.ts_wire, a.ts_wire_len);
   const int4 nm = a.series_names[s];
@@ -36,8 +36,8 @@ __device__ __forceinline__ void head(OutT<W>& o, bool st, const FormatArgs& a, i
 }
 
 // st line of emission position i (empty for a series without a tx yet)
-template <bool W>
-__device__ __forceinline__ void st_line(const FormatArgs& a, int32_t i, OutT<W>& st, bool& fb) {
+template <class O>
+__device__ __forceinline__ void st_line(const FormatArgs& a, int32_t i, O& st, bool& fb) {
   const int32_t s = a.perm[i];
   const WinStat w = a.win[s];
   if (!w.active) return;
@@ -50,8 +50,8 @@ __device__ __forceinline__ void st_line(const FormatArgs& a, int32_t i, OutT<W>&
 
 // fs line j = (emission position i, LAG rank li): lines of one series are consecutive, LAGs
 // ascending (FullStatEntry per LAG, stream_calc_z_score.js:282-306)
-template <bool W>
-__device__ __forceinline__ void fs_line(const FormatArgs& a, int32_t j, OutT<W>& fs, bool& fb) {
+template <class O>
+__device__ __forceinline__ void fs_line(const FormatArgs& a, int32_t j, O& fs, bool& fb) {
   const int32_t i = j / a.n_lags, li = j - i * a.n_lags;
   const int32_t s = a.perm[i];
   const WinStat w = a.win[s];
@@ -142,7 +142,9 @@ __global__ __launch_bounds__(256) void k_format_len(FormatArgs a) {
 // (very long names) writes its lines to HBM directly.
 constexpr int FMT_WAVE_LINES = 64;
 // Stage size: the smallest of 8 / 12 / 16 / 24 KB that holds a 64-line block of the previous
-// batch's longer stream (FormatArgs::stage_hint, x1.25).  A fixed 8 KB stage held only st blocks:
+// batch's longer stream (FormatArgs::stage_hint, x1.25); LDS occupancy sets the pace of this
+// latency-bound formatter (odd-pitch per-line slots needed 16 KB where this layout fits 12 KB:
+// 108 vs 47 us per batch, profiles/r5_s vs r5_o).  A fixed 8 KB stage held only st blocks:
 // 64 fs wire lines (~150 B) are ~9.6 KB, so nearly every fs block wrote to HBM directly (46 of 7233
 // LDS instructions per dispatch, profiles/r5_n); 12 KB: the write pass 75 -> 47 us per batch,
 // 16 KB (fewer blocks per CU) 77 us (profiles/r5_o).  APM_FMT_STAGE=0 / 8 / 12 / 16 / 24 forces one.
@@ -170,81 +172,41 @@ __global__ __launch_bounds__(FMT_WAVE_LINES) void k_format_write(FormatArgs a, i
   const int32_t nl = is_st ? a.n : a.n * a.n_lags;
   const int32_t j0 = (is_st ? (int32_t)blockIdx.x : (int32_t)blockIdx.x - st_blocks) * FMT_WAVE_LINES;
   const int32_t j1 = min(nl, j0 + FMT_WAVE_LINES);
-  const int lane = (int)threadIdx.x;
-  const int32_t j = j0 + lane;
+  const int32_t j = j0 + (int32_t)threadIdx.x;
   const uint32_t* off = is_st ? a.st_off : a.fs_off;
   char* out = is_st ? a.st_out : a.fs_out;
-  uint32_t oj = 0, len = 0;
-  if (j < j1) {
-    oj = off[j];
-    len = off[j + 1] - oj;
-  }
-  // Stage layout: each line in dwords of its own (the byte offset inside its first dword as in
-  // the output), consecutive lines an ODD number of dwords apart.  With the output's layout, 64
-  // lines of one length (a run of series with names of one length) started on few banks -- an
-  // 8-way conflict for a 160-byte line -- 5.1-6.6 conflict cycles per LDS instruction
-  // (profiles/r5_p); odd strides put 32 such lines on 32 banks.
-  const uint32_t nd = len ? ((oj & 3u) + len + 3u) >> 2 : 0u;
-  const uint32_t pitch = nd ? (nd | 1u) : 0u;
-  uint32_t inc = pitch;
-#pragma unroll
-  for (int d = 1; d < FMT_WAVE_LINES; d <<= 1) {
-    const uint32_t y = __shfl_up(inc, d, FMT_WAVE_LINES);
-    if (lane >= d) inc += y;
-  }
-  const uint32_t total = __shfl(inc, FMT_WAVE_LINES - 1, FMT_WAVE_LINES);
-  const uint32_t sd = inc - pitch;  // the line's first stage dword
-  const bool lds = LDS != 0 && total * 4u <= LDS;  // uniform across the block
+  const uint32_t g0 = off[j0], g1 = off[j1], a0 = g0 & ~3u;
+  // (LDS is a multiple of the 128-byte swizzle row: every rotated dword stays inside the stage)
+  const bool lds = LDS != 0 && (g1 - a0) <= LDS;  // uniform across the block
   if (j < j1) {
     bool fb = false;
-    OutT<true> o(lds ? stage + 4u * sd + (oj & 3u) : out + oj);
-    if (is_st) st_line(a, j, o, fb);
-    else fs_line(a, j, o, fb);
-    o.finish();
+    if (lds) {
+      // the stage as the output's bytes from a0, each 32-dword row rotated by its index
+      // (stage_swz): 64 lines of one length started on few banks in the plain layout -- an 8-way
+      // conflict for 160-byte lines, 5.1-6.6 conflict cycles per LDS instruction (profiles/r5_p)
+      OutT<true, true> o(stage, off[j] - a0);
+      if (is_st) st_line(a, j, o, fb);
+      else fs_line(a, j, o, fb);
+      o.finish();
+    } else {
+      OutT<true> o(out + off[j]);
+      if (is_st) st_line(a, j, o, fb);
+      else fs_line(a, j, o, fb);
+      o.finish();
+    }
   }
   if (!lds) return;
-  // copy-out in output order, 64 dwords per step (contiguous stores, consecutive stage dwords
-  // within a line).  The non-empty lines, compacted, tile [g0, g1); a step ORs in, line by line
-  // (a scalar loop, ~2-3 lines per 256-byte window), each line's bytes of the lanes' dwords.
-  __shared__ uint32_t lo_s[FMT_WAVE_LINES + 1], ls_s[FMT_WAVE_LINES];
-  const uint64_t ne_mask = __ballot(nd != 0u);
-  const uint32_t ne = (uint32_t)__popcll(ne_mask);
-  if (ne == 0) return;
-  const uint32_t g0 = off[j0], g1 = off[j1];
-  if (nd) {
-    const uint32_t c = (uint32_t)__popcll(ne_mask & ((1ull << lane) - 1ull));
-    lo_s[c] = oj;
-    ls_s[c] = sd - (oj >> 2);  // stage dword of output dword d = ls + d
-  }
-  if (lane == 0) lo_s[ne] = g1;
   __syncthreads();
-  const uint32_t lo_r = (uint32_t)lane < ne ? lo_s[lane] : g1;
-  const uint32_t hi_r = (uint32_t)lane < ne ? lo_s[lane + 1] : g1;
-  const uint32_t ls_r = (uint32_t)lane < ne ? ls_s[lane] : 0u;
-  const uint32_t d0 = g0 >> 2, d1 = (g1 + 3u) >> 2;
-  int32_t c = 0;  // uniform: the first line not yet wholly copied
-  for (uint32_t w = d0; w < d1; w += FMT_WAVE_LINES) {
-    const uint32_t d = w + (uint32_t)lane, b0 = 4u * d, wend = 4u * (w + FMT_WAVE_LINES);
-    uint32_t v = 0;
-    for (; c < (int32_t)ne; ++c) {
-      const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)lo_r, c);
-      if (lo >= wend) break;
-      const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)hi_r, c);
-      const uint32_t ls = (uint32_t)__builtin_amdgcn_readlane((int)ls_r, c);
-      if (b0 + 4u > lo && b0 < hi) {
-        const uint32_t x = *reinterpret_cast<const uint32_t*>(stage + 4u * (ls + d));
-        const uint32_t lb = lo > b0 ? lo - b0 : 0u, hb = hi < b0 + 4u ? hi - b0 : 4u;
-        v |= x & (uint32_t)(((1ull << (8u * hb)) - 1ull) & ~((1ull << (8u * lb)) - 1ull));
-      }
-      if (hi > wend) break;  // continues into the next window
-    }
-    if (d < d1) {
-      if (b0 >= g0 && b0 + 4u <= g1) {
-        *reinterpret_cast<uint32_t*>(out + b0) = v;
-      } else {  // the block's first / last dword is shared with a neighbouring block: byte stores
-        for (uint32_t b = 0; b < 4; ++b)
-          if (b0 + b >= g0 && b0 + b < g1) out[b0 + b] = (char)(v >> (8u * b));
-      }
+  // copy-out: each 32-lane group reads one whole row (32 distinct banks), contiguous stores
+  const uint32_t nd = (g1 - a0 + 3u) >> 2;
+  for (uint32_t t = threadIdx.x; t < nd; t += FMT_WAVE_LINES) {
+    const uint32_t v = *reinterpret_cast<const uint32_t*>(stage + 4u * stage_swz(t));
+    const uint32_t ga = a0 + 4u * t;
+    if (ga >= g0 && ga + 4u <= g1) {
+      *reinterpret_cast<uint32_t*>(out + ga) = v;
+    } else {  // the block's first / last dword is shared with a neighbour: byte stores
+      for (uint32_t b = 0; b < 4; ++b)
+        if (ga + b >= g0 && ga + b < g1) out[ga + b] = (char)(v >> (8u * b));
     }
   }
 }

@@ -602,15 +602,16 @@ Engine::~Engine() {
   if (dj_) {
     hipStreamSynchronize(out_stream_);
     hipHostFree(h_ring_min_); hipHostFree(h_rel_n_); hipHostFree(h_rel_total_); hipHostFree(h_unseen_flag_);
-    for (int k = 0; k < 2; ++k) {
+    for (int r = 0; r < REL_RING; ++r) {
       {  // zero-copy db rows still referenced by the sink (bounded wait, as for st/fs)
         FmtHolds& hs = *fmt_holds_;
         std::unique_lock<std::mutex> lk(hs.mu);
-        if (!hs.cv.wait_for(lk, std::chrono::seconds(60), [&] { return hs.n[4 + k] == 0; })) continue;
+        if (!hs.cv.wait_for(lk, std::chrono::seconds(60), [&] { return hs.n[6 + FMT_RING + r] == 0; })) continue;
       }
-      if (h_rel_text_[k]) hipHostFree(h_rel_text_[k]);
-      if (h_rel_offs_[k]) hipHostFree(h_rel_offs_[k]);
+      if (h_rel_text_[r]) hipHostFree(h_rel_text_[r]);
     }
+    for (int k = 0; k < 2; ++k)
+      if (h_rel_offs_[k]) hipHostFree(h_rel_offs_[k]);
 
     dj_.reset();
   }
@@ -2445,36 +2446,39 @@ void Engine::release_device_finish() {
       d2h(h_rel_offs_[k], d_rel_offs_, ((size_t)released + 1) * 4, stream_);
     }
     HIP_OK(hipEventRecord(ev_rel_[k], stream_));
-    rel_task_[k] = post_rel([this, k, total, rows, released, host_enc]() {
+    const int rk = rel_ring_k_;
+    rel_ring_k_ = (rel_ring_k_ + 1) % REL_RING;
+    rel_task_[k] = post_rel([this, k, rk, total, rows, released, host_enc]() {
       const double tw0 = now_ms();
       HIP_OK(hipEventSynchronize(ev_rel_[k]));
       const double tw1 = now_ms();
-      wait_fmt_holds(4 + k);  // the sink still writes from this buffer (zero-copy COPY rows)
+      wait_fmt_holds(6 + FMT_RING + rk);  // the sink still writes from this slot (zero-copy COPY rows)
       trace_event("lane db wait gather", tw0, tw1, 4);
       trace_event("lane db wait sink", tw1, now_ms(), 4);
-      if (total > h_rel_text_cap_[k]) {
-        if (h_rel_text_[k]) HIP_OK(hipHostFree(h_rel_text_[k]));
-        h_rel_text_cap_[k] = total * 2 + (4 << 20);  // (a pinned allocation costs ms: 2x headroom)
-        HIP_OK(hipHostMalloc((void**)&h_rel_text_[k], h_rel_text_cap_[k], hipHostMallocDefault));
+      char*& h = h_rel_text_[rk];
+      if (total > h_rel_text_cap_[rk]) {
+        if (h) HIP_OK(hipHostFree(h));
+        h_rel_text_cap_[rk] = total * 2 + (4 << 20);  // (a pinned allocation costs ms: 2x headroom)
+        HIP_OK(hipHostMalloc((void**)&h, h_rel_text_cap_[rk], hipHostMallocDefault));
       }
       const double tl0 = now_ms();
       if (rel_lane_on_) {
-        lane_d2h(h_rel_text_[k], d_rel_text_[k], total, rel_stream_);
+        lane_d2h(h, d_rel_text_[k], total, rel_stream_);
         HIP_OK(hipStreamSynchronize(rel_stream_));
       } else {
-        lane_d2h(h_rel_text_[k], d_rel_text_[k], total);
+        lane_d2h(h, d_rel_text_[k], total);
         lane_sync();
       }
       const double tl1 = now_ms();
       if (host_enc) {
         std::string enc[5];
         int64_t counts[5] = {0, 0, 0, 0, 0};
-        copyenc::encode_blob(std::string_view(h_rel_text_[k], total), enc, counts);
+        copyenc::encode_blob(std::string_view(h, total), enc, counts);
         emit_bytes(OUT_DB, enc[0].data(), enc[0].size());
       } else if (rows) {
-        emit_bytes_held(OUT_DB, h_rel_text_[k], total, 4 + k, h_rel_offs_[k], (size_t)released);
+        emit_bytes_held(OUT_DB, h, total, 6 + FMT_RING + rk, h_rel_offs_[k], (size_t)released);
       } else {
-        emit_bytes(OUT_DB, h_rel_text_[k], total);
+        emit_bytes(OUT_DB, h, total);
       }
       trace_event("lane db D2H", tl0, tl1, 4);
       trace_event("lane db emit", tl1, now_ms(), 4);

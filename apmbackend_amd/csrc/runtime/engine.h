@@ -502,13 +502,13 @@ class Engine {
   void emit_bytes_held(int kind, const char* p, size_t n, int k, const uint32_t* row_off = nullptr,
                        size_t nrows = 0);
   void wait_fmt_holds(int k);
-  static constexpr int FMT_RING = 4;
+  static constexpr int FMT_RING = 4, REL_RING = 4;
   struct FmtHolds {  // shared with the holds: a release after the engine is gone stays safe
     std::mutex mu;
     std::condition_variable cv;
     // st/fs device-written staging 0, 1 (APM_FMT_HOST); fb staging 2, 3; released db text 4, 5;
-    // st/fs host ring 6 .. 6 + FMT_RING
-    int n[6 + FMT_RING] = {};
+    // st/fs host ring 6 .. 6 + FMT_RING; released db text ring after it
+    int n[6 + FMT_RING + REL_RING] = {};
   };
   std::shared_ptr<FmtHolds> fmt_holds_ = std::make_shared<FmtHolds>();
   void upload_series_tables(int32_t lo);
@@ -775,8 +775,11 @@ class Engine {
   uint32_t* hd_rel_total_ = nullptr;
   char* d_rel_text_[2] = {nullptr, nullptr};
   size_t rel_text_cap_[2] = {0, 0};
-  char* h_rel_text_[2] = {nullptr, nullptr};
-  size_t h_rel_text_cap_[2] = {0, 0};
+  // pinned released-line text, a ring (the sink's spool writers hold a slot until written; with
+  // two the release lane waited 1.7 ms per batch for them, profiles/r5_s)
+  char* h_rel_text_[REL_RING] = {};
+  size_t h_rel_text_cap_[REL_RING] = {};
+  int rel_ring_k_ = 0;  // stats thread
   uint32_t* h_rel_offs_[2] = {nullptr, nullptr};  // pinned: the released rows' offsets (sink flush cuts)
   size_t h_rel_offs_cap_[2] = {0, 0};
   hipStream_t out_stream_ = nullptr;
@@ -1127,7 +1130,7 @@ class Engine {
   std::atomic<uint32_t> fmt_block_bytes_{0};
   void note_fmt_block(size_t st_bytes, size_t st_lines, size_t fs_bytes, size_t fs_lines) {
     const size_t a = std::max(st_lines ? st_bytes / st_lines : 0, fs_lines ? fs_bytes / fs_lines : 0);
-    if (a) fmt_block_bytes_.store((uint32_t)std::min<size_t>(a * 80 + 768, 1u << 20), std::memory_order_relaxed);
+    if (a) fmt_block_bytes_.store((uint32_t)std::min<size_t>(a * 80 + 64, 1u << 20), std::memory_order_relaxed);
   }
   int fmt_k_ = 0;
   uint32_t* h_fmt_meta_ = nullptr;               // pinned: per slot k, [4k] st total, [4k+1] fs total
