@@ -141,8 +141,8 @@ __global__ __launch_bounds__(256) void k_format_len(FormatArgs a) {
 // lane per store (256 B per store instruction).  A block whose range does not fit the stage
 // (very long names) writes its lines to HBM directly.
 constexpr int FMT_WAVE_LINES = 64;
-// Stage size: the smallest of 8 / 12 / 16 / 24 KB that holds a 64-line block of the previous
-// batch's longer stream (FormatArgs::stage_hint, x1.25); LDS occupancy sets the pace of this
+// Stage size: 8 / 12 / 16 / 24 KB by the bytes of an average 64-line block of the previous
+// batch's longer stream (FormatArgs::stage_hint); LDS occupancy sets the pace of this
 // latency-bound formatter (odd-pitch per-line slots needed 16 KB where this layout fits 12 KB:
 // 108 vs 47 us per batch, profiles/r5_s vs r5_o).  A fixed 8 KB stage held only st blocks:
 // 64 fs wire lines (~150 B) are ~9.6 KB, so nearly every fs block wrote to HBM directly (46 of 7233
@@ -180,20 +180,13 @@ __global__ __launch_bounds__(FMT_WAVE_LINES) void k_format_write(FormatArgs a, i
   const bool lds = LDS != 0 && (g1 - a0) <= LDS;  // uniform across the block
   if (j < j1) {
     bool fb = false;
-    if (lds) {
-      // the stage as the output's bytes from a0, each 32-dword row rotated by its index
-      // (stage_swz): 64 lines of one length started on few banks in the plain layout -- an 8-way
-      // conflict for 160-byte lines, 5.1-6.6 conflict cycles per LDS instruction (profiles/r5_p)
-      OutT<true, true> o(stage, off[j] - a0);
-      if (is_st) st_line(a, j, o, fb);
-      else fs_line(a, j, o, fb);
-      o.finish();
-    } else {
-      OutT<true> o(out + off[j]);
-      if (is_st) st_line(a, j, o, fb);
-      else fs_line(a, j, o, fb);
-      o.finish();
-    }
+    // staged: the output's bytes from a0, each 32-dword row rotated by its index (stage_swz): 64
+    // lines of one length started on few banks in the plain layout -- an 8-way conflict for
+    // 160-byte lines, 5.1-6.6 conflict cycles per LDS instruction (profiles/r5_p)
+    OutT<true, true> o(lds ? stage : out, lds ? off[j] - a0 : off[j], lds);
+    if (is_st) st_line(a, j, o, fb);
+    else fs_line(a, j, o, fb);
+    o.finish();
   }
   if (!lds) return;
   __syncthreads();
@@ -407,14 +400,16 @@ void apm_format_write(FormatArgs* a, hipStream_t stream) {
     const char* e = std::getenv("APM_FMT_STAGE");  // diagnostic: stage KB (0 = no LDS stage)
     return e ? std::atoi(e) : -1;
   }();
+  // (a block a little over the stage writes straight to HBM: the next size down costs occupancy
+  // on every block -- 12 KB beat 16 KB on 64 COPY rows of ~190 B, profiles/r5_o)
   const uint32_t want = forced >= 0 ? (uint32_t)forced * 1024u : (a->stage_hint ? a->stage_hint : 12288u);
   if (forced == 0)
     hipLaunchKernelGGL(k_format_write<0>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);
-  else if (want <= FMT_LDS)
+  else if (want <= 7168)
     hipLaunchKernelGGL(k_format_write<FMT_LDS>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);
-  else if (want <= 12288)
+  else if (want <= 12800)
     hipLaunchKernelGGL(k_format_write<12288>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);
-  else if (want <= 16384)
+  else if (want <= 16896)
     hipLaunchKernelGGL(k_format_write<16384>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);
   else
     hipLaunchKernelGGL(k_format_write<24576>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);

@@ -139,7 +139,7 @@ struct FormatArgs {
   // fs as Postgres COPY rows (the DB sink's K13 encoding fused into K12): the fs stream then
   // carries `timestamp \t server \t service \t tpm \t lag \t stats-json` rows (copyenc.cpp)
   int32_t fs_copy;
-  uint32_t stage_hint;  // bytes of a 64-line block of the longer stream (previous batch); 0 = unknown
+  uint32_t stage_hint;  // bytes of an average 64-line block of the longer stream (previous batch); 0 = unknown
   int32_t ts_copy_len;
   char ts_copy[32];        // edge_ts as 'YYYY-MM-DD HH:MM:SS.mmm+00'
   int32_t ts_wire_len;

@@ -48,8 +48,9 @@ __device__ __noinline__ static uint32_t text_big_fixed(char* buf, bool neg, doub
 // and lines of one length no longer start on the same few banks.
 __device__ __forceinline__ uint32_t stage_swz(uint32_t t) { return (t & ~31u) | ((t + (t >> 5)) & 31u); }
 
-// SWZ = true: the line is written into an LDS stage laid out by stage_swz (base = the stage,
-// lo = the line's byte offset in it); otherwise base is the line's first byte.
+// SWZ = true: byte x of the line is base + lo + x, through stage_swz when `sw` (an LDS stage laid
+// out by it) -- one writer for the staged and the direct path (two inlined writers took the write
+// pass from 52 to 84 VGPRs); otherwise base is the line's first byte.
 template <bool W, bool SWZ = false>
 struct OutT {
   char* base;   // the line's first byte (W), or the stage (SWZ)
@@ -57,12 +58,15 @@ struct OutT {
   uint32_t n = 0;
   uint32_t acc = 0;
   uint32_t lo = 0;
+  bool sw = false;
   __device__ __forceinline__ explicit OutT(char* p) : base(p), mis(W ? (uint32_t)((uintptr_t)p & 3u) : 0u) {}
-  __device__ __forceinline__ OutT(char* stage, uint32_t line_off) : base(stage), mis(line_off & 3u), lo(line_off) {}
+  // (base 4-byte aligned)
+  __device__ __forceinline__ OutT(char* b, uint32_t line_off, bool swz)
+      : base(b), mis(line_off & 3u), lo(line_off), sw(swz) {}
   __device__ __forceinline__ char* at(uint32_t x) const {
     if constexpr (SWZ) {
       const uint32_t b = lo + x;
-      return base + (stage_swz(b >> 2) << 2) + (b & 3u);
+      return base + (sw ? (stage_swz(b >> 2) << 2) + (b & 3u) : b);
     } else {
       return base + x;
     }

@@ -1126,11 +1126,11 @@ class Engine {
   char* h_fmt_ring_[FMT_RING] = {};
   size_t h_fmt_ring_cap_[FMT_RING] = {};
   int fmt_ring_k_ = 0;  // stats thread
-  // K12's LDS stage: bytes of a 64-line block of the longer stream in the last batch, x1.25
+  // K12's LDS stage: bytes of an average 64-line block of the longer stream in the last batch
   std::atomic<uint32_t> fmt_block_bytes_{0};
   void note_fmt_block(size_t st_bytes, size_t st_lines, size_t fs_bytes, size_t fs_lines) {
     const size_t a = std::max(st_lines ? st_bytes / st_lines : 0, fs_lines ? fs_bytes / fs_lines : 0);
-    if (a) fmt_block_bytes_.store((uint32_t)std::min<size_t>(a * 80 + 64, 1u << 20), std::memory_order_relaxed);
+    if (a) fmt_block_bytes_.store((uint32_t)std::min<size_t>(a * 64, 1u << 20), std::memory_order_relaxed);
   }
   int fmt_k_ = 0;
   uint32_t* h_fmt_meta_ = nullptr;               // pinned: per slot k, [4k] st total, [4k+1] fs total
