@@ -24,8 +24,8 @@ namespace apm {
 
 namespace {
 
-template <class O>
-__device__ __forceinline__ void head(O& o, bool st, const FormatArgs& a, int32_t s) {
+template <bool W>
+__device__ __forceinline__ void head(OutT<W>& o, bool st, const FormatArgs& a, int32_t s) {
   if (st) o.lit("st|"); else o.lit("fs|");
   o.sb(a.ts_wire, a.ts_wire_len);
   const int4 nm = a.series_names[s];
@@ -36,8 +36,8 @@ __device__ __forceinline__ void head(O& o, bool st, const FormatArgs& a, int32_t
 }
 
 // st line of emission position i (empty for a series without a tx yet)
-template <class O>
-__device__ __forceinline__ void st_line(const FormatArgs& a, int32_t i, O& st, bool& fb) {
+template <bool W>
+__device__ __forceinline__ void st_line(const FormatArgs& a, int32_t i, OutT<W>& st, bool& fb) {
   const int32_t s = a.perm[i];
   const WinStat w = a.win[s];
   if (!w.active) return;
@@ -50,8 +50,8 @@ __device__ __forceinline__ void st_line(const FormatArgs& a, int32_t i, O& st, b
 
 // fs line j = (emission position i, LAG rank li): lines of one series are consecutive, LAGs
 // ascending (FullStatEntry per LAG, stream_calc_z_score.js:282-306)
-template <class O>
-__device__ __forceinline__ void fs_line(const FormatArgs& a, int32_t j, O& fs, bool& fb) {
+template <bool W>
+__device__ __forceinline__ void fs_line(const FormatArgs& a, int32_t j, OutT<W>& fs, bool& fb) {
   const int32_t i = j / a.n_lags, li = j - i * a.n_lags;
   const int32_t s = a.perm[i];
   const WinStat w = a.win[s];
@@ -142,12 +142,15 @@ __global__ __launch_bounds__(256) void k_format_len(FormatArgs a) {
 // (very long names) writes its lines to HBM directly.
 constexpr int FMT_WAVE_LINES = 64;
 // Stage size: 8 / 12 / 16 / 24 KB by the bytes of an average 64-line block of the previous
-// batch's longer stream (FormatArgs::stage_hint); LDS occupancy sets the pace of this
-// latency-bound formatter (odd-pitch per-line slots needed 16 KB where this layout fits 12 KB:
-// 108 vs 47 us per batch, profiles/r5_s vs r5_o).  A fixed 8 KB stage held only st blocks:
-// 64 fs wire lines (~150 B) are ~9.6 KB, so nearly every fs block wrote to HBM directly (46 of 7233
-// LDS instructions per dispatch, profiles/r5_n); 12 KB: the write pass 75 -> 47 us per batch,
-// 16 KB (fewer blocks per CU) 77 us (profiles/r5_o).  APM_FMT_STAGE=0 / 8 / 12 / 16 / 24 forces one.
+// batch's longer stream (FormatArgs::stage_hint); a block a little over the stage writes to HBM
+// directly -- the next size up costs occupancy on every block (this latency-bound writer runs
+// LDS-limited).  A fixed 8 KB stage held only st blocks: 64 fs wire lines (~150 B) are ~9.6 KB,
+// so nearly every fs block wrote to HBM directly (46 of 7233 LDS instructions per dispatch,
+// profiles/r5_n); 12 KB: the write pass 75 -> 47 us per batch, 16 KB 77 us (profiles/r5_o).
+// Stage layouts that avoid the stores' bank conflicts (odd-pitch per-line slots, rows rotated by
+// index: 0.6-0.7 conflict cycles per LDS instruction against 5.1-6.6 here) measured slower: more
+// LDS per block, or computed store addresses (no immediate offsets) that took the writer from 105
+// to 162 VGPRs (profiles/r5_q .. r5_u).  APM_FMT_STAGE=0 / 8 / 12 / 16 / 24 forces one.
 constexpr uint32_t FMT_LDS = 8192;
 
 __device__ __forceinline__ void wave_copy_out(const char* __restrict__ lds, char* __restrict__ out, uint32_t g0,
@@ -175,33 +178,17 @@ __global__ __launch_bounds__(FMT_WAVE_LINES) void k_format_write(FormatArgs a, i
   const int32_t j = j0 + (int32_t)threadIdx.x;
   const uint32_t* off = is_st ? a.st_off : a.fs_off;
   char* out = is_st ? a.st_out : a.fs_out;
-  const uint32_t g0 = off[j0], g1 = off[j1], a0 = g0 & ~3u;
-  // (LDS is a multiple of the 128-byte swizzle row: every rotated dword stays inside the stage)
-  const bool lds = LDS != 0 && (g1 - a0) <= LDS;  // uniform across the block
+  const uint32_t g0 = off[j0], g1 = off[j1];
+  const bool lds = LDS != 0 && (g1 - (g0 & ~3u)) <= LDS;  // uniform across the block
   if (j < j1) {
     bool fb = false;
-    // staged: the output's bytes from a0, each 32-dword row rotated by its index (stage_swz): 64
-    // lines of one length started on few banks in the plain layout -- an 8-way conflict for
-    // 160-byte lines, 5.1-6.6 conflict cycles per LDS instruction (profiles/r5_p)
-    OutT<true, true> o(lds ? stage : out, lds ? off[j] - a0 : off[j], lds);
+    OutT<true> o(lds ? stage + (off[j] - (g0 & ~3u)) : out + off[j]);
     if (is_st) st_line(a, j, o, fb);
     else fs_line(a, j, o, fb);
     o.finish();
   }
-  if (!lds) return;
   __syncthreads();
-  // copy-out: each 32-lane group reads one whole row (32 distinct banks), contiguous stores
-  const uint32_t nd = (g1 - a0 + 3u) >> 2;
-  for (uint32_t t = threadIdx.x; t < nd; t += FMT_WAVE_LINES) {
-    const uint32_t v = *reinterpret_cast<const uint32_t*>(stage + 4u * stage_swz(t));
-    const uint32_t ga = a0 + 4u * t;
-    if (ga >= g0 && ga + 4u <= g1) {
-      *reinterpret_cast<uint32_t*>(out + ga) = v;
-    } else {  // the block's first / last dword is shared with a neighbour: byte stores
-      for (uint32_t b = 0; b < 4; ++b)
-        if (ga + b >= g0 && ga + b < g1) out[ga + b] = (char)(v >> (8u * b));
-    }
-  }
+  if (lds) wave_copy_out(stage, out, g0, g1);
 }
 
 // ---- fb: fleet baseline rows ------------------------------------------------------------
@@ -400,8 +387,6 @@ void apm_format_write(FormatArgs* a, hipStream_t stream) {
     const char* e = std::getenv("APM_FMT_STAGE");  // diagnostic: stage KB (0 = no LDS stage)
     return e ? std::atoi(e) : -1;
   }();
-  // (a block a little over the stage writes straight to HBM: the next size down costs occupancy
-  // on every block -- 12 KB beat 16 KB on 64 COPY rows of ~190 B, profiles/r5_o)
   const uint32_t want = forced >= 0 ? (uint32_t)forced * 1024u : (a->stage_hint ? a->stage_hint : 12288u);
   if (forced == 0)
     hipLaunchKernelGGL(k_format_write<0>, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, st_blocks);

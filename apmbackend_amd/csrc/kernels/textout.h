@@ -43,40 +43,19 @@ __device__ __noinline__ static uint32_t text_big_fixed(char* buf, bool neg, doub
 // line, which it shares with its neighbours' lines, are written bytewise.  (One ds_write_b8 per
 // character from 64 lanes ~300 B apart was the write pass's cost: 8.65 LDS bank-conflict cycles
 // per instruction, profiles/r2_pmc_kernels.md.)
-// LDS stage swizzle (format.hip K12): dword t of a stage sits at t's 32-dword row, rotated by the
-// row index -- a line's dwords keep their row, consecutive dwords of a row stay on distinct banks,
-// and lines of one length no longer start on the same few banks.
-__device__ __forceinline__ uint32_t stage_swz(uint32_t t) { return (t & ~31u) | ((t + (t >> 5)) & 31u); }
-
-// SWZ = true: byte x of the line is base + lo + x, through stage_swz when `sw` (an LDS stage laid
-// out by it) -- one writer for the staged and the direct path (two inlined writers took the write
-// pass from 52 to 84 VGPRs); otherwise base is the line's first byte.
-template <bool W, bool SWZ = false>
+template <bool W>
 struct OutT {
-  char* base;   // the line's first byte (W), or the stage (SWZ)
-  uint32_t mis; // the line's offset inside its dword
+  char* base;   // the line's first byte (W)
+  uint32_t mis; // base's offset inside its dword
   uint32_t n = 0;
   uint32_t acc = 0;
-  uint32_t lo = 0;
-  bool sw = false;
   __device__ __forceinline__ explicit OutT(char* p) : base(p), mis(W ? (uint32_t)((uintptr_t)p & 3u) : 0u) {}
-  // (base 4-byte aligned)
-  __device__ __forceinline__ OutT(char* b, uint32_t line_off, bool swz)
-      : base(b), mis(line_off & 3u), lo(line_off), sw(swz) {}
-  __device__ __forceinline__ char* at(uint32_t x) const {
-    if constexpr (SWZ) {
-      const uint32_t b = lo + x;
-      return base + (sw ? (stage_swz(b >> 2) << 2) + (b & 3u) : b);
-    } else {
-      return base + x;
-    }
-  }
   __device__ __forceinline__ void store_dword() {
     // acc holds the dword ending at byte n - 1 (absolute alignment)
     if (n >= 4) {
-      *reinterpret_cast<uint32_t*>(at(n - 4)) = acc;
+      *reinterpret_cast<uint32_t*>(base + n - 4) = acc;
     } else {  // the line's first dword is shared with the previous line
-      for (uint32_t b = 0; b < n; ++b) *at(b) = (char)(acc >> (8u * ((mis + b) & 3u)));
+      for (uint32_t b = 0; b < n; ++b) base[b] = (char)(acc >> (8u * ((mis + b) & 3u)));
     }
     acc = 0;
   }
@@ -96,7 +75,7 @@ struct OutT {
     const uint32_t k = (mis + n) & 3u;
     if (k == 0) return;
     const uint32_t b0 = n > k ? n - k : 0;
-    for (uint32_t b = b0; b < n; ++b) *at(b) = (char)(acc >> (8u * ((mis + b) & 3u)));
+    for (uint32_t b = b0; b < n; ++b) base[b] = (char)(acc >> (8u * ((mis + b) & 3u)));
   }
   // Bytes from memory: one aligned 16-byte load per 16 bytes (the block around src), so a lane
   // waits on memory once per 16 characters instead of once per character.  The load may touch
