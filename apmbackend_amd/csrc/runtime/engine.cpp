@@ -1471,12 +1471,20 @@ void Engine::flush() {
     node_alerts_ = 0;
   }
   {
+    // one export kernel into the spare words of the pinned format meta block ([8, 15)): three
+    // pageable hipMemcpyAsync round trips were part of every drain
     unsigned long long u[3] = {0, 0, 0};
     int32_t fb = 0;
-    if (dev()) HIP_OK(hipMemcpyAsync(&u[0], d_unmapped_, 8, hipMemcpyDeviceToHost, stream_));
-    HIP_OK(hipMemcpyAsync(&u[1], d_spill_drop_, 16, hipMemcpyDeviceToHost, stream_));
-    HIP_OK(hipMemcpyAsync(&fb, d_fmt_fallback_, 4, hipMemcpyDeviceToHost, stream_));
+    ExportArgs ex{};
+    if (dev()) ex.add(d_unmapped_, hd_fmt_meta_ + 8, 8);
+    ex.add(d_spill_drop_, hd_fmt_meta_ + 10, 8);
+    ex.add(d_spill_drop_ + 1, hd_fmt_meta_ + 12, 8);
+    ex.add(d_fmt_fallback_, hd_fmt_meta_ + 14, 4);
+    apm_export(&ex, stream_);
     HIP_OK(hipStreamSynchronize(stream_));
+    if (dev()) std::memcpy(&u[0], h_fmt_meta_ + 8, 8);
+    std::memcpy(&u[1], h_fmt_meta_ + 10, 16);
+    std::memcpy(&fb, h_fmt_meta_ + 14, 4);
     metrics_.series_overflow_tx = u[0];
     metrics_.spill_dropped = u[1];
     metrics_.nan_windows_clipped = u[2];
