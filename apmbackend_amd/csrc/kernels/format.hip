@@ -243,18 +243,24 @@ __device__ __forceinline__ uint32_t fleet_row(const FleetFormatArgs& a, int32_t 
   return o.n;
 }
 
-// One pass (was: length kernel + rocprim scan + write kernel, three launches of ~80 blocks that
-// left most CUs idle): one wave per 64 rows counts its rows' bytes, scans them across lanes, gets
-// its byte offset from the waves before it by a decoupled look-back over epoch-tagged status
-// words (blocks start in index order, so a wave only ever waits for a wave that is running or
-// done), formats its rows into an LDS stage laid out like the output and copies the stage out
-// with dword stores.  Status word: flag (bits 62-63: 1 = the wave's own total, 2 = inclusive
-// prefix) | epoch (bits 32-61) | bytes (bits 0-31).
+// Two passes, no scan launch and no look-back: k_fleet_len stores each 64-row wave's byte total;
+// k_fleet_rows has every wave add up the totals before it (<= a few hundred words, 64 lanes at a
+// time), scan its own rows across lanes, format them into an LDS stage laid out like the output
+// and copy the stage out with dword stores.  (Round 4's one-pass decoupled look-back made each wave
+// wait for its predecessor's inclusive prefix: on the lowest-priority stream, behind other
+// streams' waves, a serial chain of 313 waves -- 100-240 us for ~1.3 MB, ~13 GB/s,
+// profiles/r5_n / r5_o timeline.)
 constexpr uint32_t FLEET_LDS = 16384;
-constexpr unsigned long long FST_AGG = 1ull << 62, FST_INC = 2ull << 62;
 
-__device__ __forceinline__ unsigned long long fleet_status(uint32_t epoch, unsigned long long flag, uint32_t v) {
-  return flag | ((unsigned long long)(epoch & 0x3fffffffu) << 32) | v;
+__global__ __launch_bounds__(FMT_WAVE_LINES) void k_fleet_len(FleetFormatArgs a) {
+  const int32_t n = a.n_slots * a.n_lags;
+  const int32_t i = (int32_t)blockIdx.x * FMT_WAVE_LINES + (int32_t)threadIdx.x;
+  bool fb = false;
+  uint32_t len = i < n ? fleet_row<false>(a, i, nullptr, fb) : 0u;
+  if (fb) atomicAdd(a.fallback, 1);  // (counted here only)
+#pragma unroll
+  for (int d = FMT_WAVE_LINES / 2; d > 0; d >>= 1) len += __shfl_xor(len, d, FMT_WAVE_LINES);
+  if (threadIdx.x == 0) a.status[blockIdx.x] = len;
 }
 
 __global__ __launch_bounds__(FMT_WAVE_LINES) void k_fleet_rows(FleetFormatArgs a) {
@@ -272,38 +278,15 @@ __global__ __launch_bounds__(FMT_WAVE_LINES) void k_fleet_rows(FleetFormatArgs a
     if (lane >= d) inc += y;
   }
   const uint32_t total = __shfl(inc, FMT_WAVE_LINES - 1, FMT_WAVE_LINES);
-  // look-back: lane 0 publishes the wave's total, then sums its predecessors'
+  // the waves before this one
   uint32_t prefix = 0;
-  if (lane == 0) {
-    const uint32_t b = blockIdx.x;
-    const unsigned long long ep = (unsigned long long)(a.epoch & 0x3fffffffu);
-    if (b == 0) {
-      __hip_atomic_store(&a.status[0], fleet_status(a.epoch, FST_INC, total), __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __hip_atomic_store(&a.status[b], fleet_status(a.epoch, FST_AGG, total), __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      for (int32_t j = (int32_t)b - 1; j >= 0;) {
-        const unsigned long long w =
-            __hip_atomic_load(&a.status[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        if (((w >> 32) & 0x3fffffffull) != ep || (w >> 62) == 0) {
-          __builtin_amdgcn_s_sleep(1);  // wave j has not published yet (it is running)
-          continue;
-        }
-        prefix += (uint32_t)w;
-        if ((w >> 62) == 2) break;
-        --j;
-      }
-      __hip_atomic_store(&a.status[b], fleet_status(a.epoch, FST_INC, prefix + total), __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (b == gridDim.x - 1) *a.total = prefix + total;
-  }
-  prefix = __shfl(prefix, 0, FMT_WAVE_LINES);
+  for (uint32_t k = (uint32_t)lane; k < blockIdx.x; k += FMT_WAVE_LINES) prefix += (uint32_t)a.status[k];
+#pragma unroll
+  for (int d = FMT_WAVE_LINES / 2; d > 0; d >>= 1) prefix += __shfl_xor(prefix, d, FMT_WAVE_LINES);
+  if (blockIdx.x == gridDim.x - 1 && lane == 0) *a.total = prefix + total;
   const uint32_t g0 = prefix, g1 = prefix + total;
   const uint32_t off = prefix + inc - len;
   const bool lds = (g1 - (g0 & ~3u)) <= FLEET_LDS;  // uniform across the wave
-  if (fb) atomicAdd(a.fallback, 1);  // (counted once, from the length pass)
   bool fb2 = false;
   if (i < n && len) fleet_row<true>(a, i, lds ? stage + (off - (g0 & ~3u)) : a.out + off, fb2);
   __syncthreads();
@@ -367,14 +350,16 @@ uint32_t apm_fleet_format_blocks(int32_t n_rows) {
   return (uint32_t)((std::max<int32_t>(n_rows, 1) + FMT_WAVE_LINES - 1) / FMT_WAVE_LINES);
 }
 
-// one launch; afterwards *a->total holds the bytes written (device)
+// two launches; afterwards *a->total holds the bytes written (device)
 void apm_fleet_format(FleetFormatArgs* a, hipStream_t stream) {
   const int32_t n = a->n_slots * a->n_lags;
   if (n <= 0) {
     HIP_OK(hipMemsetAsync(a->total, 0, 4, stream));
     return;
   }
-  hipLaunchKernelGGL(k_fleet_rows, dim3(apm_fleet_format_blocks(n)), dim3(FMT_WAVE_LINES), 0, stream, *a);
+  const dim3 grid(apm_fleet_format_blocks(n));
+  hipLaunchKernelGGL(k_fleet_len, grid, dim3(FMT_WAVE_LINES), 0, stream, *a);
+  hipLaunchKernelGGL(k_fleet_rows, grid, dim3(FMT_WAVE_LINES), 0, stream, *a);
 }
 
 void apm_format_write(FormatArgs* a, hipStream_t stream) {

@@ -162,8 +162,8 @@ struct FleetFormatArgs {
   int32_t copy;            // 1: Postgres COPY rows (apm_fleet_stats), 0: fb wire lines
   int32_t ts_len;
   char ts[32];
-  unsigned long long* status;  // [blocks] look-back state of the one-pass offsets (epoch-tagged)
-  uint32_t epoch;          // != 0, new per launch: stale status words never match
+  unsigned long long* status;  // [blocks] each 64-row wave's byte total (k_fleet_len)
+  uint32_t epoch;          // (unused since the look-back went; kept for the struct layout)
   uint32_t* total;         // bytes written (device)
   char* out;
   int32_t* fallback;
