@@ -488,49 +488,43 @@ __global__ __launch_bounds__(TB) void k_host_flags(const Event* __restrict__ ev,
                                                    AudF* __restrict__ aud, SelCount* __restrict__ totals, uint32_t cap,
                                                    int bytewise, int staged) {
   __shared__ __attribute__((aligned(16))) uint8_t stage[TB * HF_PITCH];
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t n = min(*n_ev_dev, cap);
-  // A fixed grid (apm_dj_select_host: <= 512 blocks, one round at 2 per CU) striding over the
-  // batch's events by wave, consecutive 64-event chunks on different blocks: sized for the
-  // capacity (maxLinesPerBatch / 256 blocks of 68 KB LDS each) most blocks only exited, at 2
-  // resident per CU, and the events sat on the first ~n / 256 CUs.
-  const uint32_t lane = threadIdx.x & (APM_WAVE - 1);
-  const uint32_t stride = gridDim.x * (blockDim.x / APM_WAVE);
+  if (blockIdx.x * blockDim.x >= n) return;  // (uniform per block: the grid is sized for the capacity)
+  uint8_t fl = 0;
   uint32_t ab = 0;
-  for (uint32_t w = (threadIdx.x / APM_WAVE) * gridDim.x + blockIdx.x; w * APM_WAVE < n; w += stride) {
-    const uint32_t i = w * APM_WAVE + lane;
-    uint8_t fl = 0;
-    if (i < n) {
-      const Event e = ev[i];
-      const uint64_t fkey = e.kind == LK_APP ? file_fkey[chunk_file[e.chunk]] : 0;
-      // (staging only decides where the walk reads: a staged line is a complete copy, so the field
-      // functions -- which read bytes only in the cases hf_needs_bytes names -- are unchanged)
-      const uint8_t* p = bytes + e.off;
-      const uint32_t lead = e.off & 15u;
-      const uint32_t nvec = (lead + e.len + 15u) >> 4;
-      if (staged && hf_needs_bytes(e) && nvec * 16u <= (uint32_t)HF_SLOT) {
-        // the line's aligned 16-byte blocks, every load issued before the first LDS store (the
-        // slot is this lane's own: no barrier between strides)
-        const uint4* __restrict__ src = reinterpret_cast<const uint4*>(bytes + (e.off - lead));
-        uint4* dst = reinterpret_cast<uint4*>(stage + threadIdx.x * HF_PITCH);
-        uint4 v[HF_SLOT / 16];
+  if (i < n) {
+    const Event e = ev[i];
+    const uint64_t fkey = e.kind == LK_APP ? file_fkey[chunk_file[e.chunk]] : 0;
+    // (staging only decides where the walk reads: a staged line is a complete copy, so the field
+    // functions -- which read bytes only in the cases hf_needs_bytes names -- are unchanged)
+    const uint8_t* p = bytes + e.off;
+    const uint32_t lead = e.off & 15u;
+    const uint32_t nvec = (lead + e.len + 15u) >> 4;
+    if (staged && hf_needs_bytes(e) && nvec * 16u <= (uint32_t)HF_SLOT) {
+      // the line's aligned 16-byte blocks, every load issued before the first LDS store
+      const uint4* __restrict__ src = reinterpret_cast<const uint4*>(bytes + (e.off - lead));
+      uint4* dst = reinterpret_cast<uint4*>(stage + threadIdx.x * HF_PITCH);
+      uint4 v[HF_SLOT / 16];
 #pragma unroll
-        for (int k = 0; k < HF_SLOT / 16; ++k)
-          if ((uint32_t)k < nvec) v[k] = src[k];
+      for (int k = 0; k < HF_SLOT / 16; ++k)
+        if ((uint32_t)k < nvec) v[k] = src[k];
 #pragma unroll
-        for (int k = 0; k < HF_SLOT / 16; ++k)
-          if ((uint32_t)k < nvec) dst[k] = v[k];
-        p = stage + threadIdx.x * HF_PITCH + lead;
-      }
-      fl = hf_fields(e, p, fkey, aud, i, bytewise);
-      if (e.kind == LK_APP) {
-        if (e.mask & PM_AUTR_MAP) fl |= SEL_MH;
-        else fl |= SEL_WALK | ((e.mask & PM_AUTR_HDR) ? SEL_MH : 0);
-        if (e.mask & (PM_AUTR_MAP | PM_SW_NAME)) ab += e.len;
-      }
-      flag[i] = fl;
-      val[i] = (uint64_t)(fl & SEL_HOST) | ((fl & SEL_MH) ? 1ull << SEL_MH_SHIFT : 0ull) |
-               ((fl & SEL_WALK) ? 1ull << SEL_WALK_SHIFT : 0ull);
+      for (int k = 0; k < HF_SLOT / 16; ++k)
+        if ((uint32_t)k < nvec) dst[k] = v[k];
+      p = stage + threadIdx.x * HF_PITCH + lead;
     }
+    fl = hf_fields(e, p, fkey, aud, i, bytewise);
+    if (e.kind == LK_APP) {
+      if (e.mask & PM_AUTR_MAP) fl |= SEL_MH;
+      else fl |= SEL_WALK | ((e.mask & PM_AUTR_HDR) ? SEL_MH : 0);
+      if (e.mask & (PM_AUTR_MAP | PM_SW_NAME)) ab = e.len;
+    }
+  }
+  if (i < n) {
+    flag[i] = fl;
+    val[i] = (uint64_t)(fl & SEL_HOST) | ((fl & SEL_MH) ? 1ull << SEL_MH_SHIFT : 0ull) |
+             ((fl & SEL_WALK) ? 1ull << SEL_WALK_SHIFT : 0ull);
   }
   // bytes of map / stopWatch-name lines: one atomic per wave (totals zeroed before the launch)
   for (int o = APM_WAVE / 2; o > 0; o >>= 1) ab += __shfl_xor(ab, o, APM_WAVE);
@@ -2501,8 +2495,7 @@ static int hf_staged() {
 int apm_dj_select_host(DJArgs* a, const uint32_t* d_n_ev, uint32_t max_ev, hipStream_t s) {
   HIP_OK(hipMemsetAsync(a->n_host, 0, sizeof(SelCount), s));
   if (max_ev == 0) return 0;
-  hipLaunchKernelGGL(k_host_flags, dim3(std::min<uint32_t>((max_ev + TB - 1) / TB, 512u)), dim3(TB), 0, s, a->ev, d_n_ev,
-                     a->bytes, a->chunk_file,
+  hipLaunchKernelGGL(k_host_flags, dim3((max_ev + TB - 1) / TB), dim3(TB), 0, s, a->ev, d_n_ev, a->bytes, a->chunk_file,
                      a->file_fkey,
                      a->host_flag, a->sel_val, a->aud, a->n_host, max_ev, pre_bytewise(), hf_staged());
   dj_check(s, "k_host_flags");
