@@ -1005,16 +1005,19 @@ int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& e
   job->extra = extra;
   job->pre_commit = std::move(pre_commit);
   {
-    // the small sections' device reads become D2D copies into HBM staging (sized by the previous
-    // snapshot's want; a read that does not fit is done synchronously, as before)
+    // the small sections' device reads become D2D copies into HBM staging (1.5x the previous
+    // snapshot's want, at least 1 GiB -- the process's first snapshot has no previous want and
+    // read everything synchronously: 34-36 ms stalls, profiles/r5_final2; a read that does not
+    // fit is still done synchronously)
     CkDefer def;
-    if (ck_defer_want_ > ck_defer_cap_) {
+    constexpr size_t kMinStage = (size_t)1 << 30;
+    if (ck_defer_want_ > ck_defer_cap_ || !d_ck_defer_) {
       if (d_ck_defer_) {
         HIP_OK(hipFree(d_ck_defer_));
         std::lock_guard<std::mutex> g(alloc_mu_);
         device_bytes_ -= ck_defer_cap_;
       }
-      const size_t cap = ck_defer_want_ + ck_defer_want_ / 4;
+      const size_t cap = std::max(ck_defer_want_ + ck_defer_want_ / 2, kMinStage);
       if (hipMalloc((void**)&d_ck_defer_, cap) != hipSuccess) {
         (void)hipGetLastError();
         d_ck_defer_ = nullptr;
