@@ -227,6 +227,22 @@ class AlertNotifier:
     def _ac(self):
         return self.cfg["streamProcessAlerts"]
 
+    def send_test_email(self):
+        """sendTestEmail at alerts-module start (stream_process_alerts.js:54-56,597): the
+        reference's only "is mail working" probe, sent to ``testEmailList`` on every start
+        (``emailsEnabled`` is not consulted there either).  ``sendTestEmailOnStart: false`` in
+        the ``streamProcessAlerts`` section turns it off (new key)."""
+        ac = self._ac()
+        if not as_bool(ac.get("sendTestEmailOnStart", True)):
+            return None
+        try:
+            return self.mailer.send(ac.get("fromEmail", "apm@localhost"),
+                                    ac.get("testEmailList", ac.get("emailList", "")),
+                                    "Test APM alert email", "If you get this email, emails are working!")
+        except Exception as e:  # a broken mailer must not stop the engine
+            log.error("test e-mail failed: %s", e)
+            return None
+
     def reload(self, cfg):
         self.cfg = cfg
         self.base = self._ac()["alertCollectionIntervalInSeconds"]

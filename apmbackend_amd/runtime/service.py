@@ -271,6 +271,9 @@ class IngestService:
         elif self.mode != "none":
             raise ValueError(f"unknown gpu.outputMode {self.mode!r}")
         self.notifier = AlertNotifier(self.cfg, clock=clock) if self.rank == 0 or self.world == 1 else None
+        if self.notifier is not None:  # the alerts module's startup probe (stream_process_alerts.js:597)
+            import threading
+            threading.Thread(target=self.notifier.send_test_email, name="apm-test-email", daemon=True).start()
 
         # ---- input queue (inputMode transactions)
         self.in_qm = None

@@ -48,7 +48,7 @@ GPU_DEFAULTS: Dict[str, Any] = {
     "zscoreSigma": "sqrt_mean",       # sqrt_mean (reference quirk Q1) | stddev (true sigma)
     "exactRecomputeEveryIntervals": 360,
     "emulateOverrideAliasing": False,  # quirk Q4 (per-service overrides leak into defaults)
-    "alertClock": "entry",            # entry (log time, deterministic) | wall (reference)
+    "alertClock": "wall",             # wall (reference: stream_process_alerts.js:437,449-467) | entry (log time: replay)
     "cooldownKey": "service",         # service (reference Q7) | series
     "recordTtlSeconds": 120,          # recordCache stdTTL (stream_parse_transactions.js:215)
     "acctTtlSeconds": 120,            # acctCache stdTTL (:213)
@@ -132,9 +132,15 @@ def as_bool(v: Any) -> bool:
     return bool(v)
 
 
-def default_config() -> Dict[str, Any]:
+def default_config(replay: bool = False) -> Dict[str, Any]:
+    """The shipped config.  ``replay=True`` switches the alert clock to log time
+    (``gpu.alertClock = "entry"``): alert timestamps and cooldowns then depend only on the input,
+    which is what replays, benchmarks and oracle comparisons need.  The shipped default is the
+    reference's wall clock."""
     cfg = read_apm_config(DEFAULT_CONFIG_PATH)
     assert cfg is not None
+    if replay:
+        cfg["gpu"]["alertClock"] = "entry"
     return cfg
 
 

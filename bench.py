@@ -178,7 +178,7 @@ def main():
 
     N = _native.load(build_if_missing=False)
     n_services = args.ejb + args.providers
-    cfg = default_config()
+    cfg = default_config(replay=True)
     cfg["gpu"].update({
         "timezone": "UTC",
         "maxSeries": args.max_series or max(4096, 1 << (args.servers * n_services - 1).bit_length()),

@@ -77,7 +77,7 @@ from apmbackend_amd import _native
 from apmbackend_amd.models.pipeline import APMEngine
 from apmbackend_amd.utils.config import default_config
 N = _native.load(build_if_missing=False)
-C = default_config()
+C = default_config(replay=True)
 C["gpu"].update({"maxSeries": 4096, "batchBytes": 1 << 20, "maxLinesPerBatch": 1 << 14,
                  "collectiveInitTimeoutSeconds": 6})
 eng = APMEngine(C, device=0)

@@ -43,7 +43,7 @@ def corpus():
 
 
 def cfg():
-    C = default_config()
+    C = default_config(replay=True)
     C["streamCalcZScore"]["defaults"] = [{"LAG": 6, "THRESHOLD": 3.0, "INFLUENCE": 0.5}]
     C["streamProcessAlerts"]["rollingAlertWindowSizeInIntervals"] = 5
     C["streamProcessAlerts"]["requiredNumberBadIntervalsInAlertWindowToTrigger"] = 2

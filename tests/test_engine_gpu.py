@@ -31,7 +31,7 @@ START = 1578391200000
 
 
 def small_cfg(mode="exact"):
-    C = default_config()
+    C = default_config(replay=True)
     C["streamCalcZScore"]["defaults"] = [{"LAG": 6, "THRESHOLD": 3.0, "INFLUENCE": 0.5},
                                          {"LAG": 30, "THRESHOLD": 2.0, "INFLUENCE": 0.0}]
     C["streamCalcZScore"]["overrides"]["services"]["S:getSvc0002"] = {"6": {"THRESHOLD": 4.0, "INFLUENCE": 0.25}}

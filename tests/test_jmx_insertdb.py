@@ -24,7 +24,7 @@ class Clock:
 
 
 def test_poller_emits_jx_records_aligned_to_interval():
-    C = default_config()
+    C = default_config(replay=True)
     C["pullJvmStats"]["jvmHosts"] = ["jvm1.example.com", "jvm2.example.com", "down.example.com"]
     got = []
     syn = jmx.SyntheticJmx(3)
@@ -51,7 +51,7 @@ def test_poller_emits_jx_records_aligned_to_interval():
 def test_insert_db_process_consumes_queue():
     b = Broker(port=0).start()
     try:
-        C = default_config()
+        C = default_config(replay=True)
         C["amqpConnectionString"] = b.url
         C["apmConfigFilePath"] = None
         C["streamInsertDb"]["bufferResumeFileFullPath"] = None

@@ -34,7 +34,7 @@ START = 1578391200000
 
 
 def node_cfg():
-    C = default_config()
+    C = default_config(replay=True)
     C["streamCalcZScore"]["defaults"] = [{"LAG": 6, "THRESHOLD": 3.0, "INFLUENCE": 0.5},
                                          {"LAG": 30, "THRESHOLD": 2.0, "INFLUENCE": 0.0}]
     C["streamProcessAlerts"]["rollingAlertWindowSizeInIntervals"] = 5
@@ -288,7 +288,7 @@ def test_peer_process_death_aborts_the_group_and_supervisor_resumes_from_checkpo
     from apmbackend_amd.utils.config import default_config
     P = _oracle()
     out = str(tmp_path / "node")
-    C = default_config()
+    C = default_config(replay=True)
     C["logDir"] = str(tmp_path / "logs")
     C["appDirectory"] = FIX
     C["apmConfigFilePath"] = None
@@ -375,7 +375,7 @@ def test_elastic_degrade_keeps_state_across_the_world_change(tmp_path):
     from apmbackend_amd.utils.config import default_config
     P = _oracle()
     out = str(tmp_path / "node")
-    C = default_config()
+    C = default_config(replay=True)
     C["logDir"] = str(tmp_path / "logs")
     C["appDirectory"] = FIX
     C["apmConfigFilePath"] = None

@@ -40,7 +40,7 @@ def test_html_table_matches_reference_layout():
 
 
 def test_grafana_urls():
-    g = default_config()["grafana"]
+    g = default_config(replay=True)["grafana"]
     alerts = [entry_from_csv(al()), entry_from_csv(al("jvm02", lag=8640, ts=1578391260000))]
     url, render = notifier.grafana_urls(alerts, now_ms=1578392000000.0, grafana=g)
     assert url.startswith(g["grafanaURL"] + g["alertInspectorRelativeURL"] + "?from=1578390900000&to=1578391560000")
@@ -52,7 +52,7 @@ def test_grafana_urls():
 
 
 def test_collection_interval_backoff_and_reset(tmp_path):
-    C = default_config()
+    C = default_config(replay=True)
     ac = C["streamProcessAlerts"]
     ac.update({"alertCollectionIntervalInSeconds": 60, "maxCollectionIntervalInSeconds": 200,
                "increaseCollectionIntervalAfterAlert": True, "emailsEnabled": "true"})
@@ -83,7 +83,7 @@ def test_collection_interval_backoff_and_reset(tmp_path):
 
 
 def test_render_failure_falls_back_to_test_list(tmp_path):
-    C = default_config()
+    C = default_config(replay=True)
     clk = Clock()
     mailer = notifier.Mailer(sendmail="/nonexistent/sendmail", outbox=str(tmp_path))
 
@@ -98,7 +98,7 @@ def test_render_failure_falls_back_to_test_list(tmp_path):
 
 
 def test_emails_disabled_string_false():
-    C = default_config()
+    C = default_config(replay=True)
     C["streamProcessAlerts"]["emailsEnabled"] = "false"
     clk = Clock()
     n = notifier.AlertNotifier(C, notifier.Mailer(sendmail="/nonexistent"), clock=clk, renderer=lambda u, g: None)
@@ -123,3 +123,25 @@ def test_daily_rolling_logger_and_pruning(tmp_path):
     for h in list(lg.handlers):
         lg.removeHandler(h)
         h.close()
+
+
+def test_startup_test_email_goes_to_test_list(tmp_path):
+    """sendTestEmail at alerts-module start (stream_process_alerts.js:54-56,597)."""
+    C = default_config(replay=True)
+    mailer = notifier.Mailer(sendmail="/nonexistent/sendmail", outbox=str(tmp_path))
+    n = notifier.AlertNotifier(C, mailer, clock=Clock(), renderer=lambda u, g: None)
+    out = n.send_test_email()
+    assert out and os.path.exists(out)
+    msg = mailer.sent[0]
+    assert msg["To"] == C["streamProcessAlerts"]["testEmailList"]
+    assert msg["Subject"] == "Test APM alert email"
+    html = [p for p in msg.walk() if p.get_content_type() == "text/html"][0].get_payload(decode=True).decode()
+    assert html == "If you get this email, emails are working!"
+    C["streamProcessAlerts"]["sendTestEmailOnStart"] = "false"
+    assert n.send_test_email() is None and len(mailer.sent) == 1
+
+
+def test_shipped_config_uses_the_reference_wall_alert_clock():
+    from apmbackend_amd.utils.config import default_config as dc
+    assert dc()["gpu"]["alertClock"] == "wall"
+    assert dc(replay=True)["gpu"]["alertClock"] == "entry"

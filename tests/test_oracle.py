@@ -47,7 +47,7 @@ def test_process_zscore_golden():
 
 
 def test_zscore_process_data_golden():
-    cfg = default_config()
+    cfg = default_config(replay=True)
     cfg["streamCalcZScore"]["defaults"] = [{"LAG": 3, "THRESHOLD": 2, "INFLUENCE": 0.5}]
     out = []
     z = ZScoreOracle(cfg, out.append)
@@ -66,18 +66,18 @@ def test_zscore_process_data_golden():
 
 
 def test_override_aliasing_emulation():
-    cfg = default_config()
+    cfg = default_config(replay=True)
     z = ZScoreOracle(cfg, lambda l: None, emulate_aliasing=True)
     z.settings("S:getLateFeeWaiver")
     assert [d["THRESHOLD"] for d in cfg["streamCalcZScore"]["defaults"]] == [25.0, 25.0]
-    cfg2 = default_config()
+    cfg2 = default_config(replay=True)
     z2 = ZScoreOracle(cfg2, lambda l: None, emulate_aliasing=False)
     z2.settings("S:getLateFeeWaiver")
     assert [d["THRESHOLD"] for d in cfg2["streamCalcZScore"]["defaults"]] == [20.0, 15.0]
 
 
 def test_alert_leaky_counter_golden():
-    cfg = default_config()
+    cfg = default_config(replay=True)
     a = AlertsOracle(cfg)
     fs = FullStatEntry.make(0, "srv", "S:x", 5, "360", 900, 100, 50, 150, 1, 900, 100, 50, 150, 1,
                             900, 100, 50, 150, 1)
@@ -143,7 +143,7 @@ def test_stats_zscore_alerts_match_reference_js():
     start = 1578391200000
     an = [Anomaly("jvm00", "getSvc0001", start + 400_000, start + 1500_000, 30.0)]
     _, bl = _synth(1, duration=1500, anomalies=an)
-    C = default_config()
+    C = default_config(replay=True)
     C["streamCalcZScore"]["defaults"] = [{"LAG": 6, "THRESHOLD": 3.0, "INFLUENCE": 0.5},
                                          {"LAG": 30, "THRESHOLD": 2.0, "INFLUENCE": 0.0}]
     C["streamCalcZScore"]["overrides"]["services"]["S:getSvc0002"] = {"6": {"THRESHOLD": 4.0, "INFLUENCE": 0.25}}
@@ -188,7 +188,7 @@ def test_stats_nan_elapsed_matches_reference_js():
     import random
     import refjs
     _, bl = _synth(2, duration=900)
-    P = PipelineOracle(default_config(), UTC)
+    P = PipelineOracle(default_config(replay=True), UTC)
     P.run_batches(bl)
     rng = random.Random(11)
     lines = []
@@ -237,7 +237,7 @@ def test_config_reload_oracle_matches_reference_js():
     start = 1578391200000
     an = [Anomaly("jvm00", "getSvc0001", start + 400_000, start + 1500_000, 30.0)]
     _, bl = _synth(1, duration=1500, anomalies=an)
-    C0 = default_config()
+    C0 = default_config(replay=True)
     C0["streamCalcZScore"]["defaults"] = [{"LAG": 6, "THRESHOLD": 3.0, "INFLUENCE": 0.5},
                                           {"LAG": 30, "THRESHOLD": 2.0, "INFLUENCE": 0.0}]
     C0["streamCalcZScore"]["overrides"]["services"]["S:getSvc0002"] = {"6": {"THRESHOLD": 4.0, "INFLUENCE": 0.25}}

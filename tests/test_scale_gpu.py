@@ -35,7 +35,7 @@ INTERVALS = 50
 
 
 def bench_cfg(mode, ring, mfma=True):
-    C = default_config()  # LAG 360 / 8640, the reference's thresholds
+    C = default_config(replay=True)  # LAG 360 / 8640, the reference's thresholds
     C["gpu"].update({"timezone": "UTC", "maxSeries": 1 << 17, "batchBytes": 48 << 20, "maxLinesPerBatch": 1 << 20,
                      "zscoreMeanMode": mode, "ringDtype": ring, "bucketCellCapacity": 16,
                      "resyncOnMatrixCores": mfma})

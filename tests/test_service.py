@@ -36,7 +36,7 @@ def make_env(tmp_path, mode="inproc", servers=2, duration=400):
     sc = SynthConfig(servers=servers, duration_s=duration, tx_per_sec_per_server=3, seed=4, ejb_services=3,
                      provider_services=2, anomalies=an)
     lines = Generator(sc).generate()
-    C = default_config()
+    C = default_config(replay=True)
     C["streamCalcZScore"]["defaults"] = [{"LAG": 6, "THRESHOLD": 3.0, "INFLUENCE": 0.5}]
     C["streamProcessAlerts"]["rollingAlertWindowSizeInIntervals"] = 5
     C["streamProcessAlerts"]["requiredNumberBadIntervalsInAlertWindowToTrigger"] = 2

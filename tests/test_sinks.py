@@ -37,7 +37,7 @@ class Clock:
 
 
 def cfg(limit=3, wait_ms=5000, resume=None):
-    C = default_config()
+    C = default_config(replay=True)
     C["streamInsertDb"]["dbInsertBufferLimit"] = limit
     C["streamInsertDb"]["dbMaxTimeBetweenInsertsMs"] = wait_ms
     C["streamInsertDb"]["bufferResumeFileFullPath"] = resume
@@ -142,7 +142,7 @@ def _oracle_stream():
     sc = SynthConfig(servers=2, duration_s=800, tx_per_sec_per_server=3, seed=11, ejb_services=3,
                      provider_services=2, anomalies=an)
     lines = Generator(sc).generate()
-    C = default_config()
+    C = default_config(replay=True)
     C["streamCalcZScore"]["defaults"] = [{"LAG": 6, "THRESHOLD": 3.0, "INFLUENCE": 0.5}]
     C["streamProcessAlerts"]["rollingAlertWindowSizeInIntervals"] = 5
     C["streamProcessAlerts"]["requiredNumberBadIntervalsInAlertWindowToTrigger"] = 2

@@ -25,7 +25,7 @@ def wait_for(pred, timeout=10.0):
 
 
 def make_cfg(tmp_path, modules, **mgr):
-    C = default_config()
+    C = default_config(replay=True)
     C["logDir"] = str(tmp_path / "logs")
     C["appDirectory"] = str(tmp_path)
     C["apmConfigFilePath"] = None
