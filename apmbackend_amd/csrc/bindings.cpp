@@ -152,6 +152,7 @@ py::dict metrics_dict(const EngineMetrics& m) {
   d["t_shard_busy_ms"] = m.t_shard_busy_ms; d["t_shard_max_ms"] = m.t_shard_max_ms;
   d["t_out_ms"] = m.t_out_ms;
   d["t_lockstep_ms"] = m.t_lockstep_ms; d["t_lockstep_max_ms"] = m.t_lockstep_max_ms;
+  d["t_lockstep_stats_ms"] = m.t_lockstep_stats_ms;
   d["db_copy_rows"] = m.db_copy_rows; d["db_copy_fallbacks"] = m.db_copy_fallbacks;
   d["t_stats_tx_ms"] = m.t_stats_tx_ms; d["t_rollover_ms"] = m.t_rollover_ms;
   d["t_format_ms"] = m.t_format_ms; d["t_release_ms"] = m.t_release_ms;

@@ -9,6 +9,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <cerrno>
 #include <thread>
 
@@ -286,24 +287,37 @@ class HostCollective final : public Collective {
       }
     }
   }
-  ~HostCollective() override { shutdown_all(); }
+  ~HostCollective() override {
+    shutdown_all();
+    for (Staged* st : pool_) {
+      if (st->done) { hipEventSynchronize(st->done); hipEventDestroy(st->done); }
+      if (st->in) hipHostFree(st->in);
+      if (st->out) hipHostFree(st->out);
+      delete st;
+    }
+  }
   int nranks() const override { return n_; }
   int rank() const override { return r_; }
 
+  // Stream-ordered like RCCL: the calling thread only enqueues.  On stream `s`: D2H of the
+  // contribution into a pinned stage, a host function (HIP's callback thread) that runs the TCP
+  // exchange, H2D of the result.  The stream -- and nothing else -- waits for the peers, so the
+  // engine's split lock-step rounds overlap the join here exactly as they do over RCCL.  Every
+  // collective of an engine is on its one collective stream, so the callbacks run in issue
+  // order on every rank.  One rank: MAX / SUM over one rank is the identity, nothing to do.
   void all_reduce_f64(double* buf, size_t n, bool max, hipStream_t s) override {
-    std::vector<double> mine(n);
-    HIP_OK(hipStreamSynchronize(s));
-    HIP_OK(hipMemcpy(mine.data(), buf, n * 8, hipMemcpyDeviceToHost));
-    const std::vector<double> out = all_reduce_host(mine, max);
-    HIP_OK(hipMemcpy(buf, out.data(), n * 8, hipMemcpyHostToDevice));
+    if (aborted_.load()) throw std::runtime_error("host collective aborted: " + error());
+    if (n_ == 1 || n == 0) return;
+    enqueue(s, max ? 1u : 2u, buf, buf, n * 8, n * 8);
   }
 
   void all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
-    std::vector<uint8_t> mine(bytes);
-    HIP_OK(hipStreamSynchronize(s));
-    HIP_OK(hipMemcpy(mine.data(), send, bytes, hipMemcpyDeviceToHost));
-    const std::vector<uint8_t> out = all_gather_host(mine);
-    HIP_OK(hipMemcpy(recv, out.data(), out.size(), hipMemcpyHostToDevice));
+    if (aborted_.load()) throw std::runtime_error("host collective aborted: " + error());
+    if (n_ == 1) {
+      if (bytes && send != recv) HIP_OK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, s));
+      return;
+    }
+    enqueue(s, 3u, send, recv, bytes, bytes * (size_t)n_);
   }
 
   // rank 0 reduces in rank order: the same bits on every rank, every run
@@ -334,15 +348,88 @@ class HostCollective final : public Collective {
     });
   }
 
-  std::string async_error() override { return aborted_ ? "host collective aborted: " + err_ : ""; }
+  std::string async_error() override { return aborted_.load() ? "host collective aborted: " + error() : ""; }
   void abort() override {
-    if (err_.empty()) err_ = "aborted";
+    {
+      std::lock_guard<std::mutex> g(err_mu_);
+      if (err_.empty()) err_ = "aborted";
+    }
     aborted_ = true;
     shutdown_all();
   }
-  bool aborted() const override { return aborted_; }
+  bool aborted() const override { return aborted_.load(); }
 
  private:
+  // pinned in / out stages, reused once the H2D that read `out` has completed (`done`)
+  struct Staged {
+    size_t cap = 0;
+    void *in = nullptr, *out = nullptr;
+    hipEvent_t done = nullptr;
+    bool used = false;
+  };
+  struct Op {
+    HostCollective* self;
+    uint32_t kind;
+    Staged* st;
+    size_t in_bytes, out_bytes;
+  };
+  Staged* stage(size_t bytes) {
+    for (Staged* st : pool_) {
+      if (st->cap < bytes) continue;
+      if (!st->used || hipEventQuery(st->done) == hipSuccess) return st;
+    }
+    Staged* st = new Staged();
+    st->cap = std::max<size_t>(4096, bytes);
+    HIP_OK(hipHostMalloc(&st->in, st->cap, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc(&st->out, st->cap * (size_t)n_, hipHostMallocDefault));
+    HIP_OK(hipEventCreateWithFlags(&st->done, hipEventDisableTiming));
+    pool_.push_back(st);
+    return st;
+  }
+  void enqueue(hipStream_t s, uint32_t kind, const void* send, void* recv, size_t in_bytes, size_t out_bytes) {
+    Staged* st = stage(in_bytes);
+    HIP_OK(hipMemcpyAsync(st->in, send, in_bytes, hipMemcpyDeviceToHost, s));
+    Op* op = new Op{this, kind, st, in_bytes, out_bytes};
+    const hipError_t e = hipLaunchHostFunc(s, &HostCollective::run_op, op);
+    if (e != hipSuccess) { delete op; HIP_OK(e); }
+    HIP_OK(hipMemcpyAsync(recv, st->out, out_bytes, hipMemcpyHostToDevice, s));
+    HIP_OK(hipEventRecord(st->done, s));
+    st->used = true;
+  }
+  // HIP callback thread: no HIP calls here.  A failure marks the communicator aborted (the
+  // engine's coll_wait sees async_error() and throws); the stream goes on with zeros.
+  static void run_op(void* p) {
+    Op* op = (Op*)p;
+    HostCollective* self = op->self;
+    try {
+      if (self->aborted_.load()) throw std::runtime_error("aborted");
+      std::vector<uint8_t> out;
+      if (op->kind == 3u) {
+        out = self->all_gather_host(std::vector<uint8_t>((uint8_t*)op->st->in, (uint8_t*)op->st->in + op->in_bytes));
+      } else {
+        std::vector<double> v(op->in_bytes / 8);
+        std::memcpy(v.data(), op->st->in, op->in_bytes);
+        const std::vector<double> r = self->all_reduce_host(v, op->kind == 1u);
+        out.resize(op->in_bytes);
+        std::memcpy(out.data(), r.data(), op->in_bytes);
+      }
+      if (out.size() != op->out_bytes) throw std::runtime_error("reply of unexpected size");
+      std::memcpy(op->st->out, out.data(), out.size());
+    } catch (const std::exception& e) {
+      {
+        std::lock_guard<std::mutex> g(self->err_mu_);
+        if (self->err_.empty()) self->err_ = e.what();
+      }
+      self->aborted_ = true;
+      std::memset(op->st->out, 0, op->out_bytes);
+    }
+    delete op;
+  }
+  std::string error() {
+    std::lock_guard<std::mutex> g(err_mu_);
+    return err_;
+  }
+
   struct Hdr { uint32_t magic, op; uint64_t seq, bytes; };
   static constexpr uint32_t kMagic = 0x41504d43;  // "APMC"
 
@@ -385,7 +472,10 @@ class HostCollective final : public Collective {
     }
   }
   [[noreturn]] void fail(const std::string& why) {
-    err_ = why;
+    {
+      std::lock_guard<std::mutex> g(err_mu_);
+      err_ = why;
+    }
     aborted_ = true;
     shutdown_all();
     throw std::runtime_error("host collective: " + why);
@@ -393,7 +483,7 @@ class HostCollective final : public Collective {
 
   template <class F>
   std::vector<uint8_t> exchange(uint32_t op, std::vector<uint8_t>&& mine, F&& combine) {
-    if (aborted_) throw std::runtime_error("host collective aborted: " + err_);
+    if (aborted_.load()) throw std::runtime_error("host collective aborted: " + error());
     const uint64_t seq = ++seq_;
     if (n_ == 1) {
       std::vector<std::vector<uint8_t>> all(1);
@@ -439,8 +529,10 @@ class HostCollective final : public Collective {
   double timeout_ms_;
   std::vector<int> fd_;  // rank 0: one per peer; others: [0] = rank 0
   uint64_t seq_ = 0;
-  bool aborted_ = false;
+  std::atomic<bool> aborted_{false};
+  std::mutex err_mu_;
   std::string err_;
+  std::vector<Staged*> pool_;  // enqueue side (the engine's ingest thread)
 };
 
 }  // namespace

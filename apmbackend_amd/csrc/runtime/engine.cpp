@@ -559,7 +559,9 @@ Engine::~Engine() {
     if (h_fb_total_) hipHostFree(h_fb_total_);
     if (fb_stream_) hipStreamDestroy(fb_stream_);
     if (node_ev_) hipEventDestroy(node_ev_);
-    if (solo_sync_ev_) hipEventDestroy(solo_sync_ev_);
+    if (clock_ev_) hipEventDestroy(clock_ev_);
+    for (hipEvent_t e : bucket_ev_)
+      if (e) hipEventDestroy(e);
     if (h_node_send_) hipHostFree(h_node_send_);
     if (h_node_recv_) hipHostFree(h_node_recv_);
     hipStreamDestroy(coll_stream_);
@@ -1042,6 +1044,7 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
 
   // ---- join on the host, one task per server shard
   const double clock = now_override >= 0 ? now_override : watermark_;
+  if (lockstep_) lockstep_issue(batch_watermark(ps));
   // Event ranges per shard without walking the events (15 MB of freshly DMA'd records): events
   // are in chunk order, so each run of same-server chunks maps to one binary-searched range.
   std::vector<std::vector<std::pair<uint32_t, uint32_t>>> shard_range(shards_.size());
@@ -1117,28 +1120,21 @@ void Engine::process_batch(const uint8_t* host_bytes, uint64_t n_bytes, const st
   trace_event("join", t1, t1b, 0);
   trace_event("handoff", t1b, t2, 0);
 
-  // advance the watermark clock (max leading timestamp seen so far)
-  const unsigned long long wm = *ps.h_watermark;
-  if (wm) {
-    const double w = (double)((long long)wm - (1LL << 62));
-    if (w > watermark_) watermark_ = w;
-  }
-  // lock-step: node-wide watermark (cache clock of the next batch) and newest bucket
+  // advance the watermark clock (max leading timestamp seen so far); lock-step: the node-wide
+  // watermark (cache clock of the next batch) and the newest-bucket exchange
+  int sync_slot = -1;
   if (lockstep_) {
-    const double tl = now_ms();
     int64_t bmax = INT64_MIN;
     for (size_t k = 0; k < shards_.size(); ++k) bmax = std::max(bmax, shard_maxb_[k * 8]);
-    lockstep_sync(bmax);
-    const double te = now_ms();
-    metrics_.t_lockstep_ms += te - tl;
-    metrics_.t_lockstep_max_ms = std::max(metrics_.t_lockstep_max_ms, te - tl);
-    trace_event("lockstep", tl, te, 0);
+    sync_slot = lockstep_collect(bmax);
+  } else {
+    watermark_ = batch_watermark(ps);
   }
 
   // ---- stats / z-score / alerts: handed to the stats thread, overlapping the next batch's
   // H2D + parse (parse stream) and host join (pool) with this batch's GPU stats work.
   const double tp0 = now_ms();
-  post_stats(std::move(outs), multi, t0, lockstep_ ? sync_latest_ : INT64_MIN);
+  post_stats(std::move(outs), multi, t0, sync_slot);
   const double tp1 = now_ms();
   trace_event("post", tp0, tp1, 0);
   // post_stats returned: the stats thread finished (and packed) every earlier batch
@@ -1164,6 +1160,8 @@ void Engine::process_batch_dev_tail(ParseSlot& ps, double t0, double now_overrid
   roctxRangePushA("apm.join");
   trace_event("parse", t0, t1, 0);
   const double clock = now_override >= 0 ? now_override : watermark_;
+  // lock-step (1/2): this batch's clocks go out before its join kernels (see lockstep_issue)
+  if (lockstep_) lockstep_issue(batch_watermark(ps));
   DevJoinBatch b;
   const DeviceJoin::ParallelFor par = [this](int n, const std::function<void(int)>& fn) { pool_->run(n, fn); };
   // once this batch's join kernels are queued, a lane thread finishes the next batch's parse and
@@ -1207,21 +1205,11 @@ void Engine::process_batch_dev_tail(ParseSlot& ps, double t0, double now_overrid
     for (int i = 0; i < DeviceJoin::kPhases; ++i) trace_event(names[i], dj_->phase_t[i], dj_->phase_t[i + 1], 2);
     for (const auto& sp : dj_->spans) trace_event(sp.first, sp.second.first, sp.second.second, 2);
   }
-  const unsigned long long wm = *ps.h_watermark;
-  if (wm) {
-    const double w = (double)((long long)wm - (1LL << 62));
-    if (w > watermark_) watermark_ = w;
-  }
-  if (lockstep_) {
-    const double tl = now_ms();
-    lockstep_sync(b.max_bucket);
-    const double te = now_ms();
-    metrics_.t_lockstep_ms += te - tl;
-    metrics_.t_lockstep_max_ms = std::max(metrics_.t_lockstep_max_ms, te - tl);
-    trace_event("lockstep", tl, te, 0);
-  }
+  // lock-step (2/2): collect the clocks, send the newest bucket (the stats thread waits for it)
+  const int sync_slot = lockstep_ ? lockstep_collect(b.max_bucket) : -1;
+  if (!lockstep_) watermark_ = batch_watermark(ps);
   const double tp0 = now_ms();
-  post_stats_dev(std::move(b), t0, lockstep_ ? sync_latest_ : INT64_MIN);
+  post_stats_dev(std::move(b), t0, sync_slot);
   const double tp1 = now_ms();
   trace_event("post", tp0, tp1, 0);
   if (coll_) fleet_due_ = fleet_posted_ - 1;  // exchanged during the next batch's join (see above)
@@ -1315,7 +1303,7 @@ void Engine::stats_worker() {
       job.multi = st_job_.multi;
       job.text.swap(st_job_.text);
       job.t0 = st_job_.t0;
-      job.sync_latest = st_job_.sync_latest;
+      job.sync_slot = st_job_.sync_slot;
       job.dev = st_job_.dev;
       job.seq = st_job_.seq;
       job.round = st_job_.round;
@@ -1349,7 +1337,7 @@ void Engine::stats_worker() {
         stats_for_batch(job.txs, job.t0);
       }
       const double ta = now_ms();
-      apply_latest_locked(job.sync_latest, job.t0);
+      if (job.sync_slot >= 0) apply_latest_locked(lockstep_latest(job.sync_slot), job.t0);
       trace_event("st.apply_latest", ta, now_ms(), 1);
       fleet_pack_locked();
       if (roll_pending_) finish_rollover();  // (a rollover the lane does not take: decided here)
@@ -1385,7 +1373,7 @@ void Engine::stats_worker() {
   }
 }
 
-void Engine::post_stats(std::vector<std::vector<TxOut>>&& outs, bool multi, double t0, int64_t sync_latest) {
+void Engine::post_stats(std::vector<std::vector<TxOut>>&& outs, bool multi, double t0, int sync_slot) {
   std::unique_lock<std::mutex> lk(st_mu_);
   st_cv_.wait(lk, [&]() { return !st_busy_; });
   if (!st_error_.empty()) { std::string e = st_error_; st_error_.clear(); throw std::runtime_error(e); }
@@ -1408,7 +1396,7 @@ void Engine::post_stats(std::vector<std::vector<TxOut>>&& outs, bool multi, doub
     }
   }
   st_job_.t0 = t0;
-  st_job_.sync_latest = sync_latest;
+  st_job_.sync_slot = sync_slot;
   st_job_.seq = batch_no_;
   st_job_.round = fleet_posted_;
   if (coll_) ++fleet_posted_;
@@ -1419,7 +1407,7 @@ void Engine::post_stats(std::vector<std::vector<TxOut>>&& outs, bool multi, doub
   if (!cfg_.async_stats) flush();
 }
 
-void Engine::post_stats_dev(DevJoinBatch&& b, double t0, int64_t sync_latest) {
+void Engine::post_stats_dev(DevJoinBatch&& b, double t0, int sync_slot) {
   std::unique_lock<std::mutex> lk(st_mu_);
   st_cv_.wait(lk, [&]() { return !st_busy_; });
   if (!st_error_.empty()) { std::string e = st_error_; st_error_.clear(); throw std::runtime_error(e); }
@@ -1430,7 +1418,7 @@ void Engine::post_stats_dev(DevJoinBatch&& b, double t0, int64_t sync_latest) {
   st_job_.dev = true;
   st_job_.dj = std::move(b);
   st_job_.t0 = t0;
-  st_job_.sync_latest = sync_latest;
+  st_job_.sync_slot = sync_slot;
   st_job_.seq = batch_no_;
   st_job_.round = fleet_posted_;
   if (coll_) ++fleet_posted_;
@@ -3413,12 +3401,12 @@ void Engine::fleet_setup(int32_t cap, bool lockstep) {
   lockstep_ = lockstep;
   if (lockstep_) {
     d_sync_ = (double*)dmalloc(64);
-    HIP_OK(hipHostMalloc((void**)&h_sync_, 128, hipHostMallocDefault));  // [0,4) values, [4,8) solo result, [8,12) sent
-    HIP_OK(hipEventCreateWithFlags(&solo_sync_ev_, hipEventDisableTiming));
-    const char* sw = std::getenv("APM_LOCKSTEP_SOLO_WAIT");
-    lockstep_solo_wait_ = sw && sw[0] == '1';
+    HIP_OK(hipHostMalloc((void**)&h_sync_, 256, hipHostMallocDefault));  // layout: engine.h
+    std::memset(h_sync_, 0, 256);
+    HIP_OK(hipEventCreateWithFlags(&clock_ev_, hipEventDisableTiming));
+    for (hipEvent_t& e : bucket_ev_) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    clock_pending_ = false;
   }
-  sync_latest_ = latest_;  // the stats thread is idle (flush above)
   fleet_cap_ = cap;
   fleet_elems_ = (size_t)cap * MAX_LAGS * NSTAT * 3;  // (capacity: a reload may change the LAG count)
   for (int i = 0; i < 2; ++i) {
@@ -3482,54 +3470,76 @@ void Engine::coll_wait(hipStream_t s, hipEvent_t ev, const char* what) {
   }
 }
 
-// Ingest thread, after the join of a batch: the node-wide watermark becomes the cache clock of
-// the next batch, and the node-wide newest bucket decides this batch's rollovers.  The bucket is
-// the one stats_for_batch derives (non-db tx with a usable endTs), so ranks agree on `latest`
-// without the stats thread touching the communicator.
-void Engine::lockstep_sync(int64_t batch_max) {
+// Lock-step rounds.  Every rank must see the same cache clock per batch (the node-wide
+// watermark: the newest leading timestamp any rank has parsed) and roll over on the same batch
+// (the node-wide newest bucket of the joined tx), as the single reference parser / stats process
+// does (stream_parse_transactions.js:211-239, stream_calc_stats.js:331-371).  Two MAX
+// all-reduces per batch on the collective stream, neither of them a barrier on the ingest thread:
+//   (1) lockstep_issue, before batch k's join: the watermark through batch k (its parse is done)
+//       -- the cache clock of batch k + 1 -- plus "services waiting for a registry slot" and the
+//       oldest staged reload.  It runs while the join kernels run; lockstep_collect takes the
+//       result after the join, so a peer up to one join behind costs this rank nothing.
+//   (2) lockstep_collect, after batch k's join: the newest bucket of batch k's tx.  Only the stats
+//       thread waits for it (lockstep_latest, after batch k's bucket appends), right before it
+//       decides batch k's rollovers; the ingest thread goes on with batch k + 1.
+// The same rounds run at every world size, N = 1 included (MAX over one rank is the identity):
+// a one-GPU run pays exactly the per-batch exchanges and waits of each rank of an 8-GPU node.
+double Engine::batch_watermark(const ParseSlot& ps) const {
+  double w = watermark_;
+  const unsigned long long wm = *ps.h_watermark;
+  if (wm) {
+    const double v = (double)((long long)wm - (1LL << 62));
+    if (v > w) w = v;
+  }
+  return w;
+}
+
+void Engine::lockstep_issue(double wm) {
   if (coll_->aborted()) throw std::runtime_error("collective communicator was aborted");
-  const int64_t b = std::max(sync_latest_, batch_max);
-  // The collective runs at every world size, N = 1 included (MAX over one rank is the identity,
-  // but the single-GPU run then does the same per-batch GPU work -- H2D, all-reduce, D2H -- as
-  // each rank of an 8-GPU node; at N = 1 only the host's wait is skipped, see below).
-  h_sync_[0] = watermark_;
-  h_sync_[1] = b == INT64_MIN ? -1.0 : (double)b;  // buckets < 2^53: exact in a double
-  h_sync_[2] = (double)reg_pending_count();        // any rank with unregistered services?
-  h_sync_[3] = -(double)reconfig_staged_gen();     // MAX of -gen: the node's oldest newest reload
+  if (clock_pending_) throw std::runtime_error("lock-step: clock round issued twice");
   // the values travel as kernel arguments: a kernel reading them from pinned memory queues its
   // PCIe read behind the output lane's D2H traffic (tens of us in the bench timeline)
-  if (fleet_nranks_ == 1 && !lockstep_solo_wait_) {
-    // One rank: MAX over one rank is the identity, known before the exchange runs.  The exchange
-    // is still issued (the GPU does the per-batch work of every rank of a node) but the ingest
-    // thread does not wait for it; the next batch checks that it completed and returned the
-    // values sent (APM_LOCKSTEP_SOLO_WAIT=1: wait as a multi-rank node does).
-    if (solo_sync_pending_) {
-      coll_wait(nullptr, solo_sync_ev_, "lock-step clocks (one rank)");
-      if (std::memcmp(h_sync_ + 4, h_sync_ + 8, 32) != 0)
-        throw std::runtime_error("lock-step clocks: the one-rank exchange changed its values");
-    }
-    std::memcpy(h_sync_ + 8, h_sync_, 32);
-    apm_set_f64(d_sync_, h_sync_, 4, coll_stream_);
-    coll_->all_reduce_f64(d_sync_, 4, /*max=*/true, coll_stream_);
-    d2h(h_sync_ + 4, d_sync_, 32, coll_stream_);
-    HIP_OK(hipEventRecord(solo_sync_ev_, coll_stream_));
-    solo_sync_pending_ = true;
-  } else {
-    apm_set_f64(d_sync_, h_sync_, 4, coll_stream_);
-    coll_->all_reduce_f64(d_sync_, 4, /*max=*/true, coll_stream_);
-    d2h(h_sync_, d_sync_, 32, coll_stream_);
-    coll_wait(coll_stream_, nullptr, "lock-step clocks");
-  }
-  watermark_ = h_sync_[0];
-  if (h_sync_[1] >= 0) sync_latest_ = std::max(sync_latest_, (int64_t)h_sync_[1]);
-  if (h_sync_[3] < 0) reconfig_agree((uint64_t)(-h_sync_[3]));  // every rank has it: same batch everywhere
-  if (h_sync_[2] > 0) reg_round();  // every rank sees the same max: all enter the gather
-  // the coll stream is in order: once the exchange above completed, the previous batch's alert
-  // gather has landed too (one rank without the wait: its own event)
+  const double v[4] = {wm, (double)reg_pending_count(), -(double)reconfig_staged_gen(), 0.0};
+  apm_set_f64(d_sync_, v, 4, coll_stream_);
+  coll_->all_reduce_f64(d_sync_, 4, /*max=*/true, coll_stream_);
+  d2h(h_sync_ + 4, d_sync_, 32, coll_stream_);
+  HIP_OK(hipEventRecord(clock_ev_, coll_stream_));
+  clock_pending_ = true;
+}
+
+int Engine::lockstep_collect(int64_t batch_max) {
+  const double tl = now_ms();
+  if (!clock_pending_) throw std::runtime_error("lock-step: no clock round in flight");
+  coll_wait(nullptr, clock_ev_, "lock-step clocks");
+  clock_pending_ = false;
+  watermark_ = h_sync_[4];  // (>= this rank's own watermark: it was one of the inputs)
+  if (h_sync_[6] < 0) reconfig_agree((uint64_t)(-h_sync_[6]));  // every rank has it: same batch everywhere
+  if (h_sync_[5] > 0) reg_round();  // every rank sees the same max: all enter the gather
+  // the previous batch's node-wide alert gather (issued during this batch's join)
   if (node_round_pending_) {
-    if (fleet_nranks_ == 1 && !lockstep_solo_wait_) coll_wait(nullptr, node_ev_, "node alerts");
+    coll_wait(nullptr, node_ev_, "node alerts");
     node_resolve();
   }
+  const int slot = (int)(batch_no_ & 3);
+  const double v[4] = {batch_max == INT64_MIN ? -1.0 : (double)batch_max, 0.0, 0.0, 0.0};  // buckets < 2^53
+  apm_set_f64(d_sync_ + 4, v, 4, coll_stream_);
+  coll_->all_reduce_f64(d_sync_ + 4, 4, /*max=*/true, coll_stream_);
+  d2h(h_sync_ + 8 + 4 * slot, d_sync_ + 4, 32, coll_stream_);
+  HIP_OK(hipEventRecord(bucket_ev_[slot], coll_stream_));
+  const double te = now_ms();
+  metrics_.t_lockstep_ms += te - tl;
+  metrics_.t_lockstep_max_ms = std::max(metrics_.t_lockstep_max_ms, te - tl);
+  trace_event("lockstep", tl, te, 0);
+  return slot;
+}
+
+// Stats thread: batch k's node-wide newest bucket (exchange (2) above).
+int64_t Engine::lockstep_latest(int slot) {
+  const double t0 = now_ms();
+  coll_wait(nullptr, bucket_ev_[slot], "lock-step bucket");
+  metrics_.t_lockstep_stats_ms += now_ms() - t0;
+  const double b = h_sync_[8 + 4 * slot];
+  return b >= 0 ? (int64_t)b : INT64_MIN;
 }
 
 // Stats thread: every rank rolls over when any rank saw a newer bucket, exactly as the single

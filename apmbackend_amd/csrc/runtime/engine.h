@@ -211,7 +211,8 @@ struct EngineMetrics {
   double t_stats_tx_ms = 0, t_rollover_ms = 0, t_format_ms = 0, t_release_ms = 0;  // inside t_stats_ms
   double t_out_ms = 0;                        // output lane: released-line gather + st/fs emission
   uint64_t db_copy_rows = 0, db_copy_fallbacks = 0;  // released db rows encoded on the GPU / releases encoded on the host
-  double t_lockstep_ms = 0, t_lockstep_max_ms = 0;  // ingest thread in the per-batch clock collective (sum / worst)
+  double t_lockstep_ms = 0, t_lockstep_max_ms = 0;  // ingest thread in the per-batch lock-step rounds (sum / worst)
+  double t_lockstep_stats_ms = 0;  // stats thread waiting for the newest-bucket round
   std::vector<double> rollover_latency_ms;   // batch arrival -> alert decision per rollover
 };
 
@@ -462,7 +463,7 @@ class Engine {
   void compute_series_settings(int32_t s, double* thr, double* infl, double& hard_max, uint8_t& suppressed);
   void stats_for_batch(std::vector<TxOut>& txs, double batch_t0);
   void stats_for_batch_dev(DevJoinBatch& b, double batch_t0);
-  void post_stats_dev(DevJoinBatch&& b, double t0, int64_t sync_latest);
+  void post_stats_dev(DevJoinBatch&& b, double t0, int sync_slot);
   void release_device(int64_t edge_ts);   // K9 with the device join: count + gather on the GPU
   void release_device_finish();
   void refresh_unseen_active();
@@ -521,10 +522,12 @@ class Engine {
   void node_resolve();
   void node_take_text();
   void coll_wait(hipStream_t s, hipEvent_t ev, const char* what);
-  void lockstep_sync(int64_t batch_max_bucket);
+  void lockstep_issue(double watermark_through_batch);
+  int lockstep_collect(int64_t batch_max_bucket);
+  int64_t lockstep_latest(int slot);
   void apply_latest_locked(int64_t g, double batch_t0);
   void stats_worker();
-  void post_stats(std::vector<std::vector<TxOut>>&& outs, bool multi, double t0, int64_t sync_latest = INT64_MIN);
+  void post_stats(std::vector<std::vector<TxOut>>&& outs, bool multi, double t0, int sync_slot = -1);
   void drain_sinks(uint32_t kinds = ~0u);
   void drain_kind(int k);
   // output lane (see engine.cpp): waits for the D2H of released-tx ids / formatted text and
@@ -550,14 +553,14 @@ class Engine {
   std::unique_ptr<Collective> coll_;
   hipStream_t coll_stream_ = nullptr;
   bool lockstep_ = false;
-  int64_t sync_latest_ = INT64_MIN;  // ingest thread: node-wide newest bucket so far
+  // lock-step exchanges (engine.cpp lockstep_issue / lockstep_collect): d_sync_ [0,4) clocks,
+  // [4,8) newest bucket; h_sync_ (pinned) [4,8) clock result, [8 + 4 s, 12 + 4 s) bucket result of
+  // ring slot s (batch & 3), read by the stats thread
   double* d_sync_ = nullptr;
   double* h_sync_ = nullptr;
-  // one rank: the clock exchange is issued but not waited for (its result is the identity);
-  // the next batch checks it (lockstep_sync)
-  hipEvent_t solo_sync_ev_ = nullptr;
-  bool solo_sync_pending_ = false;
-  bool lockstep_solo_wait_ = false;  // APM_LOCKSTEP_SOLO_WAIT=1
+  hipEvent_t clock_ev_ = nullptr;
+  hipEvent_t bucket_ev_[4] = {nullptr, nullptr, nullptr, nullptr};
+  bool clock_pending_ = false;
   int32_t fleet_cap_ = 0;
   size_t fleet_elems_ = 0;
   double* fleet_buf_[2] = {nullptr, nullptr};
@@ -676,7 +679,7 @@ class Engine {
     std::vector<std::vector<TxOut>> outs;  // per shard, merged by the stats thread into txs
     bool multi = false;
     std::vector<TxOut> txs; std::vector<std::string> text; double t0 = 0;
-    int64_t sync_latest = INT64_MIN;  // lock-step: node-wide newest bucket after this batch
+    int sync_slot = -1;  // lock-step: ring slot of this batch's node-wide newest-bucket exchange
     bool dev = false;                 // device join: `dj` instead of outs / txs
     uint64_t seq = 0;                 // batch index (the ingest thread's batch_no_)
     uint64_t round = 0;               // exchange round (posts since fleet_init)
@@ -835,6 +838,7 @@ class Engine {
   void process_batch_dev_tail(ParseSlot& ps, double t0, double now_override, const uint8_t* next_bytes,
                               uint64_t next_n, const std::vector<Chunk>* next_chunks);
   void finish_parse(ParseSlot& ps);
+  double batch_watermark(const ParseSlot& ps) const;  // watermark_ advanced by the slot's parse
   uint32_t* d_chunk_begin_[2] = {nullptr, nullptr};  // per parse slot (the device join reads them)
   uint8_t* d_chunk_kind_[2] = {nullptr, nullptr};
   uint32_t* d_chunk_file_[2] = {nullptr, nullptr};

@@ -48,6 +48,7 @@ from .notifier import Mailer, post_annotation
 
 # exit status of a rank that stopped because a peer rank failed (runtime/service.py)
 PEER_FAILURE_EXIT = 75
+HUNG_RANK = -1000  # blame code of a rank still running after every peer aborted on it (never an exit code)
 
 log = logging.getLogger("apm.manager")
 
@@ -265,6 +266,7 @@ class Supervisor:
         self.next_prune = clock()
         self.emails = 0
         self.gc_requests: List[str] = []
+        self._hbm_gc_at: Dict[int, float] = {}  # pid -> last HBM-triggered requestGC
         self._stop = False
         self.watcher = (ConfigWatcher(self.cfg, self._reload, ["apmConfigFilePath", "logDir",
                                                                "applicationManager.moduleSettings"])
@@ -359,6 +361,26 @@ class Supervisor:
         self.add_alert(text)
         return True
 
+    def _hung_peer(self, mod: Module, p: Proc) -> Optional[Proc]:
+        """A survivor exited PEER_FAILURE_EXIT: some peer stopped answering.  If that peer died,
+        it exits with its own code within the grace period and check_children blames it.  If it
+        hangs instead (a wedged GPU never lets the process exit), it is the one rank still running
+        once every other peer has exited PEER_FAILURE_EXIT: that rank's GPU is the one to blame."""
+        grace_end = time.monotonic() + float(self.m.get("groupAbortGraceSeconds", 5))
+        peers = [q for q in mod.procs if q is not p and q.restart_at is None]
+        while True:
+            codes = [(q, q.poll()) for q in peers]
+            if any(c not in (None, 0, PEER_FAILURE_EXIT) for _, c in codes):
+                return None  # a peer failed on its own: that exit carries the blame
+            running = [q for q, c in codes if c is None]
+            if not running:
+                return None
+            if len(running) == 1 and len(peers) > 1 and time.monotonic() >= grace_end:
+                return running[0]
+            if time.monotonic() >= grace_end:
+                return running[0] if len(running) == len(peers) == 1 else None
+            time.sleep(0.05)
+
     def _on_exit(self, mod: Module, p: Proc, code: int, now: float):
         if p not in mod.procs:  # a rank retired by an elastic restart
             return
@@ -370,7 +392,14 @@ class Supervisor:
         if quick:
             log.warning("Time since last restart is under %ss: crash loop suspected, waiting %ss",
                         self.m.get("crashLoopWindowSeconds", 5), delay)
-        if self._elastic_degrade(mod, p, code, now):
+        blame, bcode = p, code
+        if mod.ranks and code == PEER_FAILURE_EXIT:
+            hung = self._hung_peer(mod, p)
+            if hung is not None:
+                log.error("Rank %s still running after its peers aborted on it: blamed as hung", hung.name)
+                self.add_alert(f"Rank {hung.name} hung (its peers aborted their collectives on it)")
+                blame, bcode = hung, HUNG_RANK
+        if self._elastic_degrade(mod, blame, bcode, now):
             return
         targets = mod.procs if mod.ranks else [p]
         # A rank group restarts as a whole.  The survivors are expected to notice the dead peer on
@@ -573,7 +602,15 @@ class Supervisor:
                 if gthr and vram > float(gthr):
                     self.add_alert(f"Child module exceeded the GPU memory threshold - Module: {p.name} "
                                    f"Threshold(Mb): {gthr} HBMUsed(Mb): {vram:.1f}")
-                    trigger = True  # the child's requestGC trims its grow-only device memory
+                    # the child's requestGC trims its grow-only device memory; each trim flushes
+                    # the engine and rebuilds the join table, so an HBM-only trigger is sent at most
+                    # once per `gpuGcMinIntervalSeconds` (the RSS / swap triggers keep the
+                    # reference's every-inspection rule, apm_manager.js:485-508)
+                    last = self._hbm_gc_at.get(p.pid)
+                    gap = float(mod.setting("gpuGcMinIntervalSeconds", self.m) or 600)
+                    if trigger or last is None or self.clock() - last >= gap:
+                        trigger = True
+                        self._hbm_gc_at[p.pid] = self.clock()
                 if trigger:
                     log.info("Sending garbage collection request to module: %s", p.name)
                     self.gc_requests.append(p.name)

@@ -109,6 +109,31 @@ def test_memory_threshold_sends_request_gc(tmp_path):
         s.stop_all()
 
 
+def test_hbm_threshold_request_gc_is_rate_limited(tmp_path, monkeypatch):
+    """An HBM-only breach sends requestGC at most once per gpuGcMinIntervalSeconds (each trim
+    flushes the engine and rebuilds the join table); RSS / swap keep the every-inspection rule."""
+    body = "signal.signal(signal.SIGUSR1, lambda *a: None)\ntime.sleep(60)\n"
+    g = script(tmp_path, "gc.py", body)
+    C = make_cfg(tmp_path, [{"name": "hbm", "relativePath": g, "passConfig": False,
+                             "moduleGpuMemoryAlertThreshold": 1, "gpuGcMinIntervalSeconds": 100}])
+    now = [1000.0]
+    monkeypatch.setattr(sup, "pid_vram_mb", lambda pid: 5000.0)
+    s = sup.Supervisor(C, mailer=Mailer(sendmail="/nonexistent", outbox=str(tmp_path / "out")),
+                       annotate=lambda *a: None, clock=lambda: now[0])
+    s.start_all()
+    try:
+        time.sleep(0.3)
+        s.inspect_modules()
+        s.inspect_modules()
+        assert s.gc_requests == ["hbm"]  # the second breach within the interval: alert only
+        assert sum("GPU memory threshold" in a for a in s.alert_buffer) == 2
+        now[0] += 101
+        s.inspect_modules()
+        assert s.gc_requests == ["hbm", "hbm"]
+    finally:
+        s.stop_all()
+
+
 def test_stale_pid_only_killed_when_marker_matches(tmp_path):
     import subprocess
     other = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(30)"], start_new_session=True)
@@ -184,6 +209,31 @@ def test_rank_group_elastic_degrade(tmp_path):
         time.sleep(0.3)
         s.check_children()
         assert all(p.poll() is None for p in mod.procs) and mod.generation == 1
+    finally:
+        s.stop_all()
+
+
+def test_hung_rank_is_blamed_when_its_peers_abort(tmp_path):
+    """A rank that hangs never exits; its peers' watchdogs abort and exit PEER_FAILURE_EXIT (75).
+    The supervisor blames the rank still running after the grace period (its GPU is retired),
+    not a survivor, so a wedged GPU cannot restart the group forever."""
+    r = script(tmp_path, "rank.py", "import os\n"
+                                    "if os.environ['APM_DEVICE']=='2': time.sleep(60)\n"
+                                    "time.sleep(0.3); sys.exit(75)\n")
+    C = make_cfg(tmp_path, [{"name": "engine", "relativePath": r, "ranks": 4, "passConfig": False,
+                             "masterPort": 29640}],
+                 crashLoopWindowSeconds=0.0, restartDelaySeconds=0.05, elasticMaxFailures=1,
+                 elasticWindowSeconds=600, groupAbortGraceSeconds=1.0)
+    notes = []
+    s = sup.Supervisor(C, mailer=Mailer(sendmail="/nonexistent", outbox=str(tmp_path / "out")),
+                       annotate=lambda g, text, tags: notes.append(text))
+    s.start_all()
+    mod = s.modules[0]
+    try:
+        assert wait_for(lambda: (s.check_children() or True) and mod.generation == 1, timeout=20)
+        assert mod.bad_devices == {2} and mod.ranks == 2
+        assert any("hung" in a for a in s.alert_buffer)
+        assert any("GPU 2 failed" in n for n in notes)
     finally:
         s.stop_all()
 
