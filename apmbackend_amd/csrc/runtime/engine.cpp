@@ -1267,7 +1267,7 @@ void Engine::process_tx_lines(const std::string& blob, double now) {
   if (now >= 0 && now > watermark_) watermark_ = now;
   outs.resize(shards_.size());
   metrics_.lines += line;
-  post_stats(std::move(outs), /*multi=*/true, t0, INT64_MIN);
+  post_stats(std::move(outs), /*multi=*/true, t0, /*sync_slot=*/-1);
   metrics_.t_total_ms += now_ms() - t0;
   ++batch_no_;
 }
