@@ -10,6 +10,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <cstdlib>
 #include <cerrno>
 #include <thread>
 
@@ -308,6 +309,14 @@ class HostCollective final : public Collective {
   void all_reduce_f64(double* buf, size_t n, bool max, hipStream_t s) override {
     if (aborted_.load()) throw std::runtime_error("host collective aborted: " + error());
     if (n_ == 1 || n == 0) return;
+    if (sync_mode()) {  // APM_HOSTCOLL_SYNC=1: the caller waits (the round-5 form, A/B)
+      std::vector<double> mine(n);
+      HIP_OK(hipStreamSynchronize(s));
+      HIP_OK(hipMemcpy(mine.data(), buf, n * 8, hipMemcpyDeviceToHost));
+      const std::vector<double> out = all_reduce_host(mine, max);
+      HIP_OK(hipMemcpy(buf, out.data(), n * 8, hipMemcpyHostToDevice));
+      return;
+    }
     enqueue(s, max ? 1u : 2u, buf, buf, n * 8, n * 8);
   }
 
@@ -317,7 +326,19 @@ class HostCollective final : public Collective {
       if (bytes && send != recv) HIP_OK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, s));
       return;
     }
+    if (sync_mode()) {
+      std::vector<uint8_t> mine(bytes);
+      HIP_OK(hipStreamSynchronize(s));
+      HIP_OK(hipMemcpy(mine.data(), send, bytes, hipMemcpyDeviceToHost));
+      const std::vector<uint8_t> out = all_gather_host(mine);
+      HIP_OK(hipMemcpy(recv, out.data(), out.size(), hipMemcpyHostToDevice));
+      return;
+    }
     enqueue(s, 3u, send, recv, bytes, bytes * (size_t)n_);
+  }
+  static bool sync_mode() {
+    static const bool v = [] { const char* e = std::getenv("APM_HOSTCOLL_SYNC"); return e && e[0] == '1'; }();
+    return v;
   }
 
   // rank 0 reduces in rank order: the same bits on every rank, every run
