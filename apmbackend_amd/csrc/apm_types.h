@@ -85,9 +85,16 @@ static_assert(sizeof(TxRec) == 16, "TxRec layout");
 constexpr int32_t ELAPSED_NAN = (int32_t)0x80000000;
 
 // ----------------------------------------------------------------------------- stats / z-score
-constexpr int NSLOT = 40;          // bucket ring slots per series (window 31 + buffer + slack)
+// Bucket ring slots per series: config-sized (gpu.bucketRingSlots, at least window + buffer + 1:
+// removeOldBuckets keeps window + buffer buckets plus the one being filled); this is the default
+// floor (window 31 + buffer 6 + slack).  A live reload to a longer window grows the ring.
+constexpr int NSLOT_MIN = 40;
+constexpr int K8_INLINE_SLOTS = 64;  // window buckets passed to K8 as kernel arguments (more: a device array)
 constexpr int NSTAT = 3;           // avg, p75, p95
-constexpr int MAX_LAGS = 8;           // LAG settings per engine (the reference: any number)
+// LAG settings per engine.  The reference takes any number; here it is a capacity: every LAG is an
+// HBM ring of LAG x NSTAT x maxSeries values (LAG 8640 at fp64 and 131k series: 27 GB), so HBM,
+// not this table, is what bounds it -- 16 daily LAGs would not fit a 288 GB MI355X.
+constexpr int MAX_LAGS = 16;
 
 // Per-series window statistics produced at a rollover (values already rounded the way the
 // z-score stage sees them after the `st` wire format: tpm 2 dp, the rest 1 dp).

@@ -98,6 +98,7 @@ EngineConfig config_from(const py::dict& d) {
   c.interval_len = get<int>(d, "interval_len", c.interval_len);
   c.window = get<int>(d, "window", c.window);
   c.buffer = get<int>(d, "buffer", c.buffer);
+  c.nslot = get<int>(d, "nslot", c.nslot);
   c.record_ttl_ms = get<double>(d, "record_ttl_ms", c.record_ttl_ms);
   c.acct_ttl_ms = get<double>(d, "acct_ttl_ms", c.acct_ttl_ms);
   c.need_ttl_ms = get<double>(d, "need_ttl_ms", c.need_ttl_ms);
@@ -273,7 +274,8 @@ PYBIND11_MODULE(_apm_native, m) {
     const std::string s = b;
     return hash_bytes(s.data(), s.size(), seed);
   }, py::arg("data"), py::arg("seed") = kHashSeed);
-  m.attr("NSLOT") = NSLOT;
+  m.attr("NSLOT_MIN") = NSLOT_MIN;
+  m.attr("MAX_LAGS") = MAX_LAGS;
 
   // TCP host transport on host buffers (CPU tests of the multi-process collective path)
   py::class_<Collective>(m, "HostCollective")
@@ -327,6 +329,8 @@ PYBIND11_MODULE(_apm_native, m) {
         d["applied_gen"] = e.reconfig_applied_gen(); d["applied"] = e.reconfigs_applied();
         d["lag_set_changes"] = e.lag_set_changes();
         d["window_changes"] = e.window_changes();
+        d["ring_slots"] = e.ring_slots();
+        d["ring_grows"] = e.ring_grows();
         return d;
       })
       .def("lag_values", &Engine::lag_values)

@@ -1071,17 +1071,20 @@ __global__ void k_aud_walk(DJArgs a) {
 // (`fresh`: set when this call created the key; the caller counts new keys once per wave -- a
 // per-lane atomicAdd on the one n_keys_new word put ~every logId of the batch through a single
 // L2 atomic unit)
-__device__ uint32_t key_claim(KeyState* __restrict__ t, uint32_t mask, uint64_t k, int32_t server, JoinCounts* cnt,
-                              bool& fresh) {
+// Probes the dense key array (DJArgs::keys); the claiming lane also writes the key into the slot's
+// KeyState, which every later kernel reads.
+__device__ uint32_t key_claim(KeyState* __restrict__ t, uint64_t* __restrict__ keys, uint32_t mask, uint64_t k,
+                              int32_t server, JoinCounts* cnt, bool& fresh) {
   uint32_t h = home_of(k, mask);
   for (uint32_t probe = 0; probe <= mask; ++probe) {
     const uint32_t idx = (h + probe) & mask;
-    const uint64_t cur = __hip_atomic_load(&t[idx].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t cur = __hip_atomic_load(&keys[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (cur == k) return idx;
     if (cur == 0) {
-      const unsigned long long prev = atomicCAS((unsigned long long*)&t[idx].key, 0ULL, (unsigned long long)k);
+      const unsigned long long prev = atomicCAS((unsigned long long*)&keys[idx], 0ULL, (unsigned long long)k);
       if (prev == 0) {
         KeyState& s = t[idx];
+        s.key = k;
         s.acct = apm_nan();
         s.acct_exp = -__builtin_inf();
         s.rec_exp = -__builtin_inf();
@@ -1119,7 +1122,7 @@ __global__ void k_claim(DJArgs a) {
   bool fresh = false;
   if (op.op == JOP_DIRECT) key = cap;
   else if (op.op != JOP_NONE) {
-    const uint32_t s = key_claim(a.table, a.table_mask, op.gkey, op.server, a.counts, fresh);
+    const uint32_t s = key_claim(a.table, a.keys, a.table_mask, op.gkey, op.server, a.counts, fresh);
     key = s == 0xffffffffu ? cap + 1 : s;
   }
   {  // new keys: one atomic per wave
@@ -2401,6 +2404,11 @@ __global__ void k_count_le(const int64_t* __restrict__ end, int64_t n, int64_t e
   *out = lo;
 }
 
+__global__ void k_keys_sync(const KeyState* __restrict__ t, uint32_t cap, uint64_t* __restrict__ keys) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < cap) keys[i] = t[i].key;
+}
+
 }  // namespace
 }  // namespace apm
 
@@ -2877,6 +2885,11 @@ void apm_dj_fill_series(TxRec* tx, const int32_t* raw, uint32_t n, const int32_t
 void apm_dj_gather_u8(const uint8_t* src, const int32_t* idx, uint32_t n, uint8_t* out, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_gather_u8, dim3((n + TB - 1) / TB), dim3(TB), 0, s, src, idx, n, out);
 }
+void apm_dj_keys_sync(const apm::KeyState* table, uint32_t cap, uint64_t* keys, hipStream_t s) {
+  hipLaunchKernelGGL(k_keys_sync, dim3((cap + 255) / 256), dim3(256), 0, s, table, cap, keys);
+  dj_check(s, "k_keys_sync");
+}
+
 void apm_dj_cache_stats(const apm::KeyState* table, uint32_t cap, double now, unsigned long long* out, hipStream_t s) {
   HIP_OK(hipMemsetAsync(out, 0, 5 * sizeof(unsigned long long), s));
   const unsigned blocks = std::max(1u, std::min<unsigned>(1024, (cap + TB - 1) / TB));

@@ -121,6 +121,10 @@ struct DJArgs {
   void* tmp;                      // rocprim scratch
   size_t tmp_bytes;
   KeyState* table;
+  // dense copy of table[i].key (8 B per slot): k_claim probes it, so a probe sequence stays in
+  // one or two cache lines instead of touching a 128-byte KeyState per step (2M slots: 16 MB
+  // against 256 MB); only the winning slot's payload is read or initialised
+  uint64_t* keys;
   uint32_t table_mask;
   int table_bits;
   RegSlot* reg;
@@ -276,6 +280,8 @@ void apm_dj_fill_series(apm::TxRec* tx, const int32_t* raw, uint32_t n, const in
                         unsigned long long* unmapped, hipStream_t s);
 void apm_dj_gather_u8(const uint8_t* src, const int32_t* idx, uint32_t n, uint8_t* out, hipStream_t s);
 void apm_dj_cache_stats(const apm::KeyState* table, uint32_t cap, double now, unsigned long long* out, hipStream_t s);
+// keys[i] = table[i].key for every slot (after any rewrite of the table other than k_claim's)
+void apm_dj_keys_sync(const apm::KeyState* table, uint32_t cap, uint64_t* keys, hipStream_t s);
 void apm_dj_count_le(const int64_t* end, int64_t n, int64_t edge, int64_t* out, hipStream_t s);
 void apm_dj_relocate(int64_t* gid, int64_t n, char* ring, uint64_t ring_cap, uint64_t below, uint64_t dst_base,
                      unsigned long long* cursor, hipStream_t s);

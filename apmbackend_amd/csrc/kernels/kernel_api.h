@@ -10,15 +10,16 @@
 namespace apm {
 
 struct StatsState {
-  int32_t* counts;        // [NSLOT][S]
-  int32_t* cells;         // [NSLOT][S][cap]
-  int32_t* spill_n;       // [NSLOT]
-  int32_t* spill_series;  // [NSLOT][spill_cap]  (sorted by series, stably, before every K8)
-  int32_t* spill_val;     // [NSLOT][spill_cap]
+  int32_t* counts;        // [nslot][S]
+  int32_t* cells;         // [nslot][S][cap]
+  int32_t* spill_n;       // [nslot]
+  int32_t* spill_series;  // [nslot][spill_cap]  (sorted by series, stably, before every K8)
+  int32_t* spill_val;     // [nslot][spill_cap]
   uint8_t* active;        // [S]
   int32_t cap;
   int32_t spill_cap;
   int32_t S;
+  int32_t nslot = NSLOT_MIN;  // bucket ring slots (bucket b lives in slot b % nslot)
   unsigned long long* spill_drop = nullptr;  // [0] samples lost to a full spill list, [1] NaN windows clipped
   // NaN elapsed samples (stream_calc_stats.js:131 pushes parseInt -> NaN): once a series holds one,
   // the JS binaryInsert order of every later sample in its windows matters, so the series' samples
@@ -28,15 +29,16 @@ struct StatsState {
   int32_t* ord_n = nullptr;
   uint32_t* ord_done = nullptr;  // blocks of the ordered append finished (the last one resets ord_n)
   int32_t keep = 0;              // windowSz + intervalBufferSz
-  // host-mapped pinned [NSLOT]: spill_n after each append (the host's exact fill level, read once
+  // host-mapped pinned [nslot]: spill_n after each append (the host's exact fill level, read once
   // the append's event completed; it sizes the spill area so no sample is ever dropped)
   int32_t* spill_snap = nullptr;
 };
 
 struct WindowArgs {
   StatsState st;
-  int32_t win_slots[32];  // slot index per window bucket (-1 = bucket absent)
-  int32_t n_win;          // 31
+  int32_t win_slots[K8_INLINE_SLOTS];  // slot index per window bucket (-1 = bucket absent), n_win <= 64
+  const int32_t* win_slots_ext;        // device [n_win] when n_win > K8_INLINE_SLOTS (else null)
+  int32_t n_win;          // windowSizeInIntervals (31 in the shipped config)
   double tpm_div;         // windowSz * intervalLen / 60
   WinStat* out;           // [S]
   int32_t* big_list;      // series deferred to the block pass
@@ -222,7 +224,7 @@ void apm_nan_mark(const apm::TxRec* d_tx, uint32_t n, apm::StatsState* st, hipSt
 void apm_window_stats(apm::WindowArgs* a, hipStream_t stream);
 // before K8: every slot's spill list [slot * cap, + spill_n[slot]) sorted by series, stably (a
 // series' samples keep their arrival order), into (series_out, val_out); the caller swaps buffers
-size_t apm_spill_sort_tmp_bytes(int32_t spill_cap, int32_t S);
+size_t apm_spill_sort_tmp_bytes(int32_t spill_cap, int32_t S, int32_t nslot);
 int apm_spill_sort(const apm::StatsState* st, int32_t* series_out, int32_t* val_out, void* tmp, size_t tmp_bytes,
                    hipStream_t stream);
 void apm_pool_append(const apm::TxRec* d_tx, uint32_t lo, uint32_t hi, const int64_t* d_gid, int64_t* tail_end,

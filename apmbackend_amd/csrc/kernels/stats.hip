@@ -4,9 +4,10 @@
 // generateAllStatsToQueue (:157-203) with util_methods.js calcPercentile (:112-142), and the
 // min-heap release writeHeapToQueue (:136-155) / binary_heap.js popAllLessOrEqualToScore.
 //
-// Layout (MI355X): samples live in a per-series ring of NSLOT=40 ten-second bucket cells,
-// cells[slot][series][CAP] (int32 elapsed ms) + counts[slot][series]; a live bucket b sits in
-// slot b % 40 (at most 37 buckets are live, so slots never alias).  Appends are one atomicAdd
+// Layout (MI355X): samples live in a per-series ring of `nslot` ten-second bucket cells (config-
+// sized, >= window + buffer + 1; 40 by default), cells[slot][series][CAP] (int32 elapsed ms) +
+// counts[slot][series]; a live bucket b sits in slot b % nslot (at most window + buffer + 1
+// buckets are live, so slots never alias).  Appends are one atomicAdd
 // per sample into the cell (overflow beyond CAP goes to a per-slot spill list).  At a rollover
 // every active series is reduced by one wave: the 31 window cells are gathered into LDS, summed,
 // bitonic-sorted in LDS and the two percentile ranks read out with the reference index rule.
@@ -28,6 +29,11 @@ constexpr int WS_WAVES = 4;              // waves per block in the window kernel
 constexpr int WS_TILE = 1024;            // samples per wave held in LDS
 constexpr int BIG_TILE = 16384;          // samples per block in the large-series pass (64 KiB)
 
+// slot of window bucket r (kernel arguments for the first K8_INLINE_SLOTS, then a device array)
+__device__ __forceinline__ int win_slot(const WindowArgs& a, int r) {
+  return r < K8_INLINE_SLOTS ? a.win_slots[r] : a.win_slots_ext[r];
+}
+
 
 // --------------------------------------------------------------------------------- K7
 // Appends tx[lo, hi) to their bucket cells. `slot_of` maps (bucket - slot_base) -> slot or -1
@@ -47,7 +53,7 @@ __global__ void k_bucket_append(const TxRec* __restrict__ tx, uint32_t lo, uint3
     st.ord_list[atomicAdd(st.ord_n, 1)] = (int32_t)i;  // arrival order matters: ordered pass
     return;
   }
-  const int slot = (int)(b % NSLOT);
+  const int slot = (int)(b % st.nslot);
   const size_t cidx = (size_t)slot * st.S + r.series;
   const int k = atomicAdd(&st.counts[cidx], 1);
   if (k < st.cap) {
@@ -91,7 +97,8 @@ __global__ __launch_bounds__(1024) void k_bucket_append_ordered(const TxRec* __r
   const int n_ord = *st.ord_n;
   if (n_ord == 0) {
     // every append of this call is done (stream order): publish the fill levels to the host
-    if (blockIdx.x == 0 && st.spill_snap && threadIdx.x < NSLOT) st.spill_snap[threadIdx.x] = st.spill_n[threadIdx.x];
+    if (blockIdx.x == 0 && st.spill_snap)
+      for (int k = threadIdx.x; k < st.nslot; k += blockDim.x) st.spill_snap[k] = st.spill_n[k];
     return;
   }
   const uint32_t G = gridDim.x, blk = blockIdx.x;
@@ -104,7 +111,7 @@ __global__ __launch_bounds__(1024) void k_bucket_append_ordered(const TxRec* __r
     int mine = 0;
     for (int j = threadIdx.x; j < n_ord; j += blockDim.x) {
       const TxRec r = tx[st.ord_list[j]];
-      const uint32_t cell = (uint32_t)((r.end_ms / 10000) % NSLOT) * (uint32_t)st.S + (uint32_t)r.series;
+      const uint32_t cell = (uint32_t)((r.end_ms / 10000) % st.nslot) * (uint32_t)st.S + (uint32_t)r.series;
       mine += cell % G == blk;
     }
     if (mine) atomicAdd(&m_sh, mine);
@@ -119,7 +126,7 @@ __global__ __launch_bounds__(1024) void k_bucket_append_ordered(const TxRec* __r
       const uint32_t i = (uint32_t)st.ord_list[j];
       if (i - lo >= r0 && i - lo < r0 + R) {
         const TxRec r = tx[i];
-        const uint32_t cell = (uint32_t)((r.end_ms / 10000) % NSLOT) * (uint32_t)st.S + (uint32_t)r.series;
+        const uint32_t cell = (uint32_t)((r.end_ms / 10000) % st.nslot) * (uint32_t)st.S + (uint32_t)r.series;
         if (cell % G == blk) key[atomicAdd(&m_sh, 1)] = ((unsigned long long)cell << 32) | i;
       }
     }
@@ -202,7 +209,8 @@ __global__ __launch_bounds__(1024) void k_bucket_append_ordered(const TxRec* __r
     *st.ord_n = 0;
     *st.ord_done = 0;
   }
-  if (st.spill_snap && threadIdx.x < NSLOT) st.spill_snap[threadIdx.x] = atomicAdd(&st.spill_n[threadIdx.x], 0);
+  if (st.spill_snap)
+    for (int k = threadIdx.x; k < st.nslot; k += blockDim.x) st.spill_snap[k] = atomicAdd(&st.spill_n[k], 0);
 }
 
 __global__ void k_clear_slot(StatsState st, int slot) {
@@ -290,6 +298,10 @@ __global__ __launch_bounds__(WS_WAVES * APM_WAVE) void k_window_stats(WindowArgs
   if (s >= a.n_series) return;
   if (!a.st.active[s]) {
     if (lane == 0) { WinStat w{}; w.active = 0; w.n = 0; a.out[s] = w; }
+    return;
+  }
+  if (a.n_win > APM_WAVE) {  // a window longer than the wave (> 640 s): the block pass loops over its buckets
+    if (lane == 0) { const int j = atomicAdd(a.big_n, 1); a.big_list[j] = s; }
     return;
   }
   // per-window-bucket counts (lane r handles window bucket r)
@@ -408,7 +420,7 @@ __global__ __launch_bounds__(WS_WAVES * APM_WAVE) void k_window_stats(WindowArgs
 template <class F>
 __device__ __forceinline__ void for_each_window_sample(const WindowArgs& a, int s, F&& f) {
   for (int r = 0; r < a.n_win; ++r) {
-    const int sl = a.win_slots[r];
+    const int sl = win_slot(a, r);
     if (sl < 0) continue;
     const int cnt = a.st.counts[(size_t)sl * a.st.S + s];
     const int inl = min(cnt, a.st.cap);
@@ -489,7 +501,7 @@ __global__ __launch_bounds__(1024) void k_window_stats_big(WindowArgs a) {
     long long sum = 0;
     int nan = 0;
     for (int r = 0; r < a.n_win; ++r) {
-      const int sl = a.win_slots[r];
+      const int sl = win_slot(a, r);
       if (sl < 0) continue;
       const int cnt = a.st.counts[(size_t)sl * a.st.S + s];
       const int inl = min(cnt, a.st.cap);
@@ -578,7 +590,7 @@ __global__ __launch_bounds__(1024) void k_window_stats_js(WindowArgs a) {
     if (threadIdx.x == 0) { wpos = 0; first_nan = INT32_MAX; }
     __syncthreads();
     for (int r = 0; r < a.n_win; ++r) {
-      const int sl = a.win_slots[r];
+      const int sl = win_slot(a, r);
       if (sl < 0) continue;
       const int cnt = a.st.counts[(size_t)sl * a.st.S + s];
       const int inl = min(cnt, a.st.cap);
@@ -872,12 +884,12 @@ int key_bits(int32_t S) {
 }
 }  // namespace
 
-size_t apm_spill_sort_tmp_bytes(int32_t spill_cap, int32_t S) {
+size_t apm_spill_sort_tmp_bytes(int32_t spill_cap, int32_t S, int32_t nslot) {
   size_t need = 0;
   const auto beg = rocprim::make_transform_iterator(rocprim::make_counting_iterator(0), SpillOff{nullptr, spill_cap});
   const auto end = rocprim::make_transform_iterator(rocprim::make_counting_iterator(0), SpillOff{nullptr, spill_cap});
   HIP_OK(rocprim::segmented_radix_sort_pairs(nullptr, need, (int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr,
-                                             (int32_t*)nullptr, (size_t)NSLOT * spill_cap, (unsigned)NSLOT, beg, end, 0,
+                                             (int32_t*)nullptr, (size_t)nslot * spill_cap, (unsigned)nslot, beg, end, 0,
                                              key_bits(S), (hipStream_t)0));
   return need + 4096;
 }
@@ -888,11 +900,11 @@ int apm_spill_sort(const StatsState* st, int32_t* series_out, int32_t* val_out, 
   const auto beg = rocprim::make_transform_iterator(rocprim::make_counting_iterator(0), SpillOff{nullptr, st->spill_cap});
   const auto end = rocprim::make_transform_iterator(rocprim::make_counting_iterator(0), SpillOff{st->spill_n, st->spill_cap});
   HIP_OK(rocprim::segmented_radix_sort_pairs(nullptr, need, st->spill_series, series_out, st->spill_val, val_out,
-                                             (size_t)NSLOT * st->spill_cap, (unsigned)NSLOT, beg, end, 0, key_bits(st->S),
+                                             (size_t)st->nslot * st->spill_cap, (unsigned)st->nslot, beg, end, 0, key_bits(st->S),
                                              stream));
   if (need > tmp_bytes) return -1;
   HIP_OK(rocprim::segmented_radix_sort_pairs(tmp, need, st->spill_series, series_out, st->spill_val, val_out,
-                                             (size_t)NSLOT * st->spill_cap, (unsigned)NSLOT, beg, end, 0, key_bits(st->S),
+                                             (size_t)st->nslot * st->spill_cap, (unsigned)st->nslot, beg, end, 0, key_bits(st->S),
                                              stream));
   return 0;
 }

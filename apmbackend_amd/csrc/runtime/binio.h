@@ -24,7 +24,8 @@ namespace apm {
 
 // 3: join section carries the join mode (host / GPU); 4: node-wide server order; 5: rings in their own
 // trailing section (full or dirty rows, for incremental checkpoints) + NaN horizons + an opaque extra
-constexpr uint32_t kCkptVersion = 8;  // 7: device audit-trail carry (K5 on the GPU); 8: 8 LAG slots
+constexpr uint32_t kCkptVersion = 9;  // 7: device audit-trail carry (K5 on the GPU); 8: 8 LAG slots;
+                                      // 9: 16 LAG slots, config-sized bucket ring (slot table as a vector)
 
 // Section tags, in file order (checkpoint.cpp writes / reads them, merge.cpp re-shards them).
 enum : uint32_t {

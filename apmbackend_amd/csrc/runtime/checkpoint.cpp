@@ -278,8 +278,8 @@ uint64_t Engine::dump_state(const std::string& path, const std::string& reason) 
   num("spill_capacity", (double)cfg_.spill_cap); num("spill_grows", (double)m.spill_grows);
   num("pending_tx", (double)(pool_n_ + tail_n_)); num("pending_tx_capacity", (double)cfg_.pool_cap);
   {
-    std::vector<double> sb(NSLOT), sn(NSLOT);
-    for (int s = 0; s < NSLOT; ++s) {
+    std::vector<double> sb(nslot_), sn(nslot_);
+    for (int s = 0; s < nslot_; ++s) {
       sb[s] = slot_bucket_[s] == NO_BUCKET ? -1.0 : (double)slot_bucket_[s];
       sn[s] = h_spill_snap_ ? (double)h_spill_snap_[s] : -1.0;
     }
@@ -449,7 +449,7 @@ void Engine::write_small_sections(BinWriter& w) {
 
   w.begin(SEC_CLOCK);
   w.pod(watermark_); w.pod(batch_no_); w.pod(latest_); w.pod(rollover_idx_);
-  w.raw(slot_bucket_, sizeof(slot_bucket_));
+  w.vec(slot_bucket_);  // (its size is the ring's slot count)
   w.pod(next_gid_); w.pod(line_block_seq_);
   w.end();
 
@@ -480,12 +480,12 @@ void Engine::write_small_sections(BinWriter& w) {
   w.begin(SEC_BUCKETS);
   d2h_vec(w, d_active_, (size_t)n, stream_, bounce);
   {
-    std::vector<int32_t> spill_n(NSLOT);
-    HIP_OK(hipMemcpy(spill_n.data(), d_spill_n_, NSLOT * 4, hipMemcpyDeviceToHost));
+    std::vector<int32_t> spill_n(nslot_);
+    HIP_OK(hipMemcpy(spill_n.data(), d_spill_n_, (size_t)nslot_ * 4, hipMemcpyDeviceToHost));
     // the occupied cells of every live slot, packed on the device in one pass (scan + gather),
     // then written per slot straight from the pinned bounce
     std::vector<int32_t> slots;
-    for (int slot = 0; slot < NSLOT; ++slot)
+    for (int slot = 0; slot < nslot_; ++slot)
       if (slot_bucket_[slot] != NO_BUCKET) slots.push_back(slot);
     const int k = (int)slots.size();
     const int32_t cap = cfg_.cell_cap;
@@ -518,7 +518,7 @@ void Engine::write_small_sections(BinWriter& w) {
           drop();
         }
       }
-      if (!d_ck_slots_) d_ck_slots_ = (int32_t*)dmalloc_try(NSLOT * 4);
+      if (!d_ck_slots_) d_ck_slots_ = (int32_t*)dmalloc_try((size_t)nslot_ * 4);
       dev_pack = ck_pack_n_ >= N + 1 && d_ck_slots_;
     }
     if (dev_pack) {
@@ -841,7 +841,25 @@ std::string Engine::load_small_state(const std::string& path) {
 
   rd.begin(SEC_CLOCK);
   rd.pod(watermark_); rd.pod(batch_no_); rd.pod(latest_); rd.pod(rollover_idx_);
-  rd.raw(slot_bucket_, sizeof(slot_bucket_));
+  // the saver's ring may have another slot count (gpu.bucketRingSlots, a reload that grew it):
+  // its buckets are placed at b % nslot_ of this ring, grown first if they do not fit
+  const std::vector<int64_t> file_bucket = rd.vec<int64_t>();
+  {
+    int32_t live = 0;
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    for (int64_t b : file_bucket)
+      if (b != NO_BUCKET) { ++live; lo = std::min(lo, b); hi = std::max(hi, b); }
+    if (live && hi - lo + 1 > nslot_) grow_ring((int32_t)(hi - lo + 1));
+    std::fill(slot_bucket_.begin(), slot_bucket_.end(), NO_BUCKET);
+    for (int64_t b : file_bucket)
+      if (b != NO_BUCKET) slot_bucket_[(size_t)(((b % nslot_) + nslot_) % nslot_)] = b;
+  }
+  auto ring_slot_of = [&](int32_t fslot) -> int32_t {
+    if (fslot < 0 || (size_t)fslot >= file_bucket.size() || file_bucket[(size_t)fslot] == NO_BUCKET)
+      throw std::runtime_error("checkpoint: bad slot");
+    const int64_t b = file_bucket[(size_t)fslot];
+    return (int32_t)(((b % nslot_) + nslot_) % nslot_);
+  };
   rd.pod(next_gid_); rd.pod(line_block_seq_);
 
   rd.begin(SEC_JOIN);
@@ -878,9 +896,9 @@ std::string Engine::load_small_state(const std::string& path) {
   {
     std::vector<int32_t> cells((size_t)n * cfg_.cell_cap);
     for (;;) {
-      const int32_t slot = rd.pod<int32_t>();
-      if (slot < 0) break;
-      if (slot >= NSLOT) throw std::runtime_error("checkpoint: bad slot");
+      const int32_t fslot = rd.pod<int32_t>();
+      if (fslot < 0) break;
+      const int32_t slot = ring_slot_of(fslot);
       auto counts = rd.vec<int32_t>();
       auto packed = rd.vec<int32_t>();
       if ((int32_t)counts.size() != n) throw std::runtime_error("checkpoint: bucket counts size");
@@ -1066,6 +1084,7 @@ int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& e
     need += (size_t)NSTAT * lg.heads.size() * n * rb;
     job->lags.push_back(std::move(lg));
   }
+  ck_last_need_ = need;
   if (need > ck_stage_bytes_) {
     free_ck_stage();
     const size_t want = need + need / 8;  // room for the series table to grow
@@ -1208,18 +1227,43 @@ void Engine::checkpoint_writer() {
 // the files the new manifest no longer names.
 void Engine::finish_chain(const std::shared_ptr<CkJob>& job, uint64_t bytes) {
   (void)bytes;
-  std::vector<std::string> old;
+  const std::string dir = dir_of(job->prefix);
+  auto names = [&](const std::string& manifest) {  // file names of a manifest on disk ({} if none)
+    std::vector<std::string> v;
+    try {
+      if (!is_chain_manifest(manifest)) return v;
+      for (const auto& p : read_chain(manifest)) v.push_back(p.substr(p.rfind('/') + 1));
+    } catch (const std::exception&) {
+    }
+    return v;
+  };
+  std::vector<std::string> drop;
   if (job->base) {
-    old = ck_chain_;
+    if (!ck_disk_chains_read_) {  // a restarted process: the chains its predecessor left
+      ck_disk_chains_read_ = true;
+      if (ck_chain_.empty()) ck_chain_ = names(job->prefix + ".ckpt");
+      if (ck_prev_chain_.empty()) ck_prev_chain_ = names(job->prefix + ".prev.ckpt");
+    }
+    // the replaced chain becomes the previous one; the one before it goes
+    drop = ck_prev_chain_;
+    ck_prev_chain_ = ck_chain_;
     ck_chain_.assign(1, job->name);
+    if (!ck_prev_chain_.empty()) {
+      std::string prev = "APMCHAIN 1\n";
+      for (const auto& f : ck_prev_chain_) prev += f + "\n";
+      write_text_atomic(job->prefix + ".prev.ckpt", prev);
+    }
   } else {
     ck_chain_.push_back(job->name);
   }
   std::string body = "APMCHAIN 1\n";
   for (const auto& f : ck_chain_) body += f + "\n";
   write_text_atomic(job->prefix + ".ckpt", body);
-  for (const auto& f : old)
-    if (f != job->name) std::remove((dir_of(job->prefix) + "/" + f).c_str());
+  for (const auto& f : drop) {
+    if (std::find(ck_chain_.begin(), ck_chain_.end(), f) != ck_chain_.end()) continue;
+    if (std::find(ck_prev_chain_.begin(), ck_prev_chain_.end(), f) != ck_prev_chain_.end()) continue;
+    std::remove((dir + "/" + f).c_str());
+  }
 }
 
 uint64_t Engine::checkpoint_wait() {

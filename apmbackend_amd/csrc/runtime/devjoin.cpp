@@ -715,6 +715,7 @@ void DeviceJoin::rebuild_table(double now, uint32_t new_cap) {
   const bool same = new_cap == table_cap_;
   if (same && !rebuild_copy()) {  // in place (apm_dj_rebuild_inplace), then wait for the count
     rebuild_inplace(now);
+    sync_keys();
     HIP_OK(hipMemcpyAsync(h_live_, d_live_, 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     keys_live_ = *h_live_;
@@ -749,6 +750,21 @@ void DeviceJoin::rebuild_table(double now, uint32_t new_cap) {
   live_pending_ = false;
   ++table_rebuilds_;
   ensure_tmp();  // the grouping sort's key width follows the table
+  sync_keys();
+}
+
+// Dense key array (k_claim's probe target) from the table, on the join stream.
+void DeviceJoin::sync_keys() {
+  if (keys_cap_ != table_cap_) {
+    if (d_keys_) {
+      HIP_OK(hipStreamSynchronize(stream_));
+      dfree(d_keys_, (size_t)keys_cap_ * 8);
+    }
+    d_keys_ = (uint64_t*)dmalloc((size_t)table_cap_ * 8);
+    keys_cap_ = table_cap_;
+  }
+  apm_dj_keys_sync(d_table_, table_cap_, d_keys_, stream_);
+  keys_stale_ = false;
 }
 
 // The same-size rebuild in stream order, without waiting for it: the live count arrives in h_live_
@@ -788,6 +804,7 @@ void DeviceJoin::rebuild_table_async(double now) {
   } else {
     rebuild_inplace(now);
   }
+  sync_keys();  // (the join stream's idle gap, with the rebuild)
   HIP_OK(hipMemcpyAsync(h_live_, d_live_, 8, hipMemcpyDeviceToHost, st));
   if (!live_ev_) HIP_OK(hipEventCreateWithFlags(&live_ev_, hipEventDisableTiming));
   HIP_OK(hipEventRecord(live_ev_, st));
@@ -1058,7 +1075,8 @@ void DeviceJoin::run(int k, const uint8_t* hb, uint32_t n_ev, uint64_t n_bytes, 
     heads_cap_ = table_cap_;
   }
   a.slot_head = d_slot_head_; a.big = d_big_; a.group_sort = group_sort_ ? 1 : 0;
-  a.table = d_table_; a.table_mask = table_cap_ - 1; a.table_bits = table_bits_;
+  if (keys_stale_ || keys_cap_ != table_cap_) sync_keys();
+  a.table = d_table_; a.keys = d_keys_; a.table_mask = table_cap_ - 1; a.table_bits = table_bits_;
   a.pool = d_pool_; a.pool_ring = d_pool_ring_; a.pool_mask = pool_n_ - 1;
   a.reg = d_reg_; a.reg_mask = (1u << cfg_.reg_bits) - 1; a.miss = d_miss_; a.miss_cap = miss_cap_;
   a.arena = d_arena_; a.arena_cap = cfg_.arena_cap; a.arena_base = arena_head_; a.arena_limit = arena_limit;
@@ -1306,10 +1324,13 @@ size_t DeviceJoin::trim(double now) {
   const size_t before = device_bytes_;
   const uint64_t tg = table_grows_, ag = arena_grows_;  // (a shrink is not a growth event)
   auto pow2_at_least = [](uint64_t v) { uint64_t p = 1; while (p < v) p <<= 1; return p; };
-  // key table: an exact live count first (same-size rebuild, expired keys dropped at `now`)
-  rebuild_table(now, table_cap_);
-  const uint64_t want = std::max<uint64_t>(init_table_cap_, pow2_at_least(std::max<uint64_t>(keys_live_ * 4, 8)));
-  if (want < table_cap_) rebuild_table(now, (uint32_t)want);  // reinserts into a fresh, smaller table
+  // key table: an exact live count first (same-size rebuild, expired keys dropped at `now`) --
+  // only when the table is above its configured size (else nothing can shrink: no rebuild)
+  if (table_cap_ > init_table_cap_) {
+    rebuild_table(now, table_cap_);
+    const uint64_t want = std::max<uint64_t>(init_table_cap_, pow2_at_least(std::max<uint64_t>(keys_live_ * 4, 8)));
+    if (want < table_cap_) rebuild_table(now, (uint32_t)want);  // reinserts into a fresh, smaller table
+  }
   if (d_table_spare_) {  // (re-made on demand: checkpoint compaction, APM_REBUILD_COPY)
     dfree(d_table_spare_, (size_t)table_cap_ * sizeof(KeyState));
     d_table_spare_ = nullptr;
@@ -1653,6 +1674,7 @@ void DeviceJoin::load(BinReader& rd) {
     keys_live_ = live.size();
     keys_since_rebuild_ = 0;
     live_pending_ = false;
+    sync_keys();
   }
   {
     const uint32_t saved_cap = rd.pod<uint32_t>();

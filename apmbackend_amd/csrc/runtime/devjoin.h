@@ -250,6 +250,12 @@ class DeviceJoin {
   DJArgs a_{};
   DJFormatArgs f_{};
   KeyState* d_table_ = nullptr;
+  // dense key array probed by k_claim (DJArgs::keys), re-derived from the table after every
+  // rewrite other than k_claim's (rebuilds, restore): sync_keys()
+  uint64_t* d_keys_ = nullptr;
+  uint32_t keys_cap_ = 0;
+  bool keys_stale_ = true;
+  void sync_keys();
   unsigned long long* d_cstats_ = nullptr;  // cache_stats result (5 counters)
   unsigned long long* h_cstats_ = nullptr;  // (pinned)
   unsigned long long cstats_last_[5] = {0, 0, 0, 0, 0};

@@ -350,19 +350,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   d_watermark_ = (unsigned long long*)dmalloc(8);
   d_file_open_ = (uint8_t*)dmalloc(1 << 16);
   // stats
-  d_counts_cells_ = (int32_t*)dmalloc((size_t)NSLOT * S * 4);
-  d_cells_ = (int32_t*)dmalloc((size_t)NSLOT * S * cfg_.cell_cap * 4);
-  d_spill_n_ = (int32_t*)dmalloc(NSLOT * 4);
   init_spill_cap_ = cfg_.spill_cap;
-  d_spill_series_ = (int32_t*)dmalloc((size_t)NSLOT * cfg_.spill_cap * 4);
-  d_spill_val_ = (int32_t*)dmalloc((size_t)NSLOT * cfg_.spill_cap * 4);
-  d_spill_series_alt_ = (int32_t*)dmalloc((size_t)NSLOT * cfg_.spill_cap * 4);
-  d_spill_val_alt_ = (int32_t*)dmalloc((size_t)NSLOT * cfg_.spill_cap * 4);
-  spill_tmp_bytes_ = apm_spill_sort_tmp_bytes(cfg_.spill_cap, S);
-  d_spill_tmp_ = dmalloc(spill_tmp_bytes_);
-  HIP_OK(hipHostMalloc((void**)&h_spill_snap_, NSLOT * 4, hipHostMallocDefault));
-  HIP_OK(hipHostGetDevicePointer((void**)&hd_spill_snap_, h_spill_snap_, 0));
-  std::memset(h_spill_snap_, 0, NSLOT * 4);
+  alloc_ring(std::max(cfg_.nslot, ring_slots_for(cfg_.window, cfg_.buffer)));
   for (auto& m : spill_mark_) HIP_OK(hipEventCreateWithFlags(&m.ev, hipEventDisableTiming));
   metrics_.spill_capacity = cfg_.spill_cap;
   d_spill_drop_ = (unsigned long long*)dmalloc(64);
@@ -379,7 +368,6 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   d_nan_list_ = (int32_t*)dmalloc((size_t)S * 4);
   d_nan_n_ = d_big_n_ + 1;
   d_js_scratch_ = (int32_t*)dmalloc((size_t)JS_BLOCKS * kJsCap * 4);
-  for (int i = 0; i < NSLOT; ++i) slot_bucket_[i] = NO_BUCKET;
   // z-score
   for (int l = 0; l < cfg_.n_lags; ++l) {
     LagState& L = lag_[l];
@@ -1691,13 +1679,15 @@ void Engine::grow_tx_capacity(uint32_t need, uint32_t keep) {
 
 StatsState Engine::stats_state() const {
   StatsState st{d_counts_cells_, d_cells_, d_spill_n_, d_spill_series_, d_spill_val_, d_active_,
-                cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series, d_spill_drop_};
+                cfg_.cell_cap, cfg_.spill_cap, cfg_.max_series};
+  st.spill_drop = d_spill_drop_;
   st.nan_until = d_nan_until_;
   st.ord_list = d_ord_list_;
   st.ord_n = d_ord_n_;
   st.ord_done = (uint32_t*)(d_ord_n_ + 1);
   st.keep = (int32_t)(cfg_.window + cfg_.buffer);
   st.spill_snap = hd_spill_snap_;
+  st.nslot = nslot_;
   return st;
 }
 
@@ -1714,7 +1704,7 @@ void Engine::spill_reserve(uint32_t n) {
     if (hipEventQuery(m.ev) == hipSuccess) { mk = &m; break; }
   }
   int64_t worst = 0;
-  for (int s = 0; s < NSLOT; ++s) {
+  for (int s = 0; s < nslot_; ++s) {
     if (slot_bucket_[s] == NO_BUCKET) continue;
     int64_t b = (int64_t)(spill_added_ - spill_clear_at_[s]);
     if (mk && spill_clear_at_[s] <= mk->added) b = std::min<int64_t>(b, (int64_t)h_spill_snap_[s] + (int64_t)(spill_added_ - mk->added));
@@ -1724,28 +1714,28 @@ void Engine::spill_reserve(uint32_t n) {
   // the bound is too loose: read the exact levels (stream drain, rare), then grow if needed
   spill_resync();
   worst = 0;
-  for (int s = 0; s < NSLOT; ++s)
+  for (int s = 0; s < nslot_; ++s)
     if (slot_bucket_[s] != NO_BUCKET) worst = std::max<int64_t>(worst, h_spill_snap_[s]);
   if (worst + (int64_t)n <= cfg_.spill_cap) return;
   int64_t cap = cfg_.spill_cap;
   while (worst + (int64_t)n > cap) cap *= 2;
-  if (cap > INT32_MAX / NSLOT) throw std::runtime_error("bucket spill lists beyond 2^31 entries");
+  if (cap > INT32_MAX / nslot_) throw std::runtime_error("bucket spill lists beyond 2^31 entries");
   grow_spill((int32_t)cap);
 }
 
 // exact fill levels now (drains the stats stream): the newest snapshot, every older one retired
 void Engine::spill_resync() {
   HIP_OK(hipStreamSynchronize(stream_));
-  std::vector<int32_t> exact(NSLOT);
-  HIP_OK(hipMemcpy(exact.data(), d_spill_n_, NSLOT * 4, hipMemcpyDeviceToHost));
+  std::vector<int32_t> exact(nslot_);
+  HIP_OK(hipMemcpy(exact.data(), d_spill_n_, (size_t)nslot_ * 4, hipMemcpyDeviceToHost));
   for (auto& m : spill_mark_) m.live = false;
-  std::memcpy(h_spill_snap_, exact.data(), NSLOT * 4);
+  std::memcpy(h_spill_snap_, exact.data(), (size_t)nslot_ * 4);
   spill_mark_[0].added = spill_added_;
   spill_mark_[0].live = true;
   HIP_OK(hipEventRecord(spill_mark_[0].ev, stream_));
   HIP_OK(hipEventSynchronize(spill_mark_[0].ev));
   spill_mark_k_ = 1;
-  for (int s = 0; s < NSLOT; ++s) spill_clear_at_[s] = std::min(spill_clear_at_[s], spill_added_);
+  for (int s = 0; s < nslot_; ++s) spill_clear_at_[s] = std::min(spill_clear_at_[s], spill_added_);
 }
 
 // after an append's kernels were queued: its snapshot point
@@ -1755,6 +1745,73 @@ void Engine::spill_marked() {
   m.live = true;
   HIP_OK(hipEventRecord(m.ev, stream_));
   spill_mark_k_ = (spill_mark_k_ + 1) % kSpillMarks;
+}
+
+int32_t ring_slots_for(int window, int buffer) { return std::max<int32_t>(NSLOT_MIN, window + buffer + 1); }
+
+// The bucket ring at `nslot` slots: cells, counts, spill lists (+ their sort targets), the
+// host's fill snapshot and slot table.  Fresh (every slot free).
+void Engine::alloc_ring(int32_t nslot) {
+  const int32_t S = cfg_.max_series;
+  nslot_ = nslot;
+  d_counts_cells_ = (int32_t*)dmalloc((size_t)nslot * S * 4);
+  d_cells_ = (int32_t*)dmalloc((size_t)nslot * S * cfg_.cell_cap * 4);
+  d_spill_n_ = (int32_t*)dmalloc((size_t)nslot * 4);
+  d_spill_series_ = (int32_t*)dmalloc((size_t)nslot * cfg_.spill_cap * 4);
+  d_spill_val_ = (int32_t*)dmalloc((size_t)nslot * cfg_.spill_cap * 4);
+  d_spill_series_alt_ = (int32_t*)dmalloc((size_t)nslot * cfg_.spill_cap * 4);
+  d_spill_val_alt_ = (int32_t*)dmalloc((size_t)nslot * cfg_.spill_cap * 4);
+  spill_tmp_bytes_ = apm_spill_sort_tmp_bytes(cfg_.spill_cap, S, nslot);
+  d_spill_tmp_ = dmalloc(spill_tmp_bytes_);
+  d_win_slots_ = (int32_t*)dmalloc((size_t)nslot * 4);
+  HIP_OK(hipHostMalloc((void**)&h_spill_snap_, (size_t)nslot * 4, hipHostMallocDefault));
+  HIP_OK(hipHostGetDevicePointer((void**)&hd_spill_snap_, h_spill_snap_, 0));
+  std::memset(h_spill_snap_, 0, (size_t)nslot * 4);
+  slot_bucket_.assign((size_t)nslot, NO_BUCKET);
+  spill_clear_at_.assign((size_t)nslot, 0);
+}
+
+// A reload to a window the ring cannot hold (stream_calc_stats.js:228-261 takes any size): the
+// ring is re-made at `nslot` slots and every live bucket's cells, counts and spill list move to
+// slot b % nslot.  Stats thread, between rollovers (the stream is drained first).
+void Engine::grow_ring(int32_t nslot) {
+  if (nslot <= nslot_) return;
+  HIP_OK(hipStreamSynchronize(stream_));
+  const int32_t S = cfg_.max_series, cap = cfg_.cell_cap, sc = cfg_.spill_cap;
+  int32_t* o_counts = d_counts_cells_;
+  int32_t* o_cells = d_cells_;
+  int32_t* o_sn = d_spill_n_;
+  int32_t* o_ss = d_spill_series_;
+  int32_t* o_sv = d_spill_val_;
+  const std::vector<int64_t> o_bucket = slot_bucket_;
+  const std::vector<uint64_t> o_clear = spill_clear_at_;
+  std::vector<int32_t> o_snap(h_spill_snap_, h_spill_snap_ + nslot_);
+  for (void* p : {(void*)d_spill_series_alt_, (void*)d_spill_val_alt_, d_spill_tmp_, (void*)d_win_slots_}) dfree(p);
+  HIP_OK(hipHostFree(h_spill_snap_));
+  if (d_ck_slots_) { dfree(d_ck_slots_); d_ck_slots_ = nullptr; }  // (sized by the ring: re-made on demand)
+  const int32_t o_n = nslot_;
+  alloc_ring(nslot);
+  for (int32_t s = 0; s < o_n; ++s) {
+    const int64_t b = o_bucket[(size_t)s];
+    if (b == NO_BUCKET) continue;
+    const int32_t t = (int32_t)(((b % nslot) + nslot) % nslot);
+    HIP_OK(hipMemcpyAsync(d_counts_cells_ + (size_t)t * S, o_counts + (size_t)s * S, (size_t)S * 4,
+                          hipMemcpyDeviceToDevice, stream_));
+    HIP_OK(hipMemcpyAsync(d_cells_ + (size_t)t * S * cap, o_cells + (size_t)s * S * cap, (size_t)S * cap * 4,
+                          hipMemcpyDeviceToDevice, stream_));
+    HIP_OK(hipMemcpyAsync(d_spill_n_ + t, o_sn + s, 4, hipMemcpyDeviceToDevice, stream_));
+    HIP_OK(hipMemcpyAsync(d_spill_series_ + (size_t)t * sc, o_ss + (size_t)s * sc, (size_t)sc * 4,
+                          hipMemcpyDeviceToDevice, stream_));
+    HIP_OK(hipMemcpyAsync(d_spill_val_ + (size_t)t * sc, o_sv + (size_t)s * sc, (size_t)sc * 4,
+                          hipMemcpyDeviceToDevice, stream_));
+    slot_bucket_[(size_t)t] = b;
+    spill_clear_at_[(size_t)t] = o_clear[(size_t)s];
+    h_spill_snap_[t] = o_snap[(size_t)s];
+  }
+  HIP_OK(hipStreamSynchronize(stream_));
+  for (void* p : {(void*)o_counts, (void*)o_cells, (void*)o_sn, (void*)o_ss, (void*)o_sv}) dfree(p);
+  spill_resync();  // fill levels at the new slots
+  ++ring_grows_;
 }
 
 // Every slot list keeps its entries at the same positions of a longer row.
@@ -1767,10 +1824,10 @@ void Engine::resize_spill(int32_t cap) {
   HIP_OK(hipStreamSynchronize(stream_));
   const size_t old = (size_t)cfg_.spill_cap;
   const size_t w = std::min(old, (size_t)cap) * 4;  // (a shrink keeps every slot's fill: cap >= it)
-  int32_t* ser = (int32_t*)dmalloc((size_t)NSLOT * cap * 4);
-  int32_t* val = (int32_t*)dmalloc((size_t)NSLOT * cap * 4);
-  HIP_OK(hipMemcpy2DAsync(ser, (size_t)cap * 4, d_spill_series_, old * 4, w, NSLOT, hipMemcpyDeviceToDevice, stream_));
-  HIP_OK(hipMemcpy2DAsync(val, (size_t)cap * 4, d_spill_val_, old * 4, w, NSLOT, hipMemcpyDeviceToDevice, stream_));
+  int32_t* ser = (int32_t*)dmalloc((size_t)nslot_ * cap * 4);
+  int32_t* val = (int32_t*)dmalloc((size_t)nslot_ * cap * 4);
+  HIP_OK(hipMemcpy2DAsync(ser, (size_t)cap * 4, d_spill_series_, old * 4, w, nslot_, hipMemcpyDeviceToDevice, stream_));
+  HIP_OK(hipMemcpy2DAsync(val, (size_t)cap * 4, d_spill_val_, old * 4, w, nslot_, hipMemcpyDeviceToDevice, stream_));
   HIP_OK(hipStreamSynchronize(stream_));
   dfree(d_spill_series_);
   dfree(d_spill_val_);
@@ -1779,10 +1836,10 @@ void Engine::resize_spill(int32_t cap) {
   dfree(d_spill_tmp_);
   d_spill_series_ = ser;
   d_spill_val_ = val;
-  d_spill_series_alt_ = (int32_t*)dmalloc((size_t)NSLOT * cap * 4);
-  d_spill_val_alt_ = (int32_t*)dmalloc((size_t)NSLOT * cap * 4);
+  d_spill_series_alt_ = (int32_t*)dmalloc((size_t)nslot_ * cap * 4);
+  d_spill_val_alt_ = (int32_t*)dmalloc((size_t)nslot_ * cap * 4);
   cfg_.spill_cap = cap;
-  spill_tmp_bytes_ = apm_spill_sort_tmp_bytes(cfg_.spill_cap, cfg_.max_series);
+  spill_tmp_bytes_ = apm_spill_sort_tmp_bytes(cfg_.spill_cap, cfg_.max_series, nslot_);
   d_spill_tmp_ = dmalloc(spill_tmp_bytes_);
   metrics_.spill_capacity = cap;
 }
@@ -1795,8 +1852,8 @@ std::pair<size_t, size_t> Engine::trim_device_memory() {
   if (dj_) dj_->trim(watermark_);
   // spill lists: back to max(configured, 2x the fullest slot)
   {
-    std::vector<int32_t> fill(NSLOT);
-    HIP_OK(hipMemcpy(fill.data(), d_spill_n_, NSLOT * 4, hipMemcpyDeviceToHost));
+    std::vector<int32_t> fill(nslot_);
+    HIP_OK(hipMemcpy(fill.data(), d_spill_n_, (size_t)nslot_ * 4, hipMemcpyDeviceToHost));
     int32_t mx = 0;
     for (int32_t f : fill) mx = std::max(mx, std::min(f, cfg_.spill_cap));
     const int32_t want = std::max<int32_t>(init_spill_cap_, ((2 * mx + 1023) / 1024) * 1024);
@@ -1815,8 +1872,12 @@ std::pair<size_t, size_t> Engine::trim_device_memory() {
     d_ck_text_[k] = nullptr;
     ck_text_cap_[k] = 0;
   }
-  free_ck_stage();
-  if (d_ck_defer_) {  // the deferred small-section staging (the writer is idle: checkpoint_wait)
+  // the snapshot staging is kept at what the last snapshot needed (re-allocating it at the next
+  // checkpoint would stall that checkpoint and put HBM back over the threshold): freed only when
+  // it is more than twice that
+  if (ck_stage_bytes_ > 2 * ck_last_need_) free_ck_stage();
+  if (d_ck_defer_ && ck_defer_cap_ > 2 * std::max<size_t>(ck_defer_want_, (size_t)1 << 30)) {
+    // the deferred small-section staging (the writer is idle: checkpoint_wait)
     HIP_OK(hipFree(d_ck_defer_));
     d_ck_defer_ = nullptr;
     std::lock_guard<std::mutex> g(alloc_mu_);
@@ -1837,7 +1898,7 @@ void Engine::spill_sort() {
 }
 
 void Engine::ensure_bucket_slot(int64_t b) {
-  const int slot = (int)(((b % NSLOT) + NSLOT) % NSLOT);
+  const int slot = (int)(((b % nslot_) + nslot_) % nslot_);
   if (slot_bucket_[slot] == b) return;
   if (slot_bucket_[slot] != NO_BUCKET) {
     StatsState st = stats_state();
@@ -2153,7 +2214,7 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
                                            std::chrono::system_clock::now().time_since_epoch()).count();
   ++metrics_.rollovers;
   // removeOldBuckets(36): drop every bucket < L - 36
-  for (int i = 0; i < NSLOT; ++i) {
+  for (int i = 0; i < nslot_; ++i) {
     if (slot_bucket_[i] != NO_BUCKET && slot_bucket_[i] < L - keep_iv) {
       StatsState st = stats_state();
       apm_stats_clear_slot(&st, i, stream_);
@@ -2243,11 +2304,22 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   WindowArgs wa;
   wa.st = stats_state();
   wa.n_win = (int32_t)(keep_iv - cfg_.buffer + 1);
-  for (int r = 0; r < 32; ++r) wa.win_slots[r] = -1;
-  for (int r = 0; r < wa.n_win && r < 32; ++r) {
-    const int64_t b = L - keep_iv + r;
-    const int slot = (int)(((b % NSLOT) + NSLOT) % NSLOT);
-    wa.win_slots[r] = slot_bucket_[slot] == b ? slot : -1;
+  wa.win_slots_ext = nullptr;
+  {
+    std::vector<int32_t> ws((size_t)std::max<int32_t>(wa.n_win, K8_INLINE_SLOTS), -1);
+    for (int r = 0; r < wa.n_win; ++r) {
+      const int64_t b = L - keep_iv + r;
+      const int slot = (int)(((b % nslot_) + nslot_) % nslot_);
+      ws[(size_t)r] = slot_bucket_[slot] == b ? slot : -1;
+    }
+    for (int r = 0; r < K8_INLINE_SLOTS; ++r) wa.win_slots[r] = ws[(size_t)r];
+    if (wa.n_win > K8_INLINE_SLOTS) {
+      // a window longer than the argument block (> 10 min): the whole slot list from a device
+      // array, rewritten once the previous rollover's K8 (the array's last reader) has finished
+      HIP_OK(hipStreamSynchronize(stream_));
+      HIP_OK(hipMemcpy(d_win_slots_, ws.data(), (size_t)wa.n_win * 4, hipMemcpyHostToDevice));
+      wa.win_slots_ext = d_win_slots_;
+    }
   }
   wa.tpm_div = (double)cfg_.window * cfg_.interval_len / 60.0;
   {

@@ -62,9 +62,11 @@ struct ReconfigSpec {
   std::map<std::string, ServiceOverride> overrides;
 };
 
-// Bounds of the stats window the bucket ring holds: K8 reads window + 1 buckets (at most 32
-// slots of its argument block), removeOldBuckets keeps window + buffer (NSLOT ring slots).
+// Bounds of a stats window: window >= 1, buffer >= 0, interval >= 1 (the reference's are the
+// same); removeOldBuckets keeps window + buffer buckets, so the bucket ring needs window + buffer
+// + 1 slots -- it is sized for the configured window and grows on a reload to a longer one.
 void check_window(int window, int buffer, int interval_len);
+int32_t ring_slots_for(int window, int buffer);  // max(NSLOT_MIN, window + buffer + 1)
 
 struct EngineConfig {
   int device = 0;
@@ -102,6 +104,7 @@ struct EngineConfig {
   int interval_len = 10;
   int window = 30;
   int buffer = 6;
+  int nslot = 0;  // bucket ring slots (gpu.bucketRingSlots; 0 = ring_slots_for(window, buffer))
   // parse
   double record_ttl_ms = 120000, acct_ttl_ms = 120000, need_ttl_ms = 30000;
   TzTable tz{};
@@ -275,6 +278,8 @@ class Engine {
   uint64_t reconfigs_applied() const { return reconfigs_applied_.load(); }
   uint64_t lag_set_changes() const { return lag_set_changes_.load(); }
   uint64_t window_changes() const { return window_changes_.load(); }
+  int32_t ring_slots() const { return nslot_; }
+  uint64_t ring_grows() const { return ring_grows_; }
   std::vector<int32_t> lag_values() { flush(); return std::vector<int32_t>(cfg_.lags, cfg_.lags + cfg_.n_lags); }
 
   // Process one batch. `now_override` < 0 uses the engine watermark clock.  If the caller
@@ -859,14 +864,14 @@ class Engine {
   int32_t* d_spill_val_alt_ = nullptr;
   void* d_spill_tmp_ = nullptr;
   size_t spill_tmp_bytes_ = 0;
-  int32_t* h_spill_snap_ = nullptr;   // pinned [NSLOT], written by K7 after every append
+  int32_t* h_spill_snap_ = nullptr;   // pinned [nslot_], written by K7 after every append
   int32_t* hd_spill_snap_ = nullptr;  // its device alias
   // Spill sizing (no sample is ever dropped): spill_n[slot] <= spill_bound(slot) = the exact fill
   // of the newest completed append snapshot + every sample appended after it (any may spill), or
   // every sample appended since the slot was cleared.  spill_reserve() grows the lists before an
   // append whose worst case exceeds them.
   uint64_t spill_added_ = 0;
-  uint64_t spill_clear_at_[NSLOT] = {};
+  std::vector<uint64_t> spill_clear_at_;  // [nslot_]
   struct SpillMark { hipEvent_t ev = nullptr; uint64_t added = 0; bool live = false; };
   static constexpr int kSpillMarks = 4;
   SpillMark spill_mark_[kSpillMarks];
@@ -878,7 +883,13 @@ class Engine {
   void spill_sort();
   unsigned long long* d_spill_drop_ = nullptr;  // K7 samples lost to a full spill list
   uint8_t* d_active_ = nullptr;
-  int64_t slot_bucket_[NSLOT];
+  // bucket ring: bucket b lives in slot b % nslot_ (slot_bucket_[slot], NO_BUCKET = free)
+  int32_t nslot_ = NSLOT_MIN;
+  std::vector<int64_t> slot_bucket_;
+  uint64_t ring_grows_ = 0;
+  int32_t* d_win_slots_ = nullptr;  // K8's window slots when the window is longer than K8_INLINE_SLOTS
+  void alloc_ring(int32_t nslot);   // the ring's device / pinned arrays at nslot slots (fresh engine)
+  void grow_ring(int32_t nslot);    // the same with every live bucket moved to its new slot
   int64_t latest_ = 0;
   int64_t rollover_idx_ = 0;
   WinStat* d_win_ = nullptr;
@@ -935,6 +946,11 @@ class Engine {
   bool ck_busy_ = false, ck_stop_ = false, ck_all_dirty_ = true;
   std::string ck_error_, ck_prefix_;
   std::vector<std::string> ck_chain_;
+  // the chain a base replaced, kept on disk as <prefix>.prev.ckpt until the next base: every rank
+  // of a lock-step node then still holds a batch common to all ranks when one of them dies while
+  // the others write an aligned base (finish_chain)
+  std::vector<std::string> ck_prev_chain_;
+  bool ck_disk_chains_read_ = false;
   int64_t ck_seq_ = 0, ck_ridx_ = 0;
   int ck_last_mode_ = 0;
   uint64_t ck_done_ = 0, ck_skipped_ = 0, ck_sync_fallbacks_ = 0, ck_last_bytes_ = 0;
@@ -942,6 +958,7 @@ class Engine {
   double ck_last_stall_ms_ = 0, ck_last_write_ms_ = 0;
   void* d_ck_stage_ = nullptr;
   size_t ck_stage_bytes_ = 0;
+  size_t ck_last_need_ = 0;  // ring staging the last snapshot needed (trim keeps up to 2x)
   void* h_ck_bounce_ = nullptr;
   size_t ck_blob_hint_ = 0;         // size of the last small-section blob (reserve)
   char* d_ck_text_[2] = {nullptr, nullptr};  // pending-line text gathered for a checkpoint

@@ -99,7 +99,7 @@ struct Input {
   double watermark = 0;
   uint64_t batch_no = 0;
   int64_t latest = 0, rollover_idx = 0, next_gid = 0;
-  int64_t slot_bucket[NSLOT] = {};
+  std::vector<int64_t> slot_bucket;  // the saver's ring (its slot count)
   uint32_t line_block_seq = 0;
   // join
   JoinCounts jc{};
@@ -170,7 +170,7 @@ void read_small(Input& in, const std::string& path) {
 
   rd.begin(SEC_CLOCK);
   rd.pod(in.watermark); rd.pod(in.batch_no); rd.pod(in.latest); rd.pod(in.rollover_idx);
-  rd.raw(in.slot_bucket, sizeof(in.slot_bucket));
+  in.slot_bucket = rd.vec<int64_t>();
   rd.pod(in.next_gid); rd.pod(in.line_block_seq);
 
   rd.begin(SEC_JOIN);
@@ -353,7 +353,7 @@ MergeResult merge_checkpoints(const std::vector<std::string>& inputs, const std:
         x.cell_cap != I0.cell_cap || x.window != I0.window || x.buffer != I0.buffer)
       throw std::runtime_error("merge: the input checkpoints were written with different configurations");
     if (x.batch_no != I0.batch_no || x.latest != I0.latest || x.rollover_idx != I0.rollover_idx ||
-        std::memcmp(x.slot_bucket, I0.slot_bucket, sizeof(x.slot_bucket)) != 0)
+        x.slot_bucket != I0.slot_bucket)
       throw std::runtime_error("merge: the inputs are not one lock-step batch (clocks / bucket slots differ)");
   }
   const size_t rb = (size_t)I0.ring_bytes;
@@ -662,7 +662,7 @@ MergeResult merge_checkpoints(const std::vector<std::string>& inputs, const std:
     uint32_t lbs = I0.line_block_seq;
     for (const Input& x : in) { wm = std::max(wm, x.watermark); ng = std::max(ng, x.next_gid); lbs = std::max(lbs, x.line_block_seq); }
     w.pod(wm); w.pod(I0.batch_no); w.pod(I0.latest); w.pod(I0.rollover_idx);
-    w.raw(I0.slot_bucket, sizeof(I0.slot_bucket));
+    w.vec(I0.slot_bucket);
     w.pod(ng); w.pod(lbs);
   }
   w.end();

@@ -34,11 +34,11 @@ double now_ms() {
 }  // namespace
 
 void check_window(int window, int buffer, int interval_len) {
-  if (window < 1 || window + 1 > 32 || buffer < 0 || window + buffer + 1 > NSLOT || interval_len < 1)
-    throw std::runtime_error("stats window: windowSizeInIntervals 1..31, windowSizeInIntervals + bufferSizeInIntervals "
-                             "<= " + std::to_string(NSLOT - 1) + ", intervalLengthInSeconds >= 1 (got " +
-                             std::to_string(window) + " / " + std::to_string(buffer) + " / " +
-                             std::to_string(interval_len) + ")");
+  // (the ring holds any window the HBM does: window + buffer + 1 slots of maxSeries cells each)
+  if (window < 1 || buffer < 0 || interval_len < 1 || (int64_t)window + buffer > (1 << 20))
+    throw std::runtime_error("stats window: windowSizeInIntervals >= 1, bufferSizeInIntervals >= 0, "
+                             "intervalLengthInSeconds >= 1 (got " + std::to_string(window) + " / " +
+                             std::to_string(buffer) + " / " + std::to_string(interval_len) + ")");
 }
 
 void Engine::stage_reconfig(const ReconfigSpec& spec) {
@@ -173,6 +173,8 @@ void Engine::apply_reconfig(const ReconfigSpec& r) {
       for (auto& v : nu) v += dk;  // (never poisoned: 0x80808080, far below any bucket either way)
       HIP_OK(hipMemcpy(d_nan_until_, nu.data(), nu.size() * 4, hipMemcpyHostToDevice));
     }
+    // a longer window than the ring holds: grow it first (live buckets keep their samples)
+    grow_ring(ring_slots_for(r.window, r.buffer));
     cfg_.window = r.window;
     cfg_.buffer = r.buffer;
     ++window_changes_;

@@ -78,10 +78,10 @@ BucketDump Engine::export_buckets() {
   BucketDump d;
   d.latest = latest_;
   const int32_t S = cfg_.max_series, n = n_series_, cap = cfg_.cell_cap;
-  std::vector<int32_t> spill_n(NSLOT), counts(n), cells((size_t)n * cap);
-  HIP_OK(hipMemcpy(spill_n.data(), d_spill_n_, NSLOT * 4, hipMemcpyDeviceToHost));
+  std::vector<int32_t> spill_n(nslot_), counts(n), cells((size_t)n * cap);
+  HIP_OK(hipMemcpy(spill_n.data(), d_spill_n_, (size_t)nslot_ * 4, hipMemcpyDeviceToHost));
   std::vector<int64_t> slots;
-  for (int slot = 0; slot < NSLOT; ++slot)
+  for (int slot = 0; slot < nslot_; ++slot)
     if (slot_bucket_[slot] != NO_BUCKET) slots.push_back(slot);
   std::sort(slots.begin(), slots.end(), [&](int a, int b) { return slot_bucket_[a] < slot_bucket_[b]; });
   for (int64_t slot : slots) {
@@ -130,7 +130,7 @@ void Engine::import_buckets(int64_t latest, const std::vector<int32_t>& series, 
     if (bucket[i] >= latest - keep && bucket[i] <= latest) by_bucket[bucket[i]].push_back(i);
   for (auto& kv : by_bucket) {
     const int64_t b = kv.first;
-    const int slot = (int)(((b % NSLOT) + NSLOT) % NSLOT);
+    const int slot = (int)(((b % nslot_) + nslot_) % nslot_);
     if (slot_bucket_[slot] != NO_BUCKET && slot_bucket_[slot] != b) throw std::runtime_error("import_buckets: slot clash");
     slot_bucket_[slot] = b;
     std::vector<int32_t> counts(n, 0), cells((size_t)n * cap, 0), sp_s, sp_v;

@@ -32,7 +32,7 @@ OUT_KINDS = ("transactions", "audit_db", "db", "st", "fs", "al", "sx", "fb")
 # What the reference persists (db_insert queue): released + audit tx, fs, al.  `transactions`
 # and `st` are internal hand-offs that only the AMQP bridge needs.
 DB_OUTPUTS = ("audit_db", "db", "fs", "al")
-MAX_LAGS = 8  # apm_types.h MAX_LAGS: LAG settings per engine
+MAX_LAGS = 16  # apm_types.h MAX_LAGS: LAG capacity per engine (each LAG is an HBM ring; see there)
 
 
 def output_mask(kinds) -> int:
@@ -86,6 +86,8 @@ def engine_config(cfg: Dict[str, Any], device: int = 0, keep_text: bool = False,
         "alert_clock_entry": 1 if g.get("alertClock", "entry") == "entry" else 0,
         "interval_len": int(sc["intervalLengthInSeconds"]),
         "window": int(sc["windowSizeInIntervals"]),
+        # bucket ring slots (0: window + buffer + 1, at least 40); a reload to a longer window grows it
+        "nslot": int(g.get("bucketRingSlots", 0)),
         "buffer": int(sc["bufferSizeInIntervals"]),
         "record_ttl_ms": float(g.get("recordTtlSeconds", 120)) * 1000.0,
         "acct_ttl_ms": float(g.get("acctTtlSeconds", 120)) * 1000.0,
@@ -111,8 +113,8 @@ def engine_config(cfg: Dict[str, Any], device: int = 0, keep_text: bool = False,
     # intervalLengthInSeconds only scales the TPM divisor: the bucket label is endTs without its
     # last 4 digits whatever the interval (stream_calc_stats.js:89-96, :186), as here
     w, b = d["window"], d["buffer"]
-    if not (1 <= w <= 31 and b >= 0 and w + b <= 39 and d["interval_len"] >= 1):
-        raise ValueError(f"stats window: windowSizeInIntervals 1..31, window + bufferSizeInIntervals <= 39, "
+    if not (w >= 1 and b >= 0 and d["interval_len"] >= 1):
+        raise ValueError(f"stats window: windowSizeInIntervals >= 1, bufferSizeInIntervals >= 0, "
                          f"intervalLengthInSeconds >= 1 (got {w} / {b} / {d['interval_len']})")
     d.update(kw)
     return d

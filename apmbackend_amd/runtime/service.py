@@ -356,6 +356,71 @@ class IngestService:
             return False
         return True
 
+    def _chain_batches(self, rank: int) -> Dict[int, str]:
+        """batch -> chain manifest of rank `rank` that holds a checkpoint at that batch, over its
+        current and its previous chain (engine.rank<r>.ckpt / .prev.ckpt, checkpoint.cpp
+        finish_chain)."""
+        N = _native_mod()
+        out: Dict[int, str] = {}
+        for name in (f"engine.rank{rank}.prev.ckpt", f"engine.rank{rank}.ckpt"):
+            p = os.path.join(self.ckpt_dir, name)
+            if not os.path.exists(p):
+                continue
+            try:
+                for b, f in N.checkpoint_batches(p):
+                    if os.path.exists(f):
+                        out[int(b)] = p
+            except Exception as e:  # an unreadable chain: that rank offers no batch from it
+                log.warning("checkpoint chain %s unreadable: %s", p, e)
+        return out
+
+    def _node_common_batch(self, ranks) -> Tuple[int, Dict[int, str]]:
+        """The newest batch every one of `ranks` holds a checkpoint at (lock-step ranks checkpoint
+        at the same batches), and per rank the manifest holding it; (0, {}) when there is none.
+        Computed from the files alone, so every rank of the node arrives at the same batch."""
+        per = {r: self._chain_batches(r) for r in ranks}
+        common = set.intersection(*(set(v) for v in per.values())) if per else set()
+        if not common:
+            return 0, {}
+        b = max(common)
+        return b, {r: per[r][b] for r in ranks}
+
+    def _load_at(self, manifest: str, batch: int) -> bytes:
+        """load_state of `manifest`'s chain prefix that ends at `batch` (a truncated manifest next
+        to the original: the files are shared)."""
+        N = _native_mod()
+        files = [f for b, f in N.checkpoint_batches(manifest)]
+        bs = [int(b) for b, f in N.checkpoint_batches(manifest)]
+        if bs and bs[-1] == batch:
+            return self.eng.load_state(manifest)
+        k = bs.index(batch)
+        keep = [os.path.basename(x) for x in files[:k + 1]]
+        tmp = os.path.join(self.ckpt_dir, f".restore.rank{self.rank}.{os.getpid()}.ckpt")
+        with open(tmp, "w") as f:
+            f.write("APMCHAIN 1\n" + "".join(x + "\n" for x in keep))
+        try:
+            extra = self.eng.load_state(tmp)
+        except Exception:
+            os.remove(tmp)
+            raise
+        # the timeline continues from `batch`: this rank's checkpoints after it are void (their
+        # batch numbers will be reused) -- the prefix becomes the current chain, the rest goes
+        cur = os.path.join(self.ckpt_dir, f"engine.rank{self.rank}.ckpt")
+        prev = os.path.join(self.ckpt_dir, f"engine.rank{self.rank}.prev.ckpt")
+        void = [os.path.basename(x) for x in files[k + 1:]]
+        if os.path.abspath(manifest) == os.path.abspath(prev) and os.path.exists(cur):
+            void += [os.path.basename(f) for _b, f in N.checkpoint_batches(cur)]
+            os.remove(prev)
+        os.replace(tmp, cur)
+        for name in set(void) - set(keep):
+            try:
+                os.remove(os.path.join(self.ckpt_dir, name))
+            except OSError:
+                pass
+        log.warning("rank %d resumed at batch %d, the newest batch every rank holds: its %d later checkpoint "
+                    "file(s) were dropped", self.rank, batch, len(set(void) - set(keep)))
+        return extra
+
     def _restore(self) -> bool:
         ck, _ = self._ckpt_paths()
         if not os.path.exists(ck) and not glob.glob(os.path.join(self.ckpt_dir, "tail.rank*.json")):
@@ -373,8 +438,17 @@ class IngestService:
             self.resharded = True
             return False
         try:
-            self._ckpt_extra = self.eng.load_state(ck)
-            log.info("resumed engine state from %s", ck)
+            # lock-step ranks resume at the newest batch EVERY rank holds (a rank that died while
+            # the others checkpointed has an older newest file): same batch, same clocks everywhere
+            at, where = (0, {})
+            if self.world > 1:
+                at, where = self._node_common_batch(range(self.world))
+            if at and where.get(self.rank):
+                self._ckpt_extra = self._load_at(where[self.rank], at)
+                log.info("resumed engine state from %s at batch %d (newest batch of every rank)", where[self.rank], at)
+            else:
+                self._ckpt_extra = self.eng.load_state(ck)
+                log.info("resumed engine state from %s", ck)
             known = {p for p, _k, _s in self.native.files()}
             for f in self.files:  # files that appeared since the checkpoint
                 if f not in known:
@@ -433,9 +507,17 @@ class IngestService:
             log.warning("re-shard: checkpoints %s missing: this shard starts fresh", missing)
             return False
         N = _native_mod()
+        # one restore batch for the whole node: the newest batch EVERY old rank holds (not only the
+        # inputs of this rank -- two new ranks must start from the same batch, clocks and bucket
+        # slots), taken from each old rank's current or previous chain
+        at, where = self._node_common_batch(sorted(old))
+        if not at:
+            log.warning("re-shard: the old ranks' checkpoints share no batch: servers %s start fresh", sorted(mine))
+            return False
+        paths = [where[r] for r in inputs]
         out = os.path.join(self.ckpt_dir, f"engine.rank{self.rank}.resharded.{os.getpid()}.ckpt")
         t0 = time.perf_counter()
-        info = N.merge_checkpoints(paths, sorted(mine), out, b"")
+        info = N.merge_checkpoints(paths, sorted(mine), out, b"", at)
         try:
             self.eng.load_state(out)
         finally:

@@ -39,6 +39,7 @@ GPU_DEFAULTS: Dict[str, Any] = {
     "maxServices": 1 << 16,           # distinct service-name capacity
     "maxServers": 1024,
     "bucketCellCapacity": 16,         # samples per (series, 10 s bucket) kept inline
+    "bucketRingSlots": 0,             # bucket ring slots (0 = window + buffer + 1, at least 40; grows on reload)
     "bucketOverflowCapacity": 1 << 22,  # spill area for hot series
     "batchBytes": 32 << 20,           # bytes of raw log per ingest batch
     "maxLinesPerBatch": 1 << 20,

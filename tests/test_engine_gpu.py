@@ -561,6 +561,49 @@ def test_incremental_checkpoint_chain_resume(tmp_path, mode):
         assert out[k] == full[k], k
 
 
+def test_base_checkpoint_keeps_the_previous_chain(tmp_path):
+    """a new base keeps the chain it replaces as <prefix>.prev.ckpt (a lock-step peer
+    that died while the node wrote an aligned base still shares a batch with the survivors); the
+    chain before that one is deleted.  Restoring from the previous chain continues exactly like
+    the uninterrupted run."""
+    lines, bl = synth_batches(7, duration=900)
+    C = small_cfg("exact")
+    _, full = _run_engine(C, bl)
+    n = len(bl)
+    cuts = {n // 5: False, (2 * n) // 5: False, (3 * n) // 5: True, (4 * n) // 5: True}  # batch -> force base
+    eng = APMEngine(C, keep_text=True)
+    out = collections.defaultdict(list)
+    upto = collections.defaultdict(list)  # outputs through the third checkpoint (base B)
+    prefix = str(tmp_path / "engine.rank0")
+    chains = []
+    for i, (now, chunks) in enumerate(bl[:max(cuts)]):
+        eng.process_lines(chunks, now)
+        for k in ("transactions", "audit_db", "st", "fs", "al"):
+            out[k] += eng.take(k)
+        if i + 1 in cuts:
+            assert eng.checkpoint_async(prefix, b"%d" % i, cuts[i + 1]) > 0
+            eng.checkpoint_wait()
+            chains.append(open(prefix + ".ckpt").read().split()[2:])
+            if i + 1 == (3 * n) // 5:
+                upto = {k: list(v) for k, v in out.items()}
+    a_files, b_files, c_files = chains[1], chains[2], chains[3]
+    assert len(a_files) == 2 and len(b_files) == 1 and len(c_files) == 1
+    assert open(prefix + ".prev.ckpt").read().split()[2:] == b_files
+    for f in a_files:  # the chain before the previous one is gone
+        assert not os.path.exists(os.path.join(str(tmp_path), f))
+    for f in b_files + c_files:
+        assert os.path.exists(os.path.join(str(tmp_path), f))
+    del eng
+    eng2 = APMEngine(C, keep_text=True)
+    assert eng2.load_state(prefix + ".prev.ckpt") == b"%d" % ((3 * n) // 5 - 1)
+    for now, chunks in bl[(3 * n) // 5:]:
+        eng2.process_lines(chunks, now)
+        for k in ("transactions", "audit_db", "st", "fs", "al"):
+            upto[k] += eng2.take(k)
+    for k in ("transactions", "audit_db", "st", "fs", "al"):
+        assert upto[k] == full[k], k
+
+
 def test_host_join_tx_staging_grows_instead_of_failing():
     """Host-join mode with a tiny per-batch tx staging: the engine doubles it mid-batch (was: a
     'too many tx in one batch' exception) and the output is unchanged."""

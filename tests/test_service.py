@@ -332,3 +332,52 @@ def test_sink_snapshot_pruning_follows_commits(tmp_path):
     n4 = start(True)    # #3 committed: #1 may go now
     assert set(os.listdir(tmp_path)) == {n3, n4}
     assert svc._sink_committed == n3
+
+
+def _fake_ckpt(path, batch):
+    """A checkpoint file reduced to what checkpoint_batches reads: the binio header and SEC_CLOCK
+    (watermark, batch_no) -- binio.h / checkpoint.cpp."""
+    import struct
+    ver = 9  # binio.h kCkptVersion
+    with open(path, "wb") as f:
+        f.write(b"APMCKPT\0" + struct.pack("<I", ver))
+        f.write(struct.pack("<IQ", 4, 16) + struct.pack("<dQ", 1.0e12, batch))
+        f.write(struct.pack("<I", 0xE0F))
+
+
+def _manifest(path, names):
+    with open(path, "w") as f:
+        f.write("APMCHAIN 1\n" + "".join(n + "\n" for n in names))
+
+
+def test_node_restore_batch_is_common_to_every_rank_and_survives_a_lost_base(tmp_path):
+    """rank 1 died while the node wrote the aligned base at batch 130.  Rank 0 then
+    holds only the new base in its current chain -- its old chain (100, 110, 120) is kept as the
+    previous chain -- and rank 1 still has 100, 110, 120.  Every rank resumes (and a re-shard merges)
+    at 120, the newest batch both hold, each from the chain that has it."""
+    C, lines, mapping, sc = make_env(tmp_path, servers=2, duration=30)
+    ck = tmp_path / "ckpt"
+    ck.mkdir()
+    for r in (0, 1):
+        for b in (100, 110, 120):
+            _fake_ckpt(ck / f"engine.rank{r}.{'b' if b == 100 else 'i'}{b}.ckpt", b)
+    _fake_ckpt(ck / "engine.rank0.b130.ckpt", 130)
+    old = ["engine.rank0.b100.ckpt", "engine.rank0.i110.ckpt", "engine.rank0.i120.ckpt"]
+    _manifest(ck / "engine.rank0.ckpt", ["engine.rank0.b130.ckpt"])
+    _manifest(ck / "engine.rank0.prev.ckpt", old)
+    _manifest(ck / "engine.rank1.ckpt", [n.replace("rank0", "rank1") for n in old])
+    svc = IngestService(C, engine="cpu-oracle", files=sorted(mapping.values()), rank=0, world=2,
+                        server_of_path=srv_of)
+    svc.ckpt_dir = str(ck)
+    try:
+        assert sorted(svc._chain_batches(0)) == [100, 110, 120, 130]
+        at, where = svc._node_common_batch([0, 1])
+        assert at == 120
+        assert where == {0: str(ck / "engine.rank0.prev.ckpt"), 1: str(ck / "engine.rank1.ckpt")}
+        # rank 1 never got past 110: 110 is the node's batch
+        _manifest(ck / "engine.rank1.ckpt", [n.replace("rank0", "rank1") for n in old[:2]])
+        assert svc._node_common_batch([0, 1])[0] == 110
+        os.remove(ck / "engine.rank1.ckpt")
+        assert svc._node_common_batch([0, 1]) == (0, {})
+    finally:
+        svc.shutdown()
