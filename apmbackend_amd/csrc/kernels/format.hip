@@ -251,10 +251,22 @@ __device__ __forceinline__ uint32_t fleet_row(const FleetFormatArgs& a, int32_t 
 // streams' waves, a serial chain of 313 waves -- 100-240 us for ~1.3 MB, ~13 GB/s,
 // profiles/r5_n / r5_o timeline.)
 constexpr uint32_t FLEET_LDS = 16384;
+// Rows per wave (the other lanes carry none): a row's formatting is a long dependent chain per
+// lane, and 64 rows a wave left ~313 waves for the headline's 20k rows -- a third of the chip's
+// 1024 SIMDs with one latency-bound wave each (101 us isolated, profiles/r5_v).  16 rows a wave
+// put four times the waves in flight.  APM_FB_RPW (16 / 32 / 64) for A/B.
+int fleet_rows_per_wave() {
+  static const int v = [] {
+    const char* e = std::getenv("APM_FB_RPW");
+    const int r = e ? std::atoi(e) : 16;
+    return (r == 8 || r == 16 || r == 32 || r == 64) ? r : 16;
+  }();
+  return v;
+}
 
-__global__ __launch_bounds__(FMT_WAVE_LINES) void k_fleet_len(FleetFormatArgs a) {
+__global__ __launch_bounds__(FMT_WAVE_LINES) void k_fleet_len(FleetFormatArgs a, int rpw) {
   const int32_t n = a.n_slots * a.n_lags;
-  const int32_t i = (int32_t)blockIdx.x * FMT_WAVE_LINES + (int32_t)threadIdx.x;
+  const int32_t i = (int)threadIdx.x < rpw ? (int32_t)blockIdx.x * rpw + (int32_t)threadIdx.x : n;
   bool fb = false;
   uint32_t len = i < n ? fleet_row<false>(a, i, nullptr, fb) : 0u;
   if (fb) atomicAdd(a.fallback, 1);  // (counted here only)
@@ -263,10 +275,10 @@ __global__ __launch_bounds__(FMT_WAVE_LINES) void k_fleet_len(FleetFormatArgs a)
   if (threadIdx.x == 0) a.status[blockIdx.x] = len;
 }
 
-__global__ __launch_bounds__(FMT_WAVE_LINES) void k_fleet_rows(FleetFormatArgs a) {
+__global__ __launch_bounds__(FMT_WAVE_LINES) void k_fleet_rows(FleetFormatArgs a, int rpw) {
   __shared__ __align__(16) char stage[FLEET_LDS];
   const int32_t n = a.n_slots * a.n_lags;
-  const int32_t i = (int32_t)blockIdx.x * FMT_WAVE_LINES + (int32_t)threadIdx.x;
+  const int32_t i = (int)threadIdx.x < rpw ? (int32_t)blockIdx.x * rpw + (int32_t)threadIdx.x : n;
   const int lane = (int)threadIdx.x;
   bool fb = false;
   const uint32_t len = i < n ? fleet_row<false>(a, i, nullptr, fb) : 0u;
@@ -347,7 +359,8 @@ void apm_format_fixed_batch(const double* d_x, int n, int f, char* d_out, hipStr
 }
 
 uint32_t apm_fleet_format_blocks(int32_t n_rows) {
-  return (uint32_t)((std::max<int32_t>(n_rows, 1) + FMT_WAVE_LINES - 1) / FMT_WAVE_LINES);
+  const int32_t rpw = fleet_rows_per_wave();
+  return (uint32_t)((std::max<int32_t>(n_rows, 1) + rpw - 1) / rpw);
 }
 
 // two launches; afterwards *a->total holds the bytes written (device)
@@ -358,8 +371,9 @@ void apm_fleet_format(FleetFormatArgs* a, hipStream_t stream) {
     return;
   }
   const dim3 grid(apm_fleet_format_blocks(n));
-  hipLaunchKernelGGL(k_fleet_len, grid, dim3(FMT_WAVE_LINES), 0, stream, *a);
-  hipLaunchKernelGGL(k_fleet_rows, grid, dim3(FMT_WAVE_LINES), 0, stream, *a);
+  const int rpw = fleet_rows_per_wave();
+  hipLaunchKernelGGL(k_fleet_len, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, rpw);
+  hipLaunchKernelGGL(k_fleet_rows, grid, dim3(FMT_WAVE_LINES), 0, stream, *a, rpw);
 }
 
 void apm_format_write(FormatArgs* a, hipStream_t stream) {

@@ -44,7 +44,7 @@ KINDS = ("st", "fs", "al")
 
 def node_cfg():
     from apmbackend_amd.utils.config import default_config
-    C = default_config()
+    C = default_config(replay=True)
     C["streamCalcZScore"]["defaults"] = [{"LAG": 6, "THRESHOLD": 3.0, "INFLUENCE": 0.5},
                                          {"LAG": 30, "THRESHOLD": 2.0, "INFLUENCE": 0.0}]
     C["streamProcessAlerts"]["rollingAlertWindowSizeInIntervals"] = 5

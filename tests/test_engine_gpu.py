@@ -6,6 +6,7 @@
 * rolling-mean mode agrees with exact mode on signals/alerts and to 1 dp on the printed means.
 """
 import collections
+import os
 import copy
 
 import numpy as np
