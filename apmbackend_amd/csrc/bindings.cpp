@@ -99,6 +99,7 @@ EngineConfig config_from(const py::dict& d) {
   c.window = get<int>(d, "window", c.window);
   c.buffer = get<int>(d, "buffer", c.buffer);
   c.nslot = get<int>(d, "nslot", c.nslot);
+  c.ck_stage_mb = get<int64_t>(d, "ck_stage_mb", c.ck_stage_mb);
   c.record_ttl_ms = get<double>(d, "record_ttl_ms", c.record_ttl_ms);
   c.acct_ttl_ms = get<double>(d, "acct_ttl_ms", c.acct_ttl_ms);
   c.need_ttl_ms = get<double>(d, "need_ttl_ms", c.need_ttl_ms);
@@ -397,6 +398,8 @@ PYBIND11_MODULE(_apm_native, m) {
         d["chain_len"] = c.chain_len; d["last_base"] = c.last_base; d["last_stall_ms"] = c.last_stall_ms;
         d["last_write_ms"] = c.last_write_ms; d["last_bytes"] = c.last_bytes; d["stage_bytes"] = c.stage_bytes;
         d["last_deferred_bytes"] = c.last_deferred_bytes;
+        d["streamed"] = c.streamed; d["streamed_live_rows"] = c.streamed_live_rows;
+        d["side_rows"] = c.side_rows; d["guard_stalls"] = c.guard_stalls; d["stage_cap"] = c.stage_cap;
         d["last_ring_rows"] = c.last_ring_rows;
         return d;
       })

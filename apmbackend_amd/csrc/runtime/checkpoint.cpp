@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <thread>
 #include <cstring>
 #include <memory>
 
@@ -736,11 +737,20 @@ void Engine::apply_ring_file(const std::string& path) {
   const int32_t S = cfg_.max_series;
   const size_t rb = (size_t)cfg_.ring_bytes;
   for (int l = 0; l < cfg_.n_lags; ++l) {
-    const int32_t nc = rd.pod<int32_t>();
+    int32_t nc = rd.pod<int32_t>();
+    const bool row_major = nc < 0;  // a streamed snapshot: [row][stat][series] (write_streamed_ring)
+    if (row_major) nc = -nc - 1;
     const std::vector<int32_t> heads = rd.vec<int32_t>();
     if (nc > n_series_) throw std::runtime_error("checkpoint: ring section wider than the series table");
     for (int32_t h : heads)
       if (h < 0 || h >= cfg_.lags[l]) throw std::runtime_error("checkpoint: bad ring row");
+    if (row_major) {
+      for (int32_t h : heads) {
+        char* dst = (char*)lag_[l].ring + (size_t)h * S * rb;
+        h2d_rows(rd, dst, (size_t)cfg_.lags[l] * S * rb, (size_t)nc * rb, NSTAT, bounce, stream_);
+      }
+      continue;
+    }
     for (int k = 0; k < NSTAT; ++k)
       for (size_t i = 0; i < heads.size();) {  // runs of consecutive rows are contiguous in the file
         size_t j = i + 1;
@@ -1084,13 +1094,73 @@ int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& e
     need += (size_t)NSTAT * lg.heads.size() * n * rb;
     job->lags.push_back(std::move(lg));
   }
+  const size_t cap = cfg_.ck_stage_mb > 0 ? (size_t)cfg_.ck_stage_mb << 20 : SIZE_MAX;
+  const size_t row_bytes = (size_t)NSTAT * n * rb;  // one ring position of one LAG, every stat
+  if (need > cap && n > 0) {
+    // Streamed snapshot: the ring rows do not fit the staging cap (rings sized toward HBM).  Stage
+    // the rows the next rollovers overwrite first -- position (r1 + i) % L of every LAG, i = 0, 1,
+    // ... -- in 80 % of the cap; the writer reads the others from the live ring in overwrite order,
+    // and ck_guard_rollover copies a row aside (the other 20 %) if a rollover reaches it first.
+    job->streamed = true;
+    const size_t main_cap = cap / 5 * 4, side_cap = cap - main_cap;
+    if (!ck_side_ev_) HIP_OK(hipEventCreateWithFlags(&ck_side_ev_, hipEventDisableTiming));
+    std::lock_guard<std::mutex> g(cks_mu_);
+    cks_ = CkStream{};
+    cks_.on = true;
+    cks_.n_cols = n;
+    cks_.state.resize(cfg_.n_lags);
+    cks_.off.resize(cfg_.n_lags);
+    std::vector<std::vector<int32_t>> order(cfg_.n_lags);
+    for (int l = 0; l < cfg_.n_lags; ++l) {
+      const int32_t L = cfg_.lags[l];
+      cks_.state[l].assign((size_t)L, CKR_NONE);
+      cks_.off[l].assign((size_t)L, 0);
+      std::vector<int32_t> hs = job->lags[l].heads;  // this snapshot's rows, by next overwrite
+      std::sort(hs.begin(), hs.end(), [&](int32_t a, int32_t b) {
+        return ((a - r1 % L) % L + L) % L < ((b - r1 % L) % L + L) % L;
+      });
+      order[l] = std::move(hs);
+      for (int32_t h : order[l]) cks_.state[l][(size_t)h] = CKR_LIVE;
+    }
+    // round-robin over the LAGs by overwrite rank: row i of every LAG before row i + 1 of any
+    size_t staged = 0;
+    std::vector<std::vector<int32_t>> stg(cfg_.n_lags);
+    for (size_t i = 0;; ++i) {
+      bool any = false, full = false;
+      for (int l = 0; l < cfg_.n_lags && !full; ++l) {
+        if (i >= order[l].size()) continue;
+        any = true;
+        if (staged + row_bytes > main_cap) { full = true; break; }
+        stg[l].push_back(order[l][i]);
+        cks_.state[l][(size_t)order[l][i]] = CKR_STAGED;
+        cks_.off[l][(size_t)order[l][i]] = staged;
+        staged += row_bytes;
+      }
+      if (!any || full) break;
+    }
+    // file order per LAG: the live rows in overwrite order (the writer races the rollovers), then
+    // the staged ones
+    for (int l = 0; l < cfg_.n_lags; ++l) {
+      std::vector<int32_t> fo;
+      for (int32_t h : order[l])
+        if (cks_.state[l][(size_t)h] == CKR_LIVE) fo.push_back(h);
+      for (int32_t h : stg[l]) fo.push_back(h);
+      job->lags[l].heads = std::move(fo);
+    }
+    need = staged + side_cap;
+    cks_.side_cap = side_cap;
+  }
   ck_last_need_ = need;
   if (need > ck_stage_bytes_) {
     free_ck_stage();
-    const size_t want = need + need / 8;  // room for the series table to grow
+    const size_t want = job->streamed ? need : std::min(cap, need + need / 8);  // (room for the series table)
     if (hipMalloc(&d_ck_stage_, want) != hipSuccess) {
       (void)hipGetLastError();
       d_ck_stage_ = nullptr;
+      {
+        std::lock_guard<std::mutex> g(cks_mu_);
+        cks_.on = false;
+      }
       // not enough HBM for a snapshot: fall back to the synchronous writer
       ck_all_dirty_ = true;
       if (job->pre_commit) job->pre_commit();  // (first: see checkpoint_writer)
@@ -1107,21 +1177,38 @@ int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& e
     std::lock_guard<std::mutex> g(alloc_mu_);
     device_bytes_ += want;
   }
-  for (int l = 0; l < cfg_.n_lags; ++l) {
-    const CkJob::Lag& lg = job->lags[l];
-    const int32_t L = cfg_.lags[l];
-    char* dst = (char*)d_ck_stage_ + lg.off;
-    for (int k = 0; k < NSTAT; ++k)
-      for (size_t i = 0; i < lg.heads.size();) {
-        size_t j = i + 1;
-        while (j < lg.heads.size() && lg.heads[j] == lg.heads[j - 1] + 1) ++j;
-        const char* src = (const char*)lag_[l].ring + ((size_t)k * L + (size_t)lg.heads[i]) * S * rb;
-        if (n > 0)
-          HIP_OK(hipMemcpy2DAsync(dst, (size_t)n * rb, src, (size_t)S * rb, (size_t)n * rb, j - i,
-                                  hipMemcpyDeviceToDevice, stream_));
-        dst += (j - i) * (size_t)n * rb;
-        i = j;
+  if (job->streamed) {
+    // staged rows: all NSTAT planes of a position together (the row-major file layout)
+    std::lock_guard<std::mutex> g(cks_mu_);
+    d_ck_side_ = (char*)d_ck_stage_ + (need - cks_.side_cap);
+    for (int l = 0; l < cfg_.n_lags; ++l) {
+      const int32_t L = cfg_.lags[l];
+      for (int32_t h = 0; h < L; ++h) {
+        if (cks_.state[l][(size_t)h] != CKR_STAGED) continue;
+        char* dst = (char*)d_ck_stage_ + cks_.off[l][(size_t)h];
+        const char* src = (const char*)lag_[l].ring + (size_t)h * S * rb;
+        HIP_OK(hipMemcpy2DAsync(dst, (size_t)n * rb, src, (size_t)L * S * rb, (size_t)n * rb, NSTAT,
+                                hipMemcpyDeviceToDevice, stream_));
       }
+    }
+    ++ck_streamed_;
+  } else {
+    for (int l = 0; l < cfg_.n_lags; ++l) {
+      const CkJob::Lag& lg = job->lags[l];
+      const int32_t L = cfg_.lags[l];
+      char* dst = (char*)d_ck_stage_ + lg.off;
+      for (int k = 0; k < NSTAT; ++k)
+        for (size_t i = 0; i < lg.heads.size();) {
+          size_t j = i + 1;
+          while (j < lg.heads.size() && lg.heads[j] == lg.heads[j - 1] + 1) ++j;
+          const char* src = (const char*)lag_[l].ring + ((size_t)k * L + (size_t)lg.heads[i]) * S * rb;
+          if (n > 0)
+            HIP_OK(hipMemcpy2DAsync(dst, (size_t)n * rb, src, (size_t)S * rb, (size_t)n * rb, j - i,
+                                    hipMemcpyDeviceToDevice, stream_));
+          dst += (j - i) * (size_t)n * rb;
+          i = j;
+        }
+    }
   }
   if (!ck_ev_) HIP_OK(hipEventCreateWithFlags(&ck_ev_, hipEventDisableTiming));
   HIP_OK(hipEventRecord(ck_ev_, stream_));
@@ -1140,6 +1227,95 @@ int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& e
   if (!ck_thread_.joinable()) ck_thread_ = std::thread([this] { checkpoint_writer(); });
   ck_cv_.notify_all();
   return job->seq;
+}
+
+// Writer thread: the ring section of a streamed snapshot, row-major -- the NSTAT planes of a
+// position together; n_cols is stored as -(n_cols + 1), which tells apply_ring_file / merge the
+// layout.  Each row comes from the staging, the side copy a rollover made, or the live ring (read
+// under the CKR_READING mark, which a rollover about to overwrite that row waits out).
+void Engine::write_streamed_ring(const std::shared_ptr<CkJob>& job, BinWriter& w, char* bounce) {
+  const int32_t S = cfg_.max_series;
+  const size_t rb = (size_t)cfg_.ring_bytes;
+  // test hook: a slow checkpoint disk (per-row delay), so rollovers overtake the writer
+  static const int delay_us = [] { const char* e = std::getenv("APM_CK_ROW_DELAY_US"); return e ? std::atoi(e) : 0; }();
+  for (size_t l = 0; l < job->lags.size(); ++l) {
+    const CkJob::Lag& lg = job->lags[l];
+    const int32_t L = cfg_.lags[l];
+    const size_t width = (size_t)lg.n_cols * rb;
+    w.pod<int32_t>(-lg.n_cols - 1);
+    w.vec(lg.heads);
+    for (int32_t h : lg.heads) {
+      uint8_t st;
+      size_t off;
+      bool sync = false;
+      {
+        std::lock_guard<std::mutex> lk(cks_mu_);
+        st = cks_.state[l][(size_t)h];
+        off = cks_.off[l][(size_t)h];
+        if (st == CKR_LIVE) cks_.state[l][(size_t)h] = CKR_READING;
+        if (st == CKR_SIDE && cks_.side_sync) { sync = true; cks_.side_sync = false; }
+      }
+      if (sync) HIP_OK(hipEventSynchronize(ck_side_ev_));  // every side copy queued so far has run
+      const char* src;
+      size_t pitch;
+      if (st == CKR_LIVE) {
+        src = (const char*)lag_[l].ring + (size_t)h * S * rb;
+        pitch = (size_t)L * S * rb;
+      } else if (st == CKR_STAGED || st == CKR_SIDE) {
+        src = (st == CKR_STAGED ? (const char*)d_ck_stage_ : (const char*)d_ck_side_) + off;
+        pitch = width;
+      } else {
+        throw std::runtime_error("checkpoint: streamed ring row in state " + std::to_string(st));
+      }
+      d2h_rows(w, src, pitch, width, NSTAT, bounce, ck_stream_);
+      if (delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(delay_us));
+      {
+        std::lock_guard<std::mutex> lk(cks_mu_);
+        cks_.state[l][(size_t)h] = CKR_DONE;
+        if (st == CKR_LIVE) ++cks_.live_rows;
+      }
+      cks_cv_.notify_all();
+    }
+  }
+}
+
+// Stats thread, before rollover r's K10 writes ring position r % L of every LAG: a streamed
+// snapshot's row the writer has not read yet is copied aside first (D2D on this stream, ordered
+// before the overwrite); while the writer is reading it -- or the side staging is full -- the
+// rollover waits for the writer (counted: guard_stalls).
+void Engine::ck_guard_rollover(int64_t r) {
+  std::unique_lock<std::mutex> lk(cks_mu_);
+  if (!cks_.on) return;
+  const int32_t S = cfg_.max_series;
+  const size_t rb = (size_t)cfg_.ring_bytes;
+  const size_t width = (size_t)cks_.n_cols * rb, row_bytes = (size_t)NSTAT * width;
+  bool copied = false;
+  for (int l = 0; l < cfg_.n_lags && l < (int)cks_.state.size(); ++l) {
+    const int32_t L = cfg_.lags[l];
+    if ((int32_t)cks_.state[l].size() != L) continue;
+    const int32_t h = (int32_t)(r % L);
+    for (;;) {
+      if (!cks_.on) return;
+      uint8_t& st = cks_.state[l][(size_t)h];
+      if (st == CKR_LIVE && cks_.side_used + row_bytes <= cks_.side_cap) {
+        HIP_OK(hipMemcpy2DAsync(d_ck_side_ + cks_.side_used, width, (const char*)lag_[l].ring + (size_t)h * S * rb,
+                                (size_t)L * S * rb, width, NSTAT, hipMemcpyDeviceToDevice, stream_));
+        cks_.off[l][(size_t)h] = cks_.side_used;
+        cks_.side_used += row_bytes;
+        st = CKR_SIDE;
+        ++cks_.side_rows;
+        copied = true;
+        break;
+      }
+      if (st != CKR_LIVE && st != CKR_READING) break;
+      ++cks_.stalls;
+      cks_cv_.wait(lk);
+    }
+  }
+  if (copied) {
+    HIP_OK(hipEventRecord(ck_side_ev_, stream_));
+    cks_.side_sync = true;
+  }
 }
 
 void Engine::free_ck_stage() {
@@ -1180,7 +1356,9 @@ void Engine::checkpoint_writer() {
       w.raw(job->blob.data(), job->blob.size());
       w.begin(SEC_RING);
       const size_t rb = (size_t)cfg_.ring_bytes;
+      if (job->streamed) write_streamed_ring(job, w, (char*)bounce);
       for (const auto& lg : job->lags) {
+        if (job->streamed) break;
         w.pod<int32_t>(lg.n_cols);
         w.vec(lg.heads);
         size_t left = (size_t)NSTAT * lg.heads.size() * (size_t)lg.n_cols * rb;
@@ -1204,6 +1382,16 @@ void Engine::checkpoint_writer() {
       finish_chain(job, bytes);
     } catch (const std::exception& e) {
       err = e.what();
+    }
+    if (job->streamed) {  // (also on a failure: rollovers must not wait for a writer that gave up)
+      {
+        std::lock_guard<std::mutex> lk(cks_mu_);
+        cks_.on = false;
+        ck_streamed_live_ += cks_.live_rows;
+        ck_side_rows_ += cks_.side_rows;
+        ck_guard_stalls_ += cks_.stalls;
+      }
+      cks_cv_.notify_all();
     }
     {
       std::lock_guard<std::mutex> lk(ck_mu_);
@@ -1288,6 +1476,7 @@ void Engine::checkpoint_shutdown() {
   if (d_ck_defer_) { hipFree(d_ck_defer_); d_ck_defer_ = nullptr; ck_defer_cap_ = 0; }
   if (h_ck_bounce_) { hipHostFree(h_ck_bounce_); h_ck_bounce_ = nullptr; }
   if (ck_ev_) { hipEventDestroy(ck_ev_); ck_ev_ = nullptr; }
+  if (ck_side_ev_) { hipEventDestroy(ck_side_ev_); ck_side_ev_ = nullptr; }
   if (ck_stream_) { hipStreamDestroy(ck_stream_); ck_stream_ = nullptr; }
 }
 
@@ -1306,6 +1495,11 @@ CheckpointInfo Engine::checkpoint_info() {
   c.stage_bytes = ck_stage_bytes_;
   c.last_ring_rows = ck_last_ring_rows_;
   c.last_deferred_bytes = ck_deferred_bytes_;
+  c.streamed = ck_streamed_;
+  c.streamed_live_rows = ck_streamed_live_;
+  c.side_rows = ck_side_rows_;
+  c.guard_stalls = ck_guard_stalls_;
+  c.stage_cap = cfg_.ck_stage_mb > 0 ? (uint64_t)cfg_.ck_stage_mb << 20 : 0;
   return c;
 }
 

@@ -2336,7 +2336,8 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   wa.n_series = n_series_;
   HIP_OK(hipMemsetAsync(d_big_n_, 0, 12, stream_));  // big / nan windows, alert candidates
   apm_window_stats(&wa, stream_);
-  // ---- K10 z-score per LAG, K11 alert eval
+  // ---- K10 z-score per LAG, K11 alert eval (a streamed checkpoint's rows first: copy-before-overwrite)
+  ck_guard_rollover(rollover_idx_);
   for (int l = 0; l < cfg_.n_lags; ++l) {
     LagState& LS = lag_[l];
     ZArgs za;

@@ -105,6 +105,7 @@ struct EngineConfig {
   int window = 30;
   int buffer = 6;
   int nslot = 0;  // bucket ring slots (gpu.bucketRingSlots; 0 = ring_slots_for(window, buffer))
+  int64_t ck_stage_mb = 2048;  // HBM staging of a snapshot's ring rows (gpu.checkpointStageMB; 0 = unbounded)
   // parse
   double record_ttl_ms = 120000, acct_ttl_ms = 120000, need_ttl_ms = 30000;
   TzTable tz{};
@@ -195,6 +196,10 @@ struct CheckpointInfo {
   uint64_t last_bytes = 0, stage_bytes = 0;
   int64_t last_ring_rows = 0;  // ring rows (over all LAGs) the last checkpoint carried
   uint64_t last_deferred_bytes = 0;  // small-section bytes the last snapshot read D2D (not on the ingest thread)
+  // streamed bases (ring larger than gpu.checkpointStageMB): rows read from the live ring by the
+  // writer, rows a rollover copied aside first, rollovers that waited for the writer
+  uint64_t streamed = 0, streamed_live_rows = 0, side_rows = 0, guard_stalls = 0;
+  uint64_t stage_cap = 0;
 };
 
 struct EngineMetrics {
@@ -909,6 +914,7 @@ class Engine {
   // checkpoint (checkpoint.cpp)
   struct CkJob {
     struct Lag { int32_t n_cols = 0; std::vector<int32_t> heads; size_t off = 0; };
+    bool streamed = false;  // ring section row-major, rows staged / read live / copied aside (CkStream)
     bool base = false;
     int64_t seq = 0;
     std::string prefix, name, path, extra;
@@ -924,6 +930,27 @@ class Engine {
     std::vector<std::pair<size_t, int32_t>> patches;  // stored after the holes are filled
   };
   static constexpr int kMaxChain = 16;
+  // Streamed base snapshot: the z-score rings can fill most of HBM, so a base whose rows exceed
+  // the staging cap stages only the rows the next rollovers overwrite first; the writer reads the
+  // others from the live ring, and a rollover about to overwrite a row not yet read copies it
+  // aside first (copy-before-overwrite, ck_guard_rollover).  Per (lag, position) row state:
+  enum : uint8_t { CKR_NONE = 0, CKR_LIVE, CKR_READING, CKR_STAGED, CKR_SIDE, CKR_DONE };
+  struct CkStream {
+    bool on = false;
+    std::vector<std::vector<uint8_t>> state;  // [lag][ring position]
+    std::vector<std::vector<size_t>> off;     // staging (CKR_STAGED) or side (CKR_SIDE) offset
+    size_t side_used = 0, side_cap = 0;
+    bool side_sync = false;                   // side copies queued on stream_ since the writer's last sync
+    int32_t n_cols = 0;                       // series in the snapshot's rows
+    uint64_t live_rows = 0, side_rows = 0, stalls = 0;
+  } cks_;
+  std::mutex cks_mu_;
+  std::condition_variable cks_cv_;
+  char* d_ck_side_ = nullptr;
+  uint64_t ck_streamed_ = 0, ck_streamed_live_ = 0, ck_side_rows_ = 0, ck_guard_stalls_ = 0;
+  hipEvent_t ck_side_ev_ = nullptr;   // after the newest side copy (stream_)
+  void ck_guard_rollover(int64_t r);  // stats thread, before K10 of rollover r writes ring rows
+  void write_streamed_ring(const std::shared_ptr<CkJob>& job, class BinWriter& w, char* bounce);
   // staging of the deferred small-section reads (one checkpoint in flight at a time)
   char* d_ck_defer_ = nullptr;
   size_t ck_defer_cap_ = 0, ck_defer_want_ = 0;

@@ -267,7 +267,9 @@ std::vector<char> read_ring(const Input& in, int l, size_t rb) {
     BinReader rd(f);
     rd.skip_to(SEC_RING);
     for (int q = 0; q < in.n_lags; ++q) {
-      const int32_t nc = rd.pod<int32_t>();
+      int32_t nc = rd.pod<int32_t>();
+      const bool row_major = nc < 0;  // a streamed snapshot (checkpoint.cpp write_streamed_ring)
+      if (row_major) nc = -nc - 1;
       const std::vector<int32_t> heads = rd.vec<int32_t>();
       if ((size_t)nc > n) throw std::runtime_error("merge: ring rows wider than the series table");
       const size_t w = (size_t)nc * rb;
@@ -276,6 +278,16 @@ std::vector<char> read_ring(const Input& in, int l, size_t rb) {
         continue;
       }
       row.resize(w);
+      if (row_major) {
+        for (int32_t h : heads) {
+          if (h < 0 || h >= L) throw std::runtime_error("merge: bad ring row");
+          for (int k = 0; k < NSTAT; ++k) {
+            rd.raw(row.data(), w);
+            std::memcpy(ring.data() + ((size_t)k * L + (size_t)h) * n * rb, row.data(), w);
+          }
+        }
+        continue;
+      }
       for (int k = 0; k < NSTAT; ++k)
         for (int32_t h : heads) {  // (runs of consecutive rows are contiguous: row order is file order)
           if (h < 0 || h >= L) throw std::runtime_error("merge: bad ring row");

@@ -93,6 +93,7 @@ void Engine::apply_reconfig(const ReconfigSpec& r) {
   bool lag_change = r.n_lags != cfg_.n_lags;
   for (int l = 0; l < r.n_lags && !lag_change; ++l) lag_change = r.lags[l] != cfg_.lags[l];
   if (lag_change) {
+    checkpoint_wait();  // a streamed snapshot's writer may still read the rings about to be freed
     // kernels of the previous rollover (formatting on the output stream, K10/K11 and the fleet
     // pack on the stats stream) still read the old per-LAG arrays.  Only those two streams: a
     // device-wide sync would also wait for the collective stream, whose lock-step all-reduce may

@@ -68,6 +68,7 @@ GPU_DEFAULTS: Dict[str, Any] = {
     "collectiveBackend": "rccl",      # node-wide exchanges: rccl (xGMI) or host (TCP via rank 0, ranks sharing a GPU)
     "checkpointDir": "",              # binary engine checkpoints (+ tail offsets) per rank
     "checkpointEverySeconds": 60,
+    "checkpointStageMB": 2048,        # HBM staging of a checkpoint's z-score ring rows (larger bases stream)
     "importReferenceResume": False,   # seed a fresh engine from the reference's JSON resume files
     "outputMode": "inproc",           # inproc (DB insert stage in-process) | amqp (queue bridge) | none
     "bridgeQueues": [],               # amqp mode: also mirror "transactions" / "stats"

@@ -605,6 +605,51 @@ def test_base_checkpoint_keeps_the_previous_chain(tmp_path):
         assert upto[k] == full[k], k
 
 
+@pytest.mark.parametrize("row_delay_us", [0, 3000])
+def test_streamed_base_checkpoint_under_a_staging_cap(tmp_path, monkeypatch, row_delay_us):
+    """Verdict r5 #4: rings sized toward HBM do not fit a snapshot's staging.  With
+    gpu.checkpointStageMB far below the rings' size the base streams: the rows the next rollovers
+    overwrite first are staged, the writer reads the rest from the live ring, and (with a slow
+    writer: 3 ms per row) rollovers that reach a row not yet written copy it aside first or wait.
+    The engine keeps running during the write; a fresh engine restored from the file continues
+    exactly like the uninterrupted run."""
+    monkeypatch.setenv("APM_CK_ROW_DELAY_US", str(row_delay_us))
+    lines, bl = synth_batches(8, duration=900)
+    C = small_cfg("exact")
+    C["streamCalcZScore"]["defaults"] = [{"LAG": 6, "THRESHOLD": 3.0, "INFLUENCE": 0.5},
+                                         {"LAG": 120, "THRESHOLD": 2.0, "INFLUENCE": 0.0}]
+    C["gpu"]["checkpointStageMB"] = 1  # rings: (6 + 120) rows x 3 stats x 4096 series x 8 B = 12 MB
+    _, full = _run_engine(C, bl)
+    cut = len(bl) // 2
+    eng = APMEngine(C, keep_text=True)
+    out = collections.defaultdict(list)
+    prefix = str(tmp_path / "engine.rank0")
+    for i, (now, chunks) in enumerate(bl):
+        eng.process_lines(chunks, now)
+        for k in ("transactions", "audit_db", "st", "fs", "al"):
+            out[k] += eng.take(k)
+        if i + 1 == cut:
+            at_cut = {k: len(v) for k, v in out.items()}
+            assert eng.checkpoint_async(prefix, b"%d" % i, True) > 0
+    eng.checkpoint_wait()
+    info = eng.checkpoint_info()
+    assert info["streamed"] == 1 and info["streamed_live_rows"] > 0, info
+    assert info["stage_bytes"] <= (1 << 20), info
+    if row_delay_us:
+        assert info["side_rows"] + info["guard_stalls"] > 0, info  # rollovers overtook the writer
+    for k in ("transactions", "audit_db", "st", "fs", "al"):
+        assert out[k] == full[k], k
+    eng2 = APMEngine(C, keep_text=True)
+    assert eng2.load_state(prefix + ".ckpt") == b"%d" % (cut - 1)
+    rest = collections.defaultdict(list)
+    for now, chunks in bl[cut:]:
+        eng2.process_lines(chunks, now)
+        for k in ("transactions", "audit_db", "st", "fs", "al"):
+            rest[k] += eng2.take(k)
+    for k in ("transactions", "audit_db", "st", "fs", "al"):
+        assert out[k][:at_cut[k]] + rest[k] == full[k], k
+
+
 def test_host_join_tx_staging_grows_instead_of_failing():
     """Host-join mode with a tiny per-batch tx staging: the engine doubles it mid-batch (was: a
     'too many tx in one batch' exception) and the output is unchanged."""
