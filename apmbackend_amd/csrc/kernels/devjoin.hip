@@ -481,54 +481,121 @@ __device__ __forceinline__ uint8_t hf_fields(const Event& e, const uint8_t* __re
   return fl;
 }
 
+// Wave-aggregated append of this lane's index when `want` (one atomic per wave); every lane of the
+// wave calls it.  Returns the slot, ~0u when !want.
+__device__ __forceinline__ uint32_t wave_append(bool want, uint32_t* counter) {
+  const uint64_t m = __ballot(want);
+  if (!m) return ~0u;
+  const uint32_t lane = threadIdx.x & (APM_WAVE - 1);
+  const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+  base = (uint32_t)__shfl((int)base, (int)leader, APM_WAVE);
+  return want ? base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull)) : ~0u;
+}
+
+__device__ __forceinline__ uint64_t sel_pack(uint8_t fl) {
+  return (uint64_t)(fl & SEL_HOST) | ((fl & SEL_MH) ? 1ull << SEL_MH_SHIFT : 0ull) |
+         ((fl & SEL_WALK) ? 1ull << SEL_WALK_SHIFT : 0ull);
+}
+
+__device__ __forceinline__ uint8_t app_bits(const Event& e) {
+  if (e.kind != LK_APP) return 0;
+  return (e.mask & PM_AUTR_MAP) ? SEL_MH : (uint8_t)(SEL_WALK | ((e.mask & PM_AUTR_HDR) ? SEL_MH : 0));
+}
+
+// Byte work of one event: its line staged into this lane's LDS slot when it fits (independent
+// 16-byte loads, one memory latency per line), then walked there.
+__device__ __forceinline__ uint8_t hf_event(const Event& e, uint32_t i, const uint8_t* __restrict__ bytes,
+                                            const uint32_t* __restrict__ chunk_file,
+                                            const uint64_t* __restrict__ file_fkey, AudF* __restrict__ aud,
+                                            uint8_t* stage, int bytewise, int staged) {
+  const uint64_t fkey = e.kind == LK_APP ? file_fkey[chunk_file[e.chunk]] : 0;
+  // (staging only decides where the walk reads: a staged line is a complete copy, so the field
+  // functions -- which read bytes only in the cases hf_needs_bytes names -- are unchanged)
+  const uint8_t* p = bytes + e.off;
+  const uint32_t lead = e.off & 15u;
+  const uint32_t nvec = (lead + e.len + 15u) >> 4;
+  if (staged && hf_needs_bytes(e) && nvec * 16u <= (uint32_t)HF_SLOT) {
+    // the line's aligned 16-byte blocks, every load issued before the first LDS store
+    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(bytes + (e.off - lead));
+    uint4* dst = reinterpret_cast<uint4*>(stage + threadIdx.x * HF_PITCH);
+    uint4 v[HF_SLOT / 16];
+#pragma unroll
+    for (int k = 0; k < HF_SLOT / 16; ++k)
+      if ((uint32_t)k < nvec) v[k] = src[k];
+#pragma unroll
+    for (int k = 0; k < HF_SLOT / 16; ++k)
+      if ((uint32_t)k < nvec) dst[k] = v[k];
+    p = stage + threadIdx.x * HF_PITCH + lead;
+  }
+  return (uint8_t)(hf_fields(e, p, fkey, aud, i, bytewise) | app_bits(e));
+}
+
+// Host / audit selection flags per event.  `split` (default): events whose flags need their line's
+// bytes -- audit lines, SOAP request / account lines, CommonTiming exits with a BAF account, a
+// minority of the batch -- are listed instead (audit lines from the front of `list`, the others
+// from the back) and walked densely by k_host_flags_bytes; every other event is decided here
+// from its Event alone.  One lane per event over the whole batch made every wave execute each of
+// the walks its few byte events needed, the other lanes idle (the largest join-side kernel:
+// 137 us a batch, profiles/r5_final2).  split == 0: the one-pass form (APM_HF_SPLIT=0, A/B).
 __global__ __launch_bounds__(TB) void k_host_flags(const Event* __restrict__ ev, const uint32_t* __restrict__ n_ev_dev,
                                                    const uint8_t* __restrict__ bytes, const uint32_t* __restrict__ chunk_file,
                                                    const uint64_t* __restrict__ file_fkey,
                                                    uint8_t* __restrict__ flag, uint64_t* __restrict__ val,
                                                    AudF* __restrict__ aud, SelCount* __restrict__ totals, uint32_t cap,
-                                                   int bytewise, int staged) {
+                                                   int bytewise, int staged, int split, uint32_t* __restrict__ list,
+                                                   uint32_t* __restrict__ list_n) {
   __shared__ __attribute__((aligned(16))) uint8_t stage[TB * HF_PITCH];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t n = min(*n_ev_dev, cap);
   if (blockIdx.x * blockDim.x >= n) return;  // (uniform per block: the grid is sized for the capacity)
-  uint8_t fl = 0;
   uint32_t ab = 0;
+  Event e;
+  bool defer = false, front = false;
   if (i < n) {
-    const Event e = ev[i];
-    const uint64_t fkey = e.kind == LK_APP ? file_fkey[chunk_file[e.chunk]] : 0;
-    // (staging only decides where the walk reads: a staged line is a complete copy, so the field
-    // functions -- which read bytes only in the cases hf_needs_bytes names -- are unchanged)
-    const uint8_t* p = bytes + e.off;
-    const uint32_t lead = e.off & 15u;
-    const uint32_t nvec = (lead + e.len + 15u) >> 4;
-    if (staged && hf_needs_bytes(e) && nvec * 16u <= (uint32_t)HF_SLOT) {
-      // the line's aligned 16-byte blocks, every load issued before the first LDS store
-      const uint4* __restrict__ src = reinterpret_cast<const uint4*>(bytes + (e.off - lead));
-      uint4* dst = reinterpret_cast<uint4*>(stage + threadIdx.x * HF_PITCH);
-      uint4 v[HF_SLOT / 16];
-#pragma unroll
-      for (int k = 0; k < HF_SLOT / 16; ++k)
-        if ((uint32_t)k < nvec) v[k] = src[k];
-#pragma unroll
-      for (int k = 0; k < HF_SLOT / 16; ++k)
-        if ((uint32_t)k < nvec) dst[k] = v[k];
-      p = stage + threadIdx.x * HF_PITCH + lead;
-    }
-    fl = hf_fields(e, p, fkey, aud, i, bytewise);
-    if (e.kind == LK_APP) {
-      if (e.mask & PM_AUTR_MAP) fl |= SEL_MH;
-      else fl |= SEL_WALK | ((e.mask & PM_AUTR_HDR) ? SEL_MH : 0);
-      if (e.mask & (PM_AUTR_MAP | PM_SW_NAME)) ab = e.len;
-    }
+    e = ev[i];
+    if (e.kind == LK_APP && (e.mask & (PM_AUTR_MAP | PM_SW_NAME))) ab = e.len;
+    defer = split && hf_needs_bytes(e);
+    front = defer && e.kind == LK_APP;
   }
-  if (i < n) {
+  if (split) {  // (uniform: every lane takes part in both appends)
+    const uint32_t f = wave_append(front, &list_n[0]);
+    const uint32_t b = wave_append(defer && !front, &list_n[1]);
+    if (front) list[f] = i;
+    if (defer && !front) list[cap - 1 - b] = i;
+  }
+  if (i < n && !defer) {
+    const uint8_t fl = split ? (uint8_t)(hf_fields(e, bytes + e.off, 0, aud, i, bytewise) | app_bits(e))
+                             : hf_event(e, i, bytes, chunk_file, file_fkey, aud, stage, bytewise, staged);
     flag[i] = fl;
-    val[i] = (uint64_t)(fl & SEL_HOST) | ((fl & SEL_MH) ? 1ull << SEL_MH_SHIFT : 0ull) |
-             ((fl & SEL_WALK) ? 1ull << SEL_WALK_SHIFT : 0ull);
+    val[i] = sel_pack(fl);
   }
   // bytes of map / stopWatch-name lines: one atomic per wave (totals zeroed before the launch)
   for (int o = APM_WAVE / 2; o > 0; o >>= 1) ab += __shfl_xor(ab, o, APM_WAVE);
   if ((threadIdx.x & (APM_WAVE - 1)) == 0 && ab) atomicAdd(&totals->aud_bytes, ab);
+}
+
+// The listed events of k_host_flags: audit lines at [0, list_n[0]), the others at
+// [cap - list_n[1], cap) -- each wave runs (nearly) one kind of walk with every lane busy.
+__global__ __launch_bounds__(TB) void k_host_flags_bytes(const Event* __restrict__ ev, const uint8_t* __restrict__ bytes,
+                                                         const uint32_t* __restrict__ chunk_file,
+                                                         const uint64_t* __restrict__ file_fkey,
+                                                         uint8_t* __restrict__ flag, uint64_t* __restrict__ val,
+                                                         AudF* __restrict__ aud, uint32_t cap, int bytewise, int staged,
+                                                         const uint32_t* __restrict__ list,
+                                                         const uint32_t* __restrict__ list_n) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage[TB * HF_PITCH];
+  const uint32_t nf = list_n[0], nb = list_n[1];
+  const uint32_t b0 = blockIdx.x * blockDim.x, b1 = b0 + blockDim.x;
+  if (b0 >= nf && b1 <= cap - nb) return;  // a block in the gap between the two lists (uniform)
+  const uint32_t t = b0 + threadIdx.x;
+  if (t >= cap || (t >= nf && t < cap - nb)) return;
+  const uint32_t i = list[t];
+  const Event e = ev[i];
+  const uint8_t fl = hf_event(e, i, bytes, chunk_file, file_fkey, aud, stage, bytewise, staged);
+  flag[i] = fl;
+  val[i] = sel_pack(fl);
 }
 
 // host / map-header / walk lists, in event order (devscan.h over the batch's events only)
@@ -2496,6 +2563,10 @@ static int pre_bytewise() {
   static const int v = [] { const char* e = std::getenv("APM_PRE_BYTEWISE"); return e && e[0] == '1' ? 1 : 0; }();
   return v;
 }
+static int hf_split() {
+  static const int v = [] { const char* e = std::getenv("APM_HF_SPLIT"); return e && e[0] == '0' ? 0 : 1; }();
+  return v;
+}
 static int hf_staged() {
   static const int v = [] { const char* e = std::getenv("APM_HF_STAGE"); return e && e[0] == '0' ? 0 : 1; }();
   return v;
@@ -2503,10 +2574,22 @@ static int hf_staged() {
 int apm_dj_select_host(DJArgs* a, const uint32_t* d_n_ev, uint32_t max_ev, hipStream_t s) {
   HIP_OK(hipMemsetAsync(a->n_host, 0, sizeof(SelCount), s));
   if (max_ev == 0) return 0;
-  hipLaunchKernelGGL(k_host_flags, dim3((max_ev + TB - 1) / TB), dim3(TB), 0, s, a->ev, d_n_ev, a->bytes, a->chunk_file,
-                     a->file_fkey,
-                     a->host_flag, a->sel_val, a->aud, a->n_host, max_ev, pre_bytewise(), hf_staged());
+  // the listed byte events: scratch in sel_pos (written by the selection scan only afterwards;
+  // max_ev + 64 u64 words hold the max_ev u32 list entries and the two counts)
+  const int split = hf_split();
+  uint32_t* list = reinterpret_cast<uint32_t*>(a->sel_pos);
+  uint32_t* list_n = list + max_ev;
+  if (split) HIP_OK(hipMemsetAsync(list_n, 0, 8, s));
+  const dim3 grid((max_ev + TB - 1) / TB);
+  hipLaunchKernelGGL(k_host_flags, grid, dim3(TB), 0, s, a->ev, d_n_ev, a->bytes, a->chunk_file, a->file_fkey,
+                     a->host_flag, a->sel_val, a->aud, a->n_host, max_ev, pre_bytewise(), hf_staged(), split, list,
+                     list_n);
   dj_check(s, "k_host_flags");
+  if (split) {
+    hipLaunchKernelGGL(k_host_flags_bytes, grid, dim3(TB), 0, s, a->ev, a->bytes, a->chunk_file, a->file_fkey,
+                       a->host_flag, a->sel_val, a->aud, max_ev, pre_bytewise(), hf_staged(), list, list_n);
+    dj_check(s, "k_host_flags_bytes");
+  }
   // sel_pos: the tile sums, then the packed total (sel_pos has max_ev + 64 entries)
   uint64_t* total = a->sel_pos + (max_ev + DS_TILE - 1) / DS_TILE + 1;
   if (ds_scan_apply<uint64_t>(SelValF{a->sel_val},

@@ -165,7 +165,6 @@ struct FleetFormatArgs {
   int32_t ts_len;
   char ts[32];
   unsigned long long* status;  // [blocks] each 64-row wave's byte total (k_fleet_len)
-  uint32_t epoch;          // (unused since the look-back went; kept for the struct layout)
   uint32_t* total;         // bytes written (device)
   char* out;
   int32_t* fallback;

@@ -275,7 +275,13 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
         HIP_OK(hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data()));
       cu_reserved_ = reserve;
     } else {
-      HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+      // APM_STATS_PRIO=1: the stats stream (rollover chain K9..K11 -> alert candidates) at the join
+      // stream's high priority, so a batch's alert decision is not queued behind the next batch's
+      // join kernels (the ingest->alert latency, tools/latency_breakdown.py) -- A/B
+      static const bool sp = [] { const char* x = std::getenv("APM_STATS_PRIO"); return x && x[0] == '1'; }();
+      int lo = 0, hi = 0;
+      HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      HIP_OK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, sp ? hi : 0));
       HIP_OK(hipStreamCreateWithFlags(&parse_stream_, hipStreamNonBlocking));
       HIP_OK(hipStreamCreateWithFlags(&out_stream_, hipStreamNonBlocking));
     }

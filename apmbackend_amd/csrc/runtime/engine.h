@@ -660,8 +660,8 @@ class Engine {
   int32_t* d_fb_names_ = nullptr;
   size_t fb_names_cap_ = 0;
   int32_t fb_slots_up_ = 0;
-  unsigned long long* d_fb_status_ = nullptr;  // one-pass formatter's look-back words (+ 2 totals)
-  uint32_t fb_status_n_ = 0, fb_epoch_ = 0;
+  unsigned long long* d_fb_status_ = nullptr;  // per-wave byte totals of k_fleet_len (+ 2 totals)
+  uint32_t fb_status_n_ = 0;
   hipStream_t fb_stream_ = nullptr;          // fb formatting (low priority; never the collective stream)
   hipEvent_t fb_src_ev_[2] = {nullptr, nullptr};   // moments slot all-reduced (coll stream)
   char* d_fb_out_[2] = {nullptr, nullptr};

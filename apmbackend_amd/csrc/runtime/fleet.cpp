@@ -216,9 +216,6 @@ bool Engine::fleet_emit_fb(int slot) {
   fa.copy = fs_copy_ ? 1 : 0;
   fa.ts_len = pg_timestamp(fa.edge_ts, fa.ts);
   fa.status = d_fb_status_;
-  fb_epoch_ = (fb_epoch_ + 1) & 0x3fffffffu;
-  if (fb_epoch_ == 0) fb_epoch_ = 1;  // (status words start zeroed: epoch 0 never matches)
-  fa.epoch = fb_epoch_;
   fa.total = reinterpret_cast<uint32_t*>(d_fb_status_ + fb_status_n_) + k;
   fa.out = d_fb_out_[k];
   fa.fallback = d_fmt_fallback_;

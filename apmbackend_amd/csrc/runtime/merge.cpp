@@ -461,7 +461,9 @@ MergeResult merge_checkpoints(const std::vector<std::string>& inputs, const std:
       if (ser[j].at((size_t)s) >= 0) unseen.push_back(ser[j][s]);
   }
   const int64_t N = (int64_t)sr.size();
-  if (N > I0.max_series) {}  // (the loading engine checks its own gpu.maxSeries)
+  if (N > I0.max_series)  // (every input shares one config, so its maxSeries holds the merged table)
+    throw std::runtime_error("merge: " + std::to_string(N) + " merged series exceed gpu.maxSeries " +
+                             std::to_string(I0.max_series));
   res.series = N;
   auto per_series = [&](auto getter, auto& out) {  // concat of the kept columns of an [n] array
     for (size_t j = 0; j < in.size(); ++j) {
