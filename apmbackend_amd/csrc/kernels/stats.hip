@@ -22,6 +22,7 @@
 #include <rocprim/rocprim.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace apm {
 
@@ -414,6 +415,160 @@ __global__ __launch_bounds__(WS_WAVES * APM_WAVE) void k_window_stats(WindowArgs
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   if (n > 1) wave_bitonic(t, np2, lane);
   if (lane == 0) finish_series(a, s, n, sum, t);
+}
+
+// K8 for windows of at most 32 buckets (the shipped config: window 31 -> 32 window buckets): two
+// series per wave, one per 32-lane half.  Lane r of each half owns window bucket r, so the two
+// halves' count and cell loads of a bucket hit adjacent series -- the same cache line -- and the
+// prefix scans / sorting network run 32 lanes wide (5 + 15 shuffle steps instead of 6 + 21, each
+// step serving two series).  Windows of at most 32 samples (nearly all) are sorted in registers;
+// up to 512 by the half in LDS; larger ones go to the block pass, NaN windows to the JS pass.
+// APM_K8_H2=0 keeps the one-series-per-wave kernel (A/B).
+constexpr int HW = 32;                 // lanes per series
+constexpr int H2_TILE = WS_TILE / 2;   // samples per half in LDS
+
+__device__ inline void half_bitonic(int32_t* a, int n, int hl) {
+  for (int k = 2; k <= n; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = hl; i < n; i += HW) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const int32_t x = a[i], y = a[ixj];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) { a[i] = y; a[ixj] = x; }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    }
+  }
+}
+
+__global__ __launch_bounds__(WS_WAVES * APM_WAVE) void k_window_stats_h2(WindowArgs a) {
+  __shared__ int32_t tile[WS_WAVES * 2][H2_TILE];
+  const int lane = threadIdx.x & 63;
+  const int half = lane >> 5, hl = lane & (HW - 1);
+  const int wv = threadIdx.x >> 6;
+  const int s = (blockIdx.x * WS_WAVES + wv) * 2 + half;
+  // no early return per half: the shuffles below are 32 lanes wide, and both halves run them
+  const bool valid = s < a.n_series;
+  const bool active = valid && a.st.active[s];
+  if (valid && !active && hl == 0) { WinStat w{}; w.active = 0; w.n = 0; a.out[s] = w; }
+  int cnt = 0, slot = -1;
+  if (active && hl < a.n_win) {
+    slot = a.win_slots[hl];
+    if (slot >= 0) cnt = a.st.counts[(size_t)slot * a.st.S + s];
+  }
+  const int inl = min(cnt, a.st.cap);
+  const int spill = cnt - inl;
+  int pre = inl;
+#pragma unroll
+  for (int o = 1; o < HW; o <<= 1) {
+    const int v = __shfl_up(pre, o, HW);
+    if (hl >= o) pre += v;
+  }
+  const int total_inl = __shfl(pre, HW - 1, HW);
+  int total_spill = spill;
+#pragma unroll
+  for (int o = HW / 2; o > 0; o >>= 1) total_spill += __shfl_xor(total_spill, o, HW);
+  const int n = total_inl + total_spill;
+  const bool big = active && n > H2_TILE;
+  if (big && hl == 0) { const int j = atomicAdd(a.big_n, 1); a.big_list[j] = s; }
+  const bool go = active && !big;
+  int32_t* t = tile[wv * 2 + half];
+  pre -= inl;
+  long long sum = 0;
+  int nan = 0;
+  if (go && inl > 0) {
+    const int32_t* cell = a.st.cells + ((size_t)slot * a.st.S + s) * a.st.cap;
+    for (int k = 0; k < inl; ++k) { const int32_t v = cell[k]; t[pre + k] = v; sum += v; nan += v == ELAPSED_NAN; }
+  }
+  // spilled samples: each window bucket's run found by its lane, copied by the half
+  const unsigned long long any_spill = __ballot(go && total_spill > 0);
+  if (any_spill) {
+    const int32_t* run = go && spill > 0 ? spill_run(a.st, slot, s) : nullptr;
+    int spre = go ? spill : 0;
+#pragma unroll
+    for (int o = 1; o < HW; o <<= 1) {
+      const int v = __shfl_up(spre, o, HW);
+      if (hl >= o) spre += v;
+    }
+    spre -= go ? spill : 0;
+    const unsigned long long all = __ballot(go && spill > 0);
+    unsigned int todo = (unsigned int)(half ? (all >> 32) : (all & 0xffffffffull));
+    __builtin_amdgcn_wave_barrier();
+    // (both halves run the loop the larger number of times; a half with nothing left idles)
+    const unsigned int other = (unsigned int)(half ? (all & 0xffffffffull) : (all >> 32));
+    const int iters = max(__popc(todo), __popc(other));
+    for (int it = 0; it < iters; ++it) {
+      const int r = todo ? __ffs((int)todo) - 1 : 0;
+      const bool mine = todo != 0;
+      todo &= todo - 1;
+      const int m = __shfl(spill, r, HW);
+      const int off = total_inl + __shfl(spre, r, HW);
+      const uintptr_t rp = (uintptr_t)__shfl((long long)(uintptr_t)run, r, HW);
+      if (mine) {
+        const int32_t* src = (const int32_t*)rp;
+        for (int k = hl; k < m; k += HW) {
+          const int32_t v = src[k];
+          t[off + k] = v;
+          sum += v;
+          nan += v == ELAPSED_NAN;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int o = HW / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, HW);
+#pragma unroll
+  for (int o = HW / 2; o > 0; o >>= 1) nan += __shfl_xor(nan, o, HW);
+  const bool has_nan = go && nan > 0;
+  if (has_nan && hl == 0) a.nan_list[atomicAdd(a.nan_n, 1)] = s;
+  const bool ok = go && !has_nan;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  // register network for n <= 32 (every lane runs it: the shuffles need both halves)
+  int32_t v = ok && n <= HW && hl < n ? t[hl] : 0x7fffffff;
+#pragma unroll
+  for (int k = 2; k <= HW; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const int32_t o = __shfl_xor(v, j, HW);
+      const bool keep_min = ((hl & j) == 0) == ((hl & k) == 0);
+      v = keep_min ? min(v, o) : max(v, o);
+    }
+  }
+  int l75, h75, l95, h95;
+  percentile_ranks(ok && n <= HW ? n : 1, 75, l75, h75);
+  percentile_ranks(ok && n <= HW ? n : 1, 95, l95, h95);
+  const int32_t a75 = __shfl(v, max(l75, 0), HW), b75 = __shfl(v, max(h75, 0), HW);
+  const int32_t a95 = __shfl(v, max(l95, 0), HW), b95 = __shfl(v, max(h95, 0), HW);
+  if (!ok) return;
+  if (n <= HW) {
+    if (hl == 0) {
+      WinStat w;
+      w.n = n;
+      w.active = 1;
+      w.tpm = js_round_fixed((double)n / a.tpm_div, 2);
+      if (n > 0) {
+        w.avg = js_round_fixed((double)sum / (double)n, 1);
+        w.p75 = js_round_fixed(l75 == h75 ? (double)a75 : ((double)a75 + (double)b75) / 2.0, 1);
+        w.p95 = js_round_fixed(l95 == h95 ? (double)a95 : ((double)a95 + (double)b95) / 2.0, 1);
+      } else {
+        w.avg = w.p75 = w.p95 = apm_nan();
+      }
+      a.out[s] = w;
+    }
+    return;
+  }
+  // 32 < n <= 512: this half sorts its tile in LDS
+  int np2 = HW;
+  while (np2 < n) np2 <<= 1;
+  for (int i = n + hl; i < np2; i += HW) t[i] = 0x7fffffff;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  half_bitonic(t, np2, hl);
+  if (hl == 0) finish_series(a, s, n, sum, t);
 }
 
 // Every sample of series s in the window (inline cells + spill lists), visited by the block.
@@ -863,9 +1018,16 @@ void apm_nan_mark(const TxRec* d_tx, uint32_t n, StatsState* st, hipStream_t str
 
 // big_n / nan_n must be zero on entry (the engine clears them with the rollover's other counters)
 void apm_window_stats(WindowArgs* a, hipStream_t stream) {
-  const int blocks = (a->n_series + WS_WAVES - 1) / WS_WAVES;
-  if (blocks == 0) return;
-  hipLaunchKernelGGL(k_window_stats, dim3(blocks), dim3(WS_WAVES * APM_WAVE), 0, stream, *a);
+  static const bool h2 = [] { const char* e = std::getenv("APM_K8_H2"); return !(e && e[0] == '0'); }();
+  if (h2 && a->n_win <= HW && !a->lds_sort) {
+    const int blocks2 = (a->n_series + 2 * WS_WAVES - 1) / (2 * WS_WAVES);
+    if (blocks2 == 0) return;
+    hipLaunchKernelGGL(k_window_stats_h2, dim3(blocks2), dim3(WS_WAVES * APM_WAVE), 0, stream, *a);
+  } else {
+    const int blocks = (a->n_series + WS_WAVES - 1) / WS_WAVES;
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(k_window_stats, dim3(blocks), dim3(WS_WAVES * APM_WAVE), 0, stream, *a);
+  }
   hipLaunchKernelGGL(k_window_stats_big, dim3(64), dim3(1024), 0, stream, *a);
   hipLaunchKernelGGL(k_window_stats_js, dim3(JS_BLOCKS), dim3(1024), 0, stream, *a);
 }
