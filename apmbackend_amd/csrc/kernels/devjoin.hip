@@ -517,16 +517,20 @@ __device__ __forceinline__ uint8_t hf_event(const Event& e, uint32_t i, const ui
   const uint32_t lead = e.off & 15u;
   const uint32_t nvec = (lead + e.len + 15u) >> 4;
   if (staged && hf_needs_bytes(e) && nvec * 16u <= (uint32_t)HF_SLOT) {
-    // the line's aligned 16-byte blocks, every load issued before the first LDS store
+    // the line's aligned 16-byte blocks, four loads in flight before their LDS stores (sixteen
+    // held at once put the array on scratch: 272 B of private memory per lane)
     const uint4* __restrict__ src = reinterpret_cast<const uint4*>(bytes + (e.off - lead));
     uint4* dst = reinterpret_cast<uint4*>(stage + threadIdx.x * HF_PITCH);
-    uint4 v[HF_SLOT / 16];
-#pragma unroll
-    for (int k = 0; k < HF_SLOT / 16; ++k)
-      if ((uint32_t)k < nvec) v[k] = src[k];
-#pragma unroll
-    for (int k = 0; k < HF_SLOT / 16; ++k)
-      if ((uint32_t)k < nvec) dst[k] = v[k];
+    for (uint32_t k = 0; k < nvec; k += 4) {
+      const uint4 v0 = src[k];
+      const uint4 v1 = k + 1 < nvec ? src[k + 1] : v0;
+      const uint4 v2 = k + 2 < nvec ? src[k + 2] : v0;
+      const uint4 v3 = k + 3 < nvec ? src[k + 3] : v0;
+      dst[k] = v0;
+      if (k + 1 < nvec) dst[k + 1] = v1;
+      if (k + 2 < nvec) dst[k + 2] = v2;
+      if (k + 3 < nvec) dst[k + 3] = v3;
+    }
     p = stage + threadIdx.x * HF_PITCH + lead;
   }
   return (uint8_t)(hf_fields(e, p, fkey, aud, i, bytewise) | app_bits(e));
@@ -539,14 +543,17 @@ __device__ __forceinline__ uint8_t hf_event(const Event& e, uint32_t i, const ui
 // from its Event alone.  One lane per event over the whole batch made every wave execute each of
 // the walks its few byte events needed, the other lanes idle (the largest join-side kernel:
 // 137 us a batch, profiles/r5_final2).  split == 0: the one-pass form (APM_HF_SPLIT=0, A/B).
+template <bool SPLIT>
 __global__ __launch_bounds__(TB) void k_host_flags(const Event* __restrict__ ev, const uint32_t* __restrict__ n_ev_dev,
                                                    const uint8_t* __restrict__ bytes, const uint32_t* __restrict__ chunk_file,
                                                    const uint64_t* __restrict__ file_fkey,
                                                    uint8_t* __restrict__ flag, uint64_t* __restrict__ val,
                                                    AudF* __restrict__ aud, SelCount* __restrict__ totals, uint32_t cap,
-                                                   int bytewise, int staged, int split, uint32_t* __restrict__ list,
+                                                   int bytewise, int staged, uint32_t* __restrict__ list,
                                                    uint32_t* __restrict__ list_n) {
-  __shared__ __attribute__((aligned(16))) uint8_t stage[TB * HF_PITCH];
+  constexpr int split = SPLIT ? 1 : 0;
+  // (the split form reads no bytes: no LDS stage, so the occupancy is register-bound)
+  __shared__ __attribute__((aligned(16))) uint8_t stage[SPLIT ? 16 : TB * HF_PITCH];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t n = min(*n_ev_dev, cap);
   if (blockIdx.x * blockDim.x >= n) return;  // (uniform per block: the grid is sized for the capacity)
@@ -566,8 +573,9 @@ __global__ __launch_bounds__(TB) void k_host_flags(const Event* __restrict__ ev,
     if (defer && !front) list[cap - 1 - b] = i;
   }
   if (i < n && !defer) {
-    const uint8_t fl = split ? (uint8_t)(hf_fields(e, bytes + e.off, 0, aud, i, bytewise) | app_bits(e))
-                             : hf_event(e, i, bytes, chunk_file, file_fkey, aud, stage, bytewise, staged);
+    uint8_t fl;
+    if constexpr (SPLIT) fl = (uint8_t)(hf_fields(e, bytes + e.off, 0, aud, i, bytewise) | app_bits(e));
+    else fl = hf_event(e, i, bytes, chunk_file, file_fkey, aud, stage, bytewise, staged);
     flag[i] = fl;
     val[i] = sel_pack(fl);
   }
@@ -636,7 +644,7 @@ __device__ const HostOp* find_hop(const HostOp* __restrict__ h, uint32_t n, uint
   return (lo < n && h[lo].ev == ev) ? &h[lo] : nullptr;
 }
 
-__global__ void k_build_ops(DJArgs a) {
+__global__ __launch_bounds__(TB) void k_build_ops(DJArgs a) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.n_ev) return;
   const Event e = a.ev[i];
@@ -795,7 +803,7 @@ __device__ __forceinline__ uint32_t wave_fscan(uint32_t f, int lane) {
 // max(n_chunks, n_ev) + 1 lanes, and it runs before any kernel that touches them)
 // (also the batch's zero fills of the join stream: the JoinCounts prefix, out_cnt, the audit
 // carry of the next generation and the per-file first-chunk marks -- one launch, no memsets)
-__global__ void k_chunk_events(const Event* __restrict__ ev, uint32_t n_ev, uint32_t n_chunks, uint32_t* __restrict__ lo,
+__global__ __launch_bounds__(TB) void k_chunk_events(const Event* __restrict__ ev, uint32_t n_ev, uint32_t n_chunks, uint32_t* __restrict__ lo,
                                uint32_t* __restrict__ zero_words, uint32_t n_zero_words, uint32_t* __restrict__ out_cnt,
                                uint32_t* __restrict__ carry_words, uint32_t n_carry_words,
                                uint32_t* __restrict__ first_chunk, uint32_t n_files) {
@@ -830,7 +838,7 @@ __global__ __launch_bounds__(APM_WAVE) void k_soap_summary(DJArgs a) {
   if (lane == 0) a.seg_f[(size_t)c * SOAP_SEGS + g] = acc;
 }
 
-__global__ void k_soap_carry(DJArgs a) {
+__global__ __launch_bounds__(64) void k_soap_carry(DJArgs a) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= a.n_chunks || a.chunk_kind[c] != FILE_SOAP || !a.chunk_first[c]) return;
   const int32_t file = (int32_t)a.chunk_file[c];
@@ -910,7 +918,7 @@ __device__ uint32_t aud_put_txt(const DJArgs& a, const uint8_t* src, uint32_t le
   return o;
 }
 
-__global__ void k_aud_keys(DJArgs a) {
+__global__ __launch_bounds__(TB) void k_aud_keys(DJArgs a) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t nc = a.gin.n_autr;
   if (j >= nc + a.n_mh) return;
@@ -918,7 +926,7 @@ __global__ void k_aud_keys(DJArgs a) {
   a.aud_ord[j] = j;
 }
 
-__global__ void k_aud_autr(DJArgs a) {
+__global__ __launch_bounds__(TB) void k_aud_autr(DJArgs a) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t nc = a.gin.n_autr, N = nc + a.n_mh;
   if (j >= N) return;
@@ -957,7 +965,7 @@ __global__ void k_aud_autr(DJArgs a) {
   a.gout.autr[k] = t;
 }
 
-__global__ void k_aud_chunks(DJArgs a) {
+__global__ __launch_bounds__(TB) void k_aud_chunks(DJArgs a) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c < a.n_chunks && a.chunk_first[c]) a.file_first_chunk[a.chunk_file[c]] = (int32_t)c;
   // walk_lo[k] = first walk position of chunk k: lane q owns the boundaries between walk
@@ -990,7 +998,7 @@ struct AudWalk {  // one open audit block (AuditCtx of the host state machine)
   uint32_t head, tail;  // queued elapsed entries (item slots), insertion order
 };
 
-__global__ void k_aud_walk(DJArgs a) {
+__global__ __launch_bounds__(64) void k_aud_walk(DJArgs a) {
   const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t nw = a.n_walk;
   if (id >= nw + a.n_files) return;
@@ -1180,7 +1188,7 @@ __device__ int32_t reg_find(const RegSlot* __restrict__ t, uint32_t mask, uint64
   return RAW_EMPTY;
 }
 
-__global__ void k_claim(DJArgs a) {
+__global__ __launch_bounds__(TB) void k_claim(DJArgs a) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.n_ev) return;
   const JOp& op = a.ops[i];
@@ -1539,7 +1547,7 @@ struct GwRow {
     return v;
   }
 };
-__global__ void k_group_walk(DJArgs a) {
+__global__ __launch_bounds__(TB) void k_group_walk(DJArgs a) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.n_ev) return;
   const uint32_t cap = a.table_mask + 1;
@@ -1738,7 +1746,7 @@ __device__ void walk_group(DJArgs& a, uint32_t slot, const M& mem, uint32_t g) {
 }
 
 // ---- expiry of needNumRecordCache regions (NodeCache 'expired' -> outputRecord, :226-239)
-__global__ void k_exp_keys(DJArgs a) {
+__global__ __launch_bounds__(TB) void k_exp_keys(DJArgs a) {
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= a.n_exp_entries) return;
   uint64_t rem = e, v = 0;
@@ -1757,7 +1765,7 @@ __global__ void k_exp_keys(DJArgs a) {
   }
 }
 
-__global__ void k_exp_count(DJArgs a) {
+__global__ __launch_bounds__(TB) void k_exp_count(DJArgs a) {
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e > a.n_exp_entries) return;
   if (e == a.n_exp_entries) { a.exp_cnt[e] = 0; return; }
@@ -1792,7 +1800,7 @@ __global__ void k_exp_emit(DJArgs a) {
   ne.key = 0;  // the entry is gone (an expired region is reused by later batches)
 }
 
-__global__ void k_place(DJArgs a) {
+__global__ __launch_bounds__(TB) void k_place(DJArgs a) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t base = a.counts->n_exp_out;
   if (i == 0) a.counts->n_out = base + a.out_pos[a.n_ev];
@@ -1803,7 +1811,7 @@ __global__ void k_place(DJArgs a) {
   if (p < a.out_cap) a.out[p] = a.stage[(size_t)ev * 2 + sub];
 }
 
-__global__ void k_place_ovf(DJArgs a) {
+__global__ __launch_bounds__(TB) void k_place_ovf(DJArgs a) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t n = min(a.counts->pad[0], DJ_OVF_CAP);
   if (k >= n) return;
@@ -1841,7 +1849,7 @@ __device__ uint32_t line_len(const DJFormatArgs& f, const TxDev& t) {
   return n + 1;  // '\n'
 }
 
-__global__ void k_resolve_len(DJFormatArgs f) {
+__global__ __launch_bounds__(TB) void k_resolve_len(DJFormatArgs f) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t n = f.n_out;
   U4* lens = reinterpret_cast<U4*>(f.lens);
@@ -2029,7 +2037,7 @@ __device__ __forceinline__ void write_one(const DJFormatArgs& f, const TxDev& t,
   }
 }
 
-__global__ void k_cands(DJFormatArgs f) {
+__global__ __launch_bounds__(TB) void k_cands(DJFormatArgs f) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (f.counts->pad[1] != DJ_WRITE_OK || j >= f.counts->n_stats) return;
   if (j == 0 || f.tx_bmax[j] > f.tx_bmax[j - 1]) {
@@ -2581,9 +2589,12 @@ int apm_dj_select_host(DJArgs* a, const uint32_t* d_n_ev, uint32_t max_ev, hipSt
   uint32_t* list_n = list + max_ev;
   if (split) HIP_OK(hipMemsetAsync(list_n, 0, 8, s));
   const dim3 grid((max_ev + TB - 1) / TB);
-  hipLaunchKernelGGL(k_host_flags, grid, dim3(TB), 0, s, a->ev, d_n_ev, a->bytes, a->chunk_file, a->file_fkey,
-                     a->host_flag, a->sel_val, a->aud, a->n_host, max_ev, pre_bytewise(), hf_staged(), split, list,
-                     list_n);
+  if (split)
+    hipLaunchKernelGGL(k_host_flags<true>, grid, dim3(TB), 0, s, a->ev, d_n_ev, a->bytes, a->chunk_file, a->file_fkey,
+                       a->host_flag, a->sel_val, a->aud, a->n_host, max_ev, pre_bytewise(), hf_staged(), list, list_n);
+  else
+    hipLaunchKernelGGL(k_host_flags<false>, grid, dim3(TB), 0, s, a->ev, d_n_ev, a->bytes, a->chunk_file, a->file_fkey,
+                       a->host_flag, a->sel_val, a->aud, a->n_host, max_ev, pre_bytewise(), hf_staged(), list, list_n);
   dj_check(s, "k_host_flags");
   if (split) {
     hipLaunchKernelGGL(k_host_flags_bytes, grid, dim3(TB), 0, s, a->ev, a->bytes, a->chunk_file, a->file_fkey,
