@@ -99,7 +99,7 @@ EngineConfig config_from(const py::dict& d) {
   c.window = get<int>(d, "window", c.window);
   c.buffer = get<int>(d, "buffer", c.buffer);
   c.nslot = get<int>(d, "nslot", c.nslot);
-  c.ck_stage_mb = get<int64_t>(d, "ck_stage_mb", c.ck_stage_mb);
+  c.ck_stage_bytes = get<int64_t>(d, "ck_stage_bytes", c.ck_stage_bytes);
   c.record_ttl_ms = get<double>(d, "record_ttl_ms", c.record_ttl_ms);
   c.acct_ttl_ms = get<double>(d, "acct_ttl_ms", c.acct_ttl_ms);
   c.need_ttl_ms = get<double>(d, "need_ttl_ms", c.need_ttl_ms);

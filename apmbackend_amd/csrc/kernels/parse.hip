@@ -33,71 +33,112 @@ constexpr int PARSE_BLOCK = 256;           // lines per block in the parse pass
 constexpr int PARSE_LDS = 32 * 1024;       // staged bytes per block (+ 8 KB token table: 4 blocks / CU)
 
 // --------------------------------------------------------------------------------- K1
+// Each block covers NL_PER consecutive 4 KB tiles (one 16-byte vector per lane per tile, all of
+// them loaded before the first is used: four loads in flight per lane instead of one, a quarter of
+// the blocks) and still reports one newline count per 4 KB tile -- the granularity tile_off[]
+// has for k_parse_tiles.  (One tile a block: 38 + 47 us a batch for 28 MB, profiles/r6_g.)
+constexpr int NL_PER = 4;
+
+__device__ __forceinline__ uint32_t nl_count16(const uint4 v) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    // count bytes equal to '\n' (0x0a) in a 32-bit word: exact per-byte SWAR (no borrow between
+    // bytes -- the (x - 0x01..) & ~x form also flags a 0x0b right after a '\n', and k_nl_write,
+    // which counts exactly, would then leave holes in line_end)
+    const uint32_t x = w[k] ^ 0x0a0a0a0aU;
+    const uint32_t t = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+    c += __popc(t);
+  }
+  return c;
+}
+
 __global__ __launch_bounds__(NL_BLOCK) void k_nl_count(const uint8_t* __restrict__ bytes, uint64_t n,
-                                                      uint32_t* __restrict__ tile_counts, uint8_t* __restrict__ pad) {
-  const uint64_t base = (uint64_t)blockIdx.x * NL_TILE + threadIdx.x * 16;
+                                                      uint32_t* __restrict__ tile_counts, uint8_t* __restrict__ pad,
+                                                      uint32_t tiles) {
   // (folded fills) the 64 zero bytes after the batch that K2's 16-byte loads may touch, and the
   // scan's extra tile entry -- no block reads either of them
   if (blockIdx.x == 0 && threadIdx.x < 64) pad[threadIdx.x] = 0;
-  if (blockIdx.x == 0 && threadIdx.x == 64) tile_counts[gridDim.x] = 0;
-  int c = 0;
-  if (base + 16 <= n) {
-    const uint4 v = *reinterpret_cast<const uint4*>(bytes + base);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  if (blockIdx.x == 0 && threadIdx.x == 64) tile_counts[tiles] = 0;
+  uint4 v[NL_PER];
+  uint64_t base[NL_PER];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      // count bytes equal to '\n' (0x0a) in a 32-bit word: exact per-byte SWAR (no borrow
-      // between bytes -- the (x - 0x01..) & ~x form also flags a 0x0b right after a '\n', and
-      // k_nl_write, which counts exactly, would then leave holes in line_end)
-      const uint32_t x = w[k] ^ 0x0a0a0a0aU;
-      const uint32_t t = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
-      c += __popc(t);
-    }
-  } else {
-    for (uint64_t i = base; i < n && i < base + 16; ++i) c += bytes[i] == '\n';
+  for (int k = 0; k < NL_PER; ++k) {
+    base[k] = ((uint64_t)blockIdx.x * NL_PER + k) * NL_TILE + threadIdx.x * 16;
+    if (base[k] + 16 <= n) v[k] = *reinterpret_cast<const uint4*>(bytes + base[k]);
   }
-  // block reduction
-  __shared__ int red[NL_BLOCK / APM_WAVE];
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, APM_WAVE);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  // per tile counts packed two to a word (a tile has at most 4096 newlines: 16 bits each)
+  uint32_t pk[NL_PER / 2] = {0, 0};
+#pragma unroll
+  for (int k = 0; k < NL_PER; ++k) {
+    uint32_t c = 0;
+    if (base[k] + 16 <= n) {
+      c = nl_count16(v[k]);
+    } else {
+      for (uint64_t i = base[k]; i < n && i < base[k] + 16; ++i) c += bytes[i] == '\n';
+    }
+    pk[k >> 1] += c << (16 * (k & 1));
+  }
+  __shared__ uint32_t red[NL_PER / 2][NL_BLOCK / APM_WAVE];
+#pragma unroll
+  for (int h = 0; h < NL_PER / 2; ++h) {
+    uint32_t c = pk[h];
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, APM_WAVE);
+    if ((threadIdx.x & 63) == 0) red[h][threadIdx.x >> 6] = c;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int s = 0;
-    for (int i = 0; i < NL_BLOCK / APM_WAVE; ++i) s += red[i];
-    tile_counts[blockIdx.x] = s;
+  if (threadIdx.x < NL_PER) {
+    const int k = threadIdx.x;
+    uint32_t sum = 0;
+    for (int i = 0; i < NL_BLOCK / APM_WAVE; ++i) sum += red[k >> 1][i];
+    const uint32_t tile = blockIdx.x * NL_PER + k;
+    if (tile < tiles) tile_counts[tile] = (sum >> (16 * (k & 1))) & 0xFFFFu;
   }
 }
 
-// Writes the byte position of every '\n' (= line end) in order; tile_off = exclusive scan.
+// Writes the byte position of every '\n' (= line end) in order; tile_off = exclusive scan of the
+// per-tile counts.
 __global__ __launch_bounds__(NL_BLOCK) void k_nl_write(const uint8_t* __restrict__ bytes, uint64_t n,
                                                       const uint32_t* __restrict__ tile_off,
-                                                      uint32_t* __restrict__ line_end, uint32_t* __restrict__ n_lines) {
-  const uint64_t base = (uint64_t)blockIdx.x * NL_TILE + threadIdx.x * 16;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *n_lines = tile_off[gridDim.x];  // (folded D2D copy)
-  uint8_t b[16];
-  int c = 0;
-  if (base + 16 <= n) {
-    const uint4 v = *reinterpret_cast<const uint4*>(bytes + base);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+                                                      uint32_t* __restrict__ line_end, uint32_t* __restrict__ n_lines,
+                                                      uint32_t tiles) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *n_lines = tile_off[tiles];  // (folded D2D copy)
+  uint4 v[NL_PER];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[k * 4 + j] = (uint8_t)(w[k] >> (8 * j));
-    }
-  } else {
-    for (int i = 0; i < 16; ++i) b[i] = (base + i < n) ? bytes[base + i] : 0;
+  for (int k = 0; k < NL_PER; ++k) {
+    const uint64_t base = ((uint64_t)blockIdx.x * NL_PER + k) * NL_TILE + threadIdx.x * 16;
+    v[k] = base + 16 <= n ? *reinterpret_cast<const uint4*>(bytes + base) : make_uint4(0, 0, 0, 0);
   }
-#pragma unroll
-  for (int i = 0; i < 16; ++i) c += b[i] == '\n';
-  // block exclusive scan of c
   typedef rocprim::block_scan<int, NL_BLOCK> Scan;
   __shared__ typename Scan::storage_type st;
-  int excl;
-  Scan().exclusive_scan(c, excl, 0, st);
-  uint32_t pos = tile_off[blockIdx.x] + excl;
 #pragma unroll
-  for (int i = 0; i < 16; ++i)
-    if (b[i] == '\n') line_end[pos++] = (uint32_t)(base + i);
+  for (int k = 0; k < NL_PER; ++k) {
+    const uint32_t tile = blockIdx.x * NL_PER + k;
+    if (tile >= tiles) break;  // (uniform per block)
+    const uint64_t base = (uint64_t)tile * NL_TILE + threadIdx.x * 16;
+    uint8_t b[16];
+    if (base + 16 <= n) {
+      const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[q * 4 + j] = (uint8_t)(w[q] >> (8 * j));
+      }
+    } else {
+      for (int i = 0; i < 16; ++i) b[i] = (base + i < n) ? bytes[base + i] : 0;
+    }
+    int c = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) c += b[i] == '\n';
+    int excl;
+    Scan().exclusive_scan(c, excl, 0, st);
+    uint32_t pos = tile_off[tile] + excl;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (b[i] == '\n') line_end[pos++] = (uint32_t)(base + i);
+    __syncthreads();  // (the scan storage is reused by the next tile)
+  }
 }
 
 // --------------------------------------------------------------------------------- K2 helpers
@@ -1097,15 +1138,21 @@ __global__ __launch_bounds__(APM_WAVE) void k_section_apply(const uint32_t* __re
   }
 }
 
+// First line of every chunk: the newline pass's per-tile line counts bound the search to the lines
+// ending in the chunk start's 4 KB tile (~7 dependent loads, not ~20 over the whole batch: this
+// one-lane-per-chunk kernel was pure load latency, 38 us a batch, profiles/r6_g).
 __global__ void k_chunk_lines(const uint32_t* __restrict__ chunk_begin, uint32_t n_chunks,
                               const uint32_t* __restrict__ line_end, const uint32_t* __restrict__ n_lines_dev,
-                              uint32_t* __restrict__ chunk_line_lo) {
+                              uint32_t* __restrict__ chunk_line_lo, const uint32_t* __restrict__ tile_off,
+                              uint32_t tiles) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c > n_chunks) return;
   const uint32_t n_lines = *n_lines_dev;
-  // first line whose end >= chunk_begin[c]
+  // first line whose end >= chunk_begin[c]: lines ending before tile t number tile_off[t], and
+  // the line through tile t's end is at most tile_off[t + 1]
   const uint32_t pos = chunk_begin[c];
-  uint32_t lo = 0, hi = n_lines;
+  const uint32_t t = pos / (uint32_t)NL_TILE;
+  uint32_t lo = t < tiles ? tile_off[t] : n_lines, hi = t < tiles ? tile_off[t + 1] : n_lines;
   while (lo < hi) {
     uint32_t mid = (lo + hi) >> 1;
     if (line_end[mid] < pos) lo = mid + 1; else hi = mid;
@@ -1175,16 +1222,17 @@ int apm_parse_batch(const uint8_t* d_bytes, uint64_t n_bytes, const uint32_t* d_
   uint8_t* chunk_init = carve((size_t)(n_chunks + 2));
   void* scan_tmp = carve(APM_SCAN_TMP);
 
-  hipLaunchKernelGGL(k_nl_count, dim3(tiles), dim3(NL_BLOCK), 0, stream, d_bytes, n_bytes, tile_counts,
-                     const_cast<uint8_t*>(d_bytes) + n_bytes);
+  const uint32_t nl_blocks = (tiles + NL_PER - 1) / NL_PER;
+  hipLaunchKernelGGL(k_nl_count, dim3(nl_blocks), dim3(NL_BLOCK), 0, stream, d_bytes, n_bytes, tile_counts,
+                     const_cast<uint8_t*>(d_bytes) + n_bytes, tiles);
   size_t tmp_bytes = 0;
   HIP_OK(rocprim::exclusive_scan(nullptr, tmp_bytes, tile_counts, tile_off, 0u, tiles + 1,
                                  rocprim::plus<uint32_t>(), stream));
   if (tmp_bytes > APM_SCAN_TMP) return -1;
   HIP_OK(rocprim::exclusive_scan(scan_tmp, tmp_bytes, tile_counts, tile_off, 0u, tiles + 1,
                                  rocprim::plus<uint32_t>(), stream));
-  hipLaunchKernelGGL(k_nl_write, dim3(tiles), dim3(NL_BLOCK), 0, stream, d_bytes, n_bytes, tile_off, line_end,
-                     d_n_lines);
+  hipLaunchKernelGGL(k_nl_write, dim3(nl_blocks), dim3(NL_BLOCK), 0, stream, d_bytes, n_bytes, tile_off, line_end,
+                     d_n_lines, tiles);
 
   ParseArgs pa;
   pa.bytes = d_bytes;
@@ -1230,7 +1278,7 @@ int apm_parse_batch(const uint8_t* d_bytes, uint64_t n_bytes, const uint32_t* d_
             h[PP_COOP] ? (double)h[PP_HEAD] / h[PP_COOP] : 0.0, h[PP_COOP] ? (double)h[PP_TAIL] / h[PP_COOP] : 0.0);
   }
   hipLaunchKernelGGL(k_chunk_lines, dim3((n_chunks + 1 + 255) / 256), dim3(256), 0, stream, d_chunk_begin,
-                     n_chunks, line_end, d_n_lines, chunk_line_lo);
+                     n_chunks, line_end, d_n_lines, chunk_line_lo, tile_off, tiles);
   hipLaunchKernelGGL(k_section_summary, dim3(n_chunks, SEC_SEGS), dim3(APM_WAVE), 0, stream, chunk_line_lo,
                      d_chunk_kind, d_chunk_file, n_chunks, line_mask, d_file_open, seg_state, chunk_init);
   hipLaunchKernelGGL(k_section_apply, dim3(n_chunks, SEC_SEGS), dim3(APM_WAVE), 0, stream, chunk_line_lo,

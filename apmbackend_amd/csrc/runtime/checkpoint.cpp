@@ -1094,7 +1094,7 @@ int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& e
     need += (size_t)NSTAT * lg.heads.size() * n * rb;
     job->lags.push_back(std::move(lg));
   }
-  const size_t cap = cfg_.ck_stage_mb > 0 ? (size_t)cfg_.ck_stage_mb << 20 : SIZE_MAX;
+  const size_t cap = cfg_.ck_stage_bytes > 0 ? (size_t)cfg_.ck_stage_bytes : SIZE_MAX;
   const size_t row_bytes = (size_t)NSTAT * n * rb;  // one ring position of one LAG, every stat
   if (need > cap && n > 0) {
     // Streamed snapshot: the ring rows do not fit the staging cap (rings sized toward HBM).  Stage
@@ -1499,7 +1499,7 @@ CheckpointInfo Engine::checkpoint_info() {
   c.streamed_live_rows = ck_streamed_live_;
   c.side_rows = ck_side_rows_;
   c.guard_stalls = ck_guard_stalls_;
-  c.stage_cap = cfg_.ck_stage_mb > 0 ? (uint64_t)cfg_.ck_stage_mb << 20 : 0;
+  c.stage_cap = cfg_.ck_stage_bytes > 0 ? (uint64_t)cfg_.ck_stage_bytes : 0;
   return c;
 }
 

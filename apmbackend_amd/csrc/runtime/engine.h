@@ -105,7 +105,7 @@ struct EngineConfig {
   int window = 30;
   int buffer = 6;
   int nslot = 0;  // bucket ring slots (gpu.bucketRingSlots; 0 = ring_slots_for(window, buffer))
-  int64_t ck_stage_mb = 2048;  // HBM staging of a snapshot's ring rows (gpu.checkpointStageMB; 0 = unbounded)
+  int64_t ck_stage_bytes = (int64_t)2048 << 20;  // HBM staging of a snapshot's ring rows (gpu.checkpointStageMB; 0 = unbounded)
   // parse
   double record_ttl_ms = 120000, acct_ttl_ms = 120000, need_ttl_ms = 30000;
   TzTable tz{};

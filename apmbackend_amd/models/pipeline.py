@@ -89,7 +89,7 @@ def engine_config(cfg: Dict[str, Any], device: int = 0, keep_text: bool = False,
         # bucket ring slots (0: window + buffer + 1, at least 40); a reload to a longer window grows it
         "nslot": int(g.get("bucketRingSlots", 0)),
         # HBM staging of a base checkpoint's ring rows; a larger ring streams (checkpoint.cpp)
-        "ck_stage_mb": int(g.get("checkpointStageMB", 2048)),
+        "ck_stage_bytes": int(float(g.get("checkpointStageMB", 2048)) * (1 << 20)),
         "buffer": int(sc["bufferSizeInIntervals"]),
         "record_ttl_ms": float(g.get("recordTtlSeconds", 120)) * 1000.0,
         "acct_ttl_ms": float(g.get("acctTtlSeconds", 120)) * 1000.0,
