@@ -21,7 +21,7 @@ def main(root):
             for rj in sorted(glob.glob(os.path.join(rep, "rank*.json"))):
                 r = json.load(open(rj))
                 lock.append((r.get("lockstep_ms_per_step"), r.get("lockstep_max_ms")))
-            print(f"{os.path.basename(log):24s} {d['value'] / 1e6:8.1f} M  {d['ms_per_step']:.3f} ms  {extra}"
+            print(f"{os.path.basename(log):24s} {d['value'] / 1e6:8.1f} M  {d.get('ms_per_step', float('nan')):.3f} ms  {extra}"
                   + (f"  lockstep(ms/step,max)={[(round(a, 3), round(b, 2)) for a, b in lock]}" if lock else ""))
 
 
