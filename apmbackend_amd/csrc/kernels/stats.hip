@@ -427,6 +427,69 @@ __global__ __launch_bounds__(WS_WAVES * APM_WAVE) void k_window_stats(WindowArgs
 constexpr int HW = 32;                 // lanes per series
 constexpr int H2_TILE = WS_TILE / 2;   // samples per half in LDS
 
+// Cross-lane moves inside a 32-lane half without the LDS crossbar (ds_bpermute): DPP where the
+// pattern stays inside a 16-lane row (quad permutes for xor 1 / 2, row_ror:8 for xor 8, row shifts
+// and row_bcast:15 for scans), ds_swizzle (no LDS bank access, no address VGPR) for xor 4 / 16.
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ int dpp(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWS, 0xF, false); }
+template <int J>
+__device__ __forceinline__ int32_t half_xor(int32_t v) {
+  if constexpr (J == 1) return dpp<0xB1>(v);          // quad_perm [1,0,3,2]
+  else if constexpr (J == 2) return dpp<0x4E>(v);     // quad_perm [2,3,0,1]
+  else if constexpr (J == 8) return dpp<0x128>(v);    // row_ror:8 == xor 8 inside a row
+  else if constexpr (J == 4) return __builtin_amdgcn_ds_swizzle(v, 0x101F);   // BitMode xor 4
+  else return __builtin_amdgcn_ds_swizzle(v, 0x401F);                         // BitMode xor 16
+}
+// inclusive prefix sum over each 32-lane half
+__device__ __forceinline__ int half_scan(int x) {
+  x += dpp<0x111>(x);        // row_shr:1
+  x += dpp<0x112>(x);        // row_shr:2
+  x += dpp<0x114>(x);        // row_shr:4
+  x += dpp<0x118>(x);        // row_shr:8
+  x += dpp<0x142, 0xA>(x);   // row_bcast:15 -> rows 1, 3
+  return x;
+}
+// the same for doubles (exact sums of integers below 2^53): the two words move together
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = dpp<CTRL, ROWS>((int)(b & 0xffffffffll));
+  const int hi = dpp<CTRL, ROWS>((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double half_scan_f64(double x) {
+  x += dpp_f64<0x111>(x);
+  x += dpp_f64<0x112>(x);
+  x += dpp_f64<0x114>(x);
+  x += dpp_f64<0x118>(x);
+  x += dpp_f64<0x142, 0xA>(x);
+  return x;
+}
+// lane 31 of this half (a half's total after half_scan): two readlanes, no crossbar
+__device__ __forceinline__ int half_last(int x, int half) {
+  const int a = __builtin_amdgcn_readlane(x, 31), b = __builtin_amdgcn_readlane(x, 63);
+  return half ? b : a;
+}
+__device__ __forceinline__ double half_last_f64(double x, int half) {
+  const long long v = __double_as_longlong(x);
+  const int lo = half_last((int)(v & 0xffffffffll), half), hi = half_last((int)(v >> 32), half);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <int K, int J>
+__device__ __forceinline__ int32_t bitonic_step(int32_t v, int hl) {
+  const int32_t o = half_xor<J>(v);
+  const bool keep_min = ((hl & J) == 0) == ((hl & K) == 0);
+  return keep_min ? min(v, o) : max(v, o);
+}
+template <int K>
+__device__ __forceinline__ int32_t bitonic_merge(int32_t v, int hl) {
+  if constexpr (K >= 32) v = bitonic_step<K, 16>(v, hl);
+  if constexpr (K >= 16) v = bitonic_step<K, 8>(v, hl);
+  if constexpr (K >= 8) v = bitonic_step<K, 4>(v, hl);
+  if constexpr (K >= 4) v = bitonic_step<K, 2>(v, hl);
+  return bitonic_step<K, 1>(v, hl);
+}
+
 __device__ inline void half_bitonic(int32_t* a, int n, int hl) {
   for (int k = 2; k <= n; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
@@ -461,16 +524,9 @@ __global__ __launch_bounds__(WS_WAVES * APM_WAVE) void k_window_stats_h2(WindowA
   }
   const int inl = min(cnt, a.st.cap);
   const int spill = cnt - inl;
-  int pre = inl;
-#pragma unroll
-  for (int o = 1; o < HW; o <<= 1) {
-    const int v = __shfl_up(pre, o, HW);
-    if (hl >= o) pre += v;
-  }
-  const int total_inl = __shfl(pre, HW - 1, HW);
-  int total_spill = spill;
-#pragma unroll
-  for (int o = HW / 2; o > 0; o >>= 1) total_spill += __shfl_xor(total_spill, o, HW);
+  int pre = half_scan(inl);
+  const int total_inl = half_last(pre, half);
+  const int total_spill = half_last(half_scan(spill), half);
   const int n = total_inl + total_spill;
   const bool big = active && n > H2_TILE;
   if (big && hl == 0) { const int j = atomicAdd(a.big_n, 1); a.big_list[j] = s; }
@@ -487,12 +543,7 @@ __global__ __launch_bounds__(WS_WAVES * APM_WAVE) void k_window_stats_h2(WindowA
   const unsigned long long any_spill = __ballot(go && total_spill > 0);
   if (any_spill) {
     const int32_t* run = go && spill > 0 ? spill_run(a.st, slot, s) : nullptr;
-    int spre = go ? spill : 0;
-#pragma unroll
-    for (int o = 1; o < HW; o <<= 1) {
-      const int v = __shfl_up(spre, o, HW);
-      if (hl >= o) spre += v;
-    }
+    int spre = half_scan(go ? spill : 0);
     spre -= go ? spill : 0;
     const unsigned long long all = __ballot(go && spill > 0);
     unsigned int todo = (unsigned int)(half ? (all >> 32) : (all & 0xffffffffull));
@@ -518,10 +569,10 @@ __global__ __launch_bounds__(WS_WAVES * APM_WAVE) void k_window_stats_h2(WindowA
       }
     }
   }
-#pragma unroll
-  for (int o = HW / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, HW);
-#pragma unroll
-  for (int o = HW / 2; o > 0; o >>= 1) nan += __shfl_xor(nan, o, HW);
+  // (window sums of int32 samples, at most 512 per half: exact in a double)
+  const long long total_sum = (long long)half_last_f64(half_scan_f64((double)sum), half);
+  nan = half_last(half_scan(nan), half);
+  sum = total_sum;
   const bool has_nan = go && nan > 0;
   if (has_nan && hl == 0) a.nan_list[atomicAdd(a.nan_n, 1)] = s;
   const bool ok = go && !has_nan;
@@ -529,15 +580,11 @@ __global__ __launch_bounds__(WS_WAVES * APM_WAVE) void k_window_stats_h2(WindowA
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   // register network for n <= 32 (every lane runs it: the shuffles need both halves)
   int32_t v = ok && n <= HW && hl < n ? t[hl] : 0x7fffffff;
-#pragma unroll
-  for (int k = 2; k <= HW; k <<= 1) {
-#pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      const int32_t o = __shfl_xor(v, j, HW);
-      const bool keep_min = ((hl & j) == 0) == ((hl & k) == 0);
-      v = keep_min ? min(v, o) : max(v, o);
-    }
-  }
+  v = bitonic_merge<2>(v, hl);
+  v = bitonic_merge<4>(v, hl);
+  v = bitonic_merge<8>(v, hl);
+  v = bitonic_merge<16>(v, hl);
+  v = bitonic_merge<32>(v, hl);
   int l75, h75, l95, h95;
   percentile_ranks(ok && n <= HW ? n : 1, 75, l75, h75);
   percentile_ranks(ok && n <= HW ? n : 1, 95, l95, h95);

@@ -282,7 +282,10 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
       int lo = 0, hi = 0;
       HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
       HIP_OK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, sp ? hi : 0));
-      HIP_OK(hipStreamCreateWithFlags(&parse_stream_, hipStreamNonBlocking));
+      // APM_PARSE_PRIO=1: the parse stream (the next batch's K1/K2, which the ingest thread waits
+      // for at the start of every batch) at high priority too -- A/B
+      static const bool pp = [] { const char* x = std::getenv("APM_PARSE_PRIO"); return x && x[0] == '1'; }();
+      HIP_OK(hipStreamCreateWithPriority(&parse_stream_, hipStreamNonBlocking, pp ? hi : 0));
       HIP_OK(hipStreamCreateWithFlags(&out_stream_, hipStreamNonBlocking));
     }
   }
