@@ -66,7 +66,22 @@ __global__ __launch_bounds__(256) void k_zscore_resync(ZArgs a) {
     const T* col = reinterpret_cast<const T*>(a.ring) + (size_t)k * L * S + s;
     int pos = oldest + i0;
     if (pos >= L) pos -= L;
-    for (int i = i0; i < i1; ++i) {
+    int i = i0;
+    // RS_BATCH ring rows loaded before the first is summed: that many 512 B row loads in flight
+    // per wave instead of one behind each compensated add (same order, same result)
+    constexpr int RS_BATCH = 8;
+    for (; i + RS_BATCH <= i1; i += RS_BATCH) {
+      double v[RS_BATCH];
+#pragma unroll
+      for (int u = 0; u < RS_BATCH; ++u) {
+        v[u] = ld(col + (size_t)pos * S);
+        if (++pos == L) pos = 0;
+      }
+#pragma unroll
+      for (int u = 0; u < RS_BATCH; ++u)
+        if (valid(v[u])) { neumaier(sum, comp, v[u]); neumaier(sq, sqc, v[u] * v[u]); ++c; }
+    }
+    for (; i < i1; ++i) {
       const double v = ld(col + (size_t)pos * S);
       if (valid(v)) { neumaier(sum, comp, v); neumaier(sq, sqc, v * v); ++c; }
       if (++pos == L) pos = 0;
