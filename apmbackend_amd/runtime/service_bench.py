@@ -133,6 +133,7 @@ def _run(args, cfg, N, rank, root, IngestService):
     pf0 = dict(svc.perf)
     tl0 = dict(loop_t)
     ts0 = svc.tailer.stats()
+    h0 = _host_sample()
     t0 = time.perf_counter()
     drain()
     ta = time.perf_counter()
@@ -143,6 +144,7 @@ def _run(args, cfg, N, rank, root, IngestService):
     tc = time.perf_counter()
     svc.inserter.flush_all()  # every row of the timed batches encoded and written
     dt = time.perf_counter() - t0
+    host = _host_delta(h0, _host_sample(), dt)
     tail = {"loop_s": round(ta - t0, 4), "engine_flush_s": round(tb - ta, 4), "drain_outputs_s": round(tc - tb, 4),
             "sink_flush_all_s": round(t0 + dt - tc, 4)}
     m1 = svc.eng.metrics()
@@ -181,9 +183,54 @@ def _run(args, cfg, N, rank, root, IngestService):
         "checkpoint_info": {k: ck1[k] for k in ck1} if ck1 else None,
         "fleet": fleet,
         "fs_type": _fs_type(root),
+        "host": host,  # what else the host did during the timed region (run-to-run spread attribution)
         "batches": pf["batches"],
         "pre_history_batches": PRE,
     }
+
+
+def _host_sample() -> Dict[str, Any]:
+    """Host-side counters around the timed region: this process's CPU seconds, the page cache's
+    dirty / writeback bytes and the kernel's pressure-stall totals (cpu / memory / io, us)."""
+    t = os.times()
+    out: Dict[str, Any] = {"user_s": t.user, "sys_s": t.system}
+    try:
+        with open("/proc/meminfo") as f:
+            for line in f:
+                k, v = line.split(":", 1)
+                if k in ("Dirty", "Writeback", "MemFree"):
+                    out[k] = int(v.split()[0]) * 1024
+    except OSError:
+        pass
+    for r in ("cpu", "memory", "io"):
+        try:
+            with open(f"/proc/pressure/{r}") as f:
+                for line in f:
+                    kind, *fields = line.split()
+                    out[f"psi_{r}_{kind}_us"] = int(dict(x.split("=") for x in fields)["total"])
+        except (OSError, KeyError, ValueError):
+            pass
+    try:
+        with open("/proc/loadavg") as f:
+            out["loadavg1"] = float(f.read().split()[0])
+    except OSError:
+        pass
+    return out
+
+
+def _host_delta(a: Dict[str, Any], b: Dict[str, Any], dt: float) -> Dict[str, Any]:
+    d: Dict[str, Any] = {"cpu_util": round((b["user_s"] + b["sys_s"] - a["user_s"] - a["sys_s"]) / dt, 2),
+                         "sys_share": round((b["sys_s"] - a["sys_s"]) / max(b["user_s"] + b["sys_s"] - a["user_s"] - a["sys_s"], 1e-9), 3)}
+    for k in ("Dirty", "Writeback", "MemFree"):
+        if k in a and k in b:
+            d[k + "_MB_before"] = round(a[k] / 1e6, 1)
+            d[k + "_MB_after"] = round(b[k] / 1e6, 1)
+    for k in a:
+        if k.startswith("psi_") and k in b:
+            d[k[:-3] + "_pct"] = round(100.0 * (b[k] - a[k]) / 1e6 / dt, 2)  # share of the region stalled
+    if "loadavg1" in b:
+        d["loadavg1"] = b["loadavg1"]
+    return d
 
 
 def _fs_type(path: str) -> str:

@@ -27,6 +27,11 @@
 #   servicetrace       the service path with the engine's Chrome trace
 #   servicex:A,B       the service path with extra bench.py arguments A B
 #   benchx:A,B         bench.py 20/5 with extra arguments A B (commas become spaces)
+#   benchold           bench.py 20/5 of the copy under ab/old (a previous tree's package + build,
+#                      shipped by taking ./ab out of .gpurunignore for that call): same-box A/B
+#   meminfo            append the page cache's dirty / writeback counters and the vm.dirty_*
+#                      limits to OUT/meminfo.log (service-path spread attribution)
+#   sync               flush dirty pages to disk (sync) and log how long it took
 #   env:K=V            export K=V for the following tasks (A/B switches)
 #   unenv:K            unset K for the following tasks
 #   py:MODULE          python -m MODULE (diagnostics under tools/)
@@ -60,6 +65,7 @@ for task in "$@"; do
     smoke) run "smoke" 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run "bench_$n" 300 python -u bench.py --steps 20 --warmup 5 ;;
     bench:*) run "bench_$n" 400 python -u bench.py --steps "${task#bench:}" --warmup 5 ;;
+    benchold) run "benchold_$n" 300 bash -c "cd ab/old && python -u bench.py --steps 20 --warmup 5" ;;
     benchx:*) a=${task#benchx:}; run "benchx_$n" 300 python -u bench.py --steps 20 --warmup 5 ${a//,/ } ;;
     bench200) run "bench200_$n" 400 python -u bench.py --steps 200 --warmup 5 ;;
     ranks:*)
@@ -84,6 +90,11 @@ for task in "$@"; do
                 python3 bench.py --steps 20 --warmup 5 ;;
     pmc:*) c=${task#pmc:}; run "pmc_$n" 120 rocprofv3 --kernel-trace --pmc ${c//,/ } --output-format csv -d "$O/pmc_$n" -o run -- \
              python3 bench.py --steps 10 --warmup 3 ;;
+    meminfo) { echo "[$n] $(date +%T.%N)"; grep -E '^(Dirty|Writeback|MemFree|Cached):' /proc/meminfo | tr -s ' ' | tr '\n' ' ';
+               echo; for f in dirty_ratio dirty_background_ratio dirty_bytes dirty_background_bytes dirty_expire_centisecs; do
+               echo -n "$f=$(cat /proc/sys/vm/$f 2>/dev/null) "; done; echo; df -h /tmp | tail -1; echo "loadavg $(cat /proc/loadavg)";
+               for r in cpu memory io; do echo "psi.$r $(tr '\n' ' ' < /proc/pressure/$r 2>/dev/null)"; done; } >> "$O/meminfo.log" ;;
+    sync) t0=$(date +%s%N); timeout -k 10 300 sync; rc=$?; echo "[$n] sync rc=$rc $(( ($(date +%s%N) - t0) / 1000000 )) ms" | tee -a "$O/meminfo.log" ;;
     env:*) export "${task#env:}"; echo "[env] ${task#env:}" ;;
     unenv:*) unset "${task#unenv:}"; echo "[unenv] ${task#unenv:}" ;;
     py:*) run "py_$n" 600 python -u -m "${task#py:}" "$O" ;;
