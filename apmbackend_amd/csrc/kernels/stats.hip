@@ -428,8 +428,9 @@ constexpr int HW = 32;                 // lanes per series
 constexpr int H2_TILE = WS_TILE / 2;   // samples per half in LDS
 
 // Cross-lane moves inside a 32-lane half without the LDS crossbar (ds_bpermute): DPP where the
-// pattern stays inside a 16-lane row (quad permutes for xor 1 / 2, row_ror:8 for xor 8, row shifts
-// and row_bcast:15 for scans), ds_swizzle (no LDS bank access, no address VGPR) for xor 4 / 16.
+// pattern stays inside a 16-lane row (quad permutes for xor 1 / 2, a quad reversal then
+// row_half_mirror for xor 4, row_ror:8 for xor 8, row shifts and row_bcast:15 for scans), and
+// ds_swizzle (no LDS bank access, no address VGPR) only for xor 16, the one move between rows.
 template <int CTRL, int ROWS = 0xF>
 __device__ __forceinline__ int dpp(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWS, 0xF, false); }
 template <int J>
@@ -437,8 +438,8 @@ __device__ __forceinline__ int32_t half_xor(int32_t v) {
   if constexpr (J == 1) return dpp<0xB1>(v);          // quad_perm [1,0,3,2]
   else if constexpr (J == 2) return dpp<0x4E>(v);     // quad_perm [2,3,0,1]
   else if constexpr (J == 8) return dpp<0x128>(v);    // row_ror:8 == xor 8 inside a row
-  else if constexpr (J == 4) return __builtin_amdgcn_ds_swizzle(v, 0x101F);   // BitMode xor 4
-  else return __builtin_amdgcn_ds_swizzle(v, 0x401F);                         // BitMode xor 16
+  else if constexpr (J == 4) return dpp<0x141>(dpp<0x1B>(v));  // quad_perm [3,2,1,0], row_half_mirror: i^3^7
+  else return __builtin_amdgcn_ds_swizzle(v, 0x401F);         // BitMode xor 16
 }
 // inclusive prefix sum over each 32-lane half
 __device__ __forceinline__ int half_scan(int x) {
@@ -488,6 +489,61 @@ __device__ __forceinline__ int32_t bitonic_merge(int32_t v, int hl) {
   if constexpr (K >= 8) v = bitonic_step<K, 4>(v, hl);
   if constexpr (K >= 4) v = bitonic_step<K, 2>(v, hl);
   return bitonic_step<K, 1>(v, hl);
+}
+
+// Register bitonic sort of a 32-lane half's N = 32 E samples, E per lane.  Index bits 0-3 are the
+// lane's position in its 16-lane row (DPP moves), bits 4 .. 3 + log2 E the element (moves inside
+// the lane), and the top bit the row (ds_swizzle xor 16): the top bit is compared in one stage
+// only, so the network makes E swizzles in all and no LDS access (the LDS form below made ~20
+// loads / stores per stage for a 256-sample window).
+template <int E>
+__device__ __forceinline__ void reg_bitonic(int32_t (&v)[E], int hl) {
+  constexpr int N = 32 * E;
+  const int base = (hl >> 4) * (16 * E) + (hl & 15);
+#pragma unroll
+  for (int k = 2; k <= N; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j >= 16 && j < 16 * E) {
+        const int je = j >> 4;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          if (e & je) continue;
+          const bool up = ((base + e * 16) & k) == 0;
+          const int32_t x = v[e], y = v[e | je];
+          v[e] = up ? min(x, y) : max(x, y);
+          v[e | je] = up ? max(x, y) : min(x, y);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int i = base + e * 16;
+          int32_t o;
+          if (j == 1) o = half_xor<1>(v[e]);
+          else if (j == 2) o = half_xor<2>(v[e]);
+          else if (j == 4) o = half_xor<4>(v[e]);
+          else if (j == 8) o = half_xor<8>(v[e]);
+          else o = half_xor<16>(v[e]);
+          const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+          v[e] = keep_min ? min(v[e], o) : max(v[e], o);
+        }
+      }
+    }
+  }
+}
+
+// Sorts the half's n (<= 32 E) samples in t[0, n) in place (t holds at least 32 E entries).
+template <int E>
+__device__ __forceinline__ void half_sort_regs(int32_t* t, int n, int hl) {
+  const int base = (hl >> 4) * (16 * E) + (hl & 15);
+  int32_t v[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) v[e] = base + e * 16 < n ? t[base + e * 16] : 0x7fffffff;
+  reg_bitonic<E>(v, hl);
+#pragma unroll
+  for (int e = 0; e < E; ++e) t[base + e * 16] = v[e];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 }
 
 __device__ inline void half_bitonic(int32_t* a, int n, int hl) {
@@ -608,13 +664,23 @@ __global__ __launch_bounds__(WS_WAVES * APM_WAVE) void k_window_stats_h2(WindowA
     }
     return;
   }
-  // 32 < n <= 512: this half sorts its tile in LDS
-  int np2 = HW;
-  while (np2 < n) np2 <<= 1;
-  for (int i = n + hl; i < np2; i += HW) t[i] = 0x7fffffff;
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  half_bitonic(t, np2, hl);
+  // 32 < n <= 512: this half sorts its tile in registers (APM_K8_LDS=2: the LDS network, A/B)
+  if (a.lds_sort == 2) {
+    int np2 = HW;
+    while (np2 < n) np2 <<= 1;
+    for (int i = n + hl; i < np2; i += HW) t[i] = 0x7fffffff;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    half_bitonic(t, np2, hl);
+  } else if (n <= 2 * HW) {
+    half_sort_regs<2>(t, n, hl);
+  } else if (n <= 4 * HW) {
+    half_sort_regs<4>(t, n, hl);
+  } else if (n <= 8 * HW) {
+    half_sort_regs<8>(t, n, hl);
+  } else {
+    half_sort_regs<16>(t, n, hl);
+  }
   if (hl == 0) finish_series(a, s, n, sum, t);
 }
 
@@ -1066,7 +1132,7 @@ void apm_nan_mark(const TxRec* d_tx, uint32_t n, StatsState* st, hipStream_t str
 // big_n / nan_n must be zero on entry (the engine clears them with the rollover's other counters)
 void apm_window_stats(WindowArgs* a, hipStream_t stream) {
   static const bool h2 = [] { const char* e = std::getenv("APM_K8_H2"); return !(e && e[0] == '0'); }();
-  if (h2 && a->n_win <= HW && !a->lds_sort) {
+  if (h2 && a->n_win <= HW && a->lds_sort != 1) {
     const int blocks2 = (a->n_series + 2 * WS_WAVES - 1) / (2 * WS_WAVES);
     if (blocks2 == 0) return;
     hipLaunchKernelGGL(k_window_stats_h2, dim3(blocks2), dim3(WS_WAVES * APM_WAVE), 0, stream, *a);

@@ -2332,7 +2332,9 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   }
   wa.tpm_div = (double)cfg_.window * cfg_.interval_len / 60.0;
   {
-    static const int lds = [] { const char* e = std::getenv("APM_K8_LDS"); return e && e[0] == '1' ? 1 : 0; }();
+    // APM_K8_LDS=1: the LDS bitonic for every window; =2: only the two-series kernel's windows
+    // of 33-512 samples (A/B of its register network)
+    static const int lds = [] { const char* e = std::getenv("APM_K8_LDS"); return e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : 0; }();
     wa.lds_sort = lds;
   }
   wa.out = d_win_;
