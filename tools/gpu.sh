@@ -32,7 +32,8 @@
 #   meminfo            append the page cache's dirty / writeback counters and the vm.dirty_*
 #                      limits to OUT/meminfo.log (service-path spread attribution)
 #   sync               flush dirty pages to disk (sync) and log how long it took
-#   env:K=V            export K=V for the following tasks (A/B switches)
+#   env:K=V            export K=V for the following tasks (A/B switches; BENCH_EXTRA=--a=b adds
+#                      bench.py arguments to the profser / pmc runs)
 #   unenv:K            unset K for the following tasks
 #   py:MODULE          python -m MODULE (diagnostics under tools/)
 set -u
@@ -85,11 +86,11 @@ for task in "$@"; do
             python3 bench.py --steps 20 --warmup 5 ;;
     trace) run "trace_$n" 300 python -u bench.py --steps 60 --warmup 5 --trace "$O/trace_$n.json" ;;
     profser) AMD_SERIALIZE_KERNEL=3 run "profser_$n" 600 rocprofv3 --kernel-trace --stats --output-format csv \
-               -d "$O/profser_$n" -o run -- python3 bench.py --steps 10 --warmup 3 ;;
+               -d "$O/profser_$n" -o run -- python3 bench.py --steps 10 --warmup 3 ${BENCH_EXTRA:-} ;;
     timeline) run "timeline_$n" 400 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$O/tl_$n" -o run -- \
                 python3 bench.py --steps 20 --warmup 5 ;;
     pmc:*) c=${task#pmc:}; run "pmc_$n" 120 rocprofv3 --kernel-trace --pmc ${c//,/ } --output-format csv -d "$O/pmc_$n" -o run -- \
-             python3 bench.py --steps 10 --warmup 3 ;;
+             python3 bench.py --steps 10 --warmup 3 ${BENCH_EXTRA:-} ;;
     meminfo) { echo "[$n] $(date +%T.%N)"; grep -E '^(Dirty|Writeback|MemFree|Cached):' /proc/meminfo | tr -s ' ' | tr '\n' ' ';
                echo; for f in dirty_ratio dirty_background_ratio dirty_bytes dirty_background_bytes dirty_expire_centisecs; do
                echo -n "$f=$(cat /proc/sys/vm/$f 2>/dev/null) "; done; echo; df -h /tmp | tail -1; echo "loadavg $(cat /proc/loadavg)";
