@@ -1060,6 +1060,7 @@ int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& e
     def.cap = ck_defer_cap_;
     BinWriter mw{BinWriter::Memory{}, ck_blob_hint_};
     ck_defer() = &def;
+    const double ts0 = now_ms();
     try {
       write_small_sections(mw);
     } catch (...) {
@@ -1072,13 +1073,17 @@ int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& e
     // the D2D copies complete before the engine resumes (~TB/s: under a millisecond for the
     // snapshot's ~100 MB): a source array another stream writes next (the parse carry on the parse
     // stream, the z-score state on the rollover lane's) cannot change under a queued copy
+    const double ts1 = now_ms();
     for (hipStream_t ds : def.streams) HIP_OK(hipStreamSynchronize(ds));
+    trace_event("ck.small_sections", ts0, ts1, 0);
+    trace_event("ck.defer_sync", ts1, now_ms(), 0);
     for (const auto& h : def.holes) job->holes.push_back({h.blob_off, h.stage_off, h.len});
     job->patches = std::move(def.patches);
     job->blob = mw.take_memory();
     ck_blob_hint_ = job->blob.size() + job->blob.size() / 8 + (1u << 20);
   }
   // dirty ring rows -> HBM staging (D2D, stream-ordered after the quiesce point)
+  const double tring = now_ms();
   const int32_t S = cfg_.max_series, n = n_series_;
   const size_t rb = (size_t)cfg_.ring_bytes;
   const int64_t r1 = rollover_idx_;
@@ -1226,6 +1231,7 @@ int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& e
   }
   if (!ck_ev_) HIP_OK(hipEventCreateWithFlags(&ck_ev_, hipEventDisableTiming));
   HIP_OK(hipEventRecord(ck_ev_, stream_));
+  trace_event("ck.ring_stage", tring, now_ms(), 0);
   ck_ridx_ = r1;
   ck_all_dirty_ = false;
   ck_prefix_ = prefix;

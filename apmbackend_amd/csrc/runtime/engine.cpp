@@ -456,6 +456,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   HIP_OK(hipHostGetDevicePointer((void**)&hd_alert_z_, h_alert_z_, 0));
   HIP_OK(hipHostGetDevicePointer((void**)&hd_n_alerts_, h_n_alerts_, 0));
   HIP_OK(hipEventCreateWithFlags(&ev_alerts_, hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&ev_release_, hipEventDisableTiming));
   // tx + release
   d_tx_ = (TxRec*)dmalloc((size_t)cfg_.max_tx_per_batch * sizeof(TxRec));
   HIP_OK(hipHostMalloc((void**)&h_tx_, (size_t)cfg_.max_tx_per_batch * sizeof(TxRec), hipHostMallocDefault));
@@ -576,7 +577,7 @@ Engine::~Engine() {
   hipHostFree(h_alert_win_);
   hipHostFree(h_alert_z_);
   if (h_series_service_) hipHostFree(h_series_service_);
-  hipHostFree(h_n_alerts_); hipEventDestroy(ev_alerts_); hipHostFree(h_tx_); hipHostFree(h_gid_);
+  hipHostFree(h_n_alerts_); hipEventDestroy(ev_alerts_); hipEventDestroy(ev_release_); hipHostFree(h_tx_); hipHostFree(h_gid_);
   for (int k = 0; k < 2; ++k) {
     hipHostFree(h_release_gid_[k]);
     {  // the sink's references to the staging buffers (its writers drain them; bounded wait)
@@ -2234,9 +2235,10 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
   const int64_t edge_ts = (L - cfg_.buffer - 1) * 10000;
   last_edge_ts_ = edge_ts;
   const double tr0 = now_ms();
-  // ---- K9 release: merge the sorted pool with the sorted tail, hand out endTs <= edge
+  // ---- K9 release: merge the sorted pool with the sorted tail, hand out endTs <= edge (the
+  // device form is queued after K8-K11 and the alert gather, below: the alert candidates do not
+  // wait for it on the stream)
   if (dev()) {
-    release_device(edge_ts);
   } else {
     int64_t released = 0;
     for (auto it = pool_bucket_count_.begin(); it != pool_bucket_count_.end();) {
@@ -2385,6 +2387,13 @@ void Engine::do_rollover(int64_t L, double batch_t0) {
                      hd_alerts_, hd_alert_win_, hd_alert_z_, hd_n_alerts_, stream_);
     HIP_OK(hipEventRecord(ev_alerts_, stream_));
   }
+  if (dev()) {
+    const double tq = now_ms();
+    release_device(edge_ts);
+    HIP_OK(hipEventRecord(ev_release_, stream_));
+    metrics_.t_release_ms += now_ms() - tq;
+    trace_event("release (device)", tq, now_ms(), 1);
+  }
   const double tr2 = now_ms();
   trace_event("ro.K8-K11 launch", tsp, tr2, 1);
   if (want(OUT_ST) || want(OUT_FS)) format_rollover_text(edge_ts);
@@ -2435,14 +2444,18 @@ void Engine::finish_rollover_body() {
   const double t0 = now_ms();
   HIP_OK(hipEventSynchronize(ev_alerts_));
   const double t1 = now_ms();
-  if (dev()) release_device_finish();
-  const double t2 = now_ms();
   metrics_.t_rollover_ms += t1 - t0;
   trace_event("rollover wait", t0, t1, 1);
-  trace_event("release finish", t1, t2, 1);
   metrics_.rollover_latency_ms.push_back(t1 - roll_batch_t0_);
+  // the alerts first (they need only the candidates), then the release queued behind them
   flush_alerts(roll_edge_ts_);
-  trace_event("alerts", t2, now_ms(), 1);
+  const double t2 = now_ms();
+  trace_event("alerts", t1, t2, 1);
+  if (dev()) {
+    HIP_OK(hipEventSynchronize(ev_release_));
+    release_device_finish();
+  }
+  trace_event("release finish", t2, now_ms(), 1);
   if (want(OUT_SX)) format_server_rollup(roll_edge_ts_);
   metrics_.t_format_ms += now_ms() - t1;
 }

@@ -1055,6 +1055,7 @@ class Engine {
   ZOut* hd_alert_z_ = nullptr;
   int32_t* hd_n_alerts_ = nullptr;
   hipEvent_t ev_alerts_ = nullptr;  // the rollover's candidates are in host memory
+  hipEvent_t ev_release_ = nullptr; // the rollover's device release (K9 part 1) exported its counts
   std::unordered_map<std::string, double> last_alert_;  // cooldown key -> alertTimestamp
   // K11 cooldown pre-filter (AlertArgs::cool_t): per series, the time of its cooldown key's latest
   // alert; cool_series_ maps a key (hash as in NodeCand::key) to this rank's series (series_mu_)
