@@ -1162,7 +1162,12 @@ int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& e
   ck_last_need_ = need;
   if (need > ck_stage_bytes_) {
     free_ck_stage();
-    const size_t want = job->streamed ? need : std::min(cap, need + need / 8);  // (room for the series table)
+    // Sized once for the rings at maxSeries (capped): a service's first checkpoint comes while few
+    // series exist, and growing the staging at a later base put a 2 GiB hipFree + hipMalloc into
+    // that base's ingest stall (2.1 ms of 11-15 ms, profiles/r6_l servicetrace ck.ring_stage).
+    size_t full = 0;
+    for (int l = 0; l < cfg_.n_lags; ++l) full += (size_t)NSTAT * cfg_.lags[l] * (size_t)S * rb;
+    const size_t want = job->streamed ? need : std::min(cap, std::max(need + need / 8, full));  // (room for the series table)
     if (hipMalloc(&d_ck_stage_, want) != hipSuccess) {
       (void)hipGetLastError();
       d_ck_stage_ = nullptr;

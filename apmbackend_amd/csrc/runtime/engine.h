@@ -83,7 +83,7 @@ struct EngineConfig {
   int exact_mean = 0;
   int sigma_stddev = 0;
   int resync_k = 360;
-  bool resync_mfma = true;  // rolling-mode window re-sum on the matrix cores
+  bool resync_mfma = false;  // rolling-mode window re-sum on the matrix cores (gpu.resyncOnMatrixCores; the VALU form is faster: profiles/r6_l)
   int n_lags = 2;
   int32_t lags[MAX_LAGS] = {360, 8640, 0, 0};
   double thr[MAX_LAGS] = {20.0, 15.0, 0, 0};

@@ -71,7 +71,7 @@ def engine_config(cfg: Dict[str, Any], device: int = 0, keep_text: bool = False,
         "exact_mean": 1 if g.get("zscoreMeanMode", "rolling") == "exact" else 0,
         "sigma_stddev": 1 if g.get("zscoreSigma", "sqrt_mean") == "stddev" else 0,
         "resync_k": int(g.get("exactRecomputeEveryIntervals", 360)),
-        "resync_mfma": bool(g.get("resyncOnMatrixCores", True)),
+        "resync_mfma": bool(g.get("resyncOnMatrixCores", False)),
         "emulate_aliasing": 1 if g.get("emulateOverrideAliasing", False) else 0,
         "lags": lags,
         "lag_suppressed": [1 if l[0] in suppressed_lags else 0 for l in lags],

@@ -100,8 +100,9 @@ def main():
                          "window is full by then, so the history is drawn around the steady window stats "
                          "(drawn around a 2-bucket window it sat ~20 %% below the real p75/p95 and turned "
                          "the run into an alert storm after ~50 batches)")
-    ap.add_argument("--resync", default="mfma", choices=["mfma", "valu"],
-                    help="K10 rolling-sum resync on the matrix cores (v_mfma_f64_16x16x4) or on the VALU (A/B)")
+    ap.add_argument("--resync", default="valu", choices=["mfma", "valu"],
+                    help="K10 rolling-sum resync on the VALU (default: 11.1 vs 19.6 us per call, profiles/r6_l) or on "
+                         "the matrix cores (v_mfma_f64_16x16x4, a GEMV: A/B)")
     ap.add_argument("--audit-fraction", type=float, default=0.02,
                     help="share of requests logged with an audit trail (K5: the per-file state machine "
                          "runs in the host pre-pass)")
