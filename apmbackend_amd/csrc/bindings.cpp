@@ -150,6 +150,7 @@ py::dict metrics_dict(const EngineMetrics& m) {
   d["tx"] = m.tx; d["tx_db"] = m.tx_db; d["tx_dropped"] = m.tx_dropped; d["rollovers"] = m.rollovers;
   d["alerts"] = m.alerts; d["alert_candidates"] = m.alert_candidates;
   d["alert_candidates_dropped"] = m.alert_candidates_dropped; d["released"] = m.released;
+  d["staged_batches"] = m.staged_batches;
   d["t_join_shards_ms"] = m.t_join_shards_ms; d["t_merge_ms"] = m.t_merge_ms;
   d["t_shard_busy_ms"] = m.t_shard_busy_ms; d["t_shard_max_ms"] = m.t_shard_max_ms;
   d["t_out_ms"] = m.t_out_ms;
@@ -369,6 +370,12 @@ PYBIND11_MODULE(_apm_native, m) {
            py::arg("ptr"), py::arg("n"), py::arg("chunks"), py::arg("now") = -1.0, py::arg("next_ptr") = 0,
            py::arg("next_n") = 0,
            py::arg("next_chunks") = std::vector<std::tuple<int32_t, uint64_t, uint64_t>>())
+      .def("stage_batch_ptr",
+           [](Engine& e, uintptr_t ptr, uint64_t n) {
+             py::gil_scoped_release rel;
+             e.stage_batch((const uint8_t*)ptr, n);
+           },
+           py::arg("ptr"), py::arg("n"))
       .def("process_tx_lines", [](Engine& e, py::bytes b, double now) {
              std::string v = b;
              py::gil_scoped_release rel;

@@ -68,6 +68,13 @@ class DeviceJoin {
 
   // device buffers the parse kernels of slot k write into
   uint8_t* d_bytes(int k) { return sl_[k].d_bytes; }
+  // A third batch buffer for the two-ahead H2D (Engine::stage_batch), allocated on first use;
+  // swap_stage(k) hands it to slot k (whose previous buffer becomes the staging buffer).
+  uint8_t* d_stage() {
+    if (!d_stage_bytes_) d_stage_bytes_ = (uint8_t*)dmalloc(cfg_.max_batch_bytes + 256);
+    return d_stage_bytes_;
+  }
+  void swap_stage(int k) { std::swap(sl_[k].d_bytes, d_stage_bytes_); }
   Event* d_events(int k) { return sl_[k].d_events; }
   // after the parse kernels (parse stream): select host events, queue their D2H (speculative)
   void select_host(int k, const uint32_t* d_n_ev, uint32_t max_ev, hipStream_t ps);
@@ -223,6 +230,7 @@ class DeviceJoin {
     return f;
   }
   size_t device_bytes_ = 0;
+  uint8_t* d_stage_bytes_ = nullptr;  // two-ahead H2D target (d_stage / swap_stage)
   std::vector<void*> allocs_;
 
   // host pre-pass output of the current batch

@@ -522,6 +522,11 @@ Engine::~Engine() {
     roll_lane_.reset();
   }
   ahead_lane_.reset();  // drains a pending next-batch pre-pass before the join state goes
+  if (in_stage_stream_) {  // a staged input copy writes a buffer the device join frees
+    hipStreamSynchronize(in_stage_stream_);
+    hipEventDestroy(in_stage_ev_);
+    hipStreamDestroy(in_stage_stream_);
+  }
   fb_lane_.reset();     // and a pending fb emission before its buffers
   if (nm_ev_) { hipEventSynchronize(nm_ev_); hipEventDestroy(nm_ev_); }
   if (h_nm_send_) hipHostFree(h_nm_send_);
@@ -900,9 +905,19 @@ void Engine::launch_parse(ParseSlot& ps, const uint8_t* host_bytes, uint64_t n_b
   // finished -- its events copied to its own host slot -- before this launch).  Device join: the
   // slot's own device buffers (the other slot's batch may still be joined on the join stream).
   const int k = (int)(&ps - pslot_);
+  // the input already copied by stage_batch (two batches ahead): take its buffer
+  bool staged = false;
+  if (dev() && canonical && in_stage_src_ == host_bytes && in_stage_n_ == n_bytes && in_stage_ev_) {
+    HIP_OK(hipStreamWaitEvent(parse_stream_, in_stage_ev_, 0));
+    dj_->swap_stage(k);
+    staged = true;
+    ++metrics_.staged_batches;
+  }
+  in_stage_src_ = nullptr;
+  in_stage_n_ = 0;
   uint8_t* dbytes = dev() ? dj_->d_bytes(k) : d_bytes_;
   Event* devents = dev() ? dj_->d_events(k) : (ps.d_events_host ? ps.d_events_host : d_events_);
-  HIP_OK(hipMemcpyAsync(dbytes, ps.hb, off, hipMemcpyHostToDevice, parse_stream_));
+  if (!staged) HIP_OK(hipMemcpyAsync(dbytes, ps.hb, off, hipMemcpyHostToDevice, parse_stream_));
   // (apm_parse_batch zeroes the 64 bytes after the batch inside its first kernel)
   h2d(d_chunk_begin_[k], ps.h_chunk_begin, (n_chunks + 1) * 4, parse_stream_);
   h2d(d_chunk_kind_[k], ps.h_chunk_kind, n_chunks + 1, parse_stream_);
@@ -929,6 +944,23 @@ void Engine::launch_parse(ParseSlot& ps, const uint8_t* host_bytes, uint64_t n_b
   }
   ps.pending = true;
   metrics_.t_parse_ms += now_ms() - t0;
+}
+
+void Engine::stage_batch(const uint8_t* host_bytes, uint64_t n_bytes) {
+  if (!dev() || !host_bytes || n_bytes == 0 || n_bytes > cfg_.max_batch_bytes) return;
+  const double t0 = now_ms();
+  if (!in_stage_stream_) {
+    HIP_OK(hipStreamCreateWithFlags(&in_stage_stream_, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&in_stage_ev_, hipEventDisableTiming));
+  }
+  // The staging buffer is free: it is either fresh, the buffer an unconsumed earlier stage wrote
+  // (ordered behind that copy on this stream), or -- after a swap -- the parse slot buffer of the
+  // batch two back, whose join finished before the current process_batch returned.
+  HIP_OK(hipMemcpyAsync(dj_->d_stage(), host_bytes, n_bytes, hipMemcpyHostToDevice, in_stage_stream_));
+  HIP_OK(hipEventRecord(in_stage_ev_, in_stage_stream_));
+  in_stage_src_ = host_bytes;
+  in_stage_n_ = n_bytes;
+  trace_event("stage H2D (launch)", t0, now_ms(), 0);
 }
 
 // Wait for a launched parse and copy its events into the slot's pinned host buffer.

@@ -205,6 +205,7 @@ struct CheckpointInfo {
 struct EngineMetrics {
   uint64_t batches = 0, bytes = 0, lines = 0, events = 0, tx = 0, tx_db = 0, tx_dropped = 0;
   uint64_t rollovers = 0, alerts = 0, alert_candidates = 0, series = 0, released = 0;
+  uint64_t staged_batches = 0;      // parses whose input was already on the device (stage_batch)
   uint64_t alert_candidates_dropped = 0;  // beyond maxAlertCandidates in one rollover (reported)
   uint64_t formatted_bytes = 0, format_fallbacks = 0, lockstep_rollovers = 0;
   uint64_t series_overflow_tx = 0;  // tx whose series could not be created (gpu.maxSeries full)
@@ -295,6 +296,12 @@ class Engine {
                      double now_override = -1.0, const uint8_t* next_bytes = nullptr, uint64_t next_n = 0,
                      const std::vector<Chunk>* next_chunks = nullptr);
   bool prefetch_pending() const { return prefetched_; }
+  // Two-ahead input copy (device join only): starts the H2D of the batch after the next one into a
+  // third device buffer on its own stream, so that batch's parse kernels -- launched by the next
+  // process_batch -- find their input on the device instead of behind a 28 MB host-link copy.
+  // The bytes must be passed unchanged (same pointer and size, canonical chunks) to that later
+  // launch and stay valid until it; anything else just ignores the staged copy.
+  void stage_batch(const uint8_t* host_bytes, uint64_t n_bytes);
   // tx CSV lines (a reference parser stage's `transactions` queue) straight into the stats stage
   void process_tx_lines(const std::string& blob, double now = -1.0);
 
@@ -843,6 +850,11 @@ class Engine {
   uint32_t spec_events_ = 0;                    // speculative D2H size for the next prefetched parse
   int cur_slot_ = 0, last_slot_ = 0;
   bool prefetched_ = false;
+  // stage_batch: the batch whose H2D is queued on in_stage_stream_ (identity check at its launch)
+  const uint8_t* in_stage_src_ = nullptr;
+  uint64_t in_stage_n_ = 0;
+  hipStream_t in_stage_stream_ = nullptr;
+  hipEvent_t in_stage_ev_ = nullptr;
   void launch_parse(ParseSlot& ps, const uint8_t* host_bytes, uint64_t n_bytes, const std::vector<Chunk>& chunks,
                     bool speculative = false);
   void process_batch_dev_tail(ParseSlot& ps, double t0, double now_override, const uint8_t* next_bytes,

@@ -89,6 +89,8 @@ def main():
     ap.add_argument("--spool-dir", default=os.environ.get("APM_SPOOL_DIR", "/var/tmp" if os.path.isdir("/var/tmp") else None),
                     help="--db-sink spool: where the COPY spool files go (a disk, not tmpfs)")
     ap.add_argument("--no-prefetch", action="store_true", help="disable the next-batch parse overlap")
+    ap.add_argument("--no-stage-ahead", action="store_true",
+                    help="disable the two-ahead input H2D (Engine::stage_batch; A/B)")
     ap.add_argument("--no-fleet", action="store_true",
                     help="skip the fleet baseline exchange / lock-step clocks (always on by default, also at N=1)")
     ap.add_argument("--anomaly-services", type=int, default=16,
@@ -285,6 +287,7 @@ def main():
 
     last = PRE + args.warmup + args.steps - 1
     first_timed = PRE + args.warmup
+    stage_ahead = not args.no_stage_ahead and not args.no_prefetch and hasattr(eng.eng, "stage_batch_ptr")
 
     jmx_lines = []
     if args.jmx:  # one JMX record per JVM per batch (pull_jvm_stats.js at the bench's time scale)
@@ -313,6 +316,11 @@ def main():
             eng.eng.process_batch_ptr(ptr, n, chunks, -1.0, nptr, nn, nchunks)
         else:
             eng.eng.process_batch_ptr(ptr, n, chunks, -1.0)
+        # the input copy of the batch after next starts now (its parse is launched by the next
+        # step), never across a timing boundary: every timed batch's H2D is inside the region
+        j = i + 2
+        if stage_ahead and j <= last and (i >= first_timed or j < first_timed):
+            eng.eng.stage_batch_ptr(batches[j][0], batches[j][1])
 
     # ---- warmup (first batches create the series; then the z-score rings get a pre-history)
     for i in range(PRE):
@@ -460,6 +468,7 @@ def main():
             "alerts": int(m1["alerts"] - m0["alerts"]),
             "alert_candidates": int(m1["alert_candidates"] - m0["alert_candidates"]),
             "alert_candidates_dropped": int(m1.get("alert_candidates_dropped", 0)),
+            "staged_input_batches_timed": int(m1.get("staged_batches", 0) - m0.get("staged_batches", 0)),
             "device_GB": round(eng.eng.device_bytes() / 1e9, 1),
         }
         if inserter is not None:
