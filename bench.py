@@ -89,8 +89,9 @@ def main():
     ap.add_argument("--spool-dir", default=os.environ.get("APM_SPOOL_DIR", "/var/tmp" if os.path.isdir("/var/tmp") else None),
                     help="--db-sink spool: where the COPY spool files go (a disk, not tmpfs)")
     ap.add_argument("--no-prefetch", action="store_true", help="disable the next-batch parse overlap")
-    ap.add_argument("--no-stage-ahead", action="store_true",
-                    help="disable the two-ahead input H2D (Engine::stage_batch; A/B)")
+    ap.add_argument("--stage-ahead", action="store_true",
+                    help="two-ahead input H2D (Engine::stage_batch; A/B, off: measured slower -- the 28 MB "
+                         "copy delays the rollover's small copies behind it, profiles/r6_n)")
     ap.add_argument("--no-fleet", action="store_true",
                     help="skip the fleet baseline exchange / lock-step clocks (always on by default, also at N=1)")
     ap.add_argument("--anomaly-services", type=int, default=16,
@@ -287,7 +288,7 @@ def main():
 
     last = PRE + args.warmup + args.steps - 1
     first_timed = PRE + args.warmup
-    stage_ahead = not args.no_stage_ahead and not args.no_prefetch and hasattr(eng.eng, "stage_batch_ptr")
+    stage_ahead = args.stage_ahead and not args.no_prefetch and hasattr(eng.eng, "stage_batch_ptr")
 
     jmx_lines = []
     if args.jmx:  # one JMX record per JVM per batch (pull_jvm_stats.js at the bench's time scale)
