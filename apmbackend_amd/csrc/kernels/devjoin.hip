@@ -2194,6 +2194,13 @@ __global__ __launch_bounds__(RB_TB) void k_rebuild_inplace(KeyState* __restrict_
   if ((threadIdx.x & (APM_WAVE - 1)) == 0 && n_live) atomicAdd(live, (unsigned long long)n_live);
 }
 
+__global__ __launch_bounds__(TB) void k_rebase_gids(const int64_t* __restrict__ gid, int64_t n,
+                                                    const uint32_t* __restrict__ offs, uint64_t base,
+                                                    int64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (int64_t)(((base + offs[i]) << 20) | ((uint64_t)gid[i] & 0xfffffu));
+}
+
 __global__ void k_gather_len(const int64_t* __restrict__ gid, int64_t n_upper, const int64_t* __restrict__ d_n,
                              uint32_t* __restrict__ lens) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2949,6 +2956,12 @@ void apm_dj_gather_copy(const int64_t* gid, int64_t n, const char* ring, uint64_
   (void)total_bytes;  // (the blocks derive their byte ranges from offs)
   hipLaunchKernelGGL(k_gather_lines, dim3((unsigned)((n + GL_LINES - 1) / GL_LINES)), dim3(GL_TB), 0, s, gid, n, ring,
                      ring_cap, offs, out);
+}
+
+void apm_dj_rebase_gids(const int64_t* gid, int64_t n, const uint32_t* offs, uint64_t base, int64_t* out,
+                        hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_rebase_gids, dim3((unsigned)((n + TB - 1) / TB)), dim3(TB), 0, s, gid, n, offs, base, out);
 }
 
 void apm_dj_min_pos(const int64_t* gid, int64_t n, unsigned long long* out, hipStream_t s) {

@@ -270,6 +270,10 @@ void apm_dj_txcopy_write(const int64_t* gid, int64_t n, const char* ring, uint64
 // `out` must hold offs[n] = total_bytes bytes (16-byte aligned)
 void apm_dj_gather_copy(const int64_t* gid, int64_t n, const char* ring, uint64_t ring_cap, const uint32_t* offs,
                         char* out, uint64_t total_bytes, hipStream_t s);
+// checkpoint: gid i -> ((base + offs[i]) << 20) | its length, the line's offset in the saved text
+// blob (offs = apm_dj_gather_plan's scan of length + 1)
+void apm_dj_rebase_gids(const int64_t* gid, int64_t n, const uint32_t* offs, uint64_t base, int64_t* out,
+                        hipStream_t s);
 // min ring position among gids (for ring reuse); writes UINT64_MAX when n == 0
 void apm_dj_min_pos(const int64_t* gid, int64_t n, unsigned long long* out, hipStream_t s);
 // relocate gids below `below` (virtual ring pos): copy their lines to dst_base.. and rewrite

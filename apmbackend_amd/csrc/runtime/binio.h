@@ -78,6 +78,12 @@ class BinWriter {
   // state on the ingest thread.)
   struct Memory {};
   explicit BinWriter(Memory, size_t reserve = 0) : mem_(true) { buf_.reserve(reserve); }
+  // ... into a previous snapshot's buffer: its pages are already mapped, so the ingest thread's
+  // serialisation does not page-fault its way through a fresh ~100 MB allocation
+  BinWriter(Memory, MemBlob&& reuse, size_t reserve) : mem_(true), buf_(std::move(reuse)) {
+    buf_.n = 0;
+    buf_.reserve(reserve);
+  }
   MemBlob take_memory() { return std::move(buf_); }
   ~BinWriter() {
     if (f_) {

@@ -586,26 +586,40 @@ void Engine::write_small_sections(BinWriter& w) {
   d2h_vec(w, d_tail_end_, (size_t)tail_n_, stream_, bounce);
   if (dev()) {
     // pending lines live in the HBM text ring: saved as one blob (pool lines, then tail lines)
-    // with each gid rebased to its offset in the blob
-    std::vector<int64_t> gids((size_t)(pool_n_ + tail_n_));
-    d2h_bounced(gids.data(), d_pool_gid_[pool_cur_] + pool_off_, (size_t)pool_n_ * 8, stream_, (char*)bounce, kBounce);
-    d2h_bounced(gids.data() + pool_n_, d_tail_gid_, (size_t)tail_n_ * 8, stream_, (char*)bounce, kBounce);
-    uint64_t off = 0;
-    for (auto& g : gids) {
-      const uint64_t len = (uint64_t)g & 0xfffffu;
-      g = (int64_t)((off << 20) | len);
-      off += len + 1;
-    }
-    w.vec(gids);
-    // the text (pool lines, then tail lines): gathered on the device, written straight from the
-    // pinned bounce into the snapshot (was: a hipMalloc + pageable copy + two string copies)
+    // with each gid rebased to its offset in the blob -- rebased on the device from the text
+    // gather's own offsets and read with the other deferred sections (was: a synchronous D2H of
+    // every gid and a host pass over them inside the checkpoint's ingest stall)
     const int64_t* srcs[2] = {d_pool_gid_[pool_cur_] + pool_off_, d_tail_gid_};
     const int64_t cnt[2] = {pool_n_, tail_n_};
+    const size_t n_g = (size_t)(pool_n_ + tail_n_);
+    if (n_g > ck_gids_cap_) {
+      dfree(d_ck_gids_);
+      ck_gids_cap_ = n_g + n_g / 4 + 1024;
+      d_ck_gids_ = (int64_t*)dmalloc_try(ck_gids_cap_ * 8);
+      if (!d_ck_gids_) ck_gids_cap_ = 0;
+    }
+    std::vector<int64_t> gids;
+    if (!d_ck_gids_) {  // no HBM for it: the host pass
+      gids.resize(n_g);
+      d2h_bounced(gids.data(), srcs[0], (size_t)pool_n_ * 8, stream_, (char*)bounce, kBounce);
+      d2h_bounced(gids.data() + pool_n_, srcs[1], (size_t)tail_n_ * 8, stream_, (char*)bounce, kBounce);
+      uint64_t off = 0;
+      for (auto& g : gids) {
+        const uint64_t len = (uint64_t)g & 0xfffffu;
+        g = (int64_t)((off << 20) | len);
+        off += len + 1;
+      }
+    }
+    // the text (pool lines, then tail lines): gathered on the device, written straight from the
+    // pinned bounce into the snapshot (was: a hipMalloc + pageable copy + two string copies)
     uint32_t tot[2] = {0, 0};
     for (int k = 0; k < 2; ++k) {
       if (cnt[k] <= 0) continue;
       if (apm_dj_gather_plan(srcs[k], cnt[k], nullptr, d_rel_lens_, d_rel_offs_, d_release_tmp_, release_tmp_bytes_, stream_) != 0)
         throw std::runtime_error("checkpoint: ring text scratch too small");
+      if (d_ck_gids_)
+        apm_dj_rebase_gids(srcs[k], cnt[k], d_rel_offs_, k ? (uint64_t)tot[0] : 0, d_ck_gids_ + (k ? pool_n_ : 0),
+                           stream_);
       HIP_OK(hipMemcpyAsync(&tot[k], d_rel_offs_ + cnt[k], 4, hipMemcpyDeviceToHost, stream_));
       HIP_OK(hipStreamSynchronize(stream_));
       if (!tot[k]) continue;
@@ -619,6 +633,8 @@ void Engine::write_small_sections(BinWriter& w) {
       if (d_ck_text_[k])
         apm_dj_gather_copy(srcs[k], cnt[k], dj_->ring(), dj_->ring_cap(), d_rel_offs_, d_ck_text_[k], tot[k], stream_);
     }
+    if (d_ck_gids_) d2h_vec(w, d_ck_gids_, n_g, stream_, bounce);  // (deferred while a snapshot is taken)
+    else w.vec(gids);
     w.pod<uint64_t>((uint64_t)tot[0] + tot[1]);
     for (int k = 0; k < 2; ++k) {
       if (!tot[k]) continue;
@@ -1058,7 +1074,12 @@ int64_t Engine::checkpoint_async(const std::string& prefix, const std::string& e
     }
     def.stage = d_ck_defer_;
     def.cap = ck_defer_cap_;
-    BinWriter mw{BinWriter::Memory{}, ck_blob_hint_};
+    MemBlob spare;
+    {
+      std::lock_guard<std::mutex> lk(ck_mu_);
+      spare = std::move(ck_blob_spare_);
+    }
+    BinWriter mw{BinWriter::Memory{}, std::move(spare), ck_blob_hint_};
     ck_defer() = &def;
     const double ts0 = now_ms();
     try {
@@ -1428,6 +1449,7 @@ void Engine::checkpoint_writer() {
         ck_last_bytes_ = bytes;
         ++ck_done_;
       }
+      ck_blob_spare_ = std::move(job->blob);  // the next snapshot serialises into it
       ck_job_.reset();
       ck_busy_ = false;
     }

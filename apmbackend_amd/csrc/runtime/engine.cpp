@@ -1914,6 +1914,9 @@ std::pair<size_t, size_t> Engine::trim_device_memory() {
     d_ck_text_[k] = nullptr;
     ck_text_cap_[k] = 0;
   }
+  dfree(d_ck_gids_);
+  d_ck_gids_ = nullptr;
+  ck_gids_cap_ = 0;
   // the snapshot staging is kept at what the last snapshot needed (re-allocating it at the next
   // checkpoint would stall that checkpoint and put HBM back over the threshold): freed only when
   // it is more than twice that

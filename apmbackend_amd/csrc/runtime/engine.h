@@ -1000,7 +1000,10 @@ class Engine {
   size_t ck_last_need_ = 0;  // ring staging the last snapshot needed (trim keeps up to 2x)
   void* h_ck_bounce_ = nullptr;
   size_t ck_blob_hint_ = 0;         // size of the last small-section blob (reserve)
+  MemBlob ck_blob_spare_;           // the last written snapshot's blob buffer, reused (ck_mu_)
   char* d_ck_text_[2] = {nullptr, nullptr};  // pending-line text gathered for a checkpoint
+  int64_t* d_ck_gids_ = nullptr;             // the pending lines' gids rebased to that text
+  size_t ck_gids_cap_ = 0;
   size_t ck_text_cap_[2] = {0, 0};
   // checkpoint cell packing (device scan + gather of the occupied bucket cells)
   int32_t* d_ck_slots_ = nullptr;
