@@ -275,10 +275,12 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
         HIP_OK(hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data()));
       cu_reserved_ = reserve;
     } else {
-      // APM_STATS_PRIO=1: the stats stream (rollover chain K9..K11 -> alert candidates) at the join
-      // stream's high priority, so a batch's alert decision is not queued behind the next batch's
-      // join kernels (the ingest->alert latency, tools/latency_breakdown.py) -- A/B
-      static const bool sp = [] { const char* x = std::getenv("APM_STATS_PRIO"); return x && x[0] == '1'; }();
+      // The stats stream (rollover chain K8..K11 -> alert candidates) at the join stream's high
+      // priority, so a batch's alert decision is not queued behind the next batch's join kernels:
+      // 271.2 / 265.4 / 280.3 / 268.0 M against 264.9-267.3 M default-priority runs on the same
+      // boxes, p50 ingest -> alert 1.13-1.17 vs 1.17-1.24 ms (profiles/r6_g, r6_q).
+      // APM_STATS_PRIO=0: default priority (A/B).
+      static const bool sp = [] { const char* x = std::getenv("APM_STATS_PRIO"); return !(x && x[0] == '0'); }();
       int lo = 0, hi = 0;
       HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
       HIP_OK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, sp ? hi : 0));
