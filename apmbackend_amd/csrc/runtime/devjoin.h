@@ -71,7 +71,12 @@ class DeviceJoin {
   // A third batch buffer for the two-ahead H2D (Engine::stage_batch), allocated on first use;
   // swap_stage(k) hands it to slot k (whose previous buffer becomes the staging buffer).
   uint8_t* d_stage() {
-    if (!d_stage_bytes_) d_stage_bytes_ = (uint8_t*)dmalloc(cfg_.max_batch_bytes + 256);
+    if (!d_stage_bytes_) {
+      d_stage_bytes_ = (uint8_t*)dmalloc(cfg_.max_batch_bytes + 256);
+      // dmalloc's zero fill is queued on the join stream: the staged copy (another stream) must
+      // not land before it (seen: a staged batch parsed as zeros, test_two_ahead_input_staging_*)
+      HIP_OK(hipStreamSynchronize(stream_));
+    }
     return d_stage_bytes_;
   }
   void swap_stage(int k) { std::swap(sl_[k].d_bytes, d_stage_bytes_); }
