@@ -5,7 +5,10 @@
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <fcntl.h>
+#include <immintrin.h>
 #include <poll.h>
+#include <sys/mman.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -287,9 +290,11 @@ class HostCollective final : public Collective {
         std::this_thread::sleep_for(std::chrono::milliseconds(20));
       }
     }
+    shm_handshake(port, t_end);
   }
   ~HostCollective() override {
     shutdown_all();
+    if (shm_) ::munmap(shm_, shm_len_);
     for (Staged* st : pool_) {
       if (st->done) { hipEventSynchronize(st->done); hipEventDestroy(st->done); }
       if (st->in) hipHostFree(st->in);
@@ -380,6 +385,7 @@ class HostCollective final : public Collective {
       if (err_.empty()) err_ = "aborted";
     }
     aborted_ = true;
+    if (shm_) shm_hdr()->abort.store(1, std::memory_order_release);
     shutdown_all();
   }
   bool aborted() const override { return aborted_.load(); }
@@ -502,8 +508,146 @@ class HostCollective final : public Collective {
       err_ = why;
     }
     aborted_ = true;
+    if (shm_) shm_hdr()->abort.store(1, std::memory_order_release);
     shutdown_all();
     throw std::runtime_error("host collective: " + why);
+  }
+
+  // ---- shared-memory data plane (ranks on one host: the rehearsal transport's usual case).
+  // The TCP star stays for the rendezvous and for liveness: a dead peer's socket reads EOF.  Each
+  // rank writes its contribution into its slot of the current parity, publishes the sequence
+  // number, waits for every rank's, and combines all of them itself in rank order -- the same
+  // bits on every rank, no round trip through rank 0.  A rank reuses a parity only two
+  // collectives later, after every rank has published the one in between, which it does only
+  // after reading this one.  Contributions over kShmSlot bytes go through TCP (every rank
+  // decides alike: equal sizes per collective).  APM_HOSTCOLL_SHM=0: TCP only.
+  static constexpr size_t kShmSlot = (size_t)1 << 20;
+  static constexpr size_t kShmHead = 64;
+  struct ShmHdr {
+    uint64_t nonce;
+    std::atomic<uint32_t> abort;
+  };
+  struct ShmSlot {
+    std::atomic<uint64_t> seq;
+    uint32_t op;
+    uint32_t pad;
+    uint64_t bytes;
+  };
+  ShmHdr* shm_hdr() { return (ShmHdr*)shm_; }
+  char* shm_slot(int parity, int r) {
+    return (char*)shm_ + kShmHead + ((size_t)parity * (size_t)n_ + (size_t)r) * (kShmHead + kShmSlot);
+  }
+
+  void shm_handshake(int port, double t_end) {
+    const char* env = std::getenv("APM_HOSTCOLL_SHM");
+    const bool want = !(env && env[0] == '0');
+    const size_t len = kShmHead + 2 * (size_t)n_ * (kShmHead + kShmSlot);
+    if (r_ == 0) {
+      std::string name;
+      uint64_t nonce = 0;
+      void* m = MAP_FAILED;
+      int fd = -1;
+      if (want) {
+        nonce = (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count() ^ ((uint64_t)::getpid() << 32);
+        name = "/apm_hc_" + std::to_string(port) + "_" + std::to_string(::getpid()) + "_" + std::to_string(nonce & 0xffffff);
+        fd = ::shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+        if (fd >= 0 && ::ftruncate(fd, (off_t)len) == 0)
+          m = ::mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        if (m != MAP_FAILED) ((ShmHdr*)m)->nonce = nonce;
+      }
+      const uint32_t nl = m != MAP_FAILED ? (uint32_t)name.size() : 0u;
+      bool all = nl > 0;
+      for (int r = 1; r < n_; ++r) {
+        if (!send_all(fd_[(size_t)r], &nl, 4) || (nl && (!send_all(fd_[(size_t)r], name.data(), nl) ||
+                                                       !send_all(fd_[(size_t)r], &nonce, 8))))
+          fail("shared-memory handshake: rank " + std::to_string(r) + " gone");
+      }
+      for (int r = 1; r < n_; ++r) {
+        uint8_t ok = 0;
+        if (!recv_all(fd_[(size_t)r], &ok, 1, t_end)) fail("shared-memory handshake: no reply from rank " + std::to_string(r));
+        all = all && ok;
+      }
+      const uint8_t on = all ? 1 : 0;
+      for (int r = 1; r < n_; ++r)
+        if (!send_all(fd_[(size_t)r], &on, 1)) fail("shared-memory handshake: rank " + std::to_string(r) + " gone");
+      if (fd >= 0) {
+        ::shm_unlink(name.c_str());  // every rank has it mapped (or gave up): nothing left behind
+        ::close(fd);
+      }
+      if (on) { shm_ = m; shm_len_ = len; }
+      else if (m != MAP_FAILED) ::munmap(m, len);
+    } else {
+      uint32_t nl = 0;
+      if (!recv_all(fd_[0], &nl, 4, t_end)) fail("shared-memory handshake: rank 0 gone");
+      void* m = MAP_FAILED;
+      uint8_t ok = 0;
+      if (nl) {
+        std::string name(nl, '\0');
+        uint64_t nonce = 0;
+        if (!recv_all(fd_[0], &name[0], nl, t_end) || !recv_all(fd_[0], &nonce, 8, t_end))
+          fail("shared-memory handshake: rank 0 gone");
+        const int fd = want ? ::shm_open(name.c_str(), O_RDWR, 0600) : -1;
+        if (fd >= 0) {
+          m = ::mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+          ::close(fd);
+        }
+        ok = m != MAP_FAILED && ((ShmHdr*)m)->nonce == nonce;  // (another host's segment of that name: no)
+      }
+      if (!send_all(fd_[0], &ok, 1)) fail("shared-memory handshake: rank 0 gone");
+      uint8_t on = 0;
+      if (!recv_all(fd_[0], &on, 1, t_end)) fail("shared-memory handshake: rank 0 gone");
+      if (on && ok) { shm_ = m; shm_len_ = len; }
+      else if (m != MAP_FAILED) ::munmap(m, len);
+    }
+  }
+
+  // a peer's socket reading EOF (or an error) = that process is gone
+  bool peer_gone(int fd) {
+    if (fd < 0) return true;
+    pollfd q{fd, POLLIN, 0};
+    if (::poll(&q, 1, 0) <= 0) return false;
+    if (q.revents & (POLLHUP | POLLERR | POLLNVAL)) return true;
+    char c;
+    const ssize_t r = ::recv(fd, &c, 1, MSG_PEEK | MSG_DONTWAIT);
+    return r == 0 || (r < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR);
+  }
+
+  template <class F>
+  std::vector<uint8_t> shm_exchange(uint32_t op, uint64_t seq, const std::vector<uint8_t>& mine, F&& combine) {
+    const int par = (int)(seq & 1);
+    char* my = shm_slot(par, r_);
+    ShmSlot* h = (ShmSlot*)my;
+    if (!mine.empty()) std::memcpy(my + kShmHead, mine.data(), mine.size());
+    h->op = op;
+    h->bytes = mine.size();
+    h->seq.store(seq, std::memory_order_release);
+    const double t_end = mono_ms() + timeout_ms_;
+    std::vector<std::vector<uint8_t>> all((size_t)n_);
+    for (int q = 0; q < n_; ++q) {
+      ShmSlot* hq = (ShmSlot*)shm_slot(par, q);
+      double next_check = 0;
+      for (uint32_t spin = 0; hq->seq.load(std::memory_order_acquire) != seq; ++spin) {
+        if (spin < 4096) { _mm_pause(); continue; }
+        if (shm_hdr()->abort.load(std::memory_order_acquire)) fail("a rank closed its connection: the collective was aborted (peer process gone)");
+        const double now = mono_ms();
+        if (now >= next_check) {
+          if (r_ == 0) {
+            for (int r = 1; r < n_; ++r)
+              if (peer_gone(fd_[(size_t)r])) fail("rank " + std::to_string(r) + " closed its connection (peer process gone)");
+          } else if (peer_gone(fd_[0])) {
+            fail("rank 0 closed its connection (peer process gone)");
+          }
+          next_check = now + 1.0;
+        }
+        if (now >= t_end) fail("rank " + std::to_string(q) + " did not arrive within the collective timeout");
+        std::this_thread::yield();
+      }
+      if (hq->op != op || hq->bytes != mine.size())
+        fail("protocol mismatch with rank " + std::to_string(q) + " (ranks issued different collectives)");
+      const char* d = shm_slot(par, q) + kShmHead;
+      all[(size_t)q].assign(d, d + hq->bytes);
+    }
+    return combine(all);
   }
 
   template <class F>
@@ -515,6 +659,7 @@ class HostCollective final : public Collective {
       all[0] = std::move(mine);
       return combine(all);
     }
+    if (shm_ && mine.size() <= kShmSlot) return shm_exchange(op, seq, mine, combine);
     const double t_end = mono_ms() + timeout_ms_;
     const Hdr h{kMagic, op, seq, (uint64_t)mine.size()};
     if (r_ != 0) {
@@ -558,6 +703,8 @@ class HostCollective final : public Collective {
   std::mutex err_mu_;
   std::string err_;
   std::vector<Staged*> pool_;  // enqueue side (the engine's ingest thread)
+  void* shm_ = nullptr;        // shared-memory data plane (shm_handshake), or none
+  size_t shm_len_ = 0;
 };
 
 }  // namespace
