@@ -348,17 +348,38 @@ def main():
         for li in range(len(eng.ecfg["lags"])):
             eng.eng.import_alert_counters(li, ser, [need] * len(ser))
     torch.cuda.synchronize()
+    # Python's cyclic GC over the setup's garbage (the series export above: ~10^5 tuples) happens
+    # here, not at some step of the timed loop; collections inside the loop are timed and reported
+    import gc
+    gc.collect()
+    gc_ev = {"n": 0, "ms": 0.0, "max_ms": 0.0, "steps": []}
+    gc_t = [0.0]
+    cur_step = [-1]
+
+    def _gc_cb(phase, info):
+        if phase == "start":
+            gc_t[0] = time.perf_counter()
+        else:
+            d = 1000.0 * (time.perf_counter() - gc_t[0])
+            gc_ev["n"] += 1
+            gc_ev["ms"] += d
+            gc_ev["max_ms"] = max(gc_ev["max_ms"], d)
+            if d > 0.5:
+                gc_ev["steps"].append([cur_step[0], info.get("generation"), round(d, 3)])
     m0 = eng.metrics()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
+    gc.callbacks.append(_gc_cb)
     t0 = time.perf_counter()
     step_ms = []
-    for i in range(PRE, PRE + args.warmup + args.steps)[args.warmup:]:
+    for k, i in enumerate(range(PRE, PRE + args.warmup + args.steps)[args.warmup:]):
+        cur_step[0] = k
         ts = time.perf_counter()
         step(i)
         step_ms.append(1000.0 * (time.perf_counter() - ts))
     t_steps = time.perf_counter()
+    gc.callbacks.remove(_gc_cb)
     eng.eng.flush()  # the last batch's stats stage runs on the engine's stats thread
     t_flushed = time.perf_counter()
     if inserter is not None:  # alerts paged + every DB row of the timed batches written
@@ -402,6 +423,8 @@ def main():
             json.dump({"rank": rank, "world": world, "device": device, "coll": coll, "comm_ranks": comm_ranks,
                        "lines_timed": lines, "timed_s": dt, "lines_total": m1["lines"], "tx_total": m1["tx"],
                        "node_metrics": list(node_m), "step_ms": [round(x, 4) for x in step_ms],
+                       "python_gc_timed_steps": {"collections": gc_ev["n"], "ms": round(gc_ev["ms"], 3),
+                                                 "max_ms": round(gc_ev["max_ms"], 3), "over_0.5ms": gc_ev["steps"]},
                        "lockstep_ms_per_step": lock_ms, "lockstep_max_ms": m1["t_lockstep_max_ms"],
                        "alerts": int(m1["alerts"])}, fh)
     value = lines_total / dt_max
@@ -440,6 +463,8 @@ def main():
             # rank 0's steps (ingest side returns) and the drain after the last one (its stats,
             # outputs, alert decision): ms_per_step = (sum(step_ms) + drain_ms) / steps
             "step_ms": [round(x, 3) for x in step_ms],
+            "python_gc_timed_steps": {"collections": gc_ev["n"], "ms": round(gc_ev["ms"], 3),
+                                      "max_ms": round(gc_ev["max_ms"], 3), "over_0.5ms": gc_ev["steps"]},
             "drain_ms": round(1000.0 * (t0 + dt - t_steps), 3),
             "drain_flush_ms": round(1000.0 * (t_flushed - t_steps), 3),  # the engine's lanes (stats, outputs)
             "t_lockstep_ms": round(maxed[8].item(), 4),
