@@ -130,6 +130,8 @@ def _run(args, cfg, N, rank, root, IngestService):
     torch.cuda.synchronize()
     if args.trace:
         svc.eng.eng.set_trace(True)
+    import gc
+    gc.collect()  # (the corpus generation's garbage: not inside the timed region)
     pf0 = dict(svc.perf)
     tl0 = dict(loop_t)
     ts0 = svc.tailer.stats()
