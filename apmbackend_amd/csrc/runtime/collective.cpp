@@ -555,6 +555,22 @@ class HostCollective final : public Collective {
           m = ::mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
         if (m != MAP_FAILED) ((ShmHdr*)m)->nonce = nonce;
       }
+      // the segment's name goes away on every path (a peer lost mid-handshake throws from fail())
+      struct Unlink {
+        const std::string& n;
+        int fd;
+        ~Unlink() {
+          if (fd >= 0) { ::shm_unlink(n.c_str()); ::close(fd); }
+        }
+      } unlink_guard{name, fd};
+      struct Unmap {
+        void*& m;
+        size_t len;
+        bool keep = false;
+        ~Unmap() {
+          if (!keep && m != MAP_FAILED) ::munmap(m, len);
+        }
+      } unmap_guard{m, len};
       const uint32_t nl = m != MAP_FAILED ? (uint32_t)name.size() : 0u;
       bool all = nl > 0;
       for (int r = 1; r < n_; ++r) {
@@ -570,12 +586,8 @@ class HostCollective final : public Collective {
       const uint8_t on = all ? 1 : 0;
       for (int r = 1; r < n_; ++r)
         if (!send_all(fd_[(size_t)r], &on, 1)) fail("shared-memory handshake: rank " + std::to_string(r) + " gone");
-      if (fd >= 0) {
-        ::shm_unlink(name.c_str());  // every rank has it mapped (or gave up): nothing left behind
-        ::close(fd);
-      }
-      if (on) { shm_ = m; shm_len_ = len; }
-      else if (m != MAP_FAILED) ::munmap(m, len);
+      // (unlink_guard: every rank has it mapped or gave up -- nothing is left behind in /dev/shm)
+      if (on) { shm_ = m; shm_len_ = len; unmap_guard.keep = true; }
     } else {
       uint32_t nl = 0;
       if (!recv_all(fd_[0], &nl, 4, t_end)) fail("shared-memory handshake: rank 0 gone");
